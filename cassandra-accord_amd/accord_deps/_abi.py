@@ -1,0 +1,116 @@
+"""ctypes mirror of include/accord_deps.h (the C ABI of libaccord_deps.so).
+
+Struct layouts only; loading the product library lives in ``native.py``. The oracle
+wrapper (``oracle/pyoracle.py``) reuses these layouts because the oracle consumes the same
+SoA formats.
+"""
+import ctypes as C
+
+import numpy as np
+
+AD_OK = 0
+AD_E_INVAL = -1
+AD_E_NOMEM = -2
+AD_E_DEVICE = -3
+AD_E_ORDER = -4
+AD_E_DUP_EXEC = -5
+AD_E_INCONSISTENT_ID = -6
+AD_E_NOT_LOADED = -7
+AD_E_STATE = -8
+AD_E_CAPACITY = -9
+
+AD_MAP_KEY, AD_MAP_RANGE, AD_MAP_DIRECT_KEY = 0, 1, 2
+NMAPS = 3
+MAP_NAMES = ("keyDeps", "rangeDeps", "directKeyDeps")
+AD_SNAPSHOT, AD_SEQUENTIAL = 0, 1
+
+# InternalStatus ordinals (CommandsForKey.java:493-501)
+ST_TRANSITIVELY_KNOWN = 0
+ST_HISTORICAL = 1
+ST_PREACCEPTED = 2
+ST_ACCEPTED = 3
+ST_COMMITTED = 4
+ST_STABLE = 5
+ST_APPLIED = 6
+ST_INVALID = 7
+
+# Txn.Kind ordinals (Txn.java:53-112)
+KIND_READ, KIND_WRITE, KIND_EPHEMERAL_READ, KIND_SYNC_POINT, KIND_EXCLUSIVE_SYNC_POINT, KIND_LOCAL_ONLY = range(6)
+
+P = C.c_void_p
+
+
+class AdConfig(C.Structure):
+    _fields_ = [("device", C.c_int32), ("range_start_inclusive", C.c_int32), ("elide", C.c_int32),
+                ("reserved", C.c_int32), ("n_slices", C.c_uint64), ("slice_start", P), ("slice_end", P)]
+
+
+class AdCfkSoa(C.Structure):
+    _fields_ = [("n_keys", C.c_uint64), ("keys", P), ("seg", P), ("n_entries", C.c_uint64),
+                ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
+                ("exec_msb", P), ("exec_lsb", P), ("exec_node", P),
+                ("status", P), ("pruned_before", P)]
+
+
+class AdRangeCmdsSoa(C.Structure):
+    _fields_ = [("n_cmds", C.c_uint64), ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
+                ("erased", P), ("historical", P), ("range_off", P), ("range_start", P), ("range_end", P)]
+
+
+class AdRedundantSoa(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("range_start", P), ("range_end", P), ("start_epoch", P), ("end_epoch", P),
+                ("wm_msb", P), ("wm_lsb", P), ("wm_node", P)]
+
+
+class AdQuerySoa(C.Structure):
+    _fields_ = [("n_txns", C.c_uint64), ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
+                ("exec_msb", P), ("exec_lsb", P), ("exec_node", P), ("min_epoch", P),
+                ("key_off", P), ("keys", P)]
+
+
+class AdStats(C.Structure):
+    _fields_ = [("n_txns", C.c_uint64), ("n_probes", C.c_uint64), ("n_pairs", C.c_uint64 * NMAPS),
+                ("n_unique", C.c_uint64 * NMAPS), ("scan_entries", C.c_uint64),
+                ("ms_device", C.c_double), ("ms_ingest", C.c_double),
+                ("ms_stage", C.c_double * 8), ("bytes_stage", C.c_uint64 * 8)]
+
+
+class AdDepsResult(C.Structure):
+    _fields_ = [("n_txns", C.c_uint64),
+                ("keys_off", P * NMAPS), ("keys", P * NMAPS),
+                ("txn_off", P * NMAPS), ("txns", P * NMAPS),
+                ("k2t_off", P * NMAPS), ("k2t", P * NMAPS),
+                ("stats", AdStats)]
+
+
+class AdGraphSoa(C.Structure):
+    _fields_ = [("n_txns", C.c_uint64), ("exec_msb", P), ("exec_lsb", P), ("exec_node", P), ("kind", P),
+                ("key_off", P), ("keys", P), ("dep_off", P), ("deps", P)]
+
+
+def ptr(a):
+    """Pointer to a numpy array's data (None for None). Caller keeps the array alive."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays handed to the ABI must be C-contiguous"
+    return a.ctypes.data  # numpy allocates >= 1 byte, so empty arrays still get a valid pointer
+
+
+def as_u64(a):
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+def as_i64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
+
+
+def as_i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def as_u8(a):
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def as_u32(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)

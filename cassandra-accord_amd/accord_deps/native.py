@@ -1,0 +1,182 @@
+"""ctypes binding of libaccord_deps.so (the HIP product path).
+
+`DeviceCommandStore` mirrors the reference's per-store entry point for this path:
+  SafeCommandStore.mapReduceActive / PreAccept.calculatePartialDeps (PreAccept.java:245-267),
+batched: `calculate_partial_deps(queries)` answers every request of a batch, returning the
+three RelationMultiMaps of each PartialDeps. Errors surface as `AccordDepsError` carrying the
+AD_E_* code (the Java wrapper maps these to IllegalStateException).
+
+There is no CPU fallback: if the library or a GPU is missing, this module raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as A
+from .model import DepsMap, PartialDepsBatch, Tids
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaccord_deps.so")
+
+EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error", "ad_cfk_load",
+           "ad_range_cmds_load", "ad_redundant_load", "ad_deps_batch", "ad_result_free",
+           "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_levels")
+
+
+class AccordDepsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libaccord_deps error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise AccordDepsError(A.AD_E_DEVICE, "libaccord_deps.so not built (run __graft_entry__.build())")
+        # One HIP runtime per process: if PyTorch is present it must load its libamdhip64.so.7
+        # first, so that this library binds to the same runtime by soname (two runtimes in one
+        # process cannot share the device: hipErrorNoDevice).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        L = C.CDLL(LIB_PATH)
+        L.ad_abi_version.restype = C.c_int
+        L.ad_ctx_create.argtypes = [C.POINTER(A.AdConfig), C.POINTER(C.c_void_p)]
+        L.ad_ctx_destroy.argtypes = [C.c_void_p]
+        L.ad_last_error.argtypes = [C.c_void_p]
+        L.ad_last_error.restype = C.c_char_p
+        L.ad_cfk_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkSoa)]
+        L.ad_range_cmds_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsSoa)]
+        L.ad_redundant_load.argtypes = [C.c_void_p, C.POINTER(A.AdRedundantSoa)]
+        L.ad_deps_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.POINTER(C.POINTER(A.AdDepsResult))]
+        L.ad_result_free.argtypes = [C.POINTER(A.AdDepsResult)]
+        L.ad_deps_batch_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_void_p,
+                                           C.POINTER(A.AdDepsResult)]
+        L.ad_dict.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                              C.POINTER(C.c_void_p)]
+        L.ad_range_table.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ad_levels.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.POINTER(A.AdStats)]
+        _lib = L
+    return _lib
+
+
+def _view(p, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(C.cast(p, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,))
+
+
+def stats_dict(s):
+    return dict(n_txns=s.n_txns, n_probes=s.n_probes, n_pairs=list(s.n_pairs), n_unique=list(s.n_unique),
+                ms_device=s.ms_device, ms_ingest=s.ms_ingest, ms_stage=list(s.ms_stage)[:6],
+                bytes_stage=list(s.bytes_stage)[:6])
+
+
+class DeviceCommandStore:
+    """One CommandStore's snapshot resident on one MI355X (an `ad_ctx`)."""
+
+    def __init__(self, device=0, range_start_inclusive=0, elide=1, slices=None):
+        L = lib()
+        cfg = A.AdConfig()
+        cfg.device = device
+        cfg.range_start_inclusive = range_start_inclusive
+        cfg.elide = elide
+        self._keep = []
+        if slices is not None and len(slices):
+            s = np.ascontiguousarray(np.asarray(slices, np.int64)[:, 0])
+            e = np.ascontiguousarray(np.asarray(slices, np.int64)[:, 1])
+            self._keep = [s, e]
+            cfg.n_slices = len(s)
+            cfg.slice_start, cfg.slice_end = A.ptr(s), A.ptr(e)
+        h = C.c_void_p()
+        rc = L.ad_ctx_create(C.byref(cfg), C.byref(h))
+        if rc:
+            raise AccordDepsError(rc, L.ad_last_error(None).decode())
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ad_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc:
+            raise AccordDepsError(rc, lib().ad_last_error(self.h).decode())
+
+    def load(self, workload):
+        L = lib()
+        self._check(L.ad_cfk_load(self.h, C.byref(workload.cfk.soa())))
+        self._check(L.ad_range_cmds_load(self.h, C.byref(workload.cmds.soa())))
+        self._check(L.ad_redundant_load(self.h, C.byref(workload.redundant.soa())))
+        return self
+
+    def dictionary(self):
+        n = C.c_uint64()
+        pm, pl, pn = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._check(lib().ad_dict(self.h, C.byref(n), C.byref(pm), C.byref(pl), C.byref(pn)))
+        k = n.value
+        return Tids(_view(pm, k, np.uint64).copy(), _view(pl, k, np.uint64).copy(), _view(pn, k, np.int32).copy())
+
+    def range_table(self):
+        n = C.c_uint64()
+        ps, pe = C.c_void_p(), C.c_void_p()
+        self._check(lib().ad_range_table(self.h, C.byref(n), C.byref(ps), C.byref(pe)))
+        return _view(ps, n.value, np.int64).copy(), _view(pe, n.value, np.int64).copy()
+
+    def calculate_partial_deps(self, queries, flags=A.AD_SNAPSHOT):
+        """Batched PreAccept.calculatePartialDeps; host arrays in, materialised PartialDeps out."""
+        L = lib()
+        out = C.POINTER(A.AdDepsResult)()
+        self._check(L.ad_deps_batch(self.h, C.byref(queries.soa()), flags, C.byref(out)))
+        try:
+            r = out.contents
+            n = r.n_txns
+            raw = []
+            for m in range(A.NMAPS):
+                ko = _view(r.keys_off[m], n + 1, np.uint64).copy()
+                to = _view(r.txn_off[m], n + 1, np.uint64).copy()
+                oo = _view(r.k2t_off[m], n + 1, np.uint64).copy()
+                raw.append((ko, _view(r.keys[m], int(ko[-1]), np.int64).copy(), to,
+                            _view(r.txns[m], int(to[-1]), np.uint32).copy(), oo,
+                            _view(r.k2t[m], int(oo[-1]), np.int32).copy()))
+            stats = stats_dict(r.stats)
+        finally:
+            L.ad_result_free(out)
+        return self.materialise(raw, stats)
+
+    def materialise(self, raw, stats=None):
+        d = self.dictionary()
+        rs, re = self.range_table()
+        maps = []
+        for m, (ko, keys, to, tx, oo, k2t) in enumerate(raw):
+            txn = d.take(tx.astype(np.int64))
+            if m == A.AD_MAP_RANGE:
+                rid = keys.astype(np.int64)
+                maps.append(DepsMap(ko, rs[rid], re[rid], to, txn, oo, k2t))
+            else:
+                maps.append(DepsMap(ko, keys, None, to, txn, oo, k2t))
+        return PartialDepsBatch(maps, stats=stats or {})
+
+    def deps_batch_device(self, qdev, stream=None):
+        """Device-resident batch. `qdev` is an AdQuerySoa of device pointers. Returns
+        (AdDepsResult with device pointers owned by the store, stats dict)."""
+        out = A.AdDepsResult()
+        self._check(lib().ad_deps_batch_device(self.h, C.byref(qdev), A.AD_SNAPSHOT, stream, C.byref(out)))
+        return out, stats_dict(out.stats)
+
+
+def resolve(workload, device=0, elide=1):
+    st = DeviceCommandStore(device, workload.range_start_inclusive, elide, workload.slices)
+    try:
+        st.load(workload)
+        return st.calculate_partial_deps(workload.queries, workload.flags)
+    finally:
+        st.close()

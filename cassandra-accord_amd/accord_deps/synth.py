@@ -1,0 +1,398 @@
+"""Seeded synthetic workloads for the five BASELINE.json configs.
+
+Every generator is deterministic in its seed (numpy PCG64) and honours the invariants the
+reference relies on:
+  * byId strictly increasing per key (CommandsForKey.java:1438);
+  * executeAts of committed entries unique per key (:1439) and never equal to another txnId
+    (executeAt node ids live in a range disjoint from txnId node ids, as
+    CommandsForKeyTest.java:418-424,449-455 arranges);
+  * ids equal under Timestamp.equals are bit-identical;
+  * prunedBefore, when set, names an APPLIED Write of the key.
+All data is synthetic; key ordinals stand for Key.compareTo order (IntKey-like tokens).
+"""
+import numpy as np
+
+from . import _abi as A
+from .model import (CfkSnapshot, Graph, Queries, RangeCommands, Redundant, Tids, Workload,
+                    make_timestamps, make_txn_ids)
+
+EXEC_NODE_BASE = 1 << 24        # executeAt node ids never collide with txnId node ids (1..16)
+
+
+def splitmix64(x):
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def key_tokens(n_keys, salt):
+    """rank r -> i64 token (a bijection, so distinct ranks give distinct keys)."""
+    return splitmix64(np.arange(n_keys, dtype=np.uint64) + np.uint64(salt)).view(np.int64)
+
+
+class Zipf:
+    def __init__(self, n, s):
+        w = 1.0 / np.power(np.arange(1, n + 1, dtype=np.float64), s)
+        self.cdf = np.cumsum(w)
+        self.cdf /= self.cdf[-1]
+        self.p = w / w.sum()
+
+    def sample(self, rng, size):
+        return np.minimum(np.searchsorted(self.cdf, rng.random(size), side="right"), len(self.cdf) - 1)
+
+
+def distinct_rows(rng, sampler, n_rows, k):
+    """n_rows x k samples, each row without duplicates (rejection on dup, SURVEY §8d cfg 2)."""
+    out = sampler(rng, (n_rows, k))
+    while True:
+        s = np.sort(out, axis=1)
+        bad = np.nonzero((s[:, 1:] == s[:, :-1]).any(axis=1))[0]
+        if len(bad) == 0:
+            return out
+        out[bad] = sampler(rng, (len(bad), k))
+
+
+def _segments(key_rank, txn_idx, n_keys_total):
+    """Sort (key, txn) entries; return order, per-entry position-from-end, unique keys, seg offsets."""
+    order = np.lexsort((txn_idx, key_rank))
+    kr = key_rank[order]
+    uniq, start, counts = np.unique(kr, return_index=True, return_counts=True)
+    seg = np.zeros(len(uniq) + 1, dtype=np.uint64)
+    seg[1:] = np.cumsum(counts)
+    pos = np.arange(len(kr)) - np.repeat(start, counts)
+    from_end = np.repeat(counts, counts) - 1 - pos
+    return order, from_end, uniq, seg
+
+
+def build_history(rng, n_hist_txns, keys_of_txn, token_of_rank, hist_kind, tail_unapplied,
+                  epoch=1, hlc0=1):
+    """CFK snapshot for history txns j (txnId hlc = hlc0 + j, node 1..16, kind hist_kind[j]):
+    every entry APPLIED with executeAt = txnId except the last `tail_unapplied` entries per key,
+    drawn from {PREACCEPTED, ACCEPTED, COMMITTED, STABLE}; ACCEPTED/COMMITTED/STABLE carry an
+    executeAt bumped by 1..1000 hlc ticks (CommandsForKey.TxnInfo.create, :272-279)."""
+    j = np.arange(n_hist_txns, dtype=np.int64)
+    txn_node = rng.integers(1, 17, n_hist_txns).astype(np.int32)
+    bump = rng.integers(1, 1001, n_hist_txns).astype(np.uint64)
+    txn = make_txn_ids(epoch, hlc0 + j.astype(np.uint64), hist_kind, txn_node)
+    k = keys_of_txn.shape[1]
+    key_rank = keys_of_txn.reshape(-1)
+    txn_idx = np.repeat(j, k)
+    tok = token_of_rank[key_rank]
+    order, from_end, uniq_tok, seg = _segments(tok, txn_idx, None)
+    e_txn = txn_idx[order]
+    status = np.full(len(e_txn), A.ST_APPLIED, dtype=np.uint8)
+    tail = from_end < tail_unapplied
+    status[tail] = rng.integers(A.ST_PREACCEPTED, A.ST_STABLE + 1, int(tail.sum())).astype(np.uint8)
+    has_exec = (status >= A.ST_ACCEPTED) & (status <= A.ST_STABLE)
+    et = txn.take(e_txn)
+    flags = et.lsb & np.uint64(0xFFFF)
+    hlc = (et.lsb >> np.uint64(16)) | ((et.msb & np.uint64(0x7FFF)) << np.uint64(48))
+    bumped = make_timestamps(epoch, hlc + bump[e_txn], flags, EXEC_NODE_BASE + e_txn.astype(np.int64))
+    ex = Tids(np.where(has_exec, bumped.msb, et.msb), np.where(has_exec, bumped.lsb, et.lsb),
+              np.where(has_exec, bumped.node, et.node))
+    return CfkSnapshot(uniq_tok, seg, et, ex, status), txn
+
+
+def _queries(rng, n_txns, keys_rank, token_of_rank, kinds, hlc0, epoch=1, exec_bump=None):
+    node = rng.integers(1, 17, n_txns).astype(np.int32)
+    i = np.arange(n_txns, dtype=np.uint64)
+    txn = make_txn_ids(epoch, hlc0 + i, kinds, node)
+    if exec_bump is None:
+        ex = Tids(txn.msb.copy(), txn.lsb.copy(), txn.node.copy())
+    else:
+        flags = txn.lsb & np.uint64(0xFFFF)
+        bumped = make_timestamps(epoch, hlc0 + i + exec_bump.astype(np.uint64), flags,
+                                 EXEC_NODE_BASE + (1 << 22) + np.arange(n_txns))
+        sel = exec_bump > 0
+        ex = Tids(np.where(sel, bumped.msb, txn.msb), np.where(sel, bumped.lsb, txn.lsb),
+                  np.where(sel, bumped.node, txn.node))
+    tok = token_of_rank[keys_rank]
+    tok.sort(axis=1)
+    k = tok.shape[1]
+    key_off = np.arange(n_txns + 1, dtype=np.uint64) * np.uint64(k)
+    return Queries(txn, ex, key_off, tok.reshape(-1))
+
+
+def _rw_kinds(rng, n, esp_frac=0.0, sync_frac=0.0):
+    u = rng.random(n)
+    kinds = np.where(u < 0.5, A.KIND_READ, A.KIND_WRITE).astype(np.uint8)
+    r = rng.random(n)
+    kinds[r < sync_frac] = A.KIND_SYNC_POINT
+    kinds[(r >= sync_frac) & (r < sync_frac + esp_frac)] = A.KIND_EXCLUSIVE_SYNC_POINT
+    return kinds
+
+
+def config1(n_txns=10_000, keys_per_txn=4, n_keys=1_000, seed=0xACC0D001):
+    """Config 1: 10k txns x 4 keys over 1k uniform keys, single CommandStore, SEQUENTIAL
+    (each txn is PreAccepted -- inserted as PREACCEPTED -- before its deps are computed)."""
+    rng = np.random.default_rng(seed)
+    keys = distinct_rows(rng, lambda r, s: r.integers(0, n_keys, s), n_txns, keys_per_txn)
+    kinds = _rw_kinds(rng, n_txns)
+    token = np.arange(n_keys, dtype=np.int64)          # IntKey k -> ordinal k
+    q = _queries(rng, n_txns, keys, token, kinds, hlc0=1000)
+    return Workload("config1", CfkSnapshot.empty(), RangeCommands.empty(), Redundant.empty(), q,
+                    flags=A.AD_SEQUENTIAL,
+                    params=dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys, seed=seed,
+                                semantics="SEQUENTIAL"))
+
+
+def config2(n_txns=1_000_000, keys_per_txn=8, n_keys=1_000_000, n_hist_entries=16_000_000, zipf_s=0.99,
+            seed=0xACC0D002, sync_frac=0.02, esp_frac=0.01, tail_unapplied=4):
+    """Config 2: 1M txns x 8 Zipf(0.99) keys over 1M keys, 16M-entry CFK history (2M history txns x 8
+    keys), SNAPSHOT. 2% of history is SyncPoint (directKeyDeps); 1% of queries are key-domain
+    ExclusiveSyncPoints, the only kind that witnesses SyncPoints (Txn.java:221-235)."""
+    rng = np.random.default_rng(seed)
+    z = Zipf(n_keys, zipf_s)
+    token = key_tokens(n_keys, seed)
+    n_hist = n_hist_entries // keys_per_txn
+    hk = distinct_rows(rng, z.sample, n_hist, keys_per_txn)
+    hist_kind = _rw_kinds(rng, n_hist, sync_frac=sync_frac)
+    cfk, _ = build_history(rng, n_hist, hk, token, hist_kind, tail_unapplied)
+    qk = distinct_rows(rng, z.sample, n_txns, keys_per_txn)
+    q = _queries(rng, n_txns, qk, token, _rw_kinds(rng, n_txns, esp_frac=esp_frac), hlc0=n_hist + 2000)
+    return Workload("config2", cfk, RangeCommands.empty(), Redundant.empty(), q,
+                    params=dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys,
+                                n_hist_entries=n_hist * keys_per_txn, zipf_s=zipf_s, seed=seed,
+                                sync_frac=sync_frac, esp_frac=esp_frac, semantics="SNAPSHOT"))
+
+
+def shard_bounds(n_shards):
+    """EvenSplit of the i64 token space (ShardDistributor.EvenSplit, ShardDistributor.java:106-156):
+    shard g owns (lo_g, hi_g] in EndInclusive terms; returned as (lo, hi) arrays."""
+    lo = [-(1 << 63) + (g * (1 << 64)) // n_shards for g in range(n_shards)]
+    hi = [-(1 << 63) + ((g + 1) * (1 << 64)) // n_shards for g in range(n_shards)]
+    lo[0] = -(1 << 63)
+    hi[-1] = (1 << 63) - 1
+    return np.array(lo, dtype=object), np.array(hi, dtype=object)
+
+
+def config3(n_txns=64_000_000, keys_per_txn=4, n_keys=10_000_000, hist_frac=0.75, seed=0xACC0D003,
+            tail_unapplied=2):
+    """Config 3 (whole job): 64M txns over 10M uniform keys; first 75% are history (APPLIED except the
+    last 2 per key), the rest probes, SNAPSHOT. Shard with `slice_workload`."""
+    rng = np.random.default_rng(seed)
+    token = key_tokens(n_keys, seed)
+    n_hist = int(n_txns * hist_frac)
+    hk = distinct_rows(rng, lambda r, s: r.integers(0, n_keys, s), n_hist, keys_per_txn)
+    cfk, _ = build_history(rng, n_hist, hk, token, _rw_kinds(rng, n_hist), tail_unapplied)
+    nq = n_txns - n_hist
+    qk = distinct_rows(rng, lambda r, s: r.integers(0, n_keys, s), nq, keys_per_txn)
+    q = _queries(rng, nq, qk, token, _rw_kinds(rng, nq), hlc0=n_hist + 2000)
+    return Workload("config3", cfk, RangeCommands.empty(), Redundant.empty(), q,
+                    params=dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys, seed=seed,
+                                n_hist_txns=n_hist, semantics="SNAPSHOT"))
+
+
+def config4(n_txns=1_000_000, keys_per_txn=4, n_keys=1_000_000, n_ranges=100_000, n_hist_txns=1_000_000,
+            seed=0xACC0D004, log2_min=8, log2_max=20):
+    """Config 4: 100k Range-domain Write commands (EndInclusive (s, s+w], s uniform i32, w log-uniform
+    in [2^8, 2^20]) older than 1M key txns x 4 uniform keys over 1M i32 key tokens; plus a 1M-txn x 4
+    key CFK history (APPLIED except the last 2 per key) so keyDeps and rangeDeps merge. SNAPSHOT."""
+    rng = np.random.default_rng(seed)
+    token = np.unique(rng.integers(-(1 << 31), (1 << 31) - 1, int(n_keys * 1.1)))
+    token = rng.permutation(token)[:n_keys].astype(np.int64)
+    start = rng.integers(-(1 << 31), (1 << 31) - 1, n_ranges).astype(np.int64)
+    width = np.floor(np.exp2(rng.uniform(log2_min, log2_max, n_ranges))).astype(np.int64)
+    node = rng.integers(1, 17, n_ranges).astype(np.int32)
+    rtx = make_txn_ids(1, 1 + np.arange(n_ranges, dtype=np.uint64), A.KIND_WRITE, node, domain=1)
+    cmds = RangeCommands(rtx, np.arange(n_ranges + 1, dtype=np.uint64), start, start + width)
+    hk = distinct_rows(rng, lambda r, s: r.integers(0, n_keys, s), n_hist_txns, keys_per_txn)
+    cfk, _ = build_history(rng, n_hist_txns, hk, token, _rw_kinds(rng, n_hist_txns), 2,
+                           hlc0=n_ranges + 10)
+    qk = distinct_rows(rng, lambda r, s: r.integers(0, n_keys, s), n_txns, keys_per_txn)
+    q = _queries(rng, n_txns, qk, token, _rw_kinds(rng, n_txns), hlc0=n_ranges + n_hist_txns + 2000)
+    return Workload("config4", cfk, cmds, Redundant.empty(), q,
+                    params=dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys, n_ranges=n_ranges,
+                                n_hist_txns=n_hist_txns, seed=seed, semantics="SNAPSHOT"))
+
+
+def config5(n_txns=1_000_000, keys_per_txn=4, n_keys=100_000, direct_frac=0.01, seed=0xACC0D005):
+    """Config 5: 1M committed key txns x 4 keys over 100k keys, 50/50 R/W, executeAt = txnId + a
+    unique random 0..999 hlc ticks; 1% of txns carry one direct dep on an earlier-executing txn."""
+    rng = np.random.default_rng(seed)
+    keys = distinct_rows(rng, lambda r, s: r.integers(0, n_keys, s), n_txns, keys_per_txn)
+    keys.sort(axis=1)
+    kind = _rw_kinds(rng, n_txns)
+    i = np.arange(n_txns, dtype=np.uint64)
+    hlc = np.uint64(1000) + i + rng.integers(0, 1000, n_txns).astype(np.uint64)   # txnId hlc = 1000 + i
+    ex = make_timestamps(1, hlc, (kind.astype(np.uint64) << np.uint64(1)), EXEC_NODE_BASE + np.arange(n_txns))
+    order = np.lexsort(ex.order_key())
+    rank = np.empty(n_txns, np.int64)
+    rank[order] = np.arange(n_txns)
+    has = rng.random(n_txns) < direct_frac
+    dep_off = np.zeros(n_txns + 1, np.uint64)
+    dep_off[1:] = np.cumsum(has)
+    src = np.nonzero(has)[0]
+    # a direct dep on a txn executing earlier (Commands.updateWaitingOn keeps only those)
+    tgt_rank = (rng.random(len(src)) * np.maximum(rank[src], 1)).astype(np.int64)
+    deps = order[tgt_rank].astype(np.uint32)
+    deps = np.where(rank[src] > 0, deps, src.astype(np.uint32))     # self-dep of the first is dropped
+    key_off = np.arange(n_txns + 1, dtype=np.uint64) * np.uint64(keys_per_txn)
+    g = Graph(ex, kind, key_off, keys.reshape(-1).astype(np.int64), dep_off, deps)
+    return g, dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys, direct_frac=direct_frac, seed=seed)
+
+
+def slice_workload(w, lo, hi):
+    """The part of workload `w` a CommandStore owning token range (lo, hi] sees: CFK keys in the
+    slice; every request, with its keys restricted to the slice (mapReduceForKey skips keys the
+    store does not own, InMemoryCommandStore.java:280). Range commands/redundant are kept whole
+    (the store slices them itself)."""
+    keys = w.cfk.keys
+    sel = (keys > lo) & (keys <= hi)
+    ki = np.nonzero(sel)[0]
+    if len(ki):
+        e0, e1 = int(w.cfk.seg[ki[0]]), int(w.cfk.seg[ki[-1] + 1])
+        seg = w.cfk.seg[ki[0]:ki[-1] + 2] - np.uint64(e0)
+    else:
+        e0 = e1 = 0
+        seg = np.zeros(1, np.uint64)
+    cfk = CfkSnapshot(keys[sel], seg, w.cfk.txn.take(slice(e0, e1)), w.cfk.exec.take(slice(e0, e1)),
+                      w.cfk.status[e0:e1],
+                      None if w.cfk.pruned_before is None else w.cfk.pruned_before[sel])
+    q = w.queries
+    qsel = (q.keys > lo) & (q.keys <= hi)
+    counts = np.add.reduceat(qsel.astype(np.int64), q.key_off[:-1].astype(np.int64)) if len(q.keys) else \
+        np.zeros(len(q), np.int64)
+    counts = np.where(np.diff(q.key_off.astype(np.int64)) == 0, 0, counts)
+    key_off = np.zeros(len(q) + 1, np.uint64)
+    key_off[1:] = np.cumsum(counts)
+    qq = Queries(q.txn, q.exec, key_off, q.keys[qsel], q.min_epoch)
+    out = Workload(w.name, cfk, w.cmds, w.redundant, qq, w.flags, dict(w.params), w.range_start_inclusive,
+                   np.array([[lo, hi]], dtype=np.int64))
+    out.params.update(slice=(int(lo), int(hi)))
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# Small randomised workloads exercising every branch of the reference path (parity tests)
+# ------------------------------------------------------------------------------------------
+def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_range_cmds=12,
+                 n_redundant=3, with_pruned=True, accept_frac=0.3, start_inclusive=False,
+                 with_slices=False, exec_below_frac=0.05):
+    """All statuses (incl. TRANSITIVELY_KNOWN / INVALID), all globally visible kinds, prunedBefore,
+    Accept-style executeAt > txnId (so PreAccept.java:261's self exclusion matters), requests whose
+    txnId is in the CFK, range commands (erased / historical / multi-range), RedundantBefore."""
+    rng = np.random.default_rng(seed)
+    key_space = np.sort(rng.choice(np.arange(-500, 500), n_keys, replace=False)).astype(np.int64)
+    hist_kinds = rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_SYNC_POINT, A.KIND_EXCLUSIVE_SYNC_POINT],
+                            n_hist_txns, p=[0.4, 0.4, 0.1, 0.1]).astype(np.uint8)
+    hist_hlc = np.sort(rng.choice(np.arange(10, 10 * (n_hist_txns + n_txns) + 10), n_hist_txns + n_txns,
+                                  replace=False)).astype(np.uint64)
+    all_node = rng.integers(1, 17, n_hist_txns + n_txns).astype(np.int32)
+    perm = rng.permutation(n_hist_txns + n_txns)
+    h_idx, q_idx = np.sort(perm[:n_hist_txns]), np.sort(perm[n_hist_txns:])
+    q_kinds = rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_EPHEMERAL_READ, A.KIND_SYNC_POINT,
+                          A.KIND_EXCLUSIVE_SYNC_POINT], n_txns, p=[0.3, 0.3, 0.1, 0.15, 0.15]).astype(np.uint8)
+    kinds = np.zeros(n_hist_txns + n_txns, np.uint8)
+    kinds[h_idx] = hist_kinds
+    kinds[q_idx] = q_kinds
+    epochs = np.where(rng.random(n_hist_txns + n_txns) < 0.2, 2, 1).astype(np.uint64)
+    epochs = np.maximum.accumulate(epochs)
+    all_txn = make_txn_ids(epochs, hist_hlc, kinds, all_node)
+    bump = rng.integers(1, 40, n_hist_txns + n_txns).astype(np.uint64)
+    below = rng.random(n_hist_txns + n_txns) < exec_below_frac
+    ex_hlc = np.where(below, np.maximum(hist_hlc.astype(np.int64) - bump.astype(np.int64), 1).astype(np.uint64),
+                      hist_hlc + bump)
+    all_exec_bumped = make_timestamps(epochs, ex_hlc, all_txn.lsb & np.uint64(0xFFFF),
+                                      EXEC_NODE_BASE + np.arange(n_hist_txns + n_txns))
+
+    # CFK: every history txn on 1..max_keys keys; queries that are "already known" also appear
+    entries = []
+    for j in h_idx:
+        nk = rng.integers(1, max_keys + 1)
+        for kr in rng.choice(n_keys, nk, replace=False):
+            entries.append((kr, j))
+    known_q = [j for j in q_idx if rng.random() < 0.25]
+    q_keys = {}
+    for j in q_idx:
+        nk = rng.integers(0, max_keys + 1)
+        q_keys[j] = np.sort(rng.choice(n_keys, nk, replace=False))
+        if j in known_q:
+            for kr in q_keys[j]:
+                entries.append((kr, j))
+    entries = sorted(set(entries))
+    e_key = np.array([e[0] for e in entries], np.int64)
+    e_txn = np.array([e[1] for e in entries], np.int64)
+    status = rng.choice(8, len(entries), p=[0.05, 0.05, 0.15, 0.1, 0.1, 0.1, 0.4, 0.05]).astype(np.uint8)
+    has_exec = (status >= A.ST_ACCEPTED) & (status <= A.ST_APPLIED)
+    # some APPLIED/committed at executeAt == txnId
+    same = rng.random(len(entries)) < 0.5
+    use_b = has_exec & ~same
+    t = all_txn.take(e_txn)
+    b = all_exec_bumped.take(e_txn)
+    ex = Tids(np.where(use_b, b.msb, t.msb), np.where(use_b, b.lsb, t.lsb), np.where(use_b, b.node, t.node))
+    uniq, start, counts = np.unique(e_key, return_index=True, return_counts=True)
+    seg = np.zeros(len(uniq) + 1, np.uint64)
+    seg[1:] = np.cumsum(counts)
+    pruned = None
+    if with_pruned:
+        pruned = np.full(len(uniq), -1, np.int64)
+        for i in range(len(uniq)):
+            s0, s1 = int(seg[i]), int(seg[i + 1])
+            cand = [p for p in range(s0, s1) if status[p] == A.ST_APPLIED and kinds[e_txn[p]] == A.KIND_WRITE]
+            if cand and rng.random() < 0.3:
+                pruned[i] = rng.choice(cand) - s0
+    cfk = CfkSnapshot(key_space[uniq], seg, t, ex, status, pruned)
+
+    # range commands: Range-domain txnIds below/around the queries
+    rc_hlc = np.sort(rng.choice(np.arange(1, 10 * (n_hist_txns + n_txns)), n_range_cmds, replace=False) * 10 + 5)
+    rc_kind = rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_SYNC_POINT, A.KIND_EXCLUSIVE_SYNC_POINT],
+                         n_range_cmds).astype(np.uint8)
+    rc_txn = make_txn_ids(1, rc_hlc.astype(np.uint64), rc_kind, rng.integers(1, 17, n_range_cmds), domain=1)
+    r_off = [0]
+    r_s, r_e = [], []
+    for i in range(n_range_cmds):
+        nr = rng.integers(1, 4)
+        pts = np.sort(rng.choice(np.arange(-520, 520), 2 * nr, replace=False))
+        for a in range(nr):
+            r_s.append(pts[2 * a])
+            r_e.append(pts[2 * a + 1])
+        r_off.append(len(r_s))
+    # duplicate a range across commands so Range::compare-equal keys merge
+    if n_range_cmds >= 2:
+        r_s[r_off[1]] = r_s[0]
+        r_e[r_off[1]] = r_e[0]
+        # keep per-command ranges sorted & disjoint
+        seg1 = list(zip(r_s[r_off[1]:r_off[2]], r_e[r_off[1]:r_off[2]]))
+        seg1 = sorted(set(seg1))
+        merged = []
+        for s_, e_ in seg1:
+            if merged and s_ <= merged[-1][1]:
+                merged[-1] = (merged[-1][0], max(merged[-1][1], e_))
+            else:
+                merged.append((s_, e_))
+        new_s = r_s[:r_off[1]] + [m[0] for m in merged] + r_s[r_off[2]:]
+        new_e = r_e[:r_off[1]] + [m[1] for m in merged] + r_e[r_off[2]:]
+        delta = len(merged) - (r_off[2] - r_off[1])
+        r_off = r_off[:2] + [o + delta for o in r_off[2:]]
+        r_s, r_e = new_s, new_e
+    cmds = RangeCommands(rc_txn, np.array(r_off, np.uint64), np.array(r_s, np.int64), np.array(r_e, np.int64),
+                         erased=(rng.random(n_range_cmds) < 0.15).astype(np.uint8),
+                         historical=(rng.random(n_range_cmds) < 0.25).astype(np.uint8))
+
+    # redundant-before: disjoint ranges with range-domain watermarks
+    pts = np.sort(rng.choice(np.arange(-520, 520), 2 * n_redundant, replace=False))
+    rb_wm = make_txn_ids(1, rng.integers(1, 1000, n_redundant).astype(np.uint64) * 7 + 3, A.KIND_EXCLUSIVE_SYNC_POINT,
+                         rng.integers(1, 17, n_redundant), domain=1)
+    none = rng.random(n_redundant) < 0.2
+    rb_wm = Tids(np.where(none, 0, rb_wm.msb), np.where(none, 0, rb_wm.lsb), np.where(none, 0, rb_wm.node))
+    red = Redundant(pts[0::2], pts[1::2], rng.integers(0, 3, n_redundant), rng.integers(2, 5, n_redundant), rb_wm)
+
+    # queries
+    qt = all_txn.take(q_idx)
+    accept = rng.random(n_txns) < accept_frac
+    qb = all_exec_bumped.take(q_idx)
+    qe = Tids(np.where(accept, qb.msb, qt.msb), np.where(accept, qb.lsb, qt.lsb), np.where(accept, qb.node, qt.node))
+    key_off = np.zeros(n_txns + 1, np.uint64)
+    key_off[1:] = np.cumsum([len(q_keys[j]) for j in q_idx])
+    keys = np.concatenate([key_space[q_keys[j]] for j in q_idx] + [np.zeros(0, np.int64)])
+    min_epoch = rng.integers(0, 3, n_txns).astype(np.int64)
+    q = Queries(qt, qe, key_off, keys, min_epoch)
+    slices = None
+    if with_slices:
+        slices = np.array([[-400, -100], [0, 300]], np.int64)
+    return Workload("random_small", cfk, cmds, red, q, params=dict(seed=seed), range_start_inclusive=int(start_inclusive),
+                    slices=slices)

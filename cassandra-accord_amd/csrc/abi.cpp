@@ -1,0 +1,1020 @@
+// abi.cpp — C ABI of libaccord_deps.so: store context, snapshot ingest (id dictionary, ranks,
+// per-key index arrays, range-entry table) and the batch pipeline driving kernels.hip.
+//
+// Ingest restates the derived state of CommandsForKey's constructor (CommandsForKey.java:642-681:
+// committedByExecuteAt, maxAppliedWriteByExecuteAt, prunedBefore) and of
+// InMemoryCommandStore.rangeCommands (:740-763) once per snapshot; the batch pipeline then
+// answers calculatePartialDeps for every request of a batch on the GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/accord_deps.h"
+#include "common.hpp"
+#include "kernels.hpp"
+
+using namespace adx;
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    bool ensure(size_t bytes)
+    {
+        if (bytes <= cap && p) return true;
+        release();
+        size_t b = bytes ? bytes : 16;
+        if (hipMalloc(&p, b) != hipSuccess) { p = nullptr; return false; }
+        cap = b;
+        return true;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct Tid {
+    uint64_t msb, lsb;
+    int32_t node;
+};
+
+static inline NormTid norm(const Tid& t) { return norm_tid(t.msb, t.lsb, t.node); }
+
+static unsigned n_threads()
+{
+    unsigned n = std::thread::hardware_concurrency();
+    if (const char* e = getenv("OMP_NUM_THREADS")) n = std::max(1, atoi(e));
+    return std::max(1u, std::min(n, 16u));
+}
+
+template <class T, class Cmp>
+static void parallel_sort(std::vector<T>& v, Cmp cmp)
+{
+    const size_t n = v.size();
+    unsigned T_ = n_threads();
+    if (n < (1u << 16) || T_ == 1)
+    {
+        std::sort(v.begin(), v.end(), cmp);
+        return;
+    }
+    std::vector<size_t> cut(T_ + 1);
+    for (unsigned i = 0; i <= T_; ++i) cut[i] = n * i / T_;
+    {
+        std::vector<std::thread> th;
+        for (unsigned i = 0; i < T_; ++i)
+            th.emplace_back([&, i] { std::sort(v.begin() + cut[i], v.begin() + cut[i + 1], cmp); });
+        for (auto& t : th) t.join();
+    }
+    std::vector<T> tmp(n);
+    std::vector<size_t> bounds = cut;
+    bool in_v = true;
+    while (bounds.size() > 2)
+    {
+        std::vector<size_t> nb;
+        std::vector<std::thread> th;
+        std::vector<T>& src = in_v ? v : tmp;
+        std::vector<T>& dst = in_v ? tmp : v;
+        for (size_t i = 0; i + 1 < bounds.size(); i += 2)
+        {
+            if (i + 2 < bounds.size())
+            {
+                size_t a = bounds[i], m = bounds[i + 1], e = bounds[i + 2];
+                th.emplace_back([&, a, m, e] {
+                    std::merge(src.begin() + a, src.begin() + m, src.begin() + m, src.begin() + e, dst.begin() + a, cmp);
+                });
+                nb.push_back(a);
+            }
+            else
+            {
+                size_t a = bounds[i], e = bounds[i + 1];
+                th.emplace_back([&, a, e] { std::copy(src.begin() + a, src.begin() + e, dst.begin() + a); });
+                nb.push_back(a);
+            }
+        }
+        nb.push_back(n);
+        for (auto& t : th) t.join();
+        bounds.swap(nb);
+        in_v = !in_v;
+    }
+    if (!in_v) v.swap(tmp);
+}
+
+template <class F>
+static void parallel_for(size_t n, F f, size_t grain = 1 << 14)
+{
+    unsigned T_ = n_threads();
+    if (n < grain * 2 || T_ == 1)
+    {
+        f(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned i = 0; i < T_; ++i)
+    {
+        size_t a = n * i / T_, b = n * (i + 1) / T_;
+        th.emplace_back([&, a, b] { f(a, b); });
+    }
+    for (auto& t : th) t.join();
+}
+
+static double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// the store context
+// ---------------------------------------------------------------------------------------
+struct ad_ctx {
+    ad_config cfg{};
+    std::vector<int64_t> slice_s, slice_e;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // host copies of the loaded inputs (needed to rebuild after SEQUENTIAL insertions)
+    struct {
+        std::vector<int64_t> keys;
+        std::vector<uint64_t> seg;
+        std::vector<Tid> txn, exec;
+        std::vector<uint8_t> status;
+        std::vector<int64_t> pruned;           // per key; -1 none
+        bool loaded = false;
+    } cfk;
+    struct {
+        std::vector<Tid> txn;
+        std::vector<uint8_t> erased, historical;
+        std::vector<uint64_t> off;
+        std::vector<int64_t> start, end;
+    } cmds;
+    struct {
+        std::vector<int64_t> start, end, e0, e1;
+        std::vector<Tid> wm;
+    } rb;
+    bool dirty = true;
+    double ms_ingest = 0;
+
+    // built snapshot
+    std::vector<uint64_t> dict_msb, dict_lsb;
+    std::vector<int32_t> dict_node;
+    std::vector<int64_t> rt_start, rt_end;     // range table (distinct ranges, by Range.compare)
+    DevSnapshot ds{};
+    DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_seg, d_woff, d_maw, d_pruned, d_ent, d_w;
+    DevBuf d_lvl[NCLASS][MAX_LEVELS];
+    DevBuf d_rstart, d_rend, d_rtxw, d_rrid;
+    DevBuf d_rlvl[NCLASS][MAX_LEVELS];
+    DevBuf d_rb_s, d_rb_e, d_rb_e0, d_rb_e1, d_rb_wm, d_rb_rid, d_slices_s, d_slices_e;
+
+    // batch buffers
+    DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
+    DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_key, p_slice;
+    DevBuf arena, p_off, p_c0, p_c1, rarena, p_roff, p_rcnt, p_rb;
+    DevBuf sz, off, bsum, t_scr, scratch, ctl;
+    DevBuf o_keys[3], o_txns[3], o_k2t[3];
+    uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0;
+    hipEvent_t ev[8] = {};
+
+    int fail(int code, const char* fmt, ...)
+    {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+};
+
+#define HIPCHK(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) return (ctx)->fail(AD_E_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+namespace {
+
+// ---------------------------------------------------------------------------------------
+// ingest
+// ---------------------------------------------------------------------------------------
+struct DictRec {
+    uint64_t hi, lo;
+    int32_t node;
+    uint32_t pad;
+    uint64_t src;
+};
+static inline bool rec_less(const DictRec& a, const DictRec& b)
+{
+    if (a.hi != b.hi) return a.hi < b.hi;
+    if (a.lo != b.lo) return a.lo < b.lo;
+    return a.node < b.node;
+}
+static inline bool rec_eq(const DictRec& a, const DictRec& b) { return a.hi == b.hi && a.lo == b.lo && a.node == b.node; }
+
+static bool tid_gt_none(const Tid& t)
+{
+    // compareTo(Timestamp.NONE) > 0, NONE = (0, 0, 0)
+    const NormTid z = {0, 0, 0};
+    return norm_cmp(norm(t), z) > 0;
+}
+
+template <class T>
+static int upload(ad_ctx* c, DevBuf& b, const std::vector<T>& v)
+{
+    if (!b.ensure(sizeof(T) * std::max<size_t>(v.size(), 1))) return c->fail(AD_E_NOMEM, "hipMalloc %zu", sizeof(T) * v.size());
+    if (!v.empty()) HIPCHK(c, hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, c->stream));
+    return 0;
+}
+
+static int build_snapshot(ad_ctx* c)
+{
+    const double t0 = now_ms();
+    auto& K = c->cfk;
+    const uint64_t nk = K.keys.size(), ne = K.status.size();
+    const uint64_t ncmd = c->cmds.txn.size(), nrb = c->rb.wm.size();
+
+    // ---- 1. id dictionary over every id the kernels compare
+    std::vector<uint8_t> exec_differs(ne);
+    std::vector<DictRec> recs;
+    recs.reserve(ne * 2 + ncmd + nrb);
+    for (uint64_t e = 0; e < ne; ++e)
+    {
+        const NormTid n = norm(K.txn[e]);
+        recs.push_back({n.hi, n.lo, n.node, 0, e});
+        const Tid& x = K.exec[e];
+        exec_differs[e] = !(x.msb == K.txn[e].msb && x.lsb == K.txn[e].lsb && x.node == K.txn[e].node);
+        if (exec_differs[e])
+        {
+            const NormTid m = norm(x);
+            recs.push_back({m.hi, m.lo, m.node, 0, ne + e});
+        }
+    }
+    for (uint64_t i = 0; i < ncmd; ++i)
+    {
+        const NormTid n = norm(c->cmds.txn[i]);
+        recs.push_back({n.hi, n.lo, n.node, 0, 2 * ne + i});
+    }
+    for (uint64_t i = 0; i < nrb; ++i)
+    {
+        if (!tid_gt_none(c->rb.wm[i])) continue;
+        const NormTid n = norm(c->rb.wm[i]);
+        recs.push_back({n.hi, n.lo, n.node, 0, 2 * ne + ncmd + i});
+    }
+    parallel_sort(recs, rec_less);
+    auto src_tid = [&](uint64_t s) -> const Tid& {
+        if (s < ne) return K.txn[s];
+        if (s < 2 * ne) return K.exec[s - ne];
+        if (s < 2 * ne + ncmd) return c->cmds.txn[s - 2 * ne];
+        return c->rb.wm[s - 2 * ne - ncmd];
+    };
+    std::vector<uint32_t> txn_rank(ne), exec_rank(ne), cmd_rank(ncmd), wm_rank(nrb, 0);
+    c->dict_msb.clear();
+    c->dict_lsb.clear();
+    c->dict_node.clear();
+    std::vector<uint64_t> dhi, dlo;
+    std::vector<int32_t> dnode;
+    for (size_t i = 0; i < recs.size(); ++i)
+    {
+        const DictRec& r = recs[i];
+        if (i == 0 || !rec_eq(recs[i - 1], r))
+        {
+            if (c->dict_msb.size() >= MAX_DICT) return c->fail(AD_E_CAPACITY, "more than %llu distinct ids", (unsigned long long)MAX_DICT);
+            const Tid& t = src_tid(r.src);
+            c->dict_msb.push_back(t.msb);
+            c->dict_lsb.push_back(t.lsb);
+            c->dict_node.push_back(t.node);
+            dhi.push_back(r.hi);
+            dlo.push_back(r.lo);
+            dnode.push_back(r.node);
+        }
+        else
+        {
+            const Tid& t = src_tid(r.src);
+            if (t.lsb != c->dict_lsb.back())
+                return c->fail(AD_E_INCONSISTENT_ID, "ids equal under Timestamp.equals differ in flag bits (lsb %llx vs %llx)",
+                               (unsigned long long)t.lsb, (unsigned long long)c->dict_lsb.back());
+        }
+        const uint32_t rank = (uint32_t)(2 * (c->dict_msb.size() - 1) + 1);
+        const uint64_t s = r.src;
+        if (s < ne) txn_rank[s] = rank;
+        else if (s < 2 * ne) exec_rank[s - ne] = rank;
+        else if (s < 2 * ne + ncmd) cmd_rank[s - 2 * ne] = rank;
+        else wm_rank[s - 2 * ne - ncmd] = rank;
+    }
+    std::vector<DictRec>().swap(recs);
+    for (uint64_t e = 0; e < ne; ++e)
+        if (!exec_differs[e]) exec_rank[e] = txn_rank[e];
+
+    // ---- 2. per key validation, tau/txw, committed Writes by executeAt
+    std::vector<uint2> ent(ne);
+    std::vector<uint32_t> seg32(nk + 1), woff(nk + 1), pruned(nk, 0);
+    std::vector<int32_t> maw(nk, -1);
+    for (uint64_t k = 0; k <= nk; ++k) seg32[k] = (uint32_t)K.seg[k];
+    std::atomic<int> bad{0};
+    std::atomic<uint64_t> bad_key{0};
+    std::vector<uint32_t> wcount(nk, 0);
+    parallel_for(nk, [&](size_t ka, size_t kb) {
+        std::vector<uint32_t> ce;
+        for (size_t k = ka; k < kb; ++k)
+        {
+            const uint64_t s0 = K.seg[k], s1 = K.seg[k + 1];
+            ce.clear();
+            uint32_t nw = 0;
+            for (uint64_t e = s0; e < s1; ++e)
+            {
+                const uint8_t st = K.status[e];
+                const uint32_t kind = (uint32_t)((K.txn[e].lsb >> 1) & 7);
+                const uint32_t dom = (uint32_t)(K.txn[e].lsb & 1);
+                if (st > 7) { bad = AD_E_INVAL; bad_key = k; continue; }
+                if (e > s0 && txn_rank[e] <= txn_rank[e - 1]) { bad = AD_E_ORDER; bad_key = k; }
+                uint32_t tau;
+                if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED) tau = 0;
+                else if (st >= AD_ST_COMMITTED && ((KINDS_RS_OR_WS >> kind) & 1)) tau = exec_rank[e];
+                else tau = TAU_NEVER_ELIDED;
+                if (tau != 0 && dom != 0) { bad = AD_E_INVAL; bad_key = k; }   // live range-domain id in a CFK
+                ent[e] = make_uint2(tau, txn_rank[e] | (kind << RANK_BITS));
+                if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED)
+                {
+                    ce.push_back(exec_rank[e]);
+                    if (kind == AD_KIND_WRITE) ++nw;
+                }
+            }
+            std::sort(ce.begin(), ce.end());
+            for (size_t i = 1; i < ce.size(); ++i)
+                if (ce[i] == ce[i - 1]) { bad = AD_E_DUP_EXEC; bad_key = k; }
+            wcount[k] = nw;
+        }
+    });
+    if (bad.load())
+    {
+        const int code = bad.load();
+        return c->fail(code, "CommandsForKey of key %lld violates %s", (long long)K.keys[bad_key.load()],
+                       code == AD_E_ORDER ? "byId strict order (CommandsForKey.java:1438)"
+                       : code == AD_E_DUP_EXEC ? "unique committed executeAt (CommandsForKey.java:1439)"
+                                               : "status range / key-domain ids");
+    }
+    for (uint64_t k = 0; k + 1 <= nk; ++k)
+        if (k > 0 && K.keys[k - 1] >= K.keys[k]) return c->fail(AD_E_INVAL, "keys not strictly ascending");
+    woff[0] = 0;
+    for (uint64_t k = 0; k < nk; ++k) woff[k + 1] = woff[k] + wcount[k];
+    std::vector<uint2> w(woff[nk]);
+    parallel_for(nk, [&](size_t ka, size_t kb) {
+        std::vector<std::pair<uint32_t, std::pair<uint32_t, uint8_t>>> tmp;
+        for (size_t k = ka; k < kb; ++k)
+        {
+            tmp.clear();
+            for (uint64_t e = K.seg[k]; e < K.seg[k + 1]; ++e)
+            {
+                const uint8_t st = K.status[e];
+                const uint32_t kind = (uint32_t)((K.txn[e].lsb >> 1) & 7);
+                if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED && kind == AD_KIND_WRITE)
+                    tmp.push_back({exec_rank[e], {txn_rank[e], st}});
+            }
+            std::sort(tmp.begin(), tmp.end());
+            int32_t m = -1;
+            for (size_t i = 0; i < tmp.size(); ++i)
+            {
+                w[woff[k] + i] = make_uint2(tmp[i].first, tmp[i].second.first);
+                if (tmp[i].second.second == AD_ST_APPLIED) m = (int32_t)(woff[k] + i);   // maxAppliedWriteByExecuteAt
+            }
+            maw[k] = m;
+            if (!K.pruned.empty() && K.pruned[k] >= 0)
+            {
+                const uint64_t idx = K.seg[k] + (uint64_t)K.pruned[k];
+                if (idx >= K.seg[k + 1]) { bad = AD_E_INVAL; bad_key = k; continue; }
+                pruned[k] = txn_rank[idx];
+            }
+        }
+    });
+    if (bad.load()) return c->fail(AD_E_INVAL, "prunedBefore of key %lld is not in byId", (long long)K.keys[bad_key.load()]);
+
+    // ---- 3. range commands: (range, command) entries sorted by (start, end, txnId); range table
+    struct REnt { int64_t s, e; uint32_t txw; uint32_t rid; };
+    std::vector<REnt> rent;
+    for (uint64_t i = 0; i < ncmd; ++i)
+    {
+        const bool hist = !c->cmds.historical.empty() && c->cmds.historical[i];
+        if (!hist && !c->cmds.erased.empty() && c->cmds.erased[i]) continue;   // saveStatus >= Erased, :897 (historical: no status)
+        const uint32_t kind = (uint32_t)((c->cmds.txn[i].lsb >> 1) & 7);
+        if ((c->cmds.txn[i].lsb & 1) == 0) return c->fail(AD_E_INVAL, "range command %llu has a key-domain TxnId", (unsigned long long)i);
+        for (uint64_t r = c->cmds.off[i]; r < c->cmds.off[i + 1]; ++r)
+            rent.push_back({c->cmds.start[r], c->cmds.end[r], cmd_rank[i] | (kind << RANK_BITS), 0});
+    }
+    for (uint64_t i = 0; i < nrb; ++i)
+        if (i > 0 && c->rb.start[i] <= c->rb.start[i - 1]) return c->fail(AD_E_INVAL, "redundantBefore entries not ascending");
+    {
+        std::vector<std::pair<int64_t, int64_t>> rt;
+        rt.reserve(rent.size() + nrb);
+        for (auto& r : rent) rt.push_back({r.s, r.e});
+        for (uint64_t i = 0; i < nrb; ++i) rt.push_back({c->rb.start[i], c->rb.end[i]});
+        std::sort(rt.begin(), rt.end());
+        rt.erase(std::unique(rt.begin(), rt.end()), rt.end());
+        c->rt_start.resize(rt.size());
+        c->rt_end.resize(rt.size());
+        for (size_t i = 0; i < rt.size(); ++i) { c->rt_start[i] = rt[i].first; c->rt_end[i] = rt[i].second; }
+        auto rid_of = [&](int64_t s, int64_t e) -> uint32_t {
+            return (uint32_t)(std::lower_bound(rt.begin(), rt.end(), std::make_pair(s, e)) - rt.begin());
+        };
+        for (auto& r : rent) r.rid = rid_of(r.s, r.e);
+        std::sort(rent.begin(), rent.end(), [](const REnt& a, const REnt& b) {
+            if (a.rid != b.rid) return a.rid < b.rid;
+            return (a.txw & RANK_MASK) < (b.txw & RANK_MASK);
+        });
+        rent.erase(std::unique(rent.begin(), rent.end(), [](const REnt& a, const REnt& b) {
+                       return a.rid == b.rid && (a.txw & RANK_MASK) == (b.txw & RANK_MASK);
+                   }),
+                   rent.end());
+        std::vector<uint32_t> rb_rid(nrb);
+        for (uint64_t i = 0; i < nrb; ++i) rb_rid[i] = rid_of(c->rb.start[i], c->rb.end[i]);
+        std::vector<int64_t> rs(rent.size()), re(rent.size());
+        std::vector<uint32_t> rtxw(rent.size()), rrid(rent.size());
+        for (size_t i = 0; i < rent.size(); ++i) { rs[i] = rent[i].s; re[i] = rent[i].e; rtxw[i] = rent[i].txw; rrid[i] = rent[i].rid; }
+        for (uint64_t i = 0; i < nrb; ++i)
+            if (wm_rank[i] && (c->rb.wm[i].lsb & 1) == 0) return c->fail(AD_E_INVAL, "redundantBefore watermark must be range-domain");
+        int rc;
+        if ((rc = upload(c, c->d_rstart, rs)) || (rc = upload(c, c->d_rend, re)) || (rc = upload(c, c->d_rtxw, rtxw)) ||
+            (rc = upload(c, c->d_rrid, rrid)) || (rc = upload(c, c->d_rb_s, c->rb.start)) || (rc = upload(c, c->d_rb_e, c->rb.end)) ||
+            (rc = upload(c, c->d_rb_e0, c->rb.e0)) || (rc = upload(c, c->d_rb_e1, c->rb.e1)) || (rc = upload(c, c->d_rb_wm, wm_rank)) ||
+            (rc = upload(c, c->d_rb_rid, rb_rid)))
+            return rc;
+    }
+
+    // ---- 4. upload CFK + dictionary, build the trees
+    int rc;
+    if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
+        (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_seg, seg32)) || (rc = upload(c, c->d_woff, woff)) ||
+        (rc = upload(c, c->d_maw, maw)) || (rc = upload(c, c->d_pruned, pruned)) || (rc = upload(c, c->d_ent, ent)) ||
+        (rc = upload(c, c->d_w, w)) || (rc = upload(c, c->d_slices_s, c->slice_s)) || (rc = upload(c, c->d_slices_e, c->slice_e)))
+        return rc;
+
+    DevSnapshot& s = c->ds;
+    s = DevSnapshot{};
+    s.dict_hi = c->d_dict_hi.as<uint64_t>();
+    s.dict_lo = c->d_dict_lo.as<uint64_t>();
+    s.dict_node = c->d_dict_node.as<int32_t>();
+    s.n_dict = dhi.size();
+    s.n_keys = nk;
+    s.keys = c->d_keys.as<int64_t>();
+    s.seg = c->d_seg.as<uint32_t>();
+    s.woff = c->d_woff.as<uint32_t>();
+    s.maw = c->d_maw.as<int32_t>();
+    s.pruned = c->d_pruned.as<uint32_t>();
+    s.n_ent = ne;
+    s.ent = c->d_ent.as<uint2>();
+    s.w = c->d_w.as<uint2>();
+    s.lvl_n[0] = ne;
+    int L = 1;
+    while (s.lvl_n[L - 1] > 64 && L < MAX_LEVELS)
+    {
+        s.lvl_n[L] = (s.lvl_n[L - 1] + 63) / 64;
+        ++L;
+    }
+    s.n_levels = L;
+    for (int l = 1; l < L; ++l)
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * s.lvl_n[l])) return c->fail(AD_E_NOMEM, "tree level");
+            s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
+        }
+    s.n_rent = rent.size();
+    s.r_start = c->d_rstart.as<int64_t>();
+    s.r_end = c->d_rend.as<int64_t>();
+    s.r_txw = c->d_rtxw.as<uint32_t>();
+    s.r_rid = c->d_rrid.as<uint32_t>();
+    s.rlvl_n[0] = s.n_rent;
+    L = 1;
+    while (s.rlvl_n[L - 1] > 64 && L < MAX_LEVELS)
+    {
+        s.rlvl_n[L] = (s.rlvl_n[L - 1] + 63) / 64;
+        ++L;
+    }
+    s.n_rlevels = L;
+    for (int l = 1; l < L; ++l)
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            if (!c->d_rlvl[cl][l].ensure(sizeof(int64_t) * s.rlvl_n[l])) return c->fail(AD_E_NOMEM, "range tree level");
+            s.rlvl[cl][l] = c->d_rlvl[cl][l].as<int64_t>();
+        }
+    s.n_rb = nrb;
+    s.rb_start = c->d_rb_s.as<int64_t>();
+    s.rb_end = c->d_rb_e.as<int64_t>();
+    s.rb_e0 = c->d_rb_e0.as<int64_t>();
+    s.rb_e1 = c->d_rb_e1.as<int64_t>();
+    s.rb_wm = c->d_rb_wm.as<uint32_t>();
+    s.rb_rid = c->d_rb_rid.as<uint32_t>();
+    s.n_slices = c->slice_s.size();
+    s.slice_start = c->d_slices_s.as<int64_t>();
+    s.slice_end = c->d_slices_e.as<int64_t>();
+    s.start_inclusive = c->cfg.range_start_inclusive;
+    s.elide = c->cfg.elide;
+    HIPCHK(c, build_cfk_trees(s, c->stream));
+    HIPCHK(c, build_range_trees(s, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->dirty = false;
+    c->ms_ingest = now_ms() - t0;
+    return 0;
+}
+
+// SEQUENTIAL: insert every request's txnId as PREACCEPTED_OR_ACCEPTED_INVALIDATE into the
+// CommandsForKey of each of its keys in the slice (CommandsForKey.update, :972-1042; a present
+// entry below PREACCEPTED is raised, otherwise left alone).
+static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
+{
+    auto& K = c->cfk;
+    struct Ins { int64_t key; NormTid n; Tid t; };
+    std::vector<Ins> ins;
+    for (uint64_t i = 0; i < q->n_txns; ++i)
+    {
+        const Tid t{q->txn_msb[i], q->txn_lsb[i], q->txn_node[i]};
+        const Tid x{q->exec_msb[i], q->exec_lsb[i], q->exec_node[i]};
+        if (!(t.msb == x.msb && ((t.lsb ^ x.lsb) & 0xFFFFFFFFFFFF001EULL) == 0 && t.node == x.node))
+            return c->fail(AD_E_INVAL, "SEQUENTIAL (PreAccept) requests need executeAt == txnId");
+        if (i > 0)
+        {
+            const Tid p{q->txn_msb[i - 1], q->txn_lsb[i - 1], q->txn_node[i - 1]};
+            if (norm_cmp(norm(p), norm(t)) >= 0) return c->fail(AD_E_INVAL, "SEQUENTIAL requests must be in ascending TxnId order");
+        }
+        const uint32_t kind = (uint32_t)((t.lsb >> 1) & 7);
+        const bool manages = (t.lsb & 1) == 0 && ((KINDS_ANY_GLOBALLY_VISIBLE >> kind) & 1);  // CommandsForKey.manages :185-188
+        if (!manages) continue;
+        for (uint64_t k = q->key_off[i]; k < q->key_off[i + 1]; ++k)
+        {
+            const int64_t key = q->keys[k];
+            bool in = c->slice_s.empty();
+            for (size_t s = 0; s < c->slice_s.size() && !in; ++s)
+                in = range_contains(c->cfg.range_start_inclusive, c->slice_s[s], c->slice_e[s], key);
+            if (in) ins.push_back({key, norm(t), t});
+        }
+    }
+    if (ins.empty()) return 0;
+    std::stable_sort(ins.begin(), ins.end(), [](const Ins& a, const Ins& b) {
+        if (a.key != b.key) return a.key < b.key;
+        return norm_cmp(a.n, b.n) < 0;
+    });
+    std::vector<int64_t> nkeys;
+    std::vector<uint64_t> nseg{0};
+    std::vector<Tid> ntx, nex;
+    std::vector<uint8_t> nst;
+    std::vector<int64_t> npr;
+    size_t ki = 0, ii = 0;
+    const size_t nk = K.keys.size();
+    while (ki < nk || ii < ins.size())
+    {
+        int64_t key;
+        if (ii >= ins.size() || (ki < nk && K.keys[ki] <= ins[ii].key)) key = K.keys[ki];
+        else key = ins[ii].key;
+        const bool has_old = ki < nk && K.keys[ki] == key;
+        uint64_t e = has_old ? K.seg[ki] : 0, e1 = has_old ? K.seg[ki + 1] : 0;
+        const size_t base = ntx.size();
+        int64_t pr = has_old && !K.pruned.empty() ? K.pruned[ki] : -1;
+        int64_t pr_new = -1;
+        while (e < e1 || (ii < ins.size() && ins[ii].key == key))
+        {
+            const bool take_old = e < e1 && (!(ii < ins.size() && ins[ii].key == key) || norm_cmp(norm(K.txn[e]), ins[ii].n) <= 0);
+            if (take_old)
+            {
+                if ((int64_t)(e - K.seg[ki]) == pr) pr_new = (int64_t)(ntx.size() - base);
+                const bool same = ii < ins.size() && ins[ii].key == key && norm_cmp(norm(K.txn[e]), ins[ii].n) == 0;
+                ntx.push_back(K.txn[e]);
+                if (same && K.status[e] < AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE)
+                {
+                    nex.push_back(K.txn[e]);
+                    nst.push_back(AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE);
+                }
+                else
+                {
+                    nex.push_back(K.exec[e]);
+                    nst.push_back(K.status[e]);
+                }
+                if (same) ++ii;
+                ++e;
+            }
+            else
+            {
+                ntx.push_back(ins[ii].t);
+                nex.push_back(ins[ii].t);
+                nst.push_back(AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE);
+                ++ii;
+            }
+        }
+        nkeys.push_back(key);
+        nseg.push_back(ntx.size());
+        npr.push_back(pr_new);
+        if (has_old) ++ki;
+    }
+    K.keys.swap(nkeys);
+    K.seg.swap(nseg);
+    K.txn.swap(ntx);
+    K.exec.swap(nex);
+    K.status.swap(nst);
+    K.pruned.swap(npr);
+    c->dirty = true;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// batch pipeline
+// ---------------------------------------------------------------------------------------
+template <class T>
+static bool ens(DevBuf& b, uint64_t n) { return b.ensure(sizeof(T) * std::max<uint64_t>(n, 1)); }
+
+static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out)
+{
+    const uint64_t n = q->n_txns;
+    uint64_t np = 0;
+    if (n)
+    {
+        HIPCHK(c, hipMemcpyAsync(&np, q->key_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+    }
+    BatchBufs b{};
+    b.n_txns = n;
+    b.n_probes = np;
+    b.q_txn_msb = q->txn_msb; b.q_txn_lsb = q->txn_lsb; b.q_txn_node = q->txn_node;
+    b.q_exec_msb = q->exec_msb; b.q_exec_lsb = q->exec_lsb; b.q_exec_node = q->exec_node;
+    b.q_min_epoch = q->min_epoch; b.q_key_off = q->key_off; b.q_keys = q->keys;
+    const uint64_t nb = (n + 1023) / 1024;
+    if (!ens<uint32_t>(c->t_S, n) || !ens<uint32_t>(c->t_self, n) || !ens<uint32_t>(c->t_kinds, n) ||
+        !ens<int64_t>(c->t_epoch, n) || !ens<uint32_t>(c->p_txn, np) || !ens<int32_t>(c->p_key, np) ||
+        !ens<uint8_t>(c->p_slice, np) || !ens<uint32_t>(c->p_off, np) || !ens<uint32_t>(c->p_c0, np) ||
+        !ens<uint32_t>(c->p_c1, np) || !ens<uint32_t>(c->p_roff, np) || !ens<uint32_t>(c->p_rcnt, np) ||
+        !ens<uint64_t>(c->p_rb, np) || !ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) ||
+        !ens<uint64_t>(c->bsum, 9 * nb) || !ens<uint64_t>(c->t_scr, n) || !ens<BatchCtl>(c->ctl, 1))
+        return c->fail(AD_E_NOMEM, "batch buffers");
+    b.t_S = c->t_S.as<uint32_t>(); b.t_self = c->t_self.as<uint32_t>(); b.t_kinds = c->t_kinds.as<uint32_t>();
+    b.t_epoch = c->t_epoch.as<int64_t>(); b.p_txn = c->p_txn.as<uint32_t>(); b.p_key = c->p_key.as<int32_t>();
+    b.p_slice = c->p_slice.as<uint8_t>(); b.p_off = c->p_off.as<uint32_t>(); b.p_c0 = c->p_c0.as<uint32_t>();
+    b.p_c1 = c->p_c1.as<uint32_t>(); b.p_roff = c->p_roff.as<uint32_t>(); b.p_rcnt = c->p_rcnt.as<uint32_t>();
+    b.p_rb = c->p_rb.as<uint64_t>(); b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>();
+    b.bsum = c->bsum.as<uint64_t>(); b.t_scr = c->t_scr.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>();
+
+    const uint64_t waves = (uint64_t)device_cu_count() * 8 * 4;
+    uint64_t want_key = std::max<uint64_t>(np * 4 + waves * 4096, 1u << 20);
+    uint64_t want_rng = c->ds.n_rent ? std::max<uint64_t>(np * 2 + waves * 2048, 1u << 20) : 1;
+    uint64_t want_scr = 64ull << 20;
+    if (c->key_cap < want_key) c->key_cap = want_key;
+    if (c->rng_cap < want_rng) c->rng_cap = want_rng;
+    if (c->scr_cap < want_scr) c->scr_cap = want_scr;
+
+    for (int attempt = 0; attempt < 6; ++attempt)
+    {
+        if (!c->arena.ensure(sizeof(uint32_t) * c->key_cap)) return c->fail(AD_E_NOMEM, "key arena %llu", (unsigned long long)c->key_cap);
+        if (!c->rarena.ensure(sizeof(uint64_t) * c->rng_cap)) return c->fail(AD_E_NOMEM, "range arena");
+        if (!c->scratch.ensure(c->scr_cap)) return c->fail(AD_E_NOMEM, "scratch");
+        b.arena = c->arena.as<uint32_t>();
+        b.rarena = c->rarena.as<uint64_t>();
+        b.scratch = c->scratch.as<uint8_t>();
+        BatchCtl h{};
+        h.key_cap = c->key_cap;
+        h.rng_cap = c->rng_cap;
+        h.scr_cap = c->scr_cap;
+        HIPCHK(c, hipMemcpyAsync(b.ctl, &h, sizeof(h), hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipEventRecord(c->ev[0], st));
+        HIPCHK(c, run_encode(c->ds, b, st));
+        HIPCHK(c, hipEventRecord(c->ev[1], st));
+        HIPCHK(c, run_scan(c->ds, b, st));
+        HIPCHK(c, hipEventRecord(c->ev[2], st));
+        HIPCHK(c, run_range(c->ds, b, st));
+        HIPCHK(c, hipEventRecord(c->ev[3], st));
+        HIPCHK(c, run_build(c->ds, b, false, st));
+        HIPCHK(c, hipEventRecord(c->ev[4], st));
+        HIPCHK(c, run_offsets(b, st));
+        HIPCHK(c, hipEventRecord(c->ev[5], st));
+        uint64_t tot[9] = {0};
+        for (int a = 0; a < 9; ++a)
+            HIPCHK(c, hipMemcpyAsync(&tot[a], b.off + (uint64_t)a * (n + 1) + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (h.error)
+        {
+            if (h.error == ERR_STATE)
+                return c->fail(AD_E_STATE, "reference would throw: prunedBefore set but no applied Write (CommandsForKey.java:962)");
+            return c->fail(AD_E_INVAL, "invalid Txn.Kind for witnesses() in a request (Txn.java:221-235)");
+        }
+        if (h.overflow)
+        {
+            if (h.overflow & 1u) c->key_cap = std::max<uint64_t>(c->key_cap * 2, h.key_top + (h.key_top >> 1));
+            if (h.overflow & 2u) c->rng_cap = std::max<uint64_t>(c->rng_cap * 2, h.rng_top + (h.rng_top >> 1));
+            if (h.overflow & 4u) c->scr_cap = std::max<uint64_t>(c->scr_cap * 2, h.scr_top + (h.scr_top >> 1));
+            continue;
+        }
+        for (int m = 0; m < 3; ++m)
+        {
+            if (!ens<int64_t>(c->o_keys[m], tot[3 * m + 0]) || !ens<uint32_t>(c->o_txns[m], tot[3 * m + 1]) ||
+                !ens<int32_t>(c->o_k2t[m], tot[3 * m + 2]))
+                return c->fail(AD_E_NOMEM, "outputs");
+            b.o_keys[m] = c->o_keys[m].as<int64_t>();
+            b.o_txns[m] = c->o_txns[m].as<uint32_t>();
+            b.o_k2t[m] = c->o_k2t[m].as<int32_t>();
+        }
+        HIPCHK(c, hipEventRecord(c->ev[6], st));
+        HIPCHK(c, run_build(c->ds, b, true, st));
+        HIPCHK(c, hipEventRecord(c->ev[7], st));
+        HIPCHK(c, hipStreamSynchronize(st));
+
+        ad_stats& S = out->stats;
+        memset(&S, 0, sizeof(S));
+        S.n_txns = n;
+        S.n_probes = np;
+        for (int m = 0; m < 3; ++m)
+        {
+            S.n_pairs[m] = tot[3 * m + 2] - tot[3 * m + 0];
+            S.n_unique[m] = tot[3 * m + 1];
+        }
+        float ms;
+        const int pairs[6][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}};
+        double total = 0;
+        for (int i = 0; i < 6; ++i)
+        {
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
+            S.ms_stage[i] = ms;
+            total += ms;
+        }
+        S.ms_device = total;
+        S.ms_ingest = c->ms_ingest;
+        // algorithmic bytes
+        S.bytes_stage[0] = n * (2 * 20 + 8) + np * (8 + 4 + 4 + 1);
+        S.bytes_stage[1] = np * (4 + 4 + 4 + 4 + 12) + (S.n_pairs[0] + S.n_pairs[2]) * 4;
+        S.bytes_stage[2] = np * (8 + 4 + 4 + 16);
+        S.bytes_stage[5] = (S.n_pairs[0] + S.n_pairs[1] + S.n_pairs[2]) * 4 * 2 +
+                           (S.n_unique[0] + S.n_unique[1] + S.n_unique[2]) * 4 +
+                           (tot[0] + tot[3] + tot[6]) * 12;
+        out->n_txns = n;
+        for (int m = 0; m < 3; ++m)
+        {
+            out->keys_off[m] = b.off + (uint64_t)(3 * m + 0) * (n + 1);
+            out->txn_off[m] = b.off + (uint64_t)(3 * m + 1) * (n + 1);
+            out->k2t_off[m] = b.off + (uint64_t)(3 * m + 2) * (n + 1);
+            out->keys[m] = b.o_keys[m];
+            out->txns[m] = b.o_txns[m];
+            out->k2t[m] = b.o_k2t[m];
+        }
+        return 0;
+    }
+    return c->fail(AD_E_NOMEM, "arena growth did not converge");
+}
+
+template <class T>
+static T* stage_q(ad_ctx* c, DevBuf& b, const T* src, uint64_t n, int* rc)
+{
+    if (!src) return nullptr;
+    if (!b.ensure(sizeof(T) * std::max<uint64_t>(n, 1))) { *rc = c->fail(AD_E_NOMEM, "query staging"); return nullptr; }
+    if (n && hipMemcpyAsync(b.p, src, sizeof(T) * n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    {
+        *rc = c->fail(AD_E_DEVICE, "query H2D");
+        return nullptr;
+    }
+    return b.as<T>();
+}
+
+template <class T>
+static T* d2h(const T* src, uint64_t n)
+{
+    T* p = (T*)malloc(sizeof(T) * std::max<uint64_t>(n, 1));
+    if (p && n) (void)hipMemcpy(p, src, sizeof(T) * n, hipMemcpyDeviceToHost);
+    return p;
+}
+
+static int check_query_host(ad_ctx* c, const ad_query_soa* q)
+{
+    for (uint64_t i = 0; i < q->n_txns; ++i)
+        for (uint64_t k = q->key_off[i] + 1; k < q->key_off[i + 1]; ++k)
+            if (q->keys[k - 1] >= q->keys[k]) return c->fail(AD_E_INVAL, "request %llu: keys not strictly ascending", (unsigned long long)i);
+    return 0;
+}
+
+}  // namespace
+
+// =======================================================================================
+// C ABI
+// =======================================================================================
+extern "C" {
+
+int ad_abi_version(void) { return AD_ABI_VERSION; }
+
+static thread_local std::string g_create_err;
+
+int ad_ctx_create(const ad_config* cfg, ad_ctx** out)
+{
+    if (!cfg || !out) return AD_E_INVAL;
+    ad_ctx* c = new (std::nothrow) ad_ctx();
+    if (!c) return AD_E_NOMEM;
+    hipError_t e;
+    c->cfg = *cfg;
+    for (uint64_t i = 0; i < cfg->n_slices; ++i)
+    {
+        c->slice_s.push_back(cfg->slice_start[i]);
+        c->slice_e.push_back(cfg->slice_end[i]);
+    }
+    c->cfg.slice_start = nullptr;
+    c->cfg.slice_end = nullptr;
+    c->device = cfg->device;
+    if ((e = hipSetDevice(c->device)) != hipSuccess || (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
+    {
+        g_create_err = std::string("ad_ctx_create: ") + hipGetErrorName(e) + ": " + hipGetErrorString(e);
+        delete c;
+        return AD_E_DEVICE;
+    }
+    for (auto& ev : c->ev)
+        if ((e = hipEventCreate(&ev)) != hipSuccess)
+        {
+            g_create_err = std::string("ad_ctx_create: hipEventCreate: ") + hipGetErrorString(e);
+            delete c;
+            return AD_E_DEVICE;
+        }
+    *out = c;
+    return AD_OK;
+}
+
+void ad_ctx_destroy(ad_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* ad_last_error(const ad_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
+{
+    if (!c || !in) return AD_E_INVAL;
+    auto& K = c->cfk;
+    const uint64_t nk = in->n_keys, ne = in->n_entries;
+    if ((nk && (!in->keys || !in->seg)) || (!nk && ne)) return c->fail(AD_E_INVAL, "bad cfk soa");
+    if (nk && in->seg[nk] != ne) return c->fail(AD_E_INVAL, "seg[n_keys] != n_entries");
+    K.keys.assign(in->keys, in->keys + nk);
+    K.seg.assign(nk + 1, 0);
+    if (nk) std::copy(in->seg, in->seg + nk + 1, K.seg.begin());
+    for (uint64_t k = 0; k < nk; ++k)
+        if (K.seg[k] > K.seg[k + 1]) return c->fail(AD_E_INVAL, "seg not monotone");
+    K.txn.resize(ne);
+    K.exec.resize(ne);
+    for (uint64_t e = 0; e < ne; ++e)
+    {
+        K.txn[e] = {in->txn_msb[e], in->txn_lsb[e], in->txn_node[e]};
+        K.exec[e] = {in->exec_msb[e], in->exec_lsb[e], in->exec_node[e]};
+    }
+    K.status.assign(in->status, in->status + ne);
+    K.pruned.clear();
+    if (in->pruned_before) K.pruned.assign(in->pruned_before, in->pruned_before + nk);
+    K.loaded = true;
+    c->dirty = true;
+    return AD_OK;
+}
+
+int ad_range_cmds_load(ad_ctx* c, const ad_range_cmds_soa* in)
+{
+    if (!c || !in) return AD_E_INVAL;
+    auto& R = c->cmds;
+    const uint64_t n = in->n_cmds;
+    R.txn.resize(n);
+    for (uint64_t i = 0; i < n; ++i) R.txn[i] = {in->txn_msb[i], in->txn_lsb[i], in->txn_node[i]};
+    R.erased.clear();
+    R.historical.clear();
+    if (in->erased) R.erased.assign(in->erased, in->erased + n);
+    if (in->historical) R.historical.assign(in->historical, in->historical + n);
+    R.off.assign(in->range_off, in->range_off + n + 1);
+    const uint64_t nr = n ? in->range_off[n] : 0;
+    R.start.assign(in->range_start, in->range_start + nr);
+    R.end.assign(in->range_end, in->range_end + nr);
+    c->dirty = true;
+    return AD_OK;
+}
+
+int ad_redundant_load(ad_ctx* c, const ad_redundant_soa* in)
+{
+    if (!c || !in) return AD_E_INVAL;
+    auto& B = c->rb;
+    const uint64_t n = in->n;
+    B.start.assign(in->range_start, in->range_start + n);
+    B.end.assign(in->range_end, in->range_end + n);
+    B.e0.assign(in->start_epoch, in->start_epoch + n);
+    B.e1.assign(in->end_epoch, in->end_epoch + n);
+    B.wm.resize(n);
+    for (uint64_t i = 0; i < n; ++i) B.wm[i] = {in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
+    c->dirty = true;
+    return AD_OK;
+}
+
+int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_result** out)
+{
+    if (!c || !q || !out) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    int rc = check_query_host(c, q);
+    if (rc) return rc;
+    if (flags & AD_SEQUENTIAL)
+    {
+        // keep a copy so a failed batch leaves the snapshot untouched
+        auto saved = c->cfk;
+        if ((rc = apply_preaccepts(c, q))) { c->cfk = saved; return rc; }
+    }
+    if (c->dirty && (rc = build_snapshot(c))) return rc;
+    const uint64_t n = q->n_txns;
+    const uint64_t np = n ? q->key_off[n] : 0;
+    ad_query_soa d{};
+    d.n_txns = n;
+    rc = 0;
+    d.txn_msb = stage_q(c, c->q_tm, q->txn_msb, n, &rc);
+    d.txn_lsb = stage_q(c, c->q_tl, q->txn_lsb, n, &rc);
+    d.txn_node = stage_q(c, c->q_tn, q->txn_node, n, &rc);
+    d.exec_msb = stage_q(c, c->q_em, q->exec_msb, n, &rc);
+    d.exec_lsb = stage_q(c, c->q_el, q->exec_lsb, n, &rc);
+    d.exec_node = stage_q(c, c->q_en, q->exec_node, n, &rc);
+    d.min_epoch = stage_q(c, c->q_me, q->min_epoch, n, &rc);
+    d.key_off = stage_q(c, c->q_ko, q->key_off, n + 1, &rc);
+    d.keys = stage_q(c, c->q_k, q->keys, np, &rc);
+    if (rc) return rc;
+    ad_deps_result dev{};
+    if ((rc = run_pipeline(c, &d, c->stream, &dev))) return rc;
+    ad_deps_result* r = (ad_deps_result*)calloc(1, sizeof(ad_deps_result));
+    if (!r) return c->fail(AD_E_NOMEM, "result");
+    r->n_txns = n;
+    r->stats = dev.stats;
+    for (int m = 0; m < 3; ++m)
+    {
+        r->keys_off[m] = d2h(dev.keys_off[m], n + 1);
+        r->txn_off[m] = d2h(dev.txn_off[m], n + 1);
+        r->k2t_off[m] = d2h(dev.k2t_off[m], n + 1);
+        const uint64_t nk = r->keys_off[m][n], nt = r->txn_off[m][n], no = r->k2t_off[m][n];
+        r->keys[m] = d2h(dev.keys[m], nk);
+        r->txns[m] = d2h(dev.txns[m], nt);
+        r->k2t[m] = d2h(dev.k2t[m], no);
+    }
+    *out = r;
+    return AD_OK;
+}
+
+int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void* stream, ad_deps_result* out)
+{
+    if (!c || !q || !out) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (flags & AD_SEQUENTIAL) return c->fail(AD_E_INVAL, "device-resident batches are SNAPSHOT only");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    int rc;
+    if (c->dirty && (rc = build_snapshot(c))) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return run_pipeline(c, q, st, out);
+}
+
+void ad_result_free(ad_deps_result* r)
+{
+    if (!r) return;
+    for (int m = 0; m < 3; ++m)
+    {
+        free(r->keys_off[m]); free(r->keys[m]); free(r->txn_off[m]); free(r->txns[m]); free(r->k2t_off[m]); free(r->k2t[m]);
+    }
+    free(r);
+}
+
+int ad_dict(const ad_ctx* c, uint64_t* n, const uint64_t** msb, const uint64_t** lsb, const int32_t** node)
+{
+    if (!c || !n) return AD_E_INVAL;
+    *n = c->dict_msb.size();
+    if (msb) *msb = c->dict_msb.data();
+    if (lsb) *lsb = c->dict_lsb.data();
+    if (node) *node = c->dict_node.data();
+    return AD_OK;
+}
+
+int ad_range_table(const ad_ctx* c, uint64_t* n, const int64_t** start, const int64_t** end)
+{
+    if (!c || !n) return AD_E_INVAL;
+    *n = c->rt_start.size();
+    if (start) *start = c->rt_start.data();
+    if (end) *end = c->rt_end.data();
+    return AD_OK;
+}
+
+int ad_levels(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, ad_stats* stats)
+{
+    if (!c) return AD_E_INVAL;
+    return c->fail(AD_E_INVAL, "ad_levels: not implemented yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+// common.hpp — shared definitions of libaccord_deps (host runtime + gfx950 kernels).
+//
+// Device representation:
+//   * every TxnId/Timestamp of a store snapshot is replaced by its rank in a sorted id
+//     dictionary: member i -> 2i+1 (odd); a foreign id falling between members i-1 and i
+//     -> 2i (even). Rank order == Timestamp.compareTo order (Timestamp.java:208-217) and rank
+//     equality == Timestamp.equals (:244-249), so all kernels compare u32 ranks.
+//   * CommandsForKey byId entries (CommandsForKey.java:621) are `uint2 {tau, txw}`:
+//       txw = rank | kind << 29
+//       tau = elision threshold key: 0 for TRANSITIVELY_KNOWN/INVALID (never emitted),
+//             executeAt rank for committed Read/Write (emitted iff executeAt >= M),
+//             0xFFFFFFFF otherwise (never elided)                      (:930-950)
+//   * per witness class a 64-ary max tree over tau restricted to the class' kinds
+//     prunes byId[0,end) down to the emitted entries.
+#pragma once
+#include <cstdint>
+#include <cstddef>
+
+namespace adx {
+
+constexpr uint32_t RANK_BITS = 29;
+constexpr uint32_t RANK_MASK = (1u << RANK_BITS) - 1;
+constexpr uint64_t MAX_DICT = (1ull << 28) - 1;     // 2*MAX_DICT+1 < 2^29
+constexpr uint32_t TAU_NEVER_ELIDED = 0xFFFFFFFFu;
+constexpr uint32_t CLASS_DIRECT_BIT = 0x80000000u;   // K1 output: rank | direct-key-deps bit
+constexpr int NCLASS = 3;                             // Ws, RsOrWs, AnyGloballyVisible
+constexpr int MAX_LEVELS = 8;                         // 64^8 > 2^32 entries
+constexpr int WAVE = 64;
+
+// Txn.Kind.Kinds as masks over Kind ordinals (Txn.java:114-152)
+constexpr uint32_t KINDS_WS = 1u << 1;
+constexpr uint32_t KINDS_RS_OR_WS = (1u << 0) | (1u << 1);
+constexpr uint32_t KINDS_ANY_GLOBALLY_VISIBLE = (1u << 0) | (1u << 1) | (1u << 3) | (1u << 4);
+constexpr uint32_t CLASS_KINDS[NCLASS] = {KINDS_WS, KINDS_RS_OR_WS, KINDS_ANY_GLOBALLY_VISIBLE};
+
+// Txn.Kind.witnesses() (Txn.java:221-235); 0 = AssertionError (invalid kind for a query)
+__host__ __device__ inline uint32_t kind_witnesses(uint32_t kind)
+{
+    switch (kind)
+    {
+        case 0: case 2: return KINDS_WS;                    // Read, EphemeralRead
+        case 1: case 3: return KINDS_RS_OR_WS;              // Write, SyncPoint
+        case 4: return KINDS_ANY_GLOBALLY_VISIBLE;          // ExclusiveSyncPoint
+        default: return 0;
+    }
+}
+
+// smallest witness class whose kind set contains `kinds`
+__host__ __device__ inline int kinds_class(uint32_t kinds)
+{
+    if ((kinds & ~KINDS_WS) == 0) return 0;
+    if ((kinds & ~KINDS_RS_OR_WS) == 0) return 1;
+    return 2;
+}
+
+// normalised, order-preserving form of a Timestamp: (hi, lo, node) compared lexicographically,
+// hi unsigned, lo unsigned, node signed (Timestamp.compareTo)
+struct NormTid { uint64_t hi, lo; int32_t node; };
+
+__host__ __device__ inline NormTid norm_tid(uint64_t msb, uint64_t lsb, int32_t node)
+{
+    NormTid t;
+    t.hi = msb;
+    t.lo = ((lsb >> 16) << 4) | ((lsb >> 1) & 0xF);        // lowHlc, then lsb & IDENTITY_FLAGS
+    t.node = node;
+    return t;
+}
+
+__host__ __device__ inline int norm_cmp(const NormTid& a, const NormTid& b)
+{
+    if (a.hi != b.hi) return a.hi < b.hi ? -1 : 1;
+    if (a.lo != b.lo) return a.lo < b.lo ? -1 : 1;
+    if (a.node != b.node) return a.node < b.node ? -1 : 1;
+    return 0;
+}
+
+// Per-store device snapshot, passed to kernels by value.
+struct DevSnapshot {
+    // id dictionary (normalised)
+    const uint64_t* dict_hi;
+    const uint64_t* dict_lo;
+    const int32_t*  dict_node;
+    uint64_t n_dict;
+    // CommandsForKey
+    uint64_t n_keys;
+    const int64_t*  keys;          // [n_keys]
+    const uint32_t* seg;           // [n_keys+1] into ent
+    const uint32_t* woff;          // [n_keys+1] into w
+    const int32_t*  maw;           // [n_keys] index (absolute, into w) of maxAppliedWriteByExecuteAt, -1
+    const uint32_t* pruned;        // [n_keys] rank of prunedBefore, 0 = NONE
+    uint64_t n_ent;
+    const uint2*    ent;           // {tau, txw}
+    const uint2*    w;             // committed Writes by executeAt: {exec rank, txn rank}
+    const uint32_t* lvl[NCLASS][MAX_LEVELS];   // [c][l], l >= 1 (lvl[c][0] unused)
+    uint64_t lvl_n[MAX_LEVELS];
+    int n_levels;                  // number of levels incl. leaf
+    // range commands (flattened (range, command) entries sorted by (start, end, rank))
+    uint64_t n_rent;
+    const int64_t*  r_start;
+    const int64_t*  r_end;
+    const uint32_t* r_txw;         // rank | kind << 29
+    const uint32_t* r_rid;         // range id (index into the range table)
+    const int64_t*  rlvl[NCLASS][MAX_LEVELS];  // max end per 64^l block
+    uint64_t rlvl_n[MAX_LEVELS];
+    int n_rlevels;
+    // redundant-before (disjoint, ascending)
+    uint64_t n_rb;
+    const int64_t*  rb_start;
+    const int64_t*  rb_end;
+    const int64_t*  rb_e0;
+    const int64_t*  rb_e1;
+    const uint32_t* rb_wm;         // rank of shardAppliedOrInvalidatedBefore (0 = NONE / not > NONE)
+    const uint32_t* rb_rid;
+    // store slice
+    uint64_t n_slices;
+    const int64_t* slice_start;
+    const int64_t* slice_end;
+    int start_inclusive;
+    int elide;
+};
+
+// Range.contains(key) (Range.java:40-56 EndInclusive, :84-100 StartInclusive)
+__host__ __device__ inline bool range_contains(int start_inclusive, int64_t s, int64_t e, int64_t key)
+{
+    return start_inclusive ? (s <= key && key < e) : (s < key && key <= e);
+}
+
+}  // namespace adx

@@ -1,0 +1,952 @@
+// kernels.hip — hand-written gfx950 (CDNA4, wave64) kernels of the dependency-resolution path.
+//
+//   K0  k_encode_txn / k_probe_keys   request -> ranks; (request, key) -> CommandsForKey index
+//   K1  k_scan                         CommandsForKey.mapReduceActive (CommandsForKey.java:910-968)
+//   K4  k_range                        InMemoryCommandStore.mapReduceRangesInternal (:884-1017)
+//                                      + RedundantBefore.collectDeps (RedundantBefore.java:183-192)
+//   K2  k_build<EMIT>                  Deps.AbstractBuilder.add + RelationMultiMap.AbstractBuilder.build
+//                                      (Deps.java:80-106, RelationMultiMap.java:147-260) and
+//                                      PartialDeps.with (PartialDeps.java:73-81, linearUnion
+//                                      RelationMultiMap.java:561-816) as a multi-list union
+//   trees / scans                      index build and exclusive scans
+//
+// All integer work; no MFMA. Memory-/latency-bound: coalesced 64-lane loads, ballot/mbcnt
+// compaction, LDS staging, wave-uniform control.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace adx {
+
+
+__device__ __forceinline__ void set_error(BatchCtl* ctl, unsigned code) { atomicCAS(&ctl->error, 0u, code); }
+
+// ---------------------------------------------------------------------------------------
+// Index build: per witness class, 64-ary max trees over tau (CFK) and over range ends.
+// ---------------------------------------------------------------------------------------
+__global__ void k_tree_leaf_cfk(const uint2* __restrict__ ent, uint64_t n, uint32_t* __restrict__ out0,
+                                uint32_t* __restrict__ out1, uint32_t* __restrict__ out2, uint64_t n_out)
+{
+    // one wave per level-1 node: 64 coalesced leaves, wave max per class
+    const uint64_t node = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (node >= n_out) return;
+    const uint64_t i = node * 64 + lane_id();
+    uint32_t v[NCLASS] = {0, 0, 0};
+    if (i < n)
+    {
+        const uint2 e = ent[i];
+        const uint32_t kd = e.y >> RANK_BITS;
+#pragma unroll
+        for (int c = 0; c < NCLASS; ++c) v[c] = ((CLASS_KINDS[c] >> kd) & 1) ? e.x : 0u;
+    }
+#pragma unroll
+    for (int c = 0; c < NCLASS; ++c)
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v[c] = max(v[c], (uint32_t)__shfl_xor(v[c], d, 64));
+    if (lane_id() == 0) { out0[node] = v[0]; out1[node] = v[1]; out2[node] = v[2]; }
+}
+
+template <class T>
+__global__ void k_tree_up(const T* __restrict__ in, uint64_t n, T* __restrict__ out, uint64_t n_out, T neutral)
+{
+    const uint64_t node = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (node >= n_out) return;
+    const uint64_t i = node * 64 + lane_id();
+    T v = i < n ? in[i] : neutral;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1)
+    {
+        T o = __shfl_xor(v, d, 64);
+        v = o > v ? o : v;
+    }
+    if (lane_id() == 0) out[node] = v;
+}
+
+__global__ void k_tree_leaf_range(const int64_t* __restrict__ r_end, const uint32_t* __restrict__ r_txw, uint64_t n,
+                                  int64_t* __restrict__ out0, int64_t* __restrict__ out1, int64_t* __restrict__ out2,
+                                  uint64_t n_out)
+{
+    const uint64_t node = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (node >= n_out) return;
+    const uint64_t i = node * 64 + lane_id();
+    int64_t v[NCLASS] = {INT64_MIN, INT64_MIN, INT64_MIN};
+    if (i < n)
+    {
+        const int64_t e = r_end[i];
+        const uint32_t kd = r_txw[i] >> RANK_BITS;
+#pragma unroll
+        for (int c = 0; c < NCLASS; ++c) v[c] = ((CLASS_KINDS[c] >> kd) & 1) ? e : INT64_MIN;
+    }
+#pragma unroll
+    for (int c = 0; c < NCLASS; ++c)
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1)
+        {
+            int64_t o = __shfl_xor(v[c], d, 64);
+            v[c] = o > v[c] ? o : v[c];
+        }
+    if (lane_id() == 0) { out0[node] = v[0]; out1[node] = v[1]; out2[node] = v[2]; }
+}
+
+static inline unsigned grid_for_waves(uint64_t waves, unsigned waves_per_block)
+{
+    uint64_t g = (waves + waves_per_block - 1) / waves_per_block;
+    return (unsigned)(g ? g : 1);
+}
+
+hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st)
+{
+    if (s.n_levels <= 1) return hipSuccess;
+    k_tree_leaf_cfk<<<grid_for_waves(s.lvl_n[1], 4), 256, 0, st>>>(
+        s.ent, s.n_ent, const_cast<uint32_t*>(s.lvl[0][1]), const_cast<uint32_t*>(s.lvl[1][1]),
+        const_cast<uint32_t*>(s.lvl[2][1]), s.lvl_n[1]);
+    for (int l = 2; l < s.n_levels; ++l)
+        for (int c = 0; c < NCLASS; ++c)
+            k_tree_up<uint32_t><<<grid_for_waves(s.lvl_n[l], 4), 256, 0, st>>>(
+                s.lvl[c][l - 1], s.lvl_n[l - 1], const_cast<uint32_t*>(s.lvl[c][l]), s.lvl_n[l], 0u);
+    return hipGetLastError();
+}
+
+hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st)
+{
+    if (s.n_rlevels <= 1) return hipSuccess;
+    k_tree_leaf_range<<<grid_for_waves(s.rlvl_n[1], 4), 256, 0, st>>>(
+        s.r_end, s.r_txw, s.n_rent, const_cast<int64_t*>(s.rlvl[0][1]), const_cast<int64_t*>(s.rlvl[1][1]),
+        const_cast<int64_t*>(s.rlvl[2][1]), s.rlvl_n[1]);
+    for (int l = 2; l < s.n_rlevels; ++l)
+        for (int c = 0; c < NCLASS; ++c)
+            k_tree_up<int64_t><<<grid_for_waves(s.rlvl_n[l], 4), 256, 0, st>>>(
+                s.rlvl[c][l - 1], s.rlvl_n[l - 1], const_cast<int64_t*>(s.rlvl[c][l]), s.rlvl_n[l], INT64_MIN);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// K0: encode requests
+// ---------------------------------------------------------------------------------------
+// rank of an arbitrary id against the dictionary: member i -> 2i+1, else 2*lower_bound
+__device__ __forceinline__ uint32_t encode_rank(const DevSnapshot& s, uint64_t msb, uint64_t lsb, int32_t node)
+{
+    const NormTid x = norm_tid(msb, lsb, node);
+    uint64_t lo = 0, hi = s.n_dict;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        const NormTid m = {s.dict_hi[mid], s.dict_lo[mid], s.dict_node[mid]};
+        if (norm_cmp(m, x) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < s.n_dict)
+    {
+        const NormTid m = {s.dict_hi[lo], s.dict_lo[lo], s.dict_node[lo]};
+        if (norm_cmp(m, x) == 0) return (uint32_t)(2 * lo + 1);
+    }
+    return (uint32_t)(2 * lo);
+}
+
+__global__ void k_encode_txn(DevSnapshot s, BatchBufs b)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n_txns) return;
+    const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t];
+    const int32_t tn = b.q_txn_node[t];
+    const uint64_t em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
+    const int32_t en = b.q_exec_node[t];
+    const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));   // txnId.kind().witnesses()
+    if (kinds == 0) set_error(b.ctl, ERR_INVAL);
+    // p1 = executeAt.equals(txnId) ? null : txnId   (PreAccept.java:261)
+    const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
+    b.t_S[t] = encode_rank(s, em, el, en);
+    b.t_self[t] = same ? 0u : encode_rank(s, tm, tl, tn);
+    b.t_kinds[t] = kinds | ((uint32_t)kinds_class(kinds) << 8);
+    b.t_epoch[t] = (int64_t)(em >> 15);
+    for (uint64_t p = b.q_key_off[t]; p < b.q_key_off[t + 1]; ++p) b.p_txn[p] = (uint32_t)t;
+}
+
+__global__ void k_probe_keys(DevSnapshot s, BatchBufs b)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= b.n_probes) return;
+    const int64_t key = b.q_keys[p];
+    bool in_slice = s.n_slices == 0;
+    for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
+        in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+    int32_t ki = -1;
+    if (in_slice)
+    {
+        uint64_t lo = 0, hi = s.n_keys;
+        while (lo < hi)
+        {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (s.keys[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < s.n_keys && s.keys[lo] == key) ki = (int32_t)lo;   // ifLoadedAndInitialised(key) != null
+    }
+    b.p_key[p] = ki;
+    b.p_slice[p] = in_slice ? 1 : 0;
+}
+
+hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+{
+    if (b.n_txns)
+        k_encode_txn<<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
+    if (b.n_probes)
+        k_probe_keys<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// K1: CommandsForKey.mapReduceActive, one wave per (request, key) probe
+// ---------------------------------------------------------------------------------------
+constexpr int K1_WAVES = 4;
+constexpr int K1_CAP = 1024;        // LDS staging per wave (u32)
+constexpr uint32_t K1_CHUNK = 4096; // arena chunk per wave refill
+
+struct ChunkAlloc {
+    uint64_t cur = 0, end = 0;
+    // wave-uniform allocation of n elements, contiguous
+    __device__ __forceinline__ uint64_t take(unsigned long long* top, unsigned long long cap, unsigned* overflow,
+                                             unsigned ovf_bit, uint64_t n, uint64_t chunk)
+    {
+        if (n > end - cur)
+        {
+            const uint64_t sz = n > chunk ? n : chunk;
+            unsigned long long base = 0;
+            if (lane_id() == 0) base = atomicAdd(top, (unsigned long long)sz);
+            base = uniform64(base);
+            if (base + sz > cap && lane_id() == 0) atomicOr(overflow, ovf_bit);
+            cur = base;
+            end = base + sz;
+        }
+        const uint64_t r = cur;
+        cur += n;
+        return r;
+    }
+};
+
+__global__ __launch_bounds__(256) void k_scan(DevSnapshot s, BatchBufs b)
+{
+    __shared__ uint32_t stage[K1_WAVES][K1_CAP];
+    __shared__ uint64_t stk[K1_WAVES][2 * MAX_LEVELS];
+    const int wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
+    const uint64_t nw = (uint64_t)gridDim.x * K1_WAVES;
+    ChunkAlloc alloc;
+    const unsigned long long cap = b.ctl->key_cap;
+
+    for (uint64_t p = (uint64_t)blockIdx.x * K1_WAVES + wv; p < b.n_probes; p += nw)
+    {
+        const int32_t ki = b.p_key[p];
+        if (ki < 0)
+        {
+            if (lane == 0) { b.p_off[p] = 0; b.p_c0[p] = 0; b.p_c1[p] = 0; }
+            continue;
+        }
+        const uint32_t t = b.p_txn[p];
+        const uint32_t S = b.t_S[t], self = b.t_self[t], tk = b.t_kinds[t];
+        const uint32_t kinds = tk & 0xFF;
+        const int cls = (tk >> 8) & 3;
+        const uint64_t lo = s.seg[ki], hi = s.seg[ki + 1];
+
+        // end = insertPos(startedBefore)  (CommandsForKey.java:912, :1358-1363)
+        const uint64_t end = wave_lower_bound(lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
+                                              [&](uint32_t v) { return v < S; });
+
+        // maxCommittedWriteBefore (:913-928): executeAt of the last committed Write before S
+        const uint64_t wlo = s.woff[ki], whi = s.woff[ki + 1];
+        uint32_t M = 1;                      // "none": every live entry passes tau >= 1
+        uint64_t wpos = wlo;
+        if (whi > wlo)
+            wpos = wave_lower_bound(wlo, whi, [&](uint64_t i) { return s.w[i].x; }, [&](uint32_t v) { return v < S; });
+        if (s.elide && wpos > wlo) M = s.w[wpos - 1].x;
+
+        // prunedBefore substitute (:952-965): first Write at/after S, clamped to maxAppliedWrite
+        uint32_t extra = 0;
+        const uint32_t pr = s.pruned[ki];
+        if (pr != 0 && S <= pr)
+        {
+            const int32_t maw = s.maw[ki];
+            if (maw < 0) { if (lane == 0) set_error(b.ctl, ERR_STATE); }
+            else
+            {
+                const uint64_t idx = wpos <= (uint64_t)maw ? wpos : (uint64_t)maw;
+                extra = s.w[idx].y;
+                if (extra == self) extra = 0;                      // map lambda, PreAccept.java:258
+            }
+        }
+
+        uint32_t cursor = 0, c0 = 0, c1 = 0, nlt = 0;
+        bool overflow = false, dup = false;
+        auto node_want = [&](int lv, uint64_t node) { return s.lvl[cls][lv][node] >= M; };
+        auto want_of = [&](uint64_t i, bool inr, uint32_t& r, bool& is1) -> bool {
+            const uint2 e = inr ? s.ent[i] : make_uint2(0u, 0u);
+            r = e.y & RANK_MASK;
+            const uint32_t kd = e.y >> RANK_BITS;
+            is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;           // !managesExecution -> directKeyDeps
+            // testKind.test(kind); status/elision via tau >= M; self exclusion (PreAccept.java:258)
+            return inr && e.x >= M && ((kinds >> kd) & 1) && r != self;
+        };
+        auto leaf_stage = [&](uint64_t base, bool inr) {
+            uint32_t r;
+            bool is1;
+            const bool want = want_of(base + lane, inr, r, is1);
+            const uint64_t wm = ballot(want), w1 = ballot(want && is1);
+            c0 += __popcll(wm & ~w1);
+            c1 += __popcll(w1);
+            if (extra)
+            {
+                nlt += __popcll(ballot(want && !is1 && r < extra));
+                dup |= ballot(want && r == extra) != 0;
+            }
+            const uint32_t n = __popcll(wm);
+            if (!overflow && cursor + n <= K1_CAP)
+            {
+                if (want) stage[wv][cursor + mbcnt(wm)] = r | (is1 ? CLASS_DIRECT_BIT : 0u);
+                cursor += n;
+            }
+            else overflow = true;
+        };
+        wave_descent(lo, end, s.n_levels, node_want, leaf_stage, stk[wv]);
+
+        wave_lds_sync();
+        const bool has_extra = extra != 0 && !dup;
+        const uint32_t tot0 = c0 + (has_extra ? 1u : 0u), tot = tot0 + c1;
+        const uint64_t off = alloc.take(&b.ctl->key_top, cap, &b.ctl->overflow, 1u, tot, K1_CHUNK);
+        const bool fits = off + tot <= cap;
+        if (fits)
+        {
+            if (!overflow)
+            {
+                uint32_t run0 = 0, run1 = 0;
+                for (uint32_t i0 = 0; i0 < cursor; i0 += 64)
+                {
+                    const uint32_t i = i0 + lane;
+                    const bool v = i < cursor;
+                    const uint32_t x = v ? stage[wv][i] : 0u;
+                    const bool is1 = v && (x & CLASS_DIRECT_BIT);
+                    const bool is0 = v && !is1;
+                    const uint32_t r = x & ~CLASS_DIRECT_BIT;
+                    const uint64_t m0 = ballot(is0), m1 = ballot(is1);
+                    if (is0) b.arena[off + run0 + mbcnt(m0) + ((has_extra && r > extra) ? 1 : 0)] = r;
+                    if (is1) b.arena[off + tot0 + run1 + mbcnt(m1)] = r;
+                    run0 += __popcll(m0);
+                    run1 += __popcll(m1);
+                }
+            }
+            else
+            {
+                // staging overflowed: replay the descent writing straight to the exact allocation
+                uint32_t run0 = 0, run1 = 0;
+                auto leaf_direct = [&](uint64_t base, bool inr) {
+                    uint32_t r;
+                    bool is1;
+                    const bool want = want_of(base + lane, inr, r, is1);
+                    const uint64_t w1 = ballot(want && is1), w0 = ballot(want && !is1);
+                    if (want && !is1) b.arena[off + run0 + mbcnt(w0) + ((has_extra && r > extra) ? 1 : 0)] = r;
+                    if (want && is1) b.arena[off + tot0 + run1 + mbcnt(w1)] = r;
+                    run0 += __popcll(w0);
+                    run1 += __popcll(w1);
+                };
+                wave_descent(lo, end, s.n_levels, node_want, leaf_direct, stk[wv]);
+            }
+            if (has_extra && lane == 0) b.arena[off + nlt] = extra;
+        }
+        if (lane == 0)
+        {
+            b.p_off[p] = (uint32_t)off;
+            b.p_c0[p] = tot0;
+            b.p_c1[p] = c1;
+        }
+    }
+}
+
+hipError_t run_scan(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+{
+    if (!b.n_probes) return hipSuccess;
+    const uint64_t blocks_needed = (b.n_probes + K1_WAVES - 1) / K1_WAVES;
+    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
+    k_scan<<<grid, 256, 0, st>>>(s, b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// K4: range commands + redundant-before, one wave per probe
+// ---------------------------------------------------------------------------------------
+constexpr int K4_WAVES = 4;
+constexpr int K4_CAP = 512;          // LDS staging per wave (u64)
+constexpr uint32_t K4_CHUNK = 2048;
+
+__global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
+{
+    __shared__ uint64_t stage[K4_WAVES][K4_CAP];
+    __shared__ uint64_t stk[K4_WAVES][2 * MAX_LEVELS];
+    const int wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
+    const uint64_t nw = (uint64_t)gridDim.x * K4_WAVES;
+    ChunkAlloc alloc;
+    const unsigned long long cap = b.ctl->rng_cap;
+    const bool incl = s.start_inclusive != 0;
+
+    for (uint64_t p = (uint64_t)blockIdx.x * K4_WAVES + wv; p < b.n_probes; p += nw)
+    {
+        const int64_t x = b.q_keys[p];
+        const uint32_t t = b.p_txn[p];
+        // RedundantBefore.collectDeps over the request's keys (not sliced), RedundantBefore.java:420-423
+        uint64_t rbv = NO_RB;
+        if (s.n_rb)
+        {
+            const uint64_t c = wave_lower_bound(0, s.n_rb, [&](uint64_t i) { return s.rb_start[i]; },
+                                                [&](int64_t v) { return incl ? v <= x : v < x; });
+            if (c > 0)
+            {
+                const uint64_t e = c - 1;
+                if (range_contains(s.start_inclusive, s.rb_start[e], s.rb_end[e], x))
+                {
+                    // Entry.outOfBounds(minEpoch, executeAt) :262-265; watermark > NONE :188
+                    const int64_t ep = b.t_epoch[t];
+                    const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
+                    const uint32_t wm = s.rb_wm[e];
+                    if (!(ep < s.rb_e0[e] || mine >= s.rb_e1[e]) && wm != 0)
+                        rbv = ((uint64_t)s.rb_rid[e] << 32) | wm;
+                }
+            }
+        }
+
+        uint32_t cnt = 0;
+        uint64_t off = 0;
+        if (b.p_slice[p] && s.n_rent)
+        {
+            const uint32_t S = b.t_S[t], self = b.t_self[t], tk = b.t_kinds[t];
+            const uint32_t kinds = tk & 0xFF;
+            const int cls = (tk >> 8) & 3;
+            // candidate commands: range start before the key (Range.compareTo, Range.java:40-100)
+            const uint64_t hi = wave_lower_bound(0, s.n_rent, [&](uint64_t i) { return s.r_start[i]; },
+                                                 [&](int64_t v) { return incl ? v <= x : v < x; });
+            auto end_ok = [&](int64_t e) { return incl ? e > x : e >= x; };
+            auto node_want = [&](int lv, uint64_t node) { return end_ok(s.rlvl[cls][lv][node]); };
+            uint32_t cursor = 0;
+            bool overflow = false;
+            auto want_of = [&](uint64_t i, bool inr, uint64_t& val) -> bool {
+                bool want = false;
+                val = 0;
+                if (inr)
+                {
+                    const uint32_t txw = s.r_txw[i];
+                    const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
+                    // STARTED_BEFORE (:906-908), testKind (:933), contains key (:948-956), self (PreAccept.java:258)
+                    want = end_ok(s.r_end[i]) && r < S && ((kinds >> kd) & 1) && r != self;
+                    val = ((uint64_t)s.r_rid[i] << 32) | r;
+                }
+                return want;
+            };
+            auto leaf_stage = [&](uint64_t base, bool inr) {
+                uint64_t v;
+                const bool want = want_of(base + lane, inr, v);
+                const uint64_t wm = ballot(want);
+                const uint32_t n = __popcll(wm);
+                if (!overflow && cursor + n <= K4_CAP)
+                {
+                    if (want) stage[wv][cursor + mbcnt(wm)] = v;
+                }
+                else overflow = true;
+                cursor += n;
+            };
+            wave_descent(0, hi, s.n_rlevels, node_want, leaf_stage, stk[wv]);
+            wave_lds_sync();
+            cnt = cursor;
+            off = alloc.take(&b.ctl->rng_top, cap, &b.ctl->overflow, 2u, cnt, K4_CHUNK);
+            if (off + cnt <= cap)
+            {
+                if (!overflow)
+                {
+                    for (uint32_t i = lane; i < cnt; i += 64) b.rarena[off + i] = stage[wv][i];
+                }
+                else
+                {
+                    uint32_t run = 0;
+                    auto leaf_direct = [&](uint64_t base, bool inr) {
+                        uint64_t v;
+                        const bool want = want_of(base + lane, inr, v);
+                        const uint64_t wm = ballot(want);
+                        if (want) b.rarena[off + run + mbcnt(wm)] = v;
+                        run += __popcll(wm);
+                    };
+                    wave_descent(0, hi, s.n_rlevels, node_want, leaf_direct, stk[wv]);
+                }
+            }
+        }
+        if (lane == 0)
+        {
+            b.p_roff[p] = (uint32_t)off;
+            b.p_rcnt[p] = cnt;
+            b.p_rb[p] = rbv;
+        }
+    }
+}
+
+hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+{
+    if (!b.n_probes) return hipSuccess;
+    const uint64_t blocks_needed = (b.n_probes + K4_WAVES - 1) / K4_WAVES;
+    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
+    k_range<<<grid, 256, 0, st>>>(s, b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// K2: per request, build keyDeps / directKeyDeps / rangeDeps in RelationMultiMap CSR form.
+//
+// Multi-list union ("rank merge"): lists L_0..L_{n-1}, each sorted and duplicate-free.
+//   kept(x in L_a)  = no L_b, b < a, contains x      (first occurrence of each distinct value)
+//   P               = exclusive prefix of kept over the concatenation
+//   urank(x)        = sum_b (P[lb_b(x)] - P[st_b])     = number of distinct values < x
+// so values[urank(x)] = x for kept x, and urank(x) is the keysToTxnIds body entry of x
+// (RelationMultiMap.java:245-257). One wave per request; lists staged in LDS, or in global
+// scratch when a request is too large for LDS.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t K2_MAXP = 64;     // probes per request on the LDS path
+constexpr uint32_t K2_CAP = 512;     // elements per list family on the LDS path
+
+struct K2Mem {
+    uint32_t* st;      // [2*np + 2] list starts
+    uint64_t* V;       // [cap] elements (u32 ranks widened, or (rid<<32 | rank) pairs)
+    uint32_t* P;       // [cap + 1]
+    uint64_t* UP;      // [cap] unique pairs
+    uint32_t* gst;     // [cap + 1] rid group starts
+    uint32_t* P2;      // [cap + 1]
+};
+
+__device__ __forceinline__ uint64_t k2_lds_bytes()
+{
+    return (uint64_t)(2 * K2_MAXP + 2) * 4 + (uint64_t)K2_CAP * 8 * 2 + (uint64_t)(K2_CAP + 1) * 4 * 3;
+}
+
+template <class Get>
+__device__ __forceinline__ uint32_t lb_in(Get get, uint32_t lo, uint32_t hi, uint64_t x)
+{
+    while (lo < hi)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (get(mid) < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// list of element e: the largest a with st[a] <= e (st ascending, st[n] = total)
+__device__ __forceinline__ uint32_t list_of(const uint32_t* st, uint32_t n, uint32_t e)
+{
+    uint32_t lo = 0, hi = n;                 // answer in [0, n)
+    while (hi - lo > 1)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (st[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void wave_excl_scan_inplace(uint32_t* P, uint32_t n)
+{
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64)
+    {
+        const uint32_t i = i0 + lane_id();
+        const uint32_t v = i < n ? P[i] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (i < n) P[i] = carry + inc - v;
+        carry += __shfl(inc, 63, 64);
+    }
+    if (lane_id() == 0) P[n] = carry;
+}
+
+// kept flags + prefix; returns number of distinct values. Get(e) = element e of the concatenation.
+template <class Get>
+__device__ __forceinline__ uint32_t rank_merge_kept(Get get, const uint32_t* st, uint32_t nl, uint32_t total, uint32_t* P)
+{
+    for (uint32_t e0 = 0; e0 < total; e0 += 64)
+    {
+        const uint32_t e = e0 + lane_id();
+        if (e < total)
+        {
+            const uint32_t a = list_of(st, nl, e);
+            const uint64_t x = get(e);
+            uint32_t kept = 1;
+            for (uint32_t bl = 0; bl < a && kept; ++bl)
+            {
+                const uint32_t s0 = st[bl], s1 = st[bl + 1];
+                if (s1 > s0)
+                {
+                    const uint32_t j = lb_in(get, s0, s1, x);
+                    if (j < s1 && get(j) == x) kept = 0;
+                }
+            }
+            P[e] = kept;
+        }
+    }
+    __syncthreads();
+    wave_excl_scan_inplace(P, total);
+    __syncthreads();
+    return uniform(P[total]);
+}
+
+// after rank_merge_kept: unique rank of element e
+template <class Get>
+__device__ __forceinline__ uint32_t rank_merge_urank(Get get, const uint32_t* st, uint32_t nl, const uint32_t* P, uint64_t x)
+{
+    uint32_t sum = 0;
+    for (uint32_t bl = 0; bl < nl; ++bl)
+    {
+        const uint32_t s0 = st[bl], s1 = st[bl + 1];
+        if (s1 > s0) sum += P[lb_in(get, s0, s1, x)] - P[s0];
+    }
+    return sum;
+}
+
+struct BuildSizes { uint32_t nk, nv, nk2t; };
+
+__device__ __forceinline__ uint32_t dict_index(uint32_t rank) { return (rank - 1) >> 1; }
+
+template <bool EMIT>
+__global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
+{
+    extern __shared__ uint64_t lds_raw[];
+    const uint32_t lane = lane_id();
+    const uint64_t n = b.n_txns;
+    for (uint64_t t = blockIdx.x; t < n; t += gridDim.x)
+    {
+        const uint64_t p0 = b.q_key_off[t];
+        const uint32_t np = (uint32_t)(b.q_key_off[t + 1] - p0);
+
+        // totals over the request's probes
+        uint32_t tot0 = 0, tot1 = 0, totR = 0;
+        for (uint32_t i = lane; i < np; i += 64)
+        {
+            tot0 += b.p_c0[p0 + i];
+            tot1 += b.p_c1[p0 + i];
+            totR += b.p_rcnt[p0 + i] + (b.p_rb[p0 + i] != NO_RB ? 1u : 0u);
+        }
+        tot0 = uniform(wave_sum(tot0));
+        tot1 = uniform(wave_sum(tot1));
+        totR = uniform(wave_sum(totR));
+        const uint32_t capn = max(max(tot0, tot1), totR);
+        const bool big = np > K2_MAXP || capn > K2_CAP;
+
+        K2Mem mem;
+        if (!big)
+        {
+            uint8_t* base = reinterpret_cast<uint8_t*>(lds_raw);
+            mem.V = reinterpret_cast<uint64_t*>(base);
+            mem.UP = mem.V + K2_CAP;
+            mem.P = reinterpret_cast<uint32_t*>(mem.UP + K2_CAP);
+            mem.gst = mem.P + (K2_CAP + 1);
+            mem.P2 = mem.gst + (K2_CAP + 1);
+            mem.st = mem.P2 + (K2_CAP + 1);
+        }
+        else
+        {
+            // scratch: st[2np+2] u32, V/UP [capn] u64, P/gst/P2 [capn+1] u32 (8-byte aligned)
+            const uint64_t bytes = ((uint64_t)(2 * np + 2) * 4 + 7) / 8 * 8 + (uint64_t)capn * 16 +
+                                   ((uint64_t)(capn + 1) * 12 + 7) / 8 * 8;
+            uint64_t so;
+            if (!EMIT)
+            {
+                unsigned long long o = 0;
+                if (lane == 0) o = atomicAdd(&b.ctl->scr_top, (unsigned long long)bytes);
+                so = uniform64(o);
+                if (so + bytes > b.ctl->scr_cap)
+                {
+                    if (lane == 0) { atomicOr(&b.ctl->overflow, 4u); b.t_scr[t] = ~0ull; }
+                    continue;
+                }
+                if (lane == 0) b.t_scr[t] = so;
+            }
+            else
+            {
+                so = b.t_scr[t];
+                if (so == ~0ull) continue;
+            }
+            uint8_t* base = b.scratch + so;
+            mem.V = reinterpret_cast<uint64_t*>(base);
+            mem.UP = mem.V + capn;
+            mem.st = reinterpret_cast<uint32_t*>(mem.UP + capn);
+            mem.P = mem.st + ((2 * np + 2 + 1) & ~1u);
+            mem.gst = mem.P + (capn + 1);
+            mem.P2 = mem.gst + (capn + 1);
+        }
+
+        // ---- keyDeps (class 0) and directKeyDeps (class 1)
+        for (int c = 0; c < 2; ++c)
+        {
+            const int m = c == 0 ? 0 : 2;          // AD_MAP_KEY / AD_MAP_DIRECT_KEY
+            // list starts
+            uint32_t carry = 0;
+            for (uint32_t i0 = 0; i0 < np; i0 += 64)
+            {
+                const uint32_t i = i0 + lane;
+                const uint32_t cnt = i < np ? (c == 0 ? b.p_c0[p0 + i] : b.p_c1[p0 + i]) : 0u;
+                const uint32_t inc = wave_incl_scan(cnt);
+                if (i < np) mem.st[i] = carry + inc - cnt;
+                carry += __shfl(inc, 63, 64);
+            }
+            const uint32_t tot = c == 0 ? tot0 : tot1;
+            if (lane == 0) mem.st[np] = tot;
+            __syncthreads();
+            // stage elements
+            for (uint32_t i = 0; i < np; ++i)
+            {
+                const uint32_t s0 = mem.st[i], len = mem.st[i + 1] - s0;
+                if (!len) continue;
+                const uint64_t src = (uint64_t)b.p_off[p0 + i] + (c == 0 ? 0u : b.p_c0[p0 + i]);
+                for (uint32_t j = lane; j < len; j += 64) mem.V[s0 + j] = b.arena[src + j];
+            }
+            __syncthreads();
+            auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
+            const uint32_t U = rank_merge_kept(get, mem.st, np, tot, mem.P);
+            // non-empty keys
+            uint32_t nk = 0;
+            for (uint32_t i0 = 0; i0 < np; i0 += 64)
+            {
+                const uint32_t i = i0 + lane;
+                const bool ne = i < np && mem.st[i + 1] > mem.st[i];
+                nk += __popcll(ballot(ne));
+            }
+            if (!EMIT)
+            {
+                if (lane == 0)
+                {
+                    b.sz[(3 * m + 0) * n + t] = nk;
+                    b.sz[(3 * m + 1) * n + t] = U;
+                    b.sz[(3 * m + 2) * n + t] = nk + tot;
+                }
+            }
+            else
+            {
+                const uint64_t ko = b.off[(3 * m + 0) * (n + 1) + t];
+                const uint64_t vo = b.off[(3 * m + 1) * (n + 1) + t];
+                const uint64_t oo = b.off[(3 * m + 2) * (n + 1) + t];
+                // keys + heads (absolute end offsets starting at nKeys)
+                uint32_t kr = 0;
+                for (uint32_t i0 = 0; i0 < np; i0 += 64)
+                {
+                    const uint32_t i = i0 + lane;
+                    const bool ne = i < np && mem.st[i + 1] > mem.st[i];
+                    const uint64_t mk = ballot(ne);
+                    if (ne)
+                    {
+                        const uint32_t k = kr + mbcnt(mk);
+                        b.o_keys[m][ko + k] = b.q_keys[p0 + i];
+                        b.o_k2t[m][oo + k] = (int32_t)(nk + mem.st[i + 1]);
+                    }
+                    kr += __popcll(mk);
+                }
+                // values + body
+                for (uint32_t e = lane; e < tot; e += 64)
+                {
+                    const uint64_t x = mem.V[e];
+                    const uint32_t ur = rank_merge_urank(get, mem.st, np, mem.P, x);
+                    if (mem.P[e + 1] - mem.P[e]) b.o_txns[m][vo + ur] = dict_index((uint32_t)x);
+                    b.o_k2t[m][oo + nk + e] = (int32_t)ur;
+                }
+            }
+            __syncthreads();
+        }
+
+        // ---- rangeDeps: lists = per probe [range-command pairs], [redundant pair]
+        {
+            const uint32_t nl = 2 * np;
+            uint32_t carry = 0;
+            for (uint32_t i0 = 0; i0 < nl; i0 += 64)
+            {
+                const uint32_t i = i0 + lane;
+                uint32_t cnt = 0;
+                if (i < nl)
+                {
+                    const uint64_t p = p0 + (i >> 1);
+                    cnt = (i & 1) ? (b.p_rb[p] != NO_RB ? 1u : 0u) : b.p_rcnt[p];
+                }
+                const uint32_t inc = wave_incl_scan(cnt);
+                if (i < nl) mem.st[i] = carry + inc - cnt;
+                carry += __shfl(inc, 63, 64);
+            }
+            if (lane == 0) mem.st[nl] = totR;
+            __syncthreads();
+            for (uint32_t i = 0; i < np; ++i)
+            {
+                const uint32_t s0 = mem.st[2 * i], len = mem.st[2 * i + 1] - s0;
+                const uint64_t src = b.p_roff[p0 + i];
+                for (uint32_t j = lane; j < len; j += 64) mem.V[s0 + j] = b.rarena[src + j];
+                if (lane == 0 && mem.st[2 * i + 2] > mem.st[2 * i + 1]) mem.V[mem.st[2 * i + 1]] = b.p_rb[p0 + i];
+            }
+            __syncthreads();
+            auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
+            const uint32_t UPn = rank_merge_kept(get, mem.st, nl, totR, mem.P);
+            // unique pairs, sorted by (rid, rank) = (Range.compare, TxnId.compareTo)
+            for (uint32_t e = lane; e < totR; e += 64)
+            {
+                if (mem.P[e + 1] - mem.P[e])
+                {
+                    const uint64_t x = mem.V[e];
+                    mem.UP[rank_merge_urank(get, mem.st, nl, mem.P, x)] = x;
+                }
+            }
+            __syncthreads();
+            // rid groups
+            uint32_t nR = 0;
+            for (uint32_t i0 = 0; i0 < UPn; i0 += 64)
+            {
+                const uint32_t i = i0 + lane;
+                const bool first = i < UPn && (i == 0 || (mem.UP[i] >> 32) != (mem.UP[i - 1] >> 32));
+                const uint64_t mk = ballot(first);
+                if (first) mem.gst[nR + mbcnt(mk)] = i;
+                nR += __popcll(mk);
+            }
+            if (lane == 0) mem.gst[nR] = UPn;
+            __syncthreads();
+            // distinct txnIds across groups: rank merge over the groups by rank
+            auto getr = [&](uint32_t e) -> uint64_t { return mem.UP[e] & 0xFFFFFFFFull; };
+            const uint32_t UR = rank_merge_kept(getr, mem.gst, nR, UPn, mem.P2);
+            if (!EMIT)
+            {
+                if (lane == 0)
+                {
+                    b.sz[(3 * 1 + 0) * n + t] = nR;
+                    b.sz[(3 * 1 + 1) * n + t] = UR;
+                    b.sz[(3 * 1 + 2) * n + t] = nR + UPn;
+                }
+            }
+            else
+            {
+                const uint64_t ko = b.off[(3 * 1 + 0) * (n + 1) + t];
+                const uint64_t vo = b.off[(3 * 1 + 1) * (n + 1) + t];
+                const uint64_t oo = b.off[(3 * 1 + 2) * (n + 1) + t];
+                for (uint32_t g = lane; g < nR; g += 64)
+                {
+                    b.o_keys[1][ko + g] = (int64_t)(mem.UP[mem.gst[g]] >> 32);
+                    b.o_k2t[1][oo + g] = (int32_t)(nR + mem.gst[g + 1]);
+                }
+                for (uint32_t e = lane; e < UPn; e += 64)
+                {
+                    const uint64_t x = getr(e);
+                    const uint32_t ur = rank_merge_urank(getr, mem.gst, nR, mem.P2, x);
+                    if (mem.P2[e + 1] - mem.P2[e]) b.o_txns[1][vo + ur] = dict_index((uint32_t)x);
+                    b.o_k2t[1][oo + nR + e] = (int32_t)ur;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, bool emit, hipStream_t st)
+{
+    if (!b.n_txns) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<uint64_t>(b.n_txns, (uint64_t)device_cu_count() * 16);
+    const size_t lds = (size_t)(2 * K2_MAXP + 2) * 4 + (size_t)K2_CAP * 8 * 2 + (size_t)(K2_CAP + 1) * 4 * 3;
+    if (emit) k_build<true><<<grid, 64, lds, st>>>(s, b);
+    else k_build<false><<<grid, 64, lds, st>>>(s, b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// exclusive scans of the 9 size arrays -> u64 offsets [9][n+1]
+// ---------------------------------------------------------------------------------------
+constexpr int SCAN_BLOCK = 1024;
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_blocks(const uint32_t* __restrict__ sz, uint64_t n,
+                                                            uint64_t* __restrict__ off, uint64_t* __restrict__ bsum,
+                                                            uint64_t nb)
+{
+    __shared__ uint64_t wsum[SCAN_BLOCK / 64];
+    const int a = blockIdx.y;
+    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    const uint64_t v = i < n ? sz[(uint64_t)a * n + i] : 0;
+    // wave inclusive scan (u64)
+    uint64_t inc = v;
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        uint64_t tt = __shfl_up(inc, d, 64);
+        if (l >= d) inc += tt;
+    }
+    const int w = threadIdx.x >> 6;
+    if (l == 63) wsum[w] = inc;
+    __syncthreads();
+    if (threadIdx.x < SCAN_BLOCK / 64)
+    {
+        uint64_t x = wsum[threadIdx.x], sacc = x;
+        for (int d = 1; d < SCAN_BLOCK / 64; d <<= 1)
+        {
+            uint64_t tt = __shfl_up(sacc, d, 64);
+            if ((int)threadIdx.x >= d) sacc += tt;
+        }
+        wsum[threadIdx.x] = sacc - x;
+    }
+    __syncthreads();
+    if (i < n) off[(uint64_t)a * (n + 1) + i] = inc - v + wsum[w];
+    if (threadIdx.x == SCAN_BLOCK - 1) bsum[(uint64_t)a * nb + blockIdx.x] = inc + wsum[w];
+}
+
+__global__ void k_scan_sums(uint64_t* bsum, uint64_t nb, uint64_t* __restrict__ off, uint64_t n)
+{
+    // one wave per array: exclusive scan of block sums, total -> off[n]
+    const int a = blockIdx.x;
+    uint64_t carry = 0;
+    for (uint64_t i0 = 0; i0 < nb; i0 += 64)
+    {
+        const uint64_t i = i0 + lane_id();
+        const uint64_t v = i < nb ? bsum[(uint64_t)a * nb + i] : 0;
+        uint64_t inc = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            uint64_t tt = __shfl_up(inc, d, 64);
+            if ((int)lane_id() >= d) inc += tt;
+        }
+        if (i < nb) bsum[(uint64_t)a * nb + i] = carry + inc - v;
+        carry += __shfl(inc, 63, 64);
+    }
+    if (lane_id() == 0) off[(uint64_t)a * (n + 1) + n] = carry;
+}
+
+__global__ void k_scan_add(const uint64_t* __restrict__ bsum, uint64_t nb, uint64_t* __restrict__ off, uint64_t n)
+{
+    const int a = blockIdx.y;
+    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    if (i < n) off[(uint64_t)a * (n + 1) + i] += bsum[(uint64_t)a * nb + blockIdx.x];
+}
+
+hipError_t run_offsets(const BatchBufs& b, hipStream_t st)
+{
+    const uint64_t n = b.n_txns;
+    const uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    uint64_t* bsum = b.bsum;
+    if (n == 0)
+    {
+        return hipMemsetAsync(b.off, 0, sizeof(uint64_t) * 9, st);
+    }
+    dim3 g((unsigned)nb, 9);
+    k_scan_blocks<<<g, SCAN_BLOCK, 0, st>>>(b.sz, n, b.off, bsum, nb);
+    k_scan_sums<<<9, 64, 0, st>>>(bsum, nb, b.off, n);
+    k_scan_add<<<g, SCAN_BLOCK, 0, st>>>(bsum, nb, b.off, n);
+    return hipGetLastError();
+}
+
+int device_cu_count()
+{
+    static int cus = 0;
+    if (!cus)
+    {
+        int dev = 0;
+        hipGetDevice(&dev);
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+        if (cus <= 0) cus = 256;
+    }
+    return cus;
+}
+
+}  // namespace adx

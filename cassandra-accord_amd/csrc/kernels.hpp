@@ -1,0 +1,60 @@
+// kernels.hpp — host-side launch interface of the gfx950 kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace adx {
+
+// Device-side control block of one batch: arena bump pointers, overflow and error flags.
+struct BatchCtl {
+    unsigned long long key_top, key_cap;      // K1 arena (u32 elements)
+    unsigned long long rng_top, rng_cap;      // K4 arena (u64 elements)
+    unsigned long long scr_top, scr_cap;      // K2 big-txn scratch (bytes)
+    unsigned int overflow;                    // bit0 key arena, bit1 range arena, bit2 scratch
+    unsigned int error;                       // AD_E_* (negated) of the first failure, 0 = none
+};
+
+constexpr uint64_t NO_RB = ~0ull;
+constexpr unsigned ERR_INVAL = 1u;   // BatchCtl.error codes
+constexpr unsigned ERR_STATE = 8u;
+
+// Per-batch device buffers (sized by the host before the launches).
+struct BatchBufs {
+    // queries (device pointers; q_* borrowed from the caller or staged by ad_deps_batch)
+    uint64_t n_txns, n_probes;
+    const uint64_t* q_txn_msb; const uint64_t* q_txn_lsb; const int32_t* q_txn_node;
+    const uint64_t* q_exec_msb; const uint64_t* q_exec_lsb; const int32_t* q_exec_node;
+    const int64_t* q_min_epoch;      // may be null
+    const uint64_t* q_key_off;
+    const int64_t* q_keys;
+    // K0
+    uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
+    uint32_t* p_txn; int32_t* p_key; uint8_t* p_slice;
+    // K1
+    uint32_t* arena; uint32_t* p_off; uint32_t* p_c0; uint32_t* p_c1;
+    // K4
+    uint64_t* rarena; uint32_t* p_roff; uint32_t* p_rcnt; uint64_t* p_rb;
+    // K2
+    uint32_t* sz;                    // [9][n_txns]: per map m: keys, txns, k2t
+    uint64_t* off;                   // [9][n_txns+1]
+    uint64_t* bsum;                  // [9][ceil(n_txns/1024)] scan block sums
+    uint64_t* t_scr;                 // [n_txns] big-txn scratch offset (bytes), ~0 = LDS path
+    uint8_t* scratch;
+    int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
+    BatchCtl* ctl;
+};
+
+hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
+hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);
+
+hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_scan(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, bool emit, hipStream_t st);
+hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
+
+int device_cu_count();
+
+}  // namespace adx

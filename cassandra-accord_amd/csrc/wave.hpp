@@ -1,0 +1,141 @@
+// wave.hpp — wave64 building blocks for gfx950 (CDNA4): ballot/mbcnt compaction, 64-ary
+// searches and the max-tree range-threshold descent used by the conflict scan (K1) and the
+// range probe (K4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace adx {
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+// number of set bits of m below this lane
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// compiler-level ordering of LDS/global accesses between lanes of one wave (the hardware keeps
+// one wave's LDS operations in order; this stops the compiler from reordering across it)
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v)
+{
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// inclusive wave prefix sum
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (l >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// lower_bound over a sorted sequence key(i), i in [lo, hi): the first i with !(key(i) < x),
+// or hi. 64-ary: each round every lane loads one pivot (64 independent loads, one round trip).
+template <class KeyAt, class Less>
+__device__ __forceinline__ uint64_t wave_lower_bound(uint64_t lo, uint64_t hi, KeyAt key, Less less)
+{
+    const uint32_t l = lane_id();
+    while (hi - lo > 64)
+    {
+        const uint64_t n = hi - lo;
+        const uint64_t p = lo + (((uint64_t)(l + 1) * n) >> 6) - 1;     // p_63 = hi - 1
+        const uint64_t m = ballot(less(key(p)));
+        const uint32_t c = __popcll(m);
+        if (c == 64) return hi;
+        const uint64_t pc = lo + (((uint64_t)(c + 1) * n) >> 6) - 1;
+        const uint64_t nlo = c == 0 ? lo : lo + (((uint64_t)c * n) >> 6);   // p_{c-1} + 1
+        lo = nlo;
+        hi = pc;                       // key(pc) >= x: the answer is in [nlo, pc]
+    }
+    const uint64_t i = lo + l;
+    const bool v = i < hi && less(key(i));
+    return lo + __popcll(ballot(v));
+}
+
+// Max-tree range-threshold descent.
+//   Report, in ascending index order, every leaf i in [lo, end) for which leaf_want(i) holds,
+//   pruning with a 64-ary tree whose level-l node j summarises leaves [j*64^l, (j+1)*64^l):
+//   node_want(l, j) must be true whenever any leaf below j may be wanted.
+//   `leaf(base, want_lane)` is called for every level-0 frame (64 consecutive leaves from
+//   base) with the lane's own want bit; it runs the emission.
+// Stack of (base, pending-children mask) per level lives in wave-private LDS `stk`; every lane
+// writes the same (wave-uniform) value and reads back its own write, so no cross-lane sync.
+template <class NodeWant, class LeafFrame>
+__device__ __forceinline__ void wave_descent(uint64_t lo, uint64_t end, int n_levels, NodeWant node_want,
+                                             LeafFrame leaf, uint64_t* stk /* [2*MAX_LEVELS] */)
+{
+    if (end <= lo) return;
+    const uint32_t l = lane_id();
+    int k = 0;
+    while (k + 1 < n_levels && (((end - 1) >> (6 * k)) - (lo >> (6 * k))) >= 64) ++k;
+
+    auto frame = [&](int lv, uint64_t base) -> uint64_t {
+        const uint64_t node = base + l;
+        const bool inr = node >= (lo >> (6 * lv)) && node <= ((end - 1) >> (6 * lv));
+        if (lv == 0)
+        {
+            leaf(base, inr);
+            return 0;
+        }
+        return ballot(inr && node_want(lv, node));
+    };
+
+    uint64_t m = frame(k, lo >> (6 * k));
+    if (k == 0) return;
+    int lv = k;
+    stk[2 * lv] = lo >> (6 * k);
+    stk[2 * lv + 1] = m;
+    uint64_t base = lo >> (6 * k);
+    while (true)
+    {
+        if (m == 0)
+        {
+            if (++lv > k) break;
+            base = stk[2 * lv];
+            m = stk[2 * lv + 1];
+            continue;
+        }
+        const int b = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        const uint64_t cbase = (base + b) << 6;
+        if (lv == 1)
+        {
+            frame(0, cbase);           // leaves: emitted inline, nothing to push
+            continue;
+        }
+        stk[2 * lv] = base;
+        stk[2 * lv + 1] = m;
+        lv -= 1;
+        base = cbase;
+        m = frame(lv, cbase);
+    }
+}
+
+}  // namespace adx

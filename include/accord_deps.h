@@ -1,0 +1,260 @@
+/*
+ * accord_deps.h — C ABI of the MI355X-native batched dependency-resolution engine
+ * for Accord's PreAccept/Accept path (libaccord_deps.so).
+ *
+ * The library replaces, for one CommandStore (one GPU = one token-range slice):
+ *
+ *   SafeCommandStore.mapReduceActive(keys, slice, startedBefore, kinds, map, p1, acc)
+ *       accord-core/src/main/java/accord/local/SafeCommandStore.java:292
+ *     as implemented by InMemorySafeStore.mapReduceActive
+ *       accord-core/src/main/java/accord/impl/InMemoryCommandStore.java:863-871
+ *     -> CommandsForKey.mapReduceActive   (local/cfk/CommandsForKey.java:910-968)
+ *     -> mapReduceRangesInternal           (impl/InMemoryCommandStore.java:884-1017)
+ *   composed by PreAccept.calculatePartialDeps (messages/PreAccept.java:245-267)
+ *     (also reached from Accept.calculatePartialDeps, messages/Accept.java:113-117)
+ *     -> Deps.AbstractBuilder.add         (primitives/Deps.java:80-106)
+ *     -> RelationMultiMap.AbstractBuilder (utils/RelationMultiMap.java:88-260)
+ *     -> RedundantBefore.collectDeps      (local/RedundantBefore.java:183-192,420-423)
+ *     -> PartialDeps.with / linearUnion   (primitives/PartialDeps.java:73-81,
+ *                                          utils/RelationMultiMap.java:561-816)
+ *
+ * Instead of one callback per (key, txnId), a whole batch of calculatePartialDeps
+ * requests is resolved per call, and the results come back already in the CSR form
+ * that KeyDeps.SerializerSupport.create(Keys, TxnId[], int[]) (primitives/KeyDeps.java:69-72)
+ * and RangeDeps.SerializerSupport.create(Range[], TxnId[], int[]) (primitives/RangeDeps.java:100-103)
+ * wrap without a rebuild.
+ *
+ * Conventions
+ *  - TxnId / Timestamp travel as structure-of-arrays {msb u64, lsb u64, node i32}, the exact
+ *    fields of accord.primitives.Timestamp (Timestamp.java:77-79) and Node.Id.id (Node.java:104-137).
+ *    Order is Timestamp.compareTo (Timestamp.java:208-217); identity is Timestamp.equals
+ *    (Timestamp.java:244-249, mask 0xFFFFFFFFFFFF001E). Two ids equal under that identity
+ *    must be bit-identical (checked; AD_E_INCONSISTENT_ID).
+ *  - Keys and range bounds travel as order-preserving int64 ordinals (Key.compareTo ==
+ *    signed int64 compare). Ranges are EndInclusive (s,e] unless ad_config.range_start_inclusive.
+ *  - Inputs are caller-owned and only read during the call. Results are library-owned
+ *    until ad_result_free (host variant) or the next batch call (device variant).
+ *  - One ad_ctx per CommandStore / per GPU; a ctx is not thread-safe (the reference's
+ *    SafeCommandStore is single-threaded, SafeCommandStore.java:52-57).
+ *  - Every entry point returns AD_OK (0) or a negative AD_E_* code; ad_last_error(ctx)
+ *    gives the message (the Java wrapper maps it to IllegalStateException).
+ */
+#ifndef ACCORD_DEPS_H
+#define ACCORD_DEPS_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AD_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------- */
+#define AD_OK                  0
+#define AD_E_INVAL            -1  /* malformed input (unsorted keys, bad kind, ...)        */
+#define AD_E_NOMEM            -2  /* host or device allocation failed                      */
+#define AD_E_DEVICE           -3  /* HIP runtime error                                      */
+#define AD_E_ORDER            -4  /* byId not strictly increasing (CommandsForKey.java:1438)*/
+#define AD_E_DUP_EXEC         -5  /* duplicate executeAt among committed (CommandsForKey.java:1439) */
+#define AD_E_INCONSISTENT_ID  -6  /* equal ids with different bits                          */
+#define AD_E_NOT_LOADED       -7  /* batch before ad_cfk_load                               */
+#define AD_E_STATE            -8  /* reference would throw (e.g. prunedBefore walk off end) */
+#define AD_E_CAPACITY         -9  /* id dictionary exceeds 2^28 entries                     */
+
+/* ---- InternalStatus ordinals (CommandsForKey.java:493-501) -------------------------- */
+#define AD_ST_TRANSITIVELY_KNOWN                          0
+#define AD_ST_HISTORICAL                                  1
+#define AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE          2
+#define AD_ST_ACCEPTED                                    3
+#define AD_ST_COMMITTED                                   4
+#define AD_ST_STABLE                                      5
+#define AD_ST_APPLIED                                     6
+#define AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED 7
+
+/* ---- Txn.Kind ordinals (Txn.java:53-112); kind = (lsb >> 1) & 7, domain = lsb & 1 --- */
+#define AD_KIND_READ                 0
+#define AD_KIND_WRITE                1
+#define AD_KIND_EPHEMERAL_READ       2
+#define AD_KIND_SYNC_POINT           3
+#define AD_KIND_EXCLUSIVE_SYNC_POINT 4
+#define AD_KIND_LOCAL_ONLY           5
+
+/* ---- result maps (Deps.java:59-119: keyDeps, rangeDeps, directKeyDeps) --------------- */
+#define AD_MAP_KEY        0
+#define AD_MAP_RANGE      1
+#define AD_MAP_DIRECT_KEY 2
+#define AD_NMAPS          3
+
+/* ---- batch flags ------------------------------------------------------------------- */
+/* SNAPSHOT: every request reads the same immutable snapshot (GetDeps / non-participating
+ *           Accept, Accept.java:87-94).
+ * SEQUENTIAL: requests are applied in the given order; before request i's deps are computed
+ *           its txnId is inserted into each of its keys' CommandsForKey as
+ *           PREACCEPTED_OR_ACCEPTED_INVALIDATE (PreAccept.apply: Commands.preaccept precedes
+ *           calculatePartialDeps, PreAccept.java:116-132; CommandsForKey.update :972-1042).
+ *           The inserted entries stay in the ctx snapshot afterwards, as they do in the CFK. */
+#define AD_SNAPSHOT   0u
+#define AD_SEQUENTIAL 1u
+
+typedef struct ad_config {
+    int32_t device;                 /* HIP device ordinal                                   */
+    int32_t range_start_inclusive;  /* 0: Range.EndInclusive (s,e]; 1: StartInclusive [s,e) */
+    int32_t elide;                  /* CommandsForKey.ELIDE_TRANSITIVE_DEPENDENCIES (:173), 1 */
+    int32_t reserved;
+    /* the store's owned ranges (SafeCommandStore.ranges(); slice in mapReduceForKey,
+     * InMemoryCommandStore.java:280). n_slices == 0 means "owns every key". */
+    uint64_t n_slices;
+    const int64_t* slice_start;
+    const int64_t* slice_end;
+} ad_config;
+
+/* CommandsForKey snapshots of the store, in the shape of
+ * CommandsForKey.SerializerSupport.create(Key, TxnInfo[] byId, Unmanaged[], TxnId prunedBefore)
+ * (CommandsForKey.java:226-232). Entries of key k are [seg[k], seg[k+1]) in byId order. */
+typedef struct ad_cfk_soa {
+    uint64_t n_keys;
+    const int64_t*  keys;            /* [n_keys] strictly ascending                         */
+    const uint64_t* seg;             /* [n_keys+1]                                          */
+    uint64_t n_entries;
+    const uint64_t* txn_msb;         /* TxnInfo (a TxnId)                                   */
+    const uint64_t* txn_lsb;
+    const int32_t*  txn_node;
+    const uint64_t* exec_msb;        /* TxnInfo.executeAt (== txnId unless hasExecuteAt)    */
+    const uint64_t* exec_lsb;
+    const int32_t*  exec_node;
+    const uint8_t*  status;          /* AD_ST_*                                             */
+    const int64_t*  pruned_before;   /* [n_keys] index within the key's byId of prunedBefore, -1 = NONE; NULL = none */
+} ad_cfk_soa;
+
+/* Range-domain commands registered with the store (InMemoryCommandStore.rangeCommands and
+ * historicalRangeCommands, :103-104,740-763,797-830); their ranges are already sliced to
+ * the store as in InMemoryCommandStore.java:758-761. */
+typedef struct ad_range_cmds_soa {
+    uint64_t n_cmds;
+    const uint64_t* txn_msb;
+    const uint64_t* txn_lsb;
+    const int32_t*  txn_node;
+    const uint8_t*  erased;          /* 1: saveStatus >= Erased (skipped, :897); NULL = none  */
+    const uint8_t*  historical;      /* 1: historicalRangeCommands entry; NULL = none        */
+    const uint64_t* range_off;       /* [n_cmds+1]                                          */
+    const int64_t*  range_start;
+    const int64_t*  range_end;
+} ad_range_cmds_soa;
+
+/* RedundantBefore entries (RedundantBefore.java:59-120); disjoint ranges. */
+typedef struct ad_redundant_soa {
+    uint64_t n;
+    const int64_t*  range_start;
+    const int64_t*  range_end;
+    const int64_t*  start_epoch;     /* inclusive */
+    const int64_t*  end_epoch;       /* exclusive */
+    const uint64_t* wm_msb;          /* shardAppliedOrInvalidatedBefore */
+    const uint64_t* wm_lsb;
+    const int32_t*  wm_node;
+} ad_redundant_soa;
+
+/* A batch of calculatePartialDeps(safeStore, txnId, keys, ..., minEpoch, executeAt, ranges)
+ * requests (PreAccept.java:245). Keys of request i: keys[key_off[i] .. key_off[i+1]),
+ * strictly ascending (accord.primitives.Keys). */
+typedef struct ad_query_soa {
+    uint64_t n_txns;
+    const uint64_t* txn_msb;
+    const uint64_t* txn_lsb;
+    const int32_t*  txn_node;
+    const uint64_t* exec_msb;        /* executeAt: == txnId for PreAccept, proposed for Accept */
+    const uint64_t* exec_lsb;
+    const int32_t*  exec_node;
+    const int64_t*  min_epoch;       /* minUnsyncedEpoch (RedundantBefore bounds); NULL = 0  */
+    const uint64_t* key_off;         /* [n_txns+1] */
+    const int64_t*  keys;
+} ad_query_soa;
+
+typedef struct ad_stats {
+    uint64_t n_txns, n_probes;
+    uint64_t n_pairs[AD_NMAPS];      /* txn-key (or txn-range) pairs emitted per map         */
+    uint64_t n_unique[AD_NMAPS];     /* sum over txns of unique txnIds per map               */
+    uint64_t scan_entries;           /* CFK entries a reference scan would visit (sum of end) */
+    double   ms_device;              /* device time of the resolve pipeline                  */
+    double   ms_ingest;
+    /* per-stage device time (HIP events): 0 encode (K0), 1 conflict scan (K1), 2 range probe
+     * (K4), 3 build sizing (K2 pass 1), 4 offsets scan, 5 build emit (K2 pass 2) */
+    double   ms_stage[8];
+    uint64_t bytes_stage[8];         /* algorithmic bytes per stage            */
+} ad_stats;
+
+/* Results, one CSR triple per map and request, packed in request order.
+ * For request i and map m:
+ *   keys      [keys_off[m][i]  .. keys_off[m][i+1])   key ordinals (m = KEY/DIRECT_KEY) or
+ *                                                       range ids into ad_range_table (m = RANGE)
+ *   txnIds    [txn_off[m][i]   .. txn_off[m][i+1])    indices into ad_dict (ascending == sorted TxnIds)
+ *   k2t       [k2t_off[m][i]   .. k2t_off[m][i+1])    the exact int[] keysToTxnIds of
+ *             RelationMultiMap (RelationMultiMap.java:245-257): nKeys absolute end offsets
+ *             starting at nKeys, then the value indices of each key in ascending order. */
+typedef struct ad_deps_result {
+    uint64_t  n_txns;
+    uint64_t* keys_off[AD_NMAPS];
+    int64_t*  keys[AD_NMAPS];
+    uint64_t* txn_off[AD_NMAPS];
+    uint32_t* txns[AD_NMAPS];
+    uint64_t* k2t_off[AD_NMAPS];
+    int32_t*  k2t[AD_NMAPS];
+    ad_stats  stats;
+} ad_deps_result;
+
+typedef struct ad_ctx ad_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------------------- */
+int  ad_abi_version(void);
+int  ad_ctx_create(const ad_config* cfg, ad_ctx** out);
+void ad_ctx_destroy(ad_ctx* ctx);
+const char* ad_last_error(const ad_ctx* ctx);
+
+/* ---- snapshot upload (ingest; builds the id dictionary, ranks and device indexes) ---- */
+int ad_cfk_load(ad_ctx* ctx, const ad_cfk_soa* cfk);
+int ad_range_cmds_load(ad_ctx* ctx, const ad_range_cmds_soa* cmds);
+int ad_redundant_load(ad_ctx* ctx, const ad_redundant_soa* rb);
+
+/* ---- batch resolve, host buffers in / host result out ------------------------------ */
+int  ad_deps_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t flags, ad_deps_result** out);
+void ad_result_free(ad_deps_result* r);
+
+/* ---- batch resolve, device-resident (HBM) buffers in and out ----------------------- *
+ * q's arrays are device pointers. *out receives device pointers owned by ctx, valid until
+ * the next batch call on ctx; out->stats is filled after the call returns. All work is
+ * enqueued on `stream` (a hipStream_t; NULL = the ctx stream) and completes before return.
+ * Only AD_SNAPSHOT is supported here. */
+int ad_deps_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t flags, void* stream,
+                         ad_deps_result* out);
+
+/* ---- id dictionary / range table views (host copies owned by ctx) ------------------- */
+int ad_dict(const ad_ctx* ctx, uint64_t* n, const uint64_t** msb, const uint64_t** lsb,
+            const int32_t** node);
+int ad_range_table(const ad_ctx* ctx, uint64_t* n, const int64_t** start, const int64_t** end);
+
+/* ---- execution ordering (config 5): topological apply levels -------------------------
+ * Txn i: executeAt (msb/lsb/node), kind, keys [key_off[i],key_off[i+1]) and direct deps
+ * [dep_off[i], dep_off[i+1]) (indices of txns it waits on regardless of key).
+ * level[i] = 0 if T_i waits on nothing, else 1 + max level of what it waits on, where on
+ * each shared key T waits for every earlier (by executeAt) committed txn its kind witnesses
+ * (Txn.Kind.witnesses, Txn.java:221-235; CommandsForKey.notifyManaged :1193-1274;
+ * Commands.updateWaitingOn :700-775). */
+typedef struct ad_graph_soa {
+    uint64_t n_txns;
+    const uint64_t* exec_msb;
+    const uint64_t* exec_lsb;
+    const int32_t*  exec_node;
+    const uint8_t*  kind;
+    const uint64_t* key_off;
+    const int64_t*  keys;
+    const uint64_t* dep_off;         /* NULL = no direct deps */
+    const uint32_t* deps;
+} ad_graph_soa;
+
+int ad_levels(ad_ctx* ctx, const ad_graph_soa* g, uint32_t* level_out, ad_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACCORD_DEPS_H */

@@ -1,0 +1,1085 @@
+/*
+ * refcpu.c — scalar CPU restatement of the reference dependency calculation.
+ *
+ * TEST INFRASTRUCTURE ONLY (parity oracle + CPU baseline). Only tests/, the smoke() of
+ * __graft_entry__.py and bench.py's cpu_baseline leg may load it. The product library
+ * (cassandra-accord_amd/csrc) never links or calls it.
+ *
+ * Every function follows the cited Java line by line (paths relative to
+ * accord-core/src/main/java/accord/). Deliberately unoptimised: per probe it scans
+ * byId[0, end) exactly as CommandsForKey.mapReduceActive does.
+ *
+ * Parity pinning: see refcpu.h (PreAcceptTest KATs + ported model-based tests; the Java
+ * cannot be executed in this image, so there are no executed-reference vectors).
+ */
+#include "refcpu.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdarg.h>
+
+/* ------------------------------------------------------------------------------------ */
+/* Timestamp / TxnId                                                                    */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { uint64_t msb, lsb; int32_t node; } tid_t;
+
+static const uint64_t IDENTITY_LSB = 0xFFFFFFFFFFFF001EULL;  /* Timestamp.java:41 */
+static const uint64_t IDENTITY_FLAGS = 0x001EULL;            /* Timestamp.java:42 */
+
+/* Timestamp.compareTo, Timestamp.java:208-217 */
+static int tid_cmp(const tid_t* a, const tid_t* b)
+{
+    if (a->msb != b->msb) return a->msb < b->msb ? -1 : 1;              /* Long.compareUnsigned */
+    uint64_t ah = a->lsb >> 16, bh = b->lsb >> 16;                      /* lowHlc :363-366 */
+    if (ah != bh) return ah < bh ? -1 : 1;
+    uint64_t af = a->lsb & IDENTITY_FLAGS, bf = b->lsb & IDENTITY_FLAGS;
+    if (af != bf) return af < bf ? -1 : 1;
+    if (a->node != b->node) return a->node < b->node ? -1 : 1;          /* Node.Id.compareTo */
+    return 0;
+}
+
+/* Timestamp.equals, Timestamp.java:244-249 */
+static int tid_eq(const tid_t* a, const tid_t* b)
+{
+    return a->msb == b->msb && ((a->lsb ^ b->lsb) & IDENTITY_LSB) == 0 && a->node == b->node;
+}
+
+int rc_tid_cmp(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode)
+{
+    tid_t a = {amsb, alsb, anode}, b = {bmsb, blsb, bnode};
+    return tid_cmp(&a, &b);
+}
+
+static int tid_kind(const tid_t* t) { return (int)((t->lsb >> 1) & 7); }   /* TxnId.java:139-152 */
+static int tid_domain(const tid_t* t) { return (int)(t->lsb & 1); }        /* TxnId.java:154-157 */
+static int64_t tid_epoch(const tid_t* t) { return (int64_t)(t->msb >> 15); } /* Timestamp.java:343 */
+
+/* Txn.Kind.Kinds as bitmasks over Kind ordinals (Txn.java:114-152) */
+#define KINDS_WS       (1u << AD_KIND_WRITE)
+#define KINDS_RS_OR_WS ((1u << AD_KIND_READ) | (1u << AD_KIND_WRITE))
+#define KINDS_ANY_GLOBALLY_VISIBLE ((1u << AD_KIND_READ) | (1u << AD_KIND_WRITE) | (1u << AD_KIND_SYNC_POINT) | (1u << AD_KIND_EXCLUSIVE_SYNC_POINT))
+
+/* Txn.Kind.witnesses(), Txn.java:221-235; returns 0 on AssertionError/invalid ordinal */
+static unsigned kind_witnesses(int kind)
+{
+    switch (kind)
+    {
+        case AD_KIND_EPHEMERAL_READ:
+        case AD_KIND_READ: return KINDS_WS;
+        case AD_KIND_WRITE:
+        case AD_KIND_SYNC_POINT: return KINDS_RS_OR_WS;
+        case AD_KIND_EXCLUSIVE_SYNC_POINT: return KINDS_ANY_GLOBALLY_VISIBLE;
+        default: return 0;
+    }
+}
+static int kinds_test(unsigned kinds, int kind) { return (kinds >> kind) & 1; }
+
+/* CommandsForKey.managesExecution, CommandsForKey.java:196-199: Write.witnesses(kind) && key domain */
+static int manages_execution(const tid_t* t) { return kinds_test(KINDS_RS_OR_WS, tid_kind(t)) && tid_domain(t) == 0; }
+/* CommandsForKey.manages, :185-188: key domain && kind.isGloballyVisible() */
+static int manages(const tid_t* t) { return tid_domain(t) == 0 && kinds_test(KINDS_ANY_GLOBALLY_VISIBLE, tid_kind(t)); }
+
+/* ------------------------------------------------------------------------------------ */
+/* small dynamic arrays                                                                 */
+/* ------------------------------------------------------------------------------------ */
+#define VEC(T) struct { T* v; size_t n, cap; }
+#define VEC_PUSH(vec, x) do { if ((vec).n == (vec).cap) { (vec).cap = (vec).cap ? (vec).cap * 2 : 16; \
+    (vec).v = realloc((vec).v, (vec).cap * sizeof(*(vec).v)); } (vec).v[(vec).n++] = (x); } while (0)
+#define VEC_FREE(vec) do { free((vec).v); (vec).v = NULL; (vec).n = (vec).cap = 0; } while (0)
+
+/* ------------------------------------------------------------------------------------ */
+/* CommandsForKey                                                                       */
+/* ------------------------------------------------------------------------------------ */
+/* TxnInfo, CommandsForKey.java:237-378: a TxnId + InternalStatus + executeAt */
+typedef struct { tid_t txnId; uint8_t status; tid_t executeAt; } info_t;
+
+typedef struct {
+    int64_t key;
+    VEC(info_t) byId;                 /* sorted by TxnId (:621) */
+    int* cbe;                         /* committedByExecuteAt, indices into byId (:624) */
+    int ncbe;
+    int maxAppliedWriteByExecuteAt;   /* :626 */
+    int hasPrunedBefore;
+    tid_t prunedBefore;               /* :615 (NO_INFO when !hasPrunedBefore) */
+} cfk_t;
+
+static const info_t* cbe_at(const cfk_t* c, int i) { return &c->byId.v[c->cbe[i]]; }
+
+static const cfk_t* g_sort_cfk;   /* qsort context for committedByExecuteAt */
+static int cmp_cbe(const void* a, const void* b)
+{
+    const info_t* x = &g_sort_cfk->byId.v[*(const int*)a];
+    const info_t* y = &g_sort_cfk->byId.v[*(const int*)b];
+    return tid_cmp(&x->executeAt, &y->executeAt);                      /* TxnInfo::compareExecuteAt */
+}
+
+/* CommandsForKey(key, redundantBefore, prunedBefore, loadingPruned, byId, unmanageds),
+ * CommandsForKey.java:642-681: derive committedByExecuteAt and maxAppliedWriteByExecuteAt. */
+static void cfk_derive(cfk_t* c)
+{
+    free(c->cbe);
+    int countCommitted = 0;
+    for (size_t i = 0; i < c->byId.n; ++i)
+    {
+        const info_t* txn = &c->byId.v[i];
+        if (txn->status == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED) continue;
+        if (txn->status >= AD_ST_COMMITTED) ++countCommitted;
+    }
+    c->cbe = malloc(sizeof(int) * (countCommitted ? countCommitted : 1));
+    c->ncbe = 0;
+    for (size_t i = 0; i < c->byId.n; ++i)
+    {
+        const info_t* txn = &c->byId.v[i];
+        if (txn->status >= AD_ST_COMMITTED && txn->status != AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED)
+            c->cbe[c->ncbe++] = (int)i;
+    }
+    g_sort_cfk = c;
+    qsort(c->cbe, c->ncbe, sizeof(int), cmp_cbe);                      /* Arrays.sort(..., compareExecuteAt) */
+    int maxAppliedByExecuteAt = c->ncbe;
+    while (--maxAppliedByExecuteAt >= 0)
+    {
+        const info_t* txn = cbe_at(c, maxAppliedByExecuteAt);
+        if (txn->status == AD_ST_APPLIED && tid_kind(&txn->txnId) == AD_KIND_WRITE)
+            break;
+    }
+    c->maxAppliedWriteByExecuteAt = maxAppliedByExecuteAt;
+}
+
+/* CommandsForKey.insertPos, :1358-1363 (Arrays.binarySearch over byId) */
+static int cfk_insert_pos(const cfk_t* c, const tid_t* ts)
+{
+    int from = 0, to = (int)c->byId.n;
+    while (from < to)
+    {
+        int mid = (from + to) >> 1;
+        int cmp = tid_cmp(&c->byId.v[mid].txnId, ts);
+        if (cmp < 0) from = mid + 1;
+        else if (cmp > 0) to = mid;
+        else return mid;
+    }
+    return from;
+}
+
+/* SortedArrays.binarySearch(in, from, to, find, (f, v) -> f.compareTo(v.executeAt), FAST),
+ * SortedArrays.java:1045-1079, over committedByExecuteAt */
+static int cbe_binary_search(const cfk_t* c, int from, int to, const tid_t* find)
+{
+    int found = -1;
+    while (from < to)
+    {
+        int i = (int)(((unsigned)from + (unsigned)to) >> 1);
+        int cc = tid_cmp(find, &cbe_at(c, i)->executeAt);
+        if (cc < 0) to = i;
+        else if (cc > 0) from = i + 1;
+        else return i;                                                  /* FAST */
+    }
+    return found >= 0 ? found : -1 - to;
+}
+
+typedef struct store_s rc_store_t;
+typedef int (*cmd_fn)(void* acc, int is_range, int64_t k0, int64_t k1, const tid_t* txnId, const tid_t* p1);
+
+/* CommandsForKey.mapReduceActive, CommandsForKey.java:910-968 */
+static int cfk_map_reduce_active(const cfk_t* c, const tid_t* startedBefore, unsigned testKind, int elide,
+                                 cmd_fn map, const tid_t* p1, void* acc, uint64_t* scan_entries)
+{
+    int end = cfk_insert_pos(c, startedBefore);
+    if (scan_entries) *scan_entries += (uint64_t)end;
+    const tid_t* maxCommittedWriteBefore;
+    {
+        int from = 0, to = c->ncbe;
+        if (c->maxAppliedWriteByExecuteAt >= 0)
+        {
+            if (tid_cmp(&cbe_at(c, c->maxAppliedWriteByExecuteAt)->executeAt, startedBefore) <= 0) from = c->maxAppliedWriteByExecuteAt;
+            else to = c->maxAppliedWriteByExecuteAt;
+        }
+        int i = cbe_binary_search(c, from, to, startedBefore);
+        if (i < 0) i = -2 - i;
+        else --i;
+        while (i >= 0 && tid_kind(&cbe_at(c, i)->txnId) != AD_KIND_WRITE) --i;
+        maxCommittedWriteBefore = i < 0 ? NULL : &cbe_at(c, i)->executeAt;
+    }
+
+    for (int i = 0; i < end; ++i)
+    {
+        const info_t* txn = &c->byId.v[i];
+        if (!kinds_test(testKind, tid_kind(&txn->txnId)))
+            continue;
+
+        switch (txn->status)
+        {
+            case AD_ST_COMMITTED:
+            case AD_ST_STABLE:
+            case AD_ST_APPLIED:
+                if (!elide || maxCommittedWriteBefore == NULL || tid_cmp(&txn->executeAt, maxCommittedWriteBefore) >= 0
+                    || !kinds_test(KINDS_RS_OR_WS, tid_kind(&txn->txnId)))
+                    break;
+                /* fall through */
+            case AD_ST_TRANSITIVELY_KNOWN:
+            case AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED:
+                continue;
+            default:
+                break;
+        }
+
+        int rc = map(acc, 0, c->key, 0, &txn->txnId, p1);               /* txn.plainTxnId() */
+        if (rc) return rc;
+    }
+
+    if (c->hasPrunedBefore && tid_cmp(startedBefore, &c->prunedBefore) <= 0)
+    {
+        int i = cbe_binary_search(c, 0, c->maxAppliedWriteByExecuteAt, startedBefore);
+        if (i < 0) i = -1 - i;
+        while (1)
+        {
+            if (i >= c->ncbe) return AD_E_STATE;                       /* ArrayIndexOutOfBounds */
+            if (tid_kind(&cbe_at(c, i)->txnId) == AD_KIND_WRITE) break;
+            ++i;
+        }
+        int rc = map(acc, 0, c->key, 0, &cbe_at(c, i)->txnId, p1);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* RelationMultiMap.AbstractBuilder (RelationMultiMap.java:88-260), K = key or Range     */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { int64_t a, b; } rkey_t;   /* key: (ordinal, 0); Range: (start, end) */
+
+/* Key.compareTo / Range.compare (Range.java:310-317: start then end) */
+static int rkey_cmp(const rkey_t* x, const rkey_t* y)
+{
+    if (x->a != y->a) return x->a < y->a ? -1 : 1;
+    if (x->b != y->b) return x->b < y->b ? -1 : 1;
+    return 0;
+}
+static int rkey_eq(const rkey_t* x, const rkey_t* y) { return x->a == y->a && x->b == y->b; }
+
+typedef struct {
+    VEC(rkey_t) keys;
+    VEC(int) keyLimits;
+    VEC(tid_t) keysToValues;
+    int keyCount, keyOffset, totalCount;
+    int hasOrderedKeys, hasOrderedValues;
+} builder_t;
+
+typedef struct {           /* a built RelationMultiMap: keys, values, keysToValues int[] */
+    size_t nkeys, nvalues, nout;
+    rkey_t* keys;
+    tid_t* values;
+    int32_t* out;
+} rmm_t;
+
+static void builder_init(builder_t* b)
+{
+    memset(b, 0, sizeof(*b));
+    b->hasOrderedKeys = 1;
+    b->hasOrderedValues = 1;
+}
+static void builder_free(builder_t* b) { VEC_FREE(b->keys); VEC_FREE(b->keyLimits); VEC_FREE(b->keysToValues); }
+static void rmm_free(rmm_t* m) { free(m->keys); free(m->values); free(m->out); memset(m, 0, sizeof(*m)); }
+
+static int cmp_tid_q(const void* a, const void* b) { return tid_cmp((const tid_t*)a, (const tid_t*)b); }
+
+/* stable merge sort for TxnId arrays (Arrays.sort(Object[]) is a stable TimSort) */
+static void stable_sort_tids(tid_t* a, size_t n)
+{
+    if (n < 2) return;
+    tid_t* tmp = malloc(n * sizeof(tid_t));
+    for (size_t width = 1; width < n; width *= 2)
+    {
+        for (size_t lo = 0; lo < n; lo += 2 * width)
+        {
+            size_t mid = lo + width < n ? lo + width : n, hi = lo + 2 * width < n ? lo + 2 * width : n;
+            size_t i = lo, j = mid, k = lo;
+            while (i < mid && j < hi) tmp[k++] = tid_cmp(&a[j], &a[i]) < 0 ? a[j++] : a[i++];
+            while (i < mid) tmp[k++] = a[i++];
+            while (j < hi) tmp[k++] = a[j++];
+        }
+        memcpy(a, tmp, n * sizeof(tid_t));
+    }
+    free(tmp);
+    (void)cmp_tid_q;
+}
+
+/* finishKey, :147-173 */
+static void builder_finish_key(builder_t* b)
+{
+    if (b->totalCount == b->keyOffset && b->keyCount > 0)
+    {
+        --b->keyCount;       /* remove this key; no data */
+        b->keys.n = b->keyCount;
+        return;
+    }
+    if (b->keyCount == 0)
+        return;
+    if (!b->hasOrderedValues)
+    {
+        stable_sort_tids(b->keysToValues.v + b->keyOffset, (size_t)(b->totalCount - b->keyOffset));
+        int removed = 0;
+        for (int i = b->keyOffset + 1; i < b->totalCount; ++i)
+        {
+            if (tid_eq(&b->keysToValues.v[i - 1], &b->keysToValues.v[i])) ++removed;
+            else if (removed > 0) b->keysToValues.v[i - removed] = b->keysToValues.v[i];
+        }
+        b->totalCount -= removed;
+        b->keysToValues.n = (size_t)b->totalCount;
+    }
+    while ((int)b->keyLimits.n < b->keyCount) VEC_PUSH(b->keyLimits, 0);
+    b->keyLimits.v[b->keyCount - 1] = b->totalCount;
+    b->keyOffset = b->totalCount;
+}
+
+/* nextKey, :125-145 */
+static void builder_next_key(builder_t* b, const rkey_t* key)
+{
+    if (b->keyCount > 0 && rkey_cmp(&b->keys.v[b->keyCount - 1], key) >= 0)
+        b->hasOrderedKeys = 0;
+    builder_finish_key(b);
+    b->keys.n = (size_t)b->keyCount;
+    VEC_PUSH(b->keys, *key);
+    b->keyCount++;
+    b->hasOrderedValues = 1;
+}
+
+/* add(V value), :184-199 */
+static void builder_add_value(builder_t* b, const tid_t* value)
+{
+    if (b->hasOrderedValues && b->totalCount > b->keyOffset
+        && tid_cmp(&b->keysToValues.v[b->totalCount - 1], value) >= 0)
+        b->hasOrderedValues = 0;
+    b->keysToValues.n = (size_t)b->totalCount;
+    VEC_PUSH(b->keysToValues, *value);
+    b->totalCount++;
+}
+
+/* add(K key, V value), :175-180 */
+static void builder_add(builder_t* b, const rkey_t* key, const tid_t* value)
+{
+    if (b->keyCount == 0 || !rkey_eq(&b->keys.v[b->keyCount - 1], key))
+        builder_next_key(b, key);
+    builder_add_value(b, value);
+}
+
+static const rkey_t* g_sort_keys;
+static int cmp_key_idx(const void* a, const void* b)
+{
+    return rkey_cmp(&g_sort_keys[*(const int*)a], &g_sort_keys[*(const int*)b]);
+}
+
+/* build(), :201-260. Returns 0 or AD_E_INVAL ("Key ... has been visited more than once"). */
+static int builder_build(builder_t* b, rmm_t* out)
+{
+    memset(out, 0, sizeof(*out));
+    if (b->totalCount == 0)
+        return 0;                                                       /* none() */
+
+    builder_finish_key(b);
+
+    int totalCount = b->totalCount, keyCount = b->keyCount;
+    tid_t* uniqueValues = malloc(sizeof(tid_t) * totalCount);
+    memcpy(uniqueValues, b->keysToValues.v, sizeof(tid_t) * totalCount);
+    stable_sort_tids(uniqueValues, (size_t)totalCount);
+    int valueCount = 1;
+    for (int i = 1; i < totalCount; ++i)
+    {
+        if (!tid_eq(&uniqueValues[valueCount - 1], &uniqueValues[i]))
+            uniqueValues[valueCount++] = uniqueValues[i];
+    }
+
+    int* sortedKeyIndexes = NULL;        /* maps sorted position -> original key index */
+    rkey_t* sortedKeys = malloc(sizeof(rkey_t) * (keyCount ? keyCount : 1));
+    if (b->hasOrderedKeys)
+    {
+        memcpy(sortedKeys, b->keys.v, sizeof(rkey_t) * keyCount);
+    }
+    else
+    {
+        sortedKeyIndexes = malloc(sizeof(int) * keyCount);
+        for (int i = 0; i < keyCount; ++i) sortedKeyIndexes[i] = i;
+        g_sort_keys = b->keys.v;
+        qsort(sortedKeyIndexes, keyCount, sizeof(int), cmp_key_idx);
+        for (int i = 0; i < keyCount; ++i) sortedKeys[i] = b->keys.v[sortedKeyIndexes[i]];
+        for (int i = 1; i < keyCount; ++i)
+        {
+            if (rkey_eq(&sortedKeys[i - 1], &sortedKeys[i]))
+            {
+                free(uniqueValues); free(sortedKeys); free(sortedKeyIndexes);
+                return AD_E_INVAL;
+            }
+        }
+    }
+
+    int32_t* result = malloc(sizeof(int32_t) * (keyCount + totalCount));
+    int offset = keyCount;
+    for (int ki = 0; ki < keyCount; ++ki)
+    {
+        int k = sortedKeyIndexes == NULL ? ki : sortedKeyIndexes[ki];
+        int from = k == 0 ? 0 : b->keyLimits.v[k - 1];
+        int to = b->keyLimits.v[k];
+        /* SortedArrays.foldlIntersection(values, keysToValues[from,to)) :1324-1344 */
+        int li = 0;
+        for (int ri = from; ri < to; ++ri)
+        {
+            while (li < valueCount && tid_cmp(&uniqueValues[li], &b->keysToValues.v[ri]) < 0) ++li;
+            if (li < valueCount && tid_cmp(&uniqueValues[li], &b->keysToValues.v[ri]) == 0)
+                result[offset++] = li;
+        }
+        result[ki] = offset;
+    }
+
+    out->nkeys = (size_t)keyCount;
+    out->keys = sortedKeys;
+    out->nvalues = (size_t)valueCount;
+    out->values = uniqueValues;
+    out->nout = (size_t)offset;
+    out->out = result;
+    free(sortedKeyIndexes);
+    return 0;
+}
+
+/* KeyDeps.with / RangeDeps.with -> RelationMultiMap.linearUnion (RelationMultiMap.java:561-816).
+ * linearUnion produces the canonical map of the union of both pair sets (returning an input
+ * unchanged when it is a superset); restated here as: walk the sorted key union and rebuild. */
+static int rmm_with(const rmm_t* x, const rmm_t* y, rmm_t* out)
+{
+    builder_t b;
+    builder_init(&b);
+    size_t i = 0, j = 0;
+    while (i < x->nkeys || j < y->nkeys)
+    {
+        int c = i >= x->nkeys ? 1 : j >= y->nkeys ? -1 : rkey_cmp(&x->keys[i], &y->keys[j]);
+        if (c <= 0)
+        {
+            int s = i == 0 ? (int)x->nkeys : x->out[i - 1];
+            for (int p = s; p < x->out[i]; ++p) builder_add(&b, &x->keys[i], &x->values[x->out[p]]);
+        }
+        if (c >= 0)
+        {
+            int s = j == 0 ? (int)y->nkeys : y->out[j - 1];
+            for (int p = s; p < y->out[j]; ++p) builder_add(&b, &y->keys[j], &y->values[y->out[p]]);
+        }
+        if (c <= 0) ++i;
+        if (c >= 0) ++j;
+    }
+    int rc = builder_build(&b, out);
+    builder_free(&b);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Store                                                                                */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    tid_t txnId;
+    int erased, historical;
+    VEC(rkey_t) ranges;
+} rcmd_t;
+
+typedef struct {
+    rkey_t range;
+    int64_t startEpoch, endEpoch;
+    tid_t wm;
+} rb_entry_t;
+
+struct rc_store {
+    ad_config cfg;
+    int64_t* slice_start; int64_t* slice_end; size_t n_slices;
+    VEC(cfk_t) cfks;          /* sorted by key */
+    VEC(rcmd_t) cmds;         /* rangeCommands, sorted by txnId */
+    VEC(rcmd_t) hist;         /* historicalRangeCommands, sorted by txnId */
+    VEC(rb_entry_t) rb;
+    int loaded;
+    char err[256];
+};
+
+static int fail(rc_store* s, int code, const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(s->err, sizeof(s->err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+const char* rc_last_error(const rc_store* s) { return s ? s->err : "null store"; }
+
+int rc_store_create(const ad_config* cfg, rc_store** out)
+{
+    rc_store* s = calloc(1, sizeof(rc_store));
+    if (!s) return AD_E_NOMEM;
+    s->cfg = *cfg;
+    s->n_slices = cfg->n_slices;
+    if (s->n_slices)
+    {
+        s->slice_start = malloc(sizeof(int64_t) * s->n_slices);
+        s->slice_end = malloc(sizeof(int64_t) * s->n_slices);
+        memcpy(s->slice_start, cfg->slice_start, sizeof(int64_t) * s->n_slices);
+        memcpy(s->slice_end, cfg->slice_end, sizeof(int64_t) * s->n_slices);
+    }
+    s->cfg.slice_start = s->slice_start;
+    s->cfg.slice_end = s->slice_end;
+    *out = s;
+    return 0;
+}
+
+static void free_cmds(rc_store* s)
+{
+    for (size_t i = 0; i < s->cmds.n; ++i) VEC_FREE(s->cmds.v[i].ranges);
+    for (size_t i = 0; i < s->hist.n; ++i) VEC_FREE(s->hist.v[i].ranges);
+    VEC_FREE(s->cmds); VEC_FREE(s->hist);
+}
+
+static void free_cfks(rc_store* s)
+{
+    for (size_t i = 0; i < s->cfks.n; ++i) { VEC_FREE(s->cfks.v[i].byId); free(s->cfks.v[i].cbe); }
+    VEC_FREE(s->cfks);
+}
+
+void rc_store_destroy(rc_store* s)
+{
+    if (!s) return;
+    free_cfks(s);
+    free_cmds(s);
+    VEC_FREE(s->rb);
+    free(s->slice_start); free(s->slice_end);
+    free(s);
+}
+
+/* Range.contains(key) (Range.java:288-291) for EndInclusive (:40-56) / StartInclusive (:84-100) */
+static int range_contains(const rc_store* s, const rkey_t* r, int64_t key)
+{
+    if (s->cfg.range_start_inclusive) return r->a <= key && key < r->b;
+    return r->a < key && key <= r->b;
+}
+
+/* Ranges.contains(key): the store's slice (mapReduceForKey, InMemoryCommandStore.java:280) */
+static int slice_contains(const rc_store* s, int64_t key)
+{
+    if (s->n_slices == 0) return 1;
+    for (size_t i = 0; i < s->n_slices; ++i)
+    {
+        rkey_t r = {s->slice_start[i], s->slice_end[i]};
+        if (range_contains(s, &r, key)) return 1;
+    }
+    return 0;
+}
+
+static cfk_t* find_cfk(rc_store* s, int64_t key)
+{
+    size_t lo = 0, hi = s->cfks.n;
+    while (lo < hi)
+    {
+        size_t mid = (lo + hi) / 2;
+        if (s->cfks.v[mid].key < key) lo = mid + 1;
+        else if (s->cfks.v[mid].key > key) hi = mid;
+        else return &s->cfks.v[mid];
+    }
+    return NULL;
+}
+
+int rc_cfk_load(rc_store* s, const ad_cfk_soa* in)
+{
+    free_cfks(s);
+    for (uint64_t k = 0; k < in->n_keys; ++k)
+    {
+        if (k > 0 && in->keys[k - 1] >= in->keys[k])
+            return fail(s, AD_E_INVAL, "keys not strictly ascending at %llu", (unsigned long long)k);
+        cfk_t c;
+        memset(&c, 0, sizeof(c));
+        c.key = in->keys[k];
+        for (uint64_t e = in->seg[k]; e < in->seg[k + 1]; ++e)
+        {
+            info_t info;
+            info.txnId = (tid_t){in->txn_msb[e], in->txn_lsb[e], in->txn_node[e]};
+            info.executeAt = (tid_t){in->exec_msb[e], in->exec_lsb[e], in->exec_node[e]};
+            info.status = in->status[e];
+            if (info.status > 7) { VEC_FREE(c.byId); return fail(s, AD_E_INVAL, "bad status"); }
+            if (c.byId.n > 0 && tid_cmp(&c.byId.v[c.byId.n - 1].txnId, &info.txnId) >= 0)
+            {
+                VEC_FREE(c.byId);
+                return fail(s, AD_E_ORDER, "byId not strictly ascending (CommandsForKey.java:1438) key %lld", (long long)c.key);
+            }
+            VEC_PUSH(c.byId, info);
+        }
+        cfk_derive(&c);
+        for (int i = 1; i < c.ncbe; ++i)
+        {
+            if (tid_cmp(&cbe_at(&c, i - 1)->executeAt, &cbe_at(&c, i)->executeAt) >= 0)
+            {
+                VEC_FREE(c.byId); free(c.cbe);
+                return fail(s, AD_E_DUP_EXEC, "duplicate committed executeAt (CommandsForKey.java:1439)");
+            }
+        }
+        if (in->pruned_before && in->pruned_before[k] >= 0)
+        {
+            /* CommandsForKey.java:645-647: prunedBefore must be present in byId */
+            int64_t idx = in->pruned_before[k];
+            if ((uint64_t)idx >= c.byId.n) { VEC_FREE(c.byId); free(c.cbe); return fail(s, AD_E_INVAL, "prunedBefore out of range"); }
+            c.hasPrunedBefore = 1;
+            c.prunedBefore = c.byId.v[idx].txnId;
+        }
+        VEC_PUSH(s->cfks, c);
+    }
+    s->loaded = 1;
+    return 0;
+}
+
+static const tid_t* g_sort_cmd_base;
+static int cmp_cmd(const void* a, const void* b) { return tid_cmp(&((const rcmd_t*)a)->txnId, &((const rcmd_t*)b)->txnId); }
+
+int rc_range_cmds_load(rc_store* s, const ad_range_cmds_soa* in)
+{
+    free_cmds(s);
+    (void)g_sort_cmd_base;
+    for (uint64_t i = 0; i < in->n_cmds; ++i)
+    {
+        rcmd_t c;
+        memset(&c, 0, sizeof(c));
+        c.txnId = (tid_t){in->txn_msb[i], in->txn_lsb[i], in->txn_node[i]};
+        c.erased = in->erased ? in->erased[i] : 0;
+        c.historical = in->historical ? in->historical[i] : 0;
+        for (uint64_t r = in->range_off[i]; r < in->range_off[i + 1]; ++r)
+        {
+            rkey_t rg = {in->range_start[r], in->range_end[r]};
+            VEC_PUSH(c.ranges, rg);
+        }
+        if (c.historical) VEC_PUSH(s->hist, c);
+        else VEC_PUSH(s->cmds, c);
+    }
+    /* TreeMap<TxnId, ...> iteration order (InMemoryCommandStore.java:103-104) */
+    qsort(s->cmds.v, s->cmds.n, sizeof(rcmd_t), cmp_cmd);
+    qsort(s->hist.v, s->hist.n, sizeof(rcmd_t), cmp_cmd);
+    for (size_t i = 1; i < s->cmds.n; ++i)
+        if (tid_eq(&s->cmds.v[i - 1].txnId, &s->cmds.v[i].txnId)) return fail(s, AD_E_INVAL, "duplicate range command");
+    for (size_t i = 1; i < s->hist.n; ++i)
+        if (tid_eq(&s->hist.v[i - 1].txnId, &s->hist.v[i].txnId)) return fail(s, AD_E_INVAL, "duplicate historical range command");
+    return 0;
+}
+
+int rc_redundant_load(rc_store* s, const ad_redundant_soa* in)
+{
+    VEC_FREE(s->rb);
+    for (uint64_t i = 0; i < in->n; ++i)
+    {
+        rb_entry_t e;
+        e.range = (rkey_t){in->range_start[i], in->range_end[i]};
+        e.startEpoch = in->start_epoch[i];
+        e.endEpoch = in->end_epoch[i];
+        e.wm = (tid_t){in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
+        if (s->rb.n && rkey_cmp(&s->rb.v[s->rb.n - 1].range, &e.range) >= 0)
+            return fail(s, AD_E_INVAL, "redundantBefore entries not ascending");
+        VEC_PUSH(s->rb, e);
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* PreAccept.calculatePartialDeps                                                       */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { builder_t key, range, direct; } deps_builder_t;   /* Deps.AbstractBuilder */
+
+/* Deps.AbstractBuilder.add, Deps.java:80-106 */
+static int deps_builder_add(deps_builder_t* d, int is_range, int64_t k0, int64_t k1, const tid_t* txnId)
+{
+    if (is_range != tid_domain(txnId)) return AD_E_STATE;             /* Invariants.checkArgument */
+    rkey_t key = {k0, is_range ? k1 : 0};
+    if (!is_range)
+    {
+        if (manages_execution(txnId)) builder_add(&d->key, &key, txnId);
+        else builder_add(&d->direct, &key, txnId);
+    }
+    else builder_add(&d->range, &key, txnId);
+    return 0;
+}
+
+/* the map lambda of PreAccept.calculatePartialDeps, PreAccept.java:257-261 */
+static int preaccept_map(void* acc, int is_range, int64_t k0, int64_t k1, const tid_t* testTxnId, const tid_t* p1)
+{
+    if (p1 == NULL || !tid_eq(testTxnId, p1))
+        return deps_builder_add((deps_builder_t*)acc, is_range, k0, k1, testTxnId);
+    return 0;
+}
+
+typedef struct { rkey_t range; VEC(tid_t) list; } collect_entry_t;
+typedef VEC(collect_entry_t) collect_vec_t;
+
+static int collect_find_or_insert(collect_vec_t* col, const rkey_t* r)
+{
+    size_t lo = 0, hi = col->n;
+    while (lo < hi)
+    {
+        size_t mid = (lo + hi) / 2;
+        int c = rkey_cmp(&col->v[mid].range, r);
+        if (c < 0) lo = mid + 1;
+        else if (c > 0) hi = mid;
+        else return (int)mid;
+    }
+    collect_entry_t e;
+    memset(&e, 0, sizeof(e));
+    e.range = *r;
+    VEC_PUSH(*col, e);
+    memmove(&col->v[lo + 1], &col->v[lo], (col->n - 1 - lo) * sizeof(collect_entry_t));
+    col->v[lo] = e;
+    return (int)lo;
+}
+
+/* Routables.foldl(ranges, sliced keys, ...) (Routables.java:148-156) visiting each range of a
+ * command that contains at least one sliced key, then the collect fold of
+ * InMemoryCommandStore.java:950-956 */
+static void collect_command(const rc_store* s, collect_vec_t* col, const rcmd_t* c,
+                            const int64_t* sliced, size_t nsliced)
+{
+    for (size_t r = 0; r < c->ranges.n; ++r)
+    {
+        int hit = 0;
+        for (size_t k = 0; k < nsliced && !hit; ++k) hit = range_contains(s, &c->ranges.v[r], sliced[k]);
+        if (!hit) continue;
+        int pos = collect_find_or_insert(col, &c->ranges.v[r]);
+        collect_entry_t* e = &col->v[pos];
+        if (e->list.n == 0 || !tid_eq(&e->list.v[e->list.n - 1], &c->txnId))
+            VEC_PUSH(e->list, c->txnId);
+    }
+}
+
+/* InMemoryCommandStore.mapReduceRangesInternal with STARTED_BEFORE, ANY_DEPS, ANY_STATUS
+ * (InMemoryCommandStore.java:884-1017) */
+static int map_reduce_ranges_internal(const rc_store* s, const int64_t* keys, size_t nkeys, const tid_t* testTimestamp,
+                                      unsigned testKind, cmd_fn map, const tid_t* p1, void* acc)
+{
+    /* keysOrRanges.slice(slice, Minimal) */
+    int64_t* sliced = malloc(sizeof(int64_t) * (nkeys ? nkeys : 1));
+    size_t nsliced = 0;
+    for (size_t k = 0; k < nkeys; ++k) if (slice_contains(s, keys[k])) sliced[nsliced++] = keys[k];
+
+    collect_vec_t col;
+    memset(&col, 0, sizeof(col));
+    for (size_t i = 0; i < s->cmds.n; ++i)
+    {
+        const rcmd_t* c = &s->cmds.v[i];
+        if (c->erased) continue;                                        /* saveStatus >= Erased, :897 */
+        if (tid_cmp(&c->txnId, testTimestamp) >= 0) continue;           /* STARTED_BEFORE, :907 */
+        if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;       /* :933 */
+        collect_command(s, &col, c, sliced, nsliced);                   /* intersects + foldl, :948-956 */
+    }
+    for (size_t i = 0; i < s->hist.n; ++i)                               /* :959-987 */
+    {
+        const rcmd_t* c = &s->hist.v[i];
+        if (tid_cmp(&c->txnId, testTimestamp) >= 0) continue;
+        if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;
+        collect_command(s, &col, c, sliced, nsliced);
+    }
+    int rc = 0;
+    for (size_t i = 0; i < col.n && !rc; ++i)                            /* :990-997 */
+        for (size_t j = 0; j < col.v[i].list.n && !rc; ++j)
+            rc = map(acc, 1, col.v[i].range.a, col.v[i].range.b, &col.v[i].list.v[j], p1);
+    for (size_t i = 0; i < col.n; ++i) VEC_FREE(col.v[i].list);
+    VEC_FREE(col);
+    free(sliced);
+    return rc;
+}
+
+/* RedundantBefore.collectDeps (RedundantBefore.java:420-423) -> Entry.collectDep (:183-192) */
+static int redundant_collect_deps(const rc_store* s, const int64_t* keys, size_t nkeys, int64_t minEpoch,
+                                  const tid_t* executeAt, deps_builder_t* d)
+{
+    static const tid_t NONE = {0, 0, 0};
+    for (size_t k = 0; k < nkeys; ++k)
+    {
+        for (size_t i = 0; i < s->rb.n; ++i)
+        {
+            const rb_entry_t* e = &s->rb.v[i];
+            if (!range_contains(s, &e->range, keys[k])) continue;
+            /* outOfBounds(lb, ub): ub.epoch() < startEpoch || lb.epoch() >= endEpoch, :262-265 */
+            if (tid_epoch(executeAt) < e->startEpoch || minEpoch >= e->endEpoch) continue;
+            if (tid_cmp(&e->wm, &NONE) > 0)
+            {
+                int rc = deps_builder_add(d, 1, e->range.a, e->range.b, &e->wm);
+                if (rc) return rc;
+            }
+        }
+    }
+    return 0;
+}
+
+typedef struct {                     /* PartialDeps (PartialDeps.java:54-59), covering omitted */
+    rmm_t key, range, direct;
+} pdeps_t;
+
+static void pdeps_free(pdeps_t* p) { rmm_free(&p->key); rmm_free(&p->range); rmm_free(&p->direct); }
+
+static int deps_build(deps_builder_t* d, pdeps_t* out)                 /* PartialDeps.Builder.build :40-46 */
+{
+    memset(out, 0, sizeof(*out));
+    int rc = builder_build(&d->key, &out->key);
+    if (!rc) rc = builder_build(&d->range, &out->range);
+    if (!rc) rc = builder_build(&d->direct, &out->direct);
+    return rc;
+}
+
+/* PartialDeps.with, PartialDeps.java:73-81 */
+static int pdeps_with(const pdeps_t* x, const pdeps_t* y, pdeps_t* out)
+{
+    memset(out, 0, sizeof(*out));
+    int rc = rmm_with(&x->key, &y->key, &out->key);
+    if (!rc) rc = rmm_with(&x->range, &y->range, &out->range);
+    if (!rc) rc = rmm_with(&x->direct, &y->direct, &out->direct);
+    return rc;
+}
+
+/* PreAccept.calculatePartialDeps, PreAccept.java:245-267 */
+static int calculate_partial_deps(rc_store* s, const tid_t* txnId, const int64_t* keys, size_t nkeys,
+                                  int64_t minEpoch, const tid_t* executeAt, pdeps_t* out, uint64_t* scan_entries)
+{
+    unsigned kinds = kind_witnesses(tid_kind(txnId));                   /* txnId.kind().witnesses() */
+    if (!kinds) return fail(s, AD_E_INVAL, "invalid Txn.Kind %d for witnesses()", tid_kind(txnId));
+    const tid_t* p1 = tid_eq(executeAt, txnId) ? NULL : txnId;
+
+    deps_builder_t builder, redundantBuilder;
+    builder_init(&builder.key); builder_init(&builder.range); builder_init(&builder.direct);
+    builder_init(&redundantBuilder.key); builder_init(&redundantBuilder.range); builder_init(&redundantBuilder.direct);
+
+    int rc = 0;
+    /* safeStore.mapReduceActive -> InMemorySafeStore.mapReduceActive (InMemoryCommandStore.java:863-871):
+     *   mapReduceForKey (:272-307, Key domain) then mapReduceRangesInternal */
+    for (size_t k = 0; k < nkeys && !rc; ++k)
+    {
+        if (!slice_contains(s, keys[k])) continue;
+        cfk_t* cfk = find_cfk(s, keys[k]);
+        if (cfk == NULL) continue;
+        rc = cfk_map_reduce_active(cfk, executeAt, kinds, s->cfg.elide, preaccept_map, p1, &builder, scan_entries);
+    }
+    if (!rc) rc = map_reduce_ranges_internal(s, keys, nkeys, executeAt, kinds, preaccept_map, p1, &builder);
+    if (!rc) rc = redundant_collect_deps(s, keys, nkeys, minEpoch, executeAt, &redundantBuilder);
+
+    pdeps_t built, redundant;
+    memset(&built, 0, sizeof(built)); memset(&redundant, 0, sizeof(redundant));
+    if (!rc) rc = deps_build(&builder, &built);
+    if (!rc) rc = deps_build(&redundantBuilder, &redundant);
+    if (!rc) rc = pdeps_with(&built, &redundant, out);                  /* builder.build().with(redundant) */
+    pdeps_free(&built); pdeps_free(&redundant);
+    builder_free(&builder.key); builder_free(&builder.range); builder_free(&builder.direct);
+    builder_free(&redundantBuilder.key); builder_free(&redundantBuilder.range); builder_free(&redundantBuilder.direct);
+    if (rc == AD_E_STATE) return fail(s, rc, "reference would throw (domain mismatch or prunedBefore walk)");
+    if (rc == AD_E_INVAL) return fail(s, rc, "builder: key visited more than once");
+    return rc;
+}
+
+/* PREACCEPTED insertion of Commands.preaccept -> SafeCommandStore.update ->
+ * CommandsForKey.update (CommandsForKey.java:972-1042): insert TxnInfo(txnId,
+ * PREACCEPTED_OR_ACCEPTED_INVALIDATE, executeAt = txnId) or raise a lower status. */
+static void sequential_preaccept(rc_store* s, const tid_t* txnId, const int64_t* keys, size_t nkeys)
+{
+    if (!manages(txnId)) return;
+    for (size_t k = 0; k < nkeys; ++k)
+    {
+        if (!slice_contains(s, keys[k])) continue;
+        cfk_t* c = find_cfk(s, keys[k]);
+        if (c == NULL)
+        {
+            cfk_t nc;
+            memset(&nc, 0, sizeof(nc));
+            nc.key = keys[k];
+            size_t pos = 0;
+            while (pos < s->cfks.n && s->cfks.v[pos].key < keys[k]) ++pos;
+            VEC_PUSH(s->cfks, nc);
+            memmove(&s->cfks.v[pos + 1], &s->cfks.v[pos], (s->cfks.n - 1 - pos) * sizeof(cfk_t));
+            s->cfks.v[pos] = nc;
+            c = &s->cfks.v[pos];
+            cfk_derive(c);
+        }
+        int pos = cfk_insert_pos(c, txnId);
+        if (pos < (int)c->byId.n && tid_cmp(&c->byId.v[pos].txnId, txnId) == 0)
+        {
+            info_t* cur = &c->byId.v[pos];
+            if (cur->status < AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE)
+            {
+                cur->status = AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE;
+                cur->executeAt = cur->txnId;
+            }
+        }
+        else
+        {
+            info_t info = {*txnId, AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE, *txnId};
+            VEC_PUSH(c->byId, info);
+            memmove(&c->byId.v[pos + 1], &c->byId.v[pos], (c->byId.n - 1 - pos) * sizeof(info_t));
+            c->byId.v[pos] = info;
+        }
+        cfk_derive(c);
+    }
+}
+
+static void result_alloc_map(rc_result* r, int m, size_t nk, size_t nt, size_t no)
+{
+    r->keys[m] = realloc(r->keys[m], sizeof(int64_t) * (nk ? nk : 1));
+    if (m == AD_MAP_RANGE) r->keys_end[m] = realloc(r->keys_end[m], sizeof(int64_t) * (nk ? nk : 1));
+    r->txn_msb[m] = realloc(r->txn_msb[m], sizeof(uint64_t) * (nt ? nt : 1));
+    r->txn_lsb[m] = realloc(r->txn_lsb[m], sizeof(uint64_t) * (nt ? nt : 1));
+    r->txn_node[m] = realloc(r->txn_node[m], sizeof(int32_t) * (nt ? nt : 1));
+    r->k2t[m] = realloc(r->k2t[m], sizeof(int32_t) * (no ? no : 1));
+}
+
+void rc_result_free(rc_result* r)
+{
+    if (!r) return;
+    for (int m = 0; m < AD_NMAPS; ++m)
+    {
+        free(r->keys_off[m]); free(r->keys[m]); free(r->keys_end[m]);
+        free(r->txn_off[m]); free(r->txn_msb[m]); free(r->txn_lsb[m]); free(r->txn_node[m]);
+        free(r->k2t_off[m]); free(r->k2t[m]);
+    }
+    free(r);
+}
+
+int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t first, uint64_t count, rc_result** out)
+{
+    if (!s->loaded) return fail(s, AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (count == 0) count = q->n_txns - first;
+    if (first + count > q->n_txns) return fail(s, AD_E_INVAL, "query window out of range");
+    rc_result* r = calloc(1, sizeof(rc_result));
+    r->n_txns = count;
+    size_t cap[AD_NMAPS][3] = {{0}};
+    size_t len[AD_NMAPS][3] = {{0}};
+    for (int m = 0; m < AD_NMAPS; ++m)
+    {
+        r->keys_off[m] = calloc(count + 1, sizeof(uint64_t));
+        r->txn_off[m] = calloc(count + 1, sizeof(uint64_t));
+        r->k2t_off[m] = calloc(count + 1, sizeof(uint64_t));
+    }
+    int rc = 0;
+    for (uint64_t qi = 0; qi < count && !rc; ++qi)
+    {
+        uint64_t i = first + qi;
+        tid_t txnId = {q->txn_msb[i], q->txn_lsb[i], q->txn_node[i]};
+        tid_t executeAt = {q->exec_msb[i], q->exec_lsb[i], q->exec_node[i]};
+        const int64_t* keys = q->keys + q->key_off[i];
+        size_t nkeys = (size_t)(q->key_off[i + 1] - q->key_off[i]);
+        for (size_t k = 1; k < nkeys; ++k)
+            if (keys[k - 1] >= keys[k]) { rc = fail(s, AD_E_INVAL, "query keys not strictly ascending"); break; }
+        if (rc) break;
+        if (flags & AD_SEQUENTIAL) sequential_preaccept(s, &txnId, keys, nkeys);
+        pdeps_t pd;
+        rc = calculate_partial_deps(s, &txnId, keys, nkeys, q->min_epoch ? q->min_epoch[i] : 0, &executeAt, &pd, &r->scan_entries);
+        if (rc) break;
+        const rmm_t* maps[AD_NMAPS] = {&pd.key, &pd.range, &pd.direct};
+        for (int m = 0; m < AD_NMAPS; ++m)
+        {
+            const rmm_t* mm = maps[m];
+            size_t nk = len[m][0] + mm->nkeys, nt = len[m][1] + mm->nvalues, no = len[m][2] + mm->nout;
+            if (nk > cap[m][0] || nt > cap[m][1] || no > cap[m][2])
+            {
+                cap[m][0] = nk * 2 + 16; cap[m][1] = nt * 2 + 16; cap[m][2] = no * 2 + 16;
+                result_alloc_map(r, m, cap[m][0], cap[m][1], cap[m][2]);
+            }
+            for (size_t k = 0; k < mm->nkeys; ++k)
+            {
+                r->keys[m][len[m][0] + k] = mm->keys[k].a;
+                if (m == AD_MAP_RANGE) r->keys_end[m][len[m][0] + k] = mm->keys[k].b;
+            }
+            for (size_t t = 0; t < mm->nvalues; ++t)
+            {
+                r->txn_msb[m][len[m][1] + t] = mm->values[t].msb;
+                r->txn_lsb[m][len[m][1] + t] = mm->values[t].lsb;
+                r->txn_node[m][len[m][1] + t] = mm->values[t].node;
+            }
+            memcpy(r->k2t[m] + len[m][2], mm->out, sizeof(int32_t) * mm->nout);
+            len[m][0] = nk; len[m][1] = nt; len[m][2] = no;
+            r->keys_off[m][qi + 1] = nk;
+            r->txn_off[m][qi + 1] = nt;
+            r->k2t_off[m][qi + 1] = no;
+        }
+        pdeps_free(&pd);
+    }
+    if (rc) { rc_result_free(r); return rc; }
+    for (int m = 0; m < AD_NMAPS; ++m)
+        if (!r->keys[m]) result_alloc_map(r, m, 1, 1, 1);
+    *out = r;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Execution ordering levels (config 5)                                                 */
+/* ------------------------------------------------------------------------------------ */
+/* T waits, on every key it shares with P, for each P with executeAt(P) < executeAt(T) that
+ * T's kind witnesses (Txn.Kind.witnesses, Txn.java:221-235; CommandsForKey.notifyManaged
+ * CommandsForKey.java:1193-1274), and for each direct dep P with executeAt(P) < executeAt(T)
+ * (Commands.updateWaitingOn drops deps executing later, Commands.java:700-775).
+ * level(T) = 0 without waits, else 1 + max level(P). Evaluated in executeAt order. */
+typedef struct { int64_t key; tid_t e; uint32_t txn; } kv_t;
+static int cmp_kv(const void* a, const void* b)
+{
+    const kv_t* x = a; const kv_t* y = b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    return tid_cmp(&x->e, &y->e);
+}
+static const ad_graph_soa* g_graph;
+static int cmp_exec_idx(const void* a, const void* b)
+{
+    uint32_t i = *(const uint32_t*)a, j = *(const uint32_t*)b;
+    tid_t x = {g_graph->exec_msb[i], g_graph->exec_lsb[i], g_graph->exec_node[i]};
+    tid_t y = {g_graph->exec_msb[j], g_graph->exec_lsb[j], g_graph->exec_node[j]};
+    return tid_cmp(&x, &y);
+}
+
+int rc_levels(const ad_graph_soa* g, uint32_t* level)
+{
+    uint64_t n = g->n_txns;
+    uint64_t nkv = g->key_off[n];
+    kv_t* kv = malloc(sizeof(kv_t) * (nkv ? nkv : 1));
+    for (uint64_t i = 0; i < n; ++i)
+        for (uint64_t k = g->key_off[i]; k < g->key_off[i + 1]; ++k)
+            kv[k] = (kv_t){g->keys[k], {g->exec_msb[i], g->exec_lsb[i], g->exec_node[i]}, (uint32_t)i};
+    qsort(kv, nkv, sizeof(kv_t), cmp_kv);
+    /* per (key, txn) position so each txn finds its predecessors on that key */
+    uint64_t* pos_of = malloc(sizeof(uint64_t) * (nkv ? nkv : 1));   /* key-occurrence index -> position in kv */
+    uint64_t* cursor = calloc(n + 1, sizeof(uint64_t));
+    for (uint64_t p = 0; p < nkv; ++p)
+    {
+        uint32_t t = kv[p].txn;
+        pos_of[g->key_off[t] + cursor[t]++] = p;
+    }
+    uint32_t* order = malloc(sizeof(uint32_t) * (n ? n : 1));
+    for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+    g_graph = g;
+    qsort(order, n, sizeof(uint32_t), cmp_exec_idx);
+    for (uint64_t i = 1; i < n; ++i)
+        if (cmp_exec_idx(&order[i - 1], &order[i]) == 0) { free(kv); free(pos_of); free(cursor); free(order); return AD_E_DUP_EXEC; }
+    int rc = 0;
+    for (uint64_t oi = 0; oi < n; ++oi)
+    {
+        uint32_t t = order[oi];
+        unsigned w = kind_witnesses(g->kind[t]);
+        uint32_t lvl = 0;
+        int has = 0;
+        for (uint64_t k = g->key_off[t]; k < g->key_off[t + 1]; ++k)
+        {
+            uint64_t p = pos_of[k];
+            int64_t key = kv[p].key;
+            for (uint64_t q = p; q-- > 0 && kv[q].key == key;)
+            {
+                uint32_t P = kv[q].txn;
+                if (!kinds_test(w, g->kind[P])) continue;
+                has = 1;
+                if (level[P] + 1 > lvl) lvl = level[P] + 1;
+            }
+        }
+        if (g->dep_off)
+        {
+            tid_t et = {g->exec_msb[t], g->exec_lsb[t], g->exec_node[t]};
+            for (uint64_t d = g->dep_off[t]; d < g->dep_off[t + 1]; ++d)
+            {
+                uint32_t P = g->deps[d];
+                if (P >= n) { rc = AD_E_INVAL; break; }
+                tid_t ep = {g->exec_msb[P], g->exec_lsb[P], g->exec_node[P]};
+                if (tid_cmp(&ep, &et) >= 0) continue;
+                has = 1;
+                if (level[P] + 1 > lvl) lvl = level[P] + 1;
+            }
+        }
+        level[t] = has ? lvl : 0;
+    }
+    free(kv); free(pos_of); free(cursor); free(order);
+    return rc;
+}

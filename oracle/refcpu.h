@@ -1,0 +1,60 @@
+/*
+ * refcpu — CPU restatement of the reference (Apache Cassandra Accord, Java) dependency
+ * calculation for PreAccept/Accept.  TEST INFRASTRUCTURE ONLY: it is the parity oracle and
+ * the CPU baseline, never part of the product (libaccord_deps.so does not link it).
+ *
+ * Pinning: the Java reference cannot run in this image (no JDK) and ships
+ * no golden vectors; the restatement is pinned by the reference's own known-answer tests
+ * (PreAcceptTest.java:114,209,241,283) and by ports of its model-based tests
+ * (KeyDepsTest, RangeDepsTest, SearchableRangeListTest, DepsTest) under tests/.
+ *
+ * Data formats are the ones of include/accord_deps.h (shared struct layouts only).
+ */
+#ifndef ACCORD_REFCPU_H
+#define ACCORD_REFCPU_H
+
+#include "../include/accord_deps.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rc_store rc_store;
+
+/* Fully materialised result: TxnIds as {msb,lsb,node}, range keys as (start,end). */
+typedef struct rc_result {
+    uint64_t  n_txns;
+    uint64_t* keys_off[AD_NMAPS];
+    int64_t*  keys[AD_NMAPS];        /* key ordinal, or range start for AD_MAP_RANGE      */
+    int64_t*  keys_end[AD_NMAPS];    /* range end for AD_MAP_RANGE, NULL otherwise        */
+    uint64_t* txn_off[AD_NMAPS];
+    uint64_t* txn_msb[AD_NMAPS];
+    uint64_t* txn_lsb[AD_NMAPS];
+    int32_t*  txn_node[AD_NMAPS];
+    uint64_t* k2t_off[AD_NMAPS];
+    int32_t*  k2t[AD_NMAPS];
+    uint64_t  scan_entries;          /* sum over probes of CommandsForKey scan length `end` */
+} rc_result;
+
+int  rc_store_create(const ad_config* cfg, rc_store** out);
+void rc_store_destroy(rc_store* s);
+const char* rc_last_error(const rc_store* s);
+
+int rc_cfk_load(rc_store* s, const ad_cfk_soa* cfk);
+int rc_range_cmds_load(rc_store* s, const ad_range_cmds_soa* cmds);
+int rc_redundant_load(rc_store* s, const ad_redundant_soa* rb);
+
+/* Resolve queries [first, first+count) of q (count == 0: all). */
+int  rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t first,
+                   uint64_t count, rc_result** out);
+void rc_result_free(rc_result* r);
+
+int rc_levels(const ad_graph_soa* g, uint32_t* level_out);
+
+/* exposed for the tests */
+int rc_tid_cmp(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,139 @@
+"""Pure-Python mirror of the reference semantics, written independently of oracle/refcpu.c,
+used only to cross-check the C restatement on small inputs (test infrastructure).
+
+Canonical-model style of the reference's own tests: the deps of a request are computed as
+pair SETS (like KeyDepsTest's Map<Key, NavigableSet<TxnId>> model, KeyDepsTest.java:337-346,
+and RangeDepsTest's brute-force overlap model, RangeDepsTest.java:95-169), then encoded into
+the RelationMultiMap CSR (RelationMultiMap.java:245-257).
+"""
+import numpy as np
+
+IDENT = 0xFFFFFFFFFFFF001E
+
+
+def key(t):
+    """Timestamp.compareTo as a sort key (Timestamp.java:208-217)."""
+    msb, lsb, node = t
+    return (msb, lsb >> 16, lsb & 0x1E, node)
+
+
+def eq(a, b):
+    return a[0] == b[0] and ((a[1] ^ b[1]) & IDENT) == 0 and a[2] == b[2]
+
+
+def kind(t):
+    return (t[1] >> 1) & 7
+
+
+def domain(t):
+    return t[1] & 1
+
+
+WITNESSES = {0: {1}, 2: {1}, 1: {0, 1}, 3: {0, 1}, 4: {0, 1, 3, 4}}
+
+
+def contains(start_inclusive, s, e, k):
+    return (s <= k < e) if start_inclusive else (s < k <= e)
+
+
+def cfk_active(entries, S, kinds, elide=True, pruned=None):
+    """CommandsForKey.mapReduceActive (CommandsForKey.java:910-968) over entries
+    [(txnId, status, executeAt)] sorted by txnId."""
+    end = sum(1 for t, _, _ in entries if key(t) < key(S))
+    committed = sorted([e for e in entries if 4 <= e[1] <= 6], key=lambda e: key(e[2]))
+    writes_before = [e for e in committed if kind(e[0]) == 1 and key(e[2]) < key(S)]
+    M = writes_before[-1][2] if writes_before else None
+    out = []
+    for t, st, ex in entries[:end]:
+        if kind(t) not in kinds:
+            continue
+        if st in (0, 7):
+            continue
+        if st in (4, 5, 6) and elide and M is not None and key(ex) < key(M) and kind(t) in (0, 1):
+            continue
+        out.append(t)
+    if pruned is not None and key(S) <= key(pruned):
+        maw = max([i for i, e in enumerate(committed) if e[1] == 6 and kind(e[0]) == 1])
+        cand = [i for i in range(maw) if key(committed[i][2]) >= key(S)]
+        i = cand[0] if cand else maw
+        while kind(committed[i][0]) != 1:
+            i += 1
+        out.append(committed[i][0])
+    return out
+
+
+def request_pairs(w, qi, elide=True):
+    """(keyDeps, rangeDeps, directKeyDeps) pair sets of PreAccept.calculatePartialDeps."""
+    q = w.queries
+    txn = (int(q.txn.msb[qi]), int(q.txn.lsb[qi]), int(q.txn.node[qi]))
+    ex = (int(q.exec.msb[qi]), int(q.exec.lsb[qi]), int(q.exec.node[qi]))
+    keys = [int(k) for k in q.keys[int(q.key_off[qi]):int(q.key_off[qi + 1])]]
+    min_epoch = 0 if q.min_epoch is None else int(q.min_epoch[qi])
+    kinds = WITNESSES[kind(txn)]
+    p1 = None if eq(ex, txn) else txn
+    si = w.range_start_inclusive
+
+    def in_slice(k):
+        if w.slices is None:
+            return True
+        return any(contains(si, int(a), int(b), k) for a, b in w.slices)
+
+    kd, rd, dd = set(), set(), set()
+    cfk = w.cfk
+    kidx = {int(k): i for i, k in enumerate(cfk.keys)}
+    for k in keys:
+        if not in_slice(k) or k not in kidx:
+            continue
+        i = kidx[k]
+        s0, s1 = int(cfk.seg[i]), int(cfk.seg[i + 1])
+        ents = [((int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e])), int(cfk.status[e]),
+                 (int(cfk.exec.msb[e]), int(cfk.exec.lsb[e]), int(cfk.exec.node[e]))) for e in range(s0, s1)]
+        pruned = None
+        if cfk.pruned_before is not None and cfk.pruned_before[i] >= 0:
+            pruned = ents[int(cfk.pruned_before[i])][0]
+        for t in cfk_active(ents, ex, kinds, elide, pruned):
+            if p1 is not None and eq(t, p1):
+                continue
+            (kd if kind(t) in (0, 1) else dd).add((k, key(t), t))
+    sliced = [k for k in keys if in_slice(k)]
+    c = w.cmds
+    for ci in range(len(c.txn)):
+        t = (int(c.txn.msb[ci]), int(c.txn.lsb[ci]), int(c.txn.node[ci]))
+        hist = c.historical is not None and c.historical[ci]
+        if not hist and c.erased is not None and c.erased[ci]:
+            continue
+        if key(t) >= key(ex) or kind(t) not in kinds:
+            continue
+        if p1 is not None and eq(t, p1):
+            continue
+        for r in range(int(c.range_off[ci]), int(c.range_off[ci + 1])):
+            s, e = int(c.range_start[r]), int(c.range_end[r])
+            if any(contains(si, s, e, k) for k in sliced):
+                rd.add(((s, e), key(t), t))
+    rb = w.redundant
+    ep = ex[0] >> 15
+    for i in range(len(rb.range_start)):
+        s, e = int(rb.range_start[i]), int(rb.range_end[i])
+        wm = (int(rb.wm.msb[i]), int(rb.wm.lsb[i]), int(rb.wm.node[i]))
+        if not any(contains(si, s, e, k) for k in keys):
+            continue
+        if ep < int(rb.start_epoch[i]) or min_epoch >= int(rb.end_epoch[i]):
+            continue
+        if key(wm) > key((0, 0, 0)):
+            rd.add(((s, e), key(wm), wm))
+    return kd, rd, dd
+
+
+def csr(pairs):
+    """RelationMultiMap CSR of a pair set: sorted keys with >= 1 value, sorted unique values,
+    keysToValues = [absolute end offsets starting at nKeys] + value indices."""
+    keys = sorted({p[0] for p in pairs})
+    vals = sorted({(p[1], p[2]) for p in pairs})
+    vindex = {v[0]: i for i, v in enumerate(vals)}
+    out = []
+    body = []
+    for k in keys:
+        idx = sorted(vindex[p[1]] for p in pairs if p[0] == k)
+        body.extend(idx)
+        out.append(len(keys) + len(body))
+    return keys, [v[1] for v in vals], out + body

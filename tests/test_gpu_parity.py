@@ -1,0 +1,90 @@
+"""GPU parity: libaccord_deps (HIP, through the C ABI) vs the CPU restatement of the reference.
+
+Bit-exact comparison of all three RelationMultiMaps of every request's PartialDeps
+(keys, txnIds, keysToTxnIds), i.e. Deps.equals (Deps.java:294-303).
+"""
+import numpy as np
+import pytest
+
+from accord_deps import _abi as A
+from accord_deps import native, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(w, oracle, elide=1):
+    exp = oracle.resolve(w, elide=elide)
+    got = native.resolve(w, elide=elide)
+    ok, why = got.equals(exp, detail=True)
+    if not ok:
+        mm = got.first_mismatch(exp)
+        raise AssertionError("%s: %s; first mismatch %r" % (w.name, why, mm))
+    return got, exp
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_small(oracle, seed):
+    w = synth.random_small(seed, with_slices=(seed % 4 == 3), start_inclusive=(seed % 5 == 4))
+    _compare(w, oracle)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_small_no_elision(oracle, seed):
+    _compare(synth.random_small(100 + seed), oracle, elide=0)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_larger(oracle, seed):
+    w = synth.random_small(1000 + seed, n_keys=300, n_hist_txns=3000, n_txns=800, max_keys=8, n_range_cmds=200)
+    _compare(w, oracle)
+
+
+def test_config1_sequential(oracle):
+    got, exp = _compare(synth.config1(), oracle)
+    assert got.pair_count(A.AD_MAP_KEY) > 0
+
+
+def test_config2_scaled(oracle):
+    w = synth.config2(n_txns=3000, n_keys=30000, n_hist_entries=400000, esp_frac=0.01)
+    got, exp = _compare(w, oracle)
+    assert got.pair_count(A.AD_MAP_DIRECT_KEY) > 0
+
+
+def test_config3_scaled_sharded(oracle):
+    w = synth.config3(n_txns=400_000, n_keys=50_000)
+    lo, hi = synth.shard_bounds(4)
+    for g in range(4):
+        _compare(synth.slice_workload(w, lo[g], hi[g]), oracle)
+
+
+def test_config4_scaled(oracle):
+    w = synth.config4(n_txns=3000, n_keys=20000, n_ranges=5000, n_hist_txns=20000)
+    got, exp = _compare(w, oracle)
+    assert got.pair_count(A.AD_MAP_RANGE) > 0
+
+
+def test_big_requests(oracle):
+    # a hot key with thousands of live entries -> per-probe outputs beyond the LDS staging
+    w = synth.config2(n_txns=200, n_keys=50, n_hist_entries=40000, keys_per_txn=8, tail_unapplied=3000,
+                      esp_frac=0.2)
+    _compare(w, oracle)
+
+
+def test_empty_batch_and_empty_snapshot(oracle):
+    w = synth.random_small(3)
+    w.queries = w.queries.window(0, 0)
+    _compare(w, oracle)
+
+
+def test_errors():
+    w = synth.random_small(5)
+    st = native.DeviceCommandStore()
+    st.load(w)
+    q = w.queries
+    bad = q.window(0, len(q))
+    i = int(np.argmax(np.diff(bad.key_off.astype(np.int64)) >= 2))
+    k0 = int(bad.key_off[i])
+    bad.keys[k0], bad.keys[k0 + 1] = bad.keys[k0 + 1], bad.keys[k0]
+    with pytest.raises(native.AccordDepsError) as e:
+        st.calculate_partial_deps(bad)
+    assert e.value.code == A.AD_E_INVAL

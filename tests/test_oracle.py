@@ -1,0 +1,212 @@
+"""CPU tests of the oracle (oracle/refcpu.c): known answers from the reference's own tests, a
+cross-check against an independent Python restatement, and Timestamp order/identity."""
+import random
+
+import numpy as np
+import pytest
+
+from accord_deps import _abi as A
+from accord_deps import synth
+from accord_deps.model import CfkSnapshot, Queries, RangeCommands, Redundant, Workload, make_txn_ids
+
+import refmodel
+
+
+def _request(batch, i):
+    out = []
+    for m in range(3):
+        ks, ke, t, k2t = batch.maps[m].request(i)
+        keys = [int(k) for k in ks] if ke is None else [(int(a), int(b)) for a, b in zip(ks, ke)]
+        out.append((keys, t.tuples(), [int(x) for x in k2t]))
+    return out
+
+
+def _single_key_queries(txns, keys_per_txn):
+    """Queries for a list of TxnIds (Tids) with per-request keys (lists)."""
+    key_off = np.zeros(len(keys_per_txn) + 1, np.uint64)
+    key_off[1:] = np.cumsum([len(k) for k in keys_per_txn])
+    keys = np.concatenate([np.asarray(k, np.int64) for k in keys_per_txn])
+    return Queries(txns, txns, key_off, keys)
+
+
+# --------------------------------------------------------------------------------------------
+# Known answers of PreAcceptTest (accord-core/src/test/java/accord/messages/PreAcceptTest.java).
+# Every PreAcceptOk there carries PartialDeps with KeyDeps.NONE, RangeDeps.NONE, KeyDeps.NONE.
+# --------------------------------------------------------------------------------------------
+def _preaccept_store(oracle):
+    st = oracle.OracleStore()
+    w = Workload("kat", CfkSnapshot.empty(), RangeCommands.empty(), Redundant.empty(), None)
+    st.load(w)
+    return st
+
+
+def _empty(batch):
+    return all(batch.pair_count(m) == 0 for m in range(3)) and all(len(batch.maps[m].keys) == 0 for m in range(3))
+
+
+def test_kat_initial_command(oracle):
+    # initialCommandTest (:87-121): first write on key 10 -> no deps (:114)
+    st = _preaccept_store(oracle)
+    t = make_txn_ids([1], [101], [A.KIND_WRITE], [2])
+    r = st.deps_batch(_single_key_queries(t, [[10]]), A.AD_SEQUENTIAL)
+    assert _empty(r)
+
+
+def test_kat_multi_key_timestamp_update(oracle):
+    # multiKeyTimestampUpdate (:183-215): txn1 writes key 10 at hlc ~110; txn2 = TxnId(1, 50, Write,
+    # Key, ID3) on keys {10, 11} started before txn1, so it has no deps (:209)
+    st = _preaccept_store(oracle)
+    t1 = make_txn_ids([1], [110], [A.KIND_WRITE], [2])
+    assert _empty(st.deps_batch(_single_key_queries(t1, [[10]]), A.AD_SEQUENTIAL))
+    t2 = make_txn_ids([1], [50], [A.KIND_WRITE], [3])
+    assert _empty(st.deps_batch(_single_key_queries(t2, [[10, 11]]), A.AD_SEQUENTIAL))
+
+
+def test_kat_single_key_newer_timestamp(oracle):
+    # singleKeyNewerTimestamp (:221-245): TxnId(1, 110, Write, Key, ID2) on an empty store (:241)
+    st = _preaccept_store(oracle)
+    t = make_txn_ids([1], [110], [A.KIND_WRITE], [2])
+    assert _empty(st.deps_batch(_single_key_queries(t, [[10]]), A.AD_SEQUENTIAL))
+
+
+def test_kat_superseding_epoch(oracle):
+    # supersedingEpochPrecludesFastPath (:247-290): epoch-2 topology, first txn on key 10 (:283)
+    st = _preaccept_store(oracle)
+    t = make_txn_ids([1], [101], [A.KIND_WRITE], [2])
+    assert _empty(st.deps_batch(_single_key_queries(t, [[10]]), A.AD_SEQUENTIAL))
+
+
+def test_derived_write_after_write(oracle):
+    # derived from the code (not a reference KAT): a later write on the same key depends on the
+    # earlier PREACCEPTED write (never elided), a later read too (Ws), a later read on another key not
+    st = _preaccept_store(oracle)
+    t = make_txn_ids([1, 1, 1, 1], [100, 110, 120, 130], [A.KIND_WRITE, A.KIND_WRITE, A.KIND_READ, A.KIND_READ],
+                     [2, 3, 2, 3])
+    r = st.deps_batch(_single_key_queries(t, [[10], [10], [10, 11], [11]]), A.AD_SEQUENTIAL)
+    reqs = [_request(r, i) for i in range(4)]
+    tup = t.tuples()
+    assert reqs[0][0] == ([], [], [])
+    assert reqs[1][0] == ([10], [tup[0]], [2, 0])      # heads are absolute: nKeys + count
+    assert reqs[2][0] == ([10], [tup[0], tup[1]], [3, 0, 1])
+    assert reqs[3][0] == ([], [], [])                  # reads do not witness reads
+
+
+def test_elision_of_transitive_dependencies(oracle):
+    # CommandsForKey.java:913-950: M = executeAt of the last committed write before S (the STABLE
+    # write at 120); committed reads/writes executing before M are elided (ELIDE_TRANSITIVE_DEPENDENCIES)
+    t = make_txn_ids([1, 1, 1], [100, 110, 120], [A.KIND_WRITE] * 3, [1, 1, 1])
+    cfk = CfkSnapshot(np.array([7]), np.array([0, 3]), t, t, np.array([A.ST_APPLIED, A.ST_APPLIED, A.ST_STABLE]))
+    q = _single_key_queries(make_txn_ids([1], [200], [A.KIND_WRITE], [4]), [[7]])
+    w = Workload("elide", cfk, RangeCommands.empty(), Redundant.empty(), q)
+    r = oracle.resolve(w)
+    assert _request(r, 0)[0] == ([7], [t.tuples()[2]], [2, 0])
+    r = oracle.resolve(w, elide=0)
+    assert _request(r, 0)[0] == ([7], t.tuples(), [4, 0, 1, 2])   # elision off: all three
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_crosscheck_python_restatement(oracle, seed):
+    w = synth.random_small(seed, with_slices=(seed % 3 == 2), start_inclusive=(seed % 4 == 1))
+    batch = oracle.resolve(w)
+    for i in range(len(w.queries)):
+        kd, rd, dd = refmodel.request_pairs(w, i)
+        got = _request(batch, i)
+        for m, pairs in ((0, kd), (1, rd), (2, dd)):
+            keys, vals, k2t = refmodel.csr(pairs)
+            assert got[m] == (keys, vals, k2t), (seed, i, A.MAP_NAMES[m])
+
+
+def test_crosscheck_no_elision(oracle):
+    w = synth.random_small(77)
+    batch = oracle.resolve(w, elide=0)
+    for i in range(len(w.queries)):
+        kd, rd, dd = refmodel.request_pairs(w, i, elide=False)
+        got = _request(batch, i)
+        assert got[0] == tuple(refmodel.csr(kd))
+        assert got[2] == tuple(refmodel.csr(dd))
+
+
+def test_sequential_equals_augmented_snapshot(oracle):
+    # SEQUENTIAL (in ascending TxnId order) == SNAPSHOT over history + batch as PREACCEPTED
+    # (SURVEY Appendix B), the identity the device implementation relies on
+    w = synth.config1(n_txns=600, n_keys=60)
+    seq = oracle.resolve(w)
+    q = w.queries
+    ent = []
+    for i in range(len(q)):
+        for k in q.keys[int(q.key_off[i]):int(q.key_off[i + 1])]:
+            ent.append((int(k), i))
+    ent.sort()
+    keys = sorted({k for k, _ in ent})
+    seg = np.zeros(len(keys) + 1, np.uint64)
+    seg[1:] = np.cumsum([sum(1 for kk, _ in ent if kk == k) for k in keys])
+    idx = np.array([i for _, i in ent])
+    t = q.txn.take(idx)
+    cfk = CfkSnapshot(np.array(keys), seg, t, t, np.full(len(idx), A.ST_PREACCEPTED, np.uint8))
+    snap = oracle.resolve(Workload("aug", cfk, RangeCommands.empty(), Redundant.empty(), q))
+    assert seq.equals(snap)
+
+
+def test_timestamp_compare_and_equals(oracle):
+    rng = random.Random(3)
+    vals = []
+    for _ in range(400):
+        msb = rng.choice([0, 1, 5, (1 << 63) + 7, (1 << 64) - 1, rng.getrandbits(64)])
+        lsb = rng.choice([0, 1, 0x1E, 0x8000, 0xFFFF, rng.getrandbits(64)])
+        node = rng.choice([0, 1, -1, 2 ** 31 - 1, -2 ** 31, rng.randint(-5, 5)])
+        vals.append((msb, lsb, node))
+    for _ in range(4000):
+        a, b = rng.choice(vals), rng.choice(vals)
+        c = oracle.tid_cmp(a, b)
+        kk = (refmodel.key(a) > refmodel.key(b)) - (refmodel.key(a) < refmodel.key(b))
+        assert np.sign(c) == kk
+        assert (c == 0) == refmodel.eq(a, b)
+    # domain bit and REJECTED flag are not identity (Timestamp.java:41-45)
+    assert oracle.tid_cmp((1, 0x10000, 3), (1, 0x10001, 3)) == 0
+    assert oracle.tid_cmp((1, 0x10000, 3), (1, 0x18000, 3)) == 0
+    assert oracle.tid_cmp((1, 0x10000, 3), (1, 0x10002, 3)) < 0
+    assert oracle.tid_cmp((1 << 63, 0, 0), (1, 0, 0)) > 0          # unsigned msb
+
+
+def test_levels_match_round_simulation(oracle):
+    # level(T) = apply round when every txn applies as soon as all it waits on have applied
+    g, _ = synth.config5(n_txns=3000, n_keys=300)
+    lv = oracle.levels(g)
+    n = len(g.kind)
+    order = np.lexsort(g.exec.order_key())
+    pos = np.empty(n, np.int64)
+    pos[order] = np.arange(n)
+    waits = [set() for _ in range(n)]
+    by_key = {}
+    for t in range(n):
+        for k in g.keys[int(g.key_off[t]):int(g.key_off[t + 1])]:
+            by_key.setdefault(int(k), []).append(t)
+    for k, ts in by_key.items():
+        ts.sort(key=lambda t: pos[t])
+        for j, t in enumerate(ts):
+            for p in ts[:j]:
+                if int(g.kind[p]) in refmodel.WITNESSES[int(g.kind[t])]:
+                    waits[t].add(p)
+    for t in range(n):
+        for d in g.deps[int(g.dep_off[t]):int(g.dep_off[t + 1])]:
+            if pos[int(d)] < pos[t]:
+                waits[t].add(int(d))
+    level = np.full(n, -1)
+    r = 0
+    done = 0
+    while done < n:
+        ready = [t for t in range(n) if level[t] < 0 and all(level[p] >= 0 and level[p] < r for p in waits[t])]
+        for t in ready:
+            level[t] = r
+        done += len(ready)
+        r += 1
+    assert np.array_equal(level, lv.astype(np.int64))
+
+
+def test_oracle_rejects_invalid_inputs(oracle):
+    t = make_txn_ids([1, 1], [110, 100], [A.KIND_WRITE] * 2, [1, 1])
+    cfk = CfkSnapshot(np.array([1]), np.array([0, 2]), t, t, np.array([A.ST_APPLIED] * 2))
+    st = oracle.OracleStore()
+    with pytest.raises(oracle.OracleError) as e:
+        st.load(Workload("bad", cfk, RangeCommands.empty(), Redundant.empty(), None))
+    assert e.value.code == A.AD_E_ORDER
