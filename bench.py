@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X dependency-resolution hot path (BASELINE.json metric:
+"deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X").
+
+One step = one batch of PreAccept.calculatePartialDeps requests resolved on the GPU(s), with
+the requests already resident in HBM when the timed region starts and the PartialDeps CSR
+(keyDeps / rangeDeps / directKeyDeps) left in HBM:
+  K0 encode -> K1 CommandsForKey conflict scan -> K4 range probe -> K2 build (size pass,
+  offsets, emit pass)  [+ for N > 1: all-to-all of per-store partials over RCCL and K3 merge]
+
+Workload at N = 1: config 2 of BASELINE.json (1M txns x 8 Zipf(0.99) keys over 1M keys, 16M-entry
+CommandsForKey history, SNAPSHOT). For N > 1 the same per-GPU shape is scaled weakly (see
+DESIGN.md §6). Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (loads the HIP runtime first; see accord_deps.native.lib)
+
+from accord_deps import _abi as A  # noqa: E402
+from accord_deps import native, synth  # noqa: E402
+
+METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+STAGES = ["K0 encode", "K1 conflict scan", "K4 range probe", "K2 build (size)", "offsets scan", "K2 build (emit)"]
+KERNEL_OF_STAGE = ["k_encode_txn+k_probe_keys", "k_scan", "k_range", "k_build<false>", "k_scan_blocks+sums+add",
+                   "k_build<true>"]
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def to_dev(a, dev):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    return torch.from_numpy(a).to(dev)
+
+
+def device_queries(q, dev):
+    keep = {k: to_dev(getattr(v, f) if f else v, dev) for k, v, f in [
+        ("tm", q.txn, "msb"), ("tl", q.txn, "lsb"), ("tn", q.txn, "node"),
+        ("em", q.exec, "msb"), ("el", q.exec, "lsb"), ("en", q.exec, "node"),
+        ("ko", q.key_off, None), ("k", q.keys, None)]}
+    s = A.AdQuerySoa()
+    s.n_txns = len(q)
+    s.txn_msb, s.txn_lsb, s.txn_node = keep["tm"].data_ptr(), keep["tl"].data_ptr(), keep["tn"].data_ptr()
+    s.exec_msb, s.exec_lsb, s.exec_node = keep["em"].data_ptr(), keep["el"].data_ptr(), keep["en"].data_ptr()
+    s.min_epoch = None
+    s.key_off, s.keys = keep["ko"].data_ptr(), keep["k"].data_ptr()
+    return s, keep
+
+
+def stage_bytes(w, stats):
+    """Algorithmic bytes per pipeline stage and launch.
+    K1 follows SURVEY.md §8(d) config 2: every touched key's CommandsForKey segment read once
+    (17 B per entry + 16 B header) + 12 B per probe, plus its 4 B per emitted txnId.
+    K2 (emit) reads the per-probe lists and writes the CSR: 8 B per key (range) head + 4 B per
+    keysToTxnIds int + 4 B per txnId index."""
+    q = w.queries
+    keys_touched = np.unique(q.keys)
+    pos = np.searchsorted(w.cfk.keys, keys_touched)
+    ok = pos < len(w.cfk.keys)
+    pos = pos[ok]
+    pos = pos[w.cfk.keys[pos] == keys_touched[ok]]
+    seg = w.cfk.seg.astype(np.int64)
+    lk = seg[pos + 1] - seg[pos]
+    pairs = sum(stats["n_pairs"])
+    heads = sum(stats["n_keys"])
+    uniq = sum(stats["n_unique"])
+    b = [0] * 6
+    b[0] = len(q) * (3 * 20 + 8) + q.n_probes * (8 + 4 + 4 + 1)
+    b[1] = int((17 * lk + 16).sum()) + 12 * q.n_probes + 4 * pairs
+    b[2] = 16 * w.cmds.range_off[-1] + q.n_probes * (8 + 4 + 8 + 8)
+    b[3] = 4 * pairs + 16 * q.n_probes + 9 * 4 * len(q)
+    b[4] = 9 * (4 + 8) * len(q)
+    b[5] = 4 * pairs + 16 * q.n_probes + 8 * heads + 4 * (heads + pairs) + 4 * uniq
+    return b
+
+
+def cpu_baseline(w, budget_s=15.0):
+    """The CPU restatement (oracle/refcpu.c, the reference algorithm, one thread = one
+    CommandStore) on a bounded prefix of the same batch, same snapshot."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    st = pyoracle.OracleStore(w.range_start_inclusive, 1, w.slices)
+    st.load(w)
+    n = 16
+    t = 0.0
+    done_pairs = 0
+    first = 0
+    total = len(w.queries)
+    while first < total:
+        cnt = min(n, total - first)
+        t0 = time.perf_counter()
+        st.deps_batch(w.queries, w.flags, first, cnt)
+        dt = time.perf_counter() - t0
+        t += dt
+        done_pairs += int(w.queries.key_off[first + cnt] - w.queries.key_off[first])
+        first += cnt
+        if t >= budget_s:
+            break
+        n = max(1, min(int(n * 2), int(cnt * max(0.1, (budget_s - t) / max(dt, 1e-6)))))
+    st.close()
+    return dict(value=done_pairs / t, unit="txn-key pairs/s", cores=1, kind="port",
+                sample="first %d of %d requests of the same batch (%d txn-key pairs, %.1f s), refcpu = C "
+                       "restatement of the reference Java, 1 thread = 1 CommandStore" % (first, total, done_pairs, t))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests / dry runs)")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        raise SystemExit("multi-GPU bench: see accord_deps.dist (not wired into bench.py yet)")
+
+    s = args.scale
+    t0 = time.time()
+    w = synth.config2(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_hist_entries=int(16_000_000 * s))
+    gen_s = time.time() - t0
+    log("generated config2 in %.1f s: %d keys, %d entries, %d txns, %d probes" %
+        (gen_s, len(w.cfk.keys), w.cfk.n_entries, len(w.queries), w.queries.n_probes))
+
+    store = native.DeviceCommandStore(device=local)
+    store.load(w)
+    qdev, keep = device_queries(w.queries, dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    stats = None
+    for _ in range(args.warmup):
+        _, stats = store.deps_batch_device(qdev, sp)
+    torch.cuda.synchronize(dev)
+    if stats:
+        log("ingest %.1f ms (host dictionary + device index build)" % stats["ms_ingest"])
+
+    stage_ms = np.zeros(6)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        _, stats = store.deps_batch_device(qdev, sp)
+        stage_ms += np.array(stats["ms_stage"][:6])
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t_start
+    stage_ms /= max(args.steps, 1)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+
+    pairs_per_step = w.queries.n_probes
+    value = pairs_per_step * world / (ms_per_step / 1000.0)
+
+    # roofline of the dominant kernel (largest device time per step)
+    dom = int(np.argmax(stage_ms))
+    sbytes = stage_bytes(w, stats)
+    achieved = sbytes[dom] / (stage_ms[dom] / 1000.0) / 1e9 if stage_ms[dom] > 0 else 0.0
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "txn-key pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "config2: %d txns x 8 Zipf(0.99) keys over %d keys, %d-entry CommandsForKey "
+                               "history, SNAPSHOT, 1 CommandStore per GPU" % (len(w.queries), int(1_000_000 * s),
+                                                                               w.cfk.n_entries),
+                   "txns_per_step": len(w.queries), "txn_key_pairs_per_step": pairs_per_step,
+                   "parallelism": "store-per-gpu x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": KERNEL_OF_STAGE[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": sbytes[dom], "launch_ms": stage_ms[dom]},
+        "stages_ms": {STAGES[i]: round(float(stage_ms[i]), 4) for i in range(6)},
+        "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
+        "ingest_ms": stats["ms_ingest"],
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    store.close()
+
+
+if __name__ == "__main__":
+    main()

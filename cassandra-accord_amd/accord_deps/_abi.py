@@ -70,7 +70,7 @@ class AdQuerySoa(C.Structure):
 
 class AdStats(C.Structure):
     _fields_ = [("n_txns", C.c_uint64), ("n_probes", C.c_uint64), ("n_pairs", C.c_uint64 * NMAPS),
-                ("n_unique", C.c_uint64 * NMAPS), ("scan_entries", C.c_uint64),
+                ("n_unique", C.c_uint64 * NMAPS), ("n_keys", C.c_uint64 * NMAPS), ("scan_entries", C.c_uint64),
                 ("ms_device", C.c_double), ("ms_ingest", C.c_double),
                 ("ms_stage", C.c_double * 8), ("bytes_stage", C.c_uint64 * 8)]
 

@@ -19,7 +19,7 @@ from .model import DepsMap, PartialDepsBatch, Tids
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaccord_deps.so")
 
 EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error", "ad_cfk_load",
-           "ad_range_cmds_load", "ad_redundant_load", "ad_deps_batch", "ad_result_free",
+           "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_levels")
 
 
@@ -53,6 +53,7 @@ def lib():
         L.ad_cfk_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkSoa)]
         L.ad_range_cmds_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsSoa)]
         L.ad_redundant_load.argtypes = [C.c_void_p, C.POINTER(A.AdRedundantSoa)]
+        L.ad_prepare.argtypes = [C.c_void_p]
         L.ad_deps_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.POINTER(C.POINTER(A.AdDepsResult))]
         L.ad_result_free.argtypes = [C.POINTER(A.AdDepsResult)]
         L.ad_deps_batch_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_void_p,
@@ -73,6 +74,7 @@ def _view(p, n, dtype):
 
 def stats_dict(s):
     return dict(n_txns=s.n_txns, n_probes=s.n_probes, n_pairs=list(s.n_pairs), n_unique=list(s.n_unique),
+                n_keys=list(s.n_keys),
                 ms_device=s.ms_device, ms_ingest=s.ms_ingest, ms_stage=list(s.ms_stage)[:6],
                 bytes_stage=list(s.bytes_stage)[:6])
 
@@ -111,11 +113,13 @@ class DeviceCommandStore:
         if rc:
             raise AccordDepsError(rc, lib().ad_last_error(self.h).decode())
 
-    def load(self, workload):
+    def load(self, workload, prepare=True):
         L = lib()
         self._check(L.ad_cfk_load(self.h, C.byref(workload.cfk.soa())))
         self._check(L.ad_range_cmds_load(self.h, C.byref(workload.cmds.soa())))
         self._check(L.ad_redundant_load(self.h, C.byref(workload.redundant.soa())))
+        if prepare:
+            self._check(L.ad_prepare(self.h))
         return self
 
     def dictionary(self):

@@ -140,10 +140,12 @@ def config1(n_txns=10_000, keys_per_txn=4, n_keys=1_000, seed=0xACC0D001):
 
 
 def config2(n_txns=1_000_000, keys_per_txn=8, n_keys=1_000_000, n_hist_entries=16_000_000, zipf_s=0.99,
-            seed=0xACC0D002, sync_frac=0.02, esp_frac=0.01, tail_unapplied=4):
+            seed=0xACC0D002, sync_frac=0.02, esp_frac=0.0, tail_unapplied=4):
     """Config 2: 1M txns x 8 Zipf(0.99) keys over 1M keys, 16M-entry CFK history (2M history txns x 8
-    keys), SNAPSHOT. 2% of history is SyncPoint (directKeyDeps); 1% of queries are key-domain
-    ExclusiveSyncPoints, the only kind that witnesses SyncPoints (Txn.java:221-235)."""
+    keys), SNAPSHOT, Read/Write requests 50/50. 2% of history is SyncPoint; only key-domain
+    ExclusiveSyncPoint requests witness SyncPoints (Txn.java:221-235), so `esp_frac` > 0 adds those
+    (directKeyDeps; each one returns every SyncPoint of its keys). Default 0: BASELINE config 2
+    specifies Read/Write requests only."""
     rng = np.random.default_rng(seed)
     z = Zipf(n_keys, zipf_s)
     token = key_tokens(n_keys, seed)

@@ -741,6 +741,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         {
             S.n_pairs[m] = tot[3 * m + 2] - tot[3 * m + 0];
             S.n_unique[m] = tot[3 * m + 1];
+            S.n_keys[m] = tot[3 * m + 0];
         }
         float ms;
         const int pairs[6][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}};
@@ -919,6 +920,14 @@ int ad_redundant_load(ad_ctx* c, const ad_redundant_soa* in)
     for (uint64_t i = 0; i < n; ++i) B.wm[i] = {in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
     c->dirty = true;
     return AD_OK;
+}
+
+int ad_prepare(ad_ctx* c)
+{
+    if (!c) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    return c->dirty ? build_snapshot(c) : AD_OK;
 }
 
 int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_result** out)

@@ -355,9 +355,10 @@ __global__ __launch_bounds__(256) void k_scan(DevSnapshot s, BatchBufs b)
         }
         if (lane == 0)
         {
-            b.p_off[p] = (uint32_t)off;
-            b.p_c0[p] = tot0;
-            b.p_c1[p] = c1;
+            // on arena overflow record an empty list (the host grows the arena and reruns)
+            b.p_off[p] = fits ? (uint32_t)off : 0u;
+            b.p_c0[p] = fits ? tot0 : 0u;
+            b.p_c1[p] = fits ? c1 : 0u;
         }
     }
 }
@@ -457,7 +458,12 @@ __global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
             wave_lds_sync();
             cnt = cursor;
             off = alloc.take(&b.ctl->rng_top, cap, &b.ctl->overflow, 2u, cnt, K4_CHUNK);
-            if (off + cnt <= cap)
+            if (off + cnt > cap)
+            {
+                off = 0;
+                cnt = 0;                 // overflow: the host grows the arena and reruns
+            }
+            else
             {
                 if (!overflow)
                 {

@@ -175,6 +175,7 @@ typedef struct ad_stats {
     uint64_t n_txns, n_probes;
     uint64_t n_pairs[AD_NMAPS];      /* txn-key (or txn-range) pairs emitted per map         */
     uint64_t n_unique[AD_NMAPS];     /* sum over txns of unique txnIds per map               */
+    uint64_t n_keys[AD_NMAPS];       /* sum over txns of keys (ranges) with >= 1 dep per map  */
     uint64_t scan_entries;           /* CFK entries a reference scan would visit (sum of end) */
     double   ms_device;              /* device time of the resolve pipeline                  */
     double   ms_ingest;
@@ -215,6 +216,9 @@ const char* ad_last_error(const ad_ctx* ctx);
 int ad_cfk_load(ad_ctx* ctx, const ad_cfk_soa* cfk);
 int ad_range_cmds_load(ad_ctx* ctx, const ad_range_cmds_soa* cmds);
 int ad_redundant_load(ad_ctx* ctx, const ad_redundant_soa* rb);
+/* Build the id dictionary and device indexes of the loaded snapshot now (otherwise the first
+ * batch does it). Ingest time is reported in ad_stats.ms_ingest, never in ms_device. */
+int ad_prepare(ad_ctx* ctx);
 
 /* ---- batch resolve, host buffers in / host result out ------------------------------ */
 int  ad_deps_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t flags, ad_deps_result** out);
