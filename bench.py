@@ -30,9 +30,8 @@ from accord_deps import native, synth  # noqa: E402
 
 METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-STAGES = ["K0 encode", "K1 conflict scan", "K4 range probe", "K2 build (size)", "offsets scan", "K2 build (emit)"]
-KERNEL_OF_STAGE = ["k_encode_txn+k_probe_keys", "k_scan", "k_range", "k_build<false>", "k_scan_blocks+sums+add",
-                   "k_build<true>"]
+STAGES = ["K0 encode", "K1 conflict scan", "K4 range probe", "K2 build", "offsets scan", "pack"]
+KERNEL_OF_STAGE = ["k_encode_txn+k_probe_keys", "k_scan", "k_range", "k_build", "k_scan_blocks+sums+add", "k_pack"]
 
 
 def log(*a):
@@ -81,9 +80,9 @@ def stage_bytes(w, stats):
     b[0] = len(q) * (3 * 20 + 8) + q.n_probes * (8 + 4 + 4 + 1)
     b[1] = int((17 * lk + 16).sum()) + 12 * q.n_probes + 4 * pairs
     b[2] = 16 * w.cmds.range_off[-1] + q.n_probes * (8 + 4 + 8 + 8)
-    b[3] = 4 * pairs + 16 * q.n_probes + 9 * 4 * len(q)
+    b[3] = 4 * pairs + 24 * q.n_probes + 8 * heads + 4 * (heads + pairs) + 4 * uniq + 9 * 4 * len(q)
     b[4] = 9 * (4 + 8) * len(q)
-    b[5] = 4 * pairs + 16 * q.n_probes + 8 * heads + 4 * (heads + pairs) + 4 * uniq
+    b[5] = 2 * (8 * heads + 4 * (heads + pairs) + 4 * uniq) + 9 * 12 * len(q)
     return b
 
 

@@ -180,7 +180,7 @@ struct ad_ctx {
     std::vector<int32_t> dict_node;
     std::vector<int64_t> rt_start, rt_end;     // range table (distinct ranges, by Range.compare)
     DevSnapshot ds{};
-    DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_seg, d_woff, d_maw, d_pruned, d_ent, d_w;
+    DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_krec, d_ent, d_w;
     DevBuf d_lvl[NCLASS][MAX_LEVELS];
     DevBuf d_rstart, d_rend, d_rtxw, d_rrid;
     DevBuf d_rlvl[NCLASS][MAX_LEVELS];
@@ -188,11 +188,11 @@ struct ad_ctx {
 
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
-    DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_key, p_slice;
+    DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec;
     DevBuf arena, p_off, p_c0, p_c1, rarena, p_roff, p_rcnt, p_rb;
-    DevBuf sz, off, bsum, t_scr, scratch, ctl;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
-    uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0;
+    uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
 
     int fail(int code, const char* fmt, ...)
@@ -462,9 +462,21 @@ static int build_snapshot(ad_ctx* c)
 
     // ---- 4. upload CFK + dictionary, build the trees
     int rc;
+    std::vector<KeyRec> krec(nk);
+    for (uint64_t k = 0; k < nk; ++k)
+    {
+        KeyRec& r = krec[k];
+        r.seg_lo = seg32[k];
+        r.seg_hi = seg32[k + 1];
+        r.w_lo = woff[k];
+        r.w_hi = woff[k + 1];
+        r.last_txn = r.seg_hi > r.seg_lo ? (ent[r.seg_hi - 1].y & RANK_MASK) : 0u;
+        r.last_wexec = r.w_hi > r.w_lo ? w[r.w_hi - 1].x : 0u;
+        r.pruned = pruned[k];
+        r.maw = maw[k];
+    }
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
-        (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_seg, seg32)) || (rc = upload(c, c->d_woff, woff)) ||
-        (rc = upload(c, c->d_maw, maw)) || (rc = upload(c, c->d_pruned, pruned)) || (rc = upload(c, c->d_ent, ent)) ||
+        (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_ent, ent)) ||
         (rc = upload(c, c->d_w, w)) || (rc = upload(c, c->d_slices_s, c->slice_s)) || (rc = upload(c, c->d_slices_e, c->slice_e)))
         return rc;
 
@@ -476,10 +488,7 @@ static int build_snapshot(ad_ctx* c)
     s.n_dict = dhi.size();
     s.n_keys = nk;
     s.keys = c->d_keys.as<int64_t>();
-    s.seg = c->d_seg.as<uint32_t>();
-    s.woff = c->d_woff.as<uint32_t>();
-    s.maw = c->d_maw.as<int32_t>();
-    s.pruned = c->d_pruned.as<uint32_t>();
+    s.krec = c->d_krec.as<KeyRec>();
     s.n_ent = ne;
     s.ent = c->d_ent.as<uint2>();
     s.w = c->d_w.as<uint2>();
@@ -656,39 +665,45 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     b.q_min_epoch = q->min_epoch; b.q_key_off = q->key_off; b.q_keys = q->keys;
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->t_S, n) || !ens<uint32_t>(c->t_self, n) || !ens<uint32_t>(c->t_kinds, n) ||
-        !ens<int64_t>(c->t_epoch, n) || !ens<uint32_t>(c->p_txn, np) || !ens<int32_t>(c->p_key, np) ||
-        !ens<uint8_t>(c->p_slice, np) || !ens<uint32_t>(c->p_off, np) || !ens<uint32_t>(c->p_c0, np) ||
+        !ens<int64_t>(c->t_epoch, n) || !ens<uint32_t>(c->p_txn, np) || !ens<uint4>(c->p_rec, np) ||
+        !ens<uint32_t>(c->p_off, np) || !ens<uint32_t>(c->p_c0, np) ||
         !ens<uint32_t>(c->p_c1, np) || !ens<uint32_t>(c->p_roff, np) || !ens<uint32_t>(c->p_rcnt, np) ||
         !ens<uint64_t>(c->p_rb, np) || !ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) ||
-        !ens<uint64_t>(c->bsum, 9 * nb) || !ens<uint64_t>(c->t_scr, n) || !ens<BatchCtl>(c->ctl, 1))
+        !ens<uint64_t>(c->bsum, 9 * nb) || !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1))
         return c->fail(AD_E_NOMEM, "batch buffers");
     b.t_S = c->t_S.as<uint32_t>(); b.t_self = c->t_self.as<uint32_t>(); b.t_kinds = c->t_kinds.as<uint32_t>();
-    b.t_epoch = c->t_epoch.as<int64_t>(); b.p_txn = c->p_txn.as<uint32_t>(); b.p_key = c->p_key.as<int32_t>();
-    b.p_slice = c->p_slice.as<uint8_t>(); b.p_off = c->p_off.as<uint32_t>(); b.p_c0 = c->p_c0.as<uint32_t>();
+    b.t_epoch = c->t_epoch.as<int64_t>(); b.p_txn = c->p_txn.as<uint32_t>(); b.p_rec = c->p_rec.as<uint4>();
+    b.p_off = c->p_off.as<uint32_t>(); b.p_c0 = c->p_c0.as<uint32_t>();
     b.p_c1 = c->p_c1.as<uint32_t>(); b.p_roff = c->p_roff.as<uint32_t>(); b.p_rcnt = c->p_rcnt.as<uint32_t>();
     b.p_rb = c->p_rb.as<uint64_t>(); b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>();
-    b.bsum = c->bsum.as<uint64_t>(); b.t_scr = c->t_scr.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>();
+    b.bsum = c->bsum.as<uint64_t>(); b.t_reg = c->t_reg.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>();
 
     const uint64_t waves = (uint64_t)device_cu_count() * 8 * 4;
+    const uint64_t k2_waves = (uint64_t)device_cu_count() * 16;
     uint64_t want_key = std::max<uint64_t>(np * 4 + waves * 4096, 1u << 20);
     uint64_t want_rng = c->ds.n_rent ? std::max<uint64_t>(np * 2 + waves * 2048, 1u << 20) : 1;
     uint64_t want_scr = 64ull << 20;
+    uint64_t want_reg = std::max<uint64_t>(n * 3 * 8 + np * 24 + k2_waves * (3ull << 16), 16ull << 20);
     if (c->key_cap < want_key) c->key_cap = want_key;
     if (c->rng_cap < want_rng) c->rng_cap = want_rng;
     if (c->scr_cap < want_scr) c->scr_cap = want_scr;
+    if (c->reg_cap < want_reg) c->reg_cap = want_reg;
 
-    for (int attempt = 0; attempt < 6; ++attempt)
+    for (int attempt = 0; attempt < 8; ++attempt)
     {
         if (!c->arena.ensure(sizeof(uint32_t) * c->key_cap)) return c->fail(AD_E_NOMEM, "key arena %llu", (unsigned long long)c->key_cap);
         if (!c->rarena.ensure(sizeof(uint64_t) * c->rng_cap)) return c->fail(AD_E_NOMEM, "range arena");
         if (!c->scratch.ensure(c->scr_cap)) return c->fail(AD_E_NOMEM, "scratch");
+        if (!c->reg.ensure(c->reg_cap)) return c->fail(AD_E_NOMEM, "region arena");
         b.arena = c->arena.as<uint32_t>();
         b.rarena = c->rarena.as<uint64_t>();
         b.scratch = c->scratch.as<uint8_t>();
+        b.reg = c->reg.as<uint8_t>();
         BatchCtl h{};
         h.key_cap = c->key_cap;
         h.rng_cap = c->rng_cap;
         h.scr_cap = c->scr_cap;
+        h.reg_cap = c->reg_cap;
         HIPCHK(c, hipMemcpyAsync(b.ctl, &h, sizeof(h), hipMemcpyHostToDevice, st));
         HIPCHK(c, hipEventRecord(c->ev[0], st));
         HIPCHK(c, run_encode(c->ds, b, st));
@@ -697,7 +712,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipEventRecord(c->ev[2], st));
         HIPCHK(c, run_range(c->ds, b, st));
         HIPCHK(c, hipEventRecord(c->ev[3], st));
-        HIPCHK(c, run_build(c->ds, b, false, st));
+        HIPCHK(c, run_build(c->ds, b, st));
         HIPCHK(c, hipEventRecord(c->ev[4], st));
         HIPCHK(c, run_offsets(b, st));
         HIPCHK(c, hipEventRecord(c->ev[5], st));
@@ -717,6 +732,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             if (h.overflow & 1u) c->key_cap = std::max<uint64_t>(c->key_cap * 2, h.key_top + (h.key_top >> 1));
             if (h.overflow & 2u) c->rng_cap = std::max<uint64_t>(c->rng_cap * 2, h.rng_top + (h.rng_top >> 1));
             if (h.overflow & 4u) c->scr_cap = std::max<uint64_t>(c->scr_cap * 2, h.scr_top + (h.scr_top >> 1));
+            if (h.overflow & 8u) c->reg_cap = std::max<uint64_t>(c->reg_cap * 2, h.reg_top + (h.reg_top >> 1));
             continue;
         }
         for (int m = 0; m < 3; ++m)
@@ -729,7 +745,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             b.o_k2t[m] = c->o_k2t[m].as<int32_t>();
         }
         HIPCHK(c, hipEventRecord(c->ev[6], st));
-        HIPCHK(c, run_build(c->ds, b, true, st));
+        HIPCHK(c, run_pack(b, st));
         HIPCHK(c, hipEventRecord(c->ev[7], st));
         HIPCHK(c, hipStreamSynchronize(st));
 
@@ -754,13 +770,6 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         }
         S.ms_device = total;
         S.ms_ingest = c->ms_ingest;
-        // algorithmic bytes
-        S.bytes_stage[0] = n * (2 * 20 + 8) + np * (8 + 4 + 4 + 1);
-        S.bytes_stage[1] = np * (4 + 4 + 4 + 4 + 12) + (S.n_pairs[0] + S.n_pairs[2]) * 4;
-        S.bytes_stage[2] = np * (8 + 4 + 4 + 16);
-        S.bytes_stage[5] = (S.n_pairs[0] + S.n_pairs[1] + S.n_pairs[2]) * 4 * 2 +
-                           (S.n_unique[0] + S.n_unique[1] + S.n_unique[2]) * 4 +
-                           (tot[0] + tot[3] + tot[6]) * 12;
         out->n_txns = n;
         for (int m = 0; m < 3; ++m)
         {

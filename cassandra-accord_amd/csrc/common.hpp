@@ -74,6 +74,20 @@ __host__ __device__ inline int norm_cmp(const NormTid& a, const NormTid& b)
     return 0;
 }
 
+// Per-key record of the CommandsForKey index (one 32-byte load per probe).
+struct KeyRec {
+    uint32_t seg_lo, seg_hi;       // byId entries [seg_lo, seg_hi) in ent
+    uint32_t w_lo, w_hi;           // committed Writes by executeAt [w_lo, w_hi) in w
+    uint32_t last_txn;             // rank of byId[seg_hi-1] (0 if empty): tail fast path of insertPos
+    uint32_t last_wexec;           // w[w_hi-1].x (0 if none): tail fast path of maxCommittedWriteBefore
+    uint32_t pruned;               // rank of prunedBefore, 0 = NONE
+    int32_t  maw;                  // absolute index into w of maxAppliedWriteByExecuteAt, -1 = none
+};
+
+// Per-probe record written by K0: {key index (NO_KEY if absent/outside the slice), S rank,
+// self rank (0 = none), kinds | class << 8 | in_slice << 12}
+constexpr uint32_t NO_KEY = 0xFFFFFFFFu;
+
 // Per-store device snapshot, passed to kernels by value.
 struct DevSnapshot {
     // id dictionary (normalised)
@@ -84,10 +98,7 @@ struct DevSnapshot {
     // CommandsForKey
     uint64_t n_keys;
     const int64_t*  keys;          // [n_keys]
-    const uint32_t* seg;           // [n_keys+1] into ent
-    const uint32_t* woff;          // [n_keys+1] into w
-    const int32_t*  maw;           // [n_keys] index (absolute, into w) of maxAppliedWriteByExecuteAt, -1
-    const uint32_t* pruned;        // [n_keys] rank of prunedBefore, 0 = NONE
+    const KeyRec*   krec;          // [n_keys]
     uint64_t n_ent;
     const uint2*    ent;           // {tau, txw}
     const uint2*    w;             // committed Writes by executeAt: {exec rank, txn rank}

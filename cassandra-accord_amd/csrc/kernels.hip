@@ -169,10 +169,11 @@ __global__ void k_probe_keys(DevSnapshot s, BatchBufs b)
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= b.n_probes) return;
     const int64_t key = b.q_keys[p];
+    const uint32_t t = b.p_txn[p];
     bool in_slice = s.n_slices == 0;
     for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
         in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
-    int32_t ki = -1;
+    uint32_t ki = NO_KEY;
     if (in_slice)
     {
         uint64_t lo = 0, hi = s.n_keys;
@@ -182,10 +183,9 @@ __global__ void k_probe_keys(DevSnapshot s, BatchBufs b)
             if (s.keys[mid] < key) lo = mid + 1;
             else hi = mid;
         }
-        if (lo < s.n_keys && s.keys[lo] == key) ki = (int32_t)lo;   // ifLoadedAndInitialised(key) != null
+        if (lo < s.n_keys && s.keys[lo] == key) ki = (uint32_t)lo;   // ifLoadedAndInitialised(key) != null
     }
-    b.p_key[p] = ki;
-    b.p_slice[p] = in_slice ? 1 : 0;
+    b.p_rec[p] = make_uint4(ki, b.t_S[t], b.t_self[t], b.t_kinds[t] | (in_slice ? (1u << 12) : 0u));
 }
 
 hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
@@ -238,40 +238,52 @@ __global__ __launch_bounds__(256) void k_scan(DevSnapshot s, BatchBufs b)
 
     for (uint64_t p = (uint64_t)blockIdx.x * K1_WAVES + wv; p < b.n_probes; p += nw)
     {
-        const int32_t ki = b.p_key[p];
-        if (ki < 0)
+        const uint4 pr = b.p_rec[p];
+        const uint32_t ki = pr.x;
+        if (ki == NO_KEY)
         {
             if (lane == 0) { b.p_off[p] = 0; b.p_c0[p] = 0; b.p_c1[p] = 0; }
             continue;
         }
-        const uint32_t t = b.p_txn[p];
-        const uint32_t S = b.t_S[t], self = b.t_self[t], tk = b.t_kinds[t];
-        const uint32_t kinds = tk & 0xFF;
-        const int cls = (tk >> 8) & 3;
-        const uint64_t lo = s.seg[ki], hi = s.seg[ki + 1];
+        const uint32_t S = pr.y, self = pr.z;
+        const uint32_t kinds = pr.w & 0xFF;
+        const int cls = (pr.w >> 8) & 3;
+        const KeyRec kr = s.krec[ki];
+        const uint64_t lo = kr.seg_lo, hi = kr.seg_hi;
 
-        // end = insertPos(startedBefore)  (CommandsForKey.java:912, :1358-1363)
-        const uint64_t end = wave_lower_bound(lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
-                                              [&](uint32_t v) { return v < S; });
+        // end = insertPos(startedBefore)  (CommandsForKey.java:912, :1358-1363); tail fast path
+        const uint64_t end = (hi == lo || kr.last_txn < S)
+                                 ? hi
+                                 : wave_lower_bound(lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
+                                                    [&](uint32_t v) { return v < S; });
 
         // maxCommittedWriteBefore (:913-928): executeAt of the last committed Write before S
-        const uint64_t wlo = s.woff[ki], whi = s.woff[ki + 1];
-        uint32_t M = 1;                      // "none": every live entry passes tau >= 1
+        const uint64_t wlo = kr.w_lo, whi = kr.w_hi;
         uint64_t wpos = wlo;
+        uint32_t wprev = 0;
         if (whi > wlo)
-            wpos = wave_lower_bound(wlo, whi, [&](uint64_t i) { return s.w[i].x; }, [&](uint32_t v) { return v < S; });
-        if (s.elide && wpos > wlo) M = s.w[wpos - 1].x;
+        {
+            if (kr.last_wexec < S)
+            {
+                wpos = whi;
+                wprev = kr.last_wexec;
+            }
+            else
+            {
+                wpos = wave_lower_bound(wlo, whi, [&](uint64_t i) { return s.w[i].x; }, [&](uint32_t v) { return v < S; });
+                if (wpos > wlo) wprev = s.w[wpos - 1].x;
+            }
+        }
+        const uint32_t M = (s.elide && wpos > wlo) ? wprev : 1u;   // 1: "none", every live entry passes
 
         // prunedBefore substitute (:952-965): first Write at/after S, clamped to maxAppliedWrite
         uint32_t extra = 0;
-        const uint32_t pr = s.pruned[ki];
-        if (pr != 0 && S <= pr)
+        if (kr.pruned != 0 && S <= kr.pruned)
         {
-            const int32_t maw = s.maw[ki];
-            if (maw < 0) { if (lane == 0) set_error(b.ctl, ERR_STATE); }
+            if (kr.maw < 0) { if (lane == 0) set_error(b.ctl, ERR_STATE); }
             else
             {
-                const uint64_t idx = wpos <= (uint64_t)maw ? wpos : (uint64_t)maw;
+                const uint64_t idx = wpos <= (uint64_t)kr.maw ? wpos : (uint64_t)kr.maw;
                 extra = s.w[idx].y;
                 if (extra == self) extra = 0;                      // map lambda, PreAccept.java:258
             }
@@ -393,7 +405,7 @@ __global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
     for (uint64_t p = (uint64_t)blockIdx.x * K4_WAVES + wv; p < b.n_probes; p += nw)
     {
         const int64_t x = b.q_keys[p];
-        const uint32_t t = b.p_txn[p];
+        const uint4 pr = b.p_rec[p];
         // RedundantBefore.collectDeps over the request's keys (not sliced), RedundantBefore.java:420-423
         uint64_t rbv = NO_RB;
         if (s.n_rb)
@@ -406,6 +418,7 @@ __global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
                 if (range_contains(s.start_inclusive, s.rb_start[e], s.rb_end[e], x))
                 {
                     // Entry.outOfBounds(minEpoch, executeAt) :262-265; watermark > NONE :188
+                    const uint32_t t = b.p_txn[p];
                     const int64_t ep = b.t_epoch[t];
                     const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
                     const uint32_t wm = s.rb_wm[e];
@@ -417,11 +430,11 @@ __global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
 
         uint32_t cnt = 0;
         uint64_t off = 0;
-        if (b.p_slice[p] && s.n_rent)
+        if (((pr.w >> 12) & 1) && s.n_rent)
         {
-            const uint32_t S = b.t_S[t], self = b.t_self[t], tk = b.t_kinds[t];
-            const uint32_t kinds = tk & 0xFF;
-            const int cls = (tk >> 8) & 3;
+            const uint32_t S = pr.y, self = pr.z;
+            const uint32_t kinds = pr.w & 0xFF;
+            const int cls = (pr.w >> 8) & 3;
             // candidate commands: range start before the key (Range.compareTo, Range.java:40-100)
             const uint64_t hi = wave_lower_bound(0, s.n_rent, [&](uint64_t i) { return s.r_start[i]; },
                                                  [&](int64_t v) { return incl ? v <= x : v < x; });
@@ -495,6 +508,13 @@ __global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
 hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_probes) return hipSuccess;
+    if (s.n_rent == 0 && s.n_rb == 0)
+    {
+        // no range commands and no redundant-before entries: every probe's range list is empty
+        hipError_t e = hipMemsetAsync(b.p_rcnt, 0, sizeof(uint32_t) * b.n_probes, st);
+        if (e == hipSuccess) e = hipMemsetAsync(b.p_rb, 0xFF, sizeof(uint64_t) * b.n_probes, st);
+        return e;
+    }
     const uint64_t blocks_needed = (b.n_probes + K4_WAVES - 1) / K4_WAVES;
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
     k_range<<<grid, 256, 0, st>>>(s, b);
@@ -509,24 +529,57 @@ hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 //   P               = exclusive prefix of kept over the concatenation
 //   urank(x)        = sum_b (P[lb_b(x)] - P[st_b])     = number of distinct values < x
 // so values[urank(x)] = x for kept x, and urank(x) is the keysToTxnIds body entry of x
-// (RelationMultiMap.java:245-257). One wave per request; lists staged in LDS, or in global
-// scratch when a request is too large for LDS.
+// (RelationMultiMap.java:245-257). One wave per request, single pass: every list is gathered
+// with one cooperative load per 64 elements, merged in LDS (global scratch when too large),
+// and the three maps are written to a chunk-allocated region that k_pack later compacts.
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t K2_MAXP = 64;     // probes per request on the LDS path
 constexpr uint32_t K2_CAP = 512;     // elements per list family on the LDS path
+constexpr uint32_t K2_REGION_CHUNK = 1u << 16;
 
 struct K2Mem {
-    uint32_t* st;      // [2*np + 2] list starts
-    uint64_t* V;       // [cap] elements (u32 ranks widened, or (rid<<32 | rank) pairs)
+    // per-probe metadata
+    uint32_t* off; uint32_t* c0; uint32_t* c1; uint32_t* roff; uint32_t* rcnt; uint64_t* rb;
+    uint32_t* st0; uint32_t* st1; uint32_t* stR;      // [np+1], [np+1], [2np+1]
+    uint64_t* V;       // [cap] elements
     uint32_t* P;       // [cap + 1]
     uint64_t* UP;      // [cap] unique pairs
     uint32_t* gst;     // [cap + 1] rid group starts
     uint32_t* P2;      // [cap + 1]
 };
 
-__device__ __forceinline__ uint64_t k2_lds_bytes()
+constexpr size_t k2_lds_bytes()
 {
-    return (uint64_t)(2 * K2_MAXP + 2) * 4 + (uint64_t)K2_CAP * 8 * 2 + (uint64_t)(K2_CAP + 1) * 4 * 3;
+    return (size_t)K2_MAXP * (4 * 5 + 8) + (size_t)(2 * (K2_MAXP + 1) + 2 * K2_MAXP + 1) * 4 + 4 /*align*/ +
+           (size_t)K2_CAP * 8 * 2 + (size_t)(K2_CAP + 1) * 4 * 3;
+}
+
+__device__ __forceinline__ uint64_t k2_scratch_bytes(uint32_t np, uint32_t capn)
+{
+    uint64_t b = (uint64_t)np * 8 + (uint64_t)np * 4 * 5 + (uint64_t)(2 * (np + 1) + 2 * np + 1) * 4;
+    b = (b + 7) & ~7ull;
+    b += (uint64_t)capn * 16 + (uint64_t)(capn + 1) * 12;
+    return (b + 7) & ~7ull;
+}
+
+__device__ __forceinline__ void k2_carve(K2Mem& m, uint8_t* base, uint32_t np, uint32_t capn)
+{
+    m.rb = reinterpret_cast<uint64_t*>(base);
+    m.off = reinterpret_cast<uint32_t*>(m.rb + np);
+    m.c0 = m.off + np;
+    m.c1 = m.c0 + np;
+    m.roff = m.c1 + np;
+    m.rcnt = m.roff + np;
+    m.st0 = m.rcnt + np;
+    m.st1 = m.st0 + (np + 1);
+    m.stR = m.st1 + (np + 1);
+    uint8_t* q = reinterpret_cast<uint8_t*>(m.stR + (2 * np + 1));
+    q = reinterpret_cast<uint8_t*>(((uintptr_t)q + 7) & ~(uintptr_t)7);
+    m.V = reinterpret_cast<uint64_t*>(q);
+    m.UP = m.V + capn;
+    m.P = reinterpret_cast<uint32_t*>(m.UP + capn);
+    m.gst = m.P + (capn + 1);
+    m.P2 = m.gst + (capn + 1);
 }
 
 template <class Get>
@@ -552,6 +605,23 @@ __device__ __forceinline__ uint32_t list_of(const uint32_t* st, uint32_t n, uint
         else hi = mid;
     }
     return lo;
+}
+
+// exclusive wave scan of cnt(i), i < n, into st[0..n]; returns total
+template <class Cnt>
+__device__ __forceinline__ uint32_t wave_list_starts(uint32_t n, Cnt cnt, uint32_t* st)
+{
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64)
+    {
+        const uint32_t i = i0 + lane_id();
+        const uint32_t c = i < n ? cnt(i) : 0u;
+        const uint32_t inc = wave_incl_scan(c);
+        if (i < n) st[i] = carry + inc - c;
+        carry += __shfl(inc, 63, 64);
+    }
+    if (lane_id() == 0) st[n] = carry;
+    return carry;
 }
 
 __device__ __forceinline__ void wave_excl_scan_inplace(uint32_t* P, uint32_t n)
@@ -598,7 +668,7 @@ __device__ __forceinline__ uint32_t rank_merge_kept(Get get, const uint32_t* st,
     return uniform(P[total]);
 }
 
-// after rank_merge_kept: unique rank of element e
+// after rank_merge_kept: unique rank of value x
 template <class Get>
 __device__ __forceinline__ uint32_t rank_merge_urank(Get get, const uint32_t* st, uint32_t nl, const uint32_t* P, uint64_t x)
 {
@@ -611,28 +681,40 @@ __device__ __forceinline__ uint32_t rank_merge_urank(Get get, const uint32_t* st
     return sum;
 }
 
-struct BuildSizes { uint32_t nk, nv, nk2t; };
-
 __device__ __forceinline__ uint32_t dict_index(uint32_t rank) { return (rank - 1) >> 1; }
 
-template <bool EMIT>
+// region of one map of one request: [keys i64 x nk][txns u32 x U][k2t i32 x (nk + pairs)]
+__device__ __forceinline__ uint64_t region_bytes(uint32_t nk, uint32_t U, uint32_t pairs)
+{
+    return ((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + pairs) * 4 + 7) & ~7ull;
+}
+
 __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
 {
     extern __shared__ uint64_t lds_raw[];
     const uint32_t lane = lane_id();
     const uint64_t n = b.n_txns;
+    ChunkAlloc ralloc;
     for (uint64_t t = blockIdx.x; t < n; t += gridDim.x)
     {
         const uint64_t p0 = b.q_key_off[t];
         const uint32_t np = (uint32_t)(b.q_key_off[t + 1] - p0);
 
-        // totals over the request's probes
+        // one round trip for the request's probe metadata (lane = probe when np <= 64)
+        uint32_t r_off = 0, r_c0 = 0, r_c1 = 0, r_roff = 0, r_rcnt = 0;
+        uint64_t r_rb = NO_RB;
         uint32_t tot0 = 0, tot1 = 0, totR = 0;
         for (uint32_t i = lane; i < np; i += 64)
         {
-            tot0 += b.p_c0[p0 + i];
-            tot1 += b.p_c1[p0 + i];
-            totR += b.p_rcnt[p0 + i] + (b.p_rb[p0 + i] != NO_RB ? 1u : 0u);
+            r_off = b.p_off[p0 + i];
+            r_c0 = b.p_c0[p0 + i];
+            r_c1 = b.p_c1[p0 + i];
+            r_roff = b.p_roff[p0 + i];
+            r_rcnt = b.p_rcnt[p0 + i];
+            r_rb = b.p_rb[p0 + i];
+            tot0 += r_c0;
+            tot1 += r_c1;
+            totR += r_rcnt + (r_rb != NO_RB ? 1u : 0u);
         }
         tot0 = uniform(wave_sum(tot0));
         tot1 = uniform(wave_sum(tot1));
@@ -643,108 +725,96 @@ __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
         K2Mem mem;
         if (!big)
         {
-            uint8_t* base = reinterpret_cast<uint8_t*>(lds_raw);
-            mem.V = reinterpret_cast<uint64_t*>(base);
-            mem.UP = mem.V + K2_CAP;
-            mem.P = reinterpret_cast<uint32_t*>(mem.UP + K2_CAP);
-            mem.gst = mem.P + (K2_CAP + 1);
-            mem.P2 = mem.gst + (K2_CAP + 1);
-            mem.st = mem.P2 + (K2_CAP + 1);
+            k2_carve(mem, reinterpret_cast<uint8_t*>(lds_raw), K2_MAXP, K2_CAP);
+            if (lane < np)
+            {
+                mem.off[lane] = r_off; mem.c0[lane] = r_c0; mem.c1[lane] = r_c1;
+                mem.roff[lane] = r_roff; mem.rcnt[lane] = r_rcnt; mem.rb[lane] = r_rb;
+            }
         }
         else
         {
-            // scratch: st[2np+2] u32, V/UP [capn] u64, P/gst/P2 [capn+1] u32 (8-byte aligned)
-            const uint64_t bytes = ((uint64_t)(2 * np + 2) * 4 + 7) / 8 * 8 + (uint64_t)capn * 16 +
-                                   ((uint64_t)(capn + 1) * 12 + 7) / 8 * 8;
-            uint64_t so;
-            if (!EMIT)
+            const uint64_t bytes = k2_scratch_bytes(np, capn);
+            unsigned long long o = 0;
+            if (lane == 0) o = atomicAdd(&b.ctl->scr_top, (unsigned long long)bytes);
+            const uint64_t so = uniform64(o);
+            if (so + bytes > b.ctl->scr_cap)
             {
-                unsigned long long o = 0;
-                if (lane == 0) o = atomicAdd(&b.ctl->scr_top, (unsigned long long)bytes);
-                so = uniform64(o);
-                if (so + bytes > b.ctl->scr_cap)
+                if (lane == 0)
                 {
-                    if (lane == 0) { atomicOr(&b.ctl->overflow, 4u); b.t_scr[t] = ~0ull; }
-                    continue;
+                    atomicOr(&b.ctl->overflow, 4u);
+                    for (int a = 0; a < 9; ++a) b.sz[a * n + t] = 0;
                 }
-                if (lane == 0) b.t_scr[t] = so;
+                continue;
             }
-            else
+            k2_carve(mem, b.scratch + so, np, capn);
+            for (uint32_t i = lane; i < np; i += 64)
             {
-                so = b.t_scr[t];
-                if (so == ~0ull) continue;
+                mem.off[i] = b.p_off[p0 + i]; mem.c0[i] = b.p_c0[p0 + i]; mem.c1[i] = b.p_c1[p0 + i];
+                mem.roff[i] = b.p_roff[p0 + i]; mem.rcnt[i] = b.p_rcnt[p0 + i]; mem.rb[i] = b.p_rb[p0 + i];
             }
-            uint8_t* base = b.scratch + so;
-            mem.V = reinterpret_cast<uint64_t*>(base);
-            mem.UP = mem.V + capn;
-            mem.st = reinterpret_cast<uint32_t*>(mem.UP + capn);
-            mem.P = mem.st + ((2 * np + 2 + 1) & ~1u);
-            mem.gst = mem.P + (capn + 1);
-            mem.P2 = mem.gst + (capn + 1);
         }
+        __syncthreads();
+        wave_list_starts(np, [&](uint32_t i) { return mem.c0[i]; }, mem.st0);
+        wave_list_starts(np, [&](uint32_t i) { return mem.c1[i]; }, mem.st1);
+        wave_list_starts(2 * np, [&](uint32_t i) {
+            return (i & 1) ? (mem.rb[i >> 1] != NO_RB ? 1u : 0u) : mem.rcnt[i >> 1];
+        }, mem.stR);
+        __syncthreads();
 
         // ---- keyDeps (class 0) and directKeyDeps (class 1)
         for (int c = 0; c < 2; ++c)
         {
             const int m = c == 0 ? 0 : 2;          // AD_MAP_KEY / AD_MAP_DIRECT_KEY
-            // list starts
-            uint32_t carry = 0;
-            for (uint32_t i0 = 0; i0 < np; i0 += 64)
-            {
-                const uint32_t i = i0 + lane;
-                const uint32_t cnt = i < np ? (c == 0 ? b.p_c0[p0 + i] : b.p_c1[p0 + i]) : 0u;
-                const uint32_t inc = wave_incl_scan(cnt);
-                if (i < np) mem.st[i] = carry + inc - cnt;
-                carry += __shfl(inc, 63, 64);
-            }
             const uint32_t tot = c == 0 ? tot0 : tot1;
-            if (lane == 0) mem.st[np] = tot;
-            __syncthreads();
-            // stage elements
-            for (uint32_t i = 0; i < np; ++i)
+            const uint32_t* st = c == 0 ? mem.st0 : mem.st1;
+            if (tot == 0)
             {
-                const uint32_t s0 = mem.st[i], len = mem.st[i + 1] - s0;
-                if (!len) continue;
-                const uint64_t src = (uint64_t)b.p_off[p0 + i] + (c == 0 ? 0u : b.p_c0[p0 + i]);
-                for (uint32_t j = lane; j < len; j += 64) mem.V[s0 + j] = b.arena[src + j];
+                if (lane == 0) { b.sz[(3 * m) * n + t] = 0; b.sz[(3 * m + 1) * n + t] = 0; b.sz[(3 * m + 2) * n + t] = 0; }
+                continue;
+            }
+            // gather: one cooperative load per 64 elements
+            for (uint32_t e = lane; e < tot; e += 64)
+            {
+                const uint32_t a = list_of(st, np, e);
+                mem.V[e] = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
             }
             __syncthreads();
             auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
-            const uint32_t U = rank_merge_kept(get, mem.st, np, tot, mem.P);
-            // non-empty keys
+            const uint32_t U = rank_merge_kept(get, st, np, tot, mem.P);
             uint32_t nk = 0;
             for (uint32_t i0 = 0; i0 < np; i0 += 64)
             {
                 const uint32_t i = i0 + lane;
-                const bool ne = i < np && mem.st[i + 1] > mem.st[i];
-                nk += __popcll(ballot(ne));
+                nk += __popcll(ballot(i < np && st[i + 1] > st[i]));
             }
-            if (!EMIT)
+            const uint64_t rb = region_bytes(nk, U, tot);
+            const uint64_t ro = ralloc.take(&b.ctl->reg_top, b.ctl->reg_cap, &b.ctl->overflow, 8u, rb, K2_REGION_CHUNK);
+            const bool fits = ro + rb <= b.ctl->reg_cap;
+            if (lane == 0)
             {
-                if (lane == 0)
-                {
-                    b.sz[(3 * m + 0) * n + t] = nk;
-                    b.sz[(3 * m + 1) * n + t] = U;
-                    b.sz[(3 * m + 2) * n + t] = nk + tot;
-                }
+                b.sz[(3 * m) * n + t] = fits ? nk : 0;
+                b.sz[(3 * m + 1) * n + t] = fits ? U : 0;
+                b.sz[(3 * m + 2) * n + t] = fits ? nk + tot : 0;
+                b.t_reg[(uint64_t)m * n + t] = ro;
             }
-            else
+            if (fits)
             {
-                const uint64_t ko = b.off[(3 * m + 0) * (n + 1) + t];
-                const uint64_t vo = b.off[(3 * m + 1) * (n + 1) + t];
-                const uint64_t oo = b.off[(3 * m + 2) * (n + 1) + t];
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
                 // keys + heads (absolute end offsets starting at nKeys)
                 uint32_t kr = 0;
                 for (uint32_t i0 = 0; i0 < np; i0 += 64)
                 {
                     const uint32_t i = i0 + lane;
-                    const bool ne = i < np && mem.st[i + 1] > mem.st[i];
+                    const bool ne = i < np && st[i + 1] > st[i];
                     const uint64_t mk = ballot(ne);
                     if (ne)
                     {
                         const uint32_t k = kr + mbcnt(mk);
-                        b.o_keys[m][ko + k] = b.q_keys[p0 + i];
-                        b.o_k2t[m][oo + k] = (int32_t)(nk + mem.st[i + 1]);
+                        okeys[k] = b.q_keys[p0 + i];
+                        ok2t[k] = (int32_t)(nk + st[i + 1]);
                     }
                     kr += __popcll(mk);
                 }
@@ -752,9 +822,9 @@ __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
                 for (uint32_t e = lane; e < tot; e += 64)
                 {
                     const uint64_t x = mem.V[e];
-                    const uint32_t ur = rank_merge_urank(get, mem.st, np, mem.P, x);
-                    if (mem.P[e + 1] - mem.P[e]) b.o_txns[m][vo + ur] = dict_index((uint32_t)x);
-                    b.o_k2t[m][oo + nk + e] = (int32_t)ur;
+                    const uint32_t ur = rank_merge_urank(get, st, np, mem.P, x);
+                    if (mem.P[e + 1] - mem.P[e]) otx[ur] = dict_index((uint32_t)x);
+                    ok2t[nk + e] = (int32_t)ur;
                 }
             }
             __syncthreads();
@@ -763,39 +833,27 @@ __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
         // ---- rangeDeps: lists = per probe [range-command pairs], [redundant pair]
         {
             const uint32_t nl = 2 * np;
-            uint32_t carry = 0;
-            for (uint32_t i0 = 0; i0 < nl; i0 += 64)
+            if (totR == 0)
             {
-                const uint32_t i = i0 + lane;
-                uint32_t cnt = 0;
-                if (i < nl)
-                {
-                    const uint64_t p = p0 + (i >> 1);
-                    cnt = (i & 1) ? (b.p_rb[p] != NO_RB ? 1u : 0u) : b.p_rcnt[p];
-                }
-                const uint32_t inc = wave_incl_scan(cnt);
-                if (i < nl) mem.st[i] = carry + inc - cnt;
-                carry += __shfl(inc, 63, 64);
+                if (lane == 0) { b.sz[3 * n + t] = 0; b.sz[4 * n + t] = 0; b.sz[5 * n + t] = 0; }
+                continue;
             }
-            if (lane == 0) mem.st[nl] = totR;
-            __syncthreads();
-            for (uint32_t i = 0; i < np; ++i)
+            for (uint32_t e = lane; e < totR; e += 64)
             {
-                const uint32_t s0 = mem.st[2 * i], len = mem.st[2 * i + 1] - s0;
-                const uint64_t src = b.p_roff[p0 + i];
-                for (uint32_t j = lane; j < len; j += 64) mem.V[s0 + j] = b.rarena[src + j];
-                if (lane == 0 && mem.st[2 * i + 2] > mem.st[2 * i + 1]) mem.V[mem.st[2 * i + 1]] = b.p_rb[p0 + i];
+                const uint32_t a = list_of(mem.stR, nl, e);
+                const uint32_t pi = a >> 1;
+                mem.V[e] = (a & 1) ? mem.rb[pi] : b.rarena[(uint64_t)mem.roff[pi] + (e - mem.stR[a])];
             }
             __syncthreads();
             auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
-            const uint32_t UPn = rank_merge_kept(get, mem.st, nl, totR, mem.P);
+            const uint32_t UPn = rank_merge_kept(get, mem.stR, nl, totR, mem.P);
             // unique pairs, sorted by (rid, rank) = (Range.compare, TxnId.compareTo)
             for (uint32_t e = lane; e < totR; e += 64)
             {
                 if (mem.P[e + 1] - mem.P[e])
                 {
                     const uint64_t x = mem.V[e];
-                    mem.UP[rank_merge_urank(get, mem.st, nl, mem.P, x)] = x;
+                    mem.UP[rank_merge_urank(get, mem.stR, nl, mem.P, x)] = x;
                 }
             }
             __syncthreads();
@@ -814,31 +872,32 @@ __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
             // distinct txnIds across groups: rank merge over the groups by rank
             auto getr = [&](uint32_t e) -> uint64_t { return mem.UP[e] & 0xFFFFFFFFull; };
             const uint32_t UR = rank_merge_kept(getr, mem.gst, nR, UPn, mem.P2);
-            if (!EMIT)
+            const uint64_t rbytes = region_bytes(nR, UR, UPn);
+            const uint64_t ro = ralloc.take(&b.ctl->reg_top, b.ctl->reg_cap, &b.ctl->overflow, 8u, rbytes, K2_REGION_CHUNK);
+            const bool fits = ro + rbytes <= b.ctl->reg_cap;
+            if (lane == 0)
             {
-                if (lane == 0)
-                {
-                    b.sz[(3 * 1 + 0) * n + t] = nR;
-                    b.sz[(3 * 1 + 1) * n + t] = UR;
-                    b.sz[(3 * 1 + 2) * n + t] = nR + UPn;
-                }
+                b.sz[3 * n + t] = fits ? nR : 0;
+                b.sz[4 * n + t] = fits ? UR : 0;
+                b.sz[5 * n + t] = fits ? nR + UPn : 0;
+                b.t_reg[(uint64_t)1 * n + t] = ro;
             }
-            else
+            if (fits)
             {
-                const uint64_t ko = b.off[(3 * 1 + 0) * (n + 1) + t];
-                const uint64_t vo = b.off[(3 * 1 + 1) * (n + 1) + t];
-                const uint64_t oo = b.off[(3 * 1 + 2) * (n + 1) + t];
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nR);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + UR);
                 for (uint32_t g = lane; g < nR; g += 64)
                 {
-                    b.o_keys[1][ko + g] = (int64_t)(mem.UP[mem.gst[g]] >> 32);
-                    b.o_k2t[1][oo + g] = (int32_t)(nR + mem.gst[g + 1]);
+                    okeys[g] = (int64_t)(mem.UP[mem.gst[g]] >> 32);
+                    ok2t[g] = (int32_t)(nR + mem.gst[g + 1]);
                 }
                 for (uint32_t e = lane; e < UPn; e += 64)
                 {
                     const uint64_t x = getr(e);
                     const uint32_t ur = rank_merge_urank(getr, mem.gst, nR, mem.P2, x);
-                    if (mem.P2[e + 1] - mem.P2[e]) b.o_txns[1][vo + ur] = dict_index((uint32_t)x);
-                    b.o_k2t[1][oo + nR + e] = (int32_t)ur;
+                    if (mem.P2[e + 1] - mem.P2[e]) otx[ur] = dict_index((uint32_t)x);
+                    ok2t[nR + e] = (int32_t)ur;
                 }
             }
             __syncthreads();
@@ -846,13 +905,44 @@ __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
     }
 }
 
-hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, bool emit, hipStream_t st)
+hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
     const unsigned grid = (unsigned)std::min<uint64_t>(b.n_txns, (uint64_t)device_cu_count() * 16);
-    const size_t lds = (size_t)(2 * K2_MAXP + 2) * 4 + (size_t)K2_CAP * 8 * 2 + (size_t)(K2_CAP + 1) * 4 * 3;
-    if (emit) k_build<true><<<grid, 64, lds, st>>>(s, b);
-    else k_build<false><<<grid, 64, lds, st>>>(s, b);
+    k_build<<<grid, 64, k2_lds_bytes(), st>>>(s, b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// pack: per-request regions -> contiguous per-map arrays at the scanned offsets
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pack(BatchBufs b)
+{
+    const uint64_t n = b.n_txns;
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= n) return;
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+    {
+        const uint32_t nk = b.sz[(3 * m) * n + t], U = b.sz[(3 * m + 1) * n + t], no = b.sz[(3 * m + 2) * n + t];
+        if (no == 0) continue;
+        const uint8_t* base = b.reg + b.t_reg[(uint64_t)m * n + t];
+        const int64_t* ikeys = reinterpret_cast<const int64_t*>(base);
+        const uint32_t* itx = reinterpret_cast<const uint32_t*>(ikeys + nk);
+        const int32_t* ik2t = reinterpret_cast<const int32_t*>(itx + U);
+        const uint64_t ko = b.off[(3 * m) * (n + 1) + t], vo = b.off[(3 * m + 1) * (n + 1) + t],
+                       oo = b.off[(3 * m + 2) * (n + 1) + t];
+        for (uint32_t i = lane; i < nk; i += 64) b.o_keys[m][ko + i] = ikeys[i];
+        for (uint32_t i = lane; i < U; i += 64) b.o_txns[m][vo + i] = itx[i];
+        for (uint32_t i = lane; i < no; i += 64) b.o_k2t[m][oo + i] = ik2t[i];
+    }
+}
+
+hipError_t run_pack(const BatchBufs& b, hipStream_t st)
+{
+    if (!b.n_txns) return hipSuccess;
+    k_pack<<<(unsigned)((b.n_txns + 3) / 4), 256, 0, st>>>(b);
     return hipGetLastError();
 }
 

@@ -12,7 +12,8 @@ struct BatchCtl {
     unsigned long long key_top, key_cap;      // K1 arena (u32 elements)
     unsigned long long rng_top, rng_cap;      // K4 arena (u64 elements)
     unsigned long long scr_top, scr_cap;      // K2 big-txn scratch (bytes)
-    unsigned int overflow;                    // bit0 key arena, bit1 range arena, bit2 scratch
+    unsigned long long reg_top, reg_cap;      // K2 per-request output regions (bytes)
+    unsigned int overflow;                    // bit0 key arena, bit1 range arena, bit2 scratch, bit3 regions
     unsigned int error;                       // AD_E_* (negated) of the first failure, 0 = none
 };
 
@@ -31,7 +32,7 @@ struct BatchBufs {
     const int64_t* q_keys;
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
-    uint32_t* p_txn; int32_t* p_key; uint8_t* p_slice;
+    uint32_t* p_txn; uint4* p_rec;
     // K1
     uint32_t* arena; uint32_t* p_off; uint32_t* p_c0; uint32_t* p_c1;
     // K4
@@ -40,8 +41,9 @@ struct BatchBufs {
     uint32_t* sz;                    // [9][n_txns]: per map m: keys, txns, k2t
     uint64_t* off;                   // [9][n_txns+1]
     uint64_t* bsum;                  // [9][ceil(n_txns/1024)] scan block sums
-    uint64_t* t_scr;                 // [n_txns] big-txn scratch offset (bytes), ~0 = LDS path
-    uint8_t* scratch;
+    uint64_t* t_reg;                 // [3][n_txns] byte offset of each request's map region
+    uint8_t* reg;                    // per-request output regions
+    uint8_t* scratch;                // big-request scratch
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
     BatchCtl* ctl;
 };
@@ -52,8 +54,9 @@ hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);
 hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_scan(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
-hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, bool emit, hipStream_t st);
+hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
+hipError_t run_pack(const BatchBufs& b, hipStream_t st);
 
 int device_cu_count();
 
