@@ -30,8 +30,9 @@ from accord_deps import native, synth  # noqa: E402
 
 METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-STAGES = ["K0 encode", "K1 conflict scan", "K4 range probe", "K2 build", "offsets scan", "pack"]
-KERNEL_OF_STAGE = ["k_encode_txn+k_probe_keys", "k_scan", "k_range", "k_build", "k_scan_blocks+sums+add", "k_pack"]
+STAGES = ["fused resolve (K0+K1+K4+K2)", "deferred requests (split K0..K2)", "-", "-", "offsets scan", "pack"]
+KERNEL_OF_STAGE = ["k_resolve", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "-", "-",
+                   "k_scan_blocks+sums+add", "k_pack"]
 
 
 def log(*a):
@@ -61,10 +62,12 @@ def device_queries(q, dev):
 
 def stage_bytes(w, stats):
     """Algorithmic bytes per pipeline stage and launch.
-    K1 follows SURVEY.md §8(d) config 2: every touched key's CommandsForKey segment read once
-    (17 B per entry + 16 B header) + 12 B per probe, plus its 4 B per emitted txnId.
-    K2 (emit) reads the per-probe lists and writes the CSR: 8 B per key (range) head + 4 B per
-    keysToTxnIds int + 4 B per txnId index."""
+    Fused resolve: request inputs (txnId + executeAt 40 B, key_off 8 B, 8 B per key) + the
+    SURVEY.md §8(d) config-2 compulsory CommandsForKey read (every touched key's segment once,
+    17 B per entry + 16 B header) + the range-command table once (16 B per entry) + the CSR
+    output written to its region (8 B per key/range head, 4 B per keysToTxnIds int, 4 B per
+    txnId index) + 9 x 4 B sizes and 3 x 8 B region offsets per request.
+    Pack: reads and writes the CSR output once more."""
     q = w.queries
     keys_touched = np.unique(q.keys)
     pos = np.searchsorted(w.cfk.keys, keys_touched)
@@ -76,13 +79,12 @@ def stage_bytes(w, stats):
     pairs = sum(stats["n_pairs"])
     heads = sum(stats["n_keys"])
     uniq = sum(stats["n_unique"])
+    out_bytes = 8 * heads + 4 * (heads + pairs) + 4 * uniq
     b = [0] * 6
-    b[0] = len(q) * (3 * 20 + 8) + q.n_probes * (8 + 4 + 4 + 1)
-    b[1] = int((17 * lk + 16).sum()) + 12 * q.n_probes + 4 * pairs
-    b[2] = 16 * w.cmds.range_off[-1] + q.n_probes * (8 + 4 + 8 + 8)
-    b[3] = 4 * pairs + 24 * q.n_probes + 8 * heads + 4 * (heads + pairs) + 4 * uniq + 9 * 4 * len(q)
+    b[0] = len(q) * (40 + 8) + 8 * q.n_probes + int((17 * lk + 16).sum()) + 16 * int(w.cmds.range_off[-1]) + \
+        out_bytes + len(q) * (9 * 4 + 3 * 8)
     b[4] = 9 * (4 + 8) * len(q)
-    b[5] = 2 * (8 * heads + 4 * (heads + pairs) + 4 * uniq) + 9 * 12 * len(q)
+    b[5] = 2 * out_bytes + len(q) * (9 * (4 + 8) + 3 * 8)
     return b
 
 

@@ -42,7 +42,7 @@ P = C.c_void_p
 
 class AdConfig(C.Structure):
     _fields_ = [("device", C.c_int32), ("range_start_inclusive", C.c_int32), ("elide", C.c_int32),
-                ("reserved", C.c_int32), ("n_slices", C.c_uint64), ("slice_start", P), ("slice_end", P)]
+                ("path", C.c_int32), ("n_slices", C.c_uint64), ("slice_start", P), ("slice_end", P)]
 
 
 class AdCfkSoa(C.Structure):
@@ -72,7 +72,7 @@ class AdStats(C.Structure):
     _fields_ = [("n_txns", C.c_uint64), ("n_probes", C.c_uint64), ("n_pairs", C.c_uint64 * NMAPS),
                 ("n_unique", C.c_uint64 * NMAPS), ("n_keys", C.c_uint64 * NMAPS), ("scan_entries", C.c_uint64),
                 ("ms_device", C.c_double), ("ms_ingest", C.c_double),
-                ("ms_stage", C.c_double * 8), ("bytes_stage", C.c_uint64 * 8)]
+                ("ms_stage", C.c_double * 8), ("n_deferred", C.c_uint64), ("bytes_stage", C.c_uint64 * 8)]
 
 
 class AdDepsResult(C.Structure):

@@ -74,7 +74,7 @@ def _view(p, n, dtype):
 
 def stats_dict(s):
     return dict(n_txns=s.n_txns, n_probes=s.n_probes, n_pairs=list(s.n_pairs), n_unique=list(s.n_unique),
-                n_keys=list(s.n_keys),
+                n_keys=list(s.n_keys), n_deferred=s.n_deferred,
                 ms_device=s.ms_device, ms_ingest=s.ms_ingest, ms_stage=list(s.ms_stage)[:6],
                 bytes_stage=list(s.bytes_stage)[:6])
 
@@ -82,12 +82,13 @@ def stats_dict(s):
 class DeviceCommandStore:
     """One CommandStore's snapshot resident on one MI355X (an `ad_ctx`)."""
 
-    def __init__(self, device=0, range_start_inclusive=0, elide=1, slices=None):
+    def __init__(self, device=0, range_start_inclusive=0, elide=1, slices=None, path=0):
         L = lib()
         cfg = A.AdConfig()
         cfg.device = device
         cfg.range_start_inclusive = range_start_inclusive
         cfg.elide = elide
+        cfg.path = path
         self._keep = []
         if slices is not None and len(slices):
             s = np.ascontiguousarray(np.asarray(slices, np.int64)[:, 0])
@@ -177,8 +178,8 @@ class DeviceCommandStore:
         return out, stats_dict(out.stats)
 
 
-def resolve(workload, device=0, elide=1):
-    st = DeviceCommandStore(device, workload.range_start_inclusive, elide, workload.slices)
+def resolve(workload, device=0, elide=1, path=0):
+    st = DeviceCommandStore(device, workload.range_start_inclusive, elide, workload.slices, path)
     try:
         st.load(workload)
         return st.calculate_partial_deps(workload.queries, workload.flags)

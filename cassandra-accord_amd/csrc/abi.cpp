@@ -180,7 +180,7 @@ struct ad_ctx {
     std::vector<int32_t> dict_node;
     std::vector<int64_t> rt_start, rt_end;     // range table (distinct ranges, by Range.compare)
     DevSnapshot ds{};
-    DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_krec, d_ent, d_w;
+    DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_krec, d_khash, d_ent, d_w;
     DevBuf d_lvl[NCLASS][MAX_LEVELS];
     DevBuf d_rstart, d_rend, d_rtxw, d_rrid;
     DevBuf d_rlvl[NCLASS][MAX_LEVELS];
@@ -188,9 +188,12 @@ struct ad_ctx {
 
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
-    DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec;
-    DevBuf arena, p_off, p_c0, p_c1, rarena, p_roff, p_rcnt, p_rb;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl;
+    struct SplitBufs {       // per-request / per-probe arrays of the split kernels
+        DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
+    } split, sub;
+    DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
+    DevBuf arena, rarena;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
@@ -447,8 +450,10 @@ static int build_snapshot(ad_ctx* c)
                    rent.end());
         std::vector<uint32_t> rb_rid(nrb);
         for (uint64_t i = 0; i < nrb; ++i) rb_rid[i] = rid_of(c->rb.start[i], c->rb.end[i]);
-        std::vector<int64_t> rs(rent.size()), re(rent.size());
-        std::vector<uint32_t> rtxw(rent.size()), rrid(rent.size());
+        // padded to whole 64-entry frames: the fused kernel reads frames with vector loads
+        const size_t rpad = (rent.size() + 63) / 64 * 64;
+        std::vector<int64_t> rs(rpad, INT64_MAX), re(rpad, INT64_MIN);
+        std::vector<uint32_t> rtxw(rpad, 0), rrid(rpad, 0);
         for (size_t i = 0; i < rent.size(); ++i) { rs[i] = rent[i].s; re[i] = rent[i].e; rtxw[i] = rent[i].txw; rrid[i] = rent[i].rid; }
         for (uint64_t i = 0; i < nrb; ++i)
             if (wm_rank[i] && (c->rb.wm[i].lsb & 1) == 0) return c->fail(AD_E_INVAL, "redundantBefore watermark must be range-domain");
@@ -462,6 +467,7 @@ static int build_snapshot(ad_ctx* c)
 
     // ---- 4. upload CFK + dictionary, build the trees
     int rc;
+    ent.resize((ne + 63) / 64 * 64, make_uint2(0u, 0u));      // whole 64-entry frames (tau 0: never emitted)
     std::vector<KeyRec> krec(nk);
     for (uint64_t k = 0; k < nk; ++k)
     {
@@ -475,8 +481,18 @@ static int build_snapshot(ad_ctx* c)
         r.pruned = pruned[k];
         r.maw = maw[k];
     }
+    uint64_t hcap = 16;
+    while (hcap < 2 * nk) hcap <<= 1;
+    std::vector<KeySlot> khash(hcap, KeySlot{0, KEY_EMPTY, 0});
+    for (uint64_t k = 0; k < nk; ++k)
+    {
+        uint64_t h = key_hash(K.keys[k]) & (hcap - 1);
+        while (khash[h].idx != KEY_EMPTY) h = (h + 1) & (hcap - 1);
+        khash[h] = KeySlot{K.keys[k], (uint32_t)k, 0};
+    }
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
-        (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_ent, ent)) ||
+        (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_khash, khash)) ||
+        (rc = upload(c, c->d_ent, ent)) ||
         (rc = upload(c, c->d_w, w)) || (rc = upload(c, c->d_slices_s, c->slice_s)) || (rc = upload(c, c->d_slices_e, c->slice_e)))
         return rc;
 
@@ -489,6 +505,8 @@ static int build_snapshot(ad_ctx* c)
     s.n_keys = nk;
     s.keys = c->d_keys.as<int64_t>();
     s.krec = c->d_krec.as<KeyRec>();
+    s.khash = c->d_khash.as<KeySlot>();
+    s.khash_mask = hcap - 1;
     s.n_ent = ne;
     s.ent = c->d_ent.as<uint2>();
     s.w = c->d_w.as<uint2>();
@@ -503,7 +521,7 @@ static int build_snapshot(ad_ctx* c)
     for (int l = 1; l < L; ++l)
         for (int cl = 0; cl < NCLASS; ++cl)
         {
-            if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * s.lvl_n[l])) return c->fail(AD_E_NOMEM, "tree level");
+            if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * ((s.lvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "tree level");
             s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
         }
     s.n_rent = rent.size();
@@ -522,7 +540,7 @@ static int build_snapshot(ad_ctx* c)
     for (int l = 1; l < L; ++l)
         for (int cl = 0; cl < NCLASS; ++cl)
         {
-            if (!c->d_rlvl[cl][l].ensure(sizeof(int64_t) * s.rlvl_n[l])) return c->fail(AD_E_NOMEM, "range tree level");
+            if (!c->d_rlvl[cl][l].ensure(sizeof(int64_t) * ((s.rlvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "range tree level");
             s.rlvl[cl][l] = c->d_rlvl[cl][l].as<int64_t>();
         }
     s.n_rb = nrb;
@@ -648,6 +666,36 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
 template <class T>
 static bool ens(DevBuf& b, uint64_t n) { return b.ensure(sizeof(T) * std::max<uint64_t>(n, 1)); }
 
+// bind the split kernels' per-batch arrays for a batch of n requests / np probes
+static bool bind_split(ad_ctx::SplitBufs& S, BatchBufs& b, uint64_t n, uint64_t np, bool own_sizes)
+{
+    if (!ens<uint32_t>(S.t_S, n) || !ens<uint32_t>(S.t_self, n) || !ens<uint32_t>(S.t_kinds, n) ||
+        !ens<int64_t>(S.t_epoch, n) || !ens<uint32_t>(S.p_txn, np) || !ens<uint4>(S.p_rec, np) ||
+        !ens<uint32_t>(S.p_off, np) || !ens<uint32_t>(S.p_c0, np) || !ens<uint32_t>(S.p_c1, np) ||
+        !ens<uint32_t>(S.p_roff, np) || !ens<uint32_t>(S.p_rcnt, np) || !ens<uint64_t>(S.p_rb, np))
+        return false;
+    b.t_S = S.t_S.as<uint32_t>(); b.t_self = S.t_self.as<uint32_t>(); b.t_kinds = S.t_kinds.as<uint32_t>();
+    b.t_epoch = S.t_epoch.as<int64_t>(); b.p_txn = S.p_txn.as<uint32_t>(); b.p_rec = S.p_rec.as<uint4>();
+    b.p_off = S.p_off.as<uint32_t>(); b.p_c0 = S.p_c0.as<uint32_t>(); b.p_c1 = S.p_c1.as<uint32_t>();
+    b.p_roff = S.p_roff.as<uint32_t>(); b.p_rcnt = S.p_rcnt.as<uint32_t>(); b.p_rb = S.p_rb.as<uint64_t>();
+    if (own_sizes)
+    {
+        if (!ens<uint32_t>(S.sz, 9 * n) || !ens<uint64_t>(S.t_reg, 3 * n)) return false;
+        b.sz = S.sz.as<uint32_t>();
+        b.t_reg = S.t_reg.as<uint64_t>();
+    }
+    return true;
+}
+
+static int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
+{
+    HIPCHK(c, run_encode(c->ds, b, st));
+    HIPCHK(c, run_scan(c->ds, b, st));
+    HIPCHK(c, run_range(c->ds, b, st));
+    HIPCHK(c, run_build(c->ds, b, st));
+    return 0;
+}
+
 static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out)
 {
     const uint64_t n = q->n_txns;
@@ -657,6 +705,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipMemcpyAsync(&np, q->key_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
     }
+    const bool split_only = c->cfg.path == 1;
     BatchBufs b{};
     b.n_txns = n;
     b.n_probes = np;
@@ -664,24 +713,18 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     b.q_exec_msb = q->exec_msb; b.q_exec_lsb = q->exec_lsb; b.q_exec_node = q->exec_node;
     b.q_min_epoch = q->min_epoch; b.q_key_off = q->key_off; b.q_keys = q->keys;
     const uint64_t nb = (n + 1023) / 1024;
-    if (!ens<uint32_t>(c->t_S, n) || !ens<uint32_t>(c->t_self, n) || !ens<uint32_t>(c->t_kinds, n) ||
-        !ens<int64_t>(c->t_epoch, n) || !ens<uint32_t>(c->p_txn, np) || !ens<uint4>(c->p_rec, np) ||
-        !ens<uint32_t>(c->p_off, np) || !ens<uint32_t>(c->p_c0, np) ||
-        !ens<uint32_t>(c->p_c1, np) || !ens<uint32_t>(c->p_roff, np) || !ens<uint32_t>(c->p_rcnt, np) ||
-        !ens<uint64_t>(c->p_rb, np) || !ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) ||
-        !ens<uint64_t>(c->bsum, 9 * nb) || !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1))
+    if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
+        !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n))
         return c->fail(AD_E_NOMEM, "batch buffers");
-    b.t_S = c->t_S.as<uint32_t>(); b.t_self = c->t_self.as<uint32_t>(); b.t_kinds = c->t_kinds.as<uint32_t>();
-    b.t_epoch = c->t_epoch.as<int64_t>(); b.p_txn = c->p_txn.as<uint32_t>(); b.p_rec = c->p_rec.as<uint4>();
-    b.p_off = c->p_off.as<uint32_t>(); b.p_c0 = c->p_c0.as<uint32_t>();
-    b.p_c1 = c->p_c1.as<uint32_t>(); b.p_roff = c->p_roff.as<uint32_t>(); b.p_rcnt = c->p_rcnt.as<uint32_t>();
-    b.p_rb = c->p_rb.as<uint64_t>(); b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>();
-    b.bsum = c->bsum.as<uint64_t>(); b.t_reg = c->t_reg.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>();
+    b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>(); b.bsum = c->bsum.as<uint64_t>();
+    b.t_reg = c->t_reg.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>(); b.deferred = c->deferred.as<uint32_t>();
+    if (split_only && !bind_split(c->split, b, n, np, false)) return c->fail(AD_E_NOMEM, "split buffers");
 
     const uint64_t waves = (uint64_t)device_cu_count() * 8 * 4;
     const uint64_t k2_waves = (uint64_t)device_cu_count() * 16;
-    uint64_t want_key = std::max<uint64_t>(np * 4 + waves * 4096, 1u << 20);
-    uint64_t want_rng = c->ds.n_rent ? std::max<uint64_t>(np * 2 + waves * 2048, 1u << 20) : 1;
+    const uint64_t np_split = split_only ? np : std::min<uint64_t>(np, 1u << 20);
+    uint64_t want_key = std::max<uint64_t>(np_split * 4 + waves * 4096, 1u << 20);
+    uint64_t want_rng = c->ds.n_rent ? std::max<uint64_t>(np_split * 2 + waves * 2048, 1u << 20) : 1;
     uint64_t want_scr = 64ull << 20;
     uint64_t want_reg = std::max<uint64_t>(n * 3 * 8 + np * 24 + k2_waves * (3ull << 16), 16ull << 20);
     if (c->key_cap < want_key) c->key_cap = want_key;
@@ -706,16 +749,54 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         h.reg_cap = c->reg_cap;
         HIPCHK(c, hipMemcpyAsync(b.ctl, &h, sizeof(h), hipMemcpyHostToDevice, st));
         HIPCHK(c, hipEventRecord(c->ev[0], st));
-        HIPCHK(c, run_encode(c->ds, b, st));
-        HIPCHK(c, hipEventRecord(c->ev[1], st));
-        HIPCHK(c, run_scan(c->ds, b, st));
+        uint64_t nd = 0;
+        int rc;
+        if (split_only)
+        {
+            if ((rc = run_split(c, b, st))) return rc;
+            HIPCHK(c, hipEventRecord(c->ev[1], st));
+        }
+        else
+        {
+            HIPCHK(c, run_resolve(c->ds, b, st));
+            HIPCHK(c, hipEventRecord(c->ev[1], st));
+            HIPCHK(c, hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+            nd = h.n_deferred;
+            if (nd && !h.error && !(h.overflow & 8u))
+            {
+                // deferred requests: gather a sub-batch, resolve it with the split kernels, scatter back
+                if (!ens<uint32_t>(c->s_cnt, nd) || !ens<uint64_t>(c->s_ko, nd + 1))
+                    return c->fail(AD_E_NOMEM, "deferred buffers");
+                HIPCHK(c, run_defer_counts(b, b.deferred, nd, c->s_cnt.as<uint32_t>(), st));
+                HIPCHK(c, run_scan_arrays(c->s_cnt.as<uint32_t>(), c->s_ko.as<uint64_t>(), nd, 1, b.bsum, st));
+                uint64_t snp = 0;
+                HIPCHK(c, hipMemcpyAsync(&snp, c->s_ko.as<uint64_t>() + nd, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+                HIPCHK(c, hipStreamSynchronize(st));
+                BatchBufs sb = b;
+                sb.n_txns = nd;
+                sb.n_probes = snp;
+                if (!bind_split(c->sub, sb, nd, snp, true) || !ens<uint64_t>(c->s_tm, nd) || !ens<uint64_t>(c->s_tl, nd) ||
+                    !ens<int32_t>(c->s_tn, nd) || !ens<uint64_t>(c->s_em, nd) || !ens<uint64_t>(c->s_el, nd) ||
+                    !ens<int32_t>(c->s_en, nd) || !ens<int64_t>(c->s_me, nd) || !ens<int64_t>(c->s_k, snp))
+                    return c->fail(AD_E_NOMEM, "deferred buffers");
+                uint64_t* sko = c->s_ko.as<uint64_t>();     // the scanned counts are the sub-batch key_off
+                HIPCHK(c, run_defer_gather(b, b.deferred, nd, c->s_ko.as<uint64_t>(), sb, c->s_tm.as<uint64_t>(),
+                                           c->s_tl.as<uint64_t>(), c->s_tn.as<int32_t>(), c->s_em.as<uint64_t>(),
+                                           c->s_el.as<uint64_t>(), c->s_en.as<int32_t>(), c->s_me.as<int64_t>(), sko,
+                                           c->s_k.as<int64_t>(), st));
+                sb.q_txn_msb = c->s_tm.as<uint64_t>(); sb.q_txn_lsb = c->s_tl.as<uint64_t>(); sb.q_txn_node = c->s_tn.as<int32_t>();
+                sb.q_exec_msb = c->s_em.as<uint64_t>(); sb.q_exec_lsb = c->s_el.as<uint64_t>(); sb.q_exec_node = c->s_en.as<int32_t>();
+                sb.q_min_epoch = b.q_min_epoch ? c->s_me.as<int64_t>() : nullptr;
+                sb.q_key_off = sko;
+                sb.q_keys = c->s_k.as<int64_t>();
+                if ((rc = run_split(c, sb, st))) return rc;
+                HIPCHK(c, run_defer_scatter(b, b.deferred, nd, sb.sz, sb.t_reg, st));
+            }
+        }
         HIPCHK(c, hipEventRecord(c->ev[2], st));
-        HIPCHK(c, run_range(c->ds, b, st));
-        HIPCHK(c, hipEventRecord(c->ev[3], st));
-        HIPCHK(c, run_build(c->ds, b, st));
-        HIPCHK(c, hipEventRecord(c->ev[4], st));
         HIPCHK(c, run_offsets(b, st));
-        HIPCHK(c, hipEventRecord(c->ev[5], st));
+        HIPCHK(c, hipEventRecord(c->ev[3], st));
         uint64_t tot[9] = {0};
         for (int a = 0; a < 9; ++a)
             HIPCHK(c, hipMemcpyAsync(&tot[a], b.off + (uint64_t)a * (n + 1) + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -744,15 +825,16 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             b.o_txns[m] = c->o_txns[m].as<uint32_t>();
             b.o_k2t[m] = c->o_k2t[m].as<int32_t>();
         }
-        HIPCHK(c, hipEventRecord(c->ev[6], st));
+        HIPCHK(c, hipEventRecord(c->ev[4], st));
         HIPCHK(c, run_pack(b, st));
-        HIPCHK(c, hipEventRecord(c->ev[7], st));
+        HIPCHK(c, hipEventRecord(c->ev[5], st));
         HIPCHK(c, hipStreamSynchronize(st));
 
         ad_stats& S = out->stats;
         memset(&S, 0, sizeof(S));
         S.n_txns = n;
         S.n_probes = np;
+        S.n_deferred = nd;
         for (int m = 0; m < 3; ++m)
         {
             S.n_pairs[m] = tot[3 * m + 2] - tot[3 * m + 0];
@@ -760,12 +842,12 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             S.n_keys[m] = tot[3 * m + 0];
         }
         float ms;
-        const int pairs[6][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}};
+        const int pairs[4][3] = {{0, 1, 0}, {1, 2, 1}, {2, 3, 4}, {4, 5, 5}};
         double total = 0;
-        for (int i = 0; i < 6; ++i)
+        for (int i = 0; i < 4; ++i)
         {
             HIPCHK(c, hipEventElapsedTime(&ms, c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
-            S.ms_stage[i] = ms;
+            S.ms_stage[pairs[i][2]] = ms;
             total += ms;
         }
         S.ms_device = total;

@@ -88,6 +88,22 @@ struct KeyRec {
 // self rank (0 = none), kinds | class << 8 | in_slice << 12}
 constexpr uint32_t NO_KEY = 0xFFFFFFFFu;
 
+// Open-addressing hash of key ordinal -> key index (one 16-byte probe per lookup, linear probing)
+struct KeySlot {
+    int64_t key;
+    uint32_t idx;       // KEY_EMPTY = free slot
+    uint32_t pad;
+};
+constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
+
+__host__ __device__ inline uint64_t key_hash(int64_t k)
+{
+    uint64_t z = (uint64_t)k + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
 // Per-store device snapshot, passed to kernels by value.
 struct DevSnapshot {
     // id dictionary (normalised)
@@ -99,6 +115,8 @@ struct DevSnapshot {
     uint64_t n_keys;
     const int64_t*  keys;          // [n_keys]
     const KeyRec*   krec;          // [n_keys]
+    const KeySlot*  khash;         // [khash_mask + 1]
+    uint64_t khash_mask;
     uint64_t n_ent;
     const uint2*    ent;           // {tau, txw}
     const uint2*    w;             // committed Writes by executeAt: {exec rank, txn rank}

@@ -1015,21 +1015,19 @@ __global__ void k_scan_add(const uint64_t* __restrict__ bsum, uint64_t nb, uint6
     if (i < n) off[(uint64_t)a * (n + 1) + i] += bsum[(uint64_t)a * nb + blockIdx.x];
 }
 
-hipError_t run_offsets(const BatchBufs& b, hipStream_t st)
+hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st)
 {
-    const uint64_t n = b.n_txns;
+    // out[a][0..n] = exclusive prefix of in[a][0..n), out[a][n] = total, for a < n_arrays
     const uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
-    uint64_t* bsum = b.bsum;
-    if (n == 0)
-    {
-        return hipMemsetAsync(b.off, 0, sizeof(uint64_t) * 9, st);
-    }
-    dim3 g((unsigned)nb, 9);
-    k_scan_blocks<<<g, SCAN_BLOCK, 0, st>>>(b.sz, n, b.off, bsum, nb);
-    k_scan_sums<<<9, 64, 0, st>>>(bsum, nb, b.off, n);
-    k_scan_add<<<g, SCAN_BLOCK, 0, st>>>(bsum, nb, b.off, n);
+    if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint64_t) * n_arrays, st);
+    dim3 g((unsigned)nb, (unsigned)n_arrays);
+    k_scan_blocks<<<g, SCAN_BLOCK, 0, st>>>(in, n, out, bsum, nb);
+    k_scan_sums<<<n_arrays, 64, 0, st>>>(bsum, nb, out, n);
+    k_scan_add<<<g, SCAN_BLOCK, 0, st>>>(bsum, nb, out, n);
     return hipGetLastError();
 }
+
+hipError_t run_offsets(const BatchBufs& b, hipStream_t st) { return run_scan_arrays(b.sz, b.off, b.n_txns, 9, b.bsum, st); }
 
 int device_cu_count()
 {
@@ -1037,7 +1035,7 @@ int device_cu_count()
     if (!cus)
     {
         int dev = 0;
-        hipGetDevice(&dev);
+        (void)hipGetDevice(&dev);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
         if (cus <= 0) cus = 256;

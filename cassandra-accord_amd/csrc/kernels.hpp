@@ -13,6 +13,7 @@ struct BatchCtl {
     unsigned long long rng_top, rng_cap;      // K4 arena (u64 elements)
     unsigned long long scr_top, scr_cap;      // K2 big-txn scratch (bytes)
     unsigned long long reg_top, reg_cap;      // K2 per-request output regions (bytes)
+    unsigned long long n_deferred;            // requests the fused kernel hands to the split kernels
     unsigned int overflow;                    // bit0 key arena, bit1 range arena, bit2 scratch, bit3 regions
     unsigned int error;                       // AD_E_* (negated) of the first failure, 0 = none
 };
@@ -44,6 +45,7 @@ struct BatchBufs {
     uint64_t* t_reg;                 // [3][n_txns] byte offset of each request's map region
     uint8_t* reg;                    // per-request output regions
     uint8_t* scratch;                // big-request scratch
+    uint32_t* deferred;              // [n_txns] requests deferred by k_resolve
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
     BatchCtl* ctl;
 };
@@ -56,7 +58,17 @@ hipError_t run_scan(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
+hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st);
 hipError_t run_pack(const BatchBufs& b, hipStream_t st);
+
+// fused per-request path (resolve.hip)
+hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
+hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
+                            const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,
+                            uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, hipStream_t st);
+hipError_t run_defer_scatter(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint32_t* sub_sz,
+                             const uint64_t* sub_reg, hipStream_t st);
 
 int device_cu_count();
 

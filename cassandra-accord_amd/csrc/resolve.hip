@@ -1,0 +1,730 @@
+// resolve.hip — the fused per-request kernel of the dependency-resolution path (gfx950).
+//
+// One wave resolves one PreAccept.calculatePartialDeps request end to end (PreAccept.java:245-267):
+//   encode    executeAt/txnId -> dictionary ranks (64-ary wave search), keys -> CommandsForKey
+//             index (open-addressing hash, one probe)
+//   K1        CommandsForKey.mapReduceActive (CommandsForKey.java:910-968) for up to 8 keys at
+//             once: lanes 8g..8g+7 serve key g (8-ary searches, 64-ary max-tree descent with
+//             8 nodes per lane, ballot/prefix compaction into LDS)
+//   K4        mapReduceRangesInternal (InMemoryCommandStore.java:884-1017) + RedundantBefore
+//             .collectDeps (RedundantBefore.java:183-192), same group scheme
+//   K2        Deps.AbstractBuilder.add / RelationMultiMap build / PartialDeps.with as the LDS
+//             multi-list union of kernels.hip, written to a chunk-allocated region
+// Requests with more than 8 keys or with a per-key output beyond the LDS staging are deferred
+// to the general split kernels (kernels.hip), which handle any size.
+#include <hip/hip_runtime.h>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace adx {
+
+constexpr int FMAXP = 8;        // keys per request on the fused path (one 8-lane group each)
+constexpr int FCAP0 = 64;       // keyDeps txnIds staged per key
+constexpr int FCAP1 = 16;       // directKeyDeps txnIds staged per key
+constexpr int FCAPR = 32;       // range-command pairs staged per key (+1 slot: redundant pair)
+constexpr int FWAVES = 4;       // waves per workgroup
+constexpr uint32_t F_REGION_CHUNK = 1u << 16;
+
+struct FusedLds {
+    uint32_t st0[FMAXP][FCAP0];
+    uint32_t st1[FMAXP][FCAP1];
+    uint64_t rs[FMAXP][FCAPR + 1];
+    uint64_t stk[FMAXP][2 * MAX_LEVELS];
+    int64_t key[FMAXP];
+};
+
+// ascending bitonic sort of one u64 key per lane across the wave (64 lanes), with a payload
+__device__ __forceinline__ void wave_bitonic64(uint64_t& key, uint32_t& pay)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1)
+        {
+            const uint64_t ok = __shfl_xor(key, (int)j, 64);
+            const uint32_t op = __shfl_xor(pay, (int)j, 64);
+            const bool up = (l & k) == 0;
+            const bool lower = (l & j) == 0;
+            const bool take = lower ? (up ? ok < key : ok > key) : (up ? ok > key : ok < key);
+            if (take)
+            {
+                key = ok;
+                pay = op;
+            }
+        }
+}
+
+__device__ __forceinline__ void set_error_f(BatchCtl* ctl, unsigned code) { atomicCAS(&ctl->error, 0u, code); }
+
+// ---- group (8-lane) helpers --------------------------------------------------------------
+__device__ __forceinline__ uint32_t grp_bits(uint64_t m, uint32_t g) { return (uint32_t)(m >> (8 * g)) & 0xFFu; }
+
+__device__ __forceinline__ uint32_t grp_incl_scan(uint32_t v)
+{
+    const uint32_t j = lane_id() & 7;
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1)
+    {
+        const uint32_t t = __shfl_up(v, d, 8);
+        if (j >= (uint32_t)d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t grp_sum(uint32_t v)
+{
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t grp_or64(uint64_t v)
+{
+    v |= __shfl_xor(v, 1, 64);
+    v |= __shfl_xor(v, 2, 64);
+    v |= __shfl_xor(v, 4, 64);
+    return v;
+}
+
+// lower_bound over key(i), i in [lo, hi), by the 8 lanes of each active group (8-ary rounds);
+// groups proceed independently, the wave loops until every group is done
+template <class KeyAt, class Less>
+__device__ __forceinline__ uint64_t grp_lower_bound(bool active, uint64_t lo, uint64_t hi, KeyAt key, Less less)
+{
+    const uint32_t j = lane_id() & 7, g = lane_id() >> 3;
+    while (ballot(active && hi - lo > 8))
+    {
+        if (active && hi - lo > 8)
+        {
+            const uint64_t n = hi - lo;
+            const uint64_t p = lo + (((uint64_t)(j + 1) * n) >> 3) - 1;
+            const bool lt = less(key(p));
+            const uint32_t c = __popc(grp_bits(ballot(lt), g));
+            if (c == 8) lo = hi;
+            else
+            {
+                const uint64_t pc = lo + (((uint64_t)(c + 1) * n) >> 3) - 1;
+                const uint64_t nlo = c == 0 ? lo : lo + (((uint64_t)c * n) >> 3);
+                lo = nlo;
+                hi = pc;
+            }
+        }
+    }
+    const uint64_t i = lo + j;
+    const bool v = active && i < hi && less(key(i));
+    return lo + __popc(grp_bits(ballot(v), g));
+}
+
+// Group-parallel max-tree descent: like wave_descent, but each 8-lane group walks its own
+// range [lo, end) and every lane evaluates 8 consecutive nodes (leaves) of a 64-wide frame.
+//   node_bits(lv, n0, nlo, nhi) -> 8-bit want mask of nodes n0..n0+7 (within [nlo, nhi])
+//   leaf(n0)                    -> emission for leaves n0..n0+7 (group-collective)
+template <class NodeBits, class Leaf>
+__device__ __forceinline__ void grp_descent(bool active, uint64_t lo, uint64_t end, int n_levels, NodeBits node_bits,
+                                            Leaf leaf, uint64_t* stk)
+{
+    const uint32_t j = lane_id() & 7;
+    bool done = !active || end <= lo;
+    int k = 0;
+    // start at the lowest level whose aligned 64-node frame holds the whole range
+    if (!done)
+        while (k + 1 < n_levels && (lo >> (6 * (k + 1))) != ((end - 1) >> (6 * (k + 1)))) ++k;
+    int lv = k;
+    uint64_t base = done ? 0 : (lo >> (6 * k)) & ~63ull;
+    uint64_t mask = 0;
+    bool eval = !done;
+    while (ballot(!done))
+    {
+        if (!done)
+        {
+            if (eval)
+            {
+                eval = false;
+                const uint64_t n0 = base + 8 * j;
+                if (lv == 0)
+                {
+                    leaf(n0);
+                    mask = 0;
+                }
+                else
+                {
+                    const uint64_t nlo = lo >> (6 * lv), nhi = (end - 1) >> (6 * lv);
+                    const uint32_t bits = node_bits(lv, n0, nlo, nhi);
+                    mask = grp_or64((uint64_t)bits << (8 * j));
+                }
+            }
+            else if (mask == 0)
+            {
+                if (lv == k) done = true;
+                else
+                {
+                    ++lv;
+                    base = stk[2 * lv];
+                    mask = stk[2 * lv + 1];
+                }
+            }
+            else
+            {
+                const int b = __ffsll((unsigned long long)mask) - 1;
+                mask &= mask - 1;
+                stk[2 * lv] = base;
+                stk[2 * lv + 1] = mask;
+                base = (base + b) << 6;
+                --lv;
+                eval = true;
+            }
+        }
+    }
+}
+
+// 64-ary wave search of the dictionary: rank of an arbitrary id (member i -> 2i+1, else 2*lb)
+__device__ __forceinline__ uint32_t wave_dict_rank(const DevSnapshot& s, uint64_t msb, uint64_t lsb, int32_t node)
+{
+    const NormTid x = norm_tid(msb, lsb, node);
+    auto key = [&](uint64_t i) { return NormTid{s.dict_hi[i], s.dict_lo[i], s.dict_node[i]}; };
+    if (s.n_dict == 0) return 0;
+    if (norm_cmp(key(s.n_dict - 1), x) < 0) return (uint32_t)(2 * s.n_dict);   // newer than every id (new txns)
+    const uint64_t lb = wave_lower_bound(0, s.n_dict, key, [&](const NormTid& v) { return norm_cmp(v, x) < 0; });
+    bool eq = false;
+    if (lb < s.n_dict) eq = norm_cmp(key(lb), x) == 0;
+    return (uint32_t)(2 * lb + (eq ? 1 : 0));
+}
+
+// ---- LDS multi-list union with 2-D list addressing ------------------------------------------
+
+
+
+
+
+__device__ __forceinline__ uint64_t fregion_bytes(uint32_t nk, uint32_t U, uint32_t pairs)
+{
+    return ((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + pairs) * 4 + 7) & ~7ull;
+}
+
+struct FChunk {
+    uint64_t cur = 0, end = 0;
+    __device__ __forceinline__ uint64_t take(BatchCtl* ctl, uint64_t n)
+    {
+        if (n > end - cur)
+        {
+            const uint64_t sz = n > F_REGION_CHUNK ? n : F_REGION_CHUNK;
+            unsigned long long base = 0;
+            if (lane_id() == 0) base = atomicAdd(&ctl->reg_top, (unsigned long long)sz);
+            base = uniform64(base);
+            if (base + sz > ctl->reg_cap && lane_id() == 0) atomicOr(&ctl->overflow, 8u);
+            cur = base;
+            end = base + sz;
+        }
+        const uint64_t r = cur;
+        cur += n;
+        return r;
+    }
+};
+
+__global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBufs b)
+{
+    __shared__ FusedLds lds_all[FWAVES];
+    FusedLds& L = lds_all[threadIdx.x >> 6];
+    const uint32_t lane = lane_id(), g = lane >> 3, j = lane & 7;
+    const uint64_t n = b.n_txns;
+    const uint64_t nw = (uint64_t)gridDim.x * FWAVES;
+    FChunk ralloc;
+    const bool incl = s.start_inclusive != 0;
+
+    for (uint64_t t = (uint64_t)blockIdx.x * FWAVES + (threadIdx.x >> 6); t < n; t += nw)
+    {
+        const uint64_t k0 = b.q_key_off[t];
+        const uint32_t np = (uint32_t)(b.q_key_off[t + 1] - k0);
+        if (np > FMAXP)
+        {
+            if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
+            continue;
+        }
+        // ---- encode the request (PreAccept.java:251-261)
+        const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t];
+        const int32_t tn = b.q_txn_node[t];
+        const uint64_t em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
+        const int32_t en = b.q_exec_node[t];
+        const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
+        if (kinds == 0)
+        {
+            if (lane == 0) set_error_f(b.ctl, ERR_INVAL);
+            continue;
+        }
+        const int cls = kinds_class(kinds);
+        const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
+        const uint32_t S = wave_dict_rank(s, em, el, en);
+        const uint32_t self = same ? 0u : wave_dict_rank(s, tm, tl, tn);
+        const int64_t epoch = (int64_t)(em >> 15);
+        const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
+
+        // ---- per key: slice, CommandsForKey lookup (lane p < np), then broadcast to group p
+        int64_t pkey = 0;
+        uint32_t pki = NO_KEY, pslice = 0;
+        KeyRec pkr{};
+        if (lane < np)
+        {
+            pkey = b.q_keys[k0 + lane];
+            bool in_slice = s.n_slices == 0;
+            for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
+                in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], pkey);
+            pslice = in_slice ? 1u : 0u;
+            if (in_slice && s.n_keys)
+            {
+                uint64_t h = key_hash(pkey) & s.khash_mask;
+                while (true)
+                {
+                    const KeySlot ks = s.khash[h];
+                    if (ks.idx == KEY_EMPTY) break;
+                    if (ks.key == pkey) { pki = ks.idx; break; }
+                    h = (h + 1) & s.khash_mask;
+                }
+                if (pki != NO_KEY) pkr = s.krec[pki];
+            }
+            L.key[lane] = pkey;
+        }
+        const bool gact = g < np;
+        const int64_t key = __shfl(pkey, g, 64);
+        const uint32_t ki = __shfl(pki, g, 64);
+        const bool in_slice = __shfl(pslice, g, 64) != 0;
+        KeyRec kr;
+        kr.seg_lo = __shfl(pkr.seg_lo, g, 64);
+        kr.seg_hi = __shfl(pkr.seg_hi, g, 64);
+        kr.w_lo = __shfl(pkr.w_lo, g, 64);
+        kr.w_hi = __shfl(pkr.w_hi, g, 64);
+        kr.last_txn = __shfl(pkr.last_txn, g, 64);
+        kr.last_wexec = __shfl(pkr.last_wexec, g, 64);
+        kr.pruned = __shfl(pkr.pruned, g, 64);
+        kr.maw = __shfl(pkr.maw, g, 64);
+        const bool has_cfk = gact && ki != NO_KEY;
+
+        // ---- K1: end = insertPos(S), M = maxCommittedWriteBefore (CommandsForKey.java:912-928)
+        const uint64_t lo = kr.seg_lo, hi = kr.seg_hi;
+        const bool tail = !has_cfk || hi == lo || kr.last_txn < S;
+        const uint64_t end = grp_lower_bound(has_cfk && !tail, lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
+                                             [&](uint32_t v) { return v < S; });
+        const uint64_t end_g = tail ? hi : end;
+        const uint64_t wlo = kr.w_lo, whi = kr.w_hi;
+        const bool wtail = !has_cfk || whi == wlo || kr.last_wexec < S;
+        const uint64_t wsearch = grp_lower_bound(has_cfk && !wtail, wlo, whi, [&](uint64_t i) { return s.w[i].x; },
+                                                 [&](uint32_t v) { return v < S; });
+        const uint64_t wpos = !has_cfk ? wlo : (whi == wlo ? wlo : (kr.last_wexec < S ? whi : wsearch));
+        uint32_t wprev = 0;
+        if (has_cfk && wpos > wlo) wprev = (wpos == whi) ? kr.last_wexec : s.w[wpos - 1].x;
+        const uint32_t M = (s.elide && has_cfk && wpos > wlo) ? wprev : 1u;
+
+        // prunedBefore substitute (:952-965)
+        uint32_t extra = 0;
+        if (has_cfk && kr.pruned != 0 && S <= kr.pruned)
+        {
+            if (kr.maw < 0) { if (j == 0) set_error_f(b.ctl, ERR_STATE); }
+            else
+            {
+                const uint64_t idx = wpos <= (uint64_t)kr.maw ? wpos : (uint64_t)kr.maw;
+                extra = s.w[idx].y;
+                if (extra == self) extra = 0;
+            }
+        }
+
+        uint32_t c0 = 0, c1 = 0, nlt = 0;
+        bool ovf = false, dup = false;
+        auto node_bits = [&](int lv, uint64_t n0, uint64_t nlo, uint64_t nhi) -> uint32_t {
+            const uint4* p4 = reinterpret_cast<const uint4*>(s.lvl[cls][lv] + n0);
+            const uint4 a = p4[0], c = p4[1];
+            const uint32_t v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+            uint32_t bits = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (n0 + i >= nlo && n0 + i <= nhi && v[i] >= M) bits |= 1u << i;
+            return bits;
+        };
+        auto leaf = [&](uint64_t n0) {
+            const uint4* p4 = reinterpret_cast<const uint4*>(s.ent + n0);
+            uint4 q[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = p4[i];
+            uint32_t w0 = 0, w1 = 0, lt = 0, eq = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+            {
+                const uint32_t tau = (i & 1) ? q[i >> 1].z : q[i >> 1].x;
+                const uint32_t txw = (i & 1) ? q[i >> 1].w : q[i >> 1].y;
+                const uint64_t e = n0 + i;
+                const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
+                const bool want = e >= lo && e < end_g && tau >= M && ((kinds >> kd) & 1) && r != self;
+                const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;   // !managesExecution -> directKeyDeps
+                w0 |= (want && !is1) ? (1u << i) : 0u;
+                w1 |= (want && is1) ? (1u << i) : 0u;
+                lt += (want && !is1 && r < extra) ? 1u : 0u;
+                eq |= (want && r == extra) ? 1u : 0u;
+            }
+            const uint32_t n0c = __popc(w0), n1c = __popc(w1);
+            const uint32_t i0 = grp_incl_scan(n0c), i1 = grp_incl_scan(n1c);
+            const uint32_t t0 = __shfl(i0, (lane & ~7u) | 7u, 64), t1 = __shfl(i1, (lane & ~7u) | 7u, 64);
+            if (c0 + t0 <= FCAP0 && c1 + t1 <= FCAP1)
+            {
+                uint32_t p0 = c0 + i0 - n0c, p1 = c1 + i1 - n1c;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                {
+                    const uint32_t r = ((i & 1) ? q[i >> 1].w : q[i >> 1].y) & RANK_MASK;
+                    if (w0 & (1u << i)) L.st0[g][p0++] = r;
+                    if (w1 & (1u << i)) L.st1[g][p1++] = r;
+                }
+            }
+            else ovf = true;
+            c0 += t0;
+            c1 += t1;
+            if (extra)
+            {
+                nlt += grp_sum(lt);
+                dup = dup || grp_sum(eq) != 0;
+            }
+        };
+        grp_descent(has_cfk, lo, end_g, s.n_levels, node_bits, leaf, L.stk[g]);
+
+        // ---- K4: range commands containing the key + the redundant-before entry
+        uint32_t rc = 0;
+        uint64_t rbv = NO_RB;
+        if (s.n_rb)
+        {
+            const uint64_t c = grp_lower_bound(gact, 0, s.n_rb, [&](uint64_t i) { return s.rb_start[i]; },
+                                               [&](int64_t v) { return incl ? v <= key : v < key; });
+            if (gact && c > 0)
+            {
+                const uint64_t e = c - 1;
+                if (range_contains(s.start_inclusive, s.rb_start[e], s.rb_end[e], key))
+                {
+                    const uint32_t wm = s.rb_wm[e];
+                    if (!(epoch < s.rb_e0[e] || mine >= s.rb_e1[e]) && wm != 0) rbv = ((uint64_t)s.rb_rid[e] << 32) | wm;
+                }
+            }
+        }
+        if (s.n_rent)
+        {
+            const bool ract = gact && in_slice;
+            const uint64_t rhi = grp_lower_bound(ract, 0, s.n_rent, [&](uint64_t i) { return s.r_start[i]; },
+                                                 [&](int64_t v) { return incl ? v <= key : v < key; });
+            auto end_ok = [&](int64_t e) { return incl ? e > key : e >= key; };
+            auto rnode_bits = [&](int lv, uint64_t n0, uint64_t nlo, uint64_t nhi) -> uint32_t {
+                const int64_t* pv = s.rlvl[cls][lv] + n0;
+                uint32_t bits = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (n0 + i >= nlo && n0 + i <= nhi && end_ok(pv[i])) bits |= 1u << i;
+                return bits;
+            };
+            auto rleaf = [&](uint64_t n0) {
+                uint32_t wbits = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                {
+                    const uint64_t e = n0 + i;
+                    const uint32_t txw = s.r_txw[e];
+                    const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
+                    // STARTED_BEFORE, testKind, contains key, self (InMemoryCommandStore.java:906-956)
+                    if (e < rhi && end_ok(s.r_end[e]) && r < S && ((kinds >> kd) & 1) && r != self) wbits |= 1u << i;
+                }
+                const uint32_t nc = __popc(wbits);
+                const uint32_t inc = grp_incl_scan(nc);
+                const uint32_t tot = __shfl(inc, (lane & ~7u) | 7u, 64);
+                if (rc + tot <= FCAPR)
+                {
+                    uint32_t pos = rc + inc - nc;
+                    for (int i = 0; i < 8; ++i)
+                        if (wbits & (1u << i))
+                            L.rs[g][pos++] = ((uint64_t)s.r_rid[n0 + i] << 32) | (s.r_txw[n0 + i] & RANK_MASK);
+                }
+                else ovf = true;
+                rc += tot;
+            };
+            grp_descent(ract, 0, rhi, s.n_rlevels, rnode_bits, rleaf, L.stk[g]);
+        }
+        if (gact && j == 0) L.rs[g][FCAPR] = rbv;
+
+        // any key overflowing its staging -> defer the whole request to the split kernels
+        if (ballot(ovf))
+        {
+            if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
+            continue;
+        }
+        const bool has_extra = extra != 0 && !dup;
+        // insert the prunedBefore substitute at its sorted position (class 0 list)
+        if (ballot(has_extra && gact))
+        {
+            wave_lds_sync();
+            uint32_t vals[FCAP0 / 8];
+#pragma unroll
+            for (int i = 0; i < FCAP0 / 8; ++i)
+            {
+                const uint32_t idx = j + 8 * i;
+                vals[i] = (has_extra && gact && idx >= nlt && idx < c0) ? L.st0[g][idx] : 0u;
+            }
+            wave_lds_sync();
+            if (has_extra && gact)
+            {
+                if (c0 + 1 > FCAP0) ovf = true;
+                else
+                {
+#pragma unroll
+                    for (int i = 0; i < FCAP0 / 8; ++i)
+                    {
+                        const uint32_t idx = j + 8 * i;
+                        if (idx >= nlt && idx < c0) L.st0[g][idx + 1] = vals[i];
+                    }
+                    if (j == 0) L.st0[g][nlt] = extra;
+                }
+            }
+            if (ballot(ovf))
+            {
+                if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
+                continue;
+            }
+        }
+        const uint32_t cnt0 = c0 + (has_extra ? 1u : 0u);
+
+        // ---- K2: build the three maps in registers (lane = element, <= 64 per map)
+        const uint32_t q0 = __shfl(cnt0, lane * 8, 64), q1 = __shfl(c1, lane * 8, 64), qr = __shfl(rc, lane * 8, 64);
+        const uint64_t qrb = __shfl(rbv, lane * 8, 64);
+        const uint32_t sh_qr = __shfl(qr, lane >> 1, 64);
+        const uint64_t sh_rb = __shfl(qrb, lane >> 1, 64);
+        const uint32_t rl = lane < 2 * np ? ((lane & 1) ? (sh_rb != NO_RB ? 1u : 0u) : sh_qr) : 0u;
+        const uint32_t tot0 = uniform(wave_sum(lane < np ? q0 : 0u));
+        const uint32_t tot1 = uniform(wave_sum(lane < np ? q1 : 0u));
+        const uint32_t totR = uniform(wave_sum(rl));
+        if (tot0 > 64 || tot1 > 64 || totR > 64)
+        {
+            if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
+            continue;
+        }
+        wave_lds_sync();
+        // keyDeps (class 0) and directKeyDeps (class 1): lists = keys in request order
+        for (int c = 0; c < 2; ++c)
+        {
+            const int m = c == 0 ? 0 : 2;
+            const uint32_t tot = c == 0 ? tot0 : tot1;
+            const uint32_t cnt_l = c == 0 ? q0 : q1;               // lane p < np: length of key p's list
+            const uint32_t inc = wave_incl_scan(lane < np ? cnt_l : 0u);
+            const uint32_t start_l = inc - (lane < np ? cnt_l : 0u);
+            if (tot == 0)
+            {
+                if (lane == 0) { b.sz[(3 * m) * n + t] = 0; b.sz[(3 * m + 1) * n + t] = 0; b.sz[(3 * m + 2) * n + t] = 0; }
+                continue;
+            }
+            // element e = lane: its key a and value
+            uint32_t a = 0, a_start = 0;
+            for (uint32_t pp = 1; pp < np; ++pp)
+            {
+                const uint32_t sp = __shfl(start_l, pp, 64);
+                if (lane >= sp) { a = pp; a_start = sp; }
+            }
+            const bool live = lane < tot;
+            const uint32_t x = live ? (c == 0 ? L.st0[a][lane - a_start] : L.st1[a][lane - a_start]) : 0xFFFFFFFFu;
+            // sort (rank, element) ascending; dedup ranks -> values, body = unique rank of each element
+            uint64_t key = live ? (((uint64_t)x << 8) | lane) : ~0ull;
+            uint32_t pay = 0;
+            wave_bitonic64(key, pay);
+            const uint32_t xr = (uint32_t)(key >> 8);
+            const uint64_t prevk = __shfl_up(key, 1, 64);
+            const bool valid = key != ~0ull;
+            const bool uniq = valid && (lane == 0 || (uint32_t)(prevk >> 8) != xr);
+            const uint64_t um = ballot(uniq);
+            const uint32_t U = __popcll(um);
+            const uint32_t ur = __popcll(um & ((2ull << lane) - 1)) - 1;     // rank among distinct values
+            const uint64_t nem = ballot(lane < np && cnt_l > 0);
+            const uint32_t nk = __popcll(nem);
+            const uint64_t bytes = fregion_bytes(nk, U, tot);
+            const uint64_t ro = ralloc.take(b.ctl, bytes);
+            const bool fits = ro + bytes <= b.ctl->reg_cap;
+            if (lane == 0)
+            {
+                b.sz[(3 * m) * n + t] = fits ? nk : 0;
+                b.sz[(3 * m + 1) * n + t] = fits ? U : 0;
+                b.sz[(3 * m + 2) * n + t] = fits ? nk + tot : 0;
+                b.t_reg[(uint64_t)m * n + t] = ro;
+            }
+            if (fits)
+            {
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
+                if (lane < np && cnt_l > 0)
+                {
+                    const uint32_t kk = mbcnt(nem);
+                    okeys[kk] = L.key[lane];
+                    ok2t[kk] = (int32_t)(nk + start_l + cnt_l);      // absolute end offset (RelationMultiMap.java:245-257)
+                }
+                if (uniq) otx[ur] = (xr - 1) >> 1;
+                if (valid) ok2t[nk + (uint32_t)(key & 0xFF)] = (int32_t)ur;
+            }
+        }
+
+        if (totR == 0)
+        {
+            if (lane == 0) { b.sz[3 * n + t] = 0; b.sz[4 * n + t] = 0; b.sz[5 * n + t] = 0; }
+            continue;
+        }
+        {
+            // rangeDeps: element e = lane: per key [command pairs] then [redundant pair]
+            const uint32_t inc = wave_incl_scan(rl);
+            const uint32_t start_l = inc - rl;
+            uint32_t a = 0, a_start = 0;
+            for (uint32_t pp = 1; pp < 2 * np; ++pp)
+            {
+                const uint32_t sp = __shfl(start_l, pp, 64);
+                if (lane >= sp) { a = pp; a_start = sp; }
+            }
+            const bool live = lane < totR;
+            const uint64_t pr = live ? ((a & 1) ? L.rs[a >> 1][FCAPR] : L.rs[a >> 1][lane - a_start]) : ~0ull;
+            // unique (range, txnId) pairs in (Range.compare, TxnId.compareTo) order
+            uint64_t key = pr;
+            uint32_t pay = 0;
+            wave_bitonic64(key, pay);
+            const uint64_t prevk = __shfl_up(key, 1, 64);
+            const bool valid = key != ~0ull;
+            const bool uniq = valid && (lane == 0 || prevk != key);
+            const uint64_t um = ballot(uniq);
+            const uint32_t UPn = __popcll(um);
+            // compact the unique pairs to lanes 0..UPn-1
+            uint32_t src = 0;
+            {
+                // lane i takes the i-th unique pair: find its source lane by scanning the mask
+                uint64_t mm = um;
+                for (uint32_t i = 0; i < 64; ++i)
+                {
+                    if (!mm) break;
+                    const uint32_t bpos = __ffsll((unsigned long long)mm) - 1;
+                    if (lane == i) src = bpos;
+                    mm &= mm - 1;
+                }
+            }
+            const uint64_t upair = __shfl(key, src, 64);
+            const bool uplive = lane < UPn;
+            const uint32_t rid = (uint32_t)(upair >> 32), rk = (uint32_t)upair;
+            const uint32_t prid = __shfl_up(rid, 1, 64);
+            const bool gfirst = uplive && (lane == 0 || prid != rid);
+            const uint64_t gm = ballot(gfirst);
+            const uint32_t nR = __popcll(gm);
+            // group end offsets: the next group's first index (or UPn)
+            // distinct txnIds: sort (rank, pair position)
+            uint64_t k2 = uplive ? (((uint64_t)rk << 8) | lane) : ~0ull;
+            uint32_t pay2 = 0;
+            wave_bitonic64(k2, pay2);
+            const uint64_t prev2 = __shfl_up(k2, 1, 64);
+            const bool v2 = k2 != ~0ull;
+            const bool uq2 = v2 && (lane == 0 || (uint32_t)(prev2 >> 8) != (uint32_t)(k2 >> 8));
+            const uint64_t um2 = ballot(uq2);
+            const uint32_t UR = __popcll(um2);
+            const uint32_t ur2 = __popcll(um2 & ((2ull << lane) - 1)) - 1;
+            const uint64_t bytes = fregion_bytes(nR, UR, UPn);
+            const uint64_t ro = ralloc.take(b.ctl, bytes);
+            const bool fits = ro + bytes <= b.ctl->reg_cap;
+            if (lane == 0)
+            {
+                b.sz[3 * n + t] = fits ? nR : 0;
+                b.sz[4 * n + t] = fits ? UR : 0;
+                b.sz[5 * n + t] = fits ? nR + UPn : 0;
+                b.t_reg[(uint64_t)1 * n + t] = ro;
+            }
+            if (fits)
+            {
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nR);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + UR);
+                if (gfirst)
+                {
+                    const uint32_t gi = mbcnt(gm);
+                    // end of this group = start of the next group (or UPn)
+                    const uint64_t later = gm & ~((2ull << lane) - 1);
+                    const uint32_t gend = later ? (uint32_t)(__ffsll((unsigned long long)later) - 1) : UPn;
+                    okeys[gi] = (int64_t)rid;
+                    ok2t[gi] = (int32_t)(nR + gend);
+                }
+                if (uq2) otx[ur2] = ((uint32_t)(k2 >> 8) - 1) >> 1;
+                if (v2) ok2t[nR + (uint32_t)(k2 & 0xFF)] = (int32_t)ur2;
+            }
+        }
+    }
+}
+
+hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+{
+    if (!b.n_txns) return hipSuccess;
+    const uint64_t need = (b.n_txns + FWAVES - 1) / FWAVES;
+    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)device_cu_count() * 8);
+    k_resolve<<<grid, 64 * FWAVES, 0, st>>>(s, b);
+    return hipGetLastError();
+}
+
+// ---- deferred requests -> sub-batch for the split kernels, and back -------------------------
+__global__ void k_defer_counts(BatchBufs b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nd) return;
+    const uint32_t t = deferred[i];
+    cnt[i] = (uint32_t)(b.q_key_off[t + 1] - b.q_key_off[t]);
+}
+
+__global__ void k_defer_gather(BatchBufs b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off, BatchBufs sub,
+                               uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em, uint64_t* o_el, int32_t* o_en,
+                               int64_t* o_me, uint64_t* o_ko, int64_t* o_k)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (i >= nd) return;
+    const uint32_t t = deferred[i];
+    const uint32_t lane = lane_id();
+    if (lane == 0)
+    {
+        o_tm[i] = b.q_txn_msb[t]; o_tl[i] = b.q_txn_lsb[t]; o_tn[i] = b.q_txn_node[t];
+        o_em[i] = b.q_exec_msb[t]; o_el[i] = b.q_exec_lsb[t]; o_en[i] = b.q_exec_node[t];
+        if (b.q_min_epoch) o_me[i] = b.q_min_epoch[t];
+        if (o_ko != sub_off)
+        {
+            o_ko[i] = sub_off[i];
+            if (i == nd - 1) o_ko[nd] = sub_off[nd];
+        }
+    }
+    const uint64_t s0 = b.q_key_off[t], len = b.q_key_off[t + 1] - s0, d0 = sub_off[i];
+    for (uint64_t k = lane; k < len; k += 64) o_k[d0 + k] = b.q_keys[s0 + k];
+}
+
+__global__ void k_defer_scatter(BatchBufs b, const uint32_t* deferred, uint64_t nd, const uint32_t* sub_sz,
+                                const uint64_t* sub_reg)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nd) return;
+    const uint64_t t = deferred[i], n = b.n_txns;
+    for (int a = 0; a < 9; ++a) b.sz[(uint64_t)a * n + t] = sub_sz[(uint64_t)a * nd + i];
+    for (int m = 0; m < 3; ++m) b.t_reg[(uint64_t)m * n + t] = sub_reg[(uint64_t)m * nd + i];
+}
+
+hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st)
+{
+    if (!nd) return hipSuccess;
+    k_defer_counts<<<(unsigned)((nd + 255) / 256), 256, 0, st>>>(b, deferred, nd, cnt);
+    return hipGetLastError();
+}
+
+hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
+                            const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,
+                            uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, hipStream_t st)
+{
+    if (!nd) return hipSuccess;
+    k_defer_gather<<<(unsigned)((nd + 3) / 4), 256, 0, st>>>(b, deferred, nd, sub_off, sub, o_tm, o_tl, o_tn, o_em, o_el,
+                                                             o_en, o_me, o_ko, o_k);
+    return hipGetLastError();
+}
+
+hipError_t run_defer_scatter(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint32_t* sub_sz,
+                             const uint64_t* sub_reg, hipStream_t st)
+{
+    if (!nd) return hipSuccess;
+    k_defer_scatter<<<(unsigned)((nd + 255) / 256), 256, 0, st>>>(b, deferred, nd, sub_sz, sub_reg);
+    return hipGetLastError();
+}
+
+}  // namespace adx

@@ -102,7 +102,8 @@ typedef struct ad_config {
     int32_t device;                 /* HIP device ordinal                                   */
     int32_t range_start_inclusive;  /* 0: Range.EndInclusive (s,e]; 1: StartInclusive [s,e) */
     int32_t elide;                  /* CommandsForKey.ELIDE_TRANSITIVE_DEPENDENCIES (:173), 1 */
-    int32_t reserved;
+    int32_t path;                   /* 0: fused per-request kernel, split kernels for the rest
+                                     * (default); 1: split kernels only (testing)            */
     /* the store's owned ranges (SafeCommandStore.ranges(); slice in mapReduceForKey,
      * InMemoryCommandStore.java:280). n_slices == 0 means "owns every key". */
     uint64_t n_slices;
@@ -181,7 +182,9 @@ typedef struct ad_stats {
     double   ms_ingest;
     /* per-stage device time (HIP events): 0 encode (K0), 1 conflict scan (K1), 2 range probe
      * (K4), 3 build sizing (K2 pass 1), 4 offsets scan, 5 build emit (K2 pass 2) */
-    double   ms_stage[8];
+    double   ms_stage[8];            /* path 0: 0 fused resolve, 1 deferred requests (split),
+                                      * 4 offsets, 5 pack */
+    uint64_t n_deferred;             /* requests resolved by the split kernels (path 0)       */
     uint64_t bytes_stage[8];         /* algorithmic bytes per stage            */
 } ad_stats;
 

@@ -12,14 +12,18 @@ from accord_deps import native, synth
 pytestmark = pytest.mark.gpu
 
 
-def _compare(w, oracle, elide=1):
+def _compare(w, oracle, elide=1, paths=(0, 1)):
+    """Both device paths: 0 = fused per-request kernel (+ split fallback), 1 = split kernels only."""
     exp = oracle.resolve(w, elide=elide)
-    got = native.resolve(w, elide=elide)
-    ok, why = got.equals(exp, detail=True)
-    if not ok:
-        mm = got.first_mismatch(exp)
-        raise AssertionError("%s: %s; first mismatch %r" % (w.name, why, mm))
-    return got, exp
+    first = None
+    for path in paths:
+        got = native.resolve(w, elide=elide, path=path)
+        ok, why = got.equals(exp, detail=True)
+        if not ok:
+            mm = got.first_mismatch(exp)
+            raise AssertionError("%s path %d: %s; first mismatch %r" % (w.name, path, why, mm))
+        first = first or got
+    return first, exp
 
 
 @pytest.mark.parametrize("seed", range(40))
@@ -67,7 +71,15 @@ def test_big_requests(oracle):
     # a hot key with thousands of live entries -> per-probe outputs beyond the LDS staging
     w = synth.config2(n_txns=200, n_keys=50, n_hist_entries=40000, keys_per_txn=8, tail_unapplied=3000,
                       esp_frac=0.2)
-    _compare(w, oracle)
+    got, _ = _compare(w, oracle)
+    assert got.stats["n_deferred"] > 0          # exercised the fused -> split hand-off
+
+
+def test_many_keys_deferred(oracle):
+    # requests with more than 8 keys take the split kernels from the fused kernel
+    w = synth.random_small(2024, n_keys=200, n_hist_txns=2000, n_txns=300, max_keys=20, n_range_cmds=50)
+    got, _ = _compare(w, oracle)
+    assert got.stats["n_deferred"] > 0
 
 
 def test_empty_batch_and_empty_snapshot(oracle):
