@@ -18,6 +18,7 @@ AD_E_INCONSISTENT_ID = -6
 AD_E_NOT_LOADED = -7
 AD_E_STATE = -8
 AD_E_CAPACITY = -9
+AD_E_SPACE = -10
 
 AD_MAP_KEY, AD_MAP_RANGE, AD_MAP_DIRECT_KEY = 0, 1, 2
 NMAPS = 3
@@ -86,6 +87,22 @@ class AdDepsResult(C.Structure):
 class AdGraphSoa(C.Structure):
     _fields_ = [("n_txns", C.c_uint64), ("exec_msb", P), ("exec_lsb", P), ("exec_node", P), ("kind", P),
                 ("key_off", P), ("keys", P), ("dep_off", P), ("deps", P)]
+
+
+class AdParts(C.Structure):
+    _fields_ = [("n_parts", C.c_uint64), ("n_key_words", C.c_uint64), ("n_ids", C.c_uint64), ("n_k2t", C.c_uint64),
+                ("hdr", P), ("keys", P), ("ids", P), ("k2t", P),
+                ("cap_parts", C.c_uint64), ("cap_key_words", C.c_uint64), ("cap_ids", C.c_uint64),
+                ("cap_k2t", C.c_uint64)]
+
+
+class AdMerged(C.Structure):
+    _fields_ = [("n_txns", C.c_uint64), ("txn_base", C.c_uint64),
+                ("keys_off", P * NMAPS), ("keys", P * NMAPS),
+                ("txn_off", P * NMAPS), ("txns", P * NMAPS),
+                ("k2t_off", P * NMAPS), ("k2t", P * NMAPS),
+                ("n_keys", C.c_uint64 * NMAPS), ("n_ids", C.c_uint64 * NMAPS), ("n_k2t", C.c_uint64 * NMAPS),
+                ("ms_device", C.c_double)]
 
 
 def ptr(a):

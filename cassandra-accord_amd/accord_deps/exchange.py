@@ -1,0 +1,158 @@
+"""Multi-GPU path: one CommandStore per GPU, per-store partials exchanged over RCCL and merged
+on the GPU that owns each request.
+
+Reference shape: a node's key space is split into contiguous range slices, one CommandStore each
+(CommandStores.java:453-471, ShardDistributor.EvenSplit.split ShardDistributor.java:106-156); a
+PreAccept is sent to every store owning one of its keys, each computes its PartialDeps
+(PreAccept.calculatePartialDeps, PreAccept.java:245-267) and the results are reduced with
+PartialDeps.with (CommandStores.mapReduce :576-593, PreAccept.reduce PreAccept.java:140-156).
+
+Here rank g of `world` owns token slice g. One step:
+  1. resolve the local batch (requests touching slice g) on the GPU        (ad_deps_batch_device)
+  2. export the non-empty maps as parts, grouped by owning rank            (ad_parts_export)
+  3. all-to-all of part counts, then of hdr / keys / ids / k2t             (RCCL via torch.distributed)
+  4. K3: merge the parts of the owned requests                             (ad_parts_merge)
+Request t (global index) is owned by rank `owner(t)`: contiguous blocks of the global batch.
+
+The exchange protocol (`ShardExchange`) is independent of where parts come from: the product
+engine is `GpuEngine` (libaccord_deps); the CPU tests drive the same protocol over gloo with a
+CPU engine built on the oracle.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _abi as A
+from .model import Queries
+
+
+def owner_bases(n_total, world):
+    """First global request index owned by each rank (+ n_total): contiguous blocks."""
+    return [(d * n_total) // world for d in range(world)] + [n_total]
+
+
+def route(queries, lo, hi, start_inclusive=False):
+    """The requests a store owning the token slice from lo to hi receives, with their keys
+    restricted to the slice (mapReduceForKey skips keys the store does not own,
+    InMemoryCommandStore.java:280; CommandStores.mapReduce only asks stores that intersect).
+    Returns (local Queries, global request index int64 ascending)."""
+    k = queries.keys
+    sel = ((k >= lo) & (k < hi)) if start_inclusive else ((k > lo) & (k <= hi))
+    cs = np.zeros(len(k) + 1, np.int64)
+    np.cumsum(sel, out=cs[1:])
+    ko = queries.key_off.astype(np.int64)
+    counts = cs[ko[1:]] - cs[ko[:-1]]
+    idx = np.nonzero(counts)[0].astype(np.int64)
+    key_off = np.zeros(len(idx) + 1, np.uint64)
+    key_off[1:] = np.cumsum(counts[idx])
+    me = None if queries.min_epoch is None else queries.min_epoch[idx]
+    return Queries(queries.txn.take(idx), queries.exec.take(idx), key_off, k[sel], me), idx
+
+
+class PartsBuffers:
+    """Growable device arrays in the ad_parts transport format."""
+
+    def __init__(self, device):
+        self.device = device
+        self.hdr = self.keys = self.ids = self.k2t = None
+        self.ensure(1, 1, 1, 1)
+
+    def ensure(self, parts, key_words, ids, k2t):
+        def grow(t, n, dtype):
+            if t is None or t.numel() < n:
+                return torch.empty(max(int(n * 1.25), 16), dtype=dtype, device=self.device)
+            return t
+        self.hdr = grow(self.hdr, 4 * parts, torch.int64)
+        self.keys = grow(self.keys, key_words, torch.int64)
+        self.ids = grow(self.ids, 3 * ids, torch.int64)
+        self.k2t = grow(self.k2t, k2t, torch.int32)
+
+    def soa(self, n=None):
+        p = A.AdParts()
+        p.hdr, p.keys, p.ids, p.k2t = (self.hdr.data_ptr(), self.keys.data_ptr(), self.ids.data_ptr(),
+                                       self.k2t.data_ptr())
+        p.cap_parts = self.hdr.numel() // 4
+        p.cap_key_words = self.keys.numel()
+        p.cap_ids = self.ids.numel() // 3
+        p.cap_k2t = self.k2t.numel()
+        if n is not None:
+            p.n_parts, p.n_key_words, p.n_ids, p.n_k2t = (int(x) for x in n)
+        return p
+
+
+class GpuEngine:
+    """Product engine: a DeviceCommandStore with its local batch resident in HBM."""
+
+    def __init__(self, store, qdev, txn_index, device, stream=None):
+        self.store = store
+        self.qdev = qdev
+        self.device = device
+        self.txn_index = torch.from_numpy(np.ascontiguousarray(txn_index, np.int64)).to(device)
+        self.stream = stream
+        self.send = PartsBuffers(device)
+        self.recv = PartsBuffers(device)
+        self.last_stats = None
+
+    def resolve(self):
+        self.res, self.last_stats = self.store.deps_batch_device(self.qdev, self.stream)
+
+    def export(self, dest_first):
+        """-> (dict of 1-D send tensors, counts[n_dest, 4] int64)."""
+        while True:
+            p = self.send.soa()
+            rc, counts = self.store.export_parts(self.res, self.txn_index.data_ptr(), dest_first, p, self.stream)
+            if rc == A.AD_OK:
+                break
+            self.send.ensure(p.n_parts, p.n_key_words, p.n_ids, p.n_k2t)
+        return dict(hdr=self.send.hdr, keys=self.send.keys, ids=self.send.ids, k2t=self.send.k2t), \
+            counts.astype(np.int64)
+
+    def recv_buffers(self, totals):
+        self.recv.ensure(*totals)
+        return dict(hdr=self.recv.hdr, keys=self.recv.keys, ids=self.recv.ids, k2t=self.recv.k2t)
+
+    def merge(self, totals, src_parts, txn_base, n_owned):
+        return self.store.merge_parts(self.recv.soa(totals), src_parts, txn_base, n_owned, self.stream)
+
+
+# element multiplicity of each transport array per counted unit
+_UNITS = (("hdr", 4), ("keys", 1), ("ids", 3), ("k2t", 1))
+
+
+class ShardExchange:
+    """The all-to-all + merge protocol of one rank."""
+
+    def __init__(self, engine, txn_index, n_total, rank, world, group=None, count_device=None):
+        self.engine = engine
+        self.rank, self.world = rank, world
+        self.group = group
+        bases = owner_bases(n_total, world)
+        self.txn_base = bases[rank]
+        self.n_owned = bases[rank + 1] - bases[rank]
+        ti = np.asarray(txn_index, np.int64)
+        if len(ti) > 1 and not np.all(ti[1:] > ti[:-1]):
+            raise ValueError("local requests must be in ascending global order")
+        self.dest_first = np.searchsorted(ti, np.asarray(bases[:world] + [n_total], np.int64)).astype(np.uint64)
+        self.dest_first[-1] = len(ti)
+        self.count_device = count_device
+
+    def step(self):
+        e = self.engine
+        e.resolve()
+        send, counts = e.export(self.dest_first)                      # counts[d] = parts, words, ids, k2t
+        dev = self.count_device
+        sc = torch.from_numpy(counts.reshape(-1).copy())
+        rc = torch.empty_like(sc)
+        if dev is not None:
+            sc, rc = sc.to(dev), rc.to(dev)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        rcounts = rc.cpu().numpy().reshape(self.world, 4)
+        totals = rcounts.sum(axis=0)
+        recv = e.recv_buffers(totals)
+        for a, (name, mult) in enumerate(_UNITS):
+            in_splits = [int(x) * mult for x in counts[:, a]]
+            out_splits = [int(x) * mult for x in rcounts[:, a]]
+            si = send[name][:sum(in_splits)]
+            ro = recv[name][:sum(out_splits)]
+            dist.all_to_all_single(ro, si, out_splits, in_splits, group=self.group)
+        return e.merge(totals, rcounts[:, 0], self.txn_base, self.n_owned)

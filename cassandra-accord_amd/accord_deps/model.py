@@ -312,6 +312,19 @@ class PartialDepsBatch:
         mm = self.maps[m]
         return int(len(mm.k2t) - len(mm.keys))
 
+    def window(self, first, count):
+        """Requests [first, first + count) as a batch of their own (offsets rebased)."""
+        maps = []
+        for mm in self.maps:
+            k0, k1 = int(mm.keys_off[first]), int(mm.keys_off[first + count])
+            t0, t1 = int(mm.txn_off[first]), int(mm.txn_off[first + count])
+            o0, o1 = int(mm.k2t_off[first]), int(mm.k2t_off[first + count])
+            maps.append(DepsMap(mm.keys_off[first:first + count + 1] - np.uint64(k0), mm.keys[k0:k1],
+                                None if mm.keys_end is None else mm.keys_end[k0:k1],
+                                mm.txn_off[first:first + count + 1] - np.uint64(t0), mm.txn.take(slice(t0, t1)),
+                                mm.k2t_off[first:first + count + 1] - np.uint64(o0), mm.k2t[o0:o1]))
+        return PartialDepsBatch(maps)
+
 
 @dataclass
 class Workload:

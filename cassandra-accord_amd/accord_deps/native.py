@@ -20,7 +20,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaccord_d
 
 EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error", "ad_cfk_load",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
-           "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_levels")
+           "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
+           "ad_copy_to_host", "ad_levels")
 
 
 class AccordDepsError(RuntimeError):
@@ -61,6 +62,11 @@ def lib():
         L.ad_dict.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                               C.POINTER(C.c_void_p)]
         L.ad_range_table.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ad_parts_export.argtypes = [C.c_void_p, C.POINTER(A.AdDepsResult), C.c_void_p, C.c_uint32, C.c_void_p,
+                                      C.c_void_p, C.POINTER(A.AdParts), C.c_void_p]
+        L.ad_parts_merge.argtypes = [C.c_void_p, C.POINTER(A.AdParts), C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64,
+                                     C.c_void_p, C.POINTER(A.AdMerged)]
+        L.ad_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
         L.ad_levels.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.POINTER(A.AdStats)]
         _lib = L
     return _lib
@@ -176,6 +182,80 @@ class DeviceCommandStore:
         out = A.AdDepsResult()
         self._check(lib().ad_deps_batch_device(self.h, C.byref(qdev), A.AD_SNAPSHOT, stream, C.byref(out)))
         return out, stats_dict(out.stats)
+
+    # ---- multi-GPU exchange (accord_deps.h "multi-GPU exchange") ----------------
+    def export_parts(self, res, txn_index_ptr, dest_first, parts, stream=None):
+        """Export the device result `res` as parts into the device arrays of `parts` (AdParts with
+        capacities). Returns (rc, dest_counts[n_dest, 4]); rc is AD_OK or AD_E_SPACE (sizes set in
+        `parts`, caller grows its buffers and calls again)."""
+        df = np.ascontiguousarray(dest_first, dtype=np.uint64)
+        n_dest = len(df) - 1
+        counts = np.zeros((n_dest, 4), np.uint64)
+        rc = lib().ad_parts_export(self.h, C.byref(res), txn_index_ptr, n_dest, A.ptr(df), stream,
+                                   C.byref(parts), A.ptr(counts))
+        if rc not in (A.AD_OK, A.AD_E_SPACE):
+            self._check(rc)
+        return rc, counts
+
+    def merge_parts(self, parts, src_parts, txn_base, n_owned, stream=None):
+        """K3: merge received parts (device AdParts, sources concatenated in slice order) into the
+        PartialDeps of requests [txn_base, txn_base + n_owned). Returns an AdMerged (device)."""
+        sp = np.ascontiguousarray(src_parts, dtype=np.uint64)
+        out = A.AdMerged()
+        self._check(lib().ad_parts_merge(self.h, C.byref(parts), len(sp), A.ptr(sp), txn_base, n_owned, stream,
+                                         C.byref(out)))
+        return out
+
+    def _d2h(self, p, n, dtype):
+        a = np.zeros(max(n, 0), dtype)
+        if n:
+            self._check(lib().ad_copy_to_host(self.h, A.ptr(a), p, a.nbytes))
+        return a
+
+    def merged_to_host(self, mg):
+        """Materialise an AdMerged into a PartialDepsBatch (ids as TxnIds, ranges as (start, end))."""
+        n = mg.n_txns
+        maps = []
+        for m in range(A.NMAPS):
+            ko = self._d2h(mg.keys_off[m], n + 1, np.uint64)
+            to = self._d2h(mg.txn_off[m], n + 1, np.uint64)
+            oo = self._d2h(mg.k2t_off[m], n + 1, np.uint64)
+            w = 2 if m == A.AD_MAP_RANGE else 1
+            kw = self._d2h(mg.keys[m], w * int(mg.n_keys[m]), np.int64)
+            ids = self._d2h(mg.txns[m], 3 * int(mg.n_ids[m]), np.int64).reshape(-1, 3)
+            k2t = self._d2h(mg.k2t[m], int(mg.n_k2t[m]), np.int32)
+            txn = Tids(ids[:, 0].view(np.uint64).copy(), ids[:, 1].view(np.uint64).copy(),
+                       ids[:, 2].astype(np.int32))
+            if m == A.AD_MAP_RANGE:
+                maps.append(DepsMap(ko, kw[0::2].copy(), kw[1::2].copy(), to, txn, oo, k2t))
+            else:
+                maps.append(DepsMap(ko, kw, None, to, txn, oo, k2t))
+        return PartialDepsBatch(maps)
+
+
+def device_queries(q, dev):
+    """Stage a Queries batch in HBM (torch tensors as allocator). Returns (AdQuerySoa of device
+    pointers, dict of the tensors that must stay alive)."""
+    import torch
+
+    def to_dev(a):
+        a = np.ascontiguousarray(a)
+        if a.dtype == np.uint64:
+            a = a.view(np.int64)
+        return torch.from_numpy(a).to(dev)
+    keep = {k: to_dev(v) for k, v in [
+        ("tm", q.txn.msb), ("tl", q.txn.lsb), ("tn", q.txn.node),
+        ("em", q.exec.msb), ("el", q.exec.lsb), ("en", q.exec.node),
+        ("ko", q.key_off), ("k", q.keys)]}
+    if q.min_epoch is not None:
+        keep["me"] = to_dev(np.asarray(q.min_epoch, np.int64))
+    s = A.AdQuerySoa()
+    s.n_txns = len(q)
+    s.txn_msb, s.txn_lsb, s.txn_node = keep["tm"].data_ptr(), keep["tl"].data_ptr(), keep["tn"].data_ptr()
+    s.exec_msb, s.exec_lsb, s.exec_node = keep["em"].data_ptr(), keep["el"].data_ptr(), keep["en"].data_ptr()
+    s.min_epoch = keep["me"].data_ptr() if "me" in keep else None
+    s.key_off, s.keys = keep["ko"].data_ptr(), keep["k"].data_ptr()
+    return s, keep
 
 
 def resolve(workload, device=0, elide=1, path=0):

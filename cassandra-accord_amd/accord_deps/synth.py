@@ -171,6 +171,14 @@ def shard_bounds(n_shards):
     return np.array(lo, dtype=object), np.array(hi, dtype=object)
 
 
+def cut_bounds(cuts):
+    """Slices of the i64 token space cut at the given ascending points: slice g runs from lo_g to hi_g
+    (the same shape as shard_bounds, for small workloads whose keys sit near 0)."""
+    lo = [-(1 << 63)] + [int(c) for c in cuts]
+    hi = [int(c) for c in cuts] + [(1 << 63) - 1]
+    return np.array(lo, dtype=object), np.array(hi, dtype=object)
+
+
 def config3(n_txns=64_000_000, keys_per_txn=4, n_keys=10_000_000, hist_frac=0.75, seed=0xACC0D003,
             tail_unapplied=2):
     """Config 3 (whole job): 64M txns over 10M uniform keys; first 75% are history (APPLIED except the
@@ -238,12 +246,26 @@ def config5(n_txns=1_000_000, keys_per_txn=4, n_keys=100_000, direct_frac=0.01, 
 
 
 def slice_workload(w, lo, hi):
-    """The part of workload `w` a CommandStore owning token range (lo, hi] sees: CFK keys in the
-    slice; every request, with its keys restricted to the slice (mapReduceForKey skips keys the
-    store does not own, InMemoryCommandStore.java:280). Range commands/redundant are kept whole
-    (the store slices them itself)."""
+    """The part of workload `w` a CommandStore owning the token range from lo to hi sees
+    ((lo, hi] for EndInclusive ranges, [lo, hi) for StartInclusive): the CommandsForKey of its
+    keys; every request, with its keys restricted to the slice (mapReduceForKey skips keys the
+    store does not own, InMemoryCommandStore.java:280); range commands with their ranges sliced
+    to the store (Ranges.slice(..., Minimal) at registration, InMemoryCommandStore.java:758-761;
+    commands left without ranges are not registered) and RedundantBefore sliced likewise."""
+    if w.slices is not None:
+        raise ValueError("slice_workload: workload already restricted to slices")
+    inc = bool(w.range_start_inclusive)
+
+    def inside(x):
+        return ((x >= lo) & (x < hi)) if inc else ((x > lo) & (x <= hi))
+
+    def clip(s0, e0):
+        s1 = np.maximum(s0, np.int64(lo))
+        e1 = np.minimum(e0, np.int64(hi))
+        return s1, e1, s1 < e1
+
     keys = w.cfk.keys
-    sel = (keys > lo) & (keys <= hi)
+    sel = inside(keys)
     ki = np.nonzero(sel)[0]
     if len(ki):
         e0, e1 = int(w.cfk.seg[ki[0]]), int(w.cfk.seg[ki[-1] + 1])
@@ -255,17 +277,44 @@ def slice_workload(w, lo, hi):
                       w.cfk.status[e0:e1],
                       None if w.cfk.pruned_before is None else w.cfk.pruned_before[sel])
     q = w.queries
-    qsel = (q.keys > lo) & (q.keys <= hi)
-    counts = np.add.reduceat(qsel.astype(np.int64), q.key_off[:-1].astype(np.int64)) if len(q.keys) else \
-        np.zeros(len(q), np.int64)
-    counts = np.where(np.diff(q.key_off.astype(np.int64)) == 0, 0, counts)
+    qsel = inside(q.keys)
+    cs = np.zeros(len(q.keys) + 1, np.int64)
+    np.cumsum(qsel, out=cs[1:])
+    ko = q.key_off.astype(np.int64)
+    counts = cs[ko[1:]] - cs[ko[:-1]]
     key_off = np.zeros(len(q) + 1, np.uint64)
     key_off[1:] = np.cumsum(counts)
     qq = Queries(q.txn, q.exec, key_off, q.keys[qsel], q.min_epoch)
-    out = Workload(w.name, cfk, w.cmds, w.redundant, qq, w.flags, dict(w.params), w.range_start_inclusive,
+
+    c = w.cmds
+    rs, re_, keep = clip(c.range_start, c.range_end)
+    cmd_of = np.repeat(np.arange(len(c.txn)), np.diff(c.range_off.astype(np.int64)))
+    per_cmd = np.bincount(cmd_of[keep], minlength=len(c.txn))
+    live = np.nonzero(per_cmd)[0]
+    roff = np.zeros(len(live) + 1, np.uint64)
+    roff[1:] = np.cumsum(per_cmd[live])
+    cmds = RangeCommands(c.txn.take(live), roff, rs[keep], re_[keep],
+                         None if c.erased is None else c.erased[live],
+                         None if c.historical is None else c.historical[live])
+    r = w.redundant
+    bs, be, bk = clip(r.range_start, r.range_end)
+    bi = np.nonzero(bk)[0]
+    red = Redundant(bs[bi], be[bi], r.start_epoch[bi], r.end_epoch[bi], r.wm.take(bi))
+    out = Workload(w.name, cfk, cmds, red, qq, w.flags, dict(w.params), w.range_start_inclusive,
                    np.array([[lo, hi]], dtype=np.int64))
     out.params.update(slice=(int(lo), int(hi)))
     return out
+
+
+def shard_local(w, lo, hi):
+    """What the store owning slice (lo, hi] is given in the multi-GPU path: its slice of the
+    snapshot (slice_workload) and only the requests that touch it (exchange.route), with their
+    global request indices."""
+    from .exchange import route
+    s = slice_workload(w, lo, hi)
+    q, idx = route(w.queries, lo, hi, bool(w.range_start_inclusive))
+    s.queries = q
+    return s, idx
 
 
 # ------------------------------------------------------------------------------------------

@@ -21,6 +21,7 @@
 
 #include "../../include/accord_deps.h"
 #include "common.hpp"
+#include "exchange.hpp"
 #include "kernels.hpp"
 
 using namespace adx;
@@ -185,6 +186,7 @@ struct ad_ctx {
     DevBuf d_rstart, d_rend, d_rtxw, d_rrid;
     DevBuf d_rlvl[NCLASS][MAX_LEVELS];
     DevBuf d_rb_s, d_rb_e, d_rb_e0, d_rb_e1, d_rb_wm, d_rb_rid, d_slices_s, d_slices_e;
+    DevBuf d_dict_lsb_raw, d_rt_start, d_rt_end;   // raw ids and range table (multi-GPU export)
 
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
@@ -197,6 +199,10 @@ struct ad_ctx {
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
+    // multi-GPU export / merge buffers
+    DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
+    DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
+    DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -493,7 +499,9 @@ static int build_snapshot(ad_ctx* c)
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
         (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_khash, khash)) ||
         (rc = upload(c, c->d_ent, ent)) ||
-        (rc = upload(c, c->d_w, w)) || (rc = upload(c, c->d_slices_s, c->slice_s)) || (rc = upload(c, c->d_slices_e, c->slice_e)))
+        (rc = upload(c, c->d_w, w)) || (rc = upload(c, c->d_slices_s, c->slice_s)) || (rc = upload(c, c->d_slices_e, c->slice_e)) ||
+        (rc = upload(c, c->d_dict_lsb_raw, c->dict_lsb)) || (rc = upload(c, c->d_rt_start, c->rt_start)) ||
+        (rc = upload(c, c->d_rt_end, c->rt_end)))
         return rc;
 
     DevSnapshot& s = c->ds;
@@ -1108,6 +1116,163 @@ int ad_range_table(const ad_ctx* c, uint64_t* n, const int64_t** start, const in
     *n = c->rt_start.size();
     if (start) *start = c->rt_start.data();
     if (end) *end = c->rt_end.data();
+    return AD_OK;
+}
+
+int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
+                    const uint64_t* dest_first, void* stream, ad_parts* out, uint64_t* dest_counts)
+{
+    if (!c || !res || !out || !dest_first || !dest_counts || n_dest == 0) return AD_E_INVAL;
+    if (c->dirty) return c->fail(AD_E_NOT_LOADED, "ad_parts_export: no prepared snapshot");
+    const uint64_t n = res->n_txns;
+    if (n && !txn_index) return c->fail(AD_E_INVAL, "ad_parts_export: txn_index is NULL");
+    if (dest_first[0] != 0 || dest_first[n_dest] != n) return c->fail(AD_E_INVAL, "ad_parts_export: dest_first must span [0, n)");
+    for (uint32_t d = 0; d < n_dest; ++d)
+        if (dest_first[d] > dest_first[d + 1]) return c->fail(AD_E_INVAL, "ad_parts_export: dest_first not ascending");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const uint64_t items = 3 * n;
+    if (!ens<uint32_t>(c->x_sz, 4 * items) || !ens<uint64_t>(c->x_off, 4 * (items + 1)) ||
+        !ens<uint64_t>(c->x_bsum, 4 * ((items + 1023) / 1024) + 16) || !ens<uint64_t>(c->x_df, n_dest + 1) ||
+        !ens<uint64_t>(c->x_cnt, 4 * (n_dest + 1)))
+        return c->fail(AD_E_NOMEM, "export buffers");
+    ExportArgs a{};
+    a.n = n;
+    for (int m = 0; m < 3; ++m)
+    {
+        a.keys_off[m] = res->keys_off[m]; a.keys[m] = res->keys[m];
+        a.txn_off[m] = res->txn_off[m]; a.txns[m] = res->txns[m];
+        a.k2t_off[m] = res->k2t_off[m]; a.k2t[m] = res->k2t[m];
+    }
+    a.txn_index = txn_index;
+    a.dict_msb = c->d_dict_hi.as<uint64_t>();
+    a.dict_lsb = c->d_dict_lsb_raw.as<uint64_t>();
+    a.dict_node = c->d_dict_node.as<int32_t>();
+    a.rt_start = c->d_rt_start.as<int64_t>();
+    a.rt_end = c->d_rt_end.as<int64_t>();
+    a.sz = c->x_sz.as<uint32_t>();
+    a.off = c->x_off.as<uint64_t>();
+    HIPCHK(c, hipMemcpyAsync(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(c, run_export_sizes(a, st));
+    HIPCHK(c, run_scan_arrays(a.sz, a.off, items, 4, c->x_bsum.as<uint64_t>(), st));
+    HIPCHK(c, run_export_bounds(a, c->x_df.as<uint64_t>(), n_dest, c->x_cnt.as<uint64_t>(), st));
+    std::vector<uint64_t> cnt(4 * (n_dest + 1));
+    HIPCHK(c, hipMemcpyAsync(cnt.data(), c->x_cnt.p, sizeof(uint64_t) * cnt.size(), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    out->n_parts = cnt[4 * n_dest + 0];
+    out->n_key_words = cnt[4 * n_dest + 1];
+    out->n_ids = cnt[4 * n_dest + 2];
+    out->n_k2t = cnt[4 * n_dest + 3];
+    for (uint32_t d = 0; d < n_dest; ++d)
+        for (int k = 0; k < 4; ++k) dest_counts[4 * d + k] = cnt[4 * (d + 1) + k] - cnt[4 * d + k];
+    if (out->n_parts > out->cap_parts || out->n_key_words > out->cap_key_words || out->n_ids > out->cap_ids ||
+        out->n_k2t > out->cap_k2t)
+    {
+        c->fail(AD_E_SPACE, "ad_parts_export: buffers too small (need %llu parts, %llu key words, %llu ids, %llu k2t)",
+                (unsigned long long)out->n_parts, (unsigned long long)out->n_key_words,
+                (unsigned long long)out->n_ids, (unsigned long long)out->n_k2t);
+        return AD_E_SPACE;
+    }
+    a.hdr = out->hdr; a.okeys = out->keys; a.oids = out->ids; a.ok2t = out->k2t;
+    HIPCHK(c, run_export_emit(a, st));
+    return AD_OK;
+}
+
+int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
+                   uint64_t n_owned, void* stream, ad_merged* out)
+{
+    if (!c || !in || !src_parts || !out || n_src == 0 || n_src > 64) return AD_E_INVAL;
+    uint64_t tot = 0;
+    std::vector<uint64_t> first(n_src + 1, 0);
+    for (uint32_t s = 0; s < n_src; ++s) first[s + 1] = (tot += src_parts[s]);
+    if (tot != in->n_parts) return c->fail(AD_E_INVAL, "ad_parts_merge: src_parts do not sum to n_parts");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const uint64_t P = in->n_parts, G = 3 * n_owned;
+    if (!ens<uint64_t>(c->m_src, n_src + 1) || !ens<uint32_t>(c->m_psz, 3 * P) || !ens<uint64_t>(c->m_poff, 3 * (P + 1)) ||
+        !ens<int32_t>(c->m_slot, G * n_src) || !ens<uint32_t>(c->m_dup, in->n_ids) || !ens<uint32_t>(c->m_gsz, 3 * G) ||
+        !ens<uint64_t>(c->m_goff, 3 * (G + 1)) ||
+        !ens<uint64_t>(c->m_bsum, 3 * ((std::max(P, G) + 1023) / 1024) + 16) || !ens<uint32_t>(c->m_err, 1) ||
+        !ens<uint64_t>(c->m_bases, 16) || !ens<uint64_t>(c->m_ko, 3 * (n_owned + 1)) ||
+        !ens<uint64_t>(c->m_to, 3 * (n_owned + 1)) || !ens<uint64_t>(c->m_oo, 3 * (n_owned + 1)))
+        return c->fail(AD_E_NOMEM, "merge buffers");
+    MergeArgs a{};
+    a.n_parts = P;
+    a.n_owned = n_owned;
+    a.txn_base = txn_base;
+    a.n_src = n_src;
+    a.src_first = c->m_src.as<uint64_t>();
+    a.hdr = in->hdr; a.keys = in->keys; a.ids = in->ids; a.k2t = in->k2t;
+    a.psz = c->m_psz.as<uint32_t>();
+    a.poff = c->m_poff.as<uint64_t>();
+    a.slot = c->m_slot.as<int32_t>();
+    a.dup = c->m_dup.as<uint32_t>();
+    a.gsz = c->m_gsz.as<uint32_t>();
+    a.goff = c->m_goff.as<uint64_t>();
+    a.error = c->m_err.as<uint32_t>();
+    a.o_keys_off = c->m_ko.as<uint64_t>();
+    a.o_txn_off = c->m_to.as<uint64_t>();
+    a.o_k2t_off = c->m_oo.as<uint64_t>();
+    HIPCHK(c, hipEventRecord(c->ev[6], st));
+    HIPCHK(c, hipMemcpyAsync(c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemsetAsync(a.error, 0, sizeof(uint32_t), st));
+    HIPCHK(c, hipMemsetAsync(a.slot, 0xFF, sizeof(int32_t) * std::max<uint64_t>(G * n_src, 1), st));
+    HIPCHK(c, run_merge_prepare(a, st));
+    HIPCHK(c, run_scan_arrays(a.psz, a.poff, P, 3, c->m_bsum.as<uint64_t>(), st));
+    HIPCHK(c, run_merge_slots(a, st));
+    HIPCHK(c, run_merge_count(a, st));
+    HIPCHK(c, run_scan_arrays(a.gsz, a.goff, G, 3, c->m_bsum.as<uint64_t>(), st));
+    HIPCHK(c, run_merge_bases(a, c->m_bases.as<uint64_t>(), st));
+    uint64_t bases[12];
+    uint32_t err = 0;
+    HIPCHK(c, hipMemcpyAsync(bases, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (err)
+        return c->fail(AD_E_INVAL, "ad_parts_merge: malformed parts (%s)",
+                       err & 1 ? "request outside the owned range or bad map" :
+                       err & 2 ? "two parts of one request and map from one source" :
+                                 "keys of different stores overlap or are out of slice order");
+    // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
+    if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, 3 * bases[10]) || !ens<int32_t>(c->m_k2t, bases[11]))
+        return c->fail(AD_E_NOMEM, "merge outputs");
+    a.o_keys = c->m_keys.as<int64_t>();
+    a.o_ids = c->m_ids.as<int64_t>();
+    a.o_k2t = c->m_k2t.as<int32_t>();
+    if (n_owned == 0)
+        for (DevBuf* b : {&c->m_ko, &c->m_to, &c->m_oo}) HIPCHK(c, hipMemsetAsync(b->p, 0, sizeof(uint64_t) * 3, st));
+    HIPCHK(c, run_merge_emit(a, st));
+    HIPCHK(c, hipEventRecord(c->ev[7], st));
+    HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (err) return c->fail(AD_E_INVAL, "ad_parts_merge: malformed parts (ids of a part not sorted and unique)");
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
+    memset(out, 0, sizeof(*out));
+    out->n_txns = n_owned;
+    out->txn_base = txn_base;
+    out->ms_device = ms;
+    for (int m = 0; m < 3; ++m)
+    {
+        out->keys_off[m] = a.o_keys_off + (uint64_t)m * (n_owned + 1);
+        out->txn_off[m] = a.o_txn_off + (uint64_t)m * (n_owned + 1);
+        out->k2t_off[m] = a.o_k2t_off + (uint64_t)m * (n_owned + 1);
+        out->keys[m] = a.o_keys + bases[3 * m + 0];
+        out->txns[m] = a.o_ids + 3 * bases[3 * m + 1];
+        out->k2t[m] = a.o_k2t + bases[3 * m + 2];
+        out->n_keys[m] = (bases[3 * (m + 1) + 0] - bases[3 * m + 0]) / (m == AD_MAP_RANGE ? 2 : 1);
+        out->n_ids[m] = bases[3 * (m + 1) + 1] - bases[3 * m + 1];
+        out->n_k2t[m] = bases[3 * (m + 1) + 2] - bases[3 * m + 2];
+    }
+    return AD_OK;
+}
+
+int ad_copy_to_host(ad_ctx* c, void* dst, const void* src, uint64_t bytes)
+{
+    if (!c || (!dst && bytes) || (!src && bytes)) return AD_E_INVAL;
+    if (!bytes) return AD_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return AD_OK;
 }
 

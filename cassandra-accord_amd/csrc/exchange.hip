@@ -1,0 +1,446 @@
+// exchange.hip — multi-GPU path: export of one CommandStore's per-request
+// PartialDeps for an all-to-all over RCCL, and K3, the on-GPU merge of the partials a GPU
+// receives for the requests it owns.
+//
+// The merge is PartialDeps.with (PartialDeps.java:73-81) folded over the stores in slice order,
+// as CommandStores.mapReduce reduces per-store results (CommandStores.java:576-593,
+// PreAccept.reduce PreAccept.java:140-156). Slices are disjoint and ascending, so each map's
+// keys concatenate in source order; the TxnId lists need a union: RelationMultiMap.linearUnion
+// (RelationMultiMap.java:561-816) restated as a rank computation — the union index of an id x is
+//     u(x) = sum over parts q of ( lb_q(x) - dupsBefore_q(lb_q(x)) )
+// where lb_q is the lower bound of x in part q's (sorted, unique) id list and an element is a
+// dup when an earlier part of the same request holds an equal id (Timestamp.equals). Each
+// distinct id is counted once, in the first part holding it, so u is the id's position in the
+// sorted union, and every copy of an id maps to the same u (keysToTxnIds remap for free).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../include/accord_deps.h"
+#include "common.hpp"
+#include "exchange.hpp"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace adx {
+
+namespace {
+
+constexpr int XWAVES = 4;              // waves per block
+constexpr uint32_t DUP_BIT = 0x80000000u;
+
+struct Tid3 { uint64_t msb, lsb; int32_t node; };
+
+__device__ __forceinline__ Tid3 load_tid(const int64_t* ids, uint64_t i)
+{
+    const int64_t* p = ids + 3 * i;
+    return Tid3{(uint64_t)p[0], (uint64_t)p[1], (int32_t)p[2]};
+}
+
+__device__ __forceinline__ int tid_cmp3(const Tid3& a, const Tid3& b)
+{
+    return norm_cmp(norm_tid(a.msb, a.lsb, a.node), norm_tid(b.msb, b.lsb, b.node));
+}
+
+// first i in [0, n) with !(ids[base + i] < x)
+__device__ __forceinline__ uint32_t lb_tid(const int64_t* ids, uint64_t base, uint32_t n, const Tid3& x)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tid_cmp3(load_tid(ids, base + mid), x) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------------------
+// export
+// ---------------------------------------------------------------------------------------
+__global__ void k_export_sizes(ExportArgs a)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t items = 3 * a.n;
+    if (i >= items) return;
+    const uint64_t r = i / 3;
+    const int m = (int)(i % 3);
+    const uint64_t nk = a.keys_off[m][r + 1] - a.keys_off[m][r];
+    const uint64_t nt = a.txn_off[m][r + 1] - a.txn_off[m][r];
+    const uint64_t no = a.k2t_off[m][r + 1] - a.k2t_off[m][r];
+    const bool live = nk > 0;
+    a.sz[0 * items + i] = live ? 1u : 0u;
+    a.sz[1 * items + i] = live ? (uint32_t)(nk * (m == AD_MAP_RANGE ? 2 : 1)) : 0u;
+    a.sz[2 * items + i] = live ? (uint32_t)nt : 0u;
+    a.sz[3 * items + i] = live ? (uint32_t)no : 0u;
+}
+
+// one 8-lane group per (request, map) item
+__global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
+{
+    const uint64_t items = 3 * a.n;
+    const uint32_t g8 = threadIdx.x & 7;
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+    if (i >= items) return;
+    const uint64_t r = i / 3;
+    const int m = (int)(i % 3);
+    const uint64_t k0 = a.keys_off[m][r], nk = a.keys_off[m][r + 1] - k0;
+    if (nk == 0) return;
+    const uint64_t t0 = a.txn_off[m][r], nt = a.txn_off[m][r + 1] - t0;
+    const uint64_t o0 = a.k2t_off[m][r], no = a.k2t_off[m][r + 1] - o0;
+    const uint64_t P = a.off[0 * (items + 1) + i];
+    const uint64_t KW = a.off[1 * (items + 1) + i];
+    const uint64_t ID = a.off[2 * (items + 1) + i];
+    const uint64_t KO = a.off[3 * (items + 1) + i];
+    if (g8 == 0)
+    {
+        int64_t* h = a.hdr + 4 * P;
+        h[0] = (a.txn_index[r] << 2) | m;
+        h[1] = (int64_t)nk;
+        h[2] = (int64_t)nt;
+        h[3] = (int64_t)no;
+    }
+    if (m == AD_MAP_RANGE)
+    {
+        for (uint64_t j = g8; j < nk; j += 8)
+        {
+            const int64_t rid = a.keys[m][k0 + j];
+            a.okeys[KW + 2 * j] = a.rt_start[rid];
+            a.okeys[KW + 2 * j + 1] = a.rt_end[rid];
+        }
+    }
+    else
+    {
+        for (uint64_t j = g8; j < nk; j += 8) a.okeys[KW + j] = a.keys[m][k0 + j];
+    }
+    for (uint64_t j = g8; j < nt; j += 8)
+    {
+        const uint32_t d = a.txns[m][t0 + j];
+        int64_t* o = a.oids + 3 * (ID + j);
+        o[0] = (int64_t)a.dict_msb[d];
+        o[1] = (int64_t)a.dict_lsb[d];
+        o[2] = (int64_t)a.dict_node[d];
+    }
+    for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = a.k2t[m][o0 + j];
+}
+
+__global__ void k_export_bounds(ExportArgs a, const uint64_t* dest_first, uint32_t n_dest, uint64_t* counts)
+{
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d > n_dest) return;
+    const uint64_t items = 3 * a.n;
+    const uint64_t it = 3 * dest_first[d];
+    for (int k = 0; k < 4; ++k) counts[4 * d + k] = a.off[k * (items + 1) + it];
+}
+
+// ---------------------------------------------------------------------------------------
+// merge (K3)
+// ---------------------------------------------------------------------------------------
+__global__ void k_merge_part_sizes(MergeArgs a)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n_parts) return;
+    const int64_t* h = a.hdr + 4 * p;
+    const int m = (int)(h[0] & 3);
+    a.psz[0 * a.n_parts + p] = (uint32_t)(h[1] * (m == AD_MAP_RANGE ? 2 : 1));
+    a.psz[1 * a.n_parts + p] = (uint32_t)h[2];
+    a.psz[2 * a.n_parts + p] = (uint32_t)h[3];
+}
+
+__global__ void k_merge_slots(MergeArgs a)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n_parts) return;
+    uint32_t s = 0;
+    while (s + 1 < a.n_src && a.src_first[s + 1] <= p) ++s;
+    const int64_t h0 = a.hdr[4 * p];
+    const int m = (int)(h0 & 3);
+    const int64_t t = h0 >> 2;
+    if (m > 2 || t < (int64_t)a.txn_base || t >= (int64_t)(a.txn_base + a.n_owned) || a.hdr[4 * p + 1] <= 0)
+    {
+        atomicOr(a.error, 1u);
+        return;
+    }
+    const uint64_t g = (uint64_t)m * a.n_owned + (uint64_t)(t - (int64_t)a.txn_base);
+    const int32_t prev = atomicExch(&a.slot[g * a.n_src + s], (int32_t)p);
+    if (prev != -1) atomicOr(a.error, 2u);          // two parts of one request and map from one store
+}
+
+// The parts of group g in source order, staged in wave-private LDS so that lanes in divergent
+// code can read any part's bounds (no cross-lane shuffles from inactive lanes).
+struct PartInfo {
+    uint64_t ibase, kbase, obase;     // offsets of the part's ids / key words / k2t in the receive buffers
+    uint32_t ni, kw, no, nk;          // sizes: ids, key words, k2t ints, keys
+};
+
+__device__ __forceinline__ uint32_t stage_parts(const MergeArgs& a, uint64_t g, PartInfo* info)
+{
+    const uint32_t l = lane_id();
+    const int32_t v = l < a.n_src ? a.slot[g * a.n_src + l] : -1;
+    const uint64_t live = ballot(v >= 0);
+    const uint32_t np = __popcll(live);
+    if (v >= 0)
+    {
+        const uint64_t p = (uint64_t)v;
+        const uint64_t P1 = a.n_parts + 1;
+        PartInfo pi;
+        pi.kbase = a.poff[0 * P1 + p];
+        pi.kw = (uint32_t)(a.poff[0 * P1 + p + 1] - pi.kbase);
+        pi.ibase = a.poff[1 * P1 + p];
+        pi.ni = (uint32_t)(a.poff[1 * P1 + p + 1] - pi.ibase);
+        pi.obase = a.poff[2 * P1 + p];
+        pi.no = (uint32_t)(a.poff[2 * P1 + p + 1] - pi.obase);
+        pi.nk = (uint32_t)a.hdr[4 * p + 1];
+        info[mbcnt(live)] = pi;
+    }
+    wave_lds_sync();
+    return np;
+}
+
+// keys of consecutive parts must ascend (disjoint, ordered slices)
+__device__ __forceinline__ bool keys_ordered(int m, int64_t prev_s, int64_t prev_e, int64_t first_s, int64_t first_e)
+{
+    if (m == AD_MAP_RANGE) return prev_s < first_s || (prev_s == first_s && prev_e < first_e);
+    return prev_s < first_s;
+}
+
+// pass 1: dup flags with exclusive per-part dup prefix; sizes of the merged group
+__global__ void __launch_bounds__(64 * XWAVES) k_merge_count(MergeArgs a)
+{
+    __shared__ PartInfo s_info[XWAVES][64];
+    PartInfo* info = s_info[threadIdx.x >> 6];
+    const uint64_t n_groups = 3 * a.n_owned;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t l = lane_id();
+    for (uint64_t g = wave; g < n_groups; g += n_waves)
+    {
+        const int m = (int)(g / a.n_owned);
+        const int w = m == AD_MAP_RANGE ? 2 : 1;
+        wave_lds_sync();
+        const uint32_t np = stage_parts(a, g, info);
+        uint64_t kw = 0, ids = 0, k2t = 0, dups = 0;
+        if (l == 0)
+            for (uint32_t j = 1; j < np; ++j)
+            {
+                const PartInfo& pp = info[j - 1];
+                const PartInfo& pj = info[j];
+                const int64_t ls = a.keys[pp.kbase + pp.kw - w], le = w == 2 ? a.keys[pp.kbase + pp.kw - 1] : 0;
+                const int64_t fs = a.keys[pj.kbase], fe = w == 2 ? a.keys[pj.kbase + 1] : 0;
+                if (!keys_ordered(m, ls, le, fs, fe)) atomicOr(a.error, 4u);
+            }
+        for (uint32_t j = 0; j < np; ++j)
+        {
+            const PartInfo pj = info[j];
+            uint32_t run = 0;
+            for (uint32_t e0 = 0; e0 < pj.ni; e0 += 64)
+            {
+                const uint32_t e = e0 + l;
+                bool dup = false;
+                if (e < pj.ni && j > 0)
+                {
+                    const Tid3 x = load_tid(a.ids, pj.ibase + e);
+                    for (uint32_t q = 0; q < j && !dup; ++q)
+                    {
+                        const uint64_t qb = info[q].ibase;
+                        const uint32_t qn = info[q].ni;
+                        const uint32_t pos = lb_tid(a.ids, qb, qn, x);
+                        dup = pos < qn && tid_cmp3(load_tid(a.ids, qb + pos), x) == 0;
+                    }
+                }
+                const uint64_t bm = ballot(dup);
+                if (e < pj.ni) a.dup[pj.ibase + e] = (run + mbcnt(bm)) | (dup ? DUP_BIT : 0u);
+                run += __popcll(bm);
+            }
+            kw += pj.kw;
+            ids += pj.ni;
+            k2t += pj.no;
+            dups += run;
+        }
+        if (l == 0)
+        {
+            a.gsz[0 * n_groups + g] = (uint32_t)kw;
+            a.gsz[1 * n_groups + g] = (uint32_t)(ids - dups);
+            a.gsz[2 * n_groups + g] = (uint32_t)k2t;
+        }
+    }
+}
+
+// u(x) for an id x of part j whose lower bound in its own part is pos_j
+__device__ __forceinline__ uint32_t union_index(const MergeArgs& a, const PartInfo* info, uint32_t np, uint32_t j,
+                                                uint32_t pos_j, const Tid3& x)
+{
+    uint32_t u = 0;
+    for (uint32_t q = 0; q < np; ++q)
+    {
+        const uint64_t qb = info[q].ibase;
+        const uint32_t qn = info[q].ni;
+        const uint32_t lb = q == j ? pos_j : lb_tid(a.ids, qb, qn, x);
+        uint32_t dp;
+        if (lb < qn) dp = a.dup[qb + lb] & ~DUP_BIT;
+        else
+        {
+            const uint32_t d = qn ? a.dup[qb + qn - 1] : 0u;
+            dp = qn ? (d & ~DUP_BIT) + (d >> 31) : 0u;
+        }
+        u += lb - dp;
+    }
+    return u;
+}
+
+// pass 2: emit keys (concatenated), the sorted id union and the remapped keysToTxnIds
+__global__ void __launch_bounds__(64 * XWAVES) k_merge_emit(MergeArgs a)
+{
+    __shared__ PartInfo s_info[XWAVES][64];
+    PartInfo* info = s_info[threadIdx.x >> 6];
+    const uint64_t n_groups = 3 * a.n_owned;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t l = lane_id();
+    const uint64_t G1 = n_groups + 1;
+    for (uint64_t g = wave; g < n_groups; g += n_waves)
+    {
+        const int m = (int)(g / a.n_owned);
+        const uint64_t r = g - (uint64_t)m * a.n_owned;
+        const uint64_t mb = (uint64_t)m * a.n_owned;
+        const int w = m == AD_MAP_RANGE ? 2 : 1;
+        const uint64_t KW = a.goff[0 * G1 + g], ID = a.goff[1 * G1 + g], KO = a.goff[2 * G1 + g];
+        if (l == 0)
+        {
+            const uint64_t O = (uint64_t)m * (a.n_owned + 1) + r;
+            a.o_keys_off[O] = (KW - a.goff[0 * G1 + mb]) / w;
+            a.o_txn_off[O] = ID - a.goff[1 * G1 + mb];
+            a.o_k2t_off[O] = KO - a.goff[2 * G1 + mb];
+            if (r + 1 == a.n_owned)
+            {
+                a.o_keys_off[O + 1] = (a.goff[0 * G1 + g + 1] - a.goff[0 * G1 + mb]) / w;
+                a.o_txn_off[O + 1] = a.goff[1 * G1 + g + 1] - a.goff[1 * G1 + mb];
+                a.o_k2t_off[O + 1] = a.goff[2 * G1 + g + 1] - a.goff[2 * G1 + mb];
+            }
+        }
+        wave_lds_sync();
+        const uint32_t np = stage_parts(a, g, info);
+        if (np == 0) continue;
+        uint64_t nkeys_total = 0;
+        {
+            uint64_t at = KW;
+            for (uint32_t j = 0; j < np; ++j)
+            {
+                const PartInfo pj = info[j];
+                for (uint32_t e = l; e < pj.kw; e += 64) a.o_keys[at + e] = a.keys[pj.kbase + e];
+                at += pj.kw;
+                nkeys_total += pj.nk;
+            }
+        }
+        const uint64_t n_union = a.goff[1 * G1 + g + 1] - ID;
+        uint64_t keys_before = 0, pairs_before = 0;
+        for (uint32_t j = 0; j < np; ++j)
+        {
+            const PartInfo pj = info[j];
+            for (uint32_t e = l; e < pj.ni; e += 64)
+            {
+                if (a.dup[pj.ibase + e] & DUP_BIT) continue;
+                const Tid3 x = load_tid(a.ids, pj.ibase + e);
+                const uint32_t u = union_index(a, info, np, j, e, x);
+                if (u >= n_union) { atomicOr(a.error, 8u); continue; }     // ids of a part not sorted/unique
+                int64_t* o = a.o_ids + 3 * (ID + u);
+                o[0] = (int64_t)x.msb;
+                o[1] = (int64_t)x.lsb;
+                o[2] = (int64_t)x.node;
+            }
+            const uint32_t nk = pj.nk;
+            const uint32_t pairs = pj.no - nk;
+            for (uint32_t e = l; e < nk; e += 64)
+                a.o_k2t[KO + keys_before + e] =
+                    (int32_t)((uint64_t)a.k2t[pj.obase + e] - nk + nkeys_total + pairs_before);
+            for (uint32_t v = l; v < pairs; v += 64)
+            {
+                const uint32_t idx = (uint32_t)a.k2t[pj.obase + nk + v];
+                if (idx >= pj.ni) { atomicOr(a.error, 8u); continue; }
+                const Tid3 x = load_tid(a.ids, pj.ibase + idx);
+                a.o_k2t[KO + nkeys_total + pairs_before + v] = (int32_t)union_index(a, info, np, j, idx, x);
+            }
+            keys_before += nk;
+            pairs_before += pairs;
+        }
+    }
+}
+
+__global__ void k_merge_bases(MergeArgs a, uint64_t* out)
+{
+    // out[3*m + k] = goff[k][m * n_owned] for m = 0..3 (m = 3: totals)
+    const int i = threadIdx.x;
+    if (i >= 12) return;
+    const int m = i / 3, k = i % 3;
+    out[i] = a.goff[k * (3 * a.n_owned + 1) + (uint64_t)m * a.n_owned];
+}
+
+}  // namespace
+
+hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st)
+{
+    const uint64_t items = 3 * a.n;
+    if (!items) return hipSuccess;
+    k_export_sizes<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
+{
+    const uint64_t items = 3 * a.n;
+    if (!items) return hipSuccess;
+    const uint64_t threads = items * 8;
+    k_export_emit<<<(unsigned)((threads + 64 * XWAVES - 1) / (64 * XWAVES)), 64 * XWAVES, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_export_bounds(const ExportArgs& a, const uint64_t* dest_first, uint32_t n_dest, uint64_t* counts,
+                             hipStream_t st)
+{
+    k_export_bounds<<<(n_dest + 1 + 63) / 64, 64, 0, st>>>(a, dest_first, n_dest, counts);
+    return hipGetLastError();
+}
+
+hipError_t run_merge_prepare(const MergeArgs& a, hipStream_t st)
+{
+    if (!a.n_parts) return hipSuccess;
+    const unsigned b = (unsigned)((a.n_parts + 255) / 256);
+    k_merge_part_sizes<<<b, 256, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_merge_slots(const MergeArgs& a, hipStream_t st)
+{
+    if (!a.n_parts) return hipSuccess;
+    k_merge_slots<<<(unsigned)((a.n_parts + 255) / 256), 256, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+static unsigned merge_blocks(uint64_t n_groups)
+{
+    const uint64_t want = (n_groups + XWAVES - 1) / XWAVES;
+    const uint64_t cap = (uint64_t)device_cu_count() * 32;
+    return (unsigned)std::max<uint64_t>(1, std::min(want, cap));
+}
+
+hipError_t run_merge_count(const MergeArgs& a, hipStream_t st)
+{
+    if (!a.n_owned) return hipSuccess;
+    k_merge_count<<<merge_blocks(3 * a.n_owned), 64 * XWAVES, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_merge_emit(const MergeArgs& a, hipStream_t st)
+{
+    if (!a.n_owned) return hipSuccess;
+    k_merge_emit<<<merge_blocks(3 * a.n_owned), 64 * XWAVES, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_merge_bases(const MergeArgs& a, uint64_t* out, hipStream_t st)
+{
+    k_merge_bases<<<1, 64, 0, st>>>(a, out);
+    return hipGetLastError();
+}
+
+}  // namespace adx

@@ -62,6 +62,7 @@ extern "C" {
 #define AD_E_NOT_LOADED       -7  /* batch before ad_cfk_load                               */
 #define AD_E_STATE            -8  /* reference would throw (e.g. prunedBefore walk off end) */
 #define AD_E_CAPACITY         -9  /* id dictionary exceeds 2^28 entries                     */
+#define AD_E_SPACE           -10  /* a caller-provided output buffer is too small (sizes set) */
 
 /* ---- InternalStatus ordinals (CommandsForKey.java:493-501) -------------------------- */
 #define AD_ST_TRANSITIVELY_KNOWN                          0
@@ -239,6 +240,65 @@ int ad_deps_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t flags,
 int ad_dict(const ad_ctx* ctx, uint64_t* n, const uint64_t** msb, const uint64_t** lsb,
             const int32_t** node);
 int ad_range_table(const ad_ctx* ctx, uint64_t* n, const int64_t** start, const int64_t** end);
+
+/* ---- multi-GPU exchange ------------------------------------------------
+ * One ctx per GPU = one CommandStore owning a token slice (ad_config.slice_*). A request that
+ * touches several stores is resolved by each of them (CommandStores.mapReduce,
+ * CommandStores.java:576-593); the per-store PartialDeps are combined with PartialDeps.with
+ * (PartialDeps.java:73-81; PreAccept.reduce, PreAccept.java:140-156) on the GPU that owns the
+ * request. The partials travel between GPUs (RCCL all-to-all) in this flat format.
+ *
+ * Parts: the non-empty maps of one store's batch result, in request order, maps ascending.
+ *   hdr  [n_parts * 4] int64: {global request index << 2 | map, n_keys, n_ids, n_k2t}
+ *   keys [n_key_words] int64: key ordinals; AD_MAP_RANGE: {start, end} per range (2 words)
+ *   ids  [n_ids * 3]   int64: {msb, lsb, node} of each TxnId (ascending within a part)
+ *   k2t  [n_k2t]       int32: the part's keysToTxnIds (indices into its own ids)
+ * All arrays are device memory. */
+typedef struct ad_parts {
+    uint64_t n_parts, n_key_words, n_ids, n_k2t;          /* sizes                             */
+    int64_t* hdr;
+    int64_t* keys;
+    int64_t* ids;
+    int32_t* k2t;
+    uint64_t cap_parts, cap_key_words, cap_ids, cap_k2t;  /* capacities of the arrays (export) */
+} ad_parts;
+
+/* Export the device result `res_dev` of the last ad_deps_batch_device on ctx as parts, into
+ * the caller's device arrays of `out` (capacities cap_*). txn_index_dev[i] is request i's
+ * global index (ascending). Requests [dest_first[d], dest_first[d+1]) go to destination d
+ * (host array, n_dest + 1 entries, dest_first[n_dest] == batch size); dest_counts (host,
+ * n_dest * 4) receives per destination {parts, key words, ids, k2t}. If a capacity is too
+ * small, the sizes are set in `out` and AD_E_SPACE is returned with nothing written. */
+int ad_parts_export(ad_ctx* ctx, const ad_deps_result* res_dev, const int64_t* txn_index_dev, uint32_t n_dest,
+                    const uint64_t* dest_first, void* stream, ad_parts* out, uint64_t* dest_counts);
+
+/* Merged PartialDeps of the requests a GPU owns, materialised (ids as {msb,lsb,node}).
+ * For owned request r (global index txn_base + r) and map m: keys [keys_off[m][r], keys_off[m][r+1])
+ * (AD_MAP_RANGE: ranges, 2 words each in keys[m]), txns [txn_off[m][r], ..) as triplets,
+ * k2t [k2t_off[m][r], ..) the keysToTxnIds of the merged RelationMultiMap. Device memory owned
+ * by ctx, valid until the next ad_parts_merge on ctx. */
+typedef struct ad_merged {
+    uint64_t  n_txns;
+    uint64_t  txn_base;
+    uint64_t* keys_off[AD_NMAPS];
+    int64_t*  keys[AD_NMAPS];
+    uint64_t* txn_off[AD_NMAPS];
+    int64_t*  txns[AD_NMAPS];
+    uint64_t* k2t_off[AD_NMAPS];
+    int32_t*  k2t[AD_NMAPS];
+    uint64_t  n_keys[AD_NMAPS], n_ids[AD_NMAPS], n_k2t[AD_NMAPS];   /* totals per map           */
+    double    ms_device;
+} ad_merged;
+
+/* Merge the parts received from n_src stores (concatenated in source = slice order; source s
+ * sent src_parts[s] parts) for the requests [txn_base, txn_base + n_owned). Keys of different
+ * stores must be disjoint and ascending in source order (AD_E_INVAL otherwise). */
+int ad_parts_merge(ad_ctx* ctx, const ad_parts* in_dev, uint32_t n_src, const uint64_t* src_parts,
+                   uint64_t txn_base, uint64_t n_owned, void* stream, ad_merged* out);
+
+/* Copy device memory owned by the library (results) into a host buffer: for hosts without a
+ * HIP binding of their own (the Panama FFM wrapper). */
+int ad_copy_to_host(ad_ctx* ctx, void* dst, const void* src_dev, uint64_t bytes);
 
 /* ---- execution ordering (config 5): topological apply levels -------------------------
  * Txn i: executeAt (msb/lsb/node), kind, keys [key_off[i],key_off[i+1]) and direct deps

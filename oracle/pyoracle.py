@@ -50,6 +50,7 @@ def lib():
         L.rc_deps_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_uint64, C.c_uint64,
                                     C.POINTER(C.POINTER(RcResult))]
         L.rc_result_free.argtypes = [C.POINTER(RcResult)]
+        L.rc_result_merge.argtypes = [C.POINTER(C.POINTER(RcResult)), C.c_int, C.POINTER(C.POINTER(RcResult))]
         L.rc_levels.argtypes = [C.POINTER(A.AdGraphSoa), C.c_void_p]
         L.rc_tid_cmp.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         _lib = L
@@ -149,6 +150,72 @@ def resolve(workload, elide=1, first=0, count=0):
         return st.deps_batch(workload.queries, workload.flags, first, count)
     finally:
         st.close()
+
+
+def resolve_sharded(workload, n_shards, elide=1, bounds=None):
+    """Oracle of the multi-GPU path: one CommandStore per EvenSplit token slice (synth.shard_bounds),
+    each resolving every request restricted to its slice, then the per-store results combined
+    request-wise with PartialDeps.with (rc_result_merge; CommandStores.java:576-593)."""
+    from accord_deps import synth
+    L = lib()
+    lo, hi = synth.shard_bounds(n_shards) if bounds is None else bounds
+    parts = []
+    try:
+        for g in range(n_shards):
+            w = synth.slice_workload(workload, lo[g], hi[g])
+            st = OracleStore(w.range_start_inclusive, elide, w.slices)
+            try:
+                st.load(w)
+                out = C.POINTER(RcResult)()
+                st._check(L.rc_deps_batch(st.h, C.byref(w.queries.soa()), w.flags, 0, 0, C.byref(out)))
+                parts.append(out)
+            finally:
+                st.close()
+        arr = (C.POINTER(RcResult) * len(parts))(*parts)
+        merged = C.POINTER(RcResult)()
+        rc = L.rc_result_merge(arr, len(parts), C.byref(merged))
+        if rc:
+            raise OracleError(rc, "merge")
+        try:
+            return result_to_batch(merged.contents)
+        finally:
+            L.rc_result_free(merged)
+    finally:
+        for p in parts:
+            L.rc_result_free(p)
+
+
+def _batch_to_rc(b, keep):
+    """An RcResult viewing the arrays of a PartialDepsBatch (kept alive in `keep`)."""
+    r = RcResult()
+    r.n_txns = b.n_txns
+    for m in range(3):
+        mm = b.maps[m]
+        arrs = dict(keys_off=A.as_u64(mm.keys_off), keys=A.as_i64(mm.keys),
+                    keys_end=A.as_i64(mm.keys_end) if mm.keys_end is not None else
+                    (A.as_i64(mm.keys) if m == A.AD_MAP_RANGE else None),
+                    txn_off=A.as_u64(mm.txn_off), txn_msb=A.as_u64(mm.txn.msb), txn_lsb=A.as_u64(mm.txn.lsb),
+                    txn_node=A.as_i32(mm.txn.node), k2t_off=A.as_u64(mm.k2t_off), k2t=A.as_i32(mm.k2t))
+        keep.append(arrs)
+        for name, a in arrs.items():
+            getattr(r, name)[m] = A.ptr(a) if a is not None else None
+    return r
+
+
+def merge_batches(batches):
+    """Request-wise PartialDeps.with over several PartialDepsBatch of equal length (rc_result_merge)."""
+    L = lib()
+    keep = []
+    rcs = [_batch_to_rc(b, keep) for b in batches]
+    arr = (C.POINTER(RcResult) * len(rcs))(*[C.pointer(r) for r in rcs])
+    merged = C.POINTER(RcResult)()
+    rc = L.rc_result_merge(arr, len(rcs), C.byref(merged))
+    if rc:
+        raise OracleError(rc, "merge")
+    try:
+        return result_to_batch(merged.contents)
+    finally:
+        L.rc_result_free(merged)
 
 
 def levels(graph):

@@ -999,6 +999,98 @@ int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t f
     return 0;
 }
 
+/* View request i, map m of a materialised result as a RelationMultiMap (copies). */
+static void result_view(const rc_result* r, int m, uint64_t i, rmm_t* out)
+{
+    uint64_t k0 = r->keys_off[m][i], k1 = r->keys_off[m][i + 1];
+    uint64_t t0 = r->txn_off[m][i], t1 = r->txn_off[m][i + 1];
+    uint64_t o0 = r->k2t_off[m][i], o1 = r->k2t_off[m][i + 1];
+    out->nkeys = k1 - k0; out->nvalues = t1 - t0; out->nout = o1 - o0;
+    out->keys = malloc(sizeof(rkey_t) * (out->nkeys ? out->nkeys : 1));
+    out->values = malloc(sizeof(tid_t) * (out->nvalues ? out->nvalues : 1));
+    out->out = malloc(sizeof(int32_t) * (out->nout ? out->nout : 1));
+    for (uint64_t k = 0; k < out->nkeys; ++k)
+    {
+        out->keys[k].a = r->keys[m][k0 + k];
+        out->keys[k].b = m == AD_MAP_RANGE ? r->keys_end[m][k0 + k] : 0;
+    }
+    for (uint64_t t = 0; t < out->nvalues; ++t)
+    {
+        out->values[t].msb = r->txn_msb[m][t0 + t];
+        out->values[t].lsb = r->txn_lsb[m][t0 + t];
+        out->values[t].node = r->txn_node[m][t0 + t];
+    }
+    memcpy(out->out, r->k2t[m] + o0, sizeof(int32_t) * out->nout);
+}
+
+/* Combine the per-CommandStore results of the same requests the way CommandStores.mapReduce
+ * reduces them (CommandStores.java:576-593 with PreAccept.reduce, PreAccept.java:140-156):
+ * request i's result = parts[0]_i.with(parts[1]_i)...  (PartialDeps.with, PartialDeps.java:73-81,
+ * covering ranges omitted). All parts must hold the same number of requests. */
+int rc_result_merge(const rc_result* const* parts, int n_parts, rc_result** out)
+{
+    if (n_parts < 1) return AD_E_INVAL;
+    uint64_t n = parts[0]->n_txns;
+    for (int p = 1; p < n_parts; ++p)
+        if (parts[p]->n_txns != n) return AD_E_INVAL;
+    rc_result* r = calloc(1, sizeof(rc_result));
+    r->n_txns = n;
+    size_t cap[AD_NMAPS][3] = {{0}};
+    size_t len[AD_NMAPS][3] = {{0}};
+    for (int m = 0; m < AD_NMAPS; ++m)
+    {
+        r->keys_off[m] = calloc(n + 1, sizeof(uint64_t));
+        r->txn_off[m] = calloc(n + 1, sizeof(uint64_t));
+        r->k2t_off[m] = calloc(n + 1, sizeof(uint64_t));
+        result_alloc_map(r, m, 1, 1, 1);
+    }
+    for (int p = 0; p < n_parts; ++p) r->scan_entries += parts[p]->scan_entries;
+    int rc = 0;
+    for (uint64_t i = 0; i < n && !rc; ++i)
+    {
+        for (int m = 0; m < AD_NMAPS && !rc; ++m)
+        {
+            rmm_t acc;
+            result_view(parts[0], m, i, &acc);
+            for (int p = 1; p < n_parts && !rc; ++p)
+            {
+                rmm_t y, z;
+                result_view(parts[p], m, i, &y);
+                rc = rmm_with(&acc, &y, &z);
+                rmm_free(&y);
+                rmm_free(&acc);
+                acc = z;
+            }
+            size_t nk = len[m][0] + acc.nkeys, nt = len[m][1] + acc.nvalues, no = len[m][2] + acc.nout;
+            if (nk > cap[m][0] || nt > cap[m][1] || no > cap[m][2])
+            {
+                cap[m][0] = nk * 2 + 16; cap[m][1] = nt * 2 + 16; cap[m][2] = no * 2 + 16;
+                result_alloc_map(r, m, cap[m][0], cap[m][1], cap[m][2]);
+            }
+            for (size_t k = 0; k < acc.nkeys; ++k)
+            {
+                r->keys[m][len[m][0] + k] = acc.keys[k].a;
+                if (m == AD_MAP_RANGE) r->keys_end[m][len[m][0] + k] = acc.keys[k].b;
+            }
+            for (size_t t = 0; t < acc.nvalues; ++t)
+            {
+                r->txn_msb[m][len[m][1] + t] = acc.values[t].msb;
+                r->txn_lsb[m][len[m][1] + t] = acc.values[t].lsb;
+                r->txn_node[m][len[m][1] + t] = acc.values[t].node;
+            }
+            if (acc.nout) memcpy(r->k2t[m] + len[m][2], acc.out, sizeof(int32_t) * acc.nout);
+            len[m][0] = nk; len[m][1] = nt; len[m][2] = no;
+            r->keys_off[m][i + 1] = nk;
+            r->txn_off[m][i + 1] = nt;
+            r->k2t_off[m][i + 1] = no;
+            rmm_free(&acc);
+        }
+    }
+    if (rc) { rc_result_free(r); return rc; }
+    *out = r;
+    return 0;
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* Execution ordering levels (config 5)                                                 */
 /* ------------------------------------------------------------------------------------ */

@@ -49,6 +49,9 @@ int  rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t 
                    uint64_t count, rc_result** out);
 void rc_result_free(rc_result* r);
 
+/* request-wise PartialDeps.with over the results of several CommandStores (multi-GPU oracle) */
+int rc_result_merge(const rc_result* const* parts, int n_parts, rc_result** out);
+
 int rc_levels(const ad_graph_soa* g, uint32_t* level_out);
 
 /* exposed for the tests */

@@ -1,0 +1,112 @@
+"""GPU parity of the multi-GPU data path on one MI355X: several CommandStores (token slices) on
+cuda:0, each resolving the requests routed to it, exporting parts (ad_parts_export, HIP), an
+emulated all-to-all (the same source-order concatenation RCCL produces), and the K3 merge
+(ad_parts_merge, HIP) on each owner — bit-exact against the oracle of the sharded reference path
+(per-store calculatePartialDeps + PartialDeps.with, pyoracle.resolve_sharded)."""
+import numpy as np
+import pytest
+import torch
+
+import pyoracle
+from accord_deps import _abi as A
+from accord_deps import exchange, native, synth
+
+pytestmark = pytest.mark.gpu
+
+UNITS = (("hdr", 4), ("keys", 1), ("ids", 3), ("k2t", 1))
+
+
+def _parts(tensors, totals):
+    p = A.AdParts()
+    p.hdr, p.keys, p.ids, p.k2t = (tensors[k].data_ptr() for k in ("hdr", "keys", "ids", "k2t"))
+    p.n_parts, p.n_key_words, p.n_ids, p.n_k2t = (int(x) for x in totals)
+    return p
+
+
+def _run_sharded(w, bounds, n_owners):
+    dev = torch.device("cuda", 0)
+    lo, hi = bounds
+    n_total = len(w.queries)
+    bases = exchange.owner_bases(n_total, n_owners)
+    engines, keep = [], []
+    for g in range(len(lo)):
+        local, idx = synth.shard_local(w, lo[g], hi[g])
+        st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, local.slices)
+        st.load(local)
+        qdev, k = native.device_queries(local.queries, dev)
+        keep.append(k)
+        e = exchange.GpuEngine(st, qdev, idx, dev)
+        e.resolve()
+        dest_first = np.searchsorted(idx, np.asarray(bases[:n_owners], np.int64)).astype(np.uint64).tolist() + [len(idx)]
+        send, counts = e.export(np.asarray(dest_first, np.uint64))
+        engines.append((e, send, counts))
+    torch.cuda.synchronize()
+    out = []
+    for d in range(n_owners):
+        recv, totals, src_parts = {}, np.zeros(4, np.int64), []
+        for a, (name, mult) in enumerate(UNITS):
+            pieces = []
+            for e, send, counts in engines:
+                start = int(counts[:d, a].sum()) * mult
+                pieces.append(send[name][start:start + int(counts[d, a]) * mult])
+            recv[name] = torch.cat(pieces) if pieces else torch.zeros(0, device=dev)
+        for e, send, counts in engines:
+            totals += counts[d]
+            src_parts.append(int(counts[d, 0]))
+        owner = engines[d % len(engines)][0].store
+        torch.cuda.synchronize()                 # recv tensors were built on torch's stream
+        mg = owner.merge_parts(_parts(recv, totals), src_parts, bases[d], bases[d + 1] - bases[d])
+        out.append((bases[d], bases[d + 1] - bases[d], owner.merged_to_host(mg), mg.ms_device))
+    for e, _, _ in engines:
+        e.store.close()
+    return out
+
+
+def _check(w, bounds, n_owners):
+    expect = pyoracle.resolve_sharded(w, len(bounds[0]), bounds=bounds)
+    for base, n, got, _ in _run_sharded(w, bounds, n_owners):
+        ok, why = got.equals(expect.window(base, n), detail=True)
+        if not ok:
+            bad = got.first_mismatch(expect.window(base, n))
+            pytest.fail("owner base %d: %s; first mismatch %s" % (base, why, bad[:2] if bad else None))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_small_three_stores(seed):
+    w = synth.random_small(seed)
+    w.slices = None
+    _check(w, synth.cut_bounds([-100, 150]), 2)
+
+
+@pytest.mark.parametrize("n_stores,n_owners", [(2, 2), (4, 4), (8, 8), (8, 3)])
+def test_config3_scaled(n_stores, n_owners):
+    w = synth.config3(n_txns=40000, n_keys=6000, seed=11 + n_stores)
+    _check(w, synth.shard_bounds(n_stores), n_owners)
+
+
+def test_config4_ranges_sharded():
+    w = synth.config4(n_txns=3000, n_keys=4000, n_ranges=800, n_hist_txns=3000)
+    lo, hi = synth.cut_bounds([-(1 << 30), 0, 1 << 30])
+    _check(w, (lo, hi), 4)
+
+
+def test_config2_scaled_sharded():
+    w = synth.config2(n_txns=20000, n_keys=20000, n_hist_entries=200000)
+    _check(w, synth.shard_bounds(4), 4)
+
+
+def test_merge_rejects_overlapping_sources():
+    dev = torch.device("cuda", 0)
+    w = synth.config3(n_txns=4000, n_keys=500, seed=5)
+    st = native.DeviceCommandStore(0)
+    st.load(w)
+    qdev, keep = native.device_queries(w.queries, dev)
+    e = exchange.GpuEngine(st, qdev, np.arange(len(w.queries)), dev)
+    e.resolve()
+    send, counts = e.export(np.array([0, len(w.queries)], np.uint64))
+    recv = {k: torch.cat([send[k][:int(counts[0, a]) * m]] * 2) for a, (k, m) in enumerate(UNITS)}
+    torch.cuda.synchronize()
+    with pytest.raises(native.AccordDepsError) as ei:
+        st.merge_parts(_parts(recv, 2 * counts[0]), [int(counts[0, 0])] * 2, 0, len(w.queries))
+    assert ei.value.code == A.AD_E_INVAL
+    st.close()
