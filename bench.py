@@ -8,12 +8,11 @@ the requests already resident in HBM when the timed region starts and the Partia
   K0 encode -> K1 CommandsForKey conflict scan -> K4 range probe -> K2 build (size pass,
   offsets, emit pass)  [+ for N > 1: all-to-all of per-store partials over RCCL and K3 merge]
 
-Workload at N = 1: config 2 of BASELINE.json (1M txns x 8 Zipf(0.99) keys over 1M keys, 16M-entry
+Workload: config 2 of BASELINE.json (1M txns x 8 Zipf(0.99) keys over 1M keys, 16M-entry
 CommandsForKey history, SNAPSHOT). For N > 1 the same per-GPU shape is scaled weakly (see
 DESIGN.md §6). Prints ONE JSON line on rank 0.
 """
 import argparse
-import ctypes as C
 import json
 import os
 import sys
@@ -26,7 +25,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (loads the HIP runtime first; see accord_deps.native.lib)
 
 from accord_deps import _abi as A  # noqa: E402
-from accord_deps import native, synth  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from accord_deps import exchange, native, synth  # noqa: E402
 
 METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
@@ -39,25 +40,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def to_dev(a, dev):
-    a = np.ascontiguousarray(a)
-    if a.dtype == np.uint64:
-        a = a.view(np.int64)
-    return torch.from_numpy(a).to(dev)
-
-
-def device_queries(q, dev):
-    keep = {k: to_dev(getattr(v, f) if f else v, dev) for k, v, f in [
-        ("tm", q.txn, "msb"), ("tl", q.txn, "lsb"), ("tn", q.txn, "node"),
-        ("em", q.exec, "msb"), ("el", q.exec, "lsb"), ("en", q.exec, "node"),
-        ("ko", q.key_off, None), ("k", q.keys, None)]}
-    s = A.AdQuerySoa()
-    s.n_txns = len(q)
-    s.txn_msb, s.txn_lsb, s.txn_node = keep["tm"].data_ptr(), keep["tl"].data_ptr(), keep["tn"].data_ptr()
-    s.exec_msb, s.exec_lsb, s.exec_node = keep["em"].data_ptr(), keep["el"].data_ptr(), keep["en"].data_ptr()
-    s.min_epoch = None
-    s.key_off, s.keys = keep["ko"].data_ptr(), keep["k"].data_ptr()
-    return s, keep
+def measured_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary under profiles/
+    (FETCH_SIZE, doubled for gfx950, + WRITE_SIZE; scripts/summarize_prof.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        with open(f) as fh:
+            d = json.load(fh)
+        if kernel in d and d[kernel].get("fetch_bytes_per_launch") is not None:
+            r = d[kernel]
+            return 2 * r["fetch_bytes_per_launch"] + (r.get("write_bytes_per_launch") or 0), os.path.relpath(f, ROOT)
+    return None, None
 
 
 def stage_bytes(w, stats):
@@ -130,51 +124,78 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    dist = None
     if world > 1:
-        import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
-        raise SystemExit("multi-GPU bench: see accord_deps.dist (not wired into bench.py yet)")
 
     s = args.scale
     t0 = time.time()
-    w = synth.config2(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_hist_entries=int(16_000_000 * s))
-    gen_s = time.time() - t0
-    log("generated config2 in %.1f s: %d keys, %d entries, %d txns, %d probes" %
-        (gen_s, len(w.cfk.keys), w.cfk.n_entries, len(w.queries), w.queries.n_probes))
+    w, txn_index, n_total = synth.config2_sharded(rank, world, n_txns_per_gpu=int(1_000_000 * s),
+                                                  n_keys_per_gpu=int(1_000_000 * s),
+                                                  n_hist_entries_per_gpu=int(16_000_000 * s))
+    log("rank %d: generated in %.1f s: %d keys, %d entries, %d of %d requests routed here, %d probes" %
+        (rank, time.time() - t0, len(w.cfk.keys), w.cfk.n_entries, len(w.queries), n_total, w.queries.n_probes))
 
-    store = native.DeviceCommandStore(device=local)
+    store = native.DeviceCommandStore(device=local, slices=w.slices)
     store.load(w)
-    qdev, keep = device_queries(w.queries, dev)
+    qdev, keep = native.device_queries(w.queries, dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
 
+    if world > 1:
+        engine = exchange.GpuEngine(store, qdev, txn_index, dev, stream=sp)
+        ex = exchange.ShardExchange(engine, txn_index, n_total, rank, world, count_device=dev)
+
+        def step():
+            mg = ex.step()
+            return engine.last_stats, mg.ms_device
+    else:
+        def step():
+            _, st = store.deps_batch_device(qdev, sp)
+            return st, 0.0
+
     stats = None
     for _ in range(args.warmup):
-        _, stats = store.deps_batch_device(qdev, sp)
+        stats, _ = step()
     torch.cuda.synchronize(dev)
     if stats:
-        log("ingest %.1f ms (host dictionary + device index build)" % stats["ms_ingest"])
+        log("rank %d: ingest %.1f ms (host dictionary + device index build)" % (rank, stats["ms_ingest"]))
 
     stage_ms = np.zeros(6)
+    merge_ms = 0.0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        _, stats = store.deps_batch_device(qdev, sp)
+        stats, mms = step()
         stage_ms += np.array(stats["ms_stage"][:6])
+        merge_ms += mms
     torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
     elapsed = time.perf_counter() - t_start
     stage_ms /= max(args.steps, 1)
+    merge_ms /= max(args.steps, 1)
+    probes = w.queries.n_probes
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        p = torch.tensor([probes], dtype=torch.int64, device=dev)
+        dist.all_reduce(p, op=dist.ReduceOp.SUM)
+        probes = int(p.item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
-
-    pairs_per_step = w.queries.n_probes
-    value = pairs_per_step * world / (ms_per_step / 1000.0)
+    value = probes / (ms_per_step / 1000.0)
 
     # roofline of the dominant kernel (largest device time per step)
     dom = int(np.argmax(stage_ms))
     sbytes = stage_bytes(w, stats)
     achieved = sbytes[dom] / (stage_ms[dom] / 1000.0) / 1e9 if stage_ms[dom] > 0 else 0.0
+    traffic, traffic_src = measured_traffic(KERNEL_OF_STAGE[dom])
 
     out = {
         "metric": METRIC,
@@ -189,23 +210,28 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": "config2: %d txns x 8 Zipf(0.99) keys over %d keys, %d-entry CommandsForKey "
-                               "history, SNAPSHOT, 1 CommandStore per GPU" % (len(w.queries), int(1_000_000 * s),
-                                                                               w.cfk.n_entries),
-                   "txns_per_step": len(w.queries), "txn_key_pairs_per_step": pairs_per_step,
+        "config": {"workload": "config2 (weak-scaled per GPU): %d txns x 8 Zipf(0.99) keys, %d keys and a %d-entry "
+                               "CommandsForKey history per GPU, SNAPSHOT, 1 CommandStore per GPU%s" %
+                               (n_total, int(1_000_000 * s) * world, w.cfk.n_entries,
+                                ", partials all-to-all over RCCL + on-GPU merge" if world > 1 else ""),
+                   "txns_per_step": n_total, "txn_key_pairs_per_step": probes,
                    "parallelism": "store-per-gpu x%d" % world},
         "roofline": {"bound": "hbm", "kernel": KERNEL_OF_STAGE[dom], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": sbytes[dom], "launch_ms": stage_ms[dom]},
-        "stages_ms": {STAGES[i]: round(float(stage_ms[i]), 4) for i in range(6)},
+        "stages_ms": {STAGES[i]: round(float(stage_ms[i]), 4) for i in range(6) if STAGES[i] != "-"},
         "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
         "ingest_ms": stats["ms_ingest"],
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if world > 1:
+        out["stages_ms"]["merge (K3, owner)"] = round(merge_ms, 4)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     store.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -68,13 +68,13 @@ def _segments(key_rank, txn_idx, n_keys_total):
 
 
 def build_history(rng, n_hist_txns, keys_of_txn, token_of_rank, hist_kind, tail_unapplied,
-                  epoch=1, hlc0=1):
+                  epoch=1, hlc0=1, node_base=0):
     """CFK snapshot for history txns j (txnId hlc = hlc0 + j, node 1..16, kind hist_kind[j]):
     every entry APPLIED with executeAt = txnId except the last `tail_unapplied` entries per key,
     drawn from {PREACCEPTED, ACCEPTED, COMMITTED, STABLE}; ACCEPTED/COMMITTED/STABLE carry an
     executeAt bumped by 1..1000 hlc ticks (CommandsForKey.TxnInfo.create, :272-279)."""
     j = np.arange(n_hist_txns, dtype=np.int64)
-    txn_node = rng.integers(1, 17, n_hist_txns).astype(np.int32)
+    txn_node = (rng.integers(1, 17, n_hist_txns) + node_base).astype(np.int32)
     bump = rng.integers(1, 1001, n_hist_txns).astype(np.uint64)
     txn = make_txn_ids(epoch, hlc0 + j.astype(np.uint64), hist_kind, txn_node)
     k = keys_of_txn.shape[1]
@@ -159,6 +159,88 @@ def config2(n_txns=1_000_000, keys_per_txn=8, n_keys=1_000_000, n_hist_entries=1
                     params=dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys,
                                 n_hist_entries=n_hist * keys_per_txn, zipf_s=zipf_s, seed=seed,
                                 sync_frac=sync_frac, esp_frac=esp_frac, semantics="SNAPSHOT"))
+
+
+def _uniform(h):
+    """u64 hash -> float64 in [0, 1)."""
+    return (h >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+
+def slice_tokens(lo, hi, n, salt):
+    """n distinct i64 tokens inside the slice (lo, hi]: one per equal sub-interval, jittered."""
+    width = int(hi) - int(lo) - 1
+    step = width // n
+    off = np.arange(n, dtype=np.uint64) * np.uint64(step) + splitmix64(np.arange(n, dtype=np.uint64) + np.uint64(salt)) % np.uint64(step)
+    with np.errstate(over="ignore"):
+        return (np.uint64((int(lo) + 1) % (1 << 64)) + off).view(np.int64)
+
+
+def config2_sharded(rank, world, n_txns_per_gpu=1_000_000, keys_per_txn=8, n_keys_per_gpu=1_000_000,
+                    n_hist_entries_per_gpu=16_000_000, zipf_s=0.99, seed=0xACC0D002, sync_frac=0.02,
+                    tail_unapplied=4):
+    """Config 2 weak-scaled over `world` GPUs (one CommandStore per GPU, EvenSplit token slices):
+    store g owns n_keys_per_gpu keys inside slice g and a config-2 history of its own
+    (n_hist_entries_per_gpu entries, 8 Zipf(0.99) keys per history txn, txnIds node-disjoint
+    across stores); the batch holds world * n_txns_per_gpu Read/Write requests x 8 distinct keys,
+    each key on a uniformly chosen store and Zipf(0.99)-ranked within it, so every store sees the
+    config-2 key distribution and ~8 x n_txns_per_gpu probes. At world == 1 this is config 2.
+    Returns (Workload of `rank` holding only the requests routed to it, their global indices,
+    total number of requests). Deterministic in (seed, world): every rank derives the same batch."""
+    lo, hi = shard_bounds(world)
+    z = Zipf(n_keys_per_gpu, zipf_s)
+    # store `rank`: keys and history
+    tok = slice_tokens(lo[rank], hi[rank], n_keys_per_gpu, seed + 7919 * rank)
+    rng = np.random.default_rng([seed, world, rank])
+    token_of_rank = tok[rng.permutation(n_keys_per_gpu)]
+    n_hist = n_hist_entries_per_gpu // keys_per_txn
+    hk = distinct_rows(rng, z.sample, n_hist, keys_per_txn)
+    cfk, _ = build_history(rng, n_hist, hk, token_of_rank, _rw_kinds(rng, n_hist, sync_frac=sync_frac),
+                           tail_unapplied, node_base=16 * rank)
+    # the global batch (same on every rank)
+    T = world * n_txns_per_gpu
+    K = keys_per_txn
+    slot = np.arange(T * K, dtype=np.uint64)
+    salt = np.uint64(seed * 1000003 + world)
+    shard = (splitmix64(slot ^ salt) % np.uint64(world)).reshape(T, K) if world > 1 else np.zeros((T, K), np.uint64)
+    rows, cols = np.nonzero(shard == rank)
+    loc = rows.astype(np.uint64) * np.uint64(K) + cols.astype(np.uint64)
+    zr = np.minimum(np.searchsorted(z.cdf, _uniform(splitmix64(loc + salt * np.uint64(3)))), n_keys_per_gpu - 1)
+    # distinct keys per request: re-draw a slot that repeats a key already drawn in its row
+    rows = rows.astype(np.int64)
+    row_start = np.searchsorted(rows, np.arange(T + 1))        # slots of a row are contiguous
+    cand = np.arange(len(rows))
+    for rnd in range(1, 64):
+        kk = rows[cand] * n_keys_per_gpu + zr[cand]
+        o = np.argsort(kk, kind="stable")                      # equal keys: earlier slot first
+        ks = kk[o]
+        dup = np.zeros(len(o), bool)
+        dup[1:] = ks[1:] == ks[:-1]
+        if not dup.any():
+            break
+        bad = cand[o[dup]]
+        zr[bad] = np.minimum(np.searchsorted(z.cdf, _uniform(splitmix64(loc[bad] + salt * np.uint64(3 + 2 * rnd)))),
+                             n_keys_per_gpu - 1)
+        br = np.unique(rows[bad])
+        cand = np.concatenate([np.arange(row_start[r], row_start[r + 1]) for r in br]) if len(br) < 4096 else \
+            np.nonzero(np.isin(rows, br))[0]
+    qrng = np.random.default_rng([seed, world, 1 << 20])
+    kinds = _rw_kinds(qrng, T)
+    node = qrng.integers(1, 17, T).astype(np.int32)
+    hlc0 = n_hist + 2000
+    idx = np.unique(rows).astype(np.int64)
+    txn = make_txn_ids(1, np.uint64(hlc0) + idx.astype(np.uint64), kinds[idx], node[idx])
+    order = np.lexsort((token_of_rank[zr], rows))
+    keys = token_of_rank[zr][order]
+    counts = np.bincount(rows, minlength=T)[idx]
+    key_off = np.zeros(len(idx) + 1, np.uint64)
+    key_off[1:] = np.cumsum(counts)
+    q = Queries(txn, Tids(txn.msb.copy(), txn.lsb.copy(), txn.node.copy()), key_off, keys)
+    w = Workload("config2_sharded", cfk, RangeCommands.empty(), Redundant.empty(), q,
+                 params=dict(rank=rank, world=world, n_txns_per_gpu=n_txns_per_gpu, keys_per_txn=K,
+                             n_keys_per_gpu=n_keys_per_gpu, n_hist_entries_per_gpu=n_hist * K, zipf_s=zipf_s,
+                             seed=seed, sync_frac=sync_frac, semantics="SNAPSHOT"),
+                 slices=np.array([[lo[rank], hi[rank]]], dtype=np.int64))
+    return w, idx, T
 
 
 def shard_bounds(n_shards):
