@@ -111,6 +111,90 @@ def cpu_baseline(w, budget_s=15.0):
                        "restatement of the reference Java, 1 thread = 1 CommandStore" % (first, total, done_pairs, t))
 
 
+def cpu_baseline_levels(g, budget_s=15.0):
+    """The CPU restatement of the levels computation (oracle rc_levels: executeAt order, per-key
+    predecessor walk, 1 thread) on the whole graph, repeated while within budget."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    t = 0.0
+    reps = 0
+    while reps == 0 or t < budget_s / 4:
+        t0 = time.perf_counter()
+        pyoracle.levels(g)
+        t += time.perf_counter() - t0
+        reps += 1
+    pairs = int(g.key_off[-1]) * reps
+    return dict(value=pairs / t, unit="txn-key pairs/s", cores=1, kind="port",
+                sample="whole config-5 graph x%d (%d txns, %d txn-key pairs each, %.1f s), refcpu rc_levels = C "
+                       "restatement, 1 thread" % (reps, len(g.kind), int(g.key_off[-1]), t))
+
+
+def bench_levels(args, rank, world, local, dev):
+    """Config 5: execution ordering of a 1M-txn waitingOn graph -> apply levels (K5). Not sharded
+    (a txn's keys span stores and levels chain across them): with N GPUs every rank levels its own
+    replica of the graph ("replicas only")."""
+    s = args.scale
+    g, params = synth.config5(n_txns=int(1_000_000 * s), n_keys=max(1, int(100_000 * s)), seed=0xACC0D005 + rank)
+    gdev, keep = native.device_graph(g, dev)
+    out = torch.zeros(len(g.kind), dtype=torch.int32, device=dev)
+    st = native.DeviceCommandStore(device=local)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    stats = None
+    for _ in range(args.warmup):
+        stats = st.levels_device(gdev, out.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ms = np.zeros(2)
+    launches = 0
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        stats = st.levels_device(gdev, out.data_ptr(), stream)
+        ms += np.array(stats["ms_stage"][:2])
+        launches += stats["n_launches"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    ms /= max(args.steps, 1)
+    pairs = int(g.key_off[-1])
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        p = torch.tensor([pairs], dtype=torch.int64, device=dev)
+        dist.all_reduce(p, op=dist.ReduceOp.SUM)
+        pairs = int(p.item())
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    dom = int(np.argmax(ms))
+    names = ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"]
+    achieved = stats["bytes_stage"][dom] / (ms[dom] / 1000.0) / 1e9 if ms[dom] > 0 else 0.0
+    traffic, traffic_src = measured_traffic("k_level_step" if dom == 1 else "k_radix_scatter")
+    res = {
+        "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "config5: %d-txn waitingOn graph x %d keys over %d keys -> topological apply levels"
+                               "%s" % (len(g.kind), params["keys_per_txn"], params["n_keys"],
+                                       ", one replica per GPU" if world > 1 else ""),
+                   "txns_per_step": len(g.kind) * world, "txn_key_pairs_per_step": pairs,
+                   "parallelism": "replicas x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": stats["bytes_stage"][dom], "launch_ms": ms[dom]},
+        "stages_ms": {names[0]: round(float(ms[0]), 4), names[1]: round(float(ms[1]), 4)},
+        "levels": stats["n_levels"], "edges": stats["n_edges"], "frontier_launches_per_step": launches / max(args.steps, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_levels(g, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    st.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +203,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests / dry runs)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 5),
+                    help="2: BASELINE config 2 (the headline line, default); 5: execution levels (K5)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -130,6 +216,9 @@ def main():
     torch.cuda.set_device(dev)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+
+    if args.config == 5:
+        return bench_levels(args, rank, world, local, dev)
 
     s = args.scale
     t0 = time.time()

@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaccord_d
 EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error", "ad_cfk_load",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
-           "ad_copy_to_host", "ad_levels")
+           "ad_copy_to_host", "ad_levels", "ad_levels_device")
 
 
 class AccordDepsError(RuntimeError):
@@ -68,6 +68,8 @@ def lib():
                                      C.c_void_p, C.POINTER(A.AdMerged)]
         L.ad_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
         L.ad_levels.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.POINTER(A.AdStats)]
+        L.ad_levels_device.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.c_void_p,
+                                       C.POINTER(A.AdStats)]
         _lib = L
     return _lib
 
@@ -206,6 +208,12 @@ class DeviceCommandStore:
                                          C.byref(out)))
         return out
 
+    def levels_device(self, gdev, out_ptr, stream=None):
+        """ad_levels_device: graph and output already in HBM. Returns the stats dict."""
+        s = A.AdStats()
+        self._check(lib().ad_levels_device(self.h, C.byref(gdev), out_ptr, stream, C.byref(s)))
+        return levels_stats(s)
+
     def _d2h(self, p, n, dtype):
         a = np.zeros(max(n, 0), dtype)
         if n:
@@ -265,3 +273,49 @@ def resolve(workload, device=0, elide=1, path=0):
         return st.calculate_partial_deps(workload.queries, workload.flags)
     finally:
         st.close()
+
+
+def levels_stats(s):
+    d = stats_dict(s)
+    d.update(n_levels=int(s.n_levels), n_edges=int(s.n_edges), n_launches=int(s.n_launches))
+    return d
+
+
+def levels(graph, device=0):
+    """Apply levels of a waitingOn graph (model.Graph) on the GPU through ad_levels (K5).
+    Returns (u32 levels per txn, stats dict)."""
+    st = DeviceCommandStore(device)
+    try:
+        out = np.zeros(len(graph.kind), np.uint32)
+        s = A.AdStats()
+        soa = graph.soa()
+        st._check(lib().ad_levels(st.h, C.byref(soa), out.ctypes.data, C.byref(s)))
+        return out, levels_stats(s)
+    finally:
+        st.close()
+
+
+def device_graph(graph, dev):
+    """Stage a Graph in HBM (torch tensors as allocator). Returns (AdGraphSoa of device pointers,
+    dict of the tensors that must stay alive)."""
+    import torch
+
+    def to_dev(a):
+        a = np.ascontiguousarray(a)
+        if a.dtype == np.uint64:
+            a = a.view(np.int64)
+        if a.dtype == np.uint32:
+            a = a.view(np.int32)
+        return torch.from_numpy(a).to(dev)
+    keep = {k: to_dev(v) for k, v in [("em", graph.exec.msb), ("el", graph.exec.lsb), ("en", graph.exec.node),
+                                      ("kind", graph.kind), ("ko", graph.key_off), ("k", graph.keys)]}
+    if graph.dep_off is not None:
+        keep["do"] = to_dev(graph.dep_off)
+        keep["d"] = to_dev(graph.deps)
+    s = A.AdGraphSoa()
+    s.n_txns = len(graph.kind)
+    s.exec_msb, s.exec_lsb, s.exec_node = keep["em"].data_ptr(), keep["el"].data_ptr(), keep["en"].data_ptr()
+    s.kind, s.key_off, s.keys = keep["kind"].data_ptr(), keep["ko"].data_ptr(), keep["k"].data_ptr()
+    s.dep_off = keep["do"].data_ptr() if "do" in keep else None
+    s.deps = keep["d"].data_ptr() if "d" in keep else None
+    return s, keep

@@ -327,6 +327,34 @@ def config5(n_txns=1_000_000, keys_per_txn=4, n_keys=100_000, direct_frac=0.01, 
     return g, dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys, direct_frac=direct_frac, seed=seed)
 
 
+def random_graph(seed, n_txns=400, n_keys=30, max_keys=4, direct_frac=0.1, kinds=(0, 1, 2, 3, 4, 5),
+                 long_runs=False):
+    """A waitingOn graph with every Txn.Kind (Read, Write, EphemeralRead, SyncPoint,
+    ExclusiveSyncPoint, LocalOnly), 0..max_keys keys per txn, executeAt order unrelated to the
+    txn index, node ids with both signs, a few epochs, and direct deps pointing both ways in
+    executeAt order (later-executing ones must be ignored) -- for K5 parity tests."""
+    rng = np.random.default_rng(seed)
+    kind = rng.choice(np.asarray(kinds, np.uint8), n_txns).astype(np.uint8)
+    if long_runs:   # long runs of reads on a hot key: the chain walk's worst case
+        kind = np.where(rng.random(n_txns) < 0.9, A.KIND_READ, kind).astype(np.uint8)
+    nk = rng.integers(0, max_keys + 1, n_txns)
+    key_space = rng.choice(np.arange(-1000, 1000), n_keys, replace=False).astype(np.int64)
+    rows = [np.sort(rng.choice(key_space, k, replace=False)) for k in nk]
+    key_off = np.zeros(n_txns + 1, np.uint64)
+    key_off[1:] = np.cumsum(nk)
+    keys = np.concatenate(rows + [np.zeros(0, np.int64)]).astype(np.int64)
+    epoch = rng.integers(1, 4, n_txns).astype(np.uint64)
+    hlc = rng.choice(np.arange(1, 50 * n_txns), n_txns, replace=False).astype(np.uint64)
+    node = rng.integers(-3, 4, n_txns).astype(np.int32)
+    ex = make_timestamps(epoch, hlc, (kind.astype(np.uint64) << np.uint64(1)), node)
+    has = rng.random(n_txns) < direct_frac
+    cnt = np.where(has, rng.integers(1, 4, n_txns), 0)
+    dep_off = np.zeros(n_txns + 1, np.uint64)
+    dep_off[1:] = np.cumsum(cnt)
+    deps = rng.integers(0, n_txns, int(cnt.sum())).astype(np.uint32)
+    return Graph(ex, kind, key_off, keys, dep_off, deps)
+
+
 def slice_workload(w, lo, hi):
     """The part of workload `w` a CommandStore owning the token range from lo to hi sees
     ((lo, hi] for EndInclusive ranges, [lo, hi) for StartInclusive): the CommandsForKey of its

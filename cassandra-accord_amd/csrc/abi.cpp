@@ -23,6 +23,7 @@
 #include "common.hpp"
 #include "exchange.hpp"
 #include "kernels.hpp"
+#include "levels.hpp"
 
 using namespace adx;
 
@@ -203,6 +204,9 @@ struct ad_ctx {
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
     DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t;
+    // execution levels (K5)
+    LevelsWork* lv = nullptr;
+    DevBuf g_em, g_el, g_en, g_kind, g_ko, g_k, g_do, g_d, g_out;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -954,6 +958,7 @@ void ad_ctx_destroy(ad_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->lv) levels_work_destroy(c->lv);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1276,10 +1281,78 @@ int ad_copy_to_host(ad_ctx* c, void* dst, const void* src, uint64_t bytes)
     return AD_OK;
 }
 
+static int levels_run(ad_ctx* c, const LevelsIn& in, uint32_t* out_dev, hipStream_t st, ad_stats* stats)
+{
+    if (!c->lv) c->lv = levels_work_create();
+    LevelsOut lo;
+    std::string err;
+    const int rc = run_levels(c->lv, in, out_dev, st, &lo, &err);
+    if (rc) return c->fail(rc, "%s", err.c_str());
+    if (stats)
+    {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->n_txns = in.n;
+        stats->n_probes = lo.n_occ;
+        stats->ms_device = lo.ms_total;
+        stats->ms_stage[0] = lo.ms_build;
+        stats->ms_stage[1] = lo.ms_frontier;
+        stats->n_levels = lo.n_levels;
+        stats->n_edges = lo.n_edges;
+        stats->n_launches = lo.n_launch;
+        // algorithmic bytes: nodes x (8 B executeAt + 4 B offset + 4 B level)
+        // + edges x 4 B; the build additionally reads the key occurrences (8 B each) once
+        stats->bytes_stage[0] = in.n * 16 + lo.n_occ * 8;
+        stats->bytes_stage[1] = in.n * 8 + lo.n_edges * 4;
+    }
+    return AD_OK;
+}
+
+int ad_levels_device(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, void* stream, ad_stats* stats)
+{
+    if (!c || !g) return AD_E_INVAL;
+    if (g->n_txns && (!g->exec_msb || !g->exec_lsb || !g->exec_node || !g->kind || !g->key_off || !level_out))
+        return c->fail(AD_E_INVAL, "ad_levels_device: null array");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    LevelsIn in{g->n_txns, g->exec_msb, g->exec_lsb, g->exec_node, g->kind, g->key_off, g->keys, g->dep_off, g->deps};
+    return levels_run(c, in, level_out, stream ? (hipStream_t)stream : c->stream, stats);
+}
+
 int ad_levels(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, ad_stats* stats)
 {
-    if (!c) return AD_E_INVAL;
-    return c->fail(AD_E_INVAL, "ad_levels: not implemented yet");
+    if (!c || !g) return AD_E_INVAL;
+    const uint64_t n = g->n_txns;
+    if (n && (!g->exec_msb || !g->exec_lsb || !g->exec_node || !g->kind || !g->key_off || !level_out))
+        return c->fail(AD_E_INVAL, "ad_levels: null array");
+    if (n && g->key_off[0] != 0) return c->fail(AD_E_INVAL, "ad_levels: key_off must start at 0");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (n == 0)
+    {
+        if (stats) std::memset(stats, 0, sizeof(*stats));
+        return AD_OK;
+    }
+    const uint64_t nk = g->key_off[n];
+    if (nk && !g->keys) return c->fail(AD_E_INVAL, "ad_levels: null keys");
+    const uint64_t nd = g->dep_off ? g->dep_off[n] : 0;
+    if (g->dep_off && nd && !g->deps) return c->fail(AD_E_INVAL, "ad_levels: null deps");
+    auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+        if (!b.ensure(std::max<size_t>(bytes, 8))) return c->fail(AD_E_NOMEM, "hipMalloc %zu", bytes);
+        if (bytes) HIPCHK(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        return 0;
+    };
+    int rc;
+    if ((rc = up(c->g_em, g->exec_msb, 8 * n)) || (rc = up(c->g_el, g->exec_lsb, 8 * n)) ||
+        (rc = up(c->g_en, g->exec_node, 4 * n)) || (rc = up(c->g_kind, g->kind, n)) ||
+        (rc = up(c->g_ko, g->key_off, 8 * (n + 1))) || (rc = up(c->g_k, g->keys, 8 * nk)))
+        return rc;
+    if (g->dep_off && ((rc = up(c->g_do, g->dep_off, 8 * (n + 1))) || (rc = up(c->g_d, g->deps, 4 * nd)))) return rc;
+    if (!c->g_out.ensure(4 * n)) return c->fail(AD_E_NOMEM, "hipMalloc levels");
+    LevelsIn in{n, c->g_em.as<uint64_t>(), c->g_el.as<uint64_t>(), c->g_en.as<int32_t>(), c->g_kind.as<uint8_t>(),
+                c->g_ko.as<uint64_t>(), c->g_k.as<int64_t>(), g->dep_off ? c->g_do.as<uint64_t>() : nullptr,
+                g->dep_off ? c->g_d.as<uint32_t>() : nullptr};
+    if ((rc = levels_run(c, in, c->g_out.as<uint32_t>(), c->stream, stats))) return rc;
+    HIPCHK(c, hipMemcpyAsync(level_out, c->g_out.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return AD_OK;
 }
 
 }  // extern "C"

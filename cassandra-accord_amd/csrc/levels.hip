@@ -1,0 +1,656 @@
+// levels.hip — K5: execution-ordering levels for apply scheduling.
+//
+// Reference: a committed txn T executes once everything it waits on has applied
+// (Command.WaitingOn, Command.java:1224-1381; Commands.updateWaitingOn / maybeExecute,
+// Commands.java:617-775; CommandsForKey.notifyManaged, CommandsForKey.java:1193-1274). On each
+// key T waits for every txn P executing before it (executeAt order) whose kind T witnesses
+// (Txn.Kind.witnesses, Txn.java:221-235), and for its direct deps executing before it.
+// level(T) = 0 if T waits on nothing, else 1 + max level(P): the apply round of T when every txn
+// applies as soon as all it waits on has applied (oracle: rc_levels, oracle/refcpu.c).
+//
+// Device pipeline (all integer, HBM/latency bound, no MFMA):
+//   1. rank executeAts: LSD radix sort of txn indices by the normalised Timestamp
+//      (node, then lowHlc|flags, then msb; digits that are constant over the batch are skipped)
+//   2. key chains: the (key, exec rank) occurrences, generated in rank order and stably radix
+//      sorted by key, give every key's txns in executeAt order
+//   3. sparsified predecessors: per occurrence a backward walk of its chain that keeps P only
+//      while no later predecessor already dominates P's kind (a predecessor Q witnessing kind c
+//      has level(Q) > level of every earlier kind-c txn) -> successor CSR + in-degrees
+//   4. frontier loop (Kahn by levels): frontier L = txns whose in-degree reached 0 while
+//      frontier L-1 was processed; one launch per level, launched in chunks between host checks
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/accord_deps.h"
+#include "common.hpp"
+#include "kernels.hpp"
+#include "levels.hpp"
+#include "wave.hpp"
+
+namespace adx {
+
+// ---------------------------------------------------------------------------------------------
+// LSD radix sort of (u64 key, u32 val), 8-bit digits, stable
+// ---------------------------------------------------------------------------------------------
+constexpr int RS_THREADS = 256;
+constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_CHUNKS = 16;                       // 64-element chunks per wave
+constexpr int RS_TILE = RS_THREADS * RS_CHUNKS;     // 4096 elements per block
+
+uint64_t radix_hist_entries(uint64_t n) { return 256 * std::max<uint64_t>(1, (n + RS_TILE - 1) / RS_TILE); }
+
+// per block digit counts -> hist[d * nblk + b] (digit-major, so one flat exclusive scan gives
+// every (digit, block) its output base)
+__global__ __launch_bounds__(RS_THREADS) void k_radix_count(const uint64_t* __restrict__ k, uint64_t n, int shift,
+                                                             uint32_t* __restrict__ hist, uint32_t nblk)
+{
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int c = 0; c < RS_CHUNKS; ++c)
+    {
+        const uint64_t i = base + (uint64_t)c * RS_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&h[(uint32_t)(k[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * nblk + blockIdx.x] = h[threadIdx.x];
+}
+
+// stable scatter: wave w of block b owns elements [b*TILE + w*1024, +1024) in 16 chunks of 64;
+// rank inside a chunk = lanes below with the same digit (8 ballots), chunk order kept by a
+// per-wave running count per digit in LDS
+__global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint64_t* __restrict__ k, const uint32_t* __restrict__ v,
+                                                               uint64_t n, int shift, const uint64_t* __restrict__ off,
+                                                               uint32_t nblk, uint64_t* __restrict__ ko,
+                                                               uint32_t* __restrict__ vo)
+{
+    __shared__ uint64_t cnt[RS_WAVES][256];
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (int d = threadIdx.x; d < RS_WAVES * 256; d += RS_THREADS) (&cnt[0][0])[d] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * (RS_CHUNKS * 64);
+    uint64_t key[RS_CHUNKS];
+    uint32_t val[RS_CHUNKS];
+#pragma unroll
+    for (int c = 0; c < RS_CHUNKS; ++c)
+    {
+        const uint64_t i = base + (uint64_t)c * 64 + lane;
+        key[c] = i < n ? k[i] : 0;
+        val[c] = i < n ? v[i] : 0;
+        if (i < n) atomicAdd((unsigned long long*)&cnt[w][(uint32_t)(key[c] >> shift) & 255u], 1ull);
+    }
+    __syncthreads();
+    // cnt[w][d] <- global base of (d, block) + elements of digit d in earlier waves
+    {
+        const uint32_t d = threadIdx.x;
+        uint64_t run = off[(uint64_t)d * nblk + blockIdx.x];
+        for (int ww = 0; ww < RS_WAVES; ++ww)
+        {
+            const uint64_t c = cnt[ww][d];
+            cnt[ww][d] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int c = 0; c < RS_CHUNKS; ++c)
+    {
+        const uint64_t i = base + (uint64_t)c * 64 + lane;
+        const bool live = i < n;
+        const uint32_t d = (uint32_t)(key[c] >> shift) & 255u;
+        uint64_t m = ballot(live);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit)
+        {
+            const uint64_t b = ballot((d >> bit) & 1u);
+            m &= ((d >> bit) & 1u) ? b : ~b;
+        }
+        const uint64_t pos0 = live ? cnt[w][d] : 0;
+        wave_lds_sync();
+        if (live)
+        {
+            const uint64_t pos = pos0 + __popcll(m & lt);
+            ko[pos] = key[c];
+            vo[pos] = val[c];
+            if ((m >> lane) == 1ull) cnt[w][d] = pos0 + __popcll(m);    // highest lane of its digit group
+        }
+        wave_lds_sync();
+    }
+}
+
+hipError_t radix_sort_pairs(uint64_t* k_in, uint32_t* v_in, uint64_t* k_tmp, uint32_t* v_tmp, uint64_t n,
+                            uint32_t digit_mask, uint32_t* hist, uint64_t* off, uint64_t* bsum, hipStream_t st,
+                            uint64_t** k_res, uint32_t** v_res)
+{
+    uint64_t* ka = k_in;
+    uint32_t* va = v_in;
+    uint64_t* kb = k_tmp;
+    uint32_t* vb = v_tmp;
+    const uint32_t nblk = (uint32_t)std::max<uint64_t>(1, (n + RS_TILE - 1) / RS_TILE);
+    if (n > 1)
+        for (int d = 0; d < 8; ++d)
+        {
+            if (!((digit_mask >> d) & 1u)) continue;
+            k_radix_count<<<nblk, RS_THREADS, 0, st>>>(ka, n, 8 * d, hist, nblk);
+            hipError_t e = run_scan_arrays(hist, off, 256ull * nblk, 1, bsum, st);
+            if (e != hipSuccess) return e;
+            k_radix_scatter<<<nblk, RS_THREADS, 0, st>>>(ka, va, n, 8 * d, off, nblk, kb, vb);
+            std::swap(ka, kb);
+            std::swap(va, vb);
+        }
+    *k_res = ka;
+    *v_res = va;
+    return hipGetLastError();
+}
+
+static uint32_t digits_of(uint64_t diff)
+{
+    uint32_t m = 0;
+    for (int d = 0; d < 8; ++d)
+        if ((diff >> (8 * d)) & 0xFF) m |= 1u << d;
+    return m;
+}
+
+// ---------------------------------------------------------------------------------------------
+// K5 kernels
+// ---------------------------------------------------------------------------------------------
+struct LevelsCtl {
+    unsigned long long diff[4];     // OR of (word ^ word of element 0): exec node, lo, hi; occurrence keys
+    unsigned int error;             // AD_E_* (negated)
+    unsigned int pad;
+};
+
+constexpr unsigned RED_BLOCKS = 512;     // grid of the reducing kernels: one atomic per block and word
+
+// OR of v over the block (256 threads) -> one atomicOr per block
+__device__ __forceinline__ void block_or_to(unsigned long long* dst, uint64_t v, uint64_t* red /* LDS [4] */)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v |= __shfl_xor(v, d, 64);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        const uint64_t x = red[0] | red[1] | red[2] | red[3];
+        if (x) atomicOr(dst, (unsigned long long)x);
+    }
+    __syncthreads();
+}
+
+// normalised executeAt words (Timestamp.compareTo order, Timestamp.java:208-217, common.hpp
+// norm_tid): w0 = node with the sign flipped (signed compare), w1 = lowHlc|identity flags, w2 = msb
+__global__ __launch_bounds__(256) void k_exec_words(LevelsIn g, uint64_t* __restrict__ w0, uint32_t* __restrict__ idx,
+                                                    LevelsCtl* ctl)
+{
+    __shared__ uint64_t red[4];
+    uint64_t d0 = 0, d1 = 0, d2 = 0;
+    const NormTid z = norm_tid(g.exec_msb[0], g.exec_lsb[0], g.exec_node[0]);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n; i += (uint64_t)gridDim.x * blockDim.x)
+    {
+        const NormTid x = norm_tid(g.exec_msb[i], g.exec_lsb[i], g.exec_node[i]);
+        w0[i] = (uint64_t)((uint32_t)x.node ^ 0x80000000u);
+        idx[i] = (uint32_t)i;
+        d0 |= (uint64_t)((uint32_t)x.node ^ (uint32_t)z.node);
+        d1 |= x.lo ^ z.lo;
+        d2 |= x.hi ^ z.hi;
+    }
+    block_or_to(&ctl->diff[0], d0, red);
+    block_or_to(&ctl->diff[1], d1, red);
+    block_or_to(&ctl->diff[2], d2, red);
+}
+
+// next (more significant) word of the current order
+__global__ void k_exec_gather(LevelsIn g, const uint32_t* __restrict__ idx, int word, uint64_t* __restrict__ out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.n) return;
+    const uint32_t t = idx[i];
+    const NormTid x = norm_tid(g.exec_msb[t], g.exec_lsb[t], g.exec_node[t]);
+    out[i] = word == 1 ? x.lo : x.hi;
+}
+
+// rank[order[r]] = r; kind by rank; key count by rank; duplicate executeAt -> AD_E_DUP_EXEC
+// (the reference's committedByExecuteAt never holds two, CommandsForKey.java:1439)
+__global__ void k_exec_rank(LevelsIn g, const uint32_t* __restrict__ order, uint32_t* __restrict__ rank,
+                            uint8_t* __restrict__ kind_r, uint32_t* __restrict__ kcnt_r, LevelsCtl* ctl)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= g.n) return;
+    const uint32_t t = order[r];
+    rank[t] = (uint32_t)r;
+    kind_r[r] = g.kind[t];
+    kcnt_r[r] = (uint32_t)(g.key_off[t + 1] - g.key_off[t]);
+    if (r > 0)
+    {
+        const uint32_t p = order[r - 1];
+        const NormTid a = norm_tid(g.exec_msb[p], g.exec_lsb[p], g.exec_node[p]);
+        const NormTid b = norm_tid(g.exec_msb[t], g.exec_lsb[t], g.exec_node[t]);
+        if (norm_cmp(a, b) == 0) atomicCAS(&ctl->error, 0u, (unsigned)(-AD_E_DUP_EXEC));
+    }
+}
+
+// occurrences in exec-rank order: okey = key with the sign flipped, oval = rank
+__global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __restrict__ order,
+                                                  const uint64_t* __restrict__ occ_off, uint64_t* __restrict__ okey,
+                                                  uint32_t* __restrict__ oval, LevelsCtl* ctl)
+{
+    __shared__ uint64_t red[4];
+    uint64_t d = 0;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < g.n; r += (uint64_t)gridDim.x * blockDim.x)
+    {
+        const uint32_t t = order[r];
+        const uint64_t s = g.key_off[t], e = g.key_off[t + 1], o = occ_off[r];
+        const uint64_t ref = (uint64_t)g.keys[0];
+        for (uint64_t j = s; j < e; ++j)
+        {
+            const uint64_t k = (uint64_t)g.keys[j];
+            okey[o + (j - s)] = k ^ 0x8000000000000000ull;
+            oval[o + (j - s)] = (uint32_t)r;
+            d |= k ^ ref;
+        }
+    }
+    block_or_to(&ctl->diff[3], d, red);
+}
+
+// Sparsified predecessors of the occurrence at p (chain sorted by (key, rank)): walk back while
+// some kind T witnesses is not yet dominated. A txn P of kind c is dominated once a predecessor
+// (or a dominated txn) found later in the walk witnesses c: that one executes after P and waits
+// on it, so its level is larger. Pass 0: in-degree of T and out-degree of each P; pass 1: succ.
+template <int PASS>
+__global__ void k_chain(const uint64_t* __restrict__ okey, const uint32_t* __restrict__ orank, uint64_t n_occ,
+                        const uint8_t* __restrict__ kind_r, uint32_t* __restrict__ indeg, uint32_t* __restrict__ outdeg,
+                        const uint64_t* __restrict__ succ_off, uint32_t* __restrict__ cursor, uint32_t* __restrict__ succ)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_occ) return;
+    const uint64_t key = okey[p];
+    const uint32_t T = orank[p];
+    const uint32_t A = kind_witnesses(kind_r[T]);
+    uint32_t D = 0, npred = 0;
+    for (uint64_t q = p; q-- > 0 && (A & ~D) != 0;)
+    {
+        if (okey[q] != key) break;
+        const uint32_t P = orank[q];
+        const uint32_t kp = kind_r[P];
+        const uint32_t bit = kp < 32 ? 1u << kp : 0u;
+        if (A & bit & ~D)
+        {
+            ++npred;
+            if (PASS == 0) atomicAdd(&outdeg[P], 1u);
+            else succ[succ_off[P] + atomicAdd(&cursor[P], 1u)] = T;
+            D |= kind_witnesses(kp);
+        }
+        else if (D & bit)
+            D |= kind_witnesses(kp);
+    }
+    if (PASS == 0 && npred) atomicAdd(&indeg[T], npred);
+}
+
+// direct deps (Commands.updateWaitingOn keeps only those executing earlier, Commands.java:700-775)
+template <int PASS>
+__global__ void k_direct(LevelsIn g, const uint32_t* __restrict__ rank, uint32_t* __restrict__ indeg,
+                         uint32_t* __restrict__ outdeg, const uint64_t* __restrict__ succ_off,
+                         uint32_t* __restrict__ cursor, uint32_t* __restrict__ succ, LevelsCtl* ctl)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= g.n) return;
+    const uint32_t T = rank[t];
+    uint32_t npred = 0;
+    for (uint64_t d = g.dep_off[t]; d < g.dep_off[t + 1]; ++d)
+    {
+        const uint32_t src = g.deps[d];
+        if (src >= g.n)
+        {
+            atomicCAS(&ctl->error, 0u, (unsigned)(-AD_E_INVAL));
+            return;
+        }
+        const uint32_t P = rank[src];
+        if (P >= T) continue;
+        ++npred;
+        if (PASS == 0) atomicAdd(&outdeg[P], 1u);
+        else succ[succ_off[P] + atomicAdd(&cursor[P], 1u)] = T;
+    }
+    if (PASS == 0 && npred) atomicAdd(&indeg[T], npred);
+}
+
+__device__ __forceinline__ void wave_append(uint32_t* __restrict__ front, uint32_t* cnt, bool take, uint32_t v)
+{
+    const uint64_t m = ballot(take);
+    if (!m) return;
+    uint32_t base = 0;
+    const uint32_t leader = __ffsll((unsigned long long)m) - 1;
+    if (lane_id() == leader) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (take) front[base + mbcnt(m)] = v;
+}
+
+__global__ void k_frontier_init(const uint32_t* __restrict__ indeg, uint64_t n, uint32_t* __restrict__ level,
+                                uint32_t* __restrict__ front, uint32_t* cnt)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool take = r < n && indeg[r] == 0;
+    if (take) level[r] = 0;
+    wave_append(front, cnt, take, (uint32_t)r);
+}
+
+// one level: every txn of frontier L releases its successors; those whose last predecessor this
+// was form frontier L+1 (their longest path from a source is exactly L+1). Edge-parallel: a wave
+// takes STEP_GROUP frontier txns and spreads their successor edges over its 64 lanes, so a txn
+// with many successors costs rounds of 64 independent atomics, not a serial per-lane loop.
+constexpr uint32_t STEP_GROUP = 16;
+
+__global__ __launch_bounds__(256) void k_level_step(uint32_t L, const uint32_t* __restrict__ cnt,
+                                                    const uint32_t* __restrict__ front_in, uint32_t* __restrict__ front_out,
+                                                    uint32_t* cnt_out, const uint64_t* __restrict__ succ_off,
+                                                    const uint32_t* __restrict__ succ, uint32_t* __restrict__ indeg,
+                                                    uint32_t* __restrict__ level)
+{
+    const uint32_t F = cnt[L];
+    if (F == 0) return;
+    const uint32_t lane = lane_id();
+    const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (uint32_t g0 = wid * STEP_GROUP; g0 < F; g0 += n_waves * STEP_GROUP)
+    {
+        // lanes j < STEP_GROUP: frontier txn g0 + j, its first edge and degree
+        uint64_t e0 = 0;
+        uint32_t deg = 0;
+        if (lane < STEP_GROUP && g0 + lane < F)
+        {
+            const uint32_t u = front_in[g0 + lane];
+            e0 = succ_off[u];
+            deg = (uint32_t)(succ_off[u + 1] - e0);
+        }
+        uint32_t inc = deg;
+#pragma unroll
+        for (uint32_t d = 1; d < STEP_GROUP; d <<= 1)
+        {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
+        }
+        uint32_t incl[STEP_GROUP];
+#pragma unroll
+        for (uint32_t j = 0; j < STEP_GROUP; ++j) incl[j] = __shfl(inc, j, 64);
+        const uint32_t total = incl[STEP_GROUP - 1];
+        for (uint32_t x0 = 0; x0 < total; x0 += 64)
+        {
+            const uint32_t x = x0 + lane;
+            bool take = false;
+            uint32_t s = 0;
+            uint32_t owner = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < STEP_GROUP; ++j) owner += incl[j] <= x ? 1u : 0u;
+            const uint64_t eo = __shfl(e0, owner & (STEP_GROUP - 1), 64);
+            // shuffles by every lane (a lane outside the exec mask reads back 0)
+            const uint32_t prev = __shfl(inc, (owner - 1) & (STEP_GROUP - 1), 64);
+            const uint32_t before = owner == 0 ? 0u : prev;
+            if (x < total)
+            {
+                s = succ[eo + (x - before)];
+                take = atomicSub(&indeg[s], 1u) == 1u;
+                if (take) level[s] = L + 1;
+            }
+            wave_append(front_out, cnt_out, take, s);
+        }
+    }
+}
+
+__global__ void k_level_out(const uint32_t* __restrict__ order, const uint32_t* __restrict__ level_r, uint64_t n,
+                            uint32_t* __restrict__ out)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) out[order[r]] = level_r[r];
+}
+
+// ---------------------------------------------------------------------------------------------
+// host driver
+// ---------------------------------------------------------------------------------------------
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DBuf()
+    {
+        if (p) (void)hipFree(p);
+    }
+    bool ensure(size_t bytes)
+    {
+        if (p && bytes <= cap) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t b = std::max<size_t>(bytes, 64);
+        if (hipMalloc(&p, b) != hipSuccess) return false;
+        cap = b;
+        return true;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct LevelsWork {
+    DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kind_r, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
+        level, front0, front1, cnt, ctl;
+    LevelsCtl* h_ctl = nullptr;         // pinned
+    uint64_t* h_u64 = nullptr;          // pinned, 4 words
+    hipEvent_t ev[3] = {};
+    ~LevelsWork()
+    {
+        if (h_ctl) (void)hipHostFree(h_ctl);
+        if (h_u64) (void)hipHostFree(h_u64);
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+LevelsWork* levels_work_create() { return new LevelsWork(); }
+void levels_work_destroy(LevelsWork* w) { delete w; }
+
+constexpr uint32_t STEP_CHUNK = 32;     // frontier launches between host checks
+constexpr unsigned STEP_BLOCKS = 64;
+
+#define LV_CHK(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess)                                                            \
+        {                                                                                \
+            *err = std::string(#expr) + ": " + hipGetErrorString(_e);                    \
+            return AD_E_DEVICE;                                                          \
+        }                                                                                \
+    } while (0)
+#define LV_ALLOC(buf, bytes)                                                             \
+    do {                                                                                 \
+        if (!(buf).ensure(bytes))                                                        \
+        {                                                                                \
+            *err = "hipMalloc failed (" #buf ")";                                        \
+            return AD_E_NOMEM;                                                           \
+        }                                                                                \
+    } while (0)
+
+static unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)std::max<uint64_t>(1, (n + t - 1) / t); }
+
+int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_t st, LevelsOut* out, std::string* err)
+{
+    *out = LevelsOut{};
+    const uint64_t n = g.n;
+    if (n == 0) return AD_OK;
+    if (n >= (1ull << 32) - 64)
+    {
+        *err = "ad_levels: too many txns (u32 ranks)";
+        return AD_E_CAPACITY;
+    }
+    if (!w->h_ctl) LV_CHK(hipHostMalloc((void**)&w->h_ctl, sizeof(LevelsCtl), hipHostMallocDefault));
+    if (!w->h_u64) LV_CHK(hipHostMalloc((void**)&w->h_u64, 4 * sizeof(uint64_t), hipHostMallocDefault));
+    for (auto& e : w->ev)
+        if (!e) LV_CHK(hipEventCreate(&e));
+
+    // sizes: occurrences = key_off[n] (key_off[0] must be 0)
+    LV_CHK(hipMemcpyAsync(&w->h_u64[0], g.key_off, 8, hipMemcpyDeviceToHost, st));
+    LV_CHK(hipMemcpyAsync(&w->h_u64[1], g.key_off + n, 8, hipMemcpyDeviceToHost, st));
+    LV_CHK(hipStreamSynchronize(st));
+    if (w->h_u64[0] != 0 || w->h_u64[1] > (1ull << 40))
+    {
+        *err = "ad_levels: key_off must start at 0";
+        return AD_E_INVAL;
+    }
+    const uint64_t n_occ = w->h_u64[1];
+    out->n_occ = n_occ;
+    const uint64_t cap = std::max(n, n_occ);
+    const uint64_t hist_n = radix_hist_entries(cap);
+    LV_ALLOC(w->ctl, sizeof(LevelsCtl));
+    LV_ALLOC(w->ka, 8 * cap);
+    LV_ALLOC(w->kb, 8 * cap);
+    LV_ALLOC(w->va, 4 * cap);
+    LV_ALLOC(w->vb, 4 * cap);
+    LV_ALLOC(w->hist, 4 * hist_n);
+    LV_ALLOC(w->off, 8 * (hist_n + 1));
+    LV_ALLOC(w->bsum, 8 * (std::max(hist_n, n) / 1024 + 2));
+    LV_ALLOC(w->ord, 4 * n);
+    LV_ALLOC(w->rank, 4 * n);
+    LV_ALLOC(w->kind_r, n);
+    LV_ALLOC(w->kcnt, 4 * n);
+    LV_ALLOC(w->occ_off, 8 * (n + 1));
+    LV_ALLOC(w->indeg, 4 * n);
+    LV_ALLOC(w->outdeg, 4 * n);
+    LV_ALLOC(w->cursor, 4 * n);
+    LV_ALLOC(w->succ_off, 8 * (n + 1));
+    LV_ALLOC(w->level, 4 * n);
+    LV_ALLOC(w->front0, 4 * n);
+    LV_ALLOC(w->front1, 4 * n);
+    LV_ALLOC(w->cnt, 4 * (n + 2 + STEP_CHUNK));
+    LevelsCtl* ctl = w->ctl.as<LevelsCtl>();
+    uint64_t* ka = w->ka.as<uint64_t>();
+    uint64_t* kb = w->kb.as<uint64_t>();
+    uint32_t* va = w->va.as<uint32_t>();
+    uint32_t* vb = w->vb.as<uint32_t>();
+    uint32_t* hist = w->hist.as<uint32_t>();
+    uint64_t* off = w->off.as<uint64_t>();
+    uint64_t* bsum = w->bsum.as<uint64_t>();
+    uint32_t* order = w->ord.as<uint32_t>();
+    uint32_t* indeg = w->indeg.as<uint32_t>();
+    uint32_t* outdeg = w->outdeg.as<uint32_t>();
+    uint32_t* cursor = w->cursor.as<uint32_t>();
+    uint64_t* succ_off = w->succ_off.as<uint64_t>();
+    uint32_t* level = w->level.as<uint32_t>();
+    uint32_t* cnt = w->cnt.as<uint32_t>();
+
+    LV_CHK(hipEventRecord(w->ev[0], st));
+    LV_CHK(hipMemsetAsync(ctl, 0, sizeof(LevelsCtl), st));
+    LV_CHK(hipMemsetAsync(indeg, 0, 4 * n, st));
+    LV_CHK(hipMemsetAsync(outdeg, 0, 4 * n, st));
+    LV_CHK(hipMemsetAsync(cursor, 0, 4 * n, st));
+    LV_CHK(hipMemsetAsync(cnt, 0, 4 * (n + 2 + STEP_CHUNK), st));
+
+    // ---- 1. exec ranking: LSD over node, then lowHlc|flags, then msb
+    k_exec_words<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, ka, va, ctl);
+    LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
+    LV_CHK(hipStreamSynchronize(st));
+    const uint64_t dx[3] = {w->h_ctl->diff[0], w->h_ctl->diff[1], w->h_ctl->diff[2]};
+    uint64_t* kcur = ka;
+    uint32_t* vcur = va;
+    for (int word = 0; word < 3; ++word)
+    {
+        const uint32_t dm = digits_of(dx[word]);
+        if (!dm) continue;
+        if (word > 0) k_exec_gather<<<blocks_for(n, 256), 256, 0, st>>>(g, vcur, word, kcur);
+        LV_CHK(radix_sort_pairs(kcur, vcur, kcur == ka ? kb : ka, vcur == va ? vb : va, n, dm, hist, off, bsum, st,
+                                &kcur, &vcur));
+    }
+    LV_CHK(hipMemcpyAsync(order, vcur, 4 * n, hipMemcpyDeviceToDevice, st));
+    k_exec_rank<<<blocks_for(n, 256), 256, 0, st>>>(g, order, w->rank.as<uint32_t>(), w->kind_r.as<uint8_t>(),
+                                                    w->kcnt.as<uint32_t>(), ctl);
+    LV_CHK(run_scan_arrays(w->kcnt.as<uint32_t>(), w->occ_off.as<uint64_t>(), n, 1, bsum, st));
+
+    // ---- 2. key chains: occurrences in rank order, stably sorted by key
+    uint64_t* okey = ka;
+    uint32_t* oval = va;
+    if (n_occ)
+    {
+        k_occ_fill<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, order, w->occ_off.as<uint64_t>(), okey, oval, ctl);
+        LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
+        LV_CHK(hipStreamSynchronize(st));
+        LV_CHK(radix_sort_pairs(okey, oval, kb, vb, n_occ, digits_of(w->h_ctl->diff[3]), hist, off, bsum, st, &okey,
+                                &oval));
+    }
+
+    // ---- 3. sparsified predecessors -> successor CSR + in-degrees
+    if (n_occ)
+        k_chain<0><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), indeg, outdeg,
+                                                           nullptr, nullptr, nullptr);
+    if (g.dep_off)
+        k_direct<0><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), indeg, outdeg, nullptr, nullptr,
+                                                        nullptr, ctl);
+    LV_CHK(run_scan_arrays(outdeg, succ_off, n, 1, bsum, st));
+    LV_CHK(hipMemcpyAsync(&w->h_u64[2], succ_off + n, 8, hipMemcpyDeviceToHost, st));
+    LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
+    LV_CHK(hipStreamSynchronize(st));
+    if (w->h_ctl->error)
+    {
+        const int code = -(int)w->h_ctl->error;
+        *err = code == AD_E_DUP_EXEC ? "ad_levels: two txns with the same executeAt (CommandsForKey.java:1439)"
+                                     : "ad_levels: direct dep index out of range";
+        return code;
+    }
+    const uint64_t n_edges = w->h_u64[2];
+    out->n_edges = n_edges;
+    LV_ALLOC(w->succ, 4 * std::max<uint64_t>(n_edges, 1));
+    uint32_t* succ = w->succ.as<uint32_t>();
+    if (n_occ)
+        k_chain<1><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), nullptr, nullptr,
+                                                           succ_off, cursor, succ);
+    if (g.dep_off)
+        k_direct<1><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), nullptr, nullptr, succ_off, cursor,
+                                                        succ, ctl);
+    LV_CHK(hipEventRecord(w->ev[1], st));
+
+    // ---- 4. frontier loop
+    uint32_t* fr[2] = {w->front0.as<uint32_t>(), w->front1.as<uint32_t>()};
+    k_frontier_init<<<blocks_for(n, 256), 256, 0, st>>>(indeg, n, level, fr[0], cnt);
+    uint32_t L = 0;
+    while (true)
+    {
+        for (uint32_t c = 0; c < STEP_CHUNK; ++c, ++L)
+            k_level_step<<<STEP_BLOCKS, 256, 0, st>>>(L, cnt, fr[L & 1], fr[(L + 1) & 1], cnt + L + 1, succ_off, succ,
+                                                      indeg, level);
+        out->n_launch += STEP_CHUNK;
+        LV_CHK(hipGetLastError());
+        LV_CHK(hipMemcpyAsync(&w->h_u64[3], cnt + L, 4, hipMemcpyDeviceToHost, st));
+        LV_CHK(hipStreamSynchronize(st));
+        if ((uint32_t)w->h_u64[3] == 0) break;
+        if (L >= n + 1)
+        {
+            *err = "ad_levels: frontier did not drain";
+            return AD_E_STATE;
+        }
+    }
+    k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
+    LV_CHK(hipEventRecord(w->ev[2], st));
+    // levels = frontiers before the first empty one; every txn must have been levelled
+    std::vector<uint32_t> counts(L + 1);
+    LV_CHK(hipMemcpyAsync(counts.data(), cnt, 4 * (L + 1), hipMemcpyDeviceToHost, st));
+    LV_CHK(hipStreamSynchronize(st));
+    uint64_t total = 0, nl = 0;
+    for (uint32_t i = 0; i <= L && counts[i]; ++i)
+    {
+        total += counts[i];
+        nl = i + 1;
+    }
+    if (total != n)
+    {
+        *err = "ad_levels: " + std::to_string(n - total) + " txns never became ready";
+        return AD_E_STATE;
+    }
+    out->n_levels = nl;
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
+    (void)hipEventElapsedTime(&b, w->ev[1], w->ev[2]);
+    out->ms_build = a;
+    out->ms_frontier = b;
+    out->ms_total = a + b;
+    return AD_OK;
+}
+
+}  // namespace adx

@@ -187,6 +187,11 @@ typedef struct ad_stats {
                                       * 4 offsets, 5 pack */
     uint64_t n_deferred;             /* requests resolved by the split kernels (path 0)       */
     uint64_t bytes_stage[8];         /* algorithmic bytes per stage            */
+    /* ad_levels: n_txns, n_probes = txn-key occurrences, ms_stage[0] build (exec ranking, key
+     * chains, successor CSR), ms_stage[1] frontier loop, and: */
+    uint64_t n_levels;               /* 1 + max level                                         */
+    uint64_t n_edges;                /* edges of the sparsified waitingOn DAG                  */
+    uint64_t n_launches;             /* frontier-step launches                                */
 } ad_stats;
 
 /* Results, one CSR triple per map and request, packed in request order.
@@ -320,6 +325,11 @@ typedef struct ad_graph_soa {
 } ad_graph_soa;
 
 int ad_levels(ad_ctx* ctx, const ad_graph_soa* g, uint32_t* level_out, ad_stats* stats);
+
+/* As ad_levels with every array of g and level_out in device memory (HBM); the work is
+ * enqueued on `stream` (NULL = the ctx stream) and complete on return. key_off[0] must be 0.
+ * Errors: AD_E_DUP_EXEC (two txns with equal executeAt), AD_E_INVAL (dep index >= n_txns). */
+int ad_levels_device(ad_ctx* ctx, const ad_graph_soa* g_dev, uint32_t* level_out_dev, void* stream, ad_stats* stats);
 
 #ifdef __cplusplus
 }

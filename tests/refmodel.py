@@ -137,3 +137,41 @@ def csr(pairs):
         body.extend(idx)
         out.append(len(keys) + len(body))
     return keys, [v[1] for v in vals], out + body
+
+
+def levels_by_rounds(g):
+    """Apply rounds of a waitingOn graph, by direct simulation (independent of rc_levels): in
+    round r every txn applies whose waits (every earlier-executing txn on a shared key whose kind
+    it witnesses, Txn.java:221-235, and every earlier-executing direct dep) all applied before r."""
+    import numpy as np
+    n = len(g.kind)
+    order = np.lexsort(g.exec.order_key())
+    pos = np.empty(n, np.int64)
+    pos[order] = np.arange(n)
+    waits = [set() for _ in range(n)]
+    by_key = {}
+    for t in range(n):
+        for k in g.keys[int(g.key_off[t]):int(g.key_off[t + 1])]:
+            by_key.setdefault(int(k), []).append(t)
+    for ts in by_key.values():
+        ts.sort(key=lambda t: pos[t])
+        for j, t in enumerate(ts):
+            w = WITNESSES.get(int(g.kind[t]), set())
+            for p in ts[:j]:
+                if int(g.kind[p]) in w:
+                    waits[t].add(p)
+    if g.dep_off is not None:
+        for t in range(n):
+            for d in g.deps[int(g.dep_off[t]):int(g.dep_off[t + 1])]:
+                if pos[int(d)] < pos[t]:
+                    waits[t].add(int(d))
+    level = np.full(n, -1)
+    r = 0
+    done = 0
+    while done < n:
+        ready = [t for t in range(n) if level[t] < 0 and all(0 <= level[p] < r for p in waits[t])]
+        for t in ready:
+            level[t] = r
+        done += len(ready)
+        r += 1
+    return level

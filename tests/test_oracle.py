@@ -171,36 +171,14 @@ def test_timestamp_compare_and_equals(oracle):
 def test_levels_match_round_simulation(oracle):
     # level(T) = apply round when every txn applies as soon as all it waits on have applied
     g, _ = synth.config5(n_txns=3000, n_keys=300)
-    lv = oracle.levels(g)
-    n = len(g.kind)
-    order = np.lexsort(g.exec.order_key())
-    pos = np.empty(n, np.int64)
-    pos[order] = np.arange(n)
-    waits = [set() for _ in range(n)]
-    by_key = {}
-    for t in range(n):
-        for k in g.keys[int(g.key_off[t]):int(g.key_off[t + 1])]:
-            by_key.setdefault(int(k), []).append(t)
-    for k, ts in by_key.items():
-        ts.sort(key=lambda t: pos[t])
-        for j, t in enumerate(ts):
-            for p in ts[:j]:
-                if int(g.kind[p]) in refmodel.WITNESSES[int(g.kind[t])]:
-                    waits[t].add(p)
-    for t in range(n):
-        for d in g.deps[int(g.dep_off[t]):int(g.dep_off[t + 1])]:
-            if pos[int(d)] < pos[t]:
-                waits[t].add(int(d))
-    level = np.full(n, -1)
-    r = 0
-    done = 0
-    while done < n:
-        ready = [t for t in range(n) if level[t] < 0 and all(level[p] >= 0 and level[p] < r for p in waits[t])]
-        for t in ready:
-            level[t] = r
-        done += len(ready)
-        r += 1
-    assert np.array_equal(level, lv.astype(np.int64))
+    assert np.array_equal(refmodel.levels_by_rounds(g), oracle.levels(g).astype(np.int64))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_levels_all_kinds_match_round_simulation(oracle, seed):
+    # every Txn.Kind (incl. EphemeralRead / LocalOnly, witnessed by nobody), direct deps both ways
+    g = synth.random_graph(seed, n_txns=300, n_keys=12 + 4 * seed, long_runs=(seed == 5))
+    assert np.array_equal(refmodel.levels_by_rounds(g), oracle.levels(g).astype(np.int64))
 
 
 def test_oracle_rejects_invalid_inputs(oracle):
