@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures of tests/golden/ from the CPU restatement (oracle/refcpu.c).
+
+The reference (Java) cannot run in this image (no JDK) and holds no golden vectors
+of its own, so these fixtures are outputs of the oracle, which is itself pinned by the
+reference's known answers (PreAcceptTest, see kats.json) and ported model tests
+(tests/test_oracle.py). They freeze the oracle's answers so that (a) any later change to the
+oracle or the generators is caught, and (b) the GPU path is checked against committed data.
+
+Usage: python tests/golden/make_golden.py          (writes tests/golden/*.npz, MANIFEST.json)
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, "cassandra-accord_amd"), os.path.join(ROOT, "oracle"), HERE]
+
+import numpy as np  # noqa: E402
+
+import golden_io  # noqa: E402
+import pyoracle  # noqa: E402
+from accord_deps import synth  # noqa: E402
+
+
+def deps_cases():
+    """(file stem, workload, elide) — one per behaviour the reference tests exercise."""
+    yield "random_small_s0", synth.random_small(1000), 1
+    yield "random_small_s1_slices", synth.random_small(1001, with_slices=True), 1
+    yield "random_small_s2_start_inclusive", synth.random_small(1002, start_inclusive=True), 1
+    yield "random_small_s3_no_elision", synth.random_small(1003), 0
+    yield "random_small_s4_big", synth.random_small(1004, n_keys=60, n_hist_txns=1500, n_txns=300, max_keys=12,
+                                                    n_range_cmds=80), 1
+    yield "config1_n2000", synth.config1(n_txns=2000, n_keys=200), 1
+    yield "config2_small", synth.config2(n_txns=2000, n_keys=3000, n_hist_entries=40_000, esp_frac=0.05), 1
+    yield "config4_small", synth.config4(n_txns=1500, n_keys=3000, n_ranges=400, n_hist_txns=3000), 1
+
+
+def level_cases():
+    g, _ = synth.config5(n_txns=20_000, n_keys=2_000)
+    yield "levels_config5_n20000", g
+    yield "levels_random_all_kinds", synth.random_graph(2000, n_txns=3000, n_keys=40)
+
+
+def main():
+    pyoracle.build()
+    manifest = {}
+    for stem, w, elide in deps_cases():
+        exp = pyoracle.resolve(w, elide=elide)
+        d = golden_io.workload_arrays(w)
+        d.update(golden_io.batch_arrays(exp))
+        d["elide"] = np.array([elide], np.int32)
+        path = os.path.join(HERE, stem + ".npz")
+        np.savez_compressed(path, **d)
+        manifest[stem + ".npz"] = dict(kind="deps", requests=len(w.queries), pairs=[exp.pair_count(m) for m in range(3)])
+    for stem, g in level_cases():
+        lv = pyoracle.levels(g)
+        path = os.path.join(HERE, stem + ".npz")
+        np.savez_compressed(path, **golden_io.graph_arrays(g, lv))
+        manifest[stem + ".npz"] = dict(kind="levels", txns=len(g.kind), levels=int(lv.max()) + 1)
+    for f in sorted(manifest):
+        with open(os.path.join(HERE, f), "rb") as fh:
+            manifest[f]["sha256"] = hashlib.sha256(fh.read()).hexdigest()
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as fh:
+        json.dump(manifest, fh, indent=1, sort_keys=True)
+    print(json.dumps(manifest, indent=1))
+
+
+if __name__ == "__main__":
+    main()
