@@ -182,7 +182,7 @@ struct ad_ctx {
     std::vector<int32_t> dict_node;
     std::vector<int64_t> rt_start, rt_end;     // range table (distinct ranges, by Range.compare)
     DevSnapshot ds{};
-    DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_krec, d_khash, d_ent, d_w;
+    DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_krec, d_khash, d_kent, d_cand, d_cwr, d_ent, d_w;
     DevBuf d_lvl[NCLASS][MAX_LEVELS];
     DevBuf d_rstart, d_rend, d_rtxw, d_rrid;
     DevBuf d_rlvl[NCLASS][MAX_LEVELS];
@@ -477,7 +477,7 @@ static int build_snapshot(ad_ctx* c)
 
     // ---- 4. upload CFK + dictionary, build the trees
     int rc;
-    ent.resize((ne + 63) / 64 * 64, make_uint2(0u, 0u));      // whole 64-entry frames (tau 0: never emitted)
+    ent.resize(std::max<uint64_t>(64, (ne + 63) / 64 * 64), make_uint2(0u, 0u));   // whole 64-entry frames (tau 0: never emitted)
     std::vector<KeyRec> krec(nk);
     for (uint64_t k = 0; k < nk; ++k)
     {
@@ -494,14 +494,80 @@ static int build_snapshot(ad_ctx* c)
     uint64_t hcap = 16;
     while (hcap < 2 * nk) hcap <<= 1;
     std::vector<KeySlot> khash(hcap, KeySlot{0, KEY_EMPTY, 0});
+    // emission lists of the fused kernel's newest-probe path (KeyEntry, common.hpp)
+    std::vector<uint32_t> cand_off(NCLASS * nk + 1), cwr_off(nk + 1), cwr_tail(nk), last_w_txn(nk, 0);
+    {
+        std::vector<uint32_t> ccount(NCLASS * nk, 0), wcnt(nk, 0);
+        parallel_for(nk, [&](size_t ka, size_t kb) {
+            for (size_t k = ka; k < kb; ++k)
+                for (uint64_t e = seg32[k]; e < seg32[k + 1]; ++e)
+                {
+                    const uint32_t tau = ent[e].x, kd = ent[e].y >> RANK_BITS;
+                    if (tau == TAU_NEVER_ELIDED)
+                        for (int cl = 0; cl < NCLASS; ++cl) ccount[cl * nk + k] += (CLASS_KINDS[cl] >> kd) & 1;
+                    else if (tau != 0) ++wcnt[k];
+                }
+        });
+        // class-major: all keys' class-0 lists, then class 1, then class 2
+        cand_off[0] = 0;
+        for (uint64_t i = 0; i < NCLASS * nk; ++i) cand_off[i + 1] = cand_off[i] + ccount[i];
+        cwr_off[0] = 0;
+        for (uint64_t k = 0; k < nk; ++k) cwr_off[k + 1] = cwr_off[k] + wcnt[k];
+    }
+    std::vector<uint32_t> cand(std::max<uint32_t>(cand_off[NCLASS * nk], 1)), cwr(std::max<uint32_t>(cwr_off[nk], 1));
+    parallel_for(nk, [&](size_t ka, size_t kb) {
+        std::vector<uint2> tmp;
+        for (size_t k = ka; k < kb; ++k)
+        {
+            uint32_t cur[NCLASS];
+            for (int cl = 0; cl < NCLASS; ++cl) cur[cl] = cand_off[cl * nk + k];
+            tmp.clear();
+            for (uint64_t e = seg32[k]; e < seg32[k + 1]; ++e)
+            {
+                const uint32_t tau = ent[e].x, kd = ent[e].y >> RANK_BITS;
+                if (tau == TAU_NEVER_ELIDED)
+                {
+                    for (int cl = 0; cl < NCLASS; ++cl)
+                        if ((CLASS_KINDS[cl] >> kd) & 1) cand[cur[cl]++] = ent[e].y;
+                }
+                else if (tau != 0)
+                    tmp.push_back(make_uint2(tau, ent[e].y));
+            }
+            std::sort(tmp.begin(), tmp.end(), [](const uint2& a, const uint2& b) { return a.x < b.x; });
+            uint32_t tail = 0;
+            bool has_w = false;
+            for (size_t i = 0; i < tmp.size(); ++i)
+            {
+                cwr[cwr_off[k] + i] = tmp[i].y;
+                if ((tmp[i].y >> RANK_BITS) == AD_KIND_WRITE) { tail = (uint32_t)i; has_w = true; }
+            }
+            cwr_tail[k] = cwr_off[k] + (has_w ? tail : 0);      // no committed Write: M = NONE, all emitted
+            last_w_txn[k] = has_w ? (tmp[tail].y & RANK_MASK) : 0u;
+        }
+    });
+    std::vector<KeyEntry> kent(hcap);
+    for (auto& e : kent) { e = KeyEntry{}; e.idx = KEY_EMPTY; }
     for (uint64_t k = 0; k < nk; ++k)
     {
         uint64_t h = key_hash(K.keys[k]) & (hcap - 1);
         while (khash[h].idx != KEY_EMPTY) h = (h + 1) & (hcap - 1);
         khash[h] = KeySlot{K.keys[k], (uint32_t)k, 0};
+        KeyEntry& ke = kent[h];
+        ke.key = K.keys[k];
+        ke.idx = (uint32_t)k;
+        ke.last_w_txn = last_w_txn[k];
+        ke.rec = krec[k];
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            ke.cand_lo[cl] = cand_off[cl * nk + k];
+            ke.cand_hi[cl] = cand_off[cl * nk + k + 1];
+        }
+        ke.cwr_lo = cwr_off[k];
+        ke.cwr_tail = cwr_tail[k];
+        ke.cwr_hi = cwr_off[k + 1];
     }
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
-        (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_khash, khash)) ||
+        (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_khash, khash)) || (rc = upload(c, c->d_kent, kent)) || (rc = upload(c, c->d_cand, cand)) || (rc = upload(c, c->d_cwr, cwr)) ||
         (rc = upload(c, c->d_ent, ent)) ||
         (rc = upload(c, c->d_w, w)) || (rc = upload(c, c->d_slices_s, c->slice_s)) || (rc = upload(c, c->d_slices_e, c->slice_e)) ||
         (rc = upload(c, c->d_dict_lsb_raw, c->dict_lsb)) || (rc = upload(c, c->d_rt_start, c->rt_start)) ||
@@ -514,10 +580,19 @@ static int build_snapshot(ad_ctx* c)
     s.dict_lo = c->d_dict_lo.as<uint64_t>();
     s.dict_node = c->d_dict_node.as<int32_t>();
     s.n_dict = dhi.size();
+    if (!dhi.empty())
+    {
+        s.dict_last_hi = dhi.back();
+        s.dict_last_lo = dlo.back();
+        s.dict_last_node = dnode.back();
+    }
     s.n_keys = nk;
     s.keys = c->d_keys.as<int64_t>();
     s.krec = c->d_krec.as<KeyRec>();
     s.khash = c->d_khash.as<KeySlot>();
+    s.kent = c->d_kent.as<KeyEntry>();
+    s.cand = c->d_cand.as<uint32_t>();
+    s.cwr = c->d_cwr.as<uint32_t>();
     s.khash_mask = hcap - 1;
     s.n_ent = ne;
     s.ent = c->d_ent.as<uint2>();

@@ -96,6 +96,29 @@ struct KeySlot {
 };
 constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 
+// Fused path: one 128-byte hash slot (= one cache line) per key carries the key's KeyRec and
+// its emission lists: per witness class c the entries that are never elided
+// (`cand`: tau = never-elided, kind in class c, byId order) and the committed Read/Write entries by
+// executeAt (`cwr`, shared by the classes that witness Reads). A probe newer than the whole
+// CommandsForKey (S > last txnId and S > last committed Write's executeAt) emits exactly
+//   cand_c  and  { Ws: the last committed Write | RsOrWs/AnyGloballyVisible: cwr[cwr_tail, cwr_hi) }
+// (minus the request's own id): the mapReduceActive loop (CommandsForKey.java:930-950) with
+// end = byId.length and M = the last committed Write's executeAt.
+// 16-byte quarter q of the slot is loaded by lane q of the probing 8-lane group.
+struct alignas(128) KeyEntry {
+    int64_t key;                   // q0
+    uint32_t idx;                  //    KEY_EMPTY = free slot
+    uint32_t last_w_txn;           //    txn rank of the last committed Write by executeAt (0 = none)
+    KeyRec rec;                    // q1, q2
+    uint32_t cand_lo[NCLASS];      // q3.x..z
+    uint32_t cwr_lo;               // q3.w
+    uint32_t cand_hi[NCLASS];      // q4.x..z
+    uint32_t cwr_tail;             // q4.w  first cwr entry with executeAt >= the last committed Write's
+    uint32_t cwr_hi;               // q5.x
+    uint32_t pad[11];
+};
+static_assert(sizeof(KeyEntry) == 128, "KeyEntry is one cache line");
+
 __host__ __device__ inline uint64_t key_hash(int64_t k)
 {
     uint64_t z = (uint64_t)k + 0x9E3779B97F4A7C15ULL;
@@ -111,11 +134,16 @@ struct DevSnapshot {
     const uint64_t* dict_lo;
     const int32_t*  dict_node;
     uint64_t n_dict;
+    uint64_t dict_last_hi, dict_last_lo;   // the newest dictionary id (request fast path: newer than all)
+    int32_t dict_last_node;
     // CommandsForKey
     uint64_t n_keys;
     const int64_t*  keys;          // [n_keys]
     const KeyRec*   krec;          // [n_keys]
     const KeySlot*  khash;         // [khash_mask + 1]
+    const KeyEntry* kent;          // [khash_mask + 1] same slots, KeyRec + list bounds inline (fused kernel)
+    const uint32_t* cand;          // never-elided entries per key and class: txw (rank | kind << 29)
+    const uint32_t* cwr;           // committed Read/Write entries per key by executeAt: txw
     uint64_t khash_mask;
     uint64_t n_ent;
     const uint2*    ent;           // {tau, txw}

@@ -35,26 +35,32 @@ struct FusedLds {
     int64_t key[FMAXP];
 };
 
-// ascending bitonic sort of one u64 key per lane across the wave (64 lanes), with a payload
-__device__ __forceinline__ void wave_bitonic64(uint64_t& key, uint32_t& pay)
+// ascending bitonic sort of one u64 key per lane over lanes [0, KMAX) (and independently over
+// each further block of KMAX lanes): lanes >= n hold ~0, so sorting only the first 16 or 32 lanes
+// when n fits saves stages
+template <uint32_t KMAX>
+__device__ __forceinline__ void bitonic_lanes(uint64_t& key)
 {
     const uint32_t l = lane_id();
 #pragma unroll
-    for (uint32_t k = 2; k <= 64; k <<= 1)
+    for (uint32_t k = 2; k <= KMAX; k <<= 1)
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1)
         {
             const uint64_t ok = __shfl_xor(key, (int)j, 64);
-            const uint32_t op = __shfl_xor(pay, (int)j, 64);
             const bool up = (l & k) == 0;
             const bool lower = (l & j) == 0;
             const bool take = lower ? (up ? ok < key : ok > key) : (up ? ok > key : ok < key);
-            if (take)
-            {
-                key = ok;
-                pay = op;
-            }
+            if (take) key = ok;
         }
+}
+
+// sort the n (wave-uniform) live keys held in lanes [0, n); the other lanes hold ~0
+__device__ __forceinline__ void wave_bitonic64(uint64_t& key, uint32_t n)
+{
+    if (n <= 16) bitonic_lanes<16>(key);
+    else if (n <= 32) bitonic_lanes<32>(key);
+    else bitonic_lanes<64>(key);
 }
 
 __device__ __forceinline__ void set_error_f(BatchCtl* ctl, unsigned code) { atomicCAS(&ctl->error, 0u, code); }
@@ -187,7 +193,8 @@ __device__ __forceinline__ uint32_t wave_dict_rank(const DevSnapshot& s, uint64_
     const NormTid x = norm_tid(msb, lsb, node);
     auto key = [&](uint64_t i) { return NormTid{s.dict_hi[i], s.dict_lo[i], s.dict_node[i]}; };
     if (s.n_dict == 0) return 0;
-    if (norm_cmp(key(s.n_dict - 1), x) < 0) return (uint32_t)(2 * s.n_dict);   // newer than every id (new txns)
+    const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
+    if (norm_cmp(last, x) < 0) return (uint32_t)(2 * s.n_dict);   // newer than every id (new txns): no load
     const uint64_t lb = wave_lower_bound(0, s.n_dict, key, [&](const NormTid& v) { return norm_cmp(v, x) < 0; });
     bool eq = false;
     if (lb < s.n_dict) eq = norm_cmp(key(lb), x) == 0;
@@ -225,7 +232,7 @@ struct FChunk {
     }
 };
 
-__global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBufs b)
+__global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_resolve(DevSnapshot s, BatchBufs b)
 {
     __shared__ FusedLds lds_all[FWAVES];
     FusedLds& L = lds_all[threadIdx.x >> 6];
@@ -262,44 +269,47 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
         const int64_t epoch = (int64_t)(em >> 15);
         const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
 
-        // ---- per key: slice, CommandsForKey lookup (lane p < np), then broadcast to group p
-        int64_t pkey = 0;
-        uint32_t pki = NO_KEY, pslice = 0;
-        KeyRec pkr{};
-        if (lane < np)
-        {
-            pkey = b.q_keys[k0 + lane];
-            bool in_slice = s.n_slices == 0;
-            for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
-                in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], pkey);
-            pslice = in_slice ? 1u : 0u;
-            if (in_slice && s.n_keys)
-            {
-                uint64_t h = key_hash(pkey) & s.khash_mask;
-                while (true)
-                {
-                    const KeySlot ks = s.khash[h];
-                    if (ks.idx == KEY_EMPTY) break;
-                    if (ks.key == pkey) { pki = ks.idx; break; }
-                    h = (h + 1) & s.khash_mask;
-                }
-                if (pki != NO_KEY) pkr = s.krec[pki];
-            }
-            L.key[lane] = pkey;
-        }
+        // ---- per key g (8-lane group g < np): slice, then the 128-byte KeyEntry of the key's
+        // CommandsForKey (lane j of the group loads quarter j), probing linearly from its hash
         const bool gact = g < np;
-        const int64_t key = __shfl(pkey, g, 64);
-        const uint32_t ki = __shfl(pki, g, 64);
-        const bool in_slice = __shfl(pslice, g, 64) != 0;
+        const uint32_t gb = lane & ~7u;
+        const int64_t key = gact ? b.q_keys[k0 + g] : 0;
+        bool in_slice = s.n_slices == 0;
+        for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
+            in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+        if (gact && j == 0) L.key[g] = key;
+        uint32_t ki = NO_KEY;
+        uint4 kq = make_uint4(0, 0, 0, 0);
+        if (gact && in_slice && s.n_keys)
+        {
+            uint64_t h = key_hash(key) & s.khash_mask;
+            while (true)      // group-uniform
+            {
+                if (j < 6) kq = reinterpret_cast<const uint4*>(s.kent + h)[j];
+                const uint32_t kx = __shfl(kq.x, gb, 64), ky = __shfl(kq.y, gb, 64), kz = __shfl(kq.z, gb, 64);
+                if (kz == KEY_EMPTY) break;
+                if ((int64_t)(((uint64_t)ky << 32) | kx) == key)
+                {
+                    ki = kz;
+                    break;
+                }
+                h = (h + 1) & s.khash_mask;
+            }
+        }
+        if (ki == NO_KEY) kq = make_uint4(0, 0, 0, 0);
         KeyRec kr;
-        kr.seg_lo = __shfl(pkr.seg_lo, g, 64);
-        kr.seg_hi = __shfl(pkr.seg_hi, g, 64);
-        kr.w_lo = __shfl(pkr.w_lo, g, 64);
-        kr.w_hi = __shfl(pkr.w_hi, g, 64);
-        kr.last_txn = __shfl(pkr.last_txn, g, 64);
-        kr.last_wexec = __shfl(pkr.last_wexec, g, 64);
-        kr.pruned = __shfl(pkr.pruned, g, 64);
-        kr.maw = __shfl(pkr.maw, g, 64);
+        kr.seg_lo = __shfl(kq.x, gb + 1, 64);
+        kr.seg_hi = __shfl(kq.y, gb + 1, 64);
+        kr.w_lo = __shfl(kq.z, gb + 1, 64);
+        kr.w_hi = __shfl(kq.w, gb + 1, 64);
+        kr.last_txn = __shfl(kq.x, gb + 2, 64);
+        kr.last_wexec = __shfl(kq.y, gb + 2, 64);
+        kr.pruned = __shfl(kq.z, gb + 2, 64);
+        kr.maw = (int32_t)__shfl(kq.w, gb + 2, 64);
+        const uint32_t last_w_txn = __shfl(kq.w, gb, 64);
+        const uint32_t csel = cls == 0 ? kq.x : (cls == 1 ? kq.y : kq.z);
+        const uint32_t cand_lo = __shfl(csel, gb + 3, 64), cand_hi = __shfl(csel, gb + 4, 64);
+        const uint32_t cwr_tail = __shfl(kq.w, gb + 4, 64), cwr_hi = __shfl(kq.x, gb + 5, 64);
         const bool has_cfk = gact && ki != NO_KEY;
 
         // ---- K1: end = insertPos(S), M = maxCommittedWriteBefore (CommandsForKey.java:912-928)
@@ -332,21 +342,9 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
 
         uint32_t c0 = 0, c1 = 0, nlt = 0;
         bool ovf = false, dup = false;
-        auto node_bits = [&](int lv, uint64_t n0, uint64_t nlo, uint64_t nhi) -> uint32_t {
-            const uint4* p4 = reinterpret_cast<const uint4*>(s.lvl[cls][lv] + n0);
-            const uint4 a = p4[0], c = p4[1];
-            const uint32_t v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-            uint32_t bits = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (n0 + i >= nlo && n0 + i <= nhi && v[i] >= M) bits |= 1u << i;
-            return bits;
-        };
-        auto leaf = [&](uint64_t n0) {
-            const uint4* p4 = reinterpret_cast<const uint4*>(s.ent + n0);
-            uint4 q[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) q[i] = p4[i];
+        // emission of 8 consecutive byId entries n0..n0+7 held in q (mapReduceActive loop body,
+        // CommandsForKey.java:930-950): group-collective, staged in entry order into LDS
+        auto stage8 = [&](uint64_t n0, const uint4 (&q)[4], bool on) {
             uint32_t w0 = 0, w1 = 0, lt = 0, eq = 0;
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -355,7 +353,7 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
                 const uint32_t txw = (i & 1) ? q[i >> 1].w : q[i >> 1].y;
                 const uint64_t e = n0 + i;
                 const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
-                const bool want = e >= lo && e < end_g && tau >= M && ((kinds >> kd) & 1) && r != self;
+                const bool want = on && e >= lo && e < end_g && tau >= M && ((kinds >> kd) & 1) && r != self;
                 const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;   // !managesExecution -> directKeyDeps
                 w0 |= (want && !is1) ? (1u << i) : 0u;
                 w1 |= (want && is1) ? (1u << i) : 0u;
@@ -385,7 +383,59 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
                 dup = dup || grp_sum(eq) != 0;
             }
         };
-        grp_descent(has_cfk, lo, end_g, s.n_levels, node_bits, leaf, L.stk[g]);
+        auto node_bits = [&](int lv, uint64_t n0, uint64_t nlo, uint64_t nhi) -> uint32_t {
+            const uint4* p4 = reinterpret_cast<const uint4*>(s.lvl[cls][lv] + n0);
+            const uint4 a = p4[0], c = p4[1];
+            const uint32_t v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+            uint32_t bits = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (n0 + i >= nlo && n0 + i <= nhi && v[i] >= M) bits |= 1u << i;
+            return bits;
+        };
+        auto leaf = [&](uint64_t n0) {
+            const uint4* p4 = reinterpret_cast<const uint4*>(s.ent + n0);
+            uint4 q[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = p4[i];
+            stage8(n0, q, true);
+        };
+
+        // Newest probe (S above every txnId and every committed Write's executeAt of the key, elision
+        // on): the emissions are exactly two precomputed contiguous lists (KeyEntry, common.hpp);
+        // otherwise the class max tree prunes byId[lo, end) (output-sensitive descent).
+        const bool newest = has_cfk && s.elide && tail && wtail;
+        if (ballot(newest))
+        {
+            const uint32_t n1 = newest ? cand_hi - cand_lo : 0u;
+            const uint32_t n2 = !newest ? 0u : (cls == 0 ? (last_w_txn != 0 ? 1u : 0u) : cwr_hi - cwr_tail);
+            const uint32_t nn = n1 + n2;
+            for (uint32_t o = 0; ballot(o < nn); o += 8)
+            {
+                const uint32_t i = o + j;
+                bool want = i < nn;
+                uint32_t txw = 0;
+                if (want)
+                    txw = i < n1 ? s.cand[cand_lo + i]
+                                 : (cls == 0 ? (last_w_txn | (1u << RANK_BITS)) : s.cwr[cwr_tail + (i - n1)]);
+                const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
+                want = want && r != self;
+                const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;   // !managesExecution -> directKeyDeps
+                const uint32_t w0 = (want && !is1) ? 1u : 0u, w1 = (want && is1) ? 1u : 0u;
+                const uint32_t i0 = grp_incl_scan(w0), i1 = grp_incl_scan(w1);
+                const uint32_t t0 = __shfl(i0, gb | 7u, 64), t1 = __shfl(i1, gb | 7u, 64);
+                if (c0 + t0 <= FCAP0 && c1 + t1 <= FCAP1)
+                {
+                    if (w0) L.st0[g][c0 + i0 - 1] = r;
+                    if (w1) L.st1[g][c1 + i1 - 1] = r;
+                }
+                else ovf = true;
+                c0 += t0;
+                c1 += t1;
+            }
+        }
+        const bool treep = has_cfk && !newest;
+        if (ballot(treep)) grp_descent(treep, lo, end_g, s.n_levels, node_bits, leaf, L.stk[g]);
 
         // ---- K4: range commands containing the key + the redundant-before entry
         uint32_t rc = 0;
@@ -524,14 +574,24 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
             }
             const bool live = lane < tot;
             const uint32_t x = live ? (c == 0 ? L.st0[a][lane - a_start] : L.st1[a][lane - a_start]) : 0xFFFFFFFFu;
-            // sort (rank, element) ascending; dedup ranks -> values, body = unique rank of each element
-            uint64_t key = live ? (((uint64_t)x << 8) | lane) : ~0ull;
-            uint32_t pay = 0;
-            wave_bitonic64(key, pay);
-            const uint32_t xr = (uint32_t)(key >> 8);
+            // sort (rank, key, element) ascending; dedup ranks -> values; a key's body lists the
+            // unique-rank index of each of its values in ascending order (staging order is free)
+            uint64_t key = live ? (((uint64_t)x << 9) | (a << 6) | lane) : ~0ull;
+            wave_bitonic64(key, tot);
+            const uint32_t xr = (uint32_t)(key >> 9);
             const uint64_t prevk = __shfl_up(key, 1, 64);
             const bool valid = key != ~0ull;
-            const bool uniq = valid && (lane == 0 || (uint32_t)(prevk >> 8) != xr);
+            const bool uniq = valid && (lane == 0 || (uint32_t)(prevk >> 9) != xr);
+            const uint32_t ka = (uint32_t)(key >> 6) & 7u;
+            uint64_t same_key = ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 3; ++bit)
+            {
+                const uint64_t bb = ballot((ka >> bit) & 1u);
+                same_key &= ((ka >> bit) & 1u) ? bb : ~bb;
+            }
+            const uint32_t kstart = __shfl(start_l, ka, 64);
+            const uint32_t kpos = kstart + __popcll(same_key & ((1ull << lane) - 1));
             const uint64_t um = ballot(uniq);
             const uint32_t U = __popcll(um);
             const uint32_t ur = __popcll(um & ((2ull << lane) - 1)) - 1;     // rank among distinct values
@@ -559,7 +619,7 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
                     ok2t[kk] = (int32_t)(nk + start_l + cnt_l);      // absolute end offset (RelationMultiMap.java:245-257)
                 }
                 if (uniq) otx[ur] = (xr - 1) >> 1;
-                if (valid) ok2t[nk + (uint32_t)(key & 0xFF)] = (int32_t)ur;
+                if (valid) ok2t[nk + kpos] = (int32_t)ur;
             }
         }
 
@@ -582,8 +642,7 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
             const uint64_t pr = live ? ((a & 1) ? L.rs[a >> 1][FCAPR] : L.rs[a >> 1][lane - a_start]) : ~0ull;
             // unique (range, txnId) pairs in (Range.compare, TxnId.compareTo) order
             uint64_t key = pr;
-            uint32_t pay = 0;
-            wave_bitonic64(key, pay);
+            wave_bitonic64(key, totR);
             const uint64_t prevk = __shfl_up(key, 1, 64);
             const bool valid = key != ~0ull;
             const bool uniq = valid && (lane == 0 || prevk != key);
@@ -612,8 +671,7 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
             // group end offsets: the next group's first index (or UPn)
             // distinct txnIds: sort (rank, pair position)
             uint64_t k2 = uplive ? (((uint64_t)rk << 8) | lane) : ~0ull;
-            uint32_t pay2 = 0;
-            wave_bitonic64(k2, pay2);
+            wave_bitonic64(k2, UPn);
             const uint64_t prev2 = __shfl_up(k2, 1, 64);
             const bool v2 = k2 != ~0ull;
             const bool uq2 = v2 && (lane == 0 || (uint32_t)(prev2 >> 8) != (uint32_t)(k2 >> 8));
@@ -654,8 +712,17 @@ __global__ __launch_bounds__(64 * FWAVES) void k_resolve(DevSnapshot s, BatchBuf
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
+    // one resident generation of waves (grid-stride over requests): blocks per CU from the
+    // occupancy query (4 waves/SIMD at <= 128 VGPRs), never more than the requests need
+    static int per_cu = 0;
+    if (!per_cu)
+    {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve, 64 * FWAVES, 0) != hipSuccess || nb <= 0) nb = 2;
+        per_cu = std::min(nb, 8);
+    }
     const uint64_t need = (b.n_txns + FWAVES - 1) / FWAVES;
-    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)device_cu_count() * 8);
+    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu);
     k_resolve<<<grid, 64 * FWAVES, 0, st>>>(s, b);
     return hipGetLastError();
 }
