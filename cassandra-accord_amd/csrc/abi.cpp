@@ -196,10 +196,11 @@ struct ad_ctx {
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
     DevBuf arena, rarena;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, p_slot;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
+    hipEvent_t ev_slot = nullptr;      // fused path: after k_probe_slots
     // multi-GPU export / merge buffers
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
@@ -801,8 +802,11 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     b.q_min_epoch = q->min_epoch; b.q_key_off = q->key_off; b.q_keys = q->keys;
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
-        !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n))
+        !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
+        !ens<uint32_t>(c->p_slot, np))
         return c->fail(AD_E_NOMEM, "batch buffers");
+    b.p_slot = c->p_slot.as<uint32_t>();
+    if (const char* e = getenv("AD_DBG")) b.dbg = (uint32_t)atoi(e);
     b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>(); b.bsum = c->bsum.as<uint64_t>();
     b.t_reg = c->t_reg.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>(); b.deferred = c->deferred.as<uint32_t>();
     if (split_only && !bind_split(c->split, b, n, np, false)) return c->fail(AD_E_NOMEM, "split buffers");
@@ -845,6 +849,9 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         }
         else
         {
+            if (!c->ev_slot) HIPCHK(c, hipEventCreate(&c->ev_slot));
+            HIPCHK(c, run_probe_slots(c->ds, b, st));
+            HIPCHK(c, hipEventRecord(c->ev_slot, st));
             HIPCHK(c, run_resolve(c->ds, b, st));
             HIPCHK(c, hipEventRecord(c->ev[1], st));
             HIPCHK(c, hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -936,6 +943,13 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             HIPCHK(c, hipEventElapsedTime(&ms, c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
             S.ms_stage[pairs[i][2]] = ms;
             total += ms;
+        }
+        if (!split_only)
+        {
+            // stage 2: k_probe_slots; stage 0: k_resolve alone
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev_slot));
+            S.ms_stage[2] = ms;
+            S.ms_stage[0] -= ms;
         }
         S.ms_device = total;
         S.ms_ingest = c->ms_ingest;
@@ -1033,6 +1047,7 @@ void ad_ctx_destroy(ad_ctx* c)
     (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_slot) (void)hipEventDestroy(c->ev_slot);
     if (c->lv) levels_work_destroy(c->lv);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

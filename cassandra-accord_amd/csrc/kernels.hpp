@@ -34,6 +34,7 @@ struct BatchBufs {
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
     uint32_t* p_txn; uint4* p_rec;
+    uint32_t* p_slot;                // fused path: KeyEntry slot of each probe | in-slice << 31 (k_probe_slots)
     // K1
     uint32_t* arena; uint32_t* p_off; uint32_t* p_c0; uint32_t* p_c1;
     // K4
@@ -48,6 +49,7 @@ struct BatchBufs {
     uint32_t* deferred;              // [n_txns] requests deferred by k_resolve
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
     BatchCtl* ctl;
+    uint32_t dbg;                    // timing experiments only (AD_DBG): 0 = normal
 };
 
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
@@ -62,6 +64,9 @@ hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_
 hipError_t run_pack(const BatchBufs& b, hipStream_t st);
 
 // fused per-request path (resolve.hip)
+constexpr uint32_t SLOT_NONE = 0x7FFFFFFFu;    // p_slot: key has no CommandsForKey in this store
+constexpr uint32_t SLOT_IN_SLICE = 0x80000000u;
+hipError_t run_probe_slots(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,

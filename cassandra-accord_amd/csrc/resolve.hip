@@ -55,6 +55,29 @@ __device__ __forceinline__ void bitonic_lanes(uint64_t& key)
         }
 }
 
+template <uint32_t KMAX>
+__device__ __forceinline__ void bitonic_lanes32(uint32_t& key)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (uint32_t k = 2; k <= KMAX; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1)
+        {
+            const uint32_t ok = __shfl_xor(key, (int)j, 64);
+            const bool up = (l & k) == 0;
+            const bool lower = (l & j) == 0;
+            key = (lower == up) ? min(key, ok) : max(key, ok);
+        }
+}
+
+__device__ __forceinline__ void wave_bitonic32(uint32_t& key, uint32_t n)
+{
+    if (n <= 16) bitonic_lanes32<16>(key);
+    else if (n <= 32) bitonic_lanes32<32>(key);
+    else bitonic_lanes32<64>(key);
+}
+
 // sort the n (wave-uniform) live keys held in lanes [0, n); the other lanes hold ~0
 __device__ __forceinline__ void wave_bitonic64(uint64_t& key, uint32_t n)
 {
@@ -241,26 +264,79 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     const uint64_t nw = (uint64_t)gridDim.x * FWAVES;
     FChunk ralloc;
     const bool incl = s.start_inclusive != 0;
+    const uint64_t reg_cap = uniform64(b.ctl->reg_cap);     // set by the host before the launch
 
-    for (uint64_t t = (uint64_t)blockIdx.x * FWAVES + (threadIdx.x >> 6); t < n; t += nw)
+    // Software pipeline over this wave's requests t0, t0 + nw, ...: key offsets two requests
+    // ahead, ids / keys / slots one ahead (issued at the top of an iteration), the KeyEntry quarters
+    // one ahead (issued once the current request's lists are staged), so a request's dependent
+    // chain key_off -> slot -> KeyEntry -> lists is mostly hidden behind the previous request.
+    auto st1 = [&](uint64_t tt, uint64_t& k0o, uint32_t& npo) {
+        if (tt < n)
+        {
+            k0o = b.q_key_off[tt];
+            npo = (uint32_t)(b.q_key_off[tt + 1] - k0o);
+        }
+        else { k0o = 0; npo = 0; }
+    };
+    struct Ids { uint64_t tm, tl, em, el; int32_t tn, en; };
+    auto ids = [&](uint64_t tt) -> Ids {
+        Ids r{0, 0, 0, 0, 0, 0};
+        if (tt < n)
+        {
+            r.tm = b.q_txn_msb[tt]; r.tl = b.q_txn_lsb[tt]; r.tn = b.q_txn_node[tt];
+            r.em = b.q_exec_msb[tt]; r.el = b.q_exec_lsb[tt]; r.en = b.q_exec_node[tt];
+        }
+        return r;
+    };
+    auto st2 = [&](uint64_t k0i, uint32_t npi, int64_t& keyo, uint32_t& pso) {
+        const bool a = g < npi && npi <= FMAXP;
+        keyo = a ? b.q_keys[k0i + g] : 0;
+        pso = a ? b.p_slot[k0i + g] : SLOT_NONE;
+    };
+    auto st3 = [&](uint32_t psi, uint4& kqo) {
+        const uint32_t sl = psi & ~SLOT_IN_SLICE;
+        kqo = (sl != SLOT_NONE && j < 6) ? reinterpret_cast<const uint4*>(s.kent + sl)[j] : make_uint4(0, 0, 0, 0);
+    };
+    const uint64_t t0 = uniform64((uint64_t)blockIdx.x * FWAVES + (threadIdx.x >> 6));
+    uint64_t k0c, k0n;
+    uint32_t npc, npn;
+    st1(t0, k0c, npc);
+    st1(t0 + nw, k0n, npn);
+    Ids idc = ids(t0);
+    int64_t keyc;
+    uint32_t psc;
+    st2(k0c, npc, keyc, psc);
+    uint4 kqc;
+    st3(psc, kqc);
+    for (uint64_t t = t0; t < n; t += nw)
     {
-        const uint64_t k0 = b.q_key_off[t];
-        const uint32_t np = (uint32_t)(b.q_key_off[t + 1] - k0);
+        uint64_t k0nn;
+        uint32_t npnn;
+        st1(t + 2 * nw, k0nn, npnn);
+        const Ids idn = ids(t + nw);
+        int64_t keyn;
+        uint32_t psn;
+        st2(k0n, npn, keyn, psn);
+        uint4 kqn = make_uint4(0, 0, 0, 0);
+        bool pf3 = false;
+        do {
+        const uint64_t k0 = k0c;
+        const uint32_t np = npc;
         if (np > FMAXP)
         {
             if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
-            continue;
+            break;   // next request (pipeline rotation below)
         }
         // ---- encode the request (PreAccept.java:251-261)
-        const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t];
-        const int32_t tn = b.q_txn_node[t];
-        const uint64_t em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
-        const int32_t en = b.q_exec_node[t];
+        const uint64_t tm = idc.tm, tl = idc.tl;
+        const int32_t tn = idc.tn;
+        const uint64_t em = idc.em, el = idc.el;
+        const int32_t en = idc.en;
         const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
         if (kinds == 0)
         {
             if (lane == 0) set_error_f(b.ctl, ERR_INVAL);
-            continue;
+            break;   // next request (pipeline rotation below)
         }
         const int cls = kinds_class(kinds);
         const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
@@ -269,33 +345,17 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         const int64_t epoch = (int64_t)(em >> 15);
         const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
 
-        // ---- per key g (8-lane group g < np): slice, then the 128-byte KeyEntry of the key's
-        // CommandsForKey (lane j of the group loads quarter j), probing linearly from its hash
+        // ---- per key g (8-lane group g < np): the 128-byte KeyEntry of the key's CommandsForKey,
+        // found by k_probe_slots (lane j of the group loads quarter j)
         const bool gact = g < np;
         const uint32_t gb = lane & ~7u;
-        const int64_t key = gact ? b.q_keys[k0 + g] : 0;
-        bool in_slice = s.n_slices == 0;
-        for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
-            in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+        const int64_t key = keyc;
+        const uint32_t pslot = psc;
+        const bool in_slice = (pslot & SLOT_IN_SLICE) != 0;
+        const uint32_t slot = pslot & ~SLOT_IN_SLICE;
         if (gact && j == 0) L.key[g] = key;
-        uint32_t ki = NO_KEY;
-        uint4 kq = make_uint4(0, 0, 0, 0);
-        if (gact && in_slice && s.n_keys)
-        {
-            uint64_t h = key_hash(key) & s.khash_mask;
-            while (true)      // group-uniform
-            {
-                if (j < 6) kq = reinterpret_cast<const uint4*>(s.kent + h)[j];
-                const uint32_t kx = __shfl(kq.x, gb, 64), ky = __shfl(kq.y, gb, 64), kz = __shfl(kq.z, gb, 64);
-                if (kz == KEY_EMPTY) break;
-                if ((int64_t)(((uint64_t)ky << 32) | kx) == key)
-                {
-                    ki = kz;
-                    break;
-                }
-                h = (h + 1) & s.khash_mask;
-            }
-        }
+        uint4 kq = kqc;
+        const uint32_t ki = slot != SLOT_NONE ? __shfl(kq.z, gb, 64) : NO_KEY;
         if (ki == NO_KEY) kq = make_uint4(0, 0, 0, 0);
         KeyRec kr;
         kr.seg_lo = __shfl(kq.x, gb + 1, 64);
@@ -405,7 +465,8 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         // on): the emissions are exactly two precomputed contiguous lists (KeyEntry, common.hpp);
         // otherwise the class max tree prunes byId[lo, end) (output-sensitive descent).
         const bool newest = has_cfk && s.elide && tail && wtail;
-        if (ballot(newest))
+        if (b.dbg == 3) break;
+        if (ballot(newest) && b.dbg != 2)
         {
             const uint32_t n1 = newest ? cand_hi - cand_lo : 0u;
             const uint32_t n2 = !newest ? 0u : (cls == 0 ? (last_w_txn != 0 ? 1u : 0u) : cwr_hi - cwr_tail);
@@ -496,11 +557,16 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         }
         if (gact && j == 0) L.rs[g][FCAPR] = rbv;
 
+        // lists staged: the next request's KeyEntry loads go out now, behind this one's build
+        st3(psn, kqn);
+        pf3 = true;
+
+        if (b.dbg == 1) break;
         // any key overflowing its staging -> defer the whole request to the split kernels
         if (ballot(ovf))
         {
             if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
-            continue;
+            break;   // next request (pipeline rotation below)
         }
         const bool has_extra = extra != 0 && !dup;
         // insert the prunedBefore substitute at its sorted position (class 0 list)
@@ -532,7 +598,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
             if (ballot(ovf))
             {
                 if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
-                continue;
+                break;   // next request (pipeline rotation below)
             }
         }
         const uint32_t cnt0 = c0 + (has_extra ? 1u : 0u);
@@ -549,7 +615,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         if (tot0 > 64 || tot1 > 64 || totR > 64)
         {
             if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
-            continue;
+            break;   // next request (pipeline rotation below)
         }
         wave_lds_sync();
         // keyDeps (class 0) and directKeyDeps (class 1): lists = keys in request order
@@ -573,16 +639,17 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
                 if (lane >= sp) { a = pp; a_start = sp; }
             }
             const bool live = lane < tot;
-            const uint32_t x = live ? (c == 0 ? L.st0[a][lane - a_start] : L.st1[a][lane - a_start]) : 0xFFFFFFFFu;
-            // sort (rank, key, element) ascending; dedup ranks -> values; a key's body lists the
-            // unique-rank index of each of its values in ascending order (staging order is free)
-            uint64_t key = live ? (((uint64_t)x << 9) | (a << 6) | lane) : ~0ull;
-            wave_bitonic64(key, tot);
-            const uint32_t xr = (uint32_t)(key >> 9);
-            const uint64_t prevk = __shfl_up(key, 1, 64);
-            const bool valid = key != ~0ull;
-            const bool uniq = valid && (lane == 0 || (uint32_t)(prevk >> 9) != xr);
-            const uint32_t ka = (uint32_t)(key >> 6) & 7u;
+            const uint32_t x = live ? (c == 0 ? L.st0[a][lane - a_start] : L.st1[a][lane - a_start]) : 0u;
+            // sort (rank, key) ascending -- rank < 2^29, key < 8: one u32; dedup ranks -> values; a
+            // key's body lists the unique-rank index of each of its values in ascending order
+            // (staging order is free)
+            uint32_t key = live ? ((x << 3) | a) : 0xFFFFFFFFu;
+            wave_bitonic32(key, tot);
+            const uint32_t xr = key >> 3;
+            const uint32_t prevk = __shfl_up(key, 1, 64);
+            const bool valid = live;                     // the tot live keys end in lanes [0, tot)
+            const bool uniq = valid && (lane == 0 || (prevk >> 3) != xr);
+            const uint32_t ka = key & 7u;
             uint64_t same_key = ballot(valid);
 #pragma unroll
             for (int bit = 0; bit < 3; ++bit)
@@ -599,7 +666,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t nk = __popcll(nem);
             const uint64_t bytes = fregion_bytes(nk, U, tot);
             const uint64_t ro = ralloc.take(b.ctl, bytes);
-            const bool fits = ro + bytes <= b.ctl->reg_cap;
+            const bool fits = ro + bytes <= reg_cap;
             if (lane == 0)
             {
                 b.sz[(3 * m) * n + t] = fits ? nk : 0;
@@ -626,7 +693,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         if (totR == 0)
         {
             if (lane == 0) { b.sz[3 * n + t] = 0; b.sz[4 * n + t] = 0; b.sz[5 * n + t] = 0; }
-            continue;
+            break;   // next request (pipeline rotation below)
         }
         {
             // rangeDeps: element e = lane: per key [command pairs] then [redundant pair]
@@ -680,7 +747,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
             const uint32_t ur2 = __popcll(um2 & ((2ull << lane) - 1)) - 1;
             const uint64_t bytes = fregion_bytes(nR, UR, UPn);
             const uint64_t ro = ralloc.take(b.ctl, bytes);
-            const bool fits = ro + bytes <= b.ctl->reg_cap;
+            const bool fits = ro + bytes <= reg_cap;
             if (lane == 0)
             {
                 b.sz[3 * n + t] = fits ? nR : 0;
@@ -706,7 +773,50 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
                 if (v2) ok2t[nR + (uint32_t)(k2 & 0xFF)] = (int32_t)ur2;
             }
         }
+        } while (false);
+        if (!pf3) st3(psn, kqn);
+        k0c = k0n; npc = npn;
+        k0n = k0nn; npn = npnn;
+        idc = idn;
+        keyc = keyn; psc = psn;
+        kqc = kqn;
     }
+}
+
+// key -> KeyEntry slot, one thread per probe (open addressing, linear probing): keeps the
+// dependent hash probing out of the per-request kernel (InMemoryCommandStore.mapReduceForKey's
+// slice test :280 and the CommandsForKey lookup)
+__global__ __launch_bounds__(256) void k_probe_slots(DevSnapshot s, BatchBufs b)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= b.n_probes) return;
+    const int64_t key = b.q_keys[p];
+    bool in_slice = s.n_slices == 0;
+    for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
+        in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+    uint32_t slot = SLOT_NONE;
+    if (in_slice && s.n_keys)
+    {
+        uint64_t h = key_hash(key) & s.khash_mask;
+        while (true)
+        {
+            const uint4 q = reinterpret_cast<const uint4*>(s.kent + h)[0];
+            if (q.z == KEY_EMPTY) break;
+            if ((int64_t)(((uint64_t)q.y << 32) | q.x) == key)
+            {
+                slot = (uint32_t)h;
+                break;
+            }
+            h = (h + 1) & s.khash_mask;
+        }
+    }
+    b.p_slot[p] = slot | (in_slice ? SLOT_IN_SLICE : 0u);
+}
+
+hipError_t run_probe_slots(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+{
+    if (b.n_probes) k_probe_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b);
+    return hipGetLastError();
 }
 
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
