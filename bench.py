@@ -31,8 +31,9 @@ from accord_deps import exchange, native, synth  # noqa: E402
 
 METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-STAGES = ["fused resolve (K0+K1+K4+K2)", "deferred requests (split K0..K2)", "-", "-", "offsets scan", "pack"]
-KERNEL_OF_STAGE = ["k_resolve", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "-", "-",
+STAGES = ["lean fused resolve (K1+K2, newest requests)", "deferred requests (split K0..K2)", "key -> KeyEntry slots",
+          "general fused resolve (lean deferrals)", "offsets scan", "pack"]
+KERNEL_OF_STAGE = ["k_resolve_lean", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_probe_slots", "k_resolve",
                    "k_scan_blocks+sums+add", "k_pack"]
 
 
@@ -77,6 +78,7 @@ def stage_bytes(w, stats):
     b = [0] * 6
     b[0] = len(q) * (40 + 8) + 8 * q.n_probes + int((17 * lk + 16).sum()) + 16 * int(w.cmds.range_off[-1]) + \
         out_bytes + len(q) * (9 * 4 + 3 * 8)
+    b[2] = 8 * q.n_probes + 128 * q.n_probes + 4 * q.n_probes     # keys, one slot line, slot index
     b[4] = 9 * (4 + 8) * len(q)
     b[5] = 2 * out_bytes + len(q) * (9 * (4 + 8) + 3 * 8)
     return b

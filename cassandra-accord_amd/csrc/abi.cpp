@@ -196,11 +196,12 @@ struct ad_ctx {
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
     DevBuf arena, rarena;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, p_slot;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, p_slot;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t ev_slot = nullptr;      // fused path: after k_probe_slots
+    hipEvent_t ev_lean = nullptr;      // fused path: after k_resolve_lean
     // multi-GPU export / merge buffers
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
@@ -557,13 +558,14 @@ static int build_snapshot(ad_ctx* c)
         ke.key = K.keys[k];
         ke.idx = (uint32_t)k;
         ke.last_w_txn = last_w_txn[k];
+        ke.last_txn = krec[k].last_txn;
+        ke.last_wexec = krec[k].last_wexec;
         ke.rec = krec[k];
         for (int cl = 0; cl < NCLASS; ++cl)
         {
             ke.cand_lo[cl] = cand_off[cl * nk + k];
             ke.cand_hi[cl] = cand_off[cl * nk + k + 1];
         }
-        ke.cwr_lo = cwr_off[k];
         ke.cwr_tail = cwr_tail[k];
         ke.cwr_hi = cwr_off[k + 1];
     }
@@ -794,6 +796,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipStreamSynchronize(st));
     }
     const bool split_only = c->cfg.path == 1;
+    // the lean kernel covers stores without range commands / redundant-before entries, elision on
+    const bool lean = !split_only && c->ds.n_rent == 0 && c->ds.n_rb == 0 && c->ds.elide && getenv("AD_NO_LEAN") == nullptr;
     BatchBufs b{};
     b.n_txns = n;
     b.n_probes = np;
@@ -803,9 +807,10 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
         !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
-        !ens<uint32_t>(c->p_slot, np))
+        !ens<uint32_t>(c->p_slot, np) || !ens<uint32_t>(c->deferred1, n))
         return c->fail(AD_E_NOMEM, "batch buffers");
     b.p_slot = c->p_slot.as<uint32_t>();
+    b.deferred1 = c->deferred1.as<uint32_t>();
     if (const char* e = getenv("AD_DBG")) b.dbg = (uint32_t)atoi(e);
     b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>(); b.bsum = c->bsum.as<uint64_t>();
     b.t_reg = c->t_reg.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>(); b.deferred = c->deferred.as<uint32_t>();
@@ -850,9 +855,22 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         else
         {
             if (!c->ev_slot) HIPCHK(c, hipEventCreate(&c->ev_slot));
+            if (!c->ev_lean) HIPCHK(c, hipEventCreate(&c->ev_lean));
             HIPCHK(c, run_probe_slots(c->ds, b, st));
             HIPCHK(c, hipEventRecord(c->ev_slot, st));
-            HIPCHK(c, run_resolve(c->ds, b, st));
+            if (lean)
+            {
+                // lean kernel first (newest requests, 2 per wave); the general fused kernel then
+                // takes only what it deferred (count read on the device, no host round trip)
+                HIPCHK(c, run_resolve_lean(c->ds, b, st));
+                HIPCHK(c, hipEventRecord(c->ev_lean, st));
+                BatchBufs b2 = b;
+                b2.req_list = b.deferred1;
+                b2.req_count = &b.ctl->n_deferred1;
+                HIPCHK(c, run_resolve(c->ds, b2, st));
+            }
+            else
+                HIPCHK(c, run_resolve(c->ds, b, st));
             HIPCHK(c, hipEventRecord(c->ev[1], st));
             HIPCHK(c, hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
             HIPCHK(c, hipStreamSynchronize(st));
@@ -929,6 +947,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         S.n_txns = n;
         S.n_probes = np;
         S.n_deferred = nd;
+        S.n_deferred_lean = lean ? h.n_deferred1 : 0;
         for (int m = 0; m < 3; ++m)
         {
             S.n_pairs[m] = tot[3 * m + 2] - tot[3 * m + 0];
@@ -946,10 +965,18 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         }
         if (!split_only)
         {
-            // stage 2: k_probe_slots; stage 0: k_resolve alone
+            // stage 2: k_probe_slots; stage 0: k_resolve_lean (or k_resolve when not lean);
+            // stage 3: k_resolve over the lean kernel's deferrals
             HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev_slot));
             S.ms_stage[2] = ms;
             S.ms_stage[0] -= ms;
+            if (lean)
+            {
+                float ml = 0;
+                HIPCHK(c, hipEventElapsedTime(&ml, c->ev_slot, c->ev_lean));
+                S.ms_stage[3] = S.ms_stage[0] - ml;
+                S.ms_stage[0] = ml;
+            }
         }
         S.ms_device = total;
         S.ms_ingest = c->ms_ingest;
@@ -1048,6 +1075,7 @@ void ad_ctx_destroy(ad_ctx* c)
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_slot) (void)hipEventDestroy(c->ev_slot);
+    if (c->ev_lean) (void)hipEventDestroy(c->ev_lean);
     if (c->lv) levels_work_destroy(c->lv);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -104,18 +104,22 @@ constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 //   cand_c  and  { Ws: the last committed Write | RsOrWs/AnyGloballyVisible: cwr[cwr_tail, cwr_hi) }
 // (minus the request's own id): the mapReduceActive loop (CommandsForKey.java:930-950) with
 // end = byId.length and M = the last committed Write's executeAt.
-// 16-byte quarter q of the slot is loaded by lane q of the probing 8-lane group.
+// The newest-probe fields fill the first 64 bytes (quarters q0..q3, all the lean kernel reads);
+// the KeyRec of the tree path is q4, q5.
 struct alignas(128) KeyEntry {
-    int64_t key;                   // q0
-    uint32_t idx;                  //    KEY_EMPTY = free slot
-    uint32_t last_w_txn;           //    txn rank of the last committed Write by executeAt (0 = none)
-    KeyRec rec;                    // q1, q2
-    uint32_t cand_lo[NCLASS];      // q3.x..z
-    uint32_t cwr_lo;               // q3.w
-    uint32_t cand_hi[NCLASS];      // q4.x..z
-    uint32_t cwr_tail;             // q4.w  first cwr entry with executeAt >= the last committed Write's
-    uint32_t cwr_hi;               // q5.x
-    uint32_t pad[11];
+    int64_t key;                   // q0.xy
+    uint32_t idx;                  // q0.z   KEY_EMPTY = free slot
+    uint32_t last_w_txn;           // q0.w   txn rank of the last committed Write by executeAt (0 = none)
+    uint32_t last_txn;             // q1.x   rank of byId's last txnId (0 if empty)
+    uint32_t last_wexec;           // q1.y   executeAt rank of the last committed Write (0 if none)
+    uint32_t cwr_tail;             // q1.z   first cwr entry with executeAt >= the last committed Write's
+    uint32_t cwr_hi;               // q1.w
+    uint32_t cand_lo[NCLASS];      // q2.xyz
+    uint32_t pad0;
+    uint32_t cand_hi[NCLASS];      // q3.xyz
+    uint32_t pad1;
+    KeyRec rec;                    // q4, q5
+    uint32_t pad[8];
 };
 static_assert(sizeof(KeyEntry) == 128, "KeyEntry is one cache line");
 

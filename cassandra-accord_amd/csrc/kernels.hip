@@ -916,33 +916,37 @@ hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // ---------------------------------------------------------------------------------------
 // pack: per-request regions -> contiguous per-map arrays at the scanned offsets
 // ---------------------------------------------------------------------------------------
+// regions -> packed per-map arrays; 8 lanes per request (outputs are tens of elements, so a
+// wave keeps 8 requests' dependent loads in flight)
+constexpr uint32_t PACK_LANES = 8;
 __global__ __launch_bounds__(256) void k_pack(BatchBufs b)
 {
     const uint64_t n = b.n_txns;
-    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t t = (uint64_t)blockIdx.x * (256 / PACK_LANES) + (threadIdx.x / PACK_LANES);
     if (t >= n) return;
-    const uint32_t lane = lane_id();
+    const uint32_t j = threadIdx.x % PACK_LANES;
 #pragma unroll
     for (int m = 0; m < 3; ++m)
     {
-        const uint32_t nk = b.sz[(3 * m) * n + t], U = b.sz[(3 * m + 1) * n + t], no = b.sz[(3 * m + 2) * n + t];
+        const uint32_t no = b.sz[(3 * m + 2) * n + t];
         if (no == 0) continue;
+        const uint32_t nk = b.sz[(3 * m) * n + t], U = b.sz[(3 * m + 1) * n + t];
         const uint8_t* base = b.reg + b.t_reg[(uint64_t)m * n + t];
         const int64_t* ikeys = reinterpret_cast<const int64_t*>(base);
         const uint32_t* itx = reinterpret_cast<const uint32_t*>(ikeys + nk);
         const int32_t* ik2t = reinterpret_cast<const int32_t*>(itx + U);
         const uint64_t ko = b.off[(3 * m) * (n + 1) + t], vo = b.off[(3 * m + 1) * (n + 1) + t],
                        oo = b.off[(3 * m + 2) * (n + 1) + t];
-        for (uint32_t i = lane; i < nk; i += 64) b.o_keys[m][ko + i] = ikeys[i];
-        for (uint32_t i = lane; i < U; i += 64) b.o_txns[m][vo + i] = itx[i];
-        for (uint32_t i = lane; i < no; i += 64) b.o_k2t[m][oo + i] = ik2t[i];
+        for (uint32_t i = j; i < nk; i += PACK_LANES) b.o_keys[m][ko + i] = ikeys[i];
+        for (uint32_t i = j; i < U; i += PACK_LANES) b.o_txns[m][vo + i] = itx[i];
+        for (uint32_t i = j; i < no; i += PACK_LANES) b.o_k2t[m][oo + i] = ik2t[i];
     }
 }
 
 hipError_t run_pack(const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
-    k_pack<<<(unsigned)((b.n_txns + 3) / 4), 256, 0, st>>>(b);
+    k_pack<<<(unsigned)((b.n_txns + 256 / PACK_LANES - 1) / (256 / PACK_LANES)), 256, 0, st>>>(b);
     return hipGetLastError();
 }
 

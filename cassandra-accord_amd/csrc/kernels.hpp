@@ -16,6 +16,7 @@ struct BatchCtl {
     unsigned long long n_deferred;            // requests the fused kernel hands to the split kernels
     unsigned int overflow;                    // bit0 key arena, bit1 range arena, bit2 scratch, bit3 regions
     unsigned int error;                       // AD_E_* (negated) of the first failure, 0 = none
+    unsigned long long n_deferred1;           // requests the lean kernel hands to the general fused kernel
 };
 
 constexpr uint64_t NO_RB = ~0ull;
@@ -47,6 +48,9 @@ struct BatchBufs {
     uint8_t* reg;                    // per-request output regions
     uint8_t* scratch;                // big-request scratch
     uint32_t* deferred;              // [n_txns] requests deferred by k_resolve
+    uint32_t* deferred1;             // [n_txns] requests deferred by k_resolve_lean
+    const uint32_t* req_list;        // k_resolve: resolve only these requests (count *req_count); null = all
+    const unsigned long long* req_count;
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
     BatchCtl* ctl;
     uint32_t dbg;                    // timing experiments only (AD_DBG): 0 = normal
@@ -67,6 +71,7 @@ hipError_t run_pack(const BatchBufs& b, hipStream_t st);
 constexpr uint32_t SLOT_NONE = 0x7FFFFFFFu;    // p_slot: key has no CommandsForKey in this store
 constexpr uint32_t SLOT_IN_SLICE = 0x80000000u;
 hipError_t run_probe_slots(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,

@@ -270,19 +270,24 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     // ahead, ids / keys / slots one ahead (issued at the top of an iteration), the KeyEntry quarters
     // one ahead (issued once the current request's lists are staged), so a request's dependent
     // chain key_off -> slot -> KeyEntry -> lists is mostly hidden behind the previous request.
-    auto st1 = [&](uint64_t tt, uint64_t& k0o, uint32_t& npo) {
-        if (tt < n)
+    // iteration index ii -> request: all requests, or those the lean kernel deferred
+    const uint64_t n_iter = b.req_list ? uniform64(*b.req_count) : n;
+    auto tof = [&](uint64_t ii) -> uint64_t { return b.req_list ? (uint64_t)b.req_list[ii] : ii; };
+    auto st1 = [&](uint64_t ii, uint64_t& k0o, uint32_t& npo) {
+        if (ii < n_iter)
         {
+            const uint64_t tt = tof(ii);
             k0o = b.q_key_off[tt];
             npo = (uint32_t)(b.q_key_off[tt + 1] - k0o);
         }
         else { k0o = 0; npo = 0; }
     };
     struct Ids { uint64_t tm, tl, em, el; int32_t tn, en; };
-    auto ids = [&](uint64_t tt) -> Ids {
+    auto ids = [&](uint64_t ii) -> Ids {
         Ids r{0, 0, 0, 0, 0, 0};
-        if (tt < n)
+        if (ii < n_iter)
         {
+            const uint64_t tt = tof(ii);
             r.tm = b.q_txn_msb[tt]; r.tl = b.q_txn_lsb[tt]; r.tn = b.q_txn_node[tt];
             r.em = b.q_exec_msb[tt]; r.el = b.q_exec_lsb[tt]; r.en = b.q_exec_node[tt];
         }
@@ -308,12 +313,13 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     st2(k0c, npc, keyc, psc);
     uint4 kqc;
     st3(psc, kqc);
-    for (uint64_t t = t0; t < n; t += nw)
+    for (uint64_t ii = t0; ii < n_iter; ii += nw)
     {
+        const uint64_t t = tof(ii);
         uint64_t k0nn;
         uint32_t npnn;
-        st1(t + 2 * nw, k0nn, npnn);
-        const Ids idn = ids(t + nw);
+        st1(ii + 2 * nw, k0nn, npnn);
+        const Ids idn = ids(ii + nw);
         int64_t keyn;
         uint32_t psn;
         st2(k0n, npn, keyn, psn);
@@ -321,6 +327,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         bool pf3 = false;
         do {
         const uint64_t k0 = k0c;
+        (void)k0;
         const uint32_t np = npc;
         if (np > FMAXP)
         {
@@ -357,19 +364,19 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         uint4 kq = kqc;
         const uint32_t ki = slot != SLOT_NONE ? __shfl(kq.z, gb, 64) : NO_KEY;
         if (ki == NO_KEY) kq = make_uint4(0, 0, 0, 0);
-        KeyRec kr;
-        kr.seg_lo = __shfl(kq.x, gb + 1, 64);
-        kr.seg_hi = __shfl(kq.y, gb + 1, 64);
-        kr.w_lo = __shfl(kq.z, gb + 1, 64);
-        kr.w_hi = __shfl(kq.w, gb + 1, 64);
-        kr.last_txn = __shfl(kq.x, gb + 2, 64);
-        kr.last_wexec = __shfl(kq.y, gb + 2, 64);
-        kr.pruned = __shfl(kq.z, gb + 2, 64);
-        kr.maw = (int32_t)__shfl(kq.w, gb + 2, 64);
+        KeyRec kr;     // KeyEntry quarters: q0 key/idx/last_w_txn, q1 newest fields, q2/q3 cand bounds, q4/q5 KeyRec
+        kr.seg_lo = __shfl(kq.x, gb + 4, 64);
+        kr.seg_hi = __shfl(kq.y, gb + 4, 64);
+        kr.w_lo = __shfl(kq.z, gb + 4, 64);
+        kr.w_hi = __shfl(kq.w, gb + 4, 64);
+        kr.last_txn = __shfl(kq.x, gb + 5, 64);
+        kr.last_wexec = __shfl(kq.y, gb + 5, 64);
+        kr.pruned = __shfl(kq.z, gb + 5, 64);
+        kr.maw = (int32_t)__shfl(kq.w, gb + 5, 64);
         const uint32_t last_w_txn = __shfl(kq.w, gb, 64);
         const uint32_t csel = cls == 0 ? kq.x : (cls == 1 ? kq.y : kq.z);
-        const uint32_t cand_lo = __shfl(csel, gb + 3, 64), cand_hi = __shfl(csel, gb + 4, 64);
-        const uint32_t cwr_tail = __shfl(kq.w, gb + 4, 64), cwr_hi = __shfl(kq.x, gb + 5, 64);
+        const uint32_t cand_lo = __shfl(csel, gb + 2, 64), cand_hi = __shfl(csel, gb + 3, 64);
+        const uint32_t cwr_tail = __shfl(kq.z, gb + 1, 64), cwr_hi = __shfl(kq.w, gb + 1, 64);
         const bool has_cfk = gact && ki != NO_KEY;
 
         // ---- K1: end = insertPos(S), M = maxCommittedWriteBefore (CommandsForKey.java:912-928)

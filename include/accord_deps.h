@@ -192,6 +192,7 @@ typedef struct ad_stats {
     uint64_t n_levels;               /* 1 + max level                                         */
     uint64_t n_edges;                /* edges of the sparsified waitingOn DAG                  */
     uint64_t n_launches;             /* frontier-step launches                                */
+    uint64_t n_deferred_lean;        /* ad_deps_batch*: requests the lean kernel handed to the general one */
 } ad_stats;
 
 /* Results, one CSR triple per map and request, packed in request order.

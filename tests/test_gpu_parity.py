@@ -43,6 +43,29 @@ def test_random_larger(oracle, seed):
     _compare(w, oracle)
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_random_small_lean_store(oracle, seed):
+    # no range commands / redundant-before: the lean kernel runs first; older requests defer
+    w = synth.random_small(500 + seed, n_range_cmds=0, n_redundant=0, accept_frac=0.2 * (seed % 4),
+                           max_keys=2 + seed % 7)
+    _compare(w, oracle, paths=(0,))
+
+
+@pytest.mark.parametrize("esp,sync,reads", [(0.0, 0.0, False), (0.3, 0.05, False), (0.0, 0.02, True)])
+def test_config2_lean_classes(oracle, esp, sync, reads, monkeypatch):
+    # every witness class on the lean path (Read -> Ws, Write -> RsOrWs, ExclusiveSyncPoint ->
+    # AnyGloballyVisible incl. SyncPoints), with and without the lean kernel
+    w = synth.config2(n_txns=4000, n_keys=20000, n_hist_entries=300000, esp_frac=esp, sync_frac=sync)
+    if reads:
+        w.queries.txn.lsb[:] = w.queries.txn.lsb & ~np.uint64(0xE)          # all Read
+        w.queries.exec.lsb[:] = w.queries.txn.lsb
+    got, exp = _compare(w, oracle, paths=(0,))
+    assert got.stats["n_deferred_lean"] < len(w.queries)
+    monkeypatch.setenv("AD_NO_LEAN", "1")
+    got2 = native.resolve(w)
+    assert got2.equals(exp)
+
+
 def test_config1_sequential(oracle):
     got, exp = _compare(synth.config1(), oracle)
     assert got.pair_count(A.AD_MAP_KEY) > 0
