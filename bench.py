@@ -312,6 +312,7 @@ def main():
                      "algorithmic_bytes_per_launch": sbytes[dom], "launch_ms": stage_ms[dom]},
         "stages_ms": {STAGES[i]: round(float(stage_ms[i]), 4) for i in range(6) if STAGES[i] != "-"},
         "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
+        "deferred": {"lean_to_general": int(stats.get("n_deferred_lean", 0)), "to_split": int(stats["n_deferred"])},
         "ingest_ms": stats["ms_ingest"],
     }
     if world > 1:

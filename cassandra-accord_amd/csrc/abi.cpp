@@ -196,7 +196,7 @@ struct ad_ctx {
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
     DevBuf arena, rarena;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, p_slot;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, p_slot;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
@@ -563,11 +563,11 @@ static int build_snapshot(ad_ctx* c)
         ke.rec = krec[k];
         for (int cl = 0; cl < NCLASS; ++cl)
         {
-            ke.cand_lo[cl] = cand_off[cl * nk + k];
-            ke.cand_hi[cl] = cand_off[cl * nk + k + 1];
+            ke.cl[cl].cand_lo = cand_off[cl * nk + k];
+            ke.cl[cl].cand_hi = cand_off[cl * nk + k + 1];
+            ke.cl[cl].cwr_tail = cwr_tail[k];
+            ke.cl[cl].cwr_hi = cwr_off[k + 1];
         }
-        ke.cwr_tail = cwr_tail[k];
-        ke.cwr_hi = cwr_off[k + 1];
     }
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
         (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_khash, khash)) || (rc = upload(c, c->d_kent, kent)) || (rc = upload(c, c->d_cand, cand)) || (rc = upload(c, c->d_cwr, cwr)) ||
@@ -797,7 +797,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     }
     const bool split_only = c->cfg.path == 1;
     // the lean kernel covers stores without range commands / redundant-before entries, elision on
-    const bool lean = !split_only && c->ds.n_rent == 0 && c->ds.n_rb == 0 && c->ds.elide && getenv("AD_NO_LEAN") == nullptr;
+    const bool lean = !split_only && np > 0 && c->ds.n_rent == 0 && c->ds.n_rb == 0 && c->ds.elide &&
+                      getenv("AD_NO_LEAN") == nullptr;
     BatchBufs b{};
     b.n_txns = n;
     b.n_probes = np;
@@ -807,10 +808,12 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
         !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
-        !ens<uint32_t>(c->p_slot, np) || !ens<uint32_t>(c->deferred1, n))
+        !ens<uint32_t>(c->p_slot, np) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
+        !ens<uint32_t>(c->deferred2, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64))
         return c->fail(AD_E_NOMEM, "batch buffers");
     b.p_slot = c->p_slot.as<uint32_t>();
     b.deferred1 = c->deferred1.as<uint32_t>();
+    b.deferred2 = c->deferred2.as<uint32_t>();
     if (const char* e = getenv("AD_DBG")) b.dbg = (uint32_t)atoi(e);
     b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>(); b.bsum = c->bsum.as<uint64_t>();
     b.t_reg = c->t_reg.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>(); b.deferred = c->deferred.as<uint32_t>();
@@ -865,8 +868,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 HIPCHK(c, run_resolve_lean(c->ds, b, st));
                 HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 BatchBufs b2 = b;
-                b2.req_list = b.deferred1;
-                b2.req_count = &b.ctl->n_deferred1;
+                b2.req_list = b.deferred2;
+                b2.req_count = &b.ctl->n_deferred2;
                 HIPCHK(c, run_resolve(c->ds, b2, st));
             }
             else
@@ -947,7 +950,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         S.n_txns = n;
         S.n_probes = np;
         S.n_deferred = nd;
-        S.n_deferred_lean = lean ? h.n_deferred1 : 0;
+        S.n_deferred_lean = lean ? h.n_real2 : 0;     // requests the lean passes left to the general kernel
         for (int m = 0; m < 3; ++m)
         {
             S.n_pairs[m] = tot[3 * m + 2] - tot[3 * m + 0];

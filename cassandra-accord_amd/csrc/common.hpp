@@ -104,22 +104,23 @@ constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 //   cand_c  and  { Ws: the last committed Write | RsOrWs/AnyGloballyVisible: cwr[cwr_tail, cwr_hi) }
 // (minus the request's own id): the mapReduceActive loop (CommandsForKey.java:930-950) with
 // end = byId.length and M = the last committed Write's executeAt.
-// The newest-probe fields fill the first 64 bytes (quarters q0..q3, all the lean kernel reads);
-// the KeyRec of the tree path is q4, q5.
+// Quarters (16 B): q0 key/idx (the hash probe), q1 the newest test + Ws emission, q2+c the lists of
+// witness class c (the lean kernel loads q1 and one class quarter), q5/q6 the KeyRec of the tree path.
+struct KeyClassLists {
+    uint32_t cand_lo, cand_hi;     // never-elided entries of class c: cand[cand_lo, cand_hi)
+    uint32_t cwr_tail, cwr_hi;     // committed R/W from the last committed Write on: cwr[cwr_tail, cwr_hi)
+};
 struct alignas(128) KeyEntry {
-    int64_t key;                   // q0.xy
-    uint32_t idx;                  // q0.z   KEY_EMPTY = free slot
-    uint32_t last_w_txn;           // q0.w   txn rank of the last committed Write by executeAt (0 = none)
-    uint32_t last_txn;             // q1.x   rank of byId's last txnId (0 if empty)
-    uint32_t last_wexec;           // q1.y   executeAt rank of the last committed Write (0 if none)
-    uint32_t cwr_tail;             // q1.z   first cwr entry with executeAt >= the last committed Write's
-    uint32_t cwr_hi;               // q1.w
-    uint32_t cand_lo[NCLASS];      // q2.xyz
+    int64_t key;                   // q0
+    uint32_t idx;                  //    KEY_EMPTY = free slot
     uint32_t pad0;
-    uint32_t cand_hi[NCLASS];      // q3.xyz
+    uint32_t last_txn;             // q1.x  rank of byId's last txnId (0 if empty)
+    uint32_t last_wexec;           // q1.y  executeAt rank of the last committed Write (0 if none)
+    uint32_t last_w_txn;           // q1.z  txn rank of that Write (0 if none)
     uint32_t pad1;
-    KeyRec rec;                    // q4, q5
-    uint32_t pad[8];
+    KeyClassLists cl[NCLASS];      // q2..q4
+    KeyRec rec;                    // q5, q6
+    uint32_t pad2[4];              // q7
 };
 static_assert(sizeof(KeyEntry) == 128, "KeyEntry is one cache line");
 

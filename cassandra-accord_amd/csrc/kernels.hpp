@@ -16,7 +16,9 @@ struct BatchCtl {
     unsigned long long n_deferred;            // requests the fused kernel hands to the split kernels
     unsigned int overflow;                    // bit0 key arena, bit1 range arena, bit2 scratch, bit3 regions
     unsigned int error;                       // AD_E_* (negated) of the first failure, 0 = none
-    unsigned long long n_deferred1;           // requests the lean kernel hands to the general fused kernel
+    unsigned long long n_deferred1;           // lean pass 1 -> pass 2 list slots (reserved in chunks)
+    unsigned long long n_deferred2;           // lean pass 2 -> general fused kernel list slots
+    unsigned long long n_real1, n_real2;      // requests on those lists (without chunk holes)
 };
 
 constexpr uint64_t NO_RB = ~0ull;
@@ -48,7 +50,8 @@ struct BatchBufs {
     uint8_t* reg;                    // per-request output regions
     uint8_t* scratch;                // big-request scratch
     uint32_t* deferred;              // [n_txns] requests deferred by k_resolve
-    uint32_t* deferred1;             // [n_txns] requests deferred by k_resolve_lean
+    uint32_t* deferred1;             // requests deferred by lean pass 1 (+ chunk holes)
+    uint32_t* deferred2;             // requests deferred by lean pass 2 (+ chunk holes)
     const uint32_t* req_list;        // k_resolve: resolve only these requests (count *req_count); null = all
     const unsigned long long* req_count;
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
@@ -70,6 +73,8 @@ hipError_t run_pack(const BatchBufs& b, hipStream_t st);
 // fused per-request path (resolve.hip)
 constexpr uint32_t SLOT_NONE = 0x7FFFFFFFu;    // p_slot: key has no CommandsForKey in this store
 constexpr uint32_t SLOT_IN_SLICE = 0x80000000u;
+constexpr uint32_t DEFER_HOLE = 0xFFFFFFFFu;      // unused slot of a wave's deferral chunk
+constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave reserves at a time
 hipError_t run_probe_slots(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);

@@ -22,16 +22,15 @@ namespace adx {
 
 constexpr int LEAN_WAVES = 4;
 constexpr uint32_t LEAN_MAXP = 8;      // keys per request
-constexpr uint32_t LEAN_MAXE = 32;     // raw emissions per request (one lane each)
 constexpr uint32_t LEAN_CHUNK = 1u << 16;
 
-// ascending bitonic sort within each 32-lane half (lane bit 5 never selects a direction)
-template <uint32_t KMAX>
-__device__ __forceinline__ void half_bitonic(uint32_t& key)
+// ascending bitonic sort within each LPR-lane segment (a request's lanes)
+template <uint32_t K, uint32_t LPR>
+__device__ __forceinline__ void seg_bitonic(uint32_t& key)
 {
-    const uint32_t l = lane_id() & 31u;
+    const uint32_t l = lane_id() & (LPR - 1);
 #pragma unroll
-    for (uint32_t k = 2; k <= KMAX; k <<= 1)
+    for (uint32_t k = 2; k <= K; k <<= 1)
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1)
         {
@@ -41,8 +40,6 @@ __device__ __forceinline__ void half_bitonic(uint32_t& key)
             key = (lower == up) ? min(key, ok) : max(key, ok);
         }
 }
-
-__device__ __forceinline__ uint32_t half_bits(uint64_t m, uint32_t h) { return (uint32_t)(m >> (32 * h)); }
 
 struct LeanChunk {
     uint64_t cur = 0, end = 0;
@@ -65,72 +62,127 @@ struct LeanChunk {
     }
 };
 
-__global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s, BatchBufs b)
+// Request lists: `in` (null = all requests) with *in_count entries (DEFER_HOLE = skip); the
+// requests this pass cannot take are appended to `out` in per-wave chunks of DEFER_CHUNK slots
+// (*out_count counts reserved slots, *out_real the requests), holes filled with DEFER_HOLE.
+struct LeanLists {
+    const uint32_t* in;
+    const unsigned long long* in_count;
+    uint32_t* out;
+    unsigned long long* out_count;
+    unsigned long long* out_real;
+};
+
+// RPW requests per wave (2: 32 lanes each, up to 32 raw emissions; 1: 64 lanes, up to 64)
+template <uint32_t RPW>
+__global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s, BatchBufs b, LeanLists io)
 {
-    const uint32_t lane = lane_id(), h = lane >> 5, hl = lane & 31u;
-    const uint32_t below = (1u << hl) - 1u;                     // lanes below this one in its half
+    constexpr uint32_t LPR = 64 / RPW;                       // lanes per request
+    const uint32_t lane = lane_id(), h = lane / LPR, hl = lane & (LPR - 1), sb = h * LPR;
+    const uint64_t below = (1ull << hl) - 1;                 // lanes below this one in its segment
+    auto seg = [&](uint64_t m) -> uint64_t { return RPW == 1 ? m : ((m >> sb) & 0xFFFFFFFFull); };
     const uint64_t n = b.n_txns;
-    const uint64_t npairs = (n + 1) / 2;
+    const uint64_t n_slots = io.in ? uniform64(*io.in_count) : n;
+    const uint64_t n_items = (n_slots + RPW - 1) / RPW;
     const uint64_t nw = (uint64_t)gridDim.x * LEAN_WAVES;
     const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
     const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
-    const uint32_t S_new = (uint32_t)(2 * s.n_dict);            // rank of an id above every member
+    const uint32_t S = s.n_dict ? (uint32_t)(2 * s.n_dict) : 0u;   // rank of an id above every member
+    const uint32_t self = 0;   // exec == txnId: none; else a non-member rank (even): never an emission
     LeanChunk ralloc;
+    uint64_t dcur = 0, dend = 0, dreal = 0;     // this wave's reserved deferral slots [dcur, dend)
+    auto dfill = [&]() {
+        for (uint64_t i = dcur + lane_id(); i < dend; i += 64) io.out[i] = DEFER_HOLE;
+    };
 
-    for (uint64_t pr = uniform64((uint64_t)blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6)); pr < npairs; pr += nw)
+    // ---- software pipeline over the wave's items it, it + nw, ... (RPW requests each). Per
+    // iteration the next item's raw inputs are derived and its keys/slots loaded at the top, its
+    // KeyEntry quarters once this item's list loads are out: the chain key_off -> slot ->
+    // KeyEntry -> lists costs about one round trip per iteration. Pipeline loads are branch-free
+    // (clamped addresses, results masked where used) so the compiler's wait counts stay exact.
+    struct Raw { uint64_t k0, k1, tm, tl, em, el; int32_t tn, en; };
+    struct Req { uint64_t k0; uint32_t np, cls, t; bool act, defer; };
+    auto req_of = [&](uint64_t it) -> uint32_t {
+        const uint64_t si = it * RPW + h;
+        if (si >= n_slots) return DEFER_HOLE;
+        return io.in ? io.in[si] : (uint32_t)si;
+    };
+    auto loadA = [&](uint32_t t) -> Raw {
+        Raw r;
+        const uint64_t tt = t != DEFER_HOLE ? t : 0;
+        r.k0 = b.q_key_off[tt];
+        r.k1 = b.q_key_off[tt + 1];
+        r.tm = b.q_txn_msb[tt]; r.tl = b.q_txn_lsb[tt]; r.tn = b.q_txn_node[tt];
+        r.em = b.q_exec_msb[tt]; r.el = b.q_exec_lsb[tt]; r.en = b.q_exec_node[tt];
+        return r;
+    };
+    // PreAccept.java:251-261: witness class; S and self by the newest fast path or defer
+    auto derive = [&](uint32_t t, const Raw& r) -> Req {
+        Req q{0, 0, 0, t, false, false};
+        q.act = t != DEFER_HOLE;
+        if (q.act)
+        {
+            q.k0 = r.k0;
+            q.np = (uint32_t)(r.k1 - r.k0);
+            const uint32_t kinds = kind_witnesses((uint32_t)((r.tl >> 1) & 7));
+            q.cls = (uint32_t)kinds_class(kinds);
+            const bool same = r.em == r.tm && ((r.el ^ r.tl) & 0xFFFFFFFFFFFF001EULL) == 0 && r.en == r.tn;
+            const bool s_new = s.n_dict == 0 || norm_cmp(last, norm_tid(r.em, r.el, r.en)) < 0;
+            const bool t_new = same || s.n_dict == 0 || norm_cmp(last, norm_tid(r.tm, r.tl, r.tn)) < 0;
+            q.defer = q.np > LEAN_MAXP || kinds == 0 || !s_new || !t_new;
+        }
+        return q;
+    };
+    // keys and raw slots (the in-slice bit is stripped where the slot is used)
+    auto loadB = [&](const Req& q, int64_t& key, uint32_t& pslot) {
+        const bool on = q.act && !q.defer && hl < q.np;
+        const uint64_t i = on ? q.k0 + hl : 0;
+        key = b.q_keys[i];
+        pslot = b.p_slot[i];
+        if (!on) pslot = SLOT_NONE;
+    };
+    auto slot_of = [](uint32_t pslot) { return pslot & ~SLOT_IN_SLICE; };
+    auto loadC = [&](uint32_t pslot, uint32_t cls, uint4& q1, uint4& qc) {
+        const uint32_t sl = slot_of(pslot);
+        const uint4* e = reinterpret_cast<const uint4*>(s.kent + (sl != SLOT_NONE ? sl : 0u));
+        q1 = e[1];
+        qc = e[2 + cls];
+    };
+
+    const uint64_t it0 = uniform64((uint64_t)blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
+    uint32_t tc = req_of(it0);
+    Req qc = derive(tc, loadA(tc));
+    int64_t keyc;
+    uint32_t slotc;
+    loadB(qc, keyc, slotc);
+    uint4 q1c, qlc;
+    loadC(slotc, qc.cls, q1c, qlc);
+    uint32_t tN = req_of(it0 + nw);
+    Raw rN = loadA(tN);
+
+    for (uint64_t it = it0; it < n_items; it += nw)
     {
-        const uint64_t t = 2 * pr + h;
-        bool act = t < n;
-        // ---- request (PreAccept.java:251-261): ids, witness class, S / self by the newest fast path
-        uint64_t k0 = 0;
-        uint32_t np = 0;
-        uint32_t kinds = 0, S = 0, self = 0;
-        int cls = 0;
-        bool defer = false;
-        if (act)
-        {
-            k0 = b.q_key_off[t];
-            np = (uint32_t)(b.q_key_off[t + 1] - k0);
-            const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t], em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
-            const int32_t tn = b.q_txn_node[t], en = b.q_exec_node[t];
-            kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
-            cls = kinds_class(kinds);
-            const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
-            const bool s_new = s.n_dict == 0 || norm_cmp(last, norm_tid(em, el, en)) < 0;
-            const bool t_new = same || s.n_dict == 0 || norm_cmp(last, norm_tid(tm, tl, tn)) < 0;
-            S = s.n_dict ? S_new : 0u;
-            self = 0;          // same: none; else a non-member rank (even): never equal to an emission
-            defer = np > LEAN_MAXP || kinds == 0 || !s_new || !t_new;
-        }
-        // ---- per key p = hl < np: its KeyEntry (first 64 bytes)
+        const uint32_t t = qc.t;
+        const Req qn = derive(tN, rN);
+        tN = req_of(it + 2 * nw);
+        rN = loadA(tN);
+        int64_t keyn;
+        uint32_t slotn;
+        loadB(qn, keyn, slotn);
+
+        // ---- current item: per key p = hl < np, newest test and emission counts
+        bool act = qc.act;
+        bool defer = qc.defer;
+        const uint32_t np = qc.np, cls = qc.cls;
         const bool kact = act && !defer && hl < np;
-        int64_t key = 0;
-        uint32_t slot = SLOT_NONE;
-        if (kact)
-        {
-            key = b.q_keys[k0 + hl];
-            slot = b.p_slot[k0 + hl] & ~SLOT_IN_SLICE;
-        }
-        uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0, q2 = q0, q3 = q0;
-        if (slot != SLOT_NONE)
-        {
-            const uint4* e = reinterpret_cast<const uint4*>(s.kent + slot);
-            q0 = e[0];
-            q1 = e[1];
-            q2 = e[2];
-            q3 = e[3];
-        }
-        const bool has_cfk = slot != SLOT_NONE;
+        const bool has_cfk = slot_of(slotc) != SLOT_NONE;
         // newest: end = byId.length (last txnId < S) and M = the last committed Write's executeAt
         // (it executes before S), CommandsForKey.java:912-928
-        const bool newest = !has_cfk || (q1.x < S && q1.y < S);
-        const uint32_t cand_lo = cls == 0 ? q2.x : (cls == 1 ? q2.y : q2.z);
-        const uint32_t cand_hi = cls == 0 ? q3.x : (cls == 1 ? q3.y : q3.z);
-        const uint32_t n1 = has_cfk ? cand_hi - cand_lo : 0u;
-        const uint32_t n2 = !has_cfk ? 0u : (cls == 0 ? (q0.w != 0 ? 1u : 0u) : q1.w - q1.z);
+        const bool newest = !has_cfk || (q1c.x < S && q1c.y < S);
+        const uint32_t n1 = has_cfk ? qlc.y - qlc.x : 0u;
+        const uint32_t n2 = !has_cfk ? 0u : (cls == 0 ? (q1c.z != 0 ? 1u : 0u) : qlc.w - qlc.z);
         const uint32_t nn = kact ? n1 + n2 : 0u;
-        // exclusive prefix of nn over the 8 key lanes of each half
-        uint32_t inc = nn;
+        uint32_t inc = nn;       // exclusive prefix of nn over the 8 key lanes of each request
 #pragma unroll
         for (uint32_t d = 1; d < 8; d <<= 1)
         {
@@ -138,9 +190,27 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             if ((hl & 7) >= d) inc += v;
         }
         const uint32_t start = inc - nn;
-        const uint32_t T = __shfl(inc, (lane & 32u) | 7u, 64);
-        defer = defer || half_bits(ballot(kact && !newest), h) != 0 || T > LEAN_MAXE;
-        if (act && defer && hl == 0) b.deferred1[atomicAdd(&b.ctl->n_deferred1, 1ull)] = (uint32_t)t;
+        const uint32_t T = __shfl(inc, sb | 7u, 64);
+        defer = defer || seg(ballot(kact && !newest)) != 0 || T > LPR;
+        {
+            // deferrals go to a per-wave chunk of the out list (one atomic per DEFER_CHUNK)
+            const uint64_t dm = ballot(act && defer && hl == 0);
+            const uint32_t nd = __popcll(dm);
+            if (nd)
+            {
+                if (nd > dend - dcur)
+                {
+                    dfill();
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(io.out_count, (unsigned long long)DEFER_CHUNK);
+                    dcur = uniform64(base);
+                    dend = dcur + DEFER_CHUNK;
+                }
+                if (act && defer && hl == 0) io.out[dcur + __popcll(dm & ((1ull << lane) - 1))] = t;
+                dcur += nd;
+                dreal += nd;
+            }
+        }
         act = act && !defer;
 
         // ---- one raw emission per lane: element e = hl of key a
@@ -148,29 +218,33 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
 #pragma unroll
         for (uint32_t p = 1; p < LEAN_MAXP; ++p)
         {
-            const uint32_t sp = __shfl(start, (lane & 32u) | p, 64);
+            const uint32_t sp = __shfl(start, sb | p, 64);
             if (p < np && hl >= sp) a = p;
         }
-        const uint32_t src = (lane & 32u) | a;
+        const uint32_t src = sb | a;
         const uint32_t a_start = __shfl(start, src, 64), a_n1 = __shfl(n1, src, 64);
-        const uint32_t a_clo = __shfl(cand_lo, src, 64), a_ct = __shfl(q1.z, src, 64), a_lw = __shfl(q0.w, src, 64);
+        const uint32_t a_clo = __shfl(qlc.x, src, 64), a_ct = __shfl(qlc.z, src, 64), a_lw = __shfl(q1c.z, src, 64);
         const bool live = act && hl < T;
-        uint32_t txw = 0;
-        if (live)
-        {
-            const uint32_t i = hl - a_start;
-            txw = i < a_n1 ? s.cand[a_clo + i] : (cls == 0 ? (a_lw | (1u << RANK_BITS)) : s.cwr[a_ct + (i - a_n1)]);
-        }
+        const uint32_t i = hl - a_start;
+        const bool from_cand = i < a_n1;
+        const uint32_t* lp = !live ? s.cand : (from_cand ? s.cand + (a_clo + i) : (cls != 0 ? s.cwr + (a_ct + (i - a_n1)) : s.cand));
+        const uint32_t lv = *lp;
+        // the next item's KeyEntry quarters go out behind this item's list loads
+        uint4 q1n, qln;
+        loadC(slotn, qn.cls, q1n, qln);
+
+        const uint32_t txw = !live ? 0u : ((from_cand || cls != 0) ? lv : (a_lw | (1u << RANK_BITS)));
         const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
         const bool want = live && r != self;
         const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;       // !managesExecution -> directKeyDeps
+        const int64_t key = keyc;
 
         // ---- keyDeps (m = 0) and directKeyDeps (m = 2)
         for (int m = 0; m < 3; m += 2)
         {
             const bool mine = want && (m == 0 ? !is1 : is1);
             const uint64_t mb = ballot(mine);
-            const uint32_t tot = __popc(half_bits(mb, h));
+            const uint32_t tot = __popcll(seg(mb));
             if (mb == 0)
             {
                 if (act && hl == 0)
@@ -181,21 +255,23 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
                 }
                 continue;
             }
-            // sort (rank, key) per half; dedup -> txnIds; body = unique-rank index per key, ascending
+            // sort (rank, key) per request; dedup -> txnIds; body = unique-rank index per key, ascending
             uint32_t k = mine ? ((r << 3) | a) : 0xFFFFFFFFu;
-            const uint32_t kmax = uniform(max(__shfl(tot, 0, 64), __shfl(tot, 32, 64)));
-            if (kmax <= 8) half_bitonic<8>(k);
-            else if (kmax <= 16) half_bitonic<16>(k);
-            else half_bitonic<32>(k);
+            // the sort must span every lane that may hold one (raw emissions: lanes [0, T))
+            const uint32_t kmax = RPW == 1 ? uniform(T) : uniform(max(__shfl(T, 0, 64), __shfl(T, 32, 64)));
+            if (kmax <= 8) seg_bitonic<8, LPR>(k);
+            else if (kmax <= 16) seg_bitonic<16, LPR>(k);
+            else if (kmax <= 32 || LPR == 32) seg_bitonic<(LPR < 32 ? LPR : 32), LPR>(k);
+            else seg_bitonic<LPR, LPR>(k);
             const bool valid = hl < tot;
             const uint32_t xr = k >> 3, ka = k & 7u;
-            const uint32_t prev = __shfl_up(k, 1, 32);
+            const uint32_t prev = __shfl_up(k, 1, LPR);
             const bool uniq = valid && (hl == 0 || (prev >> 3) != xr);
             // index of this lane's value among the distinct values: uniques up to and including this
             // lane, minus one (equal values sit in adjacent lanes)
-            const uint64_t um = ballot(uniq);
-            const uint32_t U = __popc(half_bits(um, h));
-            const uint32_t ur = __popc(half_bits(um, h) & below) + (uniq ? 1u : 0u) - 1u;
+            const uint64_t um = seg(ballot(uniq));
+            const uint32_t U = __popcll(um);
+            const uint32_t ur = __popcll(um & below) + (uniq ? 1u : 0u) - 1u;
             uint64_t same = ballot(valid);
 #pragma unroll
             for (int bit = 0; bit < 3; ++bit)
@@ -203,16 +279,15 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
                 const uint64_t bb = ballot((ka >> bit) & 1u);
                 same &= ((ka >> bit) & 1u) ? bb : ~bb;
             }
-            const uint32_t pos_in_key = __popc(half_bits(same, h) & below);
+            const uint32_t pos_in_key = __popcll(seg(same) & below);
             // per key p (lanes hl < 8): its number of values, then body starts and heads
             uint32_t cnt = 0;
 #pragma unroll
             for (uint32_t p = 0; p < LEAN_MAXP; ++p)
             {
-                const uint32_t c = __popc(half_bits(ballot(valid && ka == p), h));
-                if ((hl & 7) == p) cnt = c;
+                const uint32_t c = __popcll(seg(ballot(valid && ka == p)));
+                if (hl == p) cnt = c;
             }
-            if (hl >= 8) cnt = 0;
             uint32_t cinc = cnt;
 #pragma unroll
             for (uint32_t d = 1; d < 8; d <<= 1)
@@ -221,13 +296,14 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
                 if ((hl & 7) >= d) cinc += v;
             }
             const uint32_t kstart_l = cinc - cnt;
-            const uint64_t nem = ballot(hl < 8 && cnt > 0);
-            const uint32_t nk = __popc(half_bits(nem, h));
-            const uint32_t kk = __popc(half_bits(nem, h) & below);
-            const uint32_t kstart = __shfl(kstart_l, (lane & 32u) | ka, 64);
-            // regions of both halves from one wave-uniform allocation
+            const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
+            const uint32_t nk = __popcll(nem);
+            const uint32_t kk = __popcll(nem & below);
+            const uint32_t kstart = __shfl(kstart_l, sb | ka, 64);
+            // regions of the wave's requests from one wave-uniform allocation
             const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
-            const uint64_t bA = uniform64(__shfl(bytes, 0, 64)), bB = uniform64(__shfl(bytes, 32, 64));
+            const uint64_t bA = uniform64(__shfl(bytes, 0, 64));
+            const uint64_t bB = RPW == 1 ? 0 : uniform64(__shfl(bytes, 32, 64));
             const uint64_t base = ralloc.take(b.ctl, bA + bB, reg_cap);
             const uint64_t ro = h ? base + bA : base;
             const bool fits = base + bA + bB <= reg_cap;
@@ -258,24 +334,42 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             b.sz[4 * n + t] = 0;
             b.sz[5 * n + t] = 0;
         }
+        qc = qn;
+        keyc = keyn;
+        slotc = slotn;
+        q1c = q1n;
+        qlc = qln;
     }
+    dfill();
+    if (lane == 0 && dreal) atomicAdd(io.out_real, (unsigned long long)dreal);
 }
 
-hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+template <uint32_t RPW>
+static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, const LeanLists& io, hipStream_t st)
 {
-    if (!b.n_txns) return hipSuccess;
     static int per_cu = 0;
     if (!per_cu)
     {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean, 64 * LEAN_WAVES, 0) != hipSuccess || nb <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW>, 64 * LEAN_WAVES, 0) != hipSuccess || nb <= 0)
             nb = 2;
         per_cu = std::min(nb, 8);
     }
-    const uint64_t need = ((b.n_txns + 1) / 2 + LEAN_WAVES - 1) / LEAN_WAVES;
-    const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu);
-    k_resolve_lean<<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b);
+    const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
+    const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu));
+    k_resolve_lean<RPW><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, io);
     return hipGetLastError();
+}
+
+// pass 1: every request, two per wave -> D1; pass 2: D1, one per wave (up to 64 emissions) -> D2
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+{
+    if (!b.n_txns) return hipSuccess;
+    LeanLists p1{nullptr, nullptr, b.deferred1, &b.ctl->n_deferred1, &b.ctl->n_real1};
+    hipError_t e = launch_lean<2>(s, b, p1, st);
+    if (e != hipSuccess) return e;
+    LeanLists p2{b.deferred1, &b.ctl->n_deferred1, b.deferred2, &b.ctl->n_deferred2, &b.ctl->n_real2};
+    return launch_lean<1>(s, b, p2, st);
 }
 
 }  // namespace adx

@@ -274,9 +274,9 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     const uint64_t n_iter = b.req_list ? uniform64(*b.req_count) : n;
     auto tof = [&](uint64_t ii) -> uint64_t { return b.req_list ? (uint64_t)b.req_list[ii] : ii; };
     auto st1 = [&](uint64_t ii, uint64_t& k0o, uint32_t& npo) {
-        if (ii < n_iter)
+        const uint64_t tt = ii < n_iter ? tof(ii) : (uint64_t)DEFER_HOLE;
+        if (tt != DEFER_HOLE)
         {
-            const uint64_t tt = tof(ii);
             k0o = b.q_key_off[tt];
             npo = (uint32_t)(b.q_key_off[tt + 1] - k0o);
         }
@@ -285,9 +285,9 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     struct Ids { uint64_t tm, tl, em, el; int32_t tn, en; };
     auto ids = [&](uint64_t ii) -> Ids {
         Ids r{0, 0, 0, 0, 0, 0};
-        if (ii < n_iter)
+        const uint64_t tt = ii < n_iter ? tof(ii) : (uint64_t)DEFER_HOLE;
+        if (tt != DEFER_HOLE)
         {
-            const uint64_t tt = tof(ii);
             r.tm = b.q_txn_msb[tt]; r.tl = b.q_txn_lsb[tt]; r.tn = b.q_txn_node[tt];
             r.em = b.q_exec_msb[tt]; r.el = b.q_exec_lsb[tt]; r.en = b.q_exec_node[tt];
         }
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     };
     auto st3 = [&](uint32_t psi, uint4& kqo) {
         const uint32_t sl = psi & ~SLOT_IN_SLICE;
-        kqo = (sl != SLOT_NONE && j < 6) ? reinterpret_cast<const uint4*>(s.kent + sl)[j] : make_uint4(0, 0, 0, 0);
+        kqo = (sl != SLOT_NONE && j < 7) ? reinterpret_cast<const uint4*>(s.kent + sl)[j] : make_uint4(0, 0, 0, 0);
     };
     const uint64_t t0 = uniform64((uint64_t)blockIdx.x * FWAVES + (threadIdx.x >> 6));
     uint64_t k0c, k0n;
@@ -326,6 +326,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         uint4 kqn = make_uint4(0, 0, 0, 0);
         bool pf3 = false;
         do {
+        if (t == DEFER_HOLE) break;                // unused slot of a lean wave's deferral chunk
         const uint64_t k0 = k0c;
         (void)k0;
         const uint32_t np = npc;
@@ -364,19 +365,19 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         uint4 kq = kqc;
         const uint32_t ki = slot != SLOT_NONE ? __shfl(kq.z, gb, 64) : NO_KEY;
         if (ki == NO_KEY) kq = make_uint4(0, 0, 0, 0);
-        KeyRec kr;     // KeyEntry quarters: q0 key/idx/last_w_txn, q1 newest fields, q2/q3 cand bounds, q4/q5 KeyRec
-        kr.seg_lo = __shfl(kq.x, gb + 4, 64);
-        kr.seg_hi = __shfl(kq.y, gb + 4, 64);
-        kr.w_lo = __shfl(kq.z, gb + 4, 64);
-        kr.w_hi = __shfl(kq.w, gb + 4, 64);
-        kr.last_txn = __shfl(kq.x, gb + 5, 64);
-        kr.last_wexec = __shfl(kq.y, gb + 5, 64);
-        kr.pruned = __shfl(kq.z, gb + 5, 64);
-        kr.maw = (int32_t)__shfl(kq.w, gb + 5, 64);
-        const uint32_t last_w_txn = __shfl(kq.w, gb, 64);
-        const uint32_t csel = cls == 0 ? kq.x : (cls == 1 ? kq.y : kq.z);
-        const uint32_t cand_lo = __shfl(csel, gb + 2, 64), cand_hi = __shfl(csel, gb + 3, 64);
-        const uint32_t cwr_tail = __shfl(kq.z, gb + 1, 64), cwr_hi = __shfl(kq.w, gb + 1, 64);
+        KeyRec kr;     // KeyEntry quarters (common.hpp): q1 newest fields, q2+cls lists, q5/q6 KeyRec
+        kr.seg_lo = __shfl(kq.x, gb + 5, 64);
+        kr.seg_hi = __shfl(kq.y, gb + 5, 64);
+        kr.w_lo = __shfl(kq.z, gb + 5, 64);
+        kr.w_hi = __shfl(kq.w, gb + 5, 64);
+        kr.last_txn = __shfl(kq.x, gb + 6, 64);
+        kr.last_wexec = __shfl(kq.y, gb + 6, 64);
+        kr.pruned = __shfl(kq.z, gb + 6, 64);
+        kr.maw = (int32_t)__shfl(kq.w, gb + 6, 64);
+        const uint32_t last_w_txn = __shfl(kq.z, gb + 1, 64);
+        const uint32_t cq = gb + 2 + (uint32_t)cls;
+        const uint32_t cand_lo = __shfl(kq.x, cq, 64), cand_hi = __shfl(kq.y, cq, 64);
+        const uint32_t cwr_tail = __shfl(kq.z, cq, 64), cwr_hi = __shfl(kq.w, cq, 64);
         const bool has_cfk = gact && ki != NO_KEY;
 
         // ---- K1: end = insertPos(S), M = maxCommittedWriteBefore (CommandsForKey.java:912-928)
