@@ -75,7 +75,7 @@ class AdStats(C.Structure):
                 ("ms_device", C.c_double), ("ms_ingest", C.c_double),
                 ("ms_stage", C.c_double * 8), ("n_deferred", C.c_uint64), ("bytes_stage", C.c_uint64 * 8),
                 ("n_levels", C.c_uint64), ("n_edges", C.c_uint64), ("n_launches", C.c_uint64),
-                ("n_deferred_lean", C.c_uint64)]
+                ("n_deferred_lean", C.c_uint64), ("n_lean_pass2", C.c_uint64)]
 
 
 class AdDepsResult(C.Structure):

@@ -201,7 +201,8 @@ struct ad_ctx {
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t ev_slot = nullptr;      // fused path: after k_probe_slots
-    hipEvent_t ev_lean = nullptr;      // fused path: after k_resolve_lean
+    hipEvent_t ev_lean = nullptr;      // fused path: after k_resolve_lean (both passes)
+    hipEvent_t ev_lean1 = nullptr;     // fused path: after lean pass 1
     // multi-GPU export / merge buffers
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
@@ -865,7 +866,10 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             {
                 // lean kernel first (newest requests, 2 per wave); the general fused kernel then
                 // takes only what it deferred (count read on the device, no host round trip)
-                HIPCHK(c, run_resolve_lean(c->ds, b, st));
+                if (!c->ev_lean1) HIPCHK(c, hipEventCreate(&c->ev_lean1));
+                HIPCHK(c, run_resolve_lean(c->ds, b, 1, st));
+                HIPCHK(c, hipEventRecord(c->ev_lean1, st));
+                HIPCHK(c, run_resolve_lean(c->ds, b, 2, st));
                 HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 BatchBufs b2 = b;
                 b2.req_list = b.deferred2;
@@ -951,6 +955,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         S.n_probes = np;
         S.n_deferred = nd;
         S.n_deferred_lean = lean ? h.n_real2 : 0;     // requests the lean passes left to the general kernel
+        S.n_lean_pass2 = lean ? h.n_real1 : 0;        // requests lean pass 1 left to pass 2
         for (int m = 0; m < 3; ++m)
         {
             S.n_pairs[m] = tot[3 * m + 2] - tot[3 * m + 0];
@@ -975,10 +980,14 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             S.ms_stage[0] -= ms;
             if (lean)
             {
-                float ml = 0;
-                HIPCHK(c, hipEventElapsedTime(&ml, c->ev_slot, c->ev_lean));
-                S.ms_stage[3] = S.ms_stage[0] - ml;
-                S.ms_stage[0] = ml;
+                // stage 0: lean pass 1 (k_resolve_lean<2>), 3: lean pass 2 (k_resolve_lean<1>),
+                // 6: the general kernel on what both passes deferred
+                float m1 = 0, m2 = 0;
+                HIPCHK(c, hipEventElapsedTime(&m1, c->ev_slot, c->ev_lean1));
+                HIPCHK(c, hipEventElapsedTime(&m2, c->ev_lean1, c->ev_lean));
+                S.ms_stage[6] = S.ms_stage[0] - m1 - m2;
+                S.ms_stage[0] = m1;
+                S.ms_stage[3] = m2;
             }
         }
         S.ms_device = total;
@@ -1079,6 +1088,7 @@ void ad_ctx_destroy(ad_ctx* c)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_slot) (void)hipEventDestroy(c->ev_slot);
     if (c->ev_lean) (void)hipEventDestroy(c->ev_lean);
+    if (c->ev_lean1) (void)hipEventDestroy(c->ev_lean1);
     if (c->lv) levels_work_destroy(c->lv);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

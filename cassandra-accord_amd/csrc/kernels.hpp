@@ -76,7 +76,7 @@ constexpr uint32_t SLOT_IN_SLICE = 0x80000000u;
 constexpr uint32_t DEFER_HOLE = 0xFFFFFFFFu;      // unused slot of a wave's deferral chunk
 constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave reserves at a time
 hipError_t run_probe_slots(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
-hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,

@@ -62,9 +62,8 @@ struct LeanChunk {
     }
 };
 
-// Request lists: `in` (null = all requests) with *in_count entries (DEFER_HOLE = skip); the
-// requests this pass cannot take are appended to `out` in per-wave chunks of DEFER_CHUNK slots
-// (*out_count counts reserved slots, *out_real the requests), holes filled with DEFER_HOLE.
+// Request lists: `in` (null = all requests) with *in_count entries; the requests this pass cannot
+// take are appended to `out` (*out_count entries; *out_real counts them too).
 struct LeanLists {
     const uint32_t* in;
     const unsigned long long* in_count;
@@ -90,9 +89,24 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     const uint32_t S = s.n_dict ? (uint32_t)(2 * s.n_dict) : 0u;   // rank of an id above every member
     const uint32_t self = 0;   // exec == txnId: none; else a non-member rank (even): never an emission
     LeanChunk ralloc;
-    uint64_t dcur = 0, dend = 0, dreal = 0;     // this wave's reserved deferral slots [dcur, dend)
-    auto dfill = [&]() {
-        for (uint64_t i = dcur + lane_id(); i < dend; i += 64) io.out[i] = DEFER_HOLE;
+    // deferrals are gathered in a per-wave LDS buffer and appended to the out list in exact-size
+    // blocks (one atomic per block, no holes)
+    __shared__ uint32_t dbuf_all[LEAN_WAVES][DEFER_CHUNK];
+    uint32_t* dbuf = dbuf_all[threadIdx.x >> 6];
+    uint32_t dn = 0;            // wave-uniform fill of dbuf
+    auto dflush = [&]() {
+        if (!dn) return;
+        unsigned long long base = 0;
+        if (lane_id() == 0)
+        {
+            base = atomicAdd(io.out_count, (unsigned long long)dn);
+            atomicAdd(io.out_real, (unsigned long long)dn);
+        }
+        base = uniform64(base);
+        wave_lds_sync();
+        if (lane_id() < dn) io.out[base + lane_id()] = dbuf[lane_id()];
+        wave_lds_sync();
+        dn = 0;
     };
 
     // ---- software pipeline over the wave's items it, it + nw, ... (RPW requests each). Per
@@ -193,22 +207,13 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         const uint32_t T = __shfl(inc, sb | 7u, 64);
         defer = defer || seg(ballot(kact && !newest)) != 0 || T > LPR;
         {
-            // deferrals go to a per-wave chunk of the out list (one atomic per DEFER_CHUNK)
             const uint64_t dm = ballot(act && defer && hl == 0);
             const uint32_t nd = __popcll(dm);
             if (nd)
             {
-                if (nd > dend - dcur)
-                {
-                    dfill();
-                    unsigned long long base = 0;
-                    if (lane == 0) base = atomicAdd(io.out_count, (unsigned long long)DEFER_CHUNK);
-                    dcur = uniform64(base);
-                    dend = dcur + DEFER_CHUNK;
-                }
-                if (act && defer && hl == 0) io.out[dcur + __popcll(dm & ((1ull << lane) - 1))] = t;
-                dcur += nd;
-                dreal += nd;
+                if (dn + nd > DEFER_CHUNK) dflush();
+                if (act && defer && hl == 0) dbuf[dn + __popcll(dm & ((1ull << lane) - 1))] = t;
+                dn += nd;
             }
         }
         act = act && !defer;
@@ -340,8 +345,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         q1c = q1n;
         qlc = qln;
     }
-    dfill();
-    if (lane == 0 && dreal) atomicAdd(io.out_real, (unsigned long long)dreal);
+    dflush();
 }
 
 template <uint32_t RPW>
@@ -362,12 +366,14 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, const Le
 }
 
 // pass 1: every request, two per wave -> D1; pass 2: D1, one per wave (up to 64 emissions) -> D2
-hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
-    LeanLists p1{nullptr, nullptr, b.deferred1, &b.ctl->n_deferred1, &b.ctl->n_real1};
-    hipError_t e = launch_lean<2>(s, b, p1, st);
-    if (e != hipSuccess) return e;
+    if (pass == 1)
+    {
+        LeanLists p1{nullptr, nullptr, b.deferred1, &b.ctl->n_deferred1, &b.ctl->n_real1};
+        return launch_lean<2>(s, b, p1, st);
+    }
     LeanLists p2{b.deferred1, &b.ctl->n_deferred1, b.deferred2, &b.ctl->n_deferred2, &b.ctl->n_real2};
     return launch_lean<1>(s, b, p2, st);
 }

@@ -192,7 +192,8 @@ typedef struct ad_stats {
     uint64_t n_levels;               /* 1 + max level                                         */
     uint64_t n_edges;                /* edges of the sparsified waitingOn DAG                  */
     uint64_t n_launches;             /* frontier-step launches                                */
-    uint64_t n_deferred_lean;        /* ad_deps_batch*: requests the lean kernel handed to the general one */
+    uint64_t n_deferred_lean;        /* ad_deps_batch*: requests the lean passes handed to the general kernel */
+    uint64_t n_lean_pass2;           /* ad_deps_batch*: requests lean pass 1 handed to lean pass 2     */
 } ad_stats;
 
 /* Results, one CSR triple per map and request, packed in request order.
