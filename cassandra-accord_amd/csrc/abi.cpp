@@ -203,6 +203,8 @@ struct ad_ctx {
     hipEvent_t ev_slot = nullptr;      // fused path: after k_probe_slots
     hipEvent_t ev_lean = nullptr;      // fused path: after k_resolve_lean (both passes)
     hipEvent_t ev_lean1 = nullptr;     // fused path: after lean pass 1
+    hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;   // split path on the fused kernels' deferrals
+    BatchCtl* h_ctl = nullptr;         // pinned mirror of the batch control block
     // multi-GPU export / merge buffers
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
@@ -879,11 +881,25 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             else
                 HIPCHK(c, run_resolve(c->ds, b, st));
             HIPCHK(c, hipEventRecord(c->ev[1], st));
-            HIPCHK(c, hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
-            HIPCHK(c, hipStreamSynchronize(st));
+        }
+        if (!c->h_ctl) HIPCHK(c, hipHostMalloc((void**)&c->h_ctl, sizeof(BatchCtl), hipHostMallocDefault));
+        if (!c->ev_sp0) HIPCHK(c, hipEventCreate(&c->ev_sp0));
+        if (!c->ev_sp1) HIPCHK(c, hipEventCreate(&c->ev_sp1));
+        // offsets of every request's three maps, totals into the control block, one host round trip
+        HIPCHK(c, hipEventRecord(c->ev[2], st));
+        HIPCHK(c, run_offsets(b, st));
+        HIPCHK(c, run_collect_totals(b, st));
+        HIPCHK(c, hipEventRecord(c->ev[3], st));
+        HIPCHK(c, hipMemcpyAsync(c->h_ctl, b.ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        h = *c->h_ctl;
+        double ms_split = 0;
+        if (!split_only)
+        {
             nd = h.n_deferred;
             if (nd && !h.error && !(h.overflow & 8u))
             {
+                HIPCHK(c, hipEventRecord(c->ev_sp0, st));
                 // deferred requests: gather a sub-batch, resolve it with the split kernels, scatter back
                 if (!ens<uint32_t>(c->s_cnt, nd) || !ens<uint64_t>(c->s_ko, nd + 1))
                     return c->fail(AD_E_NOMEM, "deferred buffers");
@@ -911,16 +927,19 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 sb.q_keys = c->s_k.as<int64_t>();
                 if ((rc = run_split(c, sb, st))) return rc;
                 HIPCHK(c, run_defer_scatter(b, b.deferred, nd, sb.sz, sb.t_reg, st));
+                HIPCHK(c, run_offsets(b, st));
+                HIPCHK(c, run_collect_totals(b, st));
+                HIPCHK(c, hipEventRecord(c->ev_sp1, st));
+                HIPCHK(c, hipMemcpyAsync(c->h_ctl, b.ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, st));
+                HIPCHK(c, hipStreamSynchronize(st));
+                h = *c->h_ctl;
+                float msp = 0;
+                HIPCHK(c, hipEventElapsedTime(&msp, c->ev_sp0, c->ev_sp1));
+                ms_split = msp;
             }
         }
-        HIPCHK(c, hipEventRecord(c->ev[2], st));
-        HIPCHK(c, run_offsets(b, st));
-        HIPCHK(c, hipEventRecord(c->ev[3], st));
-        uint64_t tot[9] = {0};
-        for (int a = 0; a < 9; ++a)
-            HIPCHK(c, hipMemcpyAsync(&tot[a], b.off + (uint64_t)a * (n + 1) + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipMemcpyAsync(&h, b.ctl, sizeof(h), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
+        uint64_t tot[9];
+        for (int a = 0; a < 9; ++a) tot[a] = h.tot[a];
         if (h.error)
         {
             if (h.error == ERR_STATE)
@@ -990,6 +1009,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 S.ms_stage[3] = m2;
             }
         }
+        S.ms_stage[1] += ms_split;           // split kernels on the fused kernels' deferrals (+ offsets re-run)
+        total += ms_split;
         S.ms_device = total;
         S.ms_ingest = c->ms_ingest;
         out->n_txns = n;
@@ -1089,6 +1110,9 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->ev_slot) (void)hipEventDestroy(c->ev_slot);
     if (c->ev_lean) (void)hipEventDestroy(c->ev_lean);
     if (c->ev_lean1) (void)hipEventDestroy(c->ev_lean1);
+    if (c->ev_sp0) (void)hipEventDestroy(c->ev_sp0);
+    if (c->ev_sp1) (void)hipEventDestroy(c->ev_sp1);
+    if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->lv) levels_work_destroy(c->lv);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;

@@ -1033,6 +1033,18 @@ hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_
 
 hipError_t run_offsets(const BatchBufs& b, hipStream_t st) { return run_scan_arrays(b.sz, b.off, b.n_txns, 9, b.bsum, st); }
 
+// the 9 totals into the control block, so one copy of it tells the host everything
+__global__ void k_collect_totals(const uint64_t* __restrict__ off, uint64_t n, BatchCtl* ctl)
+{
+    if (threadIdx.x < 9) ctl->tot[threadIdx.x] = off[(uint64_t)threadIdx.x * (n + 1) + n];
+}
+
+hipError_t run_collect_totals(const BatchBufs& b, hipStream_t st)
+{
+    k_collect_totals<<<1, 64, 0, st>>>(b.off, b.n_txns, b.ctl);
+    return hipGetLastError();
+}
+
 int device_cu_count()
 {
     static int cus = 0;

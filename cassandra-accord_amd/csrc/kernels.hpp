@@ -18,7 +18,8 @@ struct BatchCtl {
     unsigned int error;                       // AD_E_* (negated) of the first failure, 0 = none
     unsigned long long n_deferred1;           // lean pass 1 -> pass 2 list slots (reserved in chunks)
     unsigned long long n_deferred2;           // lean pass 2 -> general fused kernel list slots
-    unsigned long long n_real1, n_real2;      // requests on those lists (without chunk holes)
+    unsigned long long n_real1, n_real2;      // requests on those lists
+    unsigned long long tot[9];                // totals of the 9 per-request size arrays (after the offsets scan)
 };
 
 constexpr uint64_t NO_RB = ~0ull;
@@ -69,6 +70,7 @@ hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st);
 hipError_t run_pack(const BatchBufs& b, hipStream_t st);
+hipError_t run_collect_totals(const BatchBufs& b, hipStream_t st);
 
 // fused per-request path (resolve.hip)
 constexpr uint32_t SLOT_NONE = 0x7FFFFFFFu;    // p_slot: key has no CommandsForKey in this store

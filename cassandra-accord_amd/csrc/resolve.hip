@@ -808,7 +808,9 @@ __global__ __launch_bounds__(256) void k_probe_slots(DevSnapshot s, BatchBufs b)
         uint64_t h = key_hash(key) & s.khash_mask;
         while (true)
         {
-            const uint4 q = reinterpret_cast<const uint4*>(s.kent + h)[0];
+            // the 16-byte KeySlot table has the KeyEntry table's hash and capacity: slot h of one is
+            // slot h of the other (a 4x smaller probe footprint)
+            const uint4 q = reinterpret_cast<const uint4*>(s.khash + h)[0];
             if (q.z == KEY_EMPTY) break;
             if ((int64_t)(((uint64_t)q.y << 32) | q.x) == key)
             {
