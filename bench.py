@@ -31,9 +31,9 @@ from accord_deps import exchange, native, synth  # noqa: E402
 
 METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-STAGES = ["lean resolve pass 1 (2 requests/wave)", "deferred requests (split K0..K2)", "key -> KeyEntry slots",
+STAGES = ["lean resolve pass 1 (2 requests/wave)", "deferred requests (split K0..K2)", "prepare (request records, key slots)",
           "lean resolve pass 2 (1 request/wave)", "offsets scan", "pack", "general fused resolve (lean deferrals)"]
-KERNEL_OF_STAGE = ["k_resolve_lean<2u>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_probe_slots",
+KERNEL_OF_STAGE = ["k_resolve_lean<2u>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
                    "k_resolve_lean<1u>", "k_scan_blocks+k_scan_sums+k_scan_add", "k_pack", "k_resolve"]
 # K1 + K2 of every request run in these stages / kernels: the roofline's "dominant kernel"
 RESOLVE_STAGES = [0, 3, 6]
@@ -81,7 +81,7 @@ def stage_bytes(w, stats):
     b = [0] * 7
     b[0] = len(q) * (40 + 8) + 8 * q.n_probes + int((17 * lk + 16).sum()) + 16 * int(w.cmds.range_off[-1]) + \
         out_bytes + len(q) * (9 * 4 + 3 * 8)
-    b[2] = 8 * q.n_probes + 128 * q.n_probes + 4 * q.n_probes     # keys, one slot line, slot index
+    b[2] = len(q) * (56 + 16) + q.n_probes * (8 + 16 + 4)   # request ids + key_off, record; keys, KeySlot, slot
     b[4] = 9 * (4 + 8) * len(q)
     b[5] = 2 * out_bytes + len(q) * (9 * (4 + 8) + 3 * 8)
     return b

@@ -196,11 +196,11 @@ struct ad_ctx {
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
     DevBuf arena, rarena;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, p_slot;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, p_slot, q_rec;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
-    hipEvent_t ev_slot = nullptr;      // fused path: after k_probe_slots
+    hipEvent_t ev_slot = nullptr;      // fused path: after k_prepare
     hipEvent_t ev_lean = nullptr;      // fused path: after k_resolve_lean (both passes)
     hipEvent_t ev_lean1 = nullptr;     // fused path: after lean pass 1
     hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;   // split path on the fused kernels' deferrals
@@ -811,10 +811,11 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
         !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
-        !ens<uint32_t>(c->p_slot, np) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
+        !ens<uint32_t>(c->p_slot, np) || !ens<uint4>(c->q_rec, n) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
         !ens<uint32_t>(c->deferred2, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64))
         return c->fail(AD_E_NOMEM, "batch buffers");
     b.p_slot = c->p_slot.as<uint32_t>();
+    b.q_rec = c->q_rec.as<uint4>();
     b.deferred1 = c->deferred1.as<uint32_t>();
     b.deferred2 = c->deferred2.as<uint32_t>();
     if (const char* e = getenv("AD_DBG")) b.dbg = (uint32_t)atoi(e);
@@ -862,7 +863,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         {
             if (!c->ev_slot) HIPCHK(c, hipEventCreate(&c->ev_slot));
             if (!c->ev_lean) HIPCHK(c, hipEventCreate(&c->ev_lean));
-            HIPCHK(c, run_probe_slots(c->ds, b, st));
+            HIPCHK(c, run_prepare(c->ds, b, st));
             HIPCHK(c, hipEventRecord(c->ev_slot, st));
             if (lean)
             {
@@ -992,7 +993,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         }
         if (!split_only)
         {
-            // stage 2: k_probe_slots; stage 0: k_resolve_lean (or k_resolve when not lean);
+            // stage 2: k_prepare; stage 0: k_resolve_lean (or k_resolve when not lean);
             // stage 3: k_resolve over the lean kernel's deferrals
             HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev_slot));
             S.ms_stage[2] = ms;

@@ -38,7 +38,8 @@ struct BatchBufs {
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
     uint32_t* p_txn; uint4* p_rec;
-    uint32_t* p_slot;                // fused path: KeyEntry slot of each probe | in-slice << 31 (k_probe_slots)
+    uint32_t* p_slot;                // fused path: KeyEntry slot of each probe | in-slice << 31 (k_prepare)
+    uint4* q_rec;                    // fused path: per request {key_off lo, hi, np | cls << 16 | flags, 0} (k_prepare)
     // K1
     uint32_t* arena; uint32_t* p_off; uint32_t* p_c0; uint32_t* p_c1;
     // K4
@@ -77,7 +78,8 @@ constexpr uint32_t SLOT_NONE = 0x7FFFFFFFu;    // p_slot: key has no CommandsFor
 constexpr uint32_t SLOT_IN_SLICE = 0x80000000u;
 constexpr uint32_t DEFER_HOLE = 0xFFFFFFFFu;      // unused slot of a wave's deferral chunk
 constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave reserves at a time
-hipError_t run_probe_slots(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+constexpr uint32_t REC_FAST = 1u << 24;          // q_rec: newest fast path applies (S, self, <= 8 keys, valid kind)
+hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);

@@ -85,7 +85,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     const uint64_t n_items = (n_slots + RPW - 1) / RPW;
     const uint64_t nw = (uint64_t)gridDim.x * LEAN_WAVES;
     const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
-    const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
     const uint32_t S = s.n_dict ? (uint32_t)(2 * s.n_dict) : 0u;   // rank of an id above every member
     const uint32_t self = 0;   // exec == txnId: none; else a non-member rank (even): never an emission
     LeanChunk ralloc;
@@ -114,37 +113,23 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     // KeyEntry quarters once this item's list loads are out: the chain key_off -> slot ->
     // KeyEntry -> lists costs about one round trip per iteration. Pipeline loads are branch-free
     // (clamped addresses, results masked where used) so the compiler's wait counts stay exact.
-    struct Raw { uint64_t k0, k1, tm, tl, em, el; int32_t tn, en; };
+    using Raw = uint4;        // the request record of k_prepare
     struct Req { uint64_t k0; uint32_t np, cls, t; bool act, defer; };
     auto req_of = [&](uint64_t it) -> uint32_t {
         const uint64_t si = it * RPW + h;
         if (si >= n_slots) return DEFER_HOLE;
         return io.in ? io.in[si] : (uint32_t)si;
     };
-    auto loadA = [&](uint32_t t) -> Raw {
-        Raw r;
-        const uint64_t tt = t != DEFER_HOLE ? t : 0;
-        r.k0 = b.q_key_off[tt];
-        r.k1 = b.q_key_off[tt + 1];
-        r.tm = b.q_txn_msb[tt]; r.tl = b.q_txn_lsb[tt]; r.tn = b.q_txn_node[tt];
-        r.em = b.q_exec_msb[tt]; r.el = b.q_exec_lsb[tt]; r.en = b.q_exec_node[tt];
-        return r;
-    };
-    // PreAccept.java:251-261: witness class; S and self by the newest fast path or defer
+    auto loadA = [&](uint32_t t) -> Raw { return b.q_rec[t != DEFER_HOLE ? t : 0u]; };
+    // the record carries PreAccept.java:251-261's witness class and whether S and self take the
+    // newest fast path (k_prepare); anything else defers
     auto derive = [&](uint32_t t, const Raw& r) -> Req {
         Req q{0, 0, 0, t, false, false};
         q.act = t != DEFER_HOLE;
-        if (q.act)
-        {
-            q.k0 = r.k0;
-            q.np = (uint32_t)(r.k1 - r.k0);
-            const uint32_t kinds = kind_witnesses((uint32_t)((r.tl >> 1) & 7));
-            q.cls = (uint32_t)kinds_class(kinds);
-            const bool same = r.em == r.tm && ((r.el ^ r.tl) & 0xFFFFFFFFFFFF001EULL) == 0 && r.en == r.tn;
-            const bool s_new = s.n_dict == 0 || norm_cmp(last, norm_tid(r.em, r.el, r.en)) < 0;
-            const bool t_new = same || s.n_dict == 0 || norm_cmp(last, norm_tid(r.tm, r.tl, r.tn)) < 0;
-            q.defer = q.np > LEAN_MAXP || kinds == 0 || !s_new || !t_new;
-        }
+        q.k0 = ((uint64_t)r.y << 32) | r.x;
+        q.np = r.z & 0xFFFFu;
+        q.cls = (r.z >> 16) & 3u;
+        q.defer = (r.z & REC_FAST) == 0;
         return q;
     };
     // keys and raw slots (the in-slice bit is stripped where the slot is used)

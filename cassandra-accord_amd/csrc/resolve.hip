@@ -354,7 +354,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
 
         // ---- per key g (8-lane group g < np): the 128-byte KeyEntry of the key's CommandsForKey,
-        // found by k_probe_slots (lane j of the group loads quarter j)
+        // found by k_prepare (lane j of the group loads quarter j)
         const bool gact = g < np;
         const uint32_t gb = lane & ~7u;
         const int64_t key = keyc;
@@ -791,41 +791,86 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     }
 }
 
-// key -> KeyEntry slot, one thread per probe (open addressing, linear probing): keeps the
-// dependent hash probing out of the per-request kernel (InMemoryCommandStore.mapReduceForKey's
-// slice test :280 and the CommandsForKey lookup)
-__global__ __launch_bounds__(256) void k_probe_slots(DevSnapshot s, BatchBufs b)
+// Per-request preparation, one thread per request (PreAccept.java:251-261 and the key lookups of
+// InMemoryCommandStore.mapReduceForKey, :280): the request record the lean kernel reads instead
+// of the raw ids, and the KeyEntry slot of every (request, key) probe (open addressing, linear
+// probing in the 16-byte KeySlot table, which shares the KeyEntry table's hash and capacity).
+// Keeping the dependent key -> slot probing here leaves the per-request kernels one load shorter.
+constexpr uint32_t PREP_UNROLL = 8;     // keys whose probes are issued together
+
+__global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= b.n_probes) return;
-    const int64_t key = b.q_keys[p];
-    bool in_slice = s.n_slices == 0;
-    for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
-        in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
-    uint32_t slot = SLOT_NONE;
-    if (in_slice && s.n_keys)
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n_txns) return;
+    const uint64_t k0 = b.q_key_off[t], k1 = b.q_key_off[t + 1];
+    const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t], em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
+    const int32_t tn = b.q_txn_node[t], en = b.q_exec_node[t];
+    const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
+    const uint32_t cls = kinds ? (uint32_t)kinds_class(kinds) : 0u;
+    const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
+    const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
+    const bool s_new = s.n_dict == 0 || norm_cmp(last, norm_tid(em, el, en)) < 0;
+    const bool t_new = same || s.n_dict == 0 || norm_cmp(last, norm_tid(tm, tl, tn)) < 0;
+    const uint64_t np = k1 - k0;
+    // lean fast path: S and self need no dictionary search, at most 8 keys, a valid kind
+    const bool fast = kinds != 0 && s_new && t_new && np <= 8;
+    b.q_rec[t] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32),
+                            (uint32_t)(np < 0xFFFFu ? np : 0xFFFFu) | (cls << 16) | (fast ? REC_FAST : 0u), 0u);
+    for (uint64_t c0 = k0; c0 < k1; c0 += PREP_UNROLL)
     {
-        uint64_t h = key_hash(key) & s.khash_mask;
-        while (true)
+        int64_t key[PREP_UNROLL];
+        uint64_t h[PREP_UNROLL];
+        bool on[PREP_UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
         {
-            // the 16-byte KeySlot table has the KeyEntry table's hash and capacity: slot h of one is
-            // slot h of the other (a 4x smaller probe footprint)
-            const uint4 q = reinterpret_cast<const uint4*>(s.khash + h)[0];
-            if (q.z == KEY_EMPTY) break;
-            if ((int64_t)(((uint64_t)q.y << 32) | q.x) == key)
+            on[u] = c0 + u < k1;
+            key[u] = on[u] ? b.q_keys[c0 + u] : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
+        {
+            bool in_slice = s.n_slices == 0;
+            for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
+                in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key[u]);
+            h[u] = key_hash(key[u]) & s.khash_mask;
+            if (!on[u]) continue;
+            if (!in_slice || !s.n_keys)
             {
-                slot = (uint32_t)h;
-                break;
+                b.p_slot[c0 + u] = SLOT_NONE;
+                on[u] = false;
             }
-            h = (h + 1) & s.khash_mask;
+        }
+        uint4 q[PREP_UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
+            q[u] = on[u] ? reinterpret_cast<const uint4*>(s.khash + h[u])[0] : make_uint4(0, 0, KEY_EMPTY, 0);
+#pragma unroll
+        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
+        {
+            if (!on[u]) continue;
+            uint64_t hh = h[u];
+            uint4 qq = q[u];
+            uint32_t slot = SLOT_NONE;
+            while (true)
+            {
+                if (qq.z == KEY_EMPTY) break;
+                if ((int64_t)(((uint64_t)qq.y << 32) | qq.x) == key[u])
+                {
+                    slot = (uint32_t)hh;
+                    break;
+                }
+                hh = (hh + 1) & s.khash_mask;
+                qq = reinterpret_cast<const uint4*>(s.khash + hh)[0];
+            }
+            b.p_slot[c0 + u] = slot | SLOT_IN_SLICE;
         }
     }
-    b.p_slot[p] = slot | (in_slice ? SLOT_IN_SLICE : 0u);
 }
 
-hipError_t run_probe_slots(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
-    if (b.n_probes) k_probe_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b);
+    if (b.n_txns) k_prepare<<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
     return hipGetLastError();
 }
 
