@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../../include/accord_deps.h"
@@ -400,6 +402,170 @@ __global__ __launch_bounds__(256) void k_level_step(uint32_t L, const uint32_t* 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Dataflow leveling: every txn's counter word packs {remaining predecessors : 32, max level seen
+// : 32}; finishing txn u (level L) updates each successor s with one 64-bit CAS {cnt - 1,
+// max(lvl, L + 1)} -- the CAS that takes cnt to 0 owns s, whose level is then exactly 1 + max over
+// its predecessors, in whatever order they finished. A launch spreads its ready list evenly over
+// the waves; a wave keeps the txns it releases in an LDS stack (newest first, so a dependency chain
+// is followed as soon as it is released) and works 16 of them per step, their successor edges
+// spread over the 64 lanes (as k_level_step). After FLOW_STEPS steps (or when its stack is full)
+// a wave hands what it holds to the next launch's ready list, so work never collapses onto a few
+// waves. Nothing ever waits for another wave; launches go out in chunks between host checks.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t FLOW_Q = 1024;          // LDS stack entries per wave ({txn, level})
+constexpr uint32_t FLOW_WAVES = 4;
+constexpr uint32_t FLOW_STEPS = 8;         // steps per wave per launch
+constexpr uint32_t FLOW_SEEDS = 256;       // ready txns a wave takes at launch start (at most)
+constexpr uint32_t FLOW_CHUNK = 16;        // launches between host checks
+
+__global__ __launch_bounds__(64 * FLOW_WAVES) void k_level_flow(const uint2* __restrict__ in, const uint32_t* in_count,
+                                                                 uint2* __restrict__ out, uint32_t* out_count,
+                                                                 const uint64_t* __restrict__ succ_off,
+                                                                 const uint32_t* __restrict__ succ, unsigned long long* word,
+                                                                 uint32_t* __restrict__ level, unsigned long long* done_count,
+                                                                 uint32_t max_steps)
+{
+    __shared__ uint2 q_all[FLOW_WAVES][FLOW_Q];
+    uint2* q = q_all[threadIdx.x >> 6];
+    const uint32_t lane = lane_id();
+    const uint32_t n_waves = gridDim.x * FLOW_WAVES;
+    const uint32_t wid = blockIdx.x * FLOW_WAVES + (threadIdx.x >> 6);
+    const uint32_t ns = *in_count;
+    if (ns == 0) return;
+    // an even share of the ready list per wave (at most FLOW_SEEDS); the surplus moves on as is
+    const uint32_t per = min((ns + n_waves - 1) / n_waves, FLOW_SEEDS);
+    const uint32_t s0 = min(ns, wid * per), s1 = min(ns, s0 + per);
+    uint32_t nq = s1 - s0;                         // wave-uniform stack depth
+    for (uint32_t i = lane; i < nq; i += 64) q[i] = in[s0 + i];
+    const uint64_t cap = (uint64_t)n_waves * per;
+    if (ns > cap)
+    {
+        const uint32_t extra = ns - (uint32_t)cap, share = (extra + n_waves - 1) / n_waves;
+        const uint32_t e0 = min(extra, wid * share), e1 = min(extra, e0 + share);
+        uint32_t base = 0;
+        if (lane == 0 && e1 > e0) base = atomicAdd(out_count, e1 - e0);
+        base = __shfl(base, 0, 64);
+        for (uint32_t i = e0 + lane; i < e1; i += 64) out[base + (i - e0)] = in[cap + i];
+    }
+    wave_lds_sync();
+    uint64_t done = 0;
+    for (uint32_t step = 0; nq && step < max_steps; ++step)
+    {
+        const uint32_t g = min(nq, STEP_GROUP);
+        nq -= g;
+        uint2 me = make_uint2(0, 0);
+        uint64_t e0 = 0;
+        uint32_t deg = 0;
+        if (lane < g)
+        {
+            me = q[nq + lane];
+            level[me.x] = me.y;
+            e0 = succ_off[me.x];
+            deg = (uint32_t)(succ_off[me.x + 1] - e0);
+        }
+        wave_lds_sync();
+        done += g;
+        uint32_t inc = deg;
+#pragma unroll
+        for (uint32_t d = 1; d < STEP_GROUP; d <<= 1)
+        {
+            const uint32_t t = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += t;
+        }
+        uint32_t incl[STEP_GROUP];
+#pragma unroll
+        for (uint32_t j = 0; j < STEP_GROUP; ++j) incl[j] = __shfl(inc, j, 64);
+        const uint32_t total = incl[STEP_GROUP - 1];
+        for (uint32_t x0 = 0; x0 < total; x0 += 64)
+        {
+            const uint32_t x = x0 + lane;
+            uint32_t owner = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < STEP_GROUP; ++j) owner += incl[j] <= x ? 1u : 0u;
+            // shuffles by every lane (a lane outside the exec mask reads back 0)
+            const uint64_t eo = __shfl(e0, owner & (STEP_GROUP - 1), 64);
+            const uint32_t prev = __shfl(inc, (owner - 1) & (STEP_GROUP - 1), 64);
+            const uint32_t lu = __shfl(me.y, owner & (STEP_GROUP - 1), 64);
+            const uint32_t before = owner == 0 ? 0u : prev;
+            bool ready = false;
+            uint32_t sx = 0, sl = 0;
+            if (x < total)
+            {
+                sx = succ[eo + (x - before)];
+                unsigned long long old = __hip_atomic_load(&word[sx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                while (true)
+                {
+                    const uint32_t cnt = (uint32_t)(old >> 32), lv = (uint32_t)old;
+                    const uint32_t nl = max(lv, lu + 1);
+                    const unsigned long long nw = ((unsigned long long)(cnt - 1) << 32) | nl;
+                    if (__hip_atomic_compare_exchange_strong(&word[sx], &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT))
+                    {
+                        ready = cnt == 1;
+                        sl = nl;
+                        break;
+                    }
+                }
+            }
+            // released successors go on the stack (to the next launch when it is full)
+            const uint64_t m = ballot(ready);
+            const uint32_t nr = __popcll(m);
+            if (nr)
+            {
+                const uint32_t pos = mbcnt(m);
+                if (nq + nr <= FLOW_Q)
+                {
+                    if (ready) q[nq + pos] = make_uint2(sx, sl);
+                    nq += nr;
+                }
+                else
+                {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(out_count, nr);
+                    base = __shfl(base, 0, 64);
+                    if (ready) out[base + pos] = make_uint2(sx, sl);
+                }
+            }
+            wave_lds_sync();
+        }
+    }
+    // hand the rest of the stack to the next launch
+    if (nq)
+    {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(out_count, nq);
+        base = __shfl(base, 0, 64);
+        for (uint32_t i = lane; i < nq; i += 64) out[base + i] = q[i];
+    }
+    if (lane == 0 && done) atomicAdd(done_count, (unsigned long long)done);
+}
+
+__global__ void k_flow_init(const uint32_t* __restrict__ indeg, uint64_t n, unsigned long long* __restrict__ word,
+                            uint2* __restrict__ seeds, uint32_t* seed_count)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool src = r < n && indeg[r] == 0;
+    if (r < n) word[r] = (unsigned long long)indeg[r] << 32;
+    const uint64_t m = ballot(src);
+    if (!m) return;
+    uint32_t base = 0;
+    const uint32_t leader = __ffsll((unsigned long long)m) - 1;
+    if (lane_id() == leader) base = atomicAdd(seed_count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (src) seeds[base + mbcnt(m)] = make_uint2((uint32_t)r, 0u);
+}
+
+__global__ void k_level_max(const uint32_t* __restrict__ level, uint64_t n, uint32_t* out_max)
+{
+    uint32_t v = 0;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x)
+        v = max(v, level[r]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor(v, d, 64));
+    if (lane_id() == 0) atomicMax(out_max, v);
+}
+
 __global__ void k_level_out(const uint32_t* __restrict__ order, const uint32_t* __restrict__ level_r, uint64_t n,
                             uint32_t* __restrict__ out)
 {
@@ -433,7 +599,7 @@ struct DBuf {
 
 struct LevelsWork {
     DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kind_r, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
-        level, front0, front1, cnt, ctl;
+        level, front0, front1, cnt, ctl, word, seedA, seedB;
     LevelsCtl* h_ctl = nullptr;         // pinned
     uint64_t* h_u64 = nullptr;          // pinned, 4 words
     hipEvent_t ev[3] = {};
@@ -606,42 +772,115 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
                                                         succ, ctl);
     LV_CHK(hipEventRecord(w->ev[1], st));
 
-    // ---- 4. frontier loop
-    uint32_t* fr[2] = {w->front0.as<uint32_t>(), w->front1.as<uint32_t>()};
-    k_frontier_init<<<blocks_for(n, 256), 256, 0, st>>>(indeg, n, level, fr[0], cnt);
-    uint32_t L = 0;
-    while (true)
+    // ---- 4. level the DAG: dataflow waves (default) or the level-synchronous frontier loop
+    // default: the level-synchronous frontier loop (one launch per level); AD_LEVELS_DATAFLOW=<steps>
+    // selects the dataflow waves (FLOW_STEPS steps per wave and launch by default)
+    const char* df = getenv("AD_LEVELS_DATAFLOW");
+    const bool frontier = df == nullptr;
+    const uint32_t flow_steps = df && atoi(df) > 0 ? (uint32_t)atoi(df) : FLOW_STEPS;
+    uint64_t nl = 0;
+    if (frontier)
     {
-        for (uint32_t c = 0; c < STEP_CHUNK; ++c, ++L)
-            k_level_step<<<STEP_BLOCKS, 256, 0, st>>>(L, cnt, fr[L & 1], fr[(L + 1) & 1], cnt + L + 1, succ_off, succ,
-                                                      indeg, level);
-        out->n_launch += STEP_CHUNK;
-        LV_CHK(hipGetLastError());
-        LV_CHK(hipMemcpyAsync(&w->h_u64[3], cnt + L, 4, hipMemcpyDeviceToHost, st));
-        LV_CHK(hipStreamSynchronize(st));
-        if ((uint32_t)w->h_u64[3] == 0) break;
-        if (L >= n + 1)
+        uint32_t* fr[2] = {w->front0.as<uint32_t>(), w->front1.as<uint32_t>()};
+        k_frontier_init<<<blocks_for(n, 256), 256, 0, st>>>(indeg, n, level, fr[0], cnt);
+        uint32_t L = 0;
+        while (true)
         {
-            *err = "ad_levels: frontier did not drain";
+            for (uint32_t c = 0; c < STEP_CHUNK; ++c, ++L)
+                k_level_step<<<STEP_BLOCKS, 256, 0, st>>>(L, cnt, fr[L & 1], fr[(L + 1) & 1], cnt + L + 1, succ_off, succ,
+                                                          indeg, level);
+            out->n_launch += STEP_CHUNK;
+            LV_CHK(hipGetLastError());
+            LV_CHK(hipMemcpyAsync(&w->h_u64[3], cnt + L, 4, hipMemcpyDeviceToHost, st));
+            LV_CHK(hipStreamSynchronize(st));
+            if ((uint32_t)w->h_u64[3] == 0) break;
+            if (L >= n + 1)
+            {
+                *err = "ad_levels: frontier did not drain";
+                return AD_E_STATE;
+            }
+        }
+        k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
+        LV_CHK(hipEventRecord(w->ev[2], st));
+        // levels = frontiers before the first empty one; every txn must have been levelled
+        std::vector<uint32_t> counts(L + 1);
+        LV_CHK(hipMemcpyAsync(counts.data(), cnt, 4 * (L + 1), hipMemcpyDeviceToHost, st));
+        LV_CHK(hipStreamSynchronize(st));
+        uint64_t total = 0;
+        for (uint32_t i = 0; i <= L && counts[i]; ++i)
+        {
+            total += counts[i];
+            nl = i + 1;
+        }
+        if (total != n)
+        {
+            *err = "ad_levels: " + std::to_string(n - total) + " txns never became ready";
             return AD_E_STATE;
         }
     }
-    k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
-    LV_CHK(hipEventRecord(w->ev[2], st));
-    // levels = frontiers before the first empty one; every txn must have been levelled
-    std::vector<uint32_t> counts(L + 1);
-    LV_CHK(hipMemcpyAsync(counts.data(), cnt, 4 * (L + 1), hipMemcpyDeviceToHost, st));
-    LV_CHK(hipStreamSynchronize(st));
-    uint64_t total = 0, nl = 0;
-    for (uint32_t i = 0; i <= L && counts[i]; ++i)
+    else
     {
-        total += counts[i];
-        nl = i + 1;
-    }
-    if (total != n)
-    {
-        *err = "ad_levels: " + std::to_string(n - total) + " txns never became ready";
-        return AD_E_STATE;
+        // word[] (u64 per txn), two ready lists (uint2 per txn); counters in cnt[]: cnt[0..1] done
+        // (u64), cnt[2] max level, cnt[3 + i] = length of the list launch i of a chunk reads
+        LV_ALLOC(w->word, 8 * n);
+        LV_ALLOC(w->seedA, 8 * n);
+        LV_ALLOC(w->seedB, 8 * n);
+        unsigned long long* word = w->word.as<unsigned long long>();
+        uint2* lists[2] = {w->seedA.as<uint2>(), w->seedB.as<uint2>()};
+        uint32_t* ctr = cnt;
+        uint32_t* lc = cnt + 3;
+        LV_CHK(hipMemsetAsync(ctr, 0, 4 * (3 + FLOW_CHUNK + 1), st));
+        k_flow_init<<<blocks_for(n, 256), 256, 0, st>>>(indeg, n, word, lists[0], lc + 0);
+        static int per_cu = 0;
+        if (!per_cu)
+        {
+            int nb = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_level_flow, 64 * FLOW_WAVES, 0) != hipSuccess || nb <= 0)
+                nb = 1;
+            per_cu = std::min(nb, 4);
+        }
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const unsigned grid = (unsigned)(cus * per_cu);
+        int cur = 0;
+        for (int chunk = 0;; ++chunk)
+        {
+            for (uint32_t i = 0; i < FLOW_CHUNK; ++i, cur ^= 1)
+                k_level_flow<<<grid, 64 * FLOW_WAVES, 0, st>>>(lists[cur], lc + i, lists[cur ^ 1], lc + i + 1, succ_off, succ,
+                                                               word, level, reinterpret_cast<unsigned long long*>(ctr),
+                                                               flow_steps);
+            out->n_launch += FLOW_CHUNK;
+            LV_CHK(hipGetLastError());
+            LV_CHK(hipMemcpyAsync(&w->h_u64[3], lc + FLOW_CHUNK, 4, hipMemcpyDeviceToHost, st));
+            LV_CHK(hipStreamSynchronize(st));
+            const uint32_t left = (uint32_t)w->h_u64[3];
+            if (left == 0) break;
+            if (chunk > (int)(n / FLOW_CHUNK) + 16)
+            {
+                *err = "ad_levels: dataflow did not drain";
+                return AD_E_STATE;
+            }
+            // the next chunk starts from the last list
+            LV_CHK(hipMemsetAsync(lc, 0, 4 * (FLOW_CHUNK + 1), st));
+            w->h_u64[3] = left;
+            LV_CHK(hipMemcpyAsync(lc, &w->h_u64[3], 4, hipMemcpyHostToDevice, st));
+        }
+        LV_CHK(hipMemsetAsync(ctr + 2, 0, 4, st));
+        k_level_max<<<256, 256, 0, st>>>(level, n, ctr + 2);
+        k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
+        LV_CHK(hipEventRecord(w->ev[2], st));
+        uint32_t tail[3];
+        LV_CHK(hipMemcpyAsync(tail, ctr, sizeof(tail), hipMemcpyDeviceToHost, st));
+        LV_CHK(hipStreamSynchronize(st));
+        uint64_t total = 0;
+        std::memcpy(&total, &tail[0], 8);
+        if (total != n)
+        {
+            *err = "ad_levels: " + std::to_string(n - total) + " txns never became ready";
+            return AD_E_STATE;
+        }
+        nl = (uint64_t)tail[2] + 1;
     }
     out->n_levels = nl;
     float a = 0, b = 0;

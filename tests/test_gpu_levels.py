@@ -21,10 +21,44 @@ def _check(g, oracle):
     return got, st
 
 
+@pytest.mark.parametrize("dataflow", [None, "8", "1"])
 @pytest.mark.parametrize("seed", range(12))
-def test_random_graph_all_kinds(oracle, seed):
+def test_random_graph_all_kinds(oracle, seed, dataflow, monkeypatch):
+    # both leveling schemes: the level-synchronous frontier loop (default) and the dataflow waves
+    if dataflow:
+        monkeypatch.setenv("AD_LEVELS_DATAFLOW", dataflow)
     g = synth.random_graph(seed, n_txns=500 + 300 * seed, n_keys=10 + 7 * seed, long_runs=(seed % 4 == 3))
     _check(g, oracle)
+
+
+def test_config5_full_dataflow(oracle, monkeypatch):
+    monkeypatch.setenv("AD_LEVELS_DATAFLOW", "8")
+    g, _ = synth.config5()
+    got, st = _check(g, oracle)
+    assert st["n_levels"] == int(got.max()) + 1
+
+
+def test_many_sources_spill_path(oracle, monkeypatch):
+    # more sources than the dataflow stacks take in one launch (seed carry-over) and a hub with a
+    # fan-out far beyond one wave's stack (spills): 3M Reads (nothing witnesses a Read on a key),
+    # 2% of the later ones directly depending on txn 0
+    n = 3_000_000
+    rng = np.random.default_rng(7)
+    hlc = np.arange(1, n + 1, dtype=np.uint64)
+    ex = make_timestamps(np.ones(n, np.uint64), hlc, np.zeros(n, np.uint64), rng.integers(1, 9, n).astype(np.int32))
+    key_off = np.arange(n + 1, dtype=np.uint64)
+    keys = rng.integers(0, 1 << 40, n).astype(np.int64)
+    hub = rng.random(n) < 0.02
+    hub[0] = False
+    dep_off = np.zeros(n + 1, np.uint64)
+    dep_off[1:] = np.cumsum(hub)
+    deps = np.zeros(int(hub.sum()), np.uint32)
+    g = Graph(ex, np.zeros(n, np.uint8), key_off, keys, dep_off, deps)
+    for df in (None, "8"):
+        if df:
+            monkeypatch.setenv("AD_LEVELS_DATAFLOW", df)
+        got, st = _check(g, oracle)
+        assert st["n_levels"] == 2
 
 
 def test_config5_scaled(oracle):
