@@ -200,6 +200,132 @@ def bench_levels(args, rank, world, local, dev):
         dist.destroy_process_group()
 
 
+def _timed_steps(args, world, dev, step):
+    stats = None
+    for _ in range(args.warmup):
+        stats = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    all_stats = []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        all_stats.append(step())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, all_stats
+
+
+def _sum_over_ranks(world, dev, x):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
+def bench_ranges(args, rank, world, local, dev):
+    """Config 4: 1M key txns x 4 keys against 100k Range-domain commands plus a 1M-txn
+    CommandsForKey history (SNAPSHOT): keyDeps from the CFK and rangeDeps from the interval probe
+    (SearchableRangeList / mapReduceRangesInternal), merged per request. The store has range
+    commands, so the general fused kernel (k_resolve: K1 + K4 + K2) runs every request. With N GPUs,
+    N independent replicas."""
+    s = args.scale
+    w = synth.config4(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_ranges=max(1, int(100_000 * s)),
+                      n_hist_txns=int(1_000_000 * s), seed=0xACC0D004 + rank)
+    store = native.DeviceCommandStore(device=local, slices=w.slices)
+    store.load(w)
+    qdev, keep = native.device_queries(w.queries, dev)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    elapsed, all_stats = _timed_steps(args, world, dev, lambda: store.deps_batch_device(qdev, sp)[1])
+    stats = all_stats[-1]
+    ms = np.mean([st["ms_stage"] for st in all_stats], axis=0)
+    pairs = _sum_over_ranks(world, dev, w.queries.n_probes)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    heads = sum(stats["n_keys"])
+    out_bytes = 8 * heads + 4 * (heads + sum(stats["n_pairs"])) + 4 * sum(stats["n_unique"])
+    n_rent = int(w.cmds.range_off[-1])
+    # SURVEY §8(d) config 4: interval table once (16 B each) + 40 B per query + output
+    alg = 16 * n_rent + 40 * len(w.queries) + out_bytes
+    achieved = alg / (ms[0] / 1000.0) / 1e9 if ms[0] > 0 else 0.0
+    traffic, src = measured_traffic(["k_resolve"])
+    res = {
+        "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "config4: %d txns x 4 keys vs %d range commands + %d-entry CommandsForKey history, "
+                               "SNAPSHOT%s" % (len(w.queries), len(w.cmds.txn), w.cfk.n_entries,
+                                               ", one replica per GPU" if world > 1 else ""),
+                   "txns_per_step": len(w.queries) * world, "txn_key_pairs_per_step": pairs,
+                   "parallelism": "replicas x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_resolve", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+                     "algorithmic_bytes_per_launch": alg, "launch_ms": float(ms[0])},
+        "stages_ms": {STAGES[i]: round(float(ms[i]), 4) for i in range(7)},
+        "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    store.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_sequential(args, rank, world, local, dev):
+    """Config 1: 10k txns x 4 keys over 1k keys, one CommandStore, SEQUENTIAL PreAccept (each txn
+    inserted as PREACCEPTED before its deps). SEQUENTIAL runs through the host API: a step is one
+    ad_deps_batch call on a fresh store -- host arrays in and out, snapshot ingest (the batch's own
+    PreAccepts) and PCIe included, so this line is latency, not the device-resident throughput of
+    configs 2/4."""
+    w = synth.config1(seed=0xACC0D001 + rank)
+
+    def step():
+        st = native.DeviceCommandStore(device=local)
+        try:
+            st.load(w)
+            return st.calculate_partial_deps(w.queries, w.flags).stats
+        finally:
+            st.close()
+    elapsed, all_stats = _timed_steps(args, world, dev, step)
+    pairs = _sum_over_ranks(world, dev, w.queries.n_probes)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    stats = all_stats[-1]
+    res = {
+        "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "config1: 10000 txns x 4 keys over 1000 keys, SEQUENTIAL PreAccept, host API "
+                               "(ingest + PCIe + device per step)", "txns_per_step": len(w.queries) * world,
+                   "txn_key_pairs_per_step": pairs, "parallelism": "replicas x%d" % world},
+        "device_ms": stats["ms_device"], "ingest_ms": stats["ms_ingest"],
+        "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        t0 = time.perf_counter()
+        reps = 0
+        while reps == 0 or time.perf_counter() - t0 < args.cpu_budget / 3:
+            pyoracle.resolve(w)
+            reps += 1
+        t = time.perf_counter() - t0
+        res["cpu_baseline"] = dict(value=w.queries.n_probes * reps / t, unit="txn-key pairs/s", cores=1, kind="port",
+                                   sample="whole config-1 batch x%d (%.1f s), refcpu SEQUENTIAL, 1 thread" % (reps, t))
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,8 +334,9 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests / dry runs)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 5),
-                    help="2: BASELINE config 2 (the headline line, default); 5: execution levels (K5)")
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 4, 5),
+                    help="2: BASELINE config 2 (the headline line, default); 1: SEQUENTIAL PreAccept batch "
+                         "(host API); 4: range transactions; 5: execution levels (K5)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -224,6 +351,10 @@ def main():
 
     if args.config == 5:
         return bench_levels(args, rank, world, local, dev)
+    if args.config == 4:
+        return bench_ranges(args, rank, world, local, dev)
+    if args.config == 1:
+        return bench_sequential(args, rank, world, local, dev)
 
     s = args.scale
     t0 = time.time()

@@ -184,7 +184,7 @@ struct ad_ctx {
     DevSnapshot ds{};
     DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_krec, d_khash, d_kent, d_cand, d_cwr, d_ent, d_w;
     DevBuf d_lvl[NCLASS][MAX_LEVELS];
-    DevBuf d_rstart, d_rend, d_rtxw, d_rrid;
+    DevBuf d_rstart, d_rend, d_rtxw, d_rrid, d_cell_E, d_cell_off, d_cell_ent;
     DevBuf d_rlvl[NCLASS][MAX_LEVELS];
     DevBuf d_rb_s, d_rb_e, d_rb_e0, d_rb_e1, d_rb_wm, d_rb_rid, d_slices_s, d_slices_e;
     DevBuf d_dict_lsb_raw, d_rt_start, d_rt_end;   // raw ids and range table (multi-GPU export)
@@ -196,7 +196,7 @@ struct ad_ctx {
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
     DevBuf arena, rarena;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, p_slot, q_rec;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, p_slot, q_rec, p_cell;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
@@ -429,6 +429,8 @@ static int build_snapshot(ad_ctx* c)
 
     // ---- 3. range commands: (range, command) entries sorted by (start, end, txnId); range table
     struct REnt { int64_t s, e; uint32_t txw; uint32_t rid; };
+    std::vector<int64_t> cell_E;
+    bool cell_ok = false;
     std::vector<REnt> rent;
     for (uint64_t i = 0; i < ncmd; ++i)
     {
@@ -478,6 +480,56 @@ static int build_snapshot(ad_ctx* c)
             (rc = upload(c, c->d_rb_e0, c->rb.e0)) || (rc = upload(c, c->d_rb_e1, c->rb.e1)) || (rc = upload(c, c->d_rb_wm, wm_rank)) ||
             (rc = upload(c, c->d_rb_rid, rb_rid)))
             return rc;
+
+        // Stabbing index of the range entries (the role of SearchableRangeList /
+        // CheckpointIntervalArray, CheckpointIntervalArray.java:101-249): the distinct endpoints cut
+        // the key line into cells; cell(x) = #endpoints < x (EndInclusive) or <= x (StartInclusive),
+        // and every entry covers a contiguous run of cells [cell(start) + 1, cell(end)], with
+        // `cell` the endpoint's index. Each cell lists the (range id, txw) of the entries covering
+        // it, in entry order = (Range.compare, TxnId) order. Skipped when the total coverage is
+        // too large (deeply nested ranges): the max-end tree then serves every probe.
+        cell_E.clear();
+        cell_ok = false;
+        if (!rent.empty())
+        {
+            for (auto& r : rent) { cell_E.push_back(r.s); cell_E.push_back(r.e); }
+            std::sort(cell_E.begin(), cell_E.end());
+            cell_E.erase(std::unique(cell_E.begin(), cell_E.end()), cell_E.end());
+            const size_t m = cell_E.size();
+            auto idx = [&](int64_t v) { return (size_t)(std::lower_bound(cell_E.begin(), cell_E.end(), v) - cell_E.begin()); };
+            std::vector<uint64_t> cnt(m + 2, 0);
+            uint64_t total = 0;
+            std::vector<std::pair<uint32_t, uint32_t>> span(rent.size());
+            for (size_t i = 0; i < rent.size(); ++i)
+            {
+                const uint32_t a = (uint32_t)idx(rent[i].s) + 1, b = (uint32_t)idx(rent[i].e);
+                span[i] = {a, b};
+                if (b >= a) { cnt[a] += 1; cnt[b + 1] -= 1; total += b - a + 1; }
+            }
+            uint64_t budget = std::max<uint64_t>(64ull << 20, 32 * (uint64_t)rent.size());
+            if (const char* e = getenv("AD_CELL_BUDGET")) budget = strtoull(e, nullptr, 10);   // tests: force the tree
+            if (total <= budget && total < (1ull << 32))
+            {
+                std::vector<uint32_t> off(m + 2, 0);
+                uint64_t run = 0, acc = 0;
+                for (size_t cl = 0; cl <= m; ++cl)
+                {
+                    run += cnt[cl];
+                    off[cl] = (uint32_t)acc;
+                    acc += run;
+                }
+                off[m + 1] = (uint32_t)acc;
+                std::vector<uint64_t> ents(std::max<uint64_t>(acc, 1));
+                std::vector<uint32_t> cur(off.begin(), off.end());
+                for (size_t i = 0; i < rent.size(); ++i)
+                    for (uint32_t cl = span[i].first; cl <= span[i].second && span[i].second >= span[i].first; ++cl)
+                        ents[cur[cl]++] = ((uint64_t)rent[i].rid << 32) | rent[i].txw;
+                if ((rc = upload(c, c->d_cell_E, cell_E)) || (rc = upload(c, c->d_cell_off, off)) ||
+                    (rc = upload(c, c->d_cell_ent, ents)))
+                    return rc;
+                cell_ok = true;
+            }
+        }
     }
 
     // ---- 4. upload CFK + dictionary, build the trees
@@ -556,7 +608,14 @@ static int build_snapshot(ad_ctx* c)
     {
         uint64_t h = key_hash(K.keys[k]) & (hcap - 1);
         while (khash[h].idx != KEY_EMPTY) h = (h + 1) & (hcap - 1);
-        khash[h] = KeySlot{K.keys[k], (uint32_t)k, 0};
+        uint32_t kcell = NO_CELL;
+        if (cell_ok)
+        {
+            const int64_t x = K.keys[k];
+            kcell = (uint32_t)(c->cfg.range_start_inclusive ? std::upper_bound(cell_E.begin(), cell_E.end(), x) - cell_E.begin()
+                                                             : std::lower_bound(cell_E.begin(), cell_E.end(), x) - cell_E.begin());
+        }
+        khash[h] = KeySlot{K.keys[k], (uint32_t)k, kcell};
         KeyEntry& ke = kent[h];
         ke.key = K.keys[k];
         ke.idx = (uint32_t)k;
@@ -618,6 +677,10 @@ static int build_snapshot(ad_ctx* c)
             s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
         }
     s.n_rent = rent.size();
+    s.n_cell_E = cell_ok ? cell_E.size() : 0;
+    s.cell_E = cell_ok ? c->d_cell_E.as<int64_t>() : nullptr;
+    s.cell_off = cell_ok ? c->d_cell_off.as<uint32_t>() : nullptr;
+    s.cell_ent = cell_ok ? c->d_cell_ent.as<uint64_t>() : nullptr;
     s.r_start = c->d_rstart.as<int64_t>();
     s.r_end = c->d_rend.as<int64_t>();
     s.r_txw = c->d_rtxw.as<uint32_t>();
@@ -811,14 +874,14 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
         !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
-        !ens<uint32_t>(c->p_slot, np) || !ens<uint4>(c->q_rec, n) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
+        !ens<uint32_t>(c->p_slot, np) || !ens<uint4>(c->q_rec, n) || !ens<uint32_t>(c->p_cell, np) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
         !ens<uint32_t>(c->deferred2, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64))
         return c->fail(AD_E_NOMEM, "batch buffers");
     b.p_slot = c->p_slot.as<uint32_t>();
     b.q_rec = c->q_rec.as<uint4>();
+    b.p_cell = c->p_cell.as<uint32_t>();
     b.deferred1 = c->deferred1.as<uint32_t>();
     b.deferred2 = c->deferred2.as<uint32_t>();
-    if (const char* e = getenv("AD_DBG")) b.dbg = (uint32_t)atoi(e);
     b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>(); b.bsum = c->bsum.as<uint64_t>();
     b.t_reg = c->t_reg.as<uint64_t>(); b.ctl = c->ctl.as<BatchCtl>(); b.deferred = c->deferred.as<uint32_t>();
     if (split_only && !bind_split(c->split, b, n, np, false)) return c->fail(AD_E_NOMEM, "split buffers");

@@ -92,8 +92,9 @@ constexpr uint32_t NO_KEY = 0xFFFFFFFFu;
 struct KeySlot {
     int64_t key;
     uint32_t idx;       // KEY_EMPTY = free slot
-    uint32_t pad;
+    uint32_t cell;      // the key's cell in the range stabbing index (NO_CELL: none)
 };
+constexpr uint32_t NO_CELL = 0xFFFFFFFFu;
 constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 
 // Fused path: one 128-byte hash slot (= one cache line) per key carries the key's KeyRec and
@@ -165,6 +166,11 @@ struct DevSnapshot {
     const int64_t*  rlvl[NCLASS][MAX_LEVELS];  // max end per 64^l block
     uint64_t rlvl_n[MAX_LEVELS];
     int n_rlevels;
+    // stabbing index of the range entries (null when not built): endpoints, per-cell lists
+    uint64_t n_cell_E;
+    const int64_t*  cell_E;        // distinct endpoints, ascending
+    const uint32_t* cell_off;      // [n_cell_E + 2]
+    const uint64_t* cell_ent;      // rid << 32 | txw, per cell in (Range.compare, TxnId) order
     // redundant-before (disjoint, ascending)
     uint64_t n_rb;
     const int64_t*  rb_start;

@@ -40,6 +40,7 @@ struct BatchBufs {
     uint32_t* p_txn; uint4* p_rec;
     uint32_t* p_slot;                // fused path: KeyEntry slot of each probe | in-slice << 31 (k_prepare)
     uint4* q_rec;                    // fused path: per request {key_off lo, hi, np | cls << 16 | flags, 0} (k_prepare)
+    uint32_t* p_cell;                // fused path: range stabbing-index cell of each probe (NO_CELL: none)
     // K1
     uint32_t* arena; uint32_t* p_off; uint32_t* p_c0; uint32_t* p_c1;
     // K4
@@ -58,7 +59,6 @@ struct BatchBufs {
     const unsigned long long* req_count;
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
     BatchCtl* ctl;
-    uint32_t dbg;                    // timing experiments only (AD_DBG): 0 = normal
 };
 
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);

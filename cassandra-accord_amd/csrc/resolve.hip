@@ -473,8 +473,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         // on): the emissions are exactly two precomputed contiguous lists (KeyEntry, common.hpp);
         // otherwise the class max tree prunes byId[lo, end) (output-sensitive descent).
         const bool newest = has_cfk && s.elide && tail && wtail;
-        if (b.dbg == 3) break;
-        if (ballot(newest) && b.dbg != 2)
+        if (ballot(newest))
         {
             const uint32_t n1 = newest ? cand_hi - cand_lo : 0u;
             const uint32_t n2 = !newest ? 0u : (cls == 0 ? (last_w_txn != 0 ? 1u : 0u) : cwr_hi - cwr_tail);
@@ -523,7 +522,32 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
                 }
             }
         }
-        if (s.n_rent)
+        const uint32_t pcell = gact ? b.p_cell[k0 + g] : NO_CELL;
+        if (s.n_rent && s.cell_off)
+        {
+            // stabbing index: the key's cell lists every range entry containing it, in (range,
+            // txnId) order; keep those the reference's filter keeps (InMemoryCommandStore.java:906-956)
+            const bool ract = gact && in_slice && pcell != NO_CELL;
+            const uint32_t clo = ract ? s.cell_off[pcell] : 0u, chi = ract ? s.cell_off[pcell + 1] : 0u;
+            const uint32_t nn = chi - clo;
+            for (uint32_t o = 0; ballot(o < nn); o += 8)
+            {
+                const uint32_t i = o + j;
+                const uint64_t ce = i < nn ? s.cell_ent[clo + i] : 0ull;
+                const uint32_t txw = (uint32_t)ce, r = txw & RANK_MASK, kd = txw >> RANK_BITS;
+                const bool want = i < nn && r < S && ((kinds >> kd) & 1) && r != self;
+                const uint32_t w1 = want ? 1u : 0u;
+                const uint32_t inc = grp_incl_scan(w1);
+                const uint32_t tot = __shfl(inc, (lane & ~7u) | 7u, 64);
+                if (rc + tot <= FCAPR)
+                {
+                    if (want) L.rs[g][rc + inc - 1] = (ce & 0xFFFFFFFF00000000ull) | r;
+                }
+                else ovf = true;
+                rc += tot;
+            }
+        }
+        else if (s.n_rent)
         {
             const bool ract = gact && in_slice;
             const uint64_t rhi = grp_lower_bound(ract, 0, s.n_rent, [&](uint64_t i) { return s.r_start[i]; },
@@ -569,7 +593,6 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         st3(psn, kqn);
         pf3 = true;
 
-        if (b.dbg == 1) break;
         // any key overflowing its staging -> defer the whole request to the split kernels
         if (ballot(ovf))
         {
@@ -723,20 +746,13 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
             const bool uniq = valid && (lane == 0 || prevk != key);
             const uint64_t um = ballot(uniq);
             const uint32_t UPn = __popcll(um);
-            // compact the unique pairs to lanes 0..UPn-1
-            uint32_t src = 0;
-            {
-                // lane i takes the i-th unique pair: find its source lane by scanning the mask
-                uint64_t mm = um;
-                for (uint32_t i = 0; i < 64; ++i)
-                {
-                    if (!mm) break;
-                    const uint32_t bpos = __ffsll((unsigned long long)mm) - 1;
-                    if (lane == i) src = bpos;
-                    mm &= mm - 1;
-                }
-            }
-            const uint64_t upair = __shfl(key, src, 64);
+            // compact the unique pairs to lanes 0..UPn-1 through LDS (the staging is consumed)
+            wave_lds_sync();
+            uint64_t* cbuf = &L.rs[0][0];
+            if (uniq) cbuf[mbcnt(um)] = key;
+            wave_lds_sync();
+            const uint64_t upair = lane < UPn ? cbuf[lane] : ~0ull;
+            wave_lds_sync();
             const bool uplive = lane < UPn;
             const uint32_t rid = (uint32_t)(upair >> 32), rk = (uint32_t)upair;
             const uint32_t prid = __shfl_up(rid, 1, 64);
@@ -798,6 +814,21 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
 // Keeping the dependent key -> slot probing here leaves the per-request kernels one load shorter.
 constexpr uint32_t PREP_UNROLL = 8;     // keys whose probes are issued together
 
+// cell of key x in the range stabbing index: #endpoints < x (EndInclusive) or <= x (StartInclusive)
+__device__ __forceinline__ uint32_t cell_search(const DevSnapshot& s, int64_t x)
+{
+    if (!s.cell_off) return NO_CELL;
+    uint64_t lo = 0, hi = s.n_cell_E;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        const int64_t v = s.cell_E[mid];
+        if (s.start_inclusive ? v <= x : v < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return (uint32_t)lo;
+}
+
 __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -835,9 +866,11 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
                 in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key[u]);
             h[u] = key_hash(key[u]) & s.khash_mask;
             if (!on[u]) continue;
+            if (!in_slice) b.p_cell[c0 + u] = NO_CELL;
             if (!in_slice || !s.n_keys)
             {
                 b.p_slot[c0 + u] = SLOT_NONE;
+                if (in_slice) b.p_cell[c0 + u] = cell_search(s, key[u]);
                 on[u] = false;
             }
         }
@@ -852,18 +885,22 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
             uint64_t hh = h[u];
             uint4 qq = q[u];
             uint32_t slot = SLOT_NONE;
+            uint32_t cell = NO_CELL;
             while (true)
             {
                 if (qq.z == KEY_EMPTY) break;
                 if ((int64_t)(((uint64_t)qq.y << 32) | qq.x) == key[u])
                 {
                     slot = (uint32_t)hh;
+                    cell = qq.w;
                     break;
                 }
                 hh = (hh + 1) & s.khash_mask;
                 qq = reinterpret_cast<const uint4*>(s.khash + hh)[0];
             }
             b.p_slot[c0 + u] = slot | SLOT_IN_SLICE;
+            // the key's stabbing-index cell: from its KeySlot, else by search (keys without a CFK)
+            b.p_cell[c0 + u] = slot != SLOT_NONE ? cell : cell_search(s, key[u]);
         }
     }
 }

@@ -90,6 +90,14 @@ def test_config4_scaled(oracle):
     assert got.pair_count(A.AD_MAP_RANGE) > 0
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_range_tree_fallback(oracle, seed, monkeypatch):
+    # no stabbing index (coverage budget 0): every range probe takes the max-end tree descent
+    monkeypatch.setenv("AD_CELL_BUDGET", "0")
+    _compare(synth.random_small(700 + seed, n_range_cmds=40, start_inclusive=(seed % 2 == 1)), oracle)
+    _compare(synth.config4(n_txns=1000, n_keys=5000, n_ranges=800, n_hist_txns=4000, seed=seed), oracle, paths=(0,))
+
+
 def test_big_requests(oracle):
     # a hot key with thousands of live entries -> per-probe outputs beyond the LDS staging
     w = synth.config2(n_txns=200, n_keys=50, n_hist_entries=40000, keys_per_txn=8, tail_unapplied=3000,
