@@ -16,7 +16,7 @@ import numpy as np
 from . import _abi as A
 from .model import DepsMap, PartialDepsBatch, Tids
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaccord_deps.so")
+LIB_PATH = os.environ.get("ACCORD_DEPS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libaccord_deps.so")
 
 EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error", "ad_cfk_load",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",

@@ -602,8 +602,7 @@ static int build_snapshot(ad_ctx* c)
             last_w_txn[k] = has_w ? (tmp[tail].y & RANK_MASK) : 0u;
         }
     });
-    std::vector<KeyEntry> kent(hcap);
-    for (auto& e : kent) { e = KeyEntry{}; e.idx = KEY_EMPTY; }
+    std::vector<KeyEntry> kent(std::max<uint64_t>(nk, 1));
     for (uint64_t k = 0; k < nk; ++k)
     {
         uint64_t h = key_hash(K.keys[k]) & (hcap - 1);
@@ -616,13 +615,11 @@ static int build_snapshot(ad_ctx* c)
                                                              : std::lower_bound(cell_E.begin(), cell_E.end(), x) - cell_E.begin());
         }
         khash[h] = KeySlot{K.keys[k], (uint32_t)k, kcell};
-        KeyEntry& ke = kent[h];
-        ke.key = K.keys[k];
-        ke.idx = (uint32_t)k;
+        KeyEntry& ke = kent[k];
         ke.last_w_txn = last_w_txn[k];
         ke.last_txn = krec[k].last_txn;
         ke.last_wexec = krec[k].last_wexec;
-        ke.rec = krec[k];
+        ke.pad = 0;
         for (int cl = 0; cl < NCLASS; ++cl)
         {
             ke.cl[cl].cand_lo = cand_off[cl * nk + k];

@@ -105,25 +105,21 @@ constexpr uint32_t KEY_EMPTY = 0xFFFFFFFFu;
 //   cand_c  and  { Ws: the last committed Write | RsOrWs/AnyGloballyVisible: cwr[cwr_tail, cwr_hi) }
 // (minus the request's own id): the mapReduceActive loop (CommandsForKey.java:930-950) with
 // end = byId.length and M = the last committed Write's executeAt.
-// Quarters (16 B): q0 key/idx (the hash probe), q1 the newest test + Ws emission, q2+c the lists of
-// witness class c (the lean kernel loads q1 and one class quarter), q5/q6 the KeyRec of the tree path.
+// Indexed by key index (dense: 64 B per CommandsForKey, so hot entries pack into the caches):
+// q0 the newest test + the Ws emission, q1+c the lists of witness class c. The lean kernel loads
+// q0 and one class quarter; the tree path's KeyRec is the separate krec[] array.
 struct KeyClassLists {
     uint32_t cand_lo, cand_hi;     // never-elided entries of class c: cand[cand_lo, cand_hi)
     uint32_t cwr_tail, cwr_hi;     // committed R/W from the last committed Write on: cwr[cwr_tail, cwr_hi)
 };
-struct alignas(128) KeyEntry {
-    int64_t key;                   // q0
-    uint32_t idx;                  //    KEY_EMPTY = free slot
-    uint32_t pad0;
-    uint32_t last_txn;             // q1.x  rank of byId's last txnId (0 if empty)
-    uint32_t last_wexec;           // q1.y  executeAt rank of the last committed Write (0 if none)
-    uint32_t last_w_txn;           // q1.z  txn rank of that Write (0 if none)
-    uint32_t pad1;
-    KeyClassLists cl[NCLASS];      // q2..q4
-    KeyRec rec;                    // q5, q6
-    uint32_t pad2[4];              // q7
+struct alignas(64) KeyEntry {
+    uint32_t last_txn;             // q0.x  rank of byId's last txnId (0 if empty)
+    uint32_t last_wexec;           // q0.y  executeAt rank of the last committed Write (0 if none)
+    uint32_t last_w_txn;           // q0.z  txn rank of that Write (0 if none)
+    uint32_t pad;
+    KeyClassLists cl[NCLASS];      // q1..q3
 };
-static_assert(sizeof(KeyEntry) == 128, "KeyEntry is one cache line");
+static_assert(sizeof(KeyEntry) == 64, "KeyEntry is half a cache line");
 
 __host__ __device__ inline uint64_t key_hash(int64_t k)
 {
@@ -147,7 +143,7 @@ struct DevSnapshot {
     const int64_t*  keys;          // [n_keys]
     const KeyRec*   krec;          // [n_keys]
     const KeySlot*  khash;         // [khash_mask + 1]
-    const KeyEntry* kent;          // [khash_mask + 1] same slots, KeyRec + list bounds inline (fused kernel)
+    const KeyEntry* kent;          // [n_keys] newest-test fields + list bounds (fused kernels)
     const uint32_t* cand;          // never-elided entries per key and class: txw (rank | kind << 29)
     const uint32_t* cwr;           // committed Read/Write entries per key by executeAt: txw
     uint64_t khash_mask;

@@ -144,8 +144,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     auto loadC = [&](uint32_t pslot, uint32_t cls, uint4& q1, uint4& qc) {
         const uint32_t sl = slot_of(pslot);
         const uint4* e = reinterpret_cast<const uint4*>(s.kent + (sl != SLOT_NONE ? sl : 0u));
-        q1 = e[1];
-        qc = e[2 + cls];
+        q1 = e[0];
+        qc = e[1 + cls];
     };
 
     const uint64_t it0 = uniform64((uint64_t)blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));

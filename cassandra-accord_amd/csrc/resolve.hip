@@ -300,7 +300,10 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     };
     auto st3 = [&](uint32_t psi, uint4& kqo) {
         const uint32_t sl = psi & ~SLOT_IN_SLICE;
-        kqo = (sl != SLOT_NONE && j < 7) ? reinterpret_cast<const uint4*>(s.kent + sl)[j] : make_uint4(0, 0, 0, 0);
+        // lanes 0-3: the KeyEntry (64 B); lanes 4-5: the KeyRec (32 B)
+        kqo = make_uint4(0, 0, 0, 0);
+        if (sl != SLOT_NONE && j < 4) kqo = reinterpret_cast<const uint4*>(s.kent + sl)[j];
+        if (sl != SLOT_NONE && (j == 4 || j == 5)) kqo = reinterpret_cast<const uint4*>(s.krec + sl)[j - 4];
     };
     const uint64_t t0 = uniform64((uint64_t)blockIdx.x * FWAVES + (threadIdx.x >> 6));
     uint64_t k0c, k0n;
@@ -353,7 +356,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         const int64_t epoch = (int64_t)(em >> 15);
         const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
 
-        // ---- per key g (8-lane group g < np): the 128-byte KeyEntry of the key's CommandsForKey,
+        // ---- per key g (8-lane group g < np): the KeyEntry and KeyRec of the key's CommandsForKey,
         // found by k_prepare (lane j of the group loads quarter j)
         const bool gact = g < np;
         const uint32_t gb = lane & ~7u;
@@ -363,19 +366,18 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         const uint32_t slot = pslot & ~SLOT_IN_SLICE;
         if (gact && j == 0) L.key[g] = key;
         uint4 kq = kqc;
-        const uint32_t ki = slot != SLOT_NONE ? __shfl(kq.z, gb, 64) : NO_KEY;
-        if (ki == NO_KEY) kq = make_uint4(0, 0, 0, 0);
-        KeyRec kr;     // KeyEntry quarters (common.hpp): q1 newest fields, q2+cls lists, q5/q6 KeyRec
-        kr.seg_lo = __shfl(kq.x, gb + 5, 64);
-        kr.seg_hi = __shfl(kq.y, gb + 5, 64);
-        kr.w_lo = __shfl(kq.z, gb + 5, 64);
-        kr.w_hi = __shfl(kq.w, gb + 5, 64);
-        kr.last_txn = __shfl(kq.x, gb + 6, 64);
-        kr.last_wexec = __shfl(kq.y, gb + 6, 64);
-        kr.pruned = __shfl(kq.z, gb + 6, 64);
-        kr.maw = (int32_t)__shfl(kq.w, gb + 6, 64);
-        const uint32_t last_w_txn = __shfl(kq.z, gb + 1, 64);
-        const uint32_t cq = gb + 2 + (uint32_t)cls;
+        const uint32_t ki = slot != SLOT_NONE ? slot : NO_KEY;
+        KeyRec kr;     // lanes 4/5: KeyRec; lane 0: newest fields; lane 1 + cls: the class lists
+        kr.seg_lo = __shfl(kq.x, gb + 4, 64);
+        kr.seg_hi = __shfl(kq.y, gb + 4, 64);
+        kr.w_lo = __shfl(kq.z, gb + 4, 64);
+        kr.w_hi = __shfl(kq.w, gb + 4, 64);
+        kr.last_txn = __shfl(kq.x, gb + 5, 64);
+        kr.last_wexec = __shfl(kq.y, gb + 5, 64);
+        kr.pruned = __shfl(kq.z, gb + 5, 64);
+        kr.maw = (int32_t)__shfl(kq.w, gb + 5, 64);
+        const uint32_t last_w_txn = __shfl(kq.z, gb, 64);
+        const uint32_t cq = gb + 1 + (uint32_t)cls;
         const uint32_t cand_lo = __shfl(kq.x, cq, 64), cand_hi = __shfl(kq.y, cq, 64);
         const uint32_t cwr_tail = __shfl(kq.z, cq, 64), cwr_hi = __shfl(kq.w, cq, 64);
         const bool has_cfk = gact && ki != NO_KEY;
@@ -809,8 +811,8 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
 
 // Per-request preparation, one thread per request (PreAccept.java:251-261 and the key lookups of
 // InMemoryCommandStore.mapReduceForKey, :280): the request record the lean kernel reads instead
-// of the raw ids, and the KeyEntry slot of every (request, key) probe (open addressing, linear
-// probing in the 16-byte KeySlot table, which shares the KeyEntry table's hash and capacity).
+// of the raw ids, and the key index (KeyEntry / krec position) of every (request, key) probe (open
+// addressing, linear probing in the 16-byte KeySlot table).
 // Keeping the dependent key -> slot probing here leaves the per-request kernels one load shorter.
 constexpr uint32_t PREP_UNROLL = 8;     // keys whose probes are issued together
 
@@ -891,7 +893,7 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
                 if (qq.z == KEY_EMPTY) break;
                 if ((int64_t)(((uint64_t)qq.y << 32) | qq.x) == key[u])
                 {
-                    slot = (uint32_t)hh;
+                    slot = qq.z;              // the key's index: KeyEntry / krec position
                     cell = qq.w;
                     break;
                 }
