@@ -859,9 +859,10 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipStreamSynchronize(st));
     }
     const bool split_only = c->cfg.path == 1;
-    // the lean kernel covers stores without range commands / redundant-before entries, elision on
-    const bool lean = !split_only && np > 0 && c->ds.n_rent == 0 && c->ds.n_rb == 0 && c->ds.elide &&
-                      getenv("AD_NO_LEAN") == nullptr;
+    // the lean kernel covers stores without redundant-before entries, elision on
+    // (range commands only with their stabbing index)
+    const bool lean = !split_only && np > 0 && (c->ds.n_rent == 0 || c->ds.cell_off != nullptr) && c->ds.n_rb == 0 &&
+                      c->ds.elide && getenv("AD_NO_LEAN") == nullptr;
     BatchBufs b{};
     b.n_txns = n;
     b.n_probes = np;

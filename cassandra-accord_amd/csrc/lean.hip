@@ -41,6 +41,22 @@ __device__ __forceinline__ void seg_bitonic(uint32_t& key)
         }
 }
 
+template <uint32_t K, uint32_t LPR>
+__device__ __forceinline__ void seg_bitonic64(uint64_t& key)
+{
+    const uint32_t l = lane_id() & (LPR - 1);
+#pragma unroll
+    for (uint32_t k = 2; k <= K; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1)
+        {
+            const uint64_t ok = __shfl_xor(key, (int)j, 64);
+            const bool up = (l & k) == 0;
+            const bool lower = (l & j) == 0;
+            key = (lower == up) ? min(key, ok) : max(key, ok);
+        }
+}
+
 struct LeanChunk {
     uint64_t cur = 0, end = 0;
     // wave-uniform bump allocation from the region arena
@@ -72,8 +88,22 @@ struct LeanLists {
     unsigned long long* out_real;
 };
 
-// RPW requests per wave (2: 32 lanes each, up to 32 raw emissions; 1: 64 lanes, up to 64)
-template <uint32_t RPW>
+// segmented prefix helpers over the 8 key lanes of each request segment
+__device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
+{
+#pragma unroll
+    for (uint32_t d = 1; d < 8; d <<= 1)
+    {
+        const uint32_t t = __shfl_up(v, d, 8);
+        if ((hl & 7) >= d) v += t;
+    }
+    return v;
+}
+
+// RPW requests per wave (2: 32 lanes each, up to 32 raw emissions; 1: 64 lanes, up to 64).
+// RNG: the store has range commands (with a stabbing index): each request also gets its
+// rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
+template <uint32_t RPW, bool RNG>
 __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s, BatchBufs b, LeanLists io)
 {
     constexpr uint32_t LPR = 64 / RPW;                       // lanes per request
@@ -133,12 +163,29 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         return q;
     };
     // keys and raw slots (the in-slice bit is stripped where the slot is used)
-    auto loadB = [&](const Req& q, int64_t& key, uint32_t& pslot) {
+    auto loadB = [&](const Req& q, int64_t& key, uint32_t& pslot, uint32_t& pcell) {
         const bool on = q.act && !q.defer && hl < q.np;
         const uint64_t i = on ? q.k0 + hl : 0;
         key = b.q_keys[i];
         pslot = b.p_slot[i];
         if (!on) pslot = SLOT_NONE;
+        pcell = NO_CELL;
+        if (RNG)
+        {
+            pcell = b.p_cell[i];
+            if (!on) pcell = NO_CELL;
+        }
+    };
+    // the key's cell bounds in the range stabbing index
+    auto loadR = [&](uint32_t pcell, uint2& cb) {
+        cb = make_uint2(0, 0);
+        if (RNG)
+        {
+            const uint32_t c = pcell != NO_CELL ? pcell : 0u;
+            cb.x = s.cell_off[c];
+            cb.y = s.cell_off[c + 1];
+            if (pcell == NO_CELL) cb = make_uint2(0, 0);
+        }
     };
     auto slot_of = [](uint32_t pslot) { return pslot & ~SLOT_IN_SLICE; };
     auto loadC = [&](uint32_t pslot, uint32_t cls, uint4& q1, uint4& qc) {
@@ -152,10 +199,12 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     uint32_t tc = req_of(it0);
     Req qc = derive(tc, loadA(tc));
     int64_t keyc;
-    uint32_t slotc;
-    loadB(qc, keyc, slotc);
+    uint32_t slotc, cellc;
+    loadB(qc, keyc, slotc, cellc);
     uint4 q1c, qlc;
     loadC(slotc, qc.cls, q1c, qlc);
+    uint2 cbc;
+    loadR(cellc, cbc);
     uint32_t tN = req_of(it0 + nw);
     Raw rN = loadA(tN);
 
@@ -166,8 +215,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         tN = req_of(it + 2 * nw);
         rN = loadA(tN);
         int64_t keyn;
-        uint32_t slotn;
-        loadB(qn, keyn, slotn);
+        uint32_t slotn, celln;
+        loadB(qn, keyn, slotn, celln);
 
         // ---- current item: per key p = hl < np, newest test and emission counts
         bool act = qc.act;
@@ -190,7 +239,12 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         }
         const uint32_t start = inc - nn;
         const uint32_t T = __shfl(inc, sb | 7u, 64);
-        defer = defer || seg(ballot(kact && !newest)) != 0 || T > LPR;
+        // range raw emissions: the entries of each key's cell
+        const uint32_t rn = (RNG && kact) ? cbc.y - cbc.x : 0u;
+        const uint32_t rinc = RNG ? key_lanes_incl_scan(rn, hl) : 0u;
+        const uint32_t rstart = rinc - rn;
+        const uint32_t TR = RNG ? __shfl(rinc, sb | 7u, 64) : 0u;
+        defer = defer || seg(ballot(kact && !newest)) != 0 || T > LPR || TR > LPR;
         {
             const uint64_t dm = ballot(act && defer && hl == 0);
             const uint32_t nd = __popcll(dm);
@@ -219,9 +273,28 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         const bool from_cand = i < a_n1;
         const uint32_t* lp = !live ? s.cand : (from_cand ? s.cand + (a_clo + i) : (cls != 0 ? s.cwr + (a_ct + (i - a_n1)) : s.cand));
         const uint32_t lv = *lp;
-        // the next item's KeyEntry quarters go out behind this item's list loads
+        // range elements (same round trip as the list loads)
+        uint32_t ar = 0;
+        uint64_t ce = 0;
+        bool rlive = false;
+        if (RNG)
+        {
+#pragma unroll
+            for (uint32_t p = 1; p < LEAN_MAXP; ++p)
+            {
+                const uint32_t sp = __shfl(rstart, sb | p, 64);
+                if (p < np && hl >= sp) ar = p;
+            }
+            const uint32_t rsrc = sb | ar;
+            const uint32_t ar_start = __shfl(rstart, rsrc, 64), ar_lo = __shfl(cbc.x, rsrc, 64);
+            rlive = act && hl < TR;
+            ce = s.cell_ent[rlive ? ar_lo + (hl - ar_start) : 0u];
+        }
+        // the next item's KeyEntry quarters (and cell bounds) go out behind this item's list loads
         uint4 q1n, qln;
         loadC(slotn, qn.cls, q1n, qln);
+        uint2 cbn;
+        loadR(celln, cbn);
 
         const uint32_t txw = !live ? 0u : ((from_cand || cls != 0) ? lv : (a_lw | (1u << RANK_BITS)));
         const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
@@ -318,35 +391,121 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
                 if (valid) ok2t[nk + kstart + pos_in_key] = (int32_t)ur;
             }
         }
-        if (act && hl == 0)
+        // ---- rangeDeps (m = 1): (range, txnId) pairs of the cells, STARTED_BEFORE (always, the
+        // request is newer than every id), kind witnessed; unique pairs in (Range.compare, TxnId) order
+        const uint32_t rtxw = (uint32_t)ce, rk = rtxw & RANK_MASK, rkd = rtxw >> RANK_BITS;
+        const bool rwant = RNG && rlive && ((CLASS_KINDS[cls] >> rkd) & 1) && rk != self;
+        const uint64_t rmb = ballot(rwant);
+        if (!RNG || rmb == 0)
         {
-            b.sz[3 * n + t] = 0;      // rangeDeps: no range commands / redundant entries on this path
-            b.sz[4 * n + t] = 0;
-            b.sz[5 * n + t] = 0;
+            if (act && hl == 0)
+            {
+                b.sz[3 * n + t] = 0;
+                b.sz[4 * n + t] = 0;
+                b.sz[5 * n + t] = 0;
+            }
+        }
+        else
+        {
+            const uint32_t kmaxr = RPW == 1 ? uniform(TR) : uniform(max(__shfl(TR, 0, 64), __shfl(TR, 32, 64)));
+            uint64_t pk = rwant ? ((ce & 0xFFFFFFFF00000000ull) | rk) : ~0ull;
+            if (kmaxr <= 8) seg_bitonic64<8, LPR>(pk);
+            else if (kmaxr <= 16) seg_bitonic64<16, LPR>(pk);
+            else if (kmaxr <= 32 || LPR == 32) seg_bitonic64<(LPR < 32 ? LPR : 32), LPR>(pk);
+            else seg_bitonic64<LPR, LPR>(pk);
+            const uint32_t totp = __popcll(seg(rmb));
+            const bool pv = hl < totp;
+            const uint64_t pprev = __shfl_up(pk, 1, LPR);
+            const bool pu = pv && (hl == 0 || pprev != pk);
+            const uint64_t pum = seg(ballot(pu));
+            const uint32_t UP = __popcll(pum);
+            // the unique pairs, compacted to the first UP lanes of the segment
+            const uint32_t dst = __popcll(pum & below);
+            uint64_t up = ~0ull;
+            {
+                // lane dst takes the pair of this lane (ds_permute pushes). Lanes without a unique
+                // pair push to the segment's last lane, which is read only when all LPR pairs are
+                // unique, i.e. when there are no such lanes
+                const uint32_t my = pu ? dst : LPR - 1;
+                const int addr = (int)((sb + my) << 2);
+                const uint32_t lo32 = __builtin_amdgcn_ds_permute(addr, (int)(uint32_t)pk);
+                const uint32_t hi32 = __builtin_amdgcn_ds_permute(addr, (int)(uint32_t)(pk >> 32));
+                if (hl < UP) up = ((uint64_t)hi32 << 32) | lo32;
+            }
+            const bool uplive = hl < UP;
+            const uint32_t rid = (uint32_t)(up >> 32), urk = (uint32_t)up;
+            const uint32_t prid = __shfl_up(rid, 1, LPR);
+            const bool gfirst = uplive && (hl == 0 || prid != rid);
+            const uint64_t gm = seg(ballot(gfirst));
+            const uint32_t nR = __popcll(gm);
+            // distinct txnIds of the pairs: sort (rank, pair index)
+            uint64_t k2 = uplive ? (((uint64_t)urk << 8) | hl) : ~0ull;
+            if (kmaxr <= 8) seg_bitonic64<8, LPR>(k2);
+            else if (kmaxr <= 16) seg_bitonic64<16, LPR>(k2);
+            else if (kmaxr <= 32 || LPR == 32) seg_bitonic64<(LPR < 32 ? LPR : 32), LPR>(k2);
+            else seg_bitonic64<LPR, LPR>(k2);
+            const uint64_t p2 = __shfl_up(k2, 1, LPR);
+            const bool v2 = hl < UP;
+            const bool uq2 = v2 && (hl == 0 || (uint32_t)(p2 >> 8) != (uint32_t)(k2 >> 8));
+            const uint64_t um2 = seg(ballot(uq2));
+            const uint32_t UR = __popcll(um2);
+            const uint32_t ur2 = __popcll(um2 & below) + (uq2 ? 1u : 0u) - 1u;
+            const uint64_t bytes = act && totp ? (((uint64_t)nR * 8 + (uint64_t)UR * 4 + (uint64_t)(nR + UP) * 4 + 7) & ~7ull) : 0;
+            const uint64_t bA = uniform64(__shfl(bytes, 0, 64));
+            const uint64_t bB = RPW == 1 ? 0 : uniform64(__shfl(bytes, 32, 64));
+            const uint64_t base = ralloc.take(b.ctl, bA + bB, reg_cap);
+            const uint64_t ro = h ? base + bA : base;
+            const bool fits = base + bA + bB <= reg_cap;
+            if (act && hl == 0)
+            {
+                b.sz[3 * n + t] = fits ? nR : 0;
+                b.sz[4 * n + t] = fits ? UR : 0;
+                b.sz[5 * n + t] = fits ? nR + UP : 0;
+                b.t_reg[(uint64_t)1 * n + t] = ro;
+            }
+            if (act && totp && fits)
+            {
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nR);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + UR);
+                if (gfirst)
+                {
+                    const uint32_t gi = __popcll(gm & below);
+                    const uint64_t later = gm & ~((2ull << hl) - 1) & (LPR == 64 ? ~0ull : 0xFFFFFFFFull);
+                    const uint32_t gend = later ? (uint32_t)(__ffsll((unsigned long long)later) - 1) : UP;
+                    okeys[gi] = (int64_t)rid;                          // range id (ad_range_table)
+                    ok2t[gi] = (int32_t)(nR + gend);
+                }
+                if (uq2) otx[ur2] = ((uint32_t)(k2 >> 8) - 1) >> 1;
+                if (v2) ok2t[nR + (uint32_t)(k2 & 0xFF)] = (int32_t)ur2;
+            }
         }
         qc = qn;
         keyc = keyn;
         slotc = slotn;
+        cellc = celln;
         q1c = q1n;
         qlc = qln;
+        cbc = cbn;
     }
     dflush();
 }
 
-template <uint32_t RPW>
+template <uint32_t RPW, bool RNG>
 static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, const LeanLists& io, hipStream_t st)
 {
     static int per_cu = 0;
     if (!per_cu)
     {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW>, 64 * LEAN_WAVES, 0) != hipSuccess || nb <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG>, 64 * LEAN_WAVES, 0) != hipSuccess ||
+            nb <= 0)
             nb = 2;
         per_cu = std::min(nb, 8);
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu));
-    k_resolve_lean<RPW><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, io);
+    k_resolve_lean<RPW, RNG><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, io);
     return hipGetLastError();
 }
 
@@ -357,10 +516,10 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     if (pass == 1)
     {
         LeanLists p1{nullptr, nullptr, b.deferred1, &b.ctl->n_deferred1, &b.ctl->n_real1};
-        return launch_lean<2>(s, b, p1, st);
+        return s.n_rent ? launch_lean<2, true>(s, b, p1, st) : launch_lean<2, false>(s, b, p1, st);
     }
     LeanLists p2{b.deferred1, &b.ctl->n_deferred1, b.deferred2, &b.ctl->n_deferred2, &b.ctl->n_real2};
-    return launch_lean<1>(s, b, p2, st);
+    return s.n_rent ? launch_lean<1, true>(s, b, p2, st) : launch_lean<1, false>(s, b, p2, st);
 }
 
 }  // namespace adx

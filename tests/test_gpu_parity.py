@@ -51,6 +51,22 @@ def test_random_small_lean_store(oracle, seed):
     _compare(w, oracle, paths=(0,))
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_random_small_lean_ranges(oracle, seed):
+    # range commands with their stabbing index, no redundant-before: the lean kernel also builds
+    # rangeDeps (multi-range commands, both range conventions, slices, erased ranges)
+    w = synth.random_small(800 + seed, n_range_cmds=10 + 6 * seed, n_redundant=0, accept_frac=0.1 * (seed % 3),
+                           max_keys=2 + seed % 7, start_inclusive=(seed % 2 == 1), with_slices=(seed % 4 == 2))
+    # move (every other / every) request to epoch 3, newer than every id of the store, so it takes
+    # the lean path; the rest defer to the general kernel
+    q = w.queries
+    sel = np.arange(len(q.txn.msb)) % (1 + seed % 2) == 0
+    for ts in (q.txn, q.exec):
+        ts.msb[sel] = (ts.msb[sel] & np.uint64(0x7FFF)) | np.uint64(3 << 15)
+    got, _ = _compare(w, oracle, paths=(0,))
+    assert got.stats["n_deferred_lean"] < len(w.queries)
+
+
 @pytest.mark.parametrize("esp,sync,reads", [(0.0, 0.0, False), (0.3, 0.05, False), (0.0, 0.02, True)])
 def test_config2_lean_classes(oracle, esp, sync, reads, monkeypatch):
     # every witness class on the lean path (Read -> Ws, Write -> RsOrWs, ExclusiveSyncPoint ->
