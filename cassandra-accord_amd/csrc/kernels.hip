@@ -916,37 +916,82 @@ hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // ---------------------------------------------------------------------------------------
 // pack: per-request regions -> contiguous per-map arrays at the scanned offsets
 // ---------------------------------------------------------------------------------------
-// regions -> packed per-map arrays; 8 lanes per request (outputs are tens of elements, so a
-// wave keeps 8 requests' dependent loads in flight)
-constexpr uint32_t PACK_LANES = 8;
-__global__ __launch_bounds__(256) void k_pack(BatchBufs b)
+// Pack: one wave per 64 consecutive requests. For each (map, array) the wave's output is one
+// contiguous run [off[t0], off[t0 + 64]); lane x of a 64-word chunk copies word x from the region
+// of the request whose output range holds it (request starts and source addresses staged in LDS,
+// the owning request found by advancing monotonically). Writes are fully coalesced; reads are
+// contiguous within each request's region.
+constexpr uint32_t PACK_WAVES = 4;
+constexpr uint32_t PACK_UNROLL = 4;
+
+template <typename T>
+__device__ __forceinline__ void pack_run(const uint8_t* __restrict__ reg, const uint32_t* st, const uint64_t* src,
+                                         uint64_t total, T* __restrict__ out)
 {
-    const uint64_t n = b.n_txns;
-    const uint64_t t = (uint64_t)blockIdx.x * (256 / PACK_LANES) + (threadIdx.x / PACK_LANES);
-    if (t >= n) return;
-    const uint32_t j = threadIdx.x % PACK_LANES;
+    const uint32_t lane = lane_id();
+    uint32_t r = 0;
+    for (uint64_t xb = 0; xb < total; xb += 64 * PACK_UNROLL)
+    {
+        const T* p[PACK_UNROLL];
+        bool ok[PACK_UNROLL];
 #pragma unroll
+        for (uint32_t u = 0; u < PACK_UNROLL; ++u)
+        {
+            const uint64_t x = xb + u * 64 + lane;
+            ok[u] = x < total;
+            if (ok[u])
+                while (st[r + 1] <= (uint32_t)x) ++r;
+            p[u] = ok[u] ? reinterpret_cast<const T*>(reg + src[r]) + ((uint32_t)x - st[r]) : reinterpret_cast<const T*>(reg);
+        }
+        T v[PACK_UNROLL];
+#pragma unroll
+        for (uint32_t u = 0; u < PACK_UNROLL; ++u) v[u] = *p[u];
+#pragma unroll
+        for (uint32_t u = 0; u < PACK_UNROLL; ++u)
+            if (ok[u]) out[xb + u * 64 + lane] = v[u];
+    }
+}
+
+__global__ __launch_bounds__(64 * PACK_WAVES) void k_pack(BatchBufs b)
+{
+    __shared__ uint32_t s_start[PACK_WAVES][65];
+    __shared__ uint64_t s_src[PACK_WAVES][64];
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint64_t n = b.n_txns;
+    const uint64_t t0 = ((uint64_t)blockIdx.x * PACK_WAVES + w) * 64;
+    if (t0 >= n) return;
+    const uint64_t t = t0 + lane, te = t0 + 64 < n ? t0 + 64 : n;
+    const bool on = t < n;
+    uint32_t* st = s_start[w];
+    uint64_t* src = s_src[w];
+#pragma unroll 1
     for (int m = 0; m < 3; ++m)
     {
-        const uint32_t no = b.sz[(3 * m + 2) * n + t];
-        if (no == 0) continue;
-        const uint32_t nk = b.sz[(3 * m) * n + t], U = b.sz[(3 * m + 1) * n + t];
-        const uint8_t* base = b.reg + b.t_reg[(uint64_t)m * n + t];
-        const int64_t* ikeys = reinterpret_cast<const int64_t*>(base);
-        const uint32_t* itx = reinterpret_cast<const uint32_t*>(ikeys + nk);
-        const int32_t* ik2t = reinterpret_cast<const int32_t*>(itx + U);
-        const uint64_t ko = b.off[(3 * m) * (n + 1) + t], vo = b.off[(3 * m + 1) * (n + 1) + t],
-                       oo = b.off[(3 * m + 2) * (n + 1) + t];
-        for (uint32_t i = j; i < nk; i += PACK_LANES) b.o_keys[m][ko + i] = ikeys[i];
-        for (uint32_t i = j; i < U; i += PACK_LANES) b.o_txns[m][vo + i] = itx[i];
-        for (uint32_t i = j; i < no; i += PACK_LANES) b.o_k2t[m][oo + i] = ik2t[i];
+        const uint32_t nk = on ? b.sz[(3 * m) * n + t] : 0u, U = on ? b.sz[(3 * m + 1) * n + t] : 0u;
+        const uint64_t rb = on ? b.t_reg[(uint64_t)m * n + t] : 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+        {
+            const uint64_t* off = b.off + (uint64_t)(3 * m + a) * (n + 1);
+            const uint64_t o0 = off[t0], total = off[te] - o0;
+            if (total == 0) continue;
+            wave_lds_sync();
+            st[lane] = on ? (uint32_t)(off[t] - o0) : (uint32_t)total;
+            if (lane == 0) st[64] = (uint32_t)total;
+            src[lane] = rb + (a == 0 ? 0 : (a == 1 ? 8ull * nk : 8ull * nk + 4ull * U));
+            wave_lds_sync();
+            if (a == 0) pack_run<int64_t>(b.reg, st, src, total, b.o_keys[m] + o0);
+            else if (a == 1) pack_run<uint32_t>(b.reg, st, src, total, b.o_txns[m] + o0);
+            else pack_run<int32_t>(b.reg, st, src, total, b.o_k2t[m] + o0);
+        }
     }
 }
 
 hipError_t run_pack(const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
-    k_pack<<<(unsigned)((b.n_txns + 256 / PACK_LANES - 1) / (256 / PACK_LANES)), 256, 0, st>>>(b);
+    const uint64_t waves = (b.n_txns + 63) / 64;
+    k_pack<<<(unsigned)((waves + PACK_WAVES - 1) / PACK_WAVES), 64 * PACK_WAVES, 0, st>>>(b);
     return hipGetLastError();
 }
 

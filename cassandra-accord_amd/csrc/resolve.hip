@@ -813,8 +813,8 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
 // InMemoryCommandStore.mapReduceForKey, :280): the request record the lean kernel reads instead
 // of the raw ids, and the key index (KeyEntry / krec position) of every (request, key) probe (open
 // addressing, linear probing in the 16-byte KeySlot table).
-// Keeping the dependent key -> slot probing here leaves the per-request kernels one load shorter.
-constexpr uint32_t PREP_UNROLL = 8;     // keys whose probes are issued together
+// Keeping the dependent key -> slot probing here leaves the per-request kernels one load shorter;
+// one thread per probe (the first n_txns threads also write the request records).
 
 // cell of key x in the range stabbing index: #endpoints < x (EndInclusive) or <= x (StartInclusive)
 __device__ __forceinline__ uint32_t cell_search(const DevSnapshot& s, int64_t x)
@@ -833,65 +833,41 @@ __device__ __forceinline__ uint32_t cell_search(const DevSnapshot& s, int64_t x)
 
 __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= b.n_txns) return;
-    const uint64_t k0 = b.q_key_off[t], k1 = b.q_key_off[t + 1];
-    const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t], em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
-    const int32_t tn = b.q_txn_node[t], en = b.q_exec_node[t];
-    const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
-    const uint32_t cls = kinds ? (uint32_t)kinds_class(kinds) : 0u;
-    const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
-    const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
-    const bool s_new = s.n_dict == 0 || norm_cmp(last, norm_tid(em, el, en)) < 0;
-    const bool t_new = same || s.n_dict == 0 || norm_cmp(last, norm_tid(tm, tl, tn)) < 0;
-    const uint64_t np = k1 - k0;
-    // lean fast path: S and self need no dictionary search, at most 8 keys, a valid kind
-    const bool fast = kinds != 0 && s_new && t_new && np <= 8;
-    b.q_rec[t] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32),
-                            (uint32_t)(np < 0xFFFFu ? np : 0xFFFFu) | (cls << 16) | (fast ? REC_FAST : 0u), 0u);
-    for (uint64_t c0 = k0; c0 < k1; c0 += PREP_UNROLL)
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < b.n_txns)
     {
-        int64_t key[PREP_UNROLL];
-        uint64_t h[PREP_UNROLL];
-        bool on[PREP_UNROLL];
-#pragma unroll
-        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
+        // request g's record
+        const uint64_t t = g;
+        const uint64_t k0 = b.q_key_off[t], k1 = b.q_key_off[t + 1];
+        const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t], em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
+        const int32_t tn = b.q_txn_node[t], en = b.q_exec_node[t];
+        const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
+        const uint32_t cls = kinds ? (uint32_t)kinds_class(kinds) : 0u;
+        const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
+        const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
+        const bool s_new = s.n_dict == 0 || norm_cmp(last, norm_tid(em, el, en)) < 0;
+        const bool t_new = same || s.n_dict == 0 || norm_cmp(last, norm_tid(tm, tl, tn)) < 0;
+        const uint64_t np = k1 - k0;
+        // lean fast path: S and self need no dictionary search, at most 8 keys, a valid kind
+        const bool fast = kinds != 0 && s_new && t_new && np <= 8;
+        b.q_rec[t] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32),
+                                (uint32_t)(np < 0xFFFFu ? np : 0xFFFFu) | (cls << 16) | (fast ? REC_FAST : 0u), 0u);
+    }
+    if (g < b.n_probes)
+    {
+        // probe g: its key's index (open addressing, linear probing) and stabbing-index cell
+        const int64_t key = b.q_keys[g];
+        bool in_slice = s.n_slices == 0;
+        for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
+            in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+        uint32_t slot = SLOT_NONE, cell = NO_CELL;
+        if (in_slice && s.n_keys)
         {
-            on[u] = c0 + u < k1;
-            key[u] = on[u] ? b.q_keys[c0 + u] : 0;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
-        {
-            bool in_slice = s.n_slices == 0;
-            for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
-                in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key[u]);
-            h[u] = key_hash(key[u]) & s.khash_mask;
-            if (!on[u]) continue;
-            if (!in_slice) b.p_cell[c0 + u] = NO_CELL;
-            if (!in_slice || !s.n_keys)
+            uint64_t hh = key_hash(key) & s.khash_mask;
+            uint4 qq = reinterpret_cast<const uint4*>(s.khash + hh)[0];
+            while (qq.z != KEY_EMPTY)
             {
-                b.p_slot[c0 + u] = SLOT_NONE;
-                if (in_slice) b.p_cell[c0 + u] = cell_search(s, key[u]);
-                on[u] = false;
-            }
-        }
-        uint4 q[PREP_UNROLL];
-#pragma unroll
-        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
-            q[u] = on[u] ? reinterpret_cast<const uint4*>(s.khash + h[u])[0] : make_uint4(0, 0, KEY_EMPTY, 0);
-#pragma unroll
-        for (uint32_t u = 0; u < PREP_UNROLL; ++u)
-        {
-            if (!on[u]) continue;
-            uint64_t hh = h[u];
-            uint4 qq = q[u];
-            uint32_t slot = SLOT_NONE;
-            uint32_t cell = NO_CELL;
-            while (true)
-            {
-                if (qq.z == KEY_EMPTY) break;
-                if ((int64_t)(((uint64_t)qq.y << 32) | qq.x) == key[u])
+                if ((int64_t)(((uint64_t)qq.y << 32) | qq.x) == key)
                 {
                     slot = qq.z;              // the key's index: KeyEntry / krec position
                     cell = qq.w;
@@ -900,16 +876,17 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
                 hh = (hh + 1) & s.khash_mask;
                 qq = reinterpret_cast<const uint4*>(s.khash + hh)[0];
             }
-            b.p_slot[c0 + u] = slot | SLOT_IN_SLICE;
-            // the key's stabbing-index cell: from its KeySlot, else by search (keys without a CFK)
-            b.p_cell[c0 + u] = slot != SLOT_NONE ? cell : cell_search(s, key[u]);
         }
+        b.p_slot[g] = in_slice ? slot | SLOT_IN_SLICE : SLOT_NONE;
+        // the key's cell: from its KeySlot, else by search (keys without a CFK)
+        if (s.cell_off) b.p_cell[g] = !in_slice ? NO_CELL : (slot != SLOT_NONE ? cell : cell_search(s, key));
     }
 }
 
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
-    if (b.n_txns) k_prepare<<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
+    const uint64_t n = b.n_txns > b.n_probes ? b.n_txns : b.n_probes;
+    if (n) k_prepare<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, b);
     return hipGetLastError();
 }
 

@@ -135,6 +135,18 @@ def test_empty_batch_and_empty_snapshot(oracle):
     _compare(w, oracle)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_ranges_without_cfk(oracle, seed, monkeypatch):
+    # range commands (and redundant-before for odd seeds) on a store with no CommandsForKey: every
+    # probe misses the key index but still reads its range cell / tree
+    from accord_deps.model import CfkSnapshot
+    w = synth.random_small(900 + seed, n_range_cmds=30, n_redundant=3 * (seed % 2), start_inclusive=(seed % 4 >= 2))
+    w.cfk = CfkSnapshot.empty()
+    _compare(w, oracle, paths=(0,))
+    monkeypatch.setenv("AD_CELL_BUDGET", "0")
+    _compare(w, oracle, paths=(0,))
+
+
 def test_errors():
     w = synth.random_small(5)
     st = native.DeviceCommandStore()
