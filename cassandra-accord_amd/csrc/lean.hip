@@ -14,6 +14,8 @@
 // is appended to the deferred list and resolved by the general fused kernel (resolve.hip).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.hpp"
 #include "kernels.hpp"
 #include "wave.hpp"
@@ -501,7 +503,8 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, const Le
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG>, 64 * LEAN_WAVES, 0) != hipSuccess ||
             nb <= 0)
             nb = 2;
-        per_cu = std::min(nb, 8);
+        per_cu = std::min(nb, 5);     // measured: more resident waves only add memory contention
+        if (const char* e = getenv("AD_LEAN_PER_CU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu));
