@@ -46,6 +46,14 @@ def kernel_of_stage(i, ranges=False):
 RESOLVE_STAGES = [0, 3, 6]
 
 
+# device of the small timing / count reductions: the GPU under RCCL, the host under gloo
+RED_DEV = None
+
+
+def _red_dev(dev):
+    return RED_DEV if RED_DEV is not None else dev
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -172,10 +180,10 @@ def bench_levels(args, rank, world, local, dev):
     ms /= max(args.steps, 1)
     pairs = int(g.key_off[-1])
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=_red_dev(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        p = torch.tensor([pairs], dtype=torch.int64, device=dev)
+        p = torch.tensor([pairs], dtype=torch.int64, device=_red_dev(dev))
         dist.all_reduce(p, op=dist.ReduceOp.SUM)
         pairs = int(p.item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
@@ -224,7 +232,7 @@ def _timed_steps(args, world, dev, step):
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=_red_dev(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, all_stats
@@ -233,7 +241,7 @@ def _timed_steps(args, world, dev, step):
 def _sum_over_ranks(world, dev, x):
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.int64, device=dev)
+    t = torch.tensor([x], dtype=torch.int64, device=_red_dev(dev))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
 
@@ -347,17 +355,27 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=(1, 2, 4, 5),
                     help="2: BASELINE config 2 (the headline line, default); 1: SEQUENTIAL PreAccept batch "
                          "(host API); 4: range transactions; 5: execution levels (K5)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl (RCCL, one GPU per rank: the measured configuration); gloo: rehearsal of the "
+                         "N>1 path on fewer GPUs (ranks share GPUs, the exchange is staged through host memory)")
     args = ap.parse_args()
 
+    global RED_DEV
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    if args.dist_backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
+        RED_DEV = torch.device("cpu")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     if args.config == 5:
         return bench_levels(args, rank, world, local, dev)
@@ -382,7 +400,9 @@ def main():
 
     if world > 1:
         engine = exchange.GpuEngine(store, qdev, txn_index, dev, stream=sp)
-        ex = exchange.ShardExchange(engine, txn_index, n_total, rank, world, count_device=dev)
+        gloo = args.dist_backend == "gloo"
+        ex = exchange.ShardExchange(engine, txn_index, n_total, rank, world, count_device=None if gloo else dev,
+                                    stage_cpu=gloo)
 
         def step():
             mg = ex.step()
@@ -417,10 +437,10 @@ def main():
     merge_ms /= max(args.steps, 1)
     probes = w.queries.n_probes
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=_red_dev(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        p = torch.tensor([probes], dtype=torch.int64, device=dev)
+        p = torch.tensor([probes], dtype=torch.int64, device=_red_dev(dev))
         dist.all_reduce(p, op=dist.ReduceOp.SUM)
         probes = int(p.item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)

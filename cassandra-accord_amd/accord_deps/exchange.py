@@ -122,8 +122,9 @@ _UNITS = (("hdr", 4), ("keys", 1), ("ids", 3), ("k2t", 1))
 class ShardExchange:
     """The all-to-all + merge protocol of one rank."""
 
-    def __init__(self, engine, txn_index, n_total, rank, world, group=None, count_device=None):
+    def __init__(self, engine, txn_index, n_total, rank, world, group=None, count_device=None, stage_cpu=False):
         self.engine = engine
+        self.stage_cpu = stage_cpu          # gloo over device buffers: payload staged through host memory
         self.rank, self.world = rank, world
         self.group = group
         bases = owner_bases(n_total, world)
@@ -154,5 +155,10 @@ class ShardExchange:
             out_splits = [int(x) * mult for x in rcounts[:, a]]
             si = send[name][:sum(in_splits)]
             ro = recv[name][:sum(out_splits)]
-            dist.all_to_all_single(ro, si, out_splits, in_splits, group=self.group)
+            if self.stage_cpu and ro.is_cuda:
+                rh = torch.empty(ro.shape, dtype=ro.dtype)
+                dist.all_to_all_single(rh, si.cpu(), out_splits, in_splits, group=self.group)
+                ro.copy_(rh)
+            else:
+                dist.all_to_all_single(ro, si, out_splits, in_splits, group=self.group)
         return e.merge(totals, rcounts[:, 0], self.txn_base, self.n_owned)
