@@ -403,6 +403,9 @@ def main():
         gloo = args.dist_backend == "gloo"
         ex = exchange.ShardExchange(engine, txn_index, n_total, rank, world, count_device=None if gloo else dev,
                                     stage_cpu=gloo)
+        t_g = time.time()
+        n_global = ex.install_global_dict()       # ingest-time: ids travel as uint32 global ranks
+        log("rank %d: global dictionary of %d ids installed in %.1f s" % (rank, n_global, time.time() - t_g))
 
         def step():
             mg = ex.step()

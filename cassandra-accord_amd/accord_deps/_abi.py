@@ -95,7 +95,11 @@ class AdParts(C.Structure):
     _fields_ = [("n_parts", C.c_uint64), ("n_key_words", C.c_uint64), ("n_ids", C.c_uint64), ("n_k2t", C.c_uint64),
                 ("hdr", P), ("keys", P), ("ids", P), ("k2t", P),
                 ("cap_parts", C.c_uint64), ("cap_key_words", C.c_uint64), ("cap_ids", C.c_uint64),
-                ("cap_k2t", C.c_uint64)]
+                ("cap_k2t", C.c_uint64), ("id_format", C.c_uint32)]
+
+
+AD_IDS_TRIPLET = 0
+AD_IDS_RANK = 1
 
 
 class AdMerged(C.Structure):

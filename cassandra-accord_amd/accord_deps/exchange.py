@@ -49,22 +49,49 @@ def route(queries, lo, hi, start_inclusive=False):
     return Queries(queries.txn.take(idx), queries.exec.take(idx), key_off, k[sel], me), idx
 
 
-class PartsBuffers:
-    """Growable device arrays in the ad_parts transport format."""
+def build_global_dict(dicts):
+    """The global TxnId dictionary of a multi-store exchange: the ascending, duplicate-free union in
+    Timestamp order (msb unsigned, then (lsb >>> 16, identity flags) unsigned, then node signed;
+    Timestamp.compareTo / equals) of every store's dictionary (DeviceCommandStore.dictionary()),
+    the raw fields of an id taken from the first store holding it. Ingest-time work, run
+    identically on every rank. `dicts`: list of Tids in store order. Returns Tids."""
+    from .model import Tids
+    msb = np.concatenate([np.asarray(d.msb, np.uint64) for d in dicts]) if dicts else np.zeros(0, np.uint64)
+    lsb = np.concatenate([np.asarray(d.lsb, np.uint64) for d in dicts]) if dicts else np.zeros(0, np.uint64)
+    node = np.concatenate([np.asarray(d.node, np.int32) for d in dicts]) if dicts else np.zeros(0, np.int32)
+    lo = ((lsb >> np.uint64(16)) << np.uint64(4)) | ((lsb >> np.uint64(1)) & np.uint64(0xF))
+    src = np.concatenate([np.full(len(d.msb), i, np.int64) for i, d in enumerate(dicts)]) if dicts else \
+        np.zeros(0, np.int64)
+    order = np.lexsort((src, node, lo, msb))          # last key primary; equal ids: earliest store first
+    m, l_, n_ = msb[order], lo[order], node[order]
+    first = np.ones(len(order), bool)
+    first[1:] = (m[1:] != m[:-1]) | (l_[1:] != l_[:-1]) | (n_[1:] != n_[:-1])
+    keep = order[first]
+    return Tids(msb[keep].copy(), lsb[keep].copy(), node[keep].copy())
 
-    def __init__(self, device):
+
+class PartsBuffers:
+    """Growable device arrays in the ad_parts transport format (ids as {msb, lsb, node} int64
+    triplets, or as uint32 global ranks when `rank_ids`)."""
+
+    def __init__(self, device, rank_ids=False):
         self.device = device
+        self.rank_ids = rank_ids
         self.hdr = self.keys = self.ids = self.k2t = None
         self.ensure(1, 1, 1, 1)
 
+    @property
+    def id_mult(self):
+        return 1 if self.rank_ids else 3
+
     def ensure(self, parts, key_words, ids, k2t):
         def grow(t, n, dtype):
-            if t is None or t.numel() < n:
+            if t is None or t.numel() < n or t.dtype != dtype:
                 return torch.empty(max(int(n * 1.25), 16), dtype=dtype, device=self.device)
             return t
         self.hdr = grow(self.hdr, 4 * parts, torch.int64)
         self.keys = grow(self.keys, key_words, torch.int64)
-        self.ids = grow(self.ids, 3 * ids, torch.int64)
+        self.ids = grow(self.ids, self.id_mult * ids, torch.int32 if self.rank_ids else torch.int64)
         self.k2t = grow(self.k2t, k2t, torch.int32)
 
     def soa(self, n=None):
@@ -73,8 +100,9 @@ class PartsBuffers:
                                        self.k2t.data_ptr())
         p.cap_parts = self.hdr.numel() // 4
         p.cap_key_words = self.keys.numel()
-        p.cap_ids = self.ids.numel() // 3
+        p.cap_ids = self.ids.numel() // self.id_mult
         p.cap_k2t = self.k2t.numel()
+        p.id_format = A.AD_IDS_RANK if self.rank_ids else A.AD_IDS_TRIPLET
         if n is not None:
             p.n_parts, p.n_key_words, p.n_ids, p.n_k2t = (int(x) for x in n)
         return p
@@ -92,6 +120,19 @@ class GpuEngine:
         self.send = PartsBuffers(device)
         self.recv = PartsBuffers(device)
         self.last_stats = None
+
+    @property
+    def id_mult(self):
+        return self.send.id_mult
+
+    def dictionary(self):
+        return self.store.dictionary()
+
+    def set_global_dict(self, g):
+        """Parts travel as uint32 global ranks from now on (ad_set_global_dict)."""
+        self.store.set_global_dict(g)
+        self.send = PartsBuffers(self.device, rank_ids=True)
+        self.recv = PartsBuffers(self.device, rank_ids=True)
 
     def resolve(self):
         self.res, self.last_stats = self.store.deps_batch_device(self.qdev, self.stream)
@@ -115,8 +156,9 @@ class GpuEngine:
         return self.store.merge_parts(self.recv.soa(totals), src_parts, txn_base, n_owned, self.stream)
 
 
-# element multiplicity of each transport array per counted unit
-_UNITS = (("hdr", 4), ("keys", 1), ("ids", 3), ("k2t", 1))
+def _units(id_mult):
+    """element multiplicity of each transport array per counted unit"""
+    return (("hdr", 4), ("keys", 1), ("ids", id_mult), ("k2t", 1))
 
 
 class ShardExchange:
@@ -137,6 +179,18 @@ class ShardExchange:
         self.dest_first[-1] = len(ti)
         self.count_device = count_device
 
+    def install_global_dict(self):
+        """Ingest-time collective (once per snapshot): gather every store's dictionary, build the
+        global one identically on every rank and install it, so that the per-step all-to-all moves
+        4-byte id ranks instead of 24-byte ids and K3 merges integers."""
+        mine = self.engine.dictionary()
+        got = [None] * self.world
+        dist.all_gather_object(got, (mine.msb, mine.lsb, mine.node), group=self.group)
+        from .model import Tids
+        g = build_global_dict([Tids(*t) for t in got])
+        self.engine.set_global_dict(g)
+        return len(g.msb)
+
     def step(self):
         e = self.engine
         e.resolve()
@@ -150,7 +204,7 @@ class ShardExchange:
         rcounts = rc.cpu().numpy().reshape(self.world, 4)
         totals = rcounts.sum(axis=0)
         recv = e.recv_buffers(totals)
-        for a, (name, mult) in enumerate(_UNITS):
+        for a, (name, mult) in enumerate(_units(getattr(e, "id_mult", 3))):
             in_splits = [int(x) * mult for x in counts[:, a]]
             out_splits = [int(x) * mult for x in rcounts[:, a]]
             si = send[name][:sum(in_splits)]

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("ACCORD_DEPS_LIB") or os.path.join(os.path.dirname(os.
 EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error", "ad_cfk_load",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
-           "ad_copy_to_host", "ad_levels", "ad_levels_device")
+           "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict")
 
 
 class AccordDepsError(RuntimeError):
@@ -67,6 +67,7 @@ def lib():
         L.ad_parts_merge.argtypes = [C.c_void_p, C.POINTER(A.AdParts), C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64,
                                      C.c_void_p, C.POINTER(A.AdMerged)]
         L.ad_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.ad_set_global_dict.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.ad_levels.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.POINTER(A.AdStats)]
         L.ad_levels_device.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.c_void_p,
                                        C.POINTER(A.AdStats)]
@@ -137,6 +138,14 @@ class DeviceCommandStore:
         self._check(lib().ad_dict(self.h, C.byref(n), C.byref(pm), C.byref(pl), C.byref(pn)))
         k = n.value
         return Tids(_view(pm, k, np.uint64).copy(), _view(pl, k, np.uint64).copy(), _view(pn, k, np.int32).copy())
+
+    def set_global_dict(self, g):
+        """Install the global TxnId dictionary (Tids, ascending and unique; exchange.build_global_dict):
+        parts are then exported as uint32 global ranks (accord_deps.h ad_set_global_dict)."""
+        m = np.ascontiguousarray(g.msb, np.uint64)
+        ls = np.ascontiguousarray(g.lsb, np.uint64)
+        nd = np.ascontiguousarray(g.node, np.int32)
+        self._check(lib().ad_set_global_dict(self.h, len(m), A.ptr(m), A.ptr(ls), A.ptr(nd)))
 
     def range_table(self):
         n = C.c_uint64()

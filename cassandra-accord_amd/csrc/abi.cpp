@@ -208,7 +208,11 @@ struct ad_ctx {
     // multi-GPU export / merge buffers
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
-    DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t;
+    DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t, m_u, m_ppre;
+    // global dictionary of the multi-store exchange (ad_set_global_dict)
+    DevBuf g_msb, g_lsb, g_node, g_map, g_err;
+    uint64_t n_global = 0;
+    bool global_ok = false;
     // execution levels (K5)
     LevelsWork* lv = nullptr;
     DevBuf g_em, g_el, g_en, g_kind, g_ko, g_k, g_do, g_d, g_out;
@@ -712,6 +716,7 @@ static int build_snapshot(ad_ctx* c)
     HIPCHK(c, build_range_trees(s, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->dirty = false;
+    c->global_ok = false;        // the dictionary changed: a global dictionary must be installed again
     c->ms_ingest = now_ms() - t0;
     return 0;
 }
@@ -1341,6 +1346,39 @@ int ad_range_table(const ad_ctx* c, uint64_t* n, const int64_t** start, const in
     return AD_OK;
 }
 
+int ad_set_global_dict(ad_ctx* c, uint64_t n, const uint64_t* msb, const uint64_t* lsb, const int32_t* node)
+{
+    if (!c || (n && (!msb || !lsb || !node))) return AD_E_INVAL;
+    if (n >= (1ull << 31)) return c->fail(AD_E_CAPACITY, "ad_set_global_dict: more than 2^31 ids");
+    int rc = ad_prepare(c);
+    if (rc) return rc;
+    for (uint64_t i = 1; i < n; ++i)
+        if (norm_cmp(norm_tid(msb[i - 1], lsb[i - 1], node[i - 1]), norm_tid(msb[i], lsb[i], node[i])) >= 0)
+            return c->fail(AD_E_INVAL, "ad_set_global_dict: ids not ascending and unique at %llu", (unsigned long long)i);
+    hipStream_t st = c->stream;
+    const uint64_t nl = c->dict_msb.size();
+    if (!ens<uint64_t>(c->g_msb, n) || !ens<uint64_t>(c->g_lsb, n) || !ens<int32_t>(c->g_node, n) ||
+        !ens<uint32_t>(c->g_map, nl) || !ens<uint32_t>(c->g_err, 1))
+        return c->fail(AD_E_NOMEM, "global dictionary");
+    if (n)
+    {
+        HIPCHK(c, hipMemcpyAsync(c->g_msb.p, msb, 8 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(c->g_lsb.p, lsb, 8 * n, hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(c->g_node.p, node, 4 * n, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(c, hipMemsetAsync(c->g_err.p, 0, 4, st));
+    HIPCHK(c, run_global_map(c->d_dict_hi.as<uint64_t>(), c->d_dict_lo.as<uint64_t>(), c->d_dict_node.as<int32_t>(), nl,
+                             c->g_msb.as<uint64_t>(), c->g_lsb.as<uint64_t>(), c->g_node.as<int32_t>(), n,
+                             c->g_map.as<uint32_t>(), c->g_err.as<uint32_t>(), st));
+    uint32_t err = 0;
+    HIPCHK(c, hipMemcpyAsync(&err, c->g_err.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (err) return c->fail(AD_E_INVAL, "ad_set_global_dict: an id of this store's dictionary is missing");
+    c->n_global = n;
+    c->global_ok = true;
+    return AD_OK;
+}
+
 int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
                     const uint64_t* dest_first, void* stream, ad_parts* out, uint64_t* dest_counts)
 {
@@ -1372,6 +1410,8 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     a.dict_node = c->d_dict_node.as<int32_t>();
     a.rt_start = c->d_rt_start.as<int64_t>();
     a.rt_end = c->d_rt_end.as<int64_t>();
+    a.gmap = c->global_ok ? c->g_map.as<uint32_t>() : nullptr;
+    out->id_format = c->global_ok ? AD_IDS_RANK : AD_IDS_TRIPLET;
     a.sz = c->x_sz.as<uint32_t>();
     a.off = c->x_off.as<uint64_t>();
     HIPCHK(c, hipMemcpyAsync(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), hipMemcpyHostToDevice, st));
@@ -1411,6 +1451,12 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     const uint64_t P = in->n_parts, G = 3 * n_owned;
+    const bool rank_ids = in->id_format == AD_IDS_RANK;
+    if (in->id_format != AD_IDS_TRIPLET && !rank_ids) return c->fail(AD_E_INVAL, "ad_parts_merge: unknown id_format");
+    if (rank_ids && !c->global_ok)
+        return c->fail(AD_E_INVAL, "ad_parts_merge: rank-format parts need ad_set_global_dict on this ctx");
+    if (rank_ids && (!ens<uint32_t>(c->m_u, in->n_ids) || !ens<uint32_t>(c->m_ppre, 2 * P)))
+        return c->fail(AD_E_NOMEM, "merge buffers");
     if (!ens<uint64_t>(c->m_src, n_src + 1) || !ens<uint32_t>(c->m_psz, 3 * P) || !ens<uint64_t>(c->m_poff, 3 * (P + 1)) ||
         !ens<int32_t>(c->m_slot, G * n_src) || !ens<uint32_t>(c->m_dup, in->n_ids) || !ens<uint32_t>(c->m_gsz, 3 * G) ||
         !ens<uint64_t>(c->m_goff, 3 * (G + 1)) ||
@@ -1435,6 +1481,15 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     a.o_keys_off = c->m_ko.as<uint64_t>();
     a.o_txn_off = c->m_to.as<uint64_t>();
     a.o_k2t_off = c->m_oo.as<uint64_t>();
+    if (rank_ids)
+    {
+        a.u = c->m_u.as<uint32_t>();
+        a.ppre = c->m_ppre.as<uint32_t>();
+        a.n_global = c->n_global;
+        a.g_msb = c->g_msb.as<uint64_t>();
+        a.g_lsb = c->g_lsb.as<uint64_t>();
+        a.g_node = c->g_node.as<int32_t>();
+    }
     HIPCHK(c, hipEventRecord(c->ev[6], st));
     HIPCHK(c, hipMemcpyAsync(c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemsetAsync(a.error, 0, sizeof(uint32_t), st));
@@ -1442,7 +1497,7 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     HIPCHK(c, run_merge_prepare(a, st));
     HIPCHK(c, run_scan_arrays(a.psz, a.poff, P, 3, c->m_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_merge_slots(a, st));
-    HIPCHK(c, run_merge_count(a, st));
+    HIPCHK(c, rank_ids ? run_merge_rank(a, st) : run_merge_count(a, st));
     HIPCHK(c, run_scan_arrays(a.gsz, a.goff, G, 3, c->m_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_merge_bases(a, c->m_bases.as<uint64_t>(), st));
     uint64_t bases[12];
@@ -1452,9 +1507,11 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     HIPCHK(c, hipStreamSynchronize(st));
     if (err)
         return c->fail(AD_E_INVAL, "ad_parts_merge: malformed parts (%s)",
-                       err & 1 ? "request outside the owned range or bad map" :
-                       err & 2 ? "two parts of one request and map from one source" :
-                                 "keys of different stores overlap or are out of slice order");
+                       err & 1  ? "request outside the owned range or bad map" :
+                       err & 2  ? "two parts of one request and map from one source" :
+                       err & 4  ? "keys of different stores overlap or are out of slice order" :
+                       err & 16 ? "id rank outside the global dictionary" :
+                                  "ids of a part not sorted and unique");
     // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
     if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, 3 * bases[10]) || !ens<int32_t>(c->m_k2t, bases[11]))
         return c->fail(AD_E_NOMEM, "merge outputs");
@@ -1463,7 +1520,7 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     a.o_k2t = c->m_k2t.as<int32_t>();
     if (n_owned == 0)
         for (DevBuf* b : {&c->m_ko, &c->m_to, &c->m_oo}) HIPCHK(c, hipMemsetAsync(b->p, 0, sizeof(uint64_t) * 3, st));
-    HIPCHK(c, run_merge_emit(a, st));
+    HIPCHK(c, rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
     HIPCHK(c, hipEventRecord(c->ev[7], st));
     HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));

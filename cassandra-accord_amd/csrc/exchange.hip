@@ -113,14 +113,20 @@ __global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
     {
         for (uint64_t j = g8; j < nk; j += 8) a.okeys[KW + j] = a.keys[m][k0 + j];
     }
-    for (uint64_t j = g8; j < nt; j += 8)
+    if (a.gmap)
     {
-        const uint32_t d = a.txns[m][t0 + j];
-        int64_t* o = a.oids + 3 * (ID + j);
-        o[0] = (int64_t)a.dict_msb[d];
-        o[1] = (int64_t)a.dict_lsb[d];
-        o[2] = (int64_t)a.dict_node[d];
+        uint32_t* o = reinterpret_cast<uint32_t*>(a.oids) + ID;
+        for (uint64_t j = g8; j < nt; j += 8) o[j] = a.gmap[a.txns[m][t0 + j]];
     }
+    else
+        for (uint64_t j = g8; j < nt; j += 8)
+        {
+            const uint32_t d = a.txns[m][t0 + j];
+            int64_t* o = a.oids + 3 * (ID + j);
+            o[0] = (int64_t)a.dict_msb[d];
+            o[1] = (int64_t)a.dict_lsb[d];
+            o[2] = (int64_t)a.dict_node[d];
+        }
     for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = a.k2t[m][o0 + j];
 }
 
@@ -171,6 +177,7 @@ __global__ void k_merge_slots(MergeArgs a)
 struct PartInfo {
     uint64_t ibase, kbase, obase;     // offsets of the part's ids / key words / k2t in the receive buffers
     uint32_t ni, kw, no, nk;          // sizes: ids, key words, k2t ints, keys
+    uint32_t p;                       // part index
 };
 
 __device__ __forceinline__ uint32_t stage_parts(const MergeArgs& a, uint64_t g, PartInfo* info)
@@ -191,6 +198,7 @@ __device__ __forceinline__ uint32_t stage_parts(const MergeArgs& a, uint64_t g, 
         pi.obase = a.poff[2 * P1 + p];
         pi.no = (uint32_t)(a.poff[2 * P1 + p + 1] - pi.obase);
         pi.nk = (uint32_t)a.hdr[4 * p + 1];
+        pi.p = (uint32_t)p;
         info[mbcnt(live)] = pi;
     }
     wave_lds_sync();
@@ -366,6 +374,249 @@ __global__ void __launch_bounds__(64 * XWAVES) k_merge_emit(MergeArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// AD_IDS_RANK: parts carry uint32 ranks of one global dictionary, so the union of a group's id
+// lists is integer work. Pass 1 (wave per group): the union index u of every received id -- the
+// number of distinct ranks below it in the group -- and whether an earlier part already holds it
+// (Timestamp.equals), plus per part the key words and pairs of the earlier parts of its group.
+// Pass 2 (thread per part): keys concatenated in source order, union ids materialised from the
+// global dictionary at u, keysToTxnIds remapped through u (RelationMultiMap.linearUnion restated,
+// RelationMultiMap.java:561-816).
+// ---------------------------------------------------------------------------------------
+__global__ void k_global_map(const uint64_t* l_msb, const uint64_t* l_lo, const int32_t* l_node, uint64_t n_local,
+                             const uint64_t* g_msb, const uint64_t* g_lsb, const int32_t* g_node, uint64_t n_global,
+                             uint32_t* map, uint32_t* err)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_local) return;
+    const NormTid x{l_msb[i], l_lo[i], l_node[i]};
+    uint64_t lo = 0, hi = n_global;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (norm_cmp(norm_tid(g_msb[mid], g_lsb[mid], g_node[mid]), x) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    const bool found = lo < n_global && norm_cmp(norm_tid(g_msb[lo], g_lsb[lo], g_node[lo]), x) == 0;
+    if (!found) atomicOr(err, 1u);
+    map[i] = found ? (uint32_t)lo : 0u;
+}
+
+__device__ __forceinline__ uint32_t lb_u32(const uint32_t* v, uint64_t base, uint32_t n, uint32_t x)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (v[base + mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(64 * XWAVES) k_merge_rank(MergeArgs a)
+{
+    __shared__ PartInfo s_info[XWAVES][64];
+    __shared__ uint32_t s_ist[XWAVES][64];
+    PartInfo* info = s_info[threadIdx.x >> 6];
+    uint32_t* ist = s_ist[threadIdx.x >> 6];
+    const uint64_t n_groups = 3 * a.n_owned;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t l = lane_id();
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    for (uint64_t g = wave; g < n_groups; g += n_waves)
+    {
+        const int m = (int)(g / a.n_owned);
+        const int w = m == AD_MAP_RANGE ? 2 : 1;
+        wave_lds_sync();
+        const uint32_t np = stage_parts(a, g, info);
+        if (np == 0)
+        {
+            if (l == 0)
+            {
+                a.gsz[0 * n_groups + g] = 0;
+                a.gsz[1 * n_groups + g] = 0;
+                a.gsz[2 * n_groups + g] = 0;
+            }
+            continue;
+        }
+        // per part (lane j < np): sizes, exclusive prefixes, source-order key check
+        const bool pl = l < np;
+        const uint32_t ni_l = pl ? info[l].ni : 0u, kw_l = pl ? info[l].kw : 0u;
+        const uint32_t pr_l = pl ? info[l].no - info[l].nk : 0u, no_l = pl ? info[l].no : 0u;
+        const uint32_t ii = wave_incl_scan(ni_l), ki = wave_incl_scan(kw_l), pi = wave_incl_scan(pr_l);
+        const uint32_t T = uniform(__shfl(ii, (int)np - 1, 64));
+        const uint32_t KWt = uniform(__shfl(ki, (int)np - 1, 64));
+        const uint32_t NOt = uniform(wave_sum(no_l));
+        if (pl)
+        {
+            ist[l] = ii - ni_l;
+            a.ppre[2 * (uint64_t)info[l].p] = ki - kw_l;
+            a.ppre[2 * (uint64_t)info[l].p + 1] = pi - pr_l;
+            if (l > 0)
+            {
+                const PartInfo& pp = info[l - 1];
+                const PartInfo& pj = info[l];
+                const int64_t ls = a.keys[pp.kbase + pp.kw - w], le = w == 2 ? a.keys[pp.kbase + pp.kw - 1] : 0;
+                const int64_t fs = a.keys[pj.kbase], fe = w == 2 ? a.keys[pj.kbase + 1] : 0;
+                if (!keys_ordered(m, ls, le, fs, fe)) atomicOr(a.error, 4u);
+            }
+        }
+        wave_lds_sync();
+        uint32_t n_dup = 0;
+        if (T <= 64)
+        {
+            // one id per lane; u = number of distinct ranks below it, from a rank count over the
+            // group (wave-uniform broadcasts) minus the duplicates below it
+            const bool live = l < T;
+            uint32_t j = 0;
+            for (uint32_t q = 1; q < np; ++q)
+                if (l >= ist[q]) j = q;
+            const uint32_t idx = l - ist[j];
+            const uint64_t at = info[j].ibase + idx;
+            const uint32_t x = live ? ids[at] : 0xFFFFFFFFu;
+            if (live && idx > 0 && ids[at - 1] >= x) atomicOr(a.error, 8u);        // part not sorted / unique
+            if (live && x >= a.n_global) atomicOr(a.error, 16u);
+            uint32_t lt = 0;
+            bool dup = false;
+            for (uint32_t s2 = 0; s2 < T; ++s2)
+            {
+                const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)s2);
+                lt += y < x ? 1u : 0u;
+                dup = dup || (y == x && s2 < l);
+            }
+            const uint64_t dm = ballot(live && dup);
+            for (uint64_t b = dm; b; b &= b - 1)
+            {
+                const uint32_t s2 = (uint32_t)(__ffsll((unsigned long long)b) - 1);
+                const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)s2);
+                lt -= y < x ? 1u : 0u;
+            }
+            if (live) a.u[at] = lt | (dup ? DUP_BIT : 0u);
+            n_dup = __popcll(dm);
+        }
+        else
+        {
+            // large group: per part, dup flags against the earlier parts with an exclusive dup
+            // prefix (binary searches), then u(x) = sum over parts q of lb_q(x) - dupsBefore_q(lb_q(x))
+            for (uint32_t jj = 0; jj < np; ++jj)
+            {
+                const PartInfo pj = info[jj];
+                uint32_t run = 0;
+                for (uint32_t e0 = 0; e0 < pj.ni; e0 += 64)
+                {
+                    const uint32_t e = e0 + l;
+                    bool dup = false;
+                    if (e < pj.ni)
+                    {
+                        const uint32_t x = ids[pj.ibase + e];
+                        if (e > 0 && ids[pj.ibase + e - 1] >= x) atomicOr(a.error, 8u);
+                        if (x >= a.n_global) atomicOr(a.error, 16u);
+                        for (uint32_t q = 0; q < jj && !dup; ++q)
+                        {
+                            const uint32_t pos = lb_u32(ids, info[q].ibase, info[q].ni, x);
+                            dup = pos < info[q].ni && ids[info[q].ibase + pos] == x;
+                        }
+                    }
+                    const uint64_t bm = ballot(dup);
+                    if (e < pj.ni) a.dup[pj.ibase + e] = (run + mbcnt(bm)) | (dup ? DUP_BIT : 0u);
+                    run += __popcll(bm);
+                }
+                n_dup += run;
+            }
+            __threadfence();
+            for (uint32_t jj = 0; jj < np; ++jj)
+            {
+                const PartInfo pj = info[jj];
+                for (uint32_t e = l; e < pj.ni; e += 64)
+                {
+                    const uint32_t x = ids[pj.ibase + e];
+                    uint32_t u = 0;
+                    for (uint32_t q = 0; q < np; ++q)
+                    {
+                        const uint64_t qb = info[q].ibase;
+                        const uint32_t qn = info[q].ni;
+                        const uint32_t lb = q == jj ? e : lb_u32(ids, qb, qn, x);
+                        uint32_t dp;
+                        if (lb < qn) dp = a.dup[qb + lb] & ~DUP_BIT;
+                        else
+                        {
+                            const uint32_t d = qn ? a.dup[qb + qn - 1] : 0u;
+                            dp = qn ? (d & ~DUP_BIT) + (d >> 31) : 0u;
+                        }
+                        u += lb - dp;
+                    }
+                    a.u[pj.ibase + e] = u | (a.dup[pj.ibase + e] & DUP_BIT);
+                }
+            }
+        }
+        if (l == 0)
+        {
+            a.gsz[0 * n_groups + g] = KWt;
+            a.gsz[1 * n_groups + g] = T - n_dup;
+            a.gsz[2 * n_groups + g] = NOt;
+        }
+    }
+}
+
+// thread per part: its slice of the group's keys, union ids and keysToTxnIds
+__global__ void k_merge_emit_rank(MergeArgs a)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n_parts) return;
+    const uint64_t n_groups = 3 * a.n_owned, G1 = n_groups + 1, P1 = a.n_parts + 1;
+    const int64_t h0 = a.hdr[4 * p];
+    const int m = (int)(h0 & 3);
+    const uint64_t g = (uint64_t)m * a.n_owned + (uint64_t)((h0 >> 2) - (int64_t)a.txn_base);
+    const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
+    const uint32_t nk = (uint32_t)a.hdr[4 * p + 1], ni = (uint32_t)a.hdr[4 * p + 2], no = (uint32_t)a.hdr[4 * p + 3];
+    const uint64_t kbase = a.poff[0 * P1 + p], ibase = a.poff[1 * P1 + p], obase = a.poff[2 * P1 + p];
+    const uint64_t KW = a.goff[0 * G1 + g], ID = a.goff[1 * G1 + g], KO = a.goff[2 * G1 + g];
+    const uint32_t nkeys_total = a.gsz[0 * n_groups + g] / w;
+    const uint32_t kwb = a.ppre[2 * p], prb = a.ppre[2 * p + 1];
+    for (uint32_t e = 0; e < nk * w; ++e) a.o_keys[KW + kwb + e] = a.keys[kbase + e];
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    for (uint32_t e = 0; e < ni; ++e)
+    {
+        const uint32_t uu = a.u[ibase + e];
+        if (uu & DUP_BIT) continue;
+        const uint32_t x = ids[ibase + e];
+        int64_t* o = a.o_ids + 3 * (ID + uu);
+        o[0] = (int64_t)a.g_msb[x];
+        o[1] = (int64_t)a.g_lsb[x];
+        o[2] = (int64_t)a.g_node[x];
+    }
+    const uint32_t kb = kwb / w;
+    for (uint32_t e = 0; e < nk; ++e)
+        a.o_k2t[KO + kb + e] = (int32_t)((uint64_t)a.k2t[obase + e] - nk + nkeys_total + prb);
+    for (uint32_t v = 0; v < no - nk; ++v)
+    {
+        const uint32_t idx = (uint32_t)a.k2t[obase + nk + v];
+        if (idx >= ni)
+        {
+            atomicOr(a.error, 8u);
+            continue;
+        }
+        a.o_k2t[KO + nkeys_total + prb + v] = (int32_t)(a.u[ibase + idx] & ~DUP_BIT);
+    }
+}
+
+// per map and owned request: offsets of the merged CSR (relative to the map's first group)
+__global__ void k_merge_out_offsets(MergeArgs a)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t N1 = a.n_owned + 1;
+    if (i >= 3 * N1) return;
+    const int m = (int)(i / N1);
+    const uint64_t r = i - (uint64_t)m * N1;
+    const uint64_t G1 = 3 * a.n_owned + 1, g = (uint64_t)m * a.n_owned + r, mb = (uint64_t)m * a.n_owned;
+    const uint64_t w = m == AD_MAP_RANGE ? 2 : 1;
+    a.o_keys_off[i] = (a.goff[0 * G1 + g] - a.goff[0 * G1 + mb]) / w;
+    a.o_txn_off[i] = a.goff[1 * G1 + g] - a.goff[1 * G1 + mb];
+    a.o_k2t_off[i] = a.goff[2 * G1 + g] - a.goff[2 * G1 + mb];
+}
+
 __global__ void k_merge_bases(MergeArgs a, uint64_t* out)
 {
     // out[3*m + k] = goff[k][m * n_owned] for m = 0..3 (m = 3: totals)
@@ -434,6 +685,31 @@ hipError_t run_merge_emit(const MergeArgs& a, hipStream_t st)
 {
     if (!a.n_owned) return hipSuccess;
     k_merge_emit<<<merge_blocks(3 * a.n_owned), 64 * XWAVES, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_global_map(const uint64_t* l_msb, const uint64_t* l_lo_norm, const int32_t* l_node, uint64_t n_local,
+                          const uint64_t* g_msb, const uint64_t* g_lsb, const int32_t* g_node, uint64_t n_global,
+                          uint32_t* map, uint32_t* err, hipStream_t st)
+{
+    if (!n_local) return hipSuccess;
+    k_global_map<<<(unsigned)((n_local + 255) / 256), 256, 0, st>>>(l_msb, l_lo_norm, l_node, n_local, g_msb, g_lsb,
+                                                                   g_node, n_global, map, err);
+    return hipGetLastError();
+}
+
+hipError_t run_merge_rank(const MergeArgs& a, hipStream_t st)
+{
+    if (!a.n_owned) return hipSuccess;
+    k_merge_rank<<<merge_blocks(3 * a.n_owned), 64 * XWAVES, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_merge_emit_rank(const MergeArgs& a, hipStream_t st)
+{
+    const uint64_t n_off = 3 * (a.n_owned + 1);
+    k_merge_out_offsets<<<(unsigned)((n_off + 255) / 256), 256, 0, st>>>(a);
+    if (a.n_parts) k_merge_emit_rank<<<(unsigned)((a.n_parts + 255) / 256), 256, 0, st>>>(a);
     return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ struct ExportArgs {
     const int64_t* txn_index;                     // [n] global request index (ascending)
     const uint64_t* dict_msb; const uint64_t* dict_lsb; const int32_t* dict_node;   // raw ids
     const int64_t* rt_start; const int64_t* rt_end;                                // range table
+    const uint32_t* gmap;                         // [n_dict] global rank of each dictionary id (null: triplets)
     uint32_t* sz;                                 // [4][3n] parts, key words, ids, k2t per item
     uint64_t* off;                                // [4][3n+1]
     int64_t* hdr; int64_t* okeys; int64_t* oids; int32_t* ok2t;
@@ -37,7 +38,17 @@ struct MergeArgs {
     uint32_t* error;
     uint64_t* o_keys_off; uint64_t* o_txn_off; uint64_t* o_k2t_off;   // [3][n_owned+1]
     int64_t* o_keys; int64_t* o_ids; int32_t* o_k2t;
+    // AD_IDS_RANK parts: ids are uint32 global ranks
+    uint32_t* u;                                  // [n_ids] union index of each received id | DUP_BIT
+    uint32_t* ppre;                               // [2][n_parts] key words / pairs of earlier parts of its group
+    uint64_t n_global;
+    const uint64_t* g_msb; const uint64_t* g_lsb; const int32_t* g_node;   // the global dictionary
 };
+
+// global rank of each local dictionary id (binary search in the global dictionary)
+hipError_t run_global_map(const uint64_t* l_msb, const uint64_t* l_lo_norm, const int32_t* l_node, uint64_t n_local,
+                          const uint64_t* g_msb, const uint64_t* g_lsb, const int32_t* g_node, uint64_t n_global,
+                          uint32_t* map, uint32_t* err, hipStream_t st);
 
 hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st);
 hipError_t run_export_emit(const ExportArgs& a, hipStream_t st);
@@ -48,5 +59,8 @@ hipError_t run_merge_slots(const MergeArgs& a, hipStream_t st);
 hipError_t run_merge_count(const MergeArgs& a, hipStream_t st);
 hipError_t run_merge_emit(const MergeArgs& a, hipStream_t st);
 hipError_t run_merge_bases(const MergeArgs& a, uint64_t* out, hipStream_t st);
+// AD_IDS_RANK merge: union ranks per group (wave per group), then thread-per-part emission
+hipError_t run_merge_rank(const MergeArgs& a, hipStream_t st);
+hipError_t run_merge_emit_rank(const MergeArgs& a, hipStream_t st);
 
 }  // namespace adx

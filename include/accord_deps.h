@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define AD_ABI_VERSION 1
+#define AD_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define AD_OK                  0
@@ -268,7 +268,21 @@ typedef struct ad_parts {
     int64_t* ids;
     int32_t* k2t;
     uint64_t cap_parts, cap_key_words, cap_ids, cap_k2t;  /* capacities of the arrays (export) */
+    uint32_t id_format;   /* AD_IDS_TRIPLET: ids as above; AD_IDS_RANK: ids holds n_ids uint32 ranks
+                           * into the global dictionary (ad_set_global_dict). Set by ad_parts_export,
+                           * read by ad_parts_merge. cap_ids counts ids in either format. */
 } ad_parts;
+
+#define AD_IDS_TRIPLET 0
+#define AD_IDS_RANK    1
+
+/* Global TxnId dictionary of a multi-store node: the ascending, duplicate-free union (Timestamp
+ * order) of the dictionaries (ad_dict) of every store taking part in the exchange, built once per
+ * snapshot (ingest time, not batch time). Host arrays. Every id of this ctx's dictionary must occur
+ * in it (AD_E_INVAL otherwise). While installed, ad_parts_export writes ids as uint32 global ranks
+ * (AD_IDS_RANK: 4 bytes on the wire instead of 24) and ad_parts_merge merges integer ranks and
+ * materialises the merged ids from this table; loading a new snapshot uninstalls it. */
+int ad_set_global_dict(ad_ctx* ctx, uint64_t n, const uint64_t* msb, const uint64_t* lsb, const int32_t* node);
 
 /* Export the device result `res_dev` of the last ad_deps_batch_device on ctx as parts, into
  * the caller's device arrays of `out` (capacities cap_*). txn_index_dev[i] is request i's

@@ -106,3 +106,76 @@ def test_transport_roundtrip():
     h, k, i, o, counts = parts_ref.encode(res, idx, np.array([0, len(w.queries)], np.uint64))
     back = parts_ref.decode(h, k, i, o, [counts[0, 0]], 100, len(w.queries))[0]
     assert back.equals(res)
+
+
+def test_build_global_dict_order_and_dups():
+    # Timestamp order: msb unsigned, then (lsb >>> 16, identity flags) unsigned, then node signed;
+    # ids equal under Timestamp.equals (non-identity lsb bits may differ) appear once, raw fields
+    # from the first store holding them
+    from accord_deps.model import Tids
+    rng = np.random.default_rng(3)
+    stores = []
+    for s in range(3):
+        n = 200
+        msb = rng.integers(0, 4, n).astype(np.uint64) | np.uint64(1 << 63) * rng.integers(0, 2, n).astype(np.uint64)
+        lsb = (rng.integers(0, 50, n).astype(np.uint64) << np.uint64(16)) | rng.integers(0, 16, n).astype(np.uint64) * 2
+        node = rng.integers(-3, 4, n).astype(np.int32)
+        stores.append(Tids(msb, lsb, node))
+    # a cross-store duplicate differing only in a non-identity flag bit (0x8000 REJECTED)
+    stores[2].msb[0], stores[2].lsb[0], stores[2].node[0] = stores[0].msb[5], stores[0].lsb[5] | np.uint64(0x8000), stores[0].node[5]
+    g = exchange.build_global_dict(stores)
+
+    def key(m, l, n):
+        return (int(m), (int(l) >> 16, (int(l) >> 1) & 0xF), int(n))
+    allk = {}
+    for s in stores:
+        for m, l, n in zip(s.msb, s.lsb, s.node):
+            allk.setdefault(key(m, l, n), (m, l, n))
+    want = sorted(allk)
+    got = [key(m, l, n) for m, l, n in zip(g.msb, g.lsb, g.node)]
+    assert got == want
+    i = want.index(key(stores[0].msb[5], stores[0].lsb[5], stores[0].node[5]))
+    assert int(g.lsb[i]) == int(stores[0].lsb[5])          # first store's raw fields
+
+
+class _DictEngine:
+    def __init__(self, rank):
+        from accord_deps.model import Tids
+        r = np.arange(10, dtype=np.uint64) * np.uint64(3) + np.uint64(rank)   # overlapping across ranks
+        self.d = Tids(np.ones(10, np.uint64), r << np.uint64(16), np.zeros(10, np.int32))
+        self.g = None
+
+    def dictionary(self):
+        return self.d
+
+    def set_global_dict(self, g):
+        self.g = g
+
+
+def _dict_main(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        e = _DictEngine(rank)
+        ex = exchange.ShardExchange(e, np.arange(4), 8, rank, world)
+        n = ex.install_global_dict()
+        out_q.put((rank, n, e.g.lsb.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_install_global_dict_collective():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dict_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = sorted(set((np.arange(10) * 3).tolist() + (np.arange(10) * 3 + 1).tolist()))
+    for rank, n, lsb in got:
+        assert n == len(want)
+        assert [x >> 16 for x in lsb] == want

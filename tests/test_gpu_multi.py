@@ -14,16 +14,18 @@ from accord_deps import exchange, native, synth
 pytestmark = pytest.mark.gpu
 
 UNITS = (("hdr", 4), ("keys", 1), ("ids", 3), ("k2t", 1))
+UNITS_RANK = (("hdr", 4), ("keys", 1), ("ids", 1), ("k2t", 1))
 
 
-def _parts(tensors, totals):
+def _parts(tensors, totals, rank_ids=False):
     p = A.AdParts()
     p.hdr, p.keys, p.ids, p.k2t = (tensors[k].data_ptr() for k in ("hdr", "keys", "ids", "k2t"))
     p.n_parts, p.n_key_words, p.n_ids, p.n_k2t = (int(x) for x in totals)
+    p.id_format = A.AD_IDS_RANK if rank_ids else A.AD_IDS_TRIPLET
     return p
 
 
-def _run_sharded(w, bounds, n_owners):
+def _run_sharded(w, bounds, n_owners, rank_ids=False):
     dev = torch.device("cuda", 0)
     lo, hi = bounds
     n_total = len(w.queries)
@@ -36,15 +38,25 @@ def _run_sharded(w, bounds, n_owners):
         qdev, k = native.device_queries(local.queries, dev)
         keep.append(k)
         e = exchange.GpuEngine(st, qdev, idx, dev)
+        engines.append((e, idx))
+    if rank_ids:
+        # the ingest-time global dictionary (what ShardExchange.install_global_dict gathers)
+        g = exchange.build_global_dict([e.dictionary() for e, _ in engines])
+        for e, _ in engines:
+            e.set_global_dict(g)
+    done = []
+    for e, idx in engines:
         e.resolve()
         dest_first = np.searchsorted(idx, np.asarray(bases[:n_owners], np.int64)).astype(np.uint64).tolist() + [len(idx)]
         send, counts = e.export(np.asarray(dest_first, np.uint64))
-        engines.append((e, send, counts))
+        done.append((e, send, counts))
+    engines = done
+    units = UNITS_RANK if rank_ids else UNITS
     torch.cuda.synchronize()
     out = []
     for d in range(n_owners):
         recv, totals, src_parts = {}, np.zeros(4, np.int64), []
-        for a, (name, mult) in enumerate(UNITS):
+        for a, (name, mult) in enumerate(units):
             pieces = []
             for e, send, counts in engines:
                 start = int(counts[:d, a].sum()) * mult
@@ -55,44 +67,55 @@ def _run_sharded(w, bounds, n_owners):
             src_parts.append(int(counts[d, 0]))
         owner = engines[d % len(engines)][0].store
         torch.cuda.synchronize()                 # recv tensors were built on torch's stream
-        mg = owner.merge_parts(_parts(recv, totals), src_parts, bases[d], bases[d + 1] - bases[d])
+        mg = owner.merge_parts(_parts(recv, totals, rank_ids), src_parts, bases[d], bases[d + 1] - bases[d])
         out.append((bases[d], bases[d + 1] - bases[d], owner.merged_to_host(mg), mg.ms_device))
     for e, _, _ in engines:
         e.store.close()
     return out
 
 
-def _check(w, bounds, n_owners):
+def _check(w, bounds, n_owners, rank_ids=False):
     expect = pyoracle.resolve_sharded(w, len(bounds[0]), bounds=bounds)
-    for base, n, got, _ in _run_sharded(w, bounds, n_owners):
+    for base, n, got, _ in _run_sharded(w, bounds, n_owners, rank_ids):
         ok, why = got.equals(expect.window(base, n), detail=True)
         if not ok:
             bad = got.first_mismatch(expect.window(base, n))
             pytest.fail("owner base %d: %s; first mismatch %s" % (base, why, bad[:2] if bad else None))
 
 
+@pytest.mark.parametrize("rank_ids", [False, True])
 @pytest.mark.parametrize("seed", range(12))
-def test_random_small_three_stores(seed):
+def test_random_small_three_stores(seed, rank_ids):
     w = synth.random_small(seed)
     w.slices = None
-    _check(w, synth.cut_bounds([-100, 150]), 2)
+    _check(w, synth.cut_bounds([-100, 150]), 2, rank_ids)
 
 
+@pytest.mark.parametrize("rank_ids", [False, True])
 @pytest.mark.parametrize("n_stores,n_owners", [(2, 2), (4, 4), (8, 8), (8, 3)])
-def test_config3_scaled(n_stores, n_owners):
+def test_config3_scaled(n_stores, n_owners, rank_ids):
     w = synth.config3(n_txns=40000, n_keys=6000, seed=11 + n_stores)
-    _check(w, synth.shard_bounds(n_stores), n_owners)
+    _check(w, synth.shard_bounds(n_stores), n_owners, rank_ids)
 
 
-def test_config4_ranges_sharded():
+@pytest.mark.parametrize("rank_ids", [False, True])
+def test_config4_ranges_sharded(rank_ids):
     w = synth.config4(n_txns=3000, n_keys=4000, n_ranges=800, n_hist_txns=3000)
     lo, hi = synth.cut_bounds([-(1 << 30), 0, 1 << 30])
-    _check(w, (lo, hi), 4)
+    _check(w, (lo, hi), 4, rank_ids)
 
 
-def test_config2_scaled_sharded():
+@pytest.mark.parametrize("rank_ids", [False, True])
+def test_config2_scaled_sharded(rank_ids):
     w = synth.config2(n_txns=20000, n_keys=20000, n_hist_entries=200000)
-    _check(w, synth.shard_bounds(4), 4)
+    _check(w, synth.shard_bounds(4), 4, rank_ids)
+
+
+def test_big_groups_rank_merge():
+    # hot keys with thousands of live entries on every store: merged groups beyond 64 ids take the
+    # binary-search path of the rank merge
+    w = synth.config2(n_txns=300, n_keys=40, n_hist_entries=60000, keys_per_txn=8, tail_unapplied=400)
+    _check(w, synth.shard_bounds(4), 2, rank_ids=True)
 
 
 def test_merge_rejects_overlapping_sources():
