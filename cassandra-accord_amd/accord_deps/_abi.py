@@ -108,7 +108,7 @@ class AdMerged(C.Structure):
                 ("txn_off", P * NMAPS), ("txns", P * NMAPS),
                 ("k2t_off", P * NMAPS), ("k2t", P * NMAPS),
                 ("n_keys", C.c_uint64 * NMAPS), ("n_ids", C.c_uint64 * NMAPS), ("n_k2t", C.c_uint64 * NMAPS),
-                ("ms_device", C.c_double)]
+                ("ms_device", C.c_double), ("id_format", C.c_uint32)]
 
 
 def ptr(a):

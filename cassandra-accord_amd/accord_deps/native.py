@@ -99,6 +99,7 @@ class DeviceCommandStore:
         cfg.elide = elide
         cfg.path = path
         self._keep = []
+        self.global_dict = None          # Tids installed with set_global_dict
         if slices is not None and len(slices):
             s = np.ascontiguousarray(np.asarray(slices, np.int64)[:, 0])
             e = np.ascontiguousarray(np.asarray(slices, np.int64)[:, 1])
@@ -146,6 +147,7 @@ class DeviceCommandStore:
         ls = np.ascontiguousarray(g.lsb, np.uint64)
         nd = np.ascontiguousarray(g.node, np.int32)
         self._check(lib().ad_set_global_dict(self.h, len(m), A.ptr(m), A.ptr(ls), A.ptr(nd)))
+        self.global_dict = Tids(m, ls, nd)
 
     def range_table(self):
         n = C.c_uint64()
@@ -239,10 +241,15 @@ class DeviceCommandStore:
             oo = self._d2h(mg.k2t_off[m], n + 1, np.uint64)
             w = 2 if m == A.AD_MAP_RANGE else 1
             kw = self._d2h(mg.keys[m], w * int(mg.n_keys[m]), np.int64)
-            ids = self._d2h(mg.txns[m], 3 * int(mg.n_ids[m]), np.int64).reshape(-1, 3)
             k2t = self._d2h(mg.k2t[m], int(mg.n_k2t[m]), np.int32)
-            txn = Tids(ids[:, 0].view(np.uint64).copy(), ids[:, 1].view(np.uint64).copy(),
-                       ids[:, 2].astype(np.int32))
+            if mg.id_format == A.AD_IDS_RANK:
+                if self.global_dict is None:
+                    raise ValueError("rank-format merge result without the global dictionary")
+                txn = self.global_dict.take(self._d2h(mg.txns[m], int(mg.n_ids[m]), np.uint32).astype(np.int64))
+            else:
+                ids = self._d2h(mg.txns[m], 3 * int(mg.n_ids[m]), np.int64).reshape(-1, 3)
+                txn = Tids(ids[:, 0].view(np.uint64).copy(), ids[:, 1].view(np.uint64).copy(),
+                           ids[:, 2].astype(np.int32))
             if m == A.AD_MAP_RANGE:
                 maps.append(DepsMap(ko, kw[0::2].copy(), kw[1::2].copy(), to, txn, oo, k2t))
             else:

@@ -854,6 +854,14 @@ static int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
     return 0;
 }
 
+// requests per wave of lean pass 1: four for batches of small requests (at most 3 keys on average,
+// e.g. a store's share of requests spanning many stores), else two. AD_LEAN_RPW overrides.
+static uint32_t lean_rpw1(uint64_t n, uint64_t np)
+{
+    if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 4 ? 4u : 2u;
+    return np <= 3 * n ? 4u : 2u;
+}
+
 static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out)
 {
     const uint64_t n = q->n_txns;
@@ -936,9 +944,9 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 // lean kernel first (newest requests, 2 per wave); the general fused kernel then
                 // takes only what it deferred (count read on the device, no host round trip)
                 if (!c->ev_lean1) HIPCHK(c, hipEventCreate(&c->ev_lean1));
-                HIPCHK(c, run_resolve_lean(c->ds, b, 1, st));
+                HIPCHK(c, run_resolve_lean(c->ds, b, 1, lean_rpw1(n, np), st));
                 HIPCHK(c, hipEventRecord(c->ev_lean1, st));
-                HIPCHK(c, run_resolve_lean(c->ds, b, 2, st));
+                HIPCHK(c, run_resolve_lean(c->ds, b, 2, 0, st));
                 HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 BatchBufs b2 = b;
                 b2.req_list = b.deferred2;
@@ -1513,7 +1521,8 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
                        err & 16 ? "id rank outside the global dictionary" :
                                   "ids of a part not sorted and unique");
     // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
-    if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, 3 * bases[10]) || !ens<int32_t>(c->m_k2t, bases[11]))
+    if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, rank_ids ? (bases[10] + 1) / 2 : 3 * bases[10]) ||
+        !ens<int32_t>(c->m_k2t, bases[11]))
         return c->fail(AD_E_NOMEM, "merge outputs");
     a.o_keys = c->m_keys.as<int64_t>();
     a.o_ids = c->m_ids.as<int64_t>();
@@ -1531,13 +1540,15 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     out->n_txns = n_owned;
     out->txn_base = txn_base;
     out->ms_device = ms;
+    out->id_format = rank_ids ? AD_IDS_RANK : AD_IDS_TRIPLET;
     for (int m = 0; m < 3; ++m)
     {
         out->keys_off[m] = a.o_keys_off + (uint64_t)m * (n_owned + 1);
         out->txn_off[m] = a.o_txn_off + (uint64_t)m * (n_owned + 1);
         out->k2t_off[m] = a.o_k2t_off + (uint64_t)m * (n_owned + 1);
         out->keys[m] = a.o_keys + bases[3 * m + 0];
-        out->txns[m] = a.o_ids + 3 * bases[3 * m + 1];
+        out->txns[m] = rank_ids ? reinterpret_cast<int64_t*>(reinterpret_cast<uint32_t*>(a.o_ids) + bases[3 * m + 1])
+                                : a.o_ids + 3 * bases[3 * m + 1];
         out->k2t[m] = a.o_k2t + bases[3 * m + 2];
         out->n_keys[m] = (bases[3 * (m + 1) + 0] - bases[3 * m + 0]) / (m == AD_MAP_RANGE ? 2 : 1);
         out->n_ids[m] = bases[3 * (m + 1) + 1] - bases[3 * m + 1];

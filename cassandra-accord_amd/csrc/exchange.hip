@@ -75,59 +75,61 @@ __global__ void k_export_sizes(ExportArgs a)
     a.sz[3 * items + i] = live ? (uint32_t)no : 0u;
 }
 
-// one 8-lane group per (request, map) item
+// one 8-lane group per request, its three maps in turn
 __global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
 {
     const uint64_t items = 3 * a.n;
     const uint32_t g8 = threadIdx.x & 7;
-    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
-    if (i >= items) return;
-    const uint64_t r = i / 3;
-    const int m = (int)(i % 3);
-    const uint64_t k0 = a.keys_off[m][r], nk = a.keys_off[m][r + 1] - k0;
-    if (nk == 0) return;
-    const uint64_t t0 = a.txn_off[m][r], nt = a.txn_off[m][r + 1] - t0;
-    const uint64_t o0 = a.k2t_off[m][r], no = a.k2t_off[m][r + 1] - o0;
-    const uint64_t P = a.off[0 * (items + 1) + i];
-    const uint64_t KW = a.off[1 * (items + 1) + i];
-    const uint64_t ID = a.off[2 * (items + 1) + i];
-    const uint64_t KO = a.off[3 * (items + 1) + i];
-    if (g8 == 0)
+    const uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+    if (r >= a.n) return;
+    for (int m = 0; m < 3; ++m)
     {
-        int64_t* h = a.hdr + 4 * P;
-        h[0] = (a.txn_index[r] << 2) | m;
-        h[1] = (int64_t)nk;
-        h[2] = (int64_t)nt;
-        h[3] = (int64_t)no;
-    }
-    if (m == AD_MAP_RANGE)
-    {
-        for (uint64_t j = g8; j < nk; j += 8)
+        const uint64_t i = 3 * r + m;
+        const uint64_t k0 = a.keys_off[m][r], nk = a.keys_off[m][r + 1] - k0;
+        if (nk == 0) continue;
+        const uint64_t t0 = a.txn_off[m][r], nt = a.txn_off[m][r + 1] - t0;
+        const uint64_t o0 = a.k2t_off[m][r], no = a.k2t_off[m][r + 1] - o0;
+        const uint64_t P = a.off[0 * (items + 1) + i];
+        const uint64_t KW = a.off[1 * (items + 1) + i];
+        const uint64_t ID = a.off[2 * (items + 1) + i];
+        const uint64_t KO = a.off[3 * (items + 1) + i];
+        if (g8 == 0)
         {
-            const int64_t rid = a.keys[m][k0 + j];
-            a.okeys[KW + 2 * j] = a.rt_start[rid];
-            a.okeys[KW + 2 * j + 1] = a.rt_end[rid];
+            int64_t* h = a.hdr + 4 * P;
+            h[0] = (a.txn_index[r] << 2) | m;
+            h[1] = (int64_t)nk;
+            h[2] = (int64_t)nt;
+            h[3] = (int64_t)no;
         }
-    }
-    else
-    {
-        for (uint64_t j = g8; j < nk; j += 8) a.okeys[KW + j] = a.keys[m][k0 + j];
-    }
-    if (a.gmap)
-    {
-        uint32_t* o = reinterpret_cast<uint32_t*>(a.oids) + ID;
-        for (uint64_t j = g8; j < nt; j += 8) o[j] = a.gmap[a.txns[m][t0 + j]];
-    }
-    else
-        for (uint64_t j = g8; j < nt; j += 8)
+        if (m == AD_MAP_RANGE)
         {
-            const uint32_t d = a.txns[m][t0 + j];
-            int64_t* o = a.oids + 3 * (ID + j);
-            o[0] = (int64_t)a.dict_msb[d];
-            o[1] = (int64_t)a.dict_lsb[d];
-            o[2] = (int64_t)a.dict_node[d];
+            for (uint64_t j = g8; j < nk; j += 8)
+            {
+                const int64_t rid = a.keys[m][k0 + j];
+                a.okeys[KW + 2 * j] = a.rt_start[rid];
+                a.okeys[KW + 2 * j + 1] = a.rt_end[rid];
+            }
         }
-    for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = a.k2t[m][o0 + j];
+        else
+        {
+            for (uint64_t j = g8; j < nk; j += 8) a.okeys[KW + j] = a.keys[m][k0 + j];
+        }
+        if (a.gmap)
+        {
+            uint32_t* o = reinterpret_cast<uint32_t*>(a.oids) + ID;
+            for (uint64_t j = g8; j < nt; j += 8) o[j] = a.gmap[a.txns[m][t0 + j]];
+        }
+        else
+            for (uint64_t j = g8; j < nt; j += 8)
+            {
+                const uint32_t d = a.txns[m][t0 + j];
+                int64_t* o = a.oids + 3 * (ID + j);
+                o[0] = (int64_t)a.dict_msb[d];
+                o[1] = (int64_t)a.dict_lsb[d];
+                o[2] = (int64_t)a.dict_node[d];
+            }
+        for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = a.k2t[m][o0 + j];
+    }
 }
 
 __global__ void k_export_bounds(ExportArgs a, const uint64_t* dest_first, uint32_t n_dest, uint64_t* counts)
@@ -167,9 +169,15 @@ __global__ void k_merge_slots(MergeArgs a)
         atomicOr(a.error, 1u);
         return;
     }
+    // a source exports its parts by ascending (request, map): one part per group and source
+    // exactly when each part's (request, map) is above its predecessor's in the same source
+    if (p > a.src_first[s])
+    {
+        const int64_t hp = a.hdr[4 * (p - 1)];
+        if (((hp >> 2) << 2 | (hp & 3)) >= ((t << 2) | m)) atomicOr(a.error, 2u);
+    }
     const uint64_t g = (uint64_t)m * a.n_owned + (uint64_t)(t - (int64_t)a.txn_base);
-    const int32_t prev = atomicExch(&a.slot[g * a.n_src + s], (int32_t)p);
-    if (prev != -1) atomicOr(a.error, 2u);          // two parts of one request and map from one store
+    a.slot[g * a.n_src + s] = (int32_t)p;
 }
 
 // The parts of group g in source order, staged in wave-private LDS so that lanes in divergent
@@ -560,10 +568,13 @@ __global__ void __launch_bounds__(64 * XWAVES) k_merge_rank(MergeArgs a)
     }
 }
 
-// thread per part: its slice of the group's keys, union ids and keysToTxnIds
+// 8 lanes per part: its slice of the group's keys, union ids and keysToTxnIds
+constexpr uint32_t EMIT_LANES = 8;
+
 __global__ void k_merge_emit_rank(MergeArgs a)
 {
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t p = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / EMIT_LANES;
+    const uint32_t j8 = threadIdx.x % EMIT_LANES;
     if (p >= a.n_parts) return;
     const uint64_t n_groups = 3 * a.n_owned, G1 = n_groups + 1, P1 = a.n_parts + 1;
     const int64_t h0 = a.hdr[4 * p];
@@ -575,22 +586,18 @@ __global__ void k_merge_emit_rank(MergeArgs a)
     const uint64_t KW = a.goff[0 * G1 + g], ID = a.goff[1 * G1 + g], KO = a.goff[2 * G1 + g];
     const uint32_t nkeys_total = a.gsz[0 * n_groups + g] / w;
     const uint32_t kwb = a.ppre[2 * p], prb = a.ppre[2 * p + 1];
-    for (uint32_t e = 0; e < nk * w; ++e) a.o_keys[KW + kwb + e] = a.keys[kbase + e];
+    for (uint32_t e = j8; e < nk * w; e += EMIT_LANES) a.o_keys[KW + kwb + e] = a.keys[kbase + e];
     const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
-    for (uint32_t e = 0; e < ni; ++e)
+    for (uint32_t e = j8; e < ni; e += EMIT_LANES)
     {
         const uint32_t uu = a.u[ibase + e];
         if (uu & DUP_BIT) continue;
-        const uint32_t x = ids[ibase + e];
-        int64_t* o = a.o_ids + 3 * (ID + uu);
-        o[0] = (int64_t)a.g_msb[x];
-        o[1] = (int64_t)a.g_lsb[x];
-        o[2] = (int64_t)a.g_node[x];
+        reinterpret_cast<uint32_t*>(a.o_ids)[ID + uu] = ids[ibase + e];     // the global rank
     }
     const uint32_t kb = kwb / w;
-    for (uint32_t e = 0; e < nk; ++e)
+    for (uint32_t e = j8; e < nk; e += EMIT_LANES)
         a.o_k2t[KO + kb + e] = (int32_t)((uint64_t)a.k2t[obase + e] - nk + nkeys_total + prb);
-    for (uint32_t v = 0; v < no - nk; ++v)
+    for (uint32_t v = j8; v < no - nk; v += EMIT_LANES)
     {
         const uint32_t idx = (uint32_t)a.k2t[obase + nk + v];
         if (idx >= ni)
@@ -638,9 +645,8 @@ hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st)
 
 hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
 {
-    const uint64_t items = 3 * a.n;
-    if (!items) return hipSuccess;
-    const uint64_t threads = items * 8;
+    if (!a.n) return hipSuccess;
+    const uint64_t threads = a.n * 8;
     k_export_emit<<<(unsigned)((threads + 64 * XWAVES - 1) / (64 * XWAVES)), 64 * XWAVES, 0, st>>>(a);
     return hipGetLastError();
 }
@@ -709,7 +715,8 @@ hipError_t run_merge_emit_rank(const MergeArgs& a, hipStream_t st)
 {
     const uint64_t n_off = 3 * (a.n_owned + 1);
     k_merge_out_offsets<<<(unsigned)((n_off + 255) / 256), 256, 0, st>>>(a);
-    if (a.n_parts) k_merge_emit_rank<<<(unsigned)((a.n_parts + 255) / 256), 256, 0, st>>>(a);
+    const uint64_t threads = a.n_parts * EMIT_LANES;
+    if (a.n_parts) k_merge_emit_rank<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(a);
     return hipGetLastError();
 }
 

@@ -80,7 +80,7 @@ constexpr uint32_t DEFER_HOLE = 0xFFFFFFFFu;      // unused slot of a wave's def
 constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave reserves at a time
 constexpr uint32_t REC_FAST = 1u << 24;          // q_rec: newest fast path applies (S, self, <= 8 keys, valid kind)
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
-hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, hipStream_t st);
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,

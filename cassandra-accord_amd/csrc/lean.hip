@@ -1,7 +1,7 @@
 // lean.hip — the lean fused kernel: the common case of PreAccept.calculatePartialDeps
 // (PreAccept.java:245-267) on a CommandStore without range commands or RedundantBefore entries,
-// for requests newer than everything the store holds. Two requests per wave (lanes 0-31 and
-// 32-63), no LDS, no trees:
+// for requests newer than everything the store holds. Two (or four) requests per wave (lanes 0-31
+// and 32-63), no LDS, no trees:
 //
 //   * executeAt (and txnId) newer than every dictionary id: S = 2 * n_dict without a search
 //   * every key newest (S above its last txnId and its last committed Write's executeAt): the
@@ -102,7 +102,8 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
     return v;
 }
 
-// RPW requests per wave (2: 32 lanes each, up to 32 raw emissions; 1: 64 lanes, up to 64).
+// RPW requests per wave (4: 16 lanes each, up to 16 raw emissions -- batches of small requests,
+// e.g. a store's share of requests spanning many stores; 2: 32 lanes, up to 32; 1: 64 lanes, up to 64).
 // RNG: the store has range commands (with a stabbing index): each request also gets its
 // rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
 template <uint32_t RPW, bool RNG>
@@ -111,7 +112,15 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     constexpr uint32_t LPR = 64 / RPW;                       // lanes per request
     const uint32_t lane = lane_id(), h = lane / LPR, hl = lane & (LPR - 1), sb = h * LPR;
     const uint64_t below = (1ull << hl) - 1;                 // lanes below this one in its segment
-    auto seg = [&](uint64_t m) -> uint64_t { return RPW == 1 ? m : ((m >> sb) & 0xFFFFFFFFull); };
+    constexpr uint64_t SEGMASK = LPR == 64 ? ~0ull : ((1ull << LPR) - 1);
+    auto seg = [&](uint64_t m) -> uint64_t { return RPW == 1 ? m : ((m >> sb) & SEGMASK); };
+    // wave-uniform max over the segments' values of v (read at each segment's lane 0)
+    auto seg_max = [&](uint32_t v) -> uint32_t {
+        uint32_t mx = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < RPW; ++k) mx = max(mx, (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(k * LPR)));
+        return mx;
+    };
     const uint64_t n = b.n_txns;
     const uint64_t n_slots = io.in ? uniform64(*io.in_count) : n;
     const uint64_t n_items = (n_slots + RPW - 1) / RPW;
@@ -120,6 +129,21 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     const uint32_t S = s.n_dict ? (uint32_t)(2 * s.n_dict) : 0u;   // rank of an id above every member
     const uint32_t self = 0;   // exec == txnId: none; else a non-member rank (even): never an emission
     LeanChunk ralloc;
+    // one wave-uniform region allocation for the segments' byte counts (at each segment's lane 0):
+    // returns this segment's offset; `fits` whether the whole allocation is inside the arena
+    auto seg_alloc = [&](uint64_t bytes, bool& fits) -> uint64_t {
+        uint64_t total = 0, mine = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < RPW; ++k)
+        {
+            const uint64_t bk = uniform64(__shfl(bytes, (int)(k * LPR), 64));
+            if (k == h) mine = total;
+            total += bk;
+        }
+        const uint64_t base = ralloc.take(b.ctl, total, reg_cap);
+        fits = base + total <= reg_cap;
+        return base + mine;
+    };
     // deferrals are gathered in a per-wave LDS buffer and appended to the out list in exact-size
     // blocks (one atomic per block, no holes)
     __shared__ uint32_t dbuf_all[LEAN_WAVES][DEFER_CHUNK];
@@ -323,9 +347,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             // sort (rank, key) per request; dedup -> txnIds; body = unique-rank index per key, ascending
             uint32_t k = mine ? ((r << 3) | a) : 0xFFFFFFFFu;
             // the sort must span every lane that may hold one (raw emissions: lanes [0, T))
-            const uint32_t kmax = RPW == 1 ? uniform(T) : uniform(max(__shfl(T, 0, 64), __shfl(T, 32, 64)));
+            const uint32_t kmax = seg_max(T);
             if (kmax <= 8) seg_bitonic<8, LPR>(k);
-            else if (kmax <= 16) seg_bitonic<16, LPR>(k);
+            else if (kmax <= 16 || LPR == 16) seg_bitonic<16, LPR>(k);
             else if (kmax <= 32 || LPR == 32) seg_bitonic<(LPR < 32 ? LPR : 32), LPR>(k);
             else seg_bitonic<LPR, LPR>(k);
             const bool valid = hl < tot;
@@ -367,11 +391,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             const uint32_t kstart = __shfl(kstart_l, sb | ka, 64);
             // regions of the wave's requests from one wave-uniform allocation
             const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
-            const uint64_t bA = uniform64(__shfl(bytes, 0, 64));
-            const uint64_t bB = RPW == 1 ? 0 : uniform64(__shfl(bytes, 32, 64));
-            const uint64_t base = ralloc.take(b.ctl, bA + bB, reg_cap);
-            const uint64_t ro = h ? base + bA : base;
-            const bool fits = base + bA + bB <= reg_cap;
+            bool fits;
+            const uint64_t ro = seg_alloc(bytes, fits);
             if (act && hl == 0)
             {
                 b.sz[(3 * m) * n + t] = fits ? nk : 0;
@@ -409,10 +430,10 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         }
         else
         {
-            const uint32_t kmaxr = RPW == 1 ? uniform(TR) : uniform(max(__shfl(TR, 0, 64), __shfl(TR, 32, 64)));
+            const uint32_t kmaxr = seg_max(TR);
             uint64_t pk = rwant ? ((ce & 0xFFFFFFFF00000000ull) | rk) : ~0ull;
             if (kmaxr <= 8) seg_bitonic64<8, LPR>(pk);
-            else if (kmaxr <= 16) seg_bitonic64<16, LPR>(pk);
+            else if (kmaxr <= 16 || LPR == 16) seg_bitonic64<16, LPR>(pk);
             else if (kmaxr <= 32 || LPR == 32) seg_bitonic64<(LPR < 32 ? LPR : 32), LPR>(pk);
             else seg_bitonic64<LPR, LPR>(pk);
             const uint32_t totp = __popcll(seg(rmb));
@@ -443,7 +464,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             // distinct txnIds of the pairs: sort (rank, pair index)
             uint64_t k2 = uplive ? (((uint64_t)urk << 8) | hl) : ~0ull;
             if (kmaxr <= 8) seg_bitonic64<8, LPR>(k2);
-            else if (kmaxr <= 16) seg_bitonic64<16, LPR>(k2);
+            else if (kmaxr <= 16 || LPR == 16) seg_bitonic64<16, LPR>(k2);
             else if (kmaxr <= 32 || LPR == 32) seg_bitonic64<(LPR < 32 ? LPR : 32), LPR>(k2);
             else seg_bitonic64<LPR, LPR>(k2);
             const uint64_t p2 = __shfl_up(k2, 1, LPR);
@@ -453,11 +474,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             const uint32_t UR = __popcll(um2);
             const uint32_t ur2 = __popcll(um2 & below) + (uq2 ? 1u : 0u) - 1u;
             const uint64_t bytes = act && totp ? (((uint64_t)nR * 8 + (uint64_t)UR * 4 + (uint64_t)(nR + UP) * 4 + 7) & ~7ull) : 0;
-            const uint64_t bA = uniform64(__shfl(bytes, 0, 64));
-            const uint64_t bB = RPW == 1 ? 0 : uniform64(__shfl(bytes, 32, 64));
-            const uint64_t base = ralloc.take(b.ctl, bA + bB, reg_cap);
-            const uint64_t ro = h ? base + bA : base;
-            const bool fits = base + bA + bB <= reg_cap;
+            bool fits;
+            const uint64_t ro = seg_alloc(bytes, fits);
             if (act && hl == 0)
             {
                 b.sz[3 * n + t] = fits ? nR : 0;
@@ -473,7 +491,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
                 if (gfirst)
                 {
                     const uint32_t gi = __popcll(gm & below);
-                    const uint64_t later = gm & ~((2ull << hl) - 1) & (LPR == 64 ? ~0ull : 0xFFFFFFFFull);
+                    const uint64_t later = gm & ~((2ull << hl) - 1) & SEGMASK;
                     const uint32_t gend = later ? (uint32_t)(__ffsll((unsigned long long)later) - 1) : UP;
                     okeys[gi] = (int64_t)rid;                          // range id (ad_range_table)
                     ok2t[gi] = (int32_t)(nR + gend);
@@ -513,12 +531,13 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, const Le
 }
 
 // pass 1: every request, two per wave -> D1; pass 2: D1, one per wave (up to 64 emissions) -> D2
-hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, hipStream_t st)
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
     if (pass == 1)
     {
         LeanLists p1{nullptr, nullptr, b.deferred1, &b.ctl->n_deferred1, &b.ctl->n_real1};
+        if (rpw1 == 4) return s.n_rent ? launch_lean<4, true>(s, b, p1, st) : launch_lean<4, false>(s, b, p1, st);
         return s.n_rent ? launch_lean<2, true>(s, b, p1, st) : launch_lean<2, false>(s, b, p1, st);
     }
     LeanLists p2{b.deferred1, &b.ctl->n_deferred1, b.deferred2, &b.ctl->n_deferred2, &b.ctl->n_real2};

@@ -293,7 +293,7 @@ int ad_set_global_dict(ad_ctx* ctx, uint64_t n, const uint64_t* msb, const uint6
 int ad_parts_export(ad_ctx* ctx, const ad_deps_result* res_dev, const int64_t* txn_index_dev, uint32_t n_dest,
                     const uint64_t* dest_first, void* stream, ad_parts* out, uint64_t* dest_counts);
 
-/* Merged PartialDeps of the requests a GPU owns, materialised (ids as {msb,lsb,node}).
+/* Merged PartialDeps of the requests a GPU owns (ids as {msb,lsb,node}, or as global ranks, id_format).
  * For owned request r (global index txn_base + r) and map m: keys [keys_off[m][r], keys_off[m][r+1])
  * (AD_MAP_RANGE: ranges, 2 words each in keys[m]), txns [txn_off[m][r], ..) as triplets,
  * k2t [k2t_off[m][r], ..) the keysToTxnIds of the merged RelationMultiMap. Device memory owned
@@ -309,6 +309,9 @@ typedef struct ad_merged {
     int32_t*  k2t[AD_NMAPS];
     uint64_t  n_keys[AD_NMAPS], n_ids[AD_NMAPS], n_k2t[AD_NMAPS];   /* totals per map           */
     double    ms_device;
+    uint32_t  id_format;   /* AD_IDS_TRIPLET: txns as {msb,lsb,node} int64 triplets; AD_IDS_RANK (merges of
+                            * rank-format parts): txns[m] holds n_ids[m] uint32 ranks into the global
+                            * dictionary the caller installed (ad_set_global_dict), ascending per request */
 } ad_merged;
 
 /* Merge the parts received from n_src stores (concatenated in source = slice order; source s

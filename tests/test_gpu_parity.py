@@ -43,16 +43,20 @@ def test_random_larger(oracle, seed):
     _compare(w, oracle)
 
 
+@pytest.mark.parametrize("rpw", ["2", "4"])
 @pytest.mark.parametrize("seed", range(16))
-def test_random_small_lean_store(oracle, seed):
+def test_random_small_lean_store(oracle, seed, rpw, monkeypatch):
+    monkeypatch.setenv("AD_LEAN_RPW", rpw)     # lean pass 1 with two or four requests per wave
     # no range commands / redundant-before: the lean kernel runs first; older requests defer
     w = synth.random_small(500 + seed, n_range_cmds=0, n_redundant=0, accept_frac=0.2 * (seed % 4),
                            max_keys=2 + seed % 7)
     _compare(w, oracle, paths=(0,))
 
 
+@pytest.mark.parametrize("rpw", ["2", "4"])
 @pytest.mark.parametrize("seed", range(16))
-def test_random_small_lean_ranges(oracle, seed):
+def test_random_small_lean_ranges(oracle, seed, rpw, monkeypatch):
+    monkeypatch.setenv("AD_LEAN_RPW", rpw)
     # range commands with their stabbing index, no redundant-before: the lean kernel also builds
     # rangeDeps (multi-range commands, both range conventions, slices, erased ranges)
     w = synth.random_small(800 + seed, n_range_cmds=10 + 6 * seed, n_redundant=0, accept_frac=0.1 * (seed % 3),
@@ -77,6 +81,9 @@ def test_config2_lean_classes(oracle, esp, sync, reads, monkeypatch):
         w.queries.exec.lsb[:] = w.queries.txn.lsb
     got, exp = _compare(w, oracle, paths=(0,))
     assert got.stats["n_deferred_lean"] < len(w.queries)
+    monkeypatch.setenv("AD_LEAN_RPW", "4")
+    assert native.resolve(w).equals(exp)
+    monkeypatch.delenv("AD_LEAN_RPW")
     monkeypatch.setenv("AD_NO_LEAN", "1")
     got2 = native.resolve(w)
     assert got2.equals(exp)
