@@ -304,14 +304,15 @@ def bench_sequential(args, rank, world, local, dev):
     inserted as PREACCEPTED before its deps). SEQUENTIAL runs through the host API: a step is one
     snapshot upload + ad_deps_batch call on one store -- host arrays in and out, snapshot ingest (the
     batch's own PreAccepts) and PCIe included, so this line is latency, not the device-resident
-    throughput of configs 2/4."""
+    throughput of configs 2/4. The result stays in the C ABI's host CSR arrays (what a Java caller
+    wraps with KeyDeps.SerializerSupport.create); Python objects are not built in the timed step."""
     w = synth.config1(seed=0xACC0D001 + rank)
     st = native.DeviceCommandStore(device=local)
 
     def step():
         # SEQUENTIAL inserts the batch into the store: every step re-uploads the initial snapshot
-        st.load(w)
-        return st.calculate_partial_deps(w.queries, w.flags).stats
+        st.load(w, prepare=False)
+        return st.deps_batch_stats(w.queries, w.flags)
     elapsed, all_stats = _timed_steps(args, world, dev, step)
     st.close()
     pairs = _sum_over_ranks(world, dev, w.queries.n_probes)

@@ -176,6 +176,18 @@ class DeviceCommandStore:
             L.ad_result_free(out)
         return self.materialise(raw, stats)
 
+    def deps_batch_stats(self, queries, flags=A.AD_SNAPSHOT):
+        """ad_deps_batch as a host caller uses it (host arrays in, host CSR arrays out; snapshot
+        ingest, PCIe and device work included), without building Python objects from the result.
+        Returns the stats dict."""
+        L = lib()
+        out = C.POINTER(A.AdDepsResult)()
+        self._check(L.ad_deps_batch(self.h, C.byref(queries.soa()), flags, C.byref(out)))
+        try:
+            return stats_dict(out.contents.stats)
+        finally:
+            L.ad_result_free(out)
+
     def materialise(self, raw, stats=None):
         d = self.dictionary()
         rs, re = self.range_table()
