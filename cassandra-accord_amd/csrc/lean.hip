@@ -107,8 +107,14 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
 // RNG: the store has range commands (with a stabbing index): each request also gets its
 // rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
 template <uint32_t RPW, bool RNG>
-__global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s, BatchBufs b, LeanLists io)
+__global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s, BatchBufs b, uint32_t pass)
 {
+    // pass 1: all requests -> deferred1; pass 2: deferred1 -> deferred2 (lists derived from b
+    // where used, so they hold no scalar registers across the loop)
+    auto lists = [&]() -> LeanLists {
+        if (pass == 1) return LeanLists{nullptr, nullptr, b.deferred1, &b.ctl->n_deferred1, &b.ctl->n_real1};
+        return LeanLists{b.deferred1, &b.ctl->n_deferred1, b.deferred2, &b.ctl->n_deferred2, &b.ctl->n_real2};
+    };
     constexpr uint32_t LPR = 64 / RPW;                       // lanes per request
     const uint32_t lane = lane_id(), h = lane / LPR, hl = lane & (LPR - 1), sb = h * LPR;
     const uint64_t below = (1ull << hl) - 1;                 // lanes below this one in its segment
@@ -122,9 +128,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         return mx;
     };
     const uint64_t n = b.n_txns;
-    const uint64_t n_slots = io.in ? uniform64(*io.in_count) : n;
-    const uint64_t n_items = (n_slots + RPW - 1) / RPW;
-    const uint64_t nw = (uint64_t)gridDim.x * LEAN_WAVES;
+    const uint32_t n_slots = pass == 1 ? (uint32_t)n : (uint32_t)uniform64(b.ctl->n_deferred1);
+    const uint32_t n_items = (n_slots + RPW - 1) / RPW;
+    const uint32_t nw = gridDim.x * LEAN_WAVES;
     const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
     const uint32_t S = s.n_dict ? (uint32_t)(2 * s.n_dict) : 0u;   // rank of an id above every member
     const uint32_t self = 0;   // exec == txnId: none; else a non-member rank (even): never an emission
@@ -154,12 +160,13 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         unsigned long long base = 0;
         if (lane_id() == 0)
         {
+            const LeanLists io = lists();
             base = atomicAdd(io.out_count, (unsigned long long)dn);
             atomicAdd(io.out_real, (unsigned long long)dn);
         }
         base = uniform64(base);
         wave_lds_sync();
-        if (lane_id() < dn) io.out[base + lane_id()] = dbuf[lane_id()];
+        if (lane_id() < dn) lists().out[base + lane_id()] = dbuf[lane_id()];
         wave_lds_sync();
         dn = 0;
     };
@@ -171,10 +178,10 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     // (clamped addresses, results masked where used) so the compiler's wait counts stay exact.
     using Raw = uint4;        // the request record of k_prepare
     struct Req { uint64_t k0; uint32_t np, cls, t; bool act, defer; };
-    auto req_of = [&](uint64_t it) -> uint32_t {
-        const uint64_t si = it * RPW + h;
+    auto req_of = [&](uint32_t it) -> uint32_t {
+        const uint32_t si = it * RPW + h;
         if (si >= n_slots) return DEFER_HOLE;
-        return io.in ? io.in[si] : (uint32_t)si;
+        return pass == 1 ? (uint32_t)si : b.deferred1[si];
     };
     auto loadA = [&](uint32_t t) -> Raw { return b.q_rec[t != DEFER_HOLE ? t : 0u]; };
     // the record carries PreAccept.java:251-261's witness class and whether S and self take the
@@ -221,7 +228,18 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         qc = e[1 + cls];
     };
 
-    const uint64_t it0 = uniform64((uint64_t)blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
+    // sizes of map m (keys, txnIds, keysToTxnIds) and its region offset: one store from lanes
+    // hl = 0..3 of each segment (per-lane addresses keep the size arrays out of scalar registers)
+    auto put_sizes = [&](bool on, uint32_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro, bool with_ro) {
+        if (on && hl < 3)
+        {
+            const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);
+            b.sz[(uint64_t)(3 * m + hl) * n + t] = v;
+        }
+        if (with_ro && on && hl == 3) b.t_reg[(uint64_t)m * n + t] = ro;
+    };
+
+    const uint32_t it0 = uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
     uint32_t tc = req_of(it0);
     Req qc = derive(tc, loadA(tc));
     int64_t keyc;
@@ -234,7 +252,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     uint32_t tN = req_of(it0 + nw);
     Raw rN = loadA(tN);
 
-    for (uint64_t it = it0; it < n_items; it += nw)
+    for (uint32_t it = it0; it < n_items; it += nw)
     {
         const uint32_t t = qc.t;
         const Req qn = derive(tN, rN);
@@ -336,12 +354,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             const uint32_t tot = __popcll(seg(mb));
             if (mb == 0)
             {
-                if (act && hl == 0)
-                {
-                    b.sz[(3 * m) * n + t] = 0;
-                    b.sz[(3 * m + 1) * n + t] = 0;
-                    b.sz[(3 * m + 2) * n + t] = 0;
-                }
+                put_sizes(act, t, m, 0, 0, 0, 0, false);
                 continue;
             }
             // sort (rank, key) per request; dedup -> txnIds; body = unique-rank index per key, ascending
@@ -393,13 +406,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits);
-            if (act && hl == 0)
-            {
-                b.sz[(3 * m) * n + t] = fits ? nk : 0;
-                b.sz[(3 * m + 1) * n + t] = fits ? U : 0;
-                b.sz[(3 * m + 2) * n + t] = fits ? nk + tot : 0;
-                b.t_reg[(uint64_t)m * n + t] = ro;
-            }
+            put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
             if (act && tot && fits)
             {
                 int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
@@ -421,12 +428,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         const uint64_t rmb = ballot(rwant);
         if (!RNG || rmb == 0)
         {
-            if (act && hl == 0)
-            {
-                b.sz[3 * n + t] = 0;
-                b.sz[4 * n + t] = 0;
-                b.sz[5 * n + t] = 0;
-            }
+            put_sizes(act, t, 1, 0, 0, 0, 0, false);
         }
         else
         {
@@ -476,13 +478,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             const uint64_t bytes = act && totp ? (((uint64_t)nR * 8 + (uint64_t)UR * 4 + (uint64_t)(nR + UP) * 4 + 7) & ~7ull) : 0;
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits);
-            if (act && hl == 0)
-            {
-                b.sz[3 * n + t] = fits ? nR : 0;
-                b.sz[4 * n + t] = fits ? UR : 0;
-                b.sz[5 * n + t] = fits ? nR + UP : 0;
-                b.t_reg[(uint64_t)1 * n + t] = ro;
-            }
+            put_sizes(act, t, 1, fits ? nR : 0, fits ? UR : 0, fits ? nR + UP : 0, ro, true);
             if (act && totp && fits)
             {
                 int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
@@ -512,7 +508,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
 }
 
 template <uint32_t RPW, bool RNG>
-static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, const LeanLists& io, hipStream_t st)
+static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, uint32_t pass, hipStream_t st)
 {
     static int per_cu = 0;
     if (!per_cu)
@@ -526,7 +522,7 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, const Le
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu));
-    k_resolve_lean<RPW, RNG><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, io);
+    k_resolve_lean<RPW, RNG><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, pass);
     return hipGetLastError();
 }
 
@@ -536,12 +532,10 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     if (!b.n_txns) return hipSuccess;
     if (pass == 1)
     {
-        LeanLists p1{nullptr, nullptr, b.deferred1, &b.ctl->n_deferred1, &b.ctl->n_real1};
-        if (rpw1 == 4) return s.n_rent ? launch_lean<4, true>(s, b, p1, st) : launch_lean<4, false>(s, b, p1, st);
-        return s.n_rent ? launch_lean<2, true>(s, b, p1, st) : launch_lean<2, false>(s, b, p1, st);
+        if (rpw1 == 4) return s.n_rent ? launch_lean<4, true>(s, b, 1, st) : launch_lean<4, false>(s, b, 1, st);
+        return s.n_rent ? launch_lean<2, true>(s, b, 1, st) : launch_lean<2, false>(s, b, 1, st);
     }
-    LeanLists p2{b.deferred1, &b.ctl->n_deferred1, b.deferred2, &b.ctl->n_deferred2, &b.ctl->n_real2};
-    return s.n_rent ? launch_lean<1, true>(s, b, p2, st) : launch_lean<1, false>(s, b, p2, st);
+    return s.n_rent ? launch_lean<1, true>(s, b, 2, st) : launch_lean<1, false>(s, b, 2, st);
 }
 
 }  // namespace adx
