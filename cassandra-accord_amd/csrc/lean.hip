@@ -382,14 +382,11 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
                 same &= ((ka >> bit) & 1u) ? bb : ~bb;
             }
             const uint32_t pos_in_key = __popcll(seg(same) & below);
-            // per key p (lanes hl < 8): its number of values, then body starts and heads
-            uint32_t cnt = 0;
-#pragma unroll
-            for (uint32_t p = 0; p < LEAN_MAXP; ++p)
-            {
-                const uint32_t c = __popcll(seg(ballot(valid && ka == p)));
-                if (hl == p) cnt = c;
-            }
+            // per key p (lanes hl < 8): its number of values = its map-m emissions, counted over its
+            // raw lane range [start, start + nn) (a key's list holds distinct txnIds), then body
+            // starts and heads
+            const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
+            const uint32_t cnt = hl < 8 ? (uint32_t)__popcll(seg(mb) & rmask) : 0u;
             uint32_t cinc = cnt;
 #pragma unroll
             for (uint32_t d = 1; d < 8; d <<= 1)
