@@ -1399,9 +1399,8 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
         if (dest_first[d] > dest_first[d + 1]) return c->fail(AD_E_INVAL, "ad_parts_export: dest_first not ascending");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    const uint64_t items = 3 * n;
-    if (!ens<uint32_t>(c->x_sz, 4 * items) || !ens<uint64_t>(c->x_off, 4 * (items + 1)) ||
-        !ens<uint64_t>(c->x_bsum, 4 * ((items + 1023) / 1024) + 16) || !ens<uint64_t>(c->x_df, n_dest + 1) ||
+    if (!ens<uint32_t>(c->x_sz, std::max<uint64_t>(n, 1)) || !ens<uint64_t>(c->x_off, n + 1) ||
+        !ens<uint64_t>(c->x_bsum, (n + 1023) / 1024 + 16) || !ens<uint64_t>(c->x_df, n_dest + 1) ||
         !ens<uint64_t>(c->x_cnt, 4 * (n_dest + 1)))
         return c->fail(AD_E_NOMEM, "export buffers");
     ExportArgs a{};
@@ -1424,7 +1423,7 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     a.off = c->x_off.as<uint64_t>();
     HIPCHK(c, hipMemcpyAsync(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), hipMemcpyHostToDevice, st));
     HIPCHK(c, run_export_sizes(a, st));
-    HIPCHK(c, run_scan_arrays(a.sz, a.off, items, 4, c->x_bsum.as<uint64_t>(), st));
+    HIPCHK(c, run_scan_arrays(a.sz, a.off, n, 1, c->x_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_export_bounds(a, c->x_df.as<uint64_t>(), n_dest, c->x_cnt.as<uint64_t>(), st));
     std::vector<uint64_t> cnt(4 * (n_dest + 1));
     HIPCHK(c, hipMemcpyAsync(cnt.data(), c->x_cnt.p, sizeof(uint64_t) * cnt.size(), hipMemcpyDeviceToHost, st));

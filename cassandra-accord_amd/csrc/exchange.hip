@@ -58,41 +58,48 @@ __device__ __forceinline__ uint32_t lb_tid(const int64_t* ids, uint64_t base, ui
 // ---------------------------------------------------------------------------------------
 // export
 // ---------------------------------------------------------------------------------------
+// per request: number of non-empty maps (its parts); the part index is their exclusive scan
 __global__ void k_export_sizes(ExportArgs a)
 {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t items = 3 * a.n;
-    if (i >= items) return;
-    const uint64_t r = i / 3;
-    const int m = (int)(i % 3);
-    const uint64_t nk = a.keys_off[m][r + 1] - a.keys_off[m][r];
-    const uint64_t nt = a.txn_off[m][r + 1] - a.txn_off[m][r];
-    const uint64_t no = a.k2t_off[m][r + 1] - a.k2t_off[m][r];
-    const bool live = nk > 0;
-    a.sz[0 * items + i] = live ? 1u : 0u;
-    a.sz[1 * items + i] = live ? (uint32_t)(nk * (m == AD_MAP_RANGE ? 2 : 1)) : 0u;
-    a.sz[2 * items + i] = live ? (uint32_t)nt : 0u;
-    a.sz[3 * items + i] = live ? (uint32_t)no : 0u;
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.n) return;
+    uint32_t live = 0;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) live += a.keys_off[m][r + 1] > a.keys_off[m][r] ? 1u : 0u;
+    a.sz[r] = live;
+}
+
+// offsets of request r's first part in the four transport arrays: the part scan, and for key
+// words / ids / k2t the sums of the three maps' packed CSR offsets (maps are exported in order)
+struct PartBase { uint64_t P, KW, ID, KO; };
+
+__device__ __forceinline__ PartBase part_base(const ExportArgs& a, uint64_t r)
+{
+    PartBase b{a.off[r], 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+    {
+        b.KW += (m == AD_MAP_RANGE ? 2 : 1) * a.keys_off[m][r];
+        b.ID += a.txn_off[m][r];
+        b.KO += a.k2t_off[m][r];
+    }
+    return b;
 }
 
 // one 8-lane group per request, its three maps in turn
 __global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
 {
-    const uint64_t items = 3 * a.n;
     const uint32_t g8 = threadIdx.x & 7;
     const uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
     if (r >= a.n) return;
+    PartBase pb = part_base(a, r);
     for (int m = 0; m < 3; ++m)
     {
-        const uint64_t i = 3 * r + m;
         const uint64_t k0 = a.keys_off[m][r], nk = a.keys_off[m][r + 1] - k0;
         if (nk == 0) continue;
         const uint64_t t0 = a.txn_off[m][r], nt = a.txn_off[m][r + 1] - t0;
         const uint64_t o0 = a.k2t_off[m][r], no = a.k2t_off[m][r + 1] - o0;
-        const uint64_t P = a.off[0 * (items + 1) + i];
-        const uint64_t KW = a.off[1 * (items + 1) + i];
-        const uint64_t ID = a.off[2 * (items + 1) + i];
-        const uint64_t KO = a.off[3 * (items + 1) + i];
+        const uint64_t P = pb.P, KW = pb.KW, ID = pb.ID, KO = pb.KO;
         if (g8 == 0)
         {
             int64_t* h = a.hdr + 4 * P;
@@ -129,6 +136,10 @@ __global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
                 o[2] = (int64_t)a.dict_node[d];
             }
         for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = a.k2t[m][o0 + j];
+        pb.P += 1;
+        pb.KW += (m == AD_MAP_RANGE ? 2 : 1) * nk;
+        pb.ID += nt;
+        pb.KO += no;
     }
 }
 
@@ -136,9 +147,11 @@ __global__ void k_export_bounds(ExportArgs a, const uint64_t* dest_first, uint32
 {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d > n_dest) return;
-    const uint64_t items = 3 * a.n;
-    const uint64_t it = 3 * dest_first[d];
-    for (int k = 0; k < 4; ++k) counts[4 * d + k] = a.off[k * (items + 1) + it];
+    const PartBase b = part_base(a, dest_first[d]);
+    counts[4 * d + 0] = b.P;
+    counts[4 * d + 1] = b.KW;
+    counts[4 * d + 2] = b.ID;
+    counts[4 * d + 3] = b.KO;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -637,9 +650,8 @@ __global__ void k_merge_bases(MergeArgs a, uint64_t* out)
 
 hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st)
 {
-    const uint64_t items = 3 * a.n;
-    if (!items) return hipSuccess;
-    k_export_sizes<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(a);
+    if (!a.n) return hipSuccess;
+    k_export_sizes<<<(unsigned)((a.n + 255) / 256), 256, 0, st>>>(a);
     return hipGetLastError();
 }
 
