@@ -24,6 +24,7 @@ AD_MAP_KEY, AD_MAP_RANGE, AD_MAP_DIRECT_KEY = 0, 1, 2
 NMAPS = 3
 MAP_NAMES = ("keyDeps", "rangeDeps", "directKeyDeps")
 AD_SNAPSHOT, AD_SEQUENTIAL = 0, 1
+AD_PARTS_ONLY = 2        # ad_deps_batch_device: result only exported as parts (no packed arrays)
 
 # InternalStatus ordinals (CommandsForKey.java:493-501)
 ST_TRANSITIVELY_KNOWN = 0

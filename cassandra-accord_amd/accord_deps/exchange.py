@@ -111,8 +111,9 @@ class PartsBuffers:
 class GpuEngine:
     """Product engine: a DeviceCommandStore with its local batch resident in HBM."""
 
-    def __init__(self, store, qdev, txn_index, device, stream=None):
+    def __init__(self, store, qdev, txn_index, device, stream=None, parts_only=True):
         self.store = store
+        self.parts_only = parts_only      # the batch result is only exported (no packed arrays)
         self.qdev = qdev
         self.device = device
         self.txn_index = torch.from_numpy(np.ascontiguousarray(txn_index, np.int64)).to(device)
@@ -135,7 +136,7 @@ class GpuEngine:
         self.recv = PartsBuffers(self.device, rank_ids=True)
 
     def resolve(self):
-        self.res, self.last_stats = self.store.deps_batch_device(self.qdev, self.stream)
+        self.res, self.last_stats = self.store.deps_batch_device(self.qdev, self.stream, self.parts_only)
 
     def export(self, dest_first):
         """-> (dict of 1-D send tensors, counts[n_dest, 4] int64)."""

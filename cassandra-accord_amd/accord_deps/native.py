@@ -201,11 +201,13 @@ class DeviceCommandStore:
                 maps.append(DepsMap(ko, keys, None, to, txn, oo, k2t))
         return PartialDepsBatch(maps, stats=stats or {})
 
-    def deps_batch_device(self, qdev, stream=None):
+    def deps_batch_device(self, qdev, stream=None, parts_only=False):
         """Device-resident batch. `qdev` is an AdQuerySoa of device pointers. Returns
-        (AdDepsResult with device pointers owned by the store, stats dict)."""
+        (AdDepsResult with device pointers owned by the store, stats dict). `parts_only`: the result
+        is only exported as parts (AD_PARTS_ONLY: no packed arrays)."""
         out = A.AdDepsResult()
-        self._check(lib().ad_deps_batch_device(self.h, C.byref(qdev), A.AD_SNAPSHOT, stream, C.byref(out)))
+        flags = A.AD_SNAPSHOT | (A.AD_PARTS_ONLY if parts_only else 0)
+        self._check(lib().ad_deps_batch_device(self.h, C.byref(qdev), flags, stream, C.byref(out)))
         return out, stats_dict(out.stats)
 
     # ---- multi-GPU exchange (accord_deps.h "multi-GPU exchange"; DESIGN.md §6) ----------------

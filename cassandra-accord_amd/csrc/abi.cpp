@@ -207,6 +207,11 @@ struct ad_ctx {
     BatchCtl* h_ctl = nullptr;         // pinned mirror of the batch control block
     // multi-GPU export / merge buffers
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
+    // regions of the last device batch (ad_parts_export of an AD_PARTS_ONLY result)
+    const uint8_t* last_reg = nullptr;
+    const uint64_t* last_t_reg = nullptr;
+    uint64_t last_n = 0;
+    bool last_parts_only = false;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
     DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t, m_u, m_ppre;
     // global dictionary of the multi-store exchange (ad_set_global_dict)
@@ -862,7 +867,7 @@ static uint32_t lean_rpw1(uint64_t n, uint64_t np)
     return np <= 3 * n ? 4u : 2u;
 }
 
-static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out)
+static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false)
 {
     const uint64_t n = q->n_txns;
     uint64_t np = 0;
@@ -1029,18 +1034,24 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             if (h.overflow & 8u) c->reg_cap = std::max<uint64_t>(c->reg_cap * 2, h.reg_top + (h.reg_top >> 1));
             continue;
         }
-        for (int m = 0; m < 3; ++m)
-        {
-            if (!ens<int64_t>(c->o_keys[m], tot[3 * m + 0]) || !ens<uint32_t>(c->o_txns[m], tot[3 * m + 1]) ||
-                !ens<int32_t>(c->o_k2t[m], tot[3 * m + 2]))
-                return c->fail(AD_E_NOMEM, "outputs");
-            b.o_keys[m] = c->o_keys[m].as<int64_t>();
-            b.o_txns[m] = c->o_txns[m].as<uint32_t>();
-            b.o_k2t[m] = c->o_k2t[m].as<int32_t>();
-        }
+        if (!parts_only)
+            for (int m = 0; m < 3; ++m)
+            {
+                if (!ens<int64_t>(c->o_keys[m], tot[3 * m + 0]) || !ens<uint32_t>(c->o_txns[m], tot[3 * m + 1]) ||
+                    !ens<int32_t>(c->o_k2t[m], tot[3 * m + 2]))
+                    return c->fail(AD_E_NOMEM, "outputs");
+                b.o_keys[m] = c->o_keys[m].as<int64_t>();
+                b.o_txns[m] = c->o_txns[m].as<uint32_t>();
+                b.o_k2t[m] = c->o_k2t[m].as<int32_t>();
+            }
         HIPCHK(c, hipEventRecord(c->ev[4], st));
-        HIPCHK(c, run_pack(b, st));
+        if (!parts_only) HIPCHK(c, run_pack(b, st));
         HIPCHK(c, hipEventRecord(c->ev[5], st));
+        // the regions of this batch, for ad_parts_export of a parts-only result
+        c->last_reg = b.reg;
+        c->last_t_reg = b.t_reg;
+        c->last_n = n;
+        c->last_parts_only = parts_only;
         HIPCHK(c, hipStreamSynchronize(st));
 
         ad_stats& S = out->stats;
@@ -1094,9 +1105,9 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             out->keys_off[m] = b.off + (uint64_t)(3 * m + 0) * (n + 1);
             out->txn_off[m] = b.off + (uint64_t)(3 * m + 1) * (n + 1);
             out->k2t_off[m] = b.off + (uint64_t)(3 * m + 2) * (n + 1);
-            out->keys[m] = b.o_keys[m];
-            out->txns[m] = b.o_txns[m];
-            out->k2t[m] = b.o_k2t[m];
+            out->keys[m] = parts_only ? nullptr : b.o_keys[m];
+            out->txns[m] = parts_only ? nullptr : b.o_txns[m];
+            out->k2t[m] = parts_only ? nullptr : b.o_k2t[m];
         }
         return 0;
     }
@@ -1322,7 +1333,7 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
     int rc;
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    return run_pipeline(c, q, st, out);
+    return run_pipeline(c, q, st, out, (flags & AD_PARTS_ONLY) != 0);
 }
 
 void ad_result_free(ad_deps_result* r)
@@ -1412,6 +1423,14 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
         a.k2t_off[m] = res->k2t_off[m]; a.k2t[m] = res->k2t[m];
     }
     a.txn_index = txn_index;
+    if (!res->keys[0] || !res->txns[0] || !res->k2t[0])
+    {
+        // a parts-only result: read the batch's regions (still valid: no batch since)
+        if (!c->last_parts_only || c->last_n != n)
+            return c->fail(AD_E_INVAL, "ad_parts_export: result without packed arrays is not the ctx's last batch");
+        a.reg = c->last_reg;
+        a.t_reg = c->last_t_reg;
+    }
     a.dict_msb = c->d_dict_hi.as<uint64_t>();
     a.dict_lsb = c->d_dict_lsb_raw.as<uint64_t>();
     a.dict_node = c->d_dict_node.as<int32_t>();

@@ -100,6 +100,22 @@ __global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
         const uint64_t t0 = a.txn_off[m][r], nt = a.txn_off[m][r + 1] - t0;
         const uint64_t o0 = a.k2t_off[m][r], no = a.k2t_off[m][r + 1] - o0;
         const uint64_t P = pb.P, KW = pb.KW, ID = pb.ID, KO = pb.KO;
+        // the request's map: packed arrays, or its region (keys, txnIds, keysToTxnIds back to back)
+        const int64_t* ikeys;
+        const uint32_t* itx;
+        const int32_t* ik2t;
+        if (a.reg)
+        {
+            ikeys = reinterpret_cast<const int64_t*>(a.reg + a.t_reg[(uint64_t)m * a.n + r]);
+            itx = reinterpret_cast<const uint32_t*>(ikeys + nk);
+            ik2t = reinterpret_cast<const int32_t*>(itx + nt);
+        }
+        else
+        {
+            ikeys = a.keys[m] + k0;
+            itx = a.txns[m] + t0;
+            ik2t = a.k2t[m] + o0;
+        }
         if (g8 == 0)
         {
             int64_t* h = a.hdr + 4 * P;
@@ -112,30 +128,30 @@ __global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
         {
             for (uint64_t j = g8; j < nk; j += 8)
             {
-                const int64_t rid = a.keys[m][k0 + j];
+                const int64_t rid = ikeys[j];
                 a.okeys[KW + 2 * j] = a.rt_start[rid];
                 a.okeys[KW + 2 * j + 1] = a.rt_end[rid];
             }
         }
         else
         {
-            for (uint64_t j = g8; j < nk; j += 8) a.okeys[KW + j] = a.keys[m][k0 + j];
+            for (uint64_t j = g8; j < nk; j += 8) a.okeys[KW + j] = ikeys[j];
         }
         if (a.gmap)
         {
             uint32_t* o = reinterpret_cast<uint32_t*>(a.oids) + ID;
-            for (uint64_t j = g8; j < nt; j += 8) o[j] = a.gmap[a.txns[m][t0 + j]];
+            for (uint64_t j = g8; j < nt; j += 8) o[j] = a.gmap[itx[j]];
         }
         else
             for (uint64_t j = g8; j < nt; j += 8)
             {
-                const uint32_t d = a.txns[m][t0 + j];
+                const uint32_t d = itx[j];
                 int64_t* o = a.oids + 3 * (ID + j);
                 o[0] = (int64_t)a.dict_msb[d];
                 o[1] = (int64_t)a.dict_lsb[d];
                 o[2] = (int64_t)a.dict_node[d];
             }
-        for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = a.k2t[m][o0 + j];
+        for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = ik2t[j];
         pb.P += 1;
         pb.KW += (m == AD_MAP_RANGE ? 2 : 1) * nk;
         pb.ID += nt;

@@ -18,6 +18,7 @@ struct ExportArgs {
     const uint64_t* dict_msb; const uint64_t* dict_lsb; const int32_t* dict_node;   // raw ids
     const int64_t* rt_start; const int64_t* rt_end;                                // range table
     const uint32_t* gmap;                         // [n_dict] global rank of each dictionary id (null: triplets)
+    const uint8_t* reg; const uint64_t* t_reg;    // parts-only batch: per-request regions (null: packed arrays)
     uint32_t* sz;                                 // [n] parts (non-empty maps) per request
     uint64_t* off;                                // [n+1] their exclusive scan
     int64_t* hdr; int64_t* okeys; int64_t* oids; int32_t* ok2t;

@@ -98,6 +98,10 @@ extern "C" {
  *           The inserted entries stay in the ctx snapshot afterwards, as they do in the CFK. */
 #define AD_SNAPSHOT   0u
 #define AD_SEQUENTIAL 1u
+/* ad_deps_batch_device only: the caller exports the result as parts (ad_parts_export) and does
+ * not read the packed arrays; they are not produced (keys/txns/k2t NULL, offsets valid) and the
+ * export reads the per-request regions of the batch directly. */
+#define AD_PARTS_ONLY 2u
 
 typedef struct ad_config {
     int32_t device;                 /* HIP device ordinal                                   */

@@ -25,7 +25,7 @@ def _parts(tensors, totals, rank_ids=False):
     return p
 
 
-def _run_sharded(w, bounds, n_owners, rank_ids=False):
+def _run_sharded(w, bounds, n_owners, rank_ids=False, parts_only=True):
     dev = torch.device("cuda", 0)
     lo, hi = bounds
     n_total = len(w.queries)
@@ -37,7 +37,7 @@ def _run_sharded(w, bounds, n_owners, rank_ids=False):
         st.load(local)
         qdev, k = native.device_queries(local.queries, dev)
         keep.append(k)
-        e = exchange.GpuEngine(st, qdev, idx, dev)
+        e = exchange.GpuEngine(st, qdev, idx, dev, parts_only=parts_only)
         engines.append((e, idx))
     if rank_ids:
         # the ingest-time global dictionary (what ShardExchange.install_global_dict gathers)
@@ -74,9 +74,9 @@ def _run_sharded(w, bounds, n_owners, rank_ids=False):
     return out
 
 
-def _check(w, bounds, n_owners, rank_ids=False):
+def _check(w, bounds, n_owners, rank_ids=False, parts_only=True):
     expect = pyoracle.resolve_sharded(w, len(bounds[0]), bounds=bounds)
-    for base, n, got, _ in _run_sharded(w, bounds, n_owners, rank_ids):
+    for base, n, got, _ in _run_sharded(w, bounds, n_owners, rank_ids, parts_only):
         ok, why = got.equals(expect.window(base, n), detail=True)
         if not ok:
             bad = got.first_mismatch(expect.window(base, n))
@@ -96,6 +96,13 @@ def test_random_small_three_stores(seed, rank_ids):
 def test_config3_scaled(n_stores, n_owners, rank_ids):
     w = synth.config3(n_txns=40000, n_keys=6000, seed=11 + n_stores)
     _check(w, synth.shard_bounds(n_stores), n_owners, rank_ids)
+
+
+@pytest.mark.parametrize("rank_ids", [False, True])
+def test_export_from_packed_arrays(rank_ids):
+    # export of a full result (packed arrays) instead of the parts-only batch's regions
+    w = synth.config3(n_txns=20000, n_keys=3000, seed=41)
+    _check(w, synth.shard_bounds(4), 4, rank_ids, parts_only=False)
 
 
 @pytest.mark.parametrize("rank_ids", [False, True])
@@ -124,7 +131,7 @@ def test_merge_rejects_overlapping_sources():
     st = native.DeviceCommandStore(0)
     st.load(w)
     qdev, keep = native.device_queries(w.queries, dev)
-    e = exchange.GpuEngine(st, qdev, np.arange(len(w.queries)), dev)
+    e = exchange.GpuEngine(st, qdev, np.arange(len(w.queries)), dev, parts_only=False)
     e.resolve()
     send, counts = e.export(np.array([0, len(w.queries)], np.uint64))
     recv = {k: torch.cat([send[k][:int(counts[0, a]) * m]] * 2) for a, (k, m) in enumerate(UNITS)}
