@@ -217,27 +217,28 @@ struct PartInfo {
     uint32_t p;                       // part index
 };
 
+__device__ __forceinline__ PartInfo load_part_info(const MergeArgs& a, uint64_t p)
+{
+    const uint64_t P1 = a.n_parts + 1;
+    PartInfo pi;
+    pi.kbase = a.poff[0 * P1 + p];
+    pi.kw = (uint32_t)(a.poff[0 * P1 + p + 1] - pi.kbase);
+    pi.ibase = a.poff[1 * P1 + p];
+    pi.ni = (uint32_t)(a.poff[1 * P1 + p + 1] - pi.ibase);
+    pi.obase = a.poff[2 * P1 + p];
+    pi.no = (uint32_t)(a.poff[2 * P1 + p + 1] - pi.obase);
+    pi.nk = (uint32_t)a.hdr[4 * p + 1];
+    pi.p = (uint32_t)p;
+    return pi;
+}
+
 __device__ __forceinline__ uint32_t stage_parts(const MergeArgs& a, uint64_t g, PartInfo* info)
 {
     const uint32_t l = lane_id();
     const int32_t v = l < a.n_src ? a.slot[g * a.n_src + l] : -1;
     const uint64_t live = ballot(v >= 0);
     const uint32_t np = __popcll(live);
-    if (v >= 0)
-    {
-        const uint64_t p = (uint64_t)v;
-        const uint64_t P1 = a.n_parts + 1;
-        PartInfo pi;
-        pi.kbase = a.poff[0 * P1 + p];
-        pi.kw = (uint32_t)(a.poff[0 * P1 + p + 1] - pi.kbase);
-        pi.ibase = a.poff[1 * P1 + p];
-        pi.ni = (uint32_t)(a.poff[1 * P1 + p + 1] - pi.ibase);
-        pi.obase = a.poff[2 * P1 + p];
-        pi.no = (uint32_t)(a.poff[2 * P1 + p + 1] - pi.obase);
-        pi.nk = (uint32_t)a.hdr[4 * p + 1];
-        pi.p = (uint32_t)p;
-        info[mbcnt(live)] = pi;
-    }
+    if (v >= 0) info[mbcnt(live)] = load_part_info(a, (uint64_t)v);
     wave_lds_sync();
     return np;
 }
@@ -462,12 +463,34 @@ __global__ void __launch_bounds__(64 * XWAVES) k_merge_rank(MergeArgs a)
     const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint32_t l = lane_id();
     const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
-    for (uint64_t g = wave; g < n_groups; g += n_waves)
+    // one owned request per iteration: the slots of its three maps in one load (3 * n_src <= 64),
+    // so maps without parts cost nothing more
+    const bool combined = 3 * a.n_src <= 64;
+    for (uint64_t r = wave; r < a.n_owned; r += n_waves)
     {
-        const int m = (int)(g / a.n_owned);
+      int32_t v = -1;
+      if (combined && l < 3 * a.n_src)
+      {
+          const uint32_t ml = l / a.n_src, sl = l - ml * a.n_src;
+          v = a.slot[((uint64_t)ml * a.n_owned + r) * a.n_src + sl];
+      }
+      const uint64_t live_all = ballot(v >= 0);
+      for (int m = 0; m < 3; ++m)
+      {
+        const uint64_t g = (uint64_t)m * a.n_owned + r;
         const int w = m == AD_MAP_RANGE ? 2 : 1;
         wave_lds_sync();
-        const uint32_t np = stage_parts(a, g, info);
+        uint32_t np;
+        if (combined)
+        {
+            const uint64_t mmask = ((1ull << a.n_src) - 1) << (m * a.n_src);
+            const uint64_t live = live_all & mmask;
+            np = __popcll(live);
+            if (v >= 0 && ((mmask >> l) & 1)) info[__popcll(live & ((1ull << l) - 1))] = load_part_info(a, (uint64_t)v);
+            wave_lds_sync();
+        }
+        else
+            np = stage_parts(a, g, info);
         if (np == 0)
         {
             if (l == 0)
@@ -594,6 +617,7 @@ __global__ void __launch_bounds__(64 * XWAVES) k_merge_rank(MergeArgs a)
             a.gsz[1 * n_groups + g] = T - n_dup;
             a.gsz[2 * n_groups + g] = NOt;
         }
+      }
     }
 }
 
@@ -735,7 +759,7 @@ hipError_t run_global_map(const uint64_t* l_msb, const uint64_t* l_lo_norm, cons
 hipError_t run_merge_rank(const MergeArgs& a, hipStream_t st)
 {
     if (!a.n_owned) return hipSuccess;
-    k_merge_rank<<<merge_blocks(3 * a.n_owned), 64 * XWAVES, 0, st>>>(a);
+    k_merge_rank<<<merge_blocks(a.n_owned), 64 * XWAVES, 0, st>>>(a);
     return hipGetLastError();
 }
 
