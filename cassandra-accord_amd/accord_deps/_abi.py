@@ -25,6 +25,7 @@ NMAPS = 3
 MAP_NAMES = ("keyDeps", "rangeDeps", "directKeyDeps")
 AD_SNAPSHOT, AD_SEQUENTIAL = 0, 1
 AD_PARTS_ONLY = 2        # ad_deps_batch_device: result only exported as parts (no packed arrays)
+AD_N_KEYS = 4            # ad_deps_batch_device: AdQuerySoa.n_keys = key_off[n_txns]
 
 # InternalStatus ordinals (CommandsForKey.java:493-501)
 ST_TRANSITIVELY_KNOWN = 0
@@ -67,7 +68,7 @@ class AdRedundantSoa(C.Structure):
 class AdQuerySoa(C.Structure):
     _fields_ = [("n_txns", C.c_uint64), ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
                 ("exec_msb", P), ("exec_lsb", P), ("exec_node", P), ("min_epoch", P),
-                ("key_off", P), ("keys", P)]
+                ("key_off", P), ("keys", P), ("n_keys", C.c_uint64)]
 
 
 class AdStats(C.Structure):

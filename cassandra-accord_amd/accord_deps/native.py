@@ -206,7 +206,7 @@ class DeviceCommandStore:
         (AdDepsResult with device pointers owned by the store, stats dict). `parts_only`: the result
         is only exported as parts (AD_PARTS_ONLY: no packed arrays)."""
         out = A.AdDepsResult()
-        flags = A.AD_SNAPSHOT | (A.AD_PARTS_ONLY if parts_only else 0)
+        flags = A.AD_SNAPSHOT | A.AD_N_KEYS | (A.AD_PARTS_ONLY if parts_only else 0)
         self._check(lib().ad_deps_batch_device(self.h, C.byref(qdev), flags, stream, C.byref(out)))
         return out, stats_dict(out.stats)
 
@@ -293,6 +293,7 @@ def device_queries(q, dev):
     s.exec_msb, s.exec_lsb, s.exec_node = keep["em"].data_ptr(), keep["el"].data_ptr(), keep["en"].data_ptr()
     s.min_epoch = keep["me"].data_ptr() if "me" in keep else None
     s.key_off, s.keys = keep["ko"].data_ptr(), keep["k"].data_ptr()
+    s.n_keys = int(q.key_off[-1]) if len(q.key_off) else 0
     return s, keep
 
 

@@ -867,11 +867,14 @@ static uint32_t lean_rpw1(uint64_t n, uint64_t np)
     return np <= 3 * n ? 4u : 2u;
 }
 
-static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false)
+static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false,
+                        bool n_keys_given = false)
 {
     const uint64_t n = q->n_txns;
     uint64_t np = 0;
-    if (n)
+    if (n && n_keys_given)
+        np = q->n_keys;
+    else if (n)
     {
         HIPCHK(c, hipMemcpyAsync(&np, q->key_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
@@ -1333,7 +1336,7 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
     int rc;
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    return run_pipeline(c, q, st, out, (flags & AD_PARTS_ONLY) != 0);
+    return run_pipeline(c, q, st, out, (flags & AD_PARTS_ONLY) != 0, (flags & AD_N_KEYS) != 0);
 }
 
 void ad_result_free(ad_deps_result* r)

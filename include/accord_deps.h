@@ -102,6 +102,8 @@ extern "C" {
  * not read the packed arrays; they are not produced (keys/txns/k2t NULL, offsets valid) and the
  * export reads the per-request regions of the batch directly. */
 #define AD_PARTS_ONLY 2u
+/* ad_deps_batch_device only: ad_query_soa.n_keys holds key_off[n_txns] */
+#define AD_N_KEYS     4u
 
 typedef struct ad_config {
     int32_t device;                 /* HIP device ordinal                                   */
@@ -175,6 +177,8 @@ typedef struct ad_query_soa {
     const int64_t*  min_epoch;       /* minUnsyncedEpoch (RedundantBefore bounds); NULL = 0  */
     const uint64_t* key_off;         /* [n_txns+1] */
     const int64_t*  keys;
+    uint64_t        n_keys;          /* key_off[n_txns], read only under AD_N_KEYS (a device batch
+                                      * then needs no device-to-host read before its first kernel) */
 } ad_query_soa;
 
 typedef struct ad_stats {
