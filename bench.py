@@ -299,6 +299,57 @@ def bench_ranges(args, rank, world, local, dev):
         dist.destroy_process_group()
 
 
+def bench_preaccept(args, rank, world, local, dev):
+    """SURVEY §8 f3 on config 2's batch: the PreAccept timestamp proposal (CommandStore.preaccept
+    minus the clock) of 1M requests x 8 keys against the maxConflicts of the 16M-entry history
+    (one point interval per key). With N GPUs, N independent replicas."""
+    s = args.scale
+    w = synth.config2(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_hist_entries=int(16_000_000 * s),
+                      seed=0xACC0D002 + rank)
+    mc = synth.max_conflicts_from_cfk(w.cfk)
+    st = native.DeviceCommandStore(device=local)
+    st.load_preaccept_maps(mc, None)
+    qdev, keep = native.device_queries(w.queries, dev)
+    n = len(w.queries)
+    out = dict(msb=torch.zeros(n, dtype=torch.int64, device=dev), lsb=torch.zeros(n, dtype=torch.int64, device=dev),
+               node=torch.zeros(n, dtype=torch.int32, device=dev), flags=torch.zeros(n, dtype=torch.uint8, device=dev))
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    elapsed, all_stats = _timed_steps(args, world, dev, lambda: st.preaccept_device(qdev, out, 1, 0, sp))
+    pairs = _sum_over_ranks(world, dev, w.queries.n_probes)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    kernel_ms = float(np.mean([x["ms_device"] for x in all_stats]))
+    # algorithmic bytes: request inputs (txnId 20 B + key_off 8 B + 8 B per key), the map once
+    # (8 B start + 20 B value + 1 B present per interval), outputs 21 B per request
+    alg = 28 * n + 8 * w.queries.n_probes + 29 * len(mc) + 21 * n
+    achieved = alg / (kernel_ms / 1000.0) / 1e9 if kernel_ms > 0 else 0.0
+    res = {
+        "metric": "PreAccept witnessedAt proposals: txn-key pairs/sec", "value": pairs / (ms_per_step / 1000.0),
+        "unit": "txn-key pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": "config2 batch (%d txns x 8 keys) vs maxConflicts of %d intervals (SURVEY 8 f3)"
+                               % (n, len(mc)), "txn_key_pairs_per_step": pairs, "parallelism": "replicas x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_preaccept", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": alg,
+                     "launch_ms": kernel_ms},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        m = min(n, 200_000)
+        qs = w.queries.window(0, m)
+        t0 = time.perf_counter()
+        pyoracle.preaccept(mc, None, qs, 1, 0)
+        t = time.perf_counter() - t0
+        res["cpu_baseline"] = dict(value=qs.n_probes / t, unit="txn-key pairs/s", cores=1, kind="port",
+                                   sample="first %d requests (%.2f s), rc_preaccept, 1 thread" % (m, t))
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    st.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def bench_sequential(args, rank, world, local, dev):
     """Config 1: 10k txns x 4 keys over 1k keys, one CommandStore, SEQUENTIAL PreAccept (each txn
     inserted as PREACCEPTED before its deps). SEQUENTIAL runs through the host API: a step is one
@@ -356,6 +407,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=(1, 2, 4, 5),
                     help="2: BASELINE config 2 (the headline line, default); 1: SEQUENTIAL PreAccept batch "
                          "(host API); 4: range transactions; 5: execution levels (K5)")
+    ap.add_argument("--preaccept", action="store_true",
+                    help="with config 2: the PreAccept timestamp proposal (SURVEY 8 f3) instead of deps")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank: the measured configuration); gloo: rehearsal of the "
                          "N>1 path on fewer GPUs (ranks share GPUs, the exchange is staged through host memory)")
@@ -384,6 +437,8 @@ def main():
         return bench_ranges(args, rank, world, local, dev)
     if args.config == 1:
         return bench_sequential(args, rank, world, local, dev)
+    if args.preaccept:
+        return bench_preaccept(args, rank, world, local, dev)
 
     s = args.scale
     t0 = time.time()

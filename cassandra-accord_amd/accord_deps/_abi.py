@@ -93,6 +93,14 @@ class AdGraphSoa(C.Structure):
                 ("key_off", P), ("keys", P), ("dep_off", P), ("deps", P)]
 
 
+class AdRangeMapSoa(C.Structure):
+    _fields_ = [("n_values", C.c_uint64), ("starts", P), ("msb", P), ("lsb", P), ("node", P), ("present", P),
+                ("inclusive_ends", C.c_uint32)]
+
+
+AD_PA_FAST, AD_PA_REJECTED, AD_PA_ESP = 1, 2, 4
+
+
 class AdParts(C.Structure):
     _fields_ = [("n_parts", C.c_uint64), ("n_key_words", C.c_uint64), ("n_ids", C.c_uint64), ("n_k2t", C.c_uint64),
                 ("hdr", P), ("keys", P), ("ids", P), ("k2t", P),

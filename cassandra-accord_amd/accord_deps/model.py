@@ -250,6 +250,35 @@ class Graph:
 
 
 @dataclass
+class RangeMap:
+    """A ReducingRangeMap<Timestamp> (ReducingIntervalMap.java: starts one longer than values):
+    value i on [starts[i], starts[i+1]) or, with inclusive_ends, (starts[i], starts[i+1]]; a
+    value absent where present[i] == 0 (null). MaxConflicts / rejectBefore of a CommandStore."""
+    starts: np.ndarray          # i64 [n + 1] ascending, distinct
+    values: Tids                # [n]
+    present: np.ndarray = None  # u8 [n] (None = all present)
+    inclusive_ends: int = 0
+
+    @staticmethod
+    def empty(inclusive_ends=0):
+        z = np.zeros(0, np.uint64)
+        return RangeMap(np.zeros(0, np.int64), Tids(z, z, np.zeros(0, np.int32)), None, inclusive_ends)
+
+    def __len__(self):
+        return len(self.values.msb)
+
+    def soa(self):
+        s = A.AdRangeMapSoa()
+        s.n_values = len(self)
+        if len(self):
+            s.starts = A.ptr(self.starts)
+            s.msb, s.lsb, s.node = A.ptr(self.values.msb), A.ptr(self.values.lsb), A.ptr(self.values.node)
+            s.present = A.ptr(self.present) if self.present is not None else None
+        s.inclusive_ends = self.inclusive_ends
+        return s
+
+
+@dataclass
 class DepsMap:
     """One RelationMultiMap per request, packed: keys / txnIds / keysToTxnIds per request."""
     keys_off: np.ndarray

@@ -21,7 +21,8 @@ LIB_PATH = os.environ.get("ACCORD_DEPS_LIB") or os.path.join(os.path.dirname(os.
 EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error", "ad_cfk_load",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
-           "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict")
+           "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict", "ad_preaccept_maps_load",
+           "ad_preaccept_device")
 
 
 class AccordDepsError(RuntimeError):
@@ -68,6 +69,9 @@ def lib():
                                      C.c_void_p, C.POINTER(A.AdMerged)]
         L.ad_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
         L.ad_set_global_dict.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.ad_preaccept_maps_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdRangeMapSoa)]
+        L.ad_preaccept_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_uint64, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(A.AdStats)]
         L.ad_levels.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.POINTER(A.AdStats)]
         L.ad_levels_device.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.c_void_p,
                                        C.POINTER(A.AdStats)]
@@ -111,6 +115,7 @@ class DeviceCommandStore:
         if rc:
             raise AccordDepsError(rc, L.ad_last_error(None).decode())
         self.h = h
+        self.device = device
 
     def close(self):
         if getattr(self, "h", None):
@@ -148,6 +153,36 @@ class DeviceCommandStore:
         nd = np.ascontiguousarray(g.node, np.int32)
         self._check(lib().ad_set_global_dict(self.h, len(m), A.ptr(m), A.ptr(ls), A.ptr(nd)))
         self.global_dict = Tids(m, ls, nd)
+
+    def load_preaccept_maps(self, max_conflicts=None, reject_before=None):
+        """Install the store's maxConflicts / rejectBefore (model.RangeMap, None = empty)."""
+        mc = max_conflicts.soa() if max_conflicts is not None else None
+        rb = reject_before.soa() if reject_before is not None else None
+        self._check(lib().ad_preaccept_maps_load(self.h, C.byref(mc) if mc else None, C.byref(rb) if rb else None))
+
+    def preaccept_device(self, qdev, out, permit_fast_path=1, node_epoch=0, stream=None):
+        """ad_preaccept_device: `qdev` device queries, `out` dict of device tensors msb/lsb/node/flags.
+        Returns the stats dict."""
+        s = A.AdStats()
+        self._check(lib().ad_preaccept_device(self.h, C.byref(qdev), permit_fast_path, node_epoch, stream,
+                                              out["msb"].data_ptr(), out["lsb"].data_ptr(), out["node"].data_ptr(),
+                                              out["flags"].data_ptr(), C.byref(s)))
+        return stats_dict(s)
+
+    def preaccept(self, queries, permit_fast_path=1, node_epoch=0):
+        """Host convenience: (minNonConflicting Tids, AD_PA_* flags) per request."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        qdev, keep = device_queries(queries, dev)
+        n = len(queries)
+        out = dict(msb=torch.zeros(max(n, 1), dtype=torch.int64, device=dev),
+                   lsb=torch.zeros(max(n, 1), dtype=torch.int64, device=dev),
+                   node=torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
+                   flags=torch.zeros(max(n, 1), dtype=torch.uint8, device=dev))
+        torch.cuda.synchronize(dev)
+        st = self.preaccept_device(qdev, out, permit_fast_path, node_epoch)
+        o = {k: v.cpu().numpy()[:n] for k, v in out.items()}
+        return Tids(o["msb"].view(np.uint64), o["lsb"].view(np.uint64), o["node"]), o["flags"], st
 
     def range_table(self):
         n = C.c_uint64()

@@ -557,3 +557,85 @@ def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_rang
         slices = np.array([[-400, -100], [0, 300]], np.int64)
     return Workload("random_small", cfk, cmds, red, q, params=dict(seed=seed), range_start_inclusive=int(start_inclusive),
                     slices=slices)
+
+
+def range_map(rng, n_values, key_lo, key_hi, hlc_lo, hlc_hi, null_frac=0.1, inclusive_ends=0, epochs=(1, 2),
+              node_max=16, flag_noise=True):
+    """A random ReducingRangeMap<Timestamp> over key ordinals [key_lo, key_hi): distinct ascending
+    starts, Timestamps with random epoch / hlc / node (and, with flag_noise, non-identity lsb
+    flag bits such as REJECTED 0x8000 so ties between equal Timestamps are observable), some null."""
+    from .model import RangeMap
+    n_values = int(n_values)
+    if n_values == 0:
+        return RangeMap.empty(inclusive_ends)
+    starts = np.sort(rng.choice(np.arange(key_lo, key_hi, dtype=np.int64), n_values + 1, replace=False))
+    ep = rng.choice(np.asarray(epochs, np.uint64), n_values)
+    hlc = rng.integers(hlc_lo, hlc_hi, n_values).astype(np.uint64)
+    flags = (rng.integers(0, 5, n_values).astype(np.uint64) << np.uint64(1))
+    if flag_noise:
+        flags |= np.where(rng.random(n_values) < 0.3, np.uint64(0x8000), np.uint64(0))
+    v = make_timestamps(ep, hlc, flags, rng.integers(1, node_max + 1, n_values).astype(np.int32))
+    present = (rng.random(n_values) >= null_frac).astype(np.uint8)
+    return RangeMap(starts.astype(np.int64), v, present, int(inclusive_ends))
+
+
+def preaccept_workload(seed, n_txns=300, n_values=40, key_space=600, max_keys=6, inclusive_ends=0, with_reject=True,
+                       esp_frac=0.1):
+    """Requests (ascending keys) plus maxConflicts / rejectBefore maps with overlapping ranges of
+    keys and Timestamps around the requests' txnIds, so every branch of preaccept is taken."""
+    from .model import Queries
+    rng = np.random.default_rng(seed)
+    mc = range_map(rng, n_values, -key_space // 2, key_space // 2, 50, 150, inclusive_ends=inclusive_ends)
+    rb = range_map(rng, max(1, n_values // 4), -key_space // 2, key_space // 2, 20, 120,
+                   inclusive_ends=inclusive_ends) if with_reject else None
+    nk = rng.integers(0, max_keys + 1, n_txns)
+    key_off = np.zeros(n_txns + 1, np.uint64)
+    key_off[1:] = np.cumsum(nk)
+    keys = np.concatenate([np.sort(rng.choice(np.arange(-key_space // 2 - 20, key_space // 2 + 20), k,
+                                              replace=False)) for k in nk] + [np.zeros(0, np.int64)]).astype(np.int64)
+    # keys exactly on interval starts exercise both end conventions
+    on_start = rng.random(len(keys)) < 0.15
+    if len(mc) and on_start.any():
+        keys[on_start] = rng.choice(mc.starts, int(on_start.sum()))
+        for t in range(n_txns):
+            seg = keys[int(key_off[t]):int(key_off[t + 1])]
+            u = np.unique(seg)
+            keys[int(key_off[t]):int(key_off[t]) + len(u)] = u
+            nk[t] = len(u)
+        # re-pack after de-duplication
+        keys = np.concatenate([keys[int(key_off[t]):int(key_off[t]) + int(nk[t])] for t in range(n_txns)]
+                              + [np.zeros(0, np.int64)]).astype(np.int64)
+        key_off[1:] = np.cumsum(nk)
+    kinds = np.where(rng.random(n_txns) < esp_frac, A.KIND_EXCLUSIVE_SYNC_POINT,
+                     rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_SYNC_POINT], n_txns)).astype(np.uint8)
+    txn = make_txn_ids(rng.choice(np.asarray([1, 2], np.uint64), n_txns), rng.integers(40, 160, n_txns).astype(np.uint64),
+                       kinds, rng.integers(1, 17, n_txns).astype(np.int32))
+    return Queries(txn, txn, key_off, keys, None), mc, rb
+
+
+def max_conflicts_from_cfk(cfk):
+    """The maxConflicts a store holds after every CommandsForKey entry updated it with its executeAt
+    (CommandStore.updateMaxConflicts, CommandStore.java:282-291): per key, the max executeAt of its
+    entries on the point interval (key - 1, key] (EndInclusive), null between keys."""
+    from .model import RangeMap, Tids
+    keys = np.asarray(cfk.keys, np.int64)
+    if len(keys) == 0:
+        return RangeMap.empty(1)
+    seg = cfk.seg.astype(np.int64)
+    order = np.lexsort(cfk.exec.order_key())            # ascending Timestamp order
+    rank = np.empty(len(order), np.int64)
+    rank[order] = np.arange(len(order))
+    key_of = np.repeat(np.arange(len(keys)), np.diff(seg))
+    best = np.full(len(keys), -1, np.int64)
+    np.maximum.at(best, key_of, rank)
+    best_e = order[best]
+    starts = np.unique(np.concatenate([keys - 1, keys]))
+    n = len(starts) - 1
+    hit = np.isin(starts[1:], keys) & (starts[:-1] == starts[1:] - 1)
+    kidx = np.searchsorted(keys, starts[1:])
+    kidx = np.minimum(kidx, len(keys) - 1)
+    e = best_e[kidx]
+    z = np.zeros(n, np.uint64)
+    v = Tids(np.where(hit, cfk.exec.msb[e], z), np.where(hit, cfk.exec.lsb[e], z),
+             np.where(hit, cfk.exec.node[e], 0).astype(np.int32))
+    return RangeMap(starts, v, hit.astype(np.uint8), 1)

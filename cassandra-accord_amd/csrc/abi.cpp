@@ -214,6 +214,13 @@ struct ad_ctx {
     bool last_parts_only = false;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
     DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t, m_u, m_ppre;
+    // maxConflicts / rejectBefore of the PreAccept timestamp proposal (ad_preaccept_maps_load)
+    struct RangeMapBufs {
+        DevBuf starts, msb, lsb, node, present;
+        uint64_t n = 0;
+        uint32_t inclusive_ends = 0;
+        bool has_present = false;
+    } pa_mc, pa_rb;
     // global dictionary of the multi-store exchange (ad_set_global_dict)
     DevBuf g_msb, g_lsb, g_node, g_map, g_err;
     uint64_t n_global = 0;
@@ -1365,6 +1372,87 @@ int ad_range_table(const ad_ctx* c, uint64_t* n, const int64_t** start, const in
     *n = c->rt_start.size();
     if (start) *start = c->rt_start.data();
     if (end) *end = c->rt_end.data();
+    return AD_OK;
+}
+
+static int load_range_map(ad_ctx* c, const ad_range_map_soa* m, ad_ctx::RangeMapBufs& B, const char* what)
+{
+    B.n = 0;
+    B.has_present = false;
+    if (!m || m->n_values == 0) return AD_OK;
+    const uint64_t n = m->n_values;
+    if (!m->starts || !m->msb || !m->lsb || !m->node) return c->fail(AD_E_INVAL, "%s: NULL array", what);
+    for (uint64_t i = 0; i < n; ++i)
+        if (m->starts[i] >= m->starts[i + 1]) return c->fail(AD_E_INVAL, "%s: starts not strictly ascending at %llu", what, (unsigned long long)i);
+    if (!B.starts.ensure(8 * (n + 1)) || !B.msb.ensure(8 * n) || !B.lsb.ensure(8 * n) || !B.node.ensure(4 * n) ||
+        (m->present && !B.present.ensure(n)))
+        return c->fail(AD_E_NOMEM, "%s", what);
+    HIPCHK(c, hipMemcpy(B.starts.p, m->starts, 8 * (n + 1), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(B.msb.p, m->msb, 8 * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(B.lsb.p, m->lsb, 8 * n, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(B.node.p, m->node, 4 * n, hipMemcpyHostToDevice));
+    if (m->present) HIPCHK(c, hipMemcpy(B.present.p, m->present, n, hipMemcpyHostToDevice));
+    B.n = n;
+    B.inclusive_ends = m->inclusive_ends ? 1u : 0u;
+    B.has_present = m->present != nullptr;
+    return AD_OK;
+}
+
+static DevRangeMap dev_range_map(ad_ctx::RangeMapBufs& B)
+{
+    DevRangeMap d{};
+    d.n = B.n;
+    if (B.n)
+    {
+        d.starts = B.starts.as<int64_t>();
+        d.msb = B.msb.as<uint64_t>();
+        d.lsb = B.lsb.as<uint64_t>();
+        d.node = B.node.as<int32_t>();
+        d.present = B.has_present ? B.present.as<uint8_t>() : nullptr;
+    }
+    d.inclusive_ends = B.inclusive_ends;
+    return d;
+}
+
+int ad_preaccept_maps_load(ad_ctx* c, const ad_range_map_soa* max_conflicts, const ad_range_map_soa* reject_before)
+{
+    if (!c) return AD_E_INVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    int rc = load_range_map(c, max_conflicts, c->pa_mc, "ad_preaccept_maps_load: maxConflicts");
+    return rc ? rc : load_range_map(c, reject_before, c->pa_rb, "ad_preaccept_maps_load: rejectBefore");
+}
+
+int ad_preaccept_device(ad_ctx* c, const ad_query_soa* q, uint32_t permit_fast_path, uint64_t node_epoch, void* stream,
+                        uint64_t* out_msb, uint64_t* out_lsb, int32_t* out_node, uint8_t* out_flags, ad_stats* stats)
+{
+    if (!c || !q) return AD_E_INVAL;
+    if (q->n_txns && (!q->txn_msb || !q->txn_lsb || !q->txn_node || !q->key_off || !out_msb || !out_lsb || !out_node ||
+                      !out_flags))
+        return c->fail(AD_E_INVAL, "ad_preaccept_device: NULL array");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    PreacceptArgs a{};
+    a.n = q->n_txns;
+    a.txn_msb = q->txn_msb; a.txn_lsb = q->txn_lsb; a.txn_node = q->txn_node;
+    a.key_off = q->key_off; a.keys = q->keys;
+    a.mc = dev_range_map(c->pa_mc);
+    a.rb = dev_range_map(c->pa_rb);
+    a.permit_fast_path = permit_fast_path ? 1u : 0u;
+    a.node_epoch = node_epoch;
+    a.out_msb = out_msb; a.out_lsb = out_lsb; a.out_node = out_node; a.out_flags = out_flags;
+    HIPCHK(c, hipEventRecord(c->ev[6], st));
+    HIPCHK(c, run_preaccept(a, st));
+    HIPCHK(c, hipEventRecord(c->ev[7], st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (stats)
+    {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
+        memset(stats, 0, sizeof(*stats));
+        stats->n_txns = q->n_txns;
+        stats->ms_device = ms;
+        stats->ms_stage[0] = ms;
+    }
     return AD_OK;
 }
 

@@ -81,6 +81,27 @@ constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave 
 constexpr uint32_t REC_FAST = 1u << 24;          // q_rec: newest fast path applies (S, self, <= 8 keys, valid kind)
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, hipStream_t st);
+
+// ---- PreAccept timestamp proposal (preaccept.hip)
+struct DevRangeMap {            // a ReducingRangeMap<Timestamp> in HBM (ad_range_map_soa)
+    uint64_t n;                 // values; starts has n + 1
+    const int64_t* starts;
+    const uint64_t* msb; const uint64_t* lsb; const int32_t* node;
+    const uint8_t* present;     // null = all present
+    uint32_t inclusive_ends;
+};
+
+struct PreacceptArgs {
+    uint64_t n;
+    const uint64_t* txn_msb; const uint64_t* txn_lsb; const int32_t* txn_node;
+    const uint64_t* key_off; const int64_t* keys;
+    DevRangeMap mc, rb;         // maxConflicts, rejectBefore
+    uint32_t permit_fast_path;
+    uint64_t node_epoch;
+    uint64_t* out_msb; uint64_t* out_lsb; int32_t* out_node; uint8_t* out_flags;
+};
+
+hipError_t run_preaccept(const PreacceptArgs& a, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,

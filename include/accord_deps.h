@@ -358,6 +358,41 @@ int ad_levels(ad_ctx* ctx, const ad_graph_soa* g, uint32_t* level_out, ad_stats*
  * Errors: AD_E_DUP_EXEC (two txns with equal executeAt), AD_E_INVAL (dep index >= n_txns). */
 int ad_levels_device(ad_ctx* ctx, const ad_graph_soa* g_dev, uint32_t* level_out_dev, void* stream, ad_stats* stats);
 
+/* ---- PreAccept timestamp proposal ------------------------------------------
+ * CommandStore.preaccept (CommandStore.java:322-347) for a batch of PreAccepts on one snapshot:
+ * minNonConflicting = maxConflicts.get(keys) -- the Timestamp.max fold of a ReducingRangeMap over
+ * the request's keys (ReducingRangeMap.foldl, ReducingRangeMap.java:123-157; MaxConflicts.java:46-50)
+ * -- and the decisions that need no clock. A ReducingRangeMap as SoA: interval i covers
+ * [starts[i], starts[i+1]) (inclusive_ends = 0) or (starts[i], starts[i+1]] (inclusive_ends = 1),
+ * starts ascending key ordinals (RoutingKey order), value i = {msb, lsb, node}, present[i] = 0
+ * for a null value. */
+typedef struct ad_range_map_soa {
+    uint64_t        n_values;
+    const int64_t*  starts;          /* [n_values + 1] */
+    const uint64_t* msb;
+    const uint64_t* lsb;
+    const int32_t*  node;
+    const uint8_t*  present;         /* NULL = all present */
+    uint32_t        inclusive_ends;
+} ad_range_map_soa;
+
+/* per-request result flags of ad_preaccept_device */
+#define AD_PA_FAST     1u   /* witnessedAt = txnId (permitFastPath, txnId >= minNonConflicting, epoch)  */
+#define AD_PA_REJECTED 2u   /* rejectBefore holds an id above txnId on a key: reply uniqueNow(txnId).asRejected() */
+#define AD_PA_ESP      4u   /* ExclusiveSyncPoint: witnessedAt = txnId (markExclusiveSyncPoint on the host) */
+
+/* Install the store's maxConflicts and rejectBefore maps (NULL = empty). Host arrays, copied. */
+int ad_preaccept_maps_load(ad_ctx* ctx, const ad_range_map_soa* max_conflicts, const ad_range_map_soa* reject_before);
+
+/* For every request of q_dev (device arrays; keys ascending): out_msb/lsb/node[i] =
+ * minNonConflicting (Timestamp.NONE = zeros when no key has a value), out_flags[i] = AD_PA_*.
+ * Without FAST/REJECTED/ESP the host replies time.uniqueNow(minNonConflicting); with REJECTED
+ * the node's clock-based expiry (preAcceptTimeout) is still the host's. Outputs in device memory;
+ * enqueued on `stream` and complete on return. */
+int ad_preaccept_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t permit_fast_path, uint64_t node_epoch,
+                        void* stream, uint64_t* out_msb, uint64_t* out_lsb, int32_t* out_node, uint8_t* out_flags,
+                        ad_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,6 +52,8 @@ def lib():
         L.rc_result_free.argtypes = [C.POINTER(RcResult)]
         L.rc_result_merge.argtypes = [C.POINTER(C.POINTER(RcResult)), C.c_int, C.POINTER(C.POINTER(RcResult))]
         L.rc_levels.argtypes = [C.POINTER(A.AdGraphSoa), C.c_void_p]
+        L.rc_preaccept.argtypes = [C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdQuerySoa),
+                                   C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rc_tid_cmp.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         _lib = L
     return _lib
@@ -224,6 +226,20 @@ def levels(graph):
     if rc:
         raise OracleError(rc, "levels")
     return out
+
+
+def preaccept(max_conflicts, reject_before, queries, permit_fast_path=1, node_epoch=0):
+    """rc_preaccept: (minNonConflicting Tids, AD_PA_* flags) per request."""
+    n = len(queries)
+    om, ol = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    on, of = np.zeros(n, np.int32), np.zeros(n, np.uint8)
+    mc = max_conflicts.soa() if max_conflicts is not None else None
+    rb = reject_before.soa() if reject_before is not None else None
+    rc = lib().rc_preaccept(C.byref(mc) if mc else None, C.byref(rb) if rb else None, C.byref(queries.soa()),
+                            permit_fast_path, node_epoch, A.ptr(om), A.ptr(ol), A.ptr(on), A.ptr(of))
+    if rc:
+        raise OracleError(rc, "preaccept")
+    return Tids(om, ol, on), of
 
 
 def tid_cmp(a, b):

@@ -1175,3 +1175,108 @@ int rc_levels(const ad_graph_soa* g, uint32_t* level)
     free(kv); free(pos_of); free(cursor); free(order);
     return rc;
 }
+
+
+/* ---------------------------------------------------------------------------------------------
+ * PreAccept timestamp proposal
+ * ------------------------------------------------------------------------------------------- */
+
+/* Arrays.binarySearch over starts[lo, hi) (ascending, distinct): index, or -(insertion) - 1 */
+static int64_t bsearch_i64(const int64_t* a, int64_t lo, int64_t hi, int64_t key)
+{
+    int64_t l = lo, h = hi - 1;
+    while (l <= h)
+    {
+        int64_t mid = (l + h) >> 1;
+        if (a[mid] < key) l = mid + 1;
+        else if (a[mid] > key) h = mid - 1;
+        else return mid;
+    }
+    return -(l + 1);
+}
+
+/* Keys.findNext(from, key, FAST): first index >= from whose key is >= key, as binarySearch encodes it */
+static int64_t keys_find_next(const int64_t* keys, int64_t from, int64_t n, int64_t key)
+{
+    return bsearch_i64(keys, from, n, key);
+}
+
+typedef void (*rmap_fold_fn)(const tid_t* v, void* acc);
+
+/* ReducingRangeMap.foldl(AbstractKeys, ...) (ReducingRangeMap.java:123-157): the value of every
+ * interval holding at least one key, in ascending order, intervals with a null value skipped */
+static int rmap_foldl_keys(const ad_range_map_soa* m, const int64_t* keys, int64_t nk, rmap_fold_fn fold, void* acc,
+                           int (*terminate)(void*))
+{
+    if (!m || m->n_values == 0) return 0;
+    const int64_t* starts = m->starts;
+    const int64_t ns = (int64_t)m->n_values + 1, nv = (int64_t)m->n_values;
+    int64_t i = 0, j = keys_find_next(keys, 0, nk, starts[0]);
+    if (j < 0) j = -1 - j;
+    else if (m->inclusive_ends) ++j;
+    while (j < nk)
+    {
+        i = bsearch_i64(starts, i, ns, keys[j]);          /* exponentialSearch(starts, i, starts.length, key) */
+        if (i < 0) i = -2 - i;
+        else if (m->inclusive_ends) --i;
+        if (i >= nv) return 0;
+        int64_t nextj = keys_find_next(keys, j, nk, starts[i + 1]);
+        if (nextj < 0) nextj = -1 - nextj;
+        else if (m->inclusive_ends) ++nextj;
+        if (j != nextj && (!m->present || m->present[i]))
+        {
+            tid_t v = {m->msb[i], m->lsb[i], m->node[i]};
+            fold(&v, acc);
+            if (terminate && terminate(acc)) return 1;
+        }
+        ++i;
+        j = nextj;
+    }
+    return 0;
+}
+
+/* Timestamp::max applied as fold(value, accumulator): value if value >= accumulator */
+static void fold_max(const tid_t* v, void* acc)
+{
+    tid_t* a = (tid_t*)acc;
+    if (tid_cmp(v, a) >= 0) *a = *v;
+}
+
+/* rejectBefore: (rejectIfBefore, test) -> rejectIfBefore > test ? null : test, starting at txnId */
+typedef struct { tid_t test; int is_null; } reject_acc_t;
+
+static void fold_reject(const tid_t* v, void* acc)
+{
+    reject_acc_t* a = (reject_acc_t*)acc;
+    if (!a->is_null && tid_cmp(v, &a->test) > 0) a->is_null = 1;
+}
+
+static int reject_terminate(void* acc) { return ((reject_acc_t*)acc)->is_null; }
+
+int rc_preaccept(const ad_range_map_soa* mc, const ad_range_map_soa* rb, const ad_query_soa* q, uint32_t permit_fast_path,
+                 uint64_t node_epoch, uint64_t* out_msb, uint64_t* out_lsb, int32_t* out_node, uint8_t* out_flags)
+{
+    for (uint64_t t = 0; t < q->n_txns; ++t)
+    {
+        const tid_t txn = {q->txn_msb[t], q->txn_lsb[t], q->txn_node[t]};
+        const int64_t* keys = q->keys + q->key_off[t];
+        const int64_t nk = (int64_t)(q->key_off[t + 1] - q->key_off[t]);
+        uint8_t flags = 0;
+        tid_t mn = {0, 0, 0};                                  /* Timestamp.NONE */
+        /* isExpired via rejectBefore (the clock-based part is the host's) */
+        reject_acc_t ra = {txn, 0};
+        rmap_foldl_keys(rb, keys, nk, fold_reject, &ra, reject_terminate);
+        if (ra.is_null) flags |= AD_PA_REJECTED;
+        else if (((txn.lsb >> 1) & 7) == AD_KIND_EXCLUSIVE_SYNC_POINT) flags |= AD_PA_ESP;
+        else
+        {
+            rmap_foldl_keys(mc, keys, nk, fold_max, &mn, NULL);
+            if (permit_fast_path && tid_cmp(&txn, &mn) >= 0 && (txn.msb >> 15) >= node_epoch) flags |= AD_PA_FAST;
+        }
+        out_msb[t] = mn.msb;
+        out_lsb[t] = mn.lsb;
+        out_node[t] = mn.node;
+        out_flags[t] = flags;
+    }
+    return 0;
+}

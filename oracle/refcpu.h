@@ -54,6 +54,12 @@ int rc_result_merge(const rc_result* const* parts, int n_parts, rc_result** out)
 
 int rc_levels(const ad_graph_soa* g, uint32_t* level_out);
 
+/* CommandStore.preaccept (CommandStore.java:322-347) minus the clock: minNonConflicting and the
+ * AD_PA_* flags per request (include/accord_deps.h, ad_preaccept_device). */
+int rc_preaccept(const ad_range_map_soa* max_conflicts, const ad_range_map_soa* reject_before, const ad_query_soa* q,
+                 uint32_t permit_fast_path, uint64_t node_epoch, uint64_t* out_msb, uint64_t* out_lsb, int32_t* out_node,
+                 uint8_t* out_flags);
+
 /* exposed for the tests */
 int rc_tid_cmp(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
 

@@ -175,3 +175,41 @@ def levels_by_rounds(g):
         done += len(ready)
         r += 1
     return level
+
+
+def rmap_value(m, k):
+    """The value of ReducingRangeMap m at key k (ReducingIntervalMap.find, ReducingIntervalMap.java:
+    176-182): interval i = #starts <= k minus one ([s_i, s_i+1) intervals) or #starts < k minus
+    one ((s_i, s_i+1] intervals); None outside the map or for a null value."""
+    if m is None or len(m) == 0:
+        return None
+    st = [int(x) for x in m.starts]
+    i = sum(1 for s in st if (s < k if m.inclusive_ends else s <= k)) - 1
+    if i < 0 or i >= len(m):
+        return None
+    if m.present is not None and not m.present[i]:
+        return None
+    return (int(m.values.msb[i]), int(m.values.lsb[i]), int(m.values.node[i]))
+
+
+def preaccept_model(mc, rb, q, permit_fast_path=1, node_epoch=0):
+    """CommandStore.preaccept (CommandStore.java:322-347) without the clock, key by key:
+    -> list of (minNonConflicting (msb, lsb, node), AD_PA_* flags)."""
+    out = []
+    for t in range(len(q)):
+        txn = (int(q.txn.msb[t]), int(q.txn.lsb[t]), int(q.txn.node[t]))
+        ks = [int(k) for k in q.keys[int(q.key_off[t]):int(q.key_off[t + 1])]]
+        if any(v is not None and key(v) > key(txn) for v in (rmap_value(rb, k) for k in ks)):
+            out.append(((0, 0, 0), 2))
+            continue
+        if kind(txn) == 4:
+            out.append(((0, 0, 0), 4))
+            continue
+        acc = (0, 0, 0)
+        for k in ks:
+            v = rmap_value(mc, k)
+            if v is not None and key(v) >= key(acc):       # Timestamp::max(value, accumulator)
+                acc = v
+        fast = permit_fast_path and key(txn) >= key(acc) and (txn[0] >> 15) >= node_epoch
+        out.append((acc, 1 if fast else 0))
+    return out

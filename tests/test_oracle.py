@@ -188,3 +188,27 @@ def test_oracle_rejects_invalid_inputs(oracle):
     with pytest.raises(oracle.OracleError) as e:
         st.load(Workload("bad", cfk, RangeCommands.empty(), Redundant.empty(), None))
     assert e.value.code == A.AD_E_ORDER
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_preaccept_oracle_vs_model(oracle, seed):
+    # rc_preaccept (ReducingRangeMap.foldl restated with its search structure) against the key-by-key
+    # model in refmodel.py: both interval conventions, null values, keys on interval starts, ties
+    # of equal Timestamps with different non-identity flags, ExclusiveSyncPoints, rejectBefore
+    import refmodel
+    for ie in (0, 1):
+        q, mc, rb = synth.preaccept_workload(seed, inclusive_ends=ie, with_reject=(seed % 3 != 0))
+        for permit, ep in ((1, 0), (0, 0), (1, 2)):
+            got, fl = oracle.preaccept(mc, rb, q, permit, ep)
+            exp = refmodel.preaccept_model(mc, rb, q, permit, ep)
+            for t, (v, f) in enumerate(exp):
+                assert (int(got.msb[t]), int(got.lsb[t]), int(got.node[t])) == v and int(fl[t]) == f, (ie, permit, ep, t)
+
+
+def test_preaccept_oracle_empty_maps(oracle):
+    from accord_deps.model import RangeMap
+    q, _, _ = synth.preaccept_workload(1)
+    got, fl = oracle.preaccept(RangeMap.empty(), None, q, 1, 0)
+    assert not got.msb.any() and not got.lsb.any()
+    kinds = (q.txn.lsb >> np.uint64(1)) & np.uint64(7)
+    assert np.array_equal(fl, np.where(kinds == 4, 4, 1).astype(np.uint8))    # NONE <= every txnId
