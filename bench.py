@@ -308,6 +308,7 @@ def bench_preaccept(args, rank, world, local, dev):
                       seed=0xACC0D002 + rank)
     mc = synth.max_conflicts_from_cfk(w.cfk)
     st = native.DeviceCommandStore(device=local)
+    st.load(w)                 # the store's snapshot: its keys carry per-key interval indexes
     st.load_preaccept_maps(mc, None)
     qdev, keep = native.device_queries(w.queries, dev)
     n = len(w.queries)

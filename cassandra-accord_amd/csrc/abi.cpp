@@ -221,6 +221,9 @@ struct ad_ctx {
         uint32_t inclusive_ends = 0;
         bool has_present = false;
     } pa_mc, pa_rb;
+    uint64_t pa_gen = 0, snap_gen = 0;         // map loads / snapshot builds
+    uint64_t pa_iv_gen[2] = {~0ull, ~0ull};    // (pa_gen, snap_gen) the per-key values were built for
+    DevBuf pa_key_val;
     // global dictionary of the multi-store exchange (ad_set_global_dict)
     DevBuf g_msb, g_lsb, g_node, g_map, g_err;
     uint64_t n_global = 0;
@@ -728,6 +731,7 @@ static int build_snapshot(ad_ctx* c)
     HIPCHK(c, build_range_trees(s, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->dirty = false;
+    ++c->snap_gen;
     c->global_ok = false;        // the dictionary changed: a global dictionary must be installed again
     c->ms_ingest = now_ms() - t0;
     return 0;
@@ -1418,6 +1422,7 @@ int ad_preaccept_maps_load(ad_ctx* c, const ad_range_map_soa* max_conflicts, con
 {
     if (!c) return AD_E_INVAL;
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    ++c->pa_gen;
     int rc = load_range_map(c, max_conflicts, c->pa_mc, "ad_preaccept_maps_load: maxConflicts");
     return rc ? rc : load_range_map(c, reject_before, c->pa_rb, "ad_preaccept_maps_load: rejectBefore");
 }
@@ -1440,6 +1445,20 @@ int ad_preaccept_device(ad_ctx* c, const ad_query_soa* q, uint32_t permit_fast_p
     a.permit_fast_path = permit_fast_path ? 1u : 0u;
     a.node_epoch = node_epoch;
     a.out_msb = out_msb; a.out_lsb = out_lsb; a.out_node = out_node; a.out_flags = out_flags;
+    if (c->cfk.loaded && !c->dirty && c->ds.n_keys && c->ds.khash)
+    {
+        // per snapshot key, its values in both maps (once per snapshot and maps)
+        if (c->pa_iv_gen[0] != c->pa_gen || c->pa_iv_gen[1] != c->snap_gen)
+        {
+            if (!c->pa_key_val.ensure(2 * sizeof(PaValue) * c->ds.n_keys)) return c->fail(AD_E_NOMEM, "preaccept key values");
+            HIPCHK(c, run_preaccept_key_values(a.mc, a.rb, c->ds.keys, c->ds.n_keys, c->pa_key_val.as<PaValue>(), st));
+            c->pa_iv_gen[0] = c->pa_gen;
+            c->pa_iv_gen[1] = c->snap_gen;
+        }
+        a.khash = c->ds.khash;
+        a.khash_mask = c->ds.khash_mask;
+        a.key_val = c->pa_key_val.as<PaValue>();
+    }
     HIPCHK(c, hipEventRecord(c->ev[6], st));
     HIPCHK(c, run_preaccept(a, st));
     HIPCHK(c, hipEventRecord(c->ev[7], st));

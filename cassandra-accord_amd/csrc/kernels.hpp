@@ -99,9 +99,23 @@ struct PreacceptArgs {
     uint32_t permit_fast_path;
     uint64_t node_epoch;
     uint64_t* out_msb; uint64_t* out_lsb; int32_t* out_node; uint8_t* out_flags;
+    // the snapshot's key index (null khash: none): a key found there takes its values from
+    // key_val[2 * key index] (maxConflicts, rejectBefore): one 64-byte line per key
+    const KeySlot* khash; uint64_t khash_mask;
+    const struct PaValue* key_val;
+};
+
+struct alignas(32) PaValue {     // a map's value at one key (present = 0: none)
+    uint64_t msb, lsb;
+    int32_t node;
+    uint32_t present;
+    uint64_t pad;
 };
 
 hipError_t run_preaccept(const PreacceptArgs& a, hipStream_t st);
+// key_val[2i], key_val[2i+1] = the values of snapshot key i in maxConflicts / rejectBefore
+hipError_t run_preaccept_key_values(const DevRangeMap& mc, const DevRangeMap& rb, const int64_t* keys, uint64_t n_keys,
+                                    PaValue* key_val, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,

@@ -7,7 +7,8 @@
 //     of the intervals holding its keys (ReducingRangeMap.foldl, ReducingRangeMap.java:123-157),
 //     fold(value, accumulator) keeping the value on ties; fast path iff permitted, txnId >=
 //     minNonConflicting and txnId's epoch >= the node's.
-// 8 lanes per request; a key's interval by binary search over the map's starts.
+// 8 lanes per request; a key's values from a per-key table of the snapshot's keys (one KeySlot probe,
+// one 64-byte line), or by binary search over the map's starts.
 #include <hip/hip_runtime.h>
 
 #include "../../include/accord_deps.h"
@@ -41,6 +42,42 @@ __device__ __forceinline__ bool value_at(const DevRangeMap& m, int64_t x, uint64
     return !m.present || m.present[i];
 }
 
+__device__ __forceinline__ PaValue value_of(const DevRangeMap& m, int64_t x)
+{
+    uint64_t i;
+    PaValue v{0, 0, 0, 0, 0};
+    if (value_at(m, x, i))
+    {
+        v.msb = m.msb[i];
+        v.lsb = m.lsb[i];
+        v.node = m.node[i];
+        v.present = 1;
+    }
+    return v;
+}
+
+// the snapshot key index of x (KeySlot open addressing, as k_prepare), or KEY_EMPTY
+__device__ __forceinline__ uint32_t key_index(const PreacceptArgs& a, int64_t x)
+{
+    if (!a.khash) return KEY_EMPTY;
+    uint64_t h = key_hash(x) & a.khash_mask;
+    while (true)
+    {
+        const KeySlot ks = a.khash[h];
+        if (ks.idx == KEY_EMPTY || ks.key == x) return ks.idx;
+        h = (h + 1) & a.khash_mask;
+    }
+}
+
+__global__ void k_key_values(DevRangeMap mc, DevRangeMap rb, const int64_t* keys, uint64_t n_keys, PaValue* key_val)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_keys) return;
+    const int64_t x = keys[i];
+    key_val[2 * i] = value_of(mc, x);
+    key_val[2 * i + 1] = value_of(rb, x);
+}
+
 // 8 lanes per request: lane j searches keys j, j+8, ...; the group reduces (rejected: any;
 // max: the largest value, on ties the one of the later key, as the ascending fold keeps it)
 constexpr uint32_t PA_LANES = 8;
@@ -70,12 +107,23 @@ __global__ __launch_bounds__(256) void k_preaccept(PreacceptArgs a)
     for (uint64_t k = k0 + j; k < k1; k += PA_LANES)
     {
         const int64_t x = a.keys[k];
-        uint64_t i;
-        if (value_at(a.rb, x, i)) rejected = rejected || norm_cmp(norm_tid(a.rb.msb[i], a.rb.lsb[i], a.rb.node[i]), txn) > 0;
-        if (esp) continue;
-        if (!value_at(a.mc, x, i)) continue;
-        const uint64_t vm = a.mc.msb[i], vl = a.mc.lsb[i];
-        const int32_t vn = a.mc.node[i];
+        // the key's values: precomputed for snapshot keys, else by search
+        const uint32_t ki = key_index(a, x);
+        PaValue vmc, vrb;
+        if (ki != KEY_EMPTY)
+        {
+            vmc = a.key_val[2 * (uint64_t)ki];
+            vrb = a.key_val[2 * (uint64_t)ki + 1];
+        }
+        else
+        {
+            vmc = value_of(a.mc, x);
+            vrb = value_of(a.rb, x);
+        }
+        if (vrb.present) rejected = rejected || norm_cmp(norm_tid(vrb.msb, vrb.lsb, vrb.node), txn) > 0;
+        if (esp || !vmc.present) continue;
+        const uint64_t vm = vmc.msb, vl = vmc.lsb;
+        const int32_t vn = vmc.node;
         const NormTid v = norm_tid(vm, vl, vn);
         const uint32_t kp = (uint32_t)(k - k0) + 1;
         if (later_max(v, kp, acc, kbest) || kbest == 0)
@@ -112,6 +160,13 @@ __global__ __launch_bounds__(256) void k_preaccept(PreacceptArgs a)
 }
 
 }  // namespace
+
+hipError_t run_preaccept_key_values(const DevRangeMap& mc, const DevRangeMap& rb, const int64_t* keys, uint64_t n_keys,
+                                    PaValue* key_val, hipStream_t st)
+{
+    if (n_keys) k_key_values<<<(unsigned)((n_keys + 255) / 256), 256, 0, st>>>(mc, rb, keys, n_keys, key_val);
+    return hipGetLastError();
+}
 
 hipError_t run_preaccept(const PreacceptArgs& a, hipStream_t st)
 {

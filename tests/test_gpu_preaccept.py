@@ -10,13 +10,18 @@ from accord_deps.model import RangeMap
 pytestmark = pytest.mark.gpu
 
 
-def _check(q, mc, rb, oracle, permit=1, epoch=0):
-    st = native.DeviceCommandStore(0)
+def _check(q, mc, rb, oracle, permit=1, epoch=0, snapshot=None, st=None):
+    own = st is None
+    if own:
+        st = native.DeviceCommandStore(0)
+        if snapshot is not None:
+            st.load(snapshot)                 # keys of the snapshot take the per-key interval indexes
     try:
         st.load_preaccept_maps(mc, rb)
         got, fl, stats = st.preaccept(q, permit, epoch)
     finally:
-        st.close()
+        if own:
+            st.close()
     exp, efl = oracle.preaccept(mc, rb, q, permit, epoch)
     assert np.array_equal(fl, efl), np.nonzero(fl != efl)[0][:5]
     for a in ("msb", "lsb", "node"):
@@ -40,8 +45,28 @@ def test_empty_maps_and_batch(oracle):
 
 
 def test_config2_scale(oracle):
-    # config-2 requests against the maxConflicts of its CommandsForKey history (1M point intervals)
+    # config-2 requests against the maxConflicts of its CommandsForKey history (point intervals),
+    # with and without the snapshot loaded (per-key interval indexes vs binary search)
     w = synth.config2(n_txns=200_000, n_keys=200_000, n_hist_entries=2_000_000)
     mc = synth.max_conflicts_from_cfk(w.cfk)
     fl, stats = _check(w.queries, mc, None, oracle)
     assert (fl == 1).any() and stats["ms_device"] > 0
+    _check(w.queries, mc, None, oracle, snapshot=w)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_snapshot_key_index(oracle, seed):
+    # a loaded snapshot whose keys cover part of the requests' keys; maps replaced after first use
+    # (the per-key indexes are rebuilt for the new maps)
+    from accord_deps import synth as S
+    w = S.random_small(300 + seed, n_keys=200)
+    q, mc, rb = S.preaccept_workload(seed, key_space=1000, inclusive_ends=seed % 2)
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        _check(q, mc, rb, oracle, st=st)
+        q2, mc2, rb2 = S.preaccept_workload(seed + 50, key_space=1000, inclusive_ends=(seed + 1) % 2)
+        _check(q, mc2, rb2, oracle, st=st)
+        _check(q2, mc2, None, oracle, st=st)
+    finally:
+        st.close()
