@@ -351,6 +351,89 @@ def bench_preaccept(args, rank, world, local, dev):
         dist.destroy_process_group()
 
 
+def bench_union(args, rank, world, local, dev):
+    """SURVEY §8 f2 on config 2's batch: the coordinator's Deps.merge of R replica replies
+    (ad_parts_union). R stores hold the config-2 snapshot (replicas that agree: every pair arrives R
+    times, the full-deduplication case), each resolves the batch and exports its PartialDeps as
+    rank-format parts; the timed step is the union of all R replies for every request. With N GPUs,
+    N replicas of the job."""
+    s = args.scale
+    R = args.union
+    w = synth.config2(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_hist_entries=int(16_000_000 * s),
+                      seed=0xACC0D002 + rank)
+    n = len(w.queries)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    engines, keep = [], []
+    for r in range(R):
+        st = native.DeviceCommandStore(device=local)
+        st.load(w)
+        qdev, k = native.device_queries(w.queries, dev)
+        keep.append(k)
+        engines.append(exchange.GpuEngine(st, qdev, np.arange(n), dev, stream=sp))
+    g = exchange.build_global_dict([e.dictionary() for e in engines])
+    for e in engines:
+        e.set_global_dict(g)
+    sends = []
+    for e in engines:
+        e.resolve()
+        sends.append(e.export(np.array([0, n], np.uint64)))
+    torch.cuda.synchronize(dev)
+    recv, totals = {}, np.zeros(4, np.int64)
+    for a, (name, mult) in enumerate((("hdr", 4), ("keys", 1), ("ids", 1), ("k2t", 1))):
+        recv[name] = torch.cat([sd[0][name][:int(sd[1][0, a]) * mult] for sd in sends])
+    for sd in sends:
+        totals += sd[1][0]
+    p = A.AdParts()
+    p.hdr, p.keys, p.ids, p.k2t = (recv[k].data_ptr() for k in ("hdr", "keys", "ids", "k2t"))
+    p.n_parts, p.n_key_words, p.n_ids, p.n_k2t = (int(x) for x in totals)
+    p.id_format = A.AD_IDS_RANK
+    owner = engines[0].store
+    src = [int(sd[1][0, 0]) for sd in sends]
+    last = {}
+
+    def step():
+        last["mg"] = owner.union_parts(p, src, 0, n, sp)
+        return {"ms_device": last["mg"].ms_device}
+    elapsed, all_stats = _timed_steps(args, world, dev, step)
+    in_pairs = int(totals[3] - totals[1])
+    pairs = _sum_over_ranks(world, dev, in_pairs)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    kernel_ms = float(np.mean([x["ms_device"] for x in all_stats]))
+    mg = last["mg"]
+    out_bytes = sum(8 * int(mg.n_keys[m]) + 4 * int(mg.n_ids[m]) + 4 * int(mg.n_k2t[m]) for m in range(3))
+    alg = int(32 * totals[0] + 8 * totals[1] + 4 * totals[2] + 4 * totals[3]) + out_bytes
+    achieved = alg / (kernel_ms / 1000.0) / 1e9 if kernel_ms > 0 else 0.0
+    res = {
+        "metric": "Deps.merge of replica replies: input txn-key pairs/sec", "value": pairs / (ms_per_step / 1000.0),
+        "unit": "txn-key pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "config2 batch (%d txns x 8 keys), %d replica replies per request (SURVEY 8 f2)" % (n, R),
+                   "input_pairs_per_step": pairs, "parallelism": "replicas x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_union_rank + k_union_emit", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": alg, "launch_ms": kernel_ms},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        m = min(n, 1_000)
+        reps = [pyoracle.resolve(w, first=0, count=m) for r in range(R)]
+        t0 = time.perf_counter()
+        merged = pyoracle.merge_batches(reps)
+        t = time.perf_counter() - t0
+        sp_pairs = sum(int(b.pair_count(mm)) for b in reps for mm in range(3))
+        res["cpu_baseline"] = dict(value=sp_pairs / t, unit="txn-key pairs/s", cores=1, kind="port",
+                                   sample="first %d requests' %d replies (%.2f s), rc_result_merge, 1 thread" % (m, R, t))
+        del merged
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    for e in engines:
+        e.store.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def bench_sequential(args, rank, world, local, dev):
     """Config 1: 10k txns x 4 keys over 1k keys, one CommandStore, SEQUENTIAL PreAccept (each txn
     inserted as PREACCEPTED before its deps). SEQUENTIAL runs through the host API: a step is one
@@ -408,6 +491,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=(1, 2, 4, 5),
                     help="2: BASELINE config 2 (the headline line, default); 1: SEQUENTIAL PreAccept batch "
                          "(host API); 4: range transactions; 5: execution levels (K5)")
+    ap.add_argument("--union", type=int, default=0, metavar="R",
+                    help="with config 2: the coordinator's Deps.merge of R replica replies (SURVEY 8 f2)")
     ap.add_argument("--preaccept", action="store_true",
                     help="with config 2: the PreAccept timestamp proposal (SURVEY 8 f3) instead of deps")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -440,6 +525,8 @@ def main():
         return bench_sequential(args, rank, world, local, dev)
     if args.preaccept:
         return bench_preaccept(args, rank, world, local, dev)
+    if args.union:
+        return bench_union(args, rank, world, local, dev)
 
     s = args.scale
     t0 = time.time()

@@ -22,7 +22,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
            "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict", "ad_preaccept_maps_load",
-           "ad_preaccept_device")
+           "ad_preaccept_device", "ad_parts_union")
 
 
 class AccordDepsError(RuntimeError):
@@ -68,6 +68,8 @@ def lib():
         L.ad_parts_merge.argtypes = [C.c_void_p, C.POINTER(A.AdParts), C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64,
                                      C.c_void_p, C.POINTER(A.AdMerged)]
         L.ad_copy_to_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.ad_parts_union.argtypes = [C.c_void_p, C.POINTER(A.AdParts), C.c_uint32, C.c_void_p, C.c_uint64, C.c_uint64,
+                                     C.c_void_p, C.POINTER(A.AdMerged)]
         L.ad_set_global_dict.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
         L.ad_preaccept_maps_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdRangeMapSoa)]
         L.ad_preaccept_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_uint64, C.c_void_p,
@@ -265,6 +267,15 @@ class DeviceCommandStore:
         sp = np.ascontiguousarray(src_parts, dtype=np.uint64)
         out = A.AdMerged()
         self._check(lib().ad_parts_merge(self.h, C.byref(parts), len(sp), A.ptr(sp), txn_base, n_owned, stream,
+                                         C.byref(out)))
+        return out
+
+    def union_parts(self, parts, src_parts, txn_base, n_owned, stream=None):
+        """ad_parts_union: Deps.merge of rank-format parts whose keys may overlap across sources
+        (replica replies). Returns an AdMerged (device)."""
+        sp = np.ascontiguousarray(src_parts, dtype=np.uint64)
+        out = A.AdMerged()
+        self._check(lib().ad_parts_union(self.h, C.byref(parts), len(sp), A.ptr(sp), txn_base, n_owned, stream,
                                          C.byref(out)))
         return out
 

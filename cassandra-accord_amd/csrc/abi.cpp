@@ -214,6 +214,7 @@ struct ad_ctx {
     bool last_parts_only = false;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
     DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t, m_u, m_ppre;
+    DevBuf m_kdp, m_kuk, m_khead, m_pdp, m_ppos;   // ad_parts_union scratch
     // maxConflicts / rejectBefore of the PreAccept timestamp proposal (ad_preaccept_maps_load)
     struct RangeMapBufs {
         DevBuf starts, msb, lsb, node, present;
@@ -1576,10 +1577,12 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     return AD_OK;
 }
 
-int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
-                   uint64_t n_owned, void* stream, ad_merged* out)
+static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
+                       uint64_t n_owned, void* stream, ad_merged* out, bool union_keys)
 {
     if (!c || !in || !src_parts || !out || n_src == 0 || n_src > 64) return AD_E_INVAL;
+    if (union_keys && in->id_format != AD_IDS_RANK)
+        return c->fail(AD_E_INVAL, "ad_parts_union: parts must carry global ranks (ad_set_global_dict)");
     uint64_t tot = 0;
     std::vector<uint64_t> first(n_src + 1, 0);
     for (uint32_t s = 0; s < n_src; ++s) first[s + 1] = (tot += src_parts[s]);
@@ -1593,6 +1596,10 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
         return c->fail(AD_E_INVAL, "ad_parts_merge: rank-format parts need ad_set_global_dict on this ctx");
     if (rank_ids && (!ens<uint32_t>(c->m_u, in->n_ids) || !ens<uint32_t>(c->m_ppre, 2 * P)))
         return c->fail(AD_E_NOMEM, "merge buffers");
+    if (union_keys && (!ens<uint32_t>(c->m_kdp, in->n_key_words) || !ens<uint32_t>(c->m_kuk, in->n_key_words) ||
+                       !ens<uint32_t>(c->m_khead, in->n_key_words) || !ens<uint32_t>(c->m_pdp, in->n_k2t) ||
+                       !ens<uint32_t>(c->m_ppos, in->n_k2t)))
+        return c->fail(AD_E_NOMEM, "union buffers");
     if (!ens<uint64_t>(c->m_src, n_src + 1) || !ens<uint32_t>(c->m_psz, 3 * P) || !ens<uint64_t>(c->m_poff, 3 * (P + 1)) ||
         !ens<int32_t>(c->m_slot, G * n_src) || !ens<uint32_t>(c->m_dup, in->n_ids) || !ens<uint32_t>(c->m_gsz, 3 * G) ||
         !ens<uint64_t>(c->m_goff, 3 * (G + 1)) ||
@@ -1626,6 +1633,11 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
         a.g_lsb = c->g_lsb.as<uint64_t>();
         a.g_node = c->g_node.as<int32_t>();
     }
+    if (union_keys)
+    {
+        a.kdp = c->m_kdp.as<uint32_t>(); a.kuk = c->m_kuk.as<uint32_t>(); a.khead = c->m_khead.as<uint32_t>();
+        a.pdp = c->m_pdp.as<uint32_t>(); a.ppos = c->m_ppos.as<uint32_t>();
+    }
     HIPCHK(c, hipEventRecord(c->ev[6], st));
     HIPCHK(c, hipMemcpyAsync(c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemsetAsync(a.error, 0, sizeof(uint32_t), st));
@@ -1633,7 +1645,7 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     HIPCHK(c, run_merge_prepare(a, st));
     HIPCHK(c, run_scan_arrays(a.psz, a.poff, P, 3, c->m_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_merge_slots(a, st));
-    HIPCHK(c, rank_ids ? run_merge_rank(a, st) : run_merge_count(a, st));
+    HIPCHK(c, union_keys ? run_union_rank(a, st) : rank_ids ? run_merge_rank(a, st) : run_merge_count(a, st));
     HIPCHK(c, run_scan_arrays(a.gsz, a.goff, G, 3, c->m_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_merge_bases(a, c->m_bases.as<uint64_t>(), st));
     uint64_t bases[12];
@@ -1657,7 +1669,7 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
     a.o_k2t = c->m_k2t.as<int32_t>();
     if (n_owned == 0)
         for (DevBuf* b : {&c->m_ko, &c->m_to, &c->m_oo}) HIPCHK(c, hipMemsetAsync(b->p, 0, sizeof(uint64_t) * 3, st));
-    HIPCHK(c, rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
+    HIPCHK(c, union_keys ? run_union_emit(a, st) : rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
     HIPCHK(c, hipEventRecord(c->ev[7], st));
     HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
@@ -1683,6 +1695,18 @@ int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t
         out->n_k2t[m] = bases[3 * (m + 1) + 2] - bases[3 * m + 2];
     }
     return AD_OK;
+}
+
+int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
+                   uint64_t n_owned, void* stream, ad_merged* out)
+{
+    return parts_merge(c, in, n_src, src_parts, txn_base, n_owned, stream, out, false);
+}
+
+int ad_parts_union(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
+                   uint64_t n_owned, void* stream, ad_merged* out)
+{
+    return parts_merge(c, in, n_src, src_parts, txn_base, n_owned, stream, out, true);
 }
 
 int ad_copy_to_host(ad_ctx* c, void* dst, const void* src, uint64_t bytes)

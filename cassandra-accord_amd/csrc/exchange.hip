@@ -662,6 +662,355 @@ __global__ void k_merge_emit_rank(MergeArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// ad_parts_union: Deps.merge of replies whose key sets overlap (Deps.java:281-286 via
+// PartialDeps.with / RelationMultiMap.linearUnion, RelationMultiMap.java:561-816). Every part
+// holds three sorted, duplicate-free lists -- its keys, its ids, and its (key, id) pairs -- and
+// the merged map is their union in each: an element's union index is
+//     rank(x) = sum over parts q of ( lb_q(x) - dupsBefore_q(lb_q(x)) )
+// (an element is a dup when an earlier part holds an equal one). Keys of range maps compare as
+// (start, end) (Range.compare). Pass 1 (wave per group) ranks keys, then ids, then pairs (whose
+// value is (key union index, id union index)), and sets each union key's head = union keys +
+// distinct pairs with a smaller or equal key; pass 2 (8 lanes per part) writes them.
+// ---------------------------------------------------------------------------------------
+struct KeyV { int64_t a, b; };
+__device__ __forceinline__ bool lt(const KeyV& x, const KeyV& y) { return x.a < y.a || (x.a == y.a && x.b < y.b); }
+__device__ __forceinline__ bool eqv(const KeyV& x, const KeyV& y) { return x.a == y.a && x.b == y.b; }
+__device__ __forceinline__ bool lt(uint64_t x, uint64_t y) { return x < y; }
+__device__ __forceinline__ bool eqv(uint64_t x, uint64_t y) { return x == y; }
+
+// the P lists of one group: val(q, i), len(q), and the scratch slot of element (q, i)
+template <class V, class Val, class Len, class Slot>
+struct UnionLists {
+    uint32_t np; Val val; Len len; Slot slot;
+    __device__ uint32_t lb(uint32_t q, const V& x) const
+    {
+        uint32_t lo = 0, hi = len(q);
+        while (lo < hi)
+        {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (lt(val(q, mid), x)) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    }
+    // distinct elements of all lists below x (dp: per-list exclusive dup prefix | DUP_BIT)
+    __device__ uint32_t rank_of(const V& x, const uint32_t* dp, uint32_t own_q = ~0u, uint32_t own_pos = 0) const
+    {
+        uint32_t r = 0;
+        for (uint32_t q = 0; q < np; ++q)
+        {
+            const uint32_t n = len(q);
+            const uint32_t b = q == own_q ? own_pos : lb(q, x);
+            uint32_t before;
+            if (b < n) before = dp[slot(q, b)] & ~DUP_BIT;
+            else if (n == 0) before = 0;
+            else
+            {
+                const uint32_t d = dp[slot(q, n - 1)];
+                before = (d & ~DUP_BIT) + (d >> 31);
+            }
+            r += b - before;
+        }
+        return r;
+    }
+};
+
+template <class V, class L>
+__device__ uint32_t union_rank_all(const L& ls, uint32_t* dp, uint32_t* out, uint32_t* error)
+{
+    const uint32_t l = lane_id();
+    uint32_t total = 0, dups = 0;
+    for (uint32_t q = 0; q < ls.np; ++q)
+    {
+        const uint32_t n = ls.len(q);
+        uint32_t run = 0;
+        for (uint32_t e0 = 0; e0 < n; e0 += 64)
+        {
+            const uint32_t e = e0 + l;
+            bool dup = false;
+            if (e < n)
+            {
+                const V x = ls.val(q, e);
+                if (e > 0 && !lt(ls.val(q, e - 1), x)) atomicOr(error, 8u);       // not sorted / unique
+                for (uint32_t q2 = 0; q2 < q && !dup; ++q2)
+                {
+                    const uint32_t b = ls.lb(q2, x);
+                    dup = b < ls.len(q2) && eqv(ls.val(q2, b), x);
+                }
+            }
+            const uint64_t bm = ballot(dup);
+            if (e < n) dp[ls.slot(q, e)] = (run + mbcnt(bm)) | (dup ? DUP_BIT : 0u);
+            run += __popcll(bm);
+        }
+        total += n;
+        dups += run;
+    }
+    __threadfence_block();      // written and read back by this wave only
+    for (uint32_t q = 0; q < ls.np; ++q)
+    {
+        const uint32_t n = ls.len(q);
+        for (uint32_t e = l; e < n; e += 64)
+        {
+            const V x = ls.val(q, e);
+            const uint32_t s = ls.slot(q, e);
+            out[s] = ls.rank_of(x, dp, q, e) | (dp[s] & DUP_BIT);
+        }
+    }
+    __threadfence_block();      // written and read back by this wave only
+    return total - dups;
+}
+
+template <class V, class Val, class Len, class Slot>
+__device__ UnionLists<V, Val, Len, Slot> make_lists(uint32_t np, Val v, Len n, Slot s)
+{
+    return UnionLists<V, Val, Len, Slot>{np, v, n, s};
+}
+
+// wave-private staging of one group for the fast path (keys <= UN_KCAP, ids and pairs <= UN_ECAP)
+constexpr uint32_t UN_KCAP = 64, UN_ECAP = 256;
+struct UnionLds {
+    uint32_t kst[64], ist[64], pst[64];          // per part: first key / id / pair of the group
+    KeyV kv[UN_KCAP];
+    uint32_t head[UN_KCAP], kdp[UN_KCAP], kuk[UN_KCAP];
+    uint32_t iv[UN_ECAP], idp[UN_ECAP], iu[UN_ECAP];
+    uint32_t pidx[UN_ECAP], pdp[UN_ECAP], ppos[UN_ECAP];
+    uint64_t pv[UN_ECAP];
+};
+
+__global__ void __launch_bounds__(64 * XWAVES) k_union_rank(MergeArgs a)
+{
+    __shared__ UnionLds s_un[XWAVES];
+    __shared__ PartInfo s_info[XWAVES][64];
+    PartInfo* info = s_info[threadIdx.x >> 6];
+    const uint64_t n_groups = 3 * a.n_owned;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t l = lane_id();
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    for (uint64_t g = wave; g < n_groups; g += n_waves)
+    {
+        const int m = (int)(g / a.n_owned);
+        const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
+        wave_lds_sync();
+        const uint32_t np = stage_parts(a, g, info);
+        if (np == 0)
+        {
+            if (l == 0)
+            {
+                a.gsz[0 * n_groups + g] = 0;
+                a.gsz[1 * n_groups + g] = 0;
+                a.gsz[2 * n_groups + g] = 0;
+            }
+            continue;
+        }
+        // per part: exclusive prefixes of its keys / ids / pairs over the group
+        const bool pl = l < np;
+        const uint32_t nk_l = pl ? info[l].nk : 0u, ni_l = pl ? info[l].ni : 0u;
+        const uint32_t pr_l = pl ? info[l].no - info[l].nk : 0u;
+        const uint32_t ki = wave_incl_scan(nk_l), ii = wave_incl_scan(ni_l), pi = wave_incl_scan(pr_l);
+        const uint32_t KT = uniform(__shfl(ki, (int)np - 1, 64)), T = uniform(__shfl(ii, (int)np - 1, 64));
+        const uint32_t PT = uniform(__shfl(pi, (int)np - 1, 64));
+        if (KT <= UN_KCAP && T <= UN_ECAP && PT <= UN_ECAP)
+        {
+            // ---- fast path: the group's lists staged in wave-private LDS, ranked there
+            UnionLds& L = s_un[threadIdx.x >> 6];
+            if (pl)
+            {
+                L.kst[l] = ki - nk_l;
+                L.ist[l] = ii - ni_l;
+                L.pst[l] = pi - pr_l;
+            }
+            wave_lds_sync();
+            auto part_of = [&](const uint32_t* st, uint32_t e) -> uint32_t {
+                uint32_t q = 0;
+                for (uint32_t r = 1; r < np; ++r)
+                    if (st[r] <= e) q = r;
+                return q;
+            };
+            for (uint32_t e = l; e < KT; e += 64)
+            {
+                const uint32_t q = part_of(L.kst, e), i = e - L.kst[q];
+                const uint64_t o = info[q].kbase + (uint64_t)w * i;
+                L.kv[e] = KeyV{a.keys[o], w == 2 ? a.keys[o + 1] : 0};
+                L.head[e] = (uint32_t)a.k2t[info[q].obase + i];
+            }
+            for (uint32_t e = l; e < T; e += 64)
+            {
+                const uint32_t q = part_of(L.ist, e);
+                L.iv[e] = ids[info[q].ibase + (e - L.ist[q])];
+            }
+            for (uint32_t e = l; e < PT; e += 64)
+            {
+                const uint32_t q = part_of(L.pst, e);
+                L.pidx[e] = (uint32_t)a.k2t[info[q].obase + info[q].nk + (e - L.pst[q])];
+            }
+            wave_lds_sync();
+            auto kval = [&](uint32_t q, uint32_t i) -> KeyV { return L.kv[L.kst[q] + i]; };
+            auto klen = [&](uint32_t q) -> uint32_t { return info[q].nk; };
+            auto kslot = [&](uint32_t q, uint32_t i) -> uint32_t { return L.kst[q] + i; };
+            const uint32_t KU = union_rank_all<KeyV>(make_lists<KeyV>(np, kval, klen, kslot), L.kdp, L.kuk, a.error);
+            auto ival = [&](uint32_t q, uint32_t i) -> uint64_t { return L.iv[L.ist[q] + i]; };
+            auto ilen = [&](uint32_t q) -> uint32_t { return info[q].ni; };
+            auto islot = [&](uint32_t q, uint32_t i) -> uint32_t { return L.ist[q] + i; };
+            const uint32_t U = union_rank_all<uint64_t>(make_lists<uint64_t>(np, ival, ilen, islot), L.idp, L.iu, a.error);
+            // pair values (key union index, id union index); the key is the first whose head is above nk + i
+            for (uint32_t e = l; e < PT; e += 64)
+            {
+                const uint32_t q = part_of(L.pst, e), i = e - L.pst[q];
+                const uint32_t nk = info[q].nk, k0 = L.kst[q];
+                uint32_t key = 0;
+                while (key + 1 < nk && L.head[k0 + key] <= nk + i) ++key;
+                const uint32_t idx = L.pidx[e];
+                if (idx >= info[q].ni) atomicOr(a.error, 8u);
+                const uint32_t ui = idx < info[q].ni ? L.iu[L.ist[q] + idx] & ~DUP_BIT : 0xFFFFFFFFu;
+                L.pv[e] = ((uint64_t)(L.kuk[k0 + key] & ~DUP_BIT) << 32) | ui;
+            }
+            wave_lds_sync();
+            auto pval = [&](uint32_t q, uint32_t i) -> uint64_t { return L.pv[L.pst[q] + i]; };
+            auto plen = [&](uint32_t q) -> uint32_t { return info[q].no - info[q].nk; };
+            auto pslot = [&](uint32_t q, uint32_t i) -> uint32_t { return L.pst[q] + i; };
+            const auto PL = make_lists<uint64_t>(np, pval, plen, pslot);
+            const uint32_t PU = union_rank_all<uint64_t>(PL, L.pdp, L.ppos, a.error);
+            // results to the per-element arrays of pass 2, heads of the distinct keys
+            for (uint32_t e = l; e < KT; e += 64)
+            {
+                const uint32_t q = part_of(L.kst, e);
+                const uint64_t s = info[q].kbase + (uint64_t)w * (e - L.kst[q]);
+                const uint32_t r = L.kuk[e];
+                a.kuk[s] = r;
+                if (!(r & DUP_BIT)) a.khead[s] = KU + PL.rank_of((uint64_t)((r & ~DUP_BIT) + 1) << 32, L.pdp);
+            }
+            for (uint32_t e = l; e < T; e += 64)
+            {
+                const uint32_t q = part_of(L.ist, e);
+                a.u[info[q].ibase + (e - L.ist[q])] = L.iu[e];
+            }
+            for (uint32_t e = l; e < PT; e += 64)
+            {
+                const uint32_t q = part_of(L.pst, e);
+                a.ppos[info[q].obase + info[q].nk + (e - L.pst[q])] = L.ppos[e];
+            }
+            if (l == 0)
+            {
+                a.gsz[0 * n_groups + g] = KU * w;
+                a.gsz[1 * n_groups + g] = U;
+                a.gsz[2 * n_groups + g] = KU + PU;
+            }
+            continue;
+        }
+        // ---- general path: the same ranks over the receive buffers
+        // keys
+        auto kval = [&](uint32_t q, uint32_t i) -> KeyV {
+            const uint64_t o = info[q].kbase + (uint64_t)w * i;
+            return KeyV{a.keys[o], w == 2 ? a.keys[o + 1] : 0};
+        };
+        auto klen = [&](uint32_t q) -> uint32_t { return info[q].nk; };
+        auto kslot = [&](uint32_t q, uint32_t i) -> uint32_t { return (uint32_t)(info[q].kbase + (uint64_t)w * i); };
+        const auto KL = make_lists<KeyV>(np, kval, klen, kslot);
+        const uint32_t KU = union_rank_all<KeyV>(KL, a.kdp, a.kuk, a.error);
+        // ids
+        auto ival = [&](uint32_t q, uint32_t i) -> uint64_t { return ids[info[q].ibase + i]; };
+        auto ilen = [&](uint32_t q) -> uint32_t { return info[q].ni; };
+        auto islot = [&](uint32_t q, uint32_t i) -> uint32_t { return (uint32_t)(info[q].ibase + i); };
+        const auto IL = make_lists<uint64_t>(np, ival, ilen, islot);
+        const uint32_t U = union_rank_all<uint64_t>(IL, a.dup, a.u, a.error);
+        // pairs: body entry i of part q belongs to the key whose head (absolute end offset) is the
+        // first above nk + i; value = (key union index, id union index)
+        auto pval = [&](uint32_t q, uint32_t i) -> uint64_t {
+            const PartInfo& pi = info[q];
+            uint32_t lo = 0, hi = pi.nk;
+            while (lo < hi)
+            {
+                const uint32_t mid = (lo + hi) >> 1;
+                if ((uint32_t)a.k2t[pi.obase + mid] <= pi.nk + i) lo = mid + 1;
+                else hi = mid;
+            }
+            const uint32_t key = lo < pi.nk ? lo : pi.nk - 1;
+            const uint32_t idx = (uint32_t)a.k2t[pi.obase + pi.nk + i];
+            const uint32_t uk = a.kuk[pi.kbase + (uint64_t)w * key] & ~DUP_BIT;
+            const uint32_t ui = idx < pi.ni ? a.u[pi.ibase + idx] & ~DUP_BIT : 0xFFFFFFFFu;
+            return ((uint64_t)uk << 32) | ui;
+        };
+        auto plen = [&](uint32_t q) -> uint32_t { return info[q].no - info[q].nk; };
+        auto pslot = [&](uint32_t q, uint32_t i) -> uint32_t { return (uint32_t)(info[q].obase + info[q].nk + i); };
+        const auto PL = make_lists<uint64_t>(np, pval, plen, pslot);
+        const uint32_t PU = union_rank_all<uint64_t>(PL, a.pdp, a.ppos, a.error);
+        // heads: union keys + distinct pairs whose key index is <= the key's
+        for (uint32_t q = 0; q < np; ++q)
+            for (uint32_t i = l; i < info[q].nk; i += 64)
+            {
+                const uint32_t s = kslot(q, i);
+                const uint32_t r = a.kuk[s];
+                if (r & DUP_BIT) continue;
+                a.khead[s] = KU + PL.rank_of((uint64_t)((r & ~DUP_BIT) + 1) << 32, a.pdp);
+            }
+        if (l == 0)
+        {
+            a.gsz[0 * n_groups + g] = KU * w;
+            a.gsz[1 * n_groups + g] = U;
+            a.gsz[2 * n_groups + g] = KU + PU;
+        }
+    }
+}
+
+__global__ void k_union_emit(MergeArgs a)
+{
+    const uint64_t p = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / EMIT_LANES;
+    const uint32_t j8 = threadIdx.x % EMIT_LANES;
+    if (p >= a.n_parts) return;
+    const uint64_t n_groups = 3 * a.n_owned, G1 = n_groups + 1, P1 = a.n_parts + 1;
+    const int64_t h0 = a.hdr[4 * p];
+    const int m = (int)(h0 & 3);
+    const uint64_t g = (uint64_t)m * a.n_owned + (uint64_t)((h0 >> 2) - (int64_t)a.txn_base);
+    const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
+    const uint32_t nk = (uint32_t)a.hdr[4 * p + 1], ni = (uint32_t)a.hdr[4 * p + 2], no = (uint32_t)a.hdr[4 * p + 3];
+    const uint64_t kbase = a.poff[0 * P1 + p], ibase = a.poff[1 * P1 + p], obase = a.poff[2 * P1 + p];
+    const uint64_t KW = a.goff[0 * G1 + g], ID = a.goff[1 * G1 + g], KO = a.goff[2 * G1 + g];
+    const uint32_t KU = a.gsz[0 * n_groups + g] / w;
+    for (uint32_t i = j8; i < nk; i += EMIT_LANES)
+    {
+        const uint64_t s = kbase + (uint64_t)w * i;
+        const uint32_t r = a.kuk[s];
+        if (r & DUP_BIT) continue;
+        a.o_keys[KW + (uint64_t)w * r] = a.keys[s];
+        if (w == 2) a.o_keys[KW + 2 * (uint64_t)r + 1] = a.keys[s + 1];
+        a.o_k2t[KO + r] = (int32_t)a.khead[s];
+    }
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    for (uint32_t e = j8; e < ni; e += EMIT_LANES)
+    {
+        const uint32_t uu = a.u[ibase + e];
+        if (uu & DUP_BIT) continue;
+        reinterpret_cast<uint32_t*>(a.o_ids)[ID + uu] = ids[ibase + e];
+    }
+    for (uint32_t v = j8; v < no - nk; v += EMIT_LANES)
+    {
+        const uint32_t pp = a.ppos[obase + nk + v];
+        if (pp & DUP_BIT) continue;
+        const uint32_t idx = (uint32_t)a.k2t[obase + nk + v];
+        if (idx >= ni)
+        {
+            atomicOr(a.error, 8u);
+            continue;
+        }
+        a.o_k2t[KO + KU + pp] = (int32_t)(a.u[ibase + idx] & ~DUP_BIT);
+    }
+}
+
+hipError_t launch_union_rank(const MergeArgs& a, unsigned blocks, hipStream_t st)
+{
+    k_union_rank<<<blocks, 64 * XWAVES, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_union_emit(const MergeArgs& a, hipStream_t st)
+{
+    const uint64_t threads = a.n_parts * EMIT_LANES;
+    if (a.n_parts) k_union_emit<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(a);
+    return hipGetLastError();
+}
+
 // per map and owned request: offsets of the merged CSR (relative to the map's first group)
 __global__ void k_merge_out_offsets(MergeArgs a)
 {
@@ -770,6 +1119,19 @@ hipError_t run_merge_emit_rank(const MergeArgs& a, hipStream_t st)
     const uint64_t threads = a.n_parts * EMIT_LANES;
     if (a.n_parts) k_merge_emit_rank<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(a);
     return hipGetLastError();
+}
+
+hipError_t run_union_rank(const MergeArgs& a, hipStream_t st)
+{
+    if (!a.n_owned) return hipSuccess;
+    return launch_union_rank(a, merge_blocks(3 * a.n_owned), st);
+}
+
+hipError_t run_union_emit(const MergeArgs& a, hipStream_t st)
+{
+    const uint64_t n_off = 3 * (a.n_owned + 1);
+    k_merge_out_offsets<<<(unsigned)((n_off + 255) / 256), 256, 0, st>>>(a);
+    return launch_union_emit(a, st);
 }
 
 hipError_t run_merge_bases(const MergeArgs& a, uint64_t* out, hipStream_t st)

@@ -44,6 +44,9 @@ struct MergeArgs {
     uint32_t* ppre;                               // [2][n_parts] key words / pairs of earlier parts of its group
     uint64_t n_global;
     const uint64_t* g_msb; const uint64_t* g_lsb; const int32_t* g_node;   // the global dictionary
+    // ad_parts_union (keys of different sources may overlap): per received key word / k2t entry
+    uint32_t* kdp; uint32_t* kuk; uint32_t* khead;   // [n_key_words]: dup prefix, union key index | DUP_BIT, head
+    uint32_t* pdp; uint32_t* ppos;                   // [n_k2t]: pairs' dup prefix, body position | DUP_BIT
 };
 
 // global rank of each local dictionary id (binary search in the global dictionary)
@@ -63,5 +66,8 @@ hipError_t run_merge_bases(const MergeArgs& a, uint64_t* out, hipStream_t st);
 // AD_IDS_RANK merge: union ranks per group (wave per group), then thread-per-part emission
 hipError_t run_merge_rank(const MergeArgs& a, hipStream_t st);
 hipError_t run_merge_emit_rank(const MergeArgs& a, hipStream_t st);
+// ad_parts_union: general union (overlapping keys), rank-format ids
+hipError_t run_union_rank(const MergeArgs& a, hipStream_t st);
+hipError_t run_union_emit(const MergeArgs& a, hipStream_t st);
 
 }  // namespace adx

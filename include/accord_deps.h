@@ -328,6 +328,14 @@ typedef struct ad_merged {
 int ad_parts_merge(ad_ctx* ctx, const ad_parts* in_dev, uint32_t n_src, const uint64_t* src_parts,
                    uint64_t txn_base, uint64_t n_owned, void* stream, ad_merged* out);
 
+/* Deps.merge of replies whose key sets may overlap -- the coordinator's union of the PartialDeps
+ * its replicas return for one transaction (CoordinateTransaction.java:70-101,
+ * Deps.merge Deps.java:281-286, RelationMultiMap.linearUnion RelationMultiMap.java:561-816): as
+ * ad_parts_merge, but keys (ranges) of different sources may repeat and their TxnId sets are
+ * unioned. Parts must carry global ranks (AD_IDS_RANK). Sources in any order. */
+int ad_parts_union(ad_ctx* ctx, const ad_parts* in_dev, uint32_t n_src, const uint64_t* src_parts,
+                   uint64_t txn_base, uint64_t n_owned, void* stream, ad_merged* out);
+
 /* Copy device memory owned by the library (results) into a host buffer: for hosts without a
  * HIP binding of their own (the Panama FFM wrapper). */
 int ad_copy_to_host(ad_ctx* ctx, void* dst, const void* src_dev, uint64_t bytes);
