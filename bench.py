@@ -434,6 +434,99 @@ def bench_union(args, rank, world, local, dev):
         dist.destroy_process_group()
 
 
+def bench_recovery(args, rank, world, local, dev):
+    """SURVEY §8 f4 on config 2's snapshot: the BeginRecovery scan --recovery-scan (AD_RECOVER_*) for
+    a batch of recovering txns (half of them txnIds of the history, i.e. known to the
+    CommandsForKey, half new ones from the config-2 batch), entries carrying TxnInfo.missing()
+    lists. mapReduceFull scans every probed key's byId range (CommandsForKey.java:854), as the
+    reference does. With N GPUs, N independent replicas."""
+    s = args.scale
+    w = synth.config2(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_hist_entries=int(16_000_000 * s),
+                      seed=0xACC0D002 + rank)
+    w.cfk = synth.with_missing_fast(w.cfk, 0xACC0D00F)
+    n = max(2, int(args.recovery * s))
+    rng = np.random.default_rng(0xACC0D00F)
+    key_of = np.repeat(np.arange(len(w.cfk.keys)), np.diff(w.cfk.seg.astype(np.int64)))
+    e = rng.choice(w.cfk.n_entries, n // 2, replace=False)
+    from accord_deps.model import Queries, Tids
+    q = w.queries
+    nb = n - n // 2
+    txn = Tids.concat([w.cfk.txn.take(e), q.txn.take(np.arange(nb))])
+    keys = [w.cfk.keys[key_of[e]].reshape(-1, 1), q.keys[:int(q.key_off[nb])]]
+    off = np.concatenate([np.arange(n // 2 + 1, dtype=np.uint64), (n // 2 + q.key_off[1:nb + 1]).astype(np.uint64)])
+    rq = Queries(txn, txn, off, np.concatenate([k.reshape(-1) for k in keys]))
+    st = native.DeviceCommandStore(device=local)
+    st.load(w)
+    qdev, keep = native.device_queries(rq, dev)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    scan = args.recovery_scan
+    elapsed, all_stats = _timed_steps(args, world, dev, lambda: st.recovery_scan_device(qdev, scan, sp)[1])
+    stats = all_stats[-1]
+    probes = _sum_over_ranks(world, dev, rq.n_probes)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    ms_scan = float(np.mean([x["ms_stage"][0] for x in all_stats]))   # k_encode_recover .. k_build
+    # algorithmic bytes: compulsory read of every probed key's entries once (16 B each: ranks, status,
+    # missing offset) + their missing ids (4 B) + requests (24 B + 8 B per key) + the CSR output
+    touched = np.searchsorted(w.cfk.keys, np.unique(rq.keys))
+    ok = touched < len(w.cfk.keys)
+    touched = touched[ok][w.cfk.keys[touched[ok]] == np.unique(rq.keys)[ok]]
+    seg = w.cfk.seg.astype(np.int64)
+    ent = int((seg[touched + 1] - seg[touched]).sum())
+    mo = w.cfk.miss_off.astype(np.int64)
+    nmiss = int((mo[seg[touched + 1]] - mo[seg[touched]]).sum())
+    pk = np.searchsorted(w.cfk.keys, rq.keys)
+    hit = pk < len(w.cfk.keys)
+    hit[hit] &= w.cfk.keys[pk[hit]] == rq.keys[hit]
+    pk = pk[hit]
+    probe_seg = int((seg[pk + 1] - seg[pk]).sum())      # entries a whole-segment scan of every probe reads
+    heads = sum(stats["n_keys"])
+    out_bytes = 8 * heads + 4 * (heads + sum(stats["n_pairs"])) + 4 * sum(stats["n_unique"])
+    alg = 16 * ent + 4 * nmiss + 24 * n + 8 * rq.n_probes + out_bytes
+    achieved = alg / (ms_scan / 1000.0) / 1e9 if ms_scan > 0 else 0.0
+    names = ["AD_RECOVER_STARTED_BEFORE_ACCEPTED_NO_WITNESS", "AD_RECOVER_STARTED_BEFORE_STABLE_WITNESS",
+             "AD_RECOVER_STARTED_AFTER_ACCEPTED_NO_WITNESS", "AD_RECOVER_EXECUTES_AFTER_STABLE_NO_WITNESS"]
+    res = {
+        "metric": "BeginRecovery mapReduceFull scans: txn-key probes/sec", "value": probes / (ms_per_step / 1000.0),
+        "unit": "txn-key probes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "config2 snapshot (%d entries, missing() lists), %d recovering txns (half known), scan %s "
+                               "(SURVEY 8 f4)" % (w.cfk.n_entries, n, names[scan]),
+                   "txn_key_probes_per_step": probes, "parallelism": "replicas x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_scan_full (+ encode, probe, k_build)", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": alg, "launch_ms": ms_scan,
+                     "scan_bytes_per_launch": 16 * probe_seg},
+        "stages_ms": {"encode+probe+k_scan_full+k_build": round(ms_scan, 4),
+                      "offsets": round(float(np.mean([x["ms_stage"][4] for x in all_stats])), 4),
+                      "pack": round(float(np.mean([x["ms_stage"][5] for x in all_stats])), 4)},
+        "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        ost = pyoracle.OracleStore()
+        ost.load(w)
+        m, t, done = 16, 0.0, 0
+        while done < n and t < args.cpu_budget:
+            c = min(m, n - done)
+            t0 = time.perf_counter()
+            ost.recovery_batch(rq, scan, done, c)
+            t += time.perf_counter() - t0
+            done += c
+            m *= 2
+        ost.close()
+        pr = int(rq.key_off[done])
+        res["cpu_baseline"] = dict(value=pr / t, unit="txn-key probes/s", cores=1, kind="port",
+                                   sample="first %d of %d recovering txns (%d probes, %.1f s), rc_recovery_batch "
+                                          "(mapReduceFull restatement), 1 thread" % (done, n, pr, t))
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    st.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def bench_sequential(args, rank, world, local, dev):
     """Config 1: 10k txns x 4 keys over 1k keys, one CommandStore, SEQUENTIAL PreAccept (each txn
     inserted as PREACCEPTED before its deps). SEQUENTIAL runs through the host API: a step is one
@@ -495,6 +588,9 @@ def main():
                     help="with config 2: the coordinator's Deps.merge of R replica replies (SURVEY 8 f2)")
     ap.add_argument("--preaccept", action="store_true",
                     help="with config 2: the PreAccept timestamp proposal (SURVEY 8 f3) instead of deps")
+    ap.add_argument("--recovery", type=int, default=0, metavar="N",
+                    help="with config 2: BeginRecovery scans for N recovering txns on the config-2 snapshot (SURVEY 8 f4)")
+    ap.add_argument("--recovery-scan", type=int, default=3, choices=(0, 1, 2, 3), help="AD_RECOVER_* scan of --recovery")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank: the measured configuration); gloo: rehearsal of the "
                          "N>1 path on fewer GPUs (ranks share GPUs, the exchange is staged through host memory)")
@@ -527,6 +623,8 @@ def main():
         return bench_preaccept(args, rank, world, local, dev)
     if args.union:
         return bench_union(args, rank, world, local, dev)
+    if args.recovery:
+        return bench_recovery(args, rank, world, local, dev)
 
     s = args.scale
     t0 = time.time()

@@ -55,6 +55,18 @@ class AdCfkSoa(C.Structure):
                 ("status", P), ("pruned_before", P)]
 
 
+class AdCfkMissingSoa(C.Structure):
+    _fields_ = [("n_entries", C.c_uint64), ("off", P), ("msb", P), ("lsb", P), ("node", P)]
+
+
+# recovery scans (accord_deps.h ad_recovery_batch; BeginRecovery.java:329-380)
+AD_RECOVER_STARTED_BEFORE_ACCEPTED_NO_WITNESS = 0
+AD_RECOVER_STARTED_BEFORE_STABLE_WITNESS = 1
+AD_RECOVER_STARTED_AFTER_ACCEPTED_NO_WITNESS = 2
+AD_RECOVER_EXECUTES_AFTER_STABLE_NO_WITNESS = 3
+RECOVER_SCANS = (0, 1, 2, 3)
+
+
 class AdRangeCmdsSoa(C.Structure):
     _fields_ = [("n_cmds", C.c_uint64), ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
                 ("erased", P), ("historical", P), ("range_off", P), ("range_start", P), ("range_end", P)]

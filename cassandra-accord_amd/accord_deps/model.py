@@ -88,9 +88,14 @@ class CfkSnapshot:
     exec: Tids
     status: np.ndarray        # u8
     pruned_before: Optional[np.ndarray] = None   # i64 [n_keys], -1 = none
+    # TxnInfo.missing() (CommandsForKey.java:332-341): ids of entry e are miss[miss_off[e]:miss_off[e+1]]
+    miss_off: Optional[np.ndarray] = None        # u64 [n_entries+1]; None = every entry NO_TXNIDS
+    miss: Optional[Tids] = None
 
     def __post_init__(self):
         self.keys = A.as_i64(self.keys)
+        if self.miss_off is not None:
+            self.miss_off = A.as_u64(self.miss_off)
         self.seg = A.as_u64(self.seg)
         self.status = A.as_u8(self.status)
         if self.pruned_before is not None:
@@ -110,6 +115,16 @@ class CfkSnapshot:
         s.exec_msb, s.exec_lsb, s.exec_node = A.ptr(self.exec.msb), A.ptr(self.exec.lsb), A.ptr(self.exec.node)
         s.status = A.ptr(self.status)
         s.pruned_before = A.ptr(self.pruned_before)
+        return s
+
+    def missing_soa(self):
+        """AdCfkMissingSoa of the missing lists, or None when there are none."""
+        if self.miss_off is None:
+            return None
+        s = A.AdCfkMissingSoa()
+        s.n_entries = len(self.status)
+        s.off = A.ptr(self.miss_off)
+        s.msb, s.lsb, s.node = A.ptr(self.miss.msb), A.ptr(self.miss.lsb), A.ptr(self.miss.node)
         return s
 
     @staticmethod

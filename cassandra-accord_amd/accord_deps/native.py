@@ -22,7 +22,8 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
            "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict", "ad_preaccept_maps_load",
-           "ad_preaccept_device", "ad_parts_union")
+           "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_recovery_batch",
+           "ad_recovery_batch_device")
 
 
 class AccordDepsError(RuntimeError):
@@ -77,6 +78,11 @@ def lib():
         L.ad_levels.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.POINTER(A.AdStats)]
         L.ad_levels_device.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.c_void_p,
                                        C.POINTER(A.AdStats)]
+        L.ad_cfk_missing_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkMissingSoa)]
+        L.ad_recovery_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32,
+                                        C.POINTER(C.POINTER(A.AdDepsResult))]
+        L.ad_recovery_batch_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_void_p,
+                                               C.POINTER(A.AdDepsResult)]
         _lib = L
     return _lib
 
@@ -136,6 +142,9 @@ class DeviceCommandStore:
         self._check(L.ad_cfk_load(self.h, C.byref(workload.cfk.soa())))
         self._check(L.ad_range_cmds_load(self.h, C.byref(workload.cmds.soa())))
         self._check(L.ad_redundant_load(self.h, C.byref(workload.redundant.soa())))
+        ms = workload.cfk.missing_soa()
+        if ms is not None:
+            self._check(L.ad_cfk_missing_load(self.h, C.byref(ms)))
         if prepare:
             self._check(L.ad_prepare(self.h))
         return self
@@ -197,6 +206,23 @@ class DeviceCommandStore:
         L = lib()
         out = C.POINTER(A.AdDepsResult)()
         self._check(L.ad_deps_batch(self.h, C.byref(queries.soa()), flags, C.byref(out)))
+        return self._host_result(out)
+
+    def recovery_scan(self, queries, scan):
+        """Batched BeginRecovery scan `scan` (A.AD_RECOVER_*; ad_recovery_batch): host arrays in,
+        materialised Deps out (keyDeps / directKeyDeps of the visited (key, txnId) pairs)."""
+        out = C.POINTER(A.AdDepsResult)()
+        self._check(lib().ad_recovery_batch(self.h, C.byref(queries.soa()), scan, C.byref(out)))
+        return self._host_result(out)
+
+    def recovery_scan_device(self, qdev, scan, stream=None):
+        """Device-resident recovery scan (ad_recovery_batch_device): (AdDepsResult of device pointers, stats)."""
+        out = A.AdDepsResult()
+        self._check(lib().ad_recovery_batch_device(self.h, C.byref(qdev), scan, stream, C.byref(out)))
+        return out, stats_dict(out.stats)
+
+    def _host_result(self, out):
+        L = lib()
         try:
             r = out.contents
             n = r.n_txns
@@ -348,6 +374,16 @@ def resolve(workload, device=0, elide=1, path=0):
     try:
         st.load(workload)
         return st.calculate_partial_deps(workload.queries, workload.flags)
+    finally:
+        st.close()
+
+
+def recover(workload, scan, device=0):
+    """One BeginRecovery scan over every request of the workload (fresh store)."""
+    st = DeviceCommandStore(device, workload.range_start_inclusive, 1, workload.slices)
+    try:
+        st.load(workload)
+        return st.recovery_scan(workload.queries, scan)
     finally:
         st.close()
 

@@ -639,3 +639,95 @@ def max_conflicts_from_cfk(cfk):
     v = Tids(np.where(hit, cfk.exec.msb[e], z), np.where(hit, cfk.exec.lsb[e], z),
              np.where(hit, cfk.exec.node[e], 0).astype(np.int32))
     return RangeMap(starts, v, hit.astype(np.uint8), 1)
+
+
+def _order(t):
+    """Timestamp.compareTo sort keys (Timestamp.java:208-217) of a Tids, for np.lexsort."""
+    return (t.node.astype(np.int64), (t.lsb & np.uint64(0x1E)), (t.lsb >> np.uint64(16)), t.msb)
+
+
+def with_missing(cfk, seed, frac=0.5, max_missing=3, extra=None):
+    """A copy of `cfk` whose entries with deps (ACCEPTED..APPLIED) carry TxnInfo.missing() lists
+    (CommandsForKey.java:332-341) with probability `frac`: 1..max_missing ids drawn from the same key's
+    byId (and from `extra` ids, e.g. txnIds unknown to the store), ascending and duplicate-free."""
+    rng = np.random.default_rng(seed)
+    ne = cfk.n_entries
+    off = np.zeros(ne + 1, np.uint64)
+    pick = []
+    has_deps = (cfk.status >= A.ST_ACCEPTED) & (cfk.status <= A.ST_APPLIED)
+    for k in range(len(cfk.keys)):
+        s0, s1 = int(cfk.seg[k]), int(cfk.seg[k + 1])
+        for e in range(s0, s1):
+            ids = []
+            if has_deps[e] and rng.random() < frac:
+                n = int(rng.integers(1, max_missing + 1))
+                ids = [("e", int(i)) for i in rng.choice(np.arange(s0, s1), min(n, s1 - s0), replace=False)]
+                if extra is not None and len(extra) and rng.random() < 0.3:
+                    ids.append(("x", int(rng.integers(0, len(extra)))))
+            pick.append(ids)
+    cols = []
+    for e, ids in enumerate(pick):
+        t = Tids.concat([cfk.txn.take(np.array([i for s, i in ids if s == "e"], np.int64)),
+                         (extra.take(np.array([i for s, i in ids if s == "x"], np.int64)) if extra is not None
+                          else cfk.txn.take(np.zeros(0, np.int64)))])
+        o = np.lexsort(_order(t)) if len(t) else np.zeros(0, np.int64)
+        t = t.take(o)
+        keep = np.ones(len(t), bool)          # duplicate-free under Timestamp.equals
+        for j in range(1, len(t)):
+            keep[j] = not (t.msb[j] == t.msb[j - 1] and ((t.lsb[j] ^ t.lsb[j - 1]) & np.uint64(0xFFFFFFFFFFFF001E)) == 0
+                           and t.node[j] == t.node[j - 1])
+        cols.append(t.take(np.nonzero(keep)[0]))
+        off[e + 1] = off[e] + int(keep.sum())
+    miss = Tids.concat(cols) if cols else cfk.txn.take(np.zeros(0, np.int64))
+    return CfkSnapshot(cfk.keys, cfk.seg, cfk.txn, cfk.exec, cfk.status, cfk.pruned_before, off, miss)
+
+
+def recovery_workload(seed, n_known=40, **kw):
+    """BeginRecovery scans on a random_small store without range commands: its
+    requests (a quarter of them already in the CommandsForKey) plus `n_known` requests recovering a
+    txnId of the history over (a superset of) its keys; entries carry missing() lists."""
+    kw.setdefault("n_range_cmds", 0)
+    w = random_small(seed, **kw)
+    rng = np.random.default_rng(seed ^ 0x5EC0)
+    cfk = w.cfk
+    e_key = np.repeat(np.arange(len(cfk.keys)), np.diff(cfk.seg.astype(np.int64)))
+    qs_t, qs_k = [], []
+    if cfk.n_entries:
+        for e in rng.choice(cfk.n_entries, min(n_known, cfk.n_entries), replace=False):
+            t = cfk.txn.take(np.array([e]))
+            same = np.nonzero((cfk.txn.msb == t.msb[0]) & (cfk.txn.lsb == t.lsb[0]) & (cfk.txn.node == t.node[0]))[0]
+            ks = set(int(cfk.keys[e_key[i]]) for i in same)
+            ks |= set(int(x) for x in rng.choice(cfk.keys, min(2, len(cfk.keys)), replace=False))
+            qs_t.append(t)
+            qs_k.append(np.array(sorted(ks), np.int64))
+    q = w.queries
+    txn = Tids.concat([q.txn] + qs_t)
+    keys = [q.keys[int(q.key_off[i]):int(q.key_off[i + 1])] for i in range(len(q))] + qs_k
+    key_off = np.zeros(len(keys) + 1, np.uint64)
+    key_off[1:] = np.cumsum([len(k) for k in keys])
+    w.queries = Queries(txn, txn, key_off, np.concatenate(keys + [np.zeros(0, np.int64)]))
+    # stretch some proposed/committed executeAts far past their txnIds (Accept-style), so that earlier
+    # txns executing after the recovering one (the STARTED_BEFORE scans) are common
+    stretch = ((cfk.status >= A.ST_ACCEPTED) & (cfk.status <= A.ST_APPLIED) & (cfk.exec.node >= EXEC_NODE_BASE)
+               & (rng.random(cfk.n_entries) < 0.5))
+    bump = (rng.integers(0, 600, cfk.n_entries).astype(np.uint64) << np.uint64(16)) * stretch.astype(np.uint64)
+    cfk = CfkSnapshot(cfk.keys, cfk.seg, cfk.txn, Tids(cfk.exec.msb, cfk.exec.lsb + bump, cfk.exec.node), cfk.status,
+                      cfk.pruned_before)
+    w.cfk = with_missing(cfk, seed, extra=q.txn)
+    w.name = "recovery_small"
+    return w
+
+
+def with_missing_fast(cfk, seed, frac=0.2, back=8):
+    """Vectorised with_missing for large snapshots: a chosen entry with deps gets one missing id,
+    the txnId of an entry up to `back` positions before it in the same key's byId."""
+    rng = np.random.default_rng(seed)
+    ne = cfk.n_entries
+    key_lo = np.repeat(cfk.seg[:-1].astype(np.int64), np.diff(cfk.seg.astype(np.int64)))
+    has_deps = (cfk.status >= A.ST_ACCEPTED) & (cfk.status <= A.ST_APPLIED)
+    pick = has_deps & (rng.random(ne) < frac)
+    src = np.maximum(np.arange(ne) - rng.integers(1, back + 1, ne), key_lo)
+    off = np.zeros(ne + 1, np.uint64)
+    off[1:] = np.cumsum(pick)
+    return CfkSnapshot(cfk.keys, cfk.seg, cfk.txn, cfk.exec, cfk.status, cfk.pruned_before, off,
+                       cfk.txn.take(src[pick]))

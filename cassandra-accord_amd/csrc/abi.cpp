@@ -162,6 +162,9 @@ struct ad_ctx {
         std::vector<Tid> txn, exec;
         std::vector<uint8_t> status;
         std::vector<int64_t> pruned;           // per key; -1 none
+        std::vector<uint64_t> miss_off;        // TxnInfo.missing() per entry (ad_cfk_missing_load); empty = none
+        std::vector<Tid> miss;
+        bool miss_stale = false;               // SEQUENTIAL insertions moved the entries after the load
         bool loaded = false;
     } cfk;
     struct {
@@ -225,6 +228,10 @@ struct ad_ctx {
     uint64_t pa_gen = 0, snap_gen = 0;         // map loads / snapshot builds
     uint64_t pa_iv_gen[2] = {~0ull, ~0ull};    // (pa_gen, snap_gen) the per-key values were built for
     DevBuf pa_key_val;
+    // recovery scans (ad_recovery_batch*): entry ranks kept from the last snapshot build, device view
+    std::vector<uint32_t> h_txn_rank, h_exec_rank, h_pruned;
+    uint64_t rv_gen = ~0ull;                   // snap_gen the device view was built for
+    DevBuf rv_ent, rv_seg, rv_pruned, rv_miss;
     // global dictionary of the multi-store exchange (ad_set_global_dict)
     DevBuf g_msb, g_lsb, g_node, g_map, g_err;
     uint64_t n_global = 0;
@@ -731,6 +738,9 @@ static int build_snapshot(ad_ctx* c)
     HIPCHK(c, build_cfk_trees(s, c->stream));
     HIPCHK(c, build_range_trees(s, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->h_txn_rank.swap(txn_rank);
+    c->h_exec_rank.swap(exec_rank);
+    c->h_pruned.swap(pruned);
     c->dirty = false;
     ++c->snap_gen;
     c->global_ok = false;        // the dictionary changed: a global dictionary must be installed again
@@ -770,6 +780,7 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
         }
     }
     if (ins.empty()) return 0;
+    if (!K.miss_off.empty()) K.miss_stale = true;
     std::stable_sort(ins.begin(), ins.end(), [](const Ins& a, const Ins& b) {
         if (a.key != b.key) return a.key < b.key;
         return norm_cmp(a.n, b.n) < 0;
@@ -880,7 +891,7 @@ static uint32_t lean_rpw1(uint64_t n, uint64_t np)
 }
 
 static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false,
-                        bool n_keys_given = false)
+                        bool n_keys_given = false, int recovery_scan = -1, const RecoveryView* rv = nullptr)
 {
     const uint64_t n = q->n_txns;
     uint64_t np = 0;
@@ -891,7 +902,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipMemcpyAsync(&np, q->key_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
     }
-    const bool split_only = c->cfg.path == 1;
+    const bool split_only = c->cfg.path == 1 || recovery_scan >= 0;
     // the lean kernel covers stores without redundant-before entries, elision on
     // (range commands only with their stabbing index)
     const bool lean = !split_only && np > 0 && (c->ds.n_rent == 0 || c->ds.cell_off != nullptr) && c->ds.n_rb == 0 &&
@@ -948,7 +959,12 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipEventRecord(c->ev[0], st));
         uint64_t nd = 0;
         int rc;
-        if (split_only)
+        if (recovery_scan >= 0)
+        {
+            HIPCHK(c, run_recovery(c->ds, *rv, b, (uint32_t)recovery_scan, st));
+            HIPCHK(c, hipEventRecord(c->ev[1], st));
+        }
+        else if (split_only)
         {
             if ((rc = run_split(c, b, st))) return rc;
             HIPCHK(c, hipEventRecord(c->ev[1], st));
@@ -1039,7 +1055,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         {
             if (h.error == ERR_STATE)
                 return c->fail(AD_E_STATE, "reference would throw: prunedBefore set but no applied Write (CommandsForKey.java:962)");
-            return c->fail(AD_E_INVAL, "invalid Txn.Kind for witnesses() in a request (Txn.java:221-235)");
+            return c->fail(AD_E_INVAL, recovery_scan >= 0 ? "invalid Txn.Kind for witnessedBy() in a request (Txn.java:247-262)"
+                                                          : "invalid Txn.Kind for witnesses() in a request (Txn.java:221-235)");
         }
         if (h.overflow)
         {
@@ -1150,6 +1167,26 @@ static T* d2h(const T* src, uint64_t n)
     return p;
 }
 
+static int result_to_host(ad_ctx* c, uint64_t n, const ad_deps_result& dev, ad_deps_result** out)
+{
+    ad_deps_result* r = (ad_deps_result*)calloc(1, sizeof(ad_deps_result));
+    if (!r) return c->fail(AD_E_NOMEM, "result");
+    r->n_txns = n;
+    r->stats = dev.stats;
+    for (int m = 0; m < 3; ++m)
+    {
+        r->keys_off[m] = d2h(dev.keys_off[m], n + 1);
+        r->txn_off[m] = d2h(dev.txn_off[m], n + 1);
+        r->k2t_off[m] = d2h(dev.k2t_off[m], n + 1);
+        const uint64_t nk = r->keys_off[m][n], nt = r->txn_off[m][n], no = r->k2t_off[m][n];
+        r->keys[m] = d2h(dev.keys[m], nk);
+        r->txns[m] = d2h(dev.txns[m], nt);
+        r->k2t[m] = d2h(dev.k2t[m], no);
+    }
+    *out = r;
+    return AD_OK;
+}
+
 static int check_query_host(ad_ctx* c, const ad_query_soa* q)
 {
     for (uint64_t i = 0; i < q->n_txns; ++i)
@@ -1243,6 +1280,9 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     K.status.assign(in->status, in->status + ne);
     K.pruned.clear();
     if (in->pruned_before) K.pruned.assign(in->pruned_before, in->pruned_before + nk);
+    K.miss_off.clear();
+    K.miss.clear();
+    K.miss_stale = false;
     K.loaded = true;
     c->dirty = true;
     return AD_OK;
@@ -1321,22 +1361,7 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
     if (rc) return rc;
     ad_deps_result dev{};
     if ((rc = run_pipeline(c, &d, c->stream, &dev))) return rc;
-    ad_deps_result* r = (ad_deps_result*)calloc(1, sizeof(ad_deps_result));
-    if (!r) return c->fail(AD_E_NOMEM, "result");
-    r->n_txns = n;
-    r->stats = dev.stats;
-    for (int m = 0; m < 3; ++m)
-    {
-        r->keys_off[m] = d2h(dev.keys_off[m], n + 1);
-        r->txn_off[m] = d2h(dev.txn_off[m], n + 1);
-        r->k2t_off[m] = d2h(dev.k2t_off[m], n + 1);
-        const uint64_t nk = r->keys_off[m][n], nt = r->txn_off[m][n], no = r->k2t_off[m][n];
-        r->keys[m] = d2h(dev.keys[m], nk);
-        r->txns[m] = d2h(dev.txns[m], nt);
-        r->k2t[m] = d2h(dev.k2t[m], no);
-    }
-    *out = r;
-    return AD_OK;
+    return result_to_host(c, n, dev, out);
 }
 
 int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void* stream, ad_deps_result* out)
@@ -1349,6 +1374,127 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return run_pipeline(c, q, st, out, (flags & AD_PARTS_ONLY) != 0, (flags & AD_N_KEYS) != 0);
+}
+
+// device view of the snapshot for mapReduceFull: entries in load order with executeAt ranks,
+// status, kind and their TxnInfo.missing() lists as ranks (built once per snapshot / missing load)
+static int build_recovery_view(ad_ctx* c, RecoveryView* v)
+{
+    auto& K = c->cfk;
+    for (size_t i = 0; i < c->cmds.txn.size(); ++i)
+        if (c->cmds.erased.empty() || !c->cmds.erased[i])
+            return c->fail(AD_E_STATE, "recovery scans of range commands need their deps (InMemoryCommandStore.java:931-949)");
+    if (K.miss_stale) return c->fail(AD_E_STATE, "missing lists predate SEQUENTIAL insertions: load them again");
+    const uint64_t ne = K.status.size(), nk = K.keys.size();
+    if (c->rv_gen != c->snap_gen)
+    {
+        std::vector<uint4> ent(ne);
+        std::vector<uint32_t> seg(nk + 1), miss;
+        for (uint64_t k = 0; k <= nk; ++k) seg[k] = (uint32_t)K.seg[k];
+        // rank of an id: member i of the dictionary -> 2i+1, else 2 * lower bound (as encode_rank)
+        auto rank_of = [&](const Tid& t) -> uint32_t {
+            const NormTid x = norm(t);
+            uint64_t lo = 0, hi = c->dict_msb.size();
+            while (lo < hi)
+            {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (norm_cmp(norm_tid(c->dict_msb[mid], c->dict_lsb[mid], c->dict_node[mid]), x) < 0) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < c->dict_msb.size() && norm_cmp(norm_tid(c->dict_msb[lo], c->dict_lsb[lo], c->dict_node[lo]), x) == 0)
+                return (uint32_t)(2 * lo + 1);
+            return (uint32_t)(2 * lo);
+        };
+        for (uint64_t e = 0; e < ne; ++e)
+        {
+            const uint32_t kind = (uint32_t)((K.txn[e].lsb >> 1) & 7);
+            uint32_t nm = 0, mo = (uint32_t)miss.size();
+            if (!K.miss_off.empty())
+            {
+                const uint64_t a = K.miss_off[e], b = K.miss_off[e + 1];
+                if (b - a > RV_MAX_MISS) return c->fail(AD_E_CAPACITY, "more than %u missing ids on one entry", RV_MAX_MISS);
+                for (uint64_t j = a; j < b; ++j) miss.push_back(rank_of(K.miss[j]));
+                nm = (uint32_t)(b - a);
+            }
+            ent[e] = make_uint4(c->h_txn_rank[e], c->h_exec_rank[e], K.status[e] | (kind << 8) | (nm << RV_MISS_SHIFT), mo);
+        }
+        int rc;
+        if ((rc = upload(c, c->rv_ent, ent)) || (rc = upload(c, c->rv_seg, seg)) || (rc = upload(c, c->rv_pruned, c->h_pruned)) ||
+            (rc = upload(c, c->rv_miss, miss)))
+            return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->rv_gen = c->snap_gen;
+    }
+    v->ent = c->rv_ent.as<uint4>();
+    v->seg = c->rv_seg.as<uint32_t>();
+    v->pruned = c->rv_pruned.as<uint32_t>();
+    v->miss = c->rv_miss.as<uint32_t>();
+    return 0;
+}
+
+int ad_cfk_missing_load(ad_ctx* c, const ad_cfk_missing_soa* m)
+{
+    if (!c || !m) return AD_E_INVAL;
+    auto& K = c->cfk;
+    if (!K.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    const uint64_t ne = K.status.size();
+    if (m->n_entries != ne) return c->fail(AD_E_INVAL, "missing lists for %llu entries, snapshot has %llu",
+                                           (unsigned long long)m->n_entries, (unsigned long long)ne);
+    for (uint64_t e = 0; e < ne; ++e)
+    {
+        const uint64_t a = m->off[e], b = m->off[e + 1];
+        if (b < a) return c->fail(AD_E_INVAL, "missing offsets not monotone");
+        if (b > a && !(K.status[e] >= AD_ST_ACCEPTED && K.status[e] <= AD_ST_APPLIED))
+            return c->fail(AD_E_INVAL, "missing ids on an entry without deps (CommandsForKey.java:278)");
+        for (uint64_t j = a + 1; j < b; ++j)
+        {
+            const NormTid x = norm_tid(m->msb[j - 1], m->lsb[j - 1], m->node[j - 1]), y = norm_tid(m->msb[j], m->lsb[j], m->node[j]);
+            if (norm_cmp(x, y) >= 0) return c->fail(AD_E_INVAL, "missing ids not strictly ascending");
+        }
+    }
+    K.miss_off.assign(m->off, m->off + ne + 1);
+    const uint64_t nm = m->off[ne];
+    K.miss.resize(nm);
+    for (uint64_t j = 0; j < nm; ++j) K.miss[j] = {m->msb[j], m->lsb[j], m->node[j]};
+    K.miss_stale = false;
+    c->rv_gen = ~0ull;
+    return AD_OK;
+}
+
+int ad_recovery_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t scan, void* stream, ad_deps_result* out)
+{
+    if (!c || !q || !out) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (scan > AD_RECOVER_EXECUTES_AFTER_STABLE_NO_WITNESS) return c->fail(AD_E_INVAL, "unknown recovery scan %u", scan);
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    int rc;
+    if (c->dirty && (rc = build_snapshot(c))) return rc;
+    RecoveryView v{};
+    if ((rc = build_recovery_view(c, &v))) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return run_pipeline(c, q, st, out, false, false, (int)scan, &v);
+}
+
+int ad_recovery_batch(ad_ctx* c, const ad_query_soa* q, uint32_t scan, ad_deps_result** out)
+{
+    if (!c || !q || !out) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    int rc = check_query_host(c, q);
+    if (rc) return rc;
+    const uint64_t n = q->n_txns;
+    const uint64_t np = n ? q->key_off[n] : 0;
+    ad_query_soa d{};
+    d.n_txns = n;
+    d.txn_msb = stage_q(c, c->q_tm, q->txn_msb, n, &rc);
+    d.txn_lsb = stage_q(c, c->q_tl, q->txn_lsb, n, &rc);
+    d.txn_node = stage_q(c, c->q_tn, q->txn_node, n, &rc);
+    d.key_off = stage_q(c, c->q_ko, q->key_off, n + 1, &rc);
+    d.keys = stage_q(c, c->q_k, q->keys, np, &rc);
+    if (rc) return rc;
+    ad_deps_result dev{};
+    if ((rc = ad_recovery_batch_device(c, &d, scan, c->stream, &dev))) return rc;
+    return result_to_host(c, n, dev, out);
 }
 
 void ad_result_free(ad_deps_result* r)

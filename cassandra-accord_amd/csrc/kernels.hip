@@ -1104,4 +1104,157 @@ int device_cu_count()
     return cus;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Recovery scans: CommandsForKey.mapReduceFull (CommandsForKey.java:809-908) for
+// the four BeginRecovery queries (BeginRecovery.java:329-380), one wave per (request, key) probe,
+// emitting into the K1 arena in the k_scan layout so that k_build assembles the Deps.
+// ---------------------------------------------------------------------------------------
+// Txn.Kind.witnessedBy() (Txn.java:247-262) as a kinds mask; 0xFFFF for an AssertionError
+__device__ __forceinline__ uint32_t kind_witnessed_by(uint32_t kind)
+{
+    switch (kind)
+    {
+        case 2: return 0u;                                            // EphemeralRead: Nothing
+        case 0: return (1u << 1) | (1u << 3) | (1u << 4);             // Read: WsOrSyncPoints
+        case 1: return KINDS_ANY_GLOBALLY_VISIBLE;                    // Write
+        case 3: case 4: return 1u << 4;                               // (Exclusive)SyncPoint: ExclusiveSyncPoints
+        default: return 0xFFFFu;
+    }
+}
+
+__global__ void k_encode_recover(DevSnapshot s, BatchBufs b)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n_txns) return;
+    const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t];
+    const int32_t tn = b.q_txn_node[t];
+    uint32_t kinds = kind_witnessed_by((uint32_t)((tl >> 1) & 7));   // testKind = txnId.kind().witnessedBy()
+    if (kinds == 0xFFFFu) { set_error(b.ctl, ERR_INVAL); kinds = 0; }
+    b.t_S[t] = encode_rank(s, tm, tl, tn);                            // testTxnId
+    b.t_self[t] = 0;
+    b.t_kinds[t] = kinds;
+    b.t_epoch[t] = 0;
+    for (uint64_t p = b.q_key_off[t]; p < b.q_key_off[t + 1]; ++p) b.p_txn[p] = (uint32_t)t;
+}
+
+// scan: AD_RECOVER_* = (TestStartedAt, TestDep, TestStatus) of BeginRecovery.java:334,348,365,378:
+//   0 STARTED_BEFORE WITHOUT IS_PROPOSED, 1 STARTED_BEFORE WITH IS_STABLE,
+//   2 STARTED_AFTER WITHOUT IS_PROPOSED,  3 ANY WITHOUT IS_STABLE
+__global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, uint32_t scan)
+{
+    const int wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
+    const uint64_t nw = (uint64_t)gridDim.x * K1_WAVES;
+    ChunkAlloc alloc;
+    const unsigned long long cap = b.ctl->key_cap;
+    const bool with = scan == 1;
+    const bool proposed = scan == 0 || scan == 2;
+
+    for (uint64_t p = (uint64_t)blockIdx.x * K1_WAVES + wv; p < b.n_probes; p += nw)
+    {
+        const uint4 pr = b.p_rec[p];
+        const uint32_t ki = pr.x;
+        const uint32_t T = pr.y, kinds = pr.w & 0xFF;
+        uint64_t start = 0, end = 0;
+        bool known = false;
+        if (ki != NO_KEY && kinds != 0)
+        {
+            const uint64_t lo = v.seg[ki], hi = v.seg[ki + 1];
+            // insertPos = Arrays.binarySearch(byId, testTxnId) (:821-825)
+            const uint64_t pos = wave_lower_bound(lo, hi, [&](uint64_t i) { return v.ent[i].x; },
+                                                  [&](uint32_t r) { return r < T; });
+            known = pos < hi && v.ent[pos].x == T;
+            // unknown + WITH: nothing unless testTxnId < prunedBefore (:832-836; NONE = rank 0)
+            const bool skip = !known && with && !(T < v.pruned[ki]);
+            if (!skip)
+            {
+                if (scan == 2) { start = pos; end = hi; }            // STARTED_AFTER
+                else if (scan == 3) { start = lo; end = hi; }       // ANY
+                else { start = lo; end = pos; }                     // STARTED_BEFORE
+            }
+        }
+        // the loop body of :854-906 for entry i
+        auto want_of = [&](uint64_t i, bool& is1, uint32_t& r) -> bool {
+            if (i >= end) return false;
+            const uint4 e = v.ent[i];
+            r = e.x;
+            const uint32_t st = e.z & 0xFF, kd = (e.z >> 8) & 7;
+            is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;                 // Deps.AbstractBuilder.add routing
+            if (!((kinds >> kd) & 1)) return false;                  // testKind.test(txn.kind())
+            if (proposed ? !(st == 3u || st == 4u)   // ACCEPTED, COMMITTED
+                         : !(st == 5u || st == 6u)) return false;   // STABLE, APPLIED
+            // testDep != ANY_DEPS: hasExecuteAtOrDeps (implied by the status sets), executeAt > testTxnId
+            if (e.y <= T) return false;
+            bool has_as_dep = false;
+            if (known)
+            {
+                const uint32_t nm = e.z >> RV_MISS_SHIFT;
+                uint32_t a = e.w, c = e.w + nm;                       // Arrays.binarySearch(missing, testTxnId)
+                while (a < c)
+                {
+                    const uint32_t m = (a + c) >> 1;
+                    if (v.miss[m] < T) a = m + 1;
+                    else c = m;
+                }
+                has_as_dep = !(a < e.w + nm && v.miss[a] == T);
+            }
+            return has_as_dep == with;
+        };
+        uint32_t c0 = 0, c1 = 0;
+        for (uint64_t base = start; base < end; base += 64)
+        {
+            bool is1 = false;
+            uint32_t r = 0;
+            const bool want = want_of(base + lane, is1, r);
+            c0 += __popcll(ballot(want && !is1));
+            c1 += __popcll(ballot(want && is1));
+        }
+        const uint32_t tot = c0 + c1;
+        const uint64_t off = tot ? alloc.take(&b.ctl->key_top, cap, &b.ctl->overflow, 1u, tot, K1_CHUNK) : 0;
+        const bool fits = off + tot <= cap;
+        if (fits && tot)
+        {
+            uint32_t run0 = 0, run1 = 0;
+            for (uint64_t base = start; base < end; base += 64)
+            {
+                bool is1 = false;
+                uint32_t r = 0;
+                const bool want = want_of(base + lane, is1, r);
+                const uint64_t w0 = ballot(want && !is1), w1 = ballot(want && is1);
+                if (want && !is1) b.arena[off + run0 + mbcnt(w0)] = r;       // keyDeps, byId (= rank) order
+                if (want && is1) b.arena[off + c0 + run1 + mbcnt(w1)] = r;   // directKeyDeps
+                run0 += __popcll(w0);
+                run1 += __popcll(w1);
+            }
+        }
+        if (lane == 0)
+        {
+            b.p_off[p] = fits ? (uint32_t)off : 0u;
+            b.p_c0[p] = fits ? c0 : 0u;
+            b.p_c1[p] = fits ? c1 : 0u;
+        }
+    }
+}
+
+hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const BatchBufs& b, uint32_t scan, hipStream_t st)
+{
+    if (b.n_txns)
+        k_encode_recover<<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
+    if (b.n_probes)
+    {
+        k_probe_keys<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b);
+        const uint64_t blocks_needed = (b.n_probes + K1_WAVES - 1) / K1_WAVES;
+        const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
+        k_scan_full<<<grid, 256, 0, st>>>(v, b, scan);
+        // recovery scans of key-domain stores collect no range pairs (empty K4 lists)
+        hipError_t e = hipMemsetAsync(b.p_rcnt, 0, sizeof(uint32_t) * b.n_probes, st);
+        if (e == hipSuccess) e = hipMemsetAsync(b.p_rb, 0xFF, sizeof(uint64_t) * b.n_probes, st);
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return run_build(s, b, st);
+}
+
 }  // namespace adx

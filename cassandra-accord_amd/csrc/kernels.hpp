@@ -61,6 +61,16 @@ struct BatchBufs {
     BatchCtl* ctl;
 };
 
+// recovery scans: the CommandsForKey entries in load order, for mapReduceFull
+struct RecoveryView {
+    const uint4* ent;        // per entry {txnId rank, executeAt rank, status | kind << 8 | n_missing << 12, missing off}
+    const uint32_t* seg;     // [n_keys + 1] entry range of each key index
+    const uint32_t* pruned;  // [n_keys] prunedBefore rank, 0 = none
+    const uint32_t* miss;    // TxnInfo.missing() as ranks, ascending per entry
+};
+constexpr uint32_t RV_MISS_SHIFT = 12;
+constexpr uint32_t RV_MAX_MISS = (1u << 20) - 1;
+
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
 hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);
 
@@ -68,6 +78,7 @@ hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_scan(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const BatchBufs& b, uint32_t scan, hipStream_t st);
 hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st);
 hipError_t run_pack(const BatchBufs& b, hipStream_t st);

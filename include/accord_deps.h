@@ -401,6 +401,46 @@ int ad_preaccept_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t permit_
                         void* stream, uint64_t* out_msb, uint64_t* out_lsb, int32_t* out_node, uint8_t* out_flags,
                         ad_stats* stats);
 
+/* ---- recovery scans ---------------------------------------------------------
+ * The four CommandsForKey.mapReduceFull scans BeginRecovery runs for a recovering txnId
+ * (BeginRecovery.java:132-144, :329-380; CommandsForKey.mapReduceFull CommandsForKey.java:809-908,
+ * InMemorySafeStore.mapReduceFull InMemoryCommandStore.java:874-882), batched: request i recovers
+ * txnId i (testTxnId; executeAt and min_epoch are not read) over its keys, testKind =
+ * txnId.kind().witnessedBy() (Txn.java:247-262).
+ *
+ * TxnInfo.missing() (CommandsForKey.java:332-341): the ids each entry's deps do not hold. Entry e of
+ * the loaded ad_cfk_soa has missing ids [off[e], off[e+1]) (ascending); without a load every entry
+ * has NO_TXNIDS. Loading a new ad_cfk_soa clears them. CommandsForKey.loadingPruned is empty (no
+ * pruned ids are being loaded), as it is once a store has caught up. */
+typedef struct ad_cfk_missing_soa {
+    uint64_t n_entries;             /* == n_entries of the loaded ad_cfk_soa */
+    const uint64_t* off;            /* [n_entries + 1] */
+    const uint64_t* msb;
+    const uint64_t* lsb;
+    const int32_t*  node;
+} ad_cfk_missing_soa;
+
+int ad_cfk_missing_load(ad_ctx* ctx, const ad_cfk_missing_soa* missing);
+
+/* which scan (BeginRecovery.java): the result is the Deps its map lambda builds; for the two
+ * boolean scans the answer is "the request's result holds a pair" (the lambda returns true on the
+ * first (key, txnId) the scan visits) and the pairs are the witnesses. */
+#define AD_RECOVER_STARTED_BEFORE_ACCEPTED_NO_WITNESS 0  /* acceptedOrCommittedStartedBeforeWithoutWitnessing :329-342:
+                                                          * STARTED_BEFORE, WITHOUT, IS_PROPOSED            */
+#define AD_RECOVER_STARTED_BEFORE_STABLE_WITNESS      1  /* stableStartedBeforeAndWitnessed :344-352:
+                                                          * STARTED_BEFORE, WITH, IS_STABLE                 */
+#define AD_RECOVER_STARTED_AFTER_ACCEPTED_NO_WITNESS  2  /* hasAcceptedOrCommittedStartedAfterWithoutWitnessing
+                                                          * :354-367: STARTED_AFTER, WITHOUT, IS_PROPOSED    */
+#define AD_RECOVER_EXECUTES_AFTER_STABLE_NO_WITNESS   3  /* hasStableExecutesAfterWithoutWitnessing :369-380:
+                                                          * ANY, WITHOUT, IS_STABLE                         */
+
+/* Host buffers in, host result out (as ad_deps_batch; rangeDeps is empty). Range-domain commands
+ * need their own deps to be tested (InMemoryCommandStore.java:931-949), which this ABI does not
+ * carry: a store with live range commands fails with AD_E_STATE. */
+int ad_recovery_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t scan, ad_deps_result** out);
+/* Device buffers in and out, as ad_deps_batch_device (result valid until the next batch call). */
+int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t scan, void* stream, ad_deps_result* out);
+
 #ifdef __cplusplus
 }
 #endif

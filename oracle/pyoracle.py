@@ -54,6 +54,9 @@ def lib():
         L.rc_levels.argtypes = [C.POINTER(A.AdGraphSoa), C.c_void_p]
         L.rc_preaccept.argtypes = [C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdQuerySoa),
                                    C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rc_cfk_missing_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkMissingSoa)]
+        L.rc_recovery_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_uint64, C.c_uint64,
+                                        C.POINTER(C.POINTER(RcResult))]
         L.rc_tid_cmp.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
         _lib = L
     return _lib
@@ -116,7 +119,20 @@ class OracleStore:
         self._check(L.rc_cfk_load(self.h, C.byref(workload.cfk.soa())))
         self._check(L.rc_range_cmds_load(self.h, C.byref(workload.cmds.soa())))
         self._check(L.rc_redundant_load(self.h, C.byref(workload.redundant.soa())))
+        ms = workload.cfk.missing_soa()
+        if ms is not None:
+            self._check(L.rc_cfk_missing_load(self.h, C.byref(ms)))
         return self
+
+    def recovery_batch(self, queries, scan, first=0, count=0):
+        """rc_recovery_batch: BeginRecovery scan `scan` (AD_RECOVER_*) per request."""
+        L = lib()
+        out = C.POINTER(RcResult)()
+        self._check(L.rc_recovery_batch(self.h, C.byref(queries.soa()), scan, first, count, C.byref(out)))
+        try:
+            return result_to_batch(out.contents)
+        finally:
+            L.rc_result_free(out)
 
     def deps_batch(self, queries, flags=A.AD_SNAPSHOT, first=0, count=0):
         L = lib()
@@ -150,6 +166,16 @@ def resolve(workload, elide=1, first=0, count=0):
     try:
         st.load(workload)
         return st.deps_batch(workload.queries, workload.flags, first, count)
+    finally:
+        st.close()
+
+
+def recover(workload, scan, first=0, count=0):
+    """One BeginRecovery scan over a workload through a fresh oracle store."""
+    st = OracleStore(workload.range_start_inclusive, 1, workload.slices)
+    try:
+        st.load(workload)
+        return st.recovery_batch(workload.queries, scan, first, count)
     finally:
         st.close()
 

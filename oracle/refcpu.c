@@ -92,7 +92,8 @@ static int manages(const tid_t* t) { return tid_domain(t) == 0 && kinds_test(KIN
 /* CommandsForKey                                                                       */
 /* ------------------------------------------------------------------------------------ */
 /* TxnInfo, CommandsForKey.java:237-378: a TxnId + InternalStatus + executeAt */
-typedef struct { tid_t txnId; uint8_t status; tid_t executeAt; } info_t;
+/* missing(): ids [miss_off, miss_off + miss_n) of the store's missing pool (NO_TXNIDS when miss_n == 0) */
+typedef struct { tid_t txnId; uint8_t status; tid_t executeAt; uint32_t miss_off, miss_n; } info_t;
 
 typedef struct {
     int64_t key;
@@ -491,6 +492,7 @@ struct rc_store {
     VEC(rcmd_t) cmds;         /* rangeCommands, sorted by txnId */
     VEC(rcmd_t) hist;         /* historicalRangeCommands, sorted by txnId */
     VEC(rb_entry_t) rb;
+    VEC(tid_t) miss;          /* TxnInfo.missing() lists (rc_cfk_missing_load) */
     int loaded;
     char err[256];
 };
@@ -544,6 +546,7 @@ void rc_store_destroy(rc_store* s)
     free_cfks(s);
     free_cmds(s);
     VEC_FREE(s->rb);
+    VEC_FREE(s->miss);
     free(s->slice_start); free(s->slice_end);
     free(s);
 }
@@ -583,6 +586,7 @@ static cfk_t* find_cfk(rc_store* s, int64_t key)
 int rc_cfk_load(rc_store* s, const ad_cfk_soa* in)
 {
     free_cfks(s);
+    VEC_FREE(s->miss);
     for (uint64_t k = 0; k < in->n_keys; ++k)
     {
         if (k > 0 && in->keys[k - 1] >= in->keys[k])
@@ -596,6 +600,7 @@ int rc_cfk_load(rc_store* s, const ad_cfk_soa* in)
             info.txnId = (tid_t){in->txn_msb[e], in->txn_lsb[e], in->txn_node[e]};
             info.executeAt = (tid_t){in->exec_msb[e], in->exec_lsb[e], in->exec_node[e]};
             info.status = in->status[e];
+            info.miss_off = info.miss_n = 0;
             if (info.status > 7) { VEC_FREE(c.byId); return fail(s, AD_E_INVAL, "bad status"); }
             if (c.byId.n > 0 && tid_cmp(&c.byId.v[c.byId.n - 1].txnId, &info.txnId) >= 0)
             {
@@ -902,7 +907,7 @@ static void sequential_preaccept(rc_store* s, const tid_t* txnId, const int64_t*
         }
         else
         {
-            info_t info = {*txnId, AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE, *txnId};
+            info_t info = {*txnId, AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE, *txnId, 0, 0};
             VEC_PUSH(c->byId, info);
             memmove(&c->byId.v[pos + 1], &c->byId.v[pos], (c->byId.n - 1 - pos) * sizeof(info_t));
             c->byId.v[pos] = info;
@@ -931,6 +936,38 @@ void rc_result_free(rc_result* r)
         free(r->k2t_off[m]); free(r->k2t[m]);
     }
     free(r);
+}
+
+/* append request qi's three maps to a result under construction (cap/len: per map keys, ids, k2t) */
+static void result_append(rc_result* r, uint64_t qi, const pdeps_t* pd, size_t cap[AD_NMAPS][3], size_t len[AD_NMAPS][3])
+{
+    const rmm_t* maps[AD_NMAPS] = {&pd->key, &pd->range, &pd->direct};
+    for (int m = 0; m < AD_NMAPS; ++m)
+    {
+        const rmm_t* mm = maps[m];
+        size_t nk = len[m][0] + mm->nkeys, nt = len[m][1] + mm->nvalues, no = len[m][2] + mm->nout;
+        if (nk > cap[m][0] || nt > cap[m][1] || no > cap[m][2])
+        {
+            cap[m][0] = nk * 2 + 16; cap[m][1] = nt * 2 + 16; cap[m][2] = no * 2 + 16;
+            result_alloc_map(r, m, cap[m][0], cap[m][1], cap[m][2]);
+        }
+        for (size_t k = 0; k < mm->nkeys; ++k)
+        {
+            r->keys[m][len[m][0] + k] = mm->keys[k].a;
+            if (m == AD_MAP_RANGE) r->keys_end[m][len[m][0] + k] = mm->keys[k].b;
+        }
+        for (size_t t = 0; t < mm->nvalues; ++t)
+        {
+            r->txn_msb[m][len[m][1] + t] = mm->values[t].msb;
+            r->txn_lsb[m][len[m][1] + t] = mm->values[t].lsb;
+            r->txn_node[m][len[m][1] + t] = mm->values[t].node;
+        }
+        memcpy(r->k2t[m] + len[m][2], mm->out, sizeof(int32_t) * mm->nout);
+        len[m][0] = nk; len[m][1] = nt; len[m][2] = no;
+        r->keys_off[m][qi + 1] = nk;
+        r->txn_off[m][qi + 1] = nt;
+        r->k2t_off[m][qi + 1] = no;
+    }
 }
 
 int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t first, uint64_t count, rc_result** out)
@@ -963,33 +1000,7 @@ int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t f
         pdeps_t pd;
         rc = calculate_partial_deps(s, &txnId, keys, nkeys, q->min_epoch ? q->min_epoch[i] : 0, &executeAt, &pd, &r->scan_entries);
         if (rc) break;
-        const rmm_t* maps[AD_NMAPS] = {&pd.key, &pd.range, &pd.direct};
-        for (int m = 0; m < AD_NMAPS; ++m)
-        {
-            const rmm_t* mm = maps[m];
-            size_t nk = len[m][0] + mm->nkeys, nt = len[m][1] + mm->nvalues, no = len[m][2] + mm->nout;
-            if (nk > cap[m][0] || nt > cap[m][1] || no > cap[m][2])
-            {
-                cap[m][0] = nk * 2 + 16; cap[m][1] = nt * 2 + 16; cap[m][2] = no * 2 + 16;
-                result_alloc_map(r, m, cap[m][0], cap[m][1], cap[m][2]);
-            }
-            for (size_t k = 0; k < mm->nkeys; ++k)
-            {
-                r->keys[m][len[m][0] + k] = mm->keys[k].a;
-                if (m == AD_MAP_RANGE) r->keys_end[m][len[m][0] + k] = mm->keys[k].b;
-            }
-            for (size_t t = 0; t < mm->nvalues; ++t)
-            {
-                r->txn_msb[m][len[m][1] + t] = mm->values[t].msb;
-                r->txn_lsb[m][len[m][1] + t] = mm->values[t].lsb;
-                r->txn_node[m][len[m][1] + t] = mm->values[t].node;
-            }
-            memcpy(r->k2t[m] + len[m][2], mm->out, sizeof(int32_t) * mm->nout);
-            len[m][0] = nk; len[m][1] = nt; len[m][2] = no;
-            r->keys_off[m][qi + 1] = nk;
-            r->txn_off[m][qi + 1] = nt;
-            r->k2t_off[m][qi + 1] = no;
-        }
+        result_append(r, qi, &pd, cap, len);
         pdeps_free(&pd);
     }
     if (rc) { rc_result_free(r); return rc; }
@@ -1278,5 +1289,192 @@ int rc_preaccept(const ad_range_map_soa* mc, const ad_range_map_soa* rb, const a
         out_node[t] = mn.node;
         out_flags[t] = flags;
     }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Recovery scans                                                         */
+/* ------------------------------------------------------------------------------------ */
+int rc_cfk_missing_load(rc_store* s, const ad_cfk_missing_soa* m)
+{
+    if (!s->loaded) return fail(s, AD_E_NOT_LOADED, "rc_cfk_load not called");
+    uint64_t ne = 0;
+    for (size_t k = 0; k < s->cfks.n; ++k) ne += s->cfks.v[k].byId.n;
+    if (m->n_entries != ne) return fail(s, AD_E_INVAL, "missing lists for %llu entries, store has %llu",
+                                        (unsigned long long)m->n_entries, (unsigned long long)ne);
+    VEC_FREE(s->miss);
+    uint64_t e = 0;
+    for (size_t k = 0; k < s->cfks.n; ++k)
+        for (size_t i = 0; i < s->cfks.v[k].byId.n; ++i, ++e)
+        {
+            info_t* info = &s->cfks.v[k].byId.v[i];
+            const uint64_t a = m->off[e], b = m->off[e + 1];
+            if (b < a) return fail(s, AD_E_INVAL, "missing offsets not monotone");
+            /* TxnInfo.create: missing only with hasExecuteAtOrDeps (CommandsForKey.java:278) */
+            if (b > a && !(info->status >= AD_ST_ACCEPTED && info->status <= AD_ST_APPLIED))
+                return fail(s, AD_E_INVAL, "missing ids on an entry without deps (CommandsForKey.java:278)");
+            info->miss_off = (uint32_t)s->miss.n;
+            info->miss_n = (uint32_t)(b - a);
+            for (uint64_t j = a; j < b; ++j)
+            {
+                tid_t t = {m->msb[j], m->lsb[j], m->node[j]};
+                if (j > a && tid_cmp(&s->miss.v[s->miss.n - 1], &t) >= 0)
+                    return fail(s, AD_E_INVAL, "missing ids not strictly ascending");
+                VEC_PUSH(s->miss, t);
+            }
+        }
+    return 0;
+}
+
+/* Txn.Kind.witnessedBy(), Txn.java:247-262 (Kinds.test :139-152); -1: AssertionError */
+static int kind_witnessed_by(int kind, unsigned* out)
+{
+    switch (kind)
+    {
+        case AD_KIND_EPHEMERAL_READ: *out = 0; return 0;                               /* Nothing */
+        case AD_KIND_READ: *out = (1u << AD_KIND_WRITE) | (1u << AD_KIND_SYNC_POINT)
+                                  | (1u << AD_KIND_EXCLUSIVE_SYNC_POINT); return 0;     /* WsOrSyncPoints */
+        case AD_KIND_WRITE: *out = KINDS_ANY_GLOBALLY_VISIBLE; return 0;
+        case AD_KIND_SYNC_POINT:
+        case AD_KIND_EXCLUSIVE_SYNC_POINT: *out = 1u << AD_KIND_EXCLUSIVE_SYNC_POINT; return 0;
+        default: return -1;
+    }
+}
+
+enum { STARTED_BEFORE, STARTED_AFTER, ANY };          /* TestStartedAt */
+enum { ANY_DEPS, WITH, WITHOUT };                     /* TestDep */
+enum { ANY_STATUS, IS_PROPOSED, IS_STABLE };          /* TestStatus */
+
+static int miss_contains(const rc_store* s, const info_t* txn, const tid_t* id)
+{
+    int lo = 0, hi = (int)txn->miss_n;                                   /* Arrays.binarySearch */
+    while (lo < hi)
+    {
+        int mid = (lo + hi) >> 1;
+        int c = tid_cmp(&s->miss.v[txn->miss_off + mid], id);
+        if (c < 0) lo = mid + 1;
+        else if (c > 0) hi = mid;
+        else return 1;
+    }
+    return 0;
+}
+
+/* CommandsForKey.mapReduceFull, CommandsForKey.java:809-908, with an empty loadingPruned
+ * (loadingPrunedFor(..., NO_TXNIDS) then returns NO_TXNIDS) */
+static int cfk_map_reduce_full(const rc_store* s, const cfk_t* c, const tid_t* testTxnId, unsigned testKind,
+                               int testStartedAt, int testDep, int testStatus, deps_builder_t* acc)
+{
+    int start, end;
+    int known = 1;                         /* loadingFor == null */
+    int insertPos = cfk_insert_pos(c, testTxnId);
+    if (!(insertPos < (int)c->byId.n && tid_cmp(&c->byId.v[insertPos].txnId, testTxnId) == 0))
+    {
+        known = 0;                         /* loadingFor = NO_TXNIDS */
+        switch (testDep)
+        {
+            case ANY_DEPS: break;
+            case WITH:
+            {
+                /* testTxnId.compareTo(prunedBefore) >= 0 -> return (prunedBefore NONE when unset) */
+                static const tid_t NONE = {0, 0, 0};
+                const tid_t* pb = c->hasPrunedBefore ? &c->prunedBefore : &NONE;
+                if (tid_cmp(testTxnId, pb) >= 0) return 0;
+                break;
+            }
+            case WITHOUT: break;
+        }
+    }
+    switch (testStartedAt)
+    {
+        case STARTED_BEFORE: start = 0; end = insertPos; break;
+        case STARTED_AFTER: start = insertPos; end = (int)c->byId.n; break;
+        default: start = 0; end = (int)c->byId.n;
+    }
+    for (int i = start; i < end; ++i)
+    {
+        const info_t* txn = &c->byId.v[i];
+        if (!kinds_test(testKind, tid_kind(&txn->txnId))) continue;
+        const int status = txn->status;
+        switch (testStatus)
+        {
+            case IS_PROPOSED:
+                if (status == AD_ST_ACCEPTED || status == AD_ST_COMMITTED) break;
+                continue;
+            case IS_STABLE:
+                if (status >= AD_ST_STABLE && status < AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED) break;
+                continue;
+            case ANY_STATUS:
+                if (status == AD_ST_TRANSITIVELY_KNOWN) continue;
+        }
+        if (testDep != ANY_DEPS)
+        {
+            if (!(status >= AD_ST_ACCEPTED && status <= AD_ST_APPLIED)) continue;   /* !hasExecuteAtOrDeps */
+            if (tid_cmp(&txn->executeAt, testTxnId) <= 0) continue;
+            int hasAsDep = known ? (txn->miss_n == 0 || !miss_contains(s, txn, testTxnId)) : 0;
+            if (hasAsDep != (testDep == WITH)) continue;
+        }
+        /* the map lambdas of BeginRecovery.java:335-339,349,366,379: builder.add(keyOrRange, txnId)
+         * (acceptedOrCommittedStartedBefore...'s executeAt > startedBefore holds already) */
+        int rc = deps_builder_add(acc, 0, c->key, 0, &txn->txnId);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_t first, uint64_t count, rc_result** out)
+{
+    static const int P[4][3] = {{STARTED_BEFORE, WITHOUT, IS_PROPOSED}, {STARTED_BEFORE, WITH, IS_STABLE},
+                                {STARTED_AFTER, WITHOUT, IS_PROPOSED}, {ANY, WITHOUT, IS_STABLE}};
+    if (!s->loaded) return fail(s, AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (scan > 3) return fail(s, AD_E_INVAL, "unknown recovery scan %u", scan);
+    for (size_t i = 0; i < s->cmds.n; ++i)
+        if (!s->cmds.v[i].erased)
+            return fail(s, AD_E_STATE, "range-domain recovery scans need each range command's deps");
+    if (count == 0) count = q->n_txns - first;
+    if (first + count > q->n_txns) return fail(s, AD_E_INVAL, "query window out of range");
+    rc_result* r = calloc(1, sizeof(rc_result));
+    r->n_txns = count;
+    size_t cap[AD_NMAPS][3] = {{0}};
+    size_t len[AD_NMAPS][3] = {{0}};
+    for (int m = 0; m < AD_NMAPS; ++m)
+    {
+        r->keys_off[m] = calloc(count + 1, sizeof(uint64_t));
+        r->txn_off[m] = calloc(count + 1, sizeof(uint64_t));
+        r->k2t_off[m] = calloc(count + 1, sizeof(uint64_t));
+    }
+    int rc = 0;
+    for (uint64_t qi = 0; qi < count && !rc; ++qi)
+    {
+        uint64_t i = first + qi;
+        tid_t txnId = {q->txn_msb[i], q->txn_lsb[i], q->txn_node[i]};
+        const int64_t* keys = q->keys + q->key_off[i];
+        size_t nkeys = (size_t)(q->key_off[i + 1] - q->key_off[i]);
+        for (size_t k = 1; k < nkeys; ++k)
+            if (keys[k - 1] >= keys[k]) { rc = fail(s, AD_E_INVAL, "query keys not strictly ascending"); break; }
+        if (rc) break;
+        unsigned kinds;
+        if (kind_witnessed_by(tid_kind(&txnId), &kinds)) { rc = fail(s, AD_E_INVAL, "invalid Txn.Kind for witnessedBy()"); break; }
+        deps_builder_t builder;                                          /* Deps.builder() */
+        builder_init(&builder.key); builder_init(&builder.range); builder_init(&builder.direct);
+        /* InMemorySafeStore.mapReduceFull -> mapReduceForKey (InMemoryCommandStore.java:272-307) */
+        for (size_t k = 0; k < nkeys && !rc; ++k)
+        {
+            if (!slice_contains(s, keys[k])) continue;
+            cfk_t* cfk = find_cfk(s, keys[k]);
+            if (cfk == NULL) continue;
+            rc = cfk_map_reduce_full(s, cfk, &txnId, kinds, P[scan][0], P[scan][1], P[scan][2], &builder);
+        }
+        pdeps_t pd;
+        memset(&pd, 0, sizeof(pd));
+        if (!rc) rc = deps_build(&builder, &pd);
+        builder_free(&builder.key); builder_free(&builder.range); builder_free(&builder.direct);
+        if (rc) { rc = fail(s, rc, "recovery scan failed"); break; }
+        result_append(r, qi, &pd, cap, len);
+        pdeps_free(&pd);
+    }
+    if (rc) { rc_result_free(r); return rc; }
+    for (int m = 0; m < AD_NMAPS; ++m)
+        if (!r->keys[m]) result_alloc_map(r, m, 1, 1, 1);
+    *out = r;
     return 0;
 }

@@ -60,6 +60,12 @@ int rc_preaccept(const ad_range_map_soa* max_conflicts, const ad_range_map_soa* 
                  uint32_t permit_fast_path, uint64_t node_epoch, uint64_t* out_msb, uint64_t* out_lsb, int32_t* out_node,
                  uint8_t* out_flags);
 
+/* TxnInfo.missing() per entry of the loaded CommandsForKey snapshot (rc_cfk_load order) and the
+ * four BeginRecovery mapReduceFull scans (AD_RECOVER_*; include/accord_deps.h) */
+int rc_cfk_missing_load(rc_store* s, const ad_cfk_missing_soa* m);
+int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_t first, uint64_t count,
+                      rc_result** out);
+
 /* exposed for the tests */
 int rc_tid_cmp(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);
 

@@ -213,3 +213,56 @@ def preaccept_model(mc, rb, q, permit_fast_path=1, node_epoch=0):
         fast = permit_fast_path and key(txn) >= key(acc) and (txn[0] >> 15) >= node_epoch
         out.append((acc, 1 if fast else 0))
     return out
+
+
+WITNESSED_BY = {2: set(), 0: {1, 3, 4}, 1: {0, 1, 3, 4}, 3: {4}, 4: {4}}   # Txn.Kind.witnessedBy, Txn.java:247-262
+RECOVER = {0: ("before", False, (3, 4)), 1: ("before", True, (5, 6)),      # BeginRecovery.java:334,348,365,378
+           2: ("after", False, (3, 4)), 3: ("any", False, (5, 6))}
+
+
+def recovery_pairs(w, qi, scan):
+    """(keyDeps, directKeyDeps) pair sets of BeginRecovery scan `scan` for request qi: the entries
+    CommandsForKey.mapReduceFull (CommandsForKey.java:809-908) visits, from a flat reading of its
+    predicates (empty loadingPruned)."""
+    q, c = w.queries, w.cfk
+    T = (int(q.txn.msb[qi]), int(q.txn.lsb[qi]), int(q.txn.node[qi]))
+    keys = [int(k) for k in q.keys[int(q.key_off[qi]):int(q.key_off[qi + 1])]]
+    started, with_dep, statuses = RECOVER[scan]
+    kinds = WITNESSED_BY[kind(T)]
+    si = w.range_start_inclusive
+    kd, dd = set(), set()
+    for k in keys:
+        if w.slices is not None and not any(contains(si, int(a), int(b), k) for a, b in w.slices):
+            continue
+        pos = np.searchsorted(c.keys, k)
+        if pos >= len(c.keys) or c.keys[pos] != k:
+            continue
+        ents = range(int(c.seg[pos]), int(c.seg[pos + 1]))
+        tid = lambda e: (int(c.txn.msb[e]), int(c.txn.lsb[e]), int(c.txn.node[e]))  # noqa: E731
+        known = any(eq(tid(e), T) for e in ents)
+        if with_dep and not known:
+            pb = None
+            if c.pruned_before is not None and c.pruned_before[pos] >= 0:
+                pb = tid(int(c.seg[pos]) + int(c.pruned_before[pos]))
+            if pb is None or not key(T) < key(pb):
+                continue
+        for e in ents:
+            t = tid(e)
+            if started == "before" and not key(t) < key(T):
+                continue
+            if started == "after" and key(t) < key(T):
+                continue
+            if kind(t) not in kinds or int(c.status[e]) not in statuses:
+                continue
+            ex = (int(c.exec.msb[e]), int(c.exec.lsb[e]), int(c.exec.node[e]))
+            if not key(ex) > key(T):
+                continue
+            miss = []
+            if c.miss_off is not None:
+                m0, m1 = int(c.miss_off[e]), int(c.miss_off[e + 1])
+                miss = [(int(c.miss.msb[j]), int(c.miss.lsb[j]), int(c.miss.node[j])) for j in range(m0, m1)]
+            has_as_dep = known and not any(eq(m, T) for m in miss)
+            if has_as_dep != with_dep:
+                continue
+            (kd if kind(t) in (0, 1) else dd).add((k, key(t), t))
+    return kd, dd
