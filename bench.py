@@ -63,7 +63,7 @@ def measured_traffic(kernels):
     profiles/ that has all of them (FETCH_SIZE doubled for gfx950 as MI355X_MICROARCH.md
     prescribes, + WRITE_SIZE; scripts/summarize_prof.py), or (None, None)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))   # by name: rN_vM order (checkout mtimes are arbitrary)
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
