@@ -55,6 +55,11 @@ class AdCfkSoa(C.Structure):
                 ("status", P), ("pruned_before", P)]
 
 
+class AdCfkUpdateSoa(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("keys", P), ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
+                ("exec_msb", P), ("exec_lsb", P), ("exec_node", P), ("status", P)]
+
+
 class AdCfkMissingSoa(C.Structure):
     _fields_ = [("n_entries", C.c_uint64), ("off", P), ("msb", P), ("lsb", P), ("node", P)]
 

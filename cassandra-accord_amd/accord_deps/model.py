@@ -135,6 +135,32 @@ class CfkSnapshot:
 
 
 @dataclass
+class CfkUpdates:
+    """A batch of CommandsForKey.update calls (ad_cfk_update_soa): update i raises txn[i] in the
+    CommandsForKey of keys[i] to status[i] with executeAt exec[i]."""
+    keys: np.ndarray          # i64
+    txn: Tids
+    exec: Tids
+    status: np.ndarray        # u8 InternalStatus
+
+    def __post_init__(self):
+        self.keys = A.as_i64(self.keys)
+        self.status = A.as_u8(self.status)
+
+    def __len__(self):
+        return len(self.keys)
+
+    def soa(self):
+        s = A.AdCfkUpdateSoa()
+        s.n = len(self.keys)
+        s.keys = A.ptr(self.keys)
+        s.txn_msb, s.txn_lsb, s.txn_node = A.ptr(self.txn.msb), A.ptr(self.txn.lsb), A.ptr(self.txn.node)
+        s.exec_msb, s.exec_lsb, s.exec_node = A.ptr(self.exec.msb), A.ptr(self.exec.lsb), A.ptr(self.exec.node)
+        s.status = A.ptr(self.status)
+        return s
+
+
+@dataclass
 class RangeCommands:
     txn: Tids
     range_off: np.ndarray

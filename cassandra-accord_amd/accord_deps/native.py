@@ -23,7 +23,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
            "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict", "ad_preaccept_maps_load",
            "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_recovery_batch",
-           "ad_recovery_batch_device")
+           "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries")
 
 
 class AccordDepsError(RuntimeError):
@@ -83,6 +83,11 @@ def lib():
                                         C.POINTER(C.POINTER(A.AdDepsResult))]
         L.ad_recovery_batch_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_void_p,
                                                C.POINTER(A.AdDepsResult)]
+        L.ad_cfk_update.argtypes = [C.c_void_p, C.POINTER(A.AdCfkUpdateSoa), C.POINTER(C.c_uint64), C.POINTER(A.AdStats)]
+        L.ad_cfk_update_device.argtypes = [C.c_void_p, C.POINTER(A.AdCfkUpdateSoa), C.c_void_p, C.POINTER(C.c_uint64),
+                                           C.POINTER(A.AdStats)]
+        L.ad_cfk_entries.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                     C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         _lib = L
     return _lib
 
@@ -148,6 +153,27 @@ class DeviceCommandStore:
         if prepare:
             self._check(L.ad_prepare(self.h))
         return self
+
+    def cfk_update(self, updates):
+        """CommandsForKey.update for a batch (host arrays): returns (n_applied, stats)."""
+        n, st = C.c_uint64(), A.AdStats()
+        self._check(lib().ad_cfk_update(self.h, C.byref(updates.soa()), C.byref(n), C.byref(st)))
+        return n.value, stats_dict(st)
+
+    def cfk_update_device(self, udev, stream=None):
+        """As cfk_update over device arrays (an AdCfkUpdateSoa of device pointers)."""
+        n, st = C.c_uint64(), A.AdStats()
+        self._check(lib().ad_cfk_update_device(self.h, C.byref(udev), stream, C.byref(n), C.byref(st)))
+        return n.value, stats_dict(st)
+
+    def cfk_entries(self):
+        """(status, executeAt Tids) of every entry as the store now holds them (load order)."""
+        n = C.c_uint64()
+        ps, pm, pl, pn = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._check(lib().ad_cfk_entries(self.h, C.byref(n), C.byref(ps), C.byref(pm), C.byref(pl), C.byref(pn)))
+        k = n.value
+        return _view(ps, k, np.uint8).copy(), Tids(_view(pm, k, np.uint64).copy(), _view(pl, k, np.uint64).copy(),
+                                                   _view(pn, k, np.int32).copy())
 
     def dictionary(self):
         n = C.c_uint64()
@@ -406,6 +432,21 @@ def levels(graph, device=0):
         return out, levels_stats(s)
     finally:
         st.close()
+
+
+def device_updates(u, dev):
+    """Copy a CfkUpdates batch to device `dev`; returns (AdCfkUpdateSoa of device pointers, keepalive)."""
+    import torch
+
+    def to_dev(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int64 if a.dtype.itemsize == 8 else
+                                                              np.int32 if a.dtype.itemsize == 4 else np.uint8)).to(dev)
+    arrs = [u.keys, u.txn.msb, u.txn.lsb, u.txn.node, u.exec.msb, u.exec.lsb, u.exec.node, u.status]
+    t = [to_dev(a) for a in arrs]
+    s = A.AdCfkUpdateSoa()
+    s.n = len(u)
+    (s.keys, s.txn_msb, s.txn_lsb, s.txn_node, s.exec_msb, s.exec_lsb, s.exec_node, s.status) = [x.data_ptr() for x in t]
+    return s, t
 
 
 def device_graph(graph, dev):

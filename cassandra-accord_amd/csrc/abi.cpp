@@ -24,6 +24,7 @@
 #include "exchange.hpp"
 #include "kernels.hpp"
 #include "levels.hpp"
+#include "cfk_update.hpp"
 
 using namespace adx;
 
@@ -239,6 +240,15 @@ struct ad_ctx {
     // execution levels (K5)
     LevelsWork* lv = nullptr;
     DevBuf g_em, g_el, g_en, g_kind, g_ko, g_k, g_do, g_d, g_out;
+    // device-resident CommandsForKey maintenance (ad_cfk_update*): per-entry status, executeAt
+    // rank and key index; host copies (cfk.status / cfk.exec / h_exec_rank) are refreshed from
+    // them on demand (host_stale)
+    DevBuf d_status, d_xrank, d_ekey;
+    DevBuf u_k, u_tm, u_tl, u_tn, u_em, u_el, u_en, u_st;
+    CfkUpdWork* cu = nullptr;
+    bool host_stale = false;
+    std::vector<uint64_t> x_msb, x_lsb;        // ad_cfk_entries views
+    std::vector<int32_t> x_node;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -292,8 +302,11 @@ static int upload(ad_ctx* c, DevBuf& b, const std::vector<T>& v)
     return 0;
 }
 
+static int sync_host(ad_ctx* c);
+
 static int build_snapshot(ad_ctx* c)
 {
+    if (int rc0 = sync_host(c)) return rc0;
     const double t0 = now_ms();
     auto& K = c->cfk;
     const uint64_t nk = K.keys.size(), ne = K.status.size();
@@ -655,6 +668,13 @@ static int build_snapshot(ad_ctx* c)
             ke.cl[cl].cwr_hi = cwr_off[k + 1];
         }
     }
+    {
+        std::vector<uint32_t> ekey(std::max<uint64_t>(ne, 1), 0);
+        for (uint64_t k = 0; k < nk; ++k)
+            for (uint64_t e = K.seg[k]; e < K.seg[k + 1]; ++e) ekey[e] = (uint32_t)k;
+        if ((rc = upload(c, c->d_status, K.status)) || (rc = upload(c, c->d_xrank, exec_rank)) || (rc = upload(c, c->d_ekey, ekey)))
+            return rc;
+    }
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
         (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_khash, khash)) || (rc = upload(c, c->d_kent, kent)) || (rc = upload(c, c->d_cand, cand)) || (rc = upload(c, c->d_cwr, cwr)) ||
         (rc = upload(c, c->d_ent, ent)) ||
@@ -748,11 +768,37 @@ static int build_snapshot(ad_ctx* c)
     return 0;
 }
 
+// Host copies of the per-entry state after ad_cfk_update* changed it on the device: status and
+// executeAt (from its rank through the dictionary, raw bits of the dictionary member).
+static int sync_host(ad_ctx* c)
+{
+    if (!c->host_stale) return 0;
+    auto& K = c->cfk;
+    const uint64_t ne = K.status.size();
+    std::vector<uint32_t> xr(ne);
+    if (ne)
+    {
+        HIPCHK(c, hipMemcpyAsync(K.status.data(), c->d_status.p, ne, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(xr.data(), c->d_xrank.p, 4 * ne, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    for (uint64_t e = 0; e < ne; ++e)
+        if (xr[e] != c->h_exec_rank[e])
+        {
+            const uint64_t i = (xr[e] - 1) / 2;
+            K.exec[e] = {c->dict_msb[i], c->dict_lsb[i], c->dict_node[i]};
+        }
+    c->h_exec_rank.swap(xr);
+    c->host_stale = false;
+    return 0;
+}
+
 // SEQUENTIAL: insert every request's txnId as PREACCEPTED_OR_ACCEPTED_INVALIDATE into the
 // CommandsForKey of each of its keys in the slice (CommandsForKey.update, :972-1042; a present
 // entry below PREACCEPTED is raised, otherwise left alone).
 static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
 {
+    if (int rc0 = sync_host(c)) return rc0;
     auto& K = c->cfk;
     struct Ins { int64_t key; NormTid n; Tid t; };
     std::vector<Ins> ins;
@@ -1252,6 +1298,7 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->ev_sp1) (void)hipEventDestroy(c->ev_sp1);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->lv) levels_work_destroy(c->lv);
+    if (c->cu) cfk_upd_work_destroy(c->cu);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1284,6 +1331,7 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     K.miss.clear();
     K.miss_stale = false;
     K.loaded = true;
+    c->host_stale = false;       // the load replaces whatever ad_cfk_update applied on the device
     c->dirty = true;
     return AD_OK;
 }
@@ -1380,6 +1428,7 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
 // status, kind and their TxnInfo.missing() lists as ranks (built once per snapshot / missing load)
 static int build_recovery_view(ad_ctx* c, RecoveryView* v)
 {
+    if (int rc0 = sync_host(c)) return rc0;
     auto& K = c->cfk;
     for (size_t i = 0; i < c->cmds.txn.size(); ++i)
         if (c->cmds.erased.empty() || !c->cmds.erased[i])
@@ -1935,6 +1984,114 @@ int ad_levels(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, ad_stats* s
     if ((rc = levels_run(c, in, c->g_out.as<uint32_t>(), c->stream, stats))) return rc;
     HIPCHK(c, hipMemcpyAsync(level_out, c->g_out.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return AD_OK;
+}
+
+// ---- device-resident CommandsForKey maintenance ----------------------------
+static int cfk_need_bufs(void* vc, uint64_t n_cand, uint64_t n_cwr, uint64_t n_w, CfkDerivedBufs* b)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    if (!c->d_cand.ensure(4 * std::max<uint64_t>(n_cand, 1)) || !c->d_cwr.ensure(4 * std::max<uint64_t>(n_cwr, 1)) ||
+        !c->d_w.ensure(8 * std::max<uint64_t>(n_w, 1)))
+        return AD_E_NOMEM;
+    b->cand = c->d_cand.as<uint32_t>();
+    b->cwr = c->d_cwr.as<uint32_t>();
+    b->w = c->d_w.as<uint2>();
+    return 0;
+}
+
+static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats)
+{
+    if (c->dirty)
+        if (int rc = build_snapshot(c)) return rc;
+    if (!c->cu) c->cu = cfk_upd_work_create();
+    CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
+                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
+    CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
+                     c->d_w.as<uint2>(), c->d_w.cap / 8};
+    CfkUpdOut o;
+    std::string e;
+    const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, st, &o, &e);
+    if (rc == AD_E_NOMEM || rc == AD_E_DEVICE)
+    {
+        // the derived arrays may be half built: rebuild them from the entries at the next use
+        c->host_stale = true;
+        c->dirty = true;
+    }
+    if (rc) return c->fail(rc, "%s", e.c_str());
+    if (u.n)
+    {
+        c->host_stale = true;
+        ++c->snap_gen;            // device views built from the host state (recovery) are stale
+    }
+    if (n_applied) *n_applied = o.n_applied;
+    if (stats)
+    {
+        *stats = ad_stats{};
+        stats->n_txns = u.n;
+        stats->ms_device = o.ms_total;
+        stats->ms_stage[0] = o.ms_locate;
+        stats->ms_stage[1] = o.ms_derive;
+    }
+    return AD_OK;
+}
+
+static int check_update_soa(ad_ctx* c, const ad_cfk_update_soa* u)
+{
+    if (!u) return c->fail(AD_E_INVAL, "null update batch");
+    if (u->n && (!u->keys || !u->txn_msb || !u->txn_lsb || !u->txn_node || !u->exec_msb || !u->exec_lsb ||
+                 !u->exec_node || !u->status))
+        return c->fail(AD_E_INVAL, "update batch with null arrays");
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    return 0;
+}
+
+int ad_cfk_update_device(ad_ctx* c, const ad_cfk_update_soa* u, void* stream, uint64_t* n_applied, ad_stats* stats)
+{
+    if (!c) return AD_E_INVAL;
+    if (int rc = check_update_soa(c, u)) return rc;
+    CfkUpdIn in{u->n, u->keys, u->txn_msb, u->txn_lsb, u->txn_node, u->exec_msb, u->exec_lsb, u->exec_node, u->status};
+    return cfk_update_run(c, in, stream ? (hipStream_t)stream : c->stream, n_applied, stats);
+}
+
+int ad_cfk_update(ad_ctx* c, const ad_cfk_update_soa* u, uint64_t* n_applied, ad_stats* stats)
+{
+    if (!c) return AD_E_INVAL;
+    if (int rc = check_update_soa(c, u)) return rc;
+    const uint64_t n = u->n;
+    int rc = 0;
+    CfkUpdIn in{n, stage_q(c, c->u_k, u->keys, n, &rc), stage_q(c, c->u_tm, u->txn_msb, n, &rc),
+                stage_q(c, c->u_tl, u->txn_lsb, n, &rc), stage_q(c, c->u_tn, u->txn_node, n, &rc),
+                stage_q(c, c->u_em, u->exec_msb, n, &rc), stage_q(c, c->u_el, u->exec_lsb, n, &rc),
+                stage_q(c, c->u_en, u->exec_node, n, &rc), stage_q(c, c->u_st, u->status, n, &rc)};
+    if (rc) return rc;
+    return cfk_update_run(c, in, c->stream, n_applied, stats);
+}
+
+int ad_cfk_entries(ad_ctx* c, uint64_t* n_entries, const uint8_t** status, const uint64_t** exec_msb,
+                   const uint64_t** exec_lsb, const int32_t** exec_node)
+{
+    if (!c || !n_entries || !status || !exec_msb || !exec_lsb || !exec_node) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (int rc = sync_host(c)) return rc;
+    auto& K = c->cfk;
+    const uint64_t ne = K.status.size();
+    c->x_msb.resize(ne);
+    c->x_lsb.resize(ne);
+    c->x_node.resize(ne);
+    for (uint64_t e = 0; e < ne; ++e)
+    {
+        c->x_msb[e] = K.exec[e].msb;
+        c->x_lsb[e] = K.exec[e].lsb;
+        c->x_node[e] = K.exec[e].node;
+    }
+    *n_entries = ne;
+    *status = K.status.data();
+    *exec_msb = c->x_msb.data();
+    *exec_lsb = c->x_lsb.data();
+    *exec_node = c->x_node.data();
     return AD_OK;
 }
 

@@ -1,0 +1,485 @@
+// cfk_update.hip — SURVEY §8 f1: CommandsForKey.update (CommandsForKey.java:972-1042) applied to
+// the device-resident snapshot, so a store's steady stream of status transitions does not re-run
+// the host ingest and re-upload the snapshot.
+//
+// An update (key, txnId, InternalStatus, executeAt) raises an entry already in the key's byId:
+// the Java's update branch (:1009-1036) replaces the entry iff the new status is above the current
+// one (equal status with a higher ballot is not carried by the ABI and counts as "not above").
+// Within a batch, updates of one entry apply in order, so the entry ends at the first update of the
+// highest status (if above its current status). Entries keep their place in byId; what the
+// status/executeAt change moves is re-derived on the device from the per-entry state:
+//   * ent[e] = {tau, txw}                         (elision key, common.hpp)
+//   * committedByExecuteAt per key (:651-672)      -> stable compaction + LSD radix sort by
+//                                                    (key index, executeAt rank)
+//   * w (committed Writes by executeAt), maxAppliedWriteByExecuteAt (:660-672), krec
+//   * the newest-probe emission lists cand / cwr and KeyEntry
+//   * the 64-ary max trees over tau (build_cfk_trees).
+// Inserting ids the store has never seen needs the id dictionary to grow (rank remap of every
+// array): rejected with AD_E_STATE for now.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+
+#include "../../include/accord_deps.h"
+#include "cfk_update.hpp"
+#include "kernels.hpp"
+#include "levels.hpp"
+
+namespace adx {
+
+namespace {
+
+enum : uint32_t {
+    UE_KEY = 1,          // key not in the snapshot
+    UE_STATUS = 2,       // status > 7
+    UE_ABSENT = 3,       // txnId not in the key's byId (insert)
+    UE_NEW_EXEC = 4,     // executeAt not in the id dictionary
+    UE_FLAGS = 5,        // equal ids differing in flag bits
+    UE_DOMAIN = 6,       // live range-domain id in a CommandsForKey
+    UE_DUP_EXEC = 7,     // two committed entries of a key with one executeAt (:1439)
+};
+
+struct UpdCtl {
+    uint32_t err, err_idx;
+    unsigned long long applied;
+    uint64_t tot[4];          // cand per class, committed entries
+    uint64_t tot2[2];         // cwr, w
+};
+
+__device__ inline void upd_fail(UpdCtl* c, uint32_t code, uint32_t idx)
+{
+    if (atomicCAS(&c->err, 0u, code) == 0u) c->err_idx = idx;
+}
+
+// lower bound of t in the dictionary: member i -> 2i+1, else 0 (with *pos = i)
+__device__ inline uint32_t dict_member_rank(const DevSnapshot& s, const NormTid& t, uint64_t* pos)
+{
+    uint64_t lo = 0, hi = s.n_dict;
+    while (lo < hi)
+    {
+        const uint64_t m = (lo + hi) >> 1;
+        const NormTid d{s.dict_hi[m], s.dict_lo[m], s.dict_node[m]};
+        if (norm_cmp(d, t) < 0) lo = m + 1;
+        else hi = m;
+    }
+    *pos = lo;
+    if (lo < s.n_dict)
+    {
+        const NormTid d{s.dict_hi[lo], s.dict_lo[lo], s.dict_node[lo]};
+        if (norm_cmp(d, t) == 0) return (uint32_t)(2 * lo + 1);
+    }
+    return 0;
+}
+
+__device__ inline uint32_t tau_of(uint32_t st, uint32_t kind, uint32_t xr)
+{
+    if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED) return 0;
+    if (st >= AD_ST_COMMITTED && ((KINDS_RS_OR_WS >> kind) & 1u)) return xr;
+    return TAU_NEVER_ELIDED;
+}
+
+// thread per update: key index, entry position, executeAt rank; claim the entry for the first
+// update of the highest status (packed u64 max: status, then the lowest update index)
+__global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, CfkDevState d, CfkUpdIn u, uint32_t* loc,
+                                                    uint32_t* xr_out, unsigned long long* word, UpdCtl* ctl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u.n) return;
+    loc[i] = 0xFFFFFFFFu;
+    const int64_t key = u.keys[i];
+    uint32_t k = KEY_EMPTY;
+    if (s.n_keys)
+    {
+        uint64_t h = key_hash(key) & s.khash_mask;
+        for (;;)
+        {
+            const KeySlot sl = s.khash[h];
+            if (sl.idx == KEY_EMPTY) break;
+            if (sl.key == key) { k = sl.idx; break; }
+            h = (h + 1) & s.khash_mask;
+        }
+    }
+    if (k == KEY_EMPTY) { upd_fail(ctl, UE_KEY, (uint32_t)i); return; }
+    const uint32_t st = u.status[i];
+    if (st > 7) { upd_fail(ctl, UE_STATUS, (uint32_t)i); return; }
+    const uint64_t tl = u.txn_lsb[i];
+    uint64_t p;
+    const uint32_t r = dict_member_rank(s, norm_tid(u.txn_msb[i], tl, u.txn_node[i]), &p);
+    if (!r) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
+    if (d.dict_lsb_raw[p] != tl) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
+    const KeyRec kr = s.krec[k];
+    uint32_t lo = kr.seg_lo, hi = kr.seg_hi;
+    while (lo < hi)
+    {
+        const uint32_t m = (lo + hi) >> 1;
+        if ((s.ent[m].y & RANK_MASK) < r) lo = m + 1;
+        else hi = m;
+    }
+    if (lo >= kr.seg_hi || (s.ent[lo].y & RANK_MASK) != r) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
+    const uint64_t el = u.exec_lsb[i];
+    const uint32_t xr = dict_member_rank(s, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
+    if (!xr) { upd_fail(ctl, UE_NEW_EXEC, (uint32_t)i); return; }
+    if (d.dict_lsb_raw[p] != el) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
+    if ((tl & 1) && tau_of(st, (uint32_t)((tl >> 1) & 7), xr) != 0) { upd_fail(ctl, UE_DOMAIN, (uint32_t)i); return; }
+    loc[i] = lo;
+    xr_out[i] = xr;
+    atomicMax(word + lo, ((unsigned long long)st << 32) | (0xFFFFFFFFull - i));
+}
+
+// after a failed locate: release every claimed entry
+__global__ void k_upd_release(uint64_t n, const uint32_t* loc, unsigned long long* word)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && loc[i] != 0xFFFFFFFFu) word[loc[i]] = 0;
+}
+
+// the claiming update of each entry applies if its status is above the entry's; the entry's old
+// state is kept in bk[i] for a rollback
+__global__ void k_upd_apply(uint64_t n, const uint32_t* loc, const uint32_t* xr, unsigned long long* word,
+                            CfkDevState d, uint2* bk, UpdCtl* ctl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    bk[i] = make_uint2(0xFFFFFFFFu, 0);
+    const uint32_t e = loc[i];
+    const unsigned long long wd = word[e];
+    if ((uint32_t)wd != (uint32_t)(0xFFFFFFFFull - i)) return;
+    word[e] = 0;
+    const uint32_t st = (uint32_t)(wd >> 32);
+    const uint32_t cur = d.status[e];
+    if (st <= cur) return;
+    bk[i] = make_uint2(cur, d.xrank[e]);
+    d.status[e] = (uint8_t)st;
+    d.xrank[e] = xr[i];
+    atomicAdd(&ctl->applied, 1ull);
+}
+
+__global__ void k_upd_rollback(uint64_t n, const uint32_t* loc, const uint2* bk, CfkDevState d)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || bk[i].x == 0xFFFFFFFFu) return;
+    d.status[loc[i]] = (uint8_t)bk[i].x;
+    d.xrank[loc[i]] = bk[i].y;
+}
+
+// ---- derivation (thread per entry): tau, never-elided class flags, committed flag
+__global__ __launch_bounds__(256) void k_drv_flags(uint64_t ne, CfkDevState d, uint32_t* flags)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t st = d.status[e], y = d.ent[e].y, kind = y >> RANK_BITS;
+    const uint32_t tau = tau_of(st, kind, d.xrank[e]);
+    d.ent[e].x = tau;
+    for (int cl = 0; cl < NCLASS; ++cl)
+        flags[cl * ne + e] = tau == TAU_NEVER_ELIDED ? ((CLASS_KINDS[cl] >> kind) & 1u) : 0u;
+    flags[3 * ne + e] = (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED) ? 1u : 0u;
+}
+
+__global__ void k_drv_totals(const uint64_t* fs, uint64_t n, int n_arrays, uint64_t* tot)
+{
+    if ((int)threadIdx.x < n_arrays) tot[threadIdx.x] = fs[threadIdx.x * (n + 1) + n];
+}
+
+// cand (class-major, byId order) and the committed entries keyed (key index, executeAt rank)
+__global__ __launch_bounds__(256) void k_drv_scatter(uint64_t ne, CfkDevState d, const uint64_t* fs, const UpdCtl* ctl,
+                                                     uint32_t* cand, uint64_t* ck, uint32_t* cv)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint2 en = d.ent[e];
+    const uint32_t kind = en.y >> RANK_BITS;
+    if (en.x == TAU_NEVER_ELIDED)
+    {
+        uint64_t base = 0;
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            if ((CLASS_KINDS[cl] >> kind) & 1u) cand[base + fs[cl * (ne + 1) + e]] = en.y;
+            base += ctl->tot[cl];
+        }
+    }
+    const uint32_t st = d.status[e];
+    if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED)
+    {
+        const uint64_t j = fs[3 * (ne + 1) + e];
+        ck[j] = ((uint64_t)d.ekey[e] << 32) | d.xrank[e];
+        cv[j] = (uint32_t)e;
+    }
+}
+
+// sorted committed entries: duplicate executeAt check, cwr (Read/Write) and w (Write) flags
+__global__ __launch_bounds__(256) void k_drv_committed(uint64_t ncm, const uint64_t* ck, const uint32_t* cv,
+                                                       CfkDevState d, uint32_t* f2, UpdCtl* ctl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ncm) return;
+    if (i > 0 && ck[i - 1] == ck[i]) upd_fail(ctl, UE_DUP_EXEC, cv[i]);
+    const uint32_t kind = d.ent[cv[i]].y >> RANK_BITS;
+    f2[i] = (KINDS_RS_OR_WS >> kind) & 1u;
+    f2[ncm + i] = kind == AD_KIND_WRITE ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_drv_emit(uint64_t ncm, uint64_t ne, const uint64_t* ck, const uint32_t* cv,
+                                                  CfkDevState d, const uint64_t* fs, const uint64_t* s2,
+                                                  uint32_t* cwr, uint2* w, int32_t* maw, uint32_t* wtail)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ncm) return;
+    const uint32_t e = cv[i];
+    const uint32_t y = d.ent[e].y, kind = y >> RANK_BITS;
+    if ((KINDS_RS_OR_WS >> kind) & 1u) cwr[s2[i]] = y;
+    if (kind != AD_KIND_WRITE) return;
+    const uint64_t p = s2[(ncm + 1) + i];
+    const uint32_t k = (uint32_t)(ck[i] >> 32);
+    w[p] = make_uint2((uint32_t)ck[i], y & RANK_MASK);
+    if (d.status[e] == AD_ST_APPLIED) atomicMax(maw + k, (int32_t)p);
+    const uint64_t cm_hi = fs[3 * (ne + 1) + d.krec[k].seg_hi];
+    if (p + 1 == s2[(ncm + 1) + cm_hi]) wtail[k] = (uint32_t)s2[i];     // the key's last Write: its cwr index
+}
+
+__global__ __launch_bounds__(256) void k_drv_keys(uint64_t nk, uint64_t ne, uint64_t ncm, CfkDevState d, const uint64_t* fs,
+                                                  const uint64_t* s2, const uint2* w, const int32_t* maw,
+                                                  const uint32_t* wtail, const UpdCtl* ctl)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    KeyRec kr = d.krec[k];
+    const uint64_t cm_lo = fs[3 * (ne + 1) + kr.seg_lo], cm_hi = fs[3 * (ne + 1) + kr.seg_hi];
+    const uint32_t cwr_lo = (uint32_t)s2[cm_lo], cwr_hi = (uint32_t)s2[cm_hi];
+    const uint32_t w_lo = (uint32_t)s2[(ncm + 1) + cm_lo], w_hi = (uint32_t)s2[(ncm + 1) + cm_hi];
+    const bool has_w = w_hi > w_lo;
+    const uint2 lw = has_w ? w[w_hi - 1] : make_uint2(0u, 0u);
+    kr.w_lo = w_lo;
+    kr.w_hi = w_hi;
+    kr.last_wexec = lw.x;
+    kr.maw = maw[k];
+    d.krec[k] = kr;
+    KeyEntry ke;
+    ke.last_txn = kr.last_txn;
+    ke.last_wexec = lw.x;
+    ke.last_w_txn = lw.y;
+    ke.pad = 0;
+    uint64_t base = 0;
+    for (int cl = 0; cl < NCLASS; ++cl)
+    {
+        ke.cl[cl].cand_lo = (uint32_t)(base + fs[cl * (ne + 1) + kr.seg_lo]);
+        ke.cl[cl].cand_hi = (uint32_t)(base + fs[cl * (ne + 1) + kr.seg_hi]);
+        ke.cl[cl].cwr_tail = has_w ? wtail[k] : cwr_lo;
+        ke.cl[cl].cwr_hi = cwr_hi;
+        base += ctl->tot[cl];
+    }
+    d.kent[k] = ke;
+}
+
+unsigned blocks(uint64_t n, unsigned t = 256) { return (unsigned)std::max<uint64_t>(1, (n + t - 1) / t); }
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DBuf() { if (p) (void)hipFree(p); }
+    bool ensure(size_t b, bool zero = false)
+    {
+        if (p && b <= cap) return true;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        b = std::max<size_t>(b, 64);
+        if (hipMalloc(&p, b) != hipSuccess) return false;
+        if (zero && hipMemset(p, 0, b) != hipSuccess) return false;
+        cap = b;
+        return true;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+}  // namespace
+
+struct CfkUpdWork {
+    DBuf ctl, loc, xr, word, bk, flags, fs, bsum, ck, cv, ck2, cv2, hist, hoff, f2, s2, maw, wtail;
+    UpdCtl* h_ctl = nullptr;
+    hipEvent_t ev[3] = {};
+    ~CfkUpdWork()
+    {
+        if (h_ctl) (void)hipHostFree(h_ctl);
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+CfkUpdWork* cfk_upd_work_create() { return new CfkUpdWork(); }
+void cfk_upd_work_destroy(CfkUpdWork* w) { delete w; }
+
+static uint32_t bytes_of(uint64_t v)
+{
+    uint32_t b = 0;
+    while (v) { ++b; v >>= 8; }
+    return b;
+}
+
+#define UCHK(expr)                                                                                \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess) { *err = std::string(#expr) + ": " + hipGetErrorString(_e); return AD_E_DEVICE; } \
+    } while (0)
+#define UALLOC(buf, bytes, zero)                                                                  \
+    do {                                                                                          \
+        if (!(buf).ensure((bytes), (zero))) { *err = "device allocation (cfk update)"; return AD_E_NOMEM; } \
+    } while (0)
+
+// Rebuild ent.tau, cand, cwr, w, krec, kent and the trees from the per-entry state (status,
+// executeAt rank). A duplicate committed executeAt is reported in ctl->err.
+static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkDerivedBufs* bufs,
+                      int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*), void* need_ctx, hipStream_t st,
+                      std::string* err)
+{
+    const uint64_t ne = s.n_ent, nk = s.n_keys;
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    const uint64_t sb = (std::max<uint64_t>(ne, 1) + 1023) / 1024 + 8;
+    UALLOC(w->flags, 4ull * 4 * std::max<uint64_t>(ne, 1), false);
+    UALLOC(w->fs, 8ull * 4 * (ne + 1), false);
+    UALLOC(w->bsum, 8ull * 4 * sb + 8 * (radix_hist_entries(ne) / 1024 + 8), false);
+    if (ne)
+    {
+        k_drv_flags<<<blocks(ne), 256, 0, st>>>(ne, dd, w->flags.as<uint32_t>());
+        UCHK(hipGetLastError());
+    }
+    UCHK(run_scan_arrays(w->flags.as<uint32_t>(), w->fs.as<uint64_t>(), ne, 4, w->bsum.as<uint64_t>(), st));
+    k_drv_totals<<<1, 64, 0, st>>>(w->fs.as<uint64_t>(), ne, 4, ctl->tot);
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    const uint64_t n_cand = w->h_ctl->tot[0] + w->h_ctl->tot[1] + w->h_ctl->tot[2], ncm = w->h_ctl->tot[3];
+    int rc = need(need_ctx, n_cand, ncm, ncm, bufs);
+    if (rc) return rc;
+    UALLOC(w->ck, 8 * std::max<uint64_t>(ncm, 1), false);
+    UALLOC(w->cv, 4 * std::max<uint64_t>(ncm, 1), false);
+    UALLOC(w->ck2, 8 * std::max<uint64_t>(ncm, 1), false);
+    UALLOC(w->cv2, 4 * std::max<uint64_t>(ncm, 1), false);
+    const uint64_t hist_n = radix_hist_entries(std::max<uint64_t>(ncm, 1));
+    UALLOC(w->hist, 4 * hist_n, false);
+    UALLOC(w->hoff, 8 * (hist_n + 1), false);
+    UALLOC(w->f2, 4ull * 2 * std::max<uint64_t>(ncm, 1), false);
+    UALLOC(w->s2, 8ull * 2 * (ncm + 1), false);
+    UALLOC(w->maw, 4 * std::max<uint64_t>(nk, 1), false);
+    UALLOC(w->wtail, 4 * std::max<uint64_t>(nk, 1), false);
+    const uint64_t sb2 = (std::max<uint64_t>(std::max(ncm, hist_n), 1) + 1023) / 1024 + 8;
+    UALLOC(w->bsum, 8ull * std::max<uint64_t>(4 * sb, 2 * sb2), false);
+    if (ne)
+        k_drv_scatter<<<blocks(ne), 256, 0, st>>>(ne, dd, w->fs.as<uint64_t>(), ctl, bufs->cand, w->ck.as<uint64_t>(),
+                                                  w->cv.as<uint32_t>());
+    uint64_t* ks = w->ck.as<uint64_t>();
+    uint32_t* vs = w->cv.as<uint32_t>();
+    if (ncm > 1)
+    {
+        uint32_t mask = 0;
+        const uint32_t xb = bytes_of(2 * s.n_dict + 1), kb = bytes_of(nk ? nk - 1 : 0);
+        for (uint32_t b = 0; b < xb && b < 4; ++b) mask |= 1u << b;
+        for (uint32_t b = 0; b < kb && b < 4; ++b) mask |= 1u << (4 + b);
+        UCHK(radix_sort_pairs(ks, vs, w->ck2.as<uint64_t>(), w->cv2.as<uint32_t>(), ncm, mask, w->hist.as<uint32_t>(),
+                              w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
+    }
+    if (ncm)
+    {
+        k_drv_committed<<<blocks(ncm), 256, 0, st>>>(ncm, ks, vs, dd, w->f2.as<uint32_t>(), ctl);
+        UCHK(hipGetLastError());
+    }
+    UCHK(run_scan_arrays(w->f2.as<uint32_t>(), w->s2.as<uint64_t>(), ncm, 2, w->bsum.as<uint64_t>(), st));
+    if (nk) UCHK(hipMemsetAsync(w->maw.p, 0xFF, 4 * nk, st));
+    if (ncm)
+        k_drv_emit<<<blocks(ncm), 256, 0, st>>>(ncm, ne, ks, vs, dd, w->fs.as<uint64_t>(), w->s2.as<uint64_t>(), bufs->cwr,
+                                                bufs->w, w->maw.as<int32_t>(), w->wtail.as<uint32_t>());
+    if (nk)
+        k_drv_keys<<<blocks(nk), 256, 0, st>>>(nk, ne, ncm, dd, w->fs.as<uint64_t>(), w->s2.as<uint64_t>(), bufs->w,
+                                               w->maw.as<int32_t>(), w->wtail.as<uint32_t>(), ctl);
+    UCHK(hipGetLastError());
+    s.cand = bufs->cand;
+    s.cwr = bufs->cwr;
+    s.w = bufs->w;
+    UCHK(build_cfk_trees(s, st));
+    return AD_OK;
+}
+
+int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
+                   int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*), void* need_ctx, hipStream_t st,
+                   CfkUpdOut* out, std::string* err)
+{
+    const uint64_t n = u.n, ne = s.n_ent;
+    *out = CfkUpdOut{};
+    if (n == 0) return AD_OK;
+    if (n >= 0xFFFFFFFFull) { *err = "more than 2^32-2 updates in one batch"; return AD_E_INVAL; }
+    if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
+    for (auto& e : w->ev)
+        if (!e) UCHK(hipEventCreate(&e));
+    UALLOC(w->ctl, sizeof(UpdCtl), false);
+    UALLOC(w->loc, 4 * n, false);
+    UALLOC(w->xr, 4 * n, false);
+    UALLOC(w->bk, 8 * n, false);
+    UALLOC(w->word, 8 * std::max<uint64_t>(ne, 1), true);   // zero between batches (winners clear theirs)
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    UCHK(hipEventRecord(w->ev[0], st));
+
+    // ---- 1. locate and validate; nothing changes unless the whole batch is valid
+    k_upd_locate<<<blocks(n), 256, 0, st>>>(s, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
+                                            w->word.as<unsigned long long>(), ctl);
+    UCHK(hipGetLastError());
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    auto describe = [&](uint32_t code, uint32_t idx) -> int {
+        char b[256];
+        const char* what = "";
+        int rc = AD_E_INVAL;
+        switch (code)
+        {
+            case UE_KEY: what = "key is not in the store's snapshot"; break;
+            case UE_STATUS: what = "status is not an InternalStatus ordinal"; break;
+            case UE_ABSENT: what = "txnId is not in the key's CommandsForKey (insertion needs a snapshot load)"; rc = AD_E_STATE; break;
+            case UE_NEW_EXEC: what = "executeAt is not an id of the snapshot (needs a snapshot load)"; rc = AD_E_STATE; break;
+            case UE_FLAGS: what = "id equal to a snapshot id differs in flag bits"; rc = AD_E_INCONSISTENT_ID; break;
+            case UE_DOMAIN: what = "live range-domain TxnId in a CommandsForKey"; break;
+            case UE_DUP_EXEC: what = "two committed entries of one key share an executeAt (CommandsForKey.java:1439)"; rc = AD_E_DUP_EXEC; break;
+        }
+        snprintf(b, sizeof(b), "cfk update %u: %s", idx, what);
+        *err = b;
+        return rc;
+    };
+    if (w->h_ctl->err)
+    {
+        k_upd_release<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->word.as<unsigned long long>());
+        UCHK(hipStreamSynchronize(st));
+        return describe(w->h_ctl->err, w->h_ctl->err_idx);
+    }
+    CfkDevState dd = d;
+    k_upd_apply<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(), w->word.as<unsigned long long>(),
+                                           dd, w->bk.as<uint2>(), ctl);
+    UCHK(hipGetLastError());
+    UCHK(hipEventRecord(w->ev[1], st));
+
+    // ---- 2. re-derive the snapshot arrays from the per-entry state
+    int rc = cfk_derive(w, s, dd, bufs, need, need_ctx, st, err);
+    if (rc) return rc;
+    UCHK(hipEventRecord(w->ev[2], st));
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
+    (void)hipEventElapsedTime(&b, w->ev[1], w->ev[2]);
+    out->ms_locate = a;
+    out->ms_derive = b;
+    out->ms_total = a + b;
+    out->n_applied = w->h_ctl->applied;
+    if (w->h_ctl->err)
+    {
+        // a duplicate committed executeAt: undo the batch and derive the previous state again
+        const int code = describe(w->h_ctl->err, w->h_ctl->err_idx);
+        k_upd_rollback<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->bk.as<uint2>(), dd);
+        UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+        std::string e2;
+        if ((rc = cfk_derive(w, s, dd, bufs, need, need_ctx, st, &e2))) { *err += "; rollback: " + e2; return rc; }
+        UCHK(hipStreamSynchronize(st));
+        out->n_applied = 0;
+        return code;
+    }
+    return AD_OK;
+}
+
+}  // namespace adx

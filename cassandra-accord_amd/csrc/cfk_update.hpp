@@ -1,0 +1,57 @@
+// cfk_update.hpp — SURVEY §8 f1: CommandsForKey.update applied to the device-resident snapshot
+// (cfk_update.hip). Host launch interface.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "common.hpp"
+
+namespace adx {
+
+// A batch of updates (device pointers; ad_cfk_update_soa).
+struct CfkUpdIn {
+    uint64_t n;
+    const int64_t* keys;
+    const uint64_t* txn_msb; const uint64_t* txn_lsb; const int32_t* txn_node;
+    const uint64_t* exec_msb; const uint64_t* exec_lsb; const int32_t* exec_node;
+    const uint8_t* status;
+};
+
+// Per-entry state kept on the device beside the derived snapshot (built by the ingest): the
+// InternalStatus and executeAt rank of every byId entry and the key index each entry belongs to.
+// The derived arrays (ent, cand, cwr, w, krec, kent, trees) are rebuilt from it after an update.
+struct CfkDevState {
+    uint8_t* status;               // [n_ent]
+    uint32_t* xrank;               // [n_ent] executeAt rank
+    const uint32_t* ekey;          // [n_ent] key index
+    const uint64_t* dict_lsb_raw;  // [n_dict] raw lsb of every dictionary id (flag-bit identity check)
+    // derived arrays rewritten in place (the snapshot's const views alias them)
+    uint2* ent; KeyRec* krec; KeyEntry* kent;
+};
+
+// Output buffers the derivation may grow: returned pointers replace the snapshot's views.
+struct CfkDerivedBufs {
+    uint32_t* cand; uint64_t cand_cap;
+    uint32_t* cwr; uint64_t cwr_cap;
+    uint2* w; uint64_t w_cap;
+};
+
+struct CfkUpdOut {
+    uint64_t n_applied = 0;        // updates that changed an entry
+    double ms_locate = 0, ms_derive = 0, ms_total = 0;
+};
+
+struct CfkUpdWork;
+CfkUpdWork* cfk_upd_work_create();
+void cfk_upd_work_destroy(CfkUpdWork* w);
+
+// Applies the batch (AD_E_* on failure with the store unchanged; message in *err).
+// `need` is called with the sizes the derived arrays need; it must return buffers at least that
+// large (possibly reallocated) in *bufs.
+int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
+                   int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                   hipStream_t st, CfkUpdOut* out, std::string* err);
+
+}  // namespace adx

@@ -441,6 +441,41 @@ int ad_recovery_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t scan, ad_deps
 /* Device buffers in and out, as ad_deps_batch_device (result valid until the next batch call). */
 int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t scan, void* stream, ad_deps_result* out);
 
+/* ---- device-resident CommandsForKey maintenance ----------------------------
+ * CommandsForKey.update (CommandsForKey.java:972-1042) for a batch of status transitions, applied to
+ * the snapshot in HBM (no host ingest, no re-upload). Update i raises the byId entry of txnId i in
+ * the CommandsForKey of keys[i] to InternalStatus status[i] with executeAt i: the entry changes iff
+ * the new status is above its current one (:1012-1027; equal status with a higher ballot is not
+ * carried: "not above"); updates of one entry apply in batch order. committedByExecuteAt,
+ * maxAppliedWriteByExecuteAt and every derived device array follow (:642-681).
+ * The caller filters what the Java drops before the search (txnId < shardRedundantBefore, :995).
+ * Errors (nothing applied): AD_E_INVAL (key not in the snapshot, status > 7, live range-domain id),
+ * AD_E_STATE (txnId not in the key's byId, or an executeAt that is no id of the snapshot: inserting
+ * new ids needs ad_cfk_load), AD_E_INCONSISTENT_ID, AD_E_DUP_EXEC (two committed entries of a key
+ * with one executeAt, :1439). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
+ * follow on demand. */
+typedef struct ad_cfk_update_soa {
+    uint64_t n;
+    const int64_t*  keys;
+    const uint64_t* txn_msb;
+    const uint64_t* txn_lsb;
+    const int32_t*  txn_node;
+    const uint64_t* exec_msb;
+    const uint64_t* exec_lsb;
+    const int32_t*  exec_node;
+    const uint8_t*  status;          /* AD_ST_* = InternalStatus.from(command.saveStatus()) */
+} ad_cfk_update_soa;
+
+/* Host buffers (staged to the device). n_applied (may be null): updates that changed an entry;
+ * stats (may be null): ms_stage[0] locate+apply, ms_stage[1] re-derivation, ms_device total. */
+int ad_cfk_update(ad_ctx* ctx, const ad_cfk_update_soa* u, uint64_t* n_applied, ad_stats* stats);
+/* Device buffers, on `stream` (null: the context's stream). Synchronous on return. */
+int ad_cfk_update_device(ad_ctx* ctx, const ad_cfk_update_soa* u_dev, void* stream, uint64_t* n_applied, ad_stats* stats);
+/* The store's entries as they stand (load order): status and executeAt per entry. Views owned by
+ * the context, valid until its next call. */
+int ad_cfk_entries(ad_ctx* ctx, uint64_t* n_entries, const uint8_t** status, const uint64_t** exec_msb,
+                   const uint64_t** exec_lsb, const int32_t** exec_node);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,88 @@
+"""The CommandsForKey.update restatement (oracle/cfk_update.py) on known answers
+derived from CommandsForKey.java:992-1042: raise only above the current status, batch order,
+insertion at the binarySearch position (with prunedBefore following), new keys."""
+import os
+import sys
+
+import numpy as np
+
+from accord_deps import _abi as A, synth
+from accord_deps.model import CfkSnapshot, CfkUpdates, Tids, make_txn_ids
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import cfk_update as U  # noqa: E402
+
+
+def _store():
+    # key 10: txns hlc 100 (Write, PREACCEPTED), 200 (Read, COMMITTED); key 20: hlc 150 (Write, APPLIED)
+    txn = make_txn_ids(1, [100, 200, 150], [A.KIND_WRITE, A.KIND_READ, A.KIND_WRITE], 1)
+    return CfkSnapshot(np.array([10, 20]), np.array([0, 2, 3]), txn, txn,
+                       np.array([A.ST_PREACCEPTED, A.ST_COMMITTED, A.ST_APPLIED]), np.array([1, -1]))
+
+
+def _upd(keys, hlcs, kinds, statuses, exec_hlcs=None):
+    t = make_txn_ids(1, hlcs, kinds, 1)
+    x = t if exec_hlcs is None else make_txn_ids(1, exec_hlcs, kinds, 1)
+    return CfkUpdates(np.array(keys), t, x, np.array(statuses))
+
+
+def test_raise_skip_and_order():
+    c = _store()
+    # raise 100 to COMMITTED (exec 300), then a lower ACCEPTED (skipped), then STABLE (raises again);
+    # 200 stays COMMITTED under an equal COMMITTED
+    u = _upd([10, 10, 10, 10], [100, 100, 100, 200], [1, 1, 1, 0],
+             [A.ST_COMMITTED, A.ST_ACCEPTED, A.ST_STABLE, A.ST_COMMITTED], [300, 300, 310, 999])
+    n, applied = U.cfk_update(c, u)
+    assert applied == 2
+    assert n.status.tolist() == [A.ST_STABLE, A.ST_COMMITTED, A.ST_APPLIED]
+    assert int(n.exec.lsb[0]) >> 16 == 310 and int(n.exec.lsb[1]) >> 16 == 200
+    assert n.seg.tolist() == c.seg.tolist()
+
+
+def test_insert_position_and_pruned():
+    c = _store()
+    # 50 goes before byId[0] of key 10 (prunedBefore index 1 -> 2), 250 after; 30 is a new key
+    u = _upd([10, 10, 30, 10], [250, 50, 400, 50], [1, 0, 1, 0],
+             [A.ST_PREACCEPTED, A.ST_TRANSITIVELY_KNOWN, A.ST_ACCEPTED, A.ST_PREACCEPTED])
+    n, applied = U.cfk_update(c, u)
+    assert applied == 4        # 50 inserted, then raised to PREACCEPTED
+    assert n.keys.tolist() == [10, 20, 30]
+    assert n.seg.tolist() == [0, 4, 5, 6]
+    assert [int(x) >> 16 for x in n.txn.lsb] == [50, 100, 200, 250, 150, 400]
+    assert n.status.tolist() == [A.ST_PREACCEPTED, A.ST_PREACCEPTED, A.ST_COMMITTED, A.ST_PREACCEPTED,
+                                 A.ST_APPLIED, A.ST_ACCEPTED]
+    assert n.pruned_before.tolist() == [2, -1, -1]
+
+
+def test_identity_is_timestamp_equals():
+    # an id equal under Timestamp.equals (same msb, hlc, identity flags, node) finds the entry
+    c = _store()
+    t = make_txn_ids(1, [100], [A.KIND_WRITE], 1)
+    u = CfkUpdates(np.array([10]), t, t, np.array([A.ST_ACCEPTED]))
+    n, applied = U.cfk_update(c, u)
+    assert applied == 1 and n.n_entries == 3 and n.status[0] == A.ST_ACCEPTED
+
+
+def test_random_transitions_match_a_per_entry_model():
+    # independent model: for every entry, the first update of the highest status above its own
+    import cfk_update_gen as G
+    for seed in range(6):
+        w = synth.random_small(seed)
+        rng = np.random.default_rng(seed)
+        u, e = G.transitions(w.cfk, rng, 80)
+        n, applied = U.cfk_update(w.cfk, u)
+        exp_st = w.cfk.status.copy()
+        exp_x = w.cfk.exec.lsb.copy()
+        best = {}
+        for i, ent in enumerate(e.tolist()):
+            if ent not in best or u.status[i] > u.status[best[ent]]:
+                best[ent] = i
+        cnt = 0
+        for ent, i in best.items():
+            if u.status[i] > exp_st[ent]:
+                exp_st[ent] = u.status[i]
+                exp_x[ent] = u.exec.lsb[i]
+                cnt += 1
+        assert n.status.tolist() == exp_st.tolist()
+        assert n.exec.lsb.tolist() == exp_x.tolist()
+        assert applied >= cnt

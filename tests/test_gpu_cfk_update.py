@@ -1,0 +1,189 @@
+"""GPU parity of device-resident CommandsForKey maintenance: ad_cfk_update applies
+a batch of CommandsForKey.update status transitions to the snapshot in HBM (k_upd_locate,
+k_upd_apply, re-derivation of ent / committedByExecuteAt / cand / cwr / krec / KeyEntry / trees).
+Checked against the oracle's restatement (oracle/cfk_update.py): the entries' status and
+executeAt, and the deps every later batch computes (bit-exact vs the oracle's calculatePartialDeps
+over the updated CommandsForKey) on the lean, general and split paths; error batches leave the
+store unchanged."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from accord_deps import _abi as A, native, synth
+from accord_deps.model import CfkUpdates, Tids
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import cfk_update as U  # noqa: E402
+import cfk_update_gen as G  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(w, st, oracle, new_cfk):
+    s, x = st.cfk_entries()
+    assert s.tolist() == new_cfk.status.tolist()
+    assert x.msb.tolist() == new_cfk.exec.msb.tolist() and x.lsb.tolist() == new_cfk.exec.lsb.tolist()
+    assert x.node.tolist() == new_cfk.exec.node.tolist()
+    w2 = w
+    old = w2.cfk
+    w2.cfk = new_cfk
+    try:
+        exp = oracle.resolve(w2)
+        got = st.calculate_partial_deps(w2.queries, w2.flags)
+        ok, why = got.equals(exp, detail=True)
+        assert ok, why
+    finally:
+        w2.cfk = old
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("seed", range(8))
+def test_random_transitions(oracle, seed, path):
+    w = synth.random_small(seed, with_slices=(seed % 4 == 3), start_inclusive=(seed % 3 == 1))
+    w.flags = A.AD_SNAPSHOT
+    rng = np.random.default_rng(100 + seed)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices, path=path)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        for rnd in range(3):                     # successive batches on the same device state
+            u, e = G.transitions(cfk, rng, 60 + 30 * rnd)
+            new, _ = U.cfk_update(cfk, u)
+            n_applied, _ = st.cfk_update(u)
+            assert n_applied == int((new.status != cfk.status).sum())
+            _check(w, st, oracle, new)
+            cfk = new
+    finally:
+        st.close()
+
+
+def test_update_then_reload_equals_fresh_load(oracle):
+    # the derived device state after updates answers exactly as a store loaded from the updated SoA
+    w = synth.random_small(31, n_hist_txns=300, n_txns=120)
+    w.flags = A.AD_SNAPSHOT
+    rng = np.random.default_rng(31)
+    u, _ = G.transitions(w.cfk, rng, 400)
+    new, _ = U.cfk_update(w.cfk, u)
+    a = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    b = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        a.load(w)
+        a.cfk_update(u)
+        old = w.cfk
+        w.cfk = new
+        b.load(w)
+        ra, rb = a.calculate_partial_deps(w.queries), b.calculate_partial_deps(w.queries)
+        w.cfk = old
+        ok, why = ra.equals(rb, detail=True)
+        assert ok, why
+    finally:
+        a.close()
+        b.close()
+
+
+def test_config2_scaled_commit_wave(oracle):
+    # config 2's shape: the unapplied tail of every key commits (executeAt = txnId or its own), then applies
+    w = synth.config2(n_txns=2000, n_keys=2000, n_hist_entries=40000, seed=9)
+    live = np.nonzero(w.cfk.status < A.ST_APPLIED)[0]
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        keys = G.entry_keys(cfk)
+        for target in (A.ST_COMMITTED, A.ST_APPLIED):
+            u = CfkUpdates(keys[live], cfk.txn.take(live), cfk.exec.take(live), np.full(len(live), target, np.uint8))
+            new, _ = U.cfk_update(cfk, u)
+            st.cfk_update(u)
+            _check(w, st, oracle, new)
+            cfk = new
+    finally:
+        st.close()
+
+
+def test_device_buffers_and_recovery_follow(oracle):
+    import torch
+    w = synth.recovery_workload(4)
+    rng = np.random.default_rng(4)
+    u, _ = G.transitions(w.cfk, rng, 100)
+    new, _ = U.cfk_update(w.cfk, u)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        dev = torch.device("cuda", 0)
+        ud, keep = native.device_updates(u, dev)
+        st.cfk_update_device(ud, torch.cuda.current_stream(dev).cuda_stream)
+        old = w.cfk
+        w.cfk = new
+        new.miss_off, new.miss = old.miss_off, old.miss        # entries did not move: missing() lists hold
+        try:
+            for s in A.RECOVER_SCANS:
+                ok, why = st.recovery_scan(w.queries, s).equals(oracle.recover(w, s), detail=True)
+                assert ok, "scan %d: %s" % (s, why)
+        finally:
+            w.cfk = old
+    finally:
+        st.close()
+
+
+def _unchanged_after_error(w, st, oracle, u, code):
+    before = st.calculate_partial_deps(w.queries, w.flags)
+    with pytest.raises(native.AccordDepsError) as ei:
+        st.cfk_update(u)
+    assert ei.value.code == code
+    s, x = st.cfk_entries()
+    assert s.tolist() == w.cfk.status.tolist() and x.lsb.tolist() == w.cfk.exec.lsb.tolist()
+    ok, why = st.calculate_partial_deps(w.queries, w.flags).equals(before, detail=True)
+    assert ok, why
+
+
+def test_errors_leave_store_unchanged(oracle):
+    w = synth.random_small(7)
+    w.flags = A.AD_SNAPSHOT
+    rng = np.random.default_rng(7)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        u, _ = G.transitions(w.cfk, rng, 30, statuses=[A.ST_STABLE])
+        bad_key = CfkUpdates(u.keys.copy(), u.txn, u.exec, u.status)
+        bad_key.keys[5] = 10 ** 9
+        _unchanged_after_error(w, st, oracle, bad_key, A.AD_E_INVAL)
+        # a txnId the key does not hold (insertion): not on the device yet
+        t = Tids(u.txn.msb.copy(), u.txn.lsb.copy(), u.txn.node.copy())
+        t.node[3] = 999
+        _unchanged_after_error(w, st, oracle, CfkUpdates(u.keys, t, u.exec, u.status), A.AD_E_STATE)
+        # an executeAt no entry carries
+        x = Tids(u.exec.msb.copy(), u.exec.lsb.copy(), u.exec.node.copy())
+        x.node[2] = 12345
+        _unchanged_after_error(w, st, oracle, CfkUpdates(u.keys, u.txn, x, u.status), A.AD_E_STATE)
+        bad_st = CfkUpdates(u.keys, u.txn, u.exec, u.status.copy())
+        bad_st.status[0] = 9
+        _unchanged_after_error(w, st, oracle, bad_st, A.AD_E_INVAL)
+        # two entries of one key committed at one executeAt (CommandsForKey.java:1439): rolled back
+        seg = w.cfk.seg.astype(np.int64)
+        k = int(np.argmax(np.diff(seg)))
+        kd = [e for e in range(int(seg[k]), int(seg[k + 1])) if (int(w.cfk.txn.lsb[e]) & 1) == 0]
+        e0, e1 = kd[0], kd[1]
+        dup = CfkUpdates(np.array([w.cfk.keys[k]] * 2), w.cfk.txn.take([e0, e1]),
+                         w.cfk.txn.take([e0, e0]), np.array([A.ST_APPLIED, A.ST_APPLIED]))
+        new, _ = U.cfk_update(w.cfk, dup)
+        assert U.dup_committed_exec(new)
+        _unchanged_after_error(w, st, oracle, dup, A.AD_E_DUP_EXEC)
+        # and the store still takes a good batch afterwards
+        new, _ = U.cfk_update(w.cfk, u)
+        st.cfk_update(u)
+        _check(w, st, oracle, new)
+    finally:
+        st.close()
+
+
+def test_empty_batch_and_sequential_follows(oracle):
+    w = synth.config1(n_txns=300, n_keys=50)
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        assert st.cfk_update(CfkUpdates(np.zeros(0, np.int64), Tids(np.zeros(0), np.zeros(0), np.zeros(0)),
+                                        Tids(np.zeros(0), np.zeros(0), np.zeros(0)), np.zeros(0, np.uint8)))[0] == 0
+    finally:
+        st.close()
