@@ -789,6 +789,12 @@ static int sync_host(ad_ctx* c)
             K.exec[e] = {c->dict_msb[i], c->dict_lsb[i], c->dict_node[i]};
         }
     c->h_exec_rank.swap(xr);
+    // TxnInfo.missing() exists only for ACCEPTED..APPLIED (CommandsForKey.java:278): an entry that
+    // left that range through an update needs its lists loaded again
+    if (!K.miss_off.empty())
+        for (uint64_t e = 0; e < ne && !K.miss_stale; ++e)
+            if (K.miss_off[e + 1] > K.miss_off[e] && !(K.status[e] >= AD_ST_ACCEPTED && K.status[e] <= AD_ST_APPLIED))
+                K.miss_stale = true;
     c->host_stale = false;
     return 0;
 }
@@ -1100,7 +1106,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         if (h.error)
         {
             if (h.error == ERR_STATE)
-                return c->fail(AD_E_STATE, "reference would throw: prunedBefore set but no applied Write (CommandsForKey.java:962)");
+                return c->fail(AD_E_STATE, "reference would throw: prunedBefore set but no committed Write to substitute (CommandsForKey.java:955-962)");
             return c->fail(AD_E_INVAL, recovery_scan >= 0 ? "invalid Txn.Kind for witnessedBy() in a request (Txn.java:247-262)"
                                                           : "invalid Txn.Kind for witnesses() in a request (Txn.java:221-235)");
         }

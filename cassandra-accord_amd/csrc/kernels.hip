@@ -280,10 +280,12 @@ __global__ __launch_bounds__(256) void k_scan(DevSnapshot s, BatchBufs b)
         uint32_t extra = 0;
         if (kr.pruned != 0 && S <= kr.pruned)
         {
-            if (kr.maw < 0) { if (lane == 0) set_error(b.ctl, ERR_STATE); }
+            // no applied Write: binarySearch(committedByExecuteAt, 0, -1, S) = -1, the walk starts
+            // at the first committed entry (:955-962); no committed Write at all throws
+            if (kr.maw < 0 && whi == wlo) { if (lane == 0) set_error(b.ctl, ERR_STATE); }
             else
             {
-                const uint64_t idx = wpos <= (uint64_t)kr.maw ? wpos : (uint64_t)kr.maw;
+                const uint64_t idx = kr.maw < 0 ? wlo : (wpos <= (uint64_t)kr.maw ? wpos : (uint64_t)kr.maw);
                 extra = s.w[idx].y;
                 if (extra == self) extra = 0;                      // map lambda, PreAccept.java:258
             }

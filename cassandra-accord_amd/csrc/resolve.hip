@@ -401,10 +401,12 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         uint32_t extra = 0;
         if (has_cfk && kr.pruned != 0 && S <= kr.pruned)
         {
-            if (kr.maw < 0) { if (j == 0) set_error_f(b.ctl, ERR_STATE); }
+            // no applied Write: binarySearch(committedByExecuteAt, 0, -1, S) = -1, the walk starts
+            // at the first committed entry (:955-962); no committed Write at all throws
+            if (kr.maw < 0 && whi == wlo) { if (j == 0) set_error_f(b.ctl, ERR_STATE); }
             else
             {
-                const uint64_t idx = wpos <= (uint64_t)kr.maw ? wpos : (uint64_t)kr.maw;
+                const uint64_t idx = kr.maw < 0 ? wlo : (wpos <= (uint64_t)kr.maw ? wpos : (uint64_t)kr.maw);
                 extra = s.w[idx].y;
                 if (extra == self) extra = 0;
             }

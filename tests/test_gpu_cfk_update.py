@@ -106,7 +106,8 @@ def test_device_buffers_and_recovery_follow(oracle):
     import torch
     w = synth.recovery_workload(4)
     rng = np.random.default_rng(4)
-    u, _ = G.transitions(w.cfk, rng, 100)
+    # statuses that keep TxnInfo.missing() (ACCEPTED..APPLIED, CommandsForKey.java:278)
+    u, _ = G.transitions(w.cfk, rng, 100, statuses=range(A.ST_ACCEPTED, A.ST_APPLIED + 1))
     new, _ = U.cfk_update(w.cfk, u)
     st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
     try:
@@ -123,6 +124,14 @@ def test_device_buffers_and_recovery_follow(oracle):
                 assert ok, "scan %d: %s" % (s, why)
         finally:
             w.cfk = old
+        # an entry with missing() ids invalidated: the lists must be loaded again
+        e = int(np.nonzero(np.diff(w.cfk.miss_off.astype(np.int64)) > 0)[0][0])
+        inv = CfkUpdates(G.entry_keys(w.cfk)[[e]], w.cfk.txn.take([e]), w.cfk.txn.take([e]),
+                         np.array([A.ST_INVALID], np.uint8))
+        st.cfk_update(inv)
+        with pytest.raises(native.AccordDepsError) as ei:
+            st.recovery_scan(w.queries, 0)
+        assert ei.value.code == A.AD_E_STATE
     finally:
         st.close()
 
