@@ -527,6 +527,94 @@ def bench_recovery(args, rank, world, local, dev):
         dist.destroy_process_group()
 
 
+def bench_cfk_update(args, rank, world, local, dev):
+    """SURVEY §8 f1 on config 2's snapshot: a step is one batch of N CommandsForKey.update status
+    transitions applied to the device-resident snapshot (ad_cfk_update_device: locate + apply +
+    re-derivation of every derived array). Batch b raises a random N-subset of the entries that are
+    not APPLIED by one status (PREACCEPTED -> ACCEPTED -> COMMITTED -> STABLE -> APPLIED, executeAt
+    kept), so every step changes the store. It replaces a host re-ingest + re-upload of the snapshot
+    (ingest_ms). With N GPUs, N independent replicas."""
+    s = args.scale
+    w = synth.config2(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_hist_entries=int(16_000_000 * s),
+                      seed=0xACC0D002 + rank)
+    cfk = w.cfk
+    from accord_deps.model import CfkUpdates
+    n = max(1, int(args.cfk_update * s))
+    rng = np.random.default_rng(0xACC0D01F)
+    key_of = np.repeat(cfk.keys, np.diff(cfk.seg.astype(np.int64)))
+    status = cfk.status.copy()
+    batches = []
+    for b in range(args.warmup + args.steps):
+        live = np.nonzero(status < A.ST_APPLIED)[0]
+        e = np.sort(rng.choice(live, min(n, len(live)), replace=False)) if len(live) else np.zeros(0, np.int64)
+        st = np.maximum(status[e] + 1, A.ST_ACCEPTED).astype(np.uint8)
+        status[e] = st
+        u = CfkUpdates(key_of[e], cfk.txn.take(e), cfk.exec.take(e), st)
+        batches.append((u,) + native.device_updates(u, dev))
+    store = native.DeviceCommandStore(device=local)
+    t0 = time.time()
+    store.load(w)
+    ingest_ms = 1000 * (time.time() - t0)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    it = iter(batches)
+
+    def step():
+        b = next(it)
+        applied, stt = store.cfk_update_device(b[1], sp)
+        stt["applied"] = applied
+        return stt
+    elapsed, all_stats = _timed_steps(args, world, dev, step)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    upd = _sum_over_ranks(world, dev, sum(len(batches[args.warmup + i][0]) for i in range(args.steps)))
+    # algorithmic bytes of one launch sequence: the update batch (49 B each) + per entry the state
+    # read (status 1 + executeAt rank 4 + ent 8 + key index 4) and tau written (4) + the derived
+    # lists written (cand 4 B per never-elided class entry, cwr 4 B, w 8 B per committed Write) and
+    # the committed entries' (key, executeAt) sort (12 B written and read once) + per key krec 32 +
+    # KeyEntry 64
+    ne, nk = cfk.n_entries, len(cfk.keys)
+    kinds = cfk.txn.kind()
+    comm = (status >= A.ST_COMMITTED) & (status <= A.ST_APPLIED)
+    rw = (kinds <= A.KIND_WRITE)
+    never = (status != A.ST_TRANSITIVELY_KNOWN) & (status != A.ST_INVALID) & ~(comm & rw)
+    n_cand = int(never.sum()) * 3
+    alg = 49 * n + 21 * ne + 4 * n_cand + 4 * int((comm & rw).sum()) + 8 * int((comm & (kinds == A.KIND_WRITE)).sum()) \
+        + 24 * int(comm.sum()) + 96 * nk
+    ms_dev = float(np.mean([x["ms_device"] for x in all_stats]))
+    achieved = alg / (ms_dev / 1000.0) / 1e9 if ms_dev > 0 else 0.0
+    res = {
+        "metric": "CommandsForKey.update on the device-resident snapshot: updates/sec", "value": upd / (ms_per_step / 1000.0),
+        "unit": "updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "config2 snapshot (%d entries, %d keys), %d status transitions per batch (SURVEY 8 f1)"
+                               % (ne, nk, n), "parallelism": "replicas x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_upd_* + k_drv_* + radix sort + trees", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": alg, "launch_ms": ms_dev},
+        "stages_ms": {"locate+apply": round(float(np.mean([x["ms_stage"][0] for x in all_stats])), 4),
+                      "re-derivation": round(float(np.mean([x["ms_stage"][1] for x in all_stats])), 4)},
+        "applied": [x["applied"] for x in all_stats],
+        "ingest_ms": ingest_ms,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cfk_update as U
+        u0 = batches[0][0]
+        done = min(len(u0), 100_000)
+        sub = CfkUpdates(u0.keys[:done], u0.txn.take(np.arange(done)), u0.exec.take(np.arange(done)), u0.status[:done])
+        t0 = time.perf_counter()
+        U.cfk_update(cfk, sub)
+        t = time.perf_counter() - t0
+        res["cpu_baseline"] = dict(value=done / t, unit="updates/s", cores=1, kind="port",
+                                   sample="first %d of %d updates of the first batch (%.1f s), oracle/cfk_update.py "
+                                          "(CommandsForKey.update restatement: binarySearch + raise), 1 thread"
+                                          % (done, len(u0), t))
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    store.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def bench_sequential(args, rank, world, local, dev):
     """Config 1: 10k txns x 4 keys over 1k keys, one CommandStore, SEQUENTIAL PreAccept (each txn
     inserted as PREACCEPTED before its deps). SEQUENTIAL runs through the host API: a step is one
@@ -590,6 +678,8 @@ def main():
                     help="with config 2: the PreAccept timestamp proposal (SURVEY 8 f3) instead of deps")
     ap.add_argument("--recovery", type=int, default=0, metavar="N",
                     help="with config 2: BeginRecovery scans for N recovering txns on the config-2 snapshot (SURVEY 8 f4)")
+    ap.add_argument("--cfk-update", type=int, default=0, metavar="N",
+                    help="with config 2: batches of N CommandsForKey.update status transitions on the device (SURVEY 8 f1)")
     ap.add_argument("--recovery-scan", type=int, default=3, choices=(0, 1, 2, 3), help="AD_RECOVER_* scan of --recovery")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank: the measured configuration); gloo: rehearsal of the "
@@ -625,6 +715,8 @@ def main():
         return bench_union(args, rank, world, local, dev)
     if args.recovery:
         return bench_recovery(args, rank, world, local, dev)
+    if args.cfk_update:
+        return bench_cfk_update(args, rank, world, local, dev)
 
     s = args.scale
     t0 = time.time()

@@ -217,6 +217,7 @@ __global__ __launch_bounds__(256) void k_drv_committed(uint64_t ncm, const uint6
     const uint32_t kind = d.ent[cv[i]].y >> RANK_BITS;
     f2[i] = (KINDS_RS_OR_WS >> kind) & 1u;
     f2[ncm + i] = kind == AD_KIND_WRITE ? 1u : 0u;
+    f2[2 * ncm + i] = (kind == AD_KIND_WRITE && d.status[cv[i]] == AD_ST_APPLIED) ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(256) void k_drv_emit(uint64_t ncm, uint64_t ne, const uint64_t* ck, const uint32_t* cv,
@@ -232,9 +233,10 @@ __global__ __launch_bounds__(256) void k_drv_emit(uint64_t ncm, uint64_t ne, con
     const uint64_t p = s2[(ncm + 1) + i];
     const uint32_t k = (uint32_t)(ck[i] >> 32);
     w[p] = make_uint2((uint32_t)ck[i], y & RANK_MASK);
-    if (d.status[e] == AD_ST_APPLIED) atomicMax(maw + k, (int32_t)p);
     const uint64_t cm_hi = fs[3 * (ne + 1) + d.krec[k].seg_hi];
     if (p + 1 == s2[(ncm + 1) + cm_hi]) wtail[k] = (uint32_t)s2[i];     // the key's last Write: its cwr index
+    // maxAppliedWriteByExecuteAt: the key's last APPLIED Write (no atomics: hot keys hold ~10^6)
+    if (d.status[e] == AD_ST_APPLIED && s2[2 * (ncm + 1) + i] + 1 == s2[2 * (ncm + 1) + cm_hi]) maw[k] = (int32_t)p;
 }
 
 __global__ __launch_bounds__(256) void k_drv_keys(uint64_t nk, uint64_t ne, uint64_t ncm, CfkDevState d, const uint64_t* fs,
@@ -357,12 +359,12 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
     const uint64_t hist_n = radix_hist_entries(std::max<uint64_t>(ncm, 1));
     UALLOC(w->hist, 4 * hist_n, false);
     UALLOC(w->hoff, 8 * (hist_n + 1), false);
-    UALLOC(w->f2, 4ull * 2 * std::max<uint64_t>(ncm, 1), false);
-    UALLOC(w->s2, 8ull * 2 * (ncm + 1), false);
+    UALLOC(w->f2, 4ull * 3 * std::max<uint64_t>(ncm, 1), false);
+    UALLOC(w->s2, 8ull * 3 * (ncm + 1), false);
     UALLOC(w->maw, 4 * std::max<uint64_t>(nk, 1), false);
     UALLOC(w->wtail, 4 * std::max<uint64_t>(nk, 1), false);
     const uint64_t sb2 = (std::max<uint64_t>(std::max(ncm, hist_n), 1) + 1023) / 1024 + 8;
-    UALLOC(w->bsum, 8ull * std::max<uint64_t>(4 * sb, 2 * sb2), false);
+    UALLOC(w->bsum, 8ull * std::max<uint64_t>(4 * sb, 3 * sb2), false);
     if (ne)
         k_drv_scatter<<<blocks(ne), 256, 0, st>>>(ne, dd, w->fs.as<uint64_t>(), ctl, bufs->cand, w->ck.as<uint64_t>(),
                                                   w->cv.as<uint32_t>());
@@ -382,7 +384,7 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
         k_drv_committed<<<blocks(ncm), 256, 0, st>>>(ncm, ks, vs, dd, w->f2.as<uint32_t>(), ctl);
         UCHK(hipGetLastError());
     }
-    UCHK(run_scan_arrays(w->f2.as<uint32_t>(), w->s2.as<uint64_t>(), ncm, 2, w->bsum.as<uint64_t>(), st));
+    UCHK(run_scan_arrays(w->f2.as<uint32_t>(), w->s2.as<uint64_t>(), ncm, 3, w->bsum.as<uint64_t>(), st));
     if (nk) UCHK(hipMemsetAsync(w->maw.p, 0xFF, 4 * nk, st));
     if (ncm)
         k_drv_emit<<<blocks(ncm), 256, 0, st>>>(ncm, ne, ks, vs, dd, w->fs.as<uint64_t>(), w->s2.as<uint64_t>(), bufs->cwr,
