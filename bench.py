@@ -823,6 +823,13 @@ def main():
     if world > 1:
         out["stages_ms"]["merge (K3, owner)"] = round(merge_ms, 4)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the PCIe-inclusive rate a host caller sees through ad_deps_batch (host arrays in, packed
+        # host CSR arrays out; outside the timed region, never `value`)
+        store.deps_batch_stats(w.queries)
+        t0 = time.perf_counter()
+        store.deps_batch_stats(w.queries)
+        host_ms = 1000.0 * (time.perf_counter() - t0)
+        out["host_api"] = {"ms_per_batch": host_ms, "pairs_per_s": w.queries.n_probes / (host_ms / 1000.0)}
         out["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
