@@ -244,6 +244,8 @@ struct ad_ctx {
     // rank and key index; host copies (cfk.status / cfk.exec / h_exec_rank) are refreshed from
     // them on demand (host_stale)
     DevBuf d_status, d_xrank, d_ekey;
+    DevBuf d_ent2, d_status2, d_xrank2, d_ekey2;    // spare per-entry arrays (insertions)
+    bool host_moved = false;                         // entries were inserted on the device
     DevBuf u_k, u_tm, u_tl, u_tn, u_em, u_el, u_en, u_st;
     CfkUpdWork* cu = nullptr;
     bool host_stale = false;
@@ -774,6 +776,43 @@ static int sync_host(ad_ctx* c)
 {
     if (!c->host_stale) return 0;
     auto& K = c->cfk;
+    if (c->host_moved)
+    {
+        // entries were inserted: rebuild the host copies (byId ids from their ranks) from the device
+        const uint64_t ne = c->ds.n_ent, nk = c->ds.n_keys;
+        std::vector<uint2> ent(ne);
+        std::vector<KeyRec> kr(nk);
+        K.status.resize(ne);
+        std::vector<uint32_t> xr(ne);
+        if (ne)
+        {
+            HIPCHK(c, hipMemcpyAsync(ent.data(), c->d_ent.p, 8 * ne, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(K.status.data(), c->d_status.p, ne, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipMemcpyAsync(xr.data(), c->d_xrank.p, 4 * ne, hipMemcpyDeviceToHost, c->stream));
+        }
+        if (nk) HIPCHK(c, hipMemcpyAsync(kr.data(), c->d_krec.p, sizeof(KeyRec) * nk, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        auto tid = [&](uint32_t rank) -> Tid {
+            const uint64_t i = (rank - 1) / 2;
+            return Tid{c->dict_msb[i], c->dict_lsb[i], c->dict_node[i]};
+        };
+        K.txn.resize(ne);
+        K.exec.resize(ne);
+        c->h_txn_rank.resize(ne);
+        for (uint64_t e = 0; e < ne; ++e)
+        {
+            const uint32_t tr = ent[e].y & RANK_MASK;
+            c->h_txn_rank[e] = tr;
+            K.txn[e] = tid(tr);
+            K.exec[e] = xr[e] == tr ? K.txn[e] : tid(xr[e]);
+        }
+        for (uint64_t k = 0; k < nk; ++k) K.seg[k + 1] = kr[k].seg_hi;
+        c->h_exec_rank.swap(xr);
+        if (!K.miss_off.empty()) K.miss_stale = true;       // entries moved: load the lists again
+        c->host_moved = false;
+        c->host_stale = false;
+        return 0;
+    }
     const uint64_t ne = K.status.size();
     std::vector<uint32_t> xr(ne);
     if (ne)
@@ -1489,6 +1528,8 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
 
 int ad_cfk_missing_load(ad_ctx* c, const ad_cfk_missing_soa* m)
 {
+    if (c && c->host_stale)
+        if (int rc0 = sync_host(c)) return rc0;
     if (!c || !m) return AD_E_INVAL;
     auto& K = c->cfk;
     if (!K.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
@@ -2006,6 +2047,89 @@ static int cfk_need_bufs(void* vc, uint64_t n_cand, uint64_t n_cwr, uint64_t n_w
     return 0;
 }
 
+// DevBuf growth keeping the first `keep` bytes (slack for the next batches)
+static bool grow_keep(DevBuf& b, size_t keep, size_t need)
+{
+    if (b.p && need <= b.cap) return true;
+    void* p = nullptr;
+    const size_t cap = std::max<size_t>(need + need / 2, 64);
+    if (hipMalloc(&p, cap) != hipSuccess) return false;
+    if (keep && hipMemcpy(p, b.p, keep, hipMemcpyDeviceToDevice) != hipSuccess) { (void)hipFree(p); return false; }
+    b.release();
+    b.p = p;
+    b.cap = cap;
+    return true;
+}
+
+static int cfk_grow_dict(void* vc, uint64_t n_old, uint64_t n_new, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    if (!grow_keep(c->d_dict_hi, 8 * n_old, 8 * n_new) || !grow_keep(c->d_dict_lo, 8 * n_old, 8 * n_new) ||
+        !grow_keep(c->d_dict_node, 4 * n_old, 4 * n_new) || !grow_keep(c->d_dict_lsb_raw, 8 * n_old, 8 * n_new))
+        return AD_E_NOMEM;
+    *hi = c->d_dict_hi.as<uint64_t>();
+    *lo = c->d_dict_lo.as<uint64_t>();
+    *node = c->d_dict_node.as<int32_t>();
+    *raw = c->d_dict_lsb_raw.as<uint64_t>();
+    return 0;
+}
+
+static int cfk_grow_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    const uint64_t padded = std::max<uint64_t>(64, (ne + 63) / 64 * 64);
+    if (!grow_keep(c->d_ent2, 0, 8 * padded) || !grow_keep(c->d_status2, 0, ne) || !grow_keep(c->d_xrank2, 0, 4 * ne) ||
+        !grow_keep(c->d_ekey2, 0, 4 * ne))
+        return AD_E_NOMEM;
+    *ent = c->d_ent2.as<uint2>();
+    *st = c->d_status2.as<uint8_t>();
+    *xr = c->d_xrank2.as<uint32_t>();
+    *ek = c->d_ekey2.as<uint32_t>();
+    return 0;
+}
+
+static void swap_buf(DevBuf& a, DevBuf& b)
+{
+    std::swap(a.p, b.p);
+    std::swap(a.cap, b.cap);
+}
+
+static int size_cfk_trees(ad_ctx* c, uint64_t ne)
+{
+    DevSnapshot& s = c->ds;
+    s.n_ent = ne;
+    s.ent = c->d_ent.as<uint2>();
+    s.lvl_n[0] = ne;
+    int L = 1;
+    while (s.lvl_n[L - 1] > 64 && L < MAX_LEVELS)
+    {
+        s.lvl_n[L] = (s.lvl_n[L - 1] + 63) / 64;
+        ++L;
+    }
+    s.n_levels = L;
+    for (int l = 1; l < L; ++l)
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * ((s.lvl_n[l] + 63) / 64 * 64))) return AD_E_NOMEM;
+            s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
+        }
+    return 0;
+}
+
+static int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    swap_buf(c->d_ent, c->d_ent2);
+    swap_buf(c->d_status, c->d_status2);
+    swap_buf(c->d_xrank, c->d_xrank2);
+    swap_buf(c->d_ekey, c->d_ekey2);
+    *ent = c->d_ent.as<uint2>();
+    *st = c->d_status.as<uint8_t>();
+    *xr = c->d_xrank.as<uint32_t>();
+    *ek = c->d_ekey.as<uint32_t>();
+    return size_cfk_trees(c, ne);
+}
+
 static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats)
 {
     if (c->dirty)
@@ -2017,7 +2141,22 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
                      c->d_w.as<uint2>(), c->d_w.cap / 8};
     CfkUpdOut o;
     std::string e;
-    const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, st, &o, &e);
+    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries};
+    const uint64_t nd0 = c->dict_msb.size();
+    const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e);
+    if (c->ds.n_dict > nd0)
+    {
+        // ids appended to the device dictionary (kept even when the batch then failed): host copy
+        const uint64_t add = c->ds.n_dict - nd0;
+        c->dict_msb.resize(nd0 + add);
+        c->dict_lsb.resize(nd0 + add);
+        c->dict_node.resize(nd0 + add);
+        HIPCHK(c, hipMemcpy(c->dict_msb.data() + nd0, c->d_dict_hi.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(c->dict_lsb.data() + nd0, c->d_dict_lsb_raw.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(c->dict_node.data() + nd0, c->d_dict_node.as<int32_t>() + nd0, 4 * add, hipMemcpyDeviceToHost));
+        c->global_ok = false;        // global ranks of the multi-store exchange no longer cover the dictionary
+    }
+    if (o.n_inserted) c->host_moved = true;
     if (rc == AD_E_NOMEM || rc == AD_E_DEVICE)
     {
         // the derived arrays may be half built: rebuild them from the entries at the next use
@@ -2038,6 +2177,8 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         stats->ms_device = o.ms_total;
         stats->ms_stage[0] = o.ms_locate;
         stats->ms_stage[1] = o.ms_derive;
+        stats->n_keys[0] = o.n_inserted;         // entries inserted
+        stats->n_keys[1] = o.n_new_ids;          // ids appended to the dictionary
     }
     return AD_OK;
 }

@@ -44,8 +44,10 @@ struct UpdCtl {
     uint32_t err, err_idx;
     unsigned long long applied;
     uint64_t tot[4];          // cand per class, committed entries
-    uint64_t tot2[2];         // cwr, w
+    uint64_t tot2[2];         // new dictionary ids (unique), inserted entries (groups)
+    uint32_t n_new, n_ins;    // ids newer than the dictionary, insertion updates
 };
+constexpr uint32_t LOC_NONE = 0xFFFFFFFFu;
 
 __device__ inline void upd_fail(UpdCtl* c, uint32_t code, uint32_t idx)
 {
@@ -82,7 +84,8 @@ __device__ inline uint32_t tau_of(uint32_t st, uint32_t kind, uint32_t xr)
 // thread per update: key index, entry position, executeAt rank; claim the entry for the first
 // update of the highest status (packed u64 max: status, then the lowest update index)
 __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, CfkDevState d, CfkUpdIn u, uint32_t* loc,
-                                                    uint32_t* xr_out, unsigned long long* word, UpdCtl* ctl)
+                                                    uint32_t* xr_out, unsigned long long* word, uint64_t* ins_k,
+                                                    uint32_t* ins_v, UpdCtl* ctl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= u.n) return;
@@ -116,15 +119,172 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, CfkDevState d
         if ((s.ent[m].y & RANK_MASK) < r) lo = m + 1;
         else hi = m;
     }
-    if (lo >= kr.seg_hi || (s.ent[lo].y & RANK_MASK) != r) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
+    const bool present = lo < kr.seg_hi && (s.ent[lo].y & RANK_MASK) == r;
+    // absent: inserted at -1 - binarySearch (:1002-1007) when that is the end of byId
+    if (!present && kr.seg_hi > kr.seg_lo && r <= kr.last_txn) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
     const uint64_t el = u.exec_lsb[i];
     const uint32_t xr = dict_member_rank(s, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
     if (!xr) { upd_fail(ctl, UE_NEW_EXEC, (uint32_t)i); return; }
     if (d.dict_lsb_raw[p] != el) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
     if ((tl & 1) && tau_of(st, (uint32_t)((tl >> 1) & 7), xr) != 0) { upd_fail(ctl, UE_DOMAIN, (uint32_t)i); return; }
-    loc[i] = lo;
     xr_out[i] = xr;
+    if (!present)
+    {
+        const uint32_t j = atomicAdd(&ctl->n_ins, 1u);
+        ins_k[j] = ((uint64_t)k << 32) | r;
+        ins_v[j] = (uint32_t)i;
+        return;
+    }
+    loc[i] = lo;
     atomicMax(word + lo, ((unsigned long long)st << 32) | (0xFFFFFFFFull - i));
+}
+
+// ---- insertion ------------------------------------------------------------------------------
+__device__ inline bool newer_than_dict(const DevSnapshot& s, const NormTid& t)
+{
+    if (s.n_dict == 0) return true;
+    const NormTid l{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
+    return norm_cmp(t, l) > 0;
+}
+
+// ids newer than every dictionary id (txnIds and executeAts): words for the LSD sort + raw lsb
+__global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, CfkUpdIn u, uint64_t* nw, uint64_t cap, UpdCtl* ctl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u.n) return;
+    for (int side = 0; side < 2; ++side)
+    {
+        const uint64_t m = side ? u.exec_msb[i] : u.txn_msb[i], l = side ? u.exec_lsb[i] : u.txn_lsb[i];
+        const int32_t nd = side ? u.exec_node[i] : u.txn_node[i];
+        const NormTid t = norm_tid(m, l, nd);
+        if (!newer_than_dict(s, t)) continue;
+        const uint32_t j = atomicAdd(&ctl->n_new, 1u);
+        nw[j] = (uint64_t)((uint32_t)t.node ^ 0x80000000u);
+        nw[cap + j] = t.lo;
+        nw[2 * cap + j] = t.hi;
+        nw[3 * cap + j] = l;
+    }
+}
+
+__global__ void k_iota(uint32_t* v, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (uint32_t)i;
+}
+
+__global__ void k_gather64(const uint64_t* src, const uint32_t* idx, uint64_t n, uint64_t* out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = src[idx[i]];
+}
+
+// sorted new ids: first of each equal run; equal ids must carry equal flag bits
+__global__ void k_ins_unique(const uint32_t* order, uint64_t m, const uint64_t* nw, uint64_t cap, uint32_t* flag, UpdCtl* ctl)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    const uint32_t a = order[r];
+    bool first = r == 0;
+    if (!first)
+    {
+        const uint32_t b = order[r - 1];
+        first = nw[a] != nw[b] || nw[cap + a] != nw[cap + b] || nw[2 * cap + a] != nw[2 * cap + b];
+        if (!first && nw[3 * cap + a] != nw[3 * cap + b]) upd_fail(ctl, UE_FLAGS, 0);
+    }
+    flag[r] = first ? 1u : 0u;
+}
+
+__global__ void k_ins_append(const uint32_t* order, uint64_t m, const uint64_t* nw, uint64_t cap, const uint32_t* flag,
+                             const uint64_t* pos, uint64_t n_dict, uint64_t* dh, uint64_t* dl, int32_t* dn, uint64_t* draw)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m || !flag[r]) return;
+    const uint32_t a = order[r];
+    const uint64_t p = n_dict + pos[r];
+    dn[p] = (int32_t)((uint32_t)nw[a] ^ 0x80000000u);
+    dl[p] = nw[cap + a];
+    dh[p] = nw[2 * cap + a];
+    draw[p] = nw[3 * cap + a];
+}
+
+// insertion updates sorted by (key index, txn rank): group starts
+__global__ void k_ins_gflags(const uint64_t* ks, uint64_t q, uint32_t* gflag)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < q) gflag[j] = (j == 0 || ks[j] != ks[j - 1]) ? 1u : 0u;
+}
+
+// per group (one new entry): the first update of the highest status wins (batch order)
+__global__ void k_ins_claim(const uint64_t* ks, const uint32_t* vs, uint64_t q, const uint32_t* gflag, const uint64_t* gs,
+                            const uint8_t* status, unsigned long long* gword, uint32_t* gkey, uint32_t* grank)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= q) return;
+    const uint64_t g = gs[j] + gflag[j] - 1;
+    if (gflag[j])
+    {
+        gkey[g] = (uint32_t)(ks[j] >> 32);
+        grank[g] = (uint32_t)ks[j];
+    }
+    const uint32_t i = vs[j];
+    atomicMax(gword + g, ((unsigned long long)status[i] << 32) | (0xFFFFFFFFull - i));
+}
+
+// ib[k] = new entries of keys below k (k <= n_keys)
+__global__ void k_ins_before(uint64_t nk, const uint32_t* gkey, uint64_t G, uint32_t* ib)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > nk) return;
+    uint64_t lo = 0, hi = G;
+    while (lo < hi)
+    {
+        const uint64_t m = (lo + hi) >> 1;
+        if (gkey[m] < k) lo = m + 1;
+        else hi = m;
+    }
+    ib[k] = (uint32_t)lo;
+}
+
+struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; };
+
+__global__ __launch_bounds__(256) void k_ins_move_old(uint64_t ne, EntArrays a, const uint32_t* ib, EntArrays b)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t k = a.ekey[e];
+    const uint64_t p = e + ib[k];
+    b.ent[p] = a.ent[e];
+    b.status[p] = a.status[e];
+    b.xrank[p] = a.xrank[e];
+    b.ekey[p] = k;
+}
+
+__global__ void k_ins_place(uint64_t G, const uint32_t* gkey, const uint32_t* grank, const unsigned long long* gword,
+                            const KeyRec* krec, CfkUpdIn u, const uint32_t* xr, EntArrays b)
+{
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const uint32_t k = gkey[g];
+    const unsigned long long wd = gword[g];
+    const uint32_t i = (uint32_t)(0xFFFFFFFFull - (uint32_t)wd);
+    const uint64_t p = krec[k].seg_hi + g;
+    const uint32_t kind = (uint32_t)((u.txn_lsb[i] >> 1) & 7);
+    b.ent[p] = make_uint2(0u, grank[g] | (kind << RANK_BITS));
+    b.status[p] = (uint8_t)(wd >> 32);
+    b.xrank[p] = xr[i];
+    b.ekey[p] = k;
+}
+
+__global__ void k_ins_krec(uint64_t nk, const uint32_t* ib, const uint32_t* grank, KeyRec* krec)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    KeyRec kr = krec[k];
+    const uint32_t a = ib[k], b = ib[k + 1];
+    kr.seg_lo += a;
+    kr.seg_hi += b;
+    if (b > a) kr.last_txn = grank[b - 1];
+    krec[k] = kr;
 }
 
 // after a failed locate: release every claimed entry
@@ -143,6 +303,7 @@ __global__ void k_upd_apply(uint64_t n, const uint32_t* loc, const uint32_t* xr,
     if (i >= n) return;
     bk[i] = make_uint2(0xFFFFFFFFu, 0);
     const uint32_t e = loc[i];
+    if (e == LOC_NONE) return;                 // an insertion
     const unsigned long long wd = word[e];
     if ((uint32_t)wd != (uint32_t)(0xFFFFFFFFull - i)) return;
     word[e] = 0;
@@ -298,6 +459,7 @@ struct DBuf {
 
 struct CfkUpdWork {
     DBuf ctl, loc, xr, word, bk, flags, fs, bsum, ck, cv, ck2, cv2, hist, hoff, f2, s2, maw, wtail;
+    DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
     UpdCtl* h_ctl = nullptr;
     hipEvent_t ev[3] = {};
     ~CfkUpdWork()
@@ -400,32 +562,165 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
     return AD_OK;
 }
 
-int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
-                   int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*), void* need_ctx, hipStream_t st,
-                   CfkUpdOut* out, std::string* err)
+// the radix digits a (key index << 32 | rank) sort needs
+static uint32_t key_rank_mask(uint64_t n_dict, uint64_t nk)
 {
-    const uint64_t n = u.n, ne = s.n_ent;
-    *out = CfkUpdOut{};
-    if (n == 0) return AD_OK;
-    if (n >= 0xFFFFFFFFull) { *err = "more than 2^32-2 updates in one batch"; return AD_E_INVAL; }
-    if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
-    for (auto& e : w->ev)
-        if (!e) UCHK(hipEventCreate(&e));
-    UALLOC(w->ctl, sizeof(UpdCtl), false);
-    UALLOC(w->loc, 4 * n, false);
-    UALLOC(w->xr, 4 * n, false);
-    UALLOC(w->bk, 8 * n, false);
-    UALLOC(w->word, 8 * std::max<uint64_t>(ne, 1), true);   // zero between batches (winners clear theirs)
-    UpdCtl* ctl = w->ctl.as<UpdCtl>();
-    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
-    UCHK(hipEventRecord(w->ev[0], st));
+    uint32_t mask = 0;
+    const uint32_t xb = bytes_of(2 * n_dict + 1), kb = bytes_of(nk ? nk - 1 : 0);
+    for (uint32_t b = 0; b < xb && b < 4; ++b) mask |= 1u << b;
+    for (uint32_t b = 0; b < kb && b < 4; ++b) mask |= 1u << (4 + b);
+    return mask;
+}
 
-    // ---- 1. locate and validate; nothing changes unless the whole batch is valid
-    k_upd_locate<<<blocks(n), 256, 0, st>>>(s, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
-                                            w->word.as<unsigned long long>(), ctl);
+// Append the batch's ids newer than every dictionary id (sorted, unique) to the dictionary.
+static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, const CfkGrow& grow,
+                           hipStream_t st, CfkUpdOut* out, std::string* err)
+{
+    const uint64_t n = u.n, cap = 2 * n;
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UALLOC(w->nw, 8 * 4 * cap, false);
+    k_ins_collect<<<blocks(n), 256, 0, st>>>(s, u, w->nw.as<uint64_t>(), cap, ctl);
     UCHK(hipGetLastError());
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
+    const uint64_t m = w->h_ctl->n_new;
+    if (m == 0) return AD_OK;
+    const uint64_t* nw = w->nw.as<uint64_t>();
+    UALLOC(w->nk_a, 8 * m, false);
+    UALLOC(w->nk_b, 8 * m, false);
+    UALLOC(w->nv_a, 4 * m, false);
+    UALLOC(w->nv_b, 4 * m, false);
+    const uint64_t hist_n = radix_hist_entries(m);
+    UALLOC(w->hist, 4 * hist_n, false);
+    UALLOC(w->hoff, 8 * (hist_n + 1), false);
+    UALLOC(w->bsum, 8 * ((std::max(hist_n, m) + 1023) / 1024 + 8), false);
+    UALLOC(w->nflag, 4 * m, false);
+    UALLOC(w->npos, 8 * (m + 1), false);
+    // LSD over the three words of the normalised id: node, lo, hi (Timestamp.compareTo order)
+    k_iota<<<blocks(m), 256, 0, st>>>(w->nv_a.as<uint32_t>(), m);
+    UCHK(hipMemcpyAsync(w->nk_a.p, nw, 8 * m, hipMemcpyDeviceToDevice, st));
+    uint64_t* ks = w->nk_a.as<uint64_t>();
+    uint32_t* vs = w->nv_a.as<uint32_t>();
+    for (int word = 0; word < 3; ++word)
+    {
+        if (word > 0)
+        {
+            uint64_t* dst = ks == w->nk_a.as<uint64_t>() ? w->nk_b.as<uint64_t>() : w->nk_a.as<uint64_t>();
+            k_gather64<<<blocks(m), 256, 0, st>>>(nw + word * cap, vs, m, dst);
+            ks = dst;
+        }
+        uint64_t* kt = ks == w->nk_a.as<uint64_t>() ? w->nk_b.as<uint64_t>() : w->nk_a.as<uint64_t>();
+        uint32_t* vt = vs == w->nv_a.as<uint32_t>() ? w->nv_b.as<uint32_t>() : w->nv_a.as<uint32_t>();
+        UCHK(radix_sort_pairs(ks, vs, kt, vt, m, word == 0 ? 0x0Fu : 0xFFu, w->hist.as<uint32_t>(), w->hoff.as<uint64_t>(),
+                              w->bsum.as<uint64_t>(), st, &ks, &vs));
+    }
+    k_ins_unique<<<blocks(m), 256, 0, st>>>(vs, m, nw, cap, w->nflag.as<uint32_t>(), ctl);
+    UCHK(run_scan_arrays(w->nflag.as<uint32_t>(), w->npos.as<uint64_t>(), m, 1, w->bsum.as<uint64_t>(), st));
+    k_drv_totals<<<1, 64, 0, st>>>(w->npos.as<uint64_t>(), m, 1, ctl->tot2);
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    if (w->h_ctl->err) return AD_OK;          // reported by the caller
+    const uint64_t U = w->h_ctl->tot2[0], n0 = s.n_dict;
+    if (n0 + U > MAX_DICT) { *err = "id dictionary exceeds 2^28 entries"; return AD_E_CAPACITY; }
+    uint64_t *dh, *dl, *draw;
+    int32_t* dn;
+    if (int rc = grow.dict(grow.ctx, n0, n0 + U, &dh, &dl, &dn, &draw)) { *err = "dictionary growth"; return rc; }
+    k_ins_append<<<blocks(m), 256, 0, st>>>(vs, m, nw, cap, w->nflag.as<uint32_t>(), w->npos.as<uint64_t>(), n0, dh, dl, dn,
+                                            draw);
+    UCHK(hipGetLastError());
+    uint64_t lh = 0, ll = 0;
+    int32_t ln = 0;
+    UCHK(hipMemcpyAsync(&lh, dh + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipMemcpyAsync(&ll, dl + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipMemcpyAsync(&ln, dn + n0 + U - 1, 4, hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    s.dict_hi = dh;
+    s.dict_lo = dl;
+    s.dict_node = dn;
+    s.n_dict = n0 + U;
+    s.dict_last_hi = lh;
+    s.dict_last_lo = ll;
+    s.dict_last_node = ln;
+    d.dict_lsb_raw = draw;
+    out->n_new_ids = U;
+    return AD_OK;
+}
+
+// Insert one entry per (key, txnId) group of the insertion updates at the end of its key's byId;
+// the per-entry arrays move to the spare buffers (the current ones stay intact for a rollback).
+static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, const CfkGrow& grow,
+                          hipStream_t st, uint64_t q, uint64_t* G_out, std::string* err)
+{
+    const uint64_t ne = s.n_ent, nk = s.n_keys;
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UALLOC(w->ck, 8 * q, false);
+    UALLOC(w->cv, 4 * q, false);
+    UALLOC(w->ck2, 8 * q, false);
+    UALLOC(w->cv2, 4 * q, false);
+    const uint64_t hist_n = radix_hist_entries(q);
+    UALLOC(w->hist, 4 * hist_n, false);
+    UALLOC(w->hoff, 8 * (hist_n + 1), false);
+    UALLOC(w->bsum, 8 * ((std::max(hist_n, q) + 1023) / 1024 + 8), false);
+    UALLOC(w->gflag, 4 * q, false);
+    UALLOC(w->gs, 8 * (q + 1), false);
+    UCHK(hipMemcpyAsync(w->ck.p, w->ins_k.p, 8 * q, hipMemcpyDeviceToDevice, st));
+    UCHK(hipMemcpyAsync(w->cv.p, w->ins_v.p, 4 * q, hipMemcpyDeviceToDevice, st));
+    uint64_t* ks = w->ck.as<uint64_t>();
+    uint32_t* vs = w->cv.as<uint32_t>();
+    if (q > 1)
+    {
+        // sort the update indices first so equal (key, txnId) groups keep batch order
+        UCHK(radix_sort_pairs(ks, vs, w->ck2.as<uint64_t>(), w->cv2.as<uint32_t>(), q, key_rank_mask(s.n_dict, nk),
+                              w->hist.as<uint32_t>(), w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
+    }
+    k_ins_gflags<<<blocks(q), 256, 0, st>>>(ks, q, w->gflag.as<uint32_t>());
+    UCHK(run_scan_arrays(w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), q, 1, w->bsum.as<uint64_t>(), st));
+    k_drv_totals<<<1, 64, 0, st>>>(w->gs.as<uint64_t>(), q, 1, ctl->tot2 + 1);
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    const uint64_t G = w->h_ctl->tot2[1];
+    if (ne + G >= (1ull << 32)) { *err = "more than 2^32 CommandsForKey entries"; return AD_E_CAPACITY; }
+    UALLOC(w->gword, 8 * G, false);
+    UALLOC(w->gkey, 4 * G, false);
+    UALLOC(w->grank, 4 * G, false);
+    UALLOC(w->ib, 4 * (nk + 1), false);
+    UALLOC(w->krec_bk, sizeof(KeyRec) * std::max<uint64_t>(nk, 1), false);
+    UCHK(hipMemsetAsync(w->gword.p, 0, 8 * G, st));
+    k_ins_claim<<<blocks(q), 256, 0, st>>>(ks, vs, q, w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), u.status,
+                                           w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>());
+    k_ins_before<<<blocks(nk + 1), 256, 0, st>>>(nk, w->gkey.as<uint32_t>(), G, w->ib.as<uint32_t>());
+    UCHK(hipGetLastError());
+    EntArrays a{d.ent, d.status, d.xrank, d.ekey}, b{};
+    if (int rc = grow.entries(grow.ctx, ne + G, &b.ent, &b.status, &b.xrank, &b.ekey)) { *err = "entry growth"; return rc; }
+    const uint64_t padded = std::max<uint64_t>(64, (ne + G + 63) / 64 * 64);
+    if (padded > ne + G) UCHK(hipMemsetAsync(b.ent + ne + G, 0, sizeof(uint2) * (padded - ne - G), st));
+    if (ne) k_ins_move_old<<<blocks(ne), 256, 0, st>>>(ne, a, w->ib.as<uint32_t>(), b);
+    k_ins_place<<<blocks(G), 256, 0, st>>>(G, w->gkey.as<uint32_t>(), w->grank.as<uint32_t>(), w->gword.as<unsigned long long>(),
+                                           d.krec, u, w->xr.as<uint32_t>(), b);
+    if (nk)
+    {
+        UCHK(hipMemcpyAsync(w->krec_bk.p, d.krec, sizeof(KeyRec) * nk, hipMemcpyDeviceToDevice, st));
+        k_ins_krec<<<blocks(nk), 256, 0, st>>>(nk, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), d.krec);
+    }
+    UCHK(hipGetLastError());
+    if (int rc = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey)) { *err = "entry swap"; return rc; }
+    s.ent = d.ent;
+    s.n_ent = ne + G;
+    *G_out = G;
+    return AD_OK;
+}
+
+int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
+                   int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*), void* need_ctx, const CfkGrow& grow,
+                   hipStream_t st, CfkUpdOut* out, std::string* err)
+{
+    const uint64_t n = u.n;
+    *out = CfkUpdOut{};
+    if (n == 0) return AD_OK;
+    if (n >= 0x7FFFFFFFull) { *err = "more than 2^31-2 updates in one batch"; return AD_E_INVAL; }
+    if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
+    for (auto& e : w->ev)
+        if (!e) UCHK(hipEventCreate(&e));
     auto describe = [&](uint32_t code, uint32_t idx) -> int {
         char b[256];
         const char* what = "";
@@ -434,9 +729,9 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& d, const Cf
         {
             case UE_KEY: what = "key is not in the store's snapshot"; break;
             case UE_STATUS: what = "status is not an InternalStatus ordinal"; break;
-            case UE_ABSENT: what = "txnId is not in the key's CommandsForKey (insertion needs a snapshot load)"; rc = AD_E_STATE; break;
-            case UE_NEW_EXEC: what = "executeAt is not an id of the snapshot (needs a snapshot load)"; rc = AD_E_STATE; break;
-            case UE_FLAGS: what = "id equal to a snapshot id differs in flag bits"; rc = AD_E_INCONSISTENT_ID; break;
+            case UE_ABSENT: what = "txnId is not in the key's CommandsForKey and not newer than its last id (insertion needs a snapshot load)"; rc = AD_E_STATE; break;
+            case UE_NEW_EXEC: what = "executeAt is neither an id of the snapshot nor newer than all of them (needs a snapshot load)"; rc = AD_E_STATE; break;
+            case UE_FLAGS: what = "ids equal under Timestamp.equals differ in flag bits"; rc = AD_E_INCONSISTENT_ID; break;
             case UE_DOMAIN: what = "live range-domain TxnId in a CommandsForKey"; break;
             case UE_DUP_EXEC: what = "two committed entries of one key share an executeAt (CommandsForKey.java:1439)"; rc = AD_E_DUP_EXEC; break;
         }
@@ -444,20 +739,45 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& d, const Cf
         *err = b;
         return rc;
     };
+    UALLOC(w->ctl, sizeof(UpdCtl), false);
+    UALLOC(w->loc, 4 * n, false);
+    UALLOC(w->xr, 4 * n, false);
+    UALLOC(w->bk, 8 * n, false);
+    UALLOC(w->ins_k, 8 * n, false);
+    UALLOC(w->ins_v, 4 * n, false);
+    UALLOC(w->word, 8 * std::max<uint64_t>(s.n_ent, 1), true);   // zero between batches (winners clear theirs)
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    UCHK(hipEventRecord(w->ev[0], st));
+
+    // ---- 0. ids newer than the whole store join the dictionary (appended: no rank changes)
+    if (int rc = grow_dictionary(w, s, d, u, grow, st, out, err)) return rc;
+    if (w->h_ctl->err) return describe(w->h_ctl->err, w->h_ctl->err_idx);
+
+    // ---- 1. locate and validate; nothing changes unless the whole batch is valid
+    k_upd_locate<<<blocks(n), 256, 0, st>>>(s, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
+                                            w->word.as<unsigned long long>(), w->ins_k.as<uint64_t>(),
+                                            w->ins_v.as<uint32_t>(), ctl);
+    UCHK(hipGetLastError());
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
     if (w->h_ctl->err)
     {
         k_upd_release<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->word.as<unsigned long long>());
         UCHK(hipStreamSynchronize(st));
         return describe(w->h_ctl->err, w->h_ctl->err_idx);
     }
-    CfkDevState dd = d;
+    const uint64_t q = w->h_ctl->n_ins, ne0 = s.n_ent;
     k_upd_apply<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(), w->word.as<unsigned long long>(),
-                                           dd, w->bk.as<uint2>(), ctl);
+                                           d, w->bk.as<uint2>(), ctl);
     UCHK(hipGetLastError());
+    uint64_t G = 0;
+    if (q)
+        if (int rc = insert_entries(w, s, d, u, grow, st, q, &G, err)) return rc;
     UCHK(hipEventRecord(w->ev[1], st));
 
     // ---- 2. re-derive the snapshot arrays from the per-entry state
-    int rc = cfk_derive(w, s, dd, bufs, need, need_ctx, st, err);
+    int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err);
     if (rc) return rc;
     UCHK(hipEventRecord(w->ev[2], st));
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
@@ -468,17 +788,25 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& d, const Cf
     out->ms_locate = a;
     out->ms_derive = b;
     out->ms_total = a + b;
-    out->n_applied = w->h_ctl->applied;
+    out->n_applied = w->h_ctl->applied + G;
+    out->n_inserted = G;
     if (w->h_ctl->err)
     {
         // a duplicate committed executeAt: undo the batch and derive the previous state again
         const int code = describe(w->h_ctl->err, w->h_ctl->err_idx);
-        k_upd_rollback<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->bk.as<uint2>(), dd);
+        if (G)
+        {
+            if (grow.swap(grow.ctx, ne0, &d.ent, &d.status, &d.xrank, &d.ekey)) { *err += "; rollback failed"; return AD_E_DEVICE; }
+            s.ent = d.ent;
+            s.n_ent = ne0;
+            if (s.n_keys) UCHK(hipMemcpyAsync(d.krec, w->krec_bk.p, sizeof(KeyRec) * s.n_keys, hipMemcpyDeviceToDevice, st));
+        }
+        k_upd_rollback<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->bk.as<uint2>(), d);
         UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
         std::string e2;
-        if ((rc = cfk_derive(w, s, dd, bufs, need, need_ctx, st, &e2))) { *err += "; rollback: " + e2; return rc; }
+        if ((rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, &e2))) { *err += "; rollback: " + e2; return rc; }
         UCHK(hipStreamSynchronize(st));
-        out->n_applied = 0;
+        out->n_applied = out->n_inserted = 0;
         return code;
     }
     return AD_OK;

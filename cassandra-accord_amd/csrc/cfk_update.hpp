@@ -19,14 +19,17 @@ struct CfkUpdIn {
     const uint8_t* status;
 };
 
+// Insertions: an update whose txnId the key's byId does not hold is inserted when its txnId is
+// newer than every id of the key (always true for an id newer than the whole store: a fresh
+// PreAccept); ids newer than every dictionary id are appended to the dictionary first.
 // Per-entry state kept on the device beside the derived snapshot (built by the ingest): the
 // InternalStatus and executeAt rank of every byId entry and the key index each entry belongs to.
 // The derived arrays (ent, cand, cwr, w, krec, kent, trees) are rebuilt from it after an update.
 struct CfkDevState {
     uint8_t* status;               // [n_ent]
     uint32_t* xrank;               // [n_ent] executeAt rank
-    const uint32_t* ekey;          // [n_ent] key index
-    const uint64_t* dict_lsb_raw;  // [n_dict] raw lsb of every dictionary id (flag-bit identity check)
+    uint32_t* ekey;                // [n_ent] key index
+    uint64_t* dict_lsb_raw;  // [n_dict] raw lsb of every dictionary id (flag-bit identity check)
     // derived arrays rewritten in place (the snapshot's const views alias them)
     uint2* ent; KeyRec* krec; KeyEntry* kent;
 };
@@ -38,8 +41,22 @@ struct CfkDerivedBufs {
     uint2* w; uint64_t w_cap;
 };
 
+// Buffer growth for insertions (owned by the caller; all pointers device memory).
+struct CfkGrow {
+    void* ctx;
+    // dictionary arrays with room for n_new ids, the first n_old kept
+    int (*dict)(void* ctx, uint64_t n_old, uint64_t n_new, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** lsb_raw);
+    // spare per-entry arrays for ne_new entries (ent padded to whole 64-entry frames)
+    int (*entries)(void* ctx, uint64_t ne_new, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey);
+    // make the spare arrays current (commit = true) or current ones spare again (rollback) and size
+    // the snapshot's trees for ne entries; returns the now-current arrays
+    int (*swap)(void* ctx, uint64_t ne, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey);
+};
+
 struct CfkUpdOut {
-    uint64_t n_applied = 0;        // updates that changed an entry
+    uint64_t n_applied = 0;        // entries changed or inserted
+    uint64_t n_inserted = 0;       // entries inserted
+    uint64_t n_new_ids = 0;        // ids added to the dictionary
     double ms_locate = 0, ms_derive = 0, ms_total = 0;
 };
 
@@ -50,8 +67,8 @@ void cfk_upd_work_destroy(CfkUpdWork* w);
 // Applies the batch (AD_E_* on failure with the store unchanged; message in *err).
 // `need` is called with the sizes the derived arrays need; it must return buffers at least that
 // large (possibly reallocated) in *bufs.
-int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
+int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
                    int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
-                   hipStream_t st, CfkUpdOut* out, std::string* err);
+                   const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err);
 
 }  // namespace adx

@@ -24,3 +24,29 @@ def transitions(cfk, rng, n, repeat_frac=0.25, statuses=range(8)):
     ex = Tids(np.where(own, cfk.txn.msb[e], cfk.exec.msb[e]), np.where(own, cfk.txn.lsb[e], cfk.exec.lsb[e]),
               np.where(own, cfk.txn.node[e], cfk.exec.node[e]))
     return CfkUpdates(entry_keys(cfk)[e], cfk.txn.take(e), ex, st), e
+
+
+def fresh_preaccepts(cfk, rng, n_txns, max_keys=4, epoch=9, hlc0=1, statuses=(2,), new_exec_frac=0.0,
+                     kinds=(0, 1, 3)):
+    """PreAccepts of txnIds newer than every id of the store (epoch above the store's): each new txn
+    on 1..max_keys existing keys, inserted with a status from `statuses`; executeAt = txnId or, for
+    `new_exec_frac` of them, a later new Timestamp."""
+    from accord_deps.model import make_timestamps, make_txn_ids
+    kind = rng.choice(np.array(kinds, np.uint8), n_txns)
+    t = make_txn_ids(epoch, hlc0 + np.arange(n_txns) * 3, kind, rng.integers(1, 17, n_txns))
+    x = make_timestamps(epoch, hlc0 + np.arange(n_txns) * 3 + 1, t.lsb & np.uint64(0xFFFF), 1 << 25)
+    use_x = rng.random(n_txns) < new_exec_frac
+    ex = Tids(np.where(use_x, x.msb, t.msb), np.where(use_x, x.lsb, t.lsb), np.where(use_x, x.node, t.node))
+    keys, rows = [], []
+    for i in range(n_txns):
+        kk = rng.choice(cfk.keys, rng.integers(1, max_keys + 1), replace=False)
+        keys.extend(kk.tolist())
+        rows.extend([i] * len(kk))
+    rows = np.array(rows)
+    st = rng.choice(np.array(statuses, np.uint8), len(rows))
+    return CfkUpdates(np.array(keys, np.int64), t.take(rows), ex.take(rows), st)
+
+
+def concat(*us):
+    return CfkUpdates(np.concatenate([u.keys for u in us]), Tids.concat([u.txn for u in us]),
+                      Tids.concat([u.exec for u in us]), np.concatenate([u.status for u in us]))

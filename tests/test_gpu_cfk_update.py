@@ -196,3 +196,107 @@ def test_empty_batch_and_sequential_follows(oracle):
                                         Tids(np.zeros(0), np.zeros(0), np.zeros(0)), np.zeros(0, np.uint8)))[0] == 0
     finally:
         st.close()
+
+
+# ---- insertion of ids newer than the store (fresh PreAccepts) --------------------------------
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("seed", range(6))
+def test_insert_fresh_preaccepts(oracle, seed, path):
+    w = synth.random_small(40 + seed, with_slices=(seed % 3 == 2))
+    w.flags = A.AD_SNAPSHOT
+    rng = np.random.default_rng(40 + seed)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices, path=path)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        for rnd in range(3):                     # each round inserts newer txns, raises older ones
+            ins = G.fresh_preaccepts(cfk, rng, 15 + 10 * rnd, epoch=9 + rnd, statuses=(0, 2, 3, 4, 6),
+                                     new_exec_frac=0.3)
+            tr, _ = G.transitions(cfk, rng, 40)
+            u = G.concat(tr, ins, ins) if rnd == 1 else G.concat(ins, tr)
+            new, _ = U.cfk_update(cfk, u)
+            st.cfk_update(u)
+            assert new.n_entries > cfk.n_entries
+            _check(w, st, oracle, new)
+            cfk = new
+        # a known txnId appended to a key that does not hold it (newer than the key's last id) is
+        # an insertion too; one older than the key's last id is not on the device
+        seg = cfk.seg.astype(np.int64)
+        last = int(np.lexsort((cfk.txn.node, cfk.txn.lsb >> np.uint64(16), cfk.txn.msb))[-1])   # the newest id
+        k_of = np.repeat(np.arange(len(cfk.keys)), np.diff(seg))
+        holds = set(k_of[(cfk.txn.msb == cfk.txn.msb[last]) & (cfk.txn.lsb == cfk.txn.lsb[last]) &
+                         (cfk.txn.node == cfk.txn.node[last])].tolist())
+        other = [k for k in range(len(cfk.keys)) if k not in holds][0]
+        u = CfkUpdates(np.array([cfk.keys[other]]), cfk.txn.take([last]), cfk.txn.take([last]),
+                       np.array([A.ST_ACCEPTED], np.uint8))
+        new, _ = U.cfk_update(cfk, u)
+        st.cfk_update(u)
+        _check(w, st, oracle, new)
+    finally:
+        st.close()
+
+
+def test_insert_older_than_key_rejected(oracle):
+    w = synth.random_small(50)
+    w.flags = A.AD_SNAPSHOT
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        seg = w.cfk.seg.astype(np.int64)
+        k = int(np.argmax(np.diff(seg)))
+        e = int(seg[k])                          # the key's first id, moved to another timestamp below it
+        t = Tids(w.cfk.txn.msb[[e]], w.cfk.txn.lsb[[e]], np.array([w.cfk.txn.node[e] + 100], np.int32))
+        bad = CfkUpdates(np.array([w.cfk.keys[k]]), t, t, np.array([A.ST_PREACCEPTED], np.uint8))
+        _unchanged_after_error(w, st, oracle, bad, A.AD_E_STATE)
+    finally:
+        st.close()
+
+
+def test_insert_duplicate_exec_rolls_back(oracle):
+    w = synth.random_small(51)
+    w.flags = A.AD_SNAPSHOT
+    rng = np.random.default_rng(51)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        ins = G.fresh_preaccepts(w.cfk, rng, 2, max_keys=1, statuses=(A.ST_APPLIED,))
+        k = np.array([w.cfk.keys[0]] * len(ins))
+        x = Tids(np.repeat(ins.txn.msb[:1], len(ins)), np.repeat(ins.txn.lsb[:1], len(ins)),
+                 np.repeat(ins.txn.node[:1], len(ins)))
+        dup = CfkUpdates(k, ins.txn, x, ins.status)
+        _unchanged_after_error(w, st, oracle, dup, A.AD_E_DUP_EXEC)
+        new, _ = U.cfk_update(w.cfk, ins)
+        st.cfk_update(ins)
+        _check(w, st, oracle, new)
+    finally:
+        st.close()
+
+
+def test_sequential_and_recovery_after_inserts(oracle):
+    w = synth.random_small(52, n_range_cmds=0)
+    rng = np.random.default_rng(52)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        ins = G.fresh_preaccepts(w.cfk, rng, 20, statuses=(2, 3, 4))
+        new, _ = U.cfk_update(w.cfk, ins)
+        st.cfk_update(ins)
+        old = w.cfk
+        w.cfk = new
+        # SEQUENTIAL PreAccepts newer still (ascending, executeAt == txnId)
+        from accord_deps.model import Queries
+        q = G.fresh_preaccepts(new, rng, 30, epoch=12)
+        rows = np.r_[0, np.nonzero(np.diff(q.txn.lsb.astype(np.int64)))[0] + 1]
+        off = np.r_[rows, len(q)].astype(np.uint64)
+        keys = np.concatenate([np.sort(q.keys[int(off[i]):int(off[i + 1])]) for i in range(len(rows))])
+        w.queries = Queries(q.txn.take(rows), q.txn.take(rows), off, keys)
+        try:
+            w.flags = A.AD_SEQUENTIAL             # the host copy follows the device before inserting the batch
+            exp = oracle.resolve(w)
+            got = st.calculate_partial_deps(w.queries, A.AD_SEQUENTIAL)
+            ok, why = got.equals(exp, detail=True)
+            assert ok, why
+        finally:
+            w.cfk = old
+    finally:
+        st.close()
