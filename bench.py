@@ -544,12 +544,25 @@ def bench_cfk_update(args, rank, world, local, dev):
     key_of = np.repeat(cfk.keys, np.diff(cfk.seg.astype(np.int64)))
     status = cfk.status.copy()
     batches = []
+    n_ins = int(n * args.cfk_insert_frac) // 8 * 8       # fresh PreAccepts: 8 keys each
+    n_tr = n - n_ins
+    from accord_deps.model import Tids, make_txn_ids
     for b in range(args.warmup + args.steps):
         live = np.nonzero(status < A.ST_APPLIED)[0]
-        e = np.sort(rng.choice(live, min(n, len(live)), replace=False)) if len(live) else np.zeros(0, np.int64)
+        e = np.sort(rng.choice(live, min(n_tr, len(live)), replace=False)) if len(live) else np.zeros(0, np.int64)
         st = np.maximum(status[e] + 1, A.ST_ACCEPTED).astype(np.uint8)
         status[e] = st
         u = CfkUpdates(key_of[e], cfk.txn.take(e), cfk.exec.take(e), st)
+        if n_ins:
+            # PreAccepts of txnIds newer than the store (epoch above the history's), inserted as
+            # PREACCEPTED into 8 existing keys each (CommandsForKey.update's insert branch)
+            m = n_ins // 8
+            t = make_txn_ids(16 + b, np.arange(m, dtype=np.uint64) * 2 + 1, rng.integers(0, 2, m), rng.integers(1, 17, m))
+            rows = np.repeat(np.arange(m), 8)
+            ks = cfk.keys[rng.integers(0, len(cfk.keys), n_ins)]
+            ti = t.take(rows)
+            u = CfkUpdates(np.concatenate([u.keys, ks]), Tids.concat([u.txn, ti]), Tids.concat([u.exec, ti]),
+                           np.concatenate([u.status, np.full(n_ins, A.ST_PREACCEPTED, np.uint8)]))
         batches.append((u,) + native.device_updates(u, dev))
     store = native.DeviceCommandStore(device=local)
     t0 = time.time()
@@ -562,6 +575,7 @@ def bench_cfk_update(args, rank, world, local, dev):
         b = next(it)
         applied, stt = store.cfk_update_device(b[1], sp)
         stt["applied"] = applied
+        stt["inserted"] = stt["n_keys"][0]
         return stt
     elapsed, all_stats = _timed_steps(args, world, dev, step)
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
@@ -585,29 +599,31 @@ def bench_cfk_update(args, rank, world, local, dev):
         "metric": "CommandsForKey.update on the device-resident snapshot: updates/sec", "value": upd / (ms_per_step / 1000.0),
         "unit": "updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-        "config": {"workload": "config2 snapshot (%d entries, %d keys), %d status transitions per batch (SURVEY 8 f1)"
-                               % (ne, nk, n), "parallelism": "replicas x%d" % world},
+        "config": {"workload": "config2 snapshot (%d entries, %d keys), batches of %d status transitions + %d insertions "
+                               "(PreAccepts of new txnIds, 8 keys each) (SURVEY 8 f1)" % (ne, nk, n_tr, n_ins),
+                   "parallelism": "replicas x%d" % world},
         "roofline": {"bound": "hbm", "kernel": "k_upd_* + k_drv_* + radix sort + trees", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "algorithmic_bytes_per_launch": alg, "launch_ms": ms_dev},
         "stages_ms": {"locate+apply": round(float(np.mean([x["ms_stage"][0] for x in all_stats])), 4),
                       "re-derivation": round(float(np.mean([x["ms_stage"][1] for x in all_stats])), 4)},
         "applied": [x["applied"] for x in all_stats],
+        "inserted": [x["inserted"] for x in all_stats],
         "ingest_ms": ingest_ms,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cfk_update as U
         u0 = batches[0][0]
-        done = min(len(u0), 100_000)
+        done = min(n_tr, 100_000)
         sub = CfkUpdates(u0.keys[:done], u0.txn.take(np.arange(done)), u0.exec.take(np.arange(done)), u0.status[:done])
         t0 = time.perf_counter()
         U.cfk_update(cfk, sub)
         t = time.perf_counter() - t0
         res["cpu_baseline"] = dict(value=done / t, unit="updates/s", cores=1, kind="port",
-                                   sample="first %d of %d updates of the first batch (%.1f s), oracle/cfk_update.py "
-                                          "(CommandsForKey.update restatement: binarySearch + raise), 1 thread"
-                                          % (done, len(u0), t))
+                                   sample="first %d of %d updates of the first batch (status transitions; %.1f s), "
+                                          "oracle/cfk_update.py (CommandsForKey.update restatement: binarySearch + raise), "
+                                          "1 thread" % (done, len(u0), t))
     if rank == 0:
         print(json.dumps(res), flush=True)
     store.close()
@@ -680,6 +696,8 @@ def main():
                     help="with config 2: BeginRecovery scans for N recovering txns on the config-2 snapshot (SURVEY 8 f4)")
     ap.add_argument("--cfk-update", type=int, default=0, metavar="N",
                     help="with config 2: batches of N CommandsForKey.update status transitions on the device (SURVEY 8 f1)")
+    ap.add_argument("--cfk-insert-frac", type=float, default=0.5,
+                    help="--cfk-update: share of each batch that inserts new txnIds (fresh PreAccepts)")
     ap.add_argument("--recovery-scan", type=int, default=3, choices=(0, 1, 2, 3), help="AD_RECOVER_* scan of --recovery")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank: the measured configuration); gloo: rehearsal of the "

@@ -449,10 +449,13 @@ int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t sc
  * carried: "not above"); updates of one entry apply in batch order. committedByExecuteAt,
  * maxAppliedWriteByExecuteAt and every derived device array follow (:642-681).
  * The caller filters what the Java drops before the search (txnId < shardRedundantBefore, :995).
+ * A txnId the key's byId does not hold is inserted (:1002-1007) when it is newer than the key's last
+ * id (a fresh PreAccept); ids newer than every id of the store join the id dictionary.
  * Errors (nothing applied): AD_E_INVAL (key not in the snapshot, status > 7, live range-domain id),
- * AD_E_STATE (txnId not in the key's byId, or an executeAt that is no id of the snapshot: inserting
- * new ids needs ad_cfk_load), AD_E_INCONSISTENT_ID, AD_E_DUP_EXEC (two committed entries of a key
- * with one executeAt, :1439). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
+ * AD_E_STATE (an absent txnId older than its key's last id, or an executeAt that is neither an id of
+ * the snapshot nor newer than all of them: ad_cfk_load a new snapshot), AD_E_INCONSISTENT_ID,
+ * AD_E_DUP_EXEC (two committed entries of a key with one executeAt, :1439). Ids appended to the
+ * dictionary by a failed batch stay (they change no rank). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
  * follow on demand. */
 typedef struct ad_cfk_update_soa {
     uint64_t n;
@@ -467,7 +470,8 @@ typedef struct ad_cfk_update_soa {
 } ad_cfk_update_soa;
 
 /* Host buffers (staged to the device). n_applied (may be null): updates that changed an entry;
- * stats (may be null): ms_stage[0] locate+apply, ms_stage[1] re-derivation, ms_device total. */
+ * stats (may be null): ms_stage[0] dictionary append + locate + apply + insertion, ms_stage[1]
+ * re-derivation, ms_device total, n_keys[0] entries inserted, n_keys[1] ids added to the dictionary. */
 int ad_cfk_update(ad_ctx* ctx, const ad_cfk_update_soa* u, uint64_t* n_applied, ad_stats* stats);
 /* Device buffers, on `stream` (null: the context's stream). Synchronous on return. */
 int ad_cfk_update_device(ad_ctx* ctx, const ad_cfk_update_soa* u_dev, void* stream, uint64_t* n_applied, ad_stats* stats);
