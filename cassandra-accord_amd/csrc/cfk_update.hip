@@ -46,6 +46,7 @@ struct UpdCtl {
     uint64_t tot[4];          // cand per class, committed entries
     uint64_t tot2[2];         // new dictionary ids (unique), inserted entries (groups)
     uint32_t n_new, n_ins;    // ids newer than the dictionary, insertion updates
+    unsigned long long diff[3];   // OR of (word ^ reference) over the new ids: node, lo, hi (sort digits)
 };
 constexpr uint32_t LOC_NONE = 0xFFFFFFFFu;
 
@@ -150,9 +151,14 @@ __device__ inline bool newer_than_dict(const DevSnapshot& s, const NormTid& t)
 // ids newer than every dictionary id (txnIds and executeAts): words for the LSD sort + raw lsb
 __global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, CfkUpdIn u, uint64_t* nw, uint64_t cap, UpdCtl* ctl)
 {
+    __shared__ unsigned long long red[3];
+    if (threadIdx.x < 3) red[threadIdx.x] = 0;
+    __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= u.n) return;
-    for (int side = 0; side < 2; ++side)
+    // digits that vary among the new ids: relative to the batch's first txnId (any fixed id works)
+    const NormTid ref = norm_tid(u.txn_msb[0], u.txn_lsb[0], u.txn_node[0]);
+    unsigned long long d0 = 0, d1 = 0, d2 = 0;
+    for (int side = 0; side < 2 && i < u.n; ++side)
     {
         const uint64_t m = side ? u.exec_msb[i] : u.txn_msb[i], l = side ? u.exec_lsb[i] : u.txn_lsb[i];
         const int32_t nd = side ? u.exec_node[i] : u.txn_node[i];
@@ -163,7 +169,23 @@ __global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, CfkUpdIn u, 
         nw[cap + j] = t.lo;
         nw[2 * cap + j] = t.hi;
         nw[3 * cap + j] = l;
+        d0 |= (uint64_t)((uint32_t)t.node ^ (uint32_t)ref.node);
+        d1 |= t.lo ^ ref.lo;
+        d2 |= t.hi ^ ref.hi;
     }
+    if (d0) atomicOr(&red[0], d0);
+    if (d1) atomicOr(&red[1], d1);
+    if (d2) atomicOr(&red[2], d2);
+    __syncthreads();
+    if (threadIdx.x < 3 && red[threadIdx.x]) atomicOr(&ctl->diff[threadIdx.x], red[threadIdx.x]);
+}
+
+static uint32_t digits_that_vary(uint64_t diff)
+{
+    uint32_t m = 0;
+    for (int d = 0; d < 8; ++d)
+        if ((diff >> (8 * d)) & 0xFF) m |= 1u << d;
+    return m;
 }
 
 __global__ void k_iota(uint32_t* v, uint64_t n)
@@ -611,7 +633,9 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
         }
         uint64_t* kt = ks == w->nk_a.as<uint64_t>() ? w->nk_b.as<uint64_t>() : w->nk_a.as<uint64_t>();
         uint32_t* vt = vs == w->nv_a.as<uint32_t>() ? w->nv_b.as<uint32_t>() : w->nv_a.as<uint32_t>();
-        UCHK(radix_sort_pairs(ks, vs, kt, vt, m, word == 0 ? 0x0Fu : 0xFFu, w->hist.as<uint32_t>(), w->hoff.as<uint64_t>(),
+        const uint32_t mask = digits_that_vary(w->h_ctl->diff[word]);
+        if (!mask) continue;                      // constant word: the order stands
+        UCHK(radix_sort_pairs(ks, vs, kt, vt, m, mask, w->hist.as<uint32_t>(), w->hoff.as<uint64_t>(),
                               w->bsum.as<uint64_t>(), st, &ks, &vs));
     }
     k_ins_unique<<<blocks(m), 256, 0, st>>>(vs, m, nw, cap, w->nflag.as<uint32_t>(), ctl);

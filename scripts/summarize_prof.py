@@ -16,6 +16,7 @@ from collections import defaultdict
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     n = name.split("(")[0]
     return n.replace("void ", "").replace("adx::", "")
 
