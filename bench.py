@@ -640,11 +640,26 @@ def bench_sequential(args, rank, world, local, dev):
     wraps with KeyDeps.SerializerSupport.create); Python objects are not built in the timed step."""
     w = synth.config1(seed=0xACC0D001 + rank)
     st = native.DeviceCommandStore(device=local)
-
-    def step():
-        # SEQUENTIAL inserts the batch into the store: every step re-uploads the initial snapshot
+    if args.resident:
+        # steady state of one store (SURVEY 8 f1): the snapshot stays in HBM; batch b is config 1's
+        # batch moved to epoch +b+1 (fresh txnIds, same keys), PreAccepted by device-side insertion
+        from accord_deps.model import Queries, Tids
         st.load(w, prepare=False)
-        return st.deps_batch_stats(w.queries, w.flags)
+        st.deps_batch_stats(w.queries, w.flags)            # creates the 1k CommandsForKeys (host path)
+        qs = []
+        for b in range(args.warmup + args.steps):
+            q = w.queries
+            t = Tids(q.txn.msb + np.uint64((b + 1) << 15), q.txn.lsb, q.txn.node)
+            qs.append(Queries(t, t, q.key_off, q.keys))
+        it = iter(qs)
+
+        def step():
+            return st.deps_batch_stats(next(it), w.flags)
+    else:
+        def step():
+            # SEQUENTIAL inserts the batch into the store: every step re-uploads the initial snapshot
+            st.load(w, prepare=False)
+            return st.deps_batch_stats(w.queries, w.flags)
     elapsed, all_stats = _timed_steps(args, world, dev, step)
     st.close()
     pairs = _sum_over_ranks(world, dev, w.queries.n_probes)
@@ -654,8 +669,10 @@ def bench_sequential(args, rank, world, local, dev):
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-        "config": {"workload": "config1: 10000 txns x 4 keys over 1000 keys, SEQUENTIAL PreAccept, host API "
-                               "(ingest + PCIe + device per step)", "txns_per_step": len(w.queries) * world,
+        "config": {"workload": "config1: 10000 txns x 4 keys over 1000 keys, SEQUENTIAL PreAccept, host API " +
+                               ("(resident store: each step a fresh batch inserted on the device + PCIe + device)"
+                                if args.resident else "(ingest + PCIe + device per step)"),
+                   "txns_per_step": len(w.queries) * world,
                    "txn_key_pairs_per_step": pairs, "parallelism": "replicas x%d" % world},
         "device_ms": stats["ms_device"], "ingest_ms": stats["ms_ingest"],
         "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
@@ -696,6 +713,8 @@ def main():
                     help="with config 2: BeginRecovery scans for N recovering txns on the config-2 snapshot (SURVEY 8 f4)")
     ap.add_argument("--cfk-update", type=int, default=0, metavar="N",
                     help="with config 2: batches of N CommandsForKey.update status transitions on the device (SURVEY 8 f1)")
+    ap.add_argument("--resident", action="store_true",
+                    help="--config 1: keep the store resident, each step a fresh SEQUENTIAL batch (device-side insertion)")
     ap.add_argument("--cfk-insert-frac", type=float, default=0.5,
                     help="--cfk-update: share of each batch that inserts new txnIds (fresh PreAccepts)")
     ap.add_argument("--recovery-scan", type=int, default=3, choices=(0, 1, 2, 3), help="AD_RECOVER_* scan of --recovery")

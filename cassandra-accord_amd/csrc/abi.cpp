@@ -1423,6 +1423,60 @@ int ad_prepare(ad_ctx* c)
     return c->dirty ? build_snapshot(c) : AD_OK;
 }
 
+static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats);
+
+// SEQUENTIAL PreAccepts as device-side CommandsForKey.update insertions (PREACCEPTED, executeAt =
+// txnId) of every request into the CommandsForKey of each of its keys in the slice, as
+// apply_preaccepts does on the host. Returns 0 (applied), 1 (not applicable here: a key without a
+// CommandsForKey, an insertion before a key's last id, or no built snapshot) or an AD_E_* error.
+static int sequential_on_device(ad_ctx* c, const ad_query_soa* q)
+{
+    if (c->dirty || getenv("AD_SEQ_HOST")) return 1;
+    std::vector<int64_t> keys;
+    std::vector<uint64_t> tm, tl;
+    std::vector<int32_t> tn;
+    for (uint64_t i = 0; i < q->n_txns; ++i)
+    {
+        const Tid t{q->txn_msb[i], q->txn_lsb[i], q->txn_node[i]};
+        const Tid x{q->exec_msb[i], q->exec_lsb[i], q->exec_node[i]};
+        if (!(t.msb == x.msb && ((t.lsb ^ x.lsb) & 0xFFFFFFFFFFFF001EULL) == 0 && t.node == x.node))
+            return c->fail(AD_E_INVAL, "SEQUENTIAL (PreAccept) requests need executeAt == txnId");
+        if (i > 0)
+        {
+            const Tid p{q->txn_msb[i - 1], q->txn_lsb[i - 1], q->txn_node[i - 1]};
+            if (norm_cmp(norm(p), norm(t)) >= 0) return c->fail(AD_E_INVAL, "SEQUENTIAL requests must be in ascending TxnId order");
+        }
+        const uint32_t kind = (uint32_t)((t.lsb >> 1) & 7);
+        if (!((t.lsb & 1) == 0 && ((KINDS_ANY_GLOBALLY_VISIBLE >> kind) & 1))) continue;   // CommandsForKey.manages
+        for (uint64_t k = q->key_off[i]; k < q->key_off[i + 1]; ++k)
+        {
+            const int64_t key = q->keys[k];
+            bool in = c->slice_s.empty();
+            for (size_t s = 0; s < c->slice_s.size() && !in; ++s)
+                in = range_contains(c->cfg.range_start_inclusive, c->slice_s[s], c->slice_e[s], key);
+            if (!in) continue;
+            keys.push_back(key);
+            tm.push_back(t.msb);
+            tl.push_back(t.lsb);
+            tn.push_back(t.node);
+        }
+    }
+    if (keys.empty()) return 0;
+    std::vector<uint8_t> st(keys.size(), AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE);
+    const uint64_t n = keys.size();
+    int rc = 0;
+    CfkUpdIn in{n, stage_q(c, c->u_k, keys.data(), n, &rc), stage_q(c, c->u_tm, tm.data(), n, &rc),
+                stage_q(c, c->u_tl, tl.data(), n, &rc), stage_q(c, c->u_tn, tn.data(), n, &rc), nullptr, nullptr, nullptr,
+                stage_q(c, c->u_st, st.data(), n, &rc)};
+    if (rc) return rc;
+    in.exec_msb = in.txn_msb;
+    in.exec_lsb = in.txn_lsb;
+    in.exec_node = in.txn_node;
+    rc = cfk_update_run(c, in, c->stream, nullptr, nullptr);
+    if (rc == AD_E_INVAL || rc == AD_E_STATE) return 1;
+    return rc;
+}
+
 int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_result** out)
 {
     if (!c || !q || !out) return AD_E_INVAL;
@@ -1432,9 +1486,17 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
     if (rc) return rc;
     if (flags & AD_SEQUENTIAL)
     {
-        // keep a copy so a failed batch leaves the snapshot untouched
-        auto saved = c->cfk;
-        if ((rc = apply_preaccepts(c, q))) { c->cfk = saved; return rc; }
+        // on the device when the snapshot holds every key and the batch only appends (§6e);
+        // otherwise the host inserts and re-ingests
+        rc = sequential_on_device(c, q);
+        if (rc < 0) return rc;
+        if (rc > 0)
+        {
+            // keep a copy so a failed batch leaves the snapshot untouched
+            if ((rc = sync_host(c))) return rc;
+            auto saved = c->cfk;
+            if ((rc = apply_preaccepts(c, q))) { c->cfk = saved; return rc; }
+        }
     }
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     const uint64_t n = q->n_txns;
