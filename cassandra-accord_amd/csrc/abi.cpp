@@ -232,7 +232,8 @@ struct ad_ctx {
     // recovery scans (ad_recovery_batch*): entry ranks kept from the last snapshot build, device view
     std::vector<uint32_t> h_txn_rank, h_exec_rank, h_pruned;
     uint64_t rv_gen = ~0ull;                   // snap_gen the device view was built for
-    DevBuf rv_ent, rv_seg, rv_pruned, rv_miss;
+    DevBuf rv_ent, rv_seg, rv_pruned, rv_miss, rv_blk;
+    uint64_t rv_nblk = 0;
     // global dictionary of the multi-store exchange (ad_set_global_dict)
     DevBuf g_msb, g_lsb, g_node, g_map, g_err;
     uint64_t n_global = 0;
@@ -1574,10 +1575,21 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
             }
             ent[e] = make_uint4(c->h_txn_rank[e], c->h_exec_rank[e], K.status[e] | (kind << 8) | (nm << RV_MISS_SHIFT), mo);
         }
+        // per 64-entry block and status set (ACCEPTED/COMMITTED, STABLE/APPLIED): the largest executeAt
+        // rank; every scan wants executeAt > testTxnId (:861-866), so blocks at or below it are skipped
+        const uint64_t nb = (ne + 63) / 64;
+        std::vector<uint32_t> blk(2 * std::max<uint64_t>(nb, 1), 0);
+        for (uint64_t e = 0; e < ne; ++e)
+        {
+            const uint32_t st = K.status[e];
+            const int set = (st == 3 || st == 4) ? 0 : (st == 5 || st == 6) ? 1 : -1;
+            if (set >= 0) blk[set * nb + e / 64] = std::max(blk[set * nb + e / 64], c->h_exec_rank[e]);
+        }
         int rc;
         if ((rc = upload(c, c->rv_ent, ent)) || (rc = upload(c, c->rv_seg, seg)) || (rc = upload(c, c->rv_pruned, c->h_pruned)) ||
-            (rc = upload(c, c->rv_miss, miss)))
+            (rc = upload(c, c->rv_miss, miss)) || (rc = upload(c, c->rv_blk, blk)))
             return rc;
+        c->rv_nblk = nb;
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->rv_gen = c->snap_gen;
     }
@@ -1585,6 +1597,8 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
     v->seg = c->rv_seg.as<uint32_t>();
     v->pruned = c->rv_pruned.as<uint32_t>();
     v->miss = c->rv_miss.as<uint32_t>();
+    v->blk_max = c->rv_blk.as<uint32_t>();
+    v->n_blk = c->rv_nblk;
     return 0;
 }
 

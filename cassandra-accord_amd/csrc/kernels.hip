@@ -1203,12 +1203,17 @@ __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, 
             }
             return has_as_dep == with;
         };
+        // aligned 64-entry blocks; a block whose largest executeAt (in the scan's status set) is at
+        // or below testTxnId holds nothing the scan wants (executeAt > testTxnId, :861-866)
+        const uint32_t* bm = v.blk_max + (proposed ? 0 : v.n_blk);
+        const uint64_t first = start & ~63ull;
         uint32_t c0 = 0, c1 = 0;
-        for (uint64_t base = start; base < end; base += 64)
+        for (uint64_t base = first; base < end; base += 64)
         {
+            if (bm[base >> 6] <= T) continue;
             bool is1 = false;
             uint32_t r = 0;
-            const bool want = want_of(base + lane, is1, r);
+            const bool want = base + lane >= start && want_of(base + lane, is1, r);
             c0 += __popcll(ballot(want && !is1));
             c1 += __popcll(ballot(want && is1));
         }
@@ -1218,11 +1223,12 @@ __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, 
         if (fits && tot)
         {
             uint32_t run0 = 0, run1 = 0;
-            for (uint64_t base = start; base < end; base += 64)
+            for (uint64_t base = first; base < end; base += 64)
             {
+                if (bm[base >> 6] <= T) continue;
                 bool is1 = false;
                 uint32_t r = 0;
-                const bool want = want_of(base + lane, is1, r);
+                const bool want = base + lane >= start && want_of(base + lane, is1, r);
                 const uint64_t w0 = ballot(want && !is1), w1 = ballot(want && is1);
                 if (want && !is1) b.arena[off + run0 + mbcnt(w0)] = r;       // keyDeps, byId (= rank) order
                 if (want && is1) b.arena[off + c0 + run1 + mbcnt(w1)] = r;   // directKeyDeps

@@ -67,6 +67,8 @@ struct RecoveryView {
     const uint32_t* seg;     // [n_keys + 1] entry range of each key index
     const uint32_t* pruned;  // [n_keys] prunedBefore rank, 0 = none
     const uint32_t* miss;    // TxnInfo.missing() as ranks, ascending per entry
+    const uint32_t* blk_max; // [2][n_blk] max executeAt rank per 64-entry block: {ACCEPTED, COMMITTED}, {STABLE, APPLIED}
+    uint64_t n_blk;
 };
 constexpr uint32_t RV_MISS_SHIFT = 12;
 constexpr uint32_t RV_MAX_MISS = (1u << 20) - 1;
