@@ -1578,12 +1578,21 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
         // per 64-entry block and status set (ACCEPTED/COMMITTED, STABLE/APPLIED): the largest executeAt
         // rank; every scan wants executeAt > testTxnId (:861-866), so blocks at or below it are skipped
         const uint64_t nb = (ne + 63) / 64;
-        std::vector<uint32_t> blk(2 * std::max<uint64_t>(nb, 1), 0);
+        // and the range [min, max] of the blocks' missing() ids (min > max: none): a scan that wants
+        // entries missing a known testTxnId (WITHOUT, :868-872) skips blocks whose range misses it
+        std::vector<uint32_t> blk(4 * std::max<uint64_t>(nb, 1), 0);
+        for (uint64_t b = 0; b < nb; ++b) blk[2 * nb + b] = 0xFFFFFFFFu;
         for (uint64_t e = 0; e < ne; ++e)
         {
             const uint32_t st = K.status[e];
             const int set = (st == 3 || st == 4) ? 0 : (st == 5 || st == 6) ? 1 : -1;
             if (set >= 0) blk[set * nb + e / 64] = std::max(blk[set * nb + e / 64], c->h_exec_rank[e]);
+            const uint32_t nm = ent[e].z >> RV_MISS_SHIFT;
+            if (nm)
+            {
+                blk[2 * nb + e / 64] = std::min(blk[2 * nb + e / 64], miss[ent[e].w]);
+                blk[3 * nb + e / 64] = std::max(blk[3 * nb + e / 64], miss[ent[e].w + nm - 1]);
+            }
         }
         int rc;
         if ((rc = upload(c, c->rv_ent, ent)) || (rc = upload(c, c->rv_seg, seg)) || (rc = upload(c, c->rv_pruned, c->h_pruned)) ||

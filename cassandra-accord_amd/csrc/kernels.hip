@@ -1143,6 +1143,9 @@ __global__ void k_encode_recover(DevSnapshot s, BatchBufs b)
 // scan: AD_RECOVER_* = (TestStartedAt, TestDep, TestStatus) of BeginRecovery.java:334,348,365,378:
 //   0 STARTED_BEFORE WITHOUT IS_PROPOSED, 1 STARTED_BEFORE WITH IS_STABLE,
 //   2 STARTED_AFTER WITHOUT IS_PROPOSED,  3 ANY WITHOUT IS_STABLE
+// MISS: prune blocks by the range of their missing() ids too (pays for scan 3, whose ANY range walks
+// whole segments; measured slower for the STARTED_BEFORE scan 0, so it is compiled out there)
+template <bool MISS>
 __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, uint32_t scan)
 {
     const int wv = threadIdx.x >> 6;
@@ -1206,11 +1209,17 @@ __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, 
         // aligned 64-entry blocks; a block whose largest executeAt (in the scan's status set) is at
         // or below testTxnId holds nothing the scan wants (executeAt > testTxnId, :861-866)
         const uint32_t* bm = v.blk_max + (proposed ? 0 : v.n_blk);
+        const uint32_t* bmin = v.blk_max + 2 * v.n_blk;
+        const uint32_t* bmax = v.blk_max + 3 * v.n_blk;
+        const bool need_missing = MISS && known && !with;   // WITHOUT a known testTxnId: T must be in missing()
+        auto skip_blk = [&](uint64_t blk) {
+            return bm[blk] <= T || (need_missing && (bmin[blk] > T || bmax[blk] < T));
+        };
         const uint64_t first = start & ~63ull;
         uint32_t c0 = 0, c1 = 0;
         for (uint64_t base = first; base < end; base += 64)
         {
-            if (bm[base >> 6] <= T) continue;
+            if (skip_blk(base >> 6)) continue;
             bool is1 = false;
             uint32_t r = 0;
             const bool want = base + lane >= start && want_of(base + lane, is1, r);
@@ -1225,7 +1234,7 @@ __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, 
             uint32_t run0 = 0, run1 = 0;
             for (uint64_t base = first; base < end; base += 64)
             {
-                if (bm[base >> 6] <= T) continue;
+                if (skip_blk(base >> 6)) continue;
                 bool is1 = false;
                 uint32_t r = 0;
                 const bool want = base + lane >= start && want_of(base + lane, is1, r);
@@ -1254,7 +1263,8 @@ hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const Batch
         k_probe_keys<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b);
         const uint64_t blocks_needed = (b.n_probes + K1_WAVES - 1) / K1_WAVES;
         const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
-        k_scan_full<<<grid, 256, 0, st>>>(v, b, scan);
+        if (scan == 3) k_scan_full<true><<<grid, 256, 0, st>>>(v, b, scan);
+        else k_scan_full<false><<<grid, 256, 0, st>>>(v, b, scan);
         // recovery scans of key-domain stores collect no range pairs (empty K4 lists)
         hipError_t e = hipMemsetAsync(b.p_rcnt, 0, sizeof(uint32_t) * b.n_probes, st);
         if (e == hipSuccess) e = hipMemsetAsync(b.p_rb, 0xFF, sizeof(uint64_t) * b.n_probes, st);

@@ -67,7 +67,8 @@ struct RecoveryView {
     const uint32_t* seg;     // [n_keys + 1] entry range of each key index
     const uint32_t* pruned;  // [n_keys] prunedBefore rank, 0 = none
     const uint32_t* miss;    // TxnInfo.missing() as ranks, ascending per entry
-    const uint32_t* blk_max; // [2][n_blk] max executeAt rank per 64-entry block: {ACCEPTED, COMMITTED}, {STABLE, APPLIED}
+    const uint32_t* blk_max; // [4][n_blk] per 64-entry block: max executeAt rank of {ACCEPTED, COMMITTED},
+                             // of {STABLE, APPLIED}; min and max missing() id (min > max: none)
     uint64_t n_blk;
 };
 constexpr uint32_t RV_MISS_SHIFT = 12;
