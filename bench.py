@@ -596,7 +596,7 @@ def bench_cfk_update(args, rank, world, local, dev):
     ms_dev = float(np.mean([x["ms_device"] for x in all_stats]))
     achieved = alg / (ms_dev / 1000.0) / 1e9 if ms_dev > 0 else 0.0
     res = {
-        "metric": "CommandsForKey.update on the device-resident snapshot: updates/sec", "value": upd / (ms_per_step / 1000.0),
+        "metric": "CommandsForKey.update on the device-resident snapshot: updates/sec", "value": upd / elapsed,
         "unit": "updates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": "config2 snapshot (%d entries, %d keys), batches of %d status transitions + %d insertions "

@@ -55,10 +55,33 @@ __device__ inline void upd_fail(UpdCtl* c, uint32_t code, uint32_t idx)
     if (atomicCAS(&c->err, 0u, code) == 0u) c->err_idx = idx;
 }
 
-// lower bound of t in the dictionary: member i -> 2i+1, else 0 (with *pos = i)
-__device__ inline uint32_t dict_member_rank(const DevSnapshot& s, const NormTid& t, uint64_t* pos)
+// Every SAMP-th dictionary id, rebuilt per batch (a few 10^4 ids: cache-resident), so a search
+// touches HBM only inside one SAMP-id window.
+constexpr uint64_t SAMP = 256;
+struct DictSample { const uint64_t* hi; const uint64_t* lo; const int32_t* node; uint64_t n; };
+
+__global__ void k_dict_sample(DevSnapshot s, uint64_t* hi, uint64_t* lo, int32_t* node, uint64_t n)
 {
-    uint64_t lo = 0, hi = s.n_dict;
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    hi[j] = s.dict_hi[j * SAMP];
+    lo[j] = s.dict_lo[j * SAMP];
+    node[j] = s.dict_node[j * SAMP];
+}
+
+// lower bound of t in the dictionary: member i -> 2i+1, else 0 (with *pos = i)
+__device__ inline uint32_t dict_member_rank(const DevSnapshot& s, const DictSample& ds, const NormTid& t, uint64_t* pos)
+{
+    // last sample <= t bounds the window [j * SAMP, (j + 1) * SAMP]
+    uint64_t a = 0, b = ds.n;
+    while (a < b)
+    {
+        const uint64_t m = (a + b) >> 1;
+        const NormTid d{ds.hi[m], ds.lo[m], ds.node[m]};
+        if (norm_cmp(d, t) <= 0) a = m + 1;
+        else b = m;
+    }
+    uint64_t lo = a ? (a - 1) * SAMP : 0, hi = a < ds.n ? a * SAMP : s.n_dict;
     while (lo < hi)
     {
         const uint64_t m = (lo + hi) >> 1;
@@ -84,7 +107,7 @@ __device__ inline uint32_t tau_of(uint32_t st, uint32_t kind, uint32_t xr)
 
 // thread per update: key index, entry position, executeAt rank; claim the entry for the first
 // update of the highest status (packed u64 max: status, then the lowest update index)
-__global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, CfkDevState d, CfkUpdIn u, uint32_t* loc,
+__global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds, CfkDevState d, CfkUpdIn u, uint32_t* loc,
                                                     uint32_t* xr_out, unsigned long long* word, uint64_t* ins_k,
                                                     uint32_t* ins_v, UpdCtl* ctl)
 {
@@ -109,7 +132,7 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, CfkDevState d
     if (st > 7) { upd_fail(ctl, UE_STATUS, (uint32_t)i); return; }
     const uint64_t tl = u.txn_lsb[i];
     uint64_t p;
-    const uint32_t r = dict_member_rank(s, norm_tid(u.txn_msb[i], tl, u.txn_node[i]), &p);
+    const uint32_t r = dict_member_rank(s, ds, norm_tid(u.txn_msb[i], tl, u.txn_node[i]), &p);
     if (!r) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
     if (d.dict_lsb_raw[p] != tl) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
     const KeyRec kr = s.krec[k];
@@ -124,7 +147,7 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, CfkDevState d
     // absent: inserted at -1 - binarySearch (:1002-1007) when that is the end of byId
     if (!present && kr.seg_hi > kr.seg_lo && r <= kr.last_txn) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
     const uint64_t el = u.exec_lsb[i];
-    const uint32_t xr = dict_member_rank(s, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
+    const uint32_t xr = dict_member_rank(s, ds, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
     if (!xr) { upd_fail(ctl, UE_NEW_EXEC, (uint32_t)i); return; }
     if (d.dict_lsb_raw[p] != el) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
     if ((tl & 1) && tau_of(st, (uint32_t)((tl >> 1) & 7), xr) != 0) { upd_fail(ctl, UE_DOMAIN, (uint32_t)i); return; }
@@ -481,6 +504,7 @@ struct DBuf {
 
 struct CfkUpdWork {
     DBuf ctl, loc, xr, word, bk, flags, fs, bsum, ck, cv, ck2, cv2, hist, hoff, f2, s2, maw, wtail;
+    DBuf sm_hi, sm_lo, sm_node;
     DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
     UpdCtl* h_ctl = nullptr;
     hipEvent_t ev[3] = {};
@@ -779,7 +803,15 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     if (w->h_ctl->err) return describe(w->h_ctl->err, w->h_ctl->err_idx);
 
     // ---- 1. locate and validate; nothing changes unless the whole batch is valid
-    k_upd_locate<<<blocks(n), 256, 0, st>>>(s, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
+    const uint64_t n_samp = (s.n_dict + SAMP - 1) / SAMP;
+    UALLOC(w->sm_hi, 8 * std::max<uint64_t>(n_samp, 1), false);
+    UALLOC(w->sm_lo, 8 * std::max<uint64_t>(n_samp, 1), false);
+    UALLOC(w->sm_node, 4 * std::max<uint64_t>(n_samp, 1), false);
+    if (n_samp)
+        k_dict_sample<<<blocks(n_samp), 256, 0, st>>>(s, w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(),
+                                                      w->sm_node.as<int32_t>(), n_samp);
+    const DictSample dsm{w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(), w->sm_node.as<int32_t>(), n_samp};
+    k_upd_locate<<<blocks(n), 256, 0, st>>>(s, dsm, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
                                             w->word.as<unsigned long long>(), w->ins_k.as<uint64_t>(),
                                             w->ins_v.as<uint32_t>(), ctl);
     UCHK(hipGetLastError());
