@@ -1874,8 +1874,13 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     a.dict_node = c->d_dict_node.as<int32_t>();
     a.rt_start = c->d_rt_start.as<int64_t>();
     a.rt_end = c->d_rt_end.as<int64_t>();
-    a.gmap = c->global_ok ? c->g_map.as<uint32_t>() : nullptr;
-    out->id_format = c->global_ok ? AD_IDS_RANK : AD_IDS_TRIPLET;
+    // the id format is the caller's: its ids buffer was sized for it (cap_ids counts ids of that format)
+    if (out->id_format != AD_IDS_RANK && out->id_format != AD_IDS_TRIPLET)
+        return c->fail(AD_E_INVAL, "ad_parts_export: unknown id_format %u", out->id_format);
+    if (out->id_format == AD_IDS_RANK && !c->global_ok)
+        return c->fail(AD_E_STATE, "ad_parts_export: rank-format parts need a global dictionary covering this store's "
+                                   "ids (ad_set_global_dict after the last snapshot load or dictionary append)");
+    a.gmap = out->id_format == AD_IDS_RANK ? c->g_map.as<uint32_t>() : nullptr;
     a.sz = c->x_sz.as<uint32_t>();
     a.off = c->x_off.as<uint64_t>();
     HIPCHK(c, hipMemcpyAsync(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), hipMemcpyHostToDevice, st));
@@ -2242,7 +2247,7 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         c->global_ok = false;        // global ranks of the multi-store exchange no longer cover the dictionary
     }
     if (o.n_inserted) c->host_moved = true;
-    if (rc == AD_E_NOMEM || rc == AD_E_DEVICE)
+    if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back)
     {
         // the derived arrays may be half built: rebuild them from the entries at the next use
         c->host_stale = true;

@@ -14,8 +14,11 @@
 //   * w (committed Writes by executeAt), maxAppliedWriteByExecuteAt (:660-672), krec
 //   * the newest-probe emission lists cand / cwr and KeyEntry
 //   * the 64-ary max trees over tau (build_cfk_trees).
-// Inserting ids the store has never seen needs the id dictionary to grow (rank remap of every
-// array): rejected with AD_E_STATE for now.
+// Insertion (:1002-1007) of a txnId newer than every id of its key is supported: ids newer than
+// every dictionary id are appended to the dictionary (no rank changes) and the new entries go at
+// the end of their keys' byId. An absent txnId older than its key's last id (a mid-segment insert),
+// or an id older than the newest dictionary id but unknown to it (a rank remap of every array), is
+// rejected with AD_E_STATE. A failed batch leaves the store unchanged.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -485,13 +488,15 @@ struct DBuf {
     void* p = nullptr;
     size_t cap = 0;
     ~DBuf() { if (p) (void)hipFree(p); }
+    // grows with slack (insertions raise the entry count every batch: no reallocation, and no
+    // re-zeroing of `word`, per batch); zero: the whole new allocation is zeroed
     bool ensure(size_t b, bool zero = false)
     {
         if (p && b <= cap) return true;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        b = std::max<size_t>(b, 64);
+        b = std::max<size_t>(b + b / 4, 64);
         if (hipMalloc(&p, b) != hipSuccess) return false;
         if (zero && hipMemset(p, 0, b) != hipSuccess) return false;
         cap = b;
@@ -696,8 +701,13 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
 
 // Insert one entry per (key, txnId) group of the insertion updates at the end of its key's byId;
 // the per-entry arrays move to the spare buffers (the current ones stay intact for a rollback).
+struct InsUndo {
+    bool krec_saved = false;    // krec was saved to krec_bk and then changed
+    bool swapped = false;       // the per-entry arrays were swapped to the spare buffers
+};
+
 static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, const CfkGrow& grow,
-                          hipStream_t st, uint64_t q, uint64_t* G_out, std::string* err)
+                          hipStream_t st, uint64_t q, uint64_t* G_out, InsUndo* undo, std::string* err)
 {
     const uint64_t ne = s.n_ent, nk = s.n_keys;
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
@@ -748,10 +758,13 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     if (nk)
     {
         UCHK(hipMemcpyAsync(w->krec_bk.p, d.krec, sizeof(KeyRec) * nk, hipMemcpyDeviceToDevice, st));
+        undo->krec_saved = true;
         k_ins_krec<<<blocks(nk), 256, 0, st>>>(nk, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), d.krec);
     }
     UCHK(hipGetLastError());
-    if (int rc = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey)) { *err = "entry swap"; return rc; }
+    const int src = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey);
+    undo->swapped = true;         // the buffers are exchanged even when sizing the trees then failed
+    if (src) { *err = "entry swap"; return src; }
     s.ent = d.ent;
     s.n_ent = ne + G;
     *G_out = G;
@@ -798,9 +811,20 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
     UCHK(hipEventRecord(w->ev[0], st));
 
-    // ---- 0. ids newer than the whole store join the dictionary (appended: no rank changes)
-    if (int rc = grow_dictionary(w, s, d, u, grow, st, out, err)) return rc;
-    if (w->h_ctl->err) return describe(w->h_ctl->err, w->h_ctl->err_idx);
+    // ---- 0. ids newer than the whole store join the dictionary (appended: no rank changes). A
+    // batch that then fails drops them again (the arrays keep the bytes; nothing refers to them).
+    const uint64_t nd0 = s.n_dict, lh0 = s.dict_last_hi, ll0 = s.dict_last_lo;
+    const int32_t ln0 = s.dict_last_node;
+    auto drop_new_ids = [&](int code) -> int {
+        s.n_dict = nd0;
+        s.dict_last_hi = lh0;
+        s.dict_last_lo = ll0;
+        s.dict_last_node = ln0;
+        out->n_new_ids = 0;
+        return code;
+    };
+    if (int rc = grow_dictionary(w, s, d, u, grow, st, out, err)) return rc == AD_E_CAPACITY ? drop_new_ids(rc) : rc;
+    if (w->h_ctl->err) return drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx));
 
     // ---- 1. locate and validate; nothing changes unless the whole batch is valid
     const uint64_t n_samp = (s.n_dict + SAMP - 1) / SAMP;
@@ -821,20 +845,43 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     {
         k_upd_release<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->word.as<unsigned long long>());
         UCHK(hipStreamSynchronize(st));
-        return describe(w->h_ctl->err, w->h_ctl->err_idx);
+        return drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx));
     }
     const uint64_t q = w->h_ctl->n_ins, ne0 = s.n_ent;
     k_upd_apply<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(), w->word.as<unsigned long long>(),
                                            d, w->bk.as<uint2>(), ctl);
     UCHK(hipGetLastError());
+    // From here on the per-entry state has changed: every failure undoes the batch (status and
+    // executeAt restored, insertions swapped back, krec restored) and derives the previous state
+    // again, so that nothing changes unless the whole batch is applied.
+    InsUndo undo;
+    auto rollback = [&](int code) -> int {
+        std::string e2;
+        if (undo.swapped)
+        {
+            if (grow.swap(grow.ctx, ne0, &d.ent, &d.status, &d.xrank, &d.ekey)) { *err += "; rollback failed"; return AD_E_DEVICE; }
+            s.ent = d.ent;
+            s.n_ent = ne0;
+        }
+        if (undo.krec_saved && s.n_keys)
+            if (hipMemcpyAsync(d.krec, w->krec_bk.p, sizeof(KeyRec) * s.n_keys, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            { *err += "; rollback failed"; return AD_E_DEVICE; }
+        k_upd_rollback<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->bk.as<uint2>(), d);
+        if (hipGetLastError() != hipSuccess || hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st) != hipSuccess)
+        { *err += "; rollback failed"; return AD_E_DEVICE; }
+        if (int rc2 = cfk_derive(w, s, d, bufs, need, need_ctx, st, &e2)) { *err += "; rollback: " + e2; return rc2; }
+        if (hipStreamSynchronize(st) != hipSuccess) { *err += "; rollback failed"; return AD_E_DEVICE; }
+        out->n_applied = out->n_inserted = 0;
+        out->rolled_back = true;
+        return drop_new_ids(code);
+    };
     uint64_t G = 0;
     if (q)
-        if (int rc = insert_entries(w, s, d, u, grow, st, q, &G, err)) return rc;
+        if (int rc = insert_entries(w, s, d, u, grow, st, q, &G, &undo, err)) return rollback(rc);
     UCHK(hipEventRecord(w->ev[1], st));
 
     // ---- 2. re-derive the snapshot arrays from the per-entry state
-    int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err);
-    if (rc) return rc;
+    if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rollback(rc);
     UCHK(hipEventRecord(w->ev[2], st));
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
@@ -846,25 +893,8 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     out->ms_total = a + b;
     out->n_applied = w->h_ctl->applied + G;
     out->n_inserted = G;
-    if (w->h_ctl->err)
-    {
-        // a duplicate committed executeAt: undo the batch and derive the previous state again
-        const int code = describe(w->h_ctl->err, w->h_ctl->err_idx);
-        if (G)
-        {
-            if (grow.swap(grow.ctx, ne0, &d.ent, &d.status, &d.xrank, &d.ekey)) { *err += "; rollback failed"; return AD_E_DEVICE; }
-            s.ent = d.ent;
-            s.n_ent = ne0;
-            if (s.n_keys) UCHK(hipMemcpyAsync(d.krec, w->krec_bk.p, sizeof(KeyRec) * s.n_keys, hipMemcpyDeviceToDevice, st));
-        }
-        k_upd_rollback<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->bk.as<uint2>(), d);
-        UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
-        std::string e2;
-        if ((rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, &e2))) { *err += "; rollback: " + e2; return rc; }
-        UCHK(hipStreamSynchronize(st));
-        out->n_applied = out->n_inserted = 0;
-        return code;
-    }
+    // a duplicate committed executeAt: undo the batch and derive the previous state again
+    if (w->h_ctl->err) return rollback(describe(w->h_ctl->err, w->h_ctl->err_idx));
     return AD_OK;
 }
 

@@ -57,6 +57,7 @@ struct CfkUpdOut {
     uint64_t n_applied = 0;        // entries changed or inserted
     uint64_t n_inserted = 0;       // entries inserted
     uint64_t n_new_ids = 0;        // ids added to the dictionary
+    bool rolled_back = false;      // the batch failed after it had been applied and was undone
     double ms_locate = 0, ms_derive = 0, ms_total = 0;
 };
 

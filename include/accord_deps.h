@@ -277,8 +277,10 @@ typedef struct ad_parts {
     int32_t* k2t;
     uint64_t cap_parts, cap_key_words, cap_ids, cap_k2t;  /* capacities of the arrays (export) */
     uint32_t id_format;   /* AD_IDS_TRIPLET: ids as above; AD_IDS_RANK: ids holds n_ids uint32 ranks
-                           * into the global dictionary (ad_set_global_dict). Set by ad_parts_export,
-                           * read by ad_parts_merge. cap_ids counts ids in either format. */
+                           * into the global dictionary (ad_set_global_dict). Chosen by the caller of
+                           * ad_parts_export (the format its ids buffer was sized for; RANK without an
+                           * installed global dictionary covering the store: AD_E_STATE), read by
+                           * ad_parts_merge. cap_ids counts ids in that format. */
 } ad_parts;
 
 #define AD_IDS_TRIPLET 0
