@@ -102,6 +102,106 @@ def stage_bytes(w, stats):
     return b
 
 
+def cpu_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count(), model
+
+
+def cpu_threads():
+    """Host threads the CPU baseline may use: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU box), at most os.cpu_count()."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, n)
+
+
+def cpu_baseline_stores(w, budget_s=15.0, threads=None, gpu_take=None):
+    """The reference's own concurrency model on the host cores: the store's key space split into
+    `threads` EvenSplit token slices (ShardDistributor.EvenSplit, ShardDistributor.java:106-156), one
+    CommandStore each on its own thread (InMemoryCommandStore's single-thread executors,
+    :1144-1202), every store resolving its share of a prefix of the same batch with the CPU
+    restatement (oracle/refcpu.c), then the per-store PartialDeps reduced request-wise with
+    PartialDeps.with (CommandStores.mapReduce :576-593, rc_result_merge). Timed: the parallel
+    resolve + the reduce; median of 3 runs of a prefix sized to ~budget/3 s each. The merged result
+    of the prefix is compared bit-exactly with the GPU's (`gpu_take(idx)` -> PartialDepsBatch)."""
+    import ctypes as C
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    threads = threads or cpu_threads()
+    L = pyoracle.lib()
+    base = w
+    if w.slices is not None and len(w.slices) == 1 and int(w.slices[0][0]) == -(1 << 63) and \
+            int(w.slices[0][1]) == (1 << 63) - 1:
+        from accord_deps.model import Workload
+        base = Workload(w.name, w.cfk, w.cmds, w.redundant, w.queries, w.flags, w.params, w.range_start_inclusive, None)
+    lo, hi = synth.shard_bounds(threads)
+    subs = [synth.slice_workload(base, lo[g], hi[g]) for g in range(threads)] if threads > 1 else [base]
+    stores = [pyoracle.OracleStore(s.range_start_inclusive, 1, s.slices).load(s) for s in subs]
+    soas = [s.queries.soa() for s in subs]
+
+    def run(count):
+        outs = [C.POINTER(pyoracle.RcResult)() for _ in stores]
+        rcs = [0] * len(stores)
+
+        def one(g):
+            rcs[g] = L.rc_deps_batch(stores[g].h, C.byref(soas[g]), base.flags, 0, count, C.byref(outs[g]))
+        t0 = time.perf_counter()
+        ts = [threading.Thread(target=one, args=(g,)) for g in range(len(stores))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        merged = C.POINTER(pyoracle.RcResult)()
+        arr = (C.POINTER(pyoracle.RcResult) * len(outs))(*outs)
+        rc = L.rc_result_merge(arr, len(outs), C.byref(merged)) if len(outs) > 1 else 0
+        dt = time.perf_counter() - t0
+        if any(rcs) or rc:
+            raise RuntimeError("refcpu failed: %r %r" % (rcs, rc))
+        res = merged if len(outs) > 1 else outs[0]
+        batch = pyoracle.result_to_batch(res.contents)
+        for o in outs:
+            L.rc_result_free(o)
+        if len(outs) > 1:
+            L.rc_result_free(merged)
+        return dt, batch
+
+    n = len(base.queries)
+    p = min(n, 256)
+    dt, _ = run(p)
+    p = int(min(n, max(p, p * (budget_s / 3.0) / max(dt, 1e-6))))
+    times, batch = [], None
+    for _ in range(3):
+        dt, batch = run(p)
+        times.append(dt)
+    for s in stores:
+        s.close()
+    t = float(np.median(times))
+    pairs = int(base.queries.key_off[p])
+    ncpu, model = cpu_info()
+    out = dict(value=pairs / t, unit="txn-key pairs/s", cores=threads, kind="port",
+               sample="first %d of %d requests of the same batch (%d txn-key pairs), median of 3 runs (%s s); "
+                      "refcpu = C restatement of the reference Java, %d CommandStores (EvenSplit token slices) on %d "
+                      "threads + PartialDeps.with reduce; host %d CPUs, %s" %
+                      (p, n, pairs, "/".join("%.2f" % x for x in times), threads, threads, ncpu, model))
+    if gpu_take is not None:
+        got = gpu_take(np.arange(p))
+        ok, why = got.equals(batch, detail=True)
+        out["parity_sample"] = "%d requests bit-exact vs GPU" % p if ok else "MISMATCH: %s" % why
+    return out
+
+
 def cpu_baseline(w, budget_s=15.0):
     """The CPU restatement (oracle/refcpu.c, the reference algorithm, one thread = one
     CommandStore) on a bounded prefix of the same batch, same snapshot."""
@@ -717,6 +817,11 @@ def main():
                     help="--config 1: keep the store resident, each step a fresh SEQUENTIAL batch (device-side insertion)")
     ap.add_argument("--cfk-insert-frac", type=float, default=0.5,
                     help="--cfk-update: share of each batch that inserts new txnIds (fresh PreAccepts)")
+    ap.add_argument("--accept-frac", type=float, default=0.0,
+                    help="config 2: share of Accept requests (in-flight txns, S = proposed executeAt, self excluded)")
+    ap.add_argument("--unordered-frac", type=float, default=0.0,
+                    help="config 2: share of out-of-order PreAccepts (txnId inside the history's last ticks)")
+    ap.add_argument("--unordered-window", type=int, default=2000, help="hlc ticks of --unordered-frac's lateness")
     ap.add_argument("--recovery-scan", type=int, default=3, choices=(0, 1, 2, 3), help="AD_RECOVER_* scan of --recovery")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank: the measured configuration); gloo: rehearsal of the "
@@ -760,6 +865,11 @@ def main():
     w, txn_index, n_total = synth.config2_sharded(rank, world, n_txns_per_gpu=int(1_000_000 * s),
                                                   n_keys_per_gpu=int(1_000_000 * s),
                                                   n_hist_entries_per_gpu=int(16_000_000 * s))
+    mix = args.accept_frac > 0 or args.unordered_frac > 0
+    if mix:
+        if world > 1:
+            raise SystemExit("--accept-frac / --unordered-frac: single store only")
+        w = synth.with_request_mix(w, args.accept_frac, args.unordered_frac, args.unordered_window)
     log("rank %d: generated in %.1f s: %d keys, %d entries, %d of %d requests routed here, %d probes" %
         (rank, time.time() - t0, len(w.cfk.keys), w.cfk.n_entries, len(w.queries), n_total, w.queries.n_probes))
 
@@ -782,8 +892,10 @@ def main():
             mg = ex.step()
             return engine.last_stats, mg.ms_device
     else:
+        last = {}
+
         def step():
-            _, st = store.deps_batch_device(qdev, sp)
+            last["res"], st = store.deps_batch_device(qdev, sp)
             return st, 0.0
 
     stats = None
@@ -845,7 +957,10 @@ def main():
         "config": {"workload": "config2 (weak-scaled per GPU): %d txns x 8 Zipf(0.99) keys, %d keys and a %d-entry "
                                "CommandsForKey history per GPU, SNAPSHOT, 1 CommandStore per GPU%s" %
                                (n_total, int(1_000_000 * s) * world, w.cfk.n_entries,
-                                ", partials all-to-all over RCCL + on-GPU merge" if world > 1 else ""),
+                                ", partials all-to-all over RCCL + on-GPU merge" if world > 1 else "") +
+                               ("; request mix: %d Accepts of in-flight txns (S = executeAt, self excluded), %d PreAccepts "
+                                "up to %d hlc ticks late, the rest fresh PreAccepts" %
+                                (w.params["n_accept"], w.params["n_unordered"], args.unordered_window) if mix else ""),
                    "txns_per_step": n_total, "txn_key_pairs_per_step": probes,
                    "parallelism": "store-per-gpu x%d" % world},
         "roofline": {"bound": "hbm", "kernel": " + ".join(res_kernels), "achieved": achieved, "peak": HBM_PEAK_GBS,
@@ -862,12 +977,15 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the PCIe-inclusive rate a host caller sees through ad_deps_batch (host arrays in, packed
         # host CSR arrays out; outside the timed region, never `value`)
-        store.deps_batch_stats(w.queries)
         t0 = time.perf_counter()
         store.deps_batch_stats(w.queries)
         host_ms = 1000.0 * (time.perf_counter() - t0)
         out["host_api"] = {"ms_per_batch": host_ms, "pairs_per_s": w.queries.n_probes / (host_ms / 1000.0)}
-        out["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
+        # the device result of the same batch (the host-API call above reused the ctx buffers),
+        # read back for the baseline's parity check
+        res, _ = store.deps_batch_device(qdev, sp)
+        torch.cuda.synchronize(dev)
+        out["cpu_baseline"] = cpu_baseline_stores(w, args.cpu_budget, gpu_take=lambda idx: store.device_result_to_host(res, idx))
     if rank == 0:
         print(json.dumps(out), flush=True)
     store.close()

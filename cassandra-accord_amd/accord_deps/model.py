@@ -262,6 +262,18 @@ class Queries:
                        ko[lo:hi + 1] - ko[lo], self.keys[int(ko[lo]):int(ko[hi])],
                        None if self.min_epoch is None else self.min_epoch[lo:hi])
 
+    def take(self, idx):
+        """The requests `idx` (ascending or not) as a batch of their own (SNAPSHOT requests are
+        independent of each other, so a sample resolves to the same PartialDeps)."""
+        idx = np.asarray(idx, np.int64)
+        ko = self.key_off.astype(np.int64)
+        cnt = ko[idx + 1] - ko[idx]
+        key_off = np.zeros(len(idx) + 1, np.uint64)
+        key_off[1:] = np.cumsum(cnt)
+        src = np.repeat(ko[idx] - key_off[:-1].astype(np.int64), cnt) + np.arange(int(key_off[-1]))
+        return Queries(self.txn.take(idx), self.exec.take(idx), key_off, self.keys[src],
+                       None if self.min_epoch is None else self.min_epoch[idx])
+
 
 @dataclass
 class Graph:
@@ -381,6 +393,24 @@ class PartialDepsBatch:
     def pair_count(self, m):
         mm = self.maps[m]
         return int(len(mm.k2t) - len(mm.keys))
+
+    def take(self, idx):
+        """Requests `idx` as a batch of their own (offsets rebased)."""
+        idx = np.asarray(idx, np.int64)
+        maps = []
+        for mm in self.maps:
+            def sub(off):
+                o = off.astype(np.int64)
+                cnt = o[idx + 1] - o[idx]
+                no = np.zeros(len(idx) + 1, np.uint64)
+                no[1:] = np.cumsum(cnt)
+                return no, np.repeat(o[idx] - no[:-1].astype(np.int64), cnt) + np.arange(int(no[-1]))
+            ko, ks = sub(mm.keys_off)
+            to, ts = sub(mm.txn_off)
+            oo, os_ = sub(mm.k2t_off)
+            maps.append(DepsMap(ko, mm.keys[ks], None if mm.keys_end is None else mm.keys_end[ks], to, mm.txn.take(ts),
+                                oo, mm.k2t[os_]))
+        return PartialDepsBatch(maps)
 
     def window(self, first, count):
         """Requests [first, first + count) as a batch of their own (offsets rebased)."""

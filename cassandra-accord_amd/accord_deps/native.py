@@ -337,6 +337,33 @@ class DeviceCommandStore:
         self._check(lib().ad_levels_device(self.h, C.byref(gdev), out_ptr, stream, C.byref(s)))
         return levels_stats(s)
 
+    def device_result_to_host(self, res, idx=None):
+        """Materialise the device result `res` of the last deps_batch_device (packed arrays) as a
+        PartialDepsBatch, for every request or only the requests `idx`."""
+        n = res.n_txns
+        raw = []
+        for m in range(A.NMAPS):
+            ko = self._d2h(res.keys_off[m], n + 1, np.uint64)
+            to = self._d2h(res.txn_off[m], n + 1, np.uint64)
+            oo = self._d2h(res.k2t_off[m], n + 1, np.uint64)
+            raw.append((ko, self._d2h(res.keys[m], int(ko[-1]), np.int64), to,
+                        self._d2h(res.txns[m], int(to[-1]), np.uint32), oo, self._d2h(res.k2t[m], int(oo[-1]), np.int32)))
+        if idx is not None:
+            idx = np.asarray(idx, np.int64)
+            sub = []
+            for ko, keys, to, tx, oo, k2t in raw:
+                parts = []
+                for off, arr in ((ko, keys), (to, tx), (oo, k2t)):
+                    o = off.astype(np.int64)
+                    cnt = o[idx + 1] - o[idx]
+                    no = np.zeros(len(idx) + 1, np.uint64)
+                    no[1:] = np.cumsum(cnt)
+                    src = np.repeat(o[idx] - no[:-1].astype(np.int64), cnt) + np.arange(int(no[-1]))
+                    parts += [no, arr[src]]
+                sub.append(tuple(parts))
+            raw = sub
+        return self.materialise(raw)
+
     def _d2h(self, p, n, dtype):
         a = np.zeros(max(n, 0), dtype)
         if n:

@@ -155,10 +155,94 @@ def config2(n_txns=1_000_000, keys_per_txn=8, n_keys=1_000_000, n_hist_entries=1
     cfk, _ = build_history(rng, n_hist, hk, token, hist_kind, tail_unapplied)
     qk = distinct_rows(rng, z.sample, n_txns, keys_per_txn)
     q = _queries(rng, n_txns, qk, token, _rw_kinds(rng, n_txns, esp_frac=esp_frac), hlc0=n_hist + 2000)
-    return Workload("config2", cfk, RangeCommands.empty(), Redundant.empty(), q,
-                    params=dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys,
-                                n_hist_entries=n_hist * keys_per_txn, zipf_s=zipf_s, seed=seed,
-                                sync_frac=sync_frac, esp_frac=esp_frac, semantics="SNAPSHOT"))
+    w = Workload("config2", cfk, RangeCommands.empty(), Redundant.empty(), q,
+                 params=dict(n_txns=n_txns, keys_per_txn=keys_per_txn, n_keys=n_keys,
+                             n_hist_entries=n_hist * keys_per_txn, zipf_s=zipf_s, seed=seed,
+                             sync_frac=sync_frac, esp_frac=esp_frac, semantics="SNAPSHOT"))
+    return w
+
+
+def with_request_mix(w, accept_frac=0.0, unordered_frac=0.0, unordered_window=2000, seed=0xACC0D0A5):
+    """The config-2 workload `w` (history txn j has txnId hlc 1 + j) turned into a replica's mix of
+    deps requests (SNAPSHOT semantics), so that the paths besides the newest-request one run:
+      * Accept (Accept.java:84-117): Commands.accept ran first, so the txn -- one of the history's
+        in-flight txns (an entry PREACCEPTED or ACCEPTED) -- sits in its keys' CommandsForKey as
+        ACCEPTED with the proposed executeAt E, newer than every id of the store; the request is
+        that txnId over all of its keys, deps computed at S = E with the txnId itself excluded
+        (PreAccept.java:261; Accept.calculatePartialDeps, Accept.java:113-117).
+      * out-of-order PreAccept: txnId (= executeAt) inside the last `unordered_window` hlc ticks of
+        the history, older than the newest entries of busy keys (a coordinator whose clock lags);
+        keys and kind unchanged.
+      * the rest: fresh PreAccepts newer than everything (config 2 as generated).
+    The fractions pick disjoint random subsets of the requests (Accepts capped by the number of
+    in-flight history txns)."""
+    q = w.queries
+    n = len(q)
+    rng = np.random.default_rng(seed)
+    u = rng.random(n)
+    cfk = w.cfk
+    n_hist = int(w.params.get("n_hist_entries", w.params.get("n_hist_entries_per_gpu"))) // int(w.params["keys_per_txn"])
+    ent_j = (cfk.txn.lsb >> np.uint64(16)).astype(np.int64) - 1
+    ent_key = np.repeat(cfk.keys, np.diff(cfk.seg.astype(np.int64)))
+    inflight = (cfk.status == A.ST_PREACCEPTED) | (cfk.status == A.ST_ACCEPTED)
+    cand = np.unique(ent_j[inflight])
+    want = np.nonzero(u < accept_frac)[0]
+    n_acc = min(len(want), len(cand))
+    ai = np.sort(rng.choice(want, n_acc, replace=False)) if n_acc else np.zeros(0, np.int64)
+    acc = np.zeros(n, bool)
+    acc[ai] = True
+    uno = (u >= accept_frac) & (u < accept_frac + unordered_frac)
+    js = rng.choice(cand, n_acc, replace=False) if n_acc else np.zeros(0, np.int64)
+    # the accepted txns' entries, grouped by request (ascending keys: entries are in key order)
+    req_of_j = np.full(n_hist, -1, np.int64)
+    req_of_j[js] = np.arange(n_acc)
+    ej = req_of_j[ent_j]
+    sel = np.nonzero(ej >= 0)[0]
+    sel = sel[np.lexsort((ent_key[sel], ej[sel]))]
+    a_cnt = np.bincount(ej[sel], minlength=n_acc)
+    a_first = np.zeros(n_acc, np.int64)
+    if n_acc:
+        a_first[1:] = np.cumsum(a_cnt)[:-1]
+    # request ids and keys
+    flags = q.txn.lsb & np.uint64(0xFFFF)
+    node = q.txn.node.copy()
+    msb, lsb = q.txn.msb.copy(), q.txn.lsb.copy()
+    ui = np.nonzero(uno)[0]
+    win = max(1, int(unordered_window))
+    k = np.arange(len(ui), dtype=np.uint64)
+    late = make_timestamps(1, np.uint64(max(1, n_hist - win)) + (k % np.uint64(win)), flags[ui],
+                           17 + (k // np.uint64(win)).astype(np.int32))
+    msb[ui], lsb[ui], node[ui] = late.msb, late.lsb, late.node
+    jt = cfk.txn.take(sel[a_first]) if n_acc else cfk.txn.take(np.zeros(0, np.int64))
+    msb[ai], lsb[ai], node[ai] = jt.msb, jt.lsb, jt.node
+    txn = Tids(msb, lsb, node)
+    E = make_timestamps(1, np.uint64(n_hist + 2000 + n + 1000) + np.arange(n_acc, dtype=np.uint64),
+                        jt.lsb & np.uint64(0xFFFF), EXEC_NODE_BASE + (1 << 22) + np.arange(n_acc))
+    ex = Tids(msb.copy(), lsb.copy(), node.copy())
+    ex.msb[ai], ex.lsb[ai], ex.node[ai] = E.msb, E.lsb, E.node
+    ko = q.key_off.astype(np.int64)
+    cnt = np.diff(ko)
+    cnt[ai] = a_cnt
+    key_off = np.zeros(n + 1, np.uint64)
+    key_off[1:] = np.cumsum(cnt)
+    keep_old = ~np.repeat(acc, np.diff(ko))
+    dst_old = np.repeat(~acc, cnt)
+    keys = np.zeros(int(key_off[-1]), np.int64)
+    keys[dst_old] = q.keys[keep_old]
+    keys[~dst_old] = ent_key[sel]
+    q2 = Queries(txn, ex, key_off, keys, q.min_epoch)
+    # Commands.accept: the in-flight entries of an accepted txn become ACCEPTED at E
+    st = cfk.status.copy()
+    e_msb, e_lsb, e_node = cfk.exec.msb.copy(), cfk.exec.lsb.copy(), cfk.exec.node.copy()
+    up = sel[inflight[sel]]
+    r = ej[up]
+    st[up] = A.ST_ACCEPTED
+    e_msb[up], e_lsb[up], e_node[up] = E.msb[r], E.lsb[r], E.node[r]
+    cfk2 = CfkSnapshot(cfk.keys, cfk.seg, cfk.txn, Tids(e_msb, e_lsb, e_node), st, cfk.pruned_before)
+    p = dict(w.params)
+    p.update(accept_frac=accept_frac, unordered_frac=unordered_frac, unordered_window=unordered_window,
+             n_accept=int(n_acc), n_unordered=int(len(ui)))
+    return Workload(w.name + "_mix", cfk2, w.cmds, w.redundant, q2, w.flags, p, w.range_start_inclusive, w.slices)
 
 
 def _uniform(h):

@@ -192,6 +192,9 @@ struct ad_ctx {
     DevBuf d_rlvl[NCLASS][MAX_LEVELS];
     DevBuf d_rb_s, d_rb_e, d_rb_e0, d_rb_e1, d_rb_wm, d_rb_rid, d_slices_s, d_slices_e;
     DevBuf d_dict_lsb_raw, d_rt_start, d_rt_end;   // raw ids and range table (multi-GPU export)
+    DevBuf d_ds_hi, d_ds_lo, d_ds_node;            // every DICT_SAMP-th dictionary id (rank searches)
+    DevBuf d_kline, d_kslot, d_kcell, d_kl_disp;   // KeyLine table; per key its line and stabbing cell; displacements
+    uint64_t kline_slots = 0;
 
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
@@ -200,8 +203,10 @@ struct ad_ctx {
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
     DevBuf arena, rarena;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, p_slot, q_rec, p_cell;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, q_rec;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
+    uint64_t o_cap[9] = {};                    // capacities of the packed outputs (elements)
+    DevBuf lb_agg, lb_inc;                     // tile sums and their prefixes (run_pack_lb)
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t ev_slot = nullptr;      // fused path: after k_prepare
@@ -646,6 +651,61 @@ static int build_snapshot(ad_ctx* c)
         }
     });
     std::vector<KeyEntry> kent(std::max<uint64_t>(nk, 1));
+    std::vector<uint32_t> kslot(std::max<uint64_t>(nk, 1)), kcells(std::max<uint64_t>(nk, 1), NO_CELL);
+    // perfect hash of the keys onto KeyLines (hash and displace, common.hpp): buckets of ~4 keys,
+    // the biggest placed first, each with the first displacement that puts all its keys on free lines
+    uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
+    std::vector<uint32_t> kl_disp(kl_nb, 0);
+    {
+        uint64_t m = std::max<uint64_t>(1, nk + nk / 4);
+        std::vector<uint64_t> bo(kl_nb + 1, 0);
+        std::vector<uint32_t> bk(nk);
+        for (uint64_t k = 0; k < nk; ++k) ++bo[kl_bucket(key_hash(K.keys[k]), kl_nb) + 1];
+        for (uint64_t b = 0; b < kl_nb; ++b) bo[b + 1] += bo[b];
+        {
+            std::vector<uint64_t> cur(bo.begin(), bo.end() - 1);
+            for (uint64_t k = 0; k < nk; ++k) bk[cur[kl_bucket(key_hash(K.keys[k]), kl_nb)]++] = (uint32_t)k;
+        }
+        std::vector<uint32_t> border(kl_nb);
+        for (uint64_t b = 0; b < kl_nb; ++b) border[b] = (uint32_t)b;
+        std::stable_sort(border.begin(), border.end(), [&](uint32_t a, uint32_t b) { return bo[a + 1] - bo[a] > bo[b + 1] - bo[b]; });
+        for (int attempt = 0;; ++attempt)
+        {
+            std::vector<uint8_t> used(m, 0);
+            bool ok = true;
+            std::vector<uint64_t> pos;
+            for (uint32_t b : border)
+            {
+                const uint64_t b0 = bo[b], b1 = bo[b + 1];
+                if (b0 == b1) continue;
+                uint32_t d = 0;
+                for (;; ++d)
+                {
+                    if (d == (1u << 22)) { ok = false; break; }
+                    pos.clear();
+                    bool fit = true;
+                    for (uint64_t i = b0; i < b1 && fit; ++i)
+                    {
+                        const uint64_t p = kl_index(key_hash2(K.keys[bk[i]]), d, m);
+                        if (used[p] || std::find(pos.begin(), pos.end(), p) != pos.end()) fit = false;
+                        pos.push_back(p);
+                    }
+                    if (fit) break;
+                }
+                if (!ok) break;
+                kl_disp[b] = d;
+                for (uint64_t i = b0; i < b1; ++i)
+                {
+                    used[pos[i - b0]] = 1;
+                    kslot[bk[i]] = (uint32_t)pos[i - b0];
+                }
+            }
+            if (ok) break;
+            if (attempt == 4) return c->fail(AD_E_DEVICE, "key perfect hash did not converge");
+            m += m / 2;              // more room, try again
+        }
+        c->kline_slots = m;
+    }
     for (uint64_t k = 0; k < nk; ++k)
     {
         uint64_t h = key_hash(K.keys[k]) & (hcap - 1);
@@ -658,6 +718,7 @@ static int build_snapshot(ad_ctx* c)
                                                              : std::lower_bound(cell_E.begin(), cell_E.end(), x) - cell_E.begin());
         }
         khash[h] = KeySlot{K.keys[k], (uint32_t)k, kcell};
+        kcells[k] = kcell;
         KeyEntry& ke = kent[k];
         ke.last_w_txn = last_w_txn[k];
         ke.last_txn = krec[k].last_txn;
@@ -678,9 +739,20 @@ static int build_snapshot(ad_ctx* c)
         if ((rc = upload(c, c->d_status, K.status)) || (rc = upload(c, c->d_xrank, exec_rank)) || (rc = upload(c, c->d_ekey, ekey)))
             return rc;
     }
+    std::vector<uint64_t> shi, slo;
+    std::vector<int32_t> snode;
+    for (uint64_t i = 0; i < dhi.size(); i += DICT_SAMP)
+    {
+        shi.push_back(dhi[i]);
+        slo.push_back(dlo[i]);
+        snode.push_back(dnode[i]);
+    }
+    if ((rc = upload(c, c->d_ds_hi, shi)) || (rc = upload(c, c->d_ds_lo, slo)) || (rc = upload(c, c->d_ds_node, snode)))
+        return rc;
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
         (rc = upload(c, c->d_keys, K.keys)) || (rc = upload(c, c->d_krec, krec)) || (rc = upload(c, c->d_khash, khash)) || (rc = upload(c, c->d_kent, kent)) || (rc = upload(c, c->d_cand, cand)) || (rc = upload(c, c->d_cwr, cwr)) ||
-        (rc = upload(c, c->d_ent, ent)) ||
+        (rc = upload(c, c->d_ent, ent)) || (rc = upload(c, c->d_kslot, kslot)) || (rc = upload(c, c->d_kcell, kcells)) ||
+        (rc = upload(c, c->d_kl_disp, kl_disp)) ||
         (rc = upload(c, c->d_w, w)) || (rc = upload(c, c->d_slices_s, c->slice_s)) || (rc = upload(c, c->d_slices_e, c->slice_e)) ||
         (rc = upload(c, c->d_dict_lsb_raw, c->dict_lsb)) || (rc = upload(c, c->d_rt_start, c->rt_start)) ||
         (rc = upload(c, c->d_rt_end, c->rt_end)))
@@ -692,6 +764,10 @@ static int build_snapshot(ad_ctx* c)
     s.dict_lo = c->d_dict_lo.as<uint64_t>();
     s.dict_node = c->d_dict_node.as<int32_t>();
     s.n_dict = dhi.size();
+    s.ds_hi = c->d_ds_hi.as<uint64_t>();
+    s.ds_lo = c->d_ds_lo.as<uint64_t>();
+    s.ds_node = c->d_ds_node.as<int32_t>();
+    s.n_samp = shi.size();
     if (!dhi.empty())
     {
         s.dict_last_hi = dhi.back();
@@ -760,6 +836,14 @@ static int build_snapshot(ad_ctx* c)
     s.elide = c->cfg.elide;
     HIPCHK(c, build_cfk_trees(s, c->stream));
     HIPCHK(c, build_range_trees(s, c->stream));
+    // the lean kernels' KeyLine table, indexed by the keys' perfect hash
+    if (!c->d_kline.ensure(sizeof(KeyLine) * c->kline_slots)) return c->fail(AD_E_NOMEM, "key lines");
+    s.kline = c->d_kline.as<KeyLine>();
+    s.kl_lines = c->kline_slots;
+    s.kl_buckets = kl_nb;
+    s.kl_disp = c->d_kl_disp.as<uint32_t>();
+    HIPCHK(c, run_build_klines(s, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
+                               c->kline_slots, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->h_txn_rank.swap(txn_rank);
     c->h_exec_rank.swap(exec_rank);
@@ -1008,12 +1092,10 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
         !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
-        !ens<uint32_t>(c->p_slot, np) || !ens<uint4>(c->q_rec, n) || !ens<uint32_t>(c->p_cell, np) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
+        !ens<uint4>(c->q_rec, n) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
         !ens<uint32_t>(c->deferred2, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64))
         return c->fail(AD_E_NOMEM, "batch buffers");
-    b.p_slot = c->p_slot.as<uint32_t>();
     b.q_rec = c->q_rec.as<uint4>();
-    b.p_cell = c->p_cell.as<uint32_t>();
     b.deferred1 = c->deferred1.as<uint32_t>();
     b.deferred2 = c->deferred2.as<uint32_t>();
     b.sz = c->sz.as<uint32_t>(); b.off = c->off.as<uint64_t>(); b.bsum = c->bsum.as<uint64_t>();
@@ -1088,14 +1170,50 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         if (!c->h_ctl) HIPCHK(c, hipHostMalloc((void**)&c->h_ctl, sizeof(BatchCtl), hipHostMallocDefault));
         if (!c->ev_sp0) HIPCHK(c, hipEventCreate(&c->ev_sp0));
         if (!c->ev_sp1) HIPCHK(c, hipEventCreate(&c->ev_sp1));
-        // offsets of every request's three maps, totals into the control block, one host round trip
+        // offsets + totals + packed arrays (tile sums, their scan, streaming per-tile scan + pack), the
+        // packed arrays sized beforehand (grown to the totals and packed again when too small): the
+        // only host round trip of a batch is the final read of the control block
+        const uint64_t tiles = lb_tiles(n);
+        if (!ens<uint64_t>(c->lb_agg, 9 * tiles) || !ens<uint64_t>(c->lb_inc, 9 * tiles))
+            return c->fail(AD_E_NOMEM, "tile sums");
+        b.lb_agg = c->lb_agg.as<uint64_t>();
+        b.lb_inc = c->lb_inc.as<uint64_t>();
+        auto bind_outputs = [&]() -> int {
+            for (int m = 0; m < 3; ++m)
+            {
+                if (!ens<int64_t>(c->o_keys[m], c->o_cap[3 * m]) || !ens<uint32_t>(c->o_txns[m], c->o_cap[3 * m + 1]) ||
+                    !ens<int32_t>(c->o_k2t[m], c->o_cap[3 * m + 2]))
+                    return c->fail(AD_E_NOMEM, "outputs");
+                b.o_keys[m] = c->o_keys[m].as<int64_t>();
+                b.o_txns[m] = c->o_txns[m].as<uint32_t>();
+                b.o_k2t[m] = c->o_k2t[m].as<int32_t>();
+            }
+            for (int a = 0; a < 9; ++a) b.o_cap[a] = parts_only ? 0 : c->o_cap[a];
+            return 0;
+        };
+        if (!parts_only)
+        {
+            // first use: keys <= probes per map; ids and keysToTxnIds a guess (grown on overflow)
+            for (int m = 0; m < 3; ++m)
+            {
+                c->o_cap[3 * m] = std::max<uint64_t>(c->o_cap[3 * m], np);
+                c->o_cap[3 * m + 1] = std::max<uint64_t>(c->o_cap[3 * m + 1], 2 * np);
+                c->o_cap[3 * m + 2] = std::max<uint64_t>(c->o_cap[3 * m + 2], 4 * np);
+            }
+            if ((rc = bind_outputs())) return rc;
+        }
+        auto pack_pass = [&]() -> int {
+            HIPCHK(c, hipEventRecord(c->ev[4], st));
+            HIPCHK(c, run_pack_lb(b, !parts_only, st));
+            HIPCHK(c, hipEventRecord(c->ev[5], st));
+            HIPCHK(c, hipMemcpyAsync(c->h_ctl, b.ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+            h = *c->h_ctl;
+            return 0;
+        };
         HIPCHK(c, hipEventRecord(c->ev[2], st));
-        HIPCHK(c, run_offsets(b, st));
-        HIPCHK(c, run_collect_totals(b, st));
         HIPCHK(c, hipEventRecord(c->ev[3], st));
-        HIPCHK(c, hipMemcpyAsync(c->h_ctl, b.ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
-        h = *c->h_ctl;
+        if ((rc = pack_pass())) return rc;
         double ms_split = 0;
         if (!split_only)
         {
@@ -1130,19 +1248,15 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 sb.q_keys = c->s_k.as<int64_t>();
                 if ((rc = run_split(c, sb, st))) return rc;
                 HIPCHK(c, run_defer_scatter(b, b.deferred, nd, sb.sz, sb.t_reg, st));
-                HIPCHK(c, run_offsets(b, st));
-                HIPCHK(c, run_collect_totals(b, st));
+                // the requests are complete now: pack (k_pack_lb skips batches with split deferrals)
+                HIPCHK(c, hipMemsetAsync(&b.ctl->n_deferred, 0, sizeof(unsigned long long), st));
                 HIPCHK(c, hipEventRecord(c->ev_sp1, st));
-                HIPCHK(c, hipMemcpyAsync(c->h_ctl, b.ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, st));
-                HIPCHK(c, hipStreamSynchronize(st));
-                h = *c->h_ctl;
+                if ((rc = pack_pass())) return rc;
                 float msp = 0;
                 HIPCHK(c, hipEventElapsedTime(&msp, c->ev_sp0, c->ev_sp1));
                 ms_split = msp;
             }
         }
-        uint64_t tot[9];
-        for (int a = 0; a < 9; ++a) tot[a] = h.tot[a];
         if (h.error)
         {
             if (h.error == ERR_STATE)
@@ -1150,7 +1264,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             return c->fail(AD_E_INVAL, recovery_scan >= 0 ? "invalid Txn.Kind for witnessedBy() in a request (Txn.java:247-262)"
                                                           : "invalid Txn.Kind for witnesses() in a request (Txn.java:221-235)");
         }
-        if (h.overflow)
+        if (h.overflow & 15u)
         {
             if (h.overflow & 1u) c->key_cap = std::max<uint64_t>(c->key_cap * 2, h.key_top + (h.key_top >> 1));
             if (h.overflow & 2u) c->rng_cap = std::max<uint64_t>(c->rng_cap * 2, h.rng_top + (h.rng_top >> 1));
@@ -1158,25 +1272,22 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             if (h.overflow & 8u) c->reg_cap = std::max<uint64_t>(c->reg_cap * 2, h.reg_top + (h.reg_top >> 1));
             continue;
         }
-        if (!parts_only)
-            for (int m = 0; m < 3; ++m)
-            {
-                if (!ens<int64_t>(c->o_keys[m], tot[3 * m + 0]) || !ens<uint32_t>(c->o_txns[m], tot[3 * m + 1]) ||
-                    !ens<int32_t>(c->o_k2t[m], tot[3 * m + 2]))
-                    return c->fail(AD_E_NOMEM, "outputs");
-                b.o_keys[m] = c->o_keys[m].as<int64_t>();
-                b.o_txns[m] = c->o_txns[m].as<uint32_t>();
-                b.o_k2t[m] = c->o_k2t[m].as<int32_t>();
-            }
-        HIPCHK(c, hipEventRecord(c->ev[4], st));
-        if (!parts_only) HIPCHK(c, run_pack(b, st));
-        HIPCHK(c, hipEventRecord(c->ev[5], st));
+        if (h.overflow & OVF_PACK)
+        {
+            // packed arrays too small: grow them to the totals (with slack for the next batches), pack again
+            for (int a = 0; a < 9; ++a) c->o_cap[a] = std::max<uint64_t>(c->o_cap[a], h.tot[a] + h.tot[a] / 4);
+            if ((rc = bind_outputs())) return rc;
+            HIPCHK(c, hipMemsetAsync(&b.ctl->overflow, 0, sizeof(unsigned int), st));
+            if ((rc = pack_pass())) return rc;
+            if (h.overflow) return c->fail(AD_E_DEVICE, "pack overflow after growing the outputs to the totals");
+        }
+        uint64_t tot[9];
+        for (int a = 0; a < 9; ++a) tot[a] = h.tot[a];
         // the regions of this batch, for ad_parts_export of a parts-only result
         c->last_reg = b.reg;
         c->last_t_reg = b.t_reg;
         c->last_n = n;
         c->last_parts_only = parts_only;
-        HIPCHK(c, hipStreamSynchronize(st));
 
         ad_stats& S = out->stats;
         memset(&S, 0, sizeof(S));
@@ -2245,8 +2356,21 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         HIPCHK(c, hipMemcpy(c->dict_lsb.data() + nd0, c->d_dict_lsb_raw.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(c->dict_node.data() + nd0, c->d_dict_node.as<int32_t>() + nd0, 4 * add, hipMemcpyDeviceToHost));
         c->global_ok = false;        // global ranks of the multi-store exchange no longer cover the dictionary
+        // the sampled index over the grown dictionary (a stale one is still correct, only slower)
+        const uint64_t ns = dict_samples(c->ds.n_dict);
+        if (c->d_ds_hi.ensure(8 * ns + 8 * ns / 4) && c->d_ds_lo.ensure(8 * ns + 8 * ns / 4) && c->d_ds_node.ensure(4 * ns + 4 * ns / 4))
+        {
+            c->ds.ds_hi = c->d_ds_hi.as<uint64_t>();
+            c->ds.ds_lo = c->d_ds_lo.as<uint64_t>();
+            c->ds.ds_node = c->d_ds_node.as<int32_t>();
+            HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
+            c->ds.n_samp = ns;
+        }
     }
     if (o.n_inserted) c->host_moved = true;
+    if ((rc == 0 || o.rolled_back) && c->kline_slots)
+        HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
+                                   c->kline_slots, st));
     if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back)
     {
         // the derived arrays may be half built: rebuild them from the entries at the next use

@@ -121,12 +121,66 @@ struct alignas(64) KeyEntry {
 };
 static_assert(sizeof(KeyEntry) == 64, "KeyEntry is half a cache line");
 
+// The lean kernels' per-key record: one 128-byte line (one L2 line) per key in a table indexed by a
+// perfect hash of the key ordinal (kl_index), so a (request, key) probe costs one random line: the
+// key test, the newest test, the emission counts and -- for keys whose emissions fit -- the
+// emissions themselves.
+//   [0, 8)    key
+//   [8, 16)   the key's entries in the range stabbing index: cell_ent[cell_lo, cell_hi)
+//   [16, 28)  last txnId rank, last committed Write's executeAt rank and txnId rank (0: none)
+//   [28, 32)  meta: KL_USED | KL_INLINE | KL_NOLEAN | inline offset of the cwr tail << 24 | #cwr tail
+//   [32, 56)  per witness class c: {#never-elided entries of class c, their start in cand}
+//   [56, 64)  start of the cwr tail in cwr
+//   [64, 128) inline emissions when #class-2 entries + #cwr tail <= KL_INL: the never-elided
+//             entries nested by class -- Writes, then Reads, then SyncPoints/ExclusiveSyncPoints
+//             (class c's list is the first n_c of them) -- then the cwr tail
+struct KeyClassSpan { uint32_t n, base; };
+struct alignas(128) KeyLine {
+    int64_t key;
+    uint32_t cell_lo, cell_hi;
+    uint32_t last_txn, last_wexec, last_w_txn, meta;
+    KeyClassSpan cls[NCLASS];
+    uint32_t cwr_tail, pad;
+    uint32_t inl[16];
+};
+static_assert(sizeof(KeyLine) == 128, "KeyLine is one cache line");
+constexpr uint32_t KL_INL = 16;
+constexpr uint32_t KL_USED = 1u << 31;
+constexpr uint32_t KL_INLINE = 1u << 30;
+constexpr uint32_t KL_NOLEAN = 1u << 29;          // counts beyond the meta fields: the general kernel serves it
+constexpr uint32_t KL_NCWR_MASK = (1u << 24) - 1;
+constexpr uint32_t KL_INL_SHIFT = 24;             // 5 bits (<= KL_INL)
+
 __host__ __device__ inline uint64_t key_hash(int64_t k)
 {
     uint64_t z = (uint64_t)k + 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
+}
+
+// Perfect hash of a snapshot's keys onto KeyLine indices (hash and displace): key k lives at
+// kl_index(key_hash2(k), disp[kl_bucket(key_hash(k))]); the displacements are chosen at ingest so
+// that no two keys share a line. One small (cache-resident) lookup, then exactly one line.
+__host__ __device__ inline uint64_t key_hash2(int64_t k)
+{
+    uint64_t z = (uint64_t)k ^ 0xD1B54A32D192ED03ULL;
+    z = (z ^ (z >> 33)) * 0xFF51AFD7ED558CCDULL;
+    z = (z ^ (z >> 33)) * 0xC4CEB9FE1A85EC53ULL;
+    return z ^ (z >> 33);
+}
+__host__ __device__ inline uint64_t mulhi64(uint64_t a, uint64_t b)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+__host__ __device__ inline uint64_t kl_bucket(uint64_t h, uint64_t n_buckets) { return mulhi64(h, n_buckets); }
+__host__ __device__ inline uint64_t kl_index(uint64_t g, uint32_t d, uint64_t n_lines)
+{
+    return mulhi64(g ^ ((uint64_t)d * 0x9E3779B97F4A7C15ULL), n_lines);
 }
 
 // Per-store device snapshot, passed to kernels by value.
@@ -138,12 +192,21 @@ struct DevSnapshot {
     uint64_t n_dict;
     uint64_t dict_last_hi, dict_last_lo;   // the newest dictionary id (request fast path: newer than all)
     int32_t dict_last_node;
+    // every DICT_SAMP-th dictionary id (cache-resident): a rank search touches HBM only inside one
+    // DICT_SAMP-id window of the dictionary
+    const uint64_t* ds_hi;
+    const uint64_t* ds_lo;
+    const int32_t*  ds_node;
+    uint64_t n_samp;
     // CommandsForKey
     uint64_t n_keys;
     const int64_t*  keys;          // [n_keys]
     const KeyRec*   krec;          // [n_keys]
     const KeySlot*  khash;         // [khash_mask + 1]
     const KeyEntry* kent;          // [n_keys] newest-test fields + list bounds (fused kernels)
+    const KeyLine*  kline;         // [kl_lines] the lean kernels' per-key lines (perfect hash)
+    const uint32_t* kl_disp;       // [kl_buckets] displacements
+    uint64_t kl_lines, kl_buckets;
     const uint32_t* cand;          // never-elided entries per key and class: txw (rank | kind << 29)
     const uint32_t* cwr;           // committed Read/Write entries per key by executeAt: txw
     uint64_t khash_mask;
@@ -182,6 +245,50 @@ struct DevSnapshot {
     int start_inclusive;
     int elide;
 };
+
+constexpr uint64_t DICT_SAMP = 256;
+inline uint64_t dict_samples(uint64_t n_dict) { return (n_dict + DICT_SAMP - 1) / DICT_SAMP; }
+
+// Rank of an arbitrary id in the dictionary (member i -> 2i+1, else 2 * lower bound; above every
+// member: 2 * n_dict without a load): binary search of the sample, then of one window.
+template <class Snap>
+__device__ inline uint32_t dict_rank_sampled(const Snap& s, const NormTid& t)
+{
+    if (s.n_dict == 0) return 0;
+    const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
+    const int cl = norm_cmp(last, t);
+    if (cl < 0) return (uint32_t)(2 * s.n_dict);
+    if (cl == 0) return (uint32_t)(2 * s.n_dict - 1);
+    uint64_t a = 0, b = s.n_samp;
+    while (a < b)
+    {
+        const uint64_t m = (a + b) >> 1;
+        const NormTid d{s.ds_hi[m], s.ds_lo[m], s.ds_node[m]};
+        if (norm_cmp(d, t) <= 0) a = m + 1;
+        else b = m;
+    }
+    uint64_t lo = a ? (a - 1) * DICT_SAMP : 0, hi = a < s.n_samp ? a * DICT_SAMP : s.n_dict;
+    while (lo < hi)
+    {
+        const uint64_t m = (lo + hi) >> 1;
+        const uint64_t dh = s.dict_hi[m];
+        bool less = dh < t.hi;
+        if (dh == t.hi)
+        {
+            const NormTid d{dh, s.dict_lo[m], s.dict_node[m]};
+            less = norm_cmp(d, t) < 0;
+        }
+        if (less) lo = m + 1;
+        else hi = m;
+    }
+    bool eq = false;
+    if (lo < s.n_dict)
+    {
+        const NormTid d{s.dict_hi[lo], s.dict_lo[lo], s.dict_node[lo]};
+        eq = norm_cmp(d, t) == 0;
+    }
+    return (uint32_t)(2 * lo + (eq ? 1 : 0));
+}
 
 // Range.contains(key) (Range.java:40-56 EndInclusive, :84-100 StartInclusive)
 __host__ __device__ inline bool range_contains(int start_inclusive, int64_t s, int64_t e, int64_t key)

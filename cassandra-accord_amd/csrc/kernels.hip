@@ -931,7 +931,6 @@ __device__ __forceinline__ void pack_run(const uint8_t* __restrict__ reg, const 
                                          uint64_t total, T* __restrict__ out)
 {
     const uint32_t lane = lane_id();
-    uint32_t r = 0;
     for (uint64_t xb = 0; xb < total; xb += 64 * PACK_UNROLL)
     {
         const T* p[PACK_UNROLL];
@@ -941,8 +940,17 @@ __device__ __forceinline__ void pack_run(const uint8_t* __restrict__ reg, const 
         {
             const uint64_t x = xb + u * 64 + lane;
             ok[u] = x < total;
-            if (ok[u])
-                while (st[r + 1] <= (uint32_t)x) ++r;
+            // owning request: the last r with st[r] <= x (binary search of the 65 starts in LDS;
+            // a linear walk costs up to 64 dependent LDS reads per element)
+            uint32_t lo = 0, hi = 64;
+#pragma unroll
+            for (int it = 0; it < 7; ++it)
+            {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (st[mid] <= (uint32_t)x) lo = mid;
+                else hi = mid - 1;
+            }
+            const uint32_t r = lo;
             p[u] = ok[u] ? reinterpret_cast<const T*>(reg + src[r]) + ((uint32_t)x - st[r]) : reinterpret_cast<const T*>(reg);
         }
         T v[PACK_UNROLL];
@@ -994,6 +1002,186 @@ hipError_t run_pack(const BatchBufs& b, hipStream_t st)
     if (!b.n_txns) return hipSuccess;
     const uint64_t waves = (b.n_txns + 63) / 64;
     k_pack<<<(unsigned)((waves + PACK_WAVES - 1) / PACK_WAVES), 64 * PACK_WAVES, 0, st>>>(b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// scan + pack without a host round trip: reduce -> scan of tile sums -> pack
+// ---------------------------------------------------------------------------------------
+// Tiles of LB_TILE consecutive requests. k_tile_sums: the 9 size sums of every tile. k_tile_scan
+// (one block): exclusive prefixes of the tile sums and the batch totals (into the control block).
+// k_pack_tiles: a tile scans its 9 size arrays in LDS, adds its tile prefix, writes its offsets and
+// packs its requests' regions into the final arrays (64 requests per wave, fully coalesced writes).
+// The output arrays are sized before the launches; a tile whose run would not fit sets OVF_PACK and
+// copies nothing (the host grows them to the totals and runs the pack again). No inter-workgroup
+// waiting: every block streams.
+__global__ __launch_bounds__(LB_TILE) void k_tile_sums(BatchBufs b)
+{
+    constexpr uint32_t NW = LB_TILE / 64;
+    __shared__ uint64_t s_w[NW][9];
+    const BatchCtl* cc = b.ctl;
+    if (cc->n_deferred || cc->error || (cc->overflow & 15u)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint64_t n = b.n_txns, t = (uint64_t)blockIdx.x * LB_TILE + tid;
+#pragma unroll 1
+    for (int a = 0; a < 9; ++a)
+    {
+        uint64_t x = t < n ? b.sz[(uint64_t)a * n + t] : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+        if (lane == 0) s_w[w][a] = x;
+    }
+    __syncthreads();
+    if (tid < 9)
+    {
+        uint64_t acc = 0;
+#pragma unroll
+        for (uint32_t ww = 0; ww < NW; ++ww) acc += s_w[ww][tid];
+        b.lb_agg[(uint64_t)blockIdx.x * 9 + tid] = acc;
+    }
+}
+
+// one block of 1024 threads: lb_inc[tile][a] = exclusive prefix of lb_agg over tiles, totals. Thread
+// i owns the consecutive tiles [i * per, (i + 1) * per): a serial sum, one block scan, a serial pass.
+__global__ __launch_bounds__(1024) void k_tile_scan(BatchBufs b, uint64_t tiles)
+{
+    __shared__ uint64_t s_w[16][9];
+    const BatchCtl* cc = b.ctl;
+    if (cc->n_deferred || cc->error || (cc->overflow & 15u)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint64_t per = (tiles + 1023) / 1024;
+    const uint64_t i0 = tid * per, i1 = i0 + per < tiles ? i0 + per : tiles;
+#pragma unroll 1
+    for (int a = 0; a < 9; ++a)
+    {
+        uint64_t sum = 0;
+        for (uint64_t i = i0; i < i1; ++i) sum += b.lb_agg[i * 9 + a];
+        uint64_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if ((int)lane >= d) x += y;
+        }
+        if (lane == 63) s_w[w][a] = x;
+        __syncthreads();
+        uint64_t wpre = 0, tot = 0;
+#pragma unroll
+        for (uint32_t ww = 0; ww < 16; ++ww)
+        {
+            const uint64_t y = s_w[ww][a];
+            if (ww < w) wpre += y;
+            tot += y;
+        }
+        uint64_t e = wpre + x - sum;
+        for (uint64_t i = i0; i < i1; ++i)
+        {
+            const uint64_t y = b.lb_agg[i * 9 + a];
+            b.lb_inc[i * 9 + a] = e;
+            e += y;
+        }
+        if (tid == 0)
+        {
+            b.ctl->tot[a] = tot;
+            b.off[(uint64_t)a * (b.n_txns + 1) + b.n_txns] = tot;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
+{
+    constexpr uint32_t NW = LB_TILE / 64;
+    __shared__ uint64_t s_ex[9][LB_TILE + 1];    // offsets of the tile's requests (+ the tile end)
+    __shared__ uint64_t s_wsum[NW][9], s_wo[NW][9];
+    __shared__ uint32_t s_start[NW][65];
+    __shared__ uint64_t s_src[NW][64];
+    const BatchCtl* cc = b.ctl;
+    if (cc->n_deferred || cc->error || (cc->overflow & 15u)) return;
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+    const uint32_t tile = blockIdx.x;
+    const uint64_t n = b.n_txns;
+    const uint64_t t = (uint64_t)tile * LB_TILE + tid;
+    const bool on = t < n;
+#pragma unroll 1
+    for (int a = 0; a < 9; ++a)
+    {
+        const uint64_t v = on ? b.sz[(uint64_t)a * n + t] : 0u;
+        uint64_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if ((int)lane >= d) x += y;
+        }
+        s_ex[a][tid] = x - v;
+        if (lane == 63) s_wsum[w][a] = x;
+    }
+    __syncthreads();
+    if (tid < 9)
+    {
+        uint64_t acc = b.lb_inc[(uint64_t)tile * 9 + tid];
+#pragma unroll
+        for (uint32_t ww = 0; ww < NW; ++ww)
+        {
+            s_wo[ww][tid] = acc;
+            acc += s_wsum[ww][tid];
+        }
+        s_ex[tid][LB_TILE] = acc;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int a = 0; a < 9; ++a)
+    {
+        const uint64_t e = s_wo[w][a] + s_ex[a][tid];
+        s_ex[a][tid] = e;
+        if (on) b.off[(uint64_t)a * (n + 1) + t] = e;
+    }
+    if (!copy) return;
+    __syncthreads();
+    // pack: wave w copies requests [64 w, 64 w + 64) of the tile; per (map, array) one contiguous run
+    uint32_t* st = s_start[w];
+    uint64_t* src = s_src[w];
+    const uint64_t t0 = (uint64_t)tile * LB_TILE + 64 * w;
+    if (t0 >= n) return;
+    const uint32_t i0 = 64 * w, i1 = 64 * w + 64;     // s_ex[a][i1]: the next wave's start or the tile end
+#pragma unroll 1
+    for (int m = 0; m < 3; ++m)
+    {
+        const uint32_t nk = (uint32_t)(s_ex[3 * m][tid + 1] - s_ex[3 * m][tid]);
+        const uint32_t U = (uint32_t)(s_ex[3 * m + 1][tid + 1] - s_ex[3 * m + 1][tid]);
+        const uint64_t rb = on ? b.t_reg[(uint64_t)m * n + t] : 0;
+#pragma unroll 1
+        for (int k = 0; k < 3; ++k)
+        {
+            const int a = 3 * m + k;
+            const uint64_t o0 = s_ex[a][i0];
+            const uint64_t total = s_ex[a][i1] - o0;
+            if (total == 0) continue;
+            if (o0 + total > b.o_cap[a])
+            {
+                if (lane == 0) atomicOr(&b.ctl->overflow, OVF_PACK);
+                continue;
+            }
+            wave_lds_sync();
+            st[lane] = on ? (uint32_t)(s_ex[a][tid] - o0) : (uint32_t)total;
+            if (lane == 0) st[64] = (uint32_t)total;
+            src[lane] = rb + (k == 0 ? 0 : (k == 1 ? 8ull * nk : 8ull * nk + 4ull * U));
+            wave_lds_sync();
+            if (k == 0) pack_run<int64_t>(b.reg, st, src, total, b.o_keys[m] + o0);
+            else if (k == 1) pack_run<uint32_t>(b.reg, st, src, total, b.o_txns[m] + o0);
+            else pack_run<int32_t>(b.reg, st, src, total, b.o_k2t[m] + o0);
+        }
+    }
+}
+
+hipError_t run_pack_lb(const BatchBufs& b, bool copy, hipStream_t st)
+{
+    if (!b.n_txns) return hipMemsetAsync(b.off, 0, sizeof(uint64_t) * 9, st);     // off[a][0] = 0
+    const uint64_t tiles = lb_tiles(b.n_txns);
+    k_tile_sums<<<(unsigned)tiles, LB_TILE, 0, st>>>(b);
+    k_tile_scan<<<1, 1024, 0, st>>>(b, tiles);
+    k_pack_tiles<<<(unsigned)tiles, LB_TILE, 0, st>>>(b, copy ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -1089,6 +1277,78 @@ __global__ void k_collect_totals(const uint64_t* __restrict__ off, uint64_t n, B
 hipError_t run_collect_totals(const BatchBufs& b, hipStream_t st)
 {
     k_collect_totals<<<1, 64, 0, st>>>(b.off, b.n_txns, b.ctl);
+    return hipGetLastError();
+}
+
+// The lean kernels' KeyLine of every key (common.hpp), from the KeyEntry (newest fields, class
+// lists) and the emission lists; thread per key, written to the key's slot (empty slots: meta 0).
+__global__ __launch_bounds__(256) void k_build_klines(DevSnapshot s, const uint32_t* __restrict__ kslot,
+                                                      const uint32_t* __restrict__ kcell, KeyLine* __restrict__ out)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= s.n_keys) return;
+    const KeyEntry ke = s.kent[k];
+    KeyLine L;
+    L.key = s.keys[k];
+    const uint32_t cell = kcell ? kcell[k] : NO_CELL;
+    L.cell_lo = (cell != NO_CELL && s.cell_off) ? s.cell_off[cell] : 0u;
+    L.cell_hi = (cell != NO_CELL && s.cell_off) ? s.cell_off[cell + 1] : 0u;
+    L.last_txn = ke.last_txn;
+    L.last_wexec = ke.last_wexec;
+    L.last_w_txn = ke.last_w_txn;
+    for (int c = 0; c < NCLASS; ++c) L.cls[c] = KeyClassSpan{ke.cl[c].cand_hi - ke.cl[c].cand_lo, ke.cl[c].cand_lo};
+    L.cwr_tail = ke.cl[0].cwr_tail;
+    L.pad = 0;
+    const uint32_t n_cwr = ke.cl[0].cwr_hi - ke.cl[0].cwr_tail;
+    const uint32_t n2 = L.cls[2].n;
+    uint32_t meta = KL_USED | (n_cwr & KL_NCWR_MASK);
+    if (n_cwr > KL_NCWR_MASK) meta |= KL_NOLEAN;
+    for (uint32_t i = 0; i < KL_INL; ++i) L.inl[i] = 0;
+    if (n2 + n_cwr <= KL_INL)
+    {
+        // nested by class: Writes (class 0), then the Reads of class 1, then the (Exclusive)SyncPoints
+        // of class 2; then the cwr tail
+        uint32_t i = 0;
+        for (uint32_t j = 0; j < L.cls[0].n; ++j) L.inl[i++] = s.cand[L.cls[0].base + j];
+        for (uint32_t j = 0; j < L.cls[1].n; ++j)
+        {
+            const uint32_t x = s.cand[L.cls[1].base + j];
+            if ((x >> RANK_BITS) == 0u) L.inl[i++] = x;     // Txn.Kind.Read
+        }
+        for (uint32_t j = 0; j < L.cls[2].n; ++j)
+        {
+            const uint32_t x = s.cand[L.cls[2].base + j];
+            if (((KINDS_ANY_GLOBALLY_VISIBLE & ~KINDS_RS_OR_WS) >> (x >> RANK_BITS)) & 1u) L.inl[i++] = x;
+        }
+        for (uint32_t j = 0; j < n_cwr; ++j) L.inl[n2 + j] = s.cwr[L.cwr_tail + j];
+        meta |= KL_INLINE | (n2 << KL_INL_SHIFT);
+    }
+    L.meta = meta;
+    out[kslot[k]] = L;
+}
+
+hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const uint32_t* kcell, KeyLine* table,
+                            uint64_t table_slots, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(table, 0, sizeof(KeyLine) * table_slots, st);
+    if (e != hipSuccess || !s.n_keys) return e;
+    k_build_klines<<<(unsigned)((s.n_keys + 255) / 256), 256, 0, st>>>(s, kslot, kcell, table);
+    return hipGetLastError();
+}
+
+__global__ void k_snap_dict_sample(DevSnapshot s, uint64_t* hi, uint64_t* lo, int32_t* node, uint64_t n)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    hi[j] = s.dict_hi[j * DICT_SAMP];
+    lo[j] = s.dict_lo[j * DICT_SAMP];
+    node[j] = s.dict_node[j * DICT_SAMP];
+}
+
+hipError_t run_dict_sample(const DevSnapshot& s, uint64_t* hi, uint64_t* lo, int32_t* node, hipStream_t st)
+{
+    const uint64_t n = dict_samples(s.n_dict);
+    if (n) k_snap_dict_sample<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, hi, lo, node, n);
     return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ struct BatchCtl {
     unsigned long long n_real1, n_real2;      // requests on those lists
     unsigned long long tot[9];                // totals of the 9 per-request size arrays (after the offsets scan)
 };
+constexpr unsigned OVF_PACK = 16u;            // BatchCtl.overflow: a packed output array is too small
 
 constexpr uint64_t NO_RB = ~0ull;
 constexpr unsigned ERR_INVAL = 1u;   // BatchCtl.error codes
@@ -38,9 +39,7 @@ struct BatchBufs {
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
     uint32_t* p_txn; uint4* p_rec;
-    uint32_t* p_slot;                // fused path: KeyEntry slot of each probe | in-slice << 31 (k_prepare)
-    uint4* q_rec;                    // fused path: per request {key_off lo, hi, np | cls << 16 | flags, 0} (k_prepare)
-    uint32_t* p_cell;                // fused path: range stabbing-index cell of each probe (NO_CELL: none)
+    uint4* q_rec;                    // fused path: per request {key_off, S rank, np | cls << 16 | flags, self rank} (k_prepare)
     // K1
     uint32_t* arena; uint32_t* p_off; uint32_t* p_c0; uint32_t* p_c1;
     // K4
@@ -58,6 +57,9 @@ struct BatchBufs {
     const uint32_t* req_list;        // k_resolve: resolve only these requests (count *req_count); null = all
     const unsigned long long* req_count;
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
+    uint64_t o_cap[9];               // capacities (elements) of the packed arrays, [3 * map + array]
+    uint64_t* lb_agg;                // [tiles][9] size sums per tile (k_tile_sums)
+    uint64_t* lb_inc;                // [tiles][9] exclusive prefixes of the tile sums (k_tile_scan)
     BatchCtl* ctl;
 };
 
@@ -85,6 +87,11 @@ hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const Batch
 hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st);
 hipError_t run_pack(const BatchBufs& b, hipStream_t st);
+// offsets of the 9 size arrays + totals (+ the packed arrays when `copy`): tile sums, one-block scan
+// of the tile sums, then a streaming per-tile scan + pack; no host round trip between resolve and pack
+constexpr uint32_t LB_TILE = 256;
+inline uint64_t lb_tiles(uint64_t n) { return (n + LB_TILE - 1) / LB_TILE; }
+hipError_t run_pack_lb(const BatchBufs& b, bool copy, hipStream_t st);
 hipError_t run_collect_totals(const BatchBufs& b, hipStream_t st);
 
 // fused per-request path (resolve.hip)
@@ -92,7 +99,7 @@ constexpr uint32_t SLOT_NONE = 0x7FFFFFFFu;    // p_slot: key has no CommandsFor
 constexpr uint32_t SLOT_IN_SLICE = 0x80000000u;
 constexpr uint32_t DEFER_HOLE = 0xFFFFFFFFu;      // unused slot of a wave's deferral chunk
 constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave reserves at a time
-constexpr uint32_t REC_FAST = 1u << 24;          // q_rec: newest fast path applies (S, self, <= 8 keys, valid kind)
+constexpr uint32_t REC_FAST = 1u << 24;          // q_rec: lean path applies (<= 8 keys, valid kind, 32-bit key offsets)
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, hipStream_t st);
 
@@ -139,5 +146,11 @@ hipError_t run_defer_scatter(const BatchBufs& b, const uint32_t* deferred, uint6
                              const uint64_t* sub_reg, hipStream_t st);
 
 int device_cu_count();
+// the KeyLine table (table_slots lines) from s.kent / cand / cwr; kslot[k] = the line of key k (its
+// perfect-hash index), kcell[k] = its stabbing cell (NO_CELL; null: none)
+hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const uint32_t* kcell, KeyLine* table,
+                            uint64_t table_slots, hipStream_t st);
+// every DICT_SAMP-th id of s's dictionary into hi/lo/node (dict_samples(s.n_dict) entries)
+hipError_t run_dict_sample(const DevSnapshot& s, uint64_t* hi, uint64_t* lo, int32_t* node, hipStream_t st);
 
 }  // namespace adx

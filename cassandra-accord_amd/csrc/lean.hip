@@ -132,8 +132,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     const uint32_t n_items = (n_slots + RPW - 1) / RPW;
     const uint32_t nw = gridDim.x * LEAN_WAVES;
     const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
-    const uint32_t S = s.n_dict ? (uint32_t)(2 * s.n_dict) : 0u;   // rank of an id above every member
-    const uint32_t self = 0;   // exec == txnId: none; else a non-member rank (even): never an emission
+
     LeanChunk ralloc;
     // one wave-uniform region allocation for the segments' byte counts (at each segment's lane 0):
     // returns this segment's offset; `fits` whether the whole allocation is inside the arena
@@ -177,55 +176,77 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     // KeyEntry -> lists costs about one round trip per iteration. Pipeline loads are branch-free
     // (clamped addresses, results masked where used) so the compiler's wait counts stay exact.
     using Raw = uint4;        // the request record of k_prepare
-    struct Req { uint64_t k0; uint32_t np, cls, t; bool act, defer; };
+    struct Req { uint64_t k0; uint32_t np, cls, t, S, self; bool act, defer; };
     auto req_of = [&](uint32_t it) -> uint32_t {
         const uint32_t si = it * RPW + h;
         if (si >= n_slots) return DEFER_HOLE;
         return pass == 1 ? (uint32_t)si : b.deferred1[si];
     };
     auto loadA = [&](uint32_t t) -> Raw { return b.q_rec[t != DEFER_HOLE ? t : 0u]; };
-    // the record carries PreAccept.java:251-261's witness class and whether S and self take the
-    // newest fast path (k_prepare); anything else defers
+    // the record carries PreAccept.java:251-261's witness class, S and self as ranks (k_prepare)
+    // and whether the request fits the lean path (<= 8 keys, valid kind); anything else defers
     auto derive = [&](uint32_t t, const Raw& r) -> Req {
-        Req q{0, 0, 0, t, false, false};
+        Req q{0, 0, 0, t, 0, 0, false, false};
         q.act = t != DEFER_HOLE;
-        q.k0 = ((uint64_t)r.y << 32) | r.x;
+        q.k0 = r.x;
+        q.S = r.y;             // rank of executeAt
+        q.self = r.w;          // rank of the txnId unless it is the executeAt (0: none)
         q.np = r.z & 0xFFFFu;
         q.cls = (r.z >> 16) & 3u;
         q.defer = (r.z & REC_FAST) == 0;
         return q;
     };
-    // keys and raw slots (the in-slice bit is stripped where the slot is used)
-    auto loadB = [&](const Req& q, int64_t& key, uint32_t& pslot, uint32_t& pcell) {
+    // the key (one lane per key)
+    auto loadB = [&](const Req& q, int64_t& key) {
         const bool on = q.act && !q.defer && hl < q.np;
-        const uint64_t i = on ? q.k0 + hl : 0;
-        key = b.q_keys[i];
-        pslot = b.p_slot[i];
-        if (!on) pslot = SLOT_NONE;
-        pcell = NO_CELL;
-        if (RNG)
-        {
-            pcell = b.p_cell[i];
-            if (!on) pcell = NO_CELL;
-        }
+        key = b.q_keys[on ? q.k0 + hl : 0];
     };
-    // the key's cell bounds in the range stabbing index
-    auto loadR = [&](uint32_t pcell, uint2& cb) {
-        cb = make_uint2(0, 0);
-        if (RNG)
-        {
-            const uint32_t c = pcell != NO_CELL ? pcell : 0u;
-            cb.x = s.cell_off[c];
-            cb.y = s.cell_off[c + 1];
-            if (pcell == NO_CELL) cb = make_uint2(0, 0);
-        }
+    // the key's line (KeyLine, common.hpp): the slice test (InMemoryCommandStore.java:280), then one
+    // random line per key -- its first 64 bytes: key, cell entries, newest fields, meta, the class's
+    // {count, start} and the cwr tail start. A slot holding another key is resolved when used.
+    struct Hdr { uint4 h0, h1; uint2 h2; uint32_t h3, slot; bool look; };
+    auto in_slice_of = [&](int64_t key) {
+        bool in = s.n_slices == 0;
+        for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+        return in;
     };
-    auto slot_of = [](uint32_t pslot) { return pslot & ~SLOT_IN_SLICE; };
-    auto loadC = [&](uint32_t pslot, uint32_t cls, uint4& q1, uint4& qc) {
-        const uint32_t sl = slot_of(pslot);
-        const uint4* e = reinterpret_cast<const uint4*>(s.kent + (sl != SLOT_NONE ? sl : 0u));
-        q1 = e[0];
-        qc = e[1 + cls];
+    auto load_line = [&](uint32_t slot, uint32_t cls, Hdr& H) {
+        const uint4* L4 = reinterpret_cast<const uint4*>(s.kline + slot);
+        H.h0 = L4[0];
+        H.h1 = L4[1];
+        H.h2 = reinterpret_cast<const uint2*>(L4 + 2)[cls];
+        H.h3 = reinterpret_cast<const uint32_t*>(L4 + 3)[2];
+    };
+    // the key's displacement (a small table: cache-resident), issued ahead of its line
+    auto loadD = [&](const Req& q, int64_t key, bool& look, uint32_t& d) {
+        const bool on = q.act && !q.defer && hl < q.np;
+        look = on && in_slice_of(key);
+        d = s.kl_disp[look ? kl_bucket(key_hash(key), s.kl_buckets) : 0u];
+    };
+    auto loadC = [&](const Req& q, int64_t key, bool look, uint32_t d, Hdr& H) {
+        H.look = look;
+        H.slot = look ? (uint32_t)kl_index(key_hash2(key), d, s.kl_lines) : 0u;
+        load_line(H.slot, q.cls, H);
+    };
+    // (found, cell bounds) of a loaded line: the perfect hash put the key on this line if the
+    // store holds it; a line of another key (or an empty one) means no CommandsForKey
+    auto resolve_line = [&](int64_t key, uint32_t cls, Hdr& H, bool& found, uint2& cb) {
+        auto key_of = [](const uint4& h0) { return (int64_t)(((uint64_t)h0.y << 32) | h0.x); };
+        found = H.look && (H.h1.w & KL_USED) && key_of(H.h0) == key;
+        cb = found ? make_uint2(H.h0.z, H.h0.w) : make_uint2(0, 0);
+        if (RNG && H.look && !found && s.cell_off)
+        {
+            // a key without a CommandsForKey: its cell by search (rare)
+            uint64_t lo = 0, hi = s.n_cell_E;
+            while (lo < hi)
+            {
+                const uint64_t mid = (lo + hi) >> 1;
+                const int64_t v = s.cell_E[mid];
+                if (s.start_inclusive ? v <= key : v < key) lo = mid + 1;
+                else hi = mid;
+            }
+            cb = make_uint2(s.cell_off[lo], s.cell_off[lo + 1]);
+        }
     };
 
     // sizes of map m (keys, txnIds, keysToTxnIds) and its region offset: one store from lanes
@@ -243,12 +264,12 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
     uint32_t tc = req_of(it0);
     Req qc = derive(tc, loadA(tc));
     int64_t keyc;
-    uint32_t slotc, cellc;
-    loadB(qc, keyc, slotc, cellc);
-    uint4 q1c, qlc;
-    loadC(slotc, qc.cls, q1c, qlc);
-    uint2 cbc;
-    loadR(cellc, cbc);
+    loadB(qc, keyc);
+    bool lookc;
+    uint32_t dc;
+    loadD(qc, keyc, lookc, dc);
+    Hdr Hc;
+    loadC(qc, keyc, lookc, dc, Hc);
     uint32_t tN = req_of(it0 + nw);
     Raw rN = loadA(tN);
 
@@ -259,20 +280,24 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         tN = req_of(it + 2 * nw);
         rN = loadA(tN);
         int64_t keyn;
-        uint32_t slotn, celln;
-        loadB(qn, keyn, slotn, celln);
+        loadB(qn, keyn);
+        bool lookn;
+        uint32_t dn_;
 
         // ---- current item: per key p = hl < np, newest test and emission counts
         bool act = qc.act;
         bool defer = qc.defer;
-        const uint32_t np = qc.np, cls = qc.cls;
+        const uint32_t np = qc.np, cls = qc.cls, S = qc.S, self = qc.self;
         const bool kact = act && !defer && hl < np;
-        const bool has_cfk = slot_of(slotc) != SLOT_NONE;
+        bool has_cfk;
+        uint2 cbc;
+        resolve_line(keyc, cls, Hc, has_cfk, cbc);
+        const uint32_t meta = Hc.h1.w;
         // newest: end = byId.length (last txnId < S) and M = the last committed Write's executeAt
         // (it executes before S), CommandsForKey.java:912-928
-        const bool newest = !has_cfk || (q1c.x < S && q1c.y < S);
-        const uint32_t n1 = has_cfk ? qlc.y - qlc.x : 0u;
-        const uint32_t n2 = !has_cfk ? 0u : (cls == 0 ? (q1c.z != 0 ? 1u : 0u) : qlc.w - qlc.z);
+        const bool newest = !has_cfk || (Hc.h1.x < S && Hc.h1.y < S && !(meta & KL_NOLEAN));
+        const uint32_t n1 = has_cfk ? Hc.h2.x : 0u;
+        const uint32_t n2 = !has_cfk ? 0u : (cls == 0 ? (Hc.h1.z != 0 ? 1u : 0u) : (meta & KL_NCWR_MASK));
         const uint32_t nn = kact ? n1 + n2 : 0u;
         uint32_t inc = nn;       // exclusive prefix of nn over the 8 key lanes of each request
 #pragma unroll
@@ -288,6 +313,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         const uint32_t rinc = RNG ? key_lanes_incl_scan(rn, hl) : 0u;
         const uint32_t rstart = rinc - rn;
         const uint32_t TR = RNG ? __shfl(rinc, sb | 7u, 64) : 0u;
+        // the next item's displacements (its keys have arrived by now)
+        loadD(qn, keyn, lookn, dn_);
         defer = defer || seg(ballot(kact && !newest)) != 0 || T > LPR || TR > LPR;
         {
             const uint64_t dm = ballot(act && defer && hl == 0);
@@ -311,11 +338,18 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         }
         const uint32_t src = sb | a;
         const uint32_t a_start = __shfl(start, src, 64), a_n1 = __shfl(n1, src, 64);
-        const uint32_t a_clo = __shfl(qlc.x, src, 64), a_ct = __shfl(qlc.z, src, 64), a_lw = __shfl(q1c.z, src, 64);
+        const uint32_t a_base = __shfl(Hc.h2.y, src, 64), a_ct = __shfl(Hc.h3, src, 64), a_lw = __shfl(Hc.h1.z, src, 64);
+        const uint32_t a_meta = __shfl(meta, src, 64), a_slot = __shfl(Hc.slot, src, 64);
         const bool live = act && hl < T;
         const uint32_t i = hl - a_start;
         const bool from_cand = i < a_n1;
-        const uint32_t* lp = !live ? s.cand : (from_cand ? s.cand + (a_clo + i) : (cls != 0 ? s.cwr + (a_ct + (i - a_n1)) : s.cand));
+        // the element: inline in the key's line (the line just read: cache-hot) or in the lists
+        const uint32_t* lp;
+        if (a_meta & KL_INLINE)
+            lp = s.kline[a_slot].inl + (from_cand ? i : ((a_meta >> KL_INL_SHIFT) & 31u) + (i - a_n1));
+        else
+            lp = from_cand ? s.cand + (a_base + i) : s.cwr + (a_ct + (i - a_n1));
+        if (!live || (!from_cand && cls == 0)) lp = s.cand;        // class Ws: the last Write, no load
         const uint32_t lv = *lp;
         // range elements (same round trip as the list loads)
         uint32_t ar = 0;
@@ -334,11 +368,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
             rlive = act && hl < TR;
             ce = s.cell_ent[rlive ? ar_lo + (hl - ar_start) : 0u];
         }
-        // the next item's KeyEntry quarters (and cell bounds) go out behind this item's list loads
-        uint4 q1n, qln;
-        loadC(slotn, qn.cls, q1n, qln);
-        uint2 cbn;
-        loadR(celln, cbn);
+        // the next item's key lines go out behind this item's element loads
+        Hdr Hn;
+        loadC(qn, keyn, lookn, dn_, Hn);
 
         const uint32_t txw = !live ? 0u : ((from_cand || cls != 0) ? lv : (a_lw | (1u << RANK_BITS)));
         const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
@@ -418,10 +450,10 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
                 if (valid) ok2t[nk + kstart + pos_in_key] = (int32_t)ur;
             }
         }
-        // ---- rangeDeps (m = 1): (range, txnId) pairs of the cells, STARTED_BEFORE (always, the
-        // request is newer than every id), kind witnessed; unique pairs in (Range.compare, TxnId) order
+        // ---- rangeDeps (m = 1): (range, txnId) pairs of the cells, STARTED_BEFORE (txnId < S), kind
+        // witnessed, not self; unique pairs in (Range.compare, TxnId) order
         const uint32_t rtxw = (uint32_t)ce, rk = rtxw & RANK_MASK, rkd = rtxw >> RANK_BITS;
-        const bool rwant = RNG && rlive && ((CLASS_KINDS[cls] >> rkd) & 1) && rk != self;
+        const bool rwant = RNG && rlive && ((CLASS_KINDS[cls] >> rkd) & 1) && rk < S && rk != self;
         const uint64_t rmb = ballot(rwant);
         if (!RNG || rmb == 0)
         {
@@ -495,11 +527,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s,
         }
         qc = qn;
         keyc = keyn;
-        slotc = slotn;
-        cellc = celln;
-        q1c = q1n;
-        qlc = qln;
-        cbc = cbn;
+        Hc = Hn;
     }
     dflush();
 }

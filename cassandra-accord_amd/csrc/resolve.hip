@@ -230,6 +230,21 @@ __device__ __forceinline__ uint32_t wave_dict_rank(const DevSnapshot& s, uint64_
 
 
 
+// cell of key x in the range stabbing index: #endpoints < x (EndInclusive) or <= x (StartInclusive)
+__device__ __forceinline__ uint32_t cell_search(const DevSnapshot& s, int64_t x)
+{
+    if (!s.cell_off) return NO_CELL;
+    uint64_t lo = 0, hi = s.n_cell_E;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        const int64_t v = s.cell_E[mid];
+        if (s.start_inclusive ? v <= x : v < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return (uint32_t)lo;
+}
+
 __device__ __forceinline__ uint64_t fregion_bytes(uint32_t nk, uint32_t U, uint32_t pairs)
 {
     return ((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + pairs) * 4 + 7) & ~7ull;
@@ -293,10 +308,41 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         }
         return r;
     };
-    auto st2 = [&](uint64_t k0i, uint32_t npi, int64_t& keyo, uint32_t& pso) {
+    auto st2 = [&](uint64_t k0i, uint32_t npi, int64_t& keyo) {
         const bool a = g < npi && npi <= FMAXP;
         keyo = a ? b.q_keys[k0i + g] : 0;
-        pso = a ? b.p_slot[k0i + g] : SLOT_NONE;
+    };
+    // key -> (KeyEntry / KeyRec index | in-slice bit, stabbing cell): the slice test
+    // (InMemoryCommandStore.java:280) and an open-addressing probe of the KeySlot table by the
+    // group's 8 lanes at once (8 consecutive 16-byte slots = one line per round)
+    auto probe = [&](uint32_t npi, int64_t key, uint32_t& pso, uint32_t& pco) {
+        bool a = g < npi && npi <= FMAXP;
+        bool in_slice = s.n_slices == 0;
+        for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
+            in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+        uint32_t slot = SLOT_NONE, cell = NO_CELL;
+        bool look = a && in_slice && s.n_keys != 0;
+        uint64_t h = key_hash(key) & s.khash_mask;
+        while (ballot(look))
+        {
+            const uint4 q = look ? reinterpret_cast<const uint4*>(s.khash + ((h + j) & s.khash_mask))[0] : make_uint4(0, 0, 0, 0);
+            const bool hit = look && q.z != KEY_EMPTY && (int64_t)(((uint64_t)q.y << 32) | q.x) == key;
+            const bool emp = look && q.z == KEY_EMPTY;
+            const uint32_t hm = grp_bits(ballot(hit), g), em = grp_bits(ballot(emp), g);
+            const uint32_t fh = hm ? (uint32_t)(__ffs(hm) - 1) : 8u, fe = em ? (uint32_t)(__ffs(em) - 1) : 8u;
+            const uint32_t zs = __shfl(q.z, (lane & ~7u) | (fh & 7u), 64);      // every lane shuffles
+            const uint32_t ws = __shfl(q.w, (lane & ~7u) | (fh & 7u), 64);
+            if (look && fh < fe)
+            {
+                slot = zs;
+                cell = ws;
+            }
+            if (look && (fh < 8 || fe < 8)) look = false;
+            h += 8;
+        }
+        if (a && in_slice && slot == SLOT_NONE && s.cell_off) cell = cell_search(s, key);
+        pso = !a ? SLOT_NONE : (in_slice ? (slot | SLOT_IN_SLICE) : SLOT_NONE);
+        pco = (a && in_slice) ? cell : NO_CELL;
     };
     auto st3 = [&](uint32_t psi, uint4& kqo) {
         const uint32_t sl = psi & ~SLOT_IN_SLICE;
@@ -312,8 +358,9 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
     st1(t0 + nw, k0n, npn);
     Ids idc = ids(t0);
     int64_t keyc;
-    uint32_t psc;
-    st2(k0c, npc, keyc, psc);
+    uint32_t psc, pcc;
+    st2(k0c, npc, keyc);
+    probe(npc, keyc, psc, pcc);
     uint4 kqc;
     st3(psc, kqc);
     for (uint64_t ii = t0; ii < n_iter; ii += nw)
@@ -324,8 +371,8 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         st1(ii + 2 * nw, k0nn, npnn);
         const Ids idn = ids(ii + nw);
         int64_t keyn;
-        uint32_t psn;
-        st2(k0n, npn, keyn, psn);
+        uint32_t psn = SLOT_NONE, pcn = NO_CELL;
+        st2(k0n, npn, keyn);
         uint4 kqn = make_uint4(0, 0, 0, 0);
         bool pf3 = false;
         do {
@@ -351,8 +398,10 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         }
         const int cls = kinds_class(kinds);
         const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
-        const uint32_t S = wave_dict_rank(s, em, el, en);
-        const uint32_t self = same ? 0u : wave_dict_rank(s, tm, tl, tn);
+        (void)same;
+        const uint4 rec = b.q_rec[t];              // ranks of S and self (k_prepare)
+        const uint32_t S = rec.y;
+        const uint32_t self = rec.w;
         const int64_t epoch = (int64_t)(em >> 15);
         const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
 
@@ -526,7 +575,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
                 }
             }
         }
-        const uint32_t pcell = gact ? b.p_cell[k0 + g] : NO_CELL;
+        const uint32_t pcell = gact ? pcc : NO_CELL;
         if (s.n_rent && s.cell_off)
         {
             // stabbing index: the key's cell lists every range entry containing it, in (range,
@@ -593,7 +642,9 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         }
         if (gact && j == 0) L.rs[g][FCAPR] = rbv;
 
-        // lists staged: the next request's KeyEntry loads go out now, behind this one's build
+        // lists staged: the next request's key probe and KeyEntry loads go out now, behind this
+        // one's build
+        probe(npn, keyn, psn, pcn);
         st3(psn, kqn);
         pf3 = true;
 
@@ -802,11 +853,15 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
             }
         }
         } while (false);
-        if (!pf3) st3(psn, kqn);
+        if (!pf3)
+        {
+            probe(npn, keyn, psn, pcn);
+            st3(psn, kqn);
+        }
         k0c = k0n; npc = npn;
         k0n = k0nn; npn = npnn;
         idc = idn;
-        keyc = keyn; psc = psn;
+        keyc = keyn; psc = psn; pcc = pcn;
         kqc = kqn;
     }
 }
@@ -818,77 +873,32 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
 // Keeping the dependent key -> slot probing here leaves the per-request kernels one load shorter;
 // one thread per probe (the first n_txns threads also write the request records).
 
-// cell of key x in the range stabbing index: #endpoints < x (EndInclusive) or <= x (StartInclusive)
-__device__ __forceinline__ uint32_t cell_search(const DevSnapshot& s, int64_t x)
-{
-    if (!s.cell_off) return NO_CELL;
-    uint64_t lo = 0, hi = s.n_cell_E;
-    while (lo < hi)
-    {
-        const uint64_t mid = (lo + hi) >> 1;
-        const int64_t v = s.cell_E[mid];
-        if (s.start_inclusive ? v <= x : v < x) lo = mid + 1;
-        else hi = mid;
-    }
-    return (uint32_t)lo;
-}
-
 __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g < b.n_txns)
-    {
-        // request g's record
-        const uint64_t t = g;
-        const uint64_t k0 = b.q_key_off[t], k1 = b.q_key_off[t + 1];
-        const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t], em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
-        const int32_t tn = b.q_txn_node[t], en = b.q_exec_node[t];
-        const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
-        const uint32_t cls = kinds ? (uint32_t)kinds_class(kinds) : 0u;
-        const NormTid last{s.dict_last_hi, s.dict_last_lo, s.dict_last_node};
-        const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
-        const bool s_new = s.n_dict == 0 || norm_cmp(last, norm_tid(em, el, en)) < 0;
-        const bool t_new = same || s.n_dict == 0 || norm_cmp(last, norm_tid(tm, tl, tn)) < 0;
-        const uint64_t np = k1 - k0;
-        // lean fast path: S and self need no dictionary search, at most 8 keys, a valid kind
-        const bool fast = kinds != 0 && s_new && t_new && np <= 8;
-        b.q_rec[t] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32),
-                                (uint32_t)(np < 0xFFFFu ? np : 0xFFFFu) | (cls << 16) | (fast ? REC_FAST : 0u), 0u);
-    }
-    if (g < b.n_probes)
-    {
-        // probe g: its key's index (open addressing, linear probing) and stabbing-index cell
-        const int64_t key = b.q_keys[g];
-        bool in_slice = s.n_slices == 0;
-        for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
-            in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
-        uint32_t slot = SLOT_NONE, cell = NO_CELL;
-        if (in_slice && s.n_keys)
-        {
-            uint64_t hh = key_hash(key) & s.khash_mask;
-            uint4 qq = reinterpret_cast<const uint4*>(s.khash + hh)[0];
-            while (qq.z != KEY_EMPTY)
-            {
-                if ((int64_t)(((uint64_t)qq.y << 32) | qq.x) == key)
-                {
-                    slot = qq.z;              // the key's index: KeyEntry / krec position
-                    cell = qq.w;
-                    break;
-                }
-                hh = (hh + 1) & s.khash_mask;
-                qq = reinterpret_cast<const uint4*>(s.khash + hh)[0];
-            }
-        }
-        b.p_slot[g] = in_slice ? slot | SLOT_IN_SLICE : SLOT_NONE;
-        // the key's cell: from its KeySlot, else by search (keys without a CFK)
-        if (s.cell_off) b.p_cell[g] = !in_slice ? NO_CELL : (slot != SLOT_NONE ? cell : cell_search(s, key));
-    }
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= b.n_txns) return;
+    // request t's record
+    const uint64_t k0 = b.q_key_off[t], k1 = b.q_key_off[t + 1];
+    const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t], em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
+    const int32_t tn = b.q_txn_node[t], en = b.q_exec_node[t];
+    const uint32_t kinds = kind_witnesses((uint32_t)((tl >> 1) & 7));
+    const uint32_t cls = kinds ? (uint32_t)kinds_class(kinds) : 0u;
+    // S = executeAt, self = txnId unless it equals executeAt (PreAccept.java:251-261), as ranks:
+    // no load for ids newer than the store (fresh PreAccepts), else a search of the sampled
+    // dictionary (Accepts: S is a proposed executeAt, self a txnId the store holds)
+    const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
+    const uint32_t S = dict_rank_sampled(s, norm_tid(em, el, en));
+    const uint32_t self = same ? 0u : dict_rank_sampled(s, norm_tid(tm, tl, tn));
+    const uint64_t np = k1 - k0;
+    // lean path: at most 8 keys, a valid kind, key offsets within 32 bits
+    const bool fast = kinds != 0 && np <= 8 && k1 <= 0xFFFFFFFFull;
+    b.q_rec[t] = make_uint4((uint32_t)k0, S, (uint32_t)(np < 0xFFFFu ? np : 0xFFFFu) | (cls << 16) | (fast ? REC_FAST : 0u),
+                            self);
 }
 
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
-    const uint64_t n = b.n_txns > b.n_probes ? b.n_txns : b.n_probes;
-    if (n) k_prepare<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, b);
+    if (b.n_txns) k_prepare<<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
     return hipGetLastError();
 }
 

@@ -1,0 +1,124 @@
+"""GPU parity at BASELINE.json's full sizes: the exact batches bench.py times, resolved on the
+device through the C ABI (ad_deps_batch_device), and a sample of their requests compared bit-exactly
+(Deps.equals, Deps.java:294-303: keys, txnIds, keysToTxnIds of all three maps) with the CPU
+restatement of the reference (oracle/refcpu.c) over the same snapshot.
+
+SNAPSHOT requests are independent (each reads the one immutable snapshot), so the sample -- the
+first 2000 requests plus 2000 spread over the whole batch -- is resolved by the oracle as a batch
+of its own and must equal those requests' slices of the device result. Size-independent checks
+cover every request: CSR well-formedness (RelationMultiMap.checkValid, RelationMultiMap.java:1074-1097)
+and the totals.
+
+Configs: 2 (1M txns x 8 Zipf(0.99) keys, 16M-entry history: the headline batch), the same batch as a
+replica's mix of fresh PreAccepts, Accepts of in-flight txns (S = executeAt, self excluded:
+Accept.java:84-117, PreAccept.java:261) and out-of-order PreAccepts (general kernel), and 4 (1M txns
+vs 100k range commands).
+"""
+import numpy as np
+import pytest
+
+from accord_deps import _abi as A
+from accord_deps import native, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _sample(n, head=2000, spread=2000, seed=7):
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([np.arange(min(n, head)), rng.choice(n, min(n, spread), replace=False)]))
+    return idx
+
+
+def _check_csr(store, res):
+    """RelationMultiMap.checkValid over every request of the device result: heads ascending and
+    absolute (nKeys + running count), each key's values strictly ascending indices below nIds, keys
+    strictly ascending per request, ids strictly ascending per request."""
+    n = res.n_txns
+    for m in range(A.NMAPS):
+        ko = store._d2h(res.keys_off[m], n + 1, np.uint64).astype(np.int64)
+        to = store._d2h(res.txn_off[m], n + 1, np.uint64).astype(np.int64)
+        oo = store._d2h(res.k2t_off[m], n + 1, np.uint64).astype(np.int64)
+        nk = np.diff(ko)
+        nt = np.diff(to)
+        no = np.diff(oo)
+        assert np.all(no >= nk) and np.all((no > nk) == (nk > 0)), A.MAP_NAMES[m]
+        assert np.all((nt > 0) == (nk > 0)), A.MAP_NAMES[m]
+        tx = store._d2h(res.txns[m], int(to[-1]), np.uint32).astype(np.int64)
+        k2t = store._d2h(res.k2t[m], int(oo[-1]), np.int32).astype(np.int64)
+        keys = store._d2h(res.keys[m], int(ko[-1]), np.int64)
+        # ids ascending within a request
+        req_t = np.repeat(np.arange(n), nt)
+        same = req_t[1:] == req_t[:-1]
+        assert np.all(tx[1:][same] > tx[:-1][same]), A.MAP_NAMES[m]
+        req_k = np.repeat(np.arange(n), nk)
+        samek = req_k[1:] == req_k[:-1]
+        if m != A.AD_MAP_RANGE:
+            assert np.all(keys[1:][samek] > keys[:-1][samek]), A.MAP_NAMES[m]
+        # heads: k2t[o0 + j] for j < nk is nk + cumulative count, last one == no
+        head_pos = np.repeat(oo[:-1], nk) + (np.arange(int(ko[-1])) - np.repeat(ko[:-1], nk))
+        heads = k2t[head_pos]
+        end_of_req = np.cumsum(nk) - 1
+        assert np.all(heads[end_of_req[nk > 0]] == no[nk > 0]), A.MAP_NAMES[m]
+        base = np.repeat(nk, nk)
+        prev = np.concatenate([[0], heads[:-1]])
+        first = np.ones(len(heads), bool)
+        first[1:] = ~samek
+        prev[first] = base[first]
+        assert np.all(heads > prev), A.MAP_NAMES[m]
+        # body values index the request's ids
+        body = np.ones(int(oo[-1]), bool)
+        body[head_pos] = False
+        req_o = np.repeat(np.arange(n), no)
+        assert np.all(k2t[body] >= 0) and np.all(k2t[body] < nt[req_o[body]]), A.MAP_NAMES[m]
+
+
+def _run_full(w, oracle, expect_lean=None):
+    import torch
+    dev = torch.device("cuda", 0)
+    st = native.DeviceCommandStore(device=0, slices=w.slices)
+    try:
+        st.load(w)
+        qdev, keep = native.device_queries(w.queries, dev)
+        res, stats = st.deps_batch_device(qdev)
+        torch.cuda.synchronize(dev)
+        idx = _sample(len(w.queries))
+        got = st.device_result_to_host(res, idx)
+        _check_csr(st, res)
+        exp = oracle.OracleStore(w.range_start_inclusive, 1, w.slices).load(w).deps_batch(w.queries.take(idx), w.flags)
+        ok, why = got.equals(exp, detail=True)
+        if not ok:
+            mm = got.first_mismatch(exp)
+            raise AssertionError("%s: %s; first mismatch at sample %s (request %d): %r" %
+                                 (w.name, why, mm[0] if mm else None, idx[mm[0]] if mm else -1, mm))
+        return stats, got
+    finally:
+        st.close()
+
+
+@pytest.fixture(scope="module")
+def config2_full():
+    return synth.config2()
+
+
+def test_config2_full_headline_batch(oracle, config2_full):
+    # the bench.py headline batch: 1M requests x 8 Zipf keys over a 16M-entry history (hottest key
+    # ~1.04M entries)
+    stats, got = _run_full(config2_full, oracle)
+    assert stats["n_probes"] == 8_000_000
+    assert sum(stats["n_pairs"]) > 20_000_000
+
+
+def test_config2_full_request_mix(oracle, config2_full):
+    # the same batch as 60 % fresh PreAccepts, 30 % Accepts of in-flight txns (S = executeAt,
+    # self excluded), 10 % PreAccepts up to 2000 hlc ticks late (older than busy keys' newest
+    # entries: the general kernel's tree descent over the hot segments)
+    w = synth.with_request_mix(config2_full, accept_frac=0.3, unordered_frac=0.1, unordered_window=2000)
+    stats, got = _run_full(w, oracle)
+    assert w.params["n_accept"] > 200_000 and w.params["n_unordered"] > 50_000
+    assert stats["n_deferred_lean"] > 0          # the general kernel ran on the late requests
+
+
+def test_config4_full(oracle):
+    w = synth.config4()
+    stats, got = _run_full(w, oracle)
+    assert stats["n_pairs"][A.AD_MAP_RANGE] > 0 and got.pair_count(A.AD_MAP_RANGE) > 0
