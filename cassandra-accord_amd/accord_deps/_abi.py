@@ -138,6 +138,14 @@ class AdMerged(C.Structure):
                 ("ms_device", C.c_double), ("id_format", C.c_uint32)]
 
 
+class AdExchangeStats(C.Structure):
+    _fields_ = [("bytes_moved", C.c_uint64), ("ms_export", C.c_double), ("ms_move", C.c_double),
+                ("ms_merge", C.c_double), ("ms_total", C.c_double)]
+
+
+AD_COMM_ID_BYTES = 128
+
+
 def ptr(a):
     """Pointer to a numpy array's data (None for None). Caller keeps the array alive."""
     if a is None:

@@ -23,7 +23,8 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
            "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict", "ad_preaccept_maps_load",
            "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_recovery_batch",
-           "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries")
+           "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries",
+           "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange")
 
 
 class AccordDepsError(RuntimeError):
@@ -88,8 +89,49 @@ def lib():
                                            C.POINTER(A.AdStats)]
         L.ad_cfk_entries.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ad_exchange_local.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.POINTER(A.AdDepsResult)),
+                                        C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_void_p, C.c_void_p,
+                                        C.POINTER(A.AdMerged), C.POINTER(A.AdExchangeStats)]
+        L.ad_comm_unique_id.argtypes = [C.c_void_p]
+        L.ad_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        L.ad_exchange.argtypes = [C.c_void_p, C.POINTER(A.AdDepsResult), C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
+                                  C.c_void_p, C.POINTER(A.AdMerged), C.POINTER(A.AdExchangeStats)]
         _lib = L
     return _lib
+
+
+def exchange_stats(s):
+    return dict(bytes_moved=int(s.bytes_moved), ms_export=s.ms_export, ms_move=s.ms_move, ms_merge=s.ms_merge,
+                ms_total=s.ms_total)
+
+
+def comm_unique_id():
+    """ad_comm_unique_id: the RCCL id rank 0 shares with the other ranks (bytes)."""
+    b = (C.c_uint8 * A.AD_COMM_ID_BYTES)()
+    rc = lib().ad_comm_unique_id(C.cast(b, C.c_void_p))
+    if rc:
+        raise AccordDepsError(rc, "ad_comm_unique_id")
+    return bytes(b)
+
+
+def exchange_local(stores, results, txn_index_ptrs, dest_firsts, txn_bases, n_owned):
+    """ad_exchange_local over DeviceCommandStores of one process (slice order): every store's parts
+    moved to the owners and merged there. Returns ([AdMerged] per store, stats dict)."""
+    n = len(stores)
+    ctxs = (C.c_void_p * n)(*[st.h.value for st in stores])
+    res = (C.POINTER(A.AdDepsResult) * n)(*[C.pointer(r) for r in results])
+    ti = (C.c_void_p * n)(*txn_index_ptrs)
+    dfs = [np.ascontiguousarray(d, np.uint64) for d in dest_firsts]
+    df = (C.c_void_p * n)(*[A.ptr(d) for d in dfs])
+    tb = np.ascontiguousarray(txn_bases, np.uint64)
+    no = np.ascontiguousarray(n_owned, np.uint64)
+    out = (A.AdMerged * n)()
+    s = A.AdExchangeStats()
+    rc = lib().ad_exchange_local(ctxs, n, res, ti, df, A.ptr(tb), A.ptr(no), out, C.byref(s))
+    if rc:
+        msgs = [lib().ad_last_error(st.h).decode() for st in stores]
+        raise AccordDepsError(rc, "; ".join(m for m in msgs if m))
+    return list(out), exchange_stats(s)
 
 
 def _view(p, n, dtype):
@@ -330,6 +372,20 @@ class DeviceCommandStore:
         self._check(lib().ad_parts_union(self.h, C.byref(parts), len(sp), A.ptr(sp), txn_base, n_owned, stream,
                                          C.byref(out)))
         return out
+
+    def comm_init(self, uid, rank, world):
+        """ad_comm_init: join the node's RCCL communicator (uid from comm_unique_id on rank 0)."""
+        b = (C.c_uint8 * A.AD_COMM_ID_BYTES).from_buffer_copy(uid)
+        self._check(lib().ad_comm_init(self.h, C.cast(b, C.c_void_p), rank, world))
+
+    def exchange(self, res, txn_index_ptr, dest_first, txn_base, n_owned, stream=None):
+        """ad_exchange (RCCL): this rank's export, exchange and K3 merge. Returns (AdMerged, stats)."""
+        df = np.ascontiguousarray(dest_first, np.uint64)
+        out = A.AdMerged()
+        s = A.AdExchangeStats()
+        self._check(lib().ad_exchange(self.h, C.byref(res), txn_index_ptr, A.ptr(df), txn_base, n_owned, stream,
+                                      C.byref(out), C.byref(s)))
+        return out, exchange_stats(s)
 
     def levels_device(self, gdev, out_ptr, stream=None):
         """ad_levels_device: graph and output already in HBM. Returns the stats dict."""

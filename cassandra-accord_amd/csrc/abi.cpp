@@ -6,6 +6,7 @@
 // InMemoryCommandStore.rangeCommands (:740-763) once per snapshot; the batch pipeline then
 // answers calculatePartialDeps for every request of a batch on the GPU.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -243,6 +244,14 @@ struct ad_ctx {
     DevBuf g_msb, g_lsb, g_node, g_map, g_err;
     uint64_t n_global = 0;
     bool global_ok = false;
+    // node exchange (ad_exchange / ad_exchange_local): library-owned part buffers, RCCL communicator
+    DevBuf xs_hdr, xs_keys, xs_ids, xs_k2t;    // this store's exported parts (grouped by owner)
+    DevBuf xr_hdr, xr_keys, xr_ids, xr_k2t;    // parts received for the requests this store owns
+    DevBuf xc_dev;                             // counts table of the RCCL all-gather
+    uint64_t xs_counts[4] = {}, xr_total[4] = {};
+    std::vector<uint64_t> x_dest_counts;       // [n_dest][4] of the last export
+    ncclComm_t comm = nullptr;
+    int comm_rank = 0, comm_world = 1;
     // execution levels (K5)
     LevelsWork* lv = nullptr;
     DevBuf g_em, g_el, g_en, g_kind, g_ko, g_k, g_do, g_d, g_out;
@@ -1456,6 +1465,7 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->lv) levels_work_destroy(c->lv);
     if (c->cu) cfk_upd_work_destroy(c->cu);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -2453,6 +2463,281 @@ int ad_cfk_entries(ad_ctx* c, uint64_t* n_entries, const uint8_t** status, const
     *exec_msb = c->x_msb.data();
     *exec_lsb = c->x_lsb.data();
     *exec_node = c->x_node.data();
+    return AD_OK;
+}
+
+}  // extern "C"
+
+// =======================================================================================
+// Node exchange (SURVEY §8 e): the per-store PartialDeps of a node batch combined
+// on the store that owns each request -- CommandStores.mapReduce's reduce (CommandStores.java:576-593)
+// with PartialDeps.with (PreAccept.reduce, PreAccept.java:140-156) -- as export -> move -> K3 merge.
+// Two transports of one protocol: device copies between the contexts of one process
+// (ad_exchange_local: the Java host's one process per node, hipMemcpyPeerAsync over xGMI between
+// GPUs) and RCCL grouped send/recv between processes (ad_exchange).
+// =======================================================================================
+namespace {
+
+constexpr int XA = 4;                                  // hdr, keys, ids, k2t
+static size_t x_unit_bytes(int a, uint32_t fmt)       // bytes per counted unit of array a
+{
+    switch (a)
+    {
+        case 0: return 32;                             // 4 int64 per part
+        case 1: return 8;                              // key words
+        case 2: return fmt == AD_IDS_RANK ? 4 : 24;    // ids
+        default: return 4;                             // k2t
+    }
+}
+static DevBuf* x_send(ad_ctx* c, int a) { DevBuf* b[XA] = {&c->xs_hdr, &c->xs_keys, &c->xs_ids, &c->xs_k2t}; return b[a]; }
+static DevBuf* x_recv(ad_ctx* c, int a) { DevBuf* b[XA] = {&c->xr_hdr, &c->xr_keys, &c->xr_ids, &c->xr_k2t}; return b[a]; }
+static uint32_t x_format(const ad_ctx* c) { return c->global_ok ? AD_IDS_RANK : AD_IDS_TRIPLET; }
+
+// Export the last device batch of c as parts grouped by owner into c's send buffers (grown on
+// AD_E_SPACE); c->x_dest_counts[4 d + a] = units of array a for destination d. Complete on return.
+static int x_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
+                    const uint64_t* dest_first, hipStream_t st)
+{
+    c->x_dest_counts.assign(4 * (size_t)n_dest, 0);
+    const uint32_t fmt = x_format(c);
+    for (int attempt = 0; attempt < 3; ++attempt)
+    {
+        ad_parts p{};
+        p.hdr = c->xs_hdr.as<int64_t>();
+        p.keys = c->xs_keys.as<int64_t>();
+        p.ids = c->xs_ids.as<int64_t>();
+        p.k2t = c->xs_k2t.as<int32_t>();
+        p.cap_parts = c->xs_hdr.cap / x_unit_bytes(0, fmt);
+        p.cap_key_words = c->xs_keys.cap / x_unit_bytes(1, fmt);
+        p.cap_ids = c->xs_ids.cap / x_unit_bytes(2, fmt);
+        p.cap_k2t = c->xs_k2t.cap / x_unit_bytes(3, fmt);
+        p.id_format = fmt;
+        const int rc = ad_parts_export(c, res, txn_index, n_dest, dest_first, st, &p, c->x_dest_counts.data());
+        if (rc == AD_OK)
+        {
+            HIPCHK(c, hipStreamSynchronize(st));
+            c->xs_counts[0] = p.n_parts; c->xs_counts[1] = p.n_key_words; c->xs_counts[2] = p.n_ids; c->xs_counts[3] = p.n_k2t;
+            return AD_OK;
+        }
+        if (rc != AD_E_SPACE) return rc;
+        const uint64_t need[XA] = {p.n_parts, p.n_key_words, p.n_ids, p.n_k2t};
+        for (int a = 0; a < XA; ++a)
+            if (!x_send(c, a)->ensure(x_unit_bytes(a, fmt) * (need[a] + need[a] / 4 + 64)))
+                return c->fail(AD_E_NOMEM, "exchange send buffers");
+    }
+    return c->fail(AD_E_DEVICE, "exchange export did not fit after growing its buffers");
+}
+
+// receive buffers of c for `tot` units per array
+static int x_recv_ensure(ad_ctx* c, const uint64_t* tot, uint32_t fmt)
+{
+    for (int a = 0; a < XA; ++a)
+        if (!x_recv(c, a)->ensure(x_unit_bytes(a, fmt) * (tot[a] + tot[a] / 4 + 64)))
+            return c->fail(AD_E_NOMEM, "exchange receive buffers");
+    for (int a = 0; a < XA; ++a) c->xr_total[a] = tot[a];
+    return 0;
+}
+
+// K3 on c over its receive buffers: sources in slice (= rank / context) order
+static int x_merge(ad_ctx* c, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base, uint64_t n_owned,
+                   hipStream_t st, ad_merged* out)
+{
+    ad_parts in{};
+    in.hdr = c->xr_hdr.as<int64_t>();
+    in.keys = c->xr_keys.as<int64_t>();
+    in.ids = c->xr_ids.as<int64_t>();
+    in.k2t = c->xr_k2t.as<int32_t>();
+    in.n_parts = c->xr_total[0];
+    in.n_key_words = c->xr_total[1];
+    in.n_ids = c->xr_total[2];
+    in.n_k2t = c->xr_total[3];
+    in.id_format = x_format(c);
+    return ad_parts_merge(c, &in, n_src, src_parts, txn_base, n_owned, st, out);
+}
+
+static int nccl_fail(ad_ctx* c, ncclResult_t r, const char* what)
+{
+    return c->fail(AD_E_DEVICE, "%s: %s", what, ncclGetErrorString(r));
+}
+#define NCCLCHK(ctx, expr)                                                                         \
+    do {                                                                                           \
+        ncclResult_t _r = (expr);                                                                  \
+        if (_r != ncclSuccess) return nccl_fail((ctx), _r, #expr);                                 \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* const* res, const int64_t* const* txn_index,
+                      const uint64_t* const* dest_first, const uint64_t* txn_base, const uint64_t* n_owned,
+                      ad_merged* out, ad_exchange_stats* stats)
+{
+    if (!ctxs || n == 0 || !res || !txn_index || !dest_first || !txn_base || !n_owned || !out) return AD_E_INVAL;
+    for (uint32_t i = 0; i < n; ++i)
+        if (!ctxs[i] || !res[i]) return AD_E_INVAL;
+    const uint32_t fmt = x_format(ctxs[0]);
+    for (uint32_t i = 1; i < n; ++i)
+        if (x_format(ctxs[i]) != fmt)
+            return ctxs[i]->fail(AD_E_STATE, "ad_exchange_local: every store needs the same id format (global dictionary on all or none)");
+    const double t0 = now_ms();
+    // 1. every store exports its parts, grouped by owner
+    for (uint32_t i = 0; i < n; ++i)
+    {
+        ad_ctx* c = ctxs[i];
+        if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+        if (int rc = x_export(c, res[i], txn_index[i], n, dest_first[i], c->stream)) return rc;
+    }
+    const double t1 = now_ms();
+    uint64_t moved = 0;
+    // 2. each owner gathers what every store exported for it (slice order), device to device
+    for (uint32_t d = 0; d < n; ++d)
+    {
+        ad_ctx* o = ctxs[d];
+        if (hipSetDevice(o->device) != hipSuccess) return o->fail(AD_E_DEVICE, "hipSetDevice");
+        uint64_t tot[XA] = {0, 0, 0, 0};
+        for (uint32_t s = 0; s < n; ++s)
+            for (int a = 0; a < XA; ++a) tot[a] += ctxs[s]->x_dest_counts[4 * d + a];
+        if (int rc = x_recv_ensure(o, tot, fmt)) return rc;
+        uint64_t dst_off[XA] = {0, 0, 0, 0};
+        for (uint32_t s = 0; s < n; ++s)
+        {
+            ad_ctx* c = ctxs[s];
+            for (int a = 0; a < XA; ++a)
+            {
+                uint64_t src_off = 0;
+                for (uint32_t e = 0; e < d; ++e) src_off += c->x_dest_counts[4 * e + a];
+                const uint64_t cnt = c->x_dest_counts[4 * d + a], ub = x_unit_bytes(a, fmt);
+                if (cnt)
+                {
+                    char* dst = x_recv(o, a)->as<char>() + ub * dst_off[a];
+                    const char* src = x_send(c, a)->as<char>() + ub * src_off;
+                    if (c->device == o->device)
+                        HIPCHK(o, hipMemcpyAsync(dst, src, ub * cnt, hipMemcpyDeviceToDevice, o->stream));
+                    else
+                        HIPCHK(o, hipMemcpyPeerAsync(dst, o->device, src, c->device, ub * cnt, o->stream));
+                    if (s != d) moved += ub * cnt;
+                }
+                dst_off[a] += cnt;
+            }
+        }
+    }
+    const double t2 = now_ms();
+    // 3. K3 on every owner
+    double ms_merge = 0;
+    for (uint32_t d = 0; d < n; ++d)
+    {
+        ad_ctx* o = ctxs[d];
+        if (hipSetDevice(o->device) != hipSuccess) return o->fail(AD_E_DEVICE, "hipSetDevice");
+        std::vector<uint64_t> src_parts(n);
+        for (uint32_t s = 0; s < n; ++s) src_parts[s] = ctxs[s]->x_dest_counts[4 * d + 0];
+        if (int rc = x_merge(o, n, src_parts.data(), txn_base[d], n_owned[d], o->stream, &out[d])) return rc;
+        ms_merge += out[d].ms_device;
+    }
+    if (stats)
+    {
+        memset(stats, 0, sizeof(*stats));
+        stats->bytes_moved = moved;
+        stats->ms_export = t1 - t0;
+        stats->ms_move = t2 - t1;
+        stats->ms_merge = ms_merge;
+        stats->ms_total = now_ms() - t0;
+    }
+    return AD_OK;
+}
+
+int ad_comm_unique_id(uint8_t* id)
+{
+    if (!id) return AD_E_INVAL;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return AD_E_DEVICE;
+    memcpy(id, u.internal, AD_COMM_ID_BYTES);
+    return AD_OK;
+}
+
+int ad_comm_init(ad_ctx* c, const uint8_t* id, int rank, int world)
+{
+    if (!c || !id || world <= 0 || rank < 0 || rank >= world) return AD_E_INVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+    ncclUniqueId u;
+    memcpy(u.internal, id, AD_COMM_ID_BYTES);
+    NCCLCHK(c, ncclCommInitRank(&c->comm, world, u, rank));
+    c->comm_rank = rank;
+    c->comm_world = world;
+    return AD_OK;
+}
+
+int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, const uint64_t* dest_first, uint64_t txn_base,
+                uint64_t n_owned, void* stream, ad_merged* out, ad_exchange_stats* stats)
+{
+    if (!c || !res || !dest_first || !out) return AD_E_INVAL;
+    if (!c->comm) return c->fail(AD_E_STATE, "ad_exchange: no communicator (ad_comm_init)");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const int W = c->comm_world, R = c->comm_rank;
+    const uint32_t fmt = x_format(c);
+    const double t0 = now_ms();
+    // 1. export, grouped by owner rank
+    if (int rc = x_export(c, res, txn_index, (uint32_t)W, dest_first, st)) return rc;
+    const double t1 = now_ms();
+    // 2. the [W][W][4] counts table on every rank (one all-gather), read by the host to size the
+    //    receive buffers and place every source's parts
+    if (!c->xc_dev.ensure(sizeof(uint64_t) * 4 * (size_t)W * (W + 1))) return c->fail(AD_E_NOMEM, "counts table");
+    uint64_t* mine = c->xc_dev.as<uint64_t>() + 4 * (size_t)W * W;
+    HIPCHK(c, hipMemcpyAsync(mine, c->x_dest_counts.data(), sizeof(uint64_t) * 4 * W, hipMemcpyHostToDevice, st));
+    NCCLCHK(c, ncclAllGather(mine, c->xc_dev.as<uint64_t>(), 4 * (size_t)W, ncclUint64, c->comm, st));
+    std::vector<uint64_t> table(4 * (size_t)W * W);
+    HIPCHK(c, hipMemcpyAsync(table.data(), c->xc_dev.p, sizeof(uint64_t) * table.size(), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    auto cnt = [&](int s, int d, int a) { return table[(size_t)4 * W * s + 4 * d + a]; };
+    uint64_t tot[XA] = {0, 0, 0, 0};
+    for (int s = 0; s < W; ++s)
+        for (int a = 0; a < XA; ++a) tot[a] += cnt(s, R, a);
+    if (int rc = x_recv_ensure(c, tot, fmt)) return rc;
+    // 3. grouped send/recv of the four arrays over RCCL (own parts: a device copy)
+    uint64_t moved = 0;
+    NCCLCHK(c, ncclGroupStart());
+    for (int a = 0; a < XA; ++a)
+    {
+        const size_t ub = x_unit_bytes(a, fmt);
+        uint64_t soff = 0, roff = 0;
+        for (int p = 0; p < W; ++p)
+        {
+            const uint64_t sc = cnt(R, p, a), rcv = cnt(p, R, a);
+            const char* sp = x_send(c, a)->as<char>() + ub * soff;
+            char* rp = x_recv(c, a)->as<char>() + ub * roff;
+            if (p == R)
+            {
+                if (sc) HIPCHK(c, hipMemcpyAsync(rp, sp, ub * sc, hipMemcpyDeviceToDevice, st));
+            }
+            else
+            {
+                // bytes as uint8 (every array is a whole number of bytes; no reduction)
+                if (sc) NCCLCHK(c, ncclSend(sp, ub * sc, ncclUint8, p, c->comm, st));
+                if (rcv) NCCLCHK(c, ncclRecv(rp, ub * rcv, ncclUint8, p, c->comm, st));
+                moved += ub * sc;
+            }
+            soff += sc;
+            roff += rcv;
+        }
+    }
+    NCCLCHK(c, ncclGroupEnd());
+    HIPCHK(c, hipStreamSynchronize(st));
+    const double t2 = now_ms();
+    // 4. K3 over the parts of every source (rank = slice order)
+    std::vector<uint64_t> src_parts(W);
+    for (int s = 0; s < W; ++s) src_parts[s] = cnt(s, R, 0);
+    if (int rc = x_merge(c, (uint32_t)W, src_parts.data(), txn_base, n_owned, st, out)) return rc;
+    if (stats)
+    {
+        memset(stats, 0, sizeof(*stats));
+        stats->bytes_moved = moved;
+        stats->ms_export = t1 - t0;
+        stats->ms_move = t2 - t1;
+        stats->ms_merge = out->ms_device;
+        stats->ms_total = now_ms() - t0;
+    }
     return AD_OK;
 }
 

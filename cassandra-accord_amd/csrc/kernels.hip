@@ -924,7 +924,7 @@ hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // the owning request found by advancing monotonically). Writes are fully coalesced; reads are
 // contiguous within each request's region.
 constexpr uint32_t PACK_WAVES = 4;
-constexpr uint32_t PACK_UNROLL = 4;
+constexpr uint32_t PACK_UNROLL = 8;
 
 template <typename T>
 __device__ __forceinline__ void pack_run(const uint8_t* __restrict__ reg, const uint32_t* st, const uint64_t* src,

@@ -338,6 +338,38 @@ int ad_parts_merge(ad_ctx* ctx, const ad_parts* in_dev, uint32_t n_src, const ui
 int ad_parts_union(ad_ctx* ctx, const ad_parts* in_dev, uint32_t n_src, const uint64_t* src_parts,
                    uint64_t txn_base, uint64_t n_owned, void* stream, ad_merged* out);
 
+/* ---- node exchange (SURVEY §8 e): combine the stores' PartialDeps on the owning store --------
+ * After every store of a node resolved its share of a node batch (ad_deps_batch_device, AD_PARTS_ONLY
+ * is enough), each store's parts are exported grouped by owner, moved to the owner and merged there
+ * (K3, ad_parts_merge) -- CommandStores.mapReduce's reduce with PartialDeps.with
+ * (CommandStores.java:576-593, PreAccept.reduce PreAccept.java:140-156). Store s (slice order) owns the
+ * requests [txn_base[s], txn_base[s] + n_owned[s]) of the node batch; dest_first[s] (host, n + 1 entries)
+ * cuts store s's local batch (ascending global indices txn_index[s], device) by owner. Ids move as
+ * global ranks when every store has the node's global dictionary installed (ad_set_global_dict),
+ * else as {msb, lsb, node} triplets. Results: one ad_merged per store, device memory owned by it. */
+typedef struct ad_exchange_stats {
+    uint64_t bytes_moved;          /* bytes sent to other stores (xGMI payload) */
+    double ms_export, ms_move, ms_merge, ms_total;
+} ad_exchange_stats;
+
+/* One process driving every store of the node (the Java host: one process, a CommandStore per thread,
+ * one GPU each -- or several stores on one GPU): device copies, hipMemcpyPeerAsync over xGMI between
+ * GPUs. ctxs[s], res[s], txn_index[s], dest_first[s] per store; out[n]. */
+int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* const* res, const int64_t* const* txn_index,
+                      const uint64_t* const* dest_first, const uint64_t* txn_base, const uint64_t* n_owned,
+                      ad_merged* out, ad_exchange_stats* stats);
+
+/* One process per GPU: an RCCL communicator over the node's stores (rank = slice order). Rank 0 makes
+ * the id (ad_comm_unique_id) and the host shares it out of band; every rank then calls ad_comm_init. */
+#define AD_COMM_ID_BYTES 128
+int ad_comm_unique_id(uint8_t* id /* [AD_COMM_ID_BYTES] */);
+int ad_comm_init(ad_ctx* ctx, const uint8_t* id, int rank, int world);
+/* This rank's step: export, RCCL all-gather of the part counts, grouped send/recv of the parts over
+ * xGMI, K3 merge of the requests [txn_base, txn_base + n_owned) this rank owns. dest_first: host,
+ * world + 1 entries. Enqueued on `stream` (NULL: the ctx stream), complete on return. */
+int ad_exchange(ad_ctx* ctx, const ad_deps_result* res_dev, const int64_t* txn_index_dev, const uint64_t* dest_first,
+                uint64_t txn_base, uint64_t n_owned, void* stream, ad_merged* out, ad_exchange_stats* stats);
+
 /* Copy device memory owned by the library (results) into a host buffer: for hosts without a
  * HIP binding of their own (the Panama FFM wrapper). */
 int ad_copy_to_host(ad_ctx* ctx, void* dst, const void* src_dev, uint64_t bytes);

@@ -1,30 +1,33 @@
-"""Per-kernel sums of every counter in a pmc_lean-style output directory (p1..pN passes).
-Usage: python scripts/pmc_table.py gpurun_out/pmc_lean_TAG [kernel-substring ...]"""
-import collections
+"""Per-kernel table of the PMC passes written by scripts/pmc_r2.sh (counter values summed over the
+dispatches of a kernel, averaged per dispatch). Usage: python scripts/pmc_table.py gpurun_out/pmc_<tag> [kernel-substring ...]"""
 import csv
 import glob
 import os
 import sys
+from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("adx::", "")
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
+    return n.replace("void ", "").replace("adx::", "")
 
 
-def main(d, pats):
-    agg = collections.defaultdict(lambda: collections.defaultdict(float))
-    calls = collections.defaultdict(set)
-    for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
-        for r in csv.DictReader(open(f)):
-            k = short(r["Kernel_Name"])
-            if pats and not any(p in k for p in pats):
-                continue
-            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-            calls[(k, r["Counter_Name"])].add(r.get("Dispatch_Id", ""))
-    for k, c in agg.items():
-        print(k)
-        for n, v in sorted(c.items()):
-            print("   %-36s %16.0f  (per launch %14.0f)" % (n, v, v / max(1, len(calls[(k, n)]))))
+def main(d, filt):
+    vals = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for f in glob.glob(os.path.join(d, "p*", "run_counter_collection.csv")):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                if filt and not any(x in k for x in filt):
+                    continue
+                vals[k][row["Counter_Name"]] += float(row["Counter_Value"])
+                disp[(k, row["Counter_Name"])].add(row["Dispatch_Id"])
+    for k, cs in sorted(vals.items()):
+        print("##", k)
+        for c, v in sorted(cs.items()):
+            n = max(1, len(disp[(k, c)]))
+            print("  %-32s %16.0f" % (c, v / n))
 
 
 if __name__ == "__main__":

@@ -140,3 +140,67 @@ def test_merge_rejects_overlapping_sources():
         st.merge_parts(_parts(recv, 2 * counts[0]), [int(counts[0, 0])] * 2, 0, len(w.queries))
     assert ei.value.code == A.AD_E_INVAL
     st.close()
+
+
+def _run_exchange_local(w, bounds, rank_ids):
+    """The library's own node exchange (ad_exchange_local): N stores in this process on cuda:0,
+    parts moved device-to-device and merged on each owner -- no Python transport."""
+    dev = torch.device("cuda", 0)
+    lo, hi = bounds
+    n = len(lo)
+    n_total = len(w.queries)
+    bases = exchange.owner_bases(n_total, n)
+    stores, keep, idxs, tis = [], [], [], []
+    for g in range(n):
+        local, idx = synth.shard_local(w, lo[g], hi[g])
+        st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, local.slices)
+        st.load(local)
+        qdev, k = native.device_queries(local.queries, dev)
+        keep.append((qdev, k))
+        ti = torch.from_numpy(np.ascontiguousarray(idx, np.int64)).to(dev)
+        keep.append(ti)
+        stores.append(st)
+        idxs.append(idx)
+        tis.append(ti.data_ptr())
+    if rank_ids:
+        g = exchange.build_global_dict([st.dictionary() for st in stores])
+        for st in stores:
+            st.set_global_dict(g)
+    results = []
+    for st, (qdev, _) in zip(stores, keep[0::2]):
+        res, _ = st.deps_batch_device(qdev, None, parts_only=True)
+        results.append(res)
+    dfs = [np.searchsorted(idx, np.asarray(bases[:n], np.int64)).astype(np.uint64).tolist() + [len(idx)] for idx in idxs]
+    torch.cuda.synchronize()
+    merged, stats = native.exchange_local(stores, results, tis, dfs, bases[:n], [bases[d + 1] - bases[d] for d in range(n)])
+    out = [(bases[d], bases[d + 1] - bases[d], stores[d].merged_to_host(merged[d])) for d in range(n)]
+    for st in stores:
+        st.close()
+    return out, stats
+
+
+@pytest.mark.parametrize("rank_ids", [False, True])
+@pytest.mark.parametrize("case", ["random3", "config3_2", "config3_4", "config3_8", "config4_4", "config2_4"])
+def test_exchange_local(case, rank_ids):
+    if case == "random3":
+        w = synth.random_small(7)
+        w.slices = None
+        bounds = synth.cut_bounds([-100, 150])
+    elif case.startswith("config3"):
+        n = int(case.split("_")[1])
+        w = synth.config3(n_txns=40000, n_keys=6000, seed=21 + n)
+        bounds = synth.shard_bounds(n)
+    elif case == "config4_4":
+        w = synth.config4(n_txns=3000, n_keys=4000, n_ranges=800, n_hist_txns=3000)
+        bounds = synth.cut_bounds([-(1 << 30), 0, 1 << 30])
+    else:
+        w = synth.config2(n_txns=20000, n_keys=20000, n_hist_entries=200000)
+        bounds = synth.shard_bounds(4)
+    expect = pyoracle.resolve_sharded(w, len(bounds[0]), bounds=bounds)
+    out, stats = _run_exchange_local(w, bounds, rank_ids)
+    for base, n, got in out:
+        ok, why = got.equals(expect.window(base, n), detail=True)
+        if not ok:
+            bad = got.first_mismatch(expect.window(base, n))
+            pytest.fail("owner base %d: %s; first mismatch %s" % (base, why, bad[:2] if bad else None))
+    assert len(bounds[0]) == 1 or stats["bytes_moved"] > 0
