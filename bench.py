@@ -31,16 +31,20 @@ from accord_deps import exchange, native, synth  # noqa: E402
 
 METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-STAGES = ["lean resolve pass 1 (2 requests/wave)", "deferred requests (split K0..K2)", "prepare (request records, key slots)",
-          "lean resolve pass 2 (1 request/wave)", "offsets scan", "pack", "general fused resolve (lean deferrals)"]
+STAGES = ["lean resolve pass 1", "deferred requests (split K0..K2)", "prepare (request records: S / self ranks)",
+          "lean resolve pass 2 (1 request/wave)", "offsets scan", "offsets + pack (tile sums, tile scan, scan+pack)",
+          "general fused resolve (lean deferrals)"]
 KERNEL_OF_STAGE = ["k_resolve_lean<2u, false>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
-                   "k_resolve_lean<1u, false>", "k_scan_blocks+k_scan_sums+k_scan_add", "k_pack", "k_resolve"]
+                   "k_resolve_lean<1u, false>", "-", "k_tile_sums+k_tile_scan+k_pack_tiles", "k_resolve"]
 
 
-def kernel_of_stage(i, ranges=False):
+def kernel_of_stage(i, ranges=False, rpw1=2):
     """Kernel name (as rocprofv3 reports it, namespace and arguments stripped) of pipeline stage i;
-    the lean kernels are instantiated with range support when the store has range commands."""
+    the lean kernels are instantiated with range support when the store has range commands, and lean
+    pass 1 runs four requests per wave for batches of small requests (abi.cpp lean_rpw1)."""
     k = KERNEL_OF_STAGE[i]
+    if i == 0 and rpw1 == 4:
+        k = k.replace("<2u", "<4u")
     return k.replace("false>", "true>") if ranges else k
 # K1 + K2 of every request (SURVEY §8 a4-a10) run in these stages / kernels: the roofline's "dominant kernel"
 RESOLVE_STAGES = [0, 3, 6]
@@ -802,9 +806,10 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests / dry runs)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 4, 5),
-                    help="2: BASELINE config 2 (the headline line, default); 1: SEQUENTIAL PreAccept batch "
-                         "(host API); 4: range transactions; 5: execution levels (K5)")
+    ap.add_argument("--config", type=int, default=None, choices=(1, 2, 3, 4, 5),
+                    help="default: 2 on one GPU (BASELINE config 2, the headline), 3 on N > 1 GPUs (N/8 of BASELINE "
+                         "config 3, exactly config 3 at N = 8, through the library's RCCL node exchange); "
+                         "1: SEQUENTIAL PreAccept batch (host API); 4: range transactions; 5: execution levels (K5)")
     ap.add_argument("--union", type=int, default=0, metavar="R",
                     help="with config 2: the coordinator's Deps.merge of R replica replies (SURVEY 8 f2)")
     ap.add_argument("--preaccept", action="store_true",
@@ -823,6 +828,8 @@ def main():
                     help="config 2: share of out-of-order PreAccepts (txnId inside the history's last ticks)")
     ap.add_argument("--unordered-window", type=int, default=2000, help="hlc ticks of --unordered-frac's lateness")
     ap.add_argument("--recovery-scan", type=int, default=3, choices=(0, 1, 2, 3), help="AD_RECOVER_* scan of --recovery")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the node exchange (ad_exchange over the library's RCCL communicator) even on one GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (RCCL, one GPU per rank: the measured configuration); gloo: rehearsal of the "
                          "N>1 path on fewer GPUs (ranks share GPUs, the exchange is staged through host memory)")
@@ -845,6 +852,8 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    if args.config is None:
+        args.config = 3 if world > 1 else 2
     if args.config == 5:
         return bench_levels(args, rank, world, local, dev)
     if args.config == 4:
@@ -860,75 +869,120 @@ def main():
     if args.cfk_update:
         return bench_cfk_update(args, rank, world, local, dev)
 
+    return bench_deps(args, rank, world, local, dev)
+
+
+def bench_deps(args, rank, world, local, dev):
+    """The BASELINE metric: config 2 on one GPU (the headline); config 3 (N/8 of it on N GPUs, exactly
+    config 3 at N = 8) for the node path: every store resolves the requests touching its slice, then
+    the library's node exchange (ad_exchange: RCCL over xGMI + K3 merge on the owning GPU) combines them.
+    `--config 2` at N > 1: config 2 weak-scaled per GPU through the same exchange."""
     s = args.scale
+    cfg = args.config
     t0 = time.time()
-    w, txn_index, n_total = synth.config2_sharded(rank, world, n_txns_per_gpu=int(1_000_000 * s),
-                                                  n_keys_per_gpu=int(1_000_000 * s),
-                                                  n_hist_entries_per_gpu=int(16_000_000 * s))
+    exec_ids = None
+    if cfg == 3:
+        w, txn_index, n_total, exec_ids = synth.config3_shard(rank, world, txns_per_gpu=int(8_000_000 * s),
+                                                             keys_per_gpu=int(1_250_000 * s))
+    else:
+        w, txn_index, n_total = synth.config2_sharded(rank, world, n_txns_per_gpu=int(1_000_000 * s),
+                                                      n_keys_per_gpu=int(1_000_000 * s),
+                                                      n_hist_entries_per_gpu=int(16_000_000 * s))
     mix = args.accept_frac > 0 or args.unordered_frac > 0
     if mix:
-        if world > 1:
-            raise SystemExit("--accept-frac / --unordered-frac: single store only")
+        if world > 1 or cfg != 2:
+            raise SystemExit("--accept-frac / --unordered-frac: config 2 on a single store only")
         w = synth.with_request_mix(w, args.accept_frac, args.unordered_frac, args.unordered_window)
-    log("rank %d: generated in %.1f s: %d keys, %d entries, %d of %d requests routed here, %d probes" %
-        (rank, time.time() - t0, len(w.cfk.keys), w.cfk.n_entries, len(w.queries), n_total, w.queries.n_probes))
+    log("rank %d: config %d generated in %.1f s: %d keys, %d entries, %d of %d requests routed here, %d probes" %
+        (rank, cfg, time.time() - t0, len(w.cfk.keys), w.cfk.n_entries, len(w.queries), n_total, w.queries.n_probes))
 
     store = native.DeviceCommandStore(device=local, slices=w.slices)
+    t_ing = time.time()
     store.load(w)
+    ingest_ms = 1000.0 * (time.time() - t_ing)
     qdev, keep = native.device_queries(w.queries, dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
-
-    if world > 1:
-        engine = exchange.GpuEngine(store, qdev, txn_index, dev, stream=sp)
-        gloo = args.dist_backend == "gloo"
-        ex = exchange.ShardExchange(engine, txn_index, n_total, rank, world, count_device=None if gloo else dev,
-                                    stage_cpu=gloo)
+    last = {}
+    node_x = None
+    if (world > 1 and args.dist_backend == "nccl") or args.exchange:
+        # ingest-time: the node's global dictionary (ids travel as uint32 global ranks), the RCCL communicator
         t_g = time.time()
-        n_global = ex.install_global_dict()       # ingest-time: ids travel as uint32 global ranks
-        log("rank %d: global dictionary of %d ids installed in %.1f s" % (rank, n_global, time.time() - t_g))
+        if cfg == 3:
+            got = [None] * world
+            if world > 1:
+                dist.all_gather_object(got, (exec_ids.msb, exec_ids.lsb, exec_ids.node))
+            else:
+                got = [(exec_ids.msb, exec_ids.lsb, exec_ids.node)]
+            from accord_deps.model import Tids
+            g = synth.config3_global_dict(w.params, [Tids(*x) for x in got])
+        else:
+            mine = store.dictionary()
+            got = [None] * world
+            if world > 1:
+                dist.all_gather_object(got, (mine.msb, mine.lsb, mine.node))
+            else:
+                got = [(mine.msb, mine.lsb, mine.node)]
+            from accord_deps.model import Tids
+            g = exchange.build_global_dict([Tids(*x) for x in got])
+        store.set_global_dict(g)
+        node_x = exchange.NodeExchange(store, qdev, txn_index, n_total, rank, world, dev, stream=sp)
+        log("rank %d: global dictionary of %d ids + RCCL communicator in %.1f s" % (rank, len(g.msb), time.time() - t_g))
+
+        def step():
+            mg = node_x.step()
+            return node_x.last_stats, mg.ms_device, node_x.last_exchange
+    elif world > 1:
+        # gloo rehearsal on fewer GPUs than ranks: the same protocol with a Python transport staged
+        # through host memory (RCCL cannot put two ranks on one GPU)
+        engine = exchange.GpuEngine(store, qdev, txn_index, dev, stream=sp)
+        ex = exchange.ShardExchange(engine, txn_index, n_total, rank, world, count_device=None, stage_cpu=True)
+        ex.install_global_dict()
 
         def step():
             mg = ex.step()
-            return engine.last_stats, mg.ms_device
+            return engine.last_stats, mg.ms_device, None
     else:
-        last = {}
-
         def step():
             last["res"], st = store.deps_batch_device(qdev, sp)
-            return st, 0.0
+            return st, 0.0, None
 
     stats = None
     for _ in range(args.warmup):
-        stats, _ = step()
+        stats, _, _ = step()
     torch.cuda.synchronize(dev)
-    if stats:
-        log("rank %d: ingest %.1f ms (host dictionary + device index build)" % (rank, stats["ms_ingest"]))
 
     stage_ms = np.zeros(7)
     merge_ms = 0.0
+    xs = dict(bytes_moved=0, ms_export=0.0, ms_move=0.0, ms_merge=0.0, ms_total=0.0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        stats, mms = step()
+        stats, mms, xst = step()
         stage_ms += np.array(stats["ms_stage"][:7])
         merge_ms += mms
+        if xst:
+            for k in xs:
+                xs[k] += xst[k]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     stage_ms /= max(args.steps, 1)
     merge_ms /= max(args.steps, 1)
+    for k in xs:
+        xs[k] /= max(args.steps, 1)
     probes = w.queries.n_probes
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=_red_dev(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        p = torch.tensor([probes], dtype=torch.int64, device=_red_dev(dev))
+        p = torch.tensor([probes, xs["bytes_moved"]], dtype=torch.int64, device=_red_dev(dev))
         dist.all_reduce(p, op=dist.ReduceOp.SUM)
-        probes = int(p.item())
+        probes = int(p[0].item())
+        xs["bytes_moved_all_ranks"] = int(p[1].item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     value = probes / (ms_per_step / 1000.0)
 
@@ -938,9 +992,25 @@ def main():
     sbytes = stage_bytes(w, stats)
     res_ms = float(sum(stage_ms[i] for i in RESOLVE_STAGES))
     achieved = sbytes[0] / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
-    res_kernels = [kernel_of_stage(i) for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
+    lean_rpw1 = 4 if w.queries.n_probes <= 3 * max(1, len(w.queries)) else 2
+    res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1) for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
     traffic, traffic_src = measured_traffic(res_kernels)
-
+    if cfg == 3:
+        workload = ("config3 (%d/8 of it on %d GPU%s): %d txns over %d uniform keys, %d-txn history x 4 keys, %d-request "
+                    "probe batch, token-range sharded (EvenSplit), SNAPSHOT, 1 CommandStore per GPU%s" %
+                    (world, world, "s" if world > 1 else "", int(w.params["n_txns"]), int(w.params["n_keys"]),
+                     int(w.params["n_hist_txns"]), n_total,
+                     ", per-store partials exchanged over RCCL inside libaccord_deps (ad_exchange) + K3 merge on the owning GPU"
+                     if world > 1 else ""))
+    else:
+        workload = ("config2 (weak-scaled per GPU): %d txns x 8 Zipf(0.99) keys, %d keys and a %d-entry CommandsForKey "
+                    "history per GPU, SNAPSHOT, 1 CommandStore per GPU%s" %
+                    (n_total, int(1_000_000 * s) * world, w.cfk.n_entries,
+                     ", per-store partials exchanged over RCCL inside libaccord_deps (ad_exchange) + K3 merge on the owning GPU"
+                     if world > 1 else "") +
+                    ("; request mix: %d Accepts of in-flight txns (S = executeAt, self excluded), %d PreAccepts up to %d hlc "
+                     "ticks late, the rest fresh PreAccepts" % (w.params["n_accept"], w.params["n_unordered"],
+                                                                args.unordered_window) if mix else ""))
     out = {
         "metric": METRIC,
         "value": value,
@@ -954,14 +1024,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic",
-        "config": {"workload": "config2 (weak-scaled per GPU): %d txns x 8 Zipf(0.99) keys, %d keys and a %d-entry "
-                               "CommandsForKey history per GPU, SNAPSHOT, 1 CommandStore per GPU%s" %
-                               (n_total, int(1_000_000 * s) * world, w.cfk.n_entries,
-                                ", partials all-to-all over RCCL + on-GPU merge" if world > 1 else "") +
-                               ("; request mix: %d Accepts of in-flight txns (S = executeAt, self excluded), %d PreAccepts "
-                                "up to %d hlc ticks late, the rest fresh PreAccepts" %
-                                (w.params["n_accept"], w.params["n_unordered"], args.unordered_window) if mix else ""),
-                   "txns_per_step": n_total, "txn_key_pairs_per_step": probes,
+        "config": {"workload": workload, "txns_per_step": n_total, "txn_key_pairs_per_step": probes,
                    "parallelism": "store-per-gpu x%d" % world},
         "roofline": {"bound": "hbm", "kernel": " + ".join(res_kernels), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -970,11 +1033,15 @@ def main():
         "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
         "deferred": {"lean_pass1_to_pass2": int(stats.get("n_lean_pass2", 0)),
                      "lean_to_general": int(stats.get("n_deferred_lean", 0)), "to_split": int(stats["n_deferred"])},
-        "ingest_ms": stats["ms_ingest"],
+        "ingest_ms": ingest_ms,
     }
-    if world > 1:
+    if node_x is not None or world > 1:
         out["stages_ms"]["merge (K3, owner)"] = round(merge_ms, 4)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["exchange"] = {"ms_export": round(xs["ms_export"], 4), "ms_move": round(xs["ms_move"], 4),
+                           "ms_merge": round(xs["ms_merge"], 4), "ms_total": round(xs["ms_total"], 4),
+                           "xgmi_bytes_per_step_rank0": int(xs["bytes_moved"]),
+                           "xgmi_bytes_per_step_all_ranks": int(xs.get("bytes_moved_all_ranks", 0))}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and node_x is None:
         # the PCIe-inclusive rate a host caller sees through ad_deps_batch (host arrays in, packed
         # host CSR arrays out; outside the timed region, never `value`)
         t0 = time.perf_counter()
@@ -991,7 +1058,6 @@ def main():
     store.close()
     if world > 1:
         dist.destroy_process_group()
-
 
 if __name__ == "__main__":
     main()

@@ -217,3 +217,34 @@ class ShardExchange:
             else:
                 dist.all_to_all_single(ro, si, out_splits, in_splits, group=self.group)
         return e.merge(totals, rcounts[:, 0], self.txn_base, self.n_owned)
+
+
+class NodeExchange:
+    """The multi-GPU step on the library's own transport (accord_deps.h ad_exchange): one process per
+    GPU, an RCCL communicator inside libaccord_deps over the node's stores (rank = slice order); per
+    step the store resolves its local batch (parts only), then ad_exchange exports, moves (RCCL
+    grouped send/recv over xGMI) and merges (K3) the requests this rank owns. torch.distributed is only
+    the out-of-band channel for the communicator id and the ingest-time global dictionary."""
+
+    def __init__(self, store, qdev, txn_index, n_total, rank, world, device, stream=None, group=None):
+        import torch
+        self.store, self.qdev, self.rank, self.world, self.stream = store, qdev, rank, world, stream
+        bases = owner_bases(n_total, world)
+        self.txn_base = bases[rank]
+        self.n_owned = bases[rank + 1] - bases[rank]
+        ti = np.asarray(txn_index, np.int64)
+        self.dest_first = np.searchsorted(ti, np.asarray(bases[:world], np.int64)).astype(np.uint64).tolist() + [len(ti)]
+        self.ti = torch.from_numpy(np.ascontiguousarray(ti)).to(device)
+        from . import native
+        uid = [native.comm_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0, group=group)
+        store.comm_init(uid[0], rank, world)
+        self.last_stats = None
+        self.last_exchange = None
+
+    def step(self):
+        res, self.last_stats = self.store.deps_batch_device(self.qdev, self.stream, parts_only=True)
+        mg, self.last_exchange = self.store.exchange(res, self.ti.data_ptr(), self.dest_first, self.txn_base,
+                                                     self.n_owned, self.stream)
+        return mg

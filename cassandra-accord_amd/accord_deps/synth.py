@@ -362,6 +362,142 @@ def config3(n_txns=64_000_000, keys_per_txn=4, n_keys=10_000_000, hist_frac=0.75
                                 n_hist_txns=n_hist, semantics="SNAPSHOT"))
 
 
+def _h(x, salt):
+    return splitmix64(np.asarray(x, np.uint64) ^ np.uint64(salt & 0xFFFFFFFFFFFFFFFF))
+
+
+def _txn_keys(j, n_keys, keys_per_txn, salt):
+    """Key ranks of txns j (uint64 array), keys_per_txn distinct uniform draws each, from hashes of
+    (j, slot): every rank derives the same keys for the same txn without sharing a random stream."""
+    ks = np.empty((len(j), keys_per_txn), np.int64)
+    for i in range(keys_per_txn):
+        ks[:, i] = (_h(j * np.uint64(keys_per_txn) + np.uint64(i), salt) % np.uint64(n_keys)).astype(np.int64)
+    for rnd in range(1, 32):
+        srt = np.sort(ks, axis=1)
+        rows = np.nonzero((srt[:, 1:] == srt[:, :-1]).any(axis=1))[0]
+        if not len(rows):
+            break
+        sub = ks[rows]
+        for i in range(1, keys_per_txn):
+            d = (sub[:, i:i + 1] == sub[:, :i]).any(axis=1)
+            if d.any():
+                jj = j[rows[d]]
+                sub[d, i] = (_h(jj * np.uint64(keys_per_txn) + np.uint64(i), salt + 0x9E37 * rnd) % np.uint64(n_keys)).astype(np.int64)
+        ks[rows] = sub
+    return ks
+
+
+def config3_shard(rank, world, txns_per_gpu=8_000_000, keys_per_gpu=1_250_000, keys_per_txn=4, hist_frac=0.75,
+                  seed=0xACC0D003, tail_unapplied=2, chunk=4_000_000):
+    """BASELINE config 3 -- 64M txns over 10M uniform keys, token-range sharded across 8 GPUs, SNAPSHOT --
+    weak-scaled to `world` GPUs: world/8 of it (world x 8M txns over world x 1.25M keys), exactly config 3
+    at world = 8. The first 75 % of the txns form the history (APPLIED except the last 2 entries per key,
+    drawn from PREACCEPTED..STABLE, the proposed/committed ones at an executeAt 1..1000 hlc ticks later),
+    the rest is the probe batch. Store `rank` owns EvenSplit token slice `rank` (ShardDistributor.EvenSplit,
+    ShardDistributor.java:106-156). Every rank derives the same global txns from hashes (txn j: hlc 1 + j,
+    kind and node from its hash, keys from _txn_keys) and keeps only what touches its slice, so no rank
+    materialises the whole job. Returns (Workload of this store: its CommandsForKey and the requests
+    touching it with their keys restricted to the slice, global request indices, number of requests,
+    this store's proposed/committed executeAts for the node's global dictionary)."""
+    T = int(txns_per_gpu) * world
+    K = int(keys_per_gpu) * world
+    H = int(T * hist_frac)
+    Q = T - H
+    salt = seed * 0x100000001B3 + world
+    token = key_tokens(K, seed)
+    lo, hi = shard_bounds(world)
+    lo_r, hi_r = int(lo[rank]), int(hi[rank])
+
+    def in_slice(tok):     # EndInclusive (lo, hi], as the store's slice (synth.route, slice_workload)
+        return (tok > lo_r) & (tok <= hi_r)
+
+    # ---- history entries of this slice
+    e_tok, e_j = [], []
+    for j0 in range(0, H, chunk):
+        j = np.arange(j0, min(H, j0 + chunk), dtype=np.uint64)
+        tk = token[_txn_keys(j, K, keys_per_txn, salt)]
+        m = in_slice(tk)
+        rows, cols = np.nonzero(m)
+        e_tok.append(tk[rows, cols])
+        e_j.append(j[rows].astype(np.int64))
+    e_tok = np.concatenate(e_tok) if e_tok else np.zeros(0, np.int64)
+    e_j = np.concatenate(e_j) if e_j else np.zeros(0, np.int64)
+    order = np.argsort(e_tok, kind="stable")          # j ascending within a key (generation order)
+    e_tok, e_j = e_tok[order], e_j[order]
+    uk, start, counts = np.unique(e_tok, return_index=True, return_counts=True)
+    seg = np.zeros(len(uk) + 1, np.uint64)
+    seg[1:] = np.cumsum(counts)
+    pos = np.arange(len(e_tok)) - np.repeat(start, counts)
+    from_end = np.repeat(counts, counts) - 1 - pos
+    hj = _h(e_j.astype(np.uint64), salt + 1)
+    kind = (hj & np.uint64(1)).astype(np.uint8)                      # Read / Write 50/50 (per txn)
+    node = (1 + (hj >> np.uint64(8)) % np.uint64(16)).astype(np.int32)
+    bump = (1 + (hj >> np.uint64(16)) % np.uint64(1000)).astype(np.uint64)
+    txn = make_txn_ids(1, 1 + e_j.astype(np.uint64), kind, node)
+    status = np.full(len(e_j), A.ST_APPLIED, np.uint8)
+    tail = from_end < tail_unapplied
+    he = _h(e_j.astype(np.uint64) * np.uint64(0x10001) + (e_tok.view(np.uint64) & np.uint64(0xFFFF)), salt + 2)
+    status[tail] = (A.ST_PREACCEPTED + (he[tail] % np.uint64(4))).astype(np.uint8)
+    has_exec = (status >= A.ST_ACCEPTED) & (status <= A.ST_STABLE)
+    bumped = make_timestamps(1, 1 + e_j.astype(np.uint64) + bump, kind.astype(np.uint64) << np.uint64(1),
+                             EXEC_NODE_BASE + e_j)
+    ex = Tids(np.where(has_exec, bumped.msb, txn.msb), np.where(has_exec, bumped.lsb, txn.lsb),
+              np.where(has_exec, bumped.node, txn.node))
+    cfk = CfkSnapshot(uk, seg, txn, ex, status)
+    exec_ids = Tids(bumped.msb[has_exec], bumped.lsb[has_exec], bumped.node[has_exec])
+    # ---- the probe batch: requests touching this slice, keys restricted to it (ascending)
+    q_tok, q_row = [], []
+    for j0 in range(H, T, chunk):
+        j = np.arange(j0, min(T, j0 + chunk), dtype=np.uint64)
+        tk = token[_txn_keys(j, K, keys_per_txn, salt)]
+        m = in_slice(tk)
+        rows, cols = np.nonzero(m)
+        q_tok.append(tk[rows, cols])
+        q_row.append(j[rows].astype(np.int64) - H)
+    q_tok = np.concatenate(q_tok) if q_tok else np.zeros(0, np.int64)
+    q_row = np.concatenate(q_row) if q_row else np.zeros(0, np.int64)
+    o = np.lexsort((q_tok, q_row))
+    q_tok, q_row = q_tok[o], q_row[o]
+    idx, cnt = np.unique(q_row, return_counts=True)
+    key_off = np.zeros(len(idx) + 1, np.uint64)
+    key_off[1:] = np.cumsum(cnt)
+    jq = (idx + H).astype(np.uint64)
+    hq = _h(jq, salt + 1)
+    qtxn = make_txn_ids(1, np.uint64(H + 2000) + idx.astype(np.uint64), (hq & np.uint64(1)).astype(np.uint8),
+                        (1 + (hq >> np.uint64(8)) % np.uint64(16)).astype(np.int32))
+    q = Queries(qtxn, Tids(qtxn.msb.copy(), qtxn.lsb.copy(), qtxn.node.copy()), key_off, q_tok)
+    w = Workload("config3_shard", cfk, RangeCommands.empty(), Redundant.empty(), q,
+                 params=dict(rank=rank, world=world, n_txns=T, n_keys=K, n_hist_txns=H, keys_per_txn=keys_per_txn,
+                             seed=seed, semantics="SNAPSHOT", salt=salt),
+                 slices=np.array([[lo_r, hi_r]], dtype=np.int64))
+    return w, idx.astype(np.int64), Q, exec_ids
+
+
+def _pack_c3(t):
+    """Order-preserving u64 of config3_shard's ids (epoch 1, hlc < 2^32, identity flags, node < 2^27):
+    Timestamp.compareTo order (Timestamp.java:208-217) on these ids."""
+    hlc = t.lsb >> np.uint64(16)
+    return (hlc << np.uint64(32)) | ((t.lsb & np.uint64(0x1E)) << np.uint64(27)) | t.node.astype(np.uint64)
+
+
+def config3_global_dict(params, exec_ids):
+    """The node's global TxnId dictionary for config3_shard (ShardExchange.install_global_dict's union of
+    every store's dictionary, built without gathering the txnIds): every history txnId (all appear in
+    some store) and the proposed/committed executeAts every store reported (`exec_ids`: list of Tids),
+    ascending and unique. Valid for config3_shard's ids only (_pack_c3)."""
+    H = int(params["n_hist_txns"])
+    salt = int(params["salt"])
+    j = np.arange(H, dtype=np.uint64)
+    hj = _h(j, salt + 1)
+    txn = make_txn_ids(1, 1 + j, (hj & np.uint64(1)).astype(np.uint8), (1 + (hj >> np.uint64(8)) % np.uint64(16)).astype(np.int32))
+    packed = np.concatenate([_pack_c3(txn)] + [_pack_c3(e) for e in exec_ids])
+    u = np.unique(packed)
+    hlc = u >> np.uint64(32)
+    flags = (u >> np.uint64(27)) & np.uint64(0x1E)
+    node = (u & np.uint64((1 << 27) - 1)).astype(np.int32)
+    return make_timestamps(1, hlc, flags, node)
+
+
 def config4(n_txns=1_000_000, keys_per_txn=4, n_keys=1_000_000, n_ranges=100_000, n_hist_txns=1_000_000,
             seed=0xACC0D004, log2_min=8, log2_max=20):
     """Config 4: 100k Range-domain Write commands (EndInclusive (s, s+w], s uniform i32, w log-uniform

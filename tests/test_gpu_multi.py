@@ -204,3 +204,75 @@ def test_exchange_local(case, rank_ids):
             bad = got.first_mismatch(expect.window(base, n))
             pytest.fail("owner base %d: %s; first mismatch %s" % (base, why, bad[:2] if bad else None))
     assert len(bounds[0]) == 1 or stats["bytes_moved"] > 0
+
+
+def _whole_from_shards(parts):
+    """The node-wide workload the config3_shard stores slice: their CommandsForKeys concatenated
+    (disjoint, slice order) and every request with all its keys -- the input of the sharded oracle."""
+    from accord_deps.model import CfkSnapshot, Queries, RangeCommands, Redundant, Tids, Workload
+    cfks = [p[0].cfk for p in parts]
+    keys = np.concatenate([c.keys for c in cfks])
+    segs = [c.seg.astype(np.int64) for c in cfks]
+    off = np.cumsum([0] + [int(s[-1]) for s in segs])
+    seg = np.concatenate([segs[0]] + [s[1:] + o for s, o in zip(segs[1:], off[1:])]).astype(np.uint64)
+    cfk = CfkSnapshot(keys, seg, Tids.concat([c.txn for c in cfks]), Tids.concat([c.exec for c in cfks]),
+                      np.concatenate([c.status for c in cfks]))
+    Q = parts[0][2]
+    rows, toks = [], []
+    for w, idx, _, _ in parts:
+        q = w.queries
+        cnt = np.diff(q.key_off.astype(np.int64))
+        rows.append(np.repeat(idx, cnt))
+        toks.append(q.keys)
+    rows = np.concatenate(rows)
+    toks = np.concatenate(toks)
+    o = np.lexsort((toks, rows))
+    rows, toks = rows[o], toks[o]
+    cnt = np.bincount(rows, minlength=Q)
+    key_off = np.zeros(Q + 1, np.uint64)
+    key_off[1:] = np.cumsum(cnt)
+    # request ids: every store holds the same txnId for a request it sees
+    msb = np.zeros(Q, np.uint64)
+    lsb = np.zeros(Q, np.uint64)
+    node = np.zeros(Q, np.int32)
+    for w, idx, _, _ in parts:
+        msb[idx], lsb[idx], node[idx] = w.queries.txn.msb, w.queries.txn.lsb, w.queries.txn.node
+    t = Tids(msb, lsb, node)
+    q = Queries(t, Tids(msb.copy(), lsb.copy(), node.copy()), key_off, toks)
+    return Workload("config3_whole", cfk, RangeCommands.empty(), Redundant.empty(), q)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_config3_shards_exchange_local(world):
+    # bench.py's N > 1 workload (config3_shard per store, the analytic global dictionary, rank-format
+    # parts) through the library's node exchange, against the sharded oracle of the whole job
+    dev = torch.device("cuda", 0)
+    parts = [synth.config3_shard(r, world, txns_per_gpu=12000, keys_per_gpu=2000) for r in range(world)]
+    whole = _whole_from_shards(parts)
+    expect = pyoracle.resolve_sharded(whole, world)
+    g = synth.config3_global_dict(parts[0][0].params, [p[3] for p in parts])
+    Q = parts[0][2]
+    bases = exchange.owner_bases(Q, world)
+    stores, keep, tis, dfs, results = [], [], [], [], []
+    for w, idx, _, _ in parts:
+        st = native.DeviceCommandStore(0, 0, 1, w.slices)
+        st.load(w)
+        st.set_global_dict(g)
+        qdev, k = native.device_queries(w.queries, dev)
+        ti = torch.from_numpy(np.ascontiguousarray(idx, np.int64)).to(dev)
+        keep += [qdev, k, ti]
+        stores.append(st)
+        tis.append(ti.data_ptr())
+        dfs.append(np.searchsorted(idx, np.asarray(bases[:world], np.int64)).astype(np.uint64).tolist() + [len(idx)])
+        res, _ = st.deps_batch_device(qdev, None, parts_only=True)
+        results.append(res)
+    torch.cuda.synchronize()
+    merged, stats = native.exchange_local(stores, results, tis, dfs, bases[:world],
+                                          [bases[d + 1] - bases[d] for d in range(world)])
+    for d in range(world):
+        got = stores[d].merged_to_host(merged[d])
+        ok, why = got.equals(expect.window(bases[d], bases[d + 1] - bases[d]), detail=True)
+        assert ok, (d, why)
+    assert stats["bytes_moved"] > 0
+    for st in stores:
+        st.close()
