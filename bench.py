@@ -62,12 +62,15 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def measured_traffic(kernels):
+def measured_traffic(kernels, tag=None):
     """HBM bytes per launch summed over `kernels` from the newest committed PMC summary under
     profiles/ that has all of them (FETCH_SIZE doubled for gfx950 as MI355X_MICROARCH.md
-    prescribes, + WRITE_SIZE; scripts/summarize_prof.py), or (None, None)."""
+    prescribes, + WRITE_SIZE; scripts/summarize_prof.py), or (None, None). With `tag`, only
+    summaries whose name holds it (the profile of the same workload: "config2", "config3")."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))   # by name: rN_vM order (checkout mtimes are arbitrary)
+    if tag is not None:
+        files = [f for f in files if tag in os.path.basename(f)]
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
@@ -378,7 +381,7 @@ def bench_ranges(args, rank, world, local, dev):
     res_ms = float(sum(ms[i] for i in RESOLVE_STAGES))
     achieved = alg / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
     res_kernels = [kernel_of_stage(i, ranges=True) for i in RESOLVE_STAGES if ms[i] > 0.02]
-    traffic, src = measured_traffic(res_kernels)
+    traffic, src = measured_traffic(res_kernels, "config4")
     res = {
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
@@ -994,7 +997,7 @@ def bench_deps(args, rank, world, local, dev):
     achieved = sbytes[0] / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
     lean_rpw1 = 4 if w.queries.n_probes <= 3 * max(1, len(w.queries)) else 2
     res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1) for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
-    traffic, traffic_src = measured_traffic(res_kernels)
+    traffic, traffic_src = measured_traffic(res_kernels, "config%d" % cfg)
     if cfg == 3:
         workload = ("config3 (%d/8 of it on %d GPU%s): %d txns over %d uniform keys, %d-txn history x 4 keys, %d-request "
                     "probe batch, token-range sharded (EvenSplit), SNAPSHOT, 1 CommandStore per GPU%s" %

@@ -27,8 +27,13 @@ class RcResult(C.Structure):
                 ("k2t_off", A.P * 3), ("k2t", A.P * 3), ("scan_entries", C.c_uint64)]
 
 
-def build():
-    subprocess.check_call(["make", "-s", "-C", HERE])
+def build(target=None):
+    """make in oracle/, serialised across processes (pytest-xdist workers build concurrently)."""
+    import fcntl
+    os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
+    with open(os.path.join(HERE, "build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-C", HERE] + ([target] if target else []))
 
 
 _lib = None

@@ -107,6 +107,18 @@ typedef struct {
 
 static const info_t* cbe_at(const cfk_t* c, int i) { return &c->byId.v[c->cbe[i]]; }
 
+/* memcpy that accepts empty (possibly NULL) ranges */
+static void copy_n(void* dst, const void* src, size_t bytes)
+{
+    if (bytes) memcpy(dst, src, bytes);
+}
+
+/* qsort, skipping empty and single-element arrays (qsort's base must be non-NULL even for n == 0) */
+static void sort_n(void* base, size_t n, size_t size, int (*cmp)(const void*, const void*))
+{
+    if (n > 1) qsort(base, n, size, cmp);
+}
+
 static const cfk_t* g_sort_cfk;   /* qsort context for committedByExecuteAt */
 static int cmp_cbe(const void* a, const void* b)
 {
@@ -136,7 +148,7 @@ static void cfk_derive(cfk_t* c)
             c->cbe[c->ncbe++] = (int)i;
     }
     g_sort_cfk = c;
-    qsort(c->cbe, c->ncbe, sizeof(int), cmp_cbe);                      /* Arrays.sort(..., compareExecuteAt) */
+    sort_n(c->cbe, c->ncbe, sizeof(int), cmp_cbe);                      /* Arrays.sort(..., compareExecuteAt) */
     int maxAppliedByExecuteAt = c->ncbe;
     while (--maxAppliedByExecuteAt >= 0)
     {
@@ -299,7 +311,7 @@ static void stable_sort_tids(tid_t* a, size_t n)
             while (i < mid) tmp[k++] = a[i++];
             while (j < hi) tmp[k++] = a[j++];
         }
-        memcpy(a, tmp, n * sizeof(tid_t));
+        copy_n(a, tmp, n * sizeof(tid_t));
     }
     free(tmp);
     (void)cmp_tid_q;
@@ -381,7 +393,7 @@ static int builder_build(builder_t* b, rmm_t* out)
 
     int totalCount = b->totalCount, keyCount = b->keyCount;
     tid_t* uniqueValues = malloc(sizeof(tid_t) * totalCount);
-    memcpy(uniqueValues, b->keysToValues.v, sizeof(tid_t) * totalCount);
+    copy_n(uniqueValues, b->keysToValues.v, sizeof(tid_t) * totalCount);
     stable_sort_tids(uniqueValues, (size_t)totalCount);
     int valueCount = 1;
     for (int i = 1; i < totalCount; ++i)
@@ -394,14 +406,14 @@ static int builder_build(builder_t* b, rmm_t* out)
     rkey_t* sortedKeys = malloc(sizeof(rkey_t) * (keyCount ? keyCount : 1));
     if (b->hasOrderedKeys)
     {
-        memcpy(sortedKeys, b->keys.v, sizeof(rkey_t) * keyCount);
+        copy_n(sortedKeys, b->keys.v, sizeof(rkey_t) * keyCount);
     }
     else
     {
         sortedKeyIndexes = malloc(sizeof(int) * keyCount);
         for (int i = 0; i < keyCount; ++i) sortedKeyIndexes[i] = i;
         g_sort_keys = b->keys.v;
-        qsort(sortedKeyIndexes, keyCount, sizeof(int), cmp_key_idx);
+        sort_n(sortedKeyIndexes, keyCount, sizeof(int), cmp_key_idx);
         for (int i = 0; i < keyCount; ++i) sortedKeys[i] = b->keys.v[sortedKeyIndexes[i]];
         for (int i = 1; i < keyCount; ++i)
         {
@@ -518,8 +530,8 @@ int rc_store_create(const ad_config* cfg, rc_store** out)
     {
         s->slice_start = malloc(sizeof(int64_t) * s->n_slices);
         s->slice_end = malloc(sizeof(int64_t) * s->n_slices);
-        memcpy(s->slice_start, cfg->slice_start, sizeof(int64_t) * s->n_slices);
-        memcpy(s->slice_end, cfg->slice_end, sizeof(int64_t) * s->n_slices);
+        copy_n(s->slice_start, cfg->slice_start, sizeof(int64_t) * s->n_slices);
+        copy_n(s->slice_end, cfg->slice_end, sizeof(int64_t) * s->n_slices);
     }
     s->cfg.slice_start = s->slice_start;
     s->cfg.slice_end = s->slice_end;
@@ -655,8 +667,8 @@ int rc_range_cmds_load(rc_store* s, const ad_range_cmds_soa* in)
         else VEC_PUSH(s->cmds, c);
     }
     /* TreeMap<TxnId, ...> iteration order (InMemoryCommandStore.java:103-104) */
-    qsort(s->cmds.v, s->cmds.n, sizeof(rcmd_t), cmp_cmd);
-    qsort(s->hist.v, s->hist.n, sizeof(rcmd_t), cmp_cmd);
+    sort_n(s->cmds.v, s->cmds.n, sizeof(rcmd_t), cmp_cmd);
+    sort_n(s->hist.v, s->hist.n, sizeof(rcmd_t), cmp_cmd);
     for (size_t i = 1; i < s->cmds.n; ++i)
         if (tid_eq(&s->cmds.v[i - 1].txnId, &s->cmds.v[i].txnId)) return fail(s, AD_E_INVAL, "duplicate range command");
     for (size_t i = 1; i < s->hist.n; ++i)
@@ -962,7 +974,7 @@ static void result_append(rc_result* r, uint64_t qi, const pdeps_t* pd, size_t c
             r->txn_lsb[m][len[m][1] + t] = mm->values[t].lsb;
             r->txn_node[m][len[m][1] + t] = mm->values[t].node;
         }
-        memcpy(r->k2t[m] + len[m][2], mm->out, sizeof(int32_t) * mm->nout);
+        copy_n(r->k2t[m] + len[m][2], mm->out, sizeof(int32_t) * mm->nout);
         len[m][0] = nk; len[m][1] = nt; len[m][2] = no;
         r->keys_off[m][qi + 1] = nk;
         r->txn_off[m][qi + 1] = nt;
@@ -1031,7 +1043,7 @@ static void result_view(const rc_result* r, int m, uint64_t i, rmm_t* out)
         out->values[t].lsb = r->txn_lsb[m][t0 + t];
         out->values[t].node = r->txn_node[m][t0 + t];
     }
-    memcpy(out->out, r->k2t[m] + o0, sizeof(int32_t) * out->nout);
+    copy_n(out->out, r->k2t[m] + o0, sizeof(int32_t) * out->nout);
 }
 
 /* Combine the per-CommandStore results of the same requests the way CommandStores.mapReduce
@@ -1089,7 +1101,7 @@ int rc_result_merge(const rc_result* const* parts, int n_parts, rc_result** out)
                 r->txn_lsb[m][len[m][1] + t] = acc.values[t].lsb;
                 r->txn_node[m][len[m][1] + t] = acc.values[t].node;
             }
-            if (acc.nout) memcpy(r->k2t[m] + len[m][2], acc.out, sizeof(int32_t) * acc.nout);
+            if (acc.nout) copy_n(r->k2t[m] + len[m][2], acc.out, sizeof(int32_t) * acc.nout);
             len[m][0] = nk; len[m][1] = nt; len[m][2] = no;
             r->keys_off[m][i + 1] = nk;
             r->txn_off[m][i + 1] = nt;
@@ -1134,7 +1146,7 @@ int rc_levels(const ad_graph_soa* g, uint32_t* level)
     for (uint64_t i = 0; i < n; ++i)
         for (uint64_t k = g->key_off[i]; k < g->key_off[i + 1]; ++k)
             kv[k] = (kv_t){g->keys[k], {g->exec_msb[i], g->exec_lsb[i], g->exec_node[i]}, (uint32_t)i};
-    qsort(kv, nkv, sizeof(kv_t), cmp_kv);
+    sort_n(kv, nkv, sizeof(kv_t), cmp_kv);
     /* per (key, txn) position so each txn finds its predecessors on that key */
     uint64_t* pos_of = malloc(sizeof(uint64_t) * (nkv ? nkv : 1));   /* key-occurrence index -> position in kv */
     uint64_t* cursor = calloc(n + 1, sizeof(uint64_t));
@@ -1146,7 +1158,7 @@ int rc_levels(const ad_graph_soa* g, uint32_t* level)
     uint32_t* order = malloc(sizeof(uint32_t) * (n ? n : 1));
     for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
     g_graph = g;
-    qsort(order, n, sizeof(uint32_t), cmp_exec_idx);
+    sort_n(order, n, sizeof(uint32_t), cmp_exec_idx);
     for (uint64_t i = 1; i < n; ++i)
         if (cmp_exec_idx(&order[i - 1], &order[i]) == 0) { free(kv); free(pos_of); free(cursor); free(order); return AD_E_DUP_EXEC; }
     int rc = 0;
