@@ -222,6 +222,7 @@ struct ad_ctx {
     const uint64_t* last_t_reg = nullptr;
     uint64_t last_n = 0;
     bool last_parts_only = false;
+    DevBuf m_pinfo, m_heavy;
     DevBuf m_src, m_psz, m_poff, m_slot, m_dup, m_gsz, m_goff, m_bsum, m_err, m_bases;
     DevBuf m_ko, m_to, m_oo, m_keys, m_ids, m_k2t, m_u, m_ppre;
     DevBuf m_kdp, m_kuk, m_khead, m_pdp, m_ppos;   // ad_parts_union scratch
@@ -238,10 +239,15 @@ struct ad_ctx {
     // recovery scans (ad_recovery_batch*): entry ranks kept from the last snapshot build, device view
     std::vector<uint32_t> h_txn_rank, h_exec_rank, h_pruned;
     uint64_t rv_gen = ~0ull;                   // snap_gen the device view was built for
-    DevBuf rv_ent, rv_seg, rv_pruned, rv_miss, rv_blk;
-    uint64_t rv_nblk = 0;
+    DevBuf rv_ent, rv_seg, rv_pruned, rv_miss, rv_tree, rv_inv_off, rv_inv;
+    int rv_levels = 0;
+    std::vector<uint64_t> rv_lvl_at;
+    uint64_t rv_per_set = 0;
     // global dictionary of the multi-store exchange (ad_set_global_dict)
-    DevBuf g_msb, g_lsb, g_node, g_map, g_err;
+    // node-wide dictionary installed with ad_set_global_dict (host copy): the snapshot's dictionary
+    std::vector<uint64_t> gd_msb, gd_lsb;
+    std::vector<int32_t> gd_node;
+    bool gd_set = false, gd_strict = false;
     uint64_t n_global = 0;
     bool global_ok = false;
     // node exchange (ad_exchange / ad_exchange_local): library-owned part buffers, RCCL communicator
@@ -321,6 +327,16 @@ static int upload(ad_ctx* c, DevBuf& b, const std::vector<T>& v)
 
 static int sync_host(ad_ctx* c);
 
+// uninstall the node-wide dictionary (a new snapshot, or ids it does not hold)
+static void drop_global_dict(ad_ctx* c)
+{
+    c->gd_set = false;
+    c->global_ok = false;
+    std::vector<uint64_t>().swap(c->gd_msb);
+    std::vector<uint64_t>().swap(c->gd_lsb);
+    std::vector<int32_t>().swap(c->gd_node);
+}
+
 static int build_snapshot(ad_ctx* c)
 {
     if (int rc0 = sync_host(c)) return rc0;
@@ -369,7 +385,69 @@ static int build_snapshot(ad_ctx* c)
     c->dict_node.clear();
     std::vector<uint64_t> dhi, dlo;
     std::vector<int32_t> dnode;
-    for (size_t i = 0; i < recs.size(); ++i)
+    auto set_rank = [&](uint64_t s, uint32_t rank) {
+        if (s < ne) txn_rank[s] = rank;
+        else if (s < 2 * ne) exec_rank[s - ne] = rank;
+        else if (s < 2 * ne + ncmd) cmd_rank[s - 2 * ne] = rank;
+        else wm_rank[s - 2 * ne - ncmd] = rank;
+    };
+    bool use_global = c->gd_set;
+    if (use_global)
+    {
+        // the installed node-wide dictionary (ad_set_global_dict) is this store's dictionary: every
+        // rank is a global rank, so exported parts carry the kernels' own ids (no translation)
+        const uint64_t ng = c->gd_msb.size();
+        dhi.resize(ng);
+        dlo.resize(ng);
+        dnode.resize(ng);
+        parallel_for(ng, [&](size_t a, size_t b) {
+            for (size_t i = a; i < b; ++i)
+            {
+                const NormTid n = norm(Tid{c->gd_msb[i], c->gd_lsb[i], c->gd_node[i]});
+                dhi[i] = n.hi;
+                dlo[i] = n.lo;
+                dnode[i] = n.node;
+            }
+        });
+        uint64_t gi = 0;
+        for (size_t i = 0; i < recs.size() && use_global; ++i)
+        {
+            const DictRec& r = recs[i];
+            auto g_less = [&](uint64_t j) {
+                if (dhi[j] != r.hi) return dhi[j] < r.hi;
+                if (dlo[j] != r.lo) return dlo[j] < r.lo;
+                return dnode[j] < r.node;
+            };
+            while (gi < ng && g_less(gi)) ++gi;
+            if (gi == ng || dhi[gi] != r.hi || dlo[gi] != r.lo || dnode[gi] != r.node)
+            {
+                use_global = false;
+                break;
+            }
+            const Tid& t = src_tid(r.src);
+            if (t.lsb != c->gd_lsb[gi])
+                return c->fail(AD_E_INCONSISTENT_ID, "ids equal under Timestamp.equals differ in flag bits (lsb %llx vs %llx)",
+                               (unsigned long long)t.lsb, (unsigned long long)c->gd_lsb[gi]);
+            set_rank(r.src, (uint32_t)(2 * gi + 1));
+        }
+        if (use_global)
+        {
+            if (ng > MAX_DICT) return c->fail(AD_E_CAPACITY, "more than %llu distinct ids", (unsigned long long)MAX_DICT);
+            c->dict_msb = c->gd_msb;
+            c->dict_lsb = c->gd_lsb;
+            c->dict_node = c->gd_node;
+        }
+        else
+        {
+            if (c->gd_strict) return c->fail(AD_E_INVAL, "ad_set_global_dict: an id of this store's snapshot is missing");
+            // the snapshot outgrew the installed dictionary: uninstalled, the store's own dictionary instead
+            drop_global_dict(c);
+            dhi.clear();
+            dlo.clear();
+            dnode.clear();
+        }
+    }
+    for (size_t i = 0; i < recs.size() && !use_global; ++i)
     {
         const DictRec& r = recs[i];
         if (i == 0 || !rec_eq(recs[i - 1], r))
@@ -390,12 +468,7 @@ static int build_snapshot(ad_ctx* c)
                 return c->fail(AD_E_INCONSISTENT_ID, "ids equal under Timestamp.equals differ in flag bits (lsb %llx vs %llx)",
                                (unsigned long long)t.lsb, (unsigned long long)c->dict_lsb.back());
         }
-        const uint32_t rank = (uint32_t)(2 * (c->dict_msb.size() - 1) + 1);
-        const uint64_t s = r.src;
-        if (s < ne) txn_rank[s] = rank;
-        else if (s < 2 * ne) exec_rank[s - ne] = rank;
-        else if (s < 2 * ne + ncmd) cmd_rank[s - 2 * ne] = rank;
-        else wm_rank[s - 2 * ne - ncmd] = rank;
+        set_rank(r.src, (uint32_t)(2 * (c->dict_msb.size() - 1) + 1));
     }
     std::vector<DictRec>().swap(recs);
     for (uint64_t e = 0; e < ne; ++e)
@@ -859,7 +932,8 @@ static int build_snapshot(ad_ctx* c)
     c->h_pruned.swap(pruned);
     c->dirty = false;
     ++c->snap_gen;
-    c->global_ok = false;        // the dictionary changed: a global dictionary must be installed again
+    c->global_ok = use_global;   // parts carry global ranks exactly when the dictionary is the installed one
+    c->n_global = use_global ? c->dict_msb.size() : 0;
     c->ms_ingest = now_ms() - t0;
     return 0;
 }
@@ -1499,6 +1573,7 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     K.miss_stale = false;
     K.loaded = true;
     c->host_stale = false;       // the load replaces whatever ad_cfk_update applied on the device
+    drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
     c->dirty = true;
     return AD_OK;
 }
@@ -1518,6 +1593,7 @@ int ad_range_cmds_load(ad_ctx* c, const ad_range_cmds_soa* in)
     const uint64_t nr = n ? in->range_off[n] : 0;
     R.start.assign(in->range_start, in->range_start + nr);
     R.end.assign(in->range_end, in->range_end + nr);
+    drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
     c->dirty = true;
     return AD_OK;
 }
@@ -1533,6 +1609,7 @@ int ad_redundant_load(ad_ctx* c, const ad_redundant_soa* in)
     B.e1.assign(in->end_epoch, in->end_epoch + n);
     B.wm.resize(n);
     for (uint64_t i = 0; i < n; ++i) B.wm[i] = {in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
+    drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
     c->dirty = true;
     return AD_OK;
 }
@@ -1696,30 +1773,72 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
             }
             ent[e] = make_uint4(c->h_txn_rank[e], c->h_exec_rank[e], K.status[e] | (kind << 8) | (nm << RV_MISS_SHIFT), mo);
         }
-        // per 64-entry block and status set (ACCEPTED/COMMITTED, STABLE/APPLIED): the largest executeAt
-        // rank; every scan wants executeAt > testTxnId (:861-866), so blocks at or below it are skipped
-        const uint64_t nb = (ne + 63) / 64;
-        // and the range [min, max] of the blocks' missing() ids (min > max: none): a scan that wants
-        // entries missing a known testTxnId (WITHOUT, :868-872) skips blocks whose range misses it
-        std::vector<uint32_t> blk(4 * std::max<uint64_t>(nb, 1), 0);
-        for (uint64_t b = 0; b < nb; ++b) blk[2 * nb + b] = 0xFFFFFFFFu;
+        // per status set (ACCEPTED/COMMITTED, STABLE/APPLIED) a 64-ary max tree of the entries' executeAt
+        // ranks: every scan wants executeAt > testTxnId (:861-866), so a subtree at or below it is skipped
+        int nl = 1;
+        std::vector<uint64_t> lvl_n(1, ne);
+        while (lvl_n.back() > 1 && nl < MAX_LEVELS)
+        {
+            lvl_n.push_back((lvl_n.back() + 63) / 64);
+            ++nl;
+        }
+        if (nl < 2)
+        {
+            lvl_n.push_back(1);
+            nl = 2;
+        }
+        std::vector<uint64_t> lvl_at(nl + 1, 0);      // offset of level l (>= 1) in the per-set array
+        for (int l = 1; l < nl; ++l) lvl_at[l + 1] = lvl_at[l] + lvl_n[l];
+        const uint64_t per_set = lvl_at[nl];
+        std::vector<uint32_t> tree(2 * per_set, 0);
         for (uint64_t e = 0; e < ne; ++e)
         {
             const uint32_t st = K.status[e];
             const int set = (st == 3 || st == 4) ? 0 : (st == 5 || st == 6) ? 1 : -1;
-            if (set >= 0) blk[set * nb + e / 64] = std::max(blk[set * nb + e / 64], c->h_exec_rank[e]);
-            const uint32_t nm = ent[e].z >> RV_MISS_SHIFT;
-            if (nm)
+            if (set >= 0)
             {
-                blk[2 * nb + e / 64] = std::min(blk[2 * nb + e / 64], miss[ent[e].w]);
-                blk[3 * nb + e / 64] = std::max(blk[3 * nb + e / 64], miss[ent[e].w + nm - 1]);
+                uint32_t& x = tree[set * per_set + lvl_at[1] + e / 64];
+                x = std::max(x, c->h_exec_rank[e]);
             }
         }
+        for (int set = 0; set < 2; ++set)
+            for (int l = 2; l < nl; ++l)
+                for (uint64_t j = 0; j < lvl_n[l - 1]; ++j)
+                {
+                    uint32_t& x = tree[set * per_set + lvl_at[l] + j / 64];
+                    x = std::max(x, tree[set * per_set + lvl_at[l - 1] + j]);
+                }
+        // per key, the (missing() id, entry) pairs sorted: a WITHOUT scan of a known testTxnId wants
+        // exactly the entries whose missing() holds it (:868-872)
+        std::vector<uint64_t> inv_off(nk + 1, 0);
+        for (uint64_t k = 0; k < nk; ++k)
+        {
+            uint64_t cnt = 0;
+            for (uint64_t e = K.seg[k]; e < K.seg[k + 1]; ++e) cnt += ent[e].z >> RV_MISS_SHIFT;
+            inv_off[k + 1] = inv_off[k] + cnt;
+        }
+        std::vector<uint2> inv(inv_off[nk]);
+        parallel_for(nk, [&](size_t ka, size_t kb) {
+            for (size_t k = ka; k < kb; ++k)
+            {
+                uint64_t at = inv_off[k];
+                for (uint64_t e = K.seg[k]; e < K.seg[k + 1]; ++e)
+                {
+                    const uint32_t nm = ent[e].z >> RV_MISS_SHIFT;
+                    for (uint32_t j = 0; j < nm; ++j) inv[at++] = make_uint2(miss[ent[e].w + j], (uint32_t)e);
+                }
+                std::sort(inv.begin() + inv_off[k], inv.begin() + at,
+                          [](const uint2& x, const uint2& y) { return x.x < y.x || (x.x == y.x && x.y < y.y); });
+            }
+        });
         int rc;
         if ((rc = upload(c, c->rv_ent, ent)) || (rc = upload(c, c->rv_seg, seg)) || (rc = upload(c, c->rv_pruned, c->h_pruned)) ||
-            (rc = upload(c, c->rv_miss, miss)) || (rc = upload(c, c->rv_blk, blk)))
+            (rc = upload(c, c->rv_miss, miss)) || (rc = upload(c, c->rv_tree, tree)) || (rc = upload(c, c->rv_inv_off, inv_off)) ||
+            (rc = upload(c, c->rv_inv, inv)))
             return rc;
-        c->rv_nblk = nb;
+        c->rv_levels = nl;
+        c->rv_lvl_at.assign(lvl_at.begin(), lvl_at.end());
+        c->rv_per_set = per_set;
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->rv_gen = c->snap_gen;
     }
@@ -1727,8 +1846,13 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
     v->seg = c->rv_seg.as<uint32_t>();
     v->pruned = c->rv_pruned.as<uint32_t>();
     v->miss = c->rv_miss.as<uint32_t>();
-    v->blk_max = c->rv_blk.as<uint32_t>();
-    v->n_blk = c->rv_nblk;
+    for (int set = 0; set < 2; ++set)
+        for (int l = 0; l < MAX_LEVELS; ++l)
+            v->lvl[set][l] = (l >= 1 && l < c->rv_levels) ? c->rv_tree.as<uint32_t>() + set * c->rv_per_set + c->rv_lvl_at[l]
+                                                          : nullptr;
+    v->n_levels = c->rv_levels;
+    v->inv_off = c->rv_inv_off.as<uint64_t>();
+    v->inv = c->rv_inv.as<uint2>();
     return 0;
 }
 
@@ -1928,32 +2052,26 @@ int ad_set_global_dict(ad_ctx* c, uint64_t n, const uint64_t* msb, const uint64_
 {
     if (!c || (n && (!msb || !lsb || !node))) return AD_E_INVAL;
     if (n >= (1ull << 31)) return c->fail(AD_E_CAPACITY, "ad_set_global_dict: more than 2^31 ids");
-    int rc = ad_prepare(c);
-    if (rc) return rc;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     for (uint64_t i = 1; i < n; ++i)
         if (norm_cmp(norm_tid(msb[i - 1], lsb[i - 1], node[i - 1]), norm_tid(msb[i], lsb[i], node[i])) >= 0)
             return c->fail(AD_E_INVAL, "ad_set_global_dict: ids not ascending and unique at %llu", (unsigned long long)i);
-    hipStream_t st = c->stream;
-    const uint64_t nl = c->dict_msb.size();
-    if (!ens<uint64_t>(c->g_msb, n) || !ens<uint64_t>(c->g_lsb, n) || !ens<int32_t>(c->g_node, n) ||
-        !ens<uint32_t>(c->g_map, nl) || !ens<uint32_t>(c->g_err, 1))
-        return c->fail(AD_E_NOMEM, "global dictionary");
-    if (n)
+    // the snapshot is rebuilt over the node-wide dictionary (ingest work): its ranks become global
+    c->gd_msb.assign(msb, msb + n);
+    c->gd_lsb.assign(lsb, lsb + n);
+    c->gd_node.assign(node, node + n);
+    c->gd_set = true;
+    c->gd_strict = true;
+    c->dirty = true;
+    const int rc = build_snapshot(c);
+    c->gd_strict = false;
+    if (rc)
     {
-        HIPCHK(c, hipMemcpyAsync(c->g_msb.p, msb, 8 * n, hipMemcpyHostToDevice, st));
-        HIPCHK(c, hipMemcpyAsync(c->g_lsb.p, lsb, 8 * n, hipMemcpyHostToDevice, st));
-        HIPCHK(c, hipMemcpyAsync(c->g_node.p, node, 4 * n, hipMemcpyHostToDevice, st));
+        drop_global_dict(c);
+        c->dirty = true;
+        return rc;
     }
-    HIPCHK(c, hipMemsetAsync(c->g_err.p, 0, 4, st));
-    HIPCHK(c, run_global_map(c->d_dict_hi.as<uint64_t>(), c->d_dict_lo.as<uint64_t>(), c->d_dict_node.as<int32_t>(), nl,
-                             c->g_msb.as<uint64_t>(), c->g_lsb.as<uint64_t>(), c->g_node.as<int32_t>(), n,
-                             c->g_map.as<uint32_t>(), c->g_err.as<uint32_t>(), st));
-    uint32_t err = 0;
-    HIPCHK(c, hipMemcpyAsync(&err, c->g_err.p, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    if (err) return c->fail(AD_E_INVAL, "ad_set_global_dict: an id of this store's dictionary is missing");
-    c->n_global = n;
-    c->global_ok = true;
     return AD_OK;
 }
 
@@ -2001,7 +2119,7 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     if (out->id_format == AD_IDS_RANK && !c->global_ok)
         return c->fail(AD_E_STATE, "ad_parts_export: rank-format parts need a global dictionary covering this store's "
                                    "ids (ad_set_global_dict after the last snapshot load or dictionary append)");
-    a.gmap = out->id_format == AD_IDS_RANK ? c->g_map.as<uint32_t>() : nullptr;
+    a.rank_ids = out->id_format == AD_IDS_RANK;      // the dictionary is the global one: ids are global ranks
     a.sz = c->x_sz.as<uint32_t>();
     a.off = c->x_off.as<uint64_t>();
     HIPCHK(c, hipMemcpyAsync(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), hipMemcpyHostToDevice, st));
@@ -2045,9 +2163,13 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     const uint64_t P = in->n_parts, G = 3 * n_owned;
     const bool rank_ids = in->id_format == AD_IDS_RANK;
     if (in->id_format != AD_IDS_TRIPLET && !rank_ids) return c->fail(AD_E_INVAL, "ad_parts_merge: unknown id_format");
+    // rank-format merge of a node's stores: one 16-lane group per owned request (K3 fast path)
+    const bool by_request = rank_ids && !union_keys && n_src <= RM_MAX_SRC && in->n_key_words < (1ull << 32) &&
+                            in->n_ids < (1ull << 32) && in->n_k2t < (1ull << 32) && n_owned < (1ull << 30) &&
+                            in->n_parts < (1ull << 30);
     if (rank_ids && !c->global_ok)
         return c->fail(AD_E_INVAL, "ad_parts_merge: rank-format parts need ad_set_global_dict on this ctx");
-    if (rank_ids && (!ens<uint32_t>(c->m_u, in->n_ids) || !ens<uint32_t>(c->m_ppre, 2 * P)))
+    if (rank_ids && (!ens<uint32_t>(c->m_u, in->n_ids) || !ens<uint32_t>(c->m_ppre, 4 * std::max<uint64_t>(P, 1))))
         return c->fail(AD_E_NOMEM, "merge buffers");
     if (union_keys && (!ens<uint32_t>(c->m_kdp, in->n_key_words) || !ens<uint32_t>(c->m_kuk, in->n_key_words) ||
                        !ens<uint32_t>(c->m_khead, in->n_key_words) || !ens<uint32_t>(c->m_pdp, in->n_k2t) ||
@@ -2055,11 +2177,19 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
         return c->fail(AD_E_NOMEM, "union buffers");
     if (!ens<uint64_t>(c->m_src, n_src + 1) || !ens<uint32_t>(c->m_psz, 3 * P) || !ens<uint64_t>(c->m_poff, 3 * (P + 1)) ||
         !ens<int32_t>(c->m_slot, G * n_src) || !ens<uint32_t>(c->m_dup, in->n_ids) || !ens<uint32_t>(c->m_gsz, 3 * G) ||
-        !ens<uint64_t>(c->m_goff, 3 * (G + 1)) ||
+        !ens<uint64_t>(c->m_goff, 3 * (G + 1) + 9) ||
         !ens<uint64_t>(c->m_bsum, 3 * ((std::max(P, G) + 1023) / 1024) + 16) || !ens<uint32_t>(c->m_err, 1) ||
         !ens<uint64_t>(c->m_bases, 16) || !ens<uint64_t>(c->m_ko, 3 * (n_owned + 1)) ||
-        !ens<uint64_t>(c->m_to, 3 * (n_owned + 1)) || !ens<uint64_t>(c->m_oo, 3 * (n_owned + 1)))
+        !ens<uint64_t>(c->m_to, 3 * (n_owned + 1)) || !ens<uint64_t>(c->m_oo, 3 * (n_owned + 1)) ||
+        (by_request && (!ens<uint32_t>(c->m_pinfo, 8 * std::max<uint64_t>(P, 1)) ||
+                        !ens<uint32_t>(c->m_heavy, 3 * std::max<uint64_t>(n_owned, 1) + 1) ||
+                        !ens<uint64_t>(c->m_bsum, 9 * ((n_owned + 1023) / 1024) + 16))))
         return c->fail(AD_E_NOMEM, "merge buffers");
+    // a merged map is never larger than what it merges: the by-request path sizes its outputs by the
+    // received totals and needs no host round trip before the emit pass
+    if (by_request && (!ens<int64_t>(c->m_keys, in->n_key_words) || !ens<int64_t>(c->m_ids, (in->n_ids + 1) / 2) ||
+                       !ens<int32_t>(c->m_k2t, in->n_k2t)))
+        return c->fail(AD_E_NOMEM, "merge outputs");
     MergeArgs a{};
     a.n_parts = P;
     a.n_owned = n_owned;
@@ -2071,6 +2201,9 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     a.poff = c->m_poff.as<uint64_t>();
     a.slot = c->m_slot.as<int32_t>();
     a.dup = c->m_dup.as<uint32_t>();
+    a.pinfo = by_request ? c->m_pinfo.as<uint32_t>() : nullptr;
+    a.heavy = by_request ? c->m_heavy.as<uint32_t>() + 1 : nullptr;
+    a.n_heavy = by_request ? c->m_heavy.as<uint32_t>() : nullptr;
     a.gsz = c->m_gsz.as<uint32_t>();
     a.goff = c->m_goff.as<uint64_t>();
     a.error = c->m_err.as<uint32_t>();
@@ -2082,9 +2215,6 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
         a.u = c->m_u.as<uint32_t>();
         a.ppre = c->m_ppre.as<uint32_t>();
         a.n_global = c->n_global;
-        a.g_msb = c->g_msb.as<uint64_t>();
-        a.g_lsb = c->g_lsb.as<uint64_t>();
-        a.g_node = c->g_node.as<int32_t>();
     }
     if (union_keys)
     {
@@ -2094,39 +2224,57 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     HIPCHK(c, hipEventRecord(c->ev[6], st));
     HIPCHK(c, hipMemcpyAsync(c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemsetAsync(a.error, 0, sizeof(uint32_t), st));
-    HIPCHK(c, hipMemsetAsync(a.slot, 0xFF, sizeof(int32_t) * std::max<uint64_t>(G * n_src, 1), st));
+    HIPCHK(c, hipMemsetAsync(a.slot, 0xFF, sizeof(int32_t) * std::max<uint64_t>((by_request ? n_owned : G) * n_src, 1), st));
     HIPCHK(c, run_merge_prepare(a, st));
     HIPCHK(c, run_scan_arrays(a.psz, a.poff, P, 3, c->m_bsum.as<uint64_t>(), st));
-    HIPCHK(c, run_merge_slots(a, st));
-    HIPCHK(c, union_keys ? run_union_rank(a, st) : rank_ids ? run_merge_rank(a, st) : run_merge_count(a, st));
-    HIPCHK(c, run_scan_arrays(a.gsz, a.goff, G, 3, c->m_bsum.as<uint64_t>(), st));
-    HIPCHK(c, run_merge_bases(a, c->m_bases.as<uint64_t>(), st));
+    if (by_request)
+    {
+        HIPCHK(c, run_rmerge_slots(a, st));
+        HIPCHK(c, run_rmerge_size(a, st));
+        // per map and array: offsets of the owned requests' merged maps, each map from 0
+        HIPCHK(c, run_scan_arrays(a.gsz, a.goff, n_owned, 9, c->m_bsum.as<uint64_t>(), st));
+    }
+    else
+    {
+        HIPCHK(c, run_merge_slots(a, st));
+        HIPCHK(c, union_keys ? run_union_rank(a, st) : rank_ids ? run_merge_rank(a, st) : run_merge_count(a, st));
+        HIPCHK(c, run_scan_arrays(a.gsz, a.goff, G, 3, c->m_bsum.as<uint64_t>(), st));
+        HIPCHK(c, run_merge_bases(a, c->m_bases.as<uint64_t>(), st));
+    }
     uint64_t bases[12];
     uint32_t err = 0;
-    HIPCHK(c, hipMemcpyAsync(bases, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    if (err)
+    auto malformed = [&](uint32_t e) {
         return c->fail(AD_E_INVAL, "ad_parts_merge: malformed parts (%s)",
-                       err & 1  ? "request outside the owned range or bad map" :
-                       err & 2  ? "two parts of one request and map from one source" :
-                       err & 4  ? "keys of different stores overlap or are out of slice order" :
-                       err & 16 ? "id rank outside the global dictionary" :
-                                  "ids of a part not sorted and unique");
-    // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
-    if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, rank_ids ? (bases[10] + 1) / 2 : 3 * bases[10]) ||
-        !ens<int32_t>(c->m_k2t, bases[11]))
-        return c->fail(AD_E_NOMEM, "merge outputs");
+                       e & 1  ? "request outside the owned range or bad map" :
+                       e & 2  ? "two parts of one request and map from one source" :
+                       e & 4  ? "keys of different stores overlap or are out of slice order" :
+                       e & 16 ? "id rank outside the global dictionary" :
+                                "ids of a part not sorted and unique");
+    };
+    if (n_owned == 0 && !by_request)
+        for (DevBuf* b : {&c->m_ko, &c->m_to, &c->m_oo}) HIPCHK(c, hipMemsetAsync(b->p, 0, sizeof(uint64_t) * 3, st));
+    if (!by_request)
+    {
+        // outputs sized from the scanned group sizes (one round trip)
+        HIPCHK(c, hipMemcpyAsync(bases, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (err) return malformed(err);
+        // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
+        if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, rank_ids ? (bases[10] + 1) / 2 : 3 * bases[10]) ||
+            !ens<int32_t>(c->m_k2t, bases[11]))
+            return c->fail(AD_E_NOMEM, "merge outputs");
+    }
     a.o_keys = c->m_keys.as<int64_t>();
     a.o_ids = c->m_ids.as<int64_t>();
     a.o_k2t = c->m_k2t.as<int32_t>();
-    if (n_owned == 0)
-        for (DevBuf* b : {&c->m_ko, &c->m_to, &c->m_oo}) HIPCHK(c, hipMemsetAsync(b->p, 0, sizeof(uint64_t) * 3, st));
-    HIPCHK(c, union_keys ? run_union_emit(a, st) : rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
+    HIPCHK(c, by_request ? run_rmerge_copy(a, c->m_bases.as<uint64_t>(), st)
+                         : union_keys ? run_union_emit(a, st) : rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
     HIPCHK(c, hipEventRecord(c->ev[7], st));
+    if (by_request) HIPCHK(c, hipMemcpyAsync(bases, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    if (err) return c->fail(AD_E_INVAL, "ad_parts_merge: malformed parts (ids of a part not sorted and unique)");
+    if (err) return malformed(err);
     float ms = 0;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
     memset(out, 0, sizeof(*out));
@@ -2136,9 +2284,19 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     out->id_format = rank_ids ? AD_IDS_RANK : AD_IDS_TRIPLET;
     for (int m = 0; m < 3; ++m)
     {
-        out->keys_off[m] = a.o_keys_off + (uint64_t)m * (n_owned + 1);
-        out->txn_off[m] = a.o_txn_off + (uint64_t)m * (n_owned + 1);
-        out->k2t_off[m] = a.o_k2t_off + (uint64_t)m * (n_owned + 1);
+        if (by_request)
+        {
+            // the scan of the size pass is the merged CSR: [k*3 + m][n_owned + 1]
+            out->keys_off[m] = a.goff + (uint64_t)(0 * 3 + m) * (n_owned + 1);
+            out->txn_off[m] = a.goff + (uint64_t)(1 * 3 + m) * (n_owned + 1);
+            out->k2t_off[m] = a.goff + (uint64_t)(2 * 3 + m) * (n_owned + 1);
+        }
+        else
+        {
+            out->keys_off[m] = a.o_keys_off + (uint64_t)m * (n_owned + 1);
+            out->txn_off[m] = a.o_txn_off + (uint64_t)m * (n_owned + 1);
+            out->k2t_off[m] = a.o_k2t_off + (uint64_t)m * (n_owned + 1);
+        }
         out->keys[m] = a.o_keys + bases[3 * m + 0];
         out->txns[m] = rank_ids ? reinterpret_cast<int64_t*>(reinterpret_cast<uint32_t*>(a.o_ids) + bases[3 * m + 1])
                                 : a.o_ids + 3 * bases[3 * m + 1];
@@ -2365,7 +2523,7 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         HIPCHK(c, hipMemcpy(c->dict_msb.data() + nd0, c->d_dict_hi.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(c->dict_lsb.data() + nd0, c->d_dict_lsb_raw.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
         HIPCHK(c, hipMemcpy(c->dict_node.data() + nd0, c->d_dict_node.as<int32_t>() + nd0, 4 * add, hipMemcpyDeviceToHost));
-        c->global_ok = false;        // global ranks of the multi-store exchange no longer cover the dictionary
+        drop_global_dict(c);         // global ranks of the multi-store exchange no longer cover the dictionary
         // the sampled index over the grown dictionary (a stale one is still correct, only slower)
         const uint64_t ns = dict_samples(c->ds.n_dict);
         if (c->d_ds_hi.ensure(8 * ns + 8 * ns / 4) && c->d_ds_lo.ensure(8 * ns + 8 * ns / 4) && c->d_ds_node.ensure(4 * ns + 4 * ns / 4))

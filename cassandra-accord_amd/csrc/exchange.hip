@@ -86,76 +86,202 @@ __device__ __forceinline__ PartBase part_base(const ExportArgs& a, uint64_t r)
     return b;
 }
 
-// one 8-lane group per request, its three maps in turn
-__global__ void __launch_bounds__(64 * XWAVES) k_export_emit(ExportArgs a)
+// Load-balanced export: a block takes XT_REQ consecutive requests, lists their parts (non-empty
+// maps) in LDS with source and destination offsets, writes the headers, then streams the parts'
+// key words, ids and keysToTxnIds thread per element (binary search of the owning part in LDS).
+constexpr uint32_t XT_REQ = 128;                 // requests per block (threads)
+constexpr uint32_t XT_PARTS = 3 * XT_REQ;
+
+struct XtLds {
+    uint64_t ksrc[XT_PARTS], isrc[XT_PARTS], osrc[XT_PARTS];   // element offsets of the part's source
+    uint64_t kdst[XT_PARTS], idst[XT_PARTS], odst[XT_PARTS];   // and of its destination
+    uint32_t kpre[XT_PARTS + 1], ipre[XT_PARTS + 1], opre[XT_PARTS + 1];
+    uint32_t nk[XT_PARTS];
+    uint8_t map[XT_PARTS];
+    uint32_t cnt[XT_REQ / 64 + 1];
+    uint64_t wsum[3][XT_REQ / 64 + 1];
+};
+
+// exclusive scans of three per-thread values over the XT_REQ threads of the block
+__device__ __forceinline__ void xt_scan3(uint32_t v[3], uint32_t ex[3], uint32_t tot[3], uint64_t (*wsum)[XT_REQ / 64 + 1])
 {
-    const uint32_t g8 = threadIdx.x & 7;
-    const uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
-    if (r >= a.n) return;
-    PartBase pb = part_base(a, r);
+    const int l = lane_id(), w = threadIdx.x >> 6;
+    uint32_t inc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        inc[k] = v[k];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1)
+        {
+            const uint32_t t = __shfl_up(inc[k], d, 64);
+            if (l >= d) inc[k] += t;
+        }
+        if (l == 63) wsum[k][w] = inc[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        uint32_t before = 0, all = 0;
+        for (int j = 0; j < (int)(XT_REQ / 64); ++j)
+        {
+            const uint32_t x = (uint32_t)wsum[k][j];
+            if (j < w) before += x;
+            all += x;
+        }
+        ex[k] = inc[k] - v[k] + before;
+        tot[k] = all;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t xt_owner(const uint32_t* pre, uint32_t np, uint32_t e)
+{
+    uint32_t lo = 0, hi = np;
+    while (hi - lo > 1)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(XT_REQ) k_export_tiles(ExportArgs a)
+{
+    __shared__ XtLds L;
+    const uint32_t t = threadIdx.x;
+    const uint64_t r = (uint64_t)blockIdx.x * XT_REQ + t;
+    const bool live_r = r < a.n;
+    // this request's maps: sizes, source offsets, and its first part / key word / id / k2t in the output
+    uint32_t nk[3] = {0, 0, 0}, nt[3] = {0, 0, 0}, no[3] = {0, 0, 0};
+    uint64_t k0[3] = {0, 0, 0}, t0[3] = {0, 0, 0}, o0[3] = {0, 0, 0};
+    PartBase pb{0, 0, 0, 0};
+    if (live_r)
+    {
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+        {
+            k0[m] = a.keys_off[m][r];
+            nk[m] = (uint32_t)(a.keys_off[m][r + 1] - k0[m]);
+            t0[m] = a.txn_off[m][r];
+            nt[m] = (uint32_t)(a.txn_off[m][r + 1] - t0[m]);
+            o0[m] = a.k2t_off[m][r];
+            no[m] = (uint32_t)(a.k2t_off[m][r + 1] - o0[m]);
+        }
+        pb = part_base(a, r);
+    }
+    const uint32_t np_r = (nk[0] ? 1u : 0u) + (nk[1] ? 1u : 0u) + (nk[2] ? 1u : 0u);
+    uint32_t v3[3] = {np_r, 0, 0}, ex3[3], tot3[3];
+    xt_scan3(v3, ex3, tot3, L.wsum);
+    const uint32_t NP = tot3[0];
+    uint32_t j = ex3[0];
+    const int64_t tix = live_r ? a.txn_index[r] : 0;
+#pragma unroll
     for (int m = 0; m < 3; ++m)
     {
-        const uint64_t k0 = a.keys_off[m][r], nk = a.keys_off[m][r + 1] - k0;
-        if (nk == 0) continue;
-        const uint64_t t0 = a.txn_off[m][r], nt = a.txn_off[m][r + 1] - t0;
-        const uint64_t o0 = a.k2t_off[m][r], no = a.k2t_off[m][r + 1] - o0;
-        const uint64_t P = pb.P, KW = pb.KW, ID = pb.ID, KO = pb.KO;
-        // the request's map: packed arrays, or its region (keys, txnIds, keysToTxnIds back to back)
-        const int64_t* ikeys;
-        const uint32_t* itx;
-        const int32_t* ik2t;
+        if (!nk[m]) continue;
+        const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
+        // source: the batch's region of (request, map) (keys, txnIds, keysToTxnIds back to back), or
+        // the packed arrays; offsets in elements of each array
         if (a.reg)
         {
-            ikeys = reinterpret_cast<const int64_t*>(a.reg + a.t_reg[(uint64_t)m * a.n + r]);
-            itx = reinterpret_cast<const uint32_t*>(ikeys + nk);
-            ik2t = reinterpret_cast<const int32_t*>(itx + nt);
+            const uint64_t base = a.t_reg[(uint64_t)m * a.n + r];       // byte offset of the region
+            L.ksrc[j] = base;
+            L.isrc[j] = base + 8ull * nk[m];
+            L.osrc[j] = base + 8ull * nk[m] + 4ull * nt[m];
         }
         else
         {
-            ikeys = a.keys[m] + k0;
-            itx = a.txns[m] + t0;
-            ik2t = a.k2t[m] + o0;
+            L.ksrc[j] = k0[m];
+            L.isrc[j] = t0[m];
+            L.osrc[j] = o0[m];
         }
-        if (g8 == 0)
-        {
-            int64_t* h = a.hdr + 4 * P;
-            h[0] = (a.txn_index[r] << 2) | m;
-            h[1] = (int64_t)nk;
-            h[2] = (int64_t)nt;
-            h[3] = (int64_t)no;
-        }
-        if (m == AD_MAP_RANGE)
-        {
-            for (uint64_t j = g8; j < nk; j += 8)
-            {
-                const int64_t rid = ikeys[j];
-                a.okeys[KW + 2 * j] = a.rt_start[rid];
-                a.okeys[KW + 2 * j + 1] = a.rt_end[rid];
-            }
-        }
-        else
-        {
-            for (uint64_t j = g8; j < nk; j += 8) a.okeys[KW + j] = ikeys[j];
-        }
-        if (a.gmap)
-        {
-            uint32_t* o = reinterpret_cast<uint32_t*>(a.oids) + ID;
-            for (uint64_t j = g8; j < nt; j += 8) o[j] = a.gmap[itx[j]];
-        }
-        else
-            for (uint64_t j = g8; j < nt; j += 8)
-            {
-                const uint32_t d = itx[j];
-                int64_t* o = a.oids + 3 * (ID + j);
-                o[0] = (int64_t)a.dict_msb[d];
-                o[1] = (int64_t)a.dict_lsb[d];
-                o[2] = (int64_t)a.dict_node[d];
-            }
-        for (uint64_t j = g8; j < no; j += 8) a.ok2t[KO + j] = ik2t[j];
+        L.kdst[j] = pb.KW;
+        L.idst[j] = pb.ID;
+        L.odst[j] = pb.KO;
+        L.nk[j] = nk[m];
+        L.map[j] = (uint8_t)m;
+        int64_t* h = a.hdr + 4 * pb.P;
+        h[0] = (tix << 2) | m;
+        h[1] = (int64_t)nk[m];
+        h[2] = (int64_t)nt[m];
+        h[3] = (int64_t)no[m];
         pb.P += 1;
-        pb.KW += (m == AD_MAP_RANGE ? 2 : 1) * nk;
-        pb.ID += nt;
-        pb.KO += no;
+        pb.KW += w * nk[m];
+        pb.ID += nt[m];
+        pb.KO += no[m];
+        ++j;
+    }
+    // element prefixes over the block's parts (thread t owns its request's parts j .. j + np_r)
+    {
+        uint32_t kw = 0, ni = 0, nn = 0;
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+        {
+            kw += (m == AD_MAP_RANGE ? 2u : 1u) * nk[m];
+            ni += nt[m];
+            nn += no[m];
+        }
+        uint32_t v[3] = {kw, ni, nn}, ex[3], tot[3];
+        xt_scan3(v, ex, tot, L.wsum);
+        uint32_t jj = ex3[0];
+        uint32_t ek = ex[0], ei = ex[1], eo = ex[2];
+#pragma unroll
+        for (int m = 0; m < 3; ++m)
+        {
+            if (!nk[m]) continue;
+            L.kpre[jj] = ek;
+            L.ipre[jj] = ei;
+            L.opre[jj] = eo;
+            ek += (m == AD_MAP_RANGE ? 2u : 1u) * nk[m];
+            ei += nt[m];
+            eo += no[m];
+            ++jj;
+        }
+        if (t == 0)
+        {
+            L.kpre[NP] = tot[0];
+            L.ipre[NP] = tot[1];
+            L.opre[NP] = tot[2];
+        }
+    }
+    __syncthreads();
+    const uint32_t KT = L.kpre[NP], IT = L.ipre[NP], OT = L.opre[NP];
+    for (uint32_t e = t; e < KT; e += XT_REQ)
+    {
+        const uint32_t q = xt_owner(L.kpre, NP, e), i = e - L.kpre[q];
+        if (L.map[q] == AD_MAP_RANGE)
+        {
+            const uint32_t key = i >> 1;
+            const int64_t rid = a.reg ? reinterpret_cast<const int64_t*>(a.reg + L.ksrc[q])[key] : a.keys[AD_MAP_RANGE][L.ksrc[q] + key];
+            a.okeys[L.kdst[q] + i] = (i & 1) ? a.rt_end[rid] : a.rt_start[rid];
+        }
+        else
+        {
+            const int m = L.map[q];
+            a.okeys[L.kdst[q] + i] = a.reg ? reinterpret_cast<const int64_t*>(a.reg + L.ksrc[q])[i] : a.keys[m][L.ksrc[q] + i];
+        }
+    }
+    for (uint32_t e = t; e < IT; e += XT_REQ)
+    {
+        const uint32_t q = xt_owner(L.ipre, NP, e), i = e - L.ipre[q];
+        const uint32_t d = a.reg ? reinterpret_cast<const uint32_t*>(a.reg + L.isrc[q])[i] : a.txns[L.map[q]][L.isrc[q] + i];
+        if (a.rank_ids)
+            reinterpret_cast<uint32_t*>(a.oids)[L.idst[q] + i] = d;
+        else
+        {
+            int64_t* o = a.oids + 3 * (L.idst[q] + i);
+            o[0] = (int64_t)a.dict_msb[d];
+            o[1] = (int64_t)a.dict_lsb[d];
+            o[2] = (int64_t)a.dict_node[d];
+        }
+    }
+    for (uint32_t e = t; e < OT; e += XT_REQ)
+    {
+        const uint32_t q = xt_owner(L.opre, NP, e), i = e - L.opre[q];
+        a.ok2t[L.odst[q] + i] = a.reg ? reinterpret_cast<const int32_t*>(a.reg + L.osrc[q])[i] : a.k2t[L.map[q]][L.osrc[q] + i];
     }
 }
 
@@ -413,33 +539,14 @@ __global__ void __launch_bounds__(64 * XWAVES) k_merge_emit(MergeArgs a)
 }
 
 // ---------------------------------------------------------------------------------------
-// AD_IDS_RANK: parts carry uint32 ranks of one global dictionary, so the union of a group's id
-// lists is integer work. Pass 1 (wave per group): the union index u of every received id -- the
+// AD_IDS_RANK: parts carry uint32 ranks of one global dictionary (the dictionary every store's
+// snapshot was built over, ad_set_global_dict), so the union of a group's id lists is integer work. Pass 1 (wave per group): the union index u of every received id -- the
 // number of distinct ranks below it in the group -- and whether an earlier part already holds it
 // (Timestamp.equals), plus per part the key words and pairs of the earlier parts of its group.
 // Pass 2 (thread per part): keys concatenated in source order, union ids materialised from the
 // global dictionary at u, keysToTxnIds remapped through u (RelationMultiMap.linearUnion restated,
 // RelationMultiMap.java:561-816).
 // ---------------------------------------------------------------------------------------
-__global__ void k_global_map(const uint64_t* l_msb, const uint64_t* l_lo, const int32_t* l_node, uint64_t n_local,
-                             const uint64_t* g_msb, const uint64_t* g_lsb, const int32_t* g_node, uint64_t n_global,
-                             uint32_t* map, uint32_t* err)
-{
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_local) return;
-    const NormTid x{l_msb[i], l_lo[i], l_node[i]};
-    uint64_t lo = 0, hi = n_global;
-    while (lo < hi)
-    {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (norm_cmp(norm_tid(g_msb[mid], g_lsb[mid], g_node[mid]), x) < 0) lo = mid + 1;
-        else hi = mid;
-    }
-    const bool found = lo < n_global && norm_cmp(norm_tid(g_msb[lo], g_lsb[lo], g_node[lo]), x) == 0;
-    if (!found) atomicOr(err, 1u);
-    map[i] = found ? (uint32_t)lo : 0u;
-}
-
 __device__ __forceinline__ uint32_t lb_u32(const uint32_t* v, uint64_t base, uint32_t n, uint32_t x)
 {
     uint32_t lo = 0, hi = n;
@@ -659,6 +766,635 @@ __global__ void k_merge_emit_rank(MergeArgs a)
             continue;
         }
         a.o_k2t[KO + nkeys_total + prb + v] = (int32_t)(a.u[ibase + idx] & ~DUP_BIT);
+    }
+}
+
+constexpr uint32_t SCAN_WAVES_RC = 4;      // waves of a k_rmerge_copy block
+
+// exclusive scan over the RC_PARTS threads of a block; *total = the block's sum
+__device__ __forceinline__ uint64_t block_excl_scan_rc(uint64_t v, uint64_t* wsum, uint64_t* total)
+{
+    uint64_t inc = v;
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        const uint64_t tt = __shfl_up(inc, d, 64);
+        if (l >= d) inc += tt;
+    }
+    const int w = threadIdx.x >> 6;
+    if (l == 63) wsum[w] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+    for (int k = 0; k < (int)SCAN_WAVES_RC; ++k)
+    {
+        const uint64_t x = wsum[k];
+        if (k < w) before += x;
+        all += x;
+    }
+    *total = all;
+    __syncthreads();
+    return inc - v + before;
+}
+
+// ---------------------------------------------------------------------------------------
+// AD_IDS_RANK merge, G lanes per owned request (G = 8 for up to 8 sources, else 16; 64/G requests
+// per wave). A request's parts are found through slot[r][s] (its first part in source s; a source
+// sends a request's maps consecutively, ascending). Per map, the group's parts in source order are
+// staged in the sub-group's LDS; a group of at most 4G ids is merged in LDS: an id is a duplicate
+// when an earlier part holds it (binary search in the staged parts), and its union index is the
+// number of first occurrences below it. Larger groups keep the per-part dup prefix in global
+// memory and use the lower-bound formula of k_merge_rank. The size pass and the emit pass
+// recompute the same staging, so nothing per id travels between them except the large groups'
+// dup prefix. Offsets in the receive buffers are 32-bit (the host takes the per-group kernels
+// beyond that).
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t RM_WAVES = 4;                 // waves per block
+
+struct RmPart {
+    uint32_t kbase, ibase, obase;                // offsets in the receive buffers
+    uint32_t kw, ni, no, nk;                     // key words, ids, k2t ints, keys
+    uint32_t p;                                  // part index
+};
+
+template <uint32_t G>
+struct RmLds {
+    static constexpr uint32_t CAP = 4 * G;       // ids of a group merged in LDS
+    RmPart info[G];
+    uint32_t kst[G + 1], ist[G + 1], nst[G + 1], pst[G + 1];   // exclusive prefixes (+ total at np)
+    uint32_t id[CAP];
+    uint32_t u[CAP];                             // union index | DUP_BIT
+    uint8_t pe[CAP];                             // part of each staged id
+};
+
+template <uint32_t G>
+__device__ __forceinline__ uint64_t rm_ballot(bool p, uint32_t sub)
+{
+    if constexpr (G == 64) return ballot(p);
+    else return (ballot(p) >> (sub * G)) & ((1ull << G) - 1);
+}
+
+__device__ __forceinline__ uint32_t rm_part_of(const uint32_t* st, uint32_t np, uint32_t e)
+{
+    uint32_t q = 0;
+    for (uint32_t j = 1; j < np; ++j)
+        if (st[j] <= e) q = j;
+    return q;
+}
+
+// first i in [0, n) with !(v[i] < x), over LDS
+__device__ __forceinline__ uint32_t rm_lb_lds(const uint32_t* v, uint32_t n, uint32_t x)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (v[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// The parts of owned request r held by source lane sl: a source's parts of one request are
+// consecutive (k_rmerge_slots records the first), so the up to three records are loaded together
+// (one round trip after the slot). rm_part_for then picks map m's (compile-time m: no scratch).
+struct RmFound {
+    uint4 A[3], B[3];
+    bool ok[3];
+    uint32_t p0;                                 // part index of A[0]
+};
+
+__device__ __forceinline__ void rm_find_parts(const MergeArgs& a, uint64_t r, uint32_t sl, RmFound& f)
+{
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f.ok[k] = false;
+    if (sl >= a.n_src) return;
+    const int32_t v = a.slot[r * a.n_src + sl];
+    if (v == -1) return;
+    const uint32_t p0 = (uint32_t)v & 0x3FFFFFFFu, cnt = ((uint32_t)v >> 30) + 1;
+    const uint4* pi = reinterpret_cast<const uint4*>(a.pinfo);
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+    {
+        f.ok[k] = (uint32_t)k < cnt;
+        f.A[k] = f.ok[k] ? pi[2 * ((uint64_t)p0 + k)] : make_uint4(0, 0, 0, 0);
+        f.B[k] = f.ok[k] ? pi[2 * ((uint64_t)p0 + k) + 1] : make_uint4(0, 0, 0, 0xFFFFFFFFu);
+    }
+    f.p0 = p0;
+}
+
+__device__ __forceinline__ bool rm_part_for(const RmFound& f, int m, RmPart& q)
+{
+    bool has = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (f.ok[k] && (int)(f.B[k].w & 3) == m)
+        {
+            q = RmPart{f.A[k].x, f.A[k].y, f.A[k].z, f.B[k].x, f.B[k].y, f.B[k].z, f.A[k].w, f.p0 + (uint32_t)k};
+            has = true;
+        }
+    return has;
+}
+
+// Stage map m's parts of the request in source order; returns their number. Sets the prefix
+// arrays (kst: key words, ist: ids, nst: keys, pst: pairs; entry np = totals).
+template <uint32_t G>
+__device__ __forceinline__ uint32_t rm_stage(const MergeArgs& a, RmLds<G>& L, const RmPart& mine, bool has, uint32_t sub,
+                                             uint32_t sl, int m)
+{
+    const uint64_t live = rm_ballot<G>(has, sub);
+    const uint32_t np = __popcll(live);
+    if (np == 0) return 0;
+    if (has) L.info[__popcll(live & ((1ull << sl) - 1))] = mine;
+    wave_lds_sync();
+    if (sl < np || sl == 0)
+    {
+        // lane sl: the prefix of part sl; lane 0 also the totals (entry np)
+        const uint32_t upto = sl == 0 ? np : sl;
+        uint32_t k = 0, i = 0, n = 0, pr = 0;
+        for (uint32_t j = 0; j < upto; ++j)
+        {
+            k += L.info[j].kw;
+            i += L.info[j].ni;
+            n += L.info[j].nk;
+            pr += L.info[j].no - L.info[j].nk;
+        }
+        L.kst[upto] = k;
+        L.ist[upto] = i;
+        L.nst[upto] = n;
+        L.pst[upto] = pr;
+        if (sl == 0) L.kst[0] = L.ist[0] = L.nst[0] = L.pst[0] = 0;
+    }
+    if (sl > 0 && sl < np)
+    {
+        // keys of consecutive parts ascend (disjoint slices in source order)
+        const int w = m == AD_MAP_RANGE ? 2 : 1;
+        const RmPart& pp = L.info[sl - 1];
+        const RmPart& pj = L.info[sl];
+        const int64_t ls = a.keys[pp.kbase + pp.kw - w], le = w == 2 ? a.keys[pp.kbase + pp.kw - 1] : 0;
+        const int64_t fs = a.keys[pj.kbase], fe = w == 2 ? a.keys[pj.kbase + 1] : 0;
+        if (!keys_ordered(m, ls, le, fs, fe)) atomicOr(a.error, 4u);
+    }
+    wave_lds_sync();
+    return np;
+}
+
+// Ids of a group of T <= CAP into LDS, checked, with each id's dup bit (an earlier part holds it)
+// in L.u. Returns the number of dups.
+template <uint32_t G>
+__device__ __forceinline__ uint32_t rm_stage_ids(const MergeArgs& a, RmLds<G>& L, uint32_t np, uint32_t T, uint32_t sub,
+                                                 uint32_t sl)
+{
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    for (uint32_t e = sl; e < T; e += G)
+    {
+        const uint32_t q = rm_part_of(L.ist, np, e);
+        const uint32_t i = e - L.ist[q];
+        const uint32_t x = ids[L.info[q].ibase + i];
+        if (i > 0 && ids[L.info[q].ibase + i - 1] >= x) atomicOr(a.error, 8u);      // part not sorted / unique
+        if (x >= a.n_global) atomicOr(a.error, 16u);
+        L.id[e] = x;
+    }
+    wave_lds_sync();
+    uint32_t dups = 0;
+    for (uint32_t e0 = 0; e0 < T; e0 += G)
+    {
+        const uint32_t e = e0 + sl;
+        bool dup = false;
+        if (e < T)
+        {
+            const uint32_t q = rm_part_of(L.ist, np, e), x = L.id[e];
+            for (uint32_t q2 = 0; q2 < q && !dup; ++q2)
+            {
+                const uint32_t* v = L.id + L.ist[q2];
+                const uint32_t n = L.info[q2].ni;
+                const uint32_t b = rm_lb_lds(v, n, x);
+                dup = b < n && v[b] == x;
+            }
+            L.u[e] = dup ? DUP_BIT : 0u;
+        }
+        dups += __popcll(rm_ballot<G>(dup, sub));
+    }
+    wave_lds_sync();
+    return dups;
+}
+
+// Large group: per part, dup flags against the earlier parts with the exclusive dup prefix of the
+// part, in a.dup (global binary searches). Returns the number of dups.
+template <uint32_t G>
+__device__ __forceinline__ uint32_t rm_dups_global(const MergeArgs& a, RmLds<G>& L, uint32_t np, uint32_t sub, uint32_t sl)
+{
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    uint32_t total = 0;
+    for (uint32_t q = 0; q < np; ++q)
+    {
+        const RmPart pq = L.info[q];
+        uint32_t run = 0;
+        for (uint32_t e0 = 0; e0 < pq.ni; e0 += G)
+        {
+            const uint32_t e = e0 + sl;
+            bool dup = false;
+            if (e < pq.ni)
+            {
+                const uint32_t x = ids[pq.ibase + e];
+                if (e > 0 && ids[pq.ibase + e - 1] >= x) atomicOr(a.error, 8u);
+                if (x >= a.n_global) atomicOr(a.error, 16u);
+                for (uint32_t q2 = 0; q2 < q && !dup; ++q2)
+                {
+                    const uint32_t pos = lb_u32(ids, L.info[q2].ibase, L.info[q2].ni, x);
+                    dup = pos < L.info[q2].ni && ids[L.info[q2].ibase + pos] == x;
+                }
+            }
+            const uint64_t bm = rm_ballot<G>(dup, sub);
+            if (e < pq.ni) a.dup[pq.ibase + e] = (run + __popcll(bm & ((1ull << sl) - 1))) | (dup ? DUP_BIT : 0u);
+            run += __popcll(bm);
+        }
+        total += run;
+    }
+    return total;
+}
+
+// union index of id x (position pos_j in its own part j) of a large group (after rm_dups_global)
+template <uint32_t G>
+__device__ __forceinline__ uint32_t rm_union_global(const MergeArgs& a, const RmLds<G>& L, uint32_t np, uint32_t j,
+                                                    uint32_t pos_j, uint32_t x)
+{
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    uint32_t u = 0;
+    for (uint32_t q = 0; q < np; ++q)
+    {
+        const uint64_t qb = L.info[q].ibase;
+        const uint32_t qn = L.info[q].ni;
+        const uint32_t lb = q == j ? pos_j : lb_u32(ids, qb, qn, x);
+        uint32_t dp;
+        if (lb < qn) dp = a.dup[qb + lb] & ~DUP_BIT;
+        else
+        {
+            const uint32_t d = qn ? a.dup[qb + qn - 1] : 0u;
+            dp = qn ? (d & ~DUP_BIT) + (d >> 31) : 0u;
+        }
+        u += lb - dp;
+    }
+    return u;
+}
+
+__global__ void k_rmerge_slots(MergeArgs a)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.n_parts) return;
+    uint32_t s = 0;
+    while (s + 1 < a.n_src && a.src_first[s + 1] <= p) ++s;
+    const int64_t h0 = a.hdr[4 * p];
+    const int m = (int)(h0 & 3);
+    const int64_t t = h0 >> 2;
+    if (m > 2 || t < (int64_t)a.txn_base || t >= (int64_t)(a.txn_base + a.n_owned) || a.hdr[4 * p + 1] <= 0)
+    {
+        atomicOr(a.error, 1u);
+        reinterpret_cast<uint4*>(a.pinfo)[2 * p + 1] = make_uint4(0, 0, 0, 0xFFFFFFFFu);   // matches no request
+        return;
+    }
+    bool first = p == a.src_first[s];
+    if (!first)
+    {
+        const int64_t hp = a.hdr[4 * (p - 1)];
+        if (((hp >> 2) << 2 | (hp & 3)) >= ((t << 2) | m)) atomicOr(a.error, 2u);
+        first = (hp >> 2) != t;
+    }
+    const uint64_t rel = (uint64_t)(t - (int64_t)a.txn_base);
+    if (first)
+    {
+        // the request's parts in this source (consecutive, at most one per map): p | (count - 1) << 30
+        const uint64_t end = a.src_first[s + 1];
+        uint32_t cnt = 1;
+        if (p + 1 < end && (a.hdr[4 * (p + 1)] >> 2) == t)
+        {
+            cnt = 2;
+            if (p + 2 < end && (a.hdr[4 * (p + 2)] >> 2) == t) cnt = 3;
+        }
+        a.slot[rel * a.n_src + s] = (int32_t)((uint32_t)p | ((cnt - 1) << 30));
+    }
+    // the part's record for the merge passes: offsets in the receive buffers, sizes, request and map
+    const uint64_t P1 = a.n_parts + 1;
+    const uint64_t k0 = a.poff[0 * P1 + p], i0 = a.poff[1 * P1 + p], o0 = a.poff[2 * P1 + p];
+    uint4* pi = reinterpret_cast<uint4*>(a.pinfo);
+    pi[2 * p] = make_uint4((uint32_t)k0, (uint32_t)i0, (uint32_t)o0, (uint32_t)a.hdr[4 * p + 1]);
+    pi[2 * p + 1] = make_uint4((uint32_t)(a.poff[0 * P1 + p + 1] - k0), (uint32_t)(a.poff[1 * P1 + p + 1] - i0),
+                               (uint32_t)(a.poff[2 * P1 + p + 1] - o0), (uint32_t)(rel << 2) | (uint32_t)m);
+}
+
+// Pass 1, G lanes per owned request: per map the merged sizes (keys, union ids, k2t) into
+// gsz[k*3 + m][r], each part's place in its group (ppre[p] = {keys of the earlier parts, their
+// pairs, the group's keys, parts}), and for groups of several parts every received id's union index
+// (u[i] | DUP_BIT: an earlier part holds it).
+template <uint32_t G>
+__device__ __forceinline__ uint32_t sg_incl_scan(uint32_t v)
+{
+    const uint32_t sl = threadIdx.x % G;
+#pragma unroll
+    for (uint32_t d = 1; d < G; d <<= 1)
+    {
+        const uint32_t t = __shfl_up(v, d, G);
+        if (sl >= d) v += t;
+    }
+    return v;
+}
+
+template <uint32_t G>
+__device__ __forceinline__ uint32_t sg_sum(uint32_t v)
+{
+#pragma unroll
+    for (uint32_t d = G / 2; d >= 1; d >>= 1) v += __shfl_xor(v, d, G);
+    return v;
+}
+
+template <uint32_t G>
+__global__ void __launch_bounds__(64 * RM_WAVES) k_rmerge_size(MergeArgs a)
+{
+    __shared__ RmLds<G> s_l[RM_WAVES * (64 / G)];
+    const uint32_t sub = (threadIdx.x & 63) / G, sl = threadIdx.x % G;
+    RmLds<G>& L = s_l[threadIdx.x / G];
+    const uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    if (r >= a.n_owned || (*a.error & 3u)) return;     // malformed headers: nothing is read through them
+    const uint64_t n = a.n_owned;
+    const uint32_t* id = reinterpret_cast<const uint32_t*>(a.ids);
+    RmFound f;
+    rm_find_parts(a, r, sl, f);
+    uint4* ppre = reinterpret_cast<uint4*>(a.ppre);
+#pragma unroll 1
+    for (int m = 0; m < 3; ++m)
+    {
+        // lane sl = source sl: the group's parts are the lanes holding one, in lane (= source) order
+        RmPart q{};
+        const bool h = rm_part_for(f, m, q);
+        const uint32_t c_in = sg_incl_scan<G>(h ? 1u : 0u);
+        const uint32_t np = __shfl(c_in, (int)(G - 1), G);
+        uint32_t nk = 0, ids = 0, no = 0;
+        bool heavy = false;
+        if (np)
+        {
+            const uint32_t k_in = sg_incl_scan<G>(h ? q.nk : 0u), i_in = sg_incl_scan<G>(h ? q.ni : 0u);
+            const uint32_t p_in = sg_incl_scan<G>(h ? q.no - q.nk : 0u);
+            nk = __shfl(k_in, (int)(G - 1), G);
+            const uint32_t T = __shfl(i_in, (int)(G - 1), G), PT = __shfl(p_in, (int)(G - 1), G);
+            no = nk + PT;
+            const uint32_t j = c_in - 1, i0 = i_in - (h ? q.ni : 0u);
+            if (h) ppre[q.p] = make_uint4(k_in - q.nk, p_in - (q.no - q.nk), nk, np);
+            uint32_t dups = 0;     // one part: its ids are the union (checked by the copy pass)
+            heavy = np > 1 && T > RmLds<G>::CAP;
+            if (np > 1 && T <= RmLds<G>::CAP)
+            {
+                // stage the group's ids, element-parallel: part j's at [ist[j], ist[j] + ni)
+                wave_lds_sync();
+                if (h)
+                {
+                    L.ist[j] = i0;
+                    L.info[j].ni = q.ni;
+                    L.info[j].ibase = q.ibase;
+                }
+                if (sl == 0) L.ist[np] = T;
+                wave_lds_sync();
+                for (uint32_t e = sl; e < T; e += G)
+                {
+                    const uint32_t qq = rm_part_of(L.ist, np, e);
+                    const uint32_t x = id[L.info[qq].ibase + (e - L.ist[qq])];
+                    if (x >= a.n_global) atomicOr(a.error, 16u);
+                    L.id[e] = x;
+                    L.pe[e] = (uint8_t)qq;
+                }
+                wave_lds_sync();
+                // an id is a dup when an earlier part holds it (binary search in the staged parts)
+                for (uint32_t e0 = 0; e0 < T; e0 += G)
+                {
+                    const uint32_t e = e0 + sl;
+                    bool dup = false;
+                    if (e < T)
+                    {
+                        const uint32_t qq = L.pe[e], x = L.id[e];
+                        if (e > L.ist[qq] && L.id[e - 1] >= x) atomicOr(a.error, 8u);     // part not sorted / unique
+                        for (uint32_t q2 = 0; q2 < qq && !dup; ++q2)
+                        {
+                            const uint32_t* v = L.id + L.ist[q2];
+                            const uint32_t nn = L.info[q2].ni;
+                            const uint32_t b = rm_lb_lds(v, nn, x);
+                            dup = b < nn && v[b] == x;
+                        }
+                        L.u[e] = dup ? DUP_BIT : 0u;
+                    }
+                    dups += __popcll(rm_ballot<G>(dup, sub));
+                }
+                wave_lds_sync();
+                // union index: first occurrences below the id
+                for (uint32_t e = sl; e < T; e += G)
+                {
+                    const uint32_t x = L.id[e], qq = L.pe[e];
+                    uint32_t u = 0;
+                    for (uint32_t k = 0; k < T; ++k) u += (L.id[k] < x && !(L.u[k] & DUP_BIT)) ? 1u : 0u;
+                    a.u[L.info[qq].ibase + (e - L.ist[qq])] = u | (L.u[e] & DUP_BIT);
+                }
+            }
+            else if (np > 1 && sl == 0)
+            {
+                // more than CAP ids: k_rmerge_heavy sizes the union and places its ids
+                const uint32_t at = atomicAdd(a.n_heavy, 1u);
+                a.heavy[at] = (uint32_t)(r << 2) | (uint32_t)m;
+            }
+            if (np > 1)
+            {
+                // keys of consecutive parts ascend (disjoint slices in source order)
+                const int w = m == AD_MAP_RANGE ? 2 : 1;
+                const bool first = h && j == 0;
+                // the previous part's last key, from the nearest lower lane holding a part
+                const uint64_t holders = rm_ballot<G>(h, sub);
+                const int64_t last_s = h ? a.keys[q.kbase + q.kw - w] : 0, last_e = (h && w == 2) ? a.keys[q.kbase + q.kw - 1] : 0;
+                const uint64_t below = holders & ((1ull << sl) - 1);
+                const int src = (h && !first && below) ? 63 - __clzll(below) : -1;
+                const int64_t ps = __shfl(last_s, src < 0 ? (int)sl : src, G);
+                const int64_t pe = __shfl(last_e, src < 0 ? (int)sl : src, G);
+                if (h && !first)
+                {
+                    const int64_t fs = a.keys[q.kbase], fe = w == 2 ? a.keys[q.kbase + 1] : 0;
+                    if (!keys_ordered(m, ps, pe, fs, fe)) atomicOr(a.error, 4u);
+                }
+            }
+            ids = T - dups;
+        }
+        if (sl < 3 && !(sl == 1 && heavy))
+        {
+            const uint32_t v = sl == 0 ? nk : sl == 1 ? ids : no;
+            a.gsz[(uint64_t)(sl * 3 + m) * n + r] = v;
+        }
+    }
+}
+
+// Groups of more than CAP ids (listed by k_rmerge_size): one wave per group, the sources in its
+// lanes; dup prefix per part in global memory, union index of every id by lower bounds in the parts.
+__global__ void __launch_bounds__(64 * RM_WAVES) k_rmerge_heavy(MergeArgs a)
+{
+    __shared__ RmLds<64> s_l[RM_WAVES];
+    RmLds<64>& L = s_l[threadIdx.x >> 6];
+    if (*a.error & 3u) return;
+    const uint32_t sl = lane_id();
+    const uint32_t nh = *a.n_heavy;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint32_t* id = reinterpret_cast<const uint32_t*>(a.ids);
+    for (uint64_t k = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; k < nh; k += n_waves)
+    {
+        const uint32_t e0 = a.heavy[k];
+        const uint64_t r = e0 >> 2;
+        const int m = (int)(e0 & 3);
+        RmFound f;
+        rm_find_parts(a, r, sl, f);
+        RmPart q{};
+        const bool h = rm_part_for(f, m, q);
+        wave_lds_sync();
+        const uint32_t np = rm_stage<64>(a, L, q, h, 0, sl, m);
+        const uint32_t T = L.ist[np];
+        const uint32_t dups = rm_dups_global<64>(a, L, np, 0, sl);
+        __threadfence_block();
+        for (uint32_t e = sl; e < T; e += 64)
+        {
+            const uint32_t qq = rm_part_of(L.ist, np, e), i = e - L.ist[qq];
+            const uint64_t at = L.info[qq].ibase + i;
+            a.u[at] = rm_union_global<64>(a, L, np, qq, i, id[at]) | (a.dup[at] & DUP_BIT);
+        }
+        if (sl == 0) a.gsz[(uint64_t)(1 * 3 + m) * a.n_owned + r] = T - dups;
+    }
+}
+
+// bases[3*m + k]: offset of map m's first element in output array k (keys in words), m = 3: totals
+__global__ void k_rmerge_bases(MergeArgs a, uint64_t* out)
+{
+    if (threadIdx.x != 0) return;
+    const uint64_t n1 = a.n_owned + 1;
+    uint64_t acc[3] = {0, 0, 0};
+    for (int m = 0; m < 4; ++m)
+    {
+        for (int k = 0; k < 3; ++k) out[3 * m + k] = acc[k];
+        if (m == 3) break;
+        const uint64_t w = m == AD_MAP_RANGE ? 2 : 1;
+        acc[0] += w * a.goff[(uint64_t)(0 * 3 + m) * n1 + a.n_owned];
+        acc[1] += a.goff[(uint64_t)(1 * 3 + m) * n1 + a.n_owned];
+        acc[2] += a.goff[(uint64_t)(2 * 3 + m) * n1 + a.n_owned];
+    }
+}
+
+// Pass 2, load balanced over the receive buffers: a block takes 256 consecutive parts, places each
+// (its group's offsets + its place in the group), then streams their keys, ids and keysToTxnIds to
+// the merged arrays, thread per element (binary search of the owning part in LDS).
+constexpr uint32_t RC_PARTS = 256;
+
+struct RcLds {
+    uint32_t kbase[RC_PARTS], ibase[RC_PARTS], obase[RC_PARTS];
+    uint32_t ni[RC_PARTS], nk[RC_PARTS];
+    uint32_t kdst[RC_PARTS], idst[RC_PARTS], hdst[RC_PARTS], pdst[RC_PARTS];
+    int32_t add[RC_PARTS];                       // head adjustment: group keys + earlier pairs - own keys
+    uint32_t flags[RC_PARTS];                    // bit 0: one-part group (ids copied), bit 1: range map (2 words)
+    uint32_t kpre[RC_PARTS + 1], ipre[RC_PARTS + 1], opre[RC_PARTS + 1];
+    uint64_t wsum[SCAN_WAVES_RC + 1];
+};
+
+__device__ __forceinline__ uint32_t rc_owner(const uint32_t* pre, uint32_t np, uint32_t e)
+{
+    // last j with pre[j] <= e
+    uint32_t lo = 0, hi = np;
+    while (hi - lo > 1)
+    {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= e) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(RC_PARTS) k_rmerge_copy(MergeArgs a, const uint64_t* bases)
+{
+    __shared__ RcLds L;
+    if (*a.error & 3u) return;
+    const uint32_t t = threadIdx.x;
+    const uint64_t p0 = (uint64_t)blockIdx.x * RC_PARTS;
+    const uint32_t np = (uint32_t)min<uint64_t>(RC_PARTS, a.n_parts - p0);
+    const uint64_t n1 = a.n_owned + 1;
+    uint32_t kw = 0, ni = 0, no = 0;
+    if (t < np)
+    {
+        const uint64_t p = p0 + t;
+        const uint4* pi = reinterpret_cast<const uint4*>(a.pinfo);
+        const uint4 A = pi[2 * p], B = pi[2 * p + 1];
+        const uint4 pp = reinterpret_cast<const uint4*>(a.ppre)[p];
+        const uint32_t m = B.w & 3, r = B.w >> 2;
+        const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
+        const uint64_t K = a.goff[(uint64_t)(0 * 3 + m) * n1 + r], I = a.goff[(uint64_t)(1 * 3 + m) * n1 + r];
+        const uint64_t O = a.goff[(uint64_t)(2 * 3 + m) * n1 + r];
+        L.kbase[t] = A.x;
+        L.ibase[t] = A.y;
+        L.obase[t] = A.z;
+        L.nk[t] = A.w;
+        L.ni[t] = B.y;
+        L.kdst[t] = (uint32_t)(bases[3 * m + 0] + w * (K + pp.x));
+        L.idst[t] = (uint32_t)(bases[3 * m + 1] + I);
+        L.hdst[t] = (uint32_t)(bases[3 * m + 2] + O + pp.x);
+        L.pdst[t] = (uint32_t)(bases[3 * m + 2] + O + pp.z + pp.y);
+        L.add[t] = (int32_t)(pp.z + pp.y) - (int32_t)A.w;
+        L.flags[t] = (pp.w == 1 ? 1u : 0u) | (w == 2 ? 2u : 0u);
+        kw = B.x;
+        ni = B.y;
+        no = B.z;
+    }
+    // exclusive prefixes of the parts' element counts (one block scan each)
+    {
+        uint64_t tot;
+        uint64_t ex = block_excl_scan_rc(kw, L.wsum, &tot);
+        L.kpre[t] = (uint32_t)ex;
+        if (t == 0) L.kpre[RC_PARTS] = (uint32_t)tot;
+        ex = block_excl_scan_rc(ni, L.wsum, &tot);
+        L.ipre[t] = (uint32_t)ex;
+        if (t == 0) L.ipre[RC_PARTS] = (uint32_t)tot;
+        ex = block_excl_scan_rc(no, L.wsum, &tot);
+        L.opre[t] = (uint32_t)ex;
+        if (t == 0) L.opre[RC_PARTS] = (uint32_t)tot;
+    }
+    __syncthreads();
+    const uint32_t KT = L.kpre[RC_PARTS], IT = L.ipre[RC_PARTS], OT = L.opre[RC_PARTS];
+    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
+    uint32_t* o_ids = reinterpret_cast<uint32_t*>(a.o_ids);
+    for (uint32_t e = t; e < KT; e += RC_PARTS)
+    {
+        const uint32_t j = rc_owner(L.kpre, np, e), i = e - L.kpre[j];
+        a.o_keys[L.kdst[j] + i] = a.keys[L.kbase[j] + i];
+    }
+    for (uint32_t e = t; e < IT; e += RC_PARTS)
+    {
+        const uint32_t j = rc_owner(L.ipre, np, e), i = e - L.ipre[j];
+        const uint32_t at = L.ibase[j] + i, x = ids[at];
+        if (L.flags[j] & 1u)
+        {
+            if (i > 0 && ids[at - 1] >= x) atomicOr(a.error, 8u);      // part not sorted / unique
+            if (x >= a.n_global) atomicOr(a.error, 16u);
+            o_ids[L.idst[j] + i] = x;
+        }
+        else
+        {
+            const uint32_t uu = a.u[at];
+            if (!(uu & DUP_BIT)) o_ids[L.idst[j] + uu] = x;
+        }
+    }
+    for (uint32_t e = t; e < OT; e += RC_PARTS)
+    {
+        const uint32_t j = rc_owner(L.opre, np, e), i = e - L.opre[j];
+        const int32_t v = a.k2t[L.obase[j] + i];
+        const uint32_t nk = L.nk[j];
+        if (i < nk)
+        {
+            a.o_k2t[L.hdst[j] + i] = v + L.add[j];
+            continue;
+        }
+        const uint32_t idx = (uint32_t)v;
+        if (idx >= L.ni[j])
+        {
+            atomicOr(a.error, 8u);
+            continue;
+        }
+        a.o_k2t[L.pdst[j] + (i - nk)] = (L.flags[j] & 1u) ? (int32_t)idx : (int32_t)(a.u[L.ibase[j] + idx] & ~DUP_BIT);
     }
 }
 
@@ -1047,8 +1783,7 @@ hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st)
 hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
 {
     if (!a.n) return hipSuccess;
-    const uint64_t threads = a.n * 8;
-    k_export_emit<<<(unsigned)((threads + 64 * XWAVES - 1) / (64 * XWAVES)), 64 * XWAVES, 0, st>>>(a);
+    k_export_tiles<<<(unsigned)((a.n + XT_REQ - 1) / XT_REQ), XT_REQ, 0, st>>>(a);
     return hipGetLastError();
 }
 
@@ -1095,16 +1830,6 @@ hipError_t run_merge_emit(const MergeArgs& a, hipStream_t st)
     return hipGetLastError();
 }
 
-hipError_t run_global_map(const uint64_t* l_msb, const uint64_t* l_lo_norm, const int32_t* l_node, uint64_t n_local,
-                          const uint64_t* g_msb, const uint64_t* g_lsb, const int32_t* g_node, uint64_t n_global,
-                          uint32_t* map, uint32_t* err, hipStream_t st)
-{
-    if (!n_local) return hipSuccess;
-    k_global_map<<<(unsigned)((n_local + 255) / 256), 256, 0, st>>>(l_msb, l_lo_norm, l_node, n_local, g_msb, g_lsb,
-                                                                   g_node, n_global, map, err);
-    return hipGetLastError();
-}
-
 hipError_t run_merge_rank(const MergeArgs& a, hipStream_t st)
 {
     if (!a.n_owned) return hipSuccess;
@@ -1118,6 +1843,48 @@ hipError_t run_merge_emit_rank(const MergeArgs& a, hipStream_t st)
     k_merge_out_offsets<<<(unsigned)((n_off + 255) / 256), 256, 0, st>>>(a);
     const uint64_t threads = a.n_parts * EMIT_LANES;
     if (a.n_parts) k_merge_emit_rank<<<(unsigned)((threads + 255) / 256), 256, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_rmerge_slots(const MergeArgs& a, hipStream_t st)
+{
+    if (!a.n_parts) return hipSuccess;
+    k_rmerge_slots<<<(unsigned)((a.n_parts + 255) / 256), 256, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+template <template <uint32_t> class K>
+static hipError_t rm_launch(const MergeArgs& a, hipStream_t st)
+{
+    if (a.n_src > RM_MAX_SRC) return hipErrorInvalidValue;
+    if (!a.n_owned) return hipSuccess;
+    const uint32_t G = a.n_src <= 8 ? 8u : 16u;
+    const uint64_t threads = a.n_owned * G;
+    const unsigned blocks = (unsigned)((threads + 64 * RM_WAVES - 1) / (64 * RM_WAVES));
+    if (G == 8) K<8>::launch(blocks, a, st);
+    else K<16>::launch(blocks, a, st);
+    return hipGetLastError();
+}
+
+template <uint32_t G>
+struct RmSize {
+    static void launch(unsigned blocks, const MergeArgs& a, hipStream_t st) { k_rmerge_size<G><<<blocks, 64 * RM_WAVES, 0, st>>>(a); }
+};
+
+hipError_t run_rmerge_size(const MergeArgs& a, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(a.n_heavy, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    if ((e = rm_launch<RmSize>(a, st)) != hipSuccess) return e;
+    if (a.n_owned) k_rmerge_heavy<<<(unsigned)device_cu_count() * 2, 64 * RM_WAVES, 0, st>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t run_rmerge_copy(const MergeArgs& a, const uint64_t* bases, hipStream_t st)
+{
+    k_rmerge_bases<<<1, 64, 0, st>>>(a, const_cast<uint64_t*>(bases));
+    if (a.n_parts)
+        k_rmerge_copy<<<(unsigned)((a.n_parts + RC_PARTS - 1) / RC_PARTS), RC_PARTS, 0, st>>>(a, bases);
     return hipGetLastError();
 }
 

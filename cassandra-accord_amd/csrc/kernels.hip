@@ -1186,83 +1186,106 @@ hipError_t run_pack_lb(const BatchBufs& b, bool copy, hipStream_t st)
 }
 
 // ---------------------------------------------------------------------------------------
-// exclusive scans of the 9 size arrays -> u64 offsets [9][n+1]
+// exclusive scans of size arrays -> u64 offsets [n_arrays][n+1], reduce-then-scan: block sums of
+// the input, a parallel scan of the block sums (one block per array), then every block scans its
+// tile again with its offset (the input is read twice, the offsets written once)
 // ---------------------------------------------------------------------------------------
 constexpr int SCAN_BLOCK = 1024;
 
-__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_blocks(const uint32_t* __restrict__ sz, uint64_t n,
-                                                            uint64_t* __restrict__ off, uint64_t* __restrict__ bsum,
-                                                            uint64_t nb)
+// exclusive scan of v over the block (SCAN_BLOCK threads); *total = the block's sum
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* wsum /* [SCAN_BLOCK/64 + 1] */, uint64_t* total)
 {
-    __shared__ uint64_t wsum[SCAN_BLOCK / 64];
-    const int a = blockIdx.y;
-    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
-    const uint64_t v = i < n ? sz[(uint64_t)a * n + i] : 0;
-    // wave inclusive scan (u64)
     uint64_t inc = v;
     const int l = lane_id();
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1)
     {
-        uint64_t tt = __shfl_up(inc, d, 64);
+        const uint64_t tt = __shfl_up(inc, d, 64);
         if (l >= d) inc += tt;
     }
     const int w = threadIdx.x >> 6;
     if (l == 63) wsum[w] = inc;
     __syncthreads();
-    if (threadIdx.x < SCAN_BLOCK / 64)
+    if (threadIdx.x < 64)
     {
-        uint64_t x = wsum[threadIdx.x], sacc = x;
+        const uint64_t x = threadIdx.x < SCAN_BLOCK / 64 ? wsum[threadIdx.x] : 0;
+        uint64_t sacc = x;
+#pragma unroll
         for (int d = 1; d < SCAN_BLOCK / 64; d <<= 1)
         {
-            uint64_t tt = __shfl_up(sacc, d, 64);
-            if ((int)threadIdx.x >= d) sacc += tt;
+            const uint64_t tt = __shfl_up(sacc, d, 64);
+            if (l >= d) sacc += tt;
         }
-        wsum[threadIdx.x] = sacc - x;
+        if (threadIdx.x < SCAN_BLOCK / 64) wsum[threadIdx.x] = sacc - x;
+        if (threadIdx.x == SCAN_BLOCK / 64 - 1) wsum[SCAN_BLOCK / 64] = sacc;
     }
     __syncthreads();
-    if (i < n) off[(uint64_t)a * (n + 1) + i] = inc - v + wsum[w];
-    if (threadIdx.x == SCAN_BLOCK - 1) bsum[(uint64_t)a * nb + blockIdx.x] = inc + wsum[w];
+    const uint64_t r = inc - v + wsum[w];
+    *total = wsum[SCAN_BLOCK / 64];
+    __syncthreads();            // wsum is reused by the caller's next scan
+    return r;
 }
 
-__global__ void k_scan_sums(uint64_t* bsum, uint64_t nb, uint64_t* __restrict__ off, uint64_t n)
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t* __restrict__ sz, uint64_t n,
+                                                            uint64_t* __restrict__ bsum, uint64_t nb)
 {
-    // one wave per array: exclusive scan of block sums, total -> off[n]
-    const int a = blockIdx.x;
-    uint64_t carry = 0;
-    for (uint64_t i0 = 0; i0 < nb; i0 += 64)
-    {
-        const uint64_t i = i0 + lane_id();
-        const uint64_t v = i < nb ? bsum[(uint64_t)a * nb + i] : 0;
-        uint64_t inc = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1)
-        {
-            uint64_t tt = __shfl_up(inc, d, 64);
-            if ((int)lane_id() >= d) inc += tt;
-        }
-        if (i < nb) bsum[(uint64_t)a * nb + i] = carry + inc - v;
-        carry += __shfl(inc, 63, 64);
-    }
-    if (lane_id() == 0) off[(uint64_t)a * (n + 1) + n] = carry;
-}
-
-__global__ void k_scan_add(const uint64_t* __restrict__ bsum, uint64_t nb, uint64_t* __restrict__ off, uint64_t n)
-{
+    __shared__ uint64_t part[SCAN_BLOCK / 64];
     const int a = blockIdx.y;
     const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
-    if (i < n) off[(uint64_t)a * (n + 1) + i] += bsum[(uint64_t)a * nb + blockIdx.x];
+    uint64_t v = i < n ? sz[(uint64_t)a * n + i] : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        uint64_t t = 0;
+        for (int w = 0; w < SCAN_BLOCK / 64; ++w) t += part[w];
+        bsum[(uint64_t)a * nb + blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(uint64_t* bsum, uint64_t nb, uint64_t* __restrict__ off, uint64_t n)
+{
+    // one block per array: exclusive scan of its block sums in place, total -> off[n]
+    __shared__ uint64_t wsum[SCAN_BLOCK / 64 + 1];
+    const int a = blockIdx.x;
+    uint64_t carry = 0;
+    for (uint64_t i0 = 0; i0 < nb; i0 += SCAN_BLOCK)
+    {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint64_t v = i < nb ? bsum[(uint64_t)a * nb + i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_excl_scan(v, wsum, &tot);
+        if (i < nb) bsum[(uint64_t)a * nb + i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) off[(uint64_t)a * (n + 1) + n] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tile(const uint32_t* __restrict__ sz, uint64_t n,
+                                                          const uint64_t* __restrict__ bsum, uint64_t nb,
+                                                          uint64_t* __restrict__ off)
+{
+    __shared__ uint64_t wsum[SCAN_BLOCK / 64 + 1];
+    const int a = blockIdx.y;
+    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
+    const uint64_t v = i < n ? sz[(uint64_t)a * n + i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(v, wsum, &tot);
+    if (i < n) off[(uint64_t)a * (n + 1) + i] = bsum[(uint64_t)a * nb + blockIdx.x] + ex;
 }
 
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st)
 {
     // out[a][0..n] = exclusive prefix of in[a][0..n), out[a][n] = total, for a < n_arrays
+    // (bsum: n_arrays * ceil(n / 1024) entries)
     const uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
-    if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint64_t) * n_arrays, st);
+    if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint64_t) * n_arrays, st);    // out[a][0], a < n_arrays
     dim3 g((unsigned)nb, (unsigned)n_arrays);
-    k_scan_blocks<<<g, SCAN_BLOCK, 0, st>>>(in, n, out, bsum, nb);
-    k_scan_sums<<<n_arrays, 64, 0, st>>>(bsum, nb, out, n);
-    k_scan_add<<<g, SCAN_BLOCK, 0, st>>>(bsum, nb, out, n);
+    k_scan_reduce<<<g, SCAN_BLOCK, 0, st>>>(in, n, bsum, nb);
+    k_scan_sums<<<n_arrays, SCAN_BLOCK, 0, st>>>(bsum, nb, out, n);
+    k_scan_tile<<<g, SCAN_BLOCK, 0, st>>>(in, n, bsum, nb, out);
     return hipGetLastError();
 }
 
@@ -1403,11 +1426,15 @@ __global__ void k_encode_recover(DevSnapshot s, BatchBufs b)
 // scan: AD_RECOVER_* = (TestStartedAt, TestDep, TestStatus) of BeginRecovery.java:334,348,365,378:
 //   0 STARTED_BEFORE WITHOUT IS_PROPOSED, 1 STARTED_BEFORE WITH IS_STABLE,
 //   2 STARTED_AFTER WITHOUT IS_PROPOSED,  3 ANY WITHOUT IS_STABLE
-// MISS: prune blocks by the range of their missing() ids too (pays for scan 3, whose ANY range walks
-// whole segments; measured slower for the STARTED_BEFORE scan 0, so it is compiled out there)
-template <bool MISS>
-__global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, uint32_t scan)
+// Every scan wants executeAt > testTxnId (:861-866). The entries are found without walking the
+// probed range: a WITHOUT scan of a known testTxnId wants entries whose missing() holds it -- the
+// key's inverted missing() index (missing id, entry) lists exactly those; every other scan descends
+// the 64-ary max-executeAt tree of its status set over [start, end), so a wave touches only the
+// entries executing after testTxnId (plus a root-to-leaf path per 64-entry block it reports).
+__global__ __launch_bounds__(256) void k_recover(RecoveryView v, BatchBufs b, uint32_t scan)
 {
+    __shared__ uint32_t stage[K1_WAVES][K1_CAP];
+    __shared__ uint64_t stk[K1_WAVES][2 * MAX_LEVELS];
     const int wv = threadIdx.x >> 6;
     const uint32_t lane = lane_id();
     const uint64_t nw = (uint64_t)gridDim.x * K1_WAVES;
@@ -1415,6 +1442,7 @@ __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, 
     const unsigned long long cap = b.ctl->key_cap;
     const bool with = scan == 1;
     const bool proposed = scan == 0 || scan == 2;
+    const int set = proposed ? 0 : 1;
 
     for (uint64_t p = (uint64_t)blockIdx.x * K1_WAVES + wv; p < b.n_probes; p += nw)
     {
@@ -1441,7 +1469,7 @@ __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, 
         }
         // the loop body of :854-906 for entry i
         auto want_of = [&](uint64_t i, bool& is1, uint32_t& r) -> bool {
-            if (i >= end) return false;
+            if (i < start || i >= end) return false;
             const uint4 e = v.ent[i];
             r = e.x;
             const uint32_t st = e.z & 0xFF, kd = (e.z >> 8) & 7;
@@ -1466,43 +1494,83 @@ __global__ __launch_bounds__(256) void k_scan_full(RecoveryView v, BatchBufs b, 
             }
             return has_as_dep == with;
         };
-        // aligned 64-entry blocks; a block whose largest executeAt (in the scan's status set) is at
-        // or below testTxnId holds nothing the scan wants (executeAt > testTxnId, :861-866)
-        const uint32_t* bm = v.blk_max + (proposed ? 0 : v.n_blk);
-        const uint32_t* bmin = v.blk_max + 2 * v.n_blk;
-        const uint32_t* bmax = v.blk_max + 3 * v.n_blk;
-        const bool need_missing = MISS && known && !with;   // WITHOUT a known testTxnId: T must be in missing()
-        auto skip_blk = [&](uint64_t blk) {
-            return bm[blk] <= T || (need_missing && (bmin[blk] > T || bmax[blk] < T));
-        };
-        const uint64_t first = start & ~63ull;
-        uint32_t c0 = 0, c1 = 0;
-        for (uint64_t base = first; base < end; base += 64)
+        const bool by_missing = !with && known && end > start;
+        uint64_t ia = 0, ib = 0;
+        if (by_missing)
         {
-            if (skip_blk(base >> 6)) continue;
+            // the key's (missing id, entry) pairs naming testTxnId, entries ascending
+            const uint64_t a0 = v.inv_off[ki], a1 = v.inv_off[ki + 1];
+            ia = wave_lower_bound(a0, a1, [&](uint64_t i) { return v.inv[i].x; }, [&](uint32_t x) { return x < T; });
+            ib = wave_lower_bound(ia, a1, [&](uint64_t i) { return v.inv[i].x; }, [&](uint32_t x) { return x <= T; });
+        }
+        uint32_t cursor = 0, c0 = 0, c1 = 0;
+        bool overflow = false;
+        // one frame of 64 candidates (entry index per lane, or none): stage the wanted ones
+        auto frame_stage = [&](bool cand, uint64_t e) {
             bool is1 = false;
             uint32_t r = 0;
-            const bool want = base + lane >= start && want_of(base + lane, is1, r);
-            c0 += __popcll(ballot(want && !is1));
-            c1 += __popcll(ballot(want && is1));
-        }
+            const bool want = cand && want_of(e, is1, r);
+            const uint64_t wm = ballot(want), w1 = ballot(want && is1);
+            c0 += __popcll(wm & ~w1);
+            c1 += __popcll(w1);
+            const uint32_t n = __popcll(wm);
+            if (!overflow && cursor + n <= K1_CAP)
+            {
+                if (want) stage[wv][cursor + mbcnt(wm)] = r | (is1 ? CLASS_DIRECT_BIT : 0u);
+                cursor += n;
+            }
+            else overflow = true;
+        };
+        auto node_want = [&](int lv, uint64_t node) { return v.lvl[set][lv][node] > T; };
+        if (by_missing)
+            for (uint64_t base = ia; base < ib; base += 64)
+            {
+                const uint64_t i = base + lane;
+                frame_stage(i < ib, i < ib ? (uint64_t)v.inv[i].y : 0);
+            }
+        else if (end > start)
+            wave_descent(start, end, v.n_levels, node_want, [&](uint64_t base, bool inr) { frame_stage(inr, base + lane); },
+                         stk[wv]);
+        wave_lds_sync();
         const uint32_t tot = c0 + c1;
         const uint64_t off = tot ? alloc.take(&b.ctl->key_top, cap, &b.ctl->overflow, 1u, tot, K1_CHUNK) : 0;
         const bool fits = off + tot <= cap;
         if (fits && tot)
         {
             uint32_t run0 = 0, run1 = 0;
-            for (uint64_t base = first; base < end; base += 64)
-            {
-                if (skip_blk(base >> 6)) continue;
-                bool is1 = false;
-                uint32_t r = 0;
-                const bool want = base + lane >= start && want_of(base + lane, is1, r);
+            auto put = [&](bool want, uint32_t r, bool is1) {
                 const uint64_t w0 = ballot(want && !is1), w1 = ballot(want && is1);
                 if (want && !is1) b.arena[off + run0 + mbcnt(w0)] = r;       // keyDeps, byId (= rank) order
                 if (want && is1) b.arena[off + c0 + run1 + mbcnt(w1)] = r;   // directKeyDeps
                 run0 += __popcll(w0);
                 run1 += __popcll(w1);
+            };
+            if (!overflow)
+                for (uint32_t i0 = 0; i0 < cursor; i0 += 64)
+                {
+                    const uint32_t i = i0 + lane;
+                    const bool ok = i < cursor;
+                    const uint32_t x = ok ? stage[wv][i] : 0u;
+                    put(ok, x & ~CLASS_DIRECT_BIT, ok && (x & CLASS_DIRECT_BIT));
+                }
+            else
+            {
+                // staging overflowed: replay the walk writing straight to the exact allocation
+                auto frame_put = [&](bool cand, uint64_t e) {
+                    bool is1 = false;
+                    uint32_t r = 0;
+                    const bool want = cand && want_of(e, is1, r);
+                    put(want, r, is1);
+                };
+                if (by_missing)
+                    for (uint64_t base = ia; base < ib; base += 64)
+                    {
+                        const uint64_t i = base + lane;
+                        frame_put(i < ib, i < ib ? (uint64_t)v.inv[i].y : 0);
+                    }
+                else
+                    wave_descent(start, end, v.n_levels, node_want,
+                                 [&](uint64_t base, bool inr) { frame_put(inr, base + lane); }, stk[wv]);
             }
         }
         if (lane == 0)
@@ -1523,8 +1591,7 @@ hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const Batch
         k_probe_keys<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b);
         const uint64_t blocks_needed = (b.n_probes + K1_WAVES - 1) / K1_WAVES;
         const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
-        if (scan == 3) k_scan_full<true><<<grid, 256, 0, st>>>(v, b, scan);
-        else k_scan_full<false><<<grid, 256, 0, st>>>(v, b, scan);
+        k_recover<<<grid, 256, 0, st>>>(v, b, scan);
         // recovery scans of key-domain stores collect no range pairs (empty K4 lists)
         hipError_t e = hipMemsetAsync(b.p_rcnt, 0, sizeof(uint32_t) * b.n_probes, st);
         if (e == hipSuccess) e = hipMemsetAsync(b.p_rb, 0xFF, sizeof(uint64_t) * b.n_probes, st);

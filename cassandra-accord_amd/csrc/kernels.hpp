@@ -69,9 +69,14 @@ struct RecoveryView {
     const uint32_t* seg;     // [n_keys + 1] entry range of each key index
     const uint32_t* pruned;  // [n_keys] prunedBefore rank, 0 = none
     const uint32_t* miss;    // TxnInfo.missing() as ranks, ascending per entry
-    const uint32_t* blk_max; // [4][n_blk] per 64-entry block: max executeAt rank of {ACCEPTED, COMMITTED},
-                             // of {STABLE, APPLIED}; min and max missing() id (min > max: none)
-    uint64_t n_blk;
+    // 64-ary max trees over the entries (load order) of the executeAt ranks in each status set
+    // (0: ACCEPTED/COMMITTED, 1: STABLE/APPLIED; other entries 0): lvl[s][l][j] = max over entries
+    // [j * 64^l, (j + 1) * 64^l), l >= 1
+    const uint32_t* lvl[2][MAX_LEVELS];
+    int n_levels;            // including the entry level
+    // per key, its entries' (missing() id, entry) pairs sorted: [inv_off[k], inv_off[k + 1])
+    const uint64_t* inv_off;
+    const uint2* inv;
 };
 constexpr uint32_t RV_MISS_SHIFT = 12;
 constexpr uint32_t RV_MAX_MISS = (1u << 20) - 1;

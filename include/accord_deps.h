@@ -288,10 +288,13 @@ typedef struct ad_parts {
 
 /* Global TxnId dictionary of a multi-store node: the ascending, duplicate-free union (Timestamp
  * order) of the dictionaries (ad_dict) of every store taking part in the exchange, built once per
- * snapshot (ingest time, not batch time). Host arrays. Every id of this ctx's dictionary must occur
- * in it (AD_E_INVAL otherwise). While installed, ad_parts_export writes ids as uint32 global ranks
- * (AD_IDS_RANK: 4 bytes on the wire instead of 24) and ad_parts_merge merges integer ranks and
- * materialises the merged ids from this table; loading a new snapshot uninstalls it. */
+ * snapshot (ingest time, not batch time). Host arrays. The store's snapshot is (re)built over this
+ * dictionary: ad_dict then returns it and the txnIds of every result index into it, so the ids the
+ * kernels emit are node-wide ranks. Every id of the snapshot must occur in it (AD_E_INVAL otherwise,
+ * and the dictionary is not installed). Call it after the ad_*_load calls, before ad_prepare, to
+ * build the snapshot once. While installed, ad_parts_export writes ids as those uint32 ranks
+ * (AD_IDS_RANK: 4 bytes on the wire instead of 24, no translation) and ad_parts_merge merges
+ * integer ranks. Loading a new snapshot, or an ad_cfk_update that adds ids, uninstalls it. */
 int ad_set_global_dict(ad_ctx* ctx, uint64_t n, const uint64_t* msb, const uint64_t* lsb, const int32_t* node);
 
 /* Export the device result `res_dev` of the last ad_deps_batch_device on ctx as parts, into

@@ -125,6 +125,46 @@ def test_big_groups_rank_merge():
     _check(w, synth.shard_bounds(4), 2, rank_ids=True)
 
 
+def test_rank_merge_many_sources():
+    # more sources than the 16-lane per-request merge takes: the per-group rank merge
+    w = synth.config3(n_txns=12000, n_keys=3000, seed=9)
+    _check(w, synth.shard_bounds(18), 3, rank_ids=True)
+
+
+def test_global_dict_before_prepare():
+    # the snapshot built once over an installed node dictionary (bench config 3's ingest order)
+    w = synth.config3(n_txns=20000, n_keys=3000, seed=13)
+    lo, hi = synth.shard_bounds(2)
+    locs = [synth.shard_local(w, lo[g], hi[g]) for g in range(2)]
+    probe = []
+    for local, _ in locs:
+        st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, local.slices)
+        st.load(local)
+        probe.append(st.dictionary())
+        st.close()
+    g = exchange.build_global_dict(probe)
+    local, idx = locs[0]
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, local.slices)
+    st.load(local, prepare=False)
+    st.set_global_dict(g)
+    d = st.dictionary()
+    assert len(d.msb) == len(g.msb) and np.array_equal(d.msb, g.msb)
+    got = st.calculate_partial_deps(local.queries)
+    exp = pyoracle.resolve(local)
+    ok, why = got.equals(exp, detail=True)
+    assert ok, why
+    # a dictionary missing one of the store's ids is refused and leaves the store usable
+    st2 = native.DeviceCommandStore(0, w.range_start_inclusive, 1, local.slices)
+    st2.load(local, prepare=False)
+    with pytest.raises(native.AccordDepsError) as ei:
+        st2.set_global_dict(g.take(np.arange(1, len(g.msb))))
+    assert ei.value.code == A.AD_E_INVAL
+    ok, why = st2.calculate_partial_deps(local.queries).equals(exp, detail=True)
+    assert ok, why
+    st.close()
+    st2.close()
+
+
 def test_merge_rejects_overlapping_sources():
     dev = torch.device("cuda", 0)
     w = synth.config3(n_txns=4000, n_keys=500, seed=5)

@@ -70,3 +70,25 @@ def test_snapshot_key_index(oracle, seed):
         _check(q2, mc2, None, oracle, st=st)
     finally:
         st.close()
+
+
+def test_kat_witnessed_at_on_device(oracle):
+    # PreAcceptTest multiKeyTimestampUpdate (:210) through the device path: ad_preaccept_device's
+    # minNonConflicting + decision composed with the host node clock (accord_deps.clock)
+    import test_oracle as T
+    from accord_deps import _abi as A, clock
+    from accord_deps.model import make_txn_ids
+    t1 = make_txn_ids([1], [100], [A.KIND_WRITE], [2])
+    t2 = make_txn_ids([1], [50], [A.KIND_WRITE], [3])
+    clk = clock.NodeClock(1, 100, epoch=0)
+    clk.set_epoch(1)
+    clk.advance(10)
+    q = T._single_key_queries(t2, [[10, 11]])
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load_preaccept_maps(T._maxc_after([10], t1.tuples()[0]), None)
+        mn, fl, _ = st.preaccept(q, 1, 1)
+    finally:
+        st.close()
+    w = clk.witnessed_at_batch(t2, mn, fl)
+    assert w[0] == clock.make(1, 110, clock.flags_of(t2.tuples()[0]), 1)

@@ -76,6 +76,92 @@ def test_kat_superseding_epoch(oracle):
     assert _empty(st.deps_batch(_single_key_queries(t, [[10]]), A.AD_SEQUENTIAL))
 
 
+# witnessedAt of the same tests: rc_preaccept (the store's minNonConflicting + decision) composed
+# with the host node clock (accord_deps.clock, Node.uniqueNow). IntKey k routes as the range
+# (k - 1, k] (IntKey.asRange, end-inclusive), so a key's maxConflicts entry starts at k - 1.
+def _witnessed(oracle, clk, txns, keys, maxc, node_epoch):
+    q = _single_key_queries(txns, keys)
+    mn, fl = oracle.preaccept(maxc, None, q, 1, node_epoch)
+    return clk.witnessed_at_batch(txns, mn, fl), fl
+
+
+def _maxc_after(keys, ts):
+    from accord_deps.model import RangeMap, Tids
+    starts = []
+    for k in keys:
+        starts += [k - 1, k]
+    vals = Tids(np.array([ts[0]] * len(keys), np.uint64), np.array([ts[1]] * len(keys), np.uint64),
+                np.array([ts[2]] * len(keys), np.int32))
+    # one value per (k-1, k]; a gap (absent value) between non-adjacent keys
+    st, v, pres = [], [], []
+    for i, k in enumerate(keys):
+        if st and st[-1] == k - 1:
+            st.append(k)
+        else:
+            if st:
+                v.append(i - 1)
+                pres.append(0)
+            st += [k - 1, k]
+        v.append(i)
+        pres.append(1)
+    take = np.asarray(v, np.int64)
+    return RangeMap(np.asarray(st, np.int64), vals.take(take), np.asarray(pres, np.uint8), 1)
+
+
+def test_kat_witnessed_at_multi_key(oracle):
+    # multiKeyTimestampUpdate (:187-218): node ID1, clock 100; txn1 = idForNode(1, ID2) on key 10 takes
+    # the fast path; at clock 110, TxnId(1, 50, Write, Key, ID3) on {10, 11} is answered
+    # Timestamp.fromValues(1, 110, ID1).withExtraFlags(txnId2.flags()) (:210)
+    from accord_deps import clock
+    clk = clock.NodeClock(1, 100, epoch=0)
+    clk.set_epoch(1)
+    t1 = make_txn_ids([1], [100], [A.KIND_WRITE], [2])
+    w1, f1 = _witnessed(oracle, clk, t1, [[10]], None, 1)
+    assert f1[0] & clock.AD_PA_FAST and w1[0] == t1.tuples()[0]
+    clk.advance(10)
+    t2 = make_txn_ids([1], [50], [A.KIND_WRITE], [3])
+    w2, f2 = _witnessed(oracle, clk, t2, [[10, 11]], _maxc_after([10], t1.tuples()[0]), 1)
+    assert not f2[0] & clock.AD_PA_FAST
+    assert w2[0] == clock.make(1, 110, clock.flags_of(t2.tuples()[0]), 1)
+
+
+def test_kat_witnessed_at_superseding_epoch(oracle):
+    # supersedingEpochPrecludesFastPath (:251-291): topology at epoch 2; idForNode(1, ID2) at clock 100,
+    # processed at 110 -> Timestamp.fromValues(2, 110, ID1) (:284)
+    from accord_deps import clock
+    clk = clock.NodeClock(1, 100, epoch=0)
+    clk.set_epoch(1)
+    clk.set_epoch(2)
+    t = make_txn_ids([1], [100], [A.KIND_WRITE], [2])
+    clk.advance(10)
+    w, f = _witnessed(oracle, clk, t, [[10]], None, 2)
+    assert not f[0] & clock.AD_PA_FAST
+    assert w[0] == clock.make(2, 110, 0, 1)
+
+
+def test_kat_witnessed_at_fast_paths(oracle):
+    # initialCommandTest (:115) and singleKeyNewerTimestamp (:242): PreAcceptOk(txnId, txnId, ...)
+    from accord_deps import clock
+    for hlc in (100, 110):
+        clk = clock.NodeClock(1, 100, epoch=0)
+        clk.set_epoch(1)
+        t = make_txn_ids([1], [hlc], [A.KIND_WRITE], [2])
+        w, f = _witnessed(oracle, clk, t, [[10]], None, 1)
+        assert f[0] & clock.AD_PA_FAST and w[0] == t.tuples()[0]
+
+
+def test_node_clock_unique_and_rejected():
+    # uniqueNow is strictly increasing; a rejected answer carries REJECTED_FLAG (Timestamp.asRejected)
+    from accord_deps import clock
+    clk = clock.NodeClock(7, 1000, epoch=3)
+    a = clk.unique_now()
+    b = clk.unique_now()
+    assert clock.compare(a, b) < 0 and clock.hlc_of(a) == 1001 and clock.hlc_of(b) == 1002
+    t = clock.make(3, 5000, 2, 9)
+    r = clk.witnessed_at(t, (0, 0, 0), clock.AD_PA_REJECTED)
+    assert r[1] & clock.REJECTED_FLAG and clock.hlc_of(r) == 5001 and r[2] == 7
+
+
 def test_derived_write_after_write(oracle):
     # derived from the code (not a reference KAT): a later write on the same key depends on the
     # earlier PREACCEPTED write (never elided), a later read too (Ws), a later read on another key not
