@@ -77,6 +77,14 @@ class AdRangeCmdsSoa(C.Structure):
                 ("erased", P), ("historical", P), ("range_off", P), ("range_start", P), ("range_end", P)]
 
 
+AD_RS_PROPOSED, AD_RS_STABLE = 1, 2
+
+
+class AdRangeCmdsRecoverySoa(C.Structure):
+    _fields_ = [("n_cmds", C.c_uint64), ("status", P), ("has_deps", P), ("exec_msb", P), ("exec_lsb", P),
+                ("exec_node", P), ("dep_off", P), ("dep_msb", P), ("dep_lsb", P), ("dep_node", P)]
+
+
 class AdRedundantSoa(C.Structure):
     _fields_ = [("n", C.c_uint64), ("range_start", P), ("range_end", P), ("start_epoch", P), ("end_epoch", P),
                 ("wm_msb", P), ("wm_lsb", P), ("wm_node", P)]

@@ -168,6 +168,13 @@ class RangeCommands:
     range_end: np.ndarray
     erased: Optional[np.ndarray] = None
     historical: Optional[np.ndarray] = None
+    # recovery facts (ad_range_cmds_recovery_soa): AD_RS_* status class, deps known, executeAtOrTxnId,
+    # and per command the ids t with partialDeps().intersects(t, its ranges), ascending
+    rec_status: Optional[np.ndarray] = None
+    rec_has_deps: Optional[np.ndarray] = None
+    rec_exec: Optional[Tids] = None
+    rec_dep_off: Optional[np.ndarray] = None
+    rec_deps: Optional[Tids] = None
 
     def __post_init__(self):
         self.range_off = A.as_u64(self.range_off)
@@ -177,6 +184,22 @@ class RangeCommands:
             self.erased = A.as_u8(self.erased)
         if self.historical is not None:
             self.historical = A.as_u8(self.historical)
+        if self.rec_status is not None:
+            self.rec_status = A.as_u8(self.rec_status)
+            self.rec_has_deps = A.as_u8(self.rec_has_deps)
+            self.rec_dep_off = A.as_u64(self.rec_dep_off)
+
+    def recovery_soa(self):
+        """AdRangeCmdsRecoverySoa of the recovery facts, or None when there are none."""
+        if self.rec_status is None:
+            return None
+        s = A.AdRangeCmdsRecoverySoa()
+        s.n_cmds = len(self.txn)
+        s.status, s.has_deps = A.ptr(self.rec_status), A.ptr(self.rec_has_deps)
+        s.exec_msb, s.exec_lsb, s.exec_node = A.ptr(self.rec_exec.msb), A.ptr(self.rec_exec.lsb), A.ptr(self.rec_exec.node)
+        s.dep_off = A.ptr(self.rec_dep_off)
+        s.dep_msb, s.dep_lsb, s.dep_node = A.ptr(self.rec_deps.msb), A.ptr(self.rec_deps.lsb), A.ptr(self.rec_deps.node)
+        return s
 
     def soa(self):
         s = A.AdRangeCmdsSoa()

@@ -22,7 +22,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_range_cmds_load", "ad_redundant_load", "ad_prepare", "ad_deps_batch", "ad_result_free",
            "ad_deps_batch_device", "ad_dict", "ad_range_table", "ad_parts_export", "ad_parts_merge",
            "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict", "ad_preaccept_maps_load",
-           "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_recovery_batch",
+           "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_range_cmds_recovery_load", "ad_recovery_batch",
            "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange")
 
@@ -80,6 +80,7 @@ def lib():
         L.ad_levels_device.argtypes = [C.c_void_p, C.POINTER(A.AdGraphSoa), C.c_void_p, C.c_void_p,
                                        C.POINTER(A.AdStats)]
         L.ad_cfk_missing_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkMissingSoa)]
+        L.ad_range_cmds_recovery_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsRecoverySoa)]
         L.ad_recovery_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32,
                                         C.POINTER(C.POINTER(A.AdDepsResult))]
         L.ad_recovery_batch_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_void_p,
@@ -192,6 +193,9 @@ class DeviceCommandStore:
         ms = workload.cfk.missing_soa()
         if ms is not None:
             self._check(L.ad_cfk_missing_load(self.h, C.byref(ms)))
+        rs = workload.cmds.recovery_soa()
+        if rs is not None:
+            self._check(L.ad_range_cmds_recovery_load(self.h, C.byref(rs)))
         if prepare:
             self._check(L.ad_prepare(self.h))
         return self

@@ -934,8 +934,62 @@ def recovery_workload(seed, n_known=40, **kw):
     cfk = CfkSnapshot(cfk.keys, cfk.seg, cfk.txn, Tids(cfk.exec.msb, cfk.exec.lsb + bump, cfk.exec.node), cfk.status,
                       cfk.pruned_before)
     w.cfk = with_missing(cfk, seed, extra=q.txn)
+    w.cmds = with_range_recovery(w.cmds, seed, pool=txn)
     w.name = "recovery_small"
     return w
+
+
+def with_range_recovery(cmds, seed, pool):
+    """Recovery facts for every range command (ad_range_cmds_recovery_soa): a status class (proposed,
+    stable or neither), deps known or not, executeAtOrTxnId at or up to 4000 hlc ticks past the txnId,
+    and a deps id list drawn from `pool` (the recovering ids the scans test) -- so WITH and WITHOUT,
+    both status classes and executeAt on either side of a recovering txnId all occur."""
+    n = len(cmds.txn)
+    rng = np.random.default_rng(seed ^ 0xDE95)
+    # range-command txnIds spread over the pool's hlc span, so that commands start before and after
+    # the recovering txns
+    if n and len(pool):
+        hlc_of = (pool.msb.astype(np.uint64) & np.uint64(0x7FFF)) << np.uint64(48) | (pool.lsb >> np.uint64(16))
+        lo_h, hi_h = int(hlc_of.min()), int(hlc_of.max())
+        h = np.sort(rng.choice(np.arange(max(1, lo_h - 50), hi_h + 50), n, replace=False)).astype(np.uint64)
+        kinds = ((cmds.txn.lsb >> np.uint64(1)) & np.uint64(7)).astype(np.uint8)
+        epochs = (pool.msb >> np.uint64(15))[rng.integers(0, len(pool), n)]
+        cmds = RangeCommands(make_txn_ids(epochs, h, kinds, cmds.txn.node, domain=1), cmds.range_off,
+                             cmds.range_start, cmds.range_end, cmds.erased, cmds.historical)
+    status = rng.choice([0, A.AD_RS_PROPOSED, A.AD_RS_STABLE], n, p=[0.2, 0.4, 0.4]).astype(np.uint8)
+    has_deps = (rng.random(n) < 0.85).astype(np.uint8)
+    bump = (rng.integers(0, 4000, n).astype(np.uint64) << np.uint64(16)) * (rng.random(n) < 0.8)
+    up = (rng.random(n) < 0.3).astype(np.uint64) << np.uint64(15)          # a later epoch now and then
+    ex = Tids(cmds.txn.msb + up, cmds.txn.lsb + bump.astype(np.uint64), cmds.txn.node.copy())
+    off = [0]
+    parts = []
+    npool = len(pool)
+    for i in range(n):
+        pick = np.nonzero(rng.random(npool) < 0.2)[0] if npool else np.zeros(0, np.int64)
+        k = len(pick)
+        t = pool.take(np.asarray(pick, np.int64))
+        o = np.lexsort((t.node, t.lsb, t.msb)) if k else np.zeros(0, np.int64)
+        t = t.take(o)
+        # ascending and unique under Timestamp order (msb, lsb >> 16 ... as the oracle compares)
+        keep = []
+        for j in range(len(t.msb)):
+            cur = (int(t.msb[j]), int(t.lsb[j]), int(t.node[j]))
+            if keep and _tid_key(keep[-1]) >= _tid_key(cur):
+                continue
+            keep.append(cur)
+        parts.append(keep)
+        off.append(off[-1] + len(keep))
+    flat = [x for p in parts for x in p]
+    deps = Tids(np.array([x[0] for x in flat], np.uint64), np.array([x[1] for x in flat], np.uint64),
+                np.array([x[2] for x in flat], np.int32))
+    return RangeCommands(cmds.txn, cmds.range_off, cmds.range_start, cmds.range_end, cmds.erased, cmds.historical,
+                         rec_status=status, rec_has_deps=has_deps, rec_exec=ex, rec_dep_off=np.array(off, np.uint64),
+                         rec_deps=deps)
+
+
+def _tid_key(t):
+    """Timestamp.compareTo order of an (msb, lsb, node) triple (Timestamp.java:209-217)."""
+    return (t[0], t[1] >> 16, t[1] & 0x1E, t[2])
 
 
 def with_missing_fast(cfk, seed, frac=0.2, back=8):

@@ -174,7 +174,16 @@ struct ad_ctx {
         std::vector<uint8_t> erased, historical;
         std::vector<uint64_t> off;
         std::vector<int64_t> start, end;
+        // recovery facts (ad_range_cmds_recovery_load)
+        bool rec = false;
+        std::vector<uint8_t> rec_status, rec_has_deps;
+        std::vector<Tid> rec_exec, rec_deps;
+        std::vector<uint64_t> rec_dep_off;
     } cmds;
+    // per range entry of the snapshot (device order): live-command flag, and the command of each rank
+    std::vector<uint32_t> h_rtxw;
+    std::vector<uint8_t> h_rlive;
+    std::vector<uint32_t> h_cmd_rank;
     struct {
         std::vector<int64_t> start, end, e0, e1;
         std::vector<Tid> wm;
@@ -240,6 +249,8 @@ struct ad_ctx {
     std::vector<uint32_t> h_txn_rank, h_exec_rank, h_pruned;
     uint64_t rv_gen = ~0ull;                   // snap_gen the device view was built for
     DevBuf rv_ent, rv_seg, rv_pruned, rv_miss, rv_tree, rv_inv_off, rv_inv;
+    DevBuf rv_rcmd, rv_rflags, rv_rex_hi, rv_rex_lo, rv_rex_node, rv_rdep_off, rv_rdep_hi, rv_rdep_lo, rv_rdep_node;
+    bool rv_ranges = false;
     int rv_levels = 0;
     std::vector<uint64_t> rv_lvl_at;
     uint64_t rv_per_set = 0;
@@ -473,6 +484,7 @@ static int build_snapshot(ad_ctx* c)
     std::vector<DictRec>().swap(recs);
     for (uint64_t e = 0; e < ne; ++e)
         if (!exec_differs[e]) exec_rank[e] = txn_rank[e];
+    c->h_cmd_rank = cmd_rank;
 
     // ---- 2. per key validation, tau/txw, committed Writes by executeAt
     std::vector<uint2> ent(ne);
@@ -558,7 +570,7 @@ static int build_snapshot(ad_ctx* c)
     if (bad.load()) return c->fail(AD_E_INVAL, "prunedBefore of key %lld is not in byId", (long long)K.keys[bad_key.load()]);
 
     // ---- 3. range commands: (range, command) entries sorted by (start, end, txnId); range table
-    struct REnt { int64_t s, e; uint32_t txw; uint32_t rid; };
+    struct REnt { int64_t s, e; uint32_t txw; uint32_t rid; uint8_t live; };
     std::vector<int64_t> cell_E;
     bool cell_ok = false;
     std::vector<REnt> rent;
@@ -568,8 +580,9 @@ static int build_snapshot(ad_ctx* c)
         if (!hist && !c->cmds.erased.empty() && c->cmds.erased[i]) continue;   // saveStatus >= Erased, :897 (historical: no status)
         const uint32_t kind = (uint32_t)((c->cmds.txn[i].lsb >> 1) & 7);
         if ((c->cmds.txn[i].lsb & 1) == 0) return c->fail(AD_E_INVAL, "range command %llu has a key-domain TxnId", (unsigned long long)i);
+        const bool live = !hist && (c->cmds.erased.empty() || !c->cmds.erased[i]);     // rangeCommands, not erased
         for (uint64_t r = c->cmds.off[i]; r < c->cmds.off[i + 1]; ++r)
-            rent.push_back({c->cmds.start[r], c->cmds.end[r], cmd_rank[i] | (kind << RANK_BITS), 0});
+            rent.push_back({c->cmds.start[r], c->cmds.end[r], cmd_rank[i] | (kind << RANK_BITS), 0, (uint8_t)live});
     }
     for (uint64_t i = 0; i < nrb; ++i)
         if (i > 0 && c->rb.start[i] <= c->rb.start[i - 1]) return c->fail(AD_E_INVAL, "redundantBefore entries not ascending");
@@ -591,10 +604,18 @@ static int build_snapshot(ad_ctx* c)
             if (a.rid != b.rid) return a.rid < b.rid;
             return (a.txw & RANK_MASK) < (b.txw & RANK_MASK);
         });
-        rent.erase(std::unique(rent.begin(), rent.end(), [](const REnt& a, const REnt& b) {
-                       return a.rid == b.rid && (a.txw & RANK_MASK) == (b.txw & RANK_MASK);
-                   }),
-                   rent.end());
+        {
+            // one entry per (range, txnId); live if a live command contributed it
+            size_t o = 0;
+            for (size_t i = 0; i < rent.size(); ++i)
+            {
+                if (o > 0 && rent[o - 1].rid == rent[i].rid && (rent[o - 1].txw & RANK_MASK) == (rent[i].txw & RANK_MASK))
+                    rent[o - 1].live |= rent[i].live;
+                else
+                    rent[o++] = rent[i];
+            }
+            rent.resize(o);
+        }
         std::vector<uint32_t> rb_rid(nrb);
         for (uint64_t i = 0; i < nrb; ++i) rb_rid[i] = rid_of(c->rb.start[i], c->rb.end[i]);
         // padded to whole 64-entry frames: the fused kernel reads frames with vector loads
@@ -602,6 +623,9 @@ static int build_snapshot(ad_ctx* c)
         std::vector<int64_t> rs(rpad, INT64_MAX), re(rpad, INT64_MIN);
         std::vector<uint32_t> rtxw(rpad, 0), rrid(rpad, 0);
         for (size_t i = 0; i < rent.size(); ++i) { rs[i] = rent[i].s; re[i] = rent[i].e; rtxw[i] = rent[i].txw; rrid[i] = rent[i].rid; }
+        c->h_rtxw.assign(rtxw.begin(), rtxw.begin() + rent.size());
+        c->h_rlive.resize(rent.size());
+        for (size_t i = 0; i < rent.size(); ++i) c->h_rlive[i] = rent[i].live;
         for (uint64_t i = 0; i < nrb; ++i)
             if (wm_rank[i] && (c->rb.wm[i].lsb & 1) == 0) return c->fail(AD_E_INVAL, "redundantBefore watermark must be range-domain");
         int rc;
@@ -1593,6 +1617,8 @@ int ad_range_cmds_load(ad_ctx* c, const ad_range_cmds_soa* in)
     const uint64_t nr = n ? in->range_off[n] : 0;
     R.start.assign(in->range_start, in->range_start + nr);
     R.end.assign(in->range_end, in->range_end + nr);
+    R.rec = false;                  // recovery facts belong to the previous commands
+    c->rv_gen = ~0ull;
     drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
     c->dirty = true;
     return AD_OK;
@@ -1736,9 +1762,11 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
 {
     if (int rc0 = sync_host(c)) return rc0;
     auto& K = c->cfk;
+    bool live_cmds = false;
     for (size_t i = 0; i < c->cmds.txn.size(); ++i)
-        if (c->cmds.erased.empty() || !c->cmds.erased[i])
-            return c->fail(AD_E_STATE, "recovery scans of range commands need their deps (InMemoryCommandStore.java:931-949)");
+        live_cmds |= (c->cmds.historical.empty() || !c->cmds.historical[i]) && (c->cmds.erased.empty() || !c->cmds.erased[i]);
+    if (live_cmds && !c->cmds.rec)
+        return c->fail(AD_E_STATE, "recovery scans of range commands need their recovery facts (ad_range_cmds_recovery_load)");
     if (K.miss_stale) return c->fail(AD_E_STATE, "missing lists predate SEQUENTIAL insertions: load them again");
     const uint64_t ne = K.status.size(), nk = K.keys.size();
     if (c->rv_gen != c->snap_gen)
@@ -1839,6 +1867,48 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
         c->rv_levels = nl;
         c->rv_lvl_at.assign(lvl_at.begin(), lvl_at.end());
         c->rv_per_set = per_set;
+        // live range commands: entry -> command, the commands' facts normalised
+        {
+            const auto& R = c->cmds;
+            const size_t nc = R.txn.size(), nre = c->h_rtxw.size();
+            std::vector<uint32_t> r_cmd(std::max<size_t>(nre, 1), ~0u), flags(std::max<size_t>(nc, 1), 0), dep_off(nc + 1, 0);
+            std::vector<uint64_t> ex_hi(std::max<size_t>(nc, 1)), ex_lo(std::max<size_t>(nc, 1)), dhi, dlo;
+            std::vector<int32_t> ex_node(std::max<size_t>(nc, 1)), dnode;
+            std::vector<std::pair<uint32_t, uint32_t>> by_rank;       // (rank, command) of the live commands
+            for (size_t i = 0; i < nc; ++i)
+            {
+                const bool live = (R.historical.empty() || !R.historical[i]) && (R.erased.empty() || !R.erased[i]);
+                if (live) by_rank.push_back({c->h_cmd_rank[i], (uint32_t)i});
+                if (R.rec)
+                {
+                    flags[i] = (R.rec_status[i] & 3u) | (R.rec_has_deps[i] ? 4u : 0u);
+                    const NormTid x = norm(R.rec_exec[i]);
+                    ex_hi[i] = x.hi; ex_lo[i] = x.lo; ex_node[i] = x.node;
+                    for (uint64_t j = R.rec_dep_off[i]; j < R.rec_dep_off[i + 1]; ++j)
+                    {
+                        const NormTid d = norm(R.rec_deps[j]);
+                        dhi.push_back(d.hi); dlo.push_back(d.lo); dnode.push_back(d.node);
+                    }
+                }
+                dep_off[i + 1] = (uint32_t)dhi.size();
+            }
+            std::sort(by_rank.begin(), by_rank.end());
+            for (size_t e = 0; e < nre; ++e)
+            {
+                if (!c->h_rlive[e]) continue;
+                const uint32_t rk = c->h_rtxw[e] & RANK_MASK;
+                auto it = std::lower_bound(by_rank.begin(), by_rank.end(), std::make_pair(rk, 0u));
+                if (it != by_rank.end() && it->first == rk) r_cmd[e] = it->second;
+            }
+            if (dhi.empty()) { dhi.push_back(0); dlo.push_back(0); dnode.push_back(0); }
+            if ((rc = upload(c, c->rv_rcmd, r_cmd)) || (rc = upload(c, c->rv_rflags, flags)) ||
+                (rc = upload(c, c->rv_rex_hi, ex_hi)) || (rc = upload(c, c->rv_rex_lo, ex_lo)) ||
+                (rc = upload(c, c->rv_rex_node, ex_node)) || (rc = upload(c, c->rv_rdep_off, dep_off)) ||
+                (rc = upload(c, c->rv_rdep_hi, dhi)) || (rc = upload(c, c->rv_rdep_lo, dlo)) ||
+                (rc = upload(c, c->rv_rdep_node, dnode)))
+                return rc;
+            c->rv_ranges = live_cmds && nre > 0;
+        }
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->rv_gen = c->snap_gen;
     }
@@ -1853,6 +1923,16 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
     v->n_levels = c->rv_levels;
     v->inv_off = c->rv_inv_off.as<uint64_t>();
     v->inv = c->rv_inv.as<uint2>();
+    v->r_cmd = c->rv_rcmd.as<uint32_t>();
+    v->rc_flags = c->rv_rflags.as<uint32_t>();
+    v->rc_ex_hi = c->rv_rex_hi.as<uint64_t>();
+    v->rc_ex_lo = c->rv_rex_lo.as<uint64_t>();
+    v->rc_ex_node = c->rv_rex_node.as<int32_t>();
+    v->rc_dep_off = c->rv_rdep_off.as<uint32_t>();
+    v->rc_dep_hi = c->rv_rdep_hi.as<uint64_t>();
+    v->rc_dep_lo = c->rv_rdep_lo.as<uint64_t>();
+    v->rc_dep_node = c->rv_rdep_node.as<int32_t>();
+    v->ranges = c->rv_ranges;
     return 0;
 }
 
@@ -1883,6 +1963,38 @@ int ad_cfk_missing_load(ad_ctx* c, const ad_cfk_missing_soa* m)
     K.miss.resize(nm);
     for (uint64_t j = 0; j < nm; ++j) K.miss[j] = {m->msb[j], m->lsb[j], m->node[j]};
     K.miss_stale = false;
+    c->rv_gen = ~0ull;
+    return AD_OK;
+}
+
+int ad_range_cmds_recovery_load(ad_ctx* c, const ad_range_cmds_recovery_soa* in)
+{
+    if (!c || !in) return AD_E_INVAL;
+    auto& R = c->cmds;
+    const uint64_t n = in->n_cmds;
+    if (n != R.txn.size())
+        return c->fail(AD_E_INVAL, "recovery facts for %llu range commands, %llu loaded", (unsigned long long)n,
+                       (unsigned long long)R.txn.size());
+    if (n && (!in->status || !in->has_deps || !in->exec_msb || !in->exec_lsb || !in->exec_node || !in->dep_off))
+        return AD_E_INVAL;
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        if (in->status[i] > 3) return c->fail(AD_E_INVAL, "range command %llu: status class %u", (unsigned long long)i, in->status[i]);
+        if (in->dep_off[i + 1] < in->dep_off[i]) return c->fail(AD_E_INVAL, "range command deps offsets not monotone");
+        for (uint64_t j = in->dep_off[i] + 1; j < in->dep_off[i + 1]; ++j)
+            if (norm_cmp(norm_tid(in->dep_msb[j - 1], in->dep_lsb[j - 1], in->dep_node[j - 1]),
+                         norm_tid(in->dep_msb[j], in->dep_lsb[j], in->dep_node[j])) >= 0)
+                return c->fail(AD_E_INVAL, "range command deps not strictly ascending");
+    }
+    R.rec_status.assign(in->status, in->status + n);
+    R.rec_has_deps.assign(in->has_deps, in->has_deps + n);
+    R.rec_exec.resize(n);
+    for (uint64_t i = 0; i < n; ++i) R.rec_exec[i] = {in->exec_msb[i], in->exec_lsb[i], in->exec_node[i]};
+    R.rec_dep_off.assign(in->dep_off, in->dep_off + n + 1);
+    const uint64_t nd = n ? in->dep_off[n] : 0;
+    R.rec_deps.resize(nd);
+    for (uint64_t j = 0; j < nd; ++j) R.rec_deps[j] = {in->dep_msb[j], in->dep_lsb[j], in->dep_node[j]};
+    R.rec = true;
     c->rv_gen = ~0ull;
     return AD_OK;
 }

@@ -1037,55 +1037,64 @@ __global__ __launch_bounds__(LB_TILE) void k_tile_sums(BatchBufs b)
         uint64_t acc = 0;
 #pragma unroll
         for (uint32_t ww = 0; ww < NW; ++ww) acc += s_w[ww][tid];
-        b.lb_agg[(uint64_t)blockIdx.x * 9 + tid] = acc;
+        b.lb_agg[(uint64_t)tid * gridDim.x + blockIdx.x] = acc;      // [9][tiles]
     }
 }
 
-// one block of 1024 threads: lb_inc[tile][a] = exclusive prefix of lb_agg over tiles, totals. Thread
-// i owns the consecutive tiles [i * per, (i + 1) * per): a serial sum, one block scan, a serial pass.
+// one block of 1024 threads per array a: lb_inc[a][tile] = exclusive prefix of lb_agg[a] over the
+// tiles (4 consecutive tiles per thread, chunks of 4096 tiles with a carry), the total into the
+// control block and off[a][n].
 __global__ __launch_bounds__(1024) void k_tile_scan(BatchBufs b, uint64_t tiles)
 {
-    __shared__ uint64_t s_w[16][9];
+    __shared__ uint64_t s_w[16];
     const BatchCtl* cc = b.ctl;
     if (cc->n_deferred || cc->error || (cc->overflow & 15u)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-    const uint64_t per = (tiles + 1023) / 1024;
-    const uint64_t i0 = tid * per, i1 = i0 + per < tiles ? i0 + per : tiles;
-#pragma unroll 1
-    for (int a = 0; a < 9; ++a)
+    const int a = blockIdx.x;
+    const uint64_t* __restrict__ agg = b.lb_agg + (uint64_t)a * tiles;
+    uint64_t* __restrict__ inc = b.lb_inc + (uint64_t)a * tiles;
+    uint64_t carry = 0;
+    for (uint64_t c0 = 0; c0 < tiles; c0 += 4096)
     {
-        uint64_t sum = 0;
-        for (uint64_t i = i0; i < i1; ++i) sum += b.lb_agg[i * 9 + a];
+        const uint64_t i0 = c0 + 4ull * tid;
+        uint64_t y[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+        {
+            y[k] = i0 + k < tiles ? agg[i0 + k] : 0;
+            sum += y[k];
+        }
         uint64_t x = sum;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1)
         {
-            const uint64_t y = __shfl_up(x, d, 64);
-            if ((int)lane >= d) x += y;
+            const uint64_t z = __shfl_up(x, d, 64);
+            if ((int)lane >= d) x += z;
         }
-        if (lane == 63) s_w[w][a] = x;
+        if (lane == 63) s_w[w] = x;
         __syncthreads();
         uint64_t wpre = 0, tot = 0;
 #pragma unroll
         for (uint32_t ww = 0; ww < 16; ++ww)
         {
-            const uint64_t y = s_w[ww][a];
-            if (ww < w) wpre += y;
-            tot += y;
+            const uint64_t z = s_w[ww];
+            if (ww < w) wpre += z;
+            tot += z;
         }
-        uint64_t e = wpre + x - sum;
-        for (uint64_t i = i0; i < i1; ++i)
+        uint64_t e = carry + wpre + x - sum;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
         {
-            const uint64_t y = b.lb_agg[i * 9 + a];
-            b.lb_inc[i * 9 + a] = e;
-            e += y;
+            if (i0 + k < tiles) inc[i0 + k] = e;
+            e += y[k];
         }
-        if (tid == 0)
-        {
-            b.ctl->tot[a] = tot;
-            b.off[(uint64_t)a * (b.n_txns + 1) + b.n_txns] = tot;
-        }
+        carry += tot;
         __syncthreads();
+    }
+    if (tid == 0)
+    {
+        b.ctl->tot[a] = carry;
+        b.off[(uint64_t)a * (b.n_txns + 1) + b.n_txns] = carry;
     }
 }
 
@@ -1103,10 +1112,13 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
     const uint64_t n = b.n_txns;
     const uint64_t t = (uint64_t)tile * LB_TILE + tid;
     const bool on = t < n;
-#pragma unroll 1
+    uint32_t vv[9];
+#pragma unroll
+    for (int a = 0; a < 9; ++a) vv[a] = on ? b.sz[(uint64_t)a * n + t] : 0u;     // all in flight together
+#pragma unroll
     for (int a = 0; a < 9; ++a)
     {
-        const uint64_t v = on ? b.sz[(uint64_t)a * n + t] : 0u;
+        const uint64_t v = vv[a];
         uint64_t x = v;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1)
@@ -1120,7 +1132,7 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
     __syncthreads();
     if (tid < 9)
     {
-        uint64_t acc = b.lb_inc[(uint64_t)tile * 9 + tid];
+        uint64_t acc = b.lb_inc[(uint64_t)tid * gridDim.x + tile];
 #pragma unroll
         for (uint32_t ww = 0; ww < NW; ++ww)
         {
@@ -1180,7 +1192,7 @@ hipError_t run_pack_lb(const BatchBufs& b, bool copy, hipStream_t st)
     if (!b.n_txns) return hipMemsetAsync(b.off, 0, sizeof(uint64_t) * 9, st);     // off[a][0] = 0
     const uint64_t tiles = lb_tiles(b.n_txns);
     k_tile_sums<<<(unsigned)tiles, LB_TILE, 0, st>>>(b);
-    k_tile_scan<<<1, 1024, 0, st>>>(b, tiles);
+    k_tile_scan<<<9, 1024, 0, st>>>(b, tiles);
     k_pack_tiles<<<(unsigned)tiles, LB_TILE, 0, st>>>(b, copy ? 1 : 0);
     return hipGetLastError();
 }
@@ -1582,6 +1594,116 @@ __global__ __launch_bounds__(256) void k_recover(RecoveryView v, BatchBufs b, ui
     }
 }
 
+// The range-command half of the recovery scans (InMemorySafeStore.mapReduceFull ->
+// mapReduceRangesInternal, InMemoryCommandStore.java:884-958): one wave per (request, key) probe
+// finds the range entries holding the key by the K4 descent (start before the key, max-end tree of
+// the all-kinds class), and keeps those of live commands passing the scan's tests; their (range id,
+// txnId) pairs go to the K4 arena, so k_build assembles rangeDeps (one txnId per range, as the
+// collect fold does).
+__global__ __launch_bounds__(256) void k_range_recover(DevSnapshot s, RecoveryView v, BatchBufs b, uint32_t scan)
+{
+    __shared__ uint64_t stage[K4_WAVES][K4_CAP];
+    __shared__ uint64_t stk[K4_WAVES][2 * MAX_LEVELS];
+    const int wv = threadIdx.x >> 6;
+    const uint32_t lane = lane_id();
+    const uint64_t nw = (uint64_t)gridDim.x * K4_WAVES;
+    ChunkAlloc alloc;
+    const unsigned long long cap = b.ctl->rng_cap;
+    const bool incl = s.start_inclusive != 0;
+    const bool with = scan == 1, before = scan == 0 || scan == 1, after = scan == 2;
+    const uint32_t need = (scan == 0 || scan == 2) ? 1u : 2u;     // AD_RS_PROPOSED / AD_RS_STABLE
+    for (uint64_t p = (uint64_t)blockIdx.x * K4_WAVES + wv; p < b.n_probes; p += nw)
+    {
+        const int64_t x = b.q_keys[p];
+        const uint32_t t = b.p_txn[p];
+        const uint32_t T = b.t_S[t], kinds = b.t_kinds[t];
+        const NormTid Tn = norm_tid(b.q_txn_msb[t], b.q_txn_lsb[t], b.q_txn_node[t]);
+        uint32_t cnt = 0;
+        uint64_t off = 0;
+        const bool in_slice = (b.p_rec[p].w >> 12) & 1;
+        if (in_slice && s.n_rent && kinds)
+        {
+            const uint64_t hi = wave_lower_bound(0, s.n_rent, [&](uint64_t i) { return s.r_start[i]; },
+                                                 [&](int64_t val) { return incl ? val <= x : val < x; });
+            auto end_ok = [&](int64_t e) { return incl ? e > x : e >= x; };
+            auto node_want = [&](int lv, uint64_t node) { return end_ok(s.rlvl[2][lv][node]); };
+            auto want_of = [&](uint64_t i, bool inr, uint64_t& val) -> bool {
+                val = 0;
+                if (!inr || !end_ok(s.r_end[i])) return false;
+                const uint32_t c = v.r_cmd[i];
+                if (c == ~0u) return false;                              // not a live rangeCommands entry
+                const uint32_t txw = s.r_txw[i], r = txw & RANK_MASK, kd = txw >> RANK_BITS;
+                const uint32_t fl = v.rc_flags[c];
+                const NormTid ex{v.rc_ex_hi[c], v.rc_ex_lo[c], v.rc_ex_node[c]};
+                if (after && !(r > T)) return false;                     // STARTED_AFTER (:902-904)
+                if (before && !(r < T)) return false;                    // STARTED_BEFORE (:905-906)
+                if (!after && norm_cmp(ex, Tn) < 0) return false;        // executeAtOrTxnId >= testTxnId (:907-908)
+                if (!(fl & need)) return false;                          // IS_PROPOSED / IS_STABLE (:915-928)
+                if (!((kinds >> kd) & 1)) return false;                  // testKind (:931)
+                if (!(fl & 4u)) return false;                            // hasProposedOrDecidedDeps (:936)
+                uint32_t a = v.rc_dep_off[c], z = v.rc_dep_off[c + 1];   // partialDeps().intersects (:946)
+                while (a < z)
+                {
+                    const uint32_t m = (a + z) >> 1;
+                    if (norm_cmp(NormTid{v.rc_dep_hi[m], v.rc_dep_lo[m], v.rc_dep_node[m]}, Tn) < 0) a = m + 1;
+                    else z = m;
+                }
+                const bool inter = a < v.rc_dep_off[c + 1] && norm_cmp(NormTid{v.rc_dep_hi[a], v.rc_dep_lo[a], v.rc_dep_node[a]}, Tn) == 0;
+                if (inter != with) return false;
+                if (scan == 0 && !(norm_cmp(ex, Tn) > 0)) return false;  // the lambda: executeAt > startedBefore (BeginRecovery.java:335)
+                val = ((uint64_t)s.r_rid[i] << 32) | r;
+                return true;
+            };
+            uint32_t cursor = 0;
+            bool overflow = false;
+            auto leaf_stage = [&](uint64_t base, bool inr) {
+                uint64_t val;
+                const bool want = want_of(base + lane, inr, val);
+                const uint64_t wm = ballot(want);
+                const uint32_t n = __popcll(wm);
+                if (!overflow && cursor + n <= K4_CAP)
+                {
+                    if (want) stage[wv][cursor + mbcnt(wm)] = val;
+                }
+                else overflow = true;
+                cursor += n;
+            };
+            wave_descent(0, hi, s.n_rlevels, node_want, leaf_stage, stk[wv]);
+            wave_lds_sync();
+            cnt = cursor;
+            off = cnt ? alloc.take(&b.ctl->rng_top, cap, &b.ctl->overflow, 2u, cnt, K4_CHUNK) : 0;
+            if (off + cnt > cap)
+            {
+                off = 0;
+                cnt = 0;                 // overflow: the host grows the arena and reruns
+            }
+            else if (cnt)
+            {
+                if (!overflow)
+                    for (uint32_t i = lane; i < cnt; i += 64) b.rarena[off + i] = stage[wv][i];
+                else
+                {
+                    uint32_t run = 0;
+                    auto leaf_direct = [&](uint64_t base, bool inr) {
+                        uint64_t val;
+                        const bool want = want_of(base + lane, inr, val);
+                        const uint64_t wm = ballot(want);
+                        if (want) b.rarena[off + run + mbcnt(wm)] = val;
+                        run += __popcll(wm);
+                    };
+                    wave_descent(0, hi, s.n_rlevels, node_want, leaf_direct, stk[wv]);
+                }
+            }
+        }
+        if (lane == 0)
+        {
+            b.p_roff[p] = (uint32_t)off;
+            b.p_rcnt[p] = cnt;
+            b.p_rb[p] = NO_RB;
+        }
+    }
+}
+
 hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const BatchBufs& b, uint32_t scan, hipStream_t st)
 {
     if (b.n_txns)
@@ -1592,10 +1714,15 @@ hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const Batch
         const uint64_t blocks_needed = (b.n_probes + K1_WAVES - 1) / K1_WAVES;
         const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
         k_recover<<<grid, 256, 0, st>>>(v, b, scan);
-        // recovery scans of key-domain stores collect no range pairs (empty K4 lists)
-        hipError_t e = hipMemsetAsync(b.p_rcnt, 0, sizeof(uint32_t) * b.n_probes, st);
-        if (e == hipSuccess) e = hipMemsetAsync(b.p_rb, 0xFF, sizeof(uint64_t) * b.n_probes, st);
-        if (e != hipSuccess) return e;
+        if (v.ranges)
+            k_range_recover<<<grid, 256, 0, st>>>(s, v, b, scan);
+        else
+        {
+            // no live range commands: no range pairs (empty K4 lists)
+            hipError_t e = hipMemsetAsync(b.p_rcnt, 0, sizeof(uint32_t) * b.n_probes, st);
+            if (e == hipSuccess) e = hipMemsetAsync(b.p_rb, 0xFF, sizeof(uint64_t) * b.n_probes, st);
+            if (e != hipSuccess) return e;
+        }
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -58,8 +58,8 @@ struct BatchBufs {
     const unsigned long long* req_count;
     int64_t* o_keys[3]; uint32_t* o_txns[3]; int32_t* o_k2t[3];
     uint64_t o_cap[9];               // capacities (elements) of the packed arrays, [3 * map + array]
-    uint64_t* lb_agg;                // [tiles][9] size sums per tile (k_tile_sums)
-    uint64_t* lb_inc;                // [tiles][9] exclusive prefixes of the tile sums (k_tile_scan)
+    uint64_t* lb_agg;                // [9][tiles] size sums per tile (k_tile_sums)
+    uint64_t* lb_inc;                // [9][tiles] exclusive prefixes of the tile sums (k_tile_scan)
     BatchCtl* ctl;
 };
 
@@ -77,6 +77,15 @@ struct RecoveryView {
     // per key, its entries' (missing() id, entry) pairs sorted: [inv_off[k], inv_off[k + 1])
     const uint64_t* inv_off;
     const uint2* inv;
+    // live range commands (ad_range_cmds_recovery_load): per range entry of the snapshot its command
+    // (load order) or ~0u; per command AD_RS_* | has_deps << 2, executeAtOrTxnId and the ids t with
+    // partialDeps().intersects(t, its ranges) (ascending), normalised for norm_cmp
+    const uint32_t* r_cmd;
+    const uint32_t* rc_flags;
+    const uint64_t* rc_ex_hi; const uint64_t* rc_ex_lo; const int32_t* rc_ex_node;
+    const uint32_t* rc_dep_off;
+    const uint64_t* rc_dep_hi; const uint64_t* rc_dep_lo; const int32_t* rc_dep_node;
+    bool ranges;             // the store has live range commands
 };
 constexpr uint32_t RV_MISS_SHIFT = 12;
 constexpr uint32_t RV_MAX_MISS = (1u << 20) - 1;

@@ -471,9 +471,36 @@ int ad_cfk_missing_load(ad_ctx* ctx, const ad_cfk_missing_soa* missing);
 #define AD_RECOVER_EXECUTES_AFTER_STABLE_NO_WITNESS   3  /* hasStableExecutesAfterWithoutWitnessing :369-380:
                                                           * ANY, WITHOUT, IS_STABLE                         */
 
-/* Host buffers in, host result out (as ad_deps_batch; rangeDeps is empty). Range-domain commands
- * need their own deps to be tested (InMemoryCommandStore.java:931-949), which this ABI does not
- * carry: a store with live range commands fails with AD_E_STATE. */
+/* What the recovery scans read of the store's live range commands (InMemorySafeStore.mapReduceFull ->
+ * mapReduceRangesInternal, InMemoryCommandStore.java:884-958): per command of the last
+ * ad_range_cmds_load (same order; historical and erased ones are not read), its status class, whether
+ * it knows deps (known().deps.hasProposedOrDecidedDeps()), executeAtOrTxnId, and the TxnIds t for
+ * which partialDeps().intersects(t, the command's ranges) holds (ascending) -- the witness test of
+ * :946. A scan then tests, per range command whose ranges hold one of the request's keys:
+ * STARTED_AFTER txnId > testTxnId; STARTED_BEFORE txnId < testTxnId and executeAtOrTxnId >=
+ * testTxnId; ANY executeAtOrTxnId >= testTxnId; the status class; testKind; deps known; WITH: the
+ * list holds testTxnId, WITHOUT: it does not; the pairs (range, txnId) go to rangeDeps (scan 0's
+ * lambda also wants executeAt > testTxnId, :335). */
+#define AD_RS_PROPOSED 1   /* Status PreCommitted, Committed or Accepted (IS_PROPOSED, :917-925)   */
+#define AD_RS_STABLE   2   /* Stable <= Status < Truncated (IS_STABLE, :926-928)                   */
+typedef struct ad_range_cmds_recovery_soa {
+    uint64_t n_cmds;                /* == n_cmds of the loaded ad_range_cmds_soa */
+    const uint8_t*  status;         /* AD_RS_* (0: neither)                       */
+    const uint8_t*  has_deps;
+    const uint64_t* exec_msb;       /* executeAtOrTxnId                           */
+    const uint64_t* exec_lsb;
+    const int32_t*  exec_node;
+    const uint64_t* dep_off;        /* [n_cmds + 1]                               */
+    const uint64_t* dep_msb;
+    const uint64_t* dep_lsb;
+    const int32_t*  dep_node;
+} ad_range_cmds_recovery_soa;
+
+int ad_range_cmds_recovery_load(ad_ctx* ctx, const ad_range_cmds_recovery_soa* rec);
+
+/* Host buffers in, host result out (as ad_deps_batch). A store with live range commands needs
+ * their recovery facts (ad_range_cmds_recovery_load after the last ad_range_cmds_load), else
+ * AD_E_STATE. */
 int ad_recovery_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t scan, ad_deps_result** out);
 /* Device buffers in and out, as ad_deps_batch_device (result valid until the next batch call). */
 int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t scan, void* stream, ad_deps_result* out);

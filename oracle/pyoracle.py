@@ -60,6 +60,7 @@ def lib():
         L.rc_preaccept.argtypes = [C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdRangeMapSoa), C.POINTER(A.AdQuerySoa),
                                    C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rc_cfk_missing_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkMissingSoa)]
+        L.rc_range_cmds_recovery_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsRecoverySoa)]
         L.rc_recovery_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_uint64, C.c_uint64,
                                         C.POINTER(C.POINTER(RcResult))]
         L.rc_tid_cmp.argtypes = [C.c_uint64, C.c_uint64, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32]
@@ -127,6 +128,9 @@ class OracleStore:
         ms = workload.cfk.missing_soa()
         if ms is not None:
             self._check(L.rc_cfk_missing_load(self.h, C.byref(ms)))
+        rs = workload.cmds.recovery_soa()
+        if rs is not None:
+            self._check(L.rc_range_cmds_recovery_load(self.h, C.byref(rs)))
         return self
 
     def recovery_batch(self, queries, scan, first=0, count=0):

@@ -489,6 +489,11 @@ typedef struct {
     tid_t txnId;
     int erased, historical;
     VEC(rkey_t) ranges;
+    size_t orig;              /* index in the ad_range_cmds_soa it was loaded from */
+    /* recovery facts (rc_range_cmds_recovery_load; InMemoryCommandStore.java:884-958) */
+    int has_rec, rstatus, has_deps;
+    tid_t exec;               /* executeAtOrTxnId */
+    VEC(tid_t) deps;          /* t with partialDeps().intersects(t, ranges), ascending */
 } rcmd_t;
 
 typedef struct {
@@ -541,8 +546,8 @@ int rc_store_create(const ad_config* cfg, rc_store** out)
 
 static void free_cmds(rc_store* s)
 {
-    for (size_t i = 0; i < s->cmds.n; ++i) VEC_FREE(s->cmds.v[i].ranges);
-    for (size_t i = 0; i < s->hist.n; ++i) VEC_FREE(s->hist.v[i].ranges);
+    for (size_t i = 0; i < s->cmds.n; ++i) { VEC_FREE(s->cmds.v[i].ranges); VEC_FREE(s->cmds.v[i].deps); }
+    for (size_t i = 0; i < s->hist.n; ++i) { VEC_FREE(s->hist.v[i].ranges); VEC_FREE(s->hist.v[i].deps); }
     VEC_FREE(s->cmds); VEC_FREE(s->hist);
 }
 
@@ -656,6 +661,7 @@ int rc_range_cmds_load(rc_store* s, const ad_range_cmds_soa* in)
         rcmd_t c;
         memset(&c, 0, sizeof(c));
         c.txnId = (tid_t){in->txn_msb[i], in->txn_lsb[i], in->txn_node[i]};
+        c.orig = (size_t)i;
         c.erased = in->erased ? in->erased[i] : 0;
         c.historical = in->historical ? in->historical[i] : 0;
         for (uint64_t r = in->range_off[i]; r < in->range_off[i + 1]; ++r)
@@ -1433,6 +1439,107 @@ static int cfk_map_reduce_full(const rc_store* s, const cfk_t* c, const tid_t* t
     return 0;
 }
 
+int rc_range_cmds_recovery_load(rc_store* s, const ad_range_cmds_recovery_soa* in)
+{
+    const size_t n = s->cmds.n + s->hist.n;
+    if (in->n_cmds != n) return fail(s, AD_E_INVAL, "recovery facts for %llu range commands, %llu loaded",
+                                     (unsigned long long)in->n_cmds, (unsigned long long)n);
+    for (size_t i = 0; i < s->cmds.n; ++i)
+    {
+        rcmd_t* c = &s->cmds.v[i];
+        const size_t o = c->orig;
+        VEC_FREE(c->deps);
+        c->has_rec = 1;
+        c->rstatus = in->status[o];
+        c->has_deps = in->has_deps[o] != 0;
+        c->exec = (tid_t){in->exec_msb[o], in->exec_lsb[o], in->exec_node[o]};
+        if (in->dep_off[o + 1] < in->dep_off[o]) return fail(s, AD_E_INVAL, "range command deps offsets not monotone");
+        for (uint64_t j = in->dep_off[o]; j < in->dep_off[o + 1]; ++j)
+        {
+            const tid_t t = {in->dep_msb[j], in->dep_lsb[j], in->dep_node[j]};
+            if (c->deps.n && tid_cmp(&c->deps.v[c->deps.n - 1], &t) >= 0)
+                return fail(s, AD_E_INVAL, "range command deps not strictly ascending");
+            VEC_PUSH(c->deps, t);
+        }
+    }
+    return 0;
+}
+
+static int tids_contain(const tid_t* v, size_t n, const tid_t* x)
+{
+    size_t lo = 0, hi = n;
+    while (lo < hi)
+    {
+        const size_t mid = (lo + hi) / 2;
+        if (tid_cmp(&v[mid], x) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && tid_eq(&v[lo], x);
+}
+
+/* InMemorySafeStore.mapReduceFull's range half: mapReduceRangesInternal (InMemoryCommandStore.java:884-958)
+ * for a recovery scan (testStatus != ANY_STATUS: no historical commands), then the collect fold
+ * (:1005-1014) into the scan's lambda (BeginRecovery.java:334-380; scan 0 wants executeAt > its
+ * testTxnId) */
+static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t nkeys, const tid_t* T, unsigned testKind,
+                                  int startedAt, int testDep, int testStatus, int exec_after, deps_builder_t* b)
+{
+    int64_t* sliced = malloc(sizeof(int64_t) * (nkeys ? nkeys : 1));
+    size_t nsliced = 0;
+    for (size_t k = 0; k < nkeys; ++k) if (slice_contains(s, keys[k])) sliced[nsliced++] = keys[k];
+    collect_vec_t col;
+    memset(&col, 0, sizeof(col));
+    for (size_t i = 0; i < s->cmds.n; ++i)
+    {
+        const rcmd_t* c = &s->cmds.v[i];
+        if (c->erased) continue;                                           /* :897 */
+        switch (startedAt)                                                 /* :900-913 */
+        {
+            case STARTED_AFTER:
+                if (tid_cmp(&c->txnId, T) <= 0) continue;
+                break;
+            case STARTED_BEFORE:
+                if (tid_cmp(&c->txnId, T) >= 0) continue;
+                /* fall through */
+            default:
+                if (testDep != ANY_DEPS && tid_cmp(&c->exec, T) < 0) continue;
+        }
+        if (testStatus == IS_PROPOSED && !(c->rstatus & AD_RS_PROPOSED)) continue;     /* :915-925 */
+        if (testStatus == IS_STABLE && !(c->rstatus & AD_RS_STABLE)) continue;         /* :926-928 */
+        if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;                       /* :931 */
+        if (testDep != ANY_DEPS)                                                        /* :934-947 */
+        {
+            if (!c->has_deps) continue;
+            const int inter = tids_contain(c->deps.v, c->deps.n, T);
+            if ((testDep == WITH) == !inter) continue;
+        }
+        collect_command(s, &col, c, sliced, nsliced);                                   /* :949-956 */
+    }
+    int rc = 0;
+    for (size_t i = 0; i < col.n && !rc; ++i)
+        for (size_t j = 0; j < col.v[i].list.n && !rc; ++j)
+        {
+            const tid_t* id = &col.v[i].list.v[j];
+            if (exec_after)
+            {
+                /* the command's executeAt (rangeCommands is sorted by txnId) */
+                size_t lo = 0, hi = s->cmds.n;
+                while (lo < hi)
+                {
+                    const size_t mid = (lo + hi) / 2;
+                    if (tid_cmp(&s->cmds.v[mid].txnId, id) < 0) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (!(tid_cmp(&s->cmds.v[lo].exec, T) > 0)) continue;
+            }
+            rc = deps_builder_add(b, 1, col.v[i].range.a, col.v[i].range.b, id);
+        }
+    for (size_t i = 0; i < col.n; ++i) VEC_FREE(col.v[i].list);
+    VEC_FREE(col);
+    free(sliced);
+    return rc;
+}
+
 int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_t first, uint64_t count, rc_result** out)
 {
     static const int P[4][3] = {{STARTED_BEFORE, WITHOUT, IS_PROPOSED}, {STARTED_BEFORE, WITH, IS_STABLE},
@@ -1440,8 +1547,8 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
     if (!s->loaded) return fail(s, AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (scan > 3) return fail(s, AD_E_INVAL, "unknown recovery scan %u", scan);
     for (size_t i = 0; i < s->cmds.n; ++i)
-        if (!s->cmds.v[i].erased)
-            return fail(s, AD_E_STATE, "range-domain recovery scans need each range command's deps");
+        if (!s->cmds.v[i].erased && !s->cmds.v[i].has_rec)
+            return fail(s, AD_E_STATE, "recovery scans of range commands need their recovery facts (rc_range_cmds_recovery_load)");
     if (count == 0) count = q->n_txns - first;
     if (first + count > q->n_txns) return fail(s, AD_E_INVAL, "query window out of range");
     rc_result* r = calloc(1, sizeof(rc_result));
@@ -1476,6 +1583,8 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
             if (cfk == NULL) continue;
             rc = cfk_map_reduce_full(s, cfk, &txnId, kinds, P[scan][0], P[scan][1], P[scan][2], &builder);
         }
+        if (!rc)
+            rc = map_reduce_ranges_full(s, keys, nkeys, &txnId, kinds, P[scan][0], P[scan][1], P[scan][2], scan == 0, &builder);
         pdeps_t pd;
         memset(&pd, 0, sizeof(pd));
         if (!rc) rc = deps_build(&builder, &pd);

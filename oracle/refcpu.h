@@ -65,6 +65,8 @@ int rc_preaccept(const ad_range_map_soa* max_conflicts, const ad_range_map_soa* 
 int rc_cfk_missing_load(rc_store* s, const ad_cfk_missing_soa* m);
 int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_t first, uint64_t count,
                       rc_result** out);
+/* the range commands' recovery facts (ad_range_cmds_recovery_load) */
+int rc_range_cmds_recovery_load(rc_store* s, const ad_range_cmds_recovery_soa* rec);
 
 /* exposed for the tests */
 int rc_tid_cmp(uint64_t amsb, uint64_t alsb, int32_t anode, uint64_t bmsb, uint64_t blsb, int32_t bnode);

@@ -266,3 +266,46 @@ def recovery_pairs(w, qi, scan):
                 continue
             (kd if kind(t) in (0, 1) else dd).add((k, key(t), t))
     return kd, dd
+
+
+def recovery_range_pairs(w, qi, scan):
+    """rangeDeps pairs of BeginRecovery scan `scan` for request qi from the store's live range commands,
+    a flat reading of mapReduceRangesInternal's predicates (InMemoryCommandStore.java:884-958) and the
+    scan's lambda (BeginRecovery.java:334-380): ((start, end), order key, txnId)."""
+    q, cm = w.queries, w.cmds
+    out = set()
+    if len(cm.txn) == 0:
+        return out
+    T = (int(q.txn.msb[qi]), int(q.txn.lsb[qi]), int(q.txn.node[qi]))
+    keys = [int(k) for k in q.keys[int(q.key_off[qi]):int(q.key_off[qi + 1])]]
+    si = w.range_start_inclusive
+    if w.slices is not None:
+        keys = [k for k in keys if any(contains(si, int(a), int(b), k) for a, b in w.slices)]
+    started, with_dep, statuses = RECOVER[scan]
+    need = 1 if statuses == (3, 4) else 2                  # AD_RS_PROPOSED / AD_RS_STABLE
+    kinds = WITNESSED_BY[kind(T)]
+    for i in range(len(cm.txn)):
+        if (cm.historical is not None and cm.historical[i]) or (cm.erased is not None and cm.erased[i]):
+            continue
+        t = (int(cm.txn.msb[i]), int(cm.txn.lsb[i]), int(cm.txn.node[i]))
+        ex = (int(cm.rec_exec.msb[i]), int(cm.rec_exec.lsb[i]), int(cm.rec_exec.node[i]))
+        if started == "after" and not key(t) > key(T):
+            continue
+        if started == "before" and not key(t) < key(T):
+            continue
+        if started in ("before", "any") and key(ex) < key(T):
+            continue
+        if not int(cm.rec_status[i]) & need or kind(t) not in kinds or not cm.rec_has_deps[i]:
+            continue
+        d0, d1 = int(cm.rec_dep_off[i]), int(cm.rec_dep_off[i + 1])
+        inter = any(eq((int(cm.rec_deps.msb[j]), int(cm.rec_deps.lsb[j]), int(cm.rec_deps.node[j])), T)
+                    for j in range(d0, d1))
+        if inter != with_dep:
+            continue
+        if scan == 0 and not key(ex) > key(T):
+            continue
+        for r in range(int(cm.range_off[i]), int(cm.range_off[i + 1])):
+            a, b = int(cm.range_start[r]), int(cm.range_end[r])
+            if any(contains(si, a, b, k) for k in keys):
+                out.add(((a, b), key(t), t))
+    return out

@@ -96,3 +96,36 @@ def test_errors():
         assert got.n_txns == len(q)
     finally:
         st.close()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_recovery_with_ranges(oracle, seed):
+    # live range commands with their recovery facts: the range half of mapReduceFull
+    # (InMemoryCommandStore.java:884-958) -> rangeDeps, plus erased / historical commands it skips
+    w = synth.recovery_workload(seed, n_range_cmds=16 + 8 * seed, with_slices=(seed % 3 == 2),
+                                start_inclusive=(seed % 4 == 1))
+    _same(w, oracle)
+
+
+def test_many_range_commands_recovery(oracle):
+    # hundreds of range entries: several frames of the range descent per probe
+    w = synth.recovery_workload(31, n_range_cmds=400, n_hist_txns=300)
+    assert sum(oracle.recover(w, s).pair_count(1) for s in A.RECOVER_SCANS) > 0
+    _same(w, oracle)
+
+
+def test_range_facts_cleared_by_reload():
+    # loading range commands again drops the facts of the previous ones: recovery refuses until reloaded
+    w = synth.recovery_workload(5, n_range_cmds=12)
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        st.recovery_scan(w.queries, 3)
+        from accord_deps import native as N
+        import ctypes as C
+        N.lib().ad_range_cmds_load(st.h, C.byref(w.cmds.soa()))
+        with pytest.raises(native.AccordDepsError) as e:
+            st.recovery_scan(w.queries, 3)
+        assert e.value.code == A.AD_E_STATE
+    finally:
+        st.close()

@@ -12,20 +12,35 @@ import refmodel
 from test_oracle import _request
 
 
+@pytest.mark.parametrize("ranges", [False, True])
 @pytest.mark.parametrize("seed", range(8))
 @pytest.mark.parametrize("scan", A.RECOVER_SCANS)
-def test_recovery_crosscheck(oracle, seed, scan):
-    w = synth.recovery_workload(seed, with_slices=(seed % 3 == 2), start_inclusive=(seed % 4 == 1))
+def test_recovery_crosscheck(oracle, seed, scan, ranges):
+    w = synth.recovery_workload(seed, with_slices=(seed % 3 == 2), start_inclusive=(seed % 4 == 1),
+                                n_range_cmds=16 if ranges else 0)
     batch = oracle.recover(w, scan)
-    hits = 0
+    hits = rhits = 0
     for i in range(len(w.queries)):
         kd, dd = refmodel.recovery_pairs(w, i, scan)
+        rd = refmodel.recovery_range_pairs(w, i, scan)
         got = _request(batch, i)
-        assert got[1] == ([], [], [])                      # key-domain stores: no rangeDeps
-        for m, pairs in ((0, kd), (2, dd)):
+        for m, pairs in ((0, kd), (1, rd), (2, dd)):
             assert got[m] == tuple(refmodel.csr(pairs)), (seed, scan, i, A.MAP_NAMES[m])
         hits += len(kd) + len(dd)
+        rhits += len(rd)
     assert seed % 4 or hits > 0 or scan in (0, 2)          # the workloads reach the emitting branches
+
+
+
+def test_recovery_ranges_reach_every_scan(oracle):
+    # the range-command half emits in every scan over a few seeds
+    tot = {s: 0 for s in A.RECOVER_SCANS}
+    for seed in range(8):
+        w = synth.recovery_workload(seed, n_range_cmds=16)
+        for s in A.RECOVER_SCANS:
+            b = oracle.recover(w, s)
+            tot[s] += b.pair_count(1)
+    assert all(v > 0 for v in tot.values()), tot
 
 
 def test_recovery_branches_covered(oracle):
