@@ -23,6 +23,10 @@
 namespace adx {
 
 constexpr int LEAN_WAVES = 4;
+#ifndef LEAN_OCC_N
+#define LEAN_OCC_N 5
+#endif
+constexpr int LEAN_OCC = LEAN_OCC_N;        // waves per SIMD the register budget is sized for
 constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 constexpr uint32_t LEAN_CHUNK = 1u << 16;
 
@@ -107,7 +111,7 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
 // RNG: the store has range commands (with a stabbing index): each request also gets its
 // rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
 template <uint32_t RPW, bool RNG>
-__global__ __launch_bounds__(64 * LEAN_WAVES) void k_resolve_lean(DevSnapshot s, BatchBufs b, uint32_t pass)
+__global__ __launch_bounds__(64 * LEAN_WAVES, LEAN_OCC) void k_resolve_lean(DevSnapshot s, BatchBufs b, uint32_t pass)
 {
     // pass 1: all requests -> deferred1; pass 2: deferred1 -> deferred2 (lists derived from b
     // where used, so they hold no scalar registers across the loop)
