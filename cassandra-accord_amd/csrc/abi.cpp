@@ -199,6 +199,7 @@ struct ad_ctx {
     DevBuf d_dict_hi, d_dict_lo, d_dict_node, d_keys, d_krec, d_khash, d_kent, d_cand, d_cwr, d_ent, d_w;
     DevBuf d_lvl[NCLASS][MAX_LEVELS];
     DevBuf d_rstart, d_rend, d_rtxw, d_rrid, d_cell_E, d_cell_off, d_cell_ent;
+    uint64_t n_cell_ent = 0;                   // entries of d_cell_ent
     DevBuf d_rlvl[NCLASS][MAX_LEVELS];
     DevBuf d_rb_s, d_rb_e, d_rb_e0, d_rb_e1, d_rb_wm, d_rb_rid, d_slices_s, d_slices_e;
     DevBuf d_dict_lsb_raw, d_rt_start, d_rt_end;   // raw ids and range table (multi-GPU export)
@@ -277,6 +278,7 @@ struct ad_ctx {
     // them on demand (host_stale)
     DevBuf d_status, d_xrank, d_ekey;
     DevBuf d_ent2, d_status2, d_xrank2, d_ekey2;    // spare per-entry arrays (insertions)
+    DevBuf d_dict_hi2, d_dict_lo2, d_dict_node2, d_dict_raw2;   // spare dictionary arrays (merges)
     bool host_moved = false;                         // entries were inserted on the device
     DevBuf u_k, u_tm, u_tl, u_tn, u_em, u_el, u_en, u_st;
     CfkUpdWork* cu = nullptr;
@@ -682,6 +684,7 @@ static int build_snapshot(ad_ctx* c)
                     (rc = upload(c, c->d_cell_ent, ents)))
                     return rc;
                 cell_ok = true;
+                c->n_cell_ent = acc;
             }
         }
     }
@@ -910,6 +913,7 @@ static int build_snapshot(ad_ctx* c)
     s.cell_E = cell_ok ? c->d_cell_E.as<int64_t>() : nullptr;
     s.cell_off = cell_ok ? c->d_cell_off.as<uint32_t>() : nullptr;
     s.cell_ent = cell_ok ? c->d_cell_ent.as<uint64_t>() : nullptr;
+    if (!cell_ok) c->n_cell_ent = 0;
     s.r_start = c->d_rstart.as<int64_t>();
     s.r_end = c->d_rend.as<int64_t>();
     s.r_txw = c->d_rtxw.as<uint32_t>();
@@ -2611,6 +2615,61 @@ static int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, ui
     return size_cfk_trees(c, ne);
 }
 
+static int cfk_dict_spare(void* vc, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    if (!c->d_dict_hi2.ensure(8 * n + 8 * (n / 8)) || !c->d_dict_lo2.ensure(8 * n + 8 * (n / 8)) ||
+        !c->d_dict_node2.ensure(4 * n + 4 * (n / 8)) || !c->d_dict_raw2.ensure(8 * n + 8 * (n / 8)))
+        return AD_E_NOMEM;
+    *hi = c->d_dict_hi2.as<uint64_t>();
+    *lo = c->d_dict_lo2.as<uint64_t>();
+    *node = c->d_dict_node2.as<int32_t>();
+    *raw = c->d_dict_raw2.as<uint64_t>();
+    return 0;
+}
+
+static int cfk_dict_swap(void* vc, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    swap_buf(c->d_dict_hi, c->d_dict_hi2);
+    swap_buf(c->d_dict_lo, c->d_dict_lo2);
+    swap_buf(c->d_dict_node, c->d_dict_node2);
+    swap_buf(c->d_dict_lsb_raw, c->d_dict_raw2);
+    *hi = c->d_dict_hi.as<uint64_t>();
+    *lo = c->d_dict_lo.as<uint64_t>();
+    *node = c->d_dict_node.as<int32_t>();
+    *raw = c->d_dict_lsb_raw.as<uint64_t>();
+    return 0;
+}
+
+// After a dictionary merge on the device: the host dictionary copy and the host-side rank arrays
+// (r = 2i+1 -> 2(i + #{pos <= i}) + 1, the device remap)
+static int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipStream_t st)
+{
+    const uint64_t nd = c->ds.n_dict;
+    std::vector<uint64_t> pos(U);
+    c->dict_msb.resize(nd);
+    c->dict_lsb.resize(nd);
+    c->dict_node.resize(nd);
+    HIPCHK(c, hipMemcpyAsync(pos.data(), pos_dev, 8 * U, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(c->dict_node.data(), c->d_dict_node.p, 4 * nd, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    auto remap = [&](uint32_t r) -> uint32_t {
+        if (r == 0) return 0;
+        const uint64_t i = (r - 1) / 2;
+        return (uint32_t)(2 * (i + (uint64_t)(std::upper_bound(pos.begin(), pos.end(), i) - pos.begin())) + 1);
+    };
+    auto remap_txw = [&](uint32_t y) -> uint32_t { return (y & ~RANK_MASK) | remap(y & RANK_MASK); };
+    for (auto& r : c->h_txn_rank) r = remap(r);
+    for (auto& r : c->h_exec_rank) r = remap(r);
+    for (auto& r : c->h_pruned) r = remap(r);
+    for (auto& r : c->h_cmd_rank) r = remap(r);
+    for (auto& y : c->h_rtxw) y = remap_txw(y);
+    return 0;
+}
+
 static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats)
 {
     if (c->dirty)
@@ -2622,9 +2681,20 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
                      c->d_w.as<uint2>(), c->d_w.cap / 8};
     CfkUpdOut o;
     std::string e;
-    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries};
+    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_dict_spare, cfk_dict_swap,
+                       c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb};
     const uint64_t nd0 = c->dict_msb.size();
     const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e);
+    if (o.merged)
+    {
+        // ids merged into the device dictionary (they stay when the batch then failed): host copies
+        if (int rc2 = cfk_after_merge(c, o.merge_pos, o.n_new_ids, st)) return rc2;
+        drop_global_dict(c);
+        c->host_moved = true;        // entry ranks changed: host copies rebuilt from the device
+        c->host_stale = true;
+        ++c->snap_gen;
+    }
     if (c->ds.n_dict > nd0)
     {
         // ids appended to the device dictionary (kept even when the batch then failed): host copy
@@ -2648,10 +2718,10 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         }
     }
     if (o.n_inserted) c->host_moved = true;
-    if ((rc == 0 || o.rolled_back) && c->kline_slots)
+    if ((rc == 0 || o.rolled_back || o.rederived) && c->kline_slots)
         HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
                                    c->kline_slots, st));
-    if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back)
+    if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back && !o.rederived)
     {
         // the derived arrays may be half built: rebuild them from the entries at the next use
         c->host_stale = true;

@@ -14,11 +14,12 @@
 //   * w (committed Writes by executeAt), maxAppliedWriteByExecuteAt (:660-672), krec
 //   * the newest-probe emission lists cand / cwr and KeyEntry
 //   * the 64-ary max trees over tau (build_cfk_trees).
-// Insertion (:1002-1007) of a txnId newer than every id of its key is supported: ids newer than
-// every dictionary id are appended to the dictionary (no rank changes) and the new entries go at
-// the end of their keys' byId. An absent txnId older than its key's last id (a mid-segment insert),
-// or an id older than the newest dictionary id but unknown to it (a rank remap of every array), is
-// rejected with AD_E_STATE. A failed batch leaves the store unchanged.
+// Insertion (:1002-1007): an absent txnId is inserted at its byId position (-1 - binarySearch; the
+// per-entry arrays are rewritten once per batch with every key's new entries spliced in). Ids the
+// dictionary does not hold (txnIds and executeAts) join it first: appended when newer than all of
+// it (no rank changes), otherwise merged, which remaps every stored rank in place (monotone, so all
+// rank-sorted arrays stay sorted) before the batch is located. A failed batch leaves the store's
+// content unchanged (a merged dictionary stays: it adds ids, changes no answer).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,8 +49,9 @@ struct UpdCtl {
     unsigned long long applied;
     uint64_t tot[4];          // cand per class, committed entries
     uint64_t tot2[2];         // new dictionary ids (unique), inserted entries (groups)
-    uint32_t n_new, n_ins;    // ids newer than the dictionary, insertion updates
+    uint32_t n_new, n_ins;    // ids the dictionary does not hold, insertion updates
     unsigned long long diff[3];   // OR of (word ^ reference) over the new ids: node, lo, hi (sort digits)
+    uint32_t older, pad;      // a new id is older than the newest dictionary id (dictionary merge)
 };
 constexpr uint32_t LOC_NONE = 0xFFFFFFFFu;
 
@@ -146,9 +148,8 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds
         if ((s.ent[m].y & RANK_MASK) < r) lo = m + 1;
         else hi = m;
     }
+    // absent: inserted at -1 - binarySearch (:1002-1007), placed by insert_entries
     const bool present = lo < kr.seg_hi && (s.ent[lo].y & RANK_MASK) == r;
-    // absent: inserted at -1 - binarySearch (:1002-1007) when that is the end of byId
-    if (!present && kr.seg_hi > kr.seg_lo && r <= kr.last_txn) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
     const uint64_t el = u.exec_lsb[i];
     const uint32_t xr = dict_member_rank(s, ds, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
     if (!xr) { upd_fail(ctl, UE_NEW_EXEC, (uint32_t)i); return; }
@@ -174,8 +175,10 @@ __device__ inline bool newer_than_dict(const DevSnapshot& s, const NormTid& t)
     return norm_cmp(t, l) > 0;
 }
 
-// ids newer than every dictionary id (txnIds and executeAts): words for the LSD sort + raw lsb
-__global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, CfkUpdIn u, uint64_t* nw, uint64_t cap, UpdCtl* ctl)
+// ids the dictionary does not hold (txnIds and executeAts): words for the LSD sort + raw lsb;
+// ctl->older is set when one of them is older than the newest dictionary id (a merge, not an append)
+__global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, DictSample ds, CfkUpdIn u, uint64_t* nw, uint64_t cap,
+                                                     UpdCtl* ctl)
 {
     __shared__ unsigned long long red[3];
     if (threadIdx.x < 3) red[threadIdx.x] = 0;
@@ -189,7 +192,12 @@ __global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, CfkUpdIn u, 
         const uint64_t m = side ? u.exec_msb[i] : u.txn_msb[i], l = side ? u.exec_lsb[i] : u.txn_lsb[i];
         const int32_t nd = side ? u.exec_node[i] : u.txn_node[i];
         const NormTid t = norm_tid(m, l, nd);
-        if (!newer_than_dict(s, t)) continue;
+        if (!newer_than_dict(s, t))
+        {
+            uint64_t p;
+            if (dict_member_rank(s, ds, t, &p)) continue;
+            ctl->older = 1u;
+        }
         const uint32_t j = atomicAdd(&ctl->n_new, 1u);
         nw[j] = (uint64_t)((uint32_t)t.node ^ 0x80000000u);
         nw[cap + j] = t.lo;
@@ -255,6 +263,105 @@ __global__ void k_ins_append(const uint32_t* order, uint64_t m, const uint64_t* 
     draw[p] = nw[3 * cap + a];
 }
 
+// ---- dictionary merge: new ids older than the newest dictionary id ---------------------------
+// Every rank moves: old id i -> i + #{new ids below it}, new id j (sorted) -> pos[j] + j where pos[j]
+// = its lower bound among the old ids. The rank order is kept, so every rank-keyed array stays
+// sorted; the ranks stored in the per-entry state, krec and the range arrays are rewritten in
+// place and the derived arrays rebuilt from them.
+__global__ void k_merge_pos(DevSnapshot s, DictSample ds, uint64_t U, const uint64_t* uh, const uint64_t* ul,
+                            const int32_t* un, uint64_t* pos)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= U) return;
+    const NormTid t{uh[j], ul[j], un[j]};
+    uint64_t p;
+    (void)dict_member_rank(s, ds, t, &p);
+    pos[j] = p;
+}
+
+// #{j : pos[j] <= i} over the sorted merge positions (U is small: cache-resident)
+__device__ inline uint64_t merged_before(const uint64_t* pos, uint64_t U, uint64_t i)
+{
+    uint64_t lo = 0, hi = U;
+    while (lo < hi)
+    {
+        const uint64_t m = (lo + hi) >> 1;
+        if (pos[m] <= i) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+__device__ inline uint32_t remap_rank(uint32_t r, const uint64_t* pos, uint64_t U)
+{
+    if (r == 0) return 0;                       // NONE
+    const uint64_t i = (r - 1) >> 1;            // every stored rank is a member rank
+    return (uint32_t)(2 * (i + merged_before(pos, U, i)) + 1);
+}
+
+struct DictArrays { uint64_t* hi; uint64_t* lo; int32_t* node; uint64_t* raw; };
+
+__global__ __launch_bounds__(256) void k_merge_old(DevSnapshot s, const uint64_t* raw, const uint64_t* pos, uint64_t U, DictArrays nd)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= s.n_dict) return;
+    const uint64_t p = i + merged_before(pos, U, i);
+    nd.hi[p] = s.dict_hi[i];
+    nd.lo[p] = s.dict_lo[i];
+    nd.node[p] = s.dict_node[i];
+    nd.raw[p] = raw[i];
+}
+
+__global__ void k_merge_new(uint64_t U, const uint64_t* uh, const uint64_t* ul, const int32_t* un, const uint64_t* uraw,
+                            const uint64_t* pos, DictArrays nd)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= U) return;
+    const uint64_t p = pos[j] + j;
+    nd.hi[p] = uh[j];
+    nd.lo[p] = ul[j];
+    nd.node[p] = un[j];
+    nd.raw[p] = uraw[j];
+}
+
+__global__ __launch_bounds__(256) void k_remap_entries(uint64_t ne, uint2* ent, uint32_t* xrank, const uint64_t* pos, uint64_t U)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t y = ent[e].y;
+    ent[e].y = (y & ~RANK_MASK) | remap_rank(y & RANK_MASK, pos, U);
+    xrank[e] = remap_rank(xrank[e], pos, U);
+}
+
+__global__ void k_remap_krec(uint64_t nk, KeyRec* krec, const uint64_t* pos, uint64_t U)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    KeyRec kr = krec[k];
+    kr.last_txn = remap_rank(kr.last_txn, pos, U);
+    kr.last_wexec = remap_rank(kr.last_wexec, pos, U);
+    kr.pruned = remap_rank(kr.pruned, pos, U);
+    krec[k] = kr;
+}
+
+// txw words (rank | kind << RANK_BITS) of the range entries and stabbing cells, watermark ranks
+__global__ void k_remap_txw(uint64_t n, uint32_t* txw, const uint64_t* pos, uint64_t U)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t y = txw[i];
+    txw[i] = (y & ~RANK_MASK) | remap_rank(y & RANK_MASK, pos, U);
+}
+
+__global__ void k_remap_cells(uint64_t n, uint64_t* cell, const uint64_t* pos, uint64_t U)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t v = cell[i];
+    const uint32_t y = (uint32_t)v;
+    cell[i] = (v & 0xFFFFFFFF00000000ull) | ((y & ~RANK_MASK) | remap_rank(y & RANK_MASK, pos, U));
+}
+
 // insertion updates sorted by (key index, txn rank): group starts
 __global__ void k_ins_gflags(const uint64_t* ks, uint64_t q, uint32_t* gflag)
 {
@@ -295,27 +402,53 @@ __global__ void k_ins_before(uint64_t nk, const uint32_t* gkey, uint64_t G, uint
 
 struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; };
 
-__global__ __launch_bounds__(256) void k_ins_move_old(uint64_t ne, EntArrays a, const uint32_t* ib, EntArrays b)
+// an old entry moves up by the new entries before it: those of lower keys, and those of its key
+// with a lower rank (a mid-segment insert, :1002-1007)
+__global__ __launch_bounds__(256) void k_ins_move_old(uint64_t ne, EntArrays a, const uint32_t* ib, const uint32_t* grank,
+                                                      EntArrays b)
 {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= ne) return;
     const uint32_t k = a.ekey[e];
-    const uint64_t p = e + ib[k];
+    uint32_t lo = ib[k], hi = ib[k + 1];
+    if (lo < hi)
+    {
+        const uint32_t r = a.ent[e].y & RANK_MASK;
+        while (lo < hi)
+        {
+            const uint32_t m = (lo + hi) >> 1;
+            if (grank[m] < r) lo = m + 1;
+            else hi = m;
+        }
+    }
+    const uint64_t p = e + lo;
     b.ent[p] = a.ent[e];
     b.status[p] = a.status[e];
     b.xrank[p] = a.xrank[e];
     b.ekey[p] = k;
 }
 
+// a new entry lands after the old entries below it (its insertPos, -1 - binarySearch) and the new
+// entries before it (g)
 __global__ void k_ins_place(uint64_t G, const uint32_t* gkey, const uint32_t* grank, const unsigned long long* gword,
-                            const KeyRec* krec, CfkUpdIn u, const uint32_t* xr, EntArrays b)
+                            const KeyRec* krec, const uint2* old_ent, CfkUpdIn u, const uint32_t* xr, EntArrays b)
 {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= G) return;
     const uint32_t k = gkey[g];
     const unsigned long long wd = gword[g];
     const uint32_t i = (uint32_t)(0xFFFFFFFFull - (uint32_t)wd);
-    const uint64_t p = krec[k].seg_hi + g;
+    const KeyRec kr = krec[k];
+    uint32_t lo = kr.seg_lo, hi = kr.seg_hi;
+    if (kr.seg_hi > kr.seg_lo && grank[g] < kr.last_txn)
+        while (lo < hi)
+        {
+            const uint32_t m = (lo + hi) >> 1;
+            if ((old_ent[m].y & RANK_MASK) < grank[g]) lo = m + 1;
+            else hi = m;
+        }
+    else lo = kr.seg_hi;
+    const uint64_t p = (uint64_t)lo + g;
     const uint32_t kind = (uint32_t)((u.txn_lsb[i] >> 1) & 7);
     b.ent[p] = make_uint2(0u, grank[g] | (kind << RANK_BITS));
     b.status[p] = (uint8_t)(wd >> 32);
@@ -331,7 +464,7 @@ __global__ void k_ins_krec(uint64_t nk, const uint32_t* ib, const uint32_t* gran
     const uint32_t a = ib[k], b = ib[k + 1];
     kr.seg_lo += a;
     kr.seg_hi += b;
-    if (b > a) kr.last_txn = grank[b - 1];
+    if (b > a && grank[b - 1] > kr.last_txn) kr.last_txn = grank[b - 1];
     krec[k] = kr;
 }
 
@@ -511,6 +644,7 @@ struct CfkUpdWork {
     DBuf ctl, loc, xr, word, bk, flags, fs, bsum, ck, cv, ck2, cv2, hist, hoff, f2, s2, maw, wtail;
     DBuf sm_hi, sm_lo, sm_node;
     DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
+    DBuf mh, ml, mn, mraw, mpos;
     UpdCtl* h_ctl = nullptr;
     hipEvent_t ev[3] = {};
     ~CfkUpdWork()
@@ -623,14 +757,63 @@ static uint32_t key_rank_mask(uint64_t n_dict, uint64_t nk)
     return mask;
 }
 
-// Append the batch's ids newer than every dictionary id (sorted, unique) to the dictionary.
-static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, const CfkGrow& grow,
-                           hipStream_t st, CfkUpdOut* out, std::string* err)
+// Merge the sorted unique new ids (nflag/npos over the sorted order vs) into the dictionary: new
+// arrays (spare buffers), then every stored rank remapped in place.
+static int merge_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const DictSample& ds, const CfkGrow& grow,
+                            const uint32_t* vs, uint64_t m, uint64_t cap, uint64_t U, hipStream_t st, CfkUpdOut* out,
+                            std::string* err)
+{
+    const uint64_t n0 = s.n_dict, ne = s.n_ent, nk = s.n_keys;
+    UALLOC(w->mh, 8 * U, false);
+    UALLOC(w->ml, 8 * U, false);
+    UALLOC(w->mn, 4 * U, false);
+    UALLOC(w->mraw, 8 * U, false);
+    UALLOC(w->mpos, 8 * U, false);
+    uint64_t* mpos = w->mpos.as<uint64_t>();
+    k_ins_append<<<blocks(m), 256, 0, st>>>(vs, m, w->nw.as<uint64_t>(), cap, w->nflag.as<uint32_t>(), w->npos.as<uint64_t>(), 0,
+                                            w->mh.as<uint64_t>(), w->ml.as<uint64_t>(), w->mn.as<int32_t>(), w->mraw.as<uint64_t>());
+    k_merge_pos<<<blocks(U), 256, 0, st>>>(s, ds, U, w->mh.as<uint64_t>(), w->ml.as<uint64_t>(), w->mn.as<int32_t>(), mpos);
+    DictArrays nd{};
+    if (int rc = grow.dict_spare(grow.ctx, n0 + U, &nd.hi, &nd.lo, &nd.node, &nd.raw)) { *err = "dictionary merge"; return rc; }
+    if (n0) k_merge_old<<<blocks(n0), 256, 0, st>>>(s, d.dict_lsb_raw, mpos, U, nd);
+    k_merge_new<<<blocks(U), 256, 0, st>>>(U, w->mh.as<uint64_t>(), w->ml.as<uint64_t>(), w->mn.as<int32_t>(),
+                                           w->mraw.as<uint64_t>(), mpos, nd);
+    if (ne) k_remap_entries<<<blocks(ne), 256, 0, st>>>(ne, d.ent, d.xrank, mpos, U);
+    if (nk) k_remap_krec<<<blocks(nk), 256, 0, st>>>(nk, d.krec, mpos, U);
+    if (grow.n_rtxw) k_remap_txw<<<blocks(grow.n_rtxw), 256, 0, st>>>(grow.n_rtxw, grow.r_txw, mpos, U);
+    if (grow.n_cell_ent) k_remap_cells<<<blocks(grow.n_cell_ent), 256, 0, st>>>(grow.n_cell_ent, grow.cell_ent, mpos, U);
+    if (grow.n_rb) k_remap_txw<<<blocks(grow.n_rb), 256, 0, st>>>(grow.n_rb, grow.rb_wm, mpos, U);
+    UCHK(hipGetLastError());
+    if (int rc = grow.dict_swap(grow.ctx, &nd.hi, &nd.lo, &nd.node, &nd.raw)) { *err = "dictionary merge"; return rc; }
+    uint64_t lh = 0, ll = 0;
+    int32_t ln = 0;
+    UCHK(hipMemcpyAsync(&lh, nd.hi + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipMemcpyAsync(&ll, nd.lo + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipMemcpyAsync(&ln, nd.node + n0 + U - 1, 4, hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    s.dict_hi = nd.hi;
+    s.dict_lo = nd.lo;
+    s.dict_node = nd.node;
+    s.n_dict = n0 + U;
+    s.dict_last_hi = lh;
+    s.dict_last_lo = ll;
+    s.dict_last_node = ln;
+    d.dict_lsb_raw = nd.raw;
+    out->n_new_ids = U;
+    out->merged = true;
+    out->merge_pos = mpos;
+    return AD_OK;
+}
+
+// Add the batch's ids the dictionary does not hold (sorted, unique): appended when all are newer
+// than its newest id, merged otherwise.
+static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const DictSample& ds, const CfkUpdIn& u,
+                           const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err)
 {
     const uint64_t n = u.n, cap = 2 * n;
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
     UALLOC(w->nw, 8 * 4 * cap, false);
-    k_ins_collect<<<blocks(n), 256, 0, st>>>(s, u, w->nw.as<uint64_t>(), cap, ctl);
+    k_ins_collect<<<blocks(n), 256, 0, st>>>(s, ds, u, w->nw.as<uint64_t>(), cap, ctl);
     UCHK(hipGetLastError());
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
@@ -675,6 +858,7 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
     if (w->h_ctl->err) return AD_OK;          // reported by the caller
     const uint64_t U = w->h_ctl->tot2[0], n0 = s.n_dict;
     if (n0 + U > MAX_DICT) { *err = "id dictionary exceeds 2^28 entries"; return AD_E_CAPACITY; }
+    if (w->h_ctl->older) return merge_dictionary(w, s, d, ds, grow, vs, m, cap, U, st, out, err);
     uint64_t *dh, *dl, *draw;
     int32_t* dn;
     if (int rc = grow.dict(grow.ctx, n0, n0 + U, &dh, &dl, &dn, &draw)) { *err = "dictionary growth"; return rc; }
@@ -699,8 +883,8 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
     return AD_OK;
 }
 
-// Insert one entry per (key, txnId) group of the insertion updates at the end of its key's byId;
-// the per-entry arrays move to the spare buffers (the current ones stay intact for a rollback).
+// Insert one entry per (key, txnId) group of the insertion updates at its byId position; the
+// per-entry arrays move to the spare buffers (the current ones stay intact for a rollback).
 struct InsUndo {
     bool krec_saved = false;    // krec was saved to krec_bk and then changed
     bool swapped = false;       // the per-entry arrays were swapped to the spare buffers
@@ -752,9 +936,9 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     if (int rc = grow.entries(grow.ctx, ne + G, &b.ent, &b.status, &b.xrank, &b.ekey)) { *err = "entry growth"; return rc; }
     const uint64_t padded = std::max<uint64_t>(64, (ne + G + 63) / 64 * 64);
     if (padded > ne + G) UCHK(hipMemsetAsync(b.ent + ne + G, 0, sizeof(uint2) * (padded - ne - G), st));
-    if (ne) k_ins_move_old<<<blocks(ne), 256, 0, st>>>(ne, a, w->ib.as<uint32_t>(), b);
+    if (ne) k_ins_move_old<<<blocks(ne), 256, 0, st>>>(ne, a, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), b);
     k_ins_place<<<blocks(G), 256, 0, st>>>(G, w->gkey.as<uint32_t>(), w->grank.as<uint32_t>(), w->gword.as<unsigned long long>(),
-                                           d.krec, u, w->xr.as<uint32_t>(), b);
+                                           d.krec, a.ent, u, w->xr.as<uint32_t>(), b);
     if (nk)
     {
         UCHK(hipMemcpyAsync(w->krec_bk.p, d.krec, sizeof(KeyRec) * nk, hipMemcpyDeviceToDevice, st));
@@ -790,8 +974,8 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         {
             case UE_KEY: what = "key is not in the store's snapshot"; break;
             case UE_STATUS: what = "status is not an InternalStatus ordinal"; break;
-            case UE_ABSENT: what = "txnId is not in the key's CommandsForKey and not newer than its last id (insertion needs a snapshot load)"; rc = AD_E_STATE; break;
-            case UE_NEW_EXEC: what = "executeAt is neither an id of the snapshot nor newer than all of them (needs a snapshot load)"; rc = AD_E_STATE; break;
+            case UE_ABSENT: what = "txnId missing from the id dictionary after its merge (internal)"; rc = AD_E_STATE; break;
+            case UE_NEW_EXEC: what = "executeAt missing from the id dictionary after its merge (internal)"; rc = AD_E_STATE; break;
             case UE_FLAGS: what = "ids equal under Timestamp.equals differ in flag bits"; rc = AD_E_INCONSISTENT_ID; break;
             case UE_DOMAIN: what = "live range-domain TxnId in a CommandsForKey"; break;
             case UE_DUP_EXEC: what = "two committed entries of one key share an executeAt (CommandsForKey.java:1439)"; rc = AD_E_DUP_EXEC; break;
@@ -811,11 +995,14 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
     UCHK(hipEventRecord(w->ev[0], st));
 
-    // ---- 0. ids newer than the whole store join the dictionary (appended: no rank changes). A
-    // batch that then fails drops them again (the arrays keep the bytes; nothing refers to them).
+    // ---- 0. ids the dictionary does not hold join it. Ids newer than all of it are appended (no
+    // rank changes): a batch that then fails drops them again (the arrays keep the bytes; nothing
+    // refers to them). Older ones are merged with a rank remap of every stored rank: the merge
+    // stands when the batch then fails (it changes no content), and the derived arrays are rebuilt.
     const uint64_t nd0 = s.n_dict, lh0 = s.dict_last_hi, ll0 = s.dict_last_lo;
     const int32_t ln0 = s.dict_last_node;
     auto drop_new_ids = [&](int code) -> int {
+        if (out->merged) return code;
         s.n_dict = nd0;
         s.dict_last_hi = lh0;
         s.dict_last_lo = ll0;
@@ -823,18 +1010,35 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         out->n_new_ids = 0;
         return code;
     };
-    if (int rc = grow_dictionary(w, s, d, u, grow, st, out, err)) return rc == AD_E_CAPACITY ? drop_new_ids(rc) : rc;
-    if (w->h_ctl->err) return drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx));
+    UALLOC(w->sm_hi, 8 * std::max<uint64_t>((s.n_dict + n + n + SAMP - 1) / SAMP, 1), false);
+    UALLOC(w->sm_lo, 8 * std::max<uint64_t>((s.n_dict + n + n + SAMP - 1) / SAMP, 1), false);
+    UALLOC(w->sm_node, 4 * std::max<uint64_t>((s.n_dict + n + n + SAMP - 1) / SAMP, 1), false);
+    auto sample = [&]() -> DictSample {
+        const uint64_t n_samp = (s.n_dict + SAMP - 1) / SAMP;
+        if (n_samp)
+            k_dict_sample<<<blocks(n_samp), 256, 0, st>>>(s, w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(),
+                                                          w->sm_node.as<int32_t>(), n_samp);
+        return DictSample{w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(), w->sm_node.as<int32_t>(), n_samp};
+    };
+    // a failure after a merge: the entries are as they were, under the new ranks; derive again
+    auto rederive = [&](int code) -> int {
+        if (!out->merged) return code;
+        std::string e2;
+        if (hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st) != hipSuccess) { *err += "; re-derivation failed"; return AD_E_DEVICE; }
+        if (int rc2 = cfk_derive(w, s, d, bufs, need, need_ctx, st, &e2)) { *err += "; re-derivation: " + e2; return rc2; }
+        if (hipStreamSynchronize(st) != hipSuccess) { *err += "; re-derivation failed"; return AD_E_DEVICE; }
+        out->rederived = true;
+        return code;
+    };
+    {
+        const DictSample ds0 = sample();
+        if (int rc = grow_dictionary(w, s, d, ds0, u, grow, st, out, err))
+            return rc == AD_E_CAPACITY ? drop_new_ids(rc) : rederive(rc);
+    }
+    if (w->h_ctl->err) return rederive(drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx)));
 
     // ---- 1. locate and validate; nothing changes unless the whole batch is valid
-    const uint64_t n_samp = (s.n_dict + SAMP - 1) / SAMP;
-    UALLOC(w->sm_hi, 8 * std::max<uint64_t>(n_samp, 1), false);
-    UALLOC(w->sm_lo, 8 * std::max<uint64_t>(n_samp, 1), false);
-    UALLOC(w->sm_node, 4 * std::max<uint64_t>(n_samp, 1), false);
-    if (n_samp)
-        k_dict_sample<<<blocks(n_samp), 256, 0, st>>>(s, w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(),
-                                                      w->sm_node.as<int32_t>(), n_samp);
-    const DictSample dsm{w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(), w->sm_node.as<int32_t>(), n_samp};
+    const DictSample dsm = sample();
     k_upd_locate<<<blocks(n), 256, 0, st>>>(s, dsm, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
                                             w->word.as<unsigned long long>(), w->ins_k.as<uint64_t>(),
                                             w->ins_v.as<uint32_t>(), ctl);
@@ -845,7 +1049,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     {
         k_upd_release<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->word.as<unsigned long long>());
         UCHK(hipStreamSynchronize(st));
-        return drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx));
+        return rederive(drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx)));
     }
     const uint64_t q = w->h_ctl->n_ins, ne0 = s.n_ent;
     k_upd_apply<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(), w->word.as<unsigned long long>(),

@@ -19,9 +19,9 @@ struct CfkUpdIn {
     const uint8_t* status;
 };
 
-// Insertions: an update whose txnId the key's byId does not hold is inserted when its txnId is
-// newer than every id of the key (always true for an id newer than the whole store: a fresh
-// PreAccept); ids newer than every dictionary id are appended to the dictionary first.
+// Insertions: an update whose txnId the key's byId does not hold is inserted at its byId position;
+// ids the dictionary does not hold join it first (appended when newer than all of them, merged
+// with a rank remap otherwise).
 // Per-entry state kept on the device beside the derived snapshot (built by the ingest): the
 // InternalStatus and executeAt rank of every byId entry and the key index each entry belongs to.
 // The derived arrays (ent, cand, cwr, w, krec, kent, trees) are rebuilt from it after an update.
@@ -51,12 +51,26 @@ struct CfkGrow {
     // make the spare arrays current (commit = true) or current ones spare again (rollback) and size
     // the snapshot's trees for ne entries; returns the now-current arrays
     int (*swap)(void* ctx, uint64_t ne, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey);
+    // dictionary merge (new ids older than the newest one): spare dictionary arrays for n ids, and
+    // making them current (returns the now-current arrays)
+    int (*dict_spare)(void* ctx, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** lsb_raw);
+    int (*dict_swap)(void* ctx, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** lsb_raw);
+    // rank-holding arrays outside the per-entry state, rewritten by a merge: range entries' txw,
+    // stabbing cells (rid << 32 | txw), redundantBefore watermark ranks
+    uint32_t* r_txw; uint64_t n_rtxw;
+    uint64_t* cell_ent; uint64_t n_cell_ent;
+    uint32_t* rb_wm; uint64_t n_rb;
 };
 
 struct CfkUpdOut {
     uint64_t n_applied = 0;        // entries changed or inserted
     uint64_t n_inserted = 0;       // entries inserted
     uint64_t n_new_ids = 0;        // ids added to the dictionary
+    // a dictionary merge: every rank r = 2i+1 became 2(i + #{j : merge_pos[j] <= i}) + 1; the merge
+    // stands even when the batch then fails (the store's content is unchanged by it)
+    bool merged = false;
+    const uint64_t* merge_pos = nullptr;   // device, [n_new_ids] ascending
+    bool rederived = false;        // the derived arrays were rebuilt although the batch failed
     bool rolled_back = false;      // the batch failed after it had been applied and was undone
     double ms_locate = 0, ms_derive = 0, ms_total = 0;
 };

@@ -513,13 +513,13 @@ int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t sc
  * carried: "not above"); updates of one entry apply in batch order. committedByExecuteAt,
  * maxAppliedWriteByExecuteAt and every derived device array follow (:642-681).
  * The caller filters what the Java drops before the search (txnId < shardRedundantBefore, :995).
- * A txnId the key's byId does not hold is inserted (:1002-1007) when it is newer than the key's last
- * id (a fresh PreAccept); ids newer than every id of the store join the id dictionary.
- * Errors (nothing applied): AD_E_INVAL (key not in the snapshot, status > 7, live range-domain id),
- * AD_E_STATE (an absent txnId older than its key's last id, or an executeAt that is neither an id of
- * the snapshot nor newer than all of them: ad_cfk_load a new snapshot), AD_E_INCONSISTENT_ID,
- * AD_E_DUP_EXEC (two committed entries of a key with one executeAt, :1439). Ids appended to the
- * dictionary by a failed batch stay (they change no rank). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
+ * A txnId the key's byId does not hold is inserted at its byId position (:1002-1007, -1 - binarySearch).
+ * Ids the store's id dictionary does not hold (txnIds and executeAts) join it: appended when newer
+ * than every id of the store, otherwise merged, which renumbers every id rank on the device (a
+ * monotone remap: nothing is re-sorted). Errors (nothing applied): AD_E_INVAL (key not in the
+ * snapshot, status > 7, live range-domain id), AD_E_INCONSISTENT_ID, AD_E_DUP_EXEC (two committed
+ * entries of a key with one executeAt, :1439). Ids added to the dictionary by a failed batch stay
+ * (they change no answer). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
  * follow on demand. */
 typedef struct ad_cfk_update_soa {
     uint64_t n;

@@ -50,3 +50,27 @@ def fresh_preaccepts(cfk, rng, n_txns, max_keys=4, epoch=9, hlc0=1, statuses=(2,
 def concat(*us):
     return CfkUpdates(np.concatenate([u.keys for u in us]), Tids.concat([u.txn for u in us]),
                       Tids.concat([u.exec for u in us]), np.concatenate([u.status for u in us]))
+
+
+def older_inserts(cfk, rng, n, known_frac=0.3, new_exec_frac=0.3, statuses=range(8)):
+    """Insertions below the newest id of the store: txnIds next to existing ones (same msb and
+    flags, another node: ids the dictionary does not hold, landing mid-segment), and for
+    `known_frac` of them ids the store holds under another key. executeAt = txnId or, for
+    `new_exec_frac`, an unknown Timestamp next to an existing one."""
+    ne = cfk.n_entries
+    e = rng.integers(0, ne, n)
+    ek = entry_keys(cfk)
+    keys = rng.choice(cfk.keys, n)
+    known = rng.random(n) < known_frac
+    node = cfk.txn.node[e].astype(np.int64) + np.where(known, 0, 1000 + rng.integers(0, 50, n))
+    t = Tids(cfk.txn.msb[e].copy(), cfk.txn.lsb[e].copy(), node.astype(np.int32))
+    # a known id goes to a key that does not hold it (else it is an update of that entry)
+    keys = np.where(known & (keys == ek[e]), cfk.keys[(np.searchsorted(cfk.keys, ek[e]) + 1) % len(cfk.keys)], keys)
+    st = rng.choice(np.array(list(statuses), np.uint8), n)
+    rd = (t.lsb & np.uint64(1)) == 1
+    st[rd] = np.where(rng.random(int(rd.sum())) < 0.5, 0, 7).astype(np.uint8)
+    f = rng.integers(0, ne, n)
+    use_x = (rng.random(n) < new_exec_frac) & ~rd
+    x = Tids(np.where(use_x, cfk.exec.msb[f], t.msb), np.where(use_x, cfk.exec.lsb[f], t.lsb),
+             np.where(use_x, cfk.exec.node[f].astype(np.int64) + 3000 + np.arange(n), t.node).astype(np.int32))
+    return CfkUpdates(keys.astype(np.int64), t, x, st)
