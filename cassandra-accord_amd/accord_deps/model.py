@@ -91,6 +91,8 @@ class CfkSnapshot:
     # TxnInfo.missing() (CommandsForKey.java:332-341): ids of entry e are miss[miss_off[e]:miss_off[e+1]]
     miss_off: Optional[np.ndarray] = None        # u64 [n_entries+1]; None = every entry NO_TXNIDS
     miss: Optional[Tids] = None
+    # TxnInfo.ballot() per entry (TxnInfoExtra, CommandsForKey.java:273-283); None = Ballot.ZERO
+    ballot: Optional[Tids] = None
 
     def __post_init__(self):
         self.keys = A.as_i64(self.keys)
@@ -117,6 +119,13 @@ class CfkSnapshot:
         s.pruned_before = A.ptr(self.pruned_before)
         return s
 
+    def ballot_arrays(self):
+        """(msb, lsb, node) of the ballots for ad_cfk_ballots_load, or None."""
+        if self.ballot is None:
+            return None
+        return (np.ascontiguousarray(self.ballot.msb, np.uint64), np.ascontiguousarray(self.ballot.lsb, np.uint64),
+                np.ascontiguousarray(self.ballot.node, np.int32))
+
     def missing_soa(self):
         """AdCfkMissingSoa of the missing lists, or None when there are none."""
         if self.miss_off is None:
@@ -137,11 +146,13 @@ class CfkSnapshot:
 @dataclass
 class CfkUpdates:
     """A batch of CommandsForKey.update calls (ad_cfk_update_soa): update i raises txn[i] in the
-    CommandsForKey of keys[i] to status[i] with executeAt exec[i]."""
+    CommandsForKey of keys[i] to status[i] with executeAt exec[i] and the command's ballot
+    (acceptedOrCommitted; None = Ballot.ZERO)."""
     keys: np.ndarray          # i64
     txn: Tids
     exec: Tids
     status: np.ndarray        # u8 InternalStatus
+    ballot: Optional[Tids] = None
 
     def __post_init__(self):
         self.keys = A.as_i64(self.keys)
@@ -157,6 +168,8 @@ class CfkUpdates:
         s.txn_msb, s.txn_lsb, s.txn_node = A.ptr(self.txn.msb), A.ptr(self.txn.lsb), A.ptr(self.txn.node)
         s.exec_msb, s.exec_lsb, s.exec_node = A.ptr(self.exec.msb), A.ptr(self.exec.lsb), A.ptr(self.exec.node)
         s.status = A.ptr(self.status)
+        if self.ballot is not None:
+            s.ballot_msb, s.ballot_lsb, s.ballot_node = A.ptr(self.ballot.msb), A.ptr(self.ballot.lsb), A.ptr(self.ballot.node)
         return s
 
 

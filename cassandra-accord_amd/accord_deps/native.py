@@ -24,6 +24,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_copy_to_host", "ad_levels", "ad_levels_device", "ad_set_global_dict", "ad_preaccept_maps_load",
            "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_range_cmds_recovery_load", "ad_recovery_batch",
            "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries",
+           "ad_cfk_ballots_load", "ad_cfk_ballots",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange")
 
 
@@ -88,6 +89,9 @@ def lib():
         L.ad_cfk_update.argtypes = [C.c_void_p, C.POINTER(A.AdCfkUpdateSoa), C.POINTER(C.c_uint64), C.POINTER(A.AdStats)]
         L.ad_cfk_update_device.argtypes = [C.c_void_p, C.POINTER(A.AdCfkUpdateSoa), C.c_void_p, C.POINTER(C.c_uint64),
                                            C.POINTER(A.AdStats)]
+        L.ad_cfk_ballots_load.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.ad_cfk_ballots.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                     C.POINTER(C.c_void_p)]
         L.ad_cfk_entries.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.ad_exchange_local.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.POINTER(A.AdDepsResult)),
@@ -190,6 +194,9 @@ class DeviceCommandStore:
         self._check(L.ad_cfk_load(self.h, C.byref(workload.cfk.soa())))
         self._check(L.ad_range_cmds_load(self.h, C.byref(workload.cmds.soa())))
         self._check(L.ad_redundant_load(self.h, C.byref(workload.redundant.soa())))
+        ba = workload.cfk.ballot_arrays()
+        if ba is not None:
+            self._check(L.ad_cfk_ballots_load(self.h, len(ba[0]), A.ptr(ba[0]), A.ptr(ba[1]), A.ptr(ba[2])))
         ms = workload.cfk.missing_soa()
         if ms is not None:
             self._check(L.ad_cfk_missing_load(self.h, C.byref(ms)))
@@ -220,6 +227,14 @@ class DeviceCommandStore:
         k = n.value
         return _view(ps, k, np.uint8).copy(), Tids(_view(pm, k, np.uint64).copy(), _view(pl, k, np.uint64).copy(),
                                                    _view(pn, k, np.int32).copy())
+
+    def cfk_ballots(self):
+        """TxnInfo.ballot() of every entry as the store now holds them (Tids, load order)."""
+        n = C.c_uint64()
+        pm, pl, pn = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._check(lib().ad_cfk_ballots(self.h, C.byref(n), C.byref(pm), C.byref(pl), C.byref(pn)))
+        k = n.value
+        return Tids(_view(pm, k, np.uint64).copy(), _view(pl, k, np.uint64).copy(), _view(pn, k, np.int32).copy())
 
     def dictionary(self):
         n = C.c_uint64()
@@ -529,10 +544,14 @@ def device_updates(u, dev):
         return torch.from_numpy(np.ascontiguousarray(a).view(np.int64 if a.dtype.itemsize == 8 else
                                                               np.int32 if a.dtype.itemsize == 4 else np.uint8)).to(dev)
     arrs = [u.keys, u.txn.msb, u.txn.lsb, u.txn.node, u.exec.msb, u.exec.lsb, u.exec.node, u.status]
+    if u.ballot is not None:
+        arrs += [u.ballot.msb, u.ballot.lsb, u.ballot.node]
     t = [to_dev(a) for a in arrs]
     s = A.AdCfkUpdateSoa()
     s.n = len(u)
-    (s.keys, s.txn_msb, s.txn_lsb, s.txn_node, s.exec_msb, s.exec_lsb, s.exec_node, s.status) = [x.data_ptr() for x in t]
+    (s.keys, s.txn_msb, s.txn_lsb, s.txn_node, s.exec_msb, s.exec_lsb, s.exec_node, s.status) = [x.data_ptr() for x in t[:8]]
+    if u.ballot is not None:
+        s.ballot_msb, s.ballot_lsb, s.ballot_node = [x.data_ptr() for x in t[8:]]
     return s, t
 
 

@@ -166,6 +166,7 @@ struct ad_ctx {
         std::vector<int64_t> pruned;           // per key; -1 none
         std::vector<uint64_t> miss_off;        // TxnInfo.missing() per entry (ad_cfk_missing_load); empty = none
         std::vector<Tid> miss;
+        std::vector<Tid> ballot;               // TxnInfo.ballot() per entry; empty = all Ballot.ZERO
         bool miss_stale = false;               // SEQUENTIAL insertions moved the entries after the load
         bool loaded = false;
     } cfk;
@@ -280,7 +281,8 @@ struct ad_ctx {
     DevBuf d_ent2, d_status2, d_xrank2, d_ekey2;    // spare per-entry arrays (insertions)
     DevBuf d_dict_hi2, d_dict_lo2, d_dict_node2, d_dict_raw2;   // spare dictionary arrays (merges)
     bool host_moved = false;                         // entries were inserted on the device
-    DevBuf u_k, u_tm, u_tl, u_tn, u_em, u_el, u_en, u_st;
+    DevBuf u_k, u_tm, u_tl, u_tn, u_em, u_el, u_en, u_st, u_bm, u_bl, u_bn;
+    DevBuf d_ballot, d_ballot2;                      // TxnInfo.ballot() per entry (Bal), when the store has any
     CfkUpdWork* cu = nullptr;
     bool host_stale = false;
     std::vector<uint64_t> x_msb, x_lsb;        // ad_cfk_entries views
@@ -845,6 +847,14 @@ static int build_snapshot(ad_ctx* c)
         std::vector<uint32_t> ekey(std::max<uint64_t>(ne, 1), 0);
         for (uint64_t k = 0; k < nk; ++k)
             for (uint64_t e = K.seg[k]; e < K.seg[k + 1]; ++e) ekey[e] = (uint32_t)k;
+        if (!K.ballot.empty())
+        {
+            std::vector<Bal> bl(ne);
+            for (uint64_t e = 0; e < ne; ++e) bl[e] = Bal{K.ballot[e].msb, K.ballot[e].lsb, K.ballot[e].node, 0};
+            if ((rc = upload(c, c->d_ballot, bl))) return rc;
+        }
+        else
+            c->d_ballot.release();
         if ((rc = upload(c, c->d_status, K.status)) || (rc = upload(c, c->d_xrank, exec_rank)) || (rc = upload(c, c->d_ekey, ekey)))
             return rc;
     }
@@ -972,6 +982,14 @@ static int sync_host(ad_ctx* c)
 {
     if (!c->host_stale) return 0;
     auto& K = c->cfk;
+    if (c->d_ballot.p)
+    {
+        const uint64_t ne = c->ds.n_ent;
+        std::vector<Bal> bl(ne);
+        if (ne) HIPCHK(c, hipMemcpy(bl.data(), c->d_ballot.p, sizeof(Bal) * ne, hipMemcpyDeviceToHost));
+        K.ballot.resize(ne);
+        for (uint64_t e = 0; e < ne; ++e) K.ballot[e] = Tid{bl[e].msb, bl[e].lsb, bl[e].node};
+    }
     if (c->host_moved)
     {
         // entries were inserted: rebuild the host copies (byId ids from their ranks) from the device
@@ -1077,6 +1095,8 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
     std::vector<Tid> ntx, nex;
     std::vector<uint8_t> nst;
     std::vector<int64_t> npr;
+    std::vector<Tid> nbal;
+    const bool bal = !K.ballot.empty();
     size_t ki = 0, ii = 0;
     const size_t nk = K.keys.size();
     while (ki < nk || ii < ins.size())
@@ -1097,6 +1117,7 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
                 if ((int64_t)(e - K.seg[ki]) == pr) pr_new = (int64_t)(ntx.size() - base);
                 const bool same = ii < ins.size() && ins[ii].key == key && norm_cmp(norm(K.txn[e]), ins[ii].n) == 0;
                 ntx.push_back(K.txn[e]);
+                if (bal) nbal.push_back(K.ballot[e]);
                 if (same && K.status[e] < AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE)
                 {
                     nex.push_back(K.txn[e]);
@@ -1113,6 +1134,7 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
             else
             {
                 ntx.push_back(ins[ii].t);
+                if (bal) nbal.push_back(Tid{0, 0, 0});          // a PreAccept: Ballot.ZERO
                 nex.push_back(ins[ii].t);
                 nst.push_back(AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE);
                 ++ii;
@@ -1129,6 +1151,7 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
     K.exec.swap(nex);
     K.status.swap(nst);
     K.pruned.swap(npr);
+    K.ballot.swap(nbal);
     c->dirty = true;
     return 0;
 }
@@ -1599,6 +1622,9 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     K.miss_off.clear();
     K.miss.clear();
     K.miss_stale = false;
+    K.ballot.clear();
+    c->d_ballot.release();
+    c->d_ballot2.release();
     K.loaded = true;
     c->host_stale = false;       // the load replaces whatever ad_cfk_update applied on the device
     drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
@@ -2559,13 +2585,19 @@ static int cfk_grow_dict(void* vc, uint64_t n_old, uint64_t n_new, uint64_t** hi
     return 0;
 }
 
-static int cfk_grow_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek)
+static int cfk_grow_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal)
 {
     ad_ctx* c = (ad_ctx*)vc;
     const uint64_t padded = std::max<uint64_t>(64, (ne + 63) / 64 * 64);
     if (!grow_keep(c->d_ent2, 0, 8 * padded) || !grow_keep(c->d_status2, 0, ne) || !grow_keep(c->d_xrank2, 0, 4 * ne) ||
         !grow_keep(c->d_ekey2, 0, 4 * ne))
         return AD_E_NOMEM;
+    *bal = nullptr;
+    if (c->d_ballot.p)
+    {
+        if (!grow_keep(c->d_ballot2, 0, sizeof(Bal) * ne)) return AD_E_NOMEM;
+        *bal = c->d_ballot2.as<Bal>();
+    }
     *ent = c->d_ent2.as<uint2>();
     *st = c->d_status2.as<uint8_t>();
     *xr = c->d_xrank2.as<uint32_t>();
@@ -2601,18 +2633,29 @@ static int size_cfk_trees(ad_ctx* c, uint64_t ne)
     return 0;
 }
 
-static int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek)
+static int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal)
 {
     ad_ctx* c = (ad_ctx*)vc;
     swap_buf(c->d_ent, c->d_ent2);
     swap_buf(c->d_status, c->d_status2);
     swap_buf(c->d_xrank, c->d_xrank2);
     swap_buf(c->d_ekey, c->d_ekey2);
+    if (c->d_ballot.p) swap_buf(c->d_ballot, c->d_ballot2);
+    *bal = c->d_ballot.as<Bal>();
     *ent = c->d_ent.as<uint2>();
     *st = c->d_status.as<uint8_t>();
     *xr = c->d_xrank.as<uint32_t>();
     *ek = c->d_ekey.as<uint32_t>();
     return size_cfk_trees(c, ne);
+}
+
+static int cfk_ballot_init(void* vc, uint64_t ne, Bal** bal)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    if (!c->d_ballot.ensure(sizeof(Bal) * ne + sizeof(Bal) * (ne / 4))) return AD_E_NOMEM;
+    if (hipMemset(c->d_ballot.p, 0, sizeof(Bal) * ne) != hipSuccess) return AD_E_DEVICE;
+    *bal = c->d_ballot.as<Bal>();
+    return 0;
 }
 
 static int cfk_dict_spare(void* vc, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw)
@@ -2676,12 +2719,13 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         if (int rc = build_snapshot(c)) return rc;
     if (!c->cu) c->cu = cfk_upd_work_create();
     CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
-                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
+                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
+                  c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
     CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
                      c->d_w.as<uint2>(), c->d_w.cap / 8};
     CfkUpdOut o;
     std::string e;
-    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_dict_spare, cfk_dict_swap,
+    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
                        c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
                        c->d_rb_wm.as<uint32_t>(), c->ds.n_rb};
     const uint64_t nd0 = c->dict_msb.size();
@@ -2762,7 +2806,8 @@ int ad_cfk_update_device(ad_ctx* c, const ad_cfk_update_soa* u, void* stream, ui
 {
     if (!c) return AD_E_INVAL;
     if (int rc = check_update_soa(c, u)) return rc;
-    CfkUpdIn in{u->n, u->keys, u->txn_msb, u->txn_lsb, u->txn_node, u->exec_msb, u->exec_lsb, u->exec_node, u->status};
+    CfkUpdIn in{u->n, u->keys, u->txn_msb, u->txn_lsb, u->txn_node, u->exec_msb, u->exec_lsb, u->exec_node, u->status,
+                u->ballot_msb, u->ballot_lsb, u->ballot_node};
     return cfk_update_run(c, in, stream ? (hipStream_t)stream : c->stream, n_applied, stats);
 }
 
@@ -2775,7 +2820,13 @@ int ad_cfk_update(ad_ctx* c, const ad_cfk_update_soa* u, uint64_t* n_applied, ad
     CfkUpdIn in{n, stage_q(c, c->u_k, u->keys, n, &rc), stage_q(c, c->u_tm, u->txn_msb, n, &rc),
                 stage_q(c, c->u_tl, u->txn_lsb, n, &rc), stage_q(c, c->u_tn, u->txn_node, n, &rc),
                 stage_q(c, c->u_em, u->exec_msb, n, &rc), stage_q(c, c->u_el, u->exec_lsb, n, &rc),
-                stage_q(c, c->u_en, u->exec_node, n, &rc), stage_q(c, c->u_st, u->status, n, &rc)};
+                stage_q(c, c->u_en, u->exec_node, n, &rc), stage_q(c, c->u_st, u->status, n, &rc), nullptr, nullptr, nullptr};
+    if (u->ballot_msb)
+    {
+        in.bal_msb = stage_q(c, c->u_bm, u->ballot_msb, n, &rc);
+        in.bal_lsb = stage_q(c, c->u_bl, u->ballot_lsb, n, &rc);
+        in.bal_node = stage_q(c, c->u_bn, u->ballot_node, n, &rc);
+    }
     if (rc) return rc;
     return cfk_update_run(c, in, c->stream, n_applied, stats);
 }
@@ -2803,6 +2854,53 @@ int ad_cfk_entries(ad_ctx* c, uint64_t* n_entries, const uint8_t** status, const
     *exec_msb = c->x_msb.data();
     *exec_lsb = c->x_lsb.data();
     *exec_node = c->x_node.data();
+    return AD_OK;
+}
+
+int ad_cfk_ballots_load(ad_ctx* c, uint64_t n_entries, const uint64_t* msb, const uint64_t* lsb, const int32_t* node)
+{
+    if (!c || (n_entries && (!msb || !lsb || !node))) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (int rc = sync_host(c)) return rc;
+    auto& K = c->cfk;
+    if (n_entries != K.status.size()) return c->fail(AD_E_INVAL, "%llu ballots for %zu entries", (unsigned long long)n_entries, K.status.size());
+    K.ballot.resize(n_entries);
+    std::vector<Bal> bl(n_entries);
+    for (uint64_t e = 0; e < n_entries; ++e)
+    {
+        K.ballot[e] = Tid{msb[e], lsb[e], node[e]};
+        bl[e] = Bal{msb[e], lsb[e], node[e], 0};
+    }
+    if (!c->dirty)
+    {
+        if (int rc = upload(c, c->d_ballot, bl)) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return AD_OK;
+}
+
+int ad_cfk_ballots(ad_ctx* c, uint64_t* n_entries, const uint64_t** msb, const uint64_t** lsb, const int32_t** node)
+{
+    if (!c || !n_entries || !msb || !lsb || !node) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (int rc = sync_host(c)) return rc;
+    auto& K = c->cfk;
+    const uint64_t ne = K.status.size();
+    c->x_msb.assign(ne, 0);
+    c->x_lsb.assign(ne, 0);
+    c->x_node.assign(ne, 0);
+    for (uint64_t e = 0; e < ne && !K.ballot.empty(); ++e)
+    {
+        c->x_msb[e] = K.ballot[e].msb;
+        c->x_lsb[e] = K.ballot[e].lsb;
+        c->x_node[e] = K.ballot[e].node;
+    }
+    *n_entries = ne;
+    *msb = c->x_msb.data();
+    *lsb = c->x_lsb.data();
+    *node = c->x_node.data();
     return AD_OK;
 }
 

@@ -49,6 +49,7 @@ struct UpdCtl {
     unsigned long long applied;
     uint64_t tot[4];          // cand per class, committed entries
     uint64_t tot2[2];         // new dictionary ids (unique), inserted entries (groups)
+    uint64_t tot3[2];         // insertion updates, present updates (ballot fold)
     uint32_t n_new, n_ins;    // ids the dictionary does not hold, insertion updates
     unsigned long long diff[3];   // OR of (word ^ reference) over the new ids: node, lo, hi (sort digits)
     uint32_t older, pad;      // a new id is older than the newest dictionary id (dictionary merge)
@@ -110,15 +111,50 @@ __device__ inline uint32_t tau_of(uint32_t st, uint32_t kind, uint32_t xr)
     return TAU_NEVER_ELIDED;
 }
 
-// thread per update: key index, entry position, executeAt rank; claim the entry for the first
-// update of the highest status (packed u64 max: status, then the lowest update index)
+// InternalStatus flags (CommandsForKey.java:495-538)
+__device__ inline bool st_has_exec(uint32_t st) { return st >= AD_ST_ACCEPTED && st <= AD_ST_APPLIED; }
+__device__ inline bool st_has_ballot(uint32_t st)
+{
+    return st >= AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE && st <= AD_ST_COMMITTED;
+}
+__device__ inline bool st_has_info(uint32_t st)
+{
+    return st >= AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE && st <= AD_ST_APPLIED;
+}
+__device__ inline Bal upd_ballot(const CfkUpdIn& u, uint64_t i)
+{
+    if (!u.bal_msb) return Bal{0, 0, 0, 0};
+    return Bal{u.bal_msb[i], u.bal_lsb[i], u.bal_node[i], 0};
+}
+__device__ inline int bal_cmp(const Bal& a, const Bal& b)
+{
+    return norm_cmp(norm_tid(a.msb, a.lsb, a.node), norm_tid(b.msb, b.lsb, b.node));
+}
+// does an update (status st, the command's ballot b) replace an entry (cur, cb)? (:1018-1034)
+__device__ inline bool replaces(uint32_t st, uint32_t cur, const Bal& b, const Bal& cb)
+{
+    if (st > cur) return true;
+    if (st < cur)   // an invalidation outbidding an Accept
+        return st == AD_ST_PREACCEPTED_OR_ACCEPTED_INVALIDATE && cur == AD_ST_ACCEPTED && bal_cmp(b, cb) > 0;
+    return st_has_info(st) && bal_cmp(b, cb) > 0;
+}
+// the ballot a replacing TxnInfo keeps (TxnInfo.create :254-262)
+__device__ inline Bal kept_ballot(uint32_t st, const Bal& b) { return st_has_ballot(st) ? b : Bal{0, 0, 0, 0}; }
+
+// thread per update: key index, entry position, executeAt rank (the txnId's own rank unless the
+// status has an executeAt, TxnInfo.create :254-262). Without ballots the entry is claimed for the
+// first update of the highest status (packed u64 max: status, then the lowest update index); with
+// ballots the updates of an entry are folded in batch order by k_fold_present. Insertions are
+// flagged (ordered compaction by a scan).
 __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds, CfkDevState d, CfkUpdIn u, uint32_t* loc,
-                                                    uint32_t* xr_out, unsigned long long* word, uint64_t* ins_k,
-                                                    uint32_t* ins_v, UpdCtl* ctl)
+                                                    uint32_t* xr_out, unsigned long long* word, uint64_t* ins_key,
+                                                    uint32_t* flags, UpdCtl* ctl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= u.n) return;
     loc[i] = 0xFFFFFFFFu;
+    flags[i] = 0;                 // insertion
+    flags[u.n + i] = 0;           // present (ballot fold)
     const int64_t key = u.keys[i];
     uint32_t k = KEY_EMPTY;
     if (s.n_keys)
@@ -150,21 +186,25 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds
     }
     // absent: inserted at -1 - binarySearch (:1002-1007), placed by insert_entries
     const bool present = lo < kr.seg_hi && (s.ent[lo].y & RANK_MASK) == r;
-    const uint64_t el = u.exec_lsb[i];
-    const uint32_t xr = dict_member_rank(s, ds, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
-    if (!xr) { upd_fail(ctl, UE_NEW_EXEC, (uint32_t)i); return; }
-    if (d.dict_lsb_raw[p] != el) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
+    uint32_t xr = r;
+    if (st_has_exec(st))
+    {
+        const uint64_t el = u.exec_lsb[i];
+        xr = dict_member_rank(s, ds, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
+        if (!xr) { upd_fail(ctl, UE_NEW_EXEC, (uint32_t)i); return; }
+        if (d.dict_lsb_raw[p] != el) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
+    }
     if ((tl & 1) && tau_of(st, (uint32_t)((tl >> 1) & 7), xr) != 0) { upd_fail(ctl, UE_DOMAIN, (uint32_t)i); return; }
     xr_out[i] = xr;
     if (!present)
     {
-        const uint32_t j = atomicAdd(&ctl->n_ins, 1u);
-        ins_k[j] = ((uint64_t)k << 32) | r;
-        ins_v[j] = (uint32_t)i;
+        ins_key[i] = ((uint64_t)k << 32) | r;
+        flags[i] = 1;
         return;
     }
     loc[i] = lo;
-    atomicMax(word + lo, ((unsigned long long)st << 32) | (0xFFFFFFFFull - i));
+    if (u.bal_msb) flags[u.n + i] = 1;
+    else atomicMax(word + lo, ((unsigned long long)st << 32) | (0xFFFFFFFFull - i));
 }
 
 // ---- insertion ------------------------------------------------------------------------------
@@ -189,6 +229,7 @@ __global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, DictSample d
     unsigned long long d0 = 0, d1 = 0, d2 = 0;
     for (int side = 0; side < 2 && i < u.n; ++side)
     {
+        if (side && !st_has_exec(u.status[i])) break;      // executeAt = txnId (TxnInfo.create)
         const uint64_t m = side ? u.exec_msb[i] : u.txn_msb[i], l = side ? u.exec_lsb[i] : u.txn_lsb[i];
         const int32_t nd = side ? u.exec_node[i] : u.txn_node[i];
         const NormTid t = norm_tid(m, l, nd);
@@ -369,6 +410,75 @@ __global__ void k_ins_gflags(const uint64_t* ks, uint64_t q, uint32_t* gflag)
     if (j < q) gflag[j] = (j == 0 || ks[j] != ks[j - 1]) ? 1u : 0u;
 }
 
+// ordered compaction of the flagged updates (flags[i], exclusive prefix pos[i]): key, update index
+__global__ void k_compact(uint64_t n, const uint32_t* flags, const uint64_t* pos, const uint64_t* key, const uint32_t* loc,
+                          uint64_t* ks, uint32_t* vs)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flags[i]) return;
+    ks[pos[i]] = key ? key[i] : (uint64_t)loc[i];
+    vs[pos[i]] = (uint32_t)i;
+}
+
+// with ballots: the updates of one present entry (sorted by entry, batch order within) fold in
+// order through CommandsForKey.update's replacement test; the entry's old state is kept at its
+// first update's index for a rollback
+__global__ void k_fold_present(uint64_t m, const uint64_t* ks, const uint32_t* vs, CfkUpdIn u, const uint32_t* xr,
+                               CfkDevState d, uint2* bk, Bal* bkb, UpdCtl* ctl)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m || (j > 0 && ks[j - 1] == ks[j])) return;
+    const uint32_t e = (uint32_t)ks[j];
+    uint32_t st = d.status[e], x = d.xrank[e];
+    Bal b = d.ballot[e];
+    unsigned long long cnt = 0;
+    for (uint64_t t = j; t < m && ks[t] == e; ++t)
+    {
+        const uint32_t i = vs[t], ns = u.status[i];
+        const Bal nb = upd_ballot(u, i);
+        if (!replaces(ns, st, nb, b)) continue;
+        st = ns;
+        x = xr[i];
+        b = kept_ballot(ns, nb);
+        ++cnt;
+    }
+    if (!cnt) return;
+    const uint32_t i0 = vs[j];
+    bk[i0] = make_uint2(d.status[e], d.xrank[e]);
+    bkb[i0] = d.ballot[e];
+    d.status[e] = (uint8_t)st;
+    d.xrank[e] = x;
+    d.ballot[e] = b;
+    atomicAdd(&ctl->applied, cnt);
+}
+
+// per group (one new entry), with ballots: the group's updates fold in batch order (the first
+// inserts); gword = final status << 32 | ~(update index the entry takes executeAt and ballot from)
+__global__ void k_ins_fold(const uint64_t* ks, const uint32_t* vs, uint64_t q, const uint32_t* gflag, const uint64_t* gs,
+                           CfkUpdIn u, unsigned long long* gword, uint32_t* gkey, uint32_t* grank, UpdCtl* ctl)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= q || !gflag[j]) return;
+    const uint64_t g = gs[j];
+    gkey[g] = (uint32_t)(ks[j] >> 32);
+    grank[g] = (uint32_t)ks[j];
+    uint32_t il = vs[j], st = u.status[il];
+    Bal b = kept_ballot(st, upd_ballot(u, il));
+    unsigned long long cnt = 0;
+    for (uint64_t t = j + 1; t < q && ks[t] == ks[j]; ++t)
+    {
+        const uint32_t i = vs[t], ns = u.status[i];
+        const Bal nb = upd_ballot(u, i);
+        if (!replaces(ns, st, nb, b)) continue;
+        st = ns;
+        il = i;
+        b = kept_ballot(ns, nb);
+        ++cnt;
+    }
+    gword[g] = ((unsigned long long)st << 32) | (0xFFFFFFFFull - il);
+    if (cnt) atomicAdd(&ctl->applied, cnt);
+}
+
 // per group (one new entry): the first update of the highest status wins (batch order)
 __global__ void k_ins_claim(const uint64_t* ks, const uint32_t* vs, uint64_t q, const uint32_t* gflag, const uint64_t* gs,
                             const uint8_t* status, unsigned long long* gword, uint32_t* gkey, uint32_t* grank)
@@ -400,7 +510,7 @@ __global__ void k_ins_before(uint64_t nk, const uint32_t* gkey, uint64_t G, uint
     ib[k] = (uint32_t)lo;
 }
 
-struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; };
+struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; Bal* bal; };
 
 // an old entry moves up by the new entries before it: those of lower keys, and those of its key
 // with a lower rank (a mid-segment insert, :1002-1007)
@@ -426,6 +536,7 @@ __global__ __launch_bounds__(256) void k_ins_move_old(uint64_t ne, EntArrays a, 
     b.status[p] = a.status[e];
     b.xrank[p] = a.xrank[e];
     b.ekey[p] = k;
+    if (b.bal) b.bal[p] = a.bal[e];
 }
 
 // a new entry lands after the old entries below it (its insertPos, -1 - binarySearch) and the new
@@ -454,6 +565,7 @@ __global__ void k_ins_place(uint64_t G, const uint32_t* gkey, const uint32_t* gr
     b.status[p] = (uint8_t)(wd >> 32);
     b.xrank[p] = xr[i];
     b.ekey[p] = k;
+    if (b.bal) b.bal[p] = kept_ballot((uint32_t)(wd >> 32), upd_ballot(u, i));
 }
 
 __global__ void k_ins_krec(uint64_t nk, const uint32_t* ib, const uint32_t* grank, KeyRec* krec)
@@ -478,11 +590,10 @@ __global__ void k_upd_release(uint64_t n, const uint32_t* loc, unsigned long lon
 // the claiming update of each entry applies if its status is above the entry's; the entry's old
 // state is kept in bk[i] for a rollback
 __global__ void k_upd_apply(uint64_t n, const uint32_t* loc, const uint32_t* xr, unsigned long long* word,
-                            CfkDevState d, uint2* bk, UpdCtl* ctl)
+                            CfkDevState d, uint2* bk, Bal* bkb, UpdCtl* ctl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    bk[i] = make_uint2(0xFFFFFFFFu, 0);
     const uint32_t e = loc[i];
     if (e == LOC_NONE) return;                 // an insertion
     const unsigned long long wd = word[e];
@@ -494,15 +605,22 @@ __global__ void k_upd_apply(uint64_t n, const uint32_t* loc, const uint32_t* xr,
     bk[i] = make_uint2(cur, d.xrank[e]);
     d.status[e] = (uint8_t)st;
     d.xrank[e] = xr[i];
+    if (d.ballot)
+    {
+        // the batch carries Ballot.ZERO: the replacing TxnInfo has no ballot
+        bkb[i] = d.ballot[e];
+        d.ballot[e] = Bal{0, 0, 0, 0};
+    }
     atomicAdd(&ctl->applied, 1ull);
 }
 
-__global__ void k_upd_rollback(uint64_t n, const uint32_t* loc, const uint2* bk, CfkDevState d)
+__global__ void k_upd_rollback(uint64_t n, const uint32_t* loc, const uint2* bk, const Bal* bkb, CfkDevState d)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || bk[i].x == 0xFFFFFFFFu) return;
     d.status[loc[i]] = (uint8_t)bk[i].x;
     d.xrank[loc[i]] = bk[i].y;
+    if (d.ballot) d.ballot[loc[i]] = bkb[i];
 }
 
 // ---- derivation (thread per entry): tau, never-elided class flags, committed flag
@@ -645,6 +763,7 @@ struct CfkUpdWork {
     DBuf sm_hi, sm_lo, sm_node;
     DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
     DBuf mh, ml, mn, mraw, mpos;
+    DBuf bkb, uflag, upos;
     UpdCtl* h_ctl = nullptr;
     hipEvent_t ev[3] = {};
     ~CfkUpdWork()
@@ -905,13 +1024,12 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     UALLOC(w->bsum, 8 * ((std::max(hist_n, q) + 1023) / 1024 + 8), false);
     UALLOC(w->gflag, 4 * q, false);
     UALLOC(w->gs, 8 * (q + 1), false);
-    UCHK(hipMemcpyAsync(w->ck.p, w->ins_k.p, 8 * q, hipMemcpyDeviceToDevice, st));
-    UCHK(hipMemcpyAsync(w->cv.p, w->ins_v.p, 4 * q, hipMemcpyDeviceToDevice, st));
+    // ck / cv hold the insertion updates in batch order (k_compact)
     uint64_t* ks = w->ck.as<uint64_t>();
     uint32_t* vs = w->cv.as<uint32_t>();
     if (q > 1)
     {
-        // sort the update indices first so equal (key, txnId) groups keep batch order
+        // stable: equal (key, txnId) groups keep batch order
         UCHK(radix_sort_pairs(ks, vs, w->ck2.as<uint64_t>(), w->cv2.as<uint32_t>(), q, key_rank_mask(s.n_dict, nk),
                               w->hist.as<uint32_t>(), w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
     }
@@ -928,12 +1046,16 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     UALLOC(w->ib, 4 * (nk + 1), false);
     UALLOC(w->krec_bk, sizeof(KeyRec) * std::max<uint64_t>(nk, 1), false);
     UCHK(hipMemsetAsync(w->gword.p, 0, 8 * G, st));
-    k_ins_claim<<<blocks(q), 256, 0, st>>>(ks, vs, q, w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), u.status,
-                                           w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>());
+    if (u.bal_msb)
+        k_ins_fold<<<blocks(q), 256, 0, st>>>(ks, vs, q, w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), u,
+                                              w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>(), ctl);
+    else
+        k_ins_claim<<<blocks(q), 256, 0, st>>>(ks, vs, q, w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), u.status,
+                                               w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>());
     k_ins_before<<<blocks(nk + 1), 256, 0, st>>>(nk, w->gkey.as<uint32_t>(), G, w->ib.as<uint32_t>());
     UCHK(hipGetLastError());
-    EntArrays a{d.ent, d.status, d.xrank, d.ekey}, b{};
-    if (int rc = grow.entries(grow.ctx, ne + G, &b.ent, &b.status, &b.xrank, &b.ekey)) { *err = "entry growth"; return rc; }
+    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot}, b{};
+    if (int rc = grow.entries(grow.ctx, ne + G, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal)) { *err = "entry growth"; return rc; }
     const uint64_t padded = std::max<uint64_t>(64, (ne + G + 63) / 64 * 64);
     if (padded > ne + G) UCHK(hipMemsetAsync(b.ent + ne + G, 0, sizeof(uint2) * (padded - ne - G), st));
     if (ne) k_ins_move_old<<<blocks(ne), 256, 0, st>>>(ne, a, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), b);
@@ -946,7 +1068,7 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
         k_ins_krec<<<blocks(nk), 256, 0, st>>>(nk, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), d.krec);
     }
     UCHK(hipGetLastError());
-    const int src = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey);
+    const int src = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot);
     undo->swapped = true;         // the buffers are exchanged even when sizing the trees then failed
     if (src) { *err = "entry swap"; return src; }
     s.ent = d.ent;
@@ -1039,10 +1161,17 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
 
     // ---- 1. locate and validate; nothing changes unless the whole batch is valid
     const DictSample dsm = sample();
+    const bool bm = u.bal_msb != nullptr;
+    const int nf = bm ? 2 : 1;
+    UALLOC(w->uflag, 4ull * 2 * n, false);
+    UALLOC(w->upos, 8ull * 2 * (n + 1), false);
+    UALLOC(w->bsum, 8ull * 2 * ((n + 1023) / 1024 + 8), false);
     k_upd_locate<<<blocks(n), 256, 0, st>>>(s, dsm, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
                                             w->word.as<unsigned long long>(), w->ins_k.as<uint64_t>(),
-                                            w->ins_v.as<uint32_t>(), ctl);
+                                            w->uflag.as<uint32_t>(), ctl);
     UCHK(hipGetLastError());
+    UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), n, nf, w->bsum.as<uint64_t>(), st));
+    k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), n, nf, ctl->tot3);
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
     if (w->h_ctl->err)
@@ -1051,10 +1180,49 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         UCHK(hipStreamSynchronize(st));
         return rederive(drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx)));
     }
-    const uint64_t q = w->h_ctl->n_ins, ne0 = s.n_ent;
-    k_upd_apply<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(), w->word.as<unsigned long long>(),
-                                           d, w->bk.as<uint2>(), ctl);
+    const uint64_t q = w->h_ctl->tot3[0], mp = bm ? w->h_ctl->tot3[1] : 0, ne0 = s.n_ent;
+    // the batch's first ballots: the store's entries all hold Ballot.ZERO until now
+    if (bm && !d.ballot && ne0)
+        if (int rc = grow.ballot_init(grow.ctx, ne0, &d.ballot)) { *err = "ballot array"; return rederive(drop_new_ids(rc)); }
+    const uint64_t cq = std::max<uint64_t>(std::max(q, mp), 1);
+    UALLOC(w->ck, 8 * cq, false);
+    UALLOC(w->cv, 4 * cq, false);
+    UALLOC(w->ck2, 8 * cq, false);
+    UALLOC(w->cv2, 4 * cq, false);
+    UALLOC(w->bkb, sizeof(Bal) * n, false);
+    UCHK(hipMemsetAsync(w->bk.p, 0xFF, 8 * n, st));          // bk[i].x = none: nothing to roll back
+    if (bm)
+    {
+        if (mp)
+        {
+            // the present entries' updates, sorted by entry (stable: batch order within), folded
+            uint64_t* ks = w->ck.as<uint64_t>();
+            uint32_t* vs = w->cv.as<uint32_t>();
+            k_compact<<<blocks(n), 256, 0, st>>>(n, w->uflag.as<uint32_t>() + n, w->upos.as<uint64_t>() + (n + 1), nullptr,
+                                                 w->loc.as<uint32_t>(), ks, vs);
+            if (mp > 1)
+            {
+                const uint64_t hist_n = radix_hist_entries(mp);
+                UALLOC(w->hist, 4 * hist_n, false);
+                UALLOC(w->hoff, 8 * (hist_n + 1), false);
+                UALLOC(w->bsum, 8 * ((std::max(hist_n, mp) + 1023) / 1024 + 8), false);
+                uint32_t mask = 0;
+                for (uint32_t b = 0; b < bytes_of(ne0 ? ne0 - 1 : 0) && b < 4; ++b) mask |= 1u << b;
+                if (mask)
+                    UCHK(radix_sort_pairs(ks, vs, w->ck2.as<uint64_t>(), w->cv2.as<uint32_t>(), mp, mask, w->hist.as<uint32_t>(),
+                                          w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
+            }
+            k_fold_present<<<blocks(mp), 256, 0, st>>>(mp, ks, vs, u, w->xr.as<uint32_t>(), d, w->bk.as<uint2>(),
+                                                       w->bkb.as<Bal>(), ctl);
+        }
+    }
+    else
+        k_upd_apply<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(), w->word.as<unsigned long long>(),
+                                               d, w->bk.as<uint2>(), w->bkb.as<Bal>(), ctl);
     UCHK(hipGetLastError());
+    if (q)   // the insertion updates in batch order, for insert_entries
+        k_compact<<<blocks(n), 256, 0, st>>>(n, w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), w->ins_k.as<uint64_t>(),
+                                             nullptr, w->ck.as<uint64_t>(), w->cv.as<uint32_t>());
     // From here on the per-entry state has changed: every failure undoes the batch (status and
     // executeAt restored, insertions swapped back, krec restored) and derives the previous state
     // again, so that nothing changes unless the whole batch is applied.
@@ -1063,14 +1231,14 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         std::string e2;
         if (undo.swapped)
         {
-            if (grow.swap(grow.ctx, ne0, &d.ent, &d.status, &d.xrank, &d.ekey)) { *err += "; rollback failed"; return AD_E_DEVICE; }
+            if (grow.swap(grow.ctx, ne0, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot)) { *err += "; rollback failed"; return AD_E_DEVICE; }
             s.ent = d.ent;
             s.n_ent = ne0;
         }
         if (undo.krec_saved && s.n_keys)
             if (hipMemcpyAsync(d.krec, w->krec_bk.p, sizeof(KeyRec) * s.n_keys, hipMemcpyDeviceToDevice, st) != hipSuccess)
             { *err += "; rollback failed"; return AD_E_DEVICE; }
-        k_upd_rollback<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->bk.as<uint2>(), d);
+        k_upd_rollback<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->bk.as<uint2>(), w->bkb.as<Bal>(), d);
         if (hipGetLastError() != hipSuccess || hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st) != hipSuccess)
         { *err += "; rollback failed"; return AD_E_DEVICE; }
         if (int rc2 = cfk_derive(w, s, d, bufs, need, need_ctx, st, &e2)) { *err += "; rollback: " + e2; return rc2; }

@@ -17,6 +17,14 @@ struct CfkUpdIn {
     const uint64_t* txn_msb; const uint64_t* txn_lsb; const int32_t* txn_node;
     const uint64_t* exec_msb; const uint64_t* exec_lsb; const int32_t* exec_node;
     const uint8_t* status;
+    // the command's ballot (acceptedOrCommitted) per update; null = Ballot.ZERO for every update
+    const uint64_t* bal_msb; const uint64_t* bal_lsb; const int32_t* bal_node;
+};
+
+// TxnInfo.ballot() of an entry (raw Timestamp fields; zero = Ballot.ZERO)
+struct Bal {
+    uint64_t msb, lsb;
+    int32_t node, pad;
 };
 
 // Insertions: an update whose txnId the key's byId does not hold is inserted at its byId position;
@@ -30,6 +38,7 @@ struct CfkDevState {
     uint32_t* xrank;               // [n_ent] executeAt rank
     uint32_t* ekey;                // [n_ent] key index
     uint64_t* dict_lsb_raw;  // [n_dict] raw lsb of every dictionary id (flag-bit identity check)
+    Bal* ballot;             // [n_ent] or null: every entry's ballot is Ballot.ZERO
     // derived arrays rewritten in place (the snapshot's const views alias them)
     uint2* ent; KeyRec* krec; KeyEntry* kent;
 };
@@ -46,11 +55,14 @@ struct CfkGrow {
     void* ctx;
     // dictionary arrays with room for n_new ids, the first n_old kept
     int (*dict)(void* ctx, uint64_t n_old, uint64_t n_new, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** lsb_raw);
-    // spare per-entry arrays for ne_new entries (ent padded to whole 64-entry frames)
-    int (*entries)(void* ctx, uint64_t ne_new, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey);
+    // spare per-entry arrays for ne_new entries (ent padded to whole 64-entry frames); *bal only
+    // when the store holds ballots (else left null)
+    int (*entries)(void* ctx, uint64_t ne_new, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey, Bal** bal);
     // make the spare arrays current (commit = true) or current ones spare again (rollback) and size
     // the snapshot's trees for ne entries; returns the now-current arrays
-    int (*swap)(void* ctx, uint64_t ne, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey);
+    int (*swap)(void* ctx, uint64_t ne, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey, Bal** bal);
+    // the store's first ballots: a zeroed (Ballot.ZERO) array for ne entries
+    int (*ballot_init)(void* ctx, uint64_t ne, Bal** bal);
     // dictionary merge (new ids older than the newest one): spare dictionary arrays for n ids, and
     // making them current (returns the now-current arrays)
     int (*dict_spare)(void* ctx, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** lsb_raw);

@@ -508,9 +508,13 @@ int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t sc
 /* ---- device-resident CommandsForKey maintenance ----------------------------
  * CommandsForKey.update (CommandsForKey.java:972-1042) for a batch of status transitions, applied to
  * the snapshot in HBM (no host ingest, no re-upload). Update i raises the byId entry of txnId i in
- * the CommandsForKey of keys[i] to InternalStatus status[i] with executeAt i: the entry changes iff
- * the new status is above its current one (:1012-1027; equal status with a higher ballot is not
- * carried: "not above"); updates of one entry apply in batch order. committedByExecuteAt,
+ * the CommandsForKey of keys[i] to InternalStatus status[i] with executeAt i and the command's
+ * ballot (acceptedOrCommitted) i. The entry is replaced (:1013-1036) iff the new status is above its
+ * current one, or equal with status.hasInfo and a ballot above the entry's TxnInfo.ballot(), or is
+ * PREACCEPTED_OR_ACCEPTED_INVALIDATE over ACCEPTED with a higher ballot; the replacing TxnInfo
+ * (TxnInfo.create :254-262) keeps executeAt i only when the status has an executeAt (ACCEPTED ..
+ * APPLIED; txnId otherwise) and the ballot only when it has a ballot (PREACCEPTED_OR_ACCEPTED_INVALIDATE
+ * .. COMMITTED; Ballot.ZERO otherwise). Updates of one entry apply in batch order. committedByExecuteAt,
  * maxAppliedWriteByExecuteAt and every derived device array follow (:642-681).
  * The caller filters what the Java drops before the search (txnId < shardRedundantBefore, :995).
  * A txnId the key's byId does not hold is inserted at its byId position (:1002-1007, -1 - binarySearch).
@@ -531,6 +535,9 @@ typedef struct ad_cfk_update_soa {
     const uint64_t* exec_lsb;
     const int32_t*  exec_node;
     const uint8_t*  status;          /* AD_ST_* = InternalStatus.from(command.saveStatus()) */
+    const uint64_t* ballot_msb;      /* command.acceptedOrCommitted(); all three NULL = Ballot.ZERO */
+    const uint64_t* ballot_lsb;
+    const int32_t*  ballot_node;
 } ad_cfk_update_soa;
 
 /* Host buffers (staged to the device). n_applied (may be null): updates that changed an entry;
@@ -543,6 +550,12 @@ int ad_cfk_update_device(ad_ctx* ctx, const ad_cfk_update_soa* u_dev, void* stre
  * the context, valid until its next call. */
 int ad_cfk_entries(ad_ctx* ctx, uint64_t* n_entries, const uint8_t** status, const uint64_t** exec_msb,
                    const uint64_t** exec_lsb, const int32_t** exec_node);
+/* TxnInfo.ballot() of every entry of the loaded ad_cfk_soa (TxnInfoExtra, CommandsForKey.java:273-283;
+ * Ballot.ZERO where the TxnInfo has none). Without a load every entry holds Ballot.ZERO; loading a new
+ * ad_cfk_soa clears them. */
+int ad_cfk_ballots_load(ad_ctx* ctx, uint64_t n_entries, const uint64_t* msb, const uint64_t* lsb, const int32_t* node);
+/* The entries' ballots as they stand (views as ad_cfk_entries). */
+int ad_cfk_ballots(ad_ctx* ctx, uint64_t* n_entries, const uint64_t** msb, const uint64_t** lsb, const int32_t** node);
 
 #ifdef __cplusplus
 }

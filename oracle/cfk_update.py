@@ -9,8 +9,14 @@ Follows accord-core/src/main/java/accord/local/cfk/CommandsForKey.java:
     Timestamp.java:208-217; identity = Timestamp.equals :244-249);
   * absent -> insert at -1 - pos with (txnId, newStatus, executeAt) (:1002-1007); a key without a
     CommandsForKey gets a new one (the store creates it before the update);
-  * present -> replaced iff newStatus > cur.status (:1013-1027; the equal-status, higher-ballot case
-    needs ballots, which the batch format does not carry: never replaced);
+  * present -> replaced (:1013-1036) iff newStatus > cur.status, or newStatus == cur.status,
+    newStatus.hasInfo and the command's ballot > cur.ballot(), or newStatus is
+    PREACCEPTED_OR_ACCEPTED_INVALIDATE over an ACCEPTED entry with a higher ballot (an invalidation
+    outbidding an Accept); a batch without ballots carries Ballot.ZERO, which never outbids;
+  * the replacing TxnInfo (TxnInfo.create :254-262): executeAt = the command's executeAt when
+    newStatus.hasExecuteAt() (ACCEPTED..APPLIED), else txnId; ballot = the command's
+    acceptedOrCommitted when newStatus.hasBallot (PREACCEPTED_OR_ACCEPTED_INVALIDATE..COMMITTED),
+    else Ballot.ZERO (InternalStatus :495-538);
   * prunedBefore is an index into byId here: an insertion at or before it moves it by one.
 Not restated (the caller's job, as the ABI documents): the shardRedundantBefore filter (:995),
 loadingPruned, TxnInfo.missing() maintenance and the deps-derived additions of
@@ -34,20 +40,46 @@ def norm(msb, lsb, node):
     return (msb, ((lsb >> 16) << 4) | ((lsb >> 1) & 0xF), int(node))
 
 
+HAS_EXEC = (3, 4, 5, 6)            # InternalStatus.hasExecuteAtOrDeps
+HAS_BALLOT = (2, 3, 4)             # InternalStatus.hasBallot
+HAS_INFO = (2, 3, 4, 5, 6)         # hasExecuteAtOrDeps | hasBallot
+ZERO = (0, 0, 0)                   # Ballot.ZERO
+
+
+def replaces(st, cur_st, ballot, cur_ballot):
+    """CommandsForKey.update's test of whether a status/ballot replaces the entry (:1018-1034)."""
+    if st > cur_st:
+        return True
+    if st < cur_st:
+        return st == 2 and cur_st == 3 and norm(*ballot) > norm(*cur_ballot)
+    return st in HAS_INFO and norm(*ballot) > norm(*cur_ballot)
+
+
 def cfk_update(cfk, upd):
-    """Returns (new CfkSnapshot, n_applied): `upd` (model.CfkUpdates) applied in order."""
+    """Returns (new CfkSnapshot, n_applied): `upd` (model.CfkUpdates) applied in order. Ballots:
+    cfk.ballot / upd.ballot (Tids, or None = all Ballot.ZERO); the result carries ballots when
+    either does."""
     keys = cfk.keys
     seg = cfk.seg.astype(np.int64)
     status = cfk.status.copy()
     em, el, en = cfk.exec.msb.copy(), cfk.exec.lsb.copy(), cfk.exec.node.copy()
     tm, tl, tn = cfk.txn.msb, cfk.txn.lsb, cfk.txn.node
-    inserted = {}      # key -> {norm: [txn (m, l, n), exec (m, l, n), status]}
+    cb = getattr(cfk, "ballot", None)
+    ub = getattr(upd, "ballot", None)
+    with_ballots = cb is not None or ub is not None
+    ne = len(status)
+    bm = cb.msb.copy() if cb is not None else np.zeros(ne, np.uint64)
+    bl = cb.lsb.copy() if cb is not None else np.zeros(ne, np.uint64)
+    bn = cb.node.copy() if cb is not None else np.zeros(ne, np.int32)
+    inserted = {}      # key -> {norm: [txn (m, l, n), exec (m, l, n), status, ballot (m, l, n)]}
     applied = 0
     for i in range(len(upd)):
         key = int(upd.keys[i])
         st = int(upd.status[i])
         t = (int(upd.txn.msb[i]), int(upd.txn.lsb[i]), int(upd.txn.node[i]))
-        x = (int(upd.exec.msb[i]), int(upd.exec.lsb[i]), int(upd.exec.node[i]))
+        x = (int(upd.exec.msb[i]), int(upd.exec.lsb[i]), int(upd.exec.node[i])) if st in HAS_EXEC else t
+        b = (int(ub.msb[i]), int(ub.lsb[i]), int(ub.node[i])) if ub is not None else ZERO
+        sb = b if st in HAS_BALLOT else ZERO
         nt = norm(*t)
         k = int(np.searchsorted(keys, key))
         e = -1
@@ -62,26 +94,30 @@ def cfk_update(cfk, upd):
             if lo < int(seg[k + 1]) and norm(tm[lo], tl[lo], tn[lo]) == nt:
                 e = lo
         if e >= 0:
-            if st > int(status[e]):
+            if replaces(st, int(status[e]), b, (int(bm[e]), int(bl[e]), int(bn[e]))):
                 status[e] = st
                 em[e], el[e], en[e] = x
+                bm[e], bl[e], bn[e] = sb
                 applied += 1
             continue
         ins = inserted.setdefault(key, {})
         cur = ins.get(nt)
         if cur is None:
-            ins[nt] = [t, x, st]
+            ins[nt] = [t, x, st, sb]
             applied += 1
-        elif st > cur[2]:
-            cur[1], cur[2] = x, st
+        elif replaces(st, cur[2], b, cur[3]):
+            cur[1], cur[2], cur[3] = x, st, sb
             applied += 1
     if not inserted:
-        return CfkSnapshot(keys.copy(), cfk.seg.copy(), cfk.txn, Tids(em, el, en), status,
-                           None if cfk.pruned_before is None else cfk.pruned_before.copy(),
-                           cfk.miss_off, cfk.miss), applied
+        out = CfkSnapshot(keys.copy(), cfk.seg.copy(), cfk.txn, Tids(em, el, en), status,
+                          None if cfk.pruned_before is None else cfk.pruned_before.copy(),
+                          cfk.miss_off, cfk.miss)
+        if with_ballots:
+            out.ballot = Tids(bm, bl, bn)
+        return out, applied
     # splice the insertions into byId (new keys included), keeping every key's segment sorted
     all_keys = sorted(set(keys.tolist()) | set(inserted))
-    out = {f: [] for f in ("tm", "tl", "tn", "em", "el", "en", "st")}
+    out = {f: [] for f in ("tm", "tl", "tn", "em", "el", "en", "st", "bm", "bl", "bn")}
     new_seg = [0]
     pruned = []
     for key in all_keys:
@@ -90,22 +126,27 @@ def cfk_update(cfk, upd):
         pb = -1
         if k < len(keys) and keys[k] == key:
             for e in range(int(seg[k]), int(seg[k + 1])):
-                rows.append((norm(tm[e], tl[e], tn[e]), (tm[e], tl[e], tn[e]), (em[e], el[e], en[e]), status[e]))
+                rows.append((norm(tm[e], tl[e], tn[e]), (tm[e], tl[e], tn[e]), (em[e], el[e], en[e]), status[e],
+                             (bm[e], bl[e], bn[e])))
             if cfk.pruned_before is not None and cfk.pruned_before[k] >= 0:
                 pb = rows[int(cfk.pruned_before[k])][0]
-        for nt, (t, x, st) in sorted(inserted.get(key, {}).items()):
-            bisect.insort(rows, (nt, t, x, st))
-        for _, t, x, st in rows:
+        for nt, (t, x, st, b) in sorted(inserted.get(key, {}).items()):
+            bisect.insort(rows, (nt, t, x, st, b))
+        for _, t, x, st, b in rows:
             out["tm"].append(t[0]), out["tl"].append(t[1]), out["tn"].append(t[2])
             out["em"].append(x[0]), out["el"].append(x[1]), out["en"].append(x[2])
+            out["bm"].append(b[0]), out["bl"].append(b[1]), out["bn"].append(b[2])
             out["st"].append(st)
         pruned.append(-1 if pb == -1 else [r[0] for r in rows].index(pb))
         new_seg.append(len(out["st"]))
     txn = Tids(np.array(out["tm"], np.uint64), np.array(out["tl"], np.uint64), np.array(out["tn"], np.int32))
     exe = Tids(np.array(out["em"], np.uint64), np.array(out["el"], np.uint64), np.array(out["en"], np.int32))
-    return CfkSnapshot(np.array(all_keys, np.int64), np.array(new_seg, np.uint64), txn, exe,
-                       np.array(out["st"], np.uint8),
-                       None if cfk.pruned_before is None else np.array(pruned, np.int64)), applied
+    res = CfkSnapshot(np.array(all_keys, np.int64), np.array(new_seg, np.uint64), txn, exe,
+                      np.array(out["st"], np.uint8),
+                      None if cfk.pruned_before is None else np.array(pruned, np.int64))
+    if with_ballots:
+        res.ballot = Tids(np.array(out["bm"], np.uint64), np.array(out["bl"], np.uint64), np.array(out["bn"], np.int32))
+    return res, applied
 
 
 def dup_committed_exec(cfk):

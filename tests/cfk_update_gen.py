@@ -48,8 +48,30 @@ def fresh_preaccepts(cfk, rng, n_txns, max_keys=4, epoch=9, hlc0=1, statuses=(2,
 
 
 def concat(*us):
+    b = None
+    if any(u.ballot is not None for u in us):
+        z = [Tids(np.zeros(len(u), np.uint64), np.zeros(len(u), np.uint64), np.zeros(len(u), np.int32)) for u in us]
+        b = Tids.concat([u.ballot if u.ballot is not None else zz for u, zz in zip(us, z)])
     return CfkUpdates(np.concatenate([u.keys for u in us]), Tids.concat([u.txn for u in us]),
-                      Tids.concat([u.exec for u in us]), np.concatenate([u.status for u in us]))
+                      Tids.concat([u.exec for u in us]), np.concatenate([u.status for u in us]), b)
+
+
+def ballots(rng, n, epoch=1, zero_frac=0.2, hlc_span=20):
+    """Random Ballots (Timestamp layout; a few equal, some Ballot.ZERO)."""
+    from accord_deps.model import make_timestamps
+    b = make_timestamps(epoch, rng.integers(1, hlc_span, n), np.zeros(n, np.uint64), rng.integers(1, 4, n))
+    z = rng.random(n) < zero_frac
+    return Tids(np.where(z, 0, b.msb).astype(np.uint64), np.where(z, 0, b.lsb).astype(np.uint64),
+                np.where(z, 0, b.node).astype(np.int32))
+
+
+def ballot_transitions(cfk, rng, n, statuses=(2, 3, 4, 5, 6)):
+    """Transitions that exercise the ballot rules (CommandsForKey.java:1018-1034): many updates of
+    few entries with equal statuses, PREACCEPTED_OR_ACCEPTED_INVALIDATE over ACCEPTED, random
+    ballots."""
+    u, e = transitions(cfk, rng, n, repeat_frac=0.6, statuses=statuses)
+    u.ballot = ballots(rng, n)
+    return u, e
 
 
 def older_inserts(cfk, rng, n, known_frac=0.3, new_exec_frac=0.3, statuses=range(8)):

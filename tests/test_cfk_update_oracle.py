@@ -65,6 +65,7 @@ def test_identity_is_timestamp_equals():
 
 def test_random_transitions_match_a_per_entry_model():
     # independent model: for every entry, the first update of the highest status above its own
+    # (no ballots: Ballot.ZERO never outbids)
     import cfk_update_gen as G
     for seed in range(6):
         w = synth.random_small(seed)
@@ -81,8 +82,36 @@ def test_random_transitions_match_a_per_entry_model():
         for ent, i in best.items():
             if u.status[i] > exp_st[ent]:
                 exp_st[ent] = u.status[i]
-                exp_x[ent] = u.exec.lsb[i]
+                # executeAt only for statuses with one (TxnInfo.create, CommandsForKey.java:254-262)
+                exp_x[ent] = u.exec.lsb[i] if 3 <= u.status[i] <= 6 else u.txn.lsb[i]
                 cnt += 1
         assert n.status.tolist() == exp_st.tolist()
         assert n.exec.lsb.tolist() == exp_x.tolist()
         assert applied >= cnt
+
+
+def test_ballot_rules():
+    # CommandsForKey.java:1018-1034 per case; InternalStatus.hasBallot / hasInfo (:495-538)
+    b = lambda h: (1 << 15, h << 16, 1)                      # noqa: E731  Ballot(epoch 1, hlc h)
+    z = (0, 0, 0)
+    assert U.replaces(4, 3, z, b(9))                          # higher status: always
+    assert not U.replaces(3, 3, b(5), b(9)) and U.replaces(3, 3, b(10), b(9))
+    assert not U.replaces(3, 3, b(9), b(9))                   # equal ballot: no
+    assert U.replaces(2, 3, b(10), b(9))                      # invalidation outbids an Accept
+    assert not U.replaces(2, 4, b(10), b(9))                  # ... not a Commit
+    assert not U.replaces(1, 2, b(10), z)                     # lower status otherwise: no
+    assert not U.replaces(0, 0, b(10), z)                     # TRANSITIVELY_KNOWN has no info
+    assert not U.replaces(7, 7, b(10), z)
+    assert U.replaces(6, 6, b(10), z)                         # APPLIED hasInfo (executeAt)
+    # the replacing TxnInfo: ballot kept only with hasBallot, executeAt only with hasExecuteAt
+    c = _store()
+    t = make_txn_ids(1, [100], [A.KIND_WRITE], 1)
+    x = make_txn_ids(1, [300], [A.KIND_WRITE], 1)
+    bt = Tids(np.array([b(7)[0]], np.uint64), np.array([b(7)[1]], np.uint64), np.array([1], np.int32))
+    n, _ = U.cfk_update(c, CfkUpdates(np.array([10]), t, x, np.array([A.ST_ACCEPTED]), bt))
+    assert int(n.exec.lsb[0]) >> 16 == 300 and int(n.ballot.lsb[0]) == b(7)[1]
+    n2, _ = U.cfk_update(n, CfkUpdates(np.array([10]), t, x, np.array([A.ST_STABLE]), bt))
+    assert int(n2.ballot.lsb[0]) == 0 and int(n2.exec.lsb[0]) >> 16 == 300
+    bt2 = Tids(np.array([b(8)[0]], np.uint64), np.array([b(8)[1]], np.uint64), np.array([1], np.int32))
+    n3, _ = U.cfk_update(n, CfkUpdates(np.array([10]), t, x, np.array([A.ST_PREACCEPTED]), bt2))
+    assert n3.status[0] == A.ST_PREACCEPTED and int(n3.exec.lsb[0]) == int(t.lsb[0]) and int(n3.ballot.lsb[0]) == b(8)[1]

@@ -386,3 +386,101 @@ def test_recovery_after_older_inserts(oracle, seed):
             w.cfk = old
     finally:
         st.close()
+
+
+# ---- ballots (CommandsForKey.java:1018-1034; TxnInfo.create :254-262) ---------------------------
+def _check_ballots(st, new):
+    b = st.cfk_ballots()
+    exp = new.ballot
+    assert b.msb.tolist() == exp.msb.tolist() and b.lsb.tolist() == exp.lsb.tolist() and b.node.tolist() == exp.node.tolist()
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("seed", range(6))
+def test_ballot_replacement(oracle, seed, path):
+    # equal-status updates with higher ballots, invalidations outbidding Accepts, ballots carried
+    # through insertions (fresh and older ids) and cleared by ballot-free batches
+    w = synth.random_small(70 + seed, with_slices=(seed % 3 == 1))
+    w.flags = A.AD_SNAPSHOT
+    rng = np.random.default_rng(70 + seed)
+    if seed % 2:          # a store loaded with ballots
+        w.cfk.ballot = G.ballots(rng, w.cfk.n_entries)
+        w.cfk.ballot = Tids(np.where(np.isin(w.cfk.status, (2, 3, 4)), w.cfk.ballot.msb, 0).astype(np.uint64),
+                            np.where(np.isin(w.cfk.status, (2, 3, 4)), w.cfk.ballot.lsb, 0).astype(np.uint64),
+                            np.where(np.isin(w.cfk.status, (2, 3, 4)), w.cfk.ballot.node, 0).astype(np.int32))
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices, path=path)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        for rnd in range(4):
+            bt, _ = G.ballot_transitions(cfk, rng, 60)
+            if rnd == 0:
+                u = bt
+            elif rnd == 1:
+                ins = G.fresh_preaccepts(cfk, rng, 10, epoch=9, statuses=(2, 3, 4))
+                ins.ballot = G.ballots(rng, len(ins))
+                u = G.concat(bt, ins, ins)
+            elif rnd == 2:
+                old = G.older_inserts(cfk, rng, 20)
+                old.ballot = G.ballots(rng, len(old))
+                u = G.concat(old, bt, old)
+            else:
+                u, _ = G.transitions(cfk, rng, 40)            # Ballot.ZERO: replacements drop ballots
+            new, _ = U.cfk_update(cfk, u)
+            if U.dup_committed_exec(new):
+                continue
+            if new.ballot is None:
+                new.ballot = Tids(np.zeros(new.n_entries, np.uint64), np.zeros(new.n_entries, np.uint64),
+                                  np.zeros(new.n_entries, np.int32))
+            st.cfk_update(u)
+            _check(w, st, oracle, new)
+            _check_ballots(st, new)
+            cfk = new
+    finally:
+        st.close()
+
+
+def test_ballot_rules_known_answers(oracle):
+    # one entry per rule: (status, ballot) over (cur status, cur ballot) -> replaced?
+    from accord_deps.model import make_timestamps
+    w = synth.random_small(80, n_range_cmds=0)
+    w.flags = A.AD_SNAPSHOT
+    seg = w.cfk.seg.astype(np.int64)
+    k = int(np.argmax(np.diff(seg)))
+    es = [e for e in range(int(seg[k]), int(seg[k + 1])) if (int(w.cfk.txn.lsb[e]) & 1) == 0][:6]
+    assert len(es) == 6
+    hi, lo = make_timestamps(1, 50, 0, 1), make_timestamps(1, 10, 0, 1)
+    cur = [(3, hi), (3, lo), (3, lo), (4, lo), (5, lo), (2, lo)]
+    w.cfk.status = w.cfk.status.copy()
+    bm, bl, bn = (np.zeros(w.cfk.n_entries, np.uint64), np.zeros(w.cfk.n_entries, np.uint64),
+                  np.zeros(w.cfk.n_entries, np.int32))
+    for e, (s, b) in zip(es, cur):
+        w.cfk.status[e] = s
+        w.cfk.exec.msb[e], w.cfk.exec.lsb[e], w.cfk.exec.node[e] = w.cfk.txn.msb[e], w.cfk.txn.lsb[e], w.cfk.txn.node[e]
+        if s in (2, 3, 4):
+            bm[e], bl[e], bn[e] = b.msb[0], b.lsb[0], b.node[0]
+    w.cfk.ballot = Tids(bm, bl, bn)
+    # updates: ACCEPTED lower ballot (no), ACCEPTED higher (yes), PREACC-invalidate higher over
+    # ACCEPTED (yes, executeAt -> txnId), PREACC higher over COMMITTED (no), STABLE equal status
+    # (hasInfo, higher: yes), PREACC equal higher (hasInfo via ballot: yes)
+    ups = [(3, lo), (3, hi), (2, hi), (2, hi), (5, hi), (2, hi)]
+    expect = [False, True, True, False, True, True]
+    t = w.cfk.txn.take(es)
+    # STABLE keeps no ballot: its equal-status replacement shows in executeAt (a new Timestamp)
+    xs = make_timestamps(1, 10 ** 6, 0, 77)
+    x = Tids(t.msb.copy(), t.lsb.copy(), t.node.copy())
+    x.msb[4], x.lsb[4], x.node[4] = xs.msb[0], xs.lsb[0], xs.node[0]
+    u = CfkUpdates(np.full(6, w.cfk.keys[k]), t, x, np.array([s for s, _ in ups], np.uint8),
+                   Tids(np.array([b.msb[0] for _, b in ups], np.uint64), np.array([b.lsb[0] for _, b in ups], np.uint64),
+                        np.array([b.node[0] for _, b in ups], np.int32)))
+    new, n = U.cfk_update(w.cfk, u)
+    assert [bool(new.status[e] != w.cfk.status[e] or new.ballot.lsb[e] != w.cfk.ballot.lsb[e] or
+                 new.exec.lsb[e] != w.cfk.exec.lsb[e]) for e in es] == expect
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        st.cfk_update(u)
+        _check(w, st, oracle, new)
+        _check_ballots(st, new)
+    finally:
+        st.close()
