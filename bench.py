@@ -738,6 +738,83 @@ def bench_cfk_update(args, rank, world, local, dev):
         dist.destroy_process_group()
 
 
+def bench_steady(args, rank, world, local, dev):
+    """Steady state of a config-2 store: a step resolves one batch of R fresh
+    PreAccepts (8 Zipf keys each; ad_deps_batch_device, SNAPSHOT), then one ad_cfk_update_device
+    batch registers them -- CommandsForKey.update inserting each txn PREACCEPTED into its keys -- and
+    moves the previous step's txns on to APPLIED (executeAt = txnId), plus T status transitions of
+    the history's live entries. Each step's requests are newer than the last step's, so a resolve
+    sees the previous batch in flight and everything before it applied. The store grows by R x 8
+    entries per step. With N GPUs, N independent replicas."""
+    s = args.scale
+    w = synth.config2(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_hist_entries=int(16_000_000 * s),
+                      seed=0xACC0D002 + rank)
+    R = max(1, int(args.steady * s))
+    T = int(args.steady_transitions * s) if args.steady_transitions >= 0 else R
+    n_b = args.warmup + args.steps
+    # requests on keys the store already holds (ad_cfk_update does not create a CommandsForKey)
+    stream = synth.config2_stream(w, n_b, R, seed=0xACC0D5EE + rank, held_keys_only=True)
+    cfk = w.cfk
+    from accord_deps.model import CfkUpdates, Tids
+    rng = np.random.default_rng(0xACC0D01E)
+    key_of = np.repeat(cfk.keys, np.diff(cfk.seg.astype(np.int64)))
+    status = cfk.status.copy()
+    batches = []
+    prev = None
+    for b in range(n_b):
+        q = stream[b]
+        qdev, keep = native.device_queries(q, dev)
+        live = np.nonzero(status < A.ST_APPLIED)[0]
+        e = np.sort(rng.choice(live, min(T, len(live)), replace=False)) if len(live) else np.zeros(0, np.int64)
+        st = np.maximum(status[e] + 1, A.ST_ACCEPTED).astype(np.uint8)
+        status[e] = st
+        rows = np.repeat(np.arange(len(q)), np.diff(q.key_off.astype(np.int64)))
+        ti = q.txn.take(rows)
+        parts = [(q.keys, ti, ti, np.full(len(rows), A.ST_PREACCEPTED, np.uint8)),
+                 (key_of[e], cfk.txn.take(e), cfk.exec.take(e), st)]
+        if prev is not None:
+            parts.append((prev[0], prev[1], prev[1], np.full(len(prev[0]), A.ST_APPLIED, np.uint8)))
+        prev = (q.keys, ti)
+        u = CfkUpdates(np.concatenate([p_[0] for p_ in parts]), Tids.concat([p_[1] for p_ in parts]),
+                       Tids.concat([p_[2] for p_ in parts]), np.concatenate([p_[3] for p_ in parts]))
+        ud, ukeep = native.device_updates(u, dev)
+        batches.append((qdev, keep, ud, ukeep, len(u), q.n_probes))
+    store = native.DeviceCommandStore(device=local)
+    store.load(w)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    it = iter(batches)
+
+    def step():
+        b = next(it)
+        _, rs = store.deps_batch_device(b[0], sp)
+        _, us = store.cfk_update_device(b[2], sp)
+        return dict(resolve_ms=rs["ms_device"], update_ms=us["ms_device"], locate_ms=us["ms_stage"][0],
+                    derive_ms=us["ms_stage"][1], inserted=us["n_keys"][0], pairs=sum(rs["n_pairs"]))
+    elapsed, all_stats = _timed_steps(args, world, dev, step)
+    ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    reqs = _sum_over_ranks(world, dev, R * args.steps)
+    mean = lambda k: round(float(np.mean([x[k] for x in all_stats])), 4)   # noqa: E731
+    res = {
+        "metric": "steady-state PreAccept on a config-2 store: requests/sec (deps resolved + registered by "
+                  "CommandsForKey.update + status transitions)", "value": reqs / elapsed,
+        "unit": "requests/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "config2 store (%d entries initially), per step %d fresh PreAccepts x 8 keys resolved "
+                               "then inserted, the previous step's applied, + %d history transitions" % (cfk.n_entries, R, T),
+                   "parallelism": "replicas x%d" % world},
+        "stages_ms": {"resolve": mean("resolve_ms"), "update": mean("update_ms"), "update.locate+apply+insert":
+                      mean("locate_ms"), "update.re-derivation": mean("derive_ms")},
+        "entries_after": int(cfk.n_entries + sum(x["inserted"] for x in all_stats)),
+        "updates_per_step": int(np.mean([b_[4] for b_ in batches])),
+        "pairs_per_step": mean("pairs"),
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    store.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def bench_sequential(args, rank, world, local, dev):
     """Config 1: 10k txns x 4 keys over 1k keys, one CommandStore, SEQUENTIAL PreAccept (each txn
     inserted as PREACCEPTED before its deps). SEQUENTIAL runs through the host API: a step is one
@@ -821,6 +898,10 @@ def main():
                     help="with config 2: BeginRecovery scans for N recovering txns on the config-2 snapshot (SURVEY 8 f4)")
     ap.add_argument("--cfk-update", type=int, default=0, metavar="N",
                     help="with config 2: batches of N CommandsForKey.update status transitions on the device (SURVEY 8 f1)")
+    ap.add_argument("--steady", type=int, default=0, metavar="R",
+                    help="config-2 steady state: per step resolve R fresh PreAccepts, then register them "
+                         "(CommandsForKey.update inserts) with --steady-transitions status transitions")
+    ap.add_argument("--steady-transitions", type=int, default=-1, metavar="T", help="default 8R")
     ap.add_argument("--resident", action="store_true",
                     help="--config 1: keep the store resident, each step a fresh SEQUENTIAL batch (device-side insertion)")
     ap.add_argument("--cfk-insert-frac", type=float, default=0.5,
@@ -871,6 +952,8 @@ def main():
         return bench_recovery(args, rank, world, local, dev)
     if args.cfk_update:
         return bench_cfk_update(args, rank, world, local, dev)
+    if args.steady:
+        return bench_steady(args, rank, world, local, dev)
 
     return bench_deps(args, rank, world, local, dev)
 

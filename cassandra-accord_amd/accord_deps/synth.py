@@ -162,6 +162,29 @@ def config2(n_txns=1_000_000, keys_per_txn=8, n_keys=1_000_000, n_hist_entries=1
     return w
 
 
+def config2_stream(w, n_batches, n_txns, seed=0xACC0D5EE, held_keys_only=False):
+    """Successive config-2 request batches for a steady-state run on the config-2 store `w`: batch b
+    holds n_txns fresh PreAccepts (8 Zipf keys each, Read/Write 50/50) whose txnIds follow every id
+    of batches < b (hlc ranges after the config's own request batch). `held_keys_only`: Zipf over
+    the keys the store holds a CommandsForKey for (same ranks order)."""
+    p = w.params
+    n_keys, k = int(p["n_keys"]), int(p["keys_per_txn"])
+    rng = np.random.default_rng(seed)
+    token = key_tokens(n_keys, int(p["seed"]))
+    if held_keys_only:
+        token = token[np.isin(token, w.cfk.keys)]
+        n_keys = len(token)
+    z = Zipf(n_keys, float(p["zipf_s"]))
+    n_hist = int(p["n_hist_entries"]) // k
+    hlc = n_hist + 2000 + int(p["n_txns"]) + 4096
+    out = []
+    for _ in range(n_batches):
+        qk = distinct_rows(rng, z.sample, n_txns, k)
+        out.append(_queries(rng, n_txns, qk, token, _rw_kinds(rng, n_txns), hlc0=hlc))
+        hlc += n_txns + 16
+    return out
+
+
 def with_request_mix(w, accept_frac=0.0, unordered_frac=0.0, unordered_window=2000, seed=0xACC0D0A5):
     """The config-2 workload `w` (history txn j has txnId hlc 1 + j) turned into a replica's mix of
     deps requests (SNAPSHOT semantics), so that the paths besides the newest-request one run:
