@@ -215,7 +215,7 @@ struct ad_ctx {
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
     DevBuf arena, rarena;
-    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, q_rec;
+    DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, q_rec, big;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t o_cap[9] = {};                    // capacities of the packed outputs (elements)
     DevBuf lb_agg, lb_inc;                     // tile sums and their prefixes (run_pack_lb)
@@ -1227,8 +1227,11 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
         !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
         !ens<uint4>(c->q_rec, n) || !ens<uint32_t>(c->deferred1, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) ||
-        !ens<uint32_t>(c->deferred2, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64))
+        !ens<uint32_t>(c->deferred2, n + DEFER_CHUNK * (uint64_t)device_cu_count() * 64) || !ens<uint32_t>(c->big, n))
         return c->fail(AD_E_NOMEM, "batch buffers");
+    b.big = c->big.as<uint32_t>();
+    b.k2_big = K2_BIG;
+    if (const char* e = getenv("AD_K2_BIG")) b.k2_big = (uint32_t)strtoul(e, nullptr, 10);   // tests: force k_build_big
     b.q_rec = c->q_rec.as<uint4>();
     b.deferred1 = c->deferred1.as<uint32_t>();
     b.deferred2 = c->deferred2.as<uint32_t>();

@@ -539,6 +539,7 @@ constexpr uint32_t K2_MAXP = 64;     // probes per request on the LDS path
 constexpr uint32_t K2_CAP = 512;     // elements per list family on the LDS path
 constexpr uint32_t K2_REGION_CHUNK = 1u << 16;
 
+
 struct K2Mem {
     // per-probe metadata
     uint32_t* off; uint32_t* c0; uint32_t* c1; uint32_t* roff; uint32_t* rcnt; uint64_t* rb;
@@ -722,6 +723,12 @@ __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
         tot1 = uniform(wave_sum(tot1));
         totR = uniform(wave_sum(totR));
         const uint32_t capn = max(max(tot0, tot1), totR);
+        if (capn > b.k2_big)
+        {
+            // a heavy request (a hot key's in-flight txns): one whole workgroup, k_build_big
+            if (lane == 0) b.big[atomicAdd(&b.ctl->n_big, 1ull)] = (uint32_t)t;
+            continue;
+        }
         const bool big = np > K2_MAXP || capn > K2_CAP;
 
         K2Mem mem;
@@ -907,11 +914,300 @@ __global__ __launch_bounds__(64) void k_build(DevSnapshot s, BatchBufs b)
     }
 }
 
+// ---- K2 for heavy requests: the same build with one 1024-thread workgroup per request (a request
+// whose lists hold thousands of ids -- a Zipf-hot key's in-flight txns -- would keep one wave busy
+// for milliseconds). Every per-element step (gather, rank-merge dedup, unique ranks, writes) is
+// spread over the 16 waves; the list starts and the kept-flag prefix are block scans.
+constexpr uint32_t KB_THREADS = 1024;
+constexpr uint32_t KB_WAVES = KB_THREADS / 64;
+
+struct KbLds {
+    uint32_t wsum[KB_WAVES + 1];
+    uint32_t red[4];
+    unsigned long long so, have, ro;
+    uint32_t nk;
+};
+
+// exclusive block scan of cnt(i), i < n, into st[0..n] (st may alias the source: each i is read and
+// written by one thread); returns the total
+template <class Cnt>
+__device__ uint32_t block_scan_into(KbLds& L, uint32_t n, Cnt cnt, uint32_t* st)
+{
+    const uint32_t tid = threadIdx.x, wv = tid >> 6, lane = lane_id();
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += KB_THREADS)
+    {
+        const uint32_t i = i0 + tid;
+        const uint32_t c = i < n ? cnt(i) : 0u;
+        const uint32_t inc = wave_incl_scan(c);
+        if (lane == 63) L.wsum[wv] = inc;
+        __syncthreads();
+        if (wv == 0)
+        {
+            const uint32_t v = lane < KB_WAVES ? L.wsum[lane] : 0u;
+            const uint32_t vi = wave_incl_scan(v);
+            if (lane < KB_WAVES) L.wsum[lane] = vi - v;
+            if (lane == KB_WAVES - 1) L.wsum[KB_WAVES] = vi;
+        }
+        __syncthreads();
+        if (i < n) st[i] = carry + L.wsum[wv] + inc - c;
+        carry += L.wsum[KB_WAVES];
+        __syncthreads();
+    }
+    if (tid == 0) st[n] = carry;
+    __syncthreads();
+    return carry;
+}
+
+template <class Get>
+__device__ uint32_t block_rank_merge_kept(KbLds& L, Get get, const uint32_t* st, uint32_t nl, uint32_t total, uint32_t* P)
+{
+    for (uint32_t e = threadIdx.x; e < total; e += KB_THREADS)
+    {
+        const uint32_t a = list_of(st, nl, e);
+        const uint64_t x = get(e);
+        uint32_t kept = 1;
+        for (uint32_t bl = 0; bl < a && kept; ++bl)
+        {
+            const uint32_t s0 = st[bl], s1 = st[bl + 1];
+            if (s1 > s0)
+            {
+                const uint32_t j = lb_in(get, s0, s1, x);
+                if (j < s1 && get(j) == x) kept = 0;
+            }
+        }
+        P[e] = kept;
+    }
+    __syncthreads();
+    return block_scan_into(L, total, [&](uint32_t i) { return P[i]; }, P);
+}
+
+// region of one map: bytes taken exactly (one atomic per request and map); 0 sizes on overflow
+__device__ bool kb_region(KbLds& L, const BatchBufs& b, uint64_t bytes, uint64_t* ro)
+{
+    if (threadIdx.x == 0)
+    {
+        const unsigned long long o = atomicAdd(&b.ctl->reg_top, (unsigned long long)bytes);
+        if (o + bytes > b.ctl->reg_cap) atomicOr(&b.ctl->overflow, 8u);
+        L.ro = o;
+    }
+    __syncthreads();
+    *ro = L.ro;
+    const bool fits = L.ro + bytes <= b.ctl->reg_cap;
+    return fits;
+}
+
+__global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBufs b)
+{
+    __shared__ KbLds L;
+    const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+    const uint64_t n = b.n_txns;
+    const uint64_t nbig = b.ctl->n_big;
+    if (tid == 0) { L.so = 0; L.have = 0; }
+    __syncthreads();
+    for (uint64_t bi = blockIdx.x; bi < nbig; bi += gridDim.x)
+    {
+        const uint64_t t = b.big[bi];
+        const uint64_t p0 = b.q_key_off[t];
+        const uint32_t np = (uint32_t)(b.q_key_off[t + 1] - p0);
+        if (tid < 3) L.red[tid] = 0;
+        __syncthreads();
+        {
+            uint32_t a0 = 0, a1 = 0, aR = 0;
+            for (uint32_t i = tid; i < np; i += KB_THREADS)
+            {
+                a0 += b.p_c0[p0 + i];
+                a1 += b.p_c1[p0 + i];
+                aR += b.p_rcnt[p0 + i] + (b.p_rb[p0 + i] != NO_RB ? 1u : 0u);
+            }
+            a0 = wave_sum(a0);
+            a1 = wave_sum(a1);
+            aR = wave_sum(aR);
+            if (lane == 0)
+            {
+                if (a0) atomicAdd(&L.red[0], a0);
+                if (a1) atomicAdd(&L.red[1], a1);
+                if (aR) atomicAdd(&L.red[2], aR);
+            }
+        }
+        __syncthreads();
+        const uint32_t tot0 = L.red[0], tot1 = L.red[1], totR = L.red[2];
+        const uint32_t capn = max(max(tot0, tot1), totR);
+        // this workgroup's scratch, reused across its requests (grown when a request needs more)
+        const uint64_t bytes = k2_scratch_bytes(np, capn);
+        if (tid == 0 && bytes > L.have)
+        {
+            const unsigned long long grow = bytes + bytes / 2;
+            L.so = atomicAdd(&b.ctl->scr_top, grow);
+            L.have = L.so + grow > b.ctl->scr_cap ? 0ull : grow;
+            if (!L.have) atomicOr(&b.ctl->overflow, 4u);
+        }
+        __syncthreads();
+        if (L.have < bytes)
+        {
+            if (tid < 9) b.sz[tid * n + t] = 0;
+            __syncthreads();
+            continue;
+        }
+        K2Mem mem;
+        k2_carve(mem, b.scratch + L.so, np, capn);
+        for (uint32_t i = tid; i < np; i += KB_THREADS)
+        {
+            mem.off[i] = b.p_off[p0 + i]; mem.c0[i] = b.p_c0[p0 + i]; mem.c1[i] = b.p_c1[p0 + i];
+            mem.roff[i] = b.p_roff[p0 + i]; mem.rcnt[i] = b.p_rcnt[p0 + i]; mem.rb[i] = b.p_rb[p0 + i];
+        }
+        __syncthreads();
+        block_scan_into(L, np, [&](uint32_t i) { return mem.c0[i]; }, mem.st0);
+        block_scan_into(L, np, [&](uint32_t i) { return mem.c1[i]; }, mem.st1);
+        block_scan_into(L, 2 * np, [&](uint32_t i) {
+            return (i & 1) ? (mem.rb[i >> 1] != NO_RB ? 1u : 0u) : mem.rcnt[i >> 1];
+        }, mem.stR);
+
+        // ---- keyDeps (class 0) and directKeyDeps (class 1)
+        for (int c = 0; c < 2; ++c)
+        {
+            const int m = c == 0 ? 0 : 2;
+            const uint32_t tot = c == 0 ? tot0 : tot1;
+            const uint32_t* st = c == 0 ? mem.st0 : mem.st1;
+            if (tot == 0)
+            {
+                if (tid == 0) { b.sz[(3 * m) * n + t] = 0; b.sz[(3 * m + 1) * n + t] = 0; b.sz[(3 * m + 2) * n + t] = 0; }
+                continue;
+            }
+            for (uint32_t e = tid; e < tot; e += KB_THREADS)
+            {
+                const uint32_t a = list_of(st, np, e);
+                mem.V[e] = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
+            }
+            __syncthreads();
+            auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
+            const uint32_t U = block_rank_merge_kept(L, get, st, np, tot, mem.P);
+            if (wv == 0)
+            {
+                uint32_t nk = 0;
+                for (uint32_t i0 = 0; i0 < np; i0 += 64)
+                {
+                    const uint32_t i = i0 + lane;
+                    nk += __popcll(ballot(i < np && st[i + 1] > st[i]));
+                }
+                if (lane == 0) L.nk = nk;
+            }
+            __syncthreads();
+            const uint32_t nk = L.nk;
+            const uint64_t rb = region_bytes(nk, U, tot);
+            uint64_t ro;
+            const bool fits = kb_region(L, b, rb, &ro);
+            if (tid == 0)
+            {
+                b.sz[(3 * m) * n + t] = fits ? nk : 0;
+                b.sz[(3 * m + 1) * n + t] = fits ? U : 0;
+                b.sz[(3 * m + 2) * n + t] = fits ? nk + tot : 0;
+                b.t_reg[(uint64_t)m * n + t] = ro;
+            }
+            if (fits)
+            {
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
+                if (wv == 0)
+                {
+                    uint32_t kr = 0;
+                    for (uint32_t i0 = 0; i0 < np; i0 += 64)
+                    {
+                        const uint32_t i = i0 + lane;
+                        const bool ne = i < np && st[i + 1] > st[i];
+                        const uint64_t mk = ballot(ne);
+                        if (ne)
+                        {
+                            const uint32_t k = kr + mbcnt(mk);
+                            okeys[k] = b.q_keys[p0 + i];
+                            ok2t[k] = (int32_t)(nk + st[i + 1]);
+                        }
+                        kr += __popcll(mk);
+                    }
+                }
+                for (uint32_t e = tid; e < tot; e += KB_THREADS)
+                {
+                    const uint64_t x = mem.V[e];
+                    const uint32_t ur = rank_merge_urank(get, st, np, mem.P, x);
+                    if (mem.P[e + 1] - mem.P[e]) otx[ur] = dict_index((uint32_t)x);
+                    ok2t[nk + e] = (int32_t)ur;
+                }
+            }
+            __syncthreads();
+        }
+
+        // ---- rangeDeps: lists = per probe [range-command pairs], [redundant pair]
+        const uint32_t nl = 2 * np;
+        if (totR == 0)
+        {
+            if (tid == 0) { b.sz[3 * n + t] = 0; b.sz[4 * n + t] = 0; b.sz[5 * n + t] = 0; }
+            __syncthreads();
+            continue;
+        }
+        for (uint32_t e = tid; e < totR; e += KB_THREADS)
+        {
+            const uint32_t a = list_of(mem.stR, nl, e);
+            const uint32_t pi = a >> 1;
+            mem.V[e] = (a & 1) ? mem.rb[pi] : b.rarena[(uint64_t)mem.roff[pi] + (e - mem.stR[a])];
+        }
+        __syncthreads();
+        auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
+        const uint32_t UPn = block_rank_merge_kept(L, get, mem.stR, nl, totR, mem.P);
+        for (uint32_t e = tid; e < totR; e += KB_THREADS)
+            if (mem.P[e + 1] - mem.P[e]) mem.UP[rank_merge_urank(get, mem.stR, nl, mem.P, mem.V[e])] = mem.V[e];
+        __syncthreads();
+        // rid groups (group starts compacted in order by a block scan of the first-of-group flags)
+        const uint32_t nR = block_scan_into(L, UPn, [&](uint32_t i) {
+            return (i == 0 || (mem.UP[i] >> 32) != (mem.UP[i - 1] >> 32)) ? 1u : 0u;
+        }, mem.P2);
+        for (uint32_t i = tid; i < UPn; i += KB_THREADS)
+            if (i == 0 || (mem.UP[i] >> 32) != (mem.UP[i - 1] >> 32)) mem.gst[mem.P2[i]] = i;
+        if (tid == 0) mem.gst[nR] = UPn;
+        __syncthreads();
+        auto getr = [&](uint32_t e) -> uint64_t { return mem.UP[e] & 0xFFFFFFFFull; };
+        const uint32_t UR = block_rank_merge_kept(L, getr, mem.gst, nR, UPn, mem.P2);
+        const uint64_t rbytes = region_bytes(nR, UR, UPn);
+        uint64_t ro;
+        const bool fits = kb_region(L, b, rbytes, &ro);
+        if (tid == 0)
+        {
+            b.sz[3 * n + t] = fits ? nR : 0;
+            b.sz[4 * n + t] = fits ? UR : 0;
+            b.sz[5 * n + t] = fits ? nR + UPn : 0;
+            b.t_reg[(uint64_t)1 * n + t] = ro;
+        }
+        if (fits)
+        {
+            int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+            uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nR);
+            int32_t* ok2t = reinterpret_cast<int32_t*>(otx + UR);
+            for (uint32_t g = tid; g < nR; g += KB_THREADS)
+            {
+                okeys[g] = (int64_t)(mem.UP[mem.gst[g]] >> 32);
+                ok2t[g] = (int32_t)(nR + mem.gst[g + 1]);
+            }
+            for (uint32_t e = tid; e < UPn; e += KB_THREADS)
+            {
+                const uint64_t x = getr(e);
+                const uint32_t ur = rank_merge_urank(getr, mem.gst, nR, mem.P2, x);
+                if (mem.P2[e + 1] - mem.P2[e]) otx[ur] = dict_index((uint32_t)x);
+                ok2t[nR + e] = (int32_t)ur;
+            }
+        }
+        __syncthreads();
+    }
+}
+
 hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
+    hipError_t e = hipMemsetAsync(&b.ctl->n_big, 0, sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
     const unsigned grid = (unsigned)std::min<uint64_t>(b.n_txns, (uint64_t)device_cu_count() * 16);
     k_build<<<grid, 64, k2_lds_bytes(), st>>>(s, b);
+    // heavy requests: the count stays on the device; idle workgroups exit at once
+    k_build_big<<<(unsigned)std::min<uint64_t>(b.n_txns, (uint64_t)device_cu_count() * 2), KB_THREADS, 0, st>>>(s, b);
     return hipGetLastError();
 }
 

@@ -20,10 +20,12 @@ struct BatchCtl {
     unsigned long long n_deferred2;           // lean pass 2 -> general fused kernel list slots
     unsigned long long n_real1, n_real2;      // requests on those lists
     unsigned long long tot[9];                // totals of the 9 per-request size arrays (after the offsets scan)
+    unsigned long long n_big;                 // k_build -> k_build_big: requests with a list family > K2_BIG
 };
 constexpr unsigned OVF_PACK = 16u;            // BatchCtl.overflow: a packed output array is too small
 
 constexpr uint64_t NO_RB = ~0ull;
+constexpr uint32_t K2_BIG = 512;     // elements in a list family from which k_build_big takes a request (= the LDS path's K2_CAP)
 constexpr unsigned ERR_INVAL = 1u;   // BatchCtl.error codes
 constexpr unsigned ERR_STATE = 8u;
 
@@ -52,6 +54,8 @@ struct BatchBufs {
     uint8_t* reg;                    // per-request output regions
     uint8_t* scratch;                // big-request scratch
     uint32_t* deferred;              // [n_txns] requests deferred by k_resolve
+    uint32_t* big;                   // [n_txns] requests k_build hands to k_build_big (one workgroup each)
+    uint32_t k2_big;                 // list-family size from which it does (K2_BIG; tests lower it)
     uint32_t* deferred1;             // requests deferred by lean pass 1 (+ chunk holes)
     uint32_t* deferred2;             // requests deferred by lean pass 2 (+ chunk holes)
     const uint32_t* req_list;        // k_resolve: resolve only these requests (count *req_count); null = all

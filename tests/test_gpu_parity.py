@@ -129,6 +129,19 @@ def test_big_requests(oracle):
     assert got.stats["n_deferred"] > 0          # exercised the fused -> split hand-off
 
 
+@pytest.mark.parametrize("big", ["0", "64", "512"])
+def test_big_requests_workgroup_build(oracle, big, monkeypatch):
+    # k_build_big (one 1024-thread workgroup per heavy request): every request (0), the medium ones
+    # (64) or the default threshold, on hot keys with thousands of live entries, range commands and
+    # RedundantBefore in the mix
+    monkeypatch.setenv("AD_K2_BIG", big)
+    w = synth.config2(n_txns=200, n_keys=50, n_hist_entries=40000, keys_per_txn=8, tail_unapplied=3000,
+                      esp_frac=0.2)
+    _compare(w, oracle)
+    _compare(synth.random_small(2100 + int(big), n_keys=40, n_hist_txns=2000, n_txns=200, max_keys=10,
+                                n_range_cmds=60), oracle)
+
+
 def test_many_keys_deferred(oracle):
     # requests with more than 8 keys take the split kernels from the fused kernel
     w = synth.random_small(2024, n_keys=200, n_hist_txns=2000, n_txns=300, max_keys=20, n_range_cmds=50)
