@@ -970,6 +970,7 @@ static int build_snapshot(ad_ctx* c)
     c->h_pruned.swap(pruned);
     c->dirty = false;
     ++c->snap_gen;
+    cfk_upd_work_invalidate(c->cu);      // state the update path keeps between batches
     c->global_ok = use_global;   // parts carry global ranks exactly when the dictionary is the installed one
     c->n_global = use_global ? c->dict_msb.size() : 0;
     c->ms_ingest = now_ms() - t0;

@@ -53,6 +53,7 @@ struct UpdCtl {
     uint32_t n_new, n_ins;    // ids the dictionary does not hold, insertion updates
     unsigned long long diff[3];   // OR of (word ^ reference) over the new ids: node, lo, hi (sort digits)
     uint32_t older, pad;      // a new id is older than the newest dictionary id (dictionary merge)
+    uint64_t cm[2];           // incremental committed order: entries kept from the last one, changed committed entries
 };
 constexpr uint32_t LOC_NONE = 0xFFFFFFFFu;
 
@@ -146,9 +147,23 @@ __device__ inline Bal kept_ballot(uint32_t st, const Bal& b) { return st_has_bal
 // first update of the highest status (packed u64 max: status, then the lowest update index); with
 // ballots the updates of an entry are folded in batch order by k_fold_present. Insertions are
 // flagged (ordered compaction by a scan).
+__device__ inline uint32_t remap_rank(uint32_t r, const uint64_t* pos, uint64_t U);
+
+// the rank k_ins_collect found for an id (0: not in the dictionary then -- search it now), moved by
+// a merge since
+__device__ inline uint32_t known_rank(const DevSnapshot& s, const DictSample& ds, uint32_t r, const uint64_t* mpos, uint64_t U,
+                                      const NormTid& t, uint64_t* p)
+{
+    if (!r) return dict_member_rank(s, ds, t, p);
+    if (U) r = remap_rank(r, mpos, U);
+    *p = (r - 1) >> 1;
+    return r;
+}
+
 __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds, CfkDevState d, CfkUpdIn u, uint32_t* loc,
                                                     uint32_t* xr_out, unsigned long long* word, uint64_t* ins_key,
-                                                    uint32_t* flags, UpdCtl* ctl)
+                                                    uint32_t* flags, const uint32_t* rk, const uint64_t* mpos, uint64_t U,
+                                                    UpdCtl* ctl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= u.n) return;
@@ -173,7 +188,7 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds
     if (st > 7) { upd_fail(ctl, UE_STATUS, (uint32_t)i); return; }
     const uint64_t tl = u.txn_lsb[i];
     uint64_t p;
-    const uint32_t r = dict_member_rank(s, ds, norm_tid(u.txn_msb[i], tl, u.txn_node[i]), &p);
+    const uint32_t r = known_rank(s, ds, rk[2 * i], mpos, U, norm_tid(u.txn_msb[i], tl, u.txn_node[i]), &p);
     if (!r) { upd_fail(ctl, UE_ABSENT, (uint32_t)i); return; }
     if (d.dict_lsb_raw[p] != tl) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
     const KeyRec kr = s.krec[k];
@@ -190,7 +205,7 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds
     if (st_has_exec(st))
     {
         const uint64_t el = u.exec_lsb[i];
-        xr = dict_member_rank(s, ds, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
+        xr = known_rank(s, ds, rk[2 * i + 1], mpos, U, norm_tid(u.exec_msb[i], el, u.exec_node[i]), &p);
         if (!xr) { upd_fail(ctl, UE_NEW_EXEC, (uint32_t)i); return; }
         if (d.dict_lsb_raw[p] != el) { upd_fail(ctl, UE_FLAGS, (uint32_t)i); return; }
     }
@@ -218,7 +233,7 @@ __device__ inline bool newer_than_dict(const DevSnapshot& s, const NormTid& t)
 // ids the dictionary does not hold (txnIds and executeAts): words for the LSD sort + raw lsb;
 // ctl->older is set when one of them is older than the newest dictionary id (a merge, not an append)
 __global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, DictSample ds, CfkUpdIn u, uint64_t* nw, uint64_t cap,
-                                                     UpdCtl* ctl)
+                                                     uint32_t* rk, UpdCtl* ctl)
 {
     __shared__ unsigned long long red[3];
     if (threadIdx.x < 3) red[threadIdx.x] = 0;
@@ -229,6 +244,7 @@ __global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, DictSample d
     unsigned long long d0 = 0, d1 = 0, d2 = 0;
     for (int side = 0; side < 2 && i < u.n; ++side)
     {
+        rk[2 * i + side] = 0;
         if (side && !st_has_exec(u.status[i])) break;      // executeAt = txnId (TxnInfo.create)
         const uint64_t m = side ? u.exec_msb[i] : u.txn_msb[i], l = side ? u.exec_lsb[i] : u.txn_lsb[i];
         const int32_t nd = side ? u.exec_node[i] : u.txn_node[i];
@@ -236,7 +252,9 @@ __global__ __launch_bounds__(256) void k_ins_collect(DevSnapshot s, DictSample d
         if (!newer_than_dict(s, t))
         {
             uint64_t p;
-            if (dict_member_rank(s, ds, t, &p)) continue;
+            const uint32_t r = dict_member_rank(s, ds, t, &p);
+            rk[2 * i + side] = r;              // locate takes it from here
+            if (r) continue;
             ctl->older = 1u;
         }
         const uint32_t j = atomicAdd(&ctl->n_new, 1u);
@@ -424,7 +442,7 @@ __global__ void k_compact(uint64_t n, const uint32_t* flags, const uint64_t* pos
 // order through CommandsForKey.update's replacement test; the entry's old state is kept at its
 // first update's index for a rollback
 __global__ void k_fold_present(uint64_t m, const uint64_t* ks, const uint32_t* vs, CfkUpdIn u, const uint32_t* xr,
-                               CfkDevState d, uint2* bk, Bal* bkb, UpdCtl* ctl)
+                               CfkDevState d, uint2* bk, Bal* bkb, uint8_t* chg, UpdCtl* ctl)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m || (j > 0 && ks[j - 1] == ks[j])) return;
@@ -449,6 +467,7 @@ __global__ void k_fold_present(uint64_t m, const uint64_t* ks, const uint32_t* v
     d.status[e] = (uint8_t)st;
     d.xrank[e] = x;
     d.ballot[e] = b;
+    chg[e] = 1;
     atomicAdd(&ctl->applied, cnt);
 }
 
@@ -510,12 +529,12 @@ __global__ void k_ins_before(uint64_t nk, const uint32_t* gkey, uint64_t G, uint
     ib[k] = (uint32_t)lo;
 }
 
-struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; Bal* bal; };
+struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; Bal* bal; uint8_t* chg; };
 
 // an old entry moves up by the new entries before it: those of lower keys, and those of its key
 // with a lower rank (a mid-segment insert, :1002-1007)
 __global__ __launch_bounds__(256) void k_ins_move_old(uint64_t ne, EntArrays a, const uint32_t* ib, const uint32_t* grank,
-                                                      EntArrays b)
+                                                      EntArrays b, uint32_t* mv)
 {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= ne) return;
@@ -537,6 +556,8 @@ __global__ __launch_bounds__(256) void k_ins_move_old(uint64_t ne, EntArrays a, 
     b.xrank[p] = a.xrank[e];
     b.ekey[p] = k;
     if (b.bal) b.bal[p] = a.bal[e];
+    b.chg[p] = a.chg[e];
+    mv[e] = (uint32_t)p;
 }
 
 // a new entry lands after the old entries below it (its insertPos, -1 - binarySearch) and the new
@@ -566,6 +587,7 @@ __global__ void k_ins_place(uint64_t G, const uint32_t* gkey, const uint32_t* gr
     b.xrank[p] = xr[i];
     b.ekey[p] = k;
     if (b.bal) b.bal[p] = kept_ballot((uint32_t)(wd >> 32), upd_ballot(u, i));
+    b.chg[p] = 1;
 }
 
 __global__ void k_ins_krec(uint64_t nk, const uint32_t* ib, const uint32_t* grank, KeyRec* krec)
@@ -590,7 +612,7 @@ __global__ void k_upd_release(uint64_t n, const uint32_t* loc, unsigned long lon
 // the claiming update of each entry applies if its status is above the entry's; the entry's old
 // state is kept in bk[i] for a rollback
 __global__ void k_upd_apply(uint64_t n, const uint32_t* loc, const uint32_t* xr, unsigned long long* word,
-                            CfkDevState d, uint2* bk, Bal* bkb, UpdCtl* ctl)
+                            CfkDevState d, uint2* bk, Bal* bkb, uint8_t* chg, UpdCtl* ctl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -605,6 +627,7 @@ __global__ void k_upd_apply(uint64_t n, const uint32_t* loc, const uint32_t* xr,
     bk[i] = make_uint2(cur, d.xrank[e]);
     d.status[e] = (uint8_t)st;
     d.xrank[e] = xr[i];
+    chg[e] = 1;
     if (d.ballot)
     {
         // the batch carries Ballot.ZERO: the replacing TxnInfo has no ballot
@@ -659,7 +682,7 @@ __global__ __launch_bounds__(256) void k_drv_scatter(uint64_t ne, CfkDevState d,
         }
     }
     const uint32_t st = d.status[e];
-    if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED)
+    if (ck && st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED)
     {
         const uint64_t j = fs[3 * (ne + 1) + e];
         ck[j] = ((uint64_t)d.ekey[e] << 32) | d.xrank[e];
@@ -733,6 +756,73 @@ __global__ __launch_bounds__(256) void k_drv_keys(uint64_t nk, uint64_t ne, uint
     d.kent[k] = ke;
 }
 
+// ---- incremental committedByExecuteAt (the (key index, executeAt rank) order of the committed
+// entries): the last batch's order minus the entries this batch changed (moved by the insertion
+// map), merged with the changed entries that are committed now (sorted on their own) -- linear
+// passes instead of a radix sort of every committed entry.
+__global__ void k_cm_keep(uint64_t m, const uint32_t* cm, const uint32_t* mv, const uint8_t* chg, uint32_t* f)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    const uint32_t e = mv ? mv[cm[j]] : cm[j];
+    f[j] = chg[e] ? 0u : 1u;
+}
+
+__global__ __launch_bounds__(256) void k_cm_changed(uint64_t ne, CfkDevState d, const uint8_t* chg, uint32_t* f)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t st = d.status[e];
+    f[e] = (chg[e] && st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED) ? 1u : 0u;
+}
+
+__global__ void k_cm_compact(uint64_t m, const uint32_t* src, const uint32_t* mv, const uint32_t* f, const uint64_t* pos,
+                             CfkDevState d, uint64_t* ko, uint32_t* vo)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m || !f[j]) return;
+    uint32_t e = src ? src[j] : (uint32_t)j;
+    if (mv) e = mv[e];
+    const uint64_t p = pos[j];
+    ko[p] = ((uint64_t)d.ekey[e] << 32) | d.xrank[e];
+    vo[p] = e;
+}
+
+// each block merges 256 consecutive elements of one list into the output: the block's first and
+// last element bound its window in the other list (two searches per block), each thread then
+// searches only that window
+__global__ __launch_bounds__(256) void k_cm_merge(uint64_t na, const uint64_t* ka, const uint32_t* va, uint64_t nb,
+                                                  const uint64_t* kb, const uint32_t* vb, uint64_t* ko, uint32_t* vo)
+{
+    __shared__ uint64_t win[2];
+    const uint64_t blocks_a = (na + 255) / 256;
+    const bool from_a = blockIdx.x < blocks_a;
+    const uint64_t base = from_a ? (uint64_t)blockIdx.x * 256 : ((uint64_t)blockIdx.x - blocks_a) * 256;
+    const uint64_t nself = from_a ? na : nb, nother = from_a ? nb : na;
+    const uint64_t* self = from_a ? ka : kb;
+    const uint64_t* o = from_a ? kb : ka;
+    // A before B on equal keys (a duplicate executeAt, reported by k_drv_committed)
+    auto bound = [&](uint64_t x, uint64_t lo, uint64_t hi) {
+        while (lo < hi)
+        {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (from_a ? o[mid] < x : o[mid] <= x) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo;
+    };
+    const uint64_t last = min(base + 256, nself) - 1;
+    if (threadIdx.x == 0) win[0] = bound(self[base], 0, nother);
+    if (threadIdx.x == 1) win[1] = bound(self[last], 0, nother);
+    __syncthreads();
+    const uint64_t i = base + threadIdx.x;
+    if (i >= nself) return;
+    const uint64_t x = self[i];
+    const uint64_t p = i + bound(x, win[0], win[1]);
+    ko[p] = x;
+    vo[p] = from_a ? va[i] : vb[i];
+}
+
 unsigned blocks(uint64_t n, unsigned t = 256) { return (unsigned)std::max<uint64_t>(1, (n + t - 1) / t); }
 
 struct DBuf {
@@ -763,7 +853,13 @@ struct CfkUpdWork {
     DBuf sm_hi, sm_lo, sm_node;
     DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
     DBuf mh, ml, mn, mraw, mpos;
-    DBuf bkb, uflag, upos;
+    DBuf bkb, uflag, upos, rk;
+    // incremental committed order: the last derivation's order (entry indices), per-entry changed
+    // flags (double-buffered with the entry arrays), the insertion's old -> new entry map
+    DBuf cm, chg[2], mv, af, ap, bfl, bps, cka, cva, ckb, cvb, ckb2, cvb2;
+    int chg_cur = 0;
+    uint64_t cm_n = 0;
+    bool cm_valid = false, moved = false;
     UpdCtl* h_ctl = nullptr;
     hipEvent_t ev[3] = {};
     ~CfkUpdWork()
@@ -775,6 +871,10 @@ struct CfkUpdWork {
 };
 
 CfkUpdWork* cfk_upd_work_create() { return new CfkUpdWork(); }
+void cfk_upd_work_invalidate(CfkUpdWork* w)
+{
+    if (w) w->cm_valid = false;
+}
 void cfk_upd_work_destroy(CfkUpdWork* w) { delete w; }
 
 static uint32_t bytes_of(uint64_t v)
@@ -794,11 +894,13 @@ static uint32_t bytes_of(uint64_t v)
         if (!(buf).ensure((bytes), (zero))) { *err = "device allocation (cfk update)"; return AD_E_NOMEM; } \
     } while (0)
 
+static uint32_t key_rank_mask(uint64_t n_dict, uint64_t nk);
+
 // Rebuild ent.tau, cand, cwr, w, krec, kent and the trees from the per-entry state (status,
 // executeAt rank). A duplicate committed executeAt is reported in ctl->err.
 static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkDerivedBufs* bufs,
                       int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*), void* need_ctx, hipStream_t st,
-                      std::string* err)
+                      std::string* err, bool incr = false)
 {
     const uint64_t ne = s.n_ent, nk = s.n_keys;
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
@@ -813,9 +915,30 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
     }
     UCHK(run_scan_arrays(w->flags.as<uint32_t>(), w->fs.as<uint64_t>(), ne, 4, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->fs.as<uint64_t>(), ne, 4, ctl->tot);
+    // incremental committed order: flags of the kept old entries and of the changed committed ones
+    const bool inc = incr && w->cm_valid && ne;
+    const uint64_t m0 = inc ? w->cm_n : 0;
+    const uint8_t* chg = w->chg[w->chg_cur].as<uint8_t>();
+    const uint32_t* mv = w->moved ? w->mv.as<uint32_t>() : nullptr;
+    if (inc)
+    {
+        UALLOC(w->af, 4 * std::max<uint64_t>(m0, 1), false);
+        UALLOC(w->ap, 8 * (m0 + 1), false);
+        UALLOC(w->bfl, 4 * ne, false);
+        UALLOC(w->bps, 8 * (ne + 1), false);
+        if (m0) k_cm_keep<<<blocks(m0), 256, 0, st>>>(m0, w->cm.as<uint32_t>(), mv, chg, w->af.as<uint32_t>());
+        UCHK(run_scan_arrays(w->af.as<uint32_t>(), w->ap.as<uint64_t>(), m0, 1, w->bsum.as<uint64_t>(), st));
+        k_drv_totals<<<1, 64, 0, st>>>(w->ap.as<uint64_t>(), m0, 1, ctl->cm);
+        k_cm_changed<<<blocks(ne), 256, 0, st>>>(ne, dd, chg, w->bfl.as<uint32_t>());
+        UCHK(run_scan_arrays(w->bfl.as<uint32_t>(), w->bps.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
+        k_drv_totals<<<1, 64, 0, st>>>(w->bps.as<uint64_t>(), ne, 1, ctl->cm + 1);
+        UCHK(hipGetLastError());
+    }
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t n_cand = w->h_ctl->tot[0] + w->h_ctl->tot[1] + w->h_ctl->tot[2], ncm = w->h_ctl->tot[3];
+    const uint64_t nA = inc ? w->h_ctl->cm[0] : 0, nB = inc ? w->h_ctl->cm[1] : 0;
+    const bool use_inc = inc && nA + nB == ncm;     // else (never expected) the full sort
     int rc = need(need_ctx, n_cand, ncm, ncm, bufs);
     if (rc) return rc;
     UALLOC(w->ck, 8 * std::max<uint64_t>(ncm, 1), false);
@@ -832,11 +955,39 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
     const uint64_t sb2 = (std::max<uint64_t>(std::max(ncm, hist_n), 1) + 1023) / 1024 + 8;
     UALLOC(w->bsum, 8ull * std::max<uint64_t>(4 * sb, 3 * sb2), false);
     if (ne)
-        k_drv_scatter<<<blocks(ne), 256, 0, st>>>(ne, dd, w->fs.as<uint64_t>(), ctl, bufs->cand, w->ck.as<uint64_t>(),
-                                                  w->cv.as<uint32_t>());
+        k_drv_scatter<<<blocks(ne), 256, 0, st>>>(ne, dd, w->fs.as<uint64_t>(), ctl, bufs->cand,
+                                                  use_inc ? nullptr : w->ck.as<uint64_t>(), w->cv.as<uint32_t>());
     uint64_t* ks = w->ck.as<uint64_t>();
     uint32_t* vs = w->cv.as<uint32_t>();
-    if (ncm > 1)
+    if (use_inc)
+    {
+        UALLOC(w->cka, 8 * std::max<uint64_t>(nA, 1), false);
+        UALLOC(w->cva, 4 * std::max<uint64_t>(nA, 1), false);
+        UALLOC(w->ckb, 8 * std::max<uint64_t>(nB, 1), false);
+        UALLOC(w->cvb, 4 * std::max<uint64_t>(nB, 1), false);
+        UALLOC(w->ckb2, 8 * std::max<uint64_t>(nB, 1), false);
+        UALLOC(w->cvb2, 4 * std::max<uint64_t>(nB, 1), false);
+        if (m0)
+            k_cm_compact<<<blocks(m0), 256, 0, st>>>(m0, w->cm.as<uint32_t>(), mv, w->af.as<uint32_t>(), w->ap.as<uint64_t>(), dd,
+                                                     w->cka.as<uint64_t>(), w->cva.as<uint32_t>());
+        k_cm_compact<<<blocks(ne), 256, 0, st>>>(ne, nullptr, nullptr, w->bfl.as<uint32_t>(), w->bps.as<uint64_t>(), dd,
+                                                 w->ckb.as<uint64_t>(), w->cvb.as<uint32_t>());
+        uint64_t* kb = w->ckb.as<uint64_t>();
+        uint32_t* vb = w->cvb.as<uint32_t>();
+        if (nB > 1)
+        {
+            const uint64_t hb = radix_hist_entries(nB);
+            UALLOC(w->hist, 4 * std::max(hist_n, hb), false);
+            UALLOC(w->hoff, 8 * (std::max(hist_n, hb) + 1), false);
+            UCHK(radix_sort_pairs(kb, vb, w->ckb2.as<uint64_t>(), w->cvb2.as<uint32_t>(), nB, key_rank_mask(s.n_dict, nk),
+                                  w->hist.as<uint32_t>(), w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &kb, &vb));
+        }
+        if (ncm)
+            k_cm_merge<<<(unsigned)((nA + 255) / 256 + (nB + 255) / 256), 256, 0, st>>>(nA, w->cka.as<uint64_t>(),
+                                                                                      w->cva.as<uint32_t>(), nB, kb, vb, ks, vs);
+        UCHK(hipGetLastError());
+    }
+    else if (ncm > 1)
     {
         uint32_t mask = 0;
         const uint32_t xb = bytes_of(2 * s.n_dict + 1), kb = bytes_of(nk ? nk - 1 : 0);
@@ -859,6 +1010,15 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
         k_drv_keys<<<blocks(nk), 256, 0, st>>>(nk, ne, ncm, dd, w->fs.as<uint64_t>(), w->s2.as<uint64_t>(), bufs->w,
                                                w->maw.as<int32_t>(), w->wtail.as<uint32_t>(), ctl);
     UCHK(hipGetLastError());
+    // keep this committed order for the next batch's incremental derivation
+    if (w->cm.cap < 4 * std::max<uint64_t>(ncm, 1))
+    {
+        UCHK(hipStreamSynchronize(st));       // the old order may still be read by queued kernels
+        UALLOC(w->cm, 4 * std::max<uint64_t>(ncm, 1), false);
+    }
+    if (ncm) UCHK(hipMemcpyAsync(w->cm.p, vs, 4 * ncm, hipMemcpyDeviceToDevice, st));
+    w->cm_n = ncm;
+    w->cm_valid = true;
     s.cand = bufs->cand;
     s.cwr = bufs->cwr;
     s.w = bufs->w;
@@ -932,7 +1092,8 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
     const uint64_t n = u.n, cap = 2 * n;
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
     UALLOC(w->nw, 8 * 4 * cap, false);
-    k_ins_collect<<<blocks(n), 256, 0, st>>>(s, ds, u, w->nw.as<uint64_t>(), cap, ctl);
+    UALLOC(w->rk, 8 * n, false);
+    k_ins_collect<<<blocks(n), 256, 0, st>>>(s, ds, u, w->nw.as<uint64_t>(), cap, w->rk.as<uint32_t>(), ctl);
     UCHK(hipGetLastError());
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
@@ -1054,11 +1215,14 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
                                                w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>());
     k_ins_before<<<blocks(nk + 1), 256, 0, st>>>(nk, w->gkey.as<uint32_t>(), G, w->ib.as<uint32_t>());
     UCHK(hipGetLastError());
-    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot}, b{};
+    UALLOC(w->chg[w->chg_cur ^ 1], ne + G, false);
+    UALLOC(w->mv, 4 * std::max<uint64_t>(ne, 1), false);
+    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot, w->chg[w->chg_cur].as<uint8_t>()}, b{};
+    b.chg = w->chg[w->chg_cur ^ 1].as<uint8_t>();
     if (int rc = grow.entries(grow.ctx, ne + G, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal)) { *err = "entry growth"; return rc; }
     const uint64_t padded = std::max<uint64_t>(64, (ne + G + 63) / 64 * 64);
     if (padded > ne + G) UCHK(hipMemsetAsync(b.ent + ne + G, 0, sizeof(uint2) * (padded - ne - G), st));
-    if (ne) k_ins_move_old<<<blocks(ne), 256, 0, st>>>(ne, a, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), b);
+    if (ne) k_ins_move_old<<<blocks(ne), 256, 0, st>>>(ne, a, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), b, w->mv.as<uint32_t>());
     k_ins_place<<<blocks(G), 256, 0, st>>>(G, w->gkey.as<uint32_t>(), w->grank.as<uint32_t>(), w->gword.as<unsigned long long>(),
                                            d.krec, a.ent, u, w->xr.as<uint32_t>(), b);
     if (nk)
@@ -1070,6 +1234,8 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     UCHK(hipGetLastError());
     const int src = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot);
     undo->swapped = true;         // the buffers are exchanged even when sizing the trees then failed
+    w->chg_cur ^= 1;              // the changed flags moved with the entries
+    w->moved = true;
     if (src) { *err = "entry swap"; return src; }
     s.ent = d.ent;
     s.n_ent = ne + G;
@@ -1116,6 +1282,10 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
     UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
     UCHK(hipEventRecord(w->ev[0], st));
+    // per-entry changed flags of this batch (incremental committed order) and no insertion map yet
+    UALLOC(w->chg[w->chg_cur], std::max<uint64_t>(s.n_ent, 1), false);
+    if (s.n_ent) UCHK(hipMemsetAsync(w->chg[w->chg_cur].p, 0, s.n_ent, st));
+    w->moved = false;
 
     // ---- 0. ids the dictionary does not hold join it. Ids newer than all of it are appended (no
     // rank changes): a batch that then fails drops them again (the arrays keep the bytes; nothing
@@ -1168,7 +1338,8 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     UALLOC(w->bsum, 8ull * 2 * ((n + 1023) / 1024 + 8), false);
     k_upd_locate<<<blocks(n), 256, 0, st>>>(s, dsm, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
                                             w->word.as<unsigned long long>(), w->ins_k.as<uint64_t>(),
-                                            w->uflag.as<uint32_t>(), ctl);
+                                            w->uflag.as<uint32_t>(), w->rk.as<uint32_t>(), out->merge_pos,
+                                            out->merged ? out->n_new_ids : 0, ctl);
     UCHK(hipGetLastError());
     UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), n, nf, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), n, nf, ctl->tot3);
@@ -1213,12 +1384,12 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
                                           w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
             }
             k_fold_present<<<blocks(mp), 256, 0, st>>>(mp, ks, vs, u, w->xr.as<uint32_t>(), d, w->bk.as<uint2>(),
-                                                       w->bkb.as<Bal>(), ctl);
+                                                       w->bkb.as<Bal>(), w->chg[w->chg_cur].as<uint8_t>(), ctl);
         }
     }
     else
         k_upd_apply<<<blocks(n), 256, 0, st>>>(n, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(), w->word.as<unsigned long long>(),
-                                               d, w->bk.as<uint2>(), w->bkb.as<Bal>(), ctl);
+                                               d, w->bk.as<uint2>(), w->bkb.as<Bal>(), w->chg[w->chg_cur].as<uint8_t>(), ctl);
     UCHK(hipGetLastError());
     if (q)   // the insertion updates in batch order, for insert_entries
         k_compact<<<blocks(n), 256, 0, st>>>(n, w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), w->ins_k.as<uint64_t>(),
@@ -1252,8 +1423,8 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         if (int rc = insert_entries(w, s, d, u, grow, st, q, &G, &undo, err)) return rollback(rc);
     UCHK(hipEventRecord(w->ev[1], st));
 
-    // ---- 2. re-derive the snapshot arrays from the per-entry state
-    if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rollback(rc);
+    // ---- 2. re-derive the snapshot arrays from the per-entry state (committed order incrementally)
+    if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err, true)) return rollback(rc);
     UCHK(hipEventRecord(w->ev[2], st));
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));

@@ -90,6 +90,8 @@ struct CfkUpdOut {
 struct CfkUpdWork;
 CfkUpdWork* cfk_upd_work_create();
 void cfk_upd_work_destroy(CfkUpdWork* w);
+// the snapshot was rebuilt outside run_cfk_update: drop state kept between batches
+void cfk_upd_work_invalidate(CfkUpdWork* w);
 
 // Applies the batch (AD_E_* on failure with the store unchanged; message in *err).
 // `need` is called with the sizes the derived arrays need; it must return buffers at least that
