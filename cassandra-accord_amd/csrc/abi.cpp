@@ -1022,6 +1022,18 @@ static int sync_host(ad_ctx* c)
             K.exec[e] = xr[e] == tr ? K.txn[e] : tid(xr[e]);
         }
         for (uint64_t k = 0; k < nk; ++k) K.seg[k + 1] = kr[k].seg_hi;
+        // prunedBefore as an index into the key's byId (insertions may have moved it), and its rank
+        if (!K.pruned.empty())
+            for (uint64_t k = 0; k < nk; ++k)
+            {
+                K.pruned[k] = -1;
+                if (!kr[k].pruned) continue;
+                const auto b = c->h_txn_rank.begin();
+                const auto it = std::lower_bound(b + kr[k].seg_lo, b + kr[k].seg_hi, kr[k].pruned);
+                if (it != b + kr[k].seg_hi && *it == kr[k].pruned) K.pruned[k] = (int64_t)(it - (b + kr[k].seg_lo));
+            }
+        if (c->h_pruned.size() == nk)
+            for (uint64_t k = 0; k < nk; ++k) c->h_pruned[k] = kr[k].pruned;
         c->h_exec_rank.swap(xr);
         if (!K.miss_off.empty()) K.miss_stale = true;       // entries moved: load the lists again
         c->host_moved = false;

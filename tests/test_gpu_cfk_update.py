@@ -258,6 +258,45 @@ def test_insert_older_ids(oracle, seed, path):
         st.close()
 
 
+def _sequential_check(w, st, oracle, cfk, rng, epoch=12):
+    """A SEQUENTIAL batch of newer PreAccepts over the store as updated (the host copy follows the
+    device, prunedBefore included, before inserting the batch): bit-exact vs the oracle."""
+    from accord_deps.model import Queries
+    q = G.fresh_preaccepts(cfk, rng, 30, epoch=epoch)
+    rows = np.r_[0, np.nonzero(np.diff(q.txn.lsb.astype(np.int64)))[0] + 1]
+    off = np.r_[rows, len(q)].astype(np.uint64)
+    keys = np.concatenate([np.sort(q.keys[int(off[i]):int(off[i + 1])]) for i in range(len(rows))])
+    old_q, old_cfk, old_flags = w.queries, w.cfk, w.flags
+    w.queries = Queries(q.txn.take(rows), q.txn.take(rows), off, keys)
+    w.cfk = cfk
+    try:
+        w.flags = A.AD_SEQUENTIAL
+        exp = oracle.resolve(w)
+        got = st.calculate_partial_deps(w.queries, A.AD_SEQUENTIAL)
+        ok, why = got.equals(exp, detail=True)
+        assert ok, why
+    finally:
+        w.queries, w.cfk, w.flags = old_q, old_cfk, old_flags
+
+
+def test_insert_older_then_sequential(oracle):
+    # mid-segment inserts move prunedBefore's byId index: a host rebuild must find it again
+    for seed in range(4):
+        w = synth.random_small(90 + seed, n_range_cmds=0)
+        w.flags = A.AD_SNAPSHOT
+        rng = np.random.default_rng(90 + seed)
+        st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+        try:
+            st.load(w)
+            u = G.older_inserts(w.cfk, rng, 40, statuses=(0, 2, 3))
+            new, _ = U.cfk_update(w.cfk, u)
+            st.cfk_update(u)
+            _check(w, st, oracle, new)
+            _sequential_check(w, st, oracle, new, rng)
+        finally:
+            st.close()
+
+
 def test_insert_older_than_key_and_unknown_exec(oracle):
     w = synth.random_small(50)
     w.flags = A.AD_SNAPSHOT
