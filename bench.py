@@ -752,8 +752,9 @@ def bench_steady(args, rank, world, local, dev):
     R = max(1, int(args.steady * s))
     T = int(args.steady_transitions * s) if args.steady_transitions >= 0 else R
     n_b = args.warmup + args.steps
-    # requests on keys the store already holds (ad_cfk_update does not create a CommandsForKey)
-    stream = synth.config2_stream(w, n_b, R, seed=0xACC0D5EE + rank, held_keys_only=True)
+    # Zipf over the whole key space: keys the store has never seen get their CommandsForKey from the
+    # update that registers their first txn
+    stream = synth.config2_stream(w, n_b, R, seed=0xACC0D5EE + rank)
     cfk = w.cfk
     from accord_deps.model import CfkUpdates, Tids
     rng = np.random.default_rng(0xACC0D01E)

@@ -207,6 +207,12 @@ struct ad_ctx {
     DevBuf d_ds_hi, d_ds_lo, d_ds_node;            // every DICT_SAMP-th dictionary id (rank searches)
     DevBuf d_kline, d_kslot, d_kcell, d_kl_disp;   // KeyLine table; per key its line and stabbing cell; displacements
     uint64_t kline_slots = 0;
+    // host state of the KeyLine perfect hash (incremental placement of new keys)
+    std::vector<uint32_t> kl_disp_h;
+    std::vector<uint8_t> kl_used;
+    std::vector<std::vector<int64_t>> kl_members;
+    uint64_t kl_nb_h = 0;
+    DevBuf d_keys2, d_krec2, d_kcell2, d_khash2, d_kent2;   // spare key-indexed arrays (new keys)
 
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
@@ -350,6 +356,130 @@ static void drop_global_dict(ad_ctx* c)
     std::vector<uint64_t>().swap(c->gd_msb);
     std::vector<uint64_t>().swap(c->gd_lsb);
     std::vector<int32_t>().swap(c->gd_node);
+}
+
+// The KeyLine perfect hash (hash and displace): every bucket gets the first displacement that puts
+// all its keys on free lines, biggest buckets first; the table grows by half when a bucket does not
+// fit. Keeps the host state (displacements, used lines, bucket members) for incremental placement.
+static int kl_place_all(ad_ctx* c, const std::vector<int64_t>& keys, uint64_t nb, bool sparse)
+{
+    const uint64_t nk = keys.size();
+    // a snapshot's table is 80 % full (the lean kernels' lines stay dense); once keys arrive through
+    // updates it is rebuilt half full, where a bucket of ~4 keys is placed again in ~16 displacement
+    // tries (kl_add_keys)
+    uint64_t m = std::max<uint64_t>(1, sparse ? 2 * nk : nk + nk / 4);
+    std::vector<std::vector<int64_t>> members(nb);
+    for (int64_t key : keys) members[kl_bucket(key_hash(key), nb)].push_back(key);
+    std::vector<uint32_t> border(nb);
+    for (uint64_t b = 0; b < nb; ++b) border[b] = (uint32_t)b;
+    std::stable_sort(border.begin(), border.end(), [&](uint32_t a, uint32_t b) { return members[a].size() > members[b].size(); });
+    std::vector<uint32_t> disp(nb, 0);
+    for (int attempt = 0;; ++attempt)
+    {
+        std::vector<uint8_t> used(m, 0);
+        bool ok = true;
+        std::vector<uint64_t> pos;
+        for (uint32_t b : border)
+        {
+            const auto& mb = members[b];
+            if (mb.empty()) continue;
+            uint32_t d = 0;
+            for (;; ++d)
+            {
+                if (d == (1u << 22)) { ok = false; break; }
+                pos.clear();
+                bool fit = true;
+                for (size_t i = 0; i < mb.size() && fit; ++i)
+                {
+                    const uint64_t p = kl_index(key_hash2(mb[i]), d, m);
+                    if (used[p] || std::find(pos.begin(), pos.end(), p) != pos.end()) fit = false;
+                    pos.push_back(p);
+                }
+                if (fit) break;
+            }
+            if (!ok) break;
+            disp[b] = d;
+            for (uint64_t p : pos) used[p] = 1;
+        }
+        if (ok)
+        {
+            c->kl_used.swap(used);
+            break;
+        }
+        if (attempt == 4) return c->fail(AD_E_DEVICE, "key perfect hash did not converge");
+        m += m / 2;              // more room, try again
+    }
+    c->kline_slots = m;
+    c->kl_nb_h = nb;
+    c->kl_disp_h.swap(disp);
+    c->kl_members.swap(members);
+    return 0;
+}
+
+// New keys into the perfect hash: a bucket keeps its displacement when its new keys land on free
+// lines, else it is placed again (its old lines freed first); a bucket that does not fit, or a table
+// above 70 % load, rebuilds the whole hash. Returns whether the table was rebuilt (size may change).
+static int kl_add_keys(ad_ctx* c, const std::vector<int64_t>& nkeys, uint64_t nk_total, bool* need_rebuild)
+{
+    *need_rebuild = false;
+    const uint64_t nb = c->kl_nb_h, m = c->kline_slots;
+    if (nb == 0 || 10 * nk_total > 7 * m)
+    {
+        *need_rebuild = true;
+        return 0;
+    }
+    std::vector<std::pair<uint32_t, int64_t>> adds;
+    adds.reserve(nkeys.size());
+    for (int64_t key : nkeys) adds.push_back({(uint32_t)kl_bucket(key_hash(key), nb), key});
+    std::sort(adds.begin(), adds.end());
+    std::vector<uint64_t> pos;
+    for (size_t i = 0; i < adds.size();)
+    {
+        const uint32_t b = adds[i].first;
+        size_t j = i;
+        while (j < adds.size() && adds[j].first == b) ++j;
+        auto& mb = c->kl_members[b];
+        const uint32_t d0 = c->kl_disp_h[b];
+        // 1. the new keys on free lines under the bucket's displacement
+        pos.clear();
+        bool fit = true;
+        for (size_t x = i; x < j && fit; ++x)
+        {
+            const uint64_t p = kl_index(key_hash2(adds[x].second), d0, m);
+            if (c->kl_used[p] || std::find(pos.begin(), pos.end(), p) != pos.end()) fit = false;
+            pos.push_back(p);
+        }
+        if (!fit)
+        {
+            // 2. place the bucket again
+            for (int64_t key : mb) c->kl_used[kl_index(key_hash2(key), d0, m)] = 0;
+            std::vector<int64_t> allb(mb);
+            for (size_t x = i; x < j; ++x) allb.push_back(adds[x].second);
+            uint32_t d = 0;
+            for (;; ++d)
+            {
+                if (d == (1u << 20))
+                {
+                    *need_rebuild = true;
+                    return 0;
+                }
+                pos.clear();
+                fit = true;
+                for (size_t x = 0; x < allb.size() && fit; ++x)
+                {
+                    const uint64_t p = kl_index(key_hash2(allb[x]), d, m);
+                    if (c->kl_used[p] || std::find(pos.begin(), pos.end(), p) != pos.end()) fit = false;
+                    pos.push_back(p);
+                }
+                if (fit) break;
+            }
+            c->kl_disp_h[b] = d;
+        }
+        for (uint64_t p : pos) c->kl_used[p] = 1;
+        for (size_t x = i; x < j; ++x) mb.push_back(adds[x].second);
+        i = j;
+    }
+    return 0;
 }
 
 static int build_snapshot(ad_ctx* c)
@@ -766,57 +896,10 @@ static int build_snapshot(ad_ctx* c)
     // perfect hash of the keys onto KeyLines (hash and displace, common.hpp): buckets of ~4 keys,
     // the biggest placed first, each with the first displacement that puts all its keys on free lines
     uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
-    std::vector<uint32_t> kl_disp(kl_nb, 0);
-    {
-        uint64_t m = std::max<uint64_t>(1, nk + nk / 4);
-        std::vector<uint64_t> bo(kl_nb + 1, 0);
-        std::vector<uint32_t> bk(nk);
-        for (uint64_t k = 0; k < nk; ++k) ++bo[kl_bucket(key_hash(K.keys[k]), kl_nb) + 1];
-        for (uint64_t b = 0; b < kl_nb; ++b) bo[b + 1] += bo[b];
-        {
-            std::vector<uint64_t> cur(bo.begin(), bo.end() - 1);
-            for (uint64_t k = 0; k < nk; ++k) bk[cur[kl_bucket(key_hash(K.keys[k]), kl_nb)]++] = (uint32_t)k;
-        }
-        std::vector<uint32_t> border(kl_nb);
-        for (uint64_t b = 0; b < kl_nb; ++b) border[b] = (uint32_t)b;
-        std::stable_sort(border.begin(), border.end(), [&](uint32_t a, uint32_t b) { return bo[a + 1] - bo[a] > bo[b + 1] - bo[b]; });
-        for (int attempt = 0;; ++attempt)
-        {
-            std::vector<uint8_t> used(m, 0);
-            bool ok = true;
-            std::vector<uint64_t> pos;
-            for (uint32_t b : border)
-            {
-                const uint64_t b0 = bo[b], b1 = bo[b + 1];
-                if (b0 == b1) continue;
-                uint32_t d = 0;
-                for (;; ++d)
-                {
-                    if (d == (1u << 22)) { ok = false; break; }
-                    pos.clear();
-                    bool fit = true;
-                    for (uint64_t i = b0; i < b1 && fit; ++i)
-                    {
-                        const uint64_t p = kl_index(key_hash2(K.keys[bk[i]]), d, m);
-                        if (used[p] || std::find(pos.begin(), pos.end(), p) != pos.end()) fit = false;
-                        pos.push_back(p);
-                    }
-                    if (fit) break;
-                }
-                if (!ok) break;
-                kl_disp[b] = d;
-                for (uint64_t i = b0; i < b1; ++i)
-                {
-                    used[pos[i - b0]] = 1;
-                    kslot[bk[i]] = (uint32_t)pos[i - b0];
-                }
-            }
-            if (ok) break;
-            if (attempt == 4) return c->fail(AD_E_DEVICE, "key perfect hash did not converge");
-            m += m / 2;              // more room, try again
-        }
-        c->kline_slots = m;
-    }
+    if (int rc = kl_place_all(c, K.keys, kl_nb, false)) return rc;
+    for (uint64_t k = 0; k < nk; ++k)
+        kslot[k] = (uint32_t)kl_index(key_hash2(K.keys[k]), c->kl_disp_h[kl_bucket(key_hash(K.keys[k]), kl_nb)], c->kline_slots);
+    const std::vector<uint32_t>& kl_disp = c->kl_disp_h;
     for (uint64_t k = 0; k < nk; ++k)
     {
         uint64_t h = key_hash(K.keys[k]) & (hcap - 1);
@@ -1006,6 +1089,15 @@ static int sync_host(ad_ctx* c)
             HIPCHK(c, hipMemcpyAsync(xr.data(), c->d_xrank.p, 4 * ne, hipMemcpyDeviceToHost, c->stream));
         }
         if (nk) HIPCHK(c, hipMemcpyAsync(kr.data(), c->d_krec.p, sizeof(KeyRec) * nk, hipMemcpyDeviceToHost, c->stream));
+        if (K.keys.size() != nk)
+        {
+            // keys created on the device
+            K.keys.resize(nk);
+            if (nk) HIPCHK(c, hipMemcpyAsync(K.keys.data(), c->d_keys.p, 8 * nk, hipMemcpyDeviceToHost, c->stream));
+            K.seg.assign(nk + 1, 0);
+            if (!K.pruned.empty()) K.pruned.assign(nk, -1);
+            c->h_pruned.assign(nk, 0);
+        }
         HIPCHK(c, hipStreamSynchronize(c->stream));
         auto tid = [&](uint32_t rank) -> Tid {
             const uint64_t i = (rank - 1) / 2;
@@ -2674,6 +2766,67 @@ static int cfk_ballot_init(void* vc, uint64_t ne, Bal** bal)
     return 0;
 }
 
+static int cfk_keys_spare(void* vc, uint64_t nk, KeyBufs* b)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    uint64_t hcap = 16;
+    while (hcap < 2 * nk) hcap <<= 1;
+    const uint64_t slack = nk / 8;
+    if (!c->d_keys2.ensure(8 * (nk + slack)) || !c->d_krec2.ensure(sizeof(KeyRec) * (nk + slack)) ||
+        !c->d_kcell2.ensure(4 * (nk + slack)) || !c->d_khash2.ensure(sizeof(KeySlot) * hcap) ||
+        !c->d_kent2.ensure(sizeof(KeyEntry) * (nk + slack)))
+        return AD_E_NOMEM;
+    *b = KeyBufs{c->d_keys2.as<int64_t>(), c->d_krec2.as<KeyRec>(), c->d_kcell2.as<uint32_t>(), c->d_khash2.as<KeySlot>(),
+                 c->d_kent2.as<KeyEntry>(), hcap};
+    return 0;
+}
+
+static int cfk_keys_swap(void* vc, KeyBufs* b)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    swap_buf(c->d_keys, c->d_keys2);
+    swap_buf(c->d_krec, c->d_krec2);
+    swap_buf(c->d_kcell, c->d_kcell2);
+    swap_buf(c->d_khash, c->d_khash2);
+    swap_buf(c->d_kent, c->d_kent2);
+    b->keys = c->d_keys.as<int64_t>();
+    b->krec = c->d_krec.as<KeyRec>();
+    b->kcell = c->d_kcell.as<uint32_t>();
+    b->khash = c->d_khash.as<KeySlot>();
+    b->kent = c->d_kent.as<KeyEntry>();
+    return 0;
+}
+
+// After new keys on the device: the KeyLine perfect hash takes them (incrementally on the host),
+// displacements uploaded, every key's line recomputed on the device.
+static int cfk_after_new_keys(ad_ctx* c, const CfkUpdOut& o, hipStream_t st)
+{
+    const uint64_t nk = c->ds.n_keys, U = o.n_new_keys;
+    std::vector<int64_t> nkeys(U);
+    HIPCHK(c, hipMemcpyAsync(nkeys.data(), o.new_keys, 8 * U, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    bool rebuild = false;
+    if (int rc = kl_add_keys(c, nkeys, nk, &rebuild)) return rc;
+    if (rebuild)
+    {
+        // the whole table again, half full (every key of the store, from the device)
+        std::vector<int64_t> all(nk);
+        HIPCHK(c, hipMemcpy(all.data(), c->d_keys.p, 8 * nk, hipMemcpyDeviceToHost));
+        if (int rc = kl_place_all(c, all, std::max<uint64_t>(1, nk / 4), true)) return rc;
+    }
+    if (int rc = upload(c, c->d_kl_disp, c->kl_disp_h)) return rc;
+    if (!c->d_kslot.ensure(4 * nk + 4 * (nk / 8))) return c->fail(AD_E_NOMEM, "key slots");
+    if (!c->d_kline.ensure(sizeof(KeyLine) * c->kline_slots)) return c->fail(AD_E_NOMEM, "key lines");
+    DevSnapshot& s = c->ds;
+    s.kline = c->d_kline.as<KeyLine>();
+    s.kl_lines = c->kline_slots;
+    s.kl_buckets = c->kl_nb_h;
+    s.kl_disp = c->d_kl_disp.as<uint32_t>();
+    HIPCHK(c, run_key_slots(c->d_keys.as<int64_t>(), nk, c->d_kl_disp.as<uint32_t>(), c->kl_nb_h, c->kline_slots,
+                            c->d_kslot.as<uint32_t>(), st));
+    return 0;
+}
+
 static int cfk_dict_spare(void* vc, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw)
 {
     ad_ctx* c = (ad_ctx*)vc;
@@ -2743,9 +2896,18 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
     std::string e;
     const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
                        c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
-                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb};
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, cfk_keys_spare, cfk_keys_swap,
+                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
     const uint64_t nd0 = c->dict_msb.size();
     const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e);
+    if (o.n_new_keys)
+    {
+        // keys created on the device (they stay when the batch then failed): KeyLines, host copies
+        if (int rc2 = cfk_after_new_keys(c, o, st)) return rc2;
+        c->host_moved = true;
+        c->host_stale = true;
+        ++c->snap_gen;
+    }
     if (o.merged)
     {
         // ids merged into the device dictionary (they stay when the batch then failed): host copies

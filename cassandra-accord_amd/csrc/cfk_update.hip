@@ -54,6 +54,7 @@ struct UpdCtl {
     unsigned long long diff[3];   // OR of (word ^ reference) over the new ids: node, lo, hi (sort digits)
     uint32_t older, pad;      // a new id is older than the newest dictionary id (dictionary merge)
     uint64_t cm[2];           // incremental committed order: entries kept from the last one, changed committed entries
+    uint32_t n_newk, pad2;    // update keys without a CommandsForKey (with repeats)
 };
 constexpr uint32_t LOC_NONE = 0xFFFFFFFFu;
 
@@ -419,6 +420,121 @@ __global__ void k_remap_cells(uint64_t n, uint64_t* cell, const uint64_t* pos, u
     const uint64_t v = cell[i];
     const uint32_t y = (uint32_t)v;
     cell[i] = (v & 0xFFFFFFFF00000000ull) | ((y & ~RANK_MASK) | remap_rank(y & RANK_MASK, pos, U));
+}
+
+// ---- keys without a CommandsForKey: the update creates one (an empty byId the insertion then
+// fills). New keys are merged into the sorted key array; every key index moves up by the new keys
+// below it (monotone: segments keep their order), the key hash is rebuilt.
+__device__ inline uint32_t key_index(const DevSnapshot& s, int64_t key)
+{
+    if (!s.n_keys) return KEY_EMPTY;
+    uint64_t h = key_hash(key) & s.khash_mask;
+    for (;;)
+    {
+        const KeySlot sl = s.khash[h];
+        if (sl.idx == KEY_EMPTY) return KEY_EMPTY;
+        if (sl.key == key) return sl.idx;
+        h = (h + 1) & s.khash_mask;
+    }
+}
+
+__global__ void k_key_collect(DevSnapshot s, CfkUpdIn u, uint64_t* out, UpdCtl* ctl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u.n) return;
+    const int64_t key = u.keys[i];
+    if (key_index(s, key) != KEY_EMPTY) return;
+    out[atomicAdd(&ctl->n_newk, 1u)] = (uint64_t)key ^ 0x8000000000000000ull;     // unsigned sort order
+}
+
+__global__ void k_key_unique(const uint64_t* ks, uint64_t m, uint32_t* flag)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < m) flag[r] = (r == 0 || ks[r] != ks[r - 1]) ? 1u : 0u;
+}
+
+// the unique new keys (sorted) and their lower bounds among the old keys
+__global__ void k_key_place(DevSnapshot s, const uint64_t* ks, uint64_t m, const uint32_t* flag, const uint64_t* pos_in,
+                            int64_t* nkeys, uint64_t* kpos)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m || !flag[r]) return;
+    const int64_t key = (int64_t)(ks[r] ^ 0x8000000000000000ull);
+    uint64_t lo = 0, hi = s.n_keys;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (s.keys[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    nkeys[pos_in[r]] = key;
+    kpos[pos_in[r]] = lo;
+}
+
+__global__ __launch_bounds__(256) void k_key_move(DevSnapshot s, const uint32_t* kcell, const uint64_t* kpos, uint64_t U,
+                                                  KeyBufs nb)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= s.n_keys) return;
+    const uint64_t p = k + merged_before(kpos, U, k);
+    nb.keys[p] = s.keys[k];
+    nb.krec[p] = s.krec[k];
+    nb.kcell[p] = kcell ? kcell[k] : NO_CELL;
+}
+
+__global__ void k_key_new(DevSnapshot s, const int64_t* nkeys, const uint64_t* kpos, uint64_t U, KeyBufs nb)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= U) return;
+    const uint64_t p = kpos[j] + j;
+    const int64_t key = nkeys[j];
+    const uint32_t at = kpos[j] < s.n_keys ? s.krec[kpos[j]].seg_lo : (uint32_t)s.n_ent;
+    KeyRec r;
+    r.seg_lo = r.seg_hi = at;
+    r.w_lo = r.w_hi = 0;
+    r.last_txn = r.last_wexec = r.pruned = 0;
+    r.maw = -1;
+    nb.keys[p] = key;
+    nb.krec[p] = r;
+    uint32_t cell = NO_CELL;
+    if (s.cell_off)
+    {
+        // the key's cell of the range stabbing index (as the ingest places it)
+        uint64_t lo = 0, hi = s.n_cell_E;
+        while (lo < hi)
+        {
+            const uint64_t mid = (lo + hi) >> 1;
+            const int64_t v = s.cell_E[mid];
+            if (s.start_inclusive ? v <= key : v < key) lo = mid + 1;
+            else hi = mid;
+        }
+        cell = (uint32_t)lo;
+    }
+    nb.kcell[p] = cell;
+}
+
+__global__ __launch_bounds__(256) void k_ekey_remap(uint64_t ne, uint32_t* ekey, const uint64_t* kpos, uint64_t U)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < ne) ekey[e] += (uint32_t)merged_before(kpos, U, ekey[e]);
+}
+
+__global__ void k_khash_clear(KeySlot* h, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) h[i] = KeySlot{0, KEY_EMPTY, NO_CELL};
+}
+
+__global__ void k_khash_fill(uint64_t nk, KeyBufs nb)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    const int64_t key = nb.keys[k];
+    const uint64_t mask = nb.hcap - 1;
+    uint64_t h = key_hash(key) & mask;
+    while (atomicCAS(&nb.khash[h].idx, KEY_EMPTY, (uint32_t)k) != KEY_EMPTY) h = (h + 1) & mask;
+    nb.khash[h].key = key;
+    nb.khash[h].cell = nb.kcell[k];
 }
 
 // insertion updates sorted by (key index, txn rank): group starts
@@ -854,6 +970,7 @@ struct CfkUpdWork {
     DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
     DBuf mh, ml, mn, mraw, mpos;
     DBuf bkb, uflag, upos, rk;
+    DBuf kn_a, kn_b, kv_a, kv_b, kflag, kfpos, knew, kpos;   // new keys
     // incremental committed order: the last derivation's order (entry indices), per-entry changed
     // flags (double-buffered with the entry arrays), the insertion's old -> new entry map
     DBuf cm, chg[2], mv, af, ap, bfl, bps, cka, cva, ckb, cvb, ckb2, cvb2;
@@ -1034,6 +1151,71 @@ static uint32_t key_rank_mask(uint64_t n_dict, uint64_t nk)
     for (uint32_t b = 0; b < xb && b < 4; ++b) mask |= 1u << b;
     for (uint32_t b = 0; b < kb && b < 4; ++b) mask |= 1u << (4 + b);
     return mask;
+}
+
+// Keys of the batch without a CommandsForKey: merged into the key arrays (spare buffers), entry key
+// indices remapped, key hash rebuilt.
+static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, const CfkGrow& grow, hipStream_t st,
+                    CfkUpdOut* out, std::string* err)
+{
+    const uint64_t n = u.n, nk = s.n_keys, ne = s.n_ent;
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UALLOC(w->kn_a, 8 * n, false);
+    k_key_collect<<<blocks(n), 256, 0, st>>>(s, u, w->kn_a.as<uint64_t>(), ctl);
+    UCHK(hipGetLastError());
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    const uint64_t m = w->h_ctl->n_newk;
+    if (m == 0) return AD_OK;
+    UALLOC(w->kn_b, 8 * m, false);
+    UALLOC(w->kv_a, 4 * m, false);
+    UALLOC(w->kv_b, 4 * m, false);
+    UALLOC(w->kflag, 4 * m, false);
+    UALLOC(w->kfpos, 8 * (m + 1), false);
+    const uint64_t hist_n = radix_hist_entries(m);
+    UALLOC(w->hist, 4 * hist_n, false);
+    UALLOC(w->hoff, 8 * (hist_n + 1), false);
+    UALLOC(w->bsum, 8 * ((std::max(hist_n, m) + 1023) / 1024 + 8), false);
+    uint64_t* ks = w->kn_a.as<uint64_t>();
+    uint32_t* vs = w->kv_a.as<uint32_t>();
+    k_iota<<<blocks(m), 256, 0, st>>>(vs, m);
+    if (m > 1)
+        UCHK(radix_sort_pairs(ks, vs, w->kn_b.as<uint64_t>(), w->kv_b.as<uint32_t>(), m, 0xFFu, w->hist.as<uint32_t>(),
+                              w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
+    k_key_unique<<<blocks(m), 256, 0, st>>>(ks, m, w->kflag.as<uint32_t>());
+    UCHK(run_scan_arrays(w->kflag.as<uint32_t>(), w->kfpos.as<uint64_t>(), m, 1, w->bsum.as<uint64_t>(), st));
+    k_drv_totals<<<1, 64, 0, st>>>(w->kfpos.as<uint64_t>(), m, 1, &ctl->tot3[0]);
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    const uint64_t U = w->h_ctl->tot3[0];
+    if (nk + U >= KEY_EMPTY) { *err = "more than 2^32-1 keys"; return AD_E_CAPACITY; }
+    UALLOC(w->knew, 8 * U, false);
+    UALLOC(w->kpos, 8 * U, false);
+    k_key_place<<<blocks(m), 256, 0, st>>>(s, ks, m, w->kflag.as<uint32_t>(), w->kfpos.as<uint64_t>(), w->knew.as<int64_t>(),
+                                           w->kpos.as<uint64_t>());
+    KeyBufs nb{};
+    if (int rc = grow.keys_spare(grow.ctx, nk + U, &nb)) { *err = "key arrays"; return rc; }
+    const uint64_t* kpos = w->kpos.as<uint64_t>();
+    if (nk) k_key_move<<<blocks(nk), 256, 0, st>>>(s, grow.kcell, kpos, U, nb);
+    k_key_new<<<blocks(U), 256, 0, st>>>(s, w->knew.as<int64_t>(), kpos, U, nb);
+    if (ne) k_ekey_remap<<<blocks(ne), 256, 0, st>>>(ne, d.ekey, kpos, U);
+    k_khash_clear<<<blocks(nb.hcap), 256, 0, st>>>(nb.khash, nb.hcap);
+    k_khash_fill<<<blocks(nk + U), 256, 0, st>>>(nk + U, nb);
+    UCHK(hipGetLastError());
+    if (int rc = grow.keys_swap(grow.ctx, &nb)) { *err = "key arrays"; return rc; }
+    UCHK(hipStreamSynchronize(st));
+    s.n_keys = nk + U;
+    s.keys = nb.keys;
+    s.krec = nb.krec;
+    s.khash = nb.khash;
+    s.khash_mask = nb.hcap - 1;
+    s.kent = nb.kent;
+    d.krec = nb.krec;
+    d.kent = nb.kent;
+    out->n_new_keys = U;
+    out->new_keys = w->knew.as<int64_t>();
+    out->key_pos = kpos;
+    return AD_OK;
 }
 
 // Merge the sorted unique new ids (nflag/npos over the sorted order vs) into the dictionary: new
@@ -1260,7 +1442,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         int rc = AD_E_INVAL;
         switch (code)
         {
-            case UE_KEY: what = "key is not in the store's snapshot"; break;
+            case UE_KEY: what = "key missing from the key arrays after its creation (internal)"; rc = AD_E_STATE; break;
             case UE_STATUS: what = "status is not an InternalStatus ordinal"; break;
             case UE_ABSENT: what = "txnId missing from the id dictionary after its merge (internal)"; rc = AD_E_STATE; break;
             case UE_NEW_EXEC: what = "executeAt missing from the id dictionary after its merge (internal)"; rc = AD_E_STATE; break;
@@ -1312,9 +1494,10 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
                                                           w->sm_node.as<int32_t>(), n_samp);
         return DictSample{w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(), w->sm_node.as<int32_t>(), n_samp};
     };
-    // a failure after a merge: the entries are as they were, under the new ranks; derive again
+    // a failure after a merge or new keys: the entries are as they were, under the new ranks /
+    // key indices; derive again
     auto rederive = [&](int code) -> int {
-        if (!out->merged) return code;
+        if (!out->merged && !out->n_new_keys) return code;
         std::string e2;
         if (hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st) != hipSuccess) { *err += "; re-derivation failed"; return AD_E_DEVICE; }
         if (int rc2 = cfk_derive(w, s, d, bufs, need, need_ctx, st, &e2)) { *err += "; re-derivation: " + e2; return rc2; }
@@ -1322,6 +1505,8 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         out->rederived = true;
         return code;
     };
+    if (int rc = add_keys(w, s, d, u, grow, st, out, err)) return rc == AD_E_CAPACITY ? rc : rederive(rc);
+    if (out->n_new_keys) UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
     {
         const DictSample ds0 = sample();
         if (int rc = grow_dictionary(w, s, d, ds0, u, grow, st, out, err))

@@ -50,6 +50,12 @@ struct CfkDerivedBufs {
     uint2* w; uint64_t w_cap;
 };
 
+// Key-indexed arrays of a snapshot (new keys: spare buffers sized by keys_spare)
+struct KeyBufs {
+    int64_t* keys; KeyRec* krec; uint32_t* kcell; KeySlot* khash; KeyEntry* kent;
+    uint64_t hcap;                 // KeySlot slots (a power of two)
+};
+
 // Buffer growth for insertions (owned by the caller; all pointers device memory).
 struct CfkGrow {
     void* ctx;
@@ -72,6 +78,12 @@ struct CfkGrow {
     uint32_t* r_txw; uint64_t n_rtxw;
     uint64_t* cell_ent; uint64_t n_cell_ent;
     uint32_t* rb_wm; uint64_t n_rb;
+    // new keys (a CommandsForKey created by the update): spare key-indexed arrays for nk keys and a
+    // key hash of at least 2 nk slots; keys_swap makes them current. kcell: the current per-key
+    // stabbing cells (NO_CELL without a stabbing index)
+    int (*keys_spare)(void* ctx, uint64_t nk, KeyBufs* b);
+    int (*keys_swap)(void* ctx, KeyBufs* b);
+    const uint32_t* kcell;
 };
 
 struct CfkUpdOut {
@@ -83,6 +95,11 @@ struct CfkUpdOut {
     bool merged = false;
     const uint64_t* merge_pos = nullptr;   // device, [n_new_ids] ascending
     bool rederived = false;        // the derived arrays were rebuilt although the batch failed
+    // keys the batch created (they stand when the batch then fails: an empty CommandsForKey is no
+    // CommandsForKey to every reader): device, sorted, and their lower bounds among the old keys
+    uint64_t n_new_keys = 0;
+    const int64_t* new_keys = nullptr;
+    const uint64_t* key_pos = nullptr;
     bool rolled_back = false;      // the batch failed after it had been applied and was undone
     double ms_locate = 0, ms_derive = 0, ms_total = 0;
 };

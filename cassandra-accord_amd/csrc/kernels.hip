@@ -1658,6 +1658,21 @@ __global__ __launch_bounds__(256) void k_build_klines(DevSnapshot s, const uint3
     out[kslot[k]] = L;
 }
 
+__global__ void k_key_slots(const int64_t* __restrict__ keys, uint64_t nk, const uint32_t* __restrict__ disp, uint64_t nb,
+                            uint64_t m, uint32_t* __restrict__ kslot)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nk) kslot[k] = (uint32_t)kl_index(key_hash2(keys[k]), disp[kl_bucket(key_hash(keys[k]), nb)], m);
+}
+
+hipError_t run_key_slots(const int64_t* keys, uint64_t nk, const uint32_t* disp, uint64_t nb, uint64_t m, uint32_t* kslot,
+                         hipStream_t st)
+{
+    if (!nk) return hipSuccess;
+    k_key_slots<<<(unsigned)((nk + 255) / 256), 256, 0, st>>>(keys, nk, disp, nb, m, kslot);
+    return hipGetLastError();
+}
+
 hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const uint32_t* kcell, KeyLine* table,
                             uint64_t table_slots, hipStream_t st)
 {

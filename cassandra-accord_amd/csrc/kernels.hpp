@@ -166,6 +166,9 @@ hipError_t run_defer_scatter(const BatchBufs& b, const uint32_t* deferred, uint6
 int device_cu_count();
 // the KeyLine table (table_slots lines) from s.kent / cand / cwr; kslot[k] = the line of key k (its
 // perfect-hash index), kcell[k] = its stabbing cell (NO_CELL; null: none)
+// per key its KeyLine (the perfect hash under the displacements)
+hipError_t run_key_slots(const int64_t* keys, uint64_t nk, const uint32_t* disp, uint64_t nb, uint64_t m, uint32_t* kslot,
+                         hipStream_t st);
 hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const uint32_t* kcell, KeyLine* table,
                             uint64_t table_slots, hipStream_t st);
 // every DICT_SAMP-th id of s's dictionary into hi/lo/node (dict_samples(s.n_dict) entries)

@@ -520,10 +520,11 @@ int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t sc
  * A txnId the key's byId does not hold is inserted at its byId position (:1002-1007, -1 - binarySearch).
  * Ids the store's id dictionary does not hold (txnIds and executeAts) join it: appended when newer
  * than every id of the store, otherwise merged, which renumbers every id rank on the device (a
- * monotone remap: nothing is re-sorted). Errors (nothing applied): AD_E_INVAL (key not in the
- * snapshot, status > 7, live range-domain id), AD_E_INCONSISTENT_ID, AD_E_DUP_EXEC (two committed
- * entries of a key with one executeAt, :1439). Ids added to the dictionary by a failed batch stay
- * (they change no answer). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
+ * monotone remap: nothing is re-sorted). A key without a CommandsForKey gets one (the store creates
+ * it before the update; key indices renumbered, key hash and KeyLines follow). Errors (nothing
+ * applied): AD_E_INVAL (status > 7, live range-domain id), AD_E_INCONSISTENT_ID, AD_E_DUP_EXEC (two
+ * committed entries of a key with one executeAt, :1439). Ids and keys added by a failed batch stay
+ * (an unreferenced id or an empty CommandsForKey changes no answer). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
  * follow on demand. */
 typedef struct ad_cfk_update_soa {
     uint64_t n;

@@ -27,7 +27,7 @@ def transitions(cfk, rng, n, repeat_frac=0.25, statuses=range(8)):
 
 
 def fresh_preaccepts(cfk, rng, n_txns, max_keys=4, epoch=9, hlc0=1, statuses=(2,), new_exec_frac=0.0,
-                     kinds=(0, 1, 3)):
+                     kinds=(0, 1, 3), new_keys=None):
     """PreAccepts of txnIds newer than every id of the store (epoch above the store's): each new txn
     on 1..max_keys existing keys, inserted with a status from `statuses`; executeAt = txnId or, for
     `new_exec_frac` of them, a later new Timestamp."""
@@ -38,8 +38,9 @@ def fresh_preaccepts(cfk, rng, n_txns, max_keys=4, epoch=9, hlc0=1, statuses=(2,
     use_x = rng.random(n_txns) < new_exec_frac
     ex = Tids(np.where(use_x, x.msb, t.msb), np.where(use_x, x.lsb, t.lsb), np.where(use_x, x.node, t.node))
     keys, rows = [], []
+    pool = cfk.keys if new_keys is None else np.union1d(cfk.keys, np.asarray(new_keys, np.int64))
     for i in range(n_txns):
-        kk = rng.choice(cfk.keys, rng.integers(1, max_keys + 1), replace=False)
+        kk = rng.choice(pool, min(len(pool), rng.integers(1, max_keys + 1)), replace=False)
         keys.extend(kk.tolist())
         rows.extend([i] * len(kk))
     rows = np.array(rows)
@@ -96,3 +97,9 @@ def older_inserts(cfk, rng, n, known_frac=0.3, new_exec_frac=0.3, statuses=range
     x = Tids(np.where(use_x, cfk.exec.msb[f], t.msb), np.where(use_x, cfk.exec.lsb[f], t.lsb),
              np.where(use_x, cfk.exec.node[f].astype(np.int64) + 3000 + np.arange(n), t.node).astype(np.int32))
     return CfkUpdates(keys.astype(np.int64), t, x, st)
+
+
+def unused_keys(cfk, rng, n, lo=-500, hi=500):
+    """n key values in [lo, hi) the store holds no CommandsForKey for."""
+    free = np.setdiff1d(np.arange(lo, hi, dtype=np.int64), cfk.keys)
+    return np.sort(rng.choice(free, min(n, len(free)), replace=False))

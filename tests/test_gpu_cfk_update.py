@@ -155,9 +155,6 @@ def test_errors_leave_store_unchanged(oracle):
     try:
         st.load(w)
         u, _ = G.transitions(w.cfk, rng, 30, statuses=[A.ST_STABLE])
-        bad_key = CfkUpdates(u.keys.copy(), u.txn, u.exec, u.status)
-        bad_key.keys[5] = 10 ** 9
-        _unchanged_after_error(w, st, oracle, bad_key, A.AD_E_INVAL)
         bad_st = CfkUpdates(u.keys, u.txn, u.exec, u.status.copy())
         bad_st.status[0] = 9
         _unchanged_after_error(w, st, oracle, bad_st, A.AD_E_INVAL)
@@ -314,7 +311,7 @@ def test_insert_older_than_key_and_unknown_exec(oracle):
         assert new.txn.node[e + 1] == t.node[0] and int(new.seg[k + 1]) - 1 > e + 1
         _check(w, st, oracle, new)
         # a failed batch after a merge: content unchanged, the merged ids stay (no answer changes)
-        bad = CfkUpdates(np.array([10 ** 9]), Tids(t.msb, t.lsb, t.node + 7), t, np.array([A.ST_STABLE], np.uint8))
+        bad = CfkUpdates(u.keys, Tids(t.msb, t.lsb, t.node + 7), t, np.array([9], np.uint8))   # status 9: invalid
         w.cfk = new
         _unchanged_after_error(w, st, oracle, CfkUpdates(np.r_[u.keys, bad.keys], Tids.concat([bad.txn, bad.txn]),
                                                          Tids.concat([t, t]), np.r_[u.status, bad.status]), A.AD_E_INVAL)
@@ -521,5 +518,81 @@ def test_ballot_rules_known_answers(oracle):
         st.cfk_update(u)
         _check(w, st, oracle, new)
         _check_ballots(st, new)
+    finally:
+        st.close()
+
+
+# ---- keys without a CommandsForKey (the update creates one) -------------------------------------
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("seed", range(6))
+def test_new_keys(oracle, seed, path):
+    # fresh PreAccepts and older ids on keys the store has never seen, mixed with updates of known
+    # keys, over rounds: key indices remapped, key hash rebuilt, KeyLines placed incrementally
+    # (range commands and their stabbing cells in the store), then deps on every path
+    w = synth.random_small(110 + seed, start_inclusive=(seed % 2 == 1))
+    w.flags = A.AD_SNAPSHOT
+    rng = np.random.default_rng(110 + seed)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices, path=path)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        for rnd in range(3):
+            nk = G.unused_keys(cfk, rng, 3 + 4 * rnd)
+            ins = G.fresh_preaccepts(cfk, rng, 15, epoch=9 + rnd, statuses=(2, 3, 4, 6), new_keys=nk)
+            tr, _ = G.transitions(cfk, rng, 20)
+            u = G.concat(tr, ins) if rnd % 2 else G.concat(ins, tr, ins)
+            new, _ = U.cfk_update(cfk, u)
+            if U.dup_committed_exec(new):
+                continue
+            _, stats = st.cfk_update(u)
+            assert len(new.keys) >= len(cfk.keys)
+            # requests over the new keys too
+            from accord_deps.model import Queries
+            q = w.queries
+            keys = np.concatenate([q.keys, nk])
+            _check(w, st, oracle, new)
+            cfk = new
+        # every key the store now holds answers on the lean path
+        from accord_deps.model import Queries
+        rq = G.fresh_preaccepts(cfk, rng, 40, epoch=20, max_keys=6)
+        rows = np.r_[0, np.nonzero(np.diff(rq.txn.lsb.astype(np.int64)))[0] + 1]
+        off = np.r_[rows, len(rq)].astype(np.uint64)
+        keys = np.concatenate([np.sort(rq.keys[int(off[i]):int(off[i + 1])]) for i in range(len(rows))])
+        old_q, old_cfk = w.queries, w.cfk
+        w.queries, w.cfk = Queries(rq.txn.take(rows), rq.txn.take(rows), off, keys), cfk
+        try:
+            exp = oracle.resolve(w)
+            got = st.calculate_partial_deps(w.queries, A.AD_SNAPSHOT)
+            ok, why = got.equals(exp, detail=True)
+            assert ok, why
+        finally:
+            w.queries, w.cfk = old_q, old_cfk
+        _sequential_check(w, st, oracle, cfk, rng, epoch=30)
+    finally:
+        st.close()
+
+
+def test_new_keys_recovery_and_empty_store(oracle):
+    # recovery views after keys were created; a store loaded empty takes its first keys
+    import ctypes as C
+    w = synth.recovery_workload(9)
+    rng = np.random.default_rng(9)
+    nk = G.unused_keys(w.cfk, rng, 5, lo=-(1 << 20), hi=1 << 20)
+    u = G.fresh_preaccepts(w.cfk, rng, 10, epoch=9, statuses=(3, 4, 5), new_keys=nk)
+    new, _ = U.cfk_update(w.cfk, u)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        st.cfk_update(u)
+        _carry_missing(w.cfk, new)
+        st._check(native.lib().ad_cfk_missing_load(st.h, C.byref(new.missing_soa())))
+        old = w.cfk
+        w.cfk = new
+        try:
+            for s_ in A.RECOVER_SCANS:
+                ok, why = st.recovery_scan(w.queries, s_).equals(oracle.recover(w, s_), detail=True)
+                assert ok, "scan %d: %s" % (s_, why)
+        finally:
+            w.cfk = old
     finally:
         st.close()
