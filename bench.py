@@ -140,7 +140,7 @@ def cpu_baseline_stores(w, budget_s=15.0, threads=None, gpu_take=None):
     :1144-1202), every store resolving its share of a prefix of the same batch with the CPU
     restatement (oracle/refcpu.c), then the per-store PartialDeps reduced request-wise with
     PartialDeps.with (CommandStores.mapReduce :576-593, rc_result_merge). Timed: the parallel
-    resolve + the reduce; median of 3 runs of a prefix sized to ~budget/3 s each. The merged result
+    resolve + the reduce; median of 5 runs of a prefix sized to ~budget/5 s each. The merged result
     of the prefix is compared bit-exactly with the GPU's (`gpu_take(idx)` -> PartialDepsBatch)."""
     import ctypes as C
     import threading
@@ -187,9 +187,9 @@ def cpu_baseline_stores(w, budget_s=15.0, threads=None, gpu_take=None):
     n = len(base.queries)
     p = min(n, 256)
     dt, _ = run(p)
-    p = int(min(n, max(p, p * (budget_s / 3.0) / max(dt, 1e-6))))
+    p = int(min(n, max(p, p * (budget_s / 5.0) / max(dt, 1e-6))))
     times, batch = [], None
-    for _ in range(3):
+    for _ in range(5):
         dt, batch = run(p)
         times.append(dt)
     for s in stores:
@@ -198,7 +198,7 @@ def cpu_baseline_stores(w, budget_s=15.0, threads=None, gpu_take=None):
     pairs = int(base.queries.key_off[p])
     ncpu, model = cpu_info()
     out = dict(value=pairs / t, unit="txn-key pairs/s", cores=threads, kind="port",
-               sample="first %d of %d requests of the same batch (%d txn-key pairs), median of 3 runs (%s s); "
+               sample="first %d of %d requests of the same batch (%d txn-key pairs), median of 5 runs (%s s); "
                       "refcpu = C restatement of the reference Java, %d CommandStores (EvenSplit token slices) on %d "
                       "threads + PartialDeps.with reduce; host %d CPUs, %s" %
                       (p, n, pairs, "/".join("%.2f" % x for x in times), threads, threads, ncpu, model))

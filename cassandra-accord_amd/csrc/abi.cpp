@@ -1790,8 +1790,9 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
 
 // SEQUENTIAL PreAccepts as device-side CommandsForKey.update insertions (PREACCEPTED, executeAt =
 // txnId) of every request into the CommandsForKey of each of its keys in the slice, as
-// apply_preaccepts does on the host. Returns 0 (applied), 1 (not applicable here: a key without a
-// CommandsForKey, an insertion before a key's last id, or no built snapshot) or an AD_E_* error.
+// apply_preaccepts does on the host (keys without a CommandsForKey and older ids included). Returns
+// 0 (applied), 1 (not applicable here: no built snapshot, or a batch the device path refuses) or an
+// AD_E_* error.
 static int sequential_on_device(ad_ctx* c, const ad_query_soa* q)
 {
     if (c->dirty || getenv("AD_SEQ_HOST")) return 1;
