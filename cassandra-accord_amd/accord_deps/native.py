@@ -25,7 +25,8 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_range_cmds_recovery_load", "ad_recovery_batch",
            "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries",
            "ad_cfk_ballots_load", "ad_cfk_ballots",
-           "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange")
+           "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange",
+           "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid")
 
 
 class AccordDepsError(RuntimeError):
@@ -101,6 +102,14 @@ def lib():
         L.ad_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         L.ad_exchange.argtypes = [C.c_void_p, C.POINTER(A.AdDepsResult), C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                   C.c_void_p, C.POINTER(A.AdMerged), C.POINTER(A.AdExchangeStats)]
+        L.ad_check_result_device.argtypes = [C.c_void_p, C.POINTER(A.AdDepsResult), C.c_void_p, C.POINTER(C.c_uint64),
+                                             C.POINTER(C.c_uint64)]
+        L.ad_cfk_prune.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_int64, C.POINTER(C.c_uint64),
+                                   C.POINTER(A.AdStats)]
+        L.ad_cfk_byid.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                  C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                  C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ad_check_snapshot.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
 
@@ -218,6 +227,26 @@ class DeviceCommandStore:
         n, st = C.c_uint64(), A.AdStats()
         self._check(lib().ad_cfk_update_device(self.h, C.byref(udev), stream, C.byref(n), C.byref(st)))
         return n.value, stats_dict(st)
+
+    def cfk_prune(self, keys=None, prune_interval=1, min_hlc_delta=0):
+        """Pruning.maybePrune for the CommandsForKey of `keys` (None: every key): returns
+        (entries removed, stats)."""
+        n, st = C.c_uint64(), A.AdStats()
+        ka = None if keys is None else np.ascontiguousarray(np.asarray(keys, np.int64))
+        self._check(lib().ad_cfk_prune(self.h, None if ka is None else A.ptr(ka), 0 if ka is None else len(ka),
+                                       int(prune_interval), int(min_hlc_delta), C.byref(n), C.byref(st)))
+        return n.value, stats_dict(st)
+
+    def cfk_byid(self):
+        """(keys, seg, txnIds (Tids), prunedBefore indices) of the store's CommandsForKeys as they stand."""
+        nk, ne = C.c_uint64(), C.c_uint64()
+        pk, ps, pm, pl, pn, pp = (C.c_void_p() for _ in range(6))
+        self._check(lib().ad_cfk_byid(self.h, C.byref(nk), C.byref(pk), C.byref(ps), C.byref(ne), C.byref(pm), C.byref(pl),
+                                      C.byref(pn), C.byref(pp)))
+        k, e = nk.value, ne.value
+        return (_view(pk, k, np.int64).copy(), _view(ps, k + 1, np.uint64).copy(),
+                Tids(_view(pm, e, np.uint64).copy(), _view(pl, e, np.uint64).copy(), _view(pn, e, np.int32).copy()),
+                _view(pp, k, np.int64).copy())
 
     def cfk_entries(self):
         """(status, executeAt Tids) of every entry as the store now holds them (load order)."""
@@ -359,6 +388,19 @@ class DeviceCommandStore:
         flags = A.AD_SNAPSHOT | A.AD_N_KEYS | (A.AD_PARTS_ONLY if parts_only else 0)
         self._check(lib().ad_deps_batch_device(self.h, C.byref(qdev), flags, stream, C.byref(out)))
         return out, stats_dict(out.stats)
+
+    # ---- debug invariant checks (accord_deps.h) -------------------------------------
+    def check_result_device(self, res, stream=None):
+        """(violations, first failing request * 3 + map or None) of a device result."""
+        n, first = C.c_uint64(0), C.c_uint64(0)
+        self._check(lib().ad_check_result_device(self.h, C.byref(res), stream, C.byref(n), C.byref(first)))
+        return n.value, (None if first.value == 2 ** 64 - 1 else first.value)
+
+    def check_snapshot(self):
+        """(violations, first failing key index or None) of the prepared snapshot."""
+        n, first = C.c_uint64(0), C.c_uint64(0)
+        self._check(lib().ad_check_snapshot(self.h, C.byref(n), C.byref(first)))
+        return n.value, (None if first.value == 2 ** 64 - 1 else first.value)
 
     # ---- multi-GPU exchange (accord_deps.h "multi-GPU exchange"; DESIGN.md §6) ----------------
     def export_parts(self, res, txn_index_ptr, dest_first, parts, stream=None):

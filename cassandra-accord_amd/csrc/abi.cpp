@@ -26,6 +26,7 @@
 #include "kernels.hpp"
 #include "levels.hpp"
 #include "cfk_update.hpp"
+#include "check.hpp"
 
 using namespace adx;
 
@@ -224,6 +225,8 @@ struct ad_ctx {
     DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, q_rec, big;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
     uint64_t o_cap[9] = {};                    // capacities of the packed outputs (elements)
+    DevBuf d_prune_keys;                       // ad_cfk_prune: key indices of the list
+    DevBuf chk;                                // ad_check_*: {violations, first failing item}
     DevBuf lb_agg, lb_inc;                     // tile sums and their prefixes (run_pack_lb)
     uint64_t key_cap = 0, rng_cap = 0, scr_cap = 0, reg_cap = 0;
     hipEvent_t ev[8] = {};
@@ -293,6 +296,9 @@ struct ad_ctx {
     bool host_stale = false;
     std::vector<uint64_t> x_msb, x_lsb;        // ad_cfk_entries views
     std::vector<int32_t> x_node;
+    std::vector<uint64_t> y_msb, y_lsb;        // ad_cfk_byid views
+    std::vector<int32_t> y_node;
+    std::vector<int64_t> y_pruned;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -3356,6 +3362,164 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
         stats->ms_total = now_ms() - t0;
     }
     return AD_OK;
+}
+
+// ---- Pruning.maybePrune on the device (cfk_update.hip run_cfk_prune) -----------
+int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_interval, int64_t min_hlc_delta,
+                 uint64_t* n_removed, ad_stats* stats)
+{
+    if (!c) return AD_E_INVAL;
+    if (n_keys && !keys) return c->fail(AD_E_INVAL, "ad_cfk_prune: null key list");
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (c->dirty)
+        if (int rc = build_snapshot(c)) return rc;
+    if (int rc = sync_host(c)) return rc;
+    auto& K = c->cfk;
+    if (!K.miss.empty())
+        return c->fail(AD_E_STATE, "ad_cfk_prune: TxnInfo.missing() lists are loaded; pruneBefore's missing-subset test "
+                                   "(Pruning.java:239-251) is not on the device");
+    const uint64_t nk = c->ds.n_keys;
+    // key ordinals -> key indices of the store (keys without a CommandsForKey are skipped)
+    std::vector<uint32_t> kl;
+    if (keys)
+    {
+        kl.reserve(n_keys);
+        for (uint64_t i = 0; i < n_keys; ++i)
+        {
+            const auto it = std::lower_bound(K.keys.begin(), K.keys.end(), keys[i]);
+            if (it != K.keys.end() && *it == keys[i]) kl.push_back((uint32_t)(it - K.keys.begin()));
+        }
+        std::sort(kl.begin(), kl.end());
+        kl.erase(std::unique(kl.begin(), kl.end()), kl.end());
+        if (kl.empty())
+        {
+            if (n_removed) *n_removed = 0;
+            if (stats) *stats = ad_stats{};
+            return AD_OK;
+        }
+        if (int rc = upload(c, c->d_prune_keys, kl)) return rc;
+    }
+    if (!c->cu) c->cu = cfk_upd_work_create();
+    CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
+                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
+                  c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
+    CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
+                     c->d_w.as<uint2>(), c->d_w.cap / 8};
+    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
+                       c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, cfk_keys_spare, cfk_keys_swap,
+                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
+    CfkPruneOut o;
+    std::string e;
+    const int rc = run_cfk_prune(c->cu, c->ds, d, keys ? c->d_prune_keys.as<uint32_t>() : nullptr, keys ? kl.size() : nk,
+                                 prune_interval, min_hlc_delta, &b, cfk_need_bufs, c, grow, c->stream, &o, &e);
+    if (rc)
+    {
+        // the derived arrays may be half built: rebuild everything from the entries at the next use
+        c->host_stale = true;
+        c->dirty = true;
+        return c->fail(rc, "ad_cfk_prune: %s", e.c_str());
+    }
+    if (o.n_removed)
+    {
+        if (c->kline_slots)
+            HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
+                                       c->kline_slots, c->stream));
+        // host copies follow from the device (entries moved; prunedBefore per key as ranks and indices)
+        if (K.pruned.empty()) K.pruned.assign(nk, -1);
+        if (c->h_pruned.size() != nk) c->h_pruned.assign(nk, 0);
+        c->host_moved = true;
+        c->host_stale = true;
+        ++c->snap_gen;
+    }
+    if (n_removed) *n_removed = o.n_removed;
+    if (stats)
+    {
+        *stats = ad_stats{};
+        stats->ms_device = o.ms_total;
+        stats->n_keys[0] = o.n_removed;
+        stats->n_keys[1] = o.n_keys_pruned;
+    }
+    return AD_OK;
+}
+
+int ad_cfk_byid(ad_ctx* c, uint64_t* n_keys, const int64_t** keys, const uint64_t** seg, uint64_t* n_entries,
+                const uint64_t** txn_msb, const uint64_t** txn_lsb, const int32_t** txn_node, const int64_t** pruned_before)
+{
+    if (!c || !n_keys || !keys || !seg || !n_entries || !txn_msb || !txn_lsb || !txn_node || !pruned_before) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (int rc = sync_host(c)) return rc;
+    auto& K = c->cfk;
+    const uint64_t ne = K.txn.size(), nk = K.keys.size();
+    c->y_msb.resize(ne);
+    c->y_lsb.resize(ne);
+    c->y_node.resize(ne);
+    for (uint64_t i = 0; i < ne; ++i)
+    {
+        c->y_msb[i] = K.txn[i].msb;
+        c->y_lsb[i] = K.txn[i].lsb;
+        c->y_node[i] = K.txn[i].node;
+    }
+    if (K.pruned.size() == nk) c->y_pruned = K.pruned;
+    else c->y_pruned.assign(nk, -1);
+    *n_keys = nk;
+    *keys = K.keys.data();
+    *seg = K.seg.data();
+    *n_entries = ne;
+    *txn_msb = c->y_msb.data();
+    *txn_lsb = c->y_lsb.data();
+    *txn_node = c->y_node.data();
+    *pruned_before = c->y_pruned.data();
+    return AD_OK;
+}
+
+// ---- debug invariant checks (check.hip) ------------------------------------------
+static int check_finish(ad_ctx* c, hipStream_t st, uint64_t* n_violations, uint64_t* first)
+{
+    uint64_t h[2] = {0, ~0ull};
+    HIPCHK(c, hipMemcpyAsync(h, c->chk.p, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    *n_violations = h[0];
+    if (first) *first = h[1];
+    return AD_OK;
+}
+
+static int check_begin(ad_ctx* c, hipStream_t st)
+{
+    static const uint64_t init[2] = {0, ~0ull};
+    if (!c->chk.ensure(sizeof(init))) return c->fail(AD_E_NOMEM, "check counters");
+    HIPCHK(c, hipMemcpyAsync(c->chk.p, init, sizeof(init), hipMemcpyHostToDevice, st));
+    return AD_OK;
+}
+
+int ad_check_result_device(ad_ctx* c, const ad_deps_result* res_dev, void* stream, uint64_t* n_violations, uint64_t* first)
+{
+    if (!c || !res_dev || !n_violations) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    for (int m = 0; m < AD_NMAPS && res_dev->n_txns; ++m)
+        if (!res_dev->keys_off[m] || !res_dev->keys[m] || !res_dev->txn_off[m] || !res_dev->txns[m] || !res_dev->k2t_off[m] ||
+            !res_dev->k2t[m])
+            return c->fail(AD_E_INVAL, "ad_check_result_device: a packed array of map %d is missing (AD_PARTS_ONLY result?)", m);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    int rc;
+    if ((rc = check_begin(c, st))) return rc;
+    HIPCHK(c, run_check_result(*res_dev, c->ds.n_dict, c->chk.p, st));
+    return check_finish(c, st, n_violations, first);
+}
+
+int ad_check_snapshot(ad_ctx* c, uint64_t* n_violations, uint64_t* first)
+{
+    if (!c || !n_violations) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    int rc;
+    if (c->dirty && (rc = build_snapshot(c))) return rc;
+    if ((rc = check_begin(c, c->stream))) return rc;
+    HIPCHK(c, run_check_snapshot(c->ds, c->chk.p, c->stream));
+    return check_finish(c, c->stream, n_violations, first);
 }
 
 }  // extern "C"

@@ -20,6 +20,8 @@
 // it (no rank changes), otherwise merged, which remaps every stored rank in place (monotone, so all
 // rank-sorted arrays stay sorted) before the batch is located. A failed batch leaves the store's
 // content unchanged (a merged dictionary stays: it adds ids, changes no answer).
+// Pruning (run_cfk_prune, end of file): Pruning.maybePrune / pruneBefore for a list of keys, the
+// removed entries compacted out of the per-entry arrays and the derived arrays rebuilt.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1623,6 +1625,210 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     out->n_inserted = G;
     // a duplicate committed executeAt: undo the batch and derive the previous state again
     if (w->h_ctl->err) return rollback(describe(w->h_ctl->err, w->h_ctl->err_idx));
+    return AD_OK;
+}
+
+
+// =============================================================================================
+// Pruning.maybePrune (Pruning.java:164-199) and pruneBefore (:205-331) for a list of keys, on the
+// device state. The store's TxnInfo.missing() lists are NO_TXNIDS in this model (the caller checks
+// none are loaded), so pruneBefore removes, below the new prunedBefore's byId position, every
+// INVALID_OR_TRUNCATED entry and every APPLIED entry executing before it; nothing else moves.
+// =============================================================================================
+namespace {
+
+// Timestamp.hlc() of dictionary rank r (Timestamp.java:129-131: highHlc(msb) | lowHlc(lsb); the
+// normalised lo holds lowHlc << 4)
+__device__ __forceinline__ int64_t rank_hlc(const DevSnapshot& s, uint32_t r)
+{
+    const uint64_t i = (r - 1) >> 1;
+    return (int64_t)(((s.dict_hi[i] & 0x7FFFull) << 48) | (s.dict_lo[i] >> 4));
+}
+
+__global__ void k_prune_cflag(uint64_t ne, const uint8_t* status, uint32_t* f)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    f[e] = (status[e] >= AD_ST_COMMITTED && status[e] <= AD_ST_APPLIED) ? 1u : 0u;
+}
+
+// thread per listed key: the new prunedBefore (maybePrune :166-189) -> p_pos[k] = its byId position
+// (0: no prune), p_xr / p_tr = its executeAt / txnId ranks. cm: the committed entries sorted by
+// (key, executeAt) (committedByExecuteAt of every key, :651-672); cpos: committed entries before e.
+__global__ void k_prune_key(uint64_t nl, const uint32_t* klist, DevSnapshot s, CfkDevState d, const uint32_t* cm,
+                            const uint64_t* cpos, int32_t prune_interval, int64_t min_hlc_delta, uint32_t* p_pos,
+                            uint32_t* p_xr, uint32_t* p_tr)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nl) return;
+    const uint32_t k = klist ? klist[t] : (uint32_t)t;
+    const KeyRec kr = d.krec[k];
+    if (kr.maw < 0) return;                                   // no APPLIED Write: maxAppliedWrite = -1
+    const uint64_t c_lo = cpos[kr.seg_lo], c_hi = cpos[kr.seg_hi];
+    // maxAppliedWriteByExecuteAt as an index into the key's committedByExecuteAt
+    const uint32_t mx = s.w[kr.maw].x;
+    uint64_t lo = c_lo, hi = c_hi;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (d.xrank[cm[mid]] < mx) lo = mid + 1;
+        else hi = mid;
+    }
+    const int64_t maw = (int64_t)(lo - c_lo);
+    if (maw < (int64_t)prune_interval) return;
+    const int64_t max_prune_hlc = rank_hlc(s, mx) - min_hlc_delta;
+    int64_t i = maw;
+    uint32_t e = 0;
+    while (--i >= 0)
+    {
+        e = cm[c_lo + (uint64_t)i];
+        const uint32_t kind = d.ent[e].y >> RANK_BITS;
+        if (kind == AD_KIND_WRITE && rank_hlc(s, d.xrank[e]) <= max_prune_hlc && d.status[e] == AD_ST_APPLIED) break;
+    }
+    if (i < 0) return;
+    const uint32_t tr = d.ent[e].y & RANK_MASK;
+    if (kr.pruned && tr <= kr.pruned) return;                 // newPrunedBefore <= prunedBefore (:184)
+    const uint32_t pos = e - kr.seg_lo;                       // insertPos: it is in byId
+    if (pos == 0) return;
+    p_pos[k] = pos;
+    p_xr[k] = d.xrank[e];
+    p_tr[k] = tr;
+}
+
+// thread per entry: removed by pruneBefore (:222-254, missing() == NO_TXNIDS)
+__global__ void k_prune_mark(uint64_t ne, CfkDevState d, const uint32_t* p_pos, const uint32_t* p_xr, uint32_t* rm)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t k = d.ekey[e];
+    const uint32_t pos = p_pos[k];
+    bool r = false;
+    if (pos && e - d.krec[k].seg_lo < pos)
+    {
+        const uint32_t st = d.status[e];
+        r = st == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED || (st == AD_ST_APPLIED && d.xrank[e] < p_xr[k]);
+    }
+    rm[e] = r ? 1u : 0u;
+}
+
+// thread per key: segments after the removals; prunedBefore where entries went (:255-257: a key
+// without removals keeps its CommandsForKey, prunedBefore included)
+__global__ void k_prune_keys(uint64_t nk, KeyRec* krec, const uint64_t* rpos, const uint32_t* p_pos, const uint32_t* p_tr,
+                             unsigned long long* n_keys_pruned)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    KeyRec kr = krec[k];
+    const uint64_t r_lo = rpos[kr.seg_lo], r_hi = rpos[kr.seg_hi];
+    if (p_pos[k] && r_hi > r_lo)
+    {
+        kr.pruned = p_tr[k];
+        atomicAdd(n_keys_pruned, 1ull);
+    }
+    kr.seg_lo -= (uint32_t)r_lo;
+    kr.seg_hi -= (uint32_t)r_hi;
+    krec[k] = kr;
+}
+
+__global__ __launch_bounds__(256) void k_prune_move(uint64_t ne, EntArrays a, const uint32_t* rm, const uint64_t* rpos,
+                                                    EntArrays b)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne || rm[e]) return;
+    const uint64_t j = e - rpos[e];
+    b.ent[j] = a.ent[e];
+    b.status[j] = a.status[e];
+    b.xrank[j] = a.xrank[e];
+    b.ekey[j] = a.ekey[e];
+    if (a.bal) b.bal[j] = a.bal[e];
+}
+
+}  // namespace
+
+int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t* klist, uint64_t nl, int32_t prune_interval,
+                  int64_t min_hlc_delta, CfkDerivedBufs* bufs,
+                  int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                  const CfkGrow& grow, hipStream_t st, CfkPruneOut* out, std::string* err)
+{
+    *out = CfkPruneOut{};
+    const uint64_t ne = s.n_ent, nk = s.n_keys;
+    if (!nk || !ne || !nl) return AD_OK;
+    if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
+    for (auto& e : w->ev)
+        if (!e) UCHK(hipEventCreate(&e));
+    UALLOC(w->ctl, sizeof(UpdCtl), false);
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    UCHK(hipEventRecord(w->ev[0], st));
+    // the committed order of the current entries (a derivation keeps it; after the ingest, derive once)
+    if (!w->cm_valid)
+    {
+        UALLOC(w->chg[w->chg_cur], ne, false);
+        w->moved = false;
+        if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rc;
+        UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    }
+    UALLOC(w->flags, 4 * ne, false);
+    UALLOC(w->fs, 8 * (ne + 1), false);
+    UALLOC(w->bsum, 8 * ((ne + 1023) / 1024 + 8), false);
+    UALLOC(w->maw, 4 * nk, false);          // p_pos
+    UALLOC(w->wtail, 4 * nk, false);        // p_xr
+    UALLOC(w->gkey, 4 * nk, false);         // p_tr
+    UALLOC(w->uflag, 4 * ne, false);        // rm
+    UALLOC(w->upos, 8 * (ne + 1), false);   // rpos
+    uint32_t* p_pos = w->maw.as<uint32_t>();
+    uint32_t* p_xr = w->wtail.as<uint32_t>();
+    uint32_t* p_tr = w->gkey.as<uint32_t>();
+    k_prune_cflag<<<blocks(ne), 256, 0, st>>>(ne, d.status, w->flags.as<uint32_t>());
+    UCHK(run_scan_arrays(w->flags.as<uint32_t>(), w->fs.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
+    UCHK(hipMemsetAsync(p_pos, 0, 4 * nk, st));
+    k_prune_key<<<blocks(nl), 256, 0, st>>>(nl, klist, s, d, w->cm.as<uint32_t>(), w->fs.as<uint64_t>(), prune_interval,
+                                            min_hlc_delta, p_pos, p_xr, p_tr);
+    k_prune_mark<<<blocks(ne), 256, 0, st>>>(ne, d, p_pos, p_xr, w->uflag.as<uint32_t>());
+    UCHK(hipGetLastError());
+    UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
+    k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), ne, 1, ctl->tot2);
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    const uint64_t R = w->h_ctl->tot2[0];
+    if (R == 0)
+    {
+        UCHK(hipEventRecord(w->ev[1], st));
+        UCHK(hipEventSynchronize(w->ev[1]));
+        float a = 0;
+        (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
+        out->ms_total = a;
+        return AD_OK;
+    }
+    // compaction into the spare per-entry arrays, segments and prunedBefore, then a full derivation
+    unsigned long long* nkp = reinterpret_cast<unsigned long long*>(&ctl->tot2[1]);
+    UCHK(hipMemsetAsync(nkp, 0, 8, st));
+    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot, nullptr}, b{};
+    if (int rc = grow.entries(grow.ctx, ne - R, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal)) { *err = "entry arrays"; return rc; }
+    const uint64_t padded = std::max<uint64_t>(64, (ne - R + 63) / 64 * 64);
+    if (padded > ne - R) UCHK(hipMemsetAsync(b.ent + (ne - R), 0, sizeof(uint2) * (padded - (ne - R)), st));
+    k_prune_move<<<blocks(ne), 256, 0, st>>>(ne, a, w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), b);
+    k_prune_keys<<<blocks(nk), 256, 0, st>>>(nk, d.krec, w->upos.as<uint64_t>(), p_pos, p_tr, nkp);
+    UCHK(hipGetLastError());
+    if (int rc = grow.swap(grow.ctx, ne - R, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot)) { *err = "entry swap"; return rc; }
+    s.ent = d.ent;
+    s.n_ent = ne - R;
+    w->cm_valid = false;          // entry indices changed: the next derivation sorts afresh
+    w->moved = false;
+    UALLOC(w->chg[w->chg_cur], std::max<uint64_t>(ne - R, 1), false);
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    out->n_keys_pruned = w->h_ctl->tot2[1];
+    out->n_removed = R;
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rc;
+    UCHK(hipEventRecord(w->ev[1], st));
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    float a_ms = 0;
+    (void)hipEventElapsedTime(&a_ms, w->ev[0], w->ev[1]);
+    out->ms_total = a_ms;
+    if (w->h_ctl->err) { *err = "derivation after pruning reported an inconsistency"; return AD_E_STATE; }
     return AD_OK;
 }
 

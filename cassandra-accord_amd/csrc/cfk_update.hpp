@@ -117,4 +117,19 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
                    int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
                    const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err);
 
+struct CfkPruneOut {
+    uint64_t n_removed = 0;        // entries removed
+    uint64_t n_keys_pruned = 0;    // CommandsForKeys whose prunedBefore moved
+    double ms_total = 0;
+};
+
+// Pruning.maybePrune (Pruning.java:164-199 -> pruneBefore :205-331) for the keys klist[0..nl) (key
+// indices, device; null: every key, nl = n_keys), with TxnInfo.missing() = NO_TXNIDS for every entry.
+// Removed entries leave the per-entry arrays (compacted into the spare buffers), the segments and
+// prunedBefore follow, and the derived arrays are rebuilt. Ids stay in the dictionary.
+int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t* klist, uint64_t nl, int32_t prune_interval,
+                  int64_t min_hlc_delta, CfkDerivedBufs* bufs,
+                  int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                  const CfkGrow& grow, hipStream_t st, CfkPruneOut* out, std::string* err);
+
 }  // namespace adx

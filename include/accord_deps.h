@@ -558,6 +558,43 @@ int ad_cfk_ballots_load(ad_ctx* ctx, uint64_t n_entries, const uint64_t* msb, co
 /* The entries' ballots as they stand (views as ad_cfk_entries). */
 int ad_cfk_ballots(ad_ctx* ctx, uint64_t* n_entries, const uint64_t** msb, const uint64_t** lsb, const int32_t** node);
 
+/* Pruning.maybePrune (Pruning.java:164-199) -> pruneBefore (:205-331) on the device, for the
+ * CommandsForKey of each listed key (key ordinals, host array; keys == NULL: every key), as
+ * SafeCommandsForKey.update runs it after an Applied command updated the key
+ * (SafeCommandsForKey.java:73-78; prune_interval = agent.cfkPruneInterval(), min_hlc_delta =
+ * agent.cfkHlcPruneDelta()). Per key: with maxAppliedWriteByExecuteAt >= prune_interval, the new
+ * prunedBefore is the latest APPLIED Write before it in committedByExecuteAt whose executeAt.hlc()
+ * <= that Write's executeAt.hlc() - min_hlc_delta, taken when its TxnId is above the current
+ * prunedBefore and it is not byId[0]; below it, INVALID_OR_TRUNCATED entries and APPLIED entries
+ * executing before it leave byId and committedByExecuteAt (a key where nothing would leave is left as
+ * it was, prunedBefore included). Every TxnInfo.missing() is NO_TXNIDS in this model: with lists
+ * loaded (ad_cfk_missing_load) AD_E_STATE. Removed ids stay in the id dictionary. n_removed: entries
+ * removed; stats (may be null): ms_device, n_keys[0] entries removed, n_keys[1] keys pruned. */
+int ad_cfk_prune(ad_ctx* ctx, const int64_t* keys, uint64_t n_keys, int32_t prune_interval, int64_t min_hlc_delta,
+                 uint64_t* n_removed, ad_stats* stats);
+/* The store's CommandsForKeys as they stand: keys, byId segments ([seg[k], seg[k+1]) of the entry
+ * arrays, n_keys + 1 offsets), every entry's TxnId and each key's prunedBefore as an index into its
+ * byId (-1: none). Views owned by the context, valid until its next call. */
+int ad_cfk_byid(ad_ctx* ctx, uint64_t* n_keys, const int64_t** keys, const uint64_t** seg, uint64_t* n_entries,
+                const uint64_t** txn_msb, const uint64_t** txn_lsb, const int32_t** txn_node, const int64_t** pruned_before);
+
+/* ---- debug invariant checks ---------------------------------------------------
+ * Structural invariants the reference asserts, checked in HBM without copying anything back.
+ * ad_check_result_device: every request and map of a device result (ad_deps_batch_device,
+ * ad_recovery_batch_device; not AD_PARTS_ONLY) against RelationMultiMap.checkValid
+ * (RelationMultiMap.java:1074-1097) and the builder's layout (:147-260): keys strictly ascending,
+ * txnIds strictly ascending and inside ad_dict, keysToTxnIds = nKeys strictly increasing absolute end
+ * offsets from above nKeys to its length, each key's values strictly ascending and below nTxnIds,
+ * every TxnId some key's value, offsets monotone. *first = request * 3 + map of the first violation.
+ * ad_check_snapshot: the prepared snapshot as it stands (after ad_cfk_update batches too): keys
+ * strictly ascending, each key's byId strictly increasing by TxnId (CommandsForKey.java:1438) with
+ * dictionary member ranks and its cached last txnId, committed Writes by strictly increasing
+ * executeAt (:1439), the id dictionary strictly ascending (Timestamp.compareTo). *first = the first
+ * failing key index (n_keys + i: dictionary ids i, i + 1). first may be NULL; ~0 = none. */
+int ad_check_result_device(ad_ctx* ctx, const ad_deps_result* res_dev, void* stream, uint64_t* n_violations,
+                           uint64_t* first);
+int ad_check_snapshot(ad_ctx* ctx, uint64_t* n_violations, uint64_t* first);
+
 #ifdef __cplusplus
 }
 #endif

@@ -162,3 +162,89 @@ def dup_committed_exec(cfk):
                     return True
                 seen.add(x)
     return False
+
+
+# ---- Pruning.maybePrune / pruneBefore (accord-core/src/main/java/accord/local/cfk/Pruning.java) --------
+KIND_WRITE = 1
+APPLIED, INVALID = 6, 7
+
+
+def hlc(msb, lsb):
+    """Timestamp.hlc() (Timestamp.java:129-131, :328-336): highHlc(msb) | lowHlc(lsb)."""
+    return ((int(msb) & 0x7FFF) << 48) | (int(lsb) >> 16)
+
+
+def cfk_prune(cfk, keys=None, prune_interval=1, min_hlc_delta=0):
+    """Returns (new CfkSnapshot, entries removed, keys pruned): CommandsForKey.maybePrune
+    (Pruning.java:164-199) for the CommandsForKey of every key in `keys` (None: all), then
+    pruneBefore (:205-331) where it applies. Every TxnInfo.missing() is NO_TXNIDS (the device model:
+    the lists are not loaded), so an APPLIED entry executing before the new prunedBefore is removed
+    (:239-245 with missing == NO_TXNIDS), as is every INVALID_OR_TRUNCATED entry before it (:253-254).
+    prunedBefore is an index into the key's byId here (-1: none)."""
+    seg = cfk.seg.astype(np.int64)
+    nk = len(cfk.keys)
+    want = set(int(k) for k in keys) if keys is not None else None
+    pb_old = cfk.pruned_before if cfk.pruned_before is not None else np.full(nk, -1, np.int64)
+    keep = np.ones(cfk.n_entries, bool)
+    pruned = pb_old.copy()
+    n_keys_pruned = 0
+    tm, tl, tn = cfk.txn.msb, cfk.txn.lsb, cfk.txn.node
+    em, el, en = cfk.exec.msb, cfk.exec.lsb, cfk.exec.node
+
+    def tnorm(e):
+        return norm(tm[e], tl[e], tn[e])
+
+    def xnorm(e):
+        return norm(em[e], el[e], en[e])
+
+    for k in range(nk):
+        if want is not None and int(cfk.keys[k]) not in want:
+            continue
+        lo, hi = int(seg[k]), int(seg[k + 1])
+        # committedByExecuteAt (CommandsForKey.java:651-672) and maxAppliedWriteByExecuteAt (:673-679)
+        committed = sorted((e for e in range(lo, hi) if 4 <= int(cfk.status[e]) <= 6), key=xnorm)
+        maw = len(committed) - 1
+        while maw >= 0:
+            e = committed[maw]
+            if int(cfk.status[e]) == APPLIED and ((int(tl[e]) >> 1) & 7) == KIND_WRITE:
+                break
+            maw -= 1
+        # maybePrune :166-189
+        if maw < prune_interval:
+            continue
+        max_prune_hlc = hlc(em[committed[maw]], el[committed[maw]]) - min_hlc_delta
+        i = maw - 1
+        while i >= 0:
+            e = committed[i]
+            if ((int(tl[e]) >> 1) & 7) == KIND_WRITE and hlc(em[e], el[e]) <= max_prune_hlc and int(cfk.status[e]) == APPLIED:
+                break
+            i -= 1
+        if i < 0:
+            continue
+        npb = committed[i]
+        if int(pb_old[k]) >= 0 and tnorm(npb) <= tnorm(lo + int(pb_old[k])):
+            continue
+        pos = npb - lo                              # insertPos: npb is in byId
+        if pos == 0:
+            continue
+        # pruneBefore :205-260: entries before pos that are INVALID, or APPLIED executing before npb
+        removed = []
+        for e in range(lo, lo + pos):
+            st = int(cfk.status[e])
+            if st == INVALID or (st == APPLIED and xnorm(e) < xnorm(npb)):
+                removed.append(e)
+        if not removed:
+            continue                                # pos == retainCount: the CommandsForKey as it was
+        keep[removed] = False
+        pruned[k] = pos - len(removed)             # npb's index in the new byId
+        n_keys_pruned += 1
+    idx = np.nonzero(keep)[0]
+    new_seg = np.zeros(nk + 1, np.uint64)
+    new_seg[1:] = np.cumsum([int(keep[int(seg[k]):int(seg[k + 1])].sum()) for k in range(nk)])
+    # prunedBefore indices of keys not pruned here shift by the removals before them (none: a key's
+    # removals are all below its new prunedBefore, and other keys' removals are in other segments)
+    out = CfkSnapshot(cfk.keys.copy(), new_seg, cfk.txn.take(idx), cfk.exec.take(idx), cfk.status[idx].copy(),
+                      pruned if (cfk.pruned_before is not None or n_keys_pruned) else None)
+    if getattr(cfk, "ballot", None) is not None:
+        out.ballot = cfk.ballot.take(idx)
+    return out, int((~keep).sum()), n_keys_pruned

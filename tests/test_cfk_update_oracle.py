@@ -115,3 +115,67 @@ def test_ballot_rules():
     bt2 = Tids(np.array([b(8)[0]], np.uint64), np.array([b(8)[1]], np.uint64), np.array([1], np.int32))
     n3, _ = U.cfk_update(n, CfkUpdates(np.array([10]), t, x, np.array([A.ST_PREACCEPTED]), bt2))
     assert n3.status[0] == A.ST_PREACCEPTED and int(n3.exec.lsb[0]) == int(t.lsb[0]) and int(n3.ballot.lsb[0]) == b(8)[1]
+
+
+# ---- Pruning.maybePrune / pruneBefore (Pruning.java:164-331) known answers -----------------------
+def _prune_store(rows, pruned=-1):
+    """One key (7): rows of (txn hlc, kind, status, executeAt hlc) in byId order."""
+    hl = [r[0] for r in rows]
+    kinds = [r[1] for r in rows]
+    txn = make_txn_ids(1, hl, kinds, 1)
+    exe = make_txn_ids(1, [r[3] for r in rows], kinds, 1)
+    return CfkSnapshot(np.array([7]), np.array([0, len(rows)]), txn, exe, np.array([r[2] for r in rows]),
+                       np.array([pruned]))
+
+
+W, R = A.KIND_WRITE, A.KIND_READ
+AP, ST, CM, PA, INV = A.ST_APPLIED, A.ST_STABLE, A.ST_COMMITTED, A.ST_PREACCEPTED, 7
+
+
+def _hlcs(c):
+    return [int(x) >> 16 for x in c.txn.lsb]
+
+
+def test_prune_latest_applied_write_before_max():
+    # committedByExecuteAt = [W10, R20, W30, W40]; maxAppliedWrite = W40 (index 3 >= interval 1);
+    # the latest APPLIED Write before it is W30 -> prunedBefore; W10 and R20 executed before it: gone
+    c = _prune_store([(10, W, AP, 10), (20, R, AP, 20), (30, W, AP, 30), (40, W, AP, 40)])
+    n, removed, keys = U.cfk_prune(c, None, 1, 0)
+    assert (removed, keys) == (2, 1)
+    assert _hlcs(n) == [30, 40] and n.pruned_before.tolist() == [0]
+
+
+def test_prune_interval_and_hlc_delta():
+    c = _prune_store([(10, W, AP, 10), (20, R, AP, 20), (30, W, AP, 30), (40, W, AP, 40)])
+    assert U.cfk_prune(c, None, 4, 0)[1:] == (0, 0)            # maxAppliedWrite index 3 < 4 (:168)
+    assert U.cfk_prune(c, None, 3, 0)[1:] == (2, 1)
+    # hlc(W40) - 10 = 30: W30 qualifies; - 11 = 29: only W10 (byId[0]: pos 0, :192-193)
+    assert U.cfk_prune(c, None, 1, 10)[1:] == (2, 1)
+    assert U.cfk_prune(c, None, 1, 11)[1:] == (0, 0)
+    assert U.cfk_prune(c, None, 1, 100)[1:] == (0, 0)          # no candidate (:182-183)
+
+
+def test_prune_keeps_undecided_committed_and_later_executing():
+    # below W50: INVALID goes; PREACCEPTED, STABLE and COMMITTED stay; APPLIED R20 executing after
+    # W50 (executeAt 60) stays; APPLIED W15 executing before goes
+    c = _prune_store([(10, W, INV, 10), (15, W, AP, 15), (20, R, AP, 60), (25, W, PA, 25), (30, W, ST, 30),
+                      (35, R, CM, 35), (50, W, AP, 50), (70, W, AP, 70)])
+    n, removed, keys = U.cfk_prune(c, None, 1, 0)
+    assert removed == 2 and _hlcs(n) == [20, 25, 30, 35, 50, 70]
+    assert n.status.tolist() == [AP, PA, ST, CM, AP, AP] and n.pruned_before.tolist() == [4]
+
+
+def test_prune_not_beyond_current_pruned_before():
+    rows = [(10, W, AP, 10), (20, R, AP, 20), (30, W, AP, 30), (40, W, AP, 40)]
+    # prunedBefore already W30 (index 2): the candidate is not above it (:184-185)
+    assert U.cfk_prune(_prune_store(rows, pruned=2), None, 1, 0)[1:] == (0, 0)
+    # nothing to remove below the candidate: the CommandsForKey stays as it was (:255-256)
+    c = _prune_store([(10, W, PA, 10), (30, W, AP, 30), (40, W, AP, 40)])
+    n, removed, keys = U.cfk_prune(c, None, 1, 0)
+    assert (removed, keys) == (0, 0) and n.pruned_before.tolist() == [-1]
+
+
+def test_prune_key_list():
+    c = _prune_store([(10, W, AP, 10), (20, R, AP, 20), (30, W, AP, 30), (40, W, AP, 40)])
+    assert U.cfk_prune(c, [8, 9], 1, 0)[1:] == (0, 0)
+    assert U.cfk_prune(c, [7], 1, 0)[1:] == (2, 1)

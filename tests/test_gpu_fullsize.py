@@ -84,6 +84,9 @@ def _run_full(w, oracle, expect_lean=None):
         idx = _sample(len(w.queries))
         got = st.device_result_to_host(res, idx)
         _check_csr(st, res)
+        # the same invariants checked on the device (ad_check_result_device / ad_check_snapshot)
+        assert st.check_result_device(res) == (0, None)
+        assert st.check_snapshot() == (0, None)
         exp = oracle.OracleStore(w.range_start_inclusive, 1, w.slices).load(w).deps_batch(w.queries.take(idx), w.flags)
         ok, why = got.equals(exp, detail=True)
         if not ok:
