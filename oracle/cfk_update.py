@@ -248,3 +248,199 @@ def cfk_prune(cfk, keys=None, prune_interval=1, min_hlc_delta=0):
     if getattr(cfk, "ballot", None) is not None:
         out.ballot = cfk.ballot.take(idx)
     return out, int((~keep).sum()), n_keys_pruned
+
+
+# ---- TxnInfo.missing() maintenance and deps-derived additions (Updating.java, Utils.java) -------------
+ACCEPTED, COMMITTED = 3, 4
+
+
+def _kind(raw):
+    return (int(raw[1]) >> 1) & 7
+
+
+def _witnesses(owner_raw, other_raw):
+    """owner.kind().witnesses(other) (Txn.java:221-235)."""
+    k = _kind(owner_raw)
+    mask = {0: 0b10, 2: 0b10, 1: 0b11, 3: 0b11, 4: 0b11011}.get(k, 0)
+    return (mask >> _kind(other_raw)) & 1 == 1
+
+
+def cfk_update_missing(cfk, upd, dep_off=None, deps=None):
+    """CommandsForKey.update (CommandsForKey.java:992-1042) for a batch, with the TxnInfo.missing()
+    lists and the deps-derived additions of Updating.insertOrUpdate (Updating.java:99-172):
+      * an update whose status has deps (ACCEPTED..APPLIED) runs computeInfoAndAdditions (:194-287)
+        over the key's byId and the command's deps on the key (deps[dep_off[i]:dep_off[i+1]],
+        ascending, already past shardRedundantBefore, :185): its missing() = the byId entries below
+        depsKnownBefore (:561-580) it witnesses, not COMMITTED or later, not in its deps; additions =
+        the deps byId lacks (witnessed ones inside the merge, every one past byId's end, :235-263),
+        those below prunedBefore dropped (removePrunedAdditions, Utils.java:229-246), inserted as
+        TRANSITIVELY_KNOWN (insertOrUpdateWithAdditions :364-470): every other entry with deps gets
+        the additions (and the txn itself when it is inserted below COMMITTED) below its
+        depsKnownBefore that its kind witnesses (missingTo / mergeAndFilterMissing, Utils.java:291-352),
+        and loses the txn when it becomes committed (removeOneMissing);
+      * without additions, insertOrUpdate (:289-358): a txn becoming committed leaves every missing()
+        (removeFromMissingArrays, Utils.java:68-121), one inserted below COMMITTED (not INVALID) joins
+        those of the committed entries executing after it and the ACCEPTED entries after it
+        (addToMissingArrays :123-210), one invalidated from below COMMITTED leaves them;
+      * statuses without deps carry no missing() (TxnInfo.create :254-262).
+    loadingPruned is empty; the store's missing() lists come from cfk.miss_off / cfk.miss (None:
+    NO_TXNIDS). Returns (new CfkSnapshot with miss_off / miss, n_applied, n_additions)."""
+    seg = cfk.seg.astype(np.int64)
+    cb = getattr(cfk, "ballot", None)
+    ub = getattr(upd, "ballot", None)
+    per = {}            # key -> [row]; row = [nt, t, x, st, b, miss (sorted list of nt)]
+    raw_of = {}         # nt -> raw id (missing lists are kept as normalised ids)
+    pb = {}             # key -> prunedBefore nt
+    for k in range(len(cfk.keys)):
+        key = int(cfk.keys[k])
+        rows = []
+        for e in range(int(seg[k]), int(seg[k + 1])):
+            t = (int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e]))
+            x = (int(cfk.exec.msb[e]), int(cfk.exec.lsb[e]), int(cfk.exec.node[e]))
+            b = (int(cb.msb[e]), int(cb.lsb[e]), int(cb.node[e])) if cb is not None else ZERO
+            ms = []
+            if cfk.miss_off is not None:
+                for j in range(int(cfk.miss_off[e]), int(cfk.miss_off[e + 1])):
+                    r = (int(cfk.miss.msb[j]), int(cfk.miss.lsb[j]), int(cfk.miss.node[j]))
+                    raw_of[norm(*r)] = r
+                    ms.append(norm(*r))
+            nt = norm(*t)
+            raw_of[nt] = t
+            rows.append([nt, t, x, int(cfk.status[e]), b, sorted(ms)])
+        per[key] = rows
+        if cfk.pruned_before is not None and int(cfk.pruned_before[k]) >= 0:
+            pb[key] = rows[int(cfk.pruned_before[k])][0]
+    applied = n_add = 0
+
+    def dkb_of(row):
+        """depsKnownBefore (:561-580): txnId for ACCEPTED, executeAt for COMMITTED..APPLIED."""
+        return row[0] if row[3] == ACCEPTED else norm(*row[2])
+
+    def add_to(row, ids):
+        """mergeAndFilterMissing (Utils.java:303-352): ids the row's kind witnesses join its list."""
+        keep = [a for a in ids if _witnesses(row[1], raw_of[a])]
+        if keep:
+            row[5] = sorted(set(row[5]) | set(keep))
+
+    for i in range(len(upd)):
+        key = int(upd.keys[i])
+        st = int(upd.status[i])
+        t = (int(upd.txn.msb[i]), int(upd.txn.lsb[i]), int(upd.txn.node[i]))
+        x = (int(upd.exec.msb[i]), int(upd.exec.lsb[i]), int(upd.exec.node[i])) if st in HAS_EXEC else t
+        b = (int(ub.msb[i]), int(ub.lsb[i]), int(ub.node[i])) if ub is not None else ZERO
+        sb = b if st in HAS_BALLOT else ZERO
+        nt = norm(*t)
+        raw_of[nt] = t
+        rows = per.setdefault(key, [])
+        keys_nt = [r[0] for r in rows]
+        pos = bisect.bisect_left(keys_nt, nt)
+        present = pos < len(rows) and rows[pos][0] == nt
+        cur = rows[pos] if present else None
+        if present and not replaces(st, cur[3], b, cur[4]):
+            continue
+        applied += 1
+        was_committed = present and cur[3] in (4, 5, 6)
+        new_row = [nt, t, x, st, sb, []]
+        if st in HAS_EXEC and (present or (t[1] & 1) == 0):
+            # computeInfoAndAdditions (:194-287)
+            dl = []
+            if dep_off is not None:
+                for j in range(int(dep_off[i]), int(dep_off[i + 1])):
+                    r = (int(deps.msb[j]), int(deps.lsb[j]), int(deps.node[j]))
+                    raw_of[norm(*r)] = r
+                    dl.append(norm(*r))
+            dkb = nt if st == ACCEPTED else norm(*x)
+            dpos = pos if dkb == nt else bisect.bisect_left(keys_nt, dkb, pos)
+            upos = pos if present else -1
+            missing, additions = [], []
+            ti = di = 0
+            while ti < len(rows) and di < len(dl):
+                tt, d = rows[ti], dl[di]
+                if tt[0] == d:
+                    ti += 1
+                    di += 1
+                elif tt[0] < d:
+                    if ti != upos and ti < dpos and tt[3] < COMMITTED and _witnesses(t, tt[1]):
+                        missing.append(tt[0])
+                    ti += 1
+                else:
+                    if _witnesses(t, raw_of[d]):
+                        additions.append(d)
+                    di += 1
+            if di < len(dl):
+                additions.extend(dl[di:])
+            elif ti < len(rows):
+                while ti < dpos:
+                    if ti != upos and rows[ti][3] < COMMITTED and _witnesses(t, rows[ti][1]):
+                        missing.append(rows[ti][0])
+                    ti += 1
+            new_row[5] = missing
+            if key in pb:
+                additions = [a for a in additions if a >= pb[key]]     # removePrunedAdditions
+            if additions:
+                # insertOrUpdateWithAdditions (:364-470)
+                self_missing = not present and st < COMMITTED
+                remove_self = present and st >= COMMITTED and cur[3] < COMMITTED
+                for r in rows:
+                    if r is cur or r[3] not in HAS_EXEC:
+                        continue
+                    d_r = dkb_of(r)
+                    src = [a for a in additions if a < d_r]
+                    if self_missing and nt < d_r:
+                        src.append(nt)
+                    add_to(r, src)
+                    if remove_self and nt in r[5]:
+                        r[5].remove(nt)
+                if present:
+                    rows[pos] = new_row
+                else:
+                    rows.insert(pos, new_row)
+                for a in additions:
+                    ra = raw_of[a]
+                    bisect.insort(rows, [a, ra, ra, 0, ZERO, []])
+                n_add += len(additions)
+                continue
+        # insertOrUpdate without additions (:289-358)
+        if present:
+            rows[pos] = new_row
+        else:
+            rows.insert(pos, new_row)
+        becomes_committed = st in (4, 5, 6) and not was_committed
+        if becomes_committed or (present and cur[3] < COMMITTED and st == INVALID):
+            for r in rows:                       # removeFromMissingArrays (Utils.java:68-121)
+                if r is not new_row and nt in r[5]:
+                    r[5].remove(nt)
+        elif not present and st != INVALID:
+            for r in rows:                       # addToMissingArrays (Utils.java:123-210)
+                if r is new_row or not _witnesses(r[1], t):
+                    continue
+                if r[3] in (4, 5, 6) and norm(*r[2]) > nt:
+                    add_to(r, [nt])
+                elif r[3] == ACCEPTED and r[0] > nt:
+                    add_to(r, [nt])
+    # back to the SoA (keys ascending, byId per key), missing() as raw ids
+    all_keys = sorted(per)
+    out = {f: [] for f in ("tm", "tl", "tn", "em", "el", "en", "st", "bm", "bl", "bn")}
+    new_seg, moff, mm, ml, mn, pruned = [0], [0], [], [], [], []
+    for key in all_keys:
+        rows = per[key]
+        for nt, t, x, st, b, ms in rows:
+            out["tm"].append(t[0]), out["tl"].append(t[1]), out["tn"].append(t[2])
+            out["em"].append(x[0]), out["el"].append(x[1]), out["en"].append(x[2])
+            out["bm"].append(b[0]), out["bl"].append(b[1]), out["bn"].append(b[2])
+            out["st"].append(st)
+            for a in (ms if st in HAS_EXEC else []):
+                r = raw_of[a]
+                mm.append(r[0]), ml.append(r[1]), mn.append(r[2])
+            moff.append(len(mm))
+        new_seg.append(len(out["st"]))
+        pruned.append([r[0] for r in rows].index(pb[key]) if key in pb else -1)
+    txn = Tids(np.array(out["tm"], np.uint64), np.array(out["tl"], np.uint64), np.array(out["tn"], np.int32))
+    exe = Tids(np.array(out["em"], np.uint64), np.array(out["el"], np.uint64), np.array(out["en"], np.int32))
+    res = CfkSnapshot(np.array(all_keys, np.int64), np.array(new_seg, np.uint64), txn, exe, np.array(out["st"], np.uint8),
+                      None if cfk.pruned_before is None else np.array(pruned, np.int64),
+                      np.array(moff, np.uint64),
+                      Tids(np.array(mm, np.uint64), np.array(ml, np.uint64), np.array(mn, np.int32)))
+    if cb is not None or ub is not None:
+        res.ballot = Tids(np.array(out["bm"], np.uint64), np.array(out["bl"], np.uint64), np.array(out["bn"], np.int32))
+    return res, applied, n_add

@@ -179,3 +179,92 @@ def test_prune_key_list():
     c = _prune_store([(10, W, AP, 10), (20, R, AP, 20), (30, W, AP, 30), (40, W, AP, 40)])
     assert U.cfk_prune(c, [8, 9], 1, 0)[1:] == (0, 0)
     assert U.cfk_prune(c, [7], 1, 0)[1:] == (2, 1)
+
+
+# ---- TxnInfo.missing() and deps-derived additions (Updating.java:99-470, Utils.java:68-352) -------
+def _miss_store():
+    # key 7: A(10, W, PREACCEPTED), B(20, W, COMMITTED exec 20), C(30, R, PREACCEPTED)
+    c = _prune_store([(10, W, PA, 10), (20, W, CM, 20), (30, R, PA, 30)])
+    c.pruned_before = None
+    return c
+
+
+def _ids(hlcs, kinds):
+    return make_txn_ids(1, hlcs, kinds, 1)
+
+
+def _deps(lists):
+    """CSR of per-update deps lists of (hlc, kind)."""
+    off = np.zeros(len(lists) + 1, np.uint64)
+    flat = [d for l in lists for d in l]
+    off[1:] = np.cumsum([len(l) for l in lists])
+    return off, _ids([d[0] for d in flat], [d[1] for d in flat])
+
+
+def _miss_of(c, hlc):
+    e = _hlcs(c).index(hlc)
+    return [int(x) >> 16 for x in c.miss.lsb[int(c.miss_off[e]):int(c.miss_off[e + 1])]]
+
+
+def test_missing_of_an_accepted_txn_and_additions():
+    c = _miss_store()
+    # D(40, W) ACCEPTED, deps {A, X(25, W), Y(50, W)}: missing(D) = entries below depsKnownBefore (its
+    # txnId) it witnesses, not committed, not in its deps = {C}; additions X (inside the merge) and Y
+    # (past byId's end) inserted TRANSITIVELY_KNOWN (:194-287, :364-470)
+    off, dp = _deps([[(10, W), (25, W), (50, W)]])
+    u = _upd([7], [40], [W], [A.ST_ACCEPTED])
+    n, applied, nadd = U.cfk_update_missing(c, u, off, dp)
+    assert (applied, nadd) == (1, 2)
+    assert _hlcs(n) == [10, 20, 25, 30, 40, 50]
+    assert n.status.tolist() == [PA, CM, A.ST_TRANSITIVELY_KNOWN, PA, A.ST_ACCEPTED, A.ST_TRANSITIVELY_KNOWN]
+    assert _miss_of(n, 40) == [30] and _miss_of(n, 20) == []
+
+
+def test_commit_leaves_missing_and_gets_its_own():
+    c = _miss_store()
+    off, dp = _deps([[(10, W), (25, W), (50, W)], [(10, W), (20, W)]])
+    # then C (R) commits at 30 with deps {A, B}: it leaves D's missing (removeSelfMissing /
+    # removeFromMissingArrays); its own = below executeAt 30, Writes (a Read witnesses Ws), not
+    # committed, not in deps = {X}
+    u = _upd([7, 7], [40, 30], [W, R], [A.ST_ACCEPTED, A.ST_COMMITTED], [40, 30])
+    n, applied, nadd = U.cfk_update_missing(c, u, off, dp)
+    assert _miss_of(n, 40) == [] and _miss_of(n, 30) == [25]
+
+
+def test_pending_insert_joins_committed_after_and_accepted_after():
+    c = _miss_store()
+    off, dp = _deps([[(10, W), (25, W), (50, W)], [(10, W), (20, W)], []])
+    # T(27, W) PREACCEPTED inserted: joins C (committed, executes at 30 > 27, a Read witnesses a
+    # Write) and D (ACCEPTED, 40 > 27) (addToMissingArrays, Utils.java:123-210)
+    u = _upd([7, 7, 7], [40, 30, 27], [W, R, W], [A.ST_ACCEPTED, A.ST_COMMITTED, A.ST_PREACCEPTED], [40, 30, 27])
+    n, _, _ = U.cfk_update_missing(c, u, off, dp)
+    assert _miss_of(n, 30) == [25, 27] and _miss_of(n, 40) == [27]
+    # a Read (R 35) is not witnessed by... every kind here: a Write witnesses Reads, so D gets it too;
+    # C (a Read) does not
+    u2 = _upd([7], [35], [R], [A.ST_PREACCEPTED])
+    n2, _, _ = U.cfk_update_missing(n, u2, np.zeros(2, np.uint64), _ids([], []))
+    assert _miss_of(n2, 40) == [27, 35] and _miss_of(n2, 30) == [25, 27]
+
+
+def test_additions_below_pruned_before_are_dropped():
+    c = _miss_store()
+    c.pruned_before = np.array([1])                  # prunedBefore = B (20)
+    off, dp = _deps([[(15, W), (25, W)]])
+    u = _upd([7], [40], [W], [A.ST_ACCEPTED])
+    n, _, nadd = U.cfk_update_missing(c, u, off, dp)
+    assert nadd == 1 and _hlcs(n) == [10, 20, 25, 30, 40] and n.pruned_before.tolist() == [1]
+
+
+def test_missing_only_for_statuses_with_deps_and_matches_plain_update():
+    # without deps the statuses/executeAts equal the plain restatement's
+    w = synth.random_small(7)
+    rng = np.random.default_rng(7)
+    import cfk_update_gen as G
+    u, _ = G.transitions(w.cfk, rng, 200)
+    a, na = U.cfk_update(w.cfk, u)
+    b, nb, nadd = U.cfk_update_missing(w.cfk, u)
+    assert na == nb and nadd == 0
+    assert a.status.tolist() == b.status.tolist() and a.exec.lsb.tolist() == b.exec.lsb.tolist()
+    for e in range(b.n_entries):
+        if b.status[e] not in (3, 4, 5, 6):
+            assert b.miss_off[e + 1] == b.miss_off[e]
