@@ -58,7 +58,8 @@ class AdCfkSoa(C.Structure):
 class AdCfkUpdateSoa(C.Structure):
     _fields_ = [("n", C.c_uint64), ("keys", P), ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
                 ("exec_msb", P), ("exec_lsb", P), ("exec_node", P), ("status", P),
-                ("ballot_msb", P), ("ballot_lsb", P), ("ballot_node", P)]
+                ("ballot_msb", P), ("ballot_lsb", P), ("ballot_node", P),
+                ("dep_off", P), ("dep_msb", P), ("dep_lsb", P), ("dep_node", P)]
 
 
 class AdCfkMissingSoa(C.Structure):

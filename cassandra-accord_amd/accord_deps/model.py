@@ -153,10 +153,15 @@ class CfkUpdates:
     exec: Tids
     status: np.ndarray        # u8 InternalStatus
     ballot: Optional[Tids] = None
+    # the command's deps on the key per update (ascending): deps[dep_off[i]:dep_off[i+1]]; None = none
+    dep_off: Optional[np.ndarray] = None
+    deps: Optional[Tids] = None
 
     def __post_init__(self):
         self.keys = A.as_i64(self.keys)
         self.status = A.as_u8(self.status)
+        if self.dep_off is not None:
+            self.dep_off = A.as_u64(self.dep_off)
 
     def __len__(self):
         return len(self.keys)
@@ -170,6 +175,9 @@ class CfkUpdates:
         s.status = A.ptr(self.status)
         if self.ballot is not None:
             s.ballot_msb, s.ballot_lsb, s.ballot_node = A.ptr(self.ballot.msb), A.ptr(self.ballot.lsb), A.ptr(self.ballot.node)
+        if self.dep_off is not None:
+            s.dep_off = A.ptr(self.dep_off)
+            s.dep_msb, s.dep_lsb, s.dep_node = A.ptr(self.deps.msb), A.ptr(self.deps.lsb), A.ptr(self.deps.node)
         return s
 
 

@@ -26,7 +26,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries",
            "ad_cfk_ballots_load", "ad_cfk_ballots",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange",
-           "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid")
+           "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing")
 
 
 class AccordDepsError(RuntimeError):
@@ -109,6 +109,8 @@ def lib():
         L.ad_cfk_byid.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                   C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                   C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ad_cfk_missing.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                     C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.ad_check_snapshot.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
@@ -236,6 +238,15 @@ class DeviceCommandStore:
         self._check(lib().ad_cfk_prune(self.h, None if ka is None else A.ptr(ka), 0 if ka is None else len(ka),
                                        int(prune_interval), int(min_hlc_delta), C.byref(n), C.byref(st)))
         return n.value, stats_dict(st)
+
+    def cfk_missing(self):
+        """(off, Tids) of every entry's TxnInfo.missing() as it stands."""
+        ne = C.c_uint64()
+        po, pm, pl, pn = (C.c_void_p() for _ in range(4))
+        self._check(lib().ad_cfk_missing(self.h, C.byref(ne), C.byref(po), C.byref(pm), C.byref(pl), C.byref(pn)))
+        off = _view(po, ne.value + 1, np.uint64).copy()
+        nm = int(off[-1]) if len(off) else 0
+        return off, Tids(_view(pm, nm, np.uint64).copy(), _view(pl, nm, np.uint64).copy(), _view(pn, nm, np.int32).copy())
 
     def cfk_byid(self):
         """(keys, seg, txnIds (Tids), prunedBefore indices) of the store's CommandsForKeys as they stand."""

@@ -292,6 +292,11 @@ struct ad_ctx {
     bool host_moved = false;                         // entries were inserted on the device
     DevBuf u_k, u_tm, u_tl, u_tn, u_em, u_el, u_en, u_st, u_bm, u_bl, u_bn;
     DevBuf d_ballot, d_ballot2;                      // TxnInfo.ballot() per entry (Bal), when the store has any
+    // TxnInfo.missing() on the device (CfkMiss): per entry its list (mref), the lists as rank CSR
+    DevBuf d_mref, d_mref2, d_moff, d_moff2, d_mids, d_mids2;
+    bool dmiss_on = false;                           // the device maintains them (ad_cfk_update with deps)
+    uint64_t dmiss_lists = 0, dmiss_ids = 0;
+    DevBuf u_do, u_dm, u_dl, u_dn;                   // staged deps of a host update batch
     CfkUpdWork* cu = nullptr;
     bool host_stale = false;
     std::vector<uint64_t> x_msb, x_lsb;        // ad_cfk_entries views
@@ -299,6 +304,7 @@ struct ad_ctx {
     std::vector<uint64_t> y_msb, y_lsb;        // ad_cfk_byid views
     std::vector<int32_t> y_node;
     std::vector<int64_t> y_pruned;
+    std::vector<uint64_t> z_off;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -491,6 +497,7 @@ static int kl_add_keys(ad_ctx* c, const std::vector<int64_t>& nkeys, uint64_t nk
 static int build_snapshot(ad_ctx* c)
 {
     if (int rc0 = sync_host(c)) return rc0;
+    c->dmiss_on = false;          // the host copy holds the missing() lists now; uploaded again on demand
     const double t0 = now_ms();
     auto& K = c->cfk;
     const uint64_t nk = K.keys.size(), ne = K.status.size();
@@ -1068,7 +1075,35 @@ static int build_snapshot(ad_ctx* c)
 
 // Host copies of the per-entry state after ad_cfk_update* changed it on the device: status and
 // executeAt (from its rank through the dictionary, raw bits of the dictionary member).
+static int sync_host_entries(ad_ctx* c);
+
+// TxnInfo.missing() lists maintained on the device -> the host copy (ids from their ranks)
+static int pull_missing(ad_ctx* c)
+{
+    auto& K = c->cfk;
+    const uint64_t ne = c->dmiss_lists, nm = c->dmiss_ids;
+    K.miss_off.resize(ne + 1);
+    std::vector<uint32_t> r(nm);
+    HIPCHK(c, hipMemcpy(K.miss_off.data(), c->d_moff.p, 8 * (ne + 1), hipMemcpyDeviceToHost));
+    if (nm) HIPCHK(c, hipMemcpy(r.data(), c->d_mids.p, 4 * nm, hipMemcpyDeviceToHost));
+    K.miss.resize(nm);
+    for (uint64_t j = 0; j < nm; ++j)
+    {
+        const uint64_t i = (r[j] - 1) / 2;
+        K.miss[j] = Tid{c->dict_msb[i], c->dict_lsb[i], c->dict_node[i]};
+    }
+    K.miss_stale = false;
+    return 0;
+}
+
 static int sync_host(ad_ctx* c)
+{
+    if (!c->host_stale) return 0;
+    if (int rc = sync_host_entries(c)) return rc;
+    return c->dmiss_on ? pull_missing(c) : 0;
+}
+
+static int sync_host_entries(ad_ctx* c)
 {
     if (!c->host_stale) return 0;
     auto& K = c->cfk;
@@ -1739,6 +1774,9 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     K.ballot.clear();
     c->d_ballot.release();
     c->d_ballot2.release();
+    c->dmiss_on = false;
+    c->d_mref.release();
+    c->d_mref2.release();
     K.loaded = true;
     c->host_stale = false;       // the load replaces whatever ad_cfk_update applied on the device
     drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
@@ -2700,7 +2738,8 @@ static int cfk_grow_dict(void* vc, uint64_t n_old, uint64_t n_new, uint64_t** hi
     return 0;
 }
 
-static int cfk_grow_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal)
+static int cfk_grow_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal,
+                            uint32_t** mref)
 {
     ad_ctx* c = (ad_ctx*)vc;
     const uint64_t padded = std::max<uint64_t>(64, (ne + 63) / 64 * 64);
@@ -2712,6 +2751,12 @@ static int cfk_grow_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, ui
     {
         if (!grow_keep(c->d_ballot2, 0, sizeof(Bal) * ne)) return AD_E_NOMEM;
         *bal = c->d_ballot2.as<Bal>();
+    }
+    *mref = nullptr;
+    if (c->dmiss_on)
+    {
+        if (!grow_keep(c->d_mref2, 0, 4 * ne)) return AD_E_NOMEM;
+        *mref = c->d_mref2.as<uint32_t>();
     }
     *ent = c->d_ent2.as<uint2>();
     *st = c->d_status2.as<uint8_t>();
@@ -2748,7 +2793,8 @@ static int size_cfk_trees(ad_ctx* c, uint64_t ne)
     return 0;
 }
 
-static int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal)
+static int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal,
+                            uint32_t** mref)
 {
     ad_ctx* c = (ad_ctx*)vc;
     swap_buf(c->d_ent, c->d_ent2);
@@ -2756,6 +2802,8 @@ static int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, ui
     swap_buf(c->d_xrank, c->d_xrank2);
     swap_buf(c->d_ekey, c->d_ekey2);
     if (c->d_ballot.p) swap_buf(c->d_ballot, c->d_ballot2);
+    if (c->dmiss_on) swap_buf(c->d_mref, c->d_mref2);
+    *mref = c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr;
     *bal = c->d_ballot.as<Bal>();
     *ent = c->d_ent.as<uint2>();
     *st = c->d_status.as<uint8_t>();
@@ -2889,13 +2937,92 @@ static int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipSt
     return 0;
 }
 
+static int cfk_miss_spare(void* vc, uint64_t n, uint64_t n_ids, uint64_t** off, uint32_t** ids)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    if (!c->d_moff2.ensure(8 * (n + 1) + 8 * (n / 8)) || !c->d_mids2.ensure(4 * std::max<uint64_t>(n_ids, 1) + 4 * (n_ids / 8)))
+        return AD_E_NOMEM;
+    *off = c->d_moff2.as<uint64_t>();
+    *ids = c->d_mids2.as<uint32_t>();
+    c->dmiss_lists = n;
+    c->dmiss_ids = n_ids;
+    return 0;
+}
+
+static int cfk_miss_swap(void* vc, uint64_t** off, uint32_t** ids)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    swap_buf(c->d_moff, c->d_moff2);
+    swap_buf(c->d_mids, c->d_mids2);
+    *off = c->d_moff.as<uint64_t>();
+    *ids = c->d_mids.as<uint32_t>();
+    return 0;
+}
+
+// Start maintaining TxnInfo.missing() on the device: the host lists (NO_TXNIDS everywhere without a
+// load) as rank CSR, every entry its own list. 1: the lists cannot go to the device (stale, or an
+// id outside the dictionary): they are then marked stale by updates as before.
+static int dmiss_enable(ad_ctx* c, hipStream_t st)
+{
+    if (int rc = sync_host(c)) return rc;
+    auto& K = c->cfk;
+    if (K.miss_stale) return 1;
+    const uint64_t ne = K.status.size();
+    std::vector<uint64_t> off(ne + 1, 0);
+    std::vector<uint32_t> ids;
+    if (!K.miss_off.empty())
+    {
+        off.assign(K.miss_off.begin(), K.miss_off.end());
+        ids.resize(K.miss.size());
+        for (size_t j = 0; j < K.miss.size(); ++j)
+        {
+            const NormTid x = norm(K.miss[j]);
+            uint64_t lo = 0, hi = c->dict_msb.size();
+            while (lo < hi)
+            {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (norm_cmp(norm_tid(c->dict_msb[mid], c->dict_lsb[mid], c->dict_node[mid]), x) < 0) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo >= c->dict_msb.size() || norm_cmp(norm_tid(c->dict_msb[lo], c->dict_lsb[lo], c->dict_node[lo]), x) != 0)
+                return 1;
+            ids[j] = (uint32_t)(2 * lo + 1);
+        }
+    }
+    std::vector<uint32_t> mref(ne);
+    for (uint64_t e = 0; e < ne; ++e) mref[e] = (uint32_t)e;
+    if (int rc = upload(c, c->d_moff, off)) return rc;
+    if (int rc = upload(c, c->d_mids, ids.empty() ? std::vector<uint32_t>(1, 0) : ids)) return rc;
+    if (int rc = upload(c, c->d_mref, mref.empty() ? std::vector<uint32_t>(1, 0) : mref)) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->dmiss_lists = ne;
+    c->dmiss_ids = ids.size();
+    c->dmiss_on = true;
+    (void)st;
+    return 0;
+}
+
 static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats)
 {
     if (c->dirty)
         if (int rc = build_snapshot(c)) return rc;
+    // missing() on the device while batches bring their deps; a batch without deps hands the lists
+    // back to the host, where updates mark them stale (recovery then asks for a reload)
+    if (u.dep_off && !c->dmiss_on)
+    {
+        const int rc = dmiss_enable(c, st);
+        if (rc < 0) return rc;
+    }
+    else if (!u.dep_off && c->dmiss_on)
+    {
+        if (int rc = sync_host(c)) return rc;
+        if (c->host_stale == false && c->dmiss_on) { if (int rc = pull_missing(c)) return rc; }
+        c->dmiss_on = false;
+    }
     if (!c->cu) c->cu = cfk_upd_work_create();
     CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
                   c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
+                  c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr,
                   c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
     CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
                      c->d_w.as<uint2>(), c->d_w.cap / 8};
@@ -2903,10 +3030,19 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
     std::string e;
     const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
                        c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
-                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, cfk_keys_spare, cfk_keys_swap,
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
+                       c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
                        c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
     const uint64_t nd0 = c->dict_msb.size();
-    const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e);
+    CfkMiss miss;
+    miss.on = c->dmiss_on && u.dep_off;
+    miss.n_lists = c->dmiss_lists;
+    miss.off = c->d_moff.as<uint64_t>();
+    miss.ids = c->d_mids.as<uint32_t>();
+    miss.ctx = c;
+    miss.spare = cfk_miss_spare;
+    miss.swap = cfk_miss_swap;
+    const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e, &miss);
     if (o.n_new_keys)
     {
         // keys created on the device (they stay when the batch then failed): KeyLines, host copies
@@ -2972,6 +3108,7 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         stats->ms_stage[1] = o.ms_derive;
         stats->n_keys[0] = o.n_inserted;         // entries inserted
         stats->n_keys[1] = o.n_new_ids;          // ids appended to the dictionary
+        stats->n_keys[2] = o.n_additions;        // TRANSITIVELY_KNOWN entries from deps
     }
     return AD_OK;
 }
@@ -2982,6 +3119,8 @@ static int check_update_soa(ad_ctx* c, const ad_cfk_update_soa* u)
     if (u->n && (!u->keys || !u->txn_msb || !u->txn_lsb || !u->txn_node || !u->exec_msb || !u->exec_lsb ||
                  !u->exec_node || !u->status))
         return c->fail(AD_E_INVAL, "update batch with null arrays");
+    if (u->dep_off && (!u->dep_msb || !u->dep_lsb || !u->dep_node))
+        return c->fail(AD_E_INVAL, "update batch with dep_off but null dep arrays");
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     return 0;
@@ -2992,7 +3131,7 @@ int ad_cfk_update_device(ad_ctx* c, const ad_cfk_update_soa* u, void* stream, ui
     if (!c) return AD_E_INVAL;
     if (int rc = check_update_soa(c, u)) return rc;
     CfkUpdIn in{u->n, u->keys, u->txn_msb, u->txn_lsb, u->txn_node, u->exec_msb, u->exec_lsb, u->exec_node, u->status,
-                u->ballot_msb, u->ballot_lsb, u->ballot_node};
+                u->ballot_msb, u->ballot_lsb, u->ballot_node, u->dep_off, u->dep_msb, u->dep_lsb, u->dep_node};
     return cfk_update_run(c, in, stream ? (hipStream_t)stream : c->stream, n_applied, stats);
 }
 
@@ -3005,7 +3144,16 @@ int ad_cfk_update(ad_ctx* c, const ad_cfk_update_soa* u, uint64_t* n_applied, ad
     CfkUpdIn in{n, stage_q(c, c->u_k, u->keys, n, &rc), stage_q(c, c->u_tm, u->txn_msb, n, &rc),
                 stage_q(c, c->u_tl, u->txn_lsb, n, &rc), stage_q(c, c->u_tn, u->txn_node, n, &rc),
                 stage_q(c, c->u_em, u->exec_msb, n, &rc), stage_q(c, c->u_el, u->exec_lsb, n, &rc),
-                stage_q(c, c->u_en, u->exec_node, n, &rc), stage_q(c, c->u_st, u->status, n, &rc), nullptr, nullptr, nullptr};
+                stage_q(c, c->u_en, u->exec_node, n, &rc), stage_q(c, c->u_st, u->status, n, &rc), nullptr, nullptr, nullptr,
+                nullptr, nullptr, nullptr, nullptr};
+    if (u->dep_off)
+    {
+        const uint64_t nd = u->dep_off[n];
+        in.dep_off = stage_q(c, c->u_do, u->dep_off, n + 1, &rc);
+        in.dep_msb = stage_q(c, c->u_dm, u->dep_msb, nd, &rc);
+        in.dep_lsb = stage_q(c, c->u_dl, u->dep_lsb, nd, &rc);
+        in.dep_node = stage_q(c, c->u_dn, u->dep_node, nd, &rc);
+    }
     if (u->ballot_msb)
     {
         in.bal_msb = stage_q(c, c->u_bm, u->ballot_msb, n, &rc);
@@ -3376,7 +3524,7 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
         if (int rc = build_snapshot(c)) return rc;
     if (int rc = sync_host(c)) return rc;
     auto& K = c->cfk;
-    if (!K.miss.empty())
+    if (!K.miss.empty() || c->dmiss_on)
         return c->fail(AD_E_STATE, "ad_cfk_prune: TxnInfo.missing() lists are loaded; pruneBefore's missing-subset test "
                                    "(Pruning.java:239-251) is not on the device");
     const uint64_t nk = c->ds.n_keys;
@@ -3403,12 +3551,14 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
     if (!c->cu) c->cu = cfk_upd_work_create();
     CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
                   c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
+                  c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr,
                   c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
     CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
                      c->d_w.as<uint2>(), c->d_w.cap / 8};
     const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
                        c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
-                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, cfk_keys_spare, cfk_keys_swap,
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
+                       c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
                        c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
     CfkPruneOut o;
     std::string e;
@@ -3441,6 +3591,40 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
         stats->n_keys[0] = o.n_removed;
         stats->n_keys[1] = o.n_keys_pruned;
     }
+    return AD_OK;
+}
+
+int ad_cfk_missing(ad_ctx* c, uint64_t* n_entries, const uint64_t** off, const uint64_t** msb, const uint64_t** lsb,
+                   const int32_t** node)
+{
+    if (!c || !n_entries || !off || !msb || !lsb || !node) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    if (int rc = sync_host(c)) return rc;
+    auto& K = c->cfk;
+    if (K.miss_stale) return c->fail(AD_E_STATE, "missing() lists are stale (updates without deps moved entries): load them again");
+    const uint64_t ne = K.status.size();
+    if (K.miss_off.size() != ne + 1)
+    {
+        c->z_off.assign(ne + 1, 0);
+        *off = c->z_off.data();
+    }
+    else
+        *off = K.miss_off.data();
+    const uint64_t nm = K.miss.size();
+    c->y_msb.resize(nm);
+    c->y_lsb.resize(nm);
+    c->y_node.resize(nm);
+    for (uint64_t j = 0; j < nm; ++j)
+    {
+        c->y_msb[j] = K.miss[j].msb;
+        c->y_lsb[j] = K.miss[j].lsb;
+        c->y_node[j] = K.miss[j].node;
+    }
+    *n_entries = ne;
+    *msb = c->y_msb.data();
+    *lsb = c->y_lsb.data();
+    *node = c->y_node.data();
     return AD_OK;
 }
 

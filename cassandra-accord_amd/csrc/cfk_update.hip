@@ -166,7 +166,7 @@ __device__ inline uint32_t known_rank(const DevSnapshot& s, const DictSample& ds
 __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds, CfkDevState d, CfkUpdIn u, uint32_t* loc,
                                                     uint32_t* xr_out, unsigned long long* word, uint64_t* ins_key,
                                                     uint32_t* flags, const uint32_t* rk, const uint64_t* mpos, uint64_t U,
-                                                    UpdCtl* ctl)
+                                                    UpdCtl* ctl, int fold)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= u.n) return;
@@ -221,8 +221,276 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds
         return;
     }
     loc[i] = lo;
-    if (u.bal_msb) flags[u.n + i] = 1;
+    if (fold) flags[u.n + i] = 1;
     else atomicMax(word + lo, ((unsigned long long)st << 32) | (0xFFFFFFFFull - i));
+}
+
+// ---- TxnInfo.missing() and deps-derived additions (Updating.java:99-470, Utils.java:68-352) ----
+__device__ inline bool newer_than_dict(const DevSnapshot& s, const NormTid& t);
+
+// the update of dep j (dep_off ascending)
+__device__ inline uint64_t dep_owner(const CfkUpdIn& u, uint64_t j)
+{
+    uint64_t lo = 0, hi = u.n;            // last i with dep_off[i] <= j
+    while (hi - lo > 1)
+    {
+        const uint64_t m = (lo + hi) >> 1;
+        if (u.dep_off[m] <= j) lo = m;
+        else hi = m;
+    }
+    return lo;
+}
+
+// deps of updates with a deps status join the dictionary with the batch's ids (a superset of the
+// additions: an id nothing refers to changes no answer), so the additions batch never grows it
+__global__ __launch_bounds__(256) void k_dep_collect(DevSnapshot s, DictSample ds, CfkUpdIn u, uint64_t ndep, uint64_t* nw,
+                                                     uint64_t cap, UpdCtl* ctl)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ndep) return;
+    if (!st_has_exec(u.status[dep_owner(u, j)])) return;
+    const NormTid ref = norm_tid(u.txn_msb[0], u.txn_lsb[0], u.txn_node[0]);
+    const uint64_t l = u.dep_lsb[j];
+    const NormTid t = norm_tid(u.dep_msb[j], l, u.dep_node[j]);
+    if (!newer_than_dict(s, t))
+    {
+        uint64_t p;
+        if (dict_member_rank(s, ds, t, &p)) return;
+        ctl->older = 1u;
+    }
+    const uint32_t k = atomicAdd(&ctl->n_new, 1u);
+    nw[k] = (uint64_t)((uint32_t)t.node ^ 0x80000000u);
+    nw[cap + k] = t.lo;
+    nw[2 * cap + k] = t.hi;
+    nw[3 * cap + k] = l;
+    atomicOr(&ctl->diff[0], (unsigned long long)((uint32_t)t.node ^ (uint32_t)ref.node));
+    atomicOr(&ctl->diff[1], (unsigned long long)(t.lo ^ ref.lo));
+    atomicOr(&ctl->diff[2], (unsigned long long)(t.hi ^ ref.hi));
+}
+
+__device__ inline uint32_t key_index_of(const DevSnapshot& s, int64_t key)
+{
+    if (!s.n_keys) return KEY_EMPTY;
+    uint64_t h = key_hash(key) & s.khash_mask;
+    for (;;)
+    {
+        const KeySlot sl = s.khash[h];
+        if (sl.idx == KEY_EMPTY) return KEY_EMPTY;
+        if (sl.key == key) return sl.idx;
+        h = (h + 1) & s.khash_mask;
+    }
+}
+
+// entry of rank r in key k's byId, or LOC_NONE
+__device__ inline uint32_t seg_find(const DevSnapshot& s, const KeyRec& kr, uint32_t r)
+{
+    uint32_t lo = kr.seg_lo, hi = kr.seg_hi;
+    while (lo < hi)
+    {
+        const uint32_t m = (lo + hi) >> 1;
+        if ((s.ent[m].y & RANK_MASK) < r) lo = m + 1;
+        else hi = m;
+    }
+    return (lo < kr.seg_hi && (s.ent[lo].y & RANK_MASK) == r) ? lo : LOC_NONE;
+}
+
+// rank of every dep: a member's odd rank, else the even rank of its gap
+__global__ void k_dep_rank(DevSnapshot s, DictSample ds, CfkUpdIn u, uint64_t ndep, uint32_t* drank)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= ndep) return;
+    uint64_t p;
+    const uint32_t r = dict_member_rank(s, ds, norm_tid(u.dep_msb[j], u.dep_lsb[j], u.dep_node[j]), &p);
+    drank[j] = r ? r : (uint32_t)(2 * p);
+}
+
+// Does update i derive its entry's missing() from its deps (computeInfoAndAdditions, :174-188)? It
+// was applied, its status has deps, and its txnId is a key-domain one (a live range-domain id is
+// refused by the locate).
+__device__ inline bool upd_with_deps(const CfkUpdIn& u, const uint8_t* uapp, uint64_t i)
+{
+    return (uapp[i] & 1) && st_has_exec(u.status[i]) && !(u.txn_lsb[i] & 1);
+}
+
+// additions (:210-263): the deps of applied updates with deps statuses that their kind witnesses,
+// at or above the key's prunedBefore (removePrunedAdditions, Utils.java:229-246) and not in byId
+// after the batch -> TRANSITIVELY_KNOWN insertions. Pass 0 counts per update, pass 1 writes.
+template <int WRITE>
+__global__ __launch_bounds__(256) void k_add_deps(DevSnapshot s, CfkUpdIn u, const uint8_t* uapp, const uint32_t* drank,
+                                                  uint32_t* cnt, const uint64_t* off, int64_t* ak, uint64_t* atm,
+                                                  uint64_t* atl, int32_t* atn)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u.n) return;
+    uint32_t c = 0;
+    if (upd_with_deps(u, uapp, i))
+    {
+        const uint32_t k = key_index_of(s, u.keys[i]);
+        if (k != KEY_EMPTY)
+        {
+            const KeyRec kr = s.krec[k];
+            const uint32_t wk = kind_witnesses((uint32_t)((u.txn_lsb[i] >> 1) & 7));
+            uint64_t o = WRITE ? off[i] : 0;
+            for (uint64_t j = u.dep_off[i]; j < u.dep_off[i + 1]; ++j)
+            {
+                const uint32_t r = drank[j];
+                if (!((wk >> (uint32_t)((u.dep_lsb[j] >> 1) & 7)) & 1u)) continue;
+                if (kr.pruned && r < kr.pruned) continue;
+                if (seg_find(s, kr, r) != LOC_NONE) continue;
+                if (WRITE)
+                {
+                    ak[o] = u.keys[i];
+                    atm[o] = u.dep_msb[j];
+                    atl[o] = u.dep_lsb[j];
+                    atn[o] = u.dep_node[j];
+                    ++o;
+                }
+                ++c;
+            }
+        }
+    }
+    if (!WRITE) cnt[i] = c;
+}
+
+// the entry whose TxnInfo an applied update with deps made (its last applied update): dsrc[e] = i
+__global__ void k_miss_src(DevSnapshot s, DictSample ds, CfkUpdIn u, const uint8_t* uapp, uint32_t* dsrc)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u.n || uapp[i] != 3 || !upd_with_deps(u, uapp, i)) return;
+    const uint32_t k = key_index_of(s, u.keys[i]);
+    if (k == KEY_EMPTY) return;
+    uint64_t p;
+    const uint32_t r = dict_member_rank(s, ds, norm_tid(u.txn_msb[i], u.txn_lsb[i], u.txn_node[i]), &p);
+    const uint32_t e = r ? seg_find(s, s.krec[k], r) : LOC_NONE;
+    if (e != LOC_NONE) dsrc[e] = (uint32_t)i;
+}
+
+// per entry: below COMMITTED (a candidate for others' missing()), and that and inserted by this batch
+__global__ void k_miss_flags(uint64_t ne, CfkDevState d, uint32_t* f)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const bool pend = d.status[e] < AD_ST_COMMITTED;
+    f[e] = pend ? 1u : 0u;
+    f[ne + e] = (pend && d.mref[e] == MREF_BORN) ? 1u : 0u;
+}
+
+__global__ void k_miss_scatter(uint64_t ne, const uint32_t* f, const uint64_t* pp, uint32_t* pend)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    if (f[e]) pend[pp[e]] = (uint32_t)e;
+    if (f[ne + e]) pend[pp[ne] + pp[ne + 1 + e]] = (uint32_t)e;     // the born list after the pending one
+}
+
+// Every entry's missing() after the batch (thread per entry; pass 0 counts, pass 1 writes ranks
+// ascending):
+//   * statuses without deps: NO_TXNIDS (TxnInfo.create :254-262);
+//   * an entry its batch update derived (dsrc): computeInfoAndAdditions' list (:194-287) -- the
+//     key's entries below COMMITTED, below its depsKnownBefore (:561-580), its kind witnesses, other
+//     than itself, not in its deps;
+//   * any other entry with deps: its list less the ids now COMMITTED or later / INVALID
+//     (removeFromMissingArrays / removeSelfMissing) merged with this batch's insertions below
+//     COMMITTED under its depsKnownBefore that its kind witnesses (addToMissingArrays /
+//     insertOrUpdateWithAdditions' missingSource).
+template <int WRITE>
+__global__ __launch_bounds__(256) void k_miss_build(DevSnapshot s, CfkDevState d, CfkUpdIn u, const uint32_t* dsrc,
+                                                    const uint32_t* drank, const uint64_t* pp, const uint32_t* pend,
+                                                    const uint64_t* ooff, const uint32_t* oids, uint32_t* cnt,
+                                                    const uint64_t* noff, uint32_t* nids)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t ne = s.n_ent;
+    if (e >= ne) return;
+    const uint32_t st = d.status[e];
+    uint64_t c = 0, o = WRITE ? noff[e] : 0;
+    auto emit = [&](uint32_t r) {
+        if (WRITE) nids[o++] = r;
+        ++c;
+    };
+    if (st_has_exec(st))
+    {
+        const uint32_t k = d.ekey[e];
+        const KeyRec kr = s.krec[k];
+        const uint32_t y = s.ent[e].y, self = y & RANK_MASK;
+        const uint32_t wk = kind_witnesses(y >> RANK_BITS);
+        const uint32_t dkb = st == AD_ST_ACCEPTED ? self : d.xrank[e];
+        const uint64_t n_pend = pp[ne];
+        const uint32_t i = dsrc[e];
+        if (i != LOC_NONE)
+        {
+            // depsKnownBeforePos is searched from the txn's own byId position (:202-208): the entries
+            // below its txnId count even when executeAt is below it
+            const uint32_t bound = max(dkb, self);
+            uint64_t jd = u.dep_off[i];
+            const uint64_t jd1 = u.dep_off[i + 1];
+            for (uint64_t q = pp[kr.seg_lo]; q < pp[kr.seg_hi]; ++q)
+            {
+                const uint32_t p = pend[q];
+                const uint32_t yp = s.ent[p].y, rp = yp & RANK_MASK;
+                if (rp >= bound) break;
+                if (p == e || !((wk >> (yp >> RANK_BITS)) & 1u)) continue;
+                while (jd < jd1 && drank[jd] < rp) ++jd;
+                if (jd < jd1 && drank[jd] == rp) continue;
+                emit(rp);
+            }
+        }
+        else
+        {
+            const uint32_t L = d.mref[e];
+            uint64_t a = 0, a1 = 0;
+            if (L != MREF_NONE && L != MREF_BORN)
+            {
+                a = ooff[L];
+                a1 = ooff[L + 1];
+            }
+            const uint64_t* bp = pp + (ne + 1);
+            uint64_t b = bp[kr.seg_lo], b1 = bp[kr.seg_hi];
+            const uint32_t* born = pend + n_pend;
+            // the old ids still below COMMITTED, merged with the born candidates (both ascending)
+            uint32_t ra = 0;
+            bool ha = false;
+            auto next_a = [&]() {
+                ha = false;
+                while (a < a1)
+                {
+                    const uint32_t r = oids[a++];
+                    const uint32_t pe = seg_find(s, kr, r);
+                    if (pe != LOC_NONE && d.status[pe] < AD_ST_COMMITTED) { ra = r; ha = true; return; }
+                }
+            };
+            uint32_t rb = 0;
+            bool hb = false;
+            auto next_b = [&]() {
+                hb = false;
+                while (b < b1)
+                {
+                    const uint32_t p = born[b++];
+                    const uint32_t yp = s.ent[p].y, rp = yp & RANK_MASK;
+                    if (rp >= dkb) { b = b1; return; }
+                    if (p == e || !((wk >> (yp >> RANK_BITS)) & 1u)) continue;
+                    rb = rp;
+                    hb = true;
+                    return;
+                }
+            };
+            next_a();
+            next_b();
+            while (ha || hb)
+            {
+                if (ha && (!hb || ra < rb)) { emit(ra); next_a(); }
+                else if (hb && (!ha || rb < ra)) { emit(rb); next_b(); }
+                else { emit(ra); next_a(); next_b(); }
+            }
+        }
+    }
+    if (!WRITE) cnt[e] = (uint32_t)c;
+}
+
+__global__ void k_mref_identity(uint64_t ne, uint32_t* mref)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < ne) mref[e] = (uint32_t)e;
 }
 
 // ---- insertion ------------------------------------------------------------------------------
@@ -559,32 +827,40 @@ __global__ void k_compact(uint64_t n, const uint32_t* flags, const uint64_t* pos
 // with ballots: the updates of one present entry (sorted by entry, batch order within) fold in
 // order through CommandsForKey.update's replacement test; the entry's old state is kept at its
 // first update's index for a rollback
+// uapp (non-null): per update 1 = applied (replaced the entry when its turn came), 2 = the last
+// applied update of its entry (the entry's TxnInfo comes from it). Without ballots anywhere
+// (d.ballot null) every ballot is Ballot.ZERO.
 __global__ void k_fold_present(uint64_t m, const uint64_t* ks, const uint32_t* vs, CfkUpdIn u, const uint32_t* xr,
-                               CfkDevState d, uint2* bk, Bal* bkb, uint8_t* chg, UpdCtl* ctl)
+                               CfkDevState d, uint2* bk, Bal* bkb, uint8_t* chg, UpdCtl* ctl, uint8_t* uapp)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m || (j > 0 && ks[j - 1] == ks[j])) return;
     const uint32_t e = (uint32_t)ks[j];
     uint32_t st = d.status[e], x = d.xrank[e];
-    Bal b = d.ballot[e];
+    Bal b = d.ballot ? d.ballot[e] : Bal{0, 0, 0, 0};
     unsigned long long cnt = 0;
+    uint32_t last = 0xFFFFFFFFu;
     for (uint64_t t = j; t < m && ks[t] == e; ++t)
     {
         const uint32_t i = vs[t], ns = u.status[i];
         const Bal nb = upd_ballot(u, i);
+        if (uapp) uapp[i] = 0;
         if (!replaces(ns, st, nb, b)) continue;
         st = ns;
         x = xr[i];
         b = kept_ballot(ns, nb);
         ++cnt;
+        if (uapp) uapp[i] = 1;
+        last = i;
     }
     if (!cnt) return;
+    if (uapp) uapp[last] = 3;
     const uint32_t i0 = vs[j];
     bk[i0] = make_uint2(d.status[e], d.xrank[e]);
-    bkb[i0] = d.ballot[e];
+    if (d.ballot) bkb[i0] = d.ballot[e];
     d.status[e] = (uint8_t)st;
     d.xrank[e] = x;
-    d.ballot[e] = b;
+    if (d.ballot) d.ballot[e] = b;
     chg[e] = 1;
     atomicAdd(&ctl->applied, cnt);
 }
@@ -592,7 +868,7 @@ __global__ void k_fold_present(uint64_t m, const uint64_t* ks, const uint32_t* v
 // per group (one new entry), with ballots: the group's updates fold in batch order (the first
 // inserts); gword = final status << 32 | ~(update index the entry takes executeAt and ballot from)
 __global__ void k_ins_fold(const uint64_t* ks, const uint32_t* vs, uint64_t q, const uint32_t* gflag, const uint64_t* gs,
-                           CfkUpdIn u, unsigned long long* gword, uint32_t* gkey, uint32_t* grank, UpdCtl* ctl)
+                           CfkUpdIn u, unsigned long long* gword, uint32_t* gkey, uint32_t* grank, UpdCtl* ctl, uint8_t* uapp)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= q || !gflag[j]) return;
@@ -602,16 +878,20 @@ __global__ void k_ins_fold(const uint64_t* ks, const uint32_t* vs, uint64_t q, c
     uint32_t il = vs[j], st = u.status[il];
     Bal b = kept_ballot(st, upd_ballot(u, il));
     unsigned long long cnt = 0;
+    if (uapp) uapp[il] = 1;                   // the insertion
     for (uint64_t t = j + 1; t < q && ks[t] == ks[j]; ++t)
     {
         const uint32_t i = vs[t], ns = u.status[i];
         const Bal nb = upd_ballot(u, i);
+        if (uapp) uapp[i] = 0;
         if (!replaces(ns, st, nb, b)) continue;
         st = ns;
         il = i;
         b = kept_ballot(ns, nb);
         ++cnt;
+        if (uapp) uapp[i] = 1;
     }
+    if (uapp) uapp[il] = 3;
     gword[g] = ((unsigned long long)st << 32) | (0xFFFFFFFFull - il);
     if (cnt) atomicAdd(&ctl->applied, cnt);
 }
@@ -647,7 +927,7 @@ __global__ void k_ins_before(uint64_t nk, const uint32_t* gkey, uint64_t G, uint
     ib[k] = (uint32_t)lo;
 }
 
-struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; Bal* bal; uint8_t* chg; };
+struct EntArrays { uint2* ent; uint8_t* status; uint32_t* xrank; uint32_t* ekey; Bal* bal; uint8_t* chg; uint32_t* mref; };
 
 // an old entry moves up by the new entries before it: those of lower keys, and those of its key
 // with a lower rank (a mid-segment insert, :1002-1007)
@@ -674,6 +954,7 @@ __global__ __launch_bounds__(256) void k_ins_move_old(uint64_t ne, EntArrays a, 
     b.xrank[p] = a.xrank[e];
     b.ekey[p] = k;
     if (b.bal) b.bal[p] = a.bal[e];
+    if (b.mref) b.mref[p] = a.mref[e];
     b.chg[p] = a.chg[e];
     mv[e] = (uint32_t)p;
 }
@@ -705,6 +986,7 @@ __global__ void k_ins_place(uint64_t G, const uint32_t* gkey, const uint32_t* gr
     b.xrank[p] = xr[i];
     b.ekey[p] = k;
     if (b.bal) b.bal[p] = kept_ballot((uint32_t)(wd >> 32), upd_ballot(u, i));
+    if (b.mref) b.mref[p] = MREF_BORN;
     b.chg[p] = 1;
 }
 
@@ -972,6 +1254,8 @@ struct CfkUpdWork {
     DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
     DBuf mh, ml, mn, mraw, mpos;
     DBuf bkb, uflag, upos, rk;
+    // missing() maintenance: per update applied flags, dep ranks, additions batch, derivation
+    DBuf uapp, drank, acnt, aoff, a_k, a_tm, a_tl, a_tn, a_st, dsrc, mflag, mpp, mpend, mcnt, moff;
     DBuf kn_a, kn_b, kv_a, kv_b, kflag, kfpos, knew, kpos;   // new keys
     // incremental committed order: the last derivation's order (entry indices), per-entry changed
     // flags (double-buffered with the entry arrays), the insertion's old -> new entry map
@@ -1007,6 +1291,10 @@ static uint32_t bytes_of(uint64_t v)
     do {                                                                                          \
         hipError_t _e = (expr);                                                                   \
         if (_e != hipSuccess) { *err = std::string(#expr) + ": " + hipGetErrorString(_e); return AD_E_DEVICE; } \
+    } while (0)
+#define UALLOC_V(buf, bytes)                                                                      \
+    do {                                                                                          \
+        if (!(buf).ensure((bytes), false)) return DictSample{nullptr, nullptr, nullptr, 0};       \
     } while (0)
 #define UALLOC(buf, bytes, zero)                                                                  \
     do {                                                                                          \
@@ -1246,6 +1534,7 @@ static int merge_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
     if (grow.n_rtxw) k_remap_txw<<<blocks(grow.n_rtxw), 256, 0, st>>>(grow.n_rtxw, grow.r_txw, mpos, U);
     if (grow.n_cell_ent) k_remap_cells<<<blocks(grow.n_cell_ent), 256, 0, st>>>(grow.n_cell_ent, grow.cell_ent, mpos, U);
     if (grow.n_rb) k_remap_txw<<<blocks(grow.n_rb), 256, 0, st>>>(grow.n_rb, grow.rb_wm, mpos, U);
+    if (grow.n_mids) k_remap_txw<<<blocks(grow.n_mids), 256, 0, st>>>(grow.n_mids, grow.m_ids, mpos, U);
     UCHK(hipGetLastError());
     if (int rc = grow.dict_swap(grow.ctx, &nd.hi, &nd.lo, &nd.node, &nd.raw)) { *err = "dictionary merge"; return rc; }
     uint64_t lh = 0, ll = 0;
@@ -1271,13 +1560,14 @@ static int merge_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
 // Add the batch's ids the dictionary does not hold (sorted, unique): appended when all are newer
 // than its newest id, merged otherwise.
 static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const DictSample& ds, const CfkUpdIn& u,
-                           const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err)
+                           const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err, uint64_t ndep = 0)
 {
-    const uint64_t n = u.n, cap = 2 * n;
+    const uint64_t n = u.n, cap = 2 * n + ndep;
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
     UALLOC(w->nw, 8 * 4 * cap, false);
     UALLOC(w->rk, 8 * n, false);
     k_ins_collect<<<blocks(n), 256, 0, st>>>(s, ds, u, w->nw.as<uint64_t>(), cap, w->rk.as<uint32_t>(), ctl);
+    if (ndep) k_dep_collect<<<blocks(ndep), 256, 0, st>>>(s, ds, u, ndep, w->nw.as<uint64_t>(), cap, ctl);
     UCHK(hipGetLastError());
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
@@ -1355,7 +1645,8 @@ struct InsUndo {
 };
 
 static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, const CfkGrow& grow,
-                          hipStream_t st, uint64_t q, uint64_t* G_out, InsUndo* undo, std::string* err)
+                          hipStream_t st, uint64_t q, uint64_t* G_out, InsUndo* undo, std::string* err, bool fold,
+                          uint8_t* uapp)
 {
     const uint64_t ne = s.n_ent, nk = s.n_keys;
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
@@ -1391,9 +1682,10 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     UALLOC(w->ib, 4 * (nk + 1), false);
     UALLOC(w->krec_bk, sizeof(KeyRec) * std::max<uint64_t>(nk, 1), false);
     UCHK(hipMemsetAsync(w->gword.p, 0, 8 * G, st));
-    if (u.bal_msb)
+    if (fold)
         k_ins_fold<<<blocks(q), 256, 0, st>>>(ks, vs, q, w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), u,
-                                              w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>(), ctl);
+                                              w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>(), ctl,
+                                              uapp);
     else
         k_ins_claim<<<blocks(q), 256, 0, st>>>(ks, vs, q, w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), u.status,
                                                w->gword.as<unsigned long long>(), w->gkey.as<uint32_t>(), w->grank.as<uint32_t>());
@@ -1401,9 +1693,9 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     UCHK(hipGetLastError());
     UALLOC(w->chg[w->chg_cur ^ 1], ne + G, false);
     UALLOC(w->mv, 4 * std::max<uint64_t>(ne, 1), false);
-    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot, w->chg[w->chg_cur].as<uint8_t>()}, b{};
+    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot, w->chg[w->chg_cur].as<uint8_t>(), d.mref}, b{};
     b.chg = w->chg[w->chg_cur ^ 1].as<uint8_t>();
-    if (int rc = grow.entries(grow.ctx, ne + G, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal)) { *err = "entry growth"; return rc; }
+    if (int rc = grow.entries(grow.ctx, ne + G, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal, &b.mref)) { *err = "entry growth"; return rc; }
     const uint64_t padded = std::max<uint64_t>(64, (ne + G + 63) / 64 * 64);
     if (padded > ne + G) UCHK(hipMemsetAsync(b.ent + ne + G, 0, sizeof(uint2) * (padded - ne - G), st));
     if (ne) k_ins_move_old<<<blocks(ne), 256, 0, st>>>(ne, a, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), b, w->mv.as<uint32_t>());
@@ -1416,7 +1708,7 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
         k_ins_krec<<<blocks(nk), 256, 0, st>>>(nk, w->ib.as<uint32_t>(), w->grank.as<uint32_t>(), d.krec);
     }
     UCHK(hipGetLastError());
-    const int src = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot);
+    const int src = grow.swap(grow.ctx, ne + G, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot, &d.mref);
     undo->swapped = true;         // the buffers are exchanged even when sizing the trees then failed
     w->chg_cur ^= 1;              // the changed flags moved with the entries
     w->moved = true;
@@ -1427,13 +1719,28 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     return AD_OK;
 }
 
+static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, uint64_t ndep,
+                            CfkDerivedBufs* bufs, int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*),
+                            void* need_ctx, const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err,
+                            CfkMiss* miss);
+
 int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
                    int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*), void* need_ctx, const CfkGrow& grow,
-                   hipStream_t st, CfkUpdOut* out, std::string* err)
+                   hipStream_t st, CfkUpdOut* out, std::string* err, CfkMiss* miss)
 {
     const uint64_t n = u.n;
     *out = CfkUpdOut{};
     if (n == 0) return AD_OK;
+    // missing() maintenance (with the deps of the batch): the updates fold in batch order, so each
+    // update knows whether it applied and which one an entry's TxnInfo comes from
+    const bool track = miss && miss->on && u.dep_off && d.mref;
+    uint64_t ndep = 0;
+    if (track)
+    {
+        if (hipMemcpy(&ndep, u.dep_off + n, 8, hipMemcpyDeviceToHost) != hipSuccess) { *err = "dep_off"; return AD_E_DEVICE; }
+        UALLOC(w->uapp, n, false);
+        UCHK(hipMemsetAsync(w->uapp.p, 0, n, st));
+    }
     if (n >= 0x7FFFFFFFull) { *err = "more than 2^31-2 updates in one batch"; return AD_E_INVAL; }
     if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
     for (auto& e : w->ev)
@@ -1511,7 +1818,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     if (out->n_new_keys) UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
     {
         const DictSample ds0 = sample();
-        if (int rc = grow_dictionary(w, s, d, ds0, u, grow, st, out, err))
+        if (int rc = grow_dictionary(w, s, d, ds0, u, grow, st, out, err, ndep))
             return rc == AD_E_CAPACITY ? drop_new_ids(rc) : rederive(rc);
     }
     if (w->h_ctl->err) return rederive(drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx)));
@@ -1519,14 +1826,15 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     // ---- 1. locate and validate; nothing changes unless the whole batch is valid
     const DictSample dsm = sample();
     const bool bm = u.bal_msb != nullptr;
-    const int nf = bm ? 2 : 1;
+    const bool fold = bm || track;
+    const int nf = fold ? 2 : 1;
     UALLOC(w->uflag, 4ull * 2 * n, false);
     UALLOC(w->upos, 8ull * 2 * (n + 1), false);
     UALLOC(w->bsum, 8ull * 2 * ((n + 1023) / 1024 + 8), false);
     k_upd_locate<<<blocks(n), 256, 0, st>>>(s, dsm, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
                                             w->word.as<unsigned long long>(), w->ins_k.as<uint64_t>(),
                                             w->uflag.as<uint32_t>(), w->rk.as<uint32_t>(), out->merge_pos,
-                                            out->merged ? out->n_new_ids : 0, ctl);
+                                            out->merged ? out->n_new_ids : 0, ctl, fold ? 1 : 0);
     UCHK(hipGetLastError());
     UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), n, nf, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), n, nf, ctl->tot3);
@@ -1538,7 +1846,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         UCHK(hipStreamSynchronize(st));
         return rederive(drop_new_ids(describe(w->h_ctl->err, w->h_ctl->err_idx)));
     }
-    const uint64_t q = w->h_ctl->tot3[0], mp = bm ? w->h_ctl->tot3[1] : 0, ne0 = s.n_ent;
+    const uint64_t q = w->h_ctl->tot3[0], mp = fold ? w->h_ctl->tot3[1] : 0, ne0 = s.n_ent;
     // the batch's first ballots: the store's entries all hold Ballot.ZERO until now
     if (bm && !d.ballot && ne0)
         if (int rc = grow.ballot_init(grow.ctx, ne0, &d.ballot)) { *err = "ballot array"; return rederive(drop_new_ids(rc)); }
@@ -1549,7 +1857,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     UALLOC(w->cv2, 4 * cq, false);
     UALLOC(w->bkb, sizeof(Bal) * n, false);
     UCHK(hipMemsetAsync(w->bk.p, 0xFF, 8 * n, st));          // bk[i].x = none: nothing to roll back
-    if (bm)
+    if (fold)
     {
         if (mp)
         {
@@ -1571,7 +1879,8 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
                                           w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
             }
             k_fold_present<<<blocks(mp), 256, 0, st>>>(mp, ks, vs, u, w->xr.as<uint32_t>(), d, w->bk.as<uint2>(),
-                                                       w->bkb.as<Bal>(), w->chg[w->chg_cur].as<uint8_t>(), ctl);
+                                                       w->bkb.as<Bal>(), w->chg[w->chg_cur].as<uint8_t>(), ctl,
+                                                       track ? w->uapp.as<uint8_t>() : nullptr);
         }
     }
     else
@@ -1589,7 +1898,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         std::string e2;
         if (undo.swapped)
         {
-            if (grow.swap(grow.ctx, ne0, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot)) { *err += "; rollback failed"; return AD_E_DEVICE; }
+            if (grow.swap(grow.ctx, ne0, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot, &d.mref)) { *err += "; rollback failed"; return AD_E_DEVICE; }
             s.ent = d.ent;
             s.n_ent = ne0;
         }
@@ -1607,7 +1916,8 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     };
     uint64_t G = 0;
     if (q)
-        if (int rc = insert_entries(w, s, d, u, grow, st, q, &G, &undo, err)) return rollback(rc);
+        if (int rc = insert_entries(w, s, d, u, grow, st, q, &G, &undo, err, fold, track ? w->uapp.as<uint8_t>() : nullptr))
+            return rollback(rc);
     UCHK(hipEventRecord(w->ev[1], st));
 
     // ---- 2. re-derive the snapshot arrays from the per-entry state (committed order incrementally)
@@ -1625,6 +1935,111 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     out->n_inserted = G;
     // a duplicate committed executeAt: undo the batch and derive the previous state again
     if (w->h_ctl->err) return rollback(describe(w->h_ctl->err, w->h_ctl->err_idx));
+    if (track) return miss_after_batch(w, s, d, u, ndep, bufs, need, need_ctx, grow, st, out, err, miss);
+    return AD_OK;
+}
+
+// After a batch with deps (missing() maintenance on): the additions as a second batch of
+// TRANSITIVELY_KNOWN insertions (their ids already joined the dictionary with the batch), then every
+// entry's missing() rebuilt (k_miss_build). The explicit batch stands when this part fails.
+static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, uint64_t ndep,
+                            CfkDerivedBufs* bufs, int (*need)(void*, uint64_t, uint64_t, uint64_t, CfkDerivedBufs*),
+                            void* need_ctx, const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err,
+                            CfkMiss* miss)
+{
+    const uint64_t n = u.n;
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    const uint8_t* uapp = w->uapp.as<uint8_t>();
+    auto dsample = [&]() -> DictSample {
+        const uint64_t n_samp = (s.n_dict + SAMP - 1) / SAMP;
+        UALLOC_V(w->sm_hi, 8 * std::max<uint64_t>(n_samp, 1));
+        UALLOC_V(w->sm_lo, 8 * std::max<uint64_t>(n_samp, 1));
+        UALLOC_V(w->sm_node, 4 * std::max<uint64_t>(n_samp, 1));
+        if (n_samp)
+            k_dict_sample<<<blocks(n_samp), 256, 0, st>>>(s, w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(),
+                                                          w->sm_node.as<int32_t>(), n_samp);
+        return DictSample{w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(), w->sm_node.as<int32_t>(), n_samp};
+    };
+    // ---- additions (computeInfoAndAdditions :210-263, insertOrUpdateWithAdditions)
+    UALLOC(w->drank, 4 * std::max<uint64_t>(ndep, 1), false);
+    UALLOC(w->acnt, 4 * n, false);
+    UALLOC(w->aoff, 8 * (n + 1), false);
+    UALLOC(w->bsum, 8 * ((n + 1023) / 1024 + 8), false);
+    {
+        const DictSample ds = dsample();
+        if (ndep) k_dep_rank<<<blocks(ndep), 256, 0, st>>>(s, ds, u, ndep, w->drank.as<uint32_t>());
+    }
+    k_add_deps<0><<<blocks(n), 256, 0, st>>>(s, u, uapp, w->drank.as<uint32_t>(), w->acnt.as<uint32_t>(), nullptr, nullptr,
+                                             nullptr, nullptr, nullptr);
+    UCHK(run_scan_arrays(w->acnt.as<uint32_t>(), w->aoff.as<uint64_t>(), n, 1, w->bsum.as<uint64_t>(), st));
+    uint64_t na = 0;
+    UCHK(hipMemcpyAsync(&na, w->aoff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    if (na)
+    {
+        UALLOC(w->a_k, 8 * na, false);
+        UALLOC(w->a_tm, 8 * na, false);
+        UALLOC(w->a_tl, 8 * na, false);
+        UALLOC(w->a_tn, 4 * na, false);
+        UALLOC(w->a_st, na, false);
+        k_add_deps<1><<<blocks(n), 256, 0, st>>>(s, u, uapp, w->drank.as<uint32_t>(), nullptr, w->aoff.as<uint64_t>(),
+                                                 w->a_k.as<int64_t>(), w->a_tm.as<uint64_t>(), w->a_tl.as<uint64_t>(),
+                                                 w->a_tn.as<int32_t>());
+        UCHK(hipMemsetAsync(w->a_st.p, AD_ST_TRANSITIVELY_KNOWN, na, st));
+        UCHK(hipGetLastError());
+        CfkUpdIn ua{na, w->a_k.as<int64_t>(), w->a_tm.as<uint64_t>(), w->a_tl.as<uint64_t>(), w->a_tn.as<int32_t>(),
+                    w->a_tm.as<uint64_t>(), w->a_tl.as<uint64_t>(), w->a_tn.as<int32_t>(), w->a_st.as<uint8_t>(),
+                    nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+        CfkUpdOut o2;
+        if (int rc = run_cfk_update(w, s, d, ua, bufs, need, need_ctx, grow, st, &o2, err, nullptr))
+        {
+            *err = "deps-derived additions: " + *err;
+            return rc;
+        }
+        if (o2.merged || o2.n_new_ids || o2.n_new_keys) { *err = "deps-derived additions grew the dictionary (internal)"; return AD_E_STATE; }
+        out->n_additions = o2.n_inserted;
+        out->n_applied += o2.n_inserted;
+        out->n_inserted += o2.n_inserted;
+        out->ms_derive += o2.ms_total;
+        out->ms_total += o2.ms_total;
+    }
+    // ---- every entry's missing() (k_miss_build)
+    const uint64_t ne = s.n_ent;
+    if (!ne) return AD_OK;
+    UALLOC(w->dsrc, 4 * ne, false);
+    UALLOC(w->mflag, 4 * 2 * ne, false);
+    UALLOC(w->mpp, 8 * 2 * (ne + 1), false);
+    UALLOC(w->mpend, 4 * 2 * ne, false);
+    UALLOC(w->mcnt, 4 * ne, false);
+    UALLOC(w->moff, 8 * (ne + 1), false);
+    UALLOC(w->bsum, 8 * 2 * ((ne + 1023) / 1024 + 8), false);
+    UCHK(hipMemsetAsync(w->dsrc.p, 0xFF, 4 * ne, st));
+    {
+        const DictSample ds = dsample();
+        k_miss_src<<<blocks(n), 256, 0, st>>>(s, ds, u, uapp, w->dsrc.as<uint32_t>());
+    }
+    k_miss_flags<<<blocks(ne), 256, 0, st>>>(ne, d, w->mflag.as<uint32_t>());
+    UCHK(run_scan_arrays(w->mflag.as<uint32_t>(), w->mpp.as<uint64_t>(), ne, 2, w->bsum.as<uint64_t>(), st));
+    k_miss_scatter<<<blocks(ne), 256, 0, st>>>(ne, w->mflag.as<uint32_t>(), w->mpp.as<uint64_t>(), w->mpend.as<uint32_t>());
+    k_miss_build<0><<<blocks(ne), 256, 0, st>>>(s, d, u, w->dsrc.as<uint32_t>(), w->drank.as<uint32_t>(), w->mpp.as<uint64_t>(),
+                                                w->mpend.as<uint32_t>(), miss->off, miss->ids, w->mcnt.as<uint32_t>(), nullptr,
+                                                nullptr);
+    UCHK(run_scan_arrays(w->mcnt.as<uint32_t>(), w->moff.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
+    uint64_t nm = 0;
+    UCHK(hipMemcpyAsync(&nm, w->moff.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    uint64_t* noff = nullptr;
+    uint32_t* nids = nullptr;
+    if (int rc = miss->spare(miss->ctx, ne, nm, &noff, &nids)) { *err = "missing() lists"; return rc; }
+    UCHK(hipMemcpyAsync(noff, w->moff.p, 8 * (ne + 1), hipMemcpyDeviceToDevice, st));
+    k_miss_build<1><<<blocks(ne), 256, 0, st>>>(s, d, u, w->dsrc.as<uint32_t>(), w->drank.as<uint32_t>(), w->mpp.as<uint64_t>(),
+                                                w->mpend.as<uint32_t>(), miss->off, miss->ids, nullptr, noff, nids);
+    k_mref_identity<<<blocks(ne), 256, 0, st>>>(ne, d.mref);
+    UCHK(hipGetLastError());
+    UCHK(hipStreamSynchronize(st));
+    if (int rc = miss->swap(miss->ctx, &miss->off, &miss->ids)) { *err = "missing() lists"; return rc; }
+    miss->n_lists = ne;
+    (void)ctl;
     return AD_OK;
 }
 
@@ -1741,6 +2156,7 @@ __global__ __launch_bounds__(256) void k_prune_move(uint64_t ne, EntArrays a, co
     b.xrank[j] = a.xrank[e];
     b.ekey[j] = a.ekey[e];
     if (a.bal) b.bal[j] = a.bal[e];
+    if (a.mref) b.mref[j] = a.mref[e];
 }
 
 }  // namespace
@@ -1803,14 +2219,14 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
     // compaction into the spare per-entry arrays, segments and prunedBefore, then a full derivation
     unsigned long long* nkp = reinterpret_cast<unsigned long long*>(&ctl->tot2[1]);
     UCHK(hipMemsetAsync(nkp, 0, 8, st));
-    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot, nullptr}, b{};
-    if (int rc = grow.entries(grow.ctx, ne - R, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal)) { *err = "entry arrays"; return rc; }
+    EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot, nullptr, d.mref}, b{};
+    if (int rc = grow.entries(grow.ctx, ne - R, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal, &b.mref)) { *err = "entry arrays"; return rc; }
     const uint64_t padded = std::max<uint64_t>(64, (ne - R + 63) / 64 * 64);
     if (padded > ne - R) UCHK(hipMemsetAsync(b.ent + (ne - R), 0, sizeof(uint2) * (padded - (ne - R)), st));
     k_prune_move<<<blocks(ne), 256, 0, st>>>(ne, a, w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), b);
     k_prune_keys<<<blocks(nk), 256, 0, st>>>(nk, d.krec, w->upos.as<uint64_t>(), p_pos, p_tr, nkp);
     UCHK(hipGetLastError());
-    if (int rc = grow.swap(grow.ctx, ne - R, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot)) { *err = "entry swap"; return rc; }
+    if (int rc = grow.swap(grow.ctx, ne - R, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot, &d.mref)) { *err = "entry swap"; return rc; }
     s.ent = d.ent;
     s.n_ent = ne - R;
     w->cm_valid = false;          // entry indices changed: the next derivation sorts afresh

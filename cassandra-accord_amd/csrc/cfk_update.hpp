@@ -19,6 +19,9 @@ struct CfkUpdIn {
     const uint8_t* status;
     // the command's ballot (acceptedOrCommitted) per update; null = Ballot.ZERO for every update
     const uint64_t* bal_msb; const uint64_t* bal_lsb; const int32_t* bal_node;
+    // the command's deps on the key per update (partialDeps().txnIds(key) past shardRedundantBefore,
+    // ascending): [dep_off[i], dep_off[i+1]); null = none given
+    const uint64_t* dep_off; const uint64_t* dep_msb; const uint64_t* dep_lsb; const int32_t* dep_node;
 };
 
 // TxnInfo.ballot() of an entry (raw Timestamp fields; zero = Ballot.ZERO)
@@ -39,6 +42,7 @@ struct CfkDevState {
     uint32_t* ekey;                // [n_ent] key index
     uint64_t* dict_lsb_raw;  // [n_dict] raw lsb of every dictionary id (flag-bit identity check)
     Bal* ballot;             // [n_ent] or null: every entry's ballot is Ballot.ZERO
+    uint32_t* mref;          // [n_ent] or null: the entry's TxnInfo.missing() list in CfkMiss (MREF_*)
     // derived arrays rewritten in place (the snapshot's const views alias them)
     uint2* ent; KeyRec* krec; KeyEntry* kent;
 };
@@ -63,10 +67,12 @@ struct CfkGrow {
     int (*dict)(void* ctx, uint64_t n_old, uint64_t n_new, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** lsb_raw);
     // spare per-entry arrays for ne_new entries (ent padded to whole 64-entry frames); *bal only
     // when the store holds ballots (else left null)
-    int (*entries)(void* ctx, uint64_t ne_new, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey, Bal** bal);
+    int (*entries)(void* ctx, uint64_t ne_new, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey, Bal** bal,
+                   uint32_t** mref);
     // make the spare arrays current (commit = true) or current ones spare again (rollback) and size
     // the snapshot's trees for ne entries; returns the now-current arrays
-    int (*swap)(void* ctx, uint64_t ne, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey, Bal** bal);
+    int (*swap)(void* ctx, uint64_t ne, uint2** ent, uint8_t** status, uint32_t** xrank, uint32_t** ekey, Bal** bal,
+                uint32_t** mref);
     // the store's first ballots: a zeroed (Ballot.ZERO) array for ne entries
     int (*ballot_init)(void* ctx, uint64_t ne, Bal** bal);
     // dictionary merge (new ids older than the newest one): spare dictionary arrays for n ids, and
@@ -78,12 +84,31 @@ struct CfkGrow {
     uint32_t* r_txw; uint64_t n_rtxw;
     uint64_t* cell_ent; uint64_t n_cell_ent;
     uint32_t* rb_wm; uint64_t n_rb;
+    uint32_t* m_ids; uint64_t n_mids;      // TxnInfo.missing() ids as ranks (CfkMiss), null: none
     // new keys (a CommandsForKey created by the update): spare key-indexed arrays for nk keys and a
     // key hash of at least 2 nk slots; keys_swap makes them current. kcell: the current per-key
     // stabbing cells (NO_CELL without a stabbing index)
     int (*keys_spare)(void* ctx, uint64_t nk, KeyBufs* b);
     int (*keys_swap)(void* ctx, KeyBufs* b);
     const uint32_t* kcell;
+};
+
+// TxnInfo.missing() lists on the device (CommandsForKey.java:332-341): list j = ids
+// [off[j], off[j+1]) as ranks, ascending; entry e's list is mref[e] (MREF_NONE: NO_TXNIDS;
+// MREF_BORN: inserted by the running batch). Maintained by run_cfk_update when `on`: the updates
+// with deps statuses then need their deps (CfkUpdIn.dep_*). After a batch every entry's list is its
+// own index (mref[e] = e).
+constexpr uint32_t MREF_NONE = 0xFFFFFFFFu;
+constexpr uint32_t MREF_BORN = 0xFFFFFFFEu;
+struct CfkMiss {
+    bool on = false;
+    uint64_t n_lists = 0;
+    uint64_t* off = nullptr;
+    uint32_t* ids = nullptr;
+    void* ctx = nullptr;
+    // spare CSR buffers for n lists / n_ids ids, and making them current (returns the current ones)
+    int (*spare)(void* ctx, uint64_t n, uint64_t n_ids, uint64_t** off, uint32_t** ids) = nullptr;
+    int (*swap)(void* ctx, uint64_t** off, uint32_t** ids) = nullptr;
 };
 
 struct CfkUpdOut {
@@ -101,6 +126,7 @@ struct CfkUpdOut {
     const int64_t* new_keys = nullptr;
     const uint64_t* key_pos = nullptr;
     bool rolled_back = false;      // the batch failed after it had been applied and was undone
+    uint64_t n_additions = 0;      // TRANSITIVELY_KNOWN entries inserted from deps (Updating.java:235-263)
     double ms_locate = 0, ms_derive = 0, ms_total = 0;
 };
 
@@ -113,9 +139,11 @@ void cfk_upd_work_invalidate(CfkUpdWork* w);
 // Applies the batch (AD_E_* on failure with the store unchanged; message in *err).
 // `need` is called with the sizes the derived arrays need; it must return buffers at least that
 // large (possibly reallocated) in *bufs.
+// With miss (non-null, on): the TxnInfo.missing() lists and the deps-derived additions follow
+// (Updating.insertOrUpdate, Updating.java:99-470): see run_cfk_update.
 int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn& u, CfkDerivedBufs* bufs,
                    int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
-                   const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err);
+                   const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err, CfkMiss* miss = nullptr);
 
 struct CfkPruneOut {
     uint64_t n_removed = 0;        // entries removed

@@ -526,6 +526,19 @@ int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t sc
  * committed entries of a key with one executeAt, :1439). Ids and keys added by a failed batch stay
  * (an unreferenced id or an empty CommandsForKey changes no answer). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
  * follow on demand. */
+/* TxnInfo.missing() and the deps-derived additions (Updating.insertOrUpdate, Updating.java:99-470):
+ * a batch carrying deps (dep_off non-NULL) keeps every entry's missing() list on the device, as the
+ * reference's sequence of updates leaves it -- an update with deps derives its TxnInfo's list
+ * (computeInfoAndAdditions :194-287: the key's entries below depsKnownBefore its kind witnesses, not
+ * COMMITTED or later, not in its deps), other entries lose ids that became COMMITTED or INVALID and
+ * gain the batch's insertions below COMMITTED under their depsKnownBefore that they witness
+ * (Utils.java:68-352) -- and inserts the deps the key's byId lacks as TRANSITIVELY_KNOWN entries
+ * (those the command's kind witnesses, at or above prunedBefore; removePrunedAdditions'
+ * LoadPruned is the host's). The lists start from the last ad_cfk_missing_load (NO_TXNIDS without
+ * one). A batch without deps hands them back to the host copy, where entries leaving
+ * ACCEPTED..APPLIED or moved mark them stale (ad_cfk_missing_load again). Deviation: a dep the kind
+ * does not witness (an ExclusiveSyncPoint) past the key's last id is not inserted (the Java adds
+ * it). The additions are a second internal batch: when only it fails, the explicit updates stand. */
 typedef struct ad_cfk_update_soa {
     uint64_t n;
     const int64_t*  keys;
@@ -539,14 +552,27 @@ typedef struct ad_cfk_update_soa {
     const uint64_t* ballot_msb;      /* command.acceptedOrCommitted(); all three NULL = Ballot.ZERO */
     const uint64_t* ballot_lsb;
     const int32_t*  ballot_node;
+    /* command.partialDeps().txnIds(key) past redundantBefore.shardRedundantBefore() (the cursor of
+     * Updating.computeInfoAndAdditions :184-185), ascending: deps of update i are
+     * [dep_off[i], dep_off[i+1]); read for updates with ACCEPTED..APPLIED. NULL: no deps (see below). */
+    const uint64_t* dep_off;         /* [n + 1] */
+    const uint64_t* dep_msb;
+    const uint64_t* dep_lsb;
+    const int32_t*  dep_node;
 } ad_cfk_update_soa;
 
 /* Host buffers (staged to the device). n_applied (may be null): updates that changed an entry;
  * stats (may be null): ms_stage[0] dictionary append + locate + apply + insertion, ms_stage[1]
- * re-derivation, ms_device total, n_keys[0] entries inserted, n_keys[1] ids added to the dictionary. */
+ * re-derivation, ms_device total, n_keys[0] entries inserted, n_keys[1] ids added to the dictionary,
+ * n_keys[2] TRANSITIVELY_KNOWN entries inserted from deps. */
 int ad_cfk_update(ad_ctx* ctx, const ad_cfk_update_soa* u, uint64_t* n_applied, ad_stats* stats);
 /* Device buffers, on `stream` (null: the context's stream). Synchronous on return. */
 int ad_cfk_update_device(ad_ctx* ctx, const ad_cfk_update_soa* u_dev, void* stream, uint64_t* n_applied, ad_stats* stats);
+/* TxnInfo.missing() of every entry as it stands (load order): ids [off[e], off[e+1]) ascending.
+ * AD_E_STATE when the lists are stale (updates without deps moved entries after a load). Views
+ * owned by the context, valid until its next call. */
+int ad_cfk_missing(ad_ctx* ctx, uint64_t* n_entries, const uint64_t** off, const uint64_t** msb, const uint64_t** lsb,
+                   const int32_t** node);
 /* The store's entries as they stand (load order): status and executeAt per entry. Views owned by
  * the context, valid until its next call. */
 int ad_cfk_entries(ad_ctx* ctx, uint64_t* n_entries, const uint8_t** status, const uint64_t** exec_msb,

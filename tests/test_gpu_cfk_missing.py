@@ -1,0 +1,177 @@
+"""GPU parity of TxnInfo.missing() maintenance and the deps-derived additions on the device
+(include/accord_deps.h ad_cfk_update_soa dep_*): batches of CommandsForKey.update
+carrying each command's deps on the key, applied by ad_cfk_update, against the oracle's per-update
+restatement of Updating.insertOrUpdate (oracle/cfk_update.py cfk_update_missing): the CommandsForKeys
+left (keys, segments, TxnIds, statuses, executeAts -- additions included), every entry's missing()
+list (ad_cfk_missing), and the four BeginRecovery scans (which read missing()) bit-exact vs the
+oracle's mapReduceFull over the oracle's CommandsForKeys, over successive batches."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from accord_deps import _abi as A, native, synth
+from accord_deps.model import CfkUpdates, Tids, make_txn_ids
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import cfk_update as U  # noqa: E402
+import cfk_update_gen as G  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _norm(m, l, n):
+    return U.norm(m, l, n)
+
+
+def with_deps(cfk, u, rng, keep=0.7, n_new=2, dep_kinds=(0, 1)):
+    """Deps per update with a deps status: a `keep` share of the key's ids below the txn's
+    depsKnownBefore plus `n_new` ids the store does not hold (some below, some past its ids)."""
+    seg = cfk.seg.astype(np.int64)
+    by_key = {int(cfk.keys[k]): (int(seg[k]), int(seg[k + 1])) for k in range(len(cfk.keys))}
+    offs, dm, dl, dn = [0], [], [], []
+    for i in range(len(u)):
+        ids = []
+        if int(u.status[i]) in (3, 4, 5, 6):
+            lo, hi = by_key.get(int(u.keys[i]), (0, 0))
+            for e in range(lo, hi):
+                if (int(cfk.txn.lsb[e]) & 1) == 0 and rng.random() < keep:
+                    ids.append((int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e])))
+            hlc = int(u.txn.lsb[i]) >> 16
+            nw = make_txn_ids(int(u.txn.msb[i]) >> 15, rng.integers(max(1, hlc - 50), hlc + 50, n_new),
+                              rng.choice(np.array(dep_kinds, np.uint64), n_new), rng.integers(20, 30, n_new))
+            for j in range(n_new):
+                ids.append((int(nw.msb[j]), int(nw.lsb[j]), int(nw.node[j])))
+            t = (int(u.txn.msb[i]), int(u.txn.lsb[i]), int(u.txn.node[i]))
+            # a command's deps hold only kinds it witnesses (Updating.java:243-247 asserts it of the rest)
+            ids = sorted(set(x for x in ids if _norm(*x) != _norm(*t) and U._witnesses(t, x)), key=lambda x: _norm(*x))
+            # one id per Timestamp.equals class
+            uniq, seen = [], set()
+            for x in ids:
+                if _norm(*x) not in seen:
+                    seen.add(_norm(*x))
+                    uniq.append(x)
+            ids = uniq
+        for x in ids:
+            dm.append(x[0]), dl.append(x[1]), dn.append(x[2])
+        offs.append(len(dm))
+    return CfkUpdates(u.keys, u.txn, u.exec, u.status, u.ballot, np.array(offs, np.uint64),
+                      Tids(np.array(dm, np.uint64), np.array(dl, np.uint64), np.array(dn, np.int32)))
+
+
+def consistent_missing(cfk, rng, frac=0.5):
+    """missing() lists that satisfy CommandsForKey's invariant (Utils.validateMissing,
+    Utils.java:42-62): for an entry with deps, a subset of the key's entries below its
+    depsKnownBefore, below COMMITTED, that its kind witnesses (the ones its deps would lack)."""
+    seg = cfk.seg.astype(np.int64)
+    offs, mm, ml, mn = [0], [], [], []
+    for k in range(len(cfk.keys)):
+        lo, hi = int(seg[k]), int(seg[k + 1])
+        for e in range(lo, hi):
+            st = int(cfk.status[e])
+            if st in (3, 4, 5, 6) and rng.random() < frac:
+                t = (int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e]))
+                x = (int(cfk.exec.msb[e]), int(cfk.exec.lsb[e]), int(cfk.exec.node[e]))
+                dkb = _norm(*t) if st == 3 else _norm(*x)
+                for p in range(lo, hi):
+                    q = (int(cfk.txn.msb[p]), int(cfk.txn.lsb[p]), int(cfk.txn.node[p]))
+                    if p != e and int(cfk.status[p]) < 4 and _norm(*q) < dkb and U._witnesses(t, q) and rng.random() < 0.5:
+                        mm.append(q[0]), ml.append(q[1]), mn.append(q[2])
+            offs.append(len(mm))
+    cfk.miss_off = np.array(offs, np.uint64)
+    cfk.miss = Tids(np.array(mm, np.uint64), np.array(ml, np.uint64), np.array(mn, np.int32))
+    return cfk
+
+
+def _workload(seed, **kw):
+    w = synth.recovery_workload(seed, **kw)
+    consistent_missing(w.cfk, np.random.default_rng(seed ^ 0xBEEF))
+    return w
+
+
+def _check(w, st, oracle, exp):
+    keys, seg, txn, pruned = st.cfk_byid()
+    assert keys.tolist() == exp.keys.tolist() and seg.tolist() == exp.seg.tolist()
+    assert [_norm(*x) for x in zip(txn.msb, txn.lsb, txn.node)] == [_norm(*x) for x in zip(exp.txn.msb, exp.txn.lsb, exp.txn.node)]
+    s, x = st.cfk_entries()
+    assert s.tolist() == exp.status.tolist()
+    assert x.lsb.tolist() == exp.exec.lsb.tolist() and x.msb.tolist() == exp.exec.msb.tolist()
+    off, ms = st.cfk_missing()
+    assert off.tolist() == exp.miss_off.tolist(), "missing() list sizes differ"
+    assert [_norm(*m) for m in zip(ms.msb, ms.lsb, ms.node)] == [_norm(*m) for m in zip(exp.miss.msb, exp.miss.lsb, exp.miss.node)]
+    old = w.cfk
+    w.cfk = exp
+    try:
+        for scan in A.RECOVER_SCANS:
+            got = st.recovery_scan(w.queries, scan)
+            want = oracle.recover(w, scan)
+            ok, why = got.equals(want, detail=True)
+            assert ok, "scan %d: %s" % (scan, why)
+    finally:
+        w.cfk = old
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_missing_and_additions(oracle, seed):
+    w = _workload(60 + seed, n_hist_txns=200)
+    rng = np.random.default_rng(seed)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        for rnd in range(3):
+            parts = [G.transitions(cfk, rng, 40)[0], G.fresh_preaccepts(cfk, rng, 10, statuses=(2, 3), epoch=9 + rnd,
+                                                                         hlc0=1 + 1000 * rnd)]
+            if rnd == 1:
+                parts.append(G.older_inserts(cfk, rng, 10))
+            u = with_deps(cfk, G.concat(*parts), rng)
+            exp, applied, nadd = U.cfk_update_missing(cfk, u, u.dep_off, u.deps)
+            if U.dup_committed_exec(exp):
+                continue                      # AD_E_DUP_EXEC on both sides: not this test's subject
+            n_applied, stats = st.cfk_update(u)
+            assert n_applied == applied + nadd and stats["n_keys"][2] == nadd
+            _check(w, st, oracle, exp)
+            cfk = exp
+    finally:
+        st.close()
+
+
+def test_accept_commit_apply_chain(oracle):
+    # one wave of PreAccepts, then Accept -> Commit -> Apply with deps (the common life cycle)
+    w = _workload(77, n_hist_txns=150)
+    rng = np.random.default_rng(77)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        base = G.fresh_preaccepts(cfk, rng, 12, statuses=(2,), kinds=(0, 1))
+        for target in (2, 3, 4, 6):
+            u = CfkUpdates(base.keys, base.txn, base.txn, np.full(len(base), target, np.uint8))
+            u = with_deps(cfk, u, rng, keep=0.8, n_new=1)
+            exp, applied, nadd = U.cfk_update_missing(cfk, u, u.dep_off, u.deps)
+            st.cfk_update(u)
+            _check(w, st, oracle, exp)
+            cfk = exp
+    finally:
+        st.close()
+
+
+def test_batch_without_deps_hands_lists_back(oracle):
+    w = _workload(80, n_hist_txns=150)
+    rng = np.random.default_rng(80)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        u = with_deps(w.cfk, G.transitions(w.cfk, rng, 30, statuses=(3, 4, 5, 6))[0], rng)
+        exp, _, _ = U.cfk_update_missing(w.cfk, u, u.dep_off, u.deps)
+        st.cfk_update(u)
+        _check(w, st, oracle, exp)
+        # a status-only batch (no deps) on entries that keep their deps status leaves the lists valid
+        keep = np.nonzero(np.isin(exp.status, (5, 6)))[0][:5]
+        u2 = CfkUpdates(G.entry_keys(exp)[keep], exp.txn.take(keep), exp.exec.take(keep), np.full(len(keep), 6, np.uint8))
+        st.cfk_update(u2)
+        off, _ = st.cfk_missing()
+        assert len(off) == exp.n_entries + 1
+    finally:
+        st.close()
