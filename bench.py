@@ -660,6 +660,25 @@ def bench_cfk_update(args, rank, world, local, dev):
         st = np.maximum(status[e] + 1, A.ST_ACCEPTED).astype(np.uint8)
         status[e] = st
         u = CfkUpdates(key_of[e], cfk.txn.take(e), cfk.exec.take(e), st)
+        if args.cfk_deps:
+            # each transition (a deps status) carries deps: the up-to-D entries before it in its key's
+            # byId that its kind witnesses (key-domain ids) -> the device maintains every missing()
+            # list and inserts absent deps (Updating.insertOrUpdate)
+            D = args.cfk_deps
+            lo_of = np.repeat(cfk.seg[:-1].astype(np.int64), np.diff(cfk.seg.astype(np.int64)))[e]
+            cand = e[:, None] - np.arange(1, D + 1)[None, :]
+            ok = cand >= lo_of[:, None]
+            cc = np.where(ok, cand, 0)
+            wk = np.array([0b10, 0b11, 0b10, 0b11, 0b11011, 0, 0, 0], np.uint64)[cfk.txn.kind()[e].astype(np.int64)]
+            ok &= ((wk[:, None] >> cfk.txn.kind()[cc].astype(np.uint64)) & np.uint64(1)) == 1
+            ok &= (cfk.txn.lsb[cc] & np.uint64(1)) == 0
+            ok = ok[:, ::-1]                          # ascending ids: earliest first
+            cc = cc[:, ::-1]
+            cnt = ok.sum(axis=1)
+            off = np.zeros(len(e) + 1, np.uint64)
+            off[1:] = np.cumsum(cnt)
+            sel = cc[ok]
+            u = CfkUpdates(u.keys, u.txn, u.exec, u.status, None, off, cfk.txn.take(sel))
         if n_ins:
             # PreAccepts of txnIds newer than the store (epoch above the history's), inserted as
             # PREACCEPTED into 8 existing keys each (CommandsForKey.update's insert branch)
@@ -668,8 +687,12 @@ def bench_cfk_update(args, rank, world, local, dev):
             rows = np.repeat(np.arange(m), 8)
             ks = cfk.keys[rng.integers(0, len(cfk.keys), n_ins)]
             ti = t.take(rows)
+            dep_off, deps = u.dep_off, u.deps
             u = CfkUpdates(np.concatenate([u.keys, ks]), Tids.concat([u.txn, ti]), Tids.concat([u.exec, ti]),
                            np.concatenate([u.status, np.full(n_ins, A.ST_PREACCEPTED, np.uint8)]))
+            if dep_off is not None:       # PreAccepts carry no deps (PREACCEPTED has none)
+                u.dep_off = np.concatenate([dep_off, np.full(n_ins, dep_off[-1], np.uint64)])
+                u.deps = deps
         batches.append((u,) + native.device_updates(u, dev))
     store = native.DeviceCommandStore(device=local)
     t0 = time.time()
@@ -905,6 +928,8 @@ def main():
     ap.add_argument("--steady-transitions", type=int, default=-1, metavar="T", help="default 8R")
     ap.add_argument("--resident", action="store_true",
                     help="--config 1: keep the store resident, each step a fresh SEQUENTIAL batch (device-side insertion)")
+    ap.add_argument("--cfk-deps", type=int, default=0, metavar="D",
+                    help="--cfk-update: transitions carry D deps each (device missing() maintenance + additions)")
     ap.add_argument("--cfk-insert-frac", type=float, default=0.5,
                     help="--cfk-update: share of each batch that inserts new txnIds (fresh PreAccepts)")
     ap.add_argument("--accept-frac", type=float, default=0.0,

@@ -604,7 +604,11 @@ def device_updates(u, dev):
     s.n = len(u)
     (s.keys, s.txn_msb, s.txn_lsb, s.txn_node, s.exec_msb, s.exec_lsb, s.exec_node, s.status) = [x.data_ptr() for x in t[:8]]
     if u.ballot is not None:
-        s.ballot_msb, s.ballot_lsb, s.ballot_node = [x.data_ptr() for x in t[8:]]
+        s.ballot_msb, s.ballot_lsb, s.ballot_node = [x.data_ptr() for x in t[8:11]]
+    if u.dep_off is not None:
+        dt = [to_dev(a) for a in (u.dep_off, u.deps.msb, u.deps.lsb, u.deps.node)]
+        t += dt
+        s.dep_off, s.dep_msb, s.dep_lsb, s.dep_node = [x.data_ptr() for x in dt]
     return s, t
 
 

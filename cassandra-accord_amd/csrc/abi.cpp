@@ -3524,9 +3524,13 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
         if (int rc = build_snapshot(c)) return rc;
     if (int rc = sync_host(c)) return rc;
     auto& K = c->cfk;
-    if (!K.miss.empty() || c->dmiss_on)
-        return c->fail(AD_E_STATE, "ad_cfk_prune: TxnInfo.missing() lists are loaded; pruneBefore's missing-subset test "
-                                   "(Pruning.java:239-251) is not on the device");
+    // loaded missing() lists go to the device, where pruneBefore's subset test (Pruning.java:239-251) reads them
+    if (!c->dmiss_on && !K.miss.empty())
+    {
+        const int rc = dmiss_enable(c, c->stream);
+        if (rc < 0) return rc;
+        if (rc) return c->fail(AD_E_STATE, "ad_cfk_prune: the missing() lists are stale (load them again)");
+    }
     const uint64_t nk = c->ds.n_keys;
     // key ordinals -> key indices of the store (keys without a CommandsForKey are skipped)
     std::vector<uint32_t> kl;
@@ -3562,8 +3566,16 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
                        c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
     CfkPruneOut o;
     std::string e;
+    CfkMiss miss;
+    miss.on = c->dmiss_on;
+    miss.n_lists = c->dmiss_lists;
+    miss.off = c->d_moff.as<uint64_t>();
+    miss.ids = c->d_mids.as<uint32_t>();
+    miss.ctx = c;
+    miss.spare = cfk_miss_spare;
+    miss.swap = cfk_miss_swap;
     const int rc = run_cfk_prune(c->cu, c->ds, d, keys ? c->d_prune_keys.as<uint32_t>() : nullptr, keys ? kl.size() : nk,
-                                 prune_interval, min_hlc_delta, &b, cfk_need_bufs, c, grow, c->stream, &o, &e);
+                                 prune_interval, min_hlc_delta, &b, cfk_need_bufs, c, grow, c->stream, &o, &e, &miss);
     if (rc)
     {
         // the derived arrays may be half built: rebuild everything from the entries at the next use

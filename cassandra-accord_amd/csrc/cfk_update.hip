@@ -2110,7 +2110,8 @@ __global__ void k_prune_key(uint64_t nl, const uint32_t* klist, DevSnapshot s, C
     p_tr[k] = tr;
 }
 
-// thread per entry: removed by pruneBefore (:222-254, missing() == NO_TXNIDS)
+// thread per entry: removed by pruneBefore (:222-254). With missing() lists on the device (d.mref)
+// the APPLIED entries are k_prune_subset's to decide; INVALID ones always go.
 __global__ void k_prune_mark(uint64_t ne, CfkDevState d, const uint32_t* p_pos, const uint32_t* p_xr, uint32_t* rm)
 {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2121,9 +2122,60 @@ __global__ void k_prune_mark(uint64_t ne, CfkDevState d, const uint32_t* p_pos, 
     if (pos && e - d.krec[k].seg_lo < pos)
     {
         const uint32_t st = d.status[e];
-        r = st == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED || (st == AD_ST_APPLIED && d.xrank[e] < p_xr[k]);
+        r = st == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED || (!d.mref && st == AD_ST_APPLIED && d.xrank[e] < p_xr[k]);
     }
     rm[e] = r ? 1u : 0u;
+}
+
+// thread per pruned key, with missing() lists (:222-251): walking byId below the new prunedBefore,
+// an APPLIED entry executing before it goes when its missing() is empty or inside the merged set --
+// the new prunedBefore's list united with the lists of the APPLIED entries kept before it that
+// execute at their txnId (the set is not built: the kept entries' indices go to `sc`, each id is
+// searched in their lists).
+__device__ inline bool list_has(const uint64_t* off, const uint32_t* ids, uint32_t L, uint32_t r)
+{
+    if (L == MREF_NONE || L == MREF_BORN) return false;
+    uint64_t lo = off[L], hi = off[L + 1];
+    while (lo < hi)
+    {
+        const uint64_t m = (lo + hi) >> 1;
+        if (ids[m] < r) lo = m + 1;
+        else hi = m;
+    }
+    return lo < off[L + 1] && ids[lo] == r;
+}
+
+__global__ void k_prune_subset(uint64_t nl, const uint32_t* klist, CfkDevState d, const uint32_t* p_pos, const uint32_t* p_xr,
+                               const uint64_t* moff, const uint32_t* mids, uint32_t* sc, uint32_t* rm)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nl) return;
+    const uint32_t k = klist ? klist[t] : (uint32_t)t;
+    const uint32_t pos = p_pos[k];
+    if (!pos) return;
+    const uint32_t lo = d.krec[k].seg_lo, npb = lo + pos, x_npb = p_xr[k];
+    const uint32_t L0 = d.mref[npb];
+    uint32_t nret = 0;
+    for (uint32_t e = lo; e < npb; ++e)
+    {
+        if (d.status[e] != AD_ST_APPLIED || d.xrank[e] >= x_npb) continue;
+        const uint32_t L = d.mref[e];
+        bool subset = true;
+        if (L != MREF_NONE && L != MREF_BORN)
+            for (uint64_t j = moff[L]; j < moff[L + 1] && subset; ++j)
+            {
+                const uint32_t r = mids[j];
+                bool in = list_has(moff, mids, L0, r);
+                for (uint32_t q = 0; q < nret && !in; ++q) in = list_has(moff, mids, d.mref[sc[lo + q]], r);
+                subset = in;
+            }
+        if (subset)
+        {
+            rm[e] = 1u;
+            continue;
+        }
+        if (d.xrank[e] == (d.ent[e].y & RANK_MASK)) sc[lo + nret++] = e;
+    }
 }
 
 // thread per key: segments after the removals; prunedBefore where entries went (:255-257: a key
@@ -2164,7 +2216,7 @@ __global__ __launch_bounds__(256) void k_prune_move(uint64_t ne, EntArrays a, co
 int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t* klist, uint64_t nl, int32_t prune_interval,
                   int64_t min_hlc_delta, CfkDerivedBufs* bufs,
                   int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
-                  const CfkGrow& grow, hipStream_t st, CfkPruneOut* out, std::string* err)
+                  const CfkGrow& grow, hipStream_t st, CfkPruneOut* out, std::string* err, CfkMiss* miss)
 {
     *out = CfkPruneOut{};
     const uint64_t ne = s.n_ent, nk = s.n_keys;
@@ -2201,6 +2253,13 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
     k_prune_key<<<blocks(nl), 256, 0, st>>>(nl, klist, s, d, w->cm.as<uint32_t>(), w->fs.as<uint64_t>(), prune_interval,
                                             min_hlc_delta, p_pos, p_xr, p_tr);
     k_prune_mark<<<blocks(ne), 256, 0, st>>>(ne, d, p_pos, p_xr, w->uflag.as<uint32_t>());
+    const bool lists = d.mref && miss && miss->on;
+    if (lists)
+    {
+        UALLOC(w->dsrc, 4 * ne, false);       // the subset walk's kept entries (per key, in its segment)
+        k_prune_subset<<<blocks(nl), 256, 0, st>>>(nl, klist, d, p_pos, p_xr, miss->off, miss->ids, w->dsrc.as<uint32_t>(),
+                                                   w->uflag.as<uint32_t>());
+    }
     UCHK(hipGetLastError());
     UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), ne, 1, ctl->tot2);
@@ -2238,6 +2297,41 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
     out->n_removed = R;
     UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
     if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rc;
+    if (lists)
+    {
+        // the kept entries' lists, compacted again (each entry its own list, pruned ones dropped)
+        const uint64_t n2 = s.n_ent;
+        UALLOC(w->dsrc, 4 * n2, false);
+        UALLOC(w->mflag, 4 * 2 * n2, false);
+        UALLOC(w->mpp, 8 * 2 * (n2 + 1), false);
+        UALLOC(w->mpend, 4 * 2 * n2, false);
+        UALLOC(w->mcnt, 4 * n2, false);
+        UALLOC(w->moff, 8 * (n2 + 1), false);
+        UALLOC(w->bsum, 8 * 2 * ((n2 + 1023) / 1024 + 8), false);
+        UCHK(hipMemsetAsync(w->dsrc.p, 0xFF, 4 * n2, st));
+        k_miss_flags<<<blocks(n2), 256, 0, st>>>(n2, d, w->mflag.as<uint32_t>());
+        UCHK(run_scan_arrays(w->mflag.as<uint32_t>(), w->mpp.as<uint64_t>(), n2, 2, w->bsum.as<uint64_t>(), st));
+        k_miss_scatter<<<blocks(n2), 256, 0, st>>>(n2, w->mflag.as<uint32_t>(), w->mpp.as<uint64_t>(), w->mpend.as<uint32_t>());
+        const CfkUpdIn none{};
+        k_miss_build<0><<<blocks(n2), 256, 0, st>>>(s, d, none, w->dsrc.as<uint32_t>(), nullptr, w->mpp.as<uint64_t>(),
+                                                    w->mpend.as<uint32_t>(), miss->off, miss->ids, w->mcnt.as<uint32_t>(),
+                                                    nullptr, nullptr);
+        UCHK(run_scan_arrays(w->mcnt.as<uint32_t>(), w->moff.as<uint64_t>(), n2, 1, w->bsum.as<uint64_t>(), st));
+        uint64_t nm = 0;
+        UCHK(hipMemcpyAsync(&nm, w->moff.as<uint64_t>() + n2, 8, hipMemcpyDeviceToHost, st));
+        UCHK(hipStreamSynchronize(st));
+        uint64_t* noff = nullptr;
+        uint32_t* nids = nullptr;
+        if (int rc = miss->spare(miss->ctx, n2, nm, &noff, &nids)) { *err = "missing() lists"; return rc; }
+        UCHK(hipMemcpyAsync(noff, w->moff.p, 8 * (n2 + 1), hipMemcpyDeviceToDevice, st));
+        k_miss_build<1><<<blocks(n2), 256, 0, st>>>(s, d, none, w->dsrc.as<uint32_t>(), nullptr, w->mpp.as<uint64_t>(),
+                                                    w->mpend.as<uint32_t>(), miss->off, miss->ids, nullptr, noff, nids);
+        k_mref_identity<<<blocks(n2), 256, 0, st>>>(n2, d.mref);
+        UCHK(hipGetLastError());
+        UCHK(hipStreamSynchronize(st));
+        if (int rc = miss->swap(miss->ctx, &miss->off, &miss->ids)) { *err = "missing() lists"; return rc; }
+        miss->n_lists = n2;
+    }
     UCHK(hipEventRecord(w->ev[1], st));
     UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));

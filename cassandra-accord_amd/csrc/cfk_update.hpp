@@ -152,12 +152,13 @@ struct CfkPruneOut {
 };
 
 // Pruning.maybePrune (Pruning.java:164-199 -> pruneBefore :205-331) for the keys klist[0..nl) (key
-// indices, device; null: every key, nl = n_keys), with TxnInfo.missing() = NO_TXNIDS for every entry.
+// indices, device; null: every key, nl = n_keys); TxnInfo.missing() from miss when it is on (the
+// subset test of :239-251), else NO_TXNIDS for every entry.
 // Removed entries leave the per-entry arrays (compacted into the spare buffers), the segments and
 // prunedBefore follow, and the derived arrays are rebuilt. Ids stay in the dictionary.
 int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t* klist, uint64_t nl, int32_t prune_interval,
                   int64_t min_hlc_delta, CfkDerivedBufs* bufs,
                   int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
-                  const CfkGrow& grow, hipStream_t st, CfkPruneOut* out, std::string* err);
+                  const CfkGrow& grow, hipStream_t st, CfkPruneOut* out, std::string* err, CfkMiss* miss = nullptr);
 
 }  // namespace adx

@@ -177,10 +177,11 @@ def hlc(msb, lsb):
 def cfk_prune(cfk, keys=None, prune_interval=1, min_hlc_delta=0):
     """Returns (new CfkSnapshot, entries removed, keys pruned): CommandsForKey.maybePrune
     (Pruning.java:164-199) for the CommandsForKey of every key in `keys` (None: all), then
-    pruneBefore (:205-331) where it applies. Every TxnInfo.missing() is NO_TXNIDS (the device model:
-    the lists are not loaded), so an APPLIED entry executing before the new prunedBefore is removed
-    (:239-245 with missing == NO_TXNIDS), as is every INVALID_OR_TRUNCATED entry before it (:253-254).
-    prunedBefore is an index into the key's byId here (-1: none)."""
+    pruneBefore (:205-331) where it applies: below the new prunedBefore every INVALID_OR_TRUNCATED
+    entry goes (:253-254), and every APPLIED entry executing before it whose missing() is empty or a
+    subset of the merged missing() -- the new prunedBefore's, united with those of the retained
+    APPLIED entries before it that execute at their txnId (:239-251). cfk.miss_off None: every
+    missing() is NO_TXNIDS. prunedBefore is an index into the key's byId here (-1: none)."""
     seg = cfk.seg.astype(np.int64)
     nk = len(cfk.keys)
     want = set(int(k) for k in keys) if keys is not None else None
@@ -228,11 +229,25 @@ def cfk_prune(cfk, keys=None, prune_interval=1, min_hlc_delta=0):
         if pos == 0:
             continue
         # pruneBefore :205-260: entries before pos that are INVALID, or APPLIED executing before npb
+        # whose missing() is empty or inside the merged missing() of npb and the retained APPLIED
+        # entries before them that execute at their txnId (SortedArrays.isSubset / linearUnion)
+        def miss_of(e):
+            if cfk.miss_off is None:
+                return []
+            return [norm(int(cfk.miss.msb[j]), int(cfk.miss.lsb[j]), int(cfk.miss.node[j]))
+                    for j in range(int(cfk.miss_off[e]), int(cfk.miss_off[e + 1]))]
+        merged = set(miss_of(npb))
         removed = []
         for e in range(lo, lo + pos):
             st = int(cfk.status[e])
-            if st == INVALID or (st == APPLIED and xnorm(e) < xnorm(npb)):
+            if st == INVALID:
                 removed.append(e)
+            elif st == APPLIED and xnorm(e) < xnorm(npb):
+                ms = miss_of(e)
+                if not ms or set(ms) <= merged:
+                    removed.append(e)
+                elif xnorm(e) == tnorm(e):
+                    merged |= set(ms)
         if not removed:
             continue                                # pos == retainCount: the CommandsForKey as it was
         keep[removed] = False
@@ -243,8 +258,16 @@ def cfk_prune(cfk, keys=None, prune_interval=1, min_hlc_delta=0):
     new_seg[1:] = np.cumsum([int(keep[int(seg[k]):int(seg[k + 1])].sum()) for k in range(nk)])
     # prunedBefore indices of keys not pruned here shift by the removals before them (none: a key's
     # removals are all below its new prunedBefore, and other keys' removals are in other segments)
+    moff, mtake = None, None
+    if cfk.miss_off is not None:
+        mo = cfk.miss_off.astype(np.int64)
+        cnt = (mo[1:] - mo[:-1])[idx]
+        moff = np.zeros(len(idx) + 1, np.uint64)
+        moff[1:] = np.cumsum(cnt)
+        mtake = np.concatenate([np.arange(mo[e], mo[e + 1]) for e in idx]) if len(idx) else np.zeros(0, np.int64)
     out = CfkSnapshot(cfk.keys.copy(), new_seg, cfk.txn.take(idx), cfk.exec.take(idx), cfk.status[idx].copy(),
-                      pruned if (cfk.pruned_before is not None or n_keys_pruned) else None)
+                      pruned if (cfk.pruned_before is not None or n_keys_pruned) else None,
+                      moff, None if moff is None else cfk.miss.take(mtake.astype(np.int64)))
     if getattr(cfk, "ballot", None) is not None:
         out.ballot = cfk.ballot.take(idx)
     return out, int((~keep).sum()), n_keys_pruned

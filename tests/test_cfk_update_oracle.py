@@ -268,3 +268,17 @@ def test_missing_only_for_statuses_with_deps_and_matches_plain_update():
     for e in range(b.n_entries):
         if b.status[e] not in (3, 4, 5, 6):
             assert b.miss_off[e + 1] == b.miss_off[e]
+
+
+def test_prune_missing_subset_of_merged():
+    # R5 pending; W10 and W20 APPLIED each missing R5; W30 (the new prunedBefore) missing nothing.
+    # W10's list is not inside {} -> kept, and (executing at its txnId) merged; W20's {R5} is then
+    # inside the merged set -> removed (Pruning.java:239-251)
+    c = _prune_store([(5, R, PA, 5), (10, W, AP, 10), (20, W, AP, 20), (30, W, AP, 30), (40, W, AP, 40)])
+    r5 = _ids([5], [R])
+    c.miss_off = np.array([0, 0, 1, 2, 2, 2], np.uint64)
+    c.miss = Tids.concat([r5, r5])
+    n, removed, keys = U.cfk_prune(c, None, 1, 0)
+    assert (removed, keys) == (1, 1)
+    assert _hlcs(n) == [5, 10, 30, 40] and n.pruned_before.tolist() == [2]
+    assert n.miss_off.tolist() == [0, 0, 1, 1, 1]

@@ -113,15 +113,26 @@ def test_config2_scaled_apply_then_prune(oracle):
         st.close()
 
 
-def test_prune_refuses_loaded_missing_lists():
-    w = synth.recovery_workload(4)
+@pytest.mark.parametrize("seed", range(3))
+def test_prune_with_missing_lists(oracle, seed):
+    # missing() lists on the device (loaded, then maintained by batches with deps): pruneBefore's
+    # subset test against the merged lists (Pruning.java:239-251); lists and recovery scans after
+    from test_gpu_cfk_missing import _check as check_missing, _workload, with_deps
+    w = _workload(90 + seed, n_hist_txns=200)
+    rng = np.random.default_rng(seed)
     st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
     try:
         st.load(w)
-        if w.cfk.miss is None or len(w.cfk.miss.msb) == 0:
-            pytest.skip("workload without missing() lists")
-        with pytest.raises(native.AccordDepsError) as ei:
-            st.cfk_prune(None, 1, 0)
-        assert ei.value.code == A.AD_E_STATE
+        cfk = w.cfk
+        u = with_deps(cfk, _applied_wave(cfk, rng, 0.8), rng, keep=0.9, n_new=0)
+        cfk, _, _ = U.cfk_update_missing(cfk, u, u.dep_off, u.deps)
+        st.cfk_update(u)
+        exp, removed, nkp = U.cfk_prune(cfk, None, 1, 0)
+        got_removed, stats = st.cfk_prune(None, 1, 0)
+        assert got_removed == removed and stats["n_keys"][1] == nkp
+        check_missing(w, st, oracle, exp)
+        keys, seg, txn, pruned = st.cfk_byid()
+        assert pruned.tolist() == (exp.pruned_before.tolist() if exp.pruned_before is not None else [-1] * len(keys))
+        assert st.check_snapshot() == (0, None)
     finally:
         st.close()
