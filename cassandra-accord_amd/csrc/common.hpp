@@ -268,17 +268,13 @@ __device__ inline uint32_t dict_rank_sampled(const Snap& s, const NormTid& t)
         else b = m;
     }
     uint64_t lo = a ? (a - 1) * DICT_SAMP : 0, hi = a < s.n_samp ? a * DICT_SAMP : s.n_dict;
+    // the three words of a probe are loaded together (one round trip per level: the ids of a store
+    // share their high word, so a hi-first test would wait for a second load almost every level)
     while (lo < hi)
     {
         const uint64_t m = (lo + hi) >> 1;
-        const uint64_t dh = s.dict_hi[m];
-        bool less = dh < t.hi;
-        if (dh == t.hi)
-        {
-            const NormTid d{dh, s.dict_lo[m], s.dict_node[m]};
-            less = norm_cmp(d, t) < 0;
-        }
-        if (less) lo = m + 1;
+        const NormTid d{s.dict_hi[m], s.dict_lo[m], s.dict_node[m]};
+        if (norm_cmp(d, t) < 0) lo = m + 1;
         else hi = m;
     }
     bool eq = false;

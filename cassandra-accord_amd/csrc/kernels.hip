@@ -126,23 +126,28 @@ hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st)
 // K0: encode requests
 // ---------------------------------------------------------------------------------------
 // rank of an arbitrary id against the dictionary: member i -> 2i+1, else 2*lower_bound
+// (the sampled search: the cache-resident sample, then one DICT_SAMP-id window of the dictionary)
 __device__ __forceinline__ uint32_t encode_rank(const DevSnapshot& s, uint64_t msb, uint64_t lsb, int32_t node)
 {
-    const NormTid x = norm_tid(msb, lsb, node);
-    uint64_t lo = 0, hi = s.n_dict;
-    while (lo < hi)
+    if (!s.ds_hi || !s.n_samp)
     {
-        const uint64_t mid = (lo + hi) >> 1;
-        const NormTid m = {s.dict_hi[mid], s.dict_lo[mid], s.dict_node[mid]};
-        if (norm_cmp(m, x) < 0) lo = mid + 1;
-        else hi = mid;
+        const NormTid x = norm_tid(msb, lsb, node);
+        uint64_t lo = 0, hi = s.n_dict;
+        while (lo < hi)
+        {
+            const uint64_t mid = (lo + hi) >> 1;
+            const NormTid m = {s.dict_hi[mid], s.dict_lo[mid], s.dict_node[mid]};
+            if (norm_cmp(m, x) < 0) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < s.n_dict)
+        {
+            const NormTid m = {s.dict_hi[lo], s.dict_lo[lo], s.dict_node[lo]};
+            if (norm_cmp(m, x) == 0) return (uint32_t)(2 * lo + 1);
+        }
+        return (uint32_t)(2 * lo);
     }
-    if (lo < s.n_dict)
-    {
-        const NormTid m = {s.dict_hi[lo], s.dict_lo[lo], s.dict_node[lo]};
-        if (norm_cmp(m, x) == 0) return (uint32_t)(2 * lo + 1);
-    }
-    return (uint32_t)(2 * lo);
+    return dict_rank_sampled(s, norm_tid(msb, lsb, node));
 }
 
 __global__ void k_encode_txn(DevSnapshot s, BatchBufs b)
