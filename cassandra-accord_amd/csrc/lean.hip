@@ -63,6 +63,36 @@ __device__ __forceinline__ void seg_bitonic64(uint64_t& key)
         }
 }
 
+// ascending bitonic sort of the 2 x 32 elements of each 32-lane segment, element i = 32 s + lane
+// held in register s (x0: s = 0, x1: s = 1); a partner at distance 32 is the lane's other register
+template <class T>
+__device__ __forceinline__ void seg_bitonic_wide(T& x0, T& x1)
+{
+    const uint32_t l = lane_id() & 31u;
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1)
+        {
+            if (j == 32)
+            {
+                // i = l (lower) against i = l + 32; direction from bit k of i (k == 64: ascending)
+                const bool up = (l & k) == 0;
+                const T lo = min(x0, x1), hi = max(x0, x1);
+                x0 = up ? lo : hi;
+                x1 = up ? hi : lo;
+            }
+            else
+            {
+                const T o0 = __shfl_xor(x0, (int)j, 64), o1 = __shfl_xor(x1, (int)j, 64);
+                const bool lower = (l & j) == 0;
+                const bool up0 = (l & k) == 0, up1 = ((l + 32) & k) == 0;
+                x0 = (lower == up0) ? min(x0, o0) : max(x0, o0);
+                x1 = (lower == up1) ? min(x1, o1) : max(x1, o1);
+            }
+        }
+}
+
 struct LeanChunk {
     uint64_t cur = 0, end = 0;
     // wave-uniform bump allocation from the region arena
@@ -110,8 +140,9 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
 // e.g. a store's share of requests spanning many stores; 2: 32 lanes, up to 32; 1: 64 lanes, up to 64).
 // RNG: the store has range commands (with a stabbing index): each request also gets its
 // rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
-template <uint32_t RPW, bool RNG>
-__global__ __launch_bounds__(64 * LEAN_WAVES, LEAN_OCC) void k_resolve_lean(DevSnapshot s, BatchBufs b, uint32_t pass)
+// WIDE (RPW 2, no range commands: lean pass 2): requests with up to 64 raw emissions, two per lane.
+template <uint32_t RPW, bool RNG, bool WIDE>
+__global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolve_lean(DevSnapshot s, BatchBufs b, uint32_t pass)
 {
     // pass 1: all requests -> deferred1; pass 2: deferred1 -> deferred2 (lists derived from b
     // where used, so they hold no scalar registers across the loop)
@@ -319,7 +350,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, LEAN_OCC) void k_resolve_lean(DevS
         const uint32_t TR = RNG ? __shfl(rinc, sb | 7u, 64) : 0u;
         // the next item's displacements (its keys have arrived by now)
         loadD(qn, keyn, lookn, dn_);
-        defer = defer || seg(ballot(kact && !newest)) != 0 || T > LPR || TR > LPR;
+        constexpr bool CAN_WIDE = WIDE && RPW == 2 && !RNG;
+        defer = defer || seg(ballot(kact && !newest)) != 0 || T > (CAN_WIDE ? 2 * LPR : LPR) || TR > LPR;
         {
             const uint64_t dm = ballot(act && defer && hl == 0);
             const uint32_t nd = __popcll(dm);
@@ -331,6 +363,125 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, LEAN_OCC) void k_resolve_lean(DevS
             }
         }
         act = act && !defer;
+
+        // ---- the wide item: a request with 33..64 raw emissions -> two per lane (element x = hl and
+        // hl + 32), sorted as 64 (seg_bitonic_wide), the rest as below with masks over both halves
+        if (CAN_WIDE && seg_max(act && !defer ? T : 0u) > LPR)
+        {
+            const bool wact = act && !defer;
+            auto raw_txw = [&](uint32_t x, uint32_t& ax) -> uint32_t {
+                ax = 0;
+#pragma unroll
+                for (uint32_t p = 1; p < LEAN_MAXP; ++p)
+                {
+                    const uint32_t sp = __shfl(start, sb | p, 64);
+                    if (p < np && x >= sp) ax = p;
+                }
+                const uint32_t sx = sb | ax;
+                const uint32_t x_start = __shfl(start, sx, 64), x_n1 = __shfl(n1, sx, 64);
+                const uint32_t x_base = __shfl(Hc.h2.y, sx, 64), x_ct = __shfl(Hc.h3, sx, 64), x_lw = __shfl(Hc.h1.z, sx, 64);
+                const uint32_t x_meta = __shfl(meta, sx, 64), x_slot = __shfl(Hc.slot, sx, 64);
+                const bool lv_ = wact && x < T;
+                const uint32_t ii = x - x_start;
+                const bool fc = ii < x_n1;
+                const uint32_t* lp_;
+                if (x_meta & KL_INLINE)
+                    lp_ = s.kline[x_slot].inl + (fc ? ii : ((x_meta >> KL_INL_SHIFT) & 31u) + (ii - x_n1));
+                else
+                    lp_ = fc ? s.cand + (x_base + ii) : s.cwr + (x_ct + (ii - x_n1));
+                if (!lv_ || (!fc && cls == 0)) lp_ = s.cand;
+                const uint32_t v = *lp_;
+                return !lv_ ? 0u : ((fc || cls != 0) ? v : (x_lw | (1u << RANK_BITS)));
+            };
+            uint32_t ax0, ax1;
+            const uint32_t tw0 = raw_txw(hl, ax0), tw1 = raw_txw(hl + 32, ax1);
+            Hdr Hn;
+            loadC(qn, keyn, lookn, dn_, Hn);
+            const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
+            const bool want0 = wact && hl < T && r0 != self, want1 = wact && hl + 32 < T && r1 != self;
+            const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
+            const bool is1_1 = ((KINDS_RS_OR_WS >> (tw1 >> RANK_BITS)) & 1) == 0;
+            for (int m = 0; m < 3; m += 2)
+            {
+                const bool mine0 = want0 && (m == 0 ? !is1_0 : is1_0), mine1 = want1 && (m == 0 ? !is1_1 : is1_1);
+                const uint64_t mb0 = ballot(mine0), mb1 = ballot(mine1);
+                const uint32_t tot = __popcll(seg(mb0)) + __popcll(seg(mb1));
+                if ((mb0 | mb1) == 0)
+                {
+                    put_sizes(wact, t, m, 0, 0, 0, 0, false);
+                    continue;
+                }
+                uint32_t k0 = mine0 ? ((r0 << 3) | ax0) : 0xFFFFFFFFu, k1 = mine1 ? ((r1 << 3) | ax1) : 0xFFFFFFFFu;
+                seg_bitonic_wide(k0, k1);
+                const bool v0 = hl < tot, v1 = hl + 32 < tot;
+                const uint32_t x0 = k0 >> 3, x1 = k1 >> 3, ka0 = k0 & 7u, ka1 = k1 & 7u;
+                const uint32_t p0 = __shfl_up(k0, 1, LPR);
+                const uint32_t last0 = __shfl(k0, (int)(sb | 31u), 64);
+                const uint32_t up1 = __shfl_up(k1, 1, LPR);         // by every lane (an inactive source reads 0)
+                const uint32_t p1 = hl == 0 ? last0 : up1;
+                const bool u0 = v0 && (hl == 0 || (p0 >> 3) != x0);
+                const bool u1 = v1 && (p1 >> 3) != x1;
+                const uint64_t um0 = seg(ballot(u0)), um1 = seg(ballot(u1));
+                const uint32_t nu0 = __popcll(um0);
+                const uint32_t U = nu0 + __popcll(um1);
+                const uint32_t ur0 = __popcll(um0 & below) + (u0 ? 1u : 0u) - 1u;
+                const uint32_t ur1 = nu0 + __popcll(um1 & below) + (u1 ? 1u : 0u) - 1u;
+                // elements of the same key before each one (sorted order: half 0, then half 1)
+                uint64_t s00 = ballot(v0), s01 = ballot(v0), s10 = ballot(v1), s11 = ballot(v1);
+#pragma unroll
+                for (int bit = 0; bit < 3; ++bit)
+                {
+                    const uint64_t b0 = ballot((ka0 >> bit) & 1u), b1 = ballot((ka1 >> bit) & 1u);
+                    s00 &= ((ka0 >> bit) & 1u) ? b0 : ~b0;      // half-0 elements with key ka0
+                    s10 &= ((ka0 >> bit) & 1u) ? b1 : ~b1;      // half-1 elements with key ka0
+                    s01 &= ((ka1 >> bit) & 1u) ? b0 : ~b0;      // half-0 elements with key ka1
+                    s11 &= ((ka1 >> bit) & 1u) ? b1 : ~b1;      // half-1 elements with key ka1
+                }
+                (void)s10;
+                const uint32_t pk0 = __popcll(seg(s00) & below);
+                const uint32_t pk1 = __popcll(seg(s01)) + __popcll(seg(s11) & below);
+                // per key p: its map-m emissions in its raw range [start, start + nn) over both halves
+                const uint64_t raw_m = seg(mb0) | (seg(mb1) << 32);
+                const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
+                const uint32_t cnt = hl < 8 ? (uint32_t)__popcll(raw_m & rmask) : 0u;
+                uint32_t cinc = cnt;
+#pragma unroll
+                for (uint32_t d = 1; d < 8; d <<= 1)
+                {
+                    const uint32_t v = __shfl_up(cinc, d, 8);
+                    if ((hl & 7) >= d) cinc += v;
+                }
+                const uint32_t kstart_l = cinc - cnt;
+                const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
+                const uint32_t nk = __popcll(nem);
+                const uint32_t kk = __popcll(nem & below);
+                const uint32_t kst0 = __shfl(kstart_l, sb | ka0, 64), kst1 = __shfl(kstart_l, sb | ka1, 64);
+                const uint64_t bytes = wact && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
+                bool fits;
+                const uint64_t ro = seg_alloc(bytes, fits);
+                put_sizes(wact, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
+                if (wact && tot && fits)
+                {
+                    int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                    uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
+                    int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
+                    if (hl < 8 && cnt > 0)
+                    {
+                        okeys[kk] = keyc;
+                        ok2t[kk] = (int32_t)(nk + kstart_l + cnt);
+                    }
+                    if (u0) otx[ur0] = (x0 - 1) >> 1;
+                    if (u1) otx[ur1] = (x1 - 1) >> 1;
+                    if (v0) ok2t[nk + kst0 + pk0] = (int32_t)ur0;
+                    if (v1) ok2t[nk + kst1 + pk1] = (int32_t)ur1;
+                }
+            }
+            put_sizes(wact, t, 1, 0, 0, 0, 0, false);          // no range commands on this path
+            qc = qn;
+            keyc = keyn;
+            Hc = Hn;
+            continue;
+        }
 
         // ---- one raw emission per lane: element e = hl of key a
         uint32_t a = 0;
@@ -536,26 +687,27 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, LEAN_OCC) void k_resolve_lean(DevS
     dflush();
 }
 
-template <uint32_t RPW, bool RNG>
+template <uint32_t RPW, bool RNG, bool WIDE = false>
 static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, uint32_t pass, hipStream_t st)
 {
     static int per_cu = 0;
     if (!per_cu)
     {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG>, 64 * LEAN_WAVES, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG, WIDE>, 64 * LEAN_WAVES, 0) != hipSuccess ||
             nb <= 0)
             nb = 2;
-        per_cu = std::min(nb, 5);     // measured: more resident waves only add memory contention
+        per_cu = std::min(nb, WIDE ? 4 : 5);     // measured: more resident waves only add memory contention
         if (const char* e = getenv("AD_LEAN_PER_CU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu));
-    k_resolve_lean<RPW, RNG><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, pass);
+    k_resolve_lean<RPW, RNG, WIDE><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, pass);
     return hipGetLastError();
 }
 
-// pass 1: every request, two per wave -> D1; pass 2: D1, one per wave (up to 64 emissions) -> D2
+// pass 1: every request, two per wave -> D1; pass 2: D1, two per wave with two emissions per lane
+// (one per wave with range commands; up to 64 emissions) -> D2
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
@@ -564,7 +716,8 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
         if (rpw1 == 4) return s.n_rent ? launch_lean<4, true>(s, b, 1, st) : launch_lean<4, false>(s, b, 1, st);
         return s.n_rent ? launch_lean<2, true>(s, b, 1, st) : launch_lean<2, false>(s, b, 1, st);
     }
-    return s.n_rent ? launch_lean<1, true>(s, b, 2, st) : launch_lean<1, false>(s, b, 2, st);
+    // pass 2 (requests with 33..64 raw emissions): two per wave, two emissions per lane
+    return s.n_rent ? launch_lean<1, true>(s, b, 2, st) : launch_lean<2, false, true>(s, b, 2, st);
 }
 
 }  // namespace adx
