@@ -1221,19 +1221,41 @@ hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // ---------------------------------------------------------------------------------------
 // Pack: one wave per 64 consecutive requests. For each (map, array) the wave's output is one
 // contiguous run [off[t0], off[t0 + 64]); lane x of a 64-word chunk copies word x from the region
-// of the request whose output range holds it (request starts and source addresses staged in LDS,
-// the owning request found by advancing monotonically). Writes are fully coalesced; reads are
-// contiguous within each request's region.
+// of the request whose output range holds it. Writes are fully coalesced; reads are contiguous
+// within each request's region. The owning request of every word of a window of 64 x PACK_UNROLL
+// words comes from the run starts inside the window: each non-empty request marks its start in a
+// per-chunk 64-bit LDS mask and its lane in an owner byte at that position; word x's owner is the
+// owner byte at the highest marked position <= x, or the previous chunk's last owner (one LDS
+// read and a few bit operations per word instead of a 7-step search of the starts).
 constexpr uint32_t PACK_WAVES = 4;
 constexpr uint32_t PACK_UNROLL = 8;
 
+struct PackScratch
+{
+    uint64_t msk[PACK_UNROLL];
+    uint8_t own[64 * PACK_UNROLL];
+};
+
 template <typename T>
 __device__ __forceinline__ void pack_run(const uint8_t* __restrict__ reg, const uint32_t* st, const uint64_t* src,
-                                         uint64_t total, T* __restrict__ out)
+                                         uint64_t total, T* __restrict__ out, PackScratch* ps)
 {
     const uint32_t lane = lane_id();
+    const uint32_t s0 = st[lane], s1 = st[lane + 1];
+    const bool ne = s1 > s0;
+    const uint64_t upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;     // positions <= lane
+    uint32_t carry = 0;          // owner of the word before the chunk (word 0's run starts at 0)
     for (uint64_t xb = 0; xb < total; xb += 64 * PACK_UNROLL)
     {
+        if (lane < PACK_UNROLL) ps->msk[lane] = 0;
+        wave_lds_sync();
+        if (ne && s0 >= xb && s0 < xb + 64 * PACK_UNROLL)
+        {
+            const uint32_t q = (uint32_t)(s0 - xb);
+            atomicOr(reinterpret_cast<unsigned long long*>(&ps->msk[q >> 6]), 1ull << (q & 63));
+            ps->own[q] = (uint8_t)lane;
+        }
+        wave_lds_sync();
         const T* p[PACK_UNROLL];
         bool ok[PACK_UNROLL];
 #pragma unroll
@@ -1241,17 +1263,9 @@ __device__ __forceinline__ void pack_run(const uint8_t* __restrict__ reg, const 
         {
             const uint64_t x = xb + u * 64 + lane;
             ok[u] = x < total;
-            // owning request: the last r with st[r] <= x (binary search of the 65 starts in LDS;
-            // a linear walk costs up to 64 dependent LDS reads per element)
-            uint32_t lo = 0, hi = 64;
-#pragma unroll
-            for (int it = 0; it < 7; ++it)
-            {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (st[mid] <= (uint32_t)x) lo = mid;
-                else hi = mid - 1;
-            }
-            const uint32_t r = lo;
+            const uint64_t m = ps->msk[u] & upto;
+            const uint32_t r = m ? (uint32_t)ps->own[u * 64 + 63 - __clzll((long long)m)] : carry;
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
             p[u] = ok[u] ? reinterpret_cast<const T*>(reg + src[r]) + ((uint32_t)x - st[r]) : reinterpret_cast<const T*>(reg);
         }
         T v[PACK_UNROLL];
@@ -1260,6 +1274,7 @@ __device__ __forceinline__ void pack_run(const uint8_t* __restrict__ reg, const 
 #pragma unroll
         for (uint32_t u = 0; u < PACK_UNROLL; ++u)
             if (ok[u]) out[xb + u * 64 + lane] = v[u];
+        wave_lds_sync();
     }
 }
 
@@ -1267,6 +1282,7 @@ __global__ __launch_bounds__(64 * PACK_WAVES) void k_pack(BatchBufs b)
 {
     __shared__ uint32_t s_start[PACK_WAVES][65];
     __shared__ uint64_t s_src[PACK_WAVES][64];
+    __shared__ PackScratch s_ps[PACK_WAVES];
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
     const uint64_t n = b.n_txns;
     const uint64_t t0 = ((uint64_t)blockIdx.x * PACK_WAVES + w) * 64;
@@ -1291,9 +1307,9 @@ __global__ __launch_bounds__(64 * PACK_WAVES) void k_pack(BatchBufs b)
             if (lane == 0) st[64] = (uint32_t)total;
             src[lane] = rb + (a == 0 ? 0 : (a == 1 ? 8ull * nk : 8ull * nk + 4ull * U));
             wave_lds_sync();
-            if (a == 0) pack_run<int64_t>(b.reg, st, src, total, b.o_keys[m] + o0);
-            else if (a == 1) pack_run<uint32_t>(b.reg, st, src, total, b.o_txns[m] + o0);
-            else pack_run<int32_t>(b.reg, st, src, total, b.o_k2t[m] + o0);
+            if (a == 0) pack_run<int64_t>(b.reg, st, src, total, b.o_keys[m] + o0, &s_ps[w]);
+            else if (a == 1) pack_run<uint32_t>(b.reg, st, src, total, b.o_txns[m] + o0, &s_ps[w]);
+            else pack_run<int32_t>(b.reg, st, src, total, b.o_k2t[m] + o0, &s_ps[w]);
         }
     }
 }
@@ -1406,6 +1422,7 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
     __shared__ uint64_t s_wsum[NW][9], s_wo[NW][9];
     __shared__ uint32_t s_start[NW][65];
     __shared__ uint64_t s_src[NW][64];
+    __shared__ PackScratch s_ps[NW];
     const BatchCtl* cc = b.ctl;
     if (cc->n_deferred || cc->error || (cc->overflow & 15u)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
@@ -1481,9 +1498,9 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
             if (lane == 0) st[64] = (uint32_t)total;
             src[lane] = rb + (k == 0 ? 0 : (k == 1 ? 8ull * nk : 8ull * nk + 4ull * U));
             wave_lds_sync();
-            if (k == 0) pack_run<int64_t>(b.reg, st, src, total, b.o_keys[m] + o0);
-            else if (k == 1) pack_run<uint32_t>(b.reg, st, src, total, b.o_txns[m] + o0);
-            else pack_run<int32_t>(b.reg, st, src, total, b.o_k2t[m] + o0);
+            if (k == 0) pack_run<int64_t>(b.reg, st, src, total, b.o_keys[m] + o0, &s_ps[w]);
+            else if (k == 1) pack_run<uint32_t>(b.reg, st, src, total, b.o_txns[m] + o0, &s_ps[w]);
+            else pack_run<int32_t>(b.reg, st, src, total, b.o_k2t[m] + o0, &s_ps[w]);
         }
     }
 }
