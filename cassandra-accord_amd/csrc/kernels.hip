@@ -1228,7 +1228,10 @@ hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // owner byte at the highest marked position <= x, or the previous chunk's last owner (one LDS
 // read and a few bit operations per word instead of a 7-step search of the starts).
 constexpr uint32_t PACK_WAVES = 4;
-constexpr uint32_t PACK_UNROLL = 8;
+#ifndef PACK_UNROLL_N
+#define PACK_UNROLL_N 16
+#endif
+constexpr uint32_t PACK_UNROLL = PACK_UNROLL_N;
 
 struct PackScratch
 {
@@ -1478,6 +1481,9 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
 #pragma unroll 1
     for (int m = 0; m < 3; ++m)
     {
+        if (s_ex[3 * m][i1] == s_ex[3 * m][i0] && s_ex[3 * m + 1][i1] == s_ex[3 * m + 1][i0] &&
+            s_ex[3 * m + 2][i1] == s_ex[3 * m + 2][i0])
+            continue;                                   // the map is empty for the wave's requests
         const uint32_t nk = (uint32_t)(s_ex[3 * m][tid + 1] - s_ex[3 * m][tid]);
         const uint32_t U = (uint32_t)(s_ex[3 * m + 1][tid + 1] - s_ex[3 * m + 1][tid]);
         const uint64_t rb = on ? b.t_reg[(uint64_t)m * n + t] : 0;
