@@ -130,7 +130,7 @@ static_assert(sizeof(KeyEntry) == 64, "KeyEntry is half a cache line");
 //   [16, 28)  last txnId rank, last committed Write's executeAt rank and txnId rank (0: none)
 //   [28, 32)  meta: KL_USED | KL_INLINE | KL_NOLEAN | inline offset of the cwr tail << 24 | #cwr tail
 //   [32, 56)  per witness class c: {#never-elided entries of class c, their start in cand}
-//   [56, 64)  start of the cwr tail in cwr
+//   [56, 64)  start of the cwr tail in cwr, rank of prunedBefore (0: none)
 //   [64, 128) inline emissions when #class-2 entries + #cwr tail <= KL_INL: the never-elided
 //             entries nested by class -- Writes, then Reads, then SyncPoints/ExclusiveSyncPoints
 //             (class c's list is the first n_c of them) -- then the cwr tail
@@ -140,7 +140,7 @@ struct alignas(128) KeyLine {
     uint32_t cell_lo, cell_hi;
     uint32_t last_txn, last_wexec, last_w_txn, meta;
     KeyClassSpan cls[NCLASS];
-    uint32_t cwr_tail, pad;
+    uint32_t cwr_tail, pruned;
     uint32_t inl[16];
 };
 static_assert(sizeof(KeyLine) == 128, "KeyLine is one cache line");

@@ -1657,7 +1657,7 @@ __global__ __launch_bounds__(256) void k_build_klines(DevSnapshot s, const uint3
     L.last_w_txn = ke.last_w_txn;
     for (int c = 0; c < NCLASS; ++c) L.cls[c] = KeyClassSpan{ke.cl[c].cand_hi - ke.cl[c].cand_lo, ke.cl[c].cand_lo};
     L.cwr_tail = ke.cl[0].cwr_tail;
-    L.pad = 0;
+    L.pruned = s.krec[k].pruned;
     const uint32_t n_cwr = ke.cl[0].cwr_hi - ke.cl[0].cwr_tail;
     const uint32_t n2 = L.cls[2].n;
     uint32_t meta = KL_USED | (n_cwr & KL_NCWR_MASK);

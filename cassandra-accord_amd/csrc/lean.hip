@@ -1,12 +1,14 @@
 // lean.hip — the lean fused kernel: the common case of PreAccept.calculatePartialDeps
 // (PreAccept.java:245-267) on a CommandStore without range commands or RedundantBefore entries,
-// for requests newer than everything the store holds. Two (or four) requests per wave (lanes 0-31
+// for requests whose keys' last committed Writes execute before them. Two (or four) requests per wave (lanes 0-31
 // and 32-63), no LDS, no trees:
 //
 //   * executeAt (and txnId) newer than every dictionary id: S = 2 * n_dict without a search
-//   * every key newest (S above its last txnId and its last committed Write's executeAt): the
-//     mapReduceActive emissions (CommandsForKey.java:930-950) are exactly the key's two
-//     precomputed lists (KeyEntry, common.hpp), loaded one element per lane
+//   * every key's last committed Write executes before S (and S is above prunedBefore): then
+//     maxCommittedWriteBefore(S) is the key's last committed Write, so the mapReduceActive
+//     emissions (CommandsForKey.java:930-950) are the key's two precomputed lists (KeyEntry,
+//     common.hpp) restricted to txnIds below S (insertPos(S), :912-928) -- loaded one element per
+//     lane and filtered by rank; a request newer than the whole key keeps every element
 //   * Deps.AbstractBuilder.add routing (Deps.java:80-106) and the RelationMultiMap build
 //     (RelationMultiMap.java:147-260): a 32-lane bitonic sort of (rank, key) per map
 //
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     // the key's line (KeyLine, common.hpp): the slice test (InMemoryCommandStore.java:280), then one
     // random line per key -- its first 64 bytes: key, cell entries, newest fields, meta, the class's
     // {count, start} and the cwr tail start. A slot holding another key is resolved when used.
-    struct Hdr { uint4 h0, h1; uint2 h2; uint32_t h3, slot; bool look; };
+    struct Hdr { uint4 h0, h1; uint2 h2, h3; uint32_t slot; bool look; };
     auto in_slice_of = [&](int64_t key) {
         bool in = s.n_slices == 0;
         for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         H.h0 = L4[0];
         H.h1 = L4[1];
         H.h2 = reinterpret_cast<const uint2*>(L4 + 2)[cls];
-        H.h3 = reinterpret_cast<const uint32_t*>(L4 + 3)[2];
+        H.h3 = reinterpret_cast<const uint2*>(L4 + 3)[1];       // {cwr tail start, prunedBefore rank}
     };
     // the key's displacement (a small table: cache-resident), issued ahead of its line
     auto loadD = [&](const Req& q, int64_t key, bool& look, uint32_t& d) {
@@ -328,9 +330,10 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         uint2 cbc;
         resolve_line(keyc, cls, Hc, has_cfk, cbc);
         const uint32_t meta = Hc.h1.w;
-        // newest: end = byId.length (last txnId < S) and M = the last committed Write's executeAt
-        // (it executes before S), CommandsForKey.java:912-928
-        const bool newest = !has_cfk || (Hc.h1.x < S && Hc.h1.y < S && !(meta & KL_NOLEAN));
+        // lean-served: M = the last committed Write's executeAt (it executes before S,
+        // CommandsForKey.java:912-928) and no prunedBefore substitute (S above prunedBefore,
+        // :952-965); end = insertPos(S) is the element filter rank < S below
+        const bool newest = !has_cfk || (Hc.h1.y < S && (Hc.h3.y == 0 || S > Hc.h3.y) && !(meta & KL_NOLEAN));
         const uint32_t n1 = has_cfk ? Hc.h2.x : 0u;
         const uint32_t n2 = !has_cfk ? 0u : (cls == 0 ? (Hc.h1.z != 0 ? 1u : 0u) : (meta & KL_NCWR_MASK));
         const uint32_t nn = kact ? n1 + n2 : 0u;
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
                 }
                 const uint32_t sx = sb | ax;
                 const uint32_t x_start = __shfl(start, sx, 64), x_n1 = __shfl(n1, sx, 64);
-                const uint32_t x_base = __shfl(Hc.h2.y, sx, 64), x_ct = __shfl(Hc.h3, sx, 64), x_lw = __shfl(Hc.h1.z, sx, 64);
+                const uint32_t x_base = __shfl(Hc.h2.y, sx, 64), x_ct = __shfl(Hc.h3.x, sx, 64), x_lw = __shfl(Hc.h1.z, sx, 64);
                 const uint32_t x_meta = __shfl(meta, sx, 64), x_slot = __shfl(Hc.slot, sx, 64);
                 const bool lv_ = wact && x < T;
                 const uint32_t ii = x - x_start;
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             Hdr Hn;
             loadC(qn, keyn, lookn, dn_, Hn);
             const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
-            const bool want0 = wact && hl < T && r0 != self, want1 = wact && hl + 32 < T && r1 != self;
+            const bool want0 = wact && hl < T && r0 != self && r0 < S, want1 = wact && hl + 32 < T && r1 != self && r1 < S;
             const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
             const bool is1_1 = ((KINDS_RS_OR_WS >> (tw1 >> RANK_BITS)) & 1) == 0;
             for (int m = 0; m < 3; m += 2)
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         }
         const uint32_t src = sb | a;
         const uint32_t a_start = __shfl(start, src, 64), a_n1 = __shfl(n1, src, 64);
-        const uint32_t a_base = __shfl(Hc.h2.y, src, 64), a_ct = __shfl(Hc.h3, src, 64), a_lw = __shfl(Hc.h1.z, src, 64);
+        const uint32_t a_base = __shfl(Hc.h2.y, src, 64), a_ct = __shfl(Hc.h3.x, src, 64), a_lw = __shfl(Hc.h1.z, src, 64);
         const uint32_t a_meta = __shfl(meta, src, 64), a_slot = __shfl(Hc.slot, src, 64);
         const bool live = act && hl < T;
         const uint32_t i = hl - a_start;
@@ -529,7 +532,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 
         const uint32_t txw = !live ? 0u : ((from_cand || cls != 0) ? lv : (a_lw | (1u << RANK_BITS)));
         const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
-        const bool want = live && r != self;
+        const bool want = live && r != self && r < S;
         const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;       // !managesExecution -> directKeyDeps
         const int64_t key = keyc;
 

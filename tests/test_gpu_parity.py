@@ -89,6 +89,35 @@ def test_config2_lean_classes(oracle, esp, sync, reads, monkeypatch):
     assert got2.equals(exp)
 
 
+def test_lean_requests_below_newest_txn(oracle, monkeypatch):
+    # late PreAccepts older than busy keys' newest txnIds (their uncommitted tail) but newer than
+    # the keys' last committed Write: maxCommittedWriteBefore(S) is still the last committed Write,
+    # so the lean kernel serves them with the rank < S filter (insertPos(S),
+    # CommandsForKey.java:912-928) instead of deferring them to the tree descent
+    from accord_deps.model import CfkSnapshot, Workload
+    w = synth.config2(n_txns=4000, n_keys=2000, n_hist_entries=200000, tail_unapplied=6)
+    c = w.cfk
+    st = c.status.copy()
+    st[(st == A.ST_COMMITTED) | (st == A.ST_STABLE)] = A.ST_ACCEPTED       # the tails stay uncommitted
+    w = Workload(w.name, CfkSnapshot(c.keys, c.seg, c.txn, c.exec, st, c.pruned_before), w.cmds, w.redundant,
+                 w.queries, w.flags, w.params, w.range_start_inclusive, w.slices)
+    w = synth.with_request_mix(w, unordered_frac=1.0, unordered_window=6)
+    q = w.queries
+    seg = c.seg.astype(np.int64)
+    last_hlc = (c.txn.lsb[seg[1:] - 1] >> np.uint64(16)).astype(np.int64)
+    kidx = np.searchsorted(c.keys, q.keys)
+    kidx_c = np.minimum(kidx, len(c.keys) - 1)
+    held = c.keys[kidx_c] == q.keys
+    req = np.repeat(np.arange(len(q.txn.msb)), np.diff(q.key_off.astype(np.int64)))
+    older_key = held & (last_hlc[kidx_c] >= (q.txn.lsb[req] >> np.uint64(16)).astype(np.int64))
+    n_older = len(np.unique(req[older_key]))
+    got, exp = _compare(w, oracle, paths=(0,))
+    assert n_older > 500
+    assert got.stats["n_deferred_lean"] < n_older // 2
+    monkeypatch.setenv("AD_NO_LEAN", "1")
+    assert native.resolve(w).equals(exp)
+
+
 def test_config1_sequential(oracle):
     got, exp = _compare(synth.config1(), oracle)
     assert got.pair_count(A.AD_MAP_KEY) > 0
