@@ -148,6 +148,42 @@ __device__ __forceinline__ uint64_t grp_lower_bound(bool active, uint64_t lo, ui
     return lo + __popc(grp_bits(ballot(v), g));
 }
 
+// Two lower_bounds of one threshold (key(i) < x) by the same 8-lane groups, advanced in lockstep:
+// both rounds' loads are in flight together, so the pair costs one search's chain of round trips
+template <class KeyA, class KeyB>
+__device__ __forceinline__ void grp_lower_bound2(bool act_a, uint64_t lo_a, uint64_t hi_a, KeyA key_a, bool act_b,
+                                                 uint64_t lo_b, uint64_t hi_b, KeyB key_b, uint32_t x,
+                                                 uint64_t& out_a, uint64_t& out_b)
+{
+    const uint32_t j = lane_id() & 7, g = lane_id() >> 3;
+    auto step = [&](bool on, bool lt, uint64_t& lo, uint64_t& hi) {
+        const uint32_t c = __popc(grp_bits(ballot(lt), g));
+        if (!on) return;
+        const uint64_t n = hi - lo;
+        if (c == 8) lo = hi;
+        else
+        {
+            const uint64_t pc = lo + (((uint64_t)(c + 1) * n) >> 3) - 1;
+            lo = c == 0 ? lo : lo + (((uint64_t)c * n) >> 3);
+            hi = pc;
+        }
+    };
+    while (ballot((act_a && hi_a - lo_a > 8) || (act_b && hi_b - lo_b > 8)))
+    {
+        const bool sa = act_a && hi_a - lo_a > 8, sb = act_b && hi_b - lo_b > 8;
+        const uint64_t pa = sa ? lo_a + (((uint64_t)(j + 1) * (hi_a - lo_a)) >> 3) - 1 : 0;
+        const uint64_t pb = sb ? lo_b + (((uint64_t)(j + 1) * (hi_b - lo_b)) >> 3) - 1 : 0;
+        const uint32_t va = sa ? key_a(pa) : 0u, vb = sb ? key_b(pb) : 0u;
+        step(sa, sa && va < x, lo_a, hi_a);
+        step(sb, sb && vb < x, lo_b, hi_b);
+    }
+    const uint64_t ia = lo_a + j, ib = lo_b + j;
+    const bool la = act_a && ia < hi_a, lb = act_b && ib < hi_b;
+    const uint32_t va = la ? key_a(ia) : 0u, vb = lb ? key_b(ib) : 0u;
+    out_a = lo_a + __popc(grp_bits(ballot(la && va < x), g));
+    out_b = lo_b + __popc(grp_bits(ballot(lb && vb < x), g));
+}
+
 // Group-parallel max-tree descent: like wave_descent, but each 8-lane group walks its own
 // range [lo, end) and every lane evaluates 8 consecutive nodes (leaves) of a 64-wide frame.
 //   node_bits(lv, n0, nlo, nhi) -> 8-bit want mask of nodes n0..n0+7 (within [nlo, nhi])
@@ -434,13 +470,13 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))
         // ---- K1: end = insertPos(S), M = maxCommittedWriteBefore (CommandsForKey.java:912-928)
         const uint64_t lo = kr.seg_lo, hi = kr.seg_hi;
         const bool tail = !has_cfk || hi == lo || kr.last_txn < S;
-        const uint64_t end = grp_lower_bound(has_cfk && !tail, lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
-                                             [&](uint32_t v) { return v < S; });
-        const uint64_t end_g = tail ? hi : end;
         const uint64_t wlo = kr.w_lo, whi = kr.w_hi;
         const bool wtail = !has_cfk || whi == wlo || kr.last_wexec < S;
-        const uint64_t wsearch = grp_lower_bound(has_cfk && !wtail, wlo, whi, [&](uint64_t i) { return s.w[i].x; },
-                                                 [&](uint32_t v) { return v < S; });
+        // insertPos(S) in byId and the committed Writes' executeAt search, in lockstep
+        uint64_t end, wsearch;
+        grp_lower_bound2(has_cfk && !tail, lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
+                         has_cfk && !wtail, wlo, whi, [&](uint64_t i) { return s.w[i].x; }, S, end, wsearch);
+        const uint64_t end_g = tail ? hi : end;
         const uint64_t wpos = !has_cfk ? wlo : (whi == wlo ? wlo : (kr.last_wexec < S ? whi : wsearch));
         uint32_t wprev = 0;
         if (has_cfk && wpos > wlo) wprev = (wpos == whi) ? kr.last_wexec : s.w[wpos - 1].x;
