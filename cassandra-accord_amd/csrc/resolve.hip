@@ -25,6 +25,9 @@ constexpr int FCAP0 = 64;       // keyDeps txnIds staged per key
 constexpr int FCAP1 = 16;       // directKeyDeps txnIds staged per key
 constexpr int FCAPR = 32;       // range-command pairs staged per key (+1 slot: redundant pair)
 constexpr int FWAVES = 4;       // waves per workgroup
+#ifndef FUSED_WPE
+#define FUSED_WPE 4          // waves per SIMD the general kernel's register budget is sized for
+#endif
 constexpr uint32_t F_REGION_CHUNK = 1u << 16;
 
 struct FusedLds {
@@ -306,7 +309,7 @@ struct FChunk {
     }
 };
 
-__global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(4))) void k_resolve(DevSnapshot s, BatchBufs b)
+__global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUSED_WPE))) void k_resolve(DevSnapshot s, BatchBufs b)
 {
     __shared__ FusedLds lds_all[FWAVES];
     FusedLds& L = lds_all[threadIdx.x >> 6];
