@@ -1113,19 +1113,22 @@ def bench_deps(args, rank, world, local, dev):
     lean_rpw1 = 4 if w.queries.n_probes <= 3 * max(1, len(w.queries)) else 2
     res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1) for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
     traffic, traffic_src = measured_traffic(res_kernels, "config%d" % cfg)
+    xdesc = ""
+    if world > 1:
+        xdesc = (", per-store partials exchanged over RCCL inside libaccord_deps (ad_exchange) + K3 merge on the owning GPU"
+                 if use_x else ", per-store partials exchanged over gloo staged through host memory (rehearsal: ranks "
+                 "share GPUs) + K3 merge on the owning GPU")
     if cfg == 3:
         workload = ("config3 (%d/8 of it on %d GPU%s): %d txns over %d uniform keys, %d-txn history x 4 keys, %d-request "
                     "probe batch, token-range sharded (EvenSplit), SNAPSHOT, 1 CommandStore per GPU%s" %
                     (world, world, "s" if world > 1 else "", int(w.params["n_txns"]), int(w.params["n_keys"]),
                      int(w.params["n_hist_txns"]), n_total,
-                     ", per-store partials exchanged over RCCL inside libaccord_deps (ad_exchange) + K3 merge on the owning GPU"
-                     if world > 1 else ""))
+                     xdesc))
     else:
         workload = ("config2 (weak-scaled per GPU): %d txns x 8 Zipf(0.99) keys, %d keys and a %d-entry CommandsForKey "
                     "history per GPU, SNAPSHOT, 1 CommandStore per GPU%s" %
                     (n_total, int(1_000_000 * s) * world, w.cfk.n_entries,
-                     ", per-store partials exchanged over RCCL inside libaccord_deps (ad_exchange) + K3 merge on the owning GPU"
-                     if world > 1 else "") +
+                     xdesc) +
                     ("; request mix: %d Accepts of in-flight txns (S = executeAt, self excluded), %d PreAccepts up to %d hlc "
                      "ticks late, the rest fresh PreAccepts" % (w.params["n_accept"], w.params["n_unordered"],
                                                                 args.unordered_window) if mix else ""))
