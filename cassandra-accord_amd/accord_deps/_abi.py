@@ -19,6 +19,7 @@ AD_E_NOT_LOADED = -7
 AD_E_STATE = -8
 AD_E_CAPACITY = -9
 AD_E_SPACE = -10
+AD_E_PEER = -11
 
 AD_MAP_KEY, AD_MAP_RANGE, AD_MAP_DIRECT_KEY = 0, 1, 2
 NMAPS = 3
@@ -137,6 +138,20 @@ class AdParts(C.Structure):
 
 AD_IDS_TRIPLET = 0
 AD_IDS_RANK = 1
+
+# exchange table / plan (accord_deps.h, ad_exchange_plan)
+AD_XROW_HDR = 12
+AD_XROW_MAGIC = 0x41445852
+AD_XPLAN_GROW = 1
+
+
+def xrow_words(world):
+    return 4 * world + AD_XROW_HDR
+
+
+class AdXfer(C.Structure):
+    _fields_ = [("send_off", C.c_uint64), ("send_bytes", C.c_uint64), ("recv_off", C.c_uint64),
+                ("recv_bytes", C.c_uint64)]
 
 
 class AdMerged(C.Structure):

@@ -245,6 +245,7 @@ class NodeExchange:
 
     def step(self):
         res, self.last_stats = self.store.deps_batch_device(self.qdev, self.stream, parts_only=True)
+        self.last_res = res
         mg, self.last_exchange = self.store.exchange(res, self.ti.data_ptr(), self.dest_first, self.txn_base,
                                                      self.n_owned, self.stream)
         return mg

@@ -25,7 +25,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_preaccept_device", "ad_parts_union", "ad_cfk_missing_load", "ad_range_cmds_recovery_load", "ad_recovery_batch",
            "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries",
            "ad_cfk_ballots_load", "ad_cfk_ballots",
-           "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange",
+           "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange", "ad_exchange_plan",
            "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing")
 
 
@@ -102,6 +102,8 @@ def lib():
         L.ad_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         L.ad_exchange.argtypes = [C.c_void_p, C.POINTER(A.AdDepsResult), C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64,
                                   C.c_void_p, C.POINTER(A.AdMerged), C.POINTER(A.AdExchangeStats)]
+        L.ad_exchange_plan.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(A.AdXfer), C.c_void_p,
+                                       C.c_void_p, C.POINTER(C.c_uint32)]
         L.ad_check_result_device.argtypes = [C.c_void_p, C.POINTER(A.AdDepsResult), C.c_void_p, C.POINTER(C.c_uint64),
                                              C.POINTER(C.c_uint64)]
         L.ad_cfk_prune.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_int64, C.POINTER(C.c_uint64),
@@ -128,6 +130,36 @@ def comm_unique_id():
     if rc:
         raise AccordDepsError(rc, "ad_comm_unique_id")
     return bytes(b)
+
+
+def exchange_row(counts, id_format, status=0, send_cap=None, recv_cap=None):
+    """One rank's row of the exchange table (accord_deps.h, ad_exchange_plan): counts[world, 4] units
+    per destination and array, then the header (format, status as -code, capacities in units)."""
+    counts = np.asarray(counts, np.uint64).reshape(-1, 4)
+    big = np.full(4, np.iinfo(np.uint64).max, np.uint64)
+    hdr = np.zeros(A.AD_XROW_HDR, np.uint64)
+    hdr[0] = A.AD_XROW_MAGIC
+    hdr[1] = id_format
+    hdr[2] = np.uint64(-int(status)) if status else 0
+    hdr[4:8] = big if send_cap is None else np.asarray(send_cap, np.uint64)
+    hdr[8:12] = big if recv_cap is None else np.asarray(recv_cap, np.uint64)
+    return np.concatenate([counts.reshape(-1), hdr])
+
+
+def exchange_plan(table, world, rank):
+    """ad_exchange_plan (pure host code, no device): the transfers of `rank` from the gathered
+    exchange table [world, AD_XROW_WORDS]. Returns (rc, xfers[4, world, 4] = (send_off, send_bytes,
+    recv_off, recv_bytes) in bytes, recv_units[4], src_parts[world], flags)."""
+    t = np.ascontiguousarray(table, np.uint64).reshape(-1)
+    if len(t) != world * A.xrow_words(world):
+        raise ValueError("exchange table of %d words for world %d" % (len(t), world))
+    xf = (A.AdXfer * (4 * world))()
+    ru = np.zeros(4, np.uint64)
+    sp = np.zeros(world, np.uint64)
+    fl = C.c_uint32(0)
+    rc = lib().ad_exchange_plan(A.ptr(t), world, rank, xf, A.ptr(ru), A.ptr(sp), C.byref(fl))
+    x = np.array([(f.send_off, f.send_bytes, f.recv_off, f.recv_bytes) for f in xf], np.uint64).reshape(4, world, 4)
+    return rc, x, ru, sp, int(fl.value)
 
 
 def exchange_local(stores, results, txn_index_ptrs, dest_firsts, txn_bases, n_owned):
@@ -498,29 +530,44 @@ class DeviceCommandStore:
             self._check(lib().ad_copy_to_host(self.h, A.ptr(a), p, a.nbytes))
         return a
 
-    def merged_to_host(self, mg):
-        """Materialise an AdMerged into a PartialDepsBatch (ids as TxnIds, ranges as (start, end))."""
+    def merged_to_host(self, mg, idx=None):
+        """Materialise an AdMerged into a PartialDepsBatch (ids as TxnIds, ranges as (start, end)), for
+        every owned request or only the owned requests `idx` (indices from 0 = txn_base)."""
         n = mg.n_txns
         maps = []
         for m in range(A.NMAPS):
+            w = 2 if m == A.AD_MAP_RANGE else 1
             ko = self._d2h(mg.keys_off[m], n + 1, np.uint64)
             to = self._d2h(mg.txn_off[m], n + 1, np.uint64)
             oo = self._d2h(mg.k2t_off[m], n + 1, np.uint64)
-            w = 2 if m == A.AD_MAP_RANGE else 1
-            kw = self._d2h(mg.keys[m], w * int(mg.n_keys[m]), np.int64)
+            kw = self._d2h(mg.keys[m], w * int(mg.n_keys[m]), np.int64).reshape(-1, w)
             k2t = self._d2h(mg.k2t[m], int(mg.n_k2t[m]), np.int32)
-            if mg.id_format == A.AD_IDS_RANK:
+            rank_ids = mg.id_format == A.AD_IDS_RANK
+            if rank_ids:
                 if self.global_dict is None:
                     raise ValueError("rank-format merge result without the global dictionary")
-                txn = self.global_dict.take(self._d2h(mg.txns[m], int(mg.n_ids[m]), np.uint32).astype(np.int64))
+                ids = self._d2h(mg.txns[m], int(mg.n_ids[m]), np.uint32)
             else:
                 ids = self._d2h(mg.txns[m], 3 * int(mg.n_ids[m]), np.int64).reshape(-1, 3)
-                txn = Tids(ids[:, 0].view(np.uint64).copy(), ids[:, 1].view(np.uint64).copy(),
-                           ids[:, 2].astype(np.int32))
-            if m == A.AD_MAP_RANGE:
-                maps.append(DepsMap(ko, kw[0::2].copy(), kw[1::2].copy(), to, txn, oo, k2t))
+            if idx is not None:
+                ix = np.asarray(idx, np.int64)
+                cols = []
+                for off, arr in ((ko, kw), (to, ids), (oo, k2t)):
+                    o = off.astype(np.int64)
+                    cnt = o[ix + 1] - o[ix]
+                    no = np.zeros(len(ix) + 1, np.uint64)
+                    no[1:] = np.cumsum(cnt)
+                    src = np.repeat(o[ix] - no[:-1].astype(np.int64), cnt) + np.arange(int(no[-1]))
+                    cols += [no, arr[src]]
+                ko, kw, to, ids, oo, k2t = cols
+            if rank_ids:
+                txn = self.global_dict.take(ids.astype(np.int64))
             else:
-                maps.append(DepsMap(ko, kw, None, to, txn, oo, k2t))
+                txn = Tids(ids[:, 0].view(np.uint64).copy(), ids[:, 1].view(np.uint64).copy(), ids[:, 2].astype(np.int32))
+            if m == A.AD_MAP_RANGE:
+                maps.append(DepsMap(ko, kw[:, 0].copy(), kw[:, 1].copy(), to, txn, oo, k2t))
+            else:
+                maps.append(DepsMap(ko, kw[:, 0].copy(), None, to, txn, oo, k2t))
         return PartialDepsBatch(maps)
 
 

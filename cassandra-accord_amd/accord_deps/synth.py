@@ -282,6 +282,28 @@ def slice_tokens(lo, hi, n, salt):
         return (np.uint64((int(lo) + 1) % (1 << 64)) + off).view(np.int64)
 
 
+TIMESTAMP_MAX = (0x7FFFFFFFFFFFFFFF, 0x7FFFFFFFFFFFFFFF, 0x7FFFFFFF)   # Timestamp.MAX (Timestamp.java:29)
+
+
+def with_ephemeral_reads(w, frac=0.3, seed=0xACC0DE4D):
+    """GetEphemeralReadDeps requests (GetEphemeralReadDeps.java:76): a share of the batch becomes
+    EphemeralRead txns whose deps are computed at executeAt = Timestamp.MAX (msb = lsb = Long.MAX_VALUE,
+    node Id.MAX: the flag bits read as kind 7), i.e. every started txn of a key it witnesses."""
+    import copy
+    rng = np.random.default_rng(seed)
+    q = w.queries
+    sel = rng.random(len(q)) < frac
+    lsb = q.txn.lsb.copy()
+    lsb[sel] = (lsb[sel] & ~np.uint64(0xE)) | np.uint64(A.KIND_EPHEMERAL_READ << 1)
+    txn = Tids(q.txn.msb.copy(), lsb, q.txn.node.copy())
+    em, el, en = q.exec.msb.copy(), q.exec.lsb.copy(), q.exec.node.copy()
+    em[sel], el[sel], en[sel] = np.uint64(TIMESTAMP_MAX[0]), np.uint64(TIMESTAMP_MAX[1]), np.int32(TIMESTAMP_MAX[2])
+    out = copy.copy(w)
+    out.queries = Queries(txn, Tids(em, el, en), q.key_off.copy(), q.keys.copy(), q.min_epoch)
+    out.name = w.name + "+ephemeral"
+    return out
+
+
 def config2_sharded(rank, world, n_txns_per_gpu=1_000_000, keys_per_txn=8, n_keys_per_gpu=1_000_000,
                     n_hist_entries_per_gpu=16_000_000, zipf_s=0.99, seed=0xACC0D002, sync_frac=0.02,
                     tail_unapplied=4):

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdarg>
@@ -275,11 +276,13 @@ struct ad_ctx {
     // node exchange (ad_exchange / ad_exchange_local): library-owned part buffers, RCCL communicator
     DevBuf xs_hdr, xs_keys, xs_ids, xs_k2t;    // this store's exported parts (grouped by owner)
     DevBuf xr_hdr, xr_keys, xr_ids, xr_k2t;    // parts received for the requests this store owns
-    DevBuf xc_dev;                             // counts table of the RCCL all-gather
-    uint64_t xs_counts[4] = {}, xr_total[4] = {};
-    std::vector<uint64_t> x_dest_counts;       // [n_dest][4] of the last export
+    DevBuf xc_dev;                             // exchange table of the RCCL all-gather (+ own row, status words)
+    uint64_t* h_xtab = nullptr;                // pinned host copy of the exchange table
+    size_t h_xtab_words = 0;
+    uint64_t xr_total[4] = {};
     ncclComm_t comm = nullptr;
     int comm_rank = 0, comm_world = 1;
+    hipEvent_t x_ev[3] = {};                   // ad_exchange: step start, parts emitted, move done
     // execution levels (K5)
     LevelsWork* lv = nullptr;
     DevBuf g_em, g_el, g_en, g_kind, g_ko, g_k, g_do, g_d, g_out;
@@ -1737,6 +1740,9 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->ev_sp0) (void)hipEventDestroy(c->ev_sp0);
     if (c->ev_sp1) (void)hipEventDestroy(c->ev_sp1);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+    if (c->h_xtab) (void)hipHostFree(c->h_xtab);
+    for (hipEvent_t e : c->x_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->lv) levels_work_destroy(c->lv);
     if (c->cu) cfk_upd_work_destroy(c->cu);
     if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -2370,18 +2376,28 @@ int ad_set_global_dict(ad_ctx* c, uint64_t n, const uint64_t* msb, const uint64_
     return AD_OK;
 }
 
-int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
-                    const uint64_t* dest_first, void* stream, ad_parts* out, uint64_t* dest_counts)
+}  // extern "C"
+
+// Export, phase 1 (ad_parts_export, ad_exchange, ad_exchange_local): validate, bind the export
+// arguments and enqueue the size pass; c->x_cnt then holds the cumulative [n_dest + 1][4] bounds
+// {parts, key words, ids, k2t} of the destinations. Nothing is read back.
+static int export_sizes(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
+                        const uint64_t* dest_first, uint32_t id_format, hipStream_t st, ExportArgs* pa)
 {
-    if (!c || !res || !out || !dest_first || !dest_counts || n_dest == 0) return AD_E_INVAL;
-    if (c->dirty) return c->fail(AD_E_NOT_LOADED, "ad_parts_export: no prepared snapshot");
+    if (!res || !dest_first || n_dest == 0) return c->fail(AD_E_INVAL, "export: result, dest_first and n_dest are required");
+    if (c->dirty) return c->fail(AD_E_NOT_LOADED, "export: no prepared snapshot");
     const uint64_t n = res->n_txns;
-    if (n && !txn_index) return c->fail(AD_E_INVAL, "ad_parts_export: txn_index is NULL");
-    if (dest_first[0] != 0 || dest_first[n_dest] != n) return c->fail(AD_E_INVAL, "ad_parts_export: dest_first must span [0, n)");
+    if (n && !txn_index) return c->fail(AD_E_INVAL, "export: txn_index is NULL");
+    if (dest_first[0] != 0 || dest_first[n_dest] != n) return c->fail(AD_E_INVAL, "export: dest_first must span [0, n)");
     for (uint32_t d = 0; d < n_dest; ++d)
-        if (dest_first[d] > dest_first[d + 1]) return c->fail(AD_E_INVAL, "ad_parts_export: dest_first not ascending");
+        if (dest_first[d] > dest_first[d + 1]) return c->fail(AD_E_INVAL, "export: dest_first not ascending");
+    // the id format is the caller's: its ids buffer was sized for it (cap_ids counts ids of that format)
+    if (id_format != AD_IDS_RANK && id_format != AD_IDS_TRIPLET)
+        return c->fail(AD_E_INVAL, "export: unknown id_format %u", id_format);
+    if (id_format == AD_IDS_RANK && !c->global_ok)
+        return c->fail(AD_E_STATE, "export: rank-format parts need a global dictionary covering this store's "
+                                   "ids (ad_set_global_dict after the last snapshot load or dictionary append)");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if (!ens<uint32_t>(c->x_sz, std::max<uint64_t>(n, 1)) || !ens<uint64_t>(c->x_off, n + 1) ||
         !ens<uint64_t>(c->x_bsum, (n + 1023) / 1024 + 16) || !ens<uint64_t>(c->x_df, n_dest + 1) ||
         !ens<uint64_t>(c->x_cnt, 4 * (n_dest + 1)))
@@ -2399,7 +2415,7 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     {
         // a parts-only result: read the batch's regions (still valid: no batch since)
         if (!c->last_parts_only || c->last_n != n)
-            return c->fail(AD_E_INVAL, "ad_parts_export: result without packed arrays is not the ctx's last batch");
+            return c->fail(AD_E_INVAL, "export: result without packed arrays is not the ctx's last batch");
         a.reg = c->last_reg;
         a.t_reg = c->last_t_reg;
     }
@@ -2408,19 +2424,34 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     a.dict_node = c->d_dict_node.as<int32_t>();
     a.rt_start = c->d_rt_start.as<int64_t>();
     a.rt_end = c->d_rt_end.as<int64_t>();
-    // the id format is the caller's: its ids buffer was sized for it (cap_ids counts ids of that format)
-    if (out->id_format != AD_IDS_RANK && out->id_format != AD_IDS_TRIPLET)
-        return c->fail(AD_E_INVAL, "ad_parts_export: unknown id_format %u", out->id_format);
-    if (out->id_format == AD_IDS_RANK && !c->global_ok)
-        return c->fail(AD_E_STATE, "ad_parts_export: rank-format parts need a global dictionary covering this store's "
-                                   "ids (ad_set_global_dict after the last snapshot load or dictionary append)");
-    a.rank_ids = out->id_format == AD_IDS_RANK;      // the dictionary is the global one: ids are global ranks
+    a.rank_ids = id_format == AD_IDS_RANK;      // the dictionary is the global one: ids are global ranks
     a.sz = c->x_sz.as<uint32_t>();
     a.off = c->x_off.as<uint64_t>();
     HIPCHK(c, hipMemcpyAsync(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), hipMemcpyHostToDevice, st));
     HIPCHK(c, run_export_sizes(a, st));
     HIPCHK(c, run_scan_arrays(a.sz, a.off, n, 1, c->x_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_export_bounds(a, c->x_df.as<uint64_t>(), n_dest, c->x_cnt.as<uint64_t>(), st));
+    *pa = a;
+    return AD_OK;
+}
+
+// Export, phase 2: the parts into arrays sized from phase 1's bounds (grouped by destination)
+static int export_emit(ad_ctx* c, ExportArgs& a, int64_t* hdr, int64_t* keys, int64_t* ids, int32_t* k2t, hipStream_t st)
+{
+    a.hdr = hdr; a.okeys = keys; a.oids = ids; a.ok2t = k2t;
+    HIPCHK(c, run_export_emit(a, st));
+    return AD_OK;
+}
+
+extern "C" {
+
+int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
+                    const uint64_t* dest_first, void* stream, ad_parts* out, uint64_t* dest_counts)
+{
+    if (!c || !res || !out || !dest_first || !dest_counts || n_dest == 0) return AD_E_INVAL;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    ExportArgs a{};
+    if (int rc = export_sizes(c, res, txn_index, n_dest, dest_first, out->id_format, st, &a)) return rc;
     std::vector<uint64_t> cnt(4 * (n_dest + 1));
     HIPCHK(c, hipMemcpyAsync(cnt.data(), c->x_cnt.p, sizeof(uint64_t) * cnt.size(), hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
@@ -2438,9 +2469,7 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
                 (unsigned long long)out->n_ids, (unsigned long long)out->n_k2t);
         return AD_E_SPACE;
     }
-    a.hdr = out->hdr; a.okeys = out->keys; a.oids = out->ids; a.ok2t = out->k2t;
-    HIPCHK(c, run_export_emit(a, st));
-    return AD_OK;
+    return export_emit(c, a, out->hdr, out->keys, out->ids, out->k2t, st);
 }
 
 static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
@@ -3264,66 +3293,114 @@ static DevBuf* x_send(ad_ctx* c, int a) { DevBuf* b[XA] = {&c->xs_hdr, &c->xs_ke
 static DevBuf* x_recv(ad_ctx* c, int a) { DevBuf* b[XA] = {&c->xr_hdr, &c->xr_keys, &c->xr_ids, &c->xr_k2t}; return b[a]; }
 static uint32_t x_format(const ad_ctx* c) { return c->global_ok ? AD_IDS_RANK : AD_IDS_TRIPLET; }
 
-// Export the last device batch of c as parts grouped by owner into c's send buffers (grown on
-// AD_E_SPACE); c->x_dest_counts[4 d + a] = units of array a for destination d. Complete on return.
-static int x_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
-                    const uint64_t* dest_first, hipStream_t st)
+// The plan of `R` from an agreed exchange table (layout: accord_deps.h, ad_exchange_plan). Every rank
+// runs it on the same table, so every verdict -- failure, id formats, growth round -- is collective.
+// bad: the rank whose row failed a check (-1: none).
+static int x_plan(const uint64_t* table, uint32_t W, uint32_t R, ad_xfer* xf, uint64_t* recv_units, uint64_t* src_parts,
+                  uint32_t* flags, int* bad)
 {
-    c->x_dest_counts.assign(4 * (size_t)n_dest, 0);
-    const uint32_t fmt = x_format(c);
-    for (int attempt = 0; attempt < 3; ++attempt)
+    const size_t RW = AD_XROW_WORDS(W);
+    auto row = [&](uint32_t s) { return table + RW * s; };
+    *bad = -1;
+    for (uint32_t s = 0; s < W; ++s)
+        if (row(s)[4 * W] != AD_XROW_MAGIC || row(s)[4 * W + 3] != 0) { *bad = (int)s; return AD_E_INVAL; }
+    for (uint32_t s = 0; s < W; ++s)
+        if (row(s)[4 * W + 2] != 0) { *bad = (int)s; return AD_E_PEER; }
+    const uint64_t fmt = row(0)[4 * W + 1];
+    if (fmt != AD_IDS_RANK && fmt != AD_IDS_TRIPLET) { *bad = 0; return AD_E_INVAL; }
+    for (uint32_t s = 1; s < W; ++s)
+        if (row(s)[4 * W + 1] != fmt) { *bad = (int)s; return AD_E_STATE; }
+    uint32_t fl = 0;
+    for (int a = 0; a < XA; ++a)
     {
-        ad_parts p{};
-        p.hdr = c->xs_hdr.as<int64_t>();
-        p.keys = c->xs_keys.as<int64_t>();
-        p.ids = c->xs_ids.as<int64_t>();
-        p.k2t = c->xs_k2t.as<int32_t>();
-        p.cap_parts = c->xs_hdr.cap / x_unit_bytes(0, fmt);
-        p.cap_key_words = c->xs_keys.cap / x_unit_bytes(1, fmt);
-        p.cap_ids = c->xs_ids.cap / x_unit_bytes(2, fmt);
-        p.cap_k2t = c->xs_k2t.cap / x_unit_bytes(3, fmt);
-        p.id_format = fmt;
-        const int rc = ad_parts_export(c, res, txn_index, n_dest, dest_first, st, &p, c->x_dest_counts.data());
-        if (rc == AD_OK)
+        const uint64_t ub = x_unit_bytes(a, (uint32_t)fmt);
+        uint64_t soff = 0, roff = 0;
+        for (uint32_t p = 0; p < W; ++p)
         {
-            HIPCHK(c, hipStreamSynchronize(st));
-            c->xs_counts[0] = p.n_parts; c->xs_counts[1] = p.n_key_words; c->xs_counts[2] = p.n_ids; c->xs_counts[3] = p.n_k2t;
-            return AD_OK;
+            const uint64_t sc = row(R)[4 * p + a], rc = row(p)[4 * R + a];
+            xf[(size_t)a * W + p] = ad_xfer{ub * soff, ub * sc, ub * roff, ub * rc};
+            soff += sc;      // R's parts for p follow those for the lower ranks (grouped by owner)
+            roff += rc;      // p's parts for R follow the lower ranks' (source = slice order for K3)
         }
-        if (rc != AD_E_SPACE) return rc;
-        const uint64_t need[XA] = {p.n_parts, p.n_key_words, p.n_ids, p.n_k2t};
-        for (int a = 0; a < XA; ++a)
-            if (!x_send(c, a)->ensure(x_unit_bytes(a, fmt) * (need[a] + need[a] / 4 + 64)))
-                return c->fail(AD_E_NOMEM, "exchange send buffers");
+        recv_units[a] = roff;
+        // every rank's totals against the capacities it published
+        for (uint32_t s = 0; s < W; ++s)
+        {
+            uint64_t snd = 0, rcv = 0;
+            for (uint32_t p = 0; p < W; ++p)
+            {
+                snd += row(s)[4 * p + a];
+                rcv += row(p)[4 * s + a];
+            }
+            if (snd > row(s)[4 * W + 4 + a] || rcv > row(s)[4 * W + 8 + a]) fl |= AD_XPLAN_GROW;
+        }
     }
-    return c->fail(AD_E_DEVICE, "exchange export did not fit after growing its buffers");
+    for (uint32_t p = 0; p < W; ++p) src_parts[p] = row(p)[4 * R + 0];
+    *flags = fl;
+    return AD_OK;
 }
 
-// receive buffers of c for `tot` units per array
-static int x_recv_ensure(ad_ctx* c, const uint64_t* tot, uint32_t fmt)
+// header words of c's row: format, status (-code of a failure before the move), buffer capacities in units
+static XRowHdr x_row_hdr(ad_ctx* c, uint32_t fmt, int status)
+{
+    XRowHdr h{};
+    h.w[0] = AD_XROW_MAGIC;
+    h.w[1] = fmt;
+    h.w[2] = status ? (uint64_t)(-(int64_t)status) : 0;
+    h.w[3] = 0;
+    for (int a = 0; a < XA; ++a)
+    {
+        h.w[4 + a] = x_send(c, a)->cap / x_unit_bytes(a, fmt);
+        h.w[8 + a] = x_recv(c, a)->cap / x_unit_bytes(a, fmt);
+    }
+    return h;
+}
+
+// send / receive buffers of c for the units of a step (25 % headroom when they grow)
+static int x_grow(ad_ctx* c, const uint64_t* send_units, const uint64_t* recv_units, uint32_t fmt)
 {
     for (int a = 0; a < XA; ++a)
-        if (!x_recv(c, a)->ensure(x_unit_bytes(a, fmt) * (tot[a] + tot[a] / 4 + 64)))
+    {
+        const uint64_t ub = x_unit_bytes(a, fmt);
+        if (ub * send_units[a] > x_send(c, a)->cap && !x_send(c, a)->ensure(ub * (send_units[a] + send_units[a] / 4 + 64)))
+            return c->fail(AD_E_NOMEM, "exchange send buffers");
+        if (ub * recv_units[a] > x_recv(c, a)->cap && !x_recv(c, a)->ensure(ub * (recv_units[a] + recv_units[a] / 4 + 64)))
             return c->fail(AD_E_NOMEM, "exchange receive buffers");
-    for (int a = 0; a < XA; ++a) c->xr_total[a] = tot[a];
-    return 0;
+    }
+    return AD_OK;
+}
+
+static int x_emit(ad_ctx* c, ExportArgs& a, hipStream_t st)
+{
+    return export_emit(c, a, c->xs_hdr.as<int64_t>(), c->xs_keys.as<int64_t>(), c->xs_ids.as<int64_t>(),
+                       c->xs_k2t.as<int32_t>(), st);
 }
 
 // K3 on c over its receive buffers: sources in slice (= rank / context) order
-static int x_merge(ad_ctx* c, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base, uint64_t n_owned,
-                   hipStream_t st, ad_merged* out)
+static int x_merge(ad_ctx* c, uint32_t n_src, const uint64_t* src_parts, const uint64_t* recv_units, uint32_t fmt,
+                   uint64_t txn_base, uint64_t n_owned, hipStream_t st, ad_merged* out)
 {
     ad_parts in{};
     in.hdr = c->xr_hdr.as<int64_t>();
     in.keys = c->xr_keys.as<int64_t>();
     in.ids = c->xr_ids.as<int64_t>();
     in.k2t = c->xr_k2t.as<int32_t>();
-    in.n_parts = c->xr_total[0];
-    in.n_key_words = c->xr_total[1];
-    in.n_ids = c->xr_total[2];
-    in.n_k2t = c->xr_total[3];
-    in.id_format = x_format(c);
+    in.n_parts = recv_units[0];
+    in.n_key_words = recv_units[1];
+    in.n_ids = recv_units[2];
+    in.n_k2t = recv_units[3];
+    in.id_format = fmt;
+    for (int a = 0; a < XA; ++a) c->xr_total[a] = recv_units[a];
     return ad_parts_merge(c, &in, n_src, src_parts, txn_base, n_owned, st, out);
+}
+
+// an error after the table was agreed: the peers are (or will be) inside the grouped send/recv, so the
+// communicator is torn down -- this rank returns at once and its process exits instead of waiting
+static int x_abort(ad_ctx* c, int code)
+{
+    if (c->comm) (void)ncclCommAbort(c->comm);
+    c->comm = nullptr;
+    return code;
 }
 
 static int nccl_fail(ad_ctx* c, ncclResult_t r, const char* what)
@@ -3336,9 +3413,23 @@ static int nccl_fail(ad_ctx* c, ncclResult_t r, const char* what)
         if (_r != ncclSuccess) return nccl_fail((ctx), _r, #expr);                                 \
     } while (0)
 
+static float ev_ms(hipEvent_t a, hipEvent_t b)
+{
+    float ms = 0;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.f;
+}
+
 }  // namespace
 
 extern "C" {
+
+int ad_exchange_plan(const uint64_t* table, uint32_t world, uint32_t rank, ad_xfer* xfers, uint64_t* recv_units,
+                     uint64_t* src_parts, uint32_t* flags)
+{
+    if (!table || world == 0 || rank >= world || !xfers || !recv_units || !src_parts || !flags) return AD_E_INVAL;
+    int bad = -1;
+    return x_plan(table, world, rank, xfers, recv_units, src_parts, flags, &bad);
+}
 
 int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* const* res, const int64_t* const* txn_index,
                       const uint64_t* const* dest_first, const uint64_t* txn_base, const uint64_t* n_owned,
@@ -3351,58 +3442,88 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
     for (uint32_t i = 1; i < n; ++i)
         if (x_format(ctxs[i]) != fmt)
             return ctxs[i]->fail(AD_E_STATE, "ad_exchange_local: every store needs the same id format (global dictionary on all or none)");
+    const size_t RW = AD_XROW_WORDS(n);
     const double t0 = now_ms();
-    // 1. every store exports its parts, grouped by owner
+    // 1. every store's export sizes; the bounds read back
+    std::vector<ExportArgs> ea(n);
+    std::vector<std::vector<uint64_t>> cum(n, std::vector<uint64_t>(4 * (size_t)(n + 1)));
     for (uint32_t i = 0; i < n; ++i)
     {
         ad_ctx* c = ctxs[i];
         if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
-        if (int rc = x_export(c, res[i], txn_index[i], n, dest_first[i], c->stream)) return rc;
+        if (int rc = export_sizes(c, res[i], txn_index[i], n, dest_first[i], fmt, c->stream, &ea[i])) return rc;
+        HIPCHK(c, hipMemcpyAsync(cum[i].data(), c->x_cnt.p, sizeof(uint64_t) * cum[i].size(), hipMemcpyDeviceToHost, c->stream));
+    }
+    // 2. the exchange table, as the RCCL path gathers it
+    std::vector<uint64_t> table(RW * n, 0);
+    for (uint32_t s = 0; s < n; ++s)
+    {
+        ad_ctx* c = ctxs[s];
+        if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        uint64_t* row = table.data() + RW * s;
+        for (size_t i = 0; i < 4 * (size_t)n; ++i) row[i] = cum[s][i + 4] - cum[s][i];
+        const XRowHdr h = x_row_hdr(c, fmt, 0);
+        for (uint32_t k = 0; k < AD_XROW_HDR; ++k) row[4 * n + k] = h.w[k];
+    }
+    std::vector<std::vector<ad_xfer>> xf(n, std::vector<ad_xfer>(4 * (size_t)n));
+    std::vector<std::vector<uint64_t>> src_parts(n, std::vector<uint64_t>(n));
+    std::vector<std::array<uint64_t, 4>> runits(n);
+    // 3. plan, buffers and the parts of every store
+    for (uint32_t s = 0; s < n; ++s)
+    {
+        ad_ctx* c = ctxs[s];
+        uint32_t fl = 0;
+        int bad = -1;
+        if (int rc = x_plan(table.data(), n, s, xf[s].data(), runits[s].data(), src_parts[s].data(), &fl, &bad))
+            return c->fail(rc, "ad_exchange_local: exchange table rejected (store %d)", bad);
+        uint64_t send_units[XA] = {0, 0, 0, 0};
+        for (uint32_t d = 0; d < n; ++d)
+            for (int a = 0; a < XA; ++a) send_units[a] += table[RW * s + 4 * d + a];
+        if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+        if (int rc = x_grow(c, send_units, runits[s].data(), fmt)) return rc;
+        if (int rc = x_emit(c, ea[s], c->stream)) return rc;
+    }
+    for (uint32_t s = 0; s < n; ++s)
+    {
+        if (hipSetDevice(ctxs[s]->device) != hipSuccess) return ctxs[s]->fail(AD_E_DEVICE, "hipSetDevice");
+        HIPCHK(ctxs[s], hipStreamSynchronize(ctxs[s]->stream));
     }
     const double t1 = now_ms();
     uint64_t moved = 0;
-    // 2. each owner gathers what every store exported for it (slice order), device to device
+    // 4. each owner gathers what every store exported for it (slice order), device to device
     for (uint32_t d = 0; d < n; ++d)
     {
         ad_ctx* o = ctxs[d];
         if (hipSetDevice(o->device) != hipSuccess) return o->fail(AD_E_DEVICE, "hipSetDevice");
-        uint64_t tot[XA] = {0, 0, 0, 0};
-        for (uint32_t s = 0; s < n; ++s)
-            for (int a = 0; a < XA; ++a) tot[a] += ctxs[s]->x_dest_counts[4 * d + a];
-        if (int rc = x_recv_ensure(o, tot, fmt)) return rc;
-        uint64_t dst_off[XA] = {0, 0, 0, 0};
         for (uint32_t s = 0; s < n; ++s)
         {
             ad_ctx* c = ctxs[s];
             for (int a = 0; a < XA; ++a)
             {
-                uint64_t src_off = 0;
-                for (uint32_t e = 0; e < d; ++e) src_off += c->x_dest_counts[4 * e + a];
-                const uint64_t cnt = c->x_dest_counts[4 * d + a], ub = x_unit_bytes(a, fmt);
-                if (cnt)
-                {
-                    char* dst = x_recv(o, a)->as<char>() + ub * dst_off[a];
-                    const char* src = x_send(c, a)->as<char>() + ub * src_off;
-                    if (c->device == o->device)
-                        HIPCHK(o, hipMemcpyAsync(dst, src, ub * cnt, hipMemcpyDeviceToDevice, o->stream));
-                    else
-                        HIPCHK(o, hipMemcpyPeerAsync(dst, o->device, src, c->device, ub * cnt, o->stream));
-                    if (s != d) moved += ub * cnt;
-                }
-                dst_off[a] += cnt;
+                const ad_xfer& from = xf[s][(size_t)a * n + d];
+                const ad_xfer& to = xf[d][(size_t)a * n + s];
+                if (from.send_bytes != to.recv_bytes) return o->fail(AD_E_STATE, "ad_exchange_local: plans disagree");
+                if (!from.send_bytes) continue;
+                char* dst = x_recv(o, a)->as<char>() + to.recv_off;
+                const char* src = x_send(c, a)->as<char>() + from.send_off;
+                if (c->device == o->device)
+                    HIPCHK(o, hipMemcpyAsync(dst, src, from.send_bytes, hipMemcpyDeviceToDevice, o->stream));
+                else
+                    HIPCHK(o, hipMemcpyPeerAsync(dst, o->device, src, c->device, from.send_bytes, o->stream));
+                if (s != d) moved += from.send_bytes;
             }
         }
     }
     const double t2 = now_ms();
-    // 3. K3 on every owner
+    // 5. K3 on every owner
     double ms_merge = 0;
     for (uint32_t d = 0; d < n; ++d)
     {
         ad_ctx* o = ctxs[d];
         if (hipSetDevice(o->device) != hipSuccess) return o->fail(AD_E_DEVICE, "hipSetDevice");
-        std::vector<uint64_t> src_parts(n);
-        for (uint32_t s = 0; s < n; ++s) src_parts[s] = ctxs[s]->x_dest_counts[4 * d + 0];
-        if (int rc = x_merge(o, n, src_parts.data(), txn_base[d], n_owned[d], o->stream, &out[d])) return rc;
+        if (int rc = x_merge(o, n, src_parts[d].data(), runits[d].data(), fmt, txn_base[d], n_owned[d], o->stream, &out[d]))
+            return rc;
         ms_merge += out[d].ms_device;
     }
     if (stats)
@@ -3431,6 +3552,19 @@ int ad_comm_init(ad_ctx* c, const uint8_t* id, int rank, int world)
     if (!c || !id || world <= 0 || rank < 0 || rank >= world) return AD_E_INVAL;
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
+    // the exchange table lives as long as the communicator: a step never allocates before the collective
+    const size_t RW = AD_XROW_WORDS(world), words = RW * (size_t)(world + 1) + 2 * (size_t)world + 2;
+    if (!c->xc_dev.ensure(sizeof(uint64_t) * words)) return c->fail(AD_E_NOMEM, "exchange table");
+    if (c->h_xtab_words < words)
+    {
+        if (c->h_xtab) (void)hipHostFree(c->h_xtab);
+        c->h_xtab = nullptr;
+        c->h_xtab_words = 0;
+        HIPCHK(c, hipHostMalloc((void**)&c->h_xtab, sizeof(uint64_t) * words, hipHostMallocDefault));
+        c->h_xtab_words = words;
+    }
+    for (hipEvent_t& e : c->x_ev)
+        if (!e) HIPCHK(c, hipEventCreate(&e));
     ncclUniqueId u;
     memcpy(u.internal, id, AD_COMM_ID_BYTES);
     NCCLCHK(c, ncclCommInitRank(&c->comm, world, u, rank));
@@ -3442,70 +3576,120 @@ int ad_comm_init(ad_ctx* c, const uint8_t* id, int rank, int world)
 int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, const uint64_t* dest_first, uint64_t txn_base,
                 uint64_t n_owned, void* stream, ad_merged* out, ad_exchange_stats* stats)
 {
-    if (!c || !res || !dest_first || !out) return AD_E_INVAL;
+    if (!c) return AD_E_INVAL;
     if (!c->comm) return c->fail(AD_E_STATE, "ad_exchange: no communicator (ad_comm_init)");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    const int W = c->comm_world, R = c->comm_rank;
+    const uint32_t W = (uint32_t)c->comm_world, R = (uint32_t)c->comm_rank;
     const uint32_t fmt = x_format(c);
+    const size_t RW = AD_XROW_WORDS(W);
+    uint64_t* tab = c->xc_dev.as<uint64_t>();          // [W][RW] gathered rows
+    uint64_t* mine = tab + RW * W;                      // this rank's row
+    uint64_t* sw = mine + RW;                           // growth round: own status word, then W gathered
+    uint64_t* h = c->h_xtab;
     const double t0 = now_ms();
-    // 1. export, grouped by owner rank
-    if (int rc = x_export(c, res, txn_index, (uint32_t)W, dest_first, st)) return rc;
-    const double t1 = now_ms();
-    // 2. the [W][W][4] counts table on every rank (one all-gather), read by the host to size the
-    //    receive buffers and place every source's parts
-    if (!c->xc_dev.ensure(sizeof(uint64_t) * 4 * (size_t)W * (W + 1))) return c->fail(AD_E_NOMEM, "counts table");
-    uint64_t* mine = c->xc_dev.as<uint64_t>() + 4 * (size_t)W * W;
-    HIPCHK(c, hipMemcpyAsync(mine, c->x_dest_counts.data(), sizeof(uint64_t) * 4 * W, hipMemcpyHostToDevice, st));
-    NCCLCHK(c, ncclAllGather(mine, c->xc_dev.as<uint64_t>(), 4 * (size_t)W, ncclUint64, c->comm, st));
-    std::vector<uint64_t> table(4 * (size_t)W * W);
-    HIPCHK(c, hipMemcpyAsync(table.data(), c->xc_dev.p, sizeof(uint64_t) * table.size(), hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
-    auto cnt = [&](int s, int d, int a) { return table[(size_t)4 * W * s + 4 * d + a]; };
-    uint64_t tot[XA] = {0, 0, 0, 0};
-    for (int s = 0; s < W; ++s)
-        for (int a = 0; a < XA; ++a) tot[a] += cnt(s, R, a);
-    if (int rc = x_recv_ensure(c, tot, fmt)) return rc;
-    // 3. grouped send/recv of the four arrays over RCCL (own parts: a device copy)
-    uint64_t moved = 0;
-    NCCLCHK(c, ncclGroupStart());
-    for (int a = 0; a < XA; ++a)
+    HIPCHK(c, hipEventRecord(c->x_ev[0], st));
+    // 1. export sizes -> this rank's row of the table, on the device. A failure here is published in
+    //    the row (status), so the peers learn of it from the all-gather instead of waiting for parts.
+    ExportArgs ea{};
+    int own = !res || !out || !dest_first ? c->fail(AD_E_INVAL, "ad_exchange: res, dest_first and out are required")
+                                          : export_sizes(c, res, txn_index, W, dest_first, fmt, st, &ea);
+    if (own == AD_OK && run_x_row(c->x_cnt.as<uint64_t>(), W, x_row_hdr(c, fmt, 0), mine, st) != hipSuccess)
+        own = c->fail(AD_E_DEVICE, "exchange table row");
+    if (own != AD_OK)
     {
-        const size_t ub = x_unit_bytes(a, fmt);
-        uint64_t soff = 0, roff = 0;
-        for (int p = 0; p < W; ++p)
-        {
-            const uint64_t sc = cnt(R, p, a), rcv = cnt(p, R, a);
-            const char* sp = x_send(c, a)->as<char>() + ub * soff;
-            char* rp = x_recv(c, a)->as<char>() + ub * roff;
-            if (p == R)
-            {
-                if (sc) HIPCHK(c, hipMemcpyAsync(rp, sp, ub * sc, hipMemcpyDeviceToDevice, st));
-            }
-            else
-            {
-                // bytes as uint8 (every array is a whole number of bytes; no reduction)
-                if (sc) NCCLCHK(c, ncclSend(sp, ub * sc, ncclUint8, p, c->comm, st));
-                if (rcv) NCCLCHK(c, ncclRecv(rp, ub * rcv, ncclUint8, p, c->comm, st));
-                moved += ub * sc;
-            }
-            soff += sc;
-            roff += rcv;
-        }
+        const std::string why = c->err;
+        const XRowHdr hd = x_row_hdr(c, fmt, own);
+        memset(h, 0, sizeof(uint64_t) * RW);
+        memcpy(h + 4 * W, hd.w, sizeof(hd.w));
+        if (hipMemcpy(mine, h, sizeof(uint64_t) * RW, hipMemcpyHostToDevice) != hipSuccess)
+            return x_abort(c, own);
+        c->err = why;
     }
-    NCCLCHK(c, ncclGroupEnd());
+    // 2. the table: one all-gather of the rows, read back -- the step's planning synchronisation
+    ncclResult_t nr = ncclAllGather(mine, tab, RW, ncclUint64, c->comm, st);
+    if (nr != ncclSuccess) return x_abort(c, own ? own : nccl_fail(c, nr, "ncclAllGather (exchange table)"));
+    HIPCHK(c, hipMemcpyAsync(h, tab, sizeof(uint64_t) * RW * W, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    const double t2 = now_ms();
-    // 4. K3 over the parts of every source (rank = slice order)
+    // 3. the plan, identical on every rank: a failed or inconsistent rank fails every rank here
+    std::vector<ad_xfer> xf(4 * (size_t)W);
     std::vector<uint64_t> src_parts(W);
-    for (int s = 0; s < W; ++s) src_parts[s] = cnt(s, R, 0);
-    if (int rc = x_merge(c, (uint32_t)W, src_parts.data(), txn_base, n_owned, st, out)) return rc;
+    uint64_t runits[XA];
+    uint32_t flags = 0;
+    int bad = -1;
+    if (int rc = x_plan(h, W, R, xf.data(), runits, src_parts.data(), &flags, &bad))
+    {
+        if (own) return own;
+        if (rc == AD_E_PEER)
+            return c->fail(AD_E_PEER, "ad_exchange: rank %d failed before the move (code -%llu)", bad,
+                           (unsigned long long)h[RW * bad + 4 * W + 2]);
+        if (rc == AD_E_STATE)
+            return c->fail(AD_E_STATE, "ad_exchange: ranks use different id formats (rank %d: %s, rank 0: %s; the global "
+                                       "dictionary must be installed on all or none)", bad,
+                           h[RW * bad + 4 * W + 1] == AD_IDS_RANK ? "ranks" : "triplets",
+                           h[4 * W + 1] == AD_IDS_RANK ? "ranks" : "triplets");
+        return c->fail(rc, "ad_exchange: malformed exchange table (row of rank %d)", bad);
+    }
+    uint64_t send_units[XA] = {0, 0, 0, 0};
+    for (uint32_t d = 0; d < W; ++d)
+        for (int a = 0; a < XA; ++a) send_units[a] += h[RW * R + 4 * d + a];
+    // 4. growth round, taken by every rank when any rank's buffers are short: each grows its own, then a
+    //    one-word status all-gather tells all of them whether every rank can go on
+    if (flags & AD_XPLAN_GROW)
+    {
+        const int g = x_grow(c, send_units, runits, fmt);
+        uint64_t* hs = h + RW * W;
+        hs[0] = g ? (uint64_t)(-(int64_t)g) : 0;
+        if (hipMemcpy(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
+        nr = ncclAllGather(sw, sw + 1, 1, ncclUint64, c->comm, st);
+        if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclAllGather (exchange status)"));
+        HIPCHK(c, hipMemcpyAsync(hs + 1, sw + 1, sizeof(uint64_t) * W, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (g) return g;
+        for (uint32_t s = 0; s < W; ++s)
+            if (hs[1 + s]) return c->fail(AD_E_PEER, "ad_exchange: rank %u could not grow its exchange buffers", s);
+    }
+    // 5. this rank's parts, grouped by owner, into its send buffers
+    if (int rc = x_emit(c, ea, st)) return x_abort(c, rc);
+    if (hipEventRecord(c->x_ev[1], st) != hipSuccess) return x_abort(c, c->fail(AD_E_DEVICE, "hipEventRecord"));
+    // 6. grouped send/recv of the four arrays (own parts: a device copy). The group is always closed;
+    //    a failure inside it aborts the communicator.
+    uint64_t moved = 0;
+    hipError_t he = hipSuccess;
+    for (int a = 0; a < XA && he == hipSuccess; ++a)
+    {
+        const ad_xfer& x = xf[(size_t)a * W + R];
+        if (x.send_bytes)
+            he = hipMemcpyAsync(x_recv(c, a)->as<char>() + x.recv_off, x_send(c, a)->as<char>() + x.send_off, x.send_bytes,
+                                hipMemcpyDeviceToDevice, st);
+    }
+    if (he != hipSuccess) return x_abort(c, c->fail(AD_E_DEVICE, "exchange self copy: %s", hipGetErrorString(he)));
+    nr = ncclGroupStart();
+    if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclGroupStart"));
+    for (int a = 0; a < XA && nr == ncclSuccess; ++a)
+        for (uint32_t p = 0; p < W && nr == ncclSuccess; ++p)
+        {
+            if (p == R) continue;
+            const ad_xfer& x = xf[(size_t)a * W + p];
+            // bytes as uint8 (every array is a whole number of bytes; no reduction)
+            if (x.send_bytes) nr = ncclSend(x_send(c, a)->as<char>() + x.send_off, x.send_bytes, ncclUint8, (int)p, c->comm, st);
+            if (nr == ncclSuccess && x.recv_bytes)
+                nr = ncclRecv(x_recv(c, a)->as<char>() + x.recv_off, x.recv_bytes, ncclUint8, (int)p, c->comm, st);
+            moved += x.send_bytes;
+        }
+    const ncclResult_t ne = ncclGroupEnd();
+    if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclSend/ncclRecv"));
+    if (ne != ncclSuccess) return x_abort(c, nccl_fail(c, ne, "ncclGroupEnd"));
+    if (hipEventRecord(c->x_ev[2], st) != hipSuccess) return x_abort(c, c->fail(AD_E_DEVICE, "hipEventRecord"));
+    // 7. K3 over the parts of every source (rank = slice order); its completion is the step's second
+    //    (and last) synchronisation
+    if (int rc = x_merge(c, W, src_parts.data(), runits, fmt, txn_base, n_owned, st, out)) return rc;
     if (stats)
     {
         memset(stats, 0, sizeof(*stats));
         stats->bytes_moved = moved;
-        stats->ms_export = t1 - t0;
-        stats->ms_move = t2 - t1;
+        stats->ms_export = ev_ms(c->x_ev[0], c->x_ev[1]);     // sizes, table, plan, parts
+        stats->ms_move = ev_ms(c->x_ev[1], c->x_ev[2]);
         stats->ms_merge = out->ms_device;
         stats->ms_total = now_ms() - t0;
     }

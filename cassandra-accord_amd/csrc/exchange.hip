@@ -296,6 +296,15 @@ __global__ void k_export_bounds(ExportArgs a, const uint64_t* dest_first, uint32
     counts[4 * d + 3] = b.KO;
 }
 
+// This rank's row of the exchange table (accord_deps.h, ad_exchange_plan): per destination the units of
+// each array (differences of the cumulative bounds k_export_bounds wrote), then the row header.
+__global__ void k_x_row(const uint64_t* counts, uint32_t n_dest, XRowHdr h, uint64_t* row)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 4 * n_dest) row[i] = counts[i + 4] - counts[i];
+    else if (i < 4 * n_dest + XROW_HDR) row[i] = h.w[i - 4 * n_dest];
+}
+
 // ---------------------------------------------------------------------------------------
 // merge (K3)
 // ---------------------------------------------------------------------------------------
@@ -1791,6 +1800,13 @@ hipError_t run_export_bounds(const ExportArgs& a, const uint64_t* dest_first, ui
                              hipStream_t st)
 {
     k_export_bounds<<<(n_dest + 1 + 63) / 64, 64, 0, st>>>(a, dest_first, n_dest, counts);
+    return hipGetLastError();
+}
+
+hipError_t run_x_row(const uint64_t* counts, uint32_t n_dest, const XRowHdr& h, uint64_t* row, hipStream_t st)
+{
+    const uint32_t n = 4 * n_dest + XROW_HDR;
+    k_x_row<<<(n + 63) / 64, 64, 0, st>>>(counts, n_dest, h, row);
     return hipGetLastError();
 }
 

@@ -57,6 +57,11 @@ hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st);
 hipError_t run_export_emit(const ExportArgs& a, hipStream_t st);
 hipError_t run_export_bounds(const ExportArgs& a, const uint64_t* dest_first, uint32_t n_dest, uint64_t* counts,
                              hipStream_t st);
+// the exchange table row of this rank (ad_exchange_plan's layout): counts = k_export_bounds' cumulative
+// [n_dest + 1][4], header words after the n_dest x 4 per-destination units
+constexpr uint32_t XROW_HDR = 12;
+struct XRowHdr { uint64_t w[XROW_HDR]; };
+hipError_t run_x_row(const uint64_t* counts, uint32_t n_dest, const XRowHdr& h, uint64_t* row, hipStream_t st);
 hipError_t run_merge_prepare(const MergeArgs& a, hipStream_t st);
 hipError_t run_merge_slots(const MergeArgs& a, hipStream_t st);
 hipError_t run_merge_count(const MergeArgs& a, hipStream_t st);

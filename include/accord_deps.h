@@ -63,6 +63,7 @@ extern "C" {
 #define AD_E_STATE            -8  /* reference would throw (e.g. prunedBefore walk off end) */
 #define AD_E_CAPACITY         -9  /* id dictionary exceeds 2^28 entries                     */
 #define AD_E_SPACE           -10  /* a caller-provided output buffer is too small (sizes set) */
+#define AD_E_PEER            -11  /* another rank of an exchange step reported a failure     */
 
 /* ---- InternalStatus ordinals (CommandsForKey.java:493-501) -------------------------- */
 #define AD_ST_TRANSITIVELY_KNOWN                          0
@@ -367,11 +368,44 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
 #define AD_COMM_ID_BYTES 128
 int ad_comm_unique_id(uint8_t* id /* [AD_COMM_ID_BYTES] */);
 int ad_comm_init(ad_ctx* ctx, const uint8_t* id, int rank, int world);
-/* This rank's step: export, RCCL all-gather of the part counts, grouped send/recv of the parts over
- * xGMI, K3 merge of the requests [txn_base, txn_base + n_owned) this rank owns. dest_first: host,
- * world + 1 entries. Enqueued on `stream` (NULL: the ctx stream), complete on return. */
+/* This rank's step: export sizes, RCCL all-gather of the exchange table (below), grouped send/recv of
+ * the parts over xGMI, K3 merge of the requests [txn_base, txn_base + n_owned) this rank owns.
+ * dest_first: host, world + 1 entries. Enqueued on `stream` (NULL: the ctx stream), complete on return.
+ * One host synchronisation plans the move (the table read back), one completes the merge; a step that
+ * grows some rank's buffers adds a one-word status all-gather. Failure is collective: a rank whose
+ * export fails still joins the table all-gather with its status, and every rank then returns (its own
+ * code, or AD_E_PEER). An error after the table is agreed aborts the communicator (ncclCommAbort; the
+ * next ad_exchange returns AD_E_STATE until ad_comm_init), so a failing rank exits instead of waiting. */
 int ad_exchange(ad_ctx* ctx, const ad_deps_result* res_dev, const int64_t* txn_index_dev, const uint64_t* dest_first,
                 uint64_t txn_base, uint64_t n_owned, void* stream, ad_merged* out, ad_exchange_stats* stats);
+
+/* ---- exchange plan: where every transfer of a step starts and ends ---------------------------
+ * Shared by ad_exchange and ad_exchange_local, exported for hosts that move the parts with a
+ * transport of their own. Pure host code (no device call).
+ * Exchange table: one row per rank s (slice order) of `world`, AD_XROW_WORDS(world) uint64 each:
+ *   row[4 d + a]     units of array a (0 parts, 1 key words, 2 ids, 3 k2t ints) that s sends to rank d,
+ *                    in s's send buffers grouped by destination (the order ad_parts_export writes)
+ *   row[4 W + 0]     AD_XROW_MAGIC
+ *   row[4 W + 1]     s's id format (AD_IDS_*): every rank must use the same one (else AD_E_STATE)
+ *   row[4 W + 2]     status: 0, or -(AD_E_* code) of s's failure before the move (then AD_E_PEER)
+ *   row[4 W + 3]     reserved, 0
+ *   row[4 W + 4 + a] capacity of s's send buffer of array a, in units
+ *   row[4 W + 8 + a] capacity of s's receive buffer of array a, in units
+ * Output for `rank`: xfers[a * world + p] = bytes to send to / receive from peer p (offsets into this
+ * rank's send / receive buffer of array a; receive side in source order, so K3 sees slice order);
+ * recv_units[a] = units this rank receives; src_parts[p] = parts from peer p (ad_parts_merge's
+ * src_parts); flags: AD_XPLAN_GROW if any rank's buffers are too small for the step (every rank can
+ * tell, so all take the same growth round). Every rank computes the same verdict from the same table. */
+#define AD_XROW_HDR 12
+#define AD_XROW_WORDS(world) (4u * (uint32_t)(world) + AD_XROW_HDR)
+#define AD_XROW_MAGIC 0x41445852ull        /* "ADXR" */
+#define AD_XPLAN_GROW 1u
+typedef struct ad_xfer {
+    uint64_t send_off, send_bytes;   /* this rank's send buffer: the run going to the peer        */
+    uint64_t recv_off, recv_bytes;   /* this rank's receive buffer: the run coming from the peer  */
+} ad_xfer;
+int ad_exchange_plan(const uint64_t* table, uint32_t world, uint32_t rank, ad_xfer* xfers /* [4 * world] */,
+                     uint64_t* recv_units /* [4] */, uint64_t* src_parts /* [world] */, uint32_t* flags);
 
 /* Copy device memory owned by the library (results) into a host buffer: for hosts without a
  * HIP binding of their own (the Panama FFM wrapper). */

@@ -316,3 +316,67 @@ def test_config3_shards_exchange_local(world):
     assert stats["bytes_moved"] > 0
     for st in stores:
         st.close()
+
+
+def _sample(n, head=2000, spread=2000, seed=7):
+    rng = np.random.default_rng(seed)
+    return np.unique(np.concatenate([np.arange(min(n, head)), rng.choice(n, min(n, spread), replace=False)]))
+
+
+def test_node_exchange_config3_share_full(oracle):
+    # bench.py's multi-GPU step at full size on one GPU: rank 0's whole config-3 share (1/8 of BASELINE
+    # config 3: 2M requests, 8M probes over a 24M-entry store) through NodeExchange -- the library's RCCL
+    # communicator (ad_comm_init, world 1), ad_exchange (sizes -> table all-gather -> plan -> parts ->
+    # grouped send/recv -> K3) -- sampled bit-exact against the reference path over the same store
+    dev = torch.device("cuda", 0)
+    w, idx, n_total, exec_ids = synth.config3_shard(0, 1)
+    st = native.DeviceCommandStore(0, 0, 1, w.slices)
+    try:
+        st.load(w, prepare=False)
+        st.set_global_dict(synth.config3_global_dict(w.params, [exec_ids]))
+        qdev, keep = native.device_queries(w.queries, dev)
+        nx = exchange.NodeExchange(st, qdev, idx, n_total, 0, 1, dev)
+        mg = nx.step()                            # grows the exchange buffers (growth round)
+        mg = nx.step()                            # steady step on the grown buffers
+        assert mg.n_txns == n_total and nx.last_exchange["bytes_moved"] == 0     # world 1: all self copies
+        sample = _sample(n_total)
+        got = st.merged_to_host(mg, sample)
+        exp = oracle.OracleStore(w.range_start_inclusive, 1, w.slices).load(w).deps_batch(w.queries.take(sample), w.flags)
+        ok, why = got.equals(exp, detail=True)
+        if not ok:
+            mm = got.first_mismatch(exp)
+            raise AssertionError("%s; first mismatch %r" % (why, mm[:2] if mm else None))
+        # a rank whose export fails publishes its status in the table: the step fails on every rank
+        # before the move, the communicator survives and the next step is whole again
+        bad = list(nx.dest_first)
+        bad[-1] += 1
+        with pytest.raises(native.AccordDepsError) as ei:
+            st.exchange(nx.last_res, nx.ti.data_ptr(), bad, nx.txn_base, nx.n_owned)
+        assert ei.value.code == A.AD_E_INVAL
+        mg = nx.step()
+        ok, why = st.merged_to_host(mg, sample).equals(exp, detail=True)
+        assert ok, why
+    finally:
+        st.close()
+
+
+def test_node_exchange_small_triplets_and_ranks(oracle):
+    # the same step over a small store in both id formats (the global dictionary installed or not)
+    dev = torch.device("cuda", 0)
+    w = synth.config3(n_txns=20000, n_keys=3000, seed=17)
+    exp = pyoracle.resolve(w)
+    for rank_ids in (False, True):
+        st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+        try:
+            st.load(w)
+            if rank_ids:
+                st.set_global_dict(st.dictionary())
+            qdev, keep = native.device_queries(w.queries, dev)
+            nx = exchange.NodeExchange(st, qdev, np.arange(len(w.queries)), len(w.queries), 0, 1, dev)
+            for _ in range(2):
+                mg = nx.step()
+                assert mg.id_format == (A.AD_IDS_RANK if rank_ids else A.AD_IDS_TRIPLET)
+                ok, why = st.merged_to_host(mg).equals(exp, detail=True)
+                assert ok, (rank_ids, why)
+        finally:
+            st.close()

@@ -208,3 +208,17 @@ def test_errors():
     with pytest.raises(native.AccordDepsError) as e:
         st.calculate_partial_deps(bad)
     assert e.value.code == A.AD_E_INVAL
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ephemeral_reads_at_timestamp_max(oracle, seed):
+    # GetEphemeralReadDeps (GetEphemeralReadDeps.java:76): executeAt = Timestamp.MAX -- a request above
+    # every id of the store, on the lean path (no range commands) and the general one (with them)
+    base = synth.random_small(700 + seed, n_keys=200, n_hist_txns=2000, n_txns=500, max_keys=8,
+                              n_range_cmds=0 if seed % 2 else 100, n_redundant=0 if seed % 2 else 4)
+    _compare(synth.with_ephemeral_reads(base, frac=0.5, seed=seed), oracle)
+
+
+def test_ephemeral_reads_config2_scaled(oracle):
+    w = synth.with_ephemeral_reads(synth.config2(n_txns=20000, n_keys=20000, n_hist_entries=200000), frac=0.3)
+    _compare(w, oracle, paths=(0,))

@@ -202,6 +202,23 @@ def test_crosscheck_python_restatement(oracle, seed):
             assert got[m] == (keys, vals, k2t), (seed, i, A.MAP_NAMES[m])
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_crosscheck_ephemeral_reads_at_timestamp_max(oracle, seed):
+    # GetEphemeralReadDeps.apply computes deps at executeAt = Timestamp.MAX (GetEphemeralReadDeps.java:76,
+    # Timestamp.java:29): every witnessed Write of the key started before MAX, elision below the key's
+    # last committed Write; the id's flag bits read as kind 7
+    w = synth.with_ephemeral_reads(synth.random_small(300 + seed, with_slices=(seed % 3 == 2)), frac=0.5, seed=seed)
+    batch = oracle.resolve(w)
+    n_eph = 0
+    for i in range(len(w.queries)):
+        n_eph += int(w.queries.exec.msb[i]) == synth.TIMESTAMP_MAX[0]
+        kd, rd, dd = refmodel.request_pairs(w, i)
+        got = _request(batch, i)
+        for m, pairs in ((0, kd), (1, rd), (2, dd)):
+            assert got[m] == refmodel.csr(pairs), (seed, i, A.MAP_NAMES[m])
+    assert n_eph > 0
+
+
 def test_crosscheck_no_elision(oracle):
     w = synth.random_small(77)
     batch = oracle.resolve(w, elide=0)
