@@ -26,7 +26,8 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_recovery_batch_device", "ad_cfk_update", "ad_cfk_update_device", "ad_cfk_entries",
            "ad_cfk_ballots_load", "ad_cfk_ballots",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange", "ad_exchange_plan",
-           "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing")
+           "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing",
+           "ad_cfk_load_pruned")
 
 
 class AccordDepsError(RuntimeError):
@@ -113,6 +114,7 @@ def lib():
                                   C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.ad_cfk_missing.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ad_cfk_load_pruned.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)] + [C.POINTER(C.c_void_p)] * 5
         L.ad_check_snapshot.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _lib = L
     return _lib
@@ -279,6 +281,18 @@ class DeviceCommandStore:
         off = _view(po, ne.value + 1, np.uint64).copy()
         nm = int(off[-1]) if len(off) else 0
         return off, Tids(_view(pm, nm, np.uint64).copy(), _view(pl, nm, np.uint64).copy(), _view(pn, nm, np.int32).copy())
+
+    def cfk_load_pruned(self):
+        """LoadPruned requests of the last update batch (ad_cfk_load_pruned): [(update index, key,
+        (msb, lsb, node))] in batch order."""
+        n = C.c_uint64()
+        pu, pk, pm, pl, pn = (C.c_void_p() for _ in range(5))
+        self._check(lib().ad_cfk_load_pruned(self.h, C.byref(n), C.byref(pu), C.byref(pk), C.byref(pm), C.byref(pl),
+                                             C.byref(pn)))
+        m = n.value
+        u, k = _view(pu, m, np.uint64), _view(pk, m, np.int64)
+        ms, ls, ns = _view(pm, m, np.uint64), _view(pl, m, np.uint64), _view(pn, m, np.int32)
+        return [(int(u[j]), int(k[j]), (int(ms[j]), int(ls[j]), int(ns[j]))) for j in range(m)]
 
     def cfk_byid(self):
         """(keys, seg, txnIds (Tids), prunedBefore indices) of the store's CommandsForKeys as they stand."""

@@ -308,6 +308,10 @@ struct ad_ctx {
     std::vector<int32_t> y_node;
     std::vector<int64_t> y_pruned;
     std::vector<uint64_t> z_off;
+    // LoadPruned requests of the last update batch (ad_cfk_load_pruned)
+    std::vector<uint64_t> lp_upd, lp_msb, lp_lsb;
+    std::vector<int64_t> lp_keys;
+    std::vector<int32_t> lp_node;
 
     int fail(int code, const char* fmt, ...)
     {
@@ -3071,7 +3075,18 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
     miss.ctx = c;
     miss.spare = cfk_miss_spare;
     miss.swap = cfk_miss_swap;
+    c->lp_upd.clear(); c->lp_keys.clear(); c->lp_msb.clear(); c->lp_lsb.clear(); c->lp_node.clear();
     const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e, &miss);
+    if (rc == AD_OK && o.n_load_pruned)
+    {
+        const uint64_t m = o.n_load_pruned;
+        c->lp_upd.resize(m); c->lp_keys.resize(m); c->lp_msb.resize(m); c->lp_lsb.resize(m); c->lp_node.resize(m);
+        HIPCHK(c, hipMemcpy(c->lp_upd.data(), o.lp_update, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(c->lp_keys.data(), o.lp_keys, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(c->lp_msb.data(), o.lp_msb, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(c->lp_lsb.data(), o.lp_lsb, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(c->lp_node.data(), o.lp_node, 4 * m, hipMemcpyDeviceToHost));
+    }
     if (o.n_new_keys)
     {
         // keys created on the device (they stay when the batch then failed): KeyLines, host copies
@@ -3150,6 +3165,8 @@ static int check_update_soa(ad_ctx* c, const ad_cfk_update_soa* u)
         return c->fail(AD_E_INVAL, "update batch with null arrays");
     if (u->dep_off && (!u->dep_msb || !u->dep_lsb || !u->dep_node))
         return c->fail(AD_E_INVAL, "update batch with dep_off but null dep arrays");
+    if ((u->ballot_msb != nullptr) != (u->ballot_lsb != nullptr) || (u->ballot_msb != nullptr) != (u->ballot_node != nullptr))
+        return c->fail(AD_E_INVAL, "update batch ballots: ballot_msb, ballot_lsb and ballot_node must be all set or all NULL");
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     return 0;
@@ -3216,6 +3233,19 @@ int ad_cfk_entries(ad_ctx* c, uint64_t* n_entries, const uint8_t** status, const
     *exec_msb = c->x_msb.data();
     *exec_lsb = c->x_lsb.data();
     *exec_node = c->x_node.data();
+    return AD_OK;
+}
+
+int ad_cfk_load_pruned(ad_ctx* c, uint64_t* n, const uint64_t** update, const int64_t** keys, const uint64_t** msb,
+                       const uint64_t** lsb, const int32_t** node)
+{
+    if (!c || !n || !update || !keys || !msb || !lsb || !node) return AD_E_INVAL;
+    *n = c->lp_upd.size();
+    *update = c->lp_upd.data();
+    *keys = c->lp_keys.data();
+    *msb = c->lp_msb.data();
+    *lsb = c->lp_lsb.data();
+    *node = c->lp_node.data();
     return AD_OK;
 }
 

@@ -166,7 +166,7 @@ __device__ inline uint32_t known_rank(const DevSnapshot& s, const DictSample& ds
 __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds, CfkDevState d, CfkUpdIn u, uint32_t* loc,
                                                     uint32_t* xr_out, unsigned long long* word, uint64_t* ins_key,
                                                     uint32_t* flags, const uint32_t* rk, const uint64_t* mpos, uint64_t U,
-                                                    UpdCtl* ctl, int fold)
+                                                    UpdCtl* ctl, int fold, uint32_t* trk)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= u.n) return;
@@ -214,6 +214,14 @@ __global__ __launch_bounds__(256) void k_upd_locate(DevSnapshot s, DictSample ds
     }
     if ((tl & 1) && tau_of(st, (uint32_t)((tl >> 1) & 7), xr) != 0) { upd_fail(ctl, UE_DOMAIN, (uint32_t)i); return; }
     xr_out[i] = xr;
+    if (trk)
+    {
+        // for the additions past byId's end (k_past_*): key index, the key's last txnId before the
+        // batch, this update's txnId
+        trk[3 * i + 0] = k;
+        trk[3 * i + 1] = kr.last_txn;
+        trk[3 * i + 2] = r;
+    }
     if (!present)
     {
         ins_key[i] = ((uint64_t)k << 32) | r;
@@ -312,17 +320,130 @@ __device__ inline bool upd_with_deps(const CfkUpdIn& u, const uint8_t* uapp, uin
     return (uapp[i] & 1) && st_has_exec(u.status[i]) && !(u.txn_lsb[i] & 1);
 }
 
-// additions (:210-263): the deps of applied updates with deps statuses that their kind witnesses,
-// at or above the key's prunedBefore (removePrunedAdditions, Utils.java:229-246) and not in byId
-// after the batch -> TRANSITIVELY_KNOWN insertions. Pass 0 counts per update, pass 1 writes.
-template <int WRITE>
-__global__ __launch_bounds__(256) void k_add_deps(DevSnapshot s, CfkUpdIn u, const uint8_t* uapp, const uint32_t* drank,
-                                                  uint32_t* cnt, const uint64_t* off, int64_t* ak, uint64_t* atm,
-                                                  uint64_t* atl, int32_t* atn)
+// The key's last txnId in byId as update i sees it in the sequential Java (Updating.java:210-263 walks
+// byId as it stands when update i runs): the last before the batch, raised by every earlier update of
+// the batch on the key -- its txnId (now in byId) and, for an applied update with deps, its largest dep
+// (a dep above the last id is added, :253-262). Per update: sort key (key index << 32 | batch index),
+// value v_i; an exclusive max-scan of (key index << 32 | v) over that order is a segmented max-scan
+// (segments ascend), so its low word is the max of v over the earlier updates of the same key.
+__global__ void k_past_keys(CfkUpdIn u, const uint8_t* uapp, const uint32_t* trk, const uint32_t* drank, uint64_t* sk,
+                            uint32_t* sv, uint32_t* vv)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= u.n) return;
-    uint32_t c = 0;
+    uint32_t v = trk[3 * i + 2];
+    if (upd_with_deps(u, uapp, i))
+        for (uint64_t j = u.dep_off[i]; j < u.dep_off[i + 1]; ++j) v = max(v, drank[j]);
+    sk[i] = ((uint64_t)trk[3 * i] << 32) | i;
+    sv[i] = (uint32_t)i;
+    vv[i] = v;
+}
+
+__global__ void k_past_words(uint64_t n, const uint64_t* sk, const uint32_t* sv, const uint32_t* vv, uint64_t* wd)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) wd[p] = (sk[p] & 0xFFFFFFFF00000000ull) | vv[sv[p]];
+}
+
+__global__ void k_past_last(uint64_t n, const uint64_t* sk, const uint32_t* sv, const uint64_t* ex, const uint32_t* trk,
+                            uint32_t* last)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t i = sv[p];
+    const uint32_t earlier = (ex[p] >> 32) == (sk[p] >> 32) ? (uint32_t)ex[p] : 0u;
+    last[i] = max(trk[3 * (uint64_t)i + 1], earlier);
+}
+
+// exclusive prefix max of u64 words (identity 0): per-1024 maxima, their scan (one block), the apply
+__global__ __launch_bounds__(256) void k_maxscan_blocks(const uint64_t* in, uint64_t n, uint64_t* bmax)
+{
+    __shared__ uint64_t red[256];
+    const uint64_t b0 = (uint64_t)blockIdx.x * 1024;
+    uint64_t m = 0;
+    for (uint32_t k = threadIdx.x; k < 1024; k += 256)
+        if (b0 + k < n) m = max(m, in[b0 + k]);
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (uint32_t w = 128; w; w >>= 1)
+    {
+        if (threadIdx.x < w) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (!threadIdx.x) bmax[blockIdx.x] = red[0];
+}
+
+__device__ inline uint64_t block_excl_max256(uint64_t v, uint64_t* sh)
+{
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < 256; d <<= 1)
+    {
+        const uint64_t o = threadIdx.x >= d ? sh[threadIdx.x - d] : 0;
+        __syncthreads();
+        sh[threadIdx.x] = max(sh[threadIdx.x], o);
+        __syncthreads();
+    }
+    const uint64_t ex = threadIdx.x ? sh[threadIdx.x - 1] : 0;
+    __syncthreads();
+    return ex;
+}
+
+__global__ __launch_bounds__(256) void k_maxscan_top(uint64_t* bmax, uint64_t nb)
+{
+    __shared__ uint64_t sh[256];
+    uint64_t carry = 0;
+    for (uint64_t c = 0; c < nb; c += 256)
+    {
+        const uint64_t i = c + threadIdx.x;
+        const uint64_t v = i < nb ? bmax[i] : 0;
+        const uint64_t ex = max(carry, block_excl_max256(v, sh));
+        if (i < nb) bmax[i] = ex;
+        sh[threadIdx.x] = max(ex, v);
+        __syncthreads();
+        carry = sh[255];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_maxscan_apply(const uint64_t* in, uint64_t n, const uint64_t* bex, uint64_t* out)
+{
+    __shared__ uint64_t sh[256];
+    const uint64_t b0 = (uint64_t)blockIdx.x * 1024 + 4ull * threadIdx.x;
+    uint64_t v[4], run = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+    {
+        v[k] = b0 + k < n ? in[b0 + k] : 0;
+        run = max(run, v[k]);
+    }
+    uint64_t ex = max(bex[blockIdx.x], block_excl_max256(run, sh));
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+    {
+        if (b0 + k < n) out[b0 + k] = ex;
+        ex = max(ex, v[k]);
+    }
+}
+
+// additions (:210-263): the deps of applied updates with deps statuses -- those their kind witnesses,
+// and every dep above the key's last txnId as the update sees it (`last`, :253-262: past byId's end the
+// Java adds without the witness test) -- that are not in byId after the batch -> TRANSITIVELY_KNOWN
+// insertions. Additions below the key's prunedBefore are dropped (removePrunedAdditions,
+// Utils.java:229-246) and handed back as LoadPruned (Updating.java:111-117,171: Pruning.loadPruned).
+// Pass 0 counts both per update, pass 1 writes.
+struct AddOut {
+    uint32_t* cnt; const uint64_t* off; int64_t* k; uint64_t* tm; uint64_t* tl; int32_t* tn;
+    uint32_t* pcnt; const uint64_t* poff; int64_t* pk; uint64_t* ptm; uint64_t* ptl; int32_t* ptn; uint64_t* pidx;
+};
+
+template <int WRITE>
+__global__ __launch_bounds__(256) void k_add_deps(DevSnapshot s, CfkUpdIn u, const uint8_t* uapp, const uint32_t* drank,
+                                                  const uint32_t* last, AddOut o)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u.n) return;
+    uint32_t c = 0, pc = 0;
     if (upd_with_deps(u, uapp, i))
     {
         const uint32_t k = key_index_of(s, u.keys[i]);
@@ -330,26 +451,44 @@ __global__ __launch_bounds__(256) void k_add_deps(DevSnapshot s, CfkUpdIn u, con
         {
             const KeyRec kr = s.krec[k];
             const uint32_t wk = kind_witnesses((uint32_t)((u.txn_lsb[i] >> 1) & 7));
-            uint64_t o = WRITE ? off[i] : 0;
+            const uint32_t lst = last[i];
+            uint64_t a = WRITE ? o.off[i] : 0, b = WRITE ? o.poff[i] : 0;
             for (uint64_t j = u.dep_off[i]; j < u.dep_off[i + 1]; ++j)
             {
                 const uint32_t r = drank[j];
-                if (!((wk >> (uint32_t)((u.dep_lsb[j] >> 1) & 7)) & 1u)) continue;
-                if (kr.pruned && r < kr.pruned) continue;
+                if (!((wk >> (uint32_t)((u.dep_lsb[j] >> 1) & 7)) & 1u) && r <= lst) continue;
                 if (seg_find(s, kr, r) != LOC_NONE) continue;
+                if (kr.pruned && r < kr.pruned)
+                {
+                    if (WRITE)
+                    {
+                        o.pk[b] = u.keys[i];
+                        o.ptm[b] = u.dep_msb[j];
+                        o.ptl[b] = u.dep_lsb[j];
+                        o.ptn[b] = u.dep_node[j];
+                        o.pidx[b] = i;
+                        ++b;
+                    }
+                    ++pc;
+                    continue;
+                }
                 if (WRITE)
                 {
-                    ak[o] = u.keys[i];
-                    atm[o] = u.dep_msb[j];
-                    atl[o] = u.dep_lsb[j];
-                    atn[o] = u.dep_node[j];
-                    ++o;
+                    o.k[a] = u.keys[i];
+                    o.tm[a] = u.dep_msb[j];
+                    o.tl[a] = u.dep_lsb[j];
+                    o.tn[a] = u.dep_node[j];
+                    ++a;
                 }
                 ++c;
             }
         }
     }
-    if (!WRITE) cnt[i] = c;
+    if (!WRITE)
+    {
+        o.cnt[i] = c;
+        o.pcnt[i] = pc;
+    }
 }
 
 // the entry whose TxnInfo an applied update with deps made (its last applied update): dsrc[e] = i
@@ -1256,6 +1395,8 @@ struct CfkUpdWork {
     DBuf bkb, uflag, upos, rk;
     // missing() maintenance: per update applied flags, dep ranks, additions batch, derivation
     DBuf uapp, drank, acnt, aoff, a_k, a_tm, a_tl, a_tn, a_st, dsrc, mflag, mpp, mpend, mcnt, moff;
+    // byId's last txnId as each update sees it (additions past the end) and the LoadPruned ids
+    DBuf trk, pk, pv, pk2, pv2, pvv, pw, pe, pbm, plast, lcnt, loff, l_k, l_tm, l_tl, l_tn, l_i;
     DBuf kn_a, kn_b, kv_a, kv_b, kflag, kfpos, knew, kpos;   // new keys
     // incremental committed order: the last derivation's order (entry indices), per-entry changed
     // flags (double-buffered with the entry arrays), the insertion's old -> new entry map
@@ -1828,13 +1969,15 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     const bool bm = u.bal_msb != nullptr;
     const bool fold = bm || track;
     const int nf = fold ? 2 : 1;
+    if (track) UALLOC(w->trk, 4ull * 3 * n, false);
     UALLOC(w->uflag, 4ull * 2 * n, false);
     UALLOC(w->upos, 8ull * 2 * (n + 1), false);
     UALLOC(w->bsum, 8ull * 2 * ((n + 1023) / 1024 + 8), false);
     k_upd_locate<<<blocks(n), 256, 0, st>>>(s, dsm, d, u, w->loc.as<uint32_t>(), w->xr.as<uint32_t>(),
                                             w->word.as<unsigned long long>(), w->ins_k.as<uint64_t>(),
                                             w->uflag.as<uint32_t>(), w->rk.as<uint32_t>(), out->merge_pos,
-                                            out->merged ? out->n_new_ids : 0, ctl, fold ? 1 : 0);
+                                            out->merged ? out->n_new_ids : 0, ctl, fold ? 1 : 0,
+                                            track ? w->trk.as<uint32_t>() : nullptr);
     UCHK(hipGetLastError());
     UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), n, nf, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), n, nf, ctl->tot3);
@@ -1969,22 +2112,81 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
         const DictSample ds = dsample();
         if (ndep) k_dep_rank<<<blocks(ndep), 256, 0, st>>>(s, ds, u, ndep, w->drank.as<uint32_t>());
     }
-    k_add_deps<0><<<blocks(n), 256, 0, st>>>(s, u, uapp, w->drank.as<uint32_t>(), w->acnt.as<uint32_t>(), nullptr, nullptr,
-                                             nullptr, nullptr, nullptr);
+    // byId's last txnId per update as the sequential Java sees it (k_past_*)
+    UALLOC(w->pk, 8 * n, false);
+    UALLOC(w->pv, 4 * n, false);
+    UALLOC(w->pk2, 8 * n, false);
+    UALLOC(w->pv2, 4 * n, false);
+    UALLOC(w->pvv, 4 * n, false);
+    UALLOC(w->pw, 8 * n, false);
+    UALLOC(w->pe, 8 * n, false);
+    UALLOC(w->pbm, 8 * ((n + 1023) / 1024 + 1), false);
+    UALLOC(w->plast, 4 * n, false);
+    {
+        const uint32_t* trk = w->trk.as<uint32_t>();
+        k_past_keys<<<blocks(n), 256, 0, st>>>(u, uapp, trk, w->drank.as<uint32_t>(), w->pk.as<uint64_t>(), w->pv.as<uint32_t>(),
+                                               w->pvv.as<uint32_t>());
+        uint64_t* ks = w->pk.as<uint64_t>();
+        uint32_t* vs = w->pv.as<uint32_t>();
+        uint32_t mask = 0;
+        for (uint32_t b = 0; b < bytes_of(n - 1) && b < 4; ++b) mask |= 1u << b;
+        for (uint32_t b = 0; b < bytes_of(s.n_keys ? s.n_keys - 1 : 0) && b < 4; ++b) mask |= 1u << (4 + b);
+        if (n > 1 && mask)
+        {
+            const uint64_t hist_n = radix_hist_entries(n);
+            UALLOC(w->hist, 4 * hist_n, false);
+            UALLOC(w->hoff, 8 * (hist_n + 1), false);
+            UALLOC(w->bsum, 8 * ((std::max(hist_n, n) + 1023) / 1024 + 8), false);
+            UCHK(radix_sort_pairs(ks, vs, w->pk2.as<uint64_t>(), w->pv2.as<uint32_t>(), n, mask, w->hist.as<uint32_t>(),
+                                  w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
+        }
+        const uint64_t nb = (n + 1023) / 1024;
+        k_past_words<<<blocks(n), 256, 0, st>>>(n, ks, vs, w->pvv.as<uint32_t>(), w->pw.as<uint64_t>());
+        k_maxscan_blocks<<<(unsigned)nb, 256, 0, st>>>(w->pw.as<uint64_t>(), n, w->pbm.as<uint64_t>());
+        k_maxscan_top<<<1, 256, 0, st>>>(w->pbm.as<uint64_t>(), nb);
+        k_maxscan_apply<<<(unsigned)nb, 256, 0, st>>>(w->pw.as<uint64_t>(), n, w->pbm.as<uint64_t>(), w->pe.as<uint64_t>());
+        k_past_last<<<blocks(n), 256, 0, st>>>(n, ks, vs, w->pe.as<uint64_t>(), trk, w->plast.as<uint32_t>());
+        UCHK(hipGetLastError());
+        UALLOC(w->bsum, 8 * ((n + 1023) / 1024 + 8), false);
+    }
+    UALLOC(w->lcnt, 4 * n, false);
+    UALLOC(w->loff, 8 * (n + 1), false);
+    AddOut ao{};
+    ao.cnt = w->acnt.as<uint32_t>();
+    ao.pcnt = w->lcnt.as<uint32_t>();
+    k_add_deps<0><<<blocks(n), 256, 0, st>>>(s, u, uapp, w->drank.as<uint32_t>(), w->plast.as<uint32_t>(), ao);
     UCHK(run_scan_arrays(w->acnt.as<uint32_t>(), w->aoff.as<uint64_t>(), n, 1, w->bsum.as<uint64_t>(), st));
-    uint64_t na = 0;
+    UCHK(run_scan_arrays(w->lcnt.as<uint32_t>(), w->loff.as<uint64_t>(), n, 1, w->bsum.as<uint64_t>(), st));
+    uint64_t na = 0, nl = 0;
     UCHK(hipMemcpyAsync(&na, w->aoff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipMemcpyAsync(&nl, w->loff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
+    if (na || nl)
+    {
+        UALLOC(w->a_k, 8 * std::max<uint64_t>(na, 1), false);
+        UALLOC(w->a_tm, 8 * std::max<uint64_t>(na, 1), false);
+        UALLOC(w->a_tl, 8 * std::max<uint64_t>(na, 1), false);
+        UALLOC(w->a_tn, 4 * std::max<uint64_t>(na, 1), false);
+        UALLOC(w->l_k, 8 * std::max<uint64_t>(nl, 1), false);
+        UALLOC(w->l_tm, 8 * std::max<uint64_t>(nl, 1), false);
+        UALLOC(w->l_tl, 8 * std::max<uint64_t>(nl, 1), false);
+        UALLOC(w->l_tn, 4 * std::max<uint64_t>(nl, 1), false);
+        UALLOC(w->l_i, 8 * std::max<uint64_t>(nl, 1), false);
+        AddOut wo{nullptr, w->aoff.as<uint64_t>(), w->a_k.as<int64_t>(), w->a_tm.as<uint64_t>(), w->a_tl.as<uint64_t>(),
+                  w->a_tn.as<int32_t>(), nullptr, w->loff.as<uint64_t>(), w->l_k.as<int64_t>(), w->l_tm.as<uint64_t>(),
+                  w->l_tl.as<uint64_t>(), w->l_tn.as<int32_t>(), w->l_i.as<uint64_t>()};
+        k_add_deps<1><<<blocks(n), 256, 0, st>>>(s, u, uapp, w->drank.as<uint32_t>(), w->plast.as<uint32_t>(), wo);
+        UCHK(hipGetLastError());
+    }
+    out->n_load_pruned = nl;
+    out->lp_keys = w->l_k.as<int64_t>();
+    out->lp_msb = w->l_tm.as<uint64_t>();
+    out->lp_lsb = w->l_tl.as<uint64_t>();
+    out->lp_node = w->l_tn.as<int32_t>();
+    out->lp_update = w->l_i.as<uint64_t>();
     if (na)
     {
-        UALLOC(w->a_k, 8 * na, false);
-        UALLOC(w->a_tm, 8 * na, false);
-        UALLOC(w->a_tl, 8 * na, false);
-        UALLOC(w->a_tn, 4 * na, false);
         UALLOC(w->a_st, na, false);
-        k_add_deps<1><<<blocks(n), 256, 0, st>>>(s, u, uapp, w->drank.as<uint32_t>(), nullptr, w->aoff.as<uint64_t>(),
-                                                 w->a_k.as<int64_t>(), w->a_tm.as<uint64_t>(), w->a_tl.as<uint64_t>(),
-                                                 w->a_tn.as<int32_t>());
         UCHK(hipMemsetAsync(w->a_st.p, AD_ST_TRANSITIVELY_KNOWN, na, st));
         UCHK(hipGetLastError());
         CfkUpdIn ua{na, w->a_k.as<int64_t>(), w->a_tm.as<uint64_t>(), w->a_tl.as<uint64_t>(), w->a_tn.as<int32_t>(),

@@ -127,6 +127,15 @@ struct CfkUpdOut {
     const uint64_t* key_pos = nullptr;
     bool rolled_back = false;      // the batch failed after it had been applied and was undone
     uint64_t n_additions = 0;      // TRANSITIVELY_KNOWN entries inserted from deps (Updating.java:235-263)
+    // additions below their key's prunedBefore, dropped (removePrunedAdditions) and handed back for
+    // Pruning.loadPruned / PostProcess.LoadPruned (Updating.java:111-117,171): device arrays of the
+    // work area, valid until the next batch; lp_update = the index of the update whose deps held the id
+    uint64_t n_load_pruned = 0;
+    const int64_t* lp_keys = nullptr;
+    const uint64_t* lp_msb = nullptr;
+    const uint64_t* lp_lsb = nullptr;
+    const int32_t* lp_node = nullptr;
+    const uint64_t* lp_update = nullptr;
     double ms_locate = 0, ms_derive = 0, ms_total = 0;
 };
 

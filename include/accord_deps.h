@@ -566,13 +566,14 @@ int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t sc
  * (computeInfoAndAdditions :194-287: the key's entries below depsKnownBefore its kind witnesses, not
  * COMMITTED or later, not in its deps), other entries lose ids that became COMMITTED or INVALID and
  * gain the batch's insertions below COMMITTED under their depsKnownBefore that they witness
- * (Utils.java:68-352) -- and inserts the deps the key's byId lacks as TRANSITIVELY_KNOWN entries
- * (those the command's kind witnesses, at or above prunedBefore; removePrunedAdditions'
- * LoadPruned is the host's). The lists start from the last ad_cfk_missing_load (NO_TXNIDS without
- * one). A batch without deps hands them back to the host copy, where entries leaving
- * ACCEPTED..APPLIED or moved mark them stale (ad_cfk_missing_load again). Deviation: a dep the kind
- * does not witness (an ExclusiveSyncPoint) past the key's last id is not inserted (the Java adds
- * it). The additions are a second internal batch: when only it fails, the explicit updates stand. */
+ * (Utils.java:68-352) -- and inserts the deps the key's byId lacks as TRANSITIVELY_KNOWN entries:
+ * those the command's kind witnesses, and every dep above the key's last txnId as the update sees it
+ * (past byId's end the Java adds without the witness test, :253-262). Additions below the key's
+ * prunedBefore are dropped (removePrunedAdditions, :111-117) and handed back by ad_cfk_load_pruned
+ * for the host's Pruning.loadPruned / PostProcess.LoadPruned (:171). The lists start from the last
+ * ad_cfk_missing_load (NO_TXNIDS without one). A batch without deps hands them back to the host copy,
+ * where entries leaving ACCEPTED..APPLIED or moved mark them stale (ad_cfk_missing_load again). The
+ * additions are a second internal batch: when only it fails, the explicit updates stand. */
 typedef struct ad_cfk_update_soa {
     uint64_t n;
     const int64_t*  keys;
@@ -583,7 +584,8 @@ typedef struct ad_cfk_update_soa {
     const uint64_t* exec_lsb;
     const int32_t*  exec_node;
     const uint8_t*  status;          /* AD_ST_* = InternalStatus.from(command.saveStatus()) */
-    const uint64_t* ballot_msb;      /* command.acceptedOrCommitted(); all three NULL = Ballot.ZERO */
+    const uint64_t* ballot_msb;      /* command.acceptedOrCommitted(); all three NULL = Ballot.ZERO
+                                      * (all three or none: AD_E_INVAL otherwise) */
     const uint64_t* ballot_lsb;
     const int32_t*  ballot_node;
     /* command.partialDeps().txnIds(key) past redundantBefore.shardRedundantBefore() (the cursor of
@@ -602,6 +604,12 @@ typedef struct ad_cfk_update_soa {
 int ad_cfk_update(ad_ctx* ctx, const ad_cfk_update_soa* u, uint64_t* n_applied, ad_stats* stats);
 /* Device buffers, on `stream` (null: the context's stream). Synchronous on return. */
 int ad_cfk_update_device(ad_ctx* ctx, const ad_cfk_update_soa* u_dev, void* stream, uint64_t* n_applied, ad_stats* stats);
+/* The LoadPruned requests of the last ad_cfk_update[_device] (Updating.java:111-117,171): for each
+ * addition dropped below its key's prunedBefore, the update (batch index) whose deps held it, the key
+ * and the TxnId -- the host issues the loads (Pruning.loadPruned). Batch order of the updates. Views
+ * owned by the context, valid until its next update batch. */
+int ad_cfk_load_pruned(ad_ctx* ctx, uint64_t* n, const uint64_t** update, const int64_t** keys, const uint64_t** msb,
+                       const uint64_t** lsb, const int32_t** node);
 /* TxnInfo.missing() of every entry as it stands (load order): ids [off[e], off[e+1]) ascending.
  * AD_E_STATE when the lists are stale (updates without deps moved entries after a load). Views
  * owned by the context, valid until its next call. */

@@ -288,7 +288,7 @@ def _witnesses(owner_raw, other_raw):
     return (mask >> _kind(other_raw)) & 1 == 1
 
 
-def cfk_update_missing(cfk, upd, dep_off=None, deps=None):
+def cfk_update_missing(cfk, upd, dep_off=None, deps=None, load_pruned=None):
     """CommandsForKey.update (CommandsForKey.java:992-1042) for a batch, with the TxnInfo.missing()
     lists and the deps-derived additions of Updating.insertOrUpdate (Updating.java:99-172):
       * an update whose status has deps (ACCEPTED..APPLIED) runs computeInfoAndAdditions (:194-287)
@@ -399,7 +399,11 @@ def cfk_update_missing(cfk, upd, dep_off=None, deps=None):
                     ti += 1
             new_row[5] = missing
             if key in pb:
-                additions = [a for a in additions if a >= pb[key]]     # removePrunedAdditions
+                # removePrunedAdditions (Updating.java:111-117): the ids below prunedBefore go to
+                # Pruning.loadPruned / PostProcess.LoadPruned (:171), (update index, key, TxnId)
+                if load_pruned is not None:
+                    load_pruned.extend((i, key, raw_of[a]) for a in additions if a < pb[key])
+                additions = [a for a in additions if a >= pb[key]]
             if additions:
                 # insertOrUpdateWithAdditions (:364-470)
                 self_missing = not present and st < COMMITTED

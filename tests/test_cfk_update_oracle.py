@@ -282,3 +282,46 @@ def test_prune_missing_subset_of_merged():
     assert (removed, keys) == (1, 1)
     assert _hlcs(n) == [5, 10, 30, 40] and n.pruned_before.tolist() == [2]
     assert n.miss_off.tolist() == [0, 0, 1, 1, 1]
+
+
+def test_unwitnessed_deps_past_end_are_added():
+    # Updating.java:210-263: while byId has entries the Java adds only deps the command's kind
+    # witnesses (an ExclusiveSyncPoint it does not witness is skipped, :256-259); once byId is
+    # exhausted every remaining dep is added (:253-262). C (Read, hlc 30) ACCEPTED with deps
+    # {ESP 15, ESP 45, Read 50}: ESP 15 lies inside byId -> skipped; ESP 45 and Read 50 lie past
+    # C itself, byId's end -> added although a Read witnesses neither
+    c = _miss_store()
+    esp, rd = A.KIND_EXCLUSIVE_SYNC_POINT, A.KIND_READ
+    off, dp = _deps([[(10, W), (15, esp), (20, W), (45, esp), (50, rd)]])
+    u = _upd([7], [30], [R], [A.ST_ACCEPTED])
+    n, applied, nadd = U.cfk_update_missing(c, u, off, dp)
+    assert (applied, nadd) == (1, 2)
+    assert _hlcs(n) == [10, 20, 30, 45, 50]
+
+
+def test_past_end_moves_with_the_batch():
+    # byId's end is the one the update sees: T (Write, 60) inserted earlier in the batch raises it, so
+    # C's ESP 55 dep is then inside byId (skipped); without T it would be past the end (added)
+    c = _miss_store()
+    esp = A.KIND_EXCLUSIVE_SYNC_POINT
+    off, dp = _deps([[], [(55, esp)]])
+    u = _upd([7, 7], [60, 30], [W, R], [A.ST_PREACCEPTED, A.ST_ACCEPTED])
+    _, _, nadd = U.cfk_update_missing(c, u, off, dp)
+    assert nadd == 0
+    off, dp = _deps([[(55, esp)], []])
+    u = _upd([7, 7], [30, 60], [R, W], [A.ST_ACCEPTED, A.ST_PREACCEPTED])
+    n, _, nadd = U.cfk_update_missing(c, u, off, dp)
+    assert nadd == 1 and 55 in _hlcs(n)
+
+
+def test_load_pruned_reports_dropped_additions():
+    # removePrunedAdditions (Updating.java:111-117): additions below prunedBefore are not inserted and
+    # go to Pruning.loadPruned; the LoadPruned post-process (:171) asks the store to load them
+    c = _miss_store()
+    c.pruned_before = np.array([1])                  # prunedBefore = B (20)
+    off, dp = _deps([[(12, W), (15, W), (25, W)]])
+    u = _upd([7], [40], [W], [A.ST_ACCEPTED])
+    lp = []
+    n, _, nadd = U.cfk_update_missing(c, u, off, dp, load_pruned=lp)
+    assert nadd == 1
+    assert [(i, k, int(t[1]) >> 16) for i, k, t in lp] == [(0, 7, 12), (0, 7, 15)]

@@ -25,11 +25,30 @@ def _norm(m, l, n):
     return U.norm(m, l, n)
 
 
-def with_deps(cfk, u, rng, keep=0.7, n_new=2, dep_kinds=(0, 1)):
+_PAST = [1_000_000]
+
+
+def with_deps(cfk, u, rng, keep=0.7, n_new=2, dep_kinds=(0, 1), esp=0, past_unwitnessed=0, below_pruned=0):
     """Deps per update with a deps status: a `keep` share of the key's ids below the txn's
-    depsKnownBefore plus `n_new` ids the store does not hold (some below, some past its ids)."""
+    depsKnownBefore plus `n_new` ids the store does not hold (some below, some past its ids), all of
+    kinds the txn witnesses; then
+      * `esp` ExclusiveSyncPoint ids (witnessed by ExclusiveSyncPoints only: the kind the Java lets a
+        command depend on without witnessing it, Updating.java:256-259) -- half in the txn's window,
+        half past every id of the batch;
+      * `past_unwitnessed` ids of a kind the txn does not witness, past every id the key will hold when
+        the update runs (epoch 100, rising in batch order): added only because they are past byId's
+        end (:253-262);
+      * `below_pruned` witnessed ids below the key's prunedBefore that byId lacks: dropped by
+        removePrunedAdditions and handed back as LoadPruned (:111-117)."""
     seg = cfk.seg.astype(np.int64)
     by_key = {int(cfk.keys[k]): (int(seg[k]), int(seg[k + 1])) for k in range(len(cfk.keys))}
+    pb = {}
+    if cfk.pruned_before is not None:
+        for k in range(len(cfk.keys)):
+            p = int(cfk.pruned_before[k])
+            if p >= 0:
+                e = int(seg[k]) + p
+                pb[int(cfk.keys[k])] = (int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e]))
     offs, dm, dl, dn = [0], [], [], []
     for i in range(len(u)):
         ids = []
@@ -45,7 +64,29 @@ def with_deps(cfk, u, rng, keep=0.7, n_new=2, dep_kinds=(0, 1)):
                 ids.append((int(nw.msb[j]), int(nw.lsb[j]), int(nw.node[j])))
             t = (int(u.txn.msb[i]), int(u.txn.lsb[i]), int(u.txn.node[i]))
             # a command's deps hold only kinds it witnesses (Updating.java:243-247 asserts it of the rest)
-            ids = sorted(set(x for x in ids if _norm(*x) != _norm(*t) and U._witnesses(t, x)), key=lambda x: _norm(*x))
+            ids = [x for x in ids if _norm(*x) != _norm(*t) and U._witnesses(t, x)]
+            tk = (t[1] >> 1) & 7
+            for j in range(esp):
+                if j % 2 == 0:
+                    e = make_txn_ids(int(u.txn.msb[i]) >> 15, [int(rng.integers(max(1, hlc - 50), hlc + 50))], [4],
+                                     [int(rng.integers(50, 60))])
+                else:
+                    _PAST[0] += 3
+                    e = make_txn_ids(100, [_PAST[0]], [4], [int(rng.integers(50, 60))])
+                ids.append((int(e.msb[0]), int(e.lsb[0]), int(e.node[0])))
+            unw = [k for k in (0, 1, 2, 3) if not U._witnesses(t, (0, k << 1, 0))]
+            for j in range(past_unwitnessed if unw else 0):
+                _PAST[0] += 3
+                e = make_txn_ids(100, [_PAST[0]], [int(rng.choice(unw))], [int(rng.integers(60, 70))])
+                ids.append((int(e.msb[0]), int(e.lsb[0]), int(e.node[0])))
+            p = pb.get(int(u.keys[i]))
+            if p is not None and below_pruned and tk != 4:
+                phlc = p[1] >> 16
+                for j in range(below_pruned):
+                    e = make_txn_ids(int(p[0]) >> 15, [int(rng.integers(max(1, phlc - 40), phlc))], [1],
+                                     [int(rng.integers(70, 80))])
+                    ids.append((int(e.msb[0]), int(e.lsb[0]), int(e.node[0])))
+            ids = sorted(set(ids), key=lambda x: _norm(*x))
             # one id per Timestamp.equals class
             uniq, seen = [], set()
             for x in ids:
@@ -175,3 +216,50 @@ def test_batch_without_deps_hands_lists_back(oracle):
         assert len(off) == exp.n_entries + 1
     finally:
         st.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_unwitnessed_past_end_and_load_pruned(oracle, seed):
+    # deps the command's kind does not witness: ExclusiveSyncPoints (in the window and past the end) and
+    # other kinds past the key's last id -- inserted exactly when past byId's end as the update sees it
+    # (earlier updates of the batch raise it); witnessed deps below prunedBefore come back as LoadPruned
+    w = _workload(90 + seed, n_hist_txns=220)
+    rng = np.random.default_rng(900 + seed)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        n_lp = n_add = 0
+        for rnd in range(3):
+            parts = [G.transitions(cfk, rng, 40, statuses=(3, 4, 5, 6))[0],
+                     G.fresh_preaccepts(cfk, rng, 12, statuses=(2, 3), epoch=9 + rnd, hlc0=1 + 1000 * rnd,
+                                        kinds=(0, 1, 3, 4))]
+            u = with_deps(cfk, G.concat(*parts), rng, esp=2, past_unwitnessed=1 + seed % 2, below_pruned=2)
+            lp = []
+            exp, applied, nadd = U.cfk_update_missing(cfk, u, u.dep_off, u.deps, load_pruned=lp)
+            if U.dup_committed_exec(exp):
+                continue
+            n_applied, stats = st.cfk_update(u)
+            assert n_applied == applied + nadd and stats["n_keys"][2] == nadd
+            _check(w, st, oracle, exp)
+            got = [(i, k, _norm(*t)) for i, k, t in st.cfk_load_pruned()]
+            assert got == [(i, k, _norm(*t)) for i, k, t in lp]
+            n_lp += len(lp)
+            n_add += nadd
+            cfk = exp
+        assert n_add > 0
+    finally:
+        st.close()
+
+
+def test_load_pruned_collected():
+    # the generator reaches the LoadPruned path somewhere in the seeds above (guards the test's reach)
+    total = 0
+    for seed in range(6):
+        w = _workload(90 + seed, n_hist_txns=220)
+        rng = np.random.default_rng(900 + seed)
+        u = with_deps(w.cfk, G.transitions(w.cfk, rng, 40, statuses=(3, 4, 5, 6))[0], rng, below_pruned=2)
+        lp = []
+        U.cfk_update_missing(w.cfk, u, u.dep_off, u.deps, load_pruned=lp)
+        total += len(lp)
+    assert total > 0
