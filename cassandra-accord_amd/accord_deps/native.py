@@ -27,7 +27,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_cfk_ballots_load", "ad_cfk_ballots",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange", "ad_exchange_plan",
            "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing",
-           "ad_cfk_load_pruned")
+           "ad_cfk_load_pruned", "ad_host_register", "ad_host_unregister", "ad_deps_batch_into")
 
 
 class AccordDepsError(RuntimeError):
@@ -114,6 +114,10 @@ def lib():
                                   C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.ad_cfk_missing.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
+        L.ad_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.ad_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
+        L.ad_deps_batch_into.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.POINTER(A.AdDepsResult),
+                                         C.c_void_p, C.c_void_p, C.c_uint32]
         L.ad_cfk_load_pruned.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)] + [C.POINTER(C.c_void_p)] * 5
         L.ad_check_snapshot.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         _lib = L
@@ -423,6 +427,71 @@ class DeviceCommandStore:
             return stats_dict(out.contents.stats)
         finally:
             L.ad_result_free(out)
+
+    class HostOut:
+        """Caller-owned host output arrays of ad_deps_batch_into (numpy), pinned with ad_host_register
+        when `pin`; grown (and re-pinned) when a batch needs more."""
+
+        def __init__(self, store, n, cap, pin=True):
+            self.store, self.pin, self.n = store, pin, n
+            self.off = np.zeros((9, n + 1), np.uint64)
+            self.cap = [int(x) for x in cap]
+            self.keys = [np.zeros(max(1, self.cap[3 * m]), np.int64) for m in range(3)]
+            self.txns = [np.zeros(max(1, self.cap[3 * m + 1]), np.uint32) for m in range(3)]
+            self.k2t = [np.zeros(max(1, self.cap[3 * m + 2]), np.int32) for m in range(3)]
+            self.pinned = []
+            if pin:
+                for a in [self.off] + self.keys + self.txns + self.k2t:
+                    store._check(lib().ad_host_register(store.h, A.ptr(a), a.nbytes))
+                    self.pinned.append(a)
+
+        def release(self):
+            for a in self.pinned:
+                lib().ad_host_unregister(self.store.h, A.ptr(a))
+            self.pinned = []
+
+        def soa(self):
+            r = A.AdDepsResult()
+            r.n_txns = self.n
+            for m in range(3):
+                r.keys_off[m] = A.ptr(self.off[3 * m])
+                r.txn_off[m] = A.ptr(self.off[3 * m + 1])
+                r.k2t_off[m] = A.ptr(self.off[3 * m + 2])
+                r.keys[m] = A.ptr(self.keys[m])
+                r.txns[m] = A.ptr(self.txns[m])
+                r.k2t[m] = A.ptr(self.k2t[m])
+            return r
+
+    def deps_batch_into(self, queries, flags=A.AD_SNAPSHOT, slices=0, out=None, pin=True, materialise=True):
+        """ad_deps_batch_into: host arrays in, caller-owned (pinned) host arrays out, the batch resolved in
+        slices whose copy-out overlaps the next slice. `out`: a HostOut to reuse (grown on AD_E_SPACE).
+        Returns (PartialDepsBatch or None, stats dict, the HostOut)."""
+        n = len(queries)
+        if out is None or out.n != n:
+            if out is not None:
+                out.release()
+            np_ = queries.n_probes
+            out = DeviceCommandStore.HostOut(self, n, [np_, 2 * np_, 4 * np_] * 3, pin)
+        need = np.zeros(9, np.uint64)
+        soa = queries.soa()
+        while True:
+            r = out.soa()
+            cap = np.asarray(out.cap, np.uint64)
+            rc = lib().ad_deps_batch_into(self.h, C.byref(soa), flags, C.byref(r), A.ptr(cap), A.ptr(need), slices)
+            if rc != A.AD_E_SPACE:
+                break
+            out.release()
+            out = DeviceCommandStore.HostOut(self, n, [int(x) + int(x) // 4 + 16 for x in need], pin)
+        self._check(rc)
+        stats = stats_dict(r.stats)
+        if not materialise:
+            return None, stats, out
+        raw = []
+        for m in range(3):
+            ko, to, oo = out.off[3 * m].copy(), out.off[3 * m + 1].copy(), out.off[3 * m + 2].copy()
+            raw.append((ko, out.keys[m][:int(ko[-1])].copy(), to, out.txns[m][:int(to[-1])].copy(), oo,
+                        out.k2t[m][:int(oo[-1])].copy()))
+        return self.materialise(raw, stats), stats, out
 
     def materialise(self, raw, stats=None):
         d = self.dictionary()

@@ -236,6 +236,11 @@ struct ad_ctx {
     hipEvent_t ev_lean1 = nullptr;     // fused path: after lean pass 1
     hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;   // split path on the fused kernels' deferrals
     BatchCtl* h_ctl = nullptr;         // pinned mirror of the batch control block
+    // ad_deps_batch_into: a second result bank (offsets + packed arrays) so that one slice of a batch is
+    // copied out while the next resolves, the copy-out stream and its events
+    DevBuf off_b, o_keys_b[3], o_txns_b[3], o_k2t_b[3];
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_copied[2] = {};
     // multi-GPU export / merge buffers
     DevBuf x_sz, x_off, x_bsum, x_df, x_cnt;
     // regions of the last device batch (ad_parts_export of an AD_PARTS_ONLY result)
@@ -1682,9 +1687,23 @@ static int result_to_host(ad_ctx* c, uint64_t n, const ad_deps_result& dev, ad_d
 
 static int check_query_host(ad_ctx* c, const ad_query_soa* q)
 {
-    for (uint64_t i = 0; i < q->n_txns; ++i)
-        for (uint64_t k = q->key_off[i] + 1; k < q->key_off[i + 1]; ++k)
-            if (q->keys[k - 1] >= q->keys[k]) return c->fail(AD_E_INVAL, "request %llu: keys not strictly ascending", (unsigned long long)i);
+    // host threads over request ranges; the lowest offending request is reported
+    std::atomic<uint64_t> bad{~0ull};
+    parallel_for(q->n_txns, [&](size_t a, size_t b) {
+        for (uint64_t i = a; i < b; ++i)
+        {
+            bool ok = q->key_off[i] <= q->key_off[i + 1];
+            for (uint64_t k = q->key_off[i] + 1; ok && k < q->key_off[i + 1]; ++k) ok = q->keys[k - 1] < q->keys[k];
+            if (!ok)
+            {
+                uint64_t cur = bad.load();
+                while (i < cur && !bad.compare_exchange_weak(cur, i)) {}
+                return;
+            }
+        }
+    }, 1 << 15);
+    if (bad.load() != ~0ull)
+        return c->fail(AD_E_INVAL, "request %llu: keys not strictly ascending", (unsigned long long)bad.load());
     return 0;
 }
 
@@ -1745,6 +1764,10 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->ev_sp1) (void)hipEventDestroy(c->ev_sp1);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->h_xtab) (void)hipHostFree(c->h_xtab);
+    if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
+    for (hipEvent_t e : c->ev_copied)
+        if (e) (void)hipEventDestroy(e);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     for (hipEvent_t e : c->x_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->lv) levels_work_destroy(c->lv);
@@ -1935,6 +1958,160 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
     ad_deps_result dev{};
     if ((rc = run_pipeline(c, &d, c->stream, &dev))) return rc;
     return result_to_host(c, n, dev, out);
+}
+
+int ad_host_register(ad_ctx* c, void* p, uint64_t bytes)
+{
+    if (!c || !p || !bytes) return AD_E_INVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    HIPCHK(c, hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return AD_OK;
+}
+
+int ad_host_unregister(ad_ctx* c, void* p)
+{
+    if (!c || !p) return AD_E_INVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    HIPCHK(c, hipHostUnregister(p));
+    return AD_OK;
+}
+
+int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_result* out, const uint64_t* cap,
+                       uint64_t* need, uint32_t slices)
+{
+    if (!c || !q || !out || !cap || !need) return AD_E_INVAL;
+    if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    const uint64_t n = q->n_txns;
+    for (int m = 0; m < 3; ++m)
+        if (!out->keys_off[m] || !out->txn_off[m] || !out->k2t_off[m] || (cap[3 * m] && !out->keys[m]) ||
+            (cap[3 * m + 1] && !out->txns[m]) || (cap[3 * m + 2] && !out->k2t[m]))
+            return c->fail(AD_E_INVAL, "ad_deps_batch_into: output arrays missing for map %d", m);
+    int rc = check_query_host(c, q);
+    if (rc) return rc;
+    if (flags & AD_SEQUENTIAL)
+    {
+        rc = sequential_on_device(c, q);
+        if (rc < 0) return rc;
+        if (rc > 0)
+        {
+            if ((rc = sync_host(c))) return rc;
+            auto saved = c->cfk;
+            if ((rc = apply_preaccepts(c, q))) { c->cfk = saved; return rc; }
+        }
+        slices = 1;        // the inserted requests are part of one snapshot
+    }
+    if (c->dirty && (rc = build_snapshot(c))) return rc;
+    if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    if (!c->ev_ready) HIPCHK(c, hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
+    for (hipEvent_t& e : c->ev_copied)
+        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // slices of >= 128k requests (SNAPSHOT requests are independent): slice j's result is copied out on
+    // the copy stream while slice j + 1 resolves into the other result bank
+    if (slices == 0) slices = (uint32_t)std::min<uint64_t>(4, std::max<uint64_t>(1, n >> 17));
+    slices = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(slices, std::max<uint64_t>(n, 1)));
+    auto swap_bank = [&]() {
+        auto sw = [](DevBuf& a, DevBuf& b) { std::swap(a.p, b.p); std::swap(a.cap, b.cap); };
+        sw(c->off, c->off_b);
+        for (int m = 0; m < 3; ++m)
+        {
+            sw(c->o_keys[m], c->o_keys_b[m]);
+            sw(c->o_txns[m], c->o_txns_b[m]);
+            sw(c->o_k2t[m], c->o_k2t_b[m]);
+        }
+    };
+    uint64_t base[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    bool fits = true;
+    ad_stats agg{};
+    std::vector<uint64_t> ko;
+    hipStream_t st = c->stream;
+    for (uint32_t j = 0; j < slices; ++j)
+    {
+        const uint64_t lo = n * j / slices, hi = n * (j + 1) / slices, nc = hi - lo;
+        const uint64_t k0 = n ? q->key_off[lo] : 0, k1 = n ? q->key_off[hi] : 0;
+        if (j >= 2) HIPCHK(c, hipStreamWaitEvent(st, c->ev_copied[j & 1], 0));   // this bank's last copy-out
+        ko.resize(nc + 1);
+        for (uint64_t i = 0; i <= nc; ++i) ko[i] = n ? q->key_off[lo + i] - k0 : 0;
+        ad_query_soa d{};
+        d.n_txns = nc;
+        d.n_keys = k1 - k0;
+        rc = 0;
+        d.txn_msb = stage_q(c, c->q_tm, q->txn_msb + lo, nc, &rc);
+        d.txn_lsb = stage_q(c, c->q_tl, q->txn_lsb + lo, nc, &rc);
+        d.txn_node = stage_q(c, c->q_tn, q->txn_node + lo, nc, &rc);
+        d.exec_msb = stage_q(c, c->q_em, q->exec_msb + lo, nc, &rc);
+        d.exec_lsb = stage_q(c, c->q_el, q->exec_lsb + lo, nc, &rc);
+        d.exec_node = stage_q(c, c->q_en, q->exec_node + lo, nc, &rc);
+        d.min_epoch = q->min_epoch ? stage_q(c, c->q_me, q->min_epoch + lo, nc, &rc) : nullptr;
+        d.key_off = stage_q(c, c->q_ko, ko.data(), nc + 1, &rc);
+        d.keys = stage_q(c, c->q_k, q->keys + k0, k1 - k0, &rc);
+        if (rc) return rc;
+        ad_deps_result dev{};
+        if ((rc = run_pipeline(c, &d, st, &dev, false, true))) return rc;      // complete on return
+        const ad_stats& S = dev.stats;
+        uint64_t t[9];
+        for (int m = 0; m < 3; ++m)
+        {
+            t[3 * m] = S.n_keys[m];
+            t[3 * m + 1] = S.n_unique[m];
+            t[3 * m + 2] = S.n_pairs[m] + S.n_keys[m];
+        }
+        for (int a = 0; a < 9; ++a) fits = fits && base[a] + t[a] <= cap[a];
+        if (fits)
+        {
+            // offsets relative to the whole batch, then the copy-out of this slice
+            HIPCHK(c, run_add_bases(c->off.as<uint64_t>(), nc + 1, base, st));
+            HIPCHK(c, hipEventRecord(c->ev_ready, st));
+            HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_ready, 0));
+            for (int m = 0; m < 3; ++m)
+            {
+                uint64_t* offs[3] = {out->keys_off[m], out->txn_off[m], out->k2t_off[m]};
+                if (!t[3 * m] && !t[3 * m + 2])
+                {
+                    // a map empty in this slice: its offsets are the bases (host fill, no transfer)
+                    for (int k = 0; k < 3; ++k) std::fill(offs[k] + lo, offs[k] + hi + 1, base[3 * m + k]);
+                    continue;
+                }
+                for (int k = 0; k < 3; ++k)
+                    HIPCHK(c, hipMemcpyAsync(offs[k] + lo, c->off.as<uint64_t>() + (uint64_t)(3 * m + k) * (nc + 1),
+                                             8 * (nc + 1), hipMemcpyDeviceToHost, c->cstream));
+                if (t[3 * m])
+                    HIPCHK(c, hipMemcpyAsync(out->keys[m] + base[3 * m], dev.keys[m], 8 * t[3 * m], hipMemcpyDeviceToHost, c->cstream));
+                if (t[3 * m + 1])
+                    HIPCHK(c, hipMemcpyAsync(out->txns[m] + base[3 * m + 1], dev.txns[m], 4 * t[3 * m + 1], hipMemcpyDeviceToHost,
+                                             c->cstream));
+                if (t[3 * m + 2])
+                    HIPCHK(c, hipMemcpyAsync(out->k2t[m] + base[3 * m + 2], dev.k2t[m], 4 * t[3 * m + 2], hipMemcpyDeviceToHost,
+                                             c->cstream));
+            }
+            HIPCHK(c, hipEventRecord(c->ev_copied[j & 1], c->cstream));
+            swap_bank();
+        }
+        for (int a = 0; a < 9; ++a) base[a] += t[a];
+        agg.n_txns += S.n_txns;
+        agg.n_probes += S.n_probes;
+        agg.n_deferred += S.n_deferred;
+        agg.n_deferred_lean += S.n_deferred_lean;
+        agg.n_lean_pass2 += S.n_lean_pass2;
+        for (int m = 0; m < 3; ++m)
+        {
+            agg.n_pairs[m] += S.n_pairs[m];
+            agg.n_unique[m] += S.n_unique[m];
+            agg.n_keys[m] += S.n_keys[m];
+        }
+        for (int i = 0; i < 7; ++i) agg.ms_stage[i] += S.ms_stage[i];
+        agg.ms_device += S.ms_device;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->cstream));
+    for (int a = 0; a < 9; ++a) need[a] = base[a];
+    agg.ms_ingest = c->ms_ingest;
+    out->n_txns = n;
+    out->stats = agg;
+    if (n == 0)
+        for (int m = 0; m < 3; ++m) out->keys_off[m][0] = out->txn_off[m][0] = out->k2t_off[m][0] = 0;
+    if (!fits)
+        return c->fail(AD_E_SPACE, "ad_deps_batch_into: output capacities too small (needed sizes in need[])");
+    return AD_OK;
 }
 
 int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void* stream, ad_deps_result* out)

@@ -2068,4 +2068,23 @@ hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const Batch
     return run_build(s, b, st);
 }
 
+struct Bases9 { uint64_t b[9]; };
+
+__global__ void k_add_bases(uint64_t* off, uint64_t n1, Bases9 base)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 9 * n1) return;
+    off[i] += base.b[i / n1];
+}
+
+hipError_t run_add_bases(uint64_t* off, uint64_t n1, const uint64_t* base, hipStream_t st)
+{
+    Bases9 b;
+    bool any = false;
+    for (int a = 0; a < 9; ++a) any |= (b.b[a] = base[a]) != 0;
+    if (!any || !n1) return hipSuccess;
+    k_add_bases<<<(unsigned)((9 * n1 + 255) / 256), 256, 0, st>>>(off, n1, b);
+    return hipGetLastError();
+}
+
 }  // namespace adx

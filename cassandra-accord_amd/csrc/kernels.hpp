@@ -104,6 +104,8 @@ hipError_t run_build(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 hipError_t run_recovery(const DevSnapshot& s, const RecoveryView& v, const BatchBufs& b, uint32_t scan, hipStream_t st);
 hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st);
+// off: 9 arrays of n1 offsets back to back; array a += base[a] (a slice's offsets made relative to its batch)
+hipError_t run_add_bases(uint64_t* off, uint64_t n1, const uint64_t* base, hipStream_t st);
 hipError_t run_pack(const BatchBufs& b, hipStream_t st);
 // offsets of the 9 size arrays + totals (+ the packed arrays when `copy`): tile sums, one-block scan
 // of the tile sums, then a streaming per-tile scan + pack; no host round trip between resolve and pack

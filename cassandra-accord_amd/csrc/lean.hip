@@ -31,6 +31,11 @@ constexpr int LEAN_WAVES = 4;
 constexpr int LEAN_OCC = LEAN_OCC_N;        // waves per SIMD the register budget is sized for
 constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 constexpr uint32_t LEAN_CHUNK = 1u << 16;
+// measurement switches (scripts/build_variant.sh; results are wrong with any of them set):
+// 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes
+#ifndef LEAN_EXP
+#define LEAN_EXP 0
+#endif
 
 // ascending bitonic sort within each LPR-lane segment (a request's lanes)
 template <uint32_t K, uint32_t LPR>
@@ -508,7 +513,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         else
             lp = from_cand ? s.cand + (a_base + i) : s.cwr + (a_ct + (i - a_n1));
         if (!live || (!from_cand && cls == 0)) lp = s.cand;        // class Ws: the last Write, no load
-        const uint32_t lv = *lp;
+        const uint32_t lv = (LEAN_EXP & 1) ? ((2 * hl + 1) | (1u << RANK_BITS)) : *lp;
         // range elements (same round trip as the list loads)
         uint32_t ar = 0;
         uint64_t ce = 0;
@@ -551,7 +556,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             uint32_t k = mine ? ((r << 3) | a) : 0xFFFFFFFFu;
             // the sort must span every lane that may hold one (raw emissions: lanes [0, T))
             const uint32_t kmax = seg_max(T);
-            if (kmax <= 8) seg_bitonic<8, LPR>(k);
+            if (LEAN_EXP & 2) {}
+            else if (kmax <= 8) seg_bitonic<8, LPR>(k);
             else if (kmax <= 16 || LPR == 16) seg_bitonic<16, LPR>(k);
             else if (kmax <= 32 || LPR == 32) seg_bitonic<(LPR < 32 ? LPR : 32), LPR>(k);
             else seg_bitonic<LPR, LPR>(k);
@@ -594,7 +600,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits);
             put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
-            if (act && tot && fits)
+            if (act && tot && fits && !(LEAN_EXP & 4))
             {
                 int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
                 uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);

@@ -244,6 +244,23 @@ int ad_prepare(ad_ctx* ctx);
 int  ad_deps_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t flags, ad_deps_result** out);
 void ad_result_free(ad_deps_result* r);
 
+/* Pin caller-owned host memory for DMA (hipHostRegister): a Panama Arena segment a Java host reuses
+ * batch after batch for queries and results. Unregister before freeing it. */
+int ad_host_register(ad_ctx* ctx, void* p, uint64_t bytes);
+int ad_host_unregister(ad_ctx* ctx, void* p);
+
+/* ad_deps_batch into caller-owned host arrays (the PCIe-facing path a Java host binds): `out`'s array
+ * pointers are the caller's -- per map keys_off / txn_off / k2t_off with n_txns + 1 entries each, and
+ * keys / txns / k2t with capacities cap[3 m + {0, 1, 2}] (elements); ideally registered
+ * (ad_host_register), so that every copy is a DMA. Same results as ad_deps_batch. The batch is resolved
+ * in `slices` slices of requests (0: one per 128k requests, at most 4; SEQUENTIAL batches run whole):
+ * slice j's result is copied out on a second stream while slice j + 1 is staged and resolved into a
+ * second result bank. need[9] receives the sizes the batch needed; when a capacity was too small the
+ * call returns AD_E_SPACE (the arrays' contents are then unspecified) and can be repeated with larger
+ * arrays. out->stats sums the slices' device stats. */
+int ad_deps_batch_into(ad_ctx* ctx, const ad_query_soa* q, uint32_t flags, ad_deps_result* out, const uint64_t* cap /*[9]*/,
+                       uint64_t* need /*[9]*/, uint32_t slices);
+
 /* ---- batch resolve, device-resident (HBM) buffers in and out ----------------------- *
  * q's arrays are device pointers. *out receives device pointers owned by ctx, valid until
  * the next batch call on ctx; out->stats is filled after the call returns. All work is

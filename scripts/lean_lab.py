@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Kernel lab for the config-2 headline batch: one process generates config 2 once, then times the
+in-tree libaccord_deps.so and every variants/<name>.so given (built by scripts/build_variant.sh with
+different -D flags) on the same store and batch, one after the other. Per library: per-stage HIP-event
+times (ad_stats.ms_stage), ms per step, and whether a sample of its device result equals the in-tree
+library's (variants that skip work for a measurement report "differs", as they should).
+
+    python scripts/lean_lab.py [--steps 20] [--scale 1.0] variants/a.so variants/b.so ...
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from accord_deps import native, synth  # noqa: E402
+
+
+def run(lib, w, steps, warmup, sample, dev):
+    native._lib = None
+    native.LIB_PATH = lib
+    native.lib()
+    st = native.DeviceCommandStore(device=0, slices=w.slices)
+    try:
+        st.load(w)
+        qdev, keep = native.device_queries(w.queries, dev)
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        for _ in range(warmup):
+            res, stats = st.deps_batch_device(qdev, sp)
+        torch.cuda.synchronize(dev)
+        acc = np.zeros(7)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            res, stats = st.deps_batch_device(qdev, sp)
+            acc += np.array(stats["ms_stage"][:7])
+        torch.cuda.synchronize(dev)
+        ms = 1000.0 * (time.perf_counter() - t0) / steps
+        got = st.device_result_to_host(res, sample)
+        return dict(ms_per_step=round(ms, 4), stages=[round(x / steps, 4) for x in acc],
+                    pairs=[int(x) for x in stats["n_pairs"]], n_pass2=int(stats.get("n_lean_pass2", 0)),
+                    n_general=int(stats.get("n_deferred_lean", 0))), got
+    finally:
+        st.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("libs", nargs="*")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    t = time.time()
+    s = a.scale
+    # bench.py's config-2 batch (bench_deps: config2_sharded for rank 0 of 1)
+    w, _, _ = synth.config2_sharded(0, 1, n_txns_per_gpu=int(1_000_000 * s), n_keys_per_gpu=int(1_000_000 * s),
+                                    n_hist_entries_per_gpu=int(16_000_000 * s))
+    print("config2 generated in %.1f s" % (time.time() - t), file=sys.stderr, flush=True)
+    rng = np.random.default_rng(5)
+    sample = np.unique(np.concatenate([np.arange(2000), rng.choice(len(w.queries), 4000, replace=False)]))
+    base_lib = os.path.join(ROOT, "cassandra-accord_amd", "accord_deps", "libaccord_deps.so")
+    ref = None
+    for lib in [base_lib] + a.libs:
+        r, got = run(lib, w, a.steps, a.warmup, sample, dev)
+        if ref is None:
+            ref = got
+            r["same_as_base"] = True
+        else:
+            r["same_as_base"] = bool(got.equals(ref))
+        r["lib"] = os.path.basename(lib)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+"""GPU parity of the PCIe-facing batch path a Java host binds (ad_deps_batch_into):
+host query arrays in, caller-owned pinned host arrays out, the batch resolved in slices whose copy-out
+overlaps the next slice. Results must equal the reference restatement (oracle) and ad_deps_batch's,
+for every slicing, after growing too-small outputs (AD_E_SPACE), for SEQUENTIAL batches and for empty
+batches."""
+import numpy as np
+import pytest
+
+from accord_deps import _abi as A
+from accord_deps import native, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("slices", [1, 3])
+def test_into_matches_oracle(oracle, seed, slices):
+    w = synth.random_small(seed, n_keys=80, n_hist_txns=600, n_txns=300, max_keys=6, n_range_cmds=40)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        got, stats, out = st.deps_batch_into(w.queries, slices=slices)
+        ok, why = got.equals(oracle.resolve(w), detail=True)
+        assert ok, why
+        assert stats["n_txns"] == len(w.queries)
+        out.release()
+    finally:
+        st.close()
+
+
+def test_into_config2_scaled_slicings_and_growth():
+    w = synth.config2(n_txns=60000, n_keys=40000, n_hist_entries=600000)
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        ref = st.calculate_partial_deps(w.queries)
+        out = None
+        for slices in (1, 2, 4, 7):
+            got, stats, out = st.deps_batch_into(w.queries, slices=slices, out=out)
+            ok, why = got.equals(ref, detail=True)
+            assert ok, (slices, why)
+        out.release()
+        # outputs far too small: AD_E_SPACE, then grown to the sizes the batch reported
+        small = native.DeviceCommandStore.HostOut(st, len(w.queries), [1] * 9)
+        got, _, out = st.deps_batch_into(w.queries, slices=3, out=small)
+        ok, why = got.equals(ref, detail=True)
+        assert ok, why
+        assert out is not small
+        out.release()
+    finally:
+        st.close()
+
+
+def test_into_unpinned_outputs():
+    w = synth.random_small(21, n_keys=60, n_hist_txns=400, n_txns=200)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        got, _, _ = st.deps_batch_into(w.queries, slices=2, pin=False)
+        ok, why = got.equals(st.calculate_partial_deps(w.queries), detail=True)
+        assert ok, why
+    finally:
+        st.close()
+
+
+def test_into_sequential_config1(oracle):
+    w = synth.config1(n_txns=2000)
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        got, _, out = st.deps_batch_into(w.queries, flags=A.AD_SEQUENTIAL, slices=4)
+        ok, why = got.equals(oracle.resolve(w), detail=True)
+        assert ok, why
+        out.release()
+    finally:
+        st.close()
+
+
+def test_into_empty_batch_and_bad_keys():
+    w = synth.random_small(3)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        got, stats, out = st.deps_batch_into(w.queries.take(np.zeros(0, np.int64)))
+        assert got.n_txns == 0 and stats["n_txns"] == 0
+        out.release()
+        # keys of a request not ascending: AD_E_INVAL from the (threaded) host check, nothing resolved
+        q = w.queries
+        bad = q.take(np.arange(len(q)))
+        i = int(np.nonzero(np.diff(bad.key_off.astype(np.int64)) >= 2)[0][0])
+        a, b = int(bad.key_off[i]), int(bad.key_off[i] + 1)
+        bad.keys[a], bad.keys[b] = bad.keys[b], bad.keys[a]
+        with pytest.raises(native.AccordDepsError) as ei:
+            st.deps_batch_into(bad, pin=False)
+        assert ei.value.code == A.AD_E_INVAL and ("request %d" % i) in str(ei.value)
+    finally:
+        st.close()
