@@ -265,6 +265,9 @@ struct ad_ctx {
     // recovery scans (ad_recovery_batch*): entry ranks kept from the last snapshot build, device view
     std::vector<uint32_t> h_txn_rank, h_exec_rank, h_pruned;
     uint64_t rv_gen = ~0ull;                   // snap_gen the device view was built for
+    uint64_t rank_gen = 0, rv_rng_gen = ~0ull; // rank-space changes (builds, dictionary merges); the view's range part
+    DevBuf rv_cnt, rv_eoff, rv_bsum, rv_err, rv_pk, rv_pv, rv_pk2, rv_pv2, rv_hist, rv_hoff;   // device-built view scratch
+    bool rv_dev_miss = false;                  // the view's missing() ids are the device lists (d_mids)
     DevBuf rv_ent, rv_seg, rv_pruned, rv_miss, rv_tree, rv_inv_off, rv_inv;
     DevBuf rv_rcmd, rv_rflags, rv_rex_hi, rv_rex_lo, rv_rex_node, rv_rdep_off, rv_rdep_hi, rv_rdep_lo, rv_rdep_node;
     bool rv_ranges = false;
@@ -1078,6 +1081,7 @@ static int build_snapshot(ad_ctx* c)
     c->h_pruned.swap(pruned);
     c->dirty = false;
     ++c->snap_gen;
+    ++c->rank_gen;
     cfk_upd_work_invalidate(c->cu);      // state the update path keeps between batches
     c->global_ok = use_global;   // parts carry global ranks exactly when the dictionary is the installed one
     c->n_global = use_global ? c->dict_msb.size() : 0;
@@ -1834,6 +1838,7 @@ int ad_range_cmds_load(ad_ctx* c, const ad_range_cmds_soa* in)
     R.end.assign(in->range_end, in->range_end + nr);
     R.rec = false;                  // recovery facts belong to the previous commands
     c->rv_gen = ~0ull;
+    c->rv_rng_gen = ~0ull;
     drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
     c->dirty = true;
     return AD_OK;
@@ -2128,18 +2133,154 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
 
 // device view of the snapshot for mapReduceFull: entries in load order with executeAt ranks,
 // status, kind and their TxnInfo.missing() lists as ranks (built once per snapshot / missing load)
+// The live range commands of the view: per range entry of the snapshot its command, the commands'
+// recovery facts normalised. Host-built from the loaded commands; rebuilt when ranks change.
+static int build_rv_ranges(ad_ctx* c, bool live_cmds)
+{
+    int rc;
+        const auto& R = c->cmds;
+        const size_t nc = R.txn.size(), nre = c->h_rtxw.size();
+        std::vector<uint32_t> r_cmd(std::max<size_t>(nre, 1), ~0u), flags(std::max<size_t>(nc, 1), 0), dep_off(nc + 1, 0);
+        std::vector<uint64_t> ex_hi(std::max<size_t>(nc, 1)), ex_lo(std::max<size_t>(nc, 1)), dhi, dlo;
+        std::vector<int32_t> ex_node(std::max<size_t>(nc, 1)), dnode;
+        std::vector<std::pair<uint32_t, uint32_t>> by_rank;       // (rank, command) of the live commands
+        for (size_t i = 0; i < nc; ++i)
+        {
+            const bool live = (R.historical.empty() || !R.historical[i]) && (R.erased.empty() || !R.erased[i]);
+            if (live) by_rank.push_back({c->h_cmd_rank[i], (uint32_t)i});
+            if (R.rec)
+            {
+                flags[i] = (R.rec_status[i] & 3u) | (R.rec_has_deps[i] ? 4u : 0u);
+                const NormTid x = norm(R.rec_exec[i]);
+                ex_hi[i] = x.hi; ex_lo[i] = x.lo; ex_node[i] = x.node;
+                for (uint64_t j = R.rec_dep_off[i]; j < R.rec_dep_off[i + 1]; ++j)
+                {
+                    const NormTid d = norm(R.rec_deps[j]);
+                    dhi.push_back(d.hi); dlo.push_back(d.lo); dnode.push_back(d.node);
+                }
+            }
+            dep_off[i + 1] = (uint32_t)dhi.size();
+        }
+        std::sort(by_rank.begin(), by_rank.end());
+        for (size_t e = 0; e < nre; ++e)
+        {
+            if (!c->h_rlive[e]) continue;
+            const uint32_t rk = c->h_rtxw[e] & RANK_MASK;
+            auto it = std::lower_bound(by_rank.begin(), by_rank.end(), std::make_pair(rk, 0u));
+            if (it != by_rank.end() && it->first == rk) r_cmd[e] = it->second;
+        }
+        if (dhi.empty()) { dhi.push_back(0); dlo.push_back(0); dnode.push_back(0); }
+        if ((rc = upload(c, c->rv_rcmd, r_cmd)) || (rc = upload(c, c->rv_rflags, flags)) ||
+            (rc = upload(c, c->rv_rex_hi, ex_hi)) || (rc = upload(c, c->rv_rex_lo, ex_lo)) ||
+            (rc = upload(c, c->rv_rex_node, ex_node)) || (rc = upload(c, c->rv_rdep_off, dep_off)) ||
+            (rc = upload(c, c->rv_rdep_hi, dhi)) || (rc = upload(c, c->rv_rdep_lo, dlo)) ||
+            (rc = upload(c, c->rv_rdep_node, dnode)))
+            return rc;
+        c->rv_ranges = live_cmds && nre > 0;
+    c->rv_rng_gen = c->rank_gen;
+    return 0;
+}
+
+// The view from the device state (a live store: ad_cfk_update / ad_cfk_prune keep it current, nothing
+// goes through the host): entries, segments, prunedBefore, trees and the inverted missing() index.
+static int build_recovery_view_device(ad_ctx* c)
+{
+    const uint64_t ne = c->ds.n_ent, nk = c->ds.n_keys;
+    hipStream_t st = c->stream;
+    RvDevIn in{ne, nk, c->ds.ent, c->ds.krec, c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
+               c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr, c->d_moff.as<uint64_t>(), c->d_mids.as<uint32_t>()};
+    int nl = 1;
+    std::vector<uint64_t> lvl_n(1, ne);
+    while (lvl_n.back() > 1 && nl < MAX_LEVELS)
+    {
+        lvl_n.push_back((lvl_n.back() + 63) / 64);
+        ++nl;
+    }
+    if (nl < 2)
+    {
+        lvl_n.push_back(1);
+        nl = 2;
+    }
+    std::vector<uint64_t> lvl_at(nl + 1, 0);
+    for (int l = 1; l < nl; ++l) lvl_at[l + 1] = lvl_at[l] + lvl_n[l];
+    const uint64_t per_set = lvl_at[nl];
+    if (!ens<uint4>(c->rv_ent, ne) || !ens<uint32_t>(c->rv_seg, nk + 1) || !ens<uint32_t>(c->rv_pruned, nk) ||
+        !ens<uint32_t>(c->rv_cnt, ne) || !ens<uint64_t>(c->rv_eoff, ne + 1) || !ens<uint64_t>(c->rv_bsum, (ne + 1023) / 1024 + 16) ||
+        !ens<uint32_t>(c->rv_err, 1) || !ens<uint32_t>(c->rv_tree, 2 * per_set) || !ens<uint64_t>(c->rv_inv_off, nk + 1))
+        return c->fail(AD_E_NOMEM, "recovery view");
+    uint32_t* tree = c->rv_tree.as<uint32_t>();
+    std::vector<uint32_t*> l0(nl, nullptr), l1(nl, nullptr);
+    for (int l = 1; l < nl; ++l)
+    {
+        l0[l] = tree + lvl_at[l];
+        l1[l] = tree + per_set + lvl_at[l];
+    }
+    HIPCHK(c, hipMemsetAsync(c->rv_err.p, 0, 4, st));
+    HIPCHK(c, run_rv_entries(in, c->rv_ent.as<uint4>(), c->rv_seg.as<uint32_t>(), c->rv_pruned.as<uint32_t>(),
+                             c->rv_cnt.as<uint32_t>(), c->rv_err.as<uint32_t>(), st));
+    HIPCHK(c, run_rv_trees(in, l0.data(), l1.data(), lvl_n.data(), nl, st));
+    HIPCHK(c, run_scan_arrays(c->rv_cnt.as<uint32_t>(), c->rv_eoff.as<uint64_t>(), ne, 1, c->rv_bsum.as<uint64_t>(), st));
+    uint64_t np = 0;
+    uint32_t err = 0;
+    HIPCHK(c, hipMemcpyAsync(&np, c->rv_eoff.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(&err, c->rv_err.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (err) return c->fail(AD_E_CAPACITY, "more than %u missing ids on one entry", RV_MAX_MISS);
+    // per key, its (missing() id, entry) pairs sorted by id (entries ascending within): a stable radix
+    // sort of (key index << 32 | id rank) over the pairs written in entry order
+    if (!ens<uint64_t>(c->rv_pk, np) || !ens<uint32_t>(c->rv_pv, np) || !ens<uint64_t>(c->rv_pk2, np) ||
+        !ens<uint32_t>(c->rv_pv2, np) || !ens<uint2>(c->rv_inv, np))
+        return c->fail(AD_E_NOMEM, "recovery view");
+    uint64_t* ks = c->rv_pk.as<uint64_t>();
+    uint32_t* vs = c->rv_pv.as<uint32_t>();
+    HIPCHK(c, run_rv_inv_pairs(in, c->rv_eoff.as<uint64_t>(), ks, vs, st));
+    if (np > 1)
+    {
+        auto nbytes = [](uint64_t v) { uint32_t b = 0; while (v) { ++b; v >>= 8; } return b; };
+        uint32_t mask = 0;
+        for (uint32_t b = 0; b < nbytes(2 * c->ds.n_dict + 1) && b < 4; ++b) mask |= 1u << b;
+        for (uint32_t b = 0; b < nbytes(nk ? nk - 1 : 0) && b < 4; ++b) mask |= 1u << (4 + b);
+        const uint64_t hn = radix_hist_entries(np);
+        if (!ens<uint32_t>(c->rv_hist, hn) || !ens<uint64_t>(c->rv_hoff, hn + 1) ||
+            !ens<uint64_t>(c->rv_bsum, (std::max(hn, np) + 1023) / 1024 + 16))
+            return c->fail(AD_E_NOMEM, "recovery view");
+        HIPCHK(c, radix_sort_pairs(ks, vs, c->rv_pk2.as<uint64_t>(), c->rv_pv2.as<uint32_t>(), np, mask, c->rv_hist.as<uint32_t>(),
+                                   c->rv_hoff.as<uint64_t>(), c->rv_bsum.as<uint64_t>(), st, &ks, &vs));
+    }
+    HIPCHK(c, run_rv_inv_finish(in, c->rv_eoff.as<uint64_t>(), ks, vs, np, c->rv_inv_off.as<uint64_t>(), c->rv_inv.as<uint2>(), st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->rv_levels = nl;
+    c->rv_lvl_at.assign(lvl_at.begin(), lvl_at.end());
+    c->rv_per_set = per_set;
+    c->rv_dev_miss = c->dmiss_on;
+    return 0;
+}
+
 static int build_recovery_view(ad_ctx* c, RecoveryView* v)
 {
-    if (int rc0 = sync_host(c)) return rc0;
     auto& K = c->cfk;
+    // a live store (lists on the device, or none at all): the view from the device state
+    const bool dev = !c->dirty && !getenv("AD_RV_HOST") && (c->dmiss_on || (K.miss_off.empty() && !K.miss_stale));
+    if (!dev)
+        if (int rc0 = sync_host(c)) return rc0;
     bool live_cmds = false;
     for (size_t i = 0; i < c->cmds.txn.size(); ++i)
         live_cmds |= (c->cmds.historical.empty() || !c->cmds.historical[i]) && (c->cmds.erased.empty() || !c->cmds.erased[i]);
     if (live_cmds && !c->cmds.rec)
         return c->fail(AD_E_STATE, "recovery scans of range commands need their recovery facts (ad_range_cmds_recovery_load)");
-    if (K.miss_stale) return c->fail(AD_E_STATE, "missing lists predate SEQUENTIAL insertions: load them again");
+    if (!dev && K.miss_stale) return c->fail(AD_E_STATE, "missing lists predate SEQUENTIAL insertions: load them again");
     const uint64_t ne = K.status.size(), nk = K.keys.size();
-    if (c->rv_gen != c->snap_gen)
+    if (dev && c->rv_gen != c->snap_gen)
+    {
+        if (int rc = build_recovery_view_device(c)) return rc;
+        c->rv_gen = c->snap_gen;
+    }
+    if (dev && c->rv_rng_gen != c->rank_gen)
+    {
+        if (int rc = build_rv_ranges(c, live_cmds)) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (!dev && c->rv_gen != c->snap_gen)
     {
         std::vector<uint4> ent(ne);
         std::vector<uint32_t> seg(nk + 1), miss;
@@ -2237,55 +2378,15 @@ static int build_recovery_view(ad_ctx* c, RecoveryView* v)
         c->rv_levels = nl;
         c->rv_lvl_at.assign(lvl_at.begin(), lvl_at.end());
         c->rv_per_set = per_set;
-        // live range commands: entry -> command, the commands' facts normalised
-        {
-            const auto& R = c->cmds;
-            const size_t nc = R.txn.size(), nre = c->h_rtxw.size();
-            std::vector<uint32_t> r_cmd(std::max<size_t>(nre, 1), ~0u), flags(std::max<size_t>(nc, 1), 0), dep_off(nc + 1, 0);
-            std::vector<uint64_t> ex_hi(std::max<size_t>(nc, 1)), ex_lo(std::max<size_t>(nc, 1)), dhi, dlo;
-            std::vector<int32_t> ex_node(std::max<size_t>(nc, 1)), dnode;
-            std::vector<std::pair<uint32_t, uint32_t>> by_rank;       // (rank, command) of the live commands
-            for (size_t i = 0; i < nc; ++i)
-            {
-                const bool live = (R.historical.empty() || !R.historical[i]) && (R.erased.empty() || !R.erased[i]);
-                if (live) by_rank.push_back({c->h_cmd_rank[i], (uint32_t)i});
-                if (R.rec)
-                {
-                    flags[i] = (R.rec_status[i] & 3u) | (R.rec_has_deps[i] ? 4u : 0u);
-                    const NormTid x = norm(R.rec_exec[i]);
-                    ex_hi[i] = x.hi; ex_lo[i] = x.lo; ex_node[i] = x.node;
-                    for (uint64_t j = R.rec_dep_off[i]; j < R.rec_dep_off[i + 1]; ++j)
-                    {
-                        const NormTid d = norm(R.rec_deps[j]);
-                        dhi.push_back(d.hi); dlo.push_back(d.lo); dnode.push_back(d.node);
-                    }
-                }
-                dep_off[i + 1] = (uint32_t)dhi.size();
-            }
-            std::sort(by_rank.begin(), by_rank.end());
-            for (size_t e = 0; e < nre; ++e)
-            {
-                if (!c->h_rlive[e]) continue;
-                const uint32_t rk = c->h_rtxw[e] & RANK_MASK;
-                auto it = std::lower_bound(by_rank.begin(), by_rank.end(), std::make_pair(rk, 0u));
-                if (it != by_rank.end() && it->first == rk) r_cmd[e] = it->second;
-            }
-            if (dhi.empty()) { dhi.push_back(0); dlo.push_back(0); dnode.push_back(0); }
-            if ((rc = upload(c, c->rv_rcmd, r_cmd)) || (rc = upload(c, c->rv_rflags, flags)) ||
-                (rc = upload(c, c->rv_rex_hi, ex_hi)) || (rc = upload(c, c->rv_rex_lo, ex_lo)) ||
-                (rc = upload(c, c->rv_rex_node, ex_node)) || (rc = upload(c, c->rv_rdep_off, dep_off)) ||
-                (rc = upload(c, c->rv_rdep_hi, dhi)) || (rc = upload(c, c->rv_rdep_lo, dlo)) ||
-                (rc = upload(c, c->rv_rdep_node, dnode)))
-                return rc;
-            c->rv_ranges = live_cmds && nre > 0;
-        }
+        if ((rc = build_rv_ranges(c, live_cmds))) return rc;
         HIPCHK(c, hipStreamSynchronize(c->stream));
         c->rv_gen = c->snap_gen;
+        c->rv_dev_miss = false;
     }
     v->ent = c->rv_ent.as<uint4>();
     v->seg = c->rv_seg.as<uint32_t>();
     v->pruned = c->rv_pruned.as<uint32_t>();
-    v->miss = c->rv_miss.as<uint32_t>();
+    v->miss = c->rv_dev_miss ? c->d_mids.as<uint32_t>() : c->rv_miss.as<uint32_t>();
     for (int set = 0; set < 2; ++set)
         for (int l = 0; l < MAX_LEVELS; ++l)
             v->lvl[set][l] = (l >= 1 && l < c->rv_levels) ? c->rv_tree.as<uint32_t>() + set * c->rv_per_set + c->rv_lvl_at[l]
@@ -2334,6 +2435,7 @@ int ad_cfk_missing_load(ad_ctx* c, const ad_cfk_missing_soa* m)
     for (uint64_t j = 0; j < nm; ++j) K.miss[j] = {m->msb[j], m->lsb[j], m->node[j]};
     K.miss_stale = false;
     c->rv_gen = ~0ull;
+    c->rv_rng_gen = ~0ull;
     return AD_OK;
 }
 
@@ -2366,6 +2468,7 @@ int ad_range_cmds_recovery_load(ad_ctx* c, const ad_range_cmds_recovery_soa* in)
     for (uint64_t j = 0; j < nd; ++j) R.rec_deps[j] = {in->dep_msb[j], in->dep_lsb[j], in->dep_node[j]};
     R.rec = true;
     c->rv_gen = ~0ull;
+    c->rv_rng_gen = ~0ull;
     return AD_OK;
 }
 
@@ -3144,6 +3247,7 @@ static int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipSt
     for (auto& r : c->h_pruned) r = remap(r);
     for (auto& r : c->h_cmd_rank) r = remap(r);
     for (auto& y : c->h_rtxw) y = remap_txw(y);
+    ++c->rank_gen;
     return 0;
 }
 

@@ -2087,4 +2087,140 @@ hipError_t run_add_bases(uint64_t* off, uint64_t n1, const uint64_t* base, hipSt
     return hipGetLastError();
 }
 
+// ---- RecoveryView of a live store (BeginRecovery.java:329-380 over CommandsForKey.mapReduceFull
+// :809-908): built from the per-entry device state after ad_cfk_update / ad_cfk_prune ---------------
+__global__ __launch_bounds__(256) void k_rv_entries(RvDevIn in, uint4* ent, uint32_t* cnt, uint32_t* err)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= in.n_ent) return;
+    const uint32_t txw = in.ent[e].y;
+    uint32_t nm = 0, mo = 0;
+    if (in.mref)
+    {
+        const uint32_t L = in.mref[e];
+        if (L != 0xFFFFFFFFu && L != 0xFFFFFFFEu)          // MREF_NONE / MREF_BORN: NO_TXNIDS
+        {
+            const uint64_t a = in.moff[L], b = in.moff[L + 1];
+            if (b - a > RV_MAX_MISS) atomicOr(err, 1u);
+            nm = (uint32_t)min<uint64_t>(b - a, RV_MAX_MISS);
+            mo = (uint32_t)a;
+        }
+    }
+    ent[e] = make_uint4(txw & RANK_MASK, in.xrank[e], (uint32_t)in.status[e] | ((txw >> RANK_BITS) << 8) | (nm << RV_MISS_SHIFT), mo);
+    cnt[e] = nm;
+}
+
+__global__ void k_rv_keys(RvDevIn in, uint32_t* seg, uint32_t* pruned)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < in.n_keys)
+    {
+        seg[k] = in.krec[k].seg_lo;
+        pruned[k] = in.krec[k].pruned;
+    }
+    if (k == in.n_keys) seg[k] = (uint32_t)in.n_ent;
+}
+
+hipError_t run_rv_entries(const RvDevIn& in, uint4* ent, uint32_t* seg, uint32_t* pruned, uint32_t* cnt, uint32_t* err,
+                          hipStream_t st)
+{
+    if (in.n_ent) k_rv_entries<<<(unsigned)((in.n_ent + 255) / 256), 256, 0, st>>>(in, ent, cnt, err);
+    k_rv_keys<<<(unsigned)((in.n_keys + 1 + 255) / 256), 256, 0, st>>>(in, seg, pruned);
+    return hipGetLastError();
+}
+
+// level 1: one wave per 64-entry block, the max executeAt rank of the block's entries in each set
+__global__ __launch_bounds__(256) void k_rv_tree_leaf(RvDevIn in, uint32_t* l0, uint32_t* l1, uint64_t n_blocks)
+{
+    const uint64_t blk = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (blk >= n_blocks) return;
+    const uint64_t e = blk * 64 + lane_id();
+    uint32_t a = 0, b = 0;
+    if (e < in.n_ent)
+    {
+        const uint32_t stt = in.status[e], x = in.xrank[e];
+        a = (stt == 3 || stt == 4) ? x : 0u;          // ACCEPTED, COMMITTED
+        b = (stt == 5 || stt == 6) ? x : 0u;          // STABLE, APPLIED
+    }
+#pragma unroll
+    for (int d = 32; d; d >>= 1)
+    {
+        a = max(a, (uint32_t)__shfl_xor(a, d, 64));
+        b = max(b, (uint32_t)__shfl_xor(b, d, 64));
+    }
+    if (lane_id() == 0)
+    {
+        l0[blk] = a;
+        l1[blk] = b;
+    }
+}
+
+__global__ void k_rv_tree_up(const uint32_t* c0, const uint32_t* c1, uint64_t n_child, uint32_t* p0, uint32_t* p1, uint64_t n_parent)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_parent) return;
+    uint32_t a = 0, b = 0;
+    for (uint64_t i = j * 64; i < min<uint64_t>(n_child, j * 64 + 64); ++i)
+    {
+        a = max(a, c0[i]);
+        b = max(b, c1[i]);
+    }
+    p0[j] = a;
+    p1[j] = b;
+}
+
+hipError_t run_rv_trees(const RvDevIn& in, uint32_t* const* lvl0, uint32_t* const* lvl1, const uint64_t* lvl_n, int n_levels,
+                        hipStream_t st)
+{
+    if (n_levels < 2) return hipSuccess;
+    k_rv_tree_leaf<<<(unsigned)std::max<uint64_t>(1, (lvl_n[1] + 3) / 4), 256, 0, st>>>(in, lvl0[1], lvl1[1], lvl_n[1]);
+    for (int l = 2; l < n_levels; ++l)
+        k_rv_tree_up<<<(unsigned)std::max<uint64_t>(1, (lvl_n[l] + 255) / 256), 256, 0, st>>>(lvl0[l - 1], lvl1[l - 1], lvl_n[l - 1],
+                                                                                             lvl0[l], lvl1[l], lvl_n[l]);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_rv_inv_pairs(RvDevIn in, const uint64_t* eoff, uint64_t* key, uint32_t* val)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= in.n_ent) return;
+    const uint64_t o = eoff[e], nm = eoff[e + 1] - o;
+    if (!nm) return;
+    const uint32_t L = in.mref[e];
+    const uint64_t a = in.moff[L];
+    const uint64_t k = (uint64_t)in.ekey[e] << 32;
+    for (uint64_t j = 0; j < nm; ++j)
+    {
+        key[o + j] = k | in.mids[a + j];
+        val[o + j] = (uint32_t)e;
+    }
+}
+
+__global__ void k_rv_inv_off(RvDevIn in, const uint64_t* eoff, uint64_t* inv_off)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < in.n_keys) inv_off[k] = eoff[in.krec[k].seg_lo];
+    if (k == in.n_keys) inv_off[k] = eoff[in.n_ent];
+}
+
+__global__ void k_rv_inv_out(const uint64_t* skey, const uint32_t* sval, uint64_t n, uint2* inv)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < n) inv[p] = make_uint2((uint32_t)skey[p], sval[p]);
+}
+
+hipError_t run_rv_inv_pairs(const RvDevIn& in, const uint64_t* eoff, uint64_t* key, uint32_t* val, hipStream_t st)
+{
+    if (in.n_ent && in.mref) k_rv_inv_pairs<<<(unsigned)((in.n_ent + 255) / 256), 256, 0, st>>>(in, eoff, key, val);
+    return hipGetLastError();
+}
+
+hipError_t run_rv_inv_finish(const RvDevIn& in, const uint64_t* eoff, const uint64_t* skey, const uint32_t* sval,
+                             uint64_t n_pairs, uint64_t* inv_off, uint2* inv, hipStream_t st)
+{
+    k_rv_inv_off<<<(unsigned)((in.n_keys + 1 + 255) / 256), 256, 0, st>>>(in, eoff, inv_off);
+    if (n_pairs) k_rv_inv_out<<<(unsigned)((n_pairs + 255) / 256), 256, 0, st>>>(skey, sval, n_pairs, inv);
+    return hipGetLastError();
+}
+
 }  // namespace adx

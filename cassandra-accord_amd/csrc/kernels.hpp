@@ -94,6 +94,27 @@ struct RecoveryView {
 constexpr uint32_t RV_MISS_SHIFT = 12;
 constexpr uint32_t RV_MAX_MISS = (1u << 20) - 1;
 
+// The RecoveryView of a live store, from the device state ad_cfk_update keeps current (no host copy):
+// per entry {txnId rank, executeAt rank, status | kind << 8 | #missing << 12, offset of its list in the
+// device missing() ids}, per key its segment start and prunedBefore rank; the two per-status-set max
+// trees; the per-key inverted missing() index. mref / moff: the device lists (null: no lists).
+// *err gets 1 when a list exceeds RV_MAX_MISS.
+struct RvDevIn {
+    uint64_t n_ent, n_keys;
+    const uint2* ent; const KeyRec* krec; const uint8_t* status; const uint32_t* xrank; const uint32_t* ekey;
+    const uint32_t* mref; const uint64_t* moff; const uint32_t* mids;
+};
+hipError_t run_rv_entries(const RvDevIn& in, uint4* ent, uint32_t* seg, uint32_t* pruned, uint32_t* cnt, uint32_t* err,
+                          hipStream_t st);
+// levels l >= 1 of the two trees: lvl[set][l] (l < n_levels), lvl_n[l] nodes each
+hipError_t run_rv_trees(const RvDevIn& in, uint32_t* const* lvl0, uint32_t* const* lvl1, const uint64_t* lvl_n, int n_levels,
+                        hipStream_t st);
+// the inverted pairs in entry order (key << 32 | miss rank, entry) at eoff[e] (exclusive scan of cnt)
+hipError_t run_rv_inv_pairs(const RvDevIn& in, const uint64_t* eoff, uint64_t* key, uint32_t* val, hipStream_t st);
+// inv_off[k] = eoff[segment start of k], inv_off[n_keys] = eoff[n_ent]; inv[p] = {rank, entry} of the sorted pairs
+hipError_t run_rv_inv_finish(const RvDevIn& in, const uint64_t* eoff, const uint64_t* skey, const uint32_t* sval,
+                             uint64_t n_pairs, uint64_t* inv_off, uint2* inv, hipStream_t st);
+
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
 hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);
 
