@@ -222,6 +222,7 @@ struct ad_ctx {
         DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
+    DevBuf p_slot;                             // lean passes: per probe its KeyLine (k_lean_slots)
     DevBuf arena, rarena;
     DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, q_rec, big;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];
@@ -1393,6 +1394,11 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         return c->fail(AD_E_NOMEM, "batch buffers");
     b.big = c->big.as<uint32_t>();
     b.k2_big = K2_BIG;
+    if (lean && !c->ds.n_rent)
+    {
+        if (!ens<uint32_t>(c->p_slot, std::max<uint64_t>(np, 1))) return c->fail(AD_E_NOMEM, "probe slots");
+        b.p_slot = c->p_slot.as<uint32_t>();
+    }
     if (const char* e = getenv("AD_K2_BIG")) b.k2_big = (uint32_t)strtoul(e, nullptr, 10);   // tests: force k_build_big
     b.q_rec = c->q_rec.as<uint4>();
     b.deferred1 = c->deferred1.as<uint32_t>();

@@ -38,6 +38,7 @@ struct BatchBufs {
     const int64_t* q_min_epoch;      // may be null
     const uint64_t* q_key_off;
     const int64_t* q_keys;
+    uint32_t* p_slot;                // lean passes without range commands: per probe its KeyLine (LS_NONE: outside the slice)
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
     uint32_t* p_txn; uint4* p_rec;

@@ -37,6 +37,27 @@ constexpr uint32_t LEAN_CHUNK = 1u << 16;
 #define LEAN_EXP 0
 #endif
 
+// Per probe, its KeyLine (stores without range commands, LEAN_SLOTS): the slice test
+// (InMemoryCommandStore.java:280) and the perfect-hash displacement, one thread per probe, so that the
+// lean passes load a probe's key and its line position side by side -- one dependent load shorter,
+// and no displacement gather inside them. The line still proves the key is the store's.
+#ifndef LEAN_SLOTS
+#define LEAN_SLOTS 1
+#endif
+constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void k_lean_slots(DevSnapshot s, const int64_t* keys, uint64_t np, uint32_t* slot)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const int64_t key = keys[p];
+    bool in = s.n_slices == 0;
+    for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+    uint32_t r = LS_NONE;
+    if (in) r = (uint32_t)kl_index(key_hash2(key), s.kl_disp[kl_bucket(key_hash(key), s.kl_buckets)], s.kl_lines);
+    slot[p] = r;
+}
+
 // ascending bitonic sort within each LPR-lane segment (a request's lanes)
 template <uint32_t K, uint32_t LPR>
 __device__ __forceinline__ void seg_bitonic(uint32_t& key)
@@ -148,9 +169,10 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
 // RNG: the store has range commands (with a stabbing index): each request also gets its
 // rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
 // WIDE (RPW 2, no range commands: lean pass 2): requests with up to 64 raw emissions, two per lane.
-template <uint32_t RPW, bool RNG, bool WIDE>
-__global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolve_lean(DevSnapshot s, BatchBufs b, uint32_t pass)
+template <uint32_t RPW, bool RNG, bool WIDE, int PASS>
+__global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolve_lean(DevSnapshot s, BatchBufs b)
 {
+    constexpr uint32_t pass = PASS;
     // pass 1: all requests -> deferred1; pass 2: deferred1 -> deferred2 (lists derived from b
     // where used, so they hold no scalar registers across the loop)
     auto lists = [&]() -> LeanLists {
@@ -219,10 +241,18 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     // (clamped addresses, results masked where used) so the compiler's wait counts stay exact.
     using Raw = uint4;        // the request record of k_prepare
     struct Req { uint64_t k0; uint32_t np, cls, t, S, self; bool act, defer; };
-    auto req_of = [&](uint32_t it) -> uint32_t {
+    // the request of item `it` in this segment: pass 1 its index; pass 2 the deferred1 entry, loaded
+    // (branch-free) by dload an iteration before its record is (req_of then only masks the hole)
+    auto dload = [&](uint32_t it) -> uint32_t {
+        if (PASS == 1) return 0u;
         const uint32_t si = it * RPW + h;
-        if (si >= n_slots) return DEFER_HOLE;
-        return pass == 1 ? (uint32_t)si : b.deferred1[si];
+        const uint32_t v = b.deferred1[si < n_slots ? si : 0u];
+        return si < n_slots ? v : DEFER_HOLE;
+    };
+    auto req_of = [&](uint32_t it, uint32_t loaded) -> uint32_t {
+        if (PASS == 2) return loaded;
+        const uint32_t si = it * RPW + h;
+        return si >= n_slots ? DEFER_HOLE : si;
     };
     auto loadA = [&](uint32_t t) -> Raw { return b.q_rec[t != DEFER_HOLE ? t : 0u]; };
     // the record carries PreAccept.java:251-261's witness class, S and self as ranks (k_prepare)
@@ -238,10 +268,16 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         q.defer = (r.z & REC_FAST) == 0;
         return q;
     };
-    // the key (one lane per key)
-    auto loadB = [&](const Req& q, int64_t& key) {
+    // the key (one lane per key), and with LEAN_SLOTS its line position beside it
+    constexpr bool SLOTS = !RNG && LEAN_SLOTS;
+    auto loadB = [&](const Req& q, int64_t& key, uint32_t& sl) {
         const bool on = q.act && !q.defer && hl < q.np;
         key = b.q_keys[on ? q.k0 + hl : 0];
+        if (SLOTS)
+        {
+            const uint32_t v = b.p_slot[on ? q.k0 + hl : 0];     // branch-free: exact wait counts
+            sl = on ? v : LS_NONE;
+        }
     };
     // the key's line (KeyLine, common.hpp): the slice test (InMemoryCommandStore.java:280), then one
     // random line per key -- its first 64 bytes: key, cell entries, newest fields, meta, the class's
@@ -259,15 +295,22 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         H.h2 = reinterpret_cast<const uint2*>(L4 + 2)[cls];
         H.h3 = reinterpret_cast<const uint2*>(L4 + 3)[1];       // {cwr tail start, prunedBefore rank}
     };
-    // the key's displacement (a small table: cache-resident), issued ahead of its line
-    auto loadD = [&](const Req& q, int64_t key, bool& look, uint32_t& d) {
+    // the key's displacement (a small table: cache-resident), issued ahead of its line; with LEAN_SLOTS
+    // the line position came with the key (k_lean_slots)
+    auto loadD = [&](const Req& q, int64_t key, uint32_t sl, bool& look, uint32_t& d) {
+        if (SLOTS)
+        {
+            look = sl != LS_NONE;
+            d = sl;
+            return;
+        }
         const bool on = q.act && !q.defer && hl < q.np;
         look = on && in_slice_of(key);
         d = s.kl_disp[look ? kl_bucket(key_hash(key), s.kl_buckets) : 0u];
     };
     auto loadC = [&](const Req& q, int64_t key, bool look, uint32_t d, Hdr& H) {
         H.look = look;
-        H.slot = look ? (uint32_t)kl_index(key_hash2(key), d, s.kl_lines) : 0u;
+        H.slot = !look ? 0u : SLOTS ? d : (uint32_t)kl_index(key_hash2(key), d, s.kl_lines);
         load_line(H.slot, q.cls, H);
     };
     // (found, cell bounds) of a loaded line: the perfect hash put the key on this line if the
@@ -302,29 +345,64 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         if (with_ro && on && hl == 3) b.t_reg[(uint64_t)m * n + t] = ro;
     };
 
+    // Pipeline registers at the top of iteration `it`: item it's request and lines (qc, keyc, Hc); item
+    // it + nw's request and keys / line positions (q1, key1, sl1); item it + 2 nw's record (t2, r2);
+    // pass 2: item it + 3 nw's deferred1 entry (t3). Every load of a later item is issued after this
+    // item's element loads and before its stores, and waited for an iteration later -- no wait of the
+    // loop covers the stores just issued (vmcnt counts loads and stores in order).
     const uint32_t it0 = uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
-    uint32_t tc = req_of(it0);
+    const uint32_t tc = req_of(it0, dload(it0));
     Req qc = derive(tc, loadA(tc));
     int64_t keyc;
-    loadB(qc, keyc);
-    bool lookc;
-    uint32_t dc;
-    loadD(qc, keyc, lookc, dc);
+    uint32_t slc = LS_NONE;
+    loadB(qc, keyc, slc);
     Hdr Hc;
-    loadC(qc, keyc, lookc, dc, Hc);
-    uint32_t tN = req_of(it0 + nw);
-    Raw rN = loadA(tN);
+    {
+        bool lookc;
+        uint32_t dc;
+        loadD(qc, keyc, slc, lookc, dc);
+        loadC(qc, keyc, lookc, dc, Hc);
+    }
+    const uint32_t t1 = req_of(it0 + nw, dload(it0 + nw));
+    Req q1 = derive(t1, loadA(t1));
+    int64_t key1;
+    uint32_t sl1 = LS_NONE;
+    loadB(q1, key1, sl1);
+    uint32_t t2 = req_of(it0 + 2 * nw, dload(it0 + 2 * nw));
+    Raw r2 = loadA(t2);
+    uint32_t t3 = dload(it0 + 3 * nw);
+    // the later items' loads (see above); H1 receives item it + nw's lines
+    int64_t key2;
+    uint32_t sl2 = LS_NONE, t3u = 0, t4 = 0;
+    Req q2;
+    Raw r3;
+    auto prefetch = [&](uint32_t it, Hdr& H1) {
+        bool look1;
+        uint32_t d1;
+        loadD(q1, key1, sl1, look1, d1);
+        loadC(q1, key1, look1, d1, H1);
+        q2 = derive(t2, r2);
+        sl2 = LS_NONE;
+        loadB(q2, key2, sl2);
+        t3u = req_of(it + 3 * nw, t3);
+        r3 = loadA(t3u);
+        t4 = dload(it + 4 * nw);
+    };
+    auto rotate = [&](Hdr& H1) {
+        qc = q1;
+        keyc = key1;
+        Hc = H1;
+        q1 = q2;
+        key1 = key2;
+        sl1 = sl2;
+        t2 = t3u;
+        r2 = r3;
+        t3 = t4;
+    };
 
     for (uint32_t it = it0; it < n_items; it += nw)
     {
         const uint32_t t = qc.t;
-        const Req qn = derive(tN, rN);
-        tN = req_of(it + 2 * nw);
-        rN = loadA(tN);
-        int64_t keyn;
-        loadB(qn, keyn);
-        bool lookn;
-        uint32_t dn_;
 
         // ---- current item: per key p = hl < np, newest test and emission counts
         bool act = qc.act;
@@ -356,8 +434,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         const uint32_t rinc = RNG ? key_lanes_incl_scan(rn, hl) : 0u;
         const uint32_t rstart = rinc - rn;
         const uint32_t TR = RNG ? __shfl(rinc, sb | 7u, 64) : 0u;
-        // the next item's displacements (its keys have arrived by now)
-        loadD(qn, keyn, lookn, dn_);
         constexpr bool CAN_WIDE = WIDE && RPW == 2 && !RNG;
         defer = defer || seg(ballot(kact && !newest)) != 0 || T > (CAN_WIDE ? 2 * LPR : LPR) || TR > LPR;
         {
@@ -404,7 +480,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             uint32_t ax0, ax1;
             const uint32_t tw0 = raw_txw(hl, ax0), tw1 = raw_txw(hl + 32, ax1);
             Hdr Hn;
-            loadC(qn, keyn, lookn, dn_, Hn);
+            prefetch(it, Hn);
             const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
             const bool want0 = wact && hl < T && r0 != self && r0 < S, want1 = wact && hl + 32 < T && r1 != self && r1 < S;
             const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
@@ -485,9 +561,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
                 }
             }
             put_sizes(wact, t, 1, 0, 0, 0, 0, false);          // no range commands on this path
-            qc = qn;
-            keyc = keyn;
-            Hc = Hn;
+            rotate(Hn);
             continue;
         }
 
@@ -531,9 +605,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             rlive = act && hl < TR;
             ce = s.cell_ent[rlive ? ar_lo + (hl - ar_start) : 0u];
         }
-        // the next item's key lines go out behind this item's element loads
+        // the later items' loads go out behind this item's element loads
         Hdr Hn;
-        loadC(qn, keyn, lookn, dn_, Hn);
+        prefetch(it, Hn);
 
         const uint32_t txw = !live ? 0u : ((from_cand || cls != 0) ? lv : (a_lw | (1u << RANK_BITS)));
         const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
@@ -689,21 +763,19 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
                 if (v2) ok2t[nR + (uint32_t)(k2 & 0xFF)] = (int32_t)ur2;
             }
         }
-        qc = qn;
-        keyc = keyn;
-        Hc = Hn;
+        rotate(Hn);
     }
     dflush();
 }
 
-template <uint32_t RPW, bool RNG, bool WIDE = false>
-static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, uint32_t pass, hipStream_t st)
+template <uint32_t RPW, bool RNG, bool WIDE, int PASS>
+static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     static int per_cu = 0;
     if (!per_cu)
     {
         int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG, WIDE>, 64 * LEAN_WAVES, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG, WIDE, PASS>, 64 * LEAN_WAVES, 0) != hipSuccess ||
             nb <= 0)
             nb = 2;
         per_cu = std::min(nb, WIDE ? 4 : 5);     // measured: more resident waves only add memory contention
@@ -711,7 +783,7 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, uint32_t
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu));
-    k_resolve_lean<RPW, RNG, WIDE><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b, pass);
+    k_resolve_lean<RPW, RNG, WIDE, PASS><<<grid, 64 * LEAN_WAVES, 0, st>>>(s, b);
     return hipGetLastError();
 }
 
@@ -722,11 +794,16 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     if (!b.n_txns) return hipSuccess;
     if (pass == 1)
     {
-        if (rpw1 == 4) return s.n_rent ? launch_lean<4, true>(s, b, 1, st) : launch_lean<4, false>(s, b, 1, st);
-        return s.n_rent ? launch_lean<2, true>(s, b, 1, st) : launch_lean<2, false>(s, b, 1, st);
+        if (!s.n_rent && LEAN_SLOTS)
+        {
+            if (!b.p_slot) return hipErrorInvalidValue;
+            if (b.n_probes) k_lean_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b.q_keys, b.n_probes, b.p_slot);
+        }
+        if (rpw1 == 4) return s.n_rent ? launch_lean<4, true, false, 1>(s, b, st) : launch_lean<4, false, false, 1>(s, b, st);
+        return s.n_rent ? launch_lean<2, true, false, 1>(s, b, st) : launch_lean<2, false, false, 1>(s, b, st);
     }
     // pass 2 (requests with 33..64 raw emissions): two per wave, two emissions per lane
-    return s.n_rent ? launch_lean<1, true>(s, b, 2, st) : launch_lean<2, false, true>(s, b, 2, st);
+    return s.n_rent ? launch_lean<1, true, false, 2>(s, b, st) : launch_lean<2, false, true, 2>(s, b, st);
 }
 
 }  // namespace adx
