@@ -299,9 +299,11 @@ def bench_levels(args, rank, world, local, dev):
         pairs = int(p.item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     dom = int(np.argmax(ms))
-    names = ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"]
+    pull = launches == args.steps          # one leveling launch per step: the rank-ordered dataflow (default)
+    names = (["k5 build (exec radix sort + key chains + predecessor CSR)", "k5 rank-ordered dataflow (k_level_pull)"] if pull
+             else ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"])
     achieved = stats["bytes_stage"][dom] / (ms[dom] / 1000.0) / 1e9 if ms[dom] > 0 else 0.0
-    traffic, traffic_src = measured_traffic(["k_level_step"] if dom == 1 else ["k_radix_scatter"])
+    traffic, traffic_src = measured_traffic([("k_level_pull" if pull else "k_level_step")] if dom == 1 else ["k_radix_scatter"])
     res = {
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
@@ -315,7 +317,7 @@ def bench_levels(args, rank, world, local, dev):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": stats["bytes_stage"][dom], "launch_ms": ms[dom]},
         "stages_ms": {names[0]: round(float(ms[0]), 4), names[1]: round(float(ms[1]), 4)},
-        "levels": stats["n_levels"], "edges": stats["n_edges"], "frontier_launches_per_step": launches / max(args.steps, 1),
+        "levels": stats["n_levels"], "edges": stats["n_edges"], "leveling_launches_per_step": launches / max(args.steps, 1),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_levels(g, args.cpu_budget)
@@ -914,6 +916,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (tests / dry runs)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--output", choices=("regions", "packed"), default="regions",
+                    help="config 2 on one GPU: read the result through its regions (AD_REGIONS, default) or the packed arrays")
     ap.add_argument("--config", type=int, default=None, choices=(1, 2, 3, 4, 5),
                     help="default: 2 on one GPU (BASELINE config 2, the headline), 3 on N > 1 GPUs (N/8 of BASELINE "
                          "config 3, exactly config 3 at N = 8, through the library's RCCL node exchange); "
@@ -1061,8 +1065,10 @@ def bench_deps(args, rank, world, local, dev):
             mg = ex.step()
             return engine.last_stats, mg.ms_device, None
     else:
+        regions = args.output == "regions"
+
         def step():
-            last["res"], st = store.deps_batch_device(qdev, sp)
+            last["res"], st = store.deps_batch_device(qdev, sp, regions=regions)
             return st, 0.0, None
 
     stats = None
@@ -1156,6 +1162,20 @@ def bench_deps(args, rank, world, local, dev):
                      "lean_to_general": int(stats.get("n_deferred_lean", 0)), "to_split": int(stats["n_deferred"])},
         "ingest_ms": ingest_ms,
     }
+    if node_x is None and world == 1:
+        # the output contract of the timed steps, and the packed layout's cost beside it
+        r = last["res"]
+        out["config"]["output"] = ("regions (AD_REGIONS): each request's keyDeps / rangeDeps / directKeyDeps written once "
+                                   "where the kernels build them, plus per-request sizes and packed offsets"
+                                   if args.output == "regions" else "packed arrays (request order)")
+        out["regions_bytes"] = {"in_use": int(r.regions_bytes), "payload": int(r.region_bytes)}
+        other = "packed" if args.output == "regions" else "regions"
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            store.deps_batch_device(qdev, sp, regions=(other == "regions"))
+        torch.cuda.synchronize(dev)
+        out["%s_ms_per_step" % other] = 1000.0 * (time.perf_counter() - t0) / 5
     if node_x is not None or world > 1:
         out["stages_ms"]["merge (K3, owner)"] = round(merge_ms, 4)
         out["exchange"] = {"ms_export": round(xs["ms_export"], 4), "ms_move": round(xs["ms_move"], 4),

@@ -27,6 +27,7 @@ MAP_NAMES = ("keyDeps", "rangeDeps", "directKeyDeps")
 AD_SNAPSHOT, AD_SEQUENTIAL = 0, 1
 AD_PARTS_ONLY = 2        # ad_deps_batch_device: result only exported as parts (no packed arrays)
 AD_N_KEYS = 4            # ad_deps_batch_device: AdQuerySoa.n_keys = key_off[n_txns]
+AD_REGIONS = 8           # ad_deps_batch_device: the result is read through its regions (no packed copy)
 
 # InternalStatus ordinals (CommandsForKey.java:493-501)
 ST_TRANSITIVELY_KNOWN = 0
@@ -113,7 +114,8 @@ class AdDepsResult(C.Structure):
                 ("keys_off", P * NMAPS), ("keys", P * NMAPS),
                 ("txn_off", P * NMAPS), ("txns", P * NMAPS),
                 ("k2t_off", P * NMAPS), ("k2t", P * NMAPS),
-                ("stats", AdStats)]
+                ("stats", AdStats),
+                ("regions", P), ("region_off", P * NMAPS), ("regions_bytes", C.c_uint64), ("region_bytes", C.c_uint64)]
 
 
 class AdGraphSoa(C.Structure):

@@ -506,12 +506,14 @@ class DeviceCommandStore:
                 maps.append(DepsMap(ko, keys, None, to, txn, oo, k2t))
         return PartialDepsBatch(maps, stats=stats or {})
 
-    def deps_batch_device(self, qdev, stream=None, parts_only=False):
+    def deps_batch_device(self, qdev, stream=None, parts_only=False, regions=False):
         """Device-resident batch. `qdev` is an AdQuerySoa of device pointers. Returns
         (AdDepsResult with device pointers owned by the store, stats dict). `parts_only`: the result
-        is only exported as parts (AD_PARTS_ONLY: no packed arrays)."""
+        is only exported as parts (AD_PARTS_ONLY: no packed arrays); `regions`: the result is read
+        through its regions (AD_REGIONS: no packed arrays)."""
         out = A.AdDepsResult()
-        flags = A.AD_SNAPSHOT | A.AD_N_KEYS | (A.AD_PARTS_ONLY if parts_only else 0)
+        flags = (A.AD_SNAPSHOT | A.AD_N_KEYS | (A.AD_PARTS_ONLY if parts_only else 0) |
+                 (A.AD_REGIONS if regions else 0))
         self._check(lib().ad_deps_batch_device(self.h, C.byref(qdev), flags, stream, C.byref(out)))
         return out, stats_dict(out.stats)
 
@@ -580,9 +582,14 @@ class DeviceCommandStore:
         self._check(lib().ad_levels_device(self.h, C.byref(gdev), out_ptr, stream, C.byref(s)))
         return levels_stats(s)
 
-    def device_result_to_host(self, res, idx=None):
-        """Materialise the device result `res` of the last deps_batch_device (packed arrays) as a
-        PartialDepsBatch, for every request or only the requests `idx`."""
+    def device_result_to_host(self, res, idx=None, via_regions=None):
+        """Materialise the device result `res` of the last deps_batch_device as a PartialDepsBatch, for
+        every request or only the requests `idx`: from the packed arrays, or (`via_regions`, default
+        when the packed arrays are absent: AD_REGIONS) from each request's region."""
+        if via_regions is None:
+            via_regions = not res.keys[0]
+        if via_regions:
+            return self.materialise(self._regions_raw(res, idx))
         n = res.n_txns
         raw = []
         for m in range(A.NMAPS):
@@ -606,6 +613,45 @@ class DeviceCommandStore:
                 sub.append(tuple(parts))
             raw = sub
         return self.materialise(raw)
+
+    def _regions_raw(self, res, idx=None):
+        """The (offsets, keys, offsets, txnIds, offsets, keysToTxnIds) columns of every map, read from
+        the regions of a device result (accord_deps.h ad_deps_result.regions) for the requests idx."""
+        n = res.n_txns
+        arena = self._d2h(res.regions, int(res.regions_bytes), np.uint8)
+        sel = np.arange(n, dtype=np.int64) if idx is None else np.asarray(idx, np.int64)
+
+        words = {8: arena[:len(arena) // 8 * 8].view(np.int64), 4: arena[:len(arena) // 4 * 4].view(np.int32)}
+
+        def gather(base, cnt, width, dtype):
+            # cnt[i] elements of `width` bytes from byte base[i] on (a multiple of width), concatenated
+            tot = int(cnt.sum())
+            if tot == 0:
+                return np.zeros(0, dtype)
+            w = words[width]
+            pos = np.repeat(base // width, cnt) + (np.arange(tot) - np.repeat(np.cumsum(cnt) - cnt, cnt))
+            if pos.max() >= len(w):
+                raise AssertionError("a region reaches beyond regions_bytes")
+            return w[pos].view(dtype)
+
+        raw = []
+        for m in range(A.NMAPS):
+            ko = self._d2h(res.keys_off[m], n + 1, np.uint64).astype(np.int64)
+            to = self._d2h(res.txn_off[m], n + 1, np.uint64).astype(np.int64)
+            oo = self._d2h(res.k2t_off[m], n + 1, np.uint64).astype(np.int64)
+            ro = self._d2h(res.region_off[m], n, np.uint64).astype(np.int64)
+            nk, nt, no = ko[sel + 1] - ko[sel], to[sel + 1] - to[sel], oo[sel + 1] - oo[sel]
+            base = np.where(nk > 0, ro[sel], 0)
+            if np.any(base % 8):
+                raise AssertionError("a region is not 8-byte aligned")
+            cols = []
+            for cnt, off, width, dt in ((nk, base, 8, np.int64), (nt, base + 8 * nk, 4, np.uint32),
+                                        (no, base + 8 * nk + 4 * nt, 4, np.int32)):
+                o = np.zeros(len(sel) + 1, np.uint64)
+                o[1:] = np.cumsum(cnt)
+                cols += [o, gather(off, cnt, width, dt)]
+            raw.append(tuple(cols))
+        return raw
 
     def _d2h(self, p, n, dtype):
         a = np.zeros(max(n, 0), dtype)
@@ -680,11 +726,21 @@ def device_queries(q, dev):
     return s, keep
 
 
-def resolve(workload, device=0, elide=1, path=0):
+def resolve(workload, device=0, elide=1, path=0, via="host"):
+    """PartialDeps of a workload's batch: through ad_deps_batch (via "host"), or with the queries in HBM
+    through ad_deps_batch_device read back from the packed arrays ("device") or from the regions
+    (AD_REGIONS, "regions"; SNAPSHOT batches only)."""
     st = DeviceCommandStore(device, workload.range_start_inclusive, elide, workload.slices, path)
     try:
         st.load(workload)
-        return st.calculate_partial_deps(workload.queries, workload.flags)
+        if via == "host":
+            return st.calculate_partial_deps(workload.queries, workload.flags)
+        import torch
+        dev = torch.device("cuda", device)
+        qdev, keep = device_queries(workload.queries, dev)
+        res, stats = st.deps_batch_device(qdev, regions=(via == "regions"))
+        torch.cuda.synchronize(dev)
+        return st.device_result_to_host(res)
     finally:
         st.close()
 

@@ -1640,8 +1640,13 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         S.ms_device = total;
         S.ms_ingest = c->ms_ingest;
         out->n_txns = n;
+        out->regions = b.reg;
+        out->regions_bytes = h.reg_top;
+        out->region_bytes = 0;
         for (int m = 0; m < 3; ++m)
         {
+            out->region_off[m] = b.t_reg + (uint64_t)m * n;
+            out->region_bytes += 8 * tot[3 * m + 0] + 4 * tot[3 * m + 1] + 4 * tot[3 * m + 2];
             out->keys_off[m] = b.off + (uint64_t)(3 * m + 0) * (n + 1);
             out->txn_off[m] = b.off + (uint64_t)(3 * m + 1) * (n + 1);
             out->k2t_off[m] = b.off + (uint64_t)(3 * m + 2) * (n + 1);
@@ -2134,7 +2139,8 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
     int rc;
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    return run_pipeline(c, q, st, out, (flags & AD_PARTS_ONLY) != 0, (flags & AD_N_KEYS) != 0);
+    // AD_REGIONS and AD_PARTS_ONLY: no packed copy (the regions are the result)
+    return run_pipeline(c, q, st, out, (flags & (AD_PARTS_ONLY | AD_REGIONS)) != 0, (flags & AD_N_KEYS) != 0);
 }
 
 // device view of the snapshot for mapReduceFull: entries in load order with executeAt ranks,

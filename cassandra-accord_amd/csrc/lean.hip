@@ -30,7 +30,10 @@ constexpr int LEAN_WAVES = 4;
 #endif
 constexpr int LEAN_OCC = LEAN_OCC_N;        // waves per SIMD the register budget is sized for
 constexpr uint32_t LEAN_MAXP = 8;      // keys per request
-constexpr uint32_t LEAN_CHUNK = 1u << 16;
+#ifndef LEAN_CHUNK_LOG
+#define LEAN_CHUNK_LOG 16
+#endif
+constexpr uint32_t LEAN_CHUNK = 1u << LEAN_CHUNK_LOG;   // region bytes a wave takes from the arena at a time
 // measurement switches (scripts/build_variant.sh; results are wrong with any of them set):
 // 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes
 #ifndef LEAN_EXP
@@ -45,6 +48,12 @@ constexpr uint32_t LEAN_CHUNK = 1u << 16;
 #define LEAN_SLOTS 1
 #endif
 constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
+// LEAN_QLOAD: a request's KeyLine headers are loaded by all 32 of its lanes, one 16-byte quarter of one
+// key's first 64 bytes per lane (one vector load per item instead of four, each line touched once), and
+// handed to the key lanes through a per-wave LDS stage
+#ifndef LEAN_QLOAD
+#define LEAN_QLOAD 1
+#endif
 
 __global__ __launch_bounds__(256) void k_lean_slots(DevSnapshot s, const int64_t* keys, uint64_t np, uint32_t* slot)
 {
@@ -282,7 +291,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     // the key's line (KeyLine, common.hpp): the slice test (InMemoryCommandStore.java:280), then one
     // random line per key -- its first 64 bytes: key, cell entries, newest fields, meta, the class's
     // {count, start} and the cwr tail start. A slot holding another key is resolved when used.
-    struct Hdr { uint4 h0, h1; uint2 h2, h3; uint32_t slot; bool look; };
+    struct Hdr { uint4 h0, h1; uint2 h2, h3; uint4 q; uint32_t slot; bool look; };
+    constexpr bool QL = LEAN_QLOAD && !RNG && LEAN_SLOTS && RPW == 2;
+    __shared__ uint4 qst_all[QL ? LEAN_WAVES : 1][QL ? 64 : 1];
     auto in_slice_of = [&](int64_t key) {
         bool in = s.n_slices == 0;
         for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
@@ -311,11 +322,31 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     auto loadC = [&](const Req& q, int64_t key, bool look, uint32_t d, Hdr& H) {
         H.look = look;
         H.slot = !look ? 0u : SLOTS ? d : (uint32_t)kl_index(key_hash2(key), d, s.kl_lines);
+        if (QL)
+        {
+            // lane hl loads quarter hl & 3 of key hl >> 2's line (unmasked: unpacked under the key lane's look)
+            const uint32_t ks = __shfl(look ? H.slot : LS_NONE, (int)(sb | (hl >> 2)), 64);
+            H.q = reinterpret_cast<const uint4*>(s.kline + (ks != LS_NONE ? ks : 0u))[hl & 3u];
+            return;
+        }
         load_line(H.slot, q.cls, H);
     };
     // (found, cell bounds) of a loaded line: the perfect hash put the key on this line if the
     // store holds it; a line of another key (or an empty one) means no CommandsForKey
     auto resolve_line = [&](int64_t key, uint32_t cls, Hdr& H, bool& found, uint2& cb) {
+        if (QL)
+        {
+            uint4* st = qst_all[QL ? (threadIdx.x >> 6) : 0];
+            st[lane] = H.q;
+            wave_lds_sync();
+            const uint32_t b4 = sb + 4 * (hl & 7u);
+            H.h0 = st[b4];
+            H.h1 = st[b4 + 1];
+            const uint4 q2 = st[b4 + 2], q3 = st[b4 + 3];
+            H.h2 = cls == 0 ? make_uint2(q2.x, q2.y) : (cls == 1 ? make_uint2(q2.z, q2.w) : make_uint2(q3.x, q3.y));
+            H.h3 = make_uint2(q3.z, q3.w);
+            wave_lds_sync();
+        }
         auto key_of = [](const uint4& h0) { return (int64_t)(((uint64_t)h0.y << 32) | h0.x); };
         found = H.look && (H.h1.w & KL_USED) && key_of(H.h0) == key;
         cb = found ? make_uint2(H.h0.z, H.h0.w) : make_uint2(0, 0);

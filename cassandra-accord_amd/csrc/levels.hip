@@ -262,7 +262,8 @@ __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __
 // Sparsified predecessors of the occurrence at p (chain sorted by (key, rank)): walk back while
 // some kind T witnesses is not yet dominated. A txn P of kind c is dominated once a predecessor
 // (or a dominated txn) found later in the walk witnesses c: that one executes after P and waits
-// on it, so its level is larger. Pass 0: in-degree of T and out-degree of each P; pass 1: succ.
+// on it, so its level is larger. Pass 0: in-degree of T and (outdeg non-null) out-degree of each P;
+// pass 1: succ (successor lists); pass 2: pred (predecessor lists, offsets succ_off = scan of indeg).
 template <int PASS>
 __global__ void k_chain(const uint64_t* __restrict__ okey, const uint32_t* __restrict__ orank, uint64_t n_occ,
                         const uint8_t* __restrict__ kind_r, uint32_t* __restrict__ indeg, uint32_t* __restrict__ outdeg,
@@ -283,8 +284,9 @@ __global__ void k_chain(const uint64_t* __restrict__ okey, const uint32_t* __res
         if (A & bit & ~D)
         {
             ++npred;
-            if (PASS == 0) atomicAdd(&outdeg[P], 1u);
-            else succ[succ_off[P] + atomicAdd(&cursor[P], 1u)] = T;
+            if (PASS == 0) { if (outdeg) atomicAdd(&outdeg[P], 1u); }
+            else if (PASS == 1) succ[succ_off[P] + atomicAdd(&cursor[P], 1u)] = T;
+            else succ[succ_off[T] + atomicAdd(&cursor[T], 1u)] = P;
             D |= kind_witnesses(kp);
         }
         else if (D & bit)
@@ -314,8 +316,9 @@ __global__ void k_direct(LevelsIn g, const uint32_t* __restrict__ rank, uint32_t
         const uint32_t P = rank[src];
         if (P >= T) continue;
         ++npred;
-        if (PASS == 0) atomicAdd(&outdeg[P], 1u);
-        else succ[succ_off[P] + atomicAdd(&cursor[P], 1u)] = T;
+        if (PASS == 0) { if (outdeg) atomicAdd(&outdeg[P], 1u); }
+        else if (PASS == 1) succ[succ_off[P] + atomicAdd(&cursor[P], 1u)] = T;
+        else succ[succ_off[T] + atomicAdd(&cursor[T], 1u)] = P;
     }
     if (PASS == 0 && npred) atomicAdd(&indeg[T], npred);
 }
@@ -541,6 +544,87 @@ __global__ __launch_bounds__(64 * FLOW_WAVES) void k_level_flow(const uint2* __r
     if (lane == 0 && done) atomicAdd(done_count, (unsigned long long)done);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Rank-ordered dataflow leveling. level[] (by exec rank) starts LV_UNSET. A wave takes the next 64
+// ranks by ticket, so the lowest unfinished rank always belongs to a running wave and every wait is
+// on a lower rank: a running wave (or a finished one) -- no deadlock whatever the dispatch order.
+// Each lane walks its predecessor list in order, PULL_IN_FLIGHT level loads at a time; a lane
+// blocked on an unset level retries after a sleep, a lane whose list is done publishes its level at
+// once (lanes of the same wave may wait on it). The level word is its own flag (set once, from
+// LV_UNSET to its value): agent-scope relaxed atomics, i.e. sc1 stores and sc1 loads, the
+// single-granule hand-off of MI355X_MICROARCH.md (no payload to order). A wave still waiting after
+// `budget` wall-clock ticks gives up and flags the run (the host reports AD_E_STATE).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t LV_UNSET = 0xFFFFFFFFu;
+constexpr uint32_t PULL_IN_FLIGHT = 4;
+
+__device__ __forceinline__ uint32_t lv_poll(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* __restrict__ pred_off,
+                                                    const uint32_t* __restrict__ pred, uint32_t* level, uint32_t* ticket,
+                                                    uint32_t* fail, uint64_t budget, uint32_t naps)
+{
+    const uint32_t lane = lane_id();
+    const uint64_t t_end = wall_clock64() + budget;
+    while (true)
+    {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(ticket, 1u);
+        c = __shfl(c, 0, 64);
+        if ((uint64_t)c * 64 >= n) return;
+        const uint64_t T = (uint64_t)c * 64 + lane;
+        const bool on = T < n;
+        uint64_t j = on ? pred_off[T] : 0;
+        const uint64_t e = on ? pred_off[T + 1] : 0;
+        uint32_t mx = 0;
+        bool pending = on, waited = false;
+        while (true)
+        {
+            if (pending)
+            {
+                // a lane that was blocked polls only the predecessor it waits for; otherwise
+                // PULL_IN_FLIGHT levels are loaded together
+                bool blocked = false;
+                while (j < e && !blocked)
+                {
+                    uint32_t v[PULL_IN_FLIGHT];
+                    const uint64_t w = waited ? 1 : PULL_IN_FLIGHT;
+#pragma unroll
+                    for (uint32_t k = 0; k < PULL_IN_FLIGHT; ++k)
+                        v[k] = (k < w && j + k < e) ? lv_poll(level + pred[j + k]) : LV_UNSET;
+#pragma unroll
+                    for (uint32_t k = 0; k < PULL_IN_FLIGHT; ++k)
+                        if (!blocked && k < w && j < e)
+                        {
+                            if (v[k] == LV_UNSET) blocked = true;
+                            else
+                            {
+                                mx = max(mx, v[k] + 1u);
+                                ++j;
+                            }
+                        }
+                    waited = blocked;
+                }
+                if (!blocked)
+                {
+                    __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pending = false;
+                }
+            }
+            if (!ballot(pending)) break;
+            if (wall_clock64() > t_end)
+            {
+                if (lane == 0) atomicOr(fail, 1u);
+                return;
+            }
+            for (uint32_t z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(4);
+        }
+    }
+}
+
 __global__ void k_flow_init(const uint32_t* __restrict__ indeg, uint64_t n, unsigned long long* __restrict__ word,
                             uint2* __restrict__ seeds, uint32_t* seed_count)
 {
@@ -742,14 +826,16 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
                                 &oval));
     }
 
-    // ---- 3. sparsified predecessors -> successor CSR + in-degrees
+    // ---- 3. sparsified predecessors -> predecessor CSR (pull) or successor CSR + in-degrees (frontier, dataflow)
+    const char* df = getenv("AD_LEVELS_DATAFLOW");
+    const bool pull = df == nullptr && getenv("AD_LEVELS_FRONTIER") == nullptr;
     if (n_occ)
-        k_chain<0><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), indeg, outdeg,
-                                                           nullptr, nullptr, nullptr);
+        k_chain<0><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), indeg,
+                                                           pull ? nullptr : outdeg, nullptr, nullptr, nullptr);
     if (g.dep_off)
-        k_direct<0><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), indeg, outdeg, nullptr, nullptr,
-                                                        nullptr, ctl);
-    LV_CHK(run_scan_arrays(outdeg, succ_off, n, 1, bsum, st));
+        k_direct<0><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), indeg, pull ? nullptr : outdeg, nullptr,
+                                                        nullptr, nullptr, ctl);
+    LV_CHK(run_scan_arrays(pull ? indeg : outdeg, succ_off, n, 1, bsum, st));
     LV_CHK(hipMemcpyAsync(&w->h_u64[2], succ_off + n, 8, hipMemcpyDeviceToHost, st));
     LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
     LV_CHK(hipStreamSynchronize(st));
@@ -763,23 +849,66 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     const uint64_t n_edges = w->h_u64[2];
     out->n_edges = n_edges;
     LV_ALLOC(w->succ, 4 * std::max<uint64_t>(n_edges, 1));
-    uint32_t* succ = w->succ.as<uint32_t>();
-    if (n_occ)
-        k_chain<1><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), nullptr, nullptr,
-                                                           succ_off, cursor, succ);
-    if (g.dep_off)
-        k_direct<1><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), nullptr, nullptr, succ_off, cursor,
-                                                        succ, ctl);
+    uint32_t* succ = w->succ.as<uint32_t>();     // pull: predecessor lists (offsets succ_off)
+    if (pull)
+    {
+        if (n_occ)
+            k_chain<2><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), nullptr, nullptr,
+                                                               succ_off, cursor, succ);
+        if (g.dep_off)
+            k_direct<2><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), nullptr, nullptr, succ_off, cursor,
+                                                            succ, ctl);
+    }
+    else
+    {
+        if (n_occ)
+            k_chain<1><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), nullptr, nullptr,
+                                                               succ_off, cursor, succ);
+        if (g.dep_off)
+            k_direct<1><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), nullptr, nullptr, succ_off, cursor,
+                                                            succ, ctl);
+    }
     LV_CHK(hipEventRecord(w->ev[1], st));
 
-    // ---- 4. level the DAG: dataflow waves (default) or the level-synchronous frontier loop
-    // default: the level-synchronous frontier loop (one launch per level); AD_LEVELS_DATAFLOW=<steps>
-    // selects the dataflow waves (FLOW_STEPS steps per wave and launch by default)
-    const char* df = getenv("AD_LEVELS_DATAFLOW");
-    const bool frontier = df == nullptr;
+    // ---- 4. level the DAG: rank-ordered dataflow (default), the level-synchronous frontier loop
+    // (AD_LEVELS_FRONTIER) or the dataflow waves (AD_LEVELS_DATAFLOW=<steps>, FLOW_STEPS by default)
+    const bool frontier = !pull && df == nullptr;
     const uint32_t flow_steps = df && atoi(df) > 0 ? (uint32_t)atoi(df) : FLOW_STEPS;
     uint64_t nl = 0;
-    if (frontier)
+    if (pull)
+    {
+        int dev = 0, cus = 256, khz = 100000;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+        // measured on config 5 (scripts/c5_sweep.sh): one 256-thread block per CU beats 2 and 4 (the
+        // polls of more resident waiters load the memory system the hand-offs go through); naps between
+        // polls hardly matter at that residency
+        int per_cu = 1, naps = 1, threads = 256;
+        if (const char* e = getenv("AD_LEVELS_PULL_PER_CU")) per_cu = std::max(1, std::min(8, atoi(e)));
+        if (const char* e = getenv("AD_LEVELS_PULL_NAPS")) naps = std::max(0, std::min(64, atoi(e)));
+        if (const char* e = getenv("AD_LEVELS_PULL_THREADS")) threads = atoi(e) == 64 ? 64 : (atoi(e) == 128 ? 128 : 256);
+        // cnt[0] ticket, cnt[1] failure flag, cnt[2] max level (zeroed above)
+        LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
+        const uint64_t budget = (uint64_t)std::max(khz, 1000) * 1000ull;       // one second of wall clock
+        const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, (n + threads - 1) / threads);
+        k_level_pull<<<std::max(1u, grid), threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, budget, (uint32_t)naps);
+        LV_CHK(hipGetLastError());
+        out->n_launch = 1;
+        k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);
+        k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
+        LV_CHK(hipEventRecord(w->ev[2], st));
+        uint32_t tail[3];
+        LV_CHK(hipMemcpyAsync(tail, cnt, sizeof(tail), hipMemcpyDeviceToHost, st));
+        LV_CHK(hipStreamSynchronize(st));
+        if (tail[1])
+        {
+            *err = "ad_levels: a wave waited more than a second for a predecessor's level";
+            return AD_E_STATE;
+        }
+        nl = (uint64_t)tail[2] + 1;
+    }
+    else if (frontier)
     {
         uint32_t* fr[2] = {w->front0.as<uint32_t>(), w->front1.as<uint32_t>()};
         k_frontier_init<<<blocks_for(n, 256), 256, 0, st>>>(indeg, n, level, fr[0], cnt);

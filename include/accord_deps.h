@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define AD_ABI_VERSION 2
+#define AD_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define AD_OK                  0
@@ -105,6 +105,12 @@ extern "C" {
 #define AD_PARTS_ONLY 2u
 /* ad_deps_batch_device only: ad_query_soa.n_keys holds key_off[n_txns] */
 #define AD_N_KEYS     4u
+/* ad_deps_batch_device only: the result is read through its regions (ad_deps_result.regions,
+ * region_off): each request's three RelationMultiMaps stay where the kernels wrote them, once, and
+ * the packed arrays are not produced (keys/txns/k2t NULL; the *_off arrays still give every
+ * request's sizes and its position in a packed layout). This is the device path's primary output: a
+ * Java host builds each request's KeyDeps / RangeDeps from its own region. */
+#define AD_REGIONS    8u
 
 typedef struct ad_config {
     int32_t device;                 /* HIP device ordinal                                   */
@@ -222,6 +228,18 @@ typedef struct ad_deps_result {
     uint64_t* k2t_off[AD_NMAPS];
     int32_t*  k2t[AD_NMAPS];
     ad_stats  stats;
+    /* Regions (ad_deps_batch_device; every result, AD_REGIONS or not): request i's map m, when it has
+     * nK = keys_off[m][i+1] - keys_off[m][i] > 0 keys, is the 8-byte aligned block at byte offset
+     * region_off[m][i] of `regions`:
+     *     int64 keys[nK] | uint32 txnIds[nT] | int32 keysToTxnIds[nKT]
+     * with nT, nKT the differences of txn_off / k2t_off -- the three arrays of that map as above.
+     * region_off of an empty map is unspecified. regions_bytes: bytes of `regions` in use (the regions
+     * plus the unused tails of the kernels' allocation chunks); region_bytes: the payload of the regions
+     * (their three arrays, alignment padding excluded). */
+    const uint8_t*  regions;
+    const uint64_t* region_off[AD_NMAPS];
+    uint64_t        regions_bytes;
+    uint64_t        region_bytes;
 } ad_deps_result;
 
 typedef struct ad_ctx ad_ctx;

@@ -23,7 +23,7 @@ import torch  # noqa: E402
 from accord_deps import native, synth  # noqa: E402
 
 
-def run(lib, w, steps, warmup, sample, dev):
+def run(lib, w, steps, warmup, sample, dev, regions=False):
     native._lib = None
     native.LIB_PATH = lib
     native.lib()
@@ -33,17 +33,18 @@ def run(lib, w, steps, warmup, sample, dev):
         qdev, keep = native.device_queries(w.queries, dev)
         sp = torch.cuda.current_stream(dev).cuda_stream
         for _ in range(warmup):
-            res, stats = st.deps_batch_device(qdev, sp)
+            res, stats = st.deps_batch_device(qdev, sp, regions=regions)
         torch.cuda.synchronize(dev)
         acc = np.zeros(7)
         t0 = time.perf_counter()
         for _ in range(steps):
-            res, stats = st.deps_batch_device(qdev, sp)
+            res, stats = st.deps_batch_device(qdev, sp, regions=regions)
             acc += np.array(stats["ms_stage"][:7])
         torch.cuda.synchronize(dev)
         ms = 1000.0 * (time.perf_counter() - t0) / steps
         got = st.device_result_to_host(res, sample)
-        return dict(ms_per_step=round(ms, 4), stages=[round(x / steps, 4) for x in acc],
+        return dict(ms_per_step=round(ms, 4), regions=regions, regions_bytes=[int(res.regions_bytes), int(res.region_bytes)],
+                    stages=[round(x / steps, 4) for x in acc],
                     pairs=[int(x) for x in stats["n_pairs"]], n_pass2=int(stats.get("n_lean_pass2", 0)),
                     n_general=int(stats.get("n_deferred_lean", 0))), got
     finally:
@@ -55,6 +56,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--regions", action="store_true", help="every library also timed with AD_REGIONS output")
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -69,8 +71,11 @@ def main():
     sample = np.unique(np.concatenate([np.arange(2000), rng.choice(len(w.queries), 4000, replace=False)]))
     base_lib = os.path.join(ROOT, "cassandra-accord_amd", "accord_deps", "libaccord_deps.so")
     ref = None
-    for lib in [base_lib] + a.libs:
-        r, got = run(lib, w, a.steps, a.warmup, sample, dev)
+    runs = [(lib, False) for lib in [base_lib] + a.libs]
+    if a.regions:
+        runs += [(lib, True) for lib in [base_lib] + a.libs]
+    for lib, regions in runs:
+        r, got = run(lib, w, a.steps, a.warmup, sample, dev, regions)
         if ref is None:
             ref = got
             r["same_as_base"] = True

@@ -93,6 +93,16 @@ def _run_full(w, oracle, expect_lean=None):
             mm = got.first_mismatch(exp)
             raise AssertionError("%s: %s; first mismatch at sample %s (request %d): %r" %
                                  (w.name, why, mm[0] if mm else None, idx[mm[0]] if mm else -1, mm))
+        # the packed arrays read back in full, then the same batch through its regions (AD_REGIONS, the
+        # bench's default output): every request's three maps identical to the packed ones
+        full = st.device_result_to_host(res)
+        rres, rstats = st.deps_batch_device(qdev, regions=True)
+        torch.cuda.synchronize(dev)
+        assert not rres.keys[0] and rres.regions_bytes >= rres.region_bytes > 0
+        assert rstats["n_pairs"] == stats["n_pairs"]
+        viar = st.device_result_to_host(rres)
+        ok, why = viar.equals(full, detail=True)
+        assert ok, "%s: regions differ from the packed arrays: %s" % (w.name, why)
         return stats, got
     finally:
         st.close()

@@ -21,14 +21,36 @@ def _check(g, oracle):
     return got, st
 
 
-@pytest.mark.parametrize("dataflow", [None, "8", "1"])
+def _scheme(monkeypatch, scheme):
+    # None: the rank-ordered dataflow (k_level_pull, default); "frontier": the level-synchronous
+    # frontier loop; a number: the dataflow waves with that many steps per launch
+    if scheme == "frontier":
+        monkeypatch.setenv("AD_LEVELS_FRONTIER", "1")
+    elif scheme:
+        monkeypatch.setenv("AD_LEVELS_DATAFLOW", scheme)
+
+
+@pytest.mark.parametrize("scheme", [None, "frontier", "8", "1"])
 @pytest.mark.parametrize("seed", range(12))
-def test_random_graph_all_kinds(oracle, seed, dataflow, monkeypatch):
-    # both leveling schemes: the level-synchronous frontier loop (default) and the dataflow waves
-    if dataflow:
-        monkeypatch.setenv("AD_LEVELS_DATAFLOW", dataflow)
+def test_random_graph_all_kinds(oracle, seed, scheme, monkeypatch):
+    _scheme(monkeypatch, scheme)
     g = synth.random_graph(seed, n_txns=500 + 300 * seed, n_keys=10 + 7 * seed, long_runs=(seed % 4 == 3))
     _check(g, oracle)
+
+
+@pytest.mark.parametrize("per_cu", ["1", "8"])
+def test_pull_occupancy(oracle, per_cu, monkeypatch):
+    # fewer and more resident waves than the default (every wait still on a lower rank)
+    monkeypatch.setenv("AD_LEVELS_PULL_PER_CU", per_cu)
+    g = synth.random_graph(17, n_txns=40_000, n_keys=300, long_runs=True)
+    _check(g, oracle)
+
+
+def test_config5_full_frontier(oracle, monkeypatch):
+    _scheme(monkeypatch, "frontier")
+    g, _ = synth.config5()
+    got, st = _check(g, oracle)
+    assert st["n_levels"] == int(got.max()) + 1
 
 
 def test_config5_full_dataflow(oracle, monkeypatch):
@@ -54,9 +76,8 @@ def test_many_sources_spill_path(oracle, monkeypatch):
     dep_off[1:] = np.cumsum(hub)
     deps = np.zeros(int(hub.sum()), np.uint32)
     g = Graph(ex, np.zeros(n, np.uint8), key_off, keys, dep_off, deps)
-    for df in (None, "8"):
-        if df:
-            monkeypatch.setenv("AD_LEVELS_DATAFLOW", df)
+    for df in (None, "frontier", "8"):
+        _scheme(monkeypatch, df)
         got, st = _check(g, oracle)
         assert st["n_levels"] == 2
 

@@ -32,6 +32,28 @@ def test_random_small(oracle, seed):
     _compare(w, oracle)
 
 
+@pytest.mark.parametrize("via", ["device", "regions"])
+@pytest.mark.parametrize("seed", range(12))
+def test_random_small_device_outputs(oracle, seed, via):
+    # the device entry point read back from the packed arrays and from the regions (AD_REGIONS): lean,
+    # general, split and heavy-request paths all write the regions the result points at
+    w = synth.random_small(200 + seed, with_slices=(seed % 4 == 3), n_range_cmds=(0 if seed % 3 == 0 else 30),
+                           n_redundant=(0 if seed % 2 == 0 else 3), accept_frac=0.1 * (seed % 3), max_keys=2 + seed % 9)
+    exp = oracle.resolve(w)
+    got = native.resolve(w, via=via)
+    ok, why = got.equals(exp, detail=True)
+    assert ok, "%s via %s: %s; first mismatch %r" % (w.name, via, why, got.first_mismatch(exp))
+
+
+@pytest.mark.parametrize("big", ["64", "100000"])
+def test_big_requests_regions(oracle, big, monkeypatch):
+    monkeypatch.setenv("AD_K2_BIG", big)       # heavy requests on the workgroup build (64) or one wave
+    w = synth.random_small(77, n_keys=40, n_hist_txns=6000, n_txns=300, max_keys=8, n_range_cmds=50)
+    got = native.resolve(w, via="regions")
+    ok, why = got.equals(oracle.resolve(w), detail=True)
+    assert ok, why
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_small_no_elision(oracle, seed):
     _compare(synth.random_small(100 + seed), oracle, elide=0)

@@ -26,7 +26,7 @@ def test_header_and_library_exports():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(native.EXPORTS)
-    assert L.ad_abi_version() == 2
+    assert L.ad_abi_version() == 3
 
 
 def test_fails_loudly_without_gpu():
@@ -43,7 +43,9 @@ def test_struct_layouts_match_header():
     # offsets the C side relies on (x86-64 SysV)
     assert C.sizeof(A.AdConfig) == 40
     assert A.AdQuerySoa.keys.offset == 8 * 9
-    assert C.sizeof(A.AdDepsResult) == 8 + 6 * 3 * 8 + C.sizeof(A.AdStats)
+    # n_txns, 6 x 3 pointers, stats, then regions, 3 region_off pointers, regions_bytes, region_bytes
+    assert C.sizeof(A.AdDepsResult) == 8 + 6 * 3 * 8 + C.sizeof(A.AdStats) + 8 + 3 * 8 + 8 + 8
+    assert A.AdDepsResult.regions.offset == 8 + 6 * 3 * 8 + C.sizeof(A.AdStats)
 
 
 def _check_cfk_invariants(cfk):
