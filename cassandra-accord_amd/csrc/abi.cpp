@@ -27,6 +27,7 @@
 #include "kernels.hpp"
 #include "levels.hpp"
 #include "cfk_update.hpp"
+#include "ingest.hpp"
 #include "check.hpp"
 
 using namespace adx;
@@ -311,6 +312,14 @@ struct ad_ctx {
     DevBuf u_do, u_dm, u_dl, u_dn;                   // staged deps of a host update batch
     CfkUpdWork* cu = nullptr;
     bool host_stale = false;
+    // device ingest (ingest.hip): ad_cfk_load puts the snapshot's columns in HBM (raw_dev) and the
+    // build derives everything there; the host's byId ids and dictionary copy follow on demand
+    DevBuf d_in_seg, d_in_pruned, d_in_tm, d_in_tl, d_in_tn, d_in_em, d_in_el, d_in_en, d_in_xm, d_in_xl, d_in_xn, d_ing_rank;
+    bool raw_dev = false;                            // d_in_* hold the loaded snapshot (no device update since)
+    uint64_t raw_ne = 0;
+    bool host_dict_stale = false;                    // dict_msb/lsb/node not yet read back from the device
+    bool host_ingested = false;                      // host copies pending from a device ingest (entries did not move)
+    IngestWork* ing = nullptr;
     std::vector<uint64_t> x_msb, x_lsb;        // ad_cfk_entries views
     std::vector<int32_t> x_node;
     std::vector<uint64_t> y_msb, y_lsb;        // ad_cfk_byid views
@@ -339,6 +348,11 @@ struct ad_ctx {
         hipError_t _e = (expr);                                                                   \
         if (_e != hipSuccess) return (ctx)->fail(AD_E_DEVICE, "%s: %s", #expr, hipGetErrorString(_e)); \
     } while (0)
+
+extern "C" {
+// the device ingest reuses the update path's derived-array allocation (defined with the f1 entry points)
+static int cfk_need_bufs(void* vc, uint64_t n_cand, uint64_t n_cwr, uint64_t n_w, CfkDerivedBufs* b);
+}
 
 namespace {
 
@@ -510,232 +524,20 @@ static int kl_add_keys(ad_ctx* c, const std::vector<int64_t>& nkeys, uint64_t nk
     return 0;
 }
 
-static int build_snapshot(ad_ctx* c)
-{
-    if (int rc0 = sync_host(c)) return rc0;
-    c->dmiss_on = false;          // the host copy holds the missing() lists now; uploaded again on demand
-    const double t0 = now_ms();
-    auto& K = c->cfk;
-    const uint64_t nk = K.keys.size(), ne = K.status.size();
-    const uint64_t ncmd = c->cmds.txn.size(), nrb = c->rb.wm.size();
-
-    // ---- 1. id dictionary over every id the kernels compare
-    std::vector<uint8_t> exec_differs(ne);
-    std::vector<DictRec> recs;
-    recs.reserve(ne * 2 + ncmd + nrb);
-    for (uint64_t e = 0; e < ne; ++e)
-    {
-        const NormTid n = norm(K.txn[e]);
-        recs.push_back({n.hi, n.lo, n.node, 0, e});
-        const Tid& x = K.exec[e];
-        exec_differs[e] = !(x.msb == K.txn[e].msb && x.lsb == K.txn[e].lsb && x.node == K.txn[e].node);
-        if (exec_differs[e])
-        {
-            const NormTid m = norm(x);
-            recs.push_back({m.hi, m.lo, m.node, 0, ne + e});
-        }
-    }
-    for (uint64_t i = 0; i < ncmd; ++i)
-    {
-        const NormTid n = norm(c->cmds.txn[i]);
-        recs.push_back({n.hi, n.lo, n.node, 0, 2 * ne + i});
-    }
-    for (uint64_t i = 0; i < nrb; ++i)
-    {
-        if (!tid_gt_none(c->rb.wm[i])) continue;
-        const NormTid n = norm(c->rb.wm[i]);
-        recs.push_back({n.hi, n.lo, n.node, 0, 2 * ne + ncmd + i});
-    }
-    parallel_sort(recs, rec_less);
-    auto src_tid = [&](uint64_t s) -> const Tid& {
-        if (s < ne) return K.txn[s];
-        if (s < 2 * ne) return K.exec[s - ne];
-        if (s < 2 * ne + ncmd) return c->cmds.txn[s - 2 * ne];
-        return c->rb.wm[s - 2 * ne - ncmd];
-    };
-    std::vector<uint32_t> txn_rank(ne), exec_rank(ne), cmd_rank(ncmd), wm_rank(nrb, 0);
-    c->dict_msb.clear();
-    c->dict_lsb.clear();
-    c->dict_node.clear();
-    std::vector<uint64_t> dhi, dlo;
-    std::vector<int32_t> dnode;
-    auto set_rank = [&](uint64_t s, uint32_t rank) {
-        if (s < ne) txn_rank[s] = rank;
-        else if (s < 2 * ne) exec_rank[s - ne] = rank;
-        else if (s < 2 * ne + ncmd) cmd_rank[s - 2 * ne] = rank;
-        else wm_rank[s - 2 * ne - ncmd] = rank;
-    };
-    bool use_global = c->gd_set;
-    if (use_global)
-    {
-        // the installed node-wide dictionary (ad_set_global_dict) is this store's dictionary: every
-        // rank is a global rank, so exported parts carry the kernels' own ids (no translation)
-        const uint64_t ng = c->gd_msb.size();
-        dhi.resize(ng);
-        dlo.resize(ng);
-        dnode.resize(ng);
-        parallel_for(ng, [&](size_t a, size_t b) {
-            for (size_t i = a; i < b; ++i)
-            {
-                const NormTid n = norm(Tid{c->gd_msb[i], c->gd_lsb[i], c->gd_node[i]});
-                dhi[i] = n.hi;
-                dlo[i] = n.lo;
-                dnode[i] = n.node;
-            }
-        });
-        uint64_t gi = 0;
-        for (size_t i = 0; i < recs.size() && use_global; ++i)
-        {
-            const DictRec& r = recs[i];
-            auto g_less = [&](uint64_t j) {
-                if (dhi[j] != r.hi) return dhi[j] < r.hi;
-                if (dlo[j] != r.lo) return dlo[j] < r.lo;
-                return dnode[j] < r.node;
-            };
-            while (gi < ng && g_less(gi)) ++gi;
-            if (gi == ng || dhi[gi] != r.hi || dlo[gi] != r.lo || dnode[gi] != r.node)
-            {
-                use_global = false;
-                break;
-            }
-            const Tid& t = src_tid(r.src);
-            if (t.lsb != c->gd_lsb[gi])
-                return c->fail(AD_E_INCONSISTENT_ID, "ids equal under Timestamp.equals differ in flag bits (lsb %llx vs %llx)",
-                               (unsigned long long)t.lsb, (unsigned long long)c->gd_lsb[gi]);
-            set_rank(r.src, (uint32_t)(2 * gi + 1));
-        }
-        if (use_global)
-        {
-            if (ng > MAX_DICT) return c->fail(AD_E_CAPACITY, "more than %llu distinct ids", (unsigned long long)MAX_DICT);
-            c->dict_msb = c->gd_msb;
-            c->dict_lsb = c->gd_lsb;
-            c->dict_node = c->gd_node;
-        }
-        else
-        {
-            if (c->gd_strict) return c->fail(AD_E_INVAL, "ad_set_global_dict: an id of this store's snapshot is missing");
-            // the snapshot outgrew the installed dictionary: uninstalled, the store's own dictionary instead
-            drop_global_dict(c);
-            dhi.clear();
-            dlo.clear();
-            dnode.clear();
-        }
-    }
-    for (size_t i = 0; i < recs.size() && !use_global; ++i)
-    {
-        const DictRec& r = recs[i];
-        if (i == 0 || !rec_eq(recs[i - 1], r))
-        {
-            if (c->dict_msb.size() >= MAX_DICT) return c->fail(AD_E_CAPACITY, "more than %llu distinct ids", (unsigned long long)MAX_DICT);
-            const Tid& t = src_tid(r.src);
-            c->dict_msb.push_back(t.msb);
-            c->dict_lsb.push_back(t.lsb);
-            c->dict_node.push_back(t.node);
-            dhi.push_back(r.hi);
-            dlo.push_back(r.lo);
-            dnode.push_back(r.node);
-        }
-        else
-        {
-            const Tid& t = src_tid(r.src);
-            if (t.lsb != c->dict_lsb.back())
-                return c->fail(AD_E_INCONSISTENT_ID, "ids equal under Timestamp.equals differ in flag bits (lsb %llx vs %llx)",
-                               (unsigned long long)t.lsb, (unsigned long long)c->dict_lsb.back());
-        }
-        set_rank(r.src, (uint32_t)(2 * (c->dict_msb.size() - 1) + 1));
-    }
-    std::vector<DictRec>().swap(recs);
-    for (uint64_t e = 0; e < ne; ++e)
-        if (!exec_differs[e]) exec_rank[e] = txn_rank[e];
-    c->h_cmd_rank = cmd_rank;
-
-    // ---- 2. per key validation, tau/txw, committed Writes by executeAt
-    std::vector<uint2> ent(ne);
-    std::vector<uint32_t> seg32(nk + 1), woff(nk + 1), pruned(nk, 0);
-    std::vector<int32_t> maw(nk, -1);
-    for (uint64_t k = 0; k <= nk; ++k) seg32[k] = (uint32_t)K.seg[k];
-    std::atomic<int> bad{0};
-    std::atomic<uint64_t> bad_key{0};
-    std::vector<uint32_t> wcount(nk, 0);
-    parallel_for(nk, [&](size_t ka, size_t kb) {
-        std::vector<uint32_t> ce;
-        for (size_t k = ka; k < kb; ++k)
-        {
-            const uint64_t s0 = K.seg[k], s1 = K.seg[k + 1];
-            ce.clear();
-            uint32_t nw = 0;
-            for (uint64_t e = s0; e < s1; ++e)
-            {
-                const uint8_t st = K.status[e];
-                const uint32_t kind = (uint32_t)((K.txn[e].lsb >> 1) & 7);
-                const uint32_t dom = (uint32_t)(K.txn[e].lsb & 1);
-                if (st > 7) { bad = AD_E_INVAL; bad_key = k; continue; }
-                if (e > s0 && txn_rank[e] <= txn_rank[e - 1]) { bad = AD_E_ORDER; bad_key = k; }
-                uint32_t tau;
-                if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED) tau = 0;
-                else if (st >= AD_ST_COMMITTED && ((KINDS_RS_OR_WS >> kind) & 1)) tau = exec_rank[e];
-                else tau = TAU_NEVER_ELIDED;
-                if (tau != 0 && dom != 0) { bad = AD_E_INVAL; bad_key = k; }   // live range-domain id in a CFK
-                ent[e] = make_uint2(tau, txn_rank[e] | (kind << RANK_BITS));
-                if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED)
-                {
-                    ce.push_back(exec_rank[e]);
-                    if (kind == AD_KIND_WRITE) ++nw;
-                }
-            }
-            std::sort(ce.begin(), ce.end());
-            for (size_t i = 1; i < ce.size(); ++i)
-                if (ce[i] == ce[i - 1]) { bad = AD_E_DUP_EXEC; bad_key = k; }
-            wcount[k] = nw;
-        }
-    });
-    if (bad.load())
-    {
-        const int code = bad.load();
-        return c->fail(code, "CommandsForKey of key %lld violates %s", (long long)K.keys[bad_key.load()],
-                       code == AD_E_ORDER ? "byId strict order (CommandsForKey.java:1438)"
-                       : code == AD_E_DUP_EXEC ? "unique committed executeAt (CommandsForKey.java:1439)"
-                                               : "status range / key-domain ids");
-    }
-    for (uint64_t k = 0; k + 1 <= nk; ++k)
-        if (k > 0 && K.keys[k - 1] >= K.keys[k]) return c->fail(AD_E_INVAL, "keys not strictly ascending");
-    woff[0] = 0;
-    for (uint64_t k = 0; k < nk; ++k) woff[k + 1] = woff[k] + wcount[k];
-    std::vector<uint2> w(woff[nk]);
-    parallel_for(nk, [&](size_t ka, size_t kb) {
-        std::vector<std::pair<uint32_t, std::pair<uint32_t, uint8_t>>> tmp;
-        for (size_t k = ka; k < kb; ++k)
-        {
-            tmp.clear();
-            for (uint64_t e = K.seg[k]; e < K.seg[k + 1]; ++e)
-            {
-                const uint8_t st = K.status[e];
-                const uint32_t kind = (uint32_t)((K.txn[e].lsb >> 1) & 7);
-                if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED && kind == AD_KIND_WRITE)
-                    tmp.push_back({exec_rank[e], {txn_rank[e], st}});
-            }
-            std::sort(tmp.begin(), tmp.end());
-            int32_t m = -1;
-            for (size_t i = 0; i < tmp.size(); ++i)
-            {
-                w[woff[k] + i] = make_uint2(tmp[i].first, tmp[i].second.first);
-                if (tmp[i].second.second == AD_ST_APPLIED) m = (int32_t)(woff[k] + i);   // maxAppliedWriteByExecuteAt
-            }
-            maw[k] = m;
-            if (!K.pruned.empty() && K.pruned[k] >= 0)
-            {
-                const uint64_t idx = K.seg[k] + (uint64_t)K.pruned[k];
-                if (idx >= K.seg[k + 1]) { bad = AD_E_INVAL; bad_key = k; continue; }
-                pruned[k] = txn_rank[idx];
-            }
-        }
-    });
-    if (bad.load()) return c->fail(AD_E_INVAL, "prunedBefore of key %lld is not in byId", (long long)K.keys[bad_key.load()]);
-
-    // ---- 3. range commands: (range, command) entries sorted by (start, end, txnId); range table
-    struct REnt { int64_t s, e; uint32_t txw; uint32_t rid; uint8_t live; };
+// Range commands and RedundantBefore of a snapshot build (both routes): (range, command) entries
+// sorted by (start, end, txnId), the range table, the stabbing index, uploads. cmd_rank / wm_rank:
+// the dictionary ranks of the commands' txnIds and the watermarks (0: none).
+struct RangePart {
     std::vector<int64_t> cell_E;
     bool cell_ok = false;
+    uint64_t n_rent = 0;
+};
+static int build_ranges(ad_ctx* c, const std::vector<uint32_t>& cmd_rank, const std::vector<uint32_t>& wm_rank, RangePart* out)
+{
+    const uint64_t ncmd = c->cmds.txn.size(), nrb = c->rb.wm.size();
+    struct REnt { int64_t s, e; uint32_t txw; uint32_t rid; uint8_t live; };
+    std::vector<int64_t>& cell_E = out->cell_E;
+    bool& cell_ok = out->cell_ok;
     std::vector<REnt> rent;
     for (uint64_t i = 0; i < ncmd; ++i)
     {
@@ -850,6 +652,516 @@ static int build_snapshot(ad_ctx* c)
         }
     }
 
+    out->n_rent = rent.size();
+    return 0;
+}
+
+// The DevSnapshot views over the ctx's device buffers of a built snapshot (both build routes)
+static int set_views(ad_ctx* c, uint64_t n_dict, uint64_t n_samp, const NormTid& last, uint64_t nk, uint64_t ne, uint64_t hcap,
+                     const RangePart& rp, uint64_t nrb)
+{
+    DevSnapshot& s = c->ds;
+    s = DevSnapshot{};
+    s.dict_hi = c->d_dict_hi.as<uint64_t>();
+    s.dict_lo = c->d_dict_lo.as<uint64_t>();
+    s.dict_node = c->d_dict_node.as<int32_t>();
+    s.n_dict = n_dict;
+    s.ds_hi = c->d_ds_hi.as<uint64_t>();
+    s.ds_lo = c->d_ds_lo.as<uint64_t>();
+    s.ds_node = c->d_ds_node.as<int32_t>();
+    s.n_samp = n_samp;
+    if (n_dict)
+    {
+        s.dict_last_hi = last.hi;
+        s.dict_last_lo = last.lo;
+        s.dict_last_node = last.node;
+    }
+    s.n_keys = nk;
+    s.keys = c->d_keys.as<int64_t>();
+    s.krec = c->d_krec.as<KeyRec>();
+    s.khash = c->d_khash.as<KeySlot>();
+    s.kent = c->d_kent.as<KeyEntry>();
+    s.cand = c->d_cand.as<uint32_t>();
+    s.cwr = c->d_cwr.as<uint32_t>();
+    s.khash_mask = hcap - 1;
+    s.n_ent = ne;
+    s.ent = c->d_ent.as<uint2>();
+    s.w = c->d_w.as<uint2>();
+    s.lvl_n[0] = ne;
+    int L = 1;
+    while (s.lvl_n[L - 1] > 64 && L < MAX_LEVELS)
+    {
+        s.lvl_n[L] = (s.lvl_n[L - 1] + 63) / 64;
+        ++L;
+    }
+    s.n_levels = L;
+    for (int l = 1; l < L; ++l)
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * ((s.lvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "tree level");
+            s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
+        }
+    const bool cell_ok = rp.cell_ok;
+    s.n_rent = rp.n_rent;
+    s.n_cell_E = cell_ok ? rp.cell_E.size() : 0;
+    s.cell_E = cell_ok ? c->d_cell_E.as<int64_t>() : nullptr;
+    s.cell_off = cell_ok ? c->d_cell_off.as<uint32_t>() : nullptr;
+    s.cell_ent = cell_ok ? c->d_cell_ent.as<uint64_t>() : nullptr;
+    if (!cell_ok) c->n_cell_ent = 0;
+    s.r_start = c->d_rstart.as<int64_t>();
+    s.r_end = c->d_rend.as<int64_t>();
+    s.r_txw = c->d_rtxw.as<uint32_t>();
+    s.r_rid = c->d_rrid.as<uint32_t>();
+    s.rlvl_n[0] = s.n_rent;
+    L = 1;
+    while (s.rlvl_n[L - 1] > 64 && L < MAX_LEVELS)
+    {
+        s.rlvl_n[L] = (s.rlvl_n[L - 1] + 63) / 64;
+        ++L;
+    }
+    s.n_rlevels = L;
+    for (int l = 1; l < L; ++l)
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            if (!c->d_rlvl[cl][l].ensure(sizeof(int64_t) * ((s.rlvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "range tree level");
+            s.rlvl[cl][l] = c->d_rlvl[cl][l].as<int64_t>();
+        }
+    s.n_rb = nrb;
+    s.rb_start = c->d_rb_s.as<int64_t>();
+    s.rb_end = c->d_rb_e.as<int64_t>();
+    s.rb_e0 = c->d_rb_e0.as<int64_t>();
+    s.rb_e1 = c->d_rb_e1.as<int64_t>();
+    s.rb_wm = c->d_rb_wm.as<uint32_t>();
+    s.rb_rid = c->d_rb_rid.as<uint32_t>();
+    s.n_slices = c->slice_s.size();
+    s.slice_start = c->d_slices_s.as<int64_t>();
+    s.slice_end = c->d_slices_e.as<int64_t>();
+    s.start_inclusive = c->cfg.range_start_inclusive;
+    s.elide = c->cfg.elide;
+    return 0;
+}
+
+// ---- the snapshot built on the device (ingest.hip + the update path's derivation) ----------------
+static int host_inputs(ad_ctx* c);
+static int build_snapshot_device(ad_ctx* c)
+{
+    const double t0 = now_ms();
+    const bool trace = getenv("AD_INGEST_TRACE") != nullptr;
+    double tp = t0;
+    auto phase = [&](const char* what) {
+        if (!trace) return;
+        const double t = now_ms();
+        fprintf(stderr, "ingest(device) %-28s %8.1f ms\n", what, t - tp);
+        tp = t;
+    };
+    auto& K = c->cfk;
+    const uint64_t nk = K.keys.size(), ne = c->raw_ne, ncmd = c->cmds.txn.size(), nrb = c->rb.wm.size();
+    hipStream_t st = c->stream;
+    c->dmiss_on = false;
+    // extra dictionary ids: range command txnIds, then the watermarks above NONE
+    std::vector<uint64_t> xm, xl, wm_at;
+    std::vector<int32_t> xn;
+    for (uint64_t i = 0; i < ncmd; ++i) { xm.push_back(c->cmds.txn[i].msb); xl.push_back(c->cmds.txn[i].lsb); xn.push_back(c->cmds.txn[i].node); }
+    for (uint64_t i = 0; i < nrb; ++i)
+        if (tid_gt_none(c->rb.wm[i]))
+        {
+            xm.push_back(c->rb.wm[i].msb);
+            xl.push_back(c->rb.wm[i].lsb);
+            xn.push_back(c->rb.wm[i].node);
+            wm_at.push_back(i);
+        }
+    const uint64_t nx = xm.size();
+    int rc;
+    if ((rc = upload(c, c->d_in_xm, xm)) || (rc = upload(c, c->d_in_xl, xl)) || (rc = upload(c, c->d_in_xn, xn))) return rc;
+    IngestIn in{nk, ne, nx, c->d_keys.as<int64_t>(), c->d_in_seg.as<uint64_t>(),
+                K.pruned.empty() ? nullptr : c->d_in_pruned.as<int64_t>(),
+                c->d_in_tm.as<uint64_t>(), c->d_in_tl.as<uint64_t>(), c->d_in_tn.as<int32_t>(),
+                c->d_in_em.as<uint64_t>(), c->d_in_el.as<uint64_t>(), c->d_in_en.as<int32_t>(), c->d_status.as<uint8_t>(),
+                c->d_in_xm.as<uint64_t>(), c->d_in_xl.as<uint64_t>(), c->d_in_xn.as<int32_t>()};
+    const uint64_t nrec = std::max<uint64_t>(ingest_records(in), 1);
+    const uint64_t padded = std::max<uint64_t>(64, (ne + 63) / 64 * 64);     // whole 64-entry frames (tau 0)
+    if (!c->d_dict_hi.ensure(8 * nrec) || !c->d_dict_lo.ensure(8 * nrec) || !c->d_dict_node.ensure(4 * nrec) ||
+        !c->d_dict_lsb_raw.ensure(8 * nrec) || !c->d_ing_rank.ensure(4 * nrec) || !c->d_ent.ensure(8 * padded) ||
+        !c->d_xrank.ensure(4 * std::max<uint64_t>(ne, 1)) || !c->d_ekey.ensure(4 * std::max<uint64_t>(ne, 1)) ||
+        !c->d_krec.ensure(sizeof(KeyRec) * std::max<uint64_t>(nk, 1)) || !c->d_kent.ensure(sizeof(KeyEntry) * std::max<uint64_t>(nk, 1)))
+        return c->fail(AD_E_NOMEM, "snapshot buffers");
+    HIPCHK(c, hipMemsetAsync(c->d_ent.as<uint2>() + ne, 0, 8 * (padded - ne), st));
+    IngestOut o{c->d_dict_hi.as<uint64_t>(), c->d_dict_lo.as<uint64_t>(), c->d_dict_node.as<int32_t>(),
+                c->d_dict_lsb_raw.as<uint64_t>(), c->d_ing_rank.as<uint32_t>(), c->d_ent.as<uint2>(),
+                c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(), c->d_krec.as<KeyRec>(), 0};
+    if (!c->ing) c->ing = ingest_work_create();
+    uint64_t n_dict = 0, bad = 0;
+    std::string e;
+    phase("columns");
+    if ((rc = ingest_dictionary(c->ing, in, o, st, &n_dict, &bad, &e)))
+        return c->fail(rc, "%s", e.c_str());
+    if (n_dict > MAX_DICT) return c->fail(AD_E_CAPACITY, "more than %llu distinct ids", (unsigned long long)MAX_DICT);
+    phase("dictionary");
+    if ((rc = ingest_entries(c->ing, in, o, st, &bad, &e)))
+    {
+        const long long key = bad < nk ? (long long)K.keys[bad] : -1;
+        if (rc == AD_E_STATE) return c->fail(AD_E_INVAL, "prunedBefore of key %lld is not in byId", key);
+        if (rc == AD_E_ORDER) return c->fail(rc, "CommandsForKey of key %lld violates byId strict order (CommandsForKey.java:1438)", key);
+        return c->fail(rc, "CommandsForKey of key %lld violates status range / key-domain ids / keys ascending", key);
+    }
+    phase("entries");
+    // the extras' ranks (range commands, watermarks) for the host's range part
+    std::vector<uint32_t> xr(nx), cmd_rank(ncmd), wm_rank(nrb, 0);
+    if (nx) HIPCHK(c, hipMemcpy(xr.data(), c->d_ing_rank.as<uint32_t>() + ne + o.n_diff, 4 * nx, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < ncmd; ++i) cmd_rank[i] = xr[i];
+    for (uint64_t j = 0; j < wm_at.size(); ++j) wm_rank[wm_at[j]] = xr[ncmd + j];
+    c->h_cmd_rank = cmd_rank;
+    RangePart rp;
+    if ((rc = build_ranges(c, cmd_rank, wm_rank, &rp))) return rc;
+    phase("range commands");
+    // keys: the KeyLine perfect hash placed on the host (keys only), then on the device every key's
+    // line (k_key_slots), stabbing cell and slot of the open-addressing key hash
+    uint64_t hcap = 16;
+    while (hcap < 2 * nk) hcap <<= 1;
+    const uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
+    if ((rc = kl_place_all(c, K.keys, kl_nb, false))) return rc;
+    phase("key line perfect hash");
+    if ((rc = upload(c, c->d_kl_disp, c->kl_disp_h)) || (rc = upload(c, c->d_slices_s, c->slice_s)) ||
+        (rc = upload(c, c->d_slices_e, c->slice_e)) || (rc = upload(c, c->d_rt_start, c->rt_start)) ||
+        (rc = upload(c, c->d_rt_end, c->rt_end)))
+        return rc;
+    if (!c->d_khash.ensure(sizeof(KeySlot) * hcap) || !c->d_kslot.ensure(4 * std::max<uint64_t>(nk, 1)) ||
+        !c->d_kcell.ensure(4 * std::max<uint64_t>(nk, 1)))
+        return c->fail(AD_E_NOMEM, "key tables");
+    HIPCHK(c, run_key_slots(c->d_keys.as<int64_t>(), nk, c->d_kl_disp.as<uint32_t>(), kl_nb, c->kline_slots,
+                            c->d_kslot.as<uint32_t>(), st));
+    HIPCHK(c, ingest_keys(c->d_keys.as<int64_t>(), nk, rp.cell_ok ? c->d_cell_E.as<int64_t>() : nullptr,
+                          rp.cell_ok ? rp.cell_E.size() : 0, c->cfg.range_start_inclusive, c->d_kcell.as<uint32_t>(),
+                          c->d_khash.as<KeySlot>(), hcap, st));
+    if (!K.ballot.empty())
+    {
+        std::vector<Bal> bl(ne);
+        for (uint64_t i = 0; i < ne; ++i) bl[i] = Bal{K.ballot[i].msb, K.ballot[i].lsb, K.ballot[i].node, 0};
+        if ((rc = upload(c, c->d_ballot, bl))) return rc;
+    }
+    else
+        c->d_ballot.release();
+    phase("keys");
+    // views, the sampled dictionary, the derivation (cand / cwr / w, KeyEntry, trees)
+    const uint64_t n_samp = dict_samples(n_dict);
+    if (!c->d_ds_hi.ensure(8 * std::max<uint64_t>(n_samp, 1)) || !c->d_ds_lo.ensure(8 * std::max<uint64_t>(n_samp, 1)) ||
+        !c->d_ds_node.ensure(4 * std::max<uint64_t>(n_samp, 1)))
+        return c->fail(AD_E_NOMEM, "dictionary sample");
+    NormTid last{0, 0, 0};
+    if (n_dict)
+    {
+        HIPCHK(c, hipMemcpy(&last.hi, c->d_dict_hi.as<uint64_t>() + n_dict - 1, 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(&last.lo, c->d_dict_lo.as<uint64_t>() + n_dict - 1, 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(&last.node, c->d_dict_node.as<int32_t>() + n_dict - 1, 4, hipMemcpyDeviceToHost));
+    }
+    if ((rc = set_views(c, n_dict, n_samp, last, nk, ne, hcap, rp, nrb))) return rc;
+    if (n_samp) HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
+    if (!c->cu) c->cu = cfk_upd_work_create();
+    CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
+                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr, nullptr,
+                  c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
+    CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
+                     c->d_w.as<uint2>(), c->d_w.cap / 8};
+    uint64_t bad_e = 0;
+    if ((rc = run_cfk_derive_full(c->cu, c->ds, d, &b, cfk_need_bufs, c, st, &bad_e, &e)))
+    {
+        if (rc == AD_E_DUP_EXEC)
+        {
+            uint32_t k = 0;
+            if (bad_e < ne) (void)hipMemcpy(&k, c->d_ekey.as<uint32_t>() + bad_e, 4, hipMemcpyDeviceToHost);
+            return c->fail(rc, "CommandsForKey of key %lld violates unique committed executeAt (CommandsForKey.java:1439)",
+                           k < nk ? (long long)K.keys[k] : -1ll);
+        }
+        return c->fail(rc, "%s", e.c_str());
+    }
+    phase("derivation + trees");
+    DevSnapshot& s = c->ds;
+    HIPCHK(c, build_range_trees(s, st));
+    if (!c->d_kline.ensure(sizeof(KeyLine) * c->kline_slots)) return c->fail(AD_E_NOMEM, "key lines");
+    s.kline = c->d_kline.as<KeyLine>();
+    s.kl_lines = c->kline_slots;
+    s.kl_buckets = kl_nb;
+    s.kl_disp = c->d_kl_disp.as<uint32_t>();
+    HIPCHK(c, run_build_klines(s, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
+                               c->kline_slots, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    phase("range trees + key lines");
+    // the raw columns are consumed; the host's copies (byId ids, ranks, dictionary) follow on demand
+    c->raw_dev = false;
+    for (DevBuf* bb : {&c->d_in_tm, &c->d_in_tl, &c->d_in_tn, &c->d_in_em, &c->d_in_el, &c->d_in_en}) bb->release();
+    c->dict_msb.clear();
+    c->dict_lsb.clear();
+    c->dict_node.clear();
+    c->h_txn_rank.clear();
+    c->h_exec_rank.clear();
+    c->h_pruned.assign(nk, 0);
+    K.txn.clear();
+    K.exec.clear();
+    c->host_dict_stale = true;
+    c->host_stale = true;
+    c->host_moved = true;
+    c->host_ingested = true;
+    c->dirty = false;
+    ++c->snap_gen;
+    ++c->rank_gen;
+    c->global_ok = false;
+    c->n_global = 0;
+    c->ms_ingest = now_ms() - t0;
+    return 0;
+}
+
+static int build_snapshot_host(ad_ctx* c);
+static int build_snapshot(ad_ctx* c)
+{
+    // the device route takes a snapshot whose columns the load put in HBM, unless a node-wide
+    // dictionary is installed (its ranks are the installed dictionary's: the host route)
+    if (c->raw_dev && !c->gd_set) return build_snapshot_device(c);
+    if (int rc = host_inputs(c)) return rc;
+    c->raw_dev = false;
+    return build_snapshot_host(c);
+}
+
+static int build_snapshot_host(ad_ctx* c)
+{
+    if (int rc0 = sync_host(c)) return rc0;
+    c->dmiss_on = false;          // the host copy holds the missing() lists now; uploaded again on demand
+    const double t0 = now_ms();
+    const bool trace = getenv("AD_INGEST_TRACE") != nullptr;
+    double tp = t0;
+    auto phase = [&](const char* what) {
+        if (!trace) return;
+        const double t = now_ms();
+        fprintf(stderr, "ingest %-28s %8.1f ms\n", what, t - tp);
+        tp = t;
+    };
+    auto& K = c->cfk;
+    const uint64_t nk = K.keys.size(), ne = K.status.size();
+    const uint64_t ncmd = c->cmds.txn.size(), nrb = c->rb.wm.size();
+
+    // ---- 1. id dictionary over every id the kernels compare
+    std::vector<uint8_t> exec_differs(ne);
+    std::vector<DictRec> recs;
+    recs.reserve(ne * 2 + ncmd + nrb);
+    for (uint64_t e = 0; e < ne; ++e)
+    {
+        const NormTid n = norm(K.txn[e]);
+        recs.push_back({n.hi, n.lo, n.node, 0, e});
+        const Tid& x = K.exec[e];
+        exec_differs[e] = !(x.msb == K.txn[e].msb && x.lsb == K.txn[e].lsb && x.node == K.txn[e].node);
+        if (exec_differs[e])
+        {
+            const NormTid m = norm(x);
+            recs.push_back({m.hi, m.lo, m.node, 0, ne + e});
+        }
+    }
+    for (uint64_t i = 0; i < ncmd; ++i)
+    {
+        const NormTid n = norm(c->cmds.txn[i]);
+        recs.push_back({n.hi, n.lo, n.node, 0, 2 * ne + i});
+    }
+    for (uint64_t i = 0; i < nrb; ++i)
+    {
+        if (!tid_gt_none(c->rb.wm[i])) continue;
+        const NormTid n = norm(c->rb.wm[i]);
+        recs.push_back({n.hi, n.lo, n.node, 0, 2 * ne + ncmd + i});
+    }
+    phase("dictionary records");
+    parallel_sort(recs, rec_less);
+    phase("dictionary sort");
+    auto src_tid = [&](uint64_t s) -> const Tid& {
+        if (s < ne) return K.txn[s];
+        if (s < 2 * ne) return K.exec[s - ne];
+        if (s < 2 * ne + ncmd) return c->cmds.txn[s - 2 * ne];
+        return c->rb.wm[s - 2 * ne - ncmd];
+    };
+    std::vector<uint32_t> txn_rank(ne), exec_rank(ne), cmd_rank(ncmd), wm_rank(nrb, 0);
+    c->dict_msb.clear();
+    c->dict_lsb.clear();
+    c->dict_node.clear();
+    std::vector<uint64_t> dhi, dlo;
+    std::vector<int32_t> dnode;
+    auto set_rank = [&](uint64_t s, uint32_t rank) {
+        if (s < ne) txn_rank[s] = rank;
+        else if (s < 2 * ne) exec_rank[s - ne] = rank;
+        else if (s < 2 * ne + ncmd) cmd_rank[s - 2 * ne] = rank;
+        else wm_rank[s - 2 * ne - ncmd] = rank;
+    };
+    bool use_global = c->gd_set;
+    if (use_global)
+    {
+        // the installed node-wide dictionary (ad_set_global_dict) is this store's dictionary: every
+        // rank is a global rank, so exported parts carry the kernels' own ids (no translation)
+        const uint64_t ng = c->gd_msb.size();
+        dhi.resize(ng);
+        dlo.resize(ng);
+        dnode.resize(ng);
+        parallel_for(ng, [&](size_t a, size_t b) {
+            for (size_t i = a; i < b; ++i)
+            {
+                const NormTid n = norm(Tid{c->gd_msb[i], c->gd_lsb[i], c->gd_node[i]});
+                dhi[i] = n.hi;
+                dlo[i] = n.lo;
+                dnode[i] = n.node;
+            }
+        });
+        uint64_t gi = 0;
+        for (size_t i = 0; i < recs.size() && use_global; ++i)
+        {
+            const DictRec& r = recs[i];
+            auto g_less = [&](uint64_t j) {
+                if (dhi[j] != r.hi) return dhi[j] < r.hi;
+                if (dlo[j] != r.lo) return dlo[j] < r.lo;
+                return dnode[j] < r.node;
+            };
+            while (gi < ng && g_less(gi)) ++gi;
+            if (gi == ng || dhi[gi] != r.hi || dlo[gi] != r.lo || dnode[gi] != r.node)
+            {
+                use_global = false;
+                break;
+            }
+            const Tid& t = src_tid(r.src);
+            if (t.lsb != c->gd_lsb[gi])
+                return c->fail(AD_E_INCONSISTENT_ID, "ids equal under Timestamp.equals differ in flag bits (lsb %llx vs %llx)",
+                               (unsigned long long)t.lsb, (unsigned long long)c->gd_lsb[gi]);
+            set_rank(r.src, (uint32_t)(2 * gi + 1));
+        }
+        if (use_global)
+        {
+            if (ng > MAX_DICT) return c->fail(AD_E_CAPACITY, "more than %llu distinct ids", (unsigned long long)MAX_DICT);
+            c->dict_msb = c->gd_msb;
+            c->dict_lsb = c->gd_lsb;
+            c->dict_node = c->gd_node;
+        }
+        else
+        {
+            if (c->gd_strict) return c->fail(AD_E_INVAL, "ad_set_global_dict: an id of this store's snapshot is missing");
+            // the snapshot outgrew the installed dictionary: uninstalled, the store's own dictionary instead
+            drop_global_dict(c);
+            dhi.clear();
+            dlo.clear();
+            dnode.clear();
+        }
+    }
+    for (size_t i = 0; i < recs.size() && !use_global; ++i)
+    {
+        const DictRec& r = recs[i];
+        if (i == 0 || !rec_eq(recs[i - 1], r))
+        {
+            if (c->dict_msb.size() >= MAX_DICT) return c->fail(AD_E_CAPACITY, "more than %llu distinct ids", (unsigned long long)MAX_DICT);
+            const Tid& t = src_tid(r.src);
+            c->dict_msb.push_back(t.msb);
+            c->dict_lsb.push_back(t.lsb);
+            c->dict_node.push_back(t.node);
+            dhi.push_back(r.hi);
+            dlo.push_back(r.lo);
+            dnode.push_back(r.node);
+        }
+        else
+        {
+            const Tid& t = src_tid(r.src);
+            if (t.lsb != c->dict_lsb.back())
+                return c->fail(AD_E_INCONSISTENT_ID, "ids equal under Timestamp.equals differ in flag bits (lsb %llx vs %llx)",
+                               (unsigned long long)t.lsb, (unsigned long long)c->dict_lsb.back());
+        }
+        set_rank(r.src, (uint32_t)(2 * (c->dict_msb.size() - 1) + 1));
+    }
+    std::vector<DictRec>().swap(recs);
+    for (uint64_t e = 0; e < ne; ++e)
+        if (!exec_differs[e]) exec_rank[e] = txn_rank[e];
+    c->h_cmd_rank = cmd_rank;
+    phase("dictionary + ranks");
+
+    // ---- 2. per key validation, tau/txw, committed Writes by executeAt
+    std::vector<uint2> ent(ne);
+    std::vector<uint32_t> seg32(nk + 1), woff(nk + 1), pruned(nk, 0);
+    std::vector<int32_t> maw(nk, -1);
+    for (uint64_t k = 0; k <= nk; ++k) seg32[k] = (uint32_t)K.seg[k];
+    std::atomic<int> bad{0};
+    std::atomic<uint64_t> bad_key{0};
+    std::vector<uint32_t> wcount(nk, 0);
+    parallel_for(nk, [&](size_t ka, size_t kb) {
+        std::vector<uint32_t> ce;
+        for (size_t k = ka; k < kb; ++k)
+        {
+            const uint64_t s0 = K.seg[k], s1 = K.seg[k + 1];
+            ce.clear();
+            uint32_t nw = 0;
+            for (uint64_t e = s0; e < s1; ++e)
+            {
+                const uint8_t st = K.status[e];
+                const uint32_t kind = (uint32_t)((K.txn[e].lsb >> 1) & 7);
+                const uint32_t dom = (uint32_t)(K.txn[e].lsb & 1);
+                if (st > 7) { bad = AD_E_INVAL; bad_key = k; continue; }
+                if (e > s0 && txn_rank[e] <= txn_rank[e - 1]) { bad = AD_E_ORDER; bad_key = k; }
+                uint32_t tau;
+                if (st == AD_ST_TRANSITIVELY_KNOWN || st == AD_ST_INVALID_OR_TRUNCATED_OR_UNMANAGED_COMMITTED) tau = 0;
+                else if (st >= AD_ST_COMMITTED && ((KINDS_RS_OR_WS >> kind) & 1)) tau = exec_rank[e];
+                else tau = TAU_NEVER_ELIDED;
+                if (tau != 0 && dom != 0) { bad = AD_E_INVAL; bad_key = k; }   // live range-domain id in a CFK
+                ent[e] = make_uint2(tau, txn_rank[e] | (kind << RANK_BITS));
+                if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED)
+                {
+                    ce.push_back(exec_rank[e]);
+                    if (kind == AD_KIND_WRITE) ++nw;
+                }
+            }
+            std::sort(ce.begin(), ce.end());
+            for (size_t i = 1; i < ce.size(); ++i)
+                if (ce[i] == ce[i - 1]) { bad = AD_E_DUP_EXEC; bad_key = k; }
+            wcount[k] = nw;
+        }
+    });
+    if (bad.load())
+    {
+        const int code = bad.load();
+        return c->fail(code, "CommandsForKey of key %lld violates %s", (long long)K.keys[bad_key.load()],
+                       code == AD_E_ORDER ? "byId strict order (CommandsForKey.java:1438)"
+                       : code == AD_E_DUP_EXEC ? "unique committed executeAt (CommandsForKey.java:1439)"
+                                               : "status range / key-domain ids");
+    }
+    for (uint64_t k = 0; k + 1 <= nk; ++k)
+        if (k > 0 && K.keys[k - 1] >= K.keys[k]) return c->fail(AD_E_INVAL, "keys not strictly ascending");
+    woff[0] = 0;
+    for (uint64_t k = 0; k < nk; ++k) woff[k + 1] = woff[k] + wcount[k];
+    std::vector<uint2> w(woff[nk]);
+    parallel_for(nk, [&](size_t ka, size_t kb) {
+        std::vector<std::pair<uint32_t, std::pair<uint32_t, uint8_t>>> tmp;
+        for (size_t k = ka; k < kb; ++k)
+        {
+            tmp.clear();
+            for (uint64_t e = K.seg[k]; e < K.seg[k + 1]; ++e)
+            {
+                const uint8_t st = K.status[e];
+                const uint32_t kind = (uint32_t)((K.txn[e].lsb >> 1) & 7);
+                if (st >= AD_ST_COMMITTED && st <= AD_ST_APPLIED && kind == AD_KIND_WRITE)
+                    tmp.push_back({exec_rank[e], {txn_rank[e], st}});
+            }
+            std::sort(tmp.begin(), tmp.end());
+            int32_t m = -1;
+            for (size_t i = 0; i < tmp.size(); ++i)
+            {
+                w[woff[k] + i] = make_uint2(tmp[i].first, tmp[i].second.first);
+                if (tmp[i].second.second == AD_ST_APPLIED) m = (int32_t)(woff[k] + i);   // maxAppliedWriteByExecuteAt
+            }
+            maw[k] = m;
+            if (!K.pruned.empty() && K.pruned[k] >= 0)
+            {
+                const uint64_t idx = K.seg[k] + (uint64_t)K.pruned[k];
+                if (idx >= K.seg[k + 1]) { bad = AD_E_INVAL; bad_key = k; continue; }
+                pruned[k] = txn_rank[idx];
+            }
+        }
+    });
+    if (bad.load()) return c->fail(AD_E_INVAL, "prunedBefore of key %lld is not in byId", (long long)K.keys[bad_key.load()]);
+    phase("entries + committed Writes");
+
+    // ---- 3. range commands: (range, command) entries sorted by (start, end, txnId); range table
+    RangePart rp;
+    if (int rc = build_ranges(c, cmd_rank, wm_rank, &rp)) return rc;
+    const std::vector<int64_t>& cell_E = rp.cell_E;
+    const bool cell_ok = rp.cell_ok;
+    struct { uint64_t n; uint64_t size() const { return n; } } rent{rp.n_rent};
+    phase("range commands");
     // ---- 4. upload CFK + dictionary, build the trees
     int rc;
     ent.resize(std::max<uint64_t>(64, (ne + 63) / 64 * 64), make_uint2(0u, 0u));   // whole 64-entry frames (tau 0: never emitted)
@@ -920,6 +1232,7 @@ static int build_snapshot(ad_ctx* c)
             last_w_txn[k] = has_w ? (tmp[tail].y & RANK_MASK) : 0u;
         }
     });
+    phase("emission lists");
     std::vector<KeyEntry> kent(std::max<uint64_t>(nk, 1));
     std::vector<uint32_t> kslot(std::max<uint64_t>(nk, 1)), kcells(std::max<uint64_t>(nk, 1), NO_CELL);
     // perfect hash of the keys onto KeyLines (hash and displace, common.hpp): buckets of ~4 keys,
@@ -929,6 +1242,7 @@ static int build_snapshot(ad_ctx* c)
     for (uint64_t k = 0; k < nk; ++k)
         kslot[k] = (uint32_t)kl_index(key_hash2(K.keys[k]), c->kl_disp_h[kl_bucket(key_hash(K.keys[k]), kl_nb)], c->kline_slots);
     const std::vector<uint32_t>& kl_disp = c->kl_disp_h;
+    phase("key line perfect hash");
     for (uint64_t k = 0; k < nk; ++k)
     {
         uint64_t h = key_hash(K.keys[k]) & (hcap - 1);
@@ -970,6 +1284,7 @@ static int build_snapshot(ad_ctx* c)
         if ((rc = upload(c, c->d_status, K.status)) || (rc = upload(c, c->d_xrank, exec_rank)) || (rc = upload(c, c->d_ekey, ekey)))
             return rc;
     }
+    phase("key hash + KeyEntry + entry uploads");
     std::vector<uint64_t> shi, slo;
     std::vector<int32_t> snode;
     for (uint64_t i = 0; i < dhi.size(); i += DICT_SAMP)
@@ -989,83 +1304,16 @@ static int build_snapshot(ad_ctx* c)
         (rc = upload(c, c->d_rt_end, c->rt_end)))
         return rc;
 
+    phase("uploads");
     DevSnapshot& s = c->ds;
-    s = DevSnapshot{};
-    s.dict_hi = c->d_dict_hi.as<uint64_t>();
-    s.dict_lo = c->d_dict_lo.as<uint64_t>();
-    s.dict_node = c->d_dict_node.as<int32_t>();
-    s.n_dict = dhi.size();
-    s.ds_hi = c->d_ds_hi.as<uint64_t>();
-    s.ds_lo = c->d_ds_lo.as<uint64_t>();
-    s.ds_node = c->d_ds_node.as<int32_t>();
-    s.n_samp = shi.size();
-    if (!dhi.empty())
     {
-        s.dict_last_hi = dhi.back();
-        s.dict_last_lo = dlo.back();
-        s.dict_last_node = dnode.back();
+        const NormTid last = dhi.empty() ? NormTid{0, 0, 0} : NormTid{dhi.back(), dlo.back(), dnode.back()};
+        RangePart rpv;
+        rpv.cell_ok = cell_ok;
+        rpv.n_rent = rent.size();
+        if (cell_ok) rpv.cell_E = cell_E;
+        if (int rc2 = set_views(c, dhi.size(), shi.size(), last, nk, ne, hcap, rpv, nrb)) return rc2;
     }
-    s.n_keys = nk;
-    s.keys = c->d_keys.as<int64_t>();
-    s.krec = c->d_krec.as<KeyRec>();
-    s.khash = c->d_khash.as<KeySlot>();
-    s.kent = c->d_kent.as<KeyEntry>();
-    s.cand = c->d_cand.as<uint32_t>();
-    s.cwr = c->d_cwr.as<uint32_t>();
-    s.khash_mask = hcap - 1;
-    s.n_ent = ne;
-    s.ent = c->d_ent.as<uint2>();
-    s.w = c->d_w.as<uint2>();
-    s.lvl_n[0] = ne;
-    int L = 1;
-    while (s.lvl_n[L - 1] > 64 && L < MAX_LEVELS)
-    {
-        s.lvl_n[L] = (s.lvl_n[L - 1] + 63) / 64;
-        ++L;
-    }
-    s.n_levels = L;
-    for (int l = 1; l < L; ++l)
-        for (int cl = 0; cl < NCLASS; ++cl)
-        {
-            if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * ((s.lvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "tree level");
-            s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
-        }
-    s.n_rent = rent.size();
-    s.n_cell_E = cell_ok ? cell_E.size() : 0;
-    s.cell_E = cell_ok ? c->d_cell_E.as<int64_t>() : nullptr;
-    s.cell_off = cell_ok ? c->d_cell_off.as<uint32_t>() : nullptr;
-    s.cell_ent = cell_ok ? c->d_cell_ent.as<uint64_t>() : nullptr;
-    if (!cell_ok) c->n_cell_ent = 0;
-    s.r_start = c->d_rstart.as<int64_t>();
-    s.r_end = c->d_rend.as<int64_t>();
-    s.r_txw = c->d_rtxw.as<uint32_t>();
-    s.r_rid = c->d_rrid.as<uint32_t>();
-    s.rlvl_n[0] = s.n_rent;
-    L = 1;
-    while (s.rlvl_n[L - 1] > 64 && L < MAX_LEVELS)
-    {
-        s.rlvl_n[L] = (s.rlvl_n[L - 1] + 63) / 64;
-        ++L;
-    }
-    s.n_rlevels = L;
-    for (int l = 1; l < L; ++l)
-        for (int cl = 0; cl < NCLASS; ++cl)
-        {
-            if (!c->d_rlvl[cl][l].ensure(sizeof(int64_t) * ((s.rlvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "range tree level");
-            s.rlvl[cl][l] = c->d_rlvl[cl][l].as<int64_t>();
-        }
-    s.n_rb = nrb;
-    s.rb_start = c->d_rb_s.as<int64_t>();
-    s.rb_end = c->d_rb_e.as<int64_t>();
-    s.rb_e0 = c->d_rb_e0.as<int64_t>();
-    s.rb_e1 = c->d_rb_e1.as<int64_t>();
-    s.rb_wm = c->d_rb_wm.as<uint32_t>();
-    s.rb_rid = c->d_rb_rid.as<uint32_t>();
-    s.n_slices = c->slice_s.size();
-    s.slice_start = c->d_slices_s.as<int64_t>();
-    s.slice_end = c->d_slices_e.as<int64_t>();
-    s.start_inclusive = c->cfg.range_start_inclusive;
-    s.elide = c->cfg.elide;
     HIPCHK(c, build_cfk_trees(s, c->stream));
     HIPCHK(c, build_range_trees(s, c->stream));
     // the lean kernels' KeyLine table, indexed by the keys' perfect hash
@@ -1077,6 +1325,7 @@ static int build_snapshot(ad_ctx* c)
     HIPCHK(c, run_build_klines(s, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
                                c->kline_slots, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    phase("device trees + key lines");
     c->h_txn_rank.swap(txn_rank);
     c->h_exec_rank.swap(exec_rank);
     c->h_pruned.swap(pruned);
@@ -1113,8 +1362,58 @@ static int pull_missing(ad_ctx* c)
     return 0;
 }
 
+// The dictionary's host copy after a device ingest (read back on first use)
+static int host_dict(ad_ctx* c)
+{
+    if (!c->host_dict_stale) return 0;
+    const uint64_t nd = c->ds.n_dict;
+    c->dict_msb.resize(nd);
+    c->dict_lsb.resize(nd);
+    c->dict_node.resize(nd);
+    if (nd)
+    {
+        HIPCHK(c, hipMemcpyAsync(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->dict_node.data(), c->d_dict_node.p, 4 * nd, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    c->host_dict_stale = false;
+    return 0;
+}
+
+// The loaded byId ids on the host (ad_cfk_load left them in HBM only): read back from the raw columns
+static int host_inputs(ad_ctx* c)
+{
+    auto& K = c->cfk;
+    if (!c->raw_dev || K.txn.size() == c->raw_ne) return 0;
+    const uint64_t ne = c->raw_ne;
+    std::vector<uint64_t> tm(ne), tl(ne), em(ne), el(ne);
+    std::vector<int32_t> tn(ne), en(ne);
+    if (ne)
+    {
+        HIPCHK(c, hipMemcpy(tm.data(), c->d_in_tm.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(tl.data(), c->d_in_tl.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(tn.data(), c->d_in_tn.p, 4 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(em.data(), c->d_in_em.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(el.data(), c->d_in_el.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(en.data(), c->d_in_en.p, 4 * ne, hipMemcpyDeviceToHost));
+    }
+    K.txn.resize(ne);
+    K.exec.resize(ne);
+    parallel_for(ne, [&](size_t a, size_t b) {
+        for (size_t e = a; e < b; ++e)
+        {
+            K.txn[e] = {tm[e], tl[e], tn[e]};
+            K.exec[e] = {em[e], el[e], en[e]};
+        }
+    });
+    return 0;
+}
+
 static int sync_host(ad_ctx* c)
 {
+    if (int rc = host_dict(c)) return rc;
+    if (int rc = host_inputs(c)) return rc;
     if (!c->host_stale) return 0;
     if (int rc = sync_host_entries(c)) return rc;
     return c->dmiss_on ? pull_missing(c) : 0;
@@ -1185,7 +1484,8 @@ static int sync_host_entries(ad_ctx* c)
         if (c->h_pruned.size() == nk)
             for (uint64_t k = 0; k < nk; ++k) c->h_pruned[k] = kr[k].pruned;
         c->h_exec_rank.swap(xr);
-        if (!K.miss_off.empty()) K.miss_stale = true;       // entries moved: load the lists again
+        if (!K.miss_off.empty() && !c->host_ingested) K.miss_stale = true;       // entries moved: load the lists again
+        c->host_ingested = false;
         c->host_moved = false;
         c->host_stale = false;
         return 0;
@@ -1787,6 +2087,7 @@ void ad_ctx_destroy(ad_ctx* c)
         if (e) (void)hipEventDestroy(e);
     if (c->lv) levels_work_destroy(c->lv);
     if (c->cu) cfk_upd_work_destroy(c->cu);
+    if (c->ing) ingest_work_destroy(c->ing);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1806,16 +2107,45 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     if (nk) std::copy(in->seg, in->seg + nk + 1, K.seg.begin());
     for (uint64_t k = 0; k < nk; ++k)
         if (K.seg[k] > K.seg[k + 1]) return c->fail(AD_E_INVAL, "seg not monotone");
-    K.txn.resize(ne);
-    K.exec.resize(ne);
-    for (uint64_t e = 0; e < ne; ++e)
-    {
-        K.txn[e] = {in->txn_msb[e], in->txn_lsb[e], in->txn_node[e]};
-        K.exec[e] = {in->exec_msb[e], in->exec_lsb[e], in->exec_node[e]};
-    }
     K.status.assign(in->status, in->status + ne);
     K.pruned.clear();
     if (in->pruned_before) K.pruned.assign(in->pruned_before, in->pruned_before + nk);
+    // the byId ids go to HBM as they are (the device ingest reads them there; the host copy is read
+    // back only when a host path needs it); AD_INGEST_HOST keeps the host ingest
+    c->raw_dev = false;
+    if (getenv("AD_INGEST_HOST") == nullptr)
+    {
+        if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+        auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+            if (!b.ensure(std::max<size_t>(bytes, 8))) return c->fail(AD_E_NOMEM, "hipMalloc %zu (snapshot columns)", bytes);
+            if (bytes) HIPCHK(c, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+            return 0;
+        };
+        int rc;
+        if ((rc = up(c->d_keys, in->keys, 8 * nk)) || (rc = up(c->d_in_seg, in->seg, 8 * (nk + 1))) ||
+            (rc = up(c->d_in_tm, in->txn_msb, 8 * ne)) || (rc = up(c->d_in_tl, in->txn_lsb, 8 * ne)) ||
+            (rc = up(c->d_in_tn, in->txn_node, 4 * ne)) || (rc = up(c->d_in_em, in->exec_msb, 8 * ne)) ||
+            (rc = up(c->d_in_el, in->exec_lsb, 8 * ne)) || (rc = up(c->d_in_en, in->exec_node, 4 * ne)) ||
+            (rc = up(c->d_status, in->status, ne)) ||
+            (in->pruned_before && (rc = up(c->d_in_pruned, in->pruned_before, 8 * nk))))
+            return rc;
+        K.txn.clear();
+        K.exec.clear();
+        c->raw_dev = true;
+        c->raw_ne = ne;
+    }
+    else
+    {
+        K.txn.resize(ne);
+        K.exec.resize(ne);
+        parallel_for(ne, [&](size_t a, size_t b) {
+            for (size_t e = a; e < b; ++e)
+            {
+                K.txn[e] = {in->txn_msb[e], in->txn_lsb[e], in->txn_node[e]};
+                K.exec[e] = {in->exec_msb[e], in->exec_lsb[e], in->exec_node[e]};
+            }
+        });
+    }
     K.miss_off.clear();
     K.miss.clear();
     K.miss_stale = false;
@@ -1827,6 +2157,9 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     c->d_mref2.release();
     K.loaded = true;
     c->host_stale = false;       // the load replaces whatever ad_cfk_update applied on the device
+    c->host_moved = false;
+    c->host_dict_stale = false;
+    c->host_ingested = false;
     drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
     c->dirty = true;
     return AD_OK;
@@ -2149,6 +2482,7 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
 // recovery facts normalised. Host-built from the loaded commands; rebuilt when ranks change.
 static int build_rv_ranges(ad_ctx* c, bool live_cmds)
 {
+    if (int rc = host_dict(c)) return rc;
     int rc;
         const auto& R = c->cmds;
         const size_t nc = R.txn.size(), nre = c->h_rtxw.size();
@@ -2532,6 +2866,7 @@ void ad_result_free(ad_deps_result* r)
 
 int ad_dict(const ad_ctx* c, uint64_t* n, const uint64_t** msb, const uint64_t** lsb, const int32_t** node)
 {
+    if (c && host_dict(const_cast<ad_ctx*>(c))) return AD_E_DEVICE;
     if (!c || !n) return AD_E_INVAL;
     *n = c->dict_msb.size();
     if (msb) *msb = c->dict_msb.data();
@@ -2680,6 +3015,7 @@ int ad_set_global_dict(ad_ctx* c, uint64_t n, const uint64_t* msb, const uint64_
 static int export_sizes(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, uint32_t n_dest,
                         const uint64_t* dest_first, uint32_t id_format, hipStream_t st, ExportArgs* pa)
 {
+    if (int rc = host_dict(c)) return rc;
     if (!res || !dest_first || n_dest == 0) return c->fail(AD_E_INVAL, "export: result, dest_first and n_dest are required");
     if (c->dirty) return c->fail(AD_E_NOT_LOADED, "export: no prepared snapshot");
     const uint64_t n = res->n_txns;
@@ -3238,6 +3574,9 @@ static int cfk_dict_swap(void* vc, uint64_t** hi, uint64_t** lo, int32_t** node,
 // (r = 2i+1 -> 2(i + #{pos <= i}) + 1, the device remap)
 static int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipStream_t st)
 {
+    // (the whole dictionary is read back below; host rank copies that are stale -- host_moved -- are
+    // rebuilt from the device later, their remap here is then moot)
+    c->host_dict_stale = false;
     const uint64_t nd = c->ds.n_dict;
     std::vector<uint64_t> pos(U);
     c->dict_msb.resize(nd);
@@ -3359,6 +3698,7 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
                        c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
                        c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
                        c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
+    if (int rc = host_dict(c)) return rc;
     const uint64_t nd0 = c->dict_msb.size();
     CfkMiss miss;
     miss.on = c->dmiss_on && u.dep_off;
@@ -3385,6 +3725,7 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         // keys created on the device (they stay when the batch then failed): KeyLines, host copies
         if (int rc2 = cfk_after_new_keys(c, o, st)) return rc2;
         c->host_moved = true;
+        c->host_ingested = false;     // entries moved after the ingest
         c->host_stale = true;
         ++c->snap_gen;
     }
@@ -3394,6 +3735,7 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         if (int rc2 = cfk_after_merge(c, o.merge_pos, o.n_new_ids, st)) return rc2;
         drop_global_dict(c);
         c->host_moved = true;        // entry ranks changed: host copies rebuilt from the device
+        c->host_ingested = false;     // entries moved after the ingest
         c->host_stale = true;
         ++c->snap_gen;
     }
@@ -3419,7 +3761,7 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
             c->ds.n_samp = ns;
         }
     }
-    if (o.n_inserted) c->host_moved = true;
+    if (o.n_inserted) { c->host_moved = true; c->host_ingested = false; }
     if ((rc == 0 || o.rolled_back || o.rederived) && c->kline_slots)
         HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
                                    c->kline_slots, st));
@@ -4099,6 +4441,7 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
         if (K.pruned.empty()) K.pruned.assign(nk, -1);
         if (c->h_pruned.size() != nk) c->h_pruned.assign(nk, 0);
         c->host_moved = true;
+        c->host_ingested = false;     // entries moved after the ingest
         c->host_stale = true;
         ++c->snap_gen;
     }

@@ -2415,6 +2415,29 @@ __global__ __launch_bounds__(256) void k_prune_move(uint64_t ne, EntArrays a, co
 
 }  // namespace
 
+// A freshly ingested snapshot (ingest.hip): every derived array from the per-entry state, the
+// committed order sorted in full.
+int run_cfk_derive_full(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, CfkDerivedBufs* bufs,
+                        int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                        hipStream_t st, uint64_t* bad_entry, std::string* err)
+{
+    if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
+    UALLOC(w->ctl, sizeof(UpdCtl), false);
+    UCHK(hipMemsetAsync(w->ctl.p, 0, sizeof(UpdCtl), st));
+    w->cm_valid = false;
+    w->moved = false;
+    if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rc;
+    UCHK(hipMemcpyAsync(w->h_ctl, w->ctl.p, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(hipStreamSynchronize(st));
+    if (w->h_ctl->err)
+    {
+        *bad_entry = w->h_ctl->err_idx;
+        *err = "two committed entries of one key share an executeAt (CommandsForKey.java:1439)";
+        return AD_E_DUP_EXEC;
+    }
+    return AD_OK;
+}
+
 int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t* klist, uint64_t nl, int32_t prune_interval,
                   int64_t min_hlc_delta, CfkDerivedBufs* bufs,
                   int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,

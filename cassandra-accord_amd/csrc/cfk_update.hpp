@@ -154,6 +154,13 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
                    int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
                    const CfkGrow& grow, hipStream_t st, CfkUpdOut* out, std::string* err, CfkMiss* miss = nullptr);
 
+// Every derived array (ent.tau, cand, cwr, w, krec's Write fields, kent, trees) of a snapshot whose
+// per-entry state was just built (ingest.hip); AD_E_DUP_EXEC with *bad_entry on a duplicate committed
+// executeAt (CommandsForKey.java:1439).
+int run_cfk_derive_full(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, CfkDerivedBufs* bufs,
+                        int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                        hipStream_t st, uint64_t* bad_entry, std::string* err);
+
 struct CfkPruneOut {
     uint64_t n_removed = 0;        // entries removed
     uint64_t n_keys_pruned = 0;    // CommandsForKeys whose prunedBefore moved

@@ -542,7 +542,7 @@ hipError_t run_range(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // ---------------------------------------------------------------------------------------
 constexpr uint32_t K2_MAXP = 64;     // probes per request on the LDS path
 constexpr uint32_t K2_CAP = 512;     // elements per list family on the LDS path
-constexpr uint32_t K2_REGION_CHUNK = 1u << 16;
+constexpr uint32_t K2_REGION_CHUNK = 1u << 14;
 
 
 struct K2Mem {

@@ -130,14 +130,29 @@ __device__ __forceinline__ void seg_bitonic_wide(T& x0, T& x1)
         }
 }
 
+#ifndef LEAN_ADAPT
+#define LEAN_ADAPT 1
+#endif
+constexpr uint64_t LEAN_CHUNK_MIN = 2048, LEAN_CHUNK_FIRST = 8192;
 struct LeanChunk {
-    uint64_t cur = 0, end = 0;
-    // wave-uniform bump allocation from the region arena
-    __device__ __forceinline__ uint64_t take(BatchCtl* ctl, uint64_t nbytes, uint64_t cap)
+    uint64_t cur = 0, end = 0, used = 0;
+    // wave-uniform bump allocation from the region arena. A refill is sized for what the wave will still
+    // write -- its bytes per item so far times the items it has left, + 1/8 -- between LEAN_CHUNK_MIN and
+    // LEAN_CHUNK, so the arena stays dense (the unused tail of a wave's last chunk is all it leaves) with
+    // a few refills per wave
+    __device__ __forceinline__ uint64_t take(BatchCtl* ctl, uint64_t nbytes, uint64_t cap, uint32_t items_done,
+                                             uint32_t items_left)
     {
         if (nbytes > end - cur)
         {
-            const uint64_t sz = nbytes > LEAN_CHUNK ? nbytes : LEAN_CHUNK;
+            uint64_t want = LEAN_ADAPT ? LEAN_CHUNK_FIRST : LEAN_CHUNK;
+            if (LEAN_ADAPT && items_done)
+            {
+                const uint64_t est = used / items_done * items_left;
+                want = (est + (est >> 3) + 255) & ~255ull;
+            }
+            want = want < LEAN_CHUNK_MIN ? LEAN_CHUNK_MIN : (want > LEAN_CHUNK ? LEAN_CHUNK : want);
+            const uint64_t sz = nbytes > want ? nbytes : want;
             unsigned long long base = 0;
             if (lane_id() == 0) base = atomicAdd(&ctl->reg_top, (unsigned long long)sz);
             base = uniform64(base);
@@ -147,6 +162,7 @@ struct LeanChunk {
         }
         const uint64_t r = cur;
         cur += nbytes;
+        used += nbytes;
         return r;
     }
 };
@@ -207,6 +223,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
 
     LeanChunk ralloc;
+    uint32_t cur_it = 0;         // the wave's current item (wave-uniform): sizes its region refills
+    const uint32_t it_first = uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
     // one wave-uniform region allocation for the segments' byte counts (at each segment's lane 0):
     // returns this segment's offset; `fits` whether the whole allocation is inside the arena
     auto seg_alloc = [&](uint64_t bytes, bool& fits) -> uint64_t {
@@ -218,7 +236,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             if (k == h) mine = total;
             total += bk;
         }
-        const uint64_t base = ralloc.take(b.ctl, total, reg_cap);
+        const uint32_t done = (cur_it - it_first) / nw, left = (n_items - 1 - cur_it) / nw + 1;
+        const uint64_t base = ralloc.take(b.ctl, total, reg_cap, done, left);
         fits = base + total <= reg_cap;
         return base + mine;
     };
@@ -433,6 +452,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 
     for (uint32_t it = it0; it < n_items; it += nw)
     {
+        cur_it = it;
         const uint32_t t = qc.t;
 
         // ---- current item: per key p = hl < np, newest test and emission counts

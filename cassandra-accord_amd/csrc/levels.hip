@@ -881,10 +881,10 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-        // measured on config 5 (scripts/c5_sweep.sh): one 256-thread block per CU beats 2 and 4 (the
-        // polls of more resident waiters load the memory system the hand-offs go through); naps between
-        // polls hardly matter at that residency
-        int per_cu = 1, naps = 1, threads = 256;
+        // measured on config 5 (scripts/c5_sweep.sh): one wave per CU (0.85 ms) beats a 256-thread block
+        // per CU (1.01 ms) and 2 / 4 blocks (1.13 / 1.50 ms): the polls of more resident waiters load the
+        // memory system the hand-offs go through; naps between polls hardly matter at that residency
+        int per_cu = 1, naps = 1, threads = 64;
         if (const char* e = getenv("AD_LEVELS_PULL_PER_CU")) per_cu = std::max(1, std::min(8, atoi(e)));
         if (const char* e = getenv("AD_LEVELS_PULL_NAPS")) naps = std::max(0, std::min(64, atoi(e)));
         if (const char* e = getenv("AD_LEVELS_PULL_THREADS")) threads = atoi(e) == 64 ? 64 : (atoi(e) == 128 ? 128 : 256);

@@ -28,7 +28,7 @@ constexpr int FWAVES = 4;       // waves per workgroup
 #ifndef FUSED_WPE
 #define FUSED_WPE 4          // waves per SIMD the general kernel's register budget is sized for
 #endif
-constexpr uint32_t F_REGION_CHUNK = 1u << 16;
+constexpr uint32_t F_REGION_CHUNK = 1u << 14;   // region bytes per refill (small: the arena stays dense)
 
 struct FusedLds {
     uint32_t st0[FMAXP][FCAP0];
