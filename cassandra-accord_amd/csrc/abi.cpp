@@ -213,7 +213,8 @@ struct ad_ctx {
     // host state of the KeyLine perfect hash (incremental placement of new keys)
     std::vector<uint32_t> kl_disp_h;
     std::vector<uint8_t> kl_used;
-    std::vector<std::vector<int64_t>> kl_members;
+    std::vector<std::vector<int64_t>> kl_members;   // per bucket (built on first use from kl_keys_all)
+    std::vector<int64_t> kl_keys_all;
     uint64_t kl_nb_h = 0;
     DevBuf d_keys2, d_krec2, d_kcell2, d_khash2, d_kent2;   // spare key-indexed arrays (new keys)
 
@@ -410,37 +411,56 @@ static int kl_place_all(ad_ctx* c, const std::vector<int64_t>& keys, uint64_t nb
     // updates it is rebuilt half full, where a bucket of ~4 keys is placed again in ~16 displacement
     // tries (kl_add_keys)
     uint64_t m = std::max<uint64_t>(1, sparse ? 2 * nk : nk + nk / 4);
-    std::vector<std::vector<int64_t>> members(nb);
-    for (int64_t key : keys) members[kl_bucket(key_hash(key), nb)].push_back(key);
-    std::vector<uint32_t> border(nb);
-    for (uint64_t b = 0; b < nb; ++b) border[b] = (uint32_t)b;
-    std::stable_sort(border.begin(), border.end(), [&](uint32_t a, uint32_t b) { return members[a].size() > members[b].size(); });
+    // the keys' second hashes grouped by bucket (counting sort), buckets by size, largest first
+    // (stable: equal sizes in bucket order)
+    std::vector<uint32_t> kb(nk), boff(nb + 1, 0);
+    parallel_for(nk, [&](size_t a, size_t e) {
+        for (size_t i = a; i < e; ++i) kb[i] = (uint32_t)kl_bucket(key_hash(keys[i]), nb);
+    });
+    for (uint64_t i = 0; i < nk; ++i) ++boff[kb[i] + 1];
+    uint32_t max_sz = 0;
+    for (uint64_t x = 0; x < nb; ++x) max_sz = std::max(max_sz, boff[x + 1]);
+    for (uint64_t x = 0; x < nb; ++x) boff[x + 1] += boff[x];
+    std::vector<uint64_t> hs(nk);
+    {
+        std::vector<uint32_t> cur(boff.begin(), boff.end() - 1);
+        for (uint64_t i = 0; i < nk; ++i) hs[cur[kb[i]]++] = key_hash2(keys[i]);
+    }
+    std::vector<uint32_t> border;
+    border.reserve(nb);
+    {
+        std::vector<uint32_t> by(max_sz + 2, 0);
+        for (uint64_t x = 0; x < nb; ++x) ++by[max_sz - (boff[x + 1] - boff[x]) + 1];
+        for (uint32_t z = 0; z <= max_sz; ++z) by[z + 1] += by[z];
+        border.resize(nb);
+        for (uint64_t x = 0; x < nb; ++x) border[by[max_sz - (boff[x + 1] - boff[x])]++] = (uint32_t)x;
+    }
     std::vector<uint32_t> disp(nb, 0);
+    std::vector<uint64_t> pos;
     for (int attempt = 0;; ++attempt)
     {
         std::vector<uint8_t> used(m, 0);
         bool ok = true;
-        std::vector<uint64_t> pos;
-        for (uint32_t b : border)
+        for (uint32_t bk : border)
         {
-            const auto& mb = members[b];
-            if (mb.empty()) continue;
+            const uint32_t lo = boff[bk], hi = boff[bk + 1];
+            if (lo == hi) continue;
             uint32_t d = 0;
             for (;; ++d)
             {
                 if (d == (1u << 22)) { ok = false; break; }
                 pos.clear();
                 bool fit = true;
-                for (size_t i = 0; i < mb.size() && fit; ++i)
+                for (uint32_t i = lo; i < hi && fit; ++i)
                 {
-                    const uint64_t p = kl_index(key_hash2(mb[i]), d, m);
+                    const uint64_t p = kl_index(hs[i], d, m);
                     if (used[p] || std::find(pos.begin(), pos.end(), p) != pos.end()) fit = false;
                     pos.push_back(p);
                 }
                 if (fit) break;
             }
             if (!ok) break;
-            disp[b] = d;
+            disp[bk] = d;
             for (uint64_t p : pos) used[p] = 1;
         }
         if (ok)
@@ -454,8 +474,19 @@ static int kl_place_all(ad_ctx* c, const std::vector<int64_t>& keys, uint64_t nb
     c->kline_slots = m;
     c->kl_nb_h = nb;
     c->kl_disp_h.swap(disp);
-    c->kl_members.swap(members);
+    // members per bucket, for new keys later (kl_add_keys): built on first use
+    c->kl_members.clear();
+    c->kl_keys_all = keys;
     return 0;
+}
+
+// the per-bucket members of the placed keys (kl_add_keys), from the keys the table was placed for
+static void kl_members_ensure(ad_ctx* c)
+{
+    if (!c->kl_members.empty() || c->kl_keys_all.empty()) return;
+    c->kl_members.assign(c->kl_nb_h, {});
+    for (int64_t key : c->kl_keys_all) c->kl_members[kl_bucket(key_hash(key), c->kl_nb_h)].push_back(key);
+    std::vector<int64_t>().swap(c->kl_keys_all);
 }
 
 // New keys into the perfect hash: a bucket keeps its displacement when its new keys land on free
@@ -470,6 +501,7 @@ static int kl_add_keys(ad_ctx* c, const std::vector<int64_t>& nkeys, uint64_t nk
         *need_rebuild = true;
         return 0;
     }
+    kl_members_ensure(c);
     std::vector<std::pair<uint32_t, int64_t>> adds;
     adds.reserve(nkeys.size());
     for (int64_t key : nkeys) adds.push_back({(uint32_t)kl_bucket(key_hash(key), nb), key});
@@ -792,6 +824,12 @@ static int build_snapshot_device(ad_ctx* c)
     if (!c->ing) c->ing = ingest_work_create();
     uint64_t n_dict = 0, bad = 0;
     std::string e;
+    // the KeyLine perfect hash is placed on a host thread (keys only) while the device builds the
+    // dictionary and the entries
+    const uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
+    int kl_rc = 0;
+    std::thread kl_thread([&]() { kl_rc = kl_place_all(c, K.keys, kl_nb, false); });
+    struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } kl_join{kl_thread};
     phase("columns");
     if ((rc = ingest_dictionary(c->ing, in, o, st, &n_dict, &bad, &e)))
         return c->fail(rc, "%s", e.c_str());
@@ -818,9 +856,9 @@ static int build_snapshot_device(ad_ctx* c)
     // line (k_key_slots), stabbing cell and slot of the open-addressing key hash
     uint64_t hcap = 16;
     while (hcap < 2 * nk) hcap <<= 1;
-    const uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
-    if ((rc = kl_place_all(c, K.keys, kl_nb, false))) return rc;
-    phase("key line perfect hash");
+    kl_thread.join();
+    if (kl_rc) return c->fail(kl_rc, "key perfect hash did not converge");
+    phase("key line perfect hash (wait)");
     if ((rc = upload(c, c->d_kl_disp, c->kl_disp_h)) || (rc = upload(c, c->d_slices_s, c->slice_s)) ||
         (rc = upload(c, c->d_slices_e, c->slice_e)) || (rc = upload(c, c->d_rt_start, c->rt_start)) ||
         (rc = upload(c, c->d_rt_end, c->rt_end)))
@@ -904,6 +942,9 @@ static int build_snapshot_device(ad_ctx* c)
     c->dirty = false;
     ++c->snap_gen;
     ++c->rank_gen;
+    // the update path's state between batches (incremental committed order, per-entry change flags)
+    // starts afresh, as after a host build
+    cfk_upd_work_invalidate(c->cu);
     c->global_ok = false;
     c->n_global = 0;
     c->ms_ingest = now_ms() - t0;
@@ -1718,6 +1759,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     if (c->rng_cap < want_rng) c->rng_cap = want_rng;
     if (c->scr_cap < want_scr) c->scr_cap = want_scr;
     if (c->reg_cap < want_reg) c->reg_cap = want_reg;
+    constexpr uint64_t REG_CAP_MAX = (1ull << 35) - (1ull << 20);     // lean region offsets: 32-bit, 8-byte units
+    c->reg_cap = std::min(c->reg_cap, REG_CAP_MAX);
 
     for (int attempt = 0; attempt < 8; ++attempt)
     {
@@ -1874,7 +1917,11 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             if (h.overflow & 1u) c->key_cap = std::max<uint64_t>(c->key_cap * 2, h.key_top + (h.key_top >> 1));
             if (h.overflow & 2u) c->rng_cap = std::max<uint64_t>(c->rng_cap * 2, h.rng_top + (h.rng_top >> 1));
             if (h.overflow & 4u) c->scr_cap = std::max<uint64_t>(c->scr_cap * 2, h.scr_top + (h.scr_top >> 1));
-            if (h.overflow & 8u) c->reg_cap = std::max<uint64_t>(c->reg_cap * 2, h.reg_top + (h.reg_top >> 1));
+            if (h.overflow & 8u)
+            {
+                if (c->reg_cap >= REG_CAP_MAX) return c->fail(AD_E_CAPACITY, "batch output beyond the 32 GB region arena");
+                c->reg_cap = std::min<uint64_t>(std::max<uint64_t>(c->reg_cap * 2, h.reg_top + (h.reg_top >> 1)), REG_CAP_MAX);
+            }
             continue;
         }
         if (h.overflow & OVF_PACK)

@@ -2198,7 +2198,12 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
             *err = "deps-derived additions: " + *err;
             return rc;
         }
-        if (o2.merged || o2.n_new_ids || o2.n_new_keys) { *err = "deps-derived additions grew the dictionary (internal)"; return AD_E_STATE; }
+        if (o2.merged || o2.n_new_ids || o2.n_new_keys)
+        {
+            *err = "deps-derived additions grew the dictionary (internal: merged " + std::to_string((int)o2.merged) + ", new ids " +
+                   std::to_string(o2.n_new_ids) + ", new keys " + std::to_string(o2.n_new_keys) + ")";
+            return AD_E_STATE;
+        }
         out->n_additions = o2.n_inserted;
         out->n_applied += o2.n_inserted;
         out->n_inserted += o2.n_inserted;

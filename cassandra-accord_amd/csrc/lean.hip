@@ -130,39 +130,57 @@ __device__ __forceinline__ void seg_bitonic_wide(T& x0, T& x1)
         }
 }
 
+// LEAN_ADAPT: refills sized for what the wave will still write (dense arena: 304 MB in use for 272 MB of
+// config-2 regions) -- measured 0.06 ms slower per config-2 step than fixed chunks, the estimator's
+// registers spill in pass 1; off by default
+#ifndef LEAN_P2_CHUNK_FULL
+#define LEAN_P2_CHUNK_FULL 0
+#endif
 #ifndef LEAN_ADAPT
-#define LEAN_ADAPT 1
+#define LEAN_ADAPT 0
 #endif
 constexpr uint64_t LEAN_CHUNK_MIN = 2048, LEAN_CHUNK_FIRST = 8192;
 struct LeanChunk {
-    uint64_t cur = 0, end = 0, used = 0;
-    // wave-uniform bump allocation from the region arena. A refill is sized for what the wave will still
-    // write -- its bytes per item so far times the items it has left, + 1/8 -- between LEAN_CHUNK_MIN and
-    // LEAN_CHUNK, so the arena stays dense (the unused tail of a wave's last chunk is all it leaves) with
-    // a few refills per wave
-    __device__ __forceinline__ uint64_t take(BatchCtl* ctl, uint64_t nbytes, uint64_t cap, uint32_t items_done,
-                                             uint32_t items_left)
+    // wave-uniform bump allocation from the region arena, offsets in 8-byte units (regions and chunks
+    // are multiples of 8 bytes; the arena stays below 32 GB). A refill is sized for what the wave will
+    // still write -- its bytes per item so far times the items it has left, + 1/8 -- between
+    // LEAN_CHUNK_MIN and LEAN_CHUNK, so the arena stays dense (the unused tail of a wave's last chunk is
+    // all it leaves) with a few refills per wave. Items done / left come from the wave's item `it`
+    // (items it0, it0 + nw, ...) only when a chunk is taken.
+    uint32_t cur = 0, end = 0, used = 0;
+    template <int PASS>
+    __device__ __forceinline__ uint64_t take(BatchCtl* ctl, uint64_t nbytes, uint64_t cap, uint32_t it, uint32_t n_items,
+                                             uint32_t nw)
     {
-        if (nbytes > end - cur)
+        const uint32_t n8 = (uint32_t)(nbytes >> 3);
+        if (n8 > end - cur)
         {
-            uint64_t want = LEAN_ADAPT ? LEAN_CHUNK_FIRST : LEAN_CHUNK;
-            if (LEAN_ADAPT && items_done)
+            // fixed chunks: pass 1's waves write ~50 KB each (config 2), pass 2's ~13 KB
+            uint64_t want = LEAN_ADAPT ? LEAN_CHUNK_FIRST : ((PASS == 1 || LEAN_P2_CHUNK_FULL) ? LEAN_CHUNK : LEAN_CHUNK / 4);
+            if (LEAN_ADAPT)
             {
-                const uint64_t est = used / items_done * items_left;
-                want = (est + (est >> 3) + 255) & ~255ull;
+                // in float (few registers on this rarely taken path): items done / left from the stride
+                const float rnw = __builtin_amdgcn_rcpf((float)nw);
+                const float done = (float)(it - uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6))) * rnw;
+                if (done >= 1.0f)
+                {
+                    const float left = (float)(n_items - it) * rnw + 1.0f;
+                    const float est = (float)used * 9.0f * left * __builtin_amdgcn_rcpf(done);    // 8 B units, + 1/8
+                    want = ((uint64_t)est + 255) & ~255ull;
+                }
             }
-            want = want < LEAN_CHUNK_MIN ? LEAN_CHUNK_MIN : (want > LEAN_CHUNK ? LEAN_CHUNK : want);
+            if (LEAN_ADAPT) want = want < LEAN_CHUNK_MIN ? LEAN_CHUNK_MIN : (want > LEAN_CHUNK ? LEAN_CHUNK : want);
             const uint64_t sz = nbytes > want ? nbytes : want;
             unsigned long long base = 0;
             if (lane_id() == 0) base = atomicAdd(&ctl->reg_top, (unsigned long long)sz);
             base = uniform64(base);
             if (base + sz > cap && lane_id() == 0) atomicOr(&ctl->overflow, 8u);
-            cur = base;
-            end = base + sz;
+            cur = (uint32_t)(base >> 3);
+            end = (uint32_t)((base + sz) >> 3);
         }
-        const uint64_t r = cur;
-        cur += nbytes;
-        used += nbytes;
+        const uint64_t r = (uint64_t)cur << 3;
+        cur += n8;
+        used += n8;
         return r;
     }
 };
@@ -223,11 +241,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
 
     LeanChunk ralloc;
-    uint32_t cur_it = 0;         // the wave's current item (wave-uniform): sizes its region refills
-    const uint32_t it_first = uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
     // one wave-uniform region allocation for the segments' byte counts (at each segment's lane 0):
     // returns this segment's offset; `fits` whether the whole allocation is inside the arena
-    auto seg_alloc = [&](uint64_t bytes, bool& fits) -> uint64_t {
+    auto seg_alloc = [&](uint64_t bytes, bool& fits, uint32_t it) -> uint64_t {
         uint64_t total = 0, mine = 0;
 #pragma unroll
         for (uint32_t k = 0; k < RPW; ++k)
@@ -236,8 +252,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             if (k == h) mine = total;
             total += bk;
         }
-        const uint32_t done = (cur_it - it_first) / nw, left = (n_items - 1 - cur_it) / nw + 1;
-        const uint64_t base = ralloc.take(b.ctl, total, reg_cap, done, left);
+        const uint64_t base = ralloc.template take<PASS>(b.ctl, total, reg_cap, it, n_items, nw);
         fits = base + total <= reg_cap;
         return base + mine;
     };
@@ -452,7 +467,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 
     for (uint32_t it = it0; it < n_items; it += nw)
     {
-        cur_it = it;
         const uint32_t t = qc.t;
 
         // ---- current item: per key p = hl < np, newest test and emission counts
@@ -593,7 +607,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
                 const uint32_t kst0 = __shfl(kstart_l, sb | ka0, 64), kst1 = __shfl(kstart_l, sb | ka1, 64);
                 const uint64_t bytes = wact && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
                 bool fits;
-                const uint64_t ro = seg_alloc(bytes, fits);
+                const uint64_t ro = seg_alloc(bytes, fits, it);
                 put_sizes(wact, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
                 if (wact && tot && fits)
                 {
@@ -723,7 +737,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             // regions of the wave's requests from one wave-uniform allocation
             const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
             bool fits;
-            const uint64_t ro = seg_alloc(bytes, fits);
+            const uint64_t ro = seg_alloc(bytes, fits, it);
             put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
             if (act && tot && fits && !(LEAN_EXP & 4))
             {
@@ -795,7 +809,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             const uint32_t ur2 = __popcll(um2 & below) + (uq2 ? 1u : 0u) - 1u;
             const uint64_t bytes = act && totp ? (((uint64_t)nR * 8 + (uint64_t)UR * 4 + (uint64_t)(nR + UP) * 4 + 7) & ~7ull) : 0;
             bool fits;
-            const uint64_t ro = seg_alloc(bytes, fits);
+            const uint64_t ro = seg_alloc(bytes, fits, it);
             put_sizes(act, t, 1, fits ? nR : 0, fits ? UR : 0, fits ? nR + UP : 0, ro, true);
             if (act && totp && fits)
             {

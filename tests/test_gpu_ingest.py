@@ -87,7 +87,7 @@ def test_device_ingest_then_updates(oracle, seed, monkeypatch):
     st = _store(w, False, monkeypatch)
     try:
         u1, _ = G.transitions(w.cfk, rng, 80)
-        u2, _ = G.older_inserts(w.cfk, rng, 40)
+        u2 = G.older_inserts(w.cfk, rng, 40)
         u = G.concat(u1, u2)
         new, _ = U.cfk_update(w.cfk, u)
         st.cfk_update(u)
@@ -161,11 +161,13 @@ def _pruned_outside(cfk):
 
 
 def _range_domain(cfk):
+    # Routable.Domain.Range on a live CommandsForKey entry: the txn's id in every CommandsForKey that
+    # holds it (and where it is its own executeAt), so that the bits stay one id's
     e = int(np.nonzero(cfk.status == A.ST_APPLIED)[0][0])
-    same = cfk.exec.lsb[e] == cfk.txn.lsb[e] and cfk.exec.msb[e] == cfk.txn.msb[e] and cfk.exec.node[e] == cfk.txn.node[e]
-    cfk.txn.lsb[e] |= np.uint64(1)          # Routable.Domain.Range on a live CommandsForKey entry
-    if same:
-        cfk.exec.lsb[e] |= np.uint64(1)     # (its executeAt is its txnId: the same bits)
+    m, l, n = cfk.txn.msb[e], cfk.txn.lsb[e], cfk.txn.node[e]
+    for t in (cfk.txn, cfk.exec):
+        hit = (t.msb == m) & (t.lsb == l) & (t.node == n)
+        t.lsb[hit] |= np.uint64(1)
 
 
 @pytest.mark.parametrize("mut,code", [(_swap_ids, A.AD_E_ORDER), (_dup_exec, A.AD_E_DUP_EXEC),
