@@ -41,10 +41,10 @@ KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, false>", "k_encode_txn+k_probe_key
 def kernel_of_stage(i, ranges=False, rpw1=2):
     """Kernel name (as rocprofv3 reports it, namespace and arguments stripped) of pipeline stage i;
     the lean kernels are instantiated with range support when the store has range commands, and lean
-    pass 1 runs four requests per wave for batches of small requests (abi.cpp lean_rpw1)."""
+    pass 1 runs four or eight requests per wave for batches of small requests (abi.cpp lean_rpw1)."""
     k = KERNEL_OF_STAGE[i]
-    if i == 0 and rpw1 == 4:
-        k = k.replace("<2u", "<4u")
+    if i == 0 and rpw1 in (4, 8):
+        k = k.replace("<2u", "<%du" % rpw1)
     if ranges and i == 0:
         return k.replace("false, false>", "true, false>")
     if ranges and i == 3:
@@ -299,11 +299,18 @@ def bench_levels(args, rank, world, local, dev):
         pairs = int(p.item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     dom = int(np.argmax(ms))
-    pull = launches == args.steps          # one leveling launch per step: the rank-ordered dataflow (default)
-    names = (["k5 build (exec radix sort + key chains + predecessor CSR)", "k5 rank-ordered dataflow (k_level_pull)"] if pull
-             else ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"])
+    pull = launches == args.steps          # one leveling launch per step: the rank-ordered dataflow (default CSR, or AD_LEVELS_WALK)
+    walk = pull and os.environ.get("AD_LEVELS_WALK") is not None
+    if walk:
+        names = ["k5 build (exec radix sort + key chains + occurrence positions)",
+                 "k5 rank-ordered dataflow walking the key chains (k_level_walk)"]
+    elif pull:
+        names = ["k5 build (exec radix sort + key chains + predecessor CSR)", "k5 rank-ordered dataflow (k_level_pull)"]
+    else:
+        names = ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"]
     achieved = stats["bytes_stage"][dom] / (ms[dom] / 1000.0) / 1e9 if ms[dom] > 0 else 0.0
-    traffic, traffic_src = measured_traffic([("k_level_pull" if pull else "k_level_step")] if dom == 1 else ["k_radix_scatter"])
+    lk = "k_level_walk" if walk else ("k_level_pull" if pull else "k_level_step")
+    traffic, traffic_src = measured_traffic([lk] if dom == 1 else ["k_radix_scatter"])
     res = {
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
@@ -808,7 +815,14 @@ def bench_steady(args, rank, world, local, dev):
         u = CfkUpdates(np.concatenate([p_[0] for p_ in parts]), Tids.concat([p_[1] for p_ in parts]),
                        Tids.concat([p_[2] for p_ in parts]), np.concatenate([p_[3] for p_ in parts]))
         ud, ukeep = native.device_updates(u, dev)
-        batches.append((qdev, keep, ud, ukeep, len(u), q.n_probes))
+        rdev = rkeep = None
+        if args.steady_recovery:
+            # recovery of the txns this step registers (BeginRecovery on a live store: the view is
+            # built from the device state the update just left)
+            k = min(args.steady_recovery, len(q))
+            rq = q.window(0, k)
+            rdev, rkeep = native.device_queries(rq, dev)
+        batches.append((qdev, keep, ud, ukeep, len(u), q.n_probes, rdev, rkeep))
     store = native.DeviceCommandStore(device=local)
     store.load(w)
     sp = torch.cuda.current_stream(dev).cuda_stream
@@ -818,8 +832,12 @@ def bench_steady(args, rank, world, local, dev):
         b = next(it)
         _, rs = store.deps_batch_device(b[0], sp)
         _, us = store.cfk_update_device(b[2], sp)
+        rec_ms = 0.0
+        if b[6] is not None:
+            _, rc = store.recovery_scan_device(b[6], args.recovery_scan, sp)
+            rec_ms = rc["ms_device"]
         return dict(resolve_ms=rs["ms_device"], update_ms=us["ms_device"], locate_ms=us["ms_stage"][0],
-                    derive_ms=us["ms_stage"][1], inserted=us["n_keys"][0], pairs=sum(rs["n_pairs"]))
+                    derive_ms=us["ms_stage"][1], inserted=us["n_keys"][0], pairs=sum(rs["n_pairs"]), recovery_ms=rec_ms)
     elapsed, all_stats = _timed_steps(args, world, dev, step)
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     reqs = _sum_over_ranks(world, dev, R * args.steps)
@@ -833,7 +851,8 @@ def bench_steady(args, rank, world, local, dev):
                                "then inserted, the previous step's applied, + %d history transitions" % (cfk.n_entries, R, T),
                    "parallelism": "replicas x%d" % world},
         "stages_ms": {"resolve": mean("resolve_ms"), "update": mean("update_ms"), "update.locate+apply+insert":
-                      mean("locate_ms"), "update.re-derivation": mean("derive_ms")},
+                      mean("locate_ms"), "update.re-derivation": mean("derive_ms"),
+                      "recovery (live store, view rebuilt from the device state)": mean("recovery_ms")},
         "entries_after": int(cfk.n_entries + sum(x["inserted"] for x in all_stats)),
         "updates_per_step": int(np.mean([b_[4] for b_ in batches])),
         "pairs_per_step": mean("pairs"),
@@ -934,6 +953,8 @@ def main():
                     help="config-2 steady state: per step resolve R fresh PreAccepts, then register them "
                          "(CommandsForKey.update inserts) with --steady-transitions status transitions")
     ap.add_argument("--steady-transitions", type=int, default=-1, metavar="T", help="default 8R")
+    ap.add_argument("--steady-recovery", type=int, default=0, metavar="K",
+                    help="--steady: each step also runs a recovery scan (--recovery-scan) for K of the txns it registered")
     ap.add_argument("--resident", action="store_true",
                     help="--config 1: keep the store resident, each step a fresh SEQUENTIAL batch (device-side insertion)")
     ap.add_argument("--cfk-deps", type=int, default=0, metavar="D",
@@ -1116,7 +1137,8 @@ def bench_deps(args, rank, world, local, dev):
     sbytes = stage_bytes(w, stats)
     res_ms = float(sum(stage_ms[i] for i in RESOLVE_STAGES))
     achieved = sbytes[0] / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
-    lean_rpw1 = 4 if w.queries.n_probes <= 3 * max(1, len(w.queries)) else 2
+    nq = max(1, len(w.queries))
+    lean_rpw1 = 8 if 2 * w.queries.n_probes <= 3 * nq else (4 if w.queries.n_probes <= 3 * nq else 2)
     res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1) for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
     traffic, traffic_src = measured_traffic(res_kernels, "config%d" % cfg)
     xdesc = ""
@@ -1131,9 +1153,9 @@ def bench_deps(args, rank, world, local, dev):
                      int(w.params["n_hist_txns"]), n_total,
                      xdesc))
     else:
-        workload = ("config2 (weak-scaled per GPU): %d txns x 8 Zipf(0.99) keys, %d keys and a %d-entry CommandsForKey "
-                    "history per GPU, SNAPSHOT, 1 CommandStore per GPU%s" %
-                    (n_total, int(1_000_000 * s) * world, w.cfk.n_entries,
+        workload = ("config2 (weak-scaled per GPU): per GPU %d txns x 8 Zipf(0.99) keys over %d keys and a %d-entry "
+                    "CommandsForKey history (node-wide %d txns), SNAPSHOT, 1 CommandStore per GPU%s" %
+                    (int(1_000_000 * s), int(1_000_000 * s), w.cfk.n_entries, n_total,
                      xdesc) +
                     ("; request mix: %d Accepts of in-flight txns (S = executeAt, self excluded), %d PreAccepts up to %d hlc "
                      "ticks late, the rest fresh PreAccepts" % (w.params["n_accept"], w.params["n_unordered"],

@@ -1698,10 +1698,12 @@ static int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
 
 // requests per wave of lean pass 1: four for batches of small requests (at most 3 keys on average,
 // e.g. a store's share of requests spanning many stores), else two. AD_LEAN_RPW overrides.
+// requests per wave of lean pass 1 by the batch's keys per request: 8 (<= 1.5 on average: a store's
+// share of requests spanning many stores), 4 (<= 3), else 2
 static uint32_t lean_rpw1(uint64_t n, uint64_t np)
 {
-    if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 4 ? 4u : 2u;
-    return np <= 3 * n ? 4u : 2u;
+    if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 8 ? 8u : (atoi(e) == 4 ? 4u : 2u);
+    return 2 * np <= 3 * n ? 8u : (np <= 3 * n ? 4u : 2u);
 }
 
 static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false,

@@ -207,8 +207,8 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
     return v;
 }
 
-// RPW requests per wave (4: 16 lanes each, up to 16 raw emissions -- batches of small requests,
-// e.g. a store's share of requests spanning many stores; 2: 32 lanes, up to 32; 1: 64 lanes, up to 64).
+// RPW requests per wave (8: 8 lanes each, up to 8 raw emissions -- a store's share of requests that
+// span many stores, ~1 key each; 4: 16 lanes, up to 16; 2: 32 lanes, up to 32; 1: 64 lanes, up to 64).
 // RNG: the store has range commands (with a stabbing index): each request also gets its
 // rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
 // WIDE (RPW 2, no range commands: lean pass 2): requests with up to 64 raw emissions, two per lane.
@@ -694,7 +694,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             // sort (rank, key) per request; dedup -> txnIds; body = unique-rank index per key, ascending
             uint32_t k = mine ? ((r << 3) | a) : 0xFFFFFFFFu;
             // the sort must span every lane that may hold one (raw emissions: lanes [0, T))
-            const uint32_t kmax = seg_max(T);
+            // (a deferred request of the wave may hold T > LPR: never sort across segments)
+            const uint32_t kmax = min(seg_max(T), LPR);
             if (LEAN_EXP & 2) {}
             else if (kmax <= 8) seg_bitonic<8, LPR>(k);
             else if (kmax <= 16 || LPR == 16) seg_bitonic<16, LPR>(k);
@@ -764,7 +765,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         }
         else
         {
-            const uint32_t kmaxr = seg_max(TR);
+            const uint32_t kmaxr = min(seg_max(TR), LPR);
             uint64_t pk = rwant ? ((ce & 0xFFFFFFFF00000000ull) | rk) : ~0ull;
             if (kmaxr <= 8) seg_bitonic64<8, LPR>(pk);
             else if (kmaxr <= 16 || LPR == 16) seg_bitonic64<16, LPR>(pk);
@@ -864,6 +865,7 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
             if (!b.p_slot) return hipErrorInvalidValue;
             if (b.n_probes) k_lean_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b.q_keys, b.n_probes, b.p_slot);
         }
+        if (rpw1 == 8) return s.n_rent ? launch_lean<8, true, false, 1>(s, b, st) : launch_lean<8, false, false, 1>(s, b, st);
         if (rpw1 == 4) return s.n_rent ? launch_lean<4, true, false, 1>(s, b, st) : launch_lean<4, false, false, 1>(s, b, st);
         return s.n_rent ? launch_lean<2, true, false, 1>(s, b, st) : launch_lean<2, false, false, 1>(s, b, st);
     }

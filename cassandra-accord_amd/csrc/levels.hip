@@ -237,9 +237,10 @@ __global__ void k_exec_rank(LevelsIn g, const uint32_t* __restrict__ order, uint
 }
 
 // occurrences in exec-rank order: okey = key with the sign flipped, oval = rank
+// orank (non-null: the walking dataflow): oval holds the occurrence index o and orank[o] its exec rank
 __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __restrict__ order,
                                                   const uint64_t* __restrict__ occ_off, uint64_t* __restrict__ okey,
-                                                  uint32_t* __restrict__ oval, LevelsCtl* ctl)
+                                                  uint32_t* __restrict__ oval, LevelsCtl* ctl, uint32_t* __restrict__ orank)
 {
     __shared__ uint64_t red[4];
     uint64_t d = 0;
@@ -252,7 +253,13 @@ __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __
         {
             const uint64_t k = (uint64_t)g.keys[j];
             okey[o + (j - s)] = k ^ 0x8000000000000000ull;
-            oval[o + (j - s)] = (uint32_t)r;
+            if (orank)
+            {
+                oval[o + (j - s)] = (uint32_t)(o + (j - s));
+                orank[o + (j - s)] = (uint32_t)r;
+            }
+            else
+                oval[o + (j - s)] = (uint32_t)r;
             d |= k ^ ref;
         }
     }
@@ -625,6 +632,135 @@ __global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* 
     }
 }
 
+// The walking dataflow (default): k_level_pull without a predecessor CSR. Each lane walks its txn's
+// key chains itself -- per occurrence, back along the (key, rank)-sorted occurrences while a kind T
+// witnesses is undominated, exactly k_chain's walk -- and waits on each kept predecessor as the walk
+// reaches it, then on its direct deps executing earlier (Commands.java:700-775). A lane blocked on a
+// predecessor keeps its walk state (occurrence, position, dominated kinds) and resumes after a sleep.
+// pos[o]: sorted position of occurrence o (occurrences of a txn are consecutive in rank order);
+// srank[p]: exec rank of the occurrence at sorted position p.
+__global__ void k_occ_pos(uint64_t n_occ, const uint32_t* __restrict__ oidx, const uint32_t* __restrict__ orank,
+                          uint32_t* __restrict__ pos, uint32_t* __restrict__ srank)
+{
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_occ) return;
+    const uint32_t o = oidx[p];
+    pos[o] = (uint32_t)p;
+    srank[p] = orank[o];
+}
+
+struct WalkArgs {
+    uint64_t n;
+    const uint64_t* occ_off;       // [n + 1] by rank
+    const uint32_t* pos;
+    const uint64_t* okey;          // sorted occurrence keys
+    const uint32_t* srank;
+    const uint8_t* kind_r;         // kind by rank
+    const uint32_t* order;         // rank -> txn index
+    const uint32_t* rank;          // txn index -> rank
+    const uint64_t* dep_off;       // by txn index, or null
+    const uint32_t* deps;
+};
+
+__global__ __launch_bounds__(256) void k_level_walk(WalkArgs a, uint32_t* level, uint32_t* ticket, uint32_t* fail,
+                                                    unsigned long long* n_edges, LevelsCtl* ctl, uint64_t budget, uint32_t naps)
+{
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    const uint32_t lane = lane_id();
+    const uint64_t t_end = wall_clock64() + budget;
+    while (true)
+    {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(ticket, 1u);
+        c = __shfl(c, 0, 64);
+        if ((uint64_t)c * 64 >= a.n) return;
+        const uint64_t T = (uint64_t)c * 64 + lane;
+        const bool on = T < a.n;
+        uint64_t o = on ? a.occ_off[T] : 0;
+        const uint64_t oe = on ? a.occ_off[T + 1] : 0;
+        const uint32_t A = on ? kind_witnesses(a.kind_r[T]) : 0u;
+        const uint32_t t = on ? a.order[T] : 0u;
+        uint64_t dj = (on && a.dep_off) ? a.dep_off[t] : 0, de = (on && a.dep_off) ? a.dep_off[t + 1] : 0;
+        uint64_t q = 0, key = 0;
+        uint32_t D = 0, pend = NONE, mx = 0, kept = 0;
+        bool walking = false, pending = on;
+        while (true)
+        {
+            if (pending)
+            {
+                bool blocked = false;
+                if (pend != NONE)
+                {
+                    const uint32_t v = lv_poll(level + pend);
+                    if (v == LV_UNSET) blocked = true;
+                    else { mx = max(mx, v + 1u); pend = NONE; }
+                }
+                // the key chains, back from each occurrence of T
+                while (!blocked)
+                {
+                    if (!walking)
+                    {
+                        if (o >= oe) break;
+                        q = a.pos[o++];
+                        key = a.okey[q];
+                        D = 0;
+                        walking = true;
+                    }
+                    if (q == 0 || (A & ~D) == 0) { walking = false; continue; }
+                    --q;
+                    if (a.okey[q] != key) { walking = false; continue; }
+                    const uint32_t P = a.srank[q];
+                    const uint32_t kp = a.kind_r[P];
+                    const uint32_t bit = kp < 32 ? 1u << kp : 0u;
+                    if (A & bit & ~D)
+                    {
+                        ++kept;
+                        D |= kind_witnesses(kp);
+                        const uint32_t v = lv_poll(level + P);
+                        if (v == LV_UNSET) { pend = P; blocked = true; }
+                        else mx = max(mx, v + 1u);
+                    }
+                    else if (D & bit)
+                        D |= kind_witnesses(kp);
+                }
+                // direct deps executing earlier
+                while (!blocked && dj < de)
+                {
+                    const uint32_t src = a.deps[dj++];
+                    if (src >= a.n)
+                    {
+                        atomicCAS(&ctl->error, 0u, (unsigned)(-AD_E_INVAL));
+                        dj = de;
+                        break;
+                    }
+                    const uint32_t P = a.rank[src];
+                    if (P >= T) continue;
+                    ++kept;
+                    const uint32_t v = lv_poll(level + P);
+                    if (v == LV_UNSET) { pend = P; blocked = true; }
+                    else mx = max(mx, v + 1u);
+                }
+                if (!blocked)
+                {
+                    __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pending = false;
+                }
+            }
+            if (!ballot(pending)) break;
+            if (wall_clock64() > t_end)
+            {
+                if (lane == 0) atomicOr(fail, 1u);
+                return;
+            }
+            for (uint32_t z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(4);
+        }
+        uint32_t e = kept;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) e += __shfl_xor(e, d, 64);
+        if (lane == 0 && e) atomicAdd(n_edges, (unsigned long long)e);
+    }
+}
+
 __global__ void k_flow_init(const uint32_t* __restrict__ indeg, uint64_t n, unsigned long long* __restrict__ word,
                             uint2* __restrict__ seeds, uint32_t* seed_count)
 {
@@ -683,7 +819,7 @@ struct DBuf {
 
 struct LevelsWork {
     DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kind_r, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
-        level, front0, front1, cnt, ctl, word, seedA, seedB;
+        level, front0, front1, cnt, ctl, word, seedA, seedB, orank, opos, osrank;
     LevelsCtl* h_ctl = nullptr;         // pinned
     uint64_t* h_u64 = nullptr;          // pinned, 4 words
     hipEvent_t ev[3] = {};
@@ -814,21 +950,88 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
                                                     w->kcnt.as<uint32_t>(), ctl);
     LV_CHK(run_scan_arrays(w->kcnt.as<uint32_t>(), w->occ_off.as<uint64_t>(), n, 1, bsum, st));
 
+    // leveling scheme: the dataflow over a predecessor CSR (default), the dataflow walking the key chains
+    // (AD_LEVELS_WALK; 4.2 ms against 0.85 ms on config 5: every wait re-walks a chain), the frontier loop
+    // (AD_LEVELS_FRONTIER) or the dataflow waves (AD_LEVELS_DATAFLOW=<steps>)
+    const char* df = getenv("AD_LEVELS_DATAFLOW");
+    const bool pull = df == nullptr && getenv("AD_LEVELS_FRONTIER") == nullptr;
+    const bool walk = pull && getenv("AD_LEVELS_WALK") != nullptr;
+
     // ---- 2. key chains: occurrences in rank order, stably sorted by key
     uint64_t* okey = ka;
     uint32_t* oval = va;
+    if (walk) LV_ALLOC(w->orank, 4 * std::max<uint64_t>(n_occ, 1));
     if (n_occ)
     {
-        k_occ_fill<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, order, w->occ_off.as<uint64_t>(), okey, oval, ctl);
+        k_occ_fill<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, order, w->occ_off.as<uint64_t>(), okey, oval, ctl,
+                                                                             walk ? w->orank.as<uint32_t>() : nullptr);
         LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
         LV_CHK(hipStreamSynchronize(st));
         LV_CHK(radix_sort_pairs(okey, oval, kb, vb, n_occ, digits_of(w->h_ctl->diff[3]), hist, off, bsum, st, &okey,
                                 &oval));
     }
 
+    // ---- walking dataflow: sorted positions of the occurrences, then one leveling launch
+    if (walk)
+    {
+        LV_ALLOC(w->opos, 4 * std::max<uint64_t>(n_occ, 1));
+        LV_ALLOC(w->osrank, 4 * std::max<uint64_t>(n_occ, 1));
+        if (n_occ)
+            k_occ_pos<<<blocks_for(n_occ, 256), 256, 0, st>>>(n_occ, oval, w->orank.as<uint32_t>(), w->opos.as<uint32_t>(),
+                                                              w->osrank.as<uint32_t>());
+        LV_CHK(hipEventRecord(w->ev[1], st));
+        uint32_t* level = w->level.as<uint32_t>();
+        int dev = 0, cus = 256, khz = 100000;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+        int per_cu = 1, naps = 1, threads = 64;
+        if (const char* e = getenv("AD_LEVELS_PULL_PER_CU")) per_cu = std::max(1, std::min(8, atoi(e)));
+        if (const char* e = getenv("AD_LEVELS_PULL_NAPS")) naps = std::max(0, std::min(64, atoi(e)));
+        if (const char* e = getenv("AD_LEVELS_PULL_THREADS")) threads = atoi(e) == 64 ? 64 : (atoi(e) == 128 ? 128 : 256);
+        // cnt[0] ticket, cnt[1] failure flag, cnt[2] max level, cnt[4..5] edges (zeroed above)
+        LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
+        const uint64_t budget = (uint64_t)std::max(khz, 1000) * 1000ull;
+        const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, (n + threads - 1) / threads);
+        WalkArgs wa{n, w->occ_off.as<uint64_t>(), w->opos.as<uint32_t>(), okey, w->osrank.as<uint32_t>(), w->kind_r.as<uint8_t>(),
+                    order, w->rank.as<uint32_t>(), g.dep_off, g.deps};
+        k_level_walk<<<std::max(1u, grid), threads, 0, st>>>(wa, level, cnt, cnt + 1, reinterpret_cast<unsigned long long*>(cnt + 4),
+                                                             ctl, budget, (uint32_t)naps);
+        LV_CHK(hipGetLastError());
+        out->n_launch = 1;
+        k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);
+        k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
+        LV_CHK(hipEventRecord(w->ev[2], st));
+        uint32_t tail[6];
+        LV_CHK(hipMemcpyAsync(tail, cnt, sizeof(tail), hipMemcpyDeviceToHost, st));
+        LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
+        LV_CHK(hipStreamSynchronize(st));
+        if (w->h_ctl->error)
+        {
+            const int code = -(int)w->h_ctl->error;
+            *err = code == AD_E_DUP_EXEC ? "ad_levels: two txns with the same executeAt (CommandsForKey.java:1439)"
+                                         : "ad_levels: direct dep index out of range";
+            return code;
+        }
+        if (tail[1])
+        {
+            *err = "ad_levels: a wave waited more than a second for a predecessor's level";
+            return AD_E_STATE;
+        }
+        uint64_t edges = 0;
+        std::memcpy(&edges, &tail[4], 8);
+        out->n_edges = edges;
+        out->n_levels = (uint64_t)tail[2] + 1;
+        float a = 0, b = 0;
+        (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
+        (void)hipEventElapsedTime(&b, w->ev[1], w->ev[2]);
+        out->ms_build = a;
+        out->ms_frontier = b;
+        out->ms_total = a + b;
+        return AD_OK;
+    }
+
     // ---- 3. sparsified predecessors -> predecessor CSR (pull) or successor CSR + in-degrees (frontier, dataflow)
-    const char* df = getenv("AD_LEVELS_DATAFLOW");
-    const bool pull = df == nullptr && getenv("AD_LEVELS_FRONTIER") == nullptr;
     if (n_occ)
         k_chain<0><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), indeg,
                                                            pull ? nullptr : outdeg, nullptr, nullptr, nullptr);

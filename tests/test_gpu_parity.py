@@ -65,7 +65,7 @@ def test_random_larger(oracle, seed):
     _compare(w, oracle)
 
 
-@pytest.mark.parametrize("rpw", ["2", "4"])
+@pytest.mark.parametrize("rpw", ["2", "4", "8"])
 @pytest.mark.parametrize("seed", range(16))
 def test_random_small_lean_store(oracle, seed, rpw, monkeypatch):
     monkeypatch.setenv("AD_LEAN_RPW", rpw)     # lean pass 1 with two or four requests per wave
@@ -75,7 +75,7 @@ def test_random_small_lean_store(oracle, seed, rpw, monkeypatch):
     _compare(w, oracle, paths=(0,))
 
 
-@pytest.mark.parametrize("rpw", ["2", "4"])
+@pytest.mark.parametrize("rpw", ["2", "4", "8"])
 @pytest.mark.parametrize("seed", range(16))
 def test_random_small_lean_ranges(oracle, seed, rpw, monkeypatch):
     monkeypatch.setenv("AD_LEAN_RPW", rpw)
