@@ -3092,6 +3092,7 @@ static int export_sizes(ad_ctx* c, const ad_deps_result* res, const int64_t* txn
         a.k2t_off[m] = res->k2t_off[m]; a.k2t[m] = res->k2t[m];
     }
     a.txn_index = txn_index;
+    a.ids_per_req = n ? (res->stats.n_unique[0] + res->stats.n_unique[1] + res->stats.n_unique[2]) / n : 0;
     if (!res->keys[0] || !res->txns[0] || !res->k2t[0])
     {
         // a parts-only result: read the batch's regions (still valid: no batch since)
@@ -4084,6 +4085,25 @@ static int x_grow(ad_ctx* c, const uint64_t* send_units, const uint64_t* recv_un
     return AD_OK;
 }
 
+// the parts of requests [lo, hi) stay on this store (it owns them): written by the export straight to
+// their place in its receive arrays (plan entry `self` of each array), not copied there afterwards
+static void x_keep_self(ad_ctx* c, ExportArgs& a, const ad_xfer* xf, uint32_t W, uint32_t self, uint64_t lo, uint64_t hi,
+                        uint32_t fmt)
+{
+    a.self_lo = lo;
+    a.self_hi = hi;
+    for (int k = 0; k < XA; ++k)
+    {
+        const ad_xfer& x = xf[(size_t)k * W + self];
+        const int64_t ub = (int64_t)x_unit_bytes(k, fmt);
+        a.self_delta[k] = ((int64_t)x.recv_off - (int64_t)x.send_off) / ub;
+    }
+    a.rhdr = c->xr_hdr.as<int64_t>();
+    a.rkeys = c->xr_keys.as<int64_t>();
+    a.rids = c->xr_ids.as<int64_t>();
+    a.rk2t = c->xr_k2t.as<int32_t>();
+}
+
 static int x_emit(ad_ctx* c, ExportArgs& a, hipStream_t st)
 {
     return export_emit(c, a, c->xs_hdr.as<int64_t>(), c->xs_keys.as<int64_t>(), c->xs_ids.as<int64_t>(),
@@ -4196,6 +4216,7 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
             for (int a = 0; a < XA; ++a) send_units[a] += table[RW * s + 4 * d + a];
         if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
         if (int rc = x_grow(c, send_units, runits[s].data(), fmt)) return rc;
+        x_keep_self(c, ea[s], xf[s].data(), n, s, dest_first[s][s], dest_first[s][s + 1], fmt);
         if (int rc = x_emit(c, ea[s], c->stream)) return rc;
     }
     for (uint32_t s = 0; s < n; ++s)
@@ -4218,7 +4239,7 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
                 const ad_xfer& from = xf[s][(size_t)a * n + d];
                 const ad_xfer& to = xf[d][(size_t)a * n + s];
                 if (from.send_bytes != to.recv_bytes) return o->fail(AD_E_STATE, "ad_exchange_local: plans disagree");
-                if (!from.send_bytes) continue;
+                if (!from.send_bytes || s == d) continue;          // own parts: written in place by the export
                 char* dst = x_recv(o, a)->as<char>() + to.recv_off;
                 const char* src = x_send(c, a)->as<char>() + from.send_off;
                 if (c->device == o->device)
@@ -4363,21 +4384,13 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
         for (uint32_t s = 0; s < W; ++s)
             if (hs[1 + s]) return c->fail(AD_E_PEER, "ad_exchange: rank %u could not grow its exchange buffers", s);
     }
-    // 5. this rank's parts, grouped by owner, into its send buffers
+    // 5. this rank's parts, grouped by owner, into its send buffers (its own: into its receive buffers)
+    x_keep_self(c, ea, xf.data(), W, R, dest_first[R], dest_first[R + 1], fmt);
     if (int rc = x_emit(c, ea, st)) return x_abort(c, rc);
     if (hipEventRecord(c->x_ev[1], st) != hipSuccess) return x_abort(c, c->fail(AD_E_DEVICE, "hipEventRecord"));
-    // 6. grouped send/recv of the four arrays (own parts: a device copy). The group is always closed;
-    //    a failure inside it aborts the communicator.
+    // 6. grouped send/recv of the four arrays (own parts are in place already). The group is always
+    //    closed; a failure inside it aborts the communicator.
     uint64_t moved = 0;
-    hipError_t he = hipSuccess;
-    for (int a = 0; a < XA && he == hipSuccess; ++a)
-    {
-        const ad_xfer& x = xf[(size_t)a * W + R];
-        if (x.send_bytes)
-            he = hipMemcpyAsync(x_recv(c, a)->as<char>() + x.recv_off, x_send(c, a)->as<char>() + x.send_off, x.send_bytes,
-                                hipMemcpyDeviceToDevice, st);
-    }
-    if (he != hipSuccess) return x_abort(c, c->fail(AD_E_DEVICE, "exchange self copy: %s", hipGetErrorString(he)));
     nr = ncclGroupStart();
     if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclGroupStart"));
     for (int a = 0; a < XA && nr == ncclSuccess; ++a)

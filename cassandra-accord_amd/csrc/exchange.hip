@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../../include/accord_deps.h"
 #include "common.hpp"
@@ -98,6 +99,7 @@ struct XtLds {
     uint32_t kpre[XT_PARTS + 1], ipre[XT_PARTS + 1], opre[XT_PARTS + 1];
     uint32_t nk[XT_PARTS];
     uint8_t map[XT_PARTS];
+    uint8_t self[XT_PARTS];                                    // kept part: written to the receive arrays
     uint32_t cnt[XT_REQ / 64 + 1];
     uint64_t wsum[3][XT_REQ / 64 + 1];
 };
@@ -178,6 +180,9 @@ __global__ void __launch_bounds__(XT_REQ) k_export_tiles(ExportArgs a)
     const uint32_t NP = tot3[0];
     uint32_t j = ex3[0];
     const int64_t tix = live_r ? a.txn_index[r] : 0;
+    const bool kept = r >= a.self_lo && r < a.self_hi;
+    const int64_t dp = kept ? a.self_delta[0] : 0, dk = kept ? a.self_delta[1] : 0;
+    const int64_t di = kept ? a.self_delta[2] : 0, dn = kept ? a.self_delta[3] : 0;
 #pragma unroll
     for (int m = 0; m < 3; ++m)
     {
@@ -198,12 +203,13 @@ __global__ void __launch_bounds__(XT_REQ) k_export_tiles(ExportArgs a)
             L.isrc[j] = t0[m];
             L.osrc[j] = o0[m];
         }
-        L.kdst[j] = pb.KW;
-        L.idst[j] = pb.ID;
-        L.odst[j] = pb.KO;
+        L.kdst[j] = pb.KW + dk;
+        L.idst[j] = pb.ID + di;
+        L.odst[j] = pb.KO + dn;
         L.nk[j] = nk[m];
         L.map[j] = (uint8_t)m;
-        int64_t* h = a.hdr + 4 * pb.P;
+        L.self[j] = kept ? 1 : 0;
+        int64_t* h = kept ? a.rhdr + 4 * (pb.P + dp) : a.hdr + 4 * pb.P;
         h[0] = (tix << 2) | m;
         h[1] = (int64_t)nk[m];
         h[2] = (int64_t)nt[m];
@@ -252,27 +258,29 @@ __global__ void __launch_bounds__(XT_REQ) k_export_tiles(ExportArgs a)
     for (uint32_t e = t; e < KT; e += XT_REQ)
     {
         const uint32_t q = xt_owner(L.kpre, NP, e), i = e - L.kpre[q];
+        int64_t* okeys = L.self[q] ? a.rkeys : a.okeys;
         if (L.map[q] == AD_MAP_RANGE)
         {
             const uint32_t key = i >> 1;
             const int64_t rid = a.reg ? reinterpret_cast<const int64_t*>(a.reg + L.ksrc[q])[key] : a.keys[AD_MAP_RANGE][L.ksrc[q] + key];
-            a.okeys[L.kdst[q] + i] = (i & 1) ? a.rt_end[rid] : a.rt_start[rid];
+            okeys[L.kdst[q] + i] = (i & 1) ? a.rt_end[rid] : a.rt_start[rid];
         }
         else
         {
             const int m = L.map[q];
-            a.okeys[L.kdst[q] + i] = a.reg ? reinterpret_cast<const int64_t*>(a.reg + L.ksrc[q])[i] : a.keys[m][L.ksrc[q] + i];
+            okeys[L.kdst[q] + i] = a.reg ? reinterpret_cast<const int64_t*>(a.reg + L.ksrc[q])[i] : a.keys[m][L.ksrc[q] + i];
         }
     }
     for (uint32_t e = t; e < IT; e += XT_REQ)
     {
         const uint32_t q = xt_owner(L.ipre, NP, e), i = e - L.ipre[q];
         const uint32_t d = a.reg ? reinterpret_cast<const uint32_t*>(a.reg + L.isrc[q])[i] : a.txns[L.map[q]][L.isrc[q] + i];
+        int64_t* oids = L.self[q] ? a.rids : a.oids;
         if (a.rank_ids)
-            reinterpret_cast<uint32_t*>(a.oids)[L.idst[q] + i] = d;
+            reinterpret_cast<uint32_t*>(oids)[L.idst[q] + i] = d;
         else
         {
-            int64_t* o = a.oids + 3 * (L.idst[q] + i);
+            int64_t* o = oids + 3 * (L.idst[q] + i);
             o[0] = (int64_t)a.dict_msb[d];
             o[1] = (int64_t)a.dict_lsb[d];
             o[2] = (int64_t)a.dict_node[d];
@@ -281,7 +289,95 @@ __global__ void __launch_bounds__(XT_REQ) k_export_tiles(ExportArgs a)
     for (uint32_t e = t; e < OT; e += XT_REQ)
     {
         const uint32_t q = xt_owner(L.opre, NP, e), i = e - L.opre[q];
-        a.ok2t[L.odst[q] + i] = a.reg ? reinterpret_cast<const int32_t*>(a.reg + L.osrc[q])[i] : a.k2t[L.map[q]][L.osrc[q] + i];
+        (L.self[q] ? a.rk2t : a.ok2t)[L.odst[q] + i] = a.reg ? reinterpret_cast<const int32_t*>(a.reg + L.osrc[q])[i] : a.k2t[L.map[q]][L.osrc[q] + i];
+    }
+}
+
+// Export by request groups (the default): G lanes per request copy its parts' key words, ids and
+// keysToTxnIds lane-strided (a part's elements are contiguous at both ends), with no block scans, LDS
+// or owner searches -- parts are small (a store's share of a request: a few keys, tens of ids), so the
+// per-element owner search and the block-wide barriers of k_export_tiles cost more than the copy.
+// Every lane of a group reads the request's offsets (same addresses: one line per group).
+template <uint32_t G>
+__global__ void __launch_bounds__(256) k_export_groups(ExportArgs a)
+{
+    const uint64_t r = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const uint32_t sl = threadIdx.x % G;
+    if (r >= a.n) return;                                 // whole groups (G divides the block)
+    const bool kept = r >= a.self_lo && r < a.self_hi;
+    int64_t* hdr = kept ? a.rhdr + 4 * a.self_delta[0] : a.hdr;
+    int64_t* okeys = kept ? a.rkeys + a.self_delta[1] : a.okeys;
+    int64_t* oids = kept ? a.rids + (a.rank_ids ? 0 : 3 * a.self_delta[2]) : a.oids;
+    uint32_t* oids32 = reinterpret_cast<uint32_t*>(kept ? a.rids : a.oids) + (kept && a.rank_ids ? a.self_delta[2] : 0);
+    int32_t* ok2t = kept ? a.rk2t + a.self_delta[3] : a.ok2t;
+    uint64_t k0[3], t0[3], o0[3];
+    uint32_t nk[3], nt[3], no[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+    {
+        k0[m] = a.keys_off[m][r];
+        nk[m] = (uint32_t)(a.keys_off[m][r + 1] - k0[m]);
+        t0[m] = a.txn_off[m][r];
+        nt[m] = (uint32_t)(a.txn_off[m][r + 1] - t0[m]);
+        o0[m] = a.k2t_off[m][r];
+        no[m] = (uint32_t)(a.k2t_off[m][r + 1] - o0[m]);
+    }
+    uint64_t P = a.off[r], KW = 0, ID = 0, KO = 0;
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+    {
+        KW += (m == AD_MAP_RANGE ? 2 : 1) * k0[m];
+        ID += t0[m];
+        KO += o0[m];
+    }
+    const int64_t tix = a.txn_index[r];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+    {
+        if (!nk[m]) continue;
+        const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
+        if (sl < 4)
+            hdr[4 * P + sl] = sl == 0 ? ((tix << 2) | m) : (int64_t)(sl == 1 ? nk[m] : (sl == 2 ? nt[m] : no[m]));
+        const int64_t* sk;
+        const uint32_t* si;
+        const int32_t* so;
+        if (a.reg)
+        {
+            const uint8_t* base = a.reg + a.t_reg[(uint64_t)m * a.n + r];
+            sk = reinterpret_cast<const int64_t*>(base);
+            si = reinterpret_cast<const uint32_t*>(base + 8ull * nk[m]);
+            so = reinterpret_cast<const int32_t*>(base + 8ull * nk[m] + 4ull * nt[m]);
+        }
+        else
+        {
+            sk = a.keys[m] + k0[m];
+            si = a.txns[m] + t0[m];
+            so = a.k2t[m] + o0[m];
+        }
+        if (m == AD_MAP_RANGE)
+            for (uint32_t i = sl; i < 2 * nk[m]; i += G)
+            {
+                const int64_t rid = sk[i >> 1];
+                okeys[KW + i] = (i & 1) ? a.rt_end[rid] : a.rt_start[rid];
+            }
+        else
+            for (uint32_t i = sl; i < nk[m]; i += G) okeys[KW + i] = sk[i];
+        if (a.rank_ids)
+            for (uint32_t i = sl; i < nt[m]; i += G) oids32[ID + i] = si[i];
+        else
+            for (uint32_t i = sl; i < nt[m]; i += G)
+            {
+                const uint32_t d = si[i];
+                int64_t* o = oids + 3 * (ID + i);
+                o[0] = (int64_t)a.dict_msb[d];
+                o[1] = (int64_t)a.dict_lsb[d];
+                o[2] = (int64_t)a.dict_node[d];
+            }
+        for (uint32_t i = sl; i < no[m]; i += G) ok2t[KO + i] = so[i];
+        P += 1;
+        KW += w * nk[m];
+        ID += nt[m];
+        KO += no[m];
     }
 }
 
@@ -1792,7 +1888,20 @@ hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st)
 hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
 {
     if (!a.n) return hipSuccess;
-    k_export_tiles<<<(unsigned)((a.n + XT_REQ - 1) / XT_REQ), XT_REQ, 0, st>>>(a);
+    static const bool tiles = getenv("AD_EXPORT_TILES") != nullptr;
+    if (tiles)
+    {
+        k_export_tiles<<<(unsigned)((a.n + XT_REQ - 1) / XT_REQ), XT_REQ, 0, st>>>(a);
+        return hipGetLastError();
+    }
+    // lanes per request by the batch's ids per request (a.ids_per_req: from the resolve's stats)
+    static const int gsel = getenv("AD_EXPORT_G") ? atoi(getenv("AD_EXPORT_G")) : 0;
+    const uint32_t G = gsel ? (uint32_t)gsel : a.ids_per_req <= 8 ? 4u : a.ids_per_req <= 24 ? 8u : (a.ids_per_req <= 96 ? 16u : 32u);
+    const uint64_t blocks = (a.n * G + 255) / 256;
+    if (G == 4) k_export_groups<4><<<(unsigned)blocks, 256, 0, st>>>(a);
+    else if (G == 8) k_export_groups<8><<<(unsigned)blocks, 256, 0, st>>>(a);
+    else if (G == 16) k_export_groups<16><<<(unsigned)blocks, 256, 0, st>>>(a);
+    else k_export_groups<32><<<(unsigned)blocks, 256, 0, st>>>(a);
     return hipGetLastError();
 }
 

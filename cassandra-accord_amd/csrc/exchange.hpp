@@ -22,6 +22,12 @@ struct ExportArgs {
     uint32_t* sz;                                 // [n] parts (non-empty maps) per request
     uint64_t* off;                                // [n+1] their exclusive scan
     int64_t* hdr; int64_t* okeys; int64_t* oids; int32_t* ok2t;
+    // the parts this store keeps (requests [self_lo, self_hi): it owns them) go straight to its own
+    // receive arrays, at their send position + self_delta[array] units (no send-buffer copy, no move)
+    uint64_t self_lo, self_hi;
+    uint64_t ids_per_req;                         // average ids per request (lanes per request of the export)
+    int64_t self_delta[4];
+    int64_t* rhdr; int64_t* rkeys; int64_t* rids; int32_t* rk2t;
 };
 
 // Merge (K3) of received parts for requests [txn_base, txn_base + n_owned).
