@@ -3198,6 +3198,7 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
         return c->fail(AD_E_NOMEM, "merge outputs");
     MergeArgs a{};
     a.n_parts = P;
+    a.n_elems = in->n_key_words + in->n_ids + in->n_k2t;
     a.n_owned = n_owned;
     a.txn_base = txn_base;
     a.n_src = n_src;

@@ -33,6 +33,7 @@ struct ExportArgs {
 // Merge (K3) of received parts for requests [txn_base, txn_base + n_owned).
 struct MergeArgs {
     uint64_t n_parts, n_owned, txn_base;
+    uint64_t n_elems;                             // received key words + ids + keysToTxnIds (lanes per part)
     uint32_t n_src;
     const uint64_t* src_first;                    // [n_src+1] part boundaries per source
     const int64_t* hdr; const int64_t* keys; const int64_t* ids; const int32_t* k2t;
