@@ -34,8 +34,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MI
 STAGES = ["lean resolve pass 1", "deferred requests (split K0..K2)", "prepare (request records: S / self ranks)",
           "lean resolve pass 2 (2 requests/wave, 2 emissions/lane)", "offsets scan", "offsets + pack (tile sums, tile scan, scan+pack)",
           "general fused resolve (lean deferrals)"]
-KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, false>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
-                   "k_resolve_lean<2u, false, true>", "-", "k_tile_sums+k_tile_scan+k_pack_tiles", "k_resolve"]
+KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, false, 1>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
+                   "k_resolve_lean<2u, false, true, 2>", "-", "k_tile_sums+k_tile_scan+k_pack_tiles", "k_resolve"]
 
 
 def kernel_of_stage(i, ranges=False, rpw1=2):
@@ -46,9 +46,9 @@ def kernel_of_stage(i, ranges=False, rpw1=2):
     if i == 0 and rpw1 in (4, 8):
         k = k.replace("<2u", "<%du" % rpw1)
     if ranges and i == 0:
-        return k.replace("false, false>", "true, false>")
+        return k.replace("false, false, 1>", "true, false, 1>")
     if ranges and i == 3:
-        return "k_resolve_lean<1u, true, false>"        # range stores: pass 2 one request per wave
+        return "k_resolve_lean<1u, true, false, 2>"     # range stores: pass 2 one request per wave
     return k
 # K1 + K2 of every request run in these stages / kernels: the roofline's "dominant kernel"
 RESOLVE_STAGES = [0, 3, 6]

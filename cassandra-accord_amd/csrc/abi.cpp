@@ -2427,7 +2427,9 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
     {
         const uint64_t lo = n * j / slices, hi = n * (j + 1) / slices, nc = hi - lo;
         const uint64_t k0 = n ? q->key_off[lo] : 0, k1 = n ? q->key_off[hi] : 0;
-        if (j >= 2) HIPCHK(c, hipStreamWaitEvent(st, c->ev_copied[j & 1], 0));   // this bank's last copy-out
+        // this bank's last copy-out must be complete on the host side too: the resolve below may grow
+        // (free and reallocate) the bank's buffers, which a stream-side wait would not protect
+        if (j >= 2) HIPCHK(c, hipEventSynchronize(c->ev_copied[j & 1]));
         ko.resize(nc + 1);
         for (uint64_t i = 0; i <= nc; ++i) ko[i] = n ? q->key_off[lo + i] - k0 : 0;
         ad_query_soa d{};
