@@ -31,7 +31,7 @@ from accord_deps import exchange, native, synth  # noqa: E402
 
 METRIC = "deps resolved: txn-key pairs/sec + HBM GB/s %peak at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-STAGES = ["lean resolve pass 1", "deferred requests (split K0..K2)", "prepare (request records: S / self ranks)",
+STAGES = ["lean resolve pass 1", "deferred requests (split K0..K2)", "prepare (request records: S / self ranks; probe KeyLines for the lean passes)",
           "lean resolve pass 2 (2 requests/wave, 2 emissions/lane)", "offsets scan", "offsets + pack (tile sums, tile scan, scan+pack)",
           "general fused resolve (lean deferrals)"]
 KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, false, 1>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
@@ -43,6 +43,8 @@ def kernel_of_stage(i, ranges=False, rpw1=2):
     the lean kernels are instantiated with range support when the store has range commands, and lean
     pass 1 runs four or eight requests per wave for batches of small requests (abi.cpp lean_rpw1)."""
     k = KERNEL_OF_STAGE[i]
+    if i == 2:
+        return "k_prepare<false>" if ranges else "k_prepare<true>"      # <true>: with the probes' KeyLines
     if i == 0 and rpw1 in (4, 8):
         k = k.replace("<2u", "<%du" % rpw1)
     if ranges and i == 0:
@@ -51,7 +53,8 @@ def kernel_of_stage(i, ranges=False, rpw1=2):
         return "k_resolve_lean<1u, true, false, 2>"     # range stores: pass 2 one request per wave
     return k
 # K1 + K2 of every request run in these stages / kernels: the roofline's "dominant kernel"
-RESOLVE_STAGES = [0, 3, 6]
+# (k_prepare included since it also resolves every probe's KeyLine for the lean passes)
+RESOLVE_STAGES = [0, 2, 3, 6]
 
 
 # device of the small timing / count reductions: the GPU under RCCL, the host under gloo

@@ -1741,6 +1741,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     {
         if (!ens<uint32_t>(c->p_slot, std::max<uint64_t>(np, 1))) return c->fail(AD_E_NOMEM, "probe slots");
         b.p_slot = c->p_slot.as<uint32_t>();
+        b.slots_by_prepare = getenv("AD_SLOTS_KERNEL") == nullptr;     // measurement switch: the separate launch
     }
     if (const char* e = getenv("AD_K2_BIG")) b.k2_big = (uint32_t)strtoul(e, nullptr, 10);   // tests: force k_build_big
     b.q_rec = c->q_rec.as<uint4>();

@@ -1951,9 +1951,12 @@ hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
         k_export_tiles<<<(unsigned)((a.n + XT_REQ - 1) / XT_REQ), XT_REQ, 0, st>>>(a);
         return hipGetLastError();
     }
-    // lanes per request by the batch's ids per request (a.ids_per_req: from the resolve's stats)
+    // lanes per request by the batch's ids per request (a.ids_per_req: from the resolve's stats). Measured
+    // (scripts/export_ab.sh): 4 lanes beat 8 both at ~5 ids per request (config-3 W = 8 stores: 0.95 vs
+    // 1.42 ms for the node's eight exports; block tiles 1.11) and at ~9 (config-3 N = 1: 0.245 vs 0.29 ms;
+    // tiles 0.38)
     const int gsel = getenv("AD_EXPORT_G") ? atoi(getenv("AD_EXPORT_G")) : 0;
-    const uint32_t G = (gsel == 4 || gsel == 8 || gsel == 16 || gsel == 32) ? (uint32_t)gsel : a.ids_per_req <= 8 ? 4u : a.ids_per_req <= 24 ? 8u : (a.ids_per_req <= 96 ? 16u : 32u);
+    const uint32_t G = (gsel == 4 || gsel == 8 || gsel == 16 || gsel == 32) ? (uint32_t)gsel : a.ids_per_req <= 32 ? 4u : a.ids_per_req <= 128 ? 8u : (a.ids_per_req <= 512 ? 16u : 32u);
     const uint64_t blocks = (a.n * G + 255) / 256;
     if (G == 4) k_export_groups<4><<<(unsigned)blocks, 256, 0, st>>>(a);
     else if (G == 8) k_export_groups<8><<<(unsigned)blocks, 256, 0, st>>>(a);
@@ -2072,7 +2075,8 @@ hipError_t run_rmerge_copy(const MergeArgs& a, const uint64_t* bases, hipStream_
         k_rmerge_copy<<<(unsigned)((a.n_parts + RC_PARTS - 1) / RC_PARTS), RC_PARTS, 0, st>>>(a, bases);
         return hipGetLastError();
     }
-    // lanes per part by the received elements per part
+    // lanes per part by the received elements per part (opt-in: the block tiles measured faster, 0.123 vs
+    // 0.155 ms per owner at W = 8 and 0.206 vs 0.23 ms at N = 1)
     const int gsel = getenv("AD_RMERGE_G") ? atoi(getenv("AD_RMERGE_G")) : 0;
     const uint64_t per = a.n_elems / a.n_parts;
     const uint32_t G = (gsel == 4 || gsel == 8 || gsel == 16) ? (uint32_t)gsel : per <= 16 ? 4u : per <= 48 ? 8u : 16u;

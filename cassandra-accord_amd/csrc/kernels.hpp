@@ -39,6 +39,7 @@ struct BatchBufs {
     const uint64_t* q_key_off;
     const int64_t* q_keys;
     uint32_t* p_slot;                // lean passes without range commands: per probe its KeyLine (LS_NONE: outside the slice)
+    uint32_t slots_by_prepare;       // p_slot filled by k_prepare (one launch for records and slots)
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
     uint32_t* p_txn; uint4* p_rec;

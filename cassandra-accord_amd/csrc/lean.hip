@@ -860,7 +860,7 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     if (!b.n_txns) return hipSuccess;
     if (pass == 1)
     {
-        if (!s.n_rent && LEAN_SLOTS)
+        if (!s.n_rent && LEAN_SLOTS && !b.slots_by_prepare)
         {
             if (!b.p_slot) return hipErrorInvalidValue;
             if (b.n_probes) k_lean_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b.q_keys, b.n_probes, b.p_slot);

@@ -912,9 +912,22 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
 // Keeping the dependent key -> slot probing here leaves the per-request kernels one load shorter;
 // one thread per probe (the first n_txns threads also write the request records).
 
+// SLOTS: the same launch also gives every probe its KeyLine for the lean passes (one thread per
+// probe: the slice test, then the perfect hash; 0xFFFFFFFF outside the slices) -- k_lean_slots' work
+// without a launch of its own
+template <bool SLOTS>
 __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (SLOTS && t < b.n_probes)
+    {
+        const int64_t key = b.q_keys[t];
+        bool in = s.n_slices == 0;
+        for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+        uint32_t r = 0xFFFFFFFFu;
+        if (in) r = (uint32_t)kl_index(key_hash2(key), s.kl_disp[kl_bucket(key_hash(key), s.kl_buckets)], s.kl_lines);
+        b.p_slot[t] = r;
+    }
     if (t >= b.n_txns) return;
     // request t's record
     const uint64_t k0 = b.q_key_off[t], k1 = b.q_key_off[t + 1];
@@ -937,7 +950,13 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
-    if (b.n_txns) k_prepare<<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
+    if (b.p_slot && b.slots_by_prepare)
+    {
+        const uint64_t m = std::max<uint64_t>(b.n_txns, b.n_probes);
+        if (m) k_prepare<true><<<(unsigned)((m + 255) / 256), 256, 0, st>>>(s, b);
+    }
+    else if (b.n_txns)
+        k_prepare<false><<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
     return hipGetLastError();
 }
 
