@@ -43,7 +43,13 @@ struct DevBuf {
     ~DevBuf() { release(); }
     void release()
     {
-        if (p) (void)hipFree(p);
+        // the ctx streams are non-blocking: nothing may still read or write the buffer when it is freed
+        // (growth happens mid-pipeline; a free that raced a kernel would fault it)
+        if (p)
+        {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -2168,7 +2174,8 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
         if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
         auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
             if (!b.ensure(std::max<size_t>(bytes, 8))) return c->fail(AD_E_NOMEM, "hipMalloc %zu (snapshot columns)", bytes);
-            if (bytes) HIPCHK(c, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+            // ordered on the ctx stream (non-blocking: a null-stream copy would not wait for its kernels)
+            if (bytes) HIPCHK(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
             return 0;
         };
         int rc;
@@ -2179,6 +2186,7 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
             (rc = up(c->d_status, in->status, ne)) ||
             (in->pruned_before && (rc = up(c->d_in_pruned, in->pruned_before, 8 * nk))))
             return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));     // the caller's arrays are free to go on return
         K.txn.clear();
         K.exec.clear();
         c->raw_dev = true;
@@ -3433,7 +3441,12 @@ static bool grow_keep(DevBuf& b, size_t keep, size_t need)
     void* p = nullptr;
     const size_t cap = std::max<size_t>(need + need / 2, 64);
     if (hipMalloc(&p, cap) != hipSuccess) return false;
-    if (keep && hipMemcpy(p, b.p, keep, hipMemcpyDeviceToDevice) != hipSuccess) { (void)hipFree(p); return false; }
+    // the kernels that wrote the kept bytes ran on a non-blocking stream: complete them before the copy
+    if (keep && (hipDeviceSynchronize() != hipSuccess || hipMemcpy(p, b.p, keep, hipMemcpyDeviceToDevice) != hipSuccess))
+    {
+        (void)hipFree(p);
+        return false;
+    }
     b.release();
     b.p = p;
     b.cap = cap;
@@ -3531,7 +3544,7 @@ static int cfk_ballot_init(void* vc, uint64_t ne, Bal** bal)
 {
     ad_ctx* c = (ad_ctx*)vc;
     if (!c->d_ballot.ensure(sizeof(Bal) * ne + sizeof(Bal) * (ne / 4))) return AD_E_NOMEM;
-    if (hipMemset(c->d_ballot.p, 0, sizeof(Bal) * ne) != hipSuccess) return AD_E_DEVICE;
+    if (hipMemset(c->d_ballot.p, 0, sizeof(Bal) * ne) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return AD_E_DEVICE;
     *bal = c->d_ballot.as<Bal>();
     return 0;
 }

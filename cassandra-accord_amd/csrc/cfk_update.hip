@@ -1367,18 +1367,18 @@ unsigned blocks(uint64_t n, unsigned t = 256) { return (unsigned)std::max<uint64
 struct DBuf {
     void* p = nullptr;
     size_t cap = 0;
-    ~DBuf() { if (p) (void)hipFree(p); }
+    ~DBuf() { if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); } }   // non-blocking streams: nothing in flight may use it
     // grows with slack (insertions raise the entry count every batch: no reallocation, and no
     // re-zeroing of `word`, per batch); zero: the whole new allocation is zeroed
     bool ensure(size_t b, bool zero = false)
     {
         if (p && b <= cap) return true;
-        if (p) (void)hipFree(p);
+        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
         p = nullptr;
         cap = 0;
         b = std::max<size_t>(b + b / 4, 64);
         if (hipMalloc(&p, b) != hipSuccess) return false;
-        if (zero && hipMemset(p, 0, b) != hipSuccess) return false;
+        if (zero && (hipMemset(p, 0, b) != hipSuccess || hipDeviceSynchronize() != hipSuccess)) return false;
         cap = b;
         return true;
     }

@@ -40,11 +40,11 @@ struct IngRec { uint64_t* hi; uint64_t* lo; int32_t* node; uint64_t* lsb; };
 struct IngDBuf {
     void* p = nullptr;
     size_t cap = 0;
-    ~IngDBuf() { if (p) (void)hipFree(p); }
+    ~IngDBuf() { if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); } }   // non-blocking streams: nothing in flight may use it
     bool ensure(size_t b)
     {
         if (p && b <= cap) return true;
-        if (p) (void)hipFree(p);
+        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
         p = nullptr;
         cap = 0;
         b = std::max<size_t>(b, 64);

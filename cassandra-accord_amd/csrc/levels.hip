@@ -801,12 +801,12 @@ struct DBuf {
     size_t cap = 0;
     ~DBuf()
     {
-        if (p) (void)hipFree(p);
+        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
     }
     bool ensure(size_t bytes)
     {
         if (p && bytes <= cap) return true;
-        if (p) (void)hipFree(p);
+        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
         p = nullptr;
         cap = 0;
         const size_t b = std::max<size_t>(bytes, 64);
