@@ -1956,9 +1956,10 @@ hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
     // 1.42 ms for the node's eight exports; block tiles 1.11) and at ~9 (config-3 N = 1: 0.245 vs 0.29 ms;
     // tiles 0.38)
     const int gsel = getenv("AD_EXPORT_G") ? atoi(getenv("AD_EXPORT_G")) : 0;
-    const uint32_t G = (gsel == 4 || gsel == 8 || gsel == 16 || gsel == 32) ? (uint32_t)gsel : a.ids_per_req <= 32 ? 4u : a.ids_per_req <= 128 ? 8u : (a.ids_per_req <= 512 ? 16u : 32u);
+    const uint32_t G = (gsel == 2 || gsel == 4 || gsel == 8 || gsel == 16 || gsel == 32) ? (uint32_t)gsel : a.ids_per_req <= 32 ? 4u : a.ids_per_req <= 128 ? 8u : (a.ids_per_req <= 512 ? 16u : 32u);
     const uint64_t blocks = (a.n * G + 255) / 256;
-    if (G == 4) k_export_groups<4><<<(unsigned)blocks, 256, 0, st>>>(a);
+    if (G == 2) k_export_groups<2><<<(unsigned)blocks, 256, 0, st>>>(a);
+    else if (G == 4) k_export_groups<4><<<(unsigned)blocks, 256, 0, st>>>(a);
     else if (G == 8) k_export_groups<8><<<(unsigned)blocks, 256, 0, st>>>(a);
     else if (G == 16) k_export_groups<16><<<(unsigned)blocks, 256, 0, st>>>(a);
     else k_export_groups<32><<<(unsigned)blocks, 256, 0, st>>>(a);
