@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "../../include/accord_deps.h"
@@ -336,8 +337,8 @@ __global__ void __launch_bounds__(256) k_export_groups(ExportArgs a)
     {
         if (!nk[m]) continue;
         const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
-        if (sl < 4)
-            hdr[4 * P + sl] = sl == 0 ? ((tix << 2) | m) : (int64_t)(sl == 1 ? nk[m] : (sl == 2 ? nt[m] : no[m]));
+        for (uint32_t h = sl; h < 4; h += G)
+            hdr[4 * P + h] = h == 0 ? ((tix << 2) | m) : (int64_t)(h == 1 ? nk[m] : (h == 2 ? nt[m] : no[m]));
         const int64_t* sk;
         const uint32_t* si;
         const int32_t* so;
@@ -1958,6 +1959,8 @@ hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
     const int gsel = getenv("AD_EXPORT_G") ? atoi(getenv("AD_EXPORT_G")) : 0;
     const uint32_t G = (gsel == 2 || gsel == 4 || gsel == 8 || gsel == 16 || gsel == 32) ? (uint32_t)gsel : a.ids_per_req <= 32 ? 4u : a.ids_per_req <= 128 ? 8u : (a.ids_per_req <= 512 ? 16u : 32u);
     const uint64_t blocks = (a.n * G + 255) / 256;
+    if (getenv("AD_EXPORT_TRACE")) fprintf(stderr, "export: %llu requests, %llu ids per request, %u lanes each\n",
+                                           (unsigned long long)a.n, (unsigned long long)a.ids_per_req, G);
     if (G == 2) k_export_groups<2><<<(unsigned)blocks, 256, 0, st>>>(a);
     else if (G == 4) k_export_groups<4><<<(unsigned)blocks, 256, 0, st>>>(a);
     else if (G == 8) k_export_groups<8><<<(unsigned)blocks, 256, 0, st>>>(a);

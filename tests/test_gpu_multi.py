@@ -118,7 +118,7 @@ def test_config2_scaled_sharded(rank_ids):
     _check(w, synth.shard_bounds(4), 4, rank_ids)
 
 
-@pytest.mark.parametrize("width", ["tiles", "4", "8", "16", "32"])
+@pytest.mark.parametrize("width", ["tiles", "2", "4", "8", "16", "32"])
 def test_export_and_copy_lane_widths(width, monkeypatch):
     # the export and the K3 copy at every lane width per request / part (and the block-tiled kernels),
     # whatever the batch's average part size would pick; big groups included
