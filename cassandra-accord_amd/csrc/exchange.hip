@@ -1953,11 +1953,11 @@ hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
         return hipGetLastError();
     }
     // lanes per request by the batch's ids per request (a.ids_per_req: from the resolve's stats). Measured
-    // (scripts/export_ab.sh): 4 lanes beat 8 both at ~5 ids per request (config-3 W = 8 stores: 0.95 vs
-    // 1.42 ms for the node's eight exports; block tiles 1.11) and at ~9 (config-3 N = 1: 0.245 vs 0.29 ms;
-    // tiles 0.38)
+    // (scripts/export_ab.sh, AD_EXPORT_TRACE): at 2 ids per request (config-3 W = 8 stores) 2 lanes take
+    // 0.77 ms for the node's eight exports against 0.95 with 4, 1.42 with 8 and 1.11 for the block tiles;
+    // at 9 (config-3 N = 1) 4 lanes take 0.245 ms against 0.355 with 2, 0.29 with 8 and 0.38 for tiles
     const int gsel = getenv("AD_EXPORT_G") ? atoi(getenv("AD_EXPORT_G")) : 0;
-    const uint32_t G = (gsel == 2 || gsel == 4 || gsel == 8 || gsel == 16 || gsel == 32) ? (uint32_t)gsel : a.ids_per_req <= 32 ? 4u : a.ids_per_req <= 128 ? 8u : (a.ids_per_req <= 512 ? 16u : 32u);
+    const uint32_t G = (gsel == 2 || gsel == 4 || gsel == 8 || gsel == 16 || gsel == 32) ? (uint32_t)gsel : a.ids_per_req <= 4 ? 2u : a.ids_per_req <= 32 ? 4u : a.ids_per_req <= 128 ? 8u : (a.ids_per_req <= 512 ? 16u : 32u);
     const uint64_t blocks = (a.n * G + 255) / 256;
     if (getenv("AD_EXPORT_TRACE")) fprintf(stderr, "export: %llu requests, %llu ids per request, %u lanes each\n",
                                            (unsigned long long)a.n, (unsigned long long)a.ids_per_req, G);
