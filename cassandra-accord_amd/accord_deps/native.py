@@ -432,17 +432,36 @@ class DeviceCommandStore:
         """Caller-owned host output arrays of ad_deps_batch_into (numpy), pinned with ad_host_register
         when `pin`; grown (and re-pinned) when a batch needs more."""
 
+        PAGE = 4096
+
+        @staticmethod
+        def _pages(shape, dtype):
+            # zeroed array on whole pages of its own: a registration covers exactly its pages, so pinning
+            # (page-granular) never shares a page with another array or with the Python heap, and
+            # unregistering one array cannot unpin memory something else still transfers through
+            dtype = np.dtype(dtype)
+            nbytes = int(np.prod(shape)) * dtype.itemsize
+            span = -(-max(nbytes, 1) // DeviceCommandStore.HostOut.PAGE) * DeviceCommandStore.HostOut.PAGE
+            raw = np.zeros(span + DeviceCommandStore.HostOut.PAGE, np.uint8)
+            at = (-raw.ctypes.data) % DeviceCommandStore.HostOut.PAGE
+            a = raw[at:at + nbytes].view(dtype).reshape(shape)
+            return a, span
+
         def __init__(self, store, n, cap, pin=True):
             self.store, self.pin, self.n = store, pin, n
-            self.off = np.zeros((9, n + 1), np.uint64)
             self.cap = [int(x) for x in cap]
-            self.keys = [np.zeros(max(1, self.cap[3 * m]), np.int64) for m in range(3)]
-            self.txns = [np.zeros(max(1, self.cap[3 * m + 1]), np.uint32) for m in range(3)]
-            self.k2t = [np.zeros(max(1, self.cap[3 * m + 2]), np.int32) for m in range(3)]
+            P = DeviceCommandStore.HostOut._pages
+            self.off, s_off = P((9, n + 1), np.uint64)
+            ks = [P(max(1, self.cap[3 * m]), np.int64) for m in range(3)]
+            ts = [P(max(1, self.cap[3 * m + 1]), np.uint32) for m in range(3)]
+            os_ = [P(max(1, self.cap[3 * m + 2]), np.int32) for m in range(3)]
+            self.keys = [a for a, _ in ks]
+            self.txns = [a for a, _ in ts]
+            self.k2t = [a for a, _ in os_]
             self.pinned = []
             if pin:
-                for a in [self.off] + self.keys + self.txns + self.k2t:
-                    store._check(lib().ad_host_register(store.h, A.ptr(a), a.nbytes))
+                for a, span in [(self.off, s_off)] + ks + ts + os_:
+                    store._check(lib().ad_host_register(store.h, A.ptr(a), span))
                     self.pinned.append(a)
 
         def release(self):

@@ -263,7 +263,10 @@ int  ad_deps_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t flags, ad_deps_r
 void ad_result_free(ad_deps_result* r);
 
 /* Pin caller-owned host memory for DMA (hipHostRegister): a Panama Arena segment a Java host reuses
- * batch after batch for queries and results. Unregister before freeing it. */
+ * batch after batch for queries and results. Unregister before freeing it. Pinning is page-granular:
+ * register whole pages the caller owns (page-aligned p, bytes a multiple of the page size, e.g. an Arena
+ * allocation with 4096-byte alignment); a sub-page range shares its pages with unrelated memory, which
+ * its unregistration would unpin under any transfer still using them. */
 int ad_host_register(ad_ctx* ctx, void* p, uint64_t bytes);
 int ad_host_unregister(ad_ctx* ctx, void* p);
 
