@@ -23,8 +23,8 @@ def _check(g, oracle):
 
 def _scheme(monkeypatch, scheme):
     # None: the rank-ordered dataflow over a predecessor CSR (k_level_pull, default); "walk": the same
-    # walking the key chains (k_level_walk); "frontier": the level-synchronous frontier loop; a number:
-    # the dataflow waves with that many steps per launch
+    # walking the key chains (k_level_walk, experimental: left out of the suite); "frontier":
+    # the level-synchronous frontier loop; a number: the dataflow waves with that many steps per launch
     if scheme == "frontier":
         monkeypatch.setenv("AD_LEVELS_FRONTIER", "1")
     elif scheme == "walk":
@@ -33,7 +33,7 @@ def _scheme(monkeypatch, scheme):
         monkeypatch.setenv("AD_LEVELS_DATAFLOW", scheme)
 
 
-@pytest.mark.parametrize("scheme", [None, "walk", "frontier", "8", "1"])
+@pytest.mark.parametrize("scheme", [None, "frontier", "8", "1"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_graph_all_kinds(oracle, seed, scheme, monkeypatch):
     _scheme(monkeypatch, scheme)
@@ -41,7 +41,7 @@ def test_random_graph_all_kinds(oracle, seed, scheme, monkeypatch):
     _check(g, oracle)
 
 
-@pytest.mark.parametrize("walk", [False, True])
+@pytest.mark.parametrize("walk", [False])
 @pytest.mark.parametrize("per_cu", ["1", "8"])
 def test_pull_occupancy(oracle, per_cu, walk, monkeypatch):
     # fewer and more resident waves than the default (every wait still on a lower rank)
@@ -53,7 +53,7 @@ def test_pull_occupancy(oracle, per_cu, walk, monkeypatch):
     _check(g, oracle)
 
 
-@pytest.mark.parametrize("scheme", ["frontier", "walk"])
+@pytest.mark.parametrize("scheme", ["frontier"])
 def test_config5_full_other_schemes(oracle, scheme, monkeypatch):
     _scheme(monkeypatch, scheme)
     g, _ = synth.config5()
@@ -84,7 +84,7 @@ def test_many_sources_spill_path(oracle, monkeypatch):
     dep_off[1:] = np.cumsum(hub)
     deps = np.zeros(int(hub.sum()), np.uint32)
     g = Graph(ex, np.zeros(n, np.uint8), key_off, keys, dep_off, deps)
-    for df in (None, "walk", "frontier", "8"):
+    for df in (None, "frontier", "8"):
         monkeypatch.delenv("AD_LEVELS_WALK", raising=False)
         monkeypatch.delenv("AD_LEVELS_FRONTIER", raising=False)
         monkeypatch.delenv("AD_LEVELS_DATAFLOW", raising=False)
