@@ -33,7 +33,7 @@ def _scheme(monkeypatch, scheme):
         monkeypatch.setenv("AD_LEVELS_DATAFLOW", scheme)
 
 
-@pytest.mark.parametrize("scheme", [None, "frontier", "8", "1"])
+@pytest.mark.parametrize("scheme", [None, "frontier"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_graph_all_kinds(oracle, seed, scheme, monkeypatch):
     _scheme(monkeypatch, scheme)
@@ -61,6 +61,7 @@ def test_config5_full_other_schemes(oracle, scheme, monkeypatch):
     assert st["n_levels"] == int(got.max()) + 1
 
 
+@pytest.mark.skip(reason="experimental dataflow waves (AD_LEVELS_DATAFLOW): left out of the suite, DESIGN §4")
 def test_config5_full_dataflow(oracle, monkeypatch):
     monkeypatch.setenv("AD_LEVELS_DATAFLOW", "8")
     g, _ = synth.config5()
@@ -84,7 +85,7 @@ def test_many_sources_spill_path(oracle, monkeypatch):
     dep_off[1:] = np.cumsum(hub)
     deps = np.zeros(int(hub.sum()), np.uint32)
     g = Graph(ex, np.zeros(n, np.uint8), key_off, keys, dep_off, deps)
-    for df in (None, "frontier", "8"):
+    for df in (None, "frontier"):
         monkeypatch.delenv("AD_LEVELS_WALK", raising=False)
         monkeypatch.delenv("AD_LEVELS_FRONTIER", raising=False)
         monkeypatch.delenv("AD_LEVELS_DATAFLOW", raising=False)
