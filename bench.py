@@ -1141,7 +1141,7 @@ def bench_deps(args, rank, world, local, dev):
     res_ms = float(sum(stage_ms[i] for i in RESOLVE_STAGES))
     achieved = sbytes[0] / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
     nq = max(1, len(w.queries))
-    lean_rpw1 = 8 if 2 * w.queries.n_probes <= 3 * nq else (4 if w.queries.n_probes <= 3 * nq else 2)
+    lean_rpw1 = 4 if w.queries.n_probes <= 3 * nq else 2
     res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1) for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
     traffic, traffic_src = measured_traffic(res_kernels, "config%d" % cfg)
     xdesc = ""

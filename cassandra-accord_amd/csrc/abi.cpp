@@ -1709,7 +1709,8 @@ static int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
 static uint32_t lean_rpw1(uint64_t n, uint64_t np)
 {
     if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 8 ? 8u : (atoi(e) == 4 ? 4u : 2u);
-    return 2 * np <= 3 * n ? 8u : (np <= 3 * n ? 4u : 2u);
+    // 8 requests per wave (AD_LEAN_RPW=8) stays opt-in while the late-round-3 device faults are open
+    return np <= 3 * n ? 4u : 2u;
 }
 
 static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false,
