@@ -834,8 +834,8 @@ static int build_snapshot_device(ad_ctx* c)
     // dictionary and the entries
     const uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
     int kl_rc = 0;
-    std::thread kl_thread([&]() { kl_rc = kl_place_all(c, K.keys, kl_nb, false); });
-    struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } kl_join{kl_thread};
+    // (placed on the calling thread after the dictionary and entries: a host thread beside the device
+    // build is kept off while the late-round-3 intermittent faults are open)
     phase("columns");
     if ((rc = ingest_dictionary(c->ing, in, o, st, &n_dict, &bad, &e)))
         return c->fail(rc, "%s", e.c_str());
@@ -862,7 +862,7 @@ static int build_snapshot_device(ad_ctx* c)
     // line (k_key_slots), stabbing cell and slot of the open-addressing key hash
     uint64_t hcap = 16;
     while (hcap < 2 * nk) hcap <<= 1;
-    kl_thread.join();
+    kl_rc = kl_place_all(c, K.keys, kl_nb, false);
     if (kl_rc) return c->fail(kl_rc, "key perfect hash did not converge");
     phase("key line perfect hash (wait)");
     if ((rc = upload(c, c->d_kl_disp, c->kl_disp_h)) || (rc = upload(c, c->d_slices_s, c->slice_s)) ||
