@@ -302,17 +302,13 @@ def bench_levels(args, rank, world, local, dev):
         pairs = int(p.item())
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     dom = int(np.argmax(ms))
-    pull = launches == args.steps          # one leveling launch per step: the rank-ordered dataflow (default CSR, or AD_LEVELS_WALK)
-    walk = pull and os.environ.get("AD_LEVELS_WALK") is not None
-    if walk:
-        names = ["k5 build (exec radix sort + key chains + occurrence positions)",
-                 "k5 rank-ordered dataflow walking the key chains (k_level_walk)"]
-    elif pull:
+    pull = launches == args.steps          # one leveling launch per step: the rank-ordered dataflow (default)
+    if pull:
         names = ["k5 build (exec radix sort + key chains + predecessor CSR)", "k5 rank-ordered dataflow (k_level_pull)"]
     else:
         names = ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"]
     achieved = stats["bytes_stage"][dom] / (ms[dom] / 1000.0) / 1e9 if ms[dom] > 0 else 0.0
-    lk = "k_level_walk" if walk else ("k_level_pull" if pull else "k_level_step")
+    lk = "k_level_pull" if pull else "k_level_step"
     traffic, traffic_src = measured_traffic([lk] if dom == 1 else ["k_radix_scatter"])
     res = {
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,

@@ -9,6 +9,7 @@ AD_E_* code (the Java wrapper maps these to IllegalStateException).
 There is no CPU fallback: if the library or a GPU is missing, this module raises.
 """
 import ctypes as C
+import weakref
 import os
 
 import numpy as np
@@ -27,7 +28,8 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_cfk_ballots_load", "ad_cfk_ballots",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange", "ad_exchange_plan",
            "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing",
-           "ad_cfk_load_pruned", "ad_host_register", "ad_host_unregister", "ad_deps_batch_into")
+           "ad_cfk_load_pruned", "ad_host_register", "ad_host_unregister", "ad_deps_batch_into",
+           "ad_debug_guard_check")
 
 
 class AccordDepsError(RuntimeError):
@@ -116,6 +118,7 @@ def lib():
                                      C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]
         L.ad_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.ad_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
+        L.ad_debug_guard_check.argtypes = [C.c_char_p, C.c_uint64]
         L.ad_deps_batch_into.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.POINTER(A.AdDepsResult),
                                          C.c_void_p, C.c_void_p, C.c_uint32]
         L.ad_cfk_load_pruned.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)] + [C.POINTER(C.c_void_p)] * 5
@@ -459,15 +462,33 @@ class DeviceCommandStore:
             self.txns = [a for a, _ in ts]
             self.k2t = [a for a, _ in os_]
             self.pinned = []
+            # unpinned when released, or at the latest when this object is collected (a test or caller
+            # that raises before release()): numpy must never free pages HIP still has registered. The
+            # finalizer holds the arrays (not self), so they outlive the registration; it needs no ctx.
+            self._fin = weakref.finalize(self, DeviceCommandStore.HostOut._unpin, self.pinned)
             if pin:
-                for a, span in [(self.off, s_off)] + ks + ts + os_:
-                    store._check(lib().ad_host_register(store.h, A.ptr(a), span))
-                    self.pinned.append(a)
+                try:
+                    for a, span in [(self.off, s_off)] + ks + ts + os_:
+                        store._check(lib().ad_host_register(store.h, A.ptr(a), span))
+                        self.pinned.append(a)
+                except BaseException:
+                    self.release()
+                    raise
+
+        @staticmethod
+        def _unpin(pinned):
+            bad = 0
+            for a in pinned:
+                if lib().ad_host_unregister(None, A.ptr(a)) != 0:
+                    bad += 1
+            pinned.clear()
+            if bad:
+                raise AccordDepsError(A.AD_E_DEVICE, "ad_host_unregister failed for %d pinned output arrays" % bad)
 
         def release(self):
-            for a in self.pinned:
-                lib().ad_host_unregister(self.store.h, A.ptr(a))
-            self.pinned = []
+            # the store's copy stream is drained by every ad_deps_batch_into return; the registration is
+            # process-wide, so the ctx-free unregister is right even after store.close()
+            self._fin()
 
         def soa(self):
             r = A.AdDepsResult()
@@ -493,15 +514,19 @@ class DeviceCommandStore:
             out = DeviceCommandStore.HostOut(self, n, [np_, 2 * np_, 4 * np_] * 3, pin)
         need = np.zeros(9, np.uint64)
         soa = queries.soa()
-        while True:
-            r = out.soa()
-            cap = np.asarray(out.cap, np.uint64)
-            rc = lib().ad_deps_batch_into(self.h, C.byref(soa), flags, C.byref(r), A.ptr(cap), A.ptr(need), slices)
-            if rc != A.AD_E_SPACE:
-                break
+        try:
+            while True:
+                r = out.soa()
+                cap = np.asarray(out.cap, np.uint64)
+                rc = lib().ad_deps_batch_into(self.h, C.byref(soa), flags, C.byref(r), A.ptr(cap), A.ptr(need), slices)
+                if rc != A.AD_E_SPACE:
+                    break
+                out.release()
+                out = DeviceCommandStore.HostOut(self, n, [int(x) + int(x) // 4 + 16 for x in need], pin)
+            self._check(rc)
+        except BaseException:
             out.release()
-            out = DeviceCommandStore.HostOut(self, n, [int(x) + int(x) // 4 + 16 for x in need], pin)
-        self._check(rc)
+            raise
         stats = stats_dict(r.stats)
         if not materialise:
             return None, stats, out
@@ -841,3 +866,10 @@ def device_graph(graph, dev):
     s.dep_off = keep["do"].data_ptr() if "do" in keep else None
     s.deps = keep["d"].data_ptr() if "d" in keep else None
     return s, keep
+
+
+def guard_check():
+    """AD_GUARD debug mode: (number of damaged device guard bands, report); (0, "") when the mode is off."""
+    buf = C.create_string_buffer(1 << 16)
+    bad = lib().ad_debug_guard_check(buf, len(buf))
+    return bad, buf.value.decode(errors="replace")

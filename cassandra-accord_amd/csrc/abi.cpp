@@ -29,6 +29,7 @@
 #include "cfk_update.hpp"
 #include "ingest.hpp"
 #include "check.hpp"
+#include "devmem.hpp"
 
 using namespace adx;
 
@@ -37,34 +38,6 @@ namespace {
 // ---------------------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------------------
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~DevBuf() { release(); }
-    void release()
-    {
-        // the ctx streams are non-blocking: nothing may still read or write the buffer when it is freed
-        // (growth happens mid-pipeline; a free that raced a kernel would fault it)
-        if (p)
-        {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(p);
-        }
-        p = nullptr;
-        cap = 0;
-    }
-    bool ensure(size_t bytes)
-    {
-        if (bytes <= cap && p) return true;
-        release();
-        size_t b = bytes ? bytes : 16;
-        if (hipMalloc(&p, b) != hipSuccess) { p = nullptr; return false; }
-        cap = b;
-        return true;
-    }
-    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
-};
-
 struct Tid {
     uint64_t msb, lsb;
     int32_t node;
@@ -350,6 +323,14 @@ struct ad_ctx {
     }
 };
 
+// A synchronous copy ordered after the work queued on the call's streams: the ctx streams are
+// non-blocking, so a plain null-stream hipMemcpy would not wait for their kernels (nor they for it).
+static hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind)
+{
+    dev_quiesce();
+    return hipMemcpy(dst, src, bytes, kind);
+}
+
 #define HIPCHK(ctx, expr)                                                                         \
     do {                                                                                          \
         hipError_t _e = (expr);                                                                   \
@@ -474,7 +455,7 @@ static int kl_place_all(ad_ctx* c, const std::vector<int64_t>& keys, uint64_t nb
             c->kl_used.swap(used);
             break;
         }
-        if (attempt == 4) return c->fail(AD_E_DEVICE, "key perfect hash did not converge");
+        if (attempt == 4) return AD_E_DEVICE;           // the caller reports it (this may run on a helper thread)
         m += m / 2;              // more room, try again
     }
     c->kline_slots = m;
@@ -832,10 +813,16 @@ static int build_snapshot_device(ad_ctx* c)
     std::string e;
     // the KeyLine perfect hash is placed on a host thread (keys only) while the device builds the
     // dictionary and the entries
+    // The thread reads only the loaded keys (const) and writes only the ctx's KeyLine host state
+    // (kl_used, kline_slots, kl_nb_h, kl_disp_h, kl_members, kl_keys_all), which nothing else touches
+    // before the join below; it makes no HIP call and reports failure through kl_rc (not c->err).
     const uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
     int kl_rc = 0;
-    // (placed on the calling thread after the dictionary and entries: a host thread beside the device
-    // build is kept off while the late-round-3 intermittent faults are open)
+    std::thread kl_thread([&]() { kl_rc = kl_place_all(c, K.keys, kl_nb, false); });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() { if (t.joinable()) t.join(); }
+    } kl_join{kl_thread};
     phase("columns");
     if ((rc = ingest_dictionary(c->ing, in, o, st, &n_dict, &bad, &e)))
         return c->fail(rc, "%s", e.c_str());
@@ -851,7 +838,7 @@ static int build_snapshot_device(ad_ctx* c)
     phase("entries");
     // the extras' ranks (range commands, watermarks) for the host's range part
     std::vector<uint32_t> xr(nx), cmd_rank(ncmd), wm_rank(nrb, 0);
-    if (nx) HIPCHK(c, hipMemcpy(xr.data(), c->d_ing_rank.as<uint32_t>() + ne + o.n_diff, 4 * nx, hipMemcpyDeviceToHost));
+    if (nx) HIPCHK(c, copy_sync(xr.data(), c->d_ing_rank.as<uint32_t>() + ne + o.n_diff, 4 * nx, hipMemcpyDeviceToHost));
     for (uint64_t i = 0; i < ncmd; ++i) cmd_rank[i] = xr[i];
     for (uint64_t j = 0; j < wm_at.size(); ++j) wm_rank[wm_at[j]] = xr[ncmd + j];
     c->h_cmd_rank = cmd_rank;
@@ -862,7 +849,7 @@ static int build_snapshot_device(ad_ctx* c)
     // line (k_key_slots), stabbing cell and slot of the open-addressing key hash
     uint64_t hcap = 16;
     while (hcap < 2 * nk) hcap <<= 1;
-    kl_rc = kl_place_all(c, K.keys, kl_nb, false);
+    kl_thread.join();
     if (kl_rc) return c->fail(kl_rc, "key perfect hash did not converge");
     phase("key line perfect hash (wait)");
     if ((rc = upload(c, c->d_kl_disp, c->kl_disp_h)) || (rc = upload(c, c->d_slices_s, c->slice_s)) ||
@@ -894,9 +881,9 @@ static int build_snapshot_device(ad_ctx* c)
     NormTid last{0, 0, 0};
     if (n_dict)
     {
-        HIPCHK(c, hipMemcpy(&last.hi, c->d_dict_hi.as<uint64_t>() + n_dict - 1, 8, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(&last.lo, c->d_dict_lo.as<uint64_t>() + n_dict - 1, 8, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(&last.node, c->d_dict_node.as<int32_t>() + n_dict - 1, 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(&last.hi, c->d_dict_hi.as<uint64_t>() + n_dict - 1, 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(&last.lo, c->d_dict_lo.as<uint64_t>() + n_dict - 1, 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(&last.node, c->d_dict_node.as<int32_t>() + n_dict - 1, 4, hipMemcpyDeviceToHost));
     }
     if ((rc = set_views(c, n_dict, n_samp, last, nk, ne, hcap, rp, nrb))) return rc;
     if (n_samp) HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
@@ -912,7 +899,7 @@ static int build_snapshot_device(ad_ctx* c)
         if (rc == AD_E_DUP_EXEC)
         {
             uint32_t k = 0;
-            if (bad_e < ne) (void)hipMemcpy(&k, c->d_ekey.as<uint32_t>() + bad_e, 4, hipMemcpyDeviceToHost);
+            if (bad_e < ne) (void)copy_sync(&k, c->d_ekey.as<uint32_t>() + bad_e, 4, hipMemcpyDeviceToHost);
             return c->fail(rc, "CommandsForKey of key %lld violates unique committed executeAt (CommandsForKey.java:1439)",
                            k < nk ? (long long)K.keys[k] : -1ll);
         }
@@ -1285,7 +1272,7 @@ static int build_snapshot_host(ad_ctx* c)
     // perfect hash of the keys onto KeyLines (hash and displace, common.hpp): buckets of ~4 keys,
     // the biggest placed first, each with the first displacement that puts all its keys on free lines
     uint64_t kl_nb = std::max<uint64_t>(1, nk / 4);
-    if (int rc = kl_place_all(c, K.keys, kl_nb, false)) return rc;
+    if (int rc = kl_place_all(c, K.keys, kl_nb, false)) return c->fail(rc, "key perfect hash did not converge");
     for (uint64_t k = 0; k < nk; ++k)
         kslot[k] = (uint32_t)kl_index(key_hash2(K.keys[k]), c->kl_disp_h[kl_bucket(key_hash(K.keys[k]), kl_nb)], c->kline_slots);
     const std::vector<uint32_t>& kl_disp = c->kl_disp_h;
@@ -1397,8 +1384,8 @@ static int pull_missing(ad_ctx* c)
     const uint64_t ne = c->dmiss_lists, nm = c->dmiss_ids;
     K.miss_off.resize(ne + 1);
     std::vector<uint32_t> r(nm);
-    HIPCHK(c, hipMemcpy(K.miss_off.data(), c->d_moff.p, 8 * (ne + 1), hipMemcpyDeviceToHost));
-    if (nm) HIPCHK(c, hipMemcpy(r.data(), c->d_mids.p, 4 * nm, hipMemcpyDeviceToHost));
+    HIPCHK(c, copy_sync(K.miss_off.data(), c->d_moff.p, 8 * (ne + 1), hipMemcpyDeviceToHost));
+    if (nm) HIPCHK(c, copy_sync(r.data(), c->d_mids.p, 4 * nm, hipMemcpyDeviceToHost));
     K.miss.resize(nm);
     for (uint64_t j = 0; j < nm; ++j)
     {
@@ -1438,12 +1425,12 @@ static int host_inputs(ad_ctx* c)
     std::vector<int32_t> tn(ne), en(ne);
     if (ne)
     {
-        HIPCHK(c, hipMemcpy(tm.data(), c->d_in_tm.p, 8 * ne, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(tl.data(), c->d_in_tl.p, 8 * ne, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(tn.data(), c->d_in_tn.p, 4 * ne, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(em.data(), c->d_in_em.p, 8 * ne, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(el.data(), c->d_in_el.p, 8 * ne, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(en.data(), c->d_in_en.p, 4 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(tm.data(), c->d_in_tm.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(tl.data(), c->d_in_tl.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(tn.data(), c->d_in_tn.p, 4 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(em.data(), c->d_in_em.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(el.data(), c->d_in_el.p, 8 * ne, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(en.data(), c->d_in_en.p, 4 * ne, hipMemcpyDeviceToHost));
     }
     K.txn.resize(ne);
     K.exec.resize(ne);
@@ -1474,7 +1461,7 @@ static int sync_host_entries(ad_ctx* c)
     {
         const uint64_t ne = c->ds.n_ent;
         std::vector<Bal> bl(ne);
-        if (ne) HIPCHK(c, hipMemcpy(bl.data(), c->d_ballot.p, sizeof(Bal) * ne, hipMemcpyDeviceToHost));
+        if (ne) HIPCHK(c, copy_sync(bl.data(), c->d_ballot.p, sizeof(Bal) * ne, hipMemcpyDeviceToHost));
         K.ballot.resize(ne);
         for (uint64_t e = 0; e < ne; ++e) K.ballot[e] = Tid{bl[e].msb, bl[e].lsb, bl[e].node};
     }
@@ -2029,29 +2016,59 @@ static T* stage_q(ad_ctx* c, DevBuf& b, const T* src, uint64_t n, int* rc)
     return b.as<T>();
 }
 
+// one array of a device result into a malloc'd host array (n elements, n <= bound), checked
 template <class T>
-static T* d2h(const T* src, uint64_t n)
+static int d2h(ad_ctx* c, T** out, const T* src, uint64_t n, uint64_t bound, const char* what, int m)
 {
+    if (n > bound)
+        return c->fail(AD_E_DEVICE, "result %s of map %d: %llu elements, beyond the batch total %llu", what, m,
+                       (unsigned long long)n, (unsigned long long)bound);
     T* p = (T*)malloc(sizeof(T) * std::max<uint64_t>(n, 1));
-    if (p && n) (void)hipMemcpy(p, src, sizeof(T) * n, hipMemcpyDeviceToHost);
-    return p;
+    if (!p) return c->fail(AD_E_NOMEM, "result %s of map %d: %llu elements", what, m, (unsigned long long)n);
+    *out = p;
+    if (n)
+    {
+        const hipError_t e = copy_sync(p, src, sizeof(T) * n, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return c->fail(AD_E_DEVICE, "result %s of map %d: %s", what, m, hipGetErrorString(e));
+    }
+    return 0;
 }
 
+// A device result (packed arrays) into a library-owned host result. Every copy is checked and every
+// array length is bounded by the batch totals the pipeline reported (ad_stats); the offsets must start
+// at 0 and end exactly at those totals, else AD_E_DEVICE names the map and the array (nothing is
+// sized from a value the checks have not accepted).
 static int result_to_host(ad_ctx* c, uint64_t n, const ad_deps_result& dev, ad_deps_result** out)
 {
     ad_deps_result* r = (ad_deps_result*)calloc(1, sizeof(ad_deps_result));
     if (!r) return c->fail(AD_E_NOMEM, "result");
     r->n_txns = n;
     r->stats = dev.stats;
-    for (int m = 0; m < 3; ++m)
+    auto run = [&]() -> int {
+        for (int m = 0; m < 3; ++m)
+        {
+            const uint64_t tot[3] = {dev.stats.n_keys[m], dev.stats.n_unique[m], dev.stats.n_pairs[m] + dev.stats.n_keys[m]};
+            const char* names[3] = {"keys", "txnIds", "keysToTxnIds"};
+            uint64_t** offs[3] = {&r->keys_off[m], &r->txn_off[m], &r->k2t_off[m]};
+            const uint64_t* src_off[3] = {dev.keys_off[m], dev.txn_off[m], dev.k2t_off[m]};
+            for (int a = 0; a < 3; ++a)
+            {
+                if (int rc = d2h(c, offs[a], src_off[a], n + 1, n + 1, names[a], m)) return rc;
+                const uint64_t* o = *offs[a];
+                if (o[0] != 0 || o[n] != tot[a])
+                    return c->fail(AD_E_DEVICE, "result offsets of %s, map %d: [0] = %llu, [n] = %llu, batch total %llu", names[a],
+                                   m, (unsigned long long)o[0], (unsigned long long)o[n], (unsigned long long)tot[a]);
+            }
+            if (int rc = d2h(c, &r->keys[m], dev.keys[m], tot[0], tot[0], names[0], m)) return rc;
+            if (int rc = d2h(c, &r->txns[m], dev.txns[m], tot[1], tot[1], names[1], m)) return rc;
+            if (int rc = d2h(c, &r->k2t[m], dev.k2t[m], tot[2], tot[2], names[2], m)) return rc;
+        }
+        return 0;
+    };
+    if (int rc = run())
     {
-        r->keys_off[m] = d2h(dev.keys_off[m], n + 1);
-        r->txn_off[m] = d2h(dev.txn_off[m], n + 1);
-        r->k2t_off[m] = d2h(dev.k2t_off[m], n + 1);
-        const uint64_t nk = r->keys_off[m][n], nt = r->txn_off[m][n], no = r->k2t_off[m][n];
-        r->keys[m] = d2h(dev.keys[m], nk);
-        r->txns[m] = d2h(dev.txns[m], nt);
-        r->k2t[m] = d2h(dev.k2t[m], no);
+        ad_result_free(r);
+        return rc;
     }
     *out = r;
     return AD_OK;
@@ -2173,6 +2190,7 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
     if (getenv("AD_INGEST_HOST") == nullptr)
     {
         if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+        StreamScope scope_(c->stream, c->cstream);
         auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
             if (!b.ensure(std::max<size_t>(bytes, 8))) return c->fail(AD_E_NOMEM, "hipMalloc %zu (snapshot columns)", bytes);
             // ordered on the ctx stream (non-blocking: a null-stream copy would not wait for its kernels)
@@ -2268,6 +2286,7 @@ int ad_prepare(ad_ctx* c)
     if (!c) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     return c->dirty ? build_snapshot(c) : AD_OK;
 }
 
@@ -2331,6 +2350,7 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
     if (!c || !q || !out) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     int rc = check_query_host(c, q);
     if (rc) return rc;
     if (flags & AD_SEQUENTIAL)
@@ -2372,14 +2392,36 @@ int ad_host_register(ad_ctx* c, void* p, uint64_t bytes)
 {
     if (!c || !p || !bytes) return AD_E_INVAL;
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     HIPCHK(c, hipHostRegister(p, bytes, hipHostRegisterDefault));
     return AD_OK;
 }
 
+int ad_debug_guard_check(char* buf, uint64_t n)
+{
+    std::string rep;
+    const int bad = dev_guard_check(&rep);
+    if (buf && n)
+    {
+        const size_t k = std::min<size_t>(rep.size(), n - 1);
+        memcpy(buf, rep.data(), k);
+        buf[k] = 0;
+    }
+    return bad;
+}
+
 int ad_host_unregister(ad_ctx* c, void* p)
 {
-    if (!c || !p) return AD_E_INVAL;
+    if (!p) return AD_E_INVAL;
+    if (!c)
+    {
+        // no ctx (it may be gone already): a registration is process-wide, nothing of a ctx is needed
+        return hipHostUnregister(p) == hipSuccess ? AD_OK : AD_E_DEVICE;
+    }
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
+    // nothing of this ctx may still be copying into the pages
+    if (c->cstream) HIPCHK(c, hipStreamSynchronize(c->cstream));
     HIPCHK(c, hipHostUnregister(p));
     return AD_OK;
 }
@@ -2390,6 +2432,7 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
     if (!c || !q || !out || !cap || !need) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     const uint64_t n = q->n_txns;
     for (int m = 0; m < 3; ++m)
         if (!out->keys_off[m] || !out->txn_off[m] || !out->k2t_off[m] || (cap[3 * m] && !out->keys[m]) ||
@@ -2411,6 +2454,13 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
     }
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     if (!c->cstream) HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    scope_.add(c->cstream);
+    // every return -- errors inside the slice loop included -- waits for the copy-outs already queued
+    // into the caller's arrays: the caller may unregister and free them as soon as this returns
+    struct CopyDrain {
+        hipStream_t s;
+        ~CopyDrain() { (void)hipStreamSynchronize(s); }
+    } drain_{c->cstream};
     if (!c->ev_ready) HIPCHK(c, hipEventCreateWithFlags(&c->ev_ready, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_copied)
         if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2530,9 +2580,11 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (flags & AD_SEQUENTIAL) return c->fail(AD_E_INVAL, "device-resident batches are SNAPSHOT only");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     int rc;
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    scope_.add(st);
     // AD_REGIONS and AD_PARTS_ONLY: no packed copy (the regions are the result)
     return run_pipeline(c, q, st, out, (flags & (AD_PARTS_ONLY | AD_REGIONS)) != 0, (flags & AD_N_KEYS) != 0);
 }
@@ -2885,11 +2937,13 @@ int ad_recovery_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t scan, vo
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (scan > AD_RECOVER_EXECUTES_AFTER_STABLE_NO_WITNESS) return c->fail(AD_E_INVAL, "unknown recovery scan %u", scan);
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     int rc;
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     RecoveryView v{};
     if ((rc = build_recovery_view(c, &v))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    scope_.add(st);
     return run_pipeline(c, q, st, out, false, false, (int)scan, &v);
 }
 
@@ -2898,6 +2952,7 @@ int ad_recovery_batch(ad_ctx* c, const ad_query_soa* q, uint32_t scan, ad_deps_r
     if (!c || !q || !out) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     int rc = check_query_host(c, q);
     if (rc) return rc;
     const uint64_t n = q->n_txns;
@@ -2957,11 +3012,11 @@ static int load_range_map(ad_ctx* c, const ad_range_map_soa* m, ad_ctx::RangeMap
     if (!B.starts.ensure(8 * (n + 1)) || !B.msb.ensure(8 * n) || !B.lsb.ensure(8 * n) || !B.node.ensure(4 * n) ||
         (m->present && !B.present.ensure(n)))
         return c->fail(AD_E_NOMEM, "%s", what);
-    HIPCHK(c, hipMemcpy(B.starts.p, m->starts, 8 * (n + 1), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(B.msb.p, m->msb, 8 * n, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(B.lsb.p, m->lsb, 8 * n, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(B.node.p, m->node, 4 * n, hipMemcpyHostToDevice));
-    if (m->present) HIPCHK(c, hipMemcpy(B.present.p, m->present, n, hipMemcpyHostToDevice));
+    HIPCHK(c, copy_sync(B.starts.p, m->starts, 8 * (n + 1), hipMemcpyHostToDevice));
+    HIPCHK(c, copy_sync(B.msb.p, m->msb, 8 * n, hipMemcpyHostToDevice));
+    HIPCHK(c, copy_sync(B.lsb.p, m->lsb, 8 * n, hipMemcpyHostToDevice));
+    HIPCHK(c, copy_sync(B.node.p, m->node, 4 * n, hipMemcpyHostToDevice));
+    if (m->present) HIPCHK(c, copy_sync(B.present.p, m->present, n, hipMemcpyHostToDevice));
     B.n = n;
     B.inclusive_ends = m->inclusive_ends ? 1u : 0u;
     B.has_present = m->present != nullptr;
@@ -2988,6 +3043,7 @@ int ad_preaccept_maps_load(ad_ctx* c, const ad_range_map_soa* max_conflicts, con
 {
     if (!c) return AD_E_INVAL;
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     ++c->pa_gen;
     int rc = load_range_map(c, max_conflicts, c->pa_mc, "ad_preaccept_maps_load: maxConflicts");
     return rc ? rc : load_range_map(c, reject_before, c->pa_rb, "ad_preaccept_maps_load: rejectBefore");
@@ -3001,7 +3057,9 @@ int ad_preaccept_device(ad_ctx* c, const ad_query_soa* q, uint32_t permit_fast_p
                       !out_flags))
         return c->fail(AD_E_INVAL, "ad_preaccept_device: NULL array");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    scope_.add(st);
     PreacceptArgs a{};
     a.n = q->n_txns;
     a.txn_msb = q->txn_msb; a.txn_lsb = q->txn_lsb; a.txn_node = q->txn_node;
@@ -3047,6 +3105,7 @@ int ad_set_global_dict(ad_ctx* c, uint64_t n, const uint64_t* msb, const uint64_
     if (n >= (1ull << 31)) return c->fail(AD_E_CAPACITY, "ad_set_global_dict: more than 2^31 ids");
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     for (uint64_t i = 1; i < n; ++i)
         if (norm_cmp(norm_tid(msb[i - 1], lsb[i - 1], node[i - 1]), norm_tid(msb[i], lsb[i], node[i])) >= 0)
             return c->fail(AD_E_INVAL, "ad_set_global_dict: ids not ascending and unique at %llu", (unsigned long long)i);
@@ -3091,6 +3150,7 @@ static int export_sizes(ad_ctx* c, const ad_deps_result* res, const int64_t* txn
         return c->fail(AD_E_STATE, "export: rank-format parts need a global dictionary covering this store's "
                                    "ids (ad_set_global_dict after the last snapshot load or dictionary append)");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (!ens<uint32_t>(c->x_sz, std::max<uint64_t>(n, 1)) || !ens<uint64_t>(c->x_off, n + 1) ||
         !ens<uint64_t>(c->x_bsum, (n + 1023) / 1024 + 16) || !ens<uint64_t>(c->x_df, n_dest + 1) ||
         !ens<uint64_t>(c->x_cnt, 4 * (n_dest + 1)))
@@ -3144,6 +3204,7 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
 {
     if (!c || !res || !out || !dest_first || !dest_counts || n_dest == 0) return AD_E_INVAL;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamScope scope_(st, c->stream, c->cstream);
     ExportArgs a{};
     if (int rc = export_sizes(c, res, txn_index, n_dest, dest_first, out->id_format, st, &a)) return rc;
     std::vector<uint64_t> cnt(4 * (n_dest + 1));
@@ -3177,7 +3238,9 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     for (uint32_t s = 0; s < n_src; ++s) first[s + 1] = (tot += src_parts[s]);
     if (tot != in->n_parts) return c->fail(AD_E_INVAL, "ad_parts_merge: src_parts do not sum to n_parts");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    scope_.add(st);
     const uint64_t P = in->n_parts, G = 3 * n_owned;
     const bool rank_ids = in->id_format == AD_IDS_RANK;
     if (in->id_format != AD_IDS_TRIPLET && !rank_ids) return c->fail(AD_E_INVAL, "ad_parts_merge: unknown id_format");
@@ -3344,7 +3407,8 @@ int ad_copy_to_host(ad_ctx* c, void* dst, const void* src, uint64_t bytes)
     if (!c || (!dst && bytes) || (!src && bytes)) return AD_E_INVAL;
     if (!bytes) return AD_OK;
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
-    HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    StreamScope scope_(c->stream, c->cstream);
+    HIPCHK(c, copy_sync(dst, src, bytes, hipMemcpyDeviceToHost));
     return AD_OK;
 }
 
@@ -3380,6 +3444,8 @@ int ad_levels_device(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, void
     if (g->n_txns && (!g->exec_msb || !g->exec_lsb || !g->exec_node || !g->kind || !g->key_off || !level_out))
         return c->fail(AD_E_INVAL, "ad_levels_device: null array");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
+    scope_.add((hipStream_t)stream);
     LevelsIn in{g->n_txns, g->exec_msb, g->exec_lsb, g->exec_node, g->kind, g->key_off, g->keys, g->dep_off, g->deps};
     return levels_run(c, in, level_out, stream ? (hipStream_t)stream : c->stream, stats);
 }
@@ -3392,6 +3458,7 @@ int ad_levels(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, ad_stats* s
         return c->fail(AD_E_INVAL, "ad_levels: null array");
     if (n && g->key_off[0] != 0) return c->fail(AD_E_INVAL, "ad_levels: key_off must start at 0");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (n == 0)
     {
         if (stats) std::memset(stats, 0, sizeof(*stats));
@@ -3439,13 +3506,15 @@ static int cfk_need_bufs(void* vc, uint64_t n_cand, uint64_t n_cwr, uint64_t n_w
 static bool grow_keep(DevBuf& b, size_t keep, size_t need)
 {
     if (b.p && need <= b.cap) return true;
-    void* p = nullptr;
     const size_t cap = std::max<size_t>(need + need / 2, 64);
-    if (hipMalloc(&p, cap) != hipSuccess) return false;
-    // the kernels that wrote the kept bytes ran on a non-blocking stream: complete them before the copy
-    if (keep && (hipDeviceSynchronize() != hipSuccess || hipMemcpy(p, b.p, keep, hipMemcpyDeviceToDevice) != hipSuccess))
+    void* p = dev_alloc(cap);
+    if (!p) return false;
+    // the kept bytes were written on the call's stream: the copy is ordered after them there
+    const hipStream_t st = dev_scope_stream();
+    if (keep && (hipMemcpyAsync(p, b.p, keep, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                 (st ? hipStreamSynchronize(st) : hipDeviceSynchronize()) != hipSuccess))
     {
-        (void)hipFree(p);
+        dev_free(p);
         return false;
     }
     b.release();
@@ -3545,7 +3614,7 @@ static int cfk_ballot_init(void* vc, uint64_t ne, Bal** bal)
 {
     ad_ctx* c = (ad_ctx*)vc;
     if (!c->d_ballot.ensure(sizeof(Bal) * ne + sizeof(Bal) * (ne / 4))) return AD_E_NOMEM;
-    if (hipMemset(c->d_ballot.p, 0, sizeof(Bal) * ne) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return AD_E_DEVICE;
+    if (dev_zero_sync(c->d_ballot.p, sizeof(Bal) * ne) != hipSuccess) return AD_E_DEVICE;
     *bal = c->d_ballot.as<Bal>();
     return 0;
 }
@@ -3595,8 +3664,8 @@ static int cfk_after_new_keys(ad_ctx* c, const CfkUpdOut& o, hipStream_t st)
     {
         // the whole table again, half full (every key of the store, from the device)
         std::vector<int64_t> all(nk);
-        HIPCHK(c, hipMemcpy(all.data(), c->d_keys.p, 8 * nk, hipMemcpyDeviceToHost));
-        if (int rc = kl_place_all(c, all, std::max<uint64_t>(1, nk / 4), true)) return rc;
+        HIPCHK(c, copy_sync(all.data(), c->d_keys.p, 8 * nk, hipMemcpyDeviceToHost));
+        if (int rc = kl_place_all(c, all, std::max<uint64_t>(1, nk / 4), true)) return c->fail(rc, "key perfect hash did not converge");
     }
     if (int rc = upload(c, c->d_kl_disp, c->kl_disp_h)) return rc;
     if (!c->d_kslot.ensure(4 * nk + 4 * (nk / 8))) return c->fail(AD_E_NOMEM, "key slots");
@@ -3737,6 +3806,7 @@ static int dmiss_enable(ad_ctx* c, hipStream_t st)
 
 static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats)
 {
+    StreamScope scope_(st, c->stream, c->cstream);
     if (c->dirty)
         if (int rc = build_snapshot(c)) return rc;
     // missing() on the device while batches bring their deps; a batch without deps hands the lists
@@ -3782,11 +3852,11 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
     {
         const uint64_t m = o.n_load_pruned;
         c->lp_upd.resize(m); c->lp_keys.resize(m); c->lp_msb.resize(m); c->lp_lsb.resize(m); c->lp_node.resize(m);
-        HIPCHK(c, hipMemcpy(c->lp_upd.data(), o.lp_update, 8 * m, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(c->lp_keys.data(), o.lp_keys, 8 * m, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(c->lp_msb.data(), o.lp_msb, 8 * m, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(c->lp_lsb.data(), o.lp_lsb, 8 * m, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(c->lp_node.data(), o.lp_node, 4 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->lp_upd.data(), o.lp_update, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->lp_keys.data(), o.lp_keys, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->lp_msb.data(), o.lp_msb, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->lp_lsb.data(), o.lp_lsb, 8 * m, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->lp_node.data(), o.lp_node, 4 * m, hipMemcpyDeviceToHost));
     }
     if (o.n_new_keys)
     {
@@ -3814,9 +3884,9 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         c->dict_msb.resize(nd0 + add);
         c->dict_lsb.resize(nd0 + add);
         c->dict_node.resize(nd0 + add);
-        HIPCHK(c, hipMemcpy(c->dict_msb.data() + nd0, c->d_dict_hi.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(c->dict_lsb.data() + nd0, c->d_dict_lsb_raw.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(c->dict_node.data() + nd0, c->d_dict_node.as<int32_t>() + nd0, 4 * add, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->dict_msb.data() + nd0, c->d_dict_hi.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->dict_lsb.data() + nd0, c->d_dict_lsb_raw.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
+        HIPCHK(c, copy_sync(c->dict_node.data() + nd0, c->d_dict_node.as<int32_t>() + nd0, 4 * add, hipMemcpyDeviceToHost));
         drop_global_dict(c);         // global ranks of the multi-store exchange no longer cover the dictionary
         // the sampled index over the grown dictionary (a stale one is still correct, only slower)
         const uint64_t ns = dict_samples(c->ds.n_dict);
@@ -3872,6 +3942,7 @@ static int check_update_soa(ad_ctx* c, const ad_cfk_update_soa* u)
         return c->fail(AD_E_INVAL, "update batch ballots: ballot_msb, ballot_lsb and ballot_node must be all set or all NULL");
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     return 0;
 }
 
@@ -3919,6 +3990,7 @@ int ad_cfk_entries(ad_ctx* c, uint64_t* n_entries, const uint8_t** status, const
     if (!c || !n_entries || !status || !exec_msb || !exec_lsb || !exec_node) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (int rc = sync_host(c)) return rc;
     auto& K = c->cfk;
     const uint64_t ne = K.status.size();
@@ -3957,6 +4029,7 @@ int ad_cfk_ballots_load(ad_ctx* c, uint64_t n_entries, const uint64_t* msb, cons
     if (!c || (n_entries && (!msb || !lsb || !node))) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (int rc = sync_host(c)) return rc;
     auto& K = c->cfk;
     if (n_entries != K.status.size()) return c->fail(AD_E_INVAL, "%llu ballots for %zu entries", (unsigned long long)n_entries, K.status.size());
@@ -3980,6 +4053,7 @@ int ad_cfk_ballots(ad_ctx* c, uint64_t* n_entries, const uint64_t** msb, const u
     if (!c || !n_entries || !msb || !lsb || !node) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (int rc = sync_host(c)) return rc;
     auto& K = c->cfk;
     const uint64_t ne = K.status.size();
@@ -4304,6 +4378,7 @@ int ad_comm_init(ad_ctx* c, const uint8_t* id, int rank, int world)
 {
     if (!c || !id || world <= 0 || rank < 0 || rank >= world) return AD_E_INVAL;
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (c->comm) { (void)ncclCommDestroy(c->comm); c->comm = nullptr; }
     // the exchange table lives as long as the communicator: a step never allocates before the collective
     const size_t RW = AD_XROW_WORDS(world), words = RW * (size_t)(world + 1) + 2 * (size_t)world + 2;
@@ -4332,7 +4407,9 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
     if (!c) return AD_E_INVAL;
     if (!c->comm) return c->fail(AD_E_STATE, "ad_exchange: no communicator (ad_comm_init)");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    scope_.add(st);
     const uint32_t W = (uint32_t)c->comm_world, R = (uint32_t)c->comm_rank;
     const uint32_t fmt = x_format(c);
     const size_t RW = AD_XROW_WORDS(W);
@@ -4355,7 +4432,7 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
         const XRowHdr hd = x_row_hdr(c, fmt, own);
         memset(h, 0, sizeof(uint64_t) * RW);
         memcpy(h + 4 * W, hd.w, sizeof(hd.w));
-        if (hipMemcpy(mine, h, sizeof(uint64_t) * RW, hipMemcpyHostToDevice) != hipSuccess)
+        if (copy_sync(mine, h, sizeof(uint64_t) * RW, hipMemcpyHostToDevice) != hipSuccess)
             return x_abort(c, own);
         c->err = why;
     }
@@ -4393,7 +4470,7 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
         const int g = x_grow(c, send_units, runits, fmt);
         uint64_t* hs = h + RW * W;
         hs[0] = g ? (uint64_t)(-(int64_t)g) : 0;
-        if (hipMemcpy(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
+        if (copy_sync(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
         nr = ncclAllGather(sw, sw + 1, 1, ncclUint64, c->comm, st);
         if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclAllGather (exchange status)"));
         HIPCHK(c, hipMemcpyAsync(hs + 1, sw + 1, sizeof(uint64_t) * W, hipMemcpyDeviceToHost, st));
@@ -4449,6 +4526,7 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
     if (n_keys && !keys) return c->fail(AD_E_INVAL, "ad_cfk_prune: null key list");
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (c->dirty)
         if (int rc = build_snapshot(c)) return rc;
     if (int rc = sync_host(c)) return rc;
@@ -4542,6 +4620,7 @@ int ad_cfk_missing(ad_ctx* c, uint64_t* n_entries, const uint64_t** off, const u
     if (!c || !n_entries || !off || !msb || !lsb || !node) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (int rc = sync_host(c)) return rc;
     auto& K = c->cfk;
     if (K.miss_stale) return c->fail(AD_E_STATE, "missing() lists are stale (updates without deps moved entries): load them again");
@@ -4576,6 +4655,7 @@ int ad_cfk_byid(ad_ctx* c, uint64_t* n_keys, const int64_t** keys, const uint64_
     if (!c || !n_keys || !keys || !seg || !n_entries || !txn_msb || !txn_lsb || !txn_node || !pruned_before) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     if (int rc = sync_host(c)) return rc;
     auto& K = c->cfk;
     const uint64_t ne = K.txn.size(), nk = K.keys.size();
@@ -4625,11 +4705,13 @@ int ad_check_result_device(ad_ctx* c, const ad_deps_result* res_dev, void* strea
     if (!c || !res_dev || !n_violations) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     for (int m = 0; m < AD_NMAPS && res_dev->n_txns; ++m)
         if (!res_dev->keys_off[m] || !res_dev->keys[m] || !res_dev->txn_off[m] || !res_dev->txns[m] || !res_dev->k2t_off[m] ||
             !res_dev->k2t[m])
             return c->fail(AD_E_INVAL, "ad_check_result_device: a packed array of map %d is missing (AD_PARTS_ONLY result?)", m);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    scope_.add(st);
     int rc;
     if ((rc = check_begin(c, st))) return rc;
     HIPCHK(c, run_check_result(*res_dev, c->ds.n_dict, c->chk.p, st));
@@ -4641,6 +4723,7 @@ int ad_check_snapshot(ad_ctx* c, uint64_t* n_violations, uint64_t* first)
     if (!c || !n_violations) return AD_E_INVAL;
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
     int rc;
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     if ((rc = check_begin(c, c->stream))) return rc;

@@ -29,6 +29,7 @@
 
 #include "../../include/accord_deps.h"
 #include "cfk_update.hpp"
+#include "devmem.hpp"
 #include "kernels.hpp"
 #include "levels.hpp"
 
@@ -1364,25 +1365,10 @@ __global__ __launch_bounds__(256) void k_cm_merge(uint64_t na, const uint64_t* k
 
 unsigned blocks(uint64_t n, unsigned t = 256) { return (unsigned)std::max<uint64_t>(1, (n + t - 1) / t); }
 
-struct DBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~DBuf() { if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); } }   // non-blocking streams: nothing in flight may use it
-    // grows with slack (insertions raise the entry count every batch: no reallocation, and no
-    // re-zeroing of `word`, per batch); zero: the whole new allocation is zeroed
-    bool ensure(size_t b, bool zero = false)
-    {
-        if (p && b <= cap) return true;
-        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
-        p = nullptr;
-        cap = 0;
-        b = std::max<size_t>(b + b / 4, 64);
-        if (hipMalloc(&p, b) != hipSuccess) return false;
-        if (zero && (hipMemset(p, 0, b) != hipSuccess || hipDeviceSynchronize() != hipSuccess)) return false;
-        cap = b;
-        return true;
-    }
-    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+// grows with slack (insertions raise the entry count every batch: no reallocation, and no re-zeroing
+// of `word`, per batch); zero: the whole new allocation is zeroed
+struct DBuf : DevBuf {
+    bool ensure(size_t b, bool zero = false) { return grow(b, zero); }
 };
 
 }  // namespace
@@ -1878,6 +1864,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     uint64_t ndep = 0;
     if (track)
     {
+        dev_quiesce();
         if (hipMemcpy(&ndep, u.dep_off + n, 8, hipMemcpyDeviceToHost) != hipSuccess) { *err = "dep_off"; return AD_E_DEVICE; }
         UALLOC(w->uapp, n, false);
         UCHK(hipMemsetAsync(w->uapp.p, 0, n, st));

@@ -1,0 +1,94 @@
+// devmem.hpp — device memory of libaccord_deps: one allocator and one buffer type for every
+// translation unit (ABI, ingest, derivation/update, levels, exchange).
+//
+// Release ordering. Every ctx works on non-blocking streams, so a buffer freed (or grown) in the
+// middle of a call may still be read or written by work queued on that call's streams. dev_free
+// therefore first synchronizes the streams of the innermost StreamScope on this thread (the ctx
+// stream, its copy stream, a caller's stream) -- not the whole device, so other ctxs, the caller's
+// other streams and RCCL are not stalled -- and falls back to a device synchronization only when no
+// scope is open (ctx destruction, calls spanning several ctxs).
+//
+// Debug (environment, read once): AD_GUARD=1 puts a 64 KB guard band of a known pattern after every
+// allocation and checks it when the allocation is freed and on dev_guard_check() (the ABI exports it
+// as ad_debug_guard_check): a kernel or copy writing past the end of a buffer is reported with the
+// buffer's size instead of silently corrupting its neighbour. AD_GUARD=2 also poisons new allocations
+// (0xA5 bytes), so a read of memory nothing wrote gives the same wrong value on every run instead of
+// whatever the previous owner left there.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <string>
+
+namespace adx {
+
+void* dev_alloc(size_t bytes);                 // nullptr on failure
+void dev_free(void* p);                        // stream-ordered (see above); null is a no-op
+void dev_quiesce();                            // the current scope's streams, or the device
+hipStream_t dev_scope_stream();                // the scope's first stream (null: none open)
+// zero `bytes` at p, ordered on the scope's first stream and complete on return
+hipError_t dev_zero_sync(void* p, size_t bytes);
+int dev_guard_mode();                          // 0 off, 1 guards, 2 guards + poison
+// damaged guard bands among the live allocations (and the ones freed since the last call); a
+// description of each is appended to *report
+int dev_guard_check(std::string* report);
+
+// the streams whose queued work may touch the buffers a call frees (innermost scope wins)
+struct StreamScope {
+    explicit StreamScope(hipStream_t a, hipStream_t b = nullptr, hipStream_t c = nullptr);
+    ~StreamScope();
+    StreamScope(const StreamScope&) = delete;
+    StreamScope& operator=(const StreamScope&) = delete;
+    void add(hipStream_t s);
+    hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};
+    StreamScope* prev = nullptr;
+};
+
+// A growable device buffer. ensure() keeps the buffer when it is large enough, else frees it (stream-
+// ordered) and allocates `bytes` (at least 64); grow() does the same with 1/4 slack and optional zeroing
+// (buffers that grow every batch). Contents are not kept across a reallocation.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release()
+    {
+        if (p) dev_free(p);
+        p = nullptr;
+        cap = 0;
+    }
+    bool ensure(size_t bytes)
+    {
+        if (p && bytes <= cap) return true;
+        release();
+        const size_t b = std::max<size_t>(bytes, 64);
+        p = dev_alloc(b);
+        if (!p) return false;
+        cap = b;
+        return true;
+    }
+    bool grow(size_t bytes, bool zero = false)
+    {
+        if (p && bytes <= cap) return true;
+        release();
+        const size_t b = std::max<size_t>(bytes + bytes / 4, 64);
+        p = dev_alloc(b);
+        if (!p) return false;
+        cap = b;
+        if (zero && dev_zero_sync(p, b) != hipSuccess) return false;
+        return true;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+inline void swap_bufs(DevBuf& a, DevBuf& b)
+{
+    std::swap(a.p, b.p);
+    std::swap(a.cap, b.cap);
+}
+
+}  // namespace adx

@@ -7,6 +7,7 @@
 #include <string>
 
 #include "common.hpp"
+#include "devmem.hpp"
 
 namespace adx {
 
@@ -37,23 +38,7 @@ struct IngestOut {
 
 struct IngRec { uint64_t* hi; uint64_t* lo; int32_t* node; uint64_t* lsb; };
 
-struct IngDBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~IngDBuf() { if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); } }   // non-blocking streams: nothing in flight may use it
-    bool ensure(size_t b)
-    {
-        if (p && b <= cap) return true;
-        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
-        p = nullptr;
-        cap = 0;
-        b = std::max<size_t>(b, 64);
-        if (hipMalloc(&p, b) != hipSuccess) return false;
-        cap = b;
-        return true;
-    }
-    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
-};
+using IngDBuf = DevBuf;
 
 struct IngestWork;
 IngestWork* ingest_work_create();

@@ -30,6 +30,7 @@
 #include "kernels.hpp"
 #include "levels.hpp"
 #include "wave.hpp"
+#include "devmem.hpp"
 
 namespace adx {
 
@@ -237,10 +238,9 @@ __global__ void k_exec_rank(LevelsIn g, const uint32_t* __restrict__ order, uint
 }
 
 // occurrences in exec-rank order: okey = key with the sign flipped, oval = rank
-// orank (non-null: the walking dataflow): oval holds the occurrence index o and orank[o] its exec rank
 __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __restrict__ order,
                                                   const uint64_t* __restrict__ occ_off, uint64_t* __restrict__ okey,
-                                                  uint32_t* __restrict__ oval, LevelsCtl* ctl, uint32_t* __restrict__ orank)
+                                                  uint32_t* __restrict__ oval, LevelsCtl* ctl)
 {
     __shared__ uint64_t red[4];
     uint64_t d = 0;
@@ -253,13 +253,7 @@ __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __
         {
             const uint64_t k = (uint64_t)g.keys[j];
             okey[o + (j - s)] = k ^ 0x8000000000000000ull;
-            if (orank)
-            {
-                oval[o + (j - s)] = (uint32_t)(o + (j - s));
-                orank[o + (j - s)] = (uint32_t)r;
-            }
-            else
-                oval[o + (j - s)] = (uint32_t)r;
+            oval[o + (j - s)] = (uint32_t)r;
             d |= k ^ ref;
         }
     }
@@ -413,145 +407,6 @@ __global__ __launch_bounds__(256) void k_level_step(uint32_t L, const uint32_t* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Dataflow leveling: every txn's counter word packs {remaining predecessors : 32, max level seen
-// : 32}; finishing txn u (level L) updates each successor s with one 64-bit CAS {cnt - 1,
-// max(lvl, L + 1)} -- the CAS that takes cnt to 0 owns s, whose level is then exactly 1 + max over
-// its predecessors, in whatever order they finished. A launch spreads its ready list evenly over
-// the waves; a wave keeps the txns it releases in an LDS stack (newest first, so a dependency chain
-// is followed as soon as it is released) and works 16 of them per step, their successor edges
-// spread over the 64 lanes (as k_level_step). After FLOW_STEPS steps (or when its stack is full)
-// a wave hands what it holds to the next launch's ready list, so work never collapses onto a few
-// waves. Nothing ever waits for another wave; launches go out in chunks between host checks.
-// ---------------------------------------------------------------------------------------------
-constexpr uint32_t FLOW_Q = 1024;          // LDS stack entries per wave ({txn, level})
-constexpr uint32_t FLOW_WAVES = 4;
-constexpr uint32_t FLOW_STEPS = 8;         // steps per wave per launch
-constexpr uint32_t FLOW_SEEDS = 256;       // ready txns a wave takes at launch start (at most)
-constexpr uint32_t FLOW_CHUNK = 16;        // launches between host checks
-
-__global__ __launch_bounds__(64 * FLOW_WAVES) void k_level_flow(const uint2* __restrict__ in, const uint32_t* in_count,
-                                                                 uint2* __restrict__ out, uint32_t* out_count,
-                                                                 const uint64_t* __restrict__ succ_off,
-                                                                 const uint32_t* __restrict__ succ, unsigned long long* word,
-                                                                 uint32_t* __restrict__ level, unsigned long long* done_count,
-                                                                 uint32_t max_steps)
-{
-    __shared__ uint2 q_all[FLOW_WAVES][FLOW_Q];
-    uint2* q = q_all[threadIdx.x >> 6];
-    const uint32_t lane = lane_id();
-    const uint32_t n_waves = gridDim.x * FLOW_WAVES;
-    const uint32_t wid = blockIdx.x * FLOW_WAVES + (threadIdx.x >> 6);
-    const uint32_t ns = *in_count;
-    if (ns == 0) return;
-    // an even share of the ready list per wave (at most FLOW_SEEDS); the surplus moves on as is
-    const uint32_t per = min((ns + n_waves - 1) / n_waves, FLOW_SEEDS);
-    const uint32_t s0 = min(ns, wid * per), s1 = min(ns, s0 + per);
-    uint32_t nq = s1 - s0;                         // wave-uniform stack depth
-    for (uint32_t i = lane; i < nq; i += 64) q[i] = in[s0 + i];
-    const uint64_t cap = (uint64_t)n_waves * per;
-    if (ns > cap)
-    {
-        const uint32_t extra = ns - (uint32_t)cap, share = (extra + n_waves - 1) / n_waves;
-        const uint32_t e0 = min(extra, wid * share), e1 = min(extra, e0 + share);
-        uint32_t base = 0;
-        if (lane == 0 && e1 > e0) base = atomicAdd(out_count, e1 - e0);
-        base = __shfl(base, 0, 64);
-        for (uint32_t i = e0 + lane; i < e1; i += 64) out[base + (i - e0)] = in[cap + i];
-    }
-    wave_lds_sync();
-    uint64_t done = 0;
-    for (uint32_t step = 0; nq && step < max_steps; ++step)
-    {
-        const uint32_t g = min(nq, STEP_GROUP);
-        nq -= g;
-        uint2 me = make_uint2(0, 0);
-        uint64_t e0 = 0;
-        uint32_t deg = 0;
-        if (lane < g)
-        {
-            me = q[nq + lane];
-            level[me.x] = me.y;
-            e0 = succ_off[me.x];
-            deg = (uint32_t)(succ_off[me.x + 1] - e0);
-        }
-        wave_lds_sync();
-        done += g;
-        uint32_t inc = deg;
-#pragma unroll
-        for (uint32_t d = 1; d < STEP_GROUP; d <<= 1)
-        {
-            const uint32_t t = __shfl_up(inc, d, 64);
-            if (lane >= d) inc += t;
-        }
-        uint32_t incl[STEP_GROUP];
-#pragma unroll
-        for (uint32_t j = 0; j < STEP_GROUP; ++j) incl[j] = __shfl(inc, j, 64);
-        const uint32_t total = incl[STEP_GROUP - 1];
-        for (uint32_t x0 = 0; x0 < total; x0 += 64)
-        {
-            const uint32_t x = x0 + lane;
-            uint32_t owner = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < STEP_GROUP; ++j) owner += incl[j] <= x ? 1u : 0u;
-            // shuffles by every lane (a lane outside the exec mask reads back 0)
-            const uint64_t eo = __shfl(e0, owner & (STEP_GROUP - 1), 64);
-            const uint32_t prev = __shfl(inc, (owner - 1) & (STEP_GROUP - 1), 64);
-            const uint32_t lu = __shfl(me.y, owner & (STEP_GROUP - 1), 64);
-            const uint32_t before = owner == 0 ? 0u : prev;
-            bool ready = false;
-            uint32_t sx = 0, sl = 0;
-            if (x < total)
-            {
-                sx = succ[eo + (x - before)];
-                unsigned long long old = __hip_atomic_load(&word[sx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                while (true)
-                {
-                    const uint32_t cnt = (uint32_t)(old >> 32), lv = (uint32_t)old;
-                    const uint32_t nl = max(lv, lu + 1);
-                    const unsigned long long nw = ((unsigned long long)(cnt - 1) << 32) | nl;
-                    if (__hip_atomic_compare_exchange_strong(&word[sx], &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT))
-                    {
-                        ready = cnt == 1;
-                        sl = nl;
-                        break;
-                    }
-                }
-            }
-            // released successors go on the stack (to the next launch when it is full)
-            const uint64_t m = ballot(ready);
-            const uint32_t nr = __popcll(m);
-            if (nr)
-            {
-                const uint32_t pos = mbcnt(m);
-                if (nq + nr <= FLOW_Q)
-                {
-                    if (ready) q[nq + pos] = make_uint2(sx, sl);
-                    nq += nr;
-                }
-                else
-                {
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(out_count, nr);
-                    base = __shfl(base, 0, 64);
-                    if (ready) out[base + pos] = make_uint2(sx, sl);
-                }
-            }
-            wave_lds_sync();
-        }
-    }
-    // hand the rest of the stack to the next launch
-    if (nq)
-    {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(out_count, nq);
-        base = __shfl(base, 0, 64);
-        for (uint32_t i = lane; i < nq; i += 64) out[base + i] = q[i];
-    }
-    if (lane == 0 && done) atomicAdd(done_count, (unsigned long long)done);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Rank-ordered dataflow leveling. level[] (by exec rank) starts LV_UNSET. A wave takes the next 64
 // ranks by ticket, so the lowest unfinished rank always belongs to a running wave and every wait is
 // on a lower rank: a running wave (or a finished one) -- no deadlock whatever the dispatch order.
@@ -632,150 +487,6 @@ __global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* 
     }
 }
 
-// The walking dataflow (default): k_level_pull without a predecessor CSR. Each lane walks its txn's
-// key chains itself -- per occurrence, back along the (key, rank)-sorted occurrences while a kind T
-// witnesses is undominated, exactly k_chain's walk -- and waits on each kept predecessor as the walk
-// reaches it, then on its direct deps executing earlier (Commands.java:700-775). A lane blocked on a
-// predecessor keeps its walk state (occurrence, position, dominated kinds) and resumes after a sleep.
-// pos[o]: sorted position of occurrence o (occurrences of a txn are consecutive in rank order);
-// srank[p]: exec rank of the occurrence at sorted position p.
-__global__ void k_occ_pos(uint64_t n_occ, const uint32_t* __restrict__ oidx, const uint32_t* __restrict__ orank,
-                          uint32_t* __restrict__ pos, uint32_t* __restrict__ srank)
-{
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_occ) return;
-    const uint32_t o = oidx[p];
-    pos[o] = (uint32_t)p;
-    srank[p] = orank[o];
-}
-
-struct WalkArgs {
-    uint64_t n;
-    const uint64_t* occ_off;       // [n + 1] by rank
-    const uint32_t* pos;
-    const uint64_t* okey;          // sorted occurrence keys
-    const uint32_t* srank;
-    const uint8_t* kind_r;         // kind by rank
-    const uint32_t* order;         // rank -> txn index
-    const uint32_t* rank;          // txn index -> rank
-    const uint64_t* dep_off;       // by txn index, or null
-    const uint32_t* deps;
-};
-
-__global__ __launch_bounds__(256) void k_level_walk(WalkArgs a, uint32_t* level, uint32_t* ticket, uint32_t* fail,
-                                                    unsigned long long* n_edges, LevelsCtl* ctl, uint64_t budget, uint32_t naps)
-{
-    constexpr uint32_t NONE = 0xFFFFFFFFu;
-    const uint32_t lane = lane_id();
-    const uint64_t t_end = wall_clock64() + budget;
-    while (true)
-    {
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(ticket, 1u);
-        c = __shfl(c, 0, 64);
-        if ((uint64_t)c * 64 >= a.n) return;
-        const uint64_t T = (uint64_t)c * 64 + lane;
-        const bool on = T < a.n;
-        uint64_t o = on ? a.occ_off[T] : 0;
-        const uint64_t oe = on ? a.occ_off[T + 1] : 0;
-        const uint32_t A = on ? kind_witnesses(a.kind_r[T]) : 0u;
-        const uint32_t t = on ? a.order[T] : 0u;
-        uint64_t dj = (on && a.dep_off) ? a.dep_off[t] : 0, de = (on && a.dep_off) ? a.dep_off[t + 1] : 0;
-        uint64_t q = 0, key = 0;
-        uint32_t D = 0, pend = NONE, mx = 0, kept = 0;
-        bool walking = false, pending = on;
-        while (true)
-        {
-            if (pending)
-            {
-                bool blocked = false;
-                if (pend != NONE)
-                {
-                    const uint32_t v = lv_poll(level + pend);
-                    if (v == LV_UNSET) blocked = true;
-                    else { mx = max(mx, v + 1u); pend = NONE; }
-                }
-                // the key chains, back from each occurrence of T
-                while (!blocked)
-                {
-                    if (!walking)
-                    {
-                        if (o >= oe) break;
-                        q = a.pos[o++];
-                        key = a.okey[q];
-                        D = 0;
-                        walking = true;
-                    }
-                    if (q == 0 || (A & ~D) == 0) { walking = false; continue; }
-                    --q;
-                    if (a.okey[q] != key) { walking = false; continue; }
-                    const uint32_t P = a.srank[q];
-                    const uint32_t kp = a.kind_r[P];
-                    const uint32_t bit = kp < 32 ? 1u << kp : 0u;
-                    if (A & bit & ~D)
-                    {
-                        ++kept;
-                        D |= kind_witnesses(kp);
-                        const uint32_t v = lv_poll(level + P);
-                        if (v == LV_UNSET) { pend = P; blocked = true; }
-                        else mx = max(mx, v + 1u);
-                    }
-                    else if (D & bit)
-                        D |= kind_witnesses(kp);
-                }
-                // direct deps executing earlier
-                while (!blocked && dj < de)
-                {
-                    const uint32_t src = a.deps[dj++];
-                    if (src >= a.n)
-                    {
-                        atomicCAS(&ctl->error, 0u, (unsigned)(-AD_E_INVAL));
-                        dj = de;
-                        break;
-                    }
-                    const uint32_t P = a.rank[src];
-                    if (P >= T) continue;
-                    ++kept;
-                    const uint32_t v = lv_poll(level + P);
-                    if (v == LV_UNSET) { pend = P; blocked = true; }
-                    else mx = max(mx, v + 1u);
-                }
-                if (!blocked)
-                {
-                    __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    pending = false;
-                }
-            }
-            if (!ballot(pending)) break;
-            if (wall_clock64() > t_end)
-            {
-                if (lane == 0) atomicOr(fail, 1u);
-                return;
-            }
-            for (uint32_t z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(4);
-        }
-        uint32_t e = kept;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) e += __shfl_xor(e, d, 64);
-        if (lane == 0 && e) atomicAdd(n_edges, (unsigned long long)e);
-    }
-}
-
-__global__ void k_flow_init(const uint32_t* __restrict__ indeg, uint64_t n, unsigned long long* __restrict__ word,
-                            uint2* __restrict__ seeds, uint32_t* seed_count)
-{
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool src = r < n && indeg[r] == 0;
-    if (r < n) word[r] = (unsigned long long)indeg[r] << 32;
-    const uint64_t m = ballot(src);
-    if (!m) return;
-    uint32_t base = 0;
-    const uint32_t leader = __ffsll((unsigned long long)m) - 1;
-    if (lane_id() == leader) base = atomicAdd(seed_count, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
-    if (src) seeds[base + mbcnt(m)] = make_uint2((uint32_t)r, 0u);
-}
-
 __global__ void k_level_max(const uint32_t* __restrict__ level, uint64_t n, uint32_t* out_max)
 {
     uint32_t v = 0;
@@ -796,30 +507,11 @@ __global__ void k_level_out(const uint32_t* __restrict__ order, const uint32_t* 
 // ---------------------------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------------------------
-struct DBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    ~DBuf()
-    {
-        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
-    }
-    bool ensure(size_t bytes)
-    {
-        if (p && bytes <= cap) return true;
-        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }   // non-blocking streams: nothing in flight may use it
-        p = nullptr;
-        cap = 0;
-        const size_t b = std::max<size_t>(bytes, 64);
-        if (hipMalloc(&p, b) != hipSuccess) return false;
-        cap = b;
-        return true;
-    }
-    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
-};
+using DBuf = DevBuf;
 
 struct LevelsWork {
     DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kind_r, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
-        level, front0, front1, cnt, ctl, word, seedA, seedB, orank, opos, osrank;
+        level, front0, front1, cnt, ctl;
     LevelsCtl* h_ctl = nullptr;         // pinned
     uint64_t* h_u64 = nullptr;          // pinned, 4 words
     hipEvent_t ev[3] = {};
@@ -950,88 +642,22 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
                                                     w->kcnt.as<uint32_t>(), ctl);
     LV_CHK(run_scan_arrays(w->kcnt.as<uint32_t>(), w->occ_off.as<uint64_t>(), n, 1, bsum, st));
 
-    // leveling scheme: the dataflow over a predecessor CSR (default), the dataflow walking the key chains
-    // (AD_LEVELS_WALK; 4.2 ms against 0.85 ms on config 5: every wait re-walks a chain), the frontier loop
-    // (AD_LEVELS_FRONTIER) or the dataflow waves (AD_LEVELS_DATAFLOW=<steps>)
-    const char* df = getenv("AD_LEVELS_DATAFLOW");
-    const bool pull = df == nullptr && getenv("AD_LEVELS_FRONTIER") == nullptr;
-    const bool walk = pull && getenv("AD_LEVELS_WALK") != nullptr;
+    // leveling scheme: the dataflow over a predecessor CSR (default) or the frontier loop (AD_LEVELS_FRONTIER)
+    const bool pull = getenv("AD_LEVELS_FRONTIER") == nullptr;
 
     // ---- 2. key chains: occurrences in rank order, stably sorted by key
     uint64_t* okey = ka;
     uint32_t* oval = va;
-    if (walk) LV_ALLOC(w->orank, 4 * std::max<uint64_t>(n_occ, 1));
     if (n_occ)
     {
-        k_occ_fill<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, order, w->occ_off.as<uint64_t>(), okey, oval, ctl,
-                                                                             walk ? w->orank.as<uint32_t>() : nullptr);
+        k_occ_fill<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, order, w->occ_off.as<uint64_t>(), okey, oval, ctl);
         LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
         LV_CHK(hipStreamSynchronize(st));
         LV_CHK(radix_sort_pairs(okey, oval, kb, vb, n_occ, digits_of(w->h_ctl->diff[3]), hist, off, bsum, st, &okey,
                                 &oval));
     }
 
-    // ---- walking dataflow: sorted positions of the occurrences, then one leveling launch
-    if (walk)
-    {
-        LV_ALLOC(w->opos, 4 * std::max<uint64_t>(n_occ, 1));
-        LV_ALLOC(w->osrank, 4 * std::max<uint64_t>(n_occ, 1));
-        if (n_occ)
-            k_occ_pos<<<blocks_for(n_occ, 256), 256, 0, st>>>(n_occ, oval, w->orank.as<uint32_t>(), w->opos.as<uint32_t>(),
-                                                              w->osrank.as<uint32_t>());
-        LV_CHK(hipEventRecord(w->ev[1], st));
-        uint32_t* level = w->level.as<uint32_t>();
-        int dev = 0, cus = 256, khz = 100000;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-        int per_cu = 1, naps = 1, threads = 64;
-        if (const char* e = getenv("AD_LEVELS_PULL_PER_CU")) per_cu = std::max(1, std::min(8, atoi(e)));
-        if (const char* e = getenv("AD_LEVELS_PULL_NAPS")) naps = std::max(0, std::min(64, atoi(e)));
-        if (const char* e = getenv("AD_LEVELS_PULL_THREADS")) threads = atoi(e) == 64 ? 64 : (atoi(e) == 128 ? 128 : 256);
-        // cnt[0] ticket, cnt[1] failure flag, cnt[2] max level, cnt[4..5] edges (zeroed above)
-        LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
-        const uint64_t budget = (uint64_t)std::max(khz, 1000) * 1000ull;
-        const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, (n + threads - 1) / threads);
-        WalkArgs wa{n, w->occ_off.as<uint64_t>(), w->opos.as<uint32_t>(), okey, w->osrank.as<uint32_t>(), w->kind_r.as<uint8_t>(),
-                    order, w->rank.as<uint32_t>(), g.dep_off, g.deps};
-        k_level_walk<<<std::max(1u, grid), threads, 0, st>>>(wa, level, cnt, cnt + 1, reinterpret_cast<unsigned long long*>(cnt + 4),
-                                                             ctl, budget, (uint32_t)naps);
-        LV_CHK(hipGetLastError());
-        out->n_launch = 1;
-        k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);
-        k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
-        LV_CHK(hipEventRecord(w->ev[2], st));
-        uint32_t tail[6];
-        LV_CHK(hipMemcpyAsync(tail, cnt, sizeof(tail), hipMemcpyDeviceToHost, st));
-        LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
-        LV_CHK(hipStreamSynchronize(st));
-        if (w->h_ctl->error)
-        {
-            const int code = -(int)w->h_ctl->error;
-            *err = code == AD_E_DUP_EXEC ? "ad_levels: two txns with the same executeAt (CommandsForKey.java:1439)"
-                                         : "ad_levels: direct dep index out of range";
-            return code;
-        }
-        if (tail[1])
-        {
-            *err = "ad_levels: a wave waited more than a second for a predecessor's level";
-            return AD_E_STATE;
-        }
-        uint64_t edges = 0;
-        std::memcpy(&edges, &tail[4], 8);
-        out->n_edges = edges;
-        out->n_levels = (uint64_t)tail[2] + 1;
-        float a = 0, b = 0;
-        (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
-        (void)hipEventElapsedTime(&b, w->ev[1], w->ev[2]);
-        out->ms_build = a;
-        out->ms_frontier = b;
-        out->ms_total = a + b;
-        return AD_OK;
-    }
-
-    // ---- 3. sparsified predecessors -> predecessor CSR (pull) or successor CSR + in-degrees (frontier, dataflow)
+    // ---- 3. sparsified predecessors -> predecessor CSR (pull) or successor CSR + in-degrees (frontier)
     if (n_occ)
         k_chain<0><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), indeg,
                                                            pull ? nullptr : outdeg, nullptr, nullptr, nullptr);
@@ -1073,10 +699,8 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     }
     LV_CHK(hipEventRecord(w->ev[1], st));
 
-    // ---- 4. level the DAG: rank-ordered dataflow (default), the level-synchronous frontier loop
-    // (AD_LEVELS_FRONTIER) or the dataflow waves (AD_LEVELS_DATAFLOW=<steps>, FLOW_STEPS by default)
-    const bool frontier = !pull && df == nullptr;
-    const uint32_t flow_steps = df && atoi(df) > 0 ? (uint32_t)atoi(df) : FLOW_STEPS;
+    // ---- 4. level the DAG: rank-ordered dataflow (default) or the level-synchronous frontier loop
+    // (AD_LEVELS_FRONTIER)
     uint64_t nl = 0;
     if (pull)
     {
@@ -1111,7 +735,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         }
         nl = (uint64_t)tail[2] + 1;
     }
-    else if (frontier)
+    else
     {
         uint32_t* fr[2] = {w->front0.as<uint32_t>(), w->front1.as<uint32_t>()};
         k_frontier_init<<<blocks_for(n, 256), 256, 0, st>>>(indeg, n, level, fr[0], cnt);
@@ -1149,70 +773,6 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
             *err = "ad_levels: " + std::to_string(n - total) + " txns never became ready";
             return AD_E_STATE;
         }
-    }
-    else
-    {
-        // word[] (u64 per txn), two ready lists (uint2 per txn); counters in cnt[]: cnt[0..1] done
-        // (u64), cnt[2] max level, cnt[3 + i] = length of the list launch i of a chunk reads
-        LV_ALLOC(w->word, 8 * n);
-        LV_ALLOC(w->seedA, 8 * n);
-        LV_ALLOC(w->seedB, 8 * n);
-        unsigned long long* word = w->word.as<unsigned long long>();
-        uint2* lists[2] = {w->seedA.as<uint2>(), w->seedB.as<uint2>()};
-        uint32_t* ctr = cnt;
-        uint32_t* lc = cnt + 3;
-        LV_CHK(hipMemsetAsync(ctr, 0, 4 * (3 + FLOW_CHUNK + 1), st));
-        k_flow_init<<<blocks_for(n, 256), 256, 0, st>>>(indeg, n, word, lists[0], lc + 0);
-        static int per_cu = 0;
-        if (!per_cu)
-        {
-            int nb = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_level_flow, 64 * FLOW_WAVES, 0) != hipSuccess || nb <= 0)
-                nb = 1;
-            per_cu = std::min(nb, 4);
-        }
-        int dev = 0, cus = 256;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const unsigned grid = (unsigned)(cus * per_cu);
-        int cur = 0;
-        for (int chunk = 0;; ++chunk)
-        {
-            for (uint32_t i = 0; i < FLOW_CHUNK; ++i, cur ^= 1)
-                k_level_flow<<<grid, 64 * FLOW_WAVES, 0, st>>>(lists[cur], lc + i, lists[cur ^ 1], lc + i + 1, succ_off, succ,
-                                                               word, level, reinterpret_cast<unsigned long long*>(ctr),
-                                                               flow_steps);
-            out->n_launch += FLOW_CHUNK;
-            LV_CHK(hipGetLastError());
-            LV_CHK(hipMemcpyAsync(&w->h_u64[3], lc + FLOW_CHUNK, 4, hipMemcpyDeviceToHost, st));
-            LV_CHK(hipStreamSynchronize(st));
-            const uint32_t left = (uint32_t)w->h_u64[3];
-            if (left == 0) break;
-            if (chunk > (int)(n / FLOW_CHUNK) + 16)
-            {
-                *err = "ad_levels: dataflow did not drain";
-                return AD_E_STATE;
-            }
-            // the next chunk starts from the last list
-            LV_CHK(hipMemsetAsync(lc, 0, 4 * (FLOW_CHUNK + 1), st));
-            w->h_u64[3] = left;
-            LV_CHK(hipMemcpyAsync(lc, &w->h_u64[3], 4, hipMemcpyHostToDevice, st));
-        }
-        LV_CHK(hipMemsetAsync(ctr + 2, 0, 4, st));
-        k_level_max<<<256, 256, 0, st>>>(level, n, ctr + 2);
-        k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
-        LV_CHK(hipEventRecord(w->ev[2], st));
-        uint32_t tail[3];
-        LV_CHK(hipMemcpyAsync(tail, ctr, sizeof(tail), hipMemcpyDeviceToHost, st));
-        LV_CHK(hipStreamSynchronize(st));
-        uint64_t total = 0;
-        std::memcpy(&total, &tail[0], 8);
-        if (total != n)
-        {
-            *err = "ad_levels: " + std::to_string(n - total) + " txns never became ready";
-            return AD_E_STATE;
-        }
-        nl = (uint64_t)tail[2] + 1;
     }
     out->n_levels = nl;
     float a = 0, b = 0;

@@ -266,9 +266,15 @@ void ad_result_free(ad_deps_result* r);
  * batch after batch for queries and results. Unregister before freeing it. Pinning is page-granular:
  * register whole pages the caller owns (page-aligned p, bytes a multiple of the page size, e.g. an Arena
  * allocation with 4096-byte alignment); a sub-page range shares its pages with unrelated memory, which
- * its unregistration would unpin under any transfer still using them. */
+ * its unregistration would unpin under any transfer still using them. ad_host_unregister accepts a
+ * NULL ctx (a registration is process-wide): a finalizer can unpin memory whose ctx is already gone. */
 int ad_host_register(ad_ctx* ctx, void* p, uint64_t bytes);
 int ad_host_unregister(ad_ctx* ctx, void* p);
+
+/* Debug (AD_GUARD=1 or 2 in the environment): device allocations carry guard bands; returns the number
+ * of damaged bands found among live allocations and those freed since the last call (0: none, or the
+ * mode is off) and writes a description into buf (up to n bytes, NUL-terminated). */
+int ad_debug_guard_check(char* buf, uint64_t n);
 
 /* ad_deps_batch into caller-owned host arrays (the PCIe-facing path a Java host binds): `out`'s array
  * pointers are the caller's -- per map keys_off / txn_off / k2t_off with n_txns + 1 entries each, and

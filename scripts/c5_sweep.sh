@@ -1,5 +1,5 @@
 #!/bin/bash
-# config-5 leveling schemes: the CSR dataflow (default) over residency, the walking dataflow, the frontier loop
+# config-5 leveling schemes: the CSR dataflow (default) over residency, the frontier loop
 set -o pipefail
 mkdir -p gpurun_out
 run() {
@@ -9,6 +9,4 @@ run() {
 run csr-64x1
 AD_LEVELS_PULL_THREADS=128 run csr-128x1
 AD_LEVELS_PULL_PER_CU=2 run csr-64x2
-AD_LEVELS_WALK=1 run walk-64x1
-AD_LEVELS_WALK=1 AD_LEVELS_PULL_THREADS=128 run walk-128x1
 AD_LEVELS_FRONTIER=1 run frontier

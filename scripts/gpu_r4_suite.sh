@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4 fault check: the whole -m gpu suite with device guard bands (AD_GUARD=1: every allocation's
+# tail band checked after each test and at every free), then the plain unserialized suite, then the
+# default bench line. Stops at the first step that does not end normally.
+set -o pipefail
+mkdir -p gpurun_out
+TAG=${1:-r4}
+AD_GUARD=1 timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_${TAG}_guard.log 2>&1
+rc=$?; echo guard=$rc; tail -3 gpurun_out/t_${TAG}_guard.log; [ $rc -eq 0 ] || exit 1
+timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_${TAG}_plain.log 2>&1
+rc=$?; echo plain=$rc; tail -3 gpurun_out/t_${TAG}_plain.log; [ $rc -eq 0 ] || exit 2
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b_${TAG}.log 2>&1 || exit 3
+tail -c 1500 gpurun_out/b_${TAG}.log

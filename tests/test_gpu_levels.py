@@ -22,15 +22,10 @@ def _check(g, oracle):
 
 
 def _scheme(monkeypatch, scheme):
-    # None: the rank-ordered dataflow over a predecessor CSR (k_level_pull, default); "walk": the same
-    # walking the key chains (k_level_walk, experimental: left out of the suite); "frontier":
-    # the level-synchronous frontier loop; a number: the dataflow waves with that many steps per launch
+    # None: the rank-ordered dataflow over a predecessor CSR (k_level_pull, default); "frontier": the
+    # level-synchronous frontier loop (the two schemes the library has)
     if scheme == "frontier":
         monkeypatch.setenv("AD_LEVELS_FRONTIER", "1")
-    elif scheme == "walk":
-        monkeypatch.setenv("AD_LEVELS_WALK", "1")
-    elif scheme:
-        monkeypatch.setenv("AD_LEVELS_DATAFLOW", scheme)
 
 
 @pytest.mark.parametrize("scheme", [None, "frontier"])
@@ -41,14 +36,11 @@ def test_random_graph_all_kinds(oracle, seed, scheme, monkeypatch):
     _check(g, oracle)
 
 
-@pytest.mark.parametrize("walk", [False])
 @pytest.mark.parametrize("per_cu", ["1", "8"])
-def test_pull_occupancy(oracle, per_cu, walk, monkeypatch):
+def test_pull_occupancy(oracle, per_cu, monkeypatch):
     # fewer and more resident waves than the default (every wait still on a lower rank)
     monkeypatch.setenv("AD_LEVELS_PULL_PER_CU", per_cu)
     monkeypatch.setenv("AD_LEVELS_PULL_THREADS", "256")
-    if walk:
-        monkeypatch.setenv("AD_LEVELS_WALK", "1")
     g = synth.random_graph(17, n_txns=40_000, n_keys=300, long_runs=True)
     _check(g, oracle)
 
@@ -61,18 +53,9 @@ def test_config5_full_other_schemes(oracle, scheme, monkeypatch):
     assert st["n_levels"] == int(got.max()) + 1
 
 
-@pytest.mark.skip(reason="experimental dataflow waves (AD_LEVELS_DATAFLOW): left out of the suite, DESIGN §4")
-def test_config5_full_dataflow(oracle, monkeypatch):
-    monkeypatch.setenv("AD_LEVELS_DATAFLOW", "8")
-    g, _ = synth.config5()
-    got, st = _check(g, oracle)
-    assert st["n_levels"] == int(got.max()) + 1
-
-
 def test_many_sources_spill_path(oracle, monkeypatch):
-    # more sources than the dataflow stacks take in one launch (seed carry-over) and a hub with a
-    # fan-out far beyond one wave's stack (spills): 3M Reads (nothing witnesses a Read on a key),
-    # 2% of the later ones directly depending on txn 0
+    # 3M sources (nothing witnesses a Read on a key) and a hub with a fan-out of 60k: 2% of the later
+    # Reads directly depend on txn 0
     n = 3_000_000
     rng = np.random.default_rng(7)
     hlc = np.arange(1, n + 1, dtype=np.uint64)
@@ -86,9 +69,7 @@ def test_many_sources_spill_path(oracle, monkeypatch):
     deps = np.zeros(int(hub.sum()), np.uint32)
     g = Graph(ex, np.zeros(n, np.uint8), key_off, keys, dep_off, deps)
     for df in (None, "frontier"):
-        monkeypatch.delenv("AD_LEVELS_WALK", raising=False)
         monkeypatch.delenv("AD_LEVELS_FRONTIER", raising=False)
-        monkeypatch.delenv("AD_LEVELS_DATAFLOW", raising=False)
         _scheme(monkeypatch, df)
         got, st = _check(g, oracle)
         assert st["n_levels"] == 2
