@@ -42,11 +42,23 @@ def route(queries, lo, hi, start_inclusive=False):
     np.cumsum(sel, out=cs[1:])
     ko = queries.key_off.astype(np.int64)
     counts = cs[ko[1:]] - cs[ko[:-1]]
-    idx = np.nonzero(counts)[0].astype(np.int64)
+    touch = counts > 0
+    ro = rs = re_ = None
+    if queries.range_off is not None:
+        # a Range-domain request goes to every store whose slice one of its ranges intersects, ranges
+        # unchanged (the store slices them, InMemoryCommandStore.java:291)
+        hit = np.maximum(queries.range_start, lo) < np.minimum(queries.range_end, hi)
+        rc = np.zeros(len(hit) + 1, np.int64)
+        np.cumsum(hit, out=rc[1:])
+        roff = queries.range_off.astype(np.int64)
+        touch |= (rc[roff[1:]] - rc[roff[:-1]]) > 0
+    idx = np.nonzero(touch)[0].astype(np.int64)
     key_off = np.zeros(len(idx) + 1, np.uint64)
     key_off[1:] = np.cumsum(counts[idx])
     me = None if queries.min_epoch is None else queries.min_epoch[idx]
-    return Queries(queries.txn.take(idx), queries.exec.take(idx), key_off, k[sel], me), idx
+    if queries.range_off is not None:
+        ro, (rs, re_) = Queries._gather(queries.range_off, [queries.range_start, queries.range_end], idx)
+    return Queries(queries.txn.take(idx), queries.exec.take(idx), key_off, k[sel], me, ro, rs, re_), idx
 
 
 def build_global_dict(dicts):

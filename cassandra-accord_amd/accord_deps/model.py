@@ -271,17 +271,27 @@ class Redundant:
 
 @dataclass
 class Queries:
+    """A batch of calculatePartialDeps requests (ad_query_soa). Key-domain requests carry keys
+    (key_off / keys); Range-domain requests (range_off not None) carry normalised Ranges
+    (range_off / range_start / range_end) and no keys."""
     txn: Tids
     exec: Tids
     key_off: np.ndarray
     keys: np.ndarray
     min_epoch: Optional[np.ndarray] = None
+    range_off: Optional[np.ndarray] = None
+    range_start: Optional[np.ndarray] = None
+    range_end: Optional[np.ndarray] = None
 
     def __post_init__(self):
         self.key_off = A.as_u64(self.key_off)
         self.keys = A.as_i64(self.keys)
         if self.min_epoch is not None:
             self.min_epoch = A.as_i64(self.min_epoch)
+        if self.range_off is not None:
+            self.range_off = A.as_u64(self.range_off)
+            self.range_start = A.as_i64(self.range_start)
+            self.range_end = A.as_i64(self.range_end)
 
     def __len__(self):
         return len(self.txn)
@@ -289,6 +299,17 @@ class Queries:
     @property
     def n_probes(self):
         return int(self.key_off[-1]) if len(self.key_off) else 0
+
+    @property
+    def n_ranges(self):
+        return int(self.range_off[-1]) if self.range_off is not None and len(self.range_off) else 0
+
+    def ranges_of(self, i):
+        """[(start, end)] of request i (empty for a key-domain request)."""
+        if self.range_off is None:
+            return []
+        a, b = int(self.range_off[i]), int(self.range_off[i + 1])
+        return list(zip(self.range_start[a:b].tolist(), self.range_end[a:b].tolist()))
 
     def soa(self):
         s = A.AdQuerySoa()
@@ -298,25 +319,36 @@ class Queries:
         s.min_epoch = A.ptr(self.min_epoch)
         s.key_off = A.ptr(self.key_off)
         s.keys = A.ptr(self.keys)
+        s.n_keys = self.n_probes
+        if self.range_off is not None:
+            s.range_off = A.ptr(self.range_off)
+            s.range_start = A.ptr(self.range_start)
+            s.range_end = A.ptr(self.range_end)
+            s.n_ranges = self.n_ranges
         return s
 
     def window(self, lo, hi):
-        ko = self.key_off
-        return Queries(self.txn.take(slice(lo, hi)), self.exec.take(slice(lo, hi)),
-                       ko[lo:hi + 1] - ko[lo], self.keys[int(ko[lo]):int(ko[hi])],
-                       None if self.min_epoch is None else self.min_epoch[lo:hi])
+        return self.take(np.arange(lo, hi, dtype=np.int64))
+
+    @staticmethod
+    def _gather(off, vals, idx):
+        o = off.astype(np.int64)
+        cnt = o[idx + 1] - o[idx]
+        noff = np.zeros(len(idx) + 1, np.uint64)
+        noff[1:] = np.cumsum(cnt)
+        src = np.repeat(o[idx] - noff[:-1].astype(np.int64), cnt) + np.arange(int(noff[-1]))
+        return noff, [v[src] for v in vals]
 
     def take(self, idx):
         """The requests `idx` (ascending or not) as a batch of their own (SNAPSHOT requests are
         independent of each other, so a sample resolves to the same PartialDeps)."""
         idx = np.asarray(idx, np.int64)
-        ko = self.key_off.astype(np.int64)
-        cnt = ko[idx + 1] - ko[idx]
-        key_off = np.zeros(len(idx) + 1, np.uint64)
-        key_off[1:] = np.cumsum(cnt)
-        src = np.repeat(ko[idx] - key_off[:-1].astype(np.int64), cnt) + np.arange(int(key_off[-1]))
-        return Queries(self.txn.take(idx), self.exec.take(idx), key_off, self.keys[src],
-                       None if self.min_epoch is None else self.min_epoch[idx])
+        key_off, (keys,) = Queries._gather(self.key_off, [self.keys], idx)
+        ro = rs = re = None
+        if self.range_off is not None:
+            ro, (rs, re) = Queries._gather(self.range_off, [self.range_start, self.range_end], idx)
+        return Queries(self.txn.take(idx), self.exec.take(idx), key_off, keys,
+                       None if self.min_epoch is None else self.min_epoch[idx], ro, rs, re)
 
 
 @dataclass

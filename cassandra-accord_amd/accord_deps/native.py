@@ -760,6 +760,8 @@ def device_queries(q, dev):
         ("ko", q.key_off), ("k", q.keys)]}
     if q.min_epoch is not None:
         keep["me"] = to_dev(np.asarray(q.min_epoch, np.int64))
+    if q.range_off is not None:
+        keep["ro"], keep["rs"], keep["re"] = to_dev(q.range_off), to_dev(q.range_start), to_dev(q.range_end)
     s = A.AdQuerySoa()
     s.n_txns = len(q)
     s.txn_msb, s.txn_lsb, s.txn_node = keep["tm"].data_ptr(), keep["tl"].data_ptr(), keep["tn"].data_ptr()
@@ -767,6 +769,9 @@ def device_queries(q, dev):
     s.min_epoch = keep["me"].data_ptr() if "me" in keep else None
     s.key_off, s.keys = keep["ko"].data_ptr(), keep["k"].data_ptr()
     s.n_keys = int(q.key_off[-1]) if len(q.key_off) else 0
+    if q.range_off is not None:
+        s.range_off, s.range_start, s.range_end = keep["ro"].data_ptr(), keep["rs"].data_ptr(), keep["re"].data_ptr()
+        s.n_ranges = q.n_ranges
     return s, keep
 
 

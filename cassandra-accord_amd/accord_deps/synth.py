@@ -659,7 +659,8 @@ def slice_workload(w, lo, hi):
     counts = cs[ko[1:]] - cs[ko[:-1]]
     key_off = np.zeros(len(q) + 1, np.uint64)
     key_off[1:] = np.cumsum(counts)
-    qq = Queries(q.txn, q.exec, key_off, q.keys[qsel], q.min_epoch)
+    # Range-domain requests keep their ranges: the store slices them itself (ad_config slices)
+    qq = Queries(q.txn, q.exec, key_off, q.keys[qsel], q.min_epoch, q.range_off, q.range_start, q.range_end)
 
     c = w.cmds
     rs, re_, keep = clip(c.range_start, c.range_end)
@@ -697,10 +698,13 @@ def shard_local(w, lo, hi):
 # ------------------------------------------------------------------------------------------
 def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_range_cmds=12,
                  n_redundant=3, with_pruned=True, accept_frac=0.3, start_inclusive=False,
-                 with_slices=False, exec_below_frac=0.05):
+                 with_slices=False, exec_below_frac=0.05, range_frac=0.0):
     """All statuses (incl. TRANSITIVELY_KNOWN / INVALID), all globally visible kinds, prunedBefore,
     Accept-style executeAt > txnId (so PreAccept.java:261's self exclusion matters), requests whose
-    txnId is in the CFK, range commands (erased / historical / multi-range), RedundantBefore."""
+    txnId is in the CFK, range commands (erased / historical / multi-range), RedundantBefore.
+    range_frac: that share of the requests (none of them in a CommandsForKey) are Range-domain txns
+    (TxnId domain bit set) with 1-3 normalised ranges, from a few keys wide to most of the key space,
+    some touching or crossing slice, command and redundant-before boundaries."""
     rng = np.random.default_rng(seed)
     key_space = np.sort(rng.choice(np.arange(-500, 500), n_keys, replace=False)).astype(np.int64)
     hist_kinds = rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_SYNC_POINT, A.KIND_EXCLUSIVE_SYNC_POINT],
@@ -732,10 +736,13 @@ def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_rang
         for kr in rng.choice(n_keys, nk, replace=False):
             entries.append((kr, j))
     known_q = [j for j in q_idx if rng.random() < 0.25]
+    rng_q = set(j for j in q_idx if j not in known_q and rng.random() < range_frac) if range_frac else set()
     q_keys = {}
     for j in q_idx:
         nk = rng.integers(0, max_keys + 1)
         q_keys[j] = np.sort(rng.choice(n_keys, nk, replace=False))
+        if j in rng_q:
+            q_keys[j] = np.zeros(0, np.int64)
         if j in known_q:
             for kr in q_keys[j]:
                 entries.append((kr, j))
@@ -816,7 +823,32 @@ def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_rang
     key_off[1:] = np.cumsum([len(q_keys[j]) for j in q_idx])
     keys = np.concatenate([key_space[q_keys[j]] for j in q_idx] + [np.zeros(0, np.int64)])
     min_epoch = rng.integers(0, 3, n_txns).astype(np.int64)
-    q = Queries(qt, qe, key_off, keys, min_epoch)
+    ro = rs = re_ = None
+    if rng_q:
+        isr = np.array([j in rng_q for j in q_idx])
+        dom = isr.astype(np.uint64)
+        qt = Tids(qt.msb, qt.lsb | dom, qt.node)          # Range-domain TxnIds (TxnId.java:154-157)
+        qe = Tids(qe.msb, qe.lsb | dom, qe.node)
+        # ranges over the key line (endpoints may fall on keys, slice or command bounds)
+        bounds = np.concatenate([key_space, [-400, -100, 0, 300], r_s, r_e, pts]).astype(np.int64)
+        ro, rs, re_ = [0], [], []
+        for i in range(n_txns):
+            if isr[i]:
+                nr = int(rng.integers(1, 4))
+                wide = rng.random() < 0.3
+                cand = (np.sort(rng.choice(np.arange(-560, 560), 2 * nr, replace=False)) if wide else
+                        np.sort(np.unique(rng.choice(bounds, 2 * nr) + rng.integers(-1, 2, 2 * nr))))
+                for a in range(len(cand) // 2):
+                    if cand[2 * a] < cand[2 * a + 1]:
+                        rs.append(int(cand[2 * a]))
+                        re_.append(int(cand[2 * a + 1]))
+                if len(rs) == ro[-1]:                      # at least one range
+                    lo_ = int(rng.integers(-550, 500))
+                    rs.append(lo_)
+                    re_.append(lo_ + int(rng.integers(1, 60)))
+            ro.append(len(rs))
+        ro, rs, re_ = np.array(ro, np.uint64), np.array(rs, np.int64), np.array(re_, np.int64)
+    q = Queries(qt, qe, key_off, keys, min_epoch, ro, rs, re_)
     slices = None
     if with_slices:
         slices = np.array([[-400, -100], [0, 300]], np.int64)

@@ -199,6 +199,8 @@ struct ad_ctx {
 
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
+    DevBuf q_ro, q_rs, q_re;                   // Range-domain requests: staged ranges
+    DevBuf rq_cnt, rq_off, rq_err, rq_bsum, rq_keys, rq_hi, rq_kind;   // their expansion into probes
     struct SplitBufs {       // per-request / per-probe arrays of the split kernels
         DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
     } split, sub;
@@ -1712,7 +1714,48 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipMemcpyAsync(&np, q->key_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
     }
-    const bool split_only = c->cfg.path == 1 || recovery_scan >= 0;
+    // Range-domain requests (ad_query_soa.range_off): expanded into probes on the device -- keys inside
+    // the sliced ranges, the sliced ranges, the unsliced ranges (kernels.hip k_range_count /
+    // k_range_fill) -- then resolved by the split kernels
+    uint64_t nr = 0;
+    if (n && q->range_off)
+    {
+        if (n_keys_given)
+            nr = q->n_ranges;
+        else
+        {
+            uint64_t ro[2] = {0, 0};
+            HIPCHK(c, hipMemcpyAsync(&ro[0], q->range_off, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipMemcpyAsync(&ro[1], q->range_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+            nr = ro[1] - ro[0];
+        }
+    }
+    if (nr && recovery_scan >= 0) return c->fail(AD_E_INVAL, "recovery scans take key-domain requests only");
+    if (nr)
+    {
+        if (!ens<uint32_t>(c->rq_cnt, n) || !ens<uint64_t>(c->rq_off, n + 1) || !ens<uint32_t>(c->rq_err, 2) ||
+            !ens<uint64_t>(c->rq_bsum, (n + 1023) / 1024 + 16))
+            return c->fail(AD_E_NOMEM, "range request expansion");
+        HIPCHK(c, hipMemsetAsync(c->rq_err.p, 0, 8, st));
+        HIPCHK(c, run_range_count(c->ds, n, q->key_off, q->range_off, q->range_start, q->range_end, c->rq_cnt.as<uint32_t>(),
+                                  c->rq_err.as<uint32_t>(), st));
+        HIPCHK(c, run_scan_arrays(c->rq_cnt.as<uint32_t>(), c->rq_off.as<uint64_t>(), n, 1, c->rq_bsum.as<uint64_t>(), st));
+        uint64_t tail[2] = {0, 0};
+        HIPCHK(c, hipMemcpyAsync(&tail[0], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(&tail[1], c->rq_err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (tail[1])
+            return c->fail(AD_E_INVAL, "Range-domain request: keys and ranges together, or ranges not normalised "
+                                       "(start < end, ascending, disjoint)");
+        np = tail[0];
+        if (!ens<int64_t>(c->rq_keys, np) || !ens<int64_t>(c->rq_hi, np) || !ens<uint8_t>(c->rq_kind, np))
+            return c->fail(AD_E_NOMEM, "range request probes");
+        HIPCHK(c, run_range_fill(c->ds, n, q->key_off, q->keys, q->range_off, q->range_start, q->range_end,
+                                 c->rq_off.as<uint64_t>(), c->rq_keys.as<int64_t>(), c->rq_hi.as<int64_t>(),
+                                 c->rq_kind.as<uint8_t>(), st));
+    }
+    const bool split_only = c->cfg.path == 1 || recovery_scan >= 0 || nr > 0;
     // the lean kernel covers stores without redundant-before entries, elision on
     // (range commands only with their stabbing index)
     const bool lean = !split_only && np > 0 && (c->ds.n_rent == 0 || c->ds.cell_off != nullptr) && c->ds.n_rb == 0 &&
@@ -1723,6 +1766,13 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     b.q_txn_msb = q->txn_msb; b.q_txn_lsb = q->txn_lsb; b.q_txn_node = q->txn_node;
     b.q_exec_msb = q->exec_msb; b.q_exec_lsb = q->exec_lsb; b.q_exec_node = q->exec_node;
     b.q_min_epoch = q->min_epoch; b.q_key_off = q->key_off; b.q_keys = q->keys;
+    if (nr)
+    {
+        b.q_key_off = c->rq_off.as<uint64_t>();
+        b.q_keys = c->rq_keys.as<int64_t>();
+        b.q_keys_hi = c->rq_hi.as<int64_t>();
+        b.p_kind = c->rq_kind.as<uint8_t>();
+    }
     const uint64_t nb = (n + 1023) / 1024;
     if (!ens<uint32_t>(c->sz, 9 * n) || !ens<uint64_t>(c->off, 9 * (n + 1)) || !ens<uint64_t>(c->bsum, 9 * nb + 16) ||
         !ens<uint64_t>(c->t_reg, 3 * n) || !ens<BatchCtl>(c->ctl, 1) || !ens<uint32_t>(c->deferred, n) ||
@@ -2074,8 +2124,28 @@ static int result_to_host(ad_ctx* c, uint64_t n, const ad_deps_result& dev, ad_d
     return AD_OK;
 }
 
-static int check_query_host(ad_ctx* c, const ad_query_soa* q)
+static int check_query_host(ad_ctx* c, const ad_query_soa* q, uint32_t flags = 0)
 {
+    if (q->range_off && q->n_txns)
+    {
+        // Range-domain requests: ranges normalised (accord.primitives.Ranges), no keys beside them,
+        // SNAPSHOT semantics only
+        for (uint64_t i = 0; i < q->n_txns; ++i)
+        {
+            const uint64_t r0 = q->range_off[i], r1 = q->range_off[i + 1];
+            if (r1 < r0) return c->fail(AD_E_INVAL, "request %llu: range_off not monotone", (unsigned long long)i);
+            if (r1 == r0) continue;
+            if (q->key_off[i + 1] != q->key_off[i])
+                return c->fail(AD_E_INVAL, "request %llu has keys and ranges (a request is key- or Range-domain)", (unsigned long long)i);
+            if (flags & AD_SEQUENTIAL)
+                return c->fail(AD_E_INVAL, "SEQUENTIAL batches take key-domain requests only (request %llu has ranges)",
+                               (unsigned long long)i);
+            for (uint64_t j = r0; j < r1; ++j)
+                if (q->range_start[j] >= q->range_end[j] || (j > r0 && q->range_end[j - 1] > q->range_start[j]))
+                    return c->fail(AD_E_INVAL, "request %llu: ranges not normalised (start < end, ascending, disjoint)",
+                                   (unsigned long long)i);
+        }
+    }
     // host threads over request ranges; the lowest offending request is reported
     std::atomic<uint64_t> bad{~0ull};
     parallel_for(q->n_txns, [&](size_t a, size_t b) {
@@ -2116,6 +2186,14 @@ int ad_ctx_create(const ad_config* cfg, ad_ctx** out)
     c->cfg = *cfg;
     for (uint64_t i = 0; i < cfg->n_slices; ++i)
     {
+        // the store's Ranges, normalised (start < end, ascending, disjoint): Range-domain requests are
+        // sliced against them in order
+        if (cfg->slice_start[i] >= cfg->slice_end[i] || (i > 0 && cfg->slice_end[i - 1] > cfg->slice_start[i]))
+        {
+            g_create_err = "ad_ctx_create: slices not normalised (start < end, ascending, disjoint)";
+            delete c;
+            return AD_E_INVAL;
+        }
         c->slice_s.push_back(cfg->slice_start[i]);
         c->slice_e.push_back(cfg->slice_end[i]);
     }
@@ -2351,7 +2429,7 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
     if (!c->cfk.loaded) return c->fail(AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     StreamScope scope_(c->stream, c->cstream);
-    int rc = check_query_host(c, q);
+    int rc = check_query_host(c, q, flags);
     if (rc) return rc;
     if (flags & AD_SEQUENTIAL)
     {
@@ -2382,6 +2460,17 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
     d.min_epoch = stage_q(c, c->q_me, q->min_epoch, n, &rc);
     d.key_off = stage_q(c, c->q_ko, q->key_off, n + 1, &rc);
     d.keys = stage_q(c, c->q_k, q->keys, np, &rc);
+    if (n && q->range_off && q->range_off[n] > q->range_off[0])
+    {
+        const uint64_t r0 = q->range_off[0], nr = q->range_off[n] - r0;
+        std::vector<uint64_t> ro(n + 1);
+        for (uint64_t i = 0; i <= n; ++i) ro[i] = q->range_off[i] - r0;
+        d.range_off = stage_q(c, c->q_ro, ro.data(), n + 1, &rc);
+        d.range_start = stage_q(c, c->q_rs, q->range_start + r0, nr, &rc);
+        d.range_end = stage_q(c, c->q_re, q->range_end + r0, nr, &rc);
+        d.n_ranges = nr;
+        if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));     // ro is a local
+    }
     if (rc) return rc;
     ad_deps_result dev{};
     if ((rc = run_pipeline(c, &d, c->stream, &dev))) return rc;
@@ -2438,7 +2527,7 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
         if (!out->keys_off[m] || !out->txn_off[m] || !out->k2t_off[m] || (cap[3 * m] && !out->keys[m]) ||
             (cap[3 * m + 1] && !out->txns[m]) || (cap[3 * m + 2] && !out->k2t[m]))
             return c->fail(AD_E_INVAL, "ad_deps_batch_into: output arrays missing for map %d", m);
-    int rc = check_query_host(c, q);
+    int rc = check_query_host(c, q, flags);
     if (rc) return rc;
     if (flags & AD_SEQUENTIAL)
     {
@@ -2481,7 +2570,7 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
     uint64_t base[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool fits = true;
     ad_stats agg{};
-    std::vector<uint64_t> ko;
+    std::vector<uint64_t> ko, ro;
     hipStream_t st = c->stream;
     for (uint32_t j = 0; j < slices; ++j)
     {
@@ -2505,6 +2594,16 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
         d.min_epoch = q->min_epoch ? stage_q(c, c->q_me, q->min_epoch + lo, nc, &rc) : nullptr;
         d.key_off = stage_q(c, c->q_ko, ko.data(), nc + 1, &rc);
         d.keys = stage_q(c, c->q_k, q->keys + k0, k1 - k0, &rc);
+        if (nc && q->range_off && q->range_off[hi] > q->range_off[lo])
+        {
+            const uint64_t r0 = q->range_off[lo], nr = q->range_off[hi] - r0;
+            ro.resize(nc + 1);
+            for (uint64_t i = 0; i <= nc; ++i) ro[i] = q->range_off[lo + i] - r0;
+            d.range_off = stage_q(c, c->q_ro, ro.data(), nc + 1, &rc);
+            d.range_start = stage_q(c, c->q_rs, q->range_start + r0, nr, &rc);
+            d.range_end = stage_q(c, c->q_re, q->range_end + r0, nr, &rc);
+            d.n_ranges = nr;
+        }
         if (rc) return rc;
         ad_deps_result dev{};
         if ((rc = run_pipeline(c, &d, st, &dev, false, true))) return rc;      // complete on return
@@ -2956,6 +3055,8 @@ int ad_recovery_batch(ad_ctx* c, const ad_query_soa* q, uint32_t scan, ad_deps_r
     int rc = check_query_host(c, q);
     if (rc) return rc;
     const uint64_t n = q->n_txns;
+    if (n && q->range_off && q->range_off[n] > q->range_off[0])
+        return c->fail(AD_E_INVAL, "recovery scans take key-domain requests only");
     const uint64_t np = n ? q->key_off[n] : 0;
     ad_query_soa d{};
     d.n_txns = n;

@@ -175,6 +175,14 @@ __global__ void k_probe_keys(DevSnapshot s, BatchBufs b)
     if (p >= b.n_probes) return;
     const int64_t key = b.q_keys[p];
     const uint32_t t = b.p_txn[p];
+    const uint32_t pk = b.p_kind ? b.p_kind[p] : PK_KEY;
+    if (pk >= PK_RANGE)
+    {
+        // a range of a Range-domain request: no CommandsForKey (K1 visits nothing); K4 probes the range
+        // commands (sliced range, "in slice") or the redundant-before entries (unsliced range)
+        b.p_rec[p] = make_uint4(NO_KEY, b.t_S[t], b.t_self[t], b.t_kinds[t] | (pk == PK_RANGE ? (1u << 12) : 0u) | (pk << 13));
+        return;
+    }
     bool in_slice = s.n_slices == 0;
     for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
         in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
@@ -190,7 +198,7 @@ __global__ void k_probe_keys(DevSnapshot s, BatchBufs b)
         }
         if (lo < s.n_keys && s.keys[lo] == key) ki = (uint32_t)lo;   // ifLoadedAndInitialised(key) != null
     }
-    b.p_rec[p] = make_uint4(ki, b.t_S[t], b.t_self[t], b.t_kinds[t] | (in_slice ? (1u << 12) : 0u));
+    b.p_rec[p] = make_uint4(ki, b.t_S[t], b.t_self[t], b.t_kinds[t] | (in_slice ? (1u << 12) : 0u) | (pk << 13));
 }
 
 hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
@@ -199,6 +207,163 @@ hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
         k_encode_txn<<<(unsigned)((b.n_txns + 255) / 256), 256, 0, st>>>(s, b);
     if (b.n_probes)
         k_probe_keys<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Range-domain requests (SafeCommandStore.mapReduceActive over Ranges, SafeCommandStore.java:292):
+// every request becomes probes. A key-domain request keeps its keys (PK_KEY). A Range-domain request
+// gets, per range sliced to the store (Ranges.slice(slice, Minimal): each non-empty intersection with a
+// slice range, ascending), the CommandsForKey keys inside it (PK_RANGE_KEY: commandsForKey.subMap(start,
+// startInclusive, end, endInclusive), InMemoryCommandStore.java:289-304) followed by the range itself
+// (PK_RANGE, when the store has range commands: mapReduceRangesInternal's intersects/foldl,
+// :951-960), and at the end its unsliced ranges (PK_RANGE_RB, when the store has redundant-before
+// entries: RedundantBefore.collectDeps over the request's Seekables, RedundantBefore.java:420-423).
+// The keys come out ascending (sliced ranges ascending and disjoint), which is all K2 needs: range
+// probes contribute no keyDeps keys.
+// ---------------------------------------------------------------------------------------
+// first snapshot key index inside [a, b) / (a, b]: keys strictly above a (EndInclusive) or at/above a
+__device__ __forceinline__ uint64_t key_lb(const DevSnapshot& s, int64_t x, bool strictly_above)
+{
+    uint64_t lo = 0, hi = s.n_keys;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (strictly_above ? s.keys[mid] <= x : s.keys[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// the sliced part j of range [a, b) under slice sl (no slices: sl = 0 is the whole line): [*lo, *hi)
+__device__ __forceinline__ bool slice_part(const DevSnapshot& s, int64_t a, int64_t b, uint64_t sl, int64_t* lo, int64_t* hi)
+{
+    if (s.n_slices == 0)
+    {
+        *lo = a;
+        *hi = b;
+        return a < b;
+    }
+    *lo = a > s.slice_start[sl] ? a : s.slice_start[sl];
+    *hi = b < s.slice_end[sl] ? b : s.slice_end[sl];
+    return *lo < *hi;
+}
+
+__global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, const uint64_t* __restrict__ key_off,
+                                                     const uint64_t* __restrict__ range_off,
+                                                     const int64_t* __restrict__ range_start,
+                                                     const int64_t* __restrict__ range_end, uint32_t* __restrict__ cnt,
+                                                     uint32_t* err)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint64_t r0 = range_off[t], r1 = range_off[t + 1];
+    const uint64_t nk = key_off[t + 1] - key_off[t];
+    if (r1 == r0)
+    {
+        cnt[t] = (uint32_t)nk;
+        return;
+    }
+    bool bad = nk != 0;
+    const bool incl = s.start_inclusive != 0;
+    uint64_t c = 0;
+    const uint64_t n_sl = s.n_slices ? s.n_slices : 1;
+    for (uint64_t j = r0; j < r1; ++j)
+    {
+        const int64_t a = range_start[j], e = range_end[j];
+        if (a >= e || (j > r0 && range_end[j - 1] > a)) bad = true;
+        for (uint64_t sl = 0; sl < n_sl; ++sl)
+        {
+            int64_t lo, hi;
+            if (!slice_part(s, a, e, sl, &lo, &hi)) continue;
+            c += key_lb(s, hi, !incl) - key_lb(s, lo, !incl);
+            if (s.n_rent) ++c;
+        }
+    }
+    if (s.n_rb) c += r1 - r0;
+    if (bad) atomicOr(err, 1u);
+    cnt[t] = bad ? 0u : (uint32_t)min<uint64_t>(c, 0xFFFFFFFFull);
+}
+
+// one wave per request: the sliced ranges in order, their keys written lane-strided
+__global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, uint64_t n, const uint64_t* __restrict__ key_off,
+                                                    const int64_t* __restrict__ keys, const uint64_t* __restrict__ range_off,
+                                                    const int64_t* __restrict__ range_start,
+                                                    const int64_t* __restrict__ range_end, const uint64_t* __restrict__ off,
+                                                    int64_t* __restrict__ pkeys, int64_t* __restrict__ pkeys_hi,
+                                                    uint8_t* __restrict__ pkind)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (t >= n) return;
+    const uint32_t lane = lane_id();
+    const uint64_t r0 = range_off[t], r1 = range_off[t + 1];
+    uint64_t o = off[t];
+    const uint64_t o_end = off[t + 1];
+    if (r1 == r0)
+    {
+        const uint64_t k0 = key_off[t], nk = key_off[t + 1] - k0;
+        for (uint64_t i = lane; i < nk; i += 64)
+        {
+            pkeys[o + i] = keys[k0 + i];
+            pkeys_hi[o + i] = 0;
+            pkind[o + i] = PK_KEY;
+        }
+        return;
+    }
+    if (o_end == o) return;                      // rejected (k_range_count) or nothing to visit
+    const bool incl = s.start_inclusive != 0;
+    const uint64_t n_sl = s.n_slices ? s.n_slices : 1;
+    for (uint64_t j = r0; j < r1; ++j)
+    {
+        const int64_t a = range_start[j], e = range_end[j];
+        for (uint64_t sl = 0; sl < n_sl; ++sl)
+        {
+            int64_t lo, hi;
+            if (!slice_part(s, a, e, sl, &lo, &hi)) continue;
+            const uint64_t k0 = key_lb(s, lo, !incl), k1 = key_lb(s, hi, !incl);
+            for (uint64_t i = lane; i < k1 - k0; i += 64)
+            {
+                pkeys[o + i] = s.keys[k0 + i];
+                pkeys_hi[o + i] = 0;
+                pkind[o + i] = PK_RANGE_KEY;
+            }
+            o += k1 - k0;
+            if (s.n_rent)
+            {
+                if (lane == 0)
+                {
+                    pkeys[o] = lo;
+                    pkeys_hi[o] = hi;
+                    pkind[o] = PK_RANGE;
+                }
+                ++o;
+            }
+        }
+    }
+    if (s.n_rb)
+        for (uint64_t j = r0 + lane; j < r1; j += 64)
+        {
+            pkeys[o + (j - r0)] = range_start[j];
+            pkeys_hi[o + (j - r0)] = range_end[j];
+            pkind[o + (j - r0)] = PK_RANGE_RB;
+        }
+}
+
+hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
+                           const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
+                           hipStream_t st)
+{
+    if (n) k_range_count<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n, key_off, range_off, range_start, range_end, cnt, err);
+    return hipGetLastError();
+}
+
+hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
+                          const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
+                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, hipStream_t st)
+{
+    if (n)
+        k_range_fill<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(s, n, key_off, keys, range_off, range_start, range_end, off, pkeys,
+                                                              pkeys_hi, pkind);
     return hipGetLastError();
 }
 
@@ -413,9 +578,58 @@ __global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
     {
         const int64_t x = b.q_keys[p];
         const uint4 pr = b.p_rec[p];
+        const uint32_t pk = (pr.w >> 13) & 3;
+        // a range [x, xe) of a Range-domain request (PK_RANGE sliced, PK_RANGE_RB unsliced)
+        const int64_t xe = pk >= PK_RANGE ? b.q_keys_hi[p] : 0;
+        if (pk == PK_RANGE_RB)
+        {
+            // RedundantBefore.collectDeps over the request's ranges (RedundantBefore.java:420-423): every
+            // entry intersecting [x, xe) (Range.compareIntersecting, Range.java:296-305) -- the entries are
+            // disjoint and ascending, so they form one run -- in epoch bounds (:262-265) with a watermark
+            // above NONE (:188); values (rid << 32 | rank) ascending with the entries
+            const uint64_t e0 = wave_lower_bound(0, s.n_rb, [&](uint64_t i) { return s.rb_end[i]; },
+                                                 [&](int64_t v) { return v <= x; });
+            const uint64_t e1 = wave_lower_bound(0, s.n_rb, [&](uint64_t i) { return s.rb_start[i]; },
+                                                 [&](int64_t v) { return v < xe; });
+            const uint32_t t = b.p_txn[p];
+            const int64_t ep = b.t_epoch[t];
+            const int64_t mine = b.q_min_epoch ? b.q_min_epoch[t] : 0;
+            auto ok = [&](uint64_t e) { return !(ep < s.rb_e0[e] || mine >= s.rb_e1[e]) && s.rb_wm[e] != 0; };
+            uint32_t cnt = 0;
+            for (uint64_t e0r = e0; e0r < e1; e0r += 64)
+            {
+                const uint64_t e = e0r + lane;
+                cnt += __popcll(ballot(e < e1 && ok(e)));
+            }
+            uint64_t off = cnt ? alloc.take(&b.ctl->rng_top, cap, &b.ctl->overflow, 2u, cnt, K4_CHUNK) : 0;
+            if (off + cnt > cap)
+            {
+                off = 0;
+                cnt = 0;                 // overflow: the host grows the arena and reruns
+            }
+            else if (cnt)
+            {
+                uint32_t run = 0;
+                for (uint64_t e0r = e0; e0r < e1; e0r += 64)
+                {
+                    const uint64_t e = e0r + lane;
+                    const bool want = e < e1 && ok(e);
+                    const uint64_t wm = ballot(want);
+                    if (want) b.rarena[off + run + mbcnt(wm)] = ((uint64_t)s.rb_rid[e] << 32) | s.rb_wm[e];
+                    run += __popcll(wm);
+                }
+            }
+            if (lane == 0)
+            {
+                b.p_roff[p] = (uint32_t)off;
+                b.p_rcnt[p] = cnt;
+                b.p_rb[p] = NO_RB;
+            }
+            continue;
+        }
         // RedundantBefore.collectDeps over the request's keys (not sliced), RedundantBefore.java:420-423
         uint64_t rbv = NO_RB;
-        if (s.n_rb)
+        if (s.n_rb && pk == PK_KEY)
         {
             const uint64_t c = wave_lower_bound(0, s.n_rb, [&](uint64_t i) { return s.rb_start[i]; },
                                                 [&](int64_t v) { return incl ? v <= x : v < x; });
@@ -437,15 +651,18 @@ __global__ __launch_bounds__(256) void k_range(DevSnapshot s, BatchBufs b)
 
         uint32_t cnt = 0;
         uint64_t off = 0;
-        if (((pr.w >> 12) & 1) && s.n_rent)
+        if (((pr.w >> 12) & 1) && s.n_rent && pk != PK_RANGE_KEY)
         {
             const uint32_t S = pr.y, self = pr.z;
             const uint32_t kinds = pr.w & 0xFF;
             const int cls = (pr.w >> 8) & 3;
-            // candidate commands: range start before the key (Range.compareTo, Range.java:40-100)
+            // candidate commands: range start before the key (Range.compareTo, Range.java:40-100), or for
+            // a sliced range [x, xe) of a Range-domain request, start before its end and end after its start
+            // (Range.compareIntersecting, Range.java:296-305): the same prefix + max-end threshold
+            const bool rq = pk == PK_RANGE;
             const uint64_t hi = wave_lower_bound(0, s.n_rent, [&](uint64_t i) { return s.r_start[i]; },
-                                                 [&](int64_t v) { return incl ? v <= x : v < x; });
-            auto end_ok = [&](int64_t e) { return incl ? e > x : e >= x; };
+                                                 [&](int64_t v) { return rq ? v < xe : (incl ? v <= x : v < x); });
+            auto end_ok = [&](int64_t e) { return rq ? e > x : (incl ? e > x : e >= x); };
             auto node_want = [&](int lv, uint64_t node) { return end_ok(s.rlvl[cls][lv][node]); };
             uint32_t cursor = 0;
             bool overflow = false;

@@ -38,6 +38,10 @@ struct BatchBufs {
     const int64_t* q_min_epoch;      // may be null
     const uint64_t* q_key_off;
     const int64_t* q_keys;
+    // Range-domain requests (run_range_expand): per probe its kind (PK_*; null: every probe is a key of
+    // its request) and, for range and redundant-before probes, the range [q_keys[p], q_keys_hi[p])
+    const uint8_t* p_kind;
+    const int64_t* q_keys_hi;
     uint32_t* p_slot;                // lean passes without range commands: per probe its KeyLine (LS_NONE: outside the slice)
     uint32_t slots_by_prepare;       // p_slot filled by k_prepare (one launch for records and slots)
     // K0
@@ -116,6 +120,20 @@ hipError_t run_rv_inv_pairs(const RvDevIn& in, const uint64_t* eoff, uint64_t* k
 // inv_off[k] = eoff[segment start of k], inv_off[n_keys] = eoff[n_ent]; inv[p] = {rank, entry} of the sorted pairs
 hipError_t run_rv_inv_finish(const RvDevIn& in, const uint64_t* eoff, const uint64_t* skey, const uint32_t* sval,
                              uint64_t n_pairs, uint64_t* inv_off, uint2* inv, hipStream_t st);
+
+// Probe kinds of an expanded batch (a batch with Range-domain requests, run_range_expand): a key of a
+// key-domain request (K1 + K4 by key); a CommandsForKey key inside a Range-domain request's sliced ranges
+// (K1 only); one sliced range of such a request (K4: range commands whose range intersects it); one
+// unsliced range of it (K4: the RedundantBefore entries intersecting it)
+constexpr uint8_t PK_KEY = 0, PK_RANGE_KEY = 1, PK_RANGE = 2, PK_RANGE_RB = 3;
+// per request its probe count (cnt) and error flag (*err = 1: keys and ranges together, or ranges
+// not normalised); then, from the exclusive scan `off`, the probes
+hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
+                           const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
+                           hipStream_t st);
+hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
+                          const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
+                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, hipStream_t st);
 
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
 hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);

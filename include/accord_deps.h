@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define AD_ABI_VERSION 3
+#define AD_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define AD_OK                  0
@@ -186,6 +186,22 @@ typedef struct ad_query_soa {
     const int64_t*  keys;
     uint64_t        n_keys;          /* key_off[n_txns], read only under AD_N_KEYS (a device batch
                                       * then needs no device-to-host read before its first kernel) */
+    /* Range-domain requests (a txn whose Seekables are Ranges: sync points, range reads and writes;
+     * SafeCommandStore.mapReduceActive takes Seekables, SafeCommandStore.java:292). NULL range_off:
+     * every request is key-domain. Otherwise request i has the ranges
+     * [range_start[j], range_end[j]) j in [range_off[i], range_off[i+1]) -- Ranges normalised as
+     * accord.primitives.Ranges is: start < end, ascending, disjoint (end[j] <= start[j+1]), with the
+     * store's inclusivity (ad_config.range_start_inclusive) -- and then no keys (a request has keys or
+     * ranges, never both). For such a request the store visits every CommandsForKey whose key lies in
+     * the ranges sliced to the store's slices (InMemoryCommandStore.mapReduceForKey, case Range,
+     * :289-304), every range command with a range intersecting those sliced ranges
+     * (mapReduceRangesInternal, :884-1017) and the RedundantBefore entries intersecting the request's
+     * (unsliced) ranges (RedundantBefore.collectDeps, RedundantBefore.java:420-423). SNAPSHOT batches
+     * only (AD_SEQUENTIAL with a range request: AD_E_INVAL), not taken by ad_recovery_batch. */
+    const uint64_t* range_off;       /* [n_txns+1] or NULL */
+    const int64_t*  range_start;
+    const int64_t*  range_end;
+    uint64_t        n_ranges;        /* range_off[n_txns], read only under AD_N_KEYS */
 } ad_query_soa;
 
 typedef struct ad_stats {

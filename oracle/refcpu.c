@@ -587,6 +587,33 @@ static int slice_contains(const rc_store* s, int64_t key)
     return 0;
 }
 
+/* Range.compareIntersecting(that) == 0 (Range.java:296-305): this.start < that.end && this.end > that.start
+ * (the same test under both inclusivities) */
+static int range_intersects(const rkey_t* x, const rkey_t* y) { return x->a < y->b && x->b > y->a; }
+
+/* Ranges.slice(slice, Minimal) of a request's normalised ranges (AbstractRanges.slice, Range.slice
+ * Range.java:327-335): every non-empty intersection with a slice range, ascending (both sides are
+ * ascending and disjoint). out: room for nr * max(1, n_slices) ranges. */
+static size_t slice_ranges(const rc_store* s, const rkey_t* r, size_t nr, rkey_t* out)
+{
+    size_t n = 0;
+    for (size_t i = 0; i < nr; ++i)
+    {
+        if (s->n_slices == 0)
+        {
+            out[n++] = r[i];
+            continue;
+        }
+        for (size_t j = 0; j < s->n_slices; ++j)
+        {
+            const int64_t a = r[i].a > s->slice_start[j] ? r[i].a : s->slice_start[j];
+            const int64_t b = r[i].b < s->slice_end[j] ? r[i].b : s->slice_end[j];
+            if (a < b) out[n++] = (rkey_t){a, b};
+        }
+    }
+    return n;
+}
+
 static cfk_t* find_cfk(rc_store* s, int64_t key)
 {
     size_t lo = 0, hi = s->cfks.n;
@@ -753,12 +780,15 @@ static int collect_find_or_insert(collect_vec_t* col, const rkey_t* r)
  * command that contains at least one sliced key, then the collect fold of
  * InMemoryCommandStore.java:950-956 */
 static void collect_command(const rc_store* s, collect_vec_t* col, const rcmd_t* c,
-                            const int64_t* sliced, size_t nsliced)
+                            const int64_t* sliced, size_t nsliced, const rkey_t* rsliced, size_t nrsliced)
 {
     for (size_t r = 0; r < c->ranges.n; ++r)
     {
         int hit = 0;
         for (size_t k = 0; k < nsliced && !hit; ++k) hit = range_contains(s, &c->ranges.v[r], sliced[k]);
+        /* a Range-domain request: Routables.foldl(ranges, sliced ranges) visits each range of the
+         * command intersecting one of them (Routables.java:150-160) */
+        for (size_t k = 0; k < nrsliced && !hit; ++k) hit = range_intersects(&c->ranges.v[r], &rsliced[k]);
         if (!hit) continue;
         int pos = collect_find_or_insert(col, &c->ranges.v[r]);
         collect_entry_t* e = &col->v[pos];
@@ -769,10 +799,12 @@ static void collect_command(const rc_store* s, collect_vec_t* col, const rcmd_t*
 
 /* InMemoryCommandStore.mapReduceRangesInternal with STARTED_BEFORE, ANY_DEPS, ANY_STATUS
  * (InMemoryCommandStore.java:884-1017) */
-static int map_reduce_ranges_internal(const rc_store* s, const int64_t* keys, size_t nkeys, const tid_t* testTimestamp,
-                                      unsigned testKind, cmd_fn map, const tid_t* p1, void* acc)
+static int map_reduce_ranges_internal(const rc_store* s, const int64_t* keys, size_t nkeys, const rkey_t* rsliced,
+                                      size_t nrsliced, const tid_t* testTimestamp, unsigned testKind, cmd_fn map,
+                                      const tid_t* p1, void* acc)
 {
-    /* keysOrRanges.slice(slice, Minimal) */
+    /* keysOrRanges.slice(slice, Minimal) (:887): keys inside the slices; a Range-domain request's
+     * sliced ranges arrive as rsliced */
     int64_t* sliced = malloc(sizeof(int64_t) * (nkeys ? nkeys : 1));
     size_t nsliced = 0;
     for (size_t k = 0; k < nkeys; ++k) if (slice_contains(s, keys[k])) sliced[nsliced++] = keys[k];
@@ -785,14 +817,14 @@ static int map_reduce_ranges_internal(const rc_store* s, const int64_t* keys, si
         if (c->erased) continue;                                        /* saveStatus >= Erased, :897 */
         if (tid_cmp(&c->txnId, testTimestamp) >= 0) continue;           /* STARTED_BEFORE, :907 */
         if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;       /* :933 */
-        collect_command(s, &col, c, sliced, nsliced);                   /* intersects + foldl, :948-956 */
+        collect_command(s, &col, c, sliced, nsliced, rsliced, nrsliced); /* intersects + foldl, :951-960 */
     }
     for (size_t i = 0; i < s->hist.n; ++i)                               /* :959-987 */
     {
         const rcmd_t* c = &s->hist.v[i];
         if (tid_cmp(&c->txnId, testTimestamp) >= 0) continue;
         if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;
-        collect_command(s, &col, c, sliced, nsliced);
+        collect_command(s, &col, c, sliced, nsliced, rsliced, nrsliced);
     }
     int rc = 0;
     for (size_t i = 0; i < col.n && !rc; ++i)                            /* :990-997 */
@@ -805,16 +837,18 @@ static int map_reduce_ranges_internal(const rc_store* s, const int64_t* keys, si
 }
 
 /* RedundantBefore.collectDeps (RedundantBefore.java:420-423) -> Entry.collectDep (:183-192) */
-static int redundant_collect_deps(const rc_store* s, const int64_t* keys, size_t nkeys, int64_t minEpoch,
-                                  const tid_t* executeAt, deps_builder_t* d)
+static int redundant_collect_deps(const rc_store* s, const int64_t* keys, size_t nkeys, const rkey_t* ranges,
+                                  size_t nranges, int64_t minEpoch, const tid_t* executeAt, deps_builder_t* d)
 {
     static const tid_t NONE = {0, 0, 0};
-    for (size_t k = 0; k < nkeys; ++k)
+    /* RedundantBefore.foldl over the request's Seekables, unsliced: the entries holding a key, or
+     * intersecting a range of a Range-domain request */
+    for (size_t k = 0; k < nkeys + nranges; ++k)
     {
         for (size_t i = 0; i < s->rb.n; ++i)
         {
             const rb_entry_t* e = &s->rb.v[i];
-            if (!range_contains(s, &e->range, keys[k])) continue;
+            if (k < nkeys ? !range_contains(s, &e->range, keys[k]) : !range_intersects(&e->range, &ranges[k - nkeys])) continue;
             /* outOfBounds(lb, ub): ub.epoch() < startEpoch || lb.epoch() >= endEpoch, :262-265 */
             if (tid_epoch(executeAt) < e->startEpoch || minEpoch >= e->endEpoch) continue;
             if (tid_cmp(&e->wm, &NONE) > 0)
@@ -854,6 +888,7 @@ static int pdeps_with(const pdeps_t* x, const pdeps_t* y, pdeps_t* out)
 
 /* PreAccept.calculatePartialDeps, PreAccept.java:245-267 */
 static int calculate_partial_deps(rc_store* s, const tid_t* txnId, const int64_t* keys, size_t nkeys,
+                                  const rkey_t* ranges, size_t nranges,
                                   int64_t minEpoch, const tid_t* executeAt, pdeps_t* out, uint64_t* scan_entries)
 {
     unsigned kinds = kind_witnesses(tid_kind(txnId));                   /* txnId.kind().witnesses() */
@@ -874,8 +909,30 @@ static int calculate_partial_deps(rc_store* s, const tid_t* txnId, const int64_t
         if (cfk == NULL) continue;
         rc = cfk_map_reduce_active(cfk, executeAt, kinds, s->cfg.elide, preaccept_map, p1, &builder, scan_entries);
     }
-    if (!rc) rc = map_reduce_ranges_internal(s, keys, nkeys, executeAt, kinds, preaccept_map, p1, &builder);
-    if (!rc) rc = redundant_collect_deps(s, keys, nkeys, minEpoch, executeAt, &redundantBuilder);
+    /* case Range (:289-304): ranges.slice(slice, Minimal), then for each sliced range every
+     * CommandsForKey of commandsForKey.subMap(start, startInclusive, end, endInclusive), ascending */
+    size_t nrs = 0;
+    rkey_t* rsliced = NULL;
+    if (nranges)
+    {
+        rsliced = malloc(sizeof(rkey_t) * nranges * (s->n_slices ? s->n_slices : 1));
+        nrs = slice_ranges(s, ranges, nranges, rsliced);
+    }
+    for (size_t r = 0; r < nrs && !rc; ++r)
+    {
+        size_t lo = 0, hi = s->cfks.n;                /* first CommandsForKey key inside the range */
+        while (lo < hi)
+        {
+            size_t mid = (lo + hi) / 2;
+            if (s->cfg.range_start_inclusive ? s->cfks.v[mid].key < rsliced[r].a : s->cfks.v[mid].key <= rsliced[r].a) lo = mid + 1;
+            else hi = mid;
+        }
+        for (size_t k = lo; k < s->cfks.n && range_contains(s, &rsliced[r], s->cfks.v[k].key) && !rc; ++k)
+            rc = cfk_map_reduce_active(&s->cfks.v[k], executeAt, kinds, s->cfg.elide, preaccept_map, p1, &builder, scan_entries);
+    }
+    if (!rc) rc = map_reduce_ranges_internal(s, keys, nkeys, rsliced, nrs, executeAt, kinds, preaccept_map, p1, &builder);
+    if (!rc) rc = redundant_collect_deps(s, keys, nkeys, ranges, nranges, minEpoch, executeAt, &redundantBuilder);
+    free(rsliced);
 
     pdeps_t built, redundant;
     memset(&built, 0, sizeof(built)); memset(&redundant, 0, sizeof(redundant));
@@ -1014,9 +1071,31 @@ int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t f
         for (size_t k = 1; k < nkeys; ++k)
             if (keys[k - 1] >= keys[k]) { rc = fail(s, AD_E_INVAL, "query keys not strictly ascending"); break; }
         if (rc) break;
+        /* a Range-domain request: its Ranges, normalised (accord.primitives.Ranges) */
+        size_t nranges = q->range_off ? (size_t)(q->range_off[i + 1] - q->range_off[i]) : 0;
+        rkey_t* ranges = NULL;
+        if (nranges)
+        {
+            if (nkeys) { rc = fail(s, AD_E_INVAL, "request %llu has keys and ranges", (unsigned long long)i); break; }
+            if (flags & AD_SEQUENTIAL) { rc = fail(s, AD_E_INVAL, "SEQUENTIAL batches take key-domain requests only"); break; }
+            ranges = malloc(sizeof(rkey_t) * nranges);
+            for (size_t j = 0; j < nranges; ++j)
+            {
+                const uint64_t at = q->range_off[i] + j;
+                ranges[j] = (rkey_t){q->range_start[at], q->range_end[at]};
+                if (ranges[j].a >= ranges[j].b || (j > 0 && ranges[j - 1].b > ranges[j].a))
+                {
+                    rc = fail(s, AD_E_INVAL, "request %llu: ranges not normalised", (unsigned long long)i);
+                    break;
+                }
+            }
+            if (rc) { free(ranges); break; }
+        }
         if (flags & AD_SEQUENTIAL) sequential_preaccept(s, &txnId, keys, nkeys);
         pdeps_t pd;
-        rc = calculate_partial_deps(s, &txnId, keys, nkeys, q->min_epoch ? q->min_epoch[i] : 0, &executeAt, &pd, &r->scan_entries);
+        rc = calculate_partial_deps(s, &txnId, keys, nkeys, ranges, nranges, q->min_epoch ? q->min_epoch[i] : 0, &executeAt, &pd,
+                                    &r->scan_entries);
+        free(ranges);
         if (rc) break;
         result_append(r, qi, &pd, cap, len);
         pdeps_free(&pd);
@@ -1513,7 +1592,7 @@ static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t
             const int inter = tids_contain(c->deps.v, c->deps.n, T);
             if ((testDep == WITH) == !inter) continue;
         }
-        collect_command(s, &col, c, sliced, nsliced);                                   /* :949-956 */
+        collect_command(s, &col, c, sliced, nsliced, NULL, 0);                                   /* :949-956 */
     }
     int rc = 0;
     for (size_t i = 0; i < col.n && !rc; ++i)
@@ -1551,6 +1630,8 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
             return fail(s, AD_E_STATE, "recovery scans of range commands need their recovery facts (rc_range_cmds_recovery_load)");
     if (count == 0) count = q->n_txns - first;
     if (first + count > q->n_txns) return fail(s, AD_E_INVAL, "query window out of range");
+    if (q->range_off && q->range_off[q->n_txns] > q->range_off[0])
+        return fail(s, AD_E_INVAL, "recovery scans take key-domain requests only");
     rc_result* r = calloc(1, sizeof(rc_result));
     r->n_txns = count;
     size_t cap[AD_NMAPS][3] = {{0}};

@@ -1,10 +1,14 @@
 #!/bin/bash
-# Round-4 fault check: the whole -m gpu suite with device guard bands (AD_GUARD=1: every allocation's
-# tail band checked after each test and at every free), then the plain unserialized suite, then the
-# default bench line. Stops at the first step that does not end normally.
+# Round-4 GPU check: the new Range-domain request tests first (a plain failure does not stop the run;
+# a crash, abort or time limit does), then the whole -m gpu suite with device guard bands (AD_GUARD=1:
+# every allocation's tail band checked after each test and at every free), then the plain
+# unserialized suite, then the default bench line.
 set -o pipefail
 mkdir -p gpurun_out
 TAG=${1:-r4}
+crashed() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ranges.py tests/test_gpu_multi.py -k "range" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_${TAG}_ranges.log 2>&1
+rc=$?; echo ranges=$rc; tail -3 gpurun_out/t_${TAG}_ranges.log; crashed $rc && exit 9
 AD_GUARD=1 timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_${TAG}_guard.log 2>&1
 rc=$?; echo guard=$rc; tail -3 gpurun_out/t_${TAG}_guard.log; [ $rc -eq 0 ] || exit 1
 timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_${TAG}_plain.log 2>&1

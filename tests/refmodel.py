@@ -78,9 +78,16 @@ def request_pairs(w, qi, elide=True):
             return True
         return any(contains(si, int(a), int(b), k) for a, b in w.slices)
 
+    # a Range-domain request (ranges_of non-empty): its keys are every CommandsForKey key inside one of
+    # its ranges and inside the store's slices (InMemoryCommandStore.mapReduceForKey, case Range,
+    # InMemoryCommandStore.java:289-304) -- a key is in a sliced range iff it is in both
+    ranges = q.ranges_of(qi)
+    slices = [(None, None)] if w.slices is None else [(int(a), int(b)) for a, b in w.slices]
     kd, rd, dd = set(), set(), set()
     cfk = w.cfk
     kidx = {int(k): i for i, k in enumerate(cfk.keys)}
+    if ranges:
+        keys = [int(k) for k in cfk.keys if any(contains(si, a, b, int(k)) for a, b in ranges)]
     for k in keys:
         if not in_slice(k) or k not in kidx:
             continue
@@ -108,14 +115,24 @@ def request_pairs(w, qi, elide=True):
             continue
         for r in range(int(c.range_off[ci]), int(c.range_off[ci + 1])):
             s, e = int(c.range_start[r]), int(c.range_end[r])
-            if any(contains(si, s, e, k) for k in sliced):
+            if ranges:
+                # the command's range meets a request range inside a slice: three half-open intervals
+                # of one kind share a point iff the largest start is below the smallest end
+                hit = any(max(s, a, s if sa is None else sa) < min(e, b, e if sb is None else sb)
+                          for a, b in ranges for sa, sb in slices)
+            else:
+                hit = any(contains(si, s, e, k) for k in sliced)
+            if hit:
                 rd.add(((s, e), key(t), t))
     rb = w.redundant
     ep = ex[0] >> 15
     for i in range(len(rb.range_start)):
         s, e = int(rb.range_start[i]), int(rb.range_end[i])
         wm = (int(rb.wm.msb[i]), int(rb.wm.lsb[i]), int(rb.wm.node[i]))
-        if not any(contains(si, s, e, k) for k in keys):
+        if ranges:
+            if not any(max(s, a) < min(e, b) for a, b in ranges):      # unsliced request ranges
+                continue
+        elif not any(contains(si, s, e, k) for k in keys):
             continue
         if ep < int(rb.start_epoch[i]) or min_epoch >= int(rb.end_epoch[i]):
             continue

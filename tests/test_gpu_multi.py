@@ -92,6 +92,16 @@ def test_random_small_three_stores(seed, rank_ids):
 
 
 @pytest.mark.parametrize("rank_ids", [False, True])
+@pytest.mark.parametrize("seed", range(6))
+def test_range_requests_three_stores(seed, rank_ids):
+    # Range-domain requests routed to every store one of their ranges meets, sliced by each store,
+    # merged by K3 (PartialDeps.with) -- against the sharded oracle
+    w = synth.random_small(500 + seed, range_frac=0.5, n_keys=60)
+    w.slices = None
+    _check(w, synth.cut_bounds([-100, 150]), 2, rank_ids)
+
+
+@pytest.mark.parametrize("rank_ids", [False, True])
 @pytest.mark.parametrize("n_stores,n_owners", [(2, 2), (4, 4), (8, 8), (8, 3)])
 def test_config3_scaled(n_stores, n_owners, rank_ids):
     w = synth.config3(n_txns=40000, n_keys=6000, seed=11 + n_stores)

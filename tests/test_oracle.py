@@ -202,6 +202,48 @@ def test_crosscheck_python_restatement(oracle, seed):
             assert got[m] == (keys, vals, k2t), (seed, i, A.MAP_NAMES[m])
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_crosscheck_range_domain_requests(oracle, seed):
+    # Range-domain txns (SafeCommandStore.mapReduceActive over Ranges): every CommandsForKey key inside the
+    # sliced ranges (InMemoryCommandStore.java:289-304), range commands intersecting the sliced ranges
+    # (:884-1017), RedundantBefore entries intersecting the unsliced ranges (RedundantBefore.java:420-423)
+    w = synth.random_small(900 + seed, n_keys=40 + seed, n_txns=80, range_frac=0.5, with_slices=(seed % 3 == 1),
+                           start_inclusive=(seed % 4 == 2), n_redundant=(0 if seed % 5 == 4 else 4),
+                           n_range_cmds=(0 if seed % 6 == 5 else 16))
+    assert w.queries.n_ranges > 0
+    batch = oracle.resolve(w)
+    n_range_hits = 0
+    for i in range(len(w.queries)):
+        kd, rd, dd = refmodel.request_pairs(w, i)
+        n_range_hits += bool(w.queries.ranges_of(i)) and bool(kd or rd or dd)
+        got = _request(batch, i)
+        for m, pairs in ((0, kd), (1, rd), (2, dd)):
+            assert got[m] == refmodel.csr(pairs), (seed, i, A.MAP_NAMES[m])
+    assert n_range_hits > 0
+
+
+def test_range_domain_request_rejections(oracle):
+    w = synth.random_small(5, range_frac=0.5)
+    q = w.queries
+    i = next(i for i in range(len(q)) if q.ranges_of(i))
+    # keys and ranges together
+    bad = q.take(np.arange(len(q)))
+    bad.key_off = bad.key_off.copy()
+    j = int(bad.range_off[i])
+    bad.keys = np.insert(bad.keys, int(bad.key_off[i]), 3)
+    bad.key_off[i + 1:] += 1
+    w2 = synth.Workload(w.name, w.cfk, w.cmds, w.redundant, bad, w.flags, w.params, w.range_start_inclusive, w.slices)
+    with pytest.raises(RuntimeError):
+        oracle.resolve(w2)
+    # ranges not normalised (end <= start)
+    bad = q.take(np.arange(len(q)))
+    bad.range_end = bad.range_end.copy()
+    bad.range_end[j] = bad.range_start[j]
+    w2 = synth.Workload(w.name, w.cfk, w.cmds, w.redundant, bad, w.flags, w.params, w.range_start_inclusive, w.slices)
+    with pytest.raises(RuntimeError):
+        oracle.resolve(w2)
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_crosscheck_ephemeral_reads_at_timestamp_max(oracle, seed):
     # GetEphemeralReadDeps.apply computes deps at executeAt = Timestamp.MAX (GetEphemeralReadDeps.java:76,
