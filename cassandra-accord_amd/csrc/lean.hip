@@ -54,6 +54,12 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #ifndef LEAN_QLOAD
 #define LEAN_QLOAD 1
 #endif
+// LEAN_MASKED: loads move only the data their lanes use -- a request's record by one lane (broadcast by
+// readlane), keys / slots / KeyLine quarters / list elements exec-masked to the lanes that need them --
+// instead of clamped addresses on every lane (the texture data path moves bytes per active lane)
+#ifndef LEAN_MASKED
+#define LEAN_MASKED 1
+#endif
 
 __global__ __launch_bounds__(256) void k_lean_slots(DevSnapshot s, const int64_t* keys, uint64_t np, uint32_t* slot)
 {
@@ -297,10 +303,29 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         const uint32_t si = it * RPW + h;
         return si >= n_slots ? DEFER_HOLE : si;
     };
-    auto loadA = [&](uint32_t t) -> Raw { return b.q_rec[t != DEFER_HOLE ? t : 0u]; };
+    // one lane per request loads its 16-byte record (the texture data path moves 16 B per request, not
+    // per lane); derive() broadcasts it over the request's lanes
+    auto loadA = [&](uint32_t t) -> Raw {
+        if (!LEAN_MASKED) return b.q_rec[t != DEFER_HOLE ? t : 0u];
+        Raw r = make_uint4(0u, 0u, 0u, 0u);
+        if (hl == 0) r = b.q_rec[t != DEFER_HOLE ? t : 0u];
+        return r;
+    };
+    // the value of lane sb (the segment's first lane) in every lane of the segment
+    auto seg_bcast = [&](uint32_t v) -> uint32_t {
+        uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+#pragma unroll
+        for (uint32_t k = 1; k < RPW; ++k)
+        {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(k * LPR));
+            r = h == k ? x : r;
+        }
+        return r;
+    };
     // the record carries PreAccept.java:251-261's witness class, S and self as ranks (k_prepare)
     // and whether the request fits the lean path (<= 8 keys, valid kind); anything else defers
-    auto derive = [&](uint32_t t, const Raw& r) -> Req {
+    auto derive = [&](uint32_t t, const Raw& r0) -> Req {
+        const Raw r = LEAN_MASKED ? make_uint4(seg_bcast(r0.x), seg_bcast(r0.y), seg_bcast(r0.z), seg_bcast(r0.w)) : r0;
         Req q{0, 0, 0, t, 0, 0, false, false};
         q.act = t != DEFER_HOLE;
         q.k0 = r.x;
@@ -313,13 +338,25 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     };
     // the key (one lane per key), and with LEAN_SLOTS its line position beside it
     constexpr bool SLOTS = !RNG && LEAN_SLOTS;
+    // exec-masked: only the key lanes move data
     auto loadB = [&](const Req& q, int64_t& key, uint32_t& sl) {
         const bool on = q.act && !q.defer && hl < q.np;
-        key = b.q_keys[on ? q.k0 + hl : 0];
+        if (!LEAN_MASKED)
+        {
+            key = b.q_keys[on ? q.k0 + hl : 0];
+            if (SLOTS)
+            {
+                const uint32_t v = b.p_slot[on ? q.k0 + hl : 0];
+                sl = on ? v : LS_NONE;
+            }
+            return;
+        }
+        key = 0;
+        if (on) key = b.q_keys[q.k0 + hl];
         if (SLOTS)
         {
-            const uint32_t v = b.p_slot[on ? q.k0 + hl : 0];     // branch-free: exact wait counts
-            sl = on ? v : LS_NONE;
+            sl = LS_NONE;
+            if (on) sl = b.p_slot[q.k0 + hl];
         }
     };
     // the key's line (KeyLine, common.hpp): the slice test (InMemoryCommandStore.java:280), then one
@@ -360,7 +397,13 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         {
             // lane hl loads quarter hl & 3 of key hl >> 2's line (unmasked: unpacked under the key lane's look)
             const uint32_t ks = __shfl(look ? H.slot : LS_NONE, (int)(sb | (hl >> 2)), 64);
-            H.q = reinterpret_cast<const uint4*>(s.kline + (ks != LS_NONE ? ks : 0u))[hl & 3u];
+            if (!LEAN_MASKED)
+                H.q = reinterpret_cast<const uint4*>(s.kline + (ks != LS_NONE ? ks : 0u))[hl & 3u];
+            else
+            {
+                H.q = make_uint4(0u, 0u, 0u, 0u);
+                if (ks != LS_NONE) H.q = reinterpret_cast<const uint4*>(s.kline + ks)[hl & 3u];
+            }
             return;
         }
         load_line(H.slot, q.cls, H);
@@ -651,8 +694,11 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             lp = s.kline[a_slot].inl + (from_cand ? i : ((a_meta >> KL_INL_SHIFT) & 31u) + (i - a_n1));
         else
             lp = from_cand ? s.cand + (a_base + i) : s.cwr + (a_ct + (i - a_n1));
-        if (!live || (!from_cand && cls == 0)) lp = s.cand;        // class Ws: the last Write, no load
-        const uint32_t lv = (LEAN_EXP & 1) ? ((2 * hl + 1) | (1u << RANK_BITS)) : *lp;
+        // class Ws: the last Write, no load; lanes without an element load nothing
+        uint32_t lv = 0;
+        if (LEAN_EXP & 1) lv = (2 * hl + 1) | (1u << RANK_BITS);
+        else if (!LEAN_MASKED) lv = *((!live || (!from_cand && cls == 0)) ? s.cand : lp);
+        else if (live && (from_cand || cls != 0)) lv = *lp;
         // range elements (same round trip as the list loads)
         uint32_t ar = 0;
         uint64_t ce = 0;

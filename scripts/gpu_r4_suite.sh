@@ -9,6 +9,11 @@ TAG=${1:-r4}
 crashed() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
 timeout -k 10 300 python -u -m pytest tests/test_gpu_ranges.py tests/test_gpu_multi.py -k "range" -x -q --timeout 120 --timeout-method thread > gpurun_out/t_${TAG}_ranges.log 2>&1
 rc=$?; echo ranges=$rc; tail -3 gpurun_out/t_${TAG}_ranges.log; crashed $rc && exit 9
+# kernel lab: the in-tree library against the variants named in LAB (built by scripts/build_variant.sh)
+if [ -n "$LAB" ]; then
+  timeout -k 10 300 python -u scripts/lean_lab.py --steps 20 $LAB > gpurun_out/lab_${TAG}.log 2>&1
+  rc=$?; echo lab=$rc; cat gpurun_out/lab_${TAG}.log | grep "^{" ; crashed $rc && exit 8
+fi
 AD_GUARD=1 timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_${TAG}_guard.log 2>&1
 rc=$?; echo guard=$rc; tail -3 gpurun_out/t_${TAG}_guard.log; [ $rc -eq 0 ] || exit 1
 timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t_${TAG}_plain.log 2>&1
