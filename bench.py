@@ -87,6 +87,38 @@ def measured_traffic(kernels, tag=None):
     return None, None
 
 
+def measured_traffic_per_step(kernels, tag, unit_kernel):
+    """HBM bytes per step of a stage made of several kernels launched different numbers of times per
+    step (K5's build: radix passes, chain walks, scans): each kernel's per-launch bytes from the newest
+    committed PMC summary whose name holds `tag`, weighted by its launches per `unit_kernel` launch in
+    the same profile's kernel-stats CSV. Kernels absent from the profile count 0. (None, None) without
+    such a profile."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*%s*_pmc.json" % tag)))
+    for f in reversed(files):
+        stats = f[:-len("_pmc.json")] + "_kernel_stats.csv"
+        if not os.path.exists(stats):
+            continue
+        calls = {}
+        with open(stats) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Name") or row.get("KernelName") or ""
+                short = name.split("(")[0].replace("void ", "").replace("adx::", "").replace("(anonymous namespace)::", "")
+                calls[short] = calls.get(short, 0) + int(float(row.get("Calls") or 0))
+        if not calls.get(unit_kernel):
+            continue
+        with open(f) as fh:
+            d = json.load(fh)
+        tot = 0.0
+        for k in kernels:
+            if k in d and d[k].get("fetch_bytes_per_launch") is not None and calls.get(k):
+                per = 2 * d[k]["fetch_bytes_per_launch"] + (d[k].get("write_bytes_per_launch") or 0)
+                tot += per * calls[k] / calls[unit_kernel]
+        return tot, os.path.relpath(f, ROOT)
+    return None, None
+
+
 def stage_bytes(w, stats):
     """Algorithmic bytes per pipeline stage and launch.
     Fused resolve: request inputs (txnId + executeAt 40 B, key_off 8 B, 8 B per key) + the
@@ -309,7 +341,13 @@ def bench_levels(args, rank, world, local, dev):
         names = ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"]
     achieved = stats["bytes_stage"][dom] / (ms[dom] / 1000.0) / 1e9 if ms[dom] > 0 else 0.0
     lk = "k_level_pull" if pull else "k_level_step"
-    traffic, traffic_src = measured_traffic([lk] if dom == 1 else ["k_radix_scatter"])
+    if dom == 1:
+        traffic, traffic_src = measured_traffic([lk], tag="config5")
+    else:
+        build = ["k_exec_words", "k_exec_gather", "k_radix_count", "k_radix_scatter", "k_scan_reduce", "k_scan_sums",
+                 "k_scan_tile", "k_exec_rank", "k_occ_fill", "k_chain<0>", "k_chain<1>", "k_chain<2>", "k_direct<0>",
+                 "k_direct<1>", "k_direct<2>", "__amd_rocclr_copyBuffer", "__amd_rocclr_fillBufferAligned"]
+        traffic, traffic_src = measured_traffic_per_step(build, "config5", lk)
     res = {
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,

@@ -217,16 +217,25 @@ __global__ void k_exec_gather(LevelsIn g, const uint32_t* __restrict__ idx, int 
     out[i] = word == 1 ? x.lo : x.hi;
 }
 
-// rank[order[r]] = r; kind by rank; key count by rank; duplicate executeAt -> AD_E_DUP_EXEC
+// An occurrence carries its txn's exec rank and kind in one word: rank | kind << OCC_KIND_SHIFT (ranks
+// below 2^29). Kinds 6 and above (no Txn.Kind) all behave alike in the chain walk -- they witness
+// nothing and nothing witnesses them -- so they are clamped to 7.
+constexpr uint32_t OCC_KIND_SHIFT = 29;
+constexpr uint32_t OCC_RANK_MASK = (1u << OCC_KIND_SHIFT) - 1;
+__host__ __device__ inline uint32_t occ_word(uint32_t rank, uint32_t kind)
+{
+    return rank | ((kind < 7u ? kind : 7u) << OCC_KIND_SHIFT);
+}
+
+// rank[order[r]] = r; key count by rank; duplicate executeAt -> AD_E_DUP_EXEC
 // (the reference's committedByExecuteAt never holds two, CommandsForKey.java:1439)
 __global__ void k_exec_rank(LevelsIn g, const uint32_t* __restrict__ order, uint32_t* __restrict__ rank,
-                            uint8_t* __restrict__ kind_r, uint32_t* __restrict__ kcnt_r, LevelsCtl* ctl)
+                            uint32_t* __restrict__ kcnt_r, LevelsCtl* ctl)
 {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= g.n) return;
     const uint32_t t = order[r];
     rank[t] = (uint32_t)r;
-    kind_r[r] = g.kind[t];
     kcnt_r[r] = (uint32_t)(g.key_off[t + 1] - g.key_off[t]);
     if (r > 0)
     {
@@ -237,7 +246,7 @@ __global__ void k_exec_rank(LevelsIn g, const uint32_t* __restrict__ order, uint
     }
 }
 
-// occurrences in exec-rank order: okey = key with the sign flipped, oval = rank
+// occurrences in exec-rank order: okey = key with the sign flipped, oval = occ_word(rank, kind)
 __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __restrict__ order,
                                                   const uint64_t* __restrict__ occ_off, uint64_t* __restrict__ okey,
                                                   uint32_t* __restrict__ oval, LevelsCtl* ctl)
@@ -249,11 +258,12 @@ __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __
         const uint32_t t = order[r];
         const uint64_t s = g.key_off[t], e = g.key_off[t + 1], o = occ_off[r];
         const uint64_t ref = (uint64_t)g.keys[0];
+        const uint32_t w = occ_word((uint32_t)r, g.kind[t]);
         for (uint64_t j = s; j < e; ++j)
         {
             const uint64_t k = (uint64_t)g.keys[j];
             okey[o + (j - s)] = k ^ 0x8000000000000000ull;
-            oval[o + (j - s)] = (uint32_t)r;
+            oval[o + (j - s)] = w;
             d |= k ^ ref;
         }
     }
@@ -265,22 +275,25 @@ __global__ __launch_bounds__(256) void k_occ_fill(LevelsIn g, const uint32_t* __
 // (or a dominated txn) found later in the walk witnesses c: that one executes after P and waits
 // on it, so its level is larger. Pass 0: in-degree of T and (outdeg non-null) out-degree of each P;
 // pass 1: succ (successor lists); pass 2: pred (predecessor lists, offsets succ_off = scan of indeg).
+// The walk reads only the sorted occurrences (key, rank | kind): sequential, no per-step gather.
 template <int PASS>
-__global__ void k_chain(const uint64_t* __restrict__ okey, const uint32_t* __restrict__ orank, uint64_t n_occ,
-                        const uint8_t* __restrict__ kind_r, uint32_t* __restrict__ indeg, uint32_t* __restrict__ outdeg,
+__global__ void k_chain(const uint64_t* __restrict__ okey, const uint32_t* __restrict__ oval, uint64_t n_occ,
+                        uint32_t* __restrict__ indeg, uint32_t* __restrict__ outdeg,
                         const uint64_t* __restrict__ succ_off, uint32_t* __restrict__ cursor, uint32_t* __restrict__ succ)
 {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_occ) return;
     const uint64_t key = okey[p];
-    const uint32_t T = orank[p];
-    const uint32_t A = kind_witnesses(kind_r[T]);
+    const uint32_t wT = oval[p];
+    const uint32_t T = wT & OCC_RANK_MASK;
+    const uint32_t A = kind_witnesses(wT >> OCC_KIND_SHIFT);
     uint32_t D = 0, npred = 0;
     for (uint64_t q = p; q-- > 0 && (A & ~D) != 0;)
     {
         if (okey[q] != key) break;
-        const uint32_t P = orank[q];
-        const uint32_t kp = kind_r[P];
+        const uint32_t wP = oval[q];
+        const uint32_t P = wP & OCC_RANK_MASK;
+        const uint32_t kp = wP >> OCC_KIND_SHIFT;
         const uint32_t bit = kp < 32 ? 1u << kp : 0u;
         if (A & bit & ~D)
         {
@@ -510,7 +523,7 @@ __global__ void k_level_out(const uint32_t* __restrict__ order, const uint32_t* 
 using DBuf = DevBuf;
 
 struct LevelsWork {
-    DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kind_r, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
+    DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
         level, front0, front1, cnt, ctl;
     LevelsCtl* h_ctl = nullptr;         // pinned
     uint64_t* h_u64 = nullptr;          // pinned, 4 words
@@ -555,9 +568,9 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     *out = LevelsOut{};
     const uint64_t n = g.n;
     if (n == 0) return AD_OK;
-    if (n >= (1ull << 32) - 64)
+    if (n >= (1ull << OCC_KIND_SHIFT) - 64)
     {
-        *err = "ad_levels: too many txns (u32 ranks)";
+        *err = "ad_levels: too many txns (ranks below 2^29)";
         return AD_E_CAPACITY;
     }
     if (!w->h_ctl) LV_CHK(hipHostMalloc((void**)&w->h_ctl, sizeof(LevelsCtl), hipHostMallocDefault));
@@ -588,7 +601,6 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     LV_ALLOC(w->bsum, 8 * (std::max(hist_n, n) / 1024 + 2));
     LV_ALLOC(w->ord, 4 * n);
     LV_ALLOC(w->rank, 4 * n);
-    LV_ALLOC(w->kind_r, n);
     LV_ALLOC(w->kcnt, 4 * n);
     LV_ALLOC(w->occ_off, 8 * (n + 1));
     LV_ALLOC(w->indeg, 4 * n);
@@ -638,8 +650,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
                                 &kcur, &vcur));
     }
     LV_CHK(hipMemcpyAsync(order, vcur, 4 * n, hipMemcpyDeviceToDevice, st));
-    k_exec_rank<<<blocks_for(n, 256), 256, 0, st>>>(g, order, w->rank.as<uint32_t>(), w->kind_r.as<uint8_t>(),
-                                                    w->kcnt.as<uint32_t>(), ctl);
+    k_exec_rank<<<blocks_for(n, 256), 256, 0, st>>>(g, order, w->rank.as<uint32_t>(), w->kcnt.as<uint32_t>(), ctl);
     LV_CHK(run_scan_arrays(w->kcnt.as<uint32_t>(), w->occ_off.as<uint64_t>(), n, 1, bsum, st));
 
     // leveling scheme: the dataflow over a predecessor CSR (default) or the frontier loop (AD_LEVELS_FRONTIER)
@@ -659,7 +670,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
 
     // ---- 3. sparsified predecessors -> predecessor CSR (pull) or successor CSR + in-degrees (frontier)
     if (n_occ)
-        k_chain<0><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), indeg,
+        k_chain<0><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, indeg,
                                                            pull ? nullptr : outdeg, nullptr, nullptr, nullptr);
     if (g.dep_off)
         k_direct<0><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), indeg, pull ? nullptr : outdeg, nullptr,
@@ -682,7 +693,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     if (pull)
     {
         if (n_occ)
-            k_chain<2><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), nullptr, nullptr,
+            k_chain<2><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, nullptr, nullptr,
                                                                succ_off, cursor, succ);
         if (g.dep_off)
             k_direct<2><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), nullptr, nullptr, succ_off, cursor,
@@ -691,7 +702,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     else
     {
         if (n_occ)
-            k_chain<1><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, w->kind_r.as<uint8_t>(), nullptr, nullptr,
+            k_chain<1><<<blocks_for(n_occ, 256), 256, 0, st>>>(okey, oval, n_occ, nullptr, nullptr,
                                                                succ_off, cursor, succ);
         if (g.dep_off)
             k_direct<1><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), nullptr, nullptr, succ_off, cursor,
