@@ -4001,9 +4001,22 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         }
     }
     if (o.n_inserted) { c->host_moved = true; c->host_ingested = false; }
-    if ((rc == 0 || o.rolled_back || o.rederived) && c->kline_slots)
+    if ((rc == 0 || o.rolled_back || o.rederived || o.batch_stood) && c->kline_slots)
         HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
                                    c->kline_slots, st));
+    if (rc && o.batch_stood)
+    {
+        // the explicit batch stands but what follows it (additions, missing() lists) failed: the entries
+        // changed, the device lists are not this batch's -- the host copies follow on demand and the
+        // lists ask for a reload (as after a batch without deps)
+        c->host_stale = true;
+        ++c->snap_gen;
+        if (c->dmiss_on)
+        {
+            c->dmiss_on = false;
+            c->cfk.miss_stale = true;
+        }
+    }
     if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back && !o.rederived)
     {
         // the derived arrays may be half built: rebuild them from the entries at the next use

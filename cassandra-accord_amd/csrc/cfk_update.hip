@@ -45,6 +45,7 @@ enum : uint32_t {
     UE_FLAGS = 5,        // equal ids differing in flag bits
     UE_DOMAIN = 6,       // live range-domain id in a CommandsForKey
     UE_DUP_EXEC = 7,     // two committed entries of a key with one executeAt (:1439)
+    UE_UNWITNESSED = 8,  // a dep the txn's kind does not witness, inside byId, absent, not an ExclusiveSyncPoint
 };
 
 struct UpdCtl {
@@ -347,13 +348,52 @@ __global__ void k_past_words(uint64_t n, const uint64_t* sk, const uint32_t* sv,
 }
 
 __global__ void k_past_last(uint64_t n, const uint64_t* sk, const uint32_t* sv, const uint64_t* ex, const uint32_t* trk,
-                            uint32_t* last)
+                            uint32_t* last, uint32_t* pos)
 {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     const uint32_t i = sv[p];
     const uint32_t earlier = (ex[p] >> 32) == (sk[p] >> 32) ? (uint32_t)ex[p] : 0u;
     last[i] = max(trk[3 * (uint64_t)i + 1], earlier);
+    pos[i] = (uint32_t)p;          // the update's place in (key, batch index) order
+}
+
+// Updating.computeInfoAndAdditions (:239-249): a dep that falls between byId entries (not past the
+// key's last id as the update sees it), is absent from byId and is not witnessed by the txn's kind must
+// be an ExclusiveSyncPoint -- the Java's Invariants.checkState, here AD_E_INVAL. A dep an earlier update
+// of the batch on the same key added (witnessed by it, or past its last id) is in the Java's byId when
+// this update runs, so it passes. (Not distinguished: a dep only a later update of the batch inserts.)
+__global__ void k_dep_check(DevSnapshot s, CfkUpdIn u, const uint8_t* uapp, const uint32_t* drank, const uint32_t* last,
+                            const uint64_t* sk, const uint32_t* sv, const uint32_t* pos, UpdCtl* ctl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= u.n || !upd_with_deps(u, uapp, i)) return;
+    const uint32_t k = key_index_of(s, u.keys[i]);
+    if (k == KEY_EMPTY) return;
+    const KeyRec kr = s.krec[k];
+    const uint32_t wk = kind_witnesses((uint32_t)((u.txn_lsb[i] >> 1) & 7));
+    const uint32_t lst = last[i];
+    for (uint64_t j = u.dep_off[i]; j < u.dep_off[i + 1]; ++j)
+    {
+        const uint32_t r = drank[j], kd = (uint32_t)((u.dep_lsb[j] >> 1) & 7);
+        if (((wk >> kd) & 1u) || r > lst || kd == 4u /* ExclusiveSyncPoint */) continue;
+        if (seg_find(s, kr, r) != LOC_NONE) continue;
+        bool added = false;
+        const uint64_t p = pos[i];
+        for (uint64_t q = p; q-- > 0 && !added && (sk[q] >> 32) == (sk[p] >> 32);)
+        {
+            const uint32_t jj = sv[q];
+            if (!upd_with_deps(u, uapp, jj)) continue;
+            const uint32_t wj = kind_witnesses((uint32_t)((u.txn_lsb[jj] >> 1) & 7));
+            for (uint64_t d = u.dep_off[jj]; d < u.dep_off[jj + 1] && !added; ++d)
+                added = drank[d] == r && (((wj >> kd) & 1u) || r > last[jj]);
+        }
+        if (!added)
+        {
+            upd_fail(ctl, UE_UNWITNESSED, (uint32_t)i);
+            return;
+        }
+    }
 }
 
 // exclusive prefix max of u64 words (identity 0): per-1024 maxima, their scan (one block), the apply
@@ -1382,7 +1422,7 @@ struct CfkUpdWork {
     // missing() maintenance: per update applied flags, dep ranks, additions batch, derivation
     DBuf uapp, drank, acnt, aoff, a_k, a_tm, a_tl, a_tn, a_st, dsrc, mflag, mpp, mpend, mcnt, moff;
     // byId's last txnId as each update sees it (additions past the end) and the LoadPruned ids
-    DBuf trk, pk, pv, pk2, pv2, pvv, pw, pe, pbm, plast, lcnt, loff, l_k, l_tm, l_tl, l_tn, l_i;
+    DBuf trk, pk, pv, pk2, pv2, pvv, pw, pe, pbm, plast, ppos, lcnt, loff, l_k, l_tm, l_tl, l_tn, l_i;
     DBuf kn_a, kn_b, kv_a, kv_b, kflag, kfpos, knew, kpos;   // new keys
     // incremental committed order: the last derivation's order (entry indices), per-entry changed
     // flags (double-buffered with the entry arrays), the insertion's old -> new entry map
@@ -2065,6 +2105,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     out->n_inserted = G;
     // a duplicate committed executeAt: undo the batch and derive the previous state again
     if (w->h_ctl->err) return rollback(describe(w->h_ctl->err, w->h_ctl->err_idx));
+    out->batch_stood = true;
     if (track) return miss_after_batch(w, s, d, u, ndep, bufs, need, need_ctx, grow, st, out, err, miss);
     return AD_OK;
 }
@@ -2109,6 +2150,7 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
     UALLOC(w->pe, 8 * n, false);
     UALLOC(w->pbm, 8 * ((n + 1023) / 1024 + 1), false);
     UALLOC(w->plast, 4 * n, false);
+    UALLOC(w->ppos, 4 * n, false);
     {
         const uint32_t* trk = w->trk.as<uint32_t>();
         k_past_keys<<<blocks(n), 256, 0, st>>>(u, uapp, trk, w->drank.as<uint32_t>(), w->pk.as<uint64_t>(), w->pv.as<uint32_t>(),
@@ -2132,7 +2174,10 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
         k_maxscan_blocks<<<(unsigned)nb, 256, 0, st>>>(w->pw.as<uint64_t>(), n, w->pbm.as<uint64_t>());
         k_maxscan_top<<<1, 256, 0, st>>>(w->pbm.as<uint64_t>(), nb);
         k_maxscan_apply<<<(unsigned)nb, 256, 0, st>>>(w->pw.as<uint64_t>(), n, w->pbm.as<uint64_t>(), w->pe.as<uint64_t>());
-        k_past_last<<<blocks(n), 256, 0, st>>>(n, ks, vs, w->pe.as<uint64_t>(), trk, w->plast.as<uint32_t>());
+        k_past_last<<<blocks(n), 256, 0, st>>>(n, ks, vs, w->pe.as<uint64_t>(), trk, w->plast.as<uint32_t>(),
+                                               w->ppos.as<uint32_t>());
+        k_dep_check<<<blocks(n), 256, 0, st>>>(s, u, uapp, w->drank.as<uint32_t>(), w->plast.as<uint32_t>(), ks, vs,
+                                               w->ppos.as<uint32_t>(), ctl);
         UCHK(hipGetLastError());
         UALLOC(w->bsum, 8 * ((n + 1023) / 1024 + 8), false);
     }
@@ -2147,7 +2192,19 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
     uint64_t na = 0, nl = 0;
     UCHK(hipMemcpyAsync(&na, w->aoff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
     UCHK(hipMemcpyAsync(&nl, w->loff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
     UCHK(hipStreamSynchronize(st));
+    if (w->h_ctl->err == UE_UNWITNESSED)
+    {
+        // the explicit batch stands (the Java would have applied the updates before the throwing one);
+        // no additions, missing() lists marked for a reload
+        char b[200];
+        snprintf(b, sizeof(b), "cfk update %u: a dep its kind does not witness, absent from byId, is not an "
+                               "ExclusiveSyncPoint (Updating.java:239-249)", w->h_ctl->err_idx);
+        *err = b;
+        UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+        return AD_E_INVAL;
+    }
     if (na || nl)
     {
         UALLOC(w->a_k, 8 * std::max<uint64_t>(na, 1), false);

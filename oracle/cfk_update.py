@@ -288,6 +288,14 @@ def _witnesses(owner_raw, other_raw):
     return (mask >> _kind(other_raw)) & 1 == 1
 
 
+class UnwitnessedDep(ValueError):
+    """The Java's IllegalStateException of Updating.java:247 (update index, the dep's raw TxnId)."""
+
+    def __init__(self, index, dep):
+        super().__init__("update %d: unwitnessed dep %r is not an ExclusiveSyncPoint" % (index, dep))
+        self.index, self.dep = index, dep
+
+
 def cfk_update_missing(cfk, upd, dep_off=None, deps=None, load_pruned=None):
     """CommandsForKey.update (CommandsForKey.java:992-1042) for a batch, with the TxnInfo.missing()
     lists and the deps-derived additions of Updating.insertOrUpdate (Updating.java:99-172):
@@ -389,6 +397,10 @@ def cfk_update_missing(cfk, upd, dep_off=None, deps=None, load_pruned=None):
                 else:
                     if _witnesses(t, raw_of[d]):
                         additions.append(d)
+                    elif _kind(raw_of[d]) != 4:
+                        # Invariants.checkState(d.kind() == ExclusiveSyncPoint) (Updating.java:243-247): an
+                        # unwitnessed dep between byId entries must be an ExclusiveSyncPoint
+                        raise UnwitnessedDep(i, raw_of[d])
                     di += 1
             if di < len(dl):
                 additions.extend(dl[di:])

@@ -263,3 +263,53 @@ def test_load_pruned_collected():
         U.cfk_update_missing(w.cfk, u, u.dep_off, u.deps, load_pruned=lp)
         total += len(lp)
     assert total > 0
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_unwitnessed_non_esp_dep_rejected(oracle, seed):
+    # Updating.java:243-247: a dep the command's kind does not witness that falls between the key's byId
+    # entries must be an ExclusiveSyncPoint; anything else is the Java's IllegalStateException -> AD_E_INVAL
+    w = _workload(95 + seed, n_hist_txns=220)
+    rng = np.random.default_rng(950 + seed)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        cfk = w.cfk
+        base = G.transitions(cfk, rng, 30, statuses=(3, 4, 5, 6))[0]
+        u = with_deps(cfk, base, rng)
+        # a Read txn (witnesses Writes only) gets a fresh Read dep inside the key's window
+        seg = cfk.seg.astype(np.int64)
+
+        def cur_status(i):
+            k = int(np.searchsorted(cfk.keys, u.keys[i]))
+            nt = _norm(int(u.txn.msb[i]), int(u.txn.lsb[i]), int(u.txn.node[i]))
+            for e in range(int(seg[k]), int(seg[k + 1])):
+                if _norm(int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e])) == nt:
+                    return int(cfk.status[e])
+            return -1
+        # a Read update that applies (a higher status than the entry's) with a deps status
+        reads = [i for i in range(len(u)) if (int(u.txn.lsb[i]) >> 1) & 7 == 0 and int(u.status[i]) in (3, 4, 5, 6)
+                 and int(u.status[i]) > cur_status(i)]
+        assert reads, "generator gave no Read update with a deps status"
+        i = reads[0]
+        hlc = int(u.txn.lsb[i]) >> 16
+        bad = make_txn_ids(int(u.txn.msb[i]) >> 15, [max(1, hlc - 3)], [0], [97])
+        ids = [(int(a), int(b), int(c)) for a, b, c in zip(u.deps.msb, u.deps.lsb, u.deps.node)]
+        lo, hi = int(u.dep_off[i]), int(u.dep_off[i + 1])
+        row = sorted(ids[lo:hi] + [(int(bad.msb[0]), int(bad.lsb[0]), int(bad.node[0]))], key=lambda x: _norm(*x))
+        ids = ids[:lo] + row + ids[hi:]
+        off = u.dep_off.astype(np.int64).copy()
+        off[i + 1:] += 1
+        u = type(u)(u.keys, u.txn, u.exec, u.status, u.ballot, off.astype(np.uint64),
+                    Tids(np.array([x[0] for x in ids], np.uint64), np.array([x[1] for x in ids], np.uint64),
+                         np.array([x[2] for x in ids], np.int32)))
+        with pytest.raises(U.UnwitnessedDep):
+            U.cfk_update_missing(cfk, u, u.dep_off, u.deps)
+        with pytest.raises(native.AccordDepsError) as e:
+            st.cfk_update(u)
+        assert e.value.code == A.AD_E_INVAL and "ExclusiveSyncPoint" in str(e.value)
+        # the store still answers (the explicit batch stands, the lists ask for a reload)
+        got = st.calculate_partial_deps(w.queries)
+        assert got.n_txns == len(w.queries)
+    finally:
+        st.close()
