@@ -4595,8 +4595,23 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
     }
     // 5. this rank's parts, grouped by owner, into its send buffers (its own: into its receive buffers)
     x_keep_self(c, ea, xf.data(), W, R, dest_first[R], dest_first[R + 1], fmt);
-    if (int rc = x_emit(c, ea, st)) return x_abort(c, rc);
-    if (hipEventRecord(c->x_ev[1], st) != hipSuccess) return x_abort(c, c->fail(AD_E_DEVICE, "hipEventRecord"));
+    int erc = x_emit(c, ea, st);
+    if (!erc && hipEventRecord(c->x_ev[1], st) != hipSuccess) erc = c->fail(AD_E_DEVICE, "hipEventRecord");
+    // 5b. one-word status all-gather: a rank whose emit failed tells every peer before anyone posts a
+    //     send or receive, so the verdict stays collective (no rank waits inside the group for parts
+    //     that never come)
+    {
+        uint64_t* hs = h + RW * W;
+        hs[0] = erc ? (uint64_t)(-(int64_t)erc) : 0;
+        if (copy_sync(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
+        nr = ncclAllGather(sw, sw + 1, 1, ncclUint64, c->comm, st);
+        if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclAllGather (emit status)"));
+        HIPCHK(c, hipMemcpyAsync(hs + 1, sw + 1, sizeof(uint64_t) * W, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (erc) return erc;
+        for (uint32_t q = 0; q < W; ++q)
+            if (hs[1 + q]) return c->fail(AD_E_PEER, "ad_exchange: rank %u failed to emit its parts", q);
+    }
     // 6. grouped send/recv of the four arrays (own parts are in place already). The group is always
     //    closed; a failure inside it aborts the communicator.
     uint64_t moved = 0;
