@@ -325,3 +325,50 @@ def test_load_pruned_reports_dropped_additions():
     n, _, nadd = U.cfk_update_missing(c, u, off, dp, load_pruned=lp)
     assert nadd == 1
     assert [(i, k, int(t[1]) >> 16) for i, k, t in lp] == [(0, 7, 12), (0, 7, 15)]
+
+
+def test_kat_non_applied_update_does_not_move_byid_end():
+    # Known answer from CommandsForKey.update (:992-1042) + Updating.computeInfoAndAdditions (:210-263),
+    # derived by hand: update 0 lowers B (COMMITTED) to ACCEPTED -- not applied (:1013-1036), so its deps
+    # never reach computeInfoAndAdditions and byId's last id stays C (30). Update 1 accepts C (a Read) with
+    # deps {ESP 55}: the merge loop runs out of byId (10, 20, 30) first, so 55 is past the end and is added
+    # without the witness test (:253-262). Had the skipped update counted, its dep 60 would have moved the
+    # end past 55 and the ESP would have been skipped (:256-259).
+    c = _miss_store()
+    esp = A.KIND_EXCLUSIVE_SYNC_POINT
+    off, dp = _deps([[(60, W)], [(55, esp)]])
+    u = _upd([7, 7], [20, 30], [W, R], [A.ST_ACCEPTED, A.ST_ACCEPTED], [20, 30])
+    n, applied, nadd = U.cfk_update_missing(c, u, off, dp)
+    assert (applied, nadd) == (1, 1)
+    assert _hlcs(n) == [10, 20, 30, 55]
+    assert n.status.tolist() == [PA, CM, A.ST_ACCEPTED, A.ST_TRANSITIVELY_KNOWN]
+
+
+def test_kat_same_dep_below_pruned_before_in_two_updates():
+    # removePrunedAdditions (Updating.java:111-117) per update: D (W 40) ACCEPTED adds X (W 15), below
+    # prunedBefore B (20) -> dropped, LoadPruned(0, key 7, X); E (W 45) ACCEPTED in the same batch with the
+    # same dep: X is still absent from byId -> dropped again, LoadPruned(1, key 7, X). Nothing is inserted
+    # below prunedBefore; D and E are.
+    c = _miss_store()
+    c.pruned_before = np.array([1])
+    off, dp = _deps([[(15, W)], [(15, W)]])
+    u = _upd([7, 7], [40, 45], [W, W], [A.ST_ACCEPTED, A.ST_ACCEPTED])
+    lp = []
+    n, applied, nadd = U.cfk_update_missing(c, u, off, dp, load_pruned=lp)
+    assert (applied, nadd) == (2, 0)
+    assert _hlcs(n) == [10, 20, 30, 40, 45]
+    assert [(i, k, int(t[1]) >> 16) for i, k, t in lp] == [(0, 7, 15), (1, 7, 15)]
+
+
+def test_kat_unwitnessed_non_esp_dep_inside_byid_throws():
+    # Updating.java:243-247: C (a Read) accepted with a Read dep (17) that falls between byId entries and is
+    # absent: a Read does not witness a Read and it is no ExclusiveSyncPoint -> Invariants.checkState fails
+    c = _miss_store()
+    off, dp = _deps([[(10, W), (17, R)]])
+    u = _upd([7], [30], [R], [A.ST_ACCEPTED])
+    try:
+        U.cfk_update_missing(c, u, off, dp)
+    except U.UnwitnessedDep as e:
+        assert e.index == 0 and int(e.dep[1]) >> 16 == 17
+    else:
+        raise AssertionError("expected the IllegalStateException of Updating.java:247")

@@ -313,3 +313,57 @@ def test_unwitnessed_non_esp_dep_rejected(oracle, seed):
         assert got.n_txns == len(w.queries)
     finally:
         st.close()
+
+
+def _kat_cases():
+    """The hand-derived known answers of tests/test_cfk_update_oracle.py (test_kat_*), as (store, updates,
+    expect an AD_E_INVAL rejection)."""
+    import test_cfk_update_oracle as K
+    W, R, esp = A.KIND_WRITE, A.KIND_READ, A.KIND_EXCLUSIVE_SYNC_POINT
+    out = []
+    c = K._miss_store()
+    off, dp = K._deps([[(60, W)], [(55, esp)]])
+    u = K._upd([7, 7], [20, 30], [W, R], [A.ST_ACCEPTED, A.ST_ACCEPTED], [20, 30])
+    out.append((c, CfkUpdates(u.keys, u.txn, u.exec, u.status, None, off, dp), False))
+    c = K._miss_store()
+    c.pruned_before = np.array([1])
+    off, dp = K._deps([[(15, W)], [(15, W)]])
+    u = K._upd([7, 7], [40, 45], [W, W], [A.ST_ACCEPTED, A.ST_ACCEPTED])
+    out.append((c, CfkUpdates(u.keys, u.txn, u.exec, u.status, None, off, dp), False))
+    c = K._miss_store()
+    off, dp = K._deps([[(10, W), (17, R)]])
+    u = K._upd([7], [30], [R], [A.ST_ACCEPTED])
+    out.append((c, CfkUpdates(u.keys, u.txn, u.exec, u.status, None, off, dp), True))
+    return out
+
+
+@pytest.mark.parametrize("case", range(3))
+def test_hand_derived_kats_on_the_device(case):
+    # the same known answers through ad_cfk_update on the GPU: CommandsForKey, LoadPruned, or the rejection
+    from accord_deps.model import Queries, RangeCommands, Redundant, Workload
+    cfk, u, rejects = _kat_cases()[case]
+    z = np.zeros(0, np.uint64)
+    q = Queries(Tids(z, z, np.zeros(0, np.int32)), Tids(z, z, np.zeros(0, np.int32)), np.zeros(1, np.uint64),
+                np.zeros(0, np.int64))
+    w = Workload("kat", cfk, RangeCommands.empty(), Redundant.empty(), q)
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        if rejects:
+            with pytest.raises(native.AccordDepsError) as e:
+                st.cfk_update(u)
+            assert e.value.code == A.AD_E_INVAL
+            return
+        lp = []
+        exp, applied, nadd = U.cfk_update_missing(cfk, u, u.dep_off, u.deps, load_pruned=lp)
+        n_applied, stats = st.cfk_update(u)
+        assert n_applied == applied + nadd
+        keys, seg, txn, pruned = st.cfk_byid()
+        assert seg.tolist() == exp.seg.tolist()
+        assert [_norm(*x) for x in zip(txn.msb, txn.lsb, txn.node)] == \
+            [_norm(*x) for x in zip(exp.txn.msb, exp.txn.lsb, exp.txn.node)]
+        s, _ = st.cfk_entries()
+        assert s.tolist() == exp.status.tolist()
+        assert [(i, k, _norm(*t)) for i, k, t in st.cfk_load_pruned()] == [(i, k, _norm(*t)) for i, k, t in lp]
+    finally:
+        st.close()
