@@ -60,11 +60,7 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #ifndef LEAN_MASKED
 #define LEAN_MASKED 1
 #endif
-// LEAN_SIZES1: a request's 9 sizes and 3 region offsets are gathered in lanes (size j in lane j, map m's
-// offset in lane 9 + m) and stored by two instructions at the end of the item instead of two per map
-#ifndef LEAN_SIZES1
-#define LEAN_SIZES1 1
-#endif
+
 
 __global__ __launch_bounds__(256) void k_lean_slots(DevSnapshot s, const int64_t* keys, uint64_t np, uint32_t* slot)
 {
@@ -449,26 +445,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 
     // sizes of map m (keys, txnIds, keysToTxnIds) and its region offset: one store from lanes
     // hl = 0..3 of each segment (per-lane addresses keep the size arrays out of scalar registers)
-    // LEAN_SIZES1 staging (the main path): size j of the item's request in lane hl == j, map m's region
-    // offset in lane hl == 9 + m (has_ro: the map is not empty)
-    uint32_t szv = 0;
-    uint64_t rov = 0;
-    bool has_ro = false;
-    auto note_sizes = [&](int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro, bool with_ro) {
-        szv = hl == (uint32_t)(3 * m) ? v0 : (hl == (uint32_t)(3 * m + 1) ? v1 : (hl == (uint32_t)(3 * m + 2) ? v2 : szv));
-        if (with_ro && hl == (uint32_t)(9 + m))
-        {
-            rov = ro;
-            has_ro = true;
-        }
-    };
-    auto flush_sizes = [&](bool on, uint32_t t) {
-        if (on && hl < 9) b.sz[(uint64_t)hl * n + t] = szv;
-        if (on && has_ro) b.t_reg[(uint64_t)(hl - 9) * n + t] = rov;
-        szv = 0;
-        rov = 0;
-        has_ro = false;
-    };
     auto put_sizes = [&](bool on, uint32_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro, bool with_ro) {
         if (on && hl < 3)
         {
@@ -759,8 +735,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             const uint32_t tot = __popcll(seg(mb));
             if (mb == 0)
             {
-                if (LEAN_SIZES1) note_sizes(m, 0, 0, 0, 0, false);
-                else put_sizes(act, t, m, 0, 0, 0, 0, false);
+                put_sizes(act, t, m, 0, 0, 0, 0, false);
                 continue;
             }
             // sort (rank, key) per request; dedup -> txnIds; body = unique-rank index per key, ascending
@@ -811,8 +786,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits, it);
-            if (LEAN_SIZES1) note_sizes(m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
-            else put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
+            put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
             if (act && tot && fits && !(LEAN_EXP & 4))
             {
                 int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
@@ -834,8 +808,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         const uint64_t rmb = ballot(rwant);
         if (!RNG || rmb == 0)
         {
-            if (LEAN_SIZES1) note_sizes(1, 0, 0, 0, 0, false);
-            else put_sizes(act, t, 1, 0, 0, 0, 0, false);
+            put_sizes(act, t, 1, 0, 0, 0, 0, false);
         }
         else
         {
@@ -885,8 +858,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             const uint64_t bytes = act && totp ? (((uint64_t)nR * 8 + (uint64_t)UR * 4 + (uint64_t)(nR + UP) * 4 + 7) & ~7ull) : 0;
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits, it);
-            if (LEAN_SIZES1) note_sizes(1, fits ? nR : 0, fits ? UR : 0, fits ? nR + UP : 0, ro, true);
-            else put_sizes(act, t, 1, fits ? nR : 0, fits ? UR : 0, fits ? nR + UP : 0, ro, true);
+            put_sizes(act, t, 1, fits ? nR : 0, fits ? UR : 0, fits ? nR + UP : 0, ro, true);
             if (act && totp && fits)
             {
                 int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
@@ -904,7 +876,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
                 if (v2) ok2t[nR + (uint32_t)(k2 & 0xFF)] = (int32_t)ur2;
             }
         }
-        if (LEAN_SIZES1) flush_sizes(act, t);
         rotate(Hn);
     }
     dflush();
