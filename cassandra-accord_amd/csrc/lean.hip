@@ -35,7 +35,7 @@ constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 #endif
 constexpr uint32_t LEAN_CHUNK = 1u << LEAN_CHUNK_LOG;   // region bytes a wave takes from the arena at a time
 // measurement switches (scripts/build_variant.sh; results are wrong with any of them set):
-// 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes
+// 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes, 8 no size / offset stores
 #ifndef LEAN_EXP
 #define LEAN_EXP 0
 #endif
@@ -446,6 +446,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     // sizes of map m (keys, txnIds, keysToTxnIds) and its region offset: one store from lanes
     // hl = 0..3 of each segment (per-lane addresses keep the size arrays out of scalar registers)
     auto put_sizes = [&](bool on, uint32_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro, bool with_ro) {
+        if (LEAN_EXP & 8) return;
         if (on && hl < 3)
         {
             const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);

@@ -20,3 +20,5 @@ timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeo
 rc=$?; echo plain=$rc; tail -3 gpurun_out/t_${TAG}_plain.log; [ $rc -eq 0 ] || exit 2
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b_${TAG}.log 2>&1 || exit 3
 tail -c 1500 gpurun_out/b_${TAG}.log
+timeout -k 10 300 python -u bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/c5_${TAG}.log 2>&1 || exit 4
+tail -c 1200 gpurun_out/c5_${TAG}.log

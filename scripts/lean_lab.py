@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--regions", action="store_true", help="every library also timed with AD_REGIONS output")
+    ap.add_argument("--only", help="time this library alone (no in-tree base run; for counter passes)")
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -71,6 +72,8 @@ def main():
     sample = np.unique(np.concatenate([np.arange(2000), rng.choice(len(w.queries), 4000, replace=False)]))
     base_lib = os.path.join(ROOT, "cassandra-accord_amd", "accord_deps", "libaccord_deps.so")
     ref = None
+    if a.only:
+        base_lib, a.libs = a.only, []
     runs = [(lib, False) for lib in [base_lib] + a.libs]
     if a.regions:
         runs += [(lib, True) for lib in [base_lib] + a.libs]
