@@ -29,7 +29,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange", "ad_exchange_plan",
            "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing",
            "ad_cfk_load_pruned", "ad_host_register", "ad_host_unregister", "ad_deps_batch_into",
-           "ad_debug_guard_check")
+           "ad_debug_guard_check", "ad_host_alloc", "ad_host_free")
 
 
 class AccordDepsError(RuntimeError):
@@ -119,6 +119,8 @@ def lib():
         L.ad_host_register.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.ad_host_unregister.argtypes = [C.c_void_p, C.c_void_p]
         L.ad_debug_guard_check.argtypes = [C.c_char_p, C.c_uint64]
+        L.ad_host_alloc.argtypes = [C.c_uint64, C.POINTER(C.c_void_p)]
+        L.ad_host_free.argtypes = [C.c_void_p]
         L.ad_deps_batch_into.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.POINTER(A.AdDepsResult),
                                          C.c_void_p, C.c_void_p, C.c_uint32]
         L.ad_cfk_load_pruned.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)] + [C.POINTER(C.c_void_p)] * 5
@@ -432,16 +434,18 @@ class DeviceCommandStore:
             L.ad_result_free(out)
 
     class HostOut:
-        """Caller-owned host output arrays of ad_deps_batch_into (numpy), pinned with ad_host_register
-        when `pin`; grown (and re-pinned) when a batch needs more."""
+        """Caller-owned host output arrays of ad_deps_batch_into (numpy). pin=True: views of pinned memory
+        from ad_host_alloc (the default: copy-outs are DMAs straight into them); pin="register": numpy
+        pages of their own pinned with ad_host_register (the Panama binding's way, INTEGRATION.md);
+        pin=False: plain pageable numpy (filled through the library's staging). Grown (re-made) when a
+        batch needs more; release() frees / unpins, after which the arrays must not be used."""
 
         PAGE = 4096
 
         @staticmethod
         def _pages(shape, dtype):
             # zeroed array on whole pages of its own: a registration covers exactly its pages, so pinning
-            # (page-granular) never shares a page with another array or with the Python heap, and
-            # unregistering one array cannot unpin memory something else still transfers through
+            # (page-granular) never shares a page with another array or with the Python heap
             dtype = np.dtype(dtype)
             nbytes = int(np.prod(shape)) * dtype.itemsize
             span = -(-max(nbytes, 1) // DeviceCommandStore.HostOut.PAGE) * DeviceCommandStore.HostOut.PAGE
@@ -450,44 +454,67 @@ class DeviceCommandStore:
             a = raw[at:at + nbytes].view(dtype).reshape(shape)
             return a, span
 
+        @staticmethod
+        def _alloc(shape, dtype, blocks):
+            # a numpy view of library-pinned memory (ad_host_alloc); the block is freed by _free
+            dtype = np.dtype(dtype)
+            count = int(np.prod(shape))
+            nbytes = max(count * dtype.itemsize, 1)
+            p = C.c_void_p()
+            rc = lib().ad_host_alloc(nbytes, C.byref(p))
+            if rc or not p.value:
+                raise AccordDepsError(rc or A.AD_E_NOMEM, "ad_host_alloc(%d) failed" % nbytes)
+            blocks.append(p.value)
+            buf = (C.c_uint8 * nbytes).from_address(p.value)
+            a = np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
+            a[...] = 0
+            return a
+
         def __init__(self, store, n, cap, pin=True):
             self.store, self.pin, self.n = store, pin, n
             self.cap = [int(x) for x in cap]
-            P = DeviceCommandStore.HostOut._pages
-            self.off, s_off = P((9, n + 1), np.uint64)
-            ks = [P(max(1, self.cap[3 * m]), np.int64) for m in range(3)]
-            ts = [P(max(1, self.cap[3 * m + 1]), np.uint32) for m in range(3)]
-            os_ = [P(max(1, self.cap[3 * m + 2]), np.int32) for m in range(3)]
-            self.keys = [a for a, _ in ks]
-            self.txns = [a for a, _ in ts]
-            self.k2t = [a for a, _ in os_]
-            self.pinned = []
-            # unpinned when released, or at the latest when this object is collected (a test or caller
-            # that raises before release()): numpy must never free pages HIP still has registered. The
-            # finalizer holds the arrays (not self), so they outlive the registration; it needs no ctx.
-            self._fin = weakref.finalize(self, DeviceCommandStore.HostOut._unpin, self.pinned)
-            if pin:
-                try:
-                    for a, span in [(self.off, s_off)] + ks + ts + os_:
+            self.blocks, self.pinned = [], []
+            # freed / unpinned when released, or at the latest when this object is collected (a test or
+            # caller that raises before release()); the finalizer needs no ctx
+            self._fin = weakref.finalize(self, DeviceCommandStore.HostOut._free, self.blocks, self.pinned)
+            shapes = [((9, n + 1), np.uint64)] + [(max(1, self.cap[3 * m]), np.int64) for m in range(3)] + \
+                     [(max(1, self.cap[3 * m + 1]), np.uint32) for m in range(3)] + \
+                     [(max(1, self.cap[3 * m + 2]), np.int32) for m in range(3)]
+            arrs = []
+            try:
+                for shape, dt in shapes:
+                    if pin is True:
+                        arrs.append(DeviceCommandStore.HostOut._alloc(shape, dt, self.blocks))
+                    elif pin == "register":
+                        a, span = DeviceCommandStore.HostOut._pages(shape, dt)
                         store._check(lib().ad_host_register(store.h, A.ptr(a), span))
                         self.pinned.append(a)
-                except BaseException:
-                    self.release()
-                    raise
+                        arrs.append(a)
+                    else:
+                        arrs.append(np.zeros(shape, dt))
+            except BaseException:
+                self.release()
+                raise
+            self.off = arrs[0]
+            self.keys, self.txns, self.k2t = arrs[1:4], arrs[4:7], arrs[7:10]
 
         @staticmethod
-        def _unpin(pinned):
+        def _free(blocks, pinned):
             bad = 0
             for a in pinned:
                 if lib().ad_host_unregister(None, A.ptr(a)) != 0:
                     bad += 1
             pinned.clear()
+            for p in blocks:
+                if lib().ad_host_free(C.c_void_p(p)) != 0:
+                    bad += 1
+            blocks.clear()
             if bad:
-                raise AccordDepsError(A.AD_E_DEVICE, "ad_host_unregister failed for %d pinned output arrays" % bad)
+                raise AccordDepsError(A.AD_E_DEVICE, "freeing / unpinning %d output arrays failed" % bad)
 
         def release(self):
-            # the store's copy stream is drained by every ad_deps_batch_into return; the registration is
-            # process-wide, so the ctx-free unregister is right even after store.close()
+            # the store's copy stream is drained by every ad_deps_batch_into return
+            self.off = self.keys = self.txns = self.k2t = None
             self._fin()
 
         def soa(self):

@@ -327,10 +327,16 @@ struct ad_ctx {
 
 // A synchronous copy ordered after the work queued on the call's streams: the ctx streams are
 // non-blocking, so a plain null-stream hipMemcpy would not wait for their kernels (nor they for it).
+// Host memory goes through h2d / d2h (devmem.hpp: never a pageable HIP copy).
 static hipError_t copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind)
 {
     dev_quiesce();
-    return hipMemcpy(dst, src, bytes, kind);
+    const hipStream_t st = dev_scope_stream();
+    const hipError_t e = kind == hipMemcpyHostToDevice   ? h2d(dst, src, bytes, st)
+                         : kind == hipMemcpyDeviceToHost ? d2h(dst, src, bytes, st)
+                                                         : hipMemcpyAsync(dst, src, bytes, kind, st);
+    if (e != hipSuccess) return e;
+    return st ? hipStreamSynchronize(st) : hipDeviceSynchronize();
 }
 
 #define HIPCHK(ctx, expr)                                                                         \
@@ -374,7 +380,7 @@ template <class T>
 static int upload(ad_ctx* c, DevBuf& b, const std::vector<T>& v)
 {
     if (!b.ensure(sizeof(T) * std::max<size_t>(v.size(), 1))) return c->fail(AD_E_NOMEM, "hipMalloc %zu", sizeof(T) * v.size());
-    if (!v.empty()) HIPCHK(c, hipMemcpyAsync(b.p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, c->stream));
+    if (!v.empty()) HIPCHK(c, h2d(b.p, v.data(), sizeof(T) * v.size(), c->stream));
     return 0;
 }
 
@@ -1408,9 +1414,9 @@ static int host_dict(ad_ctx* c)
     c->dict_node.resize(nd);
     if (nd)
     {
-        HIPCHK(c, hipMemcpyAsync(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->dict_node.data(), c->d_dict_node.p, 4 * nd, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, d2h(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, c->stream));
+        HIPCHK(c, d2h(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, c->stream));
+        HIPCHK(c, d2h(c->dict_node.data(), c->d_dict_node.p, 4 * nd, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     c->host_dict_stale = false;
@@ -1477,16 +1483,16 @@ static int sync_host_entries(ad_ctx* c)
         std::vector<uint32_t> xr(ne);
         if (ne)
         {
-            HIPCHK(c, hipMemcpyAsync(ent.data(), c->d_ent.p, 8 * ne, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipMemcpyAsync(K.status.data(), c->d_status.p, ne, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipMemcpyAsync(xr.data(), c->d_xrank.p, 4 * ne, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, d2h(ent.data(), c->d_ent.p, 8 * ne, c->stream));
+            HIPCHK(c, d2h(K.status.data(), c->d_status.p, ne, c->stream));
+            HIPCHK(c, d2h(xr.data(), c->d_xrank.p, 4 * ne, c->stream));
         }
-        if (nk) HIPCHK(c, hipMemcpyAsync(kr.data(), c->d_krec.p, sizeof(KeyRec) * nk, hipMemcpyDeviceToHost, c->stream));
+        if (nk) HIPCHK(c, d2h(kr.data(), c->d_krec.p, sizeof(KeyRec) * nk, c->stream));
         if (K.keys.size() != nk)
         {
             // keys created on the device
             K.keys.resize(nk);
-            if (nk) HIPCHK(c, hipMemcpyAsync(K.keys.data(), c->d_keys.p, 8 * nk, hipMemcpyDeviceToHost, c->stream));
+            if (nk) HIPCHK(c, d2h(K.keys.data(), c->d_keys.p, 8 * nk, c->stream));
             K.seg.assign(nk + 1, 0);
             if (!K.pruned.empty()) K.pruned.assign(nk, -1);
             c->h_pruned.assign(nk, 0);
@@ -1530,8 +1536,8 @@ static int sync_host_entries(ad_ctx* c)
     std::vector<uint32_t> xr(ne);
     if (ne)
     {
-        HIPCHK(c, hipMemcpyAsync(K.status.data(), c->d_status.p, ne, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(xr.data(), c->d_xrank.p, 4 * ne, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, d2h(K.status.data(), c->d_status.p, ne, c->stream));
+        HIPCHK(c, d2h(xr.data(), c->d_xrank.p, 4 * ne, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     for (uint64_t e = 0; e < ne; ++e)
@@ -1711,7 +1717,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         np = q->n_keys;
     else if (n)
     {
-        HIPCHK(c, hipMemcpyAsync(&np, q->key_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, d2h(&np, q->key_off + n, sizeof(uint64_t), st));
         HIPCHK(c, hipStreamSynchronize(st));
     }
     // Range-domain requests (ad_query_soa.range_off): expanded into probes on the device -- keys inside
@@ -1725,8 +1731,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         else
         {
             uint64_t ro[2] = {0, 0};
-            HIPCHK(c, hipMemcpyAsync(&ro[0], q->range_off, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-            HIPCHK(c, hipMemcpyAsync(&ro[1], q->range_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, d2h(&ro[0], q->range_off, sizeof(uint64_t), st));
+            HIPCHK(c, d2h(&ro[1], q->range_off + n, sizeof(uint64_t), st));
             HIPCHK(c, hipStreamSynchronize(st));
             nr = ro[1] - ro[0];
         }
@@ -1742,8 +1748,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                                   c->rq_err.as<uint32_t>(), st));
         HIPCHK(c, run_scan_arrays(c->rq_cnt.as<uint32_t>(), c->rq_off.as<uint64_t>(), n, 1, c->rq_bsum.as<uint64_t>(), st));
         uint64_t tail[2] = {0, 0};
-        HIPCHK(c, hipMemcpyAsync(&tail[0], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipMemcpyAsync(&tail[1], c->rq_err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, d2h(&tail[0], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), st));
+        HIPCHK(c, d2h(&tail[1], c->rq_err.p, sizeof(uint32_t), st));
         HIPCHK(c, hipStreamSynchronize(st));
         if (tail[1])
             return c->fail(AD_E_INVAL, "Range-domain request: keys and ranges together, or ranges not normalised "
@@ -1824,7 +1830,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         h.rng_cap = c->rng_cap;
         h.scr_cap = c->scr_cap;
         h.reg_cap = c->reg_cap;
-        HIPCHK(c, hipMemcpyAsync(b.ctl, &h, sizeof(h), hipMemcpyHostToDevice, st));
+        HIPCHK(c, h2d(b.ctl, &h, sizeof(h), st));
         HIPCHK(c, hipEventRecord(c->ev[0], st));
         uint64_t nd = 0;
         int rc;
@@ -1901,7 +1907,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             HIPCHK(c, hipEventRecord(c->ev[4], st));
             HIPCHK(c, run_pack_lb(b, !parts_only, st));
             HIPCHK(c, hipEventRecord(c->ev[5], st));
-            HIPCHK(c, hipMemcpyAsync(c->h_ctl, b.ctl, sizeof(BatchCtl), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, d2h(c->h_ctl, b.ctl, sizeof(BatchCtl), st));
             HIPCHK(c, hipStreamSynchronize(st));
             h = *c->h_ctl;
             return 0;
@@ -1922,7 +1928,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 HIPCHK(c, run_defer_counts(b, b.deferred, nd, c->s_cnt.as<uint32_t>(), st));
                 HIPCHK(c, run_scan_arrays(c->s_cnt.as<uint32_t>(), c->s_ko.as<uint64_t>(), nd, 1, b.bsum, st));
                 uint64_t snp = 0;
-                HIPCHK(c, hipMemcpyAsync(&snp, c->s_ko.as<uint64_t>() + nd, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+                HIPCHK(c, d2h(&snp, c->s_ko.as<uint64_t>() + nd, sizeof(uint64_t), st));
                 HIPCHK(c, hipStreamSynchronize(st));
                 BatchBufs sb = b;
                 sb.n_txns = nd;
@@ -2058,7 +2064,7 @@ static T* stage_q(ad_ctx* c, DevBuf& b, const T* src, uint64_t n, int* rc)
 {
     if (!src) return nullptr;
     if (!b.ensure(sizeof(T) * std::max<uint64_t>(n, 1))) { *rc = c->fail(AD_E_NOMEM, "query staging"); return nullptr; }
-    if (n && hipMemcpyAsync(b.p, src, sizeof(T) * n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    if (n && h2d(b.p, src, sizeof(T) * n, c->stream) != hipSuccess)
     {
         *rc = c->fail(AD_E_DEVICE, "query H2D");
         return nullptr;
@@ -2272,7 +2278,7 @@ int ad_cfk_load(ad_ctx* c, const ad_cfk_soa* in)
         auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
             if (!b.ensure(std::max<size_t>(bytes, 8))) return c->fail(AD_E_NOMEM, "hipMalloc %zu (snapshot columns)", bytes);
             // ordered on the ctx stream (non-blocking: a null-stream copy would not wait for its kernels)
-            if (bytes) HIPCHK(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+            if (bytes) HIPCHK(c, h2d(b.p, src, bytes, c->stream));
             return 0;
         };
         int rc;
@@ -2486,6 +2492,27 @@ int ad_host_register(ad_ctx* c, void* p, uint64_t bytes)
     return AD_OK;
 }
 
+int ad_host_alloc(uint64_t bytes, void** p)
+{
+    if (!p) return AD_E_INVAL;
+    *p = nullptr;
+    if (!bytes) return AD_E_INVAL;
+    if (hipHostMalloc(p, bytes, hipHostMallocPortable) != hipSuccess)
+    {
+        *p = nullptr;
+        return AD_E_NOMEM;
+    }
+    return AD_OK;
+}
+
+int ad_host_free(void* p)
+{
+    if (!p) return AD_OK;
+    // no copy may still be landing in the pages
+    (void)hipDeviceSynchronize();
+    return hipHostFree(p) == hipSuccess ? AD_OK : AD_E_DEVICE;
+}
+
 int ad_debug_guard_check(char* buf, uint64_t n)
 {
     std::string rep;
@@ -2632,15 +2659,15 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
                     continue;
                 }
                 for (int k = 0; k < 3; ++k)
-                    HIPCHK(c, hipMemcpyAsync(offs[k] + lo, c->off.as<uint64_t>() + (uint64_t)(3 * m + k) * (nc + 1),
-                                             8 * (nc + 1), hipMemcpyDeviceToHost, c->cstream));
+                    HIPCHK(c, d2h(offs[k] + lo, c->off.as<uint64_t>() + (uint64_t)(3 * m + k) * (nc + 1),
+                                             8 * (nc + 1), c->cstream));
                 if (t[3 * m])
-                    HIPCHK(c, hipMemcpyAsync(out->keys[m] + base[3 * m], dev.keys[m], 8 * t[3 * m], hipMemcpyDeviceToHost, c->cstream));
+                    HIPCHK(c, d2h(out->keys[m] + base[3 * m], dev.keys[m], 8 * t[3 * m], c->cstream));
                 if (t[3 * m + 1])
-                    HIPCHK(c, hipMemcpyAsync(out->txns[m] + base[3 * m + 1], dev.txns[m], 4 * t[3 * m + 1], hipMemcpyDeviceToHost,
+                    HIPCHK(c, d2h(out->txns[m] + base[3 * m + 1], dev.txns[m], 4 * t[3 * m + 1],
                                              c->cstream));
                 if (t[3 * m + 2])
-                    HIPCHK(c, hipMemcpyAsync(out->k2t[m] + base[3 * m + 2], dev.k2t[m], 4 * t[3 * m + 2], hipMemcpyDeviceToHost,
+                    HIPCHK(c, d2h(out->k2t[m] + base[3 * m + 2], dev.k2t[m], 4 * t[3 * m + 2],
                                              c->cstream));
             }
             HIPCHK(c, hipEventRecord(c->ev_copied[j & 1], c->cstream));
@@ -2780,8 +2807,8 @@ static int build_recovery_view_device(ad_ctx* c)
     HIPCHK(c, run_scan_arrays(c->rv_cnt.as<uint32_t>(), c->rv_eoff.as<uint64_t>(), ne, 1, c->rv_bsum.as<uint64_t>(), st));
     uint64_t np = 0;
     uint32_t err = 0;
-    HIPCHK(c, hipMemcpyAsync(&np, c->rv_eoff.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(&err, c->rv_err.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, d2h(&np, c->rv_eoff.as<uint64_t>() + ne, 8, st));
+    HIPCHK(c, d2h(&err, c->rv_err.p, 4, st));
     HIPCHK(c, hipStreamSynchronize(st));
     if (err) return c->fail(AD_E_CAPACITY, "more than %u missing ids on one entry", RV_MAX_MISS);
     // per key, its (missing() id, entry) pairs sorted by id (entries ascending within): a stable radix
@@ -3282,7 +3309,7 @@ static int export_sizes(ad_ctx* c, const ad_deps_result* res, const int64_t* txn
     a.rank_ids = id_format == AD_IDS_RANK;      // the dictionary is the global one: ids are global ranks
     a.sz = c->x_sz.as<uint32_t>();
     a.off = c->x_off.as<uint64_t>();
-    HIPCHK(c, hipMemcpyAsync(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(c, h2d(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), st));
     HIPCHK(c, run_export_sizes(a, st));
     HIPCHK(c, run_scan_arrays(a.sz, a.off, n, 1, c->x_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_export_bounds(a, c->x_df.as<uint64_t>(), n_dest, c->x_cnt.as<uint64_t>(), st));
@@ -3309,7 +3336,7 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     ExportArgs a{};
     if (int rc = export_sizes(c, res, txn_index, n_dest, dest_first, out->id_format, st, &a)) return rc;
     std::vector<uint64_t> cnt(4 * (n_dest + 1));
-    HIPCHK(c, hipMemcpyAsync(cnt.data(), c->x_cnt.p, sizeof(uint64_t) * cnt.size(), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, d2h(cnt.data(), c->x_cnt.p, sizeof(uint64_t) * cnt.size(), st));
     HIPCHK(c, hipStreamSynchronize(st));
     out->n_parts = cnt[4 * n_dest + 0];
     out->n_key_words = cnt[4 * n_dest + 1];
@@ -3405,7 +3432,7 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
         a.pdp = c->m_pdp.as<uint32_t>(); a.ppos = c->m_ppos.as<uint32_t>();
     }
     HIPCHK(c, hipEventRecord(c->ev[6], st));
-    HIPCHK(c, hipMemcpyAsync(c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), hipMemcpyHostToDevice, st));
+    HIPCHK(c, h2d(c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), st));
     HIPCHK(c, hipMemsetAsync(a.error, 0, sizeof(uint32_t), st));
     HIPCHK(c, hipMemsetAsync(a.slot, 0xFF, sizeof(int32_t) * std::max<uint64_t>((by_request ? n_owned : G) * n_src, 1), st));
     HIPCHK(c, run_merge_prepare(a, st));
@@ -3439,8 +3466,8 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     if (!by_request)
     {
         // outputs sized from the scanned group sizes (one round trip)
-        HIPCHK(c, hipMemcpyAsync(bases, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, d2h(bases, c->m_bases.p, sizeof(bases), st));
+        HIPCHK(c, d2h(&err, a.error, sizeof(err), st));
         HIPCHK(c, hipStreamSynchronize(st));
         if (err) return malformed(err);
         // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
@@ -3454,8 +3481,8 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     HIPCHK(c, by_request ? run_rmerge_copy(a, c->m_bases.as<uint64_t>(), st)
                          : union_keys ? run_union_emit(a, st) : rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
     HIPCHK(c, hipEventRecord(c->ev[7], st));
-    if (by_request) HIPCHK(c, hipMemcpyAsync(bases, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(&err, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
+    if (by_request) HIPCHK(c, d2h(bases, c->m_bases.p, sizeof(bases), st));
+    HIPCHK(c, d2h(&err, a.error, sizeof(err), st));
     HIPCHK(c, hipStreamSynchronize(st));
     if (err) return malformed(err);
     float ms = 0;
@@ -3571,7 +3598,7 @@ int ad_levels(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, ad_stats* s
     if (g->dep_off && nd && !g->deps) return c->fail(AD_E_INVAL, "ad_levels: null deps");
     auto up = [&](DevBuf& b, const void* src, size_t bytes) -> int {
         if (!b.ensure(std::max<size_t>(bytes, 8))) return c->fail(AD_E_NOMEM, "hipMalloc %zu", bytes);
-        if (bytes) HIPCHK(c, hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, c->stream));
+        if (bytes) HIPCHK(c, h2d(b.p, src, bytes, c->stream));
         return 0;
     };
     int rc;
@@ -3585,7 +3612,7 @@ int ad_levels(ad_ctx* c, const ad_graph_soa* g, uint32_t* level_out, ad_stats* s
                 c->g_ko.as<uint64_t>(), c->g_k.as<int64_t>(), g->dep_off ? c->g_do.as<uint64_t>() : nullptr,
                 g->dep_off ? c->g_d.as<uint32_t>() : nullptr};
     if ((rc = levels_run(c, in, c->g_out.as<uint32_t>(), c->stream, stats))) return rc;
-    HIPCHK(c, hipMemcpyAsync(level_out, c->g_out.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, d2h(level_out, c->g_out.p, 4 * n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return AD_OK;
 }
@@ -3757,7 +3784,7 @@ static int cfk_after_new_keys(ad_ctx* c, const CfkUpdOut& o, hipStream_t st)
 {
     const uint64_t nk = c->ds.n_keys, U = o.n_new_keys;
     std::vector<int64_t> nkeys(U);
-    HIPCHK(c, hipMemcpyAsync(nkeys.data(), o.new_keys, 8 * U, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, d2h(nkeys.data(), o.new_keys, 8 * U, st));
     HIPCHK(c, hipStreamSynchronize(st));
     bool rebuild = false;
     if (int rc = kl_add_keys(c, nkeys, nk, &rebuild)) return rc;
@@ -3820,10 +3847,10 @@ static int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipSt
     c->dict_msb.resize(nd);
     c->dict_lsb.resize(nd);
     c->dict_node.resize(nd);
-    HIPCHK(c, hipMemcpyAsync(pos.data(), pos_dev, 8 * U, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipMemcpyAsync(c->dict_node.data(), c->d_dict_node.p, 4 * nd, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, d2h(pos.data(), pos_dev, 8 * U, st));
+    HIPCHK(c, d2h(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, st));
+    HIPCHK(c, d2h(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, st));
+    HIPCHK(c, d2h(c->dict_node.data(), c->d_dict_node.p, 4 * nd, st));
     HIPCHK(c, hipStreamSynchronize(st));
     auto remap = [&](uint32_t r) -> uint32_t {
         if (r == 0) return 0;
@@ -4392,7 +4419,7 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
         ad_ctx* c = ctxs[i];
         if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
         if (int rc = export_sizes(c, res[i], txn_index[i], n, dest_first[i], fmt, c->stream, &ea[i])) return rc;
-        HIPCHK(c, hipMemcpyAsync(cum[i].data(), c->x_cnt.p, sizeof(uint64_t) * cum[i].size(), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, d2h(cum[i].data(), c->x_cnt.p, sizeof(uint64_t) * cum[i].size(), c->stream));
     }
     // 2. the exchange table, as the RCCL path gathers it
     std::vector<uint64_t> table(RW * n, 0);
@@ -4553,7 +4580,7 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
     // 2. the table: one all-gather of the rows, read back -- the step's planning synchronisation
     ncclResult_t nr = ncclAllGather(mine, tab, RW, ncclUint64, c->comm, st);
     if (nr != ncclSuccess) return x_abort(c, own ? own : nccl_fail(c, nr, "ncclAllGather (exchange table)"));
-    HIPCHK(c, hipMemcpyAsync(h, tab, sizeof(uint64_t) * RW * W, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, d2h(h, tab, sizeof(uint64_t) * RW * W, st));
     HIPCHK(c, hipStreamSynchronize(st));
     // 3. the plan, identical on every rank: a failed or inconsistent rank fails every rank here
     std::vector<ad_xfer> xf(4 * (size_t)W);
@@ -4587,7 +4614,7 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
         if (copy_sync(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
         nr = ncclAllGather(sw, sw + 1, 1, ncclUint64, c->comm, st);
         if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclAllGather (exchange status)"));
-        HIPCHK(c, hipMemcpyAsync(hs + 1, sw + 1, sizeof(uint64_t) * W, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, d2h(hs + 1, sw + 1, sizeof(uint64_t) * W, st));
         HIPCHK(c, hipStreamSynchronize(st));
         if (g) return g;
         for (uint32_t s = 0; s < W; ++s)
@@ -4606,7 +4633,7 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
         if (copy_sync(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
         nr = ncclAllGather(sw, sw + 1, 1, ncclUint64, c->comm, st);
         if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclAllGather (emit status)"));
-        HIPCHK(c, hipMemcpyAsync(hs + 1, sw + 1, sizeof(uint64_t) * W, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, d2h(hs + 1, sw + 1, sizeof(uint64_t) * W, st));
         HIPCHK(c, hipStreamSynchronize(st));
         if (erc) return erc;
         for (uint32_t q = 0; q < W; ++q)
@@ -4814,7 +4841,7 @@ int ad_cfk_byid(ad_ctx* c, uint64_t* n_keys, const int64_t** keys, const uint64_
 static int check_finish(ad_ctx* c, hipStream_t st, uint64_t* n_violations, uint64_t* first)
 {
     uint64_t h[2] = {0, ~0ull};
-    HIPCHK(c, hipMemcpyAsync(h, c->chk.p, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, d2h(h, c->chk.p, sizeof(h), st));
     HIPCHK(c, hipStreamSynchronize(st));
     *n_violations = h[0];
     if (first) *first = h[1];
@@ -4825,7 +4852,7 @@ static int check_begin(ad_ctx* c, hipStream_t st)
 {
     static const uint64_t init[2] = {0, ~0ull};
     if (!c->chk.ensure(sizeof(init))) return c->fail(AD_E_NOMEM, "check counters");
-    HIPCHK(c, hipMemcpyAsync(c->chk.p, init, sizeof(init), hipMemcpyHostToDevice, st));
+    HIPCHK(c, h2d(c->chk.p, init, sizeof(init), st));
     return AD_OK;
 }
 

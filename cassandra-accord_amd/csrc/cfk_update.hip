@@ -1508,7 +1508,7 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
         k_drv_totals<<<1, 64, 0, st>>>(w->bps.as<uint64_t>(), ne, 1, ctl->cm + 1);
         UCHK(hipGetLastError());
     }
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t n_cand = w->h_ctl->tot[0] + w->h_ctl->tot[1] + w->h_ctl->tot[2], ncm = w->h_ctl->tot[3];
     const uint64_t nA = inc ? w->h_ctl->cm[0] : 0, nB = inc ? w->h_ctl->cm[1] : 0;
@@ -1620,7 +1620,7 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
     UALLOC(w->kn_a, 8 * n, false);
     k_key_collect<<<blocks(n), 256, 0, st>>>(s, u, w->kn_a.as<uint64_t>(), ctl);
     UCHK(hipGetLastError());
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t m = w->h_ctl->n_newk;
     if (m == 0) return AD_OK;
@@ -1642,7 +1642,7 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
     k_key_unique<<<blocks(m), 256, 0, st>>>(ks, m, w->kflag.as<uint32_t>());
     UCHK(run_scan_arrays(w->kflag.as<uint32_t>(), w->kfpos.as<uint64_t>(), m, 1, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->kfpos.as<uint64_t>(), m, 1, &ctl->tot3[0]);
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t U = w->h_ctl->tot3[0];
     if (nk + U >= KEY_EMPTY) { *err = "more than 2^32-1 keys"; return AD_E_CAPACITY; }
@@ -1706,9 +1706,9 @@ static int merge_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
     if (int rc = grow.dict_swap(grow.ctx, &nd.hi, &nd.lo, &nd.node, &nd.raw)) { *err = "dictionary merge"; return rc; }
     uint64_t lh = 0, ll = 0;
     int32_t ln = 0;
-    UCHK(hipMemcpyAsync(&lh, nd.hi + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
-    UCHK(hipMemcpyAsync(&ll, nd.lo + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
-    UCHK(hipMemcpyAsync(&ln, nd.node + n0 + U - 1, 4, hipMemcpyDeviceToHost, st));
+    UCHK(d2h(&lh, nd.hi + n0 + U - 1, 8, st));
+    UCHK(d2h(&ll, nd.lo + n0 + U - 1, 8, st));
+    UCHK(d2h(&ln, nd.node + n0 + U - 1, 4, st));
     UCHK(hipStreamSynchronize(st));
     s.dict_hi = nd.hi;
     s.dict_lo = nd.lo;
@@ -1736,7 +1736,7 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
     k_ins_collect<<<blocks(n), 256, 0, st>>>(s, ds, u, w->nw.as<uint64_t>(), cap, w->rk.as<uint32_t>(), ctl);
     if (ndep) k_dep_collect<<<blocks(ndep), 256, 0, st>>>(s, ds, u, ndep, w->nw.as<uint64_t>(), cap, ctl);
     UCHK(hipGetLastError());
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t m = w->h_ctl->n_new;
     if (m == 0) return AD_OK;
@@ -1774,7 +1774,7 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
     k_ins_unique<<<blocks(m), 256, 0, st>>>(vs, m, nw, cap, w->nflag.as<uint32_t>(), ctl);
     UCHK(run_scan_arrays(w->nflag.as<uint32_t>(), w->npos.as<uint64_t>(), m, 1, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->npos.as<uint64_t>(), m, 1, ctl->tot2);
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     if (w->h_ctl->err) return AD_OK;          // reported by the caller
     const uint64_t U = w->h_ctl->tot2[0], n0 = s.n_dict;
@@ -1788,9 +1788,9 @@ static int grow_dictionary(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const 
     UCHK(hipGetLastError());
     uint64_t lh = 0, ll = 0;
     int32_t ln = 0;
-    UCHK(hipMemcpyAsync(&lh, dh + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
-    UCHK(hipMemcpyAsync(&ll, dl + n0 + U - 1, 8, hipMemcpyDeviceToHost, st));
-    UCHK(hipMemcpyAsync(&ln, dn + n0 + U - 1, 4, hipMemcpyDeviceToHost, st));
+    UCHK(d2h(&lh, dh + n0 + U - 1, 8, st));
+    UCHK(d2h(&ll, dl + n0 + U - 1, 8, st));
+    UCHK(d2h(&ln, dn + n0 + U - 1, 4, st));
     UCHK(hipStreamSynchronize(st));
     s.dict_hi = dh;
     s.dict_lo = dl;
@@ -1839,7 +1839,7 @@ static int insert_entries(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const C
     k_ins_gflags<<<blocks(q), 256, 0, st>>>(ks, q, w->gflag.as<uint32_t>());
     UCHK(run_scan_arrays(w->gflag.as<uint32_t>(), w->gs.as<uint64_t>(), q, 1, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->gs.as<uint64_t>(), q, 1, ctl->tot2 + 1);
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t G = w->h_ctl->tot2[1];
     if (ne + G >= (1ull << 32)) { *err = "more than 2^32 CommandsForKey entries"; return AD_E_CAPACITY; }
@@ -1905,7 +1905,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     if (track)
     {
         dev_quiesce();
-        if (hipMemcpy(&ndep, u.dep_off + n, 8, hipMemcpyDeviceToHost) != hipSuccess) { *err = "dep_off"; return AD_E_DEVICE; }
+        if (d2h(&ndep, u.dep_off + n, 8, dev_scope_stream()) != hipSuccess) { *err = "dep_off"; return AD_E_DEVICE; }
         UALLOC(w->uapp, n, false);
         UCHK(hipMemsetAsync(w->uapp.p, 0, n, st));
     }
@@ -2008,7 +2008,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     UCHK(hipGetLastError());
     UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), n, nf, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), n, nf, ctl->tot3);
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     if (w->h_ctl->err)
     {
@@ -2093,7 +2093,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     // ---- 2. re-derive the snapshot arrays from the per-entry state (committed order incrementally)
     if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err, true)) return rollback(rc);
     UCHK(hipEventRecord(w->ev[2], st));
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
@@ -2190,9 +2190,9 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
     UCHK(run_scan_arrays(w->acnt.as<uint32_t>(), w->aoff.as<uint64_t>(), n, 1, w->bsum.as<uint64_t>(), st));
     UCHK(run_scan_arrays(w->lcnt.as<uint32_t>(), w->loff.as<uint64_t>(), n, 1, w->bsum.as<uint64_t>(), st));
     uint64_t na = 0, nl = 0;
-    UCHK(hipMemcpyAsync(&na, w->aoff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
-    UCHK(hipMemcpyAsync(&nl, w->loff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(&na, w->aoff.as<uint64_t>() + n, 8, st));
+    UCHK(d2h(&nl, w->loff.as<uint64_t>() + n, 8, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     if (w->h_ctl->err == UE_UNWITNESSED)
     {
@@ -2277,7 +2277,7 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
                                                 nullptr);
     UCHK(run_scan_arrays(w->mcnt.as<uint32_t>(), w->moff.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
     uint64_t nm = 0;
-    UCHK(hipMemcpyAsync(&nm, w->moff.as<uint64_t>() + ne, 8, hipMemcpyDeviceToHost, st));
+    UCHK(d2h(&nm, w->moff.as<uint64_t>() + ne, 8, st));
     UCHK(hipStreamSynchronize(st));
     uint64_t* noff = nullptr;
     uint32_t* nids = nullptr;
@@ -2476,7 +2476,7 @@ int run_cfk_derive_full(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, CfkDerive
     w->cm_valid = false;
     w->moved = false;
     if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rc;
-    UCHK(hipMemcpyAsync(w->h_ctl, w->ctl.p, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, w->ctl.p, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     if (w->h_ctl->err)
     {
@@ -2537,7 +2537,7 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
     UCHK(hipGetLastError());
     UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), ne, 1, ctl->tot2);
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t R = w->h_ctl->tot2[0];
     if (R == 0)
@@ -2565,7 +2565,7 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
     w->cm_valid = false;          // entry indices changed: the next derivation sorts afresh
     w->moved = false;
     UALLOC(w->chg[w->chg_cur], std::max<uint64_t>(ne - R, 1), false);
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     out->n_keys_pruned = w->h_ctl->tot2[1];
     out->n_removed = R;
@@ -2592,7 +2592,7 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
                                                     nullptr, nullptr);
         UCHK(run_scan_arrays(w->mcnt.as<uint32_t>(), w->moff.as<uint64_t>(), n2, 1, w->bsum.as<uint64_t>(), st));
         uint64_t nm = 0;
-        UCHK(hipMemcpyAsync(&nm, w->moff.as<uint64_t>() + n2, 8, hipMemcpyDeviceToHost, st));
+        UCHK(d2h(&nm, w->moff.as<uint64_t>() + n2, 8, st));
         UCHK(hipStreamSynchronize(st));
         uint64_t* noff = nullptr;
         uint32_t* nids = nullptr;
@@ -2607,7 +2607,7 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
         miss->n_lists = n2;
     }
     UCHK(hipEventRecord(w->ev[1], st));
-    UCHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(UpdCtl), hipMemcpyDeviceToHost, st));
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     float a_ms = 0;
     (void)hipEventElapsedTime(&a_ms, w->ev[0], w->ev[1]);

@@ -4,6 +4,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -38,11 +40,54 @@ Registry& reg()
     return *r;
 }
 
-// the guard band of an allocation of `bytes` at p, compared on the host (after the device is idle)
+// this thread's pinned staging: two chunks, each with the event of its last device use
+constexpr size_t STAGE = 4 << 20;
+struct Staging {
+    void* buf[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    bool ok = false;
+    bool init()
+    {
+        if (ok) return true;
+        for (int k = 0; k < 2; ++k)
+        {
+            if (!buf[k] && hipHostMalloc(&buf[k], STAGE, hipHostMallocPortable) != hipSuccess) return false;
+            if (!ev[k] && hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) return false;
+        }
+        ok = true;
+        return true;
+    }
+    // chunk k free for the host to write / read
+    hipError_t wait(int k)
+    {
+        if (!busy[k]) return hipSuccess;
+        busy[k] = false;
+        return hipEventSynchronize(ev[k]);
+    }
+};
+// per thread and device (a chunk's event belongs to the device of the streams it is recorded on);
+// never freed: a thread's chunks live as long as the process
+constexpr int MAX_DEV = 16;
+thread_local Staging tl_stage[MAX_DEV];
+Staging* staging()
+{
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEV) return nullptr;
+    Staging* S = &tl_stage[d];
+    return S->init() ? S : nullptr;
+}
+
+// the guard band of an allocation of `bytes` at p, compared on the host (after the device is idle).
+// *first_bad = SIZE_MAX when the band could not be read (a device already faulted)
 bool guard_intact(void* p, size_t bytes, size_t* first_bad)
 {
     std::vector<unsigned char> h(GUARD);
-    if (hipMemcpy(h.data(), (char*)p + bytes, GUARD, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (d2h(h.data(), (char*)p + bytes, GUARD, nullptr) != hipSuccess)
+    {
+        *first_bad = SIZE_MAX;
+        return false;
+    }
     for (size_t i = 0; i < GUARD; ++i)
         if (h[i] != PATTERN)
         {
@@ -154,7 +199,8 @@ void dev_free(void* p)
         if (!guard_intact(p, bytes, &at))
         {
             char b[160];
-            snprintf(b, sizeof(b), "freed buffer %p of %zu bytes: guard overwritten at +%zu", p, bytes, at);
+            if (at == SIZE_MAX) snprintf(b, sizeof(b), "freed buffer %p of %zu bytes: guard unreadable (device error)", p, bytes);
+            else snprintf(b, sizeof(b), "freed buffer %p of %zu bytes: guard overwritten at +%zu", p, bytes, at);
             fprintf(stderr, "AD_GUARD: %s\n", b);
             std::lock_guard<std::mutex> g(reg().mu);
             reg().damaged.push_back(b);
@@ -180,13 +226,79 @@ int dev_guard_check(std::string* report)
         if (!guard_intact(p, bytes, &at))
         {
             char b[160];
-            snprintf(b, sizeof(b), "live buffer %p of %zu bytes: guard overwritten at +%zu", p, bytes, at);
+            if (at == SIZE_MAX) snprintf(b, sizeof(b), "live buffer %p of %zu bytes: guard unreadable (device error)", p, bytes);
+            else snprintf(b, sizeof(b), "live buffer %p of %zu bytes: guard overwritten at +%zu", p, bytes, at);
             found.push_back(b);
         }
     }
     if (report)
         for (auto& s : found) *report += s + "\n";
     return (int)found.size();
+}
+
+bool host_pinned(const void* p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess)
+    {
+        (void)hipGetLastError();       // pageable memory: not an error of anything else
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return hipSuccess;
+    if (host_pinned(src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    Staging* Sp = staging();
+    if (!Sp) return hipErrorOutOfMemory;
+    Staging& S = *Sp;
+    int k = 0;
+    for (size_t off = 0; off < bytes; off += STAGE, k ^= 1)
+    {
+        const size_t n = std::min(STAGE, bytes - off);
+        hipError_t e = S.wait(k);
+        if (e != hipSuccess) return e;
+        memcpy(S.buf[k], (const char*)src + off, n);
+        if ((e = hipMemcpyAsync((char*)dst + off, S.buf[k], n, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+        if ((e = hipEventRecord(S.ev[k], st)) != hipSuccess) return e;
+        S.busy[k] = true;
+    }
+    return hipSuccess;
+}
+
+hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return hipSuccess;
+    if (host_pinned(dst)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+    Staging* Sp = staging();
+    if (!Sp) return hipErrorOutOfMemory;
+    Staging& S = *Sp;
+    // chunk i is copied to the host while chunk i + 1 is in flight
+    size_t prev_off = 0, prev_n = 0;
+    int k = 0;
+    hipError_t e = hipSuccess;
+    for (size_t off = 0; off < bytes; off += STAGE, k ^= 1)
+    {
+        const size_t n = std::min(STAGE, bytes - off);
+        if ((e = S.wait(k)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(S.buf[k], (const char*)src + off, n, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipEventRecord(S.ev[k], st)) != hipSuccess) return e;
+        S.busy[k] = true;
+        if (prev_n)
+        {
+            if ((e = S.wait(k ^ 1)) != hipSuccess) return e;
+            memcpy((char*)dst + prev_off, S.buf[k ^ 1], prev_n);
+        }
+        prev_off = off;
+        prev_n = n;
+    }
+    k ^= 1;            // the last chunk issued
+    if ((e = S.wait(k)) != hipSuccess) return e;
+    memcpy((char*)dst + prev_off, S.buf[k], prev_n);
+    return hipSuccess;
 }
 
 }  // namespace adx

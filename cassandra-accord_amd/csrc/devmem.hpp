@@ -30,6 +30,16 @@ hipStream_t dev_scope_stream();                // the scope's first stream (null
 // zero `bytes` at p, ordered on the scope's first stream and complete on return
 hipError_t dev_zero_sync(void* p, size_t bytes);
 int dev_guard_mode();                          // 0 off, 1 guards, 2 guards + poison
+
+// Transfers between the device and host memory. The library never hands pageable host memory to a
+// HIP copy: a host pointer that is not pinned (hipHostMalloc'd or hipHostRegister'ed by the caller)
+// is bounced through this thread's pinned staging chunks with a host memcpy. (Pageable HIP copies were
+// the common factor of the intermittent device faults and host corruption of rounds 3-4 -- DESIGN.md
+// §7.) h2d: `src` may be reused on return, the copy is ordered on `st`. d2h: pinned `dst` -- queued on
+// `st`, like hipMemcpyAsync; pageable `dst` -- complete on return.
+bool host_pinned(const void* p);
+hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t st);
+hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st);
 // damaged guard bands among the live allocations (and the ones freed since the last call); a
 // description of each is appended to *report
 int dev_guard_check(std::string* report);

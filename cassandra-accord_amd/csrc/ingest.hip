@@ -307,7 +307,7 @@ int ingest_dictionary(IngestWork* w, const IngestIn& in, IngestOut& o, hipStream
     if (ne) k_ing_differs<<<nblk(ne), 256, 0, st>>>(in, w->f.as<uint32_t>());
     ICHK(run_scan_arrays(w->f.as<uint32_t>(), w->fpos.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
     ICHK(hipMemcpyAsync(&ctl->n_diff, w->fpos.as<uint64_t>() + ne, 8, hipMemcpyDeviceToDevice, st));
-    ICHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(IngCtl), hipMemcpyDeviceToHost, st));
+    ICHK(d2h(w->h_ctl, ctl, sizeof(IngCtl), st));
     ICHK(hipStreamSynchronize(st));
     const uint64_t nd = w->h_ctl->n_diff, n = ne + nd + in.nx;
     IALLOC(w->hi, 8 * std::max<uint64_t>(n, 1));
@@ -317,7 +317,7 @@ int ingest_dictionary(IngestWork* w, const IngestIn& in, IngestOut& o, hipStream
     IngRec r{w->hi.as<uint64_t>(), w->lo.as<uint64_t>(), w->node.as<int32_t>(), w->lsb.as<uint64_t>()};
     if (n) k_ing_records<<<std::min<unsigned>(nblk(ne + in.nx), ING_RED_BLOCKS), 256, 0, st>>>(in, w->f.as<uint32_t>(), w->fpos.as<uint64_t>(), nd, r, ctl);
     ICHK(hipGetLastError());
-    ICHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(IngCtl), hipMemcpyDeviceToHost, st));
+    ICHK(d2h(w->h_ctl, ctl, sizeof(IngCtl), st));
     ICHK(hipStreamSynchronize(st));
     // 2. LSD over node, lo, hi (digits that vary only)
     IALLOC(w->ka, 8 * std::max<uint64_t>(n, 1));
@@ -355,8 +355,8 @@ int ingest_dictionary(IngestWork* w, const IngestIn& in, IngestOut& o, hipStream
     if (n) k_ing_dict<<<nblk(n), 256, 0, st>>>(so, vcur, n, w->u.as<uint32_t>(), w->upos.as<uint64_t>(), o);
     ICHK(hipGetLastError());
     uint64_t nm = 0;
-    ICHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(IngCtl), hipMemcpyDeviceToHost, st));
-    ICHK(hipMemcpyAsync(&nm, w->upos.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    ICHK(d2h(w->h_ctl, ctl, sizeof(IngCtl), st));
+    ICHK(d2h(&nm, w->upos.as<uint64_t>() + n, 8, st));
     ICHK(hipStreamSynchronize(st));
     *n_dict = nm;
     o.n_diff = nd;
@@ -376,7 +376,7 @@ int ingest_entries(IngestWork* w, const IngestIn& in, const IngestOut& o, hipStr
     if (in.ne) k_ing_entries<<<nblk(in.ne), 256, 0, st>>>(in, w->f.as<uint32_t>(), w->fpos.as<uint64_t>(), o, ctl);
     if (in.nk) k_ing_keys<<<nblk(in.nk), 256, 0, st>>>(in, o, ctl);
     ICHK(hipGetLastError());
-    ICHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(IngCtl), hipMemcpyDeviceToHost, st));
+    ICHK(d2h(w->h_ctl, ctl, sizeof(IngCtl), st));
     ICHK(hipStreamSynchronize(st));
     if (w->h_ctl->code)
     {

@@ -579,8 +579,8 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         if (!e) LV_CHK(hipEventCreate(&e));
 
     // sizes: occurrences = key_off[n] (key_off[0] must be 0)
-    LV_CHK(hipMemcpyAsync(&w->h_u64[0], g.key_off, 8, hipMemcpyDeviceToHost, st));
-    LV_CHK(hipMemcpyAsync(&w->h_u64[1], g.key_off + n, 8, hipMemcpyDeviceToHost, st));
+    LV_CHK(d2h(&w->h_u64[0], g.key_off, 8, st));
+    LV_CHK(d2h(&w->h_u64[1], g.key_off + n, 8, st));
     LV_CHK(hipStreamSynchronize(st));
     if (w->h_u64[0] != 0 || w->h_u64[1] > (1ull << 40))
     {
@@ -636,7 +636,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
 
     // ---- 1. exec ranking: LSD over node, then lowHlc|flags, then msb
     k_exec_words<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, ka, va, ctl);
-    LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
+    LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
     LV_CHK(hipStreamSynchronize(st));
     const uint64_t dx[3] = {w->h_ctl->diff[0], w->h_ctl->diff[1], w->h_ctl->diff[2]};
     uint64_t* kcur = ka;
@@ -662,7 +662,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     if (n_occ)
     {
         k_occ_fill<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, order, w->occ_off.as<uint64_t>(), okey, oval, ctl);
-        LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
+        LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
         LV_CHK(hipStreamSynchronize(st));
         LV_CHK(radix_sort_pairs(okey, oval, kb, vb, n_occ, digits_of(w->h_ctl->diff[3]), hist, off, bsum, st, &okey,
                                 &oval));
@@ -676,8 +676,8 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         k_direct<0><<<blocks_for(n, 256), 256, 0, st>>>(g, w->rank.as<uint32_t>(), indeg, pull ? nullptr : outdeg, nullptr,
                                                         nullptr, nullptr, ctl);
     LV_CHK(run_scan_arrays(pull ? indeg : outdeg, succ_off, n, 1, bsum, st));
-    LV_CHK(hipMemcpyAsync(&w->h_u64[2], succ_off + n, 8, hipMemcpyDeviceToHost, st));
-    LV_CHK(hipMemcpyAsync(w->h_ctl, ctl, sizeof(LevelsCtl), hipMemcpyDeviceToHost, st));
+    LV_CHK(d2h(&w->h_u64[2], succ_off + n, 8, st));
+    LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
     LV_CHK(hipStreamSynchronize(st));
     if (w->h_ctl->error)
     {
@@ -737,7 +737,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
         LV_CHK(hipEventRecord(w->ev[2], st));
         uint32_t tail[3];
-        LV_CHK(hipMemcpyAsync(tail, cnt, sizeof(tail), hipMemcpyDeviceToHost, st));
+        LV_CHK(d2h(tail, cnt, sizeof(tail), st));
         LV_CHK(hipStreamSynchronize(st));
         if (tail[1])
         {
@@ -758,7 +758,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
                                                           indeg, level);
             out->n_launch += STEP_CHUNK;
             LV_CHK(hipGetLastError());
-            LV_CHK(hipMemcpyAsync(&w->h_u64[3], cnt + L, 4, hipMemcpyDeviceToHost, st));
+            LV_CHK(d2h(&w->h_u64[3], cnt + L, 4, st));
             LV_CHK(hipStreamSynchronize(st));
             if ((uint32_t)w->h_u64[3] == 0) break;
             if (L >= n + 1)
@@ -771,7 +771,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         LV_CHK(hipEventRecord(w->ev[2], st));
         // levels = frontiers before the first empty one; every txn must have been levelled
         std::vector<uint32_t> counts(L + 1);
-        LV_CHK(hipMemcpyAsync(counts.data(), cnt, 4 * (L + 1), hipMemcpyDeviceToHost, st));
+        LV_CHK(d2h(counts.data(), cnt, 4 * (L + 1), st));
         LV_CHK(hipStreamSynchronize(st));
         uint64_t total = 0;
         for (uint32_t i = 0; i <= L && counts[i]; ++i)

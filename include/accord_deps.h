@@ -286,6 +286,13 @@ void ad_result_free(ad_deps_result* r);
  * NULL ctx (a registration is process-wide): a finalizer can unpin memory whose ctx is already gone. */
 int ad_host_register(ad_ctx* ctx, void* p, uint64_t bytes);
 int ad_host_unregister(ad_ctx* ctx, void* p);
+/* Pinned host memory allocated by the library (hipHostMalloc, portable, page-aligned): the preferred home
+ * of a caller's reusable query / result arrays -- no registration of the caller's own pages. *p is set
+ * (NULL on failure: AD_E_NOMEM). ad_host_free waits for the device before releasing the pages. Whatever
+ * the caller passes that is neither (pageable memory) is bounced through the library's own pinned
+ * staging, never handed to a pageable HIP copy. */
+int ad_host_alloc(uint64_t bytes, void** p);
+int ad_host_free(void* p);
 
 /* Debug (AD_GUARD=1 or 2 in the environment): device allocations carry guard bands; returns the number
  * of damaged bands found among live allocations and those freed since the last call (0: none, or the
@@ -294,8 +301,9 @@ int ad_debug_guard_check(char* buf, uint64_t n);
 
 /* ad_deps_batch into caller-owned host arrays (the PCIe-facing path a Java host binds): `out`'s array
  * pointers are the caller's -- per map keys_off / txn_off / k2t_off with n_txns + 1 entries each, and
- * keys / txns / k2t with capacities cap[3 m + {0, 1, 2}] (elements); ideally registered
- * (ad_host_register), so that every copy is a DMA. Same results as ad_deps_batch. The batch is resolved
+ * keys / txns / k2t with capacities cap[3 m + {0, 1, 2}] (elements); ideally pinned
+ * (ad_host_alloc, or ad_host_register), so that every copy is a DMA straight into them (pageable arrays
+ * are filled through the library's staging, synchronously). Same results as ad_deps_batch. The batch is resolved
  * in `slices` slices of requests (0: one per 128k requests, at most 4; SEQUENTIAL batches run whole):
  * slice j's result is copied out on a second stream while slice j + 1 is staged and resolved into a
  * second result bank. need[9] receives the sizes the batch needed; when a capacity was too small the

@@ -22,3 +22,7 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b_${TAG}.log
 tail -c 1500 gpurun_out/b_${TAG}.log
 timeout -k 10 300 python -u bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/c5_${TAG}.log 2>&1 || exit 4
 tail -c 1200 gpurun_out/c5_${TAG}.log
+# optional counter passes (PMC=1): lean pass 1's read/write access split
+if [ -n "$PMC" ]; then
+  bash scripts/pmc_split.sh split_${TAG} && python3 scripts/pmc_table.py gpurun_out/pmc_split_${TAG} resolve_lean > gpurun_out/pmc_split_${TAG}.txt
+fi

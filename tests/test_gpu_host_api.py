@@ -95,3 +95,30 @@ def test_into_empty_batch_and_bad_keys():
         assert ei.value.code == A.AD_E_INVAL and ("request %d" % i) in str(ei.value)
     finally:
         st.close()
+
+
+def test_into_registered_outputs():
+    # the Panama binding's way: the caller's own pages pinned with ad_host_register (whole pages), reused
+    # across batches and slicings, then unpinned; same results as the library-pinned outputs
+    w = synth.config2(n_txns=30000, n_keys=20000, n_hist_entries=300000)
+    st = native.DeviceCommandStore(0)
+    try:
+        st.load(w)
+        ref = st.calculate_partial_deps(w.queries)
+        out = None
+        for slices in (1, 3):
+            got, _, out = st.deps_batch_into(w.queries, slices=slices, out=out, pin="register")
+            ok, why = got.equals(ref, detail=True)
+            assert ok, (slices, why)
+        out.release()
+    finally:
+        st.close()
+
+
+def test_host_alloc_contract():
+    import ctypes as C
+    p = C.c_void_p()
+    assert native.lib().ad_host_alloc(0, C.byref(p)) == A.AD_E_INVAL and not p.value
+    assert native.lib().ad_host_alloc(1 << 20, C.byref(p)) == 0 and p.value and p.value % 4096 == 0
+    assert native.lib().ad_host_free(p) == 0
+    assert native.lib().ad_host_free(None) == 0
