@@ -60,13 +60,6 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #ifndef LEAN_MASKED
 #define LEAN_MASKED 1
 #endif
-// LEAN_STAGE: a wave item's keyDeps / directKeyDeps regions are assembled in a per-wave LDS stage and
-// written out by 16-byte stores over consecutive lanes (full lines), from one allocation per item,
-// instead of four lane-scattered stores per map
-#ifndef LEAN_STAGE
-#define LEAN_STAGE 0
-#endif
-
 
 __global__ __launch_bounds__(256) void k_lean_slots(DevSnapshot s, const int64_t* keys, uint64_t np, uint32_t* slot)
 {
@@ -161,15 +154,12 @@ struct LeanChunk {
     // all it leaves) with a few refills per wave. Items done / left come from the wave's item `it`
     // (items it0, it0 + nw, ...) only when a chunk is taken.
     uint32_t cur = 0, end = 0, used = 0;
-    // A16: the allocation starts 16-byte aligned (the staged regions' copy-out stores 16 bytes per lane)
-    template <int PASS, bool A16 = false>
+    template <int PASS>
     __device__ __forceinline__ uint64_t take(BatchCtl* ctl, uint64_t nbytes, uint64_t cap, uint32_t it, uint32_t n_items,
                                              uint32_t nw)
     {
         const uint32_t n8 = (uint32_t)(nbytes >> 3);
-        const uint32_t c = A16 ? ((cur + 1u) & ~1u) : cur;
-        if (c <= end && n8 <= end - c) cur = c;
-        else
+        if (n8 > end - cur)
         {
             // fixed chunks: pass 1's waves write ~50 KB each (config 2), pass 2's ~13 KB
             uint64_t want = LEAN_ADAPT ? LEAN_CHUNK_FIRST : ((PASS == 1 || LEAN_P2_CHUNK_FULL) ? LEAN_CHUNK : LEAN_CHUNK / 4);
@@ -186,13 +176,12 @@ struct LeanChunk {
                 }
             }
             if (LEAN_ADAPT) want = want < LEAN_CHUNK_MIN ? LEAN_CHUNK_MIN : (want > LEAN_CHUNK ? LEAN_CHUNK : want);
-            const uint64_t sz = (nbytes > want ? nbytes : want) + (A16 ? 8u : 0u);
+            const uint64_t sz = nbytes > want ? nbytes : want;
             unsigned long long base = 0;
             if (lane_id() == 0) base = atomicAdd(&ctl->reg_top, (unsigned long long)sz);
             base = uniform64(base);
             if (base + sz > cap && lane_id() == 0) atomicOr(&ctl->overflow, 8u);
             cur = (uint32_t)(base >> 3);
-            if (A16) cur = (cur + 1u) & ~1u;
             end = (uint32_t)((base + sz) >> 3);
         }
         const uint64_t r = (uint64_t)cur << 3;
@@ -277,13 +266,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     // blocks (one atomic per block, no holes)
     __shared__ uint32_t dbuf_all[LEAN_WAVES][DEFER_CHUNK];
     uint32_t* dbuf = dbuf_all[threadIdx.x >> 6];
-    // the region stage (LEAN_STAGE): per map and segment at most 8 keys, LPR txnIds, 8 + LPR k2t entries
-    constexpr bool STG = LEAN_STAGE && !WIDE && !(LEAN_EXP & 4);
-    constexpr uint32_t STG_SEG = 8 * LEAN_MAXP + 4 * LPR + 4 * (LEAN_MAXP + LPR);
-    constexpr uint32_t STG_Q = STG ? (2 * RPW * STG_SEG + 15) / 16 : 1;
-    __shared__ uint4 stg_all[STG ? LEAN_WAVES : 1][STG_Q];
-    uint4* stg4 = stg_all[STG ? (threadIdx.x >> 6) : 0];
-    uint8_t* stg = reinterpret_cast<uint8_t*>(stg4);
     uint32_t dn = 0;            // wave-uniform fill of dbuf
     auto dflush = [&]() {
         if (!dn) return;
@@ -746,7 +728,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         const int64_t key = keyc;
 
         // ---- keyDeps (m = 0) and directKeyDeps (m = 2)
-        uint32_t sv[2][3] = {{0, 0, 0}, {0, 0, 0}}, sso[2] = {0, 0}, scur = 0;     // LEAN_STAGE: sizes, stage offsets
         for (int m = 0; m < 3; m += 2)
         {
             const bool mine = want && (m == 0 ? !is1 : is1);
@@ -754,7 +735,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             const uint32_t tot = __popcll(seg(mb));
             if (mb == 0)
             {
-                if (!STG) put_sizes(act, t, m, 0, 0, 0, 0, false);
+                put_sizes(act, t, m, 0, 0, 0, 0, false);
                 continue;
             }
             // sort (rank, key) per request; dedup -> txnIds; body = unique-rank index per key, ascending
@@ -803,39 +784,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             const uint32_t kstart = __shfl(kstart_l, sb | ka, 64);
             // regions of the wave's requests from one wave-uniform allocation
             const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
-            if (STG)
-            {
-                // the segments' regions in segment order, after the previous map's
-                uint32_t total = 0, mine_off = 0;
-#pragma unroll
-                for (uint32_t k = 0; k < RPW; ++k)
-                {
-                    const uint32_t bk = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bytes, (int)(k * LPR));
-                    if (k == h) mine_off = total;
-                    total += bk;
-                }
-                const uint32_t so = scur + mine_off;
-                scur += total;
-                const int mi = m >> 1;
-                sv[mi][0] = nk;
-                sv[mi][1] = U;
-                sv[mi][2] = nk + tot;
-                sso[mi] = so;
-                if (act && tot)
-                {
-                    int64_t* okeys = reinterpret_cast<int64_t*>(stg + so);
-                    uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
-                    int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
-                    if (hl < 8 && cnt > 0)
-                    {
-                        okeys[kk] = key;
-                        ok2t[kk] = (int32_t)(nk + kstart_l + cnt);
-                    }
-                    if (uniq) otx[ur] = (xr - 1) >> 1;
-                    if (valid) ok2t[nk + kstart + pos_in_key] = (int32_t)ur;
-                }
-                continue;
-            }
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits, it);
             put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
@@ -852,28 +800,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
                 if (uniq) otx[ur] = (xr - 1) >> 1;                  // dictionary index of the TxnId
                 if (valid) ok2t[nk + kstart + pos_in_key] = (int32_t)ur;
             }
-        }
-        if (STG)
-        {
-            // one 16-byte aligned allocation for the item's staged regions, copied out 16 bytes per lane
-            const uint32_t tot16 = (scur + 15u) & ~15u;
-            uint64_t base = 0;
-            bool fits = true;
-            if (tot16)
-            {
-                base = ralloc.template take<PASS, true>(b.ctl, tot16, reg_cap, it, n_items, nw);
-                fits = base + tot16 <= reg_cap;
-            }
-#pragma unroll
-            for (int mi = 0; mi < 2; ++mi)
-                put_sizes(act, t, 2 * mi, fits ? sv[mi][0] : 0, fits ? sv[mi][1] : 0, fits ? sv[mi][2] : 0, base + sso[mi], true);
-            if (tot16 && fits)
-            {
-                wave_lds_sync();
-                for (uint32_t o = (uint32_t)lane; o < tot16 / 16u; o += 64u)
-                    *reinterpret_cast<uint4*>(b.reg + base + 16ull * o) = stg4[o];
-            }
-            wave_lds_sync();
         }
         // ---- rangeDeps (m = 1): (range, txnId) pairs of the cells, STARTED_BEFORE (txnId < S), kind
         // witnessed, not self; unique pairs in (Range.compare, TxnId) order
