@@ -35,7 +35,8 @@ constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 #endif
 constexpr uint32_t LEAN_CHUNK = 1u << LEAN_CHUNK_LOG;   // region bytes a wave takes from the arena at a time
 // measurement switches (scripts/build_variant.sh; results are wrong with any of them set):
-// 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes, 8 no size / offset stores
+// 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes, 8 no size / offset stores,
+// 16 KeyLines from a 512 KB subset of the table (cache-resident; a line counts as the key's)
 #ifndef LEAN_EXP
 #define LEAN_EXP 0
 #endif
@@ -60,6 +61,11 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #ifndef LEAN_MASKED
 #define LEAN_MASKED 1
 #endif
+// LEAN_DPP: the sorting networks and segment scans exchange lanes by DPP / permlane swaps (wave.hpp
+// xor_lane) instead of ds_bpermute
+#ifndef LEAN_DPP
+#define LEAN_DPP 1
+#endif
 
 __global__ __launch_bounds__(256) void k_lean_slots(DevSnapshot s, const int64_t* keys, uint64_t np, uint32_t* slot)
 {
@@ -83,7 +89,7 @@ __device__ __forceinline__ void seg_bitonic(uint32_t& key)
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1)
         {
-            const uint32_t ok = __shfl_xor(key, (int)j, 64);
+            const uint32_t ok = LEAN_DPP ? xor_lane(key, j) : (uint32_t)__shfl_xor(key, (int)j, 64);
             const bool up = (l & k) == 0;
             const bool lower = (l & j) == 0;
             key = (lower == up) ? min(key, ok) : max(key, ok);
@@ -99,7 +105,7 @@ __device__ __forceinline__ void seg_bitonic64(uint64_t& key)
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1)
         {
-            const uint64_t ok = __shfl_xor(key, (int)j, 64);
+            const uint64_t ok = LEAN_DPP ? xor_lane64(key, j) : (uint64_t)__shfl_xor(key, (int)j, 64);
             const bool up = (l & k) == 0;
             const bool lower = (l & j) == 0;
             key = (lower == up) ? min(key, ok) : max(key, ok);
@@ -127,7 +133,17 @@ __device__ __forceinline__ void seg_bitonic_wide(T& x0, T& x1)
             }
             else
             {
-                const T o0 = __shfl_xor(x0, (int)j, 64), o1 = __shfl_xor(x1, (int)j, 64);
+                T o0, o1;
+                if constexpr (sizeof(T) == 4 && LEAN_DPP)
+                {
+                    o0 = xor_lane(x0, j);
+                    o1 = xor_lane(x1, j);
+                }
+                else
+                {
+                    o0 = __shfl_xor(x0, (int)j, 64);
+                    o1 = __shfl_xor(x1, (int)j, 64);
+                }
                 const bool lower = (l & j) == 0;
                 const bool up0 = (l & k) == 0, up1 = ((l + 32) & k) == 0;
                 x0 = (lower == up0) ? min(x0, o0) : max(x0, o0);
@@ -207,7 +223,7 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
 #pragma unroll
     for (uint32_t d = 1; d < 8; d <<= 1)
     {
-        const uint32_t t = __shfl_up(v, d, 8);
+        const uint32_t t = LEAN_DPP ? row_up(v, d) : (uint32_t)__shfl_up(v, d, 8);
         if ((hl & 7) >= d) v += t;
     }
     return v;
@@ -396,7 +412,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         if (QL)
         {
             // lane hl loads quarter hl & 3 of key hl >> 2's line (unmasked: unpacked under the key lane's look)
-            const uint32_t ks = __shfl(look ? H.slot : LS_NONE, (int)(sb | (hl >> 2)), 64);
+            uint32_t ks = __shfl(look ? H.slot : LS_NONE, (int)(sb | (hl >> 2)), 64);
+            if ((LEAN_EXP & 16) && ks != LS_NONE) ks &= 4095u;
             if (!LEAN_MASKED)
                 H.q = reinterpret_cast<const uint4*>(s.kline + (ks != LS_NONE ? ks : 0u))[hl & 3u];
             else
@@ -425,7 +442,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             wave_lds_sync();
         }
         auto key_of = [](const uint4& h0) { return (int64_t)(((uint64_t)h0.y << 32) | h0.x); };
-        found = H.look && (H.h1.w & KL_USED) && key_of(H.h0) == key;
+        found = H.look && (H.h1.w & KL_USED) && ((LEAN_EXP & 16) || key_of(H.h0) == key);
         cb = found ? make_uint2(H.h0.z, H.h0.w) : make_uint2(0, 0);
         if (RNG && H.look && !found && s.cell_off)
         {
@@ -533,7 +550,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 #pragma unroll
         for (uint32_t d = 1; d < 8; d <<= 1)
         {
-            const uint32_t v = __shfl_up(inc, d, 8);
+            const uint32_t v = LEAN_DPP ? row_up(inc, d) : (uint32_t)__shfl_up(inc, d, 8);
             if ((hl & 7) >= d) inc += v;
         }
         const uint32_t start = inc - nn;
@@ -608,9 +625,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
                 seg_bitonic_wide(k0, k1);
                 const bool v0 = hl < tot, v1 = hl + 32 < tot;
                 const uint32_t x0 = k0 >> 3, x1 = k1 >> 3, ka0 = k0 & 7u, ka1 = k1 & 7u;
-                const uint32_t p0 = __shfl_up(k0, 1, LPR);
+                const uint32_t p0 = LEAN_DPP ? wave_up1(k0) : (uint32_t)__shfl_up(k0, 1, LPR);
                 const uint32_t last0 = __shfl(k0, (int)(sb | 31u), 64);
-                const uint32_t up1 = __shfl_up(k1, 1, LPR);         // by every lane (an inactive source reads 0)
+                const uint32_t up1 = LEAN_DPP ? wave_up1(k1) : (uint32_t)__shfl_up(k1, 1, LPR);   // by every lane (an inactive source reads 0)
                 const uint32_t p1 = hl == 0 ? last0 : up1;
                 const bool u0 = v0 && (hl == 0 || (p0 >> 3) != x0);
                 const bool u1 = v1 && (p1 >> 3) != x1;
@@ -641,7 +658,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 #pragma unroll
                 for (uint32_t d = 1; d < 8; d <<= 1)
                 {
-                    const uint32_t v = __shfl_up(cinc, d, 8);
+                    const uint32_t v = LEAN_DPP ? row_up(cinc, d) : (uint32_t)__shfl_up(cinc, d, 8);
                     if ((hl & 7) >= d) cinc += v;
                 }
                 const uint32_t kstart_l = cinc - cnt;
@@ -750,7 +767,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             else seg_bitonic<LPR, LPR>(k);
             const bool valid = hl < tot;
             const uint32_t xr = k >> 3, ka = k & 7u;
-            const uint32_t prev = __shfl_up(k, 1, LPR);
+            const uint32_t prev = LEAN_DPP ? wave_up1(k) : (uint32_t)__shfl_up(k, 1, LPR);
             const bool uniq = valid && (hl == 0 || (prev >> 3) != xr);
             // index of this lane's value among the distinct values: uniques up to and including this
             // lane, minus one (equal values sit in adjacent lanes)
@@ -774,7 +791,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 #pragma unroll
             for (uint32_t d = 1; d < 8; d <<= 1)
             {
-                const uint32_t v = __shfl_up(cinc, d, 8);
+                const uint32_t v = LEAN_DPP ? row_up(cinc, d) : (uint32_t)__shfl_up(cinc, d, 8);
                 if ((hl & 7) >= d) cinc += v;
             }
             const uint32_t kstart_l = cinc - cnt;
@@ -820,7 +837,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             else seg_bitonic64<LPR, LPR>(pk);
             const uint32_t totp = __popcll(seg(rmb));
             const bool pv = hl < totp;
-            const uint64_t pprev = __shfl_up(pk, 1, LPR);
+            const uint64_t pprev = LEAN_DPP ? (((uint64_t)wave_up1((uint32_t)(pk >> 32)) << 32) | wave_up1((uint32_t)pk))
+                                            : (uint64_t)__shfl_up(pk, 1, LPR);
             const bool pu = pv && (hl == 0 || pprev != pk);
             const uint64_t pum = seg(ballot(pu));
             const uint32_t UP = __popcll(pum);
@@ -839,7 +857,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             }
             const bool uplive = hl < UP;
             const uint32_t rid = (uint32_t)(up >> 32), urk = (uint32_t)up;
-            const uint32_t prid = __shfl_up(rid, 1, LPR);
+            const uint32_t prid = LEAN_DPP ? wave_up1(rid) : (uint32_t)__shfl_up(rid, 1, LPR);
             const bool gfirst = uplive && (hl == 0 || prid != rid);
             const uint64_t gm = seg(ballot(gfirst));
             const uint32_t nR = __popcll(gm);
@@ -849,7 +867,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             else if (kmaxr <= 16 || LPR == 16) seg_bitonic64<16, LPR>(k2);
             else if (kmaxr <= 32 || LPR == 32) seg_bitonic64<(LPR < 32 ? LPR : 32), LPR>(k2);
             else seg_bitonic64<LPR, LPR>(k2);
-            const uint64_t p2 = __shfl_up(k2, 1, LPR);
+            const uint64_t p2 = LEAN_DPP ? (((uint64_t)wave_up1((uint32_t)(k2 >> 32)) << 32) | wave_up1((uint32_t)k2))
+                                         : (uint64_t)__shfl_up(k2, 1, LPR);
             const bool v2 = hl < UP;
             const bool uq2 = v2 && (hl == 0 || (uint32_t)(p2 >> 8) != (uint32_t)(k2 >> 8));
             const uint64_t um2 = seg(ballot(uq2));

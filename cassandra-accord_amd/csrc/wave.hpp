@@ -28,6 +28,70 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The value of lane (lane ^ J), J a power of two below 64: DPP quad permutes (J = 1, 2), row shifts
+// (J = 4, 8: the lanes with bit J clear read lane + J, the others lane - J, inside 16-lane rows) and
+// gfx950's permlane16 / permlane32 swaps (J = 16, 32) -- VALU latency instead of a ds_bpermute round
+// trip through the LDS unit. Every lane of the wave must execute it (a disabled source reads 0).
+template <uint32_t J>
+__device__ __forceinline__ uint32_t xor_lane_c(uint32_t v)
+{
+    const int x = (int)v;
+    if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    else if constexpr (J == 4 || J == 8)
+    {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x100 + (int)J, 0xF, 0xF, true);   // row_shl:J
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x110 + (int)J, 0xF, 0xF, true);   // row_shr:J
+        return (__lane_id() & J) ? dn : up;
+    }
+    else if constexpr (J == 16)
+    {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (__lane_id() & 16) ? r[0] : r[1];
+    }
+    else if constexpr (J == 32)
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (__lane_id() & 32) ? r[0] : r[1];
+    }
+    else return (uint32_t)__shfl_xor(x, (int)J, 64);
+}
+// j known after unrolling
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t j)
+{
+    switch (j)
+    {
+        case 1: return xor_lane_c<1>(v);
+        case 2: return xor_lane_c<2>(v);
+        case 4: return xor_lane_c<4>(v);
+        case 8: return xor_lane_c<8>(v);
+        case 16: return xor_lane_c<16>(v);
+        case 32: return xor_lane_c<32>(v);
+        default: return (uint32_t)__shfl_xor((int)v, (int)j, 64);
+    }
+}
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v, uint32_t j)
+{
+    return ((uint64_t)xor_lane((uint32_t)(v >> 32), j) << 32) | xor_lane((uint32_t)v, j);
+}
+// lane - d inside 16-lane rows (d in 1, 2, 4, 8, known after unrolling); lanes with (lane % 16) < d read 0
+__device__ __forceinline__ uint32_t row_up(uint32_t v, uint32_t d)
+{
+    const int x = (int)v;
+    switch (d)
+    {
+        case 1: return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x111, 0xF, 0xF, true);
+        case 2: return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x112, 0xF, 0xF, true);
+        case 4: return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x114, 0xF, 0xF, true);
+        default: return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x118, 0xF, 0xF, true);
+    }
+}
+// lane - 1 over the whole wave (lane 0 reads 0)
+__device__ __forceinline__ uint32_t wave_up1(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);      // wave_shr:1
+}
+
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uniform64(uint64_t v)
 {
