@@ -61,6 +61,11 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #ifndef LEAN_MASKED
 #define LEAN_MASKED 1
 #endif
+// LEAN_RLBC: a segment's lane-p value reaches the segment's lanes by v_readlane per segment and a select
+// (VALU) instead of a ds_bpermute (LDS round trip)
+#ifndef LEAN_RLBC
+#define LEAN_RLBC 0
+#endif
 // LEAN_DPP: the sorting networks and segment scans exchange lanes by DPP / permlane swaps (wave.hpp
 // xor_lane) instead of ds_bpermute
 #ifndef LEAN_DPP
@@ -327,6 +332,18 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         if (hl == 0) r = b.q_rec[t != DEFER_HOLE ? t : 0u];
         return r;
     };
+    // the value of the segment's lane p (p known after unrolling) in every lane of the segment
+    auto seg_lane = [&](uint32_t v, uint32_t p) -> uint32_t {
+        if (!LEAN_RLBC) return (uint32_t)__shfl((int)v, (int)(sb | p), 64);
+        uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p);
+#pragma unroll
+        for (uint32_t k = 1; k < RPW; ++k)
+        {
+            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(k * LPR + p));
+            r = h == k ? x : r;
+        }
+        return r;
+    };
     // the value of lane sb (the segment's first lane) in every lane of the segment
     auto seg_bcast = [&](uint32_t v) -> uint32_t {
         uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
@@ -554,12 +571,12 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
             if ((hl & 7) >= d) inc += v;
         }
         const uint32_t start = inc - nn;
-        const uint32_t T = __shfl(inc, sb | 7u, 64);
+        const uint32_t T = seg_lane(inc, 7u);
         // range raw emissions: the entries of each key's cell
         const uint32_t rn = (RNG && kact) ? cbc.y - cbc.x : 0u;
         const uint32_t rinc = RNG ? key_lanes_incl_scan(rn, hl) : 0u;
         const uint32_t rstart = rinc - rn;
-        const uint32_t TR = RNG ? __shfl(rinc, sb | 7u, 64) : 0u;
+        const uint32_t TR = RNG ? seg_lane(rinc, 7u) : 0u;
         constexpr bool CAN_WIDE = WIDE && RPW == 2 && !RNG;
         defer = defer || seg(ballot(kact && !newest)) != 0 || T > (CAN_WIDE ? 2 * LPR : LPR) || TR > LPR;
         {
@@ -584,7 +601,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 #pragma unroll
                 for (uint32_t p = 1; p < LEAN_MAXP; ++p)
                 {
-                    const uint32_t sp = __shfl(start, sb | p, 64);
+                    const uint32_t sp = seg_lane(start, p);
                     if (p < np && x >= sp) ax = p;
                 }
                 const uint32_t sx = sb | ax;
@@ -696,7 +713,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 #pragma unroll
         for (uint32_t p = 1; p < LEAN_MAXP; ++p)
         {
-            const uint32_t sp = __shfl(start, sb | p, 64);
+            const uint32_t sp = seg_lane(start, p);
             if (p < np && hl >= sp) a = p;
         }
         const uint32_t src = sb | a;
@@ -726,7 +743,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
 #pragma unroll
             for (uint32_t p = 1; p < LEAN_MAXP; ++p)
             {
-                const uint32_t sp = __shfl(rstart, sb | p, 64);
+                const uint32_t sp = seg_lane(rstart, p);
                 if (p < np && hl >= sp) ar = p;
             }
             const uint32_t rsrc = sb | ar;
@@ -910,7 +927,7 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, hipStrea
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG, WIDE, PASS>, 64 * LEAN_WAVES, 0) != hipSuccess ||
             nb <= 0)
             nb = 2;
-        per_cu = std::min(nb, WIDE ? 4 : 5);     // measured: more resident waves only add memory contention
+        per_cu = std::min(nb, WIDE ? 4 : LEAN_OCC);     // measured: more resident waves only add memory contention
         if (const char* e = getenv("AD_LEAN_PER_CU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
