@@ -1545,6 +1545,22 @@ hipError_t run_pack(const BatchBufs& b, hipStream_t st)
 // ---------------------------------------------------------------------------------------
 // scan + pack without a host round trip: reduce -> scan of tile sums -> pack
 // ---------------------------------------------------------------------------------------
+// inclusive prefix of 32-bit sizes over the wave: DPP steps while the wave's sum surely fits 32 bits
+// (every size below 2^25), else the 64-bit shuffle scan
+__device__ __forceinline__ uint64_t wave_size_scan(uint32_t v)
+{
+    if (ballot(v >= (1u << 25)) == 0) return wave_incl_scan_dpp(v);
+    uint64_t x = v;
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
 // Tiles of LB_TILE consecutive requests. k_tile_sums: the 9 size sums of every tile. k_tile_scan
 // (one block): exclusive prefixes of the tile sums and the batch totals (into the control block).
 // k_pack_tiles: a tile scans its 9 size arrays in LDS, adds its tile prefix, writes its offsets and
@@ -1560,13 +1576,14 @@ __global__ __launch_bounds__(LB_TILE) void k_tile_sums(BatchBufs b)
     if (cc->n_deferred || cc->error || (cc->overflow & 15u)) return;
     const uint32_t tid = threadIdx.x, w = tid >> 6, lane = lane_id();
     const uint64_t n = b.n_txns, t = (uint64_t)blockIdx.x * LB_TILE + tid;
-#pragma unroll 1
+    uint32_t v[9];
+#pragma unroll
+    for (int a = 0; a < 9; ++a) v[a] = t < n ? b.sz[(uint64_t)a * n + t] : 0u;     // all in flight together
+#pragma unroll
     for (int a = 0; a < 9; ++a)
     {
-        uint64_t x = t < n ? b.sz[(uint64_t)a * n + t] : 0u;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-        if (lane == 0) s_w[w][a] = x;
+        const uint64_t x = wave_size_scan(v[a]);
+        if (lane == 63) s_w[w][a] = x;
     }
     __syncthreads();
     if (tid < 9)
@@ -1656,14 +1673,8 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
 #pragma unroll
     for (int a = 0; a < 9; ++a)
     {
-        const uint64_t v = vv[a];
-        uint64_t x = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1)
-        {
-            const uint64_t y = __shfl_up(x, d, 64);
-            if ((int)lane >= d) x += y;
-        }
+        const uint32_t v = vv[a];
+        const uint64_t x = wave_size_scan(v);
         s_ex[a][tid] = x - v;
         if (lane == 63) s_wsum[w][a] = x;
     }

@@ -61,6 +61,11 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #ifndef LEAN_MASKED
 #define LEAN_MASKED 1
 #endif
+// LEAN_WIDE1: pass 1 also takes the requests of 33..64 raw emissions (two per lane, the pass-2 path),
+// at pass 2's register budget (4 waves per SIMD); pass 2 then sees only what exceeds 64
+#ifndef LEAN_WIDE1
+#define LEAN_WIDE1 0
+#endif
 // LEAN_RLBC: a segment's lane-p value reaches the segment's lanes by v_readlane per segment and a select
 // (VALU) instead of a ds_bpermute (LDS round trip)
 #ifndef LEAN_RLBC
@@ -950,6 +955,7 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
         }
         if (rpw1 == 8) return s.n_rent ? launch_lean<8, true, false, 1>(s, b, st) : launch_lean<8, false, false, 1>(s, b, st);
         if (rpw1 == 4) return s.n_rent ? launch_lean<4, true, false, 1>(s, b, st) : launch_lean<4, false, false, 1>(s, b, st);
+        if (LEAN_WIDE1 && !s.n_rent) return launch_lean<2, false, true, 1>(s, b, st);
         return s.n_rent ? launch_lean<2, true, false, 1>(s, b, st) : launch_lean<2, false, false, 1>(s, b, st);
     }
     // pass 2 (requests with 33..64 raw emissions): two per wave, two emissions per lane
