@@ -1545,29 +1545,6 @@ hipError_t run_pack(const BatchBufs& b, hipStream_t st)
 // ---------------------------------------------------------------------------------------
 // scan + pack without a host round trip: reduce -> scan of tile sums -> pack
 // ---------------------------------------------------------------------------------------
-// inclusive prefix of 32-bit sizes over the wave: DPP steps while the wave's sum surely fits 32 bits
-// (every size below 2^25), else the 64-bit shuffle scan
-__device__ __forceinline__ uint64_t wave_size_scan(uint32_t v)
-{
-    if (ballot(v >= (1u << 25)) == 0) return wave_incl_scan_dpp(v);
-    uint64_t x = v;
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1)
-    {
-        const uint64_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    return x;
-}
-
-// Tiles of LB_TILE consecutive requests. k_tile_sums: the 9 size sums of every tile. k_tile_scan
-// (one block): exclusive prefixes of the tile sums and the batch totals (into the control block).
-// k_pack_tiles: a tile scans its 9 size arrays in LDS, adds its tile prefix, writes its offsets and
-// packs its requests' regions into the final arrays (64 requests per wave, fully coalesced writes).
-// The output arrays are sized before the launches; a tile whose run would not fit sets OVF_PACK and
-// copies nothing (the host grows them to the totals and runs the pack again). No inter-workgroup
-// waiting: every block streams.
 __global__ __launch_bounds__(LB_TILE) void k_tile_sums(BatchBufs b)
 {
     constexpr uint32_t NW = LB_TILE / 64;
@@ -1582,7 +1559,7 @@ __global__ __launch_bounds__(LB_TILE) void k_tile_sums(BatchBufs b)
 #pragma unroll
     for (int a = 0; a < 9; ++a)
     {
-        const uint64_t x = wave_size_scan(v[a]);
+        const uint64_t x = wave_incl_scan64(v[a]);
         if (lane == 63) s_w[w][a] = x;
     }
     __syncthreads();
@@ -1674,7 +1651,7 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
     for (int a = 0; a < 9; ++a)
     {
         const uint32_t v = vv[a];
-        const uint64_t x = wave_size_scan(v);
+        const uint64_t x = wave_incl_scan64(v);
         s_ex[a][tid] = x - v;
         if (lane == 63) s_wsum[w][a] = x;
     }
@@ -1759,14 +1736,8 @@ constexpr int SCAN_BLOCK = 1024;
 // exclusive scan of v over the block (SCAN_BLOCK threads); *total = the block's sum
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* wsum /* [SCAN_BLOCK/64 + 1] */, uint64_t* total)
 {
-    uint64_t inc = v;
+    const uint64_t inc = wave_incl_scan64(v);
     const int l = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1)
-    {
-        const uint64_t tt = __shfl_up(inc, d, 64);
-        if (l >= d) inc += tt;
-    }
     const int w = threadIdx.x >> 6;
     if (l == 63) wsum[w] = inc;
     __syncthreads();
@@ -1796,10 +1767,8 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t* __re
     __shared__ uint64_t part[SCAN_BLOCK / 64];
     const int a = blockIdx.y;
     const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
-    uint64_t v = i < n ? sz[(uint64_t)a * n + i] : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    if (lane_id() == 0) part[threadIdx.x >> 6] = v;
+    const uint64_t v = wave_incl_scan64(i < n ? sz[(uint64_t)a * n + i] : 0);
+    if (lane_id() == 63) part[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0)
     {

@@ -105,6 +105,21 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x)
     return x;
 }
 
+// inclusive prefix sum of 64-bit values over the 64 lanes: DPP steps in 32 bits while the wave's sum
+// surely fits (every value below 2^25), else the shuffle scan. Every lane must execute it.
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v)
+{
+    if (__ballot(v >= (1ull << 25)) == 0) return wave_incl_scan_dpp((uint32_t)v);
+    const int l = __lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1)
+    {
+        const uint64_t t = __shfl_up(v, d, 64);
+        if (l >= d) v += t;
+    }
+    return v;
+}
+
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint64_t uniform64(uint64_t v)
 {
