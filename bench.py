@@ -34,7 +34,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MI
 STAGES = ["lean resolve pass 1", "deferred requests (split K0..K2)", "prepare (request records: S / self ranks; probe KeyLines for the lean passes)",
           "lean resolve pass 2 (2 requests/wave, 2 emissions/lane)", "offsets scan", "offsets + pack (tile sums, tile scan, scan+pack)",
           "general fused resolve (lean deferrals)"]
-KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, false, 1>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
+# lean pass 1 of a store without range commands at 2 requests per wave runs the wide path (lean.hip LEAN_WIDE1)
+KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, true, 1>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
                    "k_resolve_lean<2u, false, true, 2>", "-", "k_tile_sums+k_tile_scan+k_pack_tiles", "k_resolve"]
 
 
@@ -45,10 +46,11 @@ def kernel_of_stage(i, ranges=False, rpw1=2):
     k = KERNEL_OF_STAGE[i]
     if i == 2:
         return "k_prepare<false>" if ranges else "k_prepare<true>"      # <true>: with the probes' KeyLines
-    if i == 0 and rpw1 in (4, 8):
-        k = k.replace("<2u", "<%du" % rpw1)
-    if ranges and i == 0:
-        return k.replace("false, false, 1>", "true, false, 1>")
+    if i == 0:
+        # <RPW, RNG, WIDE, PASS>: the wide pass-1 path only at 2 requests per wave without range commands
+        rpw = rpw1 if rpw1 in (4, 8) else 2
+        return "k_resolve_lean<%du, %s, %s, 1>" % (rpw, "true" if ranges else "false",
+                                                    "true" if (rpw == 2 and not ranges) else "false")
     if ranges and i == 3:
         return "k_resolve_lean<1u, true, false, 2>"     # range stores: pass 2 one request per wave
     return k

@@ -57,14 +57,17 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #endif
 // LEAN_MASKED: loads move only the data their lanes use -- a request's record by one lane (broadcast by
 // readlane), keys / slots / KeyLine quarters / list elements exec-masked to the lanes that need them --
-// instead of clamped addresses on every lane (the texture data path moves bytes per active lane)
+// instead of clamped addresses on every lane. It cuts L1 accesses per item from 229 to 93 but measured
+// no faster with the ds_bpermute shuffles, and slower with the DPP ones (pass 1 0.462 vs 0.450 ms,
+// pass 2 0.152 vs 0.146: its branches cost the loop's exact wait counts): off
 #ifndef LEAN_MASKED
-#define LEAN_MASKED 1
+#define LEAN_MASKED 0
 #endif
 // LEAN_WIDE1: pass 1 also takes the requests of 33..64 raw emissions (two per lane, the pass-2 path),
-// at pass 2's register budget (4 waves per SIMD); pass 2 then sees only what exceeds 64
+// at pass 2's register budget (4 waves per SIMD); pass 2 then sees only what exceeds 64. Measured on
+// config 2 with unmasked loads: passes 1 + 2 0.596 -> 0.552 ms (pass 1 0.545, pass 2 0.007)
 #ifndef LEAN_WIDE1
-#define LEAN_WIDE1 0
+#define LEAN_WIDE1 1
 #endif
 // LEAN_RLBC: a segment's lane-p value reaches the segment's lanes by v_readlane per segment and a select
 // (VALU) instead of a ds_bpermute (LDS round trip)
