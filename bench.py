@@ -39,10 +39,11 @@ KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, true, 1>", "k_encode_txn+k_probe_k
                    "k_resolve_lean<2u, false, true, 2>", "-", "k_tile_sums+k_tile_scan+k_pack_tiles", "k_resolve"]
 
 
-def kernel_of_stage(i, ranges=False, rpw1=2):
+def kernel_of_stage(i, ranges=False, rpw1=2, wide1=True):
     """Kernel name (as rocprofv3 reports it, namespace and arguments stripped) of pipeline stage i;
     the lean kernels are instantiated with range support when the store has range commands, and lean
-    pass 1 runs four or eight requests per wave for batches of small requests (abi.cpp lean_rpw1)."""
+    pass 1 runs four or eight requests per wave for batches of small requests (abi.cpp lean_rpw1), at
+    two its wide or narrow kernel (abi.cpp lean_wide1; the batch's stats say which ran)."""
     k = KERNEL_OF_STAGE[i]
     if i == 2:
         return "k_prepare<false>" if ranges else "k_prepare<true>"      # <true>: with the probes' KeyLines
@@ -50,7 +51,7 @@ def kernel_of_stage(i, ranges=False, rpw1=2):
         # <RPW, RNG, WIDE, PASS>: the wide pass-1 path only at 2 requests per wave without range commands
         rpw = rpw1 if rpw1 in (4, 8) else 2
         return "k_resolve_lean<%du, %s, %s, 1>" % (rpw, "true" if ranges else "false",
-                                                    "true" if (rpw == 2 and not ranges) else "false")
+                                                    "true" if (rpw == 2 and not ranges and wide1) else "false")
     if ranges and i == 3:
         return "k_resolve_lean<1u, true, false, 2>"     # range stores: pass 2 one request per wave
     return k
@@ -418,10 +419,18 @@ def bench_ranges(args, rank, world, local, dev):
     store.load(w)
     qdev, keep = native.device_queries(w.queries, dev)
     sp = torch.cuda.current_stream(dev).cuda_stream
-    elapsed, all_stats = _timed_steps(args, world, dev, lambda: store.deps_batch_device(qdev, sp)[1])
+    regions = args.output == "regions"     # the headline's output contract (AD_REGIONS) unless --output packed
+    elapsed, all_stats = _timed_steps(args, world, dev, lambda: store.deps_batch_device(qdev, sp, regions=regions)[1])
     stats = all_stats[-1]
     ms = np.mean([st["ms_stage"] for st in all_stats], axis=0)
     pairs = _sum_over_ranks(world, dev, w.queries.n_probes)
+    other = "packed" if regions else "regions"
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        store.deps_batch_device(qdev, sp, regions=not regions)
+    torch.cuda.synchronize(dev)
+    other_ms = 1000.0 * (time.perf_counter() - t0) / 5
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     heads = sum(stats["n_keys"])
     out_bytes = 8 * heads + 4 * (heads + sum(stats["n_pairs"])) + 4 * sum(stats["n_unique"])
@@ -442,7 +451,9 @@ def bench_ranges(args, rank, world, local, dev):
                                "SNAPSHOT%s" % (len(w.queries), len(w.cmds.txn), w.cfk.n_entries,
                                                ", one replica per GPU" if world > 1 else ""),
                    "txns_per_step": len(w.queries) * world, "txn_key_pairs_per_step": pairs,
-                   "parallelism": "replicas x%d" % world},
+                   "parallelism": "replicas x%d" % world,
+                   "output": "regions (AD_REGIONS)" if regions else "packed arrays (request order)"},
+        "%s_ms_per_step" % other: other_ms,
         "roofline": {"bound": "hbm", "kernel": " + ".join(res_kernels), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
                      "algorithmic_bytes_per_launch": alg, "launch_ms": res_ms},
@@ -1178,8 +1189,9 @@ def bench_deps(args, rank, world, local, dev):
     achieved = sbytes[0] / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
     nq = max(1, len(w.queries))
     lean_rpw1 = 4 if w.queries.n_probes <= 3 * nq else 2
-    res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1) for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
-    traffic, traffic_src = measured_traffic(res_kernels, "config%d" % cfg)
+    res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1, wide1=bool(stats.get("lean_wide1", True)))
+                   for i in RESOLVE_STAGES if stage_ms[i] > 0.02]
+    traffic, traffic_src = measured_traffic(res_kernels, "mix" if mix else "config%d" % cfg)   # the same workload's profile
     xdesc = ""
     if world > 1:
         xdesc = (", per-store partials exchanged over RCCL inside libaccord_deps (ad_exchange) + K3 merge on the owning GPU"

@@ -218,6 +218,10 @@ struct ad_ctx {
     hipEvent_t ev_slot = nullptr;      // fused path: after k_prepare
     hipEvent_t ev_lean = nullptr;      // fused path: after k_resolve_lean (both passes)
     hipEvent_t ev_lean1 = nullptr;     // fused path: after lean pass 1
+    // lean pass 1's width for the next batch (lean_wide1): wide while the batches carry enough requests of
+    // 33..64 raw emissions; lean_other = the share of requests the wide pass 1 still deferred
+    bool lean_wide = true, lean_ran_wide = false;
+    double lean_other = 0.0;
     hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;   // split path on the fused kernels' deferrals
     BatchCtl* h_ctl = nullptr;         // pinned mirror of the batch control block
     // ad_deps_batch_into: a second result bank (offsets + packed arrays) so that one slice of a batch is
@@ -697,6 +701,7 @@ static int set_views(ad_ctx* c, uint64_t n_dict, uint64_t n_samp, const NormTid&
     s.ds_lo = c->d_ds_lo.as<uint64_t>();
     s.ds_node = c->d_ds_node.as<int32_t>();
     s.n_samp = n_samp;
+    s.n_samp2 = n_samp ? dict_samples2(n_dict) : 0;    // both build routes fill the second level
     if (n_dict)
     {
         s.dict_last_hi = last.hi;
@@ -882,9 +887,8 @@ static int build_snapshot_device(ad_ctx* c)
         c->d_ballot.release();
     phase("keys");
     // views, the sampled dictionary, the derivation (cand / cwr / w, KeyEntry, trees)
-    const uint64_t n_samp = dict_samples(n_dict);
-    if (!c->d_ds_hi.ensure(8 * std::max<uint64_t>(n_samp, 1)) || !c->d_ds_lo.ensure(8 * std::max<uint64_t>(n_samp, 1)) ||
-        !c->d_ds_node.ensure(4 * std::max<uint64_t>(n_samp, 1)))
+    const uint64_t n_samp = dict_samples(n_dict), n_sent = std::max<uint64_t>(dict_sample_entries(n_dict), 1);
+    if (!c->d_ds_hi.ensure(8 * n_sent) || !c->d_ds_lo.ensure(8 * n_sent) || !c->d_ds_node.ensure(4 * n_sent))
         return c->fail(AD_E_NOMEM, "dictionary sample");
     NormTid last{0, 0, 0};
     if (n_dict)
@@ -1335,6 +1339,17 @@ static int build_snapshot_host(ad_ctx* c)
         slo.push_back(dlo[i]);
         snode.push_back(dnode[i]);
     }
+    const uint64_t n_samp1 = shi.size();
+    // the second level (common.hpp dict_rank_sampled) after the first, from a 16-entry boundary
+    shi.resize(dict_samp2_base(n_samp1));
+    slo.resize(shi.size());
+    snode.resize(shi.size());
+    for (uint64_t i = 0; n_samp1 && i < dhi.size(); i += DICT_SAMP2)
+    {
+        shi.push_back(dhi[i]);
+        slo.push_back(dlo[i]);
+        snode.push_back(dnode[i]);
+    }
     if ((rc = upload(c, c->d_ds_hi, shi)) || (rc = upload(c, c->d_ds_lo, slo)) || (rc = upload(c, c->d_ds_node, snode)))
         return rc;
     if ((rc = upload(c, c->d_dict_hi, dhi)) || (rc = upload(c, c->d_dict_lo, dlo)) || (rc = upload(c, c->d_dict_node, dnode)) ||
@@ -1354,7 +1369,7 @@ static int build_snapshot_host(ad_ctx* c)
         rpv.cell_ok = cell_ok;
         rpv.n_rent = rent.size();
         if (cell_ok) rpv.cell_E = cell_E;
-        if (int rc2 = set_views(c, dhi.size(), shi.size(), last, nk, ne, hcap, rpv, nrb)) return rc2;
+        if (int rc2 = set_views(c, dhi.size(), n_samp1, last, nk, ne, hcap, rpv, nrb)) return rc2;
     }
     HIPCHK(c, build_cfk_trees(s, c->stream));
     HIPCHK(c, build_range_trees(s, c->stream));
@@ -1708,6 +1723,30 @@ static uint32_t lean_rpw1(uint64_t n, uint64_t np)
     return np <= 3 * n ? 4u : 2u;
 }
 
+// Lean pass 1 wide or narrow (rpw 2, no range commands; results identical either way). The wide kernel
+// resolves requests of 33..64 raw emissions in pass 1 but runs at 4 waves per SIMD instead of 5: worth it
+// on config 2 (Zipf keys, ~8 % of requests above 32: 0.613 -> 0.560 ms for passes 1 + 2), not on config
+// 3's store (uniform keys: 0.743 -> 0.841 ms). Chosen from the previous batch of the store: after a wide
+// batch by its share of requests above 32 (BatchCtl.n_wide1); after a narrow one by its pass-2 share less
+// what a wide pass 1 also deferred. AD_LEAN_WIDE1=0/1 forces it.
+constexpr double LEAN_WIDE_SHARE = 0.06;
+static bool lean_wide1(const ad_ctx* c)
+{
+    if (const char* e = getenv("AD_LEAN_WIDE1")) return atoi(e) != 0;
+    return c->lean_wide;
+}
+static void lean_wide1_update(ad_ctx* c, uint64_t n, const BatchCtl& h)
+{
+    if (!n) return;
+    if (c->lean_ran_wide)
+    {
+        c->lean_other = (double)h.n_real1 / (double)n;
+        c->lean_wide = (double)h.n_wide1 / (double)n >= LEAN_WIDE_SHARE;
+    }
+    else
+        c->lean_wide = (double)h.n_real1 / (double)n - c->lean_other >= LEAN_WIDE_SHARE;
+}
+
 static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false,
                         bool n_keys_given = false, int recovery_scan = -1, const RecoveryView* rv = nullptr)
 {
@@ -1834,6 +1873,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipEventRecord(c->ev[0], st));
         uint64_t nd = 0;
         int rc;
+        bool lean_track = false;    // this batch's lean pass 1 feeds lean_wide1_update
         if (recovery_scan >= 0)
         {
             HIPCHK(c, run_recovery(c->ds, *rv, b, (uint32_t)recovery_scan, st));
@@ -1855,9 +1895,13 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 // lean kernel first (newest requests, 2 per wave); the general fused kernel then
                 // takes only what it deferred (count read on the device, no host round trip)
                 if (!c->ev_lean1) HIPCHK(c, hipEventCreate(&c->ev_lean1));
-                HIPCHK(c, run_resolve_lean(c->ds, b, 1, lean_rpw1(n, np), st));
+                const uint32_t rpw1 = lean_rpw1(n, np);
+                const bool wide1 = rpw1 == 2 && !c->ds.n_rent && lean_wide1(c);
+                c->lean_ran_wide = wide1;
+                lean_track = rpw1 == 2 && !c->ds.n_rent;
+                HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
                 HIPCHK(c, hipEventRecord(c->ev_lean1, st));
-                HIPCHK(c, run_resolve_lean(c->ds, b, 2, 0, st));
+                HIPCHK(c, run_resolve_lean(c->ds, b, 2, 0, false, st));
                 HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 BatchBufs b2 = b;
                 b2.req_list = b.deferred2;
@@ -2001,6 +2045,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         S.n_deferred = nd;
         S.n_deferred_lean = lean ? h.n_real2 : 0;     // requests the lean passes left to the general kernel
         S.n_lean_pass2 = lean ? h.n_real1 : 0;        // requests lean pass 1 left to pass 2
+        S.n_launches = lean_track && c->lean_ran_wide ? 1 : 0;   // lean pass 1 ran its wide kernel
+        if (lean_track) lean_wide1_update(c, n, h);
         for (int m = 0; m < 3; ++m)
         {
             S.n_pairs[m] = tot[3 * m + 2] - tot[3 * m + 0];
@@ -4017,15 +4063,17 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
         HIPCHK(c, copy_sync(c->dict_node.data() + nd0, c->d_dict_node.as<int32_t>() + nd0, 4 * add, hipMemcpyDeviceToHost));
         drop_global_dict(c);         // global ranks of the multi-store exchange no longer cover the dictionary
         // the sampled index over the grown dictionary (a stale one is still correct, only slower)
-        const uint64_t ns = dict_samples(c->ds.n_dict);
-        if (c->d_ds_hi.ensure(8 * ns + 8 * ns / 4) && c->d_ds_lo.ensure(8 * ns + 8 * ns / 4) && c->d_ds_node.ensure(4 * ns + 4 * ns / 4))
-        {
-            c->ds.ds_hi = c->d_ds_hi.as<uint64_t>();
-            c->ds.ds_lo = c->d_ds_lo.as<uint64_t>();
-            c->ds.ds_node = c->d_ds_node.as<int32_t>();
-            HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
-            c->ds.n_samp = ns;
-        }
+        // (a buffer that could not grow may have been released: then no sample, the searches span the
+        // whole dictionary)
+        const uint64_t ns = dict_samples(c->ds.n_dict), ne = dict_sample_entries(c->ds.n_dict);
+        const bool ok = c->d_ds_hi.ensure(8 * ne + 8 * ne / 4) && c->d_ds_lo.ensure(8 * ne + 8 * ne / 4) &&
+                        c->d_ds_node.ensure(4 * ne + 4 * ne / 4);
+        c->ds.ds_hi = c->d_ds_hi.as<uint64_t>();
+        c->ds.ds_lo = c->d_ds_lo.as<uint64_t>();
+        c->ds.ds_node = c->d_ds_node.as<int32_t>();
+        c->ds.n_samp = ok ? ns : 0;
+        c->ds.n_samp2 = ok ? dict_samples2(c->ds.n_dict) : 0;
+        if (ok) HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
     }
     if (o.n_inserted) { c->host_moved = true; c->host_ingested = false; }
     if ((rc == 0 || o.rolled_back || o.rederived || o.batch_stood) && c->kline_slots)

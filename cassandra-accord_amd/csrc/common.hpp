@@ -194,10 +194,12 @@ struct DevSnapshot {
     int32_t dict_last_node;
     // every DICT_SAMP-th dictionary id (cache-resident): a rank search touches HBM only inside one
     // DICT_SAMP-id window of the dictionary
+    // (n_samp entries), then from entry dict_samp2_base(n_samp) every DICT_SAMP2-th id (n_samp2
+    // entries, 0 = none): a search then reads one 16-id window of that level and one of the dictionary
     const uint64_t* ds_hi;
     const uint64_t* ds_lo;
     const int32_t*  ds_node;
-    uint64_t n_samp;
+    uint64_t n_samp, n_samp2;
     // CommandsForKey
     uint64_t n_keys;
     const int64_t*  keys;          // [n_keys]
@@ -246,8 +248,13 @@ struct DevSnapshot {
     int elide;
 };
 
-constexpr uint64_t DICT_SAMP = 256;
+constexpr uint64_t DICT_SAMP = 256, DICT_SAMP2 = 16;
 inline uint64_t dict_samples(uint64_t n_dict) { return (n_dict + DICT_SAMP - 1) / DICT_SAMP; }
+inline uint64_t dict_samples2(uint64_t n_dict) { return (n_dict + DICT_SAMP2 - 1) / DICT_SAMP2; }
+// start of the second level in the sample arrays: a whole number of 16-entry (128-byte) windows in
+__host__ __device__ inline uint64_t dict_samp2_base(uint64_t n_samp) { return (n_samp + DICT_SAMP2 - 1) & ~(DICT_SAMP2 - 1); }
+// entries of the sample arrays (both levels) for a dictionary of n_dict ids
+inline uint64_t dict_sample_entries(uint64_t n_dict) { return dict_samp2_base(dict_samples(n_dict)) + dict_samples2(n_dict); }
 
 // Rank of an arbitrary id in the dictionary (member i -> 2i+1, else 2 * lower bound; above every
 // member: 2 * n_dict without a load): binary search of the sample, then of one window.
@@ -268,6 +275,24 @@ __device__ inline uint32_t dict_rank_sampled(const Snap& s, const NormTid& t)
         else b = m;
     }
     uint64_t lo = a ? (a - 1) * DICT_SAMP : 0, hi = a < s.n_samp ? a * DICT_SAMP : s.n_dict;
+    if (s.n_samp2)
+    {
+        // second level: the samples j*DICT_SAMP2 inside [lo, hi) -- one 128-byte window of hi / lo words
+        // -- narrow the window to DICT_SAMP2 ids (pos in [(b-1)*DICT_SAMP2, b*DICT_SAMP2] for b = the
+        // samples <= t; all of them <= t: pos <= hi as before)
+        const uint64_t base = dict_samp2_base(s.n_samp), j0 = lo / DICT_SAMP2;
+        const uint64_t j1 = min((hi + DICT_SAMP2 - 1) / DICT_SAMP2, s.n_samp2);
+        uint64_t c = j0, e = j1;
+        while (c < e)
+        {
+            const uint64_t m = (c + e) >> 1;
+            const NormTid d{s.ds_hi[base + m], s.ds_lo[base + m], s.ds_node[base + m]};
+            if (norm_cmp(d, t) <= 0) c = m + 1;
+            else e = m;
+        }
+        if (c > j0) lo = (c - 1) * DICT_SAMP2;
+        if (c < j1) hi = c * DICT_SAMP2;
+    }
     // the three words of a probe are loaded together (one round trip per level: the ids of a store
     // share their high word, so a hi-first test would wait for a second load almost every level)
     while (lo < hi)

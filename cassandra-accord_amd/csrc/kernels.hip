@@ -1907,19 +1907,24 @@ hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const u
     return hipGetLastError();
 }
 
-__global__ void k_snap_dict_sample(DevSnapshot s, uint64_t* hi, uint64_t* lo, int32_t* node, uint64_t n)
+// both levels: entries [0, n1) every DICT_SAMP-th id, [base2, base2 + n2) every DICT_SAMP2-th
+__global__ void k_snap_dict_sample(DevSnapshot s, uint64_t* hi, uint64_t* lo, int32_t* node, uint64_t n1, uint64_t base2,
+                                   uint64_t n2)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    hi[j] = s.dict_hi[j * DICT_SAMP];
-    lo[j] = s.dict_lo[j * DICT_SAMP];
-    node[j] = s.dict_node[j * DICT_SAMP];
+    uint64_t i;
+    if (j < n1) i = j * DICT_SAMP;
+    else if (j >= base2 && j < base2 + n2) i = (j - base2) * DICT_SAMP2;
+    else return;
+    hi[j] = s.dict_hi[i];
+    lo[j] = s.dict_lo[i];
+    node[j] = s.dict_node[i];
 }
 
 hipError_t run_dict_sample(const DevSnapshot& s, uint64_t* hi, uint64_t* lo, int32_t* node, hipStream_t st)
 {
-    const uint64_t n = dict_samples(s.n_dict);
-    if (n) k_snap_dict_sample<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, hi, lo, node, n);
+    const uint64_t n1 = dict_samples(s.n_dict), base2 = dict_samp2_base(n1), n2 = dict_samples2(s.n_dict);
+    if (n1) k_snap_dict_sample<<<(unsigned)((base2 + n2 + 255) / 256), 256, 0, st>>>(s, hi, lo, node, n1, base2, n2);
     return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ struct BatchCtl {
     unsigned long long n_real1, n_real2;      // requests on those lists
     unsigned long long tot[9];                // totals of the 9 per-request size arrays (after the offsets scan)
     unsigned long long n_big;                 // k_build -> k_build_big: requests with a list family > K2_BIG
+    unsigned long long n_wide1;               // wide lean pass 1: requests it took with 33..64 raw emissions
 };
 constexpr unsigned OVF_PACK = 16u;            // BatchCtl.overflow: a packed output array is too small
 
@@ -162,7 +163,9 @@ constexpr uint32_t DEFER_HOLE = 0xFFFFFFFFu;      // unused slot of a wave's def
 constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave reserves at a time
 constexpr uint32_t REC_FAST = 1u << 24;          // q_rec: lean path applies (<= 8 keys, valid kind, 32-bit key offsets)
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
-hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, hipStream_t st);
+// pass 1 with rpw1 = 2 on a store without range commands: wide1 selects the wide kernel (requests of up to
+// 64 raw emissions) over the narrow one (up to 32; the rest to pass 2)
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, bool wide1, hipStream_t st);
 
 // ---- PreAccept timestamp proposal (preaccept.hip)
 struct DevRangeMap {            // a ReducingRangeMap<Timestamp> in HBM (ad_range_map_soa)
@@ -214,7 +217,7 @@ hipError_t run_key_slots(const int64_t* keys, uint64_t nk, const uint32_t* disp,
                          hipStream_t st);
 hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const uint32_t* kcell, KeyLine* table,
                             uint64_t table_slots, hipStream_t st);
-// every DICT_SAMP-th id of s's dictionary into hi/lo/node (dict_samples(s.n_dict) entries)
+// the two-level sample of s's dictionary into hi/lo/node (dict_sample_entries(s.n_dict) entries)
 hipError_t run_dict_sample(const DevSnapshot& s, uint64_t* hi, uint64_t* lo, int32_t* node, hipStream_t st);
 
 }  // namespace adx

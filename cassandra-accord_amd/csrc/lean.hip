@@ -29,6 +29,11 @@ constexpr int LEAN_WAVES = 4;
 #define LEAN_OCC_N 5
 #endif
 constexpr int LEAN_OCC = LEAN_OCC_N;        // waves per SIMD the register budget is sized for
+// the same for the range-command kernels (RNG): 5 waves per SIMD spill a few registers
+#ifndef LEAN_OCC_RNG
+#define LEAN_OCC_RNG LEAN_OCC_N
+#endif
+template <bool RNG, bool WIDE> constexpr int lean_occ() { return WIDE ? 4 : (RNG ? LEAN_OCC_RNG : LEAN_OCC); }
 constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 #ifndef LEAN_CHUNK_LOG
 #define LEAN_CHUNK_LOG 16
@@ -49,6 +54,13 @@ constexpr uint32_t LEAN_CHUNK = 1u << LEAN_CHUNK_LOG;   // region bytes a wave t
 #define LEAN_SLOTS 1
 #endif
 constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
+// LEAN_XCD: a wave's items (it0, it0 + nw, ...) from its XCD-relabelled block id (wave.hpp xcd_block):
+// consecutive items -- whose request records, keys, size and offset words share cache lines -- run on
+// one XCD's L2 instead of being dealt over all eight
+#ifndef LEAN_XCD
+#define LEAN_XCD 1
+#endif
+__device__ __forceinline__ uint32_t lean_block() { return LEAN_XCD ? xcd_block() : blockIdx.x; }
 // LEAN_QLOAD: a request's KeyLine headers are loaded by all 32 of its lanes, one 16-byte quarter of one
 // key's first 64 bytes per lane (one vector load per item instead of four, each line touched once), and
 // handed to the key lanes through a per-wave LDS stage
@@ -63,12 +75,10 @@ constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
 #ifndef LEAN_MASKED
 #define LEAN_MASKED 0
 #endif
-// LEAN_WIDE1: pass 1 also takes the requests of 33..64 raw emissions (two per lane, the pass-2 path),
-// at pass 2's register budget (4 waves per SIMD); pass 2 then sees only what exceeds 64. Measured on
-// config 2 with unmasked loads: passes 1 + 2 0.596 -> 0.552 ms (pass 1 0.545, pass 2 0.007)
-#ifndef LEAN_WIDE1
-#define LEAN_WIDE1 1
-#endif
+// Wide pass 1 (run_resolve_lean's wide1, chosen per batch by the host): pass 1 also takes the requests of
+// 33..64 raw emissions (two per lane, the pass-2 path), at pass 2's register budget (4 waves per SIMD);
+// pass 2 then sees only what exceeds 64. Measured on config 2: passes 1 + 2 0.613 -> 0.560 ms; on
+// config 3's store (uniform keys, almost nothing above 32) 0.743 -> 0.841 ms
 // LEAN_RLBC: a segment's lane-p value reaches the segment's lanes by v_readlane per segment and a select
 // (VALU) instead of a ds_bpermute (LDS round trip)
 #ifndef LEAN_RLBC
@@ -196,7 +206,7 @@ struct LeanChunk {
             {
                 // in float (few registers on this rarely taken path): items done / left from the stride
                 const float rnw = __builtin_amdgcn_rcpf((float)nw);
-                const float done = (float)(it - uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6))) * rnw;
+                const float done = (float)(it - uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6))) * rnw;
                 if (done >= 1.0f)
                 {
                     const float left = (float)(n_items - it) * rnw + 1.0f;
@@ -248,7 +258,7 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
 // rangeDeps from the cells of its keys (mapReduceRangesInternal, InMemoryCommandStore.java:884-1017).
 // WIDE (RPW 2, no range commands: lean pass 2): requests with up to 64 raw emissions, two per lane.
 template <uint32_t RPW, bool RNG, bool WIDE, int PASS>
-__global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolve_lean(DevSnapshot s, BatchBufs b)
+__global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_resolve_lean(DevSnapshot s, BatchBufs b)
 {
     constexpr uint32_t pass = PASS;
     // pass 1: all requests -> deferred1; pass 2: deferred1 -> deferred2 (lists derived from b
@@ -501,7 +511,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
     // pass 2: item it + 3 nw's deferred1 entry (t3). Every load of a later item is issued after this
     // item's element loads and before its stores, and waited for an iteration later -- no wait of the
     // loop covers the stores just issued (vmcnt counts loads and stores in order).
-    const uint32_t it0 = uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
+    const uint32_t it0 = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6));
     const uint32_t tc = req_of(it0, dload(it0));
     Req qc = derive(tc, loadA(tc));
     int64_t keyc;
@@ -551,6 +561,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         t3 = t4;
     };
 
+    uint32_t nwide = 0;         // wave-uniform: wide pass 1's requests above LPR raw emissions
     for (uint32_t it = it0; it < n_items; it += nw)
     {
         const uint32_t t = qc.t;
@@ -604,6 +615,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         if (CAN_WIDE && seg_max(act && !defer ? T : 0u) > LPR)
         {
             const bool wact = act && !defer;
+            if (PASS == 1) nwide += __popcll(ballot(wact && hl == 0 && T > LPR));
             auto raw_txw = [&](uint32_t x, uint32_t& ax) -> uint32_t {
                 ax = 0;
 #pragma unroll
@@ -923,6 +935,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? 4 : LEAN_OCC) void k_resolv
         rotate(Hn);
     }
     dflush();
+    if (WIDE && PASS == 1 && nwide && lane == 0) atomicAdd(&b.ctl->n_wide1, (unsigned long long)nwide);
 }
 
 template <uint32_t RPW, bool RNG, bool WIDE, int PASS>
@@ -935,7 +948,7 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, hipStrea
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_resolve_lean<RPW, RNG, WIDE, PASS>, 64 * LEAN_WAVES, 0) != hipSuccess ||
             nb <= 0)
             nb = 2;
-        per_cu = std::min(nb, WIDE ? 4 : LEAN_OCC);     // measured: more resident waves only add memory contention
+        per_cu = std::min(nb, lean_occ<RNG, WIDE>());     // measured: more resident waves only add memory contention
         if (const char* e = getenv("AD_LEAN_PER_CU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
@@ -946,7 +959,7 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, hipStrea
 
 // pass 1: every request, two per wave -> D1; pass 2: D1, two per wave with two emissions per lane
 // (one per wave with range commands; up to 64 emissions) -> D2
-hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, hipStream_t st)
+hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, bool wide1, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
     if (pass == 1)
@@ -958,7 +971,7 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
         }
         if (rpw1 == 8) return s.n_rent ? launch_lean<8, true, false, 1>(s, b, st) : launch_lean<8, false, false, 1>(s, b, st);
         if (rpw1 == 4) return s.n_rent ? launch_lean<4, true, false, 1>(s, b, st) : launch_lean<4, false, false, 1>(s, b, st);
-        if (LEAN_WIDE1 && !s.n_rent) return launch_lean<2, false, true, 1>(s, b, st);
+        if (wide1 && !s.n_rent) return launch_lean<2, false, true, 1>(s, b, st);
         return s.n_rent ? launch_lean<2, true, false, 1>(s, b, st) : launch_lean<2, false, false, 1>(s, b, st);
     }
     // pass 2 (requests with 33..64 raw emissions): two per wave, two emissions per lane

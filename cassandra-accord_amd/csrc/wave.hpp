@@ -13,6 +13,15 @@ __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
+// blockIdx.x relabelled so that the blocks of one XCD (blocks are dealt round-robin over the 8 XCDs)
+// hold consecutive ids: work handed out by block id in order then shares L2 lines inside an XCD, not
+// across XCDs. Bijective for any grid size (cdna_hip_programming.md §T1).
+__device__ __forceinline__ uint32_t xcd_block()
+{
+    const uint32_t nwg = gridDim.x, bid = blockIdx.x, x = bid & 7u, q = nwg >> 3, r = nwg & 7u;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
 // number of set bits of m below this lane
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m)
 {

@@ -222,7 +222,8 @@ typedef struct ad_stats {
      * chains, successor CSR), ms_stage[1] frontier loop, and: */
     uint64_t n_levels;               /* 1 + max level                                         */
     uint64_t n_edges;                /* edges of the sparsified waitingOn DAG                  */
-    uint64_t n_launches;             /* frontier-step launches                                */
+    uint64_t n_launches;             /* frontier-step launches; ad_deps_batch*: 1 when lean pass 1
+                                      * ran its wide kernel (up to 64 raw emissions per request) */
     uint64_t n_deferred_lean;        /* ad_deps_batch*: requests the lean passes handed to the general kernel */
     uint64_t n_lean_pass2;           /* ad_deps_batch*: requests lean pass 1 handed to lean pass 2     */
 } ad_stats;

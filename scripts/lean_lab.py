@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4), help="2: the headline batch; 3: bench.py's N = 1 config-3 store; 4: bench.py's config 4")
     ap.add_argument("--regions", action="store_true", help="every library also timed with AD_REGIONS output")
     ap.add_argument("--only", help="time this library alone (no in-tree base run; for counter passes)")
     ap.add_argument("libs", nargs="*")
@@ -64,10 +65,16 @@ def main():
     torch.cuda.set_device(dev)
     t = time.time()
     s = a.scale
-    # bench.py's config-2 batch (bench_deps: config2_sharded for rank 0 of 1)
-    w, _, _ = synth.config2_sharded(0, 1, n_txns_per_gpu=int(1_000_000 * s), n_keys_per_gpu=int(1_000_000 * s),
-                                    n_hist_entries_per_gpu=int(16_000_000 * s))
-    print("config2 generated in %.1f s" % (time.time() - t), file=sys.stderr, flush=True)
+    # bench.py's batches (bench_deps for rank 0 of 1): config2_sharded, or config3_shard without the exchange
+    if a.config == 4:
+        w = synth.config4(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_ranges=max(1, int(100_000 * s)),
+                          n_hist_txns=int(1_000_000 * s), seed=0xACC0D004)
+    elif a.config == 3:
+        w = synth.config3_shard(0, 1, txns_per_gpu=int(8_000_000 * s), keys_per_gpu=int(1_250_000 * s))[0]
+    else:
+        w, _, _ = synth.config2_sharded(0, 1, n_txns_per_gpu=int(1_000_000 * s), n_keys_per_gpu=int(1_000_000 * s),
+                                        n_hist_entries_per_gpu=int(16_000_000 * s))
+    print("config%d generated in %.1f s" % (a.config, time.time() - t), file=sys.stderr, flush=True)
     rng = np.random.default_rng(5)
     sample = np.unique(np.concatenate([np.arange(2000), rng.choice(len(w.queries), 4000, replace=False)]))
     base_lib = os.path.join(ROOT, "cassandra-accord_amd", "accord_deps", "libaccord_deps.so")

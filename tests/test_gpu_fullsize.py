@@ -135,3 +135,36 @@ def test_config4_full(oracle):
     w = synth.config4()
     stats, got = _run_full(w, oracle)
     assert stats["n_pairs"][A.AD_MAP_RANGE] > 0 and got.pair_count(A.AD_MAP_RANGE) > 0
+
+
+def test_config2_full_narrow_pass1(oracle, config2_full, monkeypatch):
+    # lean pass 1's narrow kernel forced (AD_LEAN_WIDE1=0: <= 32 raw emissions per request, the requests
+    # of 33..64 through lean pass 2) -- the same result as the wide kernel of the headline test
+    monkeypatch.setenv("AD_LEAN_WIDE1", "0")
+    stats, got = _run_full(config2_full, oracle)
+    assert not stats["lean_wide1"] and stats["n_lean_pass2"] > 50_000
+
+
+def test_lean_pass1_width_follows_the_batches(oracle, config2_full, monkeypatch):
+    # abi.cpp lean_wide1: a store's first batch runs wide; config 2 (Zipf keys, ~13 % of requests above
+    # 32 raw emissions) stays wide, config 3's store (uniform keys, almost none) turns narrow -- and the
+    # narrow batch's result equals the wide one's
+    import torch
+    monkeypatch.delenv("AD_LEAN_WIDE1", raising=False)
+    dev = torch.device("cuda", 0)
+    w3 = synth.config3_shard(0, 1, txns_per_gpu=1_000_000, keys_per_gpu=160_000)[0]
+    for w, second_wide in ((config2_full, True), (w3, False)):
+        st = native.DeviceCommandStore(device=0, slices=w.slices)
+        try:
+            st.load(w)
+            qdev, keep = native.device_queries(w.queries, dev)
+            res1, s1 = st.deps_batch_device(qdev)
+            torch.cuda.synchronize(dev)
+            a = st.device_result_to_host(res1)
+            res2, s2 = st.deps_batch_device(qdev)
+            torch.cuda.synchronize(dev)
+            assert s1["lean_wide1"] and s2["lean_wide1"] == second_wide, w.name
+            ok, why = st.device_result_to_host(res2).equals(a, detail=True)
+            assert ok, "%s: second batch differs: %s" % (w.name, why)
+        finally:
+            st.close()
