@@ -1869,7 +1869,18 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         h.rng_cap = c->rng_cap;
         h.scr_cap = c->scr_cap;
         h.reg_cap = c->reg_cap;
-        HIPCHK(c, h2d(b.ctl, &h, sizeof(h), st));
+        // the fused path's k_prepare writes the control block itself (one host copy less per batch);
+        // every other path gets it copied
+        if (recovery_scan < 0 && !split_only && n)
+        {
+            b.ctl_init = 1;
+            b.init_cap[0] = h.key_cap;
+            b.init_cap[1] = h.rng_cap;
+            b.init_cap[2] = h.scr_cap;
+            b.init_cap[3] = h.reg_cap;
+        }
+        else
+            HIPCHK(c, h2d(b.ctl, &h, sizeof(h), st));
         HIPCHK(c, hipEventRecord(c->ev[0], st));
         uint64_t nd = 0;
         int rc;
@@ -1886,15 +1897,16 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         }
         else
         {
-            if (!c->ev_slot) HIPCHK(c, hipEventCreate(&c->ev_slot));
-            if (!c->ev_lean) HIPCHK(c, hipEventCreate(&c->ev_lean));
+            if (!c->ev_slot) HIPCHK(c, timing_event(&c->ev_slot));
+            if (!c->ev_lean) HIPCHK(c, timing_event(&c->ev_lean));
             HIPCHK(c, run_prepare(c->ds, b, st));
+            b.ctl_init = 0;
             HIPCHK(c, hipEventRecord(c->ev_slot, st));
             if (lean)
             {
                 // lean kernel first (newest requests, 2 per wave); the general fused kernel then
                 // takes only what it deferred (count read on the device, no host round trip)
-                if (!c->ev_lean1) HIPCHK(c, hipEventCreate(&c->ev_lean1));
+                if (!c->ev_lean1) HIPCHK(c, timing_event(&c->ev_lean1));
                 const uint32_t rpw1 = lean_rpw1(n, np);
                 const bool wide1 = rpw1 == 2 && !c->ds.n_rent && lean_wide1(c);
                 c->lean_ran_wide = wide1;
@@ -1913,8 +1925,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             HIPCHK(c, hipEventRecord(c->ev[1], st));
         }
         if (!c->h_ctl) HIPCHK(c, hipHostMalloc((void**)&c->h_ctl, sizeof(BatchCtl), hipHostMallocDefault));
-        if (!c->ev_sp0) HIPCHK(c, hipEventCreate(&c->ev_sp0));
-        if (!c->ev_sp1) HIPCHK(c, hipEventCreate(&c->ev_sp1));
+        if (!c->ev_sp0) HIPCHK(c, timing_event(&c->ev_sp0));
+        if (!c->ev_sp1) HIPCHK(c, timing_event(&c->ev_sp1));
         // offsets + totals + packed arrays (tile sums, their scan, streaming per-tile scan + pack), the
         // packed arrays sized beforehand (grown to the totals and packed again when too small): the
         // only host round trip of a batch is the final read of the control block
@@ -2259,7 +2271,7 @@ int ad_ctx_create(const ad_config* cfg, ad_ctx** out)
         return AD_E_DEVICE;
     }
     for (auto& ev : c->ev)
-        if ((e = hipEventCreate(&ev)) != hipSuccess)
+        if ((e = timing_event(&ev)) != hipSuccess)
         {
             g_create_err = std::string("ad_ctx_create: hipEventCreate: ") + hipGetErrorString(e);
             delete c;
@@ -4581,7 +4593,7 @@ int ad_comm_init(ad_ctx* c, const uint8_t* id, int rank, int world)
         c->h_xtab_words = words;
     }
     for (hipEvent_t& e : c->x_ev)
-        if (!e) HIPCHK(c, hipEventCreate(&e));
+        if (!e) HIPCHK(c, timing_event(&e));
     ncclUniqueId u;
     memcpy(u.internal, id, AD_COMM_ID_BYTES);
     NCCLCHK(c, ncclCommInitRank(&c->comm, world, u, rank));

@@ -1912,7 +1912,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     if (n >= 0x7FFFFFFFull) { *err = "more than 2^31-2 updates in one batch"; return AD_E_INVAL; }
     if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
     for (auto& e : w->ev)
-        if (!e) UCHK(hipEventCreate(&e));
+        if (!e) UCHK(timing_event(&e));
     auto describe = [&](uint32_t code, uint32_t idx) -> int {
         char b[256];
         const char* what = "";
@@ -2497,7 +2497,7 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
     if (!nk || !ne || !nl) return AD_OK;
     if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
     for (auto& e : w->ev)
-        if (!e) UCHK(hipEventCreate(&e));
+        if (!e) UCHK(timing_event(&e));
     UALLOC(w->ctl, sizeof(UpdCtl), false);
     UpdCtl* ctl = w->ctl.as<UpdCtl>();
     UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));

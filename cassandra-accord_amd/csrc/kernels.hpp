@@ -1,6 +1,7 @@
 // kernels.hpp — host-side launch interface of the gfx950 kernels (kernels.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstddef>
 #include <cstdint>
 
 #include "common.hpp"
@@ -72,7 +73,14 @@ struct BatchBufs {
     uint64_t* lb_agg;                // [9][tiles] size sums per tile (k_tile_sums)
     uint64_t* lb_inc;                // [9][tiles] exclusive prefixes of the tile sums (k_tile_scan)
     BatchCtl* ctl;
+    // fused path: k_prepare's first block writes the control block (zeros and these arena capacities:
+    // key, range, scratch, regions) instead of a host copy before the batch
+    uint32_t ctl_init;
+    uint64_t init_cap[4];
 };
+static_assert(sizeof(BatchCtl) % 8 == 0 && offsetof(BatchCtl, key_cap) == 8 && offsetof(BatchCtl, rng_cap) == 24 &&
+                  offsetof(BatchCtl, scr_cap) == 40 && offsetof(BatchCtl, reg_cap) == 56,
+              "k_prepare's control-block init writes 8-byte words");
 
 // recovery scans: the CommandsForKey entries in load order, for mapReduceFull
 struct RecoveryView {

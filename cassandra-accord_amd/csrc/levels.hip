@@ -789,7 +789,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     if (!w->h_ctl) LV_CHK(hipHostMalloc((void**)&w->h_ctl, sizeof(LevelsCtl), hipHostMallocDefault));
     if (!w->h_u64) LV_CHK(hipHostMalloc((void**)&w->h_u64, 4 * sizeof(uint64_t), hipHostMallocDefault));
     for (auto& e : w->ev)
-        if (!e) LV_CHK(hipEventCreate(&e));
+        if (!e) LV_CHK(timing_event(&e));
 
     // sizes: occurrences = key_off[n] (key_off[0] must be 0)
     LV_CHK(d2h(&w->h_u64[0], g.key_off, 8, st));

@@ -919,6 +919,11 @@ template <bool SLOTS>
 __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b.ctl_init && blockIdx.x == 0 && threadIdx.x < sizeof(BatchCtl) / 8)
+    {
+        const uint32_t i = threadIdx.x;
+        reinterpret_cast<uint64_t*>(b.ctl)[i] = (i & 1) && i < 8 ? b.init_cap[i >> 1] : 0ull;
+    }
     if (SLOTS && t < b.n_probes)
     {
         const int64_t key = b.q_keys[t];
