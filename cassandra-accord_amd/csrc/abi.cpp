@@ -223,6 +223,7 @@ struct ad_ctx {
     bool lean_wide = true, lean_ran_wide = false;
     double lean_other = 0.0;
     hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;   // split path on the fused kernels' deferrals
+    hipEvent_t ev_done = nullptr;      // end of a batch's work (default flags: the host reads what it copied)
     BatchCtl* h_ctl = nullptr;         // pinned mirror of the batch control block
     // ad_deps_batch_into: a second result bank (offsets + packed arrays) so that one slice of a batch is
     // copied out while the next resolves, the copy-out stream and its events
@@ -1747,6 +1748,21 @@ static void lean_wide1_update(ad_ctx* c, uint64_t n, const BatchCtl& h)
         c->lean_wide = (double)h.n_real1 / (double)n - c->lean_other >= LEAN_WIDE_SHARE;
 }
 
+// The wait at the end of a batch (its one host round trip). AD_SPIN_WAIT=1: poll an event recorded
+// behind the control-block copy instead of hipStreamSynchronize (measurement switch: the host's
+// wake-up latency is part of every step).
+static hipError_t batch_wait(ad_ctx* c, hipStream_t st)
+{
+    static const bool spin = getenv("AD_SPIN_WAIT") != nullptr && atoi(getenv("AD_SPIN_WAIT")) != 0;
+    if (!spin) return hipStreamSynchronize(st);
+    if (!c->ev_done)
+        if (hipError_t e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) return e;
+    if (hipError_t e = hipEventRecord(c->ev_done, st)) return e;
+    hipError_t e;
+    while ((e = hipEventQuery(c->ev_done)) == hipErrorNotReady) {}
+    return e;
+}
+
 static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_result* out, bool parts_only = false,
                         bool n_keys_given = false, int recovery_scan = -1, const RecoveryView* rv = nullptr)
 {
@@ -1964,7 +1980,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             HIPCHK(c, run_pack_lb(b, !parts_only, st));
             HIPCHK(c, hipEventRecord(c->ev[5], st));
             HIPCHK(c, d2h(c->h_ctl, b.ctl, sizeof(BatchCtl), st));
-            HIPCHK(c, hipStreamSynchronize(st));
+            HIPCHK(c, batch_wait(c, st));
             h = *c->h_ctl;
             return 0;
         };
@@ -2291,6 +2307,7 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->ev_slot) (void)hipEventDestroy(c->ev_slot);
     if (c->ev_lean) (void)hipEventDestroy(c->ev_lean);
     if (c->ev_lean1) (void)hipEventDestroy(c->ev_lean1);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->ev_sp0) (void)hipEventDestroy(c->ev_sp0);
     if (c->ev_sp1) (void)hipEventDestroy(c->ev_sp1);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
@@ -4671,7 +4688,8 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
         const int g = x_grow(c, send_units, runits, fmt);
         uint64_t* hs = h + RW * W;
         hs[0] = g ? (uint64_t)(-(int64_t)g) : 0;
-        if (copy_sync(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
+        // (hs is pinned: an ordered async copy, read by the all-gather behind it; no host round trip)
+        if (h2d(sw, hs, sizeof(uint64_t), st) != hipSuccess) return x_abort(c, AD_E_DEVICE);
         nr = ncclAllGather(sw, sw + 1, 1, ncclUint64, c->comm, st);
         if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclAllGather (exchange status)"));
         HIPCHK(c, d2h(hs + 1, sw + 1, sizeof(uint64_t) * W, st));
@@ -4690,7 +4708,7 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
     {
         uint64_t* hs = h + RW * W;
         hs[0] = erc ? (uint64_t)(-(int64_t)erc) : 0;
-        if (copy_sync(sw, hs, sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) return x_abort(c, AD_E_DEVICE);
+        if (h2d(sw, hs, sizeof(uint64_t), st) != hipSuccess) return x_abort(c, AD_E_DEVICE);
         nr = ncclAllGather(sw, sw + 1, 1, ncclUint64, c->comm, st);
         if (nr != ncclSuccess) return x_abort(c, nccl_fail(c, nr, "ncclAllGather (emit status)"));
         HIPCHK(c, d2h(hs + 1, sw + 1, sizeof(uint64_t) * W, st));

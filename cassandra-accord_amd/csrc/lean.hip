@@ -33,7 +33,11 @@ constexpr int LEAN_OCC = LEAN_OCC_N;        // waves per SIMD the register budge
 #ifndef LEAN_OCC_RNG
 #define LEAN_OCC_RNG LEAN_OCC_N
 #endif
-template <bool RNG, bool WIDE> constexpr int lean_occ() { return WIDE ? 4 : (RNG ? LEAN_OCC_RNG : LEAN_OCC); }
+// and for the wide kernels (two emissions per lane)
+#ifndef LEAN_OCC_WIDE
+#define LEAN_OCC_WIDE 4
+#endif
+template <bool RNG, bool WIDE> constexpr int lean_occ() { return WIDE ? LEAN_OCC_WIDE : (RNG ? LEAN_OCC_RNG : LEAN_OCC); }
 constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 #ifndef LEAN_CHUNK_LOG
 #define LEAN_CHUNK_LOG 16
