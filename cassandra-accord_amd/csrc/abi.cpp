@@ -1975,8 +1975,11 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             }
             if ((rc = bind_outputs())) return rc;
         }
+        // stage events: the first pack pass is timed from ev[1] (the resolve's end; one event less per
+        // batch -- each record still costs ~4 us of idle GPU), a re-run from its own ev[4]
+        int n_pack = 0;
         auto pack_pass = [&]() -> int {
-            HIPCHK(c, hipEventRecord(c->ev[4], st));
+            if (n_pack++ > 0) HIPCHK(c, hipEventRecord(c->ev[4], st));
             HIPCHK(c, run_pack_lb(b, !parts_only, st));
             HIPCHK(c, hipEventRecord(c->ev[5], st));
             HIPCHK(c, d2h(c->h_ctl, b.ctl, sizeof(BatchCtl), st));
@@ -1984,8 +1987,6 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             h = *c->h_ctl;
             return 0;
         };
-        HIPCHK(c, hipEventRecord(c->ev[2], st));
-        HIPCHK(c, hipEventRecord(c->ev[3], st));
         if ((rc = pack_pass())) return rc;
         double ms_split = 0;
         if (!split_only)
@@ -2082,14 +2083,15 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             S.n_keys[m] = tot[3 * m + 0];
         }
         float ms;
-        const int pairs[4][3] = {{0, 1, 0}, {1, 2, 1}, {2, 3, 4}, {4, 5, 5}};
+        // stage 0: the resolve (ev[0] -> ev[1]); 5: offsets + pack (the last pack pass); 1 and 4 (the gap
+        // before the offsets scan, the scan itself inside the pack pass) are 0 since no event splits them
         double total = 0;
-        for (int i = 0; i < 4; ++i)
-        {
-            HIPCHK(c, hipEventElapsedTime(&ms, c->ev[pairs[i][0]], c->ev[pairs[i][1]]));
-            S.ms_stage[pairs[i][2]] = ms;
-            total += ms;
-        }
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+        S.ms_stage[0] = ms;
+        total += ms;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[n_pack > 1 ? 4 : 1], c->ev[5]));
+        S.ms_stage[5] = ms;
+        total += ms;
         if (!split_only)
         {
             // stage 2: k_prepare; stage 0: k_resolve_lean (or k_resolve when not lean);

@@ -915,6 +915,11 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
 // SLOTS: the same launch also gives every probe its KeyLine for the lean passes (one thread per
 // probe: the slice test, then the perfect hash; 0xFFFFFFFF outside the slices) -- k_lean_slots' work
 // without a launch of its own
+// PREP_PPT probes per thread (block-strided: probe blockIdx.x * 256 * PREP_PPT + j * 256 + tid, each j a
+// coalesced pass), their key and displacement loads issued together
+#ifndef PREP_PPT
+#define PREP_PPT 2
+#endif
 template <bool SLOTS>
 __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 {
@@ -924,14 +929,33 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
         const uint32_t i = threadIdx.x;
         reinterpret_cast<uint64_t*>(b.ctl)[i] = (i & 1) && i < 8 ? b.init_cap[i >> 1] : 0ull;
     }
-    if (SLOTS && t < b.n_probes)
+    if (SLOTS)
     {
-        const int64_t key = b.q_keys[t];
-        bool in = s.n_slices == 0;
-        for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
-        uint32_t r = 0xFFFFFFFFu;
-        if (in) r = (uint32_t)kl_index(key_hash2(key), s.kl_disp[kl_bucket(key_hash(key), s.kl_buckets)], s.kl_lines);
-        b.p_slot[t] = r;
+        const uint64_t p0 = (uint64_t)blockIdx.x * blockDim.x * PREP_PPT + threadIdx.x;
+        int64_t key[PREP_PPT];
+        bool in[PREP_PPT];
+        uint32_t d[PREP_PPT];
+#pragma unroll
+        for (int j = 0; j < PREP_PPT; ++j)
+        {
+            const uint64_t p = p0 + (uint64_t)j * blockDim.x;
+            key[j] = b.q_keys[p < b.n_probes ? p : 0];
+        }
+#pragma unroll
+        for (int j = 0; j < PREP_PPT; ++j)
+        {
+            bool x = s.n_slices == 0;
+            for (uint64_t i = 0; i < s.n_slices && !x; ++i) x = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key[j]);
+            in[j] = x;
+            d[j] = 0;
+            if (x) d[j] = s.kl_disp[kl_bucket(key_hash(key[j]), s.kl_buckets)];
+        }
+#pragma unroll
+        for (int j = 0; j < PREP_PPT; ++j)
+        {
+            const uint64_t p = p0 + (uint64_t)j * blockDim.x;
+            if (p < b.n_probes) b.p_slot[p] = in[j] ? (uint32_t)kl_index(key_hash2(key[j]), d[j], s.kl_lines) : 0xFFFFFFFFu;
+        }
     }
     if (t >= b.n_txns) return;
     // request t's record
@@ -957,7 +981,7 @@ hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (b.p_slot && b.slots_by_prepare)
     {
-        const uint64_t m = std::max<uint64_t>(b.n_txns, b.n_probes);
+        const uint64_t m = std::max<uint64_t>(b.n_txns, (b.n_probes + PREP_PPT - 1) / PREP_PPT);
         if (m) k_prepare<true><<<(unsigned)((m + 255) / 256), 256, 0, st>>>(s, b);
     }
     else if (b.n_txns)
