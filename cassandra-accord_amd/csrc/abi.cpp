@@ -4722,7 +4722,9 @@ int ad_exchange(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_index, 
     if (!erc && hipEventRecord(c->x_ev[1], st) != hipSuccess) erc = c->fail(AD_E_DEVICE, "hipEventRecord");
     // 5b. one-word status all-gather: a rank whose emit failed tells every peer before anyone posts a
     //     send or receive, so the verdict stays collective (no rank waits inside the group for parts
-    //     that never come)
+    //     that never come); a single rank has no peer to tell
+    if (W == 1 && erc) return erc;
+    if (W > 1)
     {
         uint64_t* hs = h + RW * W;
         hs[0] = erc ? (uint64_t)(-(int64_t)erc) : 0;
