@@ -88,11 +88,6 @@ __device__ __forceinline__ uint32_t lean_block() { return LEAN_XCD ? xcd_block()
 #ifndef LEAN_RLBC
 #define LEAN_RLBC 0
 #endif
-// LEAN_PACKA: a lane finds its key from the segment's key starts packed into two words (one DPP OR
-// collection, two lane reads) instead of seven lane reads
-#ifndef LEAN_PACKA
-#define LEAN_PACKA 0
-#endif
 // LEAN_DPP: the sorting networks and segment scans exchange lanes by DPP / permlane swaps (wave.hpp
 // xor_lane) instead of ds_bpermute
 #ifndef LEAN_DPP
@@ -738,42 +733,15 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         }
 
         // ---- one raw emission per lane: element e = hl of key a
-        uint32_t a = 0, a_start;
-        if (LEAN_PACKA && LPR >= 8)
+        uint32_t a = 0;
+#pragma unroll
+        for (uint32_t p = 1; p < LEAN_MAXP; ++p)
         {
-            // the 8 keys' starts as bytes of two words (255 past np), OR-collected over the key lanes
-            // by DPP row shifts and read from the segment's lane 7: two lane reads instead of seven
-            const uint32_t sb8 = hl < np ? min(start, 255u) : 255u;
-            uint32_t plo = hl < 4 ? sb8 << (8 * hl) : 0u;
-            uint32_t phi = (hl >= 4 && hl < 8) ? sb8 << (8 * (hl - 4)) : 0u;
-#pragma unroll
-            for (uint32_t d = 1; d < 8; d <<= 1)
-            {
-                const uint32_t tl = row_up(plo, d), th = row_up(phi, d);
-                if ((hl & 7) >= d) { plo |= tl; phi |= th; }
-            }
-            plo = seg_lane(plo, 7u);
-            phi = seg_lane(phi, 7u);
-#pragma unroll
-            for (uint32_t p = 1; p < LEAN_MAXP; ++p)
-            {
-                const uint32_t sp = p < 4 ? (plo >> (8 * p)) & 0xFFu : (phi >> (8 * (p - 4))) & 0xFFu;
-                if (hl >= sp) a = p;
-            }
-            a_start = a < 4 ? (plo >> (8 * a)) & 0xFFu : (phi >> (8 * (a - 4))) & 0xFFu;
-        }
-        else
-        {
-#pragma unroll
-            for (uint32_t p = 1; p < LEAN_MAXP; ++p)
-            {
-                const uint32_t sp = seg_lane(start, p);
-                if (p < np && hl >= sp) a = p;
-            }
+            const uint32_t sp = seg_lane(start, p);
+            if (p < np && hl >= sp) a = p;
         }
         const uint32_t src = sb | a;
-        if (!(LEAN_PACKA && LPR >= 8)) a_start = __shfl(start, src, 64);
-        const uint32_t a_n1 = __shfl(n1, src, 64);
+        const uint32_t a_start = __shfl(start, src, 64), a_n1 = __shfl(n1, src, 64);
         const uint32_t a_base = __shfl(Hc.h2.y, src, 64), a_ct = __shfl(Hc.h3.x, src, 64), a_lw = __shfl(Hc.h1.z, src, 64);
         const uint32_t a_meta = __shfl(meta, src, 64), a_slot = __shfl(Hc.slot, src, 64);
         const bool live = act && hl < T;
