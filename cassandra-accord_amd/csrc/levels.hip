@@ -713,84 +713,6 @@ __global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* 
     }
 }
 
-// The same dataflow with lanes refilled one by one: a lane that has published its level takes the next
-// rank at once (one ticket add per wave round for every lane that needs one) instead of idling until
-// the wave's slowest lane is done. The lowest unfinished rank is still held by a polling lane, and every
-// wait is on a lower rank, so the argument above holds unchanged.
-__global__ __launch_bounds__(256) void k_level_pull_lane(uint64_t n, const uint64_t* __restrict__ pred_off,
-                                                         const uint32_t* __restrict__ pred, uint32_t* level,
-                                                         uint32_t* ticket, uint32_t* fail, uint64_t budget, uint32_t naps)
-{
-    constexpr uint64_t NONE = ~0ull;
-    const uint32_t lane = lane_id();
-    const uint64_t t_end = wall_clock64() + budget;
-    uint64_t T = NONE, j = 0, e = 0;
-    uint32_t mx = 0;
-    bool waited = false, drained = false;      // drained: the tickets ran past n (wave-uniform)
-    while (true)
-    {
-        const uint64_t need = ballot(T == NONE);
-        if (need && !drained)
-        {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(ticket, (uint32_t)__popcll(need));
-            base = (uint32_t)__shfl((int)base, 0, 64);
-            if (T == NONE)
-            {
-                const uint64_t mine = (uint64_t)base + __popcll(need & ((1ull << lane) - 1));
-                if (mine < n)
-                {
-                    T = mine;
-                    j = pred_off[T];
-                    e = pred_off[T + 1];
-                    mx = 0;
-                    waited = false;
-                }
-            }
-            if ((uint64_t)base + __popcll(need) >= n) drained = true;
-        }
-        if (!ballot(T != NONE)) return;            // drained, and every lane's last rank published
-        bool done = false;
-        if (T != NONE)
-        {
-            bool blocked = false;
-            while (j < e && !blocked)
-            {
-                uint32_t v[PULL_IN_FLIGHT];
-                const uint64_t w = waited ? 1 : PULL_IN_FLIGHT;
-#pragma unroll
-                for (uint32_t k = 0; k < PULL_IN_FLIGHT; ++k)
-                    v[k] = (k < w && j + k < e) ? lv_poll(level + pred[j + k]) : LV_UNSET;
-#pragma unroll
-                for (uint32_t k = 0; k < PULL_IN_FLIGHT; ++k)
-                    if (!blocked && k < w && j < e)
-                    {
-                        if (v[k] == LV_UNSET) blocked = true;
-                        else
-                        {
-                            mx = max(mx, v[k] + 1u);
-                            ++j;
-                        }
-                    }
-                waited = blocked;
-            }
-            if (!blocked)
-            {
-                __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                T = NONE;
-                done = true;
-            }
-        }
-        if (wall_clock64() > t_end)
-        {
-            if (lane == 0) atomicOr(fail, 1u);
-            return;
-        }
-        if (!ballot(done))
-            for (uint32_t z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(4);
-    }
-}
-
 __global__ void k_level_max(const uint32_t* __restrict__ level, uint64_t n, uint32_t* out_max)
 {
     uint32_t v = 0;
@@ -1021,13 +943,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
         const uint64_t budget = (uint64_t)std::max(khz, 1000) * 1000ull;       // one second of wall clock
         const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, (n + threads - 1) / threads);
-        // AD_LEVELS_PULL_LANE=1: lanes refilled one by one (k_level_pull_lane)
-        const bool per_lane = getenv("AD_LEVELS_PULL_LANE") != nullptr && atoi(getenv("AD_LEVELS_PULL_LANE")) != 0;
-        if (per_lane)
-            k_level_pull_lane<<<std::max(1u, grid), threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, budget,
-                                                                      (uint32_t)naps);
-        else
-            k_level_pull<<<std::max(1u, grid), threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, budget, (uint32_t)naps);
+        k_level_pull<<<std::max(1u, grid), threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, budget, (uint32_t)naps);
         LV_CHK(hipGetLastError());
         out->n_launch = 1;
         k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);

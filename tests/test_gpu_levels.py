@@ -22,16 +22,13 @@ def _check(g, oracle):
 
 
 def _scheme(monkeypatch, scheme):
-    # None: the rank-ordered dataflow over a predecessor CSR (k_level_pull, default); "lane": the same
-    # with lanes refilled one by one (k_level_pull_lane); "frontier": the level-synchronous frontier loop
-    # 
+    # None: the rank-ordered dataflow over a predecessor CSR (k_level_pull, default); "frontier": the
+    # level-synchronous frontier loop (the two schemes the library has)
     if scheme == "frontier":
         monkeypatch.setenv("AD_LEVELS_FRONTIER", "1")
-    if scheme == "lane":
-        monkeypatch.setenv("AD_LEVELS_PULL_LANE", "1")
 
 
-@pytest.mark.parametrize("scheme", [None, "lane", "frontier"])
+@pytest.mark.parametrize("scheme", [None, "frontier"])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_graph_all_kinds(oracle, seed, scheme, monkeypatch):
     _scheme(monkeypatch, scheme)
@@ -39,18 +36,16 @@ def test_random_graph_all_kinds(oracle, seed, scheme, monkeypatch):
     _check(g, oracle)
 
 
-@pytest.mark.parametrize("lane", [None, "lane"])
 @pytest.mark.parametrize("per_cu", ["1", "8"])
-def test_pull_occupancy(oracle, per_cu, lane, monkeypatch):
+def test_pull_occupancy(oracle, per_cu, monkeypatch):
     # fewer and more resident waves than the default (every wait still on a lower rank)
-    _scheme(monkeypatch, lane)
     monkeypatch.setenv("AD_LEVELS_PULL_PER_CU", per_cu)
     monkeypatch.setenv("AD_LEVELS_PULL_THREADS", "256")
     g = synth.random_graph(17, n_txns=40_000, n_keys=300, long_runs=True)
     _check(g, oracle)
 
 
-@pytest.mark.parametrize("scheme", ["lane", "frontier"])
+@pytest.mark.parametrize("scheme", ["frontier"])
 def test_config5_full_other_schemes(oracle, scheme, monkeypatch):
     _scheme(monkeypatch, scheme)
     g, _ = synth.config5()
