@@ -1903,6 +1903,10 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         uint64_t nd = 0;
         int rc;
         bool lean_track = false;    // this batch's lean pass 1 feeds lean_wide1_update
+        // the fused path's stage split (prepare, lean pass 1, pass 2, general kernel) costs three more
+        // event records (~4 us of idle GPU each); without AD_STAGE_EVENTS=1 stage 0 holds the whole resolve
+        const char* se = getenv("AD_STAGE_EVENTS");
+        const bool split_stages = se && atoi(se) != 0;
         if (recovery_scan >= 0)
         {
             HIPCHK(c, run_recovery(c->ds, *rv, b, (uint32_t)recovery_scan, st));
@@ -1919,7 +1923,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             if (!c->ev_lean) HIPCHK(c, timing_event(&c->ev_lean));
             HIPCHK(c, run_prepare(c->ds, b, st));
             b.ctl_init = 0;
-            HIPCHK(c, hipEventRecord(c->ev_slot, st));
+            if (split_stages) HIPCHK(c, hipEventRecord(c->ev_slot, st));
             if (lean)
             {
                 // lean kernel first (newest requests, 2 per wave); the general fused kernel then
@@ -1930,9 +1934,9 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 c->lean_ran_wide = wide1;
                 lean_track = rpw1 == 2 && !c->ds.n_rent;
                 HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
-                HIPCHK(c, hipEventRecord(c->ev_lean1, st));
+                if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
                 HIPCHK(c, run_resolve_lean(c->ds, b, 2, 0, false, st));
-                HIPCHK(c, hipEventRecord(c->ev_lean, st));
+                if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 BatchBufs b2 = b;
                 b2.req_list = b.deferred2;
                 b2.req_count = &b.ctl->n_deferred2;
@@ -2094,7 +2098,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev[n_pack > 1 ? 4 : 1], c->ev[5]));
         S.ms_stage[5] = ms;
         total += ms;
-        if (!split_only)
+        if (!split_only && split_stages)
         {
             // stage 2: k_prepare; stage 0: k_resolve_lean (or k_resolve when not lean);
             // stage 3: k_resolve over the lean kernel's deferrals

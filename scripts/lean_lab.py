@@ -17,6 +17,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "cassandra-accord_amd"))
 
+os.environ.setdefault("AD_STAGE_EVENTS", "1")     # per-kernel stage times (abi.cpp split_stages)
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
