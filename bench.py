@@ -432,11 +432,11 @@ def bench_ranges(args, rank, world, local, dev):
     torch.cuda.synchronize(dev)
     other_ms = 1000.0 * (time.perf_counter() - t0) / 5
     # the per-kernel split from three steps with the library's extra stage events (see bench_deps)
-    split_ms = np.zeros(8)
+    split_ms = np.zeros(7)
     os.environ["AD_STAGE_EVENTS"] = "1"
     try:
         for _ in range(3):
-            split_ms += np.array(store.deps_batch_device(qdev, sp, regions=regions)[1]["ms_stage"][:8]) / 3
+            split_ms += np.array(store.deps_batch_device(qdev, sp, regions=regions)[1]["ms_stage"][:7]) / 3
     finally:
         del os.environ["AD_STAGE_EVENTS"]
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
