@@ -215,7 +215,10 @@ typedef struct ad_stats {
     /* per-stage device time (HIP events): 0 encode (K0), 1 conflict scan (K1), 2 range probe
      * (K4), 3 build sizing (K2 pass 1), 4 offsets scan, 5 build emit (K2 pass 2) */
     double   ms_stage[8];            /* path 0: 0 fused resolve, 1 deferred requests (split),
-                                      * 4 offsets, 5 pack */
+                                      * 5 offsets + pack; with AD_STAGE_EVENTS=1 in the environment
+                                      * the resolve is split further: 2 k_prepare, 0 lean pass 1,
+                                      * 3 lean pass 2, 6 general kernel (three more event records,
+                                      * ~4 us of idle GPU each, so off by default) */
     uint64_t n_deferred;             /* requests resolved by the split kernels (path 0)       */
     uint64_t bytes_stage[8];         /* algorithmic bytes per stage            */
     /* ad_levels: n_txns, n_probes = txn-key occurrences, ms_stage[0] build (exec ranking, key
