@@ -266,24 +266,7 @@ __device__ inline uint32_t dict_rank_sampled(const Snap& s, const NormTid& t)
     const int cl = norm_cmp(last, t);
     if (cl < 0) return (uint32_t)(2 * s.n_dict);
     if (cl == 0) return (uint32_t)(2 * s.n_dict - 1);
-    // first level, 8-ary: seven independent pivot loads per round instead of one dependent load per
-    // halving (the sample is cache-resident, so the search is a chain of cache latencies)
     uint64_t a = 0, b = s.n_samp;
-    while (b - a > 8)
-    {
-        const uint64_t step = (b - a + 7) >> 3;
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t i = 1; i < 8; ++i)
-        {
-            const uint64_t p = a + step * i;
-            const uint64_t q = p < b ? p : a;
-            const NormTid d{s.ds_hi[q], s.ds_lo[q], s.ds_node[q]};
-            if (p < b && norm_cmp(d, t) <= 0) k = i;
-        }
-        a += step * k;                      // sample a <= t when k > 0
-        b = min(b, a + step);
-    }
     while (a < b)
     {
         const uint64_t m = (a + b) >> 1;
