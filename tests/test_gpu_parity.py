@@ -54,6 +54,17 @@ def test_big_requests_regions(oracle, big, monkeypatch):
     assert ok, why
 
 
+@pytest.mark.parametrize("n_hist", [7, 15, 16, 17, 120, 255, 256, 257, 511, 4097])
+def test_dictionary_sample_windows(oracle, n_hist):
+    # rank searches through the two-level dictionary sample (common.hpp dict_rank_sampled: every 256th
+    # id, then every 16th inside that window, then 16 ids) around the windows' edges: half the requests
+    # are Accepts (S = a proposed executeAt the store may hold, self = a txnId it holds), a fifth of the
+    # executeAts lie below their txnIds
+    w = synth.random_small(3000 + n_hist, n_keys=30, n_hist_txns=n_hist, n_txns=200, accept_frac=0.5,
+                           exec_below_frac=0.2, n_range_cmds=0, n_redundant=0)
+    _compare(w, oracle)
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_small_no_elision(oracle, seed):
     _compare(synth.random_small(100 + seed), oracle, elide=0)
