@@ -239,6 +239,18 @@ class RangeCommands:
         return RangeCommands(Tids(z64, z64, np.zeros(0, np.int32)), np.zeros(1, np.uint64),
                              np.zeros(0, np.int64), np.zeros(0, np.int64))
 
+    def take(self, idx):
+        """The commands idx (ascending), their ranges with them (recovery facts dropped)."""
+        idx = np.asarray(idx, np.int64)
+        o = self.range_off.astype(np.int64)
+        cnt = o[idx + 1] - o[idx]
+        off = np.zeros(len(idx) + 1, np.uint64)
+        off[1:] = np.cumsum(cnt)
+        src = np.repeat(o[idx] - off[:-1].astype(np.int64), cnt) + np.arange(int(off[-1]))
+        sel = lambda a: None if a is None else a[idx]  # noqa: E731
+        return RangeCommands(self.txn.take(idx), off, self.range_start[src], self.range_end[src], sel(self.erased),
+                             sel(self.historical))
+
 
 @dataclass
 class Redundant:

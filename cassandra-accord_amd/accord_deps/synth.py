@@ -856,6 +856,27 @@ def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_rang
                     slices=slices)
 
 
+def sequential_ranges(seed, range_frac=0.4, **kw):
+    """A SEQUENTIAL PreAccept batch (config 1's semantics) mixing key-domain and Range-domain txns (sync
+    points, range reads/writes) over a random_small store with range commands and RedundantBefore: the
+    requests in ascending TxnId order with executeAt == txnId; each registers before its deps are
+    computed (PreAccept.java:116-132) -- a Range-domain one as a range command
+    (InMemoryCommandStore.java:740-763) that every later request of the batch sees."""
+    kw.setdefault("accept_frac", 0.0)
+    w = random_small(seed, range_frac=range_frac, **kw)
+    cm, q = w.cmds, w.queries
+    ident = lambda t: set(zip(t.msb.tolist(), (t.lsb >> np.uint64(16)).tolist(),  # noqa: E731
+                              (t.lsb & np.uint64(0x1E)).tolist(), t.node.tolist()))
+    clash = ident(cm.txn) & ident(q.txn)
+    if clash:                          # a batch txn that is already a range command: not a fresh PreAccept
+        keep = np.array([x not in clash for x in zip(cm.txn.msb.tolist(), (cm.txn.lsb >> np.uint64(16)).tolist(),
+                                                     (cm.txn.lsb & np.uint64(0x1E)).tolist(), cm.txn.node.tolist())])
+        w.cmds = RangeCommands.empty() if not keep.any() else cm.take(np.nonzero(keep)[0])
+    w.flags = A.AD_SEQUENTIAL
+    w.name = "sequential_ranges"
+    return w
+
+
 def range_map(rng, n_values, key_lo, key_hi, hlc_lo, hlc_hi, null_frac=0.1, inclusive_ends=0, epochs=(1, 2),
               node_max=16, flag_noise=True):
     """A random ReducingRangeMap<Timestamp> over key ordinals [key_lo, key_hi): distinct ascending
@@ -982,7 +1003,8 @@ def with_missing(cfk, seed, frac=0.5, max_missing=3, extra=None):
 def recovery_workload(seed, n_known=40, **kw):
     """BeginRecovery scans on a random_small store without range commands: its
     requests (a quarter of them already in the CommandsForKey) plus `n_known` requests recovering a
-    txnId of the history over (a superset of) its keys; entries carry missing() lists."""
+    txnId of the history over (a superset of) its keys; entries carry missing() lists. With
+    range_frac (random_small's) that share of its own requests are Range-domain txns over Ranges."""
     kw.setdefault("n_range_cmds", 0)
     w = random_small(seed, **kw)
     rng = np.random.default_rng(seed ^ 0x5EC0)
@@ -1002,7 +1024,13 @@ def recovery_workload(seed, n_known=40, **kw):
     keys = [q.keys[int(q.key_off[i]):int(q.key_off[i + 1])] for i in range(len(q))] + qs_k
     key_off = np.zeros(len(keys) + 1, np.uint64)
     key_off[1:] = np.cumsum([len(k) for k in keys])
-    w.queries = Queries(txn, txn, key_off, np.concatenate(keys + [np.zeros(0, np.int64)]))
+    ro = rs = re_ = None
+    if q.range_off is not None:
+        # Range-domain requests (range_frac: recovering sync points and range txns over Ranges) keep
+        # their ranges; the appended history requests are key-domain
+        ro = np.concatenate([q.range_off, np.full(len(qs_k), q.range_off[-1], np.uint64)])
+        rs, re_ = q.range_start, q.range_end
+    w.queries = Queries(txn, txn, key_off, np.concatenate(keys + [np.zeros(0, np.int64)]), None, ro, rs, re_)
     # stretch some proposed/committed executeAts far past their txnIds (Accept-style), so that earlier
     # txns executing after the recovering one (the STARTED_BEFORE scans) are common
     stretch = ((cfk.status >= A.ST_ACCEPTED) & (cfk.status <= A.ST_APPLIED) & (cfk.exec.node >= EXEC_NODE_BASE)

@@ -1574,15 +1574,100 @@ static int sync_host_entries(ad_ctx* c)
     return 0;
 }
 
+// SEQUENTIAL PreAccepts of Range-domain txns (sync points, range reads / writes): Commands.preaccept
+// stores the command and InMemorySafeStore.update registers it as a range command
+// (InMemoryCommandStore.java:740-763): rangeCommands[txnId].update(ranges.slice(slice, Minimal)), slice =
+// the store's ranges less the shard-redundant ones (RedundantBefore.removeShardRedundant,
+// RedundantBefore.java:216-225,433-437: an entry in the epoch bounds of (txnId, executeAt = txnId)
+// whose shardAppliedOrInvalidatedBefore is above txnId takes its range away). Appended to the store's
+// range commands (live, not historical; recovery facts, when loaded, those of a PreAccepted command:
+// neither proposed nor stable, no deps, executeAtOrTxnId = txnId); the snapshot is rebuilt before the
+// batch resolves, so every request sees the ones below its txnId (STARTED_BEFORE) -- the sequential
+// answer (PreAccept.java:116-132). A txnId already among the range commands is refused (AD_E_INVAL;
+// RangeCommand.update's union with its earlier ranges is not modelled).
+static int register_range_txns(ad_ctx* c, const ad_query_soa* q, const std::vector<uint64_t>& idx)
+{
+    auto& R = c->cmds;
+    std::vector<NormTid> have;
+    have.reserve(R.txn.size());
+    for (const Tid& t : R.txn) have.push_back(norm(t));
+    std::sort(have.begin(), have.end(), [](const NormTid& a, const NormTid& b) { return norm_cmp(a, b) < 0; });
+    const bool incl_rb = !c->rb.wm.empty();
+    const size_t n_sl = c->slice_s.empty() ? 1 : c->slice_s.size();
+    for (uint64_t i : idx)
+    {
+        const Tid t{q->txn_msb[i], q->txn_lsb[i], q->txn_node[i]};
+        const NormTid tn = norm(t);
+        auto it = std::lower_bound(have.begin(), have.end(), tn, [](const NormTid& a, const NormTid& b) { return norm_cmp(a, b) < 0; });
+        if (it != have.end() && norm_cmp(*it, tn) == 0)
+            return c->fail(AD_E_INVAL, "SEQUENTIAL request %llu: its Range-domain txnId is already a range command of the store",
+                           (unsigned long long)i);
+        // ranges.slice(slice, Minimal): every non-empty intersection with a slice range, ascending
+        std::vector<std::pair<int64_t, int64_t>> rs;
+        for (uint64_t j = q->range_off[i]; j < q->range_off[i + 1]; ++j)
+            for (size_t sl = 0; sl < n_sl; ++sl)
+            {
+                int64_t a = q->range_start[j], b = q->range_end[j];
+                if (!c->slice_s.empty())
+                {
+                    a = std::max(a, c->slice_s[sl]);
+                    b = std::min(b, c->slice_e[sl]);
+                }
+                if (a < b) rs.push_back({a, b});
+            }
+        // removeShardRedundant: Ranges.subtract of each redundant entry's range
+        const int64_t ep = (int64_t)(t.msb >> 15);
+        for (size_t e = 0; incl_rb && e < c->rb.wm.size(); ++e)
+        {
+            if (ep < c->rb.e0[e] || ep >= c->rb.e1[e]) continue;                        // outOfBounds(txnId, executeAt)
+            if (!(norm_cmp(tn, norm(c->rb.wm[e])) < 0)) continue;                      // txnId < shardAppliedOrInvalidatedBefore
+            const int64_t x0 = c->rb.start[e], x1 = c->rb.end[e];
+            std::vector<std::pair<int64_t, int64_t>> out;
+            for (auto& r : rs)
+            {
+                if (!(r.first < x1 && r.second > x0)) { out.push_back(r); continue; }
+                if (r.first < x0) out.push_back({r.first, x0});
+                if (x1 < r.second) out.push_back({x1, r.second});
+            }
+            rs.swap(out);
+        }
+        if (R.off.empty()) R.off.push_back(0);
+        R.txn.push_back(t);
+        for (auto& r : rs)
+        {
+            R.start.push_back(r.first);
+            R.end.push_back(r.second);
+        }
+        R.off.push_back(R.start.size());
+        if (!R.erased.empty()) R.erased.push_back(0);
+        if (!R.historical.empty()) R.historical.push_back(0);
+        if (R.rec)
+        {
+            R.rec_status.push_back(0);
+            R.rec_has_deps.push_back(0);
+            R.rec_exec.push_back(t);
+            R.rec_dep_off.push_back(R.rec_dep_off.empty() ? 0 : R.rec_dep_off.back());
+        }
+        have.insert(std::lower_bound(have.begin(), have.end(), tn, [](const NormTid& a, const NormTid& b) { return norm_cmp(a, b) < 0; }), tn);
+    }
+    c->rv_gen = ~0ull;
+    c->rv_rng_gen = ~0ull;
+    drop_global_dict(c);            // new ids: a node-wide dictionary must be installed again
+    c->dirty = true;
+    return 0;
+}
+
 // SEQUENTIAL: insert every request's txnId as PREACCEPTED_OR_ACCEPTED_INVALIDATE into the
 // CommandsForKey of each of its keys in the slice (CommandsForKey.update, :972-1042; a present
-// entry below PREACCEPTED is raised, otherwise left alone).
+// entry below PREACCEPTED is raised, otherwise left alone); Range-domain requests register as range
+// commands (register_range_txns).
 static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
 {
     if (int rc0 = sync_host(c)) return rc0;
     auto& K = c->cfk;
     struct Ins { int64_t key; NormTid n; Tid t; };
     std::vector<Ins> ins;
+    std::vector<uint64_t> rng;        // the batch's Range-domain requests
     for (uint64_t i = 0; i < q->n_txns; ++i)
     {
         const Tid t{q->txn_msb[i], q->txn_lsb[i], q->txn_node[i]};
@@ -1593,6 +1678,11 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
         {
             const Tid p{q->txn_msb[i - 1], q->txn_lsb[i - 1], q->txn_node[i - 1]};
             if (norm_cmp(norm(p), norm(t)) >= 0) return c->fail(AD_E_INVAL, "SEQUENTIAL requests must be in ascending TxnId order");
+        }
+        if (q->range_off && q->range_off[i + 1] > q->range_off[i])
+        {
+            rng.push_back(i);
+            continue;
         }
         const uint32_t kind = (uint32_t)((t.lsb >> 1) & 7);
         const bool manages = (t.lsb & 1) == 0 && ((KINDS_ANY_GLOBALLY_VISIBLE >> kind) & 1);  // CommandsForKey.manages :185-188
@@ -1606,6 +1696,8 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
             if (in) ins.push_back({key, norm(t), t});
         }
     }
+    if (!rng.empty())
+        if (int rc = register_range_txns(c, q, rng)) return rc;
     if (ins.empty()) return 0;
     if (!K.miss_off.empty()) K.miss_stale = true;
     std::stable_sort(ins.begin(), ins.end(), [](const Ins& a, const Ins& b) {
@@ -1779,10 +1871,12 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     }
     // Range-domain requests (ad_query_soa.range_off): expanded into probes on the device -- keys inside
     // the sliced ranges, the sliced ranges, the unsliced ranges (kernels.hip k_range_count /
-    // k_range_fill) -- then resolved by the split kernels
+    // k_range_fill) -- then resolved by the split kernels. Recovery scans take no RedundantBefore
+    // (mapReduceFull, InMemoryCommandStore.java:874-882): no unsliced-range probes
     uint64_t nr = 0;
     if (n && q->range_off)
     {
+        if (!q->range_start || !q->range_end) return c->fail(AD_E_INVAL, "range_off without range_start / range_end");
         if (n_keys_given)
             nr = q->n_ranges;
         else
@@ -1794,7 +1888,6 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             nr = ro[1] - ro[0];
         }
     }
-    if (nr && recovery_scan >= 0) return c->fail(AD_E_INVAL, "recovery scans take key-domain requests only");
     if (nr)
     {
         if (!ens<uint32_t>(c->rq_cnt, n) || !ens<uint64_t>(c->rq_off, n + 1) || !ens<uint32_t>(c->rq_err, 2) ||
@@ -1802,7 +1895,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             return c->fail(AD_E_NOMEM, "range request expansion");
         HIPCHK(c, hipMemsetAsync(c->rq_err.p, 0, 8, st));
         HIPCHK(c, run_range_count(c->ds, n, q->key_off, q->range_off, q->range_start, q->range_end, c->rq_cnt.as<uint32_t>(),
-                                  c->rq_err.as<uint32_t>(), st));
+                                  c->rq_err.as<uint32_t>(), recovery_scan < 0, st));
         HIPCHK(c, run_scan_arrays(c->rq_cnt.as<uint32_t>(), c->rq_off.as<uint64_t>(), n, 1, c->rq_bsum.as<uint64_t>(), st));
         uint64_t tail[2] = {0, 0};
         HIPCHK(c, d2h(&tail[0], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), st));
@@ -1816,7 +1909,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
             return c->fail(AD_E_NOMEM, "range request probes");
         HIPCHK(c, run_range_fill(c->ds, n, q->key_off, q->keys, q->range_off, q->range_start, q->range_end,
                                  c->rq_off.as<uint64_t>(), c->rq_keys.as<int64_t>(), c->rq_hi.as<int64_t>(),
-                                 c->rq_kind.as<uint8_t>(), st));
+                                 c->rq_kind.as<uint8_t>(), recovery_scan < 0, st));
     }
     const bool split_only = c->cfg.path == 1 || recovery_scan >= 0 || nr > 0;
     // the lean kernel covers stores without redundant-before entries, elision on
@@ -2232,6 +2325,8 @@ static int check_query_host(ad_ctx* c, const ad_query_soa* q, uint32_t flags = 0
     {
         // Range-domain requests: ranges normalised (accord.primitives.Ranges), no keys beside them,
         // SNAPSHOT semantics only
+        if (!q->range_start || !q->range_end)
+            return c->fail(AD_E_INVAL, "range_off without range_start / range_end");
         for (uint64_t i = 0; i < q->n_txns; ++i)
         {
             const uint64_t r0 = q->range_off[i], r1 = q->range_off[i + 1];
@@ -2239,9 +2334,6 @@ static int check_query_host(ad_ctx* c, const ad_query_soa* q, uint32_t flags = 0
             if (r1 == r0) continue;
             if (q->key_off[i + 1] != q->key_off[i])
                 return c->fail(AD_E_INVAL, "request %llu has keys and ranges (a request is key- or Range-domain)", (unsigned long long)i);
-            if (flags & AD_SEQUENTIAL)
-                return c->fail(AD_E_INVAL, "SEQUENTIAL batches take key-domain requests only (request %llu has ranges)",
-                               (unsigned long long)i);
             for (uint64_t j = r0; j < r1; ++j)
                 if (q->range_start[j] >= q->range_end[j] || (j > r0 && q->range_end[j - 1] > q->range_start[j]))
                     return c->fail(AD_E_INVAL, "request %llu: ranges not normalised (start < end, ascending, disjoint)",
@@ -2481,6 +2573,9 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
 static int sequential_on_device(ad_ctx* c, const ad_query_soa* q)
 {
     if (c->dirty || getenv("AD_SEQ_HOST")) return 1;
+    // Range-domain requests register as range commands, whose part of the snapshot is host-built: the
+    // host route (apply_preaccepts + rebuild)
+    if (q->n_txns && q->range_off && q->range_off[q->n_txns] > q->range_off[0]) return 1;
     std::vector<int64_t> keys;
     std::vector<uint64_t> tm, tl;
     std::vector<int32_t> tn;
@@ -2545,7 +2640,13 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
             // keep a copy so a failed batch leaves the snapshot untouched
             if ((rc = sync_host(c))) return rc;
             auto saved = c->cfk;
-            if ((rc = apply_preaccepts(c, q))) { c->cfk = saved; return rc; }
+            auto saved_cmds = c->cmds;
+            if ((rc = apply_preaccepts(c, q)))
+            {
+                c->cfk = saved;
+                c->cmds = saved_cmds;
+                return rc;
+            }
         }
     }
     if (c->dirty && (rc = build_snapshot(c))) return rc;
@@ -2661,7 +2762,13 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
         {
             if ((rc = sync_host(c))) return rc;
             auto saved = c->cfk;
-            if ((rc = apply_preaccepts(c, q))) { c->cfk = saved; return rc; }
+            auto saved_cmds = c->cmds;
+            if ((rc = apply_preaccepts(c, q)))
+            {
+                c->cfk = saved;
+                c->cmds = saved_cmds;
+                return rc;
+            }
         }
         slices = 1;        // the inserted requests are part of one snapshot
     }
@@ -3179,8 +3286,6 @@ int ad_recovery_batch(ad_ctx* c, const ad_query_soa* q, uint32_t scan, ad_deps_r
     int rc = check_query_host(c, q);
     if (rc) return rc;
     const uint64_t n = q->n_txns;
-    if (n && q->range_off && q->range_off[n] > q->range_off[0])
-        return c->fail(AD_E_INVAL, "recovery scans take key-domain requests only");
     const uint64_t np = n ? q->key_off[n] : 0;
     ad_query_soa d{};
     d.n_txns = n;
@@ -3189,6 +3294,20 @@ int ad_recovery_batch(ad_ctx* c, const ad_query_soa* q, uint32_t scan, ad_deps_r
     d.txn_node = stage_q(c, c->q_tn, q->txn_node, n, &rc);
     d.key_off = stage_q(c, c->q_ko, q->key_off, n + 1, &rc);
     d.keys = stage_q(c, c->q_k, q->keys, np, &rc);
+    std::vector<uint64_t> ro;
+    if (n && q->range_off && q->range_off[n] > q->range_off[0])
+    {
+        // Range-domain requests: a recovering sync point or range txn over its Ranges (BeginRecovery
+        // passes partialTxn.keys(), Seekables, to mapReduceFull: BeginRecovery.java:334,348,365,378)
+        const uint64_t r0 = q->range_off[0], nr = q->range_off[n] - r0;
+        ro.resize(n + 1);
+        for (uint64_t i = 0; i <= n; ++i) ro[i] = q->range_off[i] - r0;
+        d.range_off = stage_q(c, c->q_ro, ro.data(), n + 1, &rc);
+        d.range_start = stage_q(c, c->q_rs, q->range_start + r0, nr, &rc);
+        d.range_end = stage_q(c, c->q_re, q->range_end + r0, nr, &rc);
+        d.n_ranges = nr;
+        if (!rc) HIPCHK(c, hipStreamSynchronize(c->stream));     // ro is a local
+    }
     if (rc) return rc;
     ad_deps_result dev{};
     if ((rc = ad_recovery_batch_device(c, &d, scan, c->stream, &dev))) return rc;

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, 
                                                      const uint64_t* __restrict__ range_off,
                                                      const int64_t* __restrict__ range_start,
                                                      const int64_t* __restrict__ range_end, uint32_t* __restrict__ cnt,
-                                                     uint32_t* err)
+                                                     uint32_t* err, bool with_rb)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, 
             if (s.n_rent) ++c;
         }
     }
-    if (s.n_rb) c += r1 - r0;
+    if (s.n_rb && with_rb) c += r1 - r0;
     if (bad) atomicOr(err, 1u);
     cnt[t] = bad ? 0u : (uint32_t)min<uint64_t>(c, 0xFFFFFFFFull);
 }
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, uint64_t n, c
                                                     const int64_t* __restrict__ range_start,
                                                     const int64_t* __restrict__ range_end, const uint64_t* __restrict__ off,
                                                     int64_t* __restrict__ pkeys, int64_t* __restrict__ pkeys_hi,
-                                                    uint8_t* __restrict__ pkind)
+                                                    uint8_t* __restrict__ pkind, bool with_rb)
 {
     const uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (t >= n) return;
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, uint64_t n, c
             }
         }
     }
-    if (s.n_rb)
+    if (s.n_rb && with_rb)
         for (uint64_t j = r0 + lane; j < r1; j += 64)
         {
             pkeys[o + (j - r0)] = range_start[j];
@@ -351,19 +351,22 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, uint64_t n, c
 
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
                            const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           hipStream_t st)
+                           bool with_rb, hipStream_t st)
 {
-    if (n) k_range_count<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n, key_off, range_off, range_start, range_end, cnt, err);
+    if (n)
+        k_range_count<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n, key_off, range_off, range_start, range_end, cnt, err,
+                                                                   with_rb);
     return hipGetLastError();
 }
 
 hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
                           const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
-                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, hipStream_t st)
+                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, bool with_rb,
+                          hipStream_t st)
 {
     if (n)
         k_range_fill<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(s, n, key_off, keys, range_off, range_start, range_end, off, pkeys,
-                                                              pkeys_hi, pkind);
+                                                              pkeys_hi, pkind, with_rb);
     return hipGetLastError();
 }
 
@@ -2138,7 +2141,8 @@ __global__ __launch_bounds__(256) void k_recover(RecoveryView v, BatchBufs b, ui
 // The range-command half of the recovery scans (InMemorySafeStore.mapReduceFull ->
 // mapReduceRangesInternal, InMemoryCommandStore.java:884-958): one wave per (request, key) probe
 // finds the range entries holding the key by the K4 descent (start before the key, max-end tree of
-// the all-kinds class), and keeps those of live commands passing the scan's tests; their (range id,
+// the all-kinds class) -- or, for a sliced range of a Range-domain request, the entries intersecting
+// it -- and keeps those of live commands passing the scan's tests; their (range id,
 // txnId) pairs go to the K4 arena, so k_build assembles rangeDeps (one txnId per range, as the
 // collect fold does).
 __global__ __launch_bounds__(256) void k_range_recover(DevSnapshot s, RecoveryView v, BatchBufs b, uint32_t scan)
@@ -2162,11 +2166,17 @@ __global__ __launch_bounds__(256) void k_range_recover(DevSnapshot s, RecoveryVi
         uint32_t cnt = 0;
         uint64_t off = 0;
         const bool in_slice = (b.p_rec[p].w >> 12) & 1;
-        if (in_slice && s.n_rent && kinds)
+        // a Range-domain request (k_range_fill): its sliced range [x, xe) probes the commands whose ranges
+        // intersect it (Routables.foldl over the sliced ranges, InMemoryCommandStore.java:951-956) -- the
+        // K4 prefix on start < xe, threshold end > x; the CommandsForKey keys inside it probe nothing here
+        const uint32_t pk = b.p_kind ? b.p_kind[p] : PK_KEY;
+        const bool rq = pk == PK_RANGE;
+        const int64_t xe = rq ? b.q_keys_hi[p] : 0;
+        if (in_slice && s.n_rent && kinds && pk != PK_RANGE_KEY)
         {
             const uint64_t hi = wave_lower_bound(0, s.n_rent, [&](uint64_t i) { return s.r_start[i]; },
-                                                 [&](int64_t val) { return incl ? val <= x : val < x; });
-            auto end_ok = [&](int64_t e) { return incl ? e > x : e >= x; };
+                                                 [&](int64_t val) { return rq ? val < xe : (incl ? val <= x : val < x); });
+            auto end_ok = [&](int64_t e) { return rq ? e > x : (incl ? e > x : e >= x); };
             auto node_want = [&](int lv, uint64_t node) { return end_ok(s.rlvl[2][lv][node]); };
             auto want_of = [&](uint64_t i, bool inr, uint64_t& val) -> bool {
                 val = 0;

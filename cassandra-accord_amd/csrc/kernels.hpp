@@ -139,10 +139,11 @@ constexpr uint8_t PK_KEY = 0, PK_RANGE_KEY = 1, PK_RANGE = 2, PK_RANGE_RB = 3;
 // not normalised); then, from the exclusive scan `off`, the probes
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
                            const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           hipStream_t st);
+                           bool with_rb, hipStream_t st);
 hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
                           const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
-                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, hipStream_t st);
+                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, bool with_rb,
+                          hipStream_t st);
 
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
 hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);

@@ -196,8 +196,12 @@ typedef struct ad_query_soa {
      * the ranges sliced to the store's slices (InMemoryCommandStore.mapReduceForKey, case Range,
      * :289-304), every range command with a range intersecting those sliced ranges
      * (mapReduceRangesInternal, :884-1017) and the RedundantBefore entries intersecting the request's
-     * (unsliced) ranges (RedundantBefore.collectDeps, RedundantBefore.java:420-423). SNAPSHOT batches
-     * only (AD_SEQUENTIAL with a range request: AD_E_INVAL), not taken by ad_recovery_batch. */
+     * (unsliced) ranges (RedundantBefore.collectDeps, RedundantBefore.java:420-423). In an AD_SEQUENTIAL
+     * batch such a request first registers as a range command (PreAccept.apply, PreAccept.java:116-132;
+     * InMemoryCommandStore.java:740-763): its ranges sliced to the store, less those of the
+     * RedundantBefore entries that make it shard-redundant (RedundantBefore.java:216-225), seen by every
+     * later request of the batch and kept by the store (a txnId already among the range commands:
+     * AD_E_INVAL). ad_recovery_batch takes them too (a recovering sync point or range txn). */
     const uint64_t* range_off;       /* [n_txns+1] or NULL */
     const int64_t*  range_start;
     const int64_t*  range_end;
@@ -606,7 +610,10 @@ int ad_range_cmds_recovery_load(ad_ctx* ctx, const ad_range_cmds_recovery_soa* r
 
 /* Host buffers in, host result out (as ad_deps_batch). A store with live range commands needs
  * their recovery facts (ad_range_cmds_recovery_load after the last ad_range_cmds_load), else
- * AD_E_STATE. */
+ * AD_E_STATE. Range-domain requests (ad_query_soa.range_*: a recovering sync point or range txn, whose
+ * Seekables BeginRecovery hands to mapReduceFull) scan every CommandsForKey inside their ranges sliced
+ * to the store (InMemoryCommandStore.java:289-304) and the range commands whose ranges intersect them
+ * (:884-958); RedundantBefore takes no part in these scans. */
 int ad_recovery_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t scan, ad_deps_result** out);
 /* Device buffers in and out, as ad_deps_batch_device (result valid until the next batch call). */
 int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t scan, void* stream, ad_deps_result* out);

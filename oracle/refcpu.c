@@ -991,6 +991,63 @@ static void sequential_preaccept(rc_store* s, const tid_t* txnId, const int64_t*
     }
 }
 
+/* Ranges.subtract of one range (x) from normalised ranges v[0..n): the pieces left, in place; returns
+ * the new count (room for n + 1) */
+static size_t ranges_subtract_one(rkey_t* v, size_t n, const rkey_t* x)
+{
+    rkey_t out[n + 1];
+    size_t m = 0;
+    for (size_t i = 0; i < n; ++i)
+    {
+        if (!range_intersects(&v[i], x)) { out[m++] = v[i]; continue; }
+        if (v[i].a < x->a) out[m++] = (rkey_t){v[i].a, x->a};
+        if (x->b < v[i].b) out[m++] = (rkey_t){x->b, v[i].b};
+    }
+    copy_n(v, out, sizeof(rkey_t) * m);
+    return m;
+}
+
+/* SEQUENTIAL PreAccept of a Range-domain txn: Commands.preaccept stores the command, and
+ * InMemorySafeStore.update registers it as a range command (InMemoryCommandStore.java:740-763):
+ * rangeCommands[txnId].update(ranges.slice(slice, Minimal)) with slice = the store's ranges minus the
+ * shard-redundant ones, RedundantBefore.removeShardRedundant (RedundantBefore.java:216-225,433-437: an
+ * entry in epoch bounds of (txnId, executeAt) with txnId below its shardAppliedOrInvalidatedBefore
+ * takes its range away). The command is live (PreAccepted: saveStatus below Erased), not historical;
+ * its recovery facts are a PreAccepted command's (neither proposed nor stable, no proposed or decided
+ * deps, executeAtOrTxnId = txnId). A txnId the store already registered is rejected (AD_E_INVAL;
+ * RangeCommand.update's union with the earlier ranges is not modelled). */
+static int sequential_register_range(rc_store* s, const tid_t* txnId, const rkey_t* ranges, size_t nranges)
+{
+    for (size_t i = 0; i < s->cmds.n; ++i)
+        if (tid_eq(&s->cmds.v[i].txnId, txnId)) return fail(s, AD_E_INVAL, "SEQUENTIAL range txn already a range command");
+    for (size_t i = 0; i < s->hist.n; ++i)
+        if (tid_eq(&s->hist.v[i].txnId, txnId)) return fail(s, AD_E_INVAL, "SEQUENTIAL range txn already a range command");
+    const size_t cap = nranges * (s->n_slices ? s->n_slices : 1) + s->rb.n + 1;
+    rkey_t* rs = malloc(sizeof(rkey_t) * cap);
+    size_t n = slice_ranges(s, ranges, nranges, rs);
+    const int64_t ep = tid_epoch(txnId);
+    for (size_t i = 0; i < s->rb.n; ++i)
+    {
+        const rb_entry_t* e = &s->rb.v[i];
+        if (ep < e->startEpoch || ep >= e->endEpoch) continue;           /* outOfBounds(txnId, executeAt) :262-265 */
+        if (tid_cmp(txnId, &e->wm) < 0) n = ranges_subtract_one(rs, n, &e->range);
+    }
+    rcmd_t c;
+    memset(&c, 0, sizeof(c));
+    c.txnId = *txnId;
+    c.orig = s->cmds.n + s->hist.n;
+    c.has_rec = 1;
+    c.exec = *txnId;
+    for (size_t i = 0; i < n; ++i) VEC_PUSH(c.ranges, rs[i]);
+    free(rs);
+    size_t pos = s->cmds.n;                                             /* TreeMap<TxnId, ...> order */
+    while (pos > 0 && tid_cmp(&s->cmds.v[pos - 1].txnId, txnId) > 0) --pos;
+    VEC_PUSH(s->cmds, c);
+    memmove(&s->cmds.v[pos + 1], &s->cmds.v[pos], (s->cmds.n - 1 - pos) * sizeof(rcmd_t));
+    s->cmds.v[pos] = c;
+    return 0;
+}
+
 static void result_alloc_map(rc_result* r, int m, size_t nk, size_t nt, size_t no)
 {
     r->keys[m] = realloc(r->keys[m], sizeof(int64_t) * (nk ? nk : 1));
@@ -1077,7 +1134,6 @@ int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t f
         if (nranges)
         {
             if (nkeys) { rc = fail(s, AD_E_INVAL, "request %llu has keys and ranges", (unsigned long long)i); break; }
-            if (flags & AD_SEQUENTIAL) { rc = fail(s, AD_E_INVAL, "SEQUENTIAL batches take key-domain requests only"); break; }
             ranges = malloc(sizeof(rkey_t) * nranges);
             for (size_t j = 0; j < nranges; ++j)
             {
@@ -1091,7 +1147,14 @@ int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t f
             }
             if (rc) { free(ranges); break; }
         }
-        if (flags & AD_SEQUENTIAL) sequential_preaccept(s, &txnId, keys, nkeys);
+        if (flags & AD_SEQUENTIAL)
+        {
+            /* PreAccept.apply registers the txn before computing its deps (PreAccept.java:116-132) */
+            if (!tid_eq(&txnId, &executeAt)) { free(ranges); rc = fail(s, AD_E_INVAL, "SEQUENTIAL (PreAccept) requests need executeAt == txnId"); break; }
+            if (nranges) rc = sequential_register_range(s, &txnId, ranges, nranges);
+            else sequential_preaccept(s, &txnId, keys, nkeys);
+            if (rc) { free(ranges); break; }
+        }
         pdeps_t pd;
         rc = calculate_partial_deps(s, &txnId, keys, nkeys, ranges, nranges, q->min_epoch ? q->min_epoch[i] : 0, &executeAt, &pd,
                                     &r->scan_entries);
@@ -1560,9 +1623,12 @@ static int tids_contain(const tid_t* v, size_t n, const tid_t* x)
  * for a recovery scan (testStatus != ANY_STATUS: no historical commands), then the collect fold
  * (:1005-1014) into the scan's lambda (BeginRecovery.java:334-380; scan 0 wants executeAt > its
  * testTxnId) */
-static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t nkeys, const tid_t* T, unsigned testKind,
-                                  int startedAt, int testDep, int testStatus, int exec_after, deps_builder_t* b)
+static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t nkeys, const rkey_t* rsliced, size_t nrsliced,
+                                  const tid_t* T, unsigned testKind, int startedAt, int testDep, int testStatus, int exec_after,
+                                  deps_builder_t* b)
 {
+    /* keysOrRanges.slice(slice, Minimal) (:887): keys inside the slices; a Range-domain request's sliced
+     * ranges arrive as rsliced (its intersects / Routables.foldl then test command ranges against them) */
     int64_t* sliced = malloc(sizeof(int64_t) * (nkeys ? nkeys : 1));
     size_t nsliced = 0;
     for (size_t k = 0; k < nkeys; ++k) if (slice_contains(s, keys[k])) sliced[nsliced++] = keys[k];
@@ -1592,7 +1658,7 @@ static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t
             const int inter = tids_contain(c->deps.v, c->deps.n, T);
             if ((testDep == WITH) == !inter) continue;
         }
-        collect_command(s, &col, c, sliced, nsliced, NULL, 0);                                   /* :949-956 */
+        collect_command(s, &col, c, sliced, nsliced, rsliced, nrsliced);                         /* :949-956 */
     }
     int rc = 0;
     for (size_t i = 0; i < col.n && !rc; ++i)
@@ -1630,8 +1696,6 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
             return fail(s, AD_E_STATE, "recovery scans of range commands need their recovery facts (rc_range_cmds_recovery_load)");
     if (count == 0) count = q->n_txns - first;
     if (first + count > q->n_txns) return fail(s, AD_E_INVAL, "query window out of range");
-    if (q->range_off && q->range_off[q->n_txns] > q->range_off[0])
-        return fail(s, AD_E_INVAL, "recovery scans take key-domain requests only");
     rc_result* r = calloc(1, sizeof(rc_result));
     r->n_txns = count;
     size_t cap[AD_NMAPS][3] = {{0}};
@@ -1654,6 +1718,31 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
         if (rc) break;
         unsigned kinds;
         if (kind_witnessed_by(tid_kind(&txnId), &kinds)) { rc = fail(s, AD_E_INVAL, "invalid Txn.Kind for witnessedBy()"); break; }
+        /* a Range-domain request (a recovering sync point or range txn: BeginRecovery passes
+         * partialTxn.keys(), Seekables, to mapReduceFull, BeginRecovery.java:334,348,365,378): its
+         * normalised Ranges, sliced to the store as mapReduceForKey / mapReduceRangesInternal do */
+        const size_t nranges = q->range_off ? (size_t)(q->range_off[i + 1] - q->range_off[i]) : 0;
+        rkey_t* rsliced = NULL;
+        size_t nrs = 0;
+        if (nranges)
+        {
+            if (nkeys) { rc = fail(s, AD_E_INVAL, "request %llu has keys and ranges", (unsigned long long)i); break; }
+            rkey_t* ranges = malloc(sizeof(rkey_t) * nranges);
+            for (size_t j = 0; j < nranges && !rc; ++j)
+            {
+                const uint64_t at = q->range_off[i] + j;
+                ranges[j] = (rkey_t){q->range_start[at], q->range_end[at]};
+                if (ranges[j].a >= ranges[j].b || (j > 0 && ranges[j - 1].b > ranges[j].a))
+                    rc = fail(s, AD_E_INVAL, "request %llu: ranges not normalised", (unsigned long long)i);
+            }
+            if (!rc)
+            {
+                rsliced = malloc(sizeof(rkey_t) * nranges * (s->n_slices ? s->n_slices : 1));
+                nrs = slice_ranges(s, ranges, nranges, rsliced);
+            }
+            free(ranges);
+            if (rc) break;
+        }
         deps_builder_t builder;                                          /* Deps.builder() */
         builder_init(&builder.key); builder_init(&builder.range); builder_init(&builder.direct);
         /* InMemorySafeStore.mapReduceFull -> mapReduceForKey (InMemoryCommandStore.java:272-307) */
@@ -1664,8 +1753,24 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
             if (cfk == NULL) continue;
             rc = cfk_map_reduce_full(s, cfk, &txnId, kinds, P[scan][0], P[scan][1], P[scan][2], &builder);
         }
+        /* case Range (:289-304): every CommandsForKey of commandsForKey.subMap(start, startInclusive, end,
+         * endInclusive) of each sliced range, ascending */
+        for (size_t rr = 0; rr < nrs && !rc; ++rr)
+        {
+            size_t lo = 0, hi = s->cfks.n;
+            while (lo < hi)
+            {
+                const size_t mid = (lo + hi) / 2;
+                if (s->cfg.range_start_inclusive ? s->cfks.v[mid].key < rsliced[rr].a : s->cfks.v[mid].key <= rsliced[rr].a) lo = mid + 1;
+                else hi = mid;
+            }
+            for (size_t k = lo; k < s->cfks.n && range_contains(s, &rsliced[rr], s->cfks.v[k].key) && !rc; ++k)
+                rc = cfk_map_reduce_full(s, &s->cfks.v[k], &txnId, kinds, P[scan][0], P[scan][1], P[scan][2], &builder);
+        }
         if (!rc)
-            rc = map_reduce_ranges_full(s, keys, nkeys, &txnId, kinds, P[scan][0], P[scan][1], P[scan][2], scan == 0, &builder);
+            rc = map_reduce_ranges_full(s, keys, nkeys, rsliced, nrs, &txnId, kinds, P[scan][0], P[scan][1], P[scan][2], scan == 0,
+                                        &builder);
+        free(rsliced);
         pdeps_t pd;
         memset(&pd, 0, sizeof(pd));
         if (!rc) rc = deps_build(&builder, &pd);

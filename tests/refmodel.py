@@ -247,6 +247,11 @@ def recovery_pairs(w, qi, scan):
     started, with_dep, statuses = RECOVER[scan]
     kinds = WITNESSED_BY[kind(T)]
     si = w.range_start_inclusive
+    # a Range-domain request visits every CommandsForKey key inside one of its ranges (and the store's
+    # slices, tested below): InMemoryCommandStore.mapReduceForKey, case Range (:289-304)
+    ranges = q.ranges_of(qi)
+    if ranges:
+        keys = [int(k) for k in c.keys if any(contains(si, a, b, int(k)) for a, b in ranges)]
     kd, dd = set(), set()
     for k in keys:
         if w.slices is not None and not any(contains(si, int(a), int(b), k) for a, b in w.slices):
@@ -298,6 +303,8 @@ def recovery_range_pairs(w, qi, scan):
     si = w.range_start_inclusive
     if w.slices is not None:
         keys = [k for k in keys if any(contains(si, int(a), int(b), k) for a, b in w.slices)]
+    ranges = q.ranges_of(qi)
+    slices = [(None, None)] if w.slices is None else [(int(a), int(b)) for a, b in w.slices]
     started, with_dep, statuses = RECOVER[scan]
     need = 1 if statuses == (3, 4) else 2                  # AD_RS_PROPOSED / AD_RS_STABLE
     kinds = WITNESSED_BY[kind(T)]
@@ -323,6 +330,107 @@ def recovery_range_pairs(w, qi, scan):
             continue
         for r in range(int(cm.range_off[i]), int(cm.range_off[i + 1])):
             a, b = int(cm.range_start[r]), int(cm.range_end[r])
-            if any(contains(si, a, b, k) for k in keys):
+            if ranges:
+                # the command's range meets a request range inside a slice (three half-open intervals)
+                hit = any(max(a, x, a if sa is None else sa) < min(b, y, b if sb is None else sb)
+                          for x, y in ranges for sa, sb in slices)
+            else:
+                hit = any(contains(si, a, b, k) for k in keys)
+            if hit:
                 out.add(((a, b), key(t), t))
     return out
+
+
+def sequential_augmented(w):
+    """SEQUENTIAL PreAccept semantics as a SNAPSHOT store (extended to Range-domain
+    txns): every request, in ascending TxnId order, is registered before its deps are computed
+    (PreAccept.java:116-132) -- a key-domain txn CommandsForKey manages goes into each of its keys' byId
+    in the store's slices as PREACCEPTED (executeAt = txnId; a present entry below PREACCEPTED is raised,
+    CommandsForKey.update :972-1042), a Range-domain txn becomes a live range command over its ranges
+    intersected with the slices, less the ranges of the RedundantBefore entries in its epoch bounds whose
+    shardAppliedOrInvalidatedBefore is above it (InMemoryCommandStore.java:740-763,
+    RedundantBefore.java:216-225). A request only sees registered txns below it (STARTED_BEFORE), so
+    registering the whole batch first answers the same. Returns the augmented workload (SNAPSHOT)."""
+    from accord_deps.model import CfkSnapshot, RangeCommands, Tids, Workload
+    q, c, si = w.queries, w.cfk, w.range_start_inclusive
+    slices = None if w.slices is None else [(int(a), int(b)) for a, b in w.slices]
+    tup = lambda T, i: (int(T.msb[i]), int(T.lsb[i]), int(T.node[i]))  # noqa: E731
+    by_key = {}
+    for i, k in enumerate(c.keys):
+        s0, s1 = int(c.seg[i]), int(c.seg[i + 1])
+        pb = int(c.pruned_before[i]) if c.pruned_before is not None else -1
+        ents = [[tup(c.txn, e), int(c.status[e]), tup(c.exec, e), e - s0 == pb] for e in range(s0, s1)]
+        by_key[int(k)] = ents
+    new_cmds = []
+    for qi in range(len(q)):
+        t = tup(q.txn, qi)
+        ranges = q.ranges_of(qi)
+        if ranges:
+            rs = []
+            for a, b in ranges:
+                for sa, sb in (slices or [(a, b)]):
+                    lo, hi = max(a, sa), min(b, sb)
+                    if lo < hi:
+                        rs.append((lo, hi))
+            rb = w.redundant
+            for j in range(len(rb.range_start)):
+                wm = (int(rb.wm.msb[j]), int(rb.wm.lsb[j]), int(rb.wm.node[j]))
+                ep = t[0] >> 15
+                if ep < int(rb.start_epoch[j]) or ep >= int(rb.end_epoch[j]) or not key(t) < key(wm):
+                    continue
+                x0, x1 = int(rb.range_start[j]), int(rb.range_end[j])
+                out = []
+                for a, b in rs:
+                    if not (a < x1 and b > x0):
+                        out.append((a, b))
+                        continue
+                    if a < x0:
+                        out.append((a, x0))
+                    if x1 < b:
+                        out.append((x1, b))
+                rs = out
+            new_cmds.append((t, rs))
+            continue
+        if domain(t) != 0 or kind(t) not in (0, 1, 3, 4):
+            continue
+        for k in q.keys[int(q.key_off[qi]):int(q.key_off[qi + 1])]:
+            k = int(k)
+            if slices is not None and not any(contains(si, a, b, k) for a, b in slices):
+                continue
+            ents = by_key.setdefault(k, [])
+            hit = [e for e in ents if eq(e[0], t)]
+            if hit:
+                if hit[0][1] < 2:
+                    hit[0][1], hit[0][2] = 2, t
+            else:
+                ents.append([t, 2, t, False])
+                ents.sort(key=lambda e: key(e[0]))
+    keys = sorted(by_key)
+    seg, tx, ex, st, pb = [0], [], [], [], []
+    for k in keys:
+        ents = by_key[k]
+        p = -1
+        for j, e in enumerate(ents):
+            tx.append(e[0]); st.append(e[1]); ex.append(e[2])
+            if e[3]:
+                p = j
+        pb.append(p)
+        seg.append(len(tx))
+    T = lambda xs: Tids(np.array([x[0] for x in xs], np.uint64), np.array([x[1] for x in xs], np.uint64),  # noqa: E731
+                        np.array([x[2] for x in xs], np.int32))
+    cfk = CfkSnapshot(np.array(keys, np.int64), np.array(seg, np.uint64), T(tx), T(ex), np.array(st, np.uint8),
+                      np.array(pb, np.int64) if c.pruned_before is not None else None)
+    cm = w.cmds
+    n0 = len(cm.txn)
+    txn = Tids.concat([cm.txn, T([t for t, _ in new_cmds])]) if new_cmds else cm.txn
+    off = list(int(x) for x in cm.range_off)
+    rs_, re_ = list(int(x) for x in cm.range_start), list(int(x) for x in cm.range_end)
+    for _, rs in new_cmds:
+        for a, b in rs:
+            rs_.append(a); re_.append(b)
+        off.append(len(rs_))
+    pad = lambda a: None if a is None else np.concatenate([np.asarray(a, np.uint8), np.zeros(len(new_cmds), np.uint8)])  # noqa: E731
+    cmds = RangeCommands(txn, np.array(off, np.uint64), np.array(rs_, np.int64), np.array(re_, np.int64),
+                         pad(cm.erased) if cm.erased is not None or n0 == 0 else None,
+                         pad(cm.historical) if cm.historical is not None or n0 == 0 else None)
+    return Workload(w.name + "_aug", cfk, cmds, w.redundant, q, 0, w.params, si, w.slices)

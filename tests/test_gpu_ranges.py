@@ -128,7 +128,8 @@ def test_rejections():
             with pytest.raises(native.AccordDepsError) as e:
                 native.resolve(bw, via=via)
             assert e.value.code == A.AD_E_INVAL, (mutate.__name__, via)
-    # SEQUENTIAL batches and recovery scans take key-domain requests only
+    # SEQUENTIAL batches take key-domain requests only; a recovery scan of Range-domain requests on a
+    # store whose range commands carry no recovery facts is refused as for key-domain ones
     st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
     try:
         st.load(w)
@@ -137,7 +138,7 @@ def test_rejections():
         assert e.value.code == A.AD_E_INVAL
         with pytest.raises(native.AccordDepsError) as e:
             st.recovery_scan(q, 0)
-        assert e.value.code == A.AD_E_INVAL
+        assert e.value.code == A.AD_E_STATE
         # the store still answers afterwards
         native_ok = st.calculate_partial_deps(q)
         assert native_ok.n_txns == len(q)
@@ -149,3 +150,55 @@ def test_unnormalised_slices_rejected():
     with pytest.raises(native.AccordDepsError) as e:
         native.DeviceCommandStore(0, 0, 1, np.array([[0, 300], [-400, -100]], np.int64))
     assert e.value.code == A.AD_E_INVAL
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_sequential_range_txns(oracle, seed):
+    # SEQUENTIAL batches mixing key- and Range-domain PreAccepts: each range txn registers as a range
+    # command before its deps are computed (PreAccept.java:116-132, InMemoryCommandStore.java:740-763),
+    # sliced and less its shard-redundant ranges (RedundantBefore.java:216-225); ad_deps_batch and
+    # ad_deps_batch_into against the oracle's request-by-request restatement
+    w = synth.sequential_ranges(3000 + seed, n_keys=30 + 3 * seed, n_txns=80, with_slices=(seed % 3 == 1),
+                                start_inclusive=(seed % 4 == 2), n_redundant=(0 if seed % 5 == 4 else 4))
+    assert w.queries.n_ranges > 0
+    exp = oracle.resolve(w)
+    _eq(native.resolve(w), exp, "seed %d" % seed)
+
+
+def test_sequential_range_txns_persist(oracle):
+    # the registered range commands stay in the store: two SEQUENTIAL batches, then a SNAPSHOT batch of
+    # later requests, on one store and on one oracle store
+    import pyoracle
+    w = synth.sequential_ranges(3100, n_keys=50, n_txns=150, range_frac=0.5)
+    q = w.queries
+    h = len(q) // 2
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    ost = pyoracle.OracleStore(w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        ost.load(w)
+        for lo, hi in ((0, h), (h, len(q))):
+            part = q.window(lo, hi)
+            _eq(st.calculate_partial_deps(part, A.AD_SEQUENTIAL), ost.deps_batch(part, A.AD_SEQUENTIAL), "batch %d" % lo)
+        # every request again as SNAPSHOT reads: each sees the whole batch below its txnId, itself excluded
+        _eq(st.calculate_partial_deps(q), ost.deps_batch(q), "snapshot after")
+    finally:
+        st.close()
+        ost.close()
+
+
+def test_sequential_range_txn_already_registered():
+    # a range txn the store already holds as a range command is refused, the store unchanged
+    w = synth.sequential_ranges(3200, n_txns=40)
+    q = w.queries
+    i = next(i for i in range(len(q)) if q.ranges_of(i))
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        st.calculate_partial_deps(q.window(i, i + 1), A.AD_SEQUENTIAL)
+        with pytest.raises(native.AccordDepsError) as e:
+            st.calculate_partial_deps(q.window(i, i + 1), A.AD_SEQUENTIAL)
+        assert e.value.code == A.AD_E_INVAL
+        assert st.calculate_partial_deps(q).n_txns == len(q)
+    finally:
+        st.close()

@@ -129,3 +129,54 @@ def test_range_facts_cleared_by_reload():
         assert e.value.code == A.AD_E_STATE
     finally:
         st.close()
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_range_domain_recovery(oracle, seed):
+    # recovering sync points and range txns over Ranges (BeginRecovery.java:334,348,365,378 hand their
+    # Seekables to mapReduceFull): the CommandsForKeys inside the sliced ranges
+    # (InMemoryCommandStore.java:289-304, CommandsForKey.mapReduceFull :809-908) and the range commands
+    # intersecting them under the four predicate sets (:896-961); sliced stores, both inclusivities,
+    # with and without range commands
+    w = synth.recovery_workload(seed, with_slices=(seed % 3 == 2), start_inclusive=(seed % 4 == 1),
+                                n_range_cmds=(0 if seed % 5 == 4 else 16 + 4 * seed), range_frac=0.6, n_txns=70)
+    assert w.queries.n_ranges > 0
+    _same(w, oracle)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_range_domain_recovery_device(oracle, seed):
+    # the device entry (ad_recovery_batch_device) with Range-domain requests, via the region output
+    w = synth.recovery_workload(40 + seed, n_range_cmds=24, range_frac=0.5, n_txns=90, with_slices=(seed == 1))
+    import torch
+    dev = torch.device("cuda", 0)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        qdev, keep = native.device_queries(w.queries, dev)
+        for s in A.RECOVER_SCANS:
+            res, _ = st.recovery_scan_device(qdev, s)
+            got = st.device_result_to_host(res)
+            exp = oracle.recover(w, s)
+            ok, why = got.equals(exp, detail=True)
+            assert ok, "scan %d: %s" % (s, why)
+    finally:
+        st.close()
+
+
+def test_range_domain_recovery_wide(oracle):
+    # ranges over most of the key line: hundreds of CommandsForKey per request (the K2 scratch and
+    # workgroup build), long segments, many range commands
+    w = synth.recovery_workload(57, n_keys=600, n_hist_txns=1500, n_txns=60, max_keys=5, n_range_cmds=120,
+                                range_frac=1.0)
+    q = w.queries
+    rs, re_ = q.range_start.copy(), q.range_end.copy()
+    for i in range(0, len(q), 3):
+        a, b = int(q.range_off[i]), int(q.range_off[i + 1])
+        if b > a:
+            rs[a:b] = [-600 + 10 * j for j in range(b - a)]
+            re_[a:b] = [-600 + 10 * j + 5 for j in range(b - a)]
+            re_[b - 1] = 600
+    q.range_start, q.range_end = rs, re_
+    assert max(int(q.range_off[i + 1] - q.range_off[i]) for i in range(len(q))) >= 1
+    _same(w, oracle)

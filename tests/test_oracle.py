@@ -357,3 +357,34 @@ def test_preaccept_oracle_empty_maps(oracle):
     assert not got.msb.any() and not got.lsb.any()
     kinds = (q.txn.lsb >> np.uint64(1)) & np.uint64(7)
     assert np.array_equal(fl, np.where(kinds == 4, 4, 1).astype(np.uint8))    # NONE <= every txnId
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_sequential_range_txns_match_model(oracle, seed):
+    # SEQUENTIAL batches with Range-domain txns: each registers as a range command before its deps are
+    # computed (PreAccept.java:116-132, InMemoryCommandStore.java:740-763), sliced to the store and less
+    # its shard-redundant ranges (RedundantBefore.java:216-225); later requests see it. The oracle's
+    # request-by-request restatement against the model's augmented snapshot (refmodel.sequential_augmented)
+    w = synth.sequential_ranges(2000 + seed, n_keys=30 + 2 * seed, n_txns=70, with_slices=(seed % 3 == 1),
+                                start_inclusive=(seed % 4 == 2), n_redundant=(0 if seed % 5 == 4 else 4))
+    q = w.queries
+    assert q.n_ranges > 0
+    seq = oracle.resolve(w)
+    aug = refmodel.sequential_augmented(w)
+    for i in range(len(q)):
+        kd, rd, dd = refmodel.request_pairs(aug, i)
+        got = _request(seq, i)
+        for m, pairs in ((0, kd), (1, rd), (2, dd)):
+            assert got[m] == tuple(refmodel.csr(pairs)), (seed, i, A.MAP_NAMES[m], q.ranges_of(i))
+    # and the oracle's own SNAPSHOT over the augmented store (the identity the library relies on)
+    assert seq.equals(oracle.resolve(aug))
+
+
+def test_sequential_range_txns_seen_by_later_requests(oracle):
+    # a registered range txn is a dependency of later requests on its ranges: some request's rangeDeps
+    # name a txnId of the batch itself
+    w = synth.sequential_ranges(2100, n_keys=40, n_txns=120, range_frac=0.5, n_range_cmds=0)
+    seq = oracle.resolve(w)
+    batch = set(w.queries.txn.tuples())
+    named = sum(1 for i in range(len(w.queries)) for t in _request(seq, i)[1][1] if t in batch)
+    assert named > 0

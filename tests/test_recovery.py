@@ -32,6 +32,43 @@ def test_recovery_crosscheck(oracle, seed, scan, ranges):
 
 
 
+@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("scan", A.RECOVER_SCANS)
+def test_range_domain_recovery_crosscheck(oracle, seed, scan):
+    # recovering Range-domain txns (sync points, range reads/writes: BeginRecovery hands their Ranges to
+    # mapReduceFull, BeginRecovery.java:334,348,365,378): every CommandsForKey inside the sliced ranges
+    # (InMemoryCommandStore.java:289-304) and the range commands intersecting them (:884-958)
+    w = synth.recovery_workload(seed, with_slices=(seed % 3 == 2), start_inclusive=(seed % 4 == 1),
+                                n_range_cmds=(0 if seed % 5 == 4 else 16), range_frac=0.6, n_txns=70)
+    q = w.queries
+    assert q.n_ranges > 0
+    batch = oracle.recover(w, scan)
+    for i in range(len(q)):
+        kd, dd = refmodel.recovery_pairs(w, i, scan)
+        rd = refmodel.recovery_range_pairs(w, i, scan)
+        got = _request(batch, i)
+        for m, pairs in ((0, kd), (1, rd), (2, dd)):
+            assert got[m] == tuple(refmodel.csr(pairs)), (seed, scan, i, A.MAP_NAMES[m], q.ranges_of(i))
+
+
+def test_range_domain_recovery_reaches_every_scan(oracle):
+    # over a few seeds the Range-domain requests emit keyDeps and rangeDeps in every scan
+    tot = {s: [0, 0] for s in A.RECOVER_SCANS}
+    for seed in range(8):
+        w = synth.recovery_workload(seed, n_range_cmds=16, range_frac=0.6, n_txns=70, n_hist_txns=200)
+        q = w.queries
+        isr = [i for i in range(len(q)) if q.ranges_of(i)]
+        for s in A.RECOVER_SCANS:
+            b = oracle.recover(w, s)
+            for i in isr:
+                got = _request(b, i)
+                tot[s][0] += len(got[0][1]) + len(got[2][1])
+                tot[s][1] += len(got[1][1])
+    # scan 1 (WITH) finds no key entries: a Range-domain txnId is never in a CommandsForKey's byId, and an
+    # unknown testTxnId has no witnesses there (CommandsForKey.java:826-836, hasAsDep false)
+    assert all(v[1] > 0 and (v[0] > 0) == (s != 1) for s, v in tot.items()), tot
+
+
 def test_recovery_ranges_reach_every_scan(oracle):
     # the range-command half emits in every scan over a few seeds
     tot = {s: 0 for s in A.RECOVER_SCANS}
