@@ -35,6 +35,13 @@ def workload_arrays(w):
         d["cmds.erased"] = r.erased
     if r.historical is not None:
         d["cmds.historical"] = r.historical
+    if r.rec_status is not None:
+        d["cmds.rec_status"], d["cmds.rec_has_deps"], d["cmds.rec_dep_off"] = r.rec_status, r.rec_has_deps, r.rec_dep_off
+        _put_tids(d, "cmds.rec_exec", r.rec_exec)
+        _put_tids(d, "cmds.rec_deps", r.rec_deps)
+    if c.miss_off is not None:
+        d["cfk.miss_off"] = c.miss_off
+        _put_tids(d, "cfk.miss", c.miss)
     b = w.redundant
     d["rb.start"], d["rb.end"], d["rb.e0"], d["rb.e1"] = b.range_start, b.range_end, b.start_epoch, b.end_epoch
     _put_tids(d, "rb.wm", b.wm)
@@ -44,6 +51,8 @@ def workload_arrays(w):
     d["q.key_off"], d["q.keys"] = q.key_off, q.keys
     if q.min_epoch is not None:
         d["q.min_epoch"] = q.min_epoch
+    if q.range_off is not None:
+        d["q.range_off"], d["q.range_start"], d["q.range_end"] = q.range_off, q.range_start, q.range_end
     if w.slices is not None:
         d["slices"] = np.asarray(w.slices, np.int64)
     d["meta"] = np.frombuffer(json.dumps(dict(name=w.name, flags=int(w.flags), params=w.params,
@@ -54,20 +63,25 @@ def workload_arrays(w):
 
 def arrays_workload(d):
     meta = json.loads(bytes(d["meta"]).decode())
+    miss = "cfk.miss_off" in d
     cfk = CfkSnapshot(d["cfk.keys"], d["cfk.seg"], _tids(d, "cfk.txn"), _tids(d, "cfk.exec"), d["cfk.status"],
-                      _opt(d, "cfk.pruned"))
+                      _opt(d, "cfk.pruned"), _opt(d, "cfk.miss_off"), _tids(d, "cfk.miss") if miss else None)
+    rec = "cmds.rec_status" in d
     cmds = RangeCommands(_tids(d, "cmds.txn"), d["cmds.off"], d["cmds.start"], d["cmds.end"], _opt(d, "cmds.erased"),
-                         _opt(d, "cmds.historical"))
+                         _opt(d, "cmds.historical"), _opt(d, "cmds.rec_status"), _opt(d, "cmds.rec_has_deps"),
+                         _tids(d, "cmds.rec_exec") if rec else None, _opt(d, "cmds.rec_dep_off"),
+                         _tids(d, "cmds.rec_deps") if rec else None)
     rb = Redundant(d["rb.start"], d["rb.end"], d["rb.e0"], d["rb.e1"], _tids(d, "rb.wm"))
-    q = Queries(_tids(d, "q.txn"), _tids(d, "q.exec"), d["q.key_off"], d["q.keys"], _opt(d, "q.min_epoch"))
+    q = Queries(_tids(d, "q.txn"), _tids(d, "q.exec"), d["q.key_off"], d["q.keys"], _opt(d, "q.min_epoch"),
+                _opt(d, "q.range_off"), _opt(d, "q.range_start"), _opt(d, "q.range_end"))
     return Workload(meta["name"], cfk, cmds, rb, q, flags=meta["flags"], params=meta["params"],
                     range_start_inclusive=meta["range_start_inclusive"], slices=_opt(d, "slices"))
 
 
-def batch_arrays(b):
+def batch_arrays(b, prefix=""):
     d = {}
     for m, mm in enumerate(b.maps):
-        p = "out%d." % m
+        p = prefix + "out%d." % m
         d[p + "keys_off"], d[p + "keys"] = mm.keys_off, mm.keys
         if mm.keys_end is not None:
             d[p + "keys_end"] = mm.keys_end
@@ -76,10 +90,10 @@ def batch_arrays(b):
     return d
 
 
-def arrays_batch(d):
+def arrays_batch(d, prefix=""):
     maps = []
     for m in range(3):
-        p = "out%d." % m
+        p = prefix + "out%d." % m
         maps.append(DepsMap(d[p + "keys_off"], d[p + "keys"], _opt(d, p + "keys_end"), d[p + "txn_off"],
                             _tids(d, p + "txn"), d[p + "k2t_off"], d[p + "k2t"]))
     return PartialDepsBatch(maps)

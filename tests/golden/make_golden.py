@@ -7,7 +7,8 @@ reference's known answers (PreAcceptTest, see kats.json) and ported model tests
 (tests/test_oracle.py). They freeze the oracle's answers so that (a) any later change to the
 oracle or the generators is caught, and (b) the GPU path is checked against committed data.
 
-Usage: python tests/golden/make_golden.py          (writes tests/golden/*.npz, MANIFEST.json)
+Usage: python tests/golden/make_golden.py [--all]  (writes the missing tests/golden/*.npz -- every one
+       with --all -- and MANIFEST.json)
 """
 import hashlib
 import json
@@ -36,6 +37,27 @@ def deps_cases():
     yield "config1_n2000", synth.config1(n_txns=2000, n_keys=200), 1
     yield "config2_small", synth.config2(n_txns=2000, n_keys=3000, n_hist_entries=40_000, esp_frac=0.05), 1
     yield "config4_small", synth.config4(n_txns=1500, n_keys=3000, n_ranges=400, n_hist_txns=3000), 1
+    # Range-domain txns (sync points, ExclusiveSyncPoints, range reads / writes over Ranges): SNAPSHOT and
+    # SEQUENTIAL (each registering as a range command), sliced stores, both inclusivities
+    yield "ranges_snapshot_slices", synth.random_small(1010, n_keys=60, n_hist_txns=400, n_txns=160, n_range_cmds=40,
+                                                       n_redundant=5, range_frac=0.5, with_slices=True), 1
+    yield "ranges_snapshot_start_inclusive", synth.random_small(1011, n_keys=60, n_hist_txns=400, n_txns=160,
+                                                                n_range_cmds=40, n_redundant=5, range_frac=0.5,
+                                                                start_inclusive=True), 1
+    yield "ranges_sequential_slices", synth.sequential_ranges(1012, n_keys=60, n_hist_txns=400, n_txns=160,
+                                                              n_range_cmds=40, n_redundant=5, range_frac=0.5,
+                                                              with_slices=True), 1
+    yield "ranges_sequential_start_inclusive", synth.sequential_ranges(1013, n_keys=60, n_hist_txns=400, n_txns=160,
+                                                                       n_range_cmds=40, n_redundant=5, range_frac=0.5,
+                                                                       start_inclusive=True), 1
+
+
+def recovery_cases():
+    """(file stem, workload): the four BeginRecovery scans of key- and Range-domain recovering txns."""
+    yield "recovery_ranges_slices", synth.recovery_workload(1020, n_range_cmds=30, range_frac=0.5, n_txns=100,
+                                                            with_slices=True)
+    yield "recovery_ranges_start_inclusive", synth.recovery_workload(1021, n_range_cmds=30, range_frac=0.5,
+                                                                     n_txns=100, start_inclusive=True)
 
 
 def level_cases():
@@ -45,9 +67,18 @@ def level_cases():
 
 
 def main():
+    # existing fixtures are kept as committed (their hashes are part of the record); --all rewrites them
+    rewrite = "--all" in sys.argv
     pyoracle.build()
-    manifest = {}
+    mpath = os.path.join(HERE, "MANIFEST.json")
+    manifest = {} if rewrite or not os.path.exists(mpath) else json.load(open(mpath))
+
+    def todo(stem):
+        return rewrite or not os.path.exists(os.path.join(HERE, stem + ".npz")) or stem + ".npz" not in manifest
+
     for stem, w, elide in deps_cases():
+        if not todo(stem):
+            continue
         exp = pyoracle.resolve(w, elide=elide)
         d = golden_io.workload_arrays(w)
         d.update(golden_io.batch_arrays(exp))
@@ -55,7 +86,21 @@ def main():
         path = os.path.join(HERE, stem + ".npz")
         np.savez_compressed(path, **d)
         manifest[stem + ".npz"] = dict(kind="deps", requests=len(w.queries), pairs=[exp.pair_count(m) for m in range(3)])
+    for stem, w in recovery_cases():
+        if not todo(stem):
+            continue
+        d = golden_io.workload_arrays(w)
+        pairs = []
+        for scan in range(4):
+            exp = pyoracle.recover(w, scan)
+            d.update(golden_io.batch_arrays(exp, "scan%d." % scan))
+            pairs.append([exp.pair_count(m) for m in range(3)])
+        path = os.path.join(HERE, stem + ".npz")
+        np.savez_compressed(path, **d)
+        manifest[stem + ".npz"] = dict(kind="recovery", requests=len(w.queries), pairs=pairs)
     for stem, g in level_cases():
+        if not todo(stem):
+            continue
         lv = pyoracle.levels(g)
         path = os.path.join(HERE, stem + ".npz")
         np.savez_compressed(path, **golden_io.graph_arrays(g, lv))
