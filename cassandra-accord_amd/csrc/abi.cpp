@@ -201,6 +201,7 @@ struct ad_ctx {
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
     DevBuf q_ro, q_rs, q_re;                   // Range-domain requests: staged ranges
+    DevBuf lg_stage, lg_rec, lg_keys;          // lean gather + build: staged emissions, build records, keys
     DevBuf rq_cnt, rq_off, rq_err, rq_bsum, rq_keys, rq_hi, rq_kind;   // their expansion into probes
     struct SplitBufs {       // per-request / per-probe arrays of the split kernels
         DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
@@ -1810,6 +1811,12 @@ static int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
 // e.g. a store's share of requests spanning many stores), else two. AD_LEAN_RPW overrides.
 // requests per wave of lean pass 1 by the batch's keys per request: 8 (<= 1.5 on average: a store's
 // share of requests spanning many stores), 4 (<= 3), else 2
+static bool lean_gb_on()
+{
+    static const bool on = getenv("AD_LEAN_GB") == nullptr || atoi(getenv("AD_LEAN_GB")) != 0;
+    return on;
+}
+
 static uint32_t lean_rpw1(uint64_t n, uint64_t np)
 {
     if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 8 ? 8u : (atoi(e) == 4 ? 4u : 2u);
@@ -1943,6 +1950,17 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         b.p_slot = c->p_slot.as<uint32_t>();
         b.slots_by_prepare = getenv("AD_SLOTS_KERNEL") == nullptr;     // measurement switch: the separate launch
     }
+    // lean pass 1 as gather + build (two requests per build wave, no range commands): AD_LEAN_GB=0 keeps
+    // the single fused pass
+    const bool gb = lean && !c->ds.n_rent && lean_rpw1(n, np) == 2 && lean_gb_on();
+    if (gb)
+    {
+        if (!ens<uint32_t>(c->lg_stage, n * 64) || !ens<uint4>(c->lg_rec, n) || !ens<int64_t>(c->lg_keys, n * 8))
+            return c->fail(AD_E_NOMEM, "lean stage");
+        b.lg_stage = c->lg_stage.as<uint32_t>();
+        b.lg_rec = c->lg_rec.as<uint4>();
+        b.lg_keys = c->lg_keys.as<int64_t>();
+    }
     if (const char* e = getenv("AD_K2_BIG")) b.k2_big = (uint32_t)strtoul(e, nullptr, 10);   // tests: force k_build_big
     b.q_rec = c->q_rec.as<uint4>();
     b.deferred1 = c->deferred1.as<uint32_t>();
@@ -2023,13 +2041,23 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 // takes only what it deferred (count read on the device, no host round trip)
                 if (!c->ev_lean1) HIPCHK(c, timing_event(&c->ev_lean1));
                 const uint32_t rpw1 = lean_rpw1(n, np);
-                const bool wide1 = rpw1 == 2 && !c->ds.n_rent && lean_wide1(c);
-                c->lean_ran_wide = wide1;
-                lean_track = rpw1 == 2 && !c->ds.n_rent;
-                HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
-                if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
-                HIPCHK(c, run_resolve_lean(c->ds, b, 2, 0, false, st));
-                if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
+                if (gb)
+                {
+                    // gather + build (k_lean_gather, k_lean_build): the rest to the general kernel
+                    HIPCHK(c, run_lean_gb(c->ds, b, st));
+                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
+                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
+                }
+                else
+                {
+                    const bool wide1 = rpw1 == 2 && !c->ds.n_rent && lean_wide1(c);
+                    c->lean_ran_wide = wide1;
+                    lean_track = rpw1 == 2 && !c->ds.n_rent;
+                    HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
+                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
+                    HIPCHK(c, run_resolve_lean(c->ds, b, 2, 0, false, st));
+                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
+                }
                 BatchBufs b2 = b;
                 b2.req_list = b.deferred2;
                 b2.req_count = &b.ctl->n_deferred2;

@@ -45,6 +45,9 @@ struct BatchBufs {
     const uint8_t* p_kind;
     const int64_t* q_keys_hi;
     uint32_t* p_slot;                // lean passes without range commands: per probe its KeyLine (LS_NONE: outside the slice)
+    // lean pass 1 as gather + build (run_lean_gb): per request 64 staged raw emissions, its build record
+    // {raw count | #keys << 8 | deferred << 31, eight per-key start bytes}, its keys
+    uint32_t* lg_stage; uint4* lg_rec; int64_t* lg_keys;
     uint32_t slots_by_prepare;       // p_slot filled by k_prepare (one launch for records and slots)
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
@@ -175,6 +178,9 @@ hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // pass 1 with rpw1 = 2 on a store without range commands: wide1 selects the wide kernel (requests of up to
 // 64 raw emissions) over the narrow one (up to 32; the rest to pass 2)
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, bool wide1, hipStream_t st);
+// lean pass 1 (and 2) as k_lean_gather + k_lean_build, stores without range commands: requests it cannot
+// serve are appended to deferred2 (the general kernel's list)
+hipError_t run_lean_gb(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 
 // ---- PreAccept timestamp proposal (preaccept.hip)
 struct DevRangeMap {            // a ReducingRangeMap<Timestamp> in HBM (ad_range_map_soa)

@@ -982,4 +982,380 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     return s.n_rent ? launch_lean<1, true, false, 2>(s, b, st) : launch_lean<2, false, true, 2>(s, b, st);
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// Lean pass 1 as two kernels (LEAN_GB, stores without range commands, two requests per build wave):
+//
+//   k_lean_gather: one lane per (request, key) probe, eight requests per wave iteration -- the
+//     request record, the key and its KeyLine, the newest test, the emission counts (the loop body of
+//     mapReduceActive with end = insertPos(S) and M = the key's last committed Write's executeAt,
+//     CommandsForKey.java:910-950) -- and the raw emissions copied, already filtered by txnId < S
+//     (STARTED_BEFORE) and the request's own id (PreAccept.java:258), into a fixed 64-word stage per
+//     request; per request a build record {raw count, #keys, per-key starts} and its keys. Requests the
+//     lean path cannot serve (a key needing the tree, > 64 raw emissions, > 8 keys) go to the general
+//     kernel's list.
+//   k_lean_build: two requests per wave, 32 lanes each -- the Deps.AbstractBuilder.add routing
+//     (Deps.java:80-106) and the RelationMultiMap build (RelationMultiMap.java:147-260) of the staged
+//     lists: (rank, key) bitonic sort per map, ballot dedup, CSR regions. Its inputs sit at fixed offsets
+//     from the request index, so its loads issue two items ahead with no dependent chain.
+//
+// The single fused pass waited one dependent memory round trip (record -> keys -> line -> elements) per
+// two requests; here the gather moves four times the probes per round trip at low register pressure, and
+// the build's loads never wait on each other.
+// ---------------------------------------------------------------------------------------------------
+#ifndef GB_OCC_G
+#define GB_OCC_G 8
+#endif
+#ifndef GB_OCC_B
+#define GB_OCC_B 6
+#endif
+constexpr uint32_t GB_STAGE = 64;           // staged raw emissions per request (words)
+constexpr uint32_t GB_INVALID = 0xFFFFFFFFu;  // a staged element filtered out (txnId >= S or the request's own)
+constexpr uint32_t GB_DEFER = 1u << 31;     // build record: the request went to the general kernel
+
+__global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_G) void k_lean_gather(DevSnapshot s, BatchBufs b)
+{
+    const uint32_t lane = lane_id(), h = lane >> 3, j = lane & 7u, sb8 = h * 8;
+    const uint64_t n = b.n_txns;
+    const uint32_t n_groups = (uint32_t)((n + 7) / 8);
+    const uint32_t nw = gridDim.x * LEAN_WAVES;
+    __shared__ uint32_t dbuf_all[LEAN_WAVES][DEFER_CHUNK];
+    uint32_t* dbuf = dbuf_all[threadIdx.x >> 6];
+    uint32_t dn = 0;
+    auto dflush = [&]() {
+        if (!dn) return;
+        unsigned long long base = 0;
+        if (lane_id() == 0)
+        {
+            base = atomicAdd(&b.ctl->n_deferred2, (unsigned long long)dn);
+            atomicAdd(&b.ctl->n_real2, (unsigned long long)dn);
+        }
+        base = uniform64(base);
+        wave_lds_sync();
+        if (lane_id() < dn) b.deferred2[base + lane_id()] = dbuf[lane_id()];
+        wave_lds_sync();
+        dn = 0;
+    };
+    for (uint32_t g = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6)); g < n_groups; g += nw)
+    {
+        const uint64_t t = (uint64_t)g * 8 + h;
+        const bool act = t < n;
+        const uint4 rec = b.q_rec[act ? t : 0];
+        const uint32_t k0 = rec.x, S = rec.y, np = rec.z & 0xFFFFu, cls = (rec.z >> 16) & 3u, self = rec.w;
+        const bool fast = (rec.z & REC_FAST) != 0;
+        const bool kact = act && fast && j < np;
+        const int64_t key = b.q_keys[kact ? (uint64_t)k0 + j : 0];
+        const uint32_t sl0 = b.p_slot[kact ? (uint64_t)k0 + j : 0];
+        const uint32_t sl = kact ? sl0 : LS_NONE;
+        if (kact) b.lg_keys[t * 8 + j] = key;
+        // the key's line: key, newest fields and meta, the class's {count, start}, {cwr tail, prunedBefore}
+        const bool look = sl != LS_NONE;
+        const uint4* L4 = reinterpret_cast<const uint4*>(s.kline + (look ? sl : 0u));
+        const uint4 q0 = L4[0], q1 = L4[1];
+        const uint2 qc = reinterpret_cast<const uint2*>(L4 + 2)[cls], q3 = reinterpret_cast<const uint2*>(L4 + 3)[1];
+        const uint32_t meta = q1.w;
+        const bool found = look && (meta & KL_USED) && (int64_t)(((uint64_t)q0.y << 32) | q0.x) == key;
+        // lean-served (as lean pass 1): the last committed Write executes before S, S above prunedBefore
+        const bool newest = !found || (q1.y < S && (q3.y == 0 || S > q3.y) && !(meta & KL_NOLEAN));
+        const uint32_t n1 = found ? qc.x : 0u;
+        const uint32_t n2 = !found ? 0u : (cls == 0 ? (q1.z != 0 ? 1u : 0u) : (meta & KL_NCWR_MASK));
+        const uint32_t nn = kact ? n1 + n2 : 0u;
+        const uint32_t inc = key_lanes_incl_scan(nn, j);
+        const uint32_t start = inc - nn;
+        const uint32_t T = (uint32_t)__shfl((int)inc, (int)(sb8 | 7u), 64);
+        const uint64_t seg8 = (ballot(kact && !newest) >> sb8) & 0xFFull;
+        const bool defer = act && (!fast || seg8 != 0 || T > GB_STAGE);
+        {
+            const uint64_t dm = ballot(defer && j == 0);
+            const uint32_t nd = __popcll(dm);
+            if (nd)
+            {
+                if (dn + nd > DEFER_CHUNK) dflush();
+                if (defer && j == 0) dbuf[dn + __popcll(dm & ((1ull << lane) - 1))] = (uint32_t)t;
+                dn += nd;
+            }
+        }
+        // build record: raw count | #keys << 8 | deferred, then the eight per-key starts (bytes)
+        if (act)
+        {
+            uint8_t* r8 = reinterpret_cast<uint8_t*>(b.lg_rec + t);
+            r8[4 + j] = (uint8_t)start;
+            if (j == 0) *reinterpret_cast<uint32_t*>(r8) = (defer ? GB_DEFER : 0u) | (np << 8) | (defer ? 0u : T);
+        }
+        // the raw emissions: never-elided entries of the class (cand), then the class Ws's last Write or the
+        // committed Read/Writes from the last committed Write on (cwr tail); inline in the line when they fit
+        const bool copy = act && !defer && nn > 0;
+        // wave-uniform max of the lanes' counts (<= 64): binary search by ballots
+        const uint32_t ncopy = copy ? nn : 0u;
+        uint32_t nmax = 0;
+#pragma unroll
+        for (uint32_t bit = 64; bit; bit >>= 1)
+            if (ballot(ncopy >= nmax + bit)) nmax += bit;
+        if (nmax == 0) continue;
+        const bool inl = (meta & KL_INLINE) != 0;
+        const uint32_t inl_cwr = (meta >> KL_INL_SHIFT) & 31u;
+        const uint32_t* cand_p = inl ? s.kline[look ? sl : 0u].inl : s.cand + qc.y;
+        const uint32_t* cwr_p = inl ? s.kline[look ? sl : 0u].inl + inl_cwr : s.cwr + q3.x;
+        const uint32_t lastw = q1.z | (1u << RANK_BITS);
+        uint32_t* dst = b.lg_stage + t * GB_STAGE + start;
+        for (uint32_t i0 = 0; i0 < nmax; i0 += 4)
+        {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+            {
+                const uint32_t i = i0 + u;
+                const bool on = copy && i < nn;
+                const bool fc = i < n1;
+                const uint32_t* src = !on ? s.cand : (fc ? cand_p + i : (cls == 0 ? s.cand : cwr_p + (i - n1)));
+                const uint32_t x = *src;
+                v[u] = (!fc && cls == 0) ? lastw : x;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+            {
+                const uint32_t i = i0 + u;
+                if (copy && i < nn)
+                {
+                    const uint32_t r = v[u] & RANK_MASK;
+                    dst[i] = (r < S && r != self) ? v[u] : GB_INVALID;
+                }
+            }
+        }
+    }
+    dflush();
+}
+
+__global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_B) void k_lean_build(BatchBufs b)
+{
+    constexpr uint32_t LPR = 32;
+    const uint32_t lane = lane_id(), h = lane >> 5, hl = lane & 31u, sb = h * LPR;
+    const uint64_t below = (1ull << hl) - 1;
+    auto seg = [&](uint64_t m) -> uint64_t { return (m >> sb) & 0xFFFFFFFFull; };
+    const uint64_t n = b.n_txns;
+    const uint32_t n_items = (uint32_t)((n + 1) / 2);
+    const uint32_t nw = gridDim.x * LEAN_WAVES;
+    const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
+    LeanChunk ralloc;
+    auto seg_alloc = [&](uint64_t bytes, bool& fits, uint32_t it) -> uint64_t {
+        const uint64_t b0 = uniform64(__shfl(bytes, 0, 64)), b1 = uniform64(__shfl(bytes, 32, 64));
+        const uint64_t base = ralloc.template take<1>(b.ctl, b0 + b1, reg_cap, it, n_items, nw);
+        fits = base + b0 + b1 <= reg_cap;
+        return base + (h ? b0 : 0);
+    };
+    auto put_sizes = [&](bool on, uint64_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro, bool with_ro) {
+        if (on && hl < 3)
+        {
+            const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);
+            b.sz[(uint64_t)(3 * m + hl) * n + t] = v;
+        }
+        if (with_ro && on && hl == 3) b.t_reg[(uint64_t)m * n + t] = ro;
+    };
+    // an item's inputs, all at fixed offsets from its request index: the build record, the first 32
+    // staged elements, the key of lane hl & 7
+    struct In { uint4 r; uint32_t e0; int64_t key; };
+    auto load = [&](uint32_t it) -> In {
+        const uint64_t t = (uint64_t)it * 2 + h;
+        const uint64_t tt = t < n ? t : 0;
+        In x;
+        x.r = b.lg_rec[tt];
+        x.e0 = b.lg_stage[tt * GB_STAGE + hl];
+        x.key = b.lg_keys[tt * 8 + (hl & 7u)];
+        return x;
+    };
+    const uint32_t it0 = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6));
+    In c0 = load(it0), c1 = load(it0 + nw);
+    for (uint32_t it = it0; it < n_items; it += nw)
+    {
+        const In cur = c0;
+        c0 = c1;
+        c1 = load(it + 2 * nw);
+        const uint64_t t = (uint64_t)it * 2 + h;
+        const uint32_t x = cur.r.x;
+        const bool act = t < n && !(x & GB_DEFER);
+        const uint32_t T = act ? (x & 0xFFu) : 0u, np = (x >> 8) & 0xFu;
+        // per-key starts (bytes of r.y, r.z), the key lane's own start and raw count
+        auto start_of = [&](uint32_t p) -> uint32_t { return ((p < 4 ? cur.r.y : cur.r.z) >> (8 * (p & 3))) & 0xFFu; };
+        const uint32_t kj = hl & 7u;
+        const uint32_t start = start_of(kj);
+        const uint32_t nn = !act || hl >= 8 || kj >= np ? 0u : (kj + 1 < np ? start_of(kj + 1) : T) - start;
+        // the key of element e: the last key whose start is at or below e
+        auto key_of = [&](uint32_t e) -> uint32_t {
+            uint32_t a = 0;
+#pragma unroll
+            for (uint32_t p = 1; p < LEAN_MAXP; ++p)
+                if (p < np && e >= start_of(p)) a = p;
+            return a;
+        };
+        const int64_t key = cur.key;
+        const uint32_t tmax = max(uniform(__builtin_amdgcn_readlane((int)T, 0)), uniform(__builtin_amdgcn_readlane((int)T, 32)));
+        if (tmax > LPR)
+        {
+            // a request of 33..64 raw emissions in the item: two per lane (element x = hl and hl + 32)
+            const uint32_t e1 = b.lg_stage[(t < n ? t : 0) * GB_STAGE + LPR + hl];
+            const uint32_t tw0 = act && hl < T ? cur.e0 : GB_INVALID, tw1 = act && hl + 32 < T ? e1 : GB_INVALID;
+            const uint32_t ax0 = key_of(hl), ax1 = key_of(hl + 32);
+            const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
+            const bool want0 = tw0 != GB_INVALID, want1 = tw1 != GB_INVALID;
+            const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
+            const bool is1_1 = ((KINDS_RS_OR_WS >> (tw1 >> RANK_BITS)) & 1) == 0;
+            for (int m = 0; m < 3; m += 2)
+            {
+                const bool mine0 = want0 && (m == 0 ? !is1_0 : is1_0), mine1 = want1 && (m == 0 ? !is1_1 : is1_1);
+                const uint64_t mb0 = ballot(mine0), mb1 = ballot(mine1);
+                const uint32_t tot = __popcll(seg(mb0)) + __popcll(seg(mb1));
+                if ((mb0 | mb1) == 0)
+                {
+                    put_sizes(act, t, m, 0, 0, 0, 0, false);
+                    continue;
+                }
+                uint32_t k0 = mine0 ? ((r0 << 3) | ax0) : 0xFFFFFFFFu, k1 = mine1 ? ((r1 << 3) | ax1) : 0xFFFFFFFFu;
+                seg_bitonic_wide(k0, k1);
+                const bool v0 = hl < tot, v1 = hl + 32 < tot;
+                const uint32_t x0 = k0 >> 3, x1 = k1 >> 3, ka0 = k0 & 7u, ka1 = k1 & 7u;
+                const uint32_t p0 = wave_up1(k0);
+                const uint32_t last0 = __shfl(k0, (int)(sb | 31u), 64);
+                const uint32_t up1 = wave_up1(k1);
+                const uint32_t p1 = hl == 0 ? last0 : up1;
+                const bool u0 = v0 && (hl == 0 || (p0 >> 3) != x0);
+                const bool u1 = v1 && (p1 >> 3) != x1;
+                const uint64_t um0 = seg(ballot(u0)), um1 = seg(ballot(u1));
+                const uint32_t nu0 = __popcll(um0);
+                const uint32_t U = nu0 + __popcll(um1);
+                const uint32_t ur0 = __popcll(um0 & below) + (u0 ? 1u : 0u) - 1u;
+                const uint32_t ur1 = nu0 + __popcll(um1 & below) + (u1 ? 1u : 0u) - 1u;
+                uint64_t s00 = ballot(v0), s01 = ballot(v0), s11 = ballot(v1);
+#pragma unroll
+                for (int bit = 0; bit < 3; ++bit)
+                {
+                    const uint64_t b0 = ballot((ka0 >> bit) & 1u), b1 = ballot((ka1 >> bit) & 1u);
+                    s00 &= ((ka0 >> bit) & 1u) ? b0 : ~b0;
+                    s01 &= ((ka1 >> bit) & 1u) ? b0 : ~b0;
+                    s11 &= ((ka1 >> bit) & 1u) ? b1 : ~b1;
+                }
+                const uint32_t pk0 = __popcll(seg(s00) & below);
+                const uint32_t pk1 = __popcll(seg(s01)) + __popcll(seg(s11) & below);
+                const uint64_t raw_m = seg(mb0) | (seg(mb1) << 32);
+                const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
+                const uint32_t cnt = hl < 8 ? (uint32_t)__popcll(raw_m & rmask) : 0u;
+                const uint32_t cinc = key_lanes_incl_scan(cnt, hl);
+                const uint32_t kstart_l = cinc - cnt;
+                const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
+                const uint32_t nk = __popcll(nem);
+                const uint32_t kk = __popcll(nem & below);
+                const uint32_t kst0 = __shfl(kstart_l, sb | ka0, 64), kst1 = __shfl(kstart_l, sb | ka1, 64);
+                const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
+                bool fits;
+                const uint64_t ro = seg_alloc(bytes, fits, it);
+                put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
+                if (act && tot && fits)
+                {
+                    int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                    uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
+                    int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
+                    if (hl < 8 && cnt > 0)
+                    {
+                        okeys[kk] = key;
+                        ok2t[kk] = (int32_t)(nk + kstart_l + cnt);
+                    }
+                    if (u0) otx[ur0] = (x0 - 1) >> 1;
+                    if (u1) otx[ur1] = (x1 - 1) >> 1;
+                    if (v0) ok2t[nk + kst0 + pk0] = (int32_t)ur0;
+                    if (v1) ok2t[nk + kst1 + pk1] = (int32_t)ur1;
+                }
+            }
+            put_sizes(act, t, 1, 0, 0, 0, 0, false);
+            continue;
+        }
+        // one raw emission per lane
+        const uint32_t a = key_of(hl);
+        const uint32_t txw = act && hl < T ? cur.e0 : GB_INVALID;
+        const bool want = txw != GB_INVALID;
+        const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
+        const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;       // !managesExecution -> directKeyDeps
+        for (int m = 0; m < 3; m += 2)
+        {
+            const bool mine = want && (m == 0 ? !is1 : is1);
+            const uint64_t mb = ballot(mine);
+            const uint32_t tot = __popcll(seg(mb));
+            if (mb == 0)
+            {
+                put_sizes(act, t, m, 0, 0, 0, 0, false);
+                continue;
+            }
+            uint32_t k = mine ? ((r << 3) | a) : 0xFFFFFFFFu;
+            if (tmax <= 8) seg_bitonic<8, LPR>(k);
+            else if (tmax <= 16) seg_bitonic<16, LPR>(k);
+            else seg_bitonic<32, LPR>(k);
+            const bool valid = hl < tot;
+            const uint32_t xr = k >> 3, ka = k & 7u;
+            const uint32_t prev = wave_up1(k);
+            const bool uniq = valid && (hl == 0 || (prev >> 3) != xr);
+            const uint64_t um = seg(ballot(uniq));
+            const uint32_t U = __popcll(um);
+            const uint32_t ur = __popcll(um & below) + (uniq ? 1u : 0u) - 1u;
+            uint64_t same = ballot(valid);
+#pragma unroll
+            for (int bit = 0; bit < 3; ++bit)
+            {
+                const uint64_t bb = ballot((ka >> bit) & 1u);
+                same &= ((ka >> bit) & 1u) ? bb : ~bb;
+            }
+            const uint32_t pos_in_key = __popcll(seg(same) & below);
+            const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
+            const uint32_t cnt = hl < 8 ? (uint32_t)__popcll(seg(mb) & rmask) : 0u;
+            const uint32_t cinc = key_lanes_incl_scan(cnt, hl);
+            const uint32_t kstart_l = cinc - cnt;
+            const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
+            const uint32_t nk = __popcll(nem);
+            const uint32_t kk = __popcll(nem & below);
+            const uint32_t kstart = __shfl(kstart_l, sb | ka, 64);
+            const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
+            bool fits;
+            const uint64_t ro = seg_alloc(bytes, fits, it);
+            put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
+            if (act && tot && fits)
+            {
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
+                if (hl < 8 && cnt > 0)
+                {
+                    okeys[kk] = key;
+                    ok2t[kk] = (int32_t)(nk + kstart_l + cnt);     // absolute end offsets (RelationMultiMap.java:245-257)
+                }
+                if (uniq) otx[ur] = (xr - 1) >> 1;                  // dictionary index of the TxnId
+                if (valid) ok2t[nk + kstart + pos_in_key] = (int32_t)ur;
+            }
+        }
+        put_sizes(act, t, 1, 0, 0, 0, 0, false);              // no range commands on this path
+    }
+}
+
+hipError_t run_lean_gb(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
+{
+    if (!b.n_txns) return hipSuccess;
+    if (!b.p_slot || !b.lg_stage || !b.lg_rec || !b.lg_keys || s.n_rent) return hipErrorInvalidValue;
+    if (!b.slots_by_prepare && b.n_probes)
+        k_lean_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b.q_keys, b.n_probes, b.p_slot);
+    static int per_cu_g = 0, per_cu_b = 0;
+    if (!per_cu_g)
+    {
+        int nb = 0;
+        per_cu_g = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_gather, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
+        nb = 0;
+        per_cu_b = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_build, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
+        if (const char* e = getenv("AD_GB_PER_CU_G")) per_cu_g = std::max(1, std::min(per_cu_g, atoi(e)));
+        if (const char* e = getenv("AD_GB_PER_CU_B")) per_cu_b = std::max(1, std::min(per_cu_b, atoi(e)));
+    }
+    const uint64_t cus = (uint64_t)device_cu_count();
+    const uint64_t need_g = ((b.n_txns + 7) / 8 + LEAN_WAVES - 1) / LEAN_WAVES;
+    const unsigned grid_g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need_g, cus * per_cu_g));
+    k_lean_gather<<<grid_g, 64 * LEAN_WAVES, 0, st>>>(s, b);
+    const uint64_t need_b = ((b.n_txns + 1) / 2 + LEAN_WAVES - 1) / LEAN_WAVES;
+    const unsigned grid_b = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need_b, cus * per_cu_b));
+    k_lean_build<<<grid_b, 64 * LEAN_WAVES, 0, st>>>(b);
+    return hipGetLastError();
+}
+
 }  // namespace adx
