@@ -201,7 +201,7 @@ struct ad_ctx {
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
     DevBuf q_ro, q_rs, q_re;                   // Range-domain requests: staged ranges
-    DevBuf lg_stage, lg_rec, lg_keys;          // lean gather + build: staged emissions, build records, keys
+    DevBuf lg_stage, lg_rec, lg_keys, lg_dummy;   // lean gather + build: staged emissions, build records, keys
     DevBuf rq_cnt, rq_off, rq_err, rq_bsum, rq_keys, rq_hi, rq_kind;   // their expansion into probes
     struct SplitBufs {       // per-request / per-probe arrays of the split kernels
         DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
@@ -923,9 +923,10 @@ static int build_snapshot_device(ad_ctx* c)
     phase("derivation + trees");
     DevSnapshot& s = c->ds;
     HIPCHK(c, build_range_trees(s, st));
-    if (!c->d_kline.ensure(sizeof(KeyLine) * c->kline_slots)) return c->fail(AD_E_NOMEM, "key lines");
+    if (!c->d_kline.ensure(kline_table_bytes(c->kline_slots))) return c->fail(AD_E_NOMEM, "key lines");
     s.kline = c->d_kline.as<KeyLine>();
     s.kl_lines = c->kline_slots;
+    s.kquad = kline_quads(s.kline, c->kline_slots);
     s.kl_buckets = kl_nb;
     s.kl_disp = c->d_kl_disp.as<uint32_t>();
     HIPCHK(c, run_build_klines(s, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
@@ -1377,9 +1378,10 @@ static int build_snapshot_host(ad_ctx* c)
     HIPCHK(c, build_cfk_trees(s, c->stream));
     HIPCHK(c, build_range_trees(s, c->stream));
     // the lean kernels' KeyLine table, indexed by the keys' perfect hash
-    if (!c->d_kline.ensure(sizeof(KeyLine) * c->kline_slots)) return c->fail(AD_E_NOMEM, "key lines");
+    if (!c->d_kline.ensure(kline_table_bytes(c->kline_slots))) return c->fail(AD_E_NOMEM, "key lines");
     s.kline = c->d_kline.as<KeyLine>();
     s.kl_lines = c->kline_slots;
+    s.kquad = kline_quads(s.kline, c->kline_slots);
     s.kl_buckets = kl_nb;
     s.kl_disp = c->d_kl_disp.as<uint32_t>();
     HIPCHK(c, run_build_klines(s, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
@@ -1811,10 +1813,14 @@ static int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
 // e.g. a store's share of requests spanning many stores), else two. AD_LEAN_RPW overrides.
 // requests per wave of lean pass 1 by the batch's keys per request: 8 (<= 1.5 on average: a store's
 // share of requests spanning many stores), 4 (<= 3), else 2
+// Lean pass 1 as gather + build (k_lean_gather, k_lean_build): opt-in, AD_LEAN_GB=1. Measured on config 2
+// (DESIGN §4): gather 0.19-0.30 ms + build 0.36 + wide build 0.15 against 0.54 ms for the fused pass -- the
+// build alone is issue-bound (its SIMDs ~98 % busy at ~390 VALU per two requests), so the split buys no
+// latency hiding the fused pass lacks
 static bool lean_gb_on()
 {
-    static const bool on = getenv("AD_LEAN_GB") == nullptr || atoi(getenv("AD_LEAN_GB")) != 0;
-    return on;
+    const char* e = getenv("AD_LEAN_GB");
+    return e && atoi(e) != 0;
 }
 
 static uint32_t lean_rpw1(uint64_t n, uint64_t np)
@@ -1955,8 +1961,10 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     const bool gb = lean && !c->ds.n_rent && lean_rpw1(n, np) == 2 && lean_gb_on();
     if (gb)
     {
-        if (!ens<uint32_t>(c->lg_stage, n * 64) || !ens<uint4>(c->lg_rec, n) || !ens<int64_t>(c->lg_keys, n * 8))
+        if (!ens<uint32_t>(c->lg_stage, n * 64) || !ens<uint4>(c->lg_rec, n) || !ens<int64_t>(c->lg_keys, n * 8) ||
+            !ens<uint64_t>(c->lg_dummy, (uint64_t)device_cu_count() * 64 * 16))
             return c->fail(AD_E_NOMEM, "lean stage");
+        b.lg_dummy = c->lg_dummy.as<uint64_t>();
         b.lg_stage = c->lg_stage.as<uint32_t>();
         b.lg_rec = c->lg_rec.as<uint4>();
         b.lg_keys = c->lg_keys.as<int64_t>();
@@ -4041,10 +4049,11 @@ static int cfk_after_new_keys(ad_ctx* c, const CfkUpdOut& o, hipStream_t st)
     }
     if (int rc = upload(c, c->d_kl_disp, c->kl_disp_h)) return rc;
     if (!c->d_kslot.ensure(4 * nk + 4 * (nk / 8))) return c->fail(AD_E_NOMEM, "key slots");
-    if (!c->d_kline.ensure(sizeof(KeyLine) * c->kline_slots)) return c->fail(AD_E_NOMEM, "key lines");
+    if (!c->d_kline.ensure(kline_table_bytes(c->kline_slots))) return c->fail(AD_E_NOMEM, "key lines");
     DevSnapshot& s = c->ds;
     s.kline = c->d_kline.as<KeyLine>();
     s.kl_lines = c->kline_slots;
+    s.kquad = kline_quads(s.kline, c->kline_slots);
     s.kl_buckets = c->kl_nb_h;
     s.kl_disp = c->d_kl_disp.as<uint32_t>();
     HIPCHK(c, run_key_slots(c->d_keys.as<int64_t>(), nk, c->d_kl_disp.as<uint32_t>(), c->kl_nb_h, c->kline_slots,

@@ -151,6 +151,22 @@ constexpr uint32_t KL_NOLEAN = 1u << 29;          // counts beyond the meta fiel
 constexpr uint32_t KL_NCWR_MASK = (1u << 24) - 1;
 constexpr uint32_t KL_INL_SHIFT = 24;             // 5 bits (<= KL_INL)
 
+// Per key line, beside its KeyLine (same perfect-hash index): what one (request, key) probe of witness
+// class c needs in one 16-byte load -- {thr, counts, base1, base2}: the request is served lean iff
+// S > thr (thr = max(last committed Write's executeAt, prunedBefore) ranks; ~0 when the lean path cannot
+// serve the key), its raw emissions are n1 = counts & 0x7F entries at base1 (class c's never-elided list)
+// then n2 = (counts >> 8) & 0x7F at base2 (class Ws: the last committed Write itself, base2 being its txw;
+// else the cwr tail); LQ_INLINE: both runs are word indices into the KeyLine table (its inline part) instead
+// of cand / cwr. key / used: the slot's key (k_prepare's membership test).
+constexpr uint32_t LQ_INLINE = 1u << 16;
+constexpr uint32_t LQ_NMAX = 0x7F;
+struct alignas(64) LeanQuads {
+    uint4 q[NCLASS];
+    int64_t key;
+    uint32_t used, pad;
+};
+static_assert(sizeof(LeanQuads) == 64, "LeanQuads is half a cache line");
+
 __host__ __device__ inline uint64_t key_hash(int64_t k)
 {
     uint64_t z = (uint64_t)k + 0x9E3779B97F4A7C15ULL;
@@ -207,6 +223,7 @@ struct DevSnapshot {
     const KeySlot*  khash;         // [khash_mask + 1]
     const KeyEntry* kent;          // [n_keys] newest-test fields + list bounds (fused kernels)
     const KeyLine*  kline;         // [kl_lines] the lean kernels' per-key lines (perfect hash)
+    const LeanQuads* kquad;        // [kl_lines] beside them: per class the probe's 16 bytes, the key
     const uint32_t* kl_disp;       // [kl_buckets] displacements
     uint64_t kl_lines, kl_buckets;
     const uint32_t* cand;          // never-elided entries per key and class: txw (rank | kind << 29)

@@ -1841,8 +1841,11 @@ hipError_t run_collect_totals(const BatchBufs& b, hipStream_t st)
 
 // The lean kernels' KeyLine of every key (common.hpp), from the KeyEntry (newest fields, class
 // lists) and the emission lists; thread per key, written to the key's slot (empty slots: meta 0).
+__device__ __forceinline__ uint32_t n2_inl_off(uint32_t meta) { return (meta >> KL_INL_SHIFT) & 31u; }
+
 __global__ __launch_bounds__(256) void k_build_klines(DevSnapshot s, const uint32_t* __restrict__ kslot,
-                                                      const uint32_t* __restrict__ kcell, KeyLine* __restrict__ out)
+                                                      const uint32_t* __restrict__ kcell, KeyLine* __restrict__ out,
+                                                      LeanQuads* __restrict__ kquad)
 {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s.n_keys) return;
@@ -1884,6 +1887,23 @@ __global__ __launch_bounds__(256) void k_build_klines(DevSnapshot s, const uint3
     }
     L.meta = meta;
     out[kslot[k]] = L;
+    // the probe quads (LeanQuads): the newest threshold, per class the two emission runs
+    LeanQuads Q;
+    const bool inl = (meta & KL_INLINE) != 0;
+    const uint32_t thr0 = max(L.last_wexec, L.pruned);
+    const uint32_t wbase = kslot[k] * (uint32_t)(sizeof(KeyLine) / 4) + (uint32_t)(offsetof(KeyLine, inl) / 4);
+    for (int c = 0; c < NCLASS; ++c)
+    {
+        const uint32_t n1 = L.cls[c].n, n2 = c == 0 ? (L.last_w_txn != 0 ? 1u : 0u) : n_cwr;
+        const bool lean = !(meta & KL_NOLEAN) && n1 <= LQ_NMAX && n2 <= LQ_NMAX;
+        const uint32_t b1 = inl ? wbase : L.cls[c].base;
+        const uint32_t b2 = c == 0 ? (L.last_w_txn | (1u << RANK_BITS)) : (inl ? wbase + n2_inl_off(meta) : L.cwr_tail);
+        Q.q[c] = make_uint4(lean ? thr0 : 0xFFFFFFFFu, lean ? (n1 | (n2 << 8) | (inl ? LQ_INLINE : 0u)) : 0u, b1, b2);
+    }
+    Q.key = L.key;
+    Q.used = 1;
+    Q.pad = 0;
+    kquad[kslot[k]] = Q;
 }
 
 __global__ void k_key_slots(const int64_t* __restrict__ keys, uint64_t nk, const uint32_t* __restrict__ disp, uint64_t nb,
@@ -1904,9 +1924,11 @@ hipError_t run_key_slots(const int64_t* keys, uint64_t nk, const uint32_t* disp,
 hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const uint32_t* kcell, KeyLine* table,
                             uint64_t table_slots, hipStream_t st)
 {
-    hipError_t e = hipMemsetAsync(table, 0, sizeof(KeyLine) * table_slots, st);
+    // the LeanQuads sit right after the KeyLines (one allocation: kline_table_bytes)
+    LeanQuads* quads = reinterpret_cast<LeanQuads*>(table + table_slots);
+    hipError_t e = hipMemsetAsync(table, 0, kline_table_bytes(table_slots), st);
     if (e != hipSuccess || !s.n_keys) return e;
-    k_build_klines<<<(unsigned)((s.n_keys + 255) / 256), 256, 0, st>>>(s, kslot, kcell, table);
+    k_build_klines<<<(unsigned)((s.n_keys + 255) / 256), 256, 0, st>>>(s, kslot, kcell, table, quads);
     return hipGetLastError();
 }
 

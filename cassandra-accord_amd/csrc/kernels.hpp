@@ -48,6 +48,7 @@ struct BatchBufs {
     // lean pass 1 as gather + build (run_lean_gb): per request 64 staged raw emissions, its build record
     // {raw count | #keys << 8 | deferred << 31, eight per-key start bytes}, its keys
     uint32_t* lg_stage; uint4* lg_rec; int64_t* lg_keys;
+    uint64_t* lg_dummy;              // per build wave one 128-byte line its disabled lanes' stores go to
     uint32_t slots_by_prepare;       // p_slot filled by k_prepare (one launch for records and slots)
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
@@ -232,6 +233,12 @@ hipError_t run_key_slots(const int64_t* keys, uint64_t nk, const uint32_t* disp,
                          hipStream_t st);
 hipError_t run_build_klines(const DevSnapshot& s, const uint32_t* kslot, const uint32_t* kcell, KeyLine* table,
                             uint64_t table_slots, hipStream_t st);
+// bytes of the KeyLine table allocation: the lines, then one LeanQuads per line
+inline uint64_t kline_table_bytes(uint64_t slots) { return (sizeof(KeyLine) + sizeof(LeanQuads)) * slots; }
+inline const LeanQuads* kline_quads(const KeyLine* table, uint64_t slots)
+{
+    return reinterpret_cast<const LeanQuads*>(table + slots);
+}
 // the two-level sample of s's dictionary into hi/lo/node (dict_sample_entries(s.n_dict) entries)
 hipError_t run_dict_sample(const DevSnapshot& s, uint64_t* hi, uint64_t* lo, int32_t* node, hipStream_t st);
 

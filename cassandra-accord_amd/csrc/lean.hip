@@ -1012,6 +1012,7 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
 constexpr uint32_t GB_STAGE = 64;           // staged raw emissions per request (words)
 constexpr uint32_t GB_INVALID = 0xFFFFFFFFu;  // a staged element filtered out (txnId >= S or the request's own)
 constexpr uint32_t GB_DEFER = 1u << 31;     // build record: the request went to the general kernel
+constexpr uint32_t GB_WIDE = 1u << 30;      // build record: 33..64 raw emissions, built by the wide build
 
 __global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_G) void k_lean_gather(DevSnapshot s, BatchBufs b)
 {
@@ -1019,6 +1020,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_G) void k_lean_gather(DevSn
     const uint64_t n = b.n_txns;
     const uint32_t n_groups = (uint32_t)((n + 7) / 8);
     const uint32_t nw = gridDim.x * LEAN_WAVES;
+    const uint32_t* kl32 = reinterpret_cast<const uint32_t*>(s.kline);
+    __shared__ uint32_t mk_all[LEAN_WAVES][64];
+    uint32_t* mk = mk_all[threadIdx.x >> 6];
     __shared__ uint32_t dbuf_all[LEAN_WAVES][DEFER_CHUNK];
     uint32_t* dbuf = dbuf_all[threadIdx.x >> 6];
     uint32_t dn = 0;
@@ -1036,8 +1040,23 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_G) void k_lean_gather(DevSn
         wave_lds_sync();
         dn = 0;
     };
+    // the wide build's list (deferred1 / n_deferred1, unused otherwise on this path)
+    __shared__ uint32_t wbuf_all[LEAN_WAVES][DEFER_CHUNK];
+    uint32_t* wbuf = wbuf_all[threadIdx.x >> 6];
+    uint32_t wn = 0;
+    auto wflush = [&]() {
+        if (!wn) return;
+        unsigned long long base = 0;
+        if (lane_id() == 0) base = atomicAdd(&b.ctl->n_deferred1, (unsigned long long)wn);
+        base = uniform64(base);
+        wave_lds_sync();
+        if (lane_id() < wn) b.deferred1[base + lane_id()] = wbuf[lane_id()];
+        wave_lds_sync();
+        wn = 0;
+    };
     for (uint32_t g = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6)); g < n_groups; g += nw)
     {
+        // ---- one lane per (request, key) probe: lane 8h + j is key j of request 8g + h
         const uint64_t t = (uint64_t)g * 8 + h;
         const bool act = t < n;
         const uint4 rec = b.q_rec[act ? t : 0];
@@ -1046,19 +1065,16 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_G) void k_lean_gather(DevSn
         const bool kact = act && fast && j < np;
         const int64_t key = b.q_keys[kact ? (uint64_t)k0 + j : 0];
         const uint32_t sl0 = b.p_slot[kact ? (uint64_t)k0 + j : 0];
-        const uint32_t sl = kact ? sl0 : LS_NONE;
+        const uint32_t sl = kact ? sl0 : LS_NONE;          // k_prepare: the key's line (LS_NONE: outside the slice)
         if (kact) b.lg_keys[t * 8 + j] = key;
-        // the key's line: key, newest fields and meta, the class's {count, start}, {cwr tail, prunedBefore}
-        const bool look = sl != LS_NONE;
-        const uint4* L4 = reinterpret_cast<const uint4*>(s.kline + (look ? sl : 0u));
-        const uint4 q0 = L4[0], q1 = L4[1];
-        const uint2 qc = reinterpret_cast<const uint2*>(L4 + 2)[cls], q3 = reinterpret_cast<const uint2*>(L4 + 3)[1];
-        const uint32_t meta = q1.w;
-        const bool found = look && (meta & KL_USED) && (int64_t)(((uint64_t)q0.y << 32) | q0.x) == key;
-        // lean-served (as lean pass 1): the last committed Write executes before S, S above prunedBefore
-        const bool newest = !found || (q1.y < S && (q3.y == 0 || S > q3.y) && !(meta & KL_NOLEAN));
-        const uint32_t n1 = found ? qc.x : 0u;
-        const uint32_t n2 = !found ? 0u : (cls == 0 ? (q1.z != 0 ? 1u : 0u) : (meta & KL_NCWR_MASK));
+        // the probe's 16 bytes of its line (threshold, counts, the two runs) and the line's key: the perfect
+        // hash puts every key of the store on its own line, any other key on some line whose key differs
+        const uint4* Q4 = reinterpret_cast<const uint4*>(s.kquad + (sl != LS_NONE ? sl : 0u));
+        const uint4 q = Q4[cls], qk = Q4[3];
+        const bool found = sl != LS_NONE && qk.z != 0 && (int64_t)(((uint64_t)qk.y << 32) | qk.x) == key;
+        // lean-served (as lean pass 1): S above the key's last committed Write's executeAt and prunedBefore
+        const bool newest = !found || S > q.x;
+        const uint32_t n1 = found ? (q.y & LQ_NMAX) : 0u, n2 = found ? ((q.y >> 8) & LQ_NMAX) : 0u;
         const uint32_t nn = kact ? n1 + n2 : 0u;
         const uint32_t inc = key_lanes_incl_scan(nn, j);
         const uint32_t start = inc - nn;
@@ -1075,111 +1091,150 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_G) void k_lean_gather(DevSn
                 dn += nd;
             }
         }
-        // build record: raw count | #keys << 8 | deferred, then the eight per-key starts (bytes)
+        // requests of 33..64 raw emissions: the wide build's list (two per lane there)
+        const bool wide = act && !defer && T > 32;
+        {
+            const uint64_t wm = ballot(wide && j == 0);
+            const uint32_t nwd = __popcll(wm);
+            if (nwd)
+            {
+                if (wn + nwd > DEFER_CHUNK) wflush();
+                if (wide && j == 0) wbuf[wn + __popcll(wm & ((1ull << lane) - 1))] = (uint32_t)t;
+                wn += nwd;
+            }
+        }
+        // build record: raw count | #keys << 8 | wide | deferred, then the eight per-key starts (bytes)
         if (act)
         {
             uint8_t* r8 = reinterpret_cast<uint8_t*>(b.lg_rec + t);
             r8[4 + j] = (uint8_t)start;
-            if (j == 0) *reinterpret_cast<uint32_t*>(r8) = (defer ? GB_DEFER : 0u) | (np << 8) | (defer ? 0u : T);
+            if (j == 0)
+                *reinterpret_cast<uint32_t*>(r8) = (defer ? GB_DEFER : 0u) | (wide ? GB_WIDE : 0u) | (np << 8) | (defer ? 0u : T);
         }
-        // the raw emissions: never-elided entries of the class (cand), then the class Ws's last Write or the
-        // committed Read/Writes from the last committed Write on (cwr tail); inline in the line when they fit
-        const bool copy = act && !defer && nn > 0;
-        // wave-uniform max of the lanes' counts (<= 64): binary search by ballots
-        const uint32_t ncopy = copy ? nn : 0u;
-        uint32_t nmax = 0;
-#pragma unroll
-        for (uint32_t bit = 64; bit; bit >>= 1)
-            if (ballot(ncopy >= nmax + bit)) nmax += bit;
-        if (nmax == 0) continue;
-        const bool inl = (meta & KL_INLINE) != 0;
-        const uint32_t inl_cwr = (meta >> KL_INL_SHIFT) & 31u;
-        const uint32_t* cand_p = inl ? s.kline[look ? sl : 0u].inl : s.cand + qc.y;
-        const uint32_t* cwr_p = inl ? s.kline[look ? sl : 0u].inl + inl_cwr : s.cwr + q3.x;
-        const uint32_t lastw = q1.z | (1u << RANK_BITS);
-        uint32_t* dst = b.lg_stage + t * GB_STAGE + start;
-        for (uint32_t i0 = 0; i0 < nmax; i0 += 4)
+        // ---- the raw emissions of the group's served requests, one per lane: consecutive lanes take
+        // consecutive elements of a run (coalesced loads) and write consecutive stage words
+        const uint32_t cnt = act && !defer ? nn : 0u;
+        const uint32_t ginc = wave_incl_scan_dpp(cnt);
+        const uint32_t gst = ginc - cnt;                  // the probe's first element in the group
+        const uint32_t E = uniform(__builtin_amdgcn_readlane((int)ginc, 63));
+        if (E == 0) continue;
+        // per probe, what its elements need (read by the element lanes through ds_bpermute)
+        const bool inl = (q.y & LQ_INLINE) != 0;
+        const uint32_t pk = gst | (n1 << 10) | (cls << 17) | (inl ? (1u << 19) : 0u) | (h << 20) | (start << 23);
+        const uint32_t pb1 = q.z, pb2 = q.w;
+        uint32_t carry = 0;                               // probe lane + 1 of the run open at the round's start
+        for (uint32_t r0 = 0; r0 < E; r0 += 64)
         {
-            uint32_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
+            // mark the lanes where a run starts (lane + 1 of its probe), then a max scan: the probe of
+            // every element lane (runs are contiguous and in lane order)
+            const bool starts_here = cnt > 0 && gst >= r0 && gst < r0 + 64;
+            mk[lane] = 0;
+            wave_lds_sync();
+            if (starts_here) mk[gst - r0] = lane + 1;        // run starts are distinct
+            wave_lds_sync();
+            uint32_t mark = mk[lane];
+            wave_lds_sync();
+            mark = wave_incl_max_dpp(max(mark, lane == 0 ? carry : 0u));
+            carry = uniform(__builtin_amdgcn_readlane((int)mark, 63));
+            const uint32_t e = r0 + lane;
+            const bool on = e < E;
+            const int src = (int)(((mark ? mark - 1 : 0u)) << 2);
+            const uint32_t xk = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pk);
+            const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb1);
+            const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb2);
+            const uint32_t xS = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)S);
+            const uint32_t xself = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)self);
+            const uint32_t i = e - (xk & 0x3FFu);
+            const uint32_t xn1 = (xk >> 10) & 0x7Fu, xcls = (xk >> 17) & 3u;
+            const bool xinl = (xk >> 19) & 1u;
+            const bool fc = i < xn1;
+            // the element: the class list (cand or the line's inline words), then the cwr tail (idem), or for
+            // class Ws the last committed Write (its txw in the quad, no load)
+            const uint32_t* arr = xinl ? kl32 : (fc ? s.cand : s.cwr);
+            const uint32_t idx = fc ? x1 + i : x2 + (i - xn1);
+            const bool ld = on && (fc || xcls != 0);
+            const uint32_t v0 = (ld ? arr : s.cand)[ld ? idx : 0u];
+            const uint32_t v = fc || xcls != 0 ? v0 : x2;
+            const uint32_t r = v & RANK_MASK;
+            if (on)
             {
-                const uint32_t i = i0 + u;
-                const bool on = copy && i < nn;
-                const bool fc = i < n1;
-                const uint32_t* src = !on ? s.cand : (fc ? cand_p + i : (cls == 0 ? s.cand : cwr_p + (i - n1)));
-                const uint32_t x = *src;
-                v[u] = (!fc && cls == 0) ? lastw : x;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-            {
-                const uint32_t i = i0 + u;
-                if (copy && i < nn)
-                {
-                    const uint32_t r = v[u] & RANK_MASK;
-                    dst[i] = (r < S && r != self) ? v[u] : GB_INVALID;
-                }
+                const uint64_t tt = (uint64_t)g * 8 + ((xk >> 20) & 7u);
+                b.lg_stage[tt * GB_STAGE + ((xk >> 23) & 0x7Fu) + i] = (r < xS && r != xself) ? v : GB_INVALID;
             }
         }
     }
     dflush();
+    wflush();
 }
 
-__global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_B) void k_lean_build(BatchBufs b)
+#ifndef GB_OCC_BW
+#define GB_OCC_BW 5
+#endif
+// The build, one item = two requests (32 lanes each). WIDE: the requests of the wide list (33..64 raw
+// emissions, two per lane); else consecutive requests, those of at most 32. Every iteration issues the
+// same vector-memory instructions -- loads of the items two (the wide list's entries three) iterations
+// ahead, then a fixed sequence of stores whose disabled lanes write a per-wave dummy word -- so the
+// compiler's wait counts stay exact across the loop: a wait for an item's inputs never waits for the
+// stores just issued (vmcnt counts loads and stores in issue order).
+template <bool WIDE>
+__global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? GB_OCC_BW : GB_OCC_B) void k_lean_build(BatchBufs b)
 {
     constexpr uint32_t LPR = 32;
     const uint32_t lane = lane_id(), h = lane >> 5, hl = lane & 31u, sb = h * LPR;
     const uint64_t below = (1ull << hl) - 1;
     auto seg = [&](uint64_t m) -> uint64_t { return (m >> sb) & 0xFFFFFFFFull; };
     const uint64_t n = b.n_txns;
-    const uint32_t n_items = (uint32_t)((n + 1) / 2);
+    const uint32_t n_slots = WIDE ? (uint32_t)uniform64(b.ctl->n_deferred1) : (uint32_t)n;
+    const uint32_t n_items = (n_slots + 1) / 2;
     const uint32_t nw = gridDim.x * LEAN_WAVES;
     const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
+    const uint32_t wid = uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
+    uint64_t* const dummy = b.lg_dummy + (uint64_t)wid * 16;     // one 128-byte line per wave
     LeanChunk ralloc;
     auto seg_alloc = [&](uint64_t bytes, bool& fits, uint32_t it) -> uint64_t {
-        const uint64_t b0 = uniform64(__shfl(bytes, 0, 64)), b1 = uniform64(__shfl(bytes, 32, 64));
+        const uint64_t b0 = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)bytes, 0) |
+                            ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(bytes >> 32), 0) << 32);
+        const uint64_t b1 = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)bytes, 32) |
+                            ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(bytes >> 32), 32) << 32);
         const uint64_t base = ralloc.template take<1>(b.ctl, b0 + b1, reg_cap, it, n_items, nw);
         fits = base + b0 + b1 <= reg_cap;
         return base + (h ? b0 : 0);
     };
-    auto put_sizes = [&](bool on, uint64_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro, bool with_ro) {
-        if (on && hl < 3)
-        {
-            const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);
-            b.sz[(uint64_t)(3 * m + hl) * n + t] = v;
-        }
-        if (with_ro && on && hl == 3) b.t_reg[(uint64_t)m * n + t] = ro;
+    // stores with every lane issuing: a disabled lane writes the wave's dummy word
+    auto st32 = [&](uint32_t* p, bool on, uint32_t v) { *(on ? p : reinterpret_cast<uint32_t*>(dummy)) = v; };
+    auto st64 = [&](uint64_t* p, bool on, uint64_t v) { *(on ? p : dummy) = v; };
+    auto put_sizes = [&](bool on, uint64_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro) {
+        const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);
+        st32(b.sz + (uint64_t)(3 * m + (hl < 3 ? hl : 0)) * n + t, on && hl < 3, v);
+        st64(b.t_reg + (uint64_t)m * n + t, on && hl == 3, ro);
     };
-    // an item's inputs, all at fixed offsets from its request index: the build record, the first 32
-    // staged elements, the key of lane hl & 7
-    struct In { uint4 r; uint32_t e0; int64_t key; };
-    auto load = [&](uint32_t it) -> In {
-        const uint64_t t = (uint64_t)it * 2 + h;
+    struct In { uint4 r; uint32_t e0, e1; int64_t key; uint32_t t; };
+    auto load = [&](uint32_t t) -> In {
         const uint64_t tt = t < n ? t : 0;
         In x;
+        x.t = t;
         x.r = b.lg_rec[tt];
         x.e0 = b.lg_stage[tt * GB_STAGE + hl];
+        x.e1 = WIDE ? b.lg_stage[tt * GB_STAGE + LPR + hl] : 0u;
         x.key = b.lg_keys[tt * 8 + (hl & 7u)];
         return x;
     };
-    const uint32_t it0 = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6));
-    In c0 = load(it0), c1 = load(it0 + nw);
-    for (uint32_t it = it0; it < n_items; it += nw)
-    {
-        const In cur = c0;
-        c0 = c1;
-        c1 = load(it + 2 * nw);
-        const uint64_t t = (uint64_t)it * 2 + h;
+    // the request of item `it` in this half: the list entry (wide) or its index
+    auto list_at = [&](uint32_t it) -> uint32_t {
+        const uint32_t si = it * 2 + h;
+        if (!WIDE) return si < n_slots ? si : DEFER_HOLE;
+        const uint32_t v = b.deferred1[si < n_slots ? si : 0u];
+        return si < n_slots ? v : DEFER_HOLE;
+    };
+    auto process = [&](const In& cur, uint32_t it) {
+        const uint64_t t = cur.t != DEFER_HOLE ? cur.t : 0;
         const uint32_t x = cur.r.x;
-        const bool act = t < n && !(x & GB_DEFER);
+        const bool act = cur.t != DEFER_HOLE && !(x & GB_DEFER) && (WIDE || !(x & GB_WIDE));
         const uint32_t T = act ? (x & 0xFFu) : 0u, np = (x >> 8) & 0xFu;
-        // per-key starts (bytes of r.y, r.z), the key lane's own start and raw count
         auto start_of = [&](uint32_t p) -> uint32_t { return ((p < 4 ? cur.r.y : cur.r.z) >> (8 * (p & 3))) & 0xFFu; };
         const uint32_t kj = hl & 7u;
         const uint32_t start = start_of(kj);
         const uint32_t nn = !act || hl >= 8 || kj >= np ? 0u : (kj + 1 < np ? start_of(kj + 1) : T) - start;
-        // the key of element e: the last key whose start is at or below e
         auto key_of = [&](uint32_t e) -> uint32_t {
             uint32_t a = 0;
 #pragma unroll
@@ -1189,162 +1244,129 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_B) void k_lean_build(BatchB
         };
         const int64_t key = cur.key;
         const uint32_t tmax = max(uniform(__builtin_amdgcn_readlane((int)T, 0)), uniform(__builtin_amdgcn_readlane((int)T, 32)));
-        if (tmax > LPR)
+        const uint32_t tw0 = act && hl < T ? cur.e0 : GB_INVALID;
+        const uint32_t tw1 = WIDE && act && hl + 32 < T ? cur.e1 : GB_INVALID;
+        const uint32_t ax0 = key_of(hl), ax1 = WIDE ? key_of(hl + 32) : 0u;
+        const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
+        const bool want0 = tw0 != GB_INVALID, want1 = tw1 != GB_INVALID;
+        const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
+        const bool is1_1 = ((KINDS_RS_OR_WS >> (tw1 >> RANK_BITS)) & 1) == 0;
+#pragma unroll
+        for (int m = 0; m < 3; m += 2)
         {
-            // a request of 33..64 raw emissions in the item: two per lane (element x = hl and hl + 32)
-            const uint32_t e1 = b.lg_stage[(t < n ? t : 0) * GB_STAGE + LPR + hl];
-            const uint32_t tw0 = act && hl < T ? cur.e0 : GB_INVALID, tw1 = act && hl + 32 < T ? e1 : GB_INVALID;
-            const uint32_t ax0 = key_of(hl), ax1 = key_of(hl + 32);
-            const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
-            const bool want0 = tw0 != GB_INVALID, want1 = tw1 != GB_INVALID;
-            const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
-            const bool is1_1 = ((KINDS_RS_OR_WS >> (tw1 >> RANK_BITS)) & 1) == 0;
-            for (int m = 0; m < 3; m += 2)
+            const bool mine0 = want0 && (m == 0 ? !is1_0 : is1_0), mine1 = want1 && (m == 0 ? !is1_1 : is1_1);
+            const uint64_t mb0 = ballot(mine0), mb1 = WIDE ? ballot(mine1) : 0ull;
+            const uint32_t tot = __popcll(seg(mb0)) + (WIDE ? __popcll(seg(mb1)) : 0u);
+            // the map's CSR: values sorted and deduplicated, per key its positions (VALU only; the stores
+            // below are issued whatever the branch)
+            uint32_t x0 = 0, x1 = 0, ka0 = 0, ka1 = 0, U = 0, ur0 = 0, ur1 = 0, pk0 = 0, pk1 = 0, cnt = 0, kstart_l = 0, nk = 0,
+                     kk = 0, kst0 = 0, kst1 = 0;
+            bool u0 = false, u1 = false, v0 = false, v1 = false;
+            if ((mb0 | mb1) != 0)
             {
-                const bool mine0 = want0 && (m == 0 ? !is1_0 : is1_0), mine1 = want1 && (m == 0 ? !is1_1 : is1_1);
-                const uint64_t mb0 = ballot(mine0), mb1 = ballot(mine1);
-                const uint32_t tot = __popcll(seg(mb0)) + __popcll(seg(mb1));
-                if ((mb0 | mb1) == 0)
-                {
-                    put_sizes(act, t, m, 0, 0, 0, 0, false);
-                    continue;
-                }
                 uint32_t k0 = mine0 ? ((r0 << 3) | ax0) : 0xFFFFFFFFu, k1 = mine1 ? ((r1 << 3) | ax1) : 0xFFFFFFFFu;
-                seg_bitonic_wide(k0, k1);
-                const bool v0 = hl < tot, v1 = hl + 32 < tot;
-                const uint32_t x0 = k0 >> 3, x1 = k1 >> 3, ka0 = k0 & 7u, ka1 = k1 & 7u;
+                if (WIDE) seg_bitonic_wide(k0, k1);
+                else if (tmax <= 8) seg_bitonic<8, LPR>(k0);
+                else if (tmax <= 16) seg_bitonic<16, LPR>(k0);
+                else seg_bitonic<32, LPR>(k0);
+                v0 = hl < tot;
+                v1 = WIDE && hl + 32 < tot;
+                x0 = k0 >> 3; x1 = k1 >> 3; ka0 = k0 & 7u; ka1 = k1 & 7u;
                 const uint32_t p0 = wave_up1(k0);
-                const uint32_t last0 = __shfl(k0, (int)(sb | 31u), 64);
-                const uint32_t up1 = wave_up1(k1);
-                const uint32_t p1 = hl == 0 ? last0 : up1;
-                const bool u0 = v0 && (hl == 0 || (p0 >> 3) != x0);
-                const bool u1 = v1 && (p1 >> 3) != x1;
-                const uint64_t um0 = seg(ballot(u0)), um1 = seg(ballot(u1));
+                u0 = v0 && (hl == 0 || (p0 >> 3) != x0);
+                const uint64_t um0 = seg(ballot(u0));
                 const uint32_t nu0 = __popcll(um0);
-                const uint32_t U = nu0 + __popcll(um1);
-                const uint32_t ur0 = __popcll(um0 & below) + (u0 ? 1u : 0u) - 1u;
-                const uint32_t ur1 = nu0 + __popcll(um1 & below) + (u1 ? 1u : 0u) - 1u;
-                uint64_t s00 = ballot(v0), s01 = ballot(v0), s11 = ballot(v1);
+                ur0 = __popcll(um0 & below) + (u0 ? 1u : 0u) - 1u;
+                U = nu0;
+                uint64_t s00 = ballot(v0), s01 = ballot(v0), s11 = WIDE ? ballot(v1) : 0ull;
+                if (WIDE)
+                {
+                    const uint32_t last0 = (uint32_t)__builtin_amdgcn_readlane((int)k0, 31), last0b = (uint32_t)__builtin_amdgcn_readlane((int)k0, 63);
+                    const uint32_t up1 = wave_up1(k1);
+                    const uint32_t p1 = hl == 0 ? (h ? last0b : last0) : up1;
+                    u1 = v1 && (p1 >> 3) != x1;
+                    const uint64_t um1 = seg(ballot(u1));
+                    U = nu0 + __popcll(um1);
+                    ur1 = nu0 + __popcll(um1 & below) + (u1 ? 1u : 0u) - 1u;
+                }
 #pragma unroll
                 for (int bit = 0; bit < 3; ++bit)
                 {
-                    const uint64_t b0 = ballot((ka0 >> bit) & 1u), b1 = ballot((ka1 >> bit) & 1u);
+                    const uint64_t b0 = ballot((ka0 >> bit) & 1u);
                     s00 &= ((ka0 >> bit) & 1u) ? b0 : ~b0;
-                    s01 &= ((ka1 >> bit) & 1u) ? b0 : ~b0;
-                    s11 &= ((ka1 >> bit) & 1u) ? b1 : ~b1;
-                }
-                const uint32_t pk0 = __popcll(seg(s00) & below);
-                const uint32_t pk1 = __popcll(seg(s01)) + __popcll(seg(s11) & below);
-                const uint64_t raw_m = seg(mb0) | (seg(mb1) << 32);
-                const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
-                const uint32_t cnt = hl < 8 ? (uint32_t)__popcll(raw_m & rmask) : 0u;
-                const uint32_t cinc = key_lanes_incl_scan(cnt, hl);
-                const uint32_t kstart_l = cinc - cnt;
-                const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
-                const uint32_t nk = __popcll(nem);
-                const uint32_t kk = __popcll(nem & below);
-                const uint32_t kst0 = __shfl(kstart_l, sb | ka0, 64), kst1 = __shfl(kstart_l, sb | ka1, 64);
-                const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
-                bool fits;
-                const uint64_t ro = seg_alloc(bytes, fits, it);
-                put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
-                if (act && tot && fits)
-                {
-                    int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
-                    uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
-                    int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
-                    if (hl < 8 && cnt > 0)
+                    if (WIDE)
                     {
-                        okeys[kk] = key;
-                        ok2t[kk] = (int32_t)(nk + kstart_l + cnt);
+                        const uint64_t b1 = ballot((ka1 >> bit) & 1u);
+                        s01 &= ((ka1 >> bit) & 1u) ? b0 : ~b0;
+                        s11 &= ((ka1 >> bit) & 1u) ? b1 : ~b1;
                     }
-                    if (u0) otx[ur0] = (x0 - 1) >> 1;
-                    if (u1) otx[ur1] = (x1 - 1) >> 1;
-                    if (v0) ok2t[nk + kst0 + pk0] = (int32_t)ur0;
-                    if (v1) ok2t[nk + kst1 + pk1] = (int32_t)ur1;
                 }
+                pk0 = __popcll(seg(s00) & below);
+                pk1 = WIDE ? __popcll(seg(s01)) + __popcll(seg(s11) & below) : 0u;
+                const uint64_t raw_m = seg(mb0) | (WIDE ? (seg(mb1) << 32) : 0ull);
+                const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
+                cnt = hl < 8 ? (uint32_t)__popcll(raw_m & rmask) : 0u;
+                const uint32_t cinc = key_lanes_incl_scan(cnt, hl);
+                kstart_l = cinc - cnt;
+                const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
+                nk = __popcll(nem);
+                kk = __popcll(nem & below);
+                kst0 = __shfl(kstart_l, sb | ka0, 64);
+                kst1 = WIDE ? __shfl(kstart_l, sb | ka1, 64) : 0u;
             }
-            put_sizes(act, t, 1, 0, 0, 0, 0, false);
-            continue;
-        }
-        // one raw emission per lane
-        const uint32_t a = key_of(hl);
-        const uint32_t txw = act && hl < T ? cur.e0 : GB_INVALID;
-        const bool want = txw != GB_INVALID;
-        const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
-        const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;       // !managesExecution -> directKeyDeps
-        for (int m = 0; m < 3; m += 2)
-        {
-            const bool mine = want && (m == 0 ? !is1 : is1);
-            const uint64_t mb = ballot(mine);
-            const uint32_t tot = __popcll(seg(mb));
-            if (mb == 0)
-            {
-                put_sizes(act, t, m, 0, 0, 0, 0, false);
-                continue;
-            }
-            uint32_t k = mine ? ((r << 3) | a) : 0xFFFFFFFFu;
-            if (tmax <= 8) seg_bitonic<8, LPR>(k);
-            else if (tmax <= 16) seg_bitonic<16, LPR>(k);
-            else seg_bitonic<32, LPR>(k);
-            const bool valid = hl < tot;
-            const uint32_t xr = k >> 3, ka = k & 7u;
-            const uint32_t prev = wave_up1(k);
-            const bool uniq = valid && (hl == 0 || (prev >> 3) != xr);
-            const uint64_t um = seg(ballot(uniq));
-            const uint32_t U = __popcll(um);
-            const uint32_t ur = __popcll(um & below) + (uniq ? 1u : 0u) - 1u;
-            uint64_t same = ballot(valid);
-#pragma unroll
-            for (int bit = 0; bit < 3; ++bit)
-            {
-                const uint64_t bb = ballot((ka >> bit) & 1u);
-                same &= ((ka >> bit) & 1u) ? bb : ~bb;
-            }
-            const uint32_t pos_in_key = __popcll(seg(same) & below);
-            const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
-            const uint32_t cnt = hl < 8 ? (uint32_t)__popcll(seg(mb) & rmask) : 0u;
-            const uint32_t cinc = key_lanes_incl_scan(cnt, hl);
-            const uint32_t kstart_l = cinc - cnt;
-            const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
-            const uint32_t nk = __popcll(nem);
-            const uint32_t kk = __popcll(nem & below);
-            const uint32_t kstart = __shfl(kstart_l, sb | ka, 64);
             const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits, it);
-            put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
-            if (act && tot && fits)
+            const bool wr = act && tot && fits;
+            put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro);
+            int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+            uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
+            int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
+            const bool kw = wr && hl < 8 && cnt > 0;
+            st64(reinterpret_cast<uint64_t*>(okeys + kk), kw, (uint64_t)key);
+            st32(reinterpret_cast<uint32_t*>(ok2t + kk), kw, nk + kstart_l + cnt);     // absolute end offsets (RelationMultiMap.java:245-257)
+            st32(otx + ur0, wr && u0, (x0 - 1) >> 1);                                // dictionary index of the TxnId
+            st32(reinterpret_cast<uint32_t*>(ok2t + nk + kst0 + pk0), wr && v0, ur0);
+            if (WIDE)
             {
-                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
-                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
-                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
-                if (hl < 8 && cnt > 0)
-                {
-                    okeys[kk] = key;
-                    ok2t[kk] = (int32_t)(nk + kstart_l + cnt);     // absolute end offsets (RelationMultiMap.java:245-257)
-                }
-                if (uniq) otx[ur] = (xr - 1) >> 1;                  // dictionary index of the TxnId
-                if (valid) ok2t[nk + kstart + pos_in_key] = (int32_t)ur;
+                st32(otx + ur1, wr && u1, (x1 - 1) >> 1);
+                st32(reinterpret_cast<uint32_t*>(ok2t + nk + kst1 + pk1), wr && v1, ur1);
             }
         }
-        put_sizes(act, t, 1, 0, 0, 0, 0, false);              // no range commands on this path
+        put_sizes(act, t, 1, 0, 0, 0, 0);            // no range commands on this path
+    };
+    // two items per trip, ping-pong input buffers (no register copies between a load and its use: a copy
+    // would wait for the load), each refilled right after its item is built
+    const uint32_t it0 = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6));
+    uint32_t la = list_at(it0 + 2 * nw), lb = list_at(it0 + 3 * nw);
+    In X = load(list_at(it0)), Y = load(list_at(it0 + nw));
+    for (uint32_t it = it0; it < n_items; it += 2 * nw)
+    {
+        process(X, it);
+        X = load(la);
+        la = list_at(it + 4 * nw);
+        if (it + nw >= n_items) break;
+        process(Y, it + nw);
+        Y = load(lb);
+        lb = list_at(it + 5 * nw);
     }
 }
 
 hipError_t run_lean_gb(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_txns) return hipSuccess;
-    if (!b.p_slot || !b.lg_stage || !b.lg_rec || !b.lg_keys || s.n_rent) return hipErrorInvalidValue;
+    if (!b.p_slot || !b.lg_stage || !b.lg_rec || !b.lg_keys || !b.lg_dummy || s.n_rent) return hipErrorInvalidValue;
     if (!b.slots_by_prepare && b.n_probes)
         k_lean_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b.q_keys, b.n_probes, b.p_slot);
-    static int per_cu_g = 0, per_cu_b = 0;
+    static int per_cu_g = 0, per_cu_b = 0, per_cu_w = 0;
     if (!per_cu_g)
     {
         int nb = 0;
         per_cu_g = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_gather, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
         nb = 0;
-        per_cu_b = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_build, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
+        per_cu_b = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_build<false>, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
+        nb = 0;
+        per_cu_w = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_build<true>, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
         if (const char* e = getenv("AD_GB_PER_CU_G")) per_cu_g = std::max(1, std::min(per_cu_g, atoi(e)));
         if (const char* e = getenv("AD_GB_PER_CU_B")) per_cu_b = std::max(1, std::min(per_cu_b, atoi(e)));
     }
@@ -1354,7 +1376,11 @@ hipError_t run_lean_gb(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
     k_lean_gather<<<grid_g, 64 * LEAN_WAVES, 0, st>>>(s, b);
     const uint64_t need_b = ((b.n_txns + 1) / 2 + LEAN_WAVES - 1) / LEAN_WAVES;
     const unsigned grid_b = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need_b, cus * per_cu_b));
-    k_lean_build<<<grid_b, 64 * LEAN_WAVES, 0, st>>>(b);
+    k_lean_build<false><<<grid_b, 64 * LEAN_WAVES, 0, st>>>(b);
+    // the wide list's length is on the device: a grid for up to an eighth of the batch, grid-strided
+    const uint64_t need_w = ((b.n_txns / 8 + 1) / 2 + LEAN_WAVES - 1) / LEAN_WAVES;
+    const unsigned grid_w = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need_w, cus * per_cu_w));
+    k_lean_build<true><<<grid_w, 64 * LEAN_WAVES, 0, st>>>(b);
     return hipGetLastError();
 }
 

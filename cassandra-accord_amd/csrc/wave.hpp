@@ -114,6 +114,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x)
     return x;
 }
 
+// inclusive prefix max over the 64 lanes in DPP steps (as wave_incl_scan_dpp; values >= 0, absent lanes read 0)
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t x)
+{
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));     // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));     // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));     // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));     // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));     // row_bcast:15 -> rows 1, 3
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));     // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 // inclusive prefix sum of 64-bit values over the 64 lanes: DPP steps in 32 bits while the wave's sum
 // surely fits (every value below 2^25), else the shuffle scan. Every lane must execute it.
 __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t v)

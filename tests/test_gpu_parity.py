@@ -76,10 +76,13 @@ def test_random_larger(oracle, seed):
     _compare(w, oracle)
 
 
-@pytest.mark.parametrize("rpw", ["2", "4", "8"])
+@pytest.mark.parametrize("rpw", ["2", "4", "8", "gb"])
 @pytest.mark.parametrize("seed", range(16))
 def test_random_small_lean_store(oracle, seed, rpw, monkeypatch):
-    monkeypatch.setenv("AD_LEAN_RPW", rpw)     # lean pass 1 with two or four requests per wave
+    # lean pass 1 with two, four or eight requests per wave, or as gather + build (AD_LEAN_GB)
+    monkeypatch.setenv("AD_LEAN_RPW", "2" if rpw == "gb" else rpw)
+    if rpw == "gb":
+        monkeypatch.setenv("AD_LEAN_GB", "1")
     # no range commands / redundant-before: the lean kernel runs first; older requests defer
     w = synth.random_small(500 + seed, n_range_cmds=0, n_redundant=0, accept_frac=0.2 * (seed % 4),
                            max_keys=2 + seed % 7)
@@ -114,6 +117,9 @@ def test_config2_lean_classes(oracle, esp, sync, reads, monkeypatch):
         w.queries.exec.lsb[:] = w.queries.txn.lsb
     got, exp = _compare(w, oracle, paths=(0,))
     assert got.stats["n_deferred_lean"] < len(w.queries)
+    monkeypatch.setenv("AD_LEAN_GB", "1")
+    assert native.resolve(w).equals(exp)
+    monkeypatch.delenv("AD_LEAN_GB")
     monkeypatch.setenv("AD_LEAN_RPW", "4")
     assert native.resolve(w).equals(exp)
     monkeypatch.delenv("AD_LEAN_RPW")
