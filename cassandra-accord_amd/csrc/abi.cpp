@@ -773,6 +773,7 @@ static int set_views(ad_ctx* c, uint64_t n_dict, uint64_t n_samp, const NormTid&
     s.slice_end = c->d_slices_e.as<int64_t>();
     s.start_inclusive = c->cfg.range_start_inclusive;
     s.elide = c->cfg.elide;
+    s.rng32 = getenv("AD_RNG64") == nullptr && c->rt_start.size() < (1ull << 26) && 2 * n_dict + 2 < (1ull << 26);
     return 0;
 }
 
@@ -1823,11 +1824,13 @@ static bool lean_gb_on()
     return e && atoi(e) != 0;
 }
 
-static uint32_t lean_rpw1(uint64_t n, uint64_t np)
+static uint32_t lean_rpw1(uint64_t n, uint64_t np, bool ranges)
 {
     if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 8 ? 8u : (atoi(e) == 4 ? 4u : 2u);
-    // 8 requests per wave (AD_LEAN_RPW=8) stays opt-in while the late-round-3 device faults are open
-    return np <= 3 * n ? 4u : 2u;
+    // 8 requests per wave (AD_LEAN_RPW=8) stays opt-in while the late-round-3 device faults are open.
+    // With range commands up to 4 keys per request on average: four per wave (config 4: pass 1 0.90 ->
+    // 0.58 ms, its deferrals -- above 16 raw emissions -- two per wave in pass 2)
+    return np <= (ranges ? 4 : 3) * n ? 4u : 2u;
 }
 
 // Lean pass 1 wide or narrow (rpw 2, no range commands; results identical either way). The wide kernel
@@ -1958,7 +1961,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     }
     // lean pass 1 as gather + build (two requests per build wave, no range commands): AD_LEAN_GB=0 keeps
     // the single fused pass
-    const bool gb = lean && !c->ds.n_rent && lean_rpw1(n, np) == 2 && lean_gb_on();
+    const bool gb = lean && !c->ds.n_rent && lean_rpw1(n, np, c->ds.n_rent != 0) == 2 && lean_gb_on();
     if (gb)
     {
         if (!ens<uint32_t>(c->lg_stage, n * 64) || !ens<uint4>(c->lg_rec, n) || !ens<int64_t>(c->lg_keys, n * 8) ||
@@ -2048,7 +2051,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 // lean kernel first (newest requests, 2 per wave); the general fused kernel then
                 // takes only what it deferred (count read on the device, no host round trip)
                 if (!c->ev_lean1) HIPCHK(c, timing_event(&c->ev_lean1));
-                const uint32_t rpw1 = lean_rpw1(n, np);
+                const uint32_t rpw1 = lean_rpw1(n, np, c->ds.n_rent != 0);
                 if (gb)
                 {
                     // gather + build (k_lean_gather, k_lean_build): the rest to the general kernel
@@ -2063,7 +2066,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                     lean_track = rpw1 == 2 && !c->ds.n_rent;
                     HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
                     if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
-                    HIPCHK(c, run_resolve_lean(c->ds, b, 2, 0, false, st));
+                    HIPCHK(c, run_resolve_lean(c->ds, b, 2, rpw1, false, st));
                     if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 }
                 BatchBufs b2 = b;

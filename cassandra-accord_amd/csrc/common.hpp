@@ -128,12 +128,15 @@ static_assert(sizeof(KeyEntry) == 64, "KeyEntry is half a cache line");
 //   [0, 8)    key
 //   [8, 16)   the key's entries in the range stabbing index: cell_ent[cell_lo, cell_hi)
 //   [16, 28)  last txnId rank, last committed Write's executeAt rank and txnId rank (0: none)
-//   [28, 32)  meta: KL_USED | KL_INLINE | KL_NOLEAN | inline offset of the cwr tail << 24 | #cwr tail
+//   [28, 32)  meta: KL_USED | KL_INLINE | KL_NOLEAN | inline offset of the cwr tail << 24 | KL_CELLINL |
+//             inline u64 offset of the stabbing-cell entries << 20 | #cwr tail
 //   [32, 56)  per witness class c: {#never-elided entries of class c, their start in cand}
 //   [56, 64)  start of the cwr tail in cwr, rank of prunedBefore (0: none)
 //   [64, 128) inline emissions when #class-2 entries + #cwr tail <= KL_INL: the never-elided
 //             entries nested by class -- Writes, then Reads, then SyncPoints/ExclusiveSyncPoints
-//             (class c's list is the first n_c of them) -- then the cwr tail
+//             (class c's list is the first n_c of them) -- then the cwr tail; then, when they fit
+//             (KL_CELLINL), the key's stabbing-cell entries (rid << 32 | txw, u64-aligned) -- a range
+//             probe then reads them from the line it already has instead of a line of cell_ent
 struct KeyClassSpan { uint32_t n, base; };
 struct alignas(128) KeyLine {
     int64_t key;
@@ -148,7 +151,9 @@ constexpr uint32_t KL_INL = 16;
 constexpr uint32_t KL_USED = 1u << 31;
 constexpr uint32_t KL_INLINE = 1u << 30;
 constexpr uint32_t KL_NOLEAN = 1u << 29;          // counts beyond the meta fields: the general kernel serves it
-constexpr uint32_t KL_NCWR_MASK = (1u << 24) - 1;
+constexpr uint32_t KL_NCWR_MASK = (1u << 20) - 1;
+constexpr uint32_t KL_CELLINL = 1u << 23;         // the cell entries are inline, at u64 offset (meta >> 20) & 7
+constexpr uint32_t KL_CELL_SHIFT = 20;
 constexpr uint32_t KL_INL_SHIFT = 24;             // 5 bits (<= KL_INL)
 
 // Per key line, beside its KeyLine (same perfect-hash index): what one (request, key) probe of witness
@@ -263,6 +268,9 @@ struct DevSnapshot {
     const int64_t* slice_end;
     int start_inclusive;
     int elide;
+    // range ids below 2^26 and id ranks below 2^26: the lean kernels' rangeDeps build sorts 32-bit keys
+    // (range id << 6 | lane, rank << 6 | pair) instead of 64-bit (range id << 32 | rank, rank << 8 | pair)
+    int rng32;
 };
 
 constexpr uint64_t DICT_SAMP = 256, DICT_SAMP2 = 16;

@@ -1885,6 +1885,17 @@ __global__ __launch_bounds__(256) void k_build_klines(DevSnapshot s, const uint3
         for (uint32_t j = 0; j < n_cwr; ++j) L.inl[n2 + j] = s.cwr[L.cwr_tail + j];
         meta |= KL_INLINE | (n2 << KL_INL_SHIFT);
     }
+    {
+        // the stabbing cell's entries after the inline emissions, when they fit (u64-aligned)
+        const uint32_t used = (meta & KL_INLINE) ? n2 + n_cwr : 0u;
+        const uint32_t co = (used + 1) & ~1u, nc = L.cell_hi - L.cell_lo;
+        if (nc > 0 && co + 2 * nc <= KL_INL)
+        {
+            uint64_t* in64 = reinterpret_cast<uint64_t*>(L.inl);
+            for (uint32_t j = 0; j < nc; ++j) in64[co / 2 + j] = s.cell_ent[L.cell_lo + j];
+            meta |= KL_CELLINL | ((co / 2) << KL_CELL_SHIFT);
+        }
+    }
     L.meta = meta;
     out[kslot[k]] = L;
     // the probe quads (LeanQuads): the newest threshold, per class the two emission runs

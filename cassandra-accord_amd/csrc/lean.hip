@@ -772,8 +772,15 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             }
             const uint32_t rsrc = sb | ar;
             const uint32_t ar_start = __shfl(rstart, rsrc, 64), ar_lo = __shfl(cbc.x, rsrc, 64);
+            // the cell's entries inline in the key's line (KL_CELLINL: the line just read) or in cell_ent
+            const uint32_t ar_meta = __shfl(has_cfk ? meta : 0u, rsrc, 64), ar_slot = __shfl(Hc.slot, rsrc, 64);
+            const bool cin = (ar_meta & KL_CELLINL) != 0;
             rlive = act && hl < TR;
-            ce = s.cell_ent[rlive ? ar_lo + (hl - ar_start) : 0u];
+            const uint64_t* kl64 = reinterpret_cast<const uint64_t*>(s.kline);
+            const uint64_t cidx = cin ? (uint64_t)ar_slot * (sizeof(KeyLine) / 8) + offsetof(KeyLine, inl) / 8 +
+                                            ((ar_meta >> KL_CELL_SHIFT) & 7u) + (hl - ar_start)
+                                      : (uint64_t)ar_lo + (hl - ar_start);
+            ce = (cin && rlive ? kl64 : s.cell_ent)[rlive ? cidx : 0u];
         }
         // the later items' loads go out behind this item's element loads
         Hdr Hn;
@@ -867,6 +874,71 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         if (!RNG || rmb == 0)
         {
             put_sizes(act, t, 1, 0, 0, 0, 0, false);
+        }
+        else if (s.rng32)
+        {
+            // 32-bit keys. Every entry of a range id covers the same interval, so each cell holding the id
+            // holds all its entries (in txnId order): a request's pairs of one range id are identical runs,
+            // one per key whose cell has it. Sort (range id << 6 | lane) -- range-major, then by key and
+            // txnId within a key's run -- and keep the run of the group's first key (the duplicates of the
+            // 64-bit sort); then the distinct txnIds by (rank << 6 | pair position).
+            const uint32_t kmaxr = min(seg_max(TR), LPR);
+            uint32_t k1 = rwant ? ((uint32_t)(ce >> 32) << 6) | hl : 0xFFFFFFFFu;
+            if (kmaxr <= 8) seg_bitonic<8, LPR>(k1);
+            else if (kmaxr <= 16 || LPR == 16) seg_bitonic<16, LPR>(k1);
+            else if (kmaxr <= 32 || LPR == 32) seg_bitonic<(LPR < 32 ? LPR : 32), LPR>(k1);
+            else seg_bitonic<LPR, LPR>(k1);
+            const uint32_t totp = __popcll(seg(rmb));
+            const bool pv = hl < totp;
+            const uint32_t rid = k1 >> 6, src = sb | (k1 & 63u);
+            // the pair's rank and key (its source lane)
+            const uint32_t rka = (uint32_t)__shfl((int)((rk << 3) | ar), (int)(pv ? src : lane), 64);
+            const uint32_t prid = LEAN_DPP ? wave_up1(rid) : (uint32_t)__shfl_up(rid, 1, LPR);
+            const bool gfirst_raw = pv && (hl == 0 || prid != rid);
+            // the key of the range id's first run (segment starts are group starts: an absolute-lane max scan)
+            const uint32_t gs = wave_incl_max_dpp(gfirst_raw ? lane : 0u);
+            const uint32_t ar0 = (uint32_t)__shfl((int)(rka & 7u), (int)gs, 64);
+            const bool pu = pv && (rka & 7u) == ar0;
+            const uint64_t pum = seg(ballot(pu));
+            const uint32_t UP = __popcll(pum);
+            const uint32_t dst = __popcll(pum & below);
+            const bool gfirst = pu && gfirst_raw;
+            const uint64_t gm = seg(ballot(gfirst));
+            const uint32_t nR = __popcll(gm);
+            // distinct txnIds of the unique pairs: sort (rank << 6 | pair position)
+            uint32_t k2 = pu ? ((rka >> 3) << 6) | dst : 0xFFFFFFFFu;
+            if (kmaxr <= 8) seg_bitonic<8, LPR>(k2);
+            else if (kmaxr <= 16 || LPR == 16) seg_bitonic<16, LPR>(k2);
+            else if (kmaxr <= 32 || LPR == 32) seg_bitonic<(LPR < 32 ? LPR : 32), LPR>(k2);
+            else seg_bitonic<LPR, LPR>(k2);
+            const uint32_t p2 = LEAN_DPP ? wave_up1(k2) : (uint32_t)__shfl_up(k2, 1, LPR);
+            const bool v2 = hl < UP;
+            const bool uq2 = v2 && (hl == 0 || (p2 >> 6) != (k2 >> 6));
+            const uint64_t um2 = seg(ballot(uq2));
+            const uint32_t UR = __popcll(um2);
+            const uint32_t ur2 = __popcll(um2 & below) + (uq2 ? 1u : 0u) - 1u;
+            const uint64_t bytes = act && totp ? (((uint64_t)nR * 8 + (uint64_t)UR * 4 + (uint64_t)(nR + UP) * 4 + 7) & ~7ull) : 0;
+            bool fits;
+            const uint64_t ro = seg_alloc(bytes, fits, it);
+            put_sizes(act, t, 1, fits ? nR : 0, fits ? UR : 0, fits ? nR + UP : 0, ro, true);
+            if (act && totp && fits)
+            {
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nR);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + UR);
+                if (gfirst)
+                {
+                    // this group's end: the pair position of the next group's first pair (or UP)
+                    const uint32_t gi = __popcll(gm & below);
+                    const uint64_t later = gm & ~((2ull << hl) - 1) & SEGMASK;
+                    const uint32_t nxt = later ? (uint32_t)(__ffsll((unsigned long long)later) - 1) : LPR;
+                    const uint32_t gend = later ? __popcll(pum & ((1ull << nxt) - 1)) : UP;
+                    okeys[gi] = (int64_t)rid;                          // range id (ad_range_table)
+                    ok2t[gi] = (int32_t)(nR + gend);
+                }
+                if (uq2) otx[ur2] = ((k2 >> 6) - 1) >> 1;
+                if (v2) ok2t[nR + (k2 & 63u)] = (int32_t)ur2;
+            }
         }
         else
         {
@@ -978,8 +1050,10 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
         if (wide1 && !s.n_rent) return launch_lean<2, false, true, 1>(s, b, st);
         return s.n_rent ? launch_lean<2, true, false, 1>(s, b, st) : launch_lean<2, false, false, 1>(s, b, st);
     }
-    // pass 2 (requests with 33..64 raw emissions): two per wave, two emissions per lane
-    return s.n_rent ? launch_lean<1, true, false, 2>(s, b, st) : launch_lean<2, false, true, 2>(s, b, st);
+    // pass 2 (requests with 33..64 raw emissions): two per wave, two emissions per lane; with range commands
+    // one per wave after a pass 1 of two per wave, two per wave (up to 32) after one of four
+    if (s.n_rent) return rpw1 == 4 ? launch_lean<2, true, false, 2>(s, b, st) : launch_lean<1, true, false, 2>(s, b, st);
+    return launch_lean<2, false, true, 2>(s, b, st);
 }
 
 
