@@ -20,6 +20,7 @@ AD_E_STATE = -8
 AD_E_CAPACITY = -9
 AD_E_SPACE = -10
 AD_E_PEER = -11
+AD_E_PARTIAL = -12
 
 AD_MAP_KEY, AD_MAP_RANGE, AD_MAP_DIRECT_KEY = 0, 1, 2
 NMAPS = 3

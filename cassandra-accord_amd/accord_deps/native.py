@@ -29,7 +29,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange", "ad_exchange_plan",
            "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing",
            "ad_cfk_load_pruned", "ad_host_register", "ad_host_unregister", "ad_deps_batch_into",
-           "ad_debug_guard_check", "ad_host_alloc", "ad_host_free")
+           "ad_debug_guard_check", "ad_host_alloc", "ad_host_free", "ad_cfk_update_status")
 
 
 class AccordDepsError(RuntimeError):
@@ -91,6 +91,7 @@ def lib():
         L.ad_recovery_batch_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_void_p,
                                                C.POINTER(A.AdDepsResult)]
         L.ad_cfk_update.argtypes = [C.c_void_p, C.POINTER(A.AdCfkUpdateSoa), C.POINTER(C.c_uint64), C.POINTER(A.AdStats)]
+        L.ad_cfk_update_status.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int64)]
         L.ad_cfk_update_device.argtypes = [C.c_void_p, C.POINTER(A.AdCfkUpdateSoa), C.c_void_p, C.POINTER(C.c_uint64),
                                            C.POINTER(A.AdStats)]
         L.ad_cfk_ballots_load.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -268,6 +269,13 @@ class DeviceCommandStore:
         self._check(lib().ad_cfk_update(self.h, C.byref(updates.soa()), C.byref(n), C.byref(st)))
         return n.value, stats_dict(st)
 
+    def cfk_update_status(self):
+        """ad_cfk_update_status: (explicit updates of the last batch stand, index of the update a failure
+        names or -1)."""
+        ap, fi = C.c_int(), C.c_int64()
+        self._check(lib().ad_cfk_update_status(self.h, C.byref(ap), C.byref(fi)))
+        return bool(ap.value), int(fi.value)
+
     def cfk_update_device(self, udev, stream=None):
         """As cfk_update over device arrays (an AdCfkUpdateSoa of device pointers)."""
         n, st = C.c_uint64(), A.AdStats()
@@ -434,89 +442,80 @@ class DeviceCommandStore:
         finally:
             L.ad_result_free(out)
 
+    class _Block:
+        """One block of output memory that owns its pinning: library-pinned (ad_host_alloc) or numpy pages
+        registered with ad_host_register. Exposes the memory through __array_interface__, so every numpy
+        view of it keeps it alive (the block is its base); the memory is freed / unpinned by a finalizer
+        when the last view and the block are gone -- a view that outlives its HostOut stays valid."""
+        PAGE = 4096
+
+        def __init__(self, store, nbytes, pin):
+            nbytes = max(int(nbytes), 1)
+            if pin is True:
+                p = C.c_void_p()
+                rc = lib().ad_host_alloc(nbytes, C.byref(p))
+                if rc or not p.value:
+                    raise AccordDepsError(rc or A.AD_E_NOMEM, "ad_host_alloc(%d) failed" % nbytes)
+                addr = p.value
+                self._fin = weakref.finalize(self, DeviceCommandStore._Block._host_free, addr)
+            else:
+                # zeroed numpy memory on whole pages of its own: a registration covers exactly its pages,
+                # so pinning (page-granular) never shares a page with another array or the Python heap
+                P = DeviceCommandStore._Block.PAGE
+                span = -(-nbytes // P) * P
+                raw = np.zeros(span + P, np.uint8)
+                at = (-raw.ctypes.data) % P
+                addr = raw.ctypes.data + at
+                if pin == "register":
+                    store._check(lib().ad_host_register(store.h, C.c_void_p(addr), span))
+                    # the finalizer holds the numpy memory until it has been unpinned
+                    self._fin = weakref.finalize(self, DeviceCommandStore._Block._unregister, addr, raw)
+                else:
+                    self._fin = weakref.finalize(self, lambda r: None, raw)
+            self.__array_interface__ = {"data": (addr, False), "shape": (nbytes,), "typestr": "|u1", "version": 3}
+
+        @staticmethod
+        def _host_free(addr):
+            if lib().ad_host_free(C.c_void_p(addr)) != 0:
+                raise AccordDepsError(A.AD_E_DEVICE, "ad_host_free failed")
+
+        @staticmethod
+        def _unregister(addr, raw):
+            if lib().ad_host_unregister(None, C.c_void_p(addr)) != 0:
+                raise AccordDepsError(A.AD_E_DEVICE, "ad_host_unregister failed")
+
+        def array(self, shape, dtype):
+            dtype = np.dtype(dtype)
+            count = int(np.prod(shape))
+            a = np.asarray(self)[:count * dtype.itemsize].view(dtype).reshape(shape)
+            a[...] = 0
+            return a
+
     class HostOut:
         """Caller-owned host output arrays of ad_deps_batch_into (numpy). pin=True: views of pinned memory
         from ad_host_alloc (the default: copy-outs are DMAs straight into them); pin="register": numpy
         pages of their own pinned with ad_host_register (the Panama binding's way, INTEGRATION.md);
         pin=False: plain pageable numpy (filled through the library's staging). Grown (re-made) when a
-        batch needs more; release() frees / unpins, after which the arrays must not be used."""
-
-        PAGE = 4096
-
-        @staticmethod
-        def _pages(shape, dtype):
-            # zeroed array on whole pages of its own: a registration covers exactly its pages, so pinning
-            # (page-granular) never shares a page with another array or with the Python heap
-            dtype = np.dtype(dtype)
-            nbytes = int(np.prod(shape)) * dtype.itemsize
-            span = -(-max(nbytes, 1) // DeviceCommandStore.HostOut.PAGE) * DeviceCommandStore.HostOut.PAGE
-            raw = np.zeros(span + DeviceCommandStore.HostOut.PAGE, np.uint8)
-            at = (-raw.ctypes.data) % DeviceCommandStore.HostOut.PAGE
-            a = raw[at:at + nbytes].view(dtype).reshape(shape)
-            return a, span
-
-        @staticmethod
-        def _alloc(shape, dtype, blocks):
-            # a numpy view of library-pinned memory (ad_host_alloc); the block is freed by _free
-            dtype = np.dtype(dtype)
-            count = int(np.prod(shape))
-            nbytes = max(count * dtype.itemsize, 1)
-            p = C.c_void_p()
-            rc = lib().ad_host_alloc(nbytes, C.byref(p))
-            if rc or not p.value:
-                raise AccordDepsError(rc or A.AD_E_NOMEM, "ad_host_alloc(%d) failed" % nbytes)
-            blocks.append(p.value)
-            buf = (C.c_uint8 * nbytes).from_address(p.value)
-            a = np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
-            a[...] = 0
-            return a
+        batch needs more. Every array keeps its memory (a _Block) alive: release() only drops this
+        object's references, and the memory is freed / unpinned once no array of it is left."""
 
         def __init__(self, store, n, cap, pin=True):
             self.store, self.pin, self.n = store, pin, n
             self.cap = [int(x) for x in cap]
-            self.blocks, self.pinned = [], []
-            # freed / unpinned when released, or at the latest when this object is collected (a test or
-            # caller that raises before release()); the finalizer needs no ctx
-            self._fin = weakref.finalize(self, DeviceCommandStore.HostOut._free, self.blocks, self.pinned)
             shapes = [((9, n + 1), np.uint64)] + [(max(1, self.cap[3 * m]), np.int64) for m in range(3)] + \
                      [(max(1, self.cap[3 * m + 1]), np.uint32) for m in range(3)] + \
                      [(max(1, self.cap[3 * m + 2]), np.int32) for m in range(3)]
             arrs = []
-            try:
-                for shape, dt in shapes:
-                    if pin is True:
-                        arrs.append(DeviceCommandStore.HostOut._alloc(shape, dt, self.blocks))
-                    elif pin == "register":
-                        a, span = DeviceCommandStore.HostOut._pages(shape, dt)
-                        store._check(lib().ad_host_register(store.h, A.ptr(a), span))
-                        self.pinned.append(a)
-                        arrs.append(a)
-                    else:
-                        arrs.append(np.zeros(shape, dt))
-            except BaseException:
-                self.release()
-                raise
+            for shape, dt in shapes:
+                nbytes = int(np.prod(shape)) * np.dtype(dt).itemsize
+                arrs.append(DeviceCommandStore._Block(store, nbytes, pin).array(shape, dt))
             self.off = arrs[0]
             self.keys, self.txns, self.k2t = arrs[1:4], arrs[4:7], arrs[7:10]
 
-        @staticmethod
-        def _free(blocks, pinned):
-            bad = 0
-            for a in pinned:
-                if lib().ad_host_unregister(None, A.ptr(a)) != 0:
-                    bad += 1
-            pinned.clear()
-            for p in blocks:
-                if lib().ad_host_free(C.c_void_p(p)) != 0:
-                    bad += 1
-            blocks.clear()
-            if bad:
-                raise AccordDepsError(A.AD_E_DEVICE, "freeing / unpinning %d output arrays failed" % bad)
-
         def release(self):
-            # the store's copy stream is drained by every ad_deps_batch_into return
+            # the store's copy stream is drained by every ad_deps_batch_into return; the memory goes with
+            # the last array of it
             self.off = self.keys = self.txns = self.k2t = None
-            self._fin()
 
         def soa(self):
             r = A.AdDepsResult()
@@ -535,11 +534,11 @@ class DeviceCommandStore:
         slices whose copy-out overlaps the next slice. `out`: a HostOut to reuse (grown on AD_E_SPACE).
         Returns (PartialDepsBatch or None, stats dict, the HostOut)."""
         n = len(queries)
+        mine = False                        # this call made `out` (a caller's HostOut is never released here)
         if out is None or out.n != n:
-            if out is not None:
-                out.release()
             np_ = queries.n_probes
             out = DeviceCommandStore.HostOut(self, n, [np_, 2 * np_, 4 * np_] * 3, pin)
+            mine = True
         need = np.zeros(9, np.uint64)
         soa = queries.soa()
         try:
@@ -549,11 +548,14 @@ class DeviceCommandStore:
                 rc = lib().ad_deps_batch_into(self.h, C.byref(soa), flags, C.byref(r), A.ptr(cap), A.ptr(need), slices)
                 if rc != A.AD_E_SPACE:
                     break
-                out.release()
+                if mine:
+                    out.release()
                 out = DeviceCommandStore.HostOut(self, n, [int(x) + int(x) // 4 + 16 for x in need], pin)
+                mine = True
             self._check(rc)
         except BaseException:
-            out.release()
+            if mine:
+                out.release()
             raise
         stats = stats_dict(r.stats)
         if not materialise:

@@ -202,6 +202,8 @@ struct ad_ctx {
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
     DevBuf q_ro, q_rs, q_re;                   // Range-domain requests: staged ranges
     DevBuf lg_stage, lg_rec, lg_keys, lg_dummy;   // lean gather + build: staged emissions, build records, keys
+    bool upd_applied = false;                  // ad_cfk_update_status: the last update batch stands
+    int64_t upd_failed = -1;                   //   and the update its failure names
     DevBuf rq_cnt, rq_off, rq_err, rq_bsum, rq_keys, rq_hi, rq_kind;   // their expansion into probes
     struct SplitBufs {       // per-request / per-probe arrays of the split kernels
         DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
@@ -1868,8 +1870,19 @@ static hipError_t batch_wait(ad_ctx* c, hipStream_t st)
     if (!c->ev_done)
         if (hipError_t e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) return e;
     if (hipError_t e = hipEventRecord(c->ev_done, st)) return e;
+    // bounded: busy polls for up to ~2 ms (a batch's usual span), then polls that yield the core (50 us
+    // sleeps), and after AD_WAIT_TIMEOUT_MS (default 120 s) the batch is given up (hipErrorTimeout ->
+    // AD_E_DEVICE) instead of a store thread spinning on a completion that never comes
+    static const double timeout_ms = getenv("AD_WAIT_TIMEOUT_MS") ? atof(getenv("AD_WAIT_TIMEOUT_MS")) : 120000.0;
+    const double t0 = now_ms();
     hipError_t e;
-    while ((e = hipEventQuery(c->ev_done)) == hipErrorNotReady) {}
+    while ((e = hipEventQuery(c->ev_done)) == hipErrorNotReady)
+    {
+        const double dt = now_ms() - t0;
+        if (dt < 2.0) continue;
+        if (dt > timeout_ms) return hipErrorTimeout;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
     return e;
 }
 
@@ -4191,6 +4204,8 @@ static int dmiss_enable(ad_ctx* c, hipStream_t st)
 static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats)
 {
     StreamScope scope_(st, c->stream, c->cstream);
+    c->upd_applied = false;
+    c->upd_failed = -1;
     if (c->dirty)
         if (int rc = build_snapshot(c)) return rc;
     // missing() on the device while batches bring their deps; a batch without deps hands the lists
@@ -4302,12 +4317,17 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
             c->cfk.miss_stale = true;
         }
     }
-    if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back && !o.rederived)
+    if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back && !o.rederived && !o.batch_stood)
     {
         // the derived arrays may be half built: rebuild them from the entries at the next use
         c->host_stale = true;
         c->dirty = true;
     }
+    c->upd_applied = rc == AD_OK || o.batch_stood;
+    c->upd_failed = o.failed_update;
+    // a failure after the explicit batch stood is AD_E_PARTIAL: a caller must not take it for "nothing
+    // applied" and retry the batch
+    if (rc && o.batch_stood) return c->fail(AD_E_PARTIAL, "explicit updates applied, deps-derived part failed: %s", e.c_str());
     if (rc) return c->fail(rc, "%s", e.c_str());
     if (u.n)
     {
@@ -4343,6 +4363,14 @@ static int check_update_soa(ad_ctx* c, const ad_cfk_update_soa* u)
     if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
     StreamScope scope_(c->stream, c->cstream);
     return 0;
+}
+
+int ad_cfk_update_status(const ad_ctx* c, int* applied, int64_t* failed_update)
+{
+    if (!c) return AD_E_INVAL;
+    if (applied) *applied = c->upd_applied ? 1 : 0;
+    if (failed_update) *failed_update = c->upd_failed;
+    return AD_OK;
 }
 
 int ad_cfk_update_device(ad_ctx* c, const ad_cfk_update_soa* u, void* stream, uint64_t* n_applied, ad_stats* stats)

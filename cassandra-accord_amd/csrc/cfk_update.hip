@@ -2202,6 +2202,7 @@ static int miss_after_batch(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const
         snprintf(b, sizeof(b), "cfk update %u: a dep its kind does not witness, absent from byId, is not an "
                                "ExclusiveSyncPoint (Updating.java:239-249)", w->h_ctl->err_idx);
         *err = b;
+        out->failed_update = w->h_ctl->err_idx;
         UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
         return AD_E_INVAL;
     }

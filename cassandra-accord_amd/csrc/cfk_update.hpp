@@ -127,6 +127,7 @@ struct CfkUpdOut {
     const uint64_t* key_pos = nullptr;
     bool rolled_back = false;      // the batch failed after it had been applied and was undone
     bool batch_stood = false;      // the explicit batch was applied and stands, whatever came after it
+    int64_t failed_update = -1;    // the update a failure names (batch index), -1: none
     uint64_t n_additions = 0;      // TRANSITIVELY_KNOWN entries inserted from deps (Updating.java:235-263)
     // additions below their key's prunedBefore, dropped (removePrunedAdditions) and handed back for
     // Pruning.loadPruned / PostProcess.LoadPruned (Updating.java:111-117,171): device arrays of the

@@ -91,17 +91,48 @@ struct Staging {
         return hipEventSynchronize(ev[k]);
     }
 };
-// per thread and device (a chunk's event belongs to the device of the streams it is recorded on);
-// never freed: a thread's chunks live as long as the process
+// A process-wide pool per device (a chunk's event belongs to the device of the streams it is recorded
+// on): a transfer checks a staging pair out and returns it, so the pairs number the most transfers ever in
+// flight at once -- not one per thread that ever called in (pooled or short-lived host threads, a Java
+// binding's, would otherwise each keep 2 x 8 MB of pinned memory). A pair returned with chunks still in
+// flight is waited for (its events) by the next user. The pool lives as long as the process.
 constexpr int MAX_DEV = 16;
-thread_local Staging tl_stage[MAX_DEV];
-Staging* staging()
-{
-    int d = 0;
-    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEV) return nullptr;
-    Staging* S = &tl_stage[d];
-    return S->init() ? S : nullptr;
-}
+struct StagingPool {
+    std::mutex mu;
+    std::vector<Staging*> free;
+};
+StagingPool g_stage_pool[MAX_DEV];
+struct StagingLease {
+    int d = -1;
+    Staging* s = nullptr;
+    StagingLease()
+    {
+        if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= MAX_DEV) return;
+        {
+            std::lock_guard<std::mutex> g(g_stage_pool[d].mu);
+            if (!g_stage_pool[d].free.empty())
+            {
+                s = g_stage_pool[d].free.back();
+                g_stage_pool[d].free.pop_back();
+            }
+        }
+        if (!s) s = new Staging();
+        if (!s->init())
+        {
+            std::lock_guard<std::mutex> g(g_stage_pool[d].mu);
+            g_stage_pool[d].free.push_back(s);        // whatever it holds is kept for a later init
+            s = nullptr;
+        }
+    }
+    ~StagingLease()
+    {
+        if (!s) return;
+        std::lock_guard<std::mutex> g(g_stage_pool[d].mu);
+        g_stage_pool[d].free.push_back(s);
+    }
+    StagingLease(const StagingLease&) = delete;
+    StagingLease& operator=(const StagingLease&) = delete;
+};
 
 // the guard band of an allocation of `bytes` at p, compared on the host (after the device is idle).
 // *first_bad = SIZE_MAX when the band could not be read (a device already faulted)
@@ -277,9 +308,9 @@ hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t st)
 {
     if (!bytes) return hipSuccess;
     if (host_pinned(src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
-    Staging* Sp = staging();
-    if (!Sp) return hipErrorOutOfMemory;
-    Staging& S = *Sp;
+    StagingLease lease;
+    if (!lease.s) return hipErrorOutOfMemory;
+    Staging& S = *lease.s;
     int k = 0;
     for (size_t off = 0; off < bytes; off += STAGE, k ^= 1)
     {
@@ -298,9 +329,9 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st)
 {
     if (!bytes) return hipSuccess;
     if (host_pinned(dst)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
-    Staging* Sp = staging();
-    if (!Sp) return hipErrorOutOfMemory;
-    Staging& S = *Sp;
+    StagingLease lease;
+    if (!lease.s) return hipErrorOutOfMemory;
+    Staging& S = *lease.s;
     // chunk i is copied to the host while chunk i + 1 is in flight
     size_t prev_off = 0, prev_n = 0;
     int k = 0;

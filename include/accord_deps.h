@@ -64,6 +64,9 @@ extern "C" {
 #define AD_E_CAPACITY         -9  /* id dictionary exceeds 2^28 entries                     */
 #define AD_E_SPACE           -10  /* a caller-provided output buffer is too small (sizes set) */
 #define AD_E_PEER            -11  /* another rank of an exchange step reported a failure     */
+#define AD_E_PARTIAL         -12  /* ad_cfk_update: the explicit updates were applied, what follows
+                                   * them (deps-derived additions, missing() lists) was not -- see
+                                   * ad_cfk_update_status                                      */
 
 /* ---- InternalStatus ordinals (CommandsForKey.java:493-501) -------------------------- */
 #define AD_ST_TRANSITIVELY_KNOWN                          0
@@ -636,7 +639,8 @@ int ad_recovery_batch_device(ad_ctx* ctx, const ad_query_soa* q_dev, uint32_t sc
  * monotone remap: nothing is re-sorted). A key without a CommandsForKey gets one (the store creates
  * it before the update; key indices renumbered, key hash and KeyLines follow). Errors (nothing
  * applied): AD_E_INVAL (status > 7, live range-domain id), AD_E_INCONSISTENT_ID, AD_E_DUP_EXEC (two
- * committed entries of a key with one executeAt, :1439). Ids and keys added by a failed batch stay
+ * committed entries of a key with one executeAt, :1439); AD_E_PARTIAL (the explicit updates applied,
+ * the deps-derived part not: ad_cfk_update_status). Ids and keys added by a failed batch stay
  * (an unreferenced id or an empty CommandsForKey changes no answer). Host copies (ad_cfk_entries, recovery views, SEQUENTIAL batches)
  * follow on demand. */
 /* TxnInfo.missing() and the deps-derived additions (Updating.insertOrUpdate, Updating.java:99-470):
@@ -683,6 +687,16 @@ typedef struct ad_cfk_update_soa {
 int ad_cfk_update(ad_ctx* ctx, const ad_cfk_update_soa* u, uint64_t* n_applied, ad_stats* stats);
 /* Device buffers, on `stream` (null: the context's stream). Synchronous on return. */
 int ad_cfk_update_device(ad_ctx* ctx, const ad_cfk_update_soa* u_dev, void* stream, uint64_t* n_applied, ad_stats* stats);
+/* What the last ad_cfk_update[_device] left: *applied = 1 when its explicit updates stand (AD_OK, or
+ * AD_E_PARTIAL), 0 when nothing was applied (every other error); *failed_update = the batch index of the
+ * update a failure names, -1 for none. AD_E_PARTIAL: a batch with deps whose update *failed_update
+ * carried a dep its kind does not witness that is absent from the key's byId and not an
+ * ExclusiveSyncPoint (Updating.java:239-249, where the Java throws) -- or a device failure in that
+ * second part: every explicit update stands (the Java would have applied those before the throwing
+ * one and none after it: the caller re-applies nothing, and fixes or drops the offending dep), no
+ * addition was inserted, and the missing() lists ask for a reload (ad_cfk_missing: AD_E_STATE until
+ * ad_cfk_missing_load). */
+int ad_cfk_update_status(const ad_ctx* ctx, int* applied, int64_t* failed_update);
 /* The LoadPruned requests of the last ad_cfk_update[_device] (Updating.java:111-117,171): for each
  * addition dropped below its key's prunedBefore, the update (batch index) whose deps held it, the key
  * and the TxnId -- the host issues the loads (Pruning.loadPruned). Batch order of the updates. Views

@@ -268,7 +268,7 @@ def test_load_pruned_collected():
 @pytest.mark.parametrize("seed", range(3))
 def test_unwitnessed_non_esp_dep_rejected(oracle, seed):
     # Updating.java:243-247: a dep the command's kind does not witness that falls between the key's byId
-    # entries must be an ExclusiveSyncPoint; anything else is the Java's IllegalStateException -> AD_E_INVAL
+    # entries must be an ExclusiveSyncPoint; anything else is the Java's IllegalStateException -> AD_E_PARTIAL
     w = _workload(95 + seed, n_hist_txns=220)
     rng = np.random.default_rng(950 + seed)
     st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
@@ -307,17 +307,30 @@ def test_unwitnessed_non_esp_dep_rejected(oracle, seed):
             U.cfk_update_missing(cfk, u, u.dep_off, u.deps)
         with pytest.raises(native.AccordDepsError) as e:
             st.cfk_update(u)
-        assert e.value.code == A.AD_E_INVAL and "ExclusiveSyncPoint" in str(e.value)
-        # the store still answers (the explicit batch stands, the lists ask for a reload)
+        # AD_E_PARTIAL, not AD_E_INVAL: the explicit updates stand (a caller must not retry the batch), the
+        # failing update is named, no addition was made and the lists ask for a reload
+        assert e.value.code == A.AD_E_PARTIAL and "ExclusiveSyncPoint" in str(e.value)
+        assert st.cfk_update_status() == (True, i)
+        exp, _ = U.cfk_update(cfk, u)
+        keys, seg, txn, _ = st.cfk_byid()
+        assert np.array_equal(keys, exp.keys) and np.array_equal(seg, exp.seg)
+        assert np.array_equal(txn.msb, exp.txn.msb) and np.array_equal(txn.lsb, exp.txn.lsb)
+        status, ex = st.cfk_entries()
+        assert np.array_equal(status, exp.status) and np.array_equal(ex.lsb, exp.exec.lsb)
+        with pytest.raises(native.AccordDepsError) as e2:
+            st.cfk_missing()
+        assert e2.value.code == A.AD_E_STATE
+        # the store still answers, as the oracle over the updated CommandsForKeys
         got = st.calculate_partial_deps(w.queries)
-        assert got.n_txns == len(w.queries)
+        w2 = type(w)(w.name, exp, w.cmds, w.redundant, w.queries, w.flags, w.params, w.range_start_inclusive, w.slices)
+        assert got.equals(oracle.resolve(w2))
     finally:
         st.close()
 
 
 def _kat_cases():
     """The hand-derived known answers of tests/test_cfk_update_oracle.py (test_kat_*), as (store, updates,
-    expect an AD_E_INVAL rejection)."""
+    expect the AD_E_PARTIAL rejection of Updating.java:247)."""
     import test_cfk_update_oracle as K
     W, R, esp = A.KIND_WRITE, A.KIND_READ, A.KIND_EXCLUSIVE_SYNC_POINT
     out = []
@@ -352,7 +365,8 @@ def test_hand_derived_kats_on_the_device(case):
         if rejects:
             with pytest.raises(native.AccordDepsError) as e:
                 st.cfk_update(u)
-            assert e.value.code == A.AD_E_INVAL
+            assert e.value.code == A.AD_E_PARTIAL
+            assert st.cfk_update_status() == (True, 0)
             return
         lp = []
         exp, applied, nadd = U.cfk_update_missing(cfk, u, u.dep_off, u.deps, load_pruned=lp)

@@ -122,3 +122,32 @@ def test_host_alloc_contract():
     assert native.lib().ad_host_alloc(1 << 20, C.byref(p)) == 0 and p.value and p.value % 4096 == 0
     assert native.lib().ad_host_free(p) == 0
     assert native.lib().ad_host_free(None) == 0
+
+
+@pytest.mark.parametrize("pin", [True, "register"])
+def test_views_outlive_their_hostout(pin):
+    # an array taken from a HostOut stays valid after the HostOut is released and collected: each block of
+    # output memory is its arrays' base, freed / unpinned by its own finalizer once no array is left
+    import gc
+    w = synth.random_small(5, n_keys=80, n_hist_txns=600, n_txns=300, max_keys=6, n_range_cmds=40)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        _, _, out = st.deps_batch_into(w.queries, pin=pin, materialise=False)
+        keep = out.txns[0][:int(out.off[1][-1])]                 # a view, not a copy
+        off = out.off                                            # the offsets block
+        exp_k, exp_o = keep.copy(), off.copy()
+        out.release()
+        del out
+        gc.collect()
+        # new pinned allocations that would reuse freed pages
+        more = [native.DeviceCommandStore.HostOut(st, len(w.queries), [4096] * 9, pin) for _ in range(3)]
+        assert np.array_equal(keep, exp_k) and np.array_equal(off, exp_o)
+        del more, keep, off
+        gc.collect()
+        # a caller's HostOut reused across batches is not released by the call
+        out2 = native.DeviceCommandStore.HostOut(st, len(w.queries), [1 << 16] * 9, pin)
+        _, _, out3 = st.deps_batch_into(w.queries, out=out2, materialise=False)
+        assert out3 is out2 and out2.off is not None
+    finally:
+        st.close()
