@@ -1871,7 +1871,7 @@ static hipError_t batch_wait(ad_ctx* c, hipStream_t st)
         if (hipError_t e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) return e;
     if (hipError_t e = hipEventRecord(c->ev_done, st)) return e;
     // bounded: busy polls for up to ~2 ms (a batch's usual span), then polls that yield the core (50 us
-    // sleeps), and after AD_WAIT_TIMEOUT_MS (default 120 s) the batch is given up (hipErrorTimeout ->
+    // sleeps), and after AD_WAIT_TIMEOUT_MS (default 120 s) the batch is given up (hipErrorLaunchTimeOut ->
     // AD_E_DEVICE) instead of a store thread spinning on a completion that never comes
     static const double timeout_ms = getenv("AD_WAIT_TIMEOUT_MS") ? atof(getenv("AD_WAIT_TIMEOUT_MS")) : 120000.0;
     const double t0 = now_ms();
@@ -1880,7 +1880,7 @@ static hipError_t batch_wait(ad_ctx* c, hipStream_t st)
     {
         const double dt = now_ms() - t0;
         if (dt < 2.0) continue;
-        if (dt > timeout_ms) return hipErrorTimeout;
+        if (dt > timeout_ms) return hipErrorLaunchTimeOut;
         std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
     return e;
