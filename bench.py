@@ -338,18 +338,28 @@ def bench_levels(args, rank, world, local, dev):
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
     dom = int(np.argmax(ms))
     pull = launches == args.steps          # one leveling launch per step: the rank-ordered dataflow (default)
-    if pull:
+    packed = bool(stats.get("packed"))
+    if packed:
+        names = ["k5 build (packed exec sort + key-chain sort + predecessor records)",
+                 "k5 rank-ordered dataflow (k_level_rec)"]
+    elif pull:
         names = ["k5 build (exec radix sort + key chains + predecessor CSR)", "k5 rank-ordered dataflow (k_level_pull)"]
     else:
         names = ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"]
     achieved = stats["bytes_stage"][dom] / (ms[dom] / 1000.0) / 1e9 if ms[dom] > 0 else 0.0
-    lk = "k_level_pull" if pull else "k_level_step"
+    lk = "k_level_rec<false>" if packed else ("k_level_pull<false>" if pull else "k_level_step")
     if dom == 1:
         traffic, traffic_src = measured_traffic([lk], tag="config5")
     else:
-        build = ["k_exec_words", "k_exec_gather", "k_radix_count", "k_radix_scatter", "k_scan_reduce", "k_scan_sums",
-                 "k_scan_tile", "k_exec_rank", "k_occ_fill", "k_chain<0>", "k_chain<1>", "k_chain<2>", "k_direct<0>",
-                 "k_direct<1>", "k_direct<2>", "__amd_rocclr_copyBuffer", "__amd_rocclr_fillBufferAligned"]
+        if packed:
+            build = ["k_exec_words", "k_exec_pack", "k_exec_rank_p", "k_direct_check", "k_occ_pack", "k_walk",
+                     "k_scan_reduce", "k_scan_sums", "k_scan_tile", "__amd_rocclr_copyBuffer",
+                     "__amd_rocclr_fillBufferAligned"] + ["k_rk_count<%d>" % d for d in range(8, 12)] + \
+                    ["k_rk_scatter<%d>" % d for d in range(8, 12)]
+        else:
+            build = ["k_exec_words", "k_exec_gather", "k_radix_count", "k_radix_scatter", "k_scan_reduce", "k_scan_sums",
+                     "k_scan_tile", "k_exec_rank", "k_occ_fill", "k_chain<0>", "k_chain<1>", "k_chain<2>", "k_direct<0>",
+                     "k_direct<1>", "k_direct<2>", "__amd_rocclr_copyBuffer", "__amd_rocclr_fillBufferAligned"]
         traffic, traffic_src = measured_traffic_per_step(build, "config5", lk)
     res = {
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,

@@ -836,7 +836,8 @@ def recover(workload, scan, device=0):
 
 def levels_stats(s):
     d = stats_dict(s)
-    d.update(n_levels=int(s.n_levels), n_edges=int(s.n_edges), n_launches=int(s.n_launches))
+    d.update(n_levels=int(s.n_levels), n_edges=int(s.n_edges), n_launches=int(s.n_launches),
+             packed=bool(s.n_deferred))
     return d
 
 

@@ -3826,6 +3826,7 @@ static int levels_run(ad_ctx* c, const LevelsIn& in, uint32_t* out_dev, hipStrea
         stats->n_levels = lo.n_levels;
         stats->n_edges = lo.n_edges;
         stats->n_launches = lo.n_launch;
+        stats->n_deferred = lo.packed ? 1 : 0;
         // algorithmic bytes: nodes x (8 B executeAt + 4 B offset + 4 B level)
         // + edges x 4 B; the build additionally reads the key occurrences (8 B each) once
         stats->bytes_stage[0] = in.n * 16 + lo.n_occ * 8;

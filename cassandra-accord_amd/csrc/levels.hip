@@ -373,12 +373,156 @@ static uint32_t digits_of(uint64_t diff)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Stable LSD radix sort of packed u64 keys (no values) on the bit field [lo, lo + bits): digits of
+// DB = 8..11 bits, as few passes as the field needs (a 17-bit field: two 9-bit passes, 42 bits: four
+// 11-bit ones). Same count / scan / scatter structure as the pair sort above; per-wave digit counts
+// in LDS as u32 (below 2^32 elements).
+// ---------------------------------------------------------------------------------------------
+template <int DB>
+__global__ __launch_bounds__(RS_THREADS) void k_rk_count(const uint64_t* __restrict__ k, uint64_t n, int shift,
+                                                          uint32_t* __restrict__ hist, uint32_t nblk)
+{
+    constexpr uint32_t R = 1u << DB;
+    __shared__ uint32_t h[R];
+    for (uint32_t d = threadIdx.x; d < R; d += RS_THREADS) h[d] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int c = 0; c < RS_CHUNKS; ++c)
+    {
+        const uint64_t i = base + (uint64_t)c * RS_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&h[(uint32_t)(k[i] >> shift) & (R - 1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < R; d += RS_THREADS) hist[(uint64_t)d * nblk + blockIdx.x] = h[d];
+}
+
+template <int DB>
+__global__ __launch_bounds__(RS_THREADS) void k_rk_scatter(const uint64_t* __restrict__ k, uint64_t n, int shift,
+                                                            const uint64_t* __restrict__ off, uint32_t nblk,
+                                                            uint64_t* __restrict__ ko)
+{
+    constexpr uint32_t R = 1u << DB;
+    __shared__ uint32_t cnt[RS_WAVES][R];
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint32_t d = threadIdx.x; d < RS_WAVES * R; d += RS_THREADS) (&cnt[0][0])[d] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * (RS_CHUNKS * 64);
+    uint64_t key[RS_CHUNKS];
+#pragma unroll
+    for (int c = 0; c < RS_CHUNKS; ++c)
+    {
+        const uint64_t i = base + (uint64_t)c * 64 + lane;
+        key[c] = i < n ? k[i] : 0;
+        if (i < n) atomicAdd(&cnt[w][(uint32_t)(key[c] >> shift) & (R - 1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < R; d += RS_THREADS)
+    {
+        uint32_t run = (uint32_t)off[(uint64_t)d * nblk + blockIdx.x];
+#pragma unroll
+        for (int ww = 0; ww < RS_WAVES; ++ww)
+        {
+            const uint32_t c = cnt[ww][d];
+            cnt[ww][d] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int c = 0; c < RS_CHUNKS; ++c)
+    {
+        const uint64_t i = base + (uint64_t)c * 64 + lane;
+        const bool live = i < n;
+        const uint32_t d = (uint32_t)(key[c] >> shift) & (R - 1);
+        uint64_t m = ballot(live);
+#pragma unroll
+        for (int bit = 0; bit < DB; ++bit)
+        {
+            const uint64_t b = ballot((d >> bit) & 1u);
+            m &= ((d >> bit) & 1u) ? b : ~b;
+        }
+        const uint32_t pos0 = live ? cnt[w][d] : 0u;
+        wave_lds_sync();
+        if (live)
+        {
+            ko[pos0 + (uint32_t)__popcll(m & lt)] = key[c];
+            if ((m >> lane) == 1ull) cnt[w][d] = pos0 + (uint32_t)__popcll(m);    // highest lane of its digit group
+        }
+        wave_lds_sync();
+    }
+}
+
+// the sorted keys end in *k_res (k_in or k_tmp)
+static hipError_t radix_sort_keys(uint64_t* k_in, uint64_t* k_tmp, uint64_t n, int lo, int bits, uint32_t* hist,
+                                  uint64_t* off, uint64_t* bsum, hipStream_t st, uint64_t** k_res)
+{
+    uint64_t* ka = k_in;
+    uint64_t* kb = k_tmp;
+    *k_res = ka;
+    if (n <= 1 || bits <= 0) return hipSuccess;
+    const int passes = (bits + 10) / 11;
+    const int db = std::max(8, (bits + passes - 1) / passes);
+    const uint32_t nblk = (uint32_t)std::max<uint64_t>(1, (n + RS_TILE - 1) / RS_TILE);
+    for (int p = 0; p < passes; ++p)
+    {
+        const int shift = lo + p * db;
+        switch (db)
+        {
+            case 8: k_rk_count<8><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, hist, nblk); break;
+            case 9: k_rk_count<9><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, hist, nblk); break;
+            case 10: k_rk_count<10><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, hist, nblk); break;
+            default: k_rk_count<11><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, hist, nblk); break;
+        }
+        hipError_t e = run_scan_arrays(hist, off, ((uint64_t)1 << db) * nblk, 1, bsum, st);
+        if (e != hipSuccess) return e;
+        switch (db)
+        {
+            case 8: k_rk_scatter<8><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, off, nblk, kb); break;
+            case 9: k_rk_scatter<9><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, off, nblk, kb); break;
+            case 10: k_rk_scatter<10><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, off, nblk, kb); break;
+            default: k_rk_scatter<11><<<nblk, RS_THREADS, 0, st>>>(ka, n, shift, off, nblk, kb); break;
+        }
+        std::swap(ka, kb);
+    }
+    *k_res = ka;
+    return hipGetLastError();
+}
+
+// hist entries the keys-only sort needs (2^11 digits per tile)
+static uint64_t radix_keys_hist_entries(uint64_t n)
+{
+    return 2048 * std::max<uint64_t>(1, (n + RS_TILE - 1) / RS_TILE);
+}
+
+// parallel bit extract: the bits of x under mask m, packed from bit 0 up in order (m uniform)
+__device__ __forceinline__ uint64_t pext64(uint64_t x, uint64_t m)
+{
+    uint64_t r = 0;
+    uint32_t o = 0;
+    while (m)
+    {
+        const uint32_t s = (uint32_t)__builtin_ctzll(m);
+        const uint64_t sh = m >> s;
+        const uint32_t len = ~sh == 0 ? 64u - s : (uint32_t)__builtin_ctzll(~sh);
+        const uint64_t lm = len >= 64 ? ~0ull : ((1ull << len) - 1);
+        r |= ((x >> s) & lm) << o;
+        o += len;
+        m &= ~(lm << s);
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------
 // K5 kernels
 // ---------------------------------------------------------------------------------------------
 struct LevelsCtl {
     unsigned long long diff[4];     // OR of (word ^ word of element 0): exec node, lo, hi; occurrence keys
     unsigned int error;             // AD_E_* (negated)
-    unsigned int pad;
+    unsigned int maxk;              // most keys of one txn
+    unsigned long long n_edges;     // packed path: key-chain + direct predecessors
+    unsigned long long pool_used;   // packed path: overflow predecessor words asked for
 };
 
 constexpr unsigned RED_BLOCKS = 512;     // grid of the reducing kernels: one atomic per block and word
@@ -400,24 +544,42 @@ __device__ __forceinline__ void block_or_to(unsigned long long* dst, uint64_t v,
 
 // normalised executeAt words (Timestamp.compareTo order, Timestamp.java:208-217, common.hpp
 // norm_tid): w0 = node with the sign flipped (signed compare), w1 = lowHlc|identity flags, w2 = msb
+// w0/idx null: the diffs only. The packed path also needs the occurrence keys' diff (n_occ keys)
+// and the most keys of one txn.
 __global__ __launch_bounds__(256) void k_exec_words(LevelsIn g, uint64_t* __restrict__ w0, uint32_t* __restrict__ idx,
-                                                    LevelsCtl* ctl)
+                                                    LevelsCtl* ctl, uint64_t n_occ)
 {
     __shared__ uint64_t red[4];
-    uint64_t d0 = 0, d1 = 0, d2 = 0;
+    uint64_t d0 = 0, d1 = 0, d2 = 0, dk = 0;
+    uint32_t mk = 0;
     const NormTid z = norm_tid(g.exec_msb[0], g.exec_lsb[0], g.exec_node[0]);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n; i += (uint64_t)gridDim.x * blockDim.x)
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n; i += stride)
     {
         const NormTid x = norm_tid(g.exec_msb[i], g.exec_lsb[i], g.exec_node[i]);
-        w0[i] = (uint64_t)((uint32_t)x.node ^ 0x80000000u);
-        idx[i] = (uint32_t)i;
+        if (w0)
+        {
+            w0[i] = (uint64_t)((uint32_t)x.node ^ 0x80000000u);
+            idx[i] = (uint32_t)i;
+        }
         d0 |= (uint64_t)((uint32_t)x.node ^ (uint32_t)z.node);
         d1 |= x.lo ^ z.lo;
         d2 |= x.hi ^ z.hi;
+        mk = max(mk, (uint32_t)std::min<uint64_t>(g.key_off[i + 1] - g.key_off[i], 0xFFFFFFFFull));
+    }
+    if (n_occ)
+    {
+        const uint64_t k0 = (uint64_t)g.keys[0];
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_occ; i += stride)
+            dk |= (uint64_t)g.keys[i] ^ k0;
     }
     block_or_to(&ctl->diff[0], d0, red);
     block_or_to(&ctl->diff[1], d1, red);
     block_or_to(&ctl->diff[2], d2, red);
+    block_or_to(&ctl->diff[3], dk, red);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mk = max(mk, (uint32_t)__shfl_xor(mk, d, 64));
+    if (lane_id() == 0 && mk) atomicMax(&ctl->maxk, mk);
 }
 
 // next (more significant) word of the current order
@@ -550,6 +712,233 @@ __global__ void k_direct(LevelsIn g, const uint32_t* __restrict__ rank, uint32_t
     if (PASS == 0 && npred) atomicAdd(&indeg[T], npred);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Packed path (the default when the fields fit one u64):
+//   exec word  = hi | lo | node bits that vary over the batch (pext, order kept) << rb | txn index
+//   occurrence = key bits that vary << (rb + 3 + jb) | exec rank << (3 + jb) | kind (clamped to 7)
+//                << jb | index of the key in the txn's key list
+// Both are sorted keys-only, on the varying field alone: the exec words by their Timestamp bits,
+// the occurrences (generated in rank order) stably by key. One walk over the sorted occurrences
+// writes every occurrence's sparsified predecessors into the txn-major record of that occurrence
+// (PredRec at occ_off[rank] + j: up to three inline, more in an overflow pool), so a txn's
+// predecessors sit in its own consecutive records -- no in-degree pass, no atomics per edge.
+// ---------------------------------------------------------------------------------------------
+struct PackCfg {
+    uint64_t m_node, m_lo, m_hi, m_key;     // varying bits
+    uint32_t rb, jb;                        // rank bits, key-list index bits
+    uint32_t s_lo, s_hi;                    // exec word: shifts of the lo and hi fields
+    uint32_t ks;                            // occurrence: shift of the key field
+};
+
+// A predecessor record (uint4 rec[o], uint4 rec2[o]): x = count (0..7), y/z/w the first three, rec2's
+// x..w the next four; or x = REC_OVF, y = pool offset, z = count for more than REC_INLINE.
+constexpr uint32_t REC_OVF = 0x80000000u;
+constexpr uint32_t REC_INLINE = 7;
+
+__global__ __launch_bounds__(256) void k_exec_pack(LevelsIn g, PackCfg p, uint64_t* __restrict__ out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= g.n) return;
+    const NormTid x = norm_tid(g.exec_msb[i], g.exec_lsb[i], g.exec_node[i]);
+    const uint64_t node = (uint64_t)((uint32_t)x.node ^ 0x80000000u);
+    out[i] = (pext64(x.hi, p.m_hi) << p.s_hi) | (pext64(x.lo, p.m_lo) << p.s_lo) | (pext64(node, p.m_node) << p.rb) | i;
+}
+
+// order[r] = txn of exec rank r, rank[t] = r, key count by rank; equal Timestamps are adjacent ->
+// AD_E_DUP_EXEC (CommandsForKey.java:1439)
+__global__ void k_exec_rank_p(LevelsIn g, const uint64_t* __restrict__ sorted, uint32_t rb, uint32_t* __restrict__ order,
+                              uint32_t* __restrict__ rank, uint32_t* __restrict__ kcnt_r, LevelsCtl* ctl)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= g.n) return;
+    const uint64_t e = sorted[r];
+    const uint32_t t = (uint32_t)(e & ((1ull << rb) - 1));
+    order[r] = t;
+    rank[t] = (uint32_t)r;
+    kcnt_r[r] = (uint32_t)(g.key_off[t + 1] - g.key_off[t]);
+    if (r > 0 && (sorted[r - 1] >> rb) == (e >> rb)) atomicCAS(&ctl->error, 0u, (unsigned)(-AD_E_DUP_EXEC));
+}
+
+__global__ __launch_bounds__(256) void k_occ_pack(LevelsIn g, PackCfg p, const uint32_t* __restrict__ order,
+                                                  const uint64_t* __restrict__ occ_off, uint64_t* __restrict__ out)
+{
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < g.n; r += (uint64_t)gridDim.x * blockDim.x)
+    {
+        const uint32_t t = order[r];
+        const uint64_t s = g.key_off[t], e = g.key_off[t + 1], o = occ_off[r];
+        const uint32_t kd = g.kind[t];
+        const uint64_t w = (r << (3 + p.jb)) | ((uint64_t)(kd < 7u ? kd : 7u) << p.jb);
+        for (uint64_t j = s; j < e; ++j)
+            out[o + (j - s)] = (pext64((uint64_t)g.keys[j], p.m_key) << p.ks) | w | (j - s);
+    }
+}
+
+// walk the chain back from occurrence p (sorted by key, then rank) as k_chain does: the first seven
+// predecessors to P[0..6], every one to dst[i] when dst is given
+__device__ __forceinline__ uint32_t walk_preds(const uint64_t* __restrict__ occ, uint64_t p, uint64_t e, PackCfg c,
+                                               uint32_t rmask, uint32_t (&P)[REC_INLINE], uint32_t* __restrict__ dst)
+{
+    const uint64_t key = e >> c.ks;
+    const uint32_t A = kind_witnesses((uint32_t)(e >> c.jb) & 7u);
+    uint32_t D = 0, np = 0;
+    uint64_t q = p;
+    bool go = A != 0 && q > 0;
+    while (go)
+    {
+        // four occurrences per step: most walks end within them
+        uint64_t w[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) w[k] = q > k ? occ[q - 1 - k] : 0ull;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+        {
+            if (!go) continue;
+            if (q <= k || (w[k] >> c.ks) != key)
+            {
+                go = false;
+                continue;
+            }
+            const uint32_t kp = (uint32_t)(w[k] >> c.jb) & 7u;
+            const uint32_t bit = 1u << kp;
+            if (A & bit & ~D)
+            {
+                const uint32_t v = (uint32_t)(w[k] >> (3 + c.jb)) & rmask;
+                if (dst) dst[np] = v;
+                else
+                {
+#pragma unroll
+                    for (uint32_t z = 0; z < REC_INLINE; ++z)
+                        if (np == z) P[z] = v;
+                }
+                ++np;
+                D |= kind_witnesses(kp);
+            }
+            else if (D & bit)
+                D |= kind_witnesses(kp);
+            if ((A & ~D) == 0) go = false;
+        }
+        q = q > 4 ? q - 4 : 0;
+        if (q == 0) go = false;
+    }
+    return np;
+}
+
+// Counters written by many blocks are sharded (NSHARD words each, block b on shard b % NSHARD): one
+// device-scope atomic per block or wave then meets few others on its address.
+constexpr uint32_t NSHARD = 256;
+struct PackCnt {
+    unsigned long long edges[NSHARD];      // key-chain + direct predecessors
+    unsigned long long pool[NSHARD];       // overflow words taken from each pool shard
+};
+
+// wave-wide exclusive prefix of v and the total (lane 63's inclusive)
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t* total)
+{
+    const uint32_t inc = wave_incl_scan(v);
+    *total = (uint32_t)__shfl(inc, 63, 64);
+    return inc - v;
+}
+
+__device__ __forceinline__ void block_sum_to(unsigned long long* dst, uint64_t v, uint64_t* red /* LDS [4] */)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane_id() == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        const uint64_t x = red[0] + red[1] + red[2] + red[3];
+        if (x) atomicAdd(dst, (unsigned long long)x);
+    }
+    __syncthreads();
+}
+
+// Occurrence p's predecessors -> its record rec[occ_off[T] + j]: up to three inline, more in the
+// pool shard of the block (one atomic per wave; a shard that runs out is reported by its count and
+// the host repeats the run with larger shards)
+__global__ __launch_bounds__(256) void k_walk(const uint64_t* __restrict__ occ, uint64_t n_occ, PackCfg c,
+                                              const uint64_t* __restrict__ occ_off, uint4* __restrict__ rec,
+                                              uint4* __restrict__ rec2, uint32_t* __restrict__ pool, uint64_t shard_cap,
+                                              PackCnt* cnt)
+{
+    __shared__ uint64_t red[4];
+    const uint32_t shard = blockIdx.x % NSHARD;
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t rmask = (uint32_t)((1ull << c.rb) - 1);
+    uint64_t e = 0;
+    uint32_t P[REC_INLINE] = {0, 0, 0, 0, 0, 0, 0}, np = 0;
+    if (p < n_occ)
+    {
+        e = occ[p];
+        np = walk_preds(occ, p, e, c, rmask, P, nullptr);
+    }
+    // overflow words: one allocation per wave
+    const uint32_t want = np > REC_INLINE ? np : 0u;
+    uint32_t wtot = 0;
+    const uint32_t wpre = wave_excl(want, &wtot);
+    uint64_t base = 0;
+    if (wtot)
+    {
+        if (lane_id() == 0) base = atomicAdd(&cnt->pool[shard], (unsigned long long)wtot);
+        base = __shfl(base, 0, 64);
+    }
+    if (p < n_occ)
+    {
+        const uint32_t T = (uint32_t)(e >> (3 + c.jb)) & rmask;
+        const uint32_t j = (uint32_t)(e & ((1ull << c.jb) - 1));
+        const uint64_t o = occ_off[T] + j;
+        if (np <= REC_INLINE)
+        {
+            rec[o] = make_uint4(np, P[0], P[1], P[2]);
+            if (np > 3) rec2[o] = make_uint4(P[3], P[4], P[5], P[6]);
+        }
+        else
+        {
+            const uint64_t at = base + wpre;
+            if (at + np <= shard_cap) walk_preds(occ, p, e, c, rmask, P, pool + shard * shard_cap + at);
+            rec[o] = make_uint4(REC_OVF, (uint32_t)(shard * shard_cap + std::min<uint64_t>(at, shard_cap)), np, 0);
+        }
+    }
+    block_sum_to(&cnt->edges[shard], np, red);
+}
+
+// direct deps: index check, the count of those executing earlier (Commands.java:700-775), and per
+// exec rank T (dirp zeroed before): P + 1 when exactly one direct dep executes earlier (rank P),
+// DIRP_MANY | txn when more do (the level kernel then reads them itself), 0 when none does
+constexpr uint32_t DIRP_MANY = 0x80000000u;
+__global__ __launch_bounds__(256) void k_direct_check(LevelsIn g, const uint32_t* __restrict__ rank,
+                                                      uint32_t* __restrict__ dirp, PackCnt* cnt, LevelsCtl* ctl)
+{
+    __shared__ uint64_t red[4];
+    uint64_t ne = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.n; t += (uint64_t)gridDim.x * blockDim.x)
+    {
+        const uint64_t d0 = g.dep_off[t], d1 = g.dep_off[t + 1];
+        if (d0 == d1) continue;
+        const uint32_t T = rank[t];
+        uint32_t np = 0, first = 0;
+        for (uint64_t d = d0; d < d1; ++d)
+        {
+            const uint32_t src = g.deps[d];
+            if (src >= g.n)
+            {
+                atomicCAS(&ctl->error, 0u, (unsigned)(-AD_E_INVAL));
+                np = 0;
+                break;
+            }
+            const uint32_t P = rank[src];
+            if (P < T)
+            {
+                if (np == 0) first = P;
+                ++np;
+            }
+        }
+        if (np) dirp[T] = np == 1 ? first + 1u : (DIRP_MANY | (uint32_t)t);
+        ne += np;
+    }
+    block_sum_to(&cnt->edges[blockIdx.x % NSHARD], ne, red);
+}
+
 __device__ __forceinline__ void wave_append(uint32_t* __restrict__ front, uint32_t* cnt, bool take, uint32_t v)
 {
     const uint64_t m = ballot(take);
@@ -636,25 +1025,44 @@ __global__ __launch_bounds__(256) void k_level_step(uint32_t L, const uint32_t* 
 // Rank-ordered dataflow leveling. level[] (by exec rank) starts LV_UNSET. A wave takes the next 64
 // ranks by ticket, so the lowest unfinished rank always belongs to a running wave and every wait is
 // on a lower rank: a running wave (or a finished one) -- no deadlock whatever the dispatch order.
-// Each lane walks its predecessor list in order, PULL_IN_FLIGHT level loads at a time; a lane
-// blocked on an unset level retries after a sleep, a lane whose list is done publishes its level at
+// Each lane takes its predecessor list in batches of PULL_BATCH: the indices stay in registers and
+// every level of the batch is loaded at once; the unset ones are polled again after a sleep (one
+// load each, no index reload), and a lane whose list is done publishes its level at
 // once (lanes of the same wave may wait on it). The level word is its own flag (set once, from
 // LV_UNSET to its value): agent-scope relaxed atomics, i.e. sc1 stores and sc1 loads, the
 // single-granule hand-off of MI355X_MICROARCH.md (no payload to order). A wave still waiting after
 // `budget` wall-clock ticks gives up and flags the run (the host reports AD_E_STATE).
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t LV_UNSET = 0xFFFFFFFFu;
-constexpr uint32_t PULL_IN_FLIGHT = 4;
+constexpr uint32_t PULL_BATCH = 8;
 
 __device__ __forceinline__ uint32_t lv_poll(const uint32_t* p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// LOCAL: every hand-off stays inside one XCD. The first block to start names its XCD (HW_REG_XCC_ID)
+// the owner; blocks on any other XCD leave at once, so the owner's CUs share one L2. Levels are then
+// stored sc0 (the line stays in that L2) and polled sc1 (L1 bypassed, L2-served): a hand-off costs an
+// L2 round trip instead of a trip through the fabric. Placement decides only which blocks work.
+template <bool LOCAL>
 __global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* __restrict__ pred_off,
                                                     const uint32_t* __restrict__ pred, uint32_t* level, uint32_t* ticket,
-                                                    uint32_t* fail, uint64_t budget, uint32_t naps)
+                                                    uint32_t* fail, uint64_t budget, uint32_t naps, uint32_t* owner)
 {
+    if (LOCAL)
+    {
+        __shared__ uint32_t own_s;
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (threadIdx.x == 0)
+        {
+            const uint32_t o = atomicCAS(owner, 0u, xcc + 1u);
+            own_s = o == 0u ? xcc + 1u : o;
+        }
+        __syncthreads();
+        if (own_s != xcc + 1u) return;
+    }
     const uint32_t lane = lane_id();
     const uint64_t t_end = wall_clock64() + budget;
     while (true)
@@ -667,39 +1075,312 @@ __global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* 
         const bool on = T < n;
         uint64_t j = on ? pred_off[T] : 0;
         const uint64_t e = on ? pred_off[T + 1] : 0;
-        uint32_t mx = 0;
-        bool pending = on, waited = false;
+        uint32_t mx = 0, pend = 0, nb = 0;
+        uint32_t pi[PULL_BATCH];
+        bool pending = on, fresh = true;
         while (true)
         {
             if (pending)
             {
-                // a lane that was blocked polls only the predecessor it waits for; otherwise
-                // PULL_IN_FLIGHT levels are loaded together
-                bool blocked = false;
-                while (j < e && !blocked)
+                // a batch of up to PULL_BATCH predecessors: indices kept in registers, every level
+                // loaded at once; only the unset ones (bits of pend) are polled again
+                while (true)
                 {
-                    uint32_t v[PULL_IN_FLIGHT];
-                    const uint64_t w = waited ? 1 : PULL_IN_FLIGHT;
+                    if (fresh)
+                    {
+                        nb = (uint32_t)std::min<uint64_t>(PULL_BATCH, e - j);
 #pragma unroll
-                    for (uint32_t k = 0; k < PULL_IN_FLIGHT; ++k)
-                        v[k] = (k < w && j + k < e) ? lv_poll(level + pred[j + k]) : LV_UNSET;
+                        for (uint32_t k = 0; k < PULL_BATCH; ++k) pi[k] = k < nb ? pred[j + k] : 0u;
+                        uint32_t v[PULL_BATCH];
 #pragma unroll
-                    for (uint32_t k = 0; k < PULL_IN_FLIGHT; ++k)
-                        if (!blocked && k < w && j < e)
+                        for (uint32_t k = 0; k < PULL_BATCH; ++k) v[k] = k < nb ? lv_poll(level + pi[k]) : 0u;
+                        pend = 0;
+#pragma unroll
+                        for (uint32_t k = 0; k < PULL_BATCH; ++k)
+                            if (k < nb)
+                            {
+                                if (v[k] == LV_UNSET) pend |= 1u << k;
+                                else mx = max(mx, v[k] + 1u);
+                            }
+                        fresh = false;
+                    }
+                    else if (pend)
+                    {
+                        uint32_t v[PULL_BATCH];
+#pragma unroll
+                        for (uint32_t k = 0; k < PULL_BATCH; ++k) v[k] = (pend >> k) & 1u ? lv_poll(level + pi[k]) : LV_UNSET;
+#pragma unroll
+                        for (uint32_t k = 0; k < PULL_BATCH; ++k)
+                            if (((pend >> k) & 1u) && v[k] != LV_UNSET)
+                            {
+                                pend &= ~(1u << k);
+                                mx = max(mx, v[k] + 1u);
+                            }
+                    }
+                    if (pend) break;
+                    j += nb;
+                    if (j >= e)
+                    {
+                        if (LOCAL) __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        pending = false;
+                        break;
+                    }
+                    fresh = true;
+                }
+            }
+            if (!ballot(pending)) break;
+            if (wall_clock64() > t_end)
+            {
+                if (lane == 0) atomicOr(fail, 1u);
+                return;
+            }
+            for (uint32_t z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(4);
+        }
+    }
+}
+
+// The same dataflow over the packed path's predecessor records: txn T's predecessors are the records
+// [occ_off[T], occ_off[T+1]) (up to seven inline each, or an overflow run in the pool) and its direct
+// deps executing earlier (dirp[T]). Every predecessor index is fetched before the first level poll, so
+// a wait is only ever on levels: a txn with at most four keys and at most REC_SLOTS predecessors in all
+// takes them in one batch, compacted into the slots; any other takes one record / overflow chunk /
+// deps chunk per batch.
+constexpr uint32_t REC_SLOTS = 16;
+
+__device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
+}
+
+template <bool LOCAL>
+__global__ __launch_bounds__(256) void k_level_rec(LevelsIn g, const uint64_t* __restrict__ occ_off,
+                                                   const uint4* __restrict__ rec, const uint4* __restrict__ rec2,
+                                                   const uint32_t* __restrict__ pool, uint64_t pool_cap,
+                                                   const uint32_t* __restrict__ dirp, const uint32_t* __restrict__ rank,
+                                                   uint32_t* level, uint32_t* ticket, uint32_t* fail, uint64_t budget,
+                                                   uint32_t naps, uint32_t* owner)
+{
+    if (LOCAL)
+    {
+        __shared__ uint32_t own_s;
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (threadIdx.x == 0)
+        {
+            const uint32_t o = atomicCAS(owner, 0u, xcc + 1u);
+            own_s = o == 0u ? xcc + 1u : o;
+        }
+        __syncthreads();
+        if (own_s != xcc + 1u) return;
+    }
+    const uint64_t n = g.n;
+    const uint32_t lane = lane_id();
+    const uint64_t t_end = wall_clock64() + budget;
+    while (true)
+    {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(ticket, 1u);
+        c = __shfl(c, 0, 64);
+        if ((uint64_t)c * 64 >= n) return;
+        const uint64_t T = (uint64_t)c * 64 + lane;
+        const bool on = T < n;
+        const uint64_t o0 = on ? occ_off[T] : 0, o1 = on ? occ_off[T + 1] : 0;
+        const uint32_t dp = (on && dirp) ? dirp[T] : 0u;
+        const uint32_t nk = (uint32_t)(o1 - o0);
+        uint4 r4[4], q4[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+        {
+            r4[i] = i < nk ? rec[o0 + i] : make_uint4(0, 0, 0, 0);
+            q4[i] = i < nk ? rec2[o0 + i] : make_uint4(0, 0, 0, 0);
+        }
+        // direct deps: one (its rank in dirp), or several (read here)
+        uint64_t d0 = 0, d1 = 0;
+        const bool dmany = (dp & DIRP_MANY) != 0;
+        if (dmany)
+        {
+            d0 = g.dep_off[dp & ~DIRP_MANY];
+            d1 = g.dep_off[(dp & ~DIRP_MANY) + 1];
+        }
+        const uint32_t nd = dmany ? (uint32_t)std::min<uint64_t>(d1 - d0, 0xFFFFull) : (dp ? 1u : 0u);
+        uint32_t cn[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i)
+        {
+            const bool ovf = (r4[i].x & REC_OVF) != 0;
+            cn[i] = ovf ? (r4[i].y + (uint64_t)r4[i].z <= pool_cap ? r4[i].z : 0u) : r4[i].x;
+        }
+        const uint32_t b1 = cn[0], b2 = b1 + cn[1], b3 = b2 + cn[2], tot = b3 + cn[3];
+        uint32_t pi[REC_SLOTS];
+        uint32_t vm = 0;
+        // phase 0: the one-batch form (done when loaded); 1: a record per batch (s, pos); 2: several
+        // direct deps (pos); 3: done
+        uint32_t ph = 3, s = 0;
+        uint64_t pos = 0;
+        if (on && nk <= 4 && tot + nd <= REC_SLOTS)
+        {
+#pragma unroll
+            for (uint32_t k = 0; k < REC_SLOTS; ++k)
+            {
+                uint32_t v = 0;
+                bool valid = false;
+                if (k < tot)
+                {
+                    const uint32_t i = (k >= b1 ? 1u : 0u) + (k >= b2 ? 1u : 0u) + (k >= b3 ? 1u : 0u);
+                    const uint32_t q = k - sel4(i, 0u, b1, b2, b3);
+                    const uint32_t x = sel4(i, r4[0].x, r4[1].x, r4[2].x, r4[3].x);
+                    const uint32_t y = sel4(i, r4[0].y, r4[1].y, r4[2].y, r4[3].y);
+                    if (x & REC_OVF) v = pool[(uint64_t)y + q];
+                    else if (q == 0) v = y;
+                    else if (q == 1) v = sel4(i, r4[0].z, r4[1].z, r4[2].z, r4[3].z);
+                    else if (q == 2) v = sel4(i, r4[0].w, r4[1].w, r4[2].w, r4[3].w);
+                    else if (q == 3) v = sel4(i, q4[0].x, q4[1].x, q4[2].x, q4[3].x);
+                    else if (q == 4) v = sel4(i, q4[0].y, q4[1].y, q4[2].y, q4[3].y);
+                    else if (q == 5) v = sel4(i, q4[0].z, q4[1].z, q4[2].z, q4[3].z);
+                    else v = sel4(i, q4[0].w, q4[1].w, q4[2].w, q4[3].w);
+                    valid = true;
+                }
+                else if (k < tot + nd)
+                {
+                    if (dmany)
+                    {
+                        const uint32_t src = g.deps[d0 + (k - tot)];
+                        v = src < n ? rank[src] : 0xFFFFFFFFu;
+                        valid = (uint64_t)v < T;
+                    }
+                    else
+                    {
+                        v = dp - 1u;
+                        valid = true;
+                    }
+                }
+                pi[k] = v;
+                if (valid) vm |= 1u << k;
+            }
+        }
+        else if (on)
+            ph = 1;
+        uint32_t mx = 0, pend = 0;
+        const bool pending0 = on;
+        bool pending = pending0, fresh = ph != 3;
+        if (!fresh && on)
+        {
+            uint32_t v[REC_SLOTS];
+#pragma unroll
+            for (uint32_t k = 0; k < REC_SLOTS; ++k) v[k] = (vm >> k) & 1u ? lv_poll(level + pi[k]) : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < REC_SLOTS; ++k)
+                if ((vm >> k) & 1u)
+                {
+                    if (v[k] == LV_UNSET) pend |= 1u << k;
+                    else mx = max(mx, v[k] + 1u);
+                }
+        }
+        while (true)
+        {
+            if (pending)
+            {
+                while (true)
+                {
+                    if (fresh)
+                    {
+                        vm = 0;
+                        if (ph == 1)
                         {
-                            if (v[k] == LV_UNSET) blocked = true;
+                            if (s < nk)
+                            {
+                                const uint4 r = rec[o0 + s];
+                                if (r.x & REC_OVF)
+                                {
+                                    const uint64_t cnt = r.z, at = r.y;
+                                    const uint32_t m = (uint32_t)std::min<uint64_t>(REC_SLOTS, cnt - pos);
+                                    const bool ok = at + cnt <= pool_cap;     // else the host repeats the run
+#pragma unroll
+                                    for (uint32_t k = 0; k < REC_SLOTS; ++k) pi[k] = (ok && k < m) ? pool[at + pos + k] : 0u;
+                                    vm = ok ? (uint32_t)((1ull << m) - 1u) : 0u;
+                                    pos += m;
+                                    if (pos >= cnt)
+                                    {
+                                        ++s;
+                                        pos = 0;
+                                    }
+                                }
+                                else
+                                {
+                                    const uint4 q = r.x > 3 ? rec2[o0 + s] : make_uint4(0, 0, 0, 0);
+                                    pi[0] = r.y;
+                                    pi[1] = r.z;
+                                    pi[2] = r.w;
+                                    pi[3] = q.x;
+                                    pi[4] = q.y;
+                                    pi[5] = q.z;
+                                    pi[6] = q.w;
+                                    vm = (1u << r.x) - 1u;
+                                    ++s;
+                                }
+                            }
+                            else if (dp && !dmany)
+                            {
+                                pi[0] = dp - 1u;
+                                vm = 1;
+                                ph = 3;
+                            }
                             else
                             {
-                                mx = max(mx, v[k] + 1u);
-                                ++j;
+                                ph = dmany && d0 < d1 ? 2 : 3;
+                                pos = 0;
                             }
                         }
-                    waited = blocked;
-                }
-                if (!blocked)
-                {
-                    __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    pending = false;
+                        else if (ph == 2)
+                        {
+                            const uint32_t m = (uint32_t)std::min<uint64_t>(REC_SLOTS, d1 - d0 - pos);
+#pragma unroll
+                            for (uint32_t k = 0; k < REC_SLOTS; ++k)
+                            {
+                                const uint32_t src = k < m ? g.deps[d0 + pos + k] : 0xFFFFFFFFu;
+                                const uint32_t P = src < n ? rank[src] : 0xFFFFFFFFu;
+                                pi[k] = P;
+                                if ((uint64_t)P < T) vm |= 1u << k;
+                            }
+                            pos += m;
+                            if (d0 + pos >= d1) ph = 3;
+                        }
+                        uint32_t v[REC_SLOTS];
+#pragma unroll
+                        for (uint32_t k = 0; k < REC_SLOTS; ++k) v[k] = (vm >> k) & 1u ? lv_poll(level + pi[k]) : 0u;
+                        pend = 0;
+#pragma unroll
+                        for (uint32_t k = 0; k < REC_SLOTS; ++k)
+                            if ((vm >> k) & 1u)
+                            {
+                                if (v[k] == LV_UNSET) pend |= 1u << k;
+                                else mx = max(mx, v[k] + 1u);
+                            }
+                        fresh = false;
+                    }
+                    else if (pend)
+                    {
+                        uint32_t v[REC_SLOTS];
+#pragma unroll
+                        for (uint32_t k = 0; k < REC_SLOTS; ++k) v[k] = (pend >> k) & 1u ? lv_poll(level + pi[k]) : LV_UNSET;
+#pragma unroll
+                        for (uint32_t k = 0; k < REC_SLOTS; ++k)
+                            if (((pend >> k) & 1u) && v[k] != LV_UNSET)
+                            {
+                                pend &= ~(1u << k);
+                                mx = max(mx, v[k] + 1u);
+                            }
+                    }
+                    if (pend) break;
+                    if (ph == 3)
+                    {
+                        if (LOCAL) __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        pending = false;
+                        break;
+                    }
+                    fresh = true;
                 }
             }
             if (!ballot(pending)) break;
@@ -737,13 +1418,15 @@ using DBuf = DevBuf;
 
 struct LevelsWork {
     DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
-        level, front0, front1, cnt, ctl;
+        level, front0, front1, cnt, ctl, rec, rec2, pool, pcnt, dirp;
     LevelsCtl* h_ctl = nullptr;         // pinned
+    struct PackCnt* h_pcnt = nullptr;   // pinned
     uint64_t* h_u64 = nullptr;          // pinned, 4 words
     hipEvent_t ev[3] = {};
     ~LevelsWork()
     {
         if (h_ctl) (void)hipHostFree(h_ctl);
+        if (h_pcnt) (void)hipHostFree(h_pcnt);
         if (h_u64) (void)hipHostFree(h_u64);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -775,6 +1458,80 @@ constexpr unsigned STEP_BLOCKS = 64;
     } while (0)
 
 static unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)std::max<uint64_t>(1, (n + t - 1) / t); }
+
+// leveling launch: the fabric dataflow (one wave per CU) or the XCD-local one (AD_LEVELS_LOCAL)
+struct PullCfg {
+    bool local;
+    unsigned grid, threads;
+    uint32_t naps;
+    uint64_t budget;
+};
+
+static PullCfg pull_cfg(uint64_t n, bool packed)
+{
+    int dev = 0, cus = 256, khz = 100000;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    // measured on config 5 (scripts/c5_sweep.sh, c5_packed.sh): the CSR kernel at one wave per CU
+    // (0.59 ms; a 256-thread block per CU or 2 / 4 blocks were slower in round 4: the polls of more
+    // resident waiters load the memory system the hand-offs go through); the record kernel, whose
+    // per-task setup is longer, at four waves per CU (0.60 ms; 1.00 / 0.62 at one / two)
+    const char* le = getenv("AD_LEVELS_LOCAL");
+    PullCfg c;
+    c.local = le && atoi(le) != 0;
+    int per_cu = c.local ? 2 : (packed ? 4 : 1), naps = 1, threads = c.local ? 256 : 64;
+    if (const char* e = getenv("AD_LEVELS_PULL_PER_CU")) per_cu = std::max(1, std::min(8, atoi(e)));
+    if (const char* e = getenv("AD_LEVELS_PULL_NAPS")) naps = std::max(0, std::min(64, atoi(e)));
+    if (const char* e = getenv("AD_LEVELS_PULL_THREADS")) threads = atoi(e) == 64 ? 64 : (atoi(e) == 128 ? 128 : 256);
+    c.threads = (unsigned)threads;
+    c.naps = (uint32_t)naps;
+    c.budget = (uint64_t)std::max(khz, 1000) * 1000ull;       // one second of wall clock
+    const uint64_t tasks = (n + threads - 1) / threads;
+    // local: blocks are dealt over the 8 XCDs, so 8x the blocks wanted on the owner
+    c.grid = c.local ? std::max(8u, (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, 8 * tasks))
+                     : std::max(1u, (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, tasks));
+    return c;
+}
+
+struct PackPlan {
+    bool ok = false;
+    PackCfg cfg{};
+    uint32_t exec_bits = 0, key_bits = 0;
+};
+
+static uint32_t bit_len(uint64_t v) { return v ? 64u - (uint32_t)__builtin_clzll(v) : 0u; }
+
+// the packed path applies when both packed words fit 64 bits (and not under AD_LEVELS_FRONTIER /
+// AD_LEVELS_PACKED=0)
+static PackPlan pack_plan(const LevelsCtl& h, uint64_t n, uint64_t n_occ)
+{
+    PackPlan p;
+    if (getenv("AD_LEVELS_FRONTIER")) return p;
+    if (const char* e = getenv("AD_LEVELS_PACKED"))
+        if (atoi(e) == 0) return p;
+    if (n >= (1ull << 31) || n_occ >= (1ull << 32)) return p;     // dirp: rank + 1 or DIRP_MANY | txn
+    PackCfg& c = p.cfg;
+    c.m_node = h.diff[0] & 0xFFFFFFFFull;
+    c.m_lo = h.diff[1];
+    c.m_hi = h.diff[2];
+    c.m_key = h.diff[3];
+    c.rb = std::max(1u, bit_len(n - 1));
+    c.jb = h.maxk > 1 ? bit_len(h.maxk - 1) : 0u;
+    const uint32_t b0 = (uint32_t)__builtin_popcountll(c.m_node), b1 = (uint32_t)__builtin_popcountll(c.m_lo),
+                   b2 = (uint32_t)__builtin_popcountll(c.m_hi), bk = (uint32_t)__builtin_popcountll(c.m_key);
+    if (c.rb + b0 + b1 + b2 > 64 || bk + c.rb + 3 + c.jb > 64) return p;
+    c.s_lo = c.rb + b0;
+    c.s_hi = c.s_lo + b1;
+    c.ks = c.rb + 3 + c.jb;
+    p.exec_bits = b0 + b1 + b2;
+    p.key_bits = bk;
+    p.ok = true;
+    return p;
+}
+
+static int run_levels_packed(LevelsWork* w, const LevelsIn& g, const PackPlan& pp, uint64_t n_occ, uint32_t* level_out,
+                             hipStream_t st, LevelsOut* out, std::string* err);
 
 int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_t st, LevelsOut* out, std::string* err)
 {
@@ -842,15 +1599,19 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
 
     LV_CHK(hipEventRecord(w->ev[0], st));
     LV_CHK(hipMemsetAsync(ctl, 0, sizeof(LevelsCtl), st));
-    LV_CHK(hipMemsetAsync(indeg, 0, 4 * n, st));
-    LV_CHK(hipMemsetAsync(outdeg, 0, 4 * n, st));
-    LV_CHK(hipMemsetAsync(cursor, 0, 4 * n, st));
     LV_CHK(hipMemsetAsync(cnt, 0, 4 * (n + 2 + STEP_CHUNK), st));
 
     // ---- 1. exec ranking: LSD over node, then lowHlc|flags, then msb
-    k_exec_words<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, ka, va, ctl);
+    k_exec_words<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, ka, va, ctl, n_occ);
     LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
     LV_CHK(hipStreamSynchronize(st));
+    {
+        const PackPlan pp = pack_plan(*w->h_ctl, n, n_occ);
+        if (pp.ok) return run_levels_packed(w, g, pp, n_occ, level_out, st, out, err);
+    }
+    LV_CHK(hipMemsetAsync(indeg, 0, 4 * n, st));
+    LV_CHK(hipMemsetAsync(outdeg, 0, 4 * n, st));
+    LV_CHK(hipMemsetAsync(cursor, 0, 4 * n, st));
     const uint64_t dx[3] = {w->h_ctl->diff[0], w->h_ctl->diff[1], w->h_ctl->diff[2]};
     uint64_t* kcur = ka;
     uint32_t* vcur = va;
@@ -928,22 +1689,14 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     uint64_t nl = 0;
     if (pull)
     {
-        int dev = 0, cus = 256, khz = 100000;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-        // measured on config 5 (scripts/c5_sweep.sh): one wave per CU (0.85 ms) beats a 256-thread block
-        // per CU (1.01 ms) and 2 / 4 blocks (1.13 / 1.50 ms): the polls of more resident waiters load the
-        // memory system the hand-offs go through; naps between polls hardly matter at that residency
-        int per_cu = 1, naps = 1, threads = 64;
-        if (const char* e = getenv("AD_LEVELS_PULL_PER_CU")) per_cu = std::max(1, std::min(8, atoi(e)));
-        if (const char* e = getenv("AD_LEVELS_PULL_NAPS")) naps = std::max(0, std::min(64, atoi(e)));
-        if (const char* e = getenv("AD_LEVELS_PULL_THREADS")) threads = atoi(e) == 64 ? 64 : (atoi(e) == 128 ? 128 : 256);
-        // cnt[0] ticket, cnt[1] failure flag, cnt[2] max level (zeroed above)
+        const PullCfg pc = pull_cfg(n, false);
         LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
-        const uint64_t budget = (uint64_t)std::max(khz, 1000) * 1000ull;       // one second of wall clock
-        const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, (n + threads - 1) / threads);
-        k_level_pull<<<std::max(1u, grid), threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, budget, (uint32_t)naps);
+        if (pc.local)
+            k_level_pull<true><<<pc.grid, pc.threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, pc.budget, pc.naps,
+                                                               cnt + 3);
+        else
+            k_level_pull<false><<<pc.grid, pc.threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, pc.budget, pc.naps,
+                                                                nullptr);
         LV_CHK(hipGetLastError());
         out->n_launch = 1;
         k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);
@@ -999,6 +1752,146 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
         }
     }
     out->n_levels = nl;
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
+    (void)hipEventElapsedTime(&b, w->ev[1], w->ev[2]);
+    out->ms_build = a;
+    out->ms_frontier = b;
+    out->ms_total = a + b;
+    return AD_OK;
+}
+
+static int run_levels_packed(LevelsWork* w, const LevelsIn& g, const PackPlan& pp, uint64_t n_occ, uint32_t* level_out,
+                             hipStream_t st, LevelsOut* out, std::string* err)
+{
+    const uint64_t n = g.n;
+    const PackCfg& c = pp.cfg;
+    const uint64_t cap = std::max(n, n_occ);
+    const uint64_t hist_n = std::max(radix_hist_entries(cap), radix_keys_hist_entries(cap));
+    LV_ALLOC(w->hist, 4 * hist_n);
+    LV_ALLOC(w->off, 8 * (hist_n + 1));
+    LV_ALLOC(w->bsum, 8 * (std::max(hist_n, n) / 1024 + 2));
+    LV_ALLOC(w->rec, 16 * std::max<uint64_t>(n_occ, 1));
+    LV_ALLOC(w->rec2, 16 * std::max<uint64_t>(n_occ, 1));
+    LV_ALLOC(w->pcnt, sizeof(PackCnt));
+    if (g.dep_off) LV_ALLOC(w->dirp, 4 * n);
+    if (!w->h_pcnt) LV_CHK(hipHostMalloc((void**)&w->h_pcnt, sizeof(PackCnt), hipHostMallocDefault));
+    // overflow pool: NSHARD shards; grown to what a run asked for when that run did not fit (it is then
+    // repeated)
+    uint64_t shard_cap = std::max<uint64_t>(w->pool.cap / 4 / NSHARD, std::max<uint64_t>(n_occ / 8 / NSHARD, 64));
+    if (shard_cap * NSHARD >= (1ull << 32))
+    {
+        *err = "ad_levels: predecessor pool beyond 2^32 words";
+        return AD_E_CAPACITY;
+    }
+    LV_ALLOC(w->pool, 4 * shard_cap * NSHARD);
+    LevelsCtl* ctl = w->ctl.as<LevelsCtl>();
+    PackCnt* pcnt = w->pcnt.as<PackCnt>();
+    uint32_t* dirp = g.dep_off ? w->dirp.as<uint32_t>() : nullptr;
+    uint64_t* ka = w->ka.as<uint64_t>();
+    uint64_t* kb = w->kb.as<uint64_t>();
+    uint32_t* hist = w->hist.as<uint32_t>();
+    uint64_t* off = w->off.as<uint64_t>();
+    uint64_t* bsum = w->bsum.as<uint64_t>();
+    uint32_t* order = w->ord.as<uint32_t>();
+    uint32_t* rank = w->rank.as<uint32_t>();
+    uint64_t* occ_off = w->occ_off.as<uint64_t>();
+    uint32_t* level = w->level.as<uint32_t>();
+    uint32_t* cnt = w->cnt.as<uint32_t>();
+    uint4* rec = w->rec.as<uint4>();
+    uint4* rec2 = w->rec2.as<uint4>();
+
+    LV_CHK(hipMemsetAsync(pcnt, 0, sizeof(PackCnt), st));
+    // ---- 1. exec ranking: one keys-only sort of the packed exec words
+    k_exec_pack<<<blocks_for(n, 256), 256, 0, st>>>(g, c, ka);
+    uint64_t* sorted = nullptr;
+    LV_CHK(radix_sort_keys(ka, kb, n, (int)c.rb, (int)pp.exec_bits, hist, off, bsum, st, &sorted));
+    k_exec_rank_p<<<blocks_for(n, 256), 256, 0, st>>>(g, sorted, c.rb, order, rank, w->kcnt.as<uint32_t>(), ctl);
+    LV_CHK(run_scan_arrays(w->kcnt.as<uint32_t>(), occ_off, n, 1, bsum, st));
+    if (g.dep_off)
+    {
+        LV_CHK(hipMemsetAsync(dirp, 0, 4 * n, st));
+        k_direct_check<<<std::min(blocks_for(n, 256), 1024u), 256, 0, st>>>(g, rank, dirp, pcnt, ctl);
+    }
+
+    // ---- 2. occurrences (rank order) sorted stably by key, one walk -> predecessor records
+    uint64_t* occ = sorted == ka ? kb : ka;
+    uint64_t* otmp = sorted;
+    if (n_occ)
+    {
+        k_occ_pack<<<std::min(blocks_for(n, 256), 4096u), 256, 0, st>>>(g, c, order, occ_off, occ);
+        LV_CHK(radix_sort_keys(occ, otmp, n_occ, (int)c.ks, (int)pp.key_bits, hist, off, bsum, st, &occ));
+    }
+    const PullCfg pc = pull_cfg(n, true);
+    for (int attempt = 0;; ++attempt)
+    {
+        uint32_t* pool = w->pool.as<uint32_t>();
+        if (n_occ)
+            k_walk<<<blocks_for(n_occ, 256), 256, 0, st>>>(occ, n_occ, c, occ_off, rec, rec2, pool, shard_cap, pcnt);
+        LV_CHK(hipEventRecord(w->ev[1], st));
+
+        // ---- 3. level the DAG (rank-ordered dataflow over the records)
+        LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
+        const uint64_t pool_cap = shard_cap * NSHARD;
+        if (pc.local)
+            k_level_rec<true><<<pc.grid, pc.threads, 0, st>>>(g, occ_off, rec, rec2, pool, pool_cap, dirp, rank, level, cnt, cnt + 1,
+                                                              pc.budget, pc.naps, cnt + 3);
+        else
+            k_level_rec<false><<<pc.grid, pc.threads, 0, st>>>(g, occ_off, rec, rec2, pool, pool_cap, dirp, rank, level, cnt,
+                                                               cnt + 1, pc.budget, pc.naps, nullptr);
+        LV_CHK(hipGetLastError());
+        out->n_launch = 1;
+        k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);
+        k_level_out<<<blocks_for(n, 256), 256, 0, st>>>(order, level, n, level_out);
+        LV_CHK(hipEventRecord(w->ev[2], st));
+        uint32_t tail[3];
+        LV_CHK(d2h(tail, cnt, sizeof(tail), st));
+        LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
+        LV_CHK(d2h(w->h_pcnt, pcnt, sizeof(PackCnt), st));
+        LV_CHK(hipStreamSynchronize(st));
+        if (w->h_ctl->error)
+        {
+            const int code = -(int)w->h_ctl->error;
+            *err = code == AD_E_DUP_EXEC ? "ad_levels: two txns with the same executeAt (CommandsForKey.java:1439)"
+                                         : "ad_levels: direct dep index out of range";
+            return code;
+        }
+        uint64_t need = 0, edges = 0;
+        for (uint32_t i = 0; i < NSHARD; ++i)
+        {
+            need = std::max<uint64_t>(need, w->h_pcnt->pool[i]);
+            edges += w->h_pcnt->edges[i];
+        }
+        if (need > shard_cap)
+        {
+            // a pool shard was too small: repeat the walk and the leveling with the size asked for
+            if (attempt > 0)
+            {
+                *err = "ad_levels: predecessor pool did not fit twice";
+                return AD_E_STATE;
+            }
+            shard_cap = need;
+            if (shard_cap * NSHARD >= (1ull << 32))
+            {
+                *err = "ad_levels: predecessor pool beyond 2^32 words";
+                return AD_E_CAPACITY;
+            }
+            LV_ALLOC(w->pool, 4 * shard_cap * NSHARD);
+            LV_CHK(hipMemsetAsync(cnt, 0, 4 * 4, st));
+            LV_CHK(hipMemsetAsync(pcnt, 0, sizeof(PackCnt), st));
+            if (g.dep_off) k_direct_check<<<std::min(blocks_for(n, 256), 1024u), 256, 0, st>>>(g, rank, dirp, pcnt, ctl);
+            continue;
+        }
+        if (tail[1])
+        {
+            *err = "ad_levels: a wave waited more than a second for a predecessor's level";
+            return AD_E_STATE;
+        }
+        out->n_edges = edges;
+        out->n_levels = (uint64_t)tail[2] + 1;
+        out->packed = true;
+        break;
+    }
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
     (void)hipEventElapsedTime(&b, w->ev[1], w->ev[2]);

@@ -26,6 +26,7 @@ struct LevelsOut {
     uint64_t n_edges = 0;        // edges of the sparsified waitingOn DAG (key chains + direct deps)
     uint64_t n_occ = 0;          // txn-key occurrences
     uint64_t n_launch = 0;       // frontier-step launches (incl. the empty tail of the last chunk)
+    bool packed = false;         // the packed path ran (keys-only sorts, predecessor records)
     double ms_build = 0;         // exec ranking + key chains + CSR of successors (HIP events)
     double ms_frontier = 0;      // frontier loop
     double ms_total = 0;

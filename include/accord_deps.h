@@ -226,7 +226,9 @@ typedef struct ad_stats {
                                       * the resolve is split further: 2 k_prepare, 0 lean pass 1,
                                       * 3 lean pass 2, 6 general kernel (three more event records,
                                       * ~4 us of idle GPU each, so off by default) */
-    uint64_t n_deferred;             /* requests resolved by the split kernels (path 0)       */
+    uint64_t n_deferred;             /* requests resolved by the split kernels (path 0);
+                                      * ad_levels: 1 when the packed path ran (keys-only sorts,
+                                      * predecessor records), 0 for the CSR path               */
     uint64_t bytes_stage[8];         /* algorithmic bytes per stage            */
     /* ad_levels: n_txns, n_probes = txn-key occurrences, ms_stage[0] build (exec ranking, key
      * chains, successor CSR), ms_stage[1] frontier loop, and: */
