@@ -387,12 +387,16 @@ __global__ __launch_bounds__(RS_THREADS) void k_rk_count(const uint64_t* __restr
     for (uint32_t d = threadIdx.x; d < R; d += RS_THREADS) h[d] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
-#pragma unroll 4
+    uint64_t key[RS_CHUNKS];
+#pragma unroll
     for (int c = 0; c < RS_CHUNKS; ++c)
     {
         const uint64_t i = base + (uint64_t)c * RS_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&h[(uint32_t)(k[i] >> shift) & (R - 1)], 1u);
+        key[c] = i < n ? k[i] : 0;
     }
+#pragma unroll
+    for (int c = 0; c < RS_CHUNKS; ++c)
+        if (base + (uint64_t)c * RS_THREADS + threadIdx.x < n) atomicAdd(&h[(uint32_t)(key[c] >> shift) & (R - 1)], 1u);
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < R; d += RS_THREADS) hist[(uint64_t)d * nblk + blockIdx.x] = h[d];
 }
@@ -523,6 +527,15 @@ struct LevelsCtl {
     unsigned int maxk;              // most keys of one txn
     unsigned long long n_edges;     // packed path: key-chain + direct predecessors
     unsigned long long pool_used;   // packed path: overflow predecessor words asked for
+    unsigned int mink_inv;          // ~(fewest keys of one txn)
+    unsigned int pad;
+};
+
+// k_exec_words' per-block partials, combined by k_exec_words_reduce (one block): a few hundred
+// blocks each ORing into the same control line would queue their atomics on it
+struct WordsPart {
+    unsigned long long diff[4];
+    unsigned int maxk, mink_inv;
 };
 
 constexpr unsigned RED_BLOCKS = 512;     // grid of the reducing kernels: one atomic per block and word
@@ -543,15 +556,15 @@ __device__ __forceinline__ void block_or_to(unsigned long long* dst, uint64_t v,
 }
 
 // normalised executeAt words (Timestamp.compareTo order, Timestamp.java:208-217, common.hpp
-// norm_tid): w0 = node with the sign flipped (signed compare), w1 = lowHlc|identity flags, w2 = msb
-// w0/idx null: the diffs only. The packed path also needs the occurrence keys' diff (n_occ keys)
-// and the most keys of one txn.
+// norm_tid): w0 = node with the sign flipped (signed compare), w1 = lowHlc|identity flags, w2 = msb.
+// w0/idx null: the diffs only. Also the occurrence keys' diff (n_occ keys) and the most / fewest keys
+// of one txn, per block into part[blockIdx.x].
 __global__ __launch_bounds__(256) void k_exec_words(LevelsIn g, uint64_t* __restrict__ w0, uint32_t* __restrict__ idx,
-                                                    LevelsCtl* ctl, uint64_t n_occ)
+                                                    WordsPart* __restrict__ part, uint64_t n_occ)
 {
-    __shared__ uint64_t red[4];
+    __shared__ uint64_t red[4][6];
     uint64_t d0 = 0, d1 = 0, d2 = 0, dk = 0;
-    uint32_t mk = 0;
+    uint32_t mk = 0, mi = 0;
     const NormTid z = norm_tid(g.exec_msb[0], g.exec_lsb[0], g.exec_node[0]);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g.n; i += stride)
@@ -565,21 +578,95 @@ __global__ __launch_bounds__(256) void k_exec_words(LevelsIn g, uint64_t* __rest
         d0 |= (uint64_t)((uint32_t)x.node ^ (uint32_t)z.node);
         d1 |= x.lo ^ z.lo;
         d2 |= x.hi ^ z.hi;
-        mk = max(mk, (uint32_t)std::min<uint64_t>(g.key_off[i + 1] - g.key_off[i], 0xFFFFFFFFull));
+        const uint32_t kc = (uint32_t)std::min<uint64_t>(g.key_off[i + 1] - g.key_off[i], 0xFFFFFFFFull);
+        mk = max(mk, kc);
+        mi = max(mi, ~kc);
     }
     if (n_occ)
     {
         const uint64_t k0 = (uint64_t)g.keys[0];
-        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_occ; i += stride)
-            dk |= (uint64_t)g.keys[i] ^ k0;
+        const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        uint64_t i = i0;
+        for (; i + 3 * stride < n_occ; i += 4 * stride)
+        {
+            const uint64_t a = (uint64_t)g.keys[i], b = (uint64_t)g.keys[i + stride], c = (uint64_t)g.keys[i + 2 * stride],
+                           d = (uint64_t)g.keys[i + 3 * stride];
+            dk |= (a ^ k0) | (b ^ k0) | (c ^ k0) | (d ^ k0);
+        }
+        for (; i < n_occ; i += stride) dk |= (uint64_t)g.keys[i] ^ k0;
     }
-    block_or_to(&ctl->diff[0], d0, red);
-    block_or_to(&ctl->diff[1], d1, red);
-    block_or_to(&ctl->diff[2], d2, red);
-    block_or_to(&ctl->diff[3], dk, red);
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) mk = max(mk, (uint32_t)__shfl_xor(mk, d, 64));
-    if (lane_id() == 0 && mk) atomicMax(&ctl->maxk, mk);
+    for (int d = 32; d >= 1; d >>= 1)
+    {
+        d0 |= __shfl_xor(d0, d, 64);
+        d1 |= __shfl_xor(d1, d, 64);
+        d2 |= __shfl_xor(d2, d, 64);
+        dk |= __shfl_xor(dk, d, 64);
+        mk = max(mk, (uint32_t)__shfl_xor(mk, d, 64));
+        mi = max(mi, (uint32_t)__shfl_xor(mi, d, 64));
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane_id() == 0)
+    {
+        red[w][0] = d0;
+        red[w][1] = d1;
+        red[w][2] = d2;
+        red[w][3] = dk;
+        red[w][4] = mk;
+        red[w][5] = mi;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6)
+    {
+        const uint32_t f = threadIdx.x;
+        uint64_t v = red[0][f];
+        for (uint32_t ww = 1; ww < (blockDim.x >> 6); ++ww) v = f < 4 ? (v | red[ww][f]) : std::max(v, red[ww][f]);
+        if (f < 4) part[blockIdx.x].diff[f] = v;
+        else if (f == 4) part[blockIdx.x].maxk = (uint32_t)v;
+        else part[blockIdx.x].mink_inv = (uint32_t)v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_exec_words_reduce(const WordsPart* __restrict__ part, uint32_t nb, LevelsCtl* ctl)
+{
+    __shared__ uint64_t red[4][6];
+    uint64_t d[4] = {0, 0, 0, 0};
+    uint32_t mk = 0, mi = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+    {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) d[f] |= part[b].diff[f];
+        mk = max(mk, part[b].maxk);
+        mi = max(mi, part[b].mink_inv);
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1)
+    {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) d[f] |= __shfl_xor(d[f], s, 64);
+        mk = max(mk, (uint32_t)__shfl_xor(mk, s, 64));
+        mi = max(mi, (uint32_t)__shfl_xor(mi, s, 64));
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane_id() == 0)
+    {
+        for (int f = 0; f < 4; ++f) red[w][f] = d[f];
+        red[w][4] = mk;
+        red[w][5] = mi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        for (uint32_t ww = 1; ww < (blockDim.x >> 6); ++ww)
+        {
+            for (int f = 0; f < 4; ++f) red[0][f] |= red[ww][f];
+            red[0][4] = std::max(red[0][4], red[ww][4]);
+            red[0][5] = std::max(red[0][5], red[ww][5]);
+        }
+        for (int f = 0; f < 4; ++f) ctl->diff[f] = red[0][f];
+        ctl->maxk = (uint32_t)red[0][4];
+        ctl->mink_inv = (uint32_t)red[0][5];
+    }
 }
 
 // next (more significant) word of the current order
@@ -728,6 +815,7 @@ struct PackCfg {
     uint32_t rb, jb;                        // rank bits, key-list index bits
     uint32_t s_lo, s_hi;                    // exec word: shifts of the lo and hi fields
     uint32_t ks;                            // occurrence: shift of the key field
+    uint32_t kuni;                          // every txn has kuni keys (occ_off[r] = r * kuni), else 0
 };
 
 // A predecessor record (uint4 rec[o], uint4 rec2[o]): x = count (0..7), y/z/w the first three, rec2's
@@ -760,8 +848,22 @@ __global__ void k_exec_rank_p(LevelsIn g, const uint64_t* __restrict__ sorted, u
 }
 
 __global__ __launch_bounds__(256) void k_occ_pack(LevelsIn g, PackCfg p, const uint32_t* __restrict__ order,
-                                                  const uint64_t* __restrict__ occ_off, uint64_t* __restrict__ out)
+                                                  const uint64_t* __restrict__ occ_off, uint64_t* __restrict__ out,
+                                                  uint64_t n_occ)
 {
+    if (p.kuni)
+    {
+        // thread per occurrence: consecutive threads read one txn's keys and write consecutive words
+        for (uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n_occ; o += (uint64_t)gridDim.x * blockDim.x)
+        {
+            const uint64_t r = o / p.kuni, j = o - r * p.kuni;
+            const uint32_t t = order[r];
+            const uint32_t kd = g.kind[t];
+            out[o] = (pext64((uint64_t)g.keys[(uint64_t)t * p.kuni + j], p.m_key) << p.ks) | (r << (3 + p.jb)) |
+                     ((uint64_t)(kd < 7u ? kd : 7u) << p.jb) | j;
+        }
+        return;
+    }
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < g.n; r += (uint64_t)gridDim.x * blockDim.x)
     {
         const uint32_t t = order[r];
@@ -886,7 +988,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint64_t* __restrict__ occ, 
     {
         const uint32_t T = (uint32_t)(e >> (3 + c.jb)) & rmask;
         const uint32_t j = (uint32_t)(e & ((1ull << c.jb) - 1));
-        const uint64_t o = occ_off[T] + j;
+        const uint64_t o = (c.kuni ? (uint64_t)T * c.kuni : occ_off[T]) + j;
         if (np <= REC_INLINE)
         {
             rec[o] = make_uint4(np, P[0], P[1], P[2]);
@@ -1159,7 +1261,7 @@ __global__ __launch_bounds__(256) void k_level_rec(LevelsIn g, const uint64_t* _
                                                    const uint32_t* __restrict__ pool, uint64_t pool_cap,
                                                    const uint32_t* __restrict__ dirp, const uint32_t* __restrict__ rank,
                                                    uint32_t* level, uint32_t* ticket, uint32_t* fail, uint64_t budget,
-                                                   uint32_t naps, uint32_t* owner)
+                                                   uint32_t naps, uint32_t* owner, uint32_t kuni)
 {
     if (LOCAL)
     {
@@ -1185,16 +1287,16 @@ __global__ __launch_bounds__(256) void k_level_rec(LevelsIn g, const uint64_t* _
         if ((uint64_t)c * 64 >= n) return;
         const uint64_t T = (uint64_t)c * 64 + lane;
         const bool on = T < n;
-        const uint64_t o0 = on ? occ_off[T] : 0, o1 = on ? occ_off[T + 1] : 0;
+        const uint64_t o0 = !on ? 0 : (kuni ? T * kuni : occ_off[T]);
+        const uint64_t o1 = !on ? 0 : (kuni ? o0 + kuni : occ_off[T + 1]);
         const uint32_t dp = (on && dirp) ? dirp[T] : 0u;
         const uint32_t nk = (uint32_t)(o1 - o0);
         uint4 r4[4], q4[4];
 #pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) r4[i] = i < nk ? rec[o0 + i] : make_uint4(0, 0, 0, 0);
+#pragma unroll
         for (uint32_t i = 0; i < 4; ++i)
-        {
-            r4[i] = i < nk ? rec[o0 + i] : make_uint4(0, 0, 0, 0);
-            q4[i] = i < nk ? rec2[o0 + i] : make_uint4(0, 0, 0, 0);
-        }
+            q4[i] = (i < nk && r4[i].x > 3 && !(r4[i].x & REC_OVF)) ? rec2[o0 + i] : make_uint4(0, 0, 0, 0);
         // direct deps: one (its rank in dirp), or several (read here)
         uint64_t d0 = 0, d1 = 0;
         const bool dmany = (dp & DIRP_MANY) != 0;
@@ -1418,7 +1520,7 @@ using DBuf = DevBuf;
 
 struct LevelsWork {
     DBuf ka, kb, va, vb, hist, off, bsum, ord, rank, kcnt, occ_off, indeg, outdeg, succ_off, cursor, succ,
-        level, front0, front1, cnt, ctl, rec, rec2, pool, pcnt, dirp;
+        level, front0, front1, cnt, ctl, rec, rec2, pool, pcnt, dirp, wpart;
     LevelsCtl* h_ctl = nullptr;         // pinned
     struct PackCnt* h_pcnt = nullptr;   // pinned
     uint64_t* h_u64 = nullptr;          // pinned, 4 words
@@ -1521,6 +1623,7 @@ static PackPlan pack_plan(const LevelsCtl& h, uint64_t n, uint64_t n_occ)
     const uint32_t b0 = (uint32_t)__builtin_popcountll(c.m_node), b1 = (uint32_t)__builtin_popcountll(c.m_lo),
                    b2 = (uint32_t)__builtin_popcountll(c.m_hi), bk = (uint32_t)__builtin_popcountll(c.m_key);
     if (c.rb + b0 + b1 + b2 > 64 || bk + c.rb + 3 + c.jb > 64) return p;
+    c.kuni = h.maxk == ~h.mink_inv ? h.maxk : 0u;
     c.s_lo = c.rb + b0;
     c.s_hi = c.s_lo + b1;
     c.ks = c.rb + 3 + c.jb;
@@ -1562,6 +1665,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     const uint64_t cap = std::max(n, n_occ);
     const uint64_t hist_n = radix_hist_entries(cap);
     LV_ALLOC(w->ctl, sizeof(LevelsCtl));
+    LV_ALLOC(w->wpart, sizeof(WordsPart) * RED_BLOCKS);
     LV_ALLOC(w->ka, 8 * cap);
     LV_ALLOC(w->kb, 8 * cap);
     LV_ALLOC(w->va, 4 * cap);
@@ -1602,7 +1706,11 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     LV_CHK(hipMemsetAsync(cnt, 0, 4 * (n + 2 + STEP_CHUNK), st));
 
     // ---- 1. exec ranking: LSD over node, then lowHlc|flags, then msb
-    k_exec_words<<<std::min(blocks_for(n, 256), RED_BLOCKS), 256, 0, st>>>(g, ka, va, ctl, n_occ);
+    {
+        const unsigned wb = std::min(blocks_for(std::max(n, n_occ / 4), 256), RED_BLOCKS);
+        k_exec_words<<<wb, 256, 0, st>>>(g, ka, va, w->wpart.as<WordsPart>(), n_occ);
+        k_exec_words_reduce<<<1, 256, 0, st>>>(w->wpart.as<WordsPart>(), wb, ctl);
+    }
     LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
     LV_CHK(hipStreamSynchronize(st));
     {
@@ -1819,7 +1927,7 @@ static int run_levels_packed(LevelsWork* w, const LevelsIn& g, const PackPlan& p
     uint64_t* otmp = sorted;
     if (n_occ)
     {
-        k_occ_pack<<<std::min(blocks_for(n, 256), 4096u), 256, 0, st>>>(g, c, order, occ_off, occ);
+        k_occ_pack<<<std::min(blocks_for(c.kuni ? n_occ : n, 256), 8192u), 256, 0, st>>>(g, c, order, occ_off, occ, n_occ);
         LV_CHK(radix_sort_keys(occ, otmp, n_occ, (int)c.ks, (int)pp.key_bits, hist, off, bsum, st, &occ));
     }
     const PullCfg pc = pull_cfg(n, true);
@@ -1835,10 +1943,10 @@ static int run_levels_packed(LevelsWork* w, const LevelsIn& g, const PackPlan& p
         const uint64_t pool_cap = shard_cap * NSHARD;
         if (pc.local)
             k_level_rec<true><<<pc.grid, pc.threads, 0, st>>>(g, occ_off, rec, rec2, pool, pool_cap, dirp, rank, level, cnt, cnt + 1,
-                                                              pc.budget, pc.naps, cnt + 3);
+                                                              pc.budget, pc.naps, cnt + 3, c.kuni);
         else
             k_level_rec<false><<<pc.grid, pc.threads, 0, st>>>(g, occ_off, rec, rec2, pool, pool_cap, dirp, rank, level, cnt,
-                                                               cnt + 1, pc.budget, pc.naps, nullptr);
+                                                               cnt + 1, pc.budget, pc.naps, nullptr, c.kuni);
         LV_CHK(hipGetLastError());
         out->n_launch = 1;
         k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);
