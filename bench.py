@@ -1306,8 +1306,11 @@ def bench_deps(args, rank, world, local, dev):
         store.deps_batch_stats(w.queries)
         host_ms = 1000.0 * (time.perf_counter() - t0)
         out["host_api"] = {"ms_per_batch": into_ms, "pairs_per_s": w.queries.n_probes / (into_ms / 1000.0),
-                           "path": "ad_deps_batch_into (pinned caller-owned outputs, 4 slices, copy-out overlapped), "
-                                   "median of 3",
+                           "path": "ad_deps_batch_into (pinned caller-owned outputs; slices of 128k+ requests packed "
+                                   "into pinned staging by the host pool and sent by SDMA while a kernel writes the "
+                                   "previous slice's results over PCIe; keyDeps keys / k2t cross as u8 indices / u16 "
+                                   "and are rebuilt by host threads), median of 3; link peaks on the box: "
+                                   "scripts/mb_pcie.hip, scripts/mb_pcie2.hip (DESIGN.md section 7)",
                            "ad_deps_batch_ms": host_ms}
         # the device result of the same batch (the host-API call above reused the ctx buffers),
         # read back for the baseline's parity check

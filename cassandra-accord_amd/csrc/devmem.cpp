@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstdint>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -44,28 +46,92 @@ Registry& reg()
 // this thread's pinned staging: two chunks, each with the event of its last device use
 constexpr size_t STAGE = 8 << 20;
 
-// host copy between a staging chunk and pageable memory, split over threads for a full chunk (one
-// thread copies ~10 GB/s: the host side, not PCIe, bounds a staged transfer)
+// ---- host worker pool (devmem.hpp): jobs queue up; a worker takes the next task of the oldest job
+// that has any left, the calling thread works on its own job until every task of it is claimed, then
+// waits for the ones still running. Jobs of several threads run side by side (the host API's staging of
+// slice j + 1 beside the output expansion of slice j - 1); a task may start a job of its own.
+struct PoolJob {
+    const std::function<void(size_t)>* f;
+    size_t n;
+    std::atomic<size_t> next{0};
+    size_t done = 0;                       // under HostPool::mu: tasks finished
+    unsigned users = 0;                    // under HostPool::mu: workers holding the job
+    std::condition_variable cv;
+};
+
+struct HostPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<PoolJob*> jobs;            // jobs with tasks left to claim
+    unsigned workers = 0;
+    // claim a task of j (false: none left); called under no lock
+    static bool run_one(PoolJob* j)
+    {
+        const size_t i = j->next.fetch_add(1);
+        if (i >= j->n) return false;
+        (*j->f)(i);
+        return true;
+    }
+    void finish(PoolJob* j, size_t k)
+    {
+        std::lock_guard<std::mutex> g(mu);
+        j->done += k;
+        --j->users;
+        if (j->done == j->n && j->users == 0) j->cv.notify_all();
+    }
+    void start(unsigned w)
+    {
+        workers = w;
+        for (unsigned i = 0; i < w; ++i)
+            std::thread([this] {
+                while (true)
+                {
+                    PoolJob* j = nullptr;
+                    {
+                        std::unique_lock<std::mutex> g(mu);
+                        cv.wait(g, [&] {
+                            while (!jobs.empty() && jobs.front()->next.load() >= jobs.front()->n) jobs.erase(jobs.begin());
+                            return !jobs.empty();
+                        });
+                        j = jobs.front();
+                        ++j->users;
+                    }
+                    size_t k = 0;
+                    while (run_one(j)) ++k;
+                    finish(j, k);
+                }
+            }).detach();
+    }
+};
+
+HostPool& host_pool()
+{
+    static HostPool* p = [] {
+        auto* hp = new HostPool();          // never destroyed: workers may outlive static destruction
+        unsigned n = std::max(1u, std::thread::hardware_concurrency());
+        if (const char* e = getenv("OMP_NUM_THREADS")) n = (unsigned)std::max(1, atoi(e));
+        hp->start(std::min(n, 16u) - 1);
+        return hp;
+    }();
+    return *p;
+}
+
+// host copy between a staging chunk and pageable memory, split over the worker pool for a full chunk
+// (one thread copies ~10 GB/s: the host side, not PCIe, bounds a staged transfer)
 void stage_copy(void* dst, const void* src, size_t n)
 {
     constexpr size_t PART = 1 << 20;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t parts = std::min<size_t>({n / PART, 8, (size_t)hw});
+    const size_t parts = std::min<size_t>(n / PART, 16);
     if (parts < 2)
     {
         memcpy(dst, src, n);
         return;
     }
     const size_t per = (n / parts + 63) & ~size_t(63);
-    std::vector<std::thread> th;
-    th.reserve(parts - 1);
-    for (size_t i = 1; i < parts; ++i)
-    {
+    host_parallel(parts, [&](size_t i) {
         const size_t a = i * per, b = std::min(n, a + per);
-        if (a < b) th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, b - a); });
-    }
-    memcpy(dst, src, std::min(n, per));
-    for (auto& t : th) t.join();
+        if (a < b) memcpy((char*)dst + a, (const char*)src + a, b - a);
+    });
 }
 struct Staging {
     void* buf[2] = {nullptr, nullptr};
@@ -356,5 +422,38 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st)
     stage_copy((char*)dst + prev_off, S.buf[k], prev_n);
     return hipSuccess;
 }
+
+void host_parallel(size_t n, const std::function<void(size_t)>& f)
+{
+    if (n == 0) return;
+    HostPool& P = host_pool();
+    if (n == 1 || P.workers == 0)
+    {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    PoolJob j;
+    j.f = &f;
+    j.n = n;
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        P.jobs.push_back(&j);
+    }
+    P.cv.notify_all();
+    size_t k = 0;
+    while (HostPool::run_one(&j)) ++k;
+    std::unique_lock<std::mutex> g(P.mu);
+    j.done += k;
+    // every task is claimed: the job leaves the queue (a worker may have dropped it already)
+    for (size_t i = 0; i < P.jobs.size(); ++i)
+        if (P.jobs[i] == &j)
+        {
+            P.jobs.erase(P.jobs.begin() + i);
+            break;
+        }
+    j.cv.wait(g, [&] { return j.done == j.n && j.users == 0; });
+}
+
+unsigned host_threads() { return host_pool().workers + 1; }
 
 }  // namespace adx

@@ -2332,6 +2332,119 @@ hipError_t run_add_bases(uint64_t* off, uint64_t n1, const uint64_t* base, hipSt
     return hipGetLastError();
 }
 
+// Copy-out of a slice of ad_deps_batch_into straight into the caller's pinned host arrays (their
+// device-mapped addresses): the CUs' stores cross PCIe, so the copy-out runs beside the next slice's
+// SDMA H2D (measured on the box, scripts/mb_pcie2.hip: kernel D2H 54 GB/s; with an SDMA H2D beside it
+// 84 GB/s in all, against 57 GB/s in all for SDMA copies both ways). Offsets segments get the slice's
+// base added on the way.
+__global__ __launch_bounds__(256) void k_copy_out(OutSegs g)
+{
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint32_t k = 0; k < g.n; ++k)
+    {
+        const OutSeg sg = g.s[k];
+        const uintptr_t al = (uintptr_t)sg.src | (uintptr_t)sg.dst | (uintptr_t)sg.bytes;
+        if (sg.mode == 1)
+        {
+            const uint64_t* a = (const uint64_t*)sg.src;
+            uint64_t* d = (uint64_t*)sg.dst;
+            for (uint64_t i = tid; i < sg.bytes / 8; i += stride) d[i] = a[i] + sg.add;
+        }
+        else if (sg.mode == 2)
+        {
+            // u32 -> u16, two per lane when aligned
+            const uint32_t* a = (const uint32_t*)sg.src;
+            uint16_t* d = (uint16_t*)sg.dst;
+            const uint64_t m = sg.bytes / 4;
+            if ((((uintptr_t)a | (uintptr_t)d) & 7) == 0)
+            {
+                for (uint64_t i = tid; 2 * i + 1 < m; i += stride)
+                {
+                    const uint2 v = ((const uint2*)a)[i];
+                    ((uint32_t*)d)[i] = (v.x & 0xFFFFu) | (v.y << 16);
+                }
+                if (tid == 0 && (m & 1)) d[m - 1] = (uint16_t)a[m - 1];
+            }
+            else
+                for (uint64_t i = tid; i < m; i += stride) d[i] = (uint16_t)a[i];
+        }
+        else if ((al & 15) == 0)
+        {
+            const uint4* a = (const uint4*)sg.src;
+            uint4* d = (uint4*)sg.dst;
+            for (uint64_t i = tid; i < sg.bytes / 16; i += stride) d[i] = a[i];
+        }
+        else if ((al & 7) == 0)
+        {
+            const uint64_t* a = (const uint64_t*)sg.src;
+            uint64_t* d = (uint64_t*)sg.dst;
+            for (uint64_t i = tid; i < sg.bytes / 8; i += stride) d[i] = a[i];
+        }
+        else if ((al & 3) == 0)
+        {
+            const uint32_t* a = (const uint32_t*)sg.src;
+            uint32_t* d = (uint32_t*)sg.dst;
+            for (uint64_t i = tid; i < sg.bytes / 4; i += stride) d[i] = a[i];
+        }
+        else
+        {
+            const uint8_t* a = (const uint8_t*)sg.src;
+            uint8_t* d = (uint8_t*)sg.dst;
+            for (uint64_t i = tid; i < sg.bytes; i += stride) d[i] = a[i];
+        }
+    }
+}
+
+// per request: its keyDeps keys (ascending, a subset of its query keys, ascending) as indices into the
+// query keys; the u16 fit of its k2t segment and unique txns. off: the slice's 9 offset rows (map 0:
+// rows 0 keys, 1 txns, 2 k2t), n + 1 entries each.
+__global__ __launch_bounds__(256) void k_key_index(uint64_t n, const uint64_t* __restrict__ q_key_off,
+                                                   const int64_t* __restrict__ q_keys, const uint64_t* __restrict__ off,
+                                                   const int64_t* __restrict__ o_keys, uint8_t* __restrict__ idx,
+                                                   uint32_t* flag)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t f = 0;
+    if (i < n)
+    {
+        const uint64_t n1 = n + 1;
+        const uint64_t qa = q_key_off[i], qb = q_key_off[i + 1];
+        uint64_t q = qa;
+        for (uint64_t k = off[i]; k < off[i + 1]; ++k)
+        {
+            const int64_t key = o_keys[k];
+            while (q < qb && q_keys[q] < key) ++q;
+            if (q >= qb || q_keys[q] != key || q - qa > 255)
+            {
+                f |= 1u;
+                break;
+            }
+            idx[k] = (uint8_t)(q - qa);
+        }
+        if (off[2 * n1 + i + 1] - off[2 * n1 + i] > 65535 || off[n1 + i + 1] - off[n1 + i] > 65535) f |= 2u;
+    }
+    f = (ballot((f & 1u) != 0) ? 1u : 0u) | (ballot((f & 2u) != 0) ? 2u : 0u);
+    if (lane_id() == 0 && f) atomicOr(flag, f);
+}
+
+hipError_t run_key_index(uint64_t n, const uint64_t* q_key_off, const int64_t* q_keys, const uint64_t* off,
+                         const int64_t* o_keys, uint8_t* idx, uint32_t* flag, hipStream_t st)
+{
+    hipError_t e = hipMemsetAsync(flag, 0, 4, st);
+    if (e != hipSuccess || !n) return e;
+    k_key_index<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, q_key_off, q_keys, off, o_keys, idx, flag);
+    return hipGetLastError();
+}
+
+hipError_t run_copy_out(const OutSegs& g, hipStream_t st)
+{
+    if (!g.n) return hipSuccess;
+    unsigned blocks = 64;       // 64 blocks fill PCIe (6.5-6.8 ms per config-2 batch against 6.7-7.7 at 256); the CUs stay with the resolve
+    if (const char* e = getenv("AD_COPY_BLOCKS")) blocks = (unsigned)std::max(1, std::min(4096, atoi(e)));
+    k_copy_out<<<blocks, 256, 0, st>>>(g);
+    return hipGetLastError();
+}
+
 // ---- RecoveryView of a live store (BeginRecovery.java:329-380 over CommandsForKey.mapReduceFull
 // :809-908): built from the per-entry device state after ad_cfk_update / ad_cfk_prune ---------------
 __global__ __launch_bounds__(256) void k_rv_entries(RvDevIn in, uint4* ent, uint32_t* cnt, uint32_t* err)

@@ -161,6 +161,26 @@ hipError_t run_offsets(const BatchBufs& b, hipStream_t st);
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st);
 // off: 9 arrays of n1 offsets back to back; array a += base[a] (a slice's offsets made relative to its batch)
 hipError_t run_add_bases(uint64_t* off, uint64_t n1, const uint64_t* base, hipStream_t st);
+// ad_deps_batch_into's copy-out: up to OUT_SEGS device -> host-mapped segments in one launch
+constexpr int OUT_SEGS = 18;
+struct OutSeg {
+    const void* src;
+    void* dst;                 // device-mapped address of pinned host memory
+    uint64_t bytes;            // of the source
+    uint64_t add;              // mode 1: every u64 word gets `add`
+    uint32_t mode;             // 0 copy, 1 u64 + add, 2 u32 -> u16 (the wire form of k2t)
+    uint32_t pad;
+};
+// the wire form of a slice's keyDeps (ad_deps_batch_into): each output key as its index among the
+// request's query keys (u8), and whether every request's k2t segment and unique-txn count fit u16
+// (flag[0] bit 0: a key not found or past index 255; bit 1: a k2t value past 65535)
+hipError_t run_key_index(uint64_t n, const uint64_t* q_key_off, const int64_t* q_keys, const uint64_t* off,
+                         const int64_t* o_keys, uint8_t* idx, uint32_t* flag, hipStream_t st);
+struct OutSegs {
+    OutSeg s[OUT_SEGS];
+    uint32_t n;
+};
+hipError_t run_copy_out(const OutSegs& g, hipStream_t st);
 hipError_t run_pack(const BatchBufs& b, hipStream_t st);
 // offsets of the 9 size arrays + totals (+ the packed arrays when `copy`): tile sums, one-block scan
 // of the tile sums, then a streaming per-tile scan + pack; no host round trip between resolve and pack

@@ -317,11 +317,15 @@ int ad_debug_guard_check(char* buf, uint64_t n);
  * keys / txns / k2t with capacities cap[3 m + {0, 1, 2}] (elements); ideally pinned
  * (ad_host_alloc, or ad_host_register), so that every copy is a DMA straight into them (pageable arrays
  * are filled through the library's staging, synchronously). Same results as ad_deps_batch. The batch is resolved
- * in `slices` slices of requests (0: one per 128k requests, at most 4; SEQUENTIAL batches run whole):
- * slice j's result is copied out on a second stream while slice j + 1 is staged and resolved into a
- * second result bank. need[9] receives the sizes the batch needed; when a capacity was too small the
- * call returns AD_E_SPACE (the arrays' contents are then unspecified) and can be repeated with larger
- * arrays. out->stats sums the slices' device stats. */
+ * in `slices` slices of requests (0: one per 128k requests, at most 8 for key-only SNAPSHOT batches and
+ * 4 otherwise; SEQUENTIAL batches run whole): slice j's result is copied out while slice j + 1 is staged
+ * and resolved into a second result bank. Key-only SNAPSHOT batches: the library's host threads pack
+ * each slice's inputs into pinned staging (checking the keys in the same pass) while the previous slice
+ * resolves, and a kernel writes the results straight into pinned output arrays over PCIe, beside the
+ * next slice's host-to-device copy. need[9] receives the sizes the batch needed; when a capacity was too
+ * small the call returns AD_E_SPACE and can be repeated with larger arrays. On any error return the
+ * output arrays' contents are unspecified (slices before the failing one may have been written).
+ * out->stats sums the slices' device stats. */
 int ad_deps_batch_into(ad_ctx* ctx, const ad_query_soa* q, uint32_t flags, ad_deps_result* out, const uint64_t* cap /*[9]*/,
                        uint64_t* need /*[9]*/, uint32_t slices);
 

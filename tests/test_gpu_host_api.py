@@ -93,6 +93,13 @@ def test_into_empty_batch_and_bad_keys():
         with pytest.raises(native.AccordDepsError) as ei:
             st.deps_batch_into(bad, pin=False)
         assert ei.value.code == A.AD_E_INVAL and ("request %d" % i) in str(ei.value)
+        # key_off not monotone (in the last slice of a sliced call): AD_E_INVAL naming the request
+        bad = q.take(np.arange(len(q)))
+        j = len(bad) - 2
+        bad.key_off[j + 1] = bad.key_off[j] - 1 if bad.key_off[j] > 0 else bad.key_off[j + 2] + 1
+        with pytest.raises(native.AccordDepsError) as ei:
+            st.deps_batch_into(bad, slices=3)
+        assert ei.value.code == A.AD_E_INVAL
     finally:
         st.close()
 
