@@ -2089,10 +2089,15 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                     HIPCHK(c, run_resolve_lean(c->ds, b, 2, rpw1, false, st));
                     if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 }
-                BatchBufs b2 = b;
-                b2.req_list = b.deferred2;
-                b2.req_count = &b.ctl->n_deferred2;
-                HIPCHK(c, run_resolve(c->ds, b2, st));
+                if (getenv("AD_DEFER_SPLIT"))
+                    HIPCHK(c, run_defer_append(b, st));
+                else
+                {
+                    BatchBufs b2 = b;
+                    b2.req_list = b.deferred2;
+                    b2.req_count = &b.ctl->n_deferred2;
+                    HIPCHK(c, run_resolve(c->ds, b2, st));
+                }
             }
             else
                 HIPCHK(c, run_resolve(c->ds, b, st));

@@ -238,6 +238,7 @@ hipError_t run_preaccept(const PreacceptArgs& a, hipStream_t st);
 hipError_t run_preaccept_key_values(const DevRangeMap& mc, const DevRangeMap& rb, const int64_t* keys, uint64_t n_keys,
                                     PaValue* key_val, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
+hipError_t run_defer_append(const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
                             const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,

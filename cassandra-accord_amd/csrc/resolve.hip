@@ -1007,6 +1007,23 @@ hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
     return hipGetLastError();
 }
 
+// the lean passes' deferrals straight to the split kernels' list (AD_DEFER_SPLIT: a measurement switch)
+__global__ void k_defer_append(BatchBufs b)
+{
+    const uint64_t nd = b.ctl->n_deferred2;
+    const uint64_t base = b.ctl->n_deferred;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += (uint64_t)gridDim.x * blockDim.x)
+        b.deferred[base + i] = b.deferred2[i];
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&b.ctl->n_deferred, (unsigned long long)nd);
+}
+
+hipError_t run_defer_append(const BatchBufs& b, hipStream_t st)
+{
+    k_defer_append<<<1, 1024, 0, st>>>(b);
+    return hipGetLastError();
+}
+
 // ---- deferred requests -> sub-batch for the split kernels, and back -------------------------
 __global__ void k_defer_counts(BatchBufs b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt)
 {
