@@ -560,8 +560,12 @@ __device__ __forceinline__ void block_or_to(unsigned long long* dst, uint64_t v,
 // w0/idx null: the diffs only. Also the occurrence keys' diff (n_occ keys) and the most / fewest keys
 // of one txn, per block into part[blockIdx.x].
 __global__ __launch_bounds__(256) void k_exec_words(LevelsIn g, uint64_t* __restrict__ w0, uint32_t* __restrict__ idx,
-                                                    WordsPart* __restrict__ part, uint64_t n_occ)
+                                                    WordsPart* __restrict__ part)
 {
+    // occurrences: key_off[n] read here, so the host learns it with the diffs in one round trip (a value
+    // past 2^40 is refused by the host before anything reads the keys past the first pass)
+    const uint64_t n_occ_raw = g.key_off[g.n];
+    const uint64_t n_occ = n_occ_raw > (1ull << 40) ? 0 : n_occ_raw;
     __shared__ uint64_t red[4][6];
     uint64_t d0 = 0, d1 = 0, d2 = 0, dk = 0;
     uint32_t mk = 0, mi = 0;
@@ -1651,9 +1655,22 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     for (auto& e : w->ev)
         if (!e) LV_CHK(timing_event(&e));
 
-    // sizes: occurrences = key_off[n] (key_off[0] must be 0)
+    // one round trip: the occurrence count (key_off[n]; key_off[0] must be 0) and the exec words' diffs,
+    // key diff and key-count range (k_exec_words reads key_off[n] itself)
+    LV_ALLOC(w->ctl, sizeof(LevelsCtl));
+    LV_ALLOC(w->wpart, sizeof(WordsPart) * RED_BLOCKS);
+    LV_ALLOC(w->cnt, 4 * (n + 2 + STEP_CHUNK));
+    LevelsCtl* ctl = w->ctl.as<LevelsCtl>();
+    uint32_t* cnt = w->cnt.as<uint32_t>();
+    LV_CHK(hipEventRecord(w->ev[0], st));
+    LV_CHK(hipMemsetAsync(ctl, 0, sizeof(LevelsCtl), st));
+    LV_CHK(hipMemsetAsync(cnt, 0, 4 * (n + 2 + STEP_CHUNK), st));
+    const unsigned wb = std::min(blocks_for(n, 64), RED_BLOCKS);
+    k_exec_words<<<wb, 256, 0, st>>>(g, nullptr, nullptr, w->wpart.as<WordsPart>());
+    k_exec_words_reduce<<<1, 256, 0, st>>>(w->wpart.as<WordsPart>(), wb, ctl);
     LV_CHK(d2h(&w->h_u64[0], g.key_off, 8, st));
     LV_CHK(d2h(&w->h_u64[1], g.key_off + n, 8, st));
+    LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
     LV_CHK(hipStreamSynchronize(st));
     if (w->h_u64[0] != 0 || w->h_u64[1] > (1ull << 40))
     {
@@ -1664,8 +1681,6 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     out->n_occ = n_occ;
     const uint64_t cap = std::max(n, n_occ);
     const uint64_t hist_n = radix_hist_entries(cap);
-    LV_ALLOC(w->ctl, sizeof(LevelsCtl));
-    LV_ALLOC(w->wpart, sizeof(WordsPart) * RED_BLOCKS);
     LV_ALLOC(w->ka, 8 * cap);
     LV_ALLOC(w->kb, 8 * cap);
     LV_ALLOC(w->va, 4 * cap);
@@ -1677,15 +1692,18 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     LV_ALLOC(w->rank, 4 * n);
     LV_ALLOC(w->kcnt, 4 * n);
     LV_ALLOC(w->occ_off, 8 * (n + 1));
+    LV_ALLOC(w->level, 4 * n);
+    {
+        const PackPlan pp = pack_plan(*w->h_ctl, n, n_occ);
+        if (pp.ok) return run_levels_packed(w, g, pp, n_occ, level_out, st, out, err);
+    }
+    // the CSR path: its buffers, and the exec words (node word + index) its first sort starts from
     LV_ALLOC(w->indeg, 4 * n);
     LV_ALLOC(w->outdeg, 4 * n);
     LV_ALLOC(w->cursor, 4 * n);
     LV_ALLOC(w->succ_off, 8 * (n + 1));
-    LV_ALLOC(w->level, 4 * n);
     LV_ALLOC(w->front0, 4 * n);
     LV_ALLOC(w->front1, 4 * n);
-    LV_ALLOC(w->cnt, 4 * (n + 2 + STEP_CHUNK));
-    LevelsCtl* ctl = w->ctl.as<LevelsCtl>();
     uint64_t* ka = w->ka.as<uint64_t>();
     uint64_t* kb = w->kb.as<uint64_t>();
     uint32_t* va = w->va.as<uint32_t>();
@@ -1699,24 +1717,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     uint32_t* cursor = w->cursor.as<uint32_t>();
     uint64_t* succ_off = w->succ_off.as<uint64_t>();
     uint32_t* level = w->level.as<uint32_t>();
-    uint32_t* cnt = w->cnt.as<uint32_t>();
-
-    LV_CHK(hipEventRecord(w->ev[0], st));
-    LV_CHK(hipMemsetAsync(ctl, 0, sizeof(LevelsCtl), st));
-    LV_CHK(hipMemsetAsync(cnt, 0, 4 * (n + 2 + STEP_CHUNK), st));
-
-    // ---- 1. exec ranking: LSD over node, then lowHlc|flags, then msb
-    {
-        const unsigned wb = std::min(blocks_for(std::max(n, n_occ / 4), 256), RED_BLOCKS);
-        k_exec_words<<<wb, 256, 0, st>>>(g, ka, va, w->wpart.as<WordsPart>(), n_occ);
-        k_exec_words_reduce<<<1, 256, 0, st>>>(w->wpart.as<WordsPart>(), wb, ctl);
-    }
-    LV_CHK(d2h(w->h_ctl, ctl, sizeof(LevelsCtl), st));
-    LV_CHK(hipStreamSynchronize(st));
-    {
-        const PackPlan pp = pack_plan(*w->h_ctl, n, n_occ);
-        if (pp.ok) return run_levels_packed(w, g, pp, n_occ, level_out, st, out, err);
-    }
+    k_exec_words<<<wb, 256, 0, st>>>(g, ka, va, w->wpart.as<WordsPart>());
     LV_CHK(hipMemsetAsync(indeg, 0, 4 * n, st));
     LV_CHK(hipMemsetAsync(outdeg, 0, 4 * n, st));
     LV_CHK(hipMemsetAsync(cursor, 0, 4 * n, st));
