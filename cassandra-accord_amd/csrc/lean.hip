@@ -307,23 +307,35 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
     };
     // deferrals are gathered in a per-wave LDS buffer and appended to the out list in exact-size
     // blocks (one atomic per block, no holes)
-    __shared__ uint32_t dbuf_all[LEAN_WAVES][DEFER_CHUNK];
-    uint32_t* dbuf = dbuf_all[threadIdx.x >> 6];
-    uint32_t dn = 0;            // wave-uniform fill of dbuf
-    auto dflush = [&]() {
-        if (!dn) return;
+    // Pass 1 keeps two: requests pass 2 can serve (more raw emissions than pass 1's lanes, within pass
+    // 2's) go to D1, the rest -- a key needing the tree, a record the lean path cannot take, more raw
+    // emissions than pass 2 takes -- straight to D2, the general kernel's list (pass 2 would only defer
+    // them again: 99k late PreAccepts of the request mix cost pass 2 0.12 ms for nothing)
+    constexpr int NBUF = PASS == 1 ? 2 : 1;
+    __shared__ uint32_t dbuf_all[LEAN_WAVES][NBUF][DEFER_CHUNK];
+    uint32_t* dbuf = dbuf_all[threadIdx.x >> 6][0];
+    uint32_t* hbuf = dbuf_all[threadIdx.x >> 6][NBUF - 1];
+    uint32_t dn = 0, hn = 0;    // wave-uniform fills of dbuf (-> lists().out) and hbuf (pass 1: -> D2)
+    auto flush_to = [&](uint32_t* buf, uint32_t& cnt, bool to_d2) {
+        if (!cnt) return;
         unsigned long long base = 0;
         if (lane_id() == 0)
         {
             const LeanLists io = lists();
-            base = atomicAdd(io.out_count, (unsigned long long)dn);
-            atomicAdd(io.out_real, (unsigned long long)dn);
+            unsigned long long* oc = to_d2 ? &b.ctl->n_deferred2 : io.out_count;
+            unsigned long long* orl = to_d2 ? &b.ctl->n_real2 : io.out_real;
+            base = atomicAdd(oc, (unsigned long long)cnt);
+            atomicAdd(orl, (unsigned long long)cnt);
         }
         base = uniform64(base);
         wave_lds_sync();
-        if (lane_id() < dn) lists().out[base + lane_id()] = dbuf[lane_id()];
+        if (lane_id() < cnt) (to_d2 ? b.deferred2 : lists().out)[base + lane_id()] = buf[lane_id()];
         wave_lds_sync();
-        dn = 0;
+        cnt = 0;
+    };
+    auto dflush = [&]() {
+        flush_to(dbuf, dn, false);
+        if (PASS == 1) flush_to(hbuf, hn, true);
     };
 
     // ---- software pipeline over the wave's items it, it + nw, ... (RPW requests each). Per
@@ -601,15 +613,31 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         const uint32_t rstart = rinc - rn;
         const uint32_t TR = RNG ? seg_lane(rinc, 7u) : 0u;
         constexpr bool CAN_WIDE = WIDE && RPW == 2 && !RNG;
-        defer = defer || seg(ballot(kact && !newest)) != 0 || T > (CAN_WIDE ? 2 * LPR : LPR) || TR > LPR;
+        // raw emissions pass 2 takes: 64 (two per lane) without range commands; with them 32 after a pass 1
+        // of four requests per wave, else 64 (run_resolve_lean)
+        constexpr uint32_t P2CAP = !RNG ? 64u : (RPW == 4 ? 32u : 64u);
+        const bool hard = defer || seg(ballot(kact && !newest)) != 0 || (PASS == 1 && (T > P2CAP || TR > P2CAP));
+        defer = hard || T > (CAN_WIDE ? 2 * LPR : LPR) || TR > LPR;
         {
-            const uint64_t dm = ballot(act && defer && hl == 0);
+            const bool soft = PASS == 1 ? !hard : true;
+            const uint64_t dm = ballot(act && defer && soft && hl == 0);
             const uint32_t nd = __popcll(dm);
             if (nd)
             {
-                if (dn + nd > DEFER_CHUNK) dflush();
-                if (act && defer && hl == 0) dbuf[dn + __popcll(dm & ((1ull << lane) - 1))] = t;
+                if (dn + nd > DEFER_CHUNK) flush_to(dbuf, dn, false);
+                if (act && defer && soft && hl == 0) dbuf[dn + __popcll(dm & ((1ull << lane) - 1))] = t;
                 dn += nd;
+            }
+            if (PASS == 1)
+            {
+                const uint64_t hm = ballot(act && hard && hl == 0);
+                const uint32_t nh = __popcll(hm);
+                if (nh)
+                {
+                    if (hn + nh > DEFER_CHUNK) flush_to(hbuf, hn, true);
+                    if (act && hard && hl == 0) hbuf[hn + __popcll(hm & ((1ull << lane) - 1))] = t;
+                    hn += nh;
+                }
             }
         }
         act = act && !defer;

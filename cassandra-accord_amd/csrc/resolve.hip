@@ -968,8 +968,12 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
     // no load for ids newer than the store (fresh PreAccepts), else a search of the sampled
     // dictionary (Accepts: S is a proposed executeAt, self a txnId the store holds)
     const bool same = em == tm && ((el ^ tl) & 0xFFFFFFFFFFFF001EULL) == 0 && en == tn;
-    const uint32_t S = dict_rank_sampled(s, norm_tid(em, el, en));
-    const uint32_t self = same ? 0u : dict_rank_sampled(s, norm_tid(tm, tl, tn));
+    // both searches advance in lockstep (one chain of round trips for an Accept's two ids)
+    const NormTid ids2[2] = {norm_tid(em, el, en), norm_tid(tm, tl, tn)};
+    const bool want2[2] = {true, !same};
+    uint32_t rk2[2];
+    dict_rank_sampled_n<2>(s, ids2, want2, rk2);
+    const uint32_t S = rk2[0], self = rk2[1];
     const uint64_t np = k1 - k0;
     // lean path: at most 8 keys, a valid kind, key offsets within 32 bits
     const bool fast = kinds != 0 && np <= 8 && k1 <= 0xFFFFFFFFull;
