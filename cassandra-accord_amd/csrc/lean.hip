@@ -29,9 +29,10 @@ constexpr int LEAN_WAVES = 4;
 #define LEAN_OCC_N 5
 #endif
 constexpr int LEAN_OCC = LEAN_OCC_N;        // waves per SIMD the register budget is sized for
-// the same for the range-command kernels (RNG): 5 waves per SIMD spill a few registers
+// the same for the range-command kernels (RNG): at 5 waves per SIMD they spill 36-52 bytes per lane; at 4
+// they do not, and config 4 measured faster (round 5: pass 1 0.594 -> 0.589, pass 2 0.166 -> 0.154 ms)
 #ifndef LEAN_OCC_RNG
-#define LEAN_OCC_RNG LEAN_OCC_N
+#define LEAN_OCC_RNG 4
 #endif
 // and for the wide kernels (two emissions per lane)
 #ifndef LEAN_OCC_WIDE
