@@ -425,6 +425,9 @@ def bench_ranges(args, rank, world, local, dev):
     s = args.scale
     w = synth.config4(n_txns=int(1_000_000 * s), n_keys=int(1_000_000 * s), n_ranges=max(1, int(100_000 * s)),
                       n_hist_txns=int(1_000_000 * s), seed=0xACC0D004 + rank)
+    if args.range_frac > 0:
+        # Range-domain requests beside the key txns: with range commands in the store they take the split kernels
+        w = synth.with_range_requests(w, args.range_frac)
     store = native.DeviceCommandStore(device=local, slices=w.slices)
     store.load(w)
     qdev, keep = native.device_queries(w.queries, dev)
@@ -480,6 +483,8 @@ def bench_ranges(args, rank, world, local, dev):
                        "per timed step" % res_ms,
         "pairs_out": {A.MAP_NAMES[m]: int(stats["n_pairs"][m]) for m in range(3)},
     }
+    if w.queries.range_off is not None:
+        res["config"]["range_requests"] = int(np.count_nonzero(np.diff(w.queries.range_off.astype(np.int64))))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
     if rank == 0:
@@ -1036,6 +1041,10 @@ def main():
     ap.add_argument("--unordered-frac", type=float, default=0.0,
                     help="config 2: share of out-of-order PreAccepts (txnId inside the history's last ticks)")
     ap.add_argument("--unordered-window", type=int, default=2000, help="hlc ticks of --unordered-frac's lateness")
+    ap.add_argument("--range-frac", type=float, default=0.0,
+                    help="config 2 / 4: this share of the requests Range-domain txns over one range of 1-8 keys each "
+                         "(synth.with_range_requests): on config 2's store (no range commands) they run the lean "
+                         "passes as the keys inside their ranges; on config 4's the split kernels, beside the lean passes")
     ap.add_argument("--recovery-scan", type=int, default=3, choices=(0, 1, 2, 3), help="AD_RECOVER_* scan of --recovery")
     ap.add_argument("--exchange", action="store_true",
                     help="run the node exchange (ad_exchange over the library's RCCL communicator) even on one GPU")
@@ -1104,6 +1113,10 @@ def bench_deps(args, rank, world, local, dev):
         if world > 1 or cfg != 2:
             raise SystemExit("--accept-frac / --unordered-frac: config 2 on a single store only")
         w = synth.with_request_mix(w, args.accept_frac, args.unordered_frac, args.unordered_window)
+    if args.range_frac > 0:
+        if world > 1 or cfg != 2:
+            raise SystemExit("--range-frac: config 2 on a single store, or config 4")
+        w = synth.with_range_requests(w, args.range_frac)
     log("rank %d: config %d generated in %.1f s: %d keys, %d entries, %d of %d requests routed here, %d probes" %
         (rank, cfg, time.time() - t0, len(w.cfk.keys), w.cfk.n_entries, len(w.queries), n_total, w.queries.n_probes))
 
@@ -1317,6 +1330,8 @@ def bench_deps(args, rank, world, local, dev):
         res, _ = store.deps_batch_device(qdev, sp)
         torch.cuda.synchronize(dev)
         out["cpu_baseline"] = cpu_baseline_stores(w, args.cpu_budget, gpu_take=lambda idx: store.device_result_to_host(res, idx))
+    if w.queries.range_off is not None:
+        out["config"]["range_requests"] = int(np.count_nonzero(np.diff(w.queries.range_off.astype(np.int64))))
     if rank == 0:
         print(json.dumps(out), flush=True)
     store.close()

@@ -185,6 +185,38 @@ def config2_stream(w, n_batches, n_txns, seed=0xACC0D5EE, held_keys_only=False):
     return out
 
 
+def with_range_requests(w, frac, max_keys=8, seed=0xACC0D0A6):
+    """The workload `w` with a random `frac` of its requests turned into Range-domain txns (TxnId and
+    executeAt domain bit set, TxnId.java:154-157; kind unchanged): each gets one normalised Range
+    (keys[i] - 1, keys[i + m]] over the store's sorted keys (m + 1 CommandsForKey, m uniform in
+    [0, max_keys)), EndInclusive, in place of its keys -- the shape of a sync point or range read in a
+    replica's batch (SafeCommandStore.mapReduceActive over Ranges, SafeCommandStore.java:292)."""
+    q = w.queries
+    n = len(q)
+    rng = np.random.default_rng(seed)
+    isr = rng.random(n) < frac
+    keys_sorted = np.sort(w.cfk.keys)
+    nk = len(keys_sorted)
+    key_cnt = np.diff(q.key_off.astype(np.int64))
+    keep = np.repeat(~isr, key_cnt)
+    new_cnt = np.where(isr, 0, key_cnt)
+    key_off = np.zeros(n + 1, np.uint64)
+    key_off[1:] = np.cumsum(new_cnt)
+    ri = np.nonzero(isr)[0]
+    a = rng.integers(0, max(nk - max_keys, 1), len(ri))
+    m = rng.integers(0, max_keys, len(ri))
+    rs = keys_sorted[a] - 1
+    re_ = keys_sorted[np.minimum(a + m, nk - 1)]
+    range_off = np.zeros(n + 1, np.uint64)
+    range_off[1:] = np.cumsum(isr.astype(np.uint64))
+    dom = isr.astype(np.uint64)
+    txn = Tids(q.txn.msb, q.txn.lsb | dom, q.txn.node)
+    ex = Tids(q.exec.msb, q.exec.lsb | dom, q.exec.node)
+    w.queries = Queries(txn, ex, key_off, q.keys[keep], q.min_epoch, range_off, rs.astype(np.int64), re_.astype(np.int64))
+    w.name = w.name + "+ranges"
+    return w
+
+
 def with_request_mix(w, accept_frac=0.0, unordered_frac=0.0, unordered_window=2000, seed=0xACC0D0A5):
     """The config-2 workload `w` (history txn j has txnId hlc 1 + j) turned into a replica's mix of
     deps requests (SNAPSHOT semantics), so that the paths besides the newest-request one run:

@@ -199,11 +199,11 @@ struct ad_ctx {
     DevBuf lg_stage, lg_rec, lg_keys, lg_dummy;   // lean gather + build: staged emissions, build records, keys
     bool upd_applied = false;                  // ad_cfk_update_status: the last update batch stands
     int64_t upd_failed = -1;                   //   and the update its failure names
-    DevBuf rq_cnt, rq_off, rq_err, rq_bsum, rq_keys, rq_hi, rq_kind;   // their expansion into probes
+    DevBuf rq_cnt, rq_off, rq_err, rq_bsum, rq_keys, rq_hi, rq_kind, rq_list;   // their expansion into probes
     struct SplitBufs {       // per-request / per-probe arrays of the split kernels
         DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
     } split, sub;
-    DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt;   // deferred sub-batch inputs
+    DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt, s_khi, s_kind;   // deferred sub-batch inputs
     DevBuf p_slot;                             // lean passes: per probe its KeyLine (k_lean_slots)
     DevBuf arena, rarena;
     DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, q_rec, big;
@@ -224,6 +224,7 @@ struct ad_ctx {
     hipEvent_t ev_sp0 = nullptr, ev_sp1 = nullptr;   // split path on the fused kernels' deferrals
     hipEvent_t ev_done = nullptr;      // end of a batch's work (default flags: the host reads what it copied)
     BatchCtl* h_ctl = nullptr;         // pinned mirror of the batch control block
+    uint64_t* h_small = nullptr;       // pinned words the batch prologue reads back (key / range totals)
     // ad_deps_batch_into: a second result bank (offsets + packed arrays) so that one slice of a batch is
     // copied out while the next resolves, the copy-out stream and its events
     DevBuf off_b, o_keys_b[3], o_txns_b[3], o_k2t_b[3];
@@ -1838,8 +1839,10 @@ static uint32_t lean_rpw1(uint64_t n, uint64_t np, bool ranges)
     if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 8 ? 8u : (atoi(e) == 4 ? 4u : 2u);
     // 8 requests per wave (AD_LEAN_RPW=8) stays opt-in while the late-round-3 device faults are open.
     // With range commands up to 4 keys per request on average: four per wave (config 4: pass 1 0.90 ->
-    // 0.58 ms, its deferrals -- above 16 raw emissions -- two per wave in pass 2)
-    return np <= (ranges ? 4 : 3) * n ? 4u : 2u;
+    // 0.58 ms, its deferrals -- above 16 raw emissions -- two per wave in pass 2); up to 4.5, so that a few
+    // Range-domain requests (their expanded probes; the split kernels resolve them) do not tip a 4-key batch
+    // over (config 4 with 1 % of them: pass 1 0.93 ms at two per wave)
+    return 2 * np <= (ranges ? 9 : 6) * n ? 4u : 2u;
 }
 
 // Lean pass 1 wide or narrow (rpw 2, no range commands; results identical either way). The wide kernel
@@ -1898,56 +1901,63 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
 {
     const uint64_t n = q->n_txns;
     uint64_t np = 0;
-    if (n && n_keys_given)
-        np = q->n_keys;
-    else if (n)
-    {
-        HIPCHK(c, d2h(&np, q->key_off + n, sizeof(uint64_t), st));
-        HIPCHK(c, hipStreamSynchronize(st));
-    }
     // Range-domain requests (ad_query_soa.range_off): expanded into probes on the device -- keys inside
     // the sliced ranges, the sliced ranges, the unsliced ranges (kernels.hip k_range_count /
-    // k_range_fill) -- then resolved by the split kernels. Recovery scans take no RedundantBefore
-    // (mapReduceFull, InMemoryCommandStore.java:874-882): no unsliced-range probes
+    // k_range_fill). Recovery scans take no RedundantBefore (mapReduceFull, InMemoryCommandStore.java:874-882):
+    // no unsliced-range probes. The totals the host needs come back through pinned words, one wait each.
+    const bool ranges = n && q->range_off;
+    if (ranges && (!q->range_start || !q->range_end)) return c->fail(AD_E_INVAL, "range_off without range_start / range_end");
+    if ((n && !n_keys_given) || ranges)
+        if (!c->h_small) HIPCHK(c, hipHostMalloc((void**)&c->h_small, 64, hipHostMallocDefault));
     uint64_t nr = 0;
-    if (n && q->range_off)
+    if (n && n_keys_given)
     {
-        if (!q->range_start || !q->range_end) return c->fail(AD_E_INVAL, "range_off without range_start / range_end");
-        if (n_keys_given)
-            nr = q->n_ranges;
-        else
+        np = q->n_keys;
+        if (ranges) nr = q->n_ranges;
+    }
+    else if (n)
+    {
+        uint64_t* hs = c->h_small;
+        hs[0] = hs[1] = hs[2] = 0;
+        HIPCHK(c, hipMemcpyAsync(&hs[0], q->key_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        if (ranges)
         {
-            uint64_t ro[2] = {0, 0};
-            HIPCHK(c, d2h(&ro[0], q->range_off, sizeof(uint64_t), st));
-            HIPCHK(c, d2h(&ro[1], q->range_off + n, sizeof(uint64_t), st));
-            HIPCHK(c, hipStreamSynchronize(st));
-            nr = ro[1] - ro[0];
+            HIPCHK(c, hipMemcpyAsync(&hs[1], q->range_off, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipMemcpyAsync(&hs[2], q->range_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
         }
+        HIPCHK(c, hipStreamSynchronize(st));
+        np = hs[0];
+        nr = hs[2] - hs[1];
     }
     if (nr)
     {
         if (!ens<uint32_t>(c->rq_cnt, n) || !ens<uint64_t>(c->rq_off, n + 1) || !ens<uint32_t>(c->rq_err, 2) ||
-            !ens<uint64_t>(c->rq_bsum, (n + 1023) / 1024 + 16))
+            !ens<uint64_t>(c->rq_bsum, (n + 1023) / 1024 + 16) || !ens<uint32_t>(c->rq_list, n))
             return c->fail(AD_E_NOMEM, "range request expansion");
         HIPCHK(c, hipMemsetAsync(c->rq_err.p, 0, 8, st));
+        // rq_err[0]: the rejection flag; rq_err[1]: the Range-domain requests, listed in rq_list
         HIPCHK(c, run_range_count(c->ds, n, q->key_off, q->range_off, q->range_start, q->range_end, c->rq_cnt.as<uint32_t>(),
-                                  c->rq_err.as<uint32_t>(), recovery_scan < 0, st));
+                                  c->rq_err.as<uint32_t>(), c->rq_list.as<uint32_t>(), recovery_scan < 0, st));
         HIPCHK(c, run_scan_arrays(c->rq_cnt.as<uint32_t>(), c->rq_off.as<uint64_t>(), n, 1, c->rq_bsum.as<uint64_t>(), st));
-        uint64_t tail[2] = {0, 0};
-        HIPCHK(c, d2h(&tail[0], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), st));
-        HIPCHK(c, d2h(&tail[1], c->rq_err.p, sizeof(uint32_t), st));
+        uint64_t* hs = c->h_small;
+        HIPCHK(c, hipMemcpyAsync(&hs[3], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(&hs[4], c->rq_err.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
-        if (tail[1])
+        const uint32_t err = (uint32_t)hs[4], n_rreq = (uint32_t)(hs[4] >> 32);
+        if (err)
             return c->fail(AD_E_INVAL, "Range-domain request: keys and ranges together, or ranges not normalised "
                                        "(start < end, ascending, disjoint)");
-        np = tail[0];
+        np = hs[3];
         if (!ens<int64_t>(c->rq_keys, np) || !ens<int64_t>(c->rq_hi, np) || !ens<uint8_t>(c->rq_kind, np))
             return c->fail(AD_E_NOMEM, "range request probes");
         HIPCHK(c, run_range_fill(c->ds, n, q->key_off, q->keys, q->range_off, q->range_start, q->range_end,
                                  c->rq_off.as<uint64_t>(), c->rq_keys.as<int64_t>(), c->rq_hi.as<int64_t>(),
-                                 c->rq_kind.as<uint8_t>(), recovery_scan < 0, st));
+                                 c->rq_kind.as<uint8_t>(), c->rq_list.as<uint32_t>(), n_rreq, recovery_scan < 0, st));
     }
-    const bool split_only = c->cfg.path == 1 || recovery_scan >= 0 || nr > 0;
+    // a batch with Range-domain requests keeps the lean / general path for its key-domain requests: k_prepare
+    // marks the Range-domain ones, k_resolve hands them to the split kernels' list (resolved after the first
+    // pack pass, like any request the fused kernels cannot take)
+    const bool split_only = c->cfg.path == 1 || recovery_scan >= 0;
     // the lean kernel covers stores without redundant-before entries, elision on
     // (range commands only with their stabbing index)
     const bool lean = !split_only && np > 0 && (c->ds.n_rent == 0 || c->ds.cell_off != nullptr) && c->ds.n_rb == 0 &&
@@ -2171,18 +2181,22 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 sb.n_probes = snp;
                 if (!bind_split(c->sub, sb, nd, snp, true) || !ens<uint64_t>(c->s_tm, nd) || !ens<uint64_t>(c->s_tl, nd) ||
                     !ens<int32_t>(c->s_tn, nd) || !ens<uint64_t>(c->s_em, nd) || !ens<uint64_t>(c->s_el, nd) ||
-                    !ens<int32_t>(c->s_en, nd) || !ens<int64_t>(c->s_me, nd) || !ens<int64_t>(c->s_k, snp))
+                    !ens<int32_t>(c->s_en, nd) || !ens<int64_t>(c->s_me, nd) || !ens<int64_t>(c->s_k, snp) ||
+                    (b.p_kind && (!ens<int64_t>(c->s_khi, snp) || !ens<uint8_t>(c->s_kind, snp))))
                     return c->fail(AD_E_NOMEM, "deferred buffers");
                 uint64_t* sko = c->s_ko.as<uint64_t>();     // the scanned counts are the sub-batch key_off
                 HIPCHK(c, run_defer_gather(b, b.deferred, nd, c->s_ko.as<uint64_t>(), sb, c->s_tm.as<uint64_t>(),
                                            c->s_tl.as<uint64_t>(), c->s_tn.as<int32_t>(), c->s_em.as<uint64_t>(),
                                            c->s_el.as<uint64_t>(), c->s_en.as<int32_t>(), c->s_me.as<int64_t>(), sko,
-                                           c->s_k.as<int64_t>(), st));
+                                           c->s_k.as<int64_t>(), b.p_kind ? c->s_khi.as<int64_t>() : nullptr,
+                                           b.p_kind ? c->s_kind.as<uint8_t>() : nullptr, st));
                 sb.q_txn_msb = c->s_tm.as<uint64_t>(); sb.q_txn_lsb = c->s_tl.as<uint64_t>(); sb.q_txn_node = c->s_tn.as<int32_t>();
                 sb.q_exec_msb = c->s_em.as<uint64_t>(); sb.q_exec_lsb = c->s_el.as<uint64_t>(); sb.q_exec_node = c->s_en.as<int32_t>();
                 sb.q_min_epoch = b.q_min_epoch ? c->s_me.as<int64_t>() : nullptr;
                 sb.q_key_off = sko;
                 sb.q_keys = c->s_k.as<int64_t>();
+                sb.q_keys_hi = b.p_kind ? c->s_khi.as<int64_t>() : nullptr;
+                sb.p_kind = b.p_kind ? c->s_kind.as<uint8_t>() : nullptr;
                 if ((rc = run_split(c, sb, st))) return rc;
                 HIPCHK(c, run_defer_scatter(b, b.deferred, nd, sb.sz, sb.t_reg, st));
                 // the requests are complete now: pack (k_pack_lb skips batches with split deferrals)
@@ -2489,6 +2503,7 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->ev_sp0) (void)hipEventDestroy(c->ev_sp0);
     if (c->ev_sp1) (void)hipEventDestroy(c->ev_sp1);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+    if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_xtab) (void)hipHostFree(c->h_xtab);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     for (hipEvent_t e : c->ev_copied)

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, 
                                                      const uint64_t* __restrict__ range_off,
                                                      const int64_t* __restrict__ range_start,
                                                      const int64_t* __restrict__ range_end, uint32_t* __restrict__ cnt,
-                                                     uint32_t* err, bool with_rb)
+                                                     uint32_t* err, uint32_t* __restrict__ list, bool with_rb)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
@@ -264,6 +264,7 @@ __global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, 
         cnt[t] = (uint32_t)nk;
         return;
     }
+    list[atomicAdd(&err[1], 1u)] = (uint32_t)t;
     bool bad = nk != 0;
     const bool incl = s.start_inclusive != 0;
     uint64_t c = 0;
@@ -285,31 +286,38 @@ __global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, 
     cnt[t] = bad ? 0u : (uint32_t)min<uint64_t>(c, 0xFFFFFFFFull);
 }
 
-// one wave per request: the sliced ranges in order, their keys written lane-strided
-__global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, uint64_t n, const uint64_t* __restrict__ key_off,
-                                                    const int64_t* __restrict__ keys, const uint64_t* __restrict__ range_off,
+// a key-domain request's keys, one thread per request (its range end is never read: PK_KEY)
+__global__ __launch_bounds__(256) void k_range_fill_keys(uint64_t n, const uint64_t* __restrict__ key_off,
+                                                         const int64_t* __restrict__ keys,
+                                                         const uint64_t* __restrict__ range_off,
+                                                         const uint64_t* __restrict__ off, int64_t* __restrict__ pkeys,
+                                                         uint8_t* __restrict__ pkind)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n || range_off[t + 1] != range_off[t]) return;
+    const uint64_t k0 = key_off[t], nk = key_off[t + 1] - k0, o = off[t];
+    for (uint64_t i = 0; i < nk; ++i)
+    {
+        pkeys[o + i] = keys[k0 + i];
+        pkind[o + i] = PK_KEY;
+    }
+}
+
+// one wave per Range-domain request (list): the sliced ranges in order, their keys written lane-strided
+__global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, const uint32_t* __restrict__ list, uint32_t n_list,
+                                                    const uint64_t* __restrict__ range_off,
                                                     const int64_t* __restrict__ range_start,
                                                     const int64_t* __restrict__ range_end, const uint64_t* __restrict__ off,
                                                     int64_t* __restrict__ pkeys, int64_t* __restrict__ pkeys_hi,
                                                     uint8_t* __restrict__ pkind, bool with_rb)
 {
-    const uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (t >= n) return;
+    const uint64_t li = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (li >= n_list) return;
+    const uint64_t t = list[li];
     const uint32_t lane = lane_id();
     const uint64_t r0 = range_off[t], r1 = range_off[t + 1];
     uint64_t o = off[t];
     const uint64_t o_end = off[t + 1];
-    if (r1 == r0)
-    {
-        const uint64_t k0 = key_off[t], nk = key_off[t + 1] - k0;
-        for (uint64_t i = lane; i < nk; i += 64)
-        {
-            pkeys[o + i] = keys[k0 + i];
-            pkeys_hi[o + i] = 0;
-            pkind[o + i] = PK_KEY;
-        }
-        return;
-    }
     if (o_end == o) return;                      // rejected (k_range_count) or nothing to visit
     const bool incl = s.start_inclusive != 0;
     const uint64_t n_sl = s.n_slices ? s.n_slices : 1;
@@ -351,22 +359,23 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, uint64_t n, c
 
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
                            const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           bool with_rb, hipStream_t st)
+                           uint32_t* list, bool with_rb, hipStream_t st)
 {
     if (n)
         k_range_count<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n, key_off, range_off, range_start, range_end, cnt, err,
-                                                                   with_rb);
+                                                                   list, with_rb);
     return hipGetLastError();
 }
 
 hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
                           const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
-                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, bool with_rb,
-                          hipStream_t st)
+                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, const uint32_t* list,
+                          uint32_t n_list, bool with_rb, hipStream_t st)
 {
-    if (n)
-        k_range_fill<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(s, n, key_off, keys, range_off, range_start, range_end, off, pkeys,
-                                                              pkeys_hi, pkind, with_rb);
+    if (n) k_range_fill_keys<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, key_off, keys, range_off, off, pkeys, pkind);
+    if (n_list)
+        k_range_fill<<<(unsigned)((n_list + 3) / 4), 256, 0, st>>>(s, list, n_list, range_off, range_start, range_end, off, pkeys,
+                                                                   pkeys_hi, pkind, with_rb);
     return hipGetLastError();
 }
 

@@ -141,13 +141,15 @@ hipError_t run_rv_inv_finish(const RvDevIn& in, const uint64_t* eoff, const uint
 constexpr uint8_t PK_KEY = 0, PK_RANGE_KEY = 1, PK_RANGE = 2, PK_RANGE_RB = 3;
 // per request its probe count (cnt) and error flag (*err = 1: keys and ranges together, or ranges
 // not normalised); then, from the exclusive scan `off`, the probes
+// (err[1]: the Range-domain requests, their indices appended to `list`); then, from the exclusive scan `off`,
+// the probes: a key-domain request's keys one thread per request, a listed request's one wave each
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
                            const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           bool with_rb, hipStream_t st);
+                           uint32_t* list, bool with_rb, hipStream_t st);
 hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
                           const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
-                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, bool with_rb,
-                          hipStream_t st);
+                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, const uint32_t* list,
+                          uint32_t n_list, bool with_rb, hipStream_t st);
 
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
 hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);
@@ -195,6 +197,7 @@ constexpr uint32_t SLOT_IN_SLICE = 0x80000000u;
 constexpr uint32_t DEFER_HOLE = 0xFFFFFFFFu;      // unused slot of a wave's deferral chunk
 constexpr uint32_t DEFER_CHUNK = 64;              // deferral slots a lean wave reserves at a time
 constexpr uint32_t REC_FAST = 1u << 24;          // q_rec: lean path applies (<= 8 keys, valid kind, 32-bit key offsets)
+constexpr uint32_t REC_SPLIT = 1u << 25;         // q_rec: a Range-domain request of a mixed batch (the split kernels resolve it)
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 // pass 1 with rpw1 = 2 on a store without range commands: wide1 selects the wide kernel (requests of up to
 // 64 raw emissions) over the narrow one (up to 32; the rest to pass 2)
@@ -242,7 +245,8 @@ hipError_t run_defer_append(const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
                             const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,
-                            uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, hipStream_t st);
+                            uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, int64_t* o_khi,
+                            uint8_t* o_kind, hipStream_t st);
 hipError_t run_defer_scatter(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint32_t* sub_sz,
                              const uint64_t* sub_reg, hipStream_t st);
 

@@ -319,19 +319,32 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
     uint32_t dn = 0, hn = 0;    // wave-uniform fills of dbuf (-> lists().out) and hbuf (pass 1: -> D2)
     auto flush_to = [&](uint32_t* buf, uint32_t& cnt, bool to_d2) {
         if (!cnt) return;
-        unsigned long long base = 0;
+        wave_lds_sync();
+        const uint32_t tv = lane_id() < cnt ? buf[lane_id()] : 0u;
+        wave_lds_sync();
+        // pass 1's hard deferrals: a Range-domain request of a mixed batch (REC_SPLIT, k_prepare) goes straight to
+        // the split kernels' list; the rest to D2
+        const bool sp = to_d2 && lane_id() < cnt && (b.q_rec[tv].z & REC_SPLIT) != 0;
+        const uint64_t spm = ballot(sp);
+        const uint32_t nsp = __popcll(spm), nrest = cnt - nsp;
+        unsigned long long base = 0, sbase = 0;
         if (lane_id() == 0)
         {
             const LeanLists io = lists();
             unsigned long long* oc = to_d2 ? &b.ctl->n_deferred2 : io.out_count;
             unsigned long long* orl = to_d2 ? &b.ctl->n_real2 : io.out_real;
-            base = atomicAdd(oc, (unsigned long long)cnt);
-            atomicAdd(orl, (unsigned long long)cnt);
+            if (nrest)
+            {
+                base = atomicAdd(oc, (unsigned long long)nrest);
+                atomicAdd(orl, (unsigned long long)nrest);
+            }
+            if (nsp) sbase = atomicAdd(&b.ctl->n_deferred, (unsigned long long)nsp);
         }
         base = uniform64(base);
-        wave_lds_sync();
-        if (lane_id() < cnt) (to_d2 ? b.deferred2 : lists().out)[base + lane_id()] = buf[lane_id()];
-        wave_lds_sync();
+        sbase = uniform64(sbase);
+        const uint64_t below = (1ull << lane_id()) - 1;
+        if (sp) b.deferred[sbase + __popcll(spm & below)] = tv;
+        else if (lane_id() < cnt) (to_d2 ? b.deferred2 : lists().out)[base + __popcll(~spm & below)] = tv;
         cnt = 0;
     };
     auto dflush = [&]() {

@@ -309,6 +309,12 @@ struct FChunk {
     }
 };
 
+// a Range-domain request the split kernels must resolve (see k_prepare)
+__device__ __forceinline__ bool range_split(const DevSnapshot& s, const BatchBufs& b, uint64_t k0, uint64_t np)
+{
+    return b.p_kind && np && b.p_kind[k0] != PK_KEY && (s.n_rent || s.n_rb);
+}
+
 __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUSED_WPE))) void k_resolve(DevSnapshot s, BatchBufs b)
 {
     __shared__ FusedLds lds_all[FWAVES];
@@ -419,7 +425,9 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
         const uint64_t k0 = k0c;
         (void)k0;
         const uint32_t np = npc;
-        if (np > FMAXP)
+        // more than 8 keys, or a Range-domain request (expanded probes: sliced parts and unsliced ranges, which
+        // only the split kernels resolve): the split kernels' list
+        if (np > FMAXP || range_split(s, b, k0c, np))
         {
             if (lane == 0) b.deferred[atomicAdd(&b.ctl->n_deferred, 1ull)] = (uint32_t)t;
             break;   // next request (pipeline rotation below)
@@ -975,9 +983,16 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
     dict_rank_sampled_n<2>(s, ids2, want2, rk2);
     const uint32_t S = rk2[0], self = rk2[1];
     const uint64_t np = k1 - k0;
-    // lean path: at most 8 keys, a valid kind, key offsets within 32 bits
-    const bool fast = kinds != 0 && np <= 8 && k1 <= 0xFFFFFFFFull;
-    b.q_rec[t] = make_uint4((uint32_t)k0, S, (uint32_t)(np < 0xFFFFu ? np : 0xFFFFu) | (cls << 16) | (fast ? REC_FAST : 0u),
+    // a Range-domain request (its probes expanded by k_range_fill; the first is not a key's) on a store with range
+    // commands or redundant-before entries -- whose sliced parts (PK_RANGE) and unsliced ranges (PK_RANGE_RB) only
+    // the split kernels resolve -- leaves the lean and general kernels for the split kernels' list. On a store
+    // with neither its probes are the CommandsForKey keys inside its sliced ranges (PK_RANGE_KEY), ascending:
+    // mapReduceActive over each as for a key-domain request (InMemoryCommandStore.java:289-304), so it stays.
+    const bool rreq = range_split(s, b, k0, np);
+    // lean path: at most 8 keys, a valid kind, key offsets within 32 bits, key-domain
+    const bool fast = kinds != 0 && np <= 8 && k1 <= 0xFFFFFFFFull && !rreq;
+    b.q_rec[t] = make_uint4((uint32_t)k0, S,
+                            (uint32_t)(np < 0xFFFFu ? np : 0xFFFFu) | (cls << 16) | (fast ? REC_FAST : 0u) | (rreq ? REC_SPLIT : 0u),
                             self);
 }
 
@@ -1039,7 +1054,7 @@ __global__ void k_defer_counts(BatchBufs b, const uint32_t* deferred, uint64_t n
 
 __global__ void k_defer_gather(BatchBufs b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off, BatchBufs sub,
                                uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em, uint64_t* o_el, int32_t* o_en,
-                               int64_t* o_me, uint64_t* o_ko, int64_t* o_k)
+                               int64_t* o_me, uint64_t* o_ko, int64_t* o_k, int64_t* o_khi, uint8_t* o_kind)
 {
     const uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (i >= nd) return;
@@ -1058,6 +1073,13 @@ __global__ void k_defer_gather(BatchBufs b, const uint32_t* deferred, uint64_t n
     }
     const uint64_t s0 = b.q_key_off[t], len = b.q_key_off[t + 1] - s0, d0 = sub_off[i];
     for (uint64_t k = lane; k < len; k += 64) o_k[d0 + k] = b.q_keys[s0 + k];
+    // a batch with Range-domain requests: each probe's kind and range end (k_range_fill)
+    if (b.p_kind)
+        for (uint64_t k = lane; k < len; k += 64)
+        {
+            o_khi[d0 + k] = b.q_keys_hi[s0 + k];
+            o_kind[d0 + k] = b.p_kind[s0 + k];
+        }
 }
 
 __global__ void k_defer_scatter(BatchBufs b, const uint32_t* deferred, uint64_t nd, const uint32_t* sub_sz,
@@ -1079,11 +1101,13 @@ hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64
 
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
                             const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,
-                            uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, hipStream_t st)
+                            uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, int64_t* o_khi,
+                            uint8_t* o_kind, hipStream_t st)
 {
     if (!nd) return hipSuccess;
+    if (b.p_kind && (!o_khi || !o_kind || !b.q_keys_hi)) return hipErrorInvalidValue;
     k_defer_gather<<<(unsigned)((nd + 3) / 4), 256, 0, st>>>(b, deferred, nd, sub_off, sub, o_tm, o_tl, o_tn, o_em, o_el,
-                                                             o_en, o_me, o_ko, o_k);
+                                                             o_en, o_me, o_ko, o_k, o_khi, o_kind);
     return hipGetLastError();
 }
 

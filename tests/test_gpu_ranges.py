@@ -37,6 +37,29 @@ def test_range_requests_match_oracle(oracle, seed):
         _eq(native.resolve(w, via=via), exp, "seed %d via %s" % (seed, via))
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_range_requests_beside_lean(oracle, seed):
+    # stores the lean kernels serve (no redundant-before entries, elision on; with and without range commands):
+    # the key-domain requests of a mixed batch run the lean passes while its Range-domain requests are handed,
+    # by k_prepare's record and the general kernel, to the split kernels after the first pack pass
+    w = _w(300 + seed, n_keys=40 + 7 * seed, n_txns=240, n_hist_txns=400, range_frac=0.08 + 0.04 * (seed % 3),
+           n_redundant=0, n_range_cmds=(0 if seed % 2 else 20), with_slices=(seed % 4 == 1),
+           start_inclusive=(seed % 4 == 2))
+    assert w.queries.n_ranges > 0
+    exp = oracle.resolve(w)
+    for via in ("host", "device", "regions"):
+        _eq(native.resolve(w, via=via), exp, "seed %d via %s" % (seed, via))
+
+
+def test_range_requests_beside_lean_config2_shape(oracle):
+    # config 2's shape, scaled: Zipf keys over a 16x history, a few percent of the requests Range-domain
+    # (synth.with_range_requests, bench.py --range-frac), checked on every request
+    w, _, _ = synth.config2_sharded(0, 1, n_txns_per_gpu=6000, n_keys_per_gpu=6000, n_hist_entries_per_gpu=96000)
+    w = synth.with_range_requests(w, 0.03)
+    assert w.queries.n_ranges > 0
+    _eq(native.resolve(w, via="regions"), oracle.resolve(w), "config2 shape + ranges")
+
+
 def test_range_requests_only_esp(oracle):
     # every request an ExclusiveSyncPoint over ranges (witnesses AnyGloballyVisible)
     w = _w(7, range_frac=1.0, n_keys=60, n_txns=120)
