@@ -222,6 +222,30 @@ def test_crosscheck_range_domain_requests(oracle, seed):
     assert n_range_hits > 0
 
 
+def test_with_range_requests_transform(oracle):
+    # synth.with_range_requests (bench.py --range-frac): a share of config 2's requests become Range-domain txns
+    # (domain bit set on txnId and executeAt, no keys) over one range holding 1-8 of the store's keys; the oracle
+    # agrees with the model on them and on the key-domain requests around them
+    w, _, _ = synth.config2_sharded(0, 1, n_txns_per_gpu=1500, n_keys_per_gpu=1500, n_hist_entries_per_gpu=12000)
+    n_before = len(w.queries)
+    w = synth.with_range_requests(w, 0.05, seed=11)
+    q = w.queries
+    assert len(q) == n_before
+    isr = np.diff(q.range_off.astype(np.int64)) > 0
+    assert 0 < int(isr.sum()) < n_before
+    assert np.all(np.diff(q.key_off.astype(np.int64))[isr] == 0)
+    assert np.all((q.txn.lsb[isr] & np.uint64(1)) == 1) and np.all((q.txn.lsb[~isr] & np.uint64(1)) == 0)
+    keys = np.sort(w.cfk.keys)
+    inside = [int(np.count_nonzero((keys > a) & (keys <= b))) for a, b in zip(q.range_start, q.range_end)]
+    assert min(inside) >= 1 and max(inside) <= 8
+    batch = oracle.resolve(w)
+    for i in list(np.nonzero(isr)[0][:40]) + list(np.nonzero(~isr)[0][:20]):
+        kd, rd, dd = refmodel.request_pairs(w, int(i))
+        got = _request(batch, int(i))
+        for m, pairs in ((0, kd), (1, rd), (2, dd)):
+            assert got[m] == refmodel.csr(pairs), (int(i), A.MAP_NAMES[m])
+
+
 def test_range_domain_request_rejections(oracle):
     w = synth.random_small(5, range_frac=0.5)
     q = w.queries
