@@ -2096,7 +2096,9 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                     lean_track = rpw1 == 2 && !c->ds.n_rent;
                     HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
                     if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
-                    HIPCHK(c, run_resolve_lean(c->ds, b, 2, rpw1, false, st));
+                    // after a wide pass 1 the pass-2 list is empty (it serves what pass 2 would, up to 64 raw
+                    // emissions, and hands the rest straight to the general kernel): no launch
+                    if (!wide1) HIPCHK(c, run_resolve_lean(c->ds, b, 2, rpw1, false, st));
                     if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
                 }
                 if (getenv("AD_DEFER_SPLIT"))
