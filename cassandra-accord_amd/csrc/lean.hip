@@ -180,6 +180,34 @@ __device__ __forceinline__ void seg_bitonic_wide(T& x0, T& x1)
         }
 }
 
+// ascending bitonic sort of the 2 x LPR elements of each LPR-lane segment (LPR <= 16: partners within a DPP
+// row), element i = LPR s + l held in register s; a partner LPR away is the lane's other register
+template <class T, uint32_t LPR>
+__device__ __forceinline__ void seg_bitonic_w(T& x0, T& x1)
+{
+    const uint32_t l = lane_id() & (LPR - 1);
+#pragma unroll
+    for (uint32_t k = 2; k <= 2 * LPR; k <<= 1)
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1)
+        {
+            if (j == LPR)
+            {
+                const T lo = min(x0, x1), hi = max(x0, x1);      // k == 2 LPR: ascending
+                x0 = lo;
+                x1 = hi;
+            }
+            else
+            {
+                const T o0 = xor_lane(x0, j), o1 = xor_lane(x1, j);
+                const bool lower = (l & j) == 0;
+                const bool up0 = (l & k) == 0, up1 = ((l + LPR) & k) == 0;
+                x0 = (lower == up0) ? min(x0, o0) : max(x0, o0);
+                x1 = (lower == up1) ? min(x1, o1) : max(x1, o1);
+            }
+        }
+}
+
 // LEAN_ADAPT: refills sized for what the wave will still write (dense arena: 304 MB in use for 272 MB of
 // config-2 regions) -- measured 0.06 ms slower per config-2 step than fixed chunks, the estimator's
 // registers spill in pass 1; off by default
@@ -630,8 +658,11 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         // raw emissions pass 2 takes: 64 (two per lane) without range commands; with them 32 after a pass 1
         // of four requests per wave, else 64 (run_resolve_lean)
         constexpr uint32_t P2CAP = !RNG ? 64u : (RPW == 4 ? 32u : 64u);
+        // four requests per wave with range commands (32-bit rangeDeps keys): a request of 17..32 range emissions
+        // takes two per lane in the range round (rwide below) instead of lean pass 2
+        const bool rw_ok = RNG && RPW == 4 && PASS == 1 && s.rng32;
         const bool hard = defer || seg(ballot(kact && !newest)) != 0 || (PASS == 1 && (T > P2CAP || TR > P2CAP));
-        defer = hard || T > (CAN_WIDE ? 2 * LPR : LPR) || TR > LPR;
+        defer = hard || T > (CAN_WIDE ? 2 * LPR : LPR) || TR > (rw_ok ? 2 * LPR : LPR);
         {
             const bool soft = PASS == 1 ? !hard : true;
             const uint64_t dm = ballot(act && defer && soft && hl == 0);
@@ -801,9 +832,10 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         else if (!LEAN_MASKED) lv = *((!live || (!from_cand && cls == 0)) ? s.cand : lp);
         else if (live && (from_cand || cls != 0)) lv = *lp;
         // range elements (same round trip as the list loads)
-        uint32_t ar = 0;
-        uint64_t ce = 0;
-        bool rlive = false;
+        uint32_t ar = 0, ar1 = 0;
+        uint64_t ce = 0, ce1 = 0;
+        bool rlive = false, rlive1 = false;
+        const bool rwide = rw_ok && seg_max(act ? TR : 0u) > LPR;      // wave-uniform
         if (RNG)
         {
 #pragma unroll
@@ -823,6 +855,26 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
                                             ((ar_meta >> KL_CELL_SHIFT) & 7u) + (hl - ar_start)
                                       : (uint64_t)ar_lo + (hl - ar_start);
             ce = (cin && rlive ? kl64 : s.cell_ent)[rlive ? cidx : 0u];
+            if (rwide)
+            {
+                // element hl + LPR of the wide range round
+                const uint32_t x1 = hl + LPR;
+#pragma unroll
+                for (uint32_t p = 1; p < LEAN_MAXP; ++p)
+                {
+                    const uint32_t sp = seg_lane(rstart, p);
+                    if (p < np && x1 >= sp) ar1 = p;
+                }
+                const uint32_t rsrc1 = sb | ar1;
+                const uint32_t ar1_start = __shfl(rstart, rsrc1, 64), ar1_lo = __shfl(cbc.x, rsrc1, 64);
+                const uint32_t ar1_meta = __shfl(has_cfk ? meta : 0u, rsrc1, 64), ar1_slot = __shfl(Hc.slot, rsrc1, 64);
+                const bool cin1 = (ar1_meta & KL_CELLINL) != 0;
+                rlive1 = act && x1 < TR;
+                const uint64_t cidx1 = cin1 ? (uint64_t)ar1_slot * (sizeof(KeyLine) / 8) + offsetof(KeyLine, inl) / 8 +
+                                                  ((ar1_meta >> KL_CELL_SHIFT) & 7u) + (x1 - ar1_start)
+                                            : (uint64_t)ar1_lo + (x1 - ar1_start);
+                ce1 = (cin1 && rlive1 ? kl64 : s.cell_ent)[rlive1 ? cidx1 : 0u];
+            }
         }
         // the later items' loads go out behind this item's element loads
         Hdr Hn;
@@ -912,10 +964,105 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         // witnessed, not self; unique pairs in (Range.compare, TxnId) order
         const uint32_t rtxw = (uint32_t)ce, rk = rtxw & RANK_MASK, rkd = rtxw >> RANK_BITS;
         const bool rwant = RNG && rlive && ((CLASS_KINDS[cls] >> rkd) & 1) && rk < S && rk != self;
-        const uint64_t rmb = ballot(rwant);
-        if (!RNG || rmb == 0)
+        const uint32_t rtxw1 = (uint32_t)ce1, rk1 = rtxw1 & RANK_MASK, rkd1 = rtxw1 >> RANK_BITS;
+        const bool rwant1 = RNG && rwide && rlive1 && ((CLASS_KINDS[cls] >> rkd1) & 1) && rk1 < S && rk1 != self;
+        const uint64_t rmb = ballot(rwant), rmb1 = RNG && rwide ? ballot(rwant1) : 0ull;
+        if (!RNG || (rmb | rmb1) == 0)
         {
             put_sizes(act, t, 1, 0, 0, 0, 0, false);
+        }
+        else if (RNG && rwide)
+        {
+            // the 32-bit range round below over 2 x LPR elements (element hl in register 0, hl + LPR in 1): sort
+            // (range id << 6 | element), keep the run of each range group's first key, then the distinct
+            // txnIds by (rank << 6 | pair position)
+            const uint32_t LW = LPR;
+            uint32_t k1a = rwant ? ((uint32_t)(ce >> 32) << 6) | hl : 0xFFFFFFFFu;
+            uint32_t k1b = rwant1 ? ((uint32_t)(ce1 >> 32) << 6) | (hl + LW) : 0xFFFFFFFFu;
+            seg_bitonic_w<uint32_t, LPR>(k1a, k1b);
+            const uint32_t totp = __popcll(seg(rmb)) + __popcll(seg(rmb1));
+            const bool pva = hl < totp, pvb = hl + LW < totp;
+            const uint32_t rida = k1a >> 6, ridb = k1b >> 6;
+            // the pair's rank and key: element e of register e / LPR at lane e % LPR
+            const uint32_t va0 = (rk << 3) | ar, va1 = (rk1 << 3) | ar1;
+            auto elem = [&](uint32_t e, bool on) -> uint32_t {
+                const int src = (int)(on ? (sb | (e & (LW - 1))) : lane);
+                const uint32_t x0 = (uint32_t)__shfl((int)va0, src, 64), x1 = (uint32_t)__shfl((int)va1, src, 64);
+                return (e & LW) ? x1 : x0;
+            };
+            const uint32_t rkaa = elem(k1a & 63u, pva), rkab = elem(k1b & 63u, pvb);
+            const uint32_t lasta = (uint32_t)__shfl((int)rida, (int)(sb | (LW - 1)), 64);
+            const uint32_t prida = LEAN_DPP ? wave_up1(rida) : (uint32_t)__shfl_up(rida, 1, LPR);
+            const uint32_t upb = LEAN_DPP ? wave_up1(ridb) : (uint32_t)__shfl_up(ridb, 1, LPR);
+            const uint32_t pridb = hl == 0 ? lasta : upb;
+            const bool gfra = pva && (hl == 0 || prida != rida), gfrb = pvb && pridb != ridb;
+            // each element's range group start (its encoded position: lane, or 64 + lane in register 1); the
+            // segment's first element starts a group, so register 0's absolute-lane max scan stays in the segment
+            const uint32_t gsa = wave_incl_max_dpp(gfra ? lane : 0u);
+            const uint32_t gsb_scan = wave_incl_max_dpp(gfrb ? 64u + lane : 0u);
+            const uint32_t carry = (uint32_t)__shfl((int)gsa, (int)(sb | (LW - 1)), 64);
+            const uint32_t gsb = (gsb_scan >= 64u + sb) ? gsb_scan : carry;
+            auto key_at = [&](uint32_t g) -> uint32_t {
+                const int src = (int)(g & 63u);
+                const uint32_t x0 = (uint32_t)__shfl((int)(rkaa & 7u), src, 64), x1 = (uint32_t)__shfl((int)(rkab & 7u), src, 64);
+                return g >= 64u ? x1 : x0;
+            };
+            const uint32_t ar0a = key_at(gsa), ar0b = key_at(gsb);
+            const bool pua = pva && (rkaa & 7u) == ar0a, pub = pvb && (rkab & 7u) == ar0b;
+            const uint64_t puma = seg(ballot(pua)), pumb = seg(ballot(pub));
+            const uint32_t npa = __popcll(puma);
+            const uint32_t UP = npa + __popcll(pumb);
+            const uint32_t dsta = __popcll(puma & below), dstb = npa + __popcll(pumb & below);
+            const bool gfa = pua && gfra, gfb = pub && gfrb;
+            const uint64_t gma = seg(ballot(gfa)), gmb = seg(ballot(gfb));
+            const uint32_t nR = __popcll(gma) + __popcll(gmb);
+            uint32_t k2a = pua ? ((rkaa >> 3) << 6) | dsta : 0xFFFFFFFFu;
+            uint32_t k2b = pub ? ((rkab >> 3) << 6) | dstb : 0xFFFFFFFFu;
+            seg_bitonic_w<uint32_t, LPR>(k2a, k2b);
+            const uint32_t last2 = (uint32_t)__shfl((int)k2a, (int)(sb | (LW - 1)), 64);
+            const uint32_t p2a = LEAN_DPP ? wave_up1(k2a) : (uint32_t)__shfl_up(k2a, 1, LPR);
+            const uint32_t up2b = LEAN_DPP ? wave_up1(k2b) : (uint32_t)__shfl_up(k2b, 1, LPR);
+            const uint32_t p2b = hl == 0 ? last2 : up2b;
+            const bool v2a = hl < UP, v2b = hl + LW < UP;
+            const bool uqa = v2a && (hl == 0 || (p2a >> 6) != (k2a >> 6)), uqb = v2b && (p2b >> 6) != (k2b >> 6);
+            const uint64_t uma = seg(ballot(uqa)), umb = seg(ballot(uqb));
+            const uint32_t nua = __popcll(uma);
+            const uint32_t UR = nua + __popcll(umb);
+            const uint32_t ura = __popcll(uma & below) + (uqa ? 1u : 0u) - 1u;
+            const uint32_t urb = nua + __popcll(umb & below) + (uqb ? 1u : 0u) - 1u;
+            const uint64_t bytes = act && totp ? (((uint64_t)nR * 8 + (uint64_t)UR * 4 + (uint64_t)(nR + UP) * 4 + 7) & ~7ull) : 0;
+            bool fits;
+            const uint64_t ro = seg_alloc(bytes, fits, it);
+            put_sizes(act, t, 1, fits ? nR : 0, fits ? UR : 0, fits ? nR + UP : 0, ro, true);
+            if (act && totp && fits)
+            {
+                int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
+                uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nR);
+                int32_t* ok2t = reinterpret_cast<int32_t*>(otx + UR);
+                // 2 LPR-bit masks over the elements in order: register 0's lanes, then register 1's
+                const uint32_t GM = (uint32_t)gma | ((uint32_t)gmb << LW), PUM = (uint32_t)puma | ((uint32_t)pumb << LW);
+                auto group_end = [&](uint32_t e) -> uint32_t {
+                    const uint32_t later = GM & ~((2u << e) - 1u);
+                    const uint32_t nxt = later ? (uint32_t)(__ffs(later) - 1) : 0u;
+                    return later ? (uint32_t)__popc(PUM & ((1u << nxt) - 1u)) : UP;
+                };
+                if (gfa)
+                {
+                    const uint32_t gi = __popcll(gma & below);
+                    okeys[gi] = (int64_t)rida;                         // range id (ad_range_table)
+                    ok2t[gi] = (int32_t)(nR + group_end(hl));
+                }
+                if (gfb)
+                {
+                    const uint32_t gi = __popcll(gma) + __popcll(gmb & below);
+                    okeys[gi] = (int64_t)ridb;
+                    ok2t[gi] = (int32_t)(nR + group_end(hl + LW));
+                }
+                if (uqa) otx[ura] = ((k2a >> 6) - 1) >> 1;
+                if (uqb) otx[urb] = ((k2b >> 6) - 1) >> 1;
+                if (v2a) ok2t[nR + (k2a & 63u)] = (int32_t)ura;
+                if (v2b) ok2t[nR + (k2b & 63u)] = (int32_t)urb;
+            }
         }
         else if (s.rng32)
         {

@@ -135,6 +135,18 @@ def test_config4_full(oracle):
     w = synth.config4()
     stats, got = _run_full(w, oracle)
     assert stats["n_pairs"][A.AD_MAP_RANGE] > 0 and got.pair_count(A.AD_MAP_RANGE) > 0
+    # the ~9 % of requests with 17..32 range emissions take lean pass 1's wide range round, not pass 2
+    assert stats["n_lean_pass2"] < 10_000      # 95k before; what is left has more than 16 key emissions
+
+
+def test_config4_dense_ranges_every_request(oracle):
+    # config 4's range density (100k range commands, ~12 stabbing entries per 4-key request) over 4k requests,
+    # every request checked: the wide range round (17..32 range emissions, two per lane) and the narrow one
+    w = synth.config4(n_txns=4_000, n_hist_txns=20_000, seed=0xACC0D0B4)
+    exp = oracle.resolve(w)
+    got = native.resolve(w, via="regions")
+    ok, why = got.equals(exp, detail=True)
+    assert ok, "%s; first mismatch %r" % (why, got.first_mismatch(exp))
 
 
 def test_config2_full_narrow_pass1(oracle, config2_full, monkeypatch):
