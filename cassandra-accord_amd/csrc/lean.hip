@@ -46,7 +46,8 @@ constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 constexpr uint32_t LEAN_CHUNK = 1u << LEAN_CHUNK_LOG;   // region bytes a wave takes from the arena at a time
 // measurement switches (scripts/build_variant.sh; results are wrong with any of them set):
 // 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes, 8 no size / offset stores,
-// 16 KeyLines from a 512 KB subset of the table (cache-resident; a line counts as the key's)
+// 16 KeyLines from a 512 KB subset of the table (cache-resident; a line counts as the key's), 32 sizes stored
+// as 64-byte per-request records (into the offsets buffer) instead of the nine SoA arrays
 #ifndef LEAN_EXP
 #define LEAN_EXP 0
 #endif
@@ -559,7 +560,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         if (on && hl < 3)
         {
             const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);
-            b.sz[(uint64_t)(3 * m + hl) * n + t] = v;
+            if (LEAN_EXP & 32) reinterpret_cast<uint32_t*>(b.off)[(uint64_t)t * 16 + 3 * m + hl] = v;   // measurement: AoS records
+            else b.sz[(uint64_t)(3 * m + hl) * n + t] = v;
         }
         if (with_ro && on && hl == 3) b.t_reg[(uint64_t)m * n + t] = ro;
     };
