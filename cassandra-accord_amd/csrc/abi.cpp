@@ -1937,7 +1937,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         HIPCHK(c, hipMemsetAsync(c->rq_err.p, 0, 8, st));
         // rq_err[0]: the rejection flag; rq_err[1]: the Range-domain requests, listed in rq_list
         HIPCHK(c, run_range_count(c->ds, n, q->key_off, q->range_off, q->range_start, q->range_end, c->rq_cnt.as<uint32_t>(),
-                                  c->rq_err.as<uint32_t>(), c->rq_list.as<uint32_t>(), recovery_scan < 0, st));
+                                  c->rq_err.as<uint32_t>(), c->rq_list.as<uint32_t>(), nr, recovery_scan < 0, st));
         HIPCHK(c, run_scan_arrays(c->rq_cnt.as<uint32_t>(), c->rq_off.as<uint64_t>(), n, 1, c->rq_bsum.as<uint64_t>(), st));
         uint64_t* hs = c->h_small;
         HIPCHK(c, hipMemcpyAsync(&hs[3], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));

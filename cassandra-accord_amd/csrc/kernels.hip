@@ -222,20 +222,6 @@ hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // The keys come out ascending (sliced ranges ascending and disjoint), which is all K2 needs: range
 // probes contribute no keyDeps keys.
 // ---------------------------------------------------------------------------------------
-// first snapshot key index inside [a, b) / (a, b]: keys strictly above a (EndInclusive) or at/above a
-__device__ __forceinline__ uint64_t key_lb(const DevSnapshot& s, int64_t x, bool strictly_above)
-{
-    uint64_t lo = 0, hi = s.n_keys;
-    while (lo < hi)
-    {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (strictly_above ? s.keys[mid] <= x : s.keys[mid] < x) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// the sliced part j of range [a, b) under slice sl (no slices: sl = 0 is the whole line): [*lo, *hi)
 __device__ __forceinline__ bool slice_part(const DevSnapshot& s, int64_t a, int64_t b, uint64_t sl, int64_t* lo, int64_t* hi)
 {
     if (s.n_slices == 0)
@@ -256,47 +242,82 @@ __global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, 
                                                      uint32_t* err, uint32_t* __restrict__ list, bool with_rb)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const uint64_t r0 = range_off[t], r1 = range_off[t + 1];
-    const uint64_t nk = key_off[t + 1] - key_off[t];
-    if (r1 == r0)
-    {
-        cnt[t] = (uint32_t)nk;
-        return;
-    }
-    list[atomicAdd(&err[1], 1u)] = (uint32_t)t;
-    bool bad = nk != 0;
-    const bool incl = s.start_inclusive != 0;
-    uint64_t c = 0;
-    const uint64_t n_sl = s.n_slices ? s.n_slices : 1;
+    const bool on = t < n;
+    const uint64_t r0 = on ? range_off[t] : 0, r1 = on ? range_off[t + 1] : 0;
+    const uint64_t nk = on ? key_off[t + 1] - key_off[t] : 0;
+    // a Range-domain request: validated here, listed (one atomic per wave), its probe count written by
+    // k_range_count_r
+    bool bad = r1 != r0 && nk != 0;
     for (uint64_t j = r0; j < r1; ++j)
     {
         const int64_t a = range_start[j], e = range_end[j];
         if (a >= e || (j > r0 && range_end[j - 1] > a)) bad = true;
+    }
+    if (bad) atomicOr(err, 1u);
+    if (on) cnt[t] = r1 == r0 ? (uint32_t)nk : 0u;
+    const bool listed = on && r1 != r0 && !bad;
+    const uint64_t lm = ballot(listed);
+    if (!lm) return;
+    uint32_t base = 0;
+    if (lane_id() == (uint32_t)(__ffsll((unsigned long long)lm) - 1)) base = atomicAdd(&err[1], (uint32_t)__popcll(lm));
+    base = (uint32_t)__shfl((int)base, __ffsll((unsigned long long)lm) - 1, 64);
+    if (listed) list[base + __popcll(lm & ((1ull << lane_id()) - 1))] = (uint32_t)t;
+}
+
+// the snapshot keys inside [lo, hi) by one wave: two 64-ary searches (k0 = first key inside, k1 = first beyond)
+__device__ __forceinline__ void wave_key_span(const DevSnapshot& s, int64_t lo, int64_t hi, bool incl, uint64_t& k0, uint64_t& k1)
+{
+    // EndInclusive (s, e]: keys > lo and <= hi; StartInclusive [s, e): keys >= lo and < hi
+    k0 = wave_lower_bound(0, s.n_keys, [&](uint64_t i) { return s.keys[i]; }, [&](int64_t v) { return incl ? v < lo : v <= lo; });
+    k1 = wave_lower_bound(k0, s.n_keys, [&](uint64_t i) { return s.keys[i]; }, [&](int64_t v) { return incl ? v < hi : v <= hi; });
+}
+
+// one wave per listed Range-domain request: its probe count (keys inside each sliced part, + the part itself with
+// range commands, + its unsliced ranges with RedundantBefore entries)
+__global__ __launch_bounds__(256) void k_range_count_r(DevSnapshot s, const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ n_list,
+                                                       const uint64_t* __restrict__ range_off,
+                                                       const int64_t* __restrict__ range_start,
+                                                       const int64_t* __restrict__ range_end, uint32_t* __restrict__ cnt,
+                                                       bool with_rb)
+{
+    const uint64_t li = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (li >= *n_list) return;
+    const uint64_t t = list[li];
+    const uint64_t r0 = range_off[t], r1 = range_off[t + 1];
+    const bool incl = s.start_inclusive != 0;
+    const uint64_t n_sl = s.n_slices ? s.n_slices : 1;
+    uint64_t c = 0;
+    for (uint64_t j = r0; j < r1; ++j)
+    {
+        const int64_t a = range_start[j], e = range_end[j];
         for (uint64_t sl = 0; sl < n_sl; ++sl)
         {
             int64_t lo, hi;
             if (!slice_part(s, a, e, sl, &lo, &hi)) continue;
-            c += key_lb(s, hi, !incl) - key_lb(s, lo, !incl);
+            uint64_t k0, k1;
+            wave_key_span(s, lo, hi, incl, k0, k1);
+            c += k1 - k0;
             if (s.n_rent) ++c;
         }
     }
     if (s.n_rb && with_rb) c += r1 - r0;
-    if (bad) atomicOr(err, 1u);
-    cnt[t] = bad ? 0u : (uint32_t)min<uint64_t>(c, 0xFFFFFFFFull);
+    if (lane_id() == 0) cnt[t] = (uint32_t)min<uint64_t>(c, 0xFFFFFFFFull);
 }
 
-// a key-domain request's keys, one thread per request (its range end is never read: PK_KEY)
+// a key-domain request's keys, 8 lanes per request (a wave copies 8 consecutive requests' keys, coalesced at both
+// ends); its range end is never read (PK_KEY)
 __global__ __launch_bounds__(256) void k_range_fill_keys(uint64_t n, const uint64_t* __restrict__ key_off,
                                                          const int64_t* __restrict__ keys,
                                                          const uint64_t* __restrict__ range_off,
                                                          const uint64_t* __restrict__ off, int64_t* __restrict__ pkeys,
                                                          uint8_t* __restrict__ pkind)
 {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3;
+    const uint32_t j = threadIdx.x & 7u;
     if (t >= n || range_off[t + 1] != range_off[t]) return;
     const uint64_t k0 = key_off[t], nk = key_off[t + 1] - k0, o = off[t];
-    for (uint64_t i = 0; i < nk; ++i)
+    for (uint64_t i = j; i < nk; i += 8)
     {
         pkeys[o + i] = keys[k0 + i];
         pkind[o + i] = PK_KEY;
@@ -328,7 +349,8 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, const uint32_
         {
             int64_t lo, hi;
             if (!slice_part(s, a, e, sl, &lo, &hi)) continue;
-            const uint64_t k0 = key_lb(s, lo, !incl), k1 = key_lb(s, hi, !incl);
+            uint64_t k0, k1;
+            wave_key_span(s, lo, hi, incl, k0, k1);
             for (uint64_t i = lane; i < k1 - k0; i += 64)
             {
                 pkeys[o + i] = s.keys[k0 + i];
@@ -359,11 +381,16 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, const uint32_
 
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
                            const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           uint32_t* list, bool with_rb, hipStream_t st)
+                           uint32_t* list, uint64_t max_list, bool with_rb, hipStream_t st)
 {
-    if (n)
-        k_range_count<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n, key_off, range_off, range_start, range_end, cnt, err,
-                                                                   list, with_rb);
+    if (!n) return hipSuccess;
+    k_range_count<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n, key_off, range_off, range_start, range_end, cnt, err,
+                                                               list, with_rb);
+    // the listed requests' counts: a wave each, the grid sized for every range of the batch (the list is shorter)
+    const uint64_t m = std::min<uint64_t>(max_list, n);
+    if (m)
+        k_range_count_r<<<(unsigned)((m + 3) / 4), 256, 0, st>>>(s, list, err + 1, range_off, range_start, range_end, cnt,
+                                                                 with_rb);
     return hipGetLastError();
 }
 
@@ -372,7 +399,7 @@ hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_
                           const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, const uint32_t* list,
                           uint32_t n_list, bool with_rb, hipStream_t st)
 {
-    if (n) k_range_fill_keys<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, key_off, keys, range_off, off, pkeys, pkind);
+    if (n) k_range_fill_keys<<<(unsigned)((8 * n + 255) / 256), 256, 0, st>>>(n, key_off, keys, range_off, off, pkeys, pkind);
     if (n_list)
         k_range_fill<<<(unsigned)((n_list + 3) / 4), 256, 0, st>>>(s, list, n_list, range_off, range_start, range_end, off, pkeys,
                                                                    pkeys_hi, pkind, with_rb);

@@ -145,7 +145,7 @@ constexpr uint8_t PK_KEY = 0, PK_RANGE_KEY = 1, PK_RANGE = 2, PK_RANGE_RB = 3;
 // the probes: a key-domain request's keys one thread per request, a listed request's one wave each
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
                            const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           uint32_t* list, bool with_rb, hipStream_t st);
+                           uint32_t* list, uint64_t max_list, bool with_rb, hipStream_t st);
 hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
                           const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
                           const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, const uint32_t* list,
