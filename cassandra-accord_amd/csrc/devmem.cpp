@@ -388,7 +388,12 @@ hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t st)
         if ((e = hipEventRecord(S.ev[k], st)) != hipSuccess) return e;
         S.busy[k] = true;
     }
-    return hipSuccess;
+    // the pair goes back to the pool with nothing in flight: its events were recorded on the caller's stream,
+    // which a context may destroy before the pair's next user would wait on them (round 5 saw one "stream is
+    // capturing" error from a staged upload on a fresh context)
+    hipError_t e = S.wait(0);
+    const hipError_t e1 = S.wait(1);
+    return e != hipSuccess ? e : e1;
 }
 
 hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st)
