@@ -1841,8 +1841,10 @@ static uint32_t lean_rpw1(uint64_t n, uint64_t np, bool ranges)
     // With range commands up to 4 keys per request on average: four per wave (config 4: pass 1 0.90 ->
     // 0.58 ms, its deferrals -- above 16 raw emissions -- two per wave in pass 2); up to 4.5, so that a few
     // Range-domain requests (their expanded probes; the split kernels resolve them) do not tip a 4-key batch
-    // over (config 4 with 1 % of them: pass 1 0.93 ms at two per wave)
-    return 2 * np <= (ranges ? 9 : 6) * n ? 4u : 2u;
+    // over (config 4 with 1 % of them: pass 1 0.93 ms at two per wave). Without range commands also up to 4.5:
+    // config 3's store (4 uniform keys per request) pass 1 0.725 -> 0.477 ms, pass 2 0.010 -> 0.099 ms for the
+    // 4 % above 16 raw emissions (scripts/lean_lab.py --config 3)
+    return 2 * np <= 9 * n ? 4u : 2u;
 }
 
 // Lean pass 1 wide or narrow (rpw 2, no range commands; results identical either way). The wide kernel

@@ -166,6 +166,10 @@ def test_lean_pass1_width_follows_the_batches(oracle, config2_full, monkeypatch)
     dev = torch.device("cuda", 0)
     w3 = synth.config3_shard(0, 1, txns_per_gpu=1_000_000, keys_per_gpu=160_000)[0]
     for w, second_wide in ((config2_full, True), (w3, False)):
+        # the width choice is lean pass 1's at two requests per wave; config 3's 4-key requests would run four per
+        # wave (abi.cpp lean_rpw1), so its store is held at two
+        if w is w3:
+            monkeypatch.setenv("AD_LEAN_RPW", "2")
         st = native.DeviceCommandStore(device=0, slices=w.slices)
         try:
             st.load(w)
