@@ -1820,10 +1820,9 @@ static int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
     return 0;
 }
 
-// requests per wave of lean pass 1: four for batches of small requests (at most 3 keys on average,
-// e.g. a store's share of requests spanning many stores), else two. AD_LEAN_RPW overrides.
-// requests per wave of lean pass 1 by the batch's keys per request: 8 (<= 1.5 on average: a store's
-// share of requests spanning many stores), 4 (<= 3), else 2
+// requests per wave of lean pass 1 by the batch's keys per request (lean_rpw1): four up to 4.5 keys on
+// average, else two; AD_LEAN_RPW overrides (8: opt-in, measured no faster on a store's share of
+// requests spanning many stores).
 // Lean pass 1 as gather + build (k_lean_gather, k_lean_build): opt-in, AD_LEAN_GB=1. Measured on config 2
 // (DESIGN §4): gather 0.19-0.30 ms + build 0.36 + wide build 0.15 against 0.54 ms for the fused pass -- the
 // build alone is issue-bound (its SIMDs ~98 % busy at ~390 VALU per two requests), so the split buys no
@@ -1834,10 +1833,9 @@ static bool lean_gb_on()
     return e && atoi(e) != 0;
 }
 
-static uint32_t lean_rpw1(uint64_t n, uint64_t np, bool ranges)
+static uint32_t lean_rpw1(uint64_t n, uint64_t np)
 {
     if (const char* e = getenv("AD_LEAN_RPW")) return atoi(e) == 8 ? 8u : (atoi(e) == 4 ? 4u : 2u);
-    // 8 requests per wave (AD_LEAN_RPW=8) stays opt-in while the late-round-3 device faults are open.
     // With range commands up to 4 keys per request on average: four per wave (config 4: pass 1 0.90 ->
     // 0.58 ms, its deferrals -- above 16 raw emissions -- two per wave in pass 2); up to 4.5, so that a few
     // Range-domain requests (their expanded probes; the split kernels resolve them) do not tip a 4-key batch
@@ -1993,7 +1991,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
     }
     // lean pass 1 as gather + build (two requests per build wave, no range commands): AD_LEAN_GB=0 keeps
     // the single fused pass
-    const bool gb = lean && !c->ds.n_rent && lean_rpw1(n, np, c->ds.n_rent != 0) == 2 && lean_gb_on();
+    const bool gb = lean && !c->ds.n_rent && lean_rpw1(n, np) == 2 && lean_gb_on();
     if (gb)
     {
         if (!ens<uint32_t>(c->lg_stage, n * 64) || !ens<uint4>(c->lg_rec, n) || !ens<int64_t>(c->lg_keys, n * 8) ||
@@ -2083,7 +2081,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                 // lean kernel first (newest requests, 2 per wave); the general fused kernel then
                 // takes only what it deferred (count read on the device, no host round trip)
                 if (!c->ev_lean1) HIPCHK(c, timing_event(&c->ev_lean1));
-                const uint32_t rpw1 = lean_rpw1(n, np, c->ds.n_rent != 0);
+                const uint32_t rpw1 = lean_rpw1(n, np);
                 if (gb)
                 {
                     // gather + build (k_lean_gather, k_lean_build): the rest to the general kernel
