@@ -60,6 +60,43 @@ def test_range_requests_beside_lean_config2_shape(oracle):
     _eq(native.resolve(w, via="regions"), oracle.resolve(w), "config2 shape + ranges")
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_range_requests_only_on_lean_store(oracle, seed):
+    # a batch of Range-domain requests only, on a store the lean passes serve: lean pass 1 takes no request
+    # and every one goes to the split kernels
+    w = _w(400 + seed, n_keys=50, n_txns=150, n_hist_txns=300, range_frac=1.0, n_redundant=0,
+           n_range_cmds=(0 if seed % 2 else 12), with_slices=(seed == 2))
+    q = w.queries
+    idx = np.array([i for i in range(len(q)) if q.ranges_of(i)])
+    assert len(idx) > 50
+    w = Workload(w.name, w.cfk, w.cmds, w.redundant, q.take(idx), w.flags, w.params, w.range_start_inclusive, w.slices)
+    exp = oracle.resolve(w)
+    for via in ("device", "regions"):
+        _eq(native.resolve(w, via=via), exp, "seed %d via %s" % (seed, via))
+
+
+@pytest.mark.parametrize("with_slices", [False, True])
+def test_range_requests_holding_no_key(oracle, with_slices):
+    # Range-domain requests whose one range lies beyond every key of the store (no CommandsForKey inside,
+    # possibly outside its slices) beside key-domain requests the lean passes serve: empty expansions
+    w = _w(420, n_keys=60, n_txns=220, n_hist_txns=400, range_frac=0.3, n_redundant=0, n_range_cmds=10,
+           with_slices=with_slices)
+    q = w.queries
+    rs, re_ = q.range_start.copy(), q.range_end.copy()
+    moved = 0
+    for i in range(len(q)):
+        a = int(q.range_off[i])
+        if int(q.range_off[i + 1]) == a + 1:
+            far = 10 ** 9 + 1000 * i
+            rs[a], re_[a] = (far, far + 100) if i % 2 else (-far - 100, -far)
+            moved += 1
+    assert moved > 5
+    q.range_start, q.range_end = rs, re_
+    exp = oracle.resolve(w)
+    for via in ("host", "device", "regions"):
+        _eq(native.resolve(w, via=via), exp, "far ranges via %s" % via)
+
+
 def test_range_requests_only_esp(oracle):
     # every request an ExclusiveSyncPoint over ranges (witnesses AnyGloballyVisible)
     w = _w(7, range_frac=1.0, n_keys=60, n_txns=120)
