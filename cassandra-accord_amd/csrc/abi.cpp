@@ -225,6 +225,11 @@ struct ad_ctx {
     hipEvent_t ev_done = nullptr;      // end of a batch's work (default flags: the host reads what it copied)
     BatchCtl* h_ctl = nullptr;         // pinned mirror of the batch control block
     uint64_t* h_small = nullptr;       // pinned words the batch prologue reads back (key / range totals)
+    // small uploads inside a call's stream of work (the export's owner bounds, the merge's source starts):
+    // one pinned slot per use, each reused after the event of its previous copy (up_small)
+    uint64_t* h_up[2] = {};
+    hipEvent_t ev_up[2] = {};
+    bool up_busy[2] = {};
     // ad_deps_batch_into: a second result bank (offsets + packed arrays) so that one slice of a batch is
     // copied out while the next resolves, the copy-out stream and its events
     DevBuf off_b, o_keys_b[3], o_txns_b[3], o_k2t_b[3];
@@ -1790,6 +1795,31 @@ static int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
 template <class T>
 static bool ens(DevBuf& b, uint64_t n) { return b.ensure(sizeof(T) * std::max<uint64_t>(n, 1)); }
 
+// A small upload (at most UP_WORDS words) ordered on st without a host wait: copied into the context's
+// pinned slot `k`, whose previous copy has completed first (its event; normally long done). A pageable
+// h2d would return only after the copy -- after everything queued before it on st.
+constexpr uint64_t UP_WORDS = 512;
+static hipError_t up_small(ad_ctx* c, int k, void* dst, const void* src, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return hipSuccess;
+    if (bytes > sizeof(uint64_t) * UP_WORDS) return h2d(dst, src, bytes, st);
+    if (!c->h_up[k])
+    {
+        if (hipError_t e = hipHostMalloc((void**)&c->h_up[k], sizeof(uint64_t) * UP_WORDS, hipHostMallocDefault)) return e;
+        if (hipError_t e = hipEventCreateWithFlags(&c->ev_up[k], hipEventDisableTiming)) return e;
+    }
+    if (c->up_busy[k])
+    {
+        if (hipError_t e = hipEventSynchronize(c->ev_up[k])) return e;
+        c->up_busy[k] = false;
+    }
+    memcpy(c->h_up[k], src, bytes);
+    if (hipError_t e = hipMemcpyAsync(dst, c->h_up[k], bytes, hipMemcpyHostToDevice, st)) return e;
+    if (hipError_t e = hipEventRecord(c->ev_up[k], st)) return e;
+    c->up_busy[k] = true;
+    return hipSuccess;
+}
+
 // bind the split kernels' per-batch arrays for a batch of n requests / np probes
 static bool bind_split(ad_ctx::SplitBufs& S, BatchBufs& b, uint64_t n, uint64_t np, bool own_sizes)
 {
@@ -2506,6 +2536,12 @@ void ad_ctx_destroy(ad_ctx* c)
     if (c->ev_sp1) (void)hipEventDestroy(c->ev_sp1);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->h_small) (void)hipHostFree(c->h_small);
+    for (int k = 0; k < 2; ++k)
+    {
+        if (c->up_busy[k]) (void)hipEventSynchronize(c->ev_up[k]);     // a copy on a caller's stream
+        if (c->ev_up[k]) (void)hipEventDestroy(c->ev_up[k]);
+        if (c->h_up[k]) (void)hipHostFree(c->h_up[k]);
+    }
     if (c->h_xtab) (void)hipHostFree(c->h_xtab);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     for (hipEvent_t e : c->ev_copied)
@@ -4066,7 +4102,7 @@ static int export_sizes(ad_ctx* c, const ad_deps_result* res, const int64_t* txn
     a.rank_ids = id_format == AD_IDS_RANK;      // the dictionary is the global one: ids are global ranks
     a.sz = c->x_sz.as<uint32_t>();
     a.off = c->x_off.as<uint64_t>();
-    HIPCHK(c, h2d(c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), st));
+    HIPCHK(c, up_small(c, 0, c->x_df.p, dest_first, sizeof(uint64_t) * (n_dest + 1), st));
     HIPCHK(c, run_export_sizes(a, st));
     HIPCHK(c, run_scan_arrays(a.sz, a.off, n, 1, c->x_bsum.as<uint64_t>(), st));
     HIPCHK(c, run_export_bounds(a, c->x_df.as<uint64_t>(), n_dest, c->x_cnt.as<uint64_t>(), st));
@@ -4189,7 +4225,7 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
         a.pdp = c->m_pdp.as<uint32_t>(); a.ppos = c->m_ppos.as<uint32_t>();
     }
     HIPCHK(c, hipEventRecord(c->ev[6], st));
-    HIPCHK(c, h2d(c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), st));
+    HIPCHK(c, up_small(c, 1, c->m_src.p, first.data(), sizeof(uint64_t) * (n_src + 1), st));
     HIPCHK(c, hipMemsetAsync(a.error, 0, sizeof(uint32_t), st));
     HIPCHK(c, hipMemsetAsync(a.slot, 0xFF, sizeof(int32_t) * std::max<uint64_t>((by_request ? n_owned : G) * n_src, 1), st));
     HIPCHK(c, run_merge_prepare(a, st));
