@@ -230,6 +230,7 @@ struct ad_ctx {
     uint64_t* h_up[2] = {};
     hipEvent_t ev_up[2] = {};
     bool up_busy[2] = {};
+    uint64_t* h_rb = nullptr;          // pinned words for small read-backs that end in one stream sync (rb_slot)
     // ad_deps_batch_into: a second result bank (offsets + packed arrays) so that one slice of a batch is
     // copied out while the next resolves, the copy-out stream and its events
     DevBuf off_b, o_keys_b[3], o_txns_b[3], o_k2t_b[3];
@@ -1820,6 +1821,16 @@ static hipError_t up_small(ad_ctx* c, int k, void* dst, const void* src, size_t 
     return hipSuccess;
 }
 
+// UP_WORDS pinned words for read-backs: several async copies into them, then one synchronisation (a
+// pageable d2h waits for its own copy -- two of them cost two round trips). Only between a call's copies
+// and its synchronisation.
+static uint64_t* rb_slot(ad_ctx* c)
+{
+    if (!c->h_rb && hipHostMalloc((void**)&c->h_rb, sizeof(uint64_t) * UP_WORDS, hipHostMallocDefault) != hipSuccess)
+        c->h_rb = nullptr;
+    return c->h_rb;
+}
+
 // bind the split kernels' per-batch arrays for a batch of n requests / np probes
 static bool bind_split(ad_ctx::SplitBufs& S, BatchBufs& b, uint64_t n, uint64_t np, bool own_sizes)
 {
@@ -2542,6 +2553,7 @@ void ad_ctx_destroy(ad_ctx* c)
         if (c->ev_up[k]) (void)hipEventDestroy(c->ev_up[k]);
         if (c->h_up[k]) (void)hipHostFree(c->h_up[k]);
     }
+    if (c->h_rb) (void)hipHostFree(c->h_rb);
     if (c->h_xtab) (void)hipHostFree(c->h_xtab);
     if (c->ev_ready) (void)hipEventDestroy(c->ev_ready);
     for (hipEvent_t e : c->ev_copied)
@@ -4259,9 +4271,13 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     if (!by_request)
     {
         // outputs sized from the scanned group sizes (one round trip)
-        HIPCHK(c, d2h(bases, c->m_bases.p, sizeof(bases), st));
-        HIPCHK(c, d2h(&err, a.error, sizeof(err), st));
+        uint64_t* rb = rb_slot(c);
+        if (!rb) return c->fail(AD_E_NOMEM, "pinned read-back words");
+        HIPCHK(c, hipMemcpyAsync(rb, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(rb + 12, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
+        memcpy(bases, rb, sizeof(bases));
+        memcpy(&err, rb + 12, sizeof(err));
         if (err) return malformed(err);
         // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
         if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, rank_ids ? (bases[10] + 1) / 2 : 3 * bases[10]) ||
@@ -4274,9 +4290,15 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     HIPCHK(c, by_request ? run_rmerge_copy(a, c->m_bases.as<uint64_t>(), st)
                          : union_keys ? run_union_emit(a, st) : rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
     HIPCHK(c, hipEventRecord(c->ev[7], st));
-    if (by_request) HIPCHK(c, d2h(bases, c->m_bases.p, sizeof(bases), st));
-    HIPCHK(c, d2h(&err, a.error, sizeof(err), st));
-    HIPCHK(c, hipStreamSynchronize(st));
+    {
+        uint64_t* rb = rb_slot(c);
+        if (!rb) return c->fail(AD_E_NOMEM, "pinned read-back words");
+        if (by_request) HIPCHK(c, hipMemcpyAsync(rb, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(rb + 12, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (by_request) memcpy(bases, rb, sizeof(bases));
+        memcpy(&err, rb + 12, sizeof(err));
+    }
     if (err) return malformed(err);
     float ms = 0;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
@@ -5231,7 +5253,10 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
         ad_ctx* c = ctxs[i];
         if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
         if (int rc = export_sizes(c, res[i], txn_index[i], n, dest_first[i], fmt, c->stream, &ea[i])) return rc;
-        HIPCHK(c, d2h(cum[i].data(), c->x_cnt.p, sizeof(uint64_t) * cum[i].size(), c->stream));
+        // into the store's pinned read-back words: the stores' size passes overlap, read after the sync below
+        uint64_t* rb = cum[i].size() <= UP_WORDS ? rb_slot(c) : nullptr;
+        if (rb) HIPCHK(c, hipMemcpyAsync(rb, c->x_cnt.p, sizeof(uint64_t) * cum[i].size(), hipMemcpyDeviceToHost, c->stream));
+        else HIPCHK(c, d2h(cum[i].data(), c->x_cnt.p, sizeof(uint64_t) * cum[i].size(), c->stream));
     }
     // 2. the exchange table, as the RCCL path gathers it
     std::vector<uint64_t> table(RW * n, 0);
@@ -5240,6 +5265,7 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
         ad_ctx* c = ctxs[s];
         if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (cum[s].size() <= UP_WORDS && c->h_rb) memcpy(cum[s].data(), c->h_rb, sizeof(uint64_t) * cum[s].size());
         uint64_t* row = table.data() + RW * s;
         for (size_t i = 0; i < 4 * (size_t)n; ++i) row[i] = cum[s][i + 4] - cum[s][i];
         const XRowHdr h = x_row_hdr(c, fmt, 0);
