@@ -4160,8 +4160,72 @@ int ad_parts_export(ad_ctx* c, const ad_deps_result* res, const int64_t* txn_ind
     return export_emit(c, a, out->hdr, out->keys, out->ids, out->k2t, st);
 }
 
+// The end of a merge once its kernels and read-backs are queued: one synchronisation, then the result's
+// views (parts_merge with a MergeTail returns before it, so that ad_exchange_local's owners merge at once)
+struct MergeTail {
+    hipStream_t st;
+    MergeArgs a;
+    bool by_request, rank_ids;
+    uint64_t n_owned, txn_base;
+};
+
+static int merge_malformed(ad_ctx* c, uint32_t e)
+{
+    return c->fail(AD_E_INVAL, "ad_parts_merge: malformed parts (%s)",
+                   e & 1  ? "request outside the owned range or bad map" :
+                   e & 2  ? "two parts of one request and map from one source" :
+                   e & 4  ? "keys of different stores overlap or are out of slice order" :
+                   e & 16 ? "id rank outside the global dictionary" :
+                            "ids of a part not sorted and unique");
+}
+
+static int merge_tail(ad_ctx* c, const MergeTail& t, ad_merged* out)
+{
+    const MergeArgs& a = t.a;
+    const uint64_t n_owned = t.n_owned;
+    uint64_t bases[12];
+    uint32_t err = 0;
+    uint64_t* rb = c->h_rb;             // filled by parts_merge's last copies
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    HIPCHK(c, hipStreamSynchronize(t.st));
+    memcpy(bases, rb, sizeof(bases));
+    memcpy(&err, rb + 12, sizeof(err));
+    if (err) return merge_malformed(c, err);
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
+    memset(out, 0, sizeof(*out));
+    out->n_txns = n_owned;
+    out->txn_base = t.txn_base;
+    out->ms_device = ms;
+    out->id_format = t.rank_ids ? AD_IDS_RANK : AD_IDS_TRIPLET;
+    for (int m = 0; m < 3; ++m)
+    {
+        if (t.by_request)
+        {
+            // the scan of the size pass is the merged CSR: [k*3 + m][n_owned + 1]
+            out->keys_off[m] = a.goff + (uint64_t)(0 * 3 + m) * (n_owned + 1);
+            out->txn_off[m] = a.goff + (uint64_t)(1 * 3 + m) * (n_owned + 1);
+            out->k2t_off[m] = a.goff + (uint64_t)(2 * 3 + m) * (n_owned + 1);
+        }
+        else
+        {
+            out->keys_off[m] = a.o_keys_off + (uint64_t)m * (n_owned + 1);
+            out->txn_off[m] = a.o_txn_off + (uint64_t)m * (n_owned + 1);
+            out->k2t_off[m] = a.o_k2t_off + (uint64_t)m * (n_owned + 1);
+        }
+        out->keys[m] = a.o_keys + bases[3 * m + 0];
+        out->txns[m] = t.rank_ids ? reinterpret_cast<int64_t*>(reinterpret_cast<uint32_t*>(a.o_ids) + bases[3 * m + 1])
+                                  : a.o_ids + 3 * bases[3 * m + 1];
+        out->k2t[m] = a.o_k2t + bases[3 * m + 2];
+        out->n_keys[m] = (bases[3 * (m + 1) + 0] - bases[3 * m + 0]) / (m == AD_MAP_RANGE ? 2 : 1);
+        out->n_ids[m] = bases[3 * (m + 1) + 1] - bases[3 * m + 1];
+        out->n_k2t[m] = bases[3 * (m + 1) + 2] - bases[3 * m + 2];
+    }
+    return AD_OK;
+}
+
 static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
-                       uint64_t n_owned, void* stream, ad_merged* out, bool union_keys)
+                       uint64_t n_owned, void* stream, ad_merged* out, bool union_keys, MergeTail* defer = nullptr)
 {
     if (!c || !in || !src_parts || !out || n_src == 0 || n_src > 64) return AD_E_INVAL;
     if (union_keys && in->id_format != AD_IDS_RANK)
@@ -4258,14 +4322,6 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     }
     uint64_t bases[12];
     uint32_t err = 0;
-    auto malformed = [&](uint32_t e) {
-        return c->fail(AD_E_INVAL, "ad_parts_merge: malformed parts (%s)",
-                       e & 1  ? "request outside the owned range or bad map" :
-                       e & 2  ? "two parts of one request and map from one source" :
-                       e & 4  ? "keys of different stores overlap or are out of slice order" :
-                       e & 16 ? "id rank outside the global dictionary" :
-                                "ids of a part not sorted and unique");
-    };
     if (n_owned == 0 && !by_request)
         for (DevBuf* b : {&c->m_ko, &c->m_to, &c->m_oo}) HIPCHK(c, hipMemsetAsync(b->p, 0, sizeof(uint64_t) * 3, st));
     if (!by_request)
@@ -4278,7 +4334,7 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
         HIPCHK(c, hipStreamSynchronize(st));
         memcpy(bases, rb, sizeof(bases));
         memcpy(&err, rb + 12, sizeof(err));
-        if (err) return malformed(err);
+        if (err) return merge_malformed(c, err);
         // bases[3*m + k]: offset of map m's first group in array k (m = 3: totals)
         if (!ens<int64_t>(c->m_keys, bases[9]) || !ens<int64_t>(c->m_ids, rank_ids ? (bases[10] + 1) / 2 : 3 * bases[10]) ||
             !ens<int32_t>(c->m_k2t, bases[11]))
@@ -4290,47 +4346,19 @@ static int parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint
     HIPCHK(c, by_request ? run_rmerge_copy(a, c->m_bases.as<uint64_t>(), st)
                          : union_keys ? run_union_emit(a, st) : rank_ids ? run_merge_emit_rank(a, st) : run_merge_emit(a, st));
     HIPCHK(c, hipEventRecord(c->ev[7], st));
+    uint64_t* rb = rb_slot(c);
+    if (!rb) return c->fail(AD_E_NOMEM, "pinned read-back words");
+    // the bases (by request: the device's; else the host's, as the emit used them) and the error word
+    if (by_request) HIPCHK(c, hipMemcpyAsync(rb, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
+    else memcpy(rb, bases, sizeof(bases));
+    HIPCHK(c, hipMemcpyAsync(rb + 12, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
+    const MergeTail t{st, a, by_request, rank_ids, n_owned, txn_base};
+    if (defer)
     {
-        uint64_t* rb = rb_slot(c);
-        if (!rb) return c->fail(AD_E_NOMEM, "pinned read-back words");
-        if (by_request) HIPCHK(c, hipMemcpyAsync(rb, c->m_bases.p, sizeof(bases), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipMemcpyAsync(rb + 12, a.error, sizeof(err), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
-        if (by_request) memcpy(bases, rb, sizeof(bases));
-        memcpy(&err, rb + 12, sizeof(err));
+        *defer = t;
+        return AD_OK;
     }
-    if (err) return malformed(err);
-    float ms = 0;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[6], c->ev[7]));
-    memset(out, 0, sizeof(*out));
-    out->n_txns = n_owned;
-    out->txn_base = txn_base;
-    out->ms_device = ms;
-    out->id_format = rank_ids ? AD_IDS_RANK : AD_IDS_TRIPLET;
-    for (int m = 0; m < 3; ++m)
-    {
-        if (by_request)
-        {
-            // the scan of the size pass is the merged CSR: [k*3 + m][n_owned + 1]
-            out->keys_off[m] = a.goff + (uint64_t)(0 * 3 + m) * (n_owned + 1);
-            out->txn_off[m] = a.goff + (uint64_t)(1 * 3 + m) * (n_owned + 1);
-            out->k2t_off[m] = a.goff + (uint64_t)(2 * 3 + m) * (n_owned + 1);
-        }
-        else
-        {
-            out->keys_off[m] = a.o_keys_off + (uint64_t)m * (n_owned + 1);
-            out->txn_off[m] = a.o_txn_off + (uint64_t)m * (n_owned + 1);
-            out->k2t_off[m] = a.o_k2t_off + (uint64_t)m * (n_owned + 1);
-        }
-        out->keys[m] = a.o_keys + bases[3 * m + 0];
-        out->txns[m] = rank_ids ? reinterpret_cast<int64_t*>(reinterpret_cast<uint32_t*>(a.o_ids) + bases[3 * m + 1])
-                                : a.o_ids + 3 * bases[3 * m + 1];
-        out->k2t[m] = a.o_k2t + bases[3 * m + 2];
-        out->n_keys[m] = (bases[3 * (m + 1) + 0] - bases[3 * m + 0]) / (m == AD_MAP_RANGE ? 2 : 1);
-        out->n_ids[m] = bases[3 * (m + 1) + 1] - bases[3 * m + 1];
-        out->n_k2t[m] = bases[3 * (m + 1) + 2] - bases[3 * m + 2];
-    }
-    return AD_OK;
+    return merge_tail(c, t, out);
 }
 
 int ad_parts_merge(ad_ctx* c, const ad_parts* in, uint32_t n_src, const uint64_t* src_parts, uint64_t txn_base,
@@ -5179,7 +5207,7 @@ static int x_emit(ad_ctx* c, ExportArgs& a, hipStream_t st)
 
 // K3 on c over its receive buffers: sources in slice (= rank / context) order
 static int x_merge(ad_ctx* c, uint32_t n_src, const uint64_t* src_parts, const uint64_t* recv_units, uint32_t fmt,
-                   uint64_t txn_base, uint64_t n_owned, hipStream_t st, ad_merged* out)
+                   uint64_t txn_base, uint64_t n_owned, hipStream_t st, ad_merged* out, MergeTail* defer = nullptr)
 {
     ad_parts in{};
     in.hdr = c->xr_hdr.as<int64_t>();
@@ -5192,7 +5220,7 @@ static int x_merge(ad_ctx* c, uint32_t n_src, const uint64_t* src_parts, const u
     in.n_k2t = recv_units[3];
     in.id_format = fmt;
     for (int a = 0; a < XA; ++a) c->xr_total[a] = recv_units[a];
-    return ad_parts_merge(c, &in, n_src, src_parts, txn_base, n_owned, st, out);
+    return parts_merge(c, &in, n_src, src_parts, txn_base, n_owned, st, out, false, defer);
 }
 
 // an error after the table was agreed: the peers are (or will be) inside the grouped send/recv, so the
@@ -5322,14 +5350,29 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
         }
     }
     const double t2 = now_ms();
-    // 5. K3 on every owner
+    // 5. K3 on every owner. Owners on distinct GPUs: all queued, then each finished (the GPUs merge at once);
+    //    owners sharing a GPU merge one after the other (each merge's device time is then its own)
+    bool distinct = true;
+    for (uint32_t d = 0; d < n && distinct; ++d)
+        for (uint32_t e = 0; e < d && distinct; ++e) distinct = ctxs[d]->device != ctxs[e]->device;
     double ms_merge = 0;
+    std::vector<MergeTail> tails(n);
     for (uint32_t d = 0; d < n; ++d)
     {
         ad_ctx* o = ctxs[d];
         if (hipSetDevice(o->device) != hipSuccess) return o->fail(AD_E_DEVICE, "hipSetDevice");
-        if (int rc = x_merge(o, n, src_parts[d].data(), runits[d].data(), fmt, txn_base[d], n_owned[d], o->stream, &out[d]))
+        if (int rc = x_merge(o, n, src_parts[d].data(), runits[d].data(), fmt, txn_base[d], n_owned[d], o->stream, &out[d],
+                             &tails[d]))
             return rc;
+        if (!distinct)
+        {
+            if (int rc = merge_tail(o, tails[d], &out[d])) return rc;
+            ms_merge += out[d].ms_device;
+        }
+    }
+    for (uint32_t d = 0; d < n && distinct; ++d)
+    {
+        if (int rc = merge_tail(ctxs[d], tails[d], &out[d])) return rc;
         ms_merge += out[d].ms_device;
     }
     if (stats)
