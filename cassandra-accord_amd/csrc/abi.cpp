@@ -1805,10 +1805,17 @@ static hipError_t up_small(ad_ctx* c, int k, void* dst, const void* src, size_t 
     if (!bytes) return hipSuccess;
     if (bytes > sizeof(uint64_t) * UP_WORDS) return h2d(dst, src, bytes, st);
     if (!c->h_up[k])
-    {
-        if (hipError_t e = hipHostMalloc((void**)&c->h_up[k], sizeof(uint64_t) * UP_WORDS, hipHostMallocDefault)) return e;
-        if (hipError_t e = hipEventCreateWithFlags(&c->ev_up[k], hipEventDisableTiming)) return e;
-    }
+        if (hipError_t e = hipHostMalloc((void**)&c->h_up[k], sizeof(uint64_t) * UP_WORDS, hipHostMallocDefault))
+        {
+            c->h_up[k] = nullptr;
+            return e;
+        }
+    if (!c->ev_up[k])
+        if (hipError_t e = hipEventCreateWithFlags(&c->ev_up[k], hipEventDisableTiming))
+        {
+            c->ev_up[k] = nullptr;
+            return e;
+        }
     if (c->up_busy[k])
     {
         if (hipError_t e = hipEventSynchronize(c->ev_up[k])) return e;
