@@ -34,30 +34,38 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak, /opt/skills/guides/MI355X_MI
 STAGES = ["lean resolve pass 1", "deferred requests (split K0..K2)", "prepare (request records: S / self ranks; probe KeyLines for the lean passes)",
           "lean resolve pass 2 (2 requests/wave, 2 emissions/lane)", "offsets scan", "offsets + pack (tile sums, tile scan, scan+pack)",
           "general fused resolve (lean deferrals)"]
-# lean pass 1 of a store without range commands at 2 requests per wave runs the wide path (lean.hip LEAN_WIDE1)
-KERNEL_OF_STAGE = ["k_resolve_lean<2u, false, true, 1>", "k_encode_txn+k_probe_keys+k_scan+k_range+k_build", "k_prepare",
-                   "k_resolve_lean<2u, false, true, 2>", "-", "k_tile_sums+k_tile_scan+k_pack_tiles", "k_resolve"]
-
-
-def kernel_of_stage(i, ranges=False, rpw1=2, wide1=True):
-    """Kernel name (as rocprofv3 reports it, namespace and arguments stripped) of pipeline stage i;
-    the lean kernels are instantiated with range support when the store has range commands, and lean
-    pass 1 runs four or eight requests per wave for batches of small requests (abi.cpp lean_rpw1), at
-    two its wide or narrow kernel (abi.cpp lean_wide1; the batch's stats say which ran)."""
-    k = KERNEL_OF_STAGE[i]
-    if i == 2:
-        return "k_prepare<false>" if ranges else "k_prepare<true>"      # <true>: with the probes' KeyLines
-    if i == 0:
-        # <RPW, RNG, WIDE, PASS>: the wide pass-1 path only at 2 requests per wave without range commands
-        rpw = rpw1 if rpw1 in (4, 8) else 2
-        return "k_resolve_lean<%du, %s, %s, 1>" % (rpw, "true" if ranges else "false",
-                                                    "true" if (rpw == 2 and not ranges and wide1) else "false")
-    if ranges and i == 3:
-        return "k_resolve_lean<1u, true, false, 2>"     # range stores: pass 2 one request per wave
-    return k
 # K1 + K2 of every request (SURVEY §8 a4-a10) run in these stages / kernels: the roofline's "dominant kernel"
 # (k_prepare included since it also resolves every probe's KeyLine for the lean passes)
 RESOLVE_STAGES = [0, 2, 3, 6]
+# the committed profiles the roofline's counter traffic may come from: this round's only (a profile of an older
+# tree may name kernels that no longer run the same way)
+PROFILE_ROUND = "r6"
+
+
+def resolve_kernels(stats, split_ms, min_ms=0.02):
+    """Names (as rocprofv3 reports them, namespace and arguments stripped) of the kernels that ran the resolve
+    stages of this batch, from what the library reports it launched (ad_stats.lean_rpw1 / lean_flags; abi.cpp
+    run_pipeline -> lean.hip run_resolve_lean, resolve.hip run_prepare): never re-derived from the workload's
+    shape. Stages that took under min_ms (e.g. an empty pass 2) are left out."""
+    rpw1 = int(stats.get("lean_rpw1", 0))
+    fl = int(stats.get("lean_flags", 0))
+    rng = bool(fl & A.AD_LEAN_RANGES)
+    names = []
+    if split_ms[2] > min_ms:
+        names.append("k_prepare<true>" if rpw1 and not rng else "k_prepare<false>")
+    if rpw1:
+        wide = bool(fl & A.AD_LEAN_WIDE1)
+        names.append("k_resolve_lean<%du, %s, %s, 1>" % (rpw1, "true" if rng else "false", "true" if wide else "false"))
+        if fl & A.AD_LEAN_PASS2 and split_ms[3] > min_ms:
+            if rng:
+                names.append("k_resolve_lean<2u, true, false, 2>" if rpw1 == 4 else "k_resolve_lean<1u, true, false, 2>")
+            else:
+                names.append("k_resolve_lean<2u, false, true, 2>")
+        if split_ms[6] > min_ms:
+            names.append("k_resolve")
+    elif split_ms[0] > min_ms:
+        names.append("k_resolve")
+    return names
 
 
 # device of the small timing / count reductions: the GPU under RCCL, the host under gloo
@@ -73,12 +81,13 @@ def log(*a):
 
 
 def measured_traffic(kernels, tag=None):
-    """HBM bytes per launch summed over `kernels` from the newest committed PMC summary under
-    profiles/ that has all of them (FETCH_SIZE doubled for gfx950 as MI355X_MICROARCH.md
-    prescribes, + WRITE_SIZE; scripts/summarize_prof.py), or (None, None). With `tag`, only
-    summaries whose name holds it (the profile of the same workload: "config2", "config3")."""
+    """HBM bytes per launch summed over `kernels` from the newest committed PMC summary of this round
+    (profiles/<PROFILE_ROUND>*_pmc.json, by name) that holds every one of them (FETCH_SIZE doubled for gfx950 as
+    MI355X_MICROARCH.md prescribes, + WRITE_SIZE; scripts/summarize_prof.py). With `tag`, only summaries whose name
+    holds it (the profile of the same workload: "config2", "config4", "mix"). Without such a profile: (None, a
+    note naming what is missing) and a warning on stderr -- never an older round's profile of other kernels."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))   # by name: rN_vM order (checkout mtimes are arbitrary)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", PROFILE_ROUND + "*_pmc.json")))
     if tag is not None:
         files = [f for f in files if tag in os.path.basename(f)]
     for f in reversed(files):
@@ -87,7 +96,9 @@ def measured_traffic(kernels, tag=None):
         if all(k in d and d[k].get("fetch_bytes_per_launch") is not None for k in kernels):
             tot = sum(2 * d[k]["fetch_bytes_per_launch"] + (d[k].get("write_bytes_per_launch") or 0) for k in kernels)
             return tot, os.path.relpath(f, ROOT)
-    return None, None
+    note = "missing: no %s profile%s holds %s" % (PROFILE_ROUND, " of " + tag if tag else "", " + ".join(kernels))
+    log("WARNING: roofline traffic unmeasured (%s)" % note)
+    return None, note
 
 
 def measured_traffic_per_step(kernels, tag, unit_kernel):
@@ -98,7 +109,7 @@ def measured_traffic_per_step(kernels, tag, unit_kernel):
     such a profile."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*%s*_pmc.json" % tag)))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "%s*%s*_pmc.json" % (PROFILE_ROUND, tag))))
     for f in reversed(files):
         stats = f[:-len("_pmc.json")] + "_kernel_stats.csv"
         if not os.path.exists(stats):
@@ -119,7 +130,9 @@ def measured_traffic_per_step(kernels, tag, unit_kernel):
                 per = 2 * d[k]["fetch_bytes_per_launch"] + (d[k].get("write_bytes_per_launch") or 0)
                 tot += per * calls[k] / calls[unit_kernel]
         return tot, os.path.relpath(f, ROOT)
-    return None, None
+    note = "missing: no %s profile of %s" % (PROFILE_ROUND, tag)
+    log("WARNING: roofline traffic unmeasured (%s)" % note)
+    return None, note
 
 
 def stage_bytes(w, stats):
@@ -462,7 +475,7 @@ def bench_ranges(args, rank, world, local, dev):
     alg = 16 * n_rent + 40 * len(w.queries) + out_bytes
     res_ms = float(sum(ms[i] for i in RESOLVE_STAGES))
     achieved = alg / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
-    res_kernels = [kernel_of_stage(i, ranges=True) for i in RESOLVE_STAGES if split_ms[i] > 0.02]
+    res_kernels = resolve_kernels(stats, split_ms)
     traffic, src = measured_traffic(res_kernels, "config4")
     res = {
         "metric": METRIC, "value": pairs / (ms_per_step / 1000.0), "unit": "txn-key pairs/s", "n_gpus": world,
@@ -1232,10 +1245,7 @@ def bench_deps(args, rank, world, local, dev):
     sbytes = stage_bytes(w, stats)
     res_ms = float(sum(stage_ms[i] for i in RESOLVE_STAGES))
     achieved = sbytes[0] / (res_ms / 1000.0) / 1e9 if res_ms > 0 else 0.0
-    nq = max(1, len(w.queries))
-    lean_rpw1 = 4 if w.queries.n_probes <= 3 * nq else 2
-    res_kernels = [kernel_of_stage(i, rpw1=lean_rpw1, wide1=bool(stats.get("lean_wide1", True)))
-                   for i in RESOLVE_STAGES if split_ms[i] > 0.02]
+    res_kernels = resolve_kernels(stats, split_ms)
     traffic, traffic_src = measured_traffic(res_kernels, "mix" if mix else "config%d" % cfg)   # the same workload's profile
     xdesc = ""
     if world > 1:

@@ -108,7 +108,11 @@ class AdStats(C.Structure):
                 ("ms_device", C.c_double), ("ms_ingest", C.c_double),
                 ("ms_stage", C.c_double * 8), ("n_deferred", C.c_uint64), ("bytes_stage", C.c_uint64 * 8),
                 ("n_levels", C.c_uint64), ("n_edges", C.c_uint64), ("n_launches", C.c_uint64),
-                ("n_deferred_lean", C.c_uint64), ("n_lean_pass2", C.c_uint64)]
+                ("n_deferred_lean", C.c_uint64), ("n_lean_pass2", C.c_uint64),
+                ("lean_rpw1", C.c_uint32), ("lean_flags", C.c_uint32)]
+
+
+AD_LEAN_WIDE1, AD_LEAN_RANGES, AD_LEAN_PASS2 = 1, 2, 4
 
 
 class AdDepsResult(C.Structure):

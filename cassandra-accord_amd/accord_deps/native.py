@@ -203,7 +203,7 @@ def _view(p, n, dtype):
 def stats_dict(s):
     return dict(n_txns=s.n_txns, n_probes=s.n_probes, n_pairs=list(s.n_pairs), n_unique=list(s.n_unique),
                 n_keys=list(s.n_keys), n_deferred=s.n_deferred, n_deferred_lean=s.n_deferred_lean, n_lean_pass2=s.n_lean_pass2,
-                lean_wide1=bool(s.n_launches),
+                lean_wide1=bool(s.n_launches), lean_rpw1=int(s.lean_rpw1), lean_flags=int(s.lean_flags),
                 ms_device=s.ms_device, ms_ingest=s.ms_ingest, ms_stage=list(s.ms_stage)[:7],
                 bytes_stage=list(s.bytes_stage)[:7])
 

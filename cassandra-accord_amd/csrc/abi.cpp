@@ -1823,7 +1823,12 @@ static hipError_t up_small(ad_ctx* c, int k, void* dst, const void* src, size_t 
     }
     memcpy(c->h_up[k], src, bytes);
     if (hipError_t e = hipMemcpyAsync(dst, c->h_up[k], bytes, hipMemcpyHostToDevice, st)) return e;
-    if (hipError_t e = hipEventRecord(c->ev_up[k], st)) return e;
+    if (hipError_t e = hipEventRecord(c->ev_up[k], st))
+    {
+        // the copy may be queued with no event covering it: the slot is free only once the stream is done
+        (void)hipStreamSynchronize(st);
+        return e;
+    }
     c->up_busy[k] = true;
     return hipSuccess;
 }
@@ -2103,6 +2108,7 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         uint64_t nd = 0;
         int rc;
         bool lean_track = false;    // this batch's lean pass 1 feeds lean_wide1_update
+        uint32_t lean_rpw = 0, lean_fl = 0;   // the lean kernels that ran (ad_stats.lean_rpw1 / lean_flags)
         // the fused path's stage split (prepare, lean pass 1, pass 2, general kernel) costs three more
         // event records (~4 us of idle GPU each); without AD_STAGE_EVENTS=1 stage 0 holds the whole resolve
         const char* se = getenv("AD_STAGE_EVENTS");
@@ -2142,6 +2148,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
                     const bool wide1 = rpw1 == 2 && !c->ds.n_rent && lean_wide1(c);
                     c->lean_ran_wide = wide1;
                     lean_track = rpw1 == 2 && !c->ds.n_rent;
+                    lean_rpw = rpw1;
+                    lean_fl = (wide1 ? AD_LEAN_WIDE1 : 0u) | (c->ds.n_rent ? AD_LEAN_RANGES : 0u) | (wide1 ? 0u : AD_LEAN_PASS2);
                     HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
                     if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
                     // after a wide pass 1 the pass-2 list is empty (it serves what pass 2 would, up to 64 raw
@@ -2302,6 +2310,8 @@ static int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_dep
         S.n_deferred_lean = lean ? h.n_real2 : 0;     // requests the lean passes left to the general kernel
         S.n_lean_pass2 = lean ? h.n_real1 : 0;        // requests lean pass 1 left to pass 2
         S.n_launches = lean_track && c->lean_ran_wide ? 1 : 0;   // lean pass 1 ran its wide kernel
+        S.lean_rpw1 = lean_rpw;
+        S.lean_flags = lean_fl;
         if (lean_track) lean_wide1_update(c, n, h);
         for (int m = 0; m < 3; ++m)
         {
@@ -4784,6 +4794,8 @@ static int dmiss_enable(ad_ctx* c, hipStream_t st)
     return 0;
 }
 
+static int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st);
+
 static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats)
 {
     StreamScope scope_(st, c->stream, c->cstream);
@@ -4819,7 +4831,6 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
                        c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
                        c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
     if (int rc = host_dict(c)) return rc;
-    const uint64_t nd0 = c->dict_msb.size();
     CfkMiss miss;
     miss.on = c->dmiss_on && u.dep_off;
     miss.n_lists = c->dmiss_lists;
@@ -4830,6 +4841,67 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
     miss.swap = cfk_miss_swap;
     c->lp_upd.clear(); c->lp_keys.clear(); c->lp_msb.clear(); c->lp_lsb.clear(); c->lp_node.clear();
     const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e, &miss);
+    // what the batch left is known here, before any follow-up copy can fail: a caller reading the status after
+    // an error must never take a batch that stands for one that did not (and apply it twice)
+    c->upd_applied = rc == AD_OK || o.batch_stood;
+    c->upd_failed = o.failed_update;
+    if (const int frc = cfk_update_follow(c, o, rc, st))
+    {
+        // the host copies and the derived arrays may be half refreshed: rebuilt from the entries at the next use
+        c->host_stale = true;
+        c->dirty = true;
+        if (c->upd_applied) return c->fail(AD_E_PARTIAL, "explicit updates applied, their follow-up failed: %s", c->err.c_str());
+        return frc;
+    }
+    if (rc && o.batch_stood)
+    {
+        // the explicit batch stands but what follows it (additions, missing() lists) failed: the entries
+        // changed, the device lists are not this batch's -- the host copies follow on demand and the
+        // lists ask for a reload (as after a batch without deps)
+        c->host_stale = true;
+        ++c->snap_gen;
+        if (c->dmiss_on)
+        {
+            c->dmiss_on = false;
+            c->cfk.miss_stale = true;
+        }
+    }
+    if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back && !o.rederived && !o.batch_stood)
+    {
+        // the derived arrays may be half built: rebuild them from the entries at the next use
+        c->host_stale = true;
+        c->dirty = true;
+    }
+    // a failure after the explicit batch stood is AD_E_PARTIAL: a caller must not take it for "nothing
+    // applied" and retry the batch
+    if (rc && o.batch_stood) return c->fail(AD_E_PARTIAL, "explicit updates applied, deps-derived part failed: %s", e.c_str());
+    if (rc) return c->fail(rc, "%s", e.c_str());
+    if (u.n)
+    {
+        c->host_stale = true;
+        ++c->snap_gen;            // device views built from the host state (recovery) are stale
+    }
+    if (n_applied) *n_applied = o.n_applied;
+    if (stats)
+    {
+        *stats = ad_stats{};
+        stats->n_txns = u.n;
+        stats->ms_device = o.ms_total;
+        stats->ms_stage[0] = o.ms_locate;
+        stats->ms_stage[1] = o.ms_derive;
+        stats->n_keys[0] = o.n_inserted;         // entries inserted
+        stats->n_keys[1] = o.n_new_ids;          // ids appended to the dictionary
+        stats->n_keys[2] = o.n_additions;        // TRANSITIVELY_KNOWN entries from deps
+    }
+    return AD_OK;
+}
+
+// The host-side follow-up of an update batch (run_cfk_update returned rc): the LoadPruned hand-back, the
+// KeyLine hash of new keys, the host dictionary after a merge or an append, the sampled dictionary index and
+// the KeyLines. Nonzero: a device failure (the message is set).
+static int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st)
+{
+    const uint64_t nd0 = c->dict_msb.size();
     if (rc == AD_OK && o.n_load_pruned)
     {
         const uint64_t m = o.n_load_pruned;
@@ -4887,53 +4959,14 @@ static int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t
     if ((rc == 0 || o.rolled_back || o.rederived || o.batch_stood) && c->kline_slots)
         HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
                                    c->kline_slots, st));
-    if (rc && o.batch_stood)
-    {
-        // the explicit batch stands but what follows it (additions, missing() lists) failed: the entries
-        // changed, the device lists are not this batch's -- the host copies follow on demand and the
-        // lists ask for a reload (as after a batch without deps)
-        c->host_stale = true;
-        ++c->snap_gen;
-        if (c->dmiss_on)
-        {
-            c->dmiss_on = false;
-            c->cfk.miss_stale = true;
-        }
-    }
-    if ((rc == AD_E_NOMEM || rc == AD_E_DEVICE) && !o.rolled_back && !o.rederived && !o.batch_stood)
-    {
-        // the derived arrays may be half built: rebuild them from the entries at the next use
-        c->host_stale = true;
-        c->dirty = true;
-    }
-    c->upd_applied = rc == AD_OK || o.batch_stood;
-    c->upd_failed = o.failed_update;
-    // a failure after the explicit batch stood is AD_E_PARTIAL: a caller must not take it for "nothing
-    // applied" and retry the batch
-    if (rc && o.batch_stood) return c->fail(AD_E_PARTIAL, "explicit updates applied, deps-derived part failed: %s", e.c_str());
-    if (rc) return c->fail(rc, "%s", e.c_str());
-    if (u.n)
-    {
-        c->host_stale = true;
-        ++c->snap_gen;            // device views built from the host state (recovery) are stale
-    }
-    if (n_applied) *n_applied = o.n_applied;
-    if (stats)
-    {
-        *stats = ad_stats{};
-        stats->n_txns = u.n;
-        stats->ms_device = o.ms_total;
-        stats->ms_stage[0] = o.ms_locate;
-        stats->ms_stage[1] = o.ms_derive;
-        stats->n_keys[0] = o.n_inserted;         // entries inserted
-        stats->n_keys[1] = o.n_new_ids;          // ids appended to the dictionary
-        stats->n_keys[2] = o.n_additions;        // TRANSITIVELY_KNOWN entries from deps
-    }
-    return AD_OK;
+    return 0;
 }
 
 static int check_update_soa(ad_ctx* c, const ad_cfk_update_soa* u)
 {
+    // the status describes this call from here on, whatever rejects it below (ad_cfk_update_status)
+    c->upd_applied = false;
+    c->upd_failed = -1;
     if (!u) return c->fail(AD_E_INVAL, "null update batch");
     if (u->n && (!u->keys || !u->txn_msb || !u->txn_lsb || !u->txn_node || !u->exec_msb || !u->exec_lsb ||
                  !u->exec_node || !u->status))
@@ -5267,6 +5300,10 @@ int ad_exchange_plan(const uint64_t* table, uint32_t world, uint32_t rank, ad_xf
     return x_plan(table, world, rank, xfers, recv_units, src_parts, flags, &bad);
 }
 
+static int exchange_local_run(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* const* res, const int64_t* const* txn_index,
+                              const uint64_t* const* dest_first, const uint64_t* txn_base, const uint64_t* n_owned,
+                              ad_merged* out, ad_exchange_stats* stats);
+
 int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* const* res, const int64_t* const* txn_index,
                       const uint64_t* const* dest_first, const uint64_t* txn_base, const uint64_t* n_owned,
                       ad_merged* out, ad_exchange_stats* stats)
@@ -5274,6 +5311,22 @@ int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* con
     if (!ctxs || n == 0 || !res || !txn_index || !dest_first || !txn_base || !n_owned || !out) return AD_E_INVAL;
     for (uint32_t i = 0; i < n; ++i)
         if (!ctxs[i] || !res[i]) return AD_E_INVAL;
+    const int rc = exchange_local_run(ctxs, n, res, txn_index, dest_first, txn_base, n_owned, out, stats);
+    if (rc)
+    {
+        // whatever an earlier store or owner had queued (exports, copies, merges, pinned read-backs) completes
+        // before the call returns, and no owner's result looks valid
+        for (uint32_t i = 0; i < n; ++i)
+            if (hipSetDevice(ctxs[i]->device) == hipSuccess) (void)hipStreamSynchronize(ctxs[i]->stream);
+        for (uint32_t i = 0; i < n; ++i) out[i] = ad_merged{};
+    }
+    return rc;
+}
+
+static int exchange_local_run(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* const* res, const int64_t* const* txn_index,
+                              const uint64_t* const* dest_first, const uint64_t* txn_base, const uint64_t* n_owned,
+                              ad_merged* out, ad_exchange_stats* stats)
+{
     const uint32_t fmt = x_format(ctxs[0]);
     for (uint32_t i = 1; i < n; ++i)
         if (x_format(ctxs[i]) != fmt)

@@ -190,9 +190,19 @@ struct StagingLease {
             s = nullptr;
         }
     }
+    // The pair goes back to the pool with nothing in flight, on every exit of a transfer, errors included: its
+    // events were recorded on the caller's stream, which a context may destroy before the pair's next user would
+    // wait on them (round 5 saw one "stream is capturing" error from a staged upload on a fresh context, DESIGN
+    // §7). A transfer that failed between queuing a copy and recording its event (st_dirty) leaves a copy the
+    // events do not cover: its stream is synchronised instead.
+    hipStream_t st = nullptr;
+    bool st_dirty = false;
     ~StagingLease()
     {
         if (!s) return;
+        (void)s->wait(0);
+        (void)s->wait(1);
+        if (st_dirty) (void)hipStreamSynchronize(st);
         std::lock_guard<std::mutex> g(g_stage_pool[d].mu);
         g_stage_pool[d].free.push_back(s);
     }
@@ -376,6 +386,7 @@ hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t st)
     if (host_pinned(src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
     StagingLease lease;
     if (!lease.s) return hipErrorOutOfMemory;
+    lease.st = st;
     Staging& S = *lease.s;
     int k = 0;
     for (size_t off = 0; off < bytes; off += STAGE, k ^= 1)
@@ -384,13 +395,13 @@ hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t st)
         hipError_t e = S.wait(k);
         if (e != hipSuccess) return e;
         stage_copy(S.buf[k], (const char*)src + off, n);
+        lease.st_dirty = true;          // until the chunk's event covers its copy
         if ((e = hipMemcpyAsync((char*)dst + off, S.buf[k], n, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
         if ((e = hipEventRecord(S.ev[k], st)) != hipSuccess) return e;
         S.busy[k] = true;
+        lease.st_dirty = false;
     }
-    // the pair goes back to the pool with nothing in flight: its events were recorded on the caller's stream,
-    // which a context may destroy before the pair's next user would wait on them (round 5 saw one "stream is
-    // capturing" error from a staged upload on a fresh context)
+    // drained here (not only by the lease) so that a failed copy is reported by this call
     hipError_t e = S.wait(0);
     const hipError_t e1 = S.wait(1);
     return e != hipSuccess ? e : e1;
@@ -402,6 +413,7 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st)
     if (host_pinned(dst)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
     StagingLease lease;
     if (!lease.s) return hipErrorOutOfMemory;
+    lease.st = st;
     Staging& S = *lease.s;
     // chunk i is copied to the host while chunk i + 1 is in flight
     size_t prev_off = 0, prev_n = 0;
@@ -411,9 +423,11 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st)
     {
         const size_t n = std::min(STAGE, bytes - off);
         if ((e = S.wait(k)) != hipSuccess) return e;
+        lease.st_dirty = true;          // until the chunk's event covers its copy
         if ((e = hipMemcpyAsync(S.buf[k], (const char*)src + off, n, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipEventRecord(S.ev[k], st)) != hipSuccess) return e;
         S.busy[k] = true;
+        lease.st_dirty = false;
         if (prev_n)
         {
             if ((e = S.wait(k ^ 1)) != hipSuccess) return e;

@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define AD_ABI_VERSION 4
+#define AD_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define AD_OK                  0
@@ -238,7 +238,14 @@ typedef struct ad_stats {
                                       * ran its wide kernel (up to 64 raw emissions per request) */
     uint64_t n_deferred_lean;        /* ad_deps_batch*: requests the lean passes handed to the general kernel */
     uint64_t n_lean_pass2;           /* ad_deps_batch*: requests lean pass 1 handed to lean pass 2     */
+    /* ad_deps_batch*: which lean kernels ran (so a profile can be matched to the batch exactly):
+     * requests per wave of lean pass 1 (0: the lean passes did not run) and AD_LEAN_* flags */
+    uint32_t lean_rpw1;
+    uint32_t lean_flags;
 } ad_stats;
+#define AD_LEAN_WIDE1  1u   /* lean pass 1 ran its wide kernel (up to 64 raw emissions per request)     */
+#define AD_LEAN_RANGES 2u   /* the lean kernels' range-command instantiation (store with range commands) */
+#define AD_LEAN_PASS2  4u   /* lean pass 2 was launched                                                 */
 
 /* Results, one CSR triple per map and request, packed in request order.
  * For request i and map m:
@@ -443,7 +450,8 @@ typedef struct ad_exchange_stats {
 
 /* One process driving every store of the node (the Java host: one process, a CommandStore per thread,
  * one GPU each -- or several stores on one GPU): device copies, hipMemcpyPeerAsync over xGMI between
- * GPUs. ctxs[s], res[s], txn_index[s], dest_first[s] per store; out[n]. */
+ * GPUs. ctxs[s], res[s], txn_index[s], dest_first[s] per store; out[n]. On an error every store's stream is
+ * synchronised before the call returns (nothing it queued is left running) and every out[] is zeroed. */
 int ad_exchange_local(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* const* res, const int64_t* const* txn_index,
                       const uint64_t* const* dest_first, const uint64_t* txn_base, const uint64_t* n_owned,
                       ad_merged* out, ad_exchange_stats* stats);

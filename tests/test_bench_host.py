@@ -44,3 +44,26 @@ def test_request_mix_invariants(oracle):
         ks, ke, t, k2t = r.maps[A.AD_MAP_KEY].request(int(i))
         keys, vals, k2 = refmodel.csr(kd)
         assert ([int(x) for x in ks], t.tuples(), [int(x) for x in k2t]) == (keys, vals, k2)
+
+
+def test_resolve_kernels_follow_the_library_stats():
+    """bench.py names the roofline's kernels from what the library reports it launched (ad_stats.lean_rpw1 /
+    lean_flags), never from the workload's shape (a 4-key batch was labelled with the 2-request
+    kernels)."""
+    split = [0.5, 0.0, 0.07, 0.1, 0.0, 0.03, 0.2]
+    st = dict(lean_rpw1=4, lean_flags=A.AD_LEAN_RANGES | A.AD_LEAN_PASS2)
+    assert bench.resolve_kernels(st, split) == ["k_prepare<false>", "k_resolve_lean<4u, true, false, 1>",
+                                                "k_resolve_lean<2u, true, false, 2>", "k_resolve"]
+    st = dict(lean_rpw1=2, lean_flags=A.AD_LEAN_WIDE1)
+    assert bench.resolve_kernels(st, split) == ["k_prepare<true>", "k_resolve_lean<2u, false, true, 1>", "k_resolve"]
+    st = dict(lean_rpw1=4, lean_flags=A.AD_LEAN_PASS2)
+    assert bench.resolve_kernels(st, [0.5, 0, 0.07, 0.01, 0, 0.03, 0.0]) == ["k_prepare<true>",
+                                                                              "k_resolve_lean<4u, false, false, 1>"]
+    # no lean pass (a store with RedundantBefore entries): the general kernel alone
+    assert bench.resolve_kernels(dict(lean_rpw1=0, lean_flags=0), [0.9, 0, 0.07, 0, 0, 0.03, 0]) == \
+        ["k_prepare<false>", "k_resolve"]
+
+
+def test_measured_traffic_never_falls_back_to_an_older_round():
+    t, src = bench.measured_traffic(["k_no_such_kernel<1>"], "config2")
+    assert t is None and src.startswith("missing")
