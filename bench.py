@@ -360,7 +360,7 @@ def bench_levels(args, rank, world, local, dev):
     else:
         names = ["k5 build (exec radix sort + key chains + successor CSR)", "k5 frontier loop (k_level_step)"]
     achieved = stats["bytes_stage"][dom] / (ms[dom] / 1000.0) / 1e9 if ms[dom] > 0 else 0.0
-    lk = "k_level_rec<false>" if packed else ("k_level_pull<false>" if pull else "k_level_step")
+    lk = "k_level_rec" if packed else ("k_level_pull" if pull else "k_level_step")
     if dom == 1:
         traffic, traffic_src = measured_traffic([lk], tag="config5")
     else:

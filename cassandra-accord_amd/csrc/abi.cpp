@@ -1500,17 +1500,8 @@ int run_split(ad_ctx* c, const BatchBufs& b, hipStream_t st)
 }
 
 // requests per wave of lean pass 1 by the batch's keys per request (lean_rpw1): four up to 4.5 keys on
-// average, else two; AD_LEAN_RPW overrides (8: opt-in, measured no faster on a store's share of
-// requests spanning many stores).
-// Lean pass 1 as gather + build (k_lean_gather, k_lean_build): opt-in, AD_LEAN_GB=1. Measured on config 2
-// (DESIGN §4): gather 0.19-0.30 ms + build 0.36 + wide build 0.15 against 0.54 ms for the fused pass -- the
-// build alone is issue-bound (its SIMDs ~98 % busy at ~390 VALU per two requests), so the split buys no
-// latency hiding the fused pass lacks
-bool lean_gb_on()
-{
-    const char* e = getenv("AD_LEAN_GB");
-    return e && atoi(e) != 0;
-}
+// average, else two; AD_LEAN_RPW overrides (tests: every width on any batch; 8 measured no faster on a
+// store's share of requests spanning many stores).
 
 uint32_t lean_rpw1(uint64_t n, uint64_t np)
 {
@@ -1668,20 +1659,6 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
     {
         if (!ens<uint32_t>(c->p_slot, std::max<uint64_t>(np, 1))) return c->fail(AD_E_NOMEM, "probe slots");
         b.p_slot = c->p_slot.as<uint32_t>();
-        b.slots_by_prepare = getenv("AD_SLOTS_KERNEL") == nullptr;     // measurement switch: the separate launch
-    }
-    // lean pass 1 as gather + build (two requests per build wave, no range commands): AD_LEAN_GB=0 keeps
-    // the single fused pass
-    const bool gb = lean && !c->ds.n_rent && lean_rpw1(n, np) == 2 && lean_gb_on();
-    if (gb)
-    {
-        if (!ens<uint32_t>(c->lg_stage, n * 64) || !ens<uint4>(c->lg_rec, n) || !ens<int64_t>(c->lg_keys, n * 8) ||
-            !ens<uint64_t>(c->lg_dummy, (uint64_t)device_cu_count() * 64 * 16))
-            return c->fail(AD_E_NOMEM, "lean stage");
-        b.lg_dummy = c->lg_dummy.as<uint64_t>();
-        b.lg_stage = c->lg_stage.as<uint32_t>();
-        b.lg_rec = c->lg_rec.as<uint4>();
-        b.lg_keys = c->lg_keys.as<int64_t>();
     }
     if (const char* e = getenv("AD_K2_BIG")) b.k2_big = (uint32_t)strtoul(e, nullptr, 10);   // tests: force k_build_big
     b.q_rec = c->q_rec.as<uint4>();
@@ -1764,36 +1741,23 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
                 // takes only what it deferred (count read on the device, no host round trip)
                 if (!c->ev_lean1) HIPCHK(c, timing_event(&c->ev_lean1));
                 const uint32_t rpw1 = lean_rpw1(n, np);
-                if (gb)
-                {
-                    // gather + build (k_lean_gather, k_lean_build): the rest to the general kernel
-                    HIPCHK(c, run_lean_gb(c->ds, b, st));
-                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
-                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
-                }
-                else
-                {
-                    const bool wide1 = rpw1 == 2 && !c->ds.n_rent && lean_wide1(c);
-                    c->lean_ran_wide = wide1;
-                    lean_track = rpw1 == 2 && !c->ds.n_rent;
-                    lean_rpw = rpw1;
-                    lean_fl = (wide1 ? AD_LEAN_WIDE1 : 0u) | (c->ds.n_rent ? AD_LEAN_RANGES : 0u) | (wide1 ? 0u : AD_LEAN_PASS2);
-                    HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
-                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
-                    // after a wide pass 1 the pass-2 list is empty (it serves what pass 2 would, up to 64 raw
-                    // emissions, and hands the rest straight to the general kernel): no launch
-                    if (!wide1) HIPCHK(c, run_resolve_lean(c->ds, b, 2, rpw1, false, st));
-                    if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
-                }
-                if (getenv("AD_DEFER_SPLIT"))
-                    HIPCHK(c, run_defer_append(b, st));
-                else
-                {
-                    BatchBufs b2 = b;
-                    b2.req_list = b.deferred2;
-                    b2.req_count = &b.ctl->n_deferred2;
-                    HIPCHK(c, run_resolve(c->ds, b2, st));
-                }
+                const bool wide1 = rpw1 == 2 && !c->ds.n_rent && lean_wide1(c);
+                c->lean_ran_wide = wide1;
+                lean_track = rpw1 == 2 && !c->ds.n_rent;
+                lean_rpw = rpw1;
+                lean_fl = (wide1 ? AD_LEAN_WIDE1 : 0u) | (c->ds.n_rent ? AD_LEAN_RANGES : 0u) | (wide1 ? 0u : AD_LEAN_PASS2);
+                HIPCHK(c, run_resolve_lean(c->ds, b, 1, rpw1, wide1, st));
+                if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean1, st));
+                // after a wide pass 1 the pass-2 list is empty (it serves what pass 2 would, up to 64 raw
+                // emissions, and hands the rest straight to the general kernel): no launch
+                if (!wide1) HIPCHK(c, run_resolve_lean(c->ds, b, 2, rpw1, false, st));
+                if (split_stages) HIPCHK(c, hipEventRecord(c->ev_lean, st));
+                // the general fused kernel on what both lean passes deferred (routing them to the split kernels
+                // instead measured 1.94 ms for the request mix against 0.98)
+                BatchBufs b2 = b;
+                b2.req_list = b.deferred2;
+                b2.req_count = &b.ctl->n_deferred2;
+                HIPCHK(c, run_resolve(c->ds, b2, st));
             }
             else
                 HIPCHK(c, run_resolve(c->ds, b, st));

@@ -201,7 +201,6 @@ struct ad_ctx {
     // batch buffers
     DevBuf q_tm, q_tl, q_tn, q_em, q_el, q_en, q_me, q_ko, q_k;
     DevBuf q_ro, q_rs, q_re;                   // Range-domain requests: staged ranges
-    DevBuf lg_stage, lg_rec, lg_keys, lg_dummy;   // lean gather + build: staged emissions, build records, keys
     bool upd_applied = false;                  // ad_cfk_update_status: the last update batch stands
     int64_t upd_failed = -1;                   //   and the update its failure names
     DevBuf rq_cnt, rq_off, rq_err, rq_bsum, rq_keys, rq_hi, rq_kind, rq_list;   // their expansion into probes
@@ -209,7 +208,7 @@ struct ad_ctx {
         DevBuf t_S, t_self, t_kinds, t_epoch, p_txn, p_rec, p_off, p_c0, p_c1, p_roff, p_rcnt, p_rb, sz, t_reg;
     } split, sub;
     DevBuf s_tm, s_tl, s_tn, s_em, s_el, s_en, s_me, s_ko, s_k, s_cnt, s_khi, s_kind;   // deferred sub-batch inputs
-    DevBuf p_slot;                             // lean passes: per probe its KeyLine (k_lean_slots)
+    DevBuf p_slot;                             // lean passes: per probe its KeyLine (k_prepare)
     DevBuf arena, rarena;
     DevBuf sz, off, bsum, t_reg, reg, scratch, ctl, deferred, deferred1, deferred2, q_rec, big;
     DevBuf o_keys[3], o_txns[3], o_k2t[3];

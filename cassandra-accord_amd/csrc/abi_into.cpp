@@ -445,8 +445,7 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
             (cap[3 * m + 1] && !out->txns[m]) || (cap[3 * m + 2] && !out->k2t[m]))
             return c->fail(AD_E_INVAL, "ad_deps_batch_into: output arrays missing for map %d", m);
     // key-only SNAPSHOT batches take the pipelined path (its staging pass checks the keys)
-    const bool fast = !(flags & AD_SEQUENTIAL) && !(n && q->range_off && q->range_off[n] > q->range_off[0]) &&
-                      getenv("AD_INTO_LEGACY") == nullptr;
+    const bool fast = !(flags & AD_SEQUENTIAL) && !(n && q->range_off && q->range_off[n] > q->range_off[0]);
     int rc = fast ? 0 : check_query_host(c, q, flags);
     if (rc) return rc;
     if (flags & AD_SEQUENTIAL)

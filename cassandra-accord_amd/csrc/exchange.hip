@@ -88,216 +88,11 @@ __device__ __forceinline__ PartBase part_base(const ExportArgs& a, uint64_t r)
     return b;
 }
 
-// Load-balanced export: a block takes XT_REQ consecutive requests, lists their parts (non-empty
-// maps) in LDS with source and destination offsets, writes the headers, then streams the parts'
-// key words, ids and keysToTxnIds thread per element (binary search of the owning part in LDS).
-constexpr uint32_t XT_REQ = 128;                 // requests per block (threads)
-constexpr uint32_t XT_PARTS = 3 * XT_REQ;
-
-struct XtLds {
-    uint64_t ksrc[XT_PARTS], isrc[XT_PARTS], osrc[XT_PARTS];   // element offsets of the part's source
-    uint64_t kdst[XT_PARTS], idst[XT_PARTS], odst[XT_PARTS];   // and of its destination
-    uint32_t kpre[XT_PARTS + 1], ipre[XT_PARTS + 1], opre[XT_PARTS + 1];
-    uint32_t nk[XT_PARTS];
-    uint8_t map[XT_PARTS];
-    uint8_t self[XT_PARTS];                                    // kept part: written to the receive arrays
-    uint32_t cnt[XT_REQ / 64 + 1];
-    uint64_t wsum[3][XT_REQ / 64 + 1];
-};
-
-// exclusive scans of three per-thread values over the XT_REQ threads of the block
-__device__ __forceinline__ void xt_scan3(uint32_t v[3], uint32_t ex[3], uint32_t tot[3], uint64_t (*wsum)[XT_REQ / 64 + 1])
-{
-    const int l = lane_id(), w = threadIdx.x >> 6;
-    uint32_t inc[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-    {
-        inc[k] = v[k];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1)
-        {
-            const uint32_t t = __shfl_up(inc[k], d, 64);
-            if (l >= d) inc[k] += t;
-        }
-        if (l == 63) wsum[k][w] = inc[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-    {
-        uint32_t before = 0, all = 0;
-        for (int j = 0; j < (int)(XT_REQ / 64); ++j)
-        {
-            const uint32_t x = (uint32_t)wsum[k][j];
-            if (j < w) before += x;
-            all += x;
-        }
-        ex[k] = inc[k] - v[k] + before;
-        tot[k] = all;
-    }
-    __syncthreads();
-}
-
-__device__ __forceinline__ uint32_t xt_owner(const uint32_t* pre, uint32_t np, uint32_t e)
-{
-    uint32_t lo = 0, hi = np;
-    while (hi - lo > 1)
-    {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= e) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
-__global__ void __launch_bounds__(XT_REQ) k_export_tiles(ExportArgs a)
-{
-    __shared__ XtLds L;
-    const uint32_t t = threadIdx.x;
-    const uint64_t r = (uint64_t)blockIdx.x * XT_REQ + t;
-    const bool live_r = r < a.n;
-    // this request's maps: sizes, source offsets, and its first part / key word / id / k2t in the output
-    uint32_t nk[3] = {0, 0, 0}, nt[3] = {0, 0, 0}, no[3] = {0, 0, 0};
-    uint64_t k0[3] = {0, 0, 0}, t0[3] = {0, 0, 0}, o0[3] = {0, 0, 0};
-    PartBase pb{0, 0, 0, 0};
-    if (live_r)
-    {
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-        {
-            k0[m] = a.keys_off[m][r];
-            nk[m] = (uint32_t)(a.keys_off[m][r + 1] - k0[m]);
-            t0[m] = a.txn_off[m][r];
-            nt[m] = (uint32_t)(a.txn_off[m][r + 1] - t0[m]);
-            o0[m] = a.k2t_off[m][r];
-            no[m] = (uint32_t)(a.k2t_off[m][r + 1] - o0[m]);
-        }
-        pb = part_base(a, r);
-    }
-    const uint32_t np_r = (nk[0] ? 1u : 0u) + (nk[1] ? 1u : 0u) + (nk[2] ? 1u : 0u);
-    uint32_t v3[3] = {np_r, 0, 0}, ex3[3], tot3[3];
-    xt_scan3(v3, ex3, tot3, L.wsum);
-    const uint32_t NP = tot3[0];
-    uint32_t j = ex3[0];
-    const int64_t tix = live_r ? a.txn_index[r] : 0;
-    const bool kept = r >= a.self_lo && r < a.self_hi;
-    const int64_t dp = kept ? a.self_delta[0] : 0, dk = kept ? a.self_delta[1] : 0;
-    const int64_t di = kept ? a.self_delta[2] : 0, dn = kept ? a.self_delta[3] : 0;
-#pragma unroll
-    for (int m = 0; m < 3; ++m)
-    {
-        if (!nk[m]) continue;
-        const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
-        // source: the batch's region of (request, map) (keys, txnIds, keysToTxnIds back to back), or
-        // the packed arrays; offsets in elements of each array
-        if (a.reg)
-        {
-            const uint64_t base = a.t_reg[(uint64_t)m * a.n + r];       // byte offset of the region
-            L.ksrc[j] = base;
-            L.isrc[j] = base + 8ull * nk[m];
-            L.osrc[j] = base + 8ull * nk[m] + 4ull * nt[m];
-        }
-        else
-        {
-            L.ksrc[j] = k0[m];
-            L.isrc[j] = t0[m];
-            L.osrc[j] = o0[m];
-        }
-        L.kdst[j] = pb.KW + dk;
-        L.idst[j] = pb.ID + di;
-        L.odst[j] = pb.KO + dn;
-        L.nk[j] = nk[m];
-        L.map[j] = (uint8_t)m;
-        L.self[j] = kept ? 1 : 0;
-        int64_t* h = kept ? a.rhdr + 4 * (pb.P + dp) : a.hdr + 4 * pb.P;
-        h[0] = (tix << 2) | m;
-        h[1] = (int64_t)nk[m];
-        h[2] = (int64_t)nt[m];
-        h[3] = (int64_t)no[m];
-        pb.P += 1;
-        pb.KW += w * nk[m];
-        pb.ID += nt[m];
-        pb.KO += no[m];
-        ++j;
-    }
-    // element prefixes over the block's parts (thread t owns its request's parts j .. j + np_r)
-    {
-        uint32_t kw = 0, ni = 0, nn = 0;
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-        {
-            kw += (m == AD_MAP_RANGE ? 2u : 1u) * nk[m];
-            ni += nt[m];
-            nn += no[m];
-        }
-        uint32_t v[3] = {kw, ni, nn}, ex[3], tot[3];
-        xt_scan3(v, ex, tot, L.wsum);
-        uint32_t jj = ex3[0];
-        uint32_t ek = ex[0], ei = ex[1], eo = ex[2];
-#pragma unroll
-        for (int m = 0; m < 3; ++m)
-        {
-            if (!nk[m]) continue;
-            L.kpre[jj] = ek;
-            L.ipre[jj] = ei;
-            L.opre[jj] = eo;
-            ek += (m == AD_MAP_RANGE ? 2u : 1u) * nk[m];
-            ei += nt[m];
-            eo += no[m];
-            ++jj;
-        }
-        if (t == 0)
-        {
-            L.kpre[NP] = tot[0];
-            L.ipre[NP] = tot[1];
-            L.opre[NP] = tot[2];
-        }
-    }
-    __syncthreads();
-    const uint32_t KT = L.kpre[NP], IT = L.ipre[NP], OT = L.opre[NP];
-    for (uint32_t e = t; e < KT; e += XT_REQ)
-    {
-        const uint32_t q = xt_owner(L.kpre, NP, e), i = e - L.kpre[q];
-        int64_t* okeys = L.self[q] ? a.rkeys : a.okeys;
-        if (L.map[q] == AD_MAP_RANGE)
-        {
-            const uint32_t key = i >> 1;
-            const int64_t rid = a.reg ? reinterpret_cast<const int64_t*>(a.reg + L.ksrc[q])[key] : a.keys[AD_MAP_RANGE][L.ksrc[q] + key];
-            okeys[L.kdst[q] + i] = (i & 1) ? a.rt_end[rid] : a.rt_start[rid];
-        }
-        else
-        {
-            const int m = L.map[q];
-            okeys[L.kdst[q] + i] = a.reg ? reinterpret_cast<const int64_t*>(a.reg + L.ksrc[q])[i] : a.keys[m][L.ksrc[q] + i];
-        }
-    }
-    for (uint32_t e = t; e < IT; e += XT_REQ)
-    {
-        const uint32_t q = xt_owner(L.ipre, NP, e), i = e - L.ipre[q];
-        const uint32_t d = a.reg ? reinterpret_cast<const uint32_t*>(a.reg + L.isrc[q])[i] : a.txns[L.map[q]][L.isrc[q] + i];
-        int64_t* oids = L.self[q] ? a.rids : a.oids;
-        if (a.rank_ids)
-            reinterpret_cast<uint32_t*>(oids)[L.idst[q] + i] = d;
-        else
-        {
-            int64_t* o = oids + 3 * (L.idst[q] + i);
-            o[0] = (int64_t)a.dict_msb[d];
-            o[1] = (int64_t)a.dict_lsb[d];
-            o[2] = (int64_t)a.dict_node[d];
-        }
-    }
-    for (uint32_t e = t; e < OT; e += XT_REQ)
-    {
-        const uint32_t q = xt_owner(L.opre, NP, e), i = e - L.opre[q];
-        (L.self[q] ? a.rk2t : a.ok2t)[L.odst[q] + i] = a.reg ? reinterpret_cast<const int32_t*>(a.reg + L.osrc[q])[i] : a.k2t[L.map[q]][L.osrc[q] + i];
-    }
-}
-
-// Export by request groups (the default): G lanes per request copy its parts' key words, ids and
-// keysToTxnIds lane-strided (a part's elements are contiguous at both ends), with no block scans, LDS
-// or owner searches -- parts are small (a store's share of a request: a few keys, tens of ids), so the
-// per-element owner search and the block-wide barriers of k_export_tiles cost more than the copy.
+// Export by request groups: G lanes per request copy its parts' key words, ids and keysToTxnIds
+// lane-strided (a part's elements are contiguous at both ends), with no block scans, LDS or owner searches --
+// parts are small (a store's share of a request: a few keys, tens of ids), so a load-balanced copy over
+// blocks of 128 requests (round 2's k_export_tiles: per-element owner search, block-wide barriers) cost more
+// than the copy (1.11 against 0.77 ms for the W = 8 node's exports; deleted in round 6).
 // Every lane of a group reads the request's offsets (same addresses: one line per group).
 template <uint32_t G>
 __global__ void __launch_bounds__(256) k_export_groups(ExportArgs a)
@@ -1946,12 +1741,6 @@ hipError_t run_export_sizes(const ExportArgs& a, hipStream_t st)
 hipError_t run_export_emit(const ExportArgs& a, hipStream_t st)
 {
     if (!a.n) return hipSuccess;
-    const bool tiles = getenv("AD_EXPORT_TILES") != nullptr;      // measurement switches, read per launch
-    if (tiles)
-    {
-        k_export_tiles<<<(unsigned)((a.n + XT_REQ - 1) / XT_REQ), XT_REQ, 0, st>>>(a);
-        return hipGetLastError();
-    }
     // lanes per request by the batch's ids per request (a.ids_per_req: from the resolve's stats). Measured
     // (scripts/export_ab.sh, AD_EXPORT_TRACE): at 2 ids per request (config-3 W = 8 stores) 2 lanes take
     // 0.77 ms for the node's eight exports against 0.95 with 4, 1.42 with 8 and 1.11 for the block tiles;

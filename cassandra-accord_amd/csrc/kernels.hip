@@ -2476,7 +2476,6 @@ hipError_t run_copy_out(const OutSegs& g, hipStream_t st)
 {
     if (!g.n) return hipSuccess;
     unsigned blocks = 64;       // 64 blocks fill PCIe (6.5-6.8 ms per config-2 batch against 6.7-7.7 at 256); the CUs stay with the resolve
-    if (const char* e = getenv("AD_COPY_BLOCKS")) blocks = (unsigned)std::max(1, std::min(4096, atoi(e)));
     k_copy_out<<<blocks, 256, 0, st>>>(g);
     return hipGetLastError();
 }

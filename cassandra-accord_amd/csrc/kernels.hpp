@@ -45,11 +45,6 @@ struct BatchBufs {
     const uint8_t* p_kind;
     const int64_t* q_keys_hi;
     uint32_t* p_slot;                // lean passes without range commands: per probe its KeyLine (LS_NONE: outside the slice)
-    // lean pass 1 as gather + build (run_lean_gb): per request 64 staged raw emissions, its build record
-    // {raw count | #keys << 8 | deferred << 31, eight per-key start bytes}, its keys
-    uint32_t* lg_stage; uint4* lg_rec; int64_t* lg_keys;
-    uint64_t* lg_dummy;              // per build wave one 128-byte line its disabled lanes' stores go to
-    uint32_t slots_by_prepare;       // p_slot filled by k_prepare (one launch for records and slots)
     // K0
     uint32_t* t_S; uint32_t* t_self; uint32_t* t_kinds; int64_t* t_epoch;
     uint32_t* p_txn; uint4* p_rec;
@@ -204,7 +199,6 @@ hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, bool wide1, hipStream_t st);
 // lean pass 1 (and 2) as k_lean_gather + k_lean_build, stores without range commands: requests it cannot
 // serve are appended to deferred2 (the general kernel's list)
-hipError_t run_lean_gb(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
 
 // ---- PreAccept timestamp proposal (preaccept.hip)
 struct DevRangeMap {            // a ReducingRangeMap<Timestamp> in HBM (ad_range_map_soa)
@@ -241,7 +235,6 @@ hipError_t run_preaccept(const PreacceptArgs& a, hipStream_t st);
 hipError_t run_preaccept_key_values(const DevRangeMap& mc, const DevRangeMap& rb, const int64_t* keys, uint64_t n_keys,
                                     PaValue* key_val, hipStream_t st);
 hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st);
-hipError_t run_defer_append(const BatchBufs& b, hipStream_t st);
 hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, uint32_t* cnt, hipStream_t st);
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
                             const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,

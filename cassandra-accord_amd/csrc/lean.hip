@@ -44,69 +44,25 @@ constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 #define LEAN_CHUNK_LOG 16
 #endif
 constexpr uint32_t LEAN_CHUNK = 1u << LEAN_CHUNK_LOG;   // region bytes a wave takes from the arena at a time
-// measurement switches (scripts/build_variant.sh; results are wrong with any of them set):
-// 1 synthetic list elements (no list loads), 2 no sort, 4 no region writes, 8 no size / offset stores,
-// 16 KeyLines from a 512 KB subset of the table (cache-resident; a line counts as the key's), 32 sizes stored
-// as 64-byte per-request records (into the offsets buffer) instead of the nine SoA arrays
-#ifndef LEAN_EXP
-#define LEAN_EXP 0
-#endif
 
-// Per probe, its KeyLine (stores without range commands, LEAN_SLOTS): the slice test
+// Per probe, its KeyLine (stores without range commands): k_prepare does the slice test
 // (InMemoryCommandStore.java:280) and the perfect-hash displacement, one thread per probe, so that the
 // lean passes load a probe's key and its line position side by side -- one dependent load shorter,
 // and no displacement gather inside them. The line still proves the key is the store's.
-#ifndef LEAN_SLOTS
-#define LEAN_SLOTS 1
-#endif
 constexpr uint32_t LS_NONE = 0xFFFFFFFFu;
-// LEAN_XCD: a wave's items (it0, it0 + nw, ...) from its XCD-relabelled block id (wave.hpp xcd_block):
-// consecutive items -- whose request records, keys, size and offset words share cache lines -- run on
-// one XCD's L2 instead of being dealt over all eight
-#ifndef LEAN_XCD
-#define LEAN_XCD 1
-#endif
-__device__ __forceinline__ uint32_t lean_block() { return LEAN_XCD ? xcd_block() : blockIdx.x; }
-// LEAN_QLOAD: a request's KeyLine headers are loaded by all 32 of its lanes, one 16-byte quarter of one
+// A wave's items (it0, it0 + nw, ...) from its XCD-relabelled block id (wave.hpp xcd_block): consecutive
+// items -- whose request records, keys, size and offset words share cache lines -- run on one XCD's L2
+// instead of being dealt over all eight
+__device__ __forceinline__ uint32_t lean_block() { return xcd_block(); }
+// Loads use clamped addresses on every lane (branch-free, so the loop's wait counts stay exact); at two
+// requests per wave a request's KeyLine headers are loaded by all 32 of its lanes, one 16-byte quarter of one
 // key's first 64 bytes per lane (one vector load per item instead of four, each line touched once), and
-// handed to the key lanes through a per-wave LDS stage
-#ifndef LEAN_QLOAD
-#define LEAN_QLOAD 1
-#endif
-// LEAN_MASKED: loads move only the data their lanes use -- a request's record by one lane (broadcast by
-// readlane), keys / slots / KeyLine quarters / list elements exec-masked to the lanes that need them --
-// instead of clamped addresses on every lane. It cuts L1 accesses per item from 229 to 93 but measured
-// no faster with the ds_bpermute shuffles, and slower with the DPP ones (pass 1 0.462 vs 0.450 ms,
-// pass 2 0.152 vs 0.146: its branches cost the loop's exact wait counts): off
-#ifndef LEAN_MASKED
-#define LEAN_MASKED 0
-#endif
+// handed to the key lanes through a per-wave LDS stage (QL below). Sorting networks and segment scans
+// exchange lanes by DPP / permlane swaps (wave.hpp xor_lane), not ds_bpermute.
 // Wide pass 1 (run_resolve_lean's wide1, chosen per batch by the host): pass 1 also takes the requests of
 // 33..64 raw emissions (two per lane, the pass-2 path), at pass 2's register budget (4 waves per SIMD);
 // pass 2 then sees only what exceeds 64. Measured on config 2: passes 1 + 2 0.613 -> 0.560 ms; on
 // config 3's store (uniform keys, almost nothing above 32) 0.743 -> 0.841 ms
-// LEAN_RLBC: a segment's lane-p value reaches the segment's lanes by v_readlane per segment and a select
-// (VALU) instead of a ds_bpermute (LDS round trip)
-#ifndef LEAN_RLBC
-#define LEAN_RLBC 0
-#endif
-// LEAN_DPP: the sorting networks and segment scans exchange lanes by DPP / permlane swaps (wave.hpp
-// xor_lane) instead of ds_bpermute
-#ifndef LEAN_DPP
-#define LEAN_DPP 1
-#endif
-
-__global__ __launch_bounds__(256) void k_lean_slots(DevSnapshot s, const int64_t* keys, uint64_t np, uint32_t* slot)
-{
-    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= np) return;
-    const int64_t key = keys[p];
-    bool in = s.n_slices == 0;
-    for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
-    uint32_t r = LS_NONE;
-    if (in) r = (uint32_t)kl_index(key_hash2(key), s.kl_disp[kl_bucket(key_hash(key), s.kl_buckets)], s.kl_lines);
-    slot[p] = r;
-}
 
 // ascending bitonic sort within each LPR-lane segment (a request's lanes)
 template <uint32_t K, uint32_t LPR>
@@ -118,7 +74,7 @@ __device__ __forceinline__ void seg_bitonic(uint32_t& key)
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1)
         {
-            const uint32_t ok = LEAN_DPP ? xor_lane(key, j) : (uint32_t)__shfl_xor(key, (int)j, 64);
+            const uint32_t ok = xor_lane(key, j);
             const bool up = (l & k) == 0;
             const bool lower = (l & j) == 0;
             key = (lower == up) ? min(key, ok) : max(key, ok);
@@ -134,7 +90,7 @@ __device__ __forceinline__ void seg_bitonic64(uint64_t& key)
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1)
         {
-            const uint64_t ok = LEAN_DPP ? xor_lane64(key, j) : (uint64_t)__shfl_xor(key, (int)j, 64);
+            const uint64_t ok = xor_lane64(key, j);
             const bool up = (l & k) == 0;
             const bool lower = (l & j) == 0;
             key = (lower == up) ? min(key, ok) : max(key, ok);
@@ -163,7 +119,7 @@ __device__ __forceinline__ void seg_bitonic_wide(T& x0, T& x1)
             else
             {
                 T o0, o1;
-                if constexpr (sizeof(T) == 4 && LEAN_DPP)
+                if constexpr (sizeof(T) == 4)
                 {
                     o0 = xor_lane(x0, j);
                     o1 = xor_lane(x1, j);
@@ -209,24 +165,12 @@ __device__ __forceinline__ void seg_bitonic_w(T& x0, T& x1)
         }
 }
 
-// LEAN_ADAPT: refills sized for what the wave will still write (dense arena: 304 MB in use for 272 MB of
-// config-2 regions) -- measured 0.06 ms slower per config-2 step than fixed chunks, the estimator's
-// registers spill in pass 1; off by default
-#ifndef LEAN_P2_CHUNK_FULL
-#define LEAN_P2_CHUNK_FULL 0
-#endif
-#ifndef LEAN_ADAPT
-#define LEAN_ADAPT 0
-#endif
-constexpr uint64_t LEAN_CHUNK_MIN = 2048, LEAN_CHUNK_FIRST = 8192;
 struct LeanChunk {
     // wave-uniform bump allocation from the region arena, offsets in 8-byte units (regions and chunks
-    // are multiples of 8 bytes; the arena stays below 32 GB). A refill is sized for what the wave will
-    // still write -- its bytes per item so far times the items it has left, + 1/8 -- between
-    // LEAN_CHUNK_MIN and LEAN_CHUNK, so the arena stays dense (the unused tail of a wave's last chunk is
-    // all it leaves) with a few refills per wave. Items done / left come from the wave's item `it`
-    // (items it0, it0 + nw, ...) only when a chunk is taken.
-    uint32_t cur = 0, end = 0, used = 0;
+    // are multiples of 8 bytes; the arena stays below 32 GB), in fixed chunks. (Refills sized for what the
+    // wave will still write kept the arena dense -- 304 MB in use for 272 MB of config-2 regions -- but
+    // measured 0.06 ms slower per config-2 step: the estimator's registers spilled in pass 1.)
+    uint32_t cur = 0, end = 0;
     template <int PASS>
     __device__ __forceinline__ uint64_t take(BatchCtl* ctl, uint64_t nbytes, uint64_t cap, uint32_t it, uint32_t n_items,
                                              uint32_t nw)
@@ -235,20 +179,7 @@ struct LeanChunk {
         if (n8 > end - cur)
         {
             // fixed chunks: pass 1's waves write ~50 KB each (config 2), pass 2's ~13 KB
-            uint64_t want = LEAN_ADAPT ? LEAN_CHUNK_FIRST : ((PASS == 1 || LEAN_P2_CHUNK_FULL) ? LEAN_CHUNK : LEAN_CHUNK / 4);
-            if (LEAN_ADAPT)
-            {
-                // in float (few registers on this rarely taken path): items done / left from the stride
-                const float rnw = __builtin_amdgcn_rcpf((float)nw);
-                const float done = (float)(it - uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6))) * rnw;
-                if (done >= 1.0f)
-                {
-                    const float left = (float)(n_items - it) * rnw + 1.0f;
-                    const float est = (float)used * 9.0f * left * __builtin_amdgcn_rcpf(done);    // 8 B units, + 1/8
-                    want = ((uint64_t)est + 255) & ~255ull;
-                }
-            }
-            if (LEAN_ADAPT) want = want < LEAN_CHUNK_MIN ? LEAN_CHUNK_MIN : (want > LEAN_CHUNK ? LEAN_CHUNK : want);
+            const uint64_t want = PASS == 1 ? LEAN_CHUNK : LEAN_CHUNK / 4;
             const uint64_t sz = nbytes > want ? nbytes : want;
             unsigned long long base = 0;
             if (lane_id() == 0) base = atomicAdd(&ctl->reg_top, (unsigned long long)sz);
@@ -259,7 +190,6 @@ struct LeanChunk {
         }
         const uint64_t r = (uint64_t)cur << 3;
         cur += n8;
-        used += n8;
         return r;
     }
 };
@@ -280,7 +210,7 @@ __device__ __forceinline__ uint32_t key_lanes_incl_scan(uint32_t v, uint32_t hl)
 #pragma unroll
     for (uint32_t d = 1; d < 8; d <<= 1)
     {
-        const uint32_t t = LEAN_DPP ? row_up(v, d) : (uint32_t)__shfl_up(v, d, 8);
+        const uint32_t t = row_up(v, d);
         if ((hl & 7) >= d) v += t;
     }
     return v;
@@ -404,38 +334,16 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
     // one lane per request loads its 16-byte record (the texture data path moves 16 B per request, not
     // per lane); derive() broadcasts it over the request's lanes
     auto loadA = [&](uint32_t t) -> Raw {
-        if (!LEAN_MASKED) return b.q_rec[t != DEFER_HOLE ? t : 0u];
-        Raw r = make_uint4(0u, 0u, 0u, 0u);
-        if (hl == 0) r = b.q_rec[t != DEFER_HOLE ? t : 0u];
-        return r;
+        return b.q_rec[t != DEFER_HOLE ? t : 0u];
     };
     // the value of the segment's lane p (p known after unrolling) in every lane of the segment
     auto seg_lane = [&](uint32_t v, uint32_t p) -> uint32_t {
-        if (!LEAN_RLBC) return (uint32_t)__shfl((int)v, (int)(sb | p), 64);
-        uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p);
-#pragma unroll
-        for (uint32_t k = 1; k < RPW; ++k)
-        {
-            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(k * LPR + p));
-            r = h == k ? x : r;
-        }
-        return r;
-    };
-    // the value of lane sb (the segment's first lane) in every lane of the segment
-    auto seg_bcast = [&](uint32_t v) -> uint32_t {
-        uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-#pragma unroll
-        for (uint32_t k = 1; k < RPW; ++k)
-        {
-            const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(k * LPR));
-            r = h == k ? x : r;
-        }
-        return r;
+        return (uint32_t)__shfl((int)v, (int)(sb | p), 64);
     };
     // the record carries PreAccept.java:251-261's witness class, S and self as ranks (k_prepare)
     // and whether the request fits the lean path (<= 8 keys, valid kind); anything else defers
     auto derive = [&](uint32_t t, const Raw& r0) -> Req {
-        const Raw r = LEAN_MASKED ? make_uint4(seg_bcast(r0.x), seg_bcast(r0.y), seg_bcast(r0.z), seg_bcast(r0.w)) : r0;
+        const Raw& r = r0;
         Req q{0, 0, 0, t, 0, 0, false, false};
         q.act = t != DEFER_HOLE;
         q.k0 = r.x;
@@ -446,34 +354,22 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         q.defer = (r.z & REC_FAST) == 0;
         return q;
     };
-    // the key (one lane per key), and with LEAN_SLOTS its line position beside it
-    constexpr bool SLOTS = !RNG && LEAN_SLOTS;
-    // exec-masked: only the key lanes move data
+    // the key (one lane per key), and without range commands its line position beside it (k_prepare)
+    constexpr bool SLOTS = !RNG;
     auto loadB = [&](const Req& q, int64_t& key, uint32_t& sl) {
         const bool on = q.act && !q.defer && hl < q.np;
-        if (!LEAN_MASKED)
-        {
-            key = b.q_keys[on ? q.k0 + hl : 0];
-            if (SLOTS)
-            {
-                const uint32_t v = b.p_slot[on ? q.k0 + hl : 0];
-                sl = on ? v : LS_NONE;
-            }
-            return;
-        }
-        key = 0;
-        if (on) key = b.q_keys[q.k0 + hl];
+        key = b.q_keys[on ? q.k0 + hl : 0];
         if (SLOTS)
         {
-            sl = LS_NONE;
-            if (on) sl = b.p_slot[q.k0 + hl];
+            const uint32_t v = b.p_slot[on ? q.k0 + hl : 0];
+            sl = on ? v : LS_NONE;
         }
     };
     // the key's line (KeyLine, common.hpp): the slice test (InMemoryCommandStore.java:280), then one
     // random line per key -- its first 64 bytes: key, cell entries, newest fields, meta, the class's
     // {count, start} and the cwr tail start. A slot holding another key is resolved when used.
     struct Hdr { uint4 h0, h1; uint2 h2, h3; uint4 q; uint32_t slot; bool look; };
-    constexpr bool QL = LEAN_QLOAD && !RNG && LEAN_SLOTS && RPW == 2;
+    constexpr bool QL = !RNG && RPW == 2;
     __shared__ uint4 qst_all[QL ? LEAN_WAVES : 1][QL ? 64 : 1];
     auto in_slice_of = [&](int64_t key) {
         bool in = s.n_slices == 0;
@@ -487,8 +383,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         H.h2 = reinterpret_cast<const uint2*>(L4 + 2)[cls];
         H.h3 = reinterpret_cast<const uint2*>(L4 + 3)[1];       // {cwr tail start, prunedBefore rank}
     };
-    // the key's displacement (a small table: cache-resident), issued ahead of its line; with LEAN_SLOTS
-    // the line position came with the key (k_lean_slots)
+    // the key's displacement (a small table: cache-resident), issued ahead of its line; without range
+    // commands the line position came with the key (k_prepare)
     auto loadD = [&](const Req& q, int64_t key, uint32_t sl, bool& look, uint32_t& d) {
         if (SLOTS)
         {
@@ -506,15 +402,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         if (QL)
         {
             // lane hl loads quarter hl & 3 of key hl >> 2's line (unmasked: unpacked under the key lane's look)
-            uint32_t ks = __shfl(look ? H.slot : LS_NONE, (int)(sb | (hl >> 2)), 64);
-            if ((LEAN_EXP & 16) && ks != LS_NONE) ks &= 4095u;
-            if (!LEAN_MASKED)
-                H.q = reinterpret_cast<const uint4*>(s.kline + (ks != LS_NONE ? ks : 0u))[hl & 3u];
-            else
-            {
-                H.q = make_uint4(0u, 0u, 0u, 0u);
-                if (ks != LS_NONE) H.q = reinterpret_cast<const uint4*>(s.kline + ks)[hl & 3u];
-            }
+            const uint32_t ks = __shfl(look ? H.slot : LS_NONE, (int)(sb | (hl >> 2)), 64);
+            H.q = reinterpret_cast<const uint4*>(s.kline + (ks != LS_NONE ? ks : 0u))[hl & 3u];
             return;
         }
         load_line(H.slot, q.cls, H);
@@ -536,7 +425,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             wave_lds_sync();
         }
         auto key_of = [](const uint4& h0) { return (int64_t)(((uint64_t)h0.y << 32) | h0.x); };
-        found = H.look && (H.h1.w & KL_USED) && ((LEAN_EXP & 16) || key_of(H.h0) == key);
+        found = H.look && (H.h1.w & KL_USED) && key_of(H.h0) == key;
         cb = found ? make_uint2(H.h0.z, H.h0.w) : make_uint2(0, 0);
         if (RNG && H.look && !found && s.cell_off)
         {
@@ -556,12 +445,10 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
     // sizes of map m (keys, txnIds, keysToTxnIds) and its region offset: one store from lanes
     // hl = 0..3 of each segment (per-lane addresses keep the size arrays out of scalar registers)
     auto put_sizes = [&](bool on, uint32_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro, bool with_ro) {
-        if (LEAN_EXP & 8) return;
         if (on && hl < 3)
         {
             const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);
-            if (LEAN_EXP & 32) reinterpret_cast<uint32_t*>(b.off)[(uint64_t)t * 16 + 3 * m + hl] = v;   // measurement: AoS records
-            else b.sz[(uint64_t)(3 * m + hl) * n + t] = v;
+            b.sz[(uint64_t)(3 * m + hl) * n + t] = v;
         }
         if (with_ro && on && hl == 3) b.t_reg[(uint64_t)m * n + t] = ro;
     };
@@ -646,7 +533,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
 #pragma unroll
         for (uint32_t d = 1; d < 8; d <<= 1)
         {
-            const uint32_t v = LEAN_DPP ? row_up(inc, d) : (uint32_t)__shfl_up(inc, d, 8);
+            const uint32_t v = row_up(inc, d);
             if ((hl & 7) >= d) inc += v;
         }
         const uint32_t start = inc - nn;
@@ -741,9 +628,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
                 seg_bitonic_wide(k0, k1);
                 const bool v0 = hl < tot, v1 = hl + 32 < tot;
                 const uint32_t x0 = k0 >> 3, x1 = k1 >> 3, ka0 = k0 & 7u, ka1 = k1 & 7u;
-                const uint32_t p0 = LEAN_DPP ? wave_up1(k0) : (uint32_t)__shfl_up(k0, 1, LPR);
+                const uint32_t p0 = wave_up1(k0);
                 const uint32_t last0 = __shfl(k0, (int)(sb | 31u), 64);
-                const uint32_t up1 = LEAN_DPP ? wave_up1(k1) : (uint32_t)__shfl_up(k1, 1, LPR);   // by every lane (an inactive source reads 0)
+                const uint32_t up1 = wave_up1(k1);   // by every lane (an inactive source reads 0)
                 const uint32_t p1 = hl == 0 ? last0 : up1;
                 const bool u0 = v0 && (hl == 0 || (p0 >> 3) != x0);
                 const bool u1 = v1 && (p1 >> 3) != x1;
@@ -774,7 +661,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
 #pragma unroll
                 for (uint32_t d = 1; d < 8; d <<= 1)
                 {
-                    const uint32_t v = LEAN_DPP ? row_up(cinc, d) : (uint32_t)__shfl_up(cinc, d, 8);
+                    const uint32_t v = row_up(cinc, d);
                     if ((hl & 7) >= d) cinc += v;
                 }
                 const uint32_t kstart_l = cinc - cnt;
@@ -829,10 +716,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         else
             lp = from_cand ? s.cand + (a_base + i) : s.cwr + (a_ct + (i - a_n1));
         // class Ws: the last Write, no load; lanes without an element load nothing
-        uint32_t lv = 0;
-        if (LEAN_EXP & 1) lv = (2 * hl + 1) | (1u << RANK_BITS);
-        else if (!LEAN_MASKED) lv = *((!live || (!from_cand && cls == 0)) ? s.cand : lp);
-        else if (live && (from_cand || cls != 0)) lv = *lp;
+        const uint32_t lv = *((!live || (!from_cand && cls == 0)) ? s.cand : lp);
         // range elements (same round trip as the list loads)
         uint32_t ar = 0, ar1 = 0;
         uint64_t ce = 0, ce1 = 0;
@@ -904,14 +788,13 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             // the sort must span every lane that may hold one (raw emissions: lanes [0, T))
             // (a deferred request of the wave may hold T > LPR: never sort across segments)
             const uint32_t kmax = min(seg_max(T), LPR);
-            if (LEAN_EXP & 2) {}
-            else if (kmax <= 8) seg_bitonic<8, LPR>(k);
+            if (kmax <= 8) seg_bitonic<8, LPR>(k);
             else if (kmax <= 16 || LPR == 16) seg_bitonic<16, LPR>(k);
             else if (kmax <= 32 || LPR == 32) seg_bitonic<(LPR < 32 ? LPR : 32), LPR>(k);
             else seg_bitonic<LPR, LPR>(k);
             const bool valid = hl < tot;
             const uint32_t xr = k >> 3, ka = k & 7u;
-            const uint32_t prev = LEAN_DPP ? wave_up1(k) : (uint32_t)__shfl_up(k, 1, LPR);
+            const uint32_t prev = wave_up1(k);
             const bool uniq = valid && (hl == 0 || (prev >> 3) != xr);
             // index of this lane's value among the distinct values: uniques up to and including this
             // lane, minus one (equal values sit in adjacent lanes)
@@ -935,7 +818,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
 #pragma unroll
             for (uint32_t d = 1; d < 8; d <<= 1)
             {
-                const uint32_t v = LEAN_DPP ? row_up(cinc, d) : (uint32_t)__shfl_up(cinc, d, 8);
+                const uint32_t v = row_up(cinc, d);
                 if ((hl & 7) >= d) cinc += v;
             }
             const uint32_t kstart_l = cinc - cnt;
@@ -948,7 +831,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             bool fits;
             const uint64_t ro = seg_alloc(bytes, fits, it);
             put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro, true);
-            if (act && tot && fits && !(LEAN_EXP & 4))
+            if (act && tot && fits)
             {
                 int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
                 uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
@@ -994,8 +877,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             };
             const uint32_t rkaa = elem(k1a & 63u, pva), rkab = elem(k1b & 63u, pvb);
             const uint32_t lasta = (uint32_t)__shfl((int)rida, (int)(sb | (LW - 1)), 64);
-            const uint32_t prida = LEAN_DPP ? wave_up1(rida) : (uint32_t)__shfl_up(rida, 1, LPR);
-            const uint32_t upb = LEAN_DPP ? wave_up1(ridb) : (uint32_t)__shfl_up(ridb, 1, LPR);
+            const uint32_t prida = wave_up1(rida);
+            const uint32_t upb = wave_up1(ridb);
             const uint32_t pridb = hl == 0 ? lasta : upb;
             const bool gfra = pva && (hl == 0 || prida != rida), gfrb = pvb && pridb != ridb;
             // each element's range group start (its encoded position: lane, or 64 + lane in register 1); the
@@ -1022,8 +905,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             uint32_t k2b = pub ? ((rkab >> 3) << 6) | dstb : 0xFFFFFFFFu;
             seg_bitonic_w<uint32_t, LPR>(k2a, k2b);
             const uint32_t last2 = (uint32_t)__shfl((int)k2a, (int)(sb | (LW - 1)), 64);
-            const uint32_t p2a = LEAN_DPP ? wave_up1(k2a) : (uint32_t)__shfl_up(k2a, 1, LPR);
-            const uint32_t up2b = LEAN_DPP ? wave_up1(k2b) : (uint32_t)__shfl_up(k2b, 1, LPR);
+            const uint32_t p2a = wave_up1(k2a);
+            const uint32_t up2b = wave_up1(k2b);
             const uint32_t p2b = hl == 0 ? last2 : up2b;
             const bool v2a = hl < UP, v2b = hl + LW < UP;
             const bool uqa = v2a && (hl == 0 || (p2a >> 6) != (k2a >> 6)), uqb = v2b && (p2b >> 6) != (k2b >> 6);
@@ -1084,7 +967,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             const uint32_t rid = k1 >> 6, src = sb | (k1 & 63u);
             // the pair's rank and key (its source lane)
             const uint32_t rka = (uint32_t)__shfl((int)((rk << 3) | ar), (int)(pv ? src : lane), 64);
-            const uint32_t prid = LEAN_DPP ? wave_up1(rid) : (uint32_t)__shfl_up(rid, 1, LPR);
+            const uint32_t prid = wave_up1(rid);
             const bool gfirst_raw = pv && (hl == 0 || prid != rid);
             // the key of the range id's first run (segment starts are group starts: an absolute-lane max scan)
             const uint32_t gs = wave_incl_max_dpp(gfirst_raw ? lane : 0u);
@@ -1102,7 +985,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             else if (kmaxr <= 16 || LPR == 16) seg_bitonic<16, LPR>(k2);
             else if (kmaxr <= 32 || LPR == 32) seg_bitonic<(LPR < 32 ? LPR : 32), LPR>(k2);
             else seg_bitonic<LPR, LPR>(k2);
-            const uint32_t p2 = LEAN_DPP ? wave_up1(k2) : (uint32_t)__shfl_up(k2, 1, LPR);
+            const uint32_t p2 = wave_up1(k2);
             const bool v2 = hl < UP;
             const bool uq2 = v2 && (hl == 0 || (p2 >> 6) != (k2 >> 6));
             const uint64_t um2 = seg(ballot(uq2));
@@ -1141,8 +1024,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             else seg_bitonic64<LPR, LPR>(pk);
             const uint32_t totp = __popcll(seg(rmb));
             const bool pv = hl < totp;
-            const uint64_t pprev = LEAN_DPP ? (((uint64_t)wave_up1((uint32_t)(pk >> 32)) << 32) | wave_up1((uint32_t)pk))
-                                            : (uint64_t)__shfl_up(pk, 1, LPR);
+            const uint64_t pprev = (((uint64_t)wave_up1((uint32_t)(pk >> 32)) << 32) | wave_up1((uint32_t)pk))
+                                           ;
             const bool pu = pv && (hl == 0 || pprev != pk);
             const uint64_t pum = seg(ballot(pu));
             const uint32_t UP = __popcll(pum);
@@ -1161,7 +1044,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             }
             const bool uplive = hl < UP;
             const uint32_t rid = (uint32_t)(up >> 32), urk = (uint32_t)up;
-            const uint32_t prid = LEAN_DPP ? wave_up1(rid) : (uint32_t)__shfl_up(rid, 1, LPR);
+            const uint32_t prid = wave_up1(rid);
             const bool gfirst = uplive && (hl == 0 || prid != rid);
             const uint64_t gm = seg(ballot(gfirst));
             const uint32_t nR = __popcll(gm);
@@ -1171,8 +1054,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             else if (kmaxr <= 16 || LPR == 16) seg_bitonic64<16, LPR>(k2);
             else if (kmaxr <= 32 || LPR == 32) seg_bitonic64<(LPR < 32 ? LPR : 32), LPR>(k2);
             else seg_bitonic64<LPR, LPR>(k2);
-            const uint64_t p2 = LEAN_DPP ? (((uint64_t)wave_up1((uint32_t)(k2 >> 32)) << 32) | wave_up1((uint32_t)k2))
-                                         : (uint64_t)__shfl_up(k2, 1, LPR);
+            const uint64_t p2 = (((uint64_t)wave_up1((uint32_t)(k2 >> 32)) << 32) | wave_up1((uint32_t)k2))
+                                        ;
             const bool v2 = hl < UP;
             const bool uq2 = v2 && (hl == 0 || (uint32_t)(p2 >> 8) != (uint32_t)(k2 >> 8));
             const uint64_t um2 = seg(ballot(uq2));
@@ -1216,7 +1099,6 @@ static hipError_t launch_lean(const DevSnapshot& s, const BatchBufs& b, hipStrea
             nb <= 0)
             nb = 2;
         per_cu = std::min(nb, lean_occ<RNG, WIDE>());     // measured: more resident waves only add memory contention
-        if (const char* e = getenv("AD_LEAN_PER_CU")) per_cu = std::max(1, std::min(per_cu, atoi(e)));
     }
     const uint64_t need = ((b.n_txns + RPW - 1) / RPW + LEAN_WAVES - 1) / LEAN_WAVES;
     const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu));
@@ -1231,11 +1113,7 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     if (!b.n_txns) return hipSuccess;
     if (pass == 1)
     {
-        if (!s.n_rent && LEAN_SLOTS && !b.slots_by_prepare)
-        {
-            if (!b.p_slot) return hipErrorInvalidValue;
-            if (b.n_probes) k_lean_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b.q_keys, b.n_probes, b.p_slot);
-        }
+        if (!s.n_rent && !b.p_slot) return hipErrorInvalidValue;     // k_prepare writes the probes' lines
         if (rpw1 == 8) return s.n_rent ? launch_lean<8, true, false, 1>(s, b, st) : launch_lean<8, false, false, 1>(s, b, st);
         if (rpw1 == 4) return s.n_rent ? launch_lean<4, true, false, 1>(s, b, st) : launch_lean<4, false, false, 1>(s, b, st);
         if (wide1 && !s.n_rent) return launch_lean<2, false, true, 1>(s, b, st);
@@ -1247,406 +1125,5 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     return launch_lean<2, false, true, 2>(s, b, st);
 }
 
-
-// ---------------------------------------------------------------------------------------------------
-// Lean pass 1 as two kernels (LEAN_GB, stores without range commands, two requests per build wave):
-//
-//   k_lean_gather: one lane per (request, key) probe, eight requests per wave iteration -- the
-//     request record, the key and its KeyLine, the newest test, the emission counts (the loop body of
-//     mapReduceActive with end = insertPos(S) and M = the key's last committed Write's executeAt,
-//     CommandsForKey.java:910-950) -- and the raw emissions copied, already filtered by txnId < S
-//     (STARTED_BEFORE) and the request's own id (PreAccept.java:258), into a fixed 64-word stage per
-//     request; per request a build record {raw count, #keys, per-key starts} and its keys. Requests the
-//     lean path cannot serve (a key needing the tree, > 64 raw emissions, > 8 keys) go to the general
-//     kernel's list.
-//   k_lean_build: two requests per wave, 32 lanes each -- the Deps.AbstractBuilder.add routing
-//     (Deps.java:80-106) and the RelationMultiMap build (RelationMultiMap.java:147-260) of the staged
-//     lists: (rank, key) bitonic sort per map, ballot dedup, CSR regions. Its inputs sit at fixed offsets
-//     from the request index, so its loads issue two items ahead with no dependent chain.
-//
-// The single fused pass waited one dependent memory round trip (record -> keys -> line -> elements) per
-// two requests; here the gather moves four times the probes per round trip at low register pressure, and
-// the build's loads never wait on each other.
-// ---------------------------------------------------------------------------------------------------
-#ifndef GB_OCC_G
-#define GB_OCC_G 8
-#endif
-#ifndef GB_OCC_B
-#define GB_OCC_B 6
-#endif
-constexpr uint32_t GB_STAGE = 64;           // staged raw emissions per request (words)
-constexpr uint32_t GB_INVALID = 0xFFFFFFFFu;  // a staged element filtered out (txnId >= S or the request's own)
-constexpr uint32_t GB_DEFER = 1u << 31;     // build record: the request went to the general kernel
-constexpr uint32_t GB_WIDE = 1u << 30;      // build record: 33..64 raw emissions, built by the wide build
-
-__global__ __launch_bounds__(64 * LEAN_WAVES, GB_OCC_G) void k_lean_gather(DevSnapshot s, BatchBufs b)
-{
-    const uint32_t lane = lane_id(), h = lane >> 3, j = lane & 7u, sb8 = h * 8;
-    const uint64_t n = b.n_txns;
-    const uint32_t n_groups = (uint32_t)((n + 7) / 8);
-    const uint32_t nw = gridDim.x * LEAN_WAVES;
-    const uint32_t* kl32 = reinterpret_cast<const uint32_t*>(s.kline);
-    __shared__ uint32_t mk_all[LEAN_WAVES][64];
-    uint32_t* mk = mk_all[threadIdx.x >> 6];
-    __shared__ uint32_t dbuf_all[LEAN_WAVES][DEFER_CHUNK];
-    uint32_t* dbuf = dbuf_all[threadIdx.x >> 6];
-    uint32_t dn = 0;
-    auto dflush = [&]() {
-        if (!dn) return;
-        unsigned long long base = 0;
-        if (lane_id() == 0)
-        {
-            base = atomicAdd(&b.ctl->n_deferred2, (unsigned long long)dn);
-            atomicAdd(&b.ctl->n_real2, (unsigned long long)dn);
-        }
-        base = uniform64(base);
-        wave_lds_sync();
-        if (lane_id() < dn) b.deferred2[base + lane_id()] = dbuf[lane_id()];
-        wave_lds_sync();
-        dn = 0;
-    };
-    // the wide build's list (deferred1 / n_deferred1, unused otherwise on this path)
-    __shared__ uint32_t wbuf_all[LEAN_WAVES][DEFER_CHUNK];
-    uint32_t* wbuf = wbuf_all[threadIdx.x >> 6];
-    uint32_t wn = 0;
-    auto wflush = [&]() {
-        if (!wn) return;
-        unsigned long long base = 0;
-        if (lane_id() == 0) base = atomicAdd(&b.ctl->n_deferred1, (unsigned long long)wn);
-        base = uniform64(base);
-        wave_lds_sync();
-        if (lane_id() < wn) b.deferred1[base + lane_id()] = wbuf[lane_id()];
-        wave_lds_sync();
-        wn = 0;
-    };
-    for (uint32_t g = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6)); g < n_groups; g += nw)
-    {
-        // ---- one lane per (request, key) probe: lane 8h + j is key j of request 8g + h
-        const uint64_t t = (uint64_t)g * 8 + h;
-        const bool act = t < n;
-        const uint4 rec = b.q_rec[act ? t : 0];
-        const uint32_t k0 = rec.x, S = rec.y, np = rec.z & 0xFFFFu, cls = (rec.z >> 16) & 3u, self = rec.w;
-        const bool fast = (rec.z & REC_FAST) != 0;
-        const bool kact = act && fast && j < np;
-        const int64_t key = b.q_keys[kact ? (uint64_t)k0 + j : 0];
-        const uint32_t sl0 = b.p_slot[kact ? (uint64_t)k0 + j : 0];
-        const uint32_t sl = kact ? sl0 : LS_NONE;          // k_prepare: the key's line (LS_NONE: outside the slice)
-        if (kact) b.lg_keys[t * 8 + j] = key;
-        // the probe's 16 bytes of its line (threshold, counts, the two runs) and the line's key: the perfect
-        // hash puts every key of the store on its own line, any other key on some line whose key differs
-        const uint4* Q4 = reinterpret_cast<const uint4*>(s.kquad + (sl != LS_NONE ? sl : 0u));
-        const uint4 q = Q4[cls], qk = Q4[3];
-        const bool found = sl != LS_NONE && qk.z != 0 && (int64_t)(((uint64_t)qk.y << 32) | qk.x) == key;
-        // lean-served (as lean pass 1): S above the key's last committed Write's executeAt and prunedBefore
-        const bool newest = !found || S > q.x;
-        const uint32_t n1 = found ? (q.y & LQ_NMAX) : 0u, n2 = found ? ((q.y >> 8) & LQ_NMAX) : 0u;
-        const uint32_t nn = kact ? n1 + n2 : 0u;
-        const uint32_t inc = key_lanes_incl_scan(nn, j);
-        const uint32_t start = inc - nn;
-        const uint32_t T = (uint32_t)__shfl((int)inc, (int)(sb8 | 7u), 64);
-        const uint64_t seg8 = (ballot(kact && !newest) >> sb8) & 0xFFull;
-        const bool defer = act && (!fast || seg8 != 0 || T > GB_STAGE);
-        {
-            const uint64_t dm = ballot(defer && j == 0);
-            const uint32_t nd = __popcll(dm);
-            if (nd)
-            {
-                if (dn + nd > DEFER_CHUNK) dflush();
-                if (defer && j == 0) dbuf[dn + __popcll(dm & ((1ull << lane) - 1))] = (uint32_t)t;
-                dn += nd;
-            }
-        }
-        // requests of 33..64 raw emissions: the wide build's list (two per lane there)
-        const bool wide = act && !defer && T > 32;
-        {
-            const uint64_t wm = ballot(wide && j == 0);
-            const uint32_t nwd = __popcll(wm);
-            if (nwd)
-            {
-                if (wn + nwd > DEFER_CHUNK) wflush();
-                if (wide && j == 0) wbuf[wn + __popcll(wm & ((1ull << lane) - 1))] = (uint32_t)t;
-                wn += nwd;
-            }
-        }
-        // build record: raw count | #keys << 8 | wide | deferred, then the eight per-key starts (bytes)
-        if (act)
-        {
-            uint8_t* r8 = reinterpret_cast<uint8_t*>(b.lg_rec + t);
-            r8[4 + j] = (uint8_t)start;
-            if (j == 0)
-                *reinterpret_cast<uint32_t*>(r8) = (defer ? GB_DEFER : 0u) | (wide ? GB_WIDE : 0u) | (np << 8) | (defer ? 0u : T);
-        }
-        // ---- the raw emissions of the group's served requests, one per lane: consecutive lanes take
-        // consecutive elements of a run (coalesced loads) and write consecutive stage words
-        const uint32_t cnt = act && !defer ? nn : 0u;
-        const uint32_t ginc = wave_incl_scan_dpp(cnt);
-        const uint32_t gst = ginc - cnt;                  // the probe's first element in the group
-        const uint32_t E = uniform(__builtin_amdgcn_readlane((int)ginc, 63));
-        if (E == 0) continue;
-        // per probe, what its elements need (read by the element lanes through ds_bpermute)
-        const bool inl = (q.y & LQ_INLINE) != 0;
-        const uint32_t pk = gst | (n1 << 10) | (cls << 17) | (inl ? (1u << 19) : 0u) | (h << 20) | (start << 23);
-        const uint32_t pb1 = q.z, pb2 = q.w;
-        uint32_t carry = 0;                               // probe lane + 1 of the run open at the round's start
-        for (uint32_t r0 = 0; r0 < E; r0 += 64)
-        {
-            // mark the lanes where a run starts (lane + 1 of its probe), then a max scan: the probe of
-            // every element lane (runs are contiguous and in lane order)
-            const bool starts_here = cnt > 0 && gst >= r0 && gst < r0 + 64;
-            mk[lane] = 0;
-            wave_lds_sync();
-            if (starts_here) mk[gst - r0] = lane + 1;        // run starts are distinct
-            wave_lds_sync();
-            uint32_t mark = mk[lane];
-            wave_lds_sync();
-            mark = wave_incl_max_dpp(max(mark, lane == 0 ? carry : 0u));
-            carry = uniform(__builtin_amdgcn_readlane((int)mark, 63));
-            const uint32_t e = r0 + lane;
-            const bool on = e < E;
-            const int src = (int)(((mark ? mark - 1 : 0u)) << 2);
-            const uint32_t xk = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pk);
-            const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb1);
-            const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)pb2);
-            const uint32_t xS = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)S);
-            const uint32_t xself = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)self);
-            const uint32_t i = e - (xk & 0x3FFu);
-            const uint32_t xn1 = (xk >> 10) & 0x7Fu, xcls = (xk >> 17) & 3u;
-            const bool xinl = (xk >> 19) & 1u;
-            const bool fc = i < xn1;
-            // the element: the class list (cand or the line's inline words), then the cwr tail (idem), or for
-            // class Ws the last committed Write (its txw in the quad, no load)
-            const uint32_t* arr = xinl ? kl32 : (fc ? s.cand : s.cwr);
-            const uint32_t idx = fc ? x1 + i : x2 + (i - xn1);
-            const bool ld = on && (fc || xcls != 0);
-            const uint32_t v0 = (ld ? arr : s.cand)[ld ? idx : 0u];
-            const uint32_t v = fc || xcls != 0 ? v0 : x2;
-            const uint32_t r = v & RANK_MASK;
-            if (on)
-            {
-                const uint64_t tt = (uint64_t)g * 8 + ((xk >> 20) & 7u);
-                b.lg_stage[tt * GB_STAGE + ((xk >> 23) & 0x7Fu) + i] = (r < xS && r != xself) ? v : GB_INVALID;
-            }
-        }
-    }
-    dflush();
-    wflush();
-}
-
-#ifndef GB_OCC_BW
-#define GB_OCC_BW 5
-#endif
-// The build, one item = two requests (32 lanes each). WIDE: the requests of the wide list (33..64 raw
-// emissions, two per lane); else consecutive requests, those of at most 32. Every iteration issues the
-// same vector-memory instructions -- loads of the items two (the wide list's entries three) iterations
-// ahead, then a fixed sequence of stores whose disabled lanes write a per-wave dummy word -- so the
-// compiler's wait counts stay exact across the loop: a wait for an item's inputs never waits for the
-// stores just issued (vmcnt counts loads and stores in issue order).
-template <bool WIDE>
-__global__ __launch_bounds__(64 * LEAN_WAVES, WIDE ? GB_OCC_BW : GB_OCC_B) void k_lean_build(BatchBufs b)
-{
-    constexpr uint32_t LPR = 32;
-    const uint32_t lane = lane_id(), h = lane >> 5, hl = lane & 31u, sb = h * LPR;
-    const uint64_t below = (1ull << hl) - 1;
-    auto seg = [&](uint64_t m) -> uint64_t { return (m >> sb) & 0xFFFFFFFFull; };
-    const uint64_t n = b.n_txns;
-    const uint32_t n_slots = WIDE ? (uint32_t)uniform64(b.ctl->n_deferred1) : (uint32_t)n;
-    const uint32_t n_items = (n_slots + 1) / 2;
-    const uint32_t nw = gridDim.x * LEAN_WAVES;
-    const uint64_t reg_cap = uniform64(b.ctl->reg_cap);
-    const uint32_t wid = uniform(blockIdx.x * LEAN_WAVES + (threadIdx.x >> 6));
-    uint64_t* const dummy = b.lg_dummy + (uint64_t)wid * 16;     // one 128-byte line per wave
-    LeanChunk ralloc;
-    auto seg_alloc = [&](uint64_t bytes, bool& fits, uint32_t it) -> uint64_t {
-        const uint64_t b0 = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)bytes, 0) |
-                            ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(bytes >> 32), 0) << 32);
-        const uint64_t b1 = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)bytes, 32) |
-                            ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(bytes >> 32), 32) << 32);
-        const uint64_t base = ralloc.template take<1>(b.ctl, b0 + b1, reg_cap, it, n_items, nw);
-        fits = base + b0 + b1 <= reg_cap;
-        return base + (h ? b0 : 0);
-    };
-    // stores with every lane issuing: a disabled lane writes the wave's dummy word
-    auto st32 = [&](uint32_t* p, bool on, uint32_t v) { *(on ? p : reinterpret_cast<uint32_t*>(dummy)) = v; };
-    auto st64 = [&](uint64_t* p, bool on, uint64_t v) { *(on ? p : dummy) = v; };
-    auto put_sizes = [&](bool on, uint64_t t, int m, uint32_t v0, uint32_t v1, uint32_t v2, uint64_t ro) {
-        const uint32_t v = hl == 0 ? v0 : (hl == 1 ? v1 : v2);
-        st32(b.sz + (uint64_t)(3 * m + (hl < 3 ? hl : 0)) * n + t, on && hl < 3, v);
-        st64(b.t_reg + (uint64_t)m * n + t, on && hl == 3, ro);
-    };
-    struct In { uint4 r; uint32_t e0, e1; int64_t key; uint32_t t; };
-    auto load = [&](uint32_t t) -> In {
-        const uint64_t tt = t < n ? t : 0;
-        In x;
-        x.t = t;
-        x.r = b.lg_rec[tt];
-        x.e0 = b.lg_stage[tt * GB_STAGE + hl];
-        x.e1 = WIDE ? b.lg_stage[tt * GB_STAGE + LPR + hl] : 0u;
-        x.key = b.lg_keys[tt * 8 + (hl & 7u)];
-        return x;
-    };
-    // the request of item `it` in this half: the list entry (wide) or its index
-    auto list_at = [&](uint32_t it) -> uint32_t {
-        const uint32_t si = it * 2 + h;
-        if (!WIDE) return si < n_slots ? si : DEFER_HOLE;
-        const uint32_t v = b.deferred1[si < n_slots ? si : 0u];
-        return si < n_slots ? v : DEFER_HOLE;
-    };
-    auto process = [&](const In& cur, uint32_t it) {
-        const uint64_t t = cur.t != DEFER_HOLE ? cur.t : 0;
-        const uint32_t x = cur.r.x;
-        const bool act = cur.t != DEFER_HOLE && !(x & GB_DEFER) && (WIDE || !(x & GB_WIDE));
-        const uint32_t T = act ? (x & 0xFFu) : 0u, np = (x >> 8) & 0xFu;
-        auto start_of = [&](uint32_t p) -> uint32_t { return ((p < 4 ? cur.r.y : cur.r.z) >> (8 * (p & 3))) & 0xFFu; };
-        const uint32_t kj = hl & 7u;
-        const uint32_t start = start_of(kj);
-        const uint32_t nn = !act || hl >= 8 || kj >= np ? 0u : (kj + 1 < np ? start_of(kj + 1) : T) - start;
-        auto key_of = [&](uint32_t e) -> uint32_t {
-            uint32_t a = 0;
-#pragma unroll
-            for (uint32_t p = 1; p < LEAN_MAXP; ++p)
-                if (p < np && e >= start_of(p)) a = p;
-            return a;
-        };
-        const int64_t key = cur.key;
-        const uint32_t tmax = max(uniform(__builtin_amdgcn_readlane((int)T, 0)), uniform(__builtin_amdgcn_readlane((int)T, 32)));
-        const uint32_t tw0 = act && hl < T ? cur.e0 : GB_INVALID;
-        const uint32_t tw1 = WIDE && act && hl + 32 < T ? cur.e1 : GB_INVALID;
-        const uint32_t ax0 = key_of(hl), ax1 = WIDE ? key_of(hl + 32) : 0u;
-        const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
-        const bool want0 = tw0 != GB_INVALID, want1 = tw1 != GB_INVALID;
-        const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
-        const bool is1_1 = ((KINDS_RS_OR_WS >> (tw1 >> RANK_BITS)) & 1) == 0;
-#pragma unroll
-        for (int m = 0; m < 3; m += 2)
-        {
-            const bool mine0 = want0 && (m == 0 ? !is1_0 : is1_0), mine1 = want1 && (m == 0 ? !is1_1 : is1_1);
-            const uint64_t mb0 = ballot(mine0), mb1 = WIDE ? ballot(mine1) : 0ull;
-            const uint32_t tot = __popcll(seg(mb0)) + (WIDE ? __popcll(seg(mb1)) : 0u);
-            // the map's CSR: values sorted and deduplicated, per key its positions (VALU only; the stores
-            // below are issued whatever the branch)
-            uint32_t x0 = 0, x1 = 0, ka0 = 0, ka1 = 0, U = 0, ur0 = 0, ur1 = 0, pk0 = 0, pk1 = 0, cnt = 0, kstart_l = 0, nk = 0,
-                     kk = 0, kst0 = 0, kst1 = 0;
-            bool u0 = false, u1 = false, v0 = false, v1 = false;
-            if ((mb0 | mb1) != 0)
-            {
-                uint32_t k0 = mine0 ? ((r0 << 3) | ax0) : 0xFFFFFFFFu, k1 = mine1 ? ((r1 << 3) | ax1) : 0xFFFFFFFFu;
-                if (WIDE) seg_bitonic_wide(k0, k1);
-                else if (tmax <= 8) seg_bitonic<8, LPR>(k0);
-                else if (tmax <= 16) seg_bitonic<16, LPR>(k0);
-                else seg_bitonic<32, LPR>(k0);
-                v0 = hl < tot;
-                v1 = WIDE && hl + 32 < tot;
-                x0 = k0 >> 3; x1 = k1 >> 3; ka0 = k0 & 7u; ka1 = k1 & 7u;
-                const uint32_t p0 = wave_up1(k0);
-                u0 = v0 && (hl == 0 || (p0 >> 3) != x0);
-                const uint64_t um0 = seg(ballot(u0));
-                const uint32_t nu0 = __popcll(um0);
-                ur0 = __popcll(um0 & below) + (u0 ? 1u : 0u) - 1u;
-                U = nu0;
-                uint64_t s00 = ballot(v0), s01 = ballot(v0), s11 = WIDE ? ballot(v1) : 0ull;
-                if (WIDE)
-                {
-                    const uint32_t last0 = (uint32_t)__builtin_amdgcn_readlane((int)k0, 31), last0b = (uint32_t)__builtin_amdgcn_readlane((int)k0, 63);
-                    const uint32_t up1 = wave_up1(k1);
-                    const uint32_t p1 = hl == 0 ? (h ? last0b : last0) : up1;
-                    u1 = v1 && (p1 >> 3) != x1;
-                    const uint64_t um1 = seg(ballot(u1));
-                    U = nu0 + __popcll(um1);
-                    ur1 = nu0 + __popcll(um1 & below) + (u1 ? 1u : 0u) - 1u;
-                }
-#pragma unroll
-                for (int bit = 0; bit < 3; ++bit)
-                {
-                    const uint64_t b0 = ballot((ka0 >> bit) & 1u);
-                    s00 &= ((ka0 >> bit) & 1u) ? b0 : ~b0;
-                    if (WIDE)
-                    {
-                        const uint64_t b1 = ballot((ka1 >> bit) & 1u);
-                        s01 &= ((ka1 >> bit) & 1u) ? b0 : ~b0;
-                        s11 &= ((ka1 >> bit) & 1u) ? b1 : ~b1;
-                    }
-                }
-                pk0 = __popcll(seg(s00) & below);
-                pk1 = WIDE ? __popcll(seg(s01)) + __popcll(seg(s11) & below) : 0u;
-                const uint64_t raw_m = seg(mb0) | (WIDE ? (seg(mb1) << 32) : 0ull);
-                const uint64_t rmask = nn >= 64 ? ~0ull : (((1ull << nn) - 1) << start);
-                cnt = hl < 8 ? (uint32_t)__popcll(raw_m & rmask) : 0u;
-                const uint32_t cinc = key_lanes_incl_scan(cnt, hl);
-                kstart_l = cinc - cnt;
-                const uint64_t nem = seg(ballot(hl < 8 && cnt > 0));
-                nk = __popcll(nem);
-                kk = __popcll(nem & below);
-                kst0 = __shfl(kstart_l, sb | ka0, 64);
-                kst1 = WIDE ? __shfl(kstart_l, sb | ka1, 64) : 0u;
-            }
-            const uint64_t bytes = act && tot ? (((uint64_t)nk * 8 + (uint64_t)U * 4 + (uint64_t)(nk + tot) * 4 + 7) & ~7ull) : 0;
-            bool fits;
-            const uint64_t ro = seg_alloc(bytes, fits, it);
-            const bool wr = act && tot && fits;
-            put_sizes(act, t, m, fits ? nk : 0, fits ? U : 0, fits ? nk + tot : 0, ro);
-            int64_t* okeys = reinterpret_cast<int64_t*>(b.reg + ro);
-            uint32_t* otx = reinterpret_cast<uint32_t*>(okeys + nk);
-            int32_t* ok2t = reinterpret_cast<int32_t*>(otx + U);
-            const bool kw = wr && hl < 8 && cnt > 0;
-            st64(reinterpret_cast<uint64_t*>(okeys + kk), kw, (uint64_t)key);
-            st32(reinterpret_cast<uint32_t*>(ok2t + kk), kw, nk + kstart_l + cnt);     // absolute end offsets (RelationMultiMap.java:245-257)
-            st32(otx + ur0, wr && u0, (x0 - 1) >> 1);                                // dictionary index of the TxnId
-            st32(reinterpret_cast<uint32_t*>(ok2t + nk + kst0 + pk0), wr && v0, ur0);
-            if (WIDE)
-            {
-                st32(otx + ur1, wr && u1, (x1 - 1) >> 1);
-                st32(reinterpret_cast<uint32_t*>(ok2t + nk + kst1 + pk1), wr && v1, ur1);
-            }
-        }
-        put_sizes(act, t, 1, 0, 0, 0, 0);            // no range commands on this path
-    };
-    // two items per trip, ping-pong input buffers (no register copies between a load and its use: a copy
-    // would wait for the load), each refilled right after its item is built
-    const uint32_t it0 = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6));
-    uint32_t la = list_at(it0 + 2 * nw), lb = list_at(it0 + 3 * nw);
-    In X = load(list_at(it0)), Y = load(list_at(it0 + nw));
-    for (uint32_t it = it0; it < n_items; it += 2 * nw)
-    {
-        process(X, it);
-        X = load(la);
-        la = list_at(it + 4 * nw);
-        if (it + nw >= n_items) break;
-        process(Y, it + nw);
-        Y = load(lb);
-        lb = list_at(it + 5 * nw);
-    }
-}
-
-hipError_t run_lean_gb(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
-{
-    if (!b.n_txns) return hipSuccess;
-    if (!b.p_slot || !b.lg_stage || !b.lg_rec || !b.lg_keys || !b.lg_dummy || s.n_rent) return hipErrorInvalidValue;
-    if (!b.slots_by_prepare && b.n_probes)
-        k_lean_slots<<<(unsigned)((b.n_probes + 255) / 256), 256, 0, st>>>(s, b.q_keys, b.n_probes, b.p_slot);
-    static int per_cu_g = 0, per_cu_b = 0, per_cu_w = 0;
-    if (!per_cu_g)
-    {
-        int nb = 0;
-        per_cu_g = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_gather, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
-        nb = 0;
-        per_cu_b = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_build<false>, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
-        nb = 0;
-        per_cu_w = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_lean_build<true>, 64 * LEAN_WAVES, 0) == hipSuccess && nb > 0 ? nb : 2;
-        if (const char* e = getenv("AD_GB_PER_CU_G")) per_cu_g = std::max(1, std::min(per_cu_g, atoi(e)));
-        if (const char* e = getenv("AD_GB_PER_CU_B")) per_cu_b = std::max(1, std::min(per_cu_b, atoi(e)));
-    }
-    const uint64_t cus = (uint64_t)device_cu_count();
-    const uint64_t need_g = ((b.n_txns + 7) / 8 + LEAN_WAVES - 1) / LEAN_WAVES;
-    const unsigned grid_g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need_g, cus * per_cu_g));
-    k_lean_gather<<<grid_g, 64 * LEAN_WAVES, 0, st>>>(s, b);
-    const uint64_t need_b = ((b.n_txns + 1) / 2 + LEAN_WAVES - 1) / LEAN_WAVES;
-    const unsigned grid_b = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need_b, cus * per_cu_b));
-    k_lean_build<false><<<grid_b, 64 * LEAN_WAVES, 0, st>>>(b);
-    // the wide list's length is on the device: a grid for up to an eighth of the batch, grid-strided
-    const uint64_t need_w = ((b.n_txns / 8 + 1) / 2 + LEAN_WAVES - 1) / LEAN_WAVES;
-    const unsigned grid_w = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(need_w, cus * per_cu_w));
-    k_lean_build<true><<<grid_w, 64 * LEAN_WAVES, 0, st>>>(b);
-    return hipGetLastError();
-}
 
 }  // namespace adx

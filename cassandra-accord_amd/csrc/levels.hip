@@ -42,18 +42,10 @@ constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_CHUNKS = 16;                       // 64-element chunks per wave
 constexpr int RS_TILE = RS_THREADS * RS_CHUNKS;     // 4096 elements per block
 
-// onesweep tiles (below): 2048 elements per 256-thread block
-constexpr int OS_THREADS = 256;
-constexpr int OS_WAVES = OS_THREADS / 64;
-constexpr int OS_CHUNKS = 8;                        // 64-element chunks per wave
-constexpr int OS_TILE = OS_THREADS * OS_CHUNKS;     // 2048
-constexpr uint64_t OS_HIST_EXTRA = 17 * 256;        // hist: global digit counts [8][256], bases [8][256], tickets [8]
-
 uint64_t radix_hist_entries(uint64_t n)
 {
-    // the per-pass path: 256 * tiles of RS_TILE; the onesweep path: its status words (u64, in `off`) per
-    // OS_TILE tile, its global counts / bases / tickets (u32, in `hist`)
-    return 256 * std::max<uint64_t>(1, (n + OS_TILE - 1) / OS_TILE) + OS_HIST_EXTRA;
+    // 256 digit counts per RS_TILE tile
+    return 256 * std::max<uint64_t>(1, (n + RS_TILE - 1) / RS_TILE);
 }
 
 // per block digit counts -> hist[d * nblk + b] (digit-major, so one flat exclusive scan gives
@@ -138,211 +130,13 @@ __global__ __launch_bounds__(RS_THREADS) void k_radix_scatter(const uint64_t* __
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Onesweep LSD radix sort: the global digit counts of every sorted digit in one pass over the keys,
-// then ONE kernel per digit that ranks its 2048-element tile, publishes the tile's per-digit counts,
-// takes its per-digit base by a decoupled look-back over the earlier tiles' published counts and
-// scatters through an LDS reorder (runs of equal digits leave as consecutive addresses). Tiles are
-// numbered by ticket in dispatch order, so a tile only waits on tiles whose blocks already run and
-// publish before they wait: no deadlock. A status word is (flag << 62 | pass tag << 32 | count):
-// flag 1 the tile's own count, 2 the inclusive prefix through the tile; the words are zeroed once per
-// sort and a word of an earlier pass carries an older tag. Agent-scope relaxed stores and polls (the
-// single-word hand-off of MI355X_MICROARCH.md: the word is its own flag).
-// ---------------------------------------------------------------------------------------------
-constexpr uint64_t OS_AGG = 1ull << 62, OS_PRE = 2ull << 62;
-
-__global__ __launch_bounds__(256) void k_os_ghist(const uint64_t* __restrict__ k, uint64_t n, uint32_t digit_mask,
-                                                  uint32_t* __restrict__ ghist)
-{
-    __shared__ uint32_t h[8][256];
-    for (int i = threadIdx.x; i < 8 * 256; i += 256) (&h[0][0])[i] = 0;
-    __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    {
-        const uint64_t x = k[i];
-#pragma unroll
-        for (int d = 0; d < 8; ++d)
-            if ((digit_mask >> d) & 1u) atomicAdd(&h[d][(uint32_t)(x >> (8 * d)) & 255u], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 8 * 256; i += 256)
-        if ((digit_mask >> (i >> 8)) & 1u)
-        {
-            const uint32_t c = (&h[0][0])[i];
-            if (c) atomicAdd(&ghist[i], c);
-        }
-}
-
-// exclusive scan of v over the 256 threads of the block (ws: LDS [4])
-__device__ __forceinline__ uint32_t block256_excl_scan(uint32_t v, uint32_t* ws)
-{
-    const uint32_t inc = wave_incl_scan(v);
-    if (lane_id() == 63) ws[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) before += ws[w];
-    __syncthreads();
-    return before + inc - v;
-}
-
-__global__ __launch_bounds__(256) void k_os_gscan(const uint32_t* __restrict__ ghist, uint32_t digit_mask,
-                                                  uint32_t* __restrict__ gbase)
-{
-    __shared__ uint32_t ws[4];
-    for (int d = 0; d < 8; ++d)
-    {
-        if (!((digit_mask >> d) & 1u)) continue;
-        gbase[d * 256 + threadIdx.x] = block256_excl_scan(ghist[d * 256 + threadIdx.x], ws);
-    }
-}
-
-__global__ __launch_bounds__(OS_THREADS) void k_onesweep(const uint64_t* __restrict__ k, const uint32_t* __restrict__ v,
-                                                         uint64_t n, int shift, uint32_t tag,
-                                                         const uint32_t* __restrict__ gbase, uint64_t* status,
-                                                         uint32_t* ticket, uint64_t* __restrict__ ko, uint32_t* __restrict__ vo)
-{
-    __shared__ uint64_t sk[OS_TILE];
-    __shared__ uint32_t sv[OS_TILE];
-    __shared__ uint32_t wcnt[OS_WAVES][256];
-    __shared__ uint32_t dstart[256], dglob[256], ws[4];
-    __shared__ uint32_t tile_s;
-    const uint32_t t = threadIdx.x, w = t >> 6, lane = lane_id();
-    if (t == 0) tile_s = atomicAdd(ticket, 1u);
-    for (int i = t; i < OS_WAVES * 256; i += OS_THREADS) (&wcnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint64_t tile = tile_s;
-    const uint64_t base = tile * OS_TILE + (uint64_t)w * (OS_CHUNKS * 64);
-    uint64_t key[OS_CHUNKS];
-    uint32_t val[OS_CHUNKS], rk[OS_CHUNKS];
-#pragma unroll
-    for (int c = 0; c < OS_CHUNKS; ++c)
-    {
-        const uint64_t i = base + (uint64_t)c * 64 + lane;
-        key[c] = i < n ? k[i] : 0;
-        val[c] = i < n ? v[i] : 0;
-    }
-    // stable rank of each element among the wave's elements of its digit (chunk order, then lane)
-    const uint64_t lt = (1ull << lane) - 1;
-#pragma unroll
-    for (int c = 0; c < OS_CHUNKS; ++c)
-    {
-        const bool live = base + (uint64_t)c * 64 + lane < n;
-        const uint32_t d = (uint32_t)(key[c] >> shift) & 255u;
-        uint64_t m = ballot(live);
-#pragma unroll
-        for (int bit = 0; bit < 8; ++bit)
-        {
-            const uint64_t b = ballot((d >> bit) & 1u);
-            m &= ((d >> bit) & 1u) ? b : ~b;
-        }
-        const uint32_t pos0 = live ? wcnt[w][d] : 0u;
-        wave_lds_sync();
-        rk[c] = pos0 + (uint32_t)__popcll(m & lt);
-        if (live && (m >> lane) == 1ull) wcnt[w][d] = pos0 + (uint32_t)__popcll(m);    // highest lane of its digit
-        wave_lds_sync();
-    }
-    __syncthreads();
-    // digit t: the tile's count, the waves' exclusive prefixes
-    uint32_t tot = 0;
-#pragma unroll
-    for (int ww = 0; ww < OS_WAVES; ++ww)
-    {
-        const uint32_t c = wcnt[ww][t];
-        wcnt[ww][t] = tot;
-        tot += c;
-    }
-    // publish, then look back for the digit's count over every earlier tile
-    const uint64_t tg = (uint64_t)tag << 32;
-    uint64_t* my = status + tile * 256 + t;
-    uint32_t excl = 0;
-    if (tile == 0)
-        __hip_atomic_store(my, OS_PRE | tg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-    {
-        __hip_atomic_store(my, OS_AGG | tg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t j = tile - 1;
-        while (true)
-        {
-            const uint64_t sw = __hip_atomic_load(status + j * 256 + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (((sw >> 32) & 0x3FFFFFFFull) != tag || (sw >> 62) == 0)
-            {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            excl += (uint32_t)sw;
-            if ((sw >> 62) == 2 || j == 0) break;
-            --j;
-        }
-        __hip_atomic_store(my, OS_PRE | tg | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const uint32_t ds = block256_excl_scan(tot, ws);
-    dstart[t] = ds;
-    dglob[t] = gbase[t] + excl;
-    __syncthreads();
-    // local order: digit, then wave, then the wave's rank
-#pragma unroll
-    for (int c = 0; c < OS_CHUNKS; ++c)
-    {
-        const uint64_t i = base + (uint64_t)c * 64 + lane;
-        if (i < n)
-        {
-            const uint32_t d = (uint32_t)(key[c] >> shift) & 255u;
-            const uint32_t lp = dstart[d] + wcnt[w][d] + rk[c];
-            sk[lp] = key[c];
-            sv[lp] = val[c];
-        }
-    }
-    __syncthreads();
-    const uint64_t t0 = tile * OS_TILE;
-    const uint32_t tn = (uint32_t)std::min<uint64_t>(OS_TILE, n - t0);
-    for (uint32_t i = t; i < tn; i += OS_THREADS)
-    {
-        const uint64_t x = sk[i];
-        const uint32_t d = (uint32_t)(x >> shift) & 255u;
-        const uint64_t pos = (uint64_t)dglob[d] + (i - dstart[d]);
-        ko[pos] = x;
-        vo[pos] = sv[i];
-    }
-}
-
 hipError_t radix_sort_pairs(uint64_t* k_in, uint32_t* v_in, uint64_t* k_tmp, uint32_t* v_tmp, uint64_t n,
                             uint32_t digit_mask, uint32_t* hist, uint64_t* off, uint64_t* bsum, hipStream_t st,
                             uint64_t** k_res, uint32_t** v_res)
 {
-    // onesweep measured no faster on the K5 sorts (1M-4M elements: 0.039 ms per digit against 0.052 for
-    // count + scan + scatter, but the global count pass and two fills per sort eat the difference): opt-in
-    const bool onesweep = getenv("AD_RADIX_ONESWEEP") != nullptr;     // read per call (tests switch it)
-    if (onesweep && n > 1 && n < (1ull << 31) && digit_mask)
-    {
-        const uint64_t tiles = (n + OS_TILE - 1) / OS_TILE;
-        uint32_t* ghist = hist;
-        uint32_t* gbase = hist + 8 * 256;
-        uint32_t* tickets = hist + 16 * 256;
-        hipError_t e;
-        if ((e = hipMemsetAsync(hist, 0, 4 * OS_HIST_EXTRA, st)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(off, 0, 8 * 256 * tiles, st)) != hipSuccess) return e;
-        // few blocks: each flushes its counts with one atomic per (digit, value), all onto the same 2 KB
-        const unsigned gb = (unsigned)std::min<uint64_t>(128, (n + 4095) / 4096);
-        k_os_ghist<<<gb, 256, 0, st>>>(k_in, n, digit_mask, ghist);
-        k_os_gscan<<<1, 256, 0, st>>>(ghist, digit_mask, gbase);
-        uint64_t* ka = k_in;
-        uint32_t* va = v_in;
-        uint64_t* kb = k_tmp;
-        uint32_t* vb = v_tmp;
-        uint32_t tag = 0;
-        for (int d = 0; d < 8; ++d)
-        {
-            if (!((digit_mask >> d) & 1u)) continue;
-            ++tag;
-            k_onesweep<<<(unsigned)tiles, OS_THREADS, 0, st>>>(ka, va, n, 8 * d, tag, gbase + 256 * d, off, tickets + d, kb, vb);
-            std::swap(ka, kb);
-            std::swap(va, vb);
-        }
-        *k_res = ka;
-        *v_res = va;
-        return hipGetLastError();
-    }
-
+    // (a onesweep variant -- one kernel per digit with a decoupled look-back -- measured no faster on the K5
+    // sorts: 0.039 ms per digit against 0.052 for count + scan + scatter, but its global count pass and two
+    // fills per sort ate the difference; deleted in round 6)
     uint64_t* ka = k_in;
     uint32_t* va = v_in;
     uint64_t* kb = k_tmp;
@@ -1147,28 +941,13 @@ __device__ __forceinline__ uint32_t lv_poll(const uint32_t* p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// LOCAL: every hand-off stays inside one XCD. The first block to start names its XCD (HW_REG_XCC_ID)
-// the owner; blocks on any other XCD leave at once, so the owner's CUs share one L2. Levels are then
-// stored sc0 (the line stays in that L2) and polled sc1 (L1 bypassed, L2-served): a hand-off costs an
-// L2 round trip instead of a trip through the fabric. Placement decides only which blocks work.
-template <bool LOCAL>
+// (An XCD-local variant -- blocks off the first block's XCD leaving, levels stored sc0 and polled sc1 so a
+// hand-off stays in one L2 -- measured 0.60 / 0.86 / 1.13 ms at 2 / 4 / 8 waves per CU of the owner XCD against
+// 0.59 on all CUs; deleted in round 6.)
 __global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* __restrict__ pred_off,
                                                     const uint32_t* __restrict__ pred, uint32_t* level, uint32_t* ticket,
-                                                    uint32_t* fail, uint64_t budget, uint32_t naps, uint32_t* owner)
+                                                    uint32_t* fail, uint64_t budget, uint32_t naps)
 {
-    if (LOCAL)
-    {
-        __shared__ uint32_t own_s;
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        if (threadIdx.x == 0)
-        {
-            const uint32_t o = atomicCAS(owner, 0u, xcc + 1u);
-            own_s = o == 0u ? xcc + 1u : o;
-        }
-        __syncthreads();
-        if (own_s != xcc + 1u) return;
-    }
     const uint32_t lane = lane_id();
     const uint64_t t_end = wall_clock64() + budget;
     while (true)
@@ -1227,8 +1006,7 @@ __global__ __launch_bounds__(256) void k_level_pull(uint64_t n, const uint64_t* 
                     j += nb;
                     if (j >= e)
                     {
-                        if (LOCAL) __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        else __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         pending = false;
                         break;
                     }
@@ -1259,27 +1037,13 @@ __device__ __forceinline__ uint32_t sel4(uint32_t i, uint32_t a, uint32_t b, uin
     return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
 
-template <bool LOCAL>
 __global__ __launch_bounds__(256) void k_level_rec(LevelsIn g, const uint64_t* __restrict__ occ_off,
                                                    const uint4* __restrict__ rec, const uint4* __restrict__ rec2,
                                                    const uint32_t* __restrict__ pool, uint64_t pool_cap,
                                                    const uint32_t* __restrict__ dirp, const uint32_t* __restrict__ rank,
                                                    uint32_t* level, uint32_t* ticket, uint32_t* fail, uint64_t budget,
-                                                   uint32_t naps, uint32_t* owner, uint32_t kuni)
+                                                   uint32_t naps, uint32_t kuni)
 {
-    if (LOCAL)
-    {
-        __shared__ uint32_t own_s;
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        if (threadIdx.x == 0)
-        {
-            const uint32_t o = atomicCAS(owner, 0u, xcc + 1u);
-            own_s = o == 0u ? xcc + 1u : o;
-        }
-        __syncthreads();
-        if (own_s != xcc + 1u) return;
-    }
     const uint64_t n = g.n;
     const uint32_t lane = lane_id();
     const uint64_t t_end = wall_clock64() + budget;
@@ -1481,8 +1245,7 @@ __global__ __launch_bounds__(256) void k_level_rec(LevelsIn g, const uint64_t* _
                     if (pend) break;
                     if (ph == 3)
                     {
-                        if (LOCAL) __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        else __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(level + T, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         pending = false;
                         break;
                     }
@@ -1565,9 +1328,8 @@ constexpr unsigned STEP_BLOCKS = 64;
 
 static unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)std::max<uint64_t>(1, (n + t - 1) / t); }
 
-// leveling launch: the fabric dataflow (one wave per CU) or the XCD-local one (AD_LEVELS_LOCAL)
+// leveling launch of the rank-ordered dataflow
 struct PullCfg {
-    bool local;
     unsigned grid, threads;
     uint32_t naps;
     uint64_t budget;
@@ -1583,20 +1345,16 @@ static PullCfg pull_cfg(uint64_t n, bool packed)
     // (0.59 ms; a 256-thread block per CU or 2 / 4 blocks were slower in round 4: the polls of more
     // resident waiters load the memory system the hand-offs go through); the record kernel, whose
     // per-task setup is longer, at four waves per CU (0.60 ms; 1.00 / 0.62 at one / two)
-    const char* le = getenv("AD_LEVELS_LOCAL");
     PullCfg c;
-    c.local = le && atoi(le) != 0;
-    int per_cu = c.local ? 2 : (packed ? 4 : 1), naps = 1, threads = c.local ? 256 : 64;
+    int per_cu = packed ? 4 : 1, threads = 64;
+    // tests vary the residency (every wave count must give the same levels)
     if (const char* e = getenv("AD_LEVELS_PULL_PER_CU")) per_cu = std::max(1, std::min(8, atoi(e)));
-    if (const char* e = getenv("AD_LEVELS_PULL_NAPS")) naps = std::max(0, std::min(64, atoi(e)));
     if (const char* e = getenv("AD_LEVELS_PULL_THREADS")) threads = atoi(e) == 64 ? 64 : (atoi(e) == 128 ? 128 : 256);
     c.threads = (unsigned)threads;
-    c.naps = (uint32_t)naps;
+    c.naps = 1;
     c.budget = (uint64_t)std::max(khz, 1000) * 1000ull;       // one second of wall clock
     const uint64_t tasks = (n + threads - 1) / threads;
-    // local: blocks are dealt over the 8 XCDs, so 8x the blocks wanted on the owner
-    c.grid = c.local ? std::max(8u, (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, 8 * tasks))
-                     : std::max(1u, (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, tasks));
+    c.grid = std::max(1u, (unsigned)std::min<uint64_t>((uint64_t)cus * per_cu, tasks));
     return c;
 }
 
@@ -1800,12 +1558,7 @@ int run_levels(LevelsWork* w, const LevelsIn& g, uint32_t* level_out, hipStream_
     {
         const PullCfg pc = pull_cfg(n, false);
         LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
-        if (pc.local)
-            k_level_pull<true><<<pc.grid, pc.threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, pc.budget, pc.naps,
-                                                               cnt + 3);
-        else
-            k_level_pull<false><<<pc.grid, pc.threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, pc.budget, pc.naps,
-                                                                nullptr);
+        k_level_pull<<<pc.grid, pc.threads, 0, st>>>(n, succ_off, succ, level, cnt, cnt + 1, pc.budget, pc.naps);
         LV_CHK(hipGetLastError());
         out->n_launch = 1;
         k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);
@@ -1942,12 +1695,8 @@ static int run_levels_packed(LevelsWork* w, const LevelsIn& g, const PackPlan& p
         // ---- 3. level the DAG (rank-ordered dataflow over the records)
         LV_CHK(hipMemsetAsync(level, 0xFF, 4 * n, st));
         const uint64_t pool_cap = shard_cap * NSHARD;
-        if (pc.local)
-            k_level_rec<true><<<pc.grid, pc.threads, 0, st>>>(g, occ_off, rec, rec2, pool, pool_cap, dirp, rank, level, cnt, cnt + 1,
-                                                              pc.budget, pc.naps, cnt + 3, c.kuni);
-        else
-            k_level_rec<false><<<pc.grid, pc.threads, 0, st>>>(g, occ_off, rec, rec2, pool, pool_cap, dirp, rank, level, cnt,
-                                                               cnt + 1, pc.budget, pc.naps, nullptr, c.kuni);
+        k_level_rec<<<pc.grid, pc.threads, 0, st>>>(g, occ_off, rec, rec2, pool, pool_cap, dirp, rank, level, cnt, cnt + 1,
+                                                    pc.budget, pc.naps, c.kuni);
         LV_CHK(hipGetLastError());
         out->n_launch = 1;
         k_level_max<<<256, 256, 0, st>>>(level, n, cnt + 2);

@@ -43,8 +43,7 @@ int run_levels(LevelsWork* w, const LevelsIn& in, uint32_t* level_out, hipStream
 // Stable LSD radix sort of (key, val) pairs by the key bits in `digit_mask` (bit d = sort on
 // bits [8d, 8d+8)); the result ends in (*k_res, *v_res). k_tmp/v_tmp: scratch of n entries,
 // hist: radix_hist_entries(n) u32, off: that + 1 u64, bsum: scan scratch (per-pass path only).
-// Count / scan / scatter kernels per digit; AD_RADIX_ONESWEEP: one kernel per digit with a decoupled
-// look-back (below 2^31 elements).
+// Count / scan / scatter kernels per digit.
 hipError_t radix_sort_pairs(uint64_t* k_in, uint32_t* v_in, uint64_t* k_tmp, uint32_t* v_tmp, uint64_t n,
                             uint32_t digit_mask, uint32_t* hist, uint64_t* off, uint64_t* bsum, hipStream_t st,
                             uint64_t** k_res, uint32_t** v_res);

@@ -921,8 +921,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
 // one thread per probe (the first n_txns threads also write the request records).
 
 // SLOTS: the same launch also gives every probe its KeyLine for the lean passes (one thread per
-// probe: the slice test, then the perfect hash; 0xFFFFFFFF outside the slices) -- k_lean_slots' work
-// without a launch of its own
+// probe: the slice test, then the perfect hash; 0xFFFFFFFF outside the slices)
 // PREP_PPT probes per thread (block-strided: probe blockIdx.x * 256 * PREP_PPT + j * 256 + tid, each j a
 // coalesced pass), their key and displacement loads issued together
 #ifndef PREP_PPT
@@ -998,7 +997,7 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 
 hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
-    if (b.p_slot && b.slots_by_prepare)
+    if (b.p_slot)
     {
         const uint64_t m = std::max<uint64_t>(b.n_txns, (b.n_probes + PREP_PPT - 1) / PREP_PPT);
         if (m) k_prepare<true><<<(unsigned)((m + 255) / 256), 256, 0, st>>>(s, b);
@@ -1023,23 +1022,6 @@ hipError_t run_resolve(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
     const uint64_t need = (b.n_txns + FWAVES - 1) / FWAVES;
     const unsigned grid = (unsigned)std::min<uint64_t>(need, (uint64_t)device_cu_count() * per_cu);
     k_resolve<<<grid, 64 * FWAVES, 0, st>>>(s, b);
-    return hipGetLastError();
-}
-
-// the lean passes' deferrals straight to the split kernels' list (AD_DEFER_SPLIT: a measurement switch)
-__global__ void k_defer_append(BatchBufs b)
-{
-    const uint64_t nd = b.ctl->n_deferred2;
-    const uint64_t base = b.ctl->n_deferred;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += (uint64_t)gridDim.x * blockDim.x)
-        b.deferred[base + i] = b.deferred2[i];
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&b.ctl->n_deferred, (unsigned long long)nd);
-}
-
-hipError_t run_defer_append(const BatchBufs& b, hipStream_t st)
-{
-    k_defer_append<<<1, 1024, 0, st>>>(b);
     return hipGetLastError();
 }
 

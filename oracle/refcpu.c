@@ -778,7 +778,7 @@ static int collect_find_or_insert(collect_vec_t* col, const rkey_t* r)
 
 /* Routables.foldl(ranges, sliced keys, ...) (Routables.java:148-156) visiting each range of a
  * command that contains at least one sliced key, then the collect fold of
- * InMemoryCommandStore.java:950-956 */
+ * InMemoryCommandStore.java:954-961 */
 static void collect_command(const rc_store* s, collect_vec_t* col, const rcmd_t* c,
                             const int64_t* sliced, size_t nsliced, const rkey_t* rsliced, size_t nrsliced)
 {
@@ -814,12 +814,12 @@ static int map_reduce_ranges_internal(const rc_store* s, const int64_t* keys, si
     for (size_t i = 0; i < s->cmds.n; ++i)
     {
         const rcmd_t* c = &s->cmds.v[i];
-        if (c->erased) continue;                                        /* saveStatus >= Erased, :897 */
-        if (tid_cmp(&c->txnId, testTimestamp) >= 0) continue;           /* STARTED_BEFORE, :907 */
-        if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;       /* :933 */
+        if (c->erased) continue;                                        /* saveStatus >= Erased, :892 */
+        if (tid_cmp(&c->txnId, testTimestamp) >= 0) continue;           /* STARTED_BEFORE, :902-903 */
+        if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;       /* :928 */
         collect_command(s, &col, c, sliced, nsliced, rsliced, nrsliced); /* intersects + foldl, :951-960 */
     }
-    for (size_t i = 0; i < s->hist.n; ++i)                               /* :959-987 */
+    for (size_t i = 0; i < s->hist.n; ++i)                               /* :963-1004 */
     {
         const rcmd_t* c = &s->hist.v[i];
         if (tid_cmp(&c->txnId, testTimestamp) >= 0) continue;
@@ -827,7 +827,7 @@ static int map_reduce_ranges_internal(const rc_store* s, const int64_t* keys, si
         collect_command(s, &col, c, sliced, nsliced, rsliced, nrsliced);
     }
     int rc = 0;
-    for (size_t i = 0; i < col.n && !rc; ++i)                            /* :990-997 */
+    for (size_t i = 0; i < col.n && !rc; ++i)                            /* :1007-1014 */
         for (size_t j = 0; j < col.v[i].list.n && !rc; ++j)
             rc = map(acc, 1, col.v[i].range.a, col.v[i].range.b, &col.v[i].list.v[j], p1);
     for (size_t i = 0; i < col.n; ++i) VEC_FREE(col.v[i].list);
@@ -1621,7 +1621,7 @@ static int tids_contain(const tid_t* v, size_t n, const tid_t* x)
 
 /* InMemorySafeStore.mapReduceFull's range half: mapReduceRangesInternal (InMemoryCommandStore.java:884-958)
  * for a recovery scan (testStatus != ANY_STATUS: no historical commands), then the collect fold
- * (:1005-1014) into the scan's lambda (BeginRecovery.java:334-380; scan 0 wants executeAt > its
+ * (:1007-1014) into the scan's lambda (BeginRecovery.java:334-380; scan 0 wants executeAt > its
  * testTxnId) */
 static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t nkeys, const rkey_t* rsliced, size_t nrsliced,
                                   const tid_t* T, unsigned testKind, int startedAt, int testDep, int testStatus, int exec_after,
@@ -1637,8 +1637,8 @@ static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t
     for (size_t i = 0; i < s->cmds.n; ++i)
     {
         const rcmd_t* c = &s->cmds.v[i];
-        if (c->erased) continue;                                           /* :897 */
-        switch (startedAt)                                                 /* :900-913 */
+        if (c->erased) continue;                                           /* :892 */
+        switch (startedAt)                                                 /* :896-907 */
         {
             case STARTED_AFTER:
                 if (tid_cmp(&c->txnId, T) <= 0) continue;
@@ -1649,16 +1649,16 @@ static int map_reduce_ranges_full(const rc_store* s, const int64_t* keys, size_t
             default:
                 if (testDep != ANY_DEPS && tid_cmp(&c->exec, T) < 0) continue;
         }
-        if (testStatus == IS_PROPOSED && !(c->rstatus & AD_RS_PROPOSED)) continue;     /* :915-925 */
-        if (testStatus == IS_STABLE && !(c->rstatus & AD_RS_STABLE)) continue;         /* :926-928 */
-        if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;                       /* :931 */
-        if (testDep != ANY_DEPS)                                                        /* :934-947 */
+        if (testStatus == IS_PROPOSED && !(c->rstatus & AD_RS_PROPOSED)) continue;     /* :909-922 */
+        if (testStatus == IS_STABLE && !(c->rstatus & AD_RS_STABLE)) continue;         /* :923-925 */
+        if (!kinds_test(testKind, tid_kind(&c->txnId))) continue;                       /* :928 */
+        if (testDep != ANY_DEPS)                                                        /* :931-949 */
         {
             if (!c->has_deps) continue;
             const int inter = tids_contain(c->deps.v, c->deps.n, T);
             if ((testDep == WITH) == !inter) continue;
         }
-        collect_command(s, &col, c, sliced, nsliced, rsliced, nrsliced);                         /* :949-956 */
+        collect_command(s, &col, c, sliced, nsliced, rsliced, nrsliced);                         /* :951-961 */
     }
     int rc = 0;
     for (size_t i = 0; i < col.n && !rc; ++i)

@@ -28,7 +28,11 @@ def test_into_matches_oracle(oracle, seed, slices):
         st.close()
 
 
-def test_into_config2_scaled_slicings_and_growth():
+@pytest.mark.parametrize("wire", ["1", "0"])
+def test_into_config2_scaled_slicings_and_growth(wire, monkeypatch):
+    # wire "0" (AD_INTO_WIRE=0): keyDeps cross PCIe full width (the path of slices whose segments do not fit
+    # the u8 key / u16 keysToTxnIds wire form), on every slicing
+    monkeypatch.setenv("AD_INTO_WIRE", wire)
     w = synth.config2(n_txns=60000, n_keys=40000, n_hist_entries=600000)
     st = native.DeviceCommandStore(0)
     try:

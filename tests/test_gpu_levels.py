@@ -88,18 +88,6 @@ def test_config5_full(oracle):
     assert st["n_txns"] == 1_000_000 and st["n_probes"] == 4_000_000
 
 
-@pytest.mark.parametrize("seed", range(3))
-def test_onesweep_radix(oracle, seed, monkeypatch):
-    # the opt-in onesweep sort (AD_RADIX_ONESWEEP: decoupled look-back over 2048-element tiles) under the
-    # same graphs: exec ranking over three words and the key sort of the occurrences, many tiles
-    monkeypatch.setenv("AD_RADIX_ONESWEEP", "1")
-    if seed == 2:
-        g, _ = synth.config5(n_txns=200_000, n_keys=20_000)
-    else:
-        g = synth.random_graph(300 + seed, n_txns=30_000, n_keys=200, long_runs=(seed == 1))
-    _check(g, oracle)
-
-
 def test_multi_block_sort_and_no_keys(oracle):
     # > 1 radix tile per pass and txns without keys / only direct deps
     g = synth.random_graph(99, n_txns=20_000, n_keys=50, max_keys=2, direct_frac=0.5)
