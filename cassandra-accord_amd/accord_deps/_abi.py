@@ -99,7 +99,11 @@ class AdQuerySoa(C.Structure):
     _fields_ = [("n_txns", C.c_uint64), ("txn_msb", P), ("txn_lsb", P), ("txn_node", P),
                 ("exec_msb", P), ("exec_lsb", P), ("exec_node", P), ("min_epoch", P),
                 ("key_off", P), ("keys", P), ("n_keys", C.c_uint64),
-                ("range_off", P), ("range_start", P), ("range_end", P), ("n_ranges", C.c_uint64)]
+                ("range_off", P), ("range_start", P), ("range_end", P), ("n_ranges", C.c_uint64),
+                ("slice_set", P)]
+
+
+AD_SLICE_STORE = 0xFFFFFFFF
 
 
 class AdStats(C.Structure):

@@ -294,12 +294,17 @@ class Queries:
     range_off: Optional[np.ndarray] = None
     range_start: Optional[np.ndarray] = None
     range_end: Optional[np.ndarray] = None
+    # per request its slice set (ad_query_soa.slice_set: an index into Workload.slice_sets, A.AD_SLICE_STORE = the
+    # store's own slices); None = every request reads the store's slices
+    slice_set: Optional[np.ndarray] = None
 
     def __post_init__(self):
         self.key_off = A.as_u64(self.key_off)
         self.keys = A.as_i64(self.keys)
         if self.min_epoch is not None:
             self.min_epoch = A.as_i64(self.min_epoch)
+        if self.slice_set is not None:
+            self.slice_set = A.as_u32(self.slice_set)
         if self.range_off is not None:
             self.range_off = A.as_u64(self.range_off)
             self.range_start = A.as_i64(self.range_start)
@@ -337,6 +342,7 @@ class Queries:
             s.range_start = A.ptr(self.range_start)
             s.range_end = A.ptr(self.range_end)
             s.n_ranges = self.n_ranges
+        s.slice_set = A.ptr(self.slice_set)
         return s
 
     def window(self, lo, hi):
@@ -360,7 +366,8 @@ class Queries:
         if self.range_off is not None:
             ro, (rs, re) = Queries._gather(self.range_off, [self.range_start, self.range_end], idx)
         return Queries(self.txn.take(idx), self.exec.take(idx), key_off, keys,
-                       None if self.min_epoch is None else self.min_epoch[idx], ro, rs, re)
+                       None if self.min_epoch is None else self.min_epoch[idx], ro, rs, re,
+                       None if self.slice_set is None else self.slice_set[idx])
 
 
 @dataclass
@@ -525,3 +532,20 @@ class Workload:
     params: dict = field(default_factory=dict)
     range_start_inclusive: int = 0
     slices: Optional[np.ndarray] = None      # (n,2) i64 owned ranges, None = all
+    # the store's slice sets (ad_slice_sets_load): [(n,2) i64 normalised ranges] per set, the
+    # RangesForEpoch.allBetween results Queries.slice_set names; None = none
+    slice_sets: Optional[list] = None
+
+    def slice_sets_csr(self):
+        """(set_off u64, start i64, end i64) of slice_sets, or None."""
+        if self.slice_sets is None:
+            return None
+        off = np.zeros(len(self.slice_sets) + 1, np.uint64)
+        st, en = [], []
+        for k, r in enumerate(self.slice_sets):
+            r = np.asarray(r, np.int64).reshape(-1, 2)
+            off[k + 1] = off[k] + len(r)
+            st.append(r[:, 0])
+            en.append(r[:, 1])
+        cat = (lambda xs: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros(0, np.int64), np.int64))
+        return off, cat(st), cat(en)

@@ -29,7 +29,8 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_exchange_local", "ad_comm_unique_id", "ad_comm_init", "ad_exchange", "ad_exchange_plan",
            "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing",
            "ad_cfk_load_pruned", "ad_host_register", "ad_host_unregister", "ad_deps_batch_into",
-           "ad_debug_guard_check", "ad_host_alloc", "ad_host_free", "ad_cfk_update_status")
+           "ad_debug_guard_check", "ad_host_alloc", "ad_host_free", "ad_cfk_update_status",
+           "ad_slice_sets_load")
 
 
 class AccordDepsError(RuntimeError):
@@ -63,6 +64,7 @@ def lib():
         L.ad_range_cmds_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsSoa)]
         L.ad_redundant_load.argtypes = [C.c_void_p, C.POINTER(A.AdRedundantSoa)]
         L.ad_prepare.argtypes = [C.c_void_p]
+        L.ad_slice_sets_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         L.ad_deps_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.POINTER(C.POINTER(A.AdDepsResult))]
         L.ad_result_free.argtypes = [C.POINTER(A.AdDepsResult)]
         L.ad_deps_batch_device.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_void_p,
@@ -259,9 +261,17 @@ class DeviceCommandStore:
         rs = workload.cmds.recovery_soa()
         if rs is not None:
             self._check(L.ad_range_cmds_recovery_load(self.h, C.byref(rs)))
+        ss = getattr(workload, "slice_sets_csr", lambda: None)()
+        if ss is not None:
+            self.load_slice_sets(*ss)
         if prepare:
             self._check(L.ad_prepare(self.h))
         return self
+
+    def load_slice_sets(self, set_off, start, end):
+        """ad_slice_sets_load: the store's slice sets (CSR of normalised ranges) that Queries.slice_set names."""
+        off, s, e = A.as_u64(set_off), A.as_i64(start), A.as_i64(end)
+        self._check(lib().ad_slice_sets_load(self.h, len(off) - 1 if len(off) else 0, A.ptr(off), A.ptr(s), A.ptr(e)))
 
     def cfk_update(self, updates):
         """CommandsForKey.update for a batch (host arrays): returns (n_applied, stats)."""
@@ -792,6 +802,8 @@ def device_queries(q, dev):
         keep["me"] = to_dev(np.asarray(q.min_epoch, np.int64))
     if q.range_off is not None:
         keep["ro"], keep["rs"], keep["re"] = to_dev(q.range_off), to_dev(q.range_start), to_dev(q.range_end)
+    if q.slice_set is not None:
+        keep["ss"] = to_dev(np.asarray(q.slice_set, np.uint32).view(np.int32))
     s = A.AdQuerySoa()
     s.n_txns = len(q)
     s.txn_msb, s.txn_lsb, s.txn_node = keep["tm"].data_ptr(), keep["tl"].data_ptr(), keep["tn"].data_ptr()
@@ -802,6 +814,7 @@ def device_queries(q, dev):
     if q.range_off is not None:
         s.range_off, s.range_start, s.range_end = keep["ro"].data_ptr(), keep["rs"].data_ptr(), keep["re"].data_ptr()
         s.n_ranges = q.n_ranges
+    s.slice_set = keep["ss"].data_ptr() if "ss" in keep else None
     return s, keep
 
 

@@ -1142,3 +1142,31 @@ def with_missing_fast(cfk, seed, frac=0.2, back=8):
     off[1:] = np.cumsum(pick)
     return CfkSnapshot(cfk.keys, cfk.seg, cfk.txn, cfk.exec, cfk.status, cfk.pruned_before, off,
                        cfk.txn.take(src[pick]))
+
+
+def with_epoch_slices(w, seed, store_every=0, n_epochs=3):
+    """The batch of a store whose ownership changed over epochs 1..n_epochs (a topology change in flight): each
+    request's minUnsyncedEpoch is drawn in [1, its executeAt's epoch] and its scan is sliced to
+    RangesForEpoch.allBetween(minUnsyncedEpoch, executeAt.epoch()) (PreAccept.java:100,130, Accept.java:115,
+    CommandStores.java:233-242) of epochs that own different random parts of the key space, the last one all of
+    it; every `store_every`-th request (0: none) reads the store's own slices instead (epochs.py)."""
+    from .epochs import RangesForEpoch, with_slice_sets
+    rng = np.random.default_rng(seed)
+    ks = np.concatenate([np.asarray(w.cfk.keys, np.int64), np.asarray(w.queries.keys, np.int64)])
+    if w.queries.range_off is not None and w.queries.n_ranges:
+        ks = np.concatenate([ks, w.queries.range_start, w.queries.range_end])
+    lo, hi = (int(ks.min()) - 3, int(ks.max()) + 3) if len(ks) else (-1000, 1000)
+
+    def random_ranges(n):
+        cuts = np.unique(rng.integers(lo, hi, 2 * n + 8, dtype=np.int64))
+        while len(cuts) < 2 * n:
+            cuts = np.unique(np.concatenate([cuts, rng.integers(lo, hi, 8, dtype=np.int64)]))
+        cuts = np.sort(rng.choice(cuts, 2 * n, replace=False))
+        return [(int(cuts[2 * i]), int(cuts[2 * i + 1])) for i in range(n)]
+    epochs = list(range(1, n_epochs + 1))
+    rfe = RangesForEpoch(epochs, [random_ranges(1 + e % 3) for e in epochs[:-1]] + [[(lo, hi)]])
+    q = w.queries.take(np.arange(len(w.queries)))
+    ex_ep = (q.exec.msb >> np.uint64(15)).astype(np.int64)
+    q.min_epoch = np.array([rng.integers(1, max(1, e) + 1) for e in ex_ep], np.int64)
+    from dataclasses import replace
+    return with_slice_sets(replace(w, queries=q), rfe, store_every)

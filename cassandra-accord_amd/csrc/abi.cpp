@@ -413,6 +413,10 @@ int set_views(ad_ctx* c, uint64_t n_dict, uint64_t n_samp, const NormTid& last, 
     s.n_slices = c->slice_s.size();
     s.slice_start = c->d_slices_s.as<int64_t>();
     s.slice_end = c->d_slices_e.as<int64_t>();
+    s.n_ssets = c->ss_off.empty() ? 0 : c->ss_off.size() - 1;
+    s.sset_off = c->d_ss_off.as<uint64_t>();
+    s.sset_start = c->d_ss_start.as<int64_t>();
+    s.sset_end = c->d_ss_end.as<int64_t>();
     s.start_inclusive = c->cfg.range_start_inclusive;
     s.elide = c->cfg.elide;
     s.rng32 = getenv("AD_RNG64") == nullptr && c->rt_start.size() < (1ull << 26) && 2 * n_dict + 2 < (1ull << 26);
@@ -1608,8 +1612,9 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
             return c->fail(AD_E_NOMEM, "range request expansion");
         HIPCHK(c, hipMemsetAsync(c->rq_err.p, 0, 8, st));
         // rq_err[0]: the rejection flag; rq_err[1]: the Range-domain requests, listed in rq_list
-        HIPCHK(c, run_range_count(c->ds, n, q->key_off, q->range_off, q->range_start, q->range_end, c->rq_cnt.as<uint32_t>(),
-                                  c->rq_err.as<uint32_t>(), c->rq_list.as<uint32_t>(), nr, recovery_scan < 0, st));
+        HIPCHK(c, run_range_count(c->ds, n, q->key_off, q->range_off, q->range_start, q->range_end, q->slice_set,
+                                  c->rq_cnt.as<uint32_t>(), c->rq_err.as<uint32_t>(), c->rq_list.as<uint32_t>(), nr,
+                                  recovery_scan < 0, st));
         HIPCHK(c, run_scan_arrays(c->rq_cnt.as<uint32_t>(), c->rq_off.as<uint64_t>(), n, 1, c->rq_bsum.as<uint64_t>(), st));
         uint64_t* hs = c->h_small;
         HIPCHK(c, hipMemcpyAsync(&hs[3], c->rq_off.as<uint64_t>() + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -1622,7 +1627,7 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
         np = hs[3];
         if (!ens<int64_t>(c->rq_keys, np) || !ens<int64_t>(c->rq_hi, np) || !ens<uint8_t>(c->rq_kind, np))
             return c->fail(AD_E_NOMEM, "range request probes");
-        HIPCHK(c, run_range_fill(c->ds, n, q->key_off, q->keys, q->range_off, q->range_start, q->range_end,
+        HIPCHK(c, run_range_fill(c->ds, n, q->key_off, q->keys, q->range_off, q->range_start, q->range_end, q->slice_set,
                                  c->rq_off.as<uint64_t>(), c->rq_keys.as<int64_t>(), c->rq_hi.as<int64_t>(),
                                  c->rq_kind.as<uint8_t>(), c->rq_list.as<uint32_t>(), n_rreq, recovery_scan < 0, st));
     }
@@ -1640,6 +1645,7 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
     b.q_txn_msb = q->txn_msb; b.q_txn_lsb = q->txn_lsb; b.q_txn_node = q->txn_node;
     b.q_exec_msb = q->exec_msb; b.q_exec_lsb = q->exec_lsb; b.q_exec_node = q->exec_node;
     b.q_min_epoch = q->min_epoch; b.q_key_off = q->key_off; b.q_keys = q->keys;
+    b.q_slice_set = q->slice_set;
     if (nr)
     {
         b.q_key_off = c->rq_off.as<uint64_t>();
@@ -1832,6 +1838,7 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
                 if (!bind_split(c->sub, sb, nd, snp, true) || !ens<uint64_t>(c->s_tm, nd) || !ens<uint64_t>(c->s_tl, nd) ||
                     !ens<int32_t>(c->s_tn, nd) || !ens<uint64_t>(c->s_em, nd) || !ens<uint64_t>(c->s_el, nd) ||
                     !ens<int32_t>(c->s_en, nd) || !ens<int64_t>(c->s_me, nd) || !ens<int64_t>(c->s_k, snp) ||
+                    (b.q_slice_set && !ens<uint32_t>(c->s_ss, nd)) ||
                     (b.p_kind && (!ens<int64_t>(c->s_khi, snp) || !ens<uint8_t>(c->s_kind, snp))))
                     return c->fail(AD_E_NOMEM, "deferred buffers");
                 uint64_t* sko = c->s_ko.as<uint64_t>();     // the scanned counts are the sub-batch key_off
@@ -1839,10 +1846,12 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
                                            c->s_tl.as<uint64_t>(), c->s_tn.as<int32_t>(), c->s_em.as<uint64_t>(),
                                            c->s_el.as<uint64_t>(), c->s_en.as<int32_t>(), c->s_me.as<int64_t>(), sko,
                                            c->s_k.as<int64_t>(), b.p_kind ? c->s_khi.as<int64_t>() : nullptr,
-                                           b.p_kind ? c->s_kind.as<uint8_t>() : nullptr, st));
+                                           b.p_kind ? c->s_kind.as<uint8_t>() : nullptr,
+                                           b.q_slice_set ? c->s_ss.as<uint32_t>() : nullptr, st));
                 sb.q_txn_msb = c->s_tm.as<uint64_t>(); sb.q_txn_lsb = c->s_tl.as<uint64_t>(); sb.q_txn_node = c->s_tn.as<int32_t>();
                 sb.q_exec_msb = c->s_em.as<uint64_t>(); sb.q_exec_lsb = c->s_el.as<uint64_t>(); sb.q_exec_node = c->s_en.as<int32_t>();
                 sb.q_min_epoch = b.q_min_epoch ? c->s_me.as<int64_t>() : nullptr;
+                sb.q_slice_set = b.q_slice_set ? c->s_ss.as<uint32_t>() : nullptr;
                 sb.q_key_off = sko;
                 sb.q_keys = c->s_k.as<int64_t>();
                 sb.q_keys_hi = b.p_kind ? c->s_khi.as<int64_t>() : nullptr;
@@ -1862,6 +1871,8 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
         {
             if (h.error == ERR_STATE)
                 return c->fail(AD_E_STATE, "reference would throw: prunedBefore set but no committed Write to substitute (CommandsForKey.java:955-962)");
+            if (h.error == ERR_SLICE)
+                return c->fail(AD_E_INVAL, "a request's slice_set is beyond the store's slice sets (ad_slice_sets_load)");
             return c->fail(AD_E_INVAL, recovery_scan >= 0 ? "invalid Txn.Kind for witnessedBy() in a request (Txn.java:247-262)"
                                                           : "invalid Txn.Kind for witnesses() in a request (Txn.java:221-235)");
         }
@@ -2039,6 +2050,14 @@ int result_to_host(ad_ctx* c, uint64_t n, const ad_deps_result& dev, ad_deps_res
 
 int check_query_host(ad_ctx* c, const ad_query_soa* q, uint32_t flags)
 {
+    if (q->slice_set)
+    {
+        const uint64_t ns = c->ss_off.empty() ? 0 : c->ss_off.size() - 1;
+        for (uint64_t i = 0; i < q->n_txns; ++i)
+            if (q->slice_set[i] != AD_SLICE_STORE && q->slice_set[i] >= ns)
+                return c->fail(AD_E_INVAL, "request %llu: slice_set %u beyond the store's %llu slice sets",
+                               (unsigned long long)i, q->slice_set[i], (unsigned long long)ns);
+    }
     if (q->range_off && q->n_txns)
     {
         // Range-domain requests: ranges normalised (accord.primitives.Ranges), no keys beside them,
@@ -2306,6 +2325,37 @@ int ad_prepare(ad_ctx* c)
     return c->dirty ? build_snapshot(c) : AD_OK;
 }
 
+int ad_slice_sets_load(ad_ctx* c, uint32_t n_sets, const uint64_t* set_off, const int64_t* start, const int64_t* end)
+{
+    if (!c || (n_sets && !set_off)) return AD_E_INVAL;
+    const uint64_t nr = n_sets ? set_off[n_sets] : 0;
+    if (nr && (!start || !end)) return c->fail(AD_E_INVAL, "slice sets: start / end required");
+    for (uint32_t k = 0; k < n_sets; ++k)
+    {
+        if (set_off[k] > set_off[k + 1]) return c->fail(AD_E_INVAL, "slice sets: set_off not monotone at set %u", k);
+        for (uint64_t j = set_off[k]; j < set_off[k + 1]; ++j)
+            if (start[j] >= end[j] || (j > set_off[k] && end[j - 1] > start[j]))
+                return c->fail(AD_E_INVAL, "slice set %u: ranges not normalised (start < end, ascending, disjoint)", k);
+    }
+    if (n_sets && set_off[0] != 0) return c->fail(AD_E_INVAL, "slice sets: set_off[0] must be 0");
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
+    c->ss_off.assign(set_off, set_off + (n_sets ? n_sets + 1 : 0));
+    c->ss_start.assign(start, start + nr);
+    c->ss_end.assign(end, end + nr);
+    int rc;
+    if ((rc = upload(c, c->d_ss_off, c->ss_off)) || (rc = upload(c, c->d_ss_start, c->ss_start)) ||
+        (rc = upload(c, c->d_ss_end, c->ss_end)))
+        return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // the views of a built snapshot (a later build takes them from the ctx too, set_views)
+    c->ds.n_ssets = n_sets;
+    c->ds.sset_off = c->d_ss_off.as<uint64_t>();
+    c->ds.sset_start = c->d_ss_start.as<int64_t>();
+    c->ds.sset_end = c->d_ss_end.as<int64_t>();
+    return AD_OK;
+}
+
 }  // extern "C"
 
 namespace adi {
@@ -2414,6 +2464,7 @@ int ad_deps_batch(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps_resu
     d.min_epoch = stage_q(c, c->q_me, q->min_epoch, n, &rc);
     d.key_off = stage_q(c, c->q_ko, q->key_off, n + 1, &rc);
     d.keys = stage_q(c, c->q_k, q->keys, np, &rc);
+    d.slice_set = stage_q(c, c->q_ss, q->slice_set, n, &rc);
     if (n && q->range_off && q->range_off[n] > q->range_off[0])
     {
         const uint64_t r0 = q->range_off[0], nr = q->range_off[n] - r0;

@@ -136,6 +136,11 @@ using namespace adi;
 struct ad_ctx {
     ad_config cfg{};
     std::vector<int64_t> slice_s, slice_e;
+    // slice sets of per-request slices (ad_slice_sets_load; DevSnapshot.sset_*)
+    std::vector<uint64_t> ss_off;
+    std::vector<int64_t> ss_start, ss_end;
+    DevBuf d_ss_off, d_ss_start, d_ss_end;
+    DevBuf q_ss, s_ss;                         // a batch's staged slice_set; the deferred sub-batch's
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;

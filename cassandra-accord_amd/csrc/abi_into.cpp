@@ -445,7 +445,8 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
             (cap[3 * m + 1] && !out->txns[m]) || (cap[3 * m + 2] && !out->k2t[m]))
             return c->fail(AD_E_INVAL, "ad_deps_batch_into: output arrays missing for map %d", m);
     // key-only SNAPSHOT batches take the pipelined path (its staging pass checks the keys)
-    const bool fast = !(flags & AD_SEQUENTIAL) && !(n && q->range_off && q->range_off[n] > q->range_off[0]);
+    // (batches naming slice sets take the staged path: its per-array copies carry slice_set)
+    const bool fast = !(flags & AD_SEQUENTIAL) && !(n && q->range_off && q->range_off[n] > q->range_off[0]) && !q->slice_set;
     int rc = fast ? 0 : check_query_host(c, q, flags);
     if (rc) return rc;
     if (flags & AD_SEQUENTIAL)
@@ -526,6 +527,7 @@ int ad_deps_batch_into(ad_ctx* c, const ad_query_soa* q, uint32_t flags, ad_deps
         d.min_epoch = q->min_epoch ? stage_q(c, c->q_me, q->min_epoch + lo, nc, &rc) : nullptr;
         d.key_off = stage_q(c, c->q_ko, ko.data(), nc + 1, &rc);
         d.keys = stage_q(c, c->q_k, q->keys + k0, k1 - k0, &rc);
+        d.slice_set = q->slice_set ? stage_q(c, c->q_ss, q->slice_set + lo, nc, &rc) : nullptr;
         if (nc && q->range_off && q->range_off[hi] > q->range_off[lo])
         {
             const uint64_t r0 = q->range_off[lo], nr = q->range_off[hi] - r0;

@@ -382,6 +382,7 @@ int ad_recovery_batch(ad_ctx* c, const ad_query_soa* q, uint32_t scan, ad_deps_r
     d.txn_node = stage_q(c, c->q_tn, q->txn_node, n, &rc);
     d.key_off = stage_q(c, c->q_ko, q->key_off, n + 1, &rc);
     d.keys = stage_q(c, c->q_k, q->keys, np, &rc);
+    d.slice_set = stage_q(c, c->q_ss, q->slice_set, n, &rc);
     std::vector<uint64_t> ro;
     if (n && q->range_off && q->range_off[n] > q->range_off[0])
     {

@@ -266,6 +266,11 @@ struct DevSnapshot {
     uint64_t n_slices;
     const int64_t* slice_start;
     const int64_t* slice_end;
+    // per-request slices (ad_slice_sets_load): set k = [sset_start, sset_end)[sset_off[k], sset_off[k + 1])
+    uint64_t n_ssets;
+    const uint64_t* sset_off;
+    const int64_t* sset_start;
+    const int64_t* sset_end;
     int start_inclusive;
     int elide;
     // range ids below 2^26 and id ranks below 2^26: the lean kernels' rangeDeps build sorts 32-bit keys
@@ -435,6 +440,35 @@ __device__ inline uint32_t dict_rank_sampled(const Snap& s, const NormTid& t)
 __host__ __device__ inline bool range_contains(int start_inclusive, int64_t s, int64_t e, int64_t key)
 {
     return start_inclusive ? (s <= key && key < e) : (s < key && key <= e);
+}
+
+// The Ranges a request's scan is sliced to -- SafeCommandStore.mapReduceActive's `slice`
+// (SafeCommandStore.java:292): PreAccept / Accept / GetDeps pass safeStore.ranges().allBetween(minUnsyncedEpoch,
+// txnId | executeAt) (PreAccept.java:100,130, Accept.java:115, CommandStores.java:233-242), which differs by epoch
+// during a topology change. A request names one of the store's slice sets (ad_query_soa.slice_set,
+// ad_slice_sets_load), or SLICE_STORE: the store's own slices (ad_config; none = every key).
+constexpr uint32_t SLICE_STORE = 0xFFFFFFFFu;
+struct SliceView {
+    const int64_t* st;
+    const int64_t* en;
+    uint64_t n;
+    bool all;          // no slicing: every key
+};
+__device__ __forceinline__ SliceView request_slice(const DevSnapshot& s, const uint32_t* sset, uint64_t t)
+{
+    const uint32_t k = sset ? sset[t] : SLICE_STORE;
+    if (k == SLICE_STORE) return SliceView{s.slice_start, s.slice_end, s.n_slices, s.n_slices == 0};
+    if (k >= s.n_ssets) return SliceView{nullptr, nullptr, 0, false};       // rejected (ERR_SLICE): no key
+    const uint64_t a = s.sset_off[k];
+    return SliceView{s.sset_start + a, s.sset_end + a, s.sset_off[k + 1] - a, false};
+}
+// Ranges.contains(key) of the slice (InMemoryCommandStore.java:280)
+__device__ __forceinline__ bool slice_has(int start_inclusive, const SliceView& v, int64_t key)
+{
+    if (v.all) return true;
+    for (uint64_t i = 0; i < v.n; ++i)
+        if (range_contains(start_inclusive, v.st[i], v.en[i], key)) return true;
+    return false;
 }
 
 }  // namespace adx

@@ -154,6 +154,7 @@ __global__ void k_encode_txn(DevSnapshot s, BatchBufs b)
 {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= b.n_txns) return;
+    if (b.q_slice_set && b.q_slice_set[t] != SLICE_STORE && b.q_slice_set[t] >= s.n_ssets) set_error(b.ctl, ERR_SLICE);
     const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t];
     const int32_t tn = b.q_txn_node[t];
     const uint64_t em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
@@ -183,9 +184,7 @@ __global__ void k_probe_keys(DevSnapshot s, BatchBufs b)
         b.p_rec[p] = make_uint4(NO_KEY, b.t_S[t], b.t_self[t], b.t_kinds[t] | (pk == PK_RANGE ? (1u << 12) : 0u) | (pk << 13));
         return;
     }
-    bool in_slice = s.n_slices == 0;
-    for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
-        in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+    const bool in_slice = slice_has(s.start_inclusive, request_slice(s, b.q_slice_set, t), key);
     uint32_t ki = NO_KEY;
     if (in_slice)
     {
@@ -222,18 +221,20 @@ hipError_t run_encode(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // The keys come out ascending (sliced ranges ascending and disjoint), which is all K2 needs: range
 // probes contribute no keyDeps keys.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool slice_part(const DevSnapshot& s, int64_t a, int64_t b, uint64_t sl, int64_t* lo, int64_t* hi)
+__device__ __forceinline__ bool slice_part(const SliceView& v, int64_t a, int64_t b, uint64_t sl, int64_t* lo, int64_t* hi)
 {
-    if (s.n_slices == 0)
+    if (v.all)
     {
         *lo = a;
         *hi = b;
         return a < b;
     }
-    *lo = a > s.slice_start[sl] ? a : s.slice_start[sl];
-    *hi = b < s.slice_end[sl] ? b : s.slice_end[sl];
+    *lo = a > v.st[sl] ? a : v.st[sl];
+    *hi = b < v.en[sl] ? b : v.en[sl];
     return *lo < *hi;
 }
+// parts of one range against the slice: one per slice range (every key: the range itself)
+__device__ __forceinline__ uint64_t slice_parts(const SliceView& v) { return v.all ? 1 : v.n; }
 
 __global__ __launch_bounds__(256) void k_range_count(DevSnapshot s, uint64_t n, const uint64_t* __restrict__ key_off,
                                                      const uint64_t* __restrict__ range_off,
@@ -278,15 +279,16 @@ __global__ __launch_bounds__(256) void k_range_count_r(DevSnapshot s, const uint
                                                        const uint32_t* __restrict__ n_list,
                                                        const uint64_t* __restrict__ range_off,
                                                        const int64_t* __restrict__ range_start,
-                                                       const int64_t* __restrict__ range_end, uint32_t* __restrict__ cnt,
-                                                       bool with_rb)
+                                                       const int64_t* __restrict__ range_end, const uint32_t* __restrict__ sset,
+                                                       uint32_t* __restrict__ cnt, bool with_rb)
 {
     const uint64_t li = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (li >= *n_list) return;
     const uint64_t t = list[li];
     const uint64_t r0 = range_off[t], r1 = range_off[t + 1];
     const bool incl = s.start_inclusive != 0;
-    const uint64_t n_sl = s.n_slices ? s.n_slices : 1;
+    const SliceView sv = request_slice(s, sset, t);
+    const uint64_t n_sl = slice_parts(sv);
     uint64_t c = 0;
     for (uint64_t j = r0; j < r1; ++j)
     {
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(256) void k_range_count_r(DevSnapshot s, const uint
         for (uint64_t sl = 0; sl < n_sl; ++sl)
         {
             int64_t lo, hi;
-            if (!slice_part(s, a, e, sl, &lo, &hi)) continue;
+            if (!slice_part(sv, a, e, sl, &lo, &hi)) continue;
             uint64_t k0, k1;
             wave_key_span(s, lo, hi, incl, k0, k1);
             c += k1 - k0;
@@ -328,9 +330,9 @@ __global__ __launch_bounds__(256) void k_range_fill_keys(uint64_t n, const uint6
 __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, const uint32_t* __restrict__ list, uint32_t n_list,
                                                     const uint64_t* __restrict__ range_off,
                                                     const int64_t* __restrict__ range_start,
-                                                    const int64_t* __restrict__ range_end, const uint64_t* __restrict__ off,
-                                                    int64_t* __restrict__ pkeys, int64_t* __restrict__ pkeys_hi,
-                                                    uint8_t* __restrict__ pkind, bool with_rb)
+                                                    const int64_t* __restrict__ range_end, const uint32_t* __restrict__ sset,
+                                                    const uint64_t* __restrict__ off, int64_t* __restrict__ pkeys,
+                                                    int64_t* __restrict__ pkeys_hi, uint8_t* __restrict__ pkind, bool with_rb)
 {
     const uint64_t li = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (li >= n_list) return;
@@ -341,14 +343,15 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, const uint32_
     const uint64_t o_end = off[t + 1];
     if (o_end == o) return;                      // rejected (k_range_count) or nothing to visit
     const bool incl = s.start_inclusive != 0;
-    const uint64_t n_sl = s.n_slices ? s.n_slices : 1;
+    const SliceView sv = request_slice(s, sset, t);
+    const uint64_t n_sl = slice_parts(sv);
     for (uint64_t j = r0; j < r1; ++j)
     {
         const int64_t a = range_start[j], e = range_end[j];
         for (uint64_t sl = 0; sl < n_sl; ++sl)
         {
             int64_t lo, hi;
-            if (!slice_part(s, a, e, sl, &lo, &hi)) continue;
+            if (!slice_part(sv, a, e, sl, &lo, &hi)) continue;
             uint64_t k0, k1;
             wave_key_span(s, lo, hi, incl, k0, k1);
             for (uint64_t i = lane; i < k1 - k0; i += 64)
@@ -380,8 +383,8 @@ __global__ __launch_bounds__(256) void k_range_fill(DevSnapshot s, const uint32_
 }
 
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
-                           const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           uint32_t* list, uint64_t max_list, bool with_rb, hipStream_t st)
+                           const int64_t* range_start, const int64_t* range_end, const uint32_t* sset, uint32_t* cnt,
+                           uint32_t* err, uint32_t* list, uint64_t max_list, bool with_rb, hipStream_t st)
 {
     if (!n) return hipSuccess;
     k_range_count<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, n, key_off, range_off, range_start, range_end, cnt, err,
@@ -389,20 +392,20 @@ hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key
     // the listed requests' counts: a wave each, the grid sized for every range of the batch (the list is shorter)
     const uint64_t m = std::min<uint64_t>(max_list, n);
     if (m)
-        k_range_count_r<<<(unsigned)((m + 3) / 4), 256, 0, st>>>(s, list, err + 1, range_off, range_start, range_end, cnt,
-                                                                 with_rb);
+        k_range_count_r<<<(unsigned)((m + 3) / 4), 256, 0, st>>>(s, list, err + 1, range_off, range_start, range_end, sset,
+                                                                 cnt, with_rb);
     return hipGetLastError();
 }
 
 hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
                           const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
-                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, const uint32_t* list,
-                          uint32_t n_list, bool with_rb, hipStream_t st)
+                          const uint32_t* sset, const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind,
+                          const uint32_t* list, uint32_t n_list, bool with_rb, hipStream_t st)
 {
     if (n) k_range_fill_keys<<<(unsigned)((8 * n + 255) / 256), 256, 0, st>>>(n, key_off, keys, range_off, off, pkeys, pkind);
     if (n_list)
-        k_range_fill<<<(unsigned)((n_list + 3) / 4), 256, 0, st>>>(s, list, n_list, range_off, range_start, range_end, off, pkeys,
-                                                                   pkeys_hi, pkind, with_rb);
+        k_range_fill<<<(unsigned)((n_list + 3) / 4), 256, 0, st>>>(s, list, n_list, range_off, range_start, range_end, sset, off,
+                                                                   pkeys, pkeys_hi, pkind, with_rb);
     return hipGetLastError();
 }
 

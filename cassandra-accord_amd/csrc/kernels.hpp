@@ -30,6 +30,7 @@ constexpr uint64_t NO_RB = ~0ull;
 constexpr uint32_t K2_BIG = 512;     // elements in a list family from which k_build_big takes a request (= the LDS path's K2_CAP)
 constexpr unsigned ERR_INVAL = 1u;   // BatchCtl.error codes
 constexpr unsigned ERR_STATE = 8u;
+constexpr unsigned ERR_SLICE = 16u;  // a request's slice_set beyond the store's slice sets
 
 // Per-batch device buffers (sized by the host before the launches).
 struct BatchBufs {
@@ -40,6 +41,7 @@ struct BatchBufs {
     const int64_t* q_min_epoch;      // may be null
     const uint64_t* q_key_off;
     const int64_t* q_keys;
+    const uint32_t* q_slice_set;     // per request its slice set (SLICE_STORE: the store's slices); null = all the store's
     // Range-domain requests (run_range_expand): per probe its kind (PK_*; null: every probe is a key of
     // its request) and, for range and redundant-before probes, the range [q_keys[p], q_keys_hi[p])
     const uint8_t* p_kind;
@@ -138,13 +140,14 @@ constexpr uint8_t PK_KEY = 0, PK_RANGE_KEY = 1, PK_RANGE = 2, PK_RANGE_RB = 3;
 // not normalised); then, from the exclusive scan `off`, the probes
 // (err[1]: the Range-domain requests, their indices appended to `list`); then, from the exclusive scan `off`,
 // the probes: a key-domain request's keys one thread per request, a listed request's one wave each
+// sset: per request its slice set (null: the store's slices)
 hipError_t run_range_count(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const uint64_t* range_off,
-                           const int64_t* range_start, const int64_t* range_end, uint32_t* cnt, uint32_t* err,
-                           uint32_t* list, uint64_t max_list, bool with_rb, hipStream_t st);
+                           const int64_t* range_start, const int64_t* range_end, const uint32_t* sset, uint32_t* cnt,
+                           uint32_t* err, uint32_t* list, uint64_t max_list, bool with_rb, hipStream_t st);
 hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_off, const int64_t* keys,
                           const uint64_t* range_off, const int64_t* range_start, const int64_t* range_end,
-                          const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind, const uint32_t* list,
-                          uint32_t n_list, bool with_rb, hipStream_t st);
+                          const uint32_t* sset, const uint64_t* off, int64_t* pkeys, int64_t* pkeys_hi, uint8_t* pkind,
+                          const uint32_t* list, uint32_t n_list, bool with_rb, hipStream_t st);
 
 hipError_t build_cfk_trees(const DevSnapshot& s, hipStream_t st);
 hipError_t build_range_trees(const DevSnapshot& s, hipStream_t st);
@@ -197,8 +200,6 @@ hipError_t run_prepare(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 // pass 1 with rpw1 = 2 on a store without range commands: wide1 selects the wide kernel (requests of up to
 // 64 raw emissions) over the narrow one (up to 32; the rest to pass 2)
 hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, uint32_t rpw1, bool wide1, hipStream_t st);
-// lean pass 1 (and 2) as k_lean_gather + k_lean_build, stores without range commands: requests it cannot
-// serve are appended to deferred2 (the general kernel's list)
 
 // ---- PreAccept timestamp proposal (preaccept.hip)
 struct DevRangeMap {            // a ReducingRangeMap<Timestamp> in HBM (ad_range_map_soa)
@@ -239,7 +240,7 @@ hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
                             const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,
                             uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, int64_t* o_khi,
-                            uint8_t* o_kind, hipStream_t st);
+                            uint8_t* o_kind, uint32_t* o_ss, hipStream_t st);
 hipError_t run_defer_scatter(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint32_t* sub_sz,
                              const uint64_t* sub_reg, hipStream_t st);
 

@@ -371,10 +371,12 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
     struct Hdr { uint4 h0, h1; uint2 h2, h3; uint4 q; uint32_t slot; bool look; };
     constexpr bool QL = !RNG && RPW == 2;
     __shared__ uint4 qst_all[QL ? LEAN_WAVES : 1][QL ? 64 : 1];
-    auto in_slice_of = [&](int64_t key) {
-        bool in = s.n_slices == 0;
-        for (uint64_t i = 0; i < s.n_slices && !in; ++i) in = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
-        return in;
+    // the request's slice (its slice set when the batch names them, SafeCommandStore.java:292)
+    auto in_slice_of = [&](uint32_t t, int64_t key) {
+        return slice_has(s.start_inclusive,
+                         b.q_slice_set ? request_slice(s, b.q_slice_set, t)
+                                       : SliceView{s.slice_start, s.slice_end, s.n_slices, s.n_slices == 0},
+                         key);
     };
     auto load_line = [&](uint32_t slot, uint32_t cls, Hdr& H) {
         const uint4* L4 = reinterpret_cast<const uint4*>(s.kline + slot);
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             return;
         }
         const bool on = q.act && !q.defer && hl < q.np;
-        look = on && in_slice_of(key);
+        look = on && in_slice_of(q.t, key);
         d = s.kl_disp[look ? kl_bucket(key_hash(key), s.kl_buckets) : 0u];
     };
     auto loadC = [&](const Req& q, int64_t key, bool look, uint32_t d, Hdr& H) {

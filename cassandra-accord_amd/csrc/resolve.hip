@@ -360,11 +360,13 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
     // key -> (KeyEntry / KeyRec index | in-slice bit, stabbing cell): the slice test
     // (InMemoryCommandStore.java:280) and an open-addressing probe of the KeySlot table by the
     // group's 8 lanes at once (8 consecutive 16-byte slots = one line per round)
-    auto probe = [&](uint32_t npi, int64_t key, uint32_t& pso, uint32_t& pco) {
+    auto probe = [&](uint64_t iix, uint32_t npi, int64_t key, uint32_t& pso, uint32_t& pco) {
         bool a = g < npi && npi <= FMAXP;
-        bool in_slice = s.n_slices == 0;
-        for (uint64_t i = 0; i < s.n_slices && !in_slice; ++i)
-            in_slice = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key);
+        // the request's slice (its slice set when the batch names them; iteration iix's request)
+        const bool in_slice = a && slice_has(s.start_inclusive,
+                                             b.q_slice_set ? request_slice(s, b.q_slice_set, tof(iix))
+                                                           : SliceView{s.slice_start, s.slice_end, s.n_slices, s.n_slices == 0},
+                                             key);
         uint32_t slot = SLOT_NONE, cell = NO_CELL;
         bool look = a && in_slice && s.n_keys != 0;
         uint64_t h = key_hash(key) & s.khash_mask;
@@ -405,7 +407,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
     int64_t keyc;
     uint32_t psc, pcc;
     st2(k0c, npc, keyc);
-    probe(npc, keyc, psc, pcc);
+    probe(t0, npc, keyc, psc, pcc);
     uint4 kqc;
     st3(psc, kqc);
     for (uint64_t ii = t0; ii < n_iter; ii += nw)
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
 
         // lists staged: the next request's key probe and KeyEntry loads go out now, behind this
         // one's build
-        probe(npn, keyn, psn, pcn);
+        probe(ii + nw, npn, keyn, psn, pcn);
         st3(psn, kqn);
         pf3 = true;
 
@@ -902,7 +904,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
         } while (false);
         if (!pf3)
         {
-            probe(npn, keyn, psn, pcn);
+            probe(ii + nw, npn, keyn, psn, pcn);
             st3(psn, kqn);
         }
         k0c = k0n; npc = npn;
@@ -951,8 +953,23 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
 #pragma unroll
         for (int j = 0; j < PREP_PPT; ++j)
         {
-            bool x = s.n_slices == 0;
-            for (uint64_t i = 0; i < s.n_slices && !x; ++i) x = range_contains(s.start_inclusive, s.slice_start[i], s.slice_end[i], key[j]);
+            bool x;
+            if (b.q_slice_set)
+            {
+                // per-request slices: the probe's request by a search of the key offsets (batches that name slice
+                // sets only; a probe-major thread does not know its request otherwise)
+                const uint64_t p = p0 + (uint64_t)j * blockDim.x;
+                uint64_t lo = 0, hi = b.n_txns;
+                while (lo + 1 < hi)
+                {
+                    const uint64_t mid = (lo + hi) >> 1;
+                    if (b.q_key_off[mid] <= p) lo = mid;
+                    else hi = mid;
+                }
+                x = p < b.n_probes && slice_has(s.start_inclusive, request_slice(s, b.q_slice_set, lo), key[j]);
+            }
+            else
+                x = slice_has(s.start_inclusive, SliceView{s.slice_start, s.slice_end, s.n_slices, s.n_slices == 0}, key[j]);
             in[j] = x;
             d[j] = 0;
             if (x) d[j] = s.kl_disp[kl_bucket(key_hash(key[j]), s.kl_buckets)];
@@ -965,6 +982,7 @@ __global__ __launch_bounds__(256) void k_prepare(DevSnapshot s, BatchBufs b)
         }
     }
     if (t >= b.n_txns) return;
+    if (b.q_slice_set && b.q_slice_set[t] != SLICE_STORE && b.q_slice_set[t] >= s.n_ssets) set_error_f(b.ctl, ERR_SLICE);
     // request t's record
     const uint64_t k0 = b.q_key_off[t], k1 = b.q_key_off[t + 1];
     const uint64_t tm = b.q_txn_msb[t], tl = b.q_txn_lsb[t], em = b.q_exec_msb[t], el = b.q_exec_lsb[t];
@@ -1036,7 +1054,7 @@ __global__ void k_defer_counts(BatchBufs b, const uint32_t* deferred, uint64_t n
 
 __global__ void k_defer_gather(BatchBufs b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off, BatchBufs sub,
                                uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em, uint64_t* o_el, int32_t* o_en,
-                               int64_t* o_me, uint64_t* o_ko, int64_t* o_k, int64_t* o_khi, uint8_t* o_kind)
+                               int64_t* o_me, uint64_t* o_ko, int64_t* o_k, int64_t* o_khi, uint8_t* o_kind, uint32_t* o_ss)
 {
     const uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (i >= nd) return;
@@ -1047,6 +1065,7 @@ __global__ void k_defer_gather(BatchBufs b, const uint32_t* deferred, uint64_t n
         o_tm[i] = b.q_txn_msb[t]; o_tl[i] = b.q_txn_lsb[t]; o_tn[i] = b.q_txn_node[t];
         o_em[i] = b.q_exec_msb[t]; o_el[i] = b.q_exec_lsb[t]; o_en[i] = b.q_exec_node[t];
         if (b.q_min_epoch) o_me[i] = b.q_min_epoch[t];
+        if (b.q_slice_set) o_ss[i] = b.q_slice_set[t];
         if (o_ko != sub_off)
         {
             o_ko[i] = sub_off[i];
@@ -1084,12 +1103,13 @@ hipError_t run_defer_counts(const BatchBufs& b, const uint32_t* deferred, uint64
 hipError_t run_defer_gather(const BatchBufs& b, const uint32_t* deferred, uint64_t nd, const uint64_t* sub_off,
                             const BatchBufs& sub, uint64_t* o_tm, uint64_t* o_tl, int32_t* o_tn, uint64_t* o_em,
                             uint64_t* o_el, int32_t* o_en, int64_t* o_me, uint64_t* o_ko, int64_t* o_k, int64_t* o_khi,
-                            uint8_t* o_kind, hipStream_t st)
+                            uint8_t* o_kind, uint32_t* o_ss, hipStream_t st)
 {
     if (!nd) return hipSuccess;
     if (b.p_kind && (!o_khi || !o_kind || !b.q_keys_hi)) return hipErrorInvalidValue;
+    if (b.q_slice_set && !o_ss) return hipErrorInvalidValue;
     k_defer_gather<<<(unsigned)((nd + 3) / 4), 256, 0, st>>>(b, deferred, nd, sub_off, sub, o_tm, o_tl, o_tn, o_em, o_el,
-                                                             o_en, o_me, o_ko, o_k, o_khi, o_kind);
+                                                             o_en, o_me, o_ko, o_k, o_khi, o_kind, o_ss);
     return hipGetLastError();
 }
 

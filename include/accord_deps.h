@@ -209,7 +209,20 @@ typedef struct ad_query_soa {
     const int64_t*  range_start;
     const int64_t*  range_end;
     uint64_t        n_ranges;        /* range_off[n_txns], read only under AD_N_KEYS */
+    /* The slice of each request's scan (SafeCommandStore.mapReduceActive's `slice`, SafeCommandStore.java:292) when
+     * it is not the store's own: PreAccept (PreAccept.java:100,130), Accept (Accept.java:115), GetDeps and
+     * GetEphemeralReadDeps (GetDeps.java:75, GetEphemeralReadDeps.java:75) slice to
+     * safeStore.ranges().allBetween(minUnsyncedEpoch, txnId | executeAt) (RangesForEpoch.allBetween,
+     * CommandStores.java:233-242), which differs between the requests of one batch during a topology change.
+     * slice_set[i] is an index into the store's slice sets (ad_slice_sets_load), or AD_SLICE_STORE for the
+     * store's own slices (ad_config.slice_*). NULL: every request reads the store's slices. It slices the keys a
+     * request scans (mapReduceForKey, InMemoryCommandStore.java:280), a Range-domain request's ranges (:289-304) and
+     * the range commands' fold (:887,951-961); RedundantBefore stays unsliced (RedundantBefore.java:420-423), and the
+     * registration of a SEQUENTIAL batch's insertions keeps the store's slices. An index beyond the loaded sets:
+     * AD_E_INVAL. ad_deps_batch_device / ad_recovery_batch_device: a device array. */
+    const uint32_t* slice_set;
 } ad_query_soa;
+#define AD_SLICE_STORE 0xFFFFFFFFu
 
 typedef struct ad_stats {
     uint64_t n_txns, n_probes;
@@ -293,6 +306,13 @@ int ad_redundant_load(ad_ctx* ctx, const ad_redundant_soa* rb);
 /* Build the id dictionary and device indexes of the loaded snapshot now (otherwise the first
  * batch does it). Ingest time is reported in ad_stats.ms_ingest, never in ms_device. */
 int ad_prepare(ad_ctx* ctx);
+
+/* The store's slice sets (ad_query_soa.slice_set): set k is the Ranges [start[j], end[j]) for j in
+ * [set_off[k], set_off[k+1]) -- normalised as accord.primitives.Ranges (start < end, ascending, disjoint), in the
+ * store's inclusivity; an empty set owns no key. A host binding loads the distinct RangesForEpoch.allBetween results
+ * its batch needs (CommandStores.java:233-242). Host arrays, copied; replaces the previous sets
+ * (no rebuild of the snapshot). n_sets == 0 removes them. */
+int ad_slice_sets_load(ad_ctx* ctx, uint32_t n_sets, const uint64_t* set_off, const int64_t* start, const int64_t* end);
 
 /* ---- batch resolve, host buffers in / host result out ------------------------------ */
 int  ad_deps_batch(ad_ctx* ctx, const ad_query_soa* q, uint32_t flags, ad_deps_result** out);

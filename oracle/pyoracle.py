@@ -52,6 +52,7 @@ def lib():
         L.rc_cfk_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkSoa)]
         L.rc_range_cmds_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsSoa)]
         L.rc_redundant_load.argtypes = [C.c_void_p, C.POINTER(A.AdRedundantSoa)]
+        L.rc_slice_sets_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rc_deps_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_uint64, C.c_uint64,
                                     C.POINTER(C.POINTER(RcResult))]
         L.rc_result_free.argtypes = [C.POINTER(RcResult)]
@@ -125,6 +126,11 @@ class OracleStore:
         self._check(L.rc_cfk_load(self.h, C.byref(workload.cfk.soa())))
         self._check(L.rc_range_cmds_load(self.h, C.byref(workload.cmds.soa())))
         self._check(L.rc_redundant_load(self.h, C.byref(workload.redundant.soa())))
+        ss = getattr(workload, "slice_sets_csr", lambda: None)()
+        if ss is not None:
+            off, st, en = ss
+            self._keep_ss = ss
+            self._check(L.rc_slice_sets_load(self.h, len(off) - 1, A.ptr(off), A.ptr(st), A.ptr(en)))
         ms = workload.cfk.missing_soa()
         if ms is not None:
             self._check(L.rc_cfk_missing_load(self.h, C.byref(ms)))

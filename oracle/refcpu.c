@@ -504,7 +504,11 @@ typedef struct {
 
 struct rc_store {
     ad_config cfg;
-    int64_t* slice_start; int64_t* slice_end; size_t n_slices;
+    /* the slice the request being resolved reads: the store's (st_*) or its slice set (slice_select) */
+    int64_t* slice_start; int64_t* slice_end; size_t n_slices; int slice_all;
+    int64_t* st_start; int64_t* st_end; size_t st_n;
+    /* slice sets (rc_slice_sets_load): set k = [ss_start, ss_end)[ss_off[k], ss_off[k + 1]) */
+    uint64_t* ss_off; int64_t* ss_start; int64_t* ss_end; uint32_t n_ssets;
     VEC(cfk_t) cfks;          /* sorted by key */
     VEC(rcmd_t) cmds;         /* rangeCommands, sorted by txnId */
     VEC(rcmd_t) hist;         /* historicalRangeCommands, sorted by txnId */
@@ -540,7 +544,46 @@ int rc_store_create(const ad_config* cfg, rc_store** out)
     }
     s->cfg.slice_start = s->slice_start;
     s->cfg.slice_end = s->slice_end;
+    s->st_start = s->slice_start;
+    s->st_end = s->slice_end;
+    s->st_n = s->n_slices;
+    s->slice_all = s->n_slices == 0;
     *out = s;
+    return 0;
+}
+
+int rc_slice_sets_load(rc_store* s, uint32_t n_sets, const uint64_t* off, const int64_t* start, const int64_t* end)
+{
+    free(s->ss_off); free(s->ss_start); free(s->ss_end);
+    s->ss_off = NULL; s->ss_start = s->ss_end = NULL; s->n_ssets = 0;
+    if (!n_sets) return 0;
+    const uint64_t nr = off[n_sets];
+    s->ss_off = malloc(sizeof(uint64_t) * (n_sets + 1));
+    s->ss_start = malloc(sizeof(int64_t) * (nr ? nr : 1));
+    s->ss_end = malloc(sizeof(int64_t) * (nr ? nr : 1));
+    copy_n(s->ss_off, off, sizeof(uint64_t) * (n_sets + 1));
+    copy_n(s->ss_start, start, sizeof(int64_t) * nr);
+    copy_n(s->ss_end, end, sizeof(int64_t) * nr);
+    s->n_ssets = n_sets;
+    return 0;
+}
+
+/* The slice request i of q reads: SafeCommandStore.mapReduceActive's `slice` (SafeCommandStore.java:292) =
+ * safeStore.ranges().allBetween(minUnsyncedEpoch, txnId | executeAt) (PreAccept.java:100,130, Accept.java:115,
+ * CommandStores.java:233-242): its slice set, or the store's own slices (q NULL or AD_SLICE_STORE). Nonzero:
+ * an index beyond the loaded sets. */
+static int slice_select(rc_store* s, const ad_query_soa* q, uint64_t i)
+{
+    const uint32_t k = q && q->slice_set ? q->slice_set[i] : AD_SLICE_STORE;
+    if (k == AD_SLICE_STORE || k >= s->n_ssets)
+    {
+        s->slice_start = s->st_start; s->slice_end = s->st_end; s->n_slices = s->st_n; s->slice_all = s->st_n == 0;
+        return k != AD_SLICE_STORE;
+    }
+    s->slice_start = s->ss_start + s->ss_off[k];
+    s->slice_end = s->ss_end + s->ss_off[k];
+    s->n_slices = (size_t)(s->ss_off[k + 1] - s->ss_off[k]);
+    s->slice_all = 0;
     return 0;
 }
 
@@ -564,7 +607,8 @@ void rc_store_destroy(rc_store* s)
     free_cmds(s);
     VEC_FREE(s->rb);
     VEC_FREE(s->miss);
-    free(s->slice_start); free(s->slice_end);
+    free(s->st_start); free(s->st_end);
+    free(s->ss_off); free(s->ss_start); free(s->ss_end);
     free(s);
 }
 
@@ -578,7 +622,7 @@ static int range_contains(const rc_store* s, const rkey_t* r, int64_t key)
 /* Ranges.contains(key): the store's slice (mapReduceForKey, InMemoryCommandStore.java:280) */
 static int slice_contains(const rc_store* s, int64_t key)
 {
-    if (s->n_slices == 0) return 1;
+    if (s->slice_all) return 1;
     for (size_t i = 0; i < s->n_slices; ++i)
     {
         rkey_t r = {s->slice_start[i], s->slice_end[i]};
@@ -599,7 +643,7 @@ static size_t slice_ranges(const rc_store* s, const rkey_t* r, size_t nr, rkey_t
     size_t n = 0;
     for (size_t i = 0; i < nr; ++i)
     {
-        if (s->n_slices == 0)
+        if (s->slice_all)
         {
             out[n++] = r[i];
             continue;
@@ -1156,8 +1200,11 @@ int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t f
             if (rc) { free(ranges); break; }
         }
         pdeps_t pd;
+        /* the request's own slice for its scan (the SEQUENTIAL registration above keeps the store's) */
+        if (slice_select(s, q, i)) { free(ranges); rc = fail(s, AD_E_INVAL, "request %llu: slice_set beyond the slice sets", (unsigned long long)i); break; }
         rc = calculate_partial_deps(s, &txnId, keys, nkeys, ranges, nranges, q->min_epoch ? q->min_epoch[i] : 0, &executeAt, &pd,
                                     &r->scan_entries);
+        slice_select(s, NULL, 0);
         free(ranges);
         if (rc) break;
         result_append(r, qi, &pd, cap, len);
@@ -1718,6 +1765,8 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
         if (rc) break;
         unsigned kinds;
         if (kind_witnessed_by(tid_kind(&txnId), &kinds)) { rc = fail(s, AD_E_INVAL, "invalid Txn.Kind for witnessedBy()"); break; }
+        /* the request's own slice (mapReduceFull's `slice`) until the next request: restored after the loop */
+        if (slice_select(s, q, i)) { rc = fail(s, AD_E_INVAL, "request %llu: slice_set beyond the slice sets", (unsigned long long)i); break; }
         /* a Range-domain request (a recovering sync point or range txn: BeginRecovery passes
          * partialTxn.keys(), Seekables, to mapReduceFull, BeginRecovery.java:334,348,365,378): its
          * normalised Ranges, sliced to the store as mapReduceForKey / mapReduceRangesInternal do */
@@ -1779,6 +1828,7 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
         result_append(r, qi, &pd, cap, len);
         pdeps_free(&pd);
     }
+    slice_select(s, NULL, 0);
     if (rc) { rc_result_free(r); return rc; }
     for (int m = 0; m < AD_NMAPS; ++m)
         if (!r->keys[m]) result_alloc_map(r, m, 1, 1, 1);

@@ -62,6 +62,17 @@ def cfk_active(entries, S, kinds, elide=True, pruned=None):
     return out
 
 
+def slices_of(w, qi):
+    """The slice request qi's scan reads (SafeCommandStore.mapReduceActive's `slice`, SafeCommandStore.java:292):
+    its slice set (Queries.slice_set into Workload.slice_sets: RangesForEpoch.allBetween results) or the store's
+    slices; None = every key."""
+    q = w.queries
+    k = None if getattr(q, "slice_set", None) is None else int(q.slice_set[qi])
+    if k is None or k == 0xFFFFFFFF:
+        return None if w.slices is None else [(int(a), int(b)) for a, b in w.slices]
+    return [(int(a), int(b)) for a, b in np.asarray(w.slice_sets[k], np.int64).reshape(-1, 2)]
+
+
 def request_pairs(w, qi, elide=True):
     """(keyDeps, rangeDeps, directKeyDeps) pair sets of PreAccept.calculatePartialDeps."""
     q = w.queries
@@ -73,16 +84,18 @@ def request_pairs(w, qi, elide=True):
     p1 = None if eq(ex, txn) else txn
     si = w.range_start_inclusive
 
+    own = slices_of(w, qi)
+
     def in_slice(k):
-        if w.slices is None:
+        if own is None:
             return True
-        return any(contains(si, int(a), int(b), k) for a, b in w.slices)
+        return any(contains(si, a, b, k) for a, b in own)
 
     # a Range-domain request (ranges_of non-empty): its keys are every CommandsForKey key inside one of
-    # its ranges and inside the store's slices (InMemoryCommandStore.mapReduceForKey, case Range,
+    # its ranges and inside the request's slices (InMemoryCommandStore.mapReduceForKey, case Range,
     # InMemoryCommandStore.java:289-304) -- a key is in a sliced range iff it is in both
     ranges = q.ranges_of(qi)
-    slices = [(None, None)] if w.slices is None else [(int(a), int(b)) for a, b in w.slices]
+    slices = [(None, None)] if own is None else own
     kd, rd, dd = set(), set(), set()
     cfk = w.cfk
     kidx = {int(k): i for i, k in enumerate(cfk.keys)}
@@ -252,9 +265,10 @@ def recovery_pairs(w, qi, scan):
     ranges = q.ranges_of(qi)
     if ranges:
         keys = [int(k) for k in c.keys if any(contains(si, a, b, int(k)) for a, b in ranges)]
+    own = slices_of(w, qi)
     kd, dd = set(), set()
     for k in keys:
-        if w.slices is not None and not any(contains(si, int(a), int(b), k) for a, b in w.slices):
+        if own is not None and not any(contains(si, a, b, k) for a, b in own):
             continue
         pos = np.searchsorted(c.keys, k)
         if pos >= len(c.keys) or c.keys[pos] != k:
@@ -301,10 +315,11 @@ def recovery_range_pairs(w, qi, scan):
     T = (int(q.txn.msb[qi]), int(q.txn.lsb[qi]), int(q.txn.node[qi]))
     keys = [int(k) for k in q.keys[int(q.key_off[qi]):int(q.key_off[qi + 1])]]
     si = w.range_start_inclusive
-    if w.slices is not None:
-        keys = [k for k in keys if any(contains(si, int(a), int(b), k) for a, b in w.slices)]
+    own = slices_of(w, qi)
+    if own is not None:
+        keys = [k for k in keys if any(contains(si, a, b, k) for a, b in own)]
     ranges = q.ranges_of(qi)
-    slices = [(None, None)] if w.slices is None else [(int(a), int(b)) for a, b in w.slices]
+    slices = [(None, None)] if own is None else own
     started, with_dep, statuses = RECOVER[scan]
     need = 1 if statuses == (3, 4) else 2                  # AD_RS_PROPOSED / AD_RS_STABLE
     kinds = WITNESSED_BY[kind(T)]
