@@ -730,13 +730,15 @@ def shard_local(w, lo, hi):
 # ------------------------------------------------------------------------------------------
 def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_range_cmds=12,
                  n_redundant=3, with_pruned=True, accept_frac=0.3, start_inclusive=False,
-                 with_slices=False, exec_below_frac=0.05, range_frac=0.0):
+                 with_slices=False, exec_below_frac=0.05, range_frac=0.0, truncated=True):
     """All statuses (incl. TRANSITIVELY_KNOWN / INVALID), all globally visible kinds, prunedBefore,
     Accept-style executeAt > txnId (so PreAccept.java:261's self exclusion matters), requests whose
     txnId is in the CFK, range commands (erased / historical / multi-range), RedundantBefore.
     range_frac: that share of the requests (none of them in a CommandsForKey) are Range-domain txns
     (TxnId domain bit set) with 1-3 normalised ranges, from a few keys wide to most of the key space,
-    some touching or crossing slice, command and redundant-before boundaries."""
+    some touching or crossing slice, command and redundant-before boundaries.
+    truncated: the CommandsForKeys as every read of the store sees them, truncated to its RedundantBefore
+    (truncate_to_redundant); False keeps the entries below the watermarks (the load-time truncation's cases)."""
     rng = np.random.default_rng(seed)
     key_space = np.sort(rng.choice(np.arange(-500, 500), n_keys, replace=False)).astype(np.int64)
     hist_kinds = rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_SYNC_POINT, A.KIND_EXCLUSIVE_SYNC_POINT],
@@ -840,8 +842,11 @@ def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_rang
 
     # redundant-before: disjoint ranges with range-domain watermarks
     pts = np.sort(rng.choice(np.arange(-520, 520), 2 * n_redundant, replace=False))
-    rb_wm = make_txn_ids(1, rng.integers(1, 1000, n_redundant).astype(np.uint64) * 7 + 3, A.KIND_EXCLUSIVE_SYNC_POINT,
-                         rng.integers(1, 17, n_redundant), domain=1)
+    # watermarks across the history's epochs and hlcs, so that truncation (SafeCommandStore.maybeTruncate) cuts
+    # into the CommandsForKeys their ranges hold
+    rb_ep = np.where(rng.random(n_redundant) < 0.6, 2, 1).astype(np.uint64)
+    rb_wm = make_txn_ids(rb_ep, rng.integers(1, (n_hist_txns + n_txns) * 10 // 7 + 2, n_redundant).astype(np.uint64) * 7 + 3,
+                         A.KIND_EXCLUSIVE_SYNC_POINT, rng.integers(1, 17, n_redundant), domain=1)
     none = rng.random(n_redundant) < 0.2
     rb_wm = Tids(np.where(none, 0, rb_wm.msb), np.where(none, 0, rb_wm.lsb), np.where(none, 0, rb_wm.node))
     red = Redundant(pts[0::2], pts[1::2], rng.integers(0, 3, n_redundant), rng.integers(2, 5, n_redundant), rb_wm)
@@ -884,8 +889,108 @@ def random_small(seed, n_keys=24, n_hist_txns=120, n_txns=60, max_keys=4, n_rang
     slices = None
     if with_slices:
         slices = np.array([[-400, -100], [0, 300]], np.int64)
+    if truncated:
+        cfk = truncate_to_redundant(cfk, red, start_inclusive)
     return Workload("random_small", cfk, cmds, red, q, params=dict(seed=seed), range_start_inclusive=int(start_inclusive),
                     slices=slices)
+
+
+def truncate_to_redundant(cfk, red, start_inclusive=False):
+    """The CommandsForKeys truncated to the RedundantBefore `red`, as SafeCommandStore.maybeTruncate leaves them
+    (SafeCommandStore.java:165-171 -> CommandsForKey.withRedundantBeforeAtLeast, CommandsForKey.java:1317-1341):
+    per key, byId below its entry's shardRedundantBefore leaves and the rest's missing() lose the ids below it
+    (Utils.removeRedundantMissing) -- both only where something left -- and a prunedBefore at or below it goes."""
+    def contains(s, e, k):
+        return (s <= k < e) if start_inclusive else (s < k <= e)
+    ne = cfk.n_entries
+    keep = np.ones(ne, bool)
+    pruned = None if cfk.pruned_before is None else cfk.pruned_before.copy()
+    lb = [None] * ne                       # per kept entry: the watermark its missing() is trimmed to
+    tid = lambda t, e: (int(t.msb[e]), int(t.lsb[e]), int(t.node[e]))  # noqa: E731
+    for k, key in enumerate(cfk.keys.tolist()):
+        wm = None
+        for i in range(len(red.range_start)):
+            if contains(int(red.range_start[i]), int(red.range_end[i]), key):
+                w = tid(red.wm, i)
+                wm = w if _tid_key(w) > (0, 0, 0, 0) else None
+                break
+        if wm is None:
+            continue
+        s0, s1 = int(cfk.seg[k]), int(cfk.seg[k + 1])
+        pos = 0
+        while s0 + pos < s1 and _tid_key(tid(cfk.txn, s0 + pos)) < _tid_key(wm):
+            pos += 1
+        keep[s0:s0 + pos] = False
+        if pos:
+            for e in range(s0 + pos, s1):
+                lb[e] = wm
+        if pruned is not None and pruned[k] >= 0:
+            pruned[k] = -1 if _tid_key(wm) >= _tid_key(tid(cfk.txn, s0 + int(pruned[k]))) else pruned[k] - pos
+    idx = np.nonzero(keep)[0]
+    e_key = np.repeat(np.arange(len(cfk.keys)), np.diff(cfk.seg.astype(np.int64)))
+    seg = np.zeros(len(cfk.keys) + 1, np.uint64)
+    seg[1:] = np.cumsum(np.bincount(e_key[idx], minlength=len(cfk.keys)))
+    off = miss = None
+    if cfk.miss_off is not None:
+        off, mi = [0], []
+        for e in idx.tolist():
+            for j in range(int(cfk.miss_off[e]), int(cfk.miss_off[e + 1])):
+                if lb[e] is None or _tid_key(tid(cfk.miss, j)) >= _tid_key(lb[e]):
+                    mi.append(j)
+            off.append(len(mi))
+        off = np.array(off, np.uint64)
+        miss = cfk.miss.take(np.array(mi, np.int64))
+    out = CfkSnapshot(cfk.keys, seg, cfk.txn.take(idx), cfk.exec.take(idx), cfk.status[idx], pruned, off, miss)
+    if getattr(cfk, "ballot", None) is not None:
+        out.ballot = cfk.ballot.take(idx)
+    return out
+
+
+def _hlc(t):
+    """Timestamp.hlc() (Timestamp.java:129-131) of a Tids."""
+    return (t.lsb >> np.uint64(16)) | ((t.msb & np.uint64(0x7FFF)) << np.uint64(48))
+
+
+def with_redundant_ranges(w, n_entries=16, seed=0xACC0D0B0, covered=0.8, wm_frac=0.3, none_frac=0.1):
+    """w with a RedundantBefore over its key line: up to n_entries disjoint ranges (about half the line) whose
+    shardAppliedOrInvalidatedBefore are range-domain ExclusiveSyncPoints at up to `wm_frac` of the history's
+    hlcs (epoch 1), `none_frac` of them NONE -- the GC watermark of a store whose oldest history is redundant."""
+    from dataclasses import replace
+    rng = np.random.default_rng(seed)
+    keys = w.cfk.keys if len(w.cfk.keys) else np.array([0, 1], np.int64)
+    lo, hi = int(keys.min()) - 1, int(keys.max()) + 1
+    # consecutive cut pairs [c0, c1), [c2, c3), ... each kept with probability `covered`: disjoint, ascending
+    cuts = np.unique(rng.integers(lo, hi, 2 * n_entries).astype(np.int64))
+    starts, ends = [], []
+    for i in range(0, len(cuts) - 1, 2):
+        if rng.random() < covered:
+            starts.append(int(cuts[i]))
+            ends.append(int(cuts[i + 1]))
+    n = len(starts)
+    hist_hlc = int(_hlc(w.cfk.txn).max()) if w.cfk.n_entries else 1000
+    wm = make_txn_ids(1, rng.integers(1, max(2, int(hist_hlc * wm_frac)), n).astype(np.uint64), A.KIND_EXCLUSIVE_SYNC_POINT,
+                      rng.integers(1, 17, n), domain=1)
+    none = rng.random(n) < none_frac
+    wm = Tids(np.where(none, 0, wm.msb), np.where(none, 0, wm.lsb), np.where(none, 0, wm.node).astype(np.int32))
+    red = Redundant(np.array(starts, np.int64), np.array(ends, np.int64), np.zeros(n, np.int64), np.full(n, 1 << 40, np.int64),
+                    wm)
+    return replace(w, redundant=red)
+
+
+def advance_redundant(red, seed, step_frac=0.15, hist_hlc=None, frac=0.7):
+    """The same RedundantBefore entries with `frac` of the watermarks moved forward by up to step_frac of
+    hist_hlc hlc ticks (NONE ones given one): GC progress, for ad_redundant_advance."""
+    rng = np.random.default_rng(seed)
+    n = len(red.range_start)
+    hlc = _hlc(red.wm)
+    span = max(2, int((hist_hlc or int(hlc.max()) + 1000) * step_frac))
+    move = rng.random(n) < frac
+    nh = hlc + rng.integers(1, span, n).astype(np.uint64)
+    ep = np.maximum(red.wm.msb >> np.uint64(15), np.uint64(1))          # each watermark keeps its epoch
+    new = make_txn_ids(ep, nh, A.KIND_EXCLUSIVE_SYNC_POINT, rng.integers(1, 17, n), domain=1)
+    pick = lambda a, b: np.where(move, b, a)  # noqa: E731
+    wm = Tids(pick(red.wm.msb, new.msb), pick(red.wm.lsb, new.lsb), pick(red.wm.node, new.node).astype(np.int32))
+    return Redundant(red.range_start, red.range_end, red.start_epoch, red.end_epoch, wm)
 
 
 def sequential_ranges(seed, range_frac=0.4, **kw):

@@ -614,10 +614,115 @@ int build_snapshot(ad_ctx* c)
 {
     // the device route takes a snapshot whose columns the load put in HBM, unless a node-wide
     // dictionary is installed (its ranks are the installed dictionary's: the host route)
-    if (c->raw_dev && !c->gd_set) return build_snapshot_device(c);
-    if (int rc = host_inputs(c)) return rc;
-    c->raw_dev = false;
-    return build_snapshot_host(c);
+    int rc;
+    if (c->raw_dev && !c->gd_set)
+        rc = build_snapshot_device(c);
+    else if (!(rc = host_inputs(c)))
+    {
+        c->raw_dev = false;
+        rc = build_snapshot_host(c);
+    }
+    // every read of a CommandsForKey truncates it to the store's RedundantBefore first: the snapshot
+    // is read only as truncated
+    return rc ? rc : truncate_to_rb(c);
+}
+
+const Tid* rb_wm_of(const ad_ctx* c, int64_t key)
+{
+    const auto& B = c->rb;
+    const int incl = c->cfg.range_start_inclusive;
+    size_t lo = 0, hi = B.start.size();
+    while (lo < hi)
+    {
+        const size_t m = (lo + hi) >> 1;
+        if (incl ? B.start[m] <= key : B.start[m] < key) lo = m + 1;
+        else hi = m;
+    }
+    if (!lo || !range_contains(incl, B.start[lo - 1], B.end[lo - 1], key)) return nullptr;
+    return tid_gt_none(B.wm[lo - 1]) ? &B.wm[lo - 1] : nullptr;
+}
+
+bool below_redundant(const ad_ctx* c, int64_t key, const Tid& t)
+{
+    const Tid* w = rb_wm_of(c, key);
+    return w && norm_cmp(norm(t), norm(*w)) < 0;
+}
+
+int truncate_to_rb(ad_ctx* c)
+{
+    bool any = false;
+    for (const Tid& t : c->rb.wm) any = any || tid_gt_none(t);
+    if (!any || !c->ds.n_keys) return 0;
+    auto& K = c->cfk;
+    const uint64_t nk = c->ds.n_keys;
+    // host-held missing() lists follow on the host (their ids need not be in the dictionary); the
+    // device-held ones (dmiss_on) on the device
+    const bool host_lists = !c->dmiss_on && !K.miss_off.empty() && !K.miss_stale;
+    if (host_lists)
+        if (int rc = sync_host(c)) return rc;          // K.seg and the lists index the device's entries
+    if (!c->cu) c->cu = cfk_upd_work_create();
+    CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
+                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
+                  c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr,
+                  c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
+    CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
+                     c->d_w.as<uint2>(), c->d_w.cap / 8};
+    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
+                       c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
+                       c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
+                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
+    CfkMiss miss;
+    miss.on = c->dmiss_on;
+    miss.n_lists = c->dmiss_lists;
+    miss.off = c->d_moff.as<uint64_t>();
+    miss.ids = c->d_mids.as<uint32_t>();
+    miss.ctx = c;
+    miss.spare = cfk_miss_spare;
+    miss.swap = cfk_miss_swap;
+    std::vector<uint32_t> pos(host_lists ? nk : 0);
+    CfkTruncOut o;
+    std::string e;
+    const int rc = run_cfk_truncate(c->cu, c->ds, d, &b, cfk_need_bufs, c, grow, c->stream, &o, &e, &miss,
+                                    host_lists ? pos.data() : nullptr);
+    if (rc)
+    {
+        c->host_stale = true;
+        c->dirty = true;
+        return c->fail(rc, "RedundantBefore truncation: %s", e.c_str());
+    }
+    c->ms_truncate += o.ms_total;
+    c->n_truncated += o.n_removed;
+    c->n_trunc_keys += o.n_keys;
+    if (!o.n_keys) return 0;
+    if (c->kline_slots)
+        HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
+                                   c->kline_slots, c->stream));
+    if (host_lists && o.n_removed)
+    {
+        // removeRedundantMissing on the kept entries of the keys that lost some (Utils.java:265-275)
+        std::vector<uint64_t> off{0};
+        std::vector<Tid> ids;
+        ids.reserve(K.miss.size());
+        for (uint64_t k = 0; k < nk; ++k)
+        {
+            const Tid* wm = pos[k] ? rb_wm_of(c, K.keys[k]) : nullptr;
+            for (uint64_t x = K.seg[k] + pos[k]; x < K.seg[k + 1]; ++x)
+            {
+                for (uint64_t j = K.miss_off[x]; j < K.miss_off[x + 1]; ++j)
+                    if (!wm || norm_cmp(norm(K.miss[j]), norm(*wm)) >= 0) ids.push_back(K.miss[j]);
+                off.push_back(ids.size());
+            }
+        }
+        K.miss_off.swap(off);
+        K.miss.swap(ids);
+    }
+    // host copies follow from the device (entries moved, prunedBefore cleared); host lists were trimmed above
+    c->host_moved = true;
+    c->host_ingested = host_lists;
+    c->host_stale = true;
+    ++c->snap_gen;
+    return 0;
 }
 
 int build_snapshot_host(ad_ctx* c)
@@ -1345,7 +1450,8 @@ int apply_preaccepts(ad_ctx* c, const ad_query_soa* q)
             bool in = c->slice_s.empty();
             for (size_t s = 0; s < c->slice_s.size() && !in; ++s)
                 in = range_contains(c->cfg.range_start_inclusive, c->slice_s[s], c->slice_e[s], key);
-            if (in) ins.push_back({key, norm(t), t});
+            // CommandsForKey.update ignores a txnId below the key's shardRedundantBefore (CommandsForKey.java:997)
+            if (in && !below_redundant(c, key, t)) ins.push_back({key, norm(t), t});
         }
     }
     if (!rng.empty())
@@ -2394,7 +2500,7 @@ int sequential_on_device(ad_ctx* c, const ad_query_soa* q)
             bool in = c->slice_s.empty();
             for (size_t s = 0; s < c->slice_s.size() && !in; ++s)
                 in = range_contains(c->cfg.range_start_inclusive, c->slice_s[s], c->slice_e[s], key);
-            if (!in) continue;
+            if (!in || below_redundant(c, key, t)) continue;          // CommandsForKey.java:997
             keys.push_back(key);
             tm.push_back(t.msb);
             tl.push_back(t.lsb);

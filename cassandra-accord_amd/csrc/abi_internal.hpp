@@ -179,6 +179,9 @@ struct ad_ctx {
     } rb;
     bool dirty = true;
     double ms_ingest = 0;
+    double ms_truncate = 0;         // RedundantBefore truncations since the last stats read (device time)
+    uint64_t n_truncated = 0;       // entries they removed
+    uint64_t n_trunc_keys = 0;      // CommandsForKeys they changed
 
     // built snapshot
     std::vector<uint64_t> dict_msb, dict_lsb;
@@ -328,6 +331,7 @@ struct ad_ctx {
     bool host_stale = false;
     // device ingest (ingest.hip): ad_cfk_load puts the snapshot's columns in HBM (raw_dev) and the
     // build derives everything there; the host's byId ids and dictionary copy follow on demand
+    DevBuf d_adv_m, d_adv_l, d_adv_n, d_adv_rank;     // ad_redundant_advance: the new watermarks, their ranks
     DevBuf d_in_seg, d_in_pruned, d_in_tm, d_in_tl, d_in_tn, d_in_em, d_in_el, d_in_en, d_in_xm, d_in_xl, d_in_xn, d_ing_rank;
     bool raw_dev = false;                            // d_in_* hold the loaded snapshot (no device update since)
     uint64_t raw_ne = 0;
@@ -414,6 +418,13 @@ uint64_t* rb_slot(ad_ctx* c);
 
 // snapshot (abi.cpp): build, host copies of the device state, the node-wide dictionary, the KeyLine hash
 int build_snapshot(ad_ctx* c);
+// the snapshot truncated to the RedundantBefore it holds (SafeCommandStore.maybeTruncate, every key)
+int truncate_to_rb(ad_ctx* c);
+// the key's shardRedundantBefore on the host copy (RedundantBefore.get; null: none or NONE), and whether
+// t is below it
+const Tid* rb_wm_of(const ad_ctx* c, int64_t key);
+bool below_redundant(const ad_ctx* c, int64_t key, const Tid& t);
+bool tid_gt_none(const Tid& t);
 int sync_host(ad_ctx* c);
 int host_dict(ad_ctx* c);
 int pull_missing(ad_ctx* c);
@@ -429,6 +440,17 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
 int result_to_host(ad_ctx* c, uint64_t n, const ad_deps_result& dev, ad_deps_result** out);
 // CommandsForKey maintenance (abi_update.cpp)
 int cfk_need_bufs(void* vc, uint64_t n_cand, uint64_t n_cwr, uint64_t n_w, CfkDerivedBufs* b);
+// the CfkGrow / CfkMiss callbacks over the ctx's buffers
+int cfk_grow_dict(void* vc, uint64_t n_old, uint64_t n_new, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw);
+int cfk_grow_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal, uint32_t** mref);
+int cfk_swap_entries(void* vc, uint64_t ne, uint2** ent, uint8_t** st, uint32_t** xr, uint32_t** ek, Bal** bal, uint32_t** mref);
+int cfk_ballot_init(void* vc, uint64_t ne, Bal** bal);
+int cfk_dict_spare(void* vc, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw);
+int cfk_dict_swap(void* vc, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw);
+int cfk_keys_spare(void* vc, uint64_t nk, KeyBufs* b);
+int cfk_keys_swap(void* vc, KeyBufs* b);
+int cfk_miss_spare(void* vc, uint64_t n, uint64_t n_ids, uint64_t** off, uint32_t** ids);
+int cfk_miss_swap(void* vc, uint64_t** off, uint32_t** ids);
 int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats);
 
 }  // namespace adi

@@ -742,6 +742,118 @@ int ad_cfk_prune(ad_ctx* c, const int64_t* keys, uint64_t n_keys, int32_t prune_
     return AD_OK;
 }
 
+// ---- RedundantBefore advanced in place (SafeCommandStore.maybeTruncate on the next reads) ----
+int ad_redundant_advance(ad_ctx* c, const ad_redundant_soa* in, ad_stats* stats)
+{
+    if (!c || !in) return AD_E_INVAL;
+    auto& B = c->rb;
+    const uint64_t n = in->n;
+    if (n != B.start.size())
+        return c->fail(AD_E_INVAL, "ad_redundant_advance: %llu entries, %llu loaded (a change of ranges is ad_redundant_load)",
+                       (unsigned long long)n, (unsigned long long)B.start.size());
+    if (n && (!in->range_start || !in->range_end || !in->start_epoch || !in->end_epoch || !in->wm_msb || !in->wm_lsb ||
+              !in->wm_node))
+        return c->fail(AD_E_INVAL, "ad_redundant_advance: null arrays");
+    std::vector<uint64_t> moved;
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        if (in->range_start[i] != B.start[i] || in->range_end[i] != B.end[i])
+            return c->fail(AD_E_INVAL, "ad_redundant_advance: entry %llu's range differs from the loaded one (a change of ranges "
+                           "is ad_redundant_load)", (unsigned long long)i);
+        const Tid t{in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
+        const int cmp = norm_cmp(norm(t), norm(B.wm[i]));
+        if (cmp < 0)
+            return c->fail(AD_E_INVAL, "ad_redundant_advance: entry %llu: expect the new shardAppliedOrInvalidatedBefore to be "
+                           "ahead of the existing one (CommandsForKey.java:1319)", (unsigned long long)i);
+        if (tid_gt_none(t) && (t.lsb & 1) == 0) return c->fail(AD_E_INVAL, "redundantBefore watermark must be range-domain");
+        if (cmp > 0) moved.push_back(i);
+    }
+    if (stats) *stats = ad_stats{};
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        B.e0[i] = in->start_epoch[i];
+        B.e1[i] = in->end_epoch[i];
+        B.wm[i] = Tid{in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
+    }
+    // before the first build the snapshot reads them (and truncates) when it is built
+    if (!c->cfk.loaded || c->dirty) return AD_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
+    const double t0 = now_ms();
+    if (int rc = upload(c, c->d_rb_e0, B.e0)) return rc;
+    if (int rc = upload(c, c->d_rb_e1, B.e1)) return rc;
+    c->ds.rb_e0 = c->d_rb_e0.as<int64_t>();
+    c->ds.rb_e1 = c->d_rb_e1.as<int64_t>();
+    if (moved.empty())
+    {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        return AD_OK;
+    }
+    // the new watermarks join the id dictionary (appended or merged with the rank remap of an update
+    // batch), their member ranks replace the moved entries' in rb_wm
+    const uint64_t nx = moved.size();
+    std::vector<uint64_t> xm(nx), xl(nx);
+    std::vector<int32_t> xn(nx);
+    for (uint64_t j = 0; j < nx; ++j)
+    {
+        xm[j] = B.wm[moved[j]].msb;
+        xl[j] = B.wm[moved[j]].lsb;
+        xn[j] = B.wm[moved[j]].node;
+    }
+    if (int rc = upload(c, c->d_adv_m, xm)) return rc;
+    if (int rc = upload(c, c->d_adv_l, xl)) return rc;
+    if (int rc = upload(c, c->d_adv_n, xn)) return rc;
+    if (!c->d_adv_rank.ensure(4 * nx)) return c->fail(AD_E_NOMEM, "watermark ranks");
+    if (int rc = host_dict(c)) return rc;
+    if (!c->cu) c->cu = cfk_upd_work_create();
+    CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
+                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
+                  c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr,
+                  c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
+    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
+                       c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
+                       c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
+                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
+    CfkUpdOut o;
+    std::string e;
+    const int rc = run_cfk_dict_ensure(c->cu, c->ds, d, c->d_adv_m.as<uint64_t>(), c->d_adv_l.as<uint64_t>(),
+                                       c->d_adv_n.as<int32_t>(), nx, grow, c->stream, &o, c->d_adv_rank.as<uint32_t>(), &e);
+    if (const int frc = cfk_update_follow(c, o, rc, c->stream))
+    {
+        c->host_stale = true;
+        c->dirty = true;
+        return frc;
+    }
+    if (rc)
+    {
+        // the loaded RedundantBefore stands for the device; rebuilt from the host copy at the next use
+        c->dirty = true;
+        return c->fail(rc, "ad_redundant_advance: %s", e.c_str());
+    }
+    std::vector<uint32_t> wr(n), nr(nx);
+    HIPCHK(c, d2h(wr.data(), c->d_rb_wm.p, 4 * n, c->stream));      // remapped by a merge
+    HIPCHK(c, d2h(nr.data(), c->d_adv_rank.p, 4 * nx, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (uint64_t j = 0; j < nx; ++j) wr[moved[j]] = nr[j];
+    if (int rc2 = upload(c, c->d_rb_wm, wr)) return rc2;
+    c->ds.rb_wm = c->d_rb_wm.as<uint32_t>();
+    const double ms_dict = now_ms() - t0;
+    c->ms_truncate = 0;
+    c->n_truncated = 0;
+    c->n_trunc_keys = 0;
+    if (int rc2 = truncate_to_rb(c)) return rc2;
+    if (stats)
+    {
+        stats->ms_device = c->ms_truncate;
+        stats->ms_stage[0] = ms_dict;               // host-timed: watermark upload + dictionary growth
+        stats->n_keys[0] = c->n_truncated;
+        stats->n_keys[1] = c->n_trunc_keys;
+        stats->n_keys[2] = o.n_new_ids;
+    }
+    return AD_OK;
+}
+
 int ad_cfk_missing(ad_ctx* c, uint64_t* n_entries, const uint64_t** off, const uint64_t** msb, const uint64_t** lsb,
                    const int32_t** node)
 {

@@ -1424,6 +1424,7 @@ struct CfkUpdWork {
     // byId's last txnId as each update sees it (additions past the end) and the LoadPruned ids
     DBuf trk, pk, pv, pk2, pv2, pvv, pw, pe, pbm, plast, ppos, lcnt, loff, l_k, l_tm, l_tl, l_tn, l_i;
     DBuf kn_a, kn_b, kv_a, kv_b, kflag, kfpos, knew, kpos;   // new keys
+    DBuf tpos, twm, ids_st, ids_rank;                          // RedundantBefore truncation / dictionary ensure
     // incremental committed order: the last derivation's order (entry indices), per-entry changed
     // flags (double-buffered with the entry arrays), the insertion's old -> new entry map
     DBuf cm, chg[2], mv, af, ap, bfl, bps, cka, cva, ckb, cvb, ckb2, cvb2;
@@ -2614,6 +2615,282 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
     (void)hipEventElapsedTime(&a_ms, w->ev[0], w->ev[1]);
     out->ms_total = a_ms;
     if (w->h_ctl->err) { *err = "derivation after pruning reported an inconsistency"; return AD_E_STATE; }
+    return AD_OK;
+}
+
+
+// =============================================================================================
+// RedundantBefore on the device: SafeCommandStore.maybeTruncate (SafeCommandStore.java:165-171) ->
+// SafeCommandsForKey.updateRedundantBefore -> CommandsForKey.withRedundantBeforeAtLeast
+// (CommandsForKey.java:1317-1341). For every key, the byId entries below its RedundantBefore entry's
+// shardRedundantBefore leave and the missing() lists of the rest lose the ids below it
+// (Utils.removeRedundantMissing, Utils.java:265-275) -- both only where something left
+// (insertPos != 0); a prunedBefore at or below it becomes NO_INFO (the constructor, :646-648). The
+// watermarks are the snapshot's rb_wm ranks (dictionary members; 0 = NONE).
+// =============================================================================================
+namespace {
+
+// the RedundantBefore entry holding key x (RedundantBefore.get: a lookup over the disjoint ascending
+// entries; epochs not read), or ~0
+__device__ inline uint64_t rb_entry_holding(const DevSnapshot& s, int64_t x)
+{
+    const bool incl = s.start_inclusive != 0;
+    uint64_t lo = 0, hi = s.n_rb;
+    while (lo < hi)
+    {
+        const uint64_t m = (lo + hi) >> 1;
+        if (incl ? s.rb_start[m] <= x : s.rb_start[m] < x) lo = m + 1;
+        else hi = m;
+    }
+    if (!lo) return ~0ull;
+    return range_contains(s.start_inclusive, s.rb_start[lo - 1], s.rb_end[lo - 1], x) ? lo - 1 : ~0ull;
+}
+
+// thread per key: t_pos[k] = insertPos(shardRedundantBefore) within byId (the entries that leave),
+// t_wm[k] = its rank (0: NONE or no entry); a prunedBefore at or below it is cleared in place;
+// *n_chg counts the keys that change
+__global__ void k_trunc_key(uint64_t nk, DevSnapshot s, KeyRec* krec, uint32_t* t_pos, uint32_t* t_wm,
+                            unsigned long long* n_chg)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    uint32_t pos = 0, wm = 0;
+    const uint64_t e = rb_entry_holding(s, s.keys[k]);
+    if (e != ~0ull) wm = s.rb_wm[e];
+    bool chg = false;
+    if (wm)
+    {
+        const KeyRec kr = krec[k];
+        uint32_t lo = kr.seg_lo, hi = kr.seg_hi;
+        while (lo < hi)
+        {
+            const uint32_t m = (lo + hi) >> 1;
+            if ((s.ent[m].y & RANK_MASK) < wm) lo = m + 1;
+            else hi = m;
+        }
+        pos = lo - kr.seg_lo;
+        chg = pos != 0;
+        if (kr.pruned && wm >= kr.pruned)
+        {
+            krec[k].pruned = 0;
+            chg = true;
+        }
+    }
+    t_pos[k] = pos;
+    t_wm[k] = wm;
+    if (chg) atomicAdd(n_chg, 1ull);
+}
+
+// thread per entry: below its key's shardRedundantBefore (a prefix of the key's byId)
+__global__ void k_trunc_mark(uint64_t ne, const uint32_t* ekey, const KeyRec* krec, const uint32_t* t_pos, uint32_t* rm)
+{
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= ne) return;
+    const uint32_t k = ekey[e];
+    rm[e] = (e - krec[k].seg_lo < t_pos[k]) ? 1u : 0u;
+}
+
+// thread per key: segments after the removals (an emptied byId has no last txnId)
+__global__ void k_trunc_keys(uint64_t nk, KeyRec* krec, const uint64_t* rpos)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    KeyRec kr = krec[k];
+    kr.seg_lo -= (uint32_t)rpos[kr.seg_lo];
+    kr.seg_hi -= (uint32_t)rpos[kr.seg_hi];
+    if (kr.seg_hi == kr.seg_lo) kr.last_txn = 0;
+    krec[k] = kr;
+}
+
+// thread per kept entry (its list mref[j] of the old CSR): the ids at or above the key's
+// shardRedundantBefore where entries left (removeRedundantMissing), all of them elsewhere. Pass 0
+// counts, pass 1 writes.
+template <int WRITE>
+__global__ __launch_bounds__(256) void k_trunc_miss(uint64_t n, const uint32_t* mref, const uint32_t* ekey,
+                                                    const uint32_t* t_pos, const uint32_t* t_wm, const uint64_t* ooff,
+                                                    const uint32_t* oids, uint32_t* cnt, const uint64_t* noff, uint32_t* nids)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t L = mref[j];
+    uint64_t c = 0, o = WRITE ? noff[j] : 0;
+    if (L != MREF_NONE && L != MREF_BORN)
+    {
+        const uint32_t k = ekey[j];
+        const uint32_t lb = t_pos[k] ? t_wm[k] : 0;
+        for (uint64_t a = ooff[L]; a < ooff[L + 1]; ++a)
+        {
+            const uint32_t r = oids[a];
+            if (r < lb) continue;
+            if (WRITE) nids[o++] = r;
+            ++c;
+        }
+    }
+    if (!WRITE) cnt[j] = (uint32_t)c;
+}
+
+// thread per id: its dictionary rank (a member after run_cfk_dict_ensure); a miss flags ctl->err
+__global__ void k_id_ranks(DevSnapshot s, DictSample ds, uint64_t n, const uint64_t* msb, const uint64_t* lsb,
+                           const int32_t* node, uint32_t* rank, UpdCtl* ctl)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t p;
+    const uint32_t r = dict_member_rank(s, ds, norm_tid(msb[i], lsb[i], node[i]), &p);
+    rank[i] = r;
+    if (!r) upd_fail(ctl, UE_ABSENT, (uint32_t)i);
+}
+
+}  // namespace
+
+int run_cfk_truncate(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, CfkDerivedBufs* bufs,
+                     int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                     const CfkGrow& grow, hipStream_t st, CfkTruncOut* out, std::string* err, CfkMiss* miss,
+                     uint32_t* h_pos)
+{
+    *out = CfkTruncOut{};
+    const uint64_t ne = s.n_ent, nk = s.n_keys;
+    if (!nk || !s.n_rb) return AD_OK;
+    if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
+    for (auto& e : w->ev)
+        if (!e) UCHK(timing_event(&e));
+    UALLOC(w->ctl, sizeof(UpdCtl), false);
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    UCHK(hipEventRecord(w->ev[0], st));
+    UALLOC(w->tpos, 4 * nk, false);
+    UALLOC(w->twm, 4 * nk, false);
+    uint32_t* t_pos = w->tpos.as<uint32_t>();
+    uint32_t* t_wm = w->twm.as<uint32_t>();
+    unsigned long long* n_chg = reinterpret_cast<unsigned long long*>(&ctl->tot2[1]);
+    k_trunc_key<<<blocks(nk), 256, 0, st>>>(nk, s, d.krec, t_pos, t_wm, n_chg);
+    if (ne)
+    {
+        UALLOC(w->uflag, 4 * ne, false);        // rm
+        UALLOC(w->upos, 8 * (ne + 1), false);   // rpos
+        UALLOC(w->bsum, 8 * ((ne + 1023) / 1024 + 8), false);
+        k_trunc_mark<<<blocks(ne), 256, 0, st>>>(ne, d.ekey, d.krec, t_pos, w->uflag.as<uint32_t>());
+        UCHK(run_scan_arrays(w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), ne, 1, w->bsum.as<uint64_t>(), st));
+        k_drv_totals<<<1, 64, 0, st>>>(w->upos.as<uint64_t>(), ne, 1, ctl->tot2);
+    }
+    UCHK(hipGetLastError());
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
+    UCHK(hipStreamSynchronize(st));
+    const uint64_t R = ne ? w->h_ctl->tot2[0] : 0, changed = w->h_ctl->tot2[1];
+    auto finish = [&]() -> int {
+        UCHK(hipEventRecord(w->ev[1], st));
+        UCHK(hipEventSynchronize(w->ev[1]));
+        float a = 0;
+        (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
+        out->ms_total = a;
+        return AD_OK;
+    };
+    if (!changed) return finish();
+    if (h_pos) UCHK(d2h(h_pos, t_pos, 4 * nk, st));      // the host's lists follow (the caller trims them)
+    if (R)
+    {
+        // compaction into the spare per-entry arrays and the segments, as pruning does
+        EntArrays a{d.ent, d.status, d.xrank, d.ekey, d.ballot, nullptr, d.mref}, b{};
+        if (int rc = grow.entries(grow.ctx, ne - R, &b.ent, &b.status, &b.xrank, &b.ekey, &b.bal, &b.mref)) { *err = "entry arrays"; return rc; }
+        const uint64_t padded = std::max<uint64_t>(64, (ne - R + 63) / 64 * 64);
+        if (padded > ne - R) UCHK(hipMemsetAsync(b.ent + (ne - R), 0, sizeof(uint2) * (padded - (ne - R)), st));
+        k_prune_move<<<blocks(ne), 256, 0, st>>>(ne, a, w->uflag.as<uint32_t>(), w->upos.as<uint64_t>(), b);
+        k_trunc_keys<<<blocks(nk), 256, 0, st>>>(nk, d.krec, w->upos.as<uint64_t>());
+        UCHK(hipGetLastError());
+        if (int rc = grow.swap(grow.ctx, ne - R, &d.ent, &d.status, &d.xrank, &d.ekey, &d.ballot, &d.mref)) { *err = "entry swap"; return rc; }
+        s.ent = d.ent;
+        s.n_ent = ne - R;
+        UALLOC(w->chg[w->chg_cur], std::max<uint64_t>(ne - R, 1), false);
+    }
+    if (!R)
+    {
+        // only prunedBefore moved (krec, in place): nothing derived reads it
+        out->n_keys = changed;
+        return finish();
+    }
+    w->cm_valid = false;          // entry indices changed: the next derivation sorts afresh
+    w->moved = false;
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rc;
+    if (d.mref && miss && miss->on)
+    {
+        // the kept entries' lists, trimmed and compacted (each entry its own list again)
+        const uint64_t n2 = s.n_ent;
+        UALLOC(w->mcnt, 4 * std::max<uint64_t>(n2, 1), false);
+        UALLOC(w->moff, 8 * (n2 + 1), false);
+        UALLOC(w->bsum, 8 * ((n2 + 1023) / 1024 + 8), false);
+        if (n2)
+            k_trunc_miss<0><<<blocks(n2), 256, 0, st>>>(n2, d.mref, d.ekey, t_pos, t_wm, miss->off, miss->ids,
+                                                        w->mcnt.as<uint32_t>(), nullptr, nullptr);
+        UCHK(run_scan_arrays(w->mcnt.as<uint32_t>(), w->moff.as<uint64_t>(), n2, 1, w->bsum.as<uint64_t>(), st));
+        uint64_t nm = 0;
+        UCHK(d2h(&nm, w->moff.as<uint64_t>() + n2, 8, st));
+        UCHK(hipStreamSynchronize(st));
+        uint64_t* noff = nullptr;
+        uint32_t* nids = nullptr;
+        if (int rc = miss->spare(miss->ctx, n2, nm, &noff, &nids)) { *err = "missing() lists"; return rc; }
+        UCHK(hipMemcpyAsync(noff, w->moff.p, 8 * (n2 + 1), hipMemcpyDeviceToDevice, st));
+        if (n2)
+        {
+            k_trunc_miss<1><<<blocks(n2), 256, 0, st>>>(n2, d.mref, d.ekey, t_pos, t_wm, miss->off, miss->ids, nullptr, noff,
+                                                        nids);
+            k_mref_identity<<<blocks(n2), 256, 0, st>>>(n2, d.mref);
+        }
+        UCHK(hipGetLastError());
+        UCHK(hipStreamSynchronize(st));
+        if (int rc = miss->swap(miss->ctx, &miss->off, &miss->ids)) { *err = "missing() lists"; return rc; }
+        miss->n_lists = n2;
+    }
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
+    UCHK(hipStreamSynchronize(st));
+    if (w->h_ctl->err) { *err = "derivation after truncation reported an inconsistency"; return AD_E_STATE; }
+    out->n_removed = R;
+    out->n_keys = changed;
+    return finish();
+}
+
+int run_cfk_dict_ensure(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint64_t* msb, const uint64_t* lsb,
+                        const int32_t* node, uint64_t n, const CfkGrow& grow, hipStream_t st, CfkUpdOut* out,
+                        uint32_t* ranks, std::string* err)
+{
+    *out = CfkUpdOut{};
+    if (!n) return AD_OK;
+    if (!w->h_ctl && hipHostMalloc((void**)&w->h_ctl, sizeof(UpdCtl)) != hipSuccess) { *err = "pinned ctl"; return AD_E_NOMEM; }
+    UALLOC(w->ctl, sizeof(UpdCtl), false);
+    UpdCtl* ctl = w->ctl.as<UpdCtl>();
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    UALLOC(w->ids_st, n, false);
+    UCHK(hipMemsetAsync(w->ids_st.p, 0, n, st));       // TRANSITIVELY_KNOWN: the txnId side only
+    CfkUpdIn u{};
+    u.n = n;
+    u.txn_msb = u.exec_msb = msb;
+    u.txn_lsb = u.exec_lsb = lsb;
+    u.txn_node = u.exec_node = node;
+    u.status = w->ids_st.as<uint8_t>();
+    const uint64_t ns = std::max<uint64_t>((s.n_dict + n + SAMP - 1) / SAMP, 1);
+    UALLOC(w->sm_hi, 8 * ns, false);
+    UALLOC(w->sm_lo, 8 * ns, false);
+    UALLOC(w->sm_node, 4 * ns, false);
+    auto sample = [&]() -> DictSample {
+        const uint64_t n_samp = (s.n_dict + SAMP - 1) / SAMP;
+        if (n_samp)
+            k_dict_sample<<<blocks(n_samp), 256, 0, st>>>(s, w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(),
+                                                          w->sm_node.as<int32_t>(), n_samp);
+        return DictSample{w->sm_hi.as<uint64_t>(), w->sm_lo.as<uint64_t>(), w->sm_node.as<int32_t>(), n_samp};
+    };
+    const DictSample ds0 = sample();
+    if (int rc = grow_dictionary(w, s, d, ds0, u, grow, st, out, err)) return rc;
+    if (w->h_ctl->err)
+    {
+        *err = "ids equal under Timestamp.equals differ in flag bits";
+        return AD_E_INCONSISTENT_ID;
+    }
+    const DictSample ds1 = sample();
+    k_id_ranks<<<blocks(n), 256, 0, st>>>(s, ds1, n, msb, lsb, node, ranks, ctl);
+    UCHK(hipGetLastError());
+    UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
+    UCHK(hipStreamSynchronize(st));
+    if (w->h_ctl->err) { *err = "id missing from the dictionary after its growth (internal)"; return AD_E_STATE; }
     return AD_OK;
 }
 

@@ -179,4 +179,28 @@ int run_cfk_prune(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint32_t*
                   int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
                   const CfkGrow& grow, hipStream_t st, CfkPruneOut* out, std::string* err, CfkMiss* miss = nullptr);
 
+struct CfkTruncOut {
+    uint64_t n_removed = 0;        // entries removed
+    uint64_t n_keys = 0;           // CommandsForKeys that changed (entries left or prunedBefore cleared)
+    double ms_total = 0;
+};
+
+// CommandsForKey.withRedundantBeforeAtLeast (CommandsForKey.java:1317-1341) of every key to the
+// snapshot's RedundantBefore (rb_* views; watermark ranks are dictionary members): the entries below
+// the key's shardRedundantBefore leave (compacted into the spare buffers), a prunedBefore at or below
+// it is cleared, the derived arrays are rebuilt, and with miss on the kept entries' missing() lists
+// lose the ids below it (Utils.removeRedundantMissing). h_pos (host, n_keys; may be null): each key's
+// count of removed entries, for host-held lists.
+int run_cfk_truncate(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, CfkDerivedBufs* bufs,
+                     int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                     const CfkGrow& grow, hipStream_t st, CfkTruncOut* out, std::string* err, CfkMiss* miss,
+                     uint32_t* h_pos);
+
+// The ids (device arrays, n) join the dictionary where it does not hold them (appended, or merged
+// with the rank remap of an update batch: out->merged / merge_pos as run_cfk_update reports them);
+// ranks[i] (device) = each id's member rank afterwards.
+int run_cfk_dict_ensure(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint64_t* msb, const uint64_t* lsb,
+                        const int32_t* node, uint64_t n, const CfkGrow& grow, hipStream_t st, CfkUpdOut* out,
+                        uint32_t* ranks, std::string* err);
+
 }  // namespace adx

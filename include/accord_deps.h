@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define AD_ABI_VERSION 5
+#define AD_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define AD_OK                  0
@@ -303,6 +303,23 @@ const char* ad_last_error(const ad_ctx* ctx);
 int ad_cfk_load(ad_ctx* ctx, const ad_cfk_soa* cfk);
 int ad_range_cmds_load(ad_ctx* ctx, const ad_range_cmds_soa* cmds);
 int ad_redundant_load(ad_ctx* ctx, const ad_redundant_soa* rb);
+/* Every read of the store sees its CommandsForKeys truncated to the RedundantBefore: the snapshot is
+ * truncated on the device when it is built (SafeCommandStore.maybeTruncate, SafeCommandStore.java:165-171
+ * -> CommandsForKey.withRedundantBeforeAtLeast, CommandsForKey.java:1317-1341): byId below the key's
+ * shardRedundantBefore leaves, the missing() lists of the rest lose the ids below it, a prunedBefore at or
+ * below it becomes NO_INFO. SEQUENTIAL PreAccepts below it register nothing (CommandsForKey.java:997);
+ * ad_cfk_update leaves that filter to the caller.
+ *
+ * ad_redundant_advance: the store's RedundantBefore moves forward in place, without a snapshot rebuild
+ * (RedundantBefore.merge as the store's GC advances it, CommandStore.upsertRedundantBefore). rb names the
+ * same entries (ranges) as the loaded RedundantBefore, in the same order, with epochs and watermarks that
+ * may change: each watermark at or above the loaded one (AD_E_INVAL otherwise, as
+ * CommandsForKey.java:1319's Invariants.checkArgument). New watermarks join the id dictionary on the
+ * device and every CommandsForKey whose watermark moved is truncated on the device (its missing() lists
+ * too, wherever they are held). A change of ranges is an ad_redundant_load. stats (may be NULL):
+ * ms_device = device time of the truncation, ms_stage[0] = the watermarks' dictionary growth (host-timed), n_keys[0]
+ * = entries removed, n_keys[1] = CommandsForKeys changed, n_keys[2] = ids added to the dictionary. */
+int ad_redundant_advance(ad_ctx* ctx, const ad_redundant_soa* rb, ad_stats* stats);
 /* Build the id dictionary and device indexes of the loaded snapshot now (otherwise the first
  * batch does it). Ingest time is reported in ad_stats.ms_ingest, never in ms_device. */
 int ad_prepare(ad_ctx* ctx);

@@ -770,6 +770,33 @@ int rc_redundant_load(rc_store* s, const ad_redundant_soa* in)
     return 0;
 }
 
+/* The store's RedundantBefore moved forward in place (ad_redundant_advance): the same entries, epochs and
+ * watermarks replaced, each watermark at or above the old one (CommandsForKey.withRedundantBeforeAtLeast's
+ * Invariants.checkArgument, CommandsForKey.java:1319). The CommandsForKeys are truncated to it when next read
+ * (store_truncate), as SafeCommandStore.maybeTruncate does. */
+int rc_redundant_advance(rc_store* s, const ad_redundant_soa* in)
+{
+    if (in->n != s->rb.n) return fail(s, AD_E_INVAL, "advance names %llu entries, %llu loaded",
+                                      (unsigned long long)in->n, (unsigned long long)s->rb.n);
+    for (uint64_t i = 0; i < in->n; ++i)
+    {
+        const rb_entry_t* e = &s->rb.v[i];
+        const tid_t wm = {in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
+        if (e->range.a != in->range_start[i] || e->range.b != in->range_end[i])
+            return fail(s, AD_E_INVAL, "advance entry %llu: range differs", (unsigned long long)i);
+        if (tid_cmp(&wm, &e->wm) < 0)
+            return fail(s, AD_E_INVAL, "advance entry %llu: watermark behind the existing one", (unsigned long long)i);
+    }
+    for (uint64_t i = 0; i < in->n; ++i)
+    {
+        rb_entry_t* e = &s->rb.v[i];
+        e->startEpoch = in->start_epoch[i];
+        e->endEpoch = in->end_epoch[i];
+        e->wm = (tid_t){in->wm_msb[i], in->wm_lsb[i], in->wm_node[i]};
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* PreAccept.calculatePartialDeps                                                       */
 /* ------------------------------------------------------------------------------------ */
@@ -994,12 +1021,16 @@ static int calculate_partial_deps(rc_store* s, const tid_t* txnId, const int64_t
 /* PREACCEPTED insertion of Commands.preaccept -> SafeCommandStore.update ->
  * CommandsForKey.update (CommandsForKey.java:972-1042): insert TxnInfo(txnId,
  * PREACCEPTED_OR_ACCEPTED_INVALIDATE, executeAt = txnId) or raise a lower status. */
+static const rb_entry_t* rb_entry_of(const rc_store* s, int64_t key);
 static void sequential_preaccept(rc_store* s, const tid_t* txnId, const int64_t* keys, size_t nkeys)
 {
     if (!manages(txnId)) return;
     for (size_t k = 0; k < nkeys; ++k)
     {
         if (!slice_contains(s, keys[k])) continue;
+        /* CommandsForKey.update: a txnId below the key's shardRedundantBefore changes nothing (:997) */
+        const rb_entry_t* rbe = rb_entry_of(s, keys[k]);
+        if (rbe && tid_cmp(txnId, &rbe->wm) < 0) continue;
         cfk_t* c = find_cfk(s, keys[k]);
         if (c == NULL)
         {
@@ -1146,9 +1177,60 @@ static void result_append(rc_result* r, uint64_t qi, const pdeps_t* pd, size_t c
     }
 }
 
+/* The RedundantBefore entry holding key (RedundantBefore.get, a ReducingRangeMap lookup: epochs not read), or NULL */
+static const rb_entry_t* rb_entry_of(const rc_store* s, int64_t key)
+{
+    for (size_t i = 0; i < s->rb.n; ++i)
+        if (range_contains(s, &s->rb.v[i].range, key)) return &s->rb.v[i];
+    return NULL;
+}
+
+/* SafeCommandStore.maybeTruncate (SafeCommandStore.java:165-171) before a CommandsForKey is read:
+ * SafeCommandsForKey.updateRedundantBefore -> CommandsForKey.withRedundantBeforeAtLeast (CommandsForKey.java:1317-1341)
+ * with the key's RedundantBefore entry -- byId[0, insertPos(shardRedundantBefore)) leaves and the missing() of the
+ * rest lose the ids below it (Utils.removeRedundantMissing, Utils.java:265-275), both only when insertPos != 0;
+ * the new CommandsForKey's constructor drops prunedBefore when shardRedundantBefore >= it (:646-648). Idempotent
+ * (a truncated CommandsForKey is truncated again to the same), so it is applied to every key before a batch reads,
+ * as every read of the Java would. */
+static void store_truncate(rc_store* s)
+{
+    static const tid_t NONE = {0, 0, 0};
+    if (s->rb.n == 0) return;
+    for (size_t k = 0; k < s->cfks.n; ++k)
+    {
+        cfk_t* c = &s->cfks.v[k];
+        const rb_entry_t* e = rb_entry_of(s, c->key);
+        if (!e || tid_cmp(&e->wm, &NONE) <= 0) continue;               /* shardRedundantBefore = NONE: nothing below */
+        const tid_t* wm = &e->wm;
+        int changed = 0;
+        const int pos = cfk_insert_pos(c, wm);
+        if (pos != 0)
+        {
+            memmove(c->byId.v, c->byId.v + pos, (c->byId.n - (size_t)pos) * sizeof(info_t));
+            c->byId.n -= (size_t)pos;
+            for (size_t i = 0; i < c->byId.n; ++i)
+            {
+                info_t* t = &c->byId.v[i];
+                uint32_t j = 0;                                         /* removeRedundantMissing: ids below wm go */
+                while (j < t->miss_n && tid_cmp(&s->miss.v[t->miss_off + j], wm) < 0) ++j;
+                t->miss_off += j;
+                t->miss_n -= j;
+            }
+            changed = 1;
+        }
+        if (c->hasPrunedBefore && tid_cmp(wm, &c->prunedBefore) >= 0)
+        {
+            c->hasPrunedBefore = 0;
+            changed = 1;
+        }
+        if (changed) cfk_derive(c);
+    }
+}
+
 int rc_deps_batch(rc_store* s, const ad_query_soa* q, uint32_t flags, uint64_t first, uint64_t count, rc_result** out)
 {
     if (!s->loaded) return fail(s, AD_E_NOT_LOADED, "ad_cfk_load not called");
+    store_truncate(s);
     if (count == 0) count = q->n_txns - first;
     if (first + count > q->n_txns) return fail(s, AD_E_INVAL, "query window out of range");
     rc_result* r = calloc(1, sizeof(rc_result));
@@ -1738,6 +1820,7 @@ int rc_recovery_batch(rc_store* s, const ad_query_soa* q, uint32_t scan, uint64_
                                 {STARTED_AFTER, WITHOUT, IS_PROPOSED}, {ANY, WITHOUT, IS_STABLE}};
     if (!s->loaded) return fail(s, AD_E_NOT_LOADED, "ad_cfk_load not called");
     if (scan > 3) return fail(s, AD_E_INVAL, "unknown recovery scan %u", scan);
+    store_truncate(s);
     for (size_t i = 0; i < s->cmds.n; ++i)
         if (!s->cmds.v[i].erased && !s->cmds.v[i].has_rec)
             return fail(s, AD_E_STATE, "recovery scans of range commands need their recovery facts (rc_range_cmds_recovery_load)");

@@ -2,7 +2,9 @@
 """Regenerate the golden fixtures of tests/golden/ from the CPU restatement (oracle/refcpu.c).
 
 The reference (Java) cannot run in this image (no JDK) and holds no golden vectors
-of its own, so these fixtures are outputs of the oracle, which is itself pinned by the
+of its own, so these fixtures are outputs of the oracle (round 6: regenerated when the oracle began
+to restate SafeCommandStore.maybeTruncate -- the synthetic stores are now generated truncated, and the
+truncate_* / recovery_truncate cases hold stores read before truncation), which is itself pinned by the
 reference's known answers (PreAcceptTest, see kats.json) and ported model tests
 (tests/test_oracle.py). They freeze the oracle's answers so that (a) any later change to the
 oracle or the generators is caught, and (b) the GPU path is checked against committed data.
@@ -34,6 +36,12 @@ def deps_cases():
     yield "random_small_s3_no_elision", synth.random_small(1003), 0
     yield "random_small_s4_big", synth.random_small(1004, n_keys=60, n_hist_txns=1500, n_txns=300, max_keys=12,
                                                     n_range_cmds=80), 1
+    # stores read before truncation: every batch sees them truncated to the RedundantBefore
+    # (SafeCommandStore.maybeTruncate -> CommandsForKey.withRedundantBeforeAtLeast)
+    yield "truncate_snapshot", synth.random_small(1005, n_keys=40, n_hist_txns=400, n_txns=160, n_redundant=6,
+                                                  truncated=False), 1
+    yield "truncate_sequential", synth.sequential_ranges(1006, n_keys=40, n_hist_txns=400, n_txns=160, n_redundant=6,
+                                                         range_frac=0.2, truncated=False), 1
     yield "config1_n2000", synth.config1(n_txns=2000, n_keys=200), 1
     yield "config2_small", synth.config2(n_txns=2000, n_keys=3000, n_hist_entries=40_000, esp_frac=0.05), 1
     yield "config4_small", synth.config4(n_txns=1500, n_keys=3000, n_ranges=400, n_hist_txns=3000), 1
@@ -54,6 +62,7 @@ def deps_cases():
 
 def recovery_cases():
     """(file stem, workload): the four BeginRecovery scans of key- and Range-domain recovering txns."""
+    yield "recovery_truncate", synth.recovery_workload(1022, n_redundant=6, range_frac=0.3, truncated=False)
     yield "recovery_ranges_slices", synth.recovery_workload(1020, n_range_cmds=30, range_frac=0.5, n_txns=100,
                                                             with_slices=True)
     yield "recovery_ranges_start_inclusive", synth.recovery_workload(1021, n_range_cmds=30, range_frac=0.5,

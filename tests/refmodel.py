@@ -62,6 +62,31 @@ def cfk_active(entries, S, kinds, elide=True, pruned=None):
     return out
 
 
+def shard_redundant_before(w, k):
+    """The shardRedundantBefore of the RedundantBefore entry holding key k (RedundantBefore.get: epochs not read),
+    or None."""
+    rb, si = w.redundant, w.range_start_inclusive
+    for i in range(len(rb.range_start)):
+        if contains(si, int(rb.range_start[i]), int(rb.range_end[i]), k):
+            wm = (int(rb.wm.msb[i]), int(rb.wm.lsb[i]), int(rb.wm.node[i]))
+            return wm if key(wm) > key((0, 0, 0)) else None
+    return None
+
+
+def truncate(w, k, lo, hi):
+    """SafeCommandStore.maybeTruncate before key k's CommandsForKey is read (SafeCommandStore.java:165-171,
+    CommandsForKey.withRedundantBeforeAtLeast :1317-1341): (first entry index kept, shardRedundantBefore or None).
+    Entries below the key's shardRedundantBefore leave; prunedBefore at or below it becomes NO_INFO."""
+    wm = shard_redundant_before(w, k)
+    if wm is None:
+        return lo, None
+    c = w.cfk
+    e = lo
+    while e < hi and key((int(c.txn.msb[e]), int(c.txn.lsb[e]), int(c.txn.node[e]))) < key(wm):
+        e += 1
+    return e, wm
+
+
 def slices_of(w, qi):
     """The slice request qi's scan reads (SafeCommandStore.mapReduceActive's `slice`, SafeCommandStore.java:292):
     its slice set (Queries.slice_set into Workload.slice_sets: RangesForEpoch.allBetween results) or the store's
@@ -106,11 +131,15 @@ def request_pairs(w, qi, elide=True):
             continue
         i = kidx[k]
         s0, s1 = int(cfk.seg[i]), int(cfk.seg[i + 1])
-        ents = [((int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e])), int(cfk.status[e]),
-                 (int(cfk.exec.msb[e]), int(cfk.exec.lsb[e]), int(cfk.exec.node[e]))) for e in range(s0, s1)]
+        t0, wm = truncate(w, k, s0, s1)
         pruned = None
         if cfk.pruned_before is not None and cfk.pruned_before[i] >= 0:
-            pruned = ents[int(cfk.pruned_before[i])][0]
+            e = s0 + int(cfk.pruned_before[i])
+            pruned = (int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e]))
+            if wm is not None and key(wm) >= key(pruned):
+                pruned = None
+        ents = [((int(cfk.txn.msb[e]), int(cfk.txn.lsb[e]), int(cfk.txn.node[e])), int(cfk.status[e]),
+                 (int(cfk.exec.msb[e]), int(cfk.exec.lsb[e]), int(cfk.exec.node[e]))) for e in range(t0, s1)]
         for t in cfk_active(ents, ex, kinds, elide, pruned):
             if p1 is not None and eq(t, p1):
                 continue
@@ -273,13 +302,17 @@ def recovery_pairs(w, qi, scan):
         pos = np.searchsorted(c.keys, k)
         if pos >= len(c.keys) or c.keys[pos] != k:
             continue
-        ents = range(int(c.seg[pos]), int(c.seg[pos + 1]))
+        t0, wm = truncate(w, k, int(c.seg[pos]), int(c.seg[pos + 1]))
+        cut = t0 > int(c.seg[pos])
+        ents = range(t0, int(c.seg[pos + 1]))
         tid = lambda e: (int(c.txn.msb[e]), int(c.txn.lsb[e]), int(c.txn.node[e]))  # noqa: E731
         known = any(eq(tid(e), T) for e in ents)
         if with_dep and not known:
             pb = None
             if c.pruned_before is not None and c.pruned_before[pos] >= 0:
                 pb = tid(int(c.seg[pos]) + int(c.pruned_before[pos]))
+                if wm is not None and key(wm) >= key(pb):
+                    pb = None
             if pb is None or not key(T) < key(pb):
                 continue
         for e in ents:
@@ -297,6 +330,8 @@ def recovery_pairs(w, qi, scan):
             if c.miss_off is not None:
                 m0, m1 = int(c.miss_off[e]), int(c.miss_off[e + 1])
                 miss = [(int(c.miss.msb[j]), int(c.miss.lsb[j]), int(c.miss.node[j])) for j in range(m0, m1)]
+                if cut:                                      # Utils.removeRedundantMissing (Utils.java:265-275)
+                    miss = [m for m in miss if key(m) >= key(wm)]
             has_as_dep = known and not any(eq(m, T) for m in miss)
             if has_as_dep != with_dep:
                 continue
@@ -411,6 +446,9 @@ def sequential_augmented(w):
         for k in q.keys[int(q.key_off[qi]):int(q.key_off[qi + 1])]:
             k = int(k)
             if slices is not None and not any(contains(si, a, b, k) for a, b in slices):
+                continue
+            wm = shard_redundant_before(w, k)
+            if wm is not None and key(t) < key(wm):      # CommandsForKey.update ignores it (:997)
                 continue
             ents = by_key.setdefault(k, [])
             hit = [e for e in ents if eq(e[0], t)]

@@ -26,7 +26,7 @@ def test_header_and_library_exports():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(native.EXPORTS)
-    assert L.ad_abi_version() == 5
+    assert L.ad_abi_version() == 6
 
 
 def test_fails_loudly_without_gpu():
