@@ -246,9 +246,13 @@ int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipStream_t 
         return (uint32_t)(2 * (i + (uint64_t)(std::upper_bound(pos.begin(), pos.end(), i) - pos.begin())) + 1);
     };
     auto remap_txw = [&](uint32_t y) -> uint32_t { return (y & ~RANK_MASK) | remap(y & RANK_MASK); };
-    for (auto& r : c->h_txn_rank) r = remap(r);
-    for (auto& r : c->h_exec_rank) r = remap(r);
-    for (auto& r : c->h_pruned) r = remap(r);
+    // the per-entry copies are rebuilt from the device when they are stale anyway (host_moved)
+    if (!c->host_moved)
+    {
+        for (auto& r : c->h_txn_rank) r = remap(r);
+        for (auto& r : c->h_exec_rank) r = remap(r);
+        for (auto& r : c->h_pruned) r = remap(r);
+    }
     for (auto& r : c->h_cmd_rank) r = remap(r);
     for (auto& y : c->h_rtxw) y = remap_txw(y);
     ++c->rank_gen;
@@ -817,6 +821,14 @@ int ad_redundant_advance(ad_ctx* c, const ad_redundant_soa* in, ad_stats* stats)
                        c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
     CfkUpdOut o;
     std::string e;
+    // the host's per-entry copies are rebuilt from the device on demand (a merge remaps every rank, the
+    // truncation moves entries): no host remap of them here
+    if (!c->host_moved)
+    {
+        c->host_moved = true;
+        c->host_ingested = true;      // ranks change, entries do not: host missing() lists stay aligned
+    }
+    c->host_stale = true;
     const int rc = run_cfk_dict_ensure(c->cu, c->ds, d, c->d_adv_m.as<uint64_t>(), c->d_adv_l.as<uint64_t>(),
                                        c->d_adv_n.as<int32_t>(), nx, grow, c->stream, &o, c->d_adv_rank.as<uint32_t>(), &e);
     if (const int frc = cfk_update_follow(c, o, rc, c->stream))

@@ -75,11 +75,29 @@ def ballot_transitions(cfk, rng, n, statuses=(2, 3, 4, 5, 6)):
     return u, e
 
 
-def older_inserts(cfk, rng, n, known_frac=0.3, new_exec_frac=0.3, statuses=range(8)):
+def below_redundant(keys, t, w):
+    """Rows whose txnId is below its key's shardRedundantBefore in workload w's RedundantBefore: the updates
+    CommandsForKey.update ignores (CommandsForKey.java:997), which ad_cfk_update leaves to its caller."""
+    red, si = w.redundant, bool(w.range_start_inclusive)
+    out = np.zeros(len(keys), bool)
+    for j in range(len(red.range_start)):
+        a, b = int(red.range_start[j]), int(red.range_end[j])
+        wm = (int(red.wm.msb[j]), int(red.wm.lsb[j]), int(red.wm.node[j]))
+        if wm == (0, 0, 0):
+            continue
+        inr = ((keys >= a) & (keys < b)) if si else ((keys > a) & (keys <= b))
+        for i in np.nonzero(inr)[0]:
+            x = (int(t.msb[i]), int(t.lsb[i]), int(t.node[i]))
+            out[i] = (x[0], x[1] >> 16, x[1] & 0x1E, x[2]) < (wm[0], wm[1] >> 16, wm[1] & 0x1E, wm[2])
+    return out
+
+
+def older_inserts(cfk, rng, n, known_frac=0.3, new_exec_frac=0.3, statuses=range(8), w=None):
     """Insertions below the newest id of the store: txnIds next to existing ones (same msb and
     flags, another node: ids the dictionary does not hold, landing mid-segment), and for
     `known_frac` of them ids the store holds under another key. executeAt = txnId or, for
-    `new_exec_frac`, an unknown Timestamp next to an existing one."""
+    `new_exec_frac`, an unknown Timestamp next to an existing one. With w, the rows below their key's
+    shardRedundantBefore are left out, as a caller of ad_cfk_update does (below_redundant)."""
     ne = cfk.n_entries
     e = rng.integers(0, ne, n)
     ek = entry_keys(cfk)
@@ -96,7 +114,11 @@ def older_inserts(cfk, rng, n, known_frac=0.3, new_exec_frac=0.3, statuses=range
     use_x = (rng.random(n) < new_exec_frac) & ~rd
     x = Tids(np.where(use_x, cfk.exec.msb[f], t.msb), np.where(use_x, cfk.exec.lsb[f], t.lsb),
              np.where(use_x, cfk.exec.node[f].astype(np.int64) + 3000 + np.arange(n), t.node).astype(np.int32))
-    return CfkUpdates(keys.astype(np.int64), t, x, st)
+    u = CfkUpdates(keys.astype(np.int64), t, x, st)
+    if w is not None:
+        keep = np.nonzero(~below_redundant(u.keys, u.txn, w))[0]
+        u = CfkUpdates(u.keys[keep], u.txn.take(keep), u.exec.take(keep), u.status[keep])
+    return u
 
 
 def unused_keys(cfk, rng, n, lo=-500, hi=500):

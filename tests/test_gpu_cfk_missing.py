@@ -165,7 +165,7 @@ def test_missing_and_additions(oracle, seed):
             parts = [G.transitions(cfk, rng, 40)[0], G.fresh_preaccepts(cfk, rng, 10, statuses=(2, 3), epoch=9 + rnd,
                                                                          hlc0=1 + 1000 * rnd)]
             if rnd == 1:
-                parts.append(G.older_inserts(cfk, rng, 10))
+                parts.append(G.older_inserts(cfk, rng, 10, w=w))
             u = with_deps(cfk, G.concat(*parts), rng)
             exp, applied, nadd = U.cfk_update_missing(cfk, u, u.dep_off, u.deps)
             if U.dup_committed_exec(exp):

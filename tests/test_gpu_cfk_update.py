@@ -21,6 +21,20 @@ import cfk_update_gen as G  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
+def _java_would_throw(w, new_cfk, oracle):
+    """Random transitions can leave a state the reference rejects when read (the prunedBefore walk running past
+    committedByExecuteAt, CommandsForKey.java:952-965): such a batch is not applied."""
+    old = w.cfk
+    w.cfk = new_cfk
+    try:
+        oracle.resolve(w)
+        return False
+    except oracle.OracleError as e:
+        return e.code == A.AD_E_STATE
+    finally:
+        w.cfk = old
+
+
 def _check(w, st, oracle, new_cfk):
     s, x = st.cfk_entries()
     assert s.tolist() == new_cfk.status.tolist()
@@ -240,7 +254,7 @@ def test_insert_older_ids(oracle, seed, path):
         st.load(w)
         cfk = w.cfk
         for rnd in range(3):
-            old = G.older_inserts(cfk, rng, 20 + 10 * rnd)
+            old = G.older_inserts(cfk, rng, 20 + 10 * rnd, w=w)
             tr, _ = G.transitions(cfk, rng, 30)
             fresh = G.fresh_preaccepts(cfk, rng, 5, epoch=9 + rnd)
             u = G.concat(old, tr, fresh, old) if rnd == 1 else G.concat(tr, old, fresh)
@@ -285,7 +299,7 @@ def test_insert_older_then_sequential(oracle):
         st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
         try:
             st.load(w)
-            u = G.older_inserts(w.cfk, rng, 40, statuses=(0, 2, 3))
+            u = G.older_inserts(w.cfk, rng, 40, statuses=(0, 2, 3), w=w)
             new, _ = U.cfk_update(w.cfk, u)
             st.cfk_update(u)
             _check(w, st, oracle, new)
@@ -398,7 +412,7 @@ def test_recovery_after_older_inserts(oracle, seed):
     import ctypes as C
     w = synth.recovery_workload(5 + seed)
     rng = np.random.default_rng(5 + seed)
-    u = G.older_inserts(w.cfk, rng, 40, statuses=(0, 2, 3, 4, 5, 6))
+    u = G.older_inserts(w.cfk, rng, 40, statuses=(0, 2, 3, 4, 5, 6), w=w)
     new, _ = U.cfk_update(w.cfk, u)
     if U.dup_committed_exec(new):
         pytest.skip("generated batch breaks CommandsForKey.java:1439")
@@ -457,13 +471,13 @@ def test_ballot_replacement(oracle, seed, path):
                 ins.ballot = G.ballots(rng, len(ins))
                 u = G.concat(bt, ins, ins)
             elif rnd == 2:
-                old = G.older_inserts(cfk, rng, 20)
+                old = G.older_inserts(cfk, rng, 20, w=w)
                 old.ballot = G.ballots(rng, len(old))
                 u = G.concat(old, bt, old)
             else:
                 u, _ = G.transitions(cfk, rng, 40)            # Ballot.ZERO: replacements drop ballots
             new, _ = U.cfk_update(cfk, u)
-            if U.dup_committed_exec(new):
+            if U.dup_committed_exec(new) or _java_would_throw(w, new, oracle):
                 continue
             if new.ballot is None:
                 new.ballot = Tids(np.zeros(new.n_entries, np.uint64), np.zeros(new.n_entries, np.uint64),

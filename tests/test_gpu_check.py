@@ -151,7 +151,7 @@ def test_snapshot_after_device_updates():
         st.load(w)
         rng = np.random.default_rng(3)
         u = G.concat(G.transitions(w.cfk, rng, 5000)[0], G.fresh_preaccepts(w.cfk, rng, 500),
-                     G.older_inserts(w.cfk, rng, 500))
+                     G.older_inserts(w.cfk, rng, 500, w=w))
         st.cfk_update(u)
         assert st.check_snapshot() == (0, None)
         qdev, keep = native.device_queries(w.queries, torch.device("cuda", 0))

@@ -87,7 +87,7 @@ def test_device_ingest_then_updates(oracle, seed, monkeypatch):
     st = _store(w, False, monkeypatch)
     try:
         u1, _ = G.transitions(w.cfk, rng, 80)
-        u2 = G.older_inserts(w.cfk, rng, 40)
+        u2 = G.older_inserts(w.cfk, rng, 40, w=w)
         u = G.concat(u1, u2)
         new, _ = U.cfk_update(w.cfk, u)
         st.cfk_update(u)

@@ -117,7 +117,7 @@ def test_device_view_equals_host_view(oracle, monkeypatch):
     w.cfk.miss_off, w.cfk.miss = None, None
     rng = np.random.default_rng(44)
     import cfk_update_gen as G
-    u = G.concat(G.transitions(w.cfk, rng, 60)[0], G.older_inserts(w.cfk, rng, 20))
+    u = G.concat(G.transitions(w.cfk, rng, 60)[0], G.older_inserts(w.cfk, rng, 20, w=w))
     exp, _ = U.cfk_update(w.cfk, u)
     if U.dup_committed_exec(exp):
         pytest.skip("duplicate committed executeAt")
