@@ -30,7 +30,7 @@ EXPORTS = ("ad_abi_version", "ad_ctx_create", "ad_ctx_destroy", "ad_last_error",
            "ad_check_result_device", "ad_check_snapshot", "ad_cfk_prune", "ad_cfk_byid", "ad_cfk_missing",
            "ad_cfk_load_pruned", "ad_host_register", "ad_host_unregister", "ad_deps_batch_into",
            "ad_debug_guard_check", "ad_host_alloc", "ad_host_free", "ad_cfk_update_status",
-           "ad_slice_sets_load", "ad_redundant_advance")
+           "ad_slice_sets_load", "ad_redundant_advance", "ad_range_cmds_update")
 
 
 class AccordDepsError(RuntimeError):
@@ -113,6 +113,7 @@ def lib():
         L.ad_check_result_device.argtypes = [C.c_void_p, C.POINTER(A.AdDepsResult), C.c_void_p, C.POINTER(C.c_uint64),
                                              C.POINTER(C.c_uint64)]
         L.ad_redundant_advance.argtypes = [C.c_void_p, C.POINTER(A.AdRedundantSoa), C.POINTER(A.AdStats)]
+        L.ad_range_cmds_update.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsSoa), C.POINTER(A.AdStats)]
         L.ad_cfk_prune.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_int64, C.POINTER(C.c_uint64),
                                    C.POINTER(A.AdStats)]
         L.ad_cfk_byid.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
@@ -292,6 +293,13 @@ class DeviceCommandStore:
         n, st = C.c_uint64(), A.AdStats()
         self._check(lib().ad_cfk_update_device(self.h, C.byref(udev), stream, C.byref(n), C.byref(st)))
         return n.value, stats_dict(st)
+
+    def range_cmds_update(self, cmds):
+        """ad_range_cmds_update: registry upkeep rows (a RangeCommands: historical / erased / update per row);
+        the range part of the snapshot follows without a rebuild. Returns stats."""
+        st = A.AdStats()
+        self._check(lib().ad_range_cmds_update(self.h, C.byref(cmds.soa()), C.byref(st)))
+        return stats_dict(st)
 
     def redundant_advance(self, redundant):
         """ad_redundant_advance: the loaded RedundantBefore's entries with epochs / watermarks moved forward; the

@@ -993,6 +993,72 @@ def advance_redundant(red, seed, step_frac=0.15, hist_hlc=None, frac=0.7):
     return Redundant(red.range_start, red.range_end, red.start_epoch, red.end_epoch, wm)
 
 
+def range_cmd_updates(cmds, seed, n, lo=-520, hi=520, epoch=1, hlc_hi=500, frac=(0.35, 0.25, 0.15, 0.25), max_width=120):
+    """Registry upkeep rows for ad_range_cmds_update (a RangeCommands whose flags say what each row is): shares
+    `frac` of (a) updates of registered live commands with more ranges (overlapping, touching or apart), (b) new
+    registrations (fresh Range-domain txnIds), (c) erasures of live commands, (d) historical merges (of historical
+    commands, of live ones -- ignored -- and new ones). Ranges normalised, within [lo, hi)."""
+    rng = np.random.default_rng(seed)
+    live = [i for i in range(len(cmds.txn.msb)) if cmds.historical is None or not cmds.historical[i]]
+    hist = [i for i in range(len(cmds.txn.msb)) if cmds.historical is not None and cmds.historical[i]]
+    kinds = rng.choice(4, n, p=np.asarray(frac) / np.sum(frac))
+    fresh = make_txn_ids(epoch, np.sort(rng.choice(np.arange(1, hlc_hi), n, replace=False)).astype(np.uint64) * 10 + 7,
+                         rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_SYNC_POINT, A.KIND_EXCLUSIVE_SYNC_POINT], n),
+                         rng.integers(1, 17, n), domain=1)
+    rows_t, er, hi_f, off, st, en = [], [], [], [0], [], []
+    made = []
+    for i in range(n):
+        k = int(kinds[i])
+        if k == 0 and live:
+            j = int(rng.choice(live))
+            t = (cmds.txn.msb[j], cmds.txn.lsb[j], cmds.txn.node[j])
+            base = [(int(cmds.range_start[x]), int(cmds.range_end[x])) for x in range(int(cmds.range_off[j]), int(cmds.range_off[j + 1]))]
+        elif k == 3 and (hist or live) and rng.random() < 0.7:
+            pool = hist if (hist and rng.random() < 0.7) else (live or hist)
+            j = int(rng.choice(pool))
+            t = (cmds.txn.msb[j], cmds.txn.lsb[j], cmds.txn.node[j])
+            base = [(int(cmds.range_start[x]), int(cmds.range_end[x])) for x in range(int(cmds.range_off[j]), int(cmds.range_off[j + 1]))]
+        elif k == 2 and live:
+            j = int(rng.choice(live))
+            t = (cmds.txn.msb[j], cmds.txn.lsb[j], cmds.txn.node[j])
+            base = []
+        elif made and rng.random() < 0.3:
+            t, base = made[int(rng.integers(0, len(made)))]        # a command this batch registered, again
+        else:
+            t = (fresh.msb[i], fresh.lsb[i], fresh.node[i])
+            base = []
+            made.append((t, base))
+        rs = []
+        if k != 2:
+            nr = int(rng.integers(1, 4))
+            pts = []
+            for _ in range(nr):
+                if base and rng.random() < 0.6:                       # near an existing range: overlap / touch / apart
+                    a, b = base[int(rng.integers(0, len(base)))]
+                    d = int(rng.integers(-3, 4))
+                    x = b + d if rng.random() < 0.5 else a - int(rng.integers(1, max(2, max_width // 4))) + d
+                    pts.append((x, x + int(rng.integers(1, max(2, max_width // 3)))))
+                else:
+                    x = int(rng.integers(lo, hi - 1))
+                    pts.append((x, min(hi, x + int(rng.integers(1, max_width)))))
+            pts.sort()
+            for a, b in pts:                                          # normalise (merge overlapping)
+                if rs and a < rs[-1][1]:
+                    rs[-1] = (rs[-1][0], max(rs[-1][1], b))
+                elif a < b:
+                    rs.append((a, b))
+        rows_t.append(t)
+        er.append(1 if k == 2 else 0)
+        hi_f.append(1 if k == 3 else 0)
+        st += [a for a, _ in rs]
+        en += [b for _, b in rs]
+        off.append(len(st))
+    ids = Tids(np.array([x[0] for x in rows_t], np.uint64), np.array([x[1] for x in rows_t], np.uint64),
+               np.array([x[2] for x in rows_t], np.int32))
+    return RangeCommands(ids, np.array(off, np.uint64), np.array(st, np.int64), np.array(en, np.int64),
+                         erased=np.array(er, np.uint8), historical=np.array(hi_f, np.uint8))
+
+
 def sequential_ranges(seed, range_frac=0.4, **kw):
     """A SEQUENTIAL PreAccept batch (config 1's semantics) mixing key-domain and Range-domain txns (sync
     points, range reads/writes) over a random_small store with range commands and RedundantBefore: the

@@ -332,6 +332,46 @@ int build_ranges(ad_ctx* c, const std::vector<uint32_t>& cmd_rank, const std::ve
     return 0;
 }
 
+// The range part's views (range entries, stabbing cells, range trees' levels, RedundantBefore)
+int set_range_views(ad_ctx* c, const RangePart& rp, uint64_t nrb)
+{
+    DevSnapshot& s = c->ds;
+    const bool cell_ok = rp.cell_ok;
+    s.n_rent = rp.n_rent;
+    s.n_cell_E = cell_ok ? rp.cell_E.size() : 0;
+    s.cell_E = cell_ok ? c->d_cell_E.as<int64_t>() : nullptr;
+    s.cell_off = cell_ok ? c->d_cell_off.as<uint32_t>() : nullptr;
+    s.cell_ent = cell_ok ? c->d_cell_ent.as<uint64_t>() : nullptr;
+    if (!cell_ok) c->n_cell_ent = 0;
+    s.r_start = c->d_rstart.as<int64_t>();
+    s.r_end = c->d_rend.as<int64_t>();
+    s.r_txw = c->d_rtxw.as<uint32_t>();
+    s.r_rid = c->d_rrid.as<uint32_t>();
+    s.rlvl_n[0] = s.n_rent;
+    int L = 1;
+    while (s.rlvl_n[L - 1] > 64 && L < MAX_LEVELS)
+    {
+        s.rlvl_n[L] = (s.rlvl_n[L - 1] + 63) / 64;
+        ++L;
+    }
+    s.n_rlevels = L;
+    for (int l = 1; l < L; ++l)
+        for (int cl = 0; cl < NCLASS; ++cl)
+        {
+            if (!c->d_rlvl[cl][l].ensure(sizeof(int64_t) * ((s.rlvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "range tree level");
+            s.rlvl[cl][l] = c->d_rlvl[cl][l].as<int64_t>();
+        }
+    s.n_rb = nrb;
+    s.rb_start = c->d_rb_s.as<int64_t>();
+    s.rb_end = c->d_rb_e.as<int64_t>();
+    s.rb_e0 = c->d_rb_e0.as<int64_t>();
+    s.rb_e1 = c->d_rb_e1.as<int64_t>();
+    s.rb_wm = c->d_rb_wm.as<uint32_t>();
+    s.rb_rid = c->d_rb_rid.as<uint32_t>();
+    s.rng32 = getenv("AD_RNG64") == nullptr && c->rt_start.size() < (1ull << 26) && 2 * s.n_dict + 2 < (1ull << 26);
+    return 0;
+}
+
 // The DevSnapshot views over the ctx's device buffers of a built snapshot (both build routes)
 int set_views(ad_ctx* c, uint64_t n_dict, uint64_t n_samp, const NormTid& last, uint64_t nk, uint64_t ne, uint64_t hcap,
                      const RangePart& rp, uint64_t nrb)
@@ -378,38 +418,7 @@ int set_views(ad_ctx* c, uint64_t n_dict, uint64_t n_samp, const NormTid& last, 
             if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * ((s.lvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "tree level");
             s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
         }
-    const bool cell_ok = rp.cell_ok;
-    s.n_rent = rp.n_rent;
-    s.n_cell_E = cell_ok ? rp.cell_E.size() : 0;
-    s.cell_E = cell_ok ? c->d_cell_E.as<int64_t>() : nullptr;
-    s.cell_off = cell_ok ? c->d_cell_off.as<uint32_t>() : nullptr;
-    s.cell_ent = cell_ok ? c->d_cell_ent.as<uint64_t>() : nullptr;
-    if (!cell_ok) c->n_cell_ent = 0;
-    s.r_start = c->d_rstart.as<int64_t>();
-    s.r_end = c->d_rend.as<int64_t>();
-    s.r_txw = c->d_rtxw.as<uint32_t>();
-    s.r_rid = c->d_rrid.as<uint32_t>();
-    s.rlvl_n[0] = s.n_rent;
-    L = 1;
-    while (s.rlvl_n[L - 1] > 64 && L < MAX_LEVELS)
-    {
-        s.rlvl_n[L] = (s.rlvl_n[L - 1] + 63) / 64;
-        ++L;
-    }
-    s.n_rlevels = L;
-    for (int l = 1; l < L; ++l)
-        for (int cl = 0; cl < NCLASS; ++cl)
-        {
-            if (!c->d_rlvl[cl][l].ensure(sizeof(int64_t) * ((s.rlvl_n[l] + 63) / 64 * 64))) return c->fail(AD_E_NOMEM, "range tree level");
-            s.rlvl[cl][l] = c->d_rlvl[cl][l].as<int64_t>();
-        }
-    s.n_rb = nrb;
-    s.rb_start = c->d_rb_s.as<int64_t>();
-    s.rb_end = c->d_rb_e.as<int64_t>();
-    s.rb_e0 = c->d_rb_e0.as<int64_t>();
-    s.rb_e1 = c->d_rb_e1.as<int64_t>();
-    s.rb_wm = c->d_rb_wm.as<uint32_t>();
-    s.rb_rid = c->d_rb_rid.as<uint32_t>();
+    if (int rc = set_range_views(c, rp, nrb)) return rc;
     s.n_slices = c->slice_s.size();
     s.slice_start = c->d_slices_s.as<int64_t>();
     s.slice_end = c->d_slices_e.as<int64_t>();
@@ -2207,6 +2216,132 @@ int check_query_host(ad_ctx* c, const ad_query_soa* q, uint32_t flags)
 // C ABI
 // =======================================================================================
 
+// ---- range-command registry upkeep (ad_range_cmds_update) ------------------------------------
+using RangeList = std::vector<std::pair<int64_t, int64_t>>;
+
+// Range.compareIntersecting (Range.java:296-305)
+static int cmp_intersecting(const std::pair<int64_t, int64_t>& x, const std::pair<int64_t, int64_t>& y)
+{
+    if (x.first >= y.second) return 1;
+    if (x.second <= y.first) return -1;
+    return 0;
+}
+
+// Ranges.with (Ranges.java:136-139): AbstractRanges.union(MERGE_OVERLAPPING) (:486-574) after
+// supersetLinearMerge (:429-474) -- a run that merged an intersection also takes touching ranges
+RangeList ranges_with(const RangeList& left, const RangeList& right)
+{
+    if (right.empty()) return left;
+    if (left.empty()) return right;
+    const RangeList* A = &left;
+    const RangeList* B = &right;
+    if ((*A)[0].first > (*B)[0].first || ((*A)[0].first == (*B)[0].first && A->back().second < B->back().second)) std::swap(A, B);
+    const RangeList& as = *A;
+    const RangeList& bs = *B;
+    size_t ai = 0, bi = 0;
+    while (ai < as.size() && bi < bs.size())
+    {
+        auto a = as[ai];
+        const auto b = bs[bi];
+        const int c = cmp_intersecting(a, b);
+        if (c < 0) ++ai;
+        else if (c > 0 || b.first < a.first) break;
+        else if (b.second <= a.second)
+        {
+            ++bi;
+            if (b.second == a.second) ++ai;
+        }
+        else
+        {
+            size_t t = ai;
+            bool out = false;
+            do
+            {
+                if (++t == as.size() || a.second != as[t].first) { out = true; break; }
+                a = as[t];
+            } while (a.second < b.second);
+            if (out) break;
+            ++bi;
+            ai = t;
+        }
+    }
+    if (bi == bs.size()) return as;
+    RangeList r(as.begin(), as.begin() + ai);
+    while (ai < as.size() && bi < bs.size())
+    {
+        auto a = as[ai];
+        const auto b = bs[bi];
+        const int c = cmp_intersecting(a, b);
+        if (c < 0) { r.push_back(a); ++ai; }
+        else if (c > 0) { r.push_back(b); ++bi; }
+        else
+        {
+            const int64_t start = std::min(a.first, b.first);
+            int64_t end = std::max(a.second, b.second);
+            ++ai;
+            ++bi;
+            while (ai < as.size() || bi < bs.size())
+            {
+                std::pair<int64_t, int64_t> mn;
+                bool from_a;
+                if (ai == as.size()) { mn = bs[bi]; from_a = false; }
+                else if (bi == bs.size() || as[ai].first < bs[bi].first) { mn = a = as[ai]; from_a = true; }
+                else { mn = bs[bi]; from_a = false; }
+                if (mn.first > end) break;
+                if (mn.second > end) end = mn.second;
+                if (from_a) ++ai;
+                else ++bi;
+            }
+            r.push_back({start, end});
+        }
+    }
+    r.insert(r.end(), as.begin() + ai, as.end());
+    r.insert(r.end(), bs.begin() + bi, bs.end());
+    return r;
+}
+
+// The range part of a built snapshot rebuilt from the host registry (range entries, range table, stabbing cells,
+// per-key cells in the key hash and KeyLines, range trees, RedundantBefore views) -- the CommandsForKeys, their
+// derived arrays and the dictionary stay; commands [n_old, n) are new: their txnIds join the dictionary first.
+int refresh_range_part(ad_ctx* c, uint64_t n_old, uint64_t* n_new_ids)
+{
+    const auto& R = c->cmds;
+    const uint64_t ncmd = R.txn.size(), nrb = c->rb.wm.size(), nk = c->ds.n_keys;
+    hipStream_t st = c->stream;
+    *n_new_ids = 0;
+    if (c->h_cmd_rank.size() != n_old) return c->fail(AD_E_STATE, "range command ranks out of step (internal)");
+    if (ncmd > n_old)
+    {
+        std::vector<Tid> ids(R.txn.begin() + n_old, R.txn.end());
+        std::vector<uint32_t> ranks;
+        if (int rc = dict_ensure_ids(c, ids, &ranks, n_new_ids)) return rc;
+        c->h_cmd_rank.insert(c->h_cmd_rank.end(), ranks.begin(), ranks.end());
+    }
+    std::vector<uint32_t> wm_rank(nrb, 0);
+    if (nrb)
+    {
+        HIPCHK(c, d2h(wm_rank.data(), c->d_rb_wm.p, 4 * nrb, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+    }
+    RangePart rp;
+    if (int rc = build_ranges(c, c->h_cmd_rank, wm_rank, &rp)) return rc;
+    if (int rc = set_range_views(c, rp, nrb)) return rc;
+    if (int rc = upload(c, c->d_rt_start, c->rt_start)) return rc;
+    if (int rc = upload(c, c->d_rt_end, c->rt_end)) return rc;
+    // every key's stabbing cell (KeySlot and the per-key array the KeyLines read) under the new endpoints
+    if (nk)
+        HIPCHK(c, ingest_keys(c->d_keys.as<int64_t>(), nk, rp.cell_ok ? c->d_cell_E.as<int64_t>() : nullptr,
+                              rp.cell_ok ? rp.cell_E.size() : 0, c->cfg.range_start_inclusive, c->d_kcell.as<uint32_t>(),
+                              c->d_khash.as<KeySlot>(), c->ds.khash_mask + 1, st));
+    HIPCHK(c, build_range_trees(c->ds, st));
+    if (c->kline_slots)
+        HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
+                                   c->kline_slots, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->rv_rng_gen = ~0ull;
+    return 0;
+}
+
 }  // namespace adi
 
 extern "C" {
@@ -2403,6 +2538,120 @@ int ad_range_cmds_load(ad_ctx* c, const ad_range_cmds_soa* in)
     c->rv_rng_gen = ~0ull;
     drop_global_dict(c);         // a new snapshot: the node-wide dictionary must be installed again
     c->dirty = true;
+    return AD_OK;
+}
+
+int ad_range_cmds_update(ad_ctx* c, const ad_range_cmds_soa* in, ad_stats* stats)
+{
+    if (!c || !in) return AD_E_INVAL;
+    const uint64_t n = in->n_cmds;
+    if (n && (!in->txn_msb || !in->txn_lsb || !in->txn_node || !in->range_off || (in->range_off[n] && (!in->range_start || !in->range_end))))
+        return c->fail(AD_E_INVAL, "ad_range_cmds_update: null arrays");
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        if ((in->txn_lsb[i] & 1) == 0) return c->fail(AD_E_INVAL, "range command %llu has a key-domain TxnId", (unsigned long long)i);
+        if (in->range_off[i + 1] < in->range_off[i]) return c->fail(AD_E_INVAL, "range_off not monotone");
+        for (uint64_t r = in->range_off[i]; r < in->range_off[i + 1]; ++r)
+            if (in->range_start[r] >= in->range_end[r] || (r > in->range_off[i] && in->range_start[r] < in->range_end[r - 1]))
+                return c->fail(AD_E_INVAL, "range command %llu: ranges not normalised", (unsigned long long)i);
+    }
+    if (stats) *stats = ad_stats{};
+    const double t0 = now_ms();
+    auto& R = c->cmds;
+    const uint64_t n_old = R.txn.size();
+    // the registry as per-command range lists (only the touched ones materialised), live / historical by TxnId
+    auto cmp = [](const NormTid& a, const NormTid& b) { return norm_cmp(a, b) < 0; };
+    std::map<NormTid, uint64_t, decltype(cmp)> live(cmp), hist(cmp);
+    for (uint64_t i = 0; i < n_old; ++i)
+        ((!R.historical.empty() && R.historical[i]) ? hist : live)[norm(R.txn[i])] = i;
+    std::map<uint64_t, RangeList> touched;
+    auto ranges_of = [&](uint64_t i) -> RangeList& {
+        auto it = touched.find(i);
+        if (it != touched.end()) return it->second;
+        RangeList& l = touched[i];
+        if (i < n_old)
+            for (uint64_t r = R.off[i]; r < R.off[i + 1]; ++r) l.push_back({R.start[r], R.end[r]});
+        return l;
+    };
+    if (R.erased.empty()) R.erased.assign(n_old, 0);
+    if (R.historical.empty()) R.historical.assign(n_old, 0);
+    auto add_cmd = [&](const Tid& t, uint8_t historical) -> uint64_t {
+        const uint64_t i = R.txn.size();
+        R.txn.push_back(t);
+        R.erased.push_back(0);
+        R.historical.push_back(historical);
+        touched[i];
+        (historical ? hist : live)[norm(t)] = i;
+        return i;
+    };
+    for (uint64_t i = 0; i < n; ++i)
+    {
+        const Tid t{in->txn_msb[i], in->txn_lsb[i], in->txn_node[i]};
+        const NormTid k = norm(t);
+        RangeList add;
+        for (uint64_t r = in->range_off[i]; r < in->range_off[i + 1]; ++r) add.push_back({in->range_start[r], in->range_end[r]});
+        if (in->historical && in->historical[i])
+        {
+            // registerHistoricalTransactions: nothing when rangeCommands holds it (InMemoryCommandStore.java:814-828)
+            if (live.count(k)) continue;
+            auto it = hist.find(k);
+            const uint64_t j = it != hist.end() ? it->second : add_cmd(t, 1);
+            RangeList& l = ranges_of(j);
+            l = ranges_with(l, add);
+        }
+        else if (in->erased && in->erased[i])
+        {
+            auto it = live.find(k);          // the command's status became Erased: the scan skips it (:892)
+            if (it != live.end()) R.erased[it->second] = 1;
+        }
+        else
+        {
+            // InMemorySafeStore.update (:740-763): computeIfAbsent(txnId).update(ranges) (RangeCommand.update :547-551)
+            auto it = live.find(k);
+            const uint64_t j = it != live.end() ? it->second : add_cmd(t, 0);
+            RangeList& l = ranges_of(j);
+            l = ranges_with(l, add);
+        }
+    }
+    // the registry's CSR again
+    const uint64_t ncmd = R.txn.size();
+    std::vector<uint64_t> off(ncmd + 1, 0);
+    std::vector<int64_t> st, en;
+    st.reserve(R.start.size() + 16);
+    en.reserve(R.end.size() + 16);
+    for (uint64_t i = 0; i < ncmd; ++i)
+    {
+        auto it = touched.find(i);
+        if (it != touched.end())
+            for (auto& p : it->second) { st.push_back(p.first); en.push_back(p.second); }
+        else
+            for (uint64_t r = R.off[i]; r < R.off[i + 1]; ++r) { st.push_back(R.start[r]); en.push_back(R.end[r]); }
+        off[i + 1] = st.size();
+    }
+    R.off.swap(off);
+    R.start.swap(st);
+    R.end.swap(en);
+    R.rec = false;                   // recovery facts belong to the registry as it was (reload them)
+    c->rv_rng_gen = ~0ull;
+    const double ms_host = now_ms() - t0;
+    if (!c->cfk.loaded || c->dirty) return AD_OK;     // the next build reads the registry
+    if (hipSetDevice(c->device) != hipSuccess) return c->fail(AD_E_DEVICE, "hipSetDevice");
+    StreamScope scope_(c->stream, c->cstream);
+    uint64_t n_new = 0;
+    const double t1 = now_ms();
+    if (int rc = refresh_range_part(c, n_old, &n_new))
+    {
+        c->dirty = true;
+        return rc;
+    }
+    if (stats)
+    {
+        stats->ms_stage[0] = ms_host;                 // registry upkeep on the host copy
+        stats->ms_stage[1] = now_ms() - t1;           // range part rebuilt (dictionary growth included)
+        stats->n_keys[0] = ncmd - n_old;              // commands registered
+        stats->n_keys[1] = c->ds.n_rent;              // range entries
+        stats->n_keys[2] = n_new;                     // ids added to the dictionary
+    }
     return AD_OK;
 }
 

@@ -23,6 +23,7 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <map>
 #include <vector>
 
 #include "../../include/accord_deps.h"
@@ -452,5 +453,9 @@ int cfk_keys_swap(void* vc, KeyBufs* b);
 int cfk_miss_spare(void* vc, uint64_t n, uint64_t n_ids, uint64_t** off, uint32_t** ids);
 int cfk_miss_swap(void* vc, uint64_t** off, uint32_t** ids);
 int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats);
+int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st);
+// ids (host) joined to the device dictionary where it does not hold them; ranks[i] their member ranks (host
+// copies follow as after an update batch). ms: host-timed.
+int dict_ensure_ids(ad_ctx* c, const std::vector<Tid>& ids, std::vector<uint32_t>* ranks, uint64_t* n_new);
 
 }  // namespace adi

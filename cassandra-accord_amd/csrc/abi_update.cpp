@@ -492,6 +492,63 @@ int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st)
     return 0;
 }
 
+int dict_ensure_ids(ad_ctx* c, const std::vector<Tid>& ids, std::vector<uint32_t>* ranks, uint64_t* n_new)
+{
+    const uint64_t nx = ids.size();
+    ranks->assign(nx, 0);
+    *n_new = 0;
+    if (!nx) return 0;
+    std::vector<uint64_t> xm(nx), xl(nx);
+    std::vector<int32_t> xn(nx);
+    for (uint64_t j = 0; j < nx; ++j)
+    {
+        xm[j] = ids[j].msb;
+        xl[j] = ids[j].lsb;
+        xn[j] = ids[j].node;
+    }
+    if (int rc = upload(c, c->d_adv_m, xm)) return rc;
+    if (int rc = upload(c, c->d_adv_l, xl)) return rc;
+    if (int rc = upload(c, c->d_adv_n, xn)) return rc;
+    if (!c->d_adv_rank.ensure(4 * nx)) return c->fail(AD_E_NOMEM, "id ranks");
+    if (int rc = host_dict(c)) return rc;
+    if (!c->cu) c->cu = cfk_upd_work_create();
+    CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
+                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
+                  c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr,
+                  c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
+    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
+                       c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
+                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
+                       c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
+                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
+    // the host's per-entry copies are rebuilt from the device on demand after a merge (it remaps every rank): no
+    // host remap of them here
+    if (!c->host_moved)
+    {
+        c->host_moved = true;
+        c->host_ingested = true;      // ranks change, entries do not: host missing() lists stay aligned
+    }
+    c->host_stale = true;
+    CfkUpdOut o;
+    std::string e;
+    const int rc = run_cfk_dict_ensure(c->cu, c->ds, d, c->d_adv_m.as<uint64_t>(), c->d_adv_l.as<uint64_t>(),
+                                       c->d_adv_n.as<int32_t>(), nx, grow, c->stream, &o, c->d_adv_rank.as<uint32_t>(), &e);
+    if (const int frc = cfk_update_follow(c, o, rc, c->stream))
+    {
+        c->dirty = true;
+        return frc;
+    }
+    if (rc)
+    {
+        c->dirty = true;        // rebuilt from the host copies at the next use
+        return c->fail(rc, "id dictionary growth: %s", e.c_str());
+    }
+    HIPCHK(c, d2h(ranks->data(), c->d_adv_rank.p, 4 * nx, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *n_new = o.n_new_ids;
+    return 0;
+}
+
 int check_update_soa(ad_ctx* c, const ad_cfk_update_soa* u)
 {
     // the status describes this call from here on, whatever rejects it below (ad_cfk_update_status)
@@ -796,56 +853,13 @@ int ad_redundant_advance(ad_ctx* c, const ad_redundant_soa* in, ad_stats* stats)
     // the new watermarks join the id dictionary (appended or merged with the rank remap of an update
     // batch), their member ranks replace the moved entries' in rb_wm
     const uint64_t nx = moved.size();
-    std::vector<uint64_t> xm(nx), xl(nx);
-    std::vector<int32_t> xn(nx);
-    for (uint64_t j = 0; j < nx; ++j)
-    {
-        xm[j] = B.wm[moved[j]].msb;
-        xl[j] = B.wm[moved[j]].lsb;
-        xn[j] = B.wm[moved[j]].node;
-    }
-    if (int rc = upload(c, c->d_adv_m, xm)) return rc;
-    if (int rc = upload(c, c->d_adv_l, xl)) return rc;
-    if (int rc = upload(c, c->d_adv_n, xn)) return rc;
-    if (!c->d_adv_rank.ensure(4 * nx)) return c->fail(AD_E_NOMEM, "watermark ranks");
-    if (int rc = host_dict(c)) return rc;
-    if (!c->cu) c->cu = cfk_upd_work_create();
-    CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
-                  c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,
-                  c->dmiss_on ? c->d_mref.as<uint32_t>() : nullptr,
-                  c->d_ent.as<uint2>(), c->d_krec.as<KeyRec>(), c->d_kent.as<KeyEntry>()};
-    const CfkGrow grow{c, cfk_grow_dict, cfk_grow_entries, cfk_swap_entries, cfk_ballot_init, cfk_dict_spare, cfk_dict_swap,
-                       c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
-                       c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
-                       c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
-                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
-    CfkUpdOut o;
-    std::string e;
-    // the host's per-entry copies are rebuilt from the device on demand (a merge remaps every rank, the
-    // truncation moves entries): no host remap of them here
-    if (!c->host_moved)
-    {
-        c->host_moved = true;
-        c->host_ingested = true;      // ranks change, entries do not: host missing() lists stay aligned
-    }
-    c->host_stale = true;
-    const int rc = run_cfk_dict_ensure(c->cu, c->ds, d, c->d_adv_m.as<uint64_t>(), c->d_adv_l.as<uint64_t>(),
-                                       c->d_adv_n.as<int32_t>(), nx, grow, c->stream, &o, c->d_adv_rank.as<uint32_t>(), &e);
-    if (const int frc = cfk_update_follow(c, o, rc, c->stream))
-    {
-        c->host_stale = true;
-        c->dirty = true;
-        return frc;
-    }
-    if (rc)
-    {
-        // the loaded RedundantBefore stands for the device; rebuilt from the host copy at the next use
-        c->dirty = true;
-        return c->fail(rc, "ad_redundant_advance: %s", e.c_str());
-    }
-    std::vector<uint32_t> wr(n), nr(nx);
+    std::vector<Tid> ids(nx);
+    for (uint64_t j = 0; j < nx; ++j) ids[j] = B.wm[moved[j]];
+    std::vector<uint32_t> nr;
+    uint64_t n_new = 0;
+    if (int rc = dict_ensure_ids(c, ids, &nr, &n_new)) return rc;
+    std::vector<uint32_t> wr(n);
     HIPCHK(c, d2h(wr.data(), c->d_rb_wm.p, 4 * n, c->stream));      // remapped by a merge
-    HIPCHK(c, d2h(nr.data(), c->d_adv_rank.p, 4 * nx, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (uint64_t j = 0; j < nx; ++j) wr[moved[j]] = nr[j];
     if (int rc2 = upload(c, c->d_rb_wm, wr)) return rc2;
@@ -861,7 +875,7 @@ int ad_redundant_advance(ad_ctx* c, const ad_redundant_soa* in, ad_stats* stats)
         stats->ms_stage[0] = ms_dict;               // host-timed: watermark upload + dictionary growth
         stats->n_keys[0] = c->n_truncated;
         stats->n_keys[1] = c->n_trunc_keys;
-        stats->n_keys[2] = o.n_new_ids;
+        stats->n_keys[2] = n_new;
     }
     return AD_OK;
 }

@@ -302,6 +302,22 @@ const char* ad_last_error(const ad_ctx* ctx);
 /* ---- snapshot upload (ingest; builds the id dictionary, ranks and device indexes) ---- */
 int ad_cfk_load(ad_ctx* ctx, const ad_cfk_soa* cfk);
 int ad_range_cmds_load(ad_ctx* ctx, const ad_range_cmds_soa* cmds);
+/* The registry's upkeep as the store applies it, command by command, without a snapshot rebuild: each row of
+ * `upd`, in order (the same SoA as the load; its flags say what the row is):
+ *   historical[i] = 1: registerHistoricalTransactions -- historicalRangeCommands.merge(txnId, ranges, Ranges::with)
+ *                      (InMemoryCommandStore.java:814-828); nothing when txnId is a live range command;
+ *   erased[i] = 1:     the live command's status became Erased (InMemorySafeStore.update returns early, the scan
+ *                      skips it, :748-749,892); nothing when the txnId is not registered;
+ *   otherwise:         InMemorySafeStore.update (:740-763): rangeCommands.computeIfAbsent(txnId).update(ranges) --
+ *                      registered when absent, else its Ranges united with these (RangeCommand.update :547-551,
+ *                      Ranges.with = AbstractRanges.union(MERGE_OVERLAPPING), AbstractRanges.java:486-574).
+ * Ranges are the host's `keysOrRanges.slice(allBetween(txnId, executeAtOrTxnId))` less the shard-redundant ones
+ * (:758-761), normalised. New commands take the next load indices (ad_range_cmds_recovery_load then describes
+ * the registry in that order; its facts are dropped by every update). New txnIds join the id dictionary on the
+ * device; the range part of the snapshot (range entries, stabbing cells, range trees, KeyLines) is rebuilt from
+ * the registry while the CommandsForKeys stay. stats (may be NULL): ms_stage[0] registry upkeep (host),
+ * ms_stage[1] range part refresh, n_keys[0] commands registered, n_keys[1] range entries, n_keys[2] ids added. */
+int ad_range_cmds_update(ad_ctx* ctx, const ad_range_cmds_soa* upd, ad_stats* stats);
 int ad_redundant_load(ad_ctx* ctx, const ad_redundant_soa* rb);
 /* Every read of the store sees its CommandsForKeys truncated to the RedundantBefore: the snapshot is
  * truncated on the device when it is built (SafeCommandStore.maybeTruncate, SafeCommandStore.java:165-171

@@ -52,6 +52,7 @@ def lib():
         L.rc_cfk_load.argtypes = [C.c_void_p, C.POINTER(A.AdCfkSoa)]
         L.rc_range_cmds_load.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsSoa)]
         L.rc_redundant_load.argtypes = [C.c_void_p, C.POINTER(A.AdRedundantSoa)]
+        L.rc_range_cmds_update.argtypes = [C.c_void_p, C.POINTER(A.AdRangeCmdsSoa)]
         L.rc_redundant_advance.argtypes = [C.c_void_p, C.POINTER(A.AdRedundantSoa)]
         L.rc_slice_sets_load.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rc_deps_batch.argtypes = [C.c_void_p, C.POINTER(A.AdQuerySoa), C.c_uint32, C.c_uint64, C.c_uint64,
@@ -139,6 +140,10 @@ class OracleStore:
         if rs is not None:
             self._check(L.rc_range_cmds_recovery_load(self.h, C.byref(rs)))
         return self
+
+    def range_cmds_update(self, cmds):
+        """rc_range_cmds_update: registry upkeep rows (a RangeCommands: historical / erased / update per row)."""
+        self._check(lib().rc_range_cmds_update(self.h, C.byref(cmds.soa())))
 
     def redundant_advance(self, redundant):
         """rc_redundant_advance: the same entries with watermarks moved forward (truncation on the next read)."""

@@ -495,6 +495,7 @@ typedef struct {
     tid_t exec;               /* executeAtOrTxnId */
     VEC(tid_t) deps;          /* t with partialDeps().intersects(t, ranges), ascending */
 } rcmd_t;
+typedef VEC(rcmd_t) rcvec_t;
 
 typedef struct {
     rkey_t range;
@@ -510,8 +511,8 @@ struct rc_store {
     /* slice sets (rc_slice_sets_load): set k = [ss_start, ss_end)[ss_off[k], ss_off[k + 1]) */
     uint64_t* ss_off; int64_t* ss_start; int64_t* ss_end; uint32_t n_ssets;
     VEC(cfk_t) cfks;          /* sorted by key */
-    VEC(rcmd_t) cmds;         /* rangeCommands, sorted by txnId */
-    VEC(rcmd_t) hist;         /* historicalRangeCommands, sorted by txnId */
+    rcvec_t cmds;             /* rangeCommands, sorted by txnId */
+    rcvec_t hist;             /* historicalRangeCommands, sorted by txnId */
     VEC(rb_entry_t) rb;
     VEC(tid_t) miss;          /* TxnInfo.missing() lists (rc_cfk_missing_load) */
     int loaded;
@@ -750,6 +751,201 @@ int rc_range_cmds_load(rc_store* s, const ad_range_cmds_soa* in)
         if (tid_eq(&s->cmds.v[i - 1].txnId, &s->cmds.v[i].txnId)) return fail(s, AD_E_INVAL, "duplicate range command");
     for (size_t i = 1; i < s->hist.n; ++i)
         if (tid_eq(&s->hist.v[i - 1].txnId, &s->hist.v[i].txnId)) return fail(s, AD_E_INVAL, "duplicate historical range command");
+    return 0;
+}
+
+/* Range.compareIntersecting (Range.java:296-305) */
+static int rk_cmp_intersecting(const rkey_t* x, const rkey_t* y)
+{
+    if (x->a >= y->b) return 1;
+    if (x->b <= y->a) return -1;
+    return 0;
+}
+
+/* AbstractRanges.supersetLinearMerge (AbstractRanges.java:429-474): how far `as` covers a prefix of `bs` */
+static void superset_linear_merge(const rkey_t* as, size_t na, const rkey_t* bs, size_t nb, size_t* pai, size_t* pbi)
+{
+    size_t ai = 0, bi = 0;
+    while (ai < na && bi < nb)
+    {
+        rkey_t a = as[ai];
+        const rkey_t b = bs[bi];
+        int c = rk_cmp_intersecting(&a, &b);
+        if (c < 0) ai++;
+        else if (c > 0) break;
+        else if (b.a < a.a) break;
+        else if (b.b <= a.b)
+        {
+            bi++;
+            if (b.b == a.b) ai++;
+        }
+        else
+        {
+            size_t t = ai;
+            int out = 0;
+            do
+            {
+                if (++t == na || a.b != as[t].a) { out = 1; break; }
+                a = as[t];
+            } while (a.b < b.b);
+            if (out) break;
+            bi++;
+            ai = t;
+        }
+    }
+    *pai = ai;
+    *pbi = bi;
+}
+
+/* Ranges.with (Ranges.java:136-139) = AbstractRanges.union(MERGE_OVERLAPPING, this, that) (:486-574) */
+static void ranges_with(const rkey_t* left, size_t nl, const rkey_t* right, size_t nr, rkey_t* out, size_t* nout)
+{
+    size_t n = 0;
+    if (nr == 0 || nl == 0)
+    {
+        const rkey_t* src = nr == 0 ? left : right;
+        const size_t m = nr == 0 ? nl : nr;
+        memcpy(out, src, m * sizeof(rkey_t));
+        *nout = m;
+        return;
+    }
+    const rkey_t *as = left, *bs = right;
+    size_t na = nl, nb = nr;
+    if (as[0].a > bs[0].a || (as[0].a == bs[0].a && as[na - 1].b < bs[nb - 1].b))
+    {
+        const rkey_t* t = as; as = bs; bs = t;
+        const size_t u = na; na = nb; nb = u;
+    }
+    size_t ai, bi;
+    superset_linear_merge(as, na, bs, nb, &ai, &bi);
+    if (bi == nb)
+    {
+        memcpy(out, as, na * sizeof(rkey_t));
+        *nout = na;
+        return;
+    }
+    memcpy(out, as, ai * sizeof(rkey_t));
+    n = ai;
+    while (ai < na && bi < nb)
+    {
+        rkey_t a = as[ai];
+        const rkey_t b = bs[bi];
+        const int c = rk_cmp_intersecting(&a, &b);
+        if (c < 0) { out[n++] = a; ai++; }
+        else if (c > 0) { out[n++] = b; bi++; }
+        else
+        {
+            const int64_t start = a.a <= b.a ? a.a : b.a;
+            int64_t end = a.b >= b.b ? a.b : b.b;
+            ai++;
+            bi++;
+            while (ai < na || bi < nb)
+            {
+                rkey_t mn;
+                int from_a;
+                if (ai == na) { mn = bs[bi]; from_a = 0; }
+                else if (bi == nb) { mn = a = as[ai]; from_a = 1; }
+                else if (as[ai].a < bs[bi].a) { mn = a = as[ai]; from_a = 1; }
+                else { mn = bs[bi]; from_a = 0; }
+                if (mn.a > end) break;
+                if (mn.b > end) end = mn.b;
+                if (from_a) ai++;
+                else bi++;
+            }
+            out[n++] = (rkey_t){start, end};
+        }
+    }
+    while (ai < na) out[n++] = as[ai++];
+    while (bi < nb) out[n++] = bs[bi++];
+    *nout = n;
+}
+
+/* The registry's upkeep as a store applies it command by command (ad_range_cmds_update): each row, in order,
+ *   historical: registerHistoricalTransactions -- historicalRangeCommands.merge(txnId, ranges, Ranges::with),
+ *               nothing when rangeCommands holds the txnId (InMemoryCommandStore.java:814-828);
+ *   erased:     the live command's status becomes Erased (the scan skips it, :892); absent: nothing;
+ *   otherwise:  InMemorySafeStore.update (:740-763) -> rangeCommands.computeIfAbsent(txnId).update(ranges)
+ *               (RangeCommand.update :547-551: the ranges, or their union with the earlier ones).
+ * New commands take the next load index (orig); recovery facts are dropped (reloaded by the host). */
+static rcmd_t* cmd_find(rcvec_t* v, const tid_t* t)
+{
+    size_t lo = 0, hi = v->n;
+    while (lo < hi)
+    {
+        const size_t m = (lo + hi) / 2;
+        if (tid_cmp(&v->v[m].txnId, t) < 0) lo = m + 1;
+        else hi = m;
+    }
+    return lo < v->n && tid_cmp(&v->v[lo].txnId, t) == 0 ? &v->v[lo] : NULL;
+}
+
+static rcmd_t* cmd_insert(rcvec_t* v, const tid_t* t, size_t orig)
+{
+    rcmd_t c;
+    memset(&c, 0, sizeof(c));
+    c.txnId = *t;
+    c.orig = orig;
+    size_t pos = v->n;
+    while (pos > 0 && tid_cmp(&v->v[pos - 1].txnId, t) > 0) --pos;
+    VEC_PUSH(*v, c);
+    memmove(&v->v[pos + 1], &v->v[pos], (v->n - 1 - pos) * sizeof(rcmd_t));
+    v->v[pos] = c;
+    return &v->v[pos];
+}
+
+static void cmd_union(rcmd_t* c, const rkey_t* add, size_t nadd)
+{
+    rkey_t* out = malloc(sizeof(rkey_t) * (c->ranges.n + nadd + 1));
+    size_t n = 0;
+    ranges_with(c->ranges.v, c->ranges.n, add, nadd, out, &n);
+    c->ranges.n = 0;
+    for (size_t i = 0; i < n; ++i) VEC_PUSH(c->ranges, out[i]);
+    free(out);
+}
+
+int rc_range_cmds_update(rc_store* s, const ad_range_cmds_soa* in)
+{
+    for (uint64_t i = 0; i < in->n_cmds; ++i)
+    {
+        const tid_t t = {in->txn_msb[i], in->txn_lsb[i], in->txn_node[i]};
+        if (!tid_domain(&t)) return fail(s, AD_E_INVAL, "range command %llu has a key-domain TxnId", (unsigned long long)i);
+        for (uint64_t r = in->range_off[i]; r < in->range_off[i + 1]; ++r)
+            if (in->range_start[r] >= in->range_end[r] || (r > in->range_off[i] && in->range_start[r] < in->range_end[r - 1]))
+                return fail(s, AD_E_INVAL, "range command %llu: ranges not normalised", (unsigned long long)i);
+        const rkey_t* add = (const rkey_t*)NULL;
+        const size_t nadd = (size_t)(in->range_off[i + 1] - in->range_off[i]);
+        rkey_t* tmp = malloc(sizeof(rkey_t) * (nadd + 1));
+        for (size_t r = 0; r < nadd; ++r) tmp[r] = (rkey_t){in->range_start[in->range_off[i] + r], in->range_end[in->range_off[i] + r]};
+        add = tmp;
+        const size_t next = s->cmds.n + s->hist.n;
+        if (in->historical && in->historical[i])
+        {
+            if (!cmd_find(&s->cmds, &t))
+            {
+                rcmd_t* c = cmd_find(&s->hist, &t);
+                if (!c)
+                {
+                    c = cmd_insert(&s->hist, &t, next);
+                    c->historical = 1;
+                }
+                cmd_union(c, add, nadd);
+            }
+        }
+        else if (in->erased && in->erased[i])
+        {
+            rcmd_t* c = cmd_find(&s->cmds, &t);
+            if (c) c->erased = 1;
+        }
+        else
+        {
+            rcmd_t* c = cmd_find(&s->cmds, &t);
+            if (!c) c = cmd_insert(&s->cmds, &t, next);
+            cmd_union(c, add, nadd);
+        }
+        free(tmp);
+    }
+    for (size_t i = 0; i < s->cmds.n; ++i) { s->cmds.v[i].has_rec = 0; VEC_FREE(s->cmds.v[i].deps); }
+    for (size_t i = 0; i < s->hist.n; ++i) { s->hist.v[i].has_rec = 0; VEC_FREE(s->hist.v[i].deps); }
     return 0;
 }
 

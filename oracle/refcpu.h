@@ -42,6 +42,7 @@ const char* rc_last_error(const rc_store* s);
 
 int rc_cfk_load(rc_store* s, const ad_cfk_soa* cfk);
 int rc_range_cmds_load(rc_store* s, const ad_range_cmds_soa* cmds);
+int rc_range_cmds_update(rc_store* s, const ad_range_cmds_soa* in);
 int rc_redundant_load(rc_store* s, const ad_redundant_soa* rb);
 int rc_redundant_advance(rc_store* s, const ad_redundant_soa* in);
 /* the store's slice sets that ad_query_soa.slice_set names (ad_slice_sets_load) */

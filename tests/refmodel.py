@@ -487,3 +487,107 @@ def sequential_augmented(w):
                          pad(cm.erased) if cm.erased is not None or n0 == 0 else None,
                          pad(cm.historical) if cm.historical is not None or n0 == 0 else None)
     return Workload(w.name + "_aug", cfk, cmds, w.redundant, q, 0, w.params, si, w.slices)
+
+
+def ranges_with(left, right):
+    """Ranges.with (Ranges.java:136-139): AbstractRanges.union(MERGE_OVERLAPPING, left, right) (:486-574) after
+    supersetLinearMerge (:429-474), over [(start, end)] lists; touching ranges join only a run that already
+    merged an intersection (the Java's `min.start().compareTo(end) > 0` test)."""
+    def inter(a, b):
+        return 1 if a[0] >= b[1] else (-1 if a[1] <= b[0] else 0)
+    if not right or not left:
+        return list(left or right)
+    A_, B_ = list(left), list(right)
+    if A_[0][0] > B_[0][0] or (A_[0][0] == B_[0][0] and A_[-1][1] < B_[-1][1]):
+        A_, B_ = B_, A_
+    ai = bi = 0
+    while ai < len(A_) and bi < len(B_):                    # supersetLinearMerge
+        a, b = A_[ai], B_[bi]
+        c = inter(a, b)
+        if c < 0:
+            ai += 1
+        elif c > 0 or b[0] < a[0]:
+            break
+        elif b[1] <= a[1]:
+            bi += 1
+            ai += b[1] == a[1]
+        else:
+            t, ok = ai, True
+            while True:
+                t += 1
+                if t == len(A_) or a[1] != A_[t][0]:
+                    ok = False
+                    break
+                a = A_[t]
+                if not a[1] < b[1]:
+                    break
+            if not ok:
+                break
+            bi, ai = bi + 1, t
+    if bi == len(B_):
+        return A_
+    out = A_[:ai]
+    while ai < len(A_) and bi < len(B_):
+        a, b = A_[ai], B_[bi]
+        c = inter(a, b)
+        if c < 0:
+            out.append(a)
+            ai += 1
+        elif c > 0:
+            out.append(b)
+            bi += 1
+        else:
+            start, end = min(a[0], b[0]), max(a[1], b[1])
+            ai, bi = ai + 1, bi + 1
+            while ai < len(A_) or bi < len(B_):
+                if ai == len(A_) or (bi < len(B_) and not A_[ai][0] < B_[bi][0]):
+                    m, from_a = B_[bi], False
+                else:
+                    m, from_a = A_[ai], True
+                if m[0] > end:
+                    break
+                end = max(end, m[1])
+                if from_a:
+                    ai += 1
+                else:
+                    bi += 1
+            out.append((start, end))
+    return out + A_[ai:] + B_[bi:]
+
+
+def range_cmds_update(cmds, upd):
+    """The registry after upkeep rows (rc_range_cmds_update's rules: historical merge unless live, erase of a live
+    command, update = register or union) as a new RangeCommands, commands in (live, historical) TxnId order."""
+    from accord_deps.model import RangeCommands, Tids
+    tup = lambda T, i: (int(T.msb[i]), int(T.lsb[i]), int(T.node[i]))  # noqa: E731
+    live, hist = {}, {}
+    for i in range(len(cmds.txn.msb)):
+        rs = [(int(cmds.range_start[j]), int(cmds.range_end[j])) for j in range(int(cmds.range_off[i]), int(cmds.range_off[i + 1]))]
+        t = tup(cmds.txn, i)
+        if cmds.historical is not None and cmds.historical[i]:
+            hist[t] = rs
+        else:
+            live[t] = [rs, bool(cmds.erased is not None and cmds.erased[i])]
+    for i in range(len(upd.txn.msb)):
+        t = tup(upd.txn, i)
+        rs = [(int(upd.range_start[j]), int(upd.range_end[j])) for j in range(int(upd.range_off[i]), int(upd.range_off[i + 1]))]
+        if upd.historical is not None and upd.historical[i]:
+            if t not in live:
+                hist[t] = ranges_with(hist[t], rs) if t in hist else rs
+        elif upd.erased is not None and upd.erased[i]:
+            if t in live:
+                live[t][1] = True
+        else:
+            live[t] = [ranges_with(live[t][0], rs), live[t][1]] if t in live else [rs, False]
+    rows = [(t, v[0], v[1], False) for t, v in sorted(live.items(), key=lambda x: key(x[0]))] + \
+           [(t, v, False, True) for t, v in sorted(hist.items(), key=lambda x: key(x[0]))]
+    off = [0]
+    st, en = [], []
+    for _, rs, _, _ in rows:
+        st += [a for a, _ in rs]
+        en += [b for _, b in rs]
+        off.append(len(st))
+    ids = Tids(np.array([r[0][0] for r in rows], np.uint64), np.array([r[0][1] for r in rows], np.uint64),
+               np.array([r[0][2] for r in rows], np.int32))
+    return RangeCommands(ids, np.array(off, np.uint64), np.array(st, np.int64), np.array(en, np.int64),
+                         erased=np.array([r[2] for r in rows], np.uint8), historical=np.array([r[3] for r in rows], np.uint8))

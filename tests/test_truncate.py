@@ -155,3 +155,41 @@ def test_oracle_advance_rejects_regress_and_ranges():
             st.redundant_advance(Redundant(moved, red.range_end, red.start_epoch, red.end_epoch, red.wm))
     finally:
         st.close()
+
+
+# ---- range-command registry upkeep (rc_range_cmds_update) ------------------------------------------------------
+def test_ranges_with_cases():
+    import refmodel as R
+    assert R.ranges_with([(0, 5)], [(5, 10)]) == [(0, 5), (5, 10)]          # touching: apart (MERGE_OVERLAPPING)
+    assert R.ranges_with([(0, 5)], [(3, 10)]) == [(0, 10)]
+    assert R.ranges_with([(0, 5), (5, 9)], [(3, 6)]) == [(0, 5), (5, 9)]    # covered through a touching chain
+    assert R.ranges_with([(0, 5), (6, 9)], [(3, 6)]) == [(0, 9)]            # a merge run takes the touching one
+    assert R.ranges_with([(0, 10)], [(2, 3), (4, 5)]) == [(0, 10)]          # superset
+    assert R.ranges_with([(2, 3)], [(0, 10)]) == [(0, 10)]
+    assert R.ranges_with([(0, 2), (8, 9)], [(3, 4)]) == [(0, 2), (3, 4), (8, 9)]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_range_cmds_update_matches_model(oracle, seed):
+    import pyoracle
+    w = synth.random_small(3700 + seed, n_keys=40, n_hist_txns=200, n_txns=80, n_range_cmds=20 + seed,
+                           range_frac=0.3 * (seed % 2), with_slices=(seed % 3 == 1), start_inclusive=(seed % 4 == 2))
+    st = pyoracle.OracleStore(w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        cmds = w.cmds
+        for step in range(3):
+            u = synth.range_cmd_updates(cmds, 50 * seed + step, 12)
+            st.range_cmds_update(u)
+            cmds = refmodel.range_cmds_update(cmds, u)
+            w2 = type(w)(w.name, w.cfk, cmds, w.redundant, w.queries, w.flags, w.params, w.range_start_inclusive,
+                         w.slices)
+            got = st.deps_batch(w.queries, w.flags)
+            assert got.equals(oracle.resolve(w2)), step
+            for i in range(len(w.queries)):
+                kd, rd, dd = refmodel.request_pairs(w2, i)
+                g = _request(got, i)
+                for m, pairs in ((0, kd), (1, rd), (2, dd)):
+                    assert g[m] == tuple(refmodel.csr(pairs)), (seed, step, i, A.MAP_NAMES[m])
+    finally:
+        st.close()
