@@ -1004,7 +1004,7 @@ def range_cmd_updates(cmds, seed, n, lo=-520, hi=520, epoch=1, hlc_hi=500, frac=
     kinds = rng.choice(4, n, p=np.asarray(frac) / np.sum(frac))
     fresh = make_txn_ids(epoch, np.sort(rng.choice(np.arange(1, hlc_hi), n, replace=False)).astype(np.uint64) * 10 + 7,
                          rng.choice([A.KIND_READ, A.KIND_WRITE, A.KIND_SYNC_POINT, A.KIND_EXCLUSIVE_SYNC_POINT], n),
-                         rng.integers(1, 17, n), domain=1)
+                         rng.integers(100, 116, n), domain=1)      # nodes no history id carries: no equal ids
     rows_t, er, hi_f, off, st, en = [], [], [], [0], [], []
     made = []
     for i in range(n):

@@ -531,8 +531,11 @@ int dict_ensure_ids(ad_ctx* c, const std::vector<Tid>& ids, std::vector<uint32_t
     c->host_stale = true;
     CfkUpdOut o;
     std::string e;
+    CfkDerivedBufs b{c->d_cand.as<uint32_t>(), c->d_cand.cap / 4, c->d_cwr.as<uint32_t>(), c->d_cwr.cap / 4,
+                     c->d_w.as<uint2>(), c->d_w.cap / 8};
     const int rc = run_cfk_dict_ensure(c->cu, c->ds, d, c->d_adv_m.as<uint64_t>(), c->d_adv_l.as<uint64_t>(),
-                                       c->d_adv_n.as<int32_t>(), nx, grow, c->stream, &o, c->d_adv_rank.as<uint32_t>(), &e);
+                                       c->d_adv_n.as<int32_t>(), nx, grow, &b, cfk_need_bufs, c, c->stream, &o,
+                                       c->d_adv_rank.as<uint32_t>(), &e);
     if (const int frc = cfk_update_follow(c, o, rc, c->stream))
     {
         c->dirty = true;

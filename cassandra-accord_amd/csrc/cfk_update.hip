@@ -2731,7 +2731,7 @@ __global__ __launch_bounds__(256) void k_trunc_miss(uint64_t n, const uint32_t* 
 
 // thread per id: its dictionary rank (a member after run_cfk_dict_ensure); a miss flags ctl->err
 __global__ void k_id_ranks(DevSnapshot s, DictSample ds, uint64_t n, const uint64_t* msb, const uint64_t* lsb,
-                           const int32_t* node, uint32_t* rank, UpdCtl* ctl)
+                           const int32_t* node, const uint64_t* dict_lsb_raw, uint32_t* rank, UpdCtl* ctl)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -2739,6 +2739,7 @@ __global__ void k_id_ranks(DevSnapshot s, DictSample ds, uint64_t n, const uint6
     const uint32_t r = dict_member_rank(s, ds, norm_tid(msb[i], lsb[i], node[i]), &p);
     rank[i] = r;
     if (!r) upd_fail(ctl, UE_ABSENT, (uint32_t)i);
+    else if (dict_lsb_raw[p] != lsb[i]) upd_fail(ctl, UE_FLAGS, (uint32_t)i);     // equal ids, other flag bits
 }
 
 }  // namespace
@@ -2850,8 +2851,9 @@ int run_cfk_truncate(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, CfkDerivedBu
 }
 
 int run_cfk_dict_ensure(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint64_t* msb, const uint64_t* lsb,
-                        const int32_t* node, uint64_t n, const CfkGrow& grow, hipStream_t st, CfkUpdOut* out,
-                        uint32_t* ranks, std::string* err)
+                        const int32_t* node, uint64_t n, const CfkGrow& grow, CfkDerivedBufs* bufs,
+                        int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                        hipStream_t st, CfkUpdOut* out, uint32_t* ranks, std::string* err)
 {
     *out = CfkUpdOut{};
     if (!n) return AD_OK;
@@ -2885,11 +2887,28 @@ int run_cfk_dict_ensure(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uin
         *err = "ids equal under Timestamp.equals differ in flag bits";
         return AD_E_INCONSISTENT_ID;
     }
+    if (out->merged)
+    {
+        // a merge remapped the per-entry ranks in place: the derived arrays (cand / cwr / w / KeyEntry / trees) hold
+        // the old ones -- derive them again (the committed order's entry indices stand, its ranks do not: sort afresh)
+        w->cm_valid = false;
+        w->moved = false;
+        UALLOC(w->chg[w->chg_cur], std::max<uint64_t>(s.n_ent, 1), false);
+        UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+        if (int rc = cfk_derive(w, s, d, bufs, need, need_ctx, st, err)) return rc;
+        out->rederived = true;
+    }
     const DictSample ds1 = sample();
-    k_id_ranks<<<blocks(n), 256, 0, st>>>(s, ds1, n, msb, lsb, node, ranks, ctl);
+    UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
+    k_id_ranks<<<blocks(n), 256, 0, st>>>(s, ds1, n, msb, lsb, node, d.dict_lsb_raw, ranks, ctl);
     UCHK(hipGetLastError());
     UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
+    if (w->h_ctl->err == UE_FLAGS)
+    {
+        *err = "ids equal under Timestamp.equals differ in flag bits";
+        return AD_E_INCONSISTENT_ID;
+    }
     if (w->h_ctl->err) { *err = "id missing from the dictionary after its growth (internal)"; return AD_E_STATE; }
     return AD_OK;
 }

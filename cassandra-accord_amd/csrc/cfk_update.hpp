@@ -198,9 +198,11 @@ int run_cfk_truncate(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, CfkDerivedBu
 
 // The ids (device arrays, n) join the dictionary where it does not hold them (appended, or merged
 // with the rank remap of an update batch: out->merged / merge_pos as run_cfk_update reports them);
-// ranks[i] (device) = each id's member rank afterwards.
+// ranks[i] (device) = each id's member rank afterwards. After a merge the derived arrays are derived again
+// (out->rederived); the caller rebuilds the KeyLines (cfk_update_follow does).
 int run_cfk_dict_ensure(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const uint64_t* msb, const uint64_t* lsb,
-                        const int32_t* node, uint64_t n, const CfkGrow& grow, hipStream_t st, CfkUpdOut* out,
-                        uint32_t* ranks, std::string* err);
+                        const int32_t* node, uint64_t n, const CfkGrow& grow, CfkDerivedBufs* bufs,
+                        int (*need)(void* ctx, uint64_t cand, uint64_t cwr, uint64_t w, CfkDerivedBufs* bufs), void* need_ctx,
+                        hipStream_t st, CfkUpdOut* out, uint32_t* ranks, std::string* err);
 
 }  // namespace adx

@@ -155,3 +155,26 @@ def test_advance_errors():
         assert got.equals(native.resolve(w))
     finally:
         st.close()
+
+
+@pytest.mark.parametrize("path", [0, 1])
+def test_advance_merging_without_removals(oracle, path):
+    # new watermarks older than the dictionary's newest id but below every entry: the dictionary merges (every
+    # stored rank moves), nothing is truncated -- the derived arrays must follow the merge alone
+    from accord_deps.model import make_txn_ids
+    w = synth.with_redundant_ranges(synth.config2(n_txns=4000, n_keys=4000, n_hist_entries=40000), 12, seed=4,
+                                    none_frac=1.0)
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices, path=path)
+    try:
+        st.load(w)
+        red = w.redundant
+        n = len(red.range_start)
+        low = make_txn_ids(1, np.zeros(n, np.uint64), A.KIND_EXCLUSIVE_SYNC_POINT, np.arange(n) + 1, domain=1)
+        red2 = Redundant(red.range_start, red.range_end, red.start_epoch, red.end_epoch, low)
+        stats = st.redundant_advance(red2)
+        assert stats["n_keys"][0] == 0 and stats["n_keys"][2] == n
+        got = st.calculate_partial_deps(w.queries, w.flags)
+        ok, why = got.equals(oracle.resolve(_with_red(w, red2)), detail=True)
+        assert ok, why
+    finally:
+        st.close()
