@@ -227,18 +227,20 @@ int cfk_dict_swap(void* vc, uint64_t** hi, uint64_t** lo, int32_t** node, uint64
 // (r = 2i+1 -> 2(i + #{pos <= i}) + 1, the device remap)
 int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipStream_t st)
 {
-    // (the whole dictionary is read back below; host rank copies that are stale -- host_moved -- are
-    // rebuilt from the device later, their remap here is then moot)
-    c->host_dict_stale = false;
+    // (a current host dictionary is read back whole below -- a stale one stays stale, read on demand; host rank
+    // copies that are stale -- host_moved -- are rebuilt from the device later, their remap here is then moot)
     const uint64_t nd = c->ds.n_dict;
     std::vector<uint64_t> pos(U);
-    c->dict_msb.resize(nd);
-    c->dict_lsb.resize(nd);
-    c->dict_node.resize(nd);
     HIPCHK(c, d2h(pos.data(), pos_dev, 8 * U, st));
-    HIPCHK(c, d2h(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, st));
-    HIPCHK(c, d2h(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, st));
-    HIPCHK(c, d2h(c->dict_node.data(), c->d_dict_node.p, 4 * nd, st));
+    if (!c->host_dict_stale)
+    {
+        c->dict_msb.resize(nd);
+        c->dict_lsb.resize(nd);
+        c->dict_node.resize(nd);
+        HIPCHK(c, d2h(c->dict_msb.data(), c->d_dict_hi.p, 8 * nd, st));
+        HIPCHK(c, d2h(c->dict_lsb.data(), c->d_dict_lsb_raw.p, 8 * nd, st));
+        HIPCHK(c, d2h(c->dict_node.data(), c->d_dict_node.p, 4 * nd, st));
+    }
     HIPCHK(c, hipStreamSynchronize(st));
     auto remap = [&](uint32_t r) -> uint32_t {
         if (r == 0) return 0;
@@ -431,7 +433,6 @@ int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_app
 // the KeyLines. Nonzero: a device failure (the message is set).
 int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st)
 {
-    const uint64_t nd0 = c->dict_msb.size();
     if (rc == AD_OK && o.n_load_pruned)
     {
         const uint64_t m = o.n_load_pruned;
@@ -461,16 +462,21 @@ int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st)
         c->host_stale = true;
         ++c->snap_gen;
     }
-    if (c->ds.n_dict > nd0)
+    if (o.n_new_ids)
     {
-        // ids appended to the device dictionary (kept even when the batch then failed): host copy
-        const uint64_t add = c->ds.n_dict - nd0;
-        c->dict_msb.resize(nd0 + add);
-        c->dict_lsb.resize(nd0 + add);
-        c->dict_node.resize(nd0 + add);
-        HIPCHK(c, copy_sync(c->dict_msb.data() + nd0, c->d_dict_hi.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
-        HIPCHK(c, copy_sync(c->dict_lsb.data() + nd0, c->d_dict_lsb_raw.as<uint64_t>() + nd0, 8 * add, hipMemcpyDeviceToHost));
-        HIPCHK(c, copy_sync(c->dict_node.data() + nd0, c->d_dict_node.as<int32_t>() + nd0, 4 * add, hipMemcpyDeviceToHost));
+        // ids appended to the device dictionary (kept even when the batch then failed): a current host copy takes
+        // them (a stale one is read whole on demand)
+        const uint64_t nd1 = c->dict_msb.size();
+        if (!c->host_dict_stale && c->ds.n_dict > nd1)
+        {
+            const uint64_t add = c->ds.n_dict - nd1;
+            c->dict_msb.resize(nd1 + add);
+            c->dict_lsb.resize(nd1 + add);
+            c->dict_node.resize(nd1 + add);
+            HIPCHK(c, copy_sync(c->dict_msb.data() + nd1, c->d_dict_hi.as<uint64_t>() + nd1, 8 * add, hipMemcpyDeviceToHost));
+            HIPCHK(c, copy_sync(c->dict_lsb.data() + nd1, c->d_dict_lsb_raw.as<uint64_t>() + nd1, 8 * add, hipMemcpyDeviceToHost));
+            HIPCHK(c, copy_sync(c->dict_node.data() + nd1, c->d_dict_node.as<int32_t>() + nd1, 4 * add, hipMemcpyDeviceToHost));
+        }
         drop_global_dict(c);         // global ranks of the multi-store exchange no longer cover the dictionary
         // the sampled index over the grown dictionary (a stale one is still correct, only slower)
         // (a buffer that could not grow may have been released: then no sample, the searches span the
@@ -510,7 +516,6 @@ int dict_ensure_ids(ad_ctx* c, const std::vector<Tid>& ids, std::vector<uint32_t
     if (int rc = upload(c, c->d_adv_l, xl)) return rc;
     if (int rc = upload(c, c->d_adv_n, xn)) return rc;
     if (!c->d_adv_rank.ensure(4 * nx)) return c->fail(AD_E_NOMEM, "id ranks");
-    if (int rc = host_dict(c)) return rc;
     if (!c->cu) c->cu = cfk_upd_work_create();
     CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
                   c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr,

@@ -162,3 +162,24 @@ def test_views_outlive_their_hostout(pin):
         assert out3 is out2 and out2.off is not None
     finally:
         st.close()
+
+
+def test_staged_upload_after_destroyed_context(oracle):
+    # the hazard commit 7295a85 closed: a staged pageable upload on context A (columns larger than
+    # one 8 MiB staging chunk, so both chunks of the pair carry events), A destroyed with its stream, then at once
+    # a staged upload on a fresh context B drawing the same staging pair from the pool -- B's uploads must not wait
+    # on events recorded on A's destroyed stream. Run once per suite; each round is checked bit-exact.
+    w = synth.config2(n_txns=4000, n_keys=20000, n_hist_entries=400000)
+    exp = oracle.resolve(w)
+    for _ in range(3):
+        a = native.DeviceCommandStore(0)
+        a.load(w, prepare=False)               # staged H2D of the pageable columns on A's stream
+        a.close()                              # ad_ctx_destroy: A's stream goes
+        b = native.DeviceCommandStore(0)
+        try:
+            b.load(w)                          # staged again, same pool pair, fresh stream
+            got = b.calculate_partial_deps(w.queries, w.flags)
+        finally:
+            b.close()
+        ok, why = got.equals(exp, detail=True)
+        assert ok, why
