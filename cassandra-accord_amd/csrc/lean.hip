@@ -461,58 +461,59 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
     // item's element loads and before its stores, and waited for an iteration later -- no wait of the
     // loop covers the stores just issued (vmcnt counts loads and stores in order).
     const uint32_t it0 = uniform(lean_block() * LEAN_WAVES + (threadIdx.x >> 6));
-    const uint32_t tc = req_of(it0, dload(it0));
-    Req qc = derive(tc, loadA(tc));
-    int64_t keyc;
-    uint32_t slc = LS_NONE;
-    loadB(qc, keyc, slc);
-    Hdr Hc;
+    // The pipeline registers, two sets used in turn (the loop body runs twice per trip, C -> N then N -> C):
+    // every later item's load lands in the other set, so the loop never copies a register whose load is in
+    // flight -- such a copy waits for it, and vmcnt counts loads and stores in order, so the back edge used to
+    // wait for every load and store of the iteration.
+    struct Pipe {
+        Req qc;          // item it: its request,
+        int64_t keyc;    //   its key lane's key,
+        Hdr Hc;          //   its line (header quarter)
+        Req q1;          // item it + nw: its request,
+        int64_t key1;    //   key and line position loads
+        uint32_t sl1;
+        uint32_t t2;     // item it + 2 nw: request index and record
+        Raw r2;
+        uint32_t t3;     // pass 2: item it + 3 nw's deferred1 entry
+    };
+    Pipe PA, PB;
     {
+        const uint32_t tc = req_of(it0, dload(it0));
+        PA.qc = derive(tc, loadA(tc));
+        uint32_t slc = LS_NONE;
+        loadB(PA.qc, PA.keyc, slc);
         bool lookc;
         uint32_t dc;
-        loadD(qc, keyc, slc, lookc, dc);
-        loadC(qc, keyc, lookc, dc, Hc);
+        loadD(PA.qc, PA.keyc, slc, lookc, dc);
+        loadC(PA.qc, PA.keyc, lookc, dc, PA.Hc);
+        const uint32_t t1 = req_of(it0 + nw, dload(it0 + nw));
+        PA.q1 = derive(t1, loadA(t1));
+        PA.sl1 = LS_NONE;
+        loadB(PA.q1, PA.key1, PA.sl1);
+        PA.t2 = req_of(it0 + 2 * nw, dload(it0 + 2 * nw));
+        PA.r2 = loadA(PA.t2);
+        PA.t3 = dload(it0 + 3 * nw);
     }
-    const uint32_t t1 = req_of(it0 + nw, dload(it0 + nw));
-    Req q1 = derive(t1, loadA(t1));
-    int64_t key1;
-    uint32_t sl1 = LS_NONE;
-    loadB(q1, key1, sl1);
-    uint32_t t2 = req_of(it0 + 2 * nw, dload(it0 + 2 * nw));
-    Raw r2 = loadA(t2);
-    uint32_t t3 = dload(it0 + 3 * nw);
-    // the later items' loads (see above); H1 receives item it + nw's lines
-    int64_t key2;
-    uint32_t sl2 = LS_NONE, t3u = 0, t4 = 0;
-    Req q2;
-    Raw r3;
-    auto prefetch = [&](uint32_t it, Hdr& H1) {
+    // the later items' loads of the step for item it (C -> N)
+    auto prefetch = [&](uint32_t it, const Pipe& C, Pipe& N) {
         bool look1;
         uint32_t d1;
-        loadD(q1, key1, sl1, look1, d1);
-        loadC(q1, key1, look1, d1, H1);
-        q2 = derive(t2, r2);
-        sl2 = LS_NONE;
-        loadB(q2, key2, sl2);
-        t3u = req_of(it + 3 * nw, t3);
-        r3 = loadA(t3u);
-        t4 = dload(it + 4 * nw);
+        loadD(C.q1, C.key1, C.sl1, look1, d1);
+        loadC(C.q1, C.key1, look1, d1, N.Hc);
+        N.q1 = derive(C.t2, C.r2);
+        N.sl1 = LS_NONE;
+        loadB(N.q1, N.key1, N.sl1);
+        N.t2 = req_of(it + 3 * nw, C.t3);
+        N.r2 = loadA(N.t2);
+        N.t3 = dload(it + 4 * nw);
+        N.qc = C.q1;
+        N.keyc = C.key1;
     };
-    auto rotate = [&](Hdr& H1) {
-        qc = q1;
-        keyc = key1;
-        Hc = H1;
-        q1 = q2;
-        key1 = key2;
-        sl1 = sl2;
-        t2 = t3u;
-        r2 = r3;
-        t3 = t4;
-    };
-
     uint32_t nwide = 0;         // wave-uniform: wide pass 1's requests above LPR raw emissions
-    for (uint32_t it = it0; it < n_items; it += nw)
-    {
+    auto step = [&](const uint32_t it, Pipe& C, Pipe& N) {
+        Req& qc = C.qc;
+        const int64_t keyc = C.keyc;
+        Hdr& Hc = C.Hc;
         const uint32_t t = qc.t;
 
         // ---- current item: per key p = hl < np, newest test and emission counts
@@ -577,6 +578,10 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             }
         }
         act = act && !defer;
+        // the later items' loads go out once, here, for both paths below, into the other register set (N); the
+        // element loads' wait covers them too. (Behind the element loads instead, as before round 6: no faster --
+        // config 2 pass 1 0.538 against 0.533 ms, config 4 / 3 / the mix within noise.)
+        prefetch(it, C, N);
 
         // ---- the wide item: a request with 33..64 raw emissions -> two per lane (element x = hl and
         // hl + 32), sorted as 64 (seg_bitonic_wide), the rest as below with masks over both halves
@@ -610,8 +615,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
             };
             uint32_t ax0, ax1;
             const uint32_t tw0 = raw_txw(hl, ax0), tw1 = raw_txw(hl + 32, ax1);
-            Hdr Hn;
-            prefetch(it, Hn);
             const uint32_t r0 = tw0 & RANK_MASK, r1 = tw1 & RANK_MASK;
             const bool want0 = wact && hl < T && r0 != self && r0 < S, want1 = wact && hl + 32 < T && r1 != self && r1 < S;
             const bool is1_0 = ((KINDS_RS_OR_WS >> (tw0 >> RANK_BITS)) & 1) == 0;
@@ -692,8 +695,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
                 }
             }
             put_sizes(wact, t, 1, 0, 0, 0, 0, false);          // no range commands on this path
-            rotate(Hn);
-            continue;
+            return;
         }
 
         // ---- one raw emission per lane: element e = hl of key a
@@ -764,9 +766,6 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
                 ce1 = (cin1 && rlive1 ? kl64 : s.cell_ent)[rlive1 ? cidx1 : 0u];
             }
         }
-        // the later items' loads go out behind this item's element loads
-        Hdr Hn;
-        prefetch(it, Hn);
 
         const uint32_t txw = !live ? 0u : ((from_cand || cls != 0) ? lv : (a_lw | (1u << RANK_BITS)));
         const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
@@ -1084,7 +1083,15 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
                 if (v2) ok2t[nR + (uint32_t)(k2 & 0xFF)] = (int32_t)ur2;
             }
         }
-        rotate(Hn);
+    };
+    for (uint32_t it = it0;;)
+    {
+        if (it >= n_items) break;
+        step(it, PA, PB);
+        it += nw;
+        if (it >= n_items) break;
+        step(it, PB, PA);
+        it += nw;
     }
     dflush();
     if (WIDE && PASS == 1 && nwide && lane == 0) atomicAdd(&b.ctl->n_wide1, (unsigned long long)nwide);
