@@ -1782,6 +1782,8 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
         b.p_slot = c->p_slot.as<uint32_t>();
     }
     if (const char* e = getenv("AD_K2_BIG")) b.k2_big = (uint32_t)strtoul(e, nullptr, 10);   // tests: force k_build_big
+    b.kb_sort = 16384;                                                                           // KB_LDS_CAP
+    if (const char* e = getenv("AD_KB_SORT")) b.kb_sort = (uint32_t)strtoul(e, nullptr, 10);   // tests: 0 = global scratch
     b.q_rec = c->q_rec.as<uint4>();
     b.deferred1 = c->deferred1.as<uint32_t>();
     b.deferred2 = c->deferred2.as<uint32_t>();

@@ -1261,9 +1261,20 @@ __device__ bool kb_region(KbLds& L, const BatchBufs& b, uint64_t bytes, uint64_t
     return fits;
 }
 
+// A heavy request's keyDeps / directKeyDeps of at most KB_LDS_CAP elements (over at most KB_LDS_LISTS lists) merge
+// in LDS: values, list starts and the kept-flag prefix held there, so the rank merge's binary searches (~8 lists x
+// ~12 probes per element, RelationMultiMap's dedup :147-260) read LDS instead of global scratch. (A block bitonic
+// sort of (value, element) in LDS measured no better: its ~80 barrier-separated stages cost about what the
+// searches through L2 did -- steady-state resolve 8.95 against 9.42 ms.)
+constexpr uint32_t KB_LDS_CAP = 16384;
+constexpr uint32_t KB_LDS_LISTS = 64;
+
 __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBufs b)
 {
     __shared__ KbLds L;
+    __shared__ uint32_t Vs[KB_LDS_CAP];
+    __shared__ uint32_t Ps[KB_LDS_CAP + 1];
+    __shared__ uint32_t Ss[KB_LDS_LISTS + 1];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
     const uint64_t n = b.n_txns;
     const uint64_t nbig = b.ctl->n_big;
@@ -1338,14 +1349,20 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
                 if (tid == 0) { b.sz[(3 * m) * n + t] = 0; b.sz[(3 * m + 1) * n + t] = 0; b.sz[(3 * m + 2) * n + t] = 0; }
                 continue;
             }
+            const bool lds = tot <= min(KB_LDS_CAP, b.kb_sort) && np <= KB_LDS_LISTS;
+            if (lds)
+                for (uint32_t i = tid; i <= np; i += KB_THREADS) Ss[i] = st[i];
             for (uint32_t e = tid; e < tot; e += KB_THREADS)
             {
                 const uint32_t a = list_of(st, np, e);
-                mem.V[e] = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
+                const uint32_t v = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
+                if (lds) Vs[e] = v;
+                else mem.V[e] = v;
             }
             __syncthreads();
             auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
-            const uint32_t U = block_rank_merge_kept(L, get, st, np, tot, mem.P);
+            auto getl = [&](uint32_t e) -> uint64_t { return Vs[e]; };
+            const uint32_t U = lds ? block_rank_merge_kept(L, getl, Ss, np, tot, Ps) : block_rank_merge_kept(L, get, st, np, tot, mem.P);
             if (wv == 0)
             {
                 uint32_t nk = 0;
@@ -1390,13 +1407,22 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
                         kr += __popcll(mk);
                     }
                 }
-                for (uint32_t e = tid; e < tot; e += KB_THREADS)
-                {
-                    const uint64_t x = mem.V[e];
-                    const uint32_t ur = rank_merge_urank(get, st, np, mem.P, x);
-                    if (mem.P[e + 1] - mem.P[e]) otx[ur] = dict_index((uint32_t)x);
-                    ok2t[nk + e] = (int32_t)ur;
-                }
+                if (lds)
+                    for (uint32_t e = tid; e < tot; e += KB_THREADS)
+                    {
+                        const uint64_t x = Vs[e];
+                        const uint32_t ur = rank_merge_urank(getl, Ss, np, Ps, x);
+                        if (Ps[e + 1] - Ps[e]) otx[ur] = dict_index((uint32_t)x);
+                        ok2t[nk + e] = (int32_t)ur;
+                    }
+                else
+                    for (uint32_t e = tid; e < tot; e += KB_THREADS)
+                    {
+                        const uint64_t x = mem.V[e];
+                        const uint32_t ur = rank_merge_urank(get, st, np, mem.P, x);
+                        if (mem.P[e + 1] - mem.P[e]) otx[ur] = dict_index((uint32_t)x);
+                        ok2t[nk + e] = (int32_t)ur;
+                    }
             }
             __syncthreads();
         }
