@@ -2403,6 +2403,7 @@ int ad_ctx_create(const ad_config* cfg, ad_ctx** out)
 void ad_ctx_destroy(ad_ctx* c)
 {
     if (!c) return;
+    kl_join(c);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->ev)
@@ -2909,8 +2910,11 @@ int ad_deps_batch_device(ad_ctx* c, const ad_query_soa* q, uint32_t flags, void*
     if (c->dirty && (rc = build_snapshot(c))) return rc;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     scope_.add(st);
+    host_trace("resolve: enter");
     // AD_REGIONS and AD_PARTS_ONLY: no packed copy (the regions are the result)
-    return run_pipeline(c, q, st, out, (flags & (AD_PARTS_ONLY | AD_REGIONS)) != 0, (flags & AD_N_KEYS) != 0);
+    rc = run_pipeline(c, q, st, out, (flags & (AD_PARTS_ONLY | AD_REGIONS)) != 0, (flags & AD_N_KEYS) != 0);
+    host_trace("resolve: done");
+    return rc;
 }
 
 void ad_result_free(ad_deps_result* r)

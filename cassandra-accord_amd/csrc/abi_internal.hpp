@@ -205,6 +205,11 @@ struct ad_ctx {
     std::vector<std::vector<int64_t>> kl_members;   // per bucket (built on first use from kl_keys_all)
     std::vector<int64_t> kl_keys_all;
     uint64_t kl_nb_h = 0;
+    // new keys of an update batch placed on a host thread while the batch runs on the device
+    // (cfk_keys_added); joined right after run_cfk_update, consumed by cfk_after_new_keys
+    std::thread kl_thread;
+    bool kl_async = false, kl_async_rebuild = false;
+    int kl_async_rc = 0;
     DevBuf d_keys2, d_krec2, d_kcell2, d_khash2, d_kent2;   // spare key-indexed arrays (new keys)
 
     // batch buffers
@@ -450,6 +455,8 @@ int cfk_dict_spare(void* vc, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t**
 int cfk_dict_swap(void* vc, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw);
 int cfk_keys_spare(void* vc, uint64_t nk, KeyBufs* b);
 int cfk_keys_swap(void* vc, KeyBufs* b);
+void cfk_keys_added(void* vc, const int64_t* keys, uint64_t n, uint64_t nk, hipStream_t st);
+void kl_join(ad_ctx* c);
 int cfk_miss_spare(void* vc, uint64_t n, uint64_t n_ids, uint64_t** off, uint32_t** ids);
 int cfk_miss_swap(void* vc, uint64_t** off, uint32_t** ids);
 int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_applied, ad_stats* stats);

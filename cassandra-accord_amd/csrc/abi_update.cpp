@@ -8,8 +8,9 @@ namespace adi {
 int cfk_need_bufs(void* vc, uint64_t n_cand, uint64_t n_cwr, uint64_t n_w, CfkDerivedBufs* b)
 {
     ad_ctx* c = (ad_ctx*)vc;
-    if (!c->d_cand.ensure(4 * std::max<uint64_t>(n_cand, 1)) || !c->d_cwr.ensure(4 * std::max<uint64_t>(n_cwr, 1)) ||
-        !c->d_w.ensure(8 * std::max<uint64_t>(n_w, 1)))
+    // (with slack: the store grows every batch -- an exact-size buffer would be reallocated by each one)
+    if (!c->d_cand.grow(4 * std::max<uint64_t>(n_cand, 1)) || !c->d_cwr.grow(4 * std::max<uint64_t>(n_cwr, 1)) ||
+        !c->d_w.grow(8 * std::max<uint64_t>(n_w, 1)))
         return AD_E_NOMEM;
     b->cand = c->d_cand.as<uint32_t>();
     b->cwr = c->d_cwr.as<uint32_t>();
@@ -100,7 +101,7 @@ int size_cfk_trees(ad_ctx* c, uint64_t ne)
     for (int l = 1; l < L; ++l)
         for (int cl = 0; cl < NCLASS; ++cl)
         {
-            if (!c->d_lvl[cl][l].ensure(sizeof(uint32_t) * ((s.lvl_n[l] + 63) / 64 * 64))) return AD_E_NOMEM;
+            if (!c->d_lvl[cl][l].grow(sizeof(uint32_t) * ((s.lvl_n[l] + 63) / 64 * 64))) return AD_E_NOMEM;
             s.lvl[cl][l] = c->d_lvl[cl][l].as<uint32_t>();
         }
     return 0;
@@ -139,10 +140,8 @@ int cfk_keys_spare(void* vc, uint64_t nk, KeyBufs* b)
     ad_ctx* c = (ad_ctx*)vc;
     uint64_t hcap = 16;
     while (hcap < 2 * nk) hcap <<= 1;
-    const uint64_t slack = nk / 8;
-    if (!c->d_keys2.ensure(8 * (nk + slack)) || !c->d_krec2.ensure(sizeof(KeyRec) * (nk + slack)) ||
-        !c->d_kcell2.ensure(4 * (nk + slack)) || !c->d_khash2.ensure(sizeof(KeySlot) * hcap) ||
-        !c->d_kent2.ensure(sizeof(KeyEntry) * (nk + slack)))
+    if (!c->d_keys2.grow(8 * nk) || !c->d_krec2.grow(sizeof(KeyRec) * nk) || !c->d_kcell2.grow(4 * nk) ||
+        !c->d_khash2.ensure(sizeof(KeySlot) * hcap) || !c->d_kent2.grow(sizeof(KeyEntry) * nk))
         return AD_E_NOMEM;
     *b = KeyBufs{c->d_keys2.as<int64_t>(), c->d_krec2.as<KeyRec>(), c->d_kcell2.as<uint32_t>(), c->d_khash2.as<KeySlot>(),
                  c->d_kent2.as<KeyEntry>(), hcap};
@@ -165,16 +164,60 @@ int cfk_keys_swap(void* vc, KeyBufs* b)
     return 0;
 }
 
-// After new keys on the device: the KeyLine perfect hash takes them (incrementally on the host),
-// displacements uploaded, every key's line recomputed on the device.
+// The batch's new keys, as soon as add_keys has them: placed in the KeyLine hash on a host thread while
+// the rest of the batch runs on the device (the placement is host work of ~0.1 ms per 1000 keys). Nothing
+// else touches the KeyLine host state until kl_join.
+void cfk_keys_added(void* vc, const int64_t* keys, uint64_t n, uint64_t nk, hipStream_t st)
+{
+    ad_ctx* c = (ad_ctx*)vc;
+    kl_join(c);
+    c->kl_async = false;
+    if (!n) return;
+    std::vector<int64_t> nkeys(n);
+    if (d2h(nkeys.data(), keys, 8 * n, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) return;   // later, synchronously
+    c->kl_async = true;
+    c->kl_async_rc = 0;
+    c->kl_async_rebuild = false;
+    try
+    {
+        c->kl_thread = std::thread([c, nkeys = std::move(nkeys), nk]() {
+            bool rebuild = false;
+            c->kl_async_rc = kl_add_keys(c, nkeys, nk, &rebuild);
+            c->kl_async_rebuild = rebuild;
+        });
+    }
+    catch (...)
+    {
+        c->kl_async = false;
+    }
+}
+
+void kl_join(ad_ctx* c)
+{
+    if (c->kl_thread.joinable()) c->kl_thread.join();
+}
+
+// After new keys on the device: the KeyLine perfect hash takes them (incrementally on the host -- already
+// done by cfk_keys_added's thread when it ran), displacements uploaded, every key's line recomputed on the device.
 int cfk_after_new_keys(ad_ctx* c, const CfkUpdOut& o, hipStream_t st)
 {
     const uint64_t nk = c->ds.n_keys, U = o.n_new_keys;
-    std::vector<int64_t> nkeys(U);
-    HIPCHK(c, d2h(nkeys.data(), o.new_keys, 8 * U, st));
-    HIPCHK(c, hipStreamSynchronize(st));
     bool rebuild = false;
-    if (int rc = kl_add_keys(c, nkeys, nk, &rebuild)) return rc;
+    kl_join(c);
+    if (c->kl_async)
+    {
+        c->kl_async = false;
+        if (c->kl_async_rc) return c->kl_async_rc;
+        rebuild = c->kl_async_rebuild;
+    }
+    else
+    {
+        std::vector<int64_t> nkeys(U);
+        HIPCHK(c, d2h(nkeys.data(), o.new_keys, 8 * U, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (int rc = kl_add_keys(c, nkeys, nk, &rebuild)) return rc;
+    }
+    host_trace("new_keys: kl_add_keys (joined)");
     if (rebuild)
     {
         // the whole table again, half full (every key of the store, from the device)
@@ -183,7 +226,8 @@ int cfk_after_new_keys(ad_ctx* c, const CfkUpdOut& o, hipStream_t st)
         if (int rc = kl_place_all(c, all, std::max<uint64_t>(1, nk / 4), true)) return c->fail(rc, "key perfect hash did not converge");
     }
     if (int rc = upload(c, c->d_kl_disp, c->kl_disp_h)) return rc;
-    if (!c->d_kslot.ensure(4 * nk + 4 * (nk / 8))) return c->fail(AD_E_NOMEM, "key slots");
+    host_trace("new_keys: disp upload");
+    if (!c->d_kslot.grow(4 * nk)) return c->fail(AD_E_NOMEM, "key slots");
     if (!c->d_kline.ensure(kline_table_bytes(c->kline_slots))) return c->fail(AD_E_NOMEM, "key lines");
     DevSnapshot& s = c->ds;
     s.kline = c->d_kline.as<KeyLine>();
@@ -199,8 +243,8 @@ int cfk_after_new_keys(ad_ctx* c, const CfkUpdOut& o, hipStream_t st)
 int cfk_dict_spare(void* vc, uint64_t n, uint64_t** hi, uint64_t** lo, int32_t** node, uint64_t** raw)
 {
     ad_ctx* c = (ad_ctx*)vc;
-    if (!c->d_dict_hi2.ensure(8 * n + 8 * (n / 8)) || !c->d_dict_lo2.ensure(8 * n + 8 * (n / 8)) ||
-        !c->d_dict_node2.ensure(4 * n + 4 * (n / 8)) || !c->d_dict_raw2.ensure(8 * n + 8 * (n / 8)))
+    if (!c->d_dict_hi2.grow(8 * n) || !c->d_dict_lo2.grow(8 * n) || !c->d_dict_node2.grow(4 * n) ||
+        !c->d_dict_raw2.grow(8 * n))
         return AD_E_NOMEM;
     *hi = c->d_dict_hi2.as<uint64_t>();
     *lo = c->d_dict_lo2.as<uint64_t>();
@@ -264,7 +308,7 @@ int cfk_after_merge(ad_ctx* c, const uint64_t* pos_dev, uint64_t U, hipStream_t 
 int cfk_miss_spare(void* vc, uint64_t n, uint64_t n_ids, uint64_t** off, uint32_t** ids)
 {
     ad_ctx* c = (ad_ctx*)vc;
-    if (!c->d_moff2.ensure(8 * (n + 1) + 8 * (n / 8)) || !c->d_mids2.ensure(4 * std::max<uint64_t>(n_ids, 1) + 4 * (n_ids / 8)))
+    if (!c->d_moff2.grow(8 * (n + 1)) || !c->d_mids2.grow(4 * std::max<uint64_t>(n_ids, 1)))
         return AD_E_NOMEM;
     *off = c->d_moff2.as<uint64_t>();
     *ids = c->d_mids2.as<uint32_t>();
@@ -332,6 +376,7 @@ int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_app
 {
     StreamScope scope_(st, c->stream, c->cstream);
     c->upd_applied = false;
+    host_trace("upd: enter");
     c->upd_failed = -1;
     if (c->dirty)
         if (int rc = build_snapshot(c)) return rc;
@@ -361,9 +406,10 @@ int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_app
                        c->d_rtxw.as<uint32_t>(), c->ds.n_rent, c->d_cell_ent.as<uint64_t>(), c->ds.cell_ent ? c->n_cell_ent : 0,
                        c->d_rb_wm.as<uint32_t>(), c->ds.n_rb, c->dmiss_on ? c->d_mids.as<uint32_t>() : nullptr,
                        c->dmiss_on ? c->dmiss_ids : 0, cfk_keys_spare, cfk_keys_swap,
-                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr};
+                       c->d_kcell.p ? c->d_kcell.as<uint32_t>() : nullptr, cfk_keys_added};
     if (int rc = host_dict(c)) return rc;
     CfkMiss miss;
+    host_trace("upd: host_dict");
     miss.on = c->dmiss_on && u.dep_off;
     miss.n_lists = c->dmiss_lists;
     miss.off = c->d_moff.as<uint64_t>();
@@ -373,11 +419,16 @@ int cfk_update_run(ad_ctx* c, const CfkUpdIn& u, hipStream_t st, uint64_t* n_app
     miss.swap = cfk_miss_swap;
     c->lp_upd.clear(); c->lp_keys.clear(); c->lp_msb.clear(); c->lp_lsb.clear(); c->lp_node.clear();
     const int rc = run_cfk_update(c->cu, c->ds, d, u, &b, cfk_need_bufs, c, grow, st, &o, &e, &miss);
+    kl_join(c);
+    if (!o.n_new_keys) c->kl_async = false;
+    host_trace("upd: run_cfk_update");
     // what the batch left is known here, before any follow-up copy can fail: a caller reading the status after
     // an error must never take a batch that stands for one that did not (and apply it twice)
     c->upd_applied = rc == AD_OK || o.batch_stood;
     c->upd_failed = o.failed_update;
-    if (const int frc = cfk_update_follow(c, o, rc, st))
+    const int frc = cfk_update_follow(c, o, rc, st);
+    c->kl_async = false;        // consumed by the follow-up, or dropped with it (a failed one leaves the store dirty)
+    if (frc)
     {
         // the host copies and the derived arrays may be half refreshed: rebuilt from the entries at the next use
         c->host_stale = true;
@@ -447,6 +498,7 @@ int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st)
     {
         // keys created on the device (they stay when the batch then failed): KeyLines, host copies
         if (int rc2 = cfk_after_new_keys(c, o, st)) return rc2;
+    host_trace("follow: after_new_keys");
         c->host_moved = true;
         c->host_ingested = false;     // entries moved after the ingest
         c->host_stale = true;
@@ -476,25 +528,27 @@ int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st)
             HIPCHK(c, copy_sync(c->dict_msb.data() + nd1, c->d_dict_hi.as<uint64_t>() + nd1, 8 * add, hipMemcpyDeviceToHost));
             HIPCHK(c, copy_sync(c->dict_lsb.data() + nd1, c->d_dict_lsb_raw.as<uint64_t>() + nd1, 8 * add, hipMemcpyDeviceToHost));
             HIPCHK(c, copy_sync(c->dict_node.data() + nd1, c->d_dict_node.as<int32_t>() + nd1, 4 * add, hipMemcpyDeviceToHost));
+    host_trace("follow: dict append copy");
         }
         drop_global_dict(c);         // global ranks of the multi-store exchange no longer cover the dictionary
         // the sampled index over the grown dictionary (a stale one is still correct, only slower)
         // (a buffer that could not grow may have been released: then no sample, the searches span the
         // whole dictionary)
         const uint64_t ns = dict_samples(c->ds.n_dict), ne = dict_sample_entries(c->ds.n_dict);
-        const bool ok = c->d_ds_hi.ensure(8 * ne + 8 * ne / 4) && c->d_ds_lo.ensure(8 * ne + 8 * ne / 4) &&
-                        c->d_ds_node.ensure(4 * ne + 4 * ne / 4);
+        const bool ok = c->d_ds_hi.grow(8 * ne) && c->d_ds_lo.grow(8 * ne) && c->d_ds_node.grow(4 * ne);
         c->ds.ds_hi = c->d_ds_hi.as<uint64_t>();
         c->ds.ds_lo = c->d_ds_lo.as<uint64_t>();
         c->ds.ds_node = c->d_ds_node.as<int32_t>();
         c->ds.n_samp = ok ? ns : 0;
         c->ds.n_samp2 = ok ? dict_samples2(c->ds.n_dict) : 0;
         if (ok) HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
+    host_trace("follow: dict sample");
     }
     if (o.n_inserted) { c->host_moved = true; c->host_ingested = false; }
     if ((rc == 0 || o.rolled_back || o.rederived || o.batch_stood) && c->kline_slots)
         HIPCHK(c, run_build_klines(c->ds, c->d_kslot.as<uint32_t>(), c->d_kcell.as<uint32_t>(), c->d_kline.as<KeyLine>(),
                                    c->kline_slots, st));
+    host_trace("follow: klines");
     return 0;
 }
 

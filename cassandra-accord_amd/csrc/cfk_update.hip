@@ -1512,6 +1512,7 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
     UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t n_cand = w->h_ctl->tot[0] + w->h_ctl->tot[1] + w->h_ctl->tot[2], ncm = w->h_ctl->tot[3];
+    host_trace("derive: totals sync");
     const uint64_t nA = inc ? w->h_ctl->cm[0] : 0, nB = inc ? w->h_ctl->cm[1] : 0;
     const bool use_inc = inc && nA + nB == ncm;     // else (never expected) the full sort
     int rc = need(need_ctx, n_cand, ncm, ncm, bufs);
@@ -1598,6 +1599,7 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
     s.cwr = bufs->cwr;
     s.w = bufs->w;
     UCHK(build_cfk_trees(s, st));
+    host_trace("derive: queued");
     return AD_OK;
 }
 
@@ -1625,6 +1627,7 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
     UCHK(hipStreamSynchronize(st));
     const uint64_t m = w->h_ctl->n_newk;
     if (m == 0) return AD_OK;
+    host_trace("add_keys: collect sync");
     UALLOC(w->kn_b, 8 * m, false);
     UALLOC(w->kv_a, 4 * m, false);
     UALLOC(w->kv_b, 4 * m, false);
@@ -1646,6 +1649,7 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
     UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
     const uint64_t U = w->h_ctl->tot3[0];
+    host_trace("add_keys: sort+unique sync");
     if (nk + U >= KEY_EMPTY) { *err = "more than 2^32-1 keys"; return AD_E_CAPACITY; }
     UALLOC(w->knew, 8 * U, false);
     UALLOC(w->kpos, 8 * U, false);
@@ -1653,6 +1657,7 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
                                            w->kpos.as<uint64_t>());
     KeyBufs nb{};
     if (int rc = grow.keys_spare(grow.ctx, nk + U, &nb)) { *err = "key arrays"; return rc; }
+    host_trace("add_keys: keys_spare");
     const uint64_t* kpos = w->kpos.as<uint64_t>();
     if (nk) k_key_move<<<blocks(nk), 256, 0, st>>>(s, grow.kcell, kpos, U, nb);
     k_key_new<<<blocks(U), 256, 0, st>>>(s, w->knew.as<int64_t>(), kpos, U, nb);
@@ -1662,6 +1667,8 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
     UCHK(hipGetLastError());
     if (int rc = grow.keys_swap(grow.ctx, &nb)) { *err = "key arrays"; return rc; }
     UCHK(hipStreamSynchronize(st));
+    host_trace("add_keys: move+swap sync");
+    if (grow.keys_added) grow.keys_added(grow.ctx, w->knew.as<int64_t>(), U, nk + U, st);
     s.n_keys = nk + U;
     s.keys = nb.keys;
     s.krec = nb.krec;
@@ -1984,6 +1991,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
         return code;
     };
     if (int rc = add_keys(w, s, d, u, grow, st, out, err)) return rc == AD_E_CAPACITY ? rc : rederive(rc);
+    host_trace("upd: add_keys");
     if (out->n_new_keys) UCHK(hipMemsetAsync(ctl, 0, sizeof(UpdCtl), st));
     {
         const DictSample ds0 = sample();
@@ -2096,6 +2104,7 @@ int run_cfk_update(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdIn
     UCHK(hipEventRecord(w->ev[2], st));
     UCHK(d2h(w->h_ctl, ctl, sizeof(UpdCtl), st));
     UCHK(hipStreamSynchronize(st));
+    host_trace("upd: derive sync");
     float a = 0, b = 0;
     (void)hipEventElapsedTime(&a, w->ev[0], w->ev[1]);
     (void)hipEventElapsedTime(&b, w->ev[1], w->ev[2]);

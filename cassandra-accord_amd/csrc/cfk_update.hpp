@@ -91,6 +91,9 @@ struct CfkGrow {
     int (*keys_spare)(void* ctx, uint64_t nk, KeyBufs* b);
     int (*keys_swap)(void* ctx, KeyBufs* b);
     const uint32_t* kcell;
+    // optional: the batch's n new keys (device, complete on `st` when called) as soon as they are known, nk
+    // keys in all -- the host may start placing them in the KeyLine hash while the batch runs on the device
+    void (*keys_added)(void* ctx, const int64_t* keys, uint64_t n, uint64_t nk, hipStream_t st);
 };
 
 // TxnInfo.missing() lists on the device (CommandsForKey.java:332-341): list j = ids

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -474,5 +475,15 @@ void host_parallel(size_t n, const std::function<void(size_t)>& f)
 }
 
 unsigned host_threads() { return host_pool().workers + 1; }
+
+void host_trace(const char* what)
+{
+    static const bool on = getenv("AD_HOST_TRACE") != nullptr;
+    if (!on) return;
+    static thread_local std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "[ht] %9.3f ms  %s\n", std::chrono::duration<double, std::milli>(now - last).count(), what);
+    last = now;
+}
 
 }  // namespace adx

@@ -51,6 +51,9 @@ unsigned host_threads();
 // damaged guard bands among the live allocations (and the ones freed since the last call); a
 // description of each is appended to *report
 int dev_guard_check(std::string* report);
+// AD_HOST_TRACE=1 (read once): host_trace(what) prints, to stderr, the host time since the previous
+// host_trace on this thread -- where a call's host-side work goes between its kernels
+void host_trace(const char* what);
 
 // the streams whose queued work may touch the buffers a call frees (innermost scope wins)
 struct StreamScope {
