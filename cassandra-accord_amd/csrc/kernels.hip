@@ -1784,13 +1784,120 @@ __global__ __launch_bounds__(LB_TILE) void k_pack_tiles(BatchBufs b, int copy)
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// The copy of a batch of few, heavy requests (BatchBufs.pack_even): k_pack_tiles's one wave per 64
+// requests leaves most of the chip idle when a batch has a few thousand requests of thousands of pairs
+// each (the steady state: 16384 requests, 56M pairs, 256 waves). Here the packed output of array a
+// (blockIdx.y) is cut into chunks of PE_CHUNK elements, a workgroup per chunk (grid-stride): the
+// chunk's requests (found by two binary searches of off[a]) in windows of PE_WIN held in LDS, each
+// element's request found in the window by a binary search from the thread's previous one.
+// ---------------------------------------------------------------------------------------
+constexpr uint32_t PE_THREADS = 256, PE_CHUNK = 8192, PE_WIN = 1024, PE_UNROLL = 4;
+
+__device__ __forceinline__ uint64_t last_le(const uint64_t* __restrict__ off, uint64_t n1, uint64_t p)
+{
+    // the last r in [0, n1) with off[r] <= p (off ascending, off[0] <= p)
+    uint64_t lo = 0, hi = n1;
+    while (hi - lo > 1)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (off[mid] <= p) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <class T>
+__device__ __forceinline__ void pack_even_array(const BatchBufs& b, int a, T* __restrict__ out, uint64_t* s_off,
+                                                uint64_t* s_src, uint64_t* s_r)
+{
+    const uint64_t n = b.n_txns;
+    const uint32_t tid = threadIdx.x;
+    const int m = a / 3, k = a % 3;
+    const uint64_t* __restrict__ off = b.off + (uint64_t)a * (n + 1);
+    const uint64_t total = off[n];
+    if (total == 0) return;
+    if (total > b.o_cap[a])
+    {
+        if (blockIdx.x == 0 && tid == 0) atomicOr(&b.ctl->overflow, OVF_PACK);
+        return;
+    }
+    for (uint64_t p0 = (uint64_t)blockIdx.x * PE_CHUNK; p0 < total; p0 += (uint64_t)gridDim.x * PE_CHUNK)
+    {
+        const uint64_t p1 = p0 + PE_CHUNK < total ? p0 + PE_CHUNK : total;
+        if (tid == 0) s_r[0] = last_le(off, n + 1, p0);
+        if (tid == 64) s_r[1] = last_le(off, n + 1, p1 - 1);
+        __syncthreads();
+        const uint64_t r0 = s_r[0], r1 = s_r[1];
+        for (uint64_t ra = r0; ra <= r1; ra += PE_WIN)
+        {
+            const uint32_t wn = (uint32_t)((r1 - ra + 1) < PE_WIN ? (r1 - ra + 1) : PE_WIN);
+            __syncthreads();                        // the previous window (and s_r) read by every thread
+            for (uint32_t i = tid; i <= wn; i += PE_THREADS) s_off[i] = off[ra + i];
+            for (uint32_t i = tid; i < wn; i += PE_THREADS)
+            {
+                const uint64_t r = ra + i;
+                uint64_t src = b.t_reg[(uint64_t)m * n + r];
+                if (k) src += 8ull * b.sz[(uint64_t)(3 * m) * n + r];
+                if (k == 2) src += 4ull * b.sz[(uint64_t)(3 * m + 1) * n + r];
+                s_src[i] = src;
+            }
+            __syncthreads();
+            const uint64_t q0 = p0 > s_off[0] ? p0 : s_off[0], q1 = p1 < s_off[wn] ? p1 : s_off[wn];
+            uint32_t lo = 0;
+            for (uint64_t base = q0 + tid; base < q1; base += PE_UNROLL * PE_THREADS)
+            {
+                T v[PE_UNROLL];
+#pragma unroll
+                for (uint32_t u = 0; u < PE_UNROLL; ++u)
+                {
+                    const uint64_t p = base + (uint64_t)u * PE_THREADS;
+                    if (p < q1)
+                    {
+                        uint32_t hi = wn;
+                        while (hi - lo > 1)
+                        {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (s_off[mid] <= p) lo = mid;
+                            else hi = mid;
+                        }
+                        v[u] = reinterpret_cast<const T*>(b.reg + s_src[lo])[p - s_off[lo]];
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < PE_UNROLL; ++u)
+                {
+                    const uint64_t p = base + (uint64_t)u * PE_THREADS;
+                    if (p < q1) out[p] = v[u];
+                }
+            }
+        }
+        __syncthreads();                            // s_r rewritten by the next chunk
+    }
+}
+
+__global__ __launch_bounds__(PE_THREADS) void k_pack_even(BatchBufs b)
+{
+    __shared__ uint64_t s_off[PE_WIN + 1];
+    __shared__ uint64_t s_src[PE_WIN];
+    __shared__ uint64_t s_r[2];
+    const BatchCtl* cc = b.ctl;
+    if (cc->n_deferred || cc->error || (cc->overflow & 15u)) return;
+    const int a = blockIdx.y, m = a / 3;
+    if (a % 3 == 0) pack_even_array<int64_t>(b, a, b.o_keys[m], s_off, s_src, s_r);
+    else if (a % 3 == 1) pack_even_array<uint32_t>(b, a, b.o_txns[m], s_off, s_src, s_r);
+    else pack_even_array<int32_t>(b, a, b.o_k2t[m], s_off, s_src, s_r);
+}
+
 hipError_t run_pack_lb(const BatchBufs& b, bool copy, hipStream_t st)
 {
     if (!b.n_txns) return hipMemsetAsync(b.off, 0, sizeof(uint64_t) * 9, st);     // off[a][0] = 0
     const uint64_t tiles = lb_tiles(b.n_txns);
     k_tile_sums<<<(unsigned)tiles, LB_TILE, 0, st>>>(b);
     k_tile_scan<<<9, 1024, 0, st>>>(b, tiles);
-    k_pack_tiles<<<(unsigned)tiles, LB_TILE, 0, st>>>(b, copy ? 1 : 0);
+    const bool even = copy && b.pack_even;
+    k_pack_tiles<<<(unsigned)tiles, LB_TILE, 0, st>>>(b, copy && !even ? 1 : 0);
+    if (even) k_pack_even<<<dim3(512, 9), PE_THREADS, 0, st>>>(b);
     return hipGetLastError();
 }
 

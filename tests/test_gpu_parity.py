@@ -54,6 +54,25 @@ def test_big_requests_regions(oracle, big, monkeypatch):
     assert ok, why
 
 
+@pytest.mark.parametrize("even", ["0", "1"])
+@pytest.mark.parametrize("case", ["heavy", "light", "mixed"])
+def test_pack_copy_paths(oracle, even, case, monkeypatch):
+    # the packed copy by k_pack_tiles (a wave per 64 requests) or k_pack_even (chunks of the output, the
+    # chunk's requests in LDS windows of 1024: "light" has chunks spanning several windows, "heavy" requests
+    # spanning several chunks)
+    monkeypatch.setenv("AD_PACK_EVEN", even)
+    if case == "heavy":
+        w = synth.config2(n_txns=300, n_keys=40, n_hist_entries=60000, keys_per_txn=8, tail_unapplied=8000)
+    elif case == "light":
+        w = synth.random_small(3100, n_keys=900, n_hist_txns=300, n_txns=6000, max_keys=2)
+    else:
+        w = synth.random_small(3101, n_keys=300, n_hist_txns=4000, n_txns=3000, max_keys=6, n_range_cmds=40)
+    _compare(w, oracle, paths=(0,))
+    got = native.resolve(w, via="device")
+    ok, why = got.equals(oracle.resolve(w), detail=True)
+    assert ok, why
+
+
 @pytest.mark.parametrize("n_hist", [7, 15, 16, 17, 120, 255, 256, 257, 511, 4097])
 def test_dictionary_sample_windows(oracle, n_hist):
     # rank searches through the two-level dictionary sample (common.hpp dict_rank_sampled: every 256th
