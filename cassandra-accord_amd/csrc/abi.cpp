@@ -1784,6 +1784,8 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
     if (const char* e = getenv("AD_K2_BIG")) b.k2_big = (uint32_t)strtoul(e, nullptr, 10);   // tests: force k_build_big
     b.kb_sort = 16384;                                                                           // KB_LDS_CAP
     if (const char* e = getenv("AD_KB_SORT")) b.kb_sort = (uint32_t)strtoul(e, nullptr, 10);   // tests: 0 = global scratch
+    b.kb_merge = 1;
+    if (const char* e = getenv("AD_KB_MERGE")) b.kb_merge = (uint32_t)strtoul(e, nullptr, 10);
     // the pack copy spread over the whole output when the batch has too few requests to fill the chip with
     // k_pack_tiles's wave per 64 requests (tests: AD_PACK_EVEN=0/1 forces either)
     b.pack_even = n <= 131072;

@@ -1269,10 +1269,67 @@ __device__ bool kb_region(KbLds& L, const BatchBufs& b, uint64_t bytes, uint64_t
 constexpr uint32_t KB_LDS_CAP = 16384;
 constexpr uint32_t KB_LDS_LISTS = 64;
 
+// The LDS merge as a merge tree (BatchBufs.kb_merge): the np sorted lists of X (starts S) merged pairwise,
+// ceil(log2 np) levels ping-ponging between X and Y -- an element's place in the merged run is its place
+// in its own run plus its co-rank in the partner run (one binary search per level: strictly-less counts for
+// the left run's elements, less-or-equal for the right run's, so equal values keep list order) -- instead
+// of the rank merge's searches in every list (~1.5 np searches per element). Then the unique flags of the
+// sorted run and their exclusive prefix (Y): an element's unique rank is the prefix at the first occurrence
+// of its value. Returns the sorted array (X or Y); *pre the prefix array (the other one), total unique.
+__device__ uint32_t block_merge_tree(KbLds& L, uint32_t* X, uint32_t* Y, const uint32_t* S, uint32_t np, uint32_t tot,
+                                     uint32_t** sorted, uint32_t** pre)
+{
+    for (uint32_t l = 0; (1u << l) < np; ++l)
+    {
+        for (uint32_t e = threadIdx.x; e < tot; e += KB_THREADS)
+        {
+            const uint32_t a = list_of(S, np, e);
+            const uint32_t run = a >> l;
+            const uint32_t la = (run & ~1u) << l;
+            const uint32_t sA = S[la];
+            const uint32_t sB = S[min(la + (1u << l), np)], eB = S[min(la + (2u << l), np)];
+            const uint32_t x = X[e];
+            uint32_t d;
+            if (!(run & 1u))
+            {
+                uint32_t lo = sB, hi = eB;           // B elements < x
+                while (lo < hi)
+                {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (X[mid] < x) lo = mid + 1;
+                    else hi = mid;
+                }
+                d = e + (lo - sB);
+            }
+            else
+            {
+                uint32_t lo = sA, hi = sB;           // A elements <= x
+                while (lo < hi)
+                {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (X[mid] <= x) lo = mid + 1;
+                    else hi = mid;
+                }
+                d = sA + (e - sB) + (lo - sA);
+            }
+            Y[d] = x;
+        }
+        __syncthreads();
+        uint32_t* t = X;
+        X = Y;
+        Y = t;
+    }
+    const uint32_t* Xc = X;
+    const uint32_t U = block_scan_into(L, tot, [&](uint32_t i) { return (i == 0 || Xc[i] != Xc[i - 1]) ? 1u : 0u; }, Y);
+    *sorted = X;
+    *pre = Y;
+    return U;
+}
+
 __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBufs b)
 {
     __shared__ KbLds L;
-    __shared__ uint32_t Vs[KB_LDS_CAP];
+    __shared__ uint32_t Vs[KB_LDS_CAP + 1];      // (+1: the merge tree may leave its prefix here)
     __shared__ uint32_t Ps[KB_LDS_CAP + 1];
     __shared__ uint32_t Ss[KB_LDS_LISTS + 1];
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
@@ -1352,17 +1409,26 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
             const bool lds = tot <= min(KB_LDS_CAP, b.kb_sort) && np <= KB_LDS_LISTS;
             if (lds)
                 for (uint32_t i = tid; i <= np; i += KB_THREADS) Ss[i] = st[i];
+            // (the merge tree in global scratch: the u32 values in V's and UP's room, 2 cap words each)
+            const bool tree = b.kb_merge;
+            uint32_t* gX = reinterpret_cast<uint32_t*>(mem.V);
             for (uint32_t e = tid; e < tot; e += KB_THREADS)
             {
                 const uint32_t a = list_of(st, np, e);
                 const uint32_t v = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
                 if (lds) Vs[e] = v;
+                else if (tree) gX[e] = v;
                 else mem.V[e] = v;
             }
             __syncthreads();
             auto get = [&](uint32_t e) -> uint64_t { return mem.V[e]; };
             auto getl = [&](uint32_t e) -> uint64_t { return Vs[e]; };
-            const uint32_t U = lds ? block_rank_merge_kept(L, getl, Ss, np, tot, Ps) : block_rank_merge_kept(L, get, st, np, tot, mem.P);
+            uint32_t *Xs = Vs, *Xp = Ps;
+            const uint32_t U = tree  ? (lds ? block_merge_tree(L, Vs, Ps, Ss, np, tot, &Xs, &Xp)
+                                            : block_merge_tree(L, gX, reinterpret_cast<uint32_t*>(mem.UP), st, np, tot, &Xs, &Xp))
+                               : lds ? block_rank_merge_kept(L, getl, Ss, np, tot, Ps)
+                                     : block_rank_merge_kept(L, get, st, np, tot, mem.P);
+            const uint32_t* Sx = lds ? Ss : st;
             if (wv == 0)
             {
                 uint32_t nk = 0;
@@ -1407,7 +1473,27 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
                         kr += __popcll(mk);
                     }
                 }
-                if (lds)
+                if (tree)
+                {
+                    // the unique values in order, then every element's unique rank: its value (gathered again, in list
+                    // order) found in the sorted run, the prefix there
+                    for (uint32_t i = tid; i < tot; i += KB_THREADS)
+                        if (i == 0 || Xs[i] != Xs[i - 1]) otx[Xp[i]] = dict_index(Xs[i]);
+                    for (uint32_t e = tid; e < tot; e += KB_THREADS)
+                    {
+                        const uint32_t a = list_of(Sx, np, e);
+                        const uint32_t x = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - Sx[a])];
+                        uint32_t lo = 0, hi = tot;
+                        while (lo < hi)
+                        {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (Xs[mid] < x) lo = mid + 1;
+                            else hi = mid;
+                        }
+                        ok2t[nk + e] = (int32_t)Xp[lo];
+                    }
+                }
+                else if (lds)
                     for (uint32_t e = tid; e < tot; e += KB_THREADS)
                     {
                         const uint64_t x = Vs[e];

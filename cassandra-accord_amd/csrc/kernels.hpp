@@ -66,6 +66,7 @@ struct BatchBufs {
     uint32_t* big;                   // [n_txns] requests k_build hands to k_build_big (one workgroup each)
     uint32_t k2_big;                 // list-family size from which it does (K2_BIG; tests lower it)
     uint32_t kb_sort;                // k_build_big merges a map in LDS up to this many elements (tests: 0 = never)
+    uint32_t kb_merge;               // k_build_big's LDS merge as a merge tree (else the rank merge; tests: AD_KB_MERGE)
     uint32_t pack_even;              // pack copy: k_pack_even (few heavy requests) instead of k_pack_tiles's waves
     uint32_t* deferred1;             // requests deferred by lean pass 1 (+ chunk holes)
     uint32_t* deferred2;             // requests deferred by lean pass 2 (+ chunk holes)

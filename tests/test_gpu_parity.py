@@ -224,14 +224,16 @@ def test_big_requests(oracle):
     assert got.stats["n_deferred"] > 0          # exercised the fused -> split hand-off
 
 
-@pytest.mark.parametrize("sort", ["8192", "0"])
+@pytest.mark.parametrize("sort", ["8192", "8192/rank", "0", "0/rank"])
 @pytest.mark.parametrize("big", ["0", "64", "512"])
 def test_big_requests_workgroup_build(oracle, big, sort, monkeypatch):
     # k_build_big (one 1024-thread workgroup per heavy request): every request (0), the medium ones
     # (64) or the default threshold, on hot keys with thousands of live entries, range commands and
     # RedundantBefore in the mix
     monkeypatch.setenv("AD_K2_BIG", big)
-    monkeypatch.setenv("AD_KB_SORT", sort)       # its maps merged in LDS (default) or in global scratch
+    # its maps merged in LDS (by the merge tree, or the rank merge) or in global scratch
+    monkeypatch.setenv("AD_KB_SORT", sort.split("/")[0])
+    monkeypatch.setenv("AD_KB_MERGE", "0" if sort.endswith("/rank") else "1")
     w = synth.config2(n_txns=200, n_keys=50, n_hist_entries=40000, keys_per_txn=8, tail_unapplied=3000,
                       esp_frac=0.2)
     _compare(w, oracle)
