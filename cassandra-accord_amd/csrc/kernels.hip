@@ -1332,6 +1332,7 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
     __shared__ uint32_t Vs[KB_LDS_CAP + 1];      // (+1: the merge tree may leave its prefix here)
     __shared__ uint32_t Ps[KB_LDS_CAP + 1];
     __shared__ uint32_t Ss[KB_LDS_LISTS + 1];
+    __shared__ uint32_t So[KB_LDS_LISTS];           // the lists' arena offsets for this class (np <= KB_LDS_LISTS)
     const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
     const uint64_t n = b.n_txns;
     const uint64_t nbig = b.ctl->n_big;
@@ -1342,9 +1343,64 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
         const uint64_t t = b.big[bi];
         const uint64_t p0 = b.q_key_off[t];
         const uint32_t np = (uint32_t)(b.q_key_off[t + 1] - p0);
-        if (tid < 3) L.red[tid] = 0;
-        __syncthreads();
+        // per-probe metadata and list starts: one wave when the request has at most 64 probes (the usual <= 8 keys:
+        // register scans, one barrier, no global round trip), else block-wide reduces and scans
+        const bool few = np <= 64;
+        if (few)
         {
+            if (wv == 0)
+            {
+                const bool on = lane < np;
+                const uint64_t pi = p0 + lane;
+                const uint32_t c0 = on ? b.p_c0[pi] : 0u, c1 = on ? b.p_c1[pi] : 0u, rc = on ? b.p_rcnt[pi] : 0u;
+                const uint64_t rbv = on ? b.p_rb[pi] : NO_RB;
+                const uint32_t of = on ? b.p_off[pi] : 0u, rof = on ? b.p_roff[pi] : 0u;
+                const uint32_t rf = rbv != NO_RB ? 1u : 0u;
+                const uint32_t i0 = wave_incl_scan(c0), i1 = wave_incl_scan(c1), iR = wave_incl_scan(rc + rf);
+                const uint32_t t0 = __shfl(i0, 63, 64), t1 = __shfl(i1, 63, 64), tR = __shfl(iR, 63, 64);
+                const uint32_t cp = max(max(t0, t1), tR);
+                const uint64_t by = k2_scratch_bytes(np, cp);
+                if (lane == 0)
+                {
+                    L.red[0] = t0;
+                    L.red[1] = t1;
+                    L.red[2] = tR;
+                    if (by > L.have)
+                    {
+                        const unsigned long long grow = by + by / 2;
+                        L.so = atomicAdd(&b.ctl->scr_top, grow);
+                        L.have = L.so + grow > b.ctl->scr_cap ? 0ull : grow;
+                        if (!L.have) atomicOr(&b.ctl->overflow, 4u);
+                    }
+                }
+                wave_lds_sync();
+                if (L.have >= by)
+                {
+                    K2Mem mm;
+                    k2_carve(mm, b.scratch + L.so, np, cp);
+                    if (on)
+                    {
+                        mm.off[lane] = of; mm.c0[lane] = c0; mm.c1[lane] = c1;
+                        mm.roff[lane] = rof; mm.rcnt[lane] = rc; mm.rb[lane] = rbv;
+                        mm.st0[lane] = i0 - c0;
+                        mm.st1[lane] = i1 - c1;
+                        mm.stR[2 * lane] = iR - rc - rf;
+                        mm.stR[2 * lane + 1] = iR - rf;
+                    }
+                    if (lane == 0)
+                    {
+                        mm.st0[np] = t0;
+                        mm.st1[np] = t1;
+                        mm.stR[2 * np] = tR;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        else
+        {
+            if (tid < 3) L.red[tid] = 0;
+            __syncthreads();
             uint32_t a0 = 0, a1 = 0, aR = 0;
             for (uint32_t i = tid; i < np; i += KB_THREADS)
             {
@@ -1361,20 +1417,22 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
                 if (a1) atomicAdd(&L.red[1], a1);
                 if (aR) atomicAdd(&L.red[2], aR);
             }
+            __syncthreads();
+            const uint32_t cp = max(max(L.red[0], L.red[1]), L.red[2]);
+            const uint64_t by = k2_scratch_bytes(np, cp);
+            // this workgroup's scratch, reused across its requests (grown when a request needs more)
+            if (tid == 0 && by > L.have)
+            {
+                const unsigned long long grow = by + by / 2;
+                L.so = atomicAdd(&b.ctl->scr_top, grow);
+                L.have = L.so + grow > b.ctl->scr_cap ? 0ull : grow;
+                if (!L.have) atomicOr(&b.ctl->overflow, 4u);
+            }
+            __syncthreads();
         }
-        __syncthreads();
         const uint32_t tot0 = L.red[0], tot1 = L.red[1], totR = L.red[2];
         const uint32_t capn = max(max(tot0, tot1), totR);
-        // this workgroup's scratch, reused across its requests (grown when a request needs more)
         const uint64_t bytes = k2_scratch_bytes(np, capn);
-        if (tid == 0 && bytes > L.have)
-        {
-            const unsigned long long grow = bytes + bytes / 2;
-            L.so = atomicAdd(&b.ctl->scr_top, grow);
-            L.have = L.so + grow > b.ctl->scr_cap ? 0ull : grow;
-            if (!L.have) atomicOr(&b.ctl->overflow, 4u);
-        }
-        __syncthreads();
         if (L.have < bytes)
         {
             if (tid < 9) b.sz[tid * n + t] = 0;
@@ -1383,17 +1441,20 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
         }
         K2Mem mem;
         k2_carve(mem, b.scratch + L.so, np, capn);
-        for (uint32_t i = tid; i < np; i += KB_THREADS)
+        if (!few)
         {
-            mem.off[i] = b.p_off[p0 + i]; mem.c0[i] = b.p_c0[p0 + i]; mem.c1[i] = b.p_c1[p0 + i];
-            mem.roff[i] = b.p_roff[p0 + i]; mem.rcnt[i] = b.p_rcnt[p0 + i]; mem.rb[i] = b.p_rb[p0 + i];
+            for (uint32_t i = tid; i < np; i += KB_THREADS)
+            {
+                mem.off[i] = b.p_off[p0 + i]; mem.c0[i] = b.p_c0[p0 + i]; mem.c1[i] = b.p_c1[p0 + i];
+                mem.roff[i] = b.p_roff[p0 + i]; mem.rcnt[i] = b.p_rcnt[p0 + i]; mem.rb[i] = b.p_rb[p0 + i];
+            }
+            __syncthreads();
+            block_scan_into(L, np, [&](uint32_t i) { return mem.c0[i]; }, mem.st0);
+            block_scan_into(L, np, [&](uint32_t i) { return mem.c1[i]; }, mem.st1);
+            block_scan_into(L, 2 * np, [&](uint32_t i) {
+                return (i & 1) ? (mem.rb[i >> 1] != NO_RB ? 1u : 0u) : mem.rcnt[i >> 1];
+            }, mem.stR);
         }
-        __syncthreads();
-        block_scan_into(L, np, [&](uint32_t i) { return mem.c0[i]; }, mem.st0);
-        block_scan_into(L, np, [&](uint32_t i) { return mem.c1[i]; }, mem.st1);
-        block_scan_into(L, 2 * np, [&](uint32_t i) {
-            return (i & 1) ? (mem.rb[i >> 1] != NO_RB ? 1u : 0u) : mem.rcnt[i >> 1];
-        }, mem.stR);
 
         // ---- keyDeps (class 0) and directKeyDeps (class 1)
         for (int c = 0; c < 2; ++c)
@@ -1407,15 +1468,31 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
                 continue;
             }
             const bool lds = tot <= min(KB_LDS_CAP, b.kb_sort) && np <= KB_LDS_LISTS;
-            if (lds)
+            // few lists (the usual <= 8 keys): their starts and arena offsets in LDS, so the gather is one global
+            // load per element instead of a search through the scratch starts and two scratch reads
+            const bool lst = np <= KB_LDS_LISTS;
+            if (lst)
+            {
                 for (uint32_t i = tid; i <= np; i += KB_THREADS) Ss[i] = st[i];
+                for (uint32_t i = tid; i < np; i += KB_THREADS) So[i] = mem.off[i] + (c == 0 ? 0u : mem.c0[i]);
+                __syncthreads();
+            }
             // (the merge tree in global scratch: the u32 values in V's and UP's room, 2 cap words each)
             const bool tree = b.kb_merge;
             uint32_t* gX = reinterpret_cast<uint32_t*>(mem.V);
             for (uint32_t e = tid; e < tot; e += KB_THREADS)
             {
-                const uint32_t a = list_of(st, np, e);
-                const uint32_t v = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
+                uint32_t v;
+                if (lst)
+                {
+                    const uint32_t a = list_of(Ss, np, e);
+                    v = b.arena[(uint64_t)So[a] + (e - Ss[a])];
+                }
+                else
+                {
+                    const uint32_t a = list_of(st, np, e);
+                    v = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
+                }
                 if (lds) Vs[e] = v;
                 else if (tree) gX[e] = v;
                 else mem.V[e] = v;
@@ -1428,7 +1505,6 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
                                             : block_merge_tree(L, gX, reinterpret_cast<uint32_t*>(mem.UP), st, np, tot, &Xs, &Xp))
                                : lds ? block_rank_merge_kept(L, getl, Ss, np, tot, Ps)
                                      : block_rank_merge_kept(L, get, st, np, tot, mem.P);
-            const uint32_t* Sx = lds ? Ss : st;
             if (wv == 0)
             {
                 uint32_t nk = 0;
@@ -1481,8 +1557,17 @@ __global__ __launch_bounds__(KB_THREADS) void k_build_big(DevSnapshot s, BatchBu
                         if (i == 0 || Xs[i] != Xs[i - 1]) otx[Xp[i]] = dict_index(Xs[i]);
                     for (uint32_t e = tid; e < tot; e += KB_THREADS)
                     {
-                        const uint32_t a = list_of(Sx, np, e);
-                        const uint32_t x = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - Sx[a])];
+                        uint32_t x;
+                        if (lst)
+                        {
+                            const uint32_t a = list_of(Ss, np, e);
+                            x = b.arena[(uint64_t)So[a] + (e - Ss[a])];
+                        }
+                        else
+                        {
+                            const uint32_t a = list_of(st, np, e);
+                            x = b.arena[(uint64_t)mem.off[a] + (c == 0 ? 0u : mem.c0[a]) + (e - st[a])];
+                        }
                         uint32_t lo = 0, hi = tot;
                         while (lo < hi)
                         {

@@ -272,6 +272,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
     // emissions than pass 2 takes -- straight to D2, the general kernel's list (pass 2 would only defer
     // them again: 99k late PreAccepts of the request mix cost pass 2 0.12 ms for nothing)
     constexpr int NBUF = PASS == 1 ? 2 : 1;
+    constexpr uint32_t SPLIT_BIT = 0x80000000u, LEAN_SPLIT_T = 256;
     __shared__ uint32_t dbuf_all[LEAN_WAVES][NBUF][DEFER_CHUNK];
     uint32_t* dbuf = dbuf_all[threadIdx.x >> 6][0];
     uint32_t* hbuf = dbuf_all[threadIdx.x >> 6][NBUF - 1];
@@ -283,7 +284,8 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         wave_lds_sync();
         // pass 1's hard deferrals: a Range-domain request of a mixed batch (REC_SPLIT, k_prepare) goes straight to
         // the split kernels' list; the rest to D2
-        const bool sp = to_d2 && lane_id() < cnt && (b.q_rec[tv].z & REC_SPLIT) != 0;
+        // (bit 31: a request with more raw emissions than the general kernel stages -- it would only defer it again)
+        const bool sp = to_d2 && lane_id() < cnt && ((tv & SPLIT_BIT) != 0 || (b.q_rec[tv & ~SPLIT_BIT].z & REC_SPLIT) != 0);
         const uint64_t spm = ballot(sp);
         const uint32_t nsp = __popcll(spm), nrest = cnt - nsp;
         unsigned long long base = 0, sbase = 0;
@@ -302,7 +304,7 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         base = uniform64(base);
         sbase = uniform64(sbase);
         const uint64_t below = (1ull << lane_id()) - 1;
-        if (sp) b.deferred[sbase + __popcll(spm & below)] = tv;
+        if (sp) b.deferred[sbase + __popcll(spm & below)] = tv & ~SPLIT_BIT;
         else if (lane_id() < cnt) (to_d2 ? b.deferred2 : lists().out)[base + __popcll(~spm & below)] = tv;
         cnt = 0;
     };
@@ -572,7 +574,9 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
                 if (nh)
                 {
                     if (hn + nh > DEFER_CHUNK) flush_to(hbuf, hn, true);
-                    if (act && hard && hl == 0) hbuf[hn + __popcll(hm & ((1ull << lane) - 1))] = t;
+                    // (more raw emissions than the general kernel stages, 64 per map: straight to the split kernels)
+                    if (act && hard && hl == 0)
+                        hbuf[hn + __popcll(hm & ((1ull << lane) - 1))] = t | (T > LEAN_SPLIT_T ? SPLIT_BIT : 0u);
                     hn += nh;
                 }
             }
