@@ -2107,20 +2107,38 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* wsum /
     return r;
 }
 
+// A block scans SCAN_BLOCK * SCAN_ITEMS elements: wave w the 512 at [w * 512, +512) as 8 coalesced chunks of 64
+// (chunk-major is memory order, so a chunk's lane prefix plus the earlier chunks' totals is the wave prefix).
+// (One element per thread, as before round 6, spent the 4-array scan of a 16M-entry derivation mostly on
+// block overhead: 64k blocks of 4 KB each.)
+constexpr int SCAN_ITEMS = 8;
+constexpr uint64_t SCAN_TILE = (uint64_t)SCAN_BLOCK * SCAN_ITEMS;
+
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t* __restrict__ sz, uint64_t n,
                                                             uint64_t* __restrict__ bsum, uint64_t nb)
 {
     __shared__ uint64_t part[SCAN_BLOCK / 64];
     const int a = blockIdx.y;
-    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
-    const uint64_t v = wave_incl_scan64(i < n ? sz[(uint64_t)a * n + i] : 0);
-    if (lane_id() == 63) part[threadIdx.x >> 6] = v;
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)(threadIdx.x >> 6) * (64 * SCAN_ITEMS) + lane_id();
+    const uint32_t* __restrict__ in = sz + (uint64_t)a * n;
+    uint32_t v[SCAN_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j)
+    {
+        const uint64_t i = base + 64ull * j;
+        v[j] = i < n ? in[i] : 0u;
+    }
+    uint64_t t = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) t += v[j];
+    t = wave_incl_scan64(t);
+    if (lane_id() == 63) part[threadIdx.x >> 6] = t;
     __syncthreads();
     if (threadIdx.x == 0)
     {
-        uint64_t t = 0;
-        for (int w = 0; w < SCAN_BLOCK / 64; ++w) t += part[w];
-        bsum[(uint64_t)a * nb + blockIdx.x] = t;
+        uint64_t x = 0;
+        for (int w = 0; w < SCAN_BLOCK / 64; ++w) x += part[w];
+        bsum[(uint64_t)a * nb + blockIdx.x] = x;
     }
 }
 
@@ -2146,20 +2164,45 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tile(const uint32_t* __rest
                                                           const uint64_t* __restrict__ bsum, uint64_t nb,
                                                           uint64_t* __restrict__ off)
 {
-    __shared__ uint64_t wsum[SCAN_BLOCK / 64 + 1];
+    __shared__ uint64_t wpre[SCAN_BLOCK / 64];
     const int a = blockIdx.y;
-    const uint64_t i = (uint64_t)blockIdx.x * SCAN_BLOCK + threadIdx.x;
-    const uint64_t v = i < n ? sz[(uint64_t)a * n + i] : 0;
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan(v, wsum, &tot);
-    if (i < n) off[(uint64_t)a * (n + 1) + i] = bsum[(uint64_t)a * nb + blockIdx.x] + ex;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)w * (64 * SCAN_ITEMS) + lane;
+    const uint32_t* __restrict__ in = sz + (uint64_t)a * n;
+    uint64_t* __restrict__ out = off + (uint64_t)a * (n + 1);
+    uint32_t v[SCAN_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j)
+    {
+        const uint64_t i = base + 64ull * j;
+        v[j] = i < n ? in[i] : 0u;
+    }
+    uint64_t ex[SCAN_ITEMS];
+    uint64_t run = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j)
+    {
+        const uint64_t inc = wave_incl_scan64(v[j]);
+        ex[j] = run + inc - v[j];
+        run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) wpre[w] = run;          // the wave's total
+    __syncthreads();
+    uint64_t pre = bsum[(uint64_t)a * nb + blockIdx.x];
+    for (uint32_t ww = 0; ww < w; ++ww) pre += wpre[ww];
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j)
+    {
+        const uint64_t i = base + 64ull * j;
+        if (i < n) out[i] = pre + ex[j];
+    }
 }
 
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st)
 {
     // out[a][0..n] = exclusive prefix of in[a][0..n), out[a][n] = total, for a < n_arrays
-    // (bsum: n_arrays * ceil(n / 1024) entries)
-    const uint64_t nb = (n + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    // (bsum: n_arrays * ceil(n / SCAN_TILE) entries -- callers size it for ceil(n / 1024), more than enough)
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint64_t) * n_arrays, st);    // out[a][0], a < n_arrays
     dim3 g((unsigned)nb, (unsigned)n_arrays);
     k_scan_reduce<<<g, SCAN_BLOCK, 0, st>>>(in, n, bsum, nb);
