@@ -59,6 +59,7 @@ struct UpdCtl {
     uint32_t older, pad;      // a new id is older than the newest dictionary id (dictionary merge)
     uint64_t cm[2];           // incremental committed order: entries kept from the last one, changed committed entries
     uint32_t n_newk, pad2;    // update keys without a CommandsForKey (with repeats)
+    unsigned long long kdiff; // OR of (key ^ the batch's first key) over them, sign-flipped (sort digits)
 };
 constexpr uint32_t LOC_NONE = 0xFFFFFFFFu;
 
@@ -894,7 +895,10 @@ __global__ void k_key_collect(DevSnapshot s, CfkUpdIn u, uint64_t* out, UpdCtl* 
     if (i >= u.n) return;
     const int64_t key = u.keys[i];
     if (key_index(s, key) != KEY_EMPTY) return;
-    out[atomicAdd(&ctl->n_newk, 1u)] = (uint64_t)key ^ 0x8000000000000000ull;     // unsigned sort order
+    const uint64_t x = (uint64_t)key ^ 0x8000000000000000ull;     // unsigned sort order
+    out[atomicAdd(&ctl->n_newk, 1u)] = x;
+    const uint64_t d = x ^ ((uint64_t)u.keys[0] ^ 0x8000000000000000ull);
+    if (d) atomicOr(&ctl->kdiff, (unsigned long long)d);
 }
 
 __global__ void k_key_unique(const uint64_t* ks, uint64_t m, uint32_t* flag)
@@ -922,11 +926,12 @@ __global__ void k_key_place(DevSnapshot s, const uint64_t* ks, uint64_t m, const
 }
 
 __global__ __launch_bounds__(256) void k_key_move(DevSnapshot s, const uint32_t* kcell, const uint64_t* kpos, uint64_t U,
-                                                  KeyBufs nb)
+                                                  KeyBufs nb, uint32_t* kmap)
 {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= s.n_keys) return;
     const uint64_t p = k + merged_before(kpos, U, k);
+    kmap[k] = (uint32_t)p;
     nb.keys[p] = s.keys[k];
     nb.krec[p] = s.krec[k];
     nb.kcell[p] = kcell ? kcell[k] : NO_CELL;
@@ -963,10 +968,12 @@ __global__ void k_key_new(DevSnapshot s, const int64_t* nkeys, const uint64_t* k
     nb.kcell[p] = cell;
 }
 
-__global__ __launch_bounds__(256) void k_ekey_remap(uint64_t ne, uint32_t* ekey, const uint64_t* kpos, uint64_t U)
+// entries' key indices through the old -> new key index map k_key_move wrote (one gather per entry, not a
+// search of the new keys' positions)
+__global__ __launch_bounds__(256) void k_ekey_remap(uint64_t ne, uint32_t* ekey, const uint32_t* kmap)
 {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < ne) ekey[e] += (uint32_t)merged_before(kpos, U, ekey[e]);
+    if (e < ne) ekey[e] = kmap[ekey[e]];
 }
 
 __global__ void k_khash_clear(KeySlot* h, uint64_t n)
@@ -1368,16 +1375,19 @@ __global__ void k_cm_compact(uint64_t m, const uint32_t* src, const uint32_t* mv
     vo[p] = e;
 }
 
-// each block merges 256 consecutive elements of one list into the output: the block's first and
-// last element bound its window in the other list (two searches per block), each thread then
-// searches only that window
+// each block merges CM_TILE consecutive elements of one list into the output: the block's first and last
+// element bound its window in the other list (two searches per block, ~20 dependent loads each -- one block
+// per 256 elements, as before round 6, spent most of the merge on them), each thread then searches only that
+// window, from its previous element's place on (its elements ascend)
+constexpr uint32_t CM_ITEMS = 8, CM_TILE = 256 * CM_ITEMS;
+
 __global__ __launch_bounds__(256) void k_cm_merge(uint64_t na, const uint64_t* ka, const uint32_t* va, uint64_t nb,
                                                   const uint64_t* kb, const uint32_t* vb, uint64_t* ko, uint32_t* vo)
 {
     __shared__ uint64_t win[2];
-    const uint64_t blocks_a = (na + 255) / 256;
+    const uint64_t blocks_a = (na + CM_TILE - 1) / CM_TILE;
     const bool from_a = blockIdx.x < blocks_a;
-    const uint64_t base = from_a ? (uint64_t)blockIdx.x * 256 : ((uint64_t)blockIdx.x - blocks_a) * 256;
+    const uint64_t base = from_a ? (uint64_t)blockIdx.x * CM_TILE : ((uint64_t)blockIdx.x - blocks_a) * CM_TILE;
     const uint64_t nself = from_a ? na : nb, nother = from_a ? nb : na;
     const uint64_t* self = from_a ? ka : kb;
     const uint64_t* o = from_a ? kb : ka;
@@ -1391,16 +1401,23 @@ __global__ __launch_bounds__(256) void k_cm_merge(uint64_t na, const uint64_t* k
         }
         return lo;
     };
-    const uint64_t last = min(base + 256, nself) - 1;
+    const uint64_t last = min(base + CM_TILE, nself) - 1;
     if (threadIdx.x == 0) win[0] = bound(self[base], 0, nother);
-    if (threadIdx.x == 1) win[1] = bound(self[last], 0, nother);
+    if (threadIdx.x == 64) win[1] = bound(self[last], 0, nother);
     __syncthreads();
-    const uint64_t i = base + threadIdx.x;
-    if (i >= nself) return;
-    const uint64_t x = self[i];
-    const uint64_t p = i + bound(x, win[0], win[1]);
-    ko[p] = x;
-    vo[p] = from_a ? va[i] : vb[i];
+    uint64_t lo = win[0];
+    const uint64_t hi = win[1];
+#pragma unroll
+    for (uint32_t j = 0; j < CM_ITEMS; ++j)
+    {
+        const uint64_t i = base + (uint64_t)j * 256 + threadIdx.x;
+        if (i >= nself) break;
+        const uint64_t x = self[i];
+        lo = bound(x, lo, hi);
+        const uint64_t p = i + lo;
+        ko[p] = x;
+        vo[p] = from_a ? va[i] : vb[i];
+    }
 }
 
 unsigned blocks(uint64_t n, unsigned t = 256) { return (unsigned)std::max<uint64_t>(1, (n + t - 1) / t); }
@@ -1414,7 +1431,7 @@ struct DBuf : DevBuf {
 }  // namespace
 
 struct CfkUpdWork {
-    DBuf ctl, loc, xr, word, bk, flags, fs, bsum, ck, cv, ck2, cv2, hist, hoff, f2, s2, maw, wtail;
+    DBuf ctl, loc, xr, word, bk, flags, fs, bsum, ck, cv, ck2, cv2, hist, hoff, f2, s2, maw, wtail, kmap;
     DBuf sm_hi, sm_lo, sm_node;
     DBuf nw, nk_a, nk_b, nv_a, nv_b, nflag, npos, ins_k, ins_v, gflag, gs, gword, gkey, grank, ib, krec_bk;
     DBuf mh, ml, mn, mraw, mpos;
@@ -1559,7 +1576,7 @@ static int cfk_derive(CfkUpdWork* w, DevSnapshot& s, const CfkDevState& dd, CfkD
                                   w->hist.as<uint32_t>(), w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &kb, &vb));
         }
         if (ncm)
-            k_cm_merge<<<(unsigned)((nA + 255) / 256 + (nB + 255) / 256), 256, 0, st>>>(nA, w->cka.as<uint64_t>(),
+            k_cm_merge<<<(unsigned)((nA + CM_TILE - 1) / CM_TILE + (nB + CM_TILE - 1) / CM_TILE), 256, 0, st>>>(nA, w->cka.as<uint64_t>(),
                                                                                       w->cva.as<uint32_t>(), nB, kb, vb, ks, vs);
         UCHK(hipGetLastError());
     }
@@ -1641,8 +1658,14 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
     uint32_t* vs = w->kv_a.as<uint32_t>();
     k_iota<<<blocks(m), 256, 0, st>>>(vs, m);
     if (m > 1)
-        UCHK(radix_sort_pairs(ks, vs, w->kn_b.as<uint64_t>(), w->kv_b.as<uint32_t>(), m, 0xFFu, w->hist.as<uint32_t>(),
+    {
+        // only the bytes in which the keys differ (a key space of 2^20: three passes, not eight)
+        uint32_t dm = 0;
+        for (int dg = 0; dg < 8; ++dg)
+            if ((w->h_ctl->kdiff >> (8 * dg)) & 0xFF) dm |= 1u << dg;
+        UCHK(radix_sort_pairs(ks, vs, w->kn_b.as<uint64_t>(), w->kv_b.as<uint32_t>(), m, dm, w->hist.as<uint32_t>(),
                               w->hoff.as<uint64_t>(), w->bsum.as<uint64_t>(), st, &ks, &vs));
+    }
     k_key_unique<<<blocks(m), 256, 0, st>>>(ks, m, w->kflag.as<uint32_t>());
     UCHK(run_scan_arrays(w->kflag.as<uint32_t>(), w->kfpos.as<uint64_t>(), m, 1, w->bsum.as<uint64_t>(), st));
     k_drv_totals<<<1, 64, 0, st>>>(w->kfpos.as<uint64_t>(), m, 1, &ctl->tot3[0]);
@@ -1659,9 +1682,10 @@ static int add_keys(CfkUpdWork* w, DevSnapshot& s, CfkDevState& d, const CfkUpdI
     if (int rc = grow.keys_spare(grow.ctx, nk + U, &nb)) { *err = "key arrays"; return rc; }
     host_trace("add_keys: keys_spare");
     const uint64_t* kpos = w->kpos.as<uint64_t>();
-    if (nk) k_key_move<<<blocks(nk), 256, 0, st>>>(s, grow.kcell, kpos, U, nb);
+    UALLOC(w->kmap, 4 * std::max<uint64_t>(nk, 1), false);
+    if (nk) k_key_move<<<blocks(nk), 256, 0, st>>>(s, grow.kcell, kpos, U, nb, w->kmap.as<uint32_t>());
     k_key_new<<<blocks(U), 256, 0, st>>>(s, w->knew.as<int64_t>(), kpos, U, nb);
-    if (ne) k_ekey_remap<<<blocks(ne), 256, 0, st>>>(ne, d.ekey, kpos, U);
+    if (ne) k_ekey_remap<<<blocks(ne), 256, 0, st>>>(ne, d.ekey, w->kmap.as<uint32_t>());
     k_khash_clear<<<blocks(nb.hcap), 256, 0, st>>>(nb.khash, nb.hcap);
     k_khash_fill<<<blocks(nk + U), 256, 0, st>>>(nk + U, nb);
     UCHK(hipGetLastError());

@@ -413,7 +413,7 @@ hipError_t run_range_fill(const DevSnapshot& s, uint64_t n, const uint64_t* key_
 // K1: CommandsForKey.mapReduceActive, one wave per (request, key) probe
 // ---------------------------------------------------------------------------------------
 constexpr int K1_WAVES = 4;
-constexpr int K1_CAP = 1024;        // LDS staging per wave (u32)
+constexpr int K1_CAP = 1024;        // LDS staging per wave (u32; k_recover, k_scan's default)
 constexpr uint32_t K1_CHUNK = 4096; // arena chunk per wave refill
 
 struct ChunkAlloc {
@@ -438,9 +438,11 @@ struct ChunkAlloc {
     }
 };
 
+// CAP: LDS staging per wave (u32); a probe emitting more replays its descent straight into the arena
+template <int CAP>
 __global__ __launch_bounds__(256) void k_scan(DevSnapshot s, BatchBufs b)
 {
-    __shared__ uint32_t stage[K1_WAVES][K1_CAP];
+    __shared__ uint32_t stage[K1_WAVES][CAP];
     __shared__ uint64_t stk[K1_WAVES][2 * MAX_LEVELS];
     const int wv = threadIdx.x >> 6;
     const uint32_t lane = lane_id();
@@ -527,7 +529,7 @@ __global__ __launch_bounds__(256) void k_scan(DevSnapshot s, BatchBufs b)
                 dup |= ballot(want && r == extra) != 0;
             }
             const uint32_t n = __popcll(wm);
-            if (!overflow && cursor + n <= K1_CAP)
+            if (!overflow && cursor + n <= CAP)
             {
                 if (want) stage[wv][cursor + mbcnt(wm)] = r | (is1 ? CLASS_DIRECT_BIT : 0u);
                 cursor += n;
@@ -593,8 +595,13 @@ hipError_t run_scan(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_probes) return hipSuccess;
     const uint64_t blocks_needed = (b.n_probes + K1_WAVES - 1) / K1_WAVES;
+    // (AD_K1_CAP: 1024 (default), 2048 or 4096 staged ids per wave -- a bigger stage saves hot keys' replayed
+    // descents at fewer waves per CU)
+    static const int cap = getenv("AD_K1_CAP") ? atoi(getenv("AD_K1_CAP")) : 1024;
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
-    k_scan<<<grid, 256, 0, st>>>(s, b);
+    if (cap >= 4096) k_scan<4096><<<grid, 256, 0, st>>>(s, b);
+    else if (cap >= 2048) k_scan<2048><<<grid, 256, 0, st>>>(s, b);
+    else k_scan<1024><<<grid, 256, 0, st>>>(s, b);
     return hipGetLastError();
 }
 
@@ -2198,8 +2205,65 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_tile(const uint32_t* __rest
     }
 }
 
+// small arrays (the radix histograms of the update's sorts, per-request counts of small batches): one block per
+// array walks it in tiles with a carry -- one launch instead of three (a step of the steady state runs ~30 scans)
+constexpr uint64_t SCAN_SMALL = 8 * SCAN_TILE;
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_small(const uint32_t* __restrict__ sz, uint64_t n, uint64_t* __restrict__ off)
+{
+    __shared__ uint64_t wtot[SCAN_BLOCK / 64];
+    const int a = blockIdx.x;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t* __restrict__ in = sz + (uint64_t)a * n;
+    uint64_t* __restrict__ out = off + (uint64_t)a * (n + 1);
+    uint64_t carry = 0;
+    for (uint64_t t0 = 0; t0 < n; t0 += SCAN_TILE)
+    {
+        const uint64_t base = t0 + (uint64_t)w * (64 * SCAN_ITEMS) + lane;
+        uint32_t v[SCAN_ITEMS];
+#pragma unroll
+        for (int j = 0; j < SCAN_ITEMS; ++j)
+        {
+            const uint64_t i = base + 64ull * j;
+            v[j] = i < n ? in[i] : 0u;
+        }
+        uint64_t ex[SCAN_ITEMS];
+        uint64_t run = 0;
+#pragma unroll
+        for (int j = 0; j < SCAN_ITEMS; ++j)
+        {
+            const uint64_t inc = wave_incl_scan64(v[j]);
+            ex[j] = run + inc - v[j];
+            run += __shfl(inc, 63, 64);
+        }
+        if (lane == 0) wtot[w] = run;
+        __syncthreads();
+        uint64_t pre = carry, tot = 0;
+        for (uint32_t ww = 0; ww < SCAN_BLOCK / 64; ++ww)
+        {
+            const uint64_t x = wtot[ww];
+            if (ww < w) pre += x;
+            tot += x;
+        }
+#pragma unroll
+        for (int j = 0; j < SCAN_ITEMS; ++j)
+        {
+            const uint64_t i = base + 64ull * j;
+            if (i < n) out[i] = pre + ex[j];
+        }
+        carry += tot;
+        __syncthreads();                    // wtot rewritten by the next tile
+    }
+    if (threadIdx.x == 0) out[n] = carry;
+}
+
 hipError_t run_scan_arrays(const uint32_t* in, uint64_t* out, uint64_t n, int n_arrays, uint64_t* bsum, hipStream_t st)
 {
+    if (n && n <= SCAN_SMALL)
+    {
+        k_scan_small<<<n_arrays, SCAN_BLOCK, 0, st>>>(in, n, out);
+        return hipGetLastError();
+    }
     // out[a][0..n] = exclusive prefix of in[a][0..n), out[a][n] = total, for a < n_arrays
     // (bsum: n_arrays * ceil(n / SCAN_TILE) entries -- callers size it for ceil(n / 1024), more than enough)
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
