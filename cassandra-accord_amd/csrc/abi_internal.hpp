@@ -426,6 +426,15 @@ uint64_t* rb_slot(ad_ctx* c);
 int build_snapshot(ad_ctx* c);
 // the snapshot truncated to the RedundantBefore it holds (SafeCommandStore.maybeTruncate, every key)
 int truncate_to_rb(ad_ctx* c);
+// Range commands and RedundantBefore of a snapshot build (abi_snapshot.cpp): the stabbing index's cell ends,
+// whether it could be built, the range entries
+struct RangePart {
+    std::vector<int64_t> cell_E;
+    bool cell_ok = false;
+    uint64_t n_rent = 0;
+};
+int build_ranges(ad_ctx* c, const std::vector<uint32_t>& cmd_rank, const std::vector<uint32_t>& wm_rank, RangePart* out);
+int set_range_views(ad_ctx* c, const RangePart& rp, uint64_t nrb);
 // the key's shardRedundantBefore on the host copy (RedundantBefore.get; null: none or NONE), and whether
 // t is below it
 const Tid* rb_wm_of(const ad_ctx* c, int64_t key);
