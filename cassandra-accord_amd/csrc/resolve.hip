@@ -171,6 +171,31 @@ __device__ __forceinline__ void grp_lower_bound2(bool act_a, uint64_t lo_a, uint
             hi = pc;
         }
     };
+    // one galloping round from the tail first: lane j probes hi - 8^(j+1), so an answer within 8^k of the end
+    // (a late PreAccept's insertPos, an Accept's last committed Write) is left in a window of 8^k after one
+    // round trip, k more rounds to go -- instead of the log8 of the key's whole segment
+    auto gallop = [&](bool on, bool lt, uint64_t p_lane, uint64_t& lo, uint64_t& hi) {
+        const uint32_t bits = grp_bits(ballot(lt), g);      // ascending j = descending position: 1...10...0 (lt)
+        const uint32_t c = __popc(~bits & 0xFFu);           // probes at or above x (nearest the tail)
+        const uint32_t gl = lane_id() & ~7u;
+        const uint64_t p_lt = __shfl(p_lane, gl + (c < 8 ? c : 7u), 64);          // nearest probe below x
+        const uint64_t p_ge = __shfl(p_lane, gl + (c > 0 ? c - 1 : 0u), 64);      // farthest probe at or above x
+        if (!on) return;
+        if (c < 8) lo = p_lt + 1;
+        if (c > 0) hi = p_ge;
+    };
+    {
+        const bool ga = act_a && hi_a - lo_a > 64, gb = act_b && hi_b - lo_b > 64;
+        if (ballot(ga || gb))
+        {
+            const uint64_t sp = 1ull << (3 * (j + 1));
+            const uint64_t pa = ga ? hi_a - (sp < hi_a - lo_a ? sp : hi_a - lo_a) : 0;
+            const uint64_t pb = gb ? hi_b - (sp < hi_b - lo_b ? sp : hi_b - lo_b) : 0;
+            const uint32_t va = ga ? key_a(pa) : 0u, vb = gb ? key_b(pb) : 0u;
+            gallop(ga, ga && va < x, pa, lo_a, hi_a);
+            gallop(gb, gb && vb < x, pb, lo_b, hi_b);
+        }
+    }
     while (ballot((act_a && hi_a - lo_a > 8) || (act_b && hi_b - lo_b > 8)))
     {
         const bool sa = act_a && hi_a - lo_a > 8, sb = act_b && hi_b - lo_b > 8;
