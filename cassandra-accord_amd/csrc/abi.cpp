@@ -16,7 +16,10 @@ namespace adi {
 // neither proposed nor stable, no deps, executeAtOrTxnId = txnId); the snapshot is rebuilt before the
 // batch resolves, so every request sees the ones below its txnId (STARTED_BEFORE) -- the sequential
 // answer (PreAccept.java:116-132). A txnId already among the range commands is refused (AD_E_INVAL;
-// RangeCommand.update's union with its earlier ranges is not modelled).
+// RangeCommand.update's union with its earlier ranges is not modelled). The registry is an unordered set:
+// a new command is appended (the oracle's TreeMap inserts it in TxnId order); the snapshot build sorts the
+// range part by TxnId and recovery facts are parallel arrays appended alongside, so nothing reads position
+// as order (tests/test_gpu_ranges.py::test_sequential_range_txn_below_registered).
 int register_range_txns(ad_ctx* c, const ad_query_soa* q, const std::vector<uint64_t>& idx)
 {
     auto& R = c->cmds;

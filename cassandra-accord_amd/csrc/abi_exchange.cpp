@@ -676,22 +676,29 @@ int exchange_local_run(ad_ctx* const* ctxs, uint32_t n, const ad_deps_result* co
         for (uint32_t e = 0; e < d && distinct; ++e) distinct = ctxs[d]->device != ctxs[e]->device;
     double ms_merge = 0;
     std::vector<MergeTail> tails(n);
+    // on a failure, every owner whose merge was queued is drained before returning (no kernel or pinned
+    // read-back left in flight behind the caller); its out[] entry is then unset
+    auto drain = [&](int rc) {
+        for (uint32_t e = 0; e < n; ++e)
+            if (hipSetDevice(ctxs[e]->device) == hipSuccess) (void)hipStreamSynchronize(ctxs[e]->stream);
+        return rc;
+    };
     for (uint32_t d = 0; d < n; ++d)
     {
         ad_ctx* o = ctxs[d];
-        if (hipSetDevice(o->device) != hipSuccess) return o->fail(AD_E_DEVICE, "hipSetDevice");
+        if (hipSetDevice(o->device) != hipSuccess) return drain(o->fail(AD_E_DEVICE, "hipSetDevice"));
         if (int rc = x_merge(o, n, src_parts[d].data(), runits[d].data(), fmt, txn_base[d], n_owned[d], o->stream, &out[d],
                              &tails[d]))
-            return rc;
+            return drain(rc);
         if (!distinct)
         {
-            if (int rc = merge_tail(o, tails[d], &out[d])) return rc;
+            if (int rc = merge_tail(o, tails[d], &out[d])) return drain(rc);
             ms_merge += out[d].ms_device;
         }
     }
     for (uint32_t d = 0; d < n && distinct; ++d)
     {
-        if (int rc = merge_tail(ctxs[d], tails[d], &out[d])) return rc;
+        if (int rc = merge_tail(ctxs[d], tails[d], &out[d])) return drain(rc);
         ms_merge += out[d].ms_device;
     }
     if (stats)

@@ -247,6 +247,30 @@ def test_sequential_range_txns_persist(oracle):
         ost.close()
 
 
+@pytest.mark.parametrize("seed", [1, 7])
+def test_sequential_range_txn_below_registered(oracle, seed):
+    # the library appends a registered range txn to the store's range commands where the oracle inserts it
+    # in TxnId order (a TreeMap): nothing may depend on the registry's order. These seeds register a
+    # Range-domain txn that sorts below an existing range command; the SEQUENTIAL batch, then SNAPSHOT
+    # reads of every request on the grown registry, against the oracle
+    import pyoracle
+    w = synth.sequential_ranges(3000 + seed, n_keys=30 + 3 * seed, n_txns=80, with_slices=(seed % 3 == 1),
+                                start_inclusive=(seed % 4 == 2), n_redundant=4)
+    q, cm = w.queries, w.cmds
+    top = max(zip(cm.txn.msb.tolist(), cm.txn.lsb.tolist()))
+    assert any(q.ranges_of(i) and (int(q.txn.msb[i]), int(q.txn.lsb[i])) < top for i in range(len(q)))
+    st = native.DeviceCommandStore(0, w.range_start_inclusive, 1, w.slices)
+    ost = pyoracle.OracleStore(w.range_start_inclusive, 1, w.slices)
+    try:
+        st.load(w)
+        ost.load(w)
+        _eq(st.calculate_partial_deps(q, A.AD_SEQUENTIAL), ost.deps_batch(q, A.AD_SEQUENTIAL), "sequential")
+        _eq(st.calculate_partial_deps(q), ost.deps_batch(q), "snapshot after")
+    finally:
+        st.close()
+        ost.close()
+
+
 def test_sequential_range_txn_already_registered():
     # a range txn the store already holds as a range command is refused, the store unchanged
     w = synth.sequential_ranges(3200, n_txns=40)
