@@ -242,7 +242,7 @@ int run_pipeline(ad_ctx* c, const ad_query_soa* q, hipStream_t st, ad_deps_resul
         return c->fail(AD_E_NOMEM, "batch buffers");
     b.big = c->big.as<uint32_t>();
     b.k2_big = K2_BIG;
-    if (lean && !c->ds.n_rent)
+    if (lean)
     {
         if (!ens<uint32_t>(c->p_slot, std::max<uint64_t>(np, 1))) return c->fail(AD_E_NOMEM, "probe slots");
         b.p_slot = c->p_slot.as<uint32_t>();

@@ -45,7 +45,7 @@ constexpr uint32_t LEAN_MAXP = 8;      // keys per request
 #endif
 constexpr uint32_t LEAN_CHUNK = 1u << LEAN_CHUNK_LOG;   // region bytes a wave takes from the arena at a time
 
-// Per probe, its KeyLine (stores without range commands): k_prepare does the slice test
+// Per probe, its KeyLine: k_prepare does the slice test
 // (InMemoryCommandStore.java:280) and the perfect-hash displacement, one thread per probe, so that the
 // lean passes load a probe's key and its line position side by side -- one dependent load shorter,
 // and no displacement gather inside them. The line still proves the key is the store's.
@@ -356,30 +356,21 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         q.defer = (r.z & REC_FAST) == 0;
         return q;
     };
-    // the key (one lane per key), and without range commands its line position beside it (k_prepare)
-    constexpr bool SLOTS = !RNG;
+    // the key (one lane per key) and its line position beside it (k_prepare: the slice test and the perfect
+    // hash's displacement, so the line load waits on no displacement gather here; round 6, config 4's range
+    // kernels: pass 1 0.622 -> 0.566 ms, k_prepare 0.020 -> 0.045)
     auto loadB = [&](const Req& q, int64_t& key, uint32_t& sl) {
         const bool on = q.act && !q.defer && hl < q.np;
         key = b.q_keys[on ? q.k0 + hl : 0];
-        if (SLOTS)
-        {
-            const uint32_t v = b.p_slot[on ? q.k0 + hl : 0];
-            sl = on ? v : LS_NONE;
-        }
+        const uint32_t v = b.p_slot[on ? q.k0 + hl : 0];
+        sl = on ? v : LS_NONE;
     };
-    // the key's line (KeyLine, common.hpp): the slice test (InMemoryCommandStore.java:280), then one
-    // random line per key -- its first 64 bytes: key, cell entries, newest fields, meta, the class's
-    // {count, start} and the cwr tail start. A slot holding another key is resolved when used.
+    // the key's line (KeyLine, common.hpp): one random line per key -- its first 64 bytes: key, cell entries,
+    // newest fields, meta, the class's {count, start} and the cwr tail start. A slot holding another key is
+    // resolved when used.
     struct Hdr { uint4 h0, h1; uint2 h2, h3; uint4 q; uint32_t slot; bool look; };
     constexpr bool QL = !RNG && RPW == 2;
     __shared__ uint4 qst_all[QL ? LEAN_WAVES : 1][QL ? 64 : 1];
-    // the request's slice (its slice set when the batch names them, SafeCommandStore.java:292)
-    auto in_slice_of = [&](uint32_t t, int64_t key) {
-        return slice_has(s.start_inclusive,
-                         b.q_slice_set ? request_slice(s, b.q_slice_set, t)
-                                       : SliceView{s.slice_start, s.slice_end, s.n_slices, s.n_slices == 0},
-                         key);
-    };
     auto load_line = [&](uint32_t slot, uint32_t cls, Hdr& H) {
         const uint4* L4 = reinterpret_cast<const uint4*>(s.kline + slot);
         H.h0 = L4[0];
@@ -387,22 +378,13 @@ __global__ __launch_bounds__(64 * LEAN_WAVES, (lean_occ<RNG, WIDE>())) void k_re
         H.h2 = reinterpret_cast<const uint2*>(L4 + 2)[cls];
         H.h3 = reinterpret_cast<const uint2*>(L4 + 3)[1];       // {cwr tail start, prunedBefore rank}
     };
-    // the key's displacement (a small table: cache-resident), issued ahead of its line; without range
-    // commands the line position came with the key (k_prepare)
-    auto loadD = [&](const Req& q, int64_t key, uint32_t sl, bool& look, uint32_t& d) {
-        if (SLOTS)
-        {
-            look = sl != LS_NONE;
-            d = sl;
-            return;
-        }
-        const bool on = q.act && !q.defer && hl < q.np;
-        look = on && in_slice_of(q.t, key);
-        d = s.kl_disp[look ? kl_bucket(key_hash(key), s.kl_buckets) : 0u];
+    auto loadD = [&](const Req&, int64_t, uint32_t sl, bool& look, uint32_t& d) {
+        look = sl != LS_NONE;
+        d = sl;
     };
     auto loadC = [&](const Req& q, int64_t key, bool look, uint32_t d, Hdr& H) {
         H.look = look;
-        H.slot = !look ? 0u : SLOTS ? d : (uint32_t)kl_index(key_hash2(key), d, s.kl_lines);
+        H.slot = !look ? 0u : d;
         if (QL)
         {
             // lane hl loads quarter hl & 3 of key hl >> 2's line (unmasked: unpacked under the key lane's look)
@@ -1126,7 +1108,7 @@ hipError_t run_resolve_lean(const DevSnapshot& s, const BatchBufs& b, int pass, 
     if (!b.n_txns) return hipSuccess;
     if (pass == 1)
     {
-        if (!s.n_rent && !b.p_slot) return hipErrorInvalidValue;     // k_prepare writes the probes' lines
+        if (!b.p_slot) return hipErrorInvalidValue;     // k_prepare writes the probes' lines
         if (rpw1 == 8) return s.n_rent ? launch_lean<8, true, false, 1>(s, b, st) : launch_lean<8, false, false, 1>(s, b, st);
         if (rpw1 == 4) return s.n_rent ? launch_lean<4, true, false, 1>(s, b, st) : launch_lean<4, false, false, 1>(s, b, st);
         if (wide1 && !s.n_rent) return launch_lean<2, false, true, 1>(s, b, st);
