@@ -197,6 +197,7 @@ struct ad_ctx {
     DevBuf d_rb_s, d_rb_e, d_rb_e0, d_rb_e1, d_rb_wm, d_rb_rid, d_slices_s, d_slices_e;
     DevBuf d_dict_lsb_raw, d_rt_start, d_rt_end;   // raw ids and range table (multi-GPU export)
     DevBuf d_ds_hi, d_ds_lo, d_ds_node;            // every DICT_SAMP-th dictionary id (rank searches)
+    DevBuf d_ds_bkt;                               // their bucket index (build_dict_buckets)
     DevBuf d_kline, d_kslot, d_kcell, d_kl_disp;   // KeyLine table; per key its line and stabbing cell; displacements
     uint64_t kline_slots = 0;
     // host state of the KeyLine perfect hash (incremental placement of new keys)
@@ -424,6 +425,7 @@ uint64_t* rb_slot(ad_ctx* c);
 
 // snapshot (abi.cpp): build, host copies of the device state, the node-wide dictionary, the KeyLine hash
 int build_snapshot(ad_ctx* c);
+int build_dict_buckets(ad_ctx* c, hipStream_t st);   // abi_snapshot.cpp: the sample level's bucket index
 // the snapshot truncated to the RedundantBefore it holds (SafeCommandStore.maybeTruncate, every key)
 int truncate_to_rb(ad_ctx* c);
 // Range commands and RedundantBefore of a snapshot build (abi_snapshot.cpp): the stabbing index's cell ends,

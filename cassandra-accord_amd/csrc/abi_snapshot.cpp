@@ -366,6 +366,21 @@ int set_range_views(ad_ctx* c, const RangePart& rp, uint64_t nrb)
     return 0;
 }
 
+// The first sample level's bucket index (common.hpp dict_bucket_of), rebuilt whenever the samples are: about one
+// sample per bucket (2^lg >= n_samp, at most 2^22). Without its buffer the searches run over all the samples.
+int build_dict_buckets(ad_ctx* c, hipStream_t st)
+{
+    DevSnapshot& s = c->ds;
+    s.ds_bkt = nullptr;
+    if (!s.n_samp || !s.ds_hi) return 0;
+    uint32_t lg = 0;
+    while ((1ull << lg) < s.n_samp && lg < 22) ++lg;
+    if (!c->d_ds_bkt.ensure(4 * (DB_HDR + (1ull << lg) + 1))) return 0;
+    HIPCHK(c, run_dict_buckets(s, c->d_ds_bkt.as<uint32_t>(), lg, st));
+    s.ds_bkt = c->d_ds_bkt.as<uint32_t>();
+    return 0;
+}
+
 // The DevSnapshot views over the ctx's device buffers of a built snapshot (both build routes)
 int set_views(ad_ctx* c, uint64_t n_dict, uint64_t n_samp, const NormTid& last, uint64_t nk, uint64_t ne, uint64_t hcap,
                      const RangePart& rp, uint64_t nrb)
@@ -553,6 +568,7 @@ int build_snapshot_device(ad_ctx* c)
     }
     if ((rc = set_views(c, n_dict, n_samp, last, nk, ne, hcap, rp, nrb))) return rc;
     if (n_samp) HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
+    if ((rc = build_dict_buckets(c, st))) return rc;
     if (!c->cu) c->cu = cfk_upd_work_create();
     CfkDevState d{c->d_status.as<uint8_t>(), c->d_xrank.as<uint32_t>(), c->d_ekey.as<uint32_t>(),
                   c->d_dict_lsb_raw.as<uint64_t>(), c->d_ballot.p ? c->d_ballot.as<Bal>() : nullptr, nullptr,
@@ -1131,6 +1147,7 @@ int build_snapshot_host(ad_ctx* c)
         rpv.n_rent = rent.size();
         if (cell_ok) rpv.cell_E = cell_E;
         if (int rc2 = set_views(c, dhi.size(), n_samp1, last, nk, ne, hcap, rpv, nrb)) return rc2;
+        if (int rc2 = build_dict_buckets(c, c->stream)) return rc2;
     }
     HIPCHK(c, build_cfk_trees(s, c->stream));
     HIPCHK(c, build_range_trees(s, c->stream));

@@ -542,6 +542,7 @@ int cfk_update_follow(ad_ctx* c, const CfkUpdOut& o, int rc, hipStream_t st)
         c->ds.n_samp = ok ? ns : 0;
         c->ds.n_samp2 = ok ? dict_samples2(c->ds.n_dict) : 0;
         if (ok) HIPCHK(c, run_dict_sample(c->ds, c->d_ds_hi.as<uint64_t>(), c->d_ds_lo.as<uint64_t>(), c->d_ds_node.as<int32_t>(), st));
+        if (int rb = build_dict_buckets(c, st)) return rb;
     host_trace("follow: dict sample");
     }
     if (o.n_inserted) { c->host_moved = true; c->host_ingested = false; }

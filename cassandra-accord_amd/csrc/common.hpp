@@ -221,6 +221,9 @@ struct DevSnapshot {
     const uint64_t* ds_lo;
     const int32_t*  ds_node;
     uint64_t n_samp, n_samp2;
+    // bucket index over the first sample level (dict_bucket; nullptr = none): DB_HDR header words, then
+    // 2^lg + 1 bucket starts
+    const uint32_t* ds_bkt;
     // CommandsForKey
     uint64_t n_keys;
     const int64_t*  keys;          // [n_keys]
@@ -352,6 +355,24 @@ __device__ inline void lockstep_partition(uint64_t (&a)[N], uint64_t (&b)[N], Pr
     }
 }
 
+// The first sample level's bucket index (round 6): bucket f(t) = min((t - first) >> shift, 2^lg - 1) over the
+// 128-bit (hi, lo) of a normalised id (0 below the first), monotone in the id order, so the samples <= t number
+// between start[f(t)] (the samples of lower buckets) and start[f(t) + 1]. A rank search reads its bucket's two
+// starts (one line) and searches only the samples between them -- instead of ~16 rounds of binary search over
+// all of them (each an L2 round trip). Header: first id's hi (2 words), lo (2), shift, lg, n_samp built for.
+constexpr uint32_t DB_HDR = 8;
+__host__ __device__ inline uint32_t bitlen128(uint64_t hi, uint64_t lo)
+{
+    return hi ? 128u - (uint32_t)__builtin_clzll(hi) : (lo ? 64u - (uint32_t)__builtin_clzll(lo) : 0u);
+}
+__host__ __device__ inline uint32_t dict_bucket_of(uint64_t mh, uint64_t ml, uint32_t sh, uint32_t lg, uint64_t hi, uint64_t lo)
+{
+    if (hi < mh || (hi == mh && lo < ml)) return 0;
+    const unsigned __int128 d = ((((unsigned __int128)hi << 64) | lo) - (((unsigned __int128)mh << 64) | ml)) >> sh;
+    const uint64_t nb = 1ull << lg;
+    return d >= nb ? (uint32_t)(nb - 1) : (uint32_t)d;
+}
+
 // Ranks of up to N arbitrary ids in the dictionary (member i -> 2i+1, else 2 * lower bound; above every
 // member: 2 * n_dict without a load), searched in lockstep (lockstep_partition): the first-level sample, then the
 // second-level window of it, then one DICT_SAMP2-id window of the dictionary. want[k] false: r[k] = 0.
@@ -374,6 +395,24 @@ __device__ inline void dict_rank_sampled_n(const Snap& s, const NormTid (&t)[N],
         }
         a[k] = 0;
         b[k] = act[k] ? s.n_samp : 0;
+    }
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) any = any || act[k];
+    if (s.ds_bkt && any)
+    {
+        // the bucket's samples only (dict_bucket_of; the header words are the same for every thread)
+        const uint32_t* B = s.ds_bkt;
+        const uint64_t mh = B[0] | ((uint64_t)B[1] << 32), ml = B[2] | ((uint64_t)B[3] << 32);
+        const uint32_t sh = B[4], lg = B[5];
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+        {
+            const uint32_t f = act[k] ? dict_bucket_of(mh, ml, sh, lg, t[k].hi, t[k].lo) : 0u;
+            const uint2 ab = act[k] ? make_uint2(B[DB_HDR + f], B[DB_HDR + f + 1]) : make_uint2(0, 0);
+            a[k] = ab.x;
+            b[k] = ab.y;
+        }
     }
     // first level: the samples <= t
     lockstep_partition<N>(a, b, [&](int k, uint64_t m) {

@@ -2414,6 +2414,48 @@ hipError_t run_dict_sample(const DevSnapshot& s, uint64_t* hi, uint64_t* lo, int
     return hipGetLastError();
 }
 
+// The bucket index of the first sample level (common.hpp dict_bucket_of), thread per bucket start: start[b] =
+// the first sample whose bucket is >= b (a binary search of the samples); thread 0 also writes the header.
+__global__ void k_dict_buckets(DevSnapshot s, uint32_t* B, uint32_t lg)
+{
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nb = 1ull << lg;
+    if (b > nb) return;
+    const uint64_t mh = s.ds_hi[0], ml = s.ds_lo[0];
+    // span of the dictionary: its last id less the first sample (= its first id)
+    const unsigned __int128 span = ((((unsigned __int128)s.dict_last_hi) << 64) | s.dict_last_lo) -
+                                   ((((unsigned __int128)mh) << 64) | ml);
+    const uint32_t bl = bitlen128((uint64_t)(span >> 64), (uint64_t)span);
+    const uint32_t sh = bl > lg ? bl - lg : 0u;
+    if (b == 0)
+    {
+        B[0] = (uint32_t)mh;
+        B[1] = (uint32_t)(mh >> 32);
+        B[2] = (uint32_t)ml;
+        B[3] = (uint32_t)(ml >> 32);
+        B[4] = sh;
+        B[5] = lg;
+        B[6] = (uint32_t)s.n_samp;
+        B[7] = 0;
+    }
+    uint64_t lo = 0, hi = s.n_samp;
+    while (lo < hi)
+    {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (dict_bucket_of(mh, ml, sh, lg, s.ds_hi[mid], s.ds_lo[mid]) < b) lo = mid + 1;
+        else hi = mid;
+    }
+    B[DB_HDR + b] = (uint32_t)lo;
+}
+
+hipError_t run_dict_buckets(const DevSnapshot& s, uint32_t* B, uint32_t lg, hipStream_t st)
+{
+    if (!s.n_samp) return hipSuccess;
+    const uint64_t n = (1ull << lg) + 1;
+    k_dict_buckets<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(s, B, lg);
+    return hipGetLastError();
+}
+
 int device_cu_count()
 {
     static int cus = 0;

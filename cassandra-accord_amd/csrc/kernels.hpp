@@ -263,5 +263,6 @@ inline const LeanQuads* kline_quads(const KeyLine* table, uint64_t slots)
 }
 // the two-level sample of s's dictionary into hi/lo/node (dict_sample_entries(s.n_dict) entries)
 hipError_t run_dict_sample(const DevSnapshot& s, uint64_t* hi, uint64_t* lo, int32_t* node, hipStream_t st);
+hipError_t run_dict_buckets(const DevSnapshot& s, uint32_t* B, uint32_t lg, hipStream_t st);
 
 }  // namespace adx
