@@ -510,9 +510,14 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
         const bool tail = !has_cfk || hi == lo || kr.last_txn < S;
         const uint64_t wlo = kr.w_lo, whi = kr.w_hi;
         const bool wtail = !has_cfk || whi == wlo || kr.last_wexec < S;
+        // S above the key's last committed Write (M is the newest one) and above prunedBefore: the emissions are
+        // the newest probe's two precomputed lists (KeyEntry) less the entries at or above S -- insertPos(S) is the
+        // element filter rank < S, no search and no descent (as the lean passes' newest test; a late PreAccept or an
+        // Accept whose S sits below some newer txnIds lands here)
+        const bool listp = has_cfk && s.elide && wtail && (tail || kr.pruned == 0 || S > kr.pruned);
         // insertPos(S) in byId and the committed Writes' executeAt search, in lockstep
         uint64_t end, wsearch;
-        grp_lower_bound2(has_cfk && !tail, lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
+        grp_lower_bound2(has_cfk && !tail && !listp, lo, hi, [&](uint64_t i) { return s.ent[i].y & RANK_MASK; },
                          has_cfk && !wtail, wlo, whi, [&](uint64_t i) { return s.w[i].x; }, S, end, wsearch);
         const uint64_t end_g = tail ? hi : end;
         const uint64_t wpos = !has_cfk ? wlo : (whi == wlo ? wlo : (kr.last_wexec < S ? whi : wsearch));
@@ -596,10 +601,10 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
             stage8(n0, q, true);
         };
 
-        // Newest probe (S above every txnId and every committed Write's executeAt of the key, elision
-        // on): the emissions are exactly two precomputed contiguous lists (KeyEntry, common.hpp);
+        // Newest probe (S above every committed Write's executeAt of the key and above prunedBefore, elision on):
+        // the emissions are the two precomputed contiguous lists (KeyEntry, common.hpp) filtered by rank < S;
         // otherwise the class max tree prunes byId[lo, end) (output-sensitive descent).
-        const bool newest = has_cfk && s.elide && tail && wtail;
+        const bool newest = listp;
         if (ballot(newest))
         {
             const uint32_t n1 = newest ? cand_hi - cand_lo : 0u;
@@ -614,7 +619,7 @@ __global__ __launch_bounds__(64 * FWAVES) __attribute__((amdgpu_waves_per_eu(FUS
                     txw = i < n1 ? s.cand[cand_lo + i]
                                  : (cls == 0 ? (last_w_txn | (1u << RANK_BITS)) : s.cwr[cwr_tail + (i - n1)]);
                 const uint32_t r = txw & RANK_MASK, kd = txw >> RANK_BITS;
-                want = want && r != self;
+                want = want && r != self && r < S;
                 const bool is1 = ((KINDS_RS_OR_WS >> kd) & 1) == 0;   // !managesExecution -> directKeyDeps
                 const uint32_t w0 = (want && !is1) ? 1u : 0u, w1 = (want && is1) ? 1u : 0u;
                 const uint32_t i0 = grp_incl_scan(w0), i1 = grp_incl_scan(w1);
