@@ -52,7 +52,7 @@ def resolve_kernels(stats, split_ms, min_ms=0.02):
     rng = bool(fl & A.AD_LEAN_RANGES)
     names = []
     if split_ms[2] > min_ms:
-        names.append("k_prepare<true>" if rpw1 and not rng else "k_prepare<false>")
+        names.append("k_prepare<true>" if rpw1 else "k_prepare<false>")     # the lean passes read its probe KeyLines
     if rpw1:
         wide = bool(fl & A.AD_LEAN_WIDE1)
         names.append("k_resolve_lean<%du, %s, %s, 1>" % (rpw1, "true" if rng else "false", "true" if wide else "false"))

@@ -52,7 +52,7 @@ def test_resolve_kernels_follow_the_library_stats():
     kernels)."""
     split = [0.5, 0.0, 0.07, 0.1, 0.0, 0.03, 0.2]
     st = dict(lean_rpw1=4, lean_flags=A.AD_LEAN_RANGES | A.AD_LEAN_PASS2)
-    assert bench.resolve_kernels(st, split) == ["k_prepare<false>", "k_resolve_lean<4u, true, false, 1>",
+    assert bench.resolve_kernels(st, split) == ["k_prepare<true>", "k_resolve_lean<4u, true, false, 1>",
                                                 "k_resolve_lean<2u, true, false, 2>", "k_resolve"]
     st = dict(lean_rpw1=2, lean_flags=A.AD_LEAN_WIDE1)
     assert bench.resolve_kernels(st, split) == ["k_prepare<true>", "k_resolve_lean<2u, false, true, 1>", "k_resolve"]
