@@ -1299,63 +1299,6 @@ __global__ void __launch_bounds__(RC_PARTS) k_rmerge_copy(MergeArgs a, const uin
     }
 }
 
-// Pass 2 by part groups (the default): G lanes per received part, lane-strided over its key words,
-// ids and keysToTxnIds (contiguous at both ends), no block scans or owner searches -- as the export.
-template <uint32_t G>
-__global__ void __launch_bounds__(256) k_rmerge_copy_groups(MergeArgs a, const uint64_t* bases)
-{
-    const uint64_t p = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
-    const uint32_t sl = threadIdx.x % G;
-    if (p >= a.n_parts || (*a.error & 3u)) return;
-    const uint64_t n1 = a.n_owned + 1;
-    const uint4* pi = reinterpret_cast<const uint4*>(a.pinfo);
-    const uint4 A = pi[2 * p], B = pi[2 * p + 1];
-    const uint4 pp = reinterpret_cast<const uint4*>(a.ppre)[p];
-    const uint32_t m = B.w & 3, r = B.w >> 2;
-    const uint32_t w = m == AD_MAP_RANGE ? 2u : 1u;
-    const uint64_t K = a.goff[(uint64_t)(0 * 3 + m) * n1 + r], I = a.goff[(uint64_t)(1 * 3 + m) * n1 + r];
-    const uint64_t O = a.goff[(uint64_t)(2 * 3 + m) * n1 + r];
-    const uint64_t kdst = bases[3 * m + 0] + w * (K + pp.x), idst = bases[3 * m + 1] + I;
-    const uint64_t hdst = bases[3 * m + 2] + O + pp.x, pdst = bases[3 * m + 2] + O + pp.z + pp.y;
-    const int32_t add = (int32_t)(pp.z + pp.y) - (int32_t)A.w;
-    const bool single = pp.w == 1;
-    const uint32_t nk = A.w, ni = B.y;
-    for (uint32_t i = sl; i < B.x; i += G) a.o_keys[kdst + i] = a.keys[A.x + i];
-    const uint32_t* ids = reinterpret_cast<const uint32_t*>(a.ids);
-    uint32_t* o_ids = reinterpret_cast<uint32_t*>(a.o_ids);
-    for (uint32_t i = sl; i < ni; i += G)
-    {
-        const uint32_t at = A.y + i, x = ids[at];
-        if (single)
-        {
-            if (i > 0 && ids[at - 1] >= x) atomicOr(a.error, 8u);      // part not sorted / unique
-            if (x >= a.n_global) atomicOr(a.error, 16u);
-            o_ids[idst + i] = x;
-        }
-        else
-        {
-            const uint32_t uu = a.u[at];
-            if (!(uu & DUP_BIT)) o_ids[idst + uu] = x;
-        }
-    }
-    for (uint32_t i = sl; i < B.z; i += G)
-    {
-        const int32_t v = a.k2t[A.z + i];
-        if (i < nk)
-        {
-            a.o_k2t[hdst + i] = v + add;
-            continue;
-        }
-        const uint32_t idx = (uint32_t)v;
-        if (idx >= ni)
-        {
-            atomicOr(a.error, 8u);
-            continue;
-        }
-        a.o_k2t[pdst + (i - nk)] = single ? (int32_t)idx : (int32_t)(a.u[A.y + idx] & ~DUP_BIT);
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // ad_parts_union: Deps.merge of replies whose key sets overlap (Deps.java:281-286 via
 // PartialDeps.with / RelationMultiMap.linearUnion, RelationMultiMap.java:561-816). Every part
@@ -1862,21 +1805,9 @@ hipError_t run_rmerge_copy(const MergeArgs& a, const uint64_t* bases, hipStream_
 {
     k_rmerge_bases<<<1, 64, 0, st>>>(a, const_cast<uint64_t*>(bases));
     if (!a.n_parts) return hipGetLastError();
-    const bool tiles = getenv("AD_RMERGE_G") == nullptr;           // groups: opt-in until measured
-    if (tiles)
-    {
-        k_rmerge_copy<<<(unsigned)((a.n_parts + RC_PARTS - 1) / RC_PARTS), RC_PARTS, 0, st>>>(a, bases);
-        return hipGetLastError();
-    }
-    // lanes per part by the received elements per part (opt-in: the block tiles measured faster, 0.123 vs
-    // 0.155 ms per owner at W = 8 and 0.206 vs 0.23 ms at N = 1)
-    const int gsel = getenv("AD_RMERGE_G") ? atoi(getenv("AD_RMERGE_G")) : 0;
-    const uint64_t per = a.n_elems / a.n_parts;
-    const uint32_t G = (gsel == 4 || gsel == 8 || gsel == 16) ? (uint32_t)gsel : per <= 16 ? 4u : per <= 48 ? 8u : 16u;
-    const unsigned blocks = (unsigned)((a.n_parts * G + 255) / 256);
-    if (G == 4) k_rmerge_copy_groups<4><<<blocks, 256, 0, st>>>(a, bases);
-    else if (G == 8) k_rmerge_copy_groups<8><<<blocks, 256, 0, st>>>(a, bases);
-    else k_rmerge_copy_groups<16><<<blocks, 256, 0, st>>>(a, bases);
+    // load-balanced over blocks of 256 parts (G lanes per part instead -- a copy like the export's -- measured
+    // slower: 0.155 against 0.123 ms per owner at W = 8, 0.23 against 0.206 ms at N = 1; deleted in round 6)
+    k_rmerge_copy<<<(unsigned)((a.n_parts + RC_PARTS - 1) / RC_PARTS), RC_PARTS, 0, st>>>(a, bases);
     return hipGetLastError();
 }
 

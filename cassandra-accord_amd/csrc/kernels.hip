@@ -595,13 +595,10 @@ hipError_t run_scan(const DevSnapshot& s, const BatchBufs& b, hipStream_t st)
 {
     if (!b.n_probes) return hipSuccess;
     const uint64_t blocks_needed = (b.n_probes + K1_WAVES - 1) / K1_WAVES;
-    // (AD_K1_CAP: 1024 (default), 2048 or 4096 staged ids per wave -- a bigger stage saves hot keys' replayed
-    // descents at fewer waves per CU)
-    static const int cap = getenv("AD_K1_CAP") ? atoi(getenv("AD_K1_CAP")) : 1024;
+    // 1024 staged ids per wave (2048 / 4096 -- fewer replayed descents for hot keys at fewer waves per CU --
+    // measured slower on the steady state: resolve 3.76 -> 3.93 / 4.06 ms; the selection was deleted in round 6)
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, (uint64_t)device_cu_count() * 8);
-    if (cap >= 4096) k_scan<4096><<<grid, 256, 0, st>>>(s, b);
-    else if (cap >= 2048) k_scan<2048><<<grid, 256, 0, st>>>(s, b);
-    else k_scan<1024><<<grid, 256, 0, st>>>(s, b);
+    k_scan<K1_CAP><<<grid, 256, 0, st>>>(s, b);
     return hipGetLastError();
 }
 

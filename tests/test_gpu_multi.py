@@ -130,10 +130,9 @@ def test_config2_scaled_sharded(rank_ids):
 
 @pytest.mark.parametrize("width", ["2", "4", "8", "16", "32"])
 def test_export_and_copy_lane_widths(width, monkeypatch):
-    # the export and the K3 copy at every lane width per request / part, whatever the batch's average part
-    # size would pick; big groups included
+    # the export at every lane width per request, whatever the batch's average ids per request would pick; big
+    # groups included
     monkeypatch.setenv("AD_EXPORT_G", width)
-    monkeypatch.setenv("AD_RMERGE_G", width)
     w = synth.config3(n_txns=20000, n_keys=3000, seed=43)
     _check(w, synth.shard_bounds(4), 3, rank_ids=True)
     _check(w, synth.shard_bounds(3), 2, rank_ids=False)
