@@ -292,3 +292,30 @@ def test_ephemeral_reads_at_timestamp_max(oracle, seed):
 def test_ephemeral_reads_config2_scaled(oracle):
     w = synth.with_ephemeral_reads(synth.config2(n_txns=20000, n_keys=20000, n_hist_entries=200000), frac=0.3)
     _compare(w, oracle, paths=(0,))
+
+
+@pytest.mark.parametrize("gap_bits", [40, 62])
+def test_dictionary_bucket_index_clusters(oracle, gap_bits):
+    # the rank searches' bucket index (common.hpp dict_bucket_of) spreads the dictionary's 128-bit span over
+    # its buckets: ids in two clusters 2^gap_bits epochs apart leave nearly every bucket empty and each
+    # cluster in one or two buckets, so the searches run over wide bucket ranges -- still exact. The ids of
+    # the request mix (Accepts' executeAt and txnId, late PreAccepts) all need the search; the shift is
+    # monotone, so the reference's answers keep their meaning
+    import dataclasses
+    from accord_deps.model import Tids
+    w = synth.config2(n_txns=4000, n_keys=2000, n_hist_entries=200000)
+    w = synth.with_request_mix(w, accept_frac=0.3, unordered_frac=0.3, unordered_window=3000)
+    c, q = w.cfk, w.queries
+    hlc_all = np.concatenate([(t.lsb >> np.uint64(16)) for t in (c.txn, c.exec, q.txn, q.exec)])
+    pivot = np.uint64(np.median(hlc_all.astype(np.float64)))
+    gap = np.uint64(1) << np.uint64(gap_bits)
+
+    def shift(t):
+        up = (t.lsb >> np.uint64(16)) >= pivot          # one epoch throughout: (msb, hlc) order is hlc order
+        return Tids(np.where(up, t.msb + gap, t.msb).astype(np.uint64), t.lsb.copy(), t.node.copy())
+
+    assert len(np.unique(c.txn.msb)) == 1 and len(np.unique(q.exec.msb)) == 1
+    w = dataclasses.replace(w, cfk=dataclasses.replace(c, txn=shift(c.txn), exec=shift(c.exec)),
+                            queries=dataclasses.replace(q, txn=shift(q.txn), exec=shift(q.exec)))
+    got, exp = _compare(w, oracle, paths=(0,))
+    assert got.stats["n_deferred_lean"] > 0
